@@ -1,0 +1,1071 @@
+// hsc_host.cpp -- host side of the MI355X serializable conflict validator.
+//
+// Implements include/hip_serial.h:
+//   * the write window: decoded from the log stream the way
+//     osql_serial_check / serial_check_this_txn walk it
+//     (bdb/serializable.c:390-539 and 60-332), kept resident on the GPU;
+//   * the marshaller: CurRangeArr (db/comdb2.h:1105-1124) or flat read sets
+//     -> device probe struct-of-arrays, applying the span and lock rules of
+//     currangearr_build_hash + serial_check_callback (db/sqlglue.c:312-351,
+//     db/glue.c:2926-2963) and the min-length memcmp padding lemma;
+//   * the drop-in entry points bdb_osql_serial_check / check_batch.
+// There is no CPU verdict path: every range verdict comes from the GPU join.
+#include "../../include/hip_serial.h"
+#include "hsc_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+using namespace hsc;
+
+namespace {
+
+struct DBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t want)
+    {
+        if (want <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t b = want + want / 8 + 256;
+        hipError_t e = hipMalloc(&p, b);
+        if (e == hipSuccess) bytes = b;
+        return e;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T *as() const { return (T *)p; }
+};
+
+struct GroupInfo {
+    int tid, ix, klen;
+};
+
+inline uint64_t load_be64(const uint8_t *b)
+{
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v = (v << 8) | b[i];
+    return v;
+}
+
+inline uint64_t ixkey(int tid, int ix) { return ((uint64_t)(uint32_t)tid << 32) | (uint32_t)ix; }
+
+}  // namespace
+
+struct hsc_ctx {
+    int device = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::mutex mu;  // one check at a time per context (re-entrant callers queue)
+
+    // dictionaries
+    std::unordered_map<std::string, int> table_ids;
+    std::vector<std::string> table_names;
+    std::unordered_map<uint64_t, int> group_ids;                    // (tid,ix,klen)
+    std::vector<GroupInfo> groups;
+    std::unordered_map<uint64_t, std::vector<int>> ix_groups;       // (tid,ix) -> gids
+
+    // host staging of the window (host ingest paths)
+    std::vector<uint32_t> h_gid;
+    std::vector<uint64_t> h_keyoff;
+    std::vector<uint8_t> h_keys;
+    std::vector<uint64_t> h_lsn;
+    std::vector<uint64_t> h_table_max;
+    bool host_staged = true;
+    bool dirty = true;
+    uint64_t end_lsn = 0, max_commit = 0;
+    uint64_t poison_regop = 0;  // max regop LSN whose prev record cannot be read
+    uint64_t poison_chain = 0;  // max commit LSN whose logical chain is broken
+    std::vector<uint64_t> record_lsns;  // all record LSNs when ingested from a log
+    uint64_t last_append_lsn = 0;
+
+    // device window
+    int W = 1;
+    size_t n = 0, cap = 0;
+    uint32_t ntiles = 0;
+    int log2T = 11, levels = 0;
+    DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
+    DBuf d_gstart, d_gend, d_tmax, d_table_max, d_group_table, d_count;
+
+    // probe workspace
+    DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;
+    DBuf p_verdict, p_bitmap;
+    DBuf w_code, w_counts, w_bucket, w_cursor, w_items, w_recs;
+
+    // marshal output
+    hsc_marshalled m{};
+    std::vector<uint64_t> m_lo, m_hi, m_snap, m_lock_snap;
+    std::vector<uint32_t> m_gid, m_txn, m_lock_table, m_lock_txn;
+    std::vector<uint8_t> m_forced;
+
+    // timing
+    bool timing = false;
+    hipEvent_t ev[8] = {};
+    hsc_timing last{};
+};
+
+static int fail(hsc_ctx *c, int code, const char *what, hipError_t e = hipSuccess)
+{
+    char buf[256];
+    if (e != hipSuccess)
+        snprintf(buf, sizeof buf, "%s: %s", what, hipGetErrorString(e));
+    else
+        snprintf(buf, sizeof buf, "%s", what);
+    c->err = buf;
+    return code;
+}
+
+#define HIPCHK(c, call)                                          \
+    do {                                                         \
+        hipError_t e_ = (call);                                  \
+        if (e_ != hipSuccess) return fail((c), HSC_EDEVICE, #call, e_); \
+    } while (0)
+
+static int table_id_or_add(hsc_ctx *c, const char *name)
+{
+    auto it = c->table_ids.find(name);
+    if (it != c->table_ids.end()) return it->second;
+    int tid = (int)c->table_names.size();
+    c->table_ids.emplace(name, tid);
+    c->table_names.emplace_back(name);
+    c->h_table_max.push_back(0);
+    return tid;
+}
+
+static int group_id_or_add(hsc_ctx *c, int tid, int ix, int klen)
+{
+    uint64_t k = ((uint64_t)(uint32_t)tid << 40) ^ ((uint64_t)(uint16_t)ix << 24) ^ (uint32_t)klen;
+    // disambiguate collisions by scanning (keys are tiny; collisions impossible
+    // for tid < 2^24, |ix| < 2^15, klen < 2^24)
+    auto it = c->group_ids.find(k);
+    if (it != c->group_ids.end()) return it->second;
+    int g = (int)c->groups.size();
+    c->groups.push_back({tid, ix, klen});
+    c->group_ids.emplace(k, g);
+    c->ix_groups[ixkey(tid, ix)].push_back(g);
+    return g;
+}
+
+static void clear_window(hsc_ctx *c)
+{
+    c->h_gid.clear();
+    c->h_keyoff.clear();
+    c->h_keys.clear();
+    c->h_lsn.clear();
+    std::fill(c->h_table_max.begin(), c->h_table_max.end(), 0);
+    c->max_commit = 0;
+    c->poison_regop = c->poison_chain = 0;
+    c->record_lsns.clear();
+    c->last_append_lsn = 0;
+    c->host_staged = true;
+    c->dirty = true;
+    c->n = 0;
+}
+
+static void add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keylen, bool has_key,
+                      uint64_t lsn)
+{
+    if (lsn > c->h_table_max[tid]) c->h_table_max[tid] = lsn;
+    if (lsn > c->max_commit) c->max_commit = lsn;
+    if (!has_key) return;
+    if (keylen < 0) keylen = 0;
+    int g = group_id_or_add(c, tid, ix, keylen);
+    c->h_gid.push_back((uint32_t)g);
+    c->h_keyoff.push_back(c->h_keys.size());
+    c->h_keys.insert(c->h_keys.end(), key, key + keylen);
+    c->h_lsn.push_back(lsn);
+}
+
+// ---------------------------------------------------------------------------
+// device window build
+// ---------------------------------------------------------------------------
+static int window_words(hsc_ctx *c)
+{
+    int W = 1;
+    for (auto &g : c->groups) W = std::max(W, (g.klen + 7) / 8);
+    return W;
+}
+
+// Sort + dedupe rows staged in d_gid/d_words/d_lsn (n_in rows, stride cap),
+// then build group spans, tile maxima and table maxima.
+static int device_build(hsc_ctx *c, size_t n_in)
+{
+    hipStream_t s = c->stream;
+    const int W = c->W;
+    const size_t cap = c->cap;
+    HIPCHK(c, c->d_gid2.ensure(cap * 4));
+    HIPCHK(c, c->d_words2.ensure(cap * 8 * W));
+    HIPCHK(c, c->d_lsn2.ensure(cap * 8));
+    HIPCHK(c, c->d_flags.ensure(cap * 4 + 64));
+    size_t scratch = std::max(radix_scratch_bytes(n_in, W), scan_scratch_bytes(n_in) + 64);
+    HIPCHK(c, c->d_scratch.ensure(scratch));
+    HIPCHK(c, c->d_count.ensure(64));
+
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPCHK(c, hipEventCreate(&e0));
+    HIPCHK(c, hipEventCreate(&e1));
+    HIPCHK(c, hipEventRecord(e0, s));
+    bool in_alt = false;
+    HIPCHK(c, radix_sort_rows(W, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
+                              c->d_lsn.as<uint64_t>(), cap, c->d_gid2.as<uint32_t>(),
+                              c->d_words2.as<uint64_t>(), c->d_lsn2.as<uint64_t>(),
+                              c->d_scratch.p, c->d_scratch.bytes, &in_alt, s));
+    // dedupe from wherever the sort left the rows into the other buffer set
+    DBuf *sg = in_alt ? &c->d_gid2 : &c->d_gid, *sw = in_alt ? &c->d_words2 : &c->d_words,
+         *sl = in_alt ? &c->d_lsn2 : &c->d_lsn;
+    DBuf *dg = in_alt ? &c->d_gid : &c->d_gid2, *dw = in_alt ? &c->d_words : &c->d_words2,
+         *dl = in_alt ? &c->d_lsn : &c->d_lsn2;
+    HIPCHK(c, dedupe_rows(W, n_in, sg->as<uint32_t>(), sw->as<uint64_t>(), sl->as<uint64_t>(), cap,
+                          dg->as<uint32_t>(), dw->as<uint64_t>(), dl->as<uint64_t>(), cap,
+                          c->d_flags.as<uint32_t>(), c->d_scratch.p, c->d_scratch.bytes,
+                          c->d_count.as<uint32_t>(), s));
+    if (!in_alt) {  // final rows must live in d_gid/d_words/d_lsn
+        std::swap(c->d_gid, c->d_gid2);
+        std::swap(c->d_words, c->d_words2);
+        std::swap(c->d_lsn, c->d_lsn2);
+    }
+    uint32_t nu = 0;
+    HIPCHK(c, hipMemcpyAsync(&nu, c->d_count.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->n = n_in ? nu : 0;
+    c->log2T = tile_log2(W);
+    c->ntiles = (uint32_t)((c->n + ((size_t)1 << c->log2T) - 1) >> c->log2T);
+    c->levels = 0;
+    while (((size_t)1 << c->levels) <= c->ntiles) c->levels++;
+    const int ng = (int)c->groups.size();
+    const int nt = (int)c->table_names.size();
+    HIPCHK(c, c->d_gstart.ensure(4 * (size_t)std::max(ng, 1)));
+    HIPCHK(c, c->d_gend.ensure(4 * (size_t)std::max(ng, 1)));
+    HIPCHK(c, c->d_tmax.ensure(8 * (size_t)std::max(1, c->levels) * std::max<uint32_t>(1, c->ntiles)));
+    HIPCHK(c, c->d_table_max.ensure(8 * (size_t)std::max(nt, 1)));
+    HIPCHK(c, c->d_group_table.ensure(4 * (size_t)std::max(ng, 1)));
+    std::vector<uint32_t> gt(std::max(ng, 1), 0);
+    for (int g = 0; g < ng; ++g) gt[g] = (uint32_t)c->groups[g].tid;
+    HIPCHK(c, hipMemcpyAsync(c->d_group_table.p, gt.data(), 4 * gt.size(), hipMemcpyHostToDevice, s));
+    std::vector<uint64_t> tm(std::max(nt, 1), 0);
+    for (int t = 0; t < nt; ++t) tm[t] = c->h_table_max[t];
+    HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, tm.data(), 8 * tm.size(), hipMemcpyHostToDevice, s));
+    WinView w{};
+    w.words = c->d_words.as<uint64_t>();
+    w.stride = cap;
+    w.lsn = c->d_lsn.as<uint64_t>();
+    w.gid = c->d_gid.as<uint32_t>();
+    w.tmax = c->d_tmax.as<uint64_t>();
+    w.n = (uint32_t)c->n;
+    w.ntiles = c->ntiles;
+    w.W = W;
+    w.log2T = c->log2T;
+    w.levels = c->levels;
+    HIPCHK(c, build_summaries(w, c->d_gstart.as<uint32_t>(), c->d_gend.as<uint32_t>(), ng,
+                              c->d_tmax.as<uint64_t>(), c->d_group_table.as<uint32_t>(),
+                              c->d_table_max.as<uint64_t>(), s));
+    HIPCHK(c, hipEventRecord(e1, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    c->last.ingest_ms = ms;
+    c->last.tiles = c->ntiles;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    // table maxima back to the host (device ingest computes them on the GPU)
+    if (nt > 0) {
+        HIPCHK(c, hipMemcpy(tm.data(), c->d_table_max.p, 8 * (size_t)nt, hipMemcpyDeviceToHost));
+        for (int t = 0; t < nt; ++t) c->h_table_max[t] = std::max(c->h_table_max[t], tm[t]);
+    }
+    c->dirty = false;
+    return HSC_OK;
+}
+
+static int build_from_host(hsc_ctx *c)
+{
+    const size_t n_in = c->h_gid.size();
+    c->W = window_words(c);
+    const int W = c->W;
+    c->cap = std::max<size_t>(64, (n_in + 63) & ~(size_t)63);
+    const size_t cap = c->cap;
+    std::vector<uint64_t> words((size_t)W * cap, 0);
+    std::vector<uint8_t> buf((size_t)W * 8);
+    for (size_t i = 0; i < n_in; ++i) {
+        const int klen = c->groups[c->h_gid[i]].klen;
+        std::fill(buf.begin(), buf.end(), 0);
+        if (klen) memcpy(buf.data(), c->h_keys.data() + c->h_keyoff[i], (size_t)klen);
+        for (int j = 0; j < W; ++j) words[(size_t)j * cap + i] = load_be64(buf.data() + 8 * j);
+    }
+    HIPCHK(c, c->d_gid.ensure(cap * 4));
+    HIPCHK(c, c->d_words.ensure(cap * 8 * W));
+    HIPCHK(c, c->d_lsn.ensure(cap * 8));
+    hipStream_t s = c->stream;
+    if (n_in) {
+        HIPCHK(c, hipMemcpyAsync(c->d_gid.p, c->h_gid.data(), 4 * n_in, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->d_words.p, words.data(), 8 * (size_t)W * cap, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->d_lsn.p, c->h_lsn.data(), 8 * n_in, hipMemcpyHostToDevice, s));
+    }
+    return device_build(c, n_in);
+}
+
+static int ensure_built(hsc_ctx *c)
+{
+    if (!c->dirty) return HSC_OK;
+    if (!c->host_staged) return fail(c, HSC_ESTATE, "device window must be re-ingested");
+    return build_from_host(c);
+}
+
+// ---------------------------------------------------------------------------
+// log decode (what osql_serial_check + serial_check_this_txn visit)
+// ---------------------------------------------------------------------------
+static long find_lsn(const hsc_llog *log, uint64_t lsn)
+{
+    const uint64_t *b = log->lsn, *e = log->lsn + log->nrec;
+    const uint64_t *p = std::lower_bound(b, e, lsn);
+    return (p != e && *p == lsn) ? (long)(p - b) : -1;
+}
+
+static bool is_regop(uint32_t t)
+{
+    return t == HSC_REC_TXN_REGOP || t == HSC_REC_TXN_REGOP_GEN || t == HSC_REC_TXN_REGOP_ROWLOCKS;
+}
+
+static int ingest_log(hsc_ctx *c, const hsc_llog *log)
+{
+    clear_window(c);
+    c->end_lsn = log->end_lsn;
+    c->record_lsns.assign(log->lsn, log->lsn + log->nrec);
+    for (size_t i = 1; i < log->nrec; ++i)
+        if (log->lsn[i] <= log->lsn[i - 1]) return fail(c, HSC_EINVAL, "log LSNs not increasing");
+    std::vector<int> tmap(log->ntbnames, -1);
+    auto tid_of = [&](int32_t t) -> int {
+        if (t < 0 || t >= log->ntbnames) return -1;
+        if (tmap[t] < 0) tmap[t] = table_id_or_add(c, log->tbnames[t]);
+        return tmap[t];
+    };
+    for (size_t i = 0; i < log->nrec; ++i) {
+        if (!is_regop(log->rectype[i])) continue;
+        const uint64_t c_lsn = log->lsn[i];
+        long p = find_lsn(log, log->prev[i]);
+        if (p < 0) {  // prevcur->get fails -> the scan errors out (nonzero)
+            c->poison_regop = std::max(c->poison_regop, c_lsn);
+            continue;
+        }
+        if (log->rectype[p] != HSC_REC_LTRAN_COMMIT) continue;
+        if ((uint32_t)(log->prev[p] >> 32) == 0) continue;  // not a write txn
+        if (log->isabort[p]) continue;
+        // committed write txn: walk prevllsn back to ltran_start
+        if (c_lsn > c->max_commit) c->max_commit = c_lsn;
+        uint64_t lsn = log->prev[p];
+        long r = find_lsn(log, lsn);
+        if (r < 0) {
+            c->poison_chain = std::max(c->poison_chain, c_lsn);
+            continue;
+        }
+        for (;;) {
+            const uint32_t t = log->rectype[r];
+            if (t == HSC_REC_LTRAN_START) break;
+            switch (t) {
+            case HSC_REC_UNDO_ADD_DTA:
+            case HSC_REC_UNDO_DEL_DTA:
+            case HSC_REC_UNDO_UPD_DTA:
+            case HSC_REC_UNDO_ADD_DTA_LK:
+            case HSC_REC_UNDO_DEL_DTA_LK:
+            case HSC_REC_UNDO_UPD_DTA_LK: {
+                int tid = tid_of(log->table[r]);
+                if (tid < 0) return fail(c, HSC_ELOG, "bad table index in log");
+                add_write(c, tid, -2, nullptr, 0, false, c_lsn);
+                break;
+            }
+            case HSC_REC_UNDO_ADD_IX:
+            case HSC_REC_UNDO_DEL_IX:
+            case HSC_REC_UNDO_DEL_IX_LK:
+            case HSC_REC_UNDO_UPD_IX:
+            case HSC_REC_UNDO_ADD_IX_LK:
+            case HSC_REC_UNDO_UPD_IX_LK: {
+                int tid = tid_of(log->table[r]);
+                if (tid < 0) return fail(c, HSC_ELOG, "bad table index in log");
+                add_write(c, tid, (int)log->ix[r], log->keys + log->key_off[r], log->keylen[r],
+                          true, c_lsn);
+                break;
+            }
+            case HSC_REC_LTRAN_COMMIT:
+            case HSC_REC_LTRAN_COMPREC:
+                break;
+            default:  // the reference abort()s (bdb/serializable.c:283-286)
+                return fail(c, HSC_ELOG, "unknown record type in logical chain");
+            }
+            lsn = log->prev[r];
+            if ((uint32_t)(lsn >> 32) == 0) break;
+            r = find_lsn(log, lsn);
+            if (r < 0) {
+                c->poison_chain = std::max(c->poison_chain, c_lsn);
+                break;
+            }
+        }
+    }
+    c->dirty = true;
+    return HSC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// marshalling
+// ---------------------------------------------------------------------------
+struct RangeRef {
+    int tid;  // window table id or -1
+    int idxnum;
+    const uint8_t *lkey, *rkey;
+    int lkeylen, rkeylen, lflag, rflag, islocked;
+};
+
+// Bound normalised to the group's key length klen (padding lemma, SURVEY
+// §8(a) A0): lower = lkey[0..min) ++ 0x00.., upper = rkey[0..min) ++ 0xFF..;
+// open bounds become 0x00^klen / 0xFF^klen.  Then zero padded to W words.
+static void norm_bound(const uint8_t *key, int keylen, int flag, int klen, bool upper, int W,
+                       uint64_t *out)
+{
+    uint8_t buf[kMaxWords * 8];
+    memset(buf, 0, (size_t)W * 8);
+    if (flag) {
+        if (upper) memset(buf, 0xFF, (size_t)klen);
+    } else {
+        int m = (key && keylen > 0) ? std::min(keylen, klen) : 0;
+        if (m) memcpy(buf, key, (size_t)m);
+        if (upper && klen > m) memset(buf + m, 0xFF, (size_t)(klen - m));
+    }
+    for (int j = 0; j < W; ++j) out[j] = load_be64(buf + 8 * j);
+}
+
+struct TxnTable {
+    int tid, islocked;
+    std::vector<int> idx, b, e;  // per idxnum span
+};
+
+static void marshal_begin(hsc_ctx *c, size_t n_txn)
+{
+    c->m_lo.clear();
+    c->m_hi.clear();
+    c->m_snap.clear();
+    c->m_gid.clear();
+    c->m_txn.clear();
+    c->m_lock_table.clear();
+    c->m_lock_snap.clear();
+    c->m_lock_txn.clear();
+    c->m_forced.assign(n_txn, 0);
+}
+
+// Forced verdicts of a full check that do not depend on the ranges.
+// Returns -1 if the device decides, else the rc.
+static int full_forced(hsc_ctx *c, uint64_t S)
+{
+    if (S >= c->end_lsn) return 0;  // DB_SET at/after the end -> DB_NOTFOUND -> 0
+    if (!c->record_lsns.empty() &&
+        !std::binary_search(c->record_lsns.begin(), c->record_lsns.end(), S))
+        return 1;                    // DB_SET inside the log on a non-record -> error
+    if (c->poison_regop > S || c->poison_chain > S) return 1;
+    return -1;
+}
+
+static int regop_rc(hsc_ctx *c, uint64_t S)
+{
+    if (S >= c->end_lsn) return 0;
+    if (!c->record_lsns.empty() &&
+        !std::binary_search(c->record_lsns.begin(), c->record_lsns.end(), S))
+        return 1;
+    return (c->max_commit > S || c->poison_regop > S) ? 1 : 0;
+}
+
+template <class Get>
+static void marshal_txn(hsc_ctx *c, uint32_t txn, uint64_t S, int nr, Get get,
+                        std::vector<TxnTable> &tabs)
+{
+    const int W = c->W;
+    tabs.clear();
+    for (int k = 0; k < nr; ++k) {
+        RangeRef r = get(k);
+        if (r.tid < 0) continue;  // table never written: nothing can conflict
+        TxnTable *tt = nullptr;
+        for (auto &t : tabs)
+            if (t.tid == r.tid) {
+                tt = &t;
+                break;
+            }
+        if (!tt) {  // first range of the table fixes islocked
+            tabs.push_back(TxnTable{r.tid, r.islocked, {}, {}, {}});
+            tt = &tabs.back();
+        }
+        size_t j = 0;
+        for (; j < tt->idx.size(); ++j)
+            if (tt->idx[j] == r.idxnum) break;
+        if (j == tt->idx.size()) {
+            tt->idx.push_back(r.idxnum);
+            tt->b.push_back(k);
+            tt->e.push_back(k);
+        } else {
+            tt->e[j] = k;
+        }
+    }
+    uint64_t wl[kMaxWords], wh[kMaxWords];
+    for (auto &t : tabs) {
+        if (t.islocked) {
+            c->m_lock_table.push_back((uint32_t)t.tid);
+            c->m_lock_snap.push_back(S);
+            c->m_lock_txn.push_back(txn);
+            continue;
+        }
+        for (size_t j = 0; j < t.idx.size(); ++j) {
+            auto it = c->ix_groups.find(ixkey(t.tid, t.idx[j]));
+            if (it == c->ix_groups.end()) continue;
+            for (int g : it->second) {
+                const int klen = c->groups[g].klen;
+                for (int k = t.b[j]; k <= t.e[j]; ++k) {  // span quirk: every array slot
+                    RangeRef r = get(k);
+                    norm_bound(r.lkey, r.lkeylen, r.lflag, klen, false, W, wl);
+                    norm_bound(r.rkey, r.rkeylen, r.rflag, klen, true, W, wh);
+                    int cmp = 0;
+                    for (int q = 0; q < W && !cmp; ++q)
+                        if (wl[q] != wh[q]) cmp = wl[q] < wh[q] ? -1 : 1;
+                    if (cmp > 0) continue;  // empty range never matches
+                    c->m_lo.insert(c->m_lo.end(), wl, wl + W);
+                    c->m_hi.insert(c->m_hi.end(), wh, wh + W);
+                    c->m_gid.push_back((uint32_t)g);
+                    c->m_snap.push_back(S);
+                    c->m_txn.push_back(txn);
+                }
+            }
+        }
+    }
+}
+
+// AoS lo/hi rows -> [W][n] words.
+static void marshal_finish(hsc_ctx *c, size_t n_txn)
+{
+    const int W = c->W;
+    const size_t n = c->m_gid.size();
+    std::vector<uint64_t> lo((size_t)W * n), hi((size_t)W * n);
+    for (size_t i = 0; i < n; ++i)
+        for (int j = 0; j < W; ++j) {
+            lo[(size_t)j * n + i] = c->m_lo[i * W + j];
+            hi[(size_t)j * n + i] = c->m_hi[i * W + j];
+        }
+    c->m_lo.swap(lo);
+    c->m_hi.swap(hi);
+    c->m.n = n;
+    c->m.n_lock = c->m_lock_table.size();
+    c->m.n_txn = n_txn;
+    c->m.words = W;
+    c->m.lo = c->m_lo.data();
+    c->m.hi = c->m_hi.data();
+    c->m.gid = c->m_gid.data();
+    c->m.snap = c->m_snap.data();
+    c->m.txn = c->m_txn.data();
+    c->m.lock_table = c->m_lock_table.data();
+    c->m.lock_snap = c->m_lock_snap.data();
+    c->m.lock_txn = c->m_lock_txn.data();
+    c->m.forced = c->m_forced.data();
+}
+
+static int marshal_readsets(hsc_ctx *c, const hsc_readsets *rs)
+{
+    marshal_begin(c, (size_t)rs->ntxn);
+    std::vector<int> tmap(rs->ntbnames, -1);
+    for (int t = 0; t < rs->ntbnames; ++t) {
+        auto it = c->table_ids.find(rs->tbnames[t]);
+        if (it != c->table_ids.end()) tmap[t] = it->second;
+    }
+    std::vector<TxnTable> tabs;
+    for (int t = 0; t < rs->ntxn; ++t) {
+        const uint64_t S = rs->snap[t];
+        int f = full_forced(c, S);
+        if (f >= 0) {
+            c->m_forced[t] = (uint8_t)f;
+            continue;
+        }
+        const int64_t r0 = rs->txn_off[t];
+        const int nr = (int)(rs->txn_off[t + 1] - r0);
+        auto get = [&](int k) {
+            const int64_t r = r0 + k;
+            RangeRef x;
+            const int32_t tb = rs->table[r];
+            x.tid = (tb >= 0 && tb < rs->ntbnames) ? tmap[tb] : -1;
+            x.idxnum = rs->idxnum[r];
+            x.lkey = rs->keys + rs->lkey_off[r];
+            x.rkey = rs->keys + rs->rkey_off[r];
+            x.lkeylen = rs->lkeylen[r];
+            x.rkeylen = rs->rkeylen[r];
+            x.lflag = rs->lflag[r];
+            x.rflag = rs->rflag[r];
+            x.islocked = rs->islocked[r];
+            return x;
+        };
+        marshal_txn(c, (uint32_t)t, S, nr, get, tabs);
+    }
+    marshal_finish(c, (size_t)rs->ntxn);
+    return HSC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// device probe
+// ---------------------------------------------------------------------------
+static WinView win_view(hsc_ctx *c)
+{
+    WinView w{};
+    w.words = c->d_words.as<uint64_t>();
+    w.stride = c->cap;
+    w.lsn = c->d_lsn.as<uint64_t>();
+    w.gid = c->d_gid.as<uint32_t>();
+    w.gstart = c->d_gstart.as<uint32_t>();
+    w.gend = c->d_gend.as<uint32_t>();
+    w.tmax = c->d_tmax.as<uint64_t>();
+    w.table_max = c->d_table_max.as<uint64_t>();
+    w.n = (uint32_t)c->n;
+    w.ntiles = c->ntiles;
+    w.ntables = (uint32_t)c->table_names.size();
+    w.W = c->W;
+    w.log2T = c->log2T;
+    w.levels = c->levels;
+    return w;
+}
+
+static int probe(hsc_ctx *c, const hsc_probe_batch *b)
+{
+    hipStream_t s = c->stream;
+    const WinView w = win_view(c);
+    if (b->n > 0xFFFFFFFFull / 2 || b->n_lock > 0xFFFFFFFFull || b->n_txn > 0xFFFFFFFFull)
+        return fail(c, HSC_EINVAL, "batch too large");
+    ProbeView p{};
+    p.lo = b->lo;
+    p.hi = b->hi;
+    p.gid = b->gid;
+    p.snap = b->snap;
+    p.txn = b->txn;
+    p.lock_table = b->lock_table;
+    p.lock_snap = b->lock_snap;
+    p.lock_txn = b->lock_txn;
+    p.n = w.n ? (uint32_t)b->n : 0;  // empty key window: no range can match
+    p.n_lock = (uint32_t)b->n_lock;
+    const uint32_t nt = std::max<uint32_t>(w.ntiles, 1);
+    HIPCHK(c, c->w_code.ensure(8 * (size_t)std::max<uint32_t>(p.n, 1)));
+    HIPCHK(c, c->w_counts.ensure(4 * ((size_t)nt + 1)));
+    HIPCHK(c, c->w_bucket.ensure(4 * ((size_t)nt + 1)));
+    HIPCHK(c, c->w_cursor.ensure(4 * ((size_t)nt + 1)));
+    HIPCHK(c, c->w_items.ensure(4 * ((size_t)nt + 1)));
+    HIPCHK(c, c->w_recs.ensure(8 * (size_t)rec_words(w.W) * 2 * std::max<uint32_t>(p.n, 1)));
+    const bool tm = c->timing;
+    if (tm)
+        for (int i = 0; i < 6; ++i)
+            if (!c->ev[i]) HIPCHK(c, hipEventCreate(&c->ev[i]));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
+    if (b->n_txn) HIPCHK(c, hipMemsetAsync(b->verdict, 0, b->n_txn, s));
+    HIPCHK(c, hipMemsetAsync(c->w_counts.p, 0, 4 * ((size_t)nt + 1), s));
+    const int grid_l = (int)std::min<size_t>(std::max<size_t>((std::max(p.n, p.n_lock) + 255) / 256, 1), 1024);
+    HIPCHK(c, launch_locate(w, p, c->w_code.as<uint64_t>(), c->w_counts.as<uint32_t>(), b->verdict,
+                            grid_l, s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
+    uint32_t max_items = 0;
+    if (p.n && w.ntiles) {
+        HIPCHK(c, launch_plan(c->w_counts.as<uint32_t>(), w.ntiles, c->w_bucket.as<uint32_t>(),
+                              c->w_cursor.as<uint32_t>(), c->w_items.as<uint32_t>(), s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
+        const int grid_s = (int)std::min<size_t>((p.n + 2047) / 2048, 1024);
+        HIPCHK(c, launch_scatter(w, p, c->w_code.as<uint64_t>(), c->w_cursor.as<uint32_t>(),
+                                 c->w_recs.as<uint64_t>(), grid_s, s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
+        max_items = w.ntiles + (uint32_t)((2 * (size_t)p.n + kJoinChunk - 1) / kJoinChunk);
+        HIPCHK(c, launch_join(w, c->w_recs.as<uint64_t>(), c->w_bucket.as<uint32_t>(),
+                              c->w_items.as<uint32_t>(), max_items, b->verdict, s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
+    } else if (tm) {
+        HIPCHK(c, hipEventRecord(c->ev[2], s));
+        HIPCHK(c, hipEventRecord(c->ev[3], s));
+        HIPCHK(c, hipEventRecord(c->ev[4], s));
+    }
+    HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
+    return HSC_OK;
+}
+
+static int collect_timing(hsc_ctx *c)
+{
+    if (!c->timing || !c->ev[5]) return HSC_OK;
+    HIPCHK(c, hipEventSynchronize(c->ev[5]));
+    float t[5];
+    for (int i = 0; i < 5; ++i) (void)hipEventElapsedTime(&t[i], c->ev[i], c->ev[i + 1]);
+    c->last.locate_ms = t[0];
+    c->last.plan_ms = t[1];
+    c->last.scatter_ms = t[2];
+    c->last.join_ms = t[3];
+    c->last.pack_ms = t[4];
+    (void)hipEventElapsedTime(&c->last.probe_total_ms, c->ev[0], c->ev[5]);
+    uint32_t nrec = 0;
+    if (c->ntiles && c->w_bucket.p)
+        HIPCHK(c, hipMemcpy(&nrec, c->w_bucket.as<uint32_t>() + c->ntiles, 4, hipMemcpyDeviceToHost));
+    c->last.records = nrec;
+    return HSC_OK;
+}
+
+// Upload the marshalled batch, run the join, read back per-txn verdicts.
+static int run_marshalled(hsc_ctx *c, int *rc_out)
+{
+    hipStream_t s = c->stream;
+    const hsc_marshalled &m = c->m;
+    const int W = c->W;
+    HIPCHK(c, c->p_lo.ensure(8 * (size_t)W * std::max<size_t>(m.n, 1)));
+    HIPCHK(c, c->p_hi.ensure(8 * (size_t)W * std::max<size_t>(m.n, 1)));
+    HIPCHK(c, c->p_gid.ensure(4 * std::max<size_t>(m.n, 1)));
+    HIPCHK(c, c->p_snap.ensure(8 * std::max<size_t>(m.n, 1)));
+    HIPCHK(c, c->p_txn.ensure(4 * std::max<size_t>(m.n, 1)));
+    HIPCHK(c, c->p_lock_table.ensure(4 * std::max<size_t>(m.n_lock, 1)));
+    HIPCHK(c, c->p_lock_snap.ensure(8 * std::max<size_t>(m.n_lock, 1)));
+    HIPCHK(c, c->p_lock_txn.ensure(4 * std::max<size_t>(m.n_lock, 1)));
+    HIPCHK(c, c->p_verdict.ensure(std::max<size_t>(m.n_txn, 1)));
+    if (m.n) {
+        HIPCHK(c, hipMemcpyAsync(c->p_lo.p, m.lo, 8 * (size_t)W * m.n, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->p_hi.p, m.hi, 8 * (size_t)W * m.n, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->p_gid.p, m.gid, 4 * m.n, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->p_snap.p, m.snap, 8 * m.n, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->p_txn.p, m.txn, 4 * m.n, hipMemcpyHostToDevice, s));
+    }
+    if (m.n_lock) {
+        HIPCHK(c, hipMemcpyAsync(c->p_lock_table.p, m.lock_table, 4 * m.n_lock, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->p_lock_snap.p, m.lock_snap, 8 * m.n_lock, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->p_lock_txn.p, m.lock_txn, 4 * m.n_lock, hipMemcpyHostToDevice, s));
+    }
+    hsc_probe_batch b{};
+    b.n = m.n;
+    b.lo = c->p_lo.as<uint64_t>();
+    b.hi = c->p_hi.as<uint64_t>();
+    b.gid = c->p_gid.as<uint32_t>();
+    b.snap = c->p_snap.as<uint64_t>();
+    b.txn = c->p_txn.as<uint32_t>();
+    b.n_lock = m.n_lock;
+    b.lock_table = c->p_lock_table.as<uint32_t>();
+    b.lock_snap = c->p_lock_snap.as<uint64_t>();
+    b.lock_txn = c->p_lock_txn.as<uint32_t>();
+    b.n_txn = m.n_txn;
+    b.verdict = c->p_verdict.as<uint8_t>();
+    b.bitmap = nullptr;
+    int rc = probe(c, &b);
+    if (rc) return rc;
+    std::vector<uint8_t> v(std::max<size_t>(m.n_txn, 1));
+    if (m.n_txn) HIPCHK(c, hipMemcpyAsync(v.data(), c->p_verdict.p, m.n_txn, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    collect_timing(c);
+    for (size_t t = 0; t < m.n_txn; ++t) rc_out[t] = (m.forced[t] | v[t]) ? 1 : 0;
+    return HSC_OK;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int hsc_device_count(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int hsc_ctx_create(int device, hsc_ctx **out)
+{
+    if (!out) return HSC_EINVAL;
+    *out = nullptr;
+    int n = hsc_device_count();
+    if (device < 0 || device >= n) return HSC_EDEVICE;
+    if (hipSetDevice(device) != hipSuccess) return HSC_EDEVICE;
+    hsc_ctx *c = new (std::nothrow) hsc_ctx();
+    if (!c) return HSC_ENOMEM;
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return HSC_EDEVICE;
+    }
+    c->stream = c->own_stream;
+    *out = c;
+    return HSC_OK;
+}
+
+void hsc_ctx_destroy(hsc_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    DBuf *bufs[] = {&c->d_gid, &c->d_words, &c->d_lsn, &c->d_gid2, &c->d_words2, &c->d_lsn2,
+                    &c->d_flags, &c->d_scratch, &c->d_gstart, &c->d_gend, &c->d_tmax,
+                    &c->d_table_max, &c->d_group_table, &c->d_count, &c->p_lo, &c->p_hi,
+                    &c->p_gid, &c->p_snap, &c->p_txn, &c->p_lock_table, &c->p_lock_snap,
+                    &c->p_lock_txn, &c->p_verdict, &c->p_bitmap, &c->w_code, &c->w_counts,
+                    &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_recs};
+    for (DBuf *b : bufs) b->release();
+    for (auto &e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+int hsc_set_stream(hsc_ctx *c, void *st)
+{
+    if (!c) return HSC_EINVAL;
+    c->stream = st ? (hipStream_t)st : c->own_stream;
+    return HSC_OK;
+}
+
+const char *hsc_last_error(hsc_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+int hsc_window_reset(hsc_ctx *c)
+{
+    if (!c) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    clear_window(c);
+    c->end_lsn = 0;
+    return HSC_OK;
+}
+
+int hsc_window_ingest_log(hsc_ctx *c, const hsc_llog *log)
+{
+    if (!c || !log) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    int rc = ingest_log(c, log);
+    if (rc) return rc;
+    return ensure_built(c);
+}
+
+int hsc_window_append(hsc_ctx *c, const hsc_write *w, size_t n)
+{
+    if (!c || (!w && n)) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->host_staged) return fail(c, HSC_ESTATE, "append after device ingest");
+    for (size_t i = 0; i < n; ++i) {
+        if (!w[i].tbname) return fail(c, HSC_EINVAL, "write without table");
+        if (w[i].commit_lsn < c->last_append_lsn) return fail(c, HSC_EINVAL, "commit LSNs must not decrease");
+        c->last_append_lsn = w[i].commit_lsn;
+        int tid = table_id_or_add(c, w[i].tbname);
+        add_write(c, tid, w[i].idxnum, (const uint8_t *)w[i].key, w[i].keylen, w[i].key != nullptr,
+                  w[i].commit_lsn);
+    }
+    c->dirty = true;
+    return HSC_OK;
+}
+
+int hsc_window_set_end(hsc_ctx *c, uint64_t end_lsn)
+{
+    if (!c) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->end_lsn = end_lsn;
+    return HSC_OK;
+}
+
+int hsc_window_build(hsc_ctx *c)
+{
+    if (!c) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    return ensure_built(c);
+}
+
+int hsc_register_group(hsc_ctx *c, const char *tbname, int idxnum, int keylen)
+{
+    if (!c || !tbname || keylen < 0 || keylen > kMaxWords * 8) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    int tid = table_id_or_add(c, tbname);
+    return group_id_or_add(c, tid, idxnum, keylen);
+}
+
+int hsc_window_ingest_device(hsc_ctx *c, size_t n, int words, const uint32_t *gid,
+                             const uint64_t *key_words, const uint64_t *lsn, uint64_t end_lsn)
+{
+    if (!c || words < 1 || words > kMaxWords || (n && (!gid || !key_words || !lsn)))
+        return HSC_EINVAL;
+    if (n >= 0xFFFFFFFFull) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    clear_window(c);
+    c->host_staged = false;
+    c->end_lsn = end_lsn;
+    if (words < window_words(c)) return fail(c, HSC_EINVAL, "fewer key words than a registered group needs");
+    c->W = words;
+    c->cap = std::max<size_t>(64, (n + 63) & ~(size_t)63);
+    HIPCHK(c, c->d_gid.ensure(c->cap * 4));
+    HIPCHK(c, c->d_words.ensure(c->cap * 8 * (size_t)words));
+    HIPCHK(c, c->d_lsn.ensure(c->cap * 8));
+    hipStream_t s = c->stream;
+    if (n) {
+        HIPCHK(c, hipMemcpyAsync(c->d_gid.p, gid, 4 * n, hipMemcpyDeviceToDevice, s));
+        for (int j = 0; j < words; ++j)
+            HIPCHK(c, hipMemcpyAsync(c->d_words.as<uint64_t>() + (size_t)j * c->cap, key_words + (size_t)j * n,
+                                     8 * n, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->d_lsn.p, lsn, 8 * n, hipMemcpyDeviceToDevice, s));
+    }
+    int rc = device_build(c, n);
+    if (rc) return rc;
+    for (uint64_t v : c->h_table_max) c->max_commit = std::max(c->max_commit, v);
+    return HSC_OK;
+}
+
+int hsc_window_words(hsc_ctx *c) { return c ? c->W : 0; }
+size_t hsc_window_keys(hsc_ctx *c) { return c ? c->n : 0; }
+uint64_t hsc_window_end(hsc_ctx *c) { return c ? c->end_lsn : 0; }
+uint64_t hsc_window_max_commit(hsc_ctx *c) { return c ? c->max_commit : 0; }
+
+int hsc_table_id(hsc_ctx *c, const char *tbname)
+{
+    if (!c || !tbname) return -1;
+    auto it = c->table_ids.find(tbname);
+    return it == c->table_ids.end() ? -1 : it->second;
+}
+
+int hsc_marshal_readsets(hsc_ctx *c, const hsc_readsets *rs, const hsc_marshalled **out)
+{
+    if (!c || !rs || !out) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    int rc = ensure_built(c);
+    if (rc) return rc;
+    rc = marshal_readsets(c, rs);
+    *out = &c->m;
+    return rc;
+}
+
+int hsc_check_readsets(hsc_ctx *c, const hsc_readsets *rs, int *rc_out)
+{
+    if (!c || !rs || (!rc_out && rs->ntxn)) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    int rc = ensure_built(c);
+    if (!rc) rc = marshal_readsets(c, rs);
+    if (!rc) rc = run_marshalled(c, rc_out);
+    if (rc)
+        for (int t = 0; t < rs->ntxn; ++t) rc_out[t] = 1;  // fail closed
+    return rc;
+}
+
+int hip_serial_check_batch(void *vctx, void *const *ranges, unsigned int *file,
+                           unsigned int *offset, int regop_only, int n, int *rc_out)
+{
+    hsc_ctx *c = (hsc_ctx *)vctx;
+    if (!c || n < 0 || (n && (!ranges || !rc_out)) || (!file) != (!offset)) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    int rc = ensure_built(c);
+    if (rc) {
+        for (int i = 0; i < n; ++i) rc_out[i] = 1;
+        return rc;
+    }
+    std::vector<int> slot(n, -1);  // element -> txn index in the device batch
+    std::vector<hsc_currangearr *> full;
+    std::vector<uint64_t> snaps;
+    for (int i = 0; i < n; ++i) {
+        hsc_currangearr *a = (hsc_currangearr *)ranges[i];
+        rc_out[i] = 0;
+        if (!a) continue;  // bdb_osql_serial_check: ranges == NULL -> 0
+        unsigned int *pf = file ? &file[i] : &a->file;
+        unsigned int *po = offset ? &offset[i] : &a->offset;
+        const uint64_t S = ((uint64_t)*pf << 32) | *po;
+        if (regop_only) {
+            rc_out[i] = regop_rc(c, S);
+            continue;
+        }
+        *pf = (unsigned int)(c->end_lsn >> 32);  // full mode: *file,*offset := curlsn
+        *po = (unsigned int)c->end_lsn;
+        slot[i] = (int)full.size();
+        full.push_back(a);
+        snaps.push_back(S);
+    }
+    if (full.empty()) return HSC_OK;
+    marshal_begin(c, full.size());
+    std::vector<TxnTable> tabs;
+    for (size_t t = 0; t < full.size(); ++t) {
+        const uint64_t S = snaps[t];
+        int f = full_forced(c, S);
+        if (f >= 0) {
+            c->m_forced[t] = (uint8_t)f;
+            continue;
+        }
+        hsc_currangearr *a = full[t];
+        auto get = [&](int k) {
+            const hsc_currange *r = a->ranges[k];
+            RangeRef x;
+            auto it = r->tbname ? c->table_ids.find(r->tbname) : c->table_ids.end();
+            x.tid = it == c->table_ids.end() ? -1 : it->second;
+            x.idxnum = r->idxnum;
+            x.lkey = (const uint8_t *)r->lkey;
+            x.rkey = (const uint8_t *)r->rkey;
+            x.lkeylen = r->lkeylen;
+            x.rkeylen = r->rkeylen;
+            x.lflag = r->lflag;
+            x.rflag = r->rflag;
+            x.islocked = r->islocked;
+            return x;
+        };
+        marshal_txn(c, (uint32_t)t, S, a->size, get, tabs);
+    }
+    marshal_finish(c, full.size());
+    std::vector<int> rcs(full.size(), 1);
+    rc = run_marshalled(c, rcs.data());
+    for (int i = 0; i < n; ++i)
+        if (slot[i] >= 0) rc_out[i] = rc ? 1 : rcs[slot[i]];
+    return rc;
+}
+
+int hip_bdb_osql_serial_check(void *ctx, void *ranges, unsigned int *file, unsigned int *offset,
+                              int regop_only)
+{
+    if (!ranges) return 0;
+    int rc_out = 1;
+    void *arr[1] = {ranges};
+    int rc = hip_serial_check_batch(ctx, arr, file, offset, regop_only, 1, &rc_out);
+    return rc ? 1 : rc_out;  // errors are "not serializable"
+}
+
+int hsc_probe_device(hsc_ctx *c, const hsc_probe_batch *b)
+{
+    if (!c || !b) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    if (c->dirty) return fail(c, HSC_ESTATE, "window not built");
+    return probe(c, b);
+}
+
+int hsc_pack_verdicts(hsc_ctx *c, const uint8_t *verdict, size_t n_txn, uint64_t *bitmap)
+{
+    if (!c || (n_txn && (!verdict || !bitmap)) || n_txn > 0xFFFFFFFFull) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    HIPCHK(c, launch_pack(verdict, (uint32_t)n_txn, bitmap, c->stream));
+    return HSC_OK;
+}
+
+int hsc_synchronize(hsc_ctx *c)
+{
+    if (!c) return HSC_EINVAL;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return collect_timing(c);
+}
+
+int hsc_get_timing(hsc_ctx *c, hsc_timing *t)
+{
+    if (!c || !t) return HSC_EINVAL;
+    *t = c->last;
+    return HSC_OK;
+}
+
+int hsc_enable_timing(hsc_ctx *c, int on)
+{
+    if (!c) return HSC_EINVAL;
+    c->timing = on != 0;
+    return HSC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,98 @@
+// hsc_internal.h -- device data layout shared by the host driver (hsc_host.cpp)
+// and the gfx950 kernels (hsc_kernels.hip).
+//
+// Resident write window (one per context / GPU), all struct-of-arrays in HBM:
+//   words[j * cap + i]  key word j of row i (big-endian bytes 8j..8j+7 of the
+//                       zero-padded key, as a native u64: numeric order of the
+//                       words == memcmp order of the bytes)
+//   lsn[i]              max commit (regop) LSN of that (group, key)
+//   gid[i]              key group = (table, index, key length)
+//   rows sorted by (gid, words[0..W-1]) and unique
+//   gstart/gend[g]      row span of group g
+//   tmax[l * ntiles + t] max lsn over tiles [t, t + 2^l)  (sparse table)
+//   table_max[tid]      max commit LSN of any write to table tid (dta too)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace hsc {
+
+constexpr int kMaxWords = 64;       // MAXKEYLEN 512 B (bbinc/cdb2_constants.h:33)
+constexpr int kTopCap = 2048;       // splitters held in LDS by the locate kernel
+constexpr int kHistCap = 8192;      // tiles whose bucket counters fit in LDS
+constexpr int kJoinThreads = 512;
+constexpr int kJoinChunk = 1024;    // join records per workgroup
+constexpr int kLdsJoinBudget = 49152;
+
+// Probe codes written by the locate kernel: a | b << 31 | kind << 62.
+constexpr uint64_t kKindFull = 1, kKindSplit = 2;
+// Join record kinds (top two bits of the gid field).
+constexpr uint32_t kRecFull = 1, kRecHead = 2, kRecTail = 3;
+
+struct WinView {
+    const uint64_t *words;
+    size_t stride;            // cap of the words array (row stride per word)
+    const uint64_t *lsn;
+    const uint32_t *gid;
+    const uint32_t *gstart, *gend;
+    const uint64_t *tmax;
+    const uint64_t *table_max;
+    uint32_t n, ntiles, ntables;
+    int W, log2T, levels;
+};
+
+struct ProbeView {
+    const uint64_t *lo, *hi;
+    const uint32_t *gid;
+    const uint64_t *snap;
+    const uint32_t *txn;
+    const uint32_t *lock_table;
+    const uint64_t *lock_snap;
+    const uint32_t *lock_txn;
+    uint32_t n, n_lock;
+};
+
+// Join-record layout: rec_words u64 per record = lo[W] hi[W] snap meta,
+// meta = txn | (gid | kind << 30) << 32.  2W+2 words -> 16-byte multiple.
+__host__ __device__ inline int rec_words(int W) { return 2 * W + 2; }
+
+// Tile size: largest power of two whose keys + lsn fit the LDS budget.
+inline int tile_log2(int W)
+{
+    int l = 11;
+    while (l > 6 && ((size_t)1 << l) * (size_t)(8 * W + 8) > (size_t)kLdsJoinBudget)
+        --l;
+    return l;
+}
+
+// ---- launchers (hsc_kernels.hip) -------------------------------------------
+// Ingest.
+hipError_t radix_sort_rows(int W, size_t n, uint32_t *gid, uint64_t *words, uint64_t *lsn,
+                           size_t stride, uint32_t *gid_alt, uint64_t *words_alt,
+                           uint64_t *lsn_alt, void *scratch, size_t scratch_bytes,
+                           bool *result_in_alt, hipStream_t s);
+size_t radix_scratch_bytes(size_t n, int W);
+hipError_t dedupe_rows(int W, size_t n, const uint32_t *gid, const uint64_t *words,
+                       const uint64_t *lsn, size_t stride_in, uint32_t *gid_out,
+                       uint64_t *words_out, uint64_t *lsn_out, size_t stride_out,
+                       uint32_t *flags, void *scratch, size_t scratch_bytes,
+                       uint32_t *d_count, hipStream_t s);
+size_t scan_scratch_bytes(size_t n);
+hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, int ngroups,
+                           uint64_t *tmax, const uint32_t *group_table,
+                           uint64_t *table_max, hipStream_t s);
+// Probe.
+hipError_t launch_locate(const WinView &w, const ProbeView &p, uint64_t *code,
+                         uint32_t *counts, uint8_t *verdict, int grid, hipStream_t s);
+hipError_t launch_plan(const uint32_t *counts, uint32_t ntiles, uint32_t *bucket_off,
+                       uint32_t *cursor, uint32_t *item_off, hipStream_t s);
+hipError_t launch_scatter(const WinView &w, const ProbeView &p, const uint64_t *code,
+                          uint32_t *cursor, uint64_t *recs, int grid, hipStream_t s);
+hipError_t launch_join(const WinView &w, const uint64_t *recs, const uint32_t *bucket_off,
+                       const uint32_t *item_off, uint32_t max_items, uint8_t *verdict,
+                       hipStream_t s);
+hipError_t launch_pack(const uint8_t *verdict, uint32_t n_txn, uint64_t *bitmap,
+                       hipStream_t s);
+
+}  // namespace hsc

@@ -1,0 +1,883 @@
+// hsc_kernels.hip -- gfx950 kernels of the serializable conflict validator.
+//
+// The reference answers one read set at a time by re-walking the log window
+// and scanning every read range of the written index linearly per write key
+// (bdb/serializable.c:390-539 -> db/glue.c:2937-2961).  Here the window is
+// resident and sorted once; a batch of read ranges becomes a range-max join:
+//
+//   locate  (one thread / range): splitter search in LDS -> first and last
+//           window tile the range can touch; whole tiles strictly inside the
+//           range are answered from the tile-max sparse table; the two end
+//           tiles get a join record (FULL, or HEAD + TAIL).  Also table locks.
+//   plan    (one workgroup): bucket offsets and work items per tile.
+//   scatter (one thread / range): LDS-aggregated slot reservation, writes the
+//           join records grouped by tile.
+//   join    (one workgroup / tile chunk): stages the tile's keys + LSNs in LDS
+//           (each window byte is read from HBM once per batch), binary-searches
+//           every record's bounds in LDS and tests max LSN > snapshot.
+//   pack    (ballot): per-read-set verdict bytes -> bitmap.
+//
+// Wave size is 64 everywhere (ballots are 64-bit).
+#include "hsc_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <utility>
+
+namespace hsc {
+
+// ============================================================================
+// helpers
+// ============================================================================
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
+{
+    for (int o = 32; o > 0; o >>= 1) {
+        uint64_t y = __shfl_xor(v, o, 64);
+        v = y > v ? y : v;
+    }
+    return v;
+}
+
+// Exclusive block scan of one u32 per thread; NT threads.
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds, uint32_t &total)
+{
+    constexpr int NW = NT / 64;
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        uint32_t s = lane < NW ? lds[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < NW; o <<= 1) {
+            uint32_t y = __shfl_up(s, o, 64);
+            if (lane >= o) s += y;
+        }
+        if (lane < NW) lds[lane] = s;
+    }
+    __syncthreads();
+    uint32_t pre = wid ? lds[wid - 1] : 0;
+    total = lds[NW - 1];
+    __syncthreads();
+    return pre + x - v;
+}
+
+// sign(A - B) for two keys of W words: A's word 0 is in a register, its word
+// j >= 1 at a_mem[j * as]; B's word j at b0[j * bs].
+__device__ __forceinline__ int cmp_words(int W, uint64_t a_w0, const uint64_t *a_mem, size_t as,
+                                         const uint64_t *b0, size_t bs)
+{
+    uint64_t b = b0[0];
+    if (a_w0 != b) return a_w0 < b ? -1 : 1;
+    for (int j = 1; j < W; ++j) {
+        const uint64_t a = a_mem[(size_t)j * as];
+        b = b0[(size_t)j * bs];
+        if (a != b) return a < b ? -1 : 1;
+    }
+    return 0;
+}
+
+// ============================================================================
+// ingest: LSD radix sort of (gid, words) rows carrying lsn, stable
+// ============================================================================
+constexpr int kSortThreads = 256;
+constexpr int kSortItems = 16;
+constexpr int kSortTile = kSortThreads * kSortItems;  // rows per block
+constexpr int kDigitsPerHist = 32;
+
+// Digit d (0 = least significant byte of the composite key).
+__device__ __forceinline__ uint32_t row_digit(int W, int d, size_t i, const uint32_t *gid,
+                                              const uint64_t *words, size_t stride)
+{
+    if (d < 8 * W) {
+        int j = W - 1 - (d >> 3);
+        return (uint32_t)(words[(size_t)j * stride + i] >> (8 * (d & 7))) & 0xFFu;
+    }
+    return (gid[i] >> (8 * (d - 8 * W))) & 0xFFu;
+}
+
+// Histograms of digits [d0, d0 + nd) over all rows (to skip constant digits).
+__global__ __launch_bounds__(256) void k_hist_digits(int W, size_t n, const uint32_t *gid,
+                                                     const uint64_t *words, size_t stride,
+                                                     int d0, int nd, uint32_t *hist)
+{
+    __shared__ uint32_t h[kDigitsPerHist * 256];
+    for (int i = threadIdx.x; i < nd * 256; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        for (int k = 0; k < nd; ++k)
+            atomicAdd(&h[k * 256 + row_digit(W, d0 + k, i, gid, words, stride)], 1u);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nd * 256; i += blockDim.x)
+        if (h[i]) atomicAdd(&hist[(size_t)d0 * 256 + i], h[i]);
+}
+
+// Per-block digit counts, digit-major: counts[digit * nblocks + block].
+__global__ __launch_bounds__(kSortThreads) void k_rs_count(int W, int d, size_t n,
+                                                           const uint32_t *gid,
+                                                           const uint64_t *words, size_t stride,
+                                                           uint32_t *counts, uint32_t nblocks)
+{
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * kSortTile;
+    for (int k = 0; k < kSortItems; ++k) {
+        size_t i = base + (size_t)k * kSortThreads + threadIdx.x;
+        if (i < n) atomicAdd(&h[row_digit(W, d, i, gid, words, stride)], 1u);
+    }
+    __syncthreads();
+    counts[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+// Stable scatter: rows of a block are ranked in index order (round-major,
+// lane order inside a round) with 8 ballots per round for the wave match.
+__global__ __launch_bounds__(kSortThreads) void k_rs_scatter(
+    int W, int d, size_t n, const uint32_t *gid, const uint64_t *words, const uint64_t *lsn,
+    size_t stride, uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o,
+    const uint32_t *offsets, uint32_t nblocks)
+{
+    __shared__ uint32_t gbase[256];
+    __shared__ uint32_t running[256];
+    __shared__ uint32_t wave_h[kSortThreads / 64][256];
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    gbase[threadIdx.x] = offsets[(size_t)threadIdx.x * nblocks + blockIdx.x];
+    running[threadIdx.x] = 0;
+    const size_t base = (size_t)blockIdx.x * kSortTile;
+    const uint64_t lt_mask = (lane ? (~0ull >> (64 - lane)) : 0ull);
+    for (int k = 0; k < kSortItems; ++k) {
+        const size_t i = base + (size_t)k * kSortThreads + threadIdx.x;
+        const bool valid = i < n;
+        uint32_t dig = valid ? row_digit(W, d, i, gid, words, stride) : 0;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            uint64_t m = __ballot((dig >> b) & 1u);
+            peers &= ((dig >> b) & 1u) ? m : ~m;
+        }
+        const uint32_t rank = __popcll(peers & lt_mask);
+        const uint32_t cnt = __popcll(peers);
+        for (int t = threadIdx.x; t < (kSortThreads / 64) * 256; t += kSortThreads)
+            (&wave_h[0][0])[t] = 0;
+        __syncthreads();
+        if (valid && rank == 0) wave_h[wid][dig] = cnt;
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = gbase[dig] + running[dig] + rank;
+            for (int w2 = 0; w2 < wid; ++w2) pos += wave_h[w2][dig];
+            gid_o[pos] = gid[i];
+            for (int j = 0; j < W; ++j) words_o[(size_t)j * stride + pos] = words[(size_t)j * stride + i];
+            lsn_o[pos] = lsn[i];
+        }
+        __syncthreads();
+        {
+            uint32_t add = 0;
+            for (int w2 = 0; w2 < kSortThreads / 64; ++w2) add += wave_h[w2][threadIdx.x];
+            running[threadIdx.x] += add;
+        }
+        __syncthreads();
+    }
+}
+
+// ---- generic exclusive scan of u32 (in place), block sums recursively -----
+constexpr int kScanThreads = 256;
+constexpr int kScanItems = 8;
+constexpr int kScanTile = kScanThreads * kScanItems;
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_tile(uint32_t *a, size_t n, uint32_t *sums)
+{
+    __shared__ uint32_t lds[kScanThreads / 64];
+    const size_t base = (size_t)blockIdx.x * kScanTile + (size_t)threadIdx.x * kScanItems;
+    uint32_t v[kScanItems];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        v[k] = (base + k < n) ? a[base + k] : 0;
+        s += v[k];
+    }
+    uint32_t total;
+    uint32_t pre = block_excl_scan<kScanThreads>(s, lds, total);
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        if (base + k < n) a[base + k] = pre;
+        pre += v[k];
+    }
+    if (threadIdx.x == 0 && sums) sums[blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_add(uint32_t *a, size_t n, const uint32_t *sums)
+{
+    const uint32_t add = sums[blockIdx.x];
+    const size_t base = (size_t)blockIdx.x * kScanTile;
+    for (int k = threadIdx.x; k < kScanTile; k += kScanThreads)
+        if (base + k < n) a[base + k] += add;
+}
+
+size_t scan_scratch_bytes(size_t n)
+{
+    size_t total = 0;
+    while (n > (size_t)kScanTile) {
+        n = (n + kScanTile - 1) / kScanTile;
+        total += n * sizeof(uint32_t);
+    }
+    return total + 256;
+}
+
+static hipError_t scan_u32(uint32_t *a, size_t n, uint32_t *scratch, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    size_t nb = (n + kScanTile - 1) / kScanTile;
+    if (nb == 1) {
+        k_scan_tile<<<1, kScanThreads, 0, s>>>(a, n, nullptr);
+        return hipGetLastError();
+    }
+    uint32_t *sums = scratch;
+    k_scan_tile<<<(unsigned)nb, kScanThreads, 0, s>>>(a, n, sums);
+    hipError_t e = scan_u32(sums, nb, scratch + nb, s);
+    if (e != hipSuccess) return e;
+    k_scan_add<<<(unsigned)nb, kScanThreads, 0, s>>>(a, n, sums);
+    return hipGetLastError();
+}
+
+size_t radix_scratch_bytes(size_t n, int W)
+{
+    size_t nblocks = (n + kSortTile - 1) / kSortTile;
+    size_t ndig = 8 * (size_t)W + 4;
+    return ndig * 256 * sizeof(uint32_t) + 256 * nblocks * sizeof(uint32_t) +
+           scan_scratch_bytes(256 * nblocks) + 1024;
+}
+
+hipError_t radix_sort_rows(int W, size_t n, uint32_t *gid, uint64_t *words, uint64_t *lsn,
+                           size_t stride, uint32_t *gid_alt, uint64_t *words_alt,
+                           uint64_t *lsn_alt, void *scratch, size_t scratch_bytes,
+                           bool *result_in_alt, hipStream_t s)
+{
+    *result_in_alt = false;
+    if (n <= 1) return hipSuccess;
+    if (scratch_bytes < radix_scratch_bytes(n, W)) return hipErrorInvalidValue;
+    const int ndig = 8 * W + 4;
+    const uint32_t nblocks = (uint32_t)((n + kSortTile - 1) / kSortTile);
+    uint32_t *hist = (uint32_t *)scratch;
+    uint32_t *counts = hist + (size_t)ndig * 256;
+    uint32_t *scan_tmp = counts + (size_t)256 * nblocks;
+    hipError_t e = hipMemsetAsync(hist, 0, (size_t)ndig * 256 * sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    const unsigned hgrid = (unsigned)std::min<size_t>((n + 255) / 256, 2048);
+    for (int d0 = 0; d0 < ndig; d0 += kDigitsPerHist) {
+        int nd = std::min(kDigitsPerHist, ndig - d0);
+        k_hist_digits<<<hgrid, 256, 0, s>>>(W, n, gid, words, stride, d0, nd, hist);
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    uint32_t *hh = (uint32_t *)malloc((size_t)ndig * 256 * sizeof(uint32_t));
+    if (!hh) return hipErrorOutOfMemory;
+    e = hipMemcpyAsync(hh, hist, (size_t)ndig * 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        free(hh);
+        return e;
+    }
+    bool alt = false;
+    uint32_t *g0 = gid, *g1 = gid_alt;
+    uint64_t *w0 = words, *w1 = words_alt, *l0 = lsn, *l1 = lsn_alt;
+    for (int d = 0; d < ndig; ++d) {
+        bool constant = false;
+        for (int b = 0; b < 256; ++b)
+            if (hh[(size_t)d * 256 + b] == n) constant = true;
+        if (constant) continue;
+        k_rs_count<<<nblocks, kSortThreads, 0, s>>>(W, d, n, g0, w0, stride, counts, nblocks);
+        e = scan_u32(counts, (size_t)256 * nblocks, scan_tmp, s);
+        if (e != hipSuccess) break;
+        k_rs_scatter<<<nblocks, kSortThreads, 0, s>>>(W, d, n, g0, w0, l0, stride, g1, w1, l1,
+                                                       counts, nblocks);
+        e = hipGetLastError();
+        if (e != hipSuccess) break;
+        std::swap(g0, g1);
+        std::swap(w0, w1);
+        std::swap(l0, l1);
+        alt = !alt;
+    }
+    free(hh);
+    *result_in_alt = alt;
+    return e;
+}
+
+// ---- dedupe: keep the last row of every run of equal (gid, key) ----------
+__global__ void k_flag_last(int W, size_t n, const uint32_t *gid, const uint64_t *words,
+                            size_t stride, uint32_t *flags)
+{
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t f = 1;
+    if (i + 1 < n && gid[i] == gid[i + 1]) {
+        f = 0;
+        for (int j = 0; j < W; ++j)
+            if (words[(size_t)j * stride + i] != words[(size_t)j * stride + i + 1]) {
+                f = 1;
+                break;
+            }
+    }
+    flags[i] = f;
+}
+
+__global__ void k_compact(int W, size_t n, const uint32_t *gid, const uint64_t *words,
+                          const uint64_t *lsn, size_t stride_in, const uint32_t *pos,
+                          const uint32_t *flags_last, uint32_t *gid_o, uint64_t *words_o,
+                          uint64_t *lsn_o, size_t stride_out, uint32_t *d_count)
+{
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    // flags were scanned in place into pos; recover "is last" from neighbours
+    uint32_t p = pos[i];
+    uint32_t nxt = (i + 1 < n) ? pos[i + 1] : flags_last[0] + p;
+    if (nxt == p) return;
+    gid_o[p] = gid[i];
+    for (int j = 0; j < W; ++j) words_o[(size_t)j * stride_out + p] = words[(size_t)j * stride_in + i];
+    lsn_o[p] = lsn[i];
+    if (i + 1 == n) *d_count = p + 1;
+}
+
+__global__ void k_copy_last_flag(const uint32_t *flags, size_t n, uint32_t *out)
+{
+    out[0] = flags[n - 1];
+}
+
+hipError_t dedupe_rows(int W, size_t n, const uint32_t *gid, const uint64_t *words,
+                       const uint64_t *lsn, size_t stride_in, uint32_t *gid_out,
+                       uint64_t *words_out, uint64_t *lsn_out, size_t stride_out,
+                       uint32_t *flags, void *scratch, size_t scratch_bytes,
+                       uint32_t *d_count, hipStream_t s)
+{
+    if (n == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
+    if (scratch_bytes < scan_scratch_bytes(n) + 16) return hipErrorInvalidValue;
+    uint32_t *last = (uint32_t *)scratch;
+    uint32_t *tmp = last + 4;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    k_flag_last<<<g, 256, 0, s>>>(W, n, gid, words, stride_in, flags);
+    k_copy_last_flag<<<1, 1, 0, s>>>(flags, n, last);
+    hipError_t e = scan_u32(flags, n, tmp, s);
+    if (e != hipSuccess) return e;
+    k_compact<<<g, 256, 0, s>>>(W, n, gid, words, lsn, stride_in, flags, last, gid_out, words_out,
+                                lsn_out, stride_out, d_count);
+    return hipGetLastError();
+}
+
+// ---- summaries: group spans, tile maxima, sparse table, table maxima ------
+__global__ void k_group_bounds(uint32_t n, const uint32_t *gid, uint32_t *gstart, uint32_t *gend)
+{
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t g = gid[i];
+    if (i == 0 || gid[i - 1] != g) gstart[g] = i;
+    if (i + 1 == n || gid[i + 1] != g) gend[g] = i + 1;
+}
+
+__global__ __launch_bounds__(256) void k_tile_max(uint32_t n, int log2T, const uint64_t *lsn,
+                                                  uint64_t *tmax0)
+{
+    __shared__ uint64_t part[4];
+    const uint32_t t0 = blockIdx.x << log2T;
+    const uint32_t t1 = min(n, t0 + (1u << log2T));
+    uint64_t m = 0;
+    for (uint32_t i = t0 + threadIdx.x; i < t1; i += 256) m = lsn[i] > m ? lsn[i] : m;
+    m = wave_max_u64(m);
+    if (lane_id() == 0) part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t r = part[0];
+        for (int k = 1; k < 4; ++k) r = part[k] > r ? part[k] : r;
+        tmax0[blockIdx.x] = r;
+    }
+}
+
+__global__ void k_sparse_level(uint32_t ntiles, int level, uint64_t *tmax)
+{
+    uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntiles) return;
+    const uint64_t *prev = tmax + (size_t)(level - 1) * ntiles;
+    uint32_t u = t + (1u << (level - 1));
+    uint64_t a = prev[t], b = u < ntiles ? prev[u] : 0;
+    tmax[(size_t)level * ntiles + t] = a > b ? a : b;
+}
+
+__global__ __launch_bounds__(256) void k_group_table_max(const uint32_t *gstart,
+                                                         const uint32_t *gend,
+                                                         const uint64_t *lsn,
+                                                         const uint32_t *group_table,
+                                                         uint64_t *table_max)
+{
+    __shared__ uint64_t part[4];
+    const uint32_t g = blockIdx.x;
+    uint64_t m = 0;
+    for (uint32_t i = gstart[g] + threadIdx.x; i < gend[g]; i += 256) m = lsn[i] > m ? lsn[i] : m;
+    m = wave_max_u64(m);
+    if (lane_id() == 0) part[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t r = part[0];
+        for (int k = 1; k < 4; ++k) r = part[k] > r ? part[k] : r;
+        if (r) atomicMax((unsigned long long *)&table_max[group_table[g]], (unsigned long long)r);
+    }
+}
+
+hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, int ngroups,
+                           uint64_t *tmax, const uint32_t *group_table, uint64_t *table_max,
+                           hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(gstart, 0, sizeof(uint32_t) * (size_t)ngroups, s);
+    if (e == hipSuccess) e = hipMemsetAsync(gend, 0, sizeof(uint32_t) * (size_t)ngroups, s);
+    if (e != hipSuccess) return e;
+    if (w.n == 0) return hipSuccess;
+    k_group_bounds<<<(w.n + 255) / 256, 256, 0, s>>>(w.n, w.gid, gstart, gend);
+    k_tile_max<<<w.ntiles, 256, 0, s>>>(w.n, w.log2T, w.lsn, tmax);
+    for (int l = 1; l < w.levels; ++l)
+        k_sparse_level<<<(w.ntiles + 255) / 256, 256, 0, s>>>(w.ntiles, l, tmax);
+    if (ngroups > 0)
+        k_group_table_max<<<ngroups, 256, 0, s>>>(gstart, gend, w.lsn, group_table, table_max);
+    return hipGetLastError();
+}
+
+// ============================================================================
+// probe
+// ============================================================================
+
+// sign((sg, splitter words) - (g, key)) for tile t's first row.
+__device__ __forceinline__ int cmp_splitter(const WinView &w, uint32_t t, uint32_t sg,
+                                            uint64_t sw0, uint32_t g, uint64_t k0, uint64_t k1,
+                                            const uint64_t *kmem, size_t ks)
+{
+    if (sg != g) return sg < g ? -1 : 1;
+    if (sw0 != k0) return sw0 < k0 ? -1 : 1;
+    if (w.W == 1) return 0;
+    const size_t pos = (size_t)t << w.log2T;
+    // words 1.. : sign(splitter - key) = -sign(key - splitter)
+    return -cmp_words(w.W - 1, k1, kmem + ks, ks, w.words + w.stride + pos, w.stride);
+}
+
+// Number of tiles whose first row compares < (g, key) (LEQ: <=).
+template <bool LEQ>
+__device__ uint32_t count_splitters(const WinView &w, const uint64_t *top_w0,
+                                    const uint32_t *top_g, uint32_t ntop, uint32_t stride_t,
+                                    uint32_t g, uint64_t k0, uint64_t k1, const uint64_t *kmem,
+                                    size_t ks)
+{
+    uint32_t lo = 0, hi = ntop;
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        int c = cmp_splitter(w, mid * stride_t, top_g[mid], top_w0[mid], g, k0, k1, kmem, ks);
+        if (LEQ ? c <= 0 : c < 0)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    if (lo == 0 || stride_t == 1) return lo * stride_t < w.ntiles ? lo * stride_t : w.ntiles;
+    uint32_t L = (lo - 1) * stride_t + 1;
+    uint32_t H = min(lo * stride_t, w.ntiles);
+    while (L < H) {
+        uint32_t mid = (L + H) >> 1;
+        const size_t pos = (size_t)mid << w.log2T;
+        int c = cmp_splitter(w, mid, w.gid[pos], w.words[pos], g, k0, k1, kmem, ks);
+        if (LEQ ? c <= 0 : c < 0)
+            L = mid + 1;
+        else
+            H = mid;
+    }
+    return L;
+}
+
+__device__ __forceinline__ uint64_t tiles_max(const WinView &w, uint32_t x, uint32_t y)
+{
+    uint32_t len = y - x + 1;
+    int k = 31 - __clz(len);
+    const uint64_t *lv = w.tmax + (size_t)k * w.ntiles;
+    uint64_t a = lv[x], b = lv[y - (1u << k) + 1];
+    return a > b ? a : b;
+}
+
+__global__ __launch_bounds__(256) void k_locate(WinView w, ProbeView p, uint64_t *code,
+                                                uint32_t *counts, uint8_t *verdict,
+                                                uint32_t ntop, uint32_t stride_t, int lds_hist)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint64_t *top_w0 = (uint64_t *)smem;
+    uint32_t *top_g = (uint32_t *)(top_w0 + ntop);
+    uint32_t *hist = top_g + ((ntop + 3) & ~3u);
+    for (uint32_t i = threadIdx.x; i < ntop; i += blockDim.x) {
+        const size_t pos = (size_t)(i * stride_t) << w.log2T;
+        top_w0[i] = w.words[pos];
+        top_g[i] = w.gid[pos];
+    }
+    if (lds_hist)
+        for (uint32_t i = threadIdx.x; i < w.ntiles; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+
+    const size_t ks = p.n;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < p.n; q += gridDim.x * blockDim.x) {
+        const uint32_t g = p.gid[q];
+        const uint64_t l0 = p.lo[q], l1 = w.W > 1 ? p.lo[ks + q] : 0;
+        const uint64_t h0 = p.hi[q], h1 = w.W > 1 ? p.hi[ks + q] : 0;
+        uint64_t cd = 0;
+        const uint32_t c2 =
+            count_splitters<true>(w, top_w0, top_g, ntop, stride_t, g, h0, h1, p.hi + q, ks);
+        if (c2 > 0) {
+            const uint32_t c =
+                count_splitters<false>(w, top_w0, top_g, ntop, stride_t, g, l0, l1, p.lo + q, ks);
+            const uint32_t a = c ? c - 1 : 0, b = c2 - 1;
+            if (a == b) {
+                cd = (uint64_t)a | ((uint64_t)a << 31) | (kKindFull << 62);
+            } else if (a < b) {
+                bool hit = false;
+                if (b > a + 1) hit = tiles_max(w, a + 1, b - 1) > p.snap[q];
+                if (hit)
+                    verdict[p.txn[q]] = 1;
+                else
+                    cd = (uint64_t)a | ((uint64_t)b << 31) | (kKindSplit << 62);
+            }
+        }
+        code[q] = cd;
+        if (cd) {
+            const uint32_t a = (uint32_t)(cd & 0x7FFFFFFFu);
+            const uint32_t b = (uint32_t)((cd >> 31) & 0x7FFFFFFFu);
+            if (lds_hist) {
+                atomicAdd(&hist[a], 1u);
+                if (b != a) atomicAdd(&hist[b], 1u);
+            } else {
+                atomicAdd(&counts[a], 1u);
+                if (b != a) atomicAdd(&counts[b], 1u);
+            }
+        }
+    }
+    // table locks: any write to a locked table after the snapshot
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < p.n_lock;
+         q += gridDim.x * blockDim.x) {
+        uint32_t t = p.lock_table[q];
+        if (t < w.ntables && w.table_max[t] > p.lock_snap[q]) verdict[p.lock_txn[q]] = 1;
+    }
+    if (lds_hist) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < w.ntiles; i += blockDim.x)
+            if (hist[i]) atomicAdd(&counts[i], hist[i]);
+    }
+}
+
+hipError_t launch_locate(const WinView &w, const ProbeView &p, uint64_t *code, uint32_t *counts,
+                         uint8_t *verdict, int grid, hipStream_t s)
+{
+    if (p.n == 0 && p.n_lock == 0) return hipSuccess;
+    uint32_t stride_t = (w.ntiles + kTopCap - 1) / kTopCap;
+    if (stride_t == 0) stride_t = 1;
+    uint32_t ntop = w.n ? (w.ntiles + stride_t - 1) / stride_t : 0;
+    int lds_hist = w.ntiles <= (uint32_t)kHistCap;
+    size_t lds = (size_t)ntop * 8 + (((size_t)ntop + 3) & ~(size_t)3) * 4 +
+                 (lds_hist ? (size_t)w.ntiles * 4 : 0);
+    k_locate<<<grid, 256, lds, s>>>(w, p, code, counts, verdict, ntop, stride_t, lds_hist);
+    return hipGetLastError();
+}
+
+// ---- plan: bucket offsets + work items (one workgroup) ---------------------
+__global__ __launch_bounds__(1024) void k_plan(const uint32_t *counts, uint32_t ntiles,
+                                               uint32_t *bucket_off, uint32_t *cursor,
+                                               uint32_t *item_off)
+{
+    __shared__ uint32_t lds[16];
+    uint32_t carry_b = 0, carry_i = 0;
+    for (uint32_t base = 0; base < ntiles; base += 1024) {
+        const uint32_t t = base + threadIdx.x;
+        const uint32_t c = t < ntiles ? counts[t] : 0;
+        const uint32_t ch = (c + kJoinChunk - 1) / kJoinChunk;
+        uint32_t tb, ti;
+        uint32_t pb = block_excl_scan<1024>(c, lds, tb);
+        uint32_t pi = block_excl_scan<1024>(ch, lds, ti);
+        if (t < ntiles) {
+            bucket_off[t] = carry_b + pb;
+            cursor[t] = carry_b + pb;
+            item_off[t] = carry_i + pi;
+        }
+        carry_b += tb;
+        carry_i += ti;
+    }
+    if (threadIdx.x == 0) {
+        bucket_off[ntiles] = carry_b;
+        item_off[ntiles] = carry_i;
+    }
+}
+
+hipError_t launch_plan(const uint32_t *counts, uint32_t ntiles, uint32_t *bucket_off,
+                       uint32_t *cursor, uint32_t *item_off, hipStream_t s)
+{
+    k_plan<<<1, 1024, 0, s>>>(counts, ntiles, bucket_off, cursor, item_off);
+    return hipGetLastError();
+}
+
+// ---- scatter: join records grouped by tile ---------------------------------
+constexpr int kScatterThreads = 256;
+constexpr int kScatterRound = 8;  // probes per thread per round
+
+__device__ __forceinline__ void write_record(uint64_t *recs, int rw, uint32_t slot, int W,
+                                             const ProbeView &p, uint32_t q, uint32_t kind)
+{
+    uint64_t *r = recs + (size_t)slot * rw;
+    const size_t ks = p.n;
+    for (int j = 0; j < W; ++j) {
+        r[j] = p.lo[(size_t)j * ks + q];
+        r[W + j] = p.hi[(size_t)j * ks + q];
+    }
+    r[2 * W] = p.snap[q];
+    r[2 * W + 1] = (uint64_t)p.txn[q] | ((uint64_t)(p.gid[q] | (kind << 30)) << 32);
+}
+
+__global__ __launch_bounds__(kScatterThreads) void k_scatter(WinView w, ProbeView p,
+                                                             const uint64_t *code,
+                                                             uint32_t *cursor, uint64_t *recs,
+                                                             int lds_agg)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t *cnt = (uint32_t *)smem;
+    const int W = w.W, rw = rec_words(W);
+    const uint32_t per_round = kScatterThreads * kScatterRound;
+    for (uint32_t base = blockIdx.x * per_round; base < p.n; base += gridDim.x * per_round) {
+        if (!lds_agg) {
+            for (int k = 0; k < kScatterRound; ++k) {
+                const uint32_t q = base + k * kScatterThreads + threadIdx.x;
+                if (q >= p.n) break;
+                const uint64_t cd = code[q];
+                if (!cd) continue;
+                const uint32_t a = (uint32_t)(cd & 0x7FFFFFFFu);
+                const uint32_t b = (uint32_t)((cd >> 31) & 0x7FFFFFFFu);
+                if ((cd >> 62) == kKindFull) {
+                    write_record(recs, rw, atomicAdd(&cursor[a], 1u), W, p, q, kRecFull);
+                } else {
+                    write_record(recs, rw, atomicAdd(&cursor[a], 1u), W, p, q, kRecHead);
+                    write_record(recs, rw, atomicAdd(&cursor[b], 1u), W, p, q, kRecTail);
+                }
+            }
+            continue;
+        }
+        for (uint32_t i = threadIdx.x; i < w.ntiles; i += kScatterThreads) cnt[i] = 0;
+        __syncthreads();
+        uint32_t la[kScatterRound], lb[kScatterRound];
+        uint64_t cds[kScatterRound];
+#pragma unroll
+        for (int k = 0; k < kScatterRound; ++k) {
+            const uint32_t q = base + k * kScatterThreads + threadIdx.x;
+            cds[k] = q < p.n ? code[q] : 0;
+            if (cds[k]) {
+                const uint32_t a = (uint32_t)(cds[k] & 0x7FFFFFFFu);
+                const uint32_t b = (uint32_t)((cds[k] >> 31) & 0x7FFFFFFFu);
+                la[k] = atomicAdd(&cnt[a], 1u);
+                if ((cds[k] >> 62) == kKindSplit) lb[k] = atomicAdd(&cnt[b], 1u);
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < w.ntiles; i += kScatterThreads) {
+            const uint32_t c = cnt[i];
+            if (c) cnt[i] = atomicAdd(&cursor[i], c);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kScatterRound; ++k) {
+            if (!cds[k]) continue;
+            const uint32_t q = base + k * kScatterThreads + threadIdx.x;
+            const uint32_t a = (uint32_t)(cds[k] & 0x7FFFFFFFu);
+            const uint32_t b = (uint32_t)((cds[k] >> 31) & 0x7FFFFFFFu);
+            if ((cds[k] >> 62) == kKindFull) {
+                write_record(recs, rw, cnt[a] + la[k], W, p, q, kRecFull);
+            } else {
+                write_record(recs, rw, cnt[a] + la[k], W, p, q, kRecHead);
+                write_record(recs, rw, cnt[b] + lb[k], W, p, q, kRecTail);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_scatter(const WinView &w, const ProbeView &p, const uint64_t *code,
+                          uint32_t *cursor, uint64_t *recs, int grid, hipStream_t s)
+{
+    if (p.n == 0) return hipSuccess;
+    int lds_agg = w.ntiles <= (uint32_t)kHistCap;
+    size_t lds = lds_agg ? (size_t)w.ntiles * 4 : 16;
+    k_scatter<<<grid, kScatterThreads, lds, s>>>(w, p, code, cursor, recs, lds_agg);
+    return hipGetLastError();
+}
+
+// ---- join: one workgroup per (tile, chunk of records) ----------------------
+// First row in [lo, hi) whose key compares >= key (LEQ=false) or > key
+// (LEQ=true); keys of the tile live in LDS as kw[j * T + i].
+template <bool UPPER>
+__device__ __forceinline__ uint32_t lds_bound(int W, const uint64_t *kw, uint32_t T, uint32_t lo,
+                                              uint32_t hi, uint64_t k0, uint64_t k1,
+                                              const uint64_t *kmem)
+{
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        // c = sign(key - row)
+        int c;
+        const uint64_t r0 = kw[mid];
+        if (k0 != r0)
+            c = k0 < r0 ? -1 : 1;
+        else if (W == 1)
+            c = 0;
+        else {
+            const uint64_t r1 = kw[T + mid];
+            if (k1 != r1)
+                c = k1 < r1 ? -1 : 1;
+            else {
+                c = 0;
+                for (int j = 2; j < W; ++j) {
+                    const uint64_t a = kmem[j], b = kw[(size_t)j * T + mid];
+                    if (a != b) {
+                        c = a < b ? -1 : 1;
+                        break;
+                    }
+                }
+            }
+        }
+        // lower bound: row < key -> go right;  upper bound: row <= key -> right
+        if (UPPER ? c >= 0 : c > 0)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// Any lsn > snap in rows [p, q) of the tile (LDS), with 64-row block maxima.
+__device__ __forceinline__ bool lds_any_after(const uint64_t *lsn, const uint64_t *bmax, uint32_t p,
+                                              uint32_t q, uint64_t snap)
+{
+    const uint32_t bp = p >> 6, bq = (q - 1) >> 6;
+    if (bp == bq || q - p <= 96) {
+        for (uint32_t i = p; i < q; ++i)
+            if (lsn[i] > snap) return true;
+        return false;
+    }
+    for (uint32_t i = p; i < (bp + 1) << 6; ++i)
+        if (lsn[i] > snap) return true;
+    for (uint32_t b = bp + 1; b < bq; ++b)
+        if (bmax[b] > snap) return true;
+    for (uint32_t i = bq << 6; i < q; ++i)
+        if (lsn[i] > snap) return true;
+    return false;
+}
+
+__global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, const uint64_t *recs,
+                                                       const uint32_t *bucket_off,
+                                                       const uint32_t *item_off,
+                                                       uint8_t *verdict)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const uint32_t item = blockIdx.x;
+    if (item >= item_off[w.ntiles]) return;
+    // tile = last t with item_off[t] <= item
+    uint32_t lo = 0, hi = w.ntiles;
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (item_off[mid] <= item)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    const uint32_t tile = lo;
+    const uint32_t rb = bucket_off[tile] + (item - item_off[tile]) * kJoinChunk;
+    const uint32_t re = min(rb + (uint32_t)kJoinChunk, bucket_off[tile + 1]);
+    const int W = w.W;
+    const uint32_t T = 1u << w.log2T;
+    const uint32_t ts = tile << w.log2T;
+    const uint32_t tn = min(T, w.n - ts);
+
+    uint64_t *kw = (uint64_t *)smem;               // [W][T]
+    uint64_t *lsn = kw + (size_t)W * T;            // [T]
+    uint64_t *bmax = lsn + T;                      // [T / 64]
+    // stage the tile: 16-byte loads (rows start 2-aligned: ts and T even)
+    for (int j = 0; j < W; ++j) {
+        const uint64_t *src = w.words + (size_t)j * w.stride + ts;
+        for (uint32_t i = 2 * threadIdx.x; i < tn; i += 2 * kJoinThreads) {
+            if (i + 1 < tn) {
+                const ulonglong2 v = *(const ulonglong2 *)(src + i);
+                kw[(size_t)j * T + i] = v.x;
+                kw[(size_t)j * T + i + 1] = v.y;
+            } else {
+                kw[(size_t)j * T + i] = src[i];
+            }
+        }
+    }
+    for (uint32_t i = 2 * threadIdx.x; i < tn; i += 2 * kJoinThreads) {
+        if (i + 1 < tn) {
+            const ulonglong2 v = *(const ulonglong2 *)(w.lsn + ts + i);
+            lsn[i] = v.x;
+            lsn[i + 1] = v.y;
+        } else {
+            lsn[i] = w.lsn[ts + i];
+        }
+    }
+    __syncthreads();
+    const int wid = threadIdx.x >> 6, lane = lane_id();
+    for (uint32_t b = wid; b < (tn + 63) / 64; b += kJoinThreads / 64) {
+        const uint32_t i = b * 64 + lane;
+        uint64_t v = i < tn ? lsn[i] : 0;
+        v = wave_max_u64(v);
+        if (lane == 0) bmax[b] = v;
+    }
+    __syncthreads();
+
+    const int rw = rec_words(W);
+    for (uint32_t r = rb + threadIdx.x; r < re; r += kJoinThreads) {
+        const uint64_t *rec = recs + (size_t)r * rw;
+        const uint64_t meta = rec[2 * W + 1];
+        const uint64_t snap = rec[2 * W];
+        const uint32_t txn = (uint32_t)meta;
+        const uint32_t gk = (uint32_t)(meta >> 32);
+        const uint32_t g = gk & 0x3FFFFFFFu, kind = gk >> 30;
+        const uint32_t gs = w.gstart[g], ge = w.gend[g];
+        const uint32_t lb = gs > ts ? min(gs - ts, tn) : 0;
+        const uint32_t ub = ge > ts ? min(ge - ts, tn) : 0;
+        if (lb >= ub) continue;
+        uint32_t pp = lb, qq = ub;
+        if (kind != kRecTail)
+            pp = lds_bound<false>(W, kw, T, lb, ub, rec[0], W > 1 ? rec[1] : 0, rec);
+        if (kind != kRecHead)
+            qq = lds_bound<true>(W, kw, T, pp, ub, rec[W], W > 1 ? rec[W + 1] : 0, rec + W);
+        if (pp < qq && lds_any_after(lsn, bmax, pp, qq, snap)) verdict[txn] = 1;
+    }
+}
+
+hipError_t launch_join(const WinView &w, const uint64_t *recs, const uint32_t *bucket_off,
+                       const uint32_t *item_off, uint32_t max_items, uint8_t *verdict,
+                       hipStream_t s)
+{
+    if (max_items == 0 || w.n == 0) return hipSuccess;
+    const size_t T = (size_t)1 << w.log2T;
+    const size_t lds = T * 8 * (size_t)w.W + T * 8 + (T / 64) * 8;
+    k_join<<<max_items, kJoinThreads, lds, s>>>(w, recs, bucket_off, item_off, verdict);
+    return hipGetLastError();
+}
+
+// ---- pack: verdict bytes -> bitmap ----------------------------------------
+__global__ void k_pack(const uint8_t *verdict, uint32_t n, uint64_t *bitmap)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool v = t < n && verdict[t] != 0;
+    const uint64_t m = __ballot(v);
+    if (lane_id() == 0 && t < n) bitmap[t >> 6] = m;
+}
+
+hipError_t launch_pack(const uint8_t *verdict, uint32_t n_txn, uint64_t *bitmap, hipStream_t s)
+{
+    if (n_txn == 0 || bitmap == nullptr) return hipSuccess;
+    k_pack<<<(n_txn + 255) / 256, 256, 0, s>>>(verdict, n_txn, bitmap);
+    return hipGetLastError();
+}
+
+}  // namespace hsc

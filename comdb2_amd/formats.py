@@ -1,0 +1,312 @@
+"""Host-side data formats shared by the validator bindings, tests and bench.
+
+* :class:`LLog` -- a decoded log stream in struct-of-arrays form, one row per
+  log record in LSN order: the view ``bdb/serializable.c`` gets from
+  ``DB_LOGC->get`` plus the generated ``llog_*_read`` decoders
+  (``bdb/llog.src:26-225``, txn regop records ``berkdb/dbinc_auto/txn_auto.h``).
+* :class:`ReadSets` -- many ``CurRangeArr`` read sets (``db/comdb2.h:1105-1124``)
+  flattened to struct-of-arrays, ranges in array order per read set (the
+  ``OSQL_SERIAL`` payload of ``db/osqlcomm.c:909-993`` after decode).
+* key encoding of the on-disk index format (``db/types.c:766-771``): every
+  field is a header byte (0x08 = data present, ``db/types.h:200-236``) followed
+  by the big-endian value with the sign bit flipped, so that ``memcmp`` order is
+  numeric order; descending fields are byte-inverted (``db/tag.c:2523-2526``).
+
+LSNs are ``(file << 32) | offset`` as uint64 (``DB_LSN`` order is
+lexicographic on (file, offset)).
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+# berkdb txn record types (berkdb/dbinc_auto/txn_auto.h:6,59,76)
+REC_TXN_REGOP = 10
+REC_TXN_REGOP_ROWLOCKS = 15
+REC_TXN_REGOP_GEN = 16
+# comdb2 logical log records (bdb/llog.src)
+REC_UNDO_ADD_DTA = 10003
+REC_UNDO_ADD_IX = 10004
+REC_LTRAN_COMMIT = 10005
+REC_LTRAN_START = 10006
+REC_LTRAN_COMPREC = 10007
+REC_UNDO_DEL_DTA = 10008
+REC_UNDO_DEL_IX = 10009
+REC_UNDO_UPD_DTA = 10010
+REC_UNDO_UPD_IX = 10011
+REC_UNDO_ADD_DTA_LK = 10013
+REC_UNDO_ADD_IX_LK = 10014
+REC_UNDO_DEL_DTA_LK = 10015
+REC_UNDO_DEL_IX_LK = 10016
+REC_UNDO_UPD_DTA_LK = 10017
+REC_UNDO_UPD_IX_LK = 10018
+
+DTA_TYPES = (REC_UNDO_ADD_DTA, REC_UNDO_DEL_DTA, REC_UNDO_UPD_DTA,
+             REC_UNDO_ADD_DTA_LK, REC_UNDO_DEL_DTA_LK, REC_UNDO_UPD_DTA_LK)
+IX_TYPES = (REC_UNDO_ADD_IX, REC_UNDO_DEL_IX, REC_UNDO_DEL_IX_LK,
+            REC_UNDO_UPD_IX, REC_UNDO_ADD_IX_LK, REC_UNDO_UPD_IX_LK)
+REGOP_TYPES = (REC_TXN_REGOP, REC_TXN_REGOP_GEN, REC_TXN_REGOP_ROWLOCKS)
+
+
+def lsn(file: int, offset: int) -> int:
+    return (int(file) << 32) | int(offset)
+
+
+def lsn_split(v: int) -> Tuple[int, int]:
+    return int(v) >> 32, int(v) & 0xFFFFFFFF
+
+
+# ---------------------------------------------------------------------------
+# on-disk key encoding
+# ---------------------------------------------------------------------------
+def enc_int64(v: int, descending: bool = False) -> bytes:
+    """One int64 field: 0x08 header + big-endian(v ^ 2^63) (db/types.c:766)."""
+    b = bytes([0x08]) + ((int(v) ^ (1 << 63)) & ((1 << 64) - 1)).to_bytes(8, "big")
+    return invert(b) if descending else b
+
+
+def enc_cstring(s: str, size: int, descending: bool = False) -> bytes:
+    """cstring[size] field: header + bytes NUL padded to size."""
+    raw = s.encode()[: size - 1]
+    b = bytes([0x08]) + raw + b"\x00" * (size - len(raw))
+    return invert(b) if descending else b
+
+
+def enc_genid(g: int) -> bytes:
+    """genid suffix of a dup index key (8 bytes, big-endian)."""
+    return int(g).to_bytes(8, "big")
+
+
+def invert(b: bytes) -> bytes:
+    return bytes((~x) & 0xFF for x in b)
+
+
+def enc_int64_array(vals: np.ndarray) -> np.ndarray:
+    """Vectorised enc_int64: int64[n] -> uint8[n, 9]."""
+    v = np.asarray(vals, dtype=np.int64).view(np.uint64) ^ np.uint64(1 << 63)
+    out = np.empty((len(v), 9), dtype=np.uint8)
+    out[:, 0] = 0x08
+    out[:, 1:] = v.astype(">u8").view(np.uint8).reshape(-1, 8)
+    return out
+
+
+# ---------------------------------------------------------------------------
+# log stream
+# ---------------------------------------------------------------------------
+@dataclasses.dataclass
+class LLog:
+    lsn: np.ndarray        # uint64[nrec]
+    rectype: np.ndarray    # uint32[nrec]
+    prev: np.ndarray       # uint64[nrec]
+    isabort: np.ndarray    # int16[nrec]
+    table: np.ndarray      # int32[nrec]
+    ix: np.ndarray         # int16[nrec]
+    key_off: np.ndarray    # uint64[nrec]
+    keylen: np.ndarray     # int32[nrec]
+    keys: np.ndarray       # uint8[...]
+    tbnames: List[str]
+    end_lsn: int
+
+    @property
+    def nrec(self) -> int:
+        return int(len(self.lsn))
+
+    def validate(self) -> None:
+        n = self.nrec
+        for name in ("rectype", "prev", "isabort", "table", "ix", "key_off", "keylen"):
+            assert len(getattr(self, name)) == n, name
+        assert np.all(self.lsn[1:] > self.lsn[:-1]), "LSNs must increase"
+        assert n == 0 or int(self.end_lsn) > int(self.lsn[-1])
+
+
+class LogBuilder:
+    """Appends log records with LSNs, tracking each txn's logical chain
+    (prevllsn = the txn's last logical LSN, bdb/ll.c:749, bdb/tran.c:1545-1560).
+    Txns may be interleaved by interleaving the calls."""
+
+    def __init__(self, tbnames: Sequence[str] = (), file: int = 1, offset0: int = 28,
+                 step: int = 64):
+        self.tbnames: List[str] = list(tbnames)
+        self._tid = {n: i for i, n in enumerate(self.tbnames)}
+        self.file, self.off, self.step = file, offset0, step
+        self.rows: list = []
+        self.keys = bytearray()
+        self._last: dict = {}
+
+    def table(self, name: str) -> int:
+        if name not in self._tid:
+            self._tid[name] = len(self.tbnames)
+            self.tbnames.append(name)
+        return self._tid[name]
+
+    def next_lsn(self) -> int:
+        return lsn(self.file, self.off)
+
+    def _put(self, rectype, prev=0, isabort=0, table=-1, ix=0, key: Optional[bytes] = None) -> int:
+        l = lsn(self.file, self.off)
+        self.off += self.step
+        if self.off >= (1 << 32) - self.step:
+            self.file += 1
+            self.off = 28
+        koff = len(self.keys)
+        klen = 0
+        if key is not None:
+            self.keys += key
+            klen = len(key)
+        self.rows.append((l, rectype, prev, isabort, table, ix, koff, klen))
+        return l
+
+    def begin(self, txn) -> int:
+        l = self._put(REC_LTRAN_START)
+        self._last[txn] = l
+        return l
+
+    def write(self, txn, rectype: int, table: str, ix: int = -2, key: Optional[bytes] = None) -> int:
+        t = self.table(table)
+        if rectype in DTA_TYPES:
+            key, ix = None, 0
+        l = self._put(rectype, prev=self._last[txn], table=t, ix=ix, key=key)
+        self._last[txn] = l
+        return l
+
+    def comprec(self, txn) -> int:
+        l = self._put(REC_LTRAN_COMPREC, prev=self._last[txn])
+        self._last[txn] = l
+        return l
+
+    def commit(self, txn, isabort: int = 0, regop: int = REC_TXN_REGOP,
+               empty: bool = False) -> int:
+        """ltran_commit + regop; returns the regop (commit) LSN.  empty=True
+        logs a read-only logical txn (prevllsn.file == 0)."""
+        prevllsn = 0 if empty else self._last.get(txn, 0)
+        c = self._put(REC_LTRAN_COMMIT, prev=prevllsn, isabort=isabort)
+        r = self._put(regop, prev=c)
+        self._last.pop(txn, None)
+        return r
+
+    def raw(self, rectype: int, prev: int = 0, isabort: int = 0, table: int = -1,
+            ix: int = 0, key: Optional[bytes] = None) -> int:
+        return self._put(rectype, prev, isabort, table, ix, key)
+
+    def build(self) -> LLog:
+        r = self.rows
+        cols = list(zip(*r)) if r else [()] * 8
+        lg = LLog(
+            lsn=np.array(cols[0], dtype=np.uint64),
+            rectype=np.array(cols[1], dtype=np.uint32),
+            prev=np.array(cols[2], dtype=np.uint64),
+            isabort=np.array(cols[3], dtype=np.int16),
+            table=np.array(cols[4], dtype=np.int32),
+            ix=np.array(cols[5], dtype=np.int16),
+            key_off=np.array(cols[6], dtype=np.uint64),
+            keylen=np.array(cols[7], dtype=np.int32),
+            keys=np.frombuffer(bytes(self.keys) or b"\x00", dtype=np.uint8).copy(),
+            tbnames=list(self.tbnames),
+            end_lsn=self.next_lsn(),
+        )
+        return lg
+
+
+# ---------------------------------------------------------------------------
+# read sets
+# ---------------------------------------------------------------------------
+@dataclasses.dataclass
+class Range:
+    """One CurRange (db/comdb2.h:1105-1115)."""
+    tbname: str
+    idxnum: int = -2
+    lkey: Optional[bytes] = None
+    rkey: Optional[bytes] = None
+    lflag: int = 0
+    rflag: int = 0
+    islocked: int = 0
+
+    @staticmethod
+    def point(tb: str, ix: int, key: bytes) -> "Range":
+        return Range(tb, ix, key, key)
+
+    @staticmethod
+    def locked(tb: str) -> "Range":
+        return Range(tb, -2, None, None, 1, 1, 1)
+
+
+@dataclasses.dataclass
+class ReadSets:
+    txn_off: np.ndarray    # int64[ntxn+1]
+    snap: np.ndarray       # uint64[ntxn]
+    table: np.ndarray      # int32[nr]
+    idxnum: np.ndarray     # int32[nr]
+    lflag: np.ndarray
+    rflag: np.ndarray
+    islocked: np.ndarray
+    lkeylen: np.ndarray
+    rkeylen: np.ndarray
+    lkey_off: np.ndarray   # uint64[nr]
+    rkey_off: np.ndarray
+    keys: np.ndarray       # uint8
+    tbnames: List[str]
+
+    @property
+    def ntxn(self) -> int:
+        return int(len(self.snap))
+
+    @property
+    def nranges(self) -> int:
+        return int(self.txn_off[-1])
+
+    @staticmethod
+    def from_lists(sets: Sequence[Sequence[Range]], snaps: Sequence[int],
+                   tbnames: Optional[Sequence[str]] = None) -> "ReadSets":
+        names = list(tbnames or [])
+        tid = {n: i for i, n in enumerate(names)}
+        off = [0]
+        cols = {k: [] for k in ("table", "idxnum", "lflag", "rflag", "islocked",
+                                "lkeylen", "rkeylen", "lkey_off", "rkey_off")}
+        keys = bytearray()
+        for rs in sets:
+            for r in rs:
+                if r.tbname not in tid:
+                    tid[r.tbname] = len(names)
+                    names.append(r.tbname)
+                cols["table"].append(tid[r.tbname])
+                cols["idxnum"].append(r.idxnum)
+                cols["lflag"].append(r.lflag)
+                cols["rflag"].append(r.rflag)
+                cols["islocked"].append(r.islocked)
+                for side, k in (("l", r.lkey), ("r", r.rkey)):
+                    cols[side + "key_off"].append(len(keys))
+                    cols[side + "keylen"].append(0 if k is None else len(k))
+                    if k is not None:
+                        keys += k
+            off.append(off[-1] + len(rs))
+        i32 = lambda x: np.array(x, dtype=np.int32)
+        return ReadSets(
+            txn_off=np.array(off, dtype=np.int64),
+            snap=np.array(snaps, dtype=np.uint64),
+            table=i32(cols["table"]), idxnum=i32(cols["idxnum"]),
+            lflag=i32(cols["lflag"]), rflag=i32(cols["rflag"]),
+            islocked=i32(cols["islocked"]),
+            lkeylen=i32(cols["lkeylen"]), rkeylen=i32(cols["rkeylen"]),
+            lkey_off=np.array(cols["lkey_off"], dtype=np.uint64),
+            rkey_off=np.array(cols["rkey_off"], dtype=np.uint64),
+            keys=np.frombuffer(bytes(keys) or b"\x00", dtype=np.uint8).copy(),
+            tbnames=names,
+        )
+
+    def subset(self, idx: Iterable[int]) -> "ReadSets":
+        """Read sets idx (in that order), sharing the key blob."""
+        idx = np.asarray(list(idx), dtype=np.int64)
+        lens = self.txn_off[idx + 1] - self.txn_off[idx]
+        off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        rows = np.concatenate([np.arange(self.txn_off[t], self.txn_off[t + 1]) for t in idx]) \
+            if len(idx) else np.zeros(0, dtype=np.int64)
+        pick = lambda a: a[rows]
+        return ReadSets(off, self.snap[idx].copy(), pick(self.table), pick(self.idxnum),
+                        pick(self.lflag), pick(self.rflag), pick(self.islocked),
+                        pick(self.lkeylen), pick(self.rkeylen), pick(self.lkey_off),
+                        pick(self.rkey_off), self.keys, list(self.tbnames))
+
+    def with_snaps(self, snaps) -> "ReadSets":
+        return dataclasses.replace(self, snap=np.asarray(snaps, dtype=np.uint64).copy())

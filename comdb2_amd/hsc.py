@@ -1,0 +1,366 @@
+"""ctypes bindings of ``libhsc.so`` (the C ABI in ``include/hip_serial.h``).
+
+The shared library is built in-tree (``comdb2_amd/lib/libhsc.so``) by
+``__graft_entry__.build()`` / ``make -C comdb2_amd/csrc``.  There is no
+fallback: if the library is missing, or no GPU is visible, the validator
+raises.  Python is only plumbing here -- marshalling and the verdicts run in
+the native library and on the GPU.
+
+Interface names follow the reference:
+  * :func:`bdb_osql_serial_check` <- ``bdb/serializable.c:571``
+  * :class:`CurRange` / :class:`CurRangeArr` <- ``db/comdb2.h:1105-1124``
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from .formats import LLog, Range, ReadSets
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libhsc.so")
+
+HSC_OK, HSC_EINVAL, HSC_EDEVICE, HSC_ENOMEM, HSC_ELOG, HSC_ESTATE = 0, -1, -2, -3, -4, -5
+
+
+class HscError(RuntimeError):
+    pass
+
+
+_p = C.c_void_p
+_u64p = C.POINTER(C.c_uint64)
+
+
+class CurRange(C.Structure):
+    """Layout mirror of CurRange (db/comdb2.h:1105-1115)."""
+    _fields_ = [("tbname", C.c_char_p), ("idxnum", C.c_int), ("lkey", _p), ("rkey", _p),
+                ("lflag", C.c_int), ("lkeylen", C.c_int), ("rflag", C.c_int),
+                ("rkeylen", C.c_int), ("islocked", C.c_int)]
+
+
+class CurRangeArr(C.Structure):
+    """Layout mirror of CurRangeArr (db/comdb2.h:1117-1124)."""
+    _fields_ = [("size", C.c_int), ("cap", C.c_int), ("file", C.c_uint), ("offset", C.c_uint),
+                ("hash", _p), ("ranges", C.POINTER(C.POINTER(CurRange)))]
+
+
+class _LLog(C.Structure):
+    _fields_ = [("nrec", C.c_size_t), ("lsn", _p), ("rectype", _p), ("prev", _p),
+                ("isabort", _p), ("table", _p), ("ix", _p), ("key_off", _p), ("keylen", _p),
+                ("keys", _p), ("tbnames", C.POINTER(C.c_char_p)), ("ntbnames", C.c_int),
+                ("end_lsn", C.c_uint64)]
+
+
+class _ReadSets(C.Structure):
+    _fields_ = [("ntxn", C.c_int), ("txn_off", _p), ("snap", _p), ("table", _p),
+                ("idxnum", _p), ("lflag", _p), ("rflag", _p), ("islocked", _p),
+                ("lkeylen", _p), ("rkeylen", _p), ("lkey_off", _p), ("rkey_off", _p),
+                ("keys", _p), ("tbnames", C.POINTER(C.c_char_p)), ("ntbnames", C.c_int)]
+
+
+class ProbeBatch(C.Structure):
+    """hsc_probe_batch: device pointers (ints) of a resident probe batch."""
+    _fields_ = [("n", C.c_size_t), ("lo", _p), ("hi", _p), ("gid", _p), ("snap", _p),
+                ("txn", _p), ("n_lock", C.c_size_t), ("lock_table", _p), ("lock_snap", _p),
+                ("lock_txn", _p), ("n_txn", C.c_size_t), ("verdict", _p), ("bitmap", _p)]
+
+
+class Timing(C.Structure):
+    _fields_ = [("locate_ms", C.c_float), ("plan_ms", C.c_float), ("scatter_ms", C.c_float),
+                ("join_ms", C.c_float), ("pack_ms", C.c_float), ("probe_total_ms", C.c_float),
+                ("ingest_ms", C.c_float), ("records", C.c_uint64), ("tiles", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Marshalled(C.Structure):
+    _fields_ = [("n", C.c_size_t), ("n_lock", C.c_size_t), ("n_txn", C.c_size_t),
+                ("words", C.c_int), ("lo", _u64p), ("hi", _u64p),
+                ("gid", C.POINTER(C.c_uint32)), ("snap", _u64p), ("txn", C.POINTER(C.c_uint32)),
+                ("lock_table", C.POINTER(C.c_uint32)), ("lock_snap", _u64p),
+                ("lock_txn", C.POINTER(C.c_uint32)), ("forced", C.POINTER(C.c_uint8))]
+
+
+# Every symbol include/hip_serial.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "hsc_ctx_create", "hsc_ctx_destroy", "hsc_set_stream", "hsc_last_error", "hsc_device_count",
+    "hsc_window_ingest_log", "hsc_window_append", "hsc_window_set_end", "hsc_window_reset",
+    "hsc_window_build", "hsc_register_group", "hsc_window_ingest_device", "hsc_window_words",
+    "hsc_window_keys", "hsc_window_end", "hsc_window_max_commit", "hsc_table_id",
+    "hip_bdb_osql_serial_check", "hip_serial_check_batch", "hsc_check_readsets",
+    "hsc_marshal_readsets", "hsc_probe_device", "hsc_pack_verdicts", "hsc_synchronize",
+    "hsc_get_timing",
+    "hsc_enable_timing",
+]
+
+_lib: Optional[C.CDLL] = None
+
+
+def load() -> C.CDLL:
+    """Load libhsc.so (raises HscError if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise HscError(f"{LIB_PATH} missing: run __graft_entry__.build() "
+                       "(make -C comdb2_amd/csrc)")
+    lib = C.CDLL(LIB_PATH)
+    ctx_pp = C.POINTER(_p)
+    sig = {
+        "hsc_ctx_create": (C.c_int, [C.c_int, ctx_pp]),
+        "hsc_ctx_destroy": (None, [_p]),
+        "hsc_set_stream": (C.c_int, [_p, _p]),
+        "hsc_last_error": (C.c_char_p, [_p]),
+        "hsc_device_count": (C.c_int, []),
+        "hsc_window_ingest_log": (C.c_int, [_p, C.POINTER(_LLog)]),
+        "hsc_window_append": (C.c_int, [_p, _p, C.c_size_t]),
+        "hsc_window_set_end": (C.c_int, [_p, C.c_uint64]),
+        "hsc_window_reset": (C.c_int, [_p]),
+        "hsc_window_build": (C.c_int, [_p]),
+        "hsc_register_group": (C.c_int, [_p, C.c_char_p, C.c_int, C.c_int]),
+        "hsc_window_ingest_device": (C.c_int, [_p, C.c_size_t, C.c_int, _p, _p, _p, C.c_uint64]),
+        "hsc_window_words": (C.c_int, [_p]),
+        "hsc_window_keys": (C.c_size_t, [_p]),
+        "hsc_window_end": (C.c_uint64, [_p]),
+        "hsc_window_max_commit": (C.c_uint64, [_p]),
+        "hsc_table_id": (C.c_int, [_p, C.c_char_p]),
+        "hip_bdb_osql_serial_check": (C.c_int, [_p, _p, C.POINTER(C.c_uint), C.POINTER(C.c_uint), C.c_int]),
+        "hip_serial_check_batch": (C.c_int, [_p, C.POINTER(_p), C.POINTER(C.c_uint),
+                                             C.POINTER(C.c_uint), C.c_int, C.c_int,
+                                             C.POINTER(C.c_int)]),
+        "hsc_check_readsets": (C.c_int, [_p, C.POINTER(_ReadSets), C.POINTER(C.c_int)]),
+        "hsc_marshal_readsets": (C.c_int, [_p, C.POINTER(_ReadSets), C.POINTER(C.POINTER(Marshalled))]),
+        "hsc_probe_device": (C.c_int, [_p, C.POINTER(ProbeBatch)]),
+        "hsc_pack_verdicts": (C.c_int, [_p, _p, C.c_size_t, _p]),
+        "hsc_synchronize": (C.c_int, [_p]),
+        "hsc_get_timing": (C.c_int, [_p, C.POINTER(Timing)]),
+        "hsc_enable_timing": (C.c_int, [_p, C.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def _names(tbnames: Sequence[str]):
+    arr = (C.c_char_p * max(1, len(tbnames)))()
+    for i, n in enumerate(tbnames):
+        arr[i] = n.encode()
+    return arr
+
+
+def llog_struct(log: LLog):
+    """(struct, keepalive) for an LLog."""
+    cols = dict(lsn=np.ascontiguousarray(log.lsn, np.uint64),
+                rectype=np.ascontiguousarray(log.rectype, np.uint32),
+                prev=np.ascontiguousarray(log.prev, np.uint64),
+                isabort=np.ascontiguousarray(log.isabort, np.int16),
+                table=np.ascontiguousarray(log.table, np.int32),
+                ix=np.ascontiguousarray(log.ix, np.int16),
+                key_off=np.ascontiguousarray(log.key_off, np.uint64),
+                keylen=np.ascontiguousarray(log.keylen, np.int32),
+                keys=np.ascontiguousarray(log.keys, np.uint8))
+    names = _names(log.tbnames)
+    s = _LLog(log.nrec, *[_ptr(cols[k]) for k in ("lsn", "rectype", "prev", "isabort", "table",
+                                                  "ix", "key_off", "keylen", "keys")],
+              names, len(log.tbnames), int(log.end_lsn))
+    return s, (cols, names)
+
+
+def readsets_struct(rs: ReadSets):
+    cols = dict(txn_off=np.ascontiguousarray(rs.txn_off, np.int64),
+                snap=np.ascontiguousarray(rs.snap, np.uint64),
+                table=np.ascontiguousarray(rs.table, np.int32),
+                idxnum=np.ascontiguousarray(rs.idxnum, np.int32),
+                lflag=np.ascontiguousarray(rs.lflag, np.int32),
+                rflag=np.ascontiguousarray(rs.rflag, np.int32),
+                islocked=np.ascontiguousarray(rs.islocked, np.int32),
+                lkeylen=np.ascontiguousarray(rs.lkeylen, np.int32),
+                rkeylen=np.ascontiguousarray(rs.rkeylen, np.int32),
+                lkey_off=np.ascontiguousarray(rs.lkey_off, np.uint64),
+                rkey_off=np.ascontiguousarray(rs.rkey_off, np.uint64),
+                keys=np.ascontiguousarray(rs.keys, np.uint8))
+    names = _names(rs.tbnames)
+    order = ("txn_off", "snap", "table", "idxnum", "lflag", "rflag", "islocked", "lkeylen",
+             "rkeylen", "lkey_off", "rkey_off", "keys")
+    s = _ReadSets(rs.ntxn, *[_ptr(cols[k]) for k in order], names, len(rs.tbnames))
+    return s, (cols, names)
+
+
+class CurRangeArrays:
+    """Heap-style CurRangeArr objects (ctypes) built from Python ranges, kept
+    alive together; what a comdb2 caller would pass to the drop-in entry."""
+
+    def __init__(self, sets: Sequence[Sequence[Range]], snaps: Sequence[int]):
+        self._keep: list = []
+        self.arrs: List[CurRangeArr] = []
+        for rs, s in zip(sets, snaps):
+            ptrs = (C.POINTER(CurRange) * max(2, len(rs)))()
+            for i, r in enumerate(rs):
+                cr = CurRange()
+                nm = C.create_string_buffer(r.tbname.encode())
+                cr.tbname = C.cast(nm, C.c_char_p)
+                cr.idxnum = r.idxnum
+                for side, k in (("l", r.lkey), ("r", r.rkey)):
+                    if k is None:
+                        setattr(cr, side + "key", None)
+                        setattr(cr, side + "keylen", 0)
+                    else:
+                        b = C.create_string_buffer(bytes(k), max(1, len(k)))
+                        self._keep.append(b)
+                        setattr(cr, side + "key", C.cast(b, _p))
+                        setattr(cr, side + "keylen", len(k))
+                cr.lflag, cr.rflag, cr.islocked = r.lflag, r.rflag, r.islocked
+                self._keep += [nm, cr]
+                ptrs[i] = C.pointer(cr)
+            a = CurRangeArr(len(rs), max(2, len(rs)), int(s) >> 32, int(s) & 0xFFFFFFFF, None,
+                            ptrs)
+            self._keep.append(ptrs)
+            self.arrs.append(a)
+
+    def pointers(self):
+        arr = (_p * max(1, len(self.arrs)))()
+        for i, a in enumerate(self.arrs):
+            arr[i] = C.cast(C.pointer(a), _p)
+        return arr
+
+
+class Validator:
+    """One GPU's validator context (hsc_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        if self.lib.hsc_device_count() <= device:
+            raise HscError(f"no HIP device {device} visible")
+        ctx = _p()
+        rc = self.lib.hsc_ctx_create(device, C.byref(ctx))
+        if rc != HSC_OK:
+            raise HscError(f"hsc_ctx_create({device}) = {rc}")
+        self.ctx = ctx
+        self._keep = None
+
+    def close(self) -> None:
+        if self.ctx:
+            self.lib.hsc_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc: int, what: str) -> None:
+        if rc != HSC_OK:
+            msg = self.lib.hsc_last_error(self.ctx)
+            raise HscError(f"{what} -> {rc}: {msg.decode() if msg else ''}")
+
+    # window
+    def ingest_log(self, log: LLog) -> None:
+        s, keep = llog_struct(log)
+        self._chk(self.lib.hsc_window_ingest_log(self.ctx, C.byref(s)), "hsc_window_ingest_log")
+
+    def register_group(self, tbname: str, idxnum: int, keylen: int) -> int:
+        g = self.lib.hsc_register_group(self.ctx, tbname.encode(), idxnum, keylen)
+        if g < 0:
+            self._chk(g, "hsc_register_group")
+        return g
+
+    def ingest_device(self, n: int, words: int, gid_ptr: int, words_ptr: int, lsn_ptr: int,
+                      end_lsn: int) -> None:
+        self._chk(self.lib.hsc_window_ingest_device(self.ctx, n, words, gid_ptr, words_ptr,
+                                                    lsn_ptr, end_lsn), "hsc_window_ingest_device")
+
+    @property
+    def words(self) -> int:
+        return self.lib.hsc_window_words(self.ctx)
+
+    @property
+    def keys(self) -> int:
+        return self.lib.hsc_window_keys(self.ctx)
+
+    @property
+    def end_lsn(self) -> int:
+        return self.lib.hsc_window_end(self.ctx)
+
+    # checks
+    def check_readsets(self, rs: ReadSets) -> np.ndarray:
+        s, keep = readsets_struct(rs)
+        out = np.zeros(max(1, rs.ntxn), dtype=np.int32)
+        rc = self.lib.hsc_check_readsets(self.ctx, C.byref(s), out.ctypes.data_as(C.POINTER(C.c_int)))
+        self._chk(rc, "hsc_check_readsets")
+        return out[: rs.ntxn]
+
+    def check_batch(self, arrs: CurRangeArrays, regop_only: int = 0) -> np.ndarray:
+        n = len(arrs.arrs)
+        out = np.zeros(max(1, n), dtype=np.int32)
+        rc = self.lib.hip_serial_check_batch(self.ctx, arrs.pointers(), None, None, regop_only, n,
+                                             out.ctypes.data_as(C.POINTER(C.c_int)))
+        self._chk(rc, "hip_serial_check_batch")
+        return out[:n]
+
+    def marshal(self, rs: ReadSets) -> dict:
+        """Marshal read sets into probe SoA (numpy copies)."""
+        s, keep = readsets_struct(rs)
+        mp = C.POINTER(Marshalled)()
+        self._chk(self.lib.hsc_marshal_readsets(self.ctx, C.byref(s), C.byref(mp)),
+                  "hsc_marshal_readsets")
+        m = mp.contents
+        W, n, nl, nt = m.words, m.n, m.n_lock, m.n_txn
+
+        def arr(p, cnt, dt):
+            if cnt == 0:
+                return np.zeros(0, dtype=dt)
+            return np.ctypeslib.as_array(p, shape=(cnt,)).astype(dt, copy=True)
+
+        return dict(words=W, n=n, n_lock=nl, n_txn=nt,
+                    lo=arr(m.lo, W * n, np.uint64).reshape(W, n) if n else np.zeros((W, 0), np.uint64),
+                    hi=arr(m.hi, W * n, np.uint64).reshape(W, n) if n else np.zeros((W, 0), np.uint64),
+                    gid=arr(m.gid, n, np.uint32), snap=arr(m.snap, n, np.uint64),
+                    txn=arr(m.txn, n, np.uint32), lock_table=arr(m.lock_table, nl, np.uint32),
+                    lock_snap=arr(m.lock_snap, nl, np.uint64), lock_txn=arr(m.lock_txn, nl, np.uint32),
+                    forced=arr(m.forced, nt, np.uint8))
+
+    def probe_device(self, batch: ProbeBatch) -> None:
+        self._chk(self.lib.hsc_probe_device(self.ctx, C.byref(batch)), "hsc_probe_device")
+
+    def pack_verdicts(self, verdict_ptr: int, n_txn: int, bitmap_ptr: int) -> None:
+        self._chk(self.lib.hsc_pack_verdicts(self.ctx, verdict_ptr, n_txn, bitmap_ptr),
+                  "hsc_pack_verdicts")
+
+    def set_stream(self, stream_handle: int) -> None:
+        self._chk(self.lib.hsc_set_stream(self.ctx, stream_handle), "hsc_set_stream")
+
+    def synchronize(self) -> None:
+        self._chk(self.lib.hsc_synchronize(self.ctx), "hsc_synchronize")
+
+    def enable_timing(self, on: bool = True) -> None:
+        self._chk(self.lib.hsc_enable_timing(self.ctx, int(on)), "hsc_enable_timing")
+
+    def timing(self) -> dict:
+        t = Timing()
+        self._chk(self.lib.hsc_get_timing(self.ctx, C.byref(t)), "hsc_get_timing")
+        return t.as_dict()
+
+
+def bdb_osql_serial_check(v: Validator, arr: Optional[CurRangeArr], regop_only: int = 0) -> int:
+    """bdb_osql_serial_check(bdb_state, ranges, &arr->file, &arr->offset, regop_only)
+    (bdb/serializable.c:571): 0 = serializable, nonzero = not (or error)."""
+    if arr is None:
+        return 0
+    f = C.c_uint(arr.file)
+    o = C.c_uint(arr.offset)
+    rc = v.lib.hip_bdb_osql_serial_check(v.ctx, C.cast(C.pointer(arr), _p), C.byref(f),
+                                         C.byref(o), regop_only)
+    arr.file, arr.offset = f.value, o.value
+    return rc

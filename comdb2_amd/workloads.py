@@ -1,0 +1,326 @@
+"""Synthetic workloads of BASELINE.json's configs (seeded, numpy-vectorised).
+
+* :func:`config2` -- 1xMI355X: N_t read sets x 10 ranges vs a log window of
+  1M commits x 10 int64 index keys on one index.
+* :func:`config1_events` -- the ``tests/tools/serial.c`` shaped commit stream
+  (20 ids x 5 accounts, read ``sum where id``, read one row, update it).
+* :func:`random_case` -- small adversarial logs + read sets exercising every
+  record type and every rule of the check (parity tests).
+* :func:`replay` -- drive a commit stream through a checker in commit order,
+  appending each passing write txn to the log (SURVEY.md §7 hard part 7a).
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import formats as F
+from .formats import LLog, LogBuilder, Range, ReadSets
+
+SEED_CONFIG1 = 0xC0FFEE01
+SEED_CONFIG2 = 0xC0FFEE02
+
+
+def lsn_of_index(idx: np.ndarray, per_file: int = 1 << 26, step: int = 64) -> np.ndarray:
+    """LSN of the idx-th record when records are `step` bytes apart and a file
+    holds `per_file` records."""
+    idx = np.asarray(idx, dtype=np.uint64)
+    f = np.uint64(1) + idx // np.uint64(per_file)
+    o = np.uint64(28) + (idx % np.uint64(per_file)) * np.uint64(step)
+    return (f << np.uint64(32)) | o
+
+
+# ---------------------------------------------------------------------------
+# config 2
+# ---------------------------------------------------------------------------
+@dataclasses.dataclass
+class Config2:
+    log: LLog
+    readsets: ReadSets
+    commit_lsn: np.ndarray      # uint64[n_commits] regop LSN of each commit
+    key_values: np.ndarray      # int64[n_commits * k] written values (log order)
+    params: dict
+
+
+def config2(seed: int = SEED_CONFIG2, n_commits: int = 1_000_000, keys_per_commit: int = 10,
+            n_txn: int = 100_000, ranges_per_txn: int = 10, value_bits: int = 40,
+            width: int = 1 << 20, snap_recent: float = 0.01, build_log: bool = True,
+            rank: int = 0, world: int = 1) -> Config2:
+    """Writes: values uniform in [0, 2^value_bits), n_commits x keys_per_commit
+    undo_upd_ix records on table "t1" index 0, one committed txn per commit.
+    Ranges (per read set, sorted by lower bound like a coalesced CurRangeArr):
+    50% point (half on a written key), 40% [v, v + width], 8% prefix ranges
+    (lower/upper endpoint = the first 6 or 7 bytes of a key), 2% open on one
+    side.  Snapshots: the regop LSN of a commit drawn uniformly from the most
+    recent `snap_recent` fraction of commits (recent snapshots keep the
+    conflict rate inside the 20-60% band SURVEY.md §8(d) asks for).
+
+    Sharded form (world > 1, weak scaling): the key space is range-partitioned,
+    rank r's window holds the keys [r, r+1) * 2^value_bits written by its own
+    n_commits commits (global commit g = c * world + r, so LSNs interleave);
+    the read sets are the global world * n_txn ones over the whole key space."""
+    K = keys_per_commit
+    R = K + 3  # ltran_start, K undo records, ltran_commit, regop
+    vals_all = [np.random.default_rng([seed, r]).integers(r << value_bits, (r + 1) << value_bits,
+                                                           size=n_commits * K, dtype=np.int64)
+                for r in range(world)]
+    vals = vals_all[rank]
+    gcommit = np.arange(n_commits, dtype=np.uint64) * np.uint64(world) + np.uint64(rank)
+    commit_lsn = lsn_of_index(gcommit * np.uint64(R) + np.uint64(R - 1))
+    end_lsn = int(lsn_of_index(np.array([world * n_commits * R]))[0])
+    log = None
+    if build_log:
+        nrec = n_commits * R
+        idx = (np.repeat(gcommit, R) * np.uint64(R) + np.tile(np.arange(R, dtype=np.uint64), n_commits))
+        lsns = lsn_of_index(idx)
+        j = np.tile(np.arange(R, dtype=np.int64), n_commits)
+        rectype = np.full(nrec, F.REC_UNDO_UPD_IX, dtype=np.uint32)
+        rectype[j == 0] = F.REC_LTRAN_START
+        rectype[j == R - 2] = F.REC_LTRAN_COMMIT
+        rectype[j == R - 1] = F.REC_TXN_REGOP
+        prev = np.zeros(nrec, dtype=np.uint64)
+        prev[1:] = lsns[:-1]
+        prev[j == 0] = 0
+        is_undo = (j >= 1) & (j <= K)
+        table = np.where(is_undo, 0, -1).astype(np.int32)
+        ix = np.zeros(nrec, dtype=np.int16)
+        keylen = np.where(is_undo, 9, 0).astype(np.int32)
+        key_off = np.zeros(nrec, dtype=np.uint64)
+        key_off[is_undo] = np.arange(n_commits * K, dtype=np.uint64) * np.uint64(9)
+        keys = F.enc_int64_array(vals).reshape(-1)
+        log = LLog(lsns, rectype, prev, np.zeros(nrec, dtype=np.int16), table, ix, key_off,
+                   keylen, keys, ["t1"], end_lsn)
+
+    # read ranges (global: identical on every rank)
+    rng = np.random.default_rng([seed, 1 << 20])
+    T = n_txn * world
+    nr = T * ranges_per_txn
+    kind = rng.choice(4, size=nr, p=[0.5, 0.4, 0.08, 0.02])
+    v = rng.integers(0, world << value_bits, size=nr, dtype=np.int64)
+    hit = rng.random(nr) < 0.5
+    allv = vals_all[0] if world == 1 else np.concatenate(vals_all)
+    v = np.where((kind == 0) & hit, allv[rng.integers(0, len(allv), size=nr)], v)
+    lo = F.enc_int64_array(v)
+    hi = F.enc_int64_array(np.where(kind == 1, v + width, v))
+    lkeylen = np.full(nr, 9, dtype=np.int32)
+    rkeylen = np.full(nr, 9, dtype=np.int32)
+    plen = rng.integers(6, 8, size=nr).astype(np.int32)
+    lkeylen[kind == 2] = plen[kind == 2]
+    rkeylen[kind == 2] = plen[kind == 2]
+    lflag = np.zeros(nr, dtype=np.int32)
+    rflag = np.zeros(nr, dtype=np.int32)
+    side = rng.random(nr) < 0.5
+    lflag[(kind == 3) & side] = 1
+    rflag[(kind == 3) & ~side] = 1
+    lkeylen[lflag == 1] = 0
+    rkeylen[rflag == 1] = 0
+    # sort each read set's ranges by lower bound (currange_cmp order: lflag first)
+    t_of = np.repeat(np.arange(T), ranges_per_txn)
+    lo_u = np.where(lflag == 1, -1, v.astype(np.int64))
+    order = np.lexsort((lo_u, t_of))
+    lo, hi = lo[order], hi[order]
+    lkeylen, rkeylen, lflag, rflag = lkeylen[order], rkeylen[order], lflag[order], rflag[order]
+    keys = np.concatenate([lo.reshape(-1), hi.reshape(-1)])
+    lkey_off = np.arange(nr, dtype=np.uint64) * np.uint64(9)
+    rkey_off = np.uint64(nr * 9) + np.arange(nr, dtype=np.uint64) * np.uint64(9)
+    ncg = world * n_commits
+    recent = max(1, int(round(ncg * snap_recent)))
+    gi = np.uint64(ncg - 1) - rng.integers(0, recent, size=T).astype(np.uint64)
+    snap = lsn_of_index(gi * np.uint64(R) + np.uint64(R - 1))
+    rs = ReadSets(txn_off=np.arange(0, nr + 1, ranges_per_txn, dtype=np.int64), snap=snap,
+                  table=np.zeros(nr, np.int32), idxnum=np.zeros(nr, np.int32), lflag=lflag,
+                  rflag=rflag, islocked=np.zeros(nr, np.int32), lkeylen=lkeylen, rkeylen=rkeylen,
+                  lkey_off=lkey_off, rkey_off=rkey_off, keys=keys, tbnames=["t1"])
+    return Config2(log, rs, commit_lsn, vals,
+                   dict(seed=seed, n_commits=n_commits, keys_per_commit=K, n_txn=n_txn,
+                        ranges_per_txn=ranges_per_txn, value_bits=value_bits, width=width,
+                        snap_recent=snap_recent, rank=rank, world=world, end_lsn=end_lsn))
+
+
+def config2_device_window(c2: Config2) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """The decoded window of config 2 as (gid u32[n], words u64[2][n], lsn u64[n])
+    in log order -- the rows hsc_window_ingest_log would stage (one group)."""
+    n = len(c2.key_values)
+    b = F.enc_int64_array(c2.key_values)
+    pad = np.zeros((n, 16), dtype=np.uint8)
+    pad[:, :9] = b
+    words = pad.view(">u8").astype(np.uint64).reshape(n, 2).T.copy()
+    lsn = np.repeat(c2.commit_lsn, c2.params["keys_per_commit"])
+    return np.zeros(n, dtype=np.uint32), words, lsn
+
+
+# ---------------------------------------------------------------------------
+# commit-stream replay
+# ---------------------------------------------------------------------------
+@dataclasses.dataclass
+class Txn:
+    name: str
+    reads: List[Range]
+    writes: List[Tuple[int, str, int, Optional[bytes]]]  # (rectype, table, ix, key)
+
+
+def replay(events: Sequence[Tuple[str, Txn]], check: Callable[[LLog, ReadSets], np.ndarray],
+           tbnames: Sequence[str] = ()) -> dict:
+    """events: ('begin', txn) / ('commit', txn) in time order.  At begin the
+    snapshot is the end-of-log LSN (bdb_get_current_lsn, bdb/tran.c:2662).  At
+    commit a write txn is checked (read-only txns never ship a read set,
+    db/sqloffload.c:280-287,357-363); if serializable its writes are logged
+    as one committed txn.  Returns {txn name: rc} for checked txns."""
+    lb = LogBuilder(tbnames)
+    snaps, rcs = {}, {}
+    for ev, t in events:
+        if ev == "begin":
+            snaps[t.name] = lb.next_lsn()
+            continue
+        if not t.writes:
+            continue
+        log = lb.build()
+        rs = ReadSets.from_lists([t.reads], [snaps[t.name]], tbnames=lb.tbnames)
+        rc = int(check(log, rs)[0])
+        rcs[t.name] = rc
+        if rc == 0:
+            lb.begin(t.name)
+            for rt, tb, ix, key in t.writes:
+                lb.write(t.name, rt, tb, ix, key)
+            lb.commit(t.name)
+    return rcs
+
+
+def config1_events(seed: int = SEED_CONFIG1, n_txn: int = 10_000, n_ids: int = 20,
+                   n_accts: int = 5, concurrency: int = 20) -> List[Tuple[str, Txn]]:
+    """tests/tools/serial.c-shaped stream: table "accounts" with unique index 0
+    = (id, acct) as two int64 fields (18-byte keys).  Each txn reads
+    sum(bal) where id=? (prefix range over the 9-byte id field), reads one
+    account row (point), and updates it (upd_dta + upd_ix).  `concurrency`
+    txns are in flight; they begin/commit in a seeded random interleaving."""
+    rng = np.random.default_rng(seed)
+    tb = "accounts"
+    txns = []
+    for i in range(n_txn):
+        idv = int(rng.integers(0, n_ids))
+        acct = int(rng.integers(0, n_accts))
+        pre = F.enc_int64(idv)
+        key = pre + F.enc_int64(acct)
+        reads = [Range(tb, 0, pre, pre), Range(tb, 0, key, key)]
+        writes = [(F.REC_UNDO_UPD_DTA, tb, -2, None), (F.REC_UNDO_UPD_IX, tb, 0, key)]
+        txns.append(Txn(f"T{i}", reads, writes))
+    events, live, nxt = [], [], 0
+    while nxt < n_txn or live:
+        if nxt < n_txn and (len(live) < concurrency and (not live or rng.random() < 0.5)):
+            events.append(("begin", txns[nxt]))
+            live.append(txns[nxt])
+            nxt += 1
+        else:
+            k = int(rng.integers(0, len(live)))
+            events.append(("commit", live.pop(k)))
+    return events
+
+
+# ---------------------------------------------------------------------------
+# random adversarial cases
+# ---------------------------------------------------------------------------
+def random_case(seed: int, n_commits: int = 60, n_txn: int = 40, tables=("ta", "tb", "tc"),
+                n_ix: int = 3, keylens=(9, 18, 5), max_ranges: int = 8, value_range: int = 64,
+                broken: bool = False) -> Tuple[LLog, ReadSets]:
+    """Small log + read sets covering: all undo record types (dta and ix, _lk
+    variants), comprec, aborted txns, read-only logical txns, regops whose
+    prev is not an ltran_commit, interleaved txns, table locks (first-range
+    rule), unsorted read sets (span quirk), prefix / over-long / open bounds,
+    empty read sets, groups with several key lengths, snapshots at every kind
+    of record and at/after the end of the log, and (broken=True) broken
+    chains and dangling regops."""
+    rng = np.random.default_rng(seed)
+    lb = LogBuilder(list(tables) + ["never_written"])
+
+    def key_for(ix):
+        kl = keylens[ix % len(keylens)]
+        v = int(rng.integers(0, value_range))
+        k = F.enc_int64(v)
+        if kl <= 9:
+            return k[:kl]
+        return (k + F.enc_int64(int(rng.integers(0, 4))) + bytes(64))[:kl]
+
+    ix_types = F.IX_TYPES
+    dta_types = F.DTA_TYPES
+    live = []
+    snaps_pool = [lb.next_lsn()]
+    c = 0
+    while c < n_commits:
+        if live and (len(live) > 3 or rng.random() < 0.35):
+            t = live.pop(int(rng.integers(0, len(live))))
+            r = rng.random()
+            regop = [F.REC_TXN_REGOP, F.REC_TXN_REGOP_GEN, F.REC_TXN_REGOP_ROWLOCKS][int(rng.integers(0, 3))]
+            if r < 0.1:
+                lb.commit(t, isabort=1, regop=regop)
+            else:
+                lb.commit(t, regop=regop)
+            c += 1
+        elif rng.random() < 0.06:
+            # read-only logical txn: commit with prevllsn.file == 0
+            lb.commit(("ro", c), empty=True)
+            c += 1
+        elif rng.random() < 0.05:
+            # a regop whose prev record is not an ltran_commit
+            s = lb.begin(("x", c))
+            lb.raw(F.REC_TXN_REGOP, prev=s)
+        else:
+            t = ("t", c, int(rng.integers(0, 1 << 30)))
+            lb.begin(t)
+            live.append(t)
+            for _ in range(int(rng.integers(1, 5))):
+                tb = tables[int(rng.integers(0, len(tables)))]
+                if rng.random() < 0.25:
+                    lb.write(t, dta_types[int(rng.integers(0, len(dta_types)))], tb)
+                else:
+                    ix = int(rng.integers(0, n_ix))
+                    lb.write(t, ix_types[int(rng.integers(0, len(ix_types)))], tb, ix, key_for(ix))
+                if rng.random() < 0.1:
+                    lb.comprec(t)
+        snaps_pool.append(lb.rows[-1][0] if lb.rows else lb.next_lsn())
+    for t in live:
+        lb.commit(t)
+    if broken:
+        # dangling regop (prev points nowhere) and a committed txn whose chain breaks
+        lb.raw(F.REC_TXN_REGOP, prev=(1 << 32) | 7)
+        t = ("broken",)
+        lb.begin(t)
+        lb.write(t, F.REC_UNDO_UPD_IX, tables[0], 0, key_for(0))
+        lb._last[t] = (1 << 32) | 13  # chain head points at a non-record
+        lb.commit(t)
+    log = lb.build()
+    all_lsn = [int(x) for x in log.lsn] + [int(log.end_lsn), int(log.end_lsn) + 64]
+
+    sets, snaps = [], []
+    for i in range(n_txn):
+        rs = []
+        nr = int(rng.integers(0, max_ranges + 1))
+        for _ in range(nr):
+            tb = (list(tables) + ["never_written", "unknown_tb"])[int(rng.integers(0, len(tables) + 2))]
+            u = rng.random()
+            if u < 0.08:
+                rs.append(Range(tb, int(rng.choice([-1, -2, 0])), None, None, 1, 1, 1))
+                continue
+            ix = int(rng.integers(-1, n_ix + 1))
+            kl = keylens[ix % len(keylens)] if ix >= 0 else 9
+
+            def bound():
+                k = key_for(max(ix, 0))
+                m = int(rng.integers(0, len(k) + 6))
+                return (k + bytes(rng.integers(0, 256, size=6).astype(np.uint8)))[:m]
+
+            lk, rk = bound(), bound()
+            if rng.random() < 0.5 and lk > rk:
+                lk, rk = rk, lk
+            lf = int(rng.random() < 0.1)
+            rf = int(rng.random() < 0.1)
+            rs.append(Range(tb, ix, None if lf and rng.random() < 0.5 else lk,
+                            None if rf and rng.random() < 0.5 else rk, lf, rf,
+                            int(rng.random() < 0.05)))
+        if rng.random() < 0.5:
+            rs.sort(key=lambda r: (r.tbname, -r.islocked, r.idxnum, r.lkey or b""))
+        sets.append(rs)
+        pool = all_lsn if rng.random() < 0.9 else [int(x) + 1 for x in log.lsn[:5]] or all_lsn
+        snaps.append(pool[int(rng.integers(0, len(pool)))])
+    return log, ReadSets.from_lists(sets, snaps, tbnames=lb.tbnames)

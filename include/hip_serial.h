@@ -1,0 +1,257 @@
+/*
+ * hip_serial.h -- C ABI of the MI355X serializable-isolation conflict validator.
+ *
+ * This library replaces the read-set check of comdb2's SERIALIZABLE isolation:
+ *
+ *   reference entry   int bdb_osql_serial_check(bdb_state_type *, void *ranges,
+ *                         unsigned int *file, unsigned int *offset, int regop_only);
+ *                     bdb/bdb_api.h:1824-1826, bdb/serializable.c:571-579
+ *   reference plugin  SERIALCHECK serial_check_callback(char *tbname, int idxnum,
+ *                         void *key, int keylen, void *ranges)
+ *                     bdb/bdb_api.h:336-337, db/glue.c:2926-2963
+ *   reference walk    osql_serial_check / serial_check_this_txn
+ *                     bdb/serializable.c:341-569, 60-332
+ *
+ * Instead of re-walking the log once per transaction and scanning every read
+ * range per logged write key, the library keeps the committed-write window
+ * resident in HBM (sorted by (group, key), deduplicated to the max commit LSN
+ * per key) and answers a whole batch of read sets with one range-overlap join
+ * written as hand-written HIP kernels for gfx950.
+ *
+ * Every entry point is plain C: pointers and sizes, no torch or HIP types.
+ * Return codes: 0 = success, negative = HSC_E* error.  For the check entry
+ * points, rc_out[i] keeps the reference meaning: 0 = serializable, nonzero =
+ * not serializable (callers never distinguish errors from conflicts,
+ * db/toblock.c:4779-4805); on any device error every rc_out[i] is set to 1
+ * (fail closed, as bdb/serializable.c:94-104,417-421 do for log errors).
+ */
+#ifndef HIP_SERIAL_H
+#define HIP_SERIAL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------------
+ * Read-set types.  Layout-identical mirrors of db/comdb2.h:1105-1124 so that a
+ * comdb2 caller passes its own CurRangeArr* straight through (the `hash`
+ * member built by currangearr_build_hash, db/sqlglue.c:312-351, is not read:
+ * the library recomputes the same first-table / [begin,end] spans itself).
+ * ------------------------------------------------------------------------ */
+typedef struct hsc_currange {
+    char *tbname;   /* NUL-terminated table name                              */
+    int idxnum;     /* index number; -1 table scan; -2 default (currange_new) */
+    void *lkey;     /* lower bound bytes (NULL or lkeylen bytes)              */
+    void *rkey;     /* upper bound bytes                                      */
+    int lflag;      /* 1: lower bound open (unbounded)                        */
+    int lkeylen;
+    int rflag;      /* 1: upper bound open                                    */
+    int rkeylen;
+    int islocked;   /* whole table read (full scan / both ends hit)           */
+} hsc_currange;
+
+typedef struct hsc_currangearr {
+    int size;
+    int cap;
+    unsigned int file;   /* snapshot LSN (bdb_get_current_lsn at begin)       */
+    unsigned int offset;
+    void *hash;          /* ignored                                           */
+    hsc_currange **ranges;
+} hsc_currangearr;
+
+/* ---------------------------------------------------------------------------
+ * Log record stream, decoded to struct-of-arrays.  One row per log record, in
+ * LSN order -- the view bdb/serializable.c gets from DB_LOGC->get plus the
+ * generated llog_*_read decoders (bdb/llog.src:26-225).  Keys of undo_add_ix /
+ * undo_del_ix[_lk] are the ones bdb_reconstruct_add/delete would recover
+ * (bdb/rowlocks.c:428-617).
+ * ------------------------------------------------------------------------ */
+enum {
+    HSC_REC_TXN_REGOP = 10,          /* berkdb/dbinc_auto/txn_auto.h:6        */
+    HSC_REC_TXN_REGOP_ROWLOCKS = 15, /* txn_auto.h:59                         */
+    HSC_REC_TXN_REGOP_GEN = 16,      /* txn_auto.h:76                         */
+    HSC_REC_UNDO_ADD_DTA = 10003,    /* bdb/llog.src:26                       */
+    HSC_REC_UNDO_ADD_IX = 10004,
+    HSC_REC_LTRAN_COMMIT = 10005,
+    HSC_REC_LTRAN_START = 10006,
+    HSC_REC_LTRAN_COMPREC = 10007,
+    HSC_REC_UNDO_DEL_DTA = 10008,
+    HSC_REC_UNDO_DEL_IX = 10009,
+    HSC_REC_UNDO_UPD_DTA = 10010,
+    HSC_REC_UNDO_UPD_IX = 10011,
+    HSC_REC_UNDO_ADD_DTA_LK = 10013,
+    HSC_REC_UNDO_ADD_IX_LK = 10014,
+    HSC_REC_UNDO_DEL_DTA_LK = 10015,
+    HSC_REC_UNDO_DEL_IX_LK = 10016,
+    HSC_REC_UNDO_UPD_DTA_LK = 10017,
+    HSC_REC_UNDO_UPD_IX_LK = 10018
+};
+
+typedef struct hsc_llog {
+    size_t nrec;
+    const uint64_t *lsn;      /* (file << 32) | offset, strictly increasing   */
+    const uint32_t *rectype;  /* HSC_REC_*                                    */
+    const uint64_t *prev;     /* regop*: prev_lsn; llog records: prevllsn     */
+    const int16_t *isabort;   /* ltran_commit: isabort                        */
+    const int32_t *table;     /* llog undo records: index into tbnames        */
+    const int16_t *ix;        /* undo_*_ix*: index number (short on disk)     */
+    const uint64_t *key_off;  /* undo_*_ix*: key byte offset into keys        */
+    const int32_t *keylen;    /* undo_*_ix*: key length                       */
+    const uint8_t *keys;
+    const char *const *tbnames;
+    int ntbnames;
+    uint64_t end_lsn;         /* __log_txn_lsn (berkdb/log/log_put.c:509)     */
+} hsc_llog;
+
+/* ---------------------------------------------------------------------------
+ * Flat read sets: many CurRangeArr's as struct-of-arrays (the OSQL_SERIAL
+ * payload of db/osqlcomm.c:909-993 after decode, without heap CurRange's).
+ * Ranges of read set t are rows [txn_off[t], txn_off[t+1]) in array order.
+ * ------------------------------------------------------------------------ */
+typedef struct hsc_readsets {
+    int ntxn;
+    const int64_t *txn_off;   /* [ntxn+1]                                     */
+    const uint64_t *snap;     /* [ntxn] snapshot LSN (file << 32 | offset)    */
+    const int32_t *table;     /* [nranges] index into tbnames                 */
+    const int32_t *idxnum;
+    const int32_t *lflag, *rflag, *islocked;
+    const int32_t *lkeylen, *rkeylen;
+    const uint64_t *lkey_off, *rkey_off; /* byte offsets into keys           */
+    const uint8_t *keys;
+    const char *const *tbnames;
+    int ntbnames;
+} hsc_readsets;
+
+/* Decoded committed write (what serial_check_this_txn hands the callback). */
+typedef struct hsc_write {
+    const char *tbname;
+    int idxnum;          /* -2 for dta records (key == NULL)                  */
+    const void *key;     /* NULL for dta records                              */
+    int keylen;
+    uint64_t commit_lsn; /* LSN of the txn's regop record                     */
+} hsc_write;
+
+/* Device-resident probe batch (what the check entry points lower to).  All
+ * pointers are device pointers on the context's GPU.  Key words are the key
+ * bytes in big-endian 8-byte words, zero padded, held as native uint64 so that
+ * numeric order of the words equals memcmp order of the bytes. */
+typedef struct hsc_probe_batch {
+    size_t n;                 /* range probes                                  */
+    const uint64_t *lo;       /* [words][n]                                    */
+    const uint64_t *hi;       /* [words][n]                                    */
+    const uint32_t *gid;      /* [n] key group (table, index, key length)      */
+    const uint64_t *snap;     /* [n] snapshot LSN of the owning read set       */
+    const uint32_t *txn;      /* [n] read-set (transaction) index              */
+    size_t n_lock;            /* table-lock probes                             */
+    const uint32_t *lock_table;
+    const uint64_t *lock_snap;
+    const uint32_t *lock_txn;
+    size_t n_txn;
+    uint8_t *verdict;         /* [n_txn] out: 1 = not serializable             */
+    uint64_t *bitmap;         /* [ceil(n_txn/64)] out (may be NULL)            */
+} hsc_probe_batch;
+
+/* Per-kernel device time of the last probe / window build, in ms. */
+typedef struct hsc_timing {
+    float locate_ms, plan_ms, scatter_ms, join_ms, pack_ms, probe_total_ms;
+    float ingest_ms;
+    uint64_t records;         /* join records emitted by the last probe         */
+    uint64_t tiles;           /* tiles in the resident window                   */
+} hsc_timing;
+
+typedef struct hsc_ctx hsc_ctx;
+
+enum {
+    HSC_OK = 0,
+    HSC_EINVAL = -1,
+    HSC_EDEVICE = -2,
+    HSC_ENOMEM = -3,
+    HSC_ELOG = -4,     /* malformed log stream (unknown record, broken link)  */
+    HSC_ESTATE = -5    /* window not built                                    */
+};
+
+/* ---- context ------------------------------------------------------------ */
+int hsc_ctx_create(int device, hsc_ctx **out);
+void hsc_ctx_destroy(hsc_ctx *ctx);
+/* Launch on this hipStream_t (NULL = the context's own stream). */
+int hsc_set_stream(hsc_ctx *ctx, void *hip_stream);
+const char *hsc_last_error(hsc_ctx *ctx);
+int hsc_device_count(void);
+
+/* ---- write window (replaces the per-call log walk) ---------------------- */
+/* Decode a log stream: every committed write txn (regop whose prev record is
+ * an ltran_commit with isabort == 0 and prevllsn.file != 0,
+ * bdb/serializable.c:426-534) contributes its logical records' (table, ix,
+ * key) at the regop's LSN.  Replaces the window. */
+int hsc_window_ingest_log(hsc_ctx *ctx, const hsc_llog *log);
+/* Append decoded writes (commit_lsn non-decreasing across calls). */
+int hsc_window_append(hsc_ctx *ctx, const hsc_write *w, size_t n);
+int hsc_window_set_end(hsc_ctx *ctx, uint64_t end_lsn);
+int hsc_window_reset(hsc_ctx *ctx);
+/* Sort + dedupe + summaries on the device; implied by the check calls. */
+int hsc_window_build(hsc_ctx *ctx);
+/* Register a key group ahead of a device-side ingest; returns gid >= 0. */
+int hsc_register_group(hsc_ctx *ctx, const char *tbname, int idxnum, int keylen);
+/* Device-side ingest of pre-padded keys (bench / sharded driver path):
+ * gid[n], words[words][n], lsn[n] are DEVICE pointers, keys already packed as
+ * described for hsc_probe_batch; gid values come from hsc_register_group.
+ * Replaces the window. */
+int hsc_window_ingest_device(hsc_ctx *ctx, size_t n, int words,
+                             const uint32_t *gid, const uint64_t *key_words,
+                             const uint64_t *lsn, uint64_t end_lsn);
+int hsc_window_words(hsc_ctx *ctx);          /* key words per key (>= 1)     */
+size_t hsc_window_keys(hsc_ctx *ctx);        /* distinct (group, key) rows   */
+uint64_t hsc_window_end(hsc_ctx *ctx);
+uint64_t hsc_window_max_commit(hsc_ctx *ctx);
+int hsc_table_id(hsc_ctx *ctx, const char *tbname); /* -1 if never written   */
+
+/* ---- drop-in checks ----------------------------------------------------- */
+/* Exactly bdb_osql_serial_check (bdb/serializable.c:571-579) for one read set:
+ * ranges == NULL -> 0; regop_only -> nonzero iff a committed write txn follows
+ * (*file,*offset); otherwise (*file,*offset) := end LSN, then the full check. */
+int hip_bdb_osql_serial_check(void *ctx, void *ranges, unsigned int *file,
+                              unsigned int *offset, int regop_only);
+/* n read sets in one device pass.  ranges[i] is a CurRangeArr* (may be NULL);
+ * file/offset are arrays of n in/out snapshot LSNs, or NULL to use (and
+ * update) ranges[i]->file / ->offset in place.  Per element the semantics and
+ * side effects of the single call.  Returns 0 or a negative HSC_E* code. */
+int hip_serial_check_batch(void *ctx, void *const *ranges, unsigned int *file,
+                           unsigned int *offset, int regop_only, int n,
+                           int *rc_out);
+/* Flat read sets (snapshots in rs->snap); rc_out[ntxn]; full checks only. */
+int hsc_check_readsets(hsc_ctx *ctx, const hsc_readsets *rs, int *rc_out);
+
+/* ---- marshalling + device probe (what the checks lower to) -------------- */
+typedef struct hsc_marshalled {
+    size_t n, n_lock, n_txn;
+    int words;
+    uint64_t *lo, *hi;        /* host [words][n] */
+    uint32_t *gid;
+    uint64_t *snap;
+    uint32_t *txn;
+    uint32_t *lock_table;
+    uint64_t *lock_snap;
+    uint32_t *lock_txn;
+    uint8_t *forced;          /* [n_txn] verdicts decided on the host (1/0)   */
+} hsc_marshalled;
+/* Marshal flat read sets against the current window into probe SoA (host
+ * memory owned by the library; valid until the next marshal / ctx destroy). */
+int hsc_marshal_readsets(hsc_ctx *ctx, const hsc_readsets *rs,
+                         const hsc_marshalled **out);
+/* Run the join for a device-resident batch, asynchronously on the stream. */
+int hsc_probe_device(hsc_ctx *ctx, const hsc_probe_batch *b);
+/* verdict bytes -> bitmap (e.g. after a cross-GPU max all-reduce). */
+int hsc_pack_verdicts(hsc_ctx *ctx, const uint8_t *verdict, size_t n_txn,
+                      uint64_t *bitmap);
+int hsc_synchronize(hsc_ctx *ctx);
+int hsc_get_timing(hsc_ctx *ctx, hsc_timing *t);
+/* Enable per-kernel HIP event timing of probes (adds event records). */
+int hsc_enable_timing(hsc_ctx *ctx, int on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HIP_SERIAL_H */

@@ -1,0 +1,103 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes wrapper of the CPU restatement
+(oracle/serial_oracle.c) of comdb2's serializable check.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module, and only as the checker / CPU baseline.  The product
+(comdb2_amd/) never imports it.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "build", "liboracle_serial.so")
+sys.path.insert(0, os.path.dirname(_HERE))
+
+from comdb2_amd.formats import LLog, ReadSets  # noqa: E402  (data containers only)
+
+_p = C.c_void_p
+_lib = None
+
+
+class _OrLog(C.Structure):
+    _fields_ = [("nrec", C.c_size_t), ("lsn", _p), ("rectype", _p), ("prev", _p),
+                ("isabort", _p), ("table", _p), ("ix", _p), ("key_off", _p), ("keylen", _p),
+                ("keys", _p), ("tbnames", C.POINTER(C.c_char_p)), ("ntbnames", C.c_int),
+                ("end_lsn", C.c_uint64)]
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB_PATH
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        lib = C.CDLL(LIB_PATH)
+        lib.or_serial_check_many.restype = C.c_double
+        lib.or_serial_check_many.argtypes = [C.POINTER(_OrLog), _p, C.c_int, C.c_int, C.c_int,
+                                             C.POINTER(C.c_int)]
+        lib.or_build_arrs.restype = _p
+        lib.or_build_arrs.argtypes = [C.c_int] + [_p] * 12 + [C.POINTER(C.c_char_p)]
+        lib.or_free_arrs.restype = None
+        lib.or_free_arrs.argtypes = [_p, C.c_int]
+        lib.or_serial_check.restype = C.c_int
+        lib.or_serial_check.argtypes = [C.POINTER(_OrLog), _p, C.POINTER(C.c_uint),
+                                        C.POINTER(C.c_uint), C.c_int]
+        _lib = lib
+    return _lib
+
+
+def _names(tbnames):
+    arr = (C.c_char_p * max(1, len(tbnames)))()
+    for i, n in enumerate(tbnames):
+        arr[i] = n.encode()
+    return arr
+
+
+class OracleLog:
+    """An LLog pinned for the oracle (keeps the arrays alive)."""
+
+    def __init__(self, log: LLog):
+        self.cols = [np.ascontiguousarray(a) for a in (
+            log.lsn.astype(np.uint64), log.rectype.astype(np.uint32), log.prev.astype(np.uint64),
+            log.isabort.astype(np.int16), log.table.astype(np.int32), log.ix.astype(np.int16),
+            log.key_off.astype(np.uint64), log.keylen.astype(np.int32), log.keys.astype(np.uint8))]
+        self.names = _names(log.tbnames)
+        self.s = _OrLog(log.nrec, *[c.ctypes.data for c in self.cols], self.names,
+                        len(log.tbnames), int(log.end_lsn))
+
+
+def check(log, rs: ReadSets, regop_only: int = 0, nthreads: int = 1):
+    """bdb_osql_serial_check per read set.  Returns (rc int32[ntxn],
+    post-call snapshot LSNs uint64[ntxn], wall seconds of the checks)."""
+    lib = load()
+    ol = log if isinstance(log, OracleLog) else OracleLog(log)
+    cols = [np.ascontiguousarray(a) for a in (
+        rs.txn_off.astype(np.int64), rs.snap.astype(np.uint64), rs.table.astype(np.int32),
+        rs.idxnum.astype(np.int32), rs.lflag.astype(np.int32), rs.rflag.astype(np.int32),
+        rs.islocked.astype(np.int32), rs.lkeylen.astype(np.int32), rs.rkeylen.astype(np.int32),
+        rs.lkey_off.astype(np.uint64), rs.rkey_off.astype(np.uint64), rs.keys.astype(np.uint8))]
+    names = _names(rs.tbnames)
+    arrs = lib.or_build_arrs(rs.ntxn, *[c.ctypes.data for c in cols], names)
+    try:
+        rc = np.zeros(max(1, rs.ntxn), dtype=np.int32)
+        secs = lib.or_serial_check_many(C.byref(ol.s), arrs, rs.ntxn, regop_only, nthreads,
+                                        rc.ctypes.data_as(C.POINTER(C.c_int)))
+        # read back (file, offset) written by the full checks
+        ptrs = C.cast(arrs, C.POINTER(C.POINTER(C.c_uint * 4)))
+        post = np.zeros(rs.ntxn, dtype=np.uint64)
+        for i in range(rs.ntxn):
+            hdr = ptrs[i].contents  # size, cap, file, offset
+            post[i] = (int(hdr[2]) << 32) | int(hdr[3])
+    finally:
+        lib.or_free_arrs(arrs, rs.ntxn)
+    return rc[: rs.ntxn], post, secs
