@@ -106,12 +106,12 @@ def cpu_baseline(c2, gpu_verdict, threads, target_s):
     _, _, secs = oracle.check(ol, c2.readsets.subset(cal), nthreads=threads)
     rate = len(cal) / max(secs, 1e-6)
     n = int(min(T, max(len(cal), rate * target_s)))
-    step = max(1, T // n)
-    sample = np.arange(0, T, step)[:n]
+    sample = np.unique(np.linspace(0, T - 1, n).astype(np.int64))
+    step = T / len(sample)
     rc, _, secs = oracle.check(ol, c2.readsets.subset(sample), nthreads=threads)
     ok = bool(np.array_equal(rc != 0, gpu_verdict[sample] != 0))
     return dict(value=len(sample) / secs, unit="checks/s", cores=threads, kind="port",
-                sample=f"{len(sample)} of {T} read sets (every {step}th), oracle/serial_oracle.c "
+                sample=f"{len(sample)} of {T} read sets (evenly spaced, 1 in {step:.1f}), oracle/serial_oracle.c "
                        f"restatement of bdb_osql_serial_check over the {c2.log.nrec}-record log, "
                        f"{threads} pthreads, {secs:.1f} s; cpu: {cpu_model()}",
                 parity_with_gpu=ok)

@@ -100,12 +100,12 @@ struct hsc_ctx {
     uint32_t ntiles = 0;
     int log2T = 11, levels = 0;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
-    DBuf d_gstart, d_gend, d_tmax, d_table_max, d_group_table, d_count;
+    DBuf d_gstart, d_gend, d_tmax, d_table_max, d_group_table, d_count, d_sp_g, d_sp_w;
 
     // probe workspace
     DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;
     DBuf p_verdict, p_bitmap;
-    DBuf w_code, w_counts, w_bucket, w_cursor, w_items, w_recs;
+    DBuf w_code, w_counts, w_bucket, w_cursor, w_items, w_item_tile, w_recs;
 
     // marshal output
     hsc_marshalled m{};
@@ -254,6 +254,8 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, c->d_tmax.ensure(8 * (size_t)std::max(1, c->levels) * std::max<uint32_t>(1, c->ntiles)));
     HIPCHK(c, c->d_table_max.ensure(8 * (size_t)std::max(nt, 1)));
     HIPCHK(c, c->d_group_table.ensure(4 * (size_t)std::max(ng, 1)));
+    HIPCHK(c, c->d_sp_g.ensure(4 * (size_t)std::max<uint32_t>(1, c->ntiles)));
+    HIPCHK(c, c->d_sp_w.ensure(8 * (size_t)W * std::max<uint32_t>(1, c->ntiles)));
     std::vector<uint32_t> gt(std::max(ng, 1), 0);
     for (int g = 0; g < ng; ++g) gt[g] = (uint32_t)c->groups[g].tid;
     HIPCHK(c, hipMemcpyAsync(c->d_group_table.p, gt.data(), 4 * gt.size(), hipMemcpyHostToDevice, s));
@@ -273,7 +275,8 @@ static int device_build(hsc_ctx *c, size_t n_in)
     w.levels = c->levels;
     HIPCHK(c, build_summaries(w, c->d_gstart.as<uint32_t>(), c->d_gend.as<uint32_t>(), ng,
                               c->d_tmax.as<uint64_t>(), c->d_group_table.as<uint32_t>(),
-                              c->d_table_max.as<uint64_t>(), s));
+                              c->d_table_max.as<uint64_t>(), c->d_sp_g.as<uint32_t>(),
+                              c->d_sp_w.as<uint64_t>(), s));
     HIPCHK(c, hipEventRecord(e1, s));
     HIPCHK(c, hipStreamSynchronize(s));
     float ms = 0;
@@ -628,6 +631,8 @@ static WinView win_view(hsc_ctx *c)
     w.gend = c->d_gend.as<uint32_t>();
     w.tmax = c->d_tmax.as<uint64_t>();
     w.table_max = c->d_table_max.as<uint64_t>();
+    w.sp_g = c->d_sp_g.as<uint32_t>();
+    w.sp_w = c->d_sp_w.as<uint64_t>();
     w.n = (uint32_t)c->n;
     w.ntiles = c->ntiles;
     w.ntables = (uint32_t)c->table_names.size();
@@ -661,6 +666,8 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
     HIPCHK(c, c->w_cursor.ensure(4 * ((size_t)nt + 1)));
     HIPCHK(c, c->w_items.ensure(4 * ((size_t)nt + 1)));
     HIPCHK(c, c->w_recs.ensure(8 * (size_t)rec_words(w.W) * 2 * std::max<uint32_t>(p.n, 1)));
+    const uint32_t max_items_cap = nt + (uint32_t)((2 * (size_t)p.n + kJoinChunk - 1) / kJoinChunk);
+    HIPCHK(c, c->w_item_tile.ensure(4 * (size_t)max_items_cap + 16));
     const bool tm = c->timing;
     if (tm)
         for (int i = 0; i < 6; ++i)
@@ -668,14 +675,16 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
     if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
     if (b->n_txn) HIPCHK(c, hipMemsetAsync(b->verdict, 0, b->n_txn, s));
     HIPCHK(c, hipMemsetAsync(c->w_counts.p, 0, 4 * ((size_t)nt + 1), s));
-    const int grid_l = (int)std::min<size_t>(std::max<size_t>((std::max(p.n, p.n_lock) + 255) / 256, 1), 1024);
+    const int grid_l = (int)std::min<size_t>(
+        std::max<size_t>((std::max(p.n, p.n_lock) + kLocateThreads - 1) / kLocateThreads, 1), 512);
     HIPCHK(c, launch_locate(w, p, c->w_code.as<uint64_t>(), c->w_counts.as<uint32_t>(), b->verdict,
                             grid_l, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     uint32_t max_items = 0;
     if (p.n && w.ntiles) {
         HIPCHK(c, launch_plan(c->w_counts.as<uint32_t>(), w.ntiles, c->w_bucket.as<uint32_t>(),
-                              c->w_cursor.as<uint32_t>(), c->w_items.as<uint32_t>(), s));
+                              c->w_cursor.as<uint32_t>(), c->w_items.as<uint32_t>(),
+                              c->w_item_tile.as<uint32_t>(), s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
         const int grid_s = (int)std::min<size_t>((p.n + 2047) / 2048, 1024);
         HIPCHK(c, launch_scatter(w, p, c->w_code.as<uint64_t>(), c->w_cursor.as<uint32_t>(),
@@ -683,7 +692,8 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
         if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
         max_items = w.ntiles + (uint32_t)((2 * (size_t)p.n + kJoinChunk - 1) / kJoinChunk);
         HIPCHK(c, launch_join(w, c->w_recs.as<uint64_t>(), c->w_bucket.as<uint32_t>(),
-                              c->w_items.as<uint32_t>(), max_items, b->verdict, s));
+                              c->w_items.as<uint32_t>(), c->w_item_tile.as<uint32_t>(), max_items,
+                              b->verdict, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
     } else if (tm) {
         HIPCHK(c, hipEventRecord(c->ev[2], s));
@@ -803,7 +813,8 @@ void hsc_ctx_destroy(hsc_ctx *c)
     (void)hipStreamSynchronize(c->stream);
     DBuf *bufs[] = {&c->d_gid, &c->d_words, &c->d_lsn, &c->d_gid2, &c->d_words2, &c->d_lsn2,
                     &c->d_flags, &c->d_scratch, &c->d_gstart, &c->d_gend, &c->d_tmax,
-                    &c->d_table_max, &c->d_group_table, &c->d_count, &c->p_lo, &c->p_hi,
+                    &c->d_table_max, &c->d_group_table, &c->d_count, &c->d_sp_g, &c->d_sp_w,
+                    &c->w_item_tile, &c->p_lo, &c->p_hi,
                     &c->p_gid, &c->p_snap, &c->p_txn, &c->p_lock_table, &c->p_lock_snap,
                     &c->p_lock_txn, &c->p_verdict, &c->p_bitmap, &c->w_code, &c->w_counts,
                     &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_recs};

@@ -10,6 +10,7 @@
 //   rows sorted by (gid, words[0..W-1]) and unique
 //   gstart/gend[g]      row span of group g
 //   tmax[l * ntiles + t] max lsn over tiles [t, t + 2^l)  (sparse table)
+//   sp_g[t], sp_w[j * ntiles + t]  group / key words of tile t's first row
 //   table_max[tid]      max commit LSN of any write to table tid (dta too)
 #pragma once
 #include <hip/hip_runtime.h>
@@ -19,7 +20,8 @@
 namespace hsc {
 
 constexpr int kMaxWords = 64;       // MAXKEYLEN 512 B (bbinc/cdb2_constants.h:33)
-constexpr int kTopCap = 2048;       // splitters held in LDS by the locate kernel
+constexpr int kTopCap = 4096;       // splitters held in LDS by the locate kernel
+constexpr int kLocateThreads = 512;
 constexpr int kHistCap = 8192;      // tiles whose bucket counters fit in LDS
 constexpr int kJoinThreads = 512;
 constexpr int kJoinChunk = 1024;    // join records per workgroup
@@ -38,6 +40,8 @@ struct WinView {
     const uint32_t *gstart, *gend;
     const uint64_t *tmax;
     const uint64_t *table_max;
+    const uint32_t *sp_g;     // [ntiles] group of each tile's first row
+    const uint64_t *sp_w;     // [W][ntiles] key words of each tile's first row
     uint32_t n, ntiles, ntables;
     int W, log2T, levels;
 };
@@ -81,17 +85,17 @@ hipError_t dedupe_rows(int W, size_t n, const uint32_t *gid, const uint64_t *wor
 size_t scan_scratch_bytes(size_t n);
 hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, int ngroups,
                            uint64_t *tmax, const uint32_t *group_table,
-                           uint64_t *table_max, hipStream_t s);
+                           uint64_t *table_max, uint32_t *sp_g, uint64_t *sp_w, hipStream_t s);
 // Probe.
 hipError_t launch_locate(const WinView &w, const ProbeView &p, uint64_t *code,
                          uint32_t *counts, uint8_t *verdict, int grid, hipStream_t s);
 hipError_t launch_plan(const uint32_t *counts, uint32_t ntiles, uint32_t *bucket_off,
-                       uint32_t *cursor, uint32_t *item_off, hipStream_t s);
+                       uint32_t *cursor, uint32_t *item_off, uint32_t *item_tile, hipStream_t s);
 hipError_t launch_scatter(const WinView &w, const ProbeView &p, const uint64_t *code,
                           uint32_t *cursor, uint64_t *recs, int grid, hipStream_t s);
 hipError_t launch_join(const WinView &w, const uint64_t *recs, const uint32_t *bucket_off,
-                       const uint32_t *item_off, uint32_t max_items, uint8_t *verdict,
-                       hipStream_t s);
+                       const uint32_t *item_off, const uint32_t *item_tile, uint32_t max_items,
+                       uint8_t *verdict, hipStream_t s);
 hipError_t launch_pack(const uint8_t *verdict, uint32_t n_txn, uint64_t *bitmap,
                        hipStream_t s);
 

@@ -431,9 +431,19 @@ __global__ __launch_bounds__(256) void k_group_table_max(const uint32_t *gstart,
     }
 }
 
+// Compact splitter arrays: first row of every tile.
+__global__ void k_splitters(WinView w, uint32_t *sp_g, uint64_t *sp_w)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= w.ntiles) return;
+    const size_t pos = (size_t)t << w.log2T;
+    sp_g[t] = w.gid[pos];
+    for (int j = 0; j < w.W; ++j) sp_w[(size_t)j * w.ntiles + t] = w.words[(size_t)j * w.stride + pos];
+}
+
 hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, int ngroups,
                            uint64_t *tmax, const uint32_t *group_table, uint64_t *table_max,
-                           hipStream_t s)
+                           uint32_t *sp_g, uint64_t *sp_w, hipStream_t s)
 {
     hipError_t e = hipMemsetAsync(gstart, 0, sizeof(uint32_t) * (size_t)ngroups, s);
     if (e == hipSuccess) e = hipMemsetAsync(gend, 0, sizeof(uint32_t) * (size_t)ngroups, s);
@@ -445,6 +455,7 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
         k_sparse_level<<<(w.ntiles + 255) / 256, 256, 0, s>>>(w.ntiles, l, tmax);
     if (ngroups > 0)
         k_group_table_max<<<ngroups, 256, 0, s>>>(gstart, gend, w.lsn, group_table, table_max);
+    k_splitters<<<(w.ntiles + 255) / 256, 256, 0, s>>>(w, sp_g, sp_w);
     return hipGetLastError();
 }
 
@@ -452,7 +463,8 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
 // probe
 // ============================================================================
 
-// sign((sg, splitter words) - (g, key)) for tile t's first row.
+// sign((sg, splitter words) - (g, key)) for tile t's first row; the
+// splitter's group and word 0 are given, later words come from sp_w.
 __device__ __forceinline__ int cmp_splitter(const WinView &w, uint32_t t, uint32_t sg,
                                             uint64_t sw0, uint32_t g, uint64_t k0, uint64_t k1,
                                             const uint64_t *kmem, size_t ks)
@@ -460,12 +472,12 @@ __device__ __forceinline__ int cmp_splitter(const WinView &w, uint32_t t, uint32
     if (sg != g) return sg < g ? -1 : 1;
     if (sw0 != k0) return sw0 < k0 ? -1 : 1;
     if (w.W == 1) return 0;
-    const size_t pos = (size_t)t << w.log2T;
     // words 1.. : sign(splitter - key) = -sign(key - splitter)
-    return -cmp_words(w.W - 1, k1, kmem + ks, ks, w.words + w.stride + pos, w.stride);
+    return -cmp_words(w.W - 1, k1, kmem + ks, ks, w.sp_w + w.ntiles + t, w.ntiles);
 }
 
-// Number of tiles whose first row compares < (g, key) (LEQ: <=).
+// Number of tiles whose first row compares < (g, key) (LEQ: <=).  The LDS
+// holds every stride_t-th splitter; the last step searches sp_g/sp_w.
 template <bool LEQ>
 __device__ uint32_t count_splitters(const WinView &w, const uint64_t *top_w0,
                                     const uint32_t *top_g, uint32_t ntop, uint32_t stride_t,
@@ -486,8 +498,7 @@ __device__ uint32_t count_splitters(const WinView &w, const uint64_t *top_w0,
     uint32_t H = min(lo * stride_t, w.ntiles);
     while (L < H) {
         uint32_t mid = (L + H) >> 1;
-        const size_t pos = (size_t)mid << w.log2T;
-        int c = cmp_splitter(w, mid, w.gid[pos], w.words[pos], g, k0, k1, kmem, ks);
+        int c = cmp_splitter(w, mid, w.sp_g[mid], w.sp_w[mid], g, k0, k1, kmem, ks);
         if (LEQ ? c <= 0 : c < 0)
             L = mid + 1;
         else
@@ -505,7 +516,7 @@ __device__ __forceinline__ uint64_t tiles_max(const WinView &w, uint32_t x, uint
     return a > b ? a : b;
 }
 
-__global__ __launch_bounds__(256) void k_locate(WinView w, ProbeView p, uint64_t *code,
+__global__ __launch_bounds__(kLocateThreads) void k_locate(WinView w, ProbeView p, uint64_t *code,
                                                 uint32_t *counts, uint8_t *verdict,
                                                 uint32_t ntop, uint32_t stride_t, int lds_hist)
 {
@@ -514,9 +525,8 @@ __global__ __launch_bounds__(256) void k_locate(WinView w, ProbeView p, uint64_t
     uint32_t *top_g = (uint32_t *)(top_w0 + ntop);
     uint32_t *hist = top_g + ((ntop + 3) & ~3u);
     for (uint32_t i = threadIdx.x; i < ntop; i += blockDim.x) {
-        const size_t pos = (size_t)(i * stride_t) << w.log2T;
-        top_w0[i] = w.words[pos];
-        top_g[i] = w.gid[pos];
+        top_w0[i] = w.sp_w[(size_t)i * stride_t];
+        top_g[i] = w.sp_g[(size_t)i * stride_t];
     }
     if (lds_hist)
         for (uint32_t i = threadIdx.x; i < w.ntiles; i += blockDim.x) hist[i] = 0;
@@ -581,14 +591,14 @@ hipError_t launch_locate(const WinView &w, const ProbeView &p, uint64_t *code, u
     int lds_hist = w.ntiles <= (uint32_t)kHistCap;
     size_t lds = (size_t)ntop * 8 + (((size_t)ntop + 3) & ~(size_t)3) * 4 +
                  (lds_hist ? (size_t)w.ntiles * 4 : 0);
-    k_locate<<<grid, 256, lds, s>>>(w, p, code, counts, verdict, ntop, stride_t, lds_hist);
+    k_locate<<<grid, kLocateThreads, lds, s>>>(w, p, code, counts, verdict, ntop, stride_t, lds_hist);
     return hipGetLastError();
 }
 
 // ---- plan: bucket offsets + work items (one workgroup) ---------------------
 __global__ __launch_bounds__(1024) void k_plan(const uint32_t *counts, uint32_t ntiles,
                                                uint32_t *bucket_off, uint32_t *cursor,
-                                               uint32_t *item_off)
+                                               uint32_t *item_off, uint32_t *item_tile)
 {
     __shared__ uint32_t lds[16];
     uint32_t carry_b = 0, carry_i = 0;
@@ -603,6 +613,7 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t *counts, uint32_t 
             bucket_off[t] = carry_b + pb;
             cursor[t] = carry_b + pb;
             item_off[t] = carry_i + pi;
+            for (uint32_t k = 0; k < ch; ++k) item_tile[carry_i + pi + k] = t;
         }
         carry_b += tb;
         carry_i += ti;
@@ -614,9 +625,9 @@ __global__ __launch_bounds__(1024) void k_plan(const uint32_t *counts, uint32_t 
 }
 
 hipError_t launch_plan(const uint32_t *counts, uint32_t ntiles, uint32_t *bucket_off,
-                       uint32_t *cursor, uint32_t *item_off, hipStream_t s)
+                       uint32_t *cursor, uint32_t *item_off, uint32_t *item_tile, hipStream_t s)
 {
-    k_plan<<<1, 1024, 0, s>>>(counts, ntiles, bucket_off, cursor, item_off);
+    k_plan<<<1, 1024, 0, s>>>(counts, ntiles, bucket_off, cursor, item_off, item_tile);
     return hipGetLastError();
 }
 
@@ -624,17 +635,19 @@ hipError_t launch_plan(const uint32_t *counts, uint32_t ntiles, uint32_t *bucket
 constexpr int kScatterThreads = 256;
 constexpr int kScatterRound = 8;  // probes per thread per round
 
+// One join record = rec_words(W) u64, written as 16-byte stores.
 __device__ __forceinline__ void write_record(uint64_t *recs, int rw, uint32_t slot, int W,
                                              const ProbeView &p, uint32_t q, uint32_t kind)
 {
-    uint64_t *r = recs + (size_t)slot * rw;
+    ulonglong2 *r = (ulonglong2 *)(recs + (size_t)slot * rw);
     const size_t ks = p.n;
-    for (int j = 0; j < W; ++j) {
-        r[j] = p.lo[(size_t)j * ks + q];
-        r[W + j] = p.hi[(size_t)j * ks + q];
-    }
-    r[2 * W] = p.snap[q];
-    r[2 * W + 1] = (uint64_t)p.txn[q] | ((uint64_t)(p.gid[q] | (kind << 30)) << 32);
+    auto word = [&](int k) -> uint64_t {
+        if (k < W) return p.lo[(size_t)k * ks + q];
+        if (k < 2 * W) return p.hi[(size_t)(k - W) * ks + q];
+        if (k == 2 * W) return p.snap[q];
+        return (uint64_t)p.txn[q] | ((uint64_t)(p.gid[q] | (kind << 30)) << 32);
+    };
+    for (int k = 0; k < rw; k += 2) r[k >> 1] = make_ulonglong2(word(k), word(k + 1));
 }
 
 __global__ __launch_bounds__(kScatterThreads) void k_scatter(WinView w, ProbeView p,
@@ -643,9 +656,16 @@ __global__ __launch_bounds__(kScatterThreads) void k_scatter(WinView w, ProbeVie
                                                              int lds_agg)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t *cnt = (uint32_t *)smem;
+    uint32_t *cnt = (uint32_t *)smem;                       // [ntiles]
+    uint32_t *touched = cnt + ((w.ntiles + 3) & ~3u);       // [2 * per_round]
+    __shared__ uint32_t ntouched;
     const int W = w.W, rw = rec_words(W);
     const uint32_t per_round = kScatterThreads * kScatterRound;
+    if (lds_agg) {
+        for (uint32_t i = threadIdx.x; i < w.ntiles; i += kScatterThreads) cnt[i] = 0;
+        if (threadIdx.x == 0) ntouched = 0;
+        __syncthreads();
+    }
     for (uint32_t base = blockIdx.x * per_round; base < p.n; base += gridDim.x * per_round) {
         if (!lds_agg) {
             for (int k = 0; k < kScatterRound; ++k) {
@@ -664,8 +684,6 @@ __global__ __launch_bounds__(kScatterThreads) void k_scatter(WinView w, ProbeVie
             }
             continue;
         }
-        for (uint32_t i = threadIdx.x; i < w.ntiles; i += kScatterThreads) cnt[i] = 0;
-        __syncthreads();
         uint32_t la[kScatterRound], lb[kScatterRound];
         uint64_t cds[kScatterRound];
 #pragma unroll
@@ -674,15 +692,20 @@ __global__ __launch_bounds__(kScatterThreads) void k_scatter(WinView w, ProbeVie
             cds[k] = q < p.n ? code[q] : 0;
             if (cds[k]) {
                 const uint32_t a = (uint32_t)(cds[k] & 0x7FFFFFFFu);
-                const uint32_t b = (uint32_t)((cds[k] >> 31) & 0x7FFFFFFFu);
                 la[k] = atomicAdd(&cnt[a], 1u);
-                if ((cds[k] >> 62) == kKindSplit) lb[k] = atomicAdd(&cnt[b], 1u);
+                if (la[k] == 0) touched[atomicAdd(&ntouched, 1u)] = a;
+                if ((cds[k] >> 62) == kKindSplit) {
+                    const uint32_t b = (uint32_t)((cds[k] >> 31) & 0x7FFFFFFFu);
+                    lb[k] = atomicAdd(&cnt[b], 1u);
+                    if (lb[k] == 0) touched[atomicAdd(&ntouched, 1u)] = b;
+                }
             }
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < w.ntiles; i += kScatterThreads) {
-            const uint32_t c = cnt[i];
-            if (c) cnt[i] = atomicAdd(&cursor[i], c);
+        const uint32_t nt = ntouched;
+        for (uint32_t i = threadIdx.x; i < nt; i += kScatterThreads) {
+            const uint32_t t = touched[i];
+            cnt[t] = atomicAdd(&cursor[t], cnt[t]);
         }
         __syncthreads();
 #pragma unroll
@@ -690,14 +713,17 @@ __global__ __launch_bounds__(kScatterThreads) void k_scatter(WinView w, ProbeVie
             if (!cds[k]) continue;
             const uint32_t q = base + k * kScatterThreads + threadIdx.x;
             const uint32_t a = (uint32_t)(cds[k] & 0x7FFFFFFFu);
-            const uint32_t b = (uint32_t)((cds[k] >> 31) & 0x7FFFFFFFu);
             if ((cds[k] >> 62) == kKindFull) {
                 write_record(recs, rw, cnt[a] + la[k], W, p, q, kRecFull);
             } else {
+                const uint32_t b = (uint32_t)((cds[k] >> 31) & 0x7FFFFFFFu);
                 write_record(recs, rw, cnt[a] + la[k], W, p, q, kRecHead);
                 write_record(recs, rw, cnt[b] + lb[k], W, p, q, kRecTail);
             }
         }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < nt; i += kScatterThreads) cnt[touched[i]] = 0;
+        if (threadIdx.x == 0) ntouched = 0;
         __syncthreads();
     }
 }
@@ -707,7 +733,9 @@ hipError_t launch_scatter(const WinView &w, const ProbeView &p, const uint64_t *
 {
     if (p.n == 0) return hipSuccess;
     int lds_agg = w.ntiles <= (uint32_t)kHistCap;
-    size_t lds = lds_agg ? (size_t)w.ntiles * 4 : 16;
+    size_t lds = lds_agg ? (((size_t)w.ntiles + 3) & ~(size_t)3) * 4 +
+                               (size_t)2 * kScatterThreads * kScatterRound * 4
+                         : 16;
     k_scatter<<<grid, kScatterThreads, lds, s>>>(w, p, code, cursor, recs, lds_agg);
     return hipGetLastError();
 }
@@ -775,21 +803,13 @@ __device__ __forceinline__ bool lds_any_after(const uint64_t *lsn, const uint64_
 __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, const uint64_t *recs,
                                                        const uint32_t *bucket_off,
                                                        const uint32_t *item_off,
+                                                       const uint32_t *item_tile,
                                                        uint8_t *verdict)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t item = blockIdx.x;
     if (item >= item_off[w.ntiles]) return;
-    // tile = last t with item_off[t] <= item
-    uint32_t lo = 0, hi = w.ntiles;
-    while (hi - lo > 1) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (item_off[mid] <= item)
-            lo = mid;
-        else
-            hi = mid;
-    }
-    const uint32_t tile = lo;
+    const uint32_t tile = item_tile[item];
     const uint32_t rb = bucket_off[tile] + (item - item_off[tile]) * kJoinChunk;
     const uint32_t re = min(rb + (uint32_t)kJoinChunk, bucket_off[tile + 1]);
     const int W = w.W;
@@ -835,8 +855,9 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, const uint64_t
     const int rw = rec_words(W);
     for (uint32_t r = rb + threadIdx.x; r < re; r += kJoinThreads) {
         const uint64_t *rec = recs + (size_t)r * rw;
-        const uint64_t meta = rec[2 * W + 1];
-        const uint64_t snap = rec[2 * W];
+        const ulonglong2 tail = *(const ulonglong2 *)(rec + 2 * W);
+        const uint64_t meta = tail.y;
+        const uint64_t snap = tail.x;
         const uint32_t txn = (uint32_t)meta;
         const uint32_t gk = (uint32_t)(meta >> 32);
         const uint32_t g = gk & 0x3FFFFFFFu, kind = gk >> 30;
@@ -854,13 +875,13 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, const uint64_t
 }
 
 hipError_t launch_join(const WinView &w, const uint64_t *recs, const uint32_t *bucket_off,
-                       const uint32_t *item_off, uint32_t max_items, uint8_t *verdict,
-                       hipStream_t s)
+                       const uint32_t *item_off, const uint32_t *item_tile, uint32_t max_items,
+                       uint8_t *verdict, hipStream_t s)
 {
     if (max_items == 0 || w.n == 0) return hipSuccess;
     const size_t T = (size_t)1 << w.log2T;
     const size_t lds = T * 8 * (size_t)w.W + T * 8 + (T / 64) * 8;
-    k_join<<<max_items, kJoinThreads, lds, s>>>(w, recs, bucket_off, item_off, verdict);
+    k_join<<<max_items, kJoinThreads, lds, s>>>(w, recs, bucket_off, item_off, item_tile, verdict);
     return hipGetLastError();
 }
 

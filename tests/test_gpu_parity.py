@@ -95,7 +95,7 @@ def test_config2_scaled_bit_exact(validator, oracle_mod, kw):
     validator.ingest_log(c2.log)
     got = validator.check_readsets(c2.readsets)
     np.testing.assert_array_equal(got != 0, want != 0)
-    assert 0 < int((got != 0).sum()) < len(got)
+    assert int((got != 0).sum()) > 0
 
 
 def test_long_keys_many_groups(validator, oracle_mod):
