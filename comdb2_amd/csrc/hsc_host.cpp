@@ -194,6 +194,10 @@ static void add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keyle
 // ---------------------------------------------------------------------------
 // device window build
 // ---------------------------------------------------------------------------
+// Row capacity: a whole number of 2048-row tiles (the join stages full tiles
+// without bounds checks; tiles are <= 2048 rows).
+static size_t window_cap(size_t n) { return std::max<size_t>(2048, (n + 2047) & ~(size_t)2047); }
+
 static int window_words(hsc_ctx *c)
 {
     int W = 1;
@@ -299,7 +303,7 @@ static int build_from_host(hsc_ctx *c)
     const size_t n_in = c->h_gid.size();
     c->W = window_words(c);
     const int W = c->W;
-    c->cap = std::max<size_t>(64, (n_in + 63) & ~(size_t)63);
+    c->cap = window_cap(n_in);
     const size_t cap = c->cap;
     std::vector<uint64_t> words((size_t)W * cap, 0);
     std::vector<uint8_t> buf((size_t)W * 8);
@@ -907,7 +911,7 @@ int hsc_window_ingest_device(hsc_ctx *c, size_t n, int words, const uint32_t *gi
     c->end_lsn = end_lsn;
     if (words < window_words(c)) return fail(c, HSC_EINVAL, "fewer key words than a registered group needs");
     c->W = words;
-    c->cap = std::max<size_t>(64, (n + 63) & ~(size_t)63);
+    c->cap = window_cap(n);
     HIPCHK(c, c->d_gid.ensure(c->cap * 4));
     HIPCHK(c, c->d_words.ensure(c->cap * 8 * (size_t)words));
     HIPCHK(c, c->d_lsn.ensure(c->cap * 8));

@@ -20,7 +20,7 @@
 namespace hsc {
 
 constexpr int kMaxWords = 64;       // MAXKEYLEN 512 B (bbinc/cdb2_constants.h:33)
-constexpr int kTopCap = 4096;       // splitters held in LDS by the locate kernel
+constexpr int kTopCap = 5120;       // splitters held in LDS by the locate kernel
 constexpr int kLocateThreads = 512;
 constexpr int kHistCap = 8192;      // tiles whose bucket counters fit in LDS
 constexpr int kJoinThreads = 512;

@@ -411,23 +411,26 @@ __global__ void k_sparse_level(uint32_t ntiles, int level, uint64_t *tmax)
     tmax[(size_t)level * ntiles + t] = a > b ? a : b;
 }
 
-__global__ __launch_bounds__(256) void k_group_table_max(const uint32_t *gstart,
-                                                         const uint32_t *gend,
+// Per-table max commit LSN over the key rows (rows sorted by gid: a wave's
+// rows usually share one group -> one atomic per wave).
+__global__ __launch_bounds__(256) void k_group_table_max(uint32_t n, const uint32_t *gid,
                                                          const uint64_t *lsn,
                                                          const uint32_t *group_table,
                                                          uint64_t *table_max)
 {
-    __shared__ uint64_t part[4];
-    const uint32_t g = blockIdx.x;
-    uint64_t m = 0;
-    for (uint32_t i = gstart[g] + threadIdx.x; i < gend[g]; i += 256) m = lsn[i] > m ? lsn[i] : m;
-    m = wave_max_u64(m);
-    if (lane_id() == 0) part[threadIdx.x >> 6] = m;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t r = part[0];
-        for (int k = 1; k < 4; ++k) r = part[k] > r ? part[k] : r;
-        if (r) atomicMax((unsigned long long *)&table_max[group_table[g]], (unsigned long long)r);
+    for (uint32_t base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
+        const uint32_t i = base + threadIdx.x;
+        const bool valid = i < n;
+        const uint32_t g = valid ? gid[i] : 0xFFFFFFFFu;
+        const uint64_t v = valid ? lsn[i] : 0;
+        const uint32_t g0 = __shfl(g, 0, 64);
+        if (__all(!valid || g == g0)) {
+            const uint64_t m = wave_max_u64(v);
+            if (lane_id() == 0 && g0 != 0xFFFFFFFFu)
+                atomicMax((unsigned long long *)&table_max[group_table[g0]], (unsigned long long)m);
+        } else if (valid) {
+            atomicMax((unsigned long long *)&table_max[group_table[g]], (unsigned long long)v);
+        }
     }
 }
 
@@ -454,7 +457,8 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
     for (int l = 1; l < w.levels; ++l)
         k_sparse_level<<<(w.ntiles + 255) / 256, 256, 0, s>>>(w.ntiles, l, tmax);
     if (ngroups > 0)
-        k_group_table_max<<<ngroups, 256, 0, s>>>(gstart, gend, w.lsn, group_table, table_max);
+        k_group_table_max<<<std::min<uint32_t>((w.n + 255) / 256, 4096), 256, 0, s>>>(
+            w.n, w.gid, w.lsn, group_table, table_max);
     k_splitters<<<(w.ntiles + 255) / 256, 256, 0, s>>>(w, sp_g, sp_w);
     return hipGetLastError();
 }
@@ -507,6 +511,40 @@ __device__ uint32_t count_splitters(const WinView &w, const uint64_t *top_w0,
     return L;
 }
 
+// Both counts of a probe at once: c = #splitters < (g, lo), c2 = #splitters
+// <= (g, hi); the two binary searches advance in lockstep so their LDS
+// reads overlap.
+__device__ __forceinline__ void count_splitters2(const WinView &w, const uint64_t *top_w0,
+                                                 const uint32_t *top_g, uint32_t ntop,
+                                                 uint32_t stride_t, uint32_t g, uint64_t l0,
+                                                 uint64_t l1, const uint64_t *lmem, uint64_t h0,
+                                                 uint64_t h1, const uint64_t *hmem, size_t ks,
+                                                 uint32_t &c, uint32_t &c2)
+{
+    if (stride_t != 1) {
+        c = count_splitters<false>(w, top_w0, top_g, ntop, stride_t, g, l0, l1, lmem, ks);
+        c2 = count_splitters<true>(w, top_w0, top_g, ntop, stride_t, g, h0, h1, hmem, ks);
+        return;
+    }
+    uint32_t alo = 0, ahi = ntop, blo = 0, bhi = ntop;
+    while (alo < ahi || blo < bhi) {
+        const uint32_t am = (alo + ahi) >> 1, bm = (blo + bhi) >> 1;
+        const uint32_t ai = min(am, ntop - 1), bi = min(bm, ntop - 1);
+        const uint32_t ag = top_g[ai], bg = top_g[bi];
+        const uint64_t aw = top_w0[ai], bw = top_w0[bi];
+        if (alo < ahi) {
+            const int ca = cmp_splitter(w, am, ag, aw, g, l0, l1, lmem, ks);
+            if (ca < 0) alo = am + 1; else ahi = am;
+        }
+        if (blo < bhi) {
+            const int cb = cmp_splitter(w, bm, bg, bw, g, h0, h1, hmem, ks);
+            if (cb <= 0) blo = bm + 1; else bhi = bm;
+        }
+    }
+    c = alo;
+    c2 = blo;
+}
+
 __device__ __forceinline__ uint64_t tiles_max(const WinView &w, uint32_t x, uint32_t y)
 {
     uint32_t len = y - x + 1;
@@ -538,11 +576,10 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate(WinView w, ProbeView 
         const uint64_t l0 = p.lo[q], l1 = w.W > 1 ? p.lo[ks + q] : 0;
         const uint64_t h0 = p.hi[q], h1 = w.W > 1 ? p.hi[ks + q] : 0;
         uint64_t cd = 0;
-        const uint32_t c2 =
-            count_splitters<true>(w, top_w0, top_g, ntop, stride_t, g, h0, h1, p.hi + q, ks);
+        uint32_t c, c2;
+        count_splitters2(w, top_w0, top_g, ntop, stride_t, g, l0, l1, p.lo + q, h0, h1, p.hi + q,
+                         ks, c, c2);
         if (c2 > 0) {
-            const uint32_t c =
-                count_splitters<false>(w, top_w0, top_g, ntop, stride_t, g, l0, l1, p.lo + q, ks);
             const uint32_t a = c ? c - 1 : 0, b = c2 - 1;
             if (a == b) {
                 cd = (uint64_t)a | ((uint64_t)a << 31) | (kKindFull << 62);
@@ -633,7 +670,7 @@ hipError_t launch_plan(const uint32_t *counts, uint32_t ntiles, uint32_t *bucket
 
 // ---- scatter: join records grouped by tile ---------------------------------
 constexpr int kScatterThreads = 256;
-constexpr int kScatterRound = 8;  // probes per thread per round
+constexpr int kScatterRound = 2;  // probes per thread per round
 
 // One join record = rec_words(W) u64, written as 16-byte stores.
 __device__ __forceinline__ void write_record(uint64_t *recs, int rw, uint32_t slot, int W,
@@ -800,6 +837,7 @@ __device__ __forceinline__ bool lds_any_after(const uint64_t *lsn, const uint64_
     return false;
 }
 
+template <int WT>  // key words if 1 or 2 (fast staging path), 0 = any
 __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, const uint64_t *recs,
                                                        const uint32_t *bucket_off,
                                                        const uint32_t *item_off,
@@ -812,7 +850,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, const uint64_t
     const uint32_t tile = item_tile[item];
     const uint32_t rb = bucket_off[tile] + (item - item_off[tile]) * kJoinChunk;
     const uint32_t re = min(rb + (uint32_t)kJoinChunk, bucket_off[tile + 1]);
-    const int W = w.W;
+    const int W = WT > 0 ? WT : w.W;
     const uint32_t T = 1u << w.log2T;
     const uint32_t ts = tile << w.log2T;
     const uint32_t tn = min(T, w.n - ts);
@@ -820,26 +858,34 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, const uint64_t
     uint64_t *kw = (uint64_t *)smem;               // [W][T]
     uint64_t *lsn = kw + (size_t)W * T;            // [T]
     uint64_t *bmax = lsn + T;                      // [T / 64]
-    // stage the tile: 16-byte loads (rows start 2-aligned: ts and T even)
-    for (int j = 0; j < W; ++j) {
-        const uint64_t *src = w.words + (size_t)j * w.stride + ts;
-        for (uint32_t i = 2 * threadIdx.x; i < tn; i += 2 * kJoinThreads) {
-            if (i + 1 < tn) {
-                const ulonglong2 v = *(const ulonglong2 *)(src + i);
-                kw[(size_t)j * T + i] = v.x;
-                kw[(size_t)j * T + i + 1] = v.y;
-            } else {
-                kw[(size_t)j * T + i] = src[i];
-            }
+    // stage the tile: every thread issues all of its 16-byte loads first and
+    // only then writes LDS, so its loads are in flight together.  The window
+    // arrays are padded to a whole number of tiles, so the loads need no
+    // bounds checks (rows >= tn are never searched).
+    if constexpr (WT > 0) {
+        constexpr int kIt = (1 << 11) / (2 * kJoinThreads);  // T == 2048 for W <= 2
+        ulonglong2 v[kIt][WT + 1];
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+            const uint32_t pr = threadIdx.x + it * kJoinThreads;
+#pragma unroll
+            for (int j = 0; j < WT; ++j)
+                v[it][j] = *(const ulonglong2 *)(w.words + (size_t)j * w.stride + ts + 2 * pr);
+            v[it][WT] = *(const ulonglong2 *)(w.lsn + ts + 2 * pr);
         }
-    }
-    for (uint32_t i = 2 * threadIdx.x; i < tn; i += 2 * kJoinThreads) {
-        if (i + 1 < tn) {
-            const ulonglong2 v = *(const ulonglong2 *)(w.lsn + ts + i);
-            lsn[i] = v.x;
-            lsn[i + 1] = v.y;
-        } else {
-            lsn[i] = w.lsn[ts + i];
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+            const uint32_t pr = threadIdx.x + it * kJoinThreads;
+#pragma unroll
+            for (int j = 0; j < WT; ++j) *(ulonglong2 *)(kw + (size_t)j * T + 2 * pr) = v[it][j];
+            *(ulonglong2 *)(lsn + 2 * pr) = v[it][WT];
+        }
+    } else {
+        for (int j = 0; j <= W; ++j) {
+            const uint64_t *src = j < W ? w.words + (size_t)j * w.stride + ts : w.lsn + ts;
+            uint64_t *dst = j < W ? kw + (size_t)j * T : lsn;
+            for (uint32_t pr = threadIdx.x; pr < T / 2; pr += kJoinThreads)
+                *(ulonglong2 *)(dst + 2 * pr) = *(const ulonglong2 *)(src + 2 * pr);
         }
     }
     __syncthreads();
@@ -881,7 +927,12 @@ hipError_t launch_join(const WinView &w, const uint64_t *recs, const uint32_t *b
     if (max_items == 0 || w.n == 0) return hipSuccess;
     const size_t T = (size_t)1 << w.log2T;
     const size_t lds = T * 8 * (size_t)w.W + T * 8 + (T / 64) * 8;
-    k_join<<<max_items, kJoinThreads, lds, s>>>(w, recs, bucket_off, item_off, item_tile, verdict);
+    if (w.W == 1 && w.log2T == 11)
+        k_join<1><<<max_items, kJoinThreads, lds, s>>>(w, recs, bucket_off, item_off, item_tile, verdict);
+    else if (w.W == 2 && w.log2T == 11)
+        k_join<2><<<max_items, kJoinThreads, lds, s>>>(w, recs, bucket_off, item_off, item_tile, verdict);
+    else
+        k_join<0><<<max_items, kJoinThreads, lds, s>>>(w, recs, bucket_off, item_off, item_tile, verdict);
     return hipGetLastError();
 }
 
