@@ -22,6 +22,7 @@ namespace hsc {
 constexpr int kMaxWords = 64;       // MAXKEYLEN 512 B (bbinc/cdb2_constants.h:33)
 constexpr int kTopCap = 5120;       // splitters held in LDS by the locate kernel
 constexpr int kLocateThreads = 512;
+constexpr int kMaxChunks = 512;     // probe chunks (locate / scatter workgroups)
 constexpr int kHistCap = 8192;      // tiles whose bucket counters fit in LDS
 constexpr int kJoinThreads = 512;
 constexpr int kJoinChunk = 1024;    // join records per workgroup
@@ -29,7 +30,7 @@ constexpr int kLdsJoinBudget = 49152;
 
 // Probe codes written by the locate kernel: a | b << 31 | kind << 62.
 constexpr uint64_t kKindFull = 1, kKindSplit = 2;
-// Join record kinds (top two bits of the gid field).
+// Join record kinds (top two bits of the record meta word).
 constexpr uint32_t kRecFull = 1, kRecHead = 2, kRecTail = 3;
 
 struct WinView {
@@ -58,7 +59,8 @@ struct ProbeView {
 };
 
 // Join-record layout: rec_words u64 per record = lo[W] hi[W] snap meta,
-// meta = txn | (gid | kind << 30) << 32.  2W+2 words -> 16-byte multiple.
+// meta = txn | lb << 32 | ub << 44 | kind << 62 ([lb, ub) = the probe's
+// group rows inside the tile).  2W+2 words -> 16-byte multiple.
 __host__ __device__ inline int rec_words(int W) { return 2 * W + 2; }
 
 // Tile size: largest power of two whose keys + lsn fit the LDS budget.
@@ -87,14 +89,24 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
                            uint64_t *tmax, const uint32_t *group_table,
                            uint64_t *table_max, uint32_t *sp_g, uint64_t *sp_w, hipStream_t s);
 // Probe.
-hipError_t launch_locate(const WinView &w, const ProbeView &p, uint64_t *code,
-                         uint32_t *counts, uint8_t *verdict, int grid, hipStream_t s);
-hipError_t launch_plan(const uint32_t *counts, uint32_t ntiles, uint32_t *bucket_off,
-                       uint32_t *cursor, uint32_t *item_off, uint32_t *item_tile, hipStream_t s);
-hipError_t launch_scatter(const WinView &w, const ProbeView &p, const uint64_t *code,
-                          uint32_t *cursor, uint64_t *recs, int grid, hipStream_t s);
-hipError_t launch_join(const WinView &w, const uint64_t *recs, const uint32_t *bucket_off,
-                       const uint32_t *item_off, const uint32_t *item_tile, uint32_t max_items,
+struct ProbeWork {
+    uint64_t *code;        // [n] a | b << 31 | kind << 62
+    uint32_t *hist;        // [G][ntiles] per-chunk record counts -> offsets
+    uint32_t *counts;      // [ntiles + 1] records per tile
+    uint32_t *bucket_off;  // [ntiles + 1]
+    uint32_t *cursor;      // [ntiles] (global-atomic mode, ntiles > kHistCap)
+    uint32_t *item_off;    // [ntiles + 1]
+    uint32_t *item_tile;   // [max items]
+    uint64_t *recs;        // join records
+    uint32_t G, chunk;     // probe chunks (one workgroup each in locate/scatter)
+    int lds_mode;          // ntiles <= kHistCap: LDS histograms, no global atomics
+};
+hipError_t launch_locate(const WinView &w, const ProbeView &p, const ProbeWork &work,
+                         uint8_t *verdict, hipStream_t s);
+hipError_t launch_plan(const WinView &w, const ProbeWork &work, hipStream_t s);
+hipError_t launch_scatter(const WinView &w, const ProbeView &p, const ProbeWork &work,
+                          hipStream_t s);
+hipError_t launch_join(const WinView &w, const ProbeWork &work, uint32_t max_items,
                        uint8_t *verdict, hipStream_t s);
 hipError_t launch_pack(const uint8_t *verdict, uint32_t n_txn, uint64_t *bitmap,
                        hipStream_t s);

@@ -466,6 +466,14 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
 // ============================================================================
 // probe
 // ============================================================================
+//
+// Probes are split into G contiguous chunks; chunk g is handled by workgroup g
+// of both k_locate and k_scatter.  k_locate counts the join records of its
+// chunk per tile in LDS and stores the row hist[g][*]; k_colscan turns every
+// column into chunk offsets inside the tile's bucket; k_plan scans the tile
+// totals.  k_scatter then seeds its LDS counters with bucket_off[t] +
+// hist[g][t], so every record slot comes from an LDS atomic: no global
+// atomics, no contention across XCDs.
 
 // sign((sg, splitter words) - (g, key)) for tile t's first row; the
 // splitter's group and word 0 are given, later words come from sp_w.
@@ -480,69 +488,66 @@ __device__ __forceinline__ int cmp_splitter(const WinView &w, uint32_t t, uint32
     return -cmp_words(w.W - 1, k1, kmem + ks, ks, w.sp_w + w.ntiles + t, w.ntiles);
 }
 
-// Number of tiles whose first row compares < (g, key) (LEQ: <=).  The LDS
-// holds every stride_t-th splitter; the last step searches sp_g/sp_w.
-template <bool LEQ>
-__device__ uint32_t count_splitters(const WinView &w, const uint64_t *top_w0,
-                                    const uint32_t *top_g, uint32_t ntop, uint32_t stride_t,
-                                    uint32_t g, uint64_t k0, uint64_t k1, const uint64_t *kmem,
-                                    size_t ks)
+// NS binary searches in lockstep over the splitters: out[i] = number of
+// tiles whose first row compares < key i (leq[i]: <=).  The LDS holds every
+// stride_t-th splitter; with stride_t > 1 a last step searches sp_g/sp_w.
+template <int NS>
+__device__ __forceinline__ void count_splitters(const WinView &w, const uint64_t *top_w0,
+                                                const uint32_t *top_g, uint32_t ntop,
+                                                uint32_t stride_t, const uint32_t (&g)[NS],
+                                                const uint64_t (&k0)[NS], const uint64_t (&k1)[NS],
+                                                const uint64_t *const (&kmem)[NS], size_t ks,
+                                                const bool (&leq)[NS], uint32_t (&out)[NS])
 {
-    uint32_t lo = 0, hi = ntop;
-    while (lo < hi) {
-        uint32_t mid = (lo + hi) >> 1;
-        int c = cmp_splitter(w, mid * stride_t, top_g[mid], top_w0[mid], g, k0, k1, kmem, ks);
-        if (LEQ ? c <= 0 : c < 0)
-            lo = mid + 1;
-        else
-            hi = mid;
+    uint32_t lo[NS], hi[NS];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        lo[i] = 0;
+        hi[i] = ntop;
     }
-    if (lo == 0 || stride_t == 1) return lo * stride_t < w.ntiles ? lo * stride_t : w.ntiles;
-    uint32_t L = (lo - 1) * stride_t + 1;
-    uint32_t H = min(lo * stride_t, w.ntiles);
-    while (L < H) {
-        uint32_t mid = (L + H) >> 1;
-        int c = cmp_splitter(w, mid, w.sp_g[mid], w.sp_w[mid], g, k0, k1, kmem, ks);
-        if (LEQ ? c <= 0 : c < 0)
-            L = mid + 1;
-        else
-            H = mid;
-    }
-    return L;
-}
-
-// Both counts of a probe at once: c = #splitters < (g, lo), c2 = #splitters
-// <= (g, hi); the two binary searches advance in lockstep so their LDS
-// reads overlap.
-__device__ __forceinline__ void count_splitters2(const WinView &w, const uint64_t *top_w0,
-                                                 const uint32_t *top_g, uint32_t ntop,
-                                                 uint32_t stride_t, uint32_t g, uint64_t l0,
-                                                 uint64_t l1, const uint64_t *lmem, uint64_t h0,
-                                                 uint64_t h1, const uint64_t *hmem, size_t ks,
-                                                 uint32_t &c, uint32_t &c2)
-{
-    if (stride_t != 1) {
-        c = count_splitters<false>(w, top_w0, top_g, ntop, stride_t, g, l0, l1, lmem, ks);
-        c2 = count_splitters<true>(w, top_w0, top_g, ntop, stride_t, g, h0, h1, hmem, ks);
-        return;
-    }
-    uint32_t alo = 0, ahi = ntop, blo = 0, bhi = ntop;
-    while (alo < ahi || blo < bhi) {
-        const uint32_t am = (alo + ahi) >> 1, bm = (blo + bhi) >> 1;
-        const uint32_t ai = min(am, ntop - 1), bi = min(bm, ntop - 1);
-        const uint32_t ag = top_g[ai], bg = top_g[bi];
-        const uint64_t aw = top_w0[ai], bw = top_w0[bi];
-        if (alo < ahi) {
-            const int ca = cmp_splitter(w, am, ag, aw, g, l0, l1, lmem, ks);
-            if (ca < 0) alo = am + 1; else ahi = am;
+    for (;;) {
+        bool any = false;
+        uint32_t sg[NS];
+        uint64_t sw[NS];
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            const uint32_t m = min((lo[i] + hi[i]) >> 1, ntop ? ntop - 1 : 0);
+            sg[i] = top_g[m];
+            sw[i] = top_w0[m];
         }
-        if (blo < bhi) {
-            const int cb = cmp_splitter(w, bm, bg, bw, g, h0, h1, hmem, ks);
-            if (cb <= 0) blo = bm + 1; else bhi = bm;
+#pragma unroll
+        for (int i = 0; i < NS; ++i) {
+            if (lo[i] < hi[i]) {
+                any = true;
+                const uint32_t m = (lo[i] + hi[i]) >> 1;
+                const int c = cmp_splitter(w, m * stride_t, sg[i], sw[i], g[i], k0[i], k1[i],
+                                           kmem[i], ks);
+                if (leq[i] ? c <= 0 : c < 0)
+                    lo[i] = m + 1;
+                else
+                    hi[i] = m;
+            }
         }
+        if (!any) break;
     }
-    c = alo;
-    c2 = blo;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) {
+        const uint32_t t = lo[i];
+        if (t == 0 || stride_t == 1) {
+            out[i] = min(t * stride_t, w.ntiles);
+            continue;
+        }
+        uint32_t L = (t - 1) * stride_t + 1, H = min(t * stride_t, w.ntiles);
+        while (L < H) {
+            const uint32_t m = (L + H) >> 1;
+            const int c = cmp_splitter(w, m, w.sp_g[m], w.sp_w[m], g[i], k0[i], k1[i], kmem[i], ks);
+            if (leq[i] ? c <= 0 : c < 0)
+                L = m + 1;
+            else
+                H = m;
+        }
+        out[i] = L;
+    }
 }
 
 __device__ __forceinline__ uint64_t tiles_max(const WinView &w, uint32_t x, uint32_t y)
@@ -554,310 +559,361 @@ __device__ __forceinline__ uint64_t tiles_max(const WinView &w, uint32_t x, uint
     return a > b ? a : b;
 }
 
-__global__ __launch_bounds__(kLocateThreads) void k_locate(WinView w, ProbeView p, uint64_t *code,
-                                                uint32_t *counts, uint8_t *verdict,
-                                                uint32_t ntop, uint32_t stride_t, int lds_hist)
+constexpr int kLocateBatch = 2;  // probes per thread advanced together
+
+__global__ __launch_bounds__(kLocateThreads) void k_locate(WinView w, ProbeView p,
+                                                           ProbeWork work, uint8_t *verdict,
+                                                           uint32_t ntop, uint32_t stride_t)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint64_t *top_w0 = (uint64_t *)smem;
     uint32_t *top_g = (uint32_t *)(top_w0 + ntop);
     uint32_t *hist = top_g + ((ntop + 3) & ~3u);
-    for (uint32_t i = threadIdx.x; i < ntop; i += blockDim.x) {
-        top_w0[i] = w.sp_w[(size_t)i * stride_t];
-        top_g[i] = w.sp_g[(size_t)i * stride_t];
+    // stage the splitters: loads in batches of 8 per thread before the stores
+    for (uint32_t base = 0; base < ntop; base += 8 * kLocateThreads) {
+        uint64_t vw[8];
+        uint32_t vg[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t i = base + k * kLocateThreads + threadIdx.x;
+            if (i < ntop) {
+                vw[k] = w.sp_w[(size_t)i * stride_t];
+                vg[k] = w.sp_g[(size_t)i * stride_t];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t i = base + k * kLocateThreads + threadIdx.x;
+            if (i < ntop) {
+                top_w0[i] = vw[k];
+                top_g[i] = vg[k];
+            }
+        }
     }
-    if (lds_hist)
-        for (uint32_t i = threadIdx.x; i < w.ntiles; i += blockDim.x) hist[i] = 0;
+    if (work.lds_mode)
+        for (uint32_t i = threadIdx.x; i < w.ntiles; i += kLocateThreads) hist[i] = 0;
     __syncthreads();
 
     const size_t ks = p.n;
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < p.n; q += gridDim.x * blockDim.x) {
-        const uint32_t g = p.gid[q];
-        const uint64_t l0 = p.lo[q], l1 = w.W > 1 ? p.lo[ks + q] : 0;
-        const uint64_t h0 = p.hi[q], h1 = w.W > 1 ? p.hi[ks + q] : 0;
-        uint64_t cd = 0;
-        uint32_t c, c2;
-        count_splitters2(w, top_w0, top_g, ntop, stride_t, g, l0, l1, p.lo + q, h0, h1, p.hi + q,
-                         ks, c, c2);
-        if (c2 > 0) {
-            const uint32_t a = c ? c - 1 : 0, b = c2 - 1;
-            if (a == b) {
-                cd = (uint64_t)a | ((uint64_t)a << 31) | (kKindFull << 62);
-            } else if (a < b) {
-                bool hit = false;
-                if (b > a + 1) hit = tiles_max(w, a + 1, b - 1) > p.snap[q];
-                if (hit)
-                    verdict[p.txn[q]] = 1;
-                else
-                    cd = (uint64_t)a | ((uint64_t)b << 31) | (kKindSplit << 62);
-            }
+    const uint32_t c0 = blockIdx.x * work.chunk;
+    const uint32_t c1 = min(p.n, c0 + work.chunk);
+    for (uint32_t base = c0; base < c1; base += kLocateBatch * kLocateThreads) {
+        constexpr int NS = 2 * kLocateBatch;
+        uint32_t qq[kLocateBatch];
+        bool valid[kLocateBatch];
+        uint32_t gg[NS];
+        uint64_t k0[NS], k1[NS];
+        const uint64_t *km[NS];
+        bool leq[NS];
+        uint32_t cnt[NS];
+#pragma unroll
+        for (int b = 0; b < kLocateBatch; ++b) {
+            qq[b] = base + b * kLocateThreads + threadIdx.x;
+            valid[b] = qq[b] < c1;
+            const uint32_t q = valid[b] ? qq[b] : c0;
+            const uint32_t g = p.gid[q];
+            gg[2 * b] = gg[2 * b + 1] = g;
+            k0[2 * b] = p.lo[q];
+            k0[2 * b + 1] = p.hi[q];
+            k1[2 * b] = w.W > 1 ? p.lo[ks + q] : 0;
+            k1[2 * b + 1] = w.W > 1 ? p.hi[ks + q] : 0;
+            km[2 * b] = p.lo + q;
+            km[2 * b + 1] = p.hi + q;
+            leq[2 * b] = false;
+            leq[2 * b + 1] = true;
         }
-        code[q] = cd;
-        if (cd) {
-            const uint32_t a = (uint32_t)(cd & 0x7FFFFFFFu);
-            const uint32_t b = (uint32_t)((cd >> 31) & 0x7FFFFFFFu);
-            if (lds_hist) {
-                atomicAdd(&hist[a], 1u);
-                if (b != a) atomicAdd(&hist[b], 1u);
-            } else {
-                atomicAdd(&counts[a], 1u);
-                if (b != a) atomicAdd(&counts[b], 1u);
+        count_splitters<NS>(w, top_w0, top_g, ntop, stride_t, gg, k0, k1, km, ks, leq, cnt);
+#pragma unroll
+        for (int b = 0; b < kLocateBatch; ++b) {
+            if (!valid[b]) continue;
+            const uint32_t q = qq[b];
+            const uint32_t c = cnt[2 * b], c2 = cnt[2 * b + 1];
+            uint64_t cd = 0;
+            if (c2 > 0) {
+                const uint32_t a = c ? c - 1 : 0, bt = c2 - 1;
+                if (a == bt) {
+                    cd = (uint64_t)a | ((uint64_t)a << 31) | (kKindFull << 62);
+                } else if (a < bt) {
+                    bool hit = false;
+                    if (bt > a + 1) hit = tiles_max(w, a + 1, bt - 1) > p.snap[q];
+                    if (hit)
+                        verdict[p.txn[q]] = 1;
+                    else
+                        cd = (uint64_t)a | ((uint64_t)bt << 31) | (kKindSplit << 62);
+                }
+            }
+            work.code[q] = cd;
+            if (cd) {
+                const uint32_t a = (uint32_t)(cd & 0x7FFFFFFFu);
+                const uint32_t bt = (uint32_t)((cd >> 31) & 0x7FFFFFFFu);
+                if (work.lds_mode) {
+                    atomicAdd(&hist[a], 1u);
+                    if (bt != a) atomicAdd(&hist[bt], 1u);
+                } else {
+                    atomicAdd(&work.counts[a], 1u);
+                    if (bt != a) atomicAdd(&work.counts[bt], 1u);
+                }
             }
         }
     }
     // table locks: any write to a locked table after the snapshot
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < p.n_lock;
-         q += gridDim.x * blockDim.x) {
-        uint32_t t = p.lock_table[q];
+    for (uint32_t q = blockIdx.x * kLocateThreads + threadIdx.x; q < p.n_lock;
+         q += gridDim.x * kLocateThreads) {
+        const uint32_t t = p.lock_table[q];
         if (t < w.ntables && w.table_max[t] > p.lock_snap[q]) verdict[p.lock_txn[q]] = 1;
     }
-    if (lds_hist) {
+    if (work.lds_mode) {
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < w.ntiles; i += blockDim.x)
-            if (hist[i]) atomicAdd(&counts[i], hist[i]);
+        uint32_t *row = work.hist + (size_t)blockIdx.x * w.ntiles;
+        for (uint32_t i = threadIdx.x; i < w.ntiles; i += kLocateThreads) row[i] = hist[i];
     }
 }
 
-hipError_t launch_locate(const WinView &w, const ProbeView &p, uint64_t *code, uint32_t *counts,
-                         uint8_t *verdict, int grid, hipStream_t s)
+hipError_t launch_locate(const WinView &w, const ProbeView &p, const ProbeWork &work,
+                         uint8_t *verdict, hipStream_t s)
 {
     if (p.n == 0 && p.n_lock == 0) return hipSuccess;
-    uint32_t stride_t = (w.ntiles + kTopCap - 1) / kTopCap;
-    if (stride_t == 0) stride_t = 1;
-    uint32_t ntop = w.n ? (w.ntiles + stride_t - 1) / stride_t : 0;
-    int lds_hist = w.ntiles <= (uint32_t)kHistCap;
+    uint32_t ntop = 0, stride_t = 1;
+    if (w.n) {
+        stride_t = (w.ntiles + kTopCap - 1) / kTopCap;
+        ntop = (w.ntiles + stride_t - 1) / stride_t;
+    }
     size_t lds = (size_t)ntop * 8 + (((size_t)ntop + 3) & ~(size_t)3) * 4 +
-                 (lds_hist ? (size_t)w.ntiles * 4 : 0);
-    k_locate<<<grid, kLocateThreads, lds, s>>>(w, p, code, counts, verdict, ntop, stride_t, lds_hist);
+                 (work.lds_mode ? (size_t)w.ntiles * 4 : 0);
+    k_locate<<<work.G, kLocateThreads, lds, s>>>(w, p, work, verdict, ntop, stride_t);
     return hipGetLastError();
 }
 
-// ---- plan: bucket offsets + work items (one workgroup) ---------------------
-__global__ __launch_bounds__(1024) void k_plan(const uint32_t *counts, uint32_t ntiles,
-                                               uint32_t *bucket_off, uint32_t *cursor,
-                                               uint32_t *item_off, uint32_t *item_tile)
+// ---- plan ------------------------------------------------------------------
+// Column scan of hist[G][ntiles]: hist[g][t] := sum over g' < g; counts[t] := total.
+__global__ __launch_bounds__(256) void k_colscan(ProbeWork work, uint32_t ntiles)
+{
+    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= ntiles) return;
+    uint32_t run = 0;
+    for (uint32_t g0 = 0; g0 < work.G; g0 += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            v[k] = (g0 + k < work.G) ? work.hist[(size_t)(g0 + k) * ntiles + t] : 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (g0 + k < work.G) work.hist[(size_t)(g0 + k) * ntiles + t] = run;
+            run += v[k];
+        }
+    }
+    work.counts[t] = run;
+}
+
+// One workgroup: bucket offsets, per-tile chunk counts, item -> tile table.
+__global__ __launch_bounds__(1024) void k_plan(ProbeWork work, uint32_t ntiles)
 {
     __shared__ uint32_t lds[16];
     uint32_t carry_b = 0, carry_i = 0;
-    for (uint32_t base = 0; base < ntiles; base += 1024) {
-        const uint32_t t = base + threadIdx.x;
-        const uint32_t c = t < ntiles ? counts[t] : 0;
-        const uint32_t ch = (c + kJoinChunk - 1) / kJoinChunk;
-        uint32_t tb, ti;
-        uint32_t pb = block_excl_scan<1024>(c, lds, tb);
-        uint32_t pi = block_excl_scan<1024>(ch, lds, ti);
-        if (t < ntiles) {
-            bucket_off[t] = carry_b + pb;
-            cursor[t] = carry_b + pb;
-            item_off[t] = carry_i + pi;
-            for (uint32_t k = 0; k < ch; ++k) item_tile[carry_i + pi + k] = t;
+    for (uint32_t base = 0; base < ntiles; base += 8 * 1024) {
+        uint32_t cv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t t = base + k * 1024 + threadIdx.x;
+            cv[k] = t < ntiles ? work.counts[t] : 0;
         }
-        carry_b += tb;
-        carry_i += ti;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t t = base + k * 1024 + threadIdx.x;
+            const uint32_t c = cv[k];
+            const uint32_t ch = (c + kJoinChunk - 1) / kJoinChunk;
+            uint32_t tb, ti;
+            const uint32_t pb = block_excl_scan<1024>(c, lds, tb);
+            const uint32_t pi = block_excl_scan<1024>(ch, lds, ti);
+            if (t < ntiles) {
+                work.bucket_off[t] = carry_b + pb;
+                work.cursor[t] = carry_b + pb;
+                work.item_off[t] = carry_i + pi;
+                for (uint32_t j = 0; j < ch; ++j) work.item_tile[carry_i + pi + j] = t;
+            }
+            carry_b += tb;
+            carry_i += ti;
+        }
     }
     if (threadIdx.x == 0) {
-        bucket_off[ntiles] = carry_b;
-        item_off[ntiles] = carry_i;
+        work.bucket_off[ntiles] = carry_b;
+        work.item_off[ntiles] = carry_i;
     }
 }
 
-hipError_t launch_plan(const uint32_t *counts, uint32_t ntiles, uint32_t *bucket_off,
-                       uint32_t *cursor, uint32_t *item_off, uint32_t *item_tile, hipStream_t s)
+hipError_t launch_plan(const WinView &w, const ProbeWork &work, hipStream_t s)
 {
-    k_plan<<<1, 1024, 0, s>>>(counts, ntiles, bucket_off, cursor, item_off, item_tile);
+    if (work.lds_mode) k_colscan<<<(w.ntiles + 255) / 256, 256, 0, s>>>(work, w.ntiles);
+    k_plan<<<1, 1024, 0, s>>>(work, w.ntiles);
     return hipGetLastError();
 }
 
 // ---- scatter: join records grouped by tile ---------------------------------
-constexpr int kScatterThreads = 256;
-constexpr int kScatterRound = 2;  // probes per thread per round
-
-// One join record = rec_words(W) u64, written as 16-byte stores.
-__device__ __forceinline__ void write_record(uint64_t *recs, int rw, uint32_t slot, int W,
-                                             const ProbeView &p, uint32_t q, uint32_t kind)
+// One join record = rec_words(W) u64: lo[W] hi[W] snap meta, with
+// meta = txn | lb << 32 | ub << 44 | kind << 62, [lb, ub) = the rows of the
+// probe's group inside the tile (so the join needs no group lookup).
+__device__ __forceinline__ void write_record(const WinView &w, uint64_t *recs, uint32_t slot,
+                                             const ProbeView &p, uint32_t q, uint32_t tile,
+                                             uint64_t kind)
 {
+    const int W = w.W, rw = rec_words(W);
+    const uint32_t T = 1u << w.log2T;
+    const uint32_t ts = tile << w.log2T;
+    const uint32_t tn = min(T, w.n - ts);
+    const uint32_t g = p.gid[q];
+    const uint32_t gs = w.gstart[g], ge = w.gend[g];
+    const uint64_t lb = gs > ts ? min(gs - ts, tn) : 0;
+    const uint64_t ub = ge > ts ? min(ge - ts, tn) : 0;
+    const uint64_t meta = (uint64_t)p.txn[q] | (lb << 32) | (ub << 44) | (kind << 62);
     ulonglong2 *r = (ulonglong2 *)(recs + (size_t)slot * rw);
     const size_t ks = p.n;
     auto word = [&](int k) -> uint64_t {
         if (k < W) return p.lo[(size_t)k * ks + q];
         if (k < 2 * W) return p.hi[(size_t)(k - W) * ks + q];
         if (k == 2 * W) return p.snap[q];
-        return (uint64_t)p.txn[q] | ((uint64_t)(p.gid[q] | (kind << 30)) << 32);
+        return meta;
     };
     for (int k = 0; k < rw; k += 2) r[k >> 1] = make_ulonglong2(word(k), word(k + 1));
 }
 
-__global__ __launch_bounds__(kScatterThreads) void k_scatter(WinView w, ProbeView p,
-                                                             const uint64_t *code,
-                                                             uint32_t *cursor, uint64_t *recs,
-                                                             int lds_agg)
+__global__ __launch_bounds__(kLocateThreads) void k_scatter(WinView w, ProbeView p,
+                                                            ProbeWork work)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t *cnt = (uint32_t *)smem;                       // [ntiles]
-    uint32_t *touched = cnt + ((w.ntiles + 3) & ~3u);       // [2 * per_round]
-    __shared__ uint32_t ntouched;
-    const int W = w.W, rw = rec_words(W);
-    const uint32_t per_round = kScatterThreads * kScatterRound;
-    if (lds_agg) {
-        for (uint32_t i = threadIdx.x; i < w.ntiles; i += kScatterThreads) cnt[i] = 0;
-        if (threadIdx.x == 0) ntouched = 0;
+    uint32_t *base_t = (uint32_t *)smem;  // [ntiles] next free slot of this chunk
+    if (work.lds_mode) {
+        const uint32_t *row = work.hist + (size_t)blockIdx.x * w.ntiles;
+        for (uint32_t b = 0; b < w.ntiles; b += 8 * kLocateThreads) {
+            uint32_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t i = b + k * kLocateThreads + threadIdx.x;
+                v[k] = i < w.ntiles ? work.bucket_off[i] + row[i] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const uint32_t i = b + k * kLocateThreads + threadIdx.x;
+                if (i < w.ntiles) base_t[i] = v[k];
+            }
+        }
         __syncthreads();
     }
-    for (uint32_t base = blockIdx.x * per_round; base < p.n; base += gridDim.x * per_round) {
-        if (!lds_agg) {
-            for (int k = 0; k < kScatterRound; ++k) {
-                const uint32_t q = base + k * kScatterThreads + threadIdx.x;
-                if (q >= p.n) break;
-                const uint64_t cd = code[q];
-                if (!cd) continue;
-                const uint32_t a = (uint32_t)(cd & 0x7FFFFFFFu);
-                const uint32_t b = (uint32_t)((cd >> 31) & 0x7FFFFFFFu);
-                if ((cd >> 62) == kKindFull) {
-                    write_record(recs, rw, atomicAdd(&cursor[a], 1u), W, p, q, kRecFull);
-                } else {
-                    write_record(recs, rw, atomicAdd(&cursor[a], 1u), W, p, q, kRecHead);
-                    write_record(recs, rw, atomicAdd(&cursor[b], 1u), W, p, q, kRecTail);
-                }
-            }
-            continue;
+    const uint32_t c0 = blockIdx.x * work.chunk;
+    const uint32_t c1 = min(p.n, c0 + work.chunk);
+    for (uint32_t q = c0 + threadIdx.x; q < c1; q += kLocateThreads) {
+        const uint64_t cd = work.code[q];
+        if (!cd) continue;
+        const uint32_t a = (uint32_t)(cd & 0x7FFFFFFFu);
+        const uint32_t b = (uint32_t)((cd >> 31) & 0x7FFFFFFFu);
+        const bool full = (cd >> 62) == kKindFull;
+        const uint32_t sa = work.lds_mode ? atomicAdd(&base_t[a], 1u) : atomicAdd(&work.cursor[a], 1u);
+        write_record(w, work.recs, sa, p, q, a, full ? kRecFull : kRecHead);
+        if (!full) {
+            const uint32_t sb = work.lds_mode ? atomicAdd(&base_t[b], 1u) : atomicAdd(&work.cursor[b], 1u);
+            write_record(w, work.recs, sb, p, q, b, kRecTail);
         }
-        uint32_t la[kScatterRound], lb[kScatterRound];
-        uint64_t cds[kScatterRound];
-#pragma unroll
-        for (int k = 0; k < kScatterRound; ++k) {
-            const uint32_t q = base + k * kScatterThreads + threadIdx.x;
-            cds[k] = q < p.n ? code[q] : 0;
-            if (cds[k]) {
-                const uint32_t a = (uint32_t)(cds[k] & 0x7FFFFFFFu);
-                la[k] = atomicAdd(&cnt[a], 1u);
-                if (la[k] == 0) touched[atomicAdd(&ntouched, 1u)] = a;
-                if ((cds[k] >> 62) == kKindSplit) {
-                    const uint32_t b = (uint32_t)((cds[k] >> 31) & 0x7FFFFFFFu);
-                    lb[k] = atomicAdd(&cnt[b], 1u);
-                    if (lb[k] == 0) touched[atomicAdd(&ntouched, 1u)] = b;
-                }
-            }
-        }
-        __syncthreads();
-        const uint32_t nt = ntouched;
-        for (uint32_t i = threadIdx.x; i < nt; i += kScatterThreads) {
-            const uint32_t t = touched[i];
-            cnt[t] = atomicAdd(&cursor[t], cnt[t]);
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kScatterRound; ++k) {
-            if (!cds[k]) continue;
-            const uint32_t q = base + k * kScatterThreads + threadIdx.x;
-            const uint32_t a = (uint32_t)(cds[k] & 0x7FFFFFFFu);
-            if ((cds[k] >> 62) == kKindFull) {
-                write_record(recs, rw, cnt[a] + la[k], W, p, q, kRecFull);
-            } else {
-                const uint32_t b = (uint32_t)((cds[k] >> 31) & 0x7FFFFFFFu);
-                write_record(recs, rw, cnt[a] + la[k], W, p, q, kRecHead);
-                write_record(recs, rw, cnt[b] + lb[k], W, p, q, kRecTail);
-            }
-        }
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < nt; i += kScatterThreads) cnt[touched[i]] = 0;
-        if (threadIdx.x == 0) ntouched = 0;
-        __syncthreads();
     }
 }
 
-hipError_t launch_scatter(const WinView &w, const ProbeView &p, const uint64_t *code,
-                          uint32_t *cursor, uint64_t *recs, int grid, hipStream_t s)
+hipError_t launch_scatter(const WinView &w, const ProbeView &p, const ProbeWork &work,
+                          hipStream_t s)
 {
     if (p.n == 0) return hipSuccess;
-    int lds_agg = w.ntiles <= (uint32_t)kHistCap;
-    size_t lds = lds_agg ? (((size_t)w.ntiles + 3) & ~(size_t)3) * 4 +
-                               (size_t)2 * kScatterThreads * kScatterRound * 4
-                         : 16;
-    k_scatter<<<grid, kScatterThreads, lds, s>>>(w, p, code, cursor, recs, lds_agg);
+    size_t lds = work.lds_mode ? (size_t)w.ntiles * 4 : 16;
+    k_scatter<<<work.G, kLocateThreads, lds, s>>>(w, p, work);
     return hipGetLastError();
 }
 
 // ---- join: one workgroup per (tile, chunk of records) ----------------------
-// First row in [lo, hi) whose key compares >= key (LEQ=false) or > key
-// (LEQ=true); keys of the tile live in LDS as kw[j * T + i].
-template <bool UPPER>
-__device__ __forceinline__ uint32_t lds_bound(int W, const uint64_t *kw, uint32_t T, uint32_t lo,
-                                              uint32_t hi, uint64_t k0, uint64_t k1,
-                                              const uint64_t *kmem)
+// Key compare of a probe key (words 0,1 in registers, later words at
+// kmem[j]) with tile row `row` (LDS, word j at kw[j * T + row]):
+// sign(key - row).
+__device__ __forceinline__ int cmp_row(int W, const uint64_t *kw, uint32_t T, uint32_t row,
+                                       uint64_t k0, uint64_t k1, const uint64_t *kmem)
 {
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        // c = sign(key - row)
-        int c;
-        const uint64_t r0 = kw[mid];
-        if (k0 != r0)
-            c = k0 < r0 ? -1 : 1;
-        else if (W == 1)
-            c = 0;
-        else {
-            const uint64_t r1 = kw[T + mid];
-            if (k1 != r1)
-                c = k1 < r1 ? -1 : 1;
-            else {
-                c = 0;
-                for (int j = 2; j < W; ++j) {
-                    const uint64_t a = kmem[j], b = kw[(size_t)j * T + mid];
-                    if (a != b) {
-                        c = a < b ? -1 : 1;
-                        break;
-                    }
-                }
-            }
-        }
-        // lower bound: row < key -> go right;  upper bound: row <= key -> right
-        if (UPPER ? c >= 0 : c > 0)
-            lo = mid + 1;
-        else
-            hi = mid;
+    const uint64_t r0 = kw[row];
+    if (k0 != r0) return k0 < r0 ? -1 : 1;
+    if (W == 1) return 0;
+    const uint64_t r1 = kw[T + row];
+    if (k1 != r1) return k1 < r1 ? -1 : 1;
+    for (int j = 2; j < W; ++j) {
+        const uint64_t a = kmem[j], b = kw[(size_t)j * T + row];
+        if (a != b) return a < b ? -1 : 1;
     }
-    return lo;
+    return 0;
 }
 
-// Any lsn > snap in rows [p, q) of the tile (LDS), with 64-row block maxima.
-__device__ __forceinline__ bool lds_any_after(const uint64_t *lsn, const uint64_t *bmax, uint32_t p,
-                                              uint32_t q, uint64_t snap)
+// Any lsn > snap in [from, to) of a[] (to - from <= N), N independent LDS
+// reads (predicated), no dependent branch chain.
+template <int N>
+__device__ __forceinline__ bool any_gt(const uint64_t *a, uint32_t from, uint32_t to, uint64_t snap)
 {
-    const uint32_t bp = p >> 6, bq = (q - 1) >> 6;
-    if (bp == bq || q - p <= 96) {
-        for (uint32_t i = p; i < q; ++i)
-            if (lsn[i] > snap) return true;
-        return false;
+    bool r = false;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const uint32_t i = from + k;
+        const uint64_t v = a[i < to ? i : from];
+        r |= (i < to) & (v > snap);
     }
-    for (uint32_t i = p; i < (bp + 1) << 6; ++i)
-        if (lsn[i] > snap) return true;
-    for (uint32_t b = bp + 1; b < bq; ++b)
-        if (bmax[b] > snap) return true;
-    for (uint32_t i = bq << 6; i < q; ++i)
-        if (lsn[i] > snap) return true;
-    return false;
+    return r;
+}
+
+// Any lsn > snap in rows [p, q) (non-empty) of the tile, with 16- and
+// 256-row block maxima.
+__device__ __forceinline__ bool lds_any_after(const uint64_t *lsn, const uint64_t *b16,
+                                              const uint64_t *b256, uint32_t p, uint32_t q,
+                                              uint64_t snap)
+{
+    if (q - p <= 16) return any_gt<16>(lsn, p, q, snap);
+    const uint32_t p16 = (p + 15) & ~15u, q16 = q & ~15u;
+    if (any_gt<15>(lsn, p, p16, snap) || any_gt<15>(lsn, q16, q, snap)) return true;
+    const uint32_t bp = p16 >> 4, bq = q16 >> 4;  // 16-blocks [bp, bq)
+    const uint32_t bp256 = (bp + 15) & ~15u, bq256 = bq & ~15u;
+    if (bp256 > bq256) return any_gt<15>(b16, bp, bq, snap);  // no 256-boundary inside
+    return any_gt<15>(b16, bp, bp256, snap) || any_gt<15>(b16, bq256, bq, snap) ||
+           any_gt<8>(b256, bp256 >> 4, bq256 >> 4, snap);
 }
 
 template <int WT>  // key words if 1 or 2 (fast staging path), 0 = any
-__global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, const uint64_t *recs,
-                                                       const uint32_t *bucket_off,
-                                                       const uint32_t *item_off,
-                                                       const uint32_t *item_tile,
+__global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, ProbeWork work,
                                                        uint8_t *verdict)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const uint32_t item = blockIdx.x;
-    if (item >= item_off[w.ntiles]) return;
-    const uint32_t tile = item_tile[item];
-    const uint32_t rb = bucket_off[tile] + (item - item_off[tile]) * kJoinChunk;
-    const uint32_t re = min(rb + (uint32_t)kJoinChunk, bucket_off[tile + 1]);
+    if (item >= work.item_off[w.ntiles]) return;
+    const uint32_t tile = work.item_tile[item];
+    const uint32_t rb = work.bucket_off[tile] + (item - work.item_off[tile]) * kJoinChunk;
+    const uint32_t re = min(rb + (uint32_t)kJoinChunk, work.bucket_off[tile + 1]);
     const int W = WT > 0 ? WT : w.W;
+    const int rw = rec_words(W);
     const uint32_t T = 1u << w.log2T;
     const uint32_t ts = tile << w.log2T;
-    const uint32_t tn = min(T, w.n - ts);
 
     uint64_t *kw = (uint64_t *)smem;               // [W][T]
     uint64_t *lsn = kw + (size_t)W * T;            // [T]
-    uint64_t *bmax = lsn + T;                      // [T / 64]
+    uint64_t *b16 = lsn + T;                       // [T / 16]
+    uint64_t *b256 = b16 + T / 16;                 // [T / 256]
+
+    // records of this thread (kJoinChunk / kJoinThreads of them), fetched
+    // before the tile so their latency overlaps the staging
+    constexpr int kRec = kJoinChunk / kJoinThreads;
+    ulonglong2 tail[kRec];
+    ulonglong2 bnd[kRec][2];
+#pragma unroll
+    for (int k = 0; k < kRec; ++k) {
+        const uint32_t r = rb + k * kJoinThreads + threadIdx.x;
+        if (r < re) {
+            const uint64_t *rec = work.recs + (size_t)r * rw;
+            tail[k] = *(const ulonglong2 *)(rec + 2 * W);
+            if constexpr (WT == 2) {
+                bnd[k][0] = *(const ulonglong2 *)rec;
+                bnd[k][1] = *(const ulonglong2 *)(rec + 2);
+            } else if constexpr (WT == 1) {
+                bnd[k][0] = *(const ulonglong2 *)rec;  // lo0, hi0
+            }
+        }
+    }
+
     // stage the tile: every thread issues all of its 16-byte loads first and
     // only then writes LDS, so its loads are in flight together.  The window
     // arrays are padded to a whole number of tiles, so the loads need no
@@ -889,50 +945,82 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, const uint64_t
         }
     }
     __syncthreads();
-    const int wid = threadIdx.x >> 6, lane = lane_id();
-    for (uint32_t b = wid; b < (tn + 63) / 64; b += kJoinThreads / 64) {
-        const uint32_t i = b * 64 + lane;
-        uint64_t v = i < tn ? lsn[i] : 0;
-        v = wave_max_u64(v);
-        if (lane == 0) bmax[b] = v;
+    // block maxima: 16-row blocks, then 256-row blocks
+    if (threadIdx.x < T / 16) {
+        const ulonglong2 *src = (const ulonglong2 *)(lsn + 16 * threadIdx.x);
+        uint64_t m = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const ulonglong2 v = src[k];
+            m = v.x > m ? v.x : m;
+            m = v.y > m ? v.y : m;
+        }
+        b16[threadIdx.x] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x < T / 256) {
+        uint64_t m = 0;
+        for (int k = 0; k < 16; ++k) m = b16[16 * threadIdx.x + k] > m ? b16[16 * threadIdx.x + k] : m;
+        b256[threadIdx.x] = m;
     }
     __syncthreads();
 
-    const int rw = rec_words(W);
-    for (uint32_t r = rb + threadIdx.x; r < re; r += kJoinThreads) {
-        const uint64_t *rec = recs + (size_t)r * rw;
-        const ulonglong2 tail = *(const ulonglong2 *)(rec + 2 * W);
-        const uint64_t meta = tail.y;
-        const uint64_t snap = tail.x;
+#pragma unroll
+    for (int k = 0; k < kRec; ++k) {
+        const uint32_t r = rb + k * kJoinThreads + threadIdx.x;
+        if (r >= re) continue;
+        const uint64_t *rec = work.recs + (size_t)r * rw;
+        const uint64_t snap = tail[k].x, meta = tail[k].y;
         const uint32_t txn = (uint32_t)meta;
-        const uint32_t gk = (uint32_t)(meta >> 32);
-        const uint32_t g = gk & 0x3FFFFFFFu, kind = gk >> 30;
-        const uint32_t gs = w.gstart[g], ge = w.gend[g];
-        const uint32_t lb = gs > ts ? min(gs - ts, tn) : 0;
-        const uint32_t ub = ge > ts ? min(ge - ts, tn) : 0;
+        const uint32_t lb = (uint32_t)(meta >> 32) & 0xFFFu;
+        const uint32_t ub = (uint32_t)(meta >> 44) & 0xFFFu;
+        const uint32_t kind = (uint32_t)(meta >> 62);
         if (lb >= ub) continue;
-        uint32_t pp = lb, qq = ub;
-        if (kind != kRecTail)
-            pp = lds_bound<false>(W, kw, T, lb, ub, rec[0], W > 1 ? rec[1] : 0, rec);
-        if (kind != kRecHead)
-            qq = lds_bound<true>(W, kw, T, pp, ub, rec[W], W > 1 ? rec[W + 1] : 0, rec + W);
-        if (pp < qq && lds_any_after(lsn, bmax, pp, qq, snap)) verdict[txn] = 1;
+        uint64_t l0, l1, h0, h1;
+        if constexpr (WT == 2) {
+            l0 = bnd[k][0].x;
+            l1 = bnd[k][0].y;
+            h0 = bnd[k][1].x;
+            h1 = bnd[k][1].y;
+        } else if constexpr (WT == 1) {
+            l0 = bnd[k][0].x;
+            h0 = bnd[k][0].y;
+            l1 = h1 = 0;
+        } else {
+            l0 = rec[0];
+            l1 = W > 1 ? rec[1] : 0;
+            h0 = rec[W];
+            h1 = W > 1 ? rec[W + 1] : 0;
+        }
+        // lower bound of lo and upper bound of hi in [lb, ub), in lockstep
+        uint32_t alo = lb, ahi = kind == kRecTail ? lb : ub;
+        uint32_t blo = kind == kRecHead ? ub : lb, bhi = ub;
+        while (alo < ahi || blo < bhi) {
+            const uint32_t am = (alo + ahi) >> 1, bm = (blo + bhi) >> 1;
+            if (alo < ahi) {
+                if (cmp_row(W, kw, T, am, l0, l1, rec) > 0) alo = am + 1; else ahi = am;
+            }
+            if (blo < bhi) {
+                if (cmp_row(W, kw, T, bm, h0, h1, rec + W) >= 0) blo = bm + 1; else bhi = bm;
+            }
+        }
+        const uint32_t pp = alo, qq = blo;
+        if (pp < qq && lds_any_after(lsn, b16, b256, pp, qq, snap)) verdict[txn] = 1;
     }
 }
 
-hipError_t launch_join(const WinView &w, const uint64_t *recs, const uint32_t *bucket_off,
-                       const uint32_t *item_off, const uint32_t *item_tile, uint32_t max_items,
+hipError_t launch_join(const WinView &w, const ProbeWork &work, uint32_t max_items,
                        uint8_t *verdict, hipStream_t s)
 {
     if (max_items == 0 || w.n == 0) return hipSuccess;
     const size_t T = (size_t)1 << w.log2T;
-    const size_t lds = T * 8 * (size_t)w.W + T * 8 + (T / 64) * 8;
+    const size_t lds = T * 8 * (size_t)w.W + T * 8 + (T / 16) * 8 + 8 * 8;
     if (w.W == 1 && w.log2T == 11)
-        k_join<1><<<max_items, kJoinThreads, lds, s>>>(w, recs, bucket_off, item_off, item_tile, verdict);
+        k_join<1><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
     else if (w.W == 2 && w.log2T == 11)
-        k_join<2><<<max_items, kJoinThreads, lds, s>>>(w, recs, bucket_off, item_off, item_tile, verdict);
+        k_join<2><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
     else
-        k_join<0><<<max_items, kJoinThreads, lds, s>>>(w, recs, bucket_off, item_off, item_tile, verdict);
+        k_join<0><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
     return hipGetLastError();
 }
 
