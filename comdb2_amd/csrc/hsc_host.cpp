@@ -643,6 +643,8 @@ static WinView win_view(hsc_ctx *c)
     w.W = c->W;
     w.log2T = c->log2T;
     w.levels = c->levels;
+    w.gbits = 0;
+    while (w.gbits < 32 && ((size_t)1 << w.gbits) < c->groups.size()) w.gbits++;
     return w;
 }
 

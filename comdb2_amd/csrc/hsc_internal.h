@@ -20,7 +20,7 @@
 namespace hsc {
 
 constexpr int kMaxWords = 64;       // MAXKEYLEN 512 B (bbinc/cdb2_constants.h:33)
-constexpr int kTopCap = 5120;       // splitters held in LDS by the locate kernel
+constexpr int kTopCap = 6144;       // splitter prefixes held in LDS by the locate kernel
 constexpr int kLocateThreads = 512;
 constexpr int kMaxChunks = 512;     // probe chunks (locate / scatter workgroups)
 constexpr int kHistCap = 8192;      // tiles whose bucket counters fit in LDS
@@ -45,6 +45,7 @@ struct WinView {
     const uint64_t *sp_w;     // [W][ntiles] key words of each tile's first row
     uint32_t n, ntiles, ntables;
     int W, log2T, levels;
+    int gbits;                // bits of gid in a splitter prefix (key_prefix)
 };
 
 struct ProbeView {

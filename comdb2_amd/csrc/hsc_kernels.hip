@@ -475,53 +475,55 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
 // hist[g][t], so every record slot comes from an LDS atomic: no global
 // atomics, no contention across XCDs.
 
-// sign((sg, splitter words) - (g, key)) for tile t's first row; the
-// splitter's group and word 0 are given, later words come from sp_w.
-__device__ __forceinline__ int cmp_splitter(const WinView &w, uint32_t t, uint32_t sg,
-                                            uint64_t sw0, uint32_t g, uint64_t k0, uint64_t k1,
-                                            const uint64_t *kmem, size_t ks)
+// 64-bit prefix of a composite key (gid, w0, ...): gid in the top gbits,
+// then the top 64 - gbits bits of w0.  Prefix order agrees with composite
+// order wherever two prefixes differ; equal prefixes need the full compare.
+__device__ __forceinline__ uint64_t key_prefix(int gbits, uint32_t g, uint64_t w0)
 {
+    return gbits ? ((uint64_t)g << (64 - gbits)) | (w0 >> gbits) : w0;
+}
+
+// sign(full splitter of tile t - (g, key)), splitter read from sp_g / sp_w.
+__device__ __forceinline__ int cmp_splitter_full(const WinView &w, uint32_t t, uint32_t g,
+                                                 uint64_t k0, const uint64_t *kmem, size_t ks)
+{
+    const uint32_t sg = w.sp_g[t];
     if (sg != g) return sg < g ? -1 : 1;
-    if (sw0 != k0) return sw0 < k0 ? -1 : 1;
-    if (w.W == 1) return 0;
-    // words 1.. : sign(splitter - key) = -sign(key - splitter)
-    return -cmp_words(w.W - 1, k1, kmem + ks, ks, w.sp_w + w.ntiles + t, w.ntiles);
+    return -cmp_words(w.W, k0, kmem, ks, w.sp_w + t, w.ntiles);
 }
 
 // NS binary searches in lockstep over the splitters: out[i] = number of
-// tiles whose first row compares < key i (leq[i]: <=).  The LDS holds every
-// stride_t-th splitter; with stride_t > 1 a last step searches sp_g/sp_w.
+// tiles whose first row compares < key i (leq[i]: <=).  LDS holds the 64-bit
+// prefix of every stride_t-th splitter; ties and (stride_t > 1) the last
+// step go to sp_g / sp_w.
 template <int NS>
-__device__ __forceinline__ void count_splitters(const WinView &w, const uint64_t *top_w0,
-                                                const uint32_t *top_g, uint32_t ntop,
-                                                uint32_t stride_t, const uint32_t (&g)[NS],
-                                                const uint64_t (&k0)[NS], const uint64_t (&k1)[NS],
+__device__ __forceinline__ void count_splitters(const WinView &w, const uint64_t *top,
+                                                uint32_t ntop, uint32_t stride_t,
+                                                const uint32_t (&g)[NS],
+                                                const uint64_t (&k0)[NS],
                                                 const uint64_t *const (&kmem)[NS], size_t ks,
                                                 const bool (&leq)[NS], uint32_t (&out)[NS])
 {
     uint32_t lo[NS], hi[NS];
+    uint64_t pk[NS];
 #pragma unroll
     for (int i = 0; i < NS; ++i) {
         lo[i] = 0;
         hi[i] = ntop;
+        pk[i] = key_prefix(w.gbits, g[i], k0[i]);
     }
     for (;;) {
         bool any = false;
-        uint32_t sg[NS];
-        uint64_t sw[NS];
+        uint64_t sp[NS];
 #pragma unroll
-        for (int i = 0; i < NS; ++i) {
-            const uint32_t m = min((lo[i] + hi[i]) >> 1, ntop ? ntop - 1 : 0);
-            sg[i] = top_g[m];
-            sw[i] = top_w0[m];
-        }
+        for (int i = 0; i < NS; ++i) sp[i] = top[min((lo[i] + hi[i]) >> 1, ntop ? ntop - 1 : 0)];
 #pragma unroll
         for (int i = 0; i < NS; ++i) {
             if (lo[i] < hi[i]) {
                 any = true;
                 const uint32_t m = (lo[i] + hi[i]) >> 1;
-                const int c = cmp_splitter(w, m * stride_t, sg[i], sw[i], g[i], k0[i], k1[i],
-                                           kmem[i], ks);
+                const int c = sp[i] != pk[i] ? (sp[i] < pk[i] ? -1 : 1)
+                                             : cmp_splitter_full(w, m * stride_t, g[i], k0[i], kmem[i], ks);
                 if (leq[i] ? c <= 0 : c < 0)
                     lo[i] = m + 1;
                 else
@@ -540,7 +542,7 @@ __device__ __forceinline__ void count_splitters(const WinView &w, const uint64_t
         uint32_t L = (t - 1) * stride_t + 1, H = min(t * stride_t, w.ntiles);
         while (L < H) {
             const uint32_t m = (L + H) >> 1;
-            const int c = cmp_splitter(w, m, w.sp_g[m], w.sp_w[m], g[i], k0[i], k1[i], kmem[i], ks);
+            const int c = cmp_splitter_full(w, m, g[i], k0[i], kmem[i], ks);
             if (leq[i] ? c <= 0 : c < 0)
                 L = m + 1;
             else
@@ -566,9 +568,8 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate(WinView w, ProbeView 
                                                            uint32_t ntop, uint32_t stride_t)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint64_t *top_w0 = (uint64_t *)smem;
-    uint32_t *top_g = (uint32_t *)(top_w0 + ntop);
-    uint32_t *hist = top_g + ((ntop + 3) & ~3u);
+    uint64_t *top = (uint64_t *)smem;              // [ntop] splitter prefixes
+    uint32_t *hist = (uint32_t *)(top + ntop);     // [ntiles]
     // stage the splitters: loads in batches of 8 per thread before the stores
     for (uint32_t base = 0; base < ntop; base += 8 * kLocateThreads) {
         uint64_t vw[8];
@@ -584,10 +585,7 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate(WinView w, ProbeView 
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const uint32_t i = base + k * kLocateThreads + threadIdx.x;
-            if (i < ntop) {
-                top_w0[i] = vw[k];
-                top_g[i] = vg[k];
-            }
+            if (i < ntop) top[i] = key_prefix(w.gbits, vg[k], vw[k]);
         }
     }
     if (work.lds_mode)
@@ -602,7 +600,7 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate(WinView w, ProbeView 
         uint32_t qq[kLocateBatch];
         bool valid[kLocateBatch];
         uint32_t gg[NS];
-        uint64_t k0[NS], k1[NS];
+        uint64_t k0[NS];
         const uint64_t *km[NS];
         bool leq[NS];
         uint32_t cnt[NS];
@@ -615,14 +613,12 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate(WinView w, ProbeView 
             gg[2 * b] = gg[2 * b + 1] = g;
             k0[2 * b] = p.lo[q];
             k0[2 * b + 1] = p.hi[q];
-            k1[2 * b] = w.W > 1 ? p.lo[ks + q] : 0;
-            k1[2 * b + 1] = w.W > 1 ? p.hi[ks + q] : 0;
             km[2 * b] = p.lo + q;
             km[2 * b + 1] = p.hi + q;
             leq[2 * b] = false;
             leq[2 * b + 1] = true;
         }
-        count_splitters<NS>(w, top_w0, top_g, ntop, stride_t, gg, k0, k1, km, ks, leq, cnt);
+        count_splitters<NS>(w, top, ntop, stride_t, gg, k0, km, ks, leq, cnt);
 #pragma unroll
         for (int b = 0; b < kLocateBatch; ++b) {
             if (!valid[b]) continue;
@@ -678,62 +674,84 @@ hipError_t launch_locate(const WinView &w, const ProbeView &p, const ProbeWork &
         stride_t = (w.ntiles + kTopCap - 1) / kTopCap;
         ntop = (w.ntiles + stride_t - 1) / stride_t;
     }
-    size_t lds = (size_t)ntop * 8 + (((size_t)ntop + 3) & ~(size_t)3) * 4 +
-                 (work.lds_mode ? (size_t)w.ntiles * 4 : 0);
+    size_t lds = (size_t)ntop * 8 + (work.lds_mode ? (size_t)w.ntiles * 4 : 0);
     k_locate<<<work.G, kLocateThreads, lds, s>>>(w, p, work, verdict, ntop, stride_t);
     return hipGetLastError();
 }
 
 // ---- plan ------------------------------------------------------------------
-// Column scan of hist[G][ntiles]: hist[g][t] := sum over g' < g; counts[t] := total.
-__global__ __launch_bounds__(256) void k_colscan(ProbeWork work, uint32_t ntiles)
+// Column scan of hist[G][ntiles]: hist[g][t] := sum over g' < g; counts[t] :=
+// total.  A workgroup owns 64 tiles (one per lane: each row access is 256
+// contiguous bytes) and splits the G rows into 16 segments (one per wave);
+// each thread holds its segment's values in registers, so the scan is one
+// pass with every load in flight.
+constexpr int kColSegRows = kMaxChunks / 16;
+__global__ __launch_bounds__(1024) void k_colscan(ProbeWork work, uint32_t ntiles)
 {
-    const uint32_t t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= ntiles) return;
+    __shared__ uint32_t segtot[16][64];
+    const int lane = lane_id(), seg = threadIdx.x >> 6;
+    const uint32_t t = blockIdx.x * 64 + lane;
+    const uint32_t per = (work.G + 15) / 16;
+    const uint32_t g0 = seg * per;
+    uint32_t v[kColSegRows];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kColSegRows; ++k) {
+        const uint32_t g = g0 + k;
+        v[k] = (k < (int)per && g < work.G && t < ntiles) ? work.hist[(size_t)g * ntiles + t] : 0;
+        sum += v[k];
+    }
+    segtot[seg][lane] = sum;
+    __syncthreads();
     uint32_t run = 0;
-    for (uint32_t g0 = 0; g0 < work.G; g0 += 8) {
-        uint32_t v[8];
+    for (int j = 0; j < seg; ++j) run += segtot[j][lane];
+    if (t < ntiles) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            v[k] = (g0 + k < work.G) ? work.hist[(size_t)(g0 + k) * ntiles + t] : 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            if (g0 + k < work.G) work.hist[(size_t)(g0 + k) * ntiles + t] = run;
+        for (int k = 0; k < kColSegRows; ++k) {
+            const uint32_t g = g0 + k;
+            if (k < (int)per && g < work.G) work.hist[(size_t)g * ntiles + t] = run;
             run += v[k];
         }
+        if (seg == 15) work.counts[t] = run;
     }
-    work.counts[t] = run;
 }
 
 // One workgroup: bucket offsets, per-tile chunk counts, item -> tile table.
+// Each thread owns 8 consecutive tiles per 8192-tile round.
 __global__ __launch_bounds__(1024) void k_plan(ProbeWork work, uint32_t ntiles)
 {
     __shared__ uint32_t lds[16];
     uint32_t carry_b = 0, carry_i = 0;
     for (uint32_t base = 0; base < ntiles; base += 8 * 1024) {
-        uint32_t cv[8];
+        const uint32_t t0 = base + 8 * threadIdx.x;
+        uint32_t cv[8], ch[8], sb = 0, si = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) cv[k] = t0 + k < ntiles ? work.counts[t0 + k] : 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const uint32_t t = base + k * 1024 + threadIdx.x;
-            cv[k] = t < ntiles ? work.counts[t] : 0;
+            ch[k] = (cv[k] + kJoinChunk - 1) / kJoinChunk;
+            sb += cv[k];
+            si += ch[k];
         }
+        uint32_t tb, ti;
+        uint32_t pb = block_excl_scan<1024>(sb, lds, tb);
+        uint32_t pi = block_excl_scan<1024>(si, lds, ti);
+        pb += carry_b;
+        pi += carry_i;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const uint32_t t = base + k * 1024 + threadIdx.x;
-            const uint32_t c = cv[k];
-            const uint32_t ch = (c + kJoinChunk - 1) / kJoinChunk;
-            uint32_t tb, ti;
-            const uint32_t pb = block_excl_scan<1024>(c, lds, tb);
-            const uint32_t pi = block_excl_scan<1024>(ch, lds, ti);
+            const uint32_t t = t0 + k;
             if (t < ntiles) {
-                work.bucket_off[t] = carry_b + pb;
-                work.cursor[t] = carry_b + pb;
-                work.item_off[t] = carry_i + pi;
-                for (uint32_t j = 0; j < ch; ++j) work.item_tile[carry_i + pi + j] = t;
+                work.bucket_off[t] = pb;
+                work.cursor[t] = pb;
+                work.item_off[t] = pi;
+                for (uint32_t j = 0; j < ch[k]; ++j) work.item_tile[pi + j] = t;
             }
-            carry_b += tb;
-            carry_i += ti;
+            pb += cv[k];
+            pi += ch[k];
         }
+        carry_b += tb;
+        carry_i += ti;
     }
     if (threadIdx.x == 0) {
         work.bucket_off[ntiles] = carry_b;
@@ -743,7 +761,7 @@ __global__ __launch_bounds__(1024) void k_plan(ProbeWork work, uint32_t ntiles)
 
 hipError_t launch_plan(const WinView &w, const ProbeWork &work, hipStream_t s)
 {
-    if (work.lds_mode) k_colscan<<<(w.ntiles + 255) / 256, 256, 0, s>>>(work, w.ntiles);
+    if (work.lds_mode) k_colscan<<<(w.ntiles + 63) / 64, 1024, 0, s>>>(work, w.ntiles);
     k_plan<<<1, 1024, 0, s>>>(work, w.ntiles);
     return hipGetLastError();
 }
@@ -800,17 +818,29 @@ __global__ __launch_bounds__(kLocateThreads) void k_scatter(WinView w, ProbeView
     }
     const uint32_t c0 = blockIdx.x * work.chunk;
     const uint32_t c1 = min(p.n, c0 + work.chunk);
-    for (uint32_t q = c0 + threadIdx.x; q < c1; q += kLocateThreads) {
-        const uint64_t cd = work.code[q];
-        if (!cd) continue;
-        const uint32_t a = (uint32_t)(cd & 0x7FFFFFFFu);
-        const uint32_t b = (uint32_t)((cd >> 31) & 0x7FFFFFFFu);
-        const bool full = (cd >> 62) == kKindFull;
-        const uint32_t sa = work.lds_mode ? atomicAdd(&base_t[a], 1u) : atomicAdd(&work.cursor[a], 1u);
-        write_record(w, work.recs, sa, p, q, a, full ? kRecFull : kRecHead);
-        if (!full) {
-            const uint32_t sb = work.lds_mode ? atomicAdd(&base_t[b], 1u) : atomicAdd(&work.cursor[b], 1u);
-            write_record(w, work.recs, sb, p, q, b, kRecTail);
+    constexpr int B = 4;
+    for (uint32_t base = c0; base < c1; base += B * kLocateThreads) {
+        uint64_t cd[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const uint32_t q = base + k * kLocateThreads + threadIdx.x;
+            cd[k] = q < c1 ? work.code[q] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            if (!cd[k]) continue;
+            const uint32_t q = base + k * kLocateThreads + threadIdx.x;
+            const uint32_t a = (uint32_t)(cd[k] & 0x7FFFFFFFu);
+            const uint32_t b = (uint32_t)((cd[k] >> 31) & 0x7FFFFFFFu);
+            const bool full = (cd[k] >> 62) == kKindFull;
+            const uint32_t sa =
+                work.lds_mode ? atomicAdd(&base_t[a], 1u) : atomicAdd(&work.cursor[a], 1u);
+            write_record(w, work.recs, sa, p, q, a, full ? kRecFull : kRecHead);
+            if (!full) {
+                const uint32_t sb =
+                    work.lds_mode ? atomicAdd(&base_t[b], 1u) : atomicAdd(&work.cursor[b], 1u);
+                write_record(w, work.recs, sb, p, q, b, kRecTail);
+            }
         }
     }
 }

@@ -22,4 +22,5 @@ run() {
 [[ $PASSES == *kt* ]] && run kt rocprofv3 --kernel-trace --stats -T --output-format csv -d gpurun_out/prof_${TAG}_kt -o run -- python3 bench.py $ARGS
 [[ $PASSES == *fetch* ]] && run fetch rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d gpurun_out/prof_${TAG}_fetch -o run -- python3 bench.py $ARGS
 [[ $PASSES == *write* ]] && run write rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d gpurun_out/prof_${TAG}_write -o run -- python3 bench.py $ARGS
+[[ $PASSES == *sq* ]] && run sq rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAVES -T --output-format csv -d gpurun_out/prof_${TAG}_sq -o run -- python3 bench.py $ARGS
 exit 0
