@@ -68,6 +68,7 @@ inline uint64_t ixkey(int tid, int ix) { return ((uint64_t)(uint32_t)tid << 32) 
 
 struct hsc_ctx {
     int device = 0;
+    bool host_only = false;
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
     std::string err;
@@ -327,6 +328,10 @@ static int build_from_host(hsc_ctx *c)
 
 static int ensure_built(hsc_ctx *c)
 {
+    if (c->host_only) {  // dictionaries + marshalling only
+        c->W = window_words(c);
+        return HSC_OK;
+    }
     if (!c->dirty) return HSC_OK;
     if (!c->host_staged) return fail(c, HSC_ESTATE, "device window must be re-ingested");
     return build_from_host(c);
@@ -650,6 +655,7 @@ static WinView win_view(hsc_ctx *c)
 
 static int probe(hsc_ctx *c, const hsc_probe_batch *b)
 {
+    if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
     hipStream_t s = c->stream;
     const WinView w = win_view(c);
     if (b->n > 0xFFFFFFFFull / 2 || b->n_lock > 0xFFFFFFFFull || b->n_txn > 0xFFFFFFFFull)
@@ -736,6 +742,7 @@ static int collect_timing(hsc_ctx *c)
 // Upload the marshalled batch, run the join, read back per-txn verdicts.
 static int run_marshalled(hsc_ctx *c, int *rc_out)
 {
+    if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
     hipStream_t s = c->stream;
     const hsc_marshalled &m = c->m;
     const int W = c->W;
@@ -800,6 +807,14 @@ int hsc_ctx_create(int device, hsc_ctx **out)
 {
     if (!out) return HSC_EINVAL;
     *out = nullptr;
+    if (device == -1) {
+        hsc_ctx *c = new (std::nothrow) hsc_ctx();
+        if (!c) return HSC_ENOMEM;
+        c->device = -1;
+        c->host_only = true;
+        *out = c;
+        return HSC_OK;
+    }
     int n = hsc_device_count();
     if (device < 0 || device >= n) return HSC_EDEVICE;
     if (hipSetDevice(device) != hipSuccess) return HSC_EDEVICE;
@@ -818,7 +833,11 @@ int hsc_ctx_create(int device, hsc_ctx **out)
 void hsc_ctx_destroy(hsc_ctx *c)
 {
     if (!c) return;
-    (void)hipSetDevice(c->device);
+    if (c->host_only) {
+        delete c;
+        return;
+    }
+    if (!c->host_only) (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     DBuf *bufs[] = {&c->d_gid, &c->d_words, &c->d_lsn, &c->d_gid2, &c->d_words2, &c->d_lsn2,
                     &c->d_flags, &c->d_scratch, &c->d_gstart, &c->d_gend, &c->d_tmax,
@@ -837,6 +856,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
 int hsc_set_stream(hsc_ctx *c, void *st)
 {
     if (!c) return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
     c->stream = st ? (hipStream_t)st : c->own_stream;
     return HSC_OK;
 }
@@ -856,7 +876,7 @@ int hsc_window_ingest_log(hsc_ctx *c, const hsc_llog *log)
 {
     if (!c || !log) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    if (!c->host_only) (void)hipSetDevice(c->device);
     int rc = ingest_log(c, log);
     if (rc) return rc;
     return ensure_built(c);
@@ -891,7 +911,7 @@ int hsc_window_build(hsc_ctx *c)
 {
     if (!c) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    if (!c->host_only) (void)hipSetDevice(c->device);
     return ensure_built(c);
 }
 
@@ -906,11 +926,12 @@ int hsc_register_group(hsc_ctx *c, const char *tbname, int idxnum, int keylen)
 int hsc_window_ingest_device(hsc_ctx *c, size_t n, int words, const uint32_t *gid,
                              const uint64_t *key_words, const uint64_t *lsn, uint64_t end_lsn)
 {
+    if (c && c->host_only) return HSC_EDEVICE;
     if (!c || words < 1 || words > kMaxWords || (n && (!gid || !key_words || !lsn)))
         return HSC_EINVAL;
     if (n >= 0xFFFFFFFFull) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    if (!c->host_only) (void)hipSetDevice(c->device);
     clear_window(c);
     c->host_staged = false;
     c->end_lsn = end_lsn;
@@ -946,11 +967,45 @@ int hsc_table_id(hsc_ctx *c, const char *tbname)
     return it == c->table_ids.end() ? -1 : it->second;
 }
 
+int hsc_group_info(hsc_ctx *c, int gid, int *table_id, int *idxnum, int *keylen)
+{
+    if (!c || gid < 0 || gid >= (int)c->groups.size()) return HSC_EINVAL;
+    if (table_id) *table_id = c->groups[gid].tid;
+    if (idxnum) *idxnum = c->groups[gid].ix;
+    if (keylen) *keylen = c->groups[gid].klen;
+    return HSC_OK;
+}
+
+int hsc_table_max(hsc_ctx *c, uint64_t *out, int n)
+{
+    if (!c || n < 0 || (n && !out)) return HSC_EINVAL;
+    const int nt = (int)c->table_names.size();
+    for (int t = 0; t < std::min(n, nt); ++t) out[t] = c->h_table_max[t];
+    return nt;
+}
+
+int hsc_merge_table_max(hsc_ctx *c, const uint64_t *in, int n)
+{
+    if (!c || n < 0 || (n && !in) || n > (int)c->table_names.size()) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    for (int t = 0; t < n; ++t) {
+        c->h_table_max[t] = std::max(c->h_table_max[t], in[t]);
+        c->max_commit = std::max(c->max_commit, in[t]);
+    }
+    if (!c->host_only && !c->dirty && n > 0) {
+        (void)hipSetDevice(c->device);
+        HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, c->h_table_max.data(), 8 * (size_t)n,
+                                 hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
+    return HSC_OK;
+}
+
 int hsc_marshal_readsets(hsc_ctx *c, const hsc_readsets *rs, const hsc_marshalled **out)
 {
     if (!c || !rs || !out) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    if (!c->host_only) (void)hipSetDevice(c->device);
     int rc = ensure_built(c);
     if (rc) return rc;
     rc = marshal_readsets(c, rs);
@@ -962,7 +1017,7 @@ int hsc_check_readsets(hsc_ctx *c, const hsc_readsets *rs, int *rc_out)
 {
     if (!c || !rs || (!rc_out && rs->ntxn)) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    if (!c->host_only) (void)hipSetDevice(c->device);
     int rc = ensure_built(c);
     if (!rc) rc = marshal_readsets(c, rs);
     if (!rc) rc = run_marshalled(c, rc_out);
@@ -977,7 +1032,7 @@ int hip_serial_check_batch(void *vctx, void *const *ranges, unsigned int *file,
     hsc_ctx *c = (hsc_ctx *)vctx;
     if (!c || n < 0 || (n && (!ranges || !rc_out)) || (!file) != (!offset)) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    if (!c->host_only) (void)hipSetDevice(c->device);
     int rc = ensure_built(c);
     if (rc) {
         for (int i = 0; i < n; ++i) rc_out[i] = 1;
@@ -1053,7 +1108,7 @@ int hsc_probe_device(hsc_ctx *c, const hsc_probe_batch *b)
 {
     if (!c || !b) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    if (!c->host_only) (void)hipSetDevice(c->device);
     if (c->dirty) return fail(c, HSC_ESTATE, "window not built");
     return probe(c, b);
 }
@@ -1061,8 +1116,9 @@ int hsc_probe_device(hsc_ctx *c, const hsc_probe_batch *b)
 int hsc_pack_verdicts(hsc_ctx *c, const uint8_t *verdict, size_t n_txn, uint64_t *bitmap)
 {
     if (!c || (n_txn && (!verdict || !bitmap)) || n_txn > 0xFFFFFFFFull) return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
     std::lock_guard<std::mutex> g(c->mu);
-    (void)hipSetDevice(c->device);
+    if (!c->host_only) (void)hipSetDevice(c->device);
     HIPCHK(c, launch_pack(verdict, (uint32_t)n_txn, bitmap, c->stream));
     return HSC_OK;
 }
@@ -1070,6 +1126,7 @@ int hsc_pack_verdicts(hsc_ctx *c, const uint8_t *verdict, size_t n_txn, uint64_t
 int hsc_synchronize(hsc_ctx *c)
 {
     if (!c) return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return collect_timing(c);
 }

@@ -91,6 +91,7 @@ EXPORTS = [
     "hsc_window_ingest_log", "hsc_window_append", "hsc_window_set_end", "hsc_window_reset",
     "hsc_window_build", "hsc_register_group", "hsc_window_ingest_device", "hsc_window_words",
     "hsc_window_keys", "hsc_window_end", "hsc_window_max_commit", "hsc_table_id",
+    "hsc_group_info", "hsc_table_max", "hsc_merge_table_max",
     "hip_bdb_osql_serial_check", "hip_serial_check_batch", "hsc_check_readsets",
     "hsc_marshal_readsets", "hsc_probe_device", "hsc_pack_verdicts", "hsc_synchronize",
     "hsc_get_timing",
@@ -128,6 +129,10 @@ def load() -> C.CDLL:
         "hsc_window_end": (C.c_uint64, [_p]),
         "hsc_window_max_commit": (C.c_uint64, [_p]),
         "hsc_table_id": (C.c_int, [_p, C.c_char_p]),
+        "hsc_group_info": (C.c_int, [_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                     C.POINTER(C.c_int)]),
+        "hsc_table_max": (C.c_int, [_p, _p, C.c_int]),
+        "hsc_merge_table_max": (C.c_int, [_p, _p, C.c_int]),
         "hip_bdb_osql_serial_check": (C.c_int, [_p, _p, C.POINTER(C.c_uint), C.POINTER(C.c_uint), C.c_int]),
         "hip_serial_check_batch": (C.c_int, [_p, C.POINTER(_p), C.POINTER(C.c_uint),
                                              C.POINTER(C.c_uint), C.c_int, C.c_int,
@@ -236,11 +241,12 @@ class CurRangeArrays:
 
 
 class Validator:
-    """One GPU's validator context (hsc_ctx)."""
+    """One GPU's validator context (hsc_ctx).  device=-1: host-only context
+    (log decode, dictionaries and marshalling; no checks)."""
 
     def __init__(self, device: int = 0):
         self.lib = load()
-        if self.lib.hsc_device_count() <= device:
+        if device != -1 and self.lib.hsc_device_count() <= device:
             raise HscError(f"no HIP device {device} visible")
         ctx = _p()
         rc = self.lib.hsc_ctx_create(device, C.byref(ctx))
@@ -330,6 +336,26 @@ class Validator:
                     txn=arr(m.txn, n, np.uint32), lock_table=arr(m.lock_table, nl, np.uint32),
                     lock_snap=arr(m.lock_snap, nl, np.uint64), lock_txn=arr(m.lock_txn, nl, np.uint32),
                     forced=arr(m.forced, nt, np.uint8))
+
+    def group_info(self, gid: int):
+        t, ix, kl = C.c_int(), C.c_int(), C.c_int()
+        self._chk(self.lib.hsc_group_info(self.ctx, gid, C.byref(t), C.byref(ix), C.byref(kl)),
+                  "hsc_group_info")
+        return t.value, ix.value, kl.value
+
+    def table_id(self, name: str) -> int:
+        return self.lib.hsc_table_id(self.ctx, name.encode())
+
+    def table_max(self) -> np.ndarray:
+        n = self.lib.hsc_table_max(self.ctx, None, 0)
+        out = np.zeros(max(1, n), dtype=np.uint64)
+        self.lib.hsc_table_max(self.ctx, out.ctypes.data, n)
+        return out[:n]
+
+    def merge_table_max(self, tm: np.ndarray) -> None:
+        tm = np.ascontiguousarray(tm, dtype=np.uint64)
+        self._chk(self.lib.hsc_merge_table_max(self.ctx, tm.ctypes.data, len(tm)),
+                  "hsc_merge_table_max")
 
     def probe_device(self, batch: ProbeBatch) -> None:
         self._chk(self.lib.hsc_probe_device(self.ctx, C.byref(batch)), "hsc_probe_device")

@@ -174,6 +174,8 @@ enum {
 };
 
 /* ---- context ------------------------------------------------------------ */
+/* device = -1 creates a host-only context: log decode, dictionaries and
+ * marshalling work; every device operation returns HSC_EDEVICE. */
 int hsc_ctx_create(int device, hsc_ctx **out);
 void hsc_ctx_destroy(hsc_ctx *ctx);
 /* Launch on this hipStream_t (NULL = the context's own stream). */
@@ -207,6 +209,13 @@ size_t hsc_window_keys(hsc_ctx *ctx);        /* distinct (group, key) rows   */
 uint64_t hsc_window_end(hsc_ctx *ctx);
 uint64_t hsc_window_max_commit(hsc_ctx *ctx);
 int hsc_table_id(hsc_ctx *ctx, const char *tbname); /* -1 if never written   */
+/* Key group gid -> (table id, index, key length); 0 or HSC_EINVAL. */
+int hsc_group_info(hsc_ctx *ctx, int gid, int *table_id, int *idxnum, int *keylen);
+/* Per-table max commit LSN (dta writes included): copies min(n, ntables)
+ * entries, returns ntables. */
+int hsc_table_max(hsc_ctx *ctx, uint64_t *out, int n);
+/* Max-merge per-table LSNs from other shards (multi-GPU lock probes). */
+int hsc_merge_table_max(hsc_ctx *ctx, const uint64_t *in, int n);
 
 /* ---- drop-in checks ----------------------------------------------------- */
 /* Exactly bdb_osql_serial_check (bdb/serializable.c:571-579) for one read set:
