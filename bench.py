@@ -30,50 +30,12 @@ METRIC = "serializable conflict checks/sec at 1–8 GPUs, % HBM roofline, vs hos
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 
-def shard_key_bounds(rank, world, value_bits, W):
-    """Key-word bounds [lo, hi] of rank's shard of int64 values."""
-    from comdb2_amd import formats as F
-
-    def words(v):
-        b = F.enc_int64(v) + bytes(8 * W - 9)
-        return [int.from_bytes(b[8 * j:8 * j + 8], "big") for j in range(W)]
-    return words(rank << value_bits), words(((rank + 1) << value_bits) - 1)
-
-
-def route_mask(m, lo_b, hi_b):
-    """Probes whose [lo, hi] overlaps the shard [lo_b, hi_b] (lexicographic on words)."""
-    W = m["words"]
-    lo, hi = m["lo"], m["hi"]
-
-    def leq(a_rows, b_vals):  # a <= b, a: [W][n] arrays, b: list of W ints
-        lt = np.zeros(a_rows.shape[1], dtype=bool)
-        eq = np.ones(a_rows.shape[1], dtype=bool)
-        for j in range(W):
-            bj = np.uint64(b_vals[j])
-            lt |= eq & (a_rows[j] < bj)
-            eq &= a_rows[j] == bj
-        return lt | eq
-
-    def geq(a_rows, b_vals):
-        gt = np.zeros(a_rows.shape[1], dtype=bool)
-        eq = np.ones(a_rows.shape[1], dtype=bool)
-        for j in range(W):
-            bj = np.uint64(b_vals[j])
-            gt |= eq & (a_rows[j] > bj)
-            eq &= a_rows[j] == bj
-        return gt | eq
-    return leq(lo, hi_b) & geq(hi, lo_b)
-
-
-def upload_batch(torch, dev, m, mask, T):
-    idx = np.nonzero(mask)[0]
+def upload_batch(torch, dev, m):
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
-    b = dict(lo=t(m["lo"][:, idx]), hi=t(m["hi"][:, idx]), gid=t(m["gid"][idx]),
-             snap=t(m["snap"][idx]), txn=t(m["txn"][idx]), n=len(idx),
-             lock_table=t(np.maximum(m["lock_table"], 0)), lock_snap=t(m["lock_snap"]),
-             lock_txn=t(m["lock_txn"]), n_lock=len(m["lock_table"]),
-             forced=m["forced"])
-    return b
+    return dict(lo=t(m["lo"]), hi=t(m["hi"]), gid=t(m["gid"]), snap=t(m["snap"]),
+                txn=t(m["txn"]), n=m["n"], lock_table=t(m["lock_table"]),
+                lock_snap=t(m["lock_snap"]), lock_txn=t(m["lock_txn"]), n_lock=m["n_lock"],
+                forced=m["forced"])
 
 
 def probe_struct(hsc, b, verdict, bitmap, T):
@@ -135,7 +97,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from comdb2_amd import hsc
+    from comdb2_amd import hsc, shard
     from comdb2_amd.workloads import SEED_CONFIG2, config2, config2_device_window
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -165,15 +127,18 @@ def main():
     ingest_ms = v.timing()["ingest_ms"]
     del tg, tw, tl
     W = v.words
-    lo_b, hi_b = shard_key_bounds(rank, world, value_bits, W)
+    shards = shard.KeyRangeShards.int64_uniform(world, value_bits, W)
+    if world > 1:  # lock probes see the table-wide max commit LSN
+        v.merge_table_max(shard.allreduce_table_max(v.table_max()))
     T = c2.readsets.ntxn
     for bi in range(args.batches):
         rs = c2.readsets if bi == 0 else config2(seed=SEED_CONFIG2 + 7919 * bi,
                                                  n_commits=args.n_commits, n_txn=args.n_txn,
                                                  rank=rank, world=world, build_log=False).readsets
         m = v.marshal(rs)
-        mask = route_mask(m, lo_b, hi_b) if world > 1 else np.ones(m["n"], dtype=bool)
-        batches.append(upload_batch(torch, dev, m, mask, T))
+        if world > 1:
+            m = shard.route(m, shards.range_mask(m, rank), shards.lock_mask(m, rank))
+        batches.append(upload_batch(torch, dev, m))
     verdict = torch.zeros(T, dtype=torch.uint8, device=dev)
     bitmap = torch.zeros((T + 63) // 64, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream()
@@ -183,7 +148,7 @@ def main():
     def step(k):
         v.probe_device(structs[k % len(structs)])
         if world > 1:
-            dist.all_reduce(verdict, op=dist.ReduceOp.MAX)
+            shard.merge_verdicts(verdict)
             v.pack_verdicts(verdict.data_ptr(), T, bitmap.data_ptr())
 
     for k in range(args.warmup):

@@ -967,6 +967,12 @@ int hsc_table_id(hsc_ctx *c, const char *tbname)
     return it == c->table_ids.end() ? -1 : it->second;
 }
 
+const char *hsc_table_name(hsc_ctx *c, int tid)
+{
+    if (!c || tid < 0 || tid >= (int)c->table_names.size()) return nullptr;
+    return c->table_names[tid].c_str();
+}
+
 int hsc_group_info(hsc_ctx *c, int gid, int *table_id, int *idxnum, int *keylen)
 {
     if (!c || gid < 0 || gid >= (int)c->groups.size()) return HSC_EINVAL;

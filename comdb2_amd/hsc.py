@@ -91,7 +91,7 @@ EXPORTS = [
     "hsc_window_ingest_log", "hsc_window_append", "hsc_window_set_end", "hsc_window_reset",
     "hsc_window_build", "hsc_register_group", "hsc_window_ingest_device", "hsc_window_words",
     "hsc_window_keys", "hsc_window_end", "hsc_window_max_commit", "hsc_table_id",
-    "hsc_group_info", "hsc_table_max", "hsc_merge_table_max",
+    "hsc_table_name", "hsc_group_info", "hsc_table_max", "hsc_merge_table_max",
     "hip_bdb_osql_serial_check", "hip_serial_check_batch", "hsc_check_readsets",
     "hsc_marshal_readsets", "hsc_probe_device", "hsc_pack_verdicts", "hsc_synchronize",
     "hsc_get_timing",
@@ -129,6 +129,7 @@ def load() -> C.CDLL:
         "hsc_window_end": (C.c_uint64, [_p]),
         "hsc_window_max_commit": (C.c_uint64, [_p]),
         "hsc_table_id": (C.c_int, [_p, C.c_char_p]),
+        "hsc_table_name": (C.c_char_p, [_p, C.c_int]),
         "hsc_group_info": (C.c_int, [_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                      C.POINTER(C.c_int)]),
         "hsc_table_max": (C.c_int, [_p, _p, C.c_int]),
@@ -342,6 +343,10 @@ class Validator:
         self._chk(self.lib.hsc_group_info(self.ctx, gid, C.byref(t), C.byref(ix), C.byref(kl)),
                   "hsc_group_info")
         return t.value, ix.value, kl.value
+
+    def table_name(self, tid: int):
+        r = self.lib.hsc_table_name(self.ctx, tid)
+        return None if r is None else r.decode()
 
     def table_id(self, name: str) -> int:
         return self.lib.hsc_table_id(self.ctx, name.encode())

@@ -209,6 +209,7 @@ size_t hsc_window_keys(hsc_ctx *ctx);        /* distinct (group, key) rows   */
 uint64_t hsc_window_end(hsc_ctx *ctx);
 uint64_t hsc_window_max_commit(hsc_ctx *ctx);
 int hsc_table_id(hsc_ctx *ctx, const char *tbname); /* -1 if never written   */
+const char *hsc_table_name(hsc_ctx *ctx, int table_id); /* NULL if unknown   */
 /* Key group gid -> (table id, index, key length); 0 or HSC_EINVAL. */
 int hsc_group_info(hsc_ctx *ctx, int gid, int *table_id, int *idxnum, int *keylen);
 /* Per-table max commit LSN (dta writes included): copies min(n, ntables)

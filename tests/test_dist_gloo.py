@@ -1,0 +1,123 @@
+"""CPU, world_size 2 over gloo: the sharded check (comdb2_amd/shard.py) --
+marshal the global batch, route probes to key-range / group shards, evaluate
+each shard's probes against only that shard's window, merge verdict bytes
+with all_reduce(MAX) -- must equal the unsharded oracle verdicts."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _merge_logs(logs):
+    from comdb2_amd.formats import LLog
+    keys, offs = [], []
+    base = 0
+    for lg in logs:
+        keys.append(lg.keys)
+        offs.append(lg.key_off + np.uint64(base))
+        base += len(lg.keys)
+    cat = lambda name: np.concatenate([getattr(lg, name) for lg in logs])
+    lsn = cat("lsn")
+    order = np.argsort(lsn, kind="stable")
+    pick = lambda a: a[order]
+    return LLog(pick(lsn), pick(cat("rectype")), pick(cat("prev")), pick(cat("isabort")),
+                pick(cat("table")), pick(cat("ix")), pick(np.concatenate(offs)),
+                pick(cat("keylen")), np.concatenate(keys), logs[0].tbnames,
+                max(int(lg.end_lsn) for lg in logs))
+
+
+def _worker(rank, world, port, mode, out_path):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+
+    from comdb2_amd import shard
+    from comdb2_amd.hsc import Validator
+    from comdb2_amd.workloads import config2, random_case
+    from probe_model import WindowModel, evaluate
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    v = Validator(-1)
+    if mode == "keyrange":
+        kw = dict(n_commits=1500, n_txn=300, value_bits=18, width=1 << 9, snap_recent=0.5)
+        shards_logs = [config2(rank=r, world=world, **kw).log for r in range(world)]
+        glog = _merge_logs(shards_logs)
+        rs = config2(rank=rank, world=world, build_log=False, **kw).readsets
+        v.ingest_log(glog)
+        m = v.marshal(rs)
+        sh = shard.KeyRangeShards.int64_uniform(world, kw["value_bits"], m["words"])
+        local = WindowModel(shards_logs[rank])
+    else:
+        glog, rs = random_case(77, n_commits=120, n_txn=80)
+        v.ingest_log(glog)
+        m = v.marshal(rs)
+        full = WindowModel(glog)
+        sizes = {}
+        gid = 0
+        while True:
+            try:
+                tid, ix, kl = v.group_info(gid)
+            except Exception:
+                break
+            sizes[gid] = len(full.groups.get((v.table_name(tid), ix, kl), ([], []))[0])
+            gid += 1
+        sh = shard.GroupShards(sizes, world)
+        mine = {(v.table_name(v.group_info(g)[0]),) + v.group_info(g)[1:]
+                for g, r in sh.owner.items() if r == rank}
+        local = WindowModel(glog, key_filter=lambda tb, ix, key: (tb, ix, len(key)) in mine)
+    # table maxima: each shard's own view, merged across ranks
+    names = sorted(local.table_max)
+    tm = np.array([local.table_max[n] for n in names], dtype=np.uint64)
+    merged_tm = shard.allreduce_table_max(tm)
+    sub = shard.route(m, sh.range_mask(m, rank), sh.lock_mask(m, rank))
+    verdict = evaluate(v, sub, local, table_max_by_name=dict(zip(names, merged_tm.tolist())))
+    t = torch.from_numpy(verdict.copy())
+    shard.merge_verdicts(t)
+    if rank == 0:
+        np.save(out_path, np.maximum(t.numpy(), m["forced"]))
+    dist.barrier()
+    dist.destroy_process_group()
+    v.close()
+
+
+def _run(mode, tmp_path):
+    import torch.multiprocessing as mp
+    out = str(tmp_path / f"verdict_{mode}.npy")
+    mp.start_processes(_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True,
+                       start_method="spawn")
+    return np.load(out)
+
+
+def test_keyrange_shards_match_oracle(tmp_path, oracle_mod):
+    from comdb2_amd.workloads import config2
+    got = _run("keyrange", tmp_path)
+    kw = dict(n_commits=1500, n_txn=300, value_bits=18, width=1 << 9, snap_recent=0.5)
+    logs = [config2(rank=r, world=2, **kw).log for r in range(2)]
+    glog = _merge_logs(logs)
+    rs = config2(rank=0, world=2, build_log=False, **kw).readsets
+    want, _, _ = oracle_mod.check(glog, rs, nthreads=8)
+    np.testing.assert_array_equal(got != 0, want != 0)
+    assert 0 < int((want != 0).sum()) < len(want)
+
+
+def test_group_shards_match_oracle(tmp_path, oracle_mod):
+    from comdb2_amd.workloads import random_case
+    got = _run("group", tmp_path)
+    glog, rs = random_case(77, n_commits=120, n_txn=80)
+    want, _, _ = oracle_mod.check(glog, rs)
+    np.testing.assert_array_equal(got != 0, want != 0)
