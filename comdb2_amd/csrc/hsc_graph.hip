@@ -1,0 +1,447 @@
+// hsc_graph.hip -- WR/WW/RW dependency graph + strongly connected components
+// on gfx950 (the Jepsen-style extension of the check).
+//
+// History: micro-ops (txn, key, read|write, observed writer) of committed
+// transactions, txn ids in commit order (a key's version order is the commit
+// order of its writers).  Edges (Adya):
+//   ww  w_i -> w_{i+1}                 consecutive writers of a key
+//   wr  writer(observed) -> reader
+//   rw  reader -> next writer after the observed version
+// Build: sort the writers by (key, txn) with the window's LSD radix sort,
+// emit edges with one thread per op (binary search of the next writer),
+// radix-sort (src, dst), merge duplicates (type bits OR-ed), and build CSR
+// (out-edges) and CSC (in-edges).
+// SCC: Orzan's colouring.  Per round every live node starts with colour =
+// its id; colours propagate forward along live edges (max) from a frontier
+// until stable; a node whose colour is still its own id is the largest
+// member of its SCC (every member reaches it), and a backward sweep over
+// in-edges restricted to that colour marks the SCC.  Marked nodes retire
+// with scc = colour.  In a dependency graph almost every edge goes forward in
+// commit order, so colours only move across stale-read (rw) windows and the
+// rounds are few.
+#include "hsc_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <utility>
+
+namespace hsc {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// writers of the history -> rows (gid 0, words (key, txn), lsn 0) at the
+// positions of an exclusive scan of the write flags
+__global__ void k_gather_writers(size_t nops, const uint32_t *txn, const uint64_t *key,
+                                 const uint8_t *is_write, const uint32_t *pos, uint32_t *gid,
+                                 uint64_t *words, uint64_t *lsn, size_t stride)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nops || !is_write[i]) return;
+    const uint32_t p = pos[i];
+    gid[p] = 0;
+    words[p] = key[i];
+    words[stride + p] = txn[i];
+    lsn[p] = 0;
+}
+
+__global__ void k_write_flags(size_t nops, const uint8_t *is_write, uint32_t *flags)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nops) flags[i] = is_write[i] ? 1u : 0u;
+}
+
+// Edge rows: word = src << 32 | dst, payload = type; invalid = ~0.
+// Slots [0, nu): ww of unique writer i -> i+1; slots nu + 2i, nu + 2i + 1:
+// wr / rw of op i.
+__global__ void k_edges_ww(uint32_t nu, const uint64_t *wkey, const uint64_t *wtxn,
+                           uint64_t *ew, uint64_t *et, uint32_t *eg)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nu) return;
+    uint64_t e = ~0ull;
+    if (i + 1 < nu && wkey[i] == wkey[i + 1]) e = (wtxn[i] << 32) | wtxn[i + 1];
+    ew[i] = e;
+    et[i] = kDepWW;
+    eg[i] = 0;
+}
+
+__global__ void k_edges_reads(size_t nops, const uint32_t *txn, const uint64_t *key,
+                              const uint8_t *is_write, const uint32_t *observed, uint32_t nu,
+                              const uint64_t *wkey, const uint64_t *wtxn, uint64_t *ew,
+                              uint64_t *et, uint32_t *eg)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nops) return;
+    uint64_t wr = ~0ull, rw = ~0ull;
+    if (!is_write[i]) {
+        const uint32_t r = txn[i], ob = observed[i];
+        const uint64_t k = key[i];
+        if (ob != kNone && ob != r) wr = ((uint64_t)ob << 32) | r;
+        // first writer (key, txn) > (k, ob), or >= (k, 0) for the initial version
+        uint32_t lo = 0, hi = nu;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            const uint64_t mk = wkey[mid], mt = wtxn[mid];
+            const bool before = mk < k || (mk == k && (ob == kNone ? false : mt <= ob));
+            if (before)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        if (lo < nu && wkey[lo] == k && wtxn[lo] != r) rw = ((uint64_t)r << 32) | wtxn[lo];
+    }
+    const size_t s = (size_t)nu + 2 * i;
+    ew[s] = wr;
+    et[s] = kDepWR;
+    eg[s] = 0;
+    ew[s + 1] = rw;
+    et[s + 1] = kDepRW;
+    eg[s + 1] = 0;
+}
+
+// Merge runs of equal edges (rows sorted, invalid ~0 rows at the end):
+// head flag for the scan, types OR-ed into the head.
+__global__ void k_edge_heads(size_t n, const uint64_t *ew, uint64_t *et, uint32_t *flags)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t e = ew[i];
+    const bool head = e != ~0ull && (i == 0 || ew[i - 1] != e);
+    flags[i] = head ? 1u : 0u;
+    if (head) {
+        uint64_t t = et[i];
+        for (size_t j = i + 1; j < n && ew[j] == e; ++j) t |= et[j];
+        et[i] = t;
+    }
+}
+
+__global__ void k_edge_compact(size_t n, const uint64_t *ew, const uint64_t *et,
+                               const uint32_t *pos, const uint32_t *flags_copy, uint32_t *src,
+                               uint32_t *dst, uint32_t *type, int swap)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flags_copy[i]) return;
+    const uint32_t p = pos[i];
+    const uint64_t e = ew[i];
+    const uint32_t a = (uint32_t)(e >> 32), b = (uint32_t)e;
+    src[p] = swap ? b : a;
+    dst[p] = swap ? a : b;
+    if (type) type[p] = (uint32_t)et[i];
+}
+
+// off[v] = first edge whose key (sorted) is >= v, for v in [0, n]
+__global__ void k_csr_offsets(size_t ne, const uint32_t *key, uint32_t nnodes, uint32_t *off)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > ne) return;
+    const uint32_t cur = i < ne ? key[i] : nnodes;
+    const uint32_t prev = i == 0 ? 0 : key[i - 1] + 1;
+    if (i == 0)
+        for (uint32_t v = 0; v <= cur && v <= nnodes; ++v) off[v] = 0;
+    else
+        for (uint32_t v = prev; v <= cur && v <= nnodes; ++v) off[v] = (uint32_t)i;
+    if (i == ne)
+        for (uint32_t v = cur; v <= nnodes; ++v) off[v] = (uint32_t)ne;
+}
+
+// ---- colouring SCC ----------------------------------------------------------
+__global__ void k_scc_init(uint32_t n, uint32_t *scc, uint32_t *active)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    scc[v] = kNone;
+    active[v] = 1;
+}
+
+// colour = id; frontier = live nodes with a live out-edge to a smaller id
+__global__ void k_color_init(uint32_t n, const uint32_t *out_off, const uint32_t *out_dst,
+                             const uint32_t *active, uint32_t *color, uint32_t *front,
+                             uint32_t *nfront)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n) return;
+    if (!active[v]) return;
+    color[v] = v;
+    bool back = false;
+    for (uint32_t e = out_off[v]; e < out_off[v + 1] && !back; ++e) {
+        const uint32_t u = out_dst[e];
+        back = u < v && active[u];
+    }
+    if (back) front[atomicAdd(nfront, 1u)] = v;
+}
+
+__global__ void k_color_step(const uint32_t *front, uint32_t nf, const uint32_t *out_off,
+                             const uint32_t *out_dst, const uint32_t *active, uint32_t *color,
+                             uint32_t *next, uint32_t *nnext)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nf) return;
+    const uint32_t v = front[k];
+    const uint32_t cv = __hip_atomic_load(&color[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t e = out_off[v]; e < out_off[v + 1]; ++e) {
+        const uint32_t u = out_dst[e];
+        if (!active[u]) continue;
+        if (__hip_atomic_load(&color[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= cv) continue;
+        const uint32_t old = atomicMax(&color[u], cv);
+        if (old < cv) next[atomicAdd(nnext, 1u)] = u;
+    }
+}
+
+// roots (colour == id) start the backward sweep
+__global__ void k_bw_init(uint32_t n, const uint32_t *active, const uint32_t *color,
+                          uint32_t *mark, uint32_t *front, uint32_t *nfront)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n || !active[v]) return;
+    if (color[v] == v) {
+        mark[v] = 1;
+        front[atomicAdd(nfront, 1u)] = v;
+    }
+}
+
+__global__ void k_bw_step(const uint32_t *front, uint32_t nf, const uint32_t *in_off,
+                          const uint32_t *in_src, const uint32_t *active, const uint32_t *color,
+                          uint32_t *mark, uint32_t *next, uint32_t *nnext)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nf) return;
+    const uint32_t x = front[k];
+    const uint32_t c = color[x];
+    for (uint32_t e = in_off[x]; e < in_off[x + 1]; ++e) {
+        const uint32_t w = in_src[e];
+        if (!active[w] || color[w] != c) continue;
+        if (__hip_atomic_load(&mark[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) continue;
+        if (atomicExch(&mark[w], 1u) == 0) next[atomicAdd(nnext, 1u)] = w;
+    }
+}
+
+__global__ void k_finalize(uint32_t n, uint32_t *active, const uint32_t *color, uint32_t *mark,
+                           uint32_t *scc, uint32_t *remaining)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n || !active[v]) return;
+    if (mark[v]) {
+        scc[v] = color[v];
+        active[v] = 0;
+        mark[v] = 0;
+    } else {
+        atomicAdd(remaining, 1u);
+    }
+}
+
+static inline unsigned blocks(size_t n) { return (unsigned)((n + 255) / 256); }
+
+hipError_t graph_build(const GraphInput &in, GraphBufs &g, hipStream_t s)
+{
+    hipError_t e = hipSuccess;
+#define CK(x)                                 \
+    do {                                      \
+        e = (x);                              \
+        if (e != hipSuccess) return e;        \
+    } while (0)
+    const size_t nops = in.nops;
+    // 1. writers -> unique sorted (key, txn)
+    CK(g.flags.ensure(4 * (nops + 1)));
+    CK(g.scratch.ensure(std::max(scan_scratch_bytes(nops + 1), (size_t)1024)));
+    if (nops) k_write_flags<<<blocks(nops), 256, 0, s>>>(nops, in.is_write, g.flags.as<uint32_t>());
+    CK(hipMemsetAsync(g.flags.as<uint32_t>() + nops, 0, 4, s));
+    CK(scan_exclusive_u32(g.flags.as<uint32_t>(), nops + 1, g.scratch.as<uint32_t>(), s));
+    uint32_t nw = 0;
+    CK(hipMemcpyAsync(&nw, g.flags.as<uint32_t>() + nops, 4, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    const size_t wcap = std::max<size_t>(64, (nw + 63) & ~(size_t)63);
+    CK(g.wg.ensure(4 * wcap));
+    CK(g.ww.ensure(16 * wcap));
+    CK(g.wl.ensure(8 * wcap));
+    CK(g.wg2.ensure(4 * wcap));
+    CK(g.ww2.ensure(16 * wcap));
+    CK(g.wl2.ensure(8 * wcap));
+    if (nops)
+        k_gather_writers<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write,
+                                                      g.flags.as<uint32_t>(), g.wg.as<uint32_t>(),
+                                                      g.ww.as<uint64_t>(), g.wl.as<uint64_t>(), wcap);
+    CK(hipGetLastError());
+    size_t rsb = std::max(radix_scratch_bytes(nw, 2), scan_scratch_bytes(nw) + 64);
+    CK(g.scratch.ensure(rsb));
+    bool alt = false;
+    CK(radix_sort_rows(2, nw, g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), g.wl.as<uint64_t>(), wcap,
+                       g.wg2.as<uint32_t>(), g.ww2.as<uint64_t>(), g.wl2.as<uint64_t>(),
+                       g.scratch.p, g.scratch.bytes, &alt, s));
+    DBuf *sg = alt ? &g.wg2 : &g.wg, *sw = alt ? &g.ww2 : &g.ww, *sl = alt ? &g.wl2 : &g.wl;
+    DBuf *dg = alt ? &g.wg : &g.wg2, *dw = alt ? &g.ww : &g.ww2, *dl = alt ? &g.wl : &g.wl2;
+    CK(g.flags.ensure(4 * (wcap + 64)));
+    CK(g.count.ensure(64));
+    CK(dedupe_rows(2, nw, sg->as<uint32_t>(), sw->as<uint64_t>(), sl->as<uint64_t>(), wcap,
+                   dg->as<uint32_t>(), dw->as<uint64_t>(), dl->as<uint64_t>(), wcap,
+                   g.flags.as<uint32_t>(), g.scratch.p, g.scratch.bytes, g.count.as<uint32_t>(), s));
+    uint32_t nu = 0;
+    CK(hipMemcpyAsync(&nu, g.count.p, 4, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    if (!nw) nu = 0;
+    const uint64_t *wkey = dw->as<uint64_t>(), *wtxn = dw->as<uint64_t>() + wcap;
+    // 2. edges
+    const size_t ne_raw = (size_t)nu + 2 * nops;
+    const size_t ecap = std::max<size_t>(64, (ne_raw + 63) & ~(size_t)63);
+    CK(g.ew.ensure(8 * ecap));
+    CK(g.et.ensure(8 * ecap));
+    CK(g.eg.ensure(4 * ecap));
+    CK(g.ew2.ensure(8 * ecap));
+    CK(g.et2.ensure(8 * ecap));
+    CK(g.eg2.ensure(4 * ecap));
+    if (nu) k_edges_ww<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, g.ew.as<uint64_t>(),
+                                                   g.et.as<uint64_t>(), g.eg.as<uint32_t>());
+    if (nops)
+        k_edges_reads<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed,
+                                                   nu, wkey, wtxn, g.ew.as<uint64_t>(),
+                                                   g.et.as<uint64_t>(), g.eg.as<uint32_t>());
+    CK(hipGetLastError());
+    // 3. sort by (src, dst), merge, compact: out-edges; then (dst, src): in-edges
+    for (int pass = 0; pass < 2; ++pass) {
+        DBuf *ew = &g.ew, *et = &g.et, *eg = &g.eg;
+        if (pass == 1) {  // rebuild rows keyed (dst, src) from the compacted out-edges
+            CK(hipMemcpyAsync(g.ew.p, g.swap_rows.p, 8 * g.ne, hipMemcpyDeviceToDevice, s));
+            CK(hipMemsetAsync(g.et.p, 0, 8 * g.ne, s));
+            CK(hipMemsetAsync(g.eg.p, 0, 4 * g.ne, s));
+        }
+        const size_t n = pass == 0 ? ne_raw : g.ne;
+        CK(g.scratch.ensure(std::max(radix_scratch_bytes(n, 1), scan_scratch_bytes(n + 1) + 64)));
+        bool a2 = false;
+        CK(radix_sort_rows(1, n, eg->as<uint32_t>(), ew->as<uint64_t>(), et->as<uint64_t>(), ecap,
+                           g.eg2.as<uint32_t>(), g.ew2.as<uint64_t>(), g.et2.as<uint64_t>(),
+                           g.scratch.p, g.scratch.bytes, &a2, s));
+        const uint64_t *rw = a2 ? g.ew2.as<uint64_t>() : g.ew.as<uint64_t>();
+        uint64_t *rt = a2 ? g.et2.as<uint64_t>() : g.et.as<uint64_t>();
+        CK(g.flags.ensure(4 * (n + 64)));
+        CK(g.flags2.ensure(4 * (n + 64)));
+        if (n) k_edge_heads<<<blocks(n), 256, 0, s>>>(n, rw, rt, g.flags.as<uint32_t>());
+        CK(hipMemsetAsync(g.flags.as<uint32_t>() + n, 0, 4, s));
+        CK(hipMemcpyAsync(g.flags2.p, g.flags.p, 4 * (n + 1), hipMemcpyDeviceToDevice, s));
+        CK(scan_exclusive_u32(g.flags.as<uint32_t>(), n + 1, g.scratch.as<uint32_t>(), s));
+        uint32_t m = 0;
+        CK(hipMemcpyAsync(&m, g.flags.as<uint32_t>() + n, 4, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        if (pass == 0) {
+            g.ne = m;
+            CK(g.out_dst.ensure(4 * ((size_t)m + 1)));
+            CK(g.src.ensure(4 * ((size_t)m + 1)));
+            CK(g.type.ensure(4 * ((size_t)m + 1)));
+            if (n)
+                k_edge_compact<<<blocks(n), 256, 0, s>>>(n, rw, rt, g.flags.as<uint32_t>(),
+                                                         g.flags2.as<uint32_t>(), g.src.as<uint32_t>(),
+                                                         g.out_dst.as<uint32_t>(), g.type.as<uint32_t>(), 0);
+            // rows for the in-edge pass: dst << 32 | src
+            CK(g.swap_rows.ensure(8 * ((size_t)m + 1)));
+            CK(swap_edge_words(m, g.src.as<uint32_t>(), g.out_dst.as<uint32_t>(),
+                               g.swap_rows.as<uint64_t>(), s));
+        } else {
+            CK(g.in_src.ensure(4 * ((size_t)m + 1)));
+            CK(g.in_dst.ensure(4 * ((size_t)m + 1)));
+            if (n)
+                k_edge_compact<<<blocks(n), 256, 0, s>>>(n, rw, rt, g.flags.as<uint32_t>(),
+                                                         g.flags2.as<uint32_t>(), g.in_src.as<uint32_t>(),
+                                                         g.in_dst.as<uint32_t>(), nullptr, 1);
+        }
+        CK(hipGetLastError());
+    }
+    // 4. CSR / CSC offsets
+    const uint32_t nn = in.ntxn;
+    CK(g.out_off.ensure(4 * ((size_t)nn + 1)));
+    CK(g.in_off.ensure(4 * ((size_t)nn + 1)));
+    k_csr_offsets<<<blocks(g.ne + 1), 256, 0, s>>>(g.ne, g.src.as<uint32_t>(), nn, g.out_off.as<uint32_t>());
+    k_csr_offsets<<<blocks(g.ne + 1), 256, 0, s>>>(g.ne, g.in_dst.as<uint32_t>(), nn, g.in_off.as<uint32_t>());
+    CK(hipGetLastError());
+#undef CK
+    return hipSuccess;
+}
+
+__global__ void k_swap_words(uint32_t m, const uint32_t *src, const uint32_t *dst, uint64_t *rows)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) rows[i] = ((uint64_t)dst[i] << 32) | src[i];
+}
+
+hipError_t swap_edge_words(uint32_t m, const uint32_t *src, const uint32_t *dst, uint64_t *rows,
+                           hipStream_t s)
+{
+    if (m) k_swap_words<<<blocks(m), 256, 0, s>>>(m, src, dst, rows);
+    return hipGetLastError();
+}
+
+hipError_t graph_scc(uint32_t nn, GraphBufs &g, uint32_t *rounds, uint32_t *iterations,
+                     hipStream_t s)
+{
+    hipError_t e = hipSuccess;
+#define CK(x)                                 \
+    do {                                      \
+        e = (x);                              \
+        if (e != hipSuccess) return e;        \
+    } while (0)
+    *rounds = *iterations = 0;
+    if (nn == 0) return hipSuccess;
+    CK(g.scc.ensure(4 * (size_t)nn));
+    CK(g.active.ensure(4 * (size_t)nn));
+    CK(g.color.ensure(4 * (size_t)nn));
+    CK(g.mark.ensure(4 * (size_t)nn));
+    CK(g.front.ensure(4 * (size_t)nn + 64));
+    CK(g.front2.ensure(4 * (size_t)nn + 64));
+    CK(g.count.ensure(64));
+    CK(hipMemsetAsync(g.mark.p, 0, 4 * (size_t)nn, s));
+    k_scc_init<<<blocks(nn), 256, 0, s>>>(nn, g.scc.as<uint32_t>(), g.active.as<uint32_t>());
+    uint32_t *cnt = g.count.as<uint32_t>();
+    uint32_t h[4];
+    for (;;) {
+        ++*rounds;
+        // forward colouring
+        CK(hipMemsetAsync(cnt, 0, 16, s));
+        k_color_init<<<blocks(nn), 256, 0, s>>>(nn, g.out_off.as<uint32_t>(), g.out_dst.as<uint32_t>(),
+                                                g.active.as<uint32_t>(), g.color.as<uint32_t>(),
+                                                g.front.as<uint32_t>(), cnt);
+        CK(hipMemcpyAsync(h, cnt, 4, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        uint32_t nf = h[0];
+        uint32_t *f = g.front.as<uint32_t>(), *f2 = g.front2.as<uint32_t>();
+        while (nf) {
+            ++*iterations;
+            CK(hipMemsetAsync(cnt + 1, 0, 4, s));
+            k_color_step<<<blocks(nf), 256, 0, s>>>(f, nf, g.out_off.as<uint32_t>(), g.out_dst.as<uint32_t>(),
+                                                    g.active.as<uint32_t>(), g.color.as<uint32_t>(), f2,
+                                                    cnt + 1);
+            CK(hipMemcpyAsync(h, cnt + 1, 4, hipMemcpyDeviceToHost, s));
+            CK(hipStreamSynchronize(s));
+            nf = h[0];
+            std::swap(f, f2);
+        }
+        // backward sweep from the roots
+        CK(hipMemsetAsync(cnt, 0, 16, s));
+        k_bw_init<<<blocks(nn), 256, 0, s>>>(nn, g.active.as<uint32_t>(), g.color.as<uint32_t>(),
+                                             g.mark.as<uint32_t>(), g.front.as<uint32_t>(), cnt);
+        CK(hipMemcpyAsync(h, cnt, 4, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        nf = h[0];
+        f = g.front.as<uint32_t>();
+        f2 = g.front2.as<uint32_t>();
+        while (nf) {
+            ++*iterations;
+            CK(hipMemsetAsync(cnt + 1, 0, 4, s));
+            k_bw_step<<<blocks(nf), 256, 0, s>>>(f, nf, g.in_off.as<uint32_t>(), g.in_src.as<uint32_t>(),
+                                                 g.active.as<uint32_t>(), g.color.as<uint32_t>(),
+                                                 g.mark.as<uint32_t>(), f2, cnt + 1);
+            CK(hipMemcpyAsync(h, cnt + 1, 4, hipMemcpyDeviceToHost, s));
+            CK(hipStreamSynchronize(s));
+            nf = h[0];
+            std::swap(f, f2);
+        }
+        CK(hipMemsetAsync(cnt + 2, 0, 4, s));
+        k_finalize<<<blocks(nn), 256, 0, s>>>(nn, g.active.as<uint32_t>(), g.color.as<uint32_t>(),
+                                              g.mark.as<uint32_t>(), g.scc.as<uint32_t>(), cnt + 2);
+        CK(hipMemcpyAsync(h, cnt + 2, 4, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        if (h[0] == 0) break;
+        if (*rounds > nn) return hipErrorUnknown;  // cannot happen: every round retires >= 1 node
+    }
+#undef CK
+    return hipSuccess;
+}
+
+}  // namespace hsc

@@ -28,29 +28,6 @@ using namespace hsc;
 
 namespace {
 
-struct DBuf {
-    void *p = nullptr;
-    size_t bytes = 0;
-    hipError_t ensure(size_t want)
-    {
-        if (want <= bytes) return hipSuccess;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-        size_t b = want + want / 8 + 256;
-        hipError_t e = hipMalloc(&p, b);
-        if (e == hipSuccess) bytes = b;
-        return e;
-    }
-    void release()
-    {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-    template <class T> T *as() const { return (T *)p; }
-};
-
 struct GroupInfo {
     int tid, ix, klen;
 };
@@ -113,6 +90,10 @@ struct hsc_ctx {
     std::vector<uint64_t> m_lo, m_hi, m_snap, m_lock_snap;
     std::vector<uint32_t> m_gid, m_txn, m_lock_table, m_lock_txn;
     std::vector<uint8_t> m_forced;
+
+    // dependency graph
+    GraphBufs graph;
+    uint32_t graph_ntxn = 0;
 
     // timing
     bool timing = false;
@@ -847,6 +828,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->p_lock_txn, &c->p_verdict, &c->p_bitmap, &c->w_code, &c->w_counts,
                     &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_recs};
     for (DBuf *b : bufs) b->release();
+    c->graph.release_all();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -1148,6 +1130,93 @@ int hsc_enable_timing(hsc_ctx *c, int on)
 {
     if (!c) return HSC_EINVAL;
     c->timing = on != 0;
+    return HSC_OK;
+}
+
+int hsc_dep_graph_scc(hsc_ctx *c, const hsc_history *h, uint32_t *scc_out, hsc_graph_stats *st)
+{
+    if (!c || !h || (h->nops && (!h->txn || !h->key || !h->is_write || !h->observed)) ||
+        (h->ntxn && !scc_out) || h->nops > 0x7FFFFFFFull)
+        return HSC_EINVAL;
+    if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    for (size_t i = 0; i < h->nops; ++i)
+        if (h->txn[i] >= h->ntxn || h->observed[i] >= (int64_t)h->ntxn || h->observed[i] < -1)
+            return fail(c, HSC_EINVAL, "history op out of range");
+    hipStream_t s = c->stream;
+    GraphBufs &gb = c->graph;
+    const size_t n = h->nops;
+    std::vector<uint32_t> obs(std::max<size_t>(n, 1));
+    for (size_t i = 0; i < n; ++i) obs[i] = h->observed[i] < 0 ? 0xFFFFFFFFu : (uint32_t)h->observed[i];
+    HIPCHK(c, gb.h_txn.ensure(4 * std::max<size_t>(n, 1)));
+    HIPCHK(c, gb.h_key.ensure(8 * std::max<size_t>(n, 1)));
+    HIPCHK(c, gb.h_isw.ensure(std::max<size_t>(n, 1)));
+    HIPCHK(c, gb.h_obs.ensure(4 * std::max<size_t>(n, 1)));
+    if (n) {
+        HIPCHK(c, hipMemcpyAsync(gb.h_txn.p, h->txn, 4 * n, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(gb.h_key.p, h->key, 8 * n, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(gb.h_isw.p, h->is_write, n, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(gb.h_obs.p, obs.data(), 4 * n, hipMemcpyHostToDevice, s));
+    }
+    GraphInput in{gb.h_txn.as<uint32_t>(), gb.h_key.as<uint64_t>(), gb.h_isw.as<uint8_t>(),
+                  gb.h_obs.as<uint32_t>(), n, h->ntxn};
+    hipEvent_t e0, e1, e2;
+    HIPCHK(c, hipEventCreate(&e0));
+    HIPCHK(c, hipEventCreate(&e1));
+    HIPCHK(c, hipEventCreate(&e2));
+    HIPCHK(c, hipEventRecord(e0, s));
+    HIPCHK(c, graph_build(in, gb, s));
+    HIPCHK(c, hipEventRecord(e1, s));
+    uint32_t rounds = 0, iters = 0;
+    HIPCHK(c, graph_scc(h->ntxn, gb, &rounds, &iters, s));
+    HIPCHK(c, hipEventRecord(e2, s));
+    if (h->ntxn)
+        HIPCHK(c, hipMemcpyAsync(scc_out, gb.scc.p, 4 * (size_t)h->ntxn, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->graph_ntxn = h->ntxn;
+    if (st) {
+        memset(st, 0, sizeof *st);
+        st->edges = gb.ne;
+        (void)hipEventElapsedTime(&st->build_ms, e0, e1);
+        (void)hipEventElapsedTime(&st->scc_ms, e1, e2);
+        std::vector<uint32_t> ty(std::max<size_t>(gb.ne, 1));
+        if (gb.ne) HIPCHK(c, hipMemcpy(ty.data(), gb.type.p, 4 * gb.ne, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < gb.ne; ++i) {
+            st->ww += (ty[i] & kDepWW) != 0;
+            st->wr += (ty[i] & kDepWR) != 0;
+            st->rw += (ty[i] & kDepRW) != 0;
+        }
+        std::vector<uint32_t> sz(std::max<uint32_t>(h->ntxn, 1), 0);
+        for (uint32_t v = 0; v < h->ntxn; ++v)
+            if (scc_out[v] < h->ntxn) sz[scc_out[v]]++;
+        for (uint32_t v = 0; v < h->ntxn; ++v)
+            if (sz[v] > 1) {
+                st->nontrivial_sccs++;
+                st->txns_in_cycles += sz[v];
+            }
+        st->rounds = rounds;
+        st->iterations = iters;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipEventDestroy(e2);
+    return HSC_OK;
+}
+
+int hsc_dep_graph_edges(hsc_ctx *c, uint32_t *src, uint32_t *dst, uint32_t *type, size_t cap,
+                        size_t *n)
+{
+    if (!c || !n) return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    GraphBufs &gb = c->graph;
+    *n = gb.ne;
+    const size_t m = std::min(cap, gb.ne);
+    if (m && src) HIPCHK(c, hipMemcpy(src, gb.src.p, 4 * m, hipMemcpyDeviceToHost));
+    if (m && dst) HIPCHK(c, hipMemcpy(dst, gb.out_dst.p, 4 * m, hipMemcpyDeviceToHost));
+    if (m && type) HIPCHK(c, hipMemcpy(type, gb.type.p, 4 * m, hipMemcpyDeviceToHost));
     return HSC_OK;
 }
 

@@ -19,6 +19,30 @@
 
 namespace hsc {
 
+// Growable device buffer (reallocated only when a larger size is needed).
+struct DBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t want)
+    {
+        if (want <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        size_t b = want + want / 8 + 256;
+        hipError_t e = hipMalloc(&p, b);
+        if (e == hipSuccess) bytes = b;
+        return e;
+    }
+    void release()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T *as() const { return (T *)p; }
+};
+
 constexpr int kMaxWords = 64;       // MAXKEYLEN 512 B (bbinc/cdb2_constants.h:33)
 constexpr int kTopCap = 6144;       // splitter prefixes held in LDS by the locate kernel
 constexpr int kLocateThreads = 512;
@@ -109,6 +133,40 @@ hipError_t launch_scatter(const WinView &w, const ProbeView &p, const ProbeWork 
                           hipStream_t s);
 hipError_t launch_join(const WinView &w, const ProbeWork &work, uint32_t max_items,
                        uint8_t *verdict, hipStream_t s);
+// Dependency graph + SCC (hsc_graph.hip).
+constexpr uint64_t kDepWW = 1, kDepWR = 2, kDepRW = 4;
+struct GraphInput {              // device pointers
+    const uint32_t *txn;         // [nops] commit order of the op's txn
+    const uint64_t *key;
+    const uint8_t *is_write;
+    const uint32_t *observed;    // reads: writer txn of the observed version, ~0 initial
+    size_t nops;
+    uint32_t ntxn;
+};
+struct GraphBufs {
+    DBuf flags, flags2, scratch, count;
+    DBuf wg, ww, wl, wg2, ww2, wl2;            // writer rows
+    DBuf ew, et, eg, ew2, et2, eg2, swap_rows;  // edge rows
+    DBuf src, out_dst, type, in_src, in_dst, out_off, in_off;
+    DBuf scc, active, color, mark, front, front2;
+    DBuf h_txn, h_key, h_isw, h_obs;           // uploaded history
+    size_t ne = 0;
+    void release_all()
+    {
+        DBuf *all[] = {&flags, &flags2, &scratch, &count, &wg, &ww, &wl, &wg2, &ww2, &wl2,
+                       &ew, &et, &eg, &ew2, &et2, &eg2, &swap_rows, &src, &out_dst, &type,
+                       &in_src, &in_dst, &out_off, &in_off, &scc, &active, &color, &mark,
+                       &front, &front2, &h_txn, &h_key, &h_isw, &h_obs};
+        for (DBuf *b : all) b->release();
+    }
+};
+hipError_t graph_build(const GraphInput &in, GraphBufs &g, hipStream_t s);
+hipError_t graph_scc(uint32_t nnodes, GraphBufs &g, uint32_t *rounds, uint32_t *iterations,
+                     hipStream_t s);
+hipError_t swap_edge_words(uint32_t m, const uint32_t *src, const uint32_t *dst, uint64_t *rows,
+                           hipStream_t s);
+hipError_t scan_exclusive_u32(uint32_t *a, size_t n, uint32_t *scratch, hipStream_t s);
+
 hipError_t launch_pack(const uint8_t *verdict, uint32_t n_txn, uint64_t *bitmap,
                        hipStream_t s);
 

@@ -250,6 +250,11 @@ static hipError_t scan_u32(uint32_t *a, size_t n, uint32_t *scratch, hipStream_t
     return hipGetLastError();
 }
 
+hipError_t scan_exclusive_u32(uint32_t *a, size_t n, uint32_t *scratch, hipStream_t s)
+{
+    return scan_u32(a, n, scratch, s);
+}
+
 size_t radix_scratch_bytes(size_t n, int W)
 {
     size_t nblocks = (n + kSortTile - 1) / kSortTile;

@@ -77,6 +77,21 @@ class Timing(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class _History(C.Structure):
+    _fields_ = [("nops", C.c_size_t), ("ntxn", C.c_uint32), ("txn", _p), ("key", _p),
+                ("is_write", _p), ("observed", _p)]
+
+
+class GraphStats(C.Structure):
+    _fields_ = [("edges", C.c_uint64), ("ww", C.c_uint64), ("wr", C.c_uint64), ("rw", C.c_uint64),
+                ("nontrivial_sccs", C.c_uint32), ("txns_in_cycles", C.c_uint32),
+                ("rounds", C.c_uint32), ("iterations", C.c_uint32), ("build_ms", C.c_float),
+                ("scc_ms", C.c_float)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 class Marshalled(C.Structure):
     _fields_ = [("n", C.c_size_t), ("n_lock", C.c_size_t), ("n_txn", C.c_size_t),
                 ("words", C.c_int), ("lo", _u64p), ("hi", _u64p),
@@ -95,7 +110,7 @@ EXPORTS = [
     "hip_bdb_osql_serial_check", "hip_serial_check_batch", "hsc_check_readsets",
     "hsc_marshal_readsets", "hsc_probe_device", "hsc_pack_verdicts", "hsc_synchronize",
     "hsc_get_timing",
-    "hsc_enable_timing",
+    "hsc_enable_timing", "hsc_dep_graph_scc", "hsc_dep_graph_edges",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -145,6 +160,8 @@ def load() -> C.CDLL:
         "hsc_synchronize": (C.c_int, [_p]),
         "hsc_get_timing": (C.c_int, [_p, C.POINTER(Timing)]),
         "hsc_enable_timing": (C.c_int, [_p, C.c_int]),
+        "hsc_dep_graph_scc": (C.c_int, [_p, C.POINTER(_History), _p, C.POINTER(GraphStats)]),
+        "hsc_dep_graph_edges": (C.c_int, [_p, _p, _p, _p, C.c_size_t, C.POINTER(C.c_size_t)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -361,6 +378,29 @@ class Validator:
         tm = np.ascontiguousarray(tm, dtype=np.uint64)
         self._chk(self.lib.hsc_merge_table_max(self.ctx, tm.ctypes.data, len(tm)),
                   "hsc_merge_table_max")
+
+    # dependency graph + SCC (A10)
+    def dep_graph_scc(self, h) -> tuple:
+        """(scc[ntxn] = largest txn id of each txn's SCC, stats dict)."""
+        cols = [np.ascontiguousarray(h.txn, np.uint32), np.ascontiguousarray(h.key, np.uint64),
+                np.ascontiguousarray(h.is_write, np.uint8), np.ascontiguousarray(h.observed, np.int64)]
+        hs = _History(len(cols[0]), h.ntxn, *[c.ctypes.data for c in cols])
+        out = np.zeros(max(1, h.ntxn), dtype=np.uint32)
+        st = GraphStats()
+        self._chk(self.lib.hsc_dep_graph_scc(self.ctx, C.byref(hs), out.ctypes.data, C.byref(st)),
+                  "hsc_dep_graph_scc")
+        return out[: h.ntxn], st.as_dict()
+
+    def dep_graph_edges(self) -> tuple:
+        n = C.c_size_t()
+        self._chk(self.lib.hsc_dep_graph_edges(self.ctx, None, None, None, 0, C.byref(n)),
+                  "hsc_dep_graph_edges")
+        m = n.value
+        a = [np.zeros(max(1, m), dtype=np.uint32) for _ in range(3)]
+        self._chk(self.lib.hsc_dep_graph_edges(self.ctx, a[0].ctypes.data, a[1].ctypes.data,
+                                               a[2].ctypes.data, m, C.byref(n)),
+                  "hsc_dep_graph_edges")
+        return tuple(x[:m] for x in a)
 
     def probe_device(self, batch: ProbeBatch) -> None:
         self._chk(self.lib.hsc_probe_device(self.ctx, C.byref(batch)), "hsc_probe_device")

@@ -324,3 +324,98 @@ def random_case(seed: int, n_commits: int = 60, n_txn: int = 40, tables=("ta", "
         pool = all_lsn if rng.random() < 0.9 else [int(x) + 1 for x in log.lsn[:5]] or all_lsn
         snaps.append(pool[int(rng.integers(0, len(pool)))])
     return log, ReadSets.from_lists(sets, snaps, tbnames=lb.tbnames)
+
+
+# ---------------------------------------------------------------------------
+# config 4: Jepsen bank/register-style histories for the dependency graph
+# ---------------------------------------------------------------------------
+SEED_CONFIG4 = 0xC0FFEE04
+
+
+@dataclasses.dataclass
+class History:
+    """Micro-ops of committed transactions.  txn ids are commit order; a read
+    records the writer txn of the version it observed (-1 = initial value),
+    as a Jepsen rw-register history with unique write values does."""
+    txn: np.ndarray        # uint32[nops]
+    key: np.ndarray        # uint64[nops]
+    is_write: np.ndarray   # uint8[nops]
+    observed: np.ndarray   # int64[nops]
+    ntxn: int
+
+    @property
+    def nops(self) -> int:
+        return int(len(self.txn))
+
+
+def config4_history(seed: int = SEED_CONFIG4, n_txn: int = 1_000_000, n_keys: int = 100_000,
+                    ops_per_txn: int = 4, write_frac: float = 0.5, concurrent_frac: float = 0.02,
+                    max_lag: int = 64, zipf: float = 0.0) -> History:
+    """Txn t commits t-th and reads from snapshot s_t: s_t = t for most txns
+    (serial), s_t = t - lag (lag <= max_lag) for `concurrent_frac` of them, so
+    stale reads create rw anti-dependencies (write skew / G2 cycles).  Every
+    txn touches ops_per_txn distinct-ish keys; each op is a read (observes the
+    latest writer < s_t) followed, with probability write_frac, by a write
+    (the bank transfer shape: read-modify-write)."""
+    rng = np.random.default_rng(seed)
+    n = n_txn * ops_per_txn
+    txn = np.repeat(np.arange(n_txn, dtype=np.uint32), ops_per_txn)
+    if zipf > 0:
+        key = (rng.zipf(1.0 + zipf, size=n) % n_keys).astype(np.uint64)
+    else:
+        key = rng.integers(0, n_keys, size=n, dtype=np.uint64)
+    lag = np.where(rng.random(n_txn) < concurrent_frac, rng.integers(1, max_lag + 1, size=n_txn), 0)
+    snap = np.maximum(np.arange(n_txn, dtype=np.int64) - lag, 0)
+    w = rng.random(n) < write_frac
+    # writes sorted by (key, txn) as one composite
+    wc = np.sort((key[w] << np.uint64(32)) | txn[w].astype(np.uint64))
+    rc = (key << np.uint64(32)) | np.repeat(snap, ops_per_txn).astype(np.uint64)
+    idx = np.searchsorted(wc, rc, side="left").astype(np.int64) - 1
+    ok = idx >= 0
+    cand = wc[np.maximum(idx, 0)]
+    ok &= (cand >> np.uint64(32)) == key
+    observed = np.where(ok, (cand & np.uint64(0xFFFFFFFF)).astype(np.int64), -1)
+    # op stream: each op is a read; written keys also get a write micro-op
+    ops_txn = np.concatenate([txn, txn[w]])
+    ops_key = np.concatenate([key, key[w]])
+    ops_w = np.concatenate([np.zeros(n, np.uint8), np.ones(int(w.sum()), np.uint8)])
+    ops_obs = np.concatenate([observed, np.full(int(w.sum()), -1, np.int64)])
+    order = np.argsort(ops_txn, kind="stable")
+    return History(ops_txn[order], ops_key[order], ops_w[order], ops_obs[order], n_txn)
+
+
+def history_to_edn(h: History, limit: Optional[int] = None) -> str:
+    """Jepsen rw-register (Elle) style EDN, one completed txn per line:
+    {:type :ok, :f :txn, :value [[:r k v] [:w k v]], :process p, :index i};
+    write values are writer txn + 1 (unique per key), nil = initial."""
+    lines = []
+    starts = np.searchsorted(h.txn, np.arange(h.ntxn + 1))
+    for t in range(h.ntxn if limit is None else min(limit, h.ntxn)):
+        mops = []
+        for i in range(starts[t], starts[t + 1]):
+            k = int(h.key[i])
+            if h.is_write[i]:
+                mops.append(f"[:w {k} {t + 1}]")
+            else:
+                ob = int(h.observed[i])
+                mops.append(f"[:r {k} {'nil' if ob < 0 else ob + 1}]")
+        lines.append(f"{{:type :ok, :f :txn, :value [{' '.join(mops)}], :process {t % 16}, :index {t}}}")
+    return "\n".join(lines)
+
+
+def history_from_edn(text: str) -> History:
+    """Parse the EDN above (only :ok txns, in history order = commit order)."""
+    import re
+    txn, key, isw, obs = [], [], [], []
+    t = 0
+    for line in text.splitlines():
+        if ":type :ok" not in line:
+            continue
+        for kind, k, v in re.findall(r"\[:(r|w) (\d+) (nil|\d+)\]", line):
+            txn.append(t)
+            key.append(int(k))
+            isw.append(1 if kind == "w" else 0)
+            obs.append(-1 if (kind == "w" or v == "nil") else int(v) - 1)
+        t += 1
+    return History(np.array(txn, np.uint32), np.array(key, np.uint64), np.array(isw, np.uint8),
+                   np.array(obs, np.int64), t)

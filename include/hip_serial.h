@@ -261,6 +261,40 @@ int hsc_get_timing(hsc_ctx *ctx, hsc_timing *t);
 /* Enable per-kernel HIP event timing of probes (adds event records). */
 int hsc_enable_timing(hsc_ctx *ctx, int on);
 
+/* ---- dependency graph + SCC ------------------------
+ * History of committed transactions as micro-ops (host pointers): txn ids
+ * are commit order (a key's version order = its writers' commit order); a
+ * read records the writer txn of the version it observed (-1 = initial), as
+ * a Jepsen rw-register history with unique write values does.  Edges (Adya):
+ * ww consecutive writers of a key, wr writer -> reader, rw reader -> next
+ * writer after the observed version; self edges dropped, parallel edges
+ * merged (type bits: 1 ww, 2 wr, 4 rw).  scc_out[v] = the largest txn id of
+ * v's strongly connected component; a component with more than one txn is a
+ * dependency cycle (G1c / G2 anomaly). */
+typedef struct hsc_history {
+    size_t nops;
+    uint32_t ntxn;
+    const uint32_t *txn;
+    const uint64_t *key;
+    const uint8_t *is_write;
+    const int64_t *observed;
+} hsc_history;
+
+typedef struct hsc_graph_stats {
+    uint64_t edges;
+    uint64_t ww, wr, rw;          /* edges carrying each type bit              */
+    uint32_t nontrivial_sccs;     /* components with >= 2 txns                 */
+    uint32_t txns_in_cycles;
+    uint32_t rounds, iterations;  /* colouring rounds / frontier steps         */
+    float build_ms, scc_ms;       /* device time                               */
+} hsc_graph_stats;
+
+int hsc_dep_graph_scc(hsc_ctx *ctx, const hsc_history *h, uint32_t *scc_out,
+                      hsc_graph_stats *stats);
+/* Edges of the last graph, sorted by (src, dst): copies min(cap, n). */
+int hsc_dep_graph_edges(hsc_ctx *ctx, uint32_t *src, uint32_t *dst, uint32_t *type,
+                        size_t cap, size_t *n);
+
 #ifdef __cplusplus
 }
 #endif

@@ -49,6 +49,11 @@ def load():
         lib.or_build_arrs.argtypes = [C.c_int] + [_p] * 12 + [C.POINTER(C.c_char_p)]
         lib.or_free_arrs.restype = None
         lib.or_free_arrs.argtypes = [_p, C.c_int]
+        lib.dg_edges.restype = C.c_size_t
+        lib.dg_edges.argtypes = [C.c_size_t, _p, _p, _p, _p, C.POINTER(_p), C.POINTER(_p),
+                                 C.POINTER(_p)]
+        lib.dg_free.argtypes = [_p]
+        lib.dg_scc.argtypes = [C.c_uint32, C.c_size_t, _p, _p, _p]
         lib.or_serial_check.restype = C.c_int
         lib.or_serial_check.argtypes = [C.POINTER(_OrLog), _p, C.POINTER(C.c_uint),
                                         C.POINTER(C.c_uint), C.c_int]
@@ -101,3 +106,30 @@ def check(log, rs: ReadSets, regop_only: int = 0, nthreads: int = 1):
     finally:
         lib.or_free_arrs(arrs, rs.ntxn)
     return rc[: rs.ntxn], post, secs
+
+
+def dep_edges(txn, key, is_write, observed):
+    """WR/WW/RW edges of a history (Adya): (src, dst, type bits) sorted by
+    (src, dst), type bits 1 = ww, 2 = wr, 4 = rw."""
+    lib = load()
+    cols = [np.ascontiguousarray(txn, np.uint32), np.ascontiguousarray(key, np.uint64),
+            np.ascontiguousarray(is_write, np.uint8), np.ascontiguousarray(observed, np.int64)]
+    ps, pd, pt = _p(), _p(), _p()
+    m = lib.dg_edges(len(cols[0]), *[c.ctypes.data for c in cols], C.byref(ps), C.byref(pd),
+                     C.byref(pt))
+    out = []
+    for p in (ps, pd, pt):
+        a = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint32)), shape=(max(m, 1),))[:m].copy()
+        lib.dg_free(p)
+        out.append(a)
+    return tuple(out)
+
+
+def scc(n, src, dst):
+    """Tarjan: scc[v] = largest node id of v's strongly connected component."""
+    lib = load()
+    src = np.ascontiguousarray(src, np.uint32)
+    dst = np.ascontiguousarray(dst, np.uint32)
+    out = np.zeros(max(1, n), dtype=np.uint32)
+    lib.dg_scc(n, len(src), src.ctypes.data, dst.ctypes.data, out.ctypes.data)
+    return out[:n]
