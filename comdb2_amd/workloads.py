@@ -419,3 +419,135 @@ def history_from_edn(text: str) -> History:
         t += 1
     return History(np.array(txn, np.uint32), np.array(key, np.uint64), np.array(isw, np.uint8),
                    np.array(obs, np.int64), t)
+
+
+# ---------------------------------------------------------------------------
+# config 3: composite keys <= 64 B over 32 (table, index) groups
+# ---------------------------------------------------------------------------
+SEED_CONFIG3 = 0xC0FFEE03
+SEED_CONFIG5 = 0xC0FFEE05
+
+# per index: list of fields (kind, size, descending) -> ondisk key bytes
+INDEX_SHAPES = [
+    [("i64", 9, False)],                                               # 9 B
+    [("i64", 9, False), ("i64", 9, True)],                             # 18 B
+    [("str", 21, False), ("i64", 9, False)],                           # 30 B
+    [("str", 31, False), ("i64", 9, True), ("i64", 9, False), ("i64", 9, False)],  # 58 B
+]
+
+
+def _enc_fields(rng, shape, n, vmax):
+    """n keys of an index shape as uint8[n, L] (memcmp-ordered ondisk)."""
+    cols = []
+    for kind, size, desc in shape:
+        if kind == "i64":
+            v = rng.integers(0, vmax, size=n, dtype=np.int64)
+            b = F.enc_int64_array(v)
+        else:
+            ln = rng.integers(1, size - 1, size=n)
+            letters = rng.integers(ord("a"), ord("a") + 6, size=(n, size - 1)).astype(np.uint8)
+            letters[np.arange(size - 1)[None, :] >= ln[:, None]] = 0
+            b = np.concatenate([np.full((n, 1), 8, np.uint8), letters], axis=1)
+        cols.append(255 - b if desc else b)
+    return np.concatenate(cols, axis=1)
+
+
+def config3(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4, n_writes: int = 200_000,
+            keys_per_commit: int = 8, n_txn: int = 20_000, ranges_per_txn: int = 10,
+            vmax: int = 1 << 12, snap_recent: float = 0.05, lock_frac: float = 0.01):
+    """Log of commits writing composite index keys (upd_ix) plus dta records
+    over n_tables x n_ix groups with log-normal group sizes, and read sets of
+    point / range / prefix ranges (and a few full-scan table locks) over 1-3
+    tables each (ranges sorted per table like coalesced arrays).  Returns
+    (LLog, ReadSets)."""
+    rng = np.random.default_rng(seed)
+    tb = [f"t{i}" for i in range(n_tables)]
+    G = n_tables * n_ix
+    w = rng.lognormal(0.0, 1.0, size=G)
+    gsize = np.maximum(1, (w / w.sum() * n_writes).astype(np.int64))
+    keys_of = []
+    for g in range(G):
+        keys_of.append(_enc_fields(rng, INDEX_SHAPES[g % n_ix], int(gsize[g]), vmax))
+    # interleave writes of all groups into commits
+    gid = np.concatenate([np.full(int(gsize[g]), g) for g in range(G)])
+    row = np.concatenate([np.arange(int(gsize[g])) for g in range(G)])
+    perm = rng.permutation(len(gid))
+    gid, row = gid[perm], row[perm]
+    lb = LogBuilder(tb)
+    commits = [lb.next_lsn()]
+    c = 0
+    for i in range(0, len(gid), keys_per_commit):
+        lb.begin(c)
+        for g, r in zip(gid[i:i + keys_per_commit], row[i:i + keys_per_commit]):
+            lb.write(c, F.REC_UNDO_UPD_IX, tb[g // n_ix], int(g % n_ix), bytes(keys_of[g][r]))
+        if rng.random() < 0.3:
+            lb.write(c, F.REC_UNDO_UPD_DTA, tb[int(rng.integers(0, n_tables))])
+        commits.append(lb.commit(c))
+        c += 1
+    log = lb.build()
+    recent = max(1, int(len(commits) * snap_recent))
+    sets, snaps = [], []
+    for t in range(n_txn):
+        rs = []
+        for tt in sorted(rng.choice(n_tables, size=int(rng.integers(1, 4)), replace=False)):
+            if rng.random() < lock_frac:
+                rs.append(Range.locked(tb[tt]))
+                continue
+            for _ in range(max(1, ranges_per_txn // 3)):
+                ix = int(rng.integers(0, n_ix))
+                g = tt * n_ix + ix
+                a = bytes(keys_of[g][int(rng.integers(0, len(keys_of[g])))])
+                u = rng.random()
+                if u < 0.5:
+                    rs.append(Range(tb[tt], ix, a, a))
+                elif u < 0.8:
+                    b = bytes(keys_of[g][int(rng.integers(0, len(keys_of[g])))])
+                    rs.append(Range(tb[tt], ix, min(a, b), max(a, b)))
+                else:
+                    p = a[: int(rng.integers(1, len(a)))]
+                    rs.append(Range(tb[tt], ix, p, p))
+        rs.sort(key=lambda r: (r.tbname, -r.islocked, r.idxnum, r.lkey or b""))
+        sets.append(rs)
+        snaps.append(commits[len(commits) - 1 - int(rng.integers(0, recent))])
+    return log, ReadSets.from_lists(sets, snaps, tbnames=lb.tbnames)
+
+
+def config5(seed: int = SEED_CONFIG5, n_commits: int = 100_000, keys_per_commit: int = 10,
+            n_txn: int = 10_000, zipf_s: float = 1.2, key_bits: int = 32, **kw) -> Config2:
+    """Config 2's shape with Zipf(s) hot keys over 2^key_bits: a few keys take
+    most writes (they collapse under dedupe) and ranges cluster on hot tiles."""
+    c2 = config2(seed=seed, n_commits=n_commits, keys_per_commit=keys_per_commit, n_txn=n_txn,
+                 value_bits=key_bits, build_log=False, **kw)
+    rng = np.random.default_rng([seed, 5])
+    z = rng.zipf(zipf_s, size=n_commits * keys_per_commit).astype(np.uint64)
+    hot = ((z * np.uint64(0x9E3779B1)) & np.uint64((1 << key_bits) - 1)).astype(np.int64)
+    K = keys_per_commit
+    R = K + 3
+    nrec = n_commits * R
+    idx = np.arange(nrec, dtype=np.uint64)
+    lsns = lsn_of_index(idx)
+    j = (idx % np.uint64(R)).astype(np.int64)
+    rectype = np.full(nrec, F.REC_UNDO_UPD_IX, dtype=np.uint32)
+    rectype[j == 0] = F.REC_LTRAN_START
+    rectype[j == R - 2] = F.REC_LTRAN_COMMIT
+    rectype[j == R - 1] = F.REC_TXN_REGOP
+    prev = np.zeros(nrec, dtype=np.uint64)
+    prev[1:] = lsns[:-1]
+    prev[j == 0] = 0
+    is_undo = (j >= 1) & (j <= K)
+    key_off = np.zeros(nrec, dtype=np.uint64)
+    key_off[is_undo] = np.arange(n_commits * K, dtype=np.uint64) * np.uint64(9)
+    log = LLog(lsns, rectype, prev, np.zeros(nrec, np.int16), np.where(is_undo, 0, -1).astype(np.int32),
+               np.zeros(nrec, np.int16), key_off, np.where(is_undo, 9, 0).astype(np.int32),
+               F.enc_int64_array(hot).reshape(-1), ["t1"], int(lsn_of_index(np.array([nrec]))[0]))
+    # point ranges aim at the hot keys half of the time
+    rs = c2.readsets
+    pts = (rs.lkeylen == 9) & (rs.rkeylen == 9)
+    sel = np.nonzero(pts & (rng.random(len(pts)) < 0.5))[0]
+    keys = rs.keys.copy().reshape(-1)
+    hk = F.enc_int64_array(hot[rng.integers(0, len(hot), size=len(sel))])
+    for side in ("lkey_off", "rkey_off"):
+        off = getattr(rs, side)[sel].astype(np.int64)
+        keys[(off[:, None] + np.arange(9)[None, :]).reshape(-1)] = hk.reshape(-1)
+    rs = dataclasses.replace(rs, keys=keys)
+    return Config2(log, rs, lsns[R - 1::R].copy(), hot, dict(c2.params, zipf_s=zipf_s))

@@ -148,3 +148,23 @@ def test_config2_full_size_sampled(validator, oracle_mod):
     perm = np.random.default_rng(1).permutation(c2.readsets.ntxn)
     got_p = validator.check_readsets(c2.readsets.subset(perm))
     np.testing.assert_array_equal(got_p, got[perm])
+
+
+@pytest.mark.parametrize("kw", [dict(n_writes=30000, n_txn=2000),
+                                dict(n_writes=200000, n_txn=5000, vmax=1 << 20)])
+def test_config3_composite_keys(validator, oracle_mod, kw):
+    from comdb2_amd.workloads import config3
+    log, rs = config3(**kw)
+    want, _, _ = oracle_mod.check(log, rs, nthreads=8)
+    validator.ingest_log(log)
+    got = validator.check_readsets(rs)
+    np.testing.assert_array_equal(got != 0, want != 0)
+
+
+def test_config5_zipf_hot_keys(validator, oracle_mod):
+    from comdb2_amd.workloads import config5
+    c5 = config5(n_commits=50000, n_txn=5000, snap_recent=0.002)
+    want, _, _ = oracle_mod.check(c5.log, c5.readsets, nthreads=8)
+    validator.ingest_log(c5.log)
+    got = validator.check_readsets(c5.readsets)
+    np.testing.assert_array_equal(got != 0, want != 0)

@@ -125,3 +125,20 @@ def test_host_only_context_refuses_device_work(host):
     from comdb2_amd.hsc import HscError
     with pytest.raises(HscError):
         host.check_readsets(rs)
+
+
+def test_config3_and_config5_host_path(host, oracle_mod):
+    from comdb2_amd.workloads import config3, config5
+    log, rs = config3(n_writes=20000, n_txn=800)
+    host.ingest_log(log)
+    m = host.marshal(rs)
+    assert m["words"] == 8 and m["n_lock"] > 0
+    want, _, _ = oracle_mod.check(log, rs, nthreads=8)
+    got = evaluate(host, m, WindowModel(log)) | m["forced"]
+    np.testing.assert_array_equal(got != 0, want != 0)
+    c5 = config5(n_commits=20000, n_txn=1000, snap_recent=0.002)
+    host.ingest_log(c5.log)
+    m = host.marshal(c5.readsets)
+    want, _, _ = oracle_mod.check(c5.log, c5.readsets, nthreads=8)
+    got = evaluate(host, m, WindowModel(c5.log)) | m["forced"]
+    np.testing.assert_array_equal(got != 0, want != 0)
