@@ -46,7 +46,8 @@ struct DBuf {
 constexpr int kMaxWords = 64;       // MAXKEYLEN 512 B (bbinc/cdb2_constants.h:33)
 constexpr int kTopCap = 6144;       // splitter prefixes held in LDS by the locate kernel
 constexpr int kLocateThreads = 512;
-constexpr int kMaxChunks = 512;     // probe chunks (locate / scatter workgroups)
+constexpr int kMaxChunks = 512;     // probe chunks (locate workgroups)
+constexpr int kMaxChunkProbes = 4096;  // probes per chunk (8 per locate thread)
 constexpr int kHistCap = 8192;      // tiles whose bucket counters fit in LDS
 constexpr int kJoinThreads = 512;
 constexpr int kJoinChunk = 1024;    // join records per workgroup
@@ -115,22 +116,21 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
                            uint64_t *table_max, uint32_t *sp_g, uint64_t *sp_w, hipStream_t s);
 // Probe.
 struct ProbeWork {
-    uint64_t *code;        // [n] a | b << 31 | kind << 62
-    uint32_t *hist;        // [G][ntiles] per-chunk record counts -> offsets
-    uint32_t *counts;      // [ntiles + 1] records per tile
-    uint32_t *bucket_off;  // [ntiles + 1]
-    uint32_t *cursor;      // [ntiles] (global-atomic mode, ntiles > kHistCap)
+    uint32_t *hist;        // [G][ntiles] per chunk: offset << 16 | count per tile
+    uint32_t *hist_tmp;    // [G][ntiles] counters when ntiles > kHistCap (else unused)
+    uint32_t *seg;         // [ntiles][G] transposed hist
+    uint32_t *pre;         // [ntiles][G] records of tile t in chunks < g
+    uint32_t *counts;      // [ntiles] records per tile
     uint32_t *item_off;    // [ntiles + 1]
     uint32_t *item_tile;   // [max items]
-    uint64_t *recs;        // join records
-    uint32_t G, chunk;     // probe chunks (one workgroup each in locate/scatter)
-    int lds_mode;          // ntiles <= kHistCap: LDS histograms, no global atomics
+    uint64_t *recs;        // [G][regcap] join records, chunk regions grouped by tile
+    uint32_t G, chunk;     // probe chunks (one locate workgroup each)
+    uint32_t regcap;       // records per chunk region (2 * chunk)
+    int lds_mode;          // ntiles <= kHistCap: chunk counters in LDS
 };
 hipError_t launch_locate(const WinView &w, const ProbeView &p, const ProbeWork &work,
                          uint8_t *verdict, hipStream_t s);
 hipError_t launch_plan(const WinView &w, const ProbeWork &work, hipStream_t s);
-hipError_t launch_scatter(const WinView &w, const ProbeView &p, const ProbeWork &work,
-                          hipStream_t s);
 hipError_t launch_join(const WinView &w, const ProbeWork &work, uint32_t max_items,
                        uint8_t *verdict, hipStream_t s);
 // Dependency graph + SCC (hsc_graph.hip).
