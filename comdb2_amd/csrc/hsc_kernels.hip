@@ -93,7 +93,6 @@ __device__ __forceinline__ int cmp_words(int W, uint64_t a_w0, const uint64_t *a
 constexpr int kSortThreads = 256;
 constexpr int kSortItems = 16;
 constexpr int kSortTile = kSortThreads * kSortItems;  // rows per block
-constexpr int kDigitsPerHist = 32;
 
 // Digit d (0 = least significant byte of the composite key).
 __device__ __forceinline__ uint32_t row_digit(int W, int d, size_t i, const uint32_t *gid,
@@ -106,21 +105,22 @@ __device__ __forceinline__ uint32_t row_digit(int W, int d, size_t i, const uint
     return (gid[i] >> (8 * (d - 8 * W))) & 0xFFu;
 }
 
-// Histograms of digits [d0, d0 + nd) over all rows (to skip constant digits).
-__global__ __launch_bounds__(256) void k_hist_digits(int W, size_t n, const uint32_t *gid,
-                                                     const uint64_t *words, size_t stride,
-                                                     int d0, int nd, uint32_t *hist)
+// Bits that vary across rows: OR over rows of (row XOR row 0), per key word
+// and for the gid (mask[W]); a radix digit whose byte is zero in the mask is
+// the same in every row and its pass is skipped.
+__global__ __launch_bounds__(256) void k_vary_mask(int W, size_t n, const uint32_t *gid,
+                                                   const uint64_t *words, size_t stride,
+                                                   unsigned long long *mask)
 {
-    __shared__ uint32_t h[kDigitsPerHist * 256];
-    for (int i = threadIdx.x; i < nd * 256; i += blockDim.x) h[i] = 0;
-    __syncthreads();
-    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-         i += (size_t)gridDim.x * blockDim.x)
-        for (int k = 0; k < nd; ++k)
-            atomicAdd(&h[k * 256 + row_digit(W, d0 + k, i, gid, words, stride)], 1u);
-    __syncthreads();
-    for (int i = threadIdx.x; i < nd * 256; i += blockDim.x)
-        if (h[i]) atomicAdd(&hist[(size_t)d0 * 256 + i], h[i]);
+    for (int j = 0; j <= W; ++j) {
+        const uint64_t ref = j < W ? words[(size_t)j * stride] : gid[0];
+        uint64_t m = 0;
+        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+             i += (size_t)gridDim.x * blockDim.x)
+            m |= (j < W ? words[(size_t)j * stride + i] : gid[i]) ^ ref;
+        for (int o = 32; o > 0; o >>= 1) m |= __shfl_xor(m, o, 64);
+        if (lane_id() == 0 && m) atomicOr(&mask[j], (unsigned long long)m);
+    }
 }
 
 // Per-block digit counts, digit-major: counts[digit * nblocks + block].
@@ -141,19 +141,36 @@ __global__ __launch_bounds__(kSortThreads) void k_rs_count(int W, int d, size_t 
     counts[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
-// Stable scatter: rows of a block are ranked in index order (round-major,
-// lane order inside a round) with 8 ballots per round for the wave match.
+// Stable scatter.  Phase 1 ranks the block's rows in index order (round-major,
+// lane order inside a round; 8 ballots per round for the wave match) into
+// block-local sorted positions and records the permutation in LDS.  Phase 2
+// walks the block in sorted order, so consecutive threads write consecutive
+// addresses of each digit's run (coalesced stores); the rows it gathers were
+// read by phase 1 and are served from L1/L2.
 __global__ __launch_bounds__(kSortThreads) void k_rs_scatter(
     int W, int d, size_t n, const uint32_t *gid, const uint64_t *words, const uint64_t *lsn,
     size_t stride, uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o,
     const uint32_t *offsets, uint32_t nblocks)
 {
     __shared__ uint32_t gbase[256];
+    __shared__ uint32_t loff[256];
     __shared__ uint32_t running[256];
     __shared__ uint32_t wave_h[kSortThreads / 64][256];
+    __shared__ uint16_t perm[kSortTile];
+    __shared__ uint32_t lds16[16];
     const int lane = lane_id(), wid = threadIdx.x >> 6;
-    gbase[threadIdx.x] = offsets[(size_t)threadIdx.x * nblocks + blockIdx.x];
-    running[threadIdx.x] = 0;
+    const uint32_t dg = threadIdx.x;  // one digit per thread
+    const size_t at = (size_t)dg * nblocks + blockIdx.x;
+    const uint32_t mine = offsets[at];
+    const size_t nxt_at = at + 1;
+    const uint32_t total_rows = (uint32_t)n;
+    // block's count of digit dg = next offset - this offset
+    const uint32_t nxt = nxt_at < (size_t)256 * nblocks ? offsets[nxt_at] : total_rows;
+    const uint32_t cnt = nxt - mine;
+    gbase[dg] = mine;
+    uint32_t tot;
+    loff[dg] = block_excl_scan<kSortThreads>(cnt, lds16, tot);
+    running[dg] = 0;
     const size_t base = (size_t)blockIdx.x * kSortTile;
     const uint64_t lt_mask = (lane ? (~0ull >> (64 - lane)) : 0ull);
     for (int k = 0; k < kSortItems; ++k) {
@@ -167,18 +184,16 @@ __global__ __launch_bounds__(kSortThreads) void k_rs_scatter(
             peers &= ((dig >> b) & 1u) ? m : ~m;
         }
         const uint32_t rank = __popcll(peers & lt_mask);
-        const uint32_t cnt = __popcll(peers);
+        const uint32_t c = __popcll(peers);
         for (int t = threadIdx.x; t < (kSortThreads / 64) * 256; t += kSortThreads)
             (&wave_h[0][0])[t] = 0;
         __syncthreads();
-        if (valid && rank == 0) wave_h[wid][dig] = cnt;
+        if (valid && rank == 0) wave_h[wid][dig] = c;
         __syncthreads();
         if (valid) {
-            uint32_t pos = gbase[dig] + running[dig] + rank;
+            uint32_t pos = loff[dig] + running[dig] + rank;
             for (int w2 = 0; w2 < wid; ++w2) pos += wave_h[w2][dig];
-            gid_o[pos] = gid[i];
-            for (int j = 0; j < W; ++j) words_o[(size_t)j * stride + pos] = words[(size_t)j * stride + i];
-            lsn_o[pos] = lsn[i];
+            perm[pos] = (uint16_t)(k * kSortThreads + threadIdx.x);
         }
         __syncthreads();
         {
@@ -187,6 +202,16 @@ __global__ __launch_bounds__(kSortThreads) void k_rs_scatter(
             running[threadIdx.x] += add;
         }
         __syncthreads();
+    }
+    // phase 2: sorted order -> contiguous runs per digit
+    const uint32_t nrows = (uint32_t)min((size_t)kSortTile, n - base);
+    for (uint32_t j = threadIdx.x; j < nrows; j += kSortThreads) {
+        const size_t i = base + perm[j];
+        const uint32_t dig = row_digit(W, d, i, gid, words, stride);
+        const uint32_t pos = gbase[dig] + (j - loff[dig]);
+        gid_o[pos] = gid[i];
+        for (int jw = 0; jw < W; ++jw) words_o[(size_t)jw * stride + pos] = words[(size_t)jw * stride + i];
+        lsn_o[pos] = lsn[i];
     }
 }
 
@@ -273,34 +298,26 @@ hipError_t radix_sort_rows(int W, size_t n, uint32_t *gid, uint64_t *words, uint
     if (scratch_bytes < radix_scratch_bytes(n, W)) return hipErrorInvalidValue;
     const int ndig = 8 * W + 4;
     const uint32_t nblocks = (uint32_t)((n + kSortTile - 1) / kSortTile);
-    uint32_t *hist = (uint32_t *)scratch;
-    uint32_t *counts = hist + (size_t)ndig * 256;
+    unsigned long long *dmask = (unsigned long long *)scratch;  // [W + 1]
+    uint32_t *counts = (uint32_t *)scratch + (size_t)ndig * 256;
     uint32_t *scan_tmp = counts + (size_t)256 * nblocks;
-    hipError_t e = hipMemsetAsync(hist, 0, (size_t)ndig * 256 * sizeof(uint32_t), s);
+    hipError_t e = hipMemsetAsync(dmask, 0, 8 * ((size_t)W + 1), s);
     if (e != hipSuccess) return e;
     const unsigned hgrid = (unsigned)std::min<size_t>((n + 255) / 256, 2048);
-    for (int d0 = 0; d0 < ndig; d0 += kDigitsPerHist) {
-        int nd = std::min(kDigitsPerHist, ndig - d0);
-        k_hist_digits<<<hgrid, 256, 0, s>>>(W, n, gid, words, stride, d0, nd, hist);
-    }
+    k_vary_mask<<<hgrid, 256, 0, s>>>(W, n, gid, words, stride, dmask);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    uint32_t *hh = (uint32_t *)malloc((size_t)ndig * 256 * sizeof(uint32_t));
-    if (!hh) return hipErrorOutOfMemory;
-    e = hipMemcpyAsync(hh, hist, (size_t)ndig * 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    unsigned long long hm[kMaxWords + 1];
+    e = hipMemcpyAsync(hm, dmask, 8 * ((size_t)W + 1), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) {
-        free(hh);
-        return e;
-    }
+    if (e != hipSuccess) return e;
     bool alt = false;
     uint32_t *g0 = gid, *g1 = gid_alt;
     uint64_t *w0 = words, *w1 = words_alt, *l0 = lsn, *l1 = lsn_alt;
     for (int d = 0; d < ndig; ++d) {
-        bool constant = false;
-        for (int b = 0; b < 256; ++b)
-            if (hh[(size_t)d * 256 + b] == n) constant = true;
-        if (constant) continue;
+        const int j = d < 8 * W ? W - 1 - (d >> 3) : W;
+        const int byte = d < 8 * W ? (d & 7) : d - 8 * W;
+        if (((hm[j] >> (8 * byte)) & 0xFFu) == 0) continue;  // digit constant across rows
         k_rs_count<<<nblocks, kSortThreads, 0, s>>>(W, d, n, g0, w0, stride, counts, nblocks);
         e = scan_u32(counts, (size_t)256 * nblocks, scan_tmp, s);
         if (e != hipSuccess) break;
@@ -313,7 +330,6 @@ hipError_t radix_sort_rows(int W, size_t n, uint32_t *gid, uint64_t *words, uint
         std::swap(l0, l1);
         alt = !alt;
     }
-    free(hh);
     *result_in_alt = alt;
     return e;
 }
