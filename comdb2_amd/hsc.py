@@ -21,7 +21,7 @@ import numpy as np
 from .formats import LLog, Range, ReadSets
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libhsc.so")
+LIB_PATH = os.environ.get("HSC_LIB") or os.path.join(_HERE, "lib", "libhsc.so")
 
 HSC_OK, HSC_EINVAL, HSC_EDEVICE, HSC_ENOMEM, HSC_ELOG, HSC_ESTATE = 0, -1, -2, -3, -4, -5
 
@@ -164,6 +164,8 @@ def load() -> C.CDLL:
         "hsc_dep_graph_edges": (C.c_int, [_p, _p, _p, _p, C.c_size_t, C.POINTER(C.c_size_t)]),
     }
     for name, (res, args) in sig.items():
+        if not hasattr(lib, name) and os.environ.get("HSC_LIB"):
+            continue  # A/B build of an older library: bind what it has
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
