@@ -56,27 +56,60 @@ def cpu_model():
     return platform.processor()
 
 
-def cpu_baseline(c2, gpu_verdict, threads, target_s):
+def cpu_baseline(c2, gpu_verdict, threads, target_s, m0=None):
     """Oracle port of bdb_osql_serial_check (per-read-set log rescan, hash
-    lookups, linear range scan, early exit) on a deterministic every-k-th
-    sample of the same batch; also checks those verdicts against the GPU's."""
+    lookups, linear range scan, early exit) on a deterministic evenly spaced
+    sample of the same batch, on `threads` pthreads and on one core; also
+    checks those verdicts against the GPU's.  With m0 (the marshalled batch)
+    adds the build's own CPU sort-join over the full batch (SURVEY.md §8(d)
+    second CPU line: same algorithm class as the GPU, on the host cores)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     ol = oracle.OracleLog(c2.log)
     T = c2.readsets.ntxn
-    cal = np.arange(0, T, max(1, T // (8 * threads)))[: 8 * threads]
-    _, _, secs = oracle.check(ol, c2.readsets.subset(cal), nthreads=threads)
-    rate = len(cal) / max(secs, 1e-6)
-    n = int(min(T, max(len(cal), rate * target_s)))
-    sample = np.unique(np.linspace(0, T - 1, n).astype(np.int64))
+
+    def timed_sample(nthreads, budget_s):
+        cal = np.arange(0, T, max(1, T // (8 * nthreads)))[: 8 * nthreads]
+        _, _, secs = oracle.check(ol, c2.readsets.subset(cal), nthreads=nthreads)
+        rate = len(cal) / max(secs, 1e-6)
+        n = int(min(T, max(len(cal), rate * budget_s)))
+        sample = np.unique(np.linspace(0, T - 1, n).astype(np.int64))
+        rc, _, secs = oracle.check(ol, c2.readsets.subset(sample), nthreads=nthreads)
+        ok = bool(np.array_equal(rc != 0, gpu_verdict[sample] != 0))
+        return sample, secs, ok
+
+    sample, secs, ok = timed_sample(threads, target_s)
     step = T / len(sample)
-    rc, _, secs = oracle.check(ol, c2.readsets.subset(sample), nthreads=threads)
-    ok = bool(np.array_equal(rc != 0, gpu_verdict[sample] != 0))
-    return dict(value=len(sample) / secs, unit="checks/s", cores=threads, kind="port",
-                sample=f"{len(sample)} of {T} read sets (evenly spaced, 1 in {step:.1f}), oracle/serial_oracle.c "
-                       f"restatement of bdb_osql_serial_check over the {c2.log.nrec}-record log, "
-                       f"{threads} pthreads, {secs:.1f} s; cpu: {cpu_model()}",
-                parity_with_gpu=ok)
+    out = dict(value=len(sample) / secs, unit="checks/s", cores=threads, kind="port",
+               sample=f"{len(sample)} of {T} read sets (evenly spaced, 1 in {step:.1f}), "
+                      f"oracle/serial_oracle.c restatement of bdb_osql_serial_check over the "
+                      f"{c2.log.nrec}-record log, {threads} pthreads, {secs:.1f} s; cpu: {cpu_model()}",
+               parity_with_gpu=ok)
+    s1, secs1, ok1 = timed_sample(1, max(2.0, target_s / 3))
+    out["single_core"] = dict(value=len(s1) / secs1, unit="checks/s", cores=1,
+                              sample=f"{len(s1)} read sets, {secs1:.1f} s", parity_with_gpu=ok1)
+    if m0 is not None:
+        from comdb2_amd.workloads import config2_device_window
+        gid, words, lsn = config2_device_window(c2)
+        sj = oracle.SortJoin(gid, words, lsn, 1)
+        table_max = np.array([lsn.max() if len(lsn) else 0], np.uint64)  # one table (t1)
+        res = {}
+        for nt in (threads, 1):
+            verdict, secs_sj = sj.probe(m0, table_max, nthreads=nt)
+            reps = max(1, int(min(target_s / 3, 10.0) / max(secs_sj, 1e-3)))
+            tot = secs_sj
+            for _ in range(reps - 1):
+                _, s_ = sj.probe(m0, table_max, nthreads=nt)
+                tot += s_
+            res[nt] = (T * reps / tot, bool(np.array_equal(verdict != 0, gpu_verdict != 0)), reps)
+        out["sortjoin"] = dict(
+            value=res[threads][0], unit="checks/s", cores=threads, kind="build CPU sort-join",
+            single_core=res[1][0], parity_with_gpu=res[threads][1] and res[1][1],
+            sample=f"full batch ({T} read sets, {m0['n']} ranges), probe phase over a resident "
+                   f"sorted window of {sj.rows} rows (window build {sj.build_s:.1f} s, not timed); "
+                   f"oracle/sortjoin.c")
+        sj.close()
+    return out
 
 
 def bench_graph(args):
@@ -163,11 +196,14 @@ def main():
     if world > 1:  # lock probes see the table-wide max commit LSN
         v.merge_table_max(shard.allreduce_table_max(v.table_max()))
     T = c2.readsets.ntxn
+    m0 = None
     for bi in range(args.batches):
         rs = c2.readsets if bi == 0 else config2(seed=SEED_CONFIG2 + 7919 * bi,
                                                  n_commits=args.n_commits, n_txn=args.n_txn,
                                                  rank=rank, world=world, build_log=False).readsets
         m = v.marshal(rs)
+        if bi == 0 and want_cpu:
+            m0 = m
         if world > 1:
             m = shard.route(m, shards.range_mask(m, rank), shards.lock_mask(m, rank))
         batches.append(upload_batch(torch, dev, m))
@@ -284,7 +320,8 @@ def main():
         "cpu_baseline": None,
     }
     if want_cpu:
-        out["cpu_baseline"] = cpu_baseline(c2, v0, args.cpu_threads, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(c2, v0, args.cpu_threads, args.cpu_seconds,
+                                           m0=m0)
     if rank == 0:
         print(json.dumps(out), flush=True)
     v.close()

@@ -83,7 +83,7 @@ struct hsc_ctx {
     // probe workspace
     DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;
     DBuf p_verdict, p_bitmap;
-    DBuf w_hist, w_hist_tmp, w_seg, w_pre, w_counts, w_items, w_item_tile, w_recs;
+    DBuf w_code, w_hist, w_counts, w_bucket, w_cursor, w_items, w_item_tile, w_recs;
 
     // marshal output
     hsc_marshalled m{};
@@ -656,26 +656,22 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
     ProbeWork work{};
     work.lds_mode = w.ntiles <= (uint32_t)kHistCap;
     const size_t nwork = std::max<size_t>(p.n, p.n_lock);
-    size_t G = std::min<size_t>(kMaxChunks, std::max<size_t>(1, (nwork + 2047) / 2048));
-    G = std::max<size_t>(G, (p.n + kMaxChunkProbes - 1) / kMaxChunkProbes);
-    work.G = (uint32_t)G;
-    work.chunk = (uint32_t)((p.n + G - 1) / G);
-    work.regcap = std::max<uint32_t>(2 * work.chunk, 2);
-    const int rw = rec_words(w.W);
-    HIPCHK(c, c->w_hist.ensure(4 * G * nt));
-    if (!work.lds_mode) HIPCHK(c, c->w_hist_tmp.ensure(4 * G * nt));
-    HIPCHK(c, c->w_seg.ensure(4 * G * nt));
-    HIPCHK(c, c->w_pre.ensure(4 * G * nt));
+    work.G = (uint32_t)std::min<size_t>(kMaxChunks, std::max<size_t>(1, (nwork + 2047) / 2048));
+    work.chunk = (uint32_t)((p.n + work.G - 1) / work.G);
+    HIPCHK(c, c->w_code.ensure(8 * (size_t)std::max<uint32_t>(p.n, 1)));
+    HIPCHK(c, c->w_hist.ensure(4 * (size_t)work.G * nt));
     HIPCHK(c, c->w_counts.ensure(4 * ((size_t)nt + 1)));
+    HIPCHK(c, c->w_bucket.ensure(4 * ((size_t)nt + 1)));
+    HIPCHK(c, c->w_cursor.ensure(4 * ((size_t)nt + 1)));
     HIPCHK(c, c->w_items.ensure(4 * ((size_t)nt + 1)));
-    HIPCHK(c, c->w_recs.ensure(8 * (size_t)rw * G * work.regcap));
+    HIPCHK(c, c->w_recs.ensure(8 * (size_t)rec_stride(w.W) * 2 * std::max<uint32_t>(p.n, 1)));
     const uint32_t max_items = nt + (uint32_t)((2 * (size_t)p.n + kJoinChunk - 1) / kJoinChunk);
     HIPCHK(c, c->w_item_tile.ensure(4 * (size_t)max_items + 16));
+    work.code = c->w_code.as<uint64_t>();
     work.hist = c->w_hist.as<uint32_t>();
-    work.hist_tmp = c->w_hist_tmp.as<uint32_t>();
-    work.seg = c->w_seg.as<uint32_t>();
-    work.pre = c->w_pre.as<uint32_t>();
     work.counts = c->w_counts.as<uint32_t>();
+    work.bucket_off = c->w_bucket.as<uint32_t>();
+    work.cursor = c->w_cursor.as<uint32_t>();
     work.item_off = c->w_items.as<uint32_t>();
     work.item_tile = c->w_item_tile.as<uint32_t>();
     work.recs = c->w_recs.as<uint64_t>();
@@ -685,11 +681,13 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
             if (!c->ev[i]) HIPCHK(c, hipEventCreate(&c->ev[i]));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
     if (b->n_txn) HIPCHK(c, hipMemsetAsync(b->verdict, 0, b->n_txn, s));
+    if (!work.lds_mode) HIPCHK(c, hipMemsetAsync(c->w_counts.p, 0, 4 * ((size_t)nt + 1), s));
     HIPCHK(c, launch_locate(w, p, work, b->verdict, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     if (p.n && w.ntiles) {
         HIPCHK(c, launch_plan(w, work, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
+        HIPCHK(c, launch_scatter(w, p, work, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
         HIPCHK(c, launch_join(w, work, max_items, b->verdict, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
@@ -715,12 +713,9 @@ static int collect_timing(hsc_ctx *c)
     c->last.join_ms = t[3];
     c->last.pack_ms = t[4];
     (void)hipEventElapsedTime(&c->last.probe_total_ms, c->ev[0], c->ev[5]);
-    uint64_t nrec = 0;
-    if (c->ntiles && c->w_counts.p) {
-        std::vector<uint32_t> cnt(c->ntiles);
-        HIPCHK(c, hipMemcpy(cnt.data(), c->w_counts.p, 4 * (size_t)c->ntiles, hipMemcpyDeviceToHost));
-        for (uint32_t v : cnt) nrec += v;
-    }
+    uint32_t nrec = 0;
+    if (c->ntiles && c->w_bucket.p)
+        HIPCHK(c, hipMemcpy(&nrec, c->w_bucket.as<uint32_t>() + c->ntiles, 4, hipMemcpyDeviceToHost));
     c->last.records = nrec;
     return HSC_OK;
 }
@@ -828,10 +823,10 @@ void hsc_ctx_destroy(hsc_ctx *c)
     DBuf *bufs[] = {&c->d_gid, &c->d_words, &c->d_lsn, &c->d_gid2, &c->d_words2, &c->d_lsn2,
                     &c->d_flags, &c->d_scratch, &c->d_gstart, &c->d_gend, &c->d_tmax,
                     &c->d_table_max, &c->d_group_table, &c->d_count, &c->d_sp_g, &c->d_sp_w,
-                    &c->w_item_tile, &c->w_hist, &c->w_hist_tmp, &c->w_seg, &c->w_pre, &c->p_lo, &c->p_hi,
+                    &c->w_item_tile, &c->w_hist, &c->p_lo, &c->p_hi,
                     &c->p_gid, &c->p_snap, &c->p_txn, &c->p_lock_table, &c->p_lock_snap,
-                    &c->p_lock_txn, &c->p_verdict, &c->p_bitmap, &c->w_counts,
-                    &c->w_items, &c->w_recs};
+                    &c->p_lock_txn, &c->p_verdict, &c->p_bitmap, &c->w_code, &c->w_counts,
+                    &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_recs};
     for (DBuf *b : bufs) b->release();
     c->graph.release_all();
     for (auto &e : c->ev)

@@ -46,8 +46,7 @@ struct DBuf {
 constexpr int kMaxWords = 64;       // MAXKEYLEN 512 B (bbinc/cdb2_constants.h:33)
 constexpr int kTopCap = 6144;       // splitter prefixes held in LDS by the locate kernel
 constexpr int kLocateThreads = 512;
-constexpr int kMaxChunks = 512;     // probe chunks (locate workgroups)
-constexpr int kMaxChunkProbes = 4096;  // probes per chunk (8 per locate thread)
+constexpr int kMaxChunks = 512;     // probe chunks (locate / scatter workgroups)
 constexpr int kHistCap = 8192;      // tiles whose bucket counters fit in LDS
 constexpr int kJoinThreads = 512;
 constexpr int kJoinChunk = 1024;    // join records per workgroup
@@ -88,6 +87,15 @@ struct ProbeView {
 // meta = txn | lb << 32 | ub << 44 | kind << 62 ([lb, ub) = the probe's
 // group rows inside the tile).  2W+2 words -> 16-byte multiple.
 __host__ __device__ inline int rec_words(int W) { return 2 * W + 2; }
+#ifndef HSC_REC_PAD
+#define HSC_REC_PAD 0
+#endif
+// Record stride in u64: with HSC_REC_PAD records start on 64-byte sectors,
+// so a scattered record is written as whole sectors.
+__host__ __device__ inline int rec_stride(int W)
+{
+    return HSC_REC_PAD ? (rec_words(W) + 7) & ~7 : rec_words(W);
+}
 
 // Tile size: largest power of two whose keys + lsn fit the LDS budget.
 inline int tile_log2(int W)
@@ -116,21 +124,22 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
                            uint64_t *table_max, uint32_t *sp_g, uint64_t *sp_w, hipStream_t s);
 // Probe.
 struct ProbeWork {
-    uint32_t *hist;        // [G][ntiles] per chunk: offset << 16 | count per tile
-    uint32_t *hist_tmp;    // [G][ntiles] counters when ntiles > kHistCap (else unused)
-    uint32_t *seg;         // [ntiles][G] transposed hist
-    uint32_t *pre;         // [ntiles][G] records of tile t in chunks < g
-    uint32_t *counts;      // [ntiles] records per tile
+    uint64_t *code;        // [n] a | b << 31 | kind << 62
+    uint32_t *hist;        // [G][ntiles] per-chunk record counts -> offsets
+    uint32_t *counts;      // [ntiles + 1] records per tile
+    uint32_t *bucket_off;  // [ntiles + 1]
+    uint32_t *cursor;      // [ntiles] (global-atomic mode, ntiles > kHistCap)
     uint32_t *item_off;    // [ntiles + 1]
     uint32_t *item_tile;   // [max items]
-    uint64_t *recs;        // [G][regcap] join records, chunk regions grouped by tile
-    uint32_t G, chunk;     // probe chunks (one locate workgroup each)
-    uint32_t regcap;       // records per chunk region (2 * chunk)
-    int lds_mode;          // ntiles <= kHistCap: chunk counters in LDS
+    uint64_t *recs;        // join records
+    uint32_t G, chunk;     // probe chunks (one workgroup each in locate/scatter)
+    int lds_mode;          // ntiles <= kHistCap: LDS histograms, no global atomics
 };
 hipError_t launch_locate(const WinView &w, const ProbeView &p, const ProbeWork &work,
                          uint8_t *verdict, hipStream_t s);
 hipError_t launch_plan(const WinView &w, const ProbeWork &work, hipStream_t s);
+hipError_t launch_scatter(const WinView &w, const ProbeView &p, const ProbeWork &work,
+                          hipStream_t s);
 hipError_t launch_join(const WinView &w, const ProbeWork &work, uint32_t max_items,
                        uint8_t *verdict, hipStream_t s);
 // Dependency graph + SCC (hsc_graph.hip).

@@ -488,12 +488,13 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
 // probe
 // ============================================================================
 //
-// Probes are split into G contiguous chunks; chunk g is handled by locate
-// workgroup g, which writes the chunk's join records into its own region,
-// grouped by tile, and its per-tile (offset, count) row.  k_transpose turns
-// the rows into per-tile segment tables; the join workgroup of tile t reads
-// its records out of every chunk region through that table.  No global
-// atomics anywhere.
+// Probes are split into G contiguous chunks; chunk g is handled by workgroup g
+// of both k_locate and k_scatter.  k_locate counts the join records of its
+// chunk per tile in LDS and stores the row hist[g][*]; k_colscan turns every
+// column into chunk offsets inside the tile's bucket; k_plan scans the tile
+// totals.  k_scatter then seeds its LDS counters with bucket_off[t] +
+// hist[g][t], so every record slot comes from an LDS atomic: no global
+// atomics, no contention across XCDs.
 
 // 64-bit prefix of a composite key (gid, w0, ...): gid in the top gbits,
 // then the top 64 - gbits bits of w0.  Prefix order agrees with composite
@@ -582,70 +583,15 @@ __device__ __forceinline__ uint64_t tiles_max(const WinView &w, uint32_t x, uint
 }
 
 constexpr int kLocateBatch = 2;  // probes per thread advanced together
-constexpr int kLocatePer = 8;    // max probes per thread (chunk <= 8 * 512)
 
-// One join record = rec_words(W) u64: lo[W] hi[W] snap meta, with
-// meta = txn | lb << 32 | ub << 44 | kind << 62, [lb, ub) = the rows of the
-// probe's group inside the tile (so the join needs no group lookup).
-__device__ __forceinline__ void write_record(const WinView &w, uint64_t *rec, const ProbeView &p,
-                                             uint32_t q, uint32_t tile, uint64_t kind)
-{
-    const int W = w.W, rw = rec_words(W);
-    const uint32_t T = 1u << w.log2T;
-    const uint32_t ts = tile << w.log2T;
-    const uint32_t tn = min(T, w.n - ts);
-    const uint32_t g = p.gid[q];
-    const uint32_t gs = w.gstart[g], ge = w.gend[g];
-    const uint64_t lb = gs > ts ? min(gs - ts, tn) : 0;
-    const uint64_t ub = ge > ts ? min(ge - ts, tn) : 0;
-    const uint64_t meta = (uint64_t)p.txn[q] | (lb << 32) | (ub << 44) | (kind << 62);
-    ulonglong2 *r = (ulonglong2 *)rec;
-    const size_t ks = p.n;
-    auto word = [&](int k) -> uint64_t {
-        if (k < W) return p.lo[(size_t)k * ks + q];
-        if (k < 2 * W) return p.hi[(size_t)(k - W) * ks + q];
-        if (k == 2 * W) return p.snap[q];
-        return meta;
-    };
-    for (int k = 0; k < rw; k += 2) r[k >> 1] = make_ulonglong2(word(k), word(k + 1));
-}
-
-// Exclusive scan of hist[0, n) in place by one workgroup (NT threads, each
-// owning a contiguous run); also stores the packed row (offset << 16 | count).
-template <int NT>
-__device__ void block_scan_rows(uint32_t *hist, uint32_t n, uint32_t *row, uint32_t *lds16)
-{
-    const uint32_t per = (n + NT - 1) / NT;
-    const uint32_t b = threadIdx.x * per, e = min(n, b + per);
-    uint32_t sum = 0;
-    for (uint32_t i = b; i < e; ++i) sum += hist[i];
-    uint32_t total;
-    uint32_t run = block_excl_scan<NT>(sum, lds16, total);
-    for (uint32_t i = b; i < e; ++i) {
-        const uint32_t c = hist[i];
-        hist[i] = run;
-        if (row) row[i] = (run << 16) | c;
-        run += c;
-    }
-}
-
-// locate + emit: one workgroup per chunk of probes.  Phase A finds each
-// probe's first/last tile (splitter search in LDS), resolves whole middle
-// tiles from the sparse table and counts the chunk's records per tile
-// (local ranks from LDS atomics); phase B writes every record into the
-// chunk's own region, grouped by tile.  The region (<= 2 records per probe)
-// stays in L2 while it is written, so the scattered 16-byte stores leave
-// as whole lines.  The per-tile (offset, count) row of the chunk goes to
-// work.hist[g][t] for the transpose.
 __global__ __launch_bounds__(kLocateThreads) void k_locate(WinView w, ProbeView p,
                                                            ProbeWork work, uint8_t *verdict,
                                                            uint32_t ntop, uint32_t stride_t)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    __shared__ uint32_t lds16[16];
-    uint64_t *top = (uint64_t *)smem;                                // [ntop] splitter prefixes
-    uint32_t *row = work.hist + (size_t)blockIdx.x * w.ntiles;       // this chunk's row
-    uint32_t *hist = work.lds_mode ? (uint32_t *)(top + ntop) : work.hist_tmp + (size_t)blockIdx.x * w.ntiles;
+    uint64_t *top = (uint64_t *)smem;              // [ntop] splitter prefixes
+    uint32_t *hist = (uint32_t *)(top + ntop);     // [ntiles]
+    // stage the splitters: loads in batches of 8 per thread before the stores
     for (uint32_t base = 0; base < ntop; base += 8 * kLocateThreads) {
         uint64_t vw[8];
         uint32_t vg[8];
@@ -663,66 +609,76 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate(WinView w, ProbeView 
             if (i < ntop) top[i] = key_prefix(w.gbits, vg[k], vw[k]);
         }
     }
-    for (uint32_t i = threadIdx.x; i < w.ntiles; i += kLocateThreads) hist[i] = 0;
+    if (work.lds_mode)
+        for (uint32_t i = threadIdx.x; i < w.ntiles; i += kLocateThreads) hist[i] = 0;
     __syncthreads();
 
     const size_t ks = p.n;
     const uint32_t c0 = blockIdx.x * work.chunk;
     const uint32_t c1 = min(p.n, c0 + work.chunk);
-    uint64_t cd[kLocatePer];
-    uint32_t ra[kLocatePer], rb[kLocatePer];
-#pragma unroll
-    for (int it = 0; it < kLocatePer / kLocateBatch; ++it) {
+    for (uint32_t base = c0; base < c1; base += kLocateBatch * kLocateThreads) {
         constexpr int NS = 2 * kLocateBatch;
+        uint32_t qq[kLocateBatch];
+        bool valid[kLocateBatch];
         uint32_t gg[NS];
         uint64_t k0[NS];
         const uint64_t *km[NS];
         bool leq[NS];
         uint32_t cnt[NS];
-        bool valid[kLocateBatch];
-        bool any = false;
 #pragma unroll
         for (int b = 0; b < kLocateBatch; ++b) {
-            const uint32_t q0 = c0 + (it * kLocateBatch + b) * kLocateThreads + threadIdx.x;
-            valid[b] = q0 < c1;
-            any |= valid[b];
-            const uint32_t q = valid[b] ? q0 : (c0 < c1 ? c0 : 0);
-            const uint32_t g = c0 < c1 ? p.gid[q] : 0;
+            qq[b] = base + b * kLocateThreads + threadIdx.x;
+            valid[b] = qq[b] < c1;
+            const uint32_t q = valid[b] ? qq[b] : c0;
+            const uint32_t g = p.gid[q];
             gg[2 * b] = gg[2 * b + 1] = g;
-            k0[2 * b] = c0 < c1 ? p.lo[q] : 0;
-            k0[2 * b + 1] = c0 < c1 ? p.hi[q] : 0;
+            k0[2 * b] = p.lo[q];
+            k0[2 * b + 1] = p.hi[q];
             km[2 * b] = p.lo + q;
             km[2 * b + 1] = p.hi + q;
             leq[2 * b] = false;
             leq[2 * b + 1] = true;
         }
-        if (any) count_splitters<NS>(w, top, ntop, stride_t, gg, k0, km, ks, leq, cnt);
+        count_splitters<NS>(w, top, ntop, stride_t, gg, k0, km, ks, leq, cnt);
+        // middle tiles of split ranges: sparse-table maxima and snapshots are
+        // loaded for every probe of the batch before any is used
+        uint64_t mid[kLocateBatch], sn[kLocateBatch];
 #pragma unroll
         for (int b = 0; b < kLocateBatch; ++b) {
-            const int k = it * kLocateBatch + b;
-            cd[k] = 0;
-            if (!valid[b]) continue;
-            const uint32_t q = c0 + k * kLocateThreads + threadIdx.x;
             const uint32_t c = cnt[2 * b], c2 = cnt[2 * b + 1];
+            const uint32_t a = c ? c - 1 : 0, bt = c2 ? c2 - 1 : 0;
+            const bool need = valid[b] && c2 > 0 && bt > a + 1;
+            mid[b] = tiles_max(w, need ? a + 1 : 0, need ? bt - 1 : 0);
+            sn[b] = p.snap[valid[b] ? qq[b] : c0];
+            if (!need) mid[b] = 0;
+        }
+#pragma unroll
+        for (int b = 0; b < kLocateBatch; ++b) {
+            if (!valid[b]) continue;
+            const uint32_t q = qq[b];
+            const uint32_t c = cnt[2 * b], c2 = cnt[2 * b + 1];
+            uint64_t cd = 0;
             if (c2 > 0) {
                 const uint32_t a = c ? c - 1 : 0, bt = c2 - 1;
                 if (a == bt) {
-                    cd[k] = (uint64_t)a | ((uint64_t)a << 31) | (kKindFull << 62);
+                    cd = (uint64_t)a | ((uint64_t)a << 31) | (kKindFull << 62);
                 } else if (a < bt) {
-                    bool hit = false;
-                    if (bt > a + 1) hit = tiles_max(w, a + 1, bt - 1) > p.snap[q];
-                    if (hit)
+                    if (mid[b] > sn[b])
                         verdict[p.txn[q]] = 1;
                     else
-                        cd[k] = (uint64_t)a | ((uint64_t)bt << 31) | (kKindSplit << 62);
+                        cd = (uint64_t)a | ((uint64_t)bt << 31) | (kKindSplit << 62);
                 }
             }
-            if (cd[k]) {
-                const uint32_t a = (uint32_t)(cd[k] & 0x7FFFFFFFu);
-                ra[k] = atomicAdd(&hist[a], 1u);
-                if ((cd[k] >> 62) == kKindSplit) {
-                    const uint32_t bt = (uint32_t)((cd[k] >> 31) & 0x7FFFFFFFu);
-                    rb[k] = atomicAdd(&hist[bt], 1u);
+            work.code[q] = cd;
+            if (cd) {
+                const uint32_t a = (uint32_t)(cd & 0x7FFFFFFFu);
+                const uint32_t bt = (uint32_t)((cd >> 31) & 0x7FFFFFFFu);
+                if (work.lds_mode) {
+                    atomicAdd(&hist[a], 1u);
+                    if (bt != a) atomicAdd(&hist[bt], 1u);
+                } else {
+                    atomicAdd(&work.counts[a], 1u);
+                    if (bt != a) atomicAdd(&work.counts[bt], 1u);
                 }
             }
         }
@@ -733,22 +689,10 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate(WinView w, ProbeView 
         const uint32_t t = p.lock_table[q];
         if (t < w.ntables && w.table_max[t] > p.lock_snap[q]) verdict[p.lock_txn[q]] = 1;
     }
-    __syncthreads();
-    block_scan_rows<kLocateThreads>(hist, w.ntiles, row, lds16);
-    __syncthreads();
-    const int rw = rec_words(w.W);
-    uint64_t *region = work.recs + (size_t)blockIdx.x * work.regcap * rw;
-#pragma unroll
-    for (int k = 0; k < kLocatePer; ++k) {
-        if (!cd[k]) continue;
-        const uint32_t q = c0 + k * kLocateThreads + threadIdx.x;
-        const uint32_t a = (uint32_t)(cd[k] & 0x7FFFFFFFu);
-        const bool full = (cd[k] >> 62) == kKindFull;
-        write_record(w, region + (size_t)(hist[a] + ra[k]) * rw, p, q, a, full ? kRecFull : kRecHead);
-        if (!full) {
-            const uint32_t bt = (uint32_t)((cd[k] >> 31) & 0x7FFFFFFFu);
-            write_record(w, region + (size_t)(hist[bt] + rb[k]) * rw, p, q, bt, kRecTail);
-        }
+    if (work.lds_mode) {
+        __syncthreads();
+        uint32_t *row = work.hist + (size_t)blockIdx.x * w.ntiles;
+        for (uint32_t i = threadIdx.x; i < w.ntiles; i += kLocateThreads) row[i] = hist[i];
     }
 }
 
@@ -766,92 +710,260 @@ hipError_t launch_locate(const WinView &w, const ProbeView &p, const ProbeWork &
     return hipGetLastError();
 }
 
-// ---- transpose: chunk rows -> per-tile segment tables -----------------------
-// seg[t][g] = hist[g][t] (offset << 16 | count of chunk g's records of tile
-// t inside chunk g's region); pre[t][g] = records of tile t in chunks < g;
-// counts[t] = records of tile t.  64 tiles x 64 chunks per LDS step.
-__global__ __launch_bounds__(256) void k_transpose(ProbeWork work, uint32_t ntiles)
+// ---- plan ------------------------------------------------------------------
+// Column scan of hist[G][ntiles]: hist[g][t] := sum over g' < g; counts[t] :=
+// total.  A workgroup owns 16 tiles (16 lanes read 64 contiguous bytes of a
+// row) and splits the G rows into 64 segments (4 per wave); each thread holds
+// its segment's values in registers, so the scan is one pass with every load
+// in flight.  ceil(ntiles / 16) workgroups keep every CU busy.
+constexpr int kColTiles = 16, kColSegs = 64;
+constexpr int kColSegRows = kMaxChunks / kColSegs;
+__global__ __launch_bounds__(1024) void k_colscan(ProbeWork work, uint32_t ntiles)
 {
-    __shared__ uint32_t tile[64][65];
-    const uint32_t t0 = blockIdx.x * 64;
-    const int lane = lane_id(), wid = threadIdx.x >> 6;
-    uint32_t carry[16];  // running prefix of the 16 tiles this wave owns
+    __shared__ uint32_t segtot[kColSegs][kColTiles];
+    const int col = threadIdx.x % kColTiles, seg = threadIdx.x / kColTiles;
+    const uint32_t t = blockIdx.x * kColTiles + col;
+    const uint32_t per = (work.G + kColSegs - 1) / kColSegs;
+    const uint32_t g0 = seg * per;
+    uint32_t v[kColSegRows];
+    uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) carry[k] = 0;
-    for (uint32_t g0 = 0; g0 < work.G; g0 += 64) {
-        // load rows g0..g0+63, columns t0..t0+63
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint32_t r = wid * 16 + k, g = g0 + r, t = t0 + lane;
-            tile[r][lane] = (g < work.G && t < ntiles) ? work.hist[(size_t)g * ntiles + t] : 0;
-        }
-        __syncthreads();
-        // wave wid owns tiles wid*16 .. wid*16+15; lane = chunk offset
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint32_t c = wid * 16 + k, t = t0 + c, g = g0 + lane;
-            const uint32_t v = tile[lane][c];
-            uint32_t x = v & 0xFFFFu;
-#pragma unroll
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t y = __shfl_up(x, o, 64);
-                if (lane >= o) x += y;
-            }
-            const uint32_t excl = carry[k] + x - (v & 0xFFFFu);
-            if (t < ntiles && g < work.G) {
-                work.seg[(size_t)t * work.G + g] = v;
-                work.pre[(size_t)t * work.G + g] = excl;
-            }
-            carry[k] += __shfl(x, 63, 64);
-        }
-        __syncthreads();
+    for (int k = 0; k < kColSegRows; ++k) {
+        const uint32_t g = g0 + k;
+        v[k] = (k < (int)per && g < work.G && t < ntiles) ? work.hist[(size_t)g * ntiles + t] : 0;
+        sum += v[k];
     }
-    if (lane == 0)
+    segtot[seg][col] = sum;
+    __syncthreads();
+    uint32_t run = 0;
+    for (int j = 0; j < seg; ++j) run += segtot[j][col];
+    if (t < ntiles) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint32_t t = t0 + wid * 16 + k;
-            if (t < ntiles) work.counts[t] = carry[k];
+        for (int k = 0; k < kColSegRows; ++k) {
+            const uint32_t g = g0 + k;
+            if (k < (int)per && g < work.G) work.hist[(size_t)g * ntiles + t] = run;
+            run += v[k];
         }
+        if (seg == kColSegs - 1) work.counts[t] = run;
+    }
 }
 
-// ---- plan: per-tile chunks of join records, item -> tile table (one WG) ----
+// One workgroup: bucket offsets, per-tile chunk counts, item -> tile table.
+// Each thread owns 8 consecutive tiles per 8192-tile round.
 __global__ __launch_bounds__(1024) void k_plan(ProbeWork work, uint32_t ntiles)
 {
     __shared__ uint32_t lds[16];
-    uint32_t carry_i = 0;
+    uint32_t carry_b = 0, carry_i = 0;
     for (uint32_t base = 0; base < ntiles; base += 8 * 1024) {
         const uint32_t t0 = base + 8 * threadIdx.x;
-        uint32_t ch[8], si = 0;
+        uint32_t cv[8], ch[8], sb = 0, si = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) cv[k] = t0 + k < ntiles ? work.counts[t0 + k] : 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const uint32_t c = t0 + k < ntiles ? work.counts[t0 + k] : 0;
-            ch[k] = (c + kJoinChunk - 1) / kJoinChunk;
+            ch[k] = (cv[k] + kJoinChunk - 1) / kJoinChunk;
+            sb += cv[k];
             si += ch[k];
         }
-        uint32_t ti;
-        uint32_t pi = block_excl_scan<1024>(si, lds, ti) + carry_i;
+        uint32_t tb, ti;
+        uint32_t pb = block_excl_scan<1024>(sb, lds, tb);
+        uint32_t pi = block_excl_scan<1024>(si, lds, ti);
+        pb += carry_b;
+        pi += carry_i;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const uint32_t t = t0 + k;
             if (t < ntiles) {
+                work.bucket_off[t] = pb;
+                work.cursor[t] = pb;
                 work.item_off[t] = pi;
                 for (uint32_t j = 0; j < ch[k]; ++j) work.item_tile[pi + j] = t;
             }
+            pb += cv[k];
             pi += ch[k];
         }
+        carry_b += tb;
         carry_i += ti;
     }
-    if (threadIdx.x == 0) work.item_off[ntiles] = carry_i;
+    if (threadIdx.x == 0) {
+        work.bucket_off[ntiles] = carry_b;
+        work.item_off[ntiles] = carry_i;
+    }
 }
 
 hipError_t launch_plan(const WinView &w, const ProbeWork &work, hipStream_t s)
 {
-    k_transpose<<<(w.ntiles + 63) / 64, 256, 0, s>>>(work, w.ntiles);
+    if (work.lds_mode) k_colscan<<<(w.ntiles + kColTiles - 1) / kColTiles, 1024, 0, s>>>(work, w.ntiles);
     k_plan<<<1, 1024, 0, s>>>(work, w.ntiles);
     return hipGetLastError();
 }
 
-// ---- join: one workgroup per (tile, chunk of its records) --------------------
+// ---- scatter: join records grouped by tile ---------------------------------
+// One join record = rec_words(W) u64: lo[W] hi[W] snap meta, with
+// meta = txn | lb << 32 | ub << 44 | kind << 62, [lb, ub) = the rows of the
+// probe's group inside the tile (so the join needs no group lookup).
+__device__ __forceinline__ void write_record(const WinView &w, uint64_t *recs, uint32_t slot,
+                                             const ProbeView &p, uint32_t q, uint32_t tile,
+                                             uint64_t kind)
+{
+    const int W = w.W, rw = rec_words(W);
+    const uint32_t T = 1u << w.log2T;
+    const uint32_t ts = tile << w.log2T;
+    const uint32_t tn = min(T, w.n - ts);
+    const uint32_t g = p.gid[q];
+    const uint32_t gs = w.gstart[g], ge = w.gend[g];
+    const uint64_t lb = gs > ts ? min(gs - ts, tn) : 0;
+    const uint64_t ub = ge > ts ? min(ge - ts, tn) : 0;
+    const uint64_t meta = (uint64_t)p.txn[q] | (lb << 32) | (ub << 44) | (kind << 62);
+    ulonglong2 *r = (ulonglong2 *)(recs + (size_t)slot * rec_stride(W));
+    const size_t ks = p.n;
+    auto word = [&](int k) -> uint64_t {
+        if (k < W) return p.lo[(size_t)k * ks + q];
+        if (k < 2 * W) return p.hi[(size_t)(k - W) * ks + q];
+        if (k == 2 * W) return p.snap[q];
+        return meta;
+    };
+    for (int k = 0; k < rw; k += 2) r[k >> 1] = make_ulonglong2(word(k), word(k + 1));
+}
+
+// Seed the LDS slot counters of chunk blockIdx.x: bucket_off[t] + hist[g][t].
+__device__ __forceinline__ void seed_slots(const WinView &w, const ProbeWork &work,
+                                           uint32_t *base_t)
+{
+    const uint32_t *row = work.hist + (size_t)blockIdx.x * w.ntiles;
+    for (uint32_t b = 0; b < w.ntiles; b += 8 * kLocateThreads) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t i = b + k * kLocateThreads + threadIdx.x;
+            v[k] = i < w.ntiles ? work.bucket_off[i] + row[i] : 0;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t i = b + k * kLocateThreads + threadIdx.x;
+            if (i < w.ntiles) base_t[i] = v[k];
+        }
+    }
+    __syncthreads();
+}
+
+// Generic key width: one record at a time.
+__global__ __launch_bounds__(kLocateThreads) void k_scatter_any(WinView w, ProbeView p,
+                                                                ProbeWork work)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t *base_t = (uint32_t *)smem;  // [ntiles] next free slot of this chunk
+    if (work.lds_mode) seed_slots(w, work, base_t);
+    const uint32_t c0 = blockIdx.x * work.chunk;
+    const uint32_t c1 = min(p.n, c0 + work.chunk);
+    for (uint32_t q = c0 + threadIdx.x; q < c1; q += kLocateThreads) {
+        const uint64_t cd = work.code[q];
+        if (!cd) continue;
+        const uint32_t a = (uint32_t)(cd & 0x7FFFFFFFu);
+        const uint32_t b = (uint32_t)((cd >> 31) & 0x7FFFFFFFu);
+        const bool full = (cd >> 62) == kKindFull;
+        const uint32_t sa = work.lds_mode ? atomicAdd(&base_t[a], 1u) : atomicAdd(&work.cursor[a], 1u);
+        write_record(w, work.recs, sa, p, q, a, full ? kRecFull : kRecHead);
+        if (!full) {
+            const uint32_t sb = work.lds_mode ? atomicAdd(&base_t[b], 1u) : atomicAdd(&work.cursor[b], 1u);
+            write_record(w, work.recs, sb, p, q, b, kRecTail);
+        }
+    }
+}
+
+// W <= 2: every global load of a batch of kScatB probes is issued before the
+// first dependent use (probe words, then group bounds), then the LDS slot
+// atomics, then the 16-byte record stores.
+constexpr int kScatB = 4;
+template <int WT>
+__global__ __launch_bounds__(kLocateThreads) void k_scatter(WinView w, ProbeView p,
+                                                            ProbeWork work)
+{
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t *base_t = (uint32_t *)smem;
+    if (work.lds_mode) seed_slots(w, work, base_t);
+    const uint32_t c0 = blockIdx.x * work.chunk;
+    const uint32_t c1 = min(p.n, c0 + work.chunk);
+    const size_t ks = p.n;
+    const uint32_t T = 1u << w.log2T;
+    constexpr int rs = HSC_REC_PAD ? 8 : 2 * WT + 2;
+    for (uint32_t base = c0; base < c1; base += kScatB * kLocateThreads) {
+        uint64_t cd[kScatB], lo[kScatB][2], hi[kScatB][2], snap[kScatB];
+        uint32_t g[kScatB], txn[kScatB], gs[kScatB], ge[kScatB];
+#pragma unroll
+        for (int k = 0; k < kScatB; ++k) {
+            const uint32_t q0 = base + k * kLocateThreads + threadIdx.x;
+            const uint32_t q = q0 < c1 ? q0 : c0;
+            cd[k] = q0 < c1 ? work.code[q] : 0;
+            g[k] = p.gid[q];
+            txn[k] = p.txn[q];
+            snap[k] = p.snap[q];
+#pragma unroll
+            for (int j = 0; j < WT; ++j) {
+                lo[k][j] = p.lo[(size_t)j * ks + q];
+                hi[k][j] = p.hi[(size_t)j * ks + q];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kScatB; ++k) {
+            gs[k] = w.gstart[g[k]];
+            ge[k] = w.gend[g[k]];
+        }
+        uint32_t slot[kScatB][2];
+#pragma unroll
+        for (int k = 0; k < kScatB; ++k) {
+            slot[k][0] = slot[k][1] = 0;
+            if (!cd[k]) continue;
+            const uint32_t a = (uint32_t)(cd[k] & 0x7FFFFFFFu);
+            const uint32_t b = (uint32_t)((cd[k] >> 31) & 0x7FFFFFFFu);
+            slot[k][0] = work.lds_mode ? atomicAdd(&base_t[a], 1u) : atomicAdd(&work.cursor[a], 1u);
+            if ((cd[k] >> 62) != kKindFull)
+                slot[k][1] = work.lds_mode ? atomicAdd(&base_t[b], 1u) : atomicAdd(&work.cursor[b], 1u);
+        }
+#pragma unroll
+        for (int k = 0; k < kScatB; ++k) {
+            if (!cd[k]) continue;
+            const bool full = (cd[k] >> 62) == kKindFull;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (h == 1 && full) break;
+                const uint32_t tile = h == 0 ? (uint32_t)(cd[k] & 0x7FFFFFFFu)
+                                             : (uint32_t)((cd[k] >> 31) & 0x7FFFFFFFu);
+                const uint64_t kind = full ? kRecFull : (h == 0 ? kRecHead : kRecTail);
+                const uint32_t ts = tile << w.log2T;
+                const uint32_t tn = min(T, w.n - ts);
+                const uint64_t lb = gs[k] > ts ? min(gs[k] - ts, tn) : 0;
+                const uint64_t ub = ge[k] > ts ? min(ge[k] - ts, tn) : 0;
+                const uint64_t meta = (uint64_t)txn[k] | (lb << 32) | (ub << 44) | (kind << 62);
+                ulonglong2 *r = (ulonglong2 *)(work.recs + (size_t)slot[k][h] * rs);
+                if constexpr (WT == 1) {
+                    r[0] = make_ulonglong2(lo[k][0], hi[k][0]);
+                    r[1] = make_ulonglong2(snap[k], meta);
+                } else {
+                    r[0] = make_ulonglong2(lo[k][0], lo[k][1]);
+                    r[1] = make_ulonglong2(hi[k][0], hi[k][1]);
+                    r[2] = make_ulonglong2(snap[k], meta);
+                }
+            }
+        }
+    }
+}
+
+hipError_t launch_scatter(const WinView &w, const ProbeView &p, const ProbeWork &work,
+                          hipStream_t s)
+{
+    if (p.n == 0) return hipSuccess;
+    size_t lds = work.lds_mode ? (size_t)w.ntiles * 4 : 16;
+    if (w.W == 1)
+        k_scatter<1><<<work.G, kLocateThreads, lds, s>>>(w, p, work);
+    else if (w.W == 2)
+        k_scatter<2><<<work.G, kLocateThreads, lds, s>>>(w, p, work);
+    else
+        k_scatter_any<<<work.G, kLocateThreads, lds, s>>>(w, p, work);
+    return hipGetLastError();
+}
+
+// ---- join: one workgroup per (tile, chunk of records) ----------------------
 // Key compare of a probe key (words 0,1 in registers, later words at
 // kmem[j]) with tile row `row` (LDS, word j at kw[j * T + row]):
 // sign(key - row).
@@ -909,82 +1021,60 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, ProbeWork work
     const uint32_t item = blockIdx.x;
     if (item >= work.item_off[w.ntiles]) return;
     const uint32_t tile = work.item_tile[item];
-    const uint32_t rb = (item - work.item_off[tile]) * kJoinChunk;  // tile-local record range
-    const uint32_t re = min(rb + (uint32_t)kJoinChunk, work.counts[tile]);
+    const uint32_t rb = work.bucket_off[tile] + (item - work.item_off[tile]) * kJoinChunk;
+    const uint32_t re = min(rb + (uint32_t)kJoinChunk, work.bucket_off[tile + 1]);
     const int W = WT > 0 ? WT : w.W;
-    const int rw = rec_words(W);
+    const int rw = rec_stride(W);
     const uint32_t T = 1u << w.log2T;
     const uint32_t ts = tile << w.log2T;
-    const uint32_t G = work.G;
 
     uint64_t *kw = (uint64_t *)smem;               // [W][T]
     uint64_t *lsn = kw + (size_t)W * T;            // [T]
     uint64_t *b16 = lsn + T;                       // [T / 16]
-    uint64_t *b256 = b16 + T / 16;                 // [8]
-    uint32_t *pre = (uint32_t *)(b256 + 8);        // [G] records of this tile in chunks < g
-    uint32_t *seg = pre + G;                       // [G] offset << 16 | count
+    uint64_t *b256 = b16 + T / 16;                 // [T / 256]
 
-    // segment table of the tile
-    for (uint32_t g = threadIdx.x; g < G; g += kJoinThreads) {
-        pre[g] = work.pre[(size_t)tile * G + g];
-        seg[g] = work.seg[(size_t)tile * G + g];
-    }
-    // stage the tile: every thread issues all of its 16-byte loads before the
-    // LDS stores (named registers: no runtime-indexed arrays); the window is
-    // padded to whole tiles, so no bounds checks.  T == 2048 for W <= 2: two
-    // row pairs per thread.
-    static_assert(kJoinThreads * 4 == 2048, "fast staging assumes 2048-row tiles");
-    const uint32_t pr0 = threadIdx.x, pr1 = threadIdx.x + kJoinThreads;
-    ulonglong2 a0{}, a1{}, a2{}, b0{}, b1{}, b2{};
-    if constexpr (WT > 0) {
-        const uint64_t *w0 = w.words + ts, *w1 = w.words + w.stride + ts, *l = w.lsn + ts;
-        a0 = *(const ulonglong2 *)(w0 + 2 * pr0);
-        b0 = *(const ulonglong2 *)(w0 + 2 * pr1);
-        if constexpr (WT == 2) {
-            a1 = *(const ulonglong2 *)(w1 + 2 * pr0);
-            b1 = *(const ulonglong2 *)(w1 + 2 * pr1);
-        }
-        a2 = *(const ulonglong2 *)(l + 2 * pr0);
-        b2 = *(const ulonglong2 *)(l + 2 * pr1);
-    }
-    __syncthreads();
-    // this thread's records: locate them in the chunk regions and load them
+    // records of this thread (kJoinChunk / kJoinThreads of them), fetched
+    // before the tile so their latency overlaps the staging
     constexpr int kRec = kJoinChunk / kJoinThreads;
-    const uint64_t *recp[kRec];
     ulonglong2 tail[kRec];
     ulonglong2 bnd[kRec][2];
 #pragma unroll
     for (int k = 0; k < kRec; ++k) {
         const uint32_t r = rb + k * kJoinThreads + threadIdx.x;
-        recp[k] = nullptr;
-        if (r >= re) continue;
-        uint32_t lo = 0, hi = G;  // last g with pre[g] <= r and a non-empty segment
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (pre[mid] <= r) lo = mid; else hi = mid;
-        }
-        while (lo + 1 < G && pre[lo + 1] <= r) ++lo;  // skip empty segments sharing pre
-        const uint32_t sg = seg[lo];
-        const uint32_t slot = (sg >> 16) + (r - pre[lo]);
-        const uint64_t *rec = work.recs + ((size_t)lo * work.regcap + slot) * rw;
-        recp[k] = rec;
-        tail[k] = *(const ulonglong2 *)(rec + 2 * W);
-        if constexpr (WT == 2) {
-            bnd[k][0] = *(const ulonglong2 *)rec;
-            bnd[k][1] = *(const ulonglong2 *)(rec + 2);
-        } else if constexpr (WT == 1) {
-            bnd[k][0] = *(const ulonglong2 *)rec;  // lo0, hi0
+        if (r < re) {
+            const uint64_t *rec = work.recs + (size_t)r * rw;
+            tail[k] = *(const ulonglong2 *)(rec + 2 * W);
+            if constexpr (WT == 2) {
+                bnd[k][0] = *(const ulonglong2 *)rec;
+                bnd[k][1] = *(const ulonglong2 *)(rec + 2);
+            } else if constexpr (WT == 1) {
+                bnd[k][0] = *(const ulonglong2 *)rec;  // lo0, hi0
+            }
         }
     }
+
+    // stage the tile: every thread issues all of its 16-byte loads first and
+    // only then writes LDS, so its loads are in flight together.  The window
+    // arrays are padded to a whole number of tiles, so the loads need no
+    // bounds checks (rows >= tn are never searched).
     if constexpr (WT > 0) {
-        *(ulonglong2 *)(kw + 2 * pr0) = a0;
-        *(ulonglong2 *)(kw + 2 * pr1) = b0;
-        if constexpr (WT == 2) {
-            *(ulonglong2 *)(kw + T + 2 * pr0) = a1;
-            *(ulonglong2 *)(kw + T + 2 * pr1) = b1;
+        constexpr int kIt = (1 << 11) / (2 * kJoinThreads);  // T == 2048 for W <= 2
+        ulonglong2 v[kIt][WT + 1];
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+            const uint32_t pr = threadIdx.x + it * kJoinThreads;
+#pragma unroll
+            for (int j = 0; j < WT; ++j)
+                v[it][j] = *(const ulonglong2 *)(w.words + (size_t)j * w.stride + ts + 2 * pr);
+            v[it][WT] = *(const ulonglong2 *)(w.lsn + ts + 2 * pr);
         }
-        *(ulonglong2 *)(lsn + 2 * pr0) = a2;
-        *(ulonglong2 *)(lsn + 2 * pr1) = b2;
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+            const uint32_t pr = threadIdx.x + it * kJoinThreads;
+#pragma unroll
+            for (int j = 0; j < WT; ++j) *(ulonglong2 *)(kw + (size_t)j * T + 2 * pr) = v[it][j];
+            *(ulonglong2 *)(lsn + 2 * pr) = v[it][WT];
+        }
     } else {
         for (int j = 0; j <= W; ++j) {
             const uint64_t *src = j < W ? w.words + (size_t)j * w.stride + ts : w.lsn + ts;
@@ -1000,9 +1090,9 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, ProbeWork work
         uint64_t m = 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const ulonglong2 x = src[k];
-            m = x.x > m ? x.x : m;
-            m = x.y > m ? x.y : m;
+            const ulonglong2 v = src[k];
+            m = v.x > m ? v.x : m;
+            m = v.y > m ? v.y : m;
         }
         b16[threadIdx.x] = m;
     }
@@ -1016,8 +1106,9 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, ProbeWork work
 
 #pragma unroll
     for (int k = 0; k < kRec; ++k) {
-        const uint64_t *rec = recp[k];
-        if (!rec) continue;
+        const uint32_t r = rb + k * kJoinThreads + threadIdx.x;
+        if (r >= re) continue;
+        const uint64_t *rec = work.recs + (size_t)r * rw;
         const uint64_t snap = tail[k].x, meta = tail[k].y;
         const uint32_t txn = (uint32_t)meta;
         const uint32_t lb = (uint32_t)(meta >> 32) & 0xFFFu;
@@ -1062,7 +1153,7 @@ hipError_t launch_join(const WinView &w, const ProbeWork &work, uint32_t max_ite
 {
     if (max_items == 0 || w.n == 0) return hipSuccess;
     const size_t T = (size_t)1 << w.log2T;
-    const size_t lds = T * 8 * (size_t)w.W + T * 8 + (T / 16) * 8 + 8 * 8 + 8 * (size_t)work.G;
+    const size_t lds = T * 8 * (size_t)w.W + T * 8 + (T / 16) * 8 + 8 * 8;
     if (w.W == 1 && w.log2T == 11)
         k_join<1><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
     else if (w.W == 2 && w.log2T == 11)

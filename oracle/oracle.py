@@ -31,6 +31,12 @@ class _OrLog(C.Structure):
                 ("end_lsn", C.c_uint64)]
 
 
+class _SjProbes(C.Structure):
+    _fields_ = [("n", C.c_size_t), ("lo", _p), ("hi", _p), ("gid", _p), ("snap", _p), ("txn", _p),
+                ("n_lock", C.c_size_t), ("lock_table", _p), ("lock_snap", _p), ("lock_txn", _p),
+                ("table_max", _p), ("ntables", C.c_uint32)]
+
+
 def build() -> str:
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return LIB_PATH
@@ -54,6 +60,13 @@ def load():
                                  C.POINTER(_p)]
         lib.dg_free.argtypes = [_p]
         lib.dg_scc.argtypes = [C.c_uint32, C.c_size_t, _p, _p, _p]
+        lib.sj_build.restype = _p
+        lib.sj_build.argtypes = [C.c_size_t, C.c_int, C.c_uint32, _p, _p, _p, C.POINTER(C.c_double)]
+        lib.sj_free.argtypes = [_p]
+        lib.sj_rows.restype = C.c_size_t
+        lib.sj_rows.argtypes = [_p]
+        lib.sj_probe.restype = C.c_double
+        lib.sj_probe.argtypes = [_p, C.POINTER(_SjProbes), C.c_int, _p]
         lib.or_serial_check.restype = C.c_int
         lib.or_serial_check.argtypes = [C.POINTER(_OrLog), _p, C.POINTER(C.c_uint),
                                         C.POINTER(C.c_uint), C.c_int]
@@ -133,3 +146,50 @@ def scc(n, src, dst):
     out = np.zeros(max(1, n), dtype=np.uint32)
     lib.dg_scc(n, len(src), src.ctypes.data, dst.ctypes.data, out.ctypes.data)
     return out[:n]
+
+
+class SortJoin:
+    """CPU BASELINE: the build's own multi-threaded sort-join (oracle/sortjoin.c)
+    over a write window given as rows (gid u32[n], words u64[W][n], lsn u64[n])."""
+
+    def __init__(self, gid, words, lsn, ngroups: int):
+        self.lib = load()
+        words = np.ascontiguousarray(np.asarray(words, np.uint64).reshape(-1, len(lsn)))
+        self.W = words.shape[0]
+        gid = np.ascontiguousarray(gid, np.uint32)
+        lsn = np.ascontiguousarray(lsn, np.uint64)
+        secs = C.c_double()
+        self.w = self.lib.sj_build(len(lsn), self.W, ngroups, gid.ctypes.data, words.ctypes.data,
+                                   lsn.ctypes.data, C.byref(secs))
+        if not self.w:
+            raise MemoryError("sj_build")
+        self.build_s = secs.value
+        self.rows = self.lib.sj_rows(self.w)
+
+    def probe(self, m: dict, table_max, nthreads: int = 1):
+        """m: a marshalled batch (Validator.marshal).  Returns (verdict uint8
+        [n_txn] including m['forced'], wall seconds of the probe phase)."""
+        assert m["words"] == self.W
+        keep = [np.ascontiguousarray(m["lo"], np.uint64), np.ascontiguousarray(m["hi"], np.uint64),
+                np.ascontiguousarray(m["gid"], np.uint32), np.ascontiguousarray(m["snap"], np.uint64),
+                np.ascontiguousarray(m["txn"], np.uint32),
+                np.ascontiguousarray(m["lock_table"], np.uint32),
+                np.ascontiguousarray(m["lock_snap"], np.uint64),
+                np.ascontiguousarray(m["lock_txn"], np.uint32),
+                np.ascontiguousarray(table_max, np.uint64)]
+        s = _SjProbes(m["n"], *[k.ctypes.data for k in keep[:5]], m["n_lock"],
+                      *[k.ctypes.data for k in keep[5:]], len(keep[8]))
+        verdict = np.ascontiguousarray(m["forced"], np.uint8).copy()
+        secs = self.lib.sj_probe(self.w, C.byref(s), nthreads, verdict.ctypes.data)
+        return verdict, secs
+
+    def close(self):
+        if self.w:
+            self.lib.sj_free(self.w)
+            self.w = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

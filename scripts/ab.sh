@@ -1,0 +1,19 @@
+#!/bin/bash
+# A/B of library builds on one GPU box: bench.py (no CPU leg) alternating
+# between the in-tree libhsc.so and each comdb2_amd/lib/ab/*.so, ROUNDS times.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+ARGS=${AB_ARGS:---steps 20 --warmup 3 --no-cpu}
+ROUNDS=${ROUNDS:-2}
+for r in $(seq 1 $ROUNDS); do
+  for lib in cur comdb2_amd/lib/ab/*.so; do
+    name=$(basename "$lib" .so)
+    if [ "$lib" = cur ]; then env=""; else env="HSC_LIB=$PWD/$lib"; fi
+    echo "== $name round $r"
+    env $env timeout -k 10 300 python bench.py $ARGS > "gpurun_out/ab_${name}_$r.log" 2>&1
+    rc=$?
+    tail -1 "gpurun_out/ab_${name}_$r.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', d['value'], d.get('kernels_ms'), d['roofline']['frac'])" || tail -5 "gpurun_out/ab_${name}_$r.log"
+    [ $rc -ne 0 ] && exit $rc
+  done
+done
+exit 0
