@@ -91,6 +91,9 @@ struct hsc_ctx {
     std::vector<uint32_t> m_gid, m_txn, m_lock_table, m_lock_txn;
     std::vector<uint8_t> m_forced;
 
+    // raw log decode output
+    DecodedLog decoded;
+
     // dependency graph
     GraphBufs graph;
     uint32_t graph_ntxn = 0;
@@ -887,6 +890,27 @@ int hsc_window_set_end(hsc_ctx *c, uint64_t end_lsn)
     std::lock_guard<std::mutex> g(c->mu);
     c->end_lsn = end_lsn;
     return HSC_OK;
+}
+
+int hsc_decode_log(hsc_ctx *c, const hsc_raw_log *raw, const hsc_llog **out)
+{
+    if (!c || !raw || !out || (raw->nrec && (!raw->lsn || !raw->off || !raw->len || !raw->buf)) ||
+        (raw->nrecon && (!raw->recon_lsn || !raw->recon_off || !raw->recon_len || !raw->recon_keys)))
+        return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    std::string err;
+    int rc = decode_raw_log(raw, c->decoded, err);
+    if (rc) return fail(c, rc, err.c_str());
+    *out = &c->decoded.llog;
+    return HSC_OK;
+}
+
+int hsc_window_ingest_raw(hsc_ctx *c, const hsc_raw_log *raw)
+{
+    const hsc_llog *lg = nullptr;
+    int rc = hsc_decode_log(c, raw, &lg);
+    if (rc) return rc;
+    return hsc_window_ingest_log(c, lg);
 }
 
 int hsc_window_build(hsc_ctx *c)

@@ -17,6 +17,11 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <string>
+#include <vector>
+
+#include "../../include/hip_serial.h"
+
 namespace hsc {
 
 // Growable device buffer (reallocated only when a larger size is needed).
@@ -175,6 +180,21 @@ hipError_t graph_scc(uint32_t nnodes, GraphBufs &g, uint32_t *rounds, uint32_t *
 hipError_t swap_edge_words(uint32_t m, const uint32_t *src, const uint32_t *dst, uint64_t *rows,
                            hipStream_t s);
 hipError_t scan_exclusive_u32(uint32_t *a, size_t n, uint32_t *scratch, hipStream_t s);
+
+// Raw log decoder (hsc_logdec.cpp): bytes -> the hsc_llog SoA it owns.
+struct DecodedLog {
+    std::vector<uint64_t> lsn, prev, key_off;
+    std::vector<uint32_t> rectype;
+    std::vector<int16_t> isabort, ix;
+    std::vector<int32_t> table, keylen;
+    std::vector<uint8_t> keys;
+    std::vector<std::string> names;
+    std::vector<const char *> name_ptrs;
+    uint64_t end_lsn = 0;
+    hsc_llog llog{};
+    void view();  // point llog at the vectors
+};
+int decode_raw_log(const hsc_raw_log *raw, DecodedLog &out, std::string &err);
 
 hipError_t launch_pack(const uint8_t *verdict, uint32_t n_txn, uint64_t *bitmap,
                        hipStream_t s);

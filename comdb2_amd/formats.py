@@ -210,6 +210,131 @@ class LogBuilder:
 
 
 # ---------------------------------------------------------------------------
+# raw log records (the bytes a log cursor returns)
+# ---------------------------------------------------------------------------
+# Field programs, bdb/llog.src:26-225 in declaration order (see
+# comdb2_amd/csrc/hsc_logdec.cpp for the letters).
+LLOG_LAYOUTS = {
+    REC_UNDO_ADD_DTA: "TiiGGPD", REC_UNDO_ADD_IX: "TIGGPki", REC_LTRAN_COMMIT: "GPGA",
+    REC_LTRAN_START: "Gi", REC_LTRAN_COMPREC: "GPL", REC_UNDO_DEL_DTA: "TGGPiiiD",
+    REC_UNDO_DEL_IX: "TGIGPDki", REC_UNDO_UPD_DTA: "TGGGPiiDDi", REC_UNDO_UPD_IX: "TGGGPIKi",
+    REC_UNDO_ADD_DTA_LK: "TiiGGP", REC_UNDO_ADD_IX_LK: "TIGGPKi", REC_UNDO_DEL_DTA_LK: "TGGPiii",
+    REC_UNDO_DEL_IX_LK: "TGIGPki", REC_UNDO_UPD_DTA_LK: "TGGGPiii", REC_UNDO_UPD_IX_LK: "TGGGPIKi",
+}
+KEYLESS_IX = (REC_UNDO_ADD_IX, REC_UNDO_DEL_IX, REC_UNDO_DEL_IX_LK)
+
+
+@dataclasses.dataclass
+class RawLog:
+    """Log records as bytes (hsc_raw_log): record i = buf[off[i]:off[i]+len[i]]
+    at lsn[i]; recon_* = keys of keyless index records by undolsn."""
+    lsn: np.ndarray
+    off: np.ndarray
+    len: np.ndarray
+    buf: np.ndarray
+    end_lsn: int
+    recon_lsn: np.ndarray
+    recon_off: np.ndarray
+    recon_len: np.ndarray
+    recon_keys: np.ndarray
+
+
+def _be32(v: int) -> bytes:
+    return (int(v) & 0xFFFFFFFF).to_bytes(4, "big")
+
+
+def _lsn_bytes(v: int) -> bytes:
+    return _be32(int(v) >> 32) + _be32(int(v) & 0xFFFFFFFF)
+
+
+def _dbt(b: bytes) -> bytes:
+    return _be32(len(b)) + b
+
+
+def encode_record(rectype: int, prev: int, isabort: int, tbname: Optional[str], ix: int,
+                  key: Optional[bytes], hdr_prev: int, txnid: int = 0x80000001,
+                  salt: int = 0) -> bytes:
+    """One log record in the gen_rec_endian.awk encoding of a little-endian
+    host (berkdb/dist/gen_rec_endian.awk:550-630): u32/short fields and LSNs
+    big-endian, genid_t native (little-endian), DBT = u32 BE size + bytes."""
+    out = [_be32(rectype), _be32(txnid), _lsn_bytes(hdr_prev)]
+    prog = LLOG_LAYOUTS.get(int(rectype))
+    if prog is None:
+        if rectype == REC_TXN_REGOP:              # txn_auto.h:7-14
+            out += [_be32(1), _be32(salt), _dbt(b"")]
+        elif rectype == REC_TXN_REGOP_GEN:        # txn_auto.h:77-86
+            out += [_be32(1), _be32(3), (salt * 7).to_bytes(8, "big"), salt.to_bytes(8, "big"),
+                    _dbt(b"")]
+        elif rectype == REC_TXN_REGOP_ROWLOCKS:   # txn_auto.h:60-74
+            out += [_be32(1), (salt + 5).to_bytes(8, "big"), _lsn_bytes(0), _lsn_bytes(0),
+                    (salt * 7).to_bytes(8, "big"), salt.to_bytes(8, "big"), _be32(0), _be32(3),
+                    _dbt(b""), _dbt(b"")]
+        return b"".join(out)
+    for f in prog:
+        if f == "T":
+            out.append(_dbt((tbname or "").encode() + b"\x00"))
+        elif f == "D":
+            out.append(_dbt(salt.to_bytes(8, "little")))
+        elif f == "K":
+            out.append(_dbt(key or b""))
+        elif f == "I":
+            out.append(_be32(ix))
+        elif f == "i":
+            out.append(_be32(salt & 0xFFFF))
+        elif f == "G":
+            out.append((0x0123456700000000 | (salt & 0xFFFFFFFF)).to_bytes(8, "little"))
+        elif f == "P":
+            out.append(_lsn_bytes(prev))
+        elif f == "L":
+            out.append(_lsn_bytes(0))
+        elif f == "k":
+            out.append(_be32(len(key or b"")))
+        elif f == "A":
+            out.append(_be32(isabort))
+    return b"".join(out)
+
+
+def encode_raw(log: LLog) -> RawLog:
+    """The byte stream a log cursor would return for `log` (test / bench
+    input for hsc_window_ingest_raw).  Logical records get header prev_lsn =
+    lsn - 1 (the physical record they undo); for keyless index records that
+    is the undolsn under which their key goes into the reconstruct table."""
+    chunks, off, lens, recon = [], [], [], []
+    pos = 0
+    for i in range(log.nrec):
+        t = int(log.rectype[i])
+        l = int(log.lsn[i])
+        key = None
+        if int(log.keylen[i]) > 0 or t in IX_TYPES:
+            o = int(log.key_off[i])
+            key = bytes(log.keys[o:o + int(log.keylen[i])])
+        tb = log.tbnames[int(log.table[i])] if 0 <= int(log.table[i]) < len(log.tbnames) else None
+        if t in LLOG_LAYOUTS:
+            hdr_prev = 0 if t == REC_LTRAN_START else l - 1
+        else:
+            hdr_prev = int(log.prev[i])
+        if t in KEYLESS_IX:
+            recon.append((hdr_prev, key or b""))
+        rec = encode_record(t, int(log.prev[i]), int(log.isabort[i]), tb, int(log.ix[i]), key,
+                            hdr_prev, salt=i)
+        chunks.append(rec)
+        off.append(pos)
+        lens.append(len(rec))
+        pos += len(rec)
+    recon.sort()
+    rk = b"".join(k for _, k in recon)
+    roff = np.cumsum([0] + [len(k) for _, k in recon])[:-1] if recon else np.zeros(0)
+    return RawLog(lsn=np.asarray(log.lsn, np.uint64).copy(), off=np.array(off, np.uint64),
+                  len=np.array(lens, np.uint32),
+                  buf=np.frombuffer(b"".join(chunks) or b"\x00", np.uint8).copy(),
+                  end_lsn=int(log.end_lsn),
+                  recon_lsn=np.array([u for u, _ in recon], np.uint64),
+                  recon_off=np.asarray(roff, np.uint64),
+                  recon_len=np.array([len(k) for _, k in recon], np.int32),
+                  recon_keys=np.frombuffer(rk or b"\x00", np.uint8).copy())
+
+
+# ---------------------------------------------------------------------------
 # read sets
 # ---------------------------------------------------------------------------
 @dataclasses.dataclass

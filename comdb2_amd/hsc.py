@@ -54,6 +54,12 @@ class _LLog(C.Structure):
                 ("end_lsn", C.c_uint64)]
 
 
+class _RawLog(C.Structure):
+    _fields_ = [("nrec", C.c_size_t), ("lsn", _p), ("off", _p), ("len", _p), ("buf", _p),
+                ("end_lsn", C.c_uint64), ("nrecon", C.c_size_t), ("recon_lsn", _p),
+                ("recon_off", _p), ("recon_len", _p), ("recon_keys", _p)]
+
+
 class _ReadSets(C.Structure):
     _fields_ = [("ntxn", C.c_int), ("txn_off", _p), ("snap", _p), ("table", _p),
                 ("idxnum", _p), ("lflag", _p), ("rflag", _p), ("islocked", _p),
@@ -111,6 +117,7 @@ EXPORTS = [
     "hsc_marshal_readsets", "hsc_probe_device", "hsc_pack_verdicts", "hsc_synchronize",
     "hsc_get_timing",
     "hsc_enable_timing", "hsc_dep_graph_scc", "hsc_dep_graph_edges",
+    "hsc_window_ingest_raw", "hsc_decode_log",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -162,6 +169,8 @@ def load() -> C.CDLL:
         "hsc_enable_timing": (C.c_int, [_p, C.c_int]),
         "hsc_dep_graph_scc": (C.c_int, [_p, C.POINTER(_History), _p, C.POINTER(GraphStats)]),
         "hsc_dep_graph_edges": (C.c_int, [_p, _p, _p, _p, C.c_size_t, C.POINTER(C.c_size_t)]),
+        "hsc_window_ingest_raw": (C.c_int, [_p, C.POINTER(_RawLog)]),
+        "hsc_decode_log": (C.c_int, [_p, C.POINTER(_RawLog), C.POINTER(C.POINTER(_LLog))]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("HSC_LIB"):
@@ -200,6 +209,18 @@ def llog_struct(log: LLog):
                                                   "ix", "key_off", "keylen", "keys")],
               names, len(log.tbnames), int(log.end_lsn))
     return s, (cols, names)
+
+
+def rawlog_struct(raw):
+    cols = [np.ascontiguousarray(raw.lsn, np.uint64), np.ascontiguousarray(raw.off, np.uint64),
+            np.ascontiguousarray(raw.len, np.uint32), np.ascontiguousarray(raw.buf, np.uint8),
+            np.ascontiguousarray(raw.recon_lsn, np.uint64),
+            np.ascontiguousarray(raw.recon_off, np.uint64),
+            np.ascontiguousarray(raw.recon_len, np.int32),
+            np.ascontiguousarray(raw.recon_keys, np.uint8)]
+    s = _RawLog(len(cols[0]), *[_ptr(c) for c in cols[:4]], int(raw.end_lsn), len(cols[4]),
+                *[_ptr(c) for c in cols[4:]])
+    return s, cols
 
 
 def readsets_struct(rs: ReadSets):
@@ -295,6 +316,34 @@ class Validator:
     def ingest_log(self, log: LLog) -> None:
         s, keep = llog_struct(log)
         self._chk(self.lib.hsc_window_ingest_log(self.ctx, C.byref(s)), "hsc_window_ingest_log")
+
+    def ingest_raw(self, raw) -> None:
+        """Decode a raw log stream (formats.RawLog) and ingest it."""
+        s, keep = rawlog_struct(raw)
+        self._chk(self.lib.hsc_window_ingest_raw(self.ctx, C.byref(s)), "hsc_window_ingest_raw")
+
+    def decode_raw(self, raw) -> LLog:
+        """Decode only; returns the decoded stream as an LLog (copies)."""
+        s, keep = rawlog_struct(raw)
+        out = C.POINTER(_LLog)()
+        self._chk(self.lib.hsc_decode_log(self.ctx, C.byref(s), C.byref(out)), "hsc_decode_log")
+        L = out.contents
+        n = L.nrec
+
+        def arr(p, cnt, dt):
+            if cnt == 0 or not p:
+                return np.zeros(cnt, dtype=dt)
+            return np.ctypeslib.as_array(C.cast(p, C.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                         shape=(cnt,)).copy()
+        keylen = arr(L.keylen, n, np.int32)
+        key_off = arr(L.key_off, n, np.uint64)
+        nkeys = int(max([int(key_off[i]) + int(keylen[i]) for i in range(n)] + [1]))
+        return LLog(lsn=arr(L.lsn, n, np.uint64), rectype=arr(L.rectype, n, np.uint32),
+                    prev=arr(L.prev, n, np.uint64), isabort=arr(L.isabort, n, np.int16),
+                    table=arr(L.table, n, np.int32), ix=arr(L.ix, n, np.int16), key_off=key_off,
+                    keylen=keylen, keys=arr(L.keys, nkeys, np.uint8),
+                    tbnames=[L.tbnames[i].decode() for i in range(L.ntbnames)],
+                    end_lsn=int(L.end_lsn))
 
     def register_group(self, tbname: str, idxnum: int, keylen: int) -> int:
         g = self.lib.hsc_register_group(self.ctx, tbname.encode(), idxnum, keylen)

@@ -189,6 +189,35 @@ int hsc_device_count(void);
  * bdb/serializable.c:426-534) contributes its logical records' (table, ix,
  * key) at the regop's LSN.  Replaces the window. */
 int hsc_window_ingest_log(hsc_ctx *ctx, const hsc_llog *log);
+/* Raw log records as a log cursor returns them (DB_LOGC->get data): the
+ * bdb/llog.src:26-225 layouts and the txn regop records
+ * (berkdb/dbinc_auto/txn_auto.h:6-86) in the gen_rec_endian.awk on-disk
+ * encoding of a little-endian host: u32/short fields and DB_LSNs big-endian,
+ * genid_t native, DBT = u32 BE size + bytes.  Record i is lsn[i] (strictly
+ * increasing), bytes buf[off[i] .. off[i] + len[i]).  undo_add_ix /
+ * undo_del_ix / undo_del_ix_lk carry no key: the reference rebuilds it from
+ * the physical log at undolsn = the record's header prev_lsn
+ * (bdb/serializable.c:123-130,174-181); the caller passes those keys as
+ * recon_* sorted by undolsn (a missing key is HSC_ELOG). */
+typedef struct hsc_raw_log {
+    size_t nrec;
+    const uint64_t *lsn;
+    const uint64_t *off;
+    const uint32_t *len;
+    const uint8_t *buf;
+    uint64_t end_lsn;
+    size_t nrecon;
+    const uint64_t *recon_lsn;
+    const uint64_t *recon_off;
+    const int32_t *recon_len;
+    const uint8_t *recon_keys;
+} hsc_raw_log;
+/* Decode + ingest (replaces the window), = hsc_window_ingest_log of the
+ * decoded stream. */
+int hsc_window_ingest_raw(hsc_ctx *ctx, const hsc_raw_log *log);
+/* Decode only: *out points at a context-owned hsc_llog valid until the next
+ * decode on this context. */
+int hsc_decode_log(hsc_ctx *ctx, const hsc_raw_log *log, const hsc_llog **out);
 /* Append decoded writes (commit_lsn non-decreasing across calls). */
 int hsc_window_append(hsc_ctx *ctx, const hsc_write *w, size_t n);
 int hsc_window_set_end(hsc_ctx *ctx, uint64_t end_lsn);

@@ -42,10 +42,11 @@ def test_struct_layouts_match_header(tmp_path):
     prog.write_text("""#include <stdio.h>
 #include <stddef.h>
 #include "hip_serial.h"
-int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n",
+int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n",
  sizeof(hsc_currange), offsetof(hsc_currange, islocked), sizeof(hsc_currangearr),
  offsetof(hsc_currangearr, ranges), sizeof(hsc_llog), sizeof(hsc_readsets),
- sizeof(hsc_probe_batch), sizeof(hsc_timing)); return 0;}""")
+ sizeof(hsc_probe_batch), sizeof(hsc_timing), sizeof(hsc_raw_log),
+ offsetof(hsc_raw_log, recon_keys), sizeof(hsc_graph_stats)); return 0;}""")
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(prog), "-o", str(exe)],
                    check=True)
@@ -54,7 +55,8 @@ int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n",
     want = [ctypes.sizeof(hsc.CurRange), hsc.CurRange.islocked.offset,
             ctypes.sizeof(hsc.CurRangeArr), hsc.CurRangeArr.ranges.offset,
             ctypes.sizeof(hsc._LLog), ctypes.sizeof(hsc._ReadSets),
-            ctypes.sizeof(hsc.ProbeBatch), ctypes.sizeof(hsc.Timing)]
+            ctypes.sizeof(hsc.ProbeBatch), ctypes.sizeof(hsc.Timing), ctypes.sizeof(hsc._RawLog),
+            hsc._RawLog.recon_keys.offset, ctypes.sizeof(hsc.GraphStats)]
     assert got == want
 
 
