@@ -91,8 +91,9 @@ struct hsc_ctx {
     std::vector<uint32_t> m_gid, m_txn, m_lock_table, m_lock_txn;
     std::vector<uint8_t> m_forced;
 
-    // raw log decode output
+    // raw log / wire decode output
     DecodedLog decoded;
+    DecodedReadSets wire;
 
     // dependency graph
     GraphBufs graph;
@@ -911,6 +912,30 @@ int hsc_window_ingest_raw(hsc_ctx *c, const hsc_raw_log *raw)
     int rc = hsc_decode_log(c, raw, &lg);
     if (rc) return rc;
     return hsc_window_ingest_log(c, lg);
+}
+
+int hsc_decode_serial(hsc_ctx *c, const hsc_serial_msgs *m, const hsc_readsets **out)
+{
+    if (!c || !m || !out || (m->nmsg && (!m->buf || !m->off || !m->len)) || m->nmsg > 0x7FFFFFFF)
+        return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    std::string err;
+    int rc = decode_serial_msgs(m, c->wire, err);
+    if (rc) return fail(c, rc, err.c_str());
+    *out = &c->wire.rs;
+    return HSC_OK;
+}
+
+int hsc_check_serial(hsc_ctx *c, const hsc_serial_msgs *m, int *rc_out)
+{
+    if (!c || !m || (m->nmsg && !rc_out)) return HSC_EINVAL;
+    const hsc_readsets *rs = nullptr;
+    int rc = hsc_decode_serial(c, m, &rs);
+    if (rc) {  // fail closed
+        for (size_t i = 0; i < m->nmsg; ++i) rc_out[i] = 1;
+        return rc;
+    }
+    return hsc_check_readsets(c, rs, rc_out);
 }
 
 int hsc_window_build(hsc_ctx *c)

@@ -196,6 +196,19 @@ struct DecodedLog {
 };
 int decode_raw_log(const hsc_raw_log *raw, DecodedLog &out, std::string &err);
 
+// OSQL_SERIAL wire decoder (hsc_wire.cpp): payloads -> hsc_readsets SoA.
+struct DecodedReadSets {
+    std::vector<int64_t> txn_off;
+    std::vector<uint64_t> snap, lkey_off, rkey_off;
+    std::vector<int32_t> table, idxnum, lflag, rflag, islocked, lkeylen, rkeylen;
+    std::vector<uint8_t> keys;
+    std::vector<std::string> names;
+    std::vector<const char *> name_ptrs;
+    hsc_readsets rs{};
+    void view();
+};
+int decode_serial_msgs(const hsc_serial_msgs *m, DecodedReadSets &out, std::string &err);
+
 hipError_t launch_pack(const uint8_t *verdict, uint32_t n_txn, uint64_t *bitmap,
                        hipStream_t s);
 

@@ -435,3 +435,50 @@ class ReadSets:
 
     def with_snaps(self, snaps) -> "ReadSets":
         return dataclasses.replace(self, snap=np.asarray(snaps, dtype=np.uint64).copy())
+
+
+# ---------------------------------------------------------------------------
+# OSQL_SERIAL wire payloads
+# ---------------------------------------------------------------------------
+def _buf_put(b: bytes) -> bytes:
+    """buf_put (bbinc/endian_core.amd64.h:17-44): items of 2, 4 or 8 bytes are
+    byte-swapped, any other length is copied."""
+    return b[::-1] if len(b) in (2, 4, 8) else b
+
+
+def _put_i32(v: int) -> bytes:
+    return _buf_put((int(v) & 0xFFFFFFFF).to_bytes(4, "little"))
+
+
+def encode_serial(rs: "ReadSets") -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """One OSQL_SERIAL payload per read set, as osql_send_serial writes it
+    (db/osqlcomm.c:4306-4440): osql_serial_t {buf_size, arr_size, file,
+    offset} then serial_readset_put (:909-946).  Returns (buf u8, off u64,
+    len u64) for hsc_serial_msgs."""
+    chunks, offs, lens = [], [], []
+    pos = 0
+    K = rs.keys
+    for t in range(rs.ntxn):
+        body = []
+        a, b = int(rs.txn_off[t]), int(rs.txn_off[t + 1])
+        for r in range(a, b):
+            name = rs.tbnames[int(rs.table[r])].encode() + b"\x00"
+            body += [_put_i32(len(name)), _buf_put(name), _put_i32(rs.islocked[r])]
+            if not int(rs.islocked[r]):
+                body += [_put_i32(rs.idxnum[r]), _put_i32(rs.lflag[r])]
+                if not int(rs.lflag[r]):
+                    o, n = int(rs.lkey_off[r]), int(rs.lkeylen[r])
+                    body += [_put_i32(n), _buf_put(bytes(K[o:o + n]))]
+                body.append(_put_i32(rs.rflag[r]))
+                if not int(rs.rflag[r]):
+                    o, n = int(rs.rkey_off[r]), int(rs.rkeylen[r])
+                    body += [_put_i32(n), _buf_put(bytes(K[o:o + n]))]
+        body = b"".join(body)
+        f, o = lsn_split(int(rs.snap[t]))
+        msg = _put_i32(len(body)) + _put_i32(b - a) + _put_i32(f) + _put_i32(o) + body
+        chunks.append(msg)
+        offs.append(pos)
+        lens.append(len(msg))
+        pos += len(msg)
+    return (np.frombuffer(b"".join(chunks) or b"\x00", np.uint8).copy(),
+            np.array(offs, np.uint64), np.array(lens, np.uint64))

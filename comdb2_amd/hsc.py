@@ -60,6 +60,10 @@ class _RawLog(C.Structure):
                 ("recon_off", _p), ("recon_len", _p), ("recon_keys", _p)]
 
 
+class _SerialMsgs(C.Structure):
+    _fields_ = [("nmsg", C.c_size_t), ("buf", _p), ("off", _p), ("len", _p)]
+
+
 class _ReadSets(C.Structure):
     _fields_ = [("ntxn", C.c_int), ("txn_off", _p), ("snap", _p), ("table", _p),
                 ("idxnum", _p), ("lflag", _p), ("rflag", _p), ("islocked", _p),
@@ -117,7 +121,7 @@ EXPORTS = [
     "hsc_marshal_readsets", "hsc_probe_device", "hsc_pack_verdicts", "hsc_synchronize",
     "hsc_get_timing",
     "hsc_enable_timing", "hsc_dep_graph_scc", "hsc_dep_graph_edges",
-    "hsc_window_ingest_raw", "hsc_decode_log",
+    "hsc_window_ingest_raw", "hsc_decode_log", "hsc_decode_serial", "hsc_check_serial",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -171,6 +175,9 @@ def load() -> C.CDLL:
         "hsc_dep_graph_edges": (C.c_int, [_p, _p, _p, _p, C.c_size_t, C.POINTER(C.c_size_t)]),
         "hsc_window_ingest_raw": (C.c_int, [_p, C.POINTER(_RawLog)]),
         "hsc_decode_log": (C.c_int, [_p, C.POINTER(_RawLog), C.POINTER(C.POINTER(_LLog))]),
+        "hsc_decode_serial": (C.c_int, [_p, C.POINTER(_SerialMsgs),
+                                        C.POINTER(C.POINTER(_ReadSets))]),
+        "hsc_check_serial": (C.c_int, [_p, C.POINTER(_SerialMsgs), C.POINTER(C.c_int)]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("HSC_LIB"):
@@ -344,6 +351,44 @@ class Validator:
                     keylen=keylen, keys=arr(L.keys, nkeys, np.uint8),
                     tbnames=[L.tbnames[i].decode() for i in range(L.ntbnames)],
                     end_lsn=int(L.end_lsn))
+
+    def decode_serial(self, msgs) -> ReadSets:
+        """Decode OSQL_SERIAL payloads (buf, off, len) to ReadSets (copies)."""
+        buf, off, ln = [np.ascontiguousarray(a, dt) for a, dt in
+                        zip(msgs, (np.uint8, np.uint64, np.uint64))]
+        s = _SerialMsgs(len(off), _ptr(buf), _ptr(off), _ptr(ln))
+        out = C.POINTER(_ReadSets)()
+        self._chk(self.lib.hsc_decode_serial(self.ctx, C.byref(s), C.byref(out)),
+                  "hsc_decode_serial")
+        R = out.contents
+        nt = R.ntxn
+
+        def arr(p, cnt, dt):
+            if cnt == 0 or not p:
+                return np.zeros(cnt, dtype=dt)
+            return np.ctypeslib.as_array(C.cast(p, C.POINTER(np.ctypeslib.as_ctypes_type(dt))),
+                                         shape=(cnt,)).copy()
+        txn_off = arr(R.txn_off, nt + 1, np.int64)
+        nr = int(txn_off[-1]) if nt else 0
+        cols = {k: arr(getattr(R, k), nr, np.int32) for k in
+                ("table", "idxnum", "lflag", "rflag", "islocked", "lkeylen", "rkeylen")}
+        lo, ro = arr(R.lkey_off, nr, np.uint64), arr(R.rkey_off, nr, np.uint64)
+        nk = int(max([int(lo[i]) + int(cols["lkeylen"][i]) for i in range(nr)] +
+                     [int(ro[i]) + int(cols["rkeylen"][i]) for i in range(nr)] + [1]))
+        return ReadSets(txn_off=txn_off, snap=arr(R.snap, nt, np.uint64), lkey_off=lo,
+                        rkey_off=ro, keys=arr(R.keys, nk, np.uint8),
+                        tbnames=[R.tbnames[i].decode() for i in range(R.ntbnames)], **cols)
+
+    def check_serial(self, msgs) -> np.ndarray:
+        """Decode + full check of OSQL_SERIAL payloads; rc per message."""
+        buf, off, ln = [np.ascontiguousarray(a, dt) for a, dt in
+                        zip(msgs, (np.uint8, np.uint64, np.uint64))]
+        s = _SerialMsgs(len(off), _ptr(buf), _ptr(off), _ptr(ln))
+        out = np.zeros(max(1, len(off)), dtype=np.int32)
+        self._chk(self.lib.hsc_check_serial(self.ctx, C.byref(s),
+                                            out.ctypes.data_as(C.POINTER(C.c_int))),
+                  "hsc_check_serial")
+        return out[: len(off)]
 
     def register_group(self, tbname: str, idxnum: int, keylen: int) -> int:
         g = self.lib.hsc_register_group(self.ctx, tbname.encode(), idxnum, keylen)

@@ -125,6 +125,20 @@ typedef struct hsc_readsets {
     int ntbnames;
 } hsc_readsets;
 
+/* OSQL_SERIAL payloads (one read set each) as the master receives them:
+ * message i = buf[off[i] .. off[i] + len[i]), starting at the osql_serial_t
+ * header (buf_size, arr_size, file, offset; db/osqlcomm.c:748-753,809-826)
+ * followed by the serial_readset_put ranges (db/osqlcomm.c:909-946).  Every
+ * 2/4/8-byte item is byte-swapped on the wire (buf_put,
+ * bbinc/endian_core.amd64.h:17-44) -- keys and table names of those lengths
+ * included. */
+typedef struct hsc_serial_msgs {
+    size_t nmsg;
+    const uint8_t *buf;
+    const uint64_t *off;
+    const uint64_t *len;
+} hsc_serial_msgs;
+
 /* Decoded committed write (what serial_check_this_txn hands the callback). */
 typedef struct hsc_write {
     const char *tbname;
@@ -289,6 +303,13 @@ int hsc_synchronize(hsc_ctx *ctx);
 int hsc_get_timing(hsc_ctx *ctx, hsc_timing *t);
 /* Enable per-kernel HIP event timing of probes (adds event records). */
 int hsc_enable_timing(hsc_ctx *ctx, int on);
+
+/* ---- OSQL_SERIAL wire path --------------------------------------------
+ * Decode only: *out points at context-owned read sets, valid until the next
+ * decode on this context (HSC_EINVAL names the malformed message). */
+int hsc_decode_serial(hsc_ctx *ctx, const hsc_serial_msgs *msgs, const hsc_readsets **out);
+/* Decode + full check (regop_only = 0) of every message: rc_out[nmsg]. */
+int hsc_check_serial(hsc_ctx *ctx, const hsc_serial_msgs *msgs, int *rc_out);
 
 /* ---- dependency graph + SCC ------------------------
  * History of committed transactions as micro-ops (host pointers): txn ids
