@@ -15,6 +15,6 @@ run() {  # name timeout cmd...
 }
 STEPS=${STEPS:-smoke,pytest,bench}
 [[ $STEPS == *smoke* ]] && { run smoke 420 python -c "import __graft_entry__ as g; g.smoke()" || exit $?; }
-[[ $STEPS == *pytest* ]] && run pytest_gpu 600 python -m pytest tests -m gpu -x -q
+[[ $STEPS == *pytest* ]] && run pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 [[ $STEPS == *bench* ]] && run bench 420 python bench.py ${BENCH_ARGS:-}
 exit 0
