@@ -150,6 +150,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--wide", action="store_true", help="force the wide window layout")
     ap.add_argument("--config", type=int, default=2, choices=(2, 4),
                     help="2: the headline check batch; 4: dependency graph + SCC of a history")
     ap.add_argument("--history-txns", type=int, default=4_000_000)
@@ -179,6 +180,8 @@ def main():
     value_bits = 40
     batches = []
     v = hsc.Validator(local)
+    if args.wide:
+        v.set_layout(hsc.LAYOUT_WIDE)
     gid_t = v.register_group("t1", 0, 9)
     assert gid_t == 0
     c2 = config2(seed=SEED_CONFIG2, n_commits=args.n_commits, n_txn=args.n_txn, rank=rank,
@@ -295,6 +298,8 @@ def main():
             "window_keys_per_gpu": n_keys,
             "logged_writes_per_gpu": n_w,
             "parallelism": f"key-range shards x{world}" + (" + RCCL max all-reduce" if world > 1 else ""),
+            "window_layout": {hsc.LAYOUT_NARROW: "narrow (u32 tile-relative keys)",
+                              hsc.LAYOUT_WIDE: "wide"}.get(v.layout, "?"),
             "conflict_rate": float((v0 != 0).mean()),
         },
         "roofline": {

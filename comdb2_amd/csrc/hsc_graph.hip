@@ -267,7 +267,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, hipStream_t s)
     bool alt = false;
     CK(radix_sort_rows(2, nw, g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), g.wl.as<uint64_t>(), wcap,
                        g.wg2.as<uint32_t>(), g.ww2.as<uint64_t>(), g.wl2.as<uint64_t>(),
-                       g.scratch.p, g.scratch.bytes, &alt, s));
+                       g.scratch.p, g.scratch.bytes, &alt, nullptr, s));
     DBuf *sg = alt ? &g.wg2 : &g.wg, *sw = alt ? &g.ww2 : &g.ww, *sl = alt ? &g.wl2 : &g.wl;
     DBuf *dg = alt ? &g.wg : &g.wg2, *dw = alt ? &g.ww : &g.ww2, *dl = alt ? &g.wl : &g.wl2;
     CK(g.flags.ensure(4 * (wcap + 64)));
@@ -309,7 +309,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, hipStream_t s)
         bool a2 = false;
         CK(radix_sort_rows(1, n, eg->as<uint32_t>(), ew->as<uint64_t>(), et->as<uint64_t>(), ecap,
                            g.eg2.as<uint32_t>(), g.ew2.as<uint64_t>(), g.et2.as<uint64_t>(),
-                           g.scratch.p, g.scratch.bytes, &a2, s));
+                           g.scratch.p, g.scratch.bytes, &a2, nullptr, s));
         const uint64_t *rw = a2 ? g.ew2.as<uint64_t>() : g.ew.as<uint64_t>();
         uint64_t *rt = a2 ? g.et2.as<uint64_t>() : g.et.as<uint64_t>();
         CK(g.flags.ensure(4 * (n + 64)));

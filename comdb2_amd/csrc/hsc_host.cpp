@@ -77,13 +77,19 @@ struct hsc_ctx {
     size_t n = 0, cap = 0;
     uint32_t ntiles = 0;
     int log2T = 11, levels = 0;
+    int layout = HSC_LAYOUT_AUTO;  // hsc_set_layout
+    bool narrow = false;           // key32 tiles (hsc_narrow.hip)
+    int lw = 0, tz = 0;  // least significant varying limb / its constant low bits
+    DBuf d_key32;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
     DBuf d_gstart, d_gend, d_tmax, d_table_max, d_group_table, d_count, d_sp_g, d_sp_w;
 
     // probe workspace
     DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;
     DBuf p_verdict, p_bitmap;
-    DBuf w_code, w_hist, w_counts, w_bucket, w_cursor, w_items, w_item_tile, w_recs;
+    DBuf w_code, w_hist, w_counts, w_bucket, w_cursor, w_items, w_item_tile, w_recs, w_rtxn;
+    DBuf w_ncounts;               // narrow per-tile counters, zero between probes
+    bool ncounts_clean = false;
 
     // marshal output
     hsc_marshalled m{};
@@ -180,9 +186,13 @@ static void add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keyle
 // ---------------------------------------------------------------------------
 // device window build
 // ---------------------------------------------------------------------------
-// Row capacity: a whole number of 2048-row tiles (the join stages full tiles
-// without bounds checks; tiles are <= 2048 rows).
-static size_t window_cap(size_t n) { return std::max<size_t>(2048, (n + 2047) & ~(size_t)2047); }
+// Row capacity: a whole number of the largest tiles (the joins stage full
+// tiles without bounds checks).
+static size_t window_cap(size_t n)
+{
+    const size_t T = kMaxTileRows;
+    return std::max<size_t>(T, (n + T - 1) & ~(T - 1));
+}
 
 static int window_words(hsc_ctx *c)
 {
@@ -211,10 +221,11 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, hipEventCreate(&e1));
     HIPCHK(c, hipEventRecord(e0, s));
     bool in_alt = false;
+    uint64_t vary[kMaxWords + 1];
     HIPCHK(c, radix_sort_rows(W, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
                               c->d_lsn.as<uint64_t>(), cap, c->d_gid2.as<uint32_t>(),
                               c->d_words2.as<uint64_t>(), c->d_lsn2.as<uint64_t>(),
-                              c->d_scratch.p, c->d_scratch.bytes, &in_alt, s));
+                              c->d_scratch.p, c->d_scratch.bytes, &in_alt, vary, s));
     // dedupe from wherever the sort left the rows into the other buffer set
     DBuf *sg = in_alt ? &c->d_gid2 : &c->d_gid, *sw = in_alt ? &c->d_words2 : &c->d_words,
          *sl = in_alt ? &c->d_lsn2 : &c->d_lsn;
@@ -233,7 +244,40 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, hipMemcpyAsync(&nu, c->d_count.p, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     c->n = n_in ? nu : 0;
-    c->log2T = tile_log2(W);
+    // narrow layout if every 4096-row tile spans < 2^32 << tz
+    c->narrow = false;
+    c->lw = W;
+    c->tz = 0;
+    if (c->layout == HSC_LAYOUT_AUTO && c->n > 0) {
+        // vary[j]: bits of word j (j < W) / of gid (j == W) that differ
+        // between rows; limb 0 = gid, limb j + 1 = word j
+        c->lw = W;
+        c->tz = 63;  // no bit varies: one distinct key
+        for (int l = W; l >= 0; --l) {
+            const uint64_t m = l ? vary[l - 1] : vary[W];
+            if (m) {
+                c->lw = l;
+                c->tz = __builtin_ctzll(m);
+                break;
+            }
+        }
+        WinView wc{};
+        wc.words = c->d_words.as<uint64_t>();
+        wc.stride = cap;
+        wc.gid = c->d_gid.as<uint32_t>();
+        wc.n = (uint32_t)c->n;
+        wc.log2T = kNarrowLog2T;
+        wc.ntiles = (uint32_t)((c->n + kMaxTileRows - 1) >> kNarrowLog2T);
+        wc.W = W;
+        wc.lw = c->lw;
+        wc.tz = c->tz;
+        HIPCHK(c, narrow_check(wc, c->d_count.as<uint32_t>() + 4, s));
+        uint32_t wide = 1;
+        HIPCHK(c, hipMemcpyAsync(&wide, c->d_count.as<uint32_t>() + 4, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        c->narrow = wide == 0;
+    }
+    c->log2T = c->narrow ? kNarrowLog2T : tile_log2(W);
     c->ntiles = (uint32_t)((c->n + ((size_t)1 << c->log2T) - 1) >> c->log2T);
     c->levels = 0;
     while (((size_t)1 << c->levels) <= c->ntiles) c->levels++;
@@ -267,6 +311,14 @@ static int device_build(hsc_ctx *c, size_t n_in)
                               c->d_tmax.as<uint64_t>(), c->d_group_table.as<uint32_t>(),
                               c->d_table_max.as<uint64_t>(), c->d_sp_g.as<uint32_t>(),
                               c->d_sp_w.as<uint64_t>(), s));
+    if (c->narrow) {
+        HIPCHK(c, c->d_key32.ensure(4 * cap));
+        w.sp_g = c->d_sp_g.as<uint32_t>();
+        w.sp_w = c->d_sp_w.as<uint64_t>();
+        w.lw = c->lw;
+        w.tz = c->tz;
+        HIPCHK(c, narrow_keys(w, c->d_key32.as<uint32_t>(), s));
+    }
     HIPCHK(c, hipEventRecord(e1, s));
     HIPCHK(c, hipStreamSynchronize(s));
     float ms = 0;
@@ -635,7 +687,73 @@ static WinView win_view(hsc_ctx *c)
     w.levels = c->levels;
     w.gbits = 0;
     while (w.gbits < 32 && ((size_t)1 << w.gbits) < c->groups.size()) w.gbits++;
+    w.key32 = c->narrow ? c->d_key32.as<uint32_t>() : nullptr;
+    w.lw = c->lw;
+    w.tz = c->tz;
     return w;
+}
+
+// Narrow layout: locate (ranks records per tile; its last workgroup plans the
+// buckets) -> scatter -> join -> pack.
+static int probe_narrow(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w,
+                        const ProbeView &p)
+{
+    hipStream_t s = c->stream;
+    const uint32_t nt = std::max<uint32_t>(w.ntiles, 1);
+    NarrowWork nw{};
+    const size_t nwork = std::max<size_t>(p.n, p.n_lock);
+    const size_t per_wg = (size_t)kLocateThreads * 2;  // one batch of 2 probes per thread
+    nw.G = (uint32_t)std::max<size_t>(1, (nwork + per_wg - 1) / per_wg);
+    nw.chunk = (uint32_t)per_wg;
+    const size_t nrec = 2 * (size_t)std::max<uint32_t>(p.n, 1);
+    const uint32_t max_extra = (uint32_t)(nrec / kJoinChunk);
+    HIPCHK(c, c->w_code.ensure(16 * nrec));
+    void *old_counts = c->w_ncounts.p;
+    // arrival counter, n_extra, then the counters [nt * kCntStride]
+    HIPCHK(c, c->w_ncounts.ensure(4 * ((size_t)kCntStride * nt + 64)));
+    if (c->w_ncounts.p != old_counts) c->ncounts_clean = false;
+    HIPCHK(c, c->w_bucket.ensure(4 * ((size_t)nt + 1)));
+    HIPCHK(c, c->w_items.ensure(4 * (size_t)max_extra + 64));
+    HIPCHK(c, c->w_item_tile.ensure(4 * (size_t)max_extra + 16));
+    HIPCHK(c, c->w_recs.ensure(16 * nrec));
+    HIPCHK(c, c->w_rtxn.ensure(4 * nrec));
+    nw.code = c->w_code.as<uint4>();
+    // fixed slots in front of the counters (their positions must not move
+    // with ntiles: a stale n_extra must never become the arrival counter)
+    nw.done = c->w_ncounts.as<uint32_t>();
+    nw.n_extra = nw.done + 16;
+    nw.counts = nw.done + 64;
+    nw.bucket_off = c->w_bucket.as<uint32_t>();
+    nw.item_tile = c->w_item_tile.as<uint32_t>();
+    nw.item_chunk = c->w_items.as<uint32_t>();
+    nw.recs = c->w_recs.as<uint4>();
+    nw.rtxn = c->w_rtxn.as<uint32_t>();
+    const bool tm = c->timing;
+    if (tm)
+        for (int i = 0; i < 6; ++i)
+            if (!c->ev[i]) HIPCHK(c, hipEventCreate(&c->ev[i]));
+    if (!c->ncounts_clean)
+        HIPCHK(c, hipMemsetAsync(c->w_ncounts.p, 0, c->w_ncounts.bytes, s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
+    if (b->n_txn) HIPCHK(c, hipMemsetAsync(b->verdict, 0, b->n_txn, s));
+    c->ncounts_clean = false;  // until the locate's plan has re-zeroed them
+    HIPCHK(c, launch_locate_n(w, p, nw, b->verdict, s));
+    c->ncounts_clean = true;
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));  // plan: inside locate
+    if (p.n && w.ntiles) {
+        HIPCHK(c, launch_scatter_n(w, p, nw, s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
+        const bool sparse = p.n < 2 * (size_t)w.ntiles;
+        HIPCHK(c, launch_join_n(w, nw, max_extra, sparse, b->verdict, s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
+    } else if (tm) {
+        HIPCHK(c, hipEventRecord(c->ev[3], s));
+        HIPCHK(c, hipEventRecord(c->ev[4], s));
+    }
+    HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
+    return HSC_OK;
 }
 
 static int probe(hsc_ctx *c, const hsc_probe_batch *b)
@@ -656,6 +774,7 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
     p.lock_txn = b->lock_txn;
     p.n = w.n ? (uint32_t)b->n : 0;  // empty key window: no range can match
     p.n_lock = (uint32_t)b->n_lock;
+    if (c->narrow) return probe_narrow(c, b, w, p);
     const uint32_t nt = std::max<uint32_t>(w.ntiles, 1);
     ProbeWork work{};
     work.lds_mode = w.ntiles <= (uint32_t)kHistCap;
@@ -830,7 +949,8 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->w_item_tile, &c->w_hist, &c->p_lo, &c->p_hi,
                     &c->p_gid, &c->p_snap, &c->p_txn, &c->p_lock_table, &c->p_lock_snap,
                     &c->p_lock_txn, &c->p_verdict, &c->p_bitmap, &c->w_code, &c->w_counts,
-                    &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_recs};
+                    &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_recs, &c->w_rtxn,
+                    &c->w_ncounts, &c->d_key32};
     for (DBuf *b : bufs) b->release();
     c->graph.release_all();
     for (auto &e : c->ev)
@@ -985,6 +1105,20 @@ int hsc_window_ingest_device(hsc_ctx *c, size_t n, int words, const uint32_t *gi
     for (uint64_t v : c->h_table_max) c->max_commit = std::max(c->max_commit, v);
     return HSC_OK;
 }
+
+int hsc_set_layout(hsc_ctx *c, int layout)
+{
+    if (!c || (layout != HSC_LAYOUT_AUTO && layout != HSC_LAYOUT_WIDE)) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->layout != layout) {
+        c->layout = layout;
+        if (!c->host_staged) return fail(c, HSC_ESTATE, "device window must be re-ingested");
+        c->dirty = true;
+    }
+    return HSC_OK;
+}
+
+int hsc_window_layout(hsc_ctx *c) { return c && c->narrow ? HSC_LAYOUT_NARROW : HSC_LAYOUT_WIDE; }
 
 int hsc_window_words(hsc_ctx *c) { return c ? c->W : 0; }
 size_t hsc_window_keys(hsc_ctx *c) { return c ? c->n : 0; }

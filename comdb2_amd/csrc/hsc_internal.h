@@ -75,6 +75,11 @@ struct WinView {
     uint32_t n, ntiles, ntables;
     int W, log2T, levels;
     int gbits;                // bits of gid in a splitter prefix (key_prefix)
+    // narrow layout (hsc_narrow.hip): key32[i] = (K_i - K_first_of_tile) >> s
+    // for the composite key K = gid || words (limb 0 = gid, limb j+1 = word
+    // j); s = tz bits of limb lw + all limbs after lw
+    const uint32_t *key32;    // nullptr: wide layout
+    int lw, tz;
 };
 
 struct ProbeView {
@@ -102,6 +107,11 @@ __host__ __device__ inline int rec_stride(int W)
     return HSC_REC_PAD ? (rec_words(W) + 7) & ~7 : rec_words(W);
 }
 
+// Narrow layout: 4096-row tiles of (u32 key delta, u64 lsn) -- 48 KiB of LDS.
+constexpr int kNarrowLog2T = 12;
+constexpr int kMaxTileRows = 1 << kNarrowLog2T;  // window capacity is a multiple
+constexpr int kCntStride = 16;                    // u32 per per-tile record counter (64 B)
+
 // Tile size: largest power of two whose keys + lsn fit the LDS budget.
 inline int tile_log2(int W)
 {
@@ -116,7 +126,7 @@ inline int tile_log2(int W)
 hipError_t radix_sort_rows(int W, size_t n, uint32_t *gid, uint64_t *words, uint64_t *lsn,
                            size_t stride, uint32_t *gid_alt, uint64_t *words_alt,
                            uint64_t *lsn_alt, void *scratch, size_t scratch_bytes,
-                           bool *result_in_alt, hipStream_t s);
+                           bool *result_in_alt, uint64_t *vary_mask, hipStream_t s);
 size_t radix_scratch_bytes(size_t n, int W);
 hipError_t dedupe_rows(int W, size_t n, const uint32_t *gid, const uint64_t *words,
                        const uint64_t *lsn, size_t stride_in, uint32_t *gid_out,
@@ -147,6 +157,27 @@ hipError_t launch_scatter(const WinView &w, const ProbeView &p, const ProbeWork 
                           hipStream_t s);
 hipError_t launch_join(const WinView &w, const ProbeWork &work, uint32_t max_items,
                        uint8_t *verdict, hipStream_t s);
+// Narrow layout (hsc_narrow.hip).
+struct NarrowWork {
+    uint4 *code;           // [2n] per probe: {tile, rank, lo_rel, hi_rel} x (head, tail)
+    uint32_t *counts;      // [ntiles * kCntStride] records per tile (zero between batches)
+    uint32_t *bucket_off;  // [ntiles + 1]
+    uint32_t *item_tile;   // [max extra] overflow join items: tile,
+    uint32_t *item_chunk;  //   record chunk (>= 1) of the tile
+    uint32_t *n_extra;     // [1] overflow items of this batch
+    uint32_t *done;        // [1] locate workgroups finished (0 between batches)
+    uint4 *recs;           // join records {lo_rel, hi_rel, snap lo, snap hi}
+    uint32_t *rtxn;        // [records] read set of each record
+    uint32_t G, chunk;
+};
+hipError_t narrow_check(const WinView &w, uint32_t *flag, hipStream_t s);
+hipError_t narrow_keys(const WinView &w, uint32_t *key32, hipStream_t s);
+hipError_t launch_locate_n(const WinView &w, const ProbeView &p, const NarrowWork &nw,
+                           uint8_t *verdict, hipStream_t s);
+hipError_t launch_scatter_n(const WinView &w, const ProbeView &p, const NarrowWork &nw,
+                            hipStream_t s);
+hipError_t launch_join_n(const WinView &w, const NarrowWork &nw, uint32_t max_extra,
+                         bool sparse, uint8_t *verdict, hipStream_t s);
 // Dependency graph + SCC (hsc_graph.hip).
 constexpr uint64_t kDepWW = 1, kDepWR = 2, kDepRW = 4;
 struct GraphInput {              // device pointers

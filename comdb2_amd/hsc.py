@@ -122,7 +122,10 @@ EXPORTS = [
     "hsc_get_timing",
     "hsc_enable_timing", "hsc_dep_graph_scc", "hsc_dep_graph_edges",
     "hsc_window_ingest_raw", "hsc_decode_log", "hsc_decode_serial", "hsc_check_serial",
+    "hsc_set_layout", "hsc_window_layout",
 ]
+
+LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW = 0, 1, 2
 
 _lib: Optional[C.CDLL] = None
 
@@ -178,6 +181,8 @@ def load() -> C.CDLL:
         "hsc_decode_serial": (C.c_int, [_p, C.POINTER(_SerialMsgs),
                                         C.POINTER(C.POINTER(_ReadSets))]),
         "hsc_check_serial": (C.c_int, [_p, C.POINTER(_SerialMsgs), C.POINTER(C.c_int)]),
+        "hsc_set_layout": (C.c_int, [_p, C.c_int]),
+        "hsc_window_layout": (C.c_int, [_p]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("HSC_LIB"):
@@ -404,6 +409,15 @@ class Validator:
     @property
     def words(self) -> int:
         return self.lib.hsc_window_words(self.ctx)
+
+    def set_layout(self, layout: int) -> None:
+        """LAYOUT_AUTO (narrow tiles when the window fits them) or LAYOUT_WIDE."""
+        self._chk(self.lib.hsc_set_layout(self.ctx, layout), "hsc_set_layout")
+
+    @property
+    def layout(self) -> int:
+        """LAYOUT_NARROW or LAYOUT_WIDE: the layout of the current window."""
+        return self.lib.hsc_window_layout(self.ctx)
 
     @property
     def keys(self) -> int:

@@ -247,6 +247,16 @@ int hsc_register_group(hsc_ctx *ctx, const char *tbname, int idxnum, int keylen)
 int hsc_window_ingest_device(hsc_ctx *ctx, size_t n, int words,
                              const uint32_t *gid, const uint64_t *key_words,
                              const uint64_t *lsn, uint64_t end_lsn);
+/* Window layout.  AUTO: the narrow layout -- 4096-row tiles of 32-bit
+ * tile-relative key deltas -- whenever every tile of the sorted window fits
+ * it (int64 index keys over a dense or moderate value range), else WIDE (every
+ * key as its big-endian words).  WIDE forces the wide layout.  Verdicts are
+ * identical; a change applies at the next window build (host-staged windows
+ * rebuild; a device-ingested window returns HSC_ESTATE and must be
+ * re-ingested). */
+enum { HSC_LAYOUT_AUTO = 0, HSC_LAYOUT_WIDE = 1, HSC_LAYOUT_NARROW = 2 };
+int hsc_set_layout(hsc_ctx *ctx, int layout);
+int hsc_window_layout(hsc_ctx *ctx);         /* HSC_LAYOUT_WIDE or _NARROW   */
 int hsc_window_words(hsc_ctx *ctx);          /* key words per key (>= 1)     */
 size_t hsc_window_keys(hsc_ctx *ctx);        /* distinct (group, key) rows   */
 uint64_t hsc_window_end(hsc_ctx *ctx);
