@@ -171,6 +171,7 @@ __device__ __forceinline__ bool lds_any_after(const uint64_t *lsn, const uint64_
                                               const uint64_t *b256, uint32_t p, uint32_t q,
                                               uint64_t snap)
 {
+    if (q - p <= 2) return any_gt<2>(lsn, p, q, snap);
     if (q - p <= 16) return any_gt<16>(lsn, p, q, snap);
     const uint32_t p16 = (p + 15) & ~15u, q16 = q & ~15u;
     if (any_gt<15>(lsn, p, p16, snap) || any_gt<15>(lsn, q16, q, snap)) return true;

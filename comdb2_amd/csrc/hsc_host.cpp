@@ -78,18 +78,23 @@ struct hsc_ctx {
     uint32_t ntiles = 0;
     int log2T = 11, levels = 0;
     int layout = HSC_LAYOUT_AUTO;  // hsc_set_layout
-    bool narrow = false;           // key32 tiles (hsc_narrow.hip)
+    bool narrow = false;           // 64-bit codes + 16-ary index (hsc_narrow.hip)
     int lw = 0, tz = 0;  // least significant varying limb / its constant low bits
-    DBuf d_key32;
+    DBuf d_nkeys, d_nmaxs, d_nbase;
+    NarrowView nv{};
+    // the narrow window as one-word tile rows (codes) for the tile pipeline
+    WinView wn{};
+    DBuf d_nzero, d_ntmax, d_nsp_g, d_nsp_w, d_ngs, d_nscratch;
+    DBuf p_code_lo, p_code_hi, p_zero;
+    uint32_t probe_ntiles = 0;  // tiles of the view the last probe ran on
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
     DBuf d_gstart, d_gend, d_tmax, d_table_max, d_group_table, d_count, d_sp_g, d_sp_w;
 
     // probe workspace
     DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;
     DBuf p_verdict, p_bitmap;
-    DBuf w_code, w_hist, w_counts, w_bucket, w_cursor, w_items, w_item_tile, w_recs, w_rtxn;
-    DBuf w_ncounts;               // narrow per-tile counters, zero between probes
-    bool ncounts_clean = false;
+    DBuf w_code, w_hist, w_counts, w_bucket, w_cursor, w_items, w_item_tile, w_item_desc, w_recs;
+    DBuf w_dbg;  // A/B cycle counters
 
     // marshal output
     hsc_marshalled m{};
@@ -244,15 +249,13 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, hipMemcpyAsync(&nu, c->d_count.p, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     c->n = n_in ? nu : 0;
-    // narrow layout if every 4096-row tile spans < 2^32 << tz
+    // narrow layout if the whole window fits 62-bit codes (hsc_narrow.hip)
     c->narrow = false;
     c->lw = W;
-    c->tz = 0;
-    if (c->layout == HSC_LAYOUT_AUTO && c->n > 0) {
+    c->tz = 63;
+    if (c->layout != HSC_LAYOUT_WIDE && c->n > 0) {
         // vary[j]: bits of word j (j < W) / of gid (j == W) that differ
         // between rows; limb 0 = gid, limb j + 1 = word j
-        c->lw = W;
-        c->tz = 63;  // no bit varies: one distinct key
         for (int l = W; l >= 0; --l) {
             const uint64_t m = l ? vary[l - 1] : vary[W];
             if (m) {
@@ -266,18 +269,15 @@ static int device_build(hsc_ctx *c, size_t n_in)
         wc.stride = cap;
         wc.gid = c->d_gid.as<uint32_t>();
         wc.n = (uint32_t)c->n;
-        wc.log2T = kNarrowLog2T;
-        wc.ntiles = (uint32_t)((c->n + kMaxTileRows - 1) >> kNarrowLog2T);
         wc.W = W;
-        wc.lw = c->lw;
-        wc.tz = c->tz;
-        HIPCHK(c, narrow_check(wc, c->d_count.as<uint32_t>() + 4, s));
-        uint32_t wide = 1;
-        HIPCHK(c, hipMemcpyAsync(&wide, c->d_count.as<uint32_t>() + 4, 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, c->d_nbase.ensure(16 * ((size_t)W + 1)));
+        HIPCHK(c, narrow_end_rows(wc, c->d_nbase.as<uint64_t>(), s));
+        std::vector<uint64_t> ends(2 * ((size_t)W + 1));
+        HIPCHK(c, hipMemcpyAsync(ends.data(), c->d_nbase.p, 8 * ends.size(), hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
-        c->narrow = wide == 0;
+        c->narrow = narrow_span_fits(W, c->lw, c->tz, ends.data(), ends.data() + W + 1);
     }
-    c->log2T = c->narrow ? kNarrowLog2T : tile_log2(W);
+    c->log2T = tile_log2(W);
     c->ntiles = (uint32_t)((c->n + ((size_t)1 << c->log2T) - 1) >> c->log2T);
     c->levels = 0;
     while (((size_t)1 << c->levels) <= c->ntiles) c->levels++;
@@ -312,12 +312,65 @@ static int device_build(hsc_ctx *c, size_t n_in)
                               c->d_table_max.as<uint64_t>(), c->d_sp_g.as<uint32_t>(),
                               c->d_sp_w.as<uint64_t>(), s));
     if (c->narrow) {
-        HIPCHK(c, c->d_key32.ensure(4 * cap));
-        w.sp_g = c->d_sp_g.as<uint32_t>();
-        w.sp_w = c->d_sp_w.as<uint64_t>();
-        w.lw = c->lw;
-        w.tz = c->tz;
-        HIPCHK(c, narrow_keys(w, c->d_key32.as<uint32_t>(), s));
+        // level sizes: level 0 = n + 1 rounded up to whole tiles (at least one
+        // pad; the tile pipeline stages whole tiles), then roundup16(len / 16)
+        // until one 16-entry block
+        NarrowView &nv = c->nv;
+        nv = NarrowView{};
+        uint32_t len = (uint32_t)((c->n + 1 + kMaxTileRows - 1) & ~(size_t)(kMaxTileRows - 1));
+        uint64_t off = 0;
+        int L = 0;
+        for (;;) {
+            if (L == kMaxLevels) return fail(c, HSC_EINVAL, "window too large for the narrow index");
+            nv.off[L] = off;
+            nv.len[L] = len;
+            off += len;
+            ++L;
+            if (len <= 16) break;
+            len = ((len / 16) + 15) & ~15u;
+        }
+        nv.levels = L;
+        nv.lds_from = L - 1;
+        nv.lds_entries = nv.len[L - 1];
+        while (nv.lds_from > 0 && nv.lds_entries + nv.len[nv.lds_from - 1] <= 4096)
+            nv.lds_entries += nv.len[--nv.lds_from];
+        HIPCHK(c, c->d_nkeys.ensure(8 * (size_t)off));
+        HIPCHK(c, c->d_nmaxs.ensure(8 * (size_t)off));
+        nv.keys = c->d_nkeys.as<uint64_t>();
+        nv.maxs = c->d_nmaxs.as<uint64_t>();
+        nv.base = c->d_nbase.as<uint64_t>();  // row 0 limbs (narrow_end_rows)
+        nv.W = W;
+        nv.lw = c->lw;
+        nv.tz = c->tz;
+        nv.n = (uint32_t)c->n;
+        HIPCHK(c, narrow_build(w, nv, s));
+        // one-word tile view of the codes: rows (gid 0, key64), lsn
+        WinView &wn = c->wn;
+        wn = WinView{};
+        wn.words = nv.keys;
+        wn.stride = nv.len[0];
+        wn.lsn = nv.maxs;
+        wn.n = (uint32_t)c->n;
+        wn.W = 1;
+        wn.log2T = tile_log2(1);
+        wn.ntiles = (uint32_t)((c->n + ((size_t)1 << wn.log2T) - 1) >> wn.log2T);
+        wn.levels = 0;
+        while (((size_t)1 << wn.levels) <= wn.ntiles) wn.levels++;
+        HIPCHK(c, c->d_nzero.ensure(4 * (size_t)nv.len[0]));
+        HIPCHK(c, hipMemsetAsync(c->d_nzero.p, 0, 4 * (size_t)nv.len[0], s));
+        HIPCHK(c, c->d_ntmax.ensure(8 * (size_t)wn.levels * wn.ntiles));
+        HIPCHK(c, c->d_nsp_g.ensure(4 * (size_t)wn.ntiles));
+        HIPCHK(c, c->d_nsp_w.ensure(8 * (size_t)wn.ntiles));
+        HIPCHK(c, c->d_ngs.ensure(16));
+        wn.gid = c->d_nzero.as<uint32_t>();
+        wn.tmax = c->d_ntmax.as<uint64_t>();
+        HIPCHK(c, build_summaries(wn, c->d_ngs.as<uint32_t>(), c->d_ngs.as<uint32_t>() + 1, 1,
+                                  c->d_ntmax.as<uint64_t>(), nullptr, nullptr,
+                                  c->d_nsp_g.as<uint32_t>(), c->d_nsp_w.as<uint64_t>(), s));
+        wn.gstart = c->d_ngs.as<uint32_t>();
+        wn.gend = c->d_ngs.as<uint32_t>() + 1;
+        wn.sp_g = c->d_nsp_g.as<uint32_t>();
+        wn.sp_w = c->d_nsp_w.as<uint64_t>();
     }
     HIPCHK(c, hipEventRecord(e1, s));
     HIPCHK(c, hipStreamSynchronize(s));
@@ -687,79 +740,38 @@ static WinView win_view(hsc_ctx *c)
     w.levels = c->levels;
     w.gbits = 0;
     while (w.gbits < 32 && ((size_t)1 << w.gbits) < c->groups.size()) w.gbits++;
-    w.key32 = c->narrow ? c->d_key32.as<uint32_t>() : nullptr;
-    w.lw = c->lw;
-    w.tz = c->tz;
     return w;
 }
 
-// Narrow layout: locate (ranks records per tile; its last workgroup plans the
-// buckets) -> scatter -> join -> pack.
+// Narrow layout: one kernel answers every range and table lock.
 static int probe_narrow(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w,
                         const ProbeView &p)
 {
     hipStream_t s = c->stream;
-    const uint32_t nt = std::max<uint32_t>(w.ntiles, 1);
-    NarrowWork nw{};
-    const size_t nwork = std::max<size_t>(p.n, p.n_lock);
-    const size_t per_wg = (size_t)kLocateThreads * 2;  // one batch of 2 probes per thread
-    nw.G = (uint32_t)std::max<size_t>(1, (nwork + per_wg - 1) / per_wg);
-    nw.chunk = (uint32_t)per_wg;
-    const size_t nrec = 2 * (size_t)std::max<uint32_t>(p.n, 1);
-    const uint32_t max_extra = (uint32_t)(nrec / kJoinChunk);
-    HIPCHK(c, c->w_code.ensure(16 * nrec));
-    void *old_counts = c->w_ncounts.p;
-    // arrival counter, n_extra, then the counters [nt * kCntStride]
-    HIPCHK(c, c->w_ncounts.ensure(4 * ((size_t)kCntStride * nt + 64)));
-    if (c->w_ncounts.p != old_counts) c->ncounts_clean = false;
-    HIPCHK(c, c->w_bucket.ensure(4 * ((size_t)nt + 1)));
-    HIPCHK(c, c->w_items.ensure(4 * (size_t)max_extra + 64));
-    HIPCHK(c, c->w_item_tile.ensure(4 * (size_t)max_extra + 16));
-    HIPCHK(c, c->w_recs.ensure(16 * nrec));
-    HIPCHK(c, c->w_rtxn.ensure(4 * nrec));
-    nw.code = c->w_code.as<uint4>();
-    // fixed slots in front of the counters (their positions must not move
-    // with ntiles: a stale n_extra must never become the arrival counter)
-    nw.done = c->w_ncounts.as<uint32_t>();
-    nw.n_extra = nw.done + 16;
-    nw.counts = nw.done + 64;
-    nw.bucket_off = c->w_bucket.as<uint32_t>();
-    nw.item_tile = c->w_item_tile.as<uint32_t>();
-    nw.item_chunk = c->w_items.as<uint32_t>();
-    nw.recs = c->w_recs.as<uint4>();
-    nw.rtxn = c->w_rtxn.as<uint32_t>();
+    NarrowView nv = c->nv;
+    nv.table_max = w.table_max;
+    nv.ntables = w.ntables;
     const bool tm = c->timing;
     if (tm)
         for (int i = 0; i < 6; ++i)
             if (!c->ev[i]) HIPCHK(c, hipEventCreate(&c->ev[i]));
-    if (!c->ncounts_clean)
-        HIPCHK(c, hipMemsetAsync(c->w_ncounts.p, 0, c->w_ncounts.bytes, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
     if (b->n_txn) HIPCHK(c, hipMemsetAsync(b->verdict, 0, b->n_txn, s));
-    c->ncounts_clean = false;  // until the locate's plan has re-zeroed them
-    HIPCHK(c, launch_locate_n(w, p, nw, b->verdict, s));
-    c->ncounts_clean = true;
-    if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
-    if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));  // plan: inside locate
-    if (p.n && w.ntiles) {
-        HIPCHK(c, launch_scatter_n(w, p, nw, s));
-        if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
-        const bool sparse = p.n < 2 * (size_t)w.ntiles;
-        HIPCHK(c, launch_join_n(w, nw, max_extra, sparse, b->verdict, s));
-        if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
-    } else if (tm) {
-        HIPCHK(c, hipEventRecord(c->ev[3], s));
-        HIPCHK(c, hipEventRecord(c->ev[4], s));
-    }
+    // timing slots: locate = verdict clear, plan = scatter = 0, join = the probe
+    if (tm)
+        for (int i = 1; i <= 3; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
+    HIPCHK(c, launch_probe_narrow(nv, p, b->verdict, s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
     HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
     return HSC_OK;
 }
 
+static int probe_tiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w, const ProbeView &p);
+
 static int probe(hsc_ctx *c, const hsc_probe_batch *b)
 {
     if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
-    hipStream_t s = c->stream;
     const WinView w = win_view(c);
     if (b->n > 0xFFFFFFFFull / 2 || b->n_lock > 0xFFFFFFFFull || b->n_txn > 0xFFFFFFFFull)
         return fail(c, HSC_EINVAL, "batch too large");
@@ -774,7 +786,40 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
     p.lock_txn = b->lock_txn;
     p.n = w.n ? (uint32_t)b->n : 0;  // empty key window: no range can match
     p.n_lock = (uint32_t)b->n_lock;
-    if (c->narrow) return probe_narrow(c, b, w, p);
+    if (!c->narrow) return probe_tiles(c, b, w, p);
+    // narrow window: a sparse batch is answered by the direct probe; a dense
+    // one maps its bounds to codes and runs the tile pipeline on the codes
+    const bool direct = c->layout == HSC_LAYOUT_NARROW_DIRECT ||
+                        (c->layout != HSC_LAYOUT_NARROW_TILES &&
+                         (size_t)p.n < kDirectPerTile * (size_t)c->wn.ntiles);
+    if (direct) {
+        c->probe_ntiles = 0;
+        return probe_narrow(c, b, w, p);
+    }
+    WinView wn = c->wn;
+    wn.table_max = w.table_max;
+    wn.ntables = w.ntables;
+    const size_t n = std::max<uint32_t>(p.n, 1);
+    HIPCHK(c, c->p_code_lo.ensure(8 * n));
+    HIPCHK(c, c->p_code_hi.ensure(8 * n));
+    const size_t zb = c->p_zero.bytes;
+    HIPCHK(c, c->p_zero.ensure(4 * n));
+    if (c->p_zero.bytes != zb) HIPCHK(c, hipMemsetAsync(c->p_zero.p, 0, c->p_zero.bytes, c->stream));
+    NarrowView nv = c->nv;
+    HIPCHK(c, narrow_codes(nv, p, c->p_code_lo.as<uint64_t>(), c->p_code_hi.as<uint64_t>(),
+                           c->stream));
+    ProbeView pn = p;
+    pn.lo = c->p_code_lo.as<uint64_t>();
+    pn.hi = c->p_code_hi.as<uint64_t>();
+    pn.gid = c->p_zero.as<uint32_t>();
+    return probe_tiles(c, b, wn, pn);
+}
+
+// The tile pipeline: locate -> plan -> scatter -> join -> pack.
+static int probe_tiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w, const ProbeView &p)
+{
+    hipStream_t s = c->stream;
+    c->probe_ntiles = w.ntiles;
     const uint32_t nt = std::max<uint32_t>(w.ntiles, 1);
     ProbeWork work{};
     work.lds_mode = w.ntiles <= (uint32_t)kHistCap;
@@ -790,6 +835,13 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
     HIPCHK(c, c->w_recs.ensure(8 * (size_t)rec_stride(w.W) * 2 * std::max<uint32_t>(p.n, 1)));
     const uint32_t max_items = nt + (uint32_t)((2 * (size_t)p.n + kJoinChunk - 1) / kJoinChunk);
     HIPCHK(c, c->w_item_tile.ensure(4 * (size_t)max_items + 16));
+    HIPCHK(c, c->w_item_desc.ensure(16 * (size_t)max_items + 16));
+    work.item_desc = c->w_item_desc.as<uint4>();
+    if (getenv("HSC_DBG_CYCLES")) {
+        HIPCHK(c, c->w_dbg.ensure(8 * 4 * 4096));
+        HIPCHK(c, hipMemsetAsync(c->w_dbg.p, 0, 8 * 4 * 4096, s));
+        work.dbg = c->w_dbg.as<uint64_t>();
+    }
     work.code = c->w_code.as<uint64_t>();
     work.hist = c->w_hist.as<uint32_t>();
     work.counts = c->w_counts.as<uint32_t>();
@@ -837,9 +889,23 @@ static int collect_timing(hsc_ctx *c)
     c->last.pack_ms = t[4];
     (void)hipEventElapsedTime(&c->last.probe_total_ms, c->ev[0], c->ev[5]);
     uint32_t nrec = 0;
-    if (c->ntiles && c->w_bucket.p)
-        HIPCHK(c, hipMemcpy(&nrec, c->w_bucket.as<uint32_t>() + c->ntiles, 4, hipMemcpyDeviceToHost));
+    if (c->probe_ntiles && c->w_bucket.p)
+        HIPCHK(c, hipMemcpy(&nrec, c->w_bucket.as<uint32_t>() + c->probe_ntiles, 4,
+                            hipMemcpyDeviceToHost));
     c->last.records = nrec;
+    if (getenv("HSC_DBG_CYCLES") && c->w_dbg.p) {
+        std::vector<uint64_t> d(4 * 4096);
+        HIPCHK(c, hipMemcpy(d.data(), c->w_dbg.p, 8 * d.size(), hipMemcpyDeviceToHost));
+        double st = 0, se = 0, it = 0, tot = 0;
+        int nb = 0;
+        for (int b = 0; b < 4096; ++b)
+            if (d[4 * b + 3]) {
+                st += d[4 * b]; se += d[4 * b + 1]; it += d[4 * b + 2]; tot += d[4 * b + 3]; ++nb;
+            }
+        if (nb)
+            fprintf(stderr, "join cycles/WG: stage %.0f search %.0f total %.0f items %.2f (WGs %d)\n",
+                    st / nb, se / nb, tot / nb, it / nb, nb);
+    }
     return HSC_OK;
 }
 
@@ -949,8 +1015,10 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->w_item_tile, &c->w_hist, &c->p_lo, &c->p_hi,
                     &c->p_gid, &c->p_snap, &c->p_txn, &c->p_lock_table, &c->p_lock_snap,
                     &c->p_lock_txn, &c->p_verdict, &c->p_bitmap, &c->w_code, &c->w_counts,
-                    &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_recs, &c->w_rtxn,
-                    &c->w_ncounts, &c->d_key32};
+                    &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_item_desc, &c->w_recs, &c->w_dbg,
+                    &c->d_nkeys, &c->d_nmaxs, &c->d_nbase, &c->d_nzero, &c->d_ntmax,
+                    &c->d_nsp_g, &c->d_nsp_w, &c->d_ngs, &c->d_nscratch, &c->p_code_lo,
+                    &c->p_code_hi, &c->p_zero};
     for (DBuf *b : bufs) b->release();
     c->graph.release_all();
     for (auto &e : c->ev)
@@ -1108,10 +1176,13 @@ int hsc_window_ingest_device(hsc_ctx *c, size_t n, int words, const uint32_t *gi
 
 int hsc_set_layout(hsc_ctx *c, int layout)
 {
-    if (!c || (layout != HSC_LAYOUT_AUTO && layout != HSC_LAYOUT_WIDE)) return HSC_EINVAL;
+    if (!c || layout < HSC_LAYOUT_AUTO || layout > HSC_LAYOUT_NARROW_TILES ||
+        layout == HSC_LAYOUT_NARROW)
+        return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    if (c->layout != layout) {
-        c->layout = layout;
+    const bool rebuild = (c->layout == HSC_LAYOUT_WIDE) != (layout == HSC_LAYOUT_WIDE);
+    c->layout = layout;
+    if (rebuild) {
         if (!c->host_staged) return fail(c, HSC_ESTATE, "device window must be re-ingested");
         c->dirty = true;
     }

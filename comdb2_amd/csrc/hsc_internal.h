@@ -53,9 +53,10 @@ constexpr int kTopCap = 6144;       // splitter prefixes held in LDS by the loca
 constexpr int kLocateThreads = 512;
 constexpr int kMaxChunks = 512;     // probe chunks (locate / scatter workgroups)
 constexpr int kHistCap = 8192;      // tiles whose bucket counters fit in LDS
+constexpr int kDirectPerTile = 8;   // narrow: direct probe below 8 ranges per tile
 constexpr int kJoinThreads = 512;
 constexpr int kJoinChunk = 1024;    // join records per workgroup
-constexpr int kLdsJoinBudget = 49152;
+constexpr int kLdsJoinBudget = 65536;
 
 // Probe codes written by the locate kernel: a | b << 31 | kind << 62.
 constexpr uint64_t kKindFull = 1, kKindSplit = 2;
@@ -75,11 +76,6 @@ struct WinView {
     uint32_t n, ntiles, ntables;
     int W, log2T, levels;
     int gbits;                // bits of gid in a splitter prefix (key_prefix)
-    // narrow layout (hsc_narrow.hip): key32[i] = (K_i - K_first_of_tile) >> s
-    // for the composite key K = gid || words (limb 0 = gid, limb j+1 = word
-    // j); s = tz bits of limb lw + all limbs after lw
-    const uint32_t *key32;    // nullptr: wide layout
-    int lw, tz;
 };
 
 struct ProbeView {
@@ -107,15 +103,12 @@ __host__ __device__ inline int rec_stride(int W)
     return HSC_REC_PAD ? (rec_words(W) + 7) & ~7 : rec_words(W);
 }
 
-// Narrow layout: 4096-row tiles of (u32 key delta, u64 lsn) -- 48 KiB of LDS.
-constexpr int kNarrowLog2T = 12;
-constexpr int kMaxTileRows = 1 << kNarrowLog2T;  // window capacity is a multiple
-constexpr int kCntStride = 16;                    // u32 per per-tile record counter (64 B)
+constexpr int kMaxTileRows = 4096;  // window capacity is a multiple of this
 
 // Tile size: largest power of two whose keys + lsn fit the LDS budget.
 inline int tile_log2(int W)
 {
-    int l = 11;
+    int l = 12;
     while (l > 6 && ((size_t)1 << l) * (size_t)(8 * W + 8) > (size_t)kLdsJoinBudget)
         --l;
     return l;
@@ -146,6 +139,8 @@ struct ProbeWork {
     uint32_t *cursor;      // [ntiles] (global-atomic mode, ntiles > kHistCap)
     uint32_t *item_off;    // [ntiles + 1]
     uint32_t *item_tile;   // [max items]
+    uint4 *item_desc;      // [max items] {tile, first record, end record, 0}
+    uint64_t *dbg;         // A/B cycle counters (HSC_AB_CYCLES builds), may be null
     uint64_t *recs;        // join records
     uint32_t G, chunk;     // probe chunks (one workgroup each in locate/scatter)
     int lds_mode;          // ntiles <= kHistCap: LDS histograms, no global atomics
@@ -157,27 +152,32 @@ hipError_t launch_scatter(const WinView &w, const ProbeView &p, const ProbeWork 
                           hipStream_t s);
 hipError_t launch_join(const WinView &w, const ProbeWork &work, uint32_t max_items,
                        uint8_t *verdict, hipStream_t s);
-// Narrow layout (hsc_narrow.hip).
-struct NarrowWork {
-    uint4 *code;           // [2n] per probe: {tile, rank, lo_rel, hi_rel} x (head, tail)
-    uint32_t *counts;      // [ntiles * kCntStride] records per tile (zero between batches)
-    uint32_t *bucket_off;  // [ntiles + 1]
-    uint32_t *item_tile;   // [max extra] overflow join items: tile,
-    uint32_t *item_chunk;  //   record chunk (>= 1) of the tile
-    uint32_t *n_extra;     // [1] overflow items of this batch
-    uint32_t *done;        // [1] locate workgroups finished (0 between batches)
-    uint4 *recs;           // join records {lo_rel, hi_rel, snap lo, snap hi}
-    uint32_t *rtxn;        // [records] read set of each record
-    uint32_t G, chunk;
+// Narrow layout (hsc_narrow.hip): key64[i] = (K_i - K_0) >> s for the
+// composite key K = gid || words (limb 0 = gid, limb j+1 = word j), s = tz
+// bits of limb lw + every limb after lw; a 16-ary tree of key levels and a
+// parallel tree of LSN maxima.
+constexpr int kMaxLevels = 16;
+struct NarrowView {
+    const uint64_t *keys;      // key levels; level l at keys + off[l], len[l] entries
+    const uint64_t *maxs;      // LSN max levels (level 0 = row LSNs), same offsets
+    uint64_t off[kMaxLevels];
+    uint32_t len[kMaxLevels];  // multiples of 16; the top level has 16 entries
+    int levels;
+    int lds_from;              // levels >= lds_from are staged in LDS
+    uint32_t lds_entries;
+    const uint64_t *base;      // [1 + W] limbs of K_0 (device)
+    int W, lw, tz;
+    uint32_t n;
+    const uint64_t *table_max;
+    uint32_t ntables;
 };
-hipError_t narrow_check(const WinView &w, uint32_t *flag, hipStream_t s);
-hipError_t narrow_keys(const WinView &w, uint32_t *key32, hipStream_t s);
-hipError_t launch_locate_n(const WinView &w, const ProbeView &p, const NarrowWork &nw,
-                           uint8_t *verdict, hipStream_t s);
-hipError_t launch_scatter_n(const WinView &w, const ProbeView &p, const NarrowWork &nw,
-                            hipStream_t s);
-hipError_t launch_join_n(const WinView &w, const NarrowWork &nw, uint32_t max_extra,
-                         bool sparse, uint8_t *verdict, hipStream_t s);
+bool narrow_span_fits(int W, int lw, int tz, const uint64_t *first, const uint64_t *last);
+hipError_t narrow_end_rows(const WinView &w, uint64_t *out, hipStream_t s);
+hipError_t narrow_build(const WinView &w, const NarrowView &nv, hipStream_t s);
+hipError_t launch_probe_narrow(const NarrowView &nv, const ProbeView &p, uint8_t *verdict,
+                               hipStream_t s);
+hipError_t narrow_codes(const NarrowView &nv, const ProbeView &p, uint64_t *lo64, uint64_t *hi64,
+                        hipStream_t s);
 // Dependency graph + SCC (hsc_graph.hip).
 constexpr uint64_t kDepWW = 1, kDepWR = 2, kDepRW = 4;
 struct GraphInput {              // device pointers

@@ -168,7 +168,9 @@ typedef struct hsc_probe_batch {
     uint64_t *bitmap;         /* [ceil(n_txn/64)] out (may be NULL)            */
 } hsc_probe_batch;
 
-/* Per-kernel device time of the last probe / window build, in ms. */
+/* Per-kernel device time of the last probe / window build, in ms.  Wide
+ * layout: locate, plan, scatter, join, pack kernels.  Narrow layout: locate =
+ * verdict clear, join = the single probe kernel, pack; plan = scatter = 0. */
 typedef struct hsc_timing {
     float locate_ms, plan_ms, scatter_ms, join_ms, pack_ms, probe_total_ms;
     float ingest_ms;
@@ -247,14 +249,26 @@ int hsc_register_group(hsc_ctx *ctx, const char *tbname, int idxnum, int keylen)
 int hsc_window_ingest_device(hsc_ctx *ctx, size_t n, int words,
                              const uint32_t *gid, const uint64_t *key_words,
                              const uint64_t *lsn, uint64_t end_lsn);
-/* Window layout.  AUTO: the narrow layout -- 4096-row tiles of 32-bit
- * tile-relative key deltas -- whenever every tile of the sorted window fits
- * it (int64 index keys over a dense or moderate value range), else WIDE (every
- * key as its big-endian words).  WIDE forces the wide layout.  Verdicts are
- * identical; a change applies at the next window build (host-staged windows
- * rebuild; a device-ingested window returns HSC_ESTATE and must be
- * re-ingested). */
-enum { HSC_LAYOUT_AUTO = 0, HSC_LAYOUT_WIDE = 1, HSC_LAYOUT_NARROW = 2 };
+/* Window layout.  AUTO: the narrow layout -- every (group, key) as one
+ * 62-bit code under a 16-ary index, each range answered by one probe kernel
+ * without bucketing -- whenever the whole window fits it (any single int64
+ * index, any single group of keys whose varying bits span < 62 bits), else
+ * WIDE (every key as its big-endian words, ranges bucketed by window tile).
+ * A narrow window answers a sparse batch (< 8 ranges per 2048-row tile) with
+ * one direct probe kernel and a dense one with the tile pipeline over codes.
+ * WIDE forces the wide layout; NARROW_DIRECT / NARROW_TILES keep AUTO's
+ * layout choice but force that probe path (testing).  Verdicts are
+ * identical; a change between WIDE and the others applies at the next window
+ * build (host-staged windows rebuild; a device-ingested window returns
+ * HSC_ESTATE and must be re-ingested).  hsc_window_layout reports WIDE or
+ * NARROW. */
+enum {
+    HSC_LAYOUT_AUTO = 0,
+    HSC_LAYOUT_WIDE = 1,
+    HSC_LAYOUT_NARROW = 2,
+    HSC_LAYOUT_NARROW_DIRECT = 3,
+    HSC_LAYOUT_NARROW_TILES = 4
+};
 int hsc_set_layout(hsc_ctx *ctx, int layout);
 int hsc_window_layout(hsc_ctx *ctx);         /* HSC_LAYOUT_WIDE or _NARROW   */
 int hsc_window_words(hsc_ctx *ctx);          /* key words per key (>= 1)     */

@@ -1,33 +1,33 @@
-"""GPU parity of the two window layouts.
+"""GPU parity of the window layouts and probe paths.
 
-The narrow layout (4096-row tiles of 32-bit tile-relative key deltas,
-comdb2_amd/csrc/hsc_narrow.hip) and the wide layout (every key as its
-big-endian words) must give verdicts bit-identical to the oracle
-(oracle/serial_oracle.c, the bdb_osql_serial_check restatement) and to each
-other.  Every case runs twice on the same context: layout AUTO, then forced
-WIDE."""
+The narrow layout (every key as one 62-bit code under a 16-ary index,
+comdb2_amd/csrc/hsc_narrow.hip) answers a batch either with the direct probe
+kernel or with the tile pipeline over codes; the wide layout keeps every key
+as its big-endian words.  All three must give verdicts bit-identical to the
+oracle (oracle/serial_oracle.c, the bdb_osql_serial_check restatement): every
+case runs three times on the same context."""
 import numpy as np
 import pytest
 
 from comdb2_amd import formats as F
 from comdb2_amd.formats import LogBuilder, Range, ReadSets
-from comdb2_amd.hsc import LAYOUT_AUTO, LAYOUT_NARROW, LAYOUT_WIDE
+from comdb2_amd.hsc import (LAYOUT_AUTO, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT,
+                            LAYOUT_NARROW_TILES, LAYOUT_WIDE)
 from comdb2_amd.workloads import config2, config5
 
 pytestmark = pytest.mark.gpu
 
 
 def both_layouts(v, oracle_mod, log, rs, expect_auto):
+    """Direct probe, tile pipeline over codes (both on the narrow layout when
+    the window fits it) and the wide layout, each against the oracle."""
     want, _, _ = oracle_mod.check(log, rs, nthreads=8)
     got = {}
     try:
-        for layout in (LAYOUT_AUTO, LAYOUT_WIDE):
+        for layout in (LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES, LAYOUT_WIDE):
             v.set_layout(layout)
             v.ingest_log(log)
-            if layout == LAYOUT_AUTO:
-                assert v.layout == expect_auto
-            else:
-                assert v.layout == LAYOUT_WIDE
+            assert v.layout == (LAYOUT_WIDE if layout == LAYOUT_WIDE else expect_auto)
             got[layout] = v.check_readsets(rs)
             np.testing.assert_array_equal(got[layout] != 0, want != 0,
                                           err_msg=f"layout {layout}")
@@ -65,8 +65,7 @@ def keyed_case(seed, n_commits, per_commit, key_fn, range_fn, n_txn, ranges_per_
 @pytest.mark.parametrize("kw,expect", [
     (dict(n_commits=3000, n_txn=800, value_bits=20, width=1 << 10, snap_recent=0.5), LAYOUT_NARROW),
     (dict(n_commits=20000, n_txn=3000, value_bits=36, width=1 << 28, snap_recent=0.05), LAYOUT_NARROW),
-    # 49 tiles over 2^40 values: a tile spans ~2^34 > 2^32 -> wide
-    (dict(n_commits=20000, n_txn=3000, value_bits=40, width=1 << 30, snap_recent=0.05), LAYOUT_WIDE),
+    (dict(n_commits=20000, n_txn=3000, value_bits=40, width=1 << 30, snap_recent=0.05), LAYOUT_NARROW),
     (dict(n_commits=20000, n_txn=3000, value_bits=16, width=1 << 14, snap_recent=0.02), LAYOUT_NARROW),
     (dict(n_commits=5000, n_txn=1000, value_bits=8, width=4, snap_recent=1.0), LAYOUT_NARROW),
 ])
