@@ -87,6 +87,12 @@ struct hsc_ctx {
     DBuf d_nzero, d_ntmax, d_nsp_g, d_nsp_w, d_ngs, d_nscratch;
     DBuf p_code_lo, p_code_hi, p_zero;
     uint32_t probe_ntiles = 0;  // tiles of the view the last probe ran on
+    // narrow tiles: u32 key deltas + commit ranks (dense batches)
+    bool ntiles32 = false;
+    DBuf d_commits, d_cdir, d_tdir, d_key32, d_rank32, d_ctmp[4];
+    Dir16 cdir{}, tdir{};
+    uint32_t ncommit = 0;
+    DBuf w_tcode, w_tcode2, w_trecs;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
     DBuf d_gstart, d_gend, d_tmax, d_table_max, d_group_table, d_count, d_sp_g, d_sp_w;
 
@@ -94,7 +100,6 @@ struct hsc_ctx {
     DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;
     DBuf p_verdict, p_bitmap;
     DBuf w_code, w_hist, w_counts, w_bucket, w_cursor, w_items, w_item_tile, w_item_desc, w_recs;
-    DBuf w_dbg;  // A/B cycle counters
 
     // marshal output
     hsc_marshalled m{};
@@ -208,6 +213,53 @@ static int window_words(hsc_ctx *c)
 
 // Sort + dedupe rows staged in d_gid/d_words/d_lsn (n_in rows, stride cap),
 // then build group spans, tile maxima and table maxima.
+#define HIPCHK_RC(c, call)                  \
+    do {                                    \
+        const int rc_ = (call);             \
+        if (rc_ != HSC_OK) return rc_;      \
+    } while (0)
+
+// The window's distinct commit LSNs, sorted (commit ranks of the narrow
+// tiles), from the staged rows' LSNs before the key sort moves them: a log
+// stream arrives in LSN order (unique = flag + scan + compact); otherwise
+// the LSNs are radix-sorted first.
+static int build_commits(hsc_ctx *c, size_t n_in)
+{
+    hipStream_t s = c->stream;
+    const size_t cap = c->cap;
+    HIPCHK(c, c->d_nzero.ensure(4 * cap));
+    HIPCHK(c, hipMemsetAsync(c->d_nzero.p, 0, 4 * cap, s));
+    HIPCHK(c, c->d_commits.ensure(8 * n_in));
+    uint32_t *flag = c->d_count.as<uint32_t>() + 8;
+    HIPCHK(c, check_sorted_u64(c->d_lsn.as<uint64_t>(), n_in, flag, s));
+    uint32_t unsorted = 0;
+    HIPCHK(c, hipMemcpyAsync(&unsorted, flag, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const uint64_t *src = c->d_lsn.as<uint64_t>();
+    size_t stride = cap;
+    if (unsorted) {
+        for (auto &b : c->d_ctmp) HIPCHK(c, b.ensure(8 * n_in));
+        HIPCHK(c, hipMemcpyAsync(c->d_ctmp[0].p, c->d_lsn.p, 8 * n_in, hipMemcpyDeviceToDevice, s));
+        bool alt = false;
+        HIPCHK(c, radix_sort_rows(1, n_in, c->d_nzero.as<uint32_t>(), c->d_ctmp[0].as<uint64_t>(),
+                                  c->d_ctmp[1].as<uint64_t>(), n_in, c->d_gid2.as<uint32_t>(),
+                                  c->d_ctmp[2].as<uint64_t>(), c->d_ctmp[3].as<uint64_t>(),
+                                  c->d_scratch.p, c->d_scratch.bytes, &alt, nullptr, s));
+        src = (alt ? c->d_ctmp[2] : c->d_ctmp[0]).as<uint64_t>();
+        stride = n_in;
+        HIPCHK(c, hipMemsetAsync(c->d_nzero.p, 0, 4 * cap, s));
+    }
+    HIPCHK(c, dedupe_rows(1, n_in, c->d_nzero.as<uint32_t>(), src, src, stride,
+                          c->d_gid2.as<uint32_t>(), c->d_commits.as<uint64_t>(),
+                          c->d_commits.as<uint64_t>(), n_in, c->d_flags.as<uint32_t>(),
+                          c->d_scratch.p, c->d_scratch.bytes, c->d_count.as<uint32_t>() + 12, s));
+    uint32_t m = 0;
+    HIPCHK(c, hipMemcpyAsync(&m, c->d_count.as<uint32_t>() + 12, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->ncommit = m;
+    return HSC_OK;
+}
+
 static int device_build(hsc_ctx *c, size_t n_in)
 {
     hipStream_t s = c->stream;
@@ -225,6 +277,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, hipEventCreate(&e0));
     HIPCHK(c, hipEventCreate(&e1));
     HIPCHK(c, hipEventRecord(e0, s));
+    if (c->layout != HSC_LAYOUT_WIDE && n_in > 0) HIPCHK_RC(c, build_commits(c, n_in));
     bool in_alt = false;
     uint64_t vary[kMaxWords + 1];
     HIPCHK(c, radix_sort_rows(W, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
@@ -371,6 +424,24 @@ static int device_build(hsc_ctx *c, size_t n_in)
         wn.gend = c->d_ngs.as<uint32_t>() + 1;
         wn.sp_g = c->d_nsp_g.as<uint32_t>();
         wn.sp_w = c->d_nsp_w.as<uint64_t>();
+        // 8-byte tile rows when every 4096-row tile spans < 2^32 codes
+        c->ntiles32 = false;
+        if (wn.log2T == 12 && wn.ntiles <= (uint32_t)kHistCap && c->ncommit > 0) {
+            HIPCHK(c, dir16_build(c->d_commits.as<uint64_t>(), c->ncommit, c->d_cdir, c->cdir,
+                                  narrow_tiles_dir_lds(), s));
+            HIPCHK(c, dir16_build(wn.sp_w, wn.ntiles, c->d_tdir, c->tdir, narrow_tiles_dir_lds(), s));
+            HIPCHK(c, c->d_key32.ensure(4 * (size_t)nv.len[0]));
+            HIPCHK(c, c->d_rank32.ensure(4 * (size_t)nv.len[0]));
+            uint32_t *flag = c->d_count.as<uint32_t>() + 4;
+            HIPCHK(c, narrow_tiles_build(nv.keys, c->d_lsn.as<uint64_t>(), (uint32_t)c->n, nv.len[0],
+                                         c->d_commits.as<uint64_t>(), c->ncommit,
+                                         c->d_key32.as<uint32_t>(), c->d_rank32.as<uint32_t>(),
+                                         flag, s));
+            uint32_t wide32 = 1;
+            HIPCHK(c, hipMemcpyAsync(&wide32, flag, 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            c->ntiles32 = wide32 == 0;
+        }
     }
     HIPCHK(c, hipEventRecord(e1, s));
     HIPCHK(c, hipStreamSynchronize(s));
@@ -769,6 +840,72 @@ static int probe_narrow(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w,
 
 static int probe_tiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w, const ProbeView &p);
 
+// Narrow tiles (dense batch): locate (codes, snapshot ranks, per-chunk tile
+// histograms) -> column scan + plan -> scatter (16-byte records) -> join
+// (8-byte rows) -> pack.
+static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
+                        const ProbeView &p)
+{
+    hipStream_t s = c->stream;
+    c->probe_ntiles = wn.ntiles;
+    const uint32_t nt = std::max<uint32_t>(wn.ntiles, 1);
+    ProbeWork work{};
+    work.lds_mode = 1;
+    const size_t nwork = std::max<size_t>(p.n, p.n_lock);
+    // chunks of narrow_tiles_chunk() probes (at most kMaxChunks: the caller
+    // sends larger batches down the code-tile path)
+    work.chunk = narrow_tiles_chunk();
+    work.G = (uint32_t)std::max<size_t>(1, (nwork + work.chunk - 1) / work.chunk);
+    const size_t n1 = std::max<uint32_t>(p.n, 1);
+    HIPCHK(c, c->w_hist.ensure(4 * (size_t)work.G * nt));
+    HIPCHK(c, c->w_counts.ensure(4 * ((size_t)nt + 1)));
+    HIPCHK(c, c->w_bucket.ensure(4 * ((size_t)nt + 1)));
+    HIPCHK(c, c->w_cursor.ensure(4 * ((size_t)nt + 1)));
+    HIPCHK(c, c->w_items.ensure(4 * ((size_t)nt + 1)));
+    const uint32_t max_items = nt + (uint32_t)((2 * n1 + kJoinChunk - 1) / kJoinChunk);
+    HIPCHK(c, c->w_item_tile.ensure(4 * (size_t)max_items + 16));
+    HIPCHK(c, c->w_item_desc.ensure(16 * (size_t)max_items + 16));
+    HIPCHK(c, c->w_tcode.ensure(16 * n1));
+    HIPCHK(c, c->w_tcode2.ensure(16 * n1));
+    HIPCHK(c, c->w_trecs.ensure(32 * n1));
+    work.hist = c->w_hist.as<uint32_t>();
+    work.counts = c->w_counts.as<uint32_t>();
+    work.bucket_off = c->w_bucket.as<uint32_t>();
+    work.cursor = c->w_cursor.as<uint32_t>();
+    work.item_off = c->w_items.as<uint32_t>();
+    work.item_tile = c->w_item_tile.as<uint32_t>();
+    work.item_desc = c->w_item_desc.as<uint4>();
+    NarrowTiles ntl{};
+    ntl.key32 = c->d_key32.as<uint32_t>();
+    ntl.rank32 = c->d_rank32.as<uint32_t>();
+    ntl.cdir = c->cdir;
+    ntl.tdir = c->tdir;
+    ntl.code = c->w_tcode.as<uint4>();
+    ntl.code2 = c->w_tcode2.as<uint4>();
+    ntl.recs = c->w_trecs.as<uint4>();
+    const bool tm = c->timing;
+    if (tm)
+        for (int i = 0; i < 6; ++i)
+            if (!c->ev[i]) HIPCHK(c, hipEventCreate(&c->ev[i]));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
+    if (b->n_txn) HIPCHK(c, hipMemsetAsync(b->verdict, 0, b->n_txn, s));
+    HIPCHK(c, launch_locate_t(c->nv, wn, p, work, ntl, b->verdict, s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
+    if (p.n && wn.ntiles) {
+        HIPCHK(c, launch_plan(wn, work, s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
+        HIPCHK(c, launch_scatter_t(p, work, ntl, wn.ntiles, s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
+        HIPCHK(c, launch_join_t(work, ntl, wn.n, wn.ntiles, max_items, b->verdict, s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
+    } else if (tm) {
+        for (int i = 2; i <= 4; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
+    }
+    HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
+    return HSC_OK;
+}
+
 static int probe(hsc_ctx *c, const hsc_probe_batch *b)
 {
     if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
@@ -799,6 +936,11 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
     WinView wn = c->wn;
     wn.table_max = w.table_max;
     wn.ntables = w.ntables;
+    // 8-byte tile rows when they fit and the batch fits one column scan
+    const size_t nchunks = (std::max<size_t>(p.n, p.n_lock) + narrow_tiles_chunk() - 1) /
+                           narrow_tiles_chunk();
+    if (c->ntiles32 && c->layout != HSC_LAYOUT_NARROW_CODES && nchunks <= (size_t)kMaxChunks)
+        return probe_ntiles(c, b, wn, p);
     const size_t n = std::max<uint32_t>(p.n, 1);
     HIPCHK(c, c->p_code_lo.ensure(8 * n));
     HIPCHK(c, c->p_code_hi.ensure(8 * n));
@@ -837,11 +979,6 @@ static int probe_tiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w, c
     HIPCHK(c, c->w_item_tile.ensure(4 * (size_t)max_items + 16));
     HIPCHK(c, c->w_item_desc.ensure(16 * (size_t)max_items + 16));
     work.item_desc = c->w_item_desc.as<uint4>();
-    if (getenv("HSC_DBG_CYCLES")) {
-        HIPCHK(c, c->w_dbg.ensure(8 * 4 * 4096));
-        HIPCHK(c, hipMemsetAsync(c->w_dbg.p, 0, 8 * 4 * 4096, s));
-        work.dbg = c->w_dbg.as<uint64_t>();
-    }
     work.code = c->w_code.as<uint64_t>();
     work.hist = c->w_hist.as<uint32_t>();
     work.counts = c->w_counts.as<uint32_t>();
@@ -893,19 +1030,6 @@ static int collect_timing(hsc_ctx *c)
         HIPCHK(c, hipMemcpy(&nrec, c->w_bucket.as<uint32_t>() + c->probe_ntiles, 4,
                             hipMemcpyDeviceToHost));
     c->last.records = nrec;
-    if (getenv("HSC_DBG_CYCLES") && c->w_dbg.p) {
-        std::vector<uint64_t> d(4 * 4096);
-        HIPCHK(c, hipMemcpy(d.data(), c->w_dbg.p, 8 * d.size(), hipMemcpyDeviceToHost));
-        double st = 0, se = 0, it = 0, tot = 0;
-        int nb = 0;
-        for (int b = 0; b < 4096; ++b)
-            if (d[4 * b + 3]) {
-                st += d[4 * b]; se += d[4 * b + 1]; it += d[4 * b + 2]; tot += d[4 * b + 3]; ++nb;
-            }
-        if (nb)
-            fprintf(stderr, "join cycles/WG: stage %.0f search %.0f total %.0f items %.2f (WGs %d)\n",
-                    st / nb, se / nb, tot / nb, it / nb, nb);
-    }
     return HSC_OK;
 }
 
@@ -1015,10 +1139,12 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->w_item_tile, &c->w_hist, &c->p_lo, &c->p_hi,
                     &c->p_gid, &c->p_snap, &c->p_txn, &c->p_lock_table, &c->p_lock_snap,
                     &c->p_lock_txn, &c->p_verdict, &c->p_bitmap, &c->w_code, &c->w_counts,
-                    &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_item_desc, &c->w_recs, &c->w_dbg,
+                    &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_item_desc, &c->w_recs,
                     &c->d_nkeys, &c->d_nmaxs, &c->d_nbase, &c->d_nzero, &c->d_ntmax,
                     &c->d_nsp_g, &c->d_nsp_w, &c->d_ngs, &c->d_nscratch, &c->p_code_lo,
-                    &c->p_code_hi, &c->p_zero};
+                    &c->p_code_hi, &c->p_zero, &c->d_commits, &c->d_cdir, &c->d_tdir, &c->d_key32, &c->d_rank32,
+                    &c->d_ctmp[0], &c->d_ctmp[1], &c->d_ctmp[2], &c->d_ctmp[3], &c->w_tcode,
+                    &c->w_tcode2, &c->w_trecs};
     for (DBuf *b : bufs) b->release();
     c->graph.release_all();
     for (auto &e : c->ev)
@@ -1176,7 +1302,7 @@ int hsc_window_ingest_device(hsc_ctx *c, size_t n, int words, const uint32_t *gi
 
 int hsc_set_layout(hsc_ctx *c, int layout)
 {
-    if (!c || layout < HSC_LAYOUT_AUTO || layout > HSC_LAYOUT_NARROW_TILES ||
+    if (!c || layout < HSC_LAYOUT_AUTO || layout > HSC_LAYOUT_NARROW_CODES ||
         layout == HSC_LAYOUT_NARROW)
         return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);

@@ -140,7 +140,6 @@ struct ProbeWork {
     uint32_t *item_off;    // [ntiles + 1]
     uint32_t *item_tile;   // [max items]
     uint4 *item_desc;      // [max items] {tile, first record, end record, 0}
-    uint64_t *dbg;         // A/B cycle counters (HSC_AB_CYCLES builds), may be null
     uint64_t *recs;        // join records
     uint32_t G, chunk;     // probe chunks (one workgroup each in locate/scatter)
     int lds_mode;          // ntiles <= kHistCap: LDS histograms, no global atomics
@@ -178,6 +177,46 @@ hipError_t launch_probe_narrow(const NarrowView &nv, const ProbeView &p, uint8_t
                                hipStream_t s);
 hipError_t narrow_codes(const NarrowView &nv, const ProbeView &p, uint64_t *lo64, uint64_t *hi64,
                         hipStream_t s);
+// 16-ary directory over a sorted u64 array A (hsc_narrow.hip): level 0 = A
+// padded with ~0 to a multiple of 16, level l+1 [i] = level l [16 i + 15]
+// (the last entry of every 16-entry block), up to one block; levels >=
+// lds_from are staged in LDS by the searching kernel (lds_n entries).
+constexpr int kDirLevels = 12;
+struct Dir16 {
+    const uint64_t *v;          // all levels, level l at v + off[l]
+    uint32_t off[kDirLevels];
+    uint32_t len[kDirLevels];   // entries of level l (multiple of 16)
+    int levels, lds_from;
+    uint32_t lds_n;
+    uint32_t n;                 // entries of A
+};
+// Builds d over src[0 .. n) into buf (resized); at most max_lds entries in LDS.
+hipError_t dir16_build(const uint64_t *src, uint32_t n, struct DBuf &buf, Dir16 &d,
+                       uint32_t max_lds, hipStream_t s);
+
+// Narrow tiles (dense batches): 4096-row tiles of (u32 key delta, u32 commit rank).
+struct NarrowTiles {
+    const uint32_t *key32;     // [len0] key64 - first key64 of the tile
+    const uint32_t *rank32;    // [len0] 1 + index of the row's LSN in commits
+    Dir16 cdir;                // directory of the window's distinct commit LSNs
+    Dir16 tdir;                // directory of the first code of every tile
+    uint4 *code;               // [n] first record {tile << 12 | rank, lo, hi, r(S)}
+    uint4 *code2;              // [n] second record (flag kHasSecond in code.x)
+    uint4 *recs;               // [2n] {lo delta, hi delta, snapshot rank, read set}
+};
+hipError_t check_sorted_u64(const uint64_t *v, size_t n, uint32_t *flag, hipStream_t s);
+hipError_t narrow_tiles_build(const uint64_t *key64, const uint64_t *lsn, uint32_t n, uint32_t len,
+                              const uint64_t *C, uint32_t m, uint32_t *key32, uint32_t *rank32,
+                              uint32_t *flag, hipStream_t s);
+uint32_t narrow_tiles_chunk();
+uint32_t narrow_tiles_dir_lds();
+hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeView &p,
+                           const ProbeWork &work, const NarrowTiles &nt, uint8_t *verdict,
+                           hipStream_t s);
+hipError_t launch_scatter_t(const ProbeView &p, const ProbeWork &work, const NarrowTiles &nt,
+                            uint32_t ntiles, hipStream_t s);
+hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t n,
+                         uint32_t ntiles, uint32_t max_items, uint8_t *verdict, hipStream_t s);
 // Dependency graph + SCC (hsc_graph.hip).
 constexpr uint64_t kDepWW = 1, kDepWR = 2, kDepRW = 4;
 struct GraphInput {              // device pointers

@@ -997,216 +997,18 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, ProbeWork work
     }
 }
 
-// Native 2 x u64 vector (register arrays of it stay in VGPRs; arrays of the
-// HIP ulonglong2 struct were demoted to scratch across the pipelined loop).
-typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-
-// Loads of one join item into registers.  Row pair v of thread t is rows
-// 2 (t + kJoinThreads v) + {0, 1}: every load instruction of a wave reads
-// 1 KiB contiguous, every LDS store writes 1 KiB contiguous (no conflicts).
-// d = the item's {tile, first record, end record}.
-template <int WT, int LOG2T, int RV, int kRec, int RW>
-__device__ __forceinline__ void join_load(const WinView &w, const ProbeWork &work, uint4 d,
-                                          u64x2 (&rk)[WT][RV], u64x2 (&rl)[RV],
-                                          u64x2 (&rec)[kRec][RW / 2])
-{
-    const size_t ts = (size_t)d.x << LOG2T;
-#pragma unroll
-    for (int v = 0; v < RV; ++v) {
-        const size_t row = ts + 2 * (threadIdx.x + kJoinThreads * v);
-#pragma unroll
-        for (int j = 0; j < WT; ++j) rk[j][v] = *(const u64x2 *)(w.words + (size_t)j * w.stride + row);
-        rl[v] = *(const u64x2 *)(w.lsn + row);
-    }
-#pragma unroll
-    for (int k = 0; k < kRec; ++k) {
-        const uint32_t r = min(d.y + k * kJoinThreads + threadIdx.x, max(d.z, 1u) - 1);
-        const u64x2 *src = (const u64x2 *)(work.recs + (size_t)r * RW);
-#pragma unroll
-        for (int h = 0; h < RW / 2; ++h) rec[k][h] = src[h];
-    }
-}
-
-// Any lsn > snap in rows [p, q) (non-empty) of a tile with 16- and 128-row
-// block maxima (NB128 = 128-row blocks per tile).  A snapshot is usually
-// recent, so most blocks hold no later commit: the 16-row blocks at both
-// ends (and for long ranges the 128-row blocks) reject first, and rows are
-// read only for lanes whose end blocks may hold a later commit.
-template <int NB128>
-__device__ __forceinline__ bool lds_any_after_128(const uint64_t *lsn, const uint64_t *b16,
-                                                  const uint64_t *b128, uint32_t p, uint32_t q,
-                                                  uint64_t snap)
-{
-    const uint32_t q1 = q - 1;
-    const bool hot_p = b16[p >> 4] > snap, hot_q = b16[q1 >> 4] > snap;
-    if (!hot_p && !hot_q && (q1 >> 4) <= (p >> 4) + 1) return false;  // <= 2 blocks, both cold
-    if (q - p <= 16) return any_gt<16>(lsn, p, q, snap);
-    // long range: end partial blocks (only if hot), then whole blocks
-    const uint32_t p16 = (p + 15) & ~15u, q16 = q & ~15u;
-    const uint32_t bp = p16 >> 4, bq = q16 >> 4;  // whole 16-blocks [bp, bq)
-    const uint32_t bp8 = min((bp + 7) & ~7u, bq), bq8 = max(bq & ~7u, bp8);
-    bool r = false;
-    if (hot_p) r |= any_gt<15>(lsn, p, p16, snap);
-    if (hot_q) r |= any_gt<15>(lsn, q16, q, snap);
-    r |= any_gt<7>(b16, bp, bp8, snap);
-    r |= any_gt<7>(b16, bq8, bq, snap);
-    if (bp8 < bq8) r |= any_gt<NB128>(b128, bp8 >> 3, bq8 >> 3, snap);
-    return r;
-}
-
-// Persistent join for 1- and 2-word keys: one or two workgroups per CU walk
-// the join items with a stride of the grid.  While the records of item i are
-// searched in LDS, the rows and records of item i + grid are loading into
-// registers and the descriptor of item i + 2 grid is in flight (software
-// pipeline), so a workgroup's staging latency hides behind its previous
-// item's searches.  Block maxima come from lane shuffles (16 rows = 8 lanes,
-// 128 rows = a wave), so one barrier separates staging from searching;
-// searches are branch-free power-of-two steps over the probe's group rows
-// [lb, ub) of the tile.
-template <int WT, int LOG2T>
-__global__ __launch_bounds__(kJoinThreads) void k_join_p(WinView w, ProbeWork work,
-                                                         uint8_t *verdict)
-{
-    constexpr uint32_t T = 1u << LOG2T;
-    constexpr int RV = T / (2 * kJoinThreads);  // row pairs per thread
-    static_assert(RV == 2 || RV == 4, "tile of 2048 or 4096 rows");
-    constexpr int kRec = kJoinChunk / kJoinThreads;
-    constexpr int RW = 2 * WT + 2;              // record words
-    __shared__ __attribute__((aligned(16))) uint64_t kw[WT][T];
-    __shared__ __attribute__((aligned(16))) uint64_t lsn[T];
-    __shared__ uint64_t b16[T / 16];
-    __shared__ uint64_t b128[T / 128];
-
-    const uint32_t nitems = work.item_off[w.ntiles];
-    uint32_t item = blockIdx.x;
-    if (item >= nitems) return;
-    const uint32_t grid = gridDim.x;
-    u64x2 rk[WT][RV], rl[RV];
-    u64x2 rec[kRec][RW / 2];
-    uint4 dcur = work.item_desc[item];
-    uint4 dnext = work.item_desc[min(item + grid, nitems - 1)];
-    join_load<WT, LOG2T, RV, kRec, RW>(w, work, dcur, rk, rl, rec);
-#ifdef HSC_AB_CYCLES
-    uint64_t cy_stage = 0, cy_search = 0, cy_t0 = __builtin_readcyclecounter();
-    const uint64_t cy_start = cy_t0;
-    uint32_t cy_items = 0;
-#endif
-    while (true) {
-        // this item's rows -> LDS, block maxima from registers
-        u64x2 crec[kRec][RW / 2];
-#pragma unroll
-        for (int k = 0; k < kRec; ++k)
-#pragma unroll
-            for (int h = 0; h < RW / 2; ++h) crec[k][h] = rec[k][h];
-#pragma unroll
-        for (int v = 0; v < RV; ++v) {
-            const uint32_t pr = threadIdx.x + kJoinThreads * v;  // row pair
-#pragma unroll
-            for (int j = 0; j < WT; ++j) *(u64x2 *)(&kw[j][2 * pr]) = rk[j][v];
-            *(u64x2 *)(&lsn[2 * pr]) = rl[v];
-            uint64_t m = rl[v].x > rl[v].y ? rl[v].x : rl[v].y;
-#pragma unroll
-            for (int d = 1; d < 8; d <<= 1) {
-                const uint64_t o = __shfl_xor(m, d, 64);
-                m = o > m ? o : m;
-            }
-            if ((threadIdx.x & 7) == 0) b16[pr >> 3] = m;
-#pragma unroll
-            for (int d = 8; d < 64; d <<= 1) {
-                const uint64_t o = __shfl_xor(m, d, 64);
-                m = o > m ? o : m;
-            }
-            if ((threadIdx.x & 63) == 0) b128[pr >> 6] = m;
-        }
-        __syncthreads();
-#ifdef HSC_AB_CYCLES
-        { const uint64_t t = __builtin_readcyclecounter(); cy_stage += t - cy_t0; cy_t0 = t; ++cy_items; }
-#endif
-        // the next item's loads and the descriptor after it go out first
-        const uint32_t next = item + grid;
-        const uint4 d = dcur;
-        dcur = dnext;
-        if (next < nitems) {
-            dnext = work.item_desc[min(next + grid, nitems - 1)];
-            join_load<WT, LOG2T, RV, kRec, RW>(w, work, dcur, rk, rl, rec);
-        }
-        const uint32_t ts = d.x << LOG2T;
-        const uint32_t tn = min(T, w.n - ts);
-#pragma unroll
-        for (int k = 0; k < kRec; ++k) {
-            const uint32_t r = d.y + k * kJoinThreads + threadIdx.x;
-            if (r >= d.z) continue;
-            const u64x2 tailv = crec[k][WT];  // {snap, meta}
-            const uint64_t snap = tailv.x, meta = tailv.y;
-            const uint32_t txn = (uint32_t)meta;
-            const uint32_t lb = (uint32_t)(meta >> 32) & 0x1FFFu;
-            const uint32_t ub = min((uint32_t)(meta >> 45) & 0x1FFFu, tn);
-            if (lb >= ub) continue;
-            // WT 1: {lo, hi}; WT 2: {lo0, lo1}, {hi0, hi1}
-            const uint64_t l0 = crec[k][0].x;
-            const uint64_t h0 = WT == 1 ? crec[k][0].y : crec[k][WT - 1].x;
-            const uint64_t l1 = WT == 2 ? crec[k][0].y : 0;
-            const uint64_t h1 = WT == 2 ? crec[k][WT - 1].y : 0;
-            // pa = first row of [lb, ub) >= lo, pb = first row > hi: both
-            // searches' reads of a step are issued together (selects, no
-            // branches; an index past ub is clamped and its step rejected)
-            uint32_t pa = lb, pb = lb;
-#pragma unroll
-            for (uint32_t step = T; step > 0; step >>= 1) {
-                const bool oka = pa + step <= ub, okb = pb + step <= ub;
-                const uint32_t ia = min(pa + step, ub) - 1, ib = min(pb + step, ub) - 1;
-                const uint64_t ra = kw[0][ia], rb = kw[0][ib];
-                bool lt, le;
-                if (WT == 1) {
-                    lt = ra < l0;
-                    le = rb <= h0;
-                } else {
-                    const uint64_t ra1 = kw[WT - 1][ia], rb1 = kw[WT - 1][ib];
-                    lt = ra < l0 || (ra == l0 && ra1 < l1);
-                    le = rb < h0 || (rb == h0 && rb1 <= h1);
-                }
-                pa += (oka && lt) ? step : 0;
-                pb += (okb && le) ? step : 0;
-            }
-            if (pa < pb && lds_any_after_128<T / 128>(lsn, b16, b128, pa, pb, snap))
-                verdict[txn] = 1;
-        }
-#ifdef HSC_AB_CYCLES
-        __syncthreads();
-        { const uint64_t t = __builtin_readcyclecounter(); cy_search += t - cy_t0; cy_t0 = t; }
-#endif
-        if (next >= nitems) break;
-        item = next;
-        __syncthreads();  // LDS is rewritten with the prefetched rows
-    }
-#ifdef HSC_AB_CYCLES
-    if (threadIdx.x == 0 && work.dbg && blockIdx.x < 4096) {
-        work.dbg[4 * blockIdx.x + 0] = cy_stage;
-        work.dbg[4 * blockIdx.x + 1] = cy_search;
-        work.dbg[4 * blockIdx.x + 2] = cy_items;
-        work.dbg[4 * blockIdx.x + 3] = __builtin_readcyclecounter() - cy_start;
-    }
-#endif
-}
-
 hipError_t launch_join(const WinView &w, const ProbeWork &work, uint32_t max_items,
                        uint8_t *verdict, hipStream_t s)
 {
     if (max_items == 0 || w.n == 0) return hipSuccess;
     const size_t T = (size_t)1 << w.log2T;
     const size_t lds = T * 8 * (size_t)w.W + T * 8 + (T / 16) * 8 + std::max<size_t>(T / 256, 16) * 8;
-    // persistent: as many workgroups as fit the CUs at once (LDS-bound)
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint32_t per_cu = (uint32_t)std::max<size_t>(1, (160 * 1024) / (lds + 1024));
-    const uint32_t grid = std::min<uint32_t>(max_items, per_cu * (uint32_t)ncu);
     if (w.W == 1 && w.log2T == 12)
-        k_join_p<1, 12><<<grid, kJoinThreads, 0, s>>>(w, work, verdict);
+        k_join<1, 12><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
     else if (w.W == 1 && w.log2T == 11)
-        k_join_p<1, 11><<<grid, kJoinThreads, 0, s>>>(w, work, verdict);
+        k_join<1, 11><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
     else if (w.W == 2 && w.log2T == 11)
-        k_join_p<2, 11><<<grid, kJoinThreads, 0, s>>>(w, work, verdict);
+        k_join<2, 11><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
     else
         k_join<0, 0><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
     return hipGetLastError();

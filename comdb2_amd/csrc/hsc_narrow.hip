@@ -33,6 +33,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace hsc {
 
@@ -317,6 +318,523 @@ hipError_t narrow_codes(const NarrowView &nv, const ProbeView &p, uint64_t *lo64
 {
     if (p.n == 0) return hipSuccess;
     k_codes<<<(p.n + 255) / 256, 256, 0, s>>>(nv, p, lo64, hi64);
+    return hipGetLastError();
+}
+
+
+// ============================================================================
+// narrow tiles: 4096-row tiles of (u32 key delta, u32 commit rank)
+// ============================================================================
+//
+// For a dense batch the window is streamed once per batch, tile by tile,
+// and the ranges are bucketed by tile (hist matrix + column scan, the plan
+// of hsc_kernels.hip).  A row of a tile is 8 bytes:
+//
+//   key32[i]  = key64[i] - key64[first row of the tile]  (every tile spans
+//               < 2^32 codes: checked at build, else the narrow window keeps
+//               the code-tile pipeline)
+//   rank32[i] = 1 + the index of the row's commit LSN among the window's
+//               distinct commit LSNs C (sorted); a snapshot S maps to
+//               r(S) = #{c in C : c <= S} and  lsn > S  <=>  rank > r(S).
+//
+// Join records are 16 bytes: {lo delta, hi delta, r(S), read set}.
+namespace {
+constexpr uint32_t kNoTile32 = 0xFFFFFFFFu;
+constexpr int kTLog2 = 12;  // 4096-row tiles (= the code view's tiles)
+}  // namespace
+
+__global__ void k_check_sorted(const uint64_t *v, size_t n, uint32_t *flag)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x + 1;
+    if (i < n && v[i] < v[i - 1]) atomicOr(flag, 1u);
+}
+
+hipError_t check_sorted_u64(const uint64_t *v, size_t n, uint32_t *flag, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(flag, 0, 4, s);
+    if (e != hipSuccess || n < 2) return e;
+    k_check_sorted<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(v, n, flag);
+    return hipGetLastError();
+}
+
+// rank32[i] = 1 + lower_bound(C, lsn[i]) (lsn[i] is in C); pads get 0
+__global__ void k_rank32(const uint64_t *lsn, uint32_t n, uint32_t len, const uint64_t *C,
+                         uint32_t m, uint32_t *rank)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= len) return;
+    if (i >= n) {
+        rank[i] = 0;
+        return;
+    }
+    const uint64_t x = lsn[i];
+    uint32_t lo = 0, hi = m;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (C[mid] < x) lo = mid + 1; else hi = mid;
+    }
+    rank[i] = lo + 1;
+}
+
+// key32 = key64 - first key64 of the tile; flag := 1 if a tile spans >= 2^32
+__global__ void k_key32(const uint64_t *key64, uint32_t n, uint32_t len, uint32_t *key32,
+                        uint32_t *flag)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= len) return;
+    if (i >= n) {
+        key32[i] = 0xFFFFFFFFu;
+        return;
+    }
+    const uint64_t d = key64[i] - key64[(size_t)(i >> kTLog2) << kTLog2];
+    if (d > 0xFFFFFFFFull) atomicOr(flag, 1u);
+    key32[i] = (uint32_t)d;
+}
+
+hipError_t narrow_tiles_build(const uint64_t *key64, const uint64_t *lsn, uint32_t n, uint32_t len,
+                              const uint64_t *C, uint32_t m, uint32_t *key32, uint32_t *rank32,
+                              uint32_t *flag, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(flag, 0, 4, s);
+    if (e != hipSuccess || len == 0) return e;
+    k_key32<<<(len + 255) / 256, 256, 0, s>>>(key64, n, len, key32, flag);
+    k_rank32<<<(len + 255) / 256, 256, 0, s>>>(lsn, n, len, C, m, rank32);
+    return hipGetLastError();
+}
+
+// ---- 16-ary directories over sorted u64 arrays ----
+__global__ void k_dir_level0(const uint64_t *src, uint32_t n, uint32_t len, uint64_t *dst)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < len) dst[i] = i < n ? src[i] : ~0ull;
+}
+
+__global__ void k_dir_up(const uint64_t *src, uint32_t len_src, uint64_t *dst, uint32_t len_dst)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < len_dst) dst[i] = i < len_src / 16 ? src[16 * (size_t)i + 15] : ~0ull;
+}
+
+hipError_t dir16_build(const uint64_t *src, uint32_t n, DBuf &buf, Dir16 &d, uint32_t max_lds,
+                       hipStream_t s)
+{
+    d = Dir16{};
+    d.n = n;
+    uint32_t len = (n + 16) & ~15u;  // at least one pad: every level ends in ~0
+    uint64_t off = 0;
+    int L = 0;
+    for (;;) {
+        if (L == kDirLevels) return hipErrorInvalidValue;
+        d.off[L] = (uint32_t)off;
+        d.len[L] = len;
+        off += len;
+        ++L;
+        if (len <= 16) break;
+        len = ((len / 16) + 15) & ~15u;
+    }
+    d.levels = L;
+    d.lds_from = L - 1;
+    d.lds_n = d.len[L - 1];
+    while (d.lds_from > 0 && d.lds_n + d.len[d.lds_from - 1] <= max_lds) d.lds_n += d.len[--d.lds_from];
+    hipError_t e = buf.ensure(8 * off);
+    if (e != hipSuccess) return e;
+    uint64_t *v = buf.as<uint64_t>();
+    d.v = v;
+    k_dir_level0<<<(d.len[0] + 255) / 256, 256, 0, s>>>(src, n, d.len[0], v);
+    for (int l = 1; l < L; ++l)
+        k_dir_up<<<(d.len[l] + 255) / 256, 256, 0, s>>>(v + d.off[l - 1], d.len[l - 1],
+                                                          v + d.off[l], d.len[l]);
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ void dir16_stage(const Dir16 &d, uint64_t *lds)
+{
+    const uint64_t *src = d.v + d.off[d.lds_from];
+    for (uint32_t i = threadIdx.x; i < d.lds_n; i += blockDim.x) lds[i] = src[i];
+}
+
+// out[k] = #{entries of the directory's array <= x[k]} (le[k]) or < x[k],
+// for K keys in lockstep; act[k] false gives 0.  Per level a branch-free
+// 4-step search inside one 16-entry block (one 128-byte line): a block's
+// last entry is never below a key (every level ends in padding ~0 and a
+// block's last entry bounds the key at the level above).
+template <int K>
+__device__ __forceinline__ void dir16_count(const Dir16 &d, const uint64_t *lds,
+                                            const uint64_t (&x)[K], const bool (&le)[K],
+                                            const bool (&act)[K], uint32_t (&out)[K])
+{
+    uint32_t c[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) c[k] = 0;
+    const uint32_t lds_base = d.off[d.lds_from];
+    for (int l = d.levels - 1; l >= 0; --l) {
+        const uint64_t *lv = l >= d.lds_from ? lds + (d.off[l] - lds_base) : d.v + d.off[l];
+        uint32_t pos[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) pos[k] = 0;
+#pragma unroll
+        for (uint32_t step = 8; step > 0; step >>= 1) {
+            uint64_t v[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) v[k] = lv[16 * c[k] + pos[k] + step - 1];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const bool below = le[k] ? v[k] <= x[k] : v[k] < x[k];
+                pos[k] += below ? step : 0;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < K; ++k) c[k] = 16 * c[k] + pos[k];
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) out[k] = act[k] ? min(c[k], d.n) : 0;
+}
+
+// ---- locate: codes, snapshot ranks, end tiles, per-chunk tile histogram ----
+// One workgroup per chunk of kLocTP * kLocateThreads probes; thread t owns
+// probes c0 + t + kLocateThreads j, j < kLocTP (consecutive lanes =
+// consecutive probes, so a read set's ranges sit in neighbouring lanes).
+// Every probe load is issued up front; the tile and snapshot-rank searches
+// run for all kLocTP probes in lockstep over 16-ary directories whose upper
+// levels are staged in LDS (one 128-byte line per global level).  Output per
+// probe: its first join record {tile << 12 | rank, lo, hi, r(S)} and, for a
+// range that spans two tiles, its second one.
+constexpr int kLocTP = 4;
+constexpr uint32_t kHasSecond = 1u << 31;
+constexpr int kDirLds = 512;  // directory entries staged per directory
+
+__global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinView wt,
+                                                             ProbeView p, ProbeWork work,
+                                                             NarrowTiles nt, uint8_t *verdict)
+{
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds64[];
+    uint64_t *tdir = lds64;                       // [tdir.lds_n]
+    uint64_t *cdir = tdir + nt.tdir.lds_n;        // [cdir.lds_n]
+    uint32_t *hist = (uint32_t *)(cdir + nt.cdir.lds_n);  // [ntiles]
+    const uint32_t ntiles = wt.ntiles;
+    const size_t ks = p.n;
+    const uint32_t c0 = blockIdx.x * work.chunk;
+    const uint32_t c1 = min(p.n, c0 + work.chunk);
+    const int lane = threadIdx.x & 63;
+    // all probe loads first
+    uint32_t qq[kLocTP], gg[kLocTP];
+    bool valid[kLocTP];
+    uint64_t snap[kLocTP], l0[kLocTP], l1[kLocTP], h0[kLocTP], h1[kLocTP];
+#pragma unroll
+    for (int j = 0; j < kLocTP; ++j) {
+        qq[j] = c0 + threadIdx.x + kLocateThreads * j;
+        valid[j] = qq[j] < c1;
+        const uint32_t q = valid[j] ? qq[j] : 0;
+        gg[j] = p.n ? p.gid[q] : 0;
+        snap[j] = p.n ? p.snap[q] : 0;
+        l0[j] = p.n ? p.lo[q] : 0;
+        h0[j] = p.n ? p.hi[q] : 0;
+        l1[j] = p.n && nv.W > 1 ? p.lo[ks + q] : 0;
+        h1[j] = p.n && nv.W > 1 ? p.hi[ks + q] : 0;
+    }
+    dir16_stage(nt.tdir, tdir);
+    dir16_stage(nt.cdir, cdir);
+    for (uint32_t i = threadIdx.x; i < ntiles; i += kLocateThreads) hist[i] = 0;
+    // codes of the bounds (a range below the window is empty)
+    uint64_t lo[kLocTP], hi[kLocTP];
+#pragma unroll
+    for (int j = 0; j < kLocTP; ++j) {
+        const uint32_t q = valid[j] ? qq[j] : 0;
+        uint64_t v;
+        bool rem;
+        uint64_t a = 0;
+        bool live;
+        if (nv.W <= 2) {  // words from registers
+            const uint64_t xl[2] = {l0[j], l1[j]}, xh[2] = {h0[j], h1[j]};
+            a = rel_diff(nv.W, nv.lw, nv.tz, gg[j], xl, 1, nv.base[0], nv.base + 1, 1, kSat, v, rem)
+                    ? (v >= kSat ? kSat : v + (rem ? 1 : 0))
+                    : 0;
+            live = rel_diff(nv.W, nv.lw, nv.tz, gg[j], xh, 1, nv.base[0], nv.base + 1, 1, kSat, v,
+                            rem);
+        } else {
+            a = rel_diff(nv.W, nv.lw, nv.tz, gg[j], p.lo + q, ks, nv.base[0], nv.base + 1, 1, kSat,
+                         v, rem)
+                    ? (v >= kSat ? kSat : v + (rem ? 1 : 0))
+                    : 0;
+            live = rel_diff(nv.W, nv.lw, nv.tz, gg[j], p.hi + q, ks, nv.base[0], nv.base + 1, 1,
+                            kSat, v, rem);
+        }
+        lo[j] = live ? a : kSat;
+        hi[j] = live ? v : 0;
+    }
+    __syncthreads();  // directories staged, histogram zeroed
+    // snapshot ranks r(S) = #commits <= S: searched by the first lane of
+    // every run of equal snapshots in the wave, then broadcast
+    bool head[kLocTP], le_t[kLocTP];
+#pragma unroll
+    for (int j = 0; j < kLocTP; ++j) {
+        const uint64_t prev = __shfl_up(snap[j], 1, 64);
+        head[j] = lane == 0 || prev != snap[j];
+        le_t[j] = true;
+    }
+    uint32_t rs[kLocTP];
+    {
+        uint32_t r[kLocTP];
+        dir16_count<kLocTP>(nt.cdir, cdir, snap, le_t, head, r);
+        const uint64_t lem = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+#pragma unroll
+        for (int j = 0; j < kLocTP; ++j) {
+            const int src = 63 - __clzll(__ballot(head[j]) & lem);
+            rs[j] = __shfl(r[j], src, 64);
+        }
+    }
+    // end tiles: a = #first < lo - 1 (the tile holding the first row >= lo),
+    // bt = #first <= hi - 1 (the tile holding the last row <= hi)
+    uint64_t keys[2 * kLocTP];
+    bool act[2 * kLocTP], le[2 * kLocTP];
+#pragma unroll
+    for (int j = 0; j < kLocTP; ++j) {
+        keys[2 * j] = lo[j];
+        keys[2 * j + 1] = hi[j];
+        le[2 * j] = false;
+        le[2 * j + 1] = true;
+        act[2 * j] = act[2 * j + 1] = valid[j] && lo[j] <= hi[j];
+    }
+    uint32_t cnt[2 * kLocTP];
+    dir16_count<2 * kLocTP>(nt.tdir, tdir, keys, le, act, cnt);
+#pragma unroll
+    for (int j = 0; j < kLocTP; ++j) {
+        if (!valid[j]) continue;
+        const uint32_t q = qq[j];
+        const uint32_t ca = cnt[2 * j], cb = cnt[2 * j + 1];
+        uint4 rec[2];
+        int nrec = 0;
+        const uint32_t a = ca ? ca - 1 : 0;
+        const uint32_t bt = cb ? cb - 1 : 0;
+        if (cb > 0 && a <= bt && lo[j] <= hi[j]) {
+            const bool mid = bt > a + 1 && tiles_max(wt, a + 1, bt - 1) > snap[j];
+            if (mid) {
+                verdict[p.txn[q]] = 1;
+            } else {
+                // tile-relative bounds
+                const uint64_t fa = wt.sp_w[a], fb = wt.sp_w[bt];
+                const uint64_t lo_a = lo[j] <= fa ? 0 : lo[j] - fa;  // > 2^32-1: none
+                const uint64_t hi_a = a == bt ? (hi[j] < fa ? ~0ull : hi[j] - fa) : 0xFFFFFFFFull;
+                const uint64_t hi_b = hi[j] < fb ? ~0ull : hi[j] - fb;
+                const bool full_a = lo_a == 0 && (a < bt || hi_a >= 0xFFFFFFFFull);
+                if (lo_a <= 0xFFFFFFFFull && hi_a != ~0ull && lo_a <= hi_a) {
+                    if (full_a) {
+                        if (tiles_max(wt, a, a) > snap[j]) verdict[p.txn[q]] = 1;
+                    } else {
+                        rec[nrec++] = make_uint4(a << 12 | atomicAdd(&hist[a], 1u), (uint32_t)lo_a,
+                                                 (uint32_t)min(hi_a, 0xFFFFFFFFull), rs[j]);
+                    }
+                }
+                if (a < bt && hi_b != ~0ull) {
+                    if (hi_b >= 0xFFFFFFFFull) {
+                        if (tiles_max(wt, bt, bt) > snap[j]) verdict[p.txn[q]] = 1;
+                    } else {
+                        rec[nrec++] = make_uint4(bt << 12 | atomicAdd(&hist[bt], 1u), 0,
+                                                 (uint32_t)hi_b, rs[j]);
+                    }
+                }
+            }
+        }
+        if (nrec == 0) rec[0] = make_uint4(kNoTile32, 0, 0, 0);
+        if (nrec == 2) {
+            rec[0].x |= kHasSecond;
+            nt.code2[q] = rec[1];
+        }
+        nt.code[q] = rec[0];
+    }
+    // table locks: any write to a locked table after the snapshot
+    for (uint32_t q = blockIdx.x * kLocateThreads + threadIdx.x; q < p.n_lock;
+         q += gridDim.x * kLocateThreads) {
+        const uint32_t t = p.lock_table[q];
+        if (t < wt.ntables && wt.table_max[t] > p.lock_snap[q]) verdict[p.lock_txn[q]] = 1;
+    }
+    __syncthreads();
+    uint32_t *row = work.hist + (size_t)blockIdx.x * ntiles;
+    for (uint32_t i = threadIdx.x; i < ntiles; i += kLocateThreads) row[i] = hist[i];
+}
+
+hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeView &p,
+                           const ProbeWork &work, const NarrowTiles &nt, uint8_t *verdict,
+                           hipStream_t s)
+{
+    if (p.n == 0 && p.n_lock == 0) return hipSuccess;
+    const size_t lds = 8 * ((size_t)nt.tdir.lds_n + nt.cdir.lds_n) + 4 * (size_t)wt.ntiles + 16;
+    k_locate_t<<<work.G, kLocateThreads, lds, s>>>(nv, wt, p, work, nt, verdict);
+    return hipGetLastError();
+}
+
+// probes per locate workgroup, directory entries staged in LDS
+uint32_t narrow_tiles_chunk() { return kLocTP * kLocateThreads; }
+uint32_t narrow_tiles_dir_lds() { return kDirLds; }
+
+// ---- scatter: 16-byte records into tile buckets ----
+__global__ __launch_bounds__(256) void k_scatter_t(ProbeView p, ProbeWork work, NarrowTiles nt,
+                                                   uint32_t ntiles)
+{
+    const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+    if (q >= p.n) return;
+    const uint4 a = nt.code[q];
+    if (a.x == kNoTile32) return;
+    const uint32_t txn = p.txn[q];
+    const uint32_t *row = work.hist + (size_t)(q / work.chunk) * ntiles;
+    const uint32_t ta = (a.x & ~kHasSecond) >> 12;
+    nt.recs[work.bucket_off[ta] + row[ta] + (a.x & 0xFFFu)] = make_uint4(a.y, a.z, a.w, txn);
+    if (a.x & kHasSecond) {
+        const uint4 b = nt.code2[q];
+        const uint32_t tb = b.x >> 12;
+        nt.recs[work.bucket_off[tb] + row[tb] + (b.x & 0xFFFu)] = make_uint4(b.y, b.z, b.w, txn);
+    }
+}
+
+hipError_t launch_scatter_t(const ProbeView &p, const ProbeWork &work, const NarrowTiles &nt,
+                            uint32_t ntiles, hipStream_t s)
+{
+    if (p.n == 0) return hipSuccess;
+    k_scatter_t<<<(p.n + 255) / 256, 256, 0, s>>>(p, work, nt, ntiles);
+    return hipGetLastError();
+}
+
+// Native 4 x u32 vector: register arrays of it stay in VGPRs (arrays of the
+// HIP uint4 struct are demoted to scratch across the pipelined loop).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// ---- join: 8-byte rows ----
+// Row quad v of thread t = rows 4 (t + kJoinThreads v) .. + 3: one 16-byte
+// load of keys and one of ranks per quad; 16-row maxima over 4 lanes,
+// 128-row maxima over 32 lanes.
+template <int RQ, int kRec>
+__device__ __forceinline__ void tjoin_load(const NarrowTiles &nt, uint4 d, u32x4 (&rk)[RQ],
+                                           u32x4 (&rr)[RQ], u32x4 (&rec)[kRec])
+{
+    const size_t ts = (size_t)d.x << kTLog2;
+#pragma unroll
+    for (int v = 0; v < RQ; ++v) {
+        const size_t row = ts + 4 * (threadIdx.x + kJoinThreads * v);
+        rk[v] = *(const u32x4 *)(nt.key32 + row);
+        rr[v] = *(const u32x4 *)(nt.rank32 + row);
+    }
+#pragma unroll
+    for (int k = 0; k < kRec; ++k) {
+        const uint32_t r = min(d.y + k * kJoinThreads + threadIdx.x, max(d.z, 1u) - 1);
+        rec[k] = *(const u32x4 *)(nt.recs + r);
+    }
+}
+
+template <int N>
+__device__ __forceinline__ bool any_gt32(const uint32_t *a, uint32_t from, uint32_t to, uint32_t s)
+{
+    bool r = false;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const uint32_t i = from + k;
+        const uint32_t v = a[i < to ? i : from];
+        r |= (i < to) & (v > s);
+    }
+    return r;
+}
+
+__device__ __forceinline__ bool any_after32(const uint32_t *rank, const uint32_t *b16,
+                                            const uint32_t *b128, uint32_t p, uint32_t q,
+                                            uint32_t s)
+{
+    const uint32_t q1 = q - 1;
+    const bool hot_p = b16[p >> 4] > s, hot_q = b16[q1 >> 4] > s;
+    if (!hot_p && !hot_q && (q1 >> 4) <= (p >> 4) + 1) return false;
+    if (q - p <= 16) return any_gt32<16>(rank, p, q, s);
+    const uint32_t p16 = (p + 15) & ~15u, q16 = q & ~15u;
+    const uint32_t bp = p16 >> 4, bq = q16 >> 4;
+    const uint32_t bp8 = min((bp + 7) & ~7u, bq), bq8 = max(bq & ~7u, bp8);
+    bool r = false;
+    if (hot_p) r |= any_gt32<15>(rank, p, p16, s);
+    if (hot_q) r |= any_gt32<15>(rank, q16, q, s);
+    r |= any_gt32<7>(b16, bp, bp8, s);
+    r |= any_gt32<7>(b16, bq8, bq, s);
+    if (bp8 < bq8) r |= any_gt32<32>(b128, bp8 >> 3, bq8 >> 3, s);
+    return r;
+}
+
+__global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowTiles nt,
+                                                         uint32_t n, uint32_t ntiles,
+                                                         uint8_t *verdict)
+{
+    constexpr uint32_t T = 1u << kTLog2;
+    constexpr int RQ = T / (4 * kJoinThreads);  // row quads per thread (2)
+    constexpr int kRec = kJoinChunk / kJoinThreads;
+    __shared__ __attribute__((aligned(16))) uint32_t keys[T];
+    __shared__ __attribute__((aligned(16))) uint32_t rank[T];
+    __shared__ uint32_t b16[T / 16];
+    __shared__ uint32_t b128[T / 128];
+
+    const uint32_t nitems = work.item_off[ntiles];
+    uint32_t item = blockIdx.x;
+    if (item >= nitems) return;
+    const uint32_t grid = gridDim.x;
+    u32x4 rk[RQ], rr[RQ], rec[kRec];
+    uint4 dcur = work.item_desc[item];
+    uint4 dnext = work.item_desc[min(item + grid, nitems - 1)];
+    tjoin_load<RQ, kRec>(nt, dcur, rk, rr, rec);
+    while (true) {
+        u32x4 crec[kRec];
+#pragma unroll
+        for (int k = 0; k < kRec; ++k) crec[k] = rec[k];
+#pragma unroll
+        for (int v = 0; v < RQ; ++v) {
+            const uint32_t quad = threadIdx.x + kJoinThreads * v;
+            ((u32x4 *)keys)[quad] = rk[v];
+            ((u32x4 *)rank)[quad] = rr[v];
+            uint32_t m = max(max(rr[v].x, rr[v].y), max(rr[v].z, rr[v].w));
+            m = max(m, (uint32_t)__shfl_xor((int)m, 1, 64));
+            m = max(m, (uint32_t)__shfl_xor((int)m, 2, 64));
+            if ((threadIdx.x & 3) == 0) b16[quad >> 2] = m;
+#pragma unroll
+            for (int d = 4; d < 32; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+            if ((threadIdx.x & 31) == 0) b128[quad >> 5] = m;
+        }
+        __syncthreads();
+        const uint32_t next = item + grid;
+        const uint4 d = dcur;
+        dcur = dnext;
+        if (next < nitems) {
+            dnext = work.item_desc[min(next + grid, nitems - 1)];
+            tjoin_load<RQ, kRec>(nt, dcur, rk, rr, rec);
+        }
+        const uint32_t tn = min(T, n - (d.x << kTLog2));
+#pragma unroll
+        for (int k = 0; k < kRec; ++k) {
+            const uint32_t r = d.y + k * kJoinThreads + threadIdx.x;
+            if (r >= d.z) continue;
+            const uint32_t lo = crec[k].x, hi = crec[k].y, rs = crec[k].z;
+            // pa = #keys < lo, pb = #keys <= hi over rows [0, tn): both reads
+            // of a step in flight together
+            uint32_t pa = 0, pb = 0;
+#pragma unroll
+            for (uint32_t step = T; step > 0; step >>= 1) {
+                const bool oka = pa + step <= tn, okb = pb + step <= tn;
+                const uint32_t ka = keys[min(pa + step, tn) - 1], kb = keys[min(pb + step, tn) - 1];
+                pa += (oka && ka < lo) ? step : 0;
+                pb += (okb && kb <= hi) ? step : 0;
+            }
+            if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) verdict[crec[k].w] = 1;
+        }
+        if (next >= nitems) break;
+        item = next;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t n,
+                         uint32_t ntiles, uint32_t max_items, uint8_t *verdict, hipStream_t s)
+{
+    if (max_items == 0 || n == 0) return hipSuccess;
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    // one workgroup per item (measured faster than a persistent grid of 2-8
+    // workgroups per CU); HSC_JOIN_WG_PER_CU = k runs k per CU persistently
+    uint32_t per_cu = 0;
+    if (const char *e = getenv("HSC_JOIN_WG_PER_CU")) per_cu = (uint32_t)atoi(e);
+    const uint32_t grid = per_cu ? std::min<uint32_t>(max_items, per_cu * (uint32_t)ncu) : max_items;
+    k_join_t<<<grid, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
     return hipGetLastError();
 }
 

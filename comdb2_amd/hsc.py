@@ -125,7 +125,8 @@ EXPORTS = [
     "hsc_set_layout", "hsc_window_layout",
 ]
 
-LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES = 0, 1, 2, 3, 4
+(LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES,
+ LAYOUT_NARROW_CODES) = 0, 1, 2, 3, 4, 5
 
 _lib: Optional[C.CDLL] = None
 

@@ -256,8 +256,11 @@ int hsc_window_ingest_device(hsc_ctx *ctx, size_t n, int words,
  * WIDE (every key as its big-endian words, ranges bucketed by window tile).
  * A narrow window answers a sparse batch (< 8 ranges per 2048-row tile) with
  * one direct probe kernel and a dense one with the tile pipeline over codes.
- * WIDE forces the wide layout; NARROW_DIRECT / NARROW_TILES keep AUTO's
- * layout choice but force that probe path (testing).  Verdicts are
+ * A dense batch runs on 8-byte tile rows (u32 key delta, u32 commit rank)
+ * when every 4096-row tile spans < 2^32 codes, else on the codes as 16-byte
+ * rows.  WIDE forces the wide layout; NARROW_DIRECT / NARROW_TILES /
+ * NARROW_CODES keep AUTO's layout choice but force that probe path (tiles:
+ * 8-byte rows where they fit; codes: always 16-byte code rows) -- testing.  Verdicts are
  * identical; a change between WIDE and the others applies at the next window
  * build (host-staged windows rebuild; a device-ingested window returns
  * HSC_ESTATE and must be re-ingested).  hsc_window_layout reports WIDE or
@@ -267,7 +270,8 @@ enum {
     HSC_LAYOUT_WIDE = 1,
     HSC_LAYOUT_NARROW = 2,
     HSC_LAYOUT_NARROW_DIRECT = 3,
-    HSC_LAYOUT_NARROW_TILES = 4
+    HSC_LAYOUT_NARROW_TILES = 4,
+    HSC_LAYOUT_NARROW_CODES = 5
 };
 int hsc_set_layout(hsc_ctx *ctx, int layout);
 int hsc_window_layout(hsc_ctx *ctx);         /* HSC_LAYOUT_WIDE or _NARROW   */

@@ -1,18 +1,20 @@
 """GPU parity of the window layouts and probe paths.
 
 The narrow layout (every key as one 62-bit code under a 16-ary index,
-comdb2_amd/csrc/hsc_narrow.hip) answers a batch either with the direct probe
-kernel or with the tile pipeline over codes; the wide layout keeps every key
-as its big-endian words.  All three must give verdicts bit-identical to the
-oracle (oracle/serial_oracle.c, the bdb_osql_serial_check restatement): every
-case runs three times on the same context."""
+comdb2_amd/csrc/hsc_narrow.hip) answers a batch with the direct probe
+kernel, with the tile pipeline on 8-byte rows (u32 key delta + commit rank,
+where every tile fits) or with the tile pipeline over 16-byte code rows; the
+wide layout keeps every key as its big-endian words.  All four must give
+verdicts bit-identical to the oracle (oracle/serial_oracle.c, the
+bdb_osql_serial_check restatement): every case runs four times on the same
+context."""
 import numpy as np
 import pytest
 
 from comdb2_amd import formats as F
 from comdb2_amd.formats import LogBuilder, Range, ReadSets
-from comdb2_amd.hsc import (LAYOUT_AUTO, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT,
-                            LAYOUT_NARROW_TILES, LAYOUT_WIDE)
+from comdb2_amd.hsc import (LAYOUT_AUTO, LAYOUT_NARROW, LAYOUT_NARROW_CODES,
+                            LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES, LAYOUT_WIDE)
 from comdb2_amd.workloads import config2, config5
 
 pytestmark = pytest.mark.gpu
@@ -24,7 +26,7 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
     want, _, _ = oracle_mod.check(log, rs, nthreads=8)
     got = {}
     try:
-        for layout in (LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES, LAYOUT_WIDE):
+        for layout in (LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES, LAYOUT_NARROW_CODES, LAYOUT_WIDE):
             v.set_layout(layout)
             v.ingest_log(log)
             assert v.layout == (LAYOUT_WIDE if layout == LAYOUT_WIDE else expect_auto)
