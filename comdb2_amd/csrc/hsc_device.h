@@ -7,6 +7,11 @@
 
 namespace hsc {
 
+// Native vectors: register arrays of these stay in VGPRs (arrays of the HIP
+// uint4 / ulonglong2 structs can be demoted to scratch).
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)

@@ -447,45 +447,56 @@ hipError_t dir16_build(const uint64_t *src, uint32_t n, DBuf &buf, Dir16 &d, uin
     return hipGetLastError();
 }
 
+// Upper levels [lds_from, levels) of a directory into LDS (16-byte copies:
+// every level is a whole number of 128-byte blocks).
 __device__ __forceinline__ void dir16_stage(const Dir16 &d, uint64_t *lds)
 {
-    const uint64_t *src = d.v + d.off[d.lds_from];
-    for (uint32_t i = threadIdx.x; i < d.lds_n; i += blockDim.x) lds[i] = src[i];
+    const u64x2 *src = (const u64x2 *)(d.v + d.off[d.lds_from]);
+    u64x2 *dst = (u64x2 *)lds;
+    for (uint32_t i = threadIdx.x; i < d.lds_n / 2; i += blockDim.x) dst[i] = src[i];
 }
 
-// out[k] = #{entries of the directory's array <= x[k]} (le[k]) or < x[k],
-// for K keys in lockstep; act[k] false gives 0.  Per level a branch-free
-// 4-step search inside one 16-entry block (one 128-byte line): a block's
-// last entry is never below a key (every level ends in padding ~0 and a
-// block's last entry bounds the key at the level above).
+// One level of a 16-ary directory for K keys in lockstep: c[k] (block index
+// at this level) becomes 16 c[k] + #{entries of the block below xx[k]}.  Two
+// rounds of three independent reads (entries 3, 7, 11 pick the quarter, then
+// its first three entries) instead of a 4-step dependent chain.  A block's
+// last entry is never below a key (levels end in ~0 padding and a block's last
+// entry bounds the key one level up), so the count fits 0..15.
+template <int K>
+__device__ __forceinline__ void dir16_level(const uint64_t *lv, const uint64_t (&xx)[K],
+                                            uint32_t (&c)[K])
+{
+    uint32_t qd[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t *b = lv + 16 * c[k];
+        qd[k] = (uint32_t)(b[3] < xx[k]) + (uint32_t)(b[7] < xx[k]) + (uint32_t)(b[11] < xx[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t *b = lv + 16 * c[k] + 4 * qd[k];
+        c[k] = 16 * c[k] + 4 * qd[k] + (uint32_t)(b[0] < xx[k]) + (uint32_t)(b[1] < xx[k]) +
+               (uint32_t)(b[2] < xx[k]);
+    }
+}
+
+// Strict bound for "entries <= x" (entries are < ~0: ~0 is padding).
+__device__ __forceinline__ uint64_t dir_le(uint64_t x) { return x >= ~0ull - 1 ? ~0ull : x + 1; }
+
+// out[k] = #{entries < xx[k]} (0 where act[k] is false).  Levels held in LDS
+// and levels in global memory run as separate loops so that every read has
+// a known address space (no flat loads).
 template <int K>
 __device__ __forceinline__ void dir16_count(const Dir16 &d, const uint64_t *lds,
-                                            const uint64_t (&x)[K], const bool (&le)[K],
-                                            const bool (&act)[K], uint32_t (&out)[K])
+                                            const uint64_t (&xx)[K], const bool (&act)[K],
+                                            uint32_t (&out)[K])
 {
     uint32_t c[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) c[k] = 0;
     const uint32_t lds_base = d.off[d.lds_from];
-    for (int l = d.levels - 1; l >= 0; --l) {
-        const uint64_t *lv = l >= d.lds_from ? lds + (d.off[l] - lds_base) : d.v + d.off[l];
-        uint32_t pos[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) pos[k] = 0;
-#pragma unroll
-        for (uint32_t step = 8; step > 0; step >>= 1) {
-            uint64_t v[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) v[k] = lv[16 * c[k] + pos[k] + step - 1];
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const bool below = le[k] ? v[k] <= x[k] : v[k] < x[k];
-                pos[k] += below ? step : 0;
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < K; ++k) c[k] = 16 * c[k] + pos[k];
-    }
+    for (int l = d.levels - 1; l >= d.lds_from; --l) dir16_level<K>(lds + (d.off[l] - lds_base), xx, c);
+    for (int l = d.lds_from - 1; l >= 0; --l) dir16_level<K>(d.v + d.off[l], xx, c);
 #pragma unroll
     for (int k = 0; k < K; ++k) out[k] = act[k] ? min(c[k], d.n) : 0;
 }
@@ -496,30 +507,60 @@ __device__ __forceinline__ void dir16_count(const Dir16 &d, const uint64_t *lds,
 // consecutive probes, so a read set's ranges sit in neighbouring lanes).
 // Every probe load is issued up front; the tile and snapshot-rank searches
 // run for all kLocTP probes in lockstep over 16-ary directories whose upper
-// levels are staged in LDS (one 128-byte line per global level).  Output per
-// probe: its first join record {tile << 12 | rank, lo, hi, r(S)} and, for a
-// range that spans two tiles, its second one.
+// levels are staged in LDS (kTileLds: the whole tile directory, so the tile
+// search and the tiles' first codes never leave LDS).  Output per probe: its
+// first join record {tile << 12 | rank, lo, hi, r(S)} and, for a range that
+// spans two tiles, its second one.
 constexpr int kLocTP = 4;
 constexpr uint32_t kHasSecond = 1u << 31;
-constexpr int kDirLds = 512;  // directory entries staged per directory
+constexpr int kDirLds = 4400;  // directory entries staged in LDS per directory
 
+template <int W>
+__device__ __forceinline__ void locate_codes(const NarrowView &nv, const ProbeView &p, uint32_t q,
+                                             uint64_t g, const uint64_t (&xl)[2 > W ? 2 : W],
+                                             const uint64_t (&xh)[2 > W ? 2 : W], uint64_t &lo,
+                                             uint64_t &hi)
+{
+    uint64_t v;
+    bool rem;
+    uint64_t a;
+    bool live;
+    if constexpr (W > 0) {
+        a = rel_diff(W, nv.lw, nv.tz, g, xl, 1, nv.base[0], nv.base + 1, 1, kSat, v, rem)
+                ? (v >= kSat ? kSat : v + (rem ? 1 : 0))
+                : 0;
+        live = rel_diff(W, nv.lw, nv.tz, g, xh, 1, nv.base[0], nv.base + 1, 1, kSat, v, rem);
+    } else {
+        a = rel_diff(nv.W, nv.lw, nv.tz, g, p.lo + q, p.n, nv.base[0], nv.base + 1, 1, kSat, v,
+                     rem)
+                ? (v >= kSat ? kSat : v + (rem ? 1 : 0))
+                : 0;
+        live = rel_diff(nv.W, nv.lw, nv.tz, g, p.hi + q, p.n, nv.base[0], nv.base + 1, 1, kSat, v,
+                        rem);
+    }
+    lo = live ? a : kSat;  // a range below the window is empty
+    hi = live ? v : 0;
+}
+
+// W = key words held in registers (1 or 2), 0 = read from memory (any W)
+template <int W, bool kTileLds>
 __global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinView wt,
                                                              ProbeView p, ProbeWork work,
                                                              NarrowTiles nt, uint8_t *verdict)
 {
+    constexpr int WR = 2 > W ? 2 : W;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds64[];
-    uint64_t *tdir = lds64;                       // [tdir.lds_n]
-    uint64_t *cdir = tdir + nt.tdir.lds_n;        // [cdir.lds_n]
+    uint64_t *tdir = lds64;                               // [tdir.lds_n]
+    uint64_t *cdir = tdir + nt.tdir.lds_n;                // [cdir.lds_n]
     uint32_t *hist = (uint32_t *)(cdir + nt.cdir.lds_n);  // [ntiles]
     const uint32_t ntiles = wt.ntiles;
-    const size_t ks = p.n;
     const uint32_t c0 = blockIdx.x * work.chunk;
     const uint32_t c1 = min(p.n, c0 + work.chunk);
     const int lane = threadIdx.x & 63;
     // all probe loads first
     uint32_t qq[kLocTP], gg[kLocTP];
     bool valid[kLocTP];
-    uint64_t snap[kLocTP], l0[kLocTP], l1[kLocTP], h0[kLocTP], h1[kLocTP];
+    uint64_t snap[kLocTP], xl[kLocTP][WR], xh[kLocTP][WR];
 #pragma unroll
     for (int j = 0; j < kLocTP; ++j) {
         qq[j] = c0 + threadIdx.x + kLocateThreads * j;
@@ -527,55 +568,34 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinV
         const uint32_t q = valid[j] ? qq[j] : 0;
         gg[j] = p.n ? p.gid[q] : 0;
         snap[j] = p.n ? p.snap[q] : 0;
-        l0[j] = p.n ? p.lo[q] : 0;
-        h0[j] = p.n ? p.hi[q] : 0;
-        l1[j] = p.n && nv.W > 1 ? p.lo[ks + q] : 0;
-        h1[j] = p.n && nv.W > 1 ? p.hi[ks + q] : 0;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            xl[j][w] = p.n ? p.lo[(size_t)w * p.n + q] : 0;
+            xh[j][w] = p.n ? p.hi[(size_t)w * p.n + q] : 0;
+        }
     }
     dir16_stage(nt.tdir, tdir);
     dir16_stage(nt.cdir, cdir);
     for (uint32_t i = threadIdx.x; i < ntiles; i += kLocateThreads) hist[i] = 0;
-    // codes of the bounds (a range below the window is empty)
     uint64_t lo[kLocTP], hi[kLocTP];
 #pragma unroll
-    for (int j = 0; j < kLocTP; ++j) {
-        const uint32_t q = valid[j] ? qq[j] : 0;
-        uint64_t v;
-        bool rem;
-        uint64_t a = 0;
-        bool live;
-        if (nv.W <= 2) {  // words from registers
-            const uint64_t xl[2] = {l0[j], l1[j]}, xh[2] = {h0[j], h1[j]};
-            a = rel_diff(nv.W, nv.lw, nv.tz, gg[j], xl, 1, nv.base[0], nv.base + 1, 1, kSat, v, rem)
-                    ? (v >= kSat ? kSat : v + (rem ? 1 : 0))
-                    : 0;
-            live = rel_diff(nv.W, nv.lw, nv.tz, gg[j], xh, 1, nv.base[0], nv.base + 1, 1, kSat, v,
-                            rem);
-        } else {
-            a = rel_diff(nv.W, nv.lw, nv.tz, gg[j], p.lo + q, ks, nv.base[0], nv.base + 1, 1, kSat,
-                         v, rem)
-                    ? (v >= kSat ? kSat : v + (rem ? 1 : 0))
-                    : 0;
-            live = rel_diff(nv.W, nv.lw, nv.tz, gg[j], p.hi + q, ks, nv.base[0], nv.base + 1, 1,
-                            kSat, v, rem);
-        }
-        lo[j] = live ? a : kSat;
-        hi[j] = live ? v : 0;
-    }
+    for (int j = 0; j < kLocTP; ++j)
+        locate_codes<W>(nv, p, valid[j] ? qq[j] : 0, gg[j], xl[j], xh[j], lo[j], hi[j]);
     __syncthreads();  // directories staged, histogram zeroed
     // snapshot ranks r(S) = #commits <= S: searched by the first lane of
     // every run of equal snapshots in the wave, then broadcast
-    bool head[kLocTP], le_t[kLocTP];
-#pragma unroll
-    for (int j = 0; j < kLocTP; ++j) {
-        const uint64_t prev = __shfl_up(snap[j], 1, 64);
-        head[j] = lane == 0 || prev != snap[j];
-        le_t[j] = true;
-    }
     uint32_t rs[kLocTP];
     {
+        bool head[kLocTP];
+        uint64_t xs[kLocTP];
+#pragma unroll
+        for (int j = 0; j < kLocTP; ++j) {
+            const uint64_t prev = __shfl_up(snap[j], 1, 64);
+            head[j] = lane == 0 || prev != snap[j];
+            xs[j] = dir_le(snap[j]);
+        }
         uint32_t r[kLocTP];
-        dir16_count<kLocTP>(nt.cdir, cdir, snap, le_t, head, r);
+        dir16_count<kLocTP>(nt.cdir, cdir, xs, head, r);
         const uint64_t lem = lane == 63 ? ~0ull : ((2ull << lane) - 1);
 #pragma unroll
         for (int j = 0; j < kLocTP; ++j) {
@@ -585,62 +605,61 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinV
     }
     // end tiles: a = #first < lo - 1 (the tile holding the first row >= lo),
     // bt = #first <= hi - 1 (the tile holding the last row <= hi)
-    uint64_t keys[2 * kLocTP];
-    bool act[2 * kLocTP], le[2 * kLocTP];
-#pragma unroll
-    for (int j = 0; j < kLocTP; ++j) {
-        keys[2 * j] = lo[j];
-        keys[2 * j + 1] = hi[j];
-        le[2 * j] = false;
-        le[2 * j + 1] = true;
-        act[2 * j] = act[2 * j + 1] = valid[j] && lo[j] <= hi[j];
-    }
     uint32_t cnt[2 * kLocTP];
-    dir16_count<2 * kLocTP>(nt.tdir, tdir, keys, le, act, cnt);
+    {
+        uint64_t keys[2 * kLocTP];
+        bool act[2 * kLocTP];
+#pragma unroll
+        for (int j = 0; j < kLocTP; ++j) {
+            keys[2 * j] = lo[j];
+            keys[2 * j + 1] = dir_le(hi[j]);
+            act[2 * j] = act[2 * j + 1] = valid[j] && lo[j] <= hi[j];
+        }
+        dir16_count<2 * kLocTP>(nt.tdir, tdir, keys, act, cnt);
+    }
+    const uint64_t *first = kTileLds ? tdir : nt.tdir.v;  // level 0 = first code of every tile
 #pragma unroll
     for (int j = 0; j < kLocTP; ++j) {
         if (!valid[j]) continue;
         const uint32_t q = qq[j];
         const uint32_t ca = cnt[2 * j], cb = cnt[2 * j + 1];
-        uint4 rec[2];
-        int nrec = 0;
         const uint32_t a = ca ? ca - 1 : 0;
         const uint32_t bt = cb ? cb - 1 : 0;
+        uint4 r0 = make_uint4(kNoTile32, 0, 0, 0), r1 = r0;
+        bool hit = false;
         if (cb > 0 && a <= bt && lo[j] <= hi[j]) {
-            const bool mid = bt > a + 1 && tiles_max(wt, a + 1, bt - 1) > snap[j];
-            if (mid) {
-                verdict[p.txn[q]] = 1;
+            if (bt > a + 1 && tiles_max(wt, a + 1, bt - 1) > snap[j]) {
+                hit = true;
             } else {
                 // tile-relative bounds
-                const uint64_t fa = wt.sp_w[a], fb = wt.sp_w[bt];
+                const uint64_t fa = first[a], fb = first[bt];
                 const uint64_t lo_a = lo[j] <= fa ? 0 : lo[j] - fa;  // > 2^32-1: none
                 const uint64_t hi_a = a == bt ? (hi[j] < fa ? ~0ull : hi[j] - fa) : 0xFFFFFFFFull;
                 const uint64_t hi_b = hi[j] < fb ? ~0ull : hi[j] - fb;
                 const bool full_a = lo_a == 0 && (a < bt || hi_a >= 0xFFFFFFFFull);
-                if (lo_a <= 0xFFFFFFFFull && hi_a != ~0ull && lo_a <= hi_a) {
-                    if (full_a) {
-                        if (tiles_max(wt, a, a) > snap[j]) verdict[p.txn[q]] = 1;
+                const bool use_a = lo_a <= 0xFFFFFFFFull && hi_a != ~0ull && lo_a <= hi_a;
+                const bool use_b = a < bt && hi_b != ~0ull;
+                const bool full_b = hi_b >= 0xFFFFFFFFull;
+                if (use_a && full_a) hit |= tiles_max(wt, a, a) > snap[j];
+                if (use_b && full_b) hit |= tiles_max(wt, bt, bt) > snap[j];
+                if (use_a && !full_a)
+                    r0 = make_uint4(a << 12 | atomicAdd(&hist[a], 1u), (uint32_t)lo_a,
+                                    (uint32_t)min(hi_a, 0xFFFFFFFFull), rs[j]);
+                if (use_b && !full_b) {
+                    const uint4 rb = make_uint4(bt << 12 | atomicAdd(&hist[bt], 1u), 0,
+                                                (uint32_t)hi_b, rs[j]);
+                    if (r0.x == kNoTile32) {
+                        r0 = rb;
                     } else {
-                        rec[nrec++] = make_uint4(a << 12 | atomicAdd(&hist[a], 1u), (uint32_t)lo_a,
-                                                 (uint32_t)min(hi_a, 0xFFFFFFFFull), rs[j]);
-                    }
-                }
-                if (a < bt && hi_b != ~0ull) {
-                    if (hi_b >= 0xFFFFFFFFull) {
-                        if (tiles_max(wt, bt, bt) > snap[j]) verdict[p.txn[q]] = 1;
-                    } else {
-                        rec[nrec++] = make_uint4(bt << 12 | atomicAdd(&hist[bt], 1u), 0,
-                                                 (uint32_t)hi_b, rs[j]);
+                        r0.x |= kHasSecond;
+                        r1 = rb;
                     }
                 }
             }
         }
-        if (nrec == 0) rec[0] = make_uint4(kNoTile32, 0, 0, 0);
-        if (nrec == 2) {
-            rec[0].x |= kHasSecond;
-            nt.code2[q] = rec[1];
-        }
-        nt.code[q] = rec[0];
+        if (hit) verdict[p.txn[q]] = 1;
+        if (r0.x & kHasSecond) nt.code2[q] = r1;
+        nt.code[q] = r0;
     }
     // table locks: any write to a locked table after the snapshot
     for (uint32_t q = blockIdx.x * kLocateThreads + threadIdx.x; q < p.n_lock;
@@ -659,7 +678,23 @@ hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeV
 {
     if (p.n == 0 && p.n_lock == 0) return hipSuccess;
     const size_t lds = 8 * ((size_t)nt.tdir.lds_n + nt.cdir.lds_n) + 4 * (size_t)wt.ntiles + 16;
-    k_locate_t<<<work.G, kLocateThreads, lds, s>>>(nv, wt, p, work, nt, verdict);
+    const bool tl = nt.tdir.lds_from == 0;
+    const int w = nv.W == 1 || nv.W == 2 ? nv.W : 0;
+#define HSC_LOCATE(W_, TL_)                                                                        \
+    k_locate_t<W_, TL_><<<work.G, kLocateThreads, lds, s>>>(nv, wt, p, work, nt, verdict)
+    if (w == 1 && tl)
+        HSC_LOCATE(1, true);
+    else if (w == 1)
+        HSC_LOCATE(1, false);
+    else if (w == 2 && tl)
+        HSC_LOCATE(2, true);
+    else if (w == 2)
+        HSC_LOCATE(2, false);
+    else if (tl)
+        HSC_LOCATE(0, true);
+    else
+        HSC_LOCATE(0, false);
+#undef HSC_LOCATE
     return hipGetLastError();
 }
 
@@ -694,9 +729,6 @@ hipError_t launch_scatter_t(const ProbeView &p, const ProbeWork &work, const Nar
     return hipGetLastError();
 }
 
-// Native 4 x u32 vector: register arrays of it stay in VGPRs (arrays of the
-// HIP uint4 struct are demoted to scratch across the pipelined loop).
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // ---- join: 8-byte rows ----
 // Row quad v of thread t = rows 4 (t + kJoinThreads v) .. + 3: one 16-byte
