@@ -89,8 +89,9 @@ struct hsc_ctx {
     uint32_t probe_ntiles = 0;  // tiles of the view the last probe ran on
     // narrow tiles: u32 key deltas + commit ranks (dense batches)
     bool ntiles32 = false;
-    DBuf d_commits, d_cdir, d_tdir, d_key32, d_rank32, d_ctmp[4];
+    DBuf d_commits, d_cdir, d_tdir, d_trad, d_key32, d_rank32, d_ctmp[4];
     Dir16 cdir{}, tdir{};
+    uint32_t trad_m = 0;       // tile bucket table size (0: none)
     uint32_t ncommit = 0;
     DBuf w_tcode, w_tcode2, w_trecs;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
@@ -426,10 +427,16 @@ static int device_build(hsc_ctx *c, size_t n_in)
         wn.sp_w = c->d_nsp_w.as<uint64_t>();
         // 8-byte tile rows when every 4096-row tile spans < 2^32 codes
         c->ntiles32 = false;
+        c->trad_m = 0;
         if (wn.log2T == 12 && wn.ntiles <= (uint32_t)kHistCap && c->ncommit > 0) {
             HIPCHK(c, dir16_build(c->d_commits.as<uint64_t>(), c->ncommit, c->d_cdir, c->cdir,
                                   narrow_tiles_dir_lds(), s));
             HIPCHK(c, dir16_build(wn.sp_w, wn.ntiles, c->d_tdir, c->tdir, narrow_tiles_dir_lds(), s));
+            c->trad_m = narrow_trad_buckets(wn.ntiles);
+            if (c->trad_m) {
+                HIPCHK(c, c->d_trad.ensure(4 * ((size_t)c->trad_m + 2)));
+                HIPCHK(c, narrow_trad_build(wn.sp_w, wn.ntiles, c->trad_m, c->d_trad.as<uint32_t>(), s));
+            }
             HIPCHK(c, c->d_key32.ensure(4 * (size_t)nv.len[0]));
             HIPCHK(c, c->d_rank32.ensure(4 * (size_t)nv.len[0]));
             uint32_t *flag = c->d_count.as<uint32_t>() + 4;
@@ -880,6 +887,8 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     ntl.rank32 = c->d_rank32.as<uint32_t>();
     ntl.cdir = c->cdir;
     ntl.tdir = c->tdir;
+    ntl.trad = c->trad_m ? c->d_trad.as<uint32_t>() : nullptr;
+    ntl.trad_m = c->trad_m;
     ntl.code = c->w_tcode.as<uint4>();
     ntl.code2 = c->w_tcode2.as<uint4>();
     ntl.recs = c->w_trecs.as<uint4>();
@@ -1142,7 +1151,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_item_desc, &c->w_recs,
                     &c->d_nkeys, &c->d_nmaxs, &c->d_nbase, &c->d_nzero, &c->d_ntmax,
                     &c->d_nsp_g, &c->d_nsp_w, &c->d_ngs, &c->d_nscratch, &c->p_code_lo,
-                    &c->p_code_hi, &c->p_zero, &c->d_commits, &c->d_cdir, &c->d_tdir, &c->d_key32, &c->d_rank32,
+                    &c->p_code_hi, &c->p_zero, &c->d_commits, &c->d_cdir, &c->d_tdir, &c->d_trad, &c->d_key32, &c->d_rank32,
                     &c->d_ctmp[0], &c->d_ctmp[1], &c->d_ctmp[2], &c->d_ctmp[3], &c->w_tcode,
                     &c->w_tcode2, &c->w_trecs};
     for (DBuf *b : bufs) b->release();

@@ -200,6 +200,10 @@ struct NarrowTiles {
     const uint32_t *rank32;    // [len0] 1 + index of the row's LSN in commits
     Dir16 cdir;                // directory of the window's distinct commit LSNs
     Dir16 tdir;                // directory of the first code of every tile
+    const uint32_t *trad;      // [trad_m + 2] bucket table over tile first codes
+                               // (trad[k] = #first < k << shift; trad[m + 1] = shift),
+                               // nullptr: search tdir instead
+    uint32_t trad_m;           // buckets (power of two)
     uint4 *code;               // [n] first record {tile << 12 | rank, lo, hi, r(S)}
     uint4 *code2;              // [n] second record (flag kHasSecond in code.x)
     uint4 *recs;               // [2n] {lo delta, hi delta, snapshot rank, read set}
@@ -209,6 +213,11 @@ hipError_t narrow_tiles_build(const uint64_t *key64, const uint64_t *lsn, uint32
                               const uint64_t *C, uint32_t m, uint32_t *key32, uint32_t *rank32,
                               uint32_t *flag, hipStream_t s);
 uint32_t narrow_tiles_chunk();
+// Bucket table of the tiles' first codes (locate's tile search from LDS);
+// returns the bucket count m (0: too many tiles, use the directory).
+uint32_t narrow_trad_buckets(uint32_t ntiles);
+hipError_t narrow_trad_build(const uint64_t *first, uint32_t ntiles, uint32_t m, uint32_t *trad,
+                             hipStream_t s);
 uint32_t narrow_tiles_dir_lds();
 hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeView &p,
                            const ProbeWork &work, const NarrowTiles &nt, uint8_t *verdict,

@@ -542,21 +542,135 @@ __device__ __forceinline__ void locate_codes(const NarrowView &nv, const ProbeVi
     hi = live ? v : 0;
 }
 
+// ---- bucket table over the tiles' first codes ----
+// first[0] = 0 (codes are relative to the window's first row), so bucket k
+// covers codes [k << shift, (k + 1) << shift) with shift the least that puts
+// the last tile's first code below m << shift.  trad[k] = #first < k << shift
+// for k <= m; trad[m + 1] = shift.
+constexpr uint32_t kTradMaxTiles = 4096;   // first codes staged in LDS (32 KiB)
+constexpr uint32_t kTradMax = 4096;        // buckets (u16 in LDS: 8 KiB)
+
+uint32_t narrow_trad_buckets(uint32_t ntiles)
+{
+    const bool off = getenv("HSC_TILE_DIR") != nullptr;  // tests: force the directory
+    if (off || ntiles == 0 || ntiles > kTradMaxTiles) return 0;
+    uint32_t m = 16;
+    while (m < 2 * ntiles && m < kTradMax) m *= 2;
+    return m;
+}
+
+__global__ void k_trad(const uint64_t *first, uint32_t ntiles, uint32_t m, uint32_t *trad)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > m + 1) return;
+    const uint64_t span = first[ntiles - 1];
+    const int bits = span ? 64 - __clzll(span) : 0;
+    const int lg = 31 - __clz(m);
+    const int shift = bits > lg ? bits - lg : 0;
+    if (k == m + 1) {
+        trad[k] = (uint32_t)shift;
+        return;
+    }
+    const uint64_t x = (uint64_t)k << shift;
+    uint32_t lo = 0, hi = ntiles;  // #first < x
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (first[mid] < x)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    trad[k] = lo;
+}
+
+hipError_t narrow_trad_build(const uint64_t *first, uint32_t ntiles, uint32_t m, uint32_t *trad,
+                             hipStream_t s)
+{
+    k_trad<<<(m + 2 + 255) / 256, 256, 0, s>>>(first, ntiles, m, trad);
+    return hipGetLastError();
+}
+
+// LDS carve of k_locate_t (same on host and device).  Tile bucket mode:
+// first codes [ntiles] + cdir levels + histogram [ntiles] + bucket table u16
+// [m + 1] + per-wave snapshot lists; directory mode: tdir levels instead of
+// the first codes and no bucket table.
+struct LocLds {
+    uint32_t first, cdir, hist, trad, sbuf, rbuf, bytes;
+};
+__host__ __device__ inline LocLds loc_lds(const NarrowTiles &nt, uint32_t ntiles)
+{
+    LocLds L{};
+    uint32_t o = 0;
+    L.first = o;
+    o += 8 * (nt.trad ? ((ntiles + 1) & ~1u) : nt.tdir.lds_n);
+    L.cdir = o;
+    o += 8 * nt.cdir.lds_n;
+    L.hist = o;
+    o += 4 * ((ntiles + 3) & ~3u);
+    L.trad = o;
+    o += nt.trad ? 2 * ((nt.trad_m + 1 + 7) & ~7u) : 0;
+    L.sbuf = o;
+    o += 8 * kLocateThreads;
+    L.rbuf = o;
+    o += 4 * kLocateThreads;
+    L.bytes = o;
+    return L;
+}
+
+// #first < x[k] over the LDS bucket table: bucket, then a binary search
+// inside it (typically 0-1 steps; a crowded bucket costs log2 of its size).
+template <int K>
+__device__ __forceinline__ void trad_count(const uint64_t *first, const uint16_t *T, uint32_t m,
+                                           int shift, uint32_t ntiles, const uint64_t (&x)[K],
+                                           const bool (&act)[K], uint32_t (&out)[K])
+{
+    uint32_t l[K], h[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const uint64_t b = x[k] >> shift;
+        const bool in = b < m;
+        const uint32_t bi = in ? (uint32_t)b : 0;
+        l[k] = in ? T[bi] : ntiles;
+        h[k] = in ? T[bi + 1] : ntiles;
+    }
+    for (;;) {
+        bool more = false;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (l[k] < h[k]) {
+                const uint32_t mid = (l[k] + h[k]) >> 1;
+                const bool below = first[mid] < x[k];
+                l[k] = below ? mid + 1 : l[k];
+                h[k] = below ? h[k] : mid;
+                more = true;
+            }
+        }
+        if (!more) break;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) out[k] = act[k] ? l[k] : 0;
+}
+
 // W = key words held in registers (1 or 2), 0 = read from memory (any W)
-template <int W, bool kTileLds>
+template <int W, bool kTrad>
 __global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinView wt,
                                                              ProbeView p, ProbeWork work,
                                                              NarrowTiles nt, uint8_t *verdict)
 {
     constexpr int WR = 2 > W ? 2 : W;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds64[];
-    uint64_t *tdir = lds64;                               // [tdir.lds_n]
-    uint64_t *cdir = tdir + nt.tdir.lds_n;                // [cdir.lds_n]
-    uint32_t *hist = (uint32_t *)(cdir + nt.cdir.lds_n);  // [ntiles]
     const uint32_t ntiles = wt.ntiles;
+    const LocLds L = loc_lds(nt, ntiles);
+    char *lb = (char *)lds64;
+    uint64_t *tfirst = (uint64_t *)(lb + L.first);  // first codes (kTrad) / tdir levels
+    uint64_t *cdir = (uint64_t *)(lb + L.cdir);
+    uint32_t *hist = (uint32_t *)(lb + L.hist);
+    uint16_t *T = (uint16_t *)(lb + L.trad);
+    const int lane = threadIdx.x & 63;
+    uint64_t *sb = (uint64_t *)(lb + L.sbuf) + (threadIdx.x & ~63u);
+    uint32_t *rb = (uint32_t *)(lb + L.rbuf) + (threadIdx.x & ~63u);
     const uint32_t c0 = blockIdx.x * work.chunk;
     const uint32_t c1 = min(p.n, c0 + work.chunk);
-    const int lane = threadIdx.x & 63;
     // all probe loads first
     uint32_t qq[kLocTP], gg[kLocTP];
     bool valid[kLocTP];
@@ -574,7 +688,17 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinV
             xh[j][w] = p.n ? p.hi[(size_t)w * p.n + q] : 0;
         }
     }
-    dir16_stage(nt.tdir, tdir);
+    int tshift = 0;
+    if constexpr (kTrad) {
+        const u64x2 *src = (const u64x2 *)wt.sp_w;
+        for (uint32_t i = threadIdx.x; i < ntiles / 2; i += kLocateThreads)
+            ((u64x2 *)tfirst)[i] = src[i];
+        if ((ntiles & 1) && threadIdx.x == 0) tfirst[ntiles - 1] = wt.sp_w[ntiles - 1];
+        for (uint32_t i = threadIdx.x; i <= nt.trad_m; i += kLocateThreads) T[i] = (uint16_t)nt.trad[i];
+        tshift = (int)nt.trad[nt.trad_m + 1];
+    } else {
+        dir16_stage(nt.tdir, tfirst);
+    }
     dir16_stage(nt.cdir, cdir);
     for (uint32_t i = threadIdx.x; i < ntiles; i += kLocateThreads) hist[i] = 0;
     uint64_t lo[kLocTP], hi[kLocTP];
@@ -582,25 +706,44 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinV
     for (int j = 0; j < kLocTP; ++j)
         locate_codes<W>(nv, p, valid[j] ? qq[j] : 0, gg[j], xl[j], xh[j], lo[j], hi[j]);
     __syncthreads();  // directories staged, histogram zeroed
-    // snapshot ranks r(S) = #commits <= S: searched by the first lane of
-    // every run of equal snapshots in the wave, then broadcast
+    // Snapshot ranks r(S) = #commits <= S.  A run of equal snapshots in
+    // neighbouring lanes (a read set's ranges) has one head; the wave packs
+    // its heads into a list and searches each once, 64 per round.
     uint32_t rs[kLocTP];
     {
+        const uint64_t le_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
         bool head[kLocTP];
-        uint64_t xs[kLocTP];
+        uint32_t slot[kLocTP];
+        uint32_t H = 0;
 #pragma unroll
         for (int j = 0; j < kLocTP; ++j) {
             const uint64_t prev = __shfl_up(snap[j], 1, 64);
             head[j] = lane == 0 || prev != snap[j];
-            xs[j] = dir_le(snap[j]);
+            const uint64_t m = __ballot(head[j]);
+            slot[j] = H + __popcll(m & le_mask) - 1;  // this lane's head
+            H += __popcll(m);
         }
-        uint32_t r[kLocTP];
-        dir16_count<kLocTP>(nt.cdir, cdir, xs, head, r);
-        const uint64_t lem = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+        for (uint32_t b0 = 0; b0 < H; b0 += 64) {
 #pragma unroll
-        for (int j = 0; j < kLocTP; ++j) {
-            const int src = 63 - __clzll(__ballot(head[j]) & lem);
-            rs[j] = __shfl(r[j], src, 64);
+            for (int j = 0; j < kLocTP; ++j)
+                if (head[j] && slot[j] - b0 < 64) sb[slot[j] - b0] = snap[j];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const bool act[1] = {lane < H - b0};
+            const uint64_t xs[1] = {act[0] ? dir_le(sb[lane]) : 0};
+            uint32_t r[1];
+            dir16_count<1>(nt.cdir, cdir, xs, act, r);
+            rb[lane] = r[0];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int j = 0; j < kLocTP; ++j)
+                if (slot[j] - b0 < 64) rs[j] = rb[slot[j] - b0];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     }
     // end tiles: a = #first < lo - 1 (the tile holding the first row >= lo),
@@ -615,9 +758,12 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinV
             keys[2 * j + 1] = dir_le(hi[j]);
             act[2 * j] = act[2 * j + 1] = valid[j] && lo[j] <= hi[j];
         }
-        dir16_count<2 * kLocTP>(nt.tdir, tdir, keys, act, cnt);
+        if constexpr (kTrad)
+            trad_count<2 * kLocTP>(tfirst, T, nt.trad_m, tshift, ntiles, keys, act, cnt);
+        else
+            dir16_count<2 * kLocTP>(nt.tdir, tfirst, keys, act, cnt);
     }
-    const uint64_t *first = kTileLds ? tdir : nt.tdir.v;  // level 0 = first code of every tile
+    const uint64_t *first = kTrad ? tfirst : wt.sp_w;  // first code of every tile
 #pragma unroll
     for (int j = 0; j < kLocTP; ++j) {
         if (!valid[j]) continue;
@@ -646,13 +792,13 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinV
                     r0 = make_uint4(a << 12 | atomicAdd(&hist[a], 1u), (uint32_t)lo_a,
                                     (uint32_t)min(hi_a, 0xFFFFFFFFull), rs[j]);
                 if (use_b && !full_b) {
-                    const uint4 rb = make_uint4(bt << 12 | atomicAdd(&hist[bt], 1u), 0,
-                                                (uint32_t)hi_b, rs[j]);
+                    const uint4 rb2 = make_uint4(bt << 12 | atomicAdd(&hist[bt], 1u), 0,
+                                                 (uint32_t)hi_b, rs[j]);
                     if (r0.x == kNoTile32) {
-                        r0 = rb;
+                        r0 = rb2;
                     } else {
                         r0.x |= kHasSecond;
-                        r1 = rb;
+                        r1 = rb2;
                     }
                 }
             }
@@ -677,20 +823,20 @@ hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeV
                            hipStream_t s)
 {
     if (p.n == 0 && p.n_lock == 0) return hipSuccess;
-    const size_t lds = 8 * ((size_t)nt.tdir.lds_n + nt.cdir.lds_n) + 4 * (size_t)wt.ntiles + 16;
-    const bool tl = nt.tdir.lds_from == 0;
+    const size_t lds = loc_lds(nt, wt.ntiles).bytes;
+    const bool tr = nt.trad != nullptr;
     const int w = nv.W == 1 || nv.W == 2 ? nv.W : 0;
-#define HSC_LOCATE(W_, TL_)                                                                        \
-    k_locate_t<W_, TL_><<<work.G, kLocateThreads, lds, s>>>(nv, wt, p, work, nt, verdict)
-    if (w == 1 && tl)
+#define HSC_LOCATE(W_, TR_)                                                                        \
+    k_locate_t<W_, TR_><<<work.G, kLocateThreads, lds, s>>>(nv, wt, p, work, nt, verdict)
+    if (w == 1 && tr)
         HSC_LOCATE(1, true);
     else if (w == 1)
         HSC_LOCATE(1, false);
-    else if (w == 2 && tl)
+    else if (w == 2 && tr)
         HSC_LOCATE(2, true);
     else if (w == 2)
         HSC_LOCATE(2, false);
-    else if (tl)
+    else if (tr)
         HSC_LOCATE(0, true);
     else
         HSC_LOCATE(0, false);

@@ -8,6 +8,8 @@ wide layout keeps every key as its big-endian words.  All four must give
 verdicts bit-identical to the oracle (oracle/serial_oracle.c, the
 bdb_osql_serial_check restatement): every case runs four times on the same
 context."""
+import os
+
 import numpy as np
 import pytest
 
@@ -25,15 +27,23 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
     the window fits it) and the wide layout, each against the oracle."""
     want, _, _ = oracle_mod.check(log, rs, nthreads=8)
     got = {}
+    # (layout, tile search): locate finds tiles through the LDS bucket table
+    # by default and through the 16-ary directory with HSC_TILE_DIR set
+    runs = [(LAYOUT_NARROW_DIRECT, 0), (LAYOUT_NARROW_TILES, 0), (LAYOUT_NARROW_TILES, 1),
+            (LAYOUT_NARROW_CODES, 0), (LAYOUT_WIDE, 0)]
     try:
-        for layout in (LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES, LAYOUT_NARROW_CODES, LAYOUT_WIDE):
+        for layout, tile_dir in runs:
+            if tile_dir:
+                os.environ["HSC_TILE_DIR"] = "1"
             v.set_layout(layout)
             v.ingest_log(log)
+            os.environ.pop("HSC_TILE_DIR", None)
             assert v.layout == (LAYOUT_WIDE if layout == LAYOUT_WIDE else expect_auto)
             got[layout] = v.check_readsets(rs)
             np.testing.assert_array_equal(got[layout] != 0, want != 0,
-                                          err_msg=f"layout {layout}")
+                                          err_msg=f"layout {layout} tile_dir {tile_dir}")
     finally:
+        os.environ.pop("HSC_TILE_DIR", None)
         v.set_layout(LAYOUT_AUTO)
     return want
 
