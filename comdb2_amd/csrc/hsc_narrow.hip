@@ -447,13 +447,20 @@ hipError_t dir16_build(const uint64_t *src, uint32_t n, DBuf &buf, Dir16 &d, uin
     return hipGetLastError();
 }
 
-// Upper levels [lds_from, levels) of a directory into LDS (16-byte copies:
-// every level is a whole number of 128-byte blocks).
+// Upper levels [lds_from, levels) of a directory into LDS, every 16-entry
+// block at a 17-entry stride: entry e of block c sits at 17 c + e, so the
+// same entry of different blocks falls in different banks (at a 16-entry
+// stride entries 3 / 7 / 11 of every block share two of the 64 banks).
+constexpr uint32_t kDirLdsStride = 17;
+__host__ __device__ inline uint32_t dir16_lds_entries(const Dir16 &d)
+{
+    return d.lds_n / 16 * kDirLdsStride;
+}
 __device__ __forceinline__ void dir16_stage(const Dir16 &d, uint64_t *lds)
 {
-    const u64x2 *src = (const u64x2 *)(d.v + d.off[d.lds_from]);
-    u64x2 *dst = (u64x2 *)lds;
-    for (uint32_t i = threadIdx.x; i < d.lds_n / 2; i += blockDim.x) dst[i] = src[i];
+    const uint64_t *src = d.v + d.off[d.lds_from];
+    for (uint32_t i = threadIdx.x; i < d.lds_n; i += blockDim.x)
+        lds[(i >> 4) * kDirLdsStride + (i & 15)] = src[i];
 }
 
 // One level of a 16-ary directory for K keys in lockstep: c[k] (block index
@@ -462,19 +469,19 @@ __device__ __forceinline__ void dir16_stage(const Dir16 &d, uint64_t *lds)
 // its first three entries) instead of a 4-step dependent chain.  A block's
 // last entry is never below a key (levels end in ~0 padding and a block's last
 // entry bounds the key one level up), so the count fits 0..15.
-template <int K>
+template <int K, uint32_t STRIDE = 16>
 __device__ __forceinline__ void dir16_level(const uint64_t *lv, const uint64_t (&xx)[K],
                                             uint32_t (&c)[K])
 {
     uint32_t qd[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const uint64_t *b = lv + 16 * c[k];
+        const uint64_t *b = lv + STRIDE * c[k];
         qd[k] = (uint32_t)(b[3] < xx[k]) + (uint32_t)(b[7] < xx[k]) + (uint32_t)(b[11] < xx[k]);
     }
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const uint64_t *b = lv + 16 * c[k] + 4 * qd[k];
+        const uint64_t *b = lv + STRIDE * c[k] + 4 * qd[k];
         c[k] = 16 * c[k] + 4 * qd[k] + (uint32_t)(b[0] < xx[k]) + (uint32_t)(b[1] < xx[k]) +
                (uint32_t)(b[2] < xx[k]);
     }
@@ -495,7 +502,8 @@ __device__ __forceinline__ void dir16_count(const Dir16 &d, const uint64_t *lds,
 #pragma unroll
     for (int k = 0; k < K; ++k) c[k] = 0;
     const uint32_t lds_base = d.off[d.lds_from];
-    for (int l = d.levels - 1; l >= d.lds_from; --l) dir16_level<K>(lds + (d.off[l] - lds_base), xx, c);
+    for (int l = d.levels - 1; l >= d.lds_from; --l)
+        dir16_level<K, kDirLdsStride>(lds + (d.off[l] - lds_base) / 16 * kDirLdsStride, xx, c);
     for (int l = d.lds_from - 1; l >= 0; --l) dir16_level<K>(d.v + d.off[l], xx, c);
 #pragma unroll
     for (int k = 0; k < K; ++k) out[k] = act[k] ? min(c[k], d.n) : 0;
@@ -602,9 +610,9 @@ __host__ __device__ inline LocLds loc_lds(const NarrowTiles &nt, uint32_t ntiles
     LocLds L{};
     uint32_t o = 0;
     L.first = o;
-    o += 8 * (nt.trad ? ((ntiles + 1) & ~1u) : nt.tdir.lds_n);
+    o += 8 * (nt.trad ? ((ntiles + 1) & ~1u) : dir16_lds_entries(nt.tdir));
     L.cdir = o;
-    o += 8 * nt.cdir.lds_n;
+    o += 8 * dir16_lds_entries(nt.cdir);
     L.hist = o;
     o += 4 * ((ntiles + 3) & ~3u);
     L.trad = o;
@@ -849,10 +857,15 @@ uint32_t narrow_tiles_chunk() { return kLocTP * kLocateThreads; }
 uint32_t narrow_tiles_dir_lds() { return kDirLds; }
 
 // ---- scatter: 16-byte records into tile buckets ----
+// Block b runs on XCD b % 8 (round-robin dispatch); blocks are renumbered so
+// that every XCD takes a contiguous run of chunks.  A bucket holds its records
+// in chunk order, so the neighbouring records of a bucket come from one XCD
+// and their partial-line writes merge in that XCD's L2.
 __global__ __launch_bounds__(256) void k_scatter_t(ProbeView p, ProbeWork work, NarrowTiles nt,
-                                                   uint32_t ntiles)
+                                                   uint32_t ntiles, uint32_t per_xcd)
 {
-    const uint32_t q = blockIdx.x * 256 + threadIdx.x;
+    const uint32_t b = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
+    const uint32_t q = b * 256 + threadIdx.x;
     if (q >= p.n) return;
     const uint4 a = nt.code[q];
     if (a.x == kNoTile32) return;
@@ -861,9 +874,9 @@ __global__ __launch_bounds__(256) void k_scatter_t(ProbeView p, ProbeWork work, 
     const uint32_t ta = (a.x & ~kHasSecond) >> 12;
     nt.recs[work.bucket_off[ta] + row[ta] + (a.x & 0xFFFu)] = make_uint4(a.y, a.z, a.w, txn);
     if (a.x & kHasSecond) {
-        const uint4 b = nt.code2[q];
-        const uint32_t tb = b.x >> 12;
-        nt.recs[work.bucket_off[tb] + row[tb] + (b.x & 0xFFFu)] = make_uint4(b.y, b.z, b.w, txn);
+        const uint4 c = nt.code2[q];
+        const uint32_t tb = c.x >> 12;
+        nt.recs[work.bucket_off[tb] + row[tb] + (c.x & 0xFFFu)] = make_uint4(c.y, c.z, c.w, txn);
     }
 }
 
@@ -871,7 +884,8 @@ hipError_t launch_scatter_t(const ProbeView &p, const ProbeWork &work, const Nar
                             uint32_t ntiles, hipStream_t s)
 {
     if (p.n == 0) return hipSuccess;
-    k_scatter_t<<<(p.n + 255) / 256, 256, 0, s>>>(p, work, nt, ntiles);
+    const uint32_t nb = (p.n + 255) / 256, per_xcd = (nb + 7) / 8;
+    k_scatter_t<<<8 * per_xcd, 256, 0, s>>>(p, work, nt, ntiles, per_xcd);
     return hipGetLastError();
 }
 
@@ -896,6 +910,19 @@ __device__ __forceinline__ void tjoin_load(const NarrowTiles &nt, uint4 d, u32x4
         const uint32_t r = min(d.y + k * kJoinThreads + threadIdx.x, max(d.z, 1u) - 1);
         rec[k] = *(const u32x4 *)(nt.recs + r);
     }
+}
+
+// Eytzinger (BFS) slot of sorted row r of a 4096-row tile: rows 0 .. 4094
+// form a perfect binary tree at slots 1 .. 4095 (in-order index i = r + 1 sits
+// at level 11 - ctz(i)), row 4095 at slot 0.  A root-to-leaf walk touches
+// slots spread over a level instead of the power-of-two strides of a binary
+// search over sorted rows, which all fall in one or two LDS banks.
+static_assert(kTLog2 == 12, "eyt12 assumes 4096-row tiles");
+__device__ __forceinline__ uint32_t eyt12(uint32_t r)
+{
+    const uint32_t i = r + 1;
+    const int tz = __builtin_ctz(i);
+    return i == 4096 ? 0 : (1u << (11 - tz)) + (i >> (tz + 1));
 }
 
 template <int N>
@@ -958,7 +985,10 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
 #pragma unroll
         for (int v = 0; v < RQ; ++v) {
             const uint32_t quad = threadIdx.x + kJoinThreads * v;
-            ((u32x4 *)keys)[quad] = rk[v];
+            keys[eyt12(4 * quad)] = rk[v].x;
+            keys[eyt12(4 * quad + 1)] = rk[v].y;
+            keys[eyt12(4 * quad + 2)] = rk[v].z;
+            keys[eyt12(4 * quad + 3)] = rk[v].w;
             ((u32x4 *)rank)[quad] = rr[v];
             uint32_t m = max(max(rr[v].x, rr[v].y), max(rr[v].z, rr[v].w));
             m = max(m, (uint32_t)__shfl_xor((int)m, 1, 64));
@@ -982,16 +1012,19 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
             const uint32_t r = d.y + k * kJoinThreads + threadIdx.x;
             if (r >= d.z) continue;
             const uint32_t lo = crec[k].x, hi = crec[k].y, rs = crec[k].z;
-            // pa = #keys < lo, pb = #keys <= hi over rows [0, tn): both reads
-            // of a step in flight together
-            uint32_t pa = 0, pb = 0;
+            // pa = #keys < lo, pb = #keys <= hi: root-to-leaf walks of the
+            // Eytzinger tree, both reads of a level in flight together; rows
+            // past tn are padding (0xFFFFFFFF, never below lo)
+            uint32_t ja = 1, jb = 1;
 #pragma unroll
-            for (uint32_t step = T; step > 0; step >>= 1) {
-                const bool oka = pa + step <= tn, okb = pb + step <= tn;
-                const uint32_t ka = keys[min(pa + step, tn) - 1], kb = keys[min(pb + step, tn) - 1];
-                pa += (oka && ka < lo) ? step : 0;
-                pb += (okb && kb <= hi) ? step : 0;
+            for (int d = 0; d < kTLog2; ++d) {
+                const uint32_t ka = keys[ja], kb = keys[jb];
+                ja = 2 * ja + (ka < lo);
+                jb = 2 * jb + (kb <= hi);
             }
+            const uint32_t kl = keys[0];  // the tile's last (largest) row
+            const uint32_t pa = min(ja - T + (kl < lo), tn);
+            const uint32_t pb = min(jb - T + (kl <= hi), tn);
             if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) verdict[crec[k].w] = 1;
         }
         if (next >= nitems) break;
