@@ -24,6 +24,36 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v)
 }
 
 // Exclusive block scan of one u32 per thread; NT threads.
+// 64-bit variant of block_excl_scan (two packed 32-bit sums that never carry).
+template <int NT>
+__device__ __forceinline__ uint64_t block_excl_scan64(uint64_t v, uint64_t *lds, uint64_t &total)
+{
+    constexpr int NW = NT / 64;
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+        uint64_t s = lane < NW ? lds[lane] : 0;
+#pragma unroll
+        for (int o = 1; o < NW; o <<= 1) {
+            const uint64_t y = __shfl_up(s, o, 64);
+            if (lane >= o) s += y;
+        }
+        if (lane < NW) lds[lane] = s;
+    }
+    __syncthreads();
+    const uint64_t pre = wid ? lds[wid - 1] : 0;
+    total = lds[NW - 1];
+    __syncthreads();
+    return pre + x - v;
+}
+
 template <int NT>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *lds, uint32_t &total)
 {

@@ -89,7 +89,7 @@ struct hsc_ctx {
     uint32_t probe_ntiles = 0;  // tiles of the view the last probe ran on
     // narrow tiles: u32 key deltas + commit ranks (dense batches)
     bool ntiles32 = false;
-    DBuf d_commits, d_cdir, d_tdir, d_trad, d_key32, d_rank32, d_ctmp[4];
+    DBuf d_commits, d_cdir, d_tdir, d_trad, d_done, w_vflags, d_key32, d_rank32, d_ctmp[4];
     Dir16 cdir{}, tdir{};
     uint32_t trad_m = 0;       // tile bucket table size (0: none)
     uint32_t ncommit = 0;
@@ -864,7 +864,11 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     work.chunk = narrow_tiles_chunk();
     work.G = (uint32_t)std::max<size_t>(1, (nwork + work.chunk - 1) / work.chunk);
     const size_t n1 = std::max<uint32_t>(p.n, 1);
-    HIPCHK(c, c->w_hist.ensure(4 * (size_t)work.G * nt));
+    HIPCHK(c, c->w_hist.ensure(4 * (size_t)hist_stride(work.G) * nt));
+    if (!c->d_done.p) {  // plan arrival counter: zeroed once, reset by its last block
+        HIPCHK(c, c->d_done.ensure(64));
+        HIPCHK(c, hipMemsetAsync(c->d_done.p, 0, 64, s));
+    }
     HIPCHK(c, c->w_counts.ensure(4 * ((size_t)nt + 1)));
     HIPCHK(c, c->w_bucket.ensure(4 * ((size_t)nt + 1)));
     HIPCHK(c, c->w_cursor.ensure(4 * ((size_t)nt + 1)));
@@ -892,25 +896,29 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     ntl.code = c->w_tcode.as<uint4>();
     ntl.code2 = c->w_tcode2.as<uint4>();
     ntl.recs = c->w_trecs.as<uint4>();
+    // conflict flags: internal, all zero between batches (the pack clears them)
+    const size_t had = c->w_vflags.bytes;
+    HIPCHK(c, c->w_vflags.ensure(std::max<size_t>(b->n_txn, 1)));
+    if (c->w_vflags.bytes != had) HIPCHK(c, hipMemsetAsync(c->w_vflags.p, 0, c->w_vflags.bytes, s));
+    uint8_t *flags = c->w_vflags.as<uint8_t>();
     const bool tm = c->timing;
     if (tm)
         for (int i = 0; i < 6; ++i)
             if (!c->ev[i]) HIPCHK(c, hipEventCreate(&c->ev[i]));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
-    if (b->n_txn) HIPCHK(c, hipMemsetAsync(b->verdict, 0, b->n_txn, s));
-    HIPCHK(c, launch_locate_t(c->nv, wn, p, work, ntl, b->verdict, s));
+    HIPCHK(c, launch_locate_t(c->nv, wn, p, work, ntl, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     if (p.n && wn.ntiles) {
-        HIPCHK(c, launch_plan(wn, work, s));
+        HIPCHK(c, launch_plan_t(work, wn.ntiles, c->d_done.as<uint32_t>(), s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
         HIPCHK(c, launch_scatter_t(p, work, ntl, wn.ntiles, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
-        HIPCHK(c, launch_join_t(work, ntl, wn.n, wn.ntiles, max_items, b->verdict, s));
+        HIPCHK(c, launch_join_t(work, ntl, wn.n, wn.ntiles, max_items, flags, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
     } else if (tm) {
         for (int i = 2; i <= 4; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
     }
-    HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
+    HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
     return HSC_OK;
 }
@@ -1039,6 +1047,7 @@ static int collect_timing(hsc_ctx *c)
         HIPCHK(c, hipMemcpy(&nrec, c->w_bucket.as<uint32_t>() + c->probe_ntiles, 4,
                             hipMemcpyDeviceToHost));
     c->last.records = nrec;
+    c->last.tiles = c->probe_ntiles;  // tiles of the view the last probe joined over
     return HSC_OK;
 }
 
@@ -1151,7 +1160,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_item_desc, &c->w_recs,
                     &c->d_nkeys, &c->d_nmaxs, &c->d_nbase, &c->d_nzero, &c->d_ntmax,
                     &c->d_nsp_g, &c->d_nsp_w, &c->d_ngs, &c->d_nscratch, &c->p_code_lo,
-                    &c->p_code_hi, &c->p_zero, &c->d_commits, &c->d_cdir, &c->d_tdir, &c->d_trad, &c->d_key32, &c->d_rank32,
+                    &c->p_code_hi, &c->p_zero, &c->d_commits, &c->d_cdir, &c->d_tdir, &c->d_trad, &c->d_done, &c->w_vflags, &c->d_key32, &c->d_rank32,
                     &c->d_ctmp[0], &c->d_ctmp[1], &c->d_ctmp[2], &c->d_ctmp[3], &c->w_tcode,
                     &c->w_tcode2, &c->w_trecs};
     for (DBuf *b : bufs) b->release();

@@ -219,6 +219,17 @@ uint32_t narrow_trad_buckets(uint32_t ntiles);
 hipError_t narrow_trad_build(const uint64_t *first, uint32_t ntiles, uint32_t m, uint32_t *trad,
                              hipStream_t s);
 uint32_t narrow_tiles_dir_lds();
+// Narrow tiles keep the chunk histogram tile-major: hist[t * hist_stride(G) + g].
+__host__ __device__ inline uint32_t hist_stride(uint32_t G) { return (G + 7) & ~7u; }
+// XCD-contiguous chunk order: block b of a grid of 8 * per blocks runs on XCD
+// b % 8 and takes chunk (b % 8) * per + b / 8.
+__host__ __device__ inline uint32_t xcd_chunk(uint32_t b, uint32_t per) { return (b & 7) * per + (b >> 3); }
+// Column scans of the tile-major histogram and the tile plan in one launch
+// (the last workgroup plans; done = a zeroed counter it resets).
+hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *done, hipStream_t s);
+// Verdict bytes + bitmap from the internal conflict flags; clears the flags.
+hipError_t launch_pack_flags(uint8_t *flags, uint32_t n_txn, uint8_t *verdict, uint64_t *bitmap,
+                             hipStream_t s);
 hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeView &p,
                            const ProbeWork &work, const NarrowTiles &nt, uint8_t *verdict,
                            hipStream_t s);

@@ -73,6 +73,46 @@ __host__ __device__ inline bool rel_diff(int W, int lw, int tz, uint64_t xg, con
     return true;
 }
 
+// rel_diff for W = 1 or 2 key words held in registers: the words subtract as
+// one 128-bit borrow chain, the gid limb after it; the limb roles come from
+// uniform branches on lw and the shift by tz (< 64) is a funnel shift whose
+// tz = 0 case needs no branch ((d << 1) << 63 = 0).
+template <int W>
+__device__ __forceinline__ bool rel_diff_w(int lw, int tz, uint64_t xg, const uint64_t (&xw)[W],
+                                           uint64_t bg, const uint64_t *bw, uint64_t sat,
+                                           uint64_t &v, bool &rem)
+{
+    static_assert(W == 1 || W == 2, "register form for 1 or 2 words");
+    typedef unsigned __int128 u128;
+    uint64_t d[W + 1];
+    bool borrow;
+    if constexpr (W == 2) {
+        const u128 x = (u128)xw[0] << 64 | xw[1], b = (u128)bw[0] << 64 | bw[1];
+        const u128 dd = x - b;
+        d[1] = (uint64_t)(dd >> 64);
+        d[2] = (uint64_t)dd;
+        borrow = x < b;
+    } else {
+        d[1] = xw[0] - bw[0];
+        borrow = xw[0] < bw[0];
+    }
+    d[0] = xg - bg - (borrow ? 1 : 0);
+    if (xg < bg || (xg == bg && borrow)) return false;
+    uint64_t below, d_last, d_prev, high;
+    if (W == 2 && lw == 2) {
+        below = 0, d_last = d[W], d_prev = d[W - 1], high = d[0];
+    } else if (lw == 1) {
+        below = d[W] & (W == 2 ? ~0ull : 0), d_last = d[1], d_prev = d[0], high = 0;
+    } else {
+        below = d[1] | d[W], d_last = d[0], d_prev = 0, high = 0;
+    }
+    const uint64_t top = d_prev >> tz;
+    const uint64_t low = (d_last >> tz) | ((d_prev << 1) << (63 - tz));
+    rem = (below | (d_last & ((1ull << tz) - 1))) != 0;
+    v = (high | top) ? sat : (low < sat ? low : sat);
+    return true;
+}
+
 bool narrow_span_fits(int W, int lw, int tz, const uint64_t *first, const uint64_t *last)
 {
     uint64_t v;
@@ -510,8 +550,8 @@ __device__ __forceinline__ void dir16_count(const Dir16 &d, const uint64_t *lds,
 }
 
 // ---- locate: codes, snapshot ranks, end tiles, per-chunk tile histogram ----
-// One workgroup per chunk of kLocTP * kLocateThreads probes; thread t owns
-// probes c0 + t + kLocateThreads j, j < kLocTP (consecutive lanes =
+// One workgroup per chunk of kLocTP * kLocTThreads probes; thread t owns
+// probes c0 + t + kLocTThreads j, j < kLocTP (consecutive lanes =
 // consecutive probes, so a read set's ranges sit in neighbouring lanes).
 // Every probe load is issued up front; the tile and snapshot-rank searches
 // run for all kLocTP probes in lockstep over 16-ary directories whose upper
@@ -520,6 +560,7 @@ __device__ __forceinline__ void dir16_count(const Dir16 &d, const uint64_t *lds,
 // first join record {tile << 12 | rank, lo, hi, r(S)} and, for a range that
 // spans two tiles, its second one.
 constexpr int kLocTP = 4;
+constexpr int kLocTThreads = 1024;  // 4096 probes per chunk (in-chunk ranks fit 12 bits)
 constexpr uint32_t kHasSecond = 1u << 31;
 constexpr int kDirLds = 4400;  // directory entries staged in LDS per directory
 
@@ -534,10 +575,12 @@ __device__ __forceinline__ void locate_codes(const NarrowView &nv, const ProbeVi
     uint64_t a;
     bool live;
     if constexpr (W > 0) {
-        a = rel_diff(W, nv.lw, nv.tz, g, xl, 1, nv.base[0], nv.base + 1, 1, kSat, v, rem)
+        const uint64_t(&wl)[W] = *(const uint64_t(*)[W])xl;
+        const uint64_t(&wh)[W] = *(const uint64_t(*)[W])xh;
+        a = rel_diff_w<W>(nv.lw, nv.tz, g, wl, nv.base[0], nv.base + 1, kSat, v, rem)
                 ? (v >= kSat ? kSat : v + (rem ? 1 : 0))
                 : 0;
-        live = rel_diff(W, nv.lw, nv.tz, g, xh, 1, nv.base[0], nv.base + 1, 1, kSat, v, rem);
+        live = rel_diff_w<W>(nv.lw, nv.tz, g, wh, nv.base[0], nv.base + 1, kSat, v, rem);
     } else {
         a = rel_diff(nv.W, nv.lw, nv.tz, g, p.lo + q, p.n, nv.base[0], nv.base + 1, 1, kSat, v,
                      rem)
@@ -618,9 +661,9 @@ __host__ __device__ inline LocLds loc_lds(const NarrowTiles &nt, uint32_t ntiles
     L.trad = o;
     o += nt.trad ? 2 * ((nt.trad_m + 1 + 7) & ~7u) : 0;
     L.sbuf = o;
-    o += 8 * kLocateThreads;
+    o += 8 * kLocTThreads;
     L.rbuf = o;
-    o += 4 * kLocateThreads;
+    o += 4 * kLocTThreads;
     L.bytes = o;
     return L;
 }
@@ -661,7 +704,7 @@ __device__ __forceinline__ void trad_count(const uint64_t *first, const uint16_t
 
 // W = key words held in registers (1 or 2), 0 = read from memory (any W)
 template <int W, bool kTrad>
-__global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinView wt,
+__global__ __launch_bounds__(kLocTThreads) void k_locate_t(NarrowView nv, WinView wt,
                                                              ProbeView p, ProbeWork work,
                                                              NarrowTiles nt, uint8_t *verdict)
 {
@@ -677,7 +720,9 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinV
     const int lane = threadIdx.x & 63;
     uint64_t *sb = (uint64_t *)(lb + L.sbuf) + (threadIdx.x & ~63u);
     uint32_t *rb = (uint32_t *)(lb + L.rbuf) + (threadIdx.x & ~63u);
-    const uint32_t c0 = blockIdx.x * work.chunk;
+    const uint32_t g = xcd_chunk(blockIdx.x, (work.G + 7) / 8);
+    if (g >= work.G) return;
+    const uint32_t c0 = g * work.chunk;
     const uint32_t c1 = min(p.n, c0 + work.chunk);
     // all probe loads first
     uint32_t qq[kLocTP], gg[kLocTP];
@@ -685,7 +730,7 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinV
     uint64_t snap[kLocTP], xl[kLocTP][WR], xh[kLocTP][WR];
 #pragma unroll
     for (int j = 0; j < kLocTP; ++j) {
-        qq[j] = c0 + threadIdx.x + kLocateThreads * j;
+        qq[j] = c0 + threadIdx.x + kLocTThreads * j;
         valid[j] = qq[j] < c1;
         const uint32_t q = valid[j] ? qq[j] : 0;
         gg[j] = p.n ? p.gid[q] : 0;
@@ -699,16 +744,16 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinV
     int tshift = 0;
     if constexpr (kTrad) {
         const u64x2 *src = (const u64x2 *)wt.sp_w;
-        for (uint32_t i = threadIdx.x; i < ntiles / 2; i += kLocateThreads)
+        for (uint32_t i = threadIdx.x; i < ntiles / 2; i += kLocTThreads)
             ((u64x2 *)tfirst)[i] = src[i];
         if ((ntiles & 1) && threadIdx.x == 0) tfirst[ntiles - 1] = wt.sp_w[ntiles - 1];
-        for (uint32_t i = threadIdx.x; i <= nt.trad_m; i += kLocateThreads) T[i] = (uint16_t)nt.trad[i];
+        for (uint32_t i = threadIdx.x; i <= nt.trad_m; i += kLocTThreads) T[i] = (uint16_t)nt.trad[i];
         tshift = (int)nt.trad[nt.trad_m + 1];
     } else {
         dir16_stage(nt.tdir, tfirst);
     }
     dir16_stage(nt.cdir, cdir);
-    for (uint32_t i = threadIdx.x; i < ntiles; i += kLocateThreads) hist[i] = 0;
+    for (uint32_t i = threadIdx.x; i < ntiles; i += kLocTThreads) hist[i] = 0;
     uint64_t lo[kLocTP], hi[kLocTP];
 #pragma unroll
     for (int j = 0; j < kLocTP; ++j)
@@ -816,14 +861,15 @@ __global__ __launch_bounds__(kLocateThreads) void k_locate_t(NarrowView nv, WinV
         nt.code[q] = r0;
     }
     // table locks: any write to a locked table after the snapshot
-    for (uint32_t q = blockIdx.x * kLocateThreads + threadIdx.x; q < p.n_lock;
-         q += gridDim.x * kLocateThreads) {
+    for (uint32_t q = g * kLocTThreads + threadIdx.x; q < p.n_lock; q += work.G * kLocTThreads) {
         const uint32_t t = p.lock_table[q];
         if (t < wt.ntables && wt.table_max[t] > p.lock_snap[q]) verdict[p.lock_txn[q]] = 1;
     }
     __syncthreads();
-    uint32_t *row = work.hist + (size_t)blockIdx.x * ntiles;
-    for (uint32_t i = threadIdx.x; i < ntiles; i += kLocateThreads) row[i] = hist[i];
+    // column g of the tile-major histogram (neighbouring chunks of a line are
+    // written from the same XCD)
+    const uint32_t hs = hist_stride(work.G);
+    for (uint32_t i = threadIdx.x; i < ntiles; i += kLocTThreads) work.hist[(size_t)i * hs + g] = hist[i];
 }
 
 hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeView &p,
@@ -835,7 +881,8 @@ hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeV
     const bool tr = nt.trad != nullptr;
     const int w = nv.W == 1 || nv.W == 2 ? nv.W : 0;
 #define HSC_LOCATE(W_, TR_)                                                                        \
-    k_locate_t<W_, TR_><<<work.G, kLocateThreads, lds, s>>>(nv, wt, p, work, nt, verdict)
+    k_locate_t<W_, TR_><<<8 * ((work.G + 7) / 8), kLocTThreads, lds, s>>>(nv, wt, p, work, nt,   \
+                                                                            verdict)
     if (w == 1 && tr)
         HSC_LOCATE(1, true);
     else if (w == 1)
@@ -853,8 +900,117 @@ hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeV
 }
 
 // probes per locate workgroup, directory entries staged in LDS
-uint32_t narrow_tiles_chunk() { return kLocTP * kLocateThreads; }
+uint32_t narrow_tiles_chunk() { return kLocTP * kLocTThreads; }
 uint32_t narrow_tiles_dir_lds() { return kDirLds; }
+
+// ---- plan: column scans + tile plan in one launch ----
+// Wave w of block b scans tile 8 b + w: its column hist[t][0 .. G) (lane l
+// owns entries 8 l .. 8 l + 7, two 16-byte loads; G <= kMaxChunks = 512)
+// becomes exclusive chunk offsets inside the tile's bucket.  Column totals go
+// to counts[] through returning atomics, which are performed at the memory
+// side, so the last block to arrive reads every total back with atomics -- no
+// L2 write-back or invalidate (an agent-scope fence per block costs an L2
+// walk each).  That block scans the totals, one lane per tile so every load
+// and store coalesces, into bucket offsets and join items, and resets the
+// arrival counter.
+constexpr int kPlanThreads = 512;
+static_assert(kMaxChunks <= 512, "one 512-entry column pass per wave");
+__global__ __launch_bounds__(kPlanThreads) void k_plan_t(ProbeWork work, uint32_t ntiles,
+                                                         uint32_t *done)
+{
+    __shared__ uint64_t lds64[16];
+    __shared__ bool last;
+    const int lane = threadIdx.x & 63;
+    const uint32_t t = blockIdx.x * (kPlanThreads / 64) + (threadIdx.x >> 6);
+    const uint32_t hs = hist_stride(work.G);
+    if (t < ntiles) {
+        u32x4 *col = (u32x4 *)(work.hist + (size_t)t * hs);
+        const uint32_t e = 8 * lane;
+        u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
+        if (e < hs) {
+            a = col[e / 4];
+            b = col[e / 4 + 1];
+        }
+        // entries past G are never written: mask them
+        const uint32_t v[8] = {e + 0 < work.G ? a.x : 0, e + 1 < work.G ? a.y : 0,
+                               e + 2 < work.G ? a.z : 0, e + 3 < work.G ? a.w : 0,
+                               e + 4 < work.G ? b.x : 0, e + 5 < work.G ? b.y : 0,
+                               e + 6 < work.G ? b.z : 0, e + 7 < work.G ? b.w : 0};
+        uint32_t sum = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sum += v[k];
+        uint32_t x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        uint32_t run = x - sum;
+        if (e < hs) {
+            u32x4 oa, ob;
+            oa.x = run; run += v[0];
+            oa.y = run; run += v[1];
+            oa.z = run; run += v[2];
+            oa.w = run; run += v[3];
+            ob.x = run; run += v[4];
+            ob.y = run; run += v[5];
+            ob.z = run; run += v[6];
+            ob.w = run;
+            col[e / 4] = oa;
+            col[e / 4 + 1] = ob;
+        }
+        if (lane == 63) (void)atomicExch(&work.counts[t], x);
+    }
+    __syncthreads();  // every wave's atomics have returned
+    if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    // every tile total in flight at once (kHistCap / kPlanThreads per thread)
+    constexpr int kRounds = kHistCap / kPlanThreads;
+    uint32_t cvs[kRounds];
+#pragma unroll
+    for (int k = 0; k < kRounds; ++k) {
+        const uint32_t tt = k * kPlanThreads + threadIdx.x;
+        cvs[k] = tt < ntiles ? atomicAdd(&work.counts[tt], 0u) : 0;
+    }
+    uint32_t carry_b = 0, carry_i = 0;
+#pragma unroll
+    for (int k = 0; k < kRounds; ++k) {
+        if (k * kPlanThreads >= ntiles) break;
+        const uint32_t tt = k * kPlanThreads + threadIdx.x;
+        const uint32_t cv = cvs[k];
+        const uint32_t ch = (cv + kJoinChunk - 1) / kJoinChunk;  // chunks of the tile
+        const uint32_t xch = ch ? ch - 1 : 0;                      // beyond its own item
+        // records (low 32 bits) and extra items (high 32 bits) in one scan
+        uint64_t tot;
+        const uint64_t pre = block_excl_scan64<kPlanThreads>(cv | (uint64_t)xch << 32, lds64, tot);
+        const uint32_t pb = (uint32_t)pre + carry_b, pi = (uint32_t)(pre >> 32) + carry_i;
+        if (tt < ntiles) {
+            work.bucket_off[tt] = pb;
+            work.item_off[tt] = pi;
+            for (uint32_t j = 1; j < ch; ++j) {  // chunk 0 is item tt itself
+                const uint32_t r0 = pb + j * kJoinChunk;
+                work.item_desc[ntiles + pi + j - 1] =
+                    make_uint4(tt, r0, min(r0 + kJoinChunk, pb + cv), 0);
+            }
+        }
+        carry_b += (uint32_t)tot;
+        carry_i += (uint32_t)(tot >> 32);
+    }
+    if (threadIdx.x == 0) {
+        work.bucket_off[ntiles] = carry_b;
+        work.item_off[ntiles] = ntiles + carry_i;  // items: one per tile + the extra chunks
+        *done = 0;
+    }
+}
+
+hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *done, hipStream_t s)
+{
+    if (ntiles == 0) return hipSuccess;
+    constexpr uint32_t per = kPlanThreads / 64;
+    k_plan_t<<<(ntiles + per - 1) / per, kPlanThreads, 0, s>>>(work, ntiles, done);
+    return hipGetLastError();
+}
 
 // ---- scatter: 16-byte records into tile buckets ----
 // Block b runs on XCD b % 8 (round-robin dispatch); blocks are renumbered so
@@ -870,13 +1026,14 @@ __global__ __launch_bounds__(256) void k_scatter_t(ProbeView p, ProbeWork work, 
     const uint4 a = nt.code[q];
     if (a.x == kNoTile32) return;
     const uint32_t txn = p.txn[q];
-    const uint32_t *row = work.hist + (size_t)(q / work.chunk) * ntiles;
+    const uint32_t *col = work.hist + q / work.chunk;  // hist[t * hs + chunk]
+    const size_t hs = hist_stride(work.G);
     const uint32_t ta = (a.x & ~kHasSecond) >> 12;
-    nt.recs[work.bucket_off[ta] + row[ta] + (a.x & 0xFFFu)] = make_uint4(a.y, a.z, a.w, txn);
+    nt.recs[work.bucket_off[ta] + col[ta * hs] + (a.x & 0xFFFu)] = make_uint4(a.y, a.z, a.w, txn);
     if (a.x & kHasSecond) {
         const uint4 c = nt.code2[q];
         const uint32_t tb = c.x >> 12;
-        nt.recs[work.bucket_off[tb] + row[tb] + (c.x & 0xFFFu)] = make_uint4(c.y, c.z, c.w, txn);
+        nt.recs[work.bucket_off[tb] + col[tb * hs] + (c.x & 0xFFFu)] = make_uint4(c.y, c.z, c.w, txn);
     }
 }
 
@@ -889,29 +1046,11 @@ hipError_t launch_scatter_t(const ProbeView &p, const ProbeWork &work, const Nar
     return hipGetLastError();
 }
 
-
 // ---- join: 8-byte rows ----
 // Row quad v of thread t = rows 4 (t + kJoinThreads v) .. + 3: one 16-byte
 // load of keys and one of ranks per quad; 16-row maxima over 4 lanes,
 // 128-row maxima over 32 lanes.
-template <int RQ, int kRec>
-__device__ __forceinline__ void tjoin_load(const NarrowTiles &nt, uint4 d, u32x4 (&rk)[RQ],
-                                           u32x4 (&rr)[RQ], u32x4 (&rec)[kRec])
-{
-    const size_t ts = (size_t)d.x << kTLog2;
-#pragma unroll
-    for (int v = 0; v < RQ; ++v) {
-        const size_t row = ts + 4 * (threadIdx.x + kJoinThreads * v);
-        rk[v] = *(const u32x4 *)(nt.key32 + row);
-        rr[v] = *(const u32x4 *)(nt.rank32 + row);
-    }
-#pragma unroll
-    for (int k = 0; k < kRec; ++k) {
-        const uint32_t r = min(d.y + k * kJoinThreads + threadIdx.x, max(d.z, 1u) - 1);
-        rec[k] = *(const u32x4 *)(nt.recs + r);
-    }
-}
-
+//
 // Eytzinger (BFS) slot of sorted row r of a 4096-row tile: rows 0 .. 4094
 // form a perfect binary tree at slots 1 .. 4095 (in-order index i = r + 1 sits
 // at level 11 - ctz(i)), row 4095 at slot 0.  A root-to-leaf walk touches
@@ -958,6 +1097,10 @@ __device__ __forceinline__ bool any_after32(const uint32_t *rank, const uint32_t
     return r;
 }
 
+// One workgroup per join item.  Item t < ntiles is the first kJoinChunk
+// records of tile t (its range comes from bucket_off, so the tile's rows are
+// requested before anything else is known); items >= ntiles are the further
+// chunks of heavy tiles, described in item_desc.
 __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowTiles nt,
                                                          uint32_t n, uint32_t ntiles,
                                                          uint8_t *verdict)
@@ -970,66 +1113,68 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
     __shared__ uint32_t b16[T / 16];
     __shared__ uint32_t b128[T / 128];
 
-    const uint32_t nitems = work.item_off[ntiles];
-    uint32_t item = blockIdx.x;
-    if (item >= nitems) return;
-    const uint32_t grid = gridDim.x;
+    const uint32_t item = blockIdx.x;
+    uint32_t tile, r0, r1;
+    if (item < ntiles) {
+        tile = item;
+    } else {
+        if (item >= work.item_off[ntiles]) return;
+        const uint4 d = work.item_desc[item];
+        tile = d.x, r0 = d.y, r1 = d.z;
+    }
     u32x4 rk[RQ], rr[RQ], rec[kRec];
-    uint4 dcur = work.item_desc[item];
-    uint4 dnext = work.item_desc[min(item + grid, nitems - 1)];
-    tjoin_load<RQ, kRec>(nt, dcur, rk, rr, rec);
-    while (true) {
-        u32x4 crec[kRec];
+    const size_t ts = (size_t)tile << kTLog2;
 #pragma unroll
-        for (int k = 0; k < kRec; ++k) crec[k] = rec[k];
+    for (int v = 0; v < RQ; ++v) {
+        const size_t row = ts + 4 * (threadIdx.x + kJoinThreads * v);
+        rk[v] = *(const u32x4 *)(nt.key32 + row);
+        rr[v] = *(const u32x4 *)(nt.rank32 + row);
+    }
+    if (item < ntiles) {
+        r0 = work.bucket_off[tile];
+        r1 = min(r0 + kJoinChunk, work.bucket_off[tile + 1]);
+    }
+    if (r0 >= r1) return;  // a tile no range reaches
 #pragma unroll
-        for (int v = 0; v < RQ; ++v) {
-            const uint32_t quad = threadIdx.x + kJoinThreads * v;
-            keys[eyt12(4 * quad)] = rk[v].x;
-            keys[eyt12(4 * quad + 1)] = rk[v].y;
-            keys[eyt12(4 * quad + 2)] = rk[v].z;
-            keys[eyt12(4 * quad + 3)] = rk[v].w;
-            ((u32x4 *)rank)[quad] = rr[v];
-            uint32_t m = max(max(rr[v].x, rr[v].y), max(rr[v].z, rr[v].w));
-            m = max(m, (uint32_t)__shfl_xor((int)m, 1, 64));
-            m = max(m, (uint32_t)__shfl_xor((int)m, 2, 64));
-            if ((threadIdx.x & 3) == 0) b16[quad >> 2] = m;
+    for (int k = 0; k < kRec; ++k)
+        rec[k] = *(const u32x4 *)(nt.recs + min(r0 + k * kJoinThreads + threadIdx.x, r1 - 1));
 #pragma unroll
-            for (int d = 4; d < 32; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
-            if ((threadIdx.x & 31) == 0) b128[quad >> 5] = m;
+    for (int v = 0; v < RQ; ++v) {
+        const uint32_t quad = threadIdx.x + kJoinThreads * v;
+        keys[eyt12(4 * quad)] = rk[v].x;
+        keys[eyt12(4 * quad + 1)] = rk[v].y;
+        keys[eyt12(4 * quad + 2)] = rk[v].z;
+        keys[eyt12(4 * quad + 3)] = rk[v].w;
+        ((u32x4 *)rank)[quad] = rr[v];
+        uint32_t m = max(max(rr[v].x, rr[v].y), max(rr[v].z, rr[v].w));
+        m = max(m, (uint32_t)__shfl_xor((int)m, 1, 64));
+        m = max(m, (uint32_t)__shfl_xor((int)m, 2, 64));
+        if ((threadIdx.x & 3) == 0) b16[quad >> 2] = m;
+#pragma unroll
+        for (int d = 4; d < 32; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+        if ((threadIdx.x & 31) == 0) b128[quad >> 5] = m;
+    }
+    __syncthreads();
+    const uint32_t tn = min(T, n - (tile << kTLog2));
+#pragma unroll
+    for (int k = 0; k < kRec; ++k) {
+        const uint32_t r = r0 + k * kJoinThreads + threadIdx.x;
+        if (r >= r1) continue;
+        const uint32_t lo = rec[k].x, hi = rec[k].y, rs = rec[k].z;
+        // pa = #keys < lo, pb = #keys <= hi: root-to-leaf walks of the
+        // Eytzinger tree, both reads of a level in flight together; rows
+        // past tn are padding (0xFFFFFFFF, never below lo)
+        uint32_t ja = 1, jb = 1;
+#pragma unroll
+        for (int d = 0; d < kTLog2; ++d) {
+            const uint32_t ka = keys[ja], kb = keys[jb];
+            ja = 2 * ja + (ka < lo);
+            jb = 2 * jb + (kb <= hi);
         }
-        __syncthreads();
-        const uint32_t next = item + grid;
-        const uint4 d = dcur;
-        dcur = dnext;
-        if (next < nitems) {
-            dnext = work.item_desc[min(next + grid, nitems - 1)];
-            tjoin_load<RQ, kRec>(nt, dcur, rk, rr, rec);
-        }
-        const uint32_t tn = min(T, n - (d.x << kTLog2));
-#pragma unroll
-        for (int k = 0; k < kRec; ++k) {
-            const uint32_t r = d.y + k * kJoinThreads + threadIdx.x;
-            if (r >= d.z) continue;
-            const uint32_t lo = crec[k].x, hi = crec[k].y, rs = crec[k].z;
-            // pa = #keys < lo, pb = #keys <= hi: root-to-leaf walks of the
-            // Eytzinger tree, both reads of a level in flight together; rows
-            // past tn are padding (0xFFFFFFFF, never below lo)
-            uint32_t ja = 1, jb = 1;
-#pragma unroll
-            for (int d = 0; d < kTLog2; ++d) {
-                const uint32_t ka = keys[ja], kb = keys[jb];
-                ja = 2 * ja + (ka < lo);
-                jb = 2 * jb + (kb <= hi);
-            }
-            const uint32_t kl = keys[0];  // the tile's last (largest) row
-            const uint32_t pa = min(ja - T + (kl < lo), tn);
-            const uint32_t pb = min(jb - T + (kl <= hi), tn);
-            if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) verdict[crec[k].w] = 1;
-        }
-        if (next >= nitems) break;
-        item = next;
-        __syncthreads();
+        const uint32_t kl = keys[0];  // the tile's last (largest) row
+        const uint32_t pa = min(ja - T + (kl < lo), tn);
+        const uint32_t pb = min(jb - T + (kl <= hi), tn);
+        if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) verdict[rec[k].w] = 1;
     }
 }
 
@@ -1037,15 +1182,29 @@ hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t 
                          uint32_t ntiles, uint32_t max_items, uint8_t *verdict, hipStream_t s)
 {
     if (max_items == 0 || n == 0) return hipSuccess;
-    int dev = 0, ncu = 256;
-    if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    // one workgroup per item (measured faster than a persistent grid of 2-8
-    // workgroups per CU); HSC_JOIN_WG_PER_CU = k runs k per CU persistently
-    uint32_t per_cu = 0;
-    if (const char *e = getenv("HSC_JOIN_WG_PER_CU")) per_cu = (uint32_t)atoi(e);
-    const uint32_t grid = per_cu ? std::min<uint32_t>(max_items, per_cu * (uint32_t)ncu) : max_items;
-    k_join_t<<<grid, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
+    k_join_t<<<max_items, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
+    return hipGetLastError();
+}
+
+// Verdict bytes of the batch from the conflict flags the probe kernels set
+// (an internal array, so nothing has to clear the caller's buffer first):
+// verdict[t] = flag, bitmap bit t = flag (one ballot per 64 transactions), and
+// set flags are cleared for the next batch.
+__global__ void k_pack_flags(uint8_t *flags, uint32_t n, uint8_t *verdict, uint64_t *bitmap)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool v = t < n && flags[t] != 0;
+    if (t < n) verdict[t] = v;
+    if (v) flags[t] = 0;
+    const uint64_t m = __ballot(v);
+    if (bitmap && (threadIdx.x & 63) == 0 && t < n) bitmap[t >> 6] = m;
+}
+
+hipError_t launch_pack_flags(uint8_t *flags, uint32_t n_txn, uint8_t *verdict, uint64_t *bitmap,
+                             hipStream_t s)
+{
+    if (n_txn == 0) return hipSuccess;
+    k_pack_flags<<<(n_txn + 255) / 256, 256, 0, s>>>(flags, n_txn, verdict, bitmap);
     return hipGetLastError();
 }
 

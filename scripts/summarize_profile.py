@@ -5,7 +5,8 @@
 reads gpurun_out/prof_TAG_{kt,fetch,write,sq}/ and writes
   profiles/TAG_kernel_stats.csv   (the --kernel-trace --stats summary)
   profiles/TAG_summary.md         (per-kernel avg time, HBM bytes, SQ counters)
-  profiles/traffic.json           (HBM bytes per k_join launch, read by bench.py)
+  profiles/traffic.json           (HBM bytes per probe batch over the probe-phase
+                                   kernels, read by bench.py as roofline.traffic)
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in
 KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide (16 B/lane)
@@ -54,7 +55,7 @@ def main(tag):
              "--no-cpu` (config 2, 1 GPU).", "",
              "| kernel | calls | avg µs | HBM read MB (2×FETCH_SIZE) | HBM write MB | GB/s |",
              "|---|---|---|---|---|---|"]
-    traffic = {}
+    traffic = {"tag": tag, "kernels": {}, "probe_hbm_bytes_per_step": 0.0}
     for r in stats:
         k = short(r["Name"])
         avg_us = float(r["AverageNs"]) / 1e3
@@ -66,9 +67,9 @@ def main(tag):
         fmt = lambda x: "" if x is None else f"{x / 1e6:.1f}"
         lines.append(f"| {k} | {r['Calls']} | {avg_us:.2f} | {fmt(rd)} | {fmt(wr)} | "
                      f"{'' if gbs is None else f'{gbs:.0f}'} |")
-        if k.startswith("k_join") and rd is not None:
-            traffic = {"kernel": k, "join_hbm_bytes_per_launch": rd + (wr or 0),
-                       "read_bytes": rd, "write_bytes": wr, "avg_us": avg_us, "tag": tag}
+        if any(k.startswith(p) for p in PROBE_KERNELS) and rd is not None:
+            traffic["kernels"][k] = {"read_bytes": rd, "write_bytes": wr, "avg_us": avg_us}
+            traffic["probe_hbm_bytes_per_step"] += rd + (wr or 0)
     if sq:
         lines += ["", "SQ counters (per dispatch average):", "",
                   "| kernel | " + " | ".join(sorted({c for _, c in sq})) + " |",
@@ -79,7 +80,7 @@ def main(tag):
             vals = [sq.get((k, c), [0]) for c in sorted({c for _, c in sq})]
             lines.append(f"| {k} | " + " | ".join(f"{sum(v) / len(v):.3g}" for v in vals) + " |")
     open(os.path.join(prof, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
-    if traffic:
+    if traffic["kernels"]:
         json.dump(traffic, open(os.path.join(prof, "traffic.json"), "w"), indent=1)
     print("\n".join(lines))
 
