@@ -184,6 +184,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--wide", action="store_true", help="force the wide window layout")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the batches rotate over (each with its own outputs and "
+                         "probe lane), so consecutive batches' kernels can overlap")
     ap.add_argument("--config", type=int, default=2, choices=(2, 4),
                     help="2: the headline check batch; 4: dependency graph + SCC of a history")
     ap.add_argument("--history-txns", type=int, default=4_000_000)
@@ -243,41 +246,61 @@ def main():
         if world > 1:
             m = shard.route(m, shards.range_mask(m, rank), shards.lock_mask(m, rank))
         batches.append(upload_batch(torch, dev, m))
-    verdict = torch.zeros(T, dtype=torch.uint8, device=dev)
-    bitmap = torch.zeros((T + 63) // 64, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream()
-    v.set_stream(stream.cuda_stream)
-    structs = [probe_struct(hsc, b, verdict, bitmap if world == 1 else None, T) for b in batches]
+    S = max(1, args.streams)
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
+    comm = torch.cuda.Stream(device=dev) if world > 1 else None
+    verdicts = [torch.zeros(T, dtype=torch.uint8, device=dev) for _ in range(S)]
+    bitmaps = [torch.zeros((T + 63) // 64, dtype=torch.int64, device=dev) for _ in range(S)]
+    structs = [[probe_struct(hsc, b, verdicts[si], bitmaps[si] if world == 1 else None, T)
+                for si in range(S)] for b in batches]
+    torch.cuda.synchronize()
 
-    def step(k):
-        v.probe_device(structs[k % len(structs)])
+    def step(k, nstreams):
+        si = k % nstreams
+        st = streams[si]
+        v.set_stream(st.cuda_stream)
+        v.probe_device(structs[k % len(structs)][si])
+        if world > 1:  # verdict merge on one comm stream: the same collective order on every rank
+            e = torch.cuda.Event()
+            e.record(st)
+            comm.wait_event(e)
+            with torch.cuda.stream(comm):
+                shard.merge_verdicts(verdicts[si])
+            e2 = torch.cuda.Event()
+            e2.record(comm)
+            st.wait_event(e2)
+            v.pack_verdicts(verdicts[si].data_ptr(), T, bitmaps[si].data_ptr())
+
+    def timed(nstreams, steps, warmup):
+        for k in range(warmup):
+            step(k, nstreams)
+        torch.cuda.synchronize()
         if world > 1:
-            shard.merge_verdicts(verdict)
-            v.pack_verdicts(verdict.data_ptr(), T, bitmap.data_ptr())
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(steps):
+            step(k, nstreams)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        if world > 1:
+            e = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = float(e.item())
+        return el
 
-    for k in range(args.warmup):
-        step(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+    elapsed = timed(S, args.steps, args.warmup)
+    # one stream (each batch's kernels strictly after the previous batch's)
+    serial_elapsed = timed(1, args.steps, args.warmup) if S > 1 else elapsed
+    v.set_stream(streams[0].cuda_stream)
 
     # verdicts of batch 0 (for the conflict rate and the CPU parity sample)
-    step(0)
+    step(0, 1)
     torch.cuda.synchronize()
-    v0 = verdict.cpu().numpy().copy()
+    v0 = verdicts[0].cpu().numpy().copy()
     forced = batches[0]["forced"]
     v0 = np.maximum(v0, forced)
 
@@ -285,7 +308,7 @@ def main():
     v.enable_timing(True)
     acc = {}
     for k in range(args.steps):
-        v.probe_device(structs[k % len(structs)])
+        v.probe_device(structs[k % len(structs)][0])
         v.synchronize()
         for key, val in v.timing().items():
             acc.setdefault(key, []).append(val)
@@ -330,6 +353,8 @@ def main():
             "window_keys_per_gpu": n_keys,
             "logged_writes_per_gpu": n_w,
             "parallelism": f"key-range shards x{world}" + (" + RCCL max all-reduce" if world > 1 else ""),
+            "streams": S,
+            "serial_ms_per_step": serial_elapsed / args.steps * 1e3,
             "window_layout": {hsc.LAYOUT_NARROW: "narrow (u32 tile-relative keys)",
                               hsc.LAYOUT_WIDE: "wide"}.get(v.layout, "?"),
             "conflict_rate": float((v0 != 0).mean()),

@@ -116,11 +116,90 @@ struct hsc_ctx {
     GraphBufs graph;
     uint32_t graph_ntxn = 0;
 
+    // Probe lanes: the probe scratch above belongs to the active lane; other
+    // lanes park theirs here.  A lane is bound to the stream that last used
+    // it, so batches on different streams never share scratch and can run
+    // concurrently; a lane taken over by another stream first waits for the
+    // lane's last batch (its done event).
+    struct Lane {
+        DBuf b[16];
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;
+        uint64_t tick = 0;
+    };
+    static constexpr int kLanes = 4;
+    Lane lanes[kLanes];
+    int lane = 0;
+    uint64_t lane_tick = 0;
+
     // timing
     bool timing = false;
     hipEvent_t ev[8] = {};
     hsc_timing last{};
 };
+
+// probe scratch that moves with a lane (hsc_ctx::Lane::b holds at most 16)
+static DBuf hsc_ctx::*const kLaneBufs[] = {
+    &hsc_ctx::w_code,      &hsc_ctx::w_hist,      &hsc_ctx::w_counts, &hsc_ctx::w_bucket,
+    &hsc_ctx::w_cursor,    &hsc_ctx::w_items,     &hsc_ctx::w_item_tile, &hsc_ctx::w_item_desc,
+    &hsc_ctx::w_recs,      &hsc_ctx::w_tcode,     &hsc_ctx::w_tcode2, &hsc_ctx::w_trecs,
+    &hsc_ctx::w_vflags,    &hsc_ctx::d_done,      &hsc_ctx::p_code_lo, &hsc_ctx::p_code_hi};
+static_assert(sizeof kLaneBufs / sizeof kLaneBufs[0] <= 16, "Lane::b size");
+
+// Make the lane of c->stream active (the least recently used lane if the
+// stream has none).
+static hipError_t select_lane(hsc_ctx *c)
+{
+    int want = -1;
+    for (int i = 0; i < hsc_ctx::kLanes; ++i)
+        if (c->lanes[i].stream == c->stream && c->lanes[i].tick) want = i;
+    if (want < 0) {
+        want = 0;
+        for (int i = 1; i < hsc_ctx::kLanes; ++i)
+            if (c->lanes[i].tick < c->lanes[want].tick) want = i;
+    }
+    if (want != c->lane) {
+        int k = 0;
+        for (DBuf hsc_ctx::*m : kLaneBufs) {
+            std::swap(c->*m, c->lanes[c->lane].b[k]);  // park the active lane's buffer
+            std::swap(c->*m, c->lanes[want].b[k]);     // take the wanted lane's
+            ++k;
+        }
+        c->lane = want;
+    }
+    hsc_ctx::Lane &L = c->lanes[want];
+    if (L.stream != c->stream) {
+        if (L.done && L.tick) {
+            hipError_t e = hipStreamWaitEvent(c->stream, L.done, 0);
+            if (e != hipSuccess) return e;
+        }
+        L.stream = c->stream;
+    }
+    L.tick = ++c->lane_tick;
+    return hipSuccess;
+}
+
+// After a batch: the lane's done event marks the end of its scratch use.
+static hipError_t lane_done(hsc_ctx *c)
+{
+    hsc_ctx::Lane &L = c->lanes[c->lane];
+    if (!L.done) {
+        hipError_t e = hipEventCreateWithFlags(&L.done, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+    }
+    return hipEventRecord(L.done, c->stream);
+}
+
+// Before the window changes: c->stream waits for every lane's last batch.
+static hipError_t wait_lanes(hsc_ctx *c)
+{
+    for (auto &L : c->lanes)
+        if (L.done && L.tick && L.stream != c->stream) {
+            hipError_t e = hipStreamWaitEvent(c->stream, L.done, 0);
+            if (e != hipSuccess) return e;
+        }
+    return hipSuccess;
+}
 
 static int fail(hsc_ctx *c, int code, const char *what, hipError_t e = hipSuccess)
 {
@@ -263,6 +342,7 @@ static int build_commits(hsc_ctx *c, size_t n_in)
 
 static int device_build(hsc_ctx *c, size_t n_in)
 {
+    HIPCHK(c, wait_lanes(c));
     hipStream_t s = c->stream;
     const int W = c->W;
     const size_t cap = c->cap;
@@ -923,9 +1003,18 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     return HSC_OK;
 }
 
+static int probe_lane(hsc_ctx *c, const hsc_probe_batch *b);
 static int probe(hsc_ctx *c, const hsc_probe_batch *b)
 {
     if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
+    HIPCHK(c, select_lane(c));
+    const int rc = probe_lane(c, b);
+    if (rc == HSC_OK) HIPCHK(c, lane_done(c));
+    return rc;
+}
+
+static int probe_lane(hsc_ctx *c, const hsc_probe_batch *b)
+{
     const WinView w = win_view(c);
     if (b->n > 0xFFFFFFFFull / 2 || b->n_lock > 0xFFFFFFFFull || b->n_txn > 0xFFFFFFFFull)
         return fail(c, HSC_EINVAL, "batch too large");
@@ -1151,6 +1240,8 @@ void hsc_ctx_destroy(hsc_ctx *c)
     }
     if (!c->host_only) (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    for (auto &L : c->lanes)
+        if (L.done) (void)hipEventSynchronize(L.done);
     DBuf *bufs[] = {&c->d_gid, &c->d_words, &c->d_lsn, &c->d_gid2, &c->d_words2, &c->d_lsn2,
                     &c->d_flags, &c->d_scratch, &c->d_gstart, &c->d_gend, &c->d_tmax,
                     &c->d_table_max, &c->d_group_table, &c->d_count, &c->d_sp_g, &c->d_sp_w,
@@ -1164,6 +1255,10 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->d_ctmp[0], &c->d_ctmp[1], &c->d_ctmp[2], &c->d_ctmp[3], &c->w_tcode,
                     &c->w_tcode2, &c->w_trecs};
     for (DBuf *b : bufs) b->release();
+    for (auto &L : c->lanes) {
+        for (DBuf &b : L.b) b.release();
+        if (L.done) (void)hipEventDestroy(L.done);
+    }
     c->graph.release_all();
     for (auto &e : c->ev)
         if (e) (void)hipEventDestroy(e);
