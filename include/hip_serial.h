@@ -194,7 +194,13 @@ enum {
  * marshalling work; every device operation returns HSC_EDEVICE. */
 int hsc_ctx_create(int device, hsc_ctx **out);
 void hsc_ctx_destroy(hsc_ctx *ctx);
-/* Launch on this hipStream_t (NULL = the context's own stream). */
+/* Launch on this hipStream_t (NULL = the context's own stream).  Probes are
+ * stream-ordered on the stream current at the call.  Each stream that probes
+ * gets its own probe lane (scratch buffers, up to 4 lanes; a fifth stream
+ * takes over the least recently used lane after waiting for that lane's last
+ * batch), so batches probed on different streams may run concurrently.
+ * Window builds wait for every lane's last batch; the caller orders a window
+ * change against later probes on other streams. */
 int hsc_set_stream(hsc_ctx *ctx, void *hip_stream);
 const char *hsc_last_error(hsc_ctx *ctx);
 int hsc_device_count(void);
