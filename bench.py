@@ -207,10 +207,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         world = max(world, 1)
+    if os.environ.get("HSC_BENCH_BACKEND", "nccl") != "nccl":
+        local = 0  # rehearsal: every rank on cuda:0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # HSC_BENCH_BACKEND=gloo rehearses the N > 1 path with every rank on one GPU
+        backend = os.environ.get("HSC_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     want_cpu = (rank == 0 and world == 1 and not args.no_cpu)
     value_bits = 40
