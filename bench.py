@@ -146,15 +146,15 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm):
     the undisturbed durations."""
     recs = tm["records"]
     tiles = tm["tiles"]
-    chunks = (n_r + 2047) // 2048
+    chunks = (n_r + 4095) // 4096
     hist = 4 * tiles * ((chunks + 7) // 8 * 8)
     if layout == 2:  # narrow tiles: 8-byte window rows, 16-byte records
         own = {
             "k_locate_t": n_r * (4 + 8 + 16 * W) + 16 * n_r + hist,
-            "k_plan_t": 2 * hist,
+            "k_plan_t": hist,
             "k_scatter_t": n_r * (16 + 4) + recs * 16,
             "k_join_t": 8 * n_keys + 16 * recs,
-            "k_pack": T + (T + 7) // 8,
+            "k_pack_flags": 2 * T + (T + 7) // 8,
         }
     else:  # wide tiles: key words + lsn + gid per row
         own = {
@@ -187,8 +187,13 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the batches rotate over (each with its own outputs and "
                          "probe lane), so consecutive batches' kernels can overlap")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 4),
-                    help="2: the headline check batch; 4: dependency graph + SCC of a history")
+    ap.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
+                    help="2: the headline check batch; 4: dependency graph + SCC of a history; "
+                         "5: Zipf hot keys over a large window (per-GPU imbalance reported)")
+    ap.add_argument("--c5-keys", type=int, default=125_000_000,
+                    help="config 5: window writes per GPU (125M x 8 GPUs = SURVEY's 1B)")
+    ap.add_argument("--check", action="store_true",
+                    help="config 5, N = 1: full-batch CPU sort-join parity (oracle/sortjoin.c)")
     ap.add_argument("--history-txns", type=int, default=4_000_000)
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per join launch (from a rocprofv3 --pmc run)")
@@ -219,36 +224,60 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    want_cpu = (rank == 0 and world == 1 and not args.no_cpu)
-    value_bits = 40
+    want_cpu = (rank == 0 and world == 1 and not args.no_cpu and args.config == 2)
     batches = []
     v = hsc.Validator(local)
     if args.wide:
         v.set_layout(hsc.LAYOUT_WIDE)
     gid_t = v.register_group("t1", 0, 9)
     assert gid_t == 0
-    c2 = config2(seed=SEED_CONFIG2, n_commits=args.n_commits, n_txn=args.n_txn, rank=rank,
-                 world=world, build_log=want_cpu)
-    gid, words, lsn = config2_device_window(c2)
+    if args.config == 2:
+        value_bits = 40
+        c2 = config2(seed=SEED_CONFIG2, n_commits=args.n_commits, n_txn=args.n_txn, rank=rank,
+                     world=world, build_log=want_cpu)
+        gid, words, lsn = config2_device_window(c2)
+        end_lsn = c2.params["end_lsn"]
+        first_rs = c2.readsets
+        more_rs = lambda bi: config2(seed=SEED_CONFIG2 + 7919 * bi, n_commits=args.n_commits,
+                                     n_txn=args.n_txn, rank=rank, world=world,
+                                     build_log=False).readsets
+        make_shards = lambda W: shard.KeyRangeShards.int64_uniform(world, value_bits, W)
+        workload = ("config2: per GPU 100k read sets x 10 ranges (1M ranges) vs a window of "
+                    "1M commits x 10 int64 index keys (10M logged keys), one index")
+        data = ("synthetic (BASELINE config 2 generator, seed 0xC0FFEE02; int64 keys in memcmp "
+                "order as big-endian u64 words)")
+    else:
+        from comdb2_amd.workloads import SEED_CONFIG5, config5_scaled
+        c5 = config5_scaled(seed=SEED_CONFIG5, keys_per_gpu=args.c5_keys, n_txn=args.n_txn,
+                            rank=rank, world=world)
+        gid, words, lsn, end_lsn = c5.gid, c5.words, c5.lsn, c5.end_lsn
+        first_rs = c5.readsets
+        more_rs = lambda bi: config5_scaled(seed=SEED_CONFIG5 + 7919 * bi,
+                                            keys_per_gpu=args.c5_keys, n_txn=args.n_txn,
+                                            rank=rank, world=world, window=False).readsets
+        span = (1 << c5.params["key_bits"]) // world
+        make_shards = lambda W: shard.KeyRangeShards.int64_spans(world, span, W)
+        workload = (f"config5: per GPU {args.c5_keys} Zipf(1.2) writes over its 2^32/N key span "
+                    f"(hot keys collapse under dedupe) and 100k read sets x 10 ranges (width "
+                    f"{c5.params['width']}, half the points on hot keys)")
+        data = "synthetic (config 5 generator, seed 0xC0FFEE05, weak scaling per GPU)"
     n_w = len(lsn)
     tg = torch.from_numpy(gid).to(dev)
     tw = torch.from_numpy(words.reshape(-1).view(np.int64)).to(dev)
     tl = torch.from_numpy(lsn.view(np.int64)).to(dev)
-    v.ingest_device(n_w, 2, tg.data_ptr(), tw.data_ptr(), tl.data_ptr(), c2.params["end_lsn"])
+    v.ingest_device(n_w, 2, tg.data_ptr(), tw.data_ptr(), tl.data_ptr(), end_lsn)
     ingest_ms = v.timing()["ingest_ms"]
     del tg, tw, tl
     W = v.words
-    shards = shard.KeyRangeShards.int64_uniform(world, value_bits, W)
+    shards = make_shards(W)
     if world > 1:  # lock probes see the table-wide max commit LSN
         v.merge_table_max(shard.allreduce_table_max(v.table_max()))
-    T = c2.readsets.ntxn
+    T = first_rs.ntxn
     m0 = None
     for bi in range(args.batches):
-        rs = c2.readsets if bi == 0 else config2(seed=SEED_CONFIG2 + 7919 * bi,
-                                                 n_commits=args.n_commits, n_txn=args.n_txn,
-                                                 rank=rank, world=world, build_log=False).readsets
+        rs = first_rs if bi == 0 else more_rs(bi)
         m = v.marshal(rs)
-        if bi == 0 and want_cpu:
+        if bi == 0 and (want_cpu or args.check):
             m0 = m
         if world > 1:
             m = shard.route(m, shards.range_mask(m, rank), shards.lock_mask(m, rank))
@@ -350,11 +379,9 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u64",
-        "data": "synthetic (BASELINE config 2 generator, seed 0xC0FFEE02; int64 keys in memcmp "
-                "order as big-endian u64 words)",
+        "data": data,
         "config": {
-            "workload": "config2: per GPU 100k read sets x 10 ranges (1M ranges) vs a window of "
-                        "1M commits x 10 int64 index keys (10M logged keys), one index",
+            "workload": workload,
             "read_sets_per_step": T,
             "ranges_per_gpu": n_r,
             "window_keys_per_gpu": n_keys,
@@ -388,6 +415,30 @@ def main():
         "cold_e2e_ms": ingest_ms + ms_step,
         "cpu_baseline": None,
     }
+    if args.config == 5:
+        out["roofline"]["traffic"] = None  # profiles/traffic.json is the config-2 run
+        # per-GPU imbalance: routed ranges and 1-stream probe time per rank
+        loc = np.array([n_r, tm["probe_total_ms"]], dtype=np.float64)
+        if world > 1:
+            g = torch.from_numpy(loc).to(dev)
+            allg = [torch.zeros_like(g) for _ in range(world)]
+            dist.all_gather(allg, g)
+            loc = torch.stack(allg).cpu().numpy()
+        else:
+            loc = loc[None, :]
+        out["imbalance"] = {"ranges_per_rank": loc[:, 0].tolist(),
+                            "probe_ms_per_rank": loc[:, 1].tolist(),
+                            "ranges_max_over_mean": float(loc[:, 0].max() / loc[:, 0].mean()),
+                            "time_max_over_mean": float(loc[:, 1].max() / loc[:, 1].mean())}
+        if args.check and world == 1:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle
+            sj = oracle.SortJoin(gid, words, lsn, 1)
+            want, secs = sj.probe(m0, np.array([lsn.max()], np.uint64), nthreads=args.cpu_threads)
+            sj.close()
+            out["parity"] = {"kind": "full batch 0 vs oracle/sortjoin.c (CPU sort-join)",
+                             "equal": bool(np.array_equal(want != 0, v0 != 0)),
+                             "cpu_s": secs}
     if want_cpu:
         out["cpu_baseline"] = cpu_baseline(c2, v0, args.cpu_threads, args.cpu_seconds,
                                            m0=m0)

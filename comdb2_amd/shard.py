@@ -66,6 +66,13 @@ class KeyRangeShards:
                                 key_words(F.enc_int64(((r + 1) << value_bits) - 1), W))
                                for r in range(world)])
 
+    @staticmethod
+    def int64_spans(world: int, span: int, W: int) -> "KeyRangeShards":
+        """Rank r owns int64 values [r * span, (r+1) * span)."""
+        return KeyRangeShards([(key_words(F.enc_int64(r * span), W),
+                                key_words(F.enc_int64((r + 1) * span - 1), W))
+                               for r in range(world)])
+
     def range_mask(self, m: dict, rank: int) -> np.ndarray:
         lo_b, hi_b = self.bounds[rank]
         return _leq(m["lo"], hi_b) & _geq(m["hi"], lo_b)

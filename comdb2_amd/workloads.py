@@ -512,6 +512,96 @@ def config3(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4, n_writes
     return log, ReadSets.from_lists(sets, snaps, tbnames=lb.tbnames)
 
 
+@dataclasses.dataclass
+class Config5Scaled:
+    gid: np.ndarray             # uint32[n] this rank's window rows (log order)
+    words: np.ndarray           # uint64[2][n] big-endian key words
+    lsn: np.ndarray             # uint64[n] commit LSN of each row
+    readsets: ReadSets          # global read sets (identical on every rank)
+    end_lsn: int
+    params: dict
+
+
+def config5_scaled(seed: int = SEED_CONFIG5, keys_per_gpu: int = 125_000_000,
+                   keys_per_commit: int = 10, n_txn: int = 100_000, ranges_per_txn: int = 10,
+                   zipf_s: float = 1.2, key_bits: int = 32, snap_recent: float = 0.01,
+                   rank: int = 0, world: int = 1, window: bool = True) -> Config5Scaled:
+    """Config 5 at scale without a log (a 1B-key window,
+    Zipf s = 1.2 over 2^key_bits keys, ranges as config 2 scaled): rank r holds
+    keys_per_gpu writes whose keys are Zipf samples hashed into its own span
+    [r, r+1) * 2^key_bits / world (weak scaling: every GPU has its own hot
+    keys, and hot keys collapse under dedupe), with config 2's commit/LSN
+    numbering (global commit g = c * world + r).  The read sets are global:
+    config 2's mix over the whole key space, range width scaled to the key
+    density (about 10 written keys per range), and half of the point ranges
+    aimed at hot keys of a uniformly chosen rank.  window=False skips the
+    window (another batch of read sets over the same window)."""
+    K = keys_per_commit
+    R = K + 3
+    span = (1 << key_bits) // world
+
+    def hot_keys(rng, r, n):
+        z = rng.zipf(zipf_s, size=n).astype(np.uint64)
+        h = (z * np.uint64(0x9E3779B1)) & np.uint64((1 << 32) - 1)
+        return (np.uint64(r * span) + h % np.uint64(span)).astype(np.int64)
+
+    n_commits = keys_per_gpu // K
+    n = n_commits * K if window else 0
+    vals = hot_keys(np.random.default_rng([seed, 5, rank]), rank, n)
+    b = F.enc_int64_array(vals)
+    pad = np.zeros((n, 16), dtype=np.uint8)
+    pad[:, :9] = b
+    words = pad.view(">u8").astype(np.uint64).reshape(n, 2).T.copy()
+    del pad, b
+    gcommit = np.arange(n // K, dtype=np.uint64) * np.uint64(world) + np.uint64(rank)
+    lsn = np.repeat(lsn_of_index(gcommit * np.uint64(R) + np.uint64(R - 1)), K)
+    end_lsn = int(lsn_of_index(np.array([world * n_commits * R]))[0])
+
+    rng = np.random.default_rng([seed, 1 << 20])
+    T = n_txn * world
+    nr = T * ranges_per_txn
+    width = max(1, int(round(10 * span / max(keys_per_gpu, 1))))
+    kind = rng.choice(4, size=nr, p=[0.5, 0.4, 0.08, 0.02])
+    v = rng.integers(0, world * span, size=nr, dtype=np.int64)
+    aim = np.nonzero((kind == 0) & (rng.random(nr) < 0.5))[0]
+    ar = rng.integers(0, world, size=len(aim))
+    for r in range(world):
+        sel = aim[ar == r]
+        v[sel] = hot_keys(rng, r, len(sel))
+    lo = F.enc_int64_array(v)
+    hi = F.enc_int64_array(np.where(kind == 1, v + width, v))
+    lkeylen = np.full(nr, 9, dtype=np.int32)
+    rkeylen = np.full(nr, 9, dtype=np.int32)
+    plen = rng.integers(6, 8, size=nr).astype(np.int32)
+    lkeylen[kind == 2] = plen[kind == 2]
+    rkeylen[kind == 2] = plen[kind == 2]
+    lflag = np.zeros(nr, dtype=np.int32)
+    rflag = np.zeros(nr, dtype=np.int32)
+    side = rng.random(nr) < 0.5
+    lflag[(kind == 3) & side] = 1
+    rflag[(kind == 3) & ~side] = 1
+    lkeylen[lflag == 1] = 0
+    rkeylen[rflag == 1] = 0
+    t_of = np.repeat(np.arange(T), ranges_per_txn)
+    order = np.lexsort((np.where(lflag == 1, -1, v), t_of))
+    lo, hi = lo[order], hi[order]
+    lkeylen, rkeylen, lflag, rflag = lkeylen[order], rkeylen[order], lflag[order], rflag[order]
+    keys = np.concatenate([lo.reshape(-1), hi.reshape(-1)])
+    ncg = world * n_commits
+    recent = max(1, int(round(ncg * snap_recent)))
+    gi = np.uint64(ncg - 1) - rng.integers(0, recent, size=T).astype(np.uint64)
+    snap = lsn_of_index(gi * np.uint64(R) + np.uint64(R - 1))
+    rs = ReadSets(txn_off=np.arange(0, nr + 1, ranges_per_txn, dtype=np.int64), snap=snap,
+                  table=np.zeros(nr, np.int32), idxnum=np.zeros(nr, np.int32), lflag=lflag,
+                  rflag=rflag, islocked=np.zeros(nr, np.int32), lkeylen=lkeylen,
+                  rkeylen=rkeylen, lkey_off=np.arange(nr, dtype=np.uint64) * np.uint64(9),
+                  rkey_off=np.uint64(nr * 9) + np.arange(nr, dtype=np.uint64) * np.uint64(9),
+                  keys=keys, tbnames=["t1"])
+    return Config5Scaled(np.zeros(n, dtype=np.uint32), words, lsn, rs, end_lsn,
+                         dict(seed=seed, keys_per_gpu=n, zipf_s=zipf_s, key_bits=key_bits,
+                              width=width, n_txn=n_txn, rank=rank, world=world))
+
+
 def config5(seed: int = SEED_CONFIG5, n_commits: int = 100_000, keys_per_commit: int = 10,
             n_txn: int = 10_000, zipf_s: float = 1.2, key_bits: int = 32, **kw) -> Config2:
     """Config 2's shape with Zipf(s) hot keys over 2^key_bits: a few keys take
