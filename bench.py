@@ -187,9 +187,12 @@ def main():
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the batches rotate over (each with its own outputs and "
                          "probe lane), so consecutive batches' kernels can overlap")
-    ap.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
-                    help="2: the headline check batch; 4: dependency graph + SCC of a history; "
+    ap.add_argument("--config", type=int, default=2, choices=(2, 3, 4, 5),
+                    help="2: the headline check batch; 3: composite keys over 32 (table, index) "
+                         "groups, group shards; 4: dependency graph + SCC of a history; "
                          "5: Zipf hot keys over a large window (per-GPU imbalance reported)")
+    ap.add_argument("--c3-writes", type=int, default=4_000_000,
+                    help="config 3: index writes per GPU (log-normal group sizes)")
     ap.add_argument("--c5-keys", type=int, default=125_000_000,
                     help="config 5: window writes per GPU (125M x 8 GPUs = SURVEY's 1B)")
     ap.add_argument("--check", action="store_true",
@@ -229,9 +232,31 @@ def main():
     v = hsc.Validator(local)
     if args.wide:
         v.set_layout(hsc.LAYOUT_WIDE)
-    gid_t = v.register_group("t1", 0, 9)
-    assert gid_t == 0
-    if args.config == 2:
+    if args.config != 3:
+        gid_t = v.register_group("t1", 0, 9)
+        assert gid_t == 0
+    c3 = None
+    if args.config == 3:
+        from comdb2_amd.workloads import SEED_CONFIG3, config3_arrays
+        c3 = config3_arrays(seed=SEED_CONFIG3, n_writes=args.c3_writes * world,
+                            n_txn=args.n_txn * world)
+        for g, (tbn, ix, L) in enumerate(c3.groups):
+            assert v.register_group(tbn, ix, L) == g
+        sizes = {g: int(n) for g, n in enumerate(np.bincount(c3.w_group, minlength=len(c3.groups)))}
+        gshards = shard.GroupShards(sizes, world)
+        mine = [g for g, r in gshards.owner.items() if r == rank]
+        gid, words, lsn = c3.window(mine)
+        end_lsn = c3.end_lsn
+        first_rs = c3.readsets
+        more_rs = lambda bi: config3_arrays(seed=SEED_CONFIG3, n_writes=args.c3_writes * world,
+                                            n_txn=args.n_txn * world, rs_seed=bi).readsets
+        make_shards = lambda W: gshards
+        workload = (f"config3: {len(c3.groups)} (table, index) groups of composite keys "
+                    f"(9-64 B, log-normal sizes), {args.c3_writes} index writes and "
+                    f"{args.n_txn} read sets per GPU (points, ranges, prefixes, table locks), "
+                    f"LPT group shards")
+        data = "synthetic (config 3 generator, seed 0xC0FFEE03, weak scaling per GPU)"
+    elif args.config == 2:
         value_bits = 40
         c2 = config2(seed=SEED_CONFIG2, n_commits=args.n_commits, n_txn=args.n_txn, rank=rank,
                      world=world, build_log=want_cpu)
@@ -265,9 +290,11 @@ def main():
     tg = torch.from_numpy(gid).to(dev)
     tw = torch.from_numpy(words.reshape(-1).view(np.int64)).to(dev)
     tl = torch.from_numpy(lsn.view(np.int64)).to(dev)
-    v.ingest_device(n_w, 2, tg.data_ptr(), tw.data_ptr(), tl.data_ptr(), end_lsn)
+    v.ingest_device(n_w, words.shape[0], tg.data_ptr(), tw.data_ptr(), tl.data_ptr(), end_lsn)
     ingest_ms = v.timing()["ingest_ms"]
     del tg, tw, tl
+    if c3 is not None:
+        v.merge_table_max(c3.table_max)  # data-row writes lock tables too
     W = v.words
     shards = make_shards(W)
     if world > 1:  # lock probes see the table-wide max commit LSN
@@ -415,6 +442,19 @@ def main():
         "cold_e2e_ms": ingest_ms + ms_step,
         "cpu_baseline": None,
     }
+    if args.config == 3:
+        out["roofline"]["traffic"] = None  # profiles/traffic.json is the config-2 run
+        out["config"]["parallelism"] = f"(table, index) group shards (LPT) x{world}" + (
+            " + RCCL max all-reduce" if world > 1 else "")
+        out["config"]["groups_per_rank"] = len(mine)
+        if args.check and world == 1:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle
+            sj = oracle.SortJoin(gid, words, lsn, len(c3.groups))
+            want, secs = sj.probe(m0, v.table_max(), nthreads=args.cpu_threads)
+            sj.close()
+            out["parity"] = {"kind": "full batch 0 vs oracle/sortjoin.c (CPU sort-join)",
+                             "equal": bool(np.array_equal(want != 0, v0 != 0)), "cpu_s": secs}
     if args.config == 5:
         out["roofline"]["traffic"] = None  # profiles/traffic.json is the config-2 run
         # per-GPU imbalance: routed ranges and 1-stream probe time per rank

@@ -95,8 +95,12 @@ class GroupShards:
         self.load = load
 
     def range_mask(self, m: dict, rank: int) -> np.ndarray:
-        own = np.array([self.owner.get(int(g), 0) == rank for g in m["gid"]], dtype=bool)
-        return own
+        lut = np.zeros(max(self.owner, default=0) + 1, dtype=np.int64)
+        for g, r in self.owner.items():
+            lut[g] = r
+        gid = np.asarray(m["gid"], dtype=np.int64)
+        owner = np.where(gid < len(lut), lut[np.minimum(gid, len(lut) - 1)], 0)
+        return owner == rank
 
     def lock_mask(self, m: dict, rank: int) -> np.ndarray:
         return np.full(m["n_lock"], rank == 0, dtype=bool)

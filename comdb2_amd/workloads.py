@@ -17,7 +17,7 @@ from typing import Callable, List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import formats as F
-from .formats import LLog, LogBuilder, Range, ReadSets
+from .formats import LLog, LogBuilder, Range, ReadSets, lsn
 
 SEED_CONFIG1 = 0xC0FFEE01
 SEED_CONFIG2 = 0xC0FFEE02
@@ -452,14 +452,49 @@ def _enc_fields(rng, shape, n, vmax):
     return np.concatenate(cols, axis=1)
 
 
-def config3(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4, n_writes: int = 200_000,
-            keys_per_commit: int = 8, n_txn: int = 20_000, ranges_per_txn: int = 10,
-            vmax: int = 1 << 12, snap_recent: float = 0.05, lock_frac: float = 0.01):
-    """Log of commits writing composite index keys (upd_ix) plus dta records
-    over n_tables x n_ix groups with log-normal group sizes, and read sets of
-    point / range / prefix ranges (and a few full-scan table locks) over 1-3
-    tables each (ranges sorted per table like coalesced arrays).  Returns
-    (LLog, ReadSets)."""
+@dataclasses.dataclass
+class Config3Arrays:
+    tbnames: List[str]
+    groups: List[Tuple[str, int, int]]  # group g = (table, index, key length)
+    keys_of: List[np.ndarray]           # uint8[gsize, L_g] per group
+    w_group: np.ndarray                 # int64[n_writes] group of each index write (log order)
+    w_row: np.ndarray                   # int64[n_writes] row in keys_of[group]
+    w_lsn: np.ndarray                   # uint64[n_writes] regop LSN of the write's commit
+    dta: List[Tuple[int, int]]          # (commit, table) of the data-row writes
+    commit_lsn: np.ndarray              # uint64[n_commits]
+    table_max: np.ndarray               # uint64[n_tables] max commit LSN of any write
+    end_lsn: int
+    readsets: ReadSets
+    keys_per_commit: int
+
+    def window(self, groups=None):
+        """Window rows (gid u32[n], words u64[W][n], lsn u64[n]) in log order
+        for the given group ids (all if None); gid = group index, W from the
+        longest key of any group."""
+        W = (max(L for _, _, L in self.groups) + 7) // 8
+        sel = np.ones(len(self.w_group), bool) if groups is None else np.isin(self.w_group, list(groups))
+        g, r, lsn = self.w_group[sel], self.w_row[sel], self.w_lsn[sel]
+        pad = np.zeros((len(g), 8 * W), dtype=np.uint8)
+        for gg in np.unique(g):
+            m = g == gg
+            kb = self.keys_of[gg][r[m]]
+            pad[m, :kb.shape[1]] = kb
+        words = pad.view(">u8").astype(np.uint64).reshape(len(g), W).T.copy()
+        return g.astype(np.uint32), words, lsn.copy()
+
+
+def config3_arrays(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4,
+                   n_writes: int = 200_000, keys_per_commit: int = 8, n_txn: int = 20_000,
+                   ranges_per_txn: int = 10, vmax: int = 1 << 12, snap_recent: float = 0.05,
+                   lock_frac: float = 0.01, rs_seed: Optional[int] = None) -> Config3Arrays:
+    """Config 3 as arrays (no log): n_tables x n_ix composite-key groups with
+    log-normal sizes, commits of keys_per_commit index writes (30% also write
+    a data row of a random table), LSNs exactly as LogBuilder assigns them
+    (ltran_start, writes, [dta], ltran_commit, regop; 64 bytes apart), and
+    read sets of point / range / prefix ranges (and a few table locks) over
+    1-3 tables each.  config3() builds the same workload as a log.  rs_seed
+    draws the read sets from their own generator (another batch over the same
+    window)."""
     rng = np.random.default_rng(seed)
     tb = [f"t{i}" for i in range(n_tables)]
     G = n_tables * n_ix
@@ -468,24 +503,35 @@ def config3(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4, n_writes
     keys_of = []
     for g in range(G):
         keys_of.append(_enc_fields(rng, INDEX_SHAPES[g % n_ix], int(gsize[g]), vmax))
-    # interleave writes of all groups into commits
     gid = np.concatenate([np.full(int(gsize[g]), g) for g in range(G)])
     row = np.concatenate([np.arange(int(gsize[g])) for g in range(G)])
     perm = rng.permutation(len(gid))
     gid, row = gid[perm], row[perm]
-    lb = LogBuilder(tb)
-    commits = [lb.next_lsn()]
-    c = 0
-    for i in range(0, len(gid), keys_per_commit):
-        lb.begin(c)
-        for g, r in zip(gid[i:i + keys_per_commit], row[i:i + keys_per_commit]):
-            lb.write(c, F.REC_UNDO_UPD_IX, tb[g // n_ix], int(g % n_ix), bytes(keys_of[g][r]))
-        if rng.random() < 0.3:
-            lb.write(c, F.REC_UNDO_UPD_DTA, tb[int(rng.integers(0, n_tables))])
-        commits.append(lb.commit(c))
-        c += 1
-    log = lb.build()
+    K = keys_per_commit
+    n_commits = (len(gid) + K - 1) // K
+    dta = []
+    nrec = np.zeros(n_commits, dtype=np.int64)
+    for c in range(n_commits):
+        k = min(K, len(gid) - c * K)
+        has = rng.random() < 0.3
+        if has:
+            dta.append((c, int(rng.integers(0, n_tables))))
+        nrec[c] = 1 + k + (1 if has else 0) + 2
+    # record index of each commit's regop (LogBuilder: file 1, offset 28 + 64 i)
+    regop_idx = np.cumsum(nrec) - 1
+    assert 28 + 64 * int(nrec.sum()) < (1 << 32) - 64, "one log file"
+    commit_lsn = (np.uint64(1) << np.uint64(32)) | (np.uint64(28) + np.uint64(64) * regop_idx.astype(np.uint64))
+    start_lsn = int(lsn(1, 28))
+    end_lsn = int(lsn(1, 28 + 64 * int(nrec.sum())))
+    w_lsn = np.repeat(commit_lsn, K)[:len(gid)]
+    table_max = np.zeros(n_tables, dtype=np.uint64)
+    np.maximum.at(table_max, gid // n_ix, w_lsn)
+    for c, t in dta:
+        table_max[t] = max(table_max[t], commit_lsn[c])
+    commits = [start_lsn] + [int(x) for x in commit_lsn]
     recent = max(1, int(len(commits) * snap_recent))
+    if rs_seed is not None:
+        rng = np.random.default_rng([seed, rs_seed])
     sets, snaps = [], []
     for t in range(n_txn):
         rs = []
@@ -509,7 +555,34 @@ def config3(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4, n_writes
         rs.sort(key=lambda r: (r.tbname, -r.islocked, r.idxnum, r.lkey or b""))
         sets.append(rs)
         snaps.append(commits[len(commits) - 1 - int(rng.integers(0, recent))])
-    return log, ReadSets.from_lists(sets, snaps, tbnames=lb.tbnames)
+    groups = [(tb[g // n_ix], g % n_ix, int(keys_of[g].shape[1])) for g in range(G)]
+    return Config3Arrays(tb, groups, keys_of, gid, row, w_lsn, dta, commit_lsn, table_max,
+                         end_lsn, ReadSets.from_lists(sets, snaps, tbnames=tb), K)
+
+
+def config3(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4, n_writes: int = 200_000,
+            keys_per_commit: int = 8, n_txn: int = 20_000, ranges_per_txn: int = 10,
+            vmax: int = 1 << 12, snap_recent: float = 0.05, lock_frac: float = 0.01):
+    """Log of commits writing composite index keys (upd_ix) plus dta records
+    over n_tables x n_ix groups with log-normal group sizes, and read sets of
+    point / range / prefix ranges (and a few full-scan table locks) over 1-3
+    tables each (ranges sorted per table like coalesced arrays).  Returns
+    (LLog, ReadSets); config3_arrays() is the same workload as arrays."""
+    a = config3_arrays(seed, n_tables, n_ix, n_writes, keys_per_commit, n_txn, ranges_per_txn,
+                       vmax, snap_recent, lock_frac)
+    n_ix_ = n_ix
+    lb = LogBuilder(a.tbnames)
+    dta = dict(a.dta)
+    K = a.keys_per_commit
+    for c in range(len(a.commit_lsn)):
+        lb.begin(c)
+        for g, r in zip(a.w_group[c * K:(c + 1) * K], a.w_row[c * K:(c + 1) * K]):
+            lb.write(c, F.REC_UNDO_UPD_IX, a.tbnames[g // n_ix_], int(g % n_ix_), bytes(a.keys_of[g][r]))
+        if c in dta:
+            lb.write(c, F.REC_UNDO_UPD_DTA, a.tbnames[dta[c]])
+        l = lb.commit(c)
+        assert l == int(a.commit_lsn[c])
+    return lb.build(), a.readsets
 
 
 @dataclasses.dataclass
