@@ -733,12 +733,14 @@ __global__ __launch_bounds__(kLocTThreads) void k_locate_t(NarrowView nv, WinVie
         qq[j] = c0 + threadIdx.x + kLocTThreads * j;
         valid[j] = qq[j] < c1;
         const uint32_t q = valid[j] ? qq[j] : 0;
-        gg[j] = p.n ? p.gid[q] : 0;
-        snap[j] = p.n ? p.snap[q] : 0;
+        // read-once inputs: non-temporal, so they do not push the window's
+        // rows out of the caches between batches
+        gg[j] = p.n ? __builtin_nontemporal_load(p.gid + q) : 0;
+        snap[j] = p.n ? __builtin_nontemporal_load(p.snap + q) : 0;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-            xl[j][w] = p.n ? p.lo[(size_t)w * p.n + q] : 0;
-            xh[j][w] = p.n ? p.hi[(size_t)w * p.n + q] : 0;
+            xl[j][w] = p.n ? __builtin_nontemporal_load(p.lo + (size_t)w * p.n + q) : 0;
+            xh[j][w] = p.n ? __builtin_nontemporal_load(p.hi + (size_t)w * p.n + q) : 0;
         }
     }
     int tshift = 0;
