@@ -79,6 +79,16 @@ def main(tag):
                 continue
             vals = [sq.get((k, c), [0]) for c in sorted({c for _, c in sq})]
             lines.append(f"| {k} | " + " | ".join(f"{sum(v) / len(v):.3g}" for v in vals) + " |")
+    # wall time per batch over the densest run of probe dispatches (batches
+    # on several streams overlap, so per-kernel averages above are inflated
+    # and do not add up to the time per batch)
+    trace = os.path.join(out, f"prof_{tag}_kt", "run_kernel_trace.csv")
+    if os.path.exists(trace):
+        import subprocess
+        ov = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "overlap.py"),
+                             f"prof_{tag}_kt"], capture_output=True, text=True).stdout
+        lines += ["", "Probe-phase overlap (scripts/overlap.py over the kernel trace):", "",
+                  "```", ov.rstrip(), "```"]
     open(os.path.join(prof, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
     if traffic["kernels"]:
         json.dump(traffic, open(os.path.join(prof, "traffic.json"), "w"), indent=1)
