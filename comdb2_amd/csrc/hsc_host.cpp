@@ -112,6 +112,12 @@ struct hsc_ctx {
     DecodedLog decoded;
     DecodedReadSets wire;
 
+    // replicant coalesce: device inputs / working arrays, host outputs
+    DBuf co_dev[18];
+    std::vector<int64_t> co_off;
+    std::vector<int32_t> co_i32[7];
+    std::vector<uint64_t> co_u64[2];
+
     // dependency graph
     GraphBufs graph;
     uint32_t graph_ntxn = 0;
@@ -1255,6 +1261,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->d_ctmp[0], &c->d_ctmp[1], &c->d_ctmp[2], &c->d_ctmp[3], &c->w_tcode,
                     &c->w_tcode2, &c->w_trecs};
     for (DBuf *b : bufs) b->release();
+    for (DBuf &b : c->co_dev) b.release();
     for (auto &L : c->lanes) {
         for (DBuf &b : L.b) b.release();
         if (L.done) (void)hipEventDestroy(L.done);
@@ -1492,6 +1499,104 @@ int hsc_marshal_readsets(hsc_ctx *c, const hsc_readsets *rs, const hsc_marshalle
     rc = marshal_readsets(c, rs);
     *out = &c->m;
     return rc;
+}
+
+int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out)
+{
+    if (!c || !rs || !out || rs->ntxn < 0) return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    const int T = rs->ntxn;
+    const size_t nr = T ? (size_t)rs->txn_off[T] : 0;
+    // strcmp rank of every table name (equal names share a rank)
+    std::vector<int32_t> rank(std::max(rs->ntbnames, 1), 0);
+    {
+        std::vector<int> order(rs->ntbnames);
+        for (int i = 0; i < rs->ntbnames; ++i) order[i] = i;
+        std::sort(order.begin(), order.end(),
+                  [&](int a, int b) { return strcmp(rs->tbnames[a], rs->tbnames[b]) < 0; });
+        for (int k = 0; k < rs->ntbnames; ++k)
+            rank[order[k]] = k && strcmp(rs->tbnames[order[k]], rs->tbnames[order[k - 1]]) == 0
+                                 ? rank[order[k - 1]]
+                                 : k;
+    }
+    for (size_t r = 0; r < nr; ++r)
+        if (rs->table[r] < 0 || rs->table[r] >= rs->ntbnames)
+            return fail(c, HSC_EINVAL, "coalesce: a range names no table");
+    uint64_t nkeys = 0;
+    for (size_t r = 0; r < nr; ++r) {
+        if (rs->lkeylen[r] > 0) nkeys = std::max<uint64_t>(nkeys, rs->lkey_off[r] + rs->lkeylen[r]);
+        if (rs->rkeylen[r] > 0) nkeys = std::max<uint64_t>(nkeys, rs->rkey_off[r] + rs->rkeylen[r]);
+    }
+    hipStream_t s = c->stream;
+    DBuf *d = c->co_dev;
+    const size_t n1 = std::max<size_t>(nr, 1);
+    const size_t sz[18] = {8 * ((size_t)T + 1), 4 * n1, 4 * n1, 4 * n1, 4 * n1, 4 * n1, 4 * n1,
+                           4 * n1, 8 * n1, 8 * n1, std::max<uint64_t>(nkeys, 1), 4 * rank.size(),
+                           4 * n1, 4 * n1, 4 * n1, 8 * n1, 8 * n1 /* ord + tmp */,
+                           4 * (size_t)std::max(T, 1)};
+    for (int k = 0; k < 18; ++k) HIPCHK(c, d[k].ensure(sz[k]));
+    const void *src[12] = {rs->txn_off, rs->table, rs->idxnum, rs->lflag, rs->rflag, rs->islocked,
+                           rs->lkeylen, rs->rkeylen, rs->lkey_off, rs->rkey_off, rs->keys,
+                           rank.data()};
+    const size_t bytes[12] = {8 * ((size_t)T + 1), 4 * nr, 4 * nr, 4 * nr, 4 * nr, 4 * nr, 4 * nr,
+                              4 * nr, 8 * nr, 8 * nr, nkeys, 4 * rank.size()};
+    for (int k = 0; k < 12; ++k)
+        if (bytes[k]) HIPCHK(c, hipMemcpyAsync(d[k].p, src[k], bytes[k], hipMemcpyHostToDevice, s));
+    CoView v{};
+    v.ntxn = T;
+    v.off = d[0].as<int64_t>();
+    v.table = d[1].as<int32_t>(), v.idxnum = d[2].as<int32_t>(), v.lflag = d[3].as<int32_t>();
+    v.rflag = d[4].as<int32_t>(), v.islocked = d[5].as<int32_t>(), v.lkeylen = d[6].as<int32_t>();
+    v.rkeylen = d[7].as<int32_t>();
+    v.lkey_off = d[8].as<uint64_t>(), v.rkey_off = d[9].as<uint64_t>();
+    v.keys = d[10].as<uint8_t>(), v.nkeys = nkeys, v.tbrank = d[11].as<int32_t>();
+    v.w_rflag = d[12].as<int32_t>(), v.w_islocked = d[13].as<int32_t>();
+    v.w_rkeylen = d[14].as<int32_t>(), v.w_rkey_off = d[15].as<uint64_t>();
+    v.ord = d[16].as<uint32_t>(), v.tmp = d[16].as<uint32_t>() + n1;
+    v.count = d[17].as<uint32_t>();
+    HIPCHK(c, launch_coalesce(v, s));
+    std::vector<uint32_t> cnt(T), ord(nr);
+    std::vector<int32_t> wrf(nr), wlk(nr), wrl(nr);
+    std::vector<uint64_t> wro(nr);
+    if (T) HIPCHK(c, hipMemcpyAsync(cnt.data(), v.count, 4 * (size_t)T, hipMemcpyDeviceToHost, s));
+    if (nr) {
+        HIPCHK(c, hipMemcpyAsync(ord.data(), v.ord, 4 * nr, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(wrf.data(), v.w_rflag, 4 * nr, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(wlk.data(), v.w_islocked, 4 * nr, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(wrl.data(), v.w_rkeylen, 4 * nr, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(wro.data(), v.w_rkey_off, 8 * nr, hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(c, hipStreamSynchronize(s));
+    // compact the surviving rows of every set, in coalesced order
+    c->co_off.assign((size_t)T + 1, 0);
+    for (auto &a : c->co_i32) a.clear();
+    for (auto &a : c->co_u64) a.clear();
+    for (int t = 0; t < T; ++t) {
+        const size_t b = (size_t)rs->txn_off[t];
+        for (uint32_t k = 0; k < cnt[t]; ++k) {
+            const uint32_t r = ord[b + k];
+            c->co_i32[0].push_back(rs->table[r]);
+            c->co_i32[1].push_back(rs->idxnum[r]);
+            c->co_i32[2].push_back(rs->lflag[r]);
+            c->co_i32[3].push_back(wrf[r]);
+            c->co_i32[4].push_back(wlk[r]);
+            c->co_i32[5].push_back(rs->lkeylen[r]);
+            c->co_i32[6].push_back(wrl[r]);
+            c->co_u64[0].push_back(rs->lkey_off[r]);
+            c->co_u64[1].push_back(wro[r]);
+        }
+        c->co_off[t + 1] = c->co_off[t] + cnt[t];
+    }
+    out->ntxn = T;
+    out->txn_off = c->co_off.data();
+    out->table = c->co_i32[0].data(), out->idxnum = c->co_i32[1].data();
+    out->lflag = c->co_i32[2].data(), out->rflag = c->co_i32[3].data();
+    out->islocked = c->co_i32[4].data(), out->lkeylen = c->co_i32[5].data();
+    out->rkeylen = c->co_i32[6].data();
+    out->lkey_off = c->co_u64[0].data(), out->rkey_off = c->co_u64[1].data();
+    return HSC_OK;
 }
 
 int hsc_check_readsets(hsc_ctx *c, const hsc_readsets *rs, int *rc_out)

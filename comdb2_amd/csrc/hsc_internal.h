@@ -219,6 +219,23 @@ uint32_t narrow_trad_buckets(uint32_t ntiles);
 hipError_t narrow_trad_build(const uint64_t *first, uint32_t ntiles, uint32_t m, uint32_t *trad,
                              hipStream_t s);
 uint32_t narrow_tiles_dir_lds();
+// Replicant coalesce (hsc_coalesce.hip): flat read sets in, per-set surviving
+// rows (ord) + the four fields merge_neighbor rewrites (w_*) out.
+struct CoView {
+    int ntxn;
+    const int64_t *off;                        // [ntxn + 1]
+    const int32_t *table, *idxnum, *lflag, *rflag, *islocked, *lkeylen, *rkeylen;
+    const uint64_t *lkey_off, *rkey_off;
+    const uint8_t *keys;
+    uint64_t nkeys;
+    const int32_t *tbrank;                     // strcmp rank of each table name
+    int32_t *w_rflag, *w_islocked, *w_rkeylen;  // [nranges] working copies
+    uint64_t *w_rkey_off;
+    uint32_t *ord, *tmp;                       // [nranges] coalesced order per set
+    uint32_t *count;                           // [ntxn] ranges left per set
+};
+hipError_t launch_coalesce(const CoView &v, hipStream_t s);
+
 // Narrow tiles keep the chunk histogram tile-major: hist[t * hist_stride(G) + g].
 __host__ __device__ inline uint32_t hist_stride(uint32_t G) { return (G + 7) & ~7u; }
 // XCD-contiguous chunk order: block b of a grid of 8 * per blocks runs on XCD

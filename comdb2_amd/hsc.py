@@ -122,7 +122,7 @@ EXPORTS = [
     "hsc_get_timing",
     "hsc_enable_timing", "hsc_dep_graph_scc", "hsc_dep_graph_edges",
     "hsc_window_ingest_raw", "hsc_decode_log", "hsc_decode_serial", "hsc_check_serial",
-    "hsc_set_layout", "hsc_window_layout",
+    "hsc_set_layout", "hsc_window_layout", "hsc_coalesce_readsets",
 ]
 
 (LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES,
@@ -254,6 +254,12 @@ def readsets_struct(rs: ReadSets):
              "rkeylen", "lkey_off", "rkey_off", "keys")
     s = _ReadSets(rs.ntxn, *[_ptr(cols[k]) for k in order], names, len(rs.tbnames))
     return s, (cols, names)
+
+
+class _Coalesced(C.Structure):
+    _fields_ = [("ntxn", C.c_int), ("txn_off", _p), ("table", _p), ("idxnum", _p),
+                ("lflag", _p), ("rflag", _p), ("islocked", _p), ("lkeylen", _p),
+                ("rkeylen", _p), ("lkey_off", _p), ("rkey_off", _p)]
 
 
 class CurRangeArrays:
@@ -443,6 +449,30 @@ class Validator:
                                              out.ctypes.data_as(C.POINTER(C.c_int)))
         self._chk(rc, "hip_serial_check_batch")
         return out[:n]
+
+    def coalesce(self, rs: ReadSets) -> ReadSets:
+        """currangearr_coalesce (db/sqlglue.c:305-311) of every read set on the
+        device; the result keeps rs.keys (its key offsets point into it)."""
+        import dataclasses
+        s, keep = readsets_struct(rs)
+        out = _Coalesced()
+        self._chk(self.lib.hsc_coalesce_readsets(self.ctx, C.byref(s), C.byref(out)),
+                  "hsc_coalesce_readsets")
+        T = out.ntxn
+        off = np.ctypeslib.as_array(C.cast(out.txn_off, C.POINTER(C.c_int64)), shape=(T + 1,)).copy()
+        n = int(off[-1])
+
+        def arr(p, ct, dt):
+            if n == 0:
+                return np.zeros(0, dtype=dt)
+            return np.ctypeslib.as_array(C.cast(p, C.POINTER(ct)), shape=(n,)).astype(dt, copy=True)
+
+        i32 = lambda p: arr(p, C.c_int32, np.int32)
+        return dataclasses.replace(
+            rs, txn_off=off, table=i32(out.table), idxnum=i32(out.idxnum), lflag=i32(out.lflag),
+            rflag=i32(out.rflag), islocked=i32(out.islocked), lkeylen=i32(out.lkeylen),
+            rkeylen=i32(out.rkeylen), lkey_off=arr(out.lkey_off, C.c_uint64, np.uint64),
+            rkey_off=arr(out.rkey_off, C.c_uint64, np.uint64))
 
     def marshal(self, rs: ReadSets) -> dict:
         """Marshal read sets into probe SoA (numpy copies)."""

@@ -309,6 +309,22 @@ int hip_serial_check_batch(void *ctx, void *const *ranges, unsigned int *file,
                            unsigned int *offset, int regop_only, int n,
                            int *rc_out);
 /* Flat read sets (snapshots in rs->snap); rc_out[ntxn]; full checks only. */
+/* Replicant read-set coalesce on the device: currangearr_coalesce
+ * (db/sqlglue.c:305-311) -- qsort by currange_cmp (:206-242, glibc's
+ * top-down merge sort), currangearr_merge_neighbor (:247-304), twice -- of
+ * every read set, with the reference's quirks (a right-key swap keeps the
+ * surviving range's rkeylen; a range open at both ends becomes a table lock
+ * that absorbs its table's other ranges).  Output arrays are owned by the
+ * context until its next coalesce; key offsets point into rs->keys.  Every
+ * range must name a table (the reference's strcmp would crash otherwise). */
+typedef struct hsc_coalesced {
+    int ntxn;
+    const int64_t *txn_off;   /* [ntxn+1] */
+    const int32_t *table, *idxnum, *lflag, *rflag, *islocked, *lkeylen, *rkeylen;
+    const uint64_t *lkey_off, *rkey_off;
+} hsc_coalesced;
+int hsc_coalesce_readsets(hsc_ctx *ctx, const hsc_readsets *rs, hsc_coalesced *out);
+
 int hsc_check_readsets(hsc_ctx *ctx, const hsc_readsets *rs, int *rc_out);
 
 /* ---- marshalling + device probe (what the checks lower to) -------------- */

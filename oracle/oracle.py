@@ -67,6 +67,9 @@ def load():
         lib.sj_rows.argtypes = [_p]
         lib.sj_probe.restype = C.c_double
         lib.sj_probe.argtypes = [_p, C.POINTER(_SjProbes), C.c_int, _p]
+        lib.co_coalesce.restype = C.c_long
+        lib.co_coalesce.argtypes = [C.c_int] + [_p] * 10 + [_p, C.c_uint64, C.POINTER(C.c_char_p),
+                                                            C.c_int] + [_p] * 10
         lib.or_serial_check.restype = C.c_int
         lib.or_serial_check.argtypes = [C.POINTER(_OrLog), _p, C.POINTER(C.c_uint),
                                         C.POINTER(C.c_uint), C.c_int]
@@ -193,3 +196,28 @@ class SortJoin:
             self.close()
         except Exception:
             pass
+
+
+def coalesce(rs: ReadSets) -> ReadSets:
+    """currangearr_coalesce (db/sqlglue.c:305-311) of every read set
+    (oracle/coalesce_oracle.c).  The result keeps rs.keys; its key offsets
+    point into it."""
+    import dataclasses
+    lib = load()
+    nr = len(rs.table)
+    i32 = lambda a: np.ascontiguousarray(a, np.int32)
+    ins = [np.ascontiguousarray(rs.txn_off, np.int64), i32(rs.table), i32(rs.idxnum), i32(rs.lflag),
+           i32(rs.rflag), i32(rs.islocked), i32(rs.lkeylen), i32(rs.rkeylen),
+           np.ascontiguousarray(rs.lkey_off, np.uint64), np.ascontiguousarray(rs.rkey_off, np.uint64)]
+    keys = np.ascontiguousarray(rs.keys, np.uint8)
+    names = (C.c_char_p * max(1, len(rs.tbnames)))(*[n.encode() for n in rs.tbnames])
+    out_off = np.zeros(rs.ntxn + 1, np.int64)
+    outs = [np.zeros(nr, np.int32) for _ in range(7)] + [np.zeros(nr, np.uint64) for _ in range(2)]
+    tot = lib.co_coalesce(rs.ntxn, *[a.ctypes.data for a in ins], keys.ctypes.data, len(keys),
+                          names, len(rs.tbnames), out_off.ctypes.data, *[a.ctypes.data for a in outs])
+    if tot < 0:
+        raise ValueError("co_coalesce: a range names no table")
+    o = [a[:tot].copy() for a in outs]
+    return dataclasses.replace(rs, txn_off=out_off, table=o[0], idxnum=o[1], lflag=o[2], rflag=o[3],
+                               islocked=o[4], lkeylen=o[5], rkeylen=o[6], lkey_off=o[7],
+                               rkey_off=o[8])
