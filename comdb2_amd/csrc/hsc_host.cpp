@@ -112,6 +112,12 @@ struct hsc_ctx {
     DecodedLog decoded;
     DecodedReadSets wire;
 
+    // rw conflict pairs: every window version (pre-dedupe rows in d_*2)
+    size_t n_all = 0;
+    DBuf e_span, e_cnt, e_txn, e_lsn, e_txn2, e_lsn2, e_gid, e_scratch, e_flags, e_after;
+    std::vector<uint32_t> e_out_txn;
+    std::vector<uint64_t> e_out_lsn;
+
     // replicant coalesce: device inputs / working arrays, host outputs
     DBuf co_dev[18];
     std::vector<int64_t> co_off;
@@ -389,6 +395,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, hipMemcpyAsync(&nu, c->d_count.p, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     c->n = n_in ? nu : 0;
+    c->n_all = n_in;  // every version, key-sorted, stays in d_gid2 / d_words2 / d_lsn2
     // narrow layout if the whole window fits 62-bit codes (hsc_narrow.hip)
     c->narrow = false;
     c->lw = W;
@@ -1262,6 +1269,9 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->w_tcode2, &c->w_trecs};
     for (DBuf *b : bufs) b->release();
     for (DBuf &b : c->co_dev) b.release();
+    for (DBuf *b : {&c->e_span, &c->e_cnt, &c->e_txn, &c->e_lsn, &c->e_txn2, &c->e_lsn2, &c->e_gid,
+                    &c->e_scratch, &c->e_flags, &c->e_after})
+        b->release();
     for (auto &L : c->lanes) {
         for (DBuf &b : L.b) b.release();
         if (L.done) (void)hipEventDestroy(L.done);
@@ -1499,6 +1509,120 @@ int hsc_marshal_readsets(hsc_ctx *c, const hsc_readsets *rs, const hsc_marshalle
     rc = marshal_readsets(c, rs);
     *out = &c->m;
     return rc;
+}
+
+int hsc_rw_edges(hsc_ctx *c, const hsc_readsets *rs, size_t *n_pairs, const uint32_t **txn,
+                 const uint64_t **writer_lsn)
+{
+    if (!c || !rs || !n_pairs || !txn || !writer_lsn) return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    int rc = ensure_built(c);
+    if (!rc) rc = marshal_readsets(c, rs);
+    if (rc) return rc;
+    hipStream_t s = c->stream;
+    const hsc_marshalled &m = c->m;
+    const int W = c->W;
+    const size_t n = m.n;
+    c->e_out_txn.clear();
+    c->e_out_lsn.clear();
+    *n_pairs = 0;
+    *txn = nullptr;
+    *writer_lsn = nullptr;
+    if (n == 0 || c->n_all == 0) return HSC_OK;
+    HIPCHK(c, c->p_lo.ensure(8 * (size_t)W * n));
+    HIPCHK(c, c->p_hi.ensure(8 * (size_t)W * n));
+    HIPCHK(c, c->p_gid.ensure(4 * n));
+    HIPCHK(c, c->p_snap.ensure(8 * n));
+    HIPCHK(c, c->p_txn.ensure(4 * n));
+    HIPCHK(c, hipMemcpyAsync(c->p_lo.p, m.lo, 8 * (size_t)W * n, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->p_hi.p, m.hi, 8 * (size_t)W * n, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->p_gid.p, m.gid, 4 * n, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->p_snap.p, m.snap, 8 * n, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->p_txn.p, m.txn, 4 * n, hipMemcpyHostToDevice, s));
+    ProbeView p{};
+    p.n = (uint32_t)n;
+    p.lo = c->p_lo.as<uint64_t>();
+    p.hi = c->p_hi.as<uint64_t>();
+    p.gid = c->p_gid.as<uint32_t>();
+    p.snap = c->p_snap.as<uint64_t>();
+    p.txn = c->p_txn.as<uint32_t>();
+    EdgeView all{};
+    all.gid = c->d_gid2.as<uint32_t>();
+    all.words = c->d_words2.as<uint64_t>();
+    all.lsn = c->d_lsn2.as<uint64_t>();
+    all.stride = c->cap;
+    all.n = (uint32_t)c->n_all;
+    all.W = W;
+    // only versions committed after the oldest snapshot of the batch can pair
+    uint64_t smin = ~0ull;
+    for (size_t q = 0; q < n; ++q) smin = std::min<uint64_t>(smin, m.snap[q]);
+    const size_t na = c->n_all;
+    HIPCHK(c, c->e_flags.ensure(4 * (na + 1) + 64));
+    HIPCHK(c, c->e_scratch.ensure(scan_scratch_bytes(na + 1) + 64));
+    HIPCHK(c, c->e_after.ensure((4 + 8 + 8 * (size_t)W) * std::max<size_t>(na, 1)));
+    EdgeView w{};
+    w.stride = std::max<size_t>(na, 1);
+    w.gid = c->e_after.as<uint32_t>();
+    w.lsn = (const uint64_t *)(c->e_after.as<uint8_t>() + 4 * w.stride + 4 * (w.stride & 1));
+    w.words = w.lsn + w.stride;
+    w.W = W;
+    uint32_t nafter = 0;
+    HIPCHK(c, edge_after(all, smin, c->e_flags.as<uint32_t>(), c->e_scratch.as<uint32_t>(), w,
+                         &nafter, s));
+    w.n = nafter;
+    if (nafter == 0) return HSC_OK;
+    HIPCHK(c, c->e_span.ensure(8 * n));
+    HIPCHK(c, c->e_cnt.ensure(4 * (n + 1)));
+    HIPCHK(c, c->e_scratch.ensure(scan_scratch_bytes(n + 1) + 64));
+    HIPCHK(c, launch_edge_count(w, p, c->e_span.as<uint2>(), c->e_cnt.as<uint32_t>(), s));
+    HIPCHK(c, hipMemsetAsync(c->e_cnt.as<uint32_t>() + n, 0, 4, s));
+    HIPCHK(c, scan_exclusive_u32(c->e_cnt.as<uint32_t>(), n + 1, c->e_scratch.as<uint32_t>(), s));
+    uint32_t total = 0;
+    HIPCHK(c, hipMemcpyAsync(&total, c->e_cnt.as<uint32_t>() + n, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (total == 0) return HSC_OK;
+    // pairs as rows (gid = txn, one word = commit LSN) for the window's sort + dedupe
+    const size_t t1 = total;
+    HIPCHK(c, c->e_txn.ensure(4 * t1));
+    HIPCHK(c, c->e_lsn.ensure(8 * t1));
+    HIPCHK(c, c->e_txn2.ensure(4 * t1));
+    HIPCHK(c, c->e_lsn2.ensure(8 * t1));
+    HIPCHK(c, c->e_gid.ensure(16 * t1));  // carried LSN (two buffers)
+    HIPCHK(c, c->e_flags.ensure(4 * t1 + 64));
+    HIPCHK(c, c->e_scratch.ensure(std::max(radix_scratch_bytes(t1, 1), scan_scratch_bytes(t1) + 64)));
+    HIPCHK(c, launch_edge_emit(w, p, c->e_span.as<uint2>(), c->e_cnt.as<uint32_t>(),
+                               c->e_txn.as<uint32_t>(), c->e_lsn.as<uint64_t>(), s));
+    uint64_t *carry = c->e_gid.as<uint64_t>(), *carry2 = carry + t1;
+    HIPCHK(c, hipMemcpyAsync(carry, c->e_lsn.p, 8 * t1, hipMemcpyDeviceToDevice, s));
+    bool in_alt = false;
+    HIPCHK(c, radix_sort_rows(1, t1, c->e_txn.as<uint32_t>(), c->e_lsn.as<uint64_t>(), carry, t1,
+                              c->e_txn2.as<uint32_t>(), c->e_lsn2.as<uint64_t>(), carry2,
+                              c->e_scratch.p, c->e_scratch.bytes, &in_alt, nullptr, s));
+    uint32_t *st = in_alt ? c->e_txn2.as<uint32_t>() : c->e_txn.as<uint32_t>();
+    uint64_t *sl = in_alt ? c->e_lsn2.as<uint64_t>() : c->e_lsn.as<uint64_t>();
+    uint64_t *sc = in_alt ? carry2 : carry;
+    uint32_t *dt = in_alt ? c->e_txn.as<uint32_t>() : c->e_txn2.as<uint32_t>();
+    uint64_t *dl = in_alt ? c->e_lsn.as<uint64_t>() : c->e_lsn2.as<uint64_t>();
+    uint64_t *dc = in_alt ? carry : carry2;
+    uint32_t *dcount = c->e_cnt.as<uint32_t>();  // reuse: n + 1 >= 1 entries
+    HIPCHK(c, dedupe_rows(1, t1, st, sl, sc, t1, dt, dl, dc, t1, c->e_flags.as<uint32_t>(),
+                          c->e_scratch.p, c->e_scratch.bytes, dcount, s));
+    uint32_t nu = 0;
+    HIPCHK(c, hipMemcpyAsync(&nu, dcount, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->e_out_txn.resize(nu);
+    c->e_out_lsn.resize(nu);
+    if (nu) {
+        HIPCHK(c, hipMemcpyAsync(c->e_out_txn.data(), dt, 4 * (size_t)nu, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(c->e_out_lsn.data(), dl, 8 * (size_t)nu, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
+    *n_pairs = nu;
+    *txn = c->e_out_txn.data();
+    *writer_lsn = c->e_out_lsn.data();
+    return HSC_OK;
 }
 
 int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out)

@@ -219,6 +219,24 @@ uint32_t narrow_trad_buckets(uint32_t ntiles);
 hipError_t narrow_trad_build(const uint64_t *first, uint32_t ntiles, uint32_t m, uint32_t *trad,
                              hipStream_t s);
 uint32_t narrow_tiles_dir_lds();
+// Read/write conflict pairs (hsc_edges.hip) over every window version: the
+// build's key-sorted rows before dedupe.
+struct EdgeView {
+    const uint32_t *gid;
+    const uint64_t *words;  // [W][stride]
+    const uint64_t *lsn;
+    size_t stride;
+    uint32_t n;
+    int W;
+};
+hipError_t edge_after(const EdgeView &w, uint64_t smin, uint32_t *flag, uint32_t *scratch,
+                      EdgeView &o, uint32_t *n_out, hipStream_t s);
+hipError_t launch_edge_count(const EdgeView &w, const ProbeView &p, uint2 *span, uint32_t *cnt,
+                             hipStream_t s);
+hipError_t launch_edge_emit(const EdgeView &w, const ProbeView &p, const uint2 *span,
+                            const uint32_t *off, uint32_t *out_txn, uint64_t *out_lsn,
+                            hipStream_t s);
+
 // Replicant coalesce (hsc_coalesce.hip): flat read sets in, per-set surviving
 // rows (ord) + the four fields merge_neighbor rewrites (w_*) out.
 struct CoView {

@@ -122,7 +122,7 @@ EXPORTS = [
     "hsc_get_timing",
     "hsc_enable_timing", "hsc_dep_graph_scc", "hsc_dep_graph_edges",
     "hsc_window_ingest_raw", "hsc_decode_log", "hsc_decode_serial", "hsc_check_serial",
-    "hsc_set_layout", "hsc_window_layout", "hsc_coalesce_readsets",
+    "hsc_set_layout", "hsc_window_layout", "hsc_coalesce_readsets", "hsc_rw_edges",
 ]
 
 (LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES,
@@ -449,6 +449,23 @@ class Validator:
                                              out.ctypes.data_as(C.POINTER(C.c_int)))
         self._chk(rc, "hip_serial_check_batch")
         return out[:n]
+
+    def rw_edges(self, rs: ReadSets):
+        """(txn uint32[k], writer commit LSN uint64[k]): every (read set,
+        writer) pair of the A0 join before its OR-reduction, sorted, unique
+        (hsc_rw_edges; range probes only)."""
+        s, keep = readsets_struct(rs)
+        n = C.c_size_t()
+        t = C.c_void_p()
+        w = C.c_void_p()
+        self._chk(self.lib.hsc_rw_edges(self.ctx, C.byref(s), C.byref(n), C.byref(t), C.byref(w)),
+                  "hsc_rw_edges")
+        k = n.value
+        if k == 0:
+            return np.zeros(0, np.uint32), np.zeros(0, np.uint64)
+        txn = np.ctypeslib.as_array(C.cast(t, C.POINTER(C.c_uint32)), shape=(k,)).copy()
+        lsn = np.ctypeslib.as_array(C.cast(w, C.POINTER(C.c_uint64)), shape=(k,)).copy()
+        return txn, lsn
 
     def coalesce(self, rs: ReadSets) -> ReadSets:
         """currangearr_coalesce (db/sqlglue.c:305-311) of every read set on the

@@ -308,7 +308,17 @@ int hip_bdb_osql_serial_check(void *ctx, void *ranges, unsigned int *file,
 int hip_serial_check_batch(void *ctx, void *const *ranges, unsigned int *file,
                            unsigned int *offset, int regop_only, int n,
                            int *rc_out);
-/* Flat read sets (snapshots in rs->snap); rc_out[ntxn]; full checks only. */
+/* Read/write conflict pairs before the OR-reduction:
+ * every (read set t, writer commit LSN c) such that a write committed at c
+ * (c > t's snapshot) has a key inside one of t's ranges -- all the pairs the
+ * A0 join would find if serial_check_callback did not stop at the first hit
+ * (db/glue.c:2926-2963), i.e. the rw-antidependency edges t -> writer.
+ * Sorted by (t, c), unique.  Range probes only: table locks and the host-side
+ * window rules (forced verdicts) yield a verdict but no pairs.  Output arrays
+ * are owned by the context until its next call. */
+int hsc_rw_edges(hsc_ctx *ctx, const hsc_readsets *rs, size_t *n_pairs, const uint32_t **txn,
+                 const uint64_t **writer_lsn);
+
 /* Replicant read-set coalesce on the device: currangearr_coalesce
  * (db/sqlglue.c:305-311) -- qsort by currange_cmp (:206-242, glibc's
  * top-down merge sort), currangearr_merge_neighbor (:247-304), twice -- of
@@ -325,6 +335,7 @@ typedef struct hsc_coalesced {
 } hsc_coalesced;
 int hsc_coalesce_readsets(hsc_ctx *ctx, const hsc_readsets *rs, hsc_coalesced *out);
 
+/* Flat read sets (snapshots in rs->snap); rc_out[ntxn]; full checks only. */
 int hsc_check_readsets(hsc_ctx *ctx, const hsc_readsets *rs, int *rc_out);
 
 /* ---- marshalling + device probe (what the checks lower to) -------------- */
