@@ -113,30 +113,102 @@ def cpu_baseline(c2, gpu_verdict, threads, target_s, m0=None):
 
 
 def bench_graph(args):
-    """Config 4 (1 GPU): WR/WW/RW dependency graph + SCC of a Jepsen
-    bank/register-style history; value = history ops analysed per second
-    (device time of build + SCC, host upload excluded)."""
-    from comdb2_amd import hsc
+    """Config 4: WR/WW/RW dependency graph + SCC of a Jepsen bank/register
+    style history (SURVEY.md §8(a) A10, 100M ops by default), sharded by key
+    over the ranks (comdb2_amd/shard.py sharded_scc): each rank builds the
+    edges of its keys from device-resident ops, the ranks OR their covers
+    (all_reduce MAX), all-gather the edges between covered txns and colour
+    that graph.  Strong scaling: the history is fixed, value = its ops / the
+    max-over-ranks wall time of one step (inputs resident in HBM)."""
+    import torch
+    import torch.distributed as dist
+
+    from comdb2_amd import hsc, shard
     from comdb2_amd.workloads import config4_history
+    world = max(1, int(os.environ.get("WORLD_SIZE", "1")))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("HSC_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = 0
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     h = config4_history(n_txn=args.history_txns, n_keys=max(1000, args.history_txns // 10))
-    v = hsc.Validator(0)
-    times, st = [], None
+    hs = shard.history_shard(h, rank, world)
+    dh = shard.device_history(hs, dev)
+    v = hsc.Validator(local)
+    g = shard.GpuGraph(v, dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    times, st, scc = [], None, None
     for k in range(args.warmup + args.steps):
-        scc, st = v.dep_graph_scc(h)
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        scc, st = shard.sharded_scc(g, dh, h.ntxn, dev)
+        torch.cuda.synchronize(dev)
+        dt = time.perf_counter() - t0
+        barrier()
         if k >= args.warmup:
-            times.append(st["build_ms"] + st["scc_ms"])
-    ms = float(np.mean(times))
-    out = {"metric": "dependency-graph ops analysed/sec (WR/WW/RW edges + SCC)",
-           "value": h.nops / (ms * 1e-3), "unit": "ops/s", "n_gpus": 1, "steps": args.steps,
-           "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": None, "dtype": "u32/u64", "data": "synthetic config-4 history",
-           "config": {"workload": f"config4: {h.ntxn} txns, {h.nops} ops", "edges": st["edges"],
-                      "nontrivial_sccs": st["nontrivial_sccs"],
-                      "txns_in_cycles": st["txns_in_cycles"], "rounds": st["rounds"],
-                      "iterations": st["iterations"], "build_ms": st["build_ms"],
-                      "scc_ms": st["scc_ms"]}}
-    print(json.dumps(out), flush=True)
+            times.append(dt)
+    dt = torch.tensor([float(np.mean(times))], dtype=torch.float64,
+                      device=dev if backend == "nccl" else "cpu")
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    ms = float(dt.item()) * 1e3
+    out = None
+    if rank == 0:
+        # the unsharded call on the whole history must give the same components
+        full, fst = v.dep_graph_scc(h)
+        same = bool(np.array_equal(full, scc.cpu().numpy().astype(np.uint32)))
+        out = {"metric": "dependency-graph ops analysed/sec (WR/WW/RW edges + SCC)",
+               "value": h.nops / (ms * 1e-3), "unit": "ops/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+               "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+               "dtype": "u32/u64", "data": "synthetic config-4 history (seed 0xC0FFEE04)",
+               "config": {"workload": f"config4: {h.ntxn} txns, {h.nops} ops, key shards x{world}",
+                          "parallelism": f"key shards x{world} (cover all_reduce MAX + cut all_gather)",
+                          "edges": fst["edges"], "ww": fst["ww"], "wr": fst["wr"], "rw": fst["rw"],
+                          "nontrivial_sccs": st["scc"]["nontrivial_sccs"],
+                          "txns_in_cycles": st["scc"]["txns_in_cycles"],
+                          "cut_nodes": st["scc"]["cut_nodes"], "cut_rows": st["cut_rows"],
+                          "rank0_ops": hs.nops, "rank0_build_ms": st["build"]["build_ms"],
+                          "scc_cut_ms": st["scc"]["scc_ms"], "rounds": st["scc"]["rounds"],
+                          "unsharded_build_ms": fst["build_ms"], "unsharded_scc_ms": fst["scc_ms"],
+                          "parity_with_unsharded_gpu": same}}
+        if world == 1 and not args.no_cpu:
+            out["cpu_baseline"] = graph_cpu_baseline(args)
     v.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if out is not None:
+        print(json.dumps(out), flush=True)
+
+
+def graph_cpu_baseline(args):
+    """oracle/scc_oracle.c (Adya edges + Tarjan, one core) on a smaller
+    history of the same generator, sized to finish in seconds."""
+    from comdb2_amd.workloads import config4_history
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    n = max(1000, min(args.history_txns, 1_000_000))
+    h = config4_history(n_txn=n, n_keys=max(1000, n // 10))
+    t0 = time.perf_counter()
+    s_, d_, _ = O.dep_edges(h.txn, h.key, h.is_write, h.observed)
+    O.scc(h.ntxn, s_, d_)
+    dt = time.perf_counter() - t0
+    return {"value": h.nops / dt, "unit": "ops/s", "cores": 1, "kind": "port",
+            "sample": f"{h.ntxn} txns / {h.nops} ops of the config-4 generator, "
+                      f"oracle/scc_oracle.c edges + Tarjan, {dt:.1f} s"}
 
 
 def kernel_bytes(layout, W, n_keys, n_r, T, tm):
@@ -197,7 +269,8 @@ def main():
                     help="config 5: window writes per GPU (125M x 8 GPUs = SURVEY's 1B)")
     ap.add_argument("--check", action="store_true",
                     help="config 5, N = 1: full-batch CPU sort-join parity (oracle/sortjoin.c)")
-    ap.add_argument("--history-txns", type=int, default=4_000_000)
+    ap.add_argument("--history-txns", type=int, default=16_700_000,
+                    help="config 4: transactions (x ~6 ops: 16.7M = SURVEY's 100M-op history)")
     ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "traffic.json"),
                     help="PMC-derived HBM bytes per join launch (from a rocprofv3 --pmc run)")
     args = ap.parse_args()

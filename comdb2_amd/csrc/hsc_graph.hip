@@ -232,7 +232,77 @@ __global__ void k_finalize(uint32_t n, uint32_t *active, const uint32_t *color, 
 
 static inline unsigned blocks(size_t n) { return (unsigned)((n + 255) / 256); }
 
-hipError_t graph_build(const GraphInput &in, GraphBufs &g, hipStream_t s)
+// Edge rows g.ew/g.et/g.eg [0, ne_raw) (capacity ecap; invalid rows ~0) ->
+// sorted unique out-edges (src, out_dst, type), in-edges (in_src, in_dst) and
+// CSR / CSC offsets over nn nodes.
+static hipError_t graph_rows_csr(size_t ne_raw, size_t ecap, uint32_t nn, GraphBufs &g,
+                                 hipStream_t s)
+{
+    hipError_t e = hipSuccess;
+#define CK(x)                                 \
+    do {                                      \
+        e = (x);                              \
+        if (e != hipSuccess) return e;        \
+    } while (0)
+    // 3. sort by (src, dst), merge, compact: out-edges; then (dst, src): in-edges
+    for (int pass = 0; pass < 2; ++pass) {
+        DBuf *ew = &g.ew, *et = &g.et, *eg = &g.eg;
+        if (pass == 1) {  // rebuild rows keyed (dst, src) from the compacted out-edges
+            CK(hipMemcpyAsync(g.ew.p, g.swap_rows.p, 8 * g.ne, hipMemcpyDeviceToDevice, s));
+            CK(hipMemsetAsync(g.et.p, 0, 8 * g.ne, s));
+            CK(hipMemsetAsync(g.eg.p, 0, 4 * g.ne, s));
+        }
+        const size_t n = pass == 0 ? ne_raw : g.ne;
+        CK(g.scratch.ensure(std::max(radix_scratch_bytes(n, 1), scan_scratch_bytes(n + 1) + 64)));
+        bool a2 = false;
+        CK(radix_sort_rows(1, n, eg->as<uint32_t>(), ew->as<uint64_t>(), et->as<uint64_t>(), ecap,
+                           g.eg2.as<uint32_t>(), g.ew2.as<uint64_t>(), g.et2.as<uint64_t>(),
+                           g.scratch.p, g.scratch.bytes, &a2, nullptr, s));
+        const uint64_t *rw = a2 ? g.ew2.as<uint64_t>() : g.ew.as<uint64_t>();
+        uint64_t *rt = a2 ? g.et2.as<uint64_t>() : g.et.as<uint64_t>();
+        CK(g.flags.ensure(4 * (n + 64)));
+        CK(g.flags2.ensure(4 * (n + 64)));
+        if (n) k_edge_heads<<<blocks(n), 256, 0, s>>>(n, rw, rt, g.flags.as<uint32_t>());
+        CK(hipMemsetAsync(g.flags.as<uint32_t>() + n, 0, 4, s));
+        CK(hipMemcpyAsync(g.flags2.p, g.flags.p, 4 * (n + 1), hipMemcpyDeviceToDevice, s));
+        CK(scan_exclusive_u32(g.flags.as<uint32_t>(), n + 1, g.scratch.as<uint32_t>(), s));
+        uint32_t m = 0;
+        CK(hipMemcpyAsync(&m, g.flags.as<uint32_t>() + n, 4, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        if (pass == 0) {
+            g.ne = m;
+            CK(g.out_dst.ensure(4 * ((size_t)m + 1)));
+            CK(g.src.ensure(4 * ((size_t)m + 1)));
+            CK(g.type.ensure(4 * ((size_t)m + 1)));
+            if (n)
+                k_edge_compact<<<blocks(n), 256, 0, s>>>(n, rw, rt, g.flags.as<uint32_t>(),
+                                                         g.flags2.as<uint32_t>(), g.src.as<uint32_t>(),
+                                                         g.out_dst.as<uint32_t>(), g.type.as<uint32_t>(), 0);
+            // rows for the in-edge pass: dst << 32 | src
+            CK(g.swap_rows.ensure(8 * ((size_t)m + 1)));
+            CK(swap_edge_words(m, g.src.as<uint32_t>(), g.out_dst.as<uint32_t>(),
+                               g.swap_rows.as<uint64_t>(), s));
+        } else {
+            CK(g.in_src.ensure(4 * ((size_t)m + 1)));
+            CK(g.in_dst.ensure(4 * ((size_t)m + 1)));
+            if (n)
+                k_edge_compact<<<blocks(n), 256, 0, s>>>(n, rw, rt, g.flags.as<uint32_t>(),
+                                                         g.flags2.as<uint32_t>(), g.in_src.as<uint32_t>(),
+                                                         g.in_dst.as<uint32_t>(), nullptr, 1);
+        }
+        CK(hipGetLastError());
+    }
+    // 4. CSR / CSC offsets
+    CK(g.out_off.ensure(4 * ((size_t)nn + 1)));
+    CK(g.in_off.ensure(4 * ((size_t)nn + 1)));
+    k_csr_offsets<<<blocks(g.ne + 1), 256, 0, s>>>(g.ne, g.src.as<uint32_t>(), nn, g.out_off.as<uint32_t>());
+    k_csr_offsets<<<blocks(g.ne + 1), 256, 0, s>>>(g.ne, g.in_dst.as<uint32_t>(), nn, g.in_off.as<uint32_t>());
+    CK(hipGetLastError());
+#undef CK
+    return hipSuccess;
+}
+
+hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_t s)
 {
     hipError_t e = hipSuccess;
 #define CK(x)                                 \
@@ -296,61 +366,13 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, hipStream_t s)
                                                    nu, wkey, wtxn, g.ew.as<uint64_t>(),
                                                    g.et.as<uint64_t>(), g.eg.as<uint32_t>());
     CK(hipGetLastError());
-    // 3. sort by (src, dst), merge, compact: out-edges; then (dst, src): in-edges
-    for (int pass = 0; pass < 2; ++pass) {
-        DBuf *ew = &g.ew, *et = &g.et, *eg = &g.eg;
-        if (pass == 1) {  // rebuild rows keyed (dst, src) from the compacted out-edges
-            CK(hipMemcpyAsync(g.ew.p, g.swap_rows.p, 8 * g.ne, hipMemcpyDeviceToDevice, s));
-            CK(hipMemsetAsync(g.et.p, 0, 8 * g.ne, s));
-            CK(hipMemsetAsync(g.eg.p, 0, 4 * g.ne, s));
-        }
-        const size_t n = pass == 0 ? ne_raw : g.ne;
-        CK(g.scratch.ensure(std::max(radix_scratch_bytes(n, 1), scan_scratch_bytes(n + 1) + 64)));
-        bool a2 = false;
-        CK(radix_sort_rows(1, n, eg->as<uint32_t>(), ew->as<uint64_t>(), et->as<uint64_t>(), ecap,
-                           g.eg2.as<uint32_t>(), g.ew2.as<uint64_t>(), g.et2.as<uint64_t>(),
-                           g.scratch.p, g.scratch.bytes, &a2, nullptr, s));
-        const uint64_t *rw = a2 ? g.ew2.as<uint64_t>() : g.ew.as<uint64_t>();
-        uint64_t *rt = a2 ? g.et2.as<uint64_t>() : g.et.as<uint64_t>();
-        CK(g.flags.ensure(4 * (n + 64)));
-        CK(g.flags2.ensure(4 * (n + 64)));
-        if (n) k_edge_heads<<<blocks(n), 256, 0, s>>>(n, rw, rt, g.flags.as<uint32_t>());
-        CK(hipMemsetAsync(g.flags.as<uint32_t>() + n, 0, 4, s));
-        CK(hipMemcpyAsync(g.flags2.p, g.flags.p, 4 * (n + 1), hipMemcpyDeviceToDevice, s));
-        CK(scan_exclusive_u32(g.flags.as<uint32_t>(), n + 1, g.scratch.as<uint32_t>(), s));
-        uint32_t m = 0;
-        CK(hipMemcpyAsync(&m, g.flags.as<uint32_t>() + n, 4, hipMemcpyDeviceToHost, s));
-        CK(hipStreamSynchronize(s));
-        if (pass == 0) {
-            g.ne = m;
-            CK(g.out_dst.ensure(4 * ((size_t)m + 1)));
-            CK(g.src.ensure(4 * ((size_t)m + 1)));
-            CK(g.type.ensure(4 * ((size_t)m + 1)));
-            if (n)
-                k_edge_compact<<<blocks(n), 256, 0, s>>>(n, rw, rt, g.flags.as<uint32_t>(),
-                                                         g.flags2.as<uint32_t>(), g.src.as<uint32_t>(),
-                                                         g.out_dst.as<uint32_t>(), g.type.as<uint32_t>(), 0);
-            // rows for the in-edge pass: dst << 32 | src
-            CK(g.swap_rows.ensure(8 * ((size_t)m + 1)));
-            CK(swap_edge_words(m, g.src.as<uint32_t>(), g.out_dst.as<uint32_t>(),
-                               g.swap_rows.as<uint64_t>(), s));
-        } else {
-            CK(g.in_src.ensure(4 * ((size_t)m + 1)));
-            CK(g.in_dst.ensure(4 * ((size_t)m + 1)));
-            if (n)
-                k_edge_compact<<<blocks(n), 256, 0, s>>>(n, rw, rt, g.flags.as<uint32_t>(),
-                                                         g.flags2.as<uint32_t>(), g.in_src.as<uint32_t>(),
-                                                         g.in_dst.as<uint32_t>(), nullptr, 1);
-        }
-        CK(hipGetLastError());
+    g.raw = !full;
+    g.ne_raw = ne_raw;
+    if (!full) {  // raw edge rows only (duplicates, ~0 holes): enough for cover / cut
+        g.ne = 0;
+        return hipSuccess;
     }
-    // 4. CSR / CSC offsets
-    const uint32_t nn = in.ntxn;
-    CK(g.out_off.ensure(4 * ((size_t)nn + 1)));
-    CK(g.in_off.ensure(4 * ((size_t)nn + 1)));
-    k_csr_offsets<<<blocks(g.ne + 1), 256, 0, s>>>(g.ne, g.src.as<uint32_t>(), nn, g.out_off.as<uint32_t>());
-    k_csr_offsets<<<blocks(g.ne + 1), 256, 0, s>>>(g.ne, g.in_dst.as<uint32_t>(), nn, g.in_off.as<uint32_t>());
-    CK(hipGetLastError());
+    CK(graph_rows_csr(ne_raw, ecap, in.ntxn, g, s));
 #undef CK
     return hipSuccess;
 }
@@ -440,6 +462,258 @@ hipError_t graph_scc(uint32_t nn, GraphBufs &g, uint32_t *rounds, uint32_t *iter
         if (h[0] == 0) break;
         if (*rounds > nn) return hipErrorUnknown;  // cannot happen: every round retires >= 1 node
     }
+#undef CK
+    return hipSuccess;
+}
+
+__global__ void k_check_ops(GraphInput in, uint32_t *bad)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= in.nops) return;
+    const uint32_t o = in.observed[i];
+    if (in.txn[i] >= in.ntxn || (o != kNone && o >= in.ntxn)) atomicOr(bad, 1u);
+}
+
+// *bad_out := 1 if an op names a txn (or observed writer) >= ntxn
+hipError_t graph_check_input(const GraphInput &in, GraphBufs &g, uint32_t *bad_out, hipStream_t s)
+{
+    hipError_t e = g.count.ensure(64);
+    if (e != hipSuccess) return e;
+    uint32_t *bad = g.count.as<uint32_t>() + 12;
+    if ((e = hipMemsetAsync(bad, 0, 4, s)) != hipSuccess) return e;
+    if (in.nops) k_check_ops<<<blocks(in.nops), 256, 0, s>>>(in, bad);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(bad_out, bad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    return hipStreamSynchronize(s);
+}
+
+// ---- sharded SCC: cover, cut, SCC of the cut --------------------------------
+// Txn ids are commit order.  Every node of a cycle lies inside [dst, src] of
+// one of the cycle's backward (src > dst) edges, so only nodes
+// covered by a backward edge's interval can share a component: the SCCs of
+// the graph induced on covered nodes are the nontrivial SCCs of the whole
+// graph, and every other node is its own component.  Shards (histories split
+// by key: all WW/WR/RW edges are per key) OR their covers, exchange only the
+// edges between covered nodes, and run the colouring on that small graph.
+
+// Edge i of a graph: raw rows (src << 32 | dst, ~0 = none) or sorted arrays.
+struct EdgeSet {
+    const uint64_t *rows;  // raw build, else nullptr
+    const uint32_t *src, *dst;
+    size_t n;
+    __device__ __forceinline__ bool get(size_t i, uint32_t &a, uint32_t &b) const
+    {
+        if (rows) {
+            const uint64_t r = rows[i];
+            a = (uint32_t)(r >> 32);
+            b = (uint32_t)r;
+            return r != ~0ull;
+        }
+        a = src[i];
+        b = dst[i];
+        return true;
+    }
+};
+
+static EdgeSet edge_set(const GraphBufs &g)
+{
+    if (g.raw) return EdgeSet{g.ew.as<uint64_t>(), nullptr, nullptr, g.ne_raw};
+    return EdgeSet{nullptr, g.src.as<uint32_t>(), g.out_dst.as<uint32_t>(), g.ne};
+}
+
+__global__ void k_back_diff(EdgeSet es, uint32_t *diff)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= es.n) return;
+    uint32_t a, b;
+    if (es.get(i, a, b) && a > b) {
+        atomicAdd(&diff[b], 1u);
+        atomicAdd(&diff[a + 1], 0xFFFFFFFFu);  // -1 mod 2^32: prefix sums stay >= 0
+    }
+}
+
+// ex = exclusive scan of the interval diffs: node v is covered iff ex[v + 1] != 0
+__global__ void k_cover_flags(uint32_t nn, const uint32_t *ex, uint8_t *cover)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < nn) cover[v] = ex[v + 1] != 0;
+}
+
+__global__ void k_cut_flags(EdgeSet es, const uint8_t *cover, uint32_t *flags)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= es.n) return;
+    uint32_t a, b;
+    flags[i] = es.get(i, a, b) && cover[a] && cover[b];
+}
+
+__global__ void k_cut_rows(EdgeSet es, const uint8_t *cover, const uint32_t *pos, uint64_t *rows)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= es.n) return;
+    uint32_t a, b;
+    if (es.get(i, a, b) && cover[a] && cover[b]) rows[pos[i]] = ((uint64_t)a << 32) | b;
+}
+
+// counts[0..2] += edges carrying the ww / wr / rw bit
+__global__ void k_type_counts(size_t ne, const uint32_t *type, unsigned long long *counts)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t t = i < ne ? type[i] : 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const uint64_t m = __ballot((t >> k) & 1u);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&counts[k], (unsigned long long)__popcll(m));
+    }
+}
+
+hipError_t graph_type_counts(GraphBufs &g, uint64_t out[3], hipStream_t s)
+{
+    hipError_t e = g.count.ensure(64);
+    if (e != hipSuccess) return e;
+    unsigned long long *c = (unsigned long long *)(g.count.as<uint32_t>() + 16);
+    if ((e = hipMemsetAsync(c, 0, 24, s)) != hipSuccess) return e;
+    if (g.ne) k_type_counts<<<blocks(g.ne), 256, 0, s>>>(g.ne, g.type.as<uint32_t>(), c);
+    if ((e = hipMemcpyAsync(out, c, 24, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    return hipStreamSynchronize(s);
+}
+
+__global__ void k_cover_u32(uint32_t nn, const uint8_t *cover, uint32_t *id)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < nn) id[v] = cover[v] != 0;
+}
+
+// id = exclusive scan of the cover: covered node v is node id[v] of the cut
+__global__ void k_txn_of(uint32_t nn, const uint8_t *cover, const uint32_t *id, uint32_t *txn_of)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < nn && cover[v]) txn_of[id[v]] = v;
+}
+
+// cut rows (txn ids; ~0 = padding) -> edge rows over cut node ids
+__global__ void k_relabel(size_t m, uint32_t nn, const uint64_t *rows, const uint8_t *cover,
+                          const uint32_t *id, uint64_t *ew, uint64_t *et, uint32_t *eg,
+                          uint32_t *bad)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint64_t r = rows[i];
+    uint64_t e = ~0ull;
+    if (r != ~0ull) {
+        const uint32_t a = (uint32_t)(r >> 32), b = (uint32_t)r;
+        if (a < nn && b < nn && cover[a] && cover[b] && a != b)
+            e = ((uint64_t)id[a] << 32) | id[b];
+        else
+            atomicOr(bad, 1u);
+    }
+    ew[i] = e;
+    et[i] = 0;
+    eg[i] = 0;
+}
+
+__global__ void k_scc_out(uint32_t nn, const uint8_t *cover, const uint32_t *id,
+                          const uint32_t *sub_scc, const uint32_t *txn_of, uint32_t *scc)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < nn) scc[v] = cover[v] ? txn_of[sub_scc[id[v]]] : v;
+}
+
+hipError_t graph_cover(GraphBufs &g, uint32_t nn, uint8_t *cover, hipStream_t s)
+{
+    hipError_t e = hipSuccess;
+    if (nn == 0) return hipSuccess;
+    DBuf &diff = g.diff, &scratch = g.scratch;
+    if ((e = diff.ensure(4 * ((size_t)nn + 2))) != hipSuccess) return e;
+    if ((e = scratch.ensure(std::max(scan_scratch_bytes((size_t)nn + 1), (size_t)1024))) != hipSuccess)
+        return e;
+    if ((e = hipMemsetAsync(diff.p, 0, 4 * ((size_t)nn + 2), s)) != hipSuccess) return e;
+    const EdgeSet es = edge_set(g);
+    if (es.n) k_back_diff<<<blocks(es.n), 256, 0, s>>>(es, diff.as<uint32_t>());
+    if ((e = scan_exclusive_u32(diff.as<uint32_t>(), (size_t)nn + 1, scratch.as<uint32_t>(), s)) !=
+        hipSuccess)
+        return e;
+    k_cover_flags<<<blocks(nn), 256, 0, s>>>(nn, diff.as<uint32_t>(), cover);
+    return hipGetLastError();
+}
+
+hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s)
+{
+    hipError_t e = hipSuccess;
+    const EdgeSet es = edge_set(g);
+    const size_t ne = es.n;
+    *m = 0;
+    if ((e = g.flags.ensure(4 * (ne + 64))) != hipSuccess) return e;
+    if ((e = g.scratch.ensure(std::max(scan_scratch_bytes(ne + 1), (size_t)1024))) != hipSuccess)
+        return e;
+    if (ne) k_cut_flags<<<blocks(ne), 256, 0, s>>>(es, cover, g.flags.as<uint32_t>());
+    if ((e = hipMemsetAsync(g.flags.as<uint32_t>() + ne, 0, 4, s)) != hipSuccess) return e;
+    if ((e = scan_exclusive_u32(g.flags.as<uint32_t>(), ne + 1, g.scratch.as<uint32_t>(), s)) !=
+        hipSuccess)
+        return e;
+    uint32_t k = 0;
+    if ((e = hipMemcpyAsync(&k, g.flags.as<uint32_t>() + ne, 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    DBuf &rows = g.cut;
+    if ((e = rows.ensure(8 * ((size_t)k + 1))) != hipSuccess) return e;
+    if (ne) k_cut_rows<<<blocks(ne), 256, 0, s>>>(es, cover, g.flags.as<uint32_t>(), rows.as<uint64_t>());
+    *m = k;
+    return hipGetLastError();
+}
+
+hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *rows, size_t m,
+                          GraphBufs &g, uint32_t *scc_out, uint32_t *n_cut, uint32_t *rounds,
+                          uint32_t *iterations, hipStream_t s)
+{
+    hipError_t e = hipSuccess;
+#define CK(x)                                 \
+    do {                                      \
+        e = (x);                              \
+        if (e != hipSuccess) return e;        \
+    } while (0)
+    *rounds = *iterations = 0;
+    *n_cut = 0;
+    if (nn == 0) return hipSuccess;
+    // cut node ids
+    CK(g.cut_id.ensure(4 * ((size_t)nn + 64)));
+    CK(g.txn_of.ensure(4 * ((size_t)nn + 64)));
+    CK(g.scratch.ensure(std::max(scan_scratch_bytes((size_t)nn + 1), (size_t)1024)));
+    CK(g.count.ensure(64));
+    uint32_t *id = g.cut_id.as<uint32_t>();
+    k_cover_u32<<<blocks(nn), 256, 0, s>>>(nn, cover, id);
+    CK(hipMemsetAsync(id + nn, 0, 4, s));
+    CK(scan_exclusive_u32(id, (size_t)nn + 1, g.scratch.as<uint32_t>(), s));
+    uint32_t nc = 0;
+    CK(hipMemcpyAsync(&nc, id + nn, 4, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    *n_cut = nc;
+    uint32_t *txn_of = g.txn_of.as<uint32_t>();
+    k_txn_of<<<blocks(nn), 256, 0, s>>>(nn, cover, id, txn_of);
+    // edge rows over cut ids -> sorted unique CSR / CSC
+    const size_t ecap = std::max<size_t>(64, (m + 63) & ~(size_t)63);
+    CK(g.ew.ensure(8 * ecap));
+    CK(g.et.ensure(8 * ecap));
+    CK(g.eg.ensure(4 * ecap));
+    CK(g.ew2.ensure(8 * ecap));
+    CK(g.et2.ensure(8 * ecap));
+    CK(g.eg2.ensure(4 * ecap));
+    uint32_t *bad = g.count.as<uint32_t>() + 8;
+    CK(hipMemsetAsync(bad, 0, 4, s));
+    if (m)
+        k_relabel<<<blocks(m), 256, 0, s>>>(m, nn, rows, cover, id, g.ew.as<uint64_t>(),
+                                            g.et.as<uint64_t>(), g.eg.as<uint32_t>(), bad);
+    CK(hipGetLastError());
+    uint32_t hbad = 0;
+    CK(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    if (hbad) return hipErrorInvalidValue;  // a row outside the cover: not a cut of it
+    CK(graph_rows_csr(m, ecap, nc, g, s));
+    CK(graph_scc(nc, g, rounds, iterations, s));
+    // sub_scc lives in g.scc (nc entries); the caller's scc_out gets all nn
+    k_scc_out<<<blocks(nn), 256, 0, s>>>(nn, cover, id, g.scc.as<uint32_t>(), txn_of, scc_out);
+    CK(hipGetLastError());
+    CK(hipStreamSynchronize(s));
 #undef CK
     return hipSuccess;
 }

@@ -126,6 +126,7 @@ struct hsc_ctx {
 
     // dependency graph
     GraphBufs graph;
+    GraphBufs subgraph;  // the graph induced on a cover (sharded SCC)
     uint32_t graph_ntxn = 0;
 
     // Probe lanes: the probe scratch above belongs to the active lane; other
@@ -1855,13 +1856,37 @@ int hsc_enable_timing(hsc_ctx *c, int on)
     return HSC_OK;
 }
 
-int hsc_dep_graph_scc(hsc_ctx *c, const hsc_history *h, uint32_t *scc_out, hsc_graph_stats *st)
+}  // extern "C"
+
+// Build c->graph from device-resident ops (edges and CSR/CSC), timed with
+// events.  Caller holds c->mu.
+static int graph_build_timed(hsc_ctx *c, const GraphInput &in, bool full, float *build_ms)
 {
-    if (!c || !h || (h->nops && (!h->txn || !h->key || !h->is_write || !h->observed)) ||
-        (h->ntxn && !scc_out) || h->nops > 0x7FFFFFFFull)
+    hipStream_t s = c->stream;
+    GraphBufs &gb = c->graph;
+    hipEvent_t e0, e1;
+    HIPCHK(c, hipEventCreate(&e0));
+    HIPCHK(c, hipEventCreate(&e1));
+    HIPCHK(c, hipEventRecord(e0, s));
+    hipError_t e = graph_build(in, gb, full, s);
+    if (e == hipSuccess) e = hipEventRecord(e1, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e == hipSuccess) (void)hipEventElapsedTime(build_ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    HIPCHK(c, e);
+    c->graph_ntxn = in.ntxn;
+    return HSC_OK;
+}
+
+// Upload a history and build its graph into c->graph (edges and CSR/CSC).
+// Caller holds c->mu.
+static int graph_upload_build(hsc_ctx *c, const hsc_history *h, bool full, float *build_ms)
+{
+    if (!h || (h->nops && (!h->txn || !h->key || !h->is_write || !h->observed)) ||
+        h->nops > 0x7FFFFFFFull)
         return HSC_EINVAL;
     if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
-    std::lock_guard<std::mutex> g(c->mu);
     (void)hipSetDevice(c->device);
     for (size_t i = 0; i < h->nops; ++i)
         if (h->txn[i] >= h->ntxn || h->observed[i] >= (int64_t)h->ntxn || h->observed[i] < -1)
@@ -1883,12 +1908,48 @@ int hsc_dep_graph_scc(hsc_ctx *c, const hsc_history *h, uint32_t *scc_out, hsc_g
     }
     GraphInput in{gb.h_txn.as<uint32_t>(), gb.h_key.as<uint64_t>(), gb.h_isw.as<uint8_t>(),
                   gb.h_obs.as<uint32_t>(), n, h->ntxn};
-    hipEvent_t e0, e1, e2;
-    HIPCHK(c, hipEventCreate(&e0));
+    return graph_build_timed(c, in, full, build_ms);
+}
+
+// Edge and edge-type counts of c->graph into st (none after a raw build).
+static int graph_edge_stats(hsc_ctx *c, hsc_graph_stats *st)
+{
+    GraphBufs &gb = c->graph;
+    st->edges = gb.ne;
+    uint64_t t[3] = {0, 0, 0};
+    HIPCHK(c, graph_type_counts(gb, t, c->stream));
+    st->ww = t[0];
+    st->wr = t[1];
+    st->rw = t[2];
+    return HSC_OK;
+}
+
+static void scc_size_stats(const uint32_t *scc, uint32_t ntxn, hsc_graph_stats *st)
+{
+    std::vector<uint32_t> sz(std::max<uint32_t>(ntxn, 1), 0);
+    for (uint32_t v = 0; v < ntxn; ++v)
+        if (scc[v] < ntxn) sz[scc[v]]++;
+    for (uint32_t v = 0; v < ntxn; ++v)
+        if (sz[v] > 1) {
+            st->nontrivial_sccs++;
+            st->txns_in_cycles += sz[v];
+        }
+}
+
+extern "C" {
+
+int hsc_dep_graph_scc(hsc_ctx *c, const hsc_history *h, uint32_t *scc_out, hsc_graph_stats *st)
+{
+    if (!c || !h || (h->ntxn && !scc_out)) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    float build_ms = 0;
+    int rc = graph_upload_build(c, h, true, &build_ms);
+    if (rc) return rc;
+    hipStream_t s = c->stream;
+    GraphBufs &gb = c->graph;
+    hipEvent_t e1, e2;
     HIPCHK(c, hipEventCreate(&e1));
     HIPCHK(c, hipEventCreate(&e2));
-    HIPCHK(c, hipEventRecord(e0, s));
-    HIPCHK(c, graph_build(in, gb, s));
     HIPCHK(c, hipEventRecord(e1, s));
     uint32_t rounds = 0, iters = 0;
     HIPCHK(c, graph_scc(h->ntxn, gb, &rounds, &iters, s));
@@ -1896,31 +1957,118 @@ int hsc_dep_graph_scc(hsc_ctx *c, const hsc_history *h, uint32_t *scc_out, hsc_g
     if (h->ntxn)
         HIPCHK(c, hipMemcpyAsync(scc_out, gb.scc.p, 4 * (size_t)h->ntxn, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    c->graph_ntxn = h->ntxn;
     if (st) {
         memset(st, 0, sizeof *st);
-        st->edges = gb.ne;
-        (void)hipEventElapsedTime(&st->build_ms, e0, e1);
+        st->build_ms = build_ms;
         (void)hipEventElapsedTime(&st->scc_ms, e1, e2);
-        std::vector<uint32_t> ty(std::max<size_t>(gb.ne, 1));
-        if (gb.ne) HIPCHK(c, hipMemcpy(ty.data(), gb.type.p, 4 * gb.ne, hipMemcpyDeviceToHost));
-        for (size_t i = 0; i < gb.ne; ++i) {
-            st->ww += (ty[i] & kDepWW) != 0;
-            st->wr += (ty[i] & kDepWR) != 0;
-            st->rw += (ty[i] & kDepRW) != 0;
-        }
-        std::vector<uint32_t> sz(std::max<uint32_t>(h->ntxn, 1), 0);
-        for (uint32_t v = 0; v < h->ntxn; ++v)
-            if (scc_out[v] < h->ntxn) sz[scc_out[v]]++;
-        for (uint32_t v = 0; v < h->ntxn; ++v)
-            if (sz[v] > 1) {
-                st->nontrivial_sccs++;
-                st->txns_in_cycles += sz[v];
-            }
+        rc = graph_edge_stats(c, st);
+        if (rc) return rc;
+        scc_size_stats(scc_out, h->ntxn, st);
         st->rounds = rounds;
         st->iterations = iters;
     }
-    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipEventDestroy(e2);
+    return HSC_OK;
+}
+
+int hsc_dep_graph_build(hsc_ctx *c, const hsc_history *h, int flags, hsc_graph_stats *st)
+{
+    if (!c || !h) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    float build_ms = 0;
+    int rc = graph_upload_build(c, h, (flags & HSC_GRAPH_FULL) != 0, &build_ms);
+    if (rc || !st) return rc;
+    memset(st, 0, sizeof *st);
+    st->build_ms = build_ms;
+    return graph_edge_stats(c, st);
+}
+
+int hsc_dep_graph_build_device(hsc_ctx *c, size_t nops, uint32_t ntxn, const uint32_t *txn_dev,
+                               const uint64_t *key_dev, const uint8_t *is_write_dev,
+                               const uint32_t *observed_dev, int flags, hsc_graph_stats *st)
+{
+    if (!c || (nops && (!txn_dev || !key_dev || !is_write_dev || !observed_dev)) ||
+        nops > 0x7FFFFFFFull)
+        return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    GraphInput in{txn_dev, key_dev, is_write_dev, observed_dev, nops, ntxn};
+    uint32_t bad = 0;
+    HIPCHK(c, graph_check_input(in, c->graph, &bad, c->stream));
+    if (bad) return fail(c, HSC_EINVAL, "history op out of range");
+    float build_ms = 0;
+    int rc = graph_build_timed(c, in, (flags & HSC_GRAPH_FULL) != 0, &build_ms);
+    if (rc || !st) return rc;
+    memset(st, 0, sizeof *st);
+    st->build_ms = build_ms;
+    return graph_edge_stats(c, st);
+}
+
+int hsc_dep_graph_cover(hsc_ctx *c, uint8_t *cover_dev)
+{
+    if (!c || (c->graph_ntxn && !cover_dev)) return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    HIPCHK(c, graph_cover(c->graph, c->graph_ntxn, cover_dev, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return HSC_OK;
+}
+
+int hsc_dep_graph_cut(hsc_ctx *c, const uint8_t *cover_dev, uint64_t *rows_dev, size_t cap,
+                      size_t *m)
+{
+    if (!c || !m || (c->graph_ntxn && !cover_dev)) return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    HIPCHK(c, graph_cut(c->graph, cover_dev, m, c->stream));
+    const size_t k = std::min(cap, *m);
+    if (k && rows_dev)
+        HIPCHK(c, hipMemcpyAsync(rows_dev, c->graph.cut.p, 8 * k, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return HSC_OK;
+}
+
+int hsc_dep_graph_scc_cut(hsc_ctx *c, uint32_t ntxn, const uint8_t *cover_dev,
+                          const uint64_t *rows_dev, size_t m, uint32_t *scc_dev,
+                          hsc_graph_stats *st)
+{
+    if (!c || (ntxn && (!cover_dev || !scc_dev)) || (m && !rows_dev) || m > 0xFFFFFFFFull)
+        return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    hipStream_t s = c->stream;
+    hipEvent_t e1, e2;
+    HIPCHK(c, hipEventCreate(&e1));
+    HIPCHK(c, hipEventCreate(&e2));
+    HIPCHK(c, hipEventRecord(e1, s));
+    uint32_t rounds = 0, iters = 0, nc = 0;
+    hipError_t e = graph_scc_rows(ntxn, cover_dev, rows_dev, m, c->subgraph, scc_dev, &nc, &rounds,
+                                  &iters, s);
+    if (e == hipErrorInvalidValue) {
+        (void)hipEventDestroy(e1);
+        (void)hipEventDestroy(e2);
+        return fail(c, HSC_EINVAL, "cut row outside the cover");
+    }
+    HIPCHK(c, e);
+    HIPCHK(c, hipEventRecord(e2, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (st) {
+        memset(st, 0, sizeof *st);
+        st->edges = c->subgraph.ne;
+        (void)hipEventElapsedTime(&st->scc_ms, e1, e2);
+        st->rounds = rounds;
+        st->iterations = iters;
+        st->cut_nodes = nc;
+        // components of >= 2 txns live in the cut: its nc colours suffice
+        std::vector<uint32_t> h(std::max<uint32_t>(nc, 1));
+        if (nc) HIPCHK(c, hipMemcpy(h.data(), c->subgraph.scc.p, 4 * (size_t)nc, hipMemcpyDeviceToHost));
+        scc_size_stats(h.data(), nc, st);
+    }
     (void)hipEventDestroy(e1);
     (void)hipEventDestroy(e2);
     return HSC_OK;

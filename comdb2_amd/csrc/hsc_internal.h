@@ -289,19 +289,35 @@ struct GraphBufs {
     DBuf src, out_dst, type, in_src, in_dst, out_off, in_off;
     DBuf scc, active, color, mark, front, front2;
     DBuf h_txn, h_key, h_isw, h_obs;           // uploaded history
+    DBuf diff, cut, cut_id, txn_of;            // sharded SCC: cover, cut rows, cut ids
     size_t ne = 0;
+    size_t ne_raw = 0;  // raw edge slots in ew
+    bool raw = false;   // last build kept raw rows only (no sort / CSR)
     void release_all()
     {
         DBuf *all[] = {&flags, &flags2, &scratch, &count, &wg, &ww, &wl, &wg2, &ww2, &wl2,
                        &ew, &et, &eg, &ew2, &et2, &eg2, &swap_rows, &src, &out_dst, &type,
                        &in_src, &in_dst, &out_off, &in_off, &scc, &active, &color, &mark,
-                       &front, &front2, &h_txn, &h_key, &h_isw, &h_obs};
+                       &front, &front2, &h_txn, &h_key, &h_isw, &h_obs, &diff, &cut,
+                       &cut_id, &txn_of};
         for (DBuf *b : all) b->release();
     }
 };
-hipError_t graph_build(const GraphInput &in, GraphBufs &g, hipStream_t s);
+// full: sorted unique edges + CSR / CSC; else raw edge rows in g.ew only.
+hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_t s);
+hipError_t graph_type_counts(GraphBufs &g, uint64_t out[3], hipStream_t s);
 hipError_t graph_scc(uint32_t nnodes, GraphBufs &g, uint32_t *rounds, uint32_t *iterations,
                      hipStream_t s);
+// Sharded SCC (hsc_graph.hip): cover[v] = 1 iff v lies inside [dst, src] of a
+// backward edge of g; the edges of g between covered nodes -> g.cut rows
+// (src << 32 | dst, *m of them); SCC of the graph induced on the cover by
+// explicit rows (~0 = padding) into scc_out[nn] (device).
+hipError_t graph_check_input(const GraphInput &in, GraphBufs &g, uint32_t *bad_out, hipStream_t s);
+hipError_t graph_cover(GraphBufs &g, uint32_t nn, uint8_t *cover, hipStream_t s);
+hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s);
+hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *rows, size_t m,
+                          GraphBufs &g, uint32_t *scc_out, uint32_t *n_cut, uint32_t *rounds,
+                          uint32_t *iterations, hipStream_t s);
 hipError_t swap_edge_words(uint32_t m, const uint32_t *src, const uint32_t *dst, uint64_t *rows,
                            hipStream_t s);
 hipError_t scan_exclusive_u32(uint32_t *a, size_t n, uint32_t *scratch, hipStream_t s);

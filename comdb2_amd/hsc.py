@@ -96,7 +96,7 @@ class GraphStats(C.Structure):
     _fields_ = [("edges", C.c_uint64), ("ww", C.c_uint64), ("wr", C.c_uint64), ("rw", C.c_uint64),
                 ("nontrivial_sccs", C.c_uint32), ("txns_in_cycles", C.c_uint32),
                 ("rounds", C.c_uint32), ("iterations", C.c_uint32), ("build_ms", C.c_float),
-                ("scc_ms", C.c_float)]
+                ("scc_ms", C.c_float), ("cut_nodes", C.c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -123,6 +123,7 @@ EXPORTS = [
     "hsc_enable_timing", "hsc_dep_graph_scc", "hsc_dep_graph_edges",
     "hsc_window_ingest_raw", "hsc_decode_log", "hsc_decode_serial", "hsc_check_serial",
     "hsc_set_layout", "hsc_window_layout", "hsc_coalesce_readsets", "hsc_rw_edges",
+    "hsc_dep_graph_build", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
 ]
 
 (LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES,
@@ -177,6 +178,13 @@ def load() -> C.CDLL:
         "hsc_enable_timing": (C.c_int, [_p, C.c_int]),
         "hsc_dep_graph_scc": (C.c_int, [_p, C.POINTER(_History), _p, C.POINTER(GraphStats)]),
         "hsc_dep_graph_edges": (C.c_int, [_p, _p, _p, _p, C.c_size_t, C.POINTER(C.c_size_t)]),
+        "hsc_dep_graph_build": (C.c_int, [_p, C.POINTER(_History), C.c_int, C.POINTER(GraphStats)]),
+        "hsc_dep_graph_cover": (C.c_int, [_p, _p]),
+        "hsc_dep_graph_build_device": (C.c_int, [_p, C.c_size_t, C.c_uint32, _p, _p, _p, _p,
+                                                 C.c_int, C.POINTER(GraphStats)]),
+        "hsc_dep_graph_cut": (C.c_int, [_p, _p, _p, C.c_size_t, C.POINTER(C.c_size_t)]),
+        "hsc_dep_graph_scc_cut": (C.c_int, [_p, C.c_uint32, _p, _p, C.c_size_t, _p,
+                                            C.POINTER(GraphStats)]),
         "hsc_window_ingest_raw": (C.c_int, [_p, C.POINTER(_RawLog)]),
         "hsc_decode_log": (C.c_int, [_p, C.POINTER(_RawLog), C.POINTER(C.POINTER(_LLog))]),
         "hsc_decode_serial": (C.c_int, [_p, C.POINTER(_SerialMsgs),
@@ -548,6 +556,52 @@ class Validator:
         self._chk(self.lib.hsc_dep_graph_scc(self.ctx, C.byref(hs), out.ctypes.data, C.byref(st)),
                   "hsc_dep_graph_scc")
         return out[: h.ntxn], st.as_dict()
+
+    @staticmethod
+    def _history(h):
+        cols = [np.ascontiguousarray(h.txn, np.uint32), np.ascontiguousarray(h.key, np.uint64),
+                np.ascontiguousarray(h.is_write, np.uint8), np.ascontiguousarray(h.observed, np.int64)]
+        return _History(len(cols[0]), h.ntxn, *[c.ctypes.data for c in cols]), cols
+
+    # -- sharded SCC (hsc_dep_graph_build / _cover / _cut / _scc_cut); the
+    #    torch-tensor flow over ranks is comdb2_amd.shard.sharded_scc --------
+    def dep_graph_build(self, h, full: bool = False) -> dict:
+        """full: sorted unique edges + CSR (dep_graph_edges, edge stats);
+        else the raw edge rows only (all the cover / cut steps need)."""
+        hs, keep = self._history(h)
+        st = GraphStats()
+        self._chk(self.lib.hsc_dep_graph_build(self.ctx, C.byref(hs), int(full), C.byref(st)),
+                  "hsc_dep_graph_build")
+        return st.as_dict()
+
+    def dep_graph_build_device(self, nops: int, ntxn: int, txn_ptr: int, key_ptr: int,
+                               is_write_ptr: int, observed_ptr: int, full: bool = False) -> dict:
+        """Device-resident ops: txn u32, key u64, is_write u8, observed u32
+        (0xFFFFFFFF = initial version)."""
+        st = GraphStats()
+        self._chk(self.lib.hsc_dep_graph_build_device(self.ctx, nops, ntxn, C.c_void_p(txn_ptr),
+                                                      C.c_void_p(key_ptr), C.c_void_p(is_write_ptr),
+                                                      C.c_void_p(observed_ptr), int(full),
+                                                      C.byref(st)),
+                  "hsc_dep_graph_build_device")
+        return st.as_dict()
+
+    def dep_graph_cover(self, cover_ptr: int) -> None:
+        self._chk(self.lib.hsc_dep_graph_cover(self.ctx, C.c_void_p(cover_ptr)), "hsc_dep_graph_cover")
+
+    def dep_graph_cut(self, cover_ptr: int, rows_ptr: Optional[int] = None, cap: int = 0) -> int:
+        m = C.c_size_t()
+        self._chk(self.lib.hsc_dep_graph_cut(self.ctx, C.c_void_p(cover_ptr), C.c_void_p(rows_ptr or 0),
+                                             cap, C.byref(m)), "hsc_dep_graph_cut")
+        return m.value
+
+    def dep_graph_scc_cut(self, ntxn: int, cover_ptr: int, rows_ptr: int, m: int,
+                          scc_ptr: int) -> dict:
+        st = GraphStats()
+        self._chk(self.lib.hsc_dep_graph_scc_cut(self.ctx, ntxn, C.c_void_p(cover_ptr),
+                                                 C.c_void_p(rows_ptr), m, C.c_void_p(scc_ptr),
+                                                 C.byref(st)), "hsc_dep_graph_scc_cut")
+        return st.as_dict()
 
     def dep_graph_edges(self) -> tuple:
         n = C.c_size_t()

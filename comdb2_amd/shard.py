@@ -131,3 +131,120 @@ def merge_verdicts(verdict, group=None) -> None:
     """In-place OR of per-shard verdict bytes across ranks."""
     import torch.distributed as dist
     dist.all_reduce(verdict, op=dist.ReduceOp.MAX, group=group)
+
+
+# ---- config 4: dependency graph + SCC sharded by key -----------------------
+# Every WW / WR / RW edge belongs to one key (hsc_graph.hip), so a history
+# split by key gives each rank an exact part of the edge set with no
+# exchange.  Cycles need a backward (src > dst in commit order) edge and stay
+# inside the intervals [dst, src] of backward edges, so the ranks OR their
+# "covers" (all_reduce MAX over u8 per txn), all-gather only their edges
+# between covered txns, and every rank colours that small graph
+# (include/hip_serial.h, hsc_dep_graph_build / _cover / _cut / _scc_cut).
+
+def key_owner(key: np.ndarray, world: int) -> np.ndarray:
+    """Rank owning each history key (Fibonacci hash of the key, mod world)."""
+    h = (np.asarray(key, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15)) >> np.uint64(32)
+    return (h % np.uint64(world)).astype(np.int64)
+
+
+def history_shard(h, rank: int, world: int):
+    """The ops of a History whose key this rank owns (order kept; txn ids and
+    ntxn stay global)."""
+    from .workloads import History
+    if world == 1:
+        return h
+    sel = key_owner(h.key, world) == rank
+    return History(h.txn[sel], h.key[sel], h.is_write[sel], h.observed[sel], h.ntxn)
+
+
+class DeviceHistory:
+    """A History's ops resident on a GPU (torch tensors: txn i32, key i64,
+    is_write u8, observed i32 with -1 = initial version)."""
+
+    def __init__(self, h, device):
+        import torch
+        self.ntxn, self.nops = int(h.ntxn), int(len(h.txn))
+        up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)
+        self.txn = up(np.asarray(h.txn, np.uint32).view(np.int32))
+        self.key = up(np.asarray(h.key, np.uint64).view(np.int64))
+        self.is_write = up(np.asarray(h.is_write, np.uint8))
+        self.observed = up(np.asarray(h.observed, np.int64).astype(np.int32))
+
+
+def device_history(h, device) -> DeviceHistory:
+    return DeviceHistory(h, device)
+
+
+class GpuGraph:
+    """The sharded-SCC steps of a Validator over torch tensors on its GPU.
+    Every call synchronises torch's stream first (the library runs on its
+    own stream and returns after synchronising it)."""
+
+    def __init__(self, validator, device, full: bool = False):
+        self.v, self.device, self.full = validator, device, full
+
+    def _sync(self):
+        import torch
+        torch.cuda.synchronize(self.device)
+
+    def build(self, h) -> dict:
+        if isinstance(h, DeviceHistory):
+            self._sync()
+            return self.v.dep_graph_build_device(h.nops, h.ntxn, h.txn.data_ptr(), h.key.data_ptr(),
+                                                 h.is_write.data_ptr(), h.observed.data_ptr(),
+                                                 self.full)
+        return self.v.dep_graph_build(h, self.full)
+
+    def cover(self, cover) -> None:
+        self._sync()
+        self.v.dep_graph_cover(cover.data_ptr())
+
+    def cut(self, cover):
+        import torch
+        self._sync()
+        m = self.v.dep_graph_cut(cover.data_ptr())
+        rows = torch.empty(max(m, 1), dtype=torch.int64, device=self.device)
+        self._sync()
+        self.v.dep_graph_cut(cover.data_ptr(), rows.data_ptr(), m)
+        return rows[:m]
+
+    def scc_cut(self, ntxn: int, cover, rows, scc) -> dict:
+        self._sync()
+        return self.v.dep_graph_scc_cut(ntxn, cover.data_ptr(), rows.data_ptr(), rows.numel(),
+                                        scc.data_ptr())
+
+
+def sharded_scc(graph, h_shard, ntxn: int, device, group=None):
+    """scc[ntxn] (int32 tensor on `device`: largest txn of each txn's
+    component, identical on every rank) of the union of the ranks' history
+    shards, plus per-step stats.  `graph` is a GpuGraph (or a model with the
+    same four methods)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    st = {"build": graph.build(h_shard)}
+    cover = torch.zeros(max(ntxn, 1), dtype=torch.uint8, device=device)
+    graph.cover(cover)
+    # gloo (CPU rehearsal of the N > 1 path) exchanges host copies
+    cd = device if world == 1 or dist.get_backend(group) == "nccl" else torch.device("cpu")
+    if world > 1:
+        c = cover.to(cd)
+        dist.all_reduce(c, op=dist.ReduceOp.MAX, group=group)
+        cover = c.to(device)
+    rows = graph.cut(cover)
+    st["cut_rows_local"] = int(rows.numel())
+    if world > 1:
+        n = torch.tensor([rows.numel()], dtype=torch.int64, device=cd)
+        sizes = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(sizes, n, group=group)
+        mx = max(1, max(int(x.item()) for x in sizes))
+        pad = torch.full((mx,), -1, dtype=torch.int64, device=cd)  # ~0 rows: padding
+        pad[: rows.numel()] = rows.to(cd)
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+        rows = torch.cat(parts).to(device)
+    st["cut_rows"] = int(rows.numel())
+    scc = torch.empty(max(ntxn, 1), dtype=torch.int32, device=device)
+    st["scc"] = graph.scc_cut(ntxn, cover, rows, scc)
+    return scc[:ntxn], st

@@ -370,18 +370,33 @@ def config4_history(seed: int = SEED_CONFIG4, n_txn: int = 1_000_000, n_keys: in
     # writes sorted by (key, txn) as one composite
     wc = np.sort((key[w] << np.uint64(32)) | txn[w].astype(np.uint64))
     rc = (key << np.uint64(32)) | np.repeat(snap, ops_per_txn).astype(np.uint64)
-    idx = np.searchsorted(wc, rc, side="left").astype(np.int64) - 1
+    qo = np.argsort(rc)  # sorted queries: searchsorted walks wc in order
+    idx = np.empty(n, np.int64)
+    idx[qo] = np.searchsorted(wc, rc[qo], side="left")
+    idx -= 1
     ok = idx >= 0
     cand = wc[np.maximum(idx, 0)]
     ok &= (cand >> np.uint64(32)) == key
     observed = np.where(ok, (cand & np.uint64(0xFFFFFFFF)).astype(np.int64), -1)
-    # op stream: each op is a read; written keys also get a write micro-op
-    ops_txn = np.concatenate([txn, txn[w]])
-    ops_key = np.concatenate([key, key[w]])
-    ops_w = np.concatenate([np.zeros(n, np.uint8), np.ones(int(w.sum()), np.uint8)])
-    ops_obs = np.concatenate([observed, np.full(int(w.sum()), -1, np.int64)])
-    order = np.argsort(ops_txn, kind="stable")
-    return History(ops_txn[order], ops_key[order], ops_w[order], ops_obs[order], n_txn)
+    # op stream: each op is a read; written keys also get a write micro-op.
+    # Per txn: its ops_per_txn reads, then its writes (in op order) -- placed
+    # directly (the order of a stable sort by txn).
+    P = ops_per_txn
+    nw_t = w.reshape(n_txn, P).sum(axis=1)
+    start = np.cumsum(P + nw_t) - (P + nw_t)
+    pos_r = (np.repeat(start, P) + np.tile(np.arange(P), n_txn)).astype(np.int64)
+    wi = np.nonzero(w)[0]
+    wt = wi // P
+    wk = np.arange(len(wi)) - (np.cumsum(nw_t) - nw_t)[wt]
+    pos_w = start[wt] + P + wk
+    m = n + len(wi)
+    o_txn = np.empty(m, np.uint32)
+    o_key = np.empty(m, np.uint64)
+    o_w = np.empty(m, np.uint8)
+    o_obs = np.empty(m, np.int64)
+    o_txn[pos_r], o_key[pos_r], o_w[pos_r], o_obs[pos_r] = txn, key, 0, observed
+    o_txn[pos_w], o_key[pos_w], o_w[pos_w], o_obs[pos_w] = txn[wi], key[wi], 1, -1
+    return History(o_txn, o_key, o_w, o_obs, n_txn)
 
 
 def history_to_edn(h: History, limit: Optional[int] = None) -> str:

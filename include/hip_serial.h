@@ -398,13 +398,49 @@ typedef struct hsc_graph_stats {
     uint32_t txns_in_cycles;
     uint32_t rounds, iterations;  /* colouring rounds / frontier steps         */
     float build_ms, scc_ms;       /* device time                               */
+    uint32_t cut_nodes;           /* hsc_dep_graph_scc_cut: nodes of the cover */
 } hsc_graph_stats;
 
 int hsc_dep_graph_scc(hsc_ctx *ctx, const hsc_history *h, uint32_t *scc_out,
                       hsc_graph_stats *stats);
-/* Edges of the last graph, sorted by (src, dst): copies min(cap, n). */
+/* Edges of the last full build, sorted by (src, dst): copies min(cap, n)
+ * (n = 0 after a raw build). */
 int hsc_dep_graph_edges(hsc_ctx *ctx, uint32_t *src, uint32_t *dst, uint32_t *type,
                         size_t cap, size_t *n);
+
+/* Sharded SCC (config 4 over N GPUs).  Every WW/WR/RW edge belongs to one
+ * key, so a history split by key gives each shard an exact part of the edge
+ * set.  Txn ids are commit order; a cycle always contains a backward edge
+ * (src > dst) and all its nodes lie inside [dst, src] of its backward edges,
+ * so components of >= 2 txns live in the graph induced on the "cover" (the
+ * nodes inside some backward edge's interval).  Per shard: build, cover
+ * (u8 per txn, merged over shards with a MAX all-reduce), cut (the shard's
+ * edges between covered nodes, exchanged with an all-gather), then the SCC of
+ * the union of the cuts -- the same scc[] as hsc_dep_graph_scc of the whole
+ * history.  Pointers named *_dev are device memory of the context's GPU. */
+/* flags: HSC_GRAPH_FULL = sorted unique edges with types and CSR / CSC (what
+ * hsc_dep_graph_edges returns, stats.edges/ww/wr/rw filled); 0 = the raw edge
+ * rows only (duplicates, no sort: all cover / cut need; stats.build_ms only). */
+#define HSC_GRAPH_FULL 1
+int hsc_dep_graph_build(hsc_ctx *ctx, const hsc_history *h, int flags, hsc_graph_stats *stats);
+/* The same from device-resident ops (observed: writer txn, 0xFFFFFFFF =
+ * initial version); ops naming a txn >= ntxn -> HSC_EINVAL. */
+int hsc_dep_graph_build_device(hsc_ctx *ctx, size_t nops, uint32_t ntxn, const uint32_t *txn_dev,
+                               const uint64_t *key_dev, const uint8_t *is_write_dev,
+                               const uint32_t *observed_dev, int flags, hsc_graph_stats *stats);
+/* cover_dev[ntxn of the last build] := 1 inside a backward edge's interval. */
+int hsc_dep_graph_cover(hsc_ctx *ctx, uint8_t *cover_dev);
+/* Edges of the last build with both ends covered, as rows src << 32 | dst
+ * (sorted): *m of them, min(cap, *m) copied to rows_dev (NULL: count only). */
+int hsc_dep_graph_cut(hsc_ctx *ctx, const uint8_t *cover_dev, uint64_t *rows_dev, size_t cap,
+                      size_t *m);
+/* scc_dev[ntxn] := largest txn of each txn's component in the graph whose
+ * only edges between covered nodes are rows_dev[m] (~0 rows are padding);
+ * uncovered txns are their own component.  HSC_EINVAL if a row leaves the
+ * cover.  Leaves the last build's edges in place (own buffers). */
+int hsc_dep_graph_scc_cut(hsc_ctx *ctx, uint32_t ntxn, const uint8_t *cover_dev,
+                          const uint64_t *rows_dev, size_t m, uint32_t *scc_dev,
+                          hsc_graph_stats *stats);
 
 #ifdef __cplusplus
 }
