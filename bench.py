@@ -228,7 +228,7 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm):
             "k_join_t": 8 * n_keys + 16 * recs,
             "k_pack_flags": 2 * T + (T + 7) // 8,
         }
-    else:  # wide tiles: key words + lsn + gid per row
+    else:  # wide tiles (compact: W = code words): key words + lsn + gid per row
         own = {
             "k_locate": n_r * (4 + 8 + 16 * W) + 8 * n_r,
             "k_plan": 0,
@@ -457,6 +457,16 @@ def main():
     Lhat = 8 * W
     s_w, s_r = Lhat + 12, 2 * Lhat + 16
     B = n_keys * s_w + n_r * s_r + (T + 7) // 8
+    if args.config == 3:  # per group L^ = 8 ceil(L / 8): window keys and ranges of each group
+        lhat = np.array([8 * ((L + 7) // 8) for (_, _, L) in c3.groups], np.int64)
+        keys_g = np.zeros(len(c3.groups), np.int64)
+        for g in mine:
+            kb = c3.keys_of[g][np.unique(c3.w_row[c3.w_group == g])]
+            keys_g[g] = len(np.unique(np.ascontiguousarray(kb).view(np.dtype((np.void, kb.shape[1])))))
+        host = lambda x: x.cpu().numpy() if hasattr(x, "cpu") else np.asarray(x)
+        rng_g = np.mean([np.bincount(host(b["gid"]), minlength=len(c3.groups)) for b in batches],
+                        axis=0)
+        B = int((keys_g * (lhat + 12)).sum() + (rng_g * (2 * lhat + 16)).sum() + (T + 7) // 8)
     ms_step = elapsed / args.steps * 1e3
     traffic = None
     if os.path.exists(args.traffic):
@@ -464,7 +474,7 @@ def main():
             traffic = json.load(open(args.traffic)).get("probe_hbm_bytes_per_step")
         except (OSError, ValueError):
             traffic = None
-    kern = kernel_bytes(v.layout, W, n_keys, n_r, T, tm)
+    kern = kernel_bytes(v.layout, v.code_words, n_keys, n_r, T, tm)
     ms_per_step = elapsed / args.steps * 1e3
     checks = T * args.steps
     out = {
@@ -490,6 +500,8 @@ def main():
             "streams": S,
             "serial_ms_per_step": serial_elapsed / args.steps * 1e3,
             "window_layout": {hsc.LAYOUT_NARROW: "narrow (u32 tile-relative keys)",
+                              hsc.LAYOUT_COMPACT: f"compact ({v.code_words}-word codes of "
+                                                  f"{W}-word keys)",
                               hsc.LAYOUT_WIDE: "wide"}.get(v.layout, "?"),
             "conflict_rate": float((v0 != 0).mean()),
         },

@@ -1,0 +1,317 @@
+// hsc_compact.hip -- compact codes for wide windows (composite keys, config 3).
+//
+// Within one (table, index, key length) group every window row agrees with
+// the group's first row on most key bits (constant field bytes, the 0x08
+// field headers, the unused bits of small integers, the zero padding of
+// short strings).  Dropping the bit positions that never vary inside a
+// group keeps the memcmp order of its rows (the order is decided by the
+// first differing bit, which is always a varying one), so each row becomes a
+// shorter code: bits_g varying bits, most significant first, left-aligned in
+// WC = floor(max bits_g / 64) + 1 words (at least one spare bit: all-ones is
+// above every code).  Config 3's 9..58-byte keys (W = 8 words) become WC = 3.
+//
+// A probe bound X (W words, padded per the reference's min-length memcmp:
+// 0x00 for lo, 0xFF for hi) maps exactly onto the codes.  Let p be the first
+// constant position where X differs from the group pattern C, and prefix =
+// X's varying bits before p (np of them).  For every row r: if r's first np
+// code bits differ from prefix they decide; if equal, r agrees with X up to
+// p and bit p decides: r < X iff X_p = 1.  Hence
+//   #rows < X  = #codes < lo'   lo' = code(X) (no p), prefix+1 then 0s
+//                               (X_p = 1; overflow: X above every row),
+//                               prefix then 0s (X_p = 0)
+//   #rows <= X = #codes <= hi'  hi' = code(X) (no p), prefix then 1s (X_p =
+//                               1), prefix-1 then 1s (X_p = 0; prefix = 0:
+//                               X below every row)
+// A range whose lo is above every row or whose hi is below every row (or
+// whose group has no rows) matches nothing and becomes (lo' = ~0, hi' = 0).
+// The window's row order, group spans, dedupe and LSNs are unchanged, so the
+// wide tile pipeline (hsc_kernels.hip) runs on the codes as it does on keys.
+//
+// Bits are gathered with Hacker's Delight's parallel-suffix compress; its
+// six move masks per (group, word) depend only on the mask and are built on
+// the host (compact_tables).
+#include "hsc_device.h"
+#include "hsc_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+namespace hsc {
+
+namespace {
+
+__device__ __forceinline__ uint64_t compress(uint64_t x, uint64_t m, const uint64_t *mv)
+{
+    x &= m;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const uint64_t t = x & mv[i];
+        x = (x ^ t) | (t >> (1 << i));
+    }
+    return x;
+}
+
+// append the c low bits of v at bit position pos (MSB-first) of out[WC]
+template <int WC>
+__device__ __forceinline__ void put_bits(uint64_t (&out)[WC], int pos, uint64_t v, int c)
+{
+    if (c == 0) return;
+    const int w = pos >> 6, off = pos & 63;
+    if (off + c <= 64) {
+        const int sh = 64 - off - c;
+#pragma unroll
+        for (int k = 0; k < WC; ++k)
+            if (k == w) out[k] |= v << sh;
+    } else {
+        const int hi = off + c - 64;  // bits spilling into word w + 1
+#pragma unroll
+        for (int k = 0; k < WC; ++k) {
+            if (k == w) out[k] |= v >> hi;
+            if (k == w + 1) out[k] |= v << (64 - hi);
+        }
+    }
+}
+
+// add (+1) or subtract (-1) one unit at bit position pos (MSB-first) of the
+// WC-word big number; returns true on carry / borrow out of the top
+template <int WC>
+__device__ __forceinline__ bool step_at(uint64_t (&out)[WC], int pos, int dir)
+{
+    const int w = pos >> 6;
+    uint64_t unit = 1ull << (63 - (pos & 63));
+    bool carry = false;
+#pragma unroll
+    for (int k = WC - 1; k >= 0; --k) {
+        if (k > w) continue;
+        if (k < w && !carry) break;
+        const uint64_t add = k == w ? unit : 1ull;
+        if (dir > 0) {
+            const uint64_t r = out[k] + add;
+            carry = r < out[k];
+            out[k] = r;
+        } else {
+            carry = out[k] < add;
+            out[k] -= add;
+        }
+        if (!carry) break;
+    }
+    return carry;
+}
+
+// set bits [from, to) (MSB-first) to one
+template <int WC>
+__device__ __forceinline__ void fill_ones(uint64_t (&out)[WC], int from, int to)
+{
+#pragma unroll
+    for (int k = 0; k < WC; ++k) {
+        const int a = max(from, 64 * k), b = min(to, 64 * k + 64);
+        if (a >= b) continue;
+        const int lo = a - 64 * k, n = b - a;  // bits lo..lo+n-1 of word k from its MSB
+        const uint64_t ones = n == 64 ? ~0ull : ((1ull << n) - 1) << (64 - lo - n);
+        out[k] |= ones;
+    }
+}
+
+struct CompactMeta {
+    const uint64_t *mask, *pat, *mv;  // [ng][W], [ng][W], [ng][W][6]
+    const uint32_t *bits;             // [ng]: varying bits, kNoRows = group has no rows
+    int W;
+};
+constexpr uint32_t kNoRows = 0xFFFFFFFFu;
+
+// code of X in group g; kind 0 = exact row, 1 = lo bound, 2 = hi bound.
+// Returns false if the bound puts the range outside the group's rows.
+template <int WC>
+__device__ bool code_of(const CompactMeta &cm, uint32_t g, const uint64_t *x, size_t xs, int kind,
+                        uint64_t (&out)[WC])
+{
+#pragma unroll
+    for (int k = 0; k < WC; ++k) out[k] = 0;
+    const uint32_t bits = cm.bits[g];
+    if (bits == kNoRows) return false;
+    const uint64_t *mk = cm.mask + (size_t)g * cm.W, *pt = cm.pat + (size_t)g * cm.W;
+    const uint64_t *mv = cm.mv + (size_t)g * cm.W * 6;
+    int pos = 0, np = -1, xb = 0;
+    for (int j = 0; j < cm.W; ++j) {
+        const uint64_t m = mk[j];
+        const int c = __popcll(m);
+        if (np < 0) {
+            const uint64_t xj = x[(size_t)j * xs];
+            const uint64_t d = kind ? (xj ^ pt[j]) & ~m : 0;
+            if (d) {
+                const int b = 63 - __clzll(d);
+                const uint64_t above = b == 63 ? 0 : ~0ull << (b + 1);
+                put_bits(out, pos, compress(xj & above, m, mv + 6 * j), c);
+                np = pos + __popcll(m & above);
+                xb = (int)((xj >> b) & 1);
+            } else {
+                put_bits(out, pos, compress(xj, m, mv + 6 * j), c);
+            }
+        }
+        pos += c;
+    }
+    if (np < 0) return true;  // X agrees with the pattern: its code is exact
+    if (kind == 1) {
+        if (xb && (np == 0 || step_at(out, np - 1, +1))) return false;  // above every row
+        return true;
+    }
+    if (!xb) {
+        if (np == 0) return false;
+        bool zero = true;
+#pragma unroll
+        for (int k = 0; k < WC; ++k) zero &= out[k] == 0;
+        if (zero) return false;  // below every row
+        step_at(out, np - 1, -1);
+    }
+    fill_ones(out, np, (int)bits);
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_group_vary(const uint64_t *words, size_t stride,
+                                                    const uint32_t *gid, uint32_t n, int W,
+                                                    const uint32_t *gstart, uint64_t *mask)
+{
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool ok = i0 < n;
+    const uint32_t i = ok ? i0 : n - 1;
+    const uint32_t g = gid[i];
+    const uint32_t g0 = __shfl(g, 0);
+    const bool uniform = __all(g == g0);
+    const uint32_t f = gstart[g];
+    for (int j = 0; j < W; ++j) {
+        uint64_t x = ok ? words[(size_t)j * stride + i] ^ words[(size_t)j * stride + f] : 0;
+        if (uniform) {
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o);
+            if (lane_id() == 0 && x) atomicOr((unsigned long long *)&mask[(size_t)g * W + j], x);
+        } else if (x) {
+            atomicOr((unsigned long long *)&mask[(size_t)g * W + j], x);
+        }
+    }
+}
+
+__global__ void k_group_pattern(const uint64_t *words, size_t stride, int W, int ng,
+                                const uint32_t *gstart, const uint32_t *gend, uint64_t *pat)
+{
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ng) return;
+    const bool rows = gend[g] > gstart[g];
+    for (int j = 0; j < W; ++j) pat[(size_t)g * W + j] = rows ? words[(size_t)j * stride + gstart[g]] : 0;
+}
+
+template <int WC>
+__global__ __launch_bounds__(256) void k_compact_rows(const uint64_t *words, size_t stride,
+                                                      const uint32_t *gid, uint32_t n,
+                                                      CompactMeta cm, uint64_t *cw)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t out[WC];
+    code_of<WC>(cm, gid[i], words + i, stride, 0, out);
+#pragma unroll
+    for (int k = 0; k < WC; ++k) cw[(size_t)k * stride + i] = out[k];
+}
+
+template <int WC>
+__global__ __launch_bounds__(256) void k_compact_probes(ProbeView p, CompactMeta cm, uint64_t *clo,
+                                                        uint64_t *chi)
+{
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= p.n) return;
+    const uint32_t g = p.gid[q];
+    uint64_t lo[WC], hi[WC];
+    bool ok = code_of<WC>(cm, g, p.lo + q, p.n, 1, lo);
+    ok = ok && code_of<WC>(cm, g, p.hi + q, p.n, 2, hi);
+#pragma unroll
+    for (int k = 0; k < WC; ++k) {
+        clo[(size_t)k * p.n + q] = ok ? lo[k] : ~0ull;
+        chi[(size_t)k * p.n + q] = ok ? hi[k] : 0;
+    }
+}
+
+template <int WC>
+hipError_t launch_rows_wc(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
+                          const CompactMeta &cm, uint64_t *cw, hipStream_t s)
+{
+    k_compact_rows<WC><<<(n + 255) / 256, 256, 0, s>>>(words, stride, gid, n, cm, cw);
+    return hipGetLastError();
+}
+
+template <int WC>
+hipError_t launch_probes_wc(const ProbeView &p, const CompactMeta &cm, uint64_t *clo,
+                            uint64_t *chi, hipStream_t s)
+{
+    k_compact_probes<WC><<<(p.n + 255) / 256, 256, 0, s>>>(p, cm, clo, chi);
+    return hipGetLastError();
+}
+
+CompactMeta meta_of(const CompactTables &t)
+{
+    return CompactMeta{t.mask, t.pat, t.mv, t.bits, t.W};
+}
+
+}  // namespace
+
+// Hacker's Delight compress move masks of m (host).
+void compress_moves(uint64_t m, uint64_t mv[6])
+{
+    uint64_t mk = ~m << 1;
+    for (int i = 0; i < 6; ++i) {
+        uint64_t mp = mk ^ (mk << 1);
+        mp ^= mp << 2;
+        mp ^= mp << 4;
+        mp ^= mp << 8;
+        mp ^= mp << 16;
+        mp ^= mp << 32;
+        const uint64_t v = mp & m;
+        mv[i] = v;
+        m = (m ^ v) | (v >> (1 << i));
+        mk &= ~mp;
+    }
+}
+
+hipError_t compact_masks(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
+                         int W, int ng, const uint32_t *gstart, const uint32_t *gend,
+                         uint64_t *mask, uint64_t *pat, hipStream_t s)
+{
+    hipError_t e = hipMemsetAsync(mask, 0, 8 * (size_t)ng * W, s);
+    if (e != hipSuccess) return e;
+    if (n) k_group_vary<<<(n + 255) / 256, 256, 0, s>>>(words, stride, gid, n, W, gstart, mask);
+    if (ng) k_group_pattern<<<(ng + 63) / 64, 64, 0, s>>>(words, stride, W, ng, gstart, gend, pat);
+    return hipGetLastError();
+}
+
+hipError_t compact_rows(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
+                        const CompactTables &t, uint64_t *cw, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    const CompactMeta cm = meta_of(t);
+    switch (t.WC) {
+    case 1: return launch_rows_wc<1>(words, stride, gid, n, cm, cw, s);
+    case 2: return launch_rows_wc<2>(words, stride, gid, n, cm, cw, s);
+    case 3: return launch_rows_wc<3>(words, stride, gid, n, cm, cw, s);
+    case 4: return launch_rows_wc<4>(words, stride, gid, n, cm, cw, s);
+    case 5: return launch_rows_wc<5>(words, stride, gid, n, cm, cw, s);
+    case 6: return launch_rows_wc<6>(words, stride, gid, n, cm, cw, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t compact_probes(const ProbeView &p, const CompactTables &t, uint64_t *clo, uint64_t *chi,
+                          hipStream_t s)
+{
+    if (p.n == 0) return hipSuccess;
+    const CompactMeta cm = meta_of(t);
+    switch (t.WC) {
+    case 1: return launch_probes_wc<1>(p, cm, clo, chi, s);
+    case 2: return launch_probes_wc<2>(p, cm, clo, chi, s);
+    case 3: return launch_probes_wc<3>(p, cm, clo, chi, s);
+    case 4: return launch_probes_wc<4>(p, cm, clo, chi, s);
+    case 5: return launch_probes_wc<5>(p, cm, clo, chi, s);
+    case 6: return launch_probes_wc<6>(p, cm, clo, chi, s);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace hsc

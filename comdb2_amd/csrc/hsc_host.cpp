@@ -96,6 +96,11 @@ struct hsc_ctx {
     DBuf w_tcode, w_tcode2, w_trecs;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
     DBuf d_gstart, d_gend, d_tmax, d_table_max, d_group_table, d_count, d_sp_g, d_sp_w;
+    // compact codes of a wide window (hsc_compact.hip): WinView wc over them
+    bool compact = false;
+    CompactTables ct{};
+    WinView wc{};
+    DBuf d_cmask, d_cpat, d_cmv, d_cbits, d_cwords, d_ctmax, d_csp_g, d_csp_w;
 
     // probe workspace
     DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;
@@ -353,6 +358,73 @@ static int build_commits(hsc_ctx *c, size_t n_in)
     return HSC_OK;
 }
 
+// Compact codes of the (wide) window w: per-group varying masks, code width
+// WC; if WC < W the codes and their tile summaries become the probe view.
+static int build_compact(hsc_ctx *c, const WinView &w)
+{
+    hipStream_t s = c->stream;
+    const int W = c->W, ng = (int)c->groups.size();
+    const size_t gw = (size_t)ng * W;
+    HIPCHK(c, c->d_cmask.ensure(8 * gw));
+    HIPCHK(c, c->d_cpat.ensure(8 * gw));
+    HIPCHK(c, compact_masks(w.words, w.stride, w.gid, w.n, W, ng, c->d_gstart.as<uint32_t>(),
+                            c->d_gend.as<uint32_t>(), c->d_cmask.as<uint64_t>(),
+                            c->d_cpat.as<uint64_t>(), s));
+    std::vector<uint64_t> mask(gw);
+    std::vector<uint32_t> gs(ng), ge(ng);
+    HIPCHK(c, hipMemcpyAsync(mask.data(), c->d_cmask.p, 8 * gw, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(gs.data(), c->d_gstart.p, 4 * (size_t)ng, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(ge.data(), c->d_gend.p, 4 * (size_t)ng, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    std::vector<uint32_t> bits(ng);
+    std::vector<uint64_t> mv(gw * 6);
+    int maxbits = 0;
+    for (int g = 0; g < ng; ++g) {
+        if (ge[g] <= gs[g]) {
+            bits[g] = 0xFFFFFFFFu;
+            continue;
+        }
+        int b = 0;
+        for (int j = 0; j < W; ++j) {
+            b += __builtin_popcountll(mask[(size_t)g * W + j]);
+            compress_moves(mask[(size_t)g * W + j], &mv[((size_t)g * W + j) * 6]);
+        }
+        bits[g] = (uint32_t)b;
+        maxbits = std::max(maxbits, b);
+    }
+    const int WC = maxbits / 64 + 1;  // >= 1 spare bit: all-ones is above every code
+    if (WC >= W || WC > kMaxCompactWords) return HSC_OK;
+    HIPCHK(c, c->d_cmv.ensure(8 * gw * 6));
+    HIPCHK(c, c->d_cbits.ensure(4 * (size_t)ng));
+    HIPCHK(c, hipMemcpyAsync(c->d_cmv.p, mv.data(), 8 * gw * 6, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_cbits.p, bits.data(), 4 * (size_t)ng, hipMemcpyHostToDevice, s));
+    c->ct = CompactTables{c->d_cmask.as<uint64_t>(), c->d_cpat.as<uint64_t>(), c->d_cmv.as<uint64_t>(),
+                          c->d_cbits.as<uint32_t>(), W, WC};
+    HIPCHK(c, c->d_cwords.ensure(8 * (size_t)WC * c->cap));
+    HIPCHK(c, compact_rows(w.words, w.stride, w.gid, w.n, c->ct, c->d_cwords.as<uint64_t>(), s));
+    WinView &v = c->wc;
+    v = w;
+    v.words = c->d_cwords.as<uint64_t>();
+    v.W = WC;
+    v.log2T = tile_log2(WC);
+    v.ntiles = (uint32_t)((c->n + ((size_t)1 << v.log2T) - 1) >> v.log2T);
+    v.levels = 0;
+    while (((size_t)1 << v.levels) <= v.ntiles) v.levels++;
+    HIPCHK(c, c->d_ctmax.ensure(8 * (size_t)std::max(1, v.levels) * std::max<uint32_t>(1, v.ntiles)));
+    HIPCHK(c, c->d_csp_g.ensure(4 * (size_t)std::max<uint32_t>(1, v.ntiles)));
+    HIPCHK(c, c->d_csp_w.ensure(8 * (size_t)WC * std::max<uint32_t>(1, v.ntiles)));
+    v.tmax = c->d_ctmax.as<uint64_t>();
+    v.sp_g = c->d_csp_g.as<uint32_t>();
+    v.sp_w = c->d_csp_w.as<uint64_t>();
+    HIPCHK(c, build_summaries(v, c->d_gstart.as<uint32_t>(), c->d_gend.as<uint32_t>(), ng,
+                              c->d_ctmax.as<uint64_t>(), nullptr, nullptr, c->d_csp_g.as<uint32_t>(),
+                              c->d_csp_w.as<uint64_t>(), s));
+    v.gstart = c->d_gstart.as<uint32_t>();
+    v.gend = c->d_gend.as<uint32_t>();
+    c->compact = true;
+    return HSC_OK;
+}
+
 static int device_build(hsc_ctx *c, size_t n_in)
 {
     HIPCHK(c, wait_lanes(c));
@@ -459,6 +531,9 @@ static int device_build(hsc_ctx *c, size_t n_in)
                               c->d_tmax.as<uint64_t>(), c->d_group_table.as<uint32_t>(),
                               c->d_table_max.as<uint64_t>(), c->d_sp_g.as<uint32_t>(),
                               c->d_sp_w.as<uint64_t>(), s));
+    c->compact = false;
+    if (!c->narrow && c->layout == HSC_LAYOUT_AUTO && c->n > 0 && W > 1 && ng > 0)
+        HIPCHK_RC(c, build_compact(c, w));
     if (c->narrow) {
         // level sizes: level 0 = n + 1 rounded up to whole tiles (at least one
         // pad; the tile pipeline stages whole tiles), then roundup16(len / 16)
@@ -939,7 +1014,8 @@ static int probe_narrow(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w,
     return HSC_OK;
 }
 
-static int probe_tiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w, const ProbeView &p);
+static int probe_tiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w, const ProbeView &p,
+                       bool started = false);
 
 // Narrow tiles (dense batch): locate (codes, snapshot ranks, per-chunk tile
 // histograms) -> column scan + plan -> scatter (16-byte records) -> join
@@ -1043,6 +1119,27 @@ static int probe_lane(hsc_ctx *c, const hsc_probe_batch *b)
     p.lock_txn = b->lock_txn;
     p.n = w.n ? (uint32_t)b->n : 0;  // empty key window: no range can match
     p.n_lock = (uint32_t)b->n_lock;
+    if (!c->narrow && c->compact) {
+        // wide keys as compact codes: map the bounds, then the tile pipeline
+        const int WC = c->ct.WC;
+        const size_t n = std::max<uint32_t>(p.n, 1);
+        HIPCHK(c, c->p_code_lo.ensure(8 * (size_t)WC * n));
+        HIPCHK(c, c->p_code_hi.ensure(8 * (size_t)WC * n));
+        if (c->timing) {
+            if (!c->ev[0]) HIPCHK(c, hipEventCreate(&c->ev[0]));
+            HIPCHK(c, hipEventRecord(c->ev[0], c->stream));
+        }
+        HIPCHK(c, compact_probes(p, c->ct, c->p_code_lo.as<uint64_t>(), c->p_code_hi.as<uint64_t>(),
+                                 c->stream));
+        ProbeView pc = p;
+        pc.lo = c->p_code_lo.as<uint64_t>();
+        pc.hi = c->p_code_hi.as<uint64_t>();
+        WinView wc = c->wc;
+        wc.table_max = w.table_max;
+        wc.ntables = w.ntables;
+        wc.gbits = w.gbits;
+        return probe_tiles(c, b, wc, pc, c->timing);
+    }
     if (!c->narrow) return probe_tiles(c, b, w, p);
     // narrow window: a sparse batch is answered by the direct probe; a dense
     // one maps its bounds to codes and runs the tile pipeline on the codes
@@ -1078,7 +1175,10 @@ static int probe_lane(hsc_ctx *c, const hsc_probe_batch *b)
 }
 
 // The tile pipeline: locate -> plan -> scatter -> join -> pack.
-static int probe_tiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w, const ProbeView &p)
+// started: ev[0] was recorded by the caller (a bound transform before locate
+// counts as locate time).
+static int probe_tiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w, const ProbeView &p,
+                       bool started)
 {
     hipStream_t s = c->stream;
     c->probe_ntiles = w.ntiles;
@@ -1111,7 +1211,7 @@ static int probe_tiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w, c
     if (tm)
         for (int i = 0; i < 6; ++i)
             if (!c->ev[i]) HIPCHK(c, hipEventCreate(&c->ev[i]));
-    if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
+    if (tm && !started) HIPCHK(c, hipEventRecord(c->ev[0], s));
     if (b->n_txn) HIPCHK(c, hipMemsetAsync(b->verdict, 0, b->n_txn, s));
     if (!work.lds_mode) HIPCHK(c, hipMemsetAsync(c->w_counts.p, 0, 4 * ((size_t)nt + 1), s));
     HIPCHK(c, launch_locate(w, p, work, b->verdict, s));
@@ -1446,7 +1546,13 @@ int hsc_set_layout(hsc_ctx *c, int layout)
     return HSC_OK;
 }
 
-int hsc_window_layout(hsc_ctx *c) { return c && c->narrow ? HSC_LAYOUT_NARROW : HSC_LAYOUT_WIDE; }
+int hsc_window_layout(hsc_ctx *c)
+{
+    if (!c) return HSC_LAYOUT_WIDE;
+    return c->narrow ? HSC_LAYOUT_NARROW : c->compact ? HSC_LAYOUT_COMPACT : HSC_LAYOUT_WIDE;
+}
+
+int hsc_window_code_words(hsc_ctx *c) { return c && c->compact ? c->ct.WC : c ? c->W : 0; }
 
 int hsc_window_words(hsc_ctx *c) { return c ? c->W : 0; }
 size_t hsc_window_keys(hsc_ctx *c) { return c ? c->n : 0; }

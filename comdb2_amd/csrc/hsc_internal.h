@@ -308,6 +308,24 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
 hipError_t graph_type_counts(GraphBufs &g, uint64_t out[3], hipStream_t s);
 hipError_t graph_scc(uint32_t nnodes, GraphBufs &g, uint32_t *rounds, uint32_t *iterations,
                      hipStream_t s);
+// Compact codes of wide windows (hsc_compact.hip): per group the key bits
+// that vary between its rows, most significant first, in WC words.
+struct CompactTables {
+    const uint64_t *mask, *pat, *mv;  // [ng][W] varying bits, first row, compress moves [ng][W][6]
+    const uint32_t *bits;             // [ng] varying bits (0xFFFFFFFF: no rows)
+    int W, WC;
+};
+constexpr int kMaxCompactWords = 6;
+void compress_moves(uint64_t m, uint64_t mv[6]);
+hipError_t compact_masks(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
+                         int W, int ng, const uint32_t *gstart, const uint32_t *gend,
+                         uint64_t *mask, uint64_t *pat, hipStream_t s);
+hipError_t compact_rows(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
+                        const CompactTables &t, uint64_t *cw, hipStream_t s);
+// lo/hi bounds (W words) -> code bounds (WC words, SoA [WC][n]); ranges that
+// miss their group's rows become (~0, 0)
+hipError_t compact_probes(const ProbeView &p, const CompactTables &t, uint64_t *clo, uint64_t *chi,
+                          hipStream_t s);
 // Sharded SCC (hsc_graph.hip): cover[v] = 1 iff v lies inside [dst, src] of a
 // backward edge of g; the edges of g between covered nodes -> g.cut rows
 // (src << 32 | dst, *m of them); SCC of the graph induced on the cover by

@@ -123,11 +123,11 @@ EXPORTS = [
     "hsc_enable_timing", "hsc_dep_graph_scc", "hsc_dep_graph_edges",
     "hsc_window_ingest_raw", "hsc_decode_log", "hsc_decode_serial", "hsc_check_serial",
     "hsc_set_layout", "hsc_window_layout", "hsc_coalesce_readsets", "hsc_rw_edges",
-    "hsc_dep_graph_build", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
+    "hsc_window_code_words", "hsc_dep_graph_build", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
 ]
 
 (LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES,
- LAYOUT_NARROW_CODES) = 0, 1, 2, 3, 4, 5
+ LAYOUT_NARROW_CODES, LAYOUT_COMPACT) = 0, 1, 2, 3, 4, 5, 6
 
 _lib: Optional[C.CDLL] = None
 
@@ -156,6 +156,7 @@ def load() -> C.CDLL:
         "hsc_register_group": (C.c_int, [_p, C.c_char_p, C.c_int, C.c_int]),
         "hsc_window_ingest_device": (C.c_int, [_p, C.c_size_t, C.c_int, _p, _p, _p, C.c_uint64]),
         "hsc_window_words": (C.c_int, [_p]),
+        "hsc_window_code_words": (C.c_int, [_p]),
         "hsc_window_keys": (C.c_size_t, [_p]),
         "hsc_window_end": (C.c_uint64, [_p]),
         "hsc_window_max_commit": (C.c_uint64, [_p]),
@@ -431,8 +432,13 @@ class Validator:
 
     @property
     def layout(self) -> int:
-        """LAYOUT_NARROW or LAYOUT_WIDE: the layout of the current window."""
+        """LAYOUT_NARROW, LAYOUT_COMPACT or LAYOUT_WIDE: the current window's."""
         return self.lib.hsc_window_layout(self.ctx)
+
+    @property
+    def code_words(self) -> int:
+        """Words per probed window row (compact codes: WC < words)."""
+        return self.lib.hsc_window_code_words(self.ctx)
 
     @property
     def keys(self) -> int:

@@ -269,18 +269,23 @@ int hsc_window_ingest_device(hsc_ctx *ctx, size_t n, int words,
  * 8-byte rows where they fit; codes: always 16-byte code rows) -- testing.  Verdicts are
  * identical; a change between WIDE and the others applies at the next window
  * build (host-staged windows rebuild; a device-ingested window returns
- * HSC_ESTATE and must be re-ingested).  hsc_window_layout reports WIDE or
- * NARROW. */
+ * HSC_ESTATE and must be re-ingested).  hsc_window_layout reports WIDE,
+ * NARROW or COMPACT (AUTO on a window too wide for 62-bit codes: each
+ * (table, index, key length) group's keys keep only the bits that vary inside
+ * the group -- hsc_compact.hip -- when that shortens the rows; WIDE disables
+ * it). */
 enum {
     HSC_LAYOUT_AUTO = 0,
     HSC_LAYOUT_WIDE = 1,
     HSC_LAYOUT_NARROW = 2,
     HSC_LAYOUT_NARROW_DIRECT = 3,
     HSC_LAYOUT_NARROW_TILES = 4,
-    HSC_LAYOUT_NARROW_CODES = 5
+    HSC_LAYOUT_NARROW_CODES = 5,
+    HSC_LAYOUT_COMPACT = 6  /* reported only: AUTO's wide window as per-group compact codes */
 };
 int hsc_set_layout(hsc_ctx *ctx, int layout);
-int hsc_window_layout(hsc_ctx *ctx);         /* HSC_LAYOUT_WIDE or _NARROW   */
+int hsc_window_layout(hsc_ctx *ctx);         /* HSC_LAYOUT_WIDE, _NARROW or _COMPACT */
+int hsc_window_code_words(hsc_ctx *ctx);     /* words per probed row (compact: WC) */
 int hsc_window_words(hsc_ctx *ctx);          /* key words per key (>= 1)     */
 size_t hsc_window_keys(hsc_ctx *ctx);        /* distinct (group, key) rows   */
 uint64_t hsc_window_end(hsc_ctx *ctx);
