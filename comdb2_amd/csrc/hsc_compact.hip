@@ -35,6 +35,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <vector>
 
 namespace hsc {
@@ -116,7 +117,7 @@ __device__ __forceinline__ void fill_ones(uint64_t (&out)[WC], int from, int to)
 struct CompactMeta {
     const uint64_t *mask, *pat, *mv;  // [ng][W], [ng][W], [ng][W][6]
     const uint32_t *bits;             // [ng]: varying bits, kNoRows = group has no rows
-    int W;
+    int W, ng;
 };
 constexpr uint32_t kNoRows = 0xFFFFFFFFu;
 
@@ -230,6 +231,191 @@ __global__ __launch_bounds__(256) void k_compact_probes(ProbeView p, CompactMeta
     }
 }
 
+// ---- probe bounds, keys of at most kProbeWords words ----
+// The same mapping as code_of, for lo and hi of one probe in one pass over
+// the group's masks, with every operand in registers: the key words are all
+// loaded first, each word's compressed bits are shifted into a right-aligned
+// accumulator (no indexing of the code by a run-time word number, which
+// would put it in scratch), and the code is left-aligned at the end.
+constexpr int kProbeWords = 8;
+
+// a = a << c | v (0 <= c <= 64, v < 2^c) over a WC-word big number
+template <int WC>
+__device__ __forceinline__ void acc_push(uint64_t (&a)[WC], uint64_t v, int c)
+{
+#pragma unroll
+    for (int k = 0; k < WC - 1; ++k) {
+        const uint64_t hi = c >= 64 ? 0 : a[k] << c;
+        const uint64_t lo = c == 0 ? 0 : a[k + 1] >> (64 - c);
+        a[k] = hi | lo;
+    }
+    a[WC - 1] = (c >= 64 ? 0 : a[WC - 1] << c) | v;
+}
+
+// left-align the low `bits` bits of a (bits <= 64 WC)
+template <int WC>
+__device__ __forceinline__ void acc_align(uint64_t (&a)[WC], int bits)
+{
+    const int s = 64 * WC - bits, ws = s >> 6, bs = s & 63;
+    uint64_t t[WC];
+#pragma unroll
+    for (int k = 0; k < WC; ++k) {
+        uint64_t v = 0;
+#pragma unroll
+        for (int m = k; m < WC; ++m) v = m == k + ws ? a[m] : v;
+        t[k] = v;
+    }
+    acc_push<WC>(t, 0, bs);
+#pragma unroll
+    for (int k = 0; k < WC; ++k) a[k] = t[k];
+}
+
+// +- one unit at bit pos (MSB-first); true on carry / borrow out of the top
+template <int WC>
+__device__ __forceinline__ bool unit_step(uint64_t (&o)[WC], int pos, bool add)
+{
+    const int w = pos >> 6;
+    const uint64_t bit = 1ull << (63 - (pos & 63));
+    bool carry = false;
+#pragma unroll
+    for (int k = WC - 1; k >= 0; --k) {
+        const uint64_t u = k == w ? bit : (k < w && carry ? 1ull : 0ull);
+        if (add) {
+            const uint64_t r = o[k] + u;
+            carry = r < o[k];
+            o[k] = r;
+        } else {
+            carry = o[k] < u;
+            o[k] -= u;
+        }
+    }
+    return carry;
+}
+
+// one word of a bound: compressed bits, and the first constant position
+// where x leaves the pattern (np, xb) if not found yet
+__device__ __forceinline__ uint64_t bound_word(uint64_t x, uint64_t m, uint64_t pt,
+                                               const uint64_t (&mv)[6], int pos, int &np, int &xb)
+{
+    if (np >= 0) return 0;
+    const uint64_t d = (x ^ pt) & ~m;
+    if (d) {
+        const int b = 63 - __clzll(d);
+        const uint64_t above = b == 63 ? 0 : ~0ull << (b + 1);
+        np = pos + __popcll(m & above);
+        xb = (int)((x >> b) & 1);
+        x &= above;
+    }
+    x &= m;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const uint64_t t = x & mv[i];
+        x = (x ^ t) | (t >> (1 << i));
+    }
+    return x;
+}
+
+// Per-group tables staged in LDS when they fit (config 3: 32 groups x 8
+// words = 16 KiB): the lanes of a wave read different groups' masks, which
+// from global memory are gathers.  Each thread maps kBoundP probes.
+constexpr int kBoundThreads = 256, kBoundP = 4;
+constexpr uint32_t kBoundLdsBytes = 48 * 1024;
+__host__ __device__ inline uint32_t bound_lds_bytes(int ng, int W)
+{
+    return (uint32_t)ng * (uint32_t)W * 8 * 8 + 4 * (uint32_t)ng;
+}
+
+template <int WC>
+__device__ __forceinline__ void bound_one(const ProbeView &p, const CompactMeta &cm, uint32_t q,
+                                          uint64_t *clo, uint64_t *chi);
+
+template <int WC, bool kLds>
+__global__ __launch_bounds__(kBoundThreads) void k_compact_bounds(ProbeView p, CompactMeta cm,
+                                                                  uint64_t *clo, uint64_t *chi)
+{
+    if constexpr (kLds) {
+        extern __shared__ __attribute__((aligned(16))) uint64_t blds[];
+        const uint32_t gw = (uint32_t)cm.ng * cm.W;
+        uint64_t *lm = blds, *lp = blds + gw, *lv = blds + 2 * gw;
+        uint32_t *lb = (uint32_t *)(blds + 8 * gw);
+        for (uint32_t i = threadIdx.x; i < gw; i += kBoundThreads) {
+            lm[i] = cm.mask[i];
+            lp[i] = cm.pat[i];
+        }
+        for (uint32_t i = threadIdx.x; i < 6 * gw; i += kBoundThreads) lv[i] = cm.mv[i];
+        for (uint32_t i = threadIdx.x; i < (uint32_t)cm.ng; i += kBoundThreads) lb[i] = cm.bits[i];
+        __syncthreads();
+        cm.mask = lm;
+        cm.pat = lp;
+        cm.mv = lv;
+        cm.bits = lb;
+    }
+    const uint32_t q0 = blockIdx.x * (kBoundThreads * kBoundP) + threadIdx.x;
+#pragma unroll 1
+    for (int j = 0; j < kBoundP; ++j) {
+        const uint32_t q = q0 + j * kBoundThreads;
+        if (q < p.n) bound_one<WC>(p, cm, q, clo, chi);
+    }
+}
+
+template <int WC>
+__device__ __forceinline__ void bound_one(const ProbeView &p, const CompactMeta &cm, uint32_t q,
+                                          uint64_t *clo, uint64_t *chi)
+{
+    const uint32_t g = p.gid[q];
+    uint64_t xl[kProbeWords], xh[kProbeWords];
+#pragma unroll
+    for (int j = 0; j < kProbeWords; ++j) {
+        const bool in = j < cm.W;
+        xl[j] = in ? __builtin_nontemporal_load(p.lo + (size_t)j * p.n + q) : 0;
+        xh[j] = in ? __builtin_nontemporal_load(p.hi + (size_t)j * p.n + q) : 0;
+    }
+    const uint32_t bits = cm.bits[g];
+    uint64_t al[WC], ah[WC];
+#pragma unroll
+    for (int k = 0; k < WC; ++k) al[k] = ah[k] = 0;
+    bool ok = bits != kNoRows;
+    if (ok) {
+        const uint64_t *mk = cm.mask + (size_t)g * cm.W, *pt = cm.pat + (size_t)g * cm.W;
+        const uint64_t *mvg = cm.mv + (size_t)g * cm.W * 6;
+        int pos = 0, npl = -1, nph = -1, xbl = 0, xbh = 0;
+#pragma unroll
+        for (int j = 0; j < kProbeWords; ++j) {
+            if (j >= cm.W) break;
+            const uint64_t m = mk[j], pj = pt[j];
+            uint64_t mv[6];
+#pragma unroll
+            for (int i = 0; i < 6; ++i) mv[i] = mvg[6 * j + i];
+            const int c = __popcll(m);
+            acc_push<WC>(al, bound_word(xl[j], m, pj, mv, pos, npl, xbl), c);
+            acc_push<WC>(ah, bound_word(xh[j], m, pj, mv, pos, nph, xbh), c);
+            pos += c;
+        }
+        acc_align<WC>(al, pos);
+        acc_align<WC>(ah, pos);
+        // lo: #rows < X = #codes < lo'
+        if (npl >= 0 && xbl && (npl == 0 || unit_step<WC>(al, npl - 1, true))) ok = false;
+        // hi: #rows <= X = #codes <= hi'
+        if (nph >= 0) {
+            if (!xbh) {
+                bool zero = true;
+#pragma unroll
+                for (int k = 0; k < WC; ++k) zero &= ah[k] == 0;
+                if (nph == 0 || zero)
+                    ok = false;
+                else
+                    unit_step<WC>(ah, nph - 1, false);
+            }
+            fill_ones<WC>(ah, nph, (int)bits);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < WC; ++k) {
+        clo[(size_t)k * p.n + q] = ok ? al[k] : ~0ull;
+        chi[(size_t)k * p.n + q] = ok ? ah[k] : 0;
+    }
+}
+
 template <int WC>
 hipError_t launch_rows_wc(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
                           const CompactMeta &cm, uint64_t *cw, hipStream_t s)
@@ -242,13 +428,22 @@ template <int WC>
 hipError_t launch_probes_wc(const ProbeView &p, const CompactMeta &cm, uint64_t *clo,
                             uint64_t *chi, hipStream_t s)
 {
-    k_compact_probes<WC><<<(p.n + 255) / 256, 256, 0, s>>>(p, cm, clo, chi);
+    static const bool generic = getenv("HSC_COMPACT_GENERIC") != nullptr;  // tests: old kernel
+    if (cm.W <= kProbeWords && !generic) {
+        const uint32_t blocks = (p.n + kBoundThreads * kBoundP - 1) / (kBoundThreads * kBoundP);
+        const uint32_t lds = bound_lds_bytes(cm.ng, cm.W);
+        if (lds <= kBoundLdsBytes)
+            k_compact_bounds<WC, true><<<blocks, kBoundThreads, lds, s>>>(p, cm, clo, chi);
+        else
+            k_compact_bounds<WC, false><<<blocks, kBoundThreads, 0, s>>>(p, cm, clo, chi);
+    } else
+        k_compact_probes<WC><<<(p.n + 255) / 256, 256, 0, s>>>(p, cm, clo, chi);
     return hipGetLastError();
 }
 
 CompactMeta meta_of(const CompactTables &t)
 {
-    return CompactMeta{t.mask, t.pat, t.mv, t.bits, t.W};
+    return CompactMeta{t.mask, t.pat, t.mv, t.bits, t.W, t.ng};
 }
 
 }  // namespace

@@ -399,7 +399,7 @@ static int build_compact(hsc_ctx *c, const WinView &w)
     HIPCHK(c, hipMemcpyAsync(c->d_cmv.p, mv.data(), 8 * gw * 6, hipMemcpyHostToDevice, s));
     HIPCHK(c, hipMemcpyAsync(c->d_cbits.p, bits.data(), 4 * (size_t)ng, hipMemcpyHostToDevice, s));
     c->ct = CompactTables{c->d_cmask.as<uint64_t>(), c->d_cpat.as<uint64_t>(), c->d_cmv.as<uint64_t>(),
-                          c->d_cbits.as<uint32_t>(), W, WC};
+                          c->d_cbits.as<uint32_t>(), W, WC, ng};
     HIPCHK(c, c->d_cwords.ensure(8 * (size_t)WC * c->cap));
     HIPCHK(c, compact_rows(w.words, w.stride, w.gid, w.n, c->ct, c->d_cwords.as<uint64_t>(), s));
     WinView &v = c->wc;

@@ -314,6 +314,7 @@ struct CompactTables {
     const uint64_t *mask, *pat, *mv;  // [ng][W] varying bits, first row, compress moves [ng][W][6]
     const uint32_t *bits;             // [ng] varying bits (0xFFFFFFFF: no rows)
     int W, WC;
+    int ng;                           // groups
 };
 constexpr int kMaxCompactWords = 6;
 void compress_moves(uint64_t m, uint64_t mv[6]);

@@ -17,11 +17,11 @@ ALPHA_ROWS = [0x08, 0x61, 0x62, 0x63]              # window key bytes (few varyi
 ALPHA_PROBE = [0x00, 0x08, 0x09, 0x60, 0x61, 0x62, 0x63, 0x64, 0x7F, 0x80, 0xE1, 0xFF]
 
 
-def _case(seed, n_commits=2500, n_txn=700, lens=(9, 24, 41, 64)):
+def _case(seed, n_commits=2500, n_txn=700, lens=(9, 24, 41, 64), n_tabs=5):
     rng = np.random.default_rng(seed)
     lb = LogBuilder()
     snaps = [lb.next_lsn()]
-    tabs = [f"t{i}" for i in range(5)]
+    tabs = [f"t{i}" for i in range(n_tabs)]
     head = {}  # per group: a fixed random prefix (constant bytes)
     for tb in tabs:
         for ix, kl in enumerate(lens):
@@ -30,7 +30,7 @@ def _case(seed, n_commits=2500, n_txn=700, lens=(9, 24, 41, 64)):
     for c in range(n_commits):
         lb.begin(c)
         for _ in range(int(rng.integers(1, 7))):
-            tb = tabs[int(rng.integers(0, 4))]  # t4 never written: its probes miss every row
+            tb = tabs[int(rng.integers(0, n_tabs - 1))]  # the last table is never written: its probes miss every row
             ix = int(rng.integers(0, len(lens)))
             kl = lens[ix]
             h = head[(tb, ix)]
@@ -61,7 +61,7 @@ def _case(seed, n_commits=2500, n_txn=700, lens=(9, 24, 41, 64)):
     for t in range(n_txn):
         rs = []
         for _ in range(int(rng.integers(1, 8))):
-            tb = tabs[int(rng.integers(0, 5))]
+            tb = tabs[int(rng.integers(0, n_tabs))]
             ix = int(rng.integers(0, len(lens)))
             a, b = probe_key(tb, ix), probe_key(tb, ix)
             u = rng.random()
@@ -107,3 +107,30 @@ def test_config3_window_is_compact(validator, oracle_mod):
     validator.ingest_log(log)
     assert validator.layout == LAYOUT_COMPACT and validator.code_words <= 3
     np.testing.assert_array_equal(validator.check_readsets(rs) != 0, want != 0)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_compact_long_keys_match_oracle(validator, oracle_mod, seed):
+    """Keys over 64 bytes (W > 8 words) take the generic bound kernel; the
+    register-resident one covers W <= 8 (the tests above)."""
+    log, rs = _case(100 + seed, n_commits=1200, n_txn=400, lens=(9, 72))
+    want, _, _ = oracle_mod.check(log, rs, nthreads=8)
+    validator.set_layout(LAYOUT_AUTO)
+    validator.ingest_log(log)
+    assert validator.layout == LAYOUT_COMPACT and validator.words > 8
+    np.testing.assert_array_equal(validator.check_readsets(rs) != 0, want != 0)
+
+
+def test_compact_many_groups_match_oracle(oracle_mod):
+    """120 groups of 8-word keys: the per-group tables exceed the bound
+    kernel's LDS budget, so it reads them from global memory."""
+    from comdb2_amd.hsc import Validator
+    log, rs = _case(7, n_commits=3000, n_txn=600, n_tabs=30)
+    want, _, _ = oracle_mod.check(log, rs, nthreads=8)
+    v = Validator(0)  # own context: the shared one's group dictionary holds longer keys
+    try:
+        v.ingest_log(log)
+        assert v.layout == LAYOUT_COMPACT and v.words == 8
+        np.testing.assert_array_equal(v.check_readsets(rs) != 0, want != 0)
+    finally:
+        v.close()
