@@ -317,59 +317,38 @@ __device__ __forceinline__ uint64_t bound_word(uint64_t x, uint64_t m, uint64_t 
 
 // Per-group tables staged in LDS when they fit (config 3: 32 groups x 8
 // words = 16 KiB): the lanes of a wave read different groups' masks, which
-// from global memory are gathers.  Each thread maps kBoundP probes.
-constexpr int kBoundThreads = 256, kBoundP = 4;
+// from global memory are gathers.  A thread maps P probes, the next probe's
+// key words loading while the current one is mapped (the first ones load
+// before the tables are staged).
+constexpr int kBoundThreads = 256;
 constexpr uint32_t kBoundLdsBytes = 48 * 1024;
 __host__ __device__ inline uint32_t bound_lds_bytes(int ng, int W)
 {
     return (uint32_t)ng * (uint32_t)W * 8 * 8 + 4 * (uint32_t)ng;
 }
 
-template <int WC>
-__device__ __forceinline__ void bound_one(const ProbeView &p, const CompactMeta &cm, uint32_t q,
-                                          uint64_t *clo, uint64_t *chi);
+struct BoundIn {
+    uint32_t g;
+    uint64_t xl[kProbeWords], xh[kProbeWords];
+};
 
-template <int WC, bool kLds>
-__global__ __launch_bounds__(kBoundThreads) void k_compact_bounds(ProbeView p, CompactMeta cm,
-                                                                  uint64_t *clo, uint64_t *chi)
+__device__ __forceinline__ void bound_load(const ProbeView &p, int W, uint32_t q, BoundIn &in)
 {
-    if constexpr (kLds) {
-        extern __shared__ __attribute__((aligned(16))) uint64_t blds[];
-        const uint32_t gw = (uint32_t)cm.ng * cm.W;
-        uint64_t *lm = blds, *lp = blds + gw, *lv = blds + 2 * gw;
-        uint32_t *lb = (uint32_t *)(blds + 8 * gw);
-        for (uint32_t i = threadIdx.x; i < gw; i += kBoundThreads) {
-            lm[i] = cm.mask[i];
-            lp[i] = cm.pat[i];
-        }
-        for (uint32_t i = threadIdx.x; i < 6 * gw; i += kBoundThreads) lv[i] = cm.mv[i];
-        for (uint32_t i = threadIdx.x; i < (uint32_t)cm.ng; i += kBoundThreads) lb[i] = cm.bits[i];
-        __syncthreads();
-        cm.mask = lm;
-        cm.pat = lp;
-        cm.mv = lv;
-        cm.bits = lb;
-    }
-    const uint32_t q0 = blockIdx.x * (kBoundThreads * kBoundP) + threadIdx.x;
-#pragma unroll 1
-    for (int j = 0; j < kBoundP; ++j) {
-        const uint32_t q = q0 + j * kBoundThreads;
-        if (q < p.n) bound_one<WC>(p, cm, q, clo, chi);
+    const bool v = q < p.n;
+    in.g = v ? p.gid[q] : 0;
+#pragma unroll
+    for (int j = 0; j < kProbeWords; ++j) {
+        const bool u = v && j < W;
+        in.xl[j] = u ? __builtin_nontemporal_load(p.lo + (size_t)j * p.n + q) : 0;
+        in.xh[j] = u ? __builtin_nontemporal_load(p.hi + (size_t)j * p.n + q) : 0;
     }
 }
 
 template <int WC>
-__device__ __forceinline__ void bound_one(const ProbeView &p, const CompactMeta &cm, uint32_t q,
-                                          uint64_t *clo, uint64_t *chi)
+__device__ __forceinline__ void bound_map(const ProbeView &p, const CompactMeta &cm, uint32_t q,
+                                          const BoundIn &in, uint64_t *clo, uint64_t *chi)
 {
-    const uint32_t g = p.gid[q];
-    uint64_t xl[kProbeWords], xh[kProbeWords];
-#pragma unroll
-    for (int j = 0; j < kProbeWords; ++j) {
-        const bool in = j < cm.W;
-        xl[j] = in ? __builtin_nontemporal_load(p.lo + (size_t)j * p.n + q) : 0;
-        xh[j] = in ? __builtin_nontemporal_load(p.hi + (size_t)j * p.n + q) : 0;
-    }
+    const uint32_t g = in.g;
     const uint32_t bits = cm.bits[g];
     uint64_t al[WC], ah[WC];
 #pragma unroll
@@ -387,8 +366,8 @@ __device__ __forceinline__ void bound_one(const ProbeView &p, const CompactMeta 
 #pragma unroll
             for (int i = 0; i < 6; ++i) mv[i] = mvg[6 * j + i];
             const int c = __popcll(m);
-            acc_push<WC>(al, bound_word(xl[j], m, pj, mv, pos, npl, xbl), c);
-            acc_push<WC>(ah, bound_word(xh[j], m, pj, mv, pos, nph, xbh), c);
+            acc_push<WC>(al, bound_word(in.xl[j], m, pj, mv, pos, npl, xbl), c);
+            acc_push<WC>(ah, bound_word(in.xh[j], m, pj, mv, pos, nph, xbh), c);
             pos += c;
         }
         acc_align<WC>(al, pos);
@@ -416,6 +395,41 @@ __device__ __forceinline__ void bound_one(const ProbeView &p, const CompactMeta 
     }
 }
 
+template <int WC, bool kLds, int P>
+__global__ __launch_bounds__(kBoundThreads) void k_compact_bounds(ProbeView p, CompactMeta cm,
+                                                                  uint64_t *clo, uint64_t *chi)
+{
+    const uint32_t q0 = blockIdx.x * (kBoundThreads * P) + threadIdx.x;
+    BoundIn cur;
+    bound_load(p, cm.W, q0, cur);
+    if constexpr (kLds) {
+        extern __shared__ __attribute__((aligned(16))) uint64_t blds[];
+        const uint32_t gw = (uint32_t)cm.ng * cm.W;
+        uint64_t *lm = blds, *lp = blds + gw, *lv = blds + 2 * gw;
+        uint32_t *lb = (uint32_t *)(blds + 8 * gw);
+        for (uint32_t i = threadIdx.x; i < gw; i += kBoundThreads) {
+            lm[i] = cm.mask[i];
+            lp[i] = cm.pat[i];
+        }
+        for (uint32_t i = threadIdx.x; i < 6 * gw; i += kBoundThreads) lv[i] = cm.mv[i];
+        for (uint32_t i = threadIdx.x; i < (uint32_t)cm.ng; i += kBoundThreads) lb[i] = cm.bits[i];
+        __syncthreads();
+        cm.mask = lm;
+        cm.pat = lp;
+        cm.mv = lv;
+        cm.bits = lb;
+    }
+#pragma unroll 1
+    for (int j = 0; j < P; ++j) {
+        const uint32_t q = q0 + j * kBoundThreads;
+        if (q >= p.n) break;
+        BoundIn nxt;
+        if (j + 1 < P) bound_load(p, cm.W, q + kBoundThreads, nxt);
+        bound_map<WC>(p, cm, q, cur, clo, chi);
+        if (j + 1 < P) cur = nxt;
+    }
+}
+
 template <int WC>
 hipError_t launch_rows_wc(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
                           const CompactMeta &cm, uint64_t *cw, hipStream_t s)
@@ -430,12 +444,17 @@ hipError_t launch_probes_wc(const ProbeView &p, const CompactMeta &cm, uint64_t 
 {
     static const bool generic = getenv("HSC_COMPACT_GENERIC") != nullptr;  // tests: old kernel
     if (cm.W <= kProbeWords && !generic) {
-        const uint32_t blocks = (p.n + kBoundThreads * kBoundP - 1) / (kBoundThreads * kBoundP);
-        const uint32_t lds = bound_lds_bytes(cm.ng, cm.W);
-        if (lds <= kBoundLdsBytes)
-            k_compact_bounds<WC, true><<<blocks, kBoundThreads, lds, s>>>(p, cm, clo, chi);
+        static const int P = getenv("HSC_BOUND_P") ? atoi(getenv("HSC_BOUND_P")) : 2;  // A/B knob
+        const uint32_t per = kBoundThreads * (P == 1 ? 1 : P == 4 ? 4 : 2);
+        const uint32_t blocks = (p.n + per - 1) / per;
+        const bool in_lds = bound_lds_bytes(cm.ng, cm.W) <= kBoundLdsBytes;
+        const uint32_t lds = in_lds ? bound_lds_bytes(cm.ng, cm.W) : 0;
+#define HSC_BOUNDS(L_, P_) k_compact_bounds<WC, L_, P_><<<blocks, kBoundThreads, lds, s>>>(p, cm, clo, chi)
+        if (in_lds)
+            P == 1 ? HSC_BOUNDS(true, 1) : P == 4 ? HSC_BOUNDS(true, 4) : HSC_BOUNDS(true, 2);
         else
-            k_compact_bounds<WC, false><<<blocks, kBoundThreads, 0, s>>>(p, cm, clo, chi);
+            P == 1 ? HSC_BOUNDS(false, 1) : P == 4 ? HSC_BOUNDS(false, 4) : HSC_BOUNDS(false, 2);
+#undef HSC_BOUNDS
     } else
         k_compact_probes<WC><<<(p.n + 255) / 256, 256, 0, s>>>(p, cm, clo, chi);
     return hipGetLastError();

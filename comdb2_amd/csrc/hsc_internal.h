@@ -76,6 +76,7 @@ struct WinView {
     uint32_t n, ntiles, ntables;
     int W, log2T, levels;
     int gbits;                // bits of gid in a splitter prefix (key_prefix)
+    int compact;              // words are per-group compact codes (hsc_compact.hip)
 };
 
 struct ProbeView {

@@ -747,7 +747,7 @@ __global__ __launch_bounds__(kLocateThreads) void k_scatter_any(WinView w, Probe
     }
 }
 
-// W <= 2: every global load of a batch of kScatB probes is issued before the
+// W <= 3: every global load of a batch of kScatB probes is issued before the
 // first dependent use (probe words, then group bounds), then the LDS slot
 // atomics, then the 16-byte record stores.
 constexpr int kScatB = 4;
@@ -764,7 +764,8 @@ __global__ __launch_bounds__(kLocateThreads) void k_scatter(WinView w, ProbeView
     const uint32_t T = 1u << w.log2T;
     constexpr int rs = HSC_REC_PAD ? 8 : 2 * WT + 2;
     for (uint32_t base = c0; base < c1; base += kScatB * kLocateThreads) {
-        uint64_t cd[kScatB], lo[kScatB][2], hi[kScatB][2], snap[kScatB];
+        constexpr int WA = WT > 2 ? WT : 2;
+        uint64_t cd[kScatB], lo[kScatB][WA], hi[kScatB][WA], snap[kScatB];
         uint32_t g[kScatB], txn[kScatB], gs[kScatB], ge[kScatB];
 #pragma unroll
         for (int k = 0; k < kScatB; ++k) {
@@ -812,14 +813,16 @@ __global__ __launch_bounds__(kLocateThreads) void k_scatter(WinView w, ProbeView
                 const uint64_t ub = ge[k] > ts ? min(ge[k] - ts, tn) : 0;
                 const uint64_t meta = (uint64_t)txn[k] | (lb << 32) | (ub << 45) | (kind << 62);
                 ulonglong2 *r = (ulonglong2 *)(work.recs + (size_t)slot[k][h] * rs);
-                if constexpr (WT == 1) {
-                    r[0] = make_ulonglong2(lo[k][0], hi[k][0]);
-                    r[1] = make_ulonglong2(snap[k], meta);
-                } else {
-                    r[0] = make_ulonglong2(lo[k][0], lo[k][1]);
-                    r[1] = make_ulonglong2(hi[k][0], hi[k][1]);
-                    r[2] = make_ulonglong2(snap[k], meta);
+                uint64_t rv[2 * WT + 2];  // lo[WT] hi[WT] snap meta
+#pragma unroll
+                for (int j = 0; j < WT; ++j) {
+                    rv[j] = lo[k][j];
+                    rv[WT + j] = hi[k][j];
                 }
+                rv[2 * WT] = snap[k];
+                rv[2 * WT + 1] = meta;
+#pragma unroll
+                for (int i = 0; i <= WT; ++i) r[i] = make_ulonglong2(rv[2 * i], rv[2 * i + 1]);
             }
         }
     }
@@ -834,6 +837,8 @@ hipError_t launch_scatter(const WinView &w, const ProbeView &p, const ProbeWork 
         k_scatter<1><<<work.G, kLocateThreads, lds, s>>>(w, p, work);
     else if (w.W == 2)
         k_scatter<2><<<work.G, kLocateThreads, lds, s>>>(w, p, work);
+    else if (w.W == 3)
+        k_scatter<3><<<work.G, kLocateThreads, lds, s>>>(w, p, work);
     else
         k_scatter_any<<<work.G, kLocateThreads, lds, s>>>(w, p, work);
     return hipGetLastError();
@@ -858,8 +863,25 @@ __device__ __forceinline__ int cmp_row(int W, const uint64_t *kw, uint32_t T, ui
     return 0;
 }
 
-// WT: key words if 1 or 2 (fast staging path, tiles of 2^LOG2T rows), 0 = any
-template <int WT, int LOG2T>
+// Word 0 of the row in LDS, later words (only on a tie of word 0) from the
+// window in global memory.  Used for compact codes, whose first word holds
+// the group's 64 most significant varying bits, so ties are rare.
+__device__ __forceinline__ int cmp_row_w0(int W, const uint64_t *kw, const WinView &w, uint32_t ts,
+                                          uint32_t row, uint64_t k0, uint64_t k1,
+                                          const uint64_t *kmem)
+{
+    const uint64_t r0 = kw[row];
+    if (k0 != r0) return k0 < r0 ? -1 : 1;
+    for (int j = 1; j < W; ++j) {
+        const uint64_t a = j == 1 ? k1 : kmem[j], b = w.words[(size_t)j * w.stride + ts + row];
+        if (a != b) return a < b ? -1 : 1;
+    }
+    return 0;
+}
+
+// WT: key words if 1..3 (fast staging path, tiles of 2^LOG2T rows), 0 = any.
+// W0: stage only key word 0 (and the LSNs) of the tile.
+template <int WT, int LOG2T, bool W0 = false>
 __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, ProbeWork work,
                                                        uint8_t *verdict)
 {
@@ -874,8 +896,9 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, ProbeWork work
     const uint32_t T = 1u << w.log2T;
     const uint32_t ts = tile << w.log2T;
 
-    uint64_t *kw = (uint64_t *)smem;               // [W][T]
-    uint64_t *lsn = kw + (size_t)W * T;            // [T]
+    constexpr int WS = W0 ? 1 : WT;                // key words staged (WT > 0)
+    uint64_t *kw = (uint64_t *)smem;               // [W][T] (W0: [1][T])
+    uint64_t *lsn = kw + (size_t)(W0 ? 1 : W) * T; // [T]
     uint64_t *b16 = lsn + T;                       // [T / 16]
     uint64_t *b256 = b16 + T / 16;                 // [T / 256]
 
@@ -893,6 +916,9 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, ProbeWork work
             if constexpr (WT == 2) {
                 bnd[k][0] = *(const ulonglong2 *)rec;
                 bnd[k][1] = *(const ulonglong2 *)(rec + 2);
+            } else if constexpr (WT >= 3) {  // words 0, 1 of lo and hi; later words from rec
+                bnd[k][0] = *(const ulonglong2 *)rec;
+                bnd[k][1] = make_ulonglong2(rec[W], rec[W + 1]);
             } else if constexpr (WT == 1) {
                 bnd[k][0] = *(const ulonglong2 *)rec;  // lo0, hi0
             }
@@ -905,21 +931,21 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, ProbeWork work
     // bounds checks (rows >= tn are never searched).
     if constexpr (WT > 0) {
         constexpr int kIt = (1 << LOG2T) / (2 * kJoinThreads);
-        ulonglong2 v[kIt][WT + 1];
+        ulonglong2 v[kIt][WS + 1];
 #pragma unroll
         for (int it = 0; it < kIt; ++it) {
             const uint32_t pr = threadIdx.x + it * kJoinThreads;
 #pragma unroll
-            for (int j = 0; j < WT; ++j)
+            for (int j = 0; j < WS; ++j)
                 v[it][j] = *(const ulonglong2 *)(w.words + (size_t)j * w.stride + ts + 2 * pr);
-            v[it][WT] = *(const ulonglong2 *)(w.lsn + ts + 2 * pr);
+            v[it][WS] = *(const ulonglong2 *)(w.lsn + ts + 2 * pr);
         }
 #pragma unroll
         for (int it = 0; it < kIt; ++it) {
             const uint32_t pr = threadIdx.x + it * kJoinThreads;
 #pragma unroll
-            for (int j = 0; j < WT; ++j) *(ulonglong2 *)(kw + (size_t)j * T + 2 * pr) = v[it][j];
-            *(ulonglong2 *)(lsn + 2 * pr) = v[it][WT];
+            for (int j = 0; j < WS; ++j) *(ulonglong2 *)(kw + (size_t)j * T + 2 * pr) = v[it][j];
+            *(ulonglong2 *)(lsn + 2 * pr) = v[it][WS];
         }
     } else {
         for (int j = 0; j <= W; ++j) {
@@ -962,7 +988,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, ProbeWork work
         const uint32_t kind = (uint32_t)(meta >> 62);
         if (lb >= ub) continue;
         uint64_t l0, l1, h0, h1;
-        if constexpr (WT == 2) {
+        if constexpr (WT >= 2) {
             l0 = bnd[k][0].x;
             l1 = bnd[k][0].y;
             h0 = bnd[k][1].x;
@@ -983,10 +1009,14 @@ __global__ __launch_bounds__(kJoinThreads) void k_join(WinView w, ProbeWork work
         while (alo < ahi || blo < bhi) {
             const uint32_t am = (alo + ahi) >> 1, bm = (blo + bhi) >> 1;
             if (alo < ahi) {
-                if (cmp_row(W, kw, T, am, l0, l1, rec) > 0) alo = am + 1; else ahi = am;
+                const int c = W0 ? cmp_row_w0(W, kw, w, ts, am, l0, l1, rec)
+                                 : cmp_row(W, kw, T, am, l0, l1, rec);
+                if (c > 0) alo = am + 1; else ahi = am;
             }
             if (blo < bhi) {
-                if (cmp_row(W, kw, T, bm, h0, h1, rec + W) >= 0) blo = bm + 1; else bhi = bm;
+                const int c = W0 ? cmp_row_w0(W, kw, w, ts, bm, h0, h1, rec + W)
+                                 : cmp_row(W, kw, T, bm, h0, h1, rec + W);
+                if (c >= 0) blo = bm + 1; else bhi = bm;
             }
         }
         const uint32_t pp = alo, qq = blo;
@@ -1002,13 +1032,20 @@ hipError_t launch_join(const WinView &w, const ProbeWork &work, uint32_t max_ite
 {
     if (max_items == 0 || w.n == 0) return hipSuccess;
     const size_t T = (size_t)1 << w.log2T;
-    const size_t lds = T * 8 * (size_t)w.W + T * 8 + (T / 16) * 8 + std::max<size_t>(T / 256, 16) * 8;
+    static const bool all_words = getenv("HSC_JOIN_ALL_WORDS") != nullptr;  // A/B: stage every word
+    const bool w0 = w.W == 3 && w.log2T == 11 && w.compact && !all_words;
+    const size_t lds = T * 8 * (size_t)(w0 ? 1 : w.W) + T * 8 + (T / 16) * 8 +
+                       std::max<size_t>(T / 256, 16) * 8;
     if (w.W == 1 && w.log2T == 12)
         k_join<1, 12><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
     else if (w.W == 1 && w.log2T == 11)
         k_join<1, 11><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
     else if (w.W == 2 && w.log2T == 11)
         k_join<2, 11><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
+    else if (w0)
+        k_join<3, 11, true><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
+    else if (w.W == 3 && w.log2T == 11)
+        k_join<3, 11><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
     else
         k_join<0, 0><<<max_items, kJoinThreads, lds, s>>>(w, work, verdict);
     return hipGetLastError();
