@@ -524,6 +524,10 @@ def main():
             "join_records": tm["records"], "tiles": tm["tiles"],
         },
         "ingest_ms": ingest_ms,
+        # window build (sort + dedupe + summaries), SURVEY 8(d): reported apart
+        # from the probe phase; bytes = N_w * (L^ + 8 LSN + 4 group)
+        "ingest": {"rows": int(n_w), "algorithmic_bytes": int(n_w) * (8 * W + 12),
+                   "GBps": int(n_w) * (8 * W + 12) / (ingest_ms * 1e-3) / 1e9 if ingest_ms else None},
         "cold_e2e_ms": ingest_ms + ms_step,
         "cpu_baseline": None,
     }

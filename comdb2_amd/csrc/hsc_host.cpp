@@ -611,9 +611,8 @@ static int device_build(hsc_ctx *c, size_t n_in)
             HIPCHK(c, c->d_rank32.ensure(4 * (size_t)nv.len[0]));
             uint32_t *flag = c->d_count.as<uint32_t>() + 4;
             HIPCHK(c, narrow_tiles_build(nv.keys, c->d_lsn.as<uint64_t>(), (uint32_t)c->n, nv.len[0],
-                                         c->d_commits.as<uint64_t>(), c->ncommit,
-                                         c->d_key32.as<uint32_t>(), c->d_rank32.as<uint32_t>(),
-                                         flag, s));
+                                         c->cdir, c->d_key32.as<uint32_t>(),
+                                         c->d_rank32.as<uint32_t>(), flag, s));
             uint32_t wide32 = 1;
             HIPCHK(c, hipMemcpyAsync(&wide32, flag, 4, hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));

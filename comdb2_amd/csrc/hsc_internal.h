@@ -210,8 +210,9 @@ struct NarrowTiles {
     uint4 *recs;               // [2n] {lo delta, hi delta, snapshot rank, read set}
 };
 hipError_t check_sorted_u64(const uint64_t *v, size_t n, uint32_t *flag, hipStream_t s);
+// rank32 by a search of cdir (the 16-ary directory over the commit LSNs C)
 hipError_t narrow_tiles_build(const uint64_t *key64, const uint64_t *lsn, uint32_t n, uint32_t len,
-                              const uint64_t *C, uint32_t m, uint32_t *key32, uint32_t *rank32,
+                              const Dir16 &cdir, uint32_t *key32, uint32_t *rank32,
                               uint32_t *flag, hipStream_t s);
 uint32_t narrow_tiles_chunk();
 // Bucket table of the tiles' first codes (locate's tile search from LDS);

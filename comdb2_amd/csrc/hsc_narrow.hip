@@ -397,24 +397,13 @@ hipError_t check_sorted_u64(const uint64_t *v, size_t n, uint32_t *flag, hipStre
     return hipGetLastError();
 }
 
-// rank32[i] = 1 + lower_bound(C, lsn[i]) (lsn[i] is in C); pads get 0
-__global__ void k_rank32(const uint64_t *lsn, uint32_t n, uint32_t len, const uint64_t *C,
-                         uint32_t m, uint32_t *rank)
-{
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= len) return;
-    if (i >= n) {
-        rank[i] = 0;
-        return;
-    }
-    const uint64_t x = lsn[i];
-    uint32_t lo = 0, hi = m;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (C[mid] < x) lo = mid + 1; else hi = mid;
-    }
-    rank[i] = lo + 1;
-}
+// rank32[i] = 1 + lower_bound(C, lsn[i]) (lsn[i] is in C); pads get 0.
+// kRankK rows per thread searched in lockstep over the commit directory,
+// whose upper levels are staged in LDS (defined with the locate kernel).
+constexpr int kRankThreads = 1024, kRankK = 8;
+__host__ __device__ inline uint32_t dir16_lds_entries(const Dir16 &d);
+__global__ __launch_bounds__(kRankThreads) void k_rank32(const uint64_t *lsn, uint32_t n,
+                                                         uint32_t len, Dir16 d, uint32_t *rank);
 
 // key32 = key64 - first key64 of the tile; flag := 1 if a tile spans >= 2^32
 __global__ void k_key32(const uint64_t *key64, uint32_t n, uint32_t len, uint32_t *key32,
@@ -432,13 +421,15 @@ __global__ void k_key32(const uint64_t *key64, uint32_t n, uint32_t len, uint32_
 }
 
 hipError_t narrow_tiles_build(const uint64_t *key64, const uint64_t *lsn, uint32_t n, uint32_t len,
-                              const uint64_t *C, uint32_t m, uint32_t *key32, uint32_t *rank32,
+                              const Dir16 &cdir, uint32_t *key32, uint32_t *rank32,
                               uint32_t *flag, hipStream_t s)
 {
     hipError_t e = hipMemsetAsync(flag, 0, 4, s);
     if (e != hipSuccess || len == 0) return e;
     k_key32<<<(len + 255) / 256, 256, 0, s>>>(key64, n, len, key32, flag);
-    k_rank32<<<(len + 255) / 256, 256, 0, s>>>(lsn, n, len, C, m, rank32);
+    const uint32_t per = kRankThreads * kRankK;
+    k_rank32<<<(len + per - 1) / per, kRankThreads, 8 * dir16_lds_entries(cdir), s>>>(lsn, n, len,
+                                                                                    cdir, rank32);
     return hipGetLastError();
 }
 
@@ -549,6 +540,30 @@ __device__ __forceinline__ void dir16_count(const Dir16 &d, const uint64_t *lds,
     for (int k = 0; k < K; ++k) out[k] = act[k] ? min(c[k], d.n) : 0;
 }
 
+__global__ __launch_bounds__(kRankThreads) void k_rank32(const uint64_t *lsn, uint32_t n,
+                                                         uint32_t len, Dir16 d, uint32_t *rank)
+{
+    extern __shared__ __attribute__((aligned(16))) uint64_t rlds[];
+    const uint32_t i0 = blockIdx.x * (kRankThreads * kRankK) + threadIdx.x;
+    uint64_t x[kRankK];
+    bool act[kRankK];
+#pragma unroll
+    for (int k = 0; k < kRankK; ++k) {
+        const uint32_t i = i0 + k * kRankThreads;
+        act[k] = i < n;
+        x[k] = act[k] ? lsn[i] : 0;
+    }
+    dir16_stage(d, rlds);
+    __syncthreads();
+    uint32_t c[kRankK];
+    dir16_count<kRankK>(d, rlds, x, act, c);
+#pragma unroll
+    for (int k = 0; k < kRankK; ++k) {
+        const uint32_t i = i0 + k * kRankThreads;
+        if (i < len) rank[i] = act[k] ? c[k] + 1 : 0;
+    }
+}
+
 // ---- locate: codes, snapshot ranks, end tiles, per-chunk tile histogram ----
 // One workgroup per chunk of kLocTP * kLocTThreads probes; thread t owns
 // probes c0 + t + kLocTThreads j, j < kLocTP (consecutive lanes =
@@ -559,10 +574,17 @@ __device__ __forceinline__ void dir16_count(const Dir16 &d, const uint64_t *lds,
 // search and the tiles' first codes never leave LDS).  Output per probe: its
 // first join record {tile << 12 | rank, lo, hi, r(S)} and, for a range that
 // spans two tiles, its second one.
-constexpr int kLocTP = 4;
-constexpr int kLocTThreads = 1024;  // 4096 probes per chunk (in-chunk ranks fit 12 bits)
+#ifndef HSC_LOC_TP
+#define HSC_LOC_TP 4
+#endif
+#ifndef HSC_DIR_LDS
+#define HSC_DIR_LDS 4400
+#endif
+constexpr int kLocTP = HSC_LOC_TP;
+constexpr int kLocTThreads = 1024;  // <= 4096 probes per chunk (in-chunk ranks fit 12 bits)
+static_assert(kLocTP * kLocTThreads <= 4096, "in-chunk ranks are 12 bits");
 constexpr uint32_t kHasSecond = 1u << 31;
-constexpr int kDirLds = 4400;  // directory entries staged in LDS per directory
+constexpr int kDirLds = HSC_DIR_LDS;  // directory entries staged in LDS per directory
 
 template <int W>
 __device__ __forceinline__ void locate_codes(const NarrowView &nv, const ProbeView &p, uint32_t q,

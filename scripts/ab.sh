@@ -12,7 +12,7 @@ for r in $(seq 1 $ROUNDS); do
     echo "== $name round $r"
     env $env timeout -k 10 300 python bench.py $ARGS > "gpurun_out/ab_${name}_$r.log" 2>&1
     rc=$?
-    tail -1 "gpurun_out/ab_${name}_$r.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', round(d['value']/1e6), {k: round(x*1e3,1) for k,x in d['probe_phase']['kernels_ms'].items()})" || tail -5 "gpurun_out/ab_${name}_$r.log"
+    tail -1 "gpurun_out/ab_${name}_$r.log" | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$name', round(d['value']/1e6), round(d['ms_per_step']*1e3,1), d['config'].get('serial_ms_per_step'), {k: round(x['event_ms']*1e3,1) for k,x in d['probe_phase']['kernels'].items()})" || tail -5 "gpurun_out/ab_${name}_$r.log"
     [ $rc -ne 0 ] && exit $rc
   done
 done
