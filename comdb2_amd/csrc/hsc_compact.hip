@@ -169,25 +169,40 @@ __device__ bool code_of(const CompactMeta &cm, uint32_t g, const uint64_t *x, si
     return true;
 }
 
+// Rows are sorted by group: each thread ORs (row XOR the group's first row)
+// over kVaryRows consecutive rows and flushes only when the group changes,
+// and a wave whose lanes end in one group combines them first, so the
+// atomics per (group, word) stay few (one per row made them contend).
+constexpr int kVaryRows = 16;
 __global__ __launch_bounds__(256) void k_group_vary(const uint64_t *words, size_t stride,
                                                     const uint32_t *gid, uint32_t n, int W,
                                                     const uint32_t *gstart, uint64_t *mask)
 {
-    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool ok = i0 < n;
-    const uint32_t i = ok ? i0 : n - 1;
-    const uint32_t g = gid[i];
-    const uint32_t g0 = __shfl(g, 0);
-    const bool uniform = __all(g == g0);
-    const uint32_t f = gstart[g];
+    const size_t base = ((size_t)blockIdx.x * blockDim.x + threadIdx.x) * kVaryRows;
+    if (__shfl(base, 0) >= n) return;  // the whole wave is past the end
+    const bool valid = base < n;
+    const uint32_t end = valid ? (uint32_t)min((size_t)n, base + kVaryRows) : 0;
     for (int j = 0; j < W; ++j) {
-        uint64_t x = ok ? words[(size_t)j * stride + i] ^ words[(size_t)j * stride + f] : 0;
-        if (uniform) {
+        const uint64_t *wj = words + (size_t)j * stride;
+        uint32_t cg = valid ? gid[base] : 0xFFFFFFFFu;
+        uint64_t f = valid ? wj[gstart[cg]] : 0, acc = 0;
+        for (uint32_t i = (uint32_t)base; i < end; ++i) {
+            const uint32_t g = gid[i];
+            if (g != cg) {
+                if (acc) atomicOr((unsigned long long *)&mask[(size_t)cg * W + j], acc);
+                cg = g;
+                f = wj[gstart[g]];
+                acc = 0;
+            }
+            acc |= wj[i] ^ f;
+        }
+        const uint32_t cg0 = __shfl(cg, 0);
+        if (__all(!valid || cg == cg0)) {
 #pragma unroll
-            for (int o = 32; o > 0; o >>= 1) x |= __shfl_xor(x, o);
-            if (lane_id() == 0 && x) atomicOr((unsigned long long *)&mask[(size_t)g * W + j], x);
-        } else if (x) {
-            atomicOr((unsigned long long *)&mask[(size_t)g * W + j], x);
+            for (int o = 32; o > 0; o >>= 1) acc |= __shfl_xor(acc, o);
+            if (lane_id() == 0 && acc) atomicOr((unsigned long long *)&mask[(size_t)cg0 * W + j], acc);
+        } else if (valid && acc) {
+            atomicOr((unsigned long long *)&mask[(size_t)cg * W + j], acc);
         }
     }
 }
@@ -491,7 +506,8 @@ hipError_t compact_masks(const uint64_t *words, size_t stride, const uint32_t *g
 {
     hipError_t e = hipMemsetAsync(mask, 0, 8 * (size_t)ng * W, s);
     if (e != hipSuccess) return e;
-    if (n) k_group_vary<<<(n + 255) / 256, 256, 0, s>>>(words, stride, gid, n, W, gstart, mask);
+    const uint32_t per = 256 * kVaryRows;
+    if (n) k_group_vary<<<(n + per - 1) / per, 256, 0, s>>>(words, stride, gid, n, W, gstart, mask);
     if (ng) k_group_pattern<<<(ng + 63) / 64, 64, 0, s>>>(words, stride, W, ng, gstart, gend, pat);
     return hipGetLastError();
 }

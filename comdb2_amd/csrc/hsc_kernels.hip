@@ -54,6 +54,7 @@ __global__ __launch_bounds__(256) void k_vary_mask(int W, size_t n, const uint32
                                                    const uint64_t *words, size_t stride,
                                                    unsigned long long *mask)
 {
+    __shared__ uint64_t part[256 / 64];
     for (int j = 0; j <= W; ++j) {
         const uint64_t ref = j < W ? words[(size_t)j * stride] : gid[0];
         uint64_t m = 0;
@@ -61,7 +62,15 @@ __global__ __launch_bounds__(256) void k_vary_mask(int W, size_t n, const uint32
              i += (size_t)gridDim.x * blockDim.x)
             m |= (j < W ? words[(size_t)j * stride + i] : gid[i]) ^ ref;
         for (int o = 32; o > 0; o >>= 1) m |= __shfl_xor(m, o, 64);
-        if (lane_id() == 0 && m) atomicOr(&mask[j], (unsigned long long)m);
+        // one atomic per block and word: all blocks OR into the same W + 1
+        // words, so per-wave atomics would queue behind each other
+        if (lane_id() == 0) part[threadIdx.x >> 6] = m;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint64_t b = part[0] | part[1] | part[2] | part[3];
+            if (b) atomicOr(&mask[j], (unsigned long long)b);
+        }
+        __syncthreads();
     }
 }
 
@@ -247,7 +256,7 @@ hipError_t radix_sort_rows(int W, size_t n, uint32_t *gid, uint64_t *words, uint
     uint32_t *scan_tmp = counts + (size_t)256 * nblocks;
     hipError_t e = hipMemsetAsync(dmask, 0, 8 * ((size_t)W + 1), s);
     if (e != hipSuccess) return e;
-    const unsigned hgrid = (unsigned)std::min<size_t>((n + 255) / 256, 2048);
+    const unsigned hgrid = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
     k_vary_mask<<<hgrid, 256, 0, s>>>(W, n, gid, words, stride, dmask);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
