@@ -92,21 +92,26 @@ __global__ __launch_bounds__(kSortThreads) void k_rs_count(int W, int d, size_t 
     counts[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
 }
 
-// Stable scatter.  Phase 1 ranks the block's rows in index order (round-major,
-// lane order inside a round; 8 ballots per round for the wave match) into
-// block-local sorted positions and records the permutation in LDS.  Phase 2
-// walks the block in sorted order, so consecutive threads write consecutive
-// addresses of each digit's run (coalesced stores); the rows it gathers were
-// read by phase 1 and are served from L1/L2.
+// Stable scatter.  Phase 1: wave w ranks rows [1024 w, 1024 w + 1024) of the
+// block in index order (16 rounds of 64 lanes; 8 ballots per round for the
+// wave match) against wave-private digit counters in LDS, so the rounds need
+// no block barrier; the per-wave counts then become per-(wave, digit) offsets
+// and the block's sorted permutation is written to LDS.  Phase 2 walks the
+// block in sorted order, so consecutive threads write consecutive addresses
+// of each digit's run (coalesced stores); the rows it gathers were read by
+// phase 1 and are served from L1/L2.
+template <int WT>  // key words if 1..3 (phase 2 holds rows in registers), 0 = any
 __global__ __launch_bounds__(kSortThreads) void k_rs_scatter(
-    int W, int d, size_t n, const uint32_t *gid, const uint64_t *words, const uint64_t *lsn,
+    int Wrt, int d, size_t n, const uint32_t *gid, const uint64_t *words, const uint64_t *lsn,
     size_t stride, uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o,
     const uint32_t *offsets, uint32_t nblocks)
 {
+    constexpr int kWaves = kSortThreads / 64;
+    constexpr uint32_t kWaveRows = kSortTile / kWaves;
+    const int W = WT > 0 ? WT : Wrt;
     __shared__ uint32_t gbase[256];
     __shared__ uint32_t loff[256];
-    __shared__ uint32_t running[256];
-    __shared__ uint32_t wave_h[kSortThreads / 64][256];
+    __shared__ uint32_t wcnt[kWaves][256];
     __shared__ uint16_t perm[kSortTile];
     __shared__ uint32_t lds16[16];
     const int lane = lane_id(), wid = threadIdx.x >> 6;
@@ -121,48 +126,113 @@ __global__ __launch_bounds__(kSortThreads) void k_rs_scatter(
     gbase[dg] = mine;
     uint32_t tot;
     loff[dg] = block_excl_scan<kSortThreads>(cnt, lds16, tot);
-    running[dg] = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) wcnt[w][dg] = 0;
+    __syncthreads();
     const size_t base = (size_t)blockIdx.x * kSortTile;
     const uint64_t lt_mask = (lane ? (~0ull >> (64 - lane)) : 0ull);
+    const uint32_t wbase = wid * kWaveRows;
+    uint32_t *wc = wcnt[wid];
+    uint32_t dig[kSortItems], lp[kSortItems];
+#pragma unroll
+    for (int k = 0; k < kSortItems; ++k) {  // every digit load in flight before the ranking
+        const size_t i = base + wbase + k * 64 + lane;
+        dig[k] = i < n ? row_digit(W, d, i, gid, words, stride) : 0;
+    }
+#pragma unroll
     for (int k = 0; k < kSortItems; ++k) {
-        const size_t i = base + (size_t)k * kSortThreads + threadIdx.x;
+        const size_t i = base + wbase + k * 64 + lane;
         const bool valid = i < n;
-        uint32_t dig = valid ? row_digit(W, d, i, gid, words, stride) : 0;
+        const uint32_t dk = dig[k];
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
-            uint64_t m = __ballot((dig >> b) & 1u);
-            peers &= ((dig >> b) & 1u) ? m : ~m;
+            const uint64_t m = __ballot((dk >> b) & 1u);
+            peers &= ((dk >> b) & 1u) ? m : ~m;
         }
-        const uint32_t rank = __popcll(peers & lt_mask);
-        const uint32_t c = __popcll(peers);
-        for (int t = threadIdx.x; t < (kSortThreads / 64) * 256; t += kSortThreads)
-            (&wave_h[0][0])[t] = 0;
-        __syncthreads();
-        if (valid && rank == 0) wave_h[wid][dig] = c;
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = loff[dig] + running[dig] + rank;
-            for (int w2 = 0; w2 < wid; ++w2) pos += wave_h[w2][dig];
-            perm[pos] = (uint16_t)(k * kSortThreads + threadIdx.x);
-        }
-        __syncthreads();
-        {
-            uint32_t add = 0;
-            for (int w2 = 0; w2 < kSortThreads / 64; ++w2) add += wave_h[w2][threadIdx.x];
-            running[threadIdx.x] += add;
-        }
-        __syncthreads();
+        const uint32_t before = wc[dk];
+        lp[k] = before + __popcll(peers & lt_mask);
+        dig[k] = valid ? dk : 0xFFFFFFFFu;
+        // every lane has read the counter before the group's first lane bumps it
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (valid && (peers & lt_mask) == 0) wc[dk] = before + __popcll(peers);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    __syncthreads();
+    {  // per-(wave, digit) start inside the block's sorted order
+        uint32_t acc = loff[dg];
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) {
+            const uint32_t t = wcnt[w][dg];
+            wcnt[w][dg] = acc;
+            acc += t;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSortItems; ++k)
+        if (dig[k] != 0xFFFFFFFFu) perm[wc[dig[k]] + lp[k]] = (uint16_t)(wbase + k * 64 + lane);
+    __syncthreads();
     // phase 2: sorted order -> contiguous runs per digit
     const uint32_t nrows = (uint32_t)min((size_t)kSortTile, n - base);
-    for (uint32_t j = threadIdx.x; j < nrows; j += kSortThreads) {
-        const size_t i = base + perm[j];
-        const uint32_t dig = row_digit(W, d, i, gid, words, stride);
-        const uint32_t pos = gbase[dig] + (j - loff[dig]);
-        gid_o[pos] = gid[i];
-        for (int jw = 0; jw < W; ++jw) words_o[(size_t)jw * stride + pos] = words[(size_t)jw * stride + i];
-        lsn_o[pos] = lsn[i];
+    if constexpr (WT == 0) {
+        for (uint32_t j = threadIdx.x; j < nrows; j += kSortThreads) {
+            const size_t i = base + perm[j];
+            const uint32_t dj = row_digit(W, d, i, gid, words, stride);
+            const uint32_t pos = gbase[dj] + (j - loff[dj]);
+            gid_o[pos] = gid[i];
+            for (int jw = 0; jw < W; ++jw) words_o[(size_t)jw * stride + pos] = words[(size_t)jw * stride + i];
+            lsn_o[pos] = lsn[i];
+        }
+        return;
+    } else {
+    // kGather rows per thread at a time, all their loads before any store
+    // (the row's digit is recomputed from the loaded words)
+    constexpr int kGather = 4;
+    for (uint32_t j0 = threadIdx.x; j0 < nrows; j0 += kGather * kSortThreads) {
+        size_t ii[kGather];
+        uint32_t gv[kGather];
+        uint64_t lv[kGather], wv[kGather][WT];
+#pragma unroll
+        for (int u = 0; u < kGather; ++u) {
+            const uint32_t j = j0 + u * kSortThreads;
+            ii[u] = base + perm[j < nrows ? j : j0];
+        }
+#pragma unroll
+        for (int u = 0; u < kGather; ++u) {
+            gv[u] = gid[ii[u]];
+            lv[u] = lsn[ii[u]];
+#pragma unroll
+            for (int jw = 0; jw < WT; ++jw)
+                if (jw < W) wv[u][jw] = words[(size_t)jw * stride + ii[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < kGather; ++u) {
+            const uint32_t j = j0 + u * kSortThreads;
+            if (j >= nrows) break;
+            uint32_t dj;
+            if (d < 8 * W) {
+                const int jw = W - 1 - (d >> 3);
+                uint64_t x = 0;
+#pragma unroll
+                for (int q = 0; q < WT; ++q)
+                    if (q == jw) x = wv[u][q];
+                dj = (uint32_t)(x >> (8 * (d & 7))) & 0xFFu;
+            } else {
+                dj = (gv[u] >> (8 * (d - 8 * W))) & 0xFFu;
+            }
+            const uint32_t pos = gbase[dj] + (j - loff[dj]);
+            gid_o[pos] = gv[u];
+#pragma unroll
+            for (int jw = 0; jw < WT; ++jw)
+                if (jw < W) words_o[(size_t)jw * stride + pos] = wv[u][jw];
+            lsn_o[pos] = lv[u];
+        }
+    }
     }
 }
 
@@ -276,8 +346,17 @@ hipError_t radix_sort_rows(int W, size_t n, uint32_t *gid, uint64_t *words, uint
         k_rs_count<<<nblocks, kSortThreads, 0, s>>>(W, d, n, g0, w0, stride, counts, nblocks);
         e = scan_u32(counts, (size_t)256 * nblocks, scan_tmp, s);
         if (e != hipSuccess) break;
-        k_rs_scatter<<<nblocks, kSortThreads, 0, s>>>(W, d, n, g0, w0, l0, stride, g1, w1, l1,
-                                                       counts, nblocks);
+#define HSC_RS(WT_) k_rs_scatter<WT_><<<nblocks, kSortThreads, 0, s>>>(W, d, n, g0, w0, l0, stride, \
+                                                                   g1, w1, l1, counts, nblocks)
+        if (W == 1)
+            HSC_RS(1);
+        else if (W == 2)
+            HSC_RS(2);
+        else if (W == 3)
+            HSC_RS(3);
+        else
+            HSC_RS(0);
+#undef HSC_RS
         e = hipGetLastError();
         if (e != hipSuccess) break;
         std::swap(g0, g1);
