@@ -174,6 +174,123 @@ def scenarios():
         },
         events=[["begin", "T1"], ["begin", "T2"], ["commit", "T2"], ["commit", "T1"]],
         expect_fail=["T1"])
+    out.update(later_scenarios(uk))
+    return out
+
+
+def enc_int32(v):
+    """One int (4-byte) field: 0x08 + big-endian(v ^ 2^31) (db/types.c)."""
+    return bytes([0x08]) + ((int(v) ^ (1 << 31)) & 0xFFFFFFFF).to_bytes(4, "big")
+
+
+def later_scenarios(uk):
+    """s6, s10-s14.  runit has no .fastinit files, so tables persist across
+    the cases, which run in glob order (s10 .. s15, s1 .. s9): s10-s14 start
+    from empty tables, s6 sees the users rows left by s1-s5 (s2 deleted 99)."""
+    out = {}
+    ng = lambda u: 6000 + u                    # genid after s6's update
+
+    # s6: T1 rewrites every row under a table lock and commits first; T2's
+    # age-99 prefix range sees none of those keys (no row is 99 years old);
+    # T3's id-88 update finds no row, so it is read-only and never checked
+    t1w = []
+    for u in sorted(uk):
+        if u != 99:
+            t1w += upd_same("users", users_keys(u, USERS[u][0], USERS[u][1], ng(u)))
+    r99 = users_keys(99, "nn", 99, 7099)
+    out["s6"] = dict(
+        txns={
+            "T1": dict(reads=[locked("users")], writes=t1w),
+            "T2": dict(reads=[rng_("users", 1, K(99), K(99))], writes=ins("users", r99) + dele("users", r99)),
+            "T3": dict(reads=[rng_("users", 0, K(88), K(88))], writes=[]),
+        },
+        events=[["begin", "T1"], ["begin", "T2"], ["begin", "T3"],
+                ["commit", "T1"], ["commit", "T2"], ["commit", "T3"]],
+        expect_fail=[])
+
+    # s10: mytab (dup KEY_CLASS = class, dup KEY_VALUE = value); each txn sums
+    # one class (prefix range on KEY_CLASS) and inserts into the other
+    def mytab_keys(cls, val, genid):
+        return {0: K(cls) + F.enc_genid(genid), 1: K(val) + F.enc_genid(genid)}
+
+    out["s10"] = dict(
+        txns={
+            "T1": dict(reads=[rng_("mytab", 0, K(1), K(1))], writes=ins("mytab", mytab_keys(2, 30, 3005))),
+            "T2": dict(reads=[rng_("mytab", 0, K(2), K(2))], writes=ins("mytab", mytab_keys(1, 300, 3006))),
+        },
+        events=[["begin", "T1"], ["begin", "T2"], ["commit", "T2"], ["commit", "T1"]],
+        expect_fail=["T1"])
+
+    # s11: colors (KEY_ID = id, dup KEY_COLOR = color), rows cycle Y, B, R.
+    # The reference inserts 9000 rows; restated over the first 90 (the
+    # verdicts depend only on the key order, which the cycle keeps).  A dup
+    # equality scan stops on the first row past the value, so the captured
+    # range ends at that row's key (B -> first R row; R -> first Y row; Y is
+    # the last value: the scan runs off the end, right side open).
+    ids = range(1, 91)
+    colour = {i: "YBR"[(i - 1) % 3] for i in ids}
+    cg = {i: 4000 + i for i in ids}
+    ckey = lambda c, g: F.enc_cstring(c, 8) + F.enc_genid(g)
+
+    def recolour_c(frm, to, gbase):
+        w = []
+        for i in ids:
+            if colour[i] == frm:
+                w += [("upd_dta", "colors", -2, None), ("upd_ix", "colors", 0, K(i).hex()),
+                      ("del_ix", "colors", 1, ckey(frm, cg[i]).hex()),
+                      ("add_ix", "colors", 1, ckey(to, gbase + i).hex())]
+        return w
+
+    first = {c: min(i for i in ids if colour[i] == c) for c in "YBR"}
+    pre = lambda c: F.enc_cstring(c, 8)
+    out["s11"] = dict(
+        txns={
+            "T1": dict(reads=[rng_("colors", 1, pre("R"), ckey("Y", cg[first["Y"]]))],
+                       writes=recolour_c("R", "Y", 10000)),
+            "T2": dict(reads=[rng_("colors", 1, pre("Y"), None, rflag=1)],
+                       writes=recolour_c("Y", "B", 20000)),
+            "T3": dict(reads=[rng_("colors", 1, pre("B"), ckey("R", cg[first["R"]]))],
+                       writes=recolour_c("B", "R", 30000)),
+        },
+        events=[["begin", "T1"], ["begin", "T2"], ["begin", "T3"],
+                ["commit", "T1"], ["commit", "T2"], ["commit", "T3"]],
+        expect_fail=["T2", "T3"])
+
+    # s12: control (KEY_DN = deposit_no) holds one row; the sub-select and the
+    # select scan the whole table (table lock); T2 moves the row's key 1 -> 2
+    out["s12"] = dict(
+        txns={
+            "T1": dict(reads=[locked("control")],
+                       writes=ins("receipt", {0: K(4), 1: K(1) + F.enc_genid(5004)})),
+            "T2": dict(reads=[locked("control")],
+                       writes=[("upd_dta", "control", -2, None), ("del_ix", "control", 0, K(1).hex()),
+                               ("add_ix", "control", 0, K(2).hex())]),
+        },
+        events=[["begin", "T1"], ["begin", "T2"], ["commit", "T2"], ["commit", "T1"]],
+        expect_fail=["T1"])
+
+    # s13: rollover (KEY_ID = id); T1 reads row 2 and updates row 1, T2
+    # updates row 2 and commits first
+    out["s13"] = dict(
+        txns={
+            "T1": dict(reads=[rng_("rollover", 0, K(2), K(2)), rng_("rollover", 0, K(1), K(1))],
+                       writes=upd_same("rollover", {0: K(1)})),
+            "T2": dict(reads=[rng_("rollover", 0, K(2), K(2))], writes=upd_same("rollover", {0: K(2)})),
+        },
+        events=[["begin", "T1"], ["begin", "T2"], ["commit", "T2"], ["commit", "T1"]],
+        expect_fail=["T1"])
+
+    # s14: t1 (ID = int id); an autocommit update (A1, not serializable, so
+    # its own check never fires) moves id 1 -> 11 while T2 has read id 1
+    mv = lambda a, b: [("upd_dta", "t1", -2, None), ("del_ix", "t1", 0, enc_int32(a).hex()),
+                       ("add_ix", "t1", 0, enc_int32(b).hex())]
+    out["s14"] = dict(
+        txns={
+            "T2": dict(reads=[rng_("t1", 0, enc_int32(1), enc_int32(1))], writes=mv(1, 2)),
+            "A1": dict(reads=[rng_("t1", 0, enc_int32(1), enc_int32(1))], writes=mv(1, 11)),
+        },
+        events=[["begin", "T2"], ["begin", "A1"], ["commit", "A1"], ["commit", "T2"]],
+        expect_fail=["T2"])
     return out
 
 

@@ -70,7 +70,7 @@ def test_single_call_entry(validator, oracle_mod):
     assert bdb_osql_serial_check(validator, None) == 0
 
 
-@pytest.mark.parametrize("name", ["s1", "s2", "s3", "s4", "s5", "s9"])
+@pytest.mark.parametrize("name", sorted(serialstep()))
 def test_serialstep_known_answers_gpu(validator, name):
     sc = serialstep()[name]
     rcs = replay(scenario_events(sc), gpu_checker(validator))

@@ -14,7 +14,7 @@ def oracle_checker(o):
     return lambda log, rs: o.check(log, rs)[0]
 
 
-@pytest.mark.parametrize("name", ["s1", "s2", "s3", "s4", "s5", "s9"])
+@pytest.mark.parametrize("name", sorted(serialstep()))
 def test_serialstep_known_answers(oracle_mod, name):
     sc = serialstep()[name]
     rcs = replay(scenario_events(sc), oracle_checker(oracle_mod))
