@@ -2,7 +2,8 @@
 // §8(f) 3): currangearr_coalesce (db/sqlglue.c:305-311) = qsort by
 // currange_cmp (:206-242), currangearr_merge_neighbor (:247-304), again.
 //
-// One thread per read set runs exactly the reference's algorithm, quirks
+// One thread per read set runs exactly the reference's algorithm (large
+// sets with a consistent order sort level-parallel instead, see CoBig), quirks
 // included: the comparator is not a consistent order (two ranges open on the
 // left each sort first; a range without a lower key ties with every range),
 // so the result depends on the sort algorithm -- glibc's qsort is a top-down
@@ -131,10 +132,11 @@ __device__ uint32_t co_merge(const CoView &v, uint32_t *ord, uint32_t n)
     return j + 1;
 }
 
-__global__ __launch_bounds__(128) void k_coalesce(CoView v)
+__global__ __launch_bounds__(128) void k_coalesce(CoView v, const uint32_t *isbig)
 {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= (uint32_t)v.ntxn) return;
+    if (isbig && isbig[t]) return;  // the level-parallel path below
     const uint64_t b = (uint64_t)v.off[t];
     const uint32_t n = (uint32_t)(v.off[t + 1] - v.off[t]);
     uint32_t *ord = v.ord + b, *tmp = v.tmp + b;
@@ -153,12 +155,128 @@ __global__ __launch_bounds__(128) void k_coalesce(CoView v)
     v.count[t] = m;
 }
 
+// ---- large sets whose comparator is a consistent order ----
+// currange_cmp ties a range with every other range of its (table, index) only
+// through a present-but-empty lower key (no lflag, lkeylen == 0) on an unlocked
+// range; two left-open ranges compare "first" both ways, which the merge rule
+// (cmp(left, right) <= 0 takes the left run) treats exactly like equal keys.
+// Without such a tie the order is a total preorder (table rank, locked first,
+// idxnum, left-open first, then lexicographic key bytes + length), so glibc's
+// merge sort returns the unique stable order, and any stable sort does too.
+// The host sends those sets (>= kCoBig ranges) here: each bottom-up merge level
+// is one launch over every element of every such set, an element's output slot
+// = its index in its run + the number of the other run's elements that go
+// before it (a binary search with the same tie rule).  lflag / lkey never
+// change and islocked only turns on, so the check holds for the second sort.
+struct CoBig {
+    const uint32_t *set;  // [nbig] set ids
+    const uint32_t *pre;  // [nbig + 1] element prefix
+    uint32_t nbig, total;
+};
+
+__device__ __forceinline__ uint32_t co_big_of(const CoBig &bg, uint32_t g)
+{
+    uint32_t lo = 0, hi = bg.nbig;  // last k with pre[k] <= g
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (bg.pre[mid] <= g) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_co_big_init(CoView v, CoBig bg)
+{
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= bg.total) return;
+    const uint32_t k = co_big_of(bg, g), t = bg.set[k];
+    const uint32_t i = g - bg.pre[k];
+    const uint64_t r = (uint64_t)v.off[t] + i;
+    v.ord[r] = (uint32_t)r;
+    v.w_rflag[r] = v.rflag[r];
+    v.w_islocked[r] = v.islocked[r];
+    v.w_rkeylen[r] = v.rkeylen[r];
+    v.w_rkey_off[r] = v.rkey_off[r];
+    if (i == 0) v.count[t] = bg.pre[k + 1] - bg.pre[k];
+}
+
+__global__ __launch_bounds__(256) void k_co_big_level(CoView v, CoBig bg, uint32_t w,
+                                                      const uint32_t *src, uint32_t *dst)
+{
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= bg.total) return;
+    const uint32_t k = co_big_of(bg, g), t = bg.set[k];
+    const uint32_t i = g - bg.pre[k], n = v.count[t];
+    if (i >= n) return;
+    const uint64_t b = (uint64_t)v.off[t];
+    const uint32_t a0 = i / (2 * w) * (2 * w);
+    const uint32_t a1 = min(a0 + w, n), b1 = min(a0 + 2 * w, n);
+    const uint32_t x = src[b + i];
+    uint32_t pos;
+    if (i < a1) {  // left run: right elements with cmp(x, y) > 0 go first
+        uint32_t lo = a1, hi = b1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (co_cmp(v, x, src[b + mid]) > 0) lo = mid + 1; else hi = mid;
+        }
+        pos = i + (lo - a1);
+    } else {  // right run: left elements with cmp(y, x) <= 0 go first
+        uint32_t lo = a0, hi = a1;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (co_cmp(v, src[b + mid], x) <= 0) lo = mid + 1; else hi = mid;
+        }
+        pos = a0 + (i - a1) + (lo - a0);
+    }
+    dst[b + pos] = x;
+}
+
+__global__ __launch_bounds__(256) void k_co_big_copy(CoView v, CoBig bg)
+{
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= bg.total) return;
+    const uint32_t k = co_big_of(bg, g), t = bg.set[k];
+    const uint32_t i = g - bg.pre[k];
+    const uint64_t b = (uint64_t)v.off[t];
+    if (i < v.count[t]) v.ord[b + i] = v.tmp[b + i];
+}
+
+__global__ void k_co_big_merge(CoView v, CoBig bg)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= bg.nbig) return;
+    const uint32_t t = bg.set[k];
+    v.count[t] = co_merge(v, v.ord + v.off[t], v.count[t]);
+}
+
+hipError_t co_big_sort(const CoView &v, const CoBig &bg, uint32_t maxn, hipStream_t s)
+{
+    const uint32_t nb = (bg.total + 255) / 256;
+    bool in_tmp = false;
+    for (uint32_t w = 1; w < maxn; w *= 2) {
+        k_co_big_level<<<nb, 256, 0, s>>>(v, bg, w, in_tmp ? v.tmp : v.ord, in_tmp ? v.ord : v.tmp);
+        in_tmp = !in_tmp;
+    }
+    if (in_tmp) k_co_big_copy<<<nb, 256, 0, s>>>(v, bg);
+    return hipGetLastError();
+}
+
 }  // namespace
 
-hipError_t launch_coalesce(const CoView &v, hipStream_t s)
+hipError_t launch_coalesce(const CoView &v, const uint32_t *isbig, const uint32_t *big_set,
+                           const uint32_t *big_pre, uint32_t nbig, uint32_t big_total,
+                           uint32_t big_maxn, hipStream_t s)
 {
     if (v.ntxn <= 0) return hipSuccess;
-    k_coalesce<<<(v.ntxn + 127) / 128, 128, 0, s>>>(v);
+    k_coalesce<<<(v.ntxn + 127) / 128, 128, 0, s>>>(v, nbig ? isbig : nullptr);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || nbig == 0 || big_total == 0) return e;
+    const CoBig bg{big_set, big_pre, nbig, big_total};
+    const uint32_t nb = (big_total + 255) / 256;
+    k_co_big_init<<<nb, 256, 0, s>>>(v, bg);
+    for (int pass = 0; pass < 2; ++pass) {
+        if ((e = co_big_sort(v, bg, big_maxn, s)) != hipSuccess) return e;
+        k_co_big_merge<<<(nbig + 63) / 64, 64, 0, s>>>(v, bg);
+    }
     return hipGetLastError();
 }
 

@@ -124,7 +124,7 @@ struct hsc_ctx {
     std::vector<uint64_t> e_out_lsn;
 
     // replicant coalesce: device inputs / working arrays, host outputs
-    DBuf co_dev[18];
+    DBuf co_dev[21];
     std::vector<int64_t> co_off;
     std::vector<int32_t> co_i32[7];
     std::vector<uint64_t> co_u64[2];
@@ -1787,7 +1787,34 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
     v.w_rkeylen = d[14].as<int32_t>(), v.w_rkey_off = d[15].as<uint64_t>();
     v.ord = d[16].as<uint32_t>(), v.tmp = d[16].as<uint32_t>() + n1;
     v.count = d[17].as<uint32_t>();
-    HIPCHK(c, launch_coalesce(v, s));
+    // large sets without a tie-with-everything range (see hsc_coalesce.hip)
+    std::vector<uint32_t> isbig((size_t)std::max(T, 1), 0), bset, bpre(1, 0);
+    uint32_t bmax = 0;
+    if (!getenv("HSC_CO_SERIAL")) {  // test knob: every set on the per-thread path
+        for (int t = 0; t < T; ++t) {
+            const size_t b = (size_t)rs->txn_off[t], e = (size_t)rs->txn_off[t + 1];
+            if (e - b < kCoBig || bpre.back() + (e - b) > 0xFFFFFFFFull) continue;
+            bool ok = true;
+            for (size_t r = b; r < e && ok; ++r)
+                ok = rs->islocked[r] || rs->lflag[r] || rs->lkeylen[r] > 0;
+            if (!ok) continue;
+            isbig[t] = 1;
+            bset.push_back((uint32_t)t);
+            bpre.push_back(bpre.back() + (uint32_t)(e - b));
+            bmax = std::max(bmax, (uint32_t)(e - b));
+        }
+    }
+    const uint32_t nbig = (uint32_t)bset.size();
+    if (nbig) {
+        HIPCHK(c, d[18].ensure(4 * isbig.size()));
+        HIPCHK(c, d[19].ensure(4 * (size_t)nbig));
+        HIPCHK(c, d[20].ensure(4 * ((size_t)nbig + 1)));
+        HIPCHK(c, hipMemcpyAsync(d[18].p, isbig.data(), 4 * isbig.size(), hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(d[19].p, bset.data(), 4 * (size_t)nbig, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(d[20].p, bpre.data(), 4 * ((size_t)nbig + 1), hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(c, launch_coalesce(v, d[18].as<uint32_t>(), d[19].as<uint32_t>(), d[20].as<uint32_t>(),
+                              nbig, bpre.back(), bmax, s));
     std::vector<uint32_t> cnt(T), ord(nr);
     std::vector<int32_t> wrf(nr), wlk(nr), wrl(nr);
     std::vector<uint64_t> wro(nr);

@@ -254,7 +254,12 @@ struct CoView {
     uint32_t *ord, *tmp;                       // [nranges] coalesced order per set
     uint32_t *count;                           // [ntxn] ranges left per set
 };
-hipError_t launch_coalesce(const CoView &v, hipStream_t s);
+// isbig[t] != 0: set t (one of big_set[0 .. nbig), elements big_pre[k] ..
+// big_pre[k + 1], at most big_maxn per set) takes the level-parallel sort.
+constexpr uint32_t kCoBig = 256;
+hipError_t launch_coalesce(const CoView &v, const uint32_t *isbig, const uint32_t *big_set,
+                           const uint32_t *big_pre, uint32_t nbig, uint32_t big_total,
+                           uint32_t big_maxn, hipStream_t s);
 
 // Narrow tiles keep the chunk histogram tile-major: hist[t * hist_stride(G) + g].
 __host__ __device__ inline uint32_t hist_stride(uint32_t G) { return (G + 7) & ~7u; }

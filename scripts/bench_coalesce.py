@@ -1,7 +1,8 @@
 """Replicant coalesce throughput: GPU hsc_coalesce_readsets
 (host arrays in and out: upload, kernel, download, compaction) vs the CPU
 restatement oracle/coalesce_oracle.c (one core), on config-2-like batches of
-many small read sets and on a few very large read sets.  Checks equality."""
+many small read sets and on a few very large read sets (with and without the
+comparator's tie-with-everything ranges).  Checks equality."""
 import json, os, sys, time
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -13,7 +14,9 @@ from comdb2_amd.hsc import Validator
 v = Validator(0)
 res = {}
 for name, kw in (("100k sets x <=20 ranges", dict(ntxn=100_000, max_ranges=20)),
-                 ("8 sets x <=200k ranges", dict(ntxn=8, max_ranges=200_000))):
+                 ("8 sets x <=200k ranges", dict(ntxn=8, max_ranges=200_000)),
+                 ("8 sets x <=200k ranges, no empty lower key (level-parallel sort)",
+                  dict(ntxn=8, max_ranges=200_000, empty_lo=0.0))):
     rs = random_readsets(7, **kw)
     t0 = time.perf_counter(); want = oracle.coalesce(rs); cpu = time.perf_counter() - t0
     v.coalesce(rs)  # warm

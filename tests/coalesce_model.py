@@ -135,9 +135,12 @@ def model_rows(sets: List[List[CR]]):
               c.rkeylen) for c in s] for s in sets]
 
 
-def random_readsets(seed: int, ntxn: int = 300, max_ranges: int = 40, tables=("ta", "tb", "tc")):
+def random_readsets(seed: int, ntxn: int = 300, max_ranges: int = 40, tables=("ta", "tb", "tc"),
+                    empty_lo: float = 0.03, min_ranges: int = 0):
     """Read sets full of coalesce corner cases: shared prefixes, equal keys,
-    prefix (shorter) bounds, open ends, table locks, several indexes."""
+    prefix (shorter) bounds, open ends, table locks, several indexes.
+    empty_lo: share of present-but-empty lower keys (the comparator's
+    tie-with-everything case); 0 gives sets with a consistent order."""
     from comdb2_amd.formats import Range
     rng = np.random.default_rng(seed)
     sets, snaps = [], []
@@ -148,7 +151,7 @@ def random_readsets(seed: int, ntxn: int = 300, max_ranges: int = 40, tables=("t
 
     for _ in range(ntxn):
         rs = []
-        for _ in range(int(rng.integers(0, max_ranges))):
+        for _ in range(int(rng.integers(min_ranges, max_ranges))):
             tb = tables[int(rng.integers(0, len(tables)))]
             u = rng.random()
             if u < 0.04:
@@ -161,7 +164,7 @@ def random_readsets(seed: int, ntxn: int = 300, max_ranges: int = 40, tables=("t
             rf = 1 if rng.random() < 0.08 else 0
             if rng.random() < 0.3:
                 hi = lo
-            if not lf and rng.random() < 0.03:
+            if not lf and rng.random() < empty_lo:
                 lo = b""  # present but empty lower key: compares as the NULL key
             rs.append(Range(tb, ix, None if lf else lo, None if rf else hi, lf, rf, 0))
         sets.append(rs)
