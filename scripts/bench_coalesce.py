@@ -17,6 +17,8 @@ for name, kw in (("100k sets x <=20 ranges", dict(ntxn=100_000, max_ranges=20)),
                  ("8 sets x <=200k ranges", dict(ntxn=8, max_ranges=200_000)),
                  ("8 sets x <=200k ranges, no empty lower key (level-parallel sort)",
                   dict(ntxn=8, max_ranges=200_000, empty_lo=0.0))):
+    if len(sys.argv) > 1 and sys.argv[1] not in name:  # case filter (profiling)
+        continue
     rs = random_readsets(7, **kw)
     t0 = time.perf_counter(); want = oracle.coalesce(rs); cpu = time.perf_counter() - t0
     v.coalesce(rs)  # warm
