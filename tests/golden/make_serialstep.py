@@ -184,8 +184,8 @@ def enc_int32(v):
 
 
 def later_scenarios(uk):
-    """s6, s10-s14.  runit has no .fastinit files, so tables persist across
-    the cases, which run in glob order (s10 .. s15, s1 .. s9): s10-s14 start
+    """s6, s10-s15.  runit has no .fastinit files, so tables persist across
+    the cases, which run in glob order (s10 .. s15, s1 .. s9): s10-s15 start
     from empty tables, s6 sees the users rows left by s1-s5 (s2 deleted 99)."""
     out = {}
     ng = lambda u: 6000 + u                    # genid after s6's update
@@ -291,6 +291,36 @@ def later_scenarios(uk):
         },
         events=[["begin", "T2"], ["begin", "A1"], ["commit", "A1"], ["commit", "T2"]],
         expect_fail=["T2"])
+
+    # s15: intv (KEY_ID = id, dup KEY_YM = intervalym, dup KEY_DS =
+    # intervalds), two rounds of the s3-style skew, once over each interval
+    # index.  Stand-in key encoding: the interval as an int64 count of months /
+    # milliseconds in the A9 int64 format (order-preserving, which is all the
+    # byte comparisons of the check see); not comdb2's interval on-disk format.
+    ym = {i: 13 * i for i in range(1, 6)}                       # '01-01' .. '05-05'
+    ds = {i: ((i * 24 + i) * 3600 + i * 61) * 1000 + 10 * i for i in range(1, 6)}
+
+    def intv_keys(i, g):
+        return {0: K(i), 1: K(ym[i]) + F.enc_genid(g), 2: K(ds[i]) + F.enc_genid(g)}
+
+    def upd_rows(ids, g):
+        w = []
+        for i in ids:
+            w += upd_same("intv", intv_keys(i, g + i))
+        return w
+
+    ym_lo, ym_hi = 2 * 12 + 10, 4 * 12                         # '02-10', '04-00'
+    ds_lo, ds_hi = (2 * 24 + 10) * 3600 * 1000, 4 * 24 * 3600 * 1000
+    out["s15"] = dict(
+        txns={
+            "T1a": dict(reads=[rng_("intv", 1, None, K(ym_lo), lflag=1)], writes=upd_rows((4, 5), 8100)),
+            "T2a": dict(reads=[rng_("intv", 1, K(ym_hi), None, rflag=1)], writes=upd_rows((1, 2), 8150)),
+            "T1b": dict(reads=[rng_("intv", 2, None, K(ds_lo), lflag=1)], writes=upd_rows((4, 5), 8200)),
+            "T2b": dict(reads=[rng_("intv", 2, K(ds_hi), None, rflag=1)], writes=upd_rows((1, 2), 8250)),
+        },
+        events=[["begin", "T1a"], ["begin", "T2a"], ["commit", "T1a"], ["commit", "T2a"],
+                ["begin", "T1b"], ["begin", "T2b"], ["commit", "T1b"], ["commit", "T2b"]],
+        expect_fail=["T2a", "T2b"])
     return out
 
 
