@@ -129,14 +129,20 @@ __device__ __forceinline__ void co_put(const CoView &v, const CoRow &p)
 
 // currangearr_merge_neighbor (db/sqlglue.c:247-304) over ord[0 .. n); returns
 // the new length
-__device__ uint32_t co_merge(const CoView &v, uint32_t *ord, uint32_t n)
+// RUN: stop at the first row of another (table rank, idxnum) and return the
+// survivors of ord[0 .. that row) (the level-parallel path's runs); *plock =
+// the last survivor's lock bit.
+template <bool RUN = false>
+__device__ uint32_t co_merge(const CoView &v, uint32_t *ord, uint32_t n, int *plock = nullptr)
 {
     if (!n) return 0;
     CoRow p = co_row(v, ord[0]);
     CoRow nx = n > 1 ? co_row(v, ord[1]) : p;
+    const int rtb = p.tb, rix = p.ix;
     uint32_t j = 0;
     for (uint32_t i = 1; i < n; ++i) {
         const CoRow q = nx;
+        if (RUN && (q.tb != rtb || q.ix != rix)) break;
         if (i + 1 < n) nx = co_row(v, ord[i + 1]);
         bool absorbed = false;
         if (p.tb == q.tb) {
@@ -164,6 +170,7 @@ __device__ uint32_t co_merge(const CoView &v, uint32_t *ord, uint32_t n)
         p = q;
     }
     co_put(v, p);
+    if (plock) *plock = p.lk;
     return j + 1;
 }
 
@@ -275,12 +282,103 @@ __global__ __launch_bounds__(256) void k_co_big_copy(CoView v, CoBig bg)
     if (i < v.count[t]) v.ord[b + i] = v.tmp[b + i];
 }
 
-__global__ void k_co_big_merge(CoView v, CoBig bg)
+// Merge scan of the large sets, split into runs of equal (table rank,
+// idxnum).  Rows of another table never merge; a run's first row follows the
+// previous run's last survivor p, which either starts a new survivor or -- if
+// p is locked -- is absorbed with everything after it in p's table (p's
+// fields do not change then).  The host admits only sets whose locked ranges
+// are open at both ends, so a locked survivor also absorbs the rest of its own
+// run: it is always its run's last survivor.  Runs merge independently
+// (k_co_big_runs: survivors compacted to the run's head, count and last lock
+// bit in tmp[run head]); k_co_big_join then drops the runs a locked survivor
+// of their table absorbed and packs the rest, in order (one workgroup per set).
+__device__ __forceinline__ uint64_t co_runkey(const CoView &v, uint32_t r)
 {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= bg.nbig) return;
-    const uint32_t t = bg.set[k];
-    v.count[t] = co_merge(v, v.ord + v.off[t], v.count[t]);
+    return (uint64_t)(uint32_t)v.tbrank[v.table[r]] << 32 | (uint32_t)v.idxnum[r];
+}
+
+__global__ __launch_bounds__(256) void k_co_big_runs(CoView v, CoBig bg)
+{
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= bg.total) return;
+    const uint32_t k = co_big_of(bg, g), t = bg.set[k];
+    const uint32_t i = g - bg.pre[k], n = v.count[t];
+    if (i >= n) return;
+    const uint64_t b = (uint64_t)v.off[t];
+    uint32_t *ord = v.ord + b;
+    // rows keep their run while runs compact (a run writes only its own rows
+    // into its own slots), so the neighbour test below is race-free
+    const bool head = i == 0 || co_runkey(v, ord[i - 1]) != co_runkey(v, ord[i]);
+    uint32_t info = 0;
+    if (head) {
+        int lk = 0;
+        const uint32_t c = co_merge<true>(v, ord + i, n - i, &lk);
+        info = c | (uint32_t)lk << 31;
+    }
+    v.tmp[b + i] = info;
+}
+
+constexpr int kJoinT = 256;
+
+__global__ __launch_bounds__(kJoinT) void k_co_big_join(CoView v, CoBig bg, uint32_t *runpos,
+                                                        uint32_t *runinfo)
+{
+    __shared__ uint32_t lds[kJoinT / 64];
+    __shared__ uint32_t nruns, mtot;
+    const uint32_t k = blockIdx.x, t = bg.set[k];
+    const uint32_t n = v.count[t];
+    const uint64_t b = (uint64_t)v.off[t];
+    uint32_t *ord = v.ord + b, *tmp = v.tmp + b, *rp = runpos + b, *ri = runinfo + 2 * b;
+    // run heads, in order
+    uint32_t base = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += kJoinT) {
+        const uint32_t i = c0 + threadIdx.x;
+        const uint32_t info = i < n ? tmp[i] : 0;
+        uint32_t tot;
+        const uint32_t pre = block_excl_scan<kJoinT>(info != 0, lds, tot);
+        if (info) {
+            rp[base + pre] = i;
+            ri[base + pre] = info;
+        }
+        base += tot;
+    }
+    __syncthreads();
+    // sequential over runs: drop the absorbed ones, output offsets of the rest
+    if (threadIdx.x == 0) {
+        int64_t locked_tb = -1;
+        uint32_t acc = 0;
+        for (uint32_t r = 0; r < base; ++r) {
+            const uint32_t info = ri[r];
+            const int64_t tb = v.tbrank[v.table[ord[rp[r]]]];
+            if (tb == locked_tb) {
+                ri[r] = ~0u;
+                continue;
+            }
+            ri[r] = acc;
+            acc += info & 0x7FFFFFFFu;
+            if (info >> 31) locked_tb = tb;
+            tmp[rp[r]] = info & 0x7FFFFFFFu;  // survivors of the run, for the copy
+        }
+        nruns = base;
+        mtot = acc;
+    }
+    __syncthreads();
+    const uint32_t R = nruns, m = mtot;
+    // survivors staged in the second half of the set's scratch [2b, 2b + 2n)
+    uint32_t *out = ri + n;
+    for (uint32_t i = threadIdx.x; i < n; i += kJoinT) {
+        uint32_t lo = 0, hi = R;  // last run with head <= i
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (rp[mid] <= i) lo = mid; else hi = mid;
+        }
+        const uint32_t h = rp[lo], dst = ri[lo];
+        if (dst == ~0u) continue;
+        if (i - h < tmp[h]) out[dst + (i - h)] = ord[i];
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < m; i += kJoinT) ord[i] = out[i];
+    if (threadIdx.x == 0) v.count[t] = m;
 }
 
 hipError_t co_big_sort(const CoView &v, const CoBig &bg, uint32_t maxn, hipStream_t s)
@@ -299,7 +397,8 @@ hipError_t co_big_sort(const CoView &v, const CoBig &bg, uint32_t maxn, hipStrea
 
 hipError_t launch_coalesce(const CoView &v, const uint32_t *isbig, const uint32_t *big_set,
                            const uint32_t *big_pre, uint32_t nbig, uint32_t big_total,
-                           uint32_t big_maxn, hipStream_t s)
+                           uint32_t big_maxn, uint32_t *big_runpos, uint32_t *big_scratch,
+                           hipStream_t s)
 {
     if (v.ntxn <= 0) return hipSuccess;
     k_coalesce<<<(v.ntxn + 127) / 128, 128, 0, s>>>(v, nbig ? isbig : nullptr);
@@ -310,7 +409,8 @@ hipError_t launch_coalesce(const CoView &v, const uint32_t *isbig, const uint32_
     k_co_big_init<<<nb, 256, 0, s>>>(v, bg);
     for (int pass = 0; pass < 2; ++pass) {
         if ((e = co_big_sort(v, bg, big_maxn, s)) != hipSuccess) return e;
-        k_co_big_merge<<<(nbig + 63) / 64, 64, 0, s>>>(v, bg);
+        k_co_big_runs<<<nb, 256, 0, s>>>(v, bg);
+        k_co_big_join<<<nbig, kJoinT, 0, s>>>(v, bg, big_runpos, big_scratch);
     }
     return hipGetLastError();
 }

@@ -124,7 +124,7 @@ struct hsc_ctx {
     std::vector<uint64_t> e_out_lsn;
 
     // replicant coalesce: device inputs / working arrays, host outputs
-    DBuf co_dev[21];
+    DBuf co_dev[23];
     std::vector<int64_t> co_off;
     std::vector<int32_t> co_i32[7];
     std::vector<uint64_t> co_u64[2];
@@ -1795,8 +1795,9 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
             const size_t b = (size_t)rs->txn_off[t], e = (size_t)rs->txn_off[t + 1];
             if (e - b < kCoBig || bpre.back() + (e - b) > 0xFFFFFFFFull) continue;
             bool ok = true;
-            for (size_t r = b; r < e && ok; ++r)
-                ok = rs->islocked[r] || rs->lflag[r] || rs->lkeylen[r] > 0;
+            for (size_t r = b; r < e && ok; ++r)  // no tie-with-everything range; locks open
+                ok = (rs->islocked[r] || rs->lflag[r] || rs->lkeylen[r] > 0) &&
+                     (!rs->islocked[r] || (rs->lflag[r] && rs->rflag[r]));
             if (!ok) continue;
             isbig[t] = 1;
             bset.push_back((uint32_t)t);
@@ -1809,12 +1810,14 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
         HIPCHK(c, d[18].ensure(4 * isbig.size()));
         HIPCHK(c, d[19].ensure(4 * (size_t)nbig));
         HIPCHK(c, d[20].ensure(4 * ((size_t)nbig + 1)));
+        HIPCHK(c, d[21].ensure(4 * n1));
+        HIPCHK(c, d[22].ensure(8 * n1));
         HIPCHK(c, hipMemcpyAsync(d[18].p, isbig.data(), 4 * isbig.size(), hipMemcpyHostToDevice, s));
         HIPCHK(c, hipMemcpyAsync(d[19].p, bset.data(), 4 * (size_t)nbig, hipMemcpyHostToDevice, s));
         HIPCHK(c, hipMemcpyAsync(d[20].p, bpre.data(), 4 * ((size_t)nbig + 1), hipMemcpyHostToDevice, s));
     }
     HIPCHK(c, launch_coalesce(v, d[18].as<uint32_t>(), d[19].as<uint32_t>(), d[20].as<uint32_t>(),
-                              nbig, bpre.back(), bmax, s));
+                              nbig, bpre.back(), bmax, d[21].as<uint32_t>(), d[22].as<uint32_t>(), s));
     std::vector<uint32_t> cnt(T), ord(nr);
     std::vector<int32_t> wrf(nr), wlk(nr), wrl(nr);
     std::vector<uint64_t> wro(nr);

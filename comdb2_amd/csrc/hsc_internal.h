@@ -259,7 +259,8 @@ struct CoView {
 constexpr uint32_t kCoBig = 256;
 hipError_t launch_coalesce(const CoView &v, const uint32_t *isbig, const uint32_t *big_set,
                            const uint32_t *big_pre, uint32_t nbig, uint32_t big_total,
-                           uint32_t big_maxn, hipStream_t s);
+                           uint32_t big_maxn, uint32_t *big_runpos /* [nranges] */,
+                           uint32_t *big_scratch /* [2 nranges] */, hipStream_t s);
 
 // Narrow tiles keep the chunk histogram tile-major: hist[t * hist_stride(G) + g].
 __host__ __device__ inline uint32_t hist_stride(uint32_t G) { return (G + 7) & ~7u; }
