@@ -331,7 +331,11 @@ int hsc_rw_edges(hsc_ctx *ctx, const hsc_readsets *rs, size_t *n_pairs, const ui
  * surviving range's rkeylen; a range open at both ends becomes a table lock
  * that absorbs its table's other ranges).  Output arrays are owned by the
  * context until its next coalesce; key offsets point into rs->keys.  Every
- * range must name a table (the reference's strcmp would crash otherwise). */
+ * range must name a table (the reference's strcmp would crash otherwise).
+ * Sets of >= 256 ranges whose comparator is a consistent order (no unlocked
+ * range with a present-but-empty lower key; locked ranges open at both ends)
+ * sort and merge level-parallel with the same result; HSC_CO_SERIAL=1 in the
+ * environment forces the per-set path (testing). */
 typedef struct hsc_coalesced {
     int ntxn;
     const int64_t *txn_off;   /* [ntxn+1] */
