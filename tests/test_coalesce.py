@@ -5,11 +5,13 @@ unpinned by the reference (no test of currangearr_coalesce there)."""
 import os
 import sys
 
+import numpy as np
 import pytest
 
 from comdb2_amd.formats import Range, ReadSets
 
 sys.path.insert(0, os.path.dirname(__file__))
+import coalesce_model  # noqa: E402
 from coalesce_model import as_rows, coalesce_readsets, model_rows, random_readsets  # noqa: E402
 
 
@@ -73,3 +75,62 @@ def test_empty_and_single(oracle_lib):
     rs = one([[], [Range("ta", 0, b"a", b"b")], []])
     out = oracle_lib.coalesce(rs)
     assert list(out.txn_off) == [0, 0, 1, 1]
+
+
+def _run_split_merge(m, arr):
+    """The GPU large-set merge (hsc_coalesce.hip k_co_big_runs/k_co_big_join):
+    merge each run of equal (table, idxnum) on its own, then drop the runs that
+    follow a locked survivor of their table."""
+    runs, start = [], 0
+    for i in range(1, len(arr) + 1):
+        if i == len(arr) or (arr[i].tbname, arr[i].idxnum) != (arr[start].tbname, arr[start].idxnum):
+            runs.append(m.merge_neighbor(arr[start:i]))
+            start = i
+    out, locked_tb = [], None
+    for r in runs:
+        if r[0].tbname == locked_tb:
+            continue
+        out += r
+        if r[-1].islocked:
+            locked_tb = r[-1].tbname
+    return out
+
+
+@pytest.mark.parametrize("seed,ntables", [(21, 3), (22, 12), (23, 40)])
+def test_level_parallel_coalesce_model(seed, ntables):
+    """CPU pin of the GPU large-set path: for sets with a consistent order (no
+    unlocked present-but-empty lower key; locked ranges open at both ends) a
+    stable sort equals glibc's msort, and the run-split merge equals
+    currangearr_merge_neighbor, through both coalesce passes."""
+    import copy
+    import functools
+
+    from coalesce_model import Model
+    rs = random_readsets(seed, ntxn=12, max_ranges=500, min_ranges=100, empty_lo=0.0,
+                         tables=tuple(f"t{i:02d}" for i in range(ntables)))
+    m = Model(bytes(np.asarray(rs.keys, np.uint8)))
+    fields = lambda a: [(c.tbname, c.idxnum, c.lflag, c.rflag, c.islocked, c.lkey, c.lkeylen,
+                         c.rkey, c.rkeylen) for c in a]
+    def tie_cmp(a, b):  # two left-open ranges: "first" both ways = a tie under the merge rule
+        r = m.cmp(a, b)
+        return 0 if r < 0 and m.cmp(b, a) < 0 else r
+
+    checked = 0
+    for t in range(rs.ntxn):
+        arr = []
+        for r in range(int(rs.txn_off[t]), int(rs.txn_off[t + 1])):
+            lk, rk = int(rs.lkeylen[r]), int(rs.rkeylen[r])
+            arr.append(coalesce_model.CR(rs.tbnames[int(rs.table[r])], int(rs.idxnum[r]),
+                                         int(rs.lflag[r]), int(rs.rflag[r]), int(rs.islocked[r]),
+                                         int(rs.lkey_off[r]) if lk > 0 else None, lk,
+                                         int(rs.rkey_off[r]) if rk > 0 else None, rk))
+        if not all((c.islocked or c.lflag or c.lkeylen > 0) and
+                   (not c.islocked or (c.lflag and c.rflag)) for c in arr):
+            continue
+        want = m.coalesce(copy.deepcopy(arr))
+        got = copy.deepcopy(arr)
+        for _ in range(2):
+            got = _run_split_merge(m, sorted(got, key=functools.cmp_to_key(tie_cmp)))
+        assert fields(got) == fields(want)
+        checked += 1
+    assert checked == rs.ntxn
