@@ -46,8 +46,11 @@ __device__ int co_cmp(const CoView &v, uint32_t i, uint32_t j)
     if (v.idxnum[i] != v.idxnum[j]) return v.idxnum[i] - v.idxnum[j];
     if (v.lflag[i]) return -1;
     if (v.lflag[j]) return 1;
+    // the lower keys compare only when both pointers are non-NULL (a NULL one,
+    // HSC_KEY_NULL, ties with every range of the index; a present empty one
+    // sorts before the longer keys)
     const int ki = v.lkeylen[i], kj = v.lkeylen[j];
-    if (ki > 0 && kj > 0) {
+    if (v.lkey_off[i] != HSC_KEY_NULL && v.lkey_off[j] != HSC_KEY_NULL) {
         const int rc = keycmp(v, v.lkey_off[i], v.lkey_off[j], ki < kj ? ki : kj);
         return rc ? rc : ki - kj;
     }
@@ -151,7 +154,7 @@ __device__ uint32_t co_merge(const CoView &v, uint32_t *ord, uint32_t n, int *pl
                 if (q.lf || p.rf || keycmp(v, q.lko, p.ro, m) <= 0) {
                     if (p.rf || q.rf) {
                         p.rf = 1;
-                        p.ro = 0;
+                        p.ro = HSC_KEY_NULL;  // free(p->rkey); p->rkey = NULL
                         p.rl = 0;
                     } else if (keycmp(v, p.ro, q.ro, p.rl < q.rl ? p.rl : q.rl) < 0) {
                         v.w_rkey_off[q.r] = p.ro;  // pointer swap, lengths stay
@@ -199,7 +202,7 @@ __global__ __launch_bounds__(128) void k_coalesce(CoView v, const uint32_t *isbi
 
 // ---- large sets whose comparator is a consistent order ----
 // currange_cmp ties a range with every other range of its (table, index) only
-// through a present-but-empty lower key (no lflag, lkeylen == 0) on an unlocked
+// through a NULL lower key (no lflag, lkey_off == HSC_KEY_NULL) on an unlocked
 // range; two left-open ranges compare "first" both ways, which the merge rule
 // (cmp(left, right) <= 0 takes the left run) treats exactly like equal keys.
 // Without such a tie the order is a total preorder (table rank, locked first,

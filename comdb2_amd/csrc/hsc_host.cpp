@@ -948,8 +948,8 @@ static int marshal_readsets(hsc_ctx *c, const hsc_readsets *rs)
             const int32_t tb = rs->table[r];
             x.tid = (tb >= 0 && tb < rs->ntbnames) ? tmap[tb] : -1;
             x.idxnum = rs->idxnum[r];
-            x.lkey = rs->keys + rs->lkey_off[r];
-            x.rkey = rs->keys + rs->rkey_off[r];
+            x.lkey = rs->lkey_off[r] == HSC_KEY_NULL ? nullptr : rs->keys + rs->lkey_off[r];
+            x.rkey = rs->rkey_off[r] == HSC_KEY_NULL ? nullptr : rs->keys + rs->rkey_off[r];
             x.lkeylen = rs->lkeylen[r];
             x.rkeylen = rs->rkeylen[r];
             x.lflag = rs->lflag[r];
@@ -1099,7 +1099,14 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
     if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
     HIPCHK(c, select_lane(c));
     const int rc = probe_lane(c, b);
-    if (rc == HSC_OK) HIPCHK(c, lane_done(c));
+    // the lane's done event fences whatever probe_lane launched, also when it
+    // failed part way: a later take-over of the lane or a window rebuild
+    // waits on it before touching the lane's scratch
+    const hipError_t e = lane_done(c);
+    if (e != hipSuccess) {
+        (void)hipStreamSynchronize(c->stream);
+        if (rc == HSC_OK) return fail(c, HSC_EDEVICE, "lane_done", e);
+    }
     return rc;
 }
 
@@ -1740,6 +1747,8 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
     (void)hipSetDevice(c->device);
     const int T = rs->ntxn;
     const size_t nr = T ? (size_t)rs->txn_off[T] : 0;
+    // rows are indexed as uint32 on the device (ord / tmp / big-set offsets)
+    if (nr > 0xFFFFFFFFull) return fail(c, HSC_EINVAL, "coalesce: more than 2^32 - 1 ranges");
     // strcmp rank of every table name (equal names share a rank)
     std::vector<int32_t> rank(std::max(rs->ntbnames, 1), 0);
     {
@@ -1757,6 +1766,9 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
             return fail(c, HSC_EINVAL, "coalesce: a range names no table");
     uint64_t nkeys = 0;
     for (size_t r = 0; r < nr; ++r) {
+        if ((rs->lkeylen[r] > 0 && rs->lkey_off[r] == HSC_KEY_NULL) ||
+            (rs->rkeylen[r] > 0 && rs->rkey_off[r] == HSC_KEY_NULL))
+            return fail(c, HSC_EINVAL, "coalesce: a NULL key with a nonzero length");
         if (rs->lkeylen[r] > 0) nkeys = std::max<uint64_t>(nkeys, rs->lkey_off[r] + rs->lkeylen[r]);
         if (rs->rkeylen[r] > 0) nkeys = std::max<uint64_t>(nkeys, rs->rkey_off[r] + rs->rkeylen[r]);
     }
@@ -1796,7 +1808,7 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
             if (e - b < kCoBig || bpre.back() + (e - b) > 0xFFFFFFFFull) continue;
             bool ok = true;
             for (size_t r = b; r < e && ok; ++r)  // no tie-with-everything range; locks open
-                ok = (rs->islocked[r] || rs->lflag[r] || rs->lkeylen[r] > 0) &&
+                ok = (rs->islocked[r] || rs->lflag[r] || rs->lkey_off[r] != HSC_KEY_NULL) &&
                      (!rs->islocked[r] || (rs->lflag[r] && rs->rflag[r]));
             if (!ok) continue;
             isbig[t] = 1;

@@ -91,7 +91,9 @@ int decode_serial_msgs(const hsc_serial_msgs *m, DecodedReadSets &out, std::stri
             }
             const int32_t islocked = r.i32();
             int32_t idxnum = -2, lflag = 1, rflag = 1, lkeylen = 0, rkeylen = 0;
-            uint64_t lkey_off = out.keys.size(), rkey_off = out.keys.size();
+            // keys the message does not carry stay NULL (currange_new,
+            // db/sqlglue.c:163-175); carried ones are malloc'd, even when empty
+            uint64_t lkey_off = HSC_KEY_NULL, rkey_off = HSC_KEY_NULL;
             if (!islocked) {
                 idxnum = r.i32();
                 lflag = r.i32();

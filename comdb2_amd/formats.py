@@ -357,6 +357,11 @@ class Range:
         return Range(tb, -2, None, None, 1, 1, 1)
 
 
+# HSC_KEY_NULL (include/hip_serial.h): a key offset standing for a NULL key
+# pointer; any other offset is a present key, also when it is empty.
+KEY_NULL = (1 << 64) - 1
+
+
 @dataclasses.dataclass
 class ReadSets:
     txn_off: np.ndarray    # int64[ntxn+1]
@@ -401,7 +406,7 @@ class ReadSets:
                 cols["rflag"].append(r.rflag)
                 cols["islocked"].append(r.islocked)
                 for side, k in (("l", r.lkey), ("r", r.rkey)):
-                    cols[side + "key_off"].append(len(keys))
+                    cols[side + "key_off"].append(KEY_NULL if k is None else len(keys))
                     cols[side + "keylen"].append(0 if k is None else len(k))
                     if k is not None:
                         keys += k

@@ -18,7 +18,7 @@ from typing import List, Optional, Sequence
 
 import numpy as np
 
-from .formats import LLog, Range, ReadSets
+from .formats import KEY_NULL, LLog, Range, ReadSets
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("HSC_LIB") or os.path.join(_HERE, "lib", "libhsc.so")
@@ -394,8 +394,9 @@ class Validator:
         cols = {k: arr(getattr(R, k), nr, np.int32) for k in
                 ("table", "idxnum", "lflag", "rflag", "islocked", "lkeylen", "rkeylen")}
         lo, ro = arr(R.lkey_off, nr, np.uint64), arr(R.rkey_off, nr, np.uint64)
-        nk = int(max([int(lo[i]) + int(cols["lkeylen"][i]) for i in range(nr)] +
-                     [int(ro[i]) + int(cols["rkeylen"][i]) for i in range(nr)] + [1]))
+        nk = int(max([int(lo[i]) + int(cols["lkeylen"][i]) for i in range(nr) if lo[i] != KEY_NULL] +
+                     [int(ro[i]) + int(cols["rkeylen"][i]) for i in range(nr) if ro[i] != KEY_NULL] +
+                     [1]))
         return ReadSets(txn_off=txn_off, snap=arr(R.snap, nt, np.uint64), lkey_off=lo,
                         rkey_off=ro, keys=arr(R.keys, nk, np.uint8),
                         tbnames=[R.tbnames[i].decode() for i in range(R.ntbnames)], **cols)

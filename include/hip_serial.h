@@ -110,7 +110,18 @@ typedef struct hsc_llog {
  * Flat read sets: many CurRangeArr's as struct-of-arrays (the OSQL_SERIAL
  * payload of db/osqlcomm.c:909-993 after decode, without heap CurRange's).
  * Ranges of read set t are rows [txn_off[t], txn_off[t+1]) in array order.
+ *
+ * Key pointers: lkey_off / rkey_off == HSC_KEY_NULL stands for a NULL key
+ * pointer (its length must be 0; currange_new leaves keys NULL,
+ * db/sqlglue.c:163-175); any other offset is a present key, also with length
+ * 0 (serial_readset_get malloc(0)s one, db/osqlcomm.c:974).  Only the
+ * coalesce comparator tells them apart: currange_cmp compares the lower keys
+ * only when both pointers are non-NULL (db/sqlglue.c:228-236), so a NULL one
+ * ties with every range of its index while a present empty key sorts before
+ * the longer ones.  The check itself reads at most min(len, keylen) bytes and
+ * treats both alike (db/glue.c:2951-2958).
  * ------------------------------------------------------------------------ */
+#define HSC_KEY_NULL UINT64_MAX
 typedef struct hsc_readsets {
     int ntxn;
     const int64_t *txn_off;   /* [ntxn+1]                                     */

@@ -13,7 +13,8 @@
  * over the flat read-set layout of include/hip_serial.h (hsc_readsets):
  *   - tbname = tbnames[table] compared with strcmp (table must be valid: a
  *     NULL tbname would crash merge_neighbor's strcmp in the reference);
- *   - a key is present iff its length is > 0 (the reference's NULL pointers);
+ *   - a key pointer is NULL iff its offset is HSC_KEY_NULL (~0); any other
+ *     offset is a present key, also when empty (include/hip_serial.h);
  *   - the right-key pointer swap of :265-270 moves only the key (offset),
  *     never rkeylen: p keeps its own length over q's key bytes (reading past
  *     the end of the keys buffer yields 0 bytes here; heap bytes there).
@@ -24,6 +25,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+
+#define CO_KEY_NULL UINT64_MAX /* HSC_KEY_NULL of include/hip_serial.h */
 
 struct co_rng {
     int32_t table, idxnum, lflag, rflag, islocked, lkeylen, rkeylen;
@@ -62,7 +65,7 @@ static int co_cmp(const struct co_ctx *c, const struct co_rng *l, const struct c
     if (l->idxnum != r->idxnum) return l->idxnum - r->idxnum;
     if (l->lflag) return -1;
     if (r->lflag) return 1;
-    if (l->lkeylen > 0 && r->lkeylen > 0) {
+    if (l->lkey_off != CO_KEY_NULL && r->lkey_off != CO_KEY_NULL) { /* l->lkey && r->lkey */
         rc = keycmp(c, l->lkey_off, r->lkey_off, l->lkeylen < r->lkeylen ? l->lkeylen : r->lkeylen);
         if (rc) return rc;
         return l->lkeylen - r->lkeylen;
@@ -107,7 +110,7 @@ static size_t co_merge(const struct co_ctx *c, struct co_rng *a, uint32_t *ord, 
                 if (q->lflag || p->rflag || keycmp(c, q->lkey_off, p->rkey_off, m) <= 0) {
                     if (p->rflag || q->rflag) {
                         p->rflag = 1;
-                        p->rkey_off = 0;
+                        p->rkey_off = CO_KEY_NULL; /* free(p->rkey); p->rkey = NULL */
                         p->rkeylen = 0;
                     } else if (keycmp(c, p->rkey_off, q->rkey_off,
                                       p->rkeylen < q->rkeylen ? p->rkeylen : q->rkeylen) < 0) {

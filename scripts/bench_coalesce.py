@@ -14,9 +14,10 @@ from comdb2_amd.hsc import Validator
 v = Validator(0)
 res = {}
 for name, kw in (("100k sets x <=20 ranges", dict(ntxn=100_000, max_ranges=20)),
-                 ("8 sets x <=200k ranges", dict(ntxn=8, max_ranges=200_000)),
-                 ("8 sets x <=200k ranges, no empty lower key (level-parallel sort)",
-                  dict(ntxn=8, max_ranges=200_000, empty_lo=0.0))):
+                 ("8 sets x <=200k ranges, NULL lower keys (tie with everything)",
+                  dict(ntxn=8, max_ranges=200_000)),
+                 ("8 sets x <=200k ranges, present empty lower keys, no NULL (level-parallel sort)",
+                  dict(ntxn=8, max_ranges=200_000, null_lo=0.0))):
     if len(sys.argv) > 1 and sys.argv[1] not in name:  # case filter (profiling)
         continue
     rs = random_readsets(7, **kw)

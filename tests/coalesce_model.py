@@ -10,7 +10,12 @@ from typing import List, Optional
 
 import numpy as np
 
-from comdb2_amd.formats import ReadSets
+from comdb2_amd.formats import KEY_NULL, ReadSets
+
+
+def _ptr(off) -> Optional[int]:
+    """A flat key offset as the model's pointer: HSC_KEY_NULL -> None (NULL)."""
+    return None if int(off) == KEY_NULL else int(off)
 
 
 @dataclass
@@ -109,8 +114,7 @@ def coalesce_readsets(rs: ReadSets) -> List[List[CR]]:
             lk, rk = int(rs.lkeylen[r]), int(rs.rkeylen[r])
             arr.append(CR(rs.tbnames[int(rs.table[r])], int(rs.idxnum[r]), int(rs.lflag[r]),
                           int(rs.rflag[r]), int(rs.islocked[r]),
-                          int(rs.lkey_off[r]) if lk > 0 else None, lk,
-                          int(rs.rkey_off[r]) if rk > 0 else None, rk))
+                          _ptr(rs.lkey_off[r]), lk, _ptr(rs.rkey_off[r]), rk))
         out.append(m.coalesce(arr))
     return out
 
@@ -124,8 +128,7 @@ def as_rows(rs: ReadSets):
             lk, rk = int(rs.lkeylen[r]), int(rs.rkeylen[r])
             rows.append((rs.tbnames[int(rs.table[r])], int(rs.idxnum[r]), int(rs.lflag[r]),
                          int(rs.rflag[r]), int(rs.islocked[r]),
-                         int(rs.lkey_off[r]) if lk > 0 else None, lk,
-                         int(rs.rkey_off[r]) if rk > 0 else None, rk))
+                         _ptr(rs.lkey_off[r]), lk, _ptr(rs.rkey_off[r]), rk))
         out.append(rows)
     return out
 
@@ -136,11 +139,12 @@ def model_rows(sets: List[List[CR]]):
 
 
 def random_readsets(seed: int, ntxn: int = 300, max_ranges: int = 40, tables=("ta", "tb", "tc"),
-                    empty_lo: float = 0.03, min_ranges: int = 0):
+                    empty_lo: float = 0.03, min_ranges: int = 0, null_lo: float = 0.03):
     """Read sets full of coalesce corner cases: shared prefixes, equal keys,
     prefix (shorter) bounds, open ends, table locks, several indexes.
-    empty_lo: share of present-but-empty lower keys (the comparator's
-    tie-with-everything case); 0 gives sets with a consistent order."""
+    empty_lo: share of present-but-empty lower keys (sort before longer keys);
+    null_lo: share of NULL lower keys without lflag (the comparator's
+    tie-with-everything case); null_lo = 0 gives sets with a consistent order."""
     from comdb2_amd.formats import Range
     rng = np.random.default_rng(seed)
     sets, snaps = [], []
@@ -164,8 +168,11 @@ def random_readsets(seed: int, ntxn: int = 300, max_ranges: int = 40, tables=("t
             rf = 1 if rng.random() < 0.08 else 0
             if rng.random() < 0.3:
                 hi = lo
-            if not lf and rng.random() < empty_lo:
-                lo = b""  # present but empty lower key: compares as the NULL key
+            u = rng.random()
+            if not lf and u < empty_lo:
+                lo = b""  # present but empty lower key (malloc(0))
+            elif not lf and u < empty_lo + null_lo:
+                lo = None  # NULL lower key, no lflag: ties with every range
             rs.append(Range(tb, ix, None if lf else lo, None if rf else hi, lf, rf, 0))
         sets.append(rs)
         snaps.append(1 << 32)

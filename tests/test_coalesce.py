@@ -106,7 +106,7 @@ def test_level_parallel_coalesce_model(seed, ntables):
     import functools
 
     from coalesce_model import Model
-    rs = random_readsets(seed, ntxn=12, max_ranges=500, min_ranges=100, empty_lo=0.0,
+    rs = random_readsets(seed, ntxn=12, max_ranges=500, min_ranges=100, null_lo=0.0,
                          tables=tuple(f"t{i:02d}" for i in range(ntables)))
     m = Model(bytes(np.asarray(rs.keys, np.uint8)))
     fields = lambda a: [(c.tbname, c.idxnum, c.lflag, c.rflag, c.islocked, c.lkey, c.lkeylen,
@@ -122,9 +122,9 @@ def test_level_parallel_coalesce_model(seed, ntables):
             lk, rk = int(rs.lkeylen[r]), int(rs.rkeylen[r])
             arr.append(coalesce_model.CR(rs.tbnames[int(rs.table[r])], int(rs.idxnum[r]),
                                          int(rs.lflag[r]), int(rs.rflag[r]), int(rs.islocked[r]),
-                                         int(rs.lkey_off[r]) if lk > 0 else None, lk,
-                                         int(rs.rkey_off[r]) if rk > 0 else None, rk))
-        if not all((c.islocked or c.lflag or c.lkeylen > 0) and
+                                         coalesce_model._ptr(rs.lkey_off[r]), lk,
+                                         coalesce_model._ptr(rs.rkey_off[r]), rk))
+        if not all((c.islocked or c.lflag or c.lkey is not None) and
                    (not c.islocked or (c.lflag and c.rflag)) for c in arr):
             continue
         want = m.coalesce(copy.deepcopy(arr))
@@ -134,3 +134,38 @@ def test_level_parallel_coalesce_model(seed, ntables):
         assert fields(got) == fields(want)
         checked += 1
     assert checked == rs.ntxn
+
+
+def test_null_vs_empty_lower_key(oracle_lib):
+    """currange_cmp (db/sqlglue.c:228-236) compares lower keys only when both
+    pointers are non-NULL: a present empty key (serial_readset_get's malloc(0),
+    db/osqlcomm.c:974) sorts before a longer key, a NULL one ties with it.  The
+    flat format keeps the difference (HSC_KEY_NULL offsets)."""
+    from comdb2_amd.formats import KEY_NULL
+    empty = one([[Range("ta", 0, b"b", b"c"), Range("ta", 0, b"", b"a")]])
+    null = one([[Range("ta", 0, b"b", b"c"), Range("ta", 0, None, b"a")]])
+    assert int(null.lkey_off[1]) == KEY_NULL and int(empty.lkey_off[1]) != KEY_NULL
+    # empty: sorted to [("", a), (b, c)]; a < b so nothing merges -> 2 ranges
+    rows_e = as_rows(oracle_lib.coalesce(empty))[0]
+    assert [r[6] for r in rows_e] == [0, 1]
+    # NULL: ties, the sort keeps (b, c) first; then NULL-lower q merges into p
+    rows_n = as_rows(oracle_lib.coalesce(null))[0]
+    assert len(rows_n) == 1 and rows_n[0][6] == 1
+    assert rows_e == model_rows(coalesce_readsets(empty))[0]
+    assert rows_n == model_rows(coalesce_readsets(null))[0]
+
+
+def test_wire_decode_keeps_key_presence():
+    """serial_readset_get leaves keys the message does not carry NULL and
+    malloc's the carried ones, also when empty (db/osqlcomm.c:948-993)."""
+    from comdb2_amd.formats import KEY_NULL, encode_serial
+    from comdb2_amd.hsc import Validator
+    rs = one([[Range("ta", 0, b"", b"a"), Range("ta", 1, None, b"z", 1, 0, 0), Range.locked("tb")]])
+    v = Validator(-1)
+    try:
+        d = v.decode_serial(encode_serial(rs))
+    finally:
+        v.close()
+    assert int(d.lkey_off[0]) != KEY_NULL and int(d.lkeylen[0]) == 0
+    assert int(d.lkey_off[1]) == KEY_NULL and int(d.rkey_off[1]) != KEY_NULL
+    assert int(d.lkey_off[2]) == KEY_NULL and int(d.rkey_off[2]) == KEY_NULL

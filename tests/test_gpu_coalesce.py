@@ -25,19 +25,19 @@ def test_gpu_coalesce_matches_oracle(validator, oracle_mod, seed, ntxn, maxr):
     assert len(got.table) < len(rs.table)  # something merged
 
 
-@pytest.mark.parametrize("seed,ntxn,lo,hi,empty_lo,ntables", [
+@pytest.mark.parametrize("seed,ntxn,lo,hi,null_lo,ntables", [
     (11, 6, 256, 3000, 0.0, 3),      # every set on the level-parallel path
     (12, 40, 200, 700, 0.0, 3),      # sizes either side of the threshold
-    (13, 8, 300, 2000, 0.002, 3),    # some sets hold a tie-with-everything range
+    (13, 8, 300, 2000, 0.002, 3),    # some sets hold a tie-with-everything (NULL) lower key
     (14, 1, 60000, 60001, 0.0, 3),   # one deep set (16 merge levels)
     (15, 4, 3000, 9000, 0.0, 60),  # ~180 (table, index) runs per set, many locked tables
 ])
 def test_gpu_coalesce_large_consistent_sets(validator, oracle_mod, monkeypatch, seed, ntxn, lo, hi,
-                                            empty_lo, ntables):
-    """Large sets whose comparator is a consistent order take the
-    level-parallel sort (hsc_coalesce.hip, CoBig): equal to the oracle and to
+                                            null_lo, ntables):
+    """Large sets whose comparator is a consistent order (present empty lower
+    keys included) take the level-parallel sort (hsc_coalesce.hip, CoBig): equal to the oracle and to
     the per-thread glibc-msort path (HSC_CO_SERIAL)."""
-    rs = random_readsets(seed, ntxn=ntxn, max_ranges=hi, min_ranges=lo, empty_lo=empty_lo,
+    rs = random_readsets(seed, ntxn=ntxn, max_ranges=hi, min_ranges=lo, null_lo=null_lo,
                          tables=tuple(f"t{i:02d}" for i in range(ntables)))
     want = oracle_mod.coalesce(rs)
     got = validator.coalesce(rs)
