@@ -18,6 +18,7 @@ import argparse
 import json
 import os
 import platform
+import subprocess
 import sys
 import time
 
@@ -244,17 +245,101 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm):
     return out
 
 
+def box_cpus():
+    """The host CPUs this run may use: the affinity mask, the cgroup v2 CPU
+    quota (a GPU box grants 16 CPUs of a larger machine) and nproc; the CPU
+    baseline runs on min(affinity, quota) threads."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
+    except (OSError, ValueError):
+        nproc = None
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    return dict(threads=threads, nproc=nproc, affinity_cpus=aff, cgroup_cpu_quota=quota,
+                cpu=cpu_model())
+
+
+PROBE_KERNELS = ("k_locate_t", "k_plan_t", "k_scatter_t", "k_join_t", "k_pack_flags")
+
+
+def pmc_traffic(args):
+    """HBM bytes per probe batch from rocprofv3 PMC passes of this same
+    workload (`bench.py --pmc-child`: the window and the first ring batch,
+    probed on one stream), one pass per counter as MI355X_MICROARCH.md
+    prescribes (FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2).  FETCH_SIZE /
+    WRITE_SIZE are KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide
+    coalesced read, so read bytes = 2 x 1024 x FETCH_SIZE, write bytes = 1024 x
+    WRITE_SIZE.  FETCH_SIZE counts Infinity-Cache hits too (L2 misses), so the
+    figure is what the kernels pull from beyond L2.  Runs before this process
+    touches the GPU."""
+    import csv
+    import shutil
+    import tempfile
+    out = {"kind": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --pmc-child "
+                   "(same window and batch shape, one stream)", "kernels": {}}
+    per = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="hsc_pmc_")
+        cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", ctr, "-T", "--output-format",
+               "csv", "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__),
+               "--pmc-child", "--config", str(args.config), "--n-commits", str(args.n_commits),
+               "--n-txn", str(args.n_txn)]
+        print(f"[bench] pmc pass {ctr}", file=sys.stderr, flush=True)
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            path = os.path.join(d, "run_counter_collection.csv")
+            if r.returncode != 0 or not os.path.exists(path):
+                out["error"] = f"{ctr}: rc {r.returncode}: {(r.stderr or '')[-300:]}"
+                return out
+            vals = {}
+            for row in csv.DictReader(open(path)):
+                k = row["Kernel_Name"].split("(")[0].replace("hsc::", "").split("<")[0]
+                k = k[5:] if k.startswith("void ") else k
+                if k in PROBE_KERNELS and row["Counter_Name"] == ctr:
+                    vals.setdefault(k, []).append(float(row["Counter_Value"]))
+            per[ctr] = {k: float(np.mean(v)) for k, v in vals.items()}
+        except (OSError, subprocess.SubprocessError) as e:
+            out["error"] = f"{ctr}: {e}"
+            return out
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    tot = 0.0
+    for k in PROBE_KERNELS:
+        f, w = per["FETCH_SIZE"].get(k), per["WRITE_SIZE"].get(k)
+        if f is None and w is None:
+            continue
+        rd, wr = 2 * 1024 * (f or 0.0), 1024 * (w or 0.0)
+        out["kernels"][k] = {"read_bytes": rd, "write_bytes": wr}
+        tot += rd + wr
+    out["bytes_per_batch"] = tot
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batches", type=int, default=2, help="distinct resident read-set batches")
+    ap.add_argument("--batches", type=int, default=2,
+                    help="distinct resident read-set batches (at least; see --ring-gb)")
+    ap.add_argument("--ring-gb", type=float, default=None,
+                    help="cycle distinct resident batches whose probe inputs total at least this "
+                         "many GB (default: 1.1 for config 2 -- past the 256 MiB Infinity Cache "
+                         "-- else 0); the 2-batch L3-resident ring is timed alongside")
     ap.add_argument("--n-commits", type=int, default=1_000_000)
     ap.add_argument("--n-txn", type=int, default=100_000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU baseline threads (0: the box's CPUs, min(affinity, cgroup quota))")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--wide", action="store_true", help="force the wide window layout")
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the batches rotate over (each with its own outputs and "
@@ -268,23 +353,27 @@ def main():
     ap.add_argument("--c5-keys", type=int, default=125_000_000,
                     help="config 5: window writes per GPU (125M x 8 GPUs = SURVEY's 1B)")
     ap.add_argument("--check", action="store_true",
-                    help="config 5, N = 1: full-batch CPU sort-join parity (oracle/sortjoin.c)")
+                    help="config 3 / 5, N = 1: full-batch CPU sort-join parity (oracle/sortjoin.c)")
     ap.add_argument("--history-txns", type=int, default=16_700_000,
                     help="config 4: transactions (x ~6 ops: 16.7M = SURVEY's 100M-op history)")
-    ap.add_argument("--traffic", type=str, default=os.path.join(ROOT, "profiles", "traffic.json"),
-                    help="PMC-derived HBM bytes per join launch (from a rocprofv3 --pmc run)")
     args = ap.parse_args()
+    if args.ring_gb is None:
+        args.ring_gb = 1.1 if args.config == 2 and not args.pmc_child else 0.0
 
     if args.config == 4:
         return bench_graph(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    traffic = None
+    if (args.config == 2 and world == 1 and not args.no_pmc and not args.pmc_child
+            and not args.wide):
+        traffic = pmc_traffic(args)  # child processes, before this one touches the GPU
     import torch
     import torch.distributed as dist
 
     from comdb2_amd import hsc, shard
     from comdb2_amd.workloads import SEED_CONFIG2, config2, config2_device_window
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         world = max(world, 1)
@@ -300,7 +389,8 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    want_cpu = (rank == 0 and world == 1 and not args.no_cpu and args.config == 2)
+    want_cpu = (rank == 0 and world == 1 and not args.no_cpu and args.config == 2
+                and not args.pmc_child)
     batches = []
     v = hsc.Validator(local)
     if args.wide:
@@ -374,14 +464,25 @@ def main():
         v.merge_table_max(shard.allreduce_table_max(v.table_max()))
     T = first_rs.ntxn
     m0 = None
-    for bi in range(args.batches):
+    ring_bytes = 0
+    bi = 0
+    nb_min = 2 if args.pmc_child else max(2, args.batches)
+    while bi < nb_min or ring_bytes < args.ring_gb * 1e9:
         rs = first_rs if bi == 0 else more_rs(bi)
         m = v.marshal(rs)
         if bi == 0 and (want_cpu or args.check):
             m0 = m
         if world > 1:
             m = shard.route(m, shards.range_mask(m, rank), shards.lock_mask(m, rank))
-        batches.append(upload_batch(torch, dev, m))
+        b = upload_batch(torch, dev, m)
+        b["bytes"] = sum(int(b[k].numel() * b[k].element_size())
+                         for k in ("lo", "hi", "gid", "snap", "txn", "lock_table", "lock_snap",
+                                   "lock_txn"))
+        ring_bytes += b["bytes"]
+        batches.append(b)
+        bi += 1
+        if bi % 8 == 0:
+            print(f"[bench] {bi} batches, {ring_bytes / 1e9:.2f} GB", file=sys.stderr, flush=True)
     S = max(1, args.streams)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
     comm = torch.cuda.Stream(device=dev) if world > 1 else None
@@ -391,11 +492,18 @@ def main():
                 for si in range(S)] for b in batches]
     torch.cuda.synchronize()
 
-    def step(k, nstreams):
+    if args.pmc_child:  # profiled by the parent's rocprofv3 --pmc pass: batch 0, one stream
+        for k in range(10):
+            v.probe_device(structs[0][0])
+        v.synchronize()
+        v.close()
+        return
+
+    def step(k, nstreams, nbatch):
         si = k % nstreams
         st = streams[si]
         v.set_stream(st.cuda_stream)
-        v.probe_device(structs[k % len(structs)][si])
+        v.probe_device(structs[k % nbatch][si])
         if world > 1:  # verdict merge on one comm stream: the same collective order on every rank
             e = torch.cuda.Event()
             e.record(st)
@@ -407,16 +515,16 @@ def main():
             st.wait_event(e2)
             v.pack_verdicts(verdicts[si].data_ptr(), T, bitmaps[si].data_ptr())
 
-    def timed(nstreams, steps, warmup):
-        for k in range(warmup):
-            step(k, nstreams)
+    def timed(nstreams, nbatch):
+        for k in range(args.warmup):
+            step(k, nstreams, nbatch)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for k in range(steps):
-            step(k, nstreams)
+        for k in range(args.warmup, args.warmup + args.steps):
+            step(k, nstreams, nbatch)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -428,23 +536,28 @@ def main():
             el = float(e.item())
         return el
 
-    elapsed = timed(S, args.steps, args.warmup)
-    # one stream (each batch's kernels strictly after the previous batch's)
-    serial_elapsed = timed(1, args.steps, args.warmup) if S > 1 else elapsed
+    NB = len(batches)
+    # the ring: every timed step probes a batch no other step of the region touches
+    # (warmup + steps <= NB) or, with a longer run, the least recently probed one
+    elapsed = timed(S, NB)
+    serial_elapsed = timed(1, NB) if S > 1 else elapsed
+    # L3-resident: two batches alternate (window + both batches fit the 256 MiB cache)
+    l3_elapsed = timed(S, 2) if NB > 2 else elapsed
+    l3_serial = timed(1, 2) if NB > 2 else serial_elapsed
     v.set_stream(streams[0].cuda_stream)
 
     # verdicts of batch 0 (for the conflict rate and the CPU parity sample)
-    step(0, 1)
+    step(0, 1, NB)
     torch.cuda.synchronize()
     v0 = verdicts[0].cpu().numpy().copy()
     forced = batches[0]["forced"]
     v0 = np.maximum(v0, forced)
 
-    # per-kernel device time (separate pass; events on the launch stream)
+    # per-kernel device time (separate pass over the ring; events on the launch stream)
     v.enable_timing(True)
     acc = {}
     for k in range(args.steps):
-        v.probe_device(structs[k % len(structs)][0])
+        v.probe_device(structs[k % NB][0])
         v.synchronize()
         for key, val in v.timing().items():
             acc.setdefault(key, []).append(val)
@@ -467,15 +580,9 @@ def main():
         rng_g = np.mean([np.bincount(host(b["gid"]), minlength=len(c3.groups)) for b in batches],
                         axis=0)
         B = int((keys_g * (lhat + 12)).sum() + (rng_g * (2 * lhat + 16)).sum() + (T + 7) // 8)
-    ms_step = elapsed / args.steps * 1e3
-    traffic = None
-    if os.path.exists(args.traffic):
-        try:
-            traffic = json.load(open(args.traffic)).get("probe_hbm_bytes_per_step")
-        except (OSError, ValueError):
-            traffic = None
     kern = kernel_bytes(v.layout, v.code_words, n_keys, n_r, T, tm)
     ms_per_step = elapsed / args.steps * 1e3
+    frac = lambda el: B / (el / args.steps) / 1e9 / HBM_PEAK_GBS
     checks = T * args.steps
     out = {
         "metric": METRIC,
@@ -499,6 +606,7 @@ def main():
             "parallelism": f"key-range shards x{world}" + (" + RCCL max all-reduce" if world > 1 else ""),
             "streams": S,
             "serial_ms_per_step": serial_elapsed / args.steps * 1e3,
+            "ring_batches": NB,
             "window_layout": {hsc.LAYOUT_NARROW: "narrow (u32 tile-relative keys)",
                               hsc.LAYOUT_COMPACT: f"compact ({v.code_words}-word codes of "
                                                   f"{W}-word keys)",
@@ -507,16 +615,31 @@ def main():
         },
         "roofline": {
             # the probe phase as SURVEY 8(d) defines it: B over the device time of
-            # one batch (the timed loop runs batches back to back)
+            # one batch (the timed loop runs batches back to back over the ring)
             "bound": "hbm",
             "kernel": "probe phase (" + ", ".join(kern) + ")",
-            "achieved": B / (ms_step * 1e-3) / 1e9,
+            "achieved": B / (ms_per_step * 1e-3) / 1e9,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": B / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
-            "traffic": traffic,
+            "frac": frac(elapsed),
+            "frac_1stream": frac(serial_elapsed),
+            "traffic": traffic.get("bytes_per_batch") if traffic else None,
             "algorithmic_bytes": B,
-            "avg_ms": ms_step,
+            "avg_ms": ms_per_step,
+            "working_set": {
+                "ring_batches": NB,
+                "ring_input_bytes": int(sum(b["bytes"] for b in batches)),
+                "note": "distinct resident probe batches cycled by the timed loop (every step "
+                        "a batch no other step of the region touches) plus the resident window; "
+                        "past the 256 MiB Infinity Cache"},
+            "l3_resident": {
+                "batches": 2,
+                "input_bytes": int(batches[0]["bytes"] + batches[min(1, NB - 1)]["bytes"]),
+                "ms_per_step": l3_elapsed / args.steps * 1e3,
+                "serial_ms_per_step": l3_serial / args.steps * 1e3,
+                "frac": frac(l3_elapsed),
+                "frac_1stream": frac(l3_serial),
+                "value": checks / l3_elapsed},
         },
         "probe_phase": {
             "event_total_ms": tm["probe_total_ms"],
@@ -528,11 +651,12 @@ def main():
         # from the probe phase; bytes = N_w * (L^ + 8 LSN + 4 group)
         "ingest": {"rows": int(n_w), "algorithmic_bytes": int(n_w) * (8 * W + 12),
                    "GBps": int(n_w) * (8 * W + 12) / (ingest_ms * 1e-3) / 1e9 if ingest_ms else None},
-        "cold_e2e_ms": ingest_ms + ms_step,
+        "cold_e2e_ms": ingest_ms + ms_per_step,
         "cpu_baseline": None,
     }
+    if traffic:
+        out["roofline"]["traffic_detail"] = traffic
     if args.config == 3:
-        out["roofline"]["traffic"] = None  # profiles/traffic.json is the config-2 run
         out["config"]["parallelism"] = f"(table, index) group shards (LPT) x{world}" + (
             " + RCCL max all-reduce" if world > 1 else "")
         out["config"]["groups_per_rank"] = len(mine)
@@ -540,12 +664,11 @@ def main():
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle
             sj = oracle.SortJoin(gid, words, lsn, len(c3.groups))
-            want, secs = sj.probe(m0, v.table_max(), nthreads=args.cpu_threads)
+            want, secs = sj.probe(m0, v.table_max(), nthreads=box_cpus()["threads"])
             sj.close()
             out["parity"] = {"kind": "full batch 0 vs oracle/sortjoin.c (CPU sort-join)",
                              "equal": bool(np.array_equal(want != 0, v0 != 0)), "cpu_s": secs}
     if args.config == 5:
-        out["roofline"]["traffic"] = None  # profiles/traffic.json is the config-2 run
         # per-GPU imbalance: routed ranges and 1-stream probe time per rank
         loc = np.array([n_r, tm["probe_total_ms"]], dtype=np.float64)
         if world > 1:
@@ -563,14 +686,18 @@ def main():
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle
             sj = oracle.SortJoin(gid, words, lsn, 1)
-            want, secs = sj.probe(m0, np.array([lsn.max()], np.uint64), nthreads=args.cpu_threads)
+            want, secs = sj.probe(m0, np.array([lsn.max()], np.uint64),
+                                  nthreads=box_cpus()["threads"])
             sj.close()
             out["parity"] = {"kind": "full batch 0 vs oracle/sortjoin.c (CPU sort-join)",
                              "equal": bool(np.array_equal(want != 0, v0 != 0)),
                              "cpu_s": secs}
     if want_cpu:
-        out["cpu_baseline"] = cpu_baseline(c2, v0, args.cpu_threads, args.cpu_seconds,
-                                           m0=m0)
+        cpus = box_cpus()
+        threads = args.cpu_threads or cpus["threads"]
+        print(f"[bench] cpu baseline on {threads} threads ({cpus})", file=sys.stderr, flush=True)
+        out["cpu_baseline"] = cpu_baseline(c2, v0, threads, args.cpu_seconds, m0=m0)
+        out["cpu_baseline"]["host"] = cpus
     if rank == 0:
         print(json.dumps(out), flush=True)
     v.close()
