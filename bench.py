@@ -245,6 +245,36 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm):
     return out
 
 
+def api_leg(hsc, v, rs, device_verdict, args):
+    """The drop-in entry end to end: hip_serial_check_batch on the batch's
+    read sets as CurRangeArr* (heap CurRange's with their own name and key
+    allocations, as a comdb2 master holds them), each call = host marshal on
+    the box's CPUs into pinned staging, upload, the join, verdict download and
+    rc_out -- pipelined in 32k-read-set chunks (db/toblock.c:4779-4836 calls
+    the check per transaction; a batching collector hands it n at once).
+    Snapshots are passed as file/offset arrays (full mode overwrites them with
+    the end LSN), one fresh pair per call, filled outside the timed region."""
+    arrs = hsc.NativeCurRangeArrs(rs)
+    T = rs.ntxn
+    K = max(3, min(args.steps, 10))
+    snaps = np.asarray(rs.snap, np.uint64)
+    fo = [(np.ascontiguousarray(snaps >> np.uint64(32), np.uint32),
+           np.ascontiguousarray(snaps & np.uint64(0xFFFFFFFF), np.uint32)) for _ in range(K + 1)]
+    v.set_stream(0)  # the context's own stream
+    rc = v.check_batch(arrs, file=fo[0][0], offset=fo[0][1])
+    t0 = time.perf_counter()
+    for k in range(K):
+        v.check_batch(arrs, file=fo[k + 1][0], offset=fo[k + 1][1])
+    el = time.perf_counter() - t0
+    arrs.close()
+    ok = bool(np.array_equal(rc != 0, np.asarray(device_verdict) != 0))
+    return {"entry": "hip_serial_check_batch (CurRangeArr* x n, full checks)",
+            "value": T * K / el, "unit": "checks/s", "calls": K, "read_sets_per_call": T,
+            "ms_per_call": el / K * 1e3, "host_threads": box_cpus()["threads"],
+            "parity_with_device_batch": ok,
+            "note": "marshal + pinned upload + probe + download + rc_out, timed over whole calls"}
+
+
 def box_cpus():
     """The host CPUs this run may use: the affinity mask, the cgroup v2 CPU
     quota (a GPU box grants 16 CPUs of a larger machine) and nproc; the CPU
@@ -339,6 +369,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 traffic passes")
+    ap.add_argument("--no-api", action="store_true",
+                    help="skip the drop-in entry leg (hip_serial_check_batch end to end)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--wide", action="store_true", help="force the wide window layout")
     ap.add_argument("--streams", type=int, default=2,
@@ -692,6 +724,8 @@ def main():
             out["parity"] = {"kind": "full batch 0 vs oracle/sortjoin.c (CPU sort-join)",
                              "equal": bool(np.array_equal(want != 0, v0 != 0)),
                              "cpu_s": secs}
+    if args.config == 2 and world == 1 and not args.no_api:
+        out["api"] = api_leg(hsc, v, first_rs, v0, args)
     if want_cpu:
         cpus = box_cpus()
         threads = args.cpu_threads or cpus["threads"]

@@ -15,12 +15,16 @@
 
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -41,7 +45,68 @@ inline uint64_t load_be64(const uint8_t *b)
 
 inline uint64_t ixkey(int tid, int ix) { return ((uint64_t)(uint32_t)tid << 32) | (uint32_t)ix; }
 
+// Host staging buffer: pinned (hipHostMalloc) on a device context, so that
+// uploads and verdict downloads are DMA from / to it; malloc on a host-only
+// one.  Grows, never shrinks.
+struct HBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    bool pinned = false;
+    // 0 or -1 (out of memory)
+    int ensure(size_t want, bool pin)
+    {
+        if (want <= bytes && pin == pinned) return 0;
+        release();
+        const size_t b = want + want / 8 + 256;
+        if (pin) {
+            if (hipHostMalloc(&p, b, hipHostMallocDefault) != hipSuccess) {
+                p = nullptr;
+                return -1;
+            }
+        } else if (!(p = malloc(b))) {
+            return -1;
+        }
+        bytes = b;
+        pinned = pin;
+        return 0;
+    }
+    void release()
+    {
+        if (p) {
+            if (pinned)
+                (void)hipHostFree(p);
+            else
+                free(p);
+        }
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T *as() const { return (T *)p; }
+};
+
+// One marshalled batch (or pipeline chunk) in host memory: probe SoA,
+// forced verdicts, and the verdict bytes read back.
+struct Stage {
+    HBuf lo, hi, gid, snap, txn, lock_table, lock_snap, lock_txn, forced, verdict;
+    size_t n = 0, n_lock = 0, n_txn = 0;
+    hipEvent_t done = nullptr;  // the chunk's verdict download
+    void release()
+    {
+        for (HBuf *b : {&lo, &hi, &gid, &snap, &txn, &lock_table, &lock_snap, &lock_txn, &forced,
+                        &verdict})
+            b->release();
+        if (done) (void)hipEventDestroy(done);
+        done = nullptr;
+    }
+};
+
+constexpr int kMarshalTxns = 2048;         // read sets per marshal work item
+constexpr int kMarshalParallelMin = 4096;  // fewer read sets: marshal on the caller's thread
+constexpr int kPipeTxns = 32768;           // read sets per pipeline chunk of a large batch
+
 }  // namespace
+
+struct MarshalPart;
 
 struct hsc_ctx {
     int device = 0;
@@ -107,11 +172,13 @@ struct hsc_ctx {
     DBuf p_verdict, p_bitmap;
     DBuf w_code, w_hist, w_counts, w_bucket, w_cursor, w_items, w_item_tile, w_item_desc, w_recs;
 
-    // marshal output
+    // marshal output: staging sets (two: a large batch is checked as a
+    // pipeline of chunks, one marshalled while the other is on the GPU),
+    // per-worker parts, host threads
     hsc_marshalled m{};
-    std::vector<uint64_t> m_lo, m_hi, m_snap, m_lock_snap;
-    std::vector<uint32_t> m_gid, m_txn, m_lock_table, m_lock_txn;
-    std::vector<uint8_t> m_forced;
+    Stage stage[2];
+    std::vector<MarshalPart> parts;
+    int threads = 1;
 
     // raw log / wire decode output
     DecodedLog decoded;
@@ -795,27 +862,9 @@ static void norm_bound(const uint8_t *key, int keylen, int flag, int klen, bool 
     for (int j = 0; j < W; ++j) out[j] = load_be64(buf + 8 * j);
 }
 
-struct TxnTable {
-    int tid, islocked;
-    std::vector<int> idx, b, e;  // per idxnum span
-};
-
-static void marshal_begin(hsc_ctx *c, size_t n_txn)
-{
-    c->m_lo.clear();
-    c->m_hi.clear();
-    c->m_snap.clear();
-    c->m_gid.clear();
-    c->m_txn.clear();
-    c->m_lock_table.clear();
-    c->m_lock_snap.clear();
-    c->m_lock_txn.clear();
-    c->m_forced.assign(n_txn, 0);
-}
-
 // Forced verdicts of a full check that do not depend on the ranges.
-// Returns -1 if the device decides, else the rc.
-static int full_forced(hsc_ctx *c, uint64_t S)
+// Returns -1 if the device decides, else the rc.  Read-only on c.
+static int full_forced(const hsc_ctx *c, uint64_t S)
 {
     if (S >= c->end_lsn) return 0;  // DB_SET at/after the end -> DB_NOTFOUND -> 0
     if (!c->record_lsns.empty() &&
@@ -834,115 +883,122 @@ static int regop_rc(hsc_ctx *c, uint64_t S)
     return (c->max_commit > S || c->poison_regop > S) ? 1 : 0;
 }
 
+// One table of a read set: islocked of its first range (db/sqlglue.c:322-326)
+// and its index spans [b, e] in array order (:327-349), spans[s0 .. s0 + ns).
+struct TxnTable {
+    int tid, islocked, s0, ns;
+};
+struct IdxSpan {
+    int idx, b, e;
+};
+
+// One worker's share of a marshal (read sets [t0, t1) of the batch): probes
+// as AoS rows (W words of lo, W of hi) plus the scratch of the span builder.
+struct MarshalPart {
+    std::vector<uint64_t> lohi;  // [n][2W]
+    std::vector<uint64_t> snap, lock_snap;
+    std::vector<uint32_t> gid, txn, lock_table, lock_txn;
+    std::vector<TxnTable> tabs;
+    std::vector<IdxSpan> spans;
+    size_t out0 = 0, lock0 = 0;  // output offsets (assembly)
+    void clear()
+    {
+        lohi.clear(), snap.clear(), lock_snap.clear(), gid.clear(), txn.clear();
+        lock_table.clear(), lock_txn.clear();
+    }
+};
+
 template <class Get>
-static void marshal_txn(hsc_ctx *c, uint32_t txn, uint64_t S, int nr, Get get,
-                        std::vector<TxnTable> &tabs)
+static void marshal_txn(const hsc_ctx *c, MarshalPart &mp, uint32_t txn, uint64_t S, int nr,
+                        Get get)
 {
     const int W = c->W;
+    auto &tabs = mp.tabs;
+    auto &spans = mp.spans;
     tabs.clear();
+    spans.clear();
+    // pass 1: tables (first range fixes islocked) and per-index [begin, end]
+    // spans in array order (currangearr_build_hash, db/sqlglue.c:312-351);
+    // spans of one table are kept contiguous by moving later tables' spans
     for (int k = 0; k < nr; ++k) {
-        RangeRef r = get(k);
+        const RangeRef r = get(k);
         if (r.tid < 0) continue;  // table never written: nothing can conflict
-        TxnTable *tt = nullptr;
-        for (auto &t : tabs)
-            if (t.tid == r.tid) {
-                tt = &t;
-                break;
-            }
-        if (!tt) {  // first range of the table fixes islocked
-            tabs.push_back(TxnTable{r.tid, r.islocked, {}, {}, {}});
-            tt = &tabs.back();
-        }
-        size_t j = 0;
-        for (; j < tt->idx.size(); ++j)
-            if (tt->idx[j] == r.idxnum) break;
-        if (j == tt->idx.size()) {
-            tt->idx.push_back(r.idxnum);
-            tt->b.push_back(k);
-            tt->e.push_back(k);
-        } else {
-            tt->e[j] = k;
-        }
-    }
-    uint64_t wl[kMaxWords], wh[kMaxWords];
-    for (auto &t : tabs) {
-        if (t.islocked) {
-            c->m_lock_table.push_back((uint32_t)t.tid);
-            c->m_lock_snap.push_back(S);
-            c->m_lock_txn.push_back(txn);
+        int ti = 0;
+        while (ti < (int)tabs.size() && tabs[ti].tid != r.tid) ++ti;
+        if (ti == (int)tabs.size()) tabs.push_back(TxnTable{r.tid, r.islocked, (int)spans.size(), 0});
+        TxnTable &tt = tabs[ti];
+        int j = 0;
+        while (j < tt.ns && spans[tt.s0 + j].idx != r.idxnum) ++j;
+        if (j < tt.ns) {
+            spans[tt.s0 + j].e = k;
             continue;
         }
-        for (size_t j = 0; j < t.idx.size(); ++j) {
-            auto it = c->ix_groups.find(ixkey(t.tid, t.idx[j]));
+        // new index of table ti: insert at tt.s0 + tt.ns (shifts later tables)
+        spans.insert(spans.begin() + tt.s0 + tt.ns, IdxSpan{r.idxnum, k, k});
+        tt.ns++;
+        for (int q = ti + 1; q < (int)tabs.size(); ++q) tabs[q].s0++;
+    }
+    uint64_t w2[2 * kMaxWords];
+    for (const TxnTable &t : tabs) {
+        if (t.islocked) {
+            mp.lock_table.push_back((uint32_t)t.tid);
+            mp.lock_snap.push_back(S);
+            mp.lock_txn.push_back(txn);
+            continue;
+        }
+        for (int j = 0; j < t.ns; ++j) {
+            const IdxSpan &sp = spans[t.s0 + j];
+            auto it = c->ix_groups.find(ixkey(t.tid, sp.idx));
             if (it == c->ix_groups.end()) continue;
             for (int g : it->second) {
                 const int klen = c->groups[g].klen;
-                for (int k = t.b[j]; k <= t.e[j]; ++k) {  // span quirk: every array slot
-                    RangeRef r = get(k);
-                    norm_bound(r.lkey, r.lkeylen, r.lflag, klen, false, W, wl);
-                    norm_bound(r.rkey, r.rkeylen, r.rflag, klen, true, W, wh);
+                for (int k = sp.b; k <= sp.e; ++k) {  // span quirk: every array slot
+                    const RangeRef r = get(k);
+                    norm_bound(r.lkey, r.lkeylen, r.lflag, klen, false, W, w2);
+                    norm_bound(r.rkey, r.rkeylen, r.rflag, klen, true, W, w2 + W);
                     int cmp = 0;
                     for (int q = 0; q < W && !cmp; ++q)
-                        if (wl[q] != wh[q]) cmp = wl[q] < wh[q] ? -1 : 1;
+                        if (w2[q] != w2[W + q]) cmp = w2[q] < w2[W + q] ? -1 : 1;
                     if (cmp > 0) continue;  // empty range never matches
-                    c->m_lo.insert(c->m_lo.end(), wl, wl + W);
-                    c->m_hi.insert(c->m_hi.end(), wh, wh + W);
-                    c->m_gid.push_back((uint32_t)g);
-                    c->m_snap.push_back(S);
-                    c->m_txn.push_back(txn);
+                    mp.lohi.insert(mp.lohi.end(), w2, w2 + 2 * W);
+                    mp.gid.push_back((uint32_t)g);
+                    mp.snap.push_back(S);
+                    mp.txn.push_back(txn);
                 }
             }
         }
     }
 }
 
-// AoS lo/hi rows -> [W][n] words.
-static void marshal_finish(hsc_ctx *c, size_t n_txn)
-{
-    const int W = c->W;
-    const size_t n = c->m_gid.size();
-    std::vector<uint64_t> lo((size_t)W * n), hi((size_t)W * n);
-    for (size_t i = 0; i < n; ++i)
-        for (int j = 0; j < W; ++j) {
-            lo[(size_t)j * n + i] = c->m_lo[i * W + j];
-            hi[(size_t)j * n + i] = c->m_hi[i * W + j];
-        }
-    c->m_lo.swap(lo);
-    c->m_hi.swap(hi);
-    c->m.n = n;
-    c->m.n_lock = c->m_lock_table.size();
-    c->m.n_txn = n_txn;
-    c->m.words = W;
-    c->m.lo = c->m_lo.data();
-    c->m.hi = c->m_hi.data();
-    c->m.gid = c->m_gid.data();
-    c->m.snap = c->m_snap.data();
-    c->m.txn = c->m_txn.data();
-    c->m.lock_table = c->m_lock_table.data();
-    c->m.lock_snap = c->m_lock_snap.data();
-    c->m.lock_txn = c->m_lock_txn.data();
-    c->m.forced = c->m_forced.data();
-}
-
-static int marshal_readsets(hsc_ctx *c, const hsc_readsets *rs)
-{
-    marshal_begin(c, (size_t)rs->ntxn);
-    std::vector<int> tmap(rs->ntbnames, -1);
-    for (int t = 0; t < rs->ntbnames; ++t) {
-        auto it = c->table_ids.find(rs->tbnames[t]);
-        if (it != c->table_ids.end()) tmap[t] = it->second;
+// Table name -> window table id, with a one-entry cache (a read set names a
+// few tables; comdb2 strdup's every CurRange's name, so pointers differ).
+struct TableLookup {
+    const hsc_ctx *c;
+    const char *last = nullptr;
+    int last_tid = -1;
+    int operator()(const char *name)
+    {
+        if (!name) return -1;
+        if (last && strcmp(name, last) == 0) return last_tid;
+        auto it = c->table_ids.find(name);
+        last = name;
+        last_tid = it == c->table_ids.end() ? -1 : it->second;
+        return last_tid;
     }
-    std::vector<TxnTable> tabs;
-    for (int t = 0; t < rs->ntxn; ++t) {
-        const uint64_t S = rs->snap[t];
-        int f = full_forced(c, S);
-        if (f >= 0) {
-            c->m_forced[t] = (uint8_t)f;
-            continue;
-        }
+};
+
+// Source of read sets: flat arrays (hsc_readsets) ...
+struct FlatSrc {
+    const hsc_readsets *rs;
+    const int *tmap;  // rs table -> window table id
+    int ntxn() const { return rs->ntxn; }
+    uint64_t snap(int t) const { return rs->snap[t]; }
+    template <class F>
+    void each(int t, TableLookup &, F f) const
+    {
         const int64_t r0 = rs->txn_off[t];
         const int nr = (int)(rs->txn_off[t + 1] - r0);
-        auto get = [&](int k) {
+        f(nr, [&](int k) {
             const int64_t r = r0 + k;
             RangeRef x;
             const int32_t tb = rs->table[r];
@@ -956,11 +1012,179 @@ static int marshal_readsets(hsc_ctx *c, const hsc_readsets *rs)
             x.rflag = rs->rflag[r];
             x.islocked = rs->islocked[r];
             return x;
-        };
-        marshal_txn(c, (uint32_t)t, S, nr, get, tabs);
+        });
     }
-    marshal_finish(c, (size_t)rs->ntxn);
+};
+
+// ... or CurRangeArr pointers (the drop-in entry; db/comdb2.h:1105-1124)
+struct ArrSrc {
+    hsc_currangearr *const *arr;
+    const uint64_t *snaps;
+    int n;
+    int ntxn() const { return n; }
+    uint64_t snap(int t) const { return snaps[t]; }
+    template <class F>
+    void each(int t, TableLookup &tl, F f) const
+    {
+        const hsc_currangearr *a = arr[t];
+        // table ids once per range (the span builder and the probe pass both
+        // read them)
+        f(a->size, [&, a](int k) {
+            const hsc_currange *r = a->ranges[k];
+            RangeRef x;
+            x.tid = tl(r->tbname);
+            x.idxnum = r->idxnum;
+            x.lkey = (const uint8_t *)r->lkey;
+            x.rkey = (const uint8_t *)r->rkey;
+            x.lkeylen = r->lkeylen;
+            x.rkeylen = r->rkeylen;
+            x.lflag = r->lflag;
+            x.rflag = r->rflag;
+            x.islocked = r->islocked;
+            return x;
+        });
+    }
+};
+
+// Host worker threads for the marshal: the box's CPUs (affinity mask, cgroup
+// quota), HSC_THREADS or hsc_set_threads.
+static int default_threads()
+{
+    if (const char *e = getenv("HSC_THREADS")) {
+        const int n = atoi(e);
+        if (n > 0) return std::min(n, 256);
+    }
+    int n = (int)std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long per = 0;
+        if (fscanf(f, "%31s %ld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0)
+            n = std::min<long>(n, std::max<long>(1, atol(q) / per));
+        fclose(f);
+    }
+    return std::max(1, std::min(n, 64));
+}
+
+// Runs f(i) for i in [0, nwork) on up to nthreads threads (the caller's
+// included).
+template <class F>
+static void par_for(int nthreads, int nwork, F f)
+{
+    const int nt = std::max(1, std::min(nthreads, nwork));
+    if (nt == 1) {
+        for (int i = 0; i < nwork; ++i) f(i);
+        return;
+    }
+    std::atomic<int> next{0};
+    auto body = [&] {
+        for (int i = next.fetch_add(1); i < nwork; i = next.fetch_add(1)) f(i);
+    };
+    std::vector<std::thread> th;
+    th.reserve(nt - 1);
+    for (int k = 1; k < nt; ++k) th.emplace_back(body);
+    body();
+    for (auto &t : th) t.join();
+}
+
+// Marshal read sets [t0, t1) of src into the staging set st: parts in
+// parallel (chunks of read sets), then the SoA assembly ([W][n] words),
+// in parallel too.  Sets c->m to point at st.
+template <class Src>
+static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
+{
+    const int W = c->W;
+    const int nt = t1 - t0;
+    // work items of ~kMarshalTxns read sets (one part each)
+    const int per = std::max(1, std::min(kMarshalTxns, (nt + c->threads - 1) / std::max(1, c->threads)));
+    const int nwork = std::max(1, (nt + per - 1) / per);
+    if ((int)c->parts.size() < nwork) c->parts.resize(nwork);
+    if (st.forced.ensure((size_t)std::max(nt, 1), !c->host_only)) return fail(c, HSC_ENOMEM, "staging");
+    uint8_t *forced = st.forced.as<uint8_t>();
+    par_for(nt >= kMarshalParallelMin ? c->threads : 1, nwork, [&](int w) {
+        MarshalPart &mp = c->parts[w];
+        mp.clear();
+        TableLookup tl{c};
+        const int a = t0 + w * per, e = std::min(t1, a + per);
+        for (int t = a; t < e; ++t) {
+            const uint64_t S = src.snap(t);
+            const int f = full_forced(c, S);
+            forced[t - t0] = f > 0;
+            if (f >= 0) continue;
+            src.each(t, tl, [&](int nr, auto get) { marshal_txn(c, mp, (uint32_t)(t - t0), S, nr, get); });
+        }
+    });
+    size_t n = 0, nl = 0;
+    for (int w = 0; w < nwork; ++w) {
+        c->parts[w].out0 = n;
+        c->parts[w].lock0 = nl;
+        n += c->parts[w].gid.size();
+        nl += c->parts[w].lock_table.size();
+    }
+    const bool pin = !c->host_only;
+    const size_t n1 = std::max<size_t>(n, 1), l1 = std::max<size_t>(nl, 1);
+    if (st.lo.ensure(8 * (size_t)W * n1, pin) || st.hi.ensure(8 * (size_t)W * n1, pin) ||
+        st.gid.ensure(4 * n1, pin) || st.snap.ensure(8 * n1, pin) || st.txn.ensure(4 * n1, pin) ||
+        st.lock_table.ensure(4 * l1, pin) || st.lock_snap.ensure(8 * l1, pin) ||
+        st.lock_txn.ensure(4 * l1, pin))
+        return fail(c, HSC_ENOMEM, "staging buffers");
+    uint64_t *lo = st.lo.as<uint64_t>(), *hi = st.hi.as<uint64_t>(), *sn = st.snap.as<uint64_t>();
+    uint32_t *gid = st.gid.as<uint32_t>(), *txn = st.txn.as<uint32_t>();
+    par_for(n >= (size_t)kMarshalParallelMin ? c->threads : 1, nwork, [&](int w) {
+        const MarshalPart &mp = c->parts[w];
+        const size_t o = mp.out0, k = mp.gid.size();
+        for (size_t i = 0; i < k; ++i)
+            for (int j = 0; j < W; ++j) {
+                lo[(size_t)j * n + o + i] = mp.lohi[i * 2 * W + j];
+                hi[(size_t)j * n + o + i] = mp.lohi[i * 2 * W + W + j];
+            }
+        if (k) {
+            memcpy(gid + o, mp.gid.data(), 4 * k);
+            memcpy(sn + o, mp.snap.data(), 8 * k);
+            memcpy(txn + o, mp.txn.data(), 4 * k);
+        }
+        const size_t lo0 = mp.lock0, kl = mp.lock_table.size();
+        if (kl) {
+            memcpy(st.lock_table.as<uint32_t>() + lo0, mp.lock_table.data(), 4 * kl);
+            memcpy(st.lock_snap.as<uint64_t>() + lo0, mp.lock_snap.data(), 8 * kl);
+            memcpy(st.lock_txn.as<uint32_t>() + lo0, mp.lock_txn.data(), 4 * kl);
+        }
+    });
+    st.n = n;
+    st.n_lock = nl;
+    st.n_txn = (size_t)nt;
+    hsc_marshalled &m = c->m;
+    m.n = n;
+    m.n_lock = nl;
+    m.n_txn = (size_t)nt;
+    m.words = W;
+    m.lo = lo;
+    m.hi = hi;
+    m.gid = gid;
+    m.snap = sn;
+    m.txn = txn;
+    m.lock_table = st.lock_table.as<uint32_t>();
+    m.lock_snap = st.lock_snap.as<uint64_t>();
+    m.lock_txn = st.lock_txn.as<uint32_t>();
+    m.forced = forced;
     return HSC_OK;
+}
+
+static FlatSrc flat_src(hsc_ctx *c, const hsc_readsets *rs, std::vector<int> &tmap)
+{
+    tmap.assign(std::max(rs->ntbnames, 0), -1);
+    for (int t = 0; t < rs->ntbnames; ++t) {
+        auto it = rs->tbnames[t] ? c->table_ids.find(rs->tbnames[t]) : c->table_ids.end();
+        if (it != c->table_ids.end()) tmap[t] = it->second;
+    }
+    return FlatSrc{rs, tmap.data()};
+}
+
+static int marshal_readsets(hsc_ctx *c, const hsc_readsets *rs)
+{
+    std::vector<int> tmap;
+    return marshal_into(c, flat_src(c, rs, tmap), 0, rs->ntxn, c->stage[0]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1261,55 +1485,97 @@ static int collect_timing(hsc_ctx *c)
     return HSC_OK;
 }
 
-// Upload the marshalled batch, run the join, read back per-txn verdicts.
-static int run_marshalled(hsc_ctx *c, int *rc_out)
+// Upload staging set st (pinned), run the join, download the verdict bytes
+// into st.verdict -- all asynchronous on c->stream; st.done marks the end.
+static int launch_stage(hsc_ctx *c, Stage &st)
 {
     if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
     hipStream_t s = c->stream;
-    const hsc_marshalled &m = c->m;
     const int W = c->W;
-    HIPCHK(c, c->p_lo.ensure(8 * (size_t)W * std::max<size_t>(m.n, 1)));
-    HIPCHK(c, c->p_hi.ensure(8 * (size_t)W * std::max<size_t>(m.n, 1)));
-    HIPCHK(c, c->p_gid.ensure(4 * std::max<size_t>(m.n, 1)));
-    HIPCHK(c, c->p_snap.ensure(8 * std::max<size_t>(m.n, 1)));
-    HIPCHK(c, c->p_txn.ensure(4 * std::max<size_t>(m.n, 1)));
-    HIPCHK(c, c->p_lock_table.ensure(4 * std::max<size_t>(m.n_lock, 1)));
-    HIPCHK(c, c->p_lock_snap.ensure(8 * std::max<size_t>(m.n_lock, 1)));
-    HIPCHK(c, c->p_lock_txn.ensure(4 * std::max<size_t>(m.n_lock, 1)));
-    HIPCHK(c, c->p_verdict.ensure(std::max<size_t>(m.n_txn, 1)));
-    if (m.n) {
-        HIPCHK(c, hipMemcpyAsync(c->p_lo.p, m.lo, 8 * (size_t)W * m.n, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->p_hi.p, m.hi, 8 * (size_t)W * m.n, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->p_gid.p, m.gid, 4 * m.n, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->p_snap.p, m.snap, 8 * m.n, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->p_txn.p, m.txn, 4 * m.n, hipMemcpyHostToDevice, s));
+    const size_t n1 = std::max<size_t>(st.n, 1), l1 = std::max<size_t>(st.n_lock, 1);
+    HIPCHK(c, c->p_lo.ensure(8 * (size_t)W * n1));
+    HIPCHK(c, c->p_hi.ensure(8 * (size_t)W * n1));
+    HIPCHK(c, c->p_gid.ensure(4 * n1));
+    HIPCHK(c, c->p_snap.ensure(8 * n1));
+    HIPCHK(c, c->p_txn.ensure(4 * n1));
+    HIPCHK(c, c->p_lock_table.ensure(4 * l1));
+    HIPCHK(c, c->p_lock_snap.ensure(8 * l1));
+    HIPCHK(c, c->p_lock_txn.ensure(4 * l1));
+    HIPCHK(c, c->p_verdict.ensure(std::max<size_t>(st.n_txn, 1)));
+    if (st.verdict.ensure(std::max<size_t>(st.n_txn, 1), true)) return fail(c, HSC_ENOMEM, "staging");
+    if (st.n) {
+        HIPCHK(c, hipMemcpyAsync(c->p_lo.p, st.lo.p, 8 * (size_t)W * st.n, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->p_hi.p, st.hi.p, 8 * (size_t)W * st.n, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->p_gid.p, st.gid.p, 4 * st.n, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->p_snap.p, st.snap.p, 8 * st.n, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->p_txn.p, st.txn.p, 4 * st.n, hipMemcpyHostToDevice, s));
     }
-    if (m.n_lock) {
-        HIPCHK(c, hipMemcpyAsync(c->p_lock_table.p, m.lock_table, 4 * m.n_lock, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->p_lock_snap.p, m.lock_snap, 8 * m.n_lock, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->p_lock_txn.p, m.lock_txn, 4 * m.n_lock, hipMemcpyHostToDevice, s));
+    if (st.n_lock) {
+        HIPCHK(c, hipMemcpyAsync(c->p_lock_table.p, st.lock_table.p, 4 * st.n_lock, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->p_lock_snap.p, st.lock_snap.p, 8 * st.n_lock, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->p_lock_txn.p, st.lock_txn.p, 4 * st.n_lock, hipMemcpyHostToDevice, s));
     }
     hsc_probe_batch b{};
-    b.n = m.n;
+    b.n = st.n;
     b.lo = c->p_lo.as<uint64_t>();
     b.hi = c->p_hi.as<uint64_t>();
     b.gid = c->p_gid.as<uint32_t>();
     b.snap = c->p_snap.as<uint64_t>();
     b.txn = c->p_txn.as<uint32_t>();
-    b.n_lock = m.n_lock;
+    b.n_lock = st.n_lock;
     b.lock_table = c->p_lock_table.as<uint32_t>();
     b.lock_snap = c->p_lock_snap.as<uint64_t>();
     b.lock_txn = c->p_lock_txn.as<uint32_t>();
-    b.n_txn = m.n_txn;
+    b.n_txn = st.n_txn;
     b.verdict = c->p_verdict.as<uint8_t>();
     b.bitmap = nullptr;
-    int rc = probe(c, &b);
+    const int rc = probe(c, &b);
     if (rc) return rc;
-    std::vector<uint8_t> v(std::max<size_t>(m.n_txn, 1));
-    if (m.n_txn) HIPCHK(c, hipMemcpyAsync(v.data(), c->p_verdict.p, m.n_txn, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
+    if (st.n_txn)
+        HIPCHK(c, hipMemcpyAsync(st.verdict.p, c->p_verdict.p, st.n_txn, hipMemcpyDeviceToHost, s));
+    if (!st.done) HIPCHK(c, hipEventCreateWithFlags(&st.done, hipEventDisableTiming));
+    HIPCHK(c, hipEventRecord(st.done, s));
+    return HSC_OK;
+}
+
+// Wait for st's download; rc_out[t] = forced | device verdict.
+static int finish_stage(hsc_ctx *c, Stage &st, int *rc_out)
+{
+    HIPCHK(c, hipEventSynchronize(st.done));
+    const uint8_t *f = st.forced.as<uint8_t>(), *v = st.verdict.as<uint8_t>();
+    for (size_t t = 0; t < st.n_txn; ++t) rc_out[t] = (f[t] | v[t]) ? 1 : 0;
+    return HSC_OK;
+}
+
+// Full checks of every read set of src: marshal (host threads) -> upload ->
+// join -> download.  A large batch runs as a pipeline of chunks over the two
+// staging sets: chunk i + 1 is marshalled on the host while chunk i is
+// uploaded, probed and read back.
+template <class Src>
+static int check_src(hsc_ctx *c, const Src &src, int *rc_out)
+{
+    if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
+    const int T = src.ntxn();
+    const int nchunks = T >= 2 * kPipeTxns ? (T + kPipeTxns - 1) / kPipeTxns : 1;
+    const int per = std::max(1, (T + nchunks - 1) / nchunks);
+    int pending[2] = {-1, -1};
+    int rc = HSC_OK;
+    for (int i = 0; i < nchunks && rc == HSC_OK; ++i) {
+        Stage &st = c->stage[i & 1];
+        if (pending[i & 1] >= 0) rc = finish_stage(c, st, rc_out + pending[i & 1]);
+        pending[i & 1] = -1;
+        const int t0 = i * per, t1 = std::min(T, t0 + per);
+        if (rc == HSC_OK) rc = marshal_into(c, src, t0, t1, st);
+        if (rc == HSC_OK) rc = launch_stage(c, st);
+        if (rc == HSC_OK) pending[i & 1] = t0;
+    }
+    for (int i = nchunks; i < nchunks + 2 && rc == HSC_OK; ++i)
+        if (pending[i & 1] >= 0) rc = finish_stage(c, c->stage[i & 1], rc_out + pending[i & 1]);
+    if (rc != HSC_OK) {
+        (void)hipStreamSynchronize(c->stream);  // nothing in flight on the staging sets
+        return rc;
+    }
     collect_timing(c);
-    for (size_t t = 0; t < m.n_txn; ++t) rc_out[t] = (m.forced[t] | v[t]) ? 1 : 0;
     return HSC_OK;
 }
 
@@ -1334,6 +1600,7 @@ int hsc_ctx_create(int device, hsc_ctx **out)
         if (!c) return HSC_ENOMEM;
         c->device = -1;
         c->host_only = true;
+        c->threads = default_threads();
         *out = c;
         return HSC_OK;
     }
@@ -1343,6 +1610,7 @@ int hsc_ctx_create(int device, hsc_ctx **out)
     hsc_ctx *c = new (std::nothrow) hsc_ctx();
     if (!c) return HSC_ENOMEM;
     c->device = device;
+    c->threads = default_threads();
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return HSC_EDEVICE;
@@ -1356,10 +1624,11 @@ void hsc_ctx_destroy(hsc_ctx *c)
 {
     if (!c) return;
     if (c->host_only) {
+        for (Stage &st : c->stage) st.release();
         delete c;
         return;
     }
-    if (!c->host_only) (void)hipSetDevice(c->device);
+    (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     for (auto &L : c->lanes)
         if (L.done) (void)hipEventSynchronize(L.done);
@@ -1376,6 +1645,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->d_ctmp[0], &c->d_ctmp[1], &c->d_ctmp[2], &c->d_ctmp[3], &c->w_tcode,
                     &c->w_tcode2, &c->w_trecs};
     for (DBuf *b : bufs) b->release();
+    for (Stage &st : c->stage) st.release();
     for (DBuf &b : c->co_dev) b.release();
     for (DBuf *b : {&c->e_span, &c->e_cnt, &c->e_txn, &c->e_lsn, &c->e_txn2, &c->e_lsn2, &c->e_gid,
                     &c->e_scratch, &c->e_flags, &c->e_after})
@@ -1878,8 +2148,10 @@ int hsc_check_readsets(hsc_ctx *c, const hsc_readsets *rs, int *rc_out)
     std::lock_guard<std::mutex> g(c->mu);
     if (!c->host_only) (void)hipSetDevice(c->device);
     int rc = ensure_built(c);
-    if (!rc) rc = marshal_readsets(c, rs);
-    if (!rc) rc = run_marshalled(c, rc_out);
+    if (!rc) {
+        std::vector<int> tmap;
+        rc = check_src(c, flat_src(c, rs, tmap), rc_out);
+    }
     if (rc)
         for (int t = 0; t < rs->ntxn; ++t) rc_out[t] = 1;  // fail closed
     return rc;
@@ -1900,6 +2172,8 @@ int hip_serial_check_batch(void *vctx, void *const *ranges, unsigned int *file,
     std::vector<int> slot(n, -1);  // element -> txn index in the device batch
     std::vector<hsc_currangearr *> full;
     std::vector<uint64_t> snaps;
+    full.reserve(n);
+    snaps.reserve(n);
     for (int i = 0; i < n; ++i) {
         hsc_currangearr *a = (hsc_currangearr *)ranges[i];
         rc_out[i] = 0;
@@ -1918,39 +2192,19 @@ int hip_serial_check_batch(void *vctx, void *const *ranges, unsigned int *file,
         snaps.push_back(S);
     }
     if (full.empty()) return HSC_OK;
-    marshal_begin(c, full.size());
-    std::vector<TxnTable> tabs;
-    for (size_t t = 0; t < full.size(); ++t) {
-        const uint64_t S = snaps[t];
-        int f = full_forced(c, S);
-        if (f >= 0) {
-            c->m_forced[t] = (uint8_t)f;
-            continue;
-        }
-        hsc_currangearr *a = full[t];
-        auto get = [&](int k) {
-            const hsc_currange *r = a->ranges[k];
-            RangeRef x;
-            auto it = r->tbname ? c->table_ids.find(r->tbname) : c->table_ids.end();
-            x.tid = it == c->table_ids.end() ? -1 : it->second;
-            x.idxnum = r->idxnum;
-            x.lkey = (const uint8_t *)r->lkey;
-            x.rkey = (const uint8_t *)r->rkey;
-            x.lkeylen = r->lkeylen;
-            x.rkeylen = r->rkeylen;
-            x.lflag = r->lflag;
-            x.rflag = r->rflag;
-            x.islocked = r->islocked;
-            return x;
-        };
-        marshal_txn(c, (uint32_t)t, S, a->size, get, tabs);
-    }
-    marshal_finish(c, full.size());
     std::vector<int> rcs(full.size(), 1);
-    rc = run_marshalled(c, rcs.data());
+    rc = check_src(c, ArrSrc{full.data(), snaps.data(), (int)full.size()}, rcs.data());
     for (int i = 0; i < n; ++i)
         if (slot[i] >= 0) rc_out[i] = rc ? 1 : rcs[slot[i]];
     return rc;
+}
+
+int hsc_set_threads(hsc_ctx *c, int n)
+{
+    if (!c || n < 0) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->threads = n ? std::min(n, 256) : default_threads();
+    return HSC_OK;
 }
 
 int hip_bdb_osql_serial_check(void *ctx, void *ranges, unsigned int *file, unsigned int *offset,

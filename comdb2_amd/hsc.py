@@ -123,7 +123,8 @@ EXPORTS = [
     "hsc_enable_timing", "hsc_dep_graph_scc", "hsc_dep_graph_edges",
     "hsc_window_ingest_raw", "hsc_decode_log", "hsc_decode_serial", "hsc_check_serial",
     "hsc_set_layout", "hsc_window_layout", "hsc_coalesce_readsets", "hsc_rw_edges",
-    "hsc_window_code_words", "hsc_dep_graph_build", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
+    "hsc_window_code_words", "hsc_set_threads", "hsc_currangearrs_build",
+    "hsc_currangearrs_free", "hsc_dep_graph_build", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
 ]
 
 (LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES,
@@ -192,6 +193,9 @@ def load() -> C.CDLL:
                                         C.POINTER(C.POINTER(_ReadSets))]),
         "hsc_check_serial": (C.c_int, [_p, C.POINTER(_SerialMsgs), C.POINTER(C.c_int)]),
         "hsc_set_layout": (C.c_int, [_p, C.c_int]),
+        "hsc_set_threads": (C.c_int, [_p, C.c_int]),
+        "hsc_currangearrs_build": (C.c_int, [C.POINTER(_ReadSets), C.POINTER(C.POINTER(_p))]),
+        "hsc_currangearrs_free": (None, [C.POINTER(_p), C.c_int]),
         "hsc_window_layout": (C.c_int, [_p]),
     }
     for name, (res, args) in sig.items():
@@ -307,6 +311,36 @@ class CurRangeArrays:
         for i, a in enumerate(self.arrs):
             arr[i] = C.cast(C.pointer(a), _p)
         return arr
+
+
+class NativeCurRangeArrs:
+    """CurRangeArr objects built by the library's harness helper
+    (hsc_currangearrs_build) from flat read sets: heap CurRange's with
+    strdup'd names and malloc'd keys, as a comdb2 master holds them.  Much
+    faster than :class:`CurRangeArrays` for large batches."""
+
+    def __init__(self, rs: ReadSets):
+        self.lib = load()
+        s, keep = readsets_struct(rs)
+        out = C.POINTER(_p)()
+        rc = self.lib.hsc_currangearrs_build(C.byref(s), C.byref(out))
+        if rc != HSC_OK:
+            raise HscError(f"hsc_currangearrs_build -> {rc}")
+        self.ptrs, self.n = out, rs.ntxn
+
+    def pointers(self):
+        return self.ptrs
+
+    def close(self):
+        if self.ptrs:
+            self.lib.hsc_currangearrs_free(self.ptrs, self.n)
+            self.ptrs = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Validator:
@@ -457,10 +491,21 @@ class Validator:
         self._chk(rc, "hsc_check_readsets")
         return out[: rs.ntxn]
 
-    def check_batch(self, arrs: CurRangeArrays, regop_only: int = 0) -> np.ndarray:
-        n = len(arrs.arrs)
+    def set_threads(self, n: int) -> None:
+        """Host threads of the marshal (0: the box's CPUs)."""
+        self._chk(self.lib.hsc_set_threads(self.ctx, n), "hsc_set_threads")
+
+    def check_batch(self, arrs, regop_only: int = 0, file: Optional[np.ndarray] = None,
+                    offset: Optional[np.ndarray] = None) -> np.ndarray:
+        """hip_serial_check_batch over CurRangeArrays / NativeCurRangeArrs.
+        file / offset: uint32[n] in/out snapshot LSNs (None: each array's own
+        file / offset, updated in place)."""
+        n = len(arrs.arrs) if hasattr(arrs, "arrs") else arrs.n
         out = np.zeros(max(1, n), dtype=np.int32)
-        rc = self.lib.hip_serial_check_batch(self.ctx, arrs.pointers(), None, None, regop_only, n,
+        u32p = C.POINTER(C.c_uint)
+        fp = file.ctypes.data_as(u32p) if file is not None else None
+        op = offset.ctypes.data_as(u32p) if offset is not None else None
+        rc = self.lib.hip_serial_check_batch(self.ctx, arrs.pointers(), fp, op, regop_only, n,
                                              out.ctypes.data_as(C.POINTER(C.c_int)))
         self._chk(rc, "hip_serial_check_batch")
         return out[:n]

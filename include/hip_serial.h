@@ -355,6 +355,13 @@ typedef struct hsc_coalesced {
 } hsc_coalesced;
 int hsc_coalesce_readsets(hsc_ctx *ctx, const hsc_readsets *rs, hsc_coalesced *out);
 
+/* Host threads that marshal a batch (0 = the box's CPUs: the affinity mask
+ * capped by the cgroup CPU quota; HSC_THREADS overrides that default).  A
+ * batch of >= 65536 read sets runs as a pipeline of 32768-set chunks over two
+ * pinned staging sets: one chunk is marshalled while the previous one is
+ * uploaded, joined and read back. */
+int hsc_set_threads(hsc_ctx *ctx, int n);
+
 /* Flat read sets (snapshots in rs->snap); rc_out[ntxn]; full checks only. */
 int hsc_check_readsets(hsc_ctx *ctx, const hsc_readsets *rs, int *rc_out);
 
@@ -461,6 +468,13 @@ int hsc_dep_graph_cut(hsc_ctx *ctx, const uint8_t *cover_dev, uint64_t *rows_dev
 int hsc_dep_graph_scc_cut(hsc_ctx *ctx, uint32_t ntxn, const uint8_t *cover_dev,
                           const uint64_t *rows_dev, size_t m, uint32_t *scc_dev,
                           hsc_graph_stats *stats);
+
+/* ---- harness support (tests / bench; not on the check path) --------------
+ * CurRangeArr objects as comdb2 holds a received read set (db/comdb2.h:1105-1124;
+ * strdup'd table names, malloc'd keys, serial_readset_get db/osqlcomm.c:948-993),
+ * one per read set of rs: *out = void *[ntxn] of hsc_currangearr *. */
+int hsc_currangearrs_build(const hsc_readsets *rs, void ***out);
+void hsc_currangearrs_free(void **arrs, int n);
 
 #ifdef __cplusplus
 }

@@ -168,3 +168,33 @@ def test_config5_zipf_hot_keys(validator, oracle_mod):
     validator.ingest_log(c5.log)
     got = validator.check_readsets(c5.readsets)
     np.testing.assert_array_equal(got != 0, want != 0)
+
+
+def test_pipelined_batch_entry_matches_oracle(validator, oracle_mod):
+    """A batch large enough for the chunked pipeline of the drop-in entry
+    (>= 65536 read sets: chunks marshalled on the host threads while the
+    previous chunk is on the GPU) equals the flat entry on every read set and
+    the oracle on a sample; post-call (file, offset) = the end LSN."""
+    from comdb2_amd.hsc import NativeCurRangeArrs
+    c2 = config2(n_commits=20_000, n_txn=70_000, value_bits=24, width=1 << 6, snap_recent=0.2)
+    validator.ingest_log(c2.log)
+    flat = validator.check_readsets(c2.readsets)
+    arrs = NativeCurRangeArrs(c2.readsets)
+    try:
+        snaps = np.asarray(c2.readsets.snap, np.uint64)
+        f = np.ascontiguousarray(snaps >> np.uint64(32), np.uint32)
+        o = np.ascontiguousarray(snaps & np.uint64(0xFFFFFFFF), np.uint32)
+        for threads in (1, 0):
+            validator.set_threads(threads)
+            ff, oo = f.copy(), o.copy()
+            got = validator.check_batch(arrs, file=ff, offset=oo)
+            np.testing.assert_array_equal(got != 0, flat != 0)
+            end = int(c2.log.end_lsn)
+            assert (ff == end >> 32).all() and (oo == end & 0xFFFFFFFF).all()
+    finally:
+        arrs.close()
+        validator.set_threads(0)
+    sample = np.arange(0, c2.readsets.ntxn, 97)
+    want, _, _ = oracle_mod.check(c2.log, c2.readsets.subset(sample))
+    np.testing.assert_array_equal(flat[sample] != 0, want != 0)
+    assert 0.05 < (flat != 0).mean() < 0.95
