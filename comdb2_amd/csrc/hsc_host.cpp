@@ -158,6 +158,8 @@ struct hsc_ctx {
     Dir16 cdir{}, tdir{};
     uint32_t trad_m = 0;       // tile bucket table size (0: none)
     uint32_t ncommit = 0;
+    bool rank_lsn32 = false;   // narrow tiles: rows carry lsn - rank_base + 1 (NarrowTiles)
+    uint64_t rank_base = 0;
     DBuf w_tcode, w_tcode2, w_trecs;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
     DBuf d_gstart, d_gend, d_tmax, d_table_max, d_group_table, d_count, d_sp_g, d_sp_w;
@@ -666,8 +668,18 @@ static int device_build(hsc_ctx *c, size_t n_in)
         c->ntiles32 = false;
         c->trad_m = 0;
         if (wn.log2T == 12 && wn.ntiles <= (uint32_t)kHistCap && c->ncommit > 0) {
-            HIPCHK(c, dir16_build(c->d_commits.as<uint64_t>(), c->ncommit, c->d_cdir, c->cdir,
-                                  narrow_tiles_dir_lds(), s));
+            // commit span: rank-free rows (lsn - oldest commit + 1) when it fits 32 bits
+            uint64_t span[2] = {0, 0};
+            HIPCHK(c, hipMemcpyAsync(&span[0], c->d_commits.as<uint64_t>(), 8, hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipMemcpyAsync(&span[1], c->d_commits.as<uint64_t>() + c->ncommit - 1, 8,
+                                     hipMemcpyDeviceToHost, s));
+            HIPCHK(c, hipStreamSynchronize(s));
+            c->rank_lsn32 = span[1] - span[0] <= kLsn32MaxSpan && !getenv("HSC_RANK_DIR");
+            c->rank_base = span[0];
+            c->cdir = Dir16{};
+            if (!c->rank_lsn32)
+                HIPCHK(c, dir16_build(c->d_commits.as<uint64_t>(), c->ncommit, c->d_cdir, c->cdir,
+                                      narrow_tiles_dir_lds(), s));
             HIPCHK(c, dir16_build(wn.sp_w, wn.ntiles, c->d_tdir, c->tdir, narrow_tiles_dir_lds(), s));
             c->trad_m = narrow_trad_buckets(wn.ntiles);
             if (c->trad_m) {
@@ -678,8 +690,9 @@ static int device_build(hsc_ctx *c, size_t n_in)
             HIPCHK(c, c->d_rank32.ensure(4 * (size_t)nv.len[0]));
             uint32_t *flag = c->d_count.as<uint32_t>() + 4;
             HIPCHK(c, narrow_tiles_build(nv.keys, c->d_lsn.as<uint64_t>(), (uint32_t)c->n, nv.len[0],
-                                         c->cdir, c->d_key32.as<uint32_t>(),
-                                         c->d_rank32.as<uint32_t>(), flag, s));
+                                         c->cdir, c->rank_lsn32, c->rank_base,
+                                         c->d_key32.as<uint32_t>(), c->d_rank32.as<uint32_t>(),
+                                         flag, s));
             uint32_t wide32 = 1;
             HIPCHK(c, hipMemcpyAsync(&wide32, flag, 4, hipMemcpyDeviceToHost, s));
             HIPCHK(c, hipStreamSynchronize(s));
@@ -1280,9 +1293,21 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     work.item_off = c->w_items.as<uint32_t>();
     work.item_tile = c->w_item_tile.as<uint32_t>();
     work.item_desc = c->w_item_desc.as<uint4>();
+#ifdef HSC_STAMPS
+    static DBuf stamp_buf;
+    if (getenv("HSC_STAMPS")) {
+        if (!stamp_buf.p) {
+            HIPCHK(c, stamp_buf.ensure(8 * 2 * 8192 * 8));
+            HIPCHK(c, hipMemsetAsync(stamp_buf.p, 0, 8 * 2 * 8192 * 8, s));
+        }
+        work.stamps = stamp_buf.as<uint64_t>();
+    }
+#endif
     NarrowTiles ntl{};
     ntl.key32 = c->d_key32.as<uint32_t>();
     ntl.rank32 = c->d_rank32.as<uint32_t>();
+    ntl.rank_lsn32 = c->rank_lsn32;
+    ntl.rank_base = c->rank_base;
     ntl.cdir = c->cdir;
     ntl.tdir = c->tdir;
     ntl.trad = c->trad_m ? c->d_trad.as<uint32_t>() : nullptr;
@@ -1314,6 +1339,44 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     }
     HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
+#ifdef HSC_STAMPS
+    if (work.stamps) {  // diagnostic build: phase durations (median over blocks, cycles)
+        std::vector<uint64_t> h(2 * 8192 * 8);
+        HIPCHK(c, hipMemcpyAsync(h.data(), work.stamps, 8 * h.size(), hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+        const uint32_t nb[2] = {8 * ((work.G + 7) / 8), max_items};
+        const int np[2] = {7, 3};
+        for (int k = 0; k < 2; ++k) {
+            fprintf(stderr, "[stamps] %s blocks %u:", k ? "join" : "locate", nb[k]);
+            uint64_t t0 = ~0ull, t1 = 0;
+            for (uint32_t b = 0; b < nb[k] && b < 8192; ++b) {
+                const uint64_t *r = &h[((size_t)k * 8192 + b) * 8];
+                if (!r[0]) continue;
+                t0 = std::min(t0, r[0]);
+                t1 = std::max(t1, r[np[k] - 1]);
+            }
+            for (int q = 1; q < np[k]; ++q) {
+                std::vector<uint64_t> d;
+                for (uint32_t b = 0; b < nb[k] && b < 8192; ++b) {
+                    const uint64_t *r = &h[((size_t)k * 8192 + b) * 8];
+                    if (r[q] && r[q - 1]) d.push_back(r[q] - r[q - 1]);
+                }
+                std::sort(d.begin(), d.end());
+                fprintf(stderr, " p%d %llu", q, d.empty() ? 0ull : (unsigned long long)d[d.size() / 2]);
+            }
+            std::vector<uint64_t> st;
+            for (uint32_t b = 0; b < nb[k] && b < 8192; ++b) {
+                const uint64_t *r = &h[((size_t)k * 8192 + b) * 8];
+                if (r[0]) st.push_back(r[0] - t0);
+            }
+            std::sort(st.begin(), st.end());
+            fprintf(stderr, " | span %llu, start p50 %llu p90 %llu\n", (unsigned long long)(t1 - t0),
+                    st.empty() ? 0ull : (unsigned long long)st[st.size() / 2],
+                    st.empty() ? 0ull : (unsigned long long)st[st.size() * 9 / 10]);
+        }
+        HIPCHK(c, hipMemsetAsync(work.stamps, 0, 8 * h.size(), s));
+    }
+#endif
     return HSC_OK;
 }
 

@@ -144,7 +144,23 @@ struct ProbeWork {
     uint64_t *recs;        // join records
     uint32_t G, chunk;     // probe chunks (one workgroup each in locate/scatter)
     int lds_mode;          // ntiles <= kHistCap: LDS histograms, no global atomics
+    uint64_t *stamps;      // diagnostic builds (HSC_STAMPS): [kernel][block][8] s_memtime
 };
+// Diagnostic phase stamps (HSC_STAMPS builds only): thread 0 of a block
+// records s_memtime at phase boundaries into a buffer of its own (never an
+// output), read back and summarized by the host.
+#ifdef HSC_STAMPS
+#define HSC_STAMP(work, kern, k)                                                          \
+    do {                                                                                  \
+        if (threadIdx.x == 0 && (work).stamps)                                            \
+            (work).stamps[((size_t)(kern) * 8192 + blockIdx.x) * 8 + (k)] =               \
+                __builtin_amdgcn_s_memtime();                                             \
+    } while (0)
+#else
+#define HSC_STAMP(work, kern, k) \
+    do {                         \
+    } while (0)
+#endif
 hipError_t launch_locate(const WinView &w, const ProbeView &p, const ProbeWork &work,
                          uint8_t *verdict, hipStream_t s);
 hipError_t launch_plan(const WinView &w, const ProbeWork &work, hipStream_t s);
@@ -198,7 +214,15 @@ hipError_t dir16_build(const uint64_t *src, uint32_t n, struct DBuf &buf, Dir16 
 // Narrow tiles (dense batches): 4096-row tiles of (u32 key delta, u32 commit rank).
 struct NarrowTiles {
     const uint32_t *key32;     // [len0] key64 - first key64 of the tile
-    const uint32_t *rank32;    // [len0] 1 + index of the row's LSN in commits
+    const uint32_t *rank32;    // [len0] commit time of the row (see rank_lsn32)
+    // rank_lsn32: the window's commit LSNs span < 2^32 - 2 (a window inside
+    // one log file, or files that close together): rank32 = lsn - base + 1
+    // and a snapshot S maps to clamp(S - base + 1) in O(1).  Otherwise
+    // rank32 = 1 + the index of the row's LSN among the distinct commit LSNs
+    // and S maps to #commits <= S through cdir.  Either way lsn > S <=>
+    // rank32 > r(S).
+    int rank_lsn32;
+    uint64_t rank_base;        // lsn32 mode: the oldest commit LSN of the window
     Dir16 cdir;                // directory of the window's distinct commit LSNs
     Dir16 tdir;                // directory of the first code of every tile
     const uint32_t *trad;      // [trad_m + 2] bucket table over tile first codes
@@ -212,8 +236,16 @@ struct NarrowTiles {
 hipError_t check_sorted_u64(const uint64_t *v, size_t n, uint32_t *flag, hipStream_t s);
 // rank32 by a search of cdir (the 16-ary directory over the commit LSNs C)
 hipError_t narrow_tiles_build(const uint64_t *key64, const uint64_t *lsn, uint32_t n, uint32_t len,
-                              const Dir16 &cdir, uint32_t *key32, uint32_t *rank32,
-                              uint32_t *flag, hipStream_t s);
+                              const Dir16 &cdir, int rank_lsn32, uint64_t rank_base,
+                              uint32_t *key32, uint32_t *rank32, uint32_t *flag, hipStream_t s);
+// r(S) of lsn32 mode: lsn > S <=> lsn - base + 1 > r(S)
+__host__ __device__ inline uint32_t lsn32_rank(uint64_t S, uint64_t base)
+{
+    if (S < base) return 0;
+    const uint64_t d = S - base + 1;
+    return d >= 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)d;
+}
+constexpr uint64_t kLsn32MaxSpan = 0xFFFFFFFDull;  // rows: lsn - base + 1 <= 0xFFFFFFFE
 uint32_t narrow_tiles_chunk();
 // Bucket table of the tiles' first codes (locate's tile search from LDS);
 // returns the bucket count m (0: too many tiles, use the directory).

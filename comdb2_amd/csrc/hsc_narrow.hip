@@ -420,16 +420,28 @@ __global__ void k_key32(const uint64_t *key64, uint32_t n, uint32_t len, uint32_
     key32[i] = (uint32_t)d;
 }
 
+// lsn32 mode: rank32 = lsn - base + 1 (pads 0)
+__global__ void k_rank_lsn32(const uint64_t *lsn, uint32_t n, uint32_t len, uint64_t base,
+                             uint32_t *rank)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < len) rank[i] = i < n ? (uint32_t)(lsn[i] - base) + 1 : 0;
+}
+
 hipError_t narrow_tiles_build(const uint64_t *key64, const uint64_t *lsn, uint32_t n, uint32_t len,
-                              const Dir16 &cdir, uint32_t *key32, uint32_t *rank32,
-                              uint32_t *flag, hipStream_t s)
+                              const Dir16 &cdir, int rank_lsn32, uint64_t rank_base,
+                              uint32_t *key32, uint32_t *rank32, uint32_t *flag, hipStream_t s)
 {
     hipError_t e = hipMemsetAsync(flag, 0, 4, s);
     if (e != hipSuccess || len == 0) return e;
     k_key32<<<(len + 255) / 256, 256, 0, s>>>(key64, n, len, key32, flag);
-    const uint32_t per = kRankThreads * kRankK;
-    k_rank32<<<(len + per - 1) / per, kRankThreads, 8 * dir16_lds_entries(cdir), s>>>(lsn, n, len,
-                                                                                    cdir, rank32);
+    if (rank_lsn32) {
+        k_rank_lsn32<<<(len + 255) / 256, 256, 0, s>>>(lsn, n, len, rank_base, rank32);
+    } else {
+        const uint32_t per = kRankThreads * kRankK;
+        k_rank32<<<(len + per - 1) / per, kRankThreads, 8 * dir16_lds_entries(cdir), s>>>(
+            lsn, n, len, cdir, rank32);
+    }
     return hipGetLastError();
 }
 
@@ -581,7 +593,10 @@ __global__ __launch_bounds__(kRankThreads) void k_rank32(const uint64_t *lsn, ui
 #define HSC_DIR_LDS 4400
 #endif
 constexpr int kLocTP = HSC_LOC_TP;
-constexpr int kLocTThreads = 1024;  // <= 4096 probes per chunk (in-chunk ranks fit 12 bits)
+#ifndef HSC_LOC_THREADS
+#define HSC_LOC_THREADS 1024
+#endif
+constexpr int kLocTThreads = HSC_LOC_THREADS;  // <= 4096 probes per chunk (in-chunk ranks fit 12 bits)
 static_assert(kLocTP * kLocTThreads <= 4096, "in-chunk ranks are 12 bits");
 constexpr uint32_t kHasSecond = 1u << 31;
 constexpr int kDirLds = HSC_DIR_LDS;  // directory entries staged in LDS per directory
@@ -677,7 +692,7 @@ __host__ __device__ inline LocLds loc_lds(const NarrowTiles &nt, uint32_t ntiles
     L.first = o;
     o += 8 * (nt.trad ? ((ntiles + 1) & ~1u) : dir16_lds_entries(nt.tdir));
     L.cdir = o;
-    o += 8 * dir16_lds_entries(nt.cdir);
+    o += nt.rank_lsn32 ? 0 : 8 * dir16_lds_entries(nt.cdir);
     L.hist = o;
     o += 4 * ((ntiles + 3) & ~3u);
     L.trad = o;
@@ -744,6 +759,7 @@ __global__ __launch_bounds__(kLocTThreads) void k_locate_t(NarrowView nv, WinVie
     uint32_t *rb = (uint32_t *)(lb + L.rbuf) + (threadIdx.x & ~63u);
     const uint32_t g = xcd_chunk(blockIdx.x, (work.G + 7) / 8);
     if (g >= work.G) return;
+    HSC_STAMP(work, 0, 0);
     const uint32_t c0 = g * work.chunk;
     const uint32_t c1 = min(p.n, c0 + work.chunk);
     // all probe loads first
@@ -776,18 +792,22 @@ __global__ __launch_bounds__(kLocTThreads) void k_locate_t(NarrowView nv, WinVie
     } else {
         dir16_stage(nt.tdir, tfirst);
     }
-    dir16_stage(nt.cdir, cdir);
+    if (!nt.rank_lsn32) dir16_stage(nt.cdir, cdir);
     for (uint32_t i = threadIdx.x; i < ntiles; i += kLocTThreads) hist[i] = 0;
     uint64_t lo[kLocTP], hi[kLocTP];
 #pragma unroll
     for (int j = 0; j < kLocTP; ++j)
         locate_codes<W>(nv, p, valid[j] ? qq[j] : 0, gg[j], xl[j], xh[j], lo[j], hi[j]);
     __syncthreads();  // directories staged, histogram zeroed
+    HSC_STAMP(work, 0, 1);
     // Snapshot ranks r(S) = #commits <= S.  A run of equal snapshots in
     // neighbouring lanes (a read set's ranges) has one head; the wave packs
     // its heads into a list and searches each once, 64 per round.
     uint32_t rs[kLocTP];
-    {
+    if (nt.rank_lsn32) {  // the window spans < 2^32 of log: r(S) in O(1)
+#pragma unroll
+        for (int j = 0; j < kLocTP; ++j) rs[j] = lsn32_rank(snap[j], nt.rank_base);
+    } else {
         const uint64_t le_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
         bool head[kLocTP];
         uint32_t slot[kLocTP];
@@ -823,6 +843,7 @@ __global__ __launch_bounds__(kLocTThreads) void k_locate_t(NarrowView nv, WinVie
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
     }
+    HSC_STAMP(work, 0, 2);
     // end tiles: a = #first < lo - 1 (the tile holding the first row >= lo),
     // bt = #first <= hi - 1 (the tile holding the last row <= hi)
     uint32_t cnt[2 * kLocTP];
@@ -840,6 +861,7 @@ __global__ __launch_bounds__(kLocTThreads) void k_locate_t(NarrowView nv, WinVie
         else
             dir16_count<2 * kLocTP>(nt.tdir, tfirst, keys, act, cnt);
     }
+    HSC_STAMP(work, 0, 3);
     const uint64_t *first = kTrad ? tfirst : wt.sp_w;  // first code of every tile
 #pragma unroll
     for (int j = 0; j < kLocTP; ++j) {
@@ -884,16 +906,19 @@ __global__ __launch_bounds__(kLocTThreads) void k_locate_t(NarrowView nv, WinVie
         if (r0.x & kHasSecond) nt.code2[q] = r1;
         nt.code[q] = r0;
     }
+    HSC_STAMP(work, 0, 4);
     // table locks: any write to a locked table after the snapshot
     for (uint32_t q = g * kLocTThreads + threadIdx.x; q < p.n_lock; q += work.G * kLocTThreads) {
         const uint32_t t = p.lock_table[q];
         if (t < wt.ntables && wt.table_max[t] > p.lock_snap[q]) verdict[p.lock_txn[q]] = 1;
     }
     __syncthreads();
+    HSC_STAMP(work, 0, 5);
     // column g of the tile-major histogram (neighbouring chunks of a line are
     // written from the same XCD)
     const uint32_t hs = hist_stride(work.G);
     for (uint32_t i = threadIdx.x; i < ntiles; i += kLocTThreads) work.hist[(size_t)i * hs + g] = hist[i];
+    HSC_STAMP(work, 0, 6);
 }
 
 hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeView &p,
@@ -1138,6 +1163,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
     __shared__ uint32_t b128[T / 128];
 
     const uint32_t item = blockIdx.x;
+    HSC_STAMP(work, 1, 0);
     uint32_t tile, r0, r1;
     if (item < ntiles) {
         tile = item;
@@ -1179,6 +1205,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
         if ((threadIdx.x & 31) == 0) b128[quad >> 5] = m;
     }
     __syncthreads();
+    HSC_STAMP(work, 1, 1);
     const uint32_t tn = min(T, n - (tile << kTLog2));
 #pragma unroll
     for (int k = 0; k < kRec; ++k) {
@@ -1200,6 +1227,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
         const uint32_t pb = min(jb - T + (kl <= hi), tn);
         if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) verdict[rec[k].w] = 1;
     }
+    HSC_STAMP(work, 1, 2);
 }
 
 hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t n,

@@ -27,33 +27,38 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
     the window fits it) and the wide layout, each against the oracle."""
     want, _, _ = oracle_mod.check(log, rs, nthreads=8)
     got = {}
-    # (layout, tile search): locate finds tiles through the LDS bucket table
-    # by default and through the 16-ary directory with HSC_TILE_DIR set
-    runs = [(LAYOUT_NARROW_DIRECT, 0), (LAYOUT_NARROW_TILES, 0), (LAYOUT_NARROW_TILES, 1),
-            (LAYOUT_NARROW_CODES, 0), (LAYOUT_WIDE, 0)]
+    # (layout, build knob): locate finds tiles through the LDS bucket table by
+    # default and through the 16-ary directory with HSC_TILE_DIR set; rows
+    # carry lsn - oldest commit + 1 when the window spans < 2^32 of log, the
+    # commit rank (directory search of snapshots) with HSC_RANK_DIR set
+    runs = [(LAYOUT_NARROW_DIRECT, None), (LAYOUT_NARROW_TILES, None),
+            (LAYOUT_NARROW_TILES, "HSC_TILE_DIR"), (LAYOUT_NARROW_TILES, "HSC_RANK_DIR"),
+            (LAYOUT_NARROW_CODES, None), (LAYOUT_WIDE, None)]
     try:
-        for layout, tile_dir in runs:
-            if tile_dir:
-                os.environ["HSC_TILE_DIR"] = "1"
+        for layout, knob in runs:
+            if knob:
+                os.environ[knob] = "1"
             v.set_layout(layout)
             v.ingest_log(log)
-            os.environ.pop("HSC_TILE_DIR", None)
+            if knob:
+                os.environ.pop(knob, None)
             assert v.layout == (LAYOUT_WIDE if layout == LAYOUT_WIDE else expect_auto)
             got[layout] = v.check_readsets(rs)
             np.testing.assert_array_equal(got[layout] != 0, want != 0,
-                                          err_msg=f"layout {layout} tile_dir {tile_dir}")
+                                          err_msg=f"layout {layout} knob {knob}")
     finally:
-        os.environ.pop("HSC_TILE_DIR", None)
+        for knob in ("HSC_TILE_DIR", "HSC_RANK_DIR"):
+            os.environ.pop(knob, None)
         v.set_layout(LAYOUT_AUTO)
     return want
 
 
 def keyed_case(seed, n_commits, per_commit, key_fn, range_fn, n_txn, ranges_per_txn=6,
-               snap_recent=0.3, dta_table=False):
+               snap_recent=0.3, dta_table=False, step=64):
     """One index of keys key_fn(rng) written by n_commits txns; read sets of
     range_fn(rng) ranges with snapshots among the most recent commits."""
     rng = np.random.default_rng(seed)
-    lb = LogBuilder()
+    lb = LogBuilder(step=step)
     commits = [lb.next_lsn()]
     for c in range(n_commits):
         lb.begin(c)
@@ -160,4 +165,18 @@ def test_empty_and_reversed_ranges(validator, oracle_mod):
         b = a - int(rng.integers(0, 100)) if rng.random() < 0.5 else a
         return Range("t1", 0, F.enc_int64(a), F.enc_int64(b))
     log, rs = keyed_case(15, 3000, 8, key, rng_range, 600)
+    both_layouts(validator, oracle_mod, log, rs, LAYOUT_NARROW)
+
+
+def test_multi_file_window_commit_ranks(validator, oracle_mod):
+    """A window over many log files (records 2^28 bytes apart: a new file every
+    16 records) spans more than 2^32 of LSN space, so the narrow tiles carry
+    commit ranks and snapshots go through the commit directory."""
+    key = lambda rng: F.enc_int64(int(rng.integers(0, 1 << 22)))
+
+    def rng_range(rng):
+        a = int(rng.integers(0, 1 << 22))
+        return Range("t1", 0, F.enc_int64(a), F.enc_int64(a + int(rng.integers(0, 1 << 14))))
+    log, rs = keyed_case(16, 4000, 6, key, rng_range, 900, step=1 << 28, snap_recent=0.05)
+    assert int(log.lsn[-1] >> 32) - int(log.lsn[0] >> 32) > 100
     both_layouts(validator, oracle_mod, log, rs, LAYOUT_NARROW)
