@@ -152,6 +152,7 @@ struct hsc_ctx {
     DBuf d_nzero, d_ntmax, d_nsp_g, d_nsp_w, d_ngs, d_nscratch;
     DBuf p_code_lo, p_code_hi, p_zero;
     uint32_t probe_ntiles = 0;  // tiles of the view the last probe ran on
+    bool probe_buckets = false; // the last probe ran the narrow tiles (fixed-capacity buckets)
     // narrow tiles: u32 key deltas + commit ranks (dense batches)
     bool ntiles32 = false;
     DBuf d_commits, d_cdir, d_tdir, d_trad, d_done, w_vflags, d_key32, d_rank32, d_ctmp[4];
@@ -1262,6 +1263,7 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
 {
     hipStream_t s = c->stream;
     c->probe_ntiles = wn.ntiles;
+    c->probe_buckets = true;
     const uint32_t nt = std::max<uint32_t>(wn.ntiles, 1);
     ProbeWork work{};
     work.lds_mode = 1;
@@ -1272,20 +1274,18 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     work.G = (uint32_t)std::max<size_t>(1, (nwork + work.chunk - 1) / work.chunk);
     const size_t n1 = std::max<uint32_t>(p.n, 1);
     HIPCHK(c, c->w_hist.ensure(4 * (size_t)hist_stride(work.G) * nt));
-    if (!c->d_done.p) {  // plan arrival counter: zeroed once, reset by its last block
-        HIPCHK(c, c->d_done.ensure(64));
-        HIPCHK(c, hipMemsetAsync(c->d_done.p, 0, 64, s));
-    }
+    // tile buckets of kTileCap records, then the overflow area (at most 2n
+    // records spill); join items: one per tile + the overflow chunks (each hot
+    // tile rounds its own run up: at most 2 ceil(2n / kJoinChunk) of them)
     HIPCHK(c, c->w_counts.ensure(4 * ((size_t)nt + 1)));
     HIPCHK(c, c->w_bucket.ensure(4 * ((size_t)nt + 1)));
-    HIPCHK(c, c->w_cursor.ensure(4 * ((size_t)nt + 1)));
-    HIPCHK(c, c->w_items.ensure(4 * ((size_t)nt + 1)));
-    const uint32_t max_items = nt + (uint32_t)((2 * n1 + kJoinChunk - 1) / kJoinChunk);
-    HIPCHK(c, c->w_item_tile.ensure(4 * (size_t)max_items + 16));
-    HIPCHK(c, c->w_item_desc.ensure(16 * (size_t)max_items + 16));
+    HIPCHK(c, c->w_items.ensure(4 * std::max<size_t>((size_t)nt + 1, 4)));
+    const uint32_t extra_items = 2 * (uint32_t)((2 * n1 + kJoinChunk - 1) / kJoinChunk);
+    const uint32_t max_items = nt + extra_items;
+    HIPCHK(c, c->w_item_desc.ensure(16 * (size_t)extra_items + 16));
     HIPCHK(c, c->w_tcode.ensure(16 * n1));
     HIPCHK(c, c->w_tcode2.ensure(16 * n1));
-    HIPCHK(c, c->w_trecs.ensure(32 * n1));
+    HIPCHK(c, c->w_trecs.ensure(16 * ((size_t)nt * kTileCap + 2 * n1)));
     work.hist = c->w_hist.as<uint32_t>();
     work.counts = c->w_counts.as<uint32_t>();
     work.bucket_off = c->w_bucket.as<uint32_t>();
@@ -1328,7 +1328,7 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     HIPCHK(c, launch_locate_t(c->nv, wn, p, work, ntl, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     if (p.n && wn.ntiles) {
-        HIPCHK(c, launch_plan_t(work, wn.ntiles, c->d_done.as<uint32_t>(), s));
+        HIPCHK(c, launch_plan_t(work, wn.ntiles, c->w_items.as<uint32_t>(), s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
         HIPCHK(c, launch_scatter_t(p, work, ntl, wn.ntiles, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
@@ -1345,7 +1345,7 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
         HIPCHK(c, hipMemcpyAsync(h.data(), work.stamps, 8 * h.size(), hipMemcpyDeviceToHost, s));
         HIPCHK(c, hipStreamSynchronize(s));
         const uint32_t nb[2] = {8 * ((work.G + 7) / 8), max_items};
-        const int np[2] = {7, 3};
+        const int np[2] = {5, 3};
         for (int k = 0; k < 2; ++k) {
             fprintf(stderr, "[stamps] %s blocks %u:", k ? "join" : "locate", nb[k]);
             uint64_t t0 = ~0ull, t1 = 0;
@@ -1476,6 +1476,7 @@ static int probe_tiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w, c
 {
     hipStream_t s = c->stream;
     c->probe_ntiles = w.ntiles;
+    c->probe_buckets = false;
     const uint32_t nt = std::max<uint32_t>(w.ntiles, 1);
     ProbeWork work{};
     work.lds_mode = w.ntiles <= (uint32_t)kHistCap;
@@ -1539,10 +1540,16 @@ static int collect_timing(hsc_ctx *c)
     c->last.join_ms = t[3];
     c->last.pack_ms = t[4];
     (void)hipEventElapsedTime(&c->last.probe_total_ms, c->ev[0], c->ev[5]);
-    uint32_t nrec = 0;
-    if (c->probe_ntiles && c->w_bucket.p)
-        HIPCHK(c, hipMemcpy(&nrec, c->w_bucket.as<uint32_t>() + c->probe_ntiles, 4,
-                            hipMemcpyDeviceToHost));
+    uint64_t nrec = 0;
+    if (c->probe_ntiles && c->w_counts.p && c->probe_buckets) {  // per-tile record counts
+        std::vector<uint32_t> cnt(c->probe_ntiles);
+        HIPCHK(c, hipMemcpy(cnt.data(), c->w_counts.p, 4 * cnt.size(), hipMemcpyDeviceToHost));
+        for (uint32_t v : cnt) nrec += v;
+    } else if (c->probe_ntiles && c->w_bucket.p) {
+        uint32_t r = 0;
+        HIPCHK(c, hipMemcpy(&r, c->w_bucket.as<uint32_t>() + c->probe_ntiles, 4, hipMemcpyDeviceToHost));
+        nrec = r;
+    }
     c->last.records = nrec;
     c->last.tiles = c->probe_ntiles;  // tiles of the view the last probe joined over
     return HSC_OK;

@@ -56,6 +56,7 @@ constexpr int kHistCap = 8192;      // tiles whose bucket counters fit in LDS
 constexpr int kDirectPerTile = 8;   // narrow: direct probe below 8 ranges per tile
 constexpr int kJoinThreads = 512;
 constexpr int kJoinChunk = 1024;    // join records per workgroup
+constexpr uint32_t kTileCap = 1024; // narrow tiles: records per tile bucket before it spills
 constexpr int kLdsJoinBudget = 65536;
 
 // Probe codes written by the locate kernel: a | b << 31 | kind << 62.
@@ -299,9 +300,9 @@ __host__ __device__ inline uint32_t hist_stride(uint32_t G) { return (G + 7) & ~
 // XCD-contiguous chunk order: block b of a grid of 8 * per blocks runs on XCD
 // b % 8 and takes chunk (b % 8) * per + b / 8.
 __host__ __device__ inline uint32_t xcd_chunk(uint32_t b, uint32_t per) { return (b & 7) * per + (b >> 3); }
-// Column scans of the tile-major histogram and the tile plan in one launch
-// (the last workgroup plans; done = a zeroed counter it resets).
-hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *done, hipStream_t s);
+// Column scans of the tile-major histogram into fixed-capacity tile buckets
+// (ctl[0..1]: overflow records / extra join items, zeroed by the locate).
+hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, hipStream_t s);
 // Verdict bytes + bitmap from the internal conflict flags; clears the flags.
 hipError_t launch_pack_flags(uint8_t *flags, uint32_t n_txn, uint8_t *verdict, uint64_t *bitmap,
                              hipStream_t s);

@@ -739,13 +739,41 @@ __device__ __forceinline__ void trad_count(const uint64_t *first, const uint16_t
     for (int k = 0; k < K; ++k) out[k] = act[k] ? l[k] : 0;
 }
 
-// W = key words held in registers (1 or 2), 0 = read from memory (any W)
+// Whole-tile checks of a probe, deferred by one sub-chunk (their sparse-table
+// loads then overlap the next sub-chunk's probe loads): tiles [x, y] hold a
+// row committed after snap -> read set txn of probe q conflicts.
+template <int K>
+struct LocDefer {
+    uint32_t x[K], y[K], q[K];
+    uint64_t snap[K];
+};
+
+template <int K>
+__device__ __forceinline__ void loc_defer_run(const WinView &wt, const ProbeView &p,
+                                              const LocDefer<K> &d, uint8_t *verdict)
+{
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+        if (d.x[k] <= d.y[k] && tiles_max(wt, d.x[k], d.y[k]) > d.snap[k]) verdict[p.txn[d.q[k]]] = 1;
+}
+
+// W = key words held in registers (1 or 2), 0 = read from memory (any W).
+// The chunk's kLocTP probes per thread run as kLocTP / kLocSub sub-chunks of
+// kLocSub probes per thread: the loads of sub-chunk s + 1 are in flight while
+// sub-chunk s is located (codes, snapshot ranks, end tiles, records), so the
+// chunk's HBM reads overlap its LDS / VALU work instead of preceding it.
+#ifndef HSC_LOC_SUB
+#define HSC_LOC_SUB 2
+#endif
+constexpr int kLocSub = HSC_LOC_SUB;
+static_assert(kLocTP % kLocSub == 0, "whole sub-chunks");
 template <int W, bool kTrad>
 __global__ __launch_bounds__(kLocTThreads) void k_locate_t(NarrowView nv, WinView wt,
                                                              ProbeView p, ProbeWork work,
                                                              NarrowTiles nt, uint8_t *verdict)
 {
     constexpr int WR = 2 > W ? 2 : W;
+    constexpr int K = kLocSub, S = kLocTP / kLocSub;
     extern __shared__ __attribute__((aligned(16))) uint64_t lds64[];
     const uint32_t ntiles = wt.ntiles;
     const LocLds L = loc_lds(nt, ntiles);
@@ -760,27 +788,33 @@ __global__ __launch_bounds__(kLocTThreads) void k_locate_t(NarrowView nv, WinVie
     const uint32_t g = xcd_chunk(blockIdx.x, (work.G + 7) / 8);
     if (g >= work.G) return;
     HSC_STAMP(work, 0, 0);
+    if (g == 0 && threadIdx.x < 2) work.item_off[threadIdx.x] = 0;  // the plan's overflow counters
     const uint32_t c0 = g * work.chunk;
     const uint32_t c1 = min(p.n, c0 + work.chunk);
-    // all probe loads first
-    uint32_t qq[kLocTP], gg[kLocTP];
-    bool valid[kLocTP];
-    uint64_t snap[kLocTP], xl[kLocTP][WR], xh[kLocTP][WR];
+    // probe registers: buffer 0 / 1 alternate between sub-chunks (the loop
+    // below is unrolled, so every index is a compile-time constant)
+    uint32_t qq[2][K], gg[2][K];
+    bool valid[2][K];
+    uint64_t snap[2][K], xl[2][K][WR], xh[2][K][WR];
+    auto load = [&](int s, int buf) {
 #pragma unroll
-    for (int j = 0; j < kLocTP; ++j) {
-        qq[j] = c0 + threadIdx.x + kLocTThreads * j;
-        valid[j] = qq[j] < c1;
-        const uint32_t q = valid[j] ? qq[j] : 0;
-        // read-once inputs: non-temporal, so they do not push the window's
-        // rows out of the caches between batches
-        gg[j] = p.n ? __builtin_nontemporal_load(p.gid + q) : 0;
-        snap[j] = p.n ? __builtin_nontemporal_load(p.snap + q) : 0;
+        for (int k = 0; k < K; ++k) {
+            const int j = s * K + k;
+            qq[buf][k] = c0 + threadIdx.x + kLocTThreads * j;
+            valid[buf][k] = qq[buf][k] < c1;
+            const uint32_t q = valid[buf][k] ? qq[buf][k] : 0;
+            // read-once inputs: non-temporal, so they do not push the window's
+            // rows out of the caches between batches
+            gg[buf][k] = p.n ? __builtin_nontemporal_load(p.gid + q) : 0;
+            snap[buf][k] = p.n ? __builtin_nontemporal_load(p.snap + q) : 0;
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-            xl[j][w] = p.n ? __builtin_nontemporal_load(p.lo + (size_t)w * p.n + q) : 0;
-            xh[j][w] = p.n ? __builtin_nontemporal_load(p.hi + (size_t)w * p.n + q) : 0;
+            for (int w = 0; w < W; ++w) {
+                xl[buf][k][w] = p.n ? __builtin_nontemporal_load(p.lo + (size_t)w * p.n + q) : 0;
+                xh[buf][k][w] = p.n ? __builtin_nontemporal_load(p.hi + (size_t)w * p.n + q) : 0;
+            }
         }
-    }
+    };
+    load(0, 0);
     int tshift = 0;
     if constexpr (kTrad) {
         const u64x2 *src = (const u64x2 *)wt.sp_w;
@@ -794,105 +828,120 @@ __global__ __launch_bounds__(kLocTThreads) void k_locate_t(NarrowView nv, WinVie
     }
     if (!nt.rank_lsn32) dir16_stage(nt.cdir, cdir);
     for (uint32_t i = threadIdx.x; i < ntiles; i += kLocTThreads) hist[i] = 0;
-    uint64_t lo[kLocTP], hi[kLocTP];
-#pragma unroll
-    for (int j = 0; j < kLocTP; ++j)
-        locate_codes<W>(nv, p, valid[j] ? qq[j] : 0, gg[j], xl[j], xh[j], lo[j], hi[j]);
     __syncthreads();  // directories staged, histogram zeroed
     HSC_STAMP(work, 0, 1);
-    // Snapshot ranks r(S) = #commits <= S.  A run of equal snapshots in
-    // neighbouring lanes (a read set's ranges) has one head; the wave packs
-    // its heads into a list and searches each once, 64 per round.
-    uint32_t rs[kLocTP];
-    if (nt.rank_lsn32) {  // the window spans < 2^32 of log: r(S) in O(1)
-#pragma unroll
-        for (int j = 0; j < kLocTP; ++j) rs[j] = lsn32_rank(snap[j], nt.rank_base);
-    } else {
-        const uint64_t le_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-        bool head[kLocTP];
-        uint32_t slot[kLocTP];
-        uint32_t H = 0;
-#pragma unroll
-        for (int j = 0; j < kLocTP; ++j) {
-            const uint64_t prev = __shfl_up(snap[j], 1, 64);
-            head[j] = lane == 0 || prev != snap[j];
-            const uint64_t m = __ballot(head[j]);
-            slot[j] = H + __popcll(m & le_mask) - 1;  // this lane's head
-            H += __popcll(m);
-        }
-        for (uint32_t b0 = 0; b0 < H; b0 += 64) {
-#pragma unroll
-            for (int j = 0; j < kLocTP; ++j)
-                if (head[j] && slot[j] - b0 < 64) sb[slot[j] - b0] = snap[j];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const bool act[1] = {lane < H - b0};
-            const uint64_t xs[1] = {act[0] ? dir_le(sb[lane]) : 0};
-            uint32_t r[1];
-            dir16_count<1>(nt.cdir, cdir, xs, act, r);
-            rb[lane] = r[0];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-            for (int j = 0; j < kLocTP; ++j)
-                if (slot[j] - b0 < 64) rs[j] = rb[slot[j] - b0];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-    }
-    HSC_STAMP(work, 0, 2);
-    // end tiles: a = #first < lo - 1 (the tile holding the first row >= lo),
-    // bt = #first <= hi - 1 (the tile holding the last row <= hi)
-    uint32_t cnt[2 * kLocTP];
-    {
-        uint64_t keys[2 * kLocTP];
-        bool act[2 * kLocTP];
-#pragma unroll
-        for (int j = 0; j < kLocTP; ++j) {
-            keys[2 * j] = lo[j];
-            keys[2 * j + 1] = dir_le(hi[j]);
-            act[2 * j] = act[2 * j + 1] = valid[j] && lo[j] <= hi[j];
-        }
-        if constexpr (kTrad)
-            trad_count<2 * kLocTP>(tfirst, T, nt.trad_m, tshift, ntiles, keys, act, cnt);
-        else
-            dir16_count<2 * kLocTP>(nt.tdir, tfirst, keys, act, cnt);
-    }
-    HSC_STAMP(work, 0, 3);
     const uint64_t *first = kTrad ? tfirst : wt.sp_w;  // first code of every tile
+    LocDefer<K> dfr;
 #pragma unroll
-    for (int j = 0; j < kLocTP; ++j) {
-        if (!valid[j]) continue;
-        const uint32_t q = qq[j];
-        const uint32_t ca = cnt[2 * j], cb = cnt[2 * j + 1];
-        const uint32_t a = ca ? ca - 1 : 0;
-        const uint32_t bt = cb ? cb - 1 : 0;
-        uint4 r0 = make_uint4(kNoTile32, 0, 0, 0), r1 = r0;
-        bool hit = false;
-        if (cb > 0 && a <= bt && lo[j] <= hi[j]) {
-            if (bt > a + 1 && tiles_max(wt, a + 1, bt - 1) > snap[j]) {
-                hit = true;
-            } else {
+    for (int k = 0; k < K; ++k) dfr.x[k] = 1, dfr.y[k] = 0;
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int cb = s & 1;
+        // 1. the previous sub-chunk's whole-tile checks: their loads are
+        //    younger than this sub-chunk's probe loads, which are needed now
+        if (s > 0) loc_defer_run<K>(wt, p, dfr, verdict);
+        // 2. the next sub-chunk's probe loads stay in flight through step 3
+        if (s + 1 < S) load(s + 1, cb ^ 1);
+        // 3. locate this sub-chunk from registers and LDS
+        uint64_t lo[K], hi[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            locate_codes<W>(nv, p, valid[cb][k] ? qq[cb][k] : 0, gg[cb][k], xl[cb][k], xh[cb][k],
+                            lo[k], hi[k]);
+        // Snapshot ranks r(S): O(1) when the window spans < 2^32 of log, else
+        // #commits <= S through the commit directory; a run of equal
+        // snapshots in neighbouring lanes (a read set's ranges) has one head,
+        // the wave packs its heads into a list and searches each once.
+        uint32_t rs[K];
+        if (nt.rank_lsn32) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) rs[k] = lsn32_rank(snap[cb][k], nt.rank_base);
+        } else {
+            const uint64_t le_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+            bool head[K];
+            uint32_t slot[K];
+            uint32_t H = 0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint64_t prev = __shfl_up(snap[cb][k], 1, 64);
+                head[k] = lane == 0 || prev != snap[cb][k];
+                const uint64_t m = __ballot(head[k]);
+                slot[k] = H + __popcll(m & le_mask) - 1;  // this lane's head
+                H += __popcll(m);
+            }
+            for (uint32_t b0 = 0; b0 < H; b0 += 64) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (head[k] && slot[k] - b0 < 64) sb[slot[k] - b0] = snap[cb][k];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const bool act[1] = {lane < H - b0};
+                const uint64_t xs[1] = {act[0] ? dir_le(sb[lane]) : 0};
+                uint32_t r[1];
+                dir16_count<1>(nt.cdir, cdir, xs, act, r);
+                rb[lane] = r[0];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (slot[k] - b0 < 64) rs[k] = rb[slot[k] - b0];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
+        // end tiles: a = #first < lo - 1 (the tile holding the first row >=
+        // lo), bt = #first <= hi - 1 (the tile holding the last row <= hi)
+        uint32_t cnt[2 * K];
+        {
+            uint64_t keys[2 * K];
+            bool act[2 * K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                keys[2 * k] = lo[k];
+                keys[2 * k + 1] = dir_le(hi[k]);
+                act[2 * k] = act[2 * k + 1] = valid[cb][k] && lo[k] <= hi[k];
+            }
+            if constexpr (kTrad)
+                trad_count<2 * K>(tfirst, T, nt.trad_m, tshift, ntiles, keys, act, cnt);
+            else
+                dir16_count<2 * K>(nt.tdir, tfirst, keys, act, cnt);
+        }
+        // records of the partly covered end tiles; the fully covered tiles
+        // between them (and fully covered end tiles) become one deferred
+        // range-maximum check [x, y]
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            dfr.x[k] = 1, dfr.y[k] = 0;
+            if (!valid[cb][k]) continue;
+            const uint32_t q = qq[cb][k];
+            const uint32_t ca = cnt[2 * k], cbt = cnt[2 * k + 1];
+            const uint32_t a = ca ? ca - 1 : 0;
+            const uint32_t bt = cbt ? cbt - 1 : 0;
+            uint4 r0 = make_uint4(kNoTile32, 0, 0, 0), r1 = r0;
+            if (cbt > 0 && a <= bt && lo[k] <= hi[k]) {
                 // tile-relative bounds
                 const uint64_t fa = first[a], fb = first[bt];
-                const uint64_t lo_a = lo[j] <= fa ? 0 : lo[j] - fa;  // > 2^32-1: none
-                const uint64_t hi_a = a == bt ? (hi[j] < fa ? ~0ull : hi[j] - fa) : 0xFFFFFFFFull;
-                const uint64_t hi_b = hi[j] < fb ? ~0ull : hi[j] - fb;
+                const uint64_t lo_a = lo[k] <= fa ? 0 : lo[k] - fa;  // > 2^32-1: none
+                const uint64_t hi_a = a == bt ? (hi[k] < fa ? ~0ull : hi[k] - fa) : 0xFFFFFFFFull;
+                const uint64_t hi_b = hi[k] < fb ? ~0ull : hi[k] - fb;
                 const bool full_a = lo_a == 0 && (a < bt || hi_a >= 0xFFFFFFFFull);
                 const bool use_a = lo_a <= 0xFFFFFFFFull && hi_a != ~0ull && lo_a <= hi_a;
                 const bool use_b = a < bt && hi_b != ~0ull;
                 const bool full_b = hi_b >= 0xFFFFFFFFull;
-                if (use_a && full_a) hit |= tiles_max(wt, a, a) > snap[j];
-                if (use_b && full_b) hit |= tiles_max(wt, bt, bt) > snap[j];
+                dfr.x[k] = use_a && full_a ? a : a + 1;
+                dfr.y[k] = a == bt ? (use_a && full_a ? a : 0) : (use_b && full_b ? bt : bt - 1);
+                if (a == bt && !(use_a && full_a)) dfr.x[k] = 1, dfr.y[k] = 0;
+                dfr.q[k] = q;
+                dfr.snap[k] = snap[cb][k];
                 if (use_a && !full_a)
                     r0 = make_uint4(a << 12 | atomicAdd(&hist[a], 1u), (uint32_t)lo_a,
-                                    (uint32_t)min(hi_a, 0xFFFFFFFFull), rs[j]);
+                                    (uint32_t)min(hi_a, 0xFFFFFFFFull), rs[k]);
                 if (use_b && !full_b) {
                     const uint4 rb2 = make_uint4(bt << 12 | atomicAdd(&hist[bt], 1u), 0,
-                                                 (uint32_t)hi_b, rs[j]);
+                                                 (uint32_t)hi_b, rs[k]);
                     if (r0.x == kNoTile32) {
                         r0 = rb2;
                     } else {
@@ -901,24 +950,24 @@ __global__ __launch_bounds__(kLocTThreads) void k_locate_t(NarrowView nv, WinVie
                     }
                 }
             }
+            if (r0.x & kHasSecond) nt.code2[q] = r1;
+            nt.code[q] = r0;
         }
-        if (hit) verdict[p.txn[q]] = 1;
-        if (r0.x & kHasSecond) nt.code2[q] = r1;
-        nt.code[q] = r0;
     }
-    HSC_STAMP(work, 0, 4);
+    loc_defer_run<K>(wt, p, dfr, verdict);
+    HSC_STAMP(work, 0, 2);
     // table locks: any write to a locked table after the snapshot
     for (uint32_t q = g * kLocTThreads + threadIdx.x; q < p.n_lock; q += work.G * kLocTThreads) {
         const uint32_t t = p.lock_table[q];
         if (t < wt.ntables && wt.table_max[t] > p.lock_snap[q]) verdict[p.lock_txn[q]] = 1;
     }
     __syncthreads();
-    HSC_STAMP(work, 0, 5);
+    HSC_STAMP(work, 0, 3);
     // column g of the tile-major histogram (neighbouring chunks of a line are
     // written from the same XCD)
     const uint32_t hs = hist_stride(work.G);
     for (uint32_t i = threadIdx.x; i < ntiles; i += kLocTThreads) work.hist[(size_t)i * hs + g] = hist[i];
-    HSC_STAMP(work, 0, 6);
+    HSC_STAMP(work, 0, 4);
 }
 
 hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeView &p,
@@ -952,112 +1001,84 @@ hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeV
 uint32_t narrow_tiles_chunk() { return kLocTP * kLocTThreads; }
 uint32_t narrow_tiles_dir_lds() { return kDirLds; }
 
-// ---- plan: column scans + tile plan in one launch ----
+// ---- plan: column scans; fixed-capacity tile buckets ----
+// Tile t's bucket is recs[t * kTileCap, (t + 1) * kTileCap): a record's place
+// is its chunk's offset inside the tile (the exclusive scan of the tile's
+// histogram column over chunks) + its in-chunk rank, so no scan over tiles
+// (and no last-block tail) is needed.  Records past kTileCap of a tile spill
+// to the overflow area after the buckets: the tile's wave reserves a run
+// there with one atomic and appends join items for it (hot tiles only).
 // Wave w of block b scans tile 8 b + w: its column hist[t][0 .. G) (lane l
 // owns entries 8 l .. 8 l + 7, two 16-byte loads; G <= kMaxChunks = 512)
-// becomes exclusive chunk offsets inside the tile's bucket.  Column totals go
-// to counts[] through returning atomics, which are performed at the memory
-// side, so the last block to arrive reads every total back with atomics -- no
-// L2 write-back or invalidate (an agent-scope fence per block costs an L2
-// walk each).  That block scans the totals, one lane per tile so every load
-// and store coalesces, into bucket offsets and join items, and resets the
-// arrival counter.
+// becomes exclusive chunk offsets inside the tile; counts[t] = its records.
+// ctl[0] (overflow records) and ctl[1] (extra join items) were zeroed by
+// this batch's locate.
 constexpr int kPlanThreads = 512;
 static_assert(kMaxChunks <= 512, "one 512-entry column pass per wave");
 __global__ __launch_bounds__(kPlanThreads) void k_plan_t(ProbeWork work, uint32_t ntiles,
-                                                         uint32_t *done)
+                                                         uint32_t *ctl)
 {
-    __shared__ uint64_t lds64[16];
-    __shared__ bool last;
     const int lane = threadIdx.x & 63;
     const uint32_t t = blockIdx.x * (kPlanThreads / 64) + (threadIdx.x >> 6);
     const uint32_t hs = hist_stride(work.G);
-    if (t < ntiles) {
-        u32x4 *col = (u32x4 *)(work.hist + (size_t)t * hs);
-        const uint32_t e = 8 * lane;
-        u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
-        if (e < hs) {
-            a = col[e / 4];
-            b = col[e / 4 + 1];
-        }
-        // entries past G are never written: mask them
-        const uint32_t v[8] = {e + 0 < work.G ? a.x : 0, e + 1 < work.G ? a.y : 0,
-                               e + 2 < work.G ? a.z : 0, e + 3 < work.G ? a.w : 0,
-                               e + 4 < work.G ? b.x : 0, e + 5 < work.G ? b.y : 0,
-                               e + 6 < work.G ? b.z : 0, e + 7 < work.G ? b.w : 0};
-        uint32_t sum = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) sum += v[k];
-        uint32_t x = sum;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(x, o, 64);
-            if (lane >= o) x += y;
-        }
-        uint32_t run = x - sum;
-        if (e < hs) {
-            u32x4 oa, ob;
-            oa.x = run; run += v[0];
-            oa.y = run; run += v[1];
-            oa.z = run; run += v[2];
-            oa.w = run; run += v[3];
-            ob.x = run; run += v[4];
-            ob.y = run; run += v[5];
-            ob.z = run; run += v[6];
-            ob.w = run;
-            col[e / 4] = oa;
-            col[e / 4 + 1] = ob;
-        }
-        if (lane == 63) (void)atomicExch(&work.counts[t], x);
+    if (t >= ntiles) return;
+    u32x4 *col = (u32x4 *)(work.hist + (size_t)t * hs);
+    const uint32_t e = 8 * lane;
+    u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
+    if (e < hs) {
+        a = col[e / 4];
+        b = col[e / 4 + 1];
     }
-    __syncthreads();  // every wave's atomics have returned
-    if (threadIdx.x == 0) last = atomicAdd(done, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    // every tile total in flight at once (kHistCap / kPlanThreads per thread)
-    constexpr int kRounds = kHistCap / kPlanThreads;
-    uint32_t cvs[kRounds];
+    // entries past G are never written: mask them
+    const uint32_t v[8] = {e + 0 < work.G ? a.x : 0, e + 1 < work.G ? a.y : 0,
+                           e + 2 < work.G ? a.z : 0, e + 3 < work.G ? a.w : 0,
+                           e + 4 < work.G ? b.x : 0, e + 5 < work.G ? b.y : 0,
+                           e + 6 < work.G ? b.z : 0, e + 7 < work.G ? b.w : 0};
+    uint32_t sum = 0;
 #pragma unroll
-    for (int k = 0; k < kRounds; ++k) {
-        const uint32_t tt = k * kPlanThreads + threadIdx.x;
-        cvs[k] = tt < ntiles ? atomicAdd(&work.counts[tt], 0u) : 0;
+    for (int k = 0; k < 8; ++k) sum += v[k];
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
     }
-    uint32_t carry_b = 0, carry_i = 0;
-#pragma unroll
-    for (int k = 0; k < kRounds; ++k) {
-        if (k * kPlanThreads >= ntiles) break;
-        const uint32_t tt = k * kPlanThreads + threadIdx.x;
-        const uint32_t cv = cvs[k];
-        const uint32_t ch = (cv + kJoinChunk - 1) / kJoinChunk;  // chunks of the tile
-        const uint32_t xch = ch ? ch - 1 : 0;                      // beyond its own item
-        // records (low 32 bits) and extra items (high 32 bits) in one scan
-        uint64_t tot;
-        const uint64_t pre = block_excl_scan64<kPlanThreads>(cv | (uint64_t)xch << 32, lds64, tot);
-        const uint32_t pb = (uint32_t)pre + carry_b, pi = (uint32_t)(pre >> 32) + carry_i;
-        if (tt < ntiles) {
-            work.bucket_off[tt] = pb;
-            work.item_off[tt] = pi;
-            for (uint32_t j = 1; j < ch; ++j) {  // chunk 0 is item tt itself
-                const uint32_t r0 = pb + j * kJoinChunk;
-                work.item_desc[ntiles + pi + j - 1] =
-                    make_uint4(tt, r0, min(r0 + kJoinChunk, pb + cv), 0);
-            }
+    uint32_t run = x - sum;
+    if (e < hs) {
+        u32x4 oa, ob;
+        oa.x = run; run += v[0];
+        oa.y = run; run += v[1];
+        oa.z = run; run += v[2];
+        oa.w = run; run += v[3];
+        ob.x = run; run += v[4];
+        ob.y = run; run += v[5];
+        ob.z = run; run += v[6];
+        ob.w = run;
+        col[e / 4] = oa;
+        col[e / 4 + 1] = ob;
+    }
+    const uint32_t total = __shfl(x, 63, 64);
+    if (lane == 0) {
+        work.counts[t] = total;
+        if (total > kTileCap) {  // hot tile: overflow run + one join item per kTileCap records
+            const uint32_t over = total - kTileCap;
+            const uint32_t base = atomicAdd(&ctl[0], over);
+            work.bucket_off[t] = base;
+            const uint32_t nx = (over + kJoinChunk - 1) / kJoinChunk;
+            const uint32_t ib = atomicAdd(&ctl[1], nx);
+            const uint32_t o0 = ntiles * kTileCap + base;
+            for (uint32_t j = 0; j < nx; ++j)
+                work.item_desc[ib + j] = make_uint4(t, o0 + j * kJoinChunk,
+                                                    o0 + min((j + 1) * kJoinChunk, over), 0);
         }
-        carry_b += (uint32_t)tot;
-        carry_i += (uint32_t)(tot >> 32);
-    }
-    if (threadIdx.x == 0) {
-        work.bucket_off[ntiles] = carry_b;
-        work.item_off[ntiles] = ntiles + carry_i;  // items: one per tile + the extra chunks
-        *done = 0;
     }
 }
 
-hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *done, hipStream_t s)
+hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, hipStream_t s)
 {
     if (ntiles == 0) return hipSuccess;
     constexpr uint32_t per = kPlanThreads / 64;
-    k_plan_t<<<(ntiles + per - 1) / per, kPlanThreads, 0, s>>>(work, ntiles, done);
+    k_plan_t<<<(ntiles + per - 1) / per, kPlanThreads, 0, s>>>(work, ntiles, ctl);
     return hipGetLastError();
 }
 
@@ -1066,6 +1087,13 @@ hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *done,
 // that every XCD takes a contiguous run of chunks.  A bucket holds its records
 // in chunk order, so the neighbouring records of a bucket come from one XCD
 // and their partial-line writes merge in that XCD's L2.
+__device__ __forceinline__ uint32_t bucket_slot(const ProbeWork &work, uint32_t ntiles, uint32_t t,
+                                                uint32_t pos)
+{
+    return pos < kTileCap ? t * kTileCap + pos
+                          : ntiles * kTileCap + work.bucket_off[t] + (pos - kTileCap);
+}
+
 __global__ __launch_bounds__(256) void k_scatter_t(ProbeView p, ProbeWork work, NarrowTiles nt,
                                                    uint32_t ntiles, uint32_t per_xcd)
 {
@@ -1078,11 +1106,11 @@ __global__ __launch_bounds__(256) void k_scatter_t(ProbeView p, ProbeWork work, 
     const uint32_t *col = work.hist + q / work.chunk;  // hist[t * hs + chunk]
     const size_t hs = hist_stride(work.G);
     const uint32_t ta = (a.x & ~kHasSecond) >> 12;
-    nt.recs[work.bucket_off[ta] + col[ta * hs] + (a.x & 0xFFFu)] = make_uint4(a.y, a.z, a.w, txn);
+    nt.recs[bucket_slot(work, ntiles, ta, col[ta * hs] + (a.x & 0xFFFu))] = make_uint4(a.y, a.z, a.w, txn);
     if (a.x & kHasSecond) {
         const uint4 c = nt.code2[q];
         const uint32_t tb = c.x >> 12;
-        nt.recs[work.bucket_off[tb] + col[tb * hs] + (c.x & 0xFFFu)] = make_uint4(c.y, c.z, c.w, txn);
+        nt.recs[bucket_slot(work, ntiles, tb, col[tb * hs] + (c.x & 0xFFFu))] = make_uint4(c.y, c.z, c.w, txn);
     }
 }
 
@@ -1167,9 +1195,9 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
     uint32_t tile, r0, r1;
     if (item < ntiles) {
         tile = item;
-    } else {
-        if (item >= work.item_off[ntiles]) return;
-        const uint4 d = work.item_desc[item];
+    } else {  // a further kJoinChunk records of a hot tile's overflow run
+        if (item - ntiles >= work.item_off[1]) return;
+        const uint4 d = work.item_desc[item - ntiles];
         tile = d.x, r0 = d.y, r1 = d.z;
     }
     u32x4 rk[RQ], rr[RQ], rec[kRec];
@@ -1180,9 +1208,9 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
         rk[v] = *(const u32x4 *)(nt.key32 + row);
         rr[v] = *(const u32x4 *)(nt.rank32 + row);
     }
-    if (item < ntiles) {
-        r0 = work.bucket_off[tile];
-        r1 = min(r0 + kJoinChunk, work.bucket_off[tile + 1]);
+    if (item < ntiles) {  // the tile's bucket
+        r0 = tile * kTileCap;
+        r1 = r0 + min(kTileCap, work.counts[tile]);
     }
     if (r0 >= r1) return;  // a tile no range reaches
 #pragma unroll

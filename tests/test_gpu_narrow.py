@@ -180,3 +180,19 @@ def test_multi_file_window_commit_ranks(validator, oracle_mod):
     log, rs = keyed_case(16, 4000, 6, key, rng_range, 900, step=1 << 28, snap_recent=0.05)
     assert int(log.lsn[-1] >> 32) - int(log.lsn[0] >> 32) > 100
     both_layouts(validator, oracle_mod, log, rs, LAYOUT_NARROW)
+
+
+def test_hot_tile_bucket_overflow(validator, oracle_mod):
+    """Most ranges of a dense batch land in one 4096-row tile: its fixed
+    bucket (1024 records) spills into the overflow area, which the join
+    covers with extra items (hsc_narrow.hip k_plan_t)."""
+    key = lambda rng: F.enc_int64(int(rng.integers(0, 1 << 24)))
+
+    def rng_range(rng):
+        if rng.random() < 0.8:  # a narrow hot band: a handful of tiles
+            a = int(rng.integers(1 << 23, (1 << 23) + (1 << 12)))
+        else:
+            a = int(rng.integers(0, 1 << 24))
+        return Range("t1", 0, F.enc_int64(a), F.enc_int64(a + int(rng.integers(0, 64))))
+    log, rs = keyed_case(17, 8000, 8, key, rng_range, 4000, ranges_per_txn=8, snap_recent=0.02)
+    both_layouts(validator, oracle_mod, log, rs, LAYOUT_NARROW)
