@@ -405,19 +405,35 @@ __host__ __device__ inline uint32_t dir16_lds_entries(const Dir16 &d);
 __global__ __launch_bounds__(kRankThreads) void k_rank32(const uint64_t *lsn, uint32_t n,
                                                          uint32_t len, Dir16 d, uint32_t *rank);
 
-// key32 = key64 - first key64 of the tile; flag := 1 if a tile spans >= 2^32
+// Eytzinger (BFS) slot of sorted row r of a 4096-row tile: rows 0 .. 4094
+// form a perfect binary tree at slots 1 .. 4095 (in-order index i = r + 1 sits
+// at level 11 - ctz(i)), row 4095 at slot 0.  A root-to-leaf walk touches
+// slots spread over a level instead of the power-of-two strides of a binary
+// search over sorted rows, which all fall in one or two LDS banks.
+static_assert(kTLog2 == 12, "eyt12 assumes 4096-row tiles");
+__device__ __forceinline__ uint32_t eyt12(uint32_t r)
+{
+    const uint32_t i = r + 1;
+    const int tz = __builtin_ctz(i);
+    return i == 4096 ? 0 : (1u << (11 - tz)) + (i >> (tz + 1));
+}
+
+// key32 = key64 - first key64 of the tile, stored in the tile's Eytzinger
+// order (the join copies a tile's keys into LDS as they lie); flag := 1 if a
+// tile spans >= 2^32
 __global__ void k_key32(const uint64_t *key64, uint32_t n, uint32_t len, uint32_t *key32,
                         uint32_t *flag)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= len) return;
+    const uint32_t dst = (i & ~((1u << kTLog2) - 1)) + eyt12(i & ((1u << kTLog2) - 1));
     if (i >= n) {
-        key32[i] = 0xFFFFFFFFu;
+        key32[dst] = 0xFFFFFFFFu;
         return;
     }
     const uint64_t d = key64[i] - key64[(size_t)(i >> kTLog2) << kTLog2];
     if (d > 0xFFFFFFFFull) atomicOr(flag, 1u);
-    key32[i] = (uint32_t)d;
+    key32[dst] = (uint32_t)d;
 }
 
 // lsn32 mode: rank32 = lsn - base + 1 (pads 0)
@@ -1083,10 +1099,13 @@ hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, 
 }
 
 // ---- scatter: 16-byte records into tile buckets ----
-// Block b runs on XCD b % 8 (round-robin dispatch); blocks are renumbered so
-// that every XCD takes a contiguous run of chunks.  A bucket holds its records
-// in chunk order, so the neighbouring records of a bucket come from one XCD
-// and their partial-line writes merge in that XCD's L2.
+// One block per locate chunk (XCD-contiguous chunk order, as the locate): the
+// chunk's offsets inside every tile bucket (its column of the scanned
+// histogram) are staged in LDS once, so a record's place costs an LDS read;
+// the record and read-set loads of all the chunk's probes are issued before
+// that staging completes.  A bucket holds its records in chunk order, so the
+// neighbouring records of a bucket come from one XCD and their partial-line
+// writes merge in that XCD's L2.
 __device__ __forceinline__ uint32_t bucket_slot(const ProbeWork &work, uint32_t ntiles, uint32_t t,
                                                 uint32_t pos)
 {
@@ -1094,23 +1113,39 @@ __device__ __forceinline__ uint32_t bucket_slot(const ProbeWork &work, uint32_t 
                           : ntiles * kTileCap + work.bucket_off[t] + (pos - kTileCap);
 }
 
-__global__ __launch_bounds__(256) void k_scatter_t(ProbeView p, ProbeWork work, NarrowTiles nt,
-                                                   uint32_t ntiles, uint32_t per_xcd)
+constexpr int kScatThreads = kLocTThreads;
+__global__ __launch_bounds__(kScatThreads) void k_scatter_t(ProbeView p, ProbeWork work,
+                                                             NarrowTiles nt, uint32_t ntiles)
 {
-    const uint32_t b = (blockIdx.x & 7) * per_xcd + (blockIdx.x >> 3);
-    const uint32_t q = b * 256 + threadIdx.x;
-    if (q >= p.n) return;
-    const uint4 a = nt.code[q];
-    if (a.x == kNoTile32) return;
-    const uint32_t txn = p.txn[q];
-    const uint32_t *col = work.hist + q / work.chunk;  // hist[t * hs + chunk]
+    extern __shared__ uint32_t soff[];  // [ntiles] this chunk's offset in each bucket
+    const uint32_t g = xcd_chunk(blockIdx.x, (work.G + 7) / 8);
+    if (g >= work.G) return;
+    constexpr int P = kLocTP;
+    const uint32_t c0 = g * work.chunk, c1 = min(p.n, c0 + work.chunk);
+    uint4 a[P];
+    uint32_t txn[P];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const uint32_t q = c0 + threadIdx.x + kScatThreads * j;
+        a[j] = q < c1 ? nt.code[q] : make_uint4(kNoTile32, 0, 0, 0);
+        txn[j] = q < c1 ? p.txn[q] : 0;
+    }
     const size_t hs = hist_stride(work.G);
-    const uint32_t ta = (a.x & ~kHasSecond) >> 12;
-    nt.recs[bucket_slot(work, ntiles, ta, col[ta * hs] + (a.x & 0xFFFu))] = make_uint4(a.y, a.z, a.w, txn);
-    if (a.x & kHasSecond) {
-        const uint4 c = nt.code2[q];
-        const uint32_t tb = c.x >> 12;
-        nt.recs[bucket_slot(work, ntiles, tb, col[tb * hs] + (c.x & 0xFFFu))] = make_uint4(c.y, c.z, c.w, txn);
+    for (uint32_t t = threadIdx.x; t < ntiles; t += kScatThreads) soff[t] = work.hist[t * hs + g];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        if (a[j].x == kNoTile32) continue;
+        const uint32_t q = c0 + threadIdx.x + kScatThreads * j;
+        const uint32_t ta = (a[j].x & ~kHasSecond) >> 12;
+        nt.recs[bucket_slot(work, ntiles, ta, soff[ta] + (a[j].x & 0xFFFu))] =
+            make_uint4(a[j].y, a[j].z, a[j].w, txn[j]);
+        if (a[j].x & kHasSecond) {
+            const uint4 c = nt.code2[q];
+            const uint32_t tb = c.x >> 12;
+            nt.recs[bucket_slot(work, ntiles, tb, soff[tb] + (c.x & 0xFFFu))] =
+                make_uint4(c.y, c.z, c.w, txn[j]);
+        }
     }
 }
 
@@ -1118,28 +1153,15 @@ hipError_t launch_scatter_t(const ProbeView &p, const ProbeWork &work, const Nar
                             uint32_t ntiles, hipStream_t s)
 {
     if (p.n == 0) return hipSuccess;
-    const uint32_t nb = (p.n + 255) / 256, per_xcd = (nb + 7) / 8;
-    k_scatter_t<<<8 * per_xcd, 256, 0, s>>>(p, work, nt, ntiles, per_xcd);
+    k_scatter_t<<<8 * ((work.G + 7) / 8), kScatThreads, 4 * (size_t)ntiles, s>>>(p, work, nt, ntiles);
     return hipGetLastError();
 }
 
 // ---- join: 8-byte rows ----
 // Row quad v of thread t = rows 4 (t + kJoinThreads v) .. + 3: one 16-byte
-// load of keys and one of ranks per quad; 16-row maxima over 4 lanes,
-// 128-row maxima over 32 lanes.
-//
-// Eytzinger (BFS) slot of sorted row r of a 4096-row tile: rows 0 .. 4094
-// form a perfect binary tree at slots 1 .. 4095 (in-order index i = r + 1 sits
-// at level 11 - ctz(i)), row 4095 at slot 0.  A root-to-leaf walk touches
-// slots spread over a level instead of the power-of-two strides of a binary
-// search over sorted rows, which all fall in one or two LDS banks.
-static_assert(kTLog2 == 12, "eyt12 assumes 4096-row tiles");
-__device__ __forceinline__ uint32_t eyt12(uint32_t r)
-{
-    const uint32_t i = r + 1;
-    const int tz = __builtin_ctz(i);
-    return i == 4096 ? 0 : (1u << (11 - tz)) + (i >> (tz + 1));
-}
+// load of keys (already in Eytzinger order, k_key32) and one of ranks per
+// quad, stored to LDS as they are; 16-row maxima over 4 lanes, 128-row maxima
+// over 32 lanes.
 
 template <int N>
 __device__ __forceinline__ bool any_gt32(const uint32_t *a, uint32_t from, uint32_t to, uint32_t s)
@@ -1174,10 +1196,10 @@ __device__ __forceinline__ bool any_after32(const uint32_t *rank, const uint32_t
     return r;
 }
 
-// One workgroup per join item.  Item t < ntiles is the first kJoinChunk
-// records of tile t (its range comes from bucket_off, so the tile's rows are
-// requested before anything else is known); items >= ntiles are the further
-// chunks of heavy tiles, described in item_desc.
+// One workgroup per tile: its bucket (at most kTileCap records; the tile's
+// rows are requested before anything else is known); blocks past the tiles
+// loop over the further kJoinChunk-record chunks of hot tiles' overflow runs
+// (item_desc).
 __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowTiles nt,
                                                          uint32_t n, uint32_t ntiles,
                                                          uint8_t *verdict)
@@ -1190,14 +1212,17 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
     __shared__ uint32_t b16[T / 16];
     __shared__ uint32_t b128[T / 128];
 
-    const uint32_t item = blockIdx.x;
     HSC_STAMP(work, 1, 0);
+    // blocks past the tiles take the hot tiles' overflow items in turn
+    const uint32_t nextra = blockIdx.x < ntiles ? 1 : work.item_off[1];
+    const uint32_t stride = gridDim.x > ntiles ? gridDim.x - ntiles : 1;  // >= 1: every loop ends
+    for (uint32_t xi = blockIdx.x < ntiles ? 0 : blockIdx.x - ntiles; xi < nextra; xi += stride) {
+    __syncthreads();  // the previous item's LDS reads are done
     uint32_t tile, r0, r1;
-    if (item < ntiles) {
-        tile = item;
+    if (blockIdx.x < ntiles) {
+        tile = blockIdx.x;
     } else {  // a further kJoinChunk records of a hot tile's overflow run
-        if (item - ntiles >= work.item_off[1]) return;
-        const uint4 d = work.item_desc[item - ntiles];
+        const uint4 d = work.item_desc[xi];
         tile = d.x, r0 = d.y, r1 = d.z;
     }
     u32x4 rk[RQ], rr[RQ], rec[kRec];
@@ -1208,21 +1233,18 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
         rk[v] = *(const u32x4 *)(nt.key32 + row);
         rr[v] = *(const u32x4 *)(nt.rank32 + row);
     }
-    if (item < ntiles) {  // the tile's bucket
+    if (blockIdx.x < ntiles) {  // the tile's bucket
         r0 = tile * kTileCap;
         r1 = r0 + min(kTileCap, work.counts[tile]);
     }
-    if (r0 >= r1) return;  // a tile no range reaches
+    if (r0 >= r1) continue;  // a tile no range reaches (uniform across the block)
 #pragma unroll
     for (int k = 0; k < kRec; ++k)
         rec[k] = *(const u32x4 *)(nt.recs + min(r0 + k * kJoinThreads + threadIdx.x, r1 - 1));
 #pragma unroll
     for (int v = 0; v < RQ; ++v) {
         const uint32_t quad = threadIdx.x + kJoinThreads * v;
-        keys[eyt12(4 * quad)] = rk[v].x;
-        keys[eyt12(4 * quad + 1)] = rk[v].y;
-        keys[eyt12(4 * quad + 2)] = rk[v].z;
-        keys[eyt12(4 * quad + 3)] = rk[v].w;
+        ((u32x4 *)keys)[quad] = rk[v];  // already in Eytzinger order (k_key32)
         ((u32x4 *)rank)[quad] = rr[v];
         uint32_t m = max(max(rr[v].x, rr[v].y), max(rr[v].z, rr[v].w));
         m = max(m, (uint32_t)__shfl_xor((int)m, 1, 64));
@@ -1255,14 +1277,19 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
         const uint32_t pb = min(jb - T + (kl <= hi), tn);
         if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) verdict[rec[k].w] = 1;
     }
+    }
     HSC_STAMP(work, 1, 2);
 }
 
 hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t n,
                          uint32_t ntiles, uint32_t max_items, uint8_t *verdict, hipStream_t s)
 {
-    if (max_items == 0 || n == 0) return hipSuccess;
-    k_join_t<<<max_items, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
+    if (max_items == 0 || n == 0 || ntiles == 0) return hipSuccess;
+    // one block per tile + up to 512 blocks looping over the overflow items
+    // (measured: one block per tile beats persistent blocks that prefetch
+    // their next tile -- 27.8 vs 32 us on config 2)
+    const uint32_t blocks = ntiles + std::min<uint32_t>(max_items - ntiles, 512);
+    k_join_t<<<blocks, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
     return hipGetLastError();
 }
 
