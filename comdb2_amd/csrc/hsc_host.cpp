@@ -134,8 +134,36 @@ struct hsc_ctx {
     uint64_t end_lsn = 0, max_commit = 0;
     uint64_t poison_regop = 0;  // max regop LSN whose prev record cannot be read
     uint64_t poison_chain = 0;  // max commit LSN whose logical chain is broken
-    std::vector<uint64_t> record_lsns;  // all record LSNs when ingested from a log
+    // the log a log-based window was decoded from (record LSNs for the
+    // DB_SET rule, records for chain walks of txns committed by appends);
+    // table = window table id
+    struct LogStore {
+        std::vector<uint64_t> lsn, prev, key_off;
+        std::vector<uint32_t> rectype;
+        std::vector<int16_t> isabort, ix;
+        std::vector<int32_t> table, keylen;
+        std::vector<uint8_t> keys;
+        void clear()
+        {
+            lsn.clear(), prev.clear(), key_off.clear(), rectype.clear(), isabort.clear();
+            ix.clear(), table.clear(), keylen.clear(), keys.clear();
+        }
+    } lg;
+    bool lg_rule = false;  // every record LSN of the window is in lg (DB_SET rule on)
     uint64_t last_append_lsn = 0;
+    // incremental window (hsc_delta.hip): writes committed after the last
+    // build, kept on the device as a sorted delta run probed beside the main
+    // window; live = a built window takes appends into the delta
+    bool live = false, merge_pending = false;
+    DBuf d_dgid[2], d_dwords[2], d_dlsn[2], d_dbmax, d_agid, d_awords, d_alsn;
+    size_t dn = 0, dcap = 0;
+    int dcur = 0;
+    std::vector<uint32_t> app_gid;   // appended rows not yet on the device
+    std::vector<uint8_t> app_keys;   // their key bytes (klen of the group each)
+    std::vector<uint64_t> app_koff, app_lsn;
+    bool app_tmax = false;           // table maxima changed since the last upload
+    HBuf h_app;                      // pinned staging of appended rows / table maxima
+    ProbeView raw_probe{};           // the batch being probed, untransformed (delta probe)
 
     // device window
     int W = 1;
@@ -340,25 +368,42 @@ static void clear_window(hsc_ctx *c)
     std::fill(c->h_table_max.begin(), c->h_table_max.end(), 0);
     c->max_commit = 0;
     c->poison_regop = c->poison_chain = 0;
-    c->record_lsns.clear();
+    c->lg.clear();
+    c->lg_rule = false;
     c->last_append_lsn = 0;
     c->host_staged = true;
     c->dirty = true;
+    c->live = false;
+    c->merge_pending = false;
+    c->dn = 0;
+    c->app_gid.clear(), c->app_keys.clear(), c->app_koff.clear(), c->app_lsn.clear();
+    c->app_tmax = false;
     c->n = 0;
 }
 
 static void add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keylen, bool has_key,
                       uint64_t lsn)
 {
-    if (lsn > c->h_table_max[tid]) c->h_table_max[tid] = lsn;
+    if (lsn > c->h_table_max[tid]) {
+        c->h_table_max[tid] = lsn;
+        c->app_tmax = true;
+    }
     if (lsn > c->max_commit) c->max_commit = lsn;
     if (!has_key) return;
     if (keylen < 0) keylen = 0;
     int g = group_id_or_add(c, tid, ix, keylen);
-    c->h_gid.push_back((uint32_t)g);
-    c->h_keyoff.push_back(c->h_keys.size());
-    c->h_keys.insert(c->h_keys.end(), key, key + keylen);
-    c->h_lsn.push_back(lsn);
+    if (c->host_staged) {
+        c->h_gid.push_back((uint32_t)g);
+        c->h_keyoff.push_back(c->h_keys.size());
+        c->h_keys.insert(c->h_keys.end(), key, key + keylen);
+        c->h_lsn.push_back(lsn);
+    }
+    if (c->live) {  // a built window: the row goes to the device delta run
+        c->app_gid.push_back((uint32_t)g);
+        c->app_koff.push_back(c->app_keys.size());
+        c->app_keys.insert(c->app_keys.end(), key, key + keylen);
+        c->app_lsn.push_back(lsn);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -714,6 +759,11 @@ static int device_build(hsc_ctx *c, size_t n_in)
         for (int t = 0; t < nt; ++t) c->h_table_max[t] = std::max(c->h_table_max[t], tm[t]);
     }
     c->dirty = false;
+    c->live = true;
+    c->merge_pending = false;
+    c->dn = 0;  // every appended row is in the rebuilt window
+    c->app_gid.clear(), c->app_keys.clear(), c->app_koff.clear(), c->app_lsn.clear();
+    c->app_tmax = false;
     return HSC_OK;
 }
 
@@ -744,6 +794,181 @@ static int build_from_host(hsc_ctx *c)
     return device_build(c, n_in);
 }
 
+// Appended rows (app_*) as a sorted SoA (gid, W words, lsn) in pinned
+// staging: returns the row count.
+static int stage_appends(hsc_ctx *c, int W, size_t *k_out)
+{
+    const size_t k = c->app_gid.size();
+    *k_out = k;
+    if (!k) return HSC_OK;
+    std::vector<uint64_t> rw(k * (size_t)W);
+    std::vector<uint32_t> ord(k);
+    uint8_t buf[kMaxWords * 8];
+    for (size_t i = 0; i < k; ++i) {
+        const int klen = c->groups[c->app_gid[i]].klen;
+        memset(buf, 0, (size_t)W * 8);
+        if (klen) memcpy(buf, c->app_keys.data() + c->app_koff[i], (size_t)klen);
+        for (int j = 0; j < W; ++j) rw[i * W + j] = load_be64(buf + 8 * j);
+        ord[i] = (uint32_t)i;
+    }
+    std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) {
+        if (c->app_gid[a] != c->app_gid[b]) return c->app_gid[a] < c->app_gid[b];
+        for (int j = 0; j < W; ++j)
+            if (rw[a * W + j] != rw[b * W + j]) return rw[a * W + j] < rw[b * W + j];
+        return false;
+    });
+    if (c->h_app.ensure(k * (4 + 8 * (size_t)W + 8) + 16, true))
+        return fail(c, HSC_ENOMEM, "append staging");
+    uint32_t *g = c->h_app.as<uint32_t>();
+    uint64_t *wd = (uint64_t *)(c->h_app.as<uint8_t>() + ((4 * k + 15) & ~(size_t)15));
+    uint64_t *ls = wd + (size_t)W * k;
+    for (size_t i = 0; i < k; ++i) {
+        const uint32_t r = ord[i];
+        g[i] = c->app_gid[r];
+        for (int j = 0; j < W; ++j) wd[(size_t)j * k + i] = rw[(size_t)r * W + j];
+        ls[i] = c->app_lsn[r];
+    }
+    return HSC_OK;
+}
+
+static DeltaView delta_view(const hsc_ctx *c)
+{
+    DeltaView d{};
+    d.gid = c->d_dgid[c->dcur].as<uint32_t>();
+    d.words = c->d_dwords[c->dcur].as<uint64_t>();
+    d.lsn = c->d_dlsn[c->dcur].as<uint64_t>();
+    d.bmax = c->d_dbmax.as<uint64_t>();
+    d.stride = c->dcap;
+    d.n = (uint32_t)c->dn;
+    d.W = c->W;
+    return d;
+}
+
+// Appends since the last call into the device delta run (one merge launch,
+// asynchronous on c->stream) and the table maxima into d_table_max.  A delta
+// past kDeltaCap, or a key longer than the window's words, schedules a merge
+// into the main window instead (at the next check).
+static int flush_appends(hsc_ctx *c)
+{
+    if (!c->live || c->host_only) return HSC_OK;
+    hipStream_t s = c->stream;
+    const size_t k = c->app_gid.size();
+    if (k && (window_words(c) > c->W || c->dn + k > kDeltaCap || c->merge_pending)) {
+        c->merge_pending = true;
+        c->dirty = true;  // rows stay in app_* for merge_delta (or in h_* for a host rebuild)
+        return HSC_OK;
+    }
+    if (!k && !c->app_tmax) return HSC_OK;
+    HIPCHK(c, wait_lanes(c));  // probes in flight on other streams keep reading the old run
+    if (c->app_tmax) {
+        const int nt = (int)c->table_names.size();
+        HIPCHK(c, c->d_table_max.ensure(8 * (size_t)std::max(nt, 1)));
+        if (c->h_app.ensure(8 * (size_t)std::max(nt, 1), true)) return fail(c, HSC_ENOMEM, "staging");
+        memcpy(c->h_app.p, c->h_table_max.data(), 8 * (size_t)nt);
+        if (nt) HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, c->h_app.p, 8 * (size_t)nt, hipMemcpyHostToDevice, s));
+        // the next staging must not overwrite h_app before the copy ran
+        HIPCHK(c, hipStreamSynchronize(s));
+        c->app_tmax = false;
+    }
+    if (!k) return HSC_OK;
+    const int W = c->W;
+    size_t kk = 0;
+    HIPCHK_RC(c, stage_appends(c, W, &kk));
+    HIPCHK(c, c->d_agid.ensure(4 * k));
+    HIPCHK(c, c->d_awords.ensure(8 * (size_t)W * k));
+    HIPCHK(c, c->d_alsn.ensure(8 * k));
+    const uint8_t *hb = c->h_app.as<uint8_t>();
+    const size_t woff = (4 * k + 15) & ~(size_t)15;
+    HIPCHK(c, hipMemcpyAsync(c->d_agid.p, hb, 4 * k, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_awords.p, hb + woff, 8 * (size_t)W * k, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_alsn.p, hb + woff + 8 * (size_t)W * k, 8 * k, hipMemcpyHostToDevice, s));
+    // both run buffers at full size for the window's words: merges never
+    // reallocate a run holding rows (a wider key schedules a rebuild above)
+    const size_t wbytes = 8 * (size_t)W * kDeltaCap;
+    if (c->dcap < kDeltaCap || c->d_dwords[0].bytes < wbytes || c->d_dwords[1].bytes < wbytes) {
+        if (c->dn) return fail(c, HSC_EINVAL, "delta run resized while holding rows");
+        c->dcap = kDeltaCap;
+        for (int b = 0; b < 2; ++b) {
+            HIPCHK(c, c->d_dgid[b].ensure(4 * (size_t)kDeltaCap));
+            HIPCHK(c, c->d_dwords[b].ensure(wbytes));
+            HIPCHK(c, c->d_dlsn[b].ensure(8 * (size_t)kDeltaCap));
+        }
+        HIPCHK(c, c->d_dbmax.ensure(8 * (size_t)(kDeltaCap / 64 + 1)));
+    }
+    DeltaView a{};
+    a.gid = c->d_agid.as<uint32_t>();
+    a.words = c->d_awords.as<uint64_t>();
+    a.lsn = c->d_alsn.as<uint64_t>();
+    a.stride = k;
+    a.n = (uint32_t)k;
+    a.W = W;
+    const DeltaView d = delta_view(c);
+    const int o = c->dcur ^ 1;
+    HIPCHK(c, delta_merge(d, a, c->d_dgid[o].as<uint32_t>(), c->d_dwords[o].as<uint64_t>(),
+                          c->d_dlsn[o].as<uint64_t>(), c->dcap, c->d_dbmax.as<uint64_t>(), s));
+    // h_app is read by the copies above: finish them before the next staging
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->dcur = o;
+    c->dn += k;
+    c->app_gid.clear(), c->app_keys.clear(), c->app_koff.clear(), c->app_lsn.clear();
+    return HSC_OK;
+}
+
+// Fold the delta run (and rows appended since) into the main window of a
+// device-ingested window: every version of the last build (key-sorted, in
+// d_*2), the delta rows and the pending rows, widened to the current key
+// words, become the input of one device rebuild.
+static int merge_delta(hsc_ctx *c)
+{
+    hipStream_t s = c->stream;
+    HIPCHK(c, wait_lanes(c));
+    const int W0 = c->W, W = std::max(c->W, window_words(c));
+    size_t k = 0;
+    HIPCHK_RC(c, stage_appends(c, W, &k));
+    const size_t na = c->n_all, nd = c->dn, n_in = na + nd + k;
+    if (n_in >= 0xFFFFFFFFull) return fail(c, HSC_EINVAL, "window too large");
+    const size_t cap = window_cap(n_in);
+    DBuf g, wd, l;
+    HIPCHK(c, g.ensure(4 * cap));
+    HIPCHK(c, wd.ensure(8 * (size_t)W * cap));
+    HIPCHK(c, l.ensure(8 * cap));
+    if (W > W0) HIPCHK(c, hipMemsetAsync(wd.p, 0, 8 * (size_t)W * cap, s));
+    if (na) {
+        HIPCHK(c, hipMemcpyAsync(g.p, c->d_gid2.p, 4 * na, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(l.p, c->d_lsn2.p, 8 * na, hipMemcpyDeviceToDevice, s));
+        for (int j = 0; j < W0; ++j)
+            HIPCHK(c, hipMemcpyAsync(wd.as<uint64_t>() + (size_t)j * cap,
+                                     c->d_words2.as<uint64_t>() + (size_t)j * c->cap, 8 * na,
+                                     hipMemcpyDeviceToDevice, s));
+    }
+    if (nd) {
+        const DeltaView d = delta_view(c);
+        HIPCHK(c, hipMemcpyAsync(g.as<uint32_t>() + na, d.gid, 4 * nd, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(l.as<uint64_t>() + na, d.lsn, 8 * nd, hipMemcpyDeviceToDevice, s));
+        for (int j = 0; j < W0; ++j)
+            HIPCHK(c, hipMemcpyAsync(wd.as<uint64_t>() + (size_t)j * cap + na, d.words + (size_t)j * d.stride,
+                                     8 * nd, hipMemcpyDeviceToDevice, s));
+    }
+    if (k) {
+        const uint8_t *hb = c->h_app.as<uint8_t>();
+        const size_t woff = (4 * k + 15) & ~(size_t)15;
+        HIPCHK(c, hipMemcpyAsync(g.as<uint32_t>() + na + nd, hb, 4 * k, hipMemcpyHostToDevice, s));
+        for (int j = 0; j < W; ++j)
+            HIPCHK(c, hipMemcpyAsync(wd.as<uint64_t>() + (size_t)j * cap + na + nd,
+                                     hb + woff + 8 * (size_t)j * k, 8 * k, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(l.as<uint64_t>() + na + nd, hb + woff + 8 * (size_t)W * k, 8 * k,
+                                 hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(c, hipStreamSynchronize(s));  // the staging and the old rows are consumed
+    std::swap(c->d_gid, g);
+    std::swap(c->d_words, wd);
+    std::swap(c->d_lsn, l);
+    g.release(), wd.release(), l.release();
+    c->W = W;
+    c->cap = cap;
+    return device_build(c, n_in);
+}
+
 static int ensure_built(hsc_ctx *c)
 {
     if (c->host_only) {  // dictionaries + marshalling only
@@ -751,59 +976,92 @@ static int ensure_built(hsc_ctx *c)
         return HSC_OK;
     }
     if (!c->dirty) return HSC_OK;
-    if (!c->host_staged) return fail(c, HSC_ESTATE, "device window must be re-ingested");
-    return build_from_host(c);
+    if (c->host_staged) return build_from_host(c);  // staged rows include the appended ones
+    if (c->merge_pending) return merge_delta(c);
+    return fail(c, HSC_ESTATE, "device window must be re-ingested");
 }
 
 // ---------------------------------------------------------------------------
 // log decode (what osql_serial_check + serial_check_this_txn visit)
 // ---------------------------------------------------------------------------
-static long find_lsn(const hsc_llog *log, uint64_t lsn)
-{
-    const uint64_t *b = log->lsn, *e = log->lsn + log->nrec;
-    const uint64_t *p = std::lower_bound(b, e, lsn);
-    return (p != e && *p == lsn) ? (long)(p - b) : -1;
-}
-
 static bool is_regop(uint32_t t)
 {
     return t == HSC_REC_TXN_REGOP || t == HSC_REC_TXN_REGOP_GEN || t == HSC_REC_TXN_REGOP_ROWLOCKS;
 }
 
-static int ingest_log(hsc_ctx *c, const hsc_llog *log)
+// Index of the stored record at lsn, or -1.
+static long lg_find(const hsc_ctx *c, uint64_t lsn)
 {
-    clear_window(c);
-    c->end_lsn = log->end_lsn;
-    c->record_lsns.assign(log->lsn, log->lsn + log->nrec);
-    for (size_t i = 1; i < log->nrec; ++i)
-        if (log->lsn[i] <= log->lsn[i - 1]) return fail(c, HSC_EINVAL, "log LSNs not increasing");
-    std::vector<int> tmap(log->ntbnames, -1);
+    const auto &v = c->lg.lsn;
+    auto p = std::lower_bound(v.begin(), v.end(), lsn);
+    return (p != v.end() && *p == lsn) ? (long)(p - v.begin()) : -1;
+}
+
+// Append log records (the continuation of the window's log: LSNs above every
+// stored one) and take in the writes of every txn they commit -- what
+// osql_serial_check / serial_check_this_txn visit (bdb/serializable.c:426-534,
+// 60-332): a regop whose prev record is an ltran_commit with isabort == 0 and
+// prevllsn.file != 0 commits the logical chain walked back from prevllsn to
+// ltran_start.  Chains may reach into records of earlier appends.  On an
+// unreadable record the reference's scan errors out (nonzero): poison LSNs.
+static int append_log(hsc_ctx *c, const hsc_llog *log)
+{
+    const uint64_t last = c->lg.lsn.empty() ? 0 : c->lg.lsn.back();
+    for (size_t i = 0; i < log->nrec; ++i)
+        if ((i ? log->lsn[i] <= log->lsn[i - 1] : (!c->lg.lsn.empty() && log->lsn[0] <= last)))
+            return fail(c, HSC_EINVAL, "log LSNs not increasing");
+    if (log->end_lsn < (log->nrec ? log->lsn[log->nrec - 1] : last))
+        return fail(c, HSC_EINVAL, "end LSN before the last record");
+    std::vector<int> tmap(std::max(log->ntbnames, 0), -1);
     auto tid_of = [&](int32_t t) -> int {
         if (t < 0 || t >= log->ntbnames) return -1;
         if (tmap[t] < 0) tmap[t] = table_id_or_add(c, log->tbnames[t]);
         return tmap[t];
     };
+    // store the new records
+    auto &L = c->lg;
+    const size_t r0 = L.lsn.size();
     for (size_t i = 0; i < log->nrec; ++i) {
-        if (!is_regop(log->rectype[i])) continue;
-        const uint64_t c_lsn = log->lsn[i];
-        long p = find_lsn(log, log->prev[i]);
+        const uint32_t t = log->rectype[i];
+        L.lsn.push_back(log->lsn[i]);
+        L.rectype.push_back(t);
+        L.prev.push_back(log->prev[i]);
+        L.isabort.push_back(log->isabort[i]);
+        const bool undo = t >= HSC_REC_UNDO_ADD_DTA && t != HSC_REC_LTRAN_COMMIT &&
+                          t != HSC_REC_LTRAN_START && t != HSC_REC_LTRAN_COMPREC;
+        L.table.push_back(undo ? tid_of(log->table[i]) : -1);
+        L.ix.push_back(log->ix[i]);
+        const int32_t kl = log->keylen[i];
+        const bool has_key = t == HSC_REC_UNDO_ADD_IX || t == HSC_REC_UNDO_DEL_IX ||
+                             t == HSC_REC_UNDO_DEL_IX_LK || t == HSC_REC_UNDO_UPD_IX ||
+                             t == HSC_REC_UNDO_ADD_IX_LK || t == HSC_REC_UNDO_UPD_IX_LK;
+        L.key_off.push_back(L.keys.size());
+        L.keylen.push_back(has_key ? kl : 0);
+        if (has_key && kl > 0) L.keys.insert(L.keys.end(), log->keys + log->key_off[i],
+                                             log->keys + log->key_off[i] + kl);
+    }
+    c->end_lsn = log->end_lsn;
+    // take in the txns the new regops commit
+    for (size_t i = r0; i < L.lsn.size(); ++i) {
+        if (!is_regop(L.rectype[i])) continue;
+        const uint64_t c_lsn = L.lsn[i];
+        long p = lg_find(c, L.prev[i]);
         if (p < 0) {  // prevcur->get fails -> the scan errors out (nonzero)
             c->poison_regop = std::max(c->poison_regop, c_lsn);
             continue;
         }
-        if (log->rectype[p] != HSC_REC_LTRAN_COMMIT) continue;
-        if ((uint32_t)(log->prev[p] >> 32) == 0) continue;  // not a write txn
-        if (log->isabort[p]) continue;
+        if (L.rectype[p] != HSC_REC_LTRAN_COMMIT) continue;
+        if ((uint32_t)(L.prev[p] >> 32) == 0) continue;  // not a write txn
+        if (L.isabort[p]) continue;
         // committed write txn: walk prevllsn back to ltran_start
         if (c_lsn > c->max_commit) c->max_commit = c_lsn;
-        uint64_t lsn = log->prev[p];
-        long r = find_lsn(log, lsn);
+        long r = lg_find(c, L.prev[p]);
         if (r < 0) {
             c->poison_chain = std::max(c->poison_chain, c_lsn);
             continue;
         }
         for (;;) {
-            const uint32_t t = log->rectype[r];
+            const uint32_t t = L.rectype[r];
             if (t == HSC_REC_LTRAN_START) break;
             switch (t) {
             case HSC_REC_UNDO_ADD_DTA:
@@ -811,41 +1069,44 @@ static int ingest_log(hsc_ctx *c, const hsc_llog *log)
             case HSC_REC_UNDO_UPD_DTA:
             case HSC_REC_UNDO_ADD_DTA_LK:
             case HSC_REC_UNDO_DEL_DTA_LK:
-            case HSC_REC_UNDO_UPD_DTA_LK: {
-                int tid = tid_of(log->table[r]);
-                if (tid < 0) return fail(c, HSC_ELOG, "bad table index in log");
-                add_write(c, tid, -2, nullptr, 0, false, c_lsn);
+            case HSC_REC_UNDO_UPD_DTA_LK:
+                if (L.table[r] < 0) return fail(c, HSC_ELOG, "bad table index in log");
+                add_write(c, L.table[r], -2, nullptr, 0, false, c_lsn);
                 break;
-            }
             case HSC_REC_UNDO_ADD_IX:
             case HSC_REC_UNDO_DEL_IX:
             case HSC_REC_UNDO_DEL_IX_LK:
             case HSC_REC_UNDO_UPD_IX:
             case HSC_REC_UNDO_ADD_IX_LK:
-            case HSC_REC_UNDO_UPD_IX_LK: {
-                int tid = tid_of(log->table[r]);
-                if (tid < 0) return fail(c, HSC_ELOG, "bad table index in log");
-                add_write(c, tid, (int)log->ix[r], log->keys + log->key_off[r], log->keylen[r],
+            case HSC_REC_UNDO_UPD_IX_LK:
+                if (L.table[r] < 0) return fail(c, HSC_ELOG, "bad table index in log");
+                add_write(c, L.table[r], (int)L.ix[r], L.keys.data() + L.key_off[r], L.keylen[r],
                           true, c_lsn);
                 break;
-            }
             case HSC_REC_LTRAN_COMMIT:
             case HSC_REC_LTRAN_COMPREC:
                 break;
             default:  // the reference abort()s (bdb/serializable.c:283-286)
                 return fail(c, HSC_ELOG, "unknown record type in logical chain");
             }
-            lsn = log->prev[r];
+            const uint64_t lsn = L.prev[r];
             if ((uint32_t)(lsn >> 32) == 0) break;
-            r = find_lsn(log, lsn);
+            r = lg_find(c, lsn);
             if (r < 0) {
                 c->poison_chain = std::max(c->poison_chain, c_lsn);
                 break;
             }
         }
     }
-    c->dirty = true;
+    if (!c->live) c->dirty = true;
     return HSC_OK;
+}
+
+static int ingest_log(hsc_ctx *c, const hsc_llog *log)
+{
+    clear_window(c);
+    c->lg_rule = true;  // every record of the window is in the store
+    return append_log(c, log);
 }
 
 // ---------------------------------------------------------------------------
@@ -881,8 +1142,7 @@ static void norm_bound(const uint8_t *key, int keylen, int flag, int klen, bool 
 static int full_forced(const hsc_ctx *c, uint64_t S)
 {
     if (S >= c->end_lsn) return 0;  // DB_SET at/after the end -> DB_NOTFOUND -> 0
-    if (!c->record_lsns.empty() &&
-        !std::binary_search(c->record_lsns.begin(), c->record_lsns.end(), S))
+    if (c->lg_rule && !std::binary_search(c->lg.lsn.begin(), c->lg.lsn.end(), S))
         return 1;                    // DB_SET inside the log on a non-record -> error
     if (c->poison_regop > S || c->poison_chain > S) return 1;
     return -1;
@@ -891,9 +1151,7 @@ static int full_forced(const hsc_ctx *c, uint64_t S)
 static int regop_rc(hsc_ctx *c, uint64_t S)
 {
     if (S >= c->end_lsn) return 0;
-    if (!c->record_lsns.empty() &&
-        !std::binary_search(c->record_lsns.begin(), c->record_lsns.end(), S))
-        return 1;
+    if (c->lg_rule && !std::binary_search(c->lg.lsn.begin(), c->lg.lsn.end(), S)) return 1;
     return (c->max_commit > S || c->poison_regop > S) ? 1 : 0;
 }
 
@@ -1228,6 +1486,8 @@ static WinView win_view(hsc_ctx *c)
     return w;
 }
 
+static int probe_delta(hsc_ctx *c, uint8_t *target);
+
 // Narrow layout: one kernel answers every range and table lock.
 static int probe_narrow(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w,
                         const ProbeView &p)
@@ -1246,6 +1506,7 @@ static int probe_narrow(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w,
     if (tm)
         for (int i = 1; i <= 3; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
     HIPCHK(c, launch_probe_narrow(nv, p, b->verdict, s));
+    HIPCHK_RC(c, probe_delta(c, b->verdict));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
     HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
@@ -1337,6 +1598,7 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     } else if (tm) {
         for (int i = 2; i <= 4; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
     }
+    HIPCHK_RC(c, probe_delta(c, flags));
     HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
 #ifdef HSC_STAMPS
@@ -1397,6 +1659,15 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
     return rc;
 }
 
+// Range probes of the batch against the delta run (appends since the last
+// build) into the path's verdict target, before its pack.
+static int probe_delta(hsc_ctx *c, uint8_t *target)
+{
+    if (!c->dn || !c->raw_probe.n) return HSC_OK;
+    HIPCHK(c, launch_probe_delta(delta_view(c), c->raw_probe, target, c->stream));
+    return HSC_OK;
+}
+
 static int probe_lane(hsc_ctx *c, const hsc_probe_batch *b)
 {
     const WinView w = win_view(c);
@@ -1413,6 +1684,8 @@ static int probe_lane(hsc_ctx *c, const hsc_probe_batch *b)
     p.lock_txn = b->lock_txn;
     p.n = w.n ? (uint32_t)b->n : 0;  // empty key window: no range can match
     p.n_lock = (uint32_t)b->n_lock;
+    c->raw_probe = p;
+    c->raw_probe.n = (uint32_t)b->n;  // the delta may hold keys of an empty main window
     if (!c->narrow && c->compact) {
         // wide keys as compact codes: map the bounds, then the tile pipeline
         const int WC = c->ct.WC;
@@ -1523,6 +1796,7 @@ static int probe_tiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w, c
         HIPCHK(c, hipEventRecord(c->ev[3], s));
         HIPCHK(c, hipEventRecord(c->ev[4], s));
     }
+    HIPCHK_RC(c, probe_delta(c, b->verdict));
     HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
     return HSC_OK;
@@ -1716,6 +1990,10 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->w_tcode2, &c->w_trecs};
     for (DBuf *b : bufs) b->release();
     for (Stage &st : c->stage) st.release();
+    for (DBuf *b : {&c->d_dgid[0], &c->d_dgid[1], &c->d_dwords[0], &c->d_dwords[1], &c->d_dlsn[0],
+                    &c->d_dlsn[1], &c->d_dbmax, &c->d_agid, &c->d_awords, &c->d_alsn})
+        b->release();
+    c->h_app.release();
     for (DBuf &b : c->co_dev) b.release();
     for (DBuf *b : {&c->e_span, &c->e_cnt, &c->e_txn, &c->e_lsn, &c->e_txn2, &c->e_lsn2, &c->e_gid,
                     &c->e_scratch, &c->e_flags, &c->e_after})
@@ -1764,18 +2042,48 @@ int hsc_window_append(hsc_ctx *c, const hsc_write *w, size_t n)
 {
     if (!c || (!w && n)) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    if (!c->host_staged) return fail(c, HSC_ESTATE, "append after device ingest");
+    if (!c->host_only) (void)hipSetDevice(c->device);
     for (size_t i = 0; i < n; ++i) {
         if (!w[i].tbname) return fail(c, HSC_EINVAL, "write without table");
         if (w[i].commit_lsn < c->last_append_lsn) return fail(c, HSC_EINVAL, "commit LSNs must not decrease");
+        if (w[i].key && (w[i].keylen < 0 || w[i].keylen > kMaxWords * 8))
+            return fail(c, HSC_EINVAL, "key longer than MAXKEYLEN");
+    }
+    // decoded writes carry no record LSNs: the window no longer knows every
+    // record, so the DB_SET-on-a-non-record rule is off from here on
+    c->lg_rule = false;
+    for (size_t i = 0; i < n; ++i) {
         c->last_append_lsn = w[i].commit_lsn;
         int tid = table_id_or_add(c, w[i].tbname);
         add_write(c, tid, w[i].idxnum, (const uint8_t *)w[i].key, w[i].keylen, w[i].key != nullptr,
                   w[i].commit_lsn);
     }
-    c->dirty = true;
-    return HSC_OK;
+    if (!c->live) {
+        c->dirty = true;
+        return HSC_OK;
+    }
+    return flush_appends(c);
 }
+
+int hsc_window_append_log(hsc_ctx *c, const hsc_llog *log)
+{
+    if (!c || !log) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->host_only) (void)hipSetDevice(c->device);
+    int rc = append_log(c, log);
+    if (rc) return rc;
+    return c->live ? flush_appends(c) : HSC_OK;
+}
+
+int hsc_window_append_raw(hsc_ctx *c, const hsc_raw_log *raw)
+{
+    const hsc_llog *lg = nullptr;
+    int rc = hsc_decode_log(c, raw, &lg);
+    if (rc) return rc;
+    return hsc_window_append_log(c, lg);
+}
+
+size_t hsc_window_delta_rows(hsc_ctx *c) { return c ? c->dn : 0; }
 
 int hsc_window_set_end(hsc_ctx *c, uint64_t end_lsn)
 {
@@ -1972,6 +2280,10 @@ int hsc_rw_edges(hsc_ctx *c, const hsc_readsets *rs, size_t *n_pairs, const uint
     if (c->host_only) return HSC_EDEVICE;
     std::lock_guard<std::mutex> g(c->mu);
     (void)hipSetDevice(c->device);
+    if (c->dn || !c->app_gid.empty()) {  // pairs need every version: fold the delta in first
+        c->merge_pending = true;
+        c->dirty = true;
+    }
     int rc = ensure_built(c);
     if (!rc) rc = marshal_readsets(c, rs);
     if (rc) return rc;

@@ -272,6 +272,25 @@ hipError_t launch_edge_emit(const EdgeView &w, const ProbeView &p, const uint2 *
                             const uint32_t *off, uint32_t *out_txn, uint64_t *out_lsn,
                             hipStream_t s);
 
+// Incremental window (hsc_delta.hip): rows appended after a build, sorted by
+// (gid, words), W words of stride `stride`; bmax = per-64-row LSN maxima.
+struct DeltaView {
+    const uint32_t *gid;
+    const uint64_t *words;  // [W][stride]
+    const uint64_t *lsn;
+    const uint64_t *bmax;   // [ceil(n / 64)]
+    size_t stride;
+    uint32_t n;
+    int W;
+};
+constexpr uint32_t kDeltaCap = 1u << 16;  // delta rows before a merge into the main window
+// out (stride ostride) = merge of d and the sorted rows a; bmax of the result
+hipError_t delta_merge(const DeltaView &d, const DeltaView &a, uint32_t *ogid, uint64_t *owords,
+                       uint64_t *olsn, size_t ostride, uint64_t *bmax, hipStream_t s);
+// flags[txn] = 1 for every range probe with a delta row of its group in
+// [lo, hi] committed after its snapshot (raw W-word bounds)
+hipError_t launch_probe_delta(const DeltaView &d, const ProbeView &p, uint8_t *flags, hipStream_t s);
+
 // Replicant coalesce (hsc_coalesce.hip): flat read sets in, per-set surviving
 // rows (ord) + the four fields merge_neighbor rewrites (w_*) out.
 struct CoView {

@@ -190,8 +190,10 @@ class LogBuilder:
             ix: int = 0, key: Optional[bytes] = None) -> int:
         return self._put(rectype, prev, isabort, table, ix, key)
 
-    def build(self) -> LLog:
-        r = self.rows
+    def build(self, start: int = 0) -> LLog:
+        """The log (records [start:] of it: the continuation of a log built
+        earlier -- key offsets still index the whole key blob)."""
+        r = self.rows[start:]
         cols = list(zip(*r)) if r else [()] * 8
         lg = LLog(
             lsn=np.array(cols[0], dtype=np.uint64),

@@ -71,6 +71,12 @@ class _ReadSets(C.Structure):
                 ("keys", _p), ("tbnames", C.POINTER(C.c_char_p)), ("ntbnames", C.c_int)]
 
 
+class _Write(C.Structure):
+    """hsc_write: one decoded committed write."""
+    _fields_ = [("tbname", C.c_char_p), ("idxnum", C.c_int), ("key", _p), ("keylen", C.c_int),
+                ("commit_lsn", C.c_uint64)]
+
+
 class ProbeBatch(C.Structure):
     """hsc_probe_batch: device pointers (ints) of a resident probe batch."""
     _fields_ = [("n", C.c_size_t), ("lo", _p), ("hi", _p), ("gid", _p), ("snap", _p),
@@ -123,7 +129,8 @@ EXPORTS = [
     "hsc_enable_timing", "hsc_dep_graph_scc", "hsc_dep_graph_edges",
     "hsc_window_ingest_raw", "hsc_decode_log", "hsc_decode_serial", "hsc_check_serial",
     "hsc_set_layout", "hsc_window_layout", "hsc_coalesce_readsets", "hsc_rw_edges",
-    "hsc_window_code_words", "hsc_set_threads", "hsc_currangearrs_build",
+    "hsc_window_code_words", "hsc_window_append_log", "hsc_window_append_raw",
+    "hsc_window_delta_rows", "hsc_set_threads", "hsc_currangearrs_build",
     "hsc_currangearrs_free", "hsc_dep_graph_build", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
 ]
 
@@ -194,6 +201,9 @@ def load() -> C.CDLL:
         "hsc_check_serial": (C.c_int, [_p, C.POINTER(_SerialMsgs), C.POINTER(C.c_int)]),
         "hsc_set_layout": (C.c_int, [_p, C.c_int]),
         "hsc_set_threads": (C.c_int, [_p, C.c_int]),
+        "hsc_window_append_log": (C.c_int, [_p, C.POINTER(_LLog)]),
+        "hsc_window_append_raw": (C.c_int, [_p, C.POINTER(_RawLog)]),
+        "hsc_window_delta_rows": (C.c_size_t, [_p]),
         "hsc_currangearrs_build": (C.c_int, [C.POINTER(_ReadSets), C.POINTER(C.POINTER(_p))]),
         "hsc_currangearrs_free": (None, [C.POINTER(_p), C.c_int]),
         "hsc_window_layout": (C.c_int, [_p]),
@@ -378,6 +388,44 @@ class Validator:
     def ingest_log(self, log: LLog) -> None:
         s, keep = llog_struct(log)
         self._chk(self.lib.hsc_window_ingest_log(self.ctx, C.byref(s)), "hsc_window_ingest_log")
+
+    def append_log(self, log: LLog) -> None:
+        """Append the continuation of the window's log (hsc_window_append_log)."""
+        s, keep = llog_struct(log)
+        self._chk(self.lib.hsc_window_append_log(self.ctx, C.byref(s)), "hsc_window_append_log")
+
+    def append_raw(self, raw) -> None:
+        """Append raw log records (hsc_window_append_raw)."""
+        s, keep = rawlog_struct(raw)
+        self._chk(self.lib.hsc_window_append_raw(self.ctx, C.byref(s)), "hsc_window_append_raw")
+
+    def append_writes(self, writes, end_lsn: Optional[int] = None) -> None:
+        """hsc_window_append of decoded writes [(tbname, idxnum, key or None,
+        commit_lsn)], then hsc_window_set_end(end_lsn) if given."""
+        n = len(writes)
+        arr = (_Write * max(1, n))()
+        keep = []
+        for i, (tb, ix, key, lsn_) in enumerate(writes):
+            nm = C.create_string_buffer(tb.encode())
+            keep.append(nm)
+            arr[i].tbname = C.cast(nm, C.c_char_p)
+            arr[i].idxnum = ix
+            if key is None:
+                arr[i].key = None
+                arr[i].keylen = 0
+            else:
+                kb = C.create_string_buffer(bytes(key), max(1, len(key)))
+                keep.append(kb)
+                arr[i].key = C.cast(kb, _p)
+                arr[i].keylen = len(key)
+            arr[i].commit_lsn = int(lsn_)
+        self._chk(self.lib.hsc_window_append(self.ctx, arr, n), "hsc_window_append")
+        if end_lsn is not None:
+            self._chk(self.lib.hsc_window_set_end(self.ctx, int(end_lsn)), "hsc_window_set_end")
+
+    @property
+    def delta_rows(self) -> int:
+        return self.lib.hsc_window_delta_rows(self.ctx)
 
     def ingest_raw(self, raw) -> None:
         """Decode a raw log stream (formats.RawLog) and ingest it."""

@@ -188,6 +188,45 @@ def replay(events: Sequence[Tuple[str, Txn]], check: Callable[[LLog, ReadSets], 
     return rcs
 
 
+def replay_incremental(events: Sequence[Tuple[str, Txn]], v, tbnames: Sequence[str] = (),
+                       mode: str = "log", on_check=None) -> dict:
+    """The commit stream of :func:`replay` against one validator whose window
+    is kept up to date incrementally: an empty log is ingested once, then
+    every passing write txn's records are appended -- as the continuation of
+    the log (``mode="log"``: hsc_window_append_log, the chains decoded on the
+    device side's host decoder) or as decoded writes (``mode="writes"``:
+    hsc_window_append + hsc_window_set_end).  Each check is the drop-in entry
+    bdb_osql_serial_check on a CurRangeArr.  Returns {txn name: rc}."""
+    from .hsc import CurRangeArrays, bdb_osql_serial_check
+    lb = LogBuilder(tbnames)
+    v.ingest_log(lb.build())
+    snaps, rcs = {}, {}
+    for ev, t in events:
+        if ev == "begin":
+            snaps[t.name] = lb.next_lsn()
+            continue
+        if not t.writes:
+            continue
+        arrs = CurRangeArrays([t.reads], [snaps[t.name]])
+        if on_check:
+            on_check()
+        rc = int(bdb_osql_serial_check(v, arrs.arrs[0]))
+        rcs[t.name] = rc
+        if rc == 0:
+            start = len(lb.rows)
+            lb.begin(t.name)
+            for rt, tb, ix, key in t.writes:
+                lb.write(t.name, rt, tb, ix, key)
+            c_lsn = lb.commit(t.name)
+            if mode == "log":
+                v.append_log(lb.build(start))
+            else:
+                v.append_writes([(tb, ix if key is not None else -2,
+                                  None if rt in F.DTA_TYPES else key, c_lsn)
+                                 for rt, tb, ix, key in t.writes], end_lsn=lb.next_lsn())
+    return rcs
+
+
 def config1_events(seed: int = SEED_CONFIG1, n_txn: int = 10_000, n_ids: int = 20,
                    n_accts: int = 5, concurrency: int = 20) -> List[Tuple[str, Txn]]:
     """tests/tools/serial.c-shaped stream: table "accounts" with unique index 0

@@ -251,8 +251,27 @@ int hsc_window_ingest_raw(hsc_ctx *ctx, const hsc_raw_log *log);
 /* Decode only: *out points at a context-owned hsc_llog valid until the next
  * decode on this context. */
 int hsc_decode_log(hsc_ctx *ctx, const hsc_raw_log *log, const hsc_llog **out);
-/* Append decoded writes (commit_lsn non-decreasing across calls). */
+/* Append decoded writes (commit_lsn non-decreasing across calls).  On a
+ * built window (log, raw, staged or device ingest) the rows go to a sorted
+ * delta run on the device (one merge launch per call; the reference sees
+ * every commit up to the end of the log on every check, bdb/serializable.c:
+ * 390-539, and commits keep appending, bdb/tran.c:1545-1560) that every probe
+ * checks beside the main window; past 65536 delta rows, or on a key longer
+ * than the window's words, the next check folds the delta into the main
+ * window with one device rebuild.  Decoded writes carry no record LSNs, so
+ * after one the DB_SET-on-a-non-record rule (bdb/serializable.c:417-421) is
+ * off for the window.  Call hsc_window_set_end for the new end of the log. */
 int hsc_window_append(hsc_ctx *ctx, const hsc_write *w, size_t n);
+/* Append log records: the continuation of the window's log (LSNs above every
+ * record taken so far; log->end_lsn is the new end).  Every txn a new regop
+ * commits contributes its writes, its logical chain walked back into records
+ * of earlier ingests / appends when it reaches them (SURVEY.md §8(f) 1,
+ * incremental decode); record LSNs, poison rules and the delta run follow. */
+int hsc_window_append_log(hsc_ctx *ctx, const hsc_llog *log);
+/* Raw-record form of hsc_window_append_log (hsc_raw_log as for ingest). */
+int hsc_window_append_raw(hsc_ctx *ctx, const hsc_raw_log *log);
+/* Rows in the delta run (appended since the last build of the main window). */
+size_t hsc_window_delta_rows(hsc_ctx *ctx);
 int hsc_window_set_end(hsc_ctx *ctx, uint64_t end_lsn);
 int hsc_window_reset(hsc_ctx *ctx);
 /* Sort + dedupe + summaries on the device; implied by the check calls. */
