@@ -20,7 +20,9 @@ keys; db/sqlglue.c cursor capture, bdb/ll.c logging):
     a key change logs del_ix(old) + add_ix(new); insert add_dta + add_ix;
     delete del_dta + del_ix;
   * read-only transactions never ship a read set (db/sqloffload.c:280-287).
-Index keys follow db/types.c:766-771 (0x08 + big-endian, sign bit flipped).
+Index keys follow db/types.c:766-771 (0x08 + big-endian, sign bit flipped);
+intervals (s15), datetimes (s7) and decimals (s8) use order-preserving int64
+stand-ins (the check compares key bytes only).
 """
 import json
 import os
@@ -321,6 +323,79 @@ def later_scenarios(uk):
         events=[["begin", "T1a"], ["begin", "T2a"], ["commit", "T1a"], ["commit", "T2a"],
                 ["begin", "T1b"], ["begin", "T2b"], ["commit", "T1b"], ["commit", "T2b"]],
         expect_fail=["T2a", "T2b"])
+    out.update(shows_scenarios())
+    return out
+
+
+def shows_scenarios():
+    """s7 / s8 on shows (shows.csc2: KEY_ID = id, dup KEY_DATE = date
+    (datetime), dup KEY_DEC = dec (decimal128)).  Both run on the 7 rows the
+    s7 setup inserts (s8 runs after s7 in glob order; tables persist).
+    Stand-in key encodings, order-preserving, which is all the byte
+    comparisons of the check see (as for s15's intervals): a datetime is its
+    UTC instant in milliseconds, a decimal its value x 10^4 (every value has at
+    most 4 decimals), both in the A9 int64 format; not comdb2's on-disk
+    datetime / decimal128 formats.  Session time zone America/New_York
+    (comdb2's default) for the literals without one; the UTC offsets of the
+    dates' zones on those days are spelled out below."""
+    import datetime as dt
+
+    def utc_ms(y, mo, d, h, mi, se, off_h):
+        t = dt.datetime(y, mo, d, h, mi, se, tzinfo=dt.timezone(dt.timedelta(hours=off_h)))
+        return int(t.timestamp() * 1000)
+
+    rows = {  # id: (date ms, dec x 1e4) -- s7_01.req, session 1
+        1: (utc_ms(2014, 10, 8, 16, 0, 8, -4), 12131),    # America/New_York, EDT
+        2: (utc_ms(2014, 12, 21, 14, 35, 0, -5), 2149),   # session zone, EST
+        3: (utc_ms(2014, 12, 21, 14, 35, 0, 8), 34320),   # Asia/Shanghai
+        7: (utc_ms(2011, 3, 26, 13, 12, 47, 8), 10000),   # Asia/Hong_Kong
+        12: (utc_ms(2014, 9, 28, 14, 35, 0, -4), 65443),  # America/Toronto, EDT
+        8: (utc_ms(2014, 5, 1, 0, 0, 0, 8), 82443),       # Asia/Taipei
+        10: (utc_ms(2014, 1, 1, 0, 0, 0, -8), 23210),     # US/Pacific, PST
+    }
+
+    def keys(i, genid):
+        d, m = rows[i]
+        return {0: K(i), 1: K(d) + F.enc_genid(genid), 2: K(m) + F.enc_genid(genid)}
+
+    def upd(ids, g):
+        w = []
+        for i in ids:
+            w += upd_same("shows", keys(i, g + i))
+        return w
+
+    late = utc_ms(2014, 10, 8, 17, 0, 0, -4)    # '2014-10-08T17:00:00 America/New_York'
+    early = utc_ms(2014, 1, 1, 0, 0, 0, -5)     # '2014-01-01T00:00:00 America/New_York'
+    after = sorted(i for i in rows if rows[i][0] > late)
+    before = sorted(i for i in rows if rows[i][0] < early)
+    assert after == [2, 3] and before == [7]   # the names s7_01.req.out prints
+    out = {}
+    # s7: T2 reads the late shows and updates the early ones, T3 the other
+    # way round; T2 commits first, so T3's early-date range holds T2's keys
+    out["s7"] = dict(
+        txns={
+            "T2": dict(reads=[rng_("shows", 1, K(late), None, rflag=1),
+                              rng_("shows", 1, None, K(early), lflag=1)], writes=upd(before, 11000)),
+            "T3": dict(reads=[rng_("shows", 1, None, K(early), lflag=1),
+                              rng_("shows", 1, K(late), None, rflag=1)], writes=upd(after, 12000)),
+        },
+        events=[["begin", "T2"], ["begin", "T3"], ["commit", "T2"], ["commit", "T3"]],
+        expect_fail=["T3"])
+    hi_dec, lo_dec = 53210, 21200               # '5.321', '2.1200'
+    big = sorted(i for i in rows if rows[i][1] > hi_dec)
+    small = sorted(i for i in rows if rows[i][1] < lo_dec)
+    assert big == [8, 12] and small == [1, 2, 7]   # s8_01.req.out's names
+    # s8: the same skew over KEY_DEC; T1 commits first, T2's dec > 5.321
+    # range holds the KEY_DEC keys T1 re-logged
+    out["s8"] = dict(
+        txns={
+            "T1": dict(reads=[rng_("shows", 2, K(hi_dec), None, rflag=1),
+                              rng_("shows", 2, None, K(lo_dec), lflag=1)], writes=upd(big, 13000)),
+            "T2": dict(reads=[rng_("shows", 2, None, K(lo_dec), lflag=1),
+                              rng_("shows", 2, K(hi_dec), None, rflag=1)], writes=upd(small, 14000)),
+        },
+        events=[["begin", "T1"], ["begin", "T2"], ["commit", "T1"], ["commit", "T2"]],
+        expect_fail=["T2"])
     return out
 
 
