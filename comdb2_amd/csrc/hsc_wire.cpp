@@ -36,7 +36,7 @@ struct WireReader {
         uint8_t *d = (uint8_t *)dst;
         if (n == 2 || n == 4 || n == 8)
             for (size_t i = 0; i < n; ++i) d[i] = p[n - 1 - i];
-        else
+        else if (n)  // an empty key lands in an empty buffer (dst may be null)
             memcpy(d, p, n);
         p += n;
         return true;

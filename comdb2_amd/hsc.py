@@ -452,7 +452,7 @@ class Validator:
                     prev=arr(L.prev, n, np.uint64), isabort=arr(L.isabort, n, np.int16),
                     table=arr(L.table, n, np.int32), ix=arr(L.ix, n, np.int16), key_off=key_off,
                     keylen=keylen, keys=arr(L.keys, nkeys, np.uint8),
-                    tbnames=[L.tbnames[i].decode() for i in range(L.ntbnames)],
+                    tbnames=[L.tbnames[i].decode("utf-8", "surrogateescape") for i in range(L.ntbnames)],
                     end_lsn=int(L.end_lsn))
 
     def decode_serial(self, msgs) -> ReadSets:
@@ -481,7 +481,7 @@ class Validator:
                      [1]))
         return ReadSets(txn_off=txn_off, snap=arr(R.snap, nt, np.uint64), lkey_off=lo,
                         rkey_off=ro, keys=arr(R.keys, nk, np.uint8),
-                        tbnames=[R.tbnames[i].decode() for i in range(R.ntbnames)], **cols)
+                        tbnames=[R.tbnames[i].decode("utf-8", "surrogateescape") for i in range(R.ntbnames)], **cols)
 
     def check_serial(self, msgs) -> np.ndarray:
         """Decode + full check of OSQL_SERIAL payloads; rc per message."""
