@@ -346,13 +346,40 @@ def api_leg(hsc, v, rs, device_verdict, args):
     for k in range(K):
         v.check_batch(arrs, file=fo[k + 1][0], offset=fo[k + 1][1])
     el = time.perf_counter() - t0
+    # the per-transaction call pattern: C threads each calling the one-set
+    # entry (hsc_collector_check, bdb_osql_serial_check's signature) on their
+    # share of the read sets; the collector batches whatever arrives together
+    conc = {}
+    want = np.asarray(device_verdict) != 0
+    for nth in (64, 256):
+        got, st = v.concurrent_check(arrs, nth)
+        st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want))
+        conc[f"threads_{nth}"] = st
+    m = min(T, 2000)  # uncollected: one device pass per call, a bounded sample
+    sub = hsc.NativeCurRangeArrs(_readsets_head(rs, m))
+    for nth in (1, 64):
+        got, st = v.concurrent_check(sub, nth, collect=False)
+        st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want[:m]))
+        st["sample"] = f"first {m} read sets"
+        conc[f"threads_{nth}_uncollected"] = st
+    sub.close()
     arrs.close()
-    ok = bool(np.array_equal(rc != 0, np.asarray(device_verdict) != 0))
+    ok = bool(np.array_equal(rc != 0, want))
     return {"entry": "hip_serial_check_batch (CurRangeArr* x n, full checks)",
             "value": T * K / el, "unit": "checks/s", "calls": K, "read_sets_per_call": T,
             "ms_per_call": el / K * 1e3, "host_threads": box_cpus()["threads"],
             "parity_with_device_batch": ok,
-            "note": "marshal + pinned upload + probe + download + rc_out, timed over whole calls"}
+            "note": "marshal + pinned upload + probe + download + rc_out, timed over whole calls",
+            "concurrent_callers": conc}
+
+
+def _readsets_head(rs, m):
+    """The first m read sets of rs (same key buffer)."""
+    from comdb2_amd.formats import ReadSets
+    e = int(rs.txn_off[m])
+    return ReadSets(rs.txn_off[:m + 1], rs.snap[:m], rs.table[:e], rs.idxnum[:e],
+                    rs.lflag[:e], rs.rflag[:e], rs.islocked[:e], rs.lkeylen[:e],
+                    rs.rkeylen[:e], rs.lkey_off[:e], rs.rkey_off[:e], rs.keys, rs.tbnames)
 
 
 def box_cpus():

@@ -11,8 +11,12 @@
 // NULL: HSC_KEY_NULL in the flat form).
 #include "../../include/hip_serial.h"
 
+#include <algorithm>
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
+#include <vector>
 
 namespace {
 
@@ -98,6 +102,48 @@ void hsc_currangearrs_free(void **arrs, int n)
     if (!arrs) return;
     for (int t = 0; t < n; ++t) free_arr((hsc_currangearr *)arrs[t]);
     free(arrs);
+}
+
+int hsc_harness_concurrent(hsc_ctx *ctx, hsc_collector *col, void *const *arrs, int n,
+                           int nthreads, int rounds, int regop_only, int *rc_out,
+                           hsc_concurrent_result *res)
+{
+    if (!ctx || n < 0 || (n && (!arrs || !rc_out)) || nthreads < 1 || rounds < 1 || !res)
+        return HSC_EINVAL;
+    using clk = std::chrono::steady_clock;
+    std::vector<std::vector<float>> lat(nthreads);
+    auto body = [&](int t) {
+        for (int r = 0; r < rounds; ++r)
+            for (int i = t; i < n; i += nthreads) {
+                const hsc_currangearr *a = (const hsc_currangearr *)arrs[i];
+                unsigned int file = a ? a->file : 0, offset = a ? a->offset : 0;
+                const auto t0 = clk::now();
+                const int rc = col ? hsc_collector_check(col, arrs[i], &file, &offset, regop_only)
+                                   : hip_bdb_osql_serial_check(ctx, arrs[i], &file, &offset,
+                                                               regop_only);
+                lat[t].push_back(std::chrono::duration<float, std::micro>(clk::now() - t0).count());
+                rc_out[i] = rc;
+            }
+    };
+    const auto w0 = clk::now();
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(body, t);
+    body(0);
+    for (auto &x : th) x.join();
+    res->seconds = std::chrono::duration<double>(clk::now() - w0).count();
+    std::vector<float> all;
+    for (auto &v : lat) all.insert(all.end(), v.begin(), v.end());
+    res->calls = all.size();
+    res->lat_mean_us = res->lat_p50_us = res->lat_p99_us = 0;
+    if (!all.empty()) {
+        double s = 0;
+        for (float x : all) s += x;
+        res->lat_mean_us = s / all.size();
+        std::sort(all.begin(), all.end());
+        res->lat_p50_us = all[all.size() / 2];
+        res->lat_p99_us = all[std::min(all.size() - 1, all.size() * 99 / 100)];
+    }
+    return HSC_OK;
 }
 
 }  // extern "C"

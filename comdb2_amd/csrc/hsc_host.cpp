@@ -86,15 +86,44 @@ struct HBuf {
 
 // One marshalled batch (or pipeline chunk) in host memory: probe SoA,
 // forced verdicts, and the verdict bytes read back.
+// Byte offsets of a marshalled batch's columns inside one staging arena (and
+// the device arena it is uploaded to with ONE copy): a small batch -- the
+// collector's usual tens of read sets -- pays one transfer, not eight.
+struct StageLayout {
+    size_t lo = 0, hi = 0, snap = 0, lock_snap = 0, gid = 0, txn = 0, lock_table = 0,
+           lock_txn = 0, total = 0;
+};
+
+static StageLayout stage_layout(int W, size_t n, size_t nl)
+{
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    StageLayout L;
+    size_t o = 0;
+    L.lo = o, o = al(o + 8 * (size_t)W * n);
+    L.hi = o, o = al(o + 8 * (size_t)W * n);
+    L.snap = o, o = al(o + 8 * n);
+    L.lock_snap = o, o = al(o + 8 * nl);
+    L.gid = o, o = al(o + 4 * n);
+    L.txn = o, o = al(o + 4 * n);
+    L.lock_table = o, o = al(o + 4 * nl);
+    L.lock_txn = o, o = al(o + 4 * nl);
+    L.total = o;
+    return L;
+}
+
 struct Stage {
-    HBuf lo, hi, gid, snap, txn, lock_table, lock_snap, lock_txn, forced, verdict;
+    HBuf arena, forced, verdict;
+    StageLayout L;
     size_t n = 0, n_lock = 0, n_txn = 0;
     hipEvent_t done = nullptr;  // the chunk's verdict download
+    template <class T>
+    T *col(size_t off) const
+    {
+        return (T *)((uint8_t *)arena.p + off);
+    }
     void release()
     {
-        for (HBuf *b : {&lo, &hi, &gid, &snap, &txn, &lock_table, &lock_snap, &lock_txn, &forced,
-                        &verdict})
-            b->release();
+        for (HBuf *b : {&arena, &forced, &verdict}) b->release();
         if (done) (void)hipEventDestroy(done);
         done = nullptr;
     }
@@ -200,6 +229,7 @@ struct hsc_ctx {
 
     // probe workspace
     DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;
+    DBuf p_arena;  // a staged batch's columns, uploaded in one copy (StageLayout)
     DBuf p_verdict, p_bitmap;
     DBuf w_code, w_hist, w_counts, w_bucket, w_cursor, w_items, w_item_tile, w_item_desc, w_recs;
 
@@ -1395,14 +1425,14 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
         nl += c->parts[w].lock_table.size();
     }
     const bool pin = !c->host_only;
-    const size_t n1 = std::max<size_t>(n, 1), l1 = std::max<size_t>(nl, 1);
-    if (st.lo.ensure(8 * (size_t)W * n1, pin) || st.hi.ensure(8 * (size_t)W * n1, pin) ||
-        st.gid.ensure(4 * n1, pin) || st.snap.ensure(8 * n1, pin) || st.txn.ensure(4 * n1, pin) ||
-        st.lock_table.ensure(4 * l1, pin) || st.lock_snap.ensure(8 * l1, pin) ||
-        st.lock_txn.ensure(4 * l1, pin))
+    st.L = stage_layout(W, n, nl);
+    if (st.arena.ensure(std::max<size_t>(st.L.total, 256), pin))
         return fail(c, HSC_ENOMEM, "staging buffers");
-    uint64_t *lo = st.lo.as<uint64_t>(), *hi = st.hi.as<uint64_t>(), *sn = st.snap.as<uint64_t>();
-    uint32_t *gid = st.gid.as<uint32_t>(), *txn = st.txn.as<uint32_t>();
+    uint64_t *lo = st.col<uint64_t>(st.L.lo), *hi = st.col<uint64_t>(st.L.hi);
+    uint64_t *sn = st.col<uint64_t>(st.L.snap);
+    uint32_t *gid = st.col<uint32_t>(st.L.gid), *txn = st.col<uint32_t>(st.L.txn);
+    uint32_t *ltab = st.col<uint32_t>(st.L.lock_table), *ltxn = st.col<uint32_t>(st.L.lock_txn);
+    uint64_t *lsnap = st.col<uint64_t>(st.L.lock_snap);
     par_for(n >= (size_t)kMarshalParallelMin ? c->threads : 1, nwork, [&](int w) {
         const MarshalPart &mp = c->parts[w];
         const size_t o = mp.out0, k = mp.gid.size();
@@ -1418,9 +1448,9 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
         }
         const size_t lo0 = mp.lock0, kl = mp.lock_table.size();
         if (kl) {
-            memcpy(st.lock_table.as<uint32_t>() + lo0, mp.lock_table.data(), 4 * kl);
-            memcpy(st.lock_snap.as<uint64_t>() + lo0, mp.lock_snap.data(), 8 * kl);
-            memcpy(st.lock_txn.as<uint32_t>() + lo0, mp.lock_txn.data(), 4 * kl);
+            memcpy(ltab + lo0, mp.lock_table.data(), 4 * kl);
+            memcpy(lsnap + lo0, mp.lock_snap.data(), 8 * kl);
+            memcpy(ltxn + lo0, mp.lock_txn.data(), 4 * kl);
         }
     });
     st.n = n;
@@ -1436,9 +1466,9 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
     m.gid = gid;
     m.snap = sn;
     m.txn = txn;
-    m.lock_table = st.lock_table.as<uint32_t>();
-    m.lock_snap = st.lock_snap.as<uint64_t>();
-    m.lock_txn = st.lock_txn.as<uint32_t>();
+    m.lock_table = ltab;
+    m.lock_snap = lsnap;
+    m.lock_txn = ltxn;
     m.forced = forced;
     return HSC_OK;
 }
@@ -1835,41 +1865,23 @@ static int launch_stage(hsc_ctx *c, Stage &st)
 {
     if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
     hipStream_t s = c->stream;
-    const int W = c->W;
-    const size_t n1 = std::max<size_t>(st.n, 1), l1 = std::max<size_t>(st.n_lock, 1);
-    HIPCHK(c, c->p_lo.ensure(8 * (size_t)W * n1));
-    HIPCHK(c, c->p_hi.ensure(8 * (size_t)W * n1));
-    HIPCHK(c, c->p_gid.ensure(4 * n1));
-    HIPCHK(c, c->p_snap.ensure(8 * n1));
-    HIPCHK(c, c->p_txn.ensure(4 * n1));
-    HIPCHK(c, c->p_lock_table.ensure(4 * l1));
-    HIPCHK(c, c->p_lock_snap.ensure(8 * l1));
-    HIPCHK(c, c->p_lock_txn.ensure(4 * l1));
+    HIPCHK(c, c->p_arena.ensure(std::max<size_t>(st.L.total, 256)));
     HIPCHK(c, c->p_verdict.ensure(std::max<size_t>(st.n_txn, 1)));
     if (st.verdict.ensure(std::max<size_t>(st.n_txn, 1), true)) return fail(c, HSC_ENOMEM, "staging");
-    if (st.n) {
-        HIPCHK(c, hipMemcpyAsync(c->p_lo.p, st.lo.p, 8 * (size_t)W * st.n, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->p_hi.p, st.hi.p, 8 * (size_t)W * st.n, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->p_gid.p, st.gid.p, 4 * st.n, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->p_snap.p, st.snap.p, 8 * st.n, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->p_txn.p, st.txn.p, 4 * st.n, hipMemcpyHostToDevice, s));
-    }
-    if (st.n_lock) {
-        HIPCHK(c, hipMemcpyAsync(c->p_lock_table.p, st.lock_table.p, 4 * st.n_lock, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->p_lock_snap.p, st.lock_snap.p, 8 * st.n_lock, hipMemcpyHostToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->p_lock_txn.p, st.lock_txn.p, 4 * st.n_lock, hipMemcpyHostToDevice, s));
-    }
+    if (st.n || st.n_lock)  // every column in one transfer
+        HIPCHK(c, hipMemcpyAsync(c->p_arena.p, st.arena.p, st.L.total, hipMemcpyHostToDevice, s));
+    auto dcol = [&](size_t off) { return (void *)((uint8_t *)c->p_arena.p + off); };
     hsc_probe_batch b{};
     b.n = st.n;
-    b.lo = c->p_lo.as<uint64_t>();
-    b.hi = c->p_hi.as<uint64_t>();
-    b.gid = c->p_gid.as<uint32_t>();
-    b.snap = c->p_snap.as<uint64_t>();
-    b.txn = c->p_txn.as<uint32_t>();
+    b.lo = (const uint64_t *)dcol(st.L.lo);
+    b.hi = (const uint64_t *)dcol(st.L.hi);
+    b.gid = (const uint32_t *)dcol(st.L.gid);
+    b.snap = (const uint64_t *)dcol(st.L.snap);
+    b.txn = (const uint32_t *)dcol(st.L.txn);
     b.n_lock = st.n_lock;
-    b.lock_table = c->p_lock_table.as<uint32_t>();
-    b.lock_snap = c->p_lock_snap.as<uint64_t>();
-    b.lock_txn = c->p_lock_txn.as<uint32_t>();
+    b.lock_table = (const uint32_t *)dcol(st.L.lock_table);
+    b.lock_snap = (const uint64_t *)dcol(st.L.lock_snap);
+    b.lock_txn = (const uint32_t *)dcol(st.L.lock_txn);
     b.n_txn = st.n_txn;
     b.verdict = c->p_verdict.as<uint8_t>();
     b.bitmap = nullptr;
@@ -1981,7 +1993,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->d_table_max, &c->d_group_table, &c->d_count, &c->d_sp_g, &c->d_sp_w,
                     &c->w_item_tile, &c->w_hist, &c->p_lo, &c->p_hi,
                     &c->p_gid, &c->p_snap, &c->p_txn, &c->p_lock_table, &c->p_lock_snap,
-                    &c->p_lock_txn, &c->p_verdict, &c->p_bitmap, &c->w_code, &c->w_counts,
+                    &c->p_lock_txn, &c->p_arena, &c->p_verdict, &c->p_bitmap, &c->w_code, &c->w_counts,
                     &c->w_bucket, &c->w_cursor, &c->w_items, &c->w_item_desc, &c->w_recs,
                     &c->d_nkeys, &c->d_nmaxs, &c->d_nbase, &c->d_nzero, &c->d_ntmax,
                     &c->d_nsp_g, &c->d_nsp_w, &c->d_ngs, &c->d_nscratch, &c->p_code_lo,

@@ -116,6 +116,15 @@ class Marshalled(C.Structure):
                 ("lock_txn", C.POINTER(C.c_uint32)), ("forced", C.POINTER(C.c_uint8))]
 
 
+class CollectorStats(C.Structure):
+    _fields_ = [("calls", C.c_uint64), ("batches", C.c_uint64), ("max_batch", C.c_uint64)]
+
+
+class ConcurrentResult(C.Structure):
+    _fields_ = [("seconds", C.c_double), ("calls", C.c_uint64), ("lat_mean_us", C.c_double),
+                ("lat_p50_us", C.c_double), ("lat_p99_us", C.c_double)]
+
+
 # Every symbol include/hip_serial.h declares (checked by tests/test_abi.py).
 EXPORTS = [
     "hsc_ctx_create", "hsc_ctx_destroy", "hsc_set_stream", "hsc_last_error", "hsc_device_count",
@@ -131,7 +140,9 @@ EXPORTS = [
     "hsc_set_layout", "hsc_window_layout", "hsc_coalesce_readsets", "hsc_rw_edges",
     "hsc_window_code_words", "hsc_window_append_log", "hsc_window_append_raw",
     "hsc_window_delta_rows", "hsc_set_threads", "hsc_currangearrs_build",
-    "hsc_currangearrs_free", "hsc_dep_graph_build", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
+    "hsc_currangearrs_free", "hsc_collector_create", "hsc_collector_destroy",
+    "hsc_collector_check", "hsc_collector_get_stats", "hsc_harness_concurrent",
+    "hsc_dep_graph_build", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
 ]
 
 (LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES,
@@ -206,6 +217,14 @@ def load() -> C.CDLL:
         "hsc_window_delta_rows": (C.c_size_t, [_p]),
         "hsc_currangearrs_build": (C.c_int, [C.POINTER(_ReadSets), C.POINTER(C.POINTER(_p))]),
         "hsc_currangearrs_free": (None, [C.POINTER(_p), C.c_int]),
+        "hsc_collector_create": (C.c_int, [_p, C.c_int, C.c_int, C.POINTER(_p)]),
+        "hsc_collector_destroy": (None, [_p]),
+        "hsc_collector_check": (C.c_int, [_p, _p, C.POINTER(C.c_uint), C.POINTER(C.c_uint),
+                                          C.c_int]),
+        "hsc_collector_get_stats": (C.c_int, [_p, C.POINTER(CollectorStats)]),
+        "hsc_harness_concurrent": (C.c_int, [_p, _p, C.POINTER(_p), C.c_int, C.c_int, C.c_int,
+                                             C.c_int, C.POINTER(C.c_int),
+                                             C.POINTER(ConcurrentResult)]),
         "hsc_window_layout": (C.c_int, [_p]),
     }
     for name, (res, args) in sig.items():
@@ -557,6 +576,40 @@ class Validator:
                                              out.ctypes.data_as(C.POINTER(C.c_int)))
         self._chk(rc, "hip_serial_check_batch")
         return out[:n]
+
+    def concurrent_check(self, arrs, nthreads: int, rounds: int = 1, regop_only: int = 0,
+                         collect: bool = True, max_batch: int = 0, max_wait_us: int = 0):
+        """nthreads native caller threads checking arrs concurrently
+        (hsc_harness_concurrent), each call one read set through a batching
+        collector (hsc_collector_check) or, collect=False, one
+        hip_bdb_osql_serial_check per call.  -> (verdicts int32[n], stats dict)."""
+        n = len(arrs.arrs) if hasattr(arrs, "arrs") else arrs.n
+        out = np.zeros(max(1, n), dtype=np.int32)
+        col = _p()
+        if collect:
+            self._chk(self.lib.hsc_collector_create(self.ctx, max_batch, max_wait_us,
+                                                    C.byref(col)), "hsc_collector_create")
+        res = ConcurrentResult()
+        try:
+            rc = self.lib.hsc_harness_concurrent(self.ctx, col, arrs.pointers(), n, nthreads,
+                                                 rounds, regop_only,
+                                                 out.ctypes.data_as(C.POINTER(C.c_int)),
+                                                 C.byref(res))
+            self._chk(rc, "hsc_harness_concurrent")
+            st = {"threads": nthreads, "calls": res.calls, "seconds": res.seconds,
+                  "checks_per_s": res.calls / res.seconds if res.seconds > 0 else 0.0,
+                  "lat_mean_us": res.lat_mean_us, "lat_p50_us": res.lat_p50_us,
+                  "lat_p99_us": res.lat_p99_us, "collector": bool(collect)}
+            if collect:
+                cs = CollectorStats()
+                self._chk(self.lib.hsc_collector_get_stats(col, C.byref(cs)),
+                          "hsc_collector_get_stats")
+                st.update(batches=cs.batches, max_batch=cs.max_batch,
+                          mean_batch=cs.calls / max(1, cs.batches))
+        finally:
+            if collect:
+                self.lib.hsc_collector_destroy(col)
+        return out[:n], st
 
     def rw_edges(self, rs: ReadSets):
         """(txn uint32[k], writer commit LSN uint64[k]): every (read set,

@@ -343,6 +343,25 @@ int hip_bdb_osql_serial_check(void *ctx, void *ranges, unsigned int *file,
 int hip_serial_check_batch(void *ctx, void *const *ranges, unsigned int *file,
                            unsigned int *offset, int regop_only, int n,
                            int *rc_out);
+/* Batching collector for concurrent callers (the reference calls
+ * bdb_osql_serial_check from every block-processor thread, db/toblock.c:
+ * 4779-4836).  hsc_collector_check has bdb_osql_serial_check's signature and
+ * contract for one read set; calls that arrive together are run as one
+ * hip_serial_check_batch by one of their callers (group-commit leader: it
+ * takes every queued call, up to max_batch -- 0 = 65536 -- after waiting up to
+ * max_wait_us for more to arrive; 0 = no wait, batches form while the previous
+ * one runs).  Thread-safe; destroy only after every caller has returned. */
+typedef struct hsc_collector hsc_collector;
+typedef struct hsc_collector_stats {
+    uint64_t calls;      /* hsc_collector_check calls that queued */
+    uint64_t batches;    /* device passes run for them */
+    uint64_t max_batch;  /* largest batch */
+} hsc_collector_stats;
+int hsc_collector_create(hsc_ctx *ctx, int max_batch, int max_wait_us, hsc_collector **out);
+void hsc_collector_destroy(hsc_collector *col);
+int hsc_collector_check(hsc_collector *col, void *ranges, unsigned int *file,
+                        unsigned int *offset, int regop_only);
+int hsc_collector_get_stats(hsc_collector *col, hsc_collector_stats *out);
 /* Read/write conflict pairs before the OR-reduction:
  * every (read set t, writer commit LSN c) such that a write committed at c
  * (c > t's snapshot) has a key inside one of t's ranges -- all the pairs the
@@ -494,6 +513,19 @@ int hsc_dep_graph_scc_cut(hsc_ctx *ctx, uint32_t ntxn, const uint8_t *cover_dev,
  * one per read set of rs: *out = void *[ntxn] of hsc_currangearr *. */
 int hsc_currangearrs_build(const hsc_readsets *rs, void ***out);
 void hsc_currangearrs_free(void **arrs, int n);
+/* nthreads caller threads, each checking read sets i = t, t + nthreads, ...
+ * of arrs[n] `rounds` times with its own (file, offset) copies of the set's
+ * snapshot -- through col (hsc_collector_check) when col != NULL, else one
+ * hip_bdb_osql_serial_check per call.  rc_out[n] = last verdicts; per-call
+ * latencies summarised in *res. */
+typedef struct hsc_concurrent_result {
+    double seconds;                             /* wall time of all threads */
+    uint64_t calls;
+    double lat_mean_us, lat_p50_us, lat_p99_us;  /* per call */
+} hsc_concurrent_result;
+int hsc_harness_concurrent(hsc_ctx *ctx, hsc_collector *col, void *const *arrs, int n,
+                           int nthreads, int rounds, int regop_only, int *rc_out,
+                           hsc_concurrent_result *res);
 
 #ifdef __cplusplus
 }

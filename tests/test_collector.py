@@ -1,0 +1,85 @@
+"""Batching collector (hsc_collector_check): many native caller threads, one
+read set per call, as comdb2's block processors call bdb_osql_serial_check
+(db/toblock.c:4779-4836 -> bdb/serializable.c:571).  Verdicts and the
+(file, offset) side effect must be exactly the single call's; the host-only
+tests drive the regop_only mode (decided on the host) and the fail-closed
+rule, the GPU tests the full check against the oracle."""
+import numpy as np
+import pytest
+
+from comdb2_amd.hsc import NativeCurRangeArrs, Validator
+from comdb2_amd.workloads import config2, random_case
+
+
+@pytest.fixture(scope="module")
+def host():
+    v = Validator(-1)
+    yield v
+    v.close()
+
+
+@pytest.mark.parametrize("nthreads", [1, 4, 16])
+def test_regop_only_through_collector(host, oracle_mod, nthreads):
+    log, rs = random_case(321 + nthreads, broken=True, n_txn=400)
+    host.ingest_log(log)
+    want, _, _ = oracle_mod.check(log, rs, regop_only=1)
+    arrs = NativeCurRangeArrs(rs)
+    got, st = host.concurrent_check(arrs, nthreads, rounds=3, regop_only=1)
+    np.testing.assert_array_equal(got != 0, want != 0)
+    assert st["calls"] == 3 * rs.ntxn
+    assert 1 <= st["batches"] <= st["calls"] and st["max_batch"] <= nthreads
+    direct, _ = host.concurrent_check(arrs, nthreads, regop_only=1, collect=False)
+    np.testing.assert_array_equal(direct, got)
+    arrs.close()
+
+
+def test_collector_bounds_batches(host, oracle_mod):
+    log, rs = random_case(99, n_txn=300)
+    host.ingest_log(log)
+    want, _, _ = oracle_mod.check(log, rs, regop_only=1)
+    arrs = NativeCurRangeArrs(rs)
+    got, st = host.concurrent_check(arrs, 16, rounds=2, regop_only=1, max_batch=3,
+                                    max_wait_us=200)
+    np.testing.assert_array_equal(got != 0, want != 0)
+    assert st["max_batch"] <= 3 and st["batches"] >= st["calls"] / 3
+    arrs.close()
+
+
+def test_full_checks_fail_closed_without_device(host):
+    # a host-only context cannot run the join: every full check answers 1
+    # (errors are "not serializable"), through the collector as directly
+    log, rs = random_case(5, n_txn=64)
+    host.ingest_log(log)
+    arrs = NativeCurRangeArrs(rs)
+    got, st = host.concurrent_check(arrs, 8, regop_only=0)
+    assert (got == 1).all() and st["calls"] == rs.ntxn
+    arrs.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nthreads", [2, 16, 64])
+def test_gpu_full_checks_through_collector(validator, oracle_mod, nthreads):
+    log, rs = random_case(700 + nthreads, broken=(nthreads == 16), n_txn=600, max_ranges=12)
+    validator.ingest_log(log)
+    want, _, _ = oracle_mod.check(log, rs)
+    arrs = NativeCurRangeArrs(rs)
+    got, st = validator.concurrent_check(arrs, nthreads, rounds=2)
+    np.testing.assert_array_equal(got != 0, want != 0)
+    assert st["calls"] == 2 * rs.ntxn and st["max_batch"] <= nthreads
+    arrs.close()
+
+
+@pytest.mark.gpu
+def test_gpu_collector_config2_sample(oracle_mod):
+    v = Validator(0)
+    try:
+        wl = config2(n_commits=20_000, n_txn=4_000, seed=11)
+        v.ingest_log(wl.log)
+        want, _, _ = oracle_mod.check(wl.log, wl.readsets)
+        arrs = NativeCurRangeArrs(wl.readsets)
+        got, st = v.concurrent_check(arrs, 32)
+        np.testing.assert_array_equal(got != 0, want != 0)
+        assert st["batches"] < st["calls"]  # calls really were batched
+        arrs.close()
+    finally:
+        v.close()
