@@ -579,19 +579,30 @@ def main():
         data = ("synthetic (BASELINE config 2 generator, seed 0xC0FFEE02; int64 keys in memcmp "
                 "order as big-endian u64 words)")
     else:
-        from comdb2_amd.workloads import SEED_CONFIG5, config5_scaled
+        from comdb2_amd.workloads import SEED_CONFIG5, config5_scaled, int64_words
         c5 = config5_scaled(seed=SEED_CONFIG5, keys_per_gpu=args.c5_keys, n_txn=args.n_txn,
                             rank=rank, world=world)
-        gid, words, lsn, end_lsn = c5.gid, c5.words, c5.lsn, c5.end_lsn
+        keys5, lsn, end_lsn = c5.keys, c5.lsn, c5.end_lsn
         first_rs = c5.readsets
         more_rs = lambda bi: config5_scaled(seed=SEED_CONFIG5 + 7919 * bi,
                                             keys_per_gpu=args.c5_keys, n_txn=args.n_txn,
                                             rank=rank, world=world, window=False).readsets
-        span = (1 << c5.params["key_bits"]) // world
-        make_shards = lambda W: shard.KeyRangeShards.int64_spans(world, span, W)
-        workload = (f"config5: per GPU {args.c5_keys} Zipf(1.2) writes over its 2^32/N key span "
-                    f"(hot keys collapse under dedupe) and 100k read sets x 10 ranges (width "
-                    f"{c5.params['width']}, half the points on hot keys)")
+        # sampled global splitters over the probe work, rows to owners
+        if world > 1:
+            c5_split = shard.sampled_splitters(keys5, c5.range_keys, world, rank,
+                                               shard.ROW_COST, shard.RANGE_COST)
+            keys5, lsn = shard.exchange_rows(keys5, lsn, c5_split["splitters"])
+        else:
+            c5_split = dict(splitters=np.zeros(0, np.int64), est_load=np.ones(1),
+                            load=lambda b: np.ones(1))
+        words = int64_words(keys5)
+        gid = np.zeros(len(keys5), dtype=np.uint32)
+        del keys5
+        make_shards = lambda W: shard.KeyRangeShards.int64_splitters(c5_split["splitters"], W)
+        workload = (f"config5: one global Zipf(1.2) law over 2^32 keys, {args.c5_keys} logged "
+                    f"writes per GPU (hot keys collapse under dedupe), sampled global splitters, "
+                    f"100k read sets x 10 ranges per GPU (width {c5.params['width']}, half the "
+                    f"points on Zipf-drawn hot keys)")
         data = "synthetic (config 5 generator, seed 0xC0FFEE05, weak scaling per GPU)"
     n_w = len(lsn)
     tg = torch.from_numpy(gid).to(dev)
@@ -814,7 +825,7 @@ def main():
                              "equal": bool(np.array_equal(want != 0, v0 != 0)), "cpu_s": secs}
     if args.config == 5:
         # per-GPU imbalance: routed ranges and 1-stream probe time per rank
-        loc = np.array([n_r, tm["probe_total_ms"]], dtype=np.float64)
+        loc = np.array([n_r, tm["probe_total_ms"], n_keys], dtype=np.float64)
         if world > 1:
             g = torch.from_numpy(loc).to(dev)
             allg = [torch.zeros_like(g) for _ in range(world)]
@@ -822,10 +833,21 @@ def main():
             loc = torch.stack(allg).cpu().numpy()
         else:
             loc = loc[None, :]
-        out["imbalance"] = {"ranges_per_rank": loc[:, 0].tolist(),
+        fixed = np.array([(j << 32) // world for j in range(1, world)], np.int64)
+        est_fixed = c5_split["load"](fixed)
+        est = c5_split["est_load"]
+        out["imbalance"] = {"partition": "sampled global splitters (distinct window keys x "
+                                         f"{shard.ROW_COST} + range lower bounds x "
+                                         f"{shard.RANGE_COST}, one all_gather)",
+                            "splitters": c5_split["splitters"].tolist(),
+                            "ranges_per_rank": loc[:, 0].tolist(),
+                            "window_keys_per_rank": loc[:, 2].tolist(),
                             "probe_ms_per_rank": loc[:, 1].tolist(),
                             "ranges_max_over_mean": float(loc[:, 0].max() / loc[:, 0].mean()),
-                            "time_max_over_mean": float(loc[:, 1].max() / loc[:, 1].mean())}
+                            "time_max_over_mean": float(loc[:, 1].max() / loc[:, 1].mean()),
+                            "sample_est_max_over_mean": float(est.max() / est.mean()),
+                            "fixed_span_sample_est_max_over_mean":
+                                float(est_fixed.max() / max(est_fixed.mean(), 1e-9))}
         if args.check and world == 1:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle

@@ -141,10 +141,13 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
         k->elected = false;
         if (!k->q.empty()) k->q.front()->cv.notify_one();  // elect the next leader now
         lk.unlock();
+        const auto t0 = std::chrono::steady_clock::now();
         run_group(k, regop, 1);
         run_group(k, full, 0);
+        const auto t1 = std::chrono::steady_clock::now();
         lk.lock();
         k->running = false;
+        k->st.busy_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
         k->st.batches++;
         k->st.max_batch = std::max<uint64_t>(k->st.max_batch, take);
         for (auto *g : {&regop, &full})

@@ -117,7 +117,8 @@ class Marshalled(C.Structure):
 
 
 class CollectorStats(C.Structure):
-    _fields_ = [("calls", C.c_uint64), ("batches", C.c_uint64), ("max_batch", C.c_uint64)]
+    _fields_ = [("calls", C.c_uint64), ("batches", C.c_uint64), ("max_batch", C.c_uint64),
+                ("busy_ns", C.c_uint64)]
 
 
 class ConcurrentResult(C.Structure):
@@ -442,6 +443,10 @@ class Validator:
         if end_lsn is not None:
             self._chk(self.lib.hsc_window_set_end(self.ctx, int(end_lsn)), "hsc_window_set_end")
 
+    def set_end(self, end_lsn: int) -> None:
+        """hsc_window_set_end: the log's end LSN (curlsn of full checks)."""
+        self._chk(self.lib.hsc_window_set_end(self.ctx, int(end_lsn)), "hsc_window_set_end")
+
     @property
     def delta_rows(self) -> int:
         return self.lib.hsc_window_delta_rows(self.ctx)
@@ -605,7 +610,9 @@ class Validator:
                 self._chk(self.lib.hsc_collector_get_stats(col, C.byref(cs)),
                           "hsc_collector_get_stats")
                 st.update(batches=cs.batches, max_batch=cs.max_batch,
-                          mean_batch=cs.calls / max(1, cs.batches))
+                          mean_batch=cs.calls / max(1, cs.batches),
+                          device_pass_us=cs.busy_ns / 1e3 / max(1, cs.batches),
+                          busy_frac=cs.busy_ns / 1e9 / max(res.seconds, 1e-9))
         finally:
             if collect:
                 self.lib.hsc_collector_destroy(col)

@@ -73,6 +73,21 @@ class KeyRangeShards:
                                 key_words(F.enc_int64((r + 1) * span - 1), W))
                                for r in range(world)])
 
+    @staticmethod
+    def int64_splitters(splitters: Sequence[int], W: int) -> "KeyRangeShards":
+        """Rank j owns int64 values [splitters[j-1], splitters[j]); the first
+        and last ranks own everything below / above (any key bytes)."""
+        sp = [int(x) for x in splitters]
+        world = len(sp) + 1
+        b = []
+        for r in range(world):
+            lo = [0] * W if r == 0 else key_words(F.enc_int64(sp[r - 1]), W)
+            # the upper bound padded with 0xFF: every key that has it as a prefix
+            hi = ([(1 << 64) - 1] * W if r == world - 1
+                  else key_words(F.enc_int64(sp[r] - 1) + b"\xff" * (8 * W - 9), W))
+            b.append((lo, hi))
+        return KeyRangeShards(b)
+
     def range_mask(self, m: dict, rank: int) -> np.ndarray:
         lo_b, hi_b = self.bounds[rank]
         return _leq(m["lo"], hi_b) & _geq(m["hi"], lo_b)
@@ -104,6 +119,109 @@ class GroupShards:
 
     def lock_mask(self, m: dict, rank: int) -> np.ndarray:
         return np.full(m["n_lock"], rank == 0, dtype=bool)
+
+
+# ---- configs 2 / 5: sampled global splitters ---------------------------------
+# A skewed key law (config 5: one Zipf(1.2) over 2^32 keys, hot keys at the low
+# end) defeats fixed spans: nearly every distinct key and every hot range falls
+# into one span.  The splitters are instead quantiles of the probe phase's
+# work over the key space, estimated from a sample every rank contributes
+# (one all_gather at window build): each rank's distinct window keys (after
+# its local dedupe; hot keys collapse there) weighted ROW_COST per row, and
+# a strided share of the batch's range lower bounds weighted RANGE_COST per
+# range (measured per-unit probe time; SURVEY.md §8(d)'s byte model
+# N_w s_w + N_r s_r underweights ranges, whose records are written and read
+# back by the scatter and the join).  Rows then move to their
+# owners with one all_to_all (exchange_rows); ranges that straddle a
+# splitter go to both sides (KeyRangeShards routing).
+
+INT64_MIN, INT64_MAX = -(1 << 63), (1 << 63) - 1
+# Relative probe-phase cost of one distinct window row and one routed range on
+# the narrow tile pipeline, fitted to a 2-rank config-5 run on MI355X
+# (t = a rows + b ranges: a ~ 17 ps, b ~ 54 ps; profiles/r02_c5_gloo2.log).
+ROW_COST, RANGE_COST = 1.0, 3.0
+
+
+def sampled_splitters(local_keys: np.ndarray, range_keys: np.ndarray, world: int, rank: int,
+                      w_row: float, w_range: float, samples: int = 4096, group=None) -> dict:
+    """world - 1 int64 splitters (rank j owns key values [split[j-1], split[j]))
+    balancing w_row * distinct window rows + w_range * ranges, identical on
+    every rank.  local_keys: this rank's window key values (any order,
+    duplicates allowed); range_keys: lower key values of the (global) batch's
+    ranges.  Returns dict(splitters int64[world-1], and the sample's estimate
+    of the per-rank load under these splitters and under fixed spans of
+    [0, 2^key_bits) for comparison, in the caller's units)."""
+    import torch
+    import torch.distributed as dist
+    uk = np.unique(np.asarray(local_keys, np.int64))
+    rk = np.sort(np.asarray(range_keys, np.int64)[rank::world])
+    s_w = min(samples, len(uk))
+    s_r = min(samples, len(rk))
+    # evenly spaced order statistics; each stands for an equal share of the rows
+    pick = lambda a, k: a[(np.arange(k) * len(a)) // max(k, 1)] if k else a[:0]
+    keys = np.concatenate([pick(uk, s_w), pick(rk, s_r)])
+    wts = np.concatenate([np.full(s_w, w_row * len(uk) / max(s_w, 1)),
+                          np.full(s_r, w_range * len(rk) / max(s_r, 1))])
+    if world > 1 and dist.is_initialized():
+        n = 2 * samples
+        kb = torch.full((n,), INT64_MAX, dtype=torch.int64)
+        wb = torch.zeros(n, dtype=torch.float64)
+        kb[:len(keys)] = torch.from_numpy(keys)
+        wb[:len(wts)] = torch.from_numpy(wts)
+        dev = torch.device("cuda", torch.cuda.current_device()) \
+            if dist.get_backend(group) == "nccl" else torch.device("cpu")
+        kb, wb = kb.to(dev), wb.to(dev)
+        ks = [torch.empty_like(kb) for _ in range(world)]
+        ws = [torch.empty_like(wb) for _ in range(world)]
+        dist.all_gather(ks, kb, group=group)
+        dist.all_gather(ws, wb, group=group)
+        keys = torch.cat(ks).cpu().numpy()
+        wts = torch.cat(ws).cpu().numpy()
+    order = np.argsort(keys, kind="stable")
+    keys, wts = keys[order], wts[order]
+    cum = np.cumsum(wts)
+    total = cum[-1] if len(cum) else 0.0
+    split = []
+    for j in range(1, world):
+        i = int(np.searchsorted(cum, total * j / world, side="left"))
+        k = int(keys[min(i, len(keys) - 1)]) if len(keys) else 0
+        if split and k <= split[-1]:
+            k = split[-1] + 1  # a single hot key cannot be split: keep splitters increasing
+        split.append(k)
+    split = np.asarray(split, np.int64)
+
+    def load(bounds):
+        own = np.searchsorted(bounds, keys, side="right")
+        return np.bincount(own, weights=wts, minlength=world)[:world]
+    return dict(splitters=split, est_load=load(split), load=load)
+
+
+def exchange_rows(keys: np.ndarray, lsn: np.ndarray, splitters: np.ndarray, group=None):
+    """Move window rows (int64 key values, u64 commit LSNs) to the rank owning
+    their key (one all_to_all; on RCCL through device buffers).  Returns this
+    rank's (keys, lsn)."""
+    import torch
+    import torch.distributed as dist
+    world = len(splitters) + 1
+    if world == 1 or not dist.is_initialized():
+        return keys, lsn
+    own = np.searchsorted(splitters, keys, side="right")
+    order = np.argsort(own, kind="stable")
+    cnt = np.bincount(own, minlength=world).astype(np.int64)
+    dev = torch.device("cuda", torch.cuda.current_device()) \
+        if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    send_n = torch.from_numpy(cnt).to(dev)
+    recv_n = torch.empty_like(send_n)
+    dist.all_to_all_single(recv_n, send_n, group=group)
+    rc = recv_n.cpu().numpy().tolist()
+    sc = cnt.tolist()
+    out = []
+    for a in (np.asarray(keys, np.int64), np.asarray(lsn, np.uint64).view(np.int64)):
+        src = torch.from_numpy(np.ascontiguousarray(a[order])).to(dev)
+        dst = torch.empty(int(sum(rc)), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(dst, src, output_split_sizes=rc, input_split_sizes=sc, group=group)
+        out.append(dst.cpu().numpy())
+    return out[0], out[1].view(np.uint64)
 
 
 def route(m: dict, range_mask: np.ndarray, lock_mask: np.ndarray) -> dict:

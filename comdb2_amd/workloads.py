@@ -641,45 +641,65 @@ def config3(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4, n_writes
 
 @dataclasses.dataclass
 class Config5Scaled:
-    gid: np.ndarray             # uint32[n] this rank's window rows (log order)
-    words: np.ndarray           # uint64[2][n] big-endian key words
-    lsn: np.ndarray             # uint64[n] commit LSN of each row
+    keys: np.ndarray            # int64[n] this rank's segment of the log: written key values
+    lsn: np.ndarray             # uint64[n] commit LSN of each row (log order)
     readsets: ReadSets          # global read sets (identical on every rank)
+    range_keys: np.ndarray      # int64[nr] lower key value of every range (splitter sampling)
     end_lsn: int
     params: dict
+
+    @property
+    def gid(self) -> np.ndarray:
+        return np.zeros(len(self.keys), dtype=np.uint32)
+
+    @property
+    def words(self) -> np.ndarray:
+        return int64_words(self.keys)
+
+
+def int64_words(vals: np.ndarray) -> np.ndarray:
+    """int64 index-key values -> uint64[2][n] big-endian key words of their
+    9-byte enc_int64 keys (db/types.c:766-771), zero padded to 16 bytes."""
+    n = len(vals)
+    pad = np.zeros((n, 16), dtype=np.uint8)
+    pad[:, :9] = F.enc_int64_array(vals)
+    return pad.view(">u8").astype(np.uint64).reshape(n, 2).T.copy()
+
+
+def zipf_keys(rng, n: int, s: float, key_bits: int) -> np.ndarray:
+    """n draws of a Zipf(s) law truncated to 2^key_bits keys: key k - 1 has
+    probability ~ k^-s, so the hot keys are the smallest values (draws past
+    the key space are redrawn)."""
+    out = rng.zipf(s, size=n).astype(np.uint64)
+    lim = np.uint64(1 << key_bits)
+    bad = np.nonzero(out > lim)[0]
+    while len(bad):
+        out[bad] = rng.zipf(s, size=len(bad)).astype(np.uint64)
+        bad = bad[out[bad] > lim]
+    return (out - np.uint64(1)).astype(np.int64)
 
 
 def config5_scaled(seed: int = SEED_CONFIG5, keys_per_gpu: int = 125_000_000,
                    keys_per_commit: int = 10, n_txn: int = 100_000, ranges_per_txn: int = 10,
                    zipf_s: float = 1.2, key_bits: int = 32, snap_recent: float = 0.01,
                    rank: int = 0, world: int = 1, window: bool = True) -> Config5Scaled:
-    """Config 5 at scale without a log (a 1B-key window,
-    Zipf s = 1.2 over 2^key_bits keys, ranges as config 2 scaled): rank r holds
-    keys_per_gpu writes whose keys are Zipf samples hashed into its own span
-    [r, r+1) * 2^key_bits / world (weak scaling: every GPU has its own hot
-    keys, and hot keys collapse under dedupe), with config 2's commit/LSN
-    numbering (global commit g = c * world + r).  The read sets are global:
-    config 2's mix over the whole key space, range width scaled to the key
-    density (about 10 written keys per range), and half of the point ranges
-    aimed at hot keys of a uniformly chosen rank.  window=False skips the
-    window (another batch of read sets over the same window)."""
+    """Config 5 (a 1B-key log window, Zipf s = 1.2 over 2^32
+    keys, ranges as config 2 scaled), weak-scaled: ONE global Zipf(s) law over
+    2^key_bits key values (hot keys are the small values, so a fixed split of
+    the key space puts nearly every distinct key and every hot range on rank
+    0); the log is world x keys_per_gpu writes and rank r generates its
+    segment -- global commits g = c * world + r, keys_per_commit writes each,
+    config 2's LSN numbering.  Which rank owns which rows is decided later by
+    sampled global splitters (shard.sampled_splitters / exchange_rows).  The
+    read sets are global: config 2's kind mix over the whole key space, range
+    width scaled to the mean key density (about 10 logged writes per range),
+    half of the point ranges on Zipf-drawn hot keys.  window=False: another
+    batch of read sets over the same log (no rows)."""
     K = keys_per_commit
     R = K + 3
-    span = (1 << key_bits) // world
-
-    def hot_keys(rng, r, n):
-        z = rng.zipf(zipf_s, size=n).astype(np.uint64)
-        h = (z * np.uint64(0x9E3779B1)) & np.uint64((1 << 32) - 1)
-        return (np.uint64(r * span) + h % np.uint64(span)).astype(np.int64)
-
     n_commits = keys_per_gpu // K
     n = n_commits * K if window else 0
-    vals = hot_keys(np.random.default_rng([seed, 5, rank]), rank, n)
-    b = F.enc_int64_array(vals)
-    pad = np.zeros((n, 16), dtype=np.uint8)
-    pad[:, :9] = b
-    words = pad.view(">u8").astype(np.uint64).reshape(n, 2).T.copy()
-    del pad, b
+    vals = zipf_keys(np.random.default_rng([seed, 5, rank]), n, zipf_s, key_bits)
     gcommit = np.arange(n // K, dtype=np.uint64) * np.uint64(world) + np.uint64(rank)
     lsn = np.repeat(lsn_of_index(gcommit * np.uint64(R) + np.uint64(R - 1)), K)
     end_lsn = int(lsn_of_index(np.array([world * n_commits * R]))[0])
@@ -687,14 +707,12 @@ def config5_scaled(seed: int = SEED_CONFIG5, keys_per_gpu: int = 125_000_000,
     rng = np.random.default_rng([seed, 1 << 20])
     T = n_txn * world
     nr = T * ranges_per_txn
-    width = max(1, int(round(10 * span / max(keys_per_gpu, 1))))
+    space = 1 << key_bits
+    width = max(1, int(round(10 * space / max(world * n_commits * K, 1))))
     kind = rng.choice(4, size=nr, p=[0.5, 0.4, 0.08, 0.02])
-    v = rng.integers(0, world * span, size=nr, dtype=np.int64)
+    v = rng.integers(0, space, size=nr, dtype=np.int64)
     aim = np.nonzero((kind == 0) & (rng.random(nr) < 0.5))[0]
-    ar = rng.integers(0, world, size=len(aim))
-    for r in range(world):
-        sel = aim[ar == r]
-        v[sel] = hot_keys(rng, r, len(sel))
+    v[aim] = zipf_keys(rng, len(aim), zipf_s, key_bits)
     lo = F.enc_int64_array(v)
     hi = F.enc_int64_array(np.where(kind == 1, v + width, v))
     lkeylen = np.full(nr, 9, dtype=np.int32)
@@ -711,7 +729,7 @@ def config5_scaled(seed: int = SEED_CONFIG5, keys_per_gpu: int = 125_000_000,
     rkeylen[rflag == 1] = 0
     t_of = np.repeat(np.arange(T), ranges_per_txn)
     order = np.lexsort((np.where(lflag == 1, -1, v), t_of))
-    lo, hi = lo[order], hi[order]
+    lo, hi, v = lo[order], hi[order], v[order]
     lkeylen, rkeylen, lflag, rflag = lkeylen[order], rkeylen[order], lflag[order], rflag[order]
     keys = np.concatenate([lo.reshape(-1), hi.reshape(-1)])
     ncg = world * n_commits
@@ -724,9 +742,42 @@ def config5_scaled(seed: int = SEED_CONFIG5, keys_per_gpu: int = 125_000_000,
                   rkeylen=rkeylen, lkey_off=np.arange(nr, dtype=np.uint64) * np.uint64(9),
                   rkey_off=np.uint64(nr * 9) + np.arange(nr, dtype=np.uint64) * np.uint64(9),
                   keys=keys, tbnames=["t1"])
-    return Config5Scaled(np.zeros(n, dtype=np.uint32), words, lsn, rs, end_lsn,
+    range_keys = np.where(lflag == 1, np.int64(-(1 << 63)), v)
+    return Config5Scaled(vals, lsn, rs, range_keys, end_lsn,
                          dict(seed=seed, keys_per_gpu=n, zipf_s=zipf_s, key_bits=key_bits,
-                              width=width, n_txn=n_txn, rank=rank, world=world))
+                              width=width, n_txn=n_txn, rank=rank, world=world,
+                              keys_per_commit=K))
+
+
+def config5_log(segments: Sequence[np.ndarray], keys_per_commit: int = 10) -> LLog:
+    """The global log of config5_scaled's per-rank key segments (rank r's
+    commit c is global commit c * world + r): per commit ltran_start, one
+    undo_upd_ix per key, ltran_commit, regop -- the LSNs config5_scaled gives
+    its rows and snapshots.  For oracle checks of small cases."""
+    world, K = len(segments), keys_per_commit
+    R = K + 3
+    n_commits = len(segments[0]) // K
+    ncg = world * n_commits
+    gkeys = np.stack([np.asarray(sg, np.int64).reshape(n_commits, K) for sg in segments], axis=1)
+    gkeys = gkeys.reshape(ncg * K)  # global commit order: (c, r) -> c * world + r
+    nrec = ncg * R
+    idx = np.arange(nrec, dtype=np.uint64)
+    lsns = lsn_of_index(idx)
+    j = (idx % np.uint64(R)).astype(np.int64)
+    rectype = np.full(nrec, F.REC_UNDO_UPD_IX, dtype=np.uint32)
+    rectype[j == 0] = F.REC_LTRAN_START
+    rectype[j == R - 2] = F.REC_LTRAN_COMMIT
+    rectype[j == R - 1] = F.REC_TXN_REGOP
+    prev = np.zeros(nrec, dtype=np.uint64)
+    prev[1:] = lsns[:-1]
+    prev[j == 0] = 0
+    is_undo = (j >= 1) & (j <= K)
+    key_off = np.zeros(nrec, dtype=np.uint64)
+    key_off[is_undo] = np.arange(ncg * K, dtype=np.uint64) * np.uint64(9)
+    return LLog(lsns, rectype, prev, np.zeros(nrec, np.int16),
+                np.where(is_undo, 0, -1).astype(np.int32), np.zeros(nrec, np.int16), key_off,
+                np.where(is_undo, 9, 0).astype(np.int32), F.enc_int64_array(gkeys).reshape(-1),
+                ["t1"], int(lsn_of_index(np.array([nrec]))[0]))
 
 
 def config5(seed: int = SEED_CONFIG5, n_commits: int = 100_000, keys_per_commit: int = 10,

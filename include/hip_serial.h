@@ -356,6 +356,7 @@ typedef struct hsc_collector_stats {
     uint64_t calls;      /* hsc_collector_check calls that queued */
     uint64_t batches;    /* device passes run for them */
     uint64_t max_batch;  /* largest batch */
+    uint64_t busy_ns;    /* time inside the batches' device passes */
 } hsc_collector_stats;
 int hsc_collector_create(hsc_ctx *ctx, int max_batch, int max_wait_us, hsc_collector **out);
 void hsc_collector_destroy(hsc_collector *col);

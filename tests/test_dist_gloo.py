@@ -53,6 +53,12 @@ def _worker(rank, world, port, mode, out_path):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     v = Validator(-1)
+    if mode == "config5":
+        _config5_rank(rank, world, v, out_path)
+        dist.barrier()
+        dist.destroy_process_group()
+        v.close()
+        return
     if mode == "keyrange":
         kw = dict(n_commits=1500, n_txn=300, value_bits=18, width=1 << 9, snap_recent=0.5)
         shards_logs = [config2(rank=r, world=world, **kw).log for r in range(world)]
@@ -95,6 +101,64 @@ def _worker(rank, world, port, mode, out_path):
     v.close()
 
 
+C5_KW = dict(keys_per_gpu=20_000, n_txn=300, snap_recent=0.3)
+W_ROW, W_RANGE = 1.0, 3.0  # shard.ROW_COST / RANGE_COST
+
+
+def _config5_rank(rank, world, v, out_path):
+    """Config 5 on `world` gloo ranks: rank r's segment of the global Zipf
+    log, sampled global splitters, one all_to_all of the rows to their
+    owners, the batch routed by the splitters, each shard's probes joined
+    against its own rows (oracle/sortjoin.c, the CPU stand-in for the HIP
+    join), verdicts merged with all_reduce(MAX)."""
+    import json
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    from comdb2_amd import shard
+    from comdb2_amd.workloads import config5_scaled, int64_words
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    c5 = config5_scaled(rank=rank, world=world, **C5_KW)
+    sp = shard.sampled_splitters(c5.keys, c5.range_keys, world, rank, W_ROW, W_RANGE,
+                                 samples=1024)
+    keys, lsn = shard.exchange_rows(c5.keys, c5.lsn, sp["splitters"])
+    v.register_group("t1", 0, 9)
+    v.set_end(c5.end_lsn)
+    m = v.marshal(c5.readsets)
+    sh = shard.KeyRangeShards.int64_splitters(sp["splitters"], m["words"])
+    sub = shard.route(m, sh.range_mask(m, rank), sh.lock_mask(m, rank))
+    tmax = shard.allreduce_table_max(np.array([lsn.max() if len(lsn) else 0], np.uint64))
+    sj = oracle.SortJoin(np.zeros(len(keys), np.uint32), int64_words(keys), lsn, 1)
+    t0 = time.perf_counter()
+    verdict, _ = sj.probe(sub, tmax, nthreads=1)
+    secs = time.perf_counter() - t0
+    rows = sj.rows
+    sj.close()
+    t = torch.from_numpy(verdict.copy())
+    shard.merge_verdicts(t)
+    loc = torch.tensor([rows, sub["n"], secs], dtype=torch.float64)
+    allg = [torch.zeros_like(loc) for _ in range(world)]
+    dist.all_gather(allg, loc)
+    per = torch.stack(allg).numpy()
+    fixed = np.array([(j << 32) // world for j in range(1, world)], np.int64)
+    if rank == 0:
+        np.save(out_path, t.numpy())
+        work = per[:, 0] * W_ROW + per[:, 1] * W_RANGE
+        est_fixed = sp["load"](fixed)
+        with open(out_path + ".json", "w") as f:
+            json.dump({"splitters": sp["splitters"].tolist(), "rows_per_rank": per[:, 0].tolist(),
+                       "ranges_per_rank": per[:, 1].tolist(),
+                       "probe_s_per_rank": per[:, 2].tolist(),
+                       "time_max_over_mean": float(per[:, 2].max() / per[:, 2].mean()),
+                       "work_max_over_mean": float(work.max() / work.mean()),
+                       "est_max_over_mean": float(sp["est_load"].max() / sp["est_load"].mean()),
+                       "fixed_span_est_max_over_mean": float(est_fixed.max() / est_fixed.mean())},
+                      f)
+
+
 def _run(mode, tmp_path):
     import torch.multiprocessing as mp
     out = str(tmp_path / f"verdict_{mode}.npy")
@@ -121,3 +185,22 @@ def test_group_shards_match_oracle(tmp_path, oracle_mod):
     glog, rs = random_case(77, n_commits=120, n_txn=80)
     want, _, _ = oracle_mod.check(glog, rs)
     np.testing.assert_array_equal(got != 0, want != 0)
+
+
+def test_config5_sampled_splitters_match_oracle(tmp_path, oracle_mod):
+    """one global Zipf(1.2) over 2^32 keys; sampled global
+    splitters balance the shards (a fixed split would not) and the merged
+    verdicts equal the oracle's over the global log."""
+    import json
+
+    from comdb2_amd.workloads import config5_log, config5_scaled
+    got = _run("config5", tmp_path)
+    st = json.load(open(str(tmp_path / "verdict_config5.npy") + ".json"))
+    segs = [config5_scaled(rank=r, world=2, **C5_KW) for r in range(2)]
+    glog = config5_log([s.keys for s in segs])
+    want, _, _ = oracle_mod.check(glog, segs[0].readsets, nthreads=8)
+    np.testing.assert_array_equal(got != 0, want != 0)
+    assert 0 < int((want != 0).sum()) < len(want)
+    assert st["fixed_span_est_max_over_mean"] > 1.4   # the skew is real (2.0 = all on one rank)
+    assert st["work_max_over_mean"] < 1.25            # and the splitters balance it
+    assert "time_max_over_mean" in st
