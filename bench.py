@@ -219,7 +219,8 @@ def bench_graph(args):
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    h = config4_history(n_txn=args.history_txns, n_keys=max(1000, args.history_txns // 10))
+    h = config4_history(n_txn=args.history_txns, n_keys=args.c4_keys or max(1000, args.history_txns // 10),
+                        concurrent_frac=args.c4_concurrent, max_lag=args.c4_max_lag)
     hs = shard.history_shard(h, rank, world)
     dh = shard.device_history(hs, dev)
     v = hsc.Validator(local)
@@ -282,7 +283,8 @@ def graph_cpu_baseline(args):
     sys.path.insert(0, ROOT)
     from oracle import oracle as O
     n = max(1000, min(args.history_txns, 1_000_000))
-    h = config4_history(n_txn=n, n_keys=max(1000, n // 10))
+    h = config4_history(n_txn=n, n_keys=args.c4_keys or max(1000, n // 10),
+                        concurrent_frac=args.c4_concurrent, max_lag=args.c4_max_lag)
     t0 = time.perf_counter()
     s_, d_, _ = O.dep_edges(h.txn, h.key, h.is_write, h.observed)
     O.scc(h.ntxn, s_, d_)
@@ -498,6 +500,10 @@ def main():
                     help="config 3 / 5, N = 1: full-batch CPU sort-join parity (oracle/sortjoin.c)")
     ap.add_argument("--history-txns", type=int, default=16_700_000,
                     help="config 4: transactions (x ~6 ops: 16.7M = SURVEY's 100M-op history)")
+    ap.add_argument("--c4-concurrent", type=float, default=0.02,
+                    help="config 4: fraction of txns reading a stale snapshot")
+    ap.add_argument("--c4-max-lag", type=int, default=64, help="config 4: max snapshot lag")
+    ap.add_argument("--c4-keys", type=int, default=0, help="config 4: keys (0: txns / 10)")
     args = ap.parse_args()
     if args.ring_gb is None:
         args.ring_gb = 1.1 if args.config == 2 and not args.pmc_child else 0.0

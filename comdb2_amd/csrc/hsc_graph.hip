@@ -69,7 +69,7 @@ __global__ void k_edges_ww(uint32_t nu, const uint64_t *wkey, const uint64_t *wt
 __global__ void k_edges_reads(size_t nops, const uint32_t *txn, const uint64_t *key,
                               const uint8_t *is_write, const uint32_t *observed, uint32_t nu,
                               const uint64_t *wkey, const uint64_t *wtxn, uint64_t *ew,
-                              uint64_t *et, uint32_t *eg)
+                              uint64_t *et, uint32_t *eg, int skip_rw)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nops) return;
@@ -89,7 +89,8 @@ __global__ void k_edges_reads(size_t nops, const uint32_t *txn, const uint64_t *
             else
                 hi = mid;
         }
-        if (lo < nu && wkey[lo] == k && wtxn[lo] != r) rw = ((uint64_t)r << 32) | wtxn[lo];
+        if (!skip_rw && lo < nu && wkey[lo] == k && wtxn[lo] != r)
+            rw = ((uint64_t)r << 32) | wtxn[lo];
     }
     const size_t s = (size_t)nu + 2 * i;
     ew[s] = wr;
@@ -351,7 +352,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     if (!nw) nu = 0;
     const uint64_t *wkey = dw->as<uint64_t>(), *wtxn = dw->as<uint64_t>() + wcap;
     // 2. edges
-    const size_t ne_raw = (size_t)nu + 2 * nops;
+    const size_t ne_raw = (size_t)nu + 2 * nops + in.n_extra;
     const size_t ecap = std::max<size_t>(64, (ne_raw + 63) & ~(size_t)63);
     CK(g.ew.ensure(8 * ecap));
     CK(g.et.ensure(8 * ecap));
@@ -364,8 +365,17 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     if (nops)
         k_edges_reads<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed,
                                                    nu, wkey, wtxn, g.ew.as<uint64_t>(),
-                                                   g.et.as<uint64_t>(), g.eg.as<uint32_t>());
+                                                   g.et.as<uint64_t>(), g.eg.as<uint32_t>(),
+                                                   in.skip_rw ? 1 : 0);
     CK(hipGetLastError());
+    if (in.n_extra) {  // staged edges (rw pairs of the validator's join) after the history's
+        const size_t o = (size_t)nu + 2 * nops;
+        CK(hipMemcpyAsync(g.ew.as<uint64_t>() + o, in.x_rows, 8 * in.n_extra,
+                          hipMemcpyDeviceToDevice, s));
+        CK(hipMemcpyAsync(g.et.as<uint64_t>() + o, in.x_type, 8 * in.n_extra,
+                          hipMemcpyDeviceToDevice, s));
+        CK(hipMemsetAsync(g.eg.as<uint32_t>() + o, 0, 4 * in.n_extra, s));
+    }
     g.raw = !full;
     g.ne_raw = ne_raw;
     if (!full) {  // raw edge rows only (duplicates, ~0 holes): enough for cover / cut
@@ -375,6 +385,45 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     CK(graph_rows_csr(ne_raw, ecap, in.ntxn, g, s));
 #undef CK
     return hipSuccess;
+}
+
+__global__ void k_pairs_rows(size_t n, const uint32_t *txn, const uint64_t *lsn, uint32_t nrs,
+                             const uint32_t *rs_txn, size_t ncommit, const uint64_t *commit_lsn,
+                             const uint32_t *commit_txn, uint64_t *rows, uint64_t *type,
+                             uint32_t *bad)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t c = lsn[i];
+    size_t lo = 0, hi = ncommit;
+    while (lo < hi) {
+        const size_t mid = (lo + hi) >> 1;
+        if (commit_lsn[mid] < c)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    const uint32_t t = txn[i];
+    uint64_t row = ~0ull;
+    if (lo == ncommit || commit_lsn[lo] != c || t >= nrs) {
+        atomicOr(bad, 1u);
+    } else {
+        const uint32_t a = rs_txn[t], b = commit_txn[lo];
+        if (a != b) row = ((uint64_t)a << 32) | b;
+    }
+    rows[i] = row;
+    type[i] = kDepRW;
+}
+
+hipError_t graph_pairs_rows(size_t n, const uint32_t *txn, const uint64_t *lsn, uint32_t nrs,
+                            const uint32_t *rs_txn, size_t ncommit, const uint64_t *commit_lsn,
+                            const uint32_t *commit_txn, uint64_t *rows, uint64_t *type,
+                            uint32_t *bad, hipStream_t s)
+{
+    if (n)
+        k_pairs_rows<<<blocks(n), 256, 0, s>>>(n, txn, lsn, nrs, rs_txn, ncommit, commit_lsn,
+                                               commit_txn, rows, type, bad);
+    return hipGetLastError();
 }
 
 __global__ void k_swap_words(uint32_t m, const uint32_t *src, const uint32_t *dst, uint64_t *rows)

@@ -250,6 +250,9 @@ struct hsc_ctx {
     DBuf e_span, e_cnt, e_txn, e_lsn, e_txn2, e_lsn2, e_gid, e_scratch, e_flags, e_after;
     std::vector<uint32_t> e_out_txn;
     std::vector<uint64_t> e_out_lsn;
+    const uint32_t *e_dev_txn = nullptr;  // the last hsc_rw_edges pairs, on the device
+    const uint64_t *e_dev_lsn = nullptr;
+    size_t e_dev_n = 0;
 
     // replicant coalesce: device inputs / working arrays, host outputs
     DBuf co_dev[23];
@@ -2305,6 +2308,7 @@ int hsc_rw_edges(hsc_ctx *c, const hsc_readsets *rs, size_t *n_pairs, const uint
     const size_t n = m.n;
     c->e_out_txn.clear();
     c->e_out_lsn.clear();
+    c->e_dev_n = 0;
     *n_pairs = 0;
     *txn = nullptr;
     *writer_lsn = nullptr;
@@ -2400,6 +2404,9 @@ int hsc_rw_edges(hsc_ctx *c, const hsc_readsets *rs, size_t *n_pairs, const uint
     *n_pairs = nu;
     *txn = c->e_out_txn.data();
     *writer_lsn = c->e_out_lsn.data();
+    c->e_dev_txn = dt;
+    c->e_dev_lsn = dl;
+    c->e_dev_n = nu;
     return HSC_OK;
 }
 
@@ -2664,7 +2671,14 @@ static int graph_build_timed(hsc_ctx *c, const GraphInput &in, bool full, float 
     HIPCHK(c, hipEventCreate(&e0));
     HIPCHK(c, hipEventCreate(&e1));
     HIPCHK(c, hipEventRecord(e0, s));
-    hipError_t e = graph_build(in, gb, full, s);
+    GraphInput gi = in;
+    if (gb.n_extra) {  // staged edges join this build, once
+        gi.x_rows = gb.x_rows.as<uint64_t>();
+        gi.x_type = gb.x_type.as<uint64_t>();
+        gi.n_extra = gb.n_extra;
+        gb.n_extra = 0;
+    }
+    hipError_t e = graph_build(gi, gb, full, s);
     if (e == hipSuccess) e = hipEventRecord(e1, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e == hipSuccess) (void)hipEventElapsedTime(build_ms, e0, e1);
@@ -2677,7 +2691,8 @@ static int graph_build_timed(hsc_ctx *c, const GraphInput &in, bool full, float 
 
 // Upload a history and build its graph into c->graph (edges and CSR/CSC).
 // Caller holds c->mu.
-static int graph_upload_build(hsc_ctx *c, const hsc_history *h, bool full, float *build_ms)
+static int graph_upload_build(hsc_ctx *c, const hsc_history *h, bool full, float *build_ms,
+                              bool skip_rw = false)
 {
     if (!h || (h->nops && (!h->txn || !h->key || !h->is_write || !h->observed)) ||
         h->nops > 0x7FFFFFFFull)
@@ -2704,6 +2719,7 @@ static int graph_upload_build(hsc_ctx *c, const hsc_history *h, bool full, float
     }
     GraphInput in{gb.h_txn.as<uint32_t>(), gb.h_key.as<uint64_t>(), gb.h_isw.as<uint8_t>(),
                   gb.h_obs.as<uint32_t>(), n, h->ntxn};
+    in.skip_rw = skip_rw;
     return graph_build_timed(c, in, full, build_ms);
 }
 
@@ -2773,7 +2789,8 @@ int hsc_dep_graph_build(hsc_ctx *c, const hsc_history *h, int flags, hsc_graph_s
     if (!c || !h) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     float build_ms = 0;
-    int rc = graph_upload_build(c, h, (flags & HSC_GRAPH_FULL) != 0, &build_ms);
+    int rc = graph_upload_build(c, h, (flags & HSC_GRAPH_FULL) != 0, &build_ms,
+                                (flags & HSC_GRAPH_NO_RW) != 0);
     if (rc || !st) return rc;
     memset(st, 0, sizeof *st);
     st->build_ms = build_ms;
@@ -2791,6 +2808,7 @@ int hsc_dep_graph_build_device(hsc_ctx *c, size_t nops, uint32_t ntxn, const uin
     std::lock_guard<std::mutex> g(c->mu);
     (void)hipSetDevice(c->device);
     GraphInput in{txn_dev, key_dev, is_write_dev, observed_dev, nops, ntxn};
+    in.skip_rw = (flags & HSC_GRAPH_NO_RW) != 0;
     uint32_t bad = 0;
     HIPCHK(c, graph_check_input(in, c->graph, &bad, c->stream));
     if (bad) return fail(c, HSC_EINVAL, "history op out of range");
@@ -2800,6 +2818,80 @@ int hsc_dep_graph_build_device(hsc_ctx *c, size_t nops, uint32_t ntxn, const uin
     memset(st, 0, sizeof *st);
     st->build_ms = build_ms;
     return graph_edge_stats(c, st);
+}
+
+int hsc_dep_graph_stage_rw_pairs(hsc_ctx *c, uint32_t nrs, const uint32_t *readset_txn,
+                                 size_t ncommit, const uint64_t *commit_lsn,
+                                 const uint32_t *commit_txn)
+{
+    if (!c || (nrs && !readset_txn) || (ncommit && (!commit_lsn || !commit_txn)))
+        return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    for (size_t i = 1; i < ncommit; ++i)
+        if (commit_lsn[i] <= commit_lsn[i - 1]) return fail(c, HSC_EINVAL, "commit LSNs not sorted");
+    hipStream_t s = c->stream;
+    GraphBufs &gb = c->graph;
+    const size_t n = c->e_dev_n;
+    gb.n_extra = 0;
+    if (n == 0) return HSC_OK;
+    // mapping tables next to each other: rs_txn[nrs] | commit_txn[ncommit] | commit_lsn[ncommit]
+    const size_t o_ct = ((size_t)nrs + 1) & ~(size_t)1, o_cl = o_ct + ncommit + (ncommit & 1);
+    HIPCHK(c, gb.x_map.ensure(4 * (o_cl + 2 * ncommit) + 64));
+    uint32_t *m32 = gb.x_map.as<uint32_t>();
+    uint64_t *cl = (uint64_t *)(m32 + o_cl);
+    uint32_t *bad = m32 + o_cl + 2 * ncommit;
+    if (nrs) HIPCHK(c, hipMemcpyAsync(m32, readset_txn, 4 * (size_t)nrs, hipMemcpyHostToDevice, s));
+    if (ncommit) {
+        HIPCHK(c, hipMemcpyAsync(m32 + o_ct, commit_txn, 4 * ncommit, hipMemcpyHostToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(cl, commit_lsn, 8 * ncommit, hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(c, hipMemsetAsync(bad, 0, 4, s));
+    HIPCHK(c, gb.x_rows.ensure(8 * n));
+    HIPCHK(c, gb.x_type.ensure(8 * n));
+    HIPCHK(c, graph_pairs_rows(n, c->e_dev_txn, c->e_dev_lsn, nrs, m32, ncommit, cl, m32 + o_ct,
+                               gb.x_rows.as<uint64_t>(), gb.x_type.as<uint64_t>(), bad, s));
+    uint32_t hb = 0;
+    HIPCHK(c, hipMemcpyAsync(&hb, bad, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (hb) return fail(c, HSC_EINVAL, "rw pair names a writer LSN or read set not in the map");
+    gb.n_extra = n;
+    return HSC_OK;
+}
+
+int hsc_dep_graph_scc_built(hsc_ctx *c, uint32_t *scc_out, hsc_graph_stats *st)
+{
+    if (!c) return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    GraphBufs &gb = c->graph;
+    const uint32_t nn = c->graph_ntxn;
+    if (nn && !scc_out) return HSC_EINVAL;
+    if (gb.raw) return fail(c, HSC_ESTATE, "last build kept raw rows only (no HSC_GRAPH_FULL)");
+    hipStream_t s = c->stream;
+    hipEvent_t e1, e2;
+    HIPCHK(c, hipEventCreate(&e1));
+    HIPCHK(c, hipEventCreate(&e2));
+    HIPCHK(c, hipEventRecord(e1, s));
+    uint32_t rounds = 0, iters = 0;
+    HIPCHK(c, graph_scc(nn, gb, &rounds, &iters, s));
+    HIPCHK(c, hipEventRecord(e2, s));
+    if (nn) HIPCHK(c, hipMemcpyAsync(scc_out, gb.scc.p, 4 * (size_t)nn, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    if (st) {
+        memset(st, 0, sizeof *st);
+        (void)hipEventElapsedTime(&st->scc_ms, e1, e2);
+        const int rc = graph_edge_stats(c, st);
+        if (rc) return rc;
+        scc_size_stats(scc_out, nn, st);
+        st->rounds = rounds;
+        st->iterations = iters;
+    }
+    (void)hipEventDestroy(e1);
+    (void)hipEventDestroy(e2);
+    return HSC_OK;
 }
 
 int hsc_dep_graph_cover(hsc_ctx *c, uint8_t *cover_dev)

@@ -341,6 +341,10 @@ struct GraphInput {              // device pointers
     const uint32_t *observed;    // reads: writer txn of the observed version, ~0 initial
     size_t nops;
     uint32_t ntxn;
+    // staged extra edges (rows src << 32 | dst, type bits) merged into the build
+    const uint64_t *x_rows = nullptr, *x_type = nullptr;
+    size_t n_extra = 0;
+    bool skip_rw = false;  // reads give wr edges only (rw come from x_rows)
 };
 struct GraphBufs {
     DBuf flags, flags2, scratch, count;
@@ -350,6 +354,8 @@ struct GraphBufs {
     DBuf scc, active, color, mark, front, front2;
     DBuf h_txn, h_key, h_isw, h_obs;           // uploaded history
     DBuf diff, cut, cut_id, txn_of;            // sharded SCC: cover, cut rows, cut ids
+    DBuf x_rows, x_type, x_map;                // staged extra edges (rw pairs)
+    size_t n_extra = 0;
     size_t ne = 0;
     size_t ne_raw = 0;  // raw edge slots in ew
     bool raw = false;   // last build kept raw rows only (no sort / CSR)
@@ -359,13 +365,20 @@ struct GraphBufs {
                        &ew, &et, &eg, &ew2, &et2, &eg2, &swap_rows, &src, &out_dst, &type,
                        &in_src, &in_dst, &out_off, &in_off, &scc, &active, &color, &mark,
                        &front, &front2, &h_txn, &h_key, &h_isw, &h_obs, &diff, &cut,
-                       &cut_id, &txn_of};
+                       &cut_id, &txn_of, &x_rows, &x_type, &x_map};
         for (DBuf *b : all) b->release();
     }
 };
 // full: sorted unique edges + CSR / CSC; else raw edge rows in g.ew only.
 hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_t s);
 hipError_t graph_type_counts(GraphBufs &g, uint64_t out[3], hipStream_t s);
+// rw pairs (read set t, writer commit LSN c) -> edge rows t' -> c' of type rw:
+// t' = rs_txn[t], c' = commit_txn[i] with commit_lsn[i] == c (sorted); a pair
+// whose LSN is not listed sets *bad; self edges become ~0 rows.
+hipError_t graph_pairs_rows(size_t n, const uint32_t *txn, const uint64_t *lsn, uint32_t nrs,
+                            const uint32_t *rs_txn, size_t ncommit, const uint64_t *commit_lsn,
+                            const uint32_t *commit_txn, uint64_t *rows, uint64_t *type,
+                            uint32_t *bad, hipStream_t s);
 hipError_t graph_scc(uint32_t nnodes, GraphBufs &g, uint32_t *rounds, uint32_t *iterations,
                      hipStream_t s);
 // Compact codes of wide windows (hsc_compact.hip): per group the key bits

@@ -143,7 +143,7 @@ EXPORTS = [
     "hsc_window_delta_rows", "hsc_set_threads", "hsc_currangearrs_build",
     "hsc_currangearrs_free", "hsc_collector_create", "hsc_collector_destroy",
     "hsc_collector_check", "hsc_collector_get_stats", "hsc_harness_concurrent",
-    "hsc_dep_graph_build", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
+    "hsc_dep_graph_build", "hsc_dep_graph_stage_rw_pairs", "hsc_dep_graph_scc_built", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
 ]
 
 (LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES,
@@ -201,6 +201,8 @@ def load() -> C.CDLL:
         "hsc_dep_graph_edges": (C.c_int, [_p, _p, _p, _p, C.c_size_t, C.POINTER(C.c_size_t)]),
         "hsc_dep_graph_build": (C.c_int, [_p, C.POINTER(_History), C.c_int, C.POINTER(GraphStats)]),
         "hsc_dep_graph_cover": (C.c_int, [_p, _p]),
+        "hsc_dep_graph_stage_rw_pairs": (C.c_int, [_p, C.c_uint32, _p, C.c_size_t, _p, _p]),
+        "hsc_dep_graph_scc_built": (C.c_int, [_p, _p, C.POINTER(GraphStats)]),
         "hsc_dep_graph_build_device": (C.c_int, [_p, C.c_size_t, C.c_uint32, _p, _p, _p, _p,
                                                  C.c_int, C.POINTER(GraphStats)]),
         "hsc_dep_graph_cut": (C.c_int, [_p, _p, _p, C.c_size_t, C.POINTER(C.c_size_t)]),
@@ -725,12 +727,32 @@ class Validator:
 
     # -- sharded SCC (hsc_dep_graph_build / _cover / _cut / _scc_cut); the
     #    torch-tensor flow over ranks is comdb2_amd.shard.sharded_scc --------
-    def dep_graph_build(self, h, full: bool = False) -> dict:
+    def dep_graph_stage_rw_pairs(self, readset_txn, commit_lsn, commit_txn) -> None:
+        """The last rw_edges() pairs as rw edges of the next dep_graph_build
+        (hsc_dep_graph_stage_rw_pairs)."""
+        rt = np.ascontiguousarray(readset_txn, np.uint32)
+        cl = np.ascontiguousarray(commit_lsn, np.uint64)
+        ct = np.ascontiguousarray(commit_txn, np.uint32)
+        self._chk(self.lib.hsc_dep_graph_stage_rw_pairs(self.ctx, len(rt), rt.ctypes.data, len(cl),
+                                                        cl.ctypes.data, ct.ctypes.data),
+                  "hsc_dep_graph_stage_rw_pairs")
+
+    def dep_graph_scc_built(self, ntxn: int) -> tuple:
+        """(scc[ntxn], stats) of the last full build (hsc_dep_graph_scc_built)."""
+        out = np.zeros(max(1, ntxn), dtype=np.uint32)
+        st = GraphStats()
+        self._chk(self.lib.hsc_dep_graph_scc_built(self.ctx, out.ctypes.data, C.byref(st)),
+                  "hsc_dep_graph_scc_built")
+        return out[:ntxn], st.as_dict()
+
+    def dep_graph_build(self, h, full: bool = False, no_rw: bool = False) -> dict:
         """full: sorted unique edges + CSR (dep_graph_edges, edge stats);
-        else the raw edge rows only (all the cover / cut steps need)."""
+        else the raw edge rows only (all the cover / cut steps need).  no_rw:
+        reads give wr edges only (rw edges staged from the validator)."""
         hs, keep = self._history(h)
         st = GraphStats()
-        self._chk(self.lib.hsc_dep_graph_build(self.ctx, C.byref(hs), int(full), C.byref(st)),
+        flags = (1 if full else 0) | (2 if no_rw else 0)
+        self._chk(self.lib.hsc_dep_graph_build(self.ctx, C.byref(hs), flags, C.byref(st)),
                   "hsc_dep_graph_build")
         return st.as_dict()
 

@@ -381,6 +381,7 @@ class History:
     is_write: np.ndarray   # uint8[nops]
     observed: np.ndarray   # int64[nops]
     ntxn: int
+    snap: Optional[np.ndarray] = None  # int64[ntxn] snapshot (reads see writers < snap)
 
     @property
     def nops(self) -> int:
@@ -435,7 +436,47 @@ def config4_history(seed: int = SEED_CONFIG4, n_txn: int = 1_000_000, n_keys: in
     o_obs = np.empty(m, np.int64)
     o_txn[pos_r], o_key[pos_r], o_w[pos_r], o_obs[pos_r] = txn, key, 0, observed
     o_txn[pos_w], o_key[pos_w], o_w[pos_w], o_obs[pos_w] = txn[wi], key[wi], 1, -1
-    return History(o_txn, o_key, o_w, o_obs, n_txn)
+    return History(o_txn, o_key, o_w, o_obs, n_txn, snap)
+
+
+@dataclasses.dataclass
+class HistoryWindow:
+    """A History as the validator sees it: txn i commits
+    at LSN commit_lsn[i]; the window holds every write (int64 key value, commit
+    LSN); txn t's reads are point ranges of read set t at the snapshot LSN just
+    below commit snap[t] -- so the join's (t, writer) pairs are exactly the
+    writers a read of t did not see, the history's rw antidependencies."""
+    keys: np.ndarray        # int64[nw] window rows
+    lsn: np.ndarray         # uint64[nw]
+    readsets: ReadSets      # one read set per txn (txn order; empty without reads)
+    commit_lsn: np.ndarray  # uint64[ntxn] strictly increasing
+    end_lsn: int
+
+
+def history_window(h: History) -> HistoryWindow:
+    assert h.snap is not None, "history without snapshots"
+    commit = lsn_of_index(np.arange(h.ntxn + 1, dtype=np.uint64))
+    w = h.is_write != 0
+    keys = h.key[w].astype(np.int64)
+    lsn_w = commit[h.txn[w].astype(np.int64)]
+    r = np.nonzero(~w)[0]
+    rt = h.txn[r].astype(np.int64)
+    order = np.argsort(rt, kind="stable")
+    r, rt = r[order], rt[order]
+    nr = len(r)
+    txn_off = np.zeros(h.ntxn + 1, np.int64)
+    np.add.at(txn_off, rt + 1, 1)
+    txn_off = np.cumsum(txn_off)
+    snap_i = np.asarray(h.snap, np.int64)
+    snap = np.where(snap_i > 0, commit[np.maximum(snap_i - 1, 0)], np.uint64(0)).astype(np.uint64)
+    kb = F.enc_int64_array(h.key[r].astype(np.int64)).reshape(-1)
+    off = np.arange(nr, dtype=np.uint64) * np.uint64(9)
+    z = np.zeros(nr, np.int32)
+    rs = ReadSets(txn_off=txn_off, snap=snap, table=z.copy(), idxnum=z.copy(), lflag=z.copy(),
+                  rflag=z.copy(), islocked=z.copy(), lkeylen=np.full(nr, 9, np.int32),
+                  rkeylen=np.full(nr, 9, np.int32), lkey_off=off, rkey_off=off.copy(), keys=kb,
+                  tbnames=["t1"])
+    return HistoryWindow(keys, lsn_w, rs, commit[:h.ntxn].copy(), int(commit[h.ntxn]))
 
 
 def history_to_edn(h: History, limit: Optional[int] = None) -> str:

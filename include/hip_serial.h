@@ -488,12 +488,30 @@ int hsc_dep_graph_edges(hsc_ctx *ctx, uint32_t *src, uint32_t *dst, uint32_t *ty
  * hsc_dep_graph_edges returns, stats.edges/ww/wr/rw filled); 0 = the raw edge
  * rows only (duplicates, no sort: all cover / cut need; stats.build_ms only). */
 #define HSC_GRAPH_FULL 1
+/* HSC_GRAPH_NO_RW: reads give their wr edge only; the rw edges come from
+ * staged pairs (hsc_dep_graph_stage_rw_pairs). */
+#define HSC_GRAPH_NO_RW 2
 int hsc_dep_graph_build(hsc_ctx *ctx, const hsc_history *h, int flags, hsc_graph_stats *stats);
 /* The same from device-resident ops (observed: writer txn, 0xFFFFFFFF =
  * initial version); ops naming a txn >= ntxn -> HSC_EINVAL. */
 int hsc_dep_graph_build_device(hsc_ctx *ctx, size_t nops, uint32_t ntxn, const uint32_t *txn_dev,
                                const uint64_t *key_dev, const uint8_t *is_write_dev,
                                const uint32_t *observed_dev, int flags, hsc_graph_stats *stats);
+/* The validator's rw pairs as graph edges: the pairs of
+ * the last hsc_rw_edges call -- still on the device -- become rw edges
+ * readset_txn[t] -> commit_txn[i] (commit_lsn[i] == the writer's commit LSN;
+ * commit_lsn sorted ascending; host arrays) and join the next
+ * hsc_dep_graph_build / _build_device (merged with its own edges, type bits
+ * OR-ed; self edges dropped).  A pair whose read set or LSN is not mapped ->
+ * HSC_EINVAL.  Pairs name every writer after the snapshot, not only the next
+ * version: the extra edges t -> later writers follow the ww chain and leave
+ * the components unchanged. */
+int hsc_dep_graph_stage_rw_pairs(hsc_ctx *ctx, uint32_t nrs, const uint32_t *readset_txn,
+                                 size_t ncommit, const uint64_t *commit_lsn,
+                                 const uint32_t *commit_txn);
+/* scc_out[ntxn] of the last HSC_GRAPH_FULL build (stats as hsc_dep_graph_scc,
+ * build_ms 0). */
+int hsc_dep_graph_scc_built(hsc_ctx *ctx, uint32_t *scc_out, hsc_graph_stats *stats);
 /* cover_dev[ntxn of the last build] := 1 inside a backward edge's interval. */
 int hsc_dep_graph_cover(hsc_ctx *ctx, uint8_t *cover_dev);
 /* Edges of the last build with both ends covered, as rows src << 32 | dst

@@ -6,6 +6,7 @@ independent Python model and hand-built histories with known cycles, and the
 GPU path (-m gpu) must reproduce the oracle's edges and components exactly."""
 import numpy as np
 import pytest
+import torch  # imported before any test initialises HIP (tensors for ingest_device)
 
 from comdb2_amd.workloads import History, config4_history, history_from_edn, history_to_edn
 
@@ -137,3 +138,69 @@ def test_gpu_graph_matches_oracle(validator, oracle_mod, kw):
     np.testing.assert_array_equal(gt, t)
     np.testing.assert_array_equal(scc, oracle_mod.scc(h.ntxn, s, d))
     assert st["edges"] == len(s)
+
+
+def _cover_frac(h, s, d):
+    back = s > d
+    diff = np.zeros(h.ntxn + 1, np.int64)
+    np.add.at(diff, d[back].astype(np.int64), 1)
+    np.add.at(diff, s[back].astype(np.int64) + 1, -1)
+    return float((np.cumsum(diff)[:h.ntxn] > 0).mean())
+
+
+# high concurrency: half the txns read a snapshot up to max_lag commits old
+STRESS = [dict(n_txn=200000, n_keys=20000, concurrent_frac=0.5, max_lag=512),
+          dict(n_txn=100000, n_keys=1000, concurrent_frac=0.5, max_lag=256)]  # giant SCCs
+
+
+@pytest.mark.parametrize("kw", STRESS[:1])
+def test_stress_history_covers_most_txns(oracle_mod, kw):
+    h = config4_history(**kw)
+    s, d, _ = oracle_mod.dep_edges(h.txn, h.key, h.is_write, h.observed)
+    assert _cover_frac(h, s, d) >= 0.10
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", STRESS)
+def test_gpu_stress_graph_matches_tarjan(validator, oracle_mod, kw):
+    h = config4_history(**kw)
+    scc, st = validator.dep_graph_scc(h)
+    s, d, _ = oracle_mod.dep_edges(h.txn, h.key, h.is_write, h.observed)
+    assert _cover_frac(h, s, d) >= 0.10
+    np.testing.assert_array_equal(scc, oracle_mod.scc(h.ntxn, s, d))
+    assert st["nontrivial_sccs"] > 0
+    print(f"stress {kw}: rounds {st['rounds']} iterations {st['iterations']} "
+          f"build {st['build_ms']:.2f} ms scc {st['scc_ms']:.2f} ms")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kw", [dict(n_txn=3000, n_keys=200, concurrent_frac=0.3, max_lag=16),
+                                dict(n_txn=60000, n_keys=4000, concurrent_frac=0.5, max_lag=128)])
+def test_gpu_rw_pairs_feed_the_graph(oracle_mod, kw):
+    """the validator's (read set, writer) pairs -- every writer
+    a read did not see -- become the graph's rw edges; with the history's ww
+    and wr edges the components equal Tarjan's over the history graph."""
+    from comdb2_amd.hsc import Validator
+    from comdb2_amd.workloads import history_window, int64_words
+    h = config4_history(**kw)
+    hw = history_window(h)
+    v = Validator(0)
+    try:
+        v.register_group("t1", 0, 9)
+        dev = torch.device("cuda", 0)
+        gid = torch.zeros(len(hw.keys), dtype=torch.int32, device=dev)
+        words = torch.from_numpy(int64_words(hw.keys).reshape(-1).view(np.int64)).to(dev)
+        lsn = torch.from_numpy(hw.lsn.view(np.int64)).to(dev)
+        v.ingest_device(len(hw.keys), 2, gid.data_ptr(), words.data_ptr(), lsn.data_ptr(),
+                        hw.end_lsn)
+        torch.cuda.synchronize()
+        txn, wl = v.rw_edges(hw.readsets)
+        assert len(txn) > 0
+        v.dep_graph_stage_rw_pairs(np.arange(h.ntxn), hw.commit_lsn, np.arange(h.ntxn))
+        v.dep_graph_build(h, full=True, no_rw=True)
+        scc, st = v.dep_graph_scc_built(h.ntxn)
+        s, d, _ = oracle_mod.dep_edges(h.txn, h.key, h.is_write, h.observed)
+        np.testing.assert_array_equal(scc, oracle_mod.scc(h.ntxn, s, d))
+        assert st["nontrivial_sccs"] > 0 and st["rw"] > 0
+    finally:
+        v.close()
