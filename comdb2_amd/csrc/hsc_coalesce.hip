@@ -396,12 +396,356 @@ hipError_t co_big_sort(const CoView &v, const CoBig &bg, uint32_t maxn, hipStrea
     return hipGetLastError();
 }
 
+// ---- large sets WITH tie-with-everything ranges (glibc's exact merge tree) --
+// A NULL lower key (unlocked, not left-open) makes currange_cmp return 0
+// against every other keyed or NULL range of its index, so the order is not a
+// preorder and the result depends on glibc msort's merge tree: top-down,
+// halves n / 2 | n - n / 2, "cmp(left, right) <= 0 takes the left".  The
+// tree is replayed level by level (deepest first), every element of every
+// node placed at once, using what the comparator leaves of a merge:
+//  * runs stay sorted by the consistent part of the key, the group (table
+//    rank; locked first, locked ranges all equal; then idxnum), so a merge
+//    merges group by group;
+//  * in an unlocked group, left-open ranges (L) compare first both ways: they
+//    form each run's prefix, the left run's before the right run's;
+//  * in the group's body (keyed K, NULL N) the left wins unless both heads are
+//    K and the right key is smaller.  A right N therefore ends the merge: the
+//    rest of the left body goes first, then the right body from that N on,
+//    verbatim.  The right body before its first N (S0) is sorted (induction),
+//    so a left body element a_i leaves after P(i) = max over the left K's up
+//    to i of #S0 keys below theirs (N's: no bound) right elements -- a prefix
+//    max -- and S0 element j leaves after the left elements with P <= j.
+// Per level: N counts (exclusive scan of the N flags, to find S0's end), the
+// left bodies' bounds and their segmented prefix max (a max-scan of
+// segment start << 32 | bound), then one scatter.
+struct CoTie {
+    uint32_t *cn;     // [total + 1] N flags -> exclusive counts
+    uint64_t *pk;     // [total] segment start << 32 | bound -> prefix max
+    uint32_t *scr32;  // scan scratch
+    uint64_t *scr64;  // max-scan scratch
+};
+
+__device__ __forceinline__ uint64_t co_gkey(const CoView &v, uint32_t r)
+{
+    const uint64_t tb = (uint32_t)v.tbrank[v.table[r]];
+    if (v.w_islocked[r]) return tb << 33;
+    return tb << 33 | 1ull << 32 | (uint32_t)(v.idxnum[r] + 0x80000000u);
+}
+
+// 0 locked, 1 left-open, 2 keyed, 3 NULL lower key
+__device__ __forceinline__ int co_class(const CoView &v, uint32_t r)
+{
+    if (v.w_islocked[r]) return 0;
+    if (v.lflag[r]) return 1;
+    return v.lkey_off[r] == HSC_KEY_NULL ? 3 : 2;
+}
+
+// lower keys of two keyed rows, as currange_cmp compares them
+__device__ __forceinline__ int co_kcmp(const CoView &v, uint32_t a, uint32_t b)
+{
+    const int ka = v.lkeylen[a], kb = v.lkeylen[b];
+    const int rc = keycmp(v, v.lkey_off[a], v.lkey_off[b], ka < kb ? ka : kb);
+    return rc ? rc : ka - kb;
+}
+
+// the node of glibc's merge tree at depth d holding index i of an n-set
+__device__ __forceinline__ void co_node(uint32_t n, uint32_t i, int d, uint32_t &b, uint32_t &len)
+{
+    b = 0;
+    len = n;
+    for (int k = 0; k < d && len > 1; ++k) {
+        const uint32_t n1 = len / 2;
+        if (i < b + n1) {
+            len = n1;
+        } else {
+            b += n1;
+            len -= n1;
+        }
+    }
+}
+
+// first index in [lo, hi) of run `a` whose group key is >= g (upper: > g)
+__device__ __forceinline__ uint32_t co_gbound(const CoView &v, const uint32_t *a, uint32_t lo,
+                                              uint32_t hi, uint64_t g, bool upper)
+{
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint64_t x = co_gkey(v, a[mid]);
+        if (x < g || (upper && x == g))
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// end of the left-open prefix of a group part [lo, hi)
+__device__ __forceinline__ uint32_t co_lend(const CoView &v, const uint32_t *a, uint32_t lo,
+                                            uint32_t hi)
+{
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (co_class(v, a[mid]) == 1)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// Geometry of one element's merge at depth d (indices within the set).
+struct CoTieAt {
+    uint32_t b, n1, len;  // node [b, b + len), left child [b, b + n1)
+    bool left;
+};
+
+__device__ __forceinline__ bool co_tie_at(uint32_t n, uint32_t i, int d, CoTieAt &m)
+{
+    co_node(n, i, d, m.b, m.len);
+    if (m.len < 2) return false;
+    m.n1 = m.len / 2;
+    m.left = i < m.b + m.n1;
+    return true;
+}
+
+// S0 = [body start, first N) of the group part [gs, ge) of the right run;
+// cn = exclusive N counts of the set (dense, index = set index)
+__device__ __forceinline__ uint32_t co_s0_end(const uint32_t *cn, uint32_t bs, uint32_t ge)
+{
+    const uint32_t c0 = cn[bs];
+    uint32_t lo = bs, hi = ge;  // first k in [bs, ge) with cn[k + 1] > c0
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (cn[mid + 1] > c0)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_tie_nflags(CoView v, CoBig bg, const uint32_t *src,
+                                                    uint32_t *cn)
+{
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g > bg.total) return;
+    if (g == bg.total) {
+        cn[g] = 0;
+        return;
+    }
+    const uint32_t k = co_big_of(bg, g), t = bg.set[k];
+    const uint32_t i = g - bg.pre[k];
+    cn[g] = i < v.count[t] && co_class(v, src[(uint64_t)v.off[t] + i]) == 3;
+}
+
+// left body elements: segment start << 32 | #S0 keys below theirs
+__global__ __launch_bounds__(256) void k_tie_bounds(CoView v, CoBig bg, int d, const uint32_t *src,
+                                                    const uint32_t *cn, uint64_t *pk)
+{
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= bg.total) return;
+    const uint32_t k = co_big_of(bg, g), t = bg.set[k];
+    const uint32_t i = g - bg.pre[k], n = v.count[t];  // the set's live ranges
+    const uint32_t *a = src + v.off[t];
+    const uint32_t *cs = cn + bg.pre[k];
+    uint64_t key = (uint64_t)g << 32;  // not a left body element: its own segment
+    if (i >= n) {
+        pk[g] = key;
+        return;
+    }
+    CoTieAt m;
+    const uint32_t x = a[i];
+    const int cl = co_class(v, x);
+    if (co_tie_at(n, i, d, m) && m.left && cl >= 2) {
+        const uint64_t gk = co_gkey(v, x);
+        const uint32_t ag = co_gbound(v, a, m.b, i, gk, false);  // x's group part ends past x
+        const uint32_t abody = co_lend(v, a, ag, i);
+        uint32_t lb = 0;
+        if (cl == 2) {
+            const uint32_t r0 = m.b + m.n1, r1 = m.b + m.len;
+            const uint32_t bgs = co_gbound(v, a, r0, r1, gk, false);
+            const uint32_t bge = co_gbound(v, a, bgs, r1, gk, true);
+            const uint32_t bs = co_lend(v, a, bgs, bge);
+            const uint32_t s0 = co_s0_end(cs, bs, bge);
+            uint32_t lo = bs, hi = s0;  // S0 keys < x's
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (co_kcmp(v, a[mid], x) < 0)
+                    lo = mid + 1;
+                else
+                    hi = mid;
+            }
+            lb = lo - bs;
+        }
+        key = (uint64_t)(bg.pre[k] + abody) << 32 | lb;
+    }
+    pk[g] = key;
+}
+
+__global__ __launch_bounds__(256) void k_tie_place(CoView v, CoBig bg, int d, const uint32_t *src,
+                                                   uint32_t *dst, const uint32_t *cn,
+                                                   const uint64_t *pk)
+{
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= bg.total) return;
+    const uint32_t k = co_big_of(bg, g), t = bg.set[k];
+    const uint32_t i = g - bg.pre[k], n = v.count[t];
+    if (i >= n) return;
+    const uint64_t base = (uint64_t)v.off[t];
+    const uint32_t *a = src + base;
+    const uint32_t x = a[i];
+    CoTieAt m;
+    if (!co_tie_at(n, i, d, m)) {
+        dst[base + i] = x;
+        return;
+    }
+    const uint32_t *cs = cn + bg.pre[k];
+    const uint64_t *ps = pk + bg.pre[k];
+    const uint64_t gk = co_gkey(v, x);
+    const int cl = co_class(v, x);
+    const uint32_t l0 = m.b, l1 = m.b + m.n1, r0 = l1, r1 = m.b + m.len;
+    uint32_t pos;
+    if (m.left) {
+        const uint32_t bgs = co_gbound(v, a, r0, r1, gk, false);
+        uint32_t before = bgs - r0;  // right elements of lower groups
+        if (cl >= 2) {
+            const uint32_t bge = co_gbound(v, a, bgs, r1, gk, true);
+            before += co_lend(v, a, bgs, bge) - bgs + (uint32_t)ps[i];
+        }
+        pos = i + before;
+    } else {
+        const uint32_t ags = co_gbound(v, a, l0, l1, gk, false);
+        uint32_t before = ags - l0;  // left elements of lower groups
+        const uint32_t age = co_gbound(v, a, ags, l1, gk, true);
+        if (cl == 0) {
+            before += age - ags;  // locked: the left part first
+        } else {
+            const uint32_t abody = co_lend(v, a, ags, age);
+            before += abody - ags;  // left-open left ranges first
+            if (cl >= 2) {
+                const uint32_t bgs = co_gbound(v, a, r0, r1, gk, false);
+                const uint32_t bge = co_gbound(v, a, bgs, r1, gk, true);
+                const uint32_t bs = co_lend(v, a, bgs, bge);
+                const uint32_t s0 = co_s0_end(cs, bs, bge);
+                if (i < s0) {  // left body elements with P <= j (P rises along the body)
+                    const uint32_t j = i - bs;
+                    uint32_t lo = abody, hi = age;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if ((uint32_t)ps[mid] <= j)
+                            lo = mid + 1;
+                        else
+                            hi = mid;
+                    }
+                    before += lo - abody;
+                } else {
+                    before += age - abody;  // from the first right N on: after the left body
+                }
+            }
+        }
+        pos = l0 + before + (i - r0);
+    }
+    dst[base + pos] = x;
+}
+
+// inclusive max-scan of u64, in place (tiles, tile maxima recursively)
+constexpr int kMaxScanT = 256, kMaxScanI = 4, kMaxScanTile = kMaxScanT * kMaxScanI;
+
+__global__ __launch_bounds__(kMaxScanT) void k_maxscan_tile(uint64_t *a, size_t n, uint64_t *sums)
+{
+    __shared__ uint64_t lds[kMaxScanT / 64];
+    const size_t base = (size_t)blockIdx.x * kMaxScanTile + (size_t)threadIdx.x * kMaxScanI;
+    uint64_t v[kMaxScanI], m = 0;
+#pragma unroll
+    for (int q = 0; q < kMaxScanI; ++q) {
+        v[q] = base + q < n ? a[base + q] : 0;
+        m = v[q] > m ? v[q] : m;
+        v[q] = m;
+    }
+    // exclusive max over the threads before this one
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    uint64_t x = m;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x = y > x ? y : x;
+    }
+    if (lane == 63) lds[wid] = x;
+    __syncthreads();
+    uint64_t pre = 0;
+    for (int w = 0; w < wid; ++w) pre = lds[w] > pre ? lds[w] : pre;
+    const uint64_t up = __shfl_up(x, 1, 64);
+    if (lane > 0) pre = up > pre ? up : pre;
+#pragma unroll
+    for (int q = 0; q < kMaxScanI; ++q)
+        if (base + q < n) a[base + q] = v[q] > pre ? v[q] : pre;
+    if (threadIdx.x == 0 && sums) {
+        uint64_t tot = 0;
+        for (int w = 0; w < kMaxScanT / 64; ++w) tot = lds[w] > tot ? lds[w] : tot;
+        sums[blockIdx.x] = tot;
+    }
+}
+
+__global__ __launch_bounds__(kMaxScanT) void k_maxscan_add(uint64_t *a, size_t n, const uint64_t *sums)
+{
+    if (blockIdx.x == 0) return;
+    const uint64_t add = sums[blockIdx.x - 1];  // inclusive max of the tiles before
+    const size_t base = (size_t)blockIdx.x * kMaxScanTile;
+    for (int q = threadIdx.x; q < kMaxScanTile; q += kMaxScanT)
+        if (base + q < n && a[base + q] < add) a[base + q] = add;
+}
+
+hipError_t maxscan_u64(uint64_t *a, size_t n, uint64_t *scratch, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    const size_t nb = (n + kMaxScanTile - 1) / kMaxScanTile;
+    k_maxscan_tile<<<(unsigned)nb, kMaxScanT, 0, s>>>(a, n, nb > 1 ? scratch : nullptr);
+    if (nb == 1) return hipGetLastError();
+    hipError_t e = maxscan_u64(scratch, nb, scratch + nb, s);
+    if (e != hipSuccess) return e;
+    k_maxscan_add<<<(unsigned)nb, kMaxScanT, 0, s>>>(a, n, scratch);
+    return hipGetLastError();
+}
+
+hipError_t co_tie_sort(const CoView &v, const CoBig &bg, uint32_t maxn, const CoTie &tw,
+                       hipStream_t s)
+{
+    int depth = 0;
+    while ((1u << depth) < maxn) ++depth;
+    const uint32_t nb = (bg.total + 255) / 256;
+    bool in_tmp = false;
+    for (int d = depth - 1; d >= 0; --d) {
+        const uint32_t *src = in_tmp ? v.tmp : v.ord;
+        uint32_t *dst = in_tmp ? v.ord : v.tmp;
+        k_tie_nflags<<<(bg.total + 256) / 256, 256, 0, s>>>(v, bg, src, tw.cn);
+        hipError_t e = scan_exclusive_u32(tw.cn, (size_t)bg.total + 1, tw.scr32, s);
+        if (e != hipSuccess) return e;
+        k_tie_bounds<<<nb, 256, 0, s>>>(v, bg, d, src, tw.cn, tw.pk);
+        if ((e = maxscan_u64(tw.pk, bg.total, tw.scr64, s)) != hipSuccess) return e;
+        k_tie_place<<<nb, 256, 0, s>>>(v, bg, d, src, dst, tw.cn, tw.pk);
+        in_tmp = !in_tmp;
+    }
+    if (in_tmp) k_co_big_copy<<<nb, 256, 0, s>>>(v, bg);
+    return hipGetLastError();
+}
+
 }  // namespace
+
+size_t coalesce_tie_scratch_bytes(uint32_t total)
+{
+    size_t m = 0, n = total;  // max-scan tile maxima, recursively
+    while (n > (size_t)kMaxScanTile) {
+        n = (n + kMaxScanTile - 1) / kMaxScanTile;
+        m += n;
+    }
+    return 4 * ((size_t)total + 2) + 8 * (size_t)total + scan_scratch_bytes((size_t)total + 1) +
+           8 * (m + 8) + 256;
+}
 
 hipError_t launch_coalesce(const CoView &v, const uint32_t *isbig, const uint32_t *big_set,
                            const uint32_t *big_pre, uint32_t nbig, uint32_t big_total,
                            uint32_t big_maxn, uint32_t *big_runpos, uint32_t *big_scratch,
-                           hipStream_t s)
+                           void *tie_scratch, hipStream_t s)
 {
     if (v.ntxn <= 0) return hipSuccess;
     k_coalesce<<<(v.ntxn + 127) / 128, 128, 0, s>>>(v, nbig ? isbig : nullptr);
@@ -410,8 +754,24 @@ hipError_t launch_coalesce(const CoView &v, const uint32_t *isbig, const uint32_
     const CoBig bg{big_set, big_pre, nbig, big_total};
     const uint32_t nb = (big_total + 255) / 256;
     k_co_big_init<<<nb, 256, 0, s>>>(v, bg);
+    CoTie tw{};
+    if (tie_scratch) {  // some set has NULL lower keys: glibc's merge tree, exactly
+        uint8_t *p = (uint8_t *)tie_scratch;
+        tw.pk = (uint64_t *)p;
+        p += 8 * (size_t)big_total;
+        tw.cn = (uint32_t *)p;
+        p += 4 * ((size_t)big_total + 2);
+        tw.scr64 = (uint64_t *)(((uintptr_t)p + 7) & ~(uintptr_t)7);
+        size_t m = 0, n = big_total;
+        while (n > (size_t)kMaxScanTile) {
+            n = (n + kMaxScanTile - 1) / kMaxScanTile;
+            m += n;
+        }
+        tw.scr32 = (uint32_t *)(tw.scr64 + m + 8);
+    }
     for (int pass = 0; pass < 2; ++pass) {
-        if ((e = co_big_sort(v, bg, big_maxn, s)) != hipSuccess) return e;
+        e = tie_scratch ? co_tie_sort(v, bg, big_maxn, tw, s) : co_big_sort(v, bg, big_maxn, s);
+        if (e != hipSuccess) return e;
         k_co_big_runs<<<nb, 256, 0, s>>>(v, bg);
         k_co_big_join<<<nbig, kJoinT, 0, s>>>(v, bg, big_runpos, big_scratch);
     }

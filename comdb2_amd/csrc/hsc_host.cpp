@@ -255,7 +255,7 @@ struct hsc_ctx {
     size_t e_dev_n = 0;
 
     // replicant coalesce: device inputs / working arrays, host outputs
-    DBuf co_dev[23];
+    DBuf co_dev[24];
     std::vector<int64_t> co_off;
     std::vector<int32_t> co_i32[7];
     std::vector<uint64_t> co_u64[2];
@@ -2470,18 +2470,22 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
     v.w_rkeylen = d[14].as<int32_t>(), v.w_rkey_off = d[15].as<uint64_t>();
     v.ord = d[16].as<uint32_t>(), v.tmp = d[16].as<uint32_t>() + n1;
     v.count = d[17].as<uint32_t>();
-    // large sets without a tie-with-everything range (see hsc_coalesce.hip)
+    // large sets take the level-parallel sort (see hsc_coalesce.hip); one with a
+    // tie-with-everything range (NULL lower key) replays glibc's merge tree
     std::vector<uint32_t> isbig((size_t)std::max(T, 1), 0), bset, bpre(1, 0);
     uint32_t bmax = 0;
+    bool ties = false;
     if (!getenv("HSC_CO_SERIAL")) {  // test knob: every set on the per-thread path
         for (int t = 0; t < T; ++t) {
             const size_t b = (size_t)rs->txn_off[t], e = (size_t)rs->txn_off[t + 1];
             if (e - b < kCoBig || bpre.back() + (e - b) > 0xFFFFFFFFull) continue;
-            bool ok = true;
-            for (size_t r = b; r < e && ok; ++r)  // no tie-with-everything range; locks open
-                ok = (rs->islocked[r] || rs->lflag[r] || rs->lkey_off[r] != HSC_KEY_NULL) &&
-                     (!rs->islocked[r] || (rs->lflag[r] && rs->rflag[r]));
+            bool ok = true, tie = false;
+            for (size_t r = b; r < e && ok; ++r) {  // locked ranges open at both ends
+                ok = !rs->islocked[r] || (rs->lflag[r] && rs->rflag[r]);
+                tie |= !rs->islocked[r] && !rs->lflag[r] && rs->lkey_off[r] == HSC_KEY_NULL;
+            }
             if (!ok) continue;
+            ties |= tie;
             isbig[t] = 1;
             bset.push_back((uint32_t)t);
             bpre.push_back(bpre.back() + (uint32_t)(e - b));
@@ -2499,8 +2503,10 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
         HIPCHK(c, hipMemcpyAsync(d[19].p, bset.data(), 4 * (size_t)nbig, hipMemcpyHostToDevice, s));
         HIPCHK(c, hipMemcpyAsync(d[20].p, bpre.data(), 4 * ((size_t)nbig + 1), hipMemcpyHostToDevice, s));
     }
+    if (ties) HIPCHK(c, d[23].ensure(coalesce_tie_scratch_bytes(bpre.back())));
     HIPCHK(c, launch_coalesce(v, d[18].as<uint32_t>(), d[19].as<uint32_t>(), d[20].as<uint32_t>(),
-                              nbig, bpre.back(), bmax, d[21].as<uint32_t>(), d[22].as<uint32_t>(), s));
+                              nbig, bpre.back(), bmax, d[21].as<uint32_t>(), d[22].as<uint32_t>(),
+                              ties ? d[23].p : nullptr, s));
     std::vector<uint32_t> cnt(T), ord(nr);
     std::vector<int32_t> wrf(nr), wlk(nr), wrl(nr);
     std::vector<uint64_t> wro(nr);

@@ -309,10 +309,13 @@ struct CoView {
 // isbig[t] != 0: set t (one of big_set[0 .. nbig), elements big_pre[k] ..
 // big_pre[k + 1], at most big_maxn per set) takes the level-parallel sort.
 constexpr uint32_t kCoBig = 256;
+// tie_scratch (coalesce_tie_scratch_bytes(big_total), NULL if no big set has a
+// NULL lower key): the big sets sort on glibc's exact merge tree instead.
+size_t coalesce_tie_scratch_bytes(uint32_t total);
 hipError_t launch_coalesce(const CoView &v, const uint32_t *isbig, const uint32_t *big_set,
                            const uint32_t *big_pre, uint32_t nbig, uint32_t big_total,
-                           uint32_t big_maxn, uint32_t *big_runpos /* [nranges] */,
-                           uint32_t *big_scratch /* [2 nranges] */, hipStream_t s);
+                           uint32_t big_maxn, uint32_t *big_runpos, uint32_t *big_scratch,
+                           void *tie_scratch, hipStream_t s);
 
 // Narrow tiles keep the chunk histogram tile-major: hist[t * hist_stride(G) + g].
 __host__ __device__ inline uint32_t hist_stride(uint32_t G) { return (G + 7) & ~7u; }

@@ -169,3 +169,139 @@ def test_wire_decode_keeps_key_presence():
     assert int(d.lkey_off[0]) != KEY_NULL and int(d.lkeylen[0]) == 0
     assert int(d.lkey_off[1]) == KEY_NULL and int(d.rkey_off[1]) != KEY_NULL
     assert int(d.lkey_off[2]) == KEY_NULL and int(d.rkey_off[2]) == KEY_NULL
+
+
+# ---- the GPU's level-parallel replay of glibc's merge tree with ties -------
+# (hsc_coalesce.hip, k_tie_bounds / k_tie_place), restated element by element
+# in Python and checked against the model's sequential msort on sets full of
+# NULL lower keys, left-open ranges and locked ranges.
+
+def _tie_sort(m, a):
+    import bisect
+    n = len(a)
+
+    def gkey(x):
+        tb = x.tbname
+        return (tb, 0, 0) if x.islocked else (tb, 1, x.idxnum)
+
+    def cls(x):
+        return 0 if x.islocked else 1 if x.lflag else 3 if x.lkey is None else 2
+
+    def kcmp(x, y):
+        rc = m.memcmp(x.lkey, y.lkey, min(x.lkeylen, y.lkeylen))
+        return rc if rc else x.lkeylen - y.lkeylen
+
+    def node(i, d):
+        b, ln = 0, n
+        for _ in range(d):
+            if ln <= 1:
+                break
+            n1 = ln // 2
+            if i < b + n1:
+                ln = n1
+            else:
+                b, ln = b + n1, ln - n1
+        return b, ln
+
+    def gbound(src, lo, hi, g, upper):
+        while lo < hi:
+            mid = (lo + hi) // 2
+            x = gkey(src[mid])
+            if x < g or (upper and x == g):
+                lo = mid + 1
+            else:
+                hi = mid
+        return lo
+
+    def lend(src, lo, hi):
+        while lo < hi and cls(src[lo]) == 1:
+            lo += 1
+        return lo
+
+    def s0_end(src, bs, ge):
+        k = bs
+        while k < ge and cls(src[k]) != 3:
+            k += 1
+        return k
+
+    depth = 0
+    while (1 << depth) < n:
+        depth += 1
+    src = list(a)
+    for d in range(depth - 1, -1, -1):
+        P = [0] * n
+        for i in range(n):  # k_tie_bounds + the segmented prefix max
+            b, ln = node(i, d)
+            if ln < 2 or i >= b + ln // 2 or cls(src[i]) < 2:
+                continue
+            n1 = ln // 2
+            g = gkey(src[i])
+            ag = gbound(src, b, b + n1, g, False)
+            abody = lend(src, ag, b + n1)
+            lb = 0
+            if cls(src[i]) == 2:
+                bgs = gbound(src, b + n1, b + ln, g, False)
+                bge = gbound(src, bgs, b + ln, g, True)
+                bs = lend(src, bgs, bge)
+                s0 = s0_end(src, bs, bge)
+                lb = sum(1 for j in range(bs, s0) if kcmp(src[j], src[i]) < 0)
+            P[i] = max(lb, P[i - 1]) if i > abody else lb  # prefix max over the left body
+        dst = [None] * n
+        for i in range(n):  # k_tie_place
+            b, ln = node(i, d)
+            x = src[i]
+            if ln < 2:
+                dst[i] = x
+                continue
+            n1 = ln // 2
+            g, c = gkey(x), cls(x)
+            l0, l1, r0, r1 = b, b + n1, b + n1, b + ln
+            if i < l1:
+                bgs = gbound(src, r0, r1, g, False)
+                before = bgs - r0
+                if c >= 2:
+                    bge = gbound(src, bgs, r1, g, True)
+                    before += lend(src, bgs, bge) - bgs + P[i]
+                pos = i + before
+            else:
+                ags = gbound(src, l0, l1, g, False)
+                age = gbound(src, ags, l1, g, True)
+                before = ags - l0
+                if c == 0:
+                    before += age - ags
+                else:
+                    abody = lend(src, ags, age)
+                    before += abody - ags
+                    if c >= 2:
+                        bgs = gbound(src, r0, r1, g, False)
+                        bge = gbound(src, bgs, r1, g, True)
+                        bs = lend(src, bgs, bge)
+                        s0 = s0_end(src, bs, bge)
+                        if i < s0:  # P rises along the left body
+                            before += bisect.bisect_right(P, i - bs, abody, age) - abody
+                        else:
+                            before += age - abody
+                pos = l0 + before + (i - r0)
+            assert dst[pos] is None
+            dst[pos] = x
+        src = dst
+    return src
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_tie_merge_tree_replay_equals_msort(seed):
+    from coalesce_model import CR, Model
+    rng = np.random.default_rng(seed)
+    buf = bytes(rng.integers(0, 4, size=4000).astype(np.uint8))
+    m = Model(buf)
+    n = int(rng.integers(2, 90))
+    a = []
+    for _ in range(n):
+        lk = None if rng.random() < 0.3 else int(rng.integers(0, 3900))
+        a.append(CR(tbname=f"t{int(rng.integers(0, 2))}", idxnum=int(rng.integers(0, 2)),
+                    lflag=int(rng.random() < 0.15), rflag=0, islocked=int(rng.random() < 0.1),
+                    lkey=lk, lkeylen=0 if lk is None else int(rng.integers(0, 4)),
+                    rkey=None, rkeylen=0))
+    want = m.msort(a)
+    got = _tie_sort(m, a)
+    assert [id(x) for x in got] == [id(x) for x in want]

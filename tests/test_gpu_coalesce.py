@@ -31,12 +31,15 @@ def test_gpu_coalesce_matches_oracle(validator, oracle_mod, seed, ntxn, maxr):
     (13, 8, 300, 2000, 0.002, 3),    # some sets hold a tie-with-everything (NULL) lower key
     (14, 1, 60000, 60001, 0.0, 3),   # one deep set (16 merge levels)
     (15, 4, 3000, 9000, 0.0, 60),  # ~180 (table, index) runs per set, many locked tables
+    (16, 4, 2000, 8000, 0.05, 3),    # NULL lower keys everywhere: glibc's merge tree replayed
+    (17, 1, 60000, 60001, 0.03, 3),  # one deep set with ties (16 levels)
+    (18, 3, 5000, 9000, 0.3, 2),     # ties dominate
 ])
-def test_gpu_coalesce_large_consistent_sets(validator, oracle_mod, monkeypatch, seed, ntxn, lo, hi,
-                                            null_lo, ntables):
-    """Large sets whose comparator is a consistent order (present empty lower
-    keys included) take the level-parallel sort (hsc_coalesce.hip, CoBig): equal to the oracle and to
-    the per-thread glibc-msort path (HSC_CO_SERIAL)."""
+def test_gpu_coalesce_large_sets(validator, oracle_mod, monkeypatch, seed, ntxn, lo, hi, null_lo,
+                                 ntables):
+    """Large sets take the level-parallel sort (hsc_coalesce.hip, CoBig; with
+    NULL lower keys the replay of glibc's merge tree, CoTie): equal to the
+    oracle and to the per-thread glibc-msort path (HSC_CO_SERIAL)."""
     rs = random_readsets(seed, ntxn=ntxn, max_ranges=hi, min_ranges=lo, null_lo=null_lo,
                          tables=tuple(f"t{i:02d}" for i in range(ntables)))
     want = oracle_mod.coalesce(rs)
