@@ -321,6 +321,266 @@ __global__ __launch_bounds__(256) void k_co_big_runs(CoView v, CoBig bg)
     v.tmp[b + i] = info;
 }
 
+// ---- the merge scan of long runs, chunk-parallel ----
+// co_merge is a state machine over a run (the open survivor p absorbs q or q
+// opens a new survivor), so it splits into chunks: each chunk is scanned as if
+// a survivor opened at its first row (k_run_local: survivors' final fields
+// kept aside, nothing written back), then one thread per run carries the true
+// state across its chunk boundaries (k_run_stitch): from a boundary it steps
+// the true machine until a row opens a survivor in both the true and the
+// chunk-local scan -- from there both are in the same state and the local
+// result stands -- and jumps to the next boundary with the chunk's last local
+// survivor as the open one.  Survivors' fields are applied and each run's
+// survivors packed to its head by one workgroup per set (k_run_pack), in the
+// layout k_co_big_join takes.  (The right-key swap's write into an absorbed
+// row is not repeated: absorbed rows leave the output.)
+constexpr uint32_t kRunChunk = 128;
+constexpr uint32_t kFlStart = 1u << 31, kFlRf = 1u << 30, kFlLk = 1u << 29, kFlHead = 1u << 28;
+constexpr uint32_t kFlRl = (1u << 28) - 1;
+
+struct CoRuns {
+    uint64_t *s_ro;   // [total] survivor's right key offset (at its first row)
+    uint32_t *s_fl;   // [total] start | rf | lk | run head | rkeylen
+    uint32_t *lastS;  // [nchunks] dense index of the chunk's last local survivor
+    uint8_t *hashead; // [nchunks] the chunk holds a run head
+};
+
+__device__ __forceinline__ uint32_t co_fl(const CoRow &p, bool head)
+{
+    return kFlStart | (p.rf ? kFlRf : 0) | (p.lk ? kFlLk : 0) | (head ? kFlHead : 0) |
+           ((uint32_t)p.rl & kFlRl);
+}
+
+// one step of currangearr_merge_neighbor inside a run: true = q absorbed into p
+__device__ __forceinline__ bool co_step(const CoView &v, CoRow &p, const CoRow &q)
+{
+    const int m = q.lkl < p.rl ? q.lkl : p.rl;
+    if (!(q.lf || p.rf || keycmp(v, q.lko, p.ro, m) <= 0)) return false;
+    if (p.rf || q.rf) {
+        p.rf = 1;
+        p.ro = HSC_KEY_NULL;
+        p.rl = 0;
+    } else if (keycmp(v, p.ro, q.ro, p.rl < q.rl ? p.rl : q.rl) < 0) {
+        p.ro = q.ro;
+    }
+    if (p.lf && p.rf) p.lk = 1;
+    return true;
+}
+
+__global__ __launch_bounds__(64) void k_run_local(CoView v, CoBig bg, CoRuns cr)
+{
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t g0 = c * kRunChunk;
+    if (g0 >= bg.total) return;
+    const uint32_t g1 = min(g0 + kRunChunk, bg.total);
+    uint32_t k = co_big_of(bg, g0);
+    CoRow p{};
+    uint32_t sp = ~0u;
+    bool sp_head = false, any_head = false;
+    uint64_t prev_key = 0;
+    uint32_t last = ~0u;
+    for (uint32_t g = g0; g < g1; ++g) {
+        while (g >= bg.pre[k + 1]) ++k;
+        const uint32_t t = bg.set[k], i = g - bg.pre[k];
+        const uint64_t b = (uint64_t)v.off[t];
+        if (i >= v.count[t]) {  // dead row (second pass): closes the open survivor
+            if (sp != ~0u) {
+                cr.s_fl[sp] = co_fl(p, sp_head);
+                cr.s_ro[sp] = p.ro;
+                sp = ~0u;
+            }
+            cr.s_fl[g] = 0;
+            continue;
+        }
+        const uint32_t r = v.ord[b + i];
+        const uint64_t rk = co_runkey(v, r);
+        if (g == g0 || i == 0) prev_key = i ? co_runkey(v, v.ord[b + i - 1]) : ~rk;
+        const bool head = i == 0 || rk != prev_key;
+        prev_key = rk;
+        any_head |= head;
+        const CoRow q = co_row(v, r);
+        if (sp != ~0u && !head && co_step(v, p, q)) {
+            cr.s_fl[g] = 0;
+            continue;
+        }
+        if (sp != ~0u) {
+            cr.s_fl[sp] = co_fl(p, sp_head);
+            cr.s_ro[sp] = p.ro;
+        }
+        p = q;
+        sp = g;
+        sp_head = head;
+        last = g;
+        cr.s_fl[g] = head ? kFlHead : 0;  // the start bit comes with the final fields
+    }
+    if (sp != ~0u) {
+        cr.s_fl[sp] = co_fl(p, sp_head);
+        cr.s_ro[sp] = p.ro;
+    }
+    cr.lastS[c] = last;
+    cr.hashead[c] = any_head;
+}
+
+// the open survivor at dense index sp, fields as the scan left them
+__device__ __forceinline__ CoRow co_open(const CoView &v, const CoBig &bg, const CoRuns &cr,
+                                        uint32_t k, uint32_t sp)
+{
+    const uint32_t t = bg.set[k];
+    CoRow p = co_row(v, v.ord[(uint64_t)v.off[t] + (sp - bg.pre[k])]);
+    const uint32_t fl = cr.s_fl[sp];
+    p.rf = (fl & kFlRf) != 0;
+    p.lk = (fl & kFlLk) != 0;
+    p.rl = (int)(fl & kFlRl);
+    p.ro = cr.s_ro[sp];
+    return p;
+}
+
+__global__ __launch_bounds__(64) void k_run_stitch(CoView v, CoBig bg, CoRuns cr)
+{
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x + 1;  // boundaries g = c * C
+    uint32_t g = c * kRunChunk;
+    if (g >= bg.total) return;
+    uint32_t k = co_big_of(bg, g);
+    uint32_t t = bg.set[k];
+    if (g - bg.pre[k] >= v.count[t] || (cr.s_fl[g] & kFlHead)) return;  // dead, or a run starts here
+    if (!cr.hashead[c - 1]) return;  // the run began in an earlier chunk: its thread walks on
+    uint32_t sp = cr.lastS[c - 1];
+    CoRow p = co_open(v, bg, cr, k, sp);
+    uint32_t sp_fl_head = cr.s_fl[sp] & kFlHead;
+    for (;;) {
+        // step the true machine from g until a shared survivor start (resync)
+        bool resync = false;
+        for (;;) {
+            const uint32_t i = g - bg.pre[k];
+            if (g >= bg.pre[k + 1] || i >= v.count[t] || (cr.s_fl[g] & kFlHead)) break;  // run ends
+            const uint32_t fl = cr.s_fl[g];
+            const CoRow q = co_row(v, v.ord[(uint64_t)v.off[t] + i]);
+            if (co_step(v, p, q)) {
+                if (fl & kFlStart) cr.s_fl[g] = 0;  // the local scan opened a survivor here
+                ++g;
+                continue;
+            }
+            cr.s_fl[sp] = co_fl(p, sp_fl_head != 0);
+            cr.s_ro[sp] = p.ro;
+            if (fl & kFlStart) {  // both scans open a survivor at g: the local rest stands
+                resync = true;
+                break;
+            }
+            p = q;
+            sp = g;
+            sp_fl_head = 0;
+            cr.s_fl[g] = kFlStart;  // fields follow when it closes
+            ++g;
+        }
+        if (!resync) {
+            cr.s_fl[sp] = co_fl(p, sp_fl_head != 0);
+            cr.s_ro[sp] = p.ro;
+            return;
+        }
+        // jump to the next chunk boundary of this run, the chunk's last survivor open
+        const uint32_t ch = g / kRunChunk;
+        g = (ch + 1) * kRunChunk;
+        if (g >= bg.pre[k + 1] || g - bg.pre[k] >= v.count[t] || (cr.s_fl[g] & kFlHead)) return;
+        sp = cr.lastS[ch];
+        p = co_open(v, bg, cr, k, sp);
+        sp_fl_head = cr.s_fl[sp] & kFlHead;
+    }
+}
+
+// inclusive max-scan of u32 over a block (NT threads)
+template <int NT>
+__device__ __forceinline__ uint32_t block_incl_max(uint32_t x, uint32_t *lds)
+{
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x = y > x ? y : x;
+    }
+    if (lane == 63) lds[wid] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int w = 0; w < wid; ++w) pre = lds[w] > pre ? lds[w] : pre;
+    __syncthreads();
+    return x > pre ? x : pre;
+}
+
+constexpr int kPackT = 256;
+
+__global__ __launch_bounds__(kPackT) void k_run_pack(CoView v, CoBig bg, CoRuns cr)
+{
+    __shared__ uint32_t lds[kPackT / 64];
+    __shared__ uint32_t lds2[kPackT / 64];
+    __shared__ uint32_t s_lk[kPackT];
+    __shared__ uint32_t carry_head, carry_cnt, carry_lk;
+    const uint32_t k = blockIdx.x, t = bg.set[k];
+    const uint32_t n = v.count[t], pre = bg.pre[k];
+    const uint64_t b = (uint64_t)v.off[t];
+    if (threadIdx.x == 0) {
+        carry_head = 0;
+        carry_cnt = 0;
+        carry_lk = 0;
+    }
+    __syncthreads();
+    for (uint32_t c0 = 0; c0 < n; c0 += kPackT) {
+        const uint32_t i = c0 + threadIdx.x;
+        const bool live = i < n;
+        const uint32_t fl = live ? cr.s_fl[pre + i] : 0;
+        const bool start = (fl & kFlStart) != 0, head = live && (fl & kFlHead);
+        const uint32_t r = live ? v.ord[b + i] : 0;
+        if (start) {  // the survivor's final fields (co_put)
+            v.w_rflag[r] = (fl & kFlRf) != 0;
+            v.w_islocked[r] = (fl & kFlLk) != 0;
+            v.w_rkeylen[r] = (int)(fl & kFlRl);
+            v.w_rkey_off[r] = cr.s_ro[pre + i];
+        }
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan<kPackT>(start ? 1u : 0u, lds, tot);
+        // nearest run head at or before i in this chunk (local index + 1), and
+        // the exclusive start count there
+        const uint32_t hj = block_incl_max<kPackT>(head ? threadIdx.x + 1 : 0, lds2);
+        s_lk[threadIdx.x] = ex;
+        __syncthreads();
+        const uint32_t hpos = hj ? c0 + hj - 1 : carry_head;
+        const uint32_t rank = hj ? ex - s_lk[hj - 1] : carry_cnt + ex;
+        // the last survivor at or before i in this chunk (lock bit of a run's end)
+        const uint32_t ls = block_incl_max<kPackT>(start ? threadIdx.x + 1 : 0, lds2);
+        __syncthreads();
+        s_lk[threadIdx.x] = start ? ((fl & kFlLk) ? 1u : 0u) : 0u;
+        __syncthreads();
+        const bool lastlk_local = ls && (!hj || ls >= hj) ? s_lk[ls - 1] != 0 : false;
+        const bool has_local = ls && (!hj || ls >= hj);
+        const uint32_t lk_now = has_local ? lastlk_local : (hj ? 0u : carry_lk);
+        // run end: the next row opens another run or the set ends
+        bool end = false;
+        if (live) {
+            const uint32_t nfl = i + 1 < n ? cr.s_fl[pre + i + 1] : kFlHead;
+            end = (nfl & kFlHead) != 0;
+        }
+        __syncthreads();  // every row of the chunk read before any packing write
+        if (start) v.ord[b + hpos + rank] = r;
+        if (live) v.tmp[b + i] = 0;
+        __syncthreads();
+        if (end) v.tmp[b + hpos] = (rank + (start ? 1u : 0u)) | (lk_now ? 1u << 31 : 0u);
+        if (threadIdx.x == kPackT - 1 || i + 1 == n) {  // carry into the next chunk
+            carry_head = hpos;
+            carry_cnt = rank + (start ? 1u : 0u);
+            carry_lk = lk_now;
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t co_run_merge(const CoView &v, const CoBig &bg, const CoRuns &cr, uint32_t nbig,
+                        hipStream_t s)
+{
+    const uint32_t nch = (bg.total + kRunChunk - 1) / kRunChunk;
+    k_run_local<<<(nch + 63) / 64, 64, 0, s>>>(v, bg, cr);
+    if (nch > 1) k_run_stitch<<<(nch - 1 + 63) / 64, 64, 0, s>>>(v, bg, cr);
+    k_run_pack<<<nbig, kPackT, 0, s>>>(v, bg, cr);
+    return hipGetLastError();
+}
+
 constexpr int kJoinT = 256;
 
 __global__ __launch_bounds__(kJoinT) void k_co_big_join(CoView v, CoBig bg, uint32_t *runpos,
@@ -731,6 +991,12 @@ hipError_t co_tie_sort(const CoView &v, const CoBig &bg, uint32_t maxn, const Co
 
 }  // namespace
 
+size_t coalesce_run_scratch_bytes(uint32_t total)
+{
+    const size_t nch = (total + kRunChunk - 1) / kRunChunk;
+    return 12 * (size_t)total + 5 * nch + 64;
+}
+
 size_t coalesce_tie_scratch_bytes(uint32_t total)
 {
     size_t m = 0, n = total;  // max-scan tile maxima, recursively
@@ -745,7 +1011,7 @@ size_t coalesce_tie_scratch_bytes(uint32_t total)
 hipError_t launch_coalesce(const CoView &v, const uint32_t *isbig, const uint32_t *big_set,
                            const uint32_t *big_pre, uint32_t nbig, uint32_t big_total,
                            uint32_t big_maxn, uint32_t *big_runpos, uint32_t *big_scratch,
-                           void *tie_scratch, hipStream_t s)
+                           void *tie_scratch, void *run_scratch, hipStream_t s)
 {
     if (v.ntxn <= 0) return hipSuccess;
     k_coalesce<<<(v.ntxn + 127) / 128, 128, 0, s>>>(v, nbig ? isbig : nullptr);
@@ -772,7 +1038,16 @@ hipError_t launch_coalesce(const CoView &v, const uint32_t *isbig, const uint32_
     for (int pass = 0; pass < 2; ++pass) {
         e = tie_scratch ? co_tie_sort(v, bg, big_maxn, tw, s) : co_big_sort(v, bg, big_maxn, s);
         if (e != hipSuccess) return e;
-        k_co_big_runs<<<nb, 256, 0, s>>>(v, bg);
+        if (run_scratch) {  // chunk-parallel merge scan (long runs)
+            const uint32_t nch = (big_total + kRunChunk - 1) / kRunChunk;
+            uint8_t *p = (uint8_t *)run_scratch;
+            CoRuns cr{(uint64_t *)p, (uint32_t *)(p + 8 * (size_t)big_total),
+                      (uint32_t *)(p + 12 * (size_t)big_total),
+                      p + 12 * (size_t)big_total + 4 * (size_t)nch};
+            if ((e = co_run_merge(v, bg, cr, nbig, s)) != hipSuccess) return e;
+        } else {
+            k_co_big_runs<<<nb, 256, 0, s>>>(v, bg);
+        }
         k_co_big_join<<<nbig, kJoinT, 0, s>>>(v, bg, big_runpos, big_scratch);
     }
     return hipGetLastError();

@@ -255,7 +255,7 @@ struct hsc_ctx {
     size_t e_dev_n = 0;
 
     // replicant coalesce: device inputs / working arrays, host outputs
-    DBuf co_dev[24];
+    DBuf co_dev[25];
     std::vector<int64_t> co_off;
     std::vector<int32_t> co_i32[7];
     std::vector<uint64_t> co_u64[2];
@@ -2504,9 +2504,12 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
         HIPCHK(c, hipMemcpyAsync(d[20].p, bpre.data(), 4 * ((size_t)nbig + 1), hipMemcpyHostToDevice, s));
     }
     if (ties) HIPCHK(c, d[23].ensure(coalesce_tie_scratch_bytes(bpre.back())));
+    // HSC_CO_RUNSCAN=0: one thread per run in the merge scan (A/B, tests)
+    static const bool run_chunks = !getenv("HSC_CO_RUNSCAN") || atoi(getenv("HSC_CO_RUNSCAN")) != 0;
+    if (nbig && run_chunks) HIPCHK(c, d[24].ensure(coalesce_run_scratch_bytes(bpre.back())));
     HIPCHK(c, launch_coalesce(v, d[18].as<uint32_t>(), d[19].as<uint32_t>(), d[20].as<uint32_t>(),
                               nbig, bpre.back(), bmax, d[21].as<uint32_t>(), d[22].as<uint32_t>(),
-                              ties ? d[23].p : nullptr, s));
+                              ties ? d[23].p : nullptr, nbig && run_chunks ? d[24].p : nullptr, s));
     std::vector<uint32_t> cnt(T), ord(nr);
     std::vector<int32_t> wrf(nr), wlk(nr), wrl(nr);
     std::vector<uint64_t> wro(nr);

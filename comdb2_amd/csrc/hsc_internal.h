@@ -311,11 +311,14 @@ struct CoView {
 constexpr uint32_t kCoBig = 256;
 // tie_scratch (coalesce_tie_scratch_bytes(big_total), NULL if no big set has a
 // NULL lower key): the big sets sort on glibc's exact merge tree instead.
+// run_scratch (coalesce_run_scratch_bytes(big_total), or NULL for one thread
+// per run): the merge scan of the big sets' runs in parallel chunks.
 size_t coalesce_tie_scratch_bytes(uint32_t total);
+size_t coalesce_run_scratch_bytes(uint32_t total);
 hipError_t launch_coalesce(const CoView &v, const uint32_t *isbig, const uint32_t *big_set,
                            const uint32_t *big_pre, uint32_t nbig, uint32_t big_total,
                            uint32_t big_maxn, uint32_t *big_runpos, uint32_t *big_scratch,
-                           void *tie_scratch, hipStream_t s);
+                           void *tie_scratch, void *run_scratch, hipStream_t s);
 
 // Narrow tiles keep the chunk histogram tile-major: hist[t * hist_stride(G) + g].
 __host__ __device__ inline uint32_t hist_stride(uint32_t G) { return (G + 7) & ~7u; }

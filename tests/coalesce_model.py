@@ -177,3 +177,20 @@ def random_readsets(seed: int, ntxn: int = 300, max_ranges: int = 40, tables=("t
         sets.append(rs)
         snaps.append(1 << 32)
     return ReadSets.from_lists(sets, snaps, tbnames=list(tables))
+
+
+def long_run_readsets(seed: int, ntxn: int = 8, n: int = 200_000, overlap: float = 0.2):
+    """Read sets that are one long (table, index) run: n closed ranges over
+    one index of 8-byte big-endian keys (no open ends, no locks), a share of
+    them overlapping their neighbour -- a large index scan's read set."""
+    from comdb2_amd.formats import Range
+    rng = np.random.default_rng(seed)
+    sets, snaps = [], []
+    for _ in range(ntxn):
+        lo = np.sort(rng.integers(0, 1 << 40, size=n))
+        w = np.where(rng.random(n) < overlap, 1 << 24, rng.integers(0, 1 << 10, size=n))
+        hi = lo + w
+        enc = lambda v: int(v).to_bytes(8, "big")
+        sets.append([Range("ta", 0, enc(a), enc(b), 0, 0, 0) for a, b in zip(lo, hi)])
+        snaps.append(1 << 32)
+    return ReadSets.from_lists(sets, snaps, tbnames=["ta"])

@@ -305,3 +305,88 @@ def test_tie_merge_tree_replay_equals_msort(seed):
     want = m.msort(a)
     got = _tie_sort(m, a)
     assert [id(x) for x in got] == [id(x) for x in want]
+
+
+# ---- the GPU's chunk-parallel merge scan (k_run_local / k_run_stitch /
+# k_run_pack), restated in Python against the model's sequential
+# currangearr_merge_neighbor over one run
+
+def _chunked_merge(m, a, C):
+    n = len(a)
+
+    def step(p, q):  # p = [rf, rkey, rkeylen, lk, lflag]; True if q absorbed
+        rf, rk, rl, lk, lf = p
+        if not (q.lflag or rf or m.memcmp(q.lkey, rk, min(q.lkeylen, rl)) <= 0):
+            return False
+        if rf or q.rflag:
+            rf, rk, rl = 1, None, 0
+        elif m.memcmp(rk, q.rkey, min(rl, q.rkeylen)) < 0:
+            rk = q.rkey
+        if lf and rf:
+            lk = 1
+        p[:] = [rf, rk, rl, lk, lf]
+        return True
+
+    fresh = lambda q: [q.rflag, q.rkey, q.rkeylen, q.islocked, q.lflag]
+    start, state, last = [False] * n, [None] * n, []
+    for c0 in range(0, n, C):  # k_run_local: each chunk opens a survivor at its first row
+        p, sp = None, None
+        for g in range(c0, min(c0 + C, n)):
+            if p is not None and step(p, a[g]):
+                continue
+            if p is not None:
+                state[sp] = list(p)
+            p, sp = fresh(a[g]), g
+            start[g] = True
+        state[sp] = list(p)
+        last.append(sp)
+    if n > C:  # k_run_stitch (one run: one thread from the first boundary)
+        g = C
+        sp = last[0]
+        p = list(state[sp])
+        while True:
+            resync = False
+            while g < n:
+                if step(p, a[g]):
+                    start[g] = False
+                    g += 1
+                    continue
+                state[sp] = list(p)
+                if start[g]:
+                    resync = True
+                    break
+                p, sp = fresh(a[g]), g
+                start[g] = True
+                g += 1
+            if not resync:
+                state[sp] = list(p)
+                break
+            ch = g // C
+            g = (ch + 1) * C
+            if g >= n:
+                break
+            sp = last[ch]
+            p = list(state[sp])
+    return [(i, tuple(state[i][:4])) for i in range(n) if start[i]]
+
+
+@pytest.mark.parametrize("seed", range(10))
+@pytest.mark.parametrize("C", [1, 3, 16])
+def test_chunked_run_merge_equals_sequential(seed, C):
+    from coalesce_model import CR, Model
+    rng = np.random.default_rng(seed)
+    buf = bytes(rng.integers(0x61, 0x64, size=3000).astype(np.uint8))
+    m = Model(buf)
+    n = int(rng.integers(1, 120))
+    lo = np.sort(rng.integers(0, 2900, size=n))
+    a = []
+    for x in lo:
+        lf, rf = int(rng.random() < 0.03), int(rng.random() < 0.03)
+        a.append(CR("ta", 0, lf, rf, 0, None if lf else int(x), 0 if lf else int(rng.integers(0, 4)),
+                    None if rf else int(x), 0 if rf else int(rng.integers(0, 5))))
+    got = _chunked_merge(m, a, C)
+    import copy
+    b = copy.deepcopy(a)
+    ids = {id(x): i for i, x in enumerate(b)}
+    want = [(ids[id(x)], (x.rflag, x.rkey, x.rkeylen, x.islocked)) for x in m.merge_neighbor(b)]
+    assert got == want

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 sys.path.insert(0, os.path.dirname(__file__))
-from coalesce_model import as_rows, random_readsets  # noqa: E402
+from coalesce_model import as_rows, long_run_readsets, random_readsets  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
@@ -55,3 +55,19 @@ def test_gpu_coalesce_empty(validator, oracle_mod):
     rs = random_readsets(5, ntxn=10, max_ranges=1)  # every set empty
     got = validator.coalesce(rs)
     assert list(got.txn_off) == [0] * 11
+
+
+@pytest.mark.parametrize("seed,ntxn,n,overlap", [(21, 2, 30000, 0.2), (22, 3, 5000, 0.9),
+                                                 (23, 1, 70000, 0.0)])
+def test_gpu_coalesce_long_runs(validator, oracle_mod, monkeypatch, seed, ntxn, n, overlap):
+    """Sets that are one long (table, index) run: the merge scan splits into
+    chunks stitched per run (k_run_local / k_run_stitch / k_run_pack); equal
+    to the oracle and to one thread per run (HSC_CO_RUNSCAN=0 is read once
+    per process, so the serial path is checked through HSC_CO_SERIAL)."""
+    rs = long_run_readsets(seed, ntxn=ntxn, n=n, overlap=overlap)
+    want = oracle_mod.coalesce(rs)
+    got = validator.coalesce(rs)
+    assert list(got.txn_off) == list(want.txn_off)
+    assert as_rows(got) == as_rows(want)
+    monkeypatch.setenv("HSC_CO_SERIAL", "1")
+    assert as_rows(validator.coalesce(rs)) == as_rows(want)
