@@ -404,7 +404,9 @@ def box_cpus():
                 cpu=cpu_model())
 
 
-PROBE_KERNELS = ("k_locate_t", "k_plan_t", "k_scatter_t", "k_join_t", "k_pack_flags")
+PROBE_KERNELS = ("k_locate_t", "k_plan_t", "k_scatter_t", "k_join_t", "k_pack_flags",  # narrow
+                 "k_compact_bounds", "k_locate", "k_colscan", "k_plan", "k_scatter", "k_join",
+                 "k_pack", "k_probe_delta")  # compact / wide, delta run
 
 
 def pmc_traffic(args):
@@ -428,7 +430,8 @@ def pmc_traffic(args):
         cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", ctr, "-T", "--output-format",
                "csv", "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__),
                "--pmc-child", "--config", str(args.config), "--n-commits", str(args.n_commits),
-               "--n-txn", str(args.n_txn)]
+               "--n-txn", str(args.n_txn), "--c3-writes", str(args.c3_writes),
+               "--c5-keys", str(args.c5_keys)]
         print(f"[bench] pmc pass {ctr}", file=sys.stderr, flush=True)
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
@@ -506,7 +509,7 @@ def main():
     ap.add_argument("--c4-keys", type=int, default=0, help="config 4: keys (0: txns / 10)")
     args = ap.parse_args()
     if args.ring_gb is None:
-        args.ring_gb = 1.1 if args.config == 2 and not args.pmc_child else 0.0
+        args.ring_gb = 1.1 if args.config in (2, 3, 5) and not args.pmc_child else 0.0
 
     if args.config == 4:
         return bench_graph(args)
@@ -515,7 +518,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     traffic = None
-    if (args.config == 2 and world == 1 and not args.no_pmc and not args.pmc_child
+    if (args.config in (2, 3, 5) and world == 1 and not args.no_pmc and not args.pmc_child
             and not args.wide):
         traffic = pmc_traffic(args)  # child processes, before this one touches the GPU
     import torch

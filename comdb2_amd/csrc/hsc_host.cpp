@@ -216,6 +216,7 @@ struct hsc_ctx {
     Dir16 cdir{}, tdir{};
     uint32_t trad_m = 0;       // tile bucket table size (0: none)
     uint32_t ncommit = 0;
+    uint64_t commit_span[2] = {0, 0};  // oldest / newest distinct commit LSN of the window
     bool rank_lsn32 = false;   // narrow tiles: rows carry lsn - rank_base + 1 (NarrowTiles)
     uint64_t rank_base = 0;
     DBuf w_tcode, w_tcode2, w_trecs;
@@ -499,10 +500,8 @@ static int build_commits(hsc_ctx *c, size_t n_in)
                           c->d_gid2.as<uint32_t>(), c->d_commits.as<uint64_t>(),
                           c->d_commits.as<uint64_t>(), n_in, c->d_flags.as<uint32_t>(),
                           c->d_scratch.p, c->d_scratch.bytes, c->d_count.as<uint32_t>() + 12, s));
-    uint32_t m = 0;
-    HIPCHK(c, hipMemcpyAsync(&m, c->d_count.as<uint32_t>() + 12, 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
-    c->ncommit = m;
+    // the count (d_count[12]) and the span (narrow_commit_span) come back with
+    // the window's own sizes, in device_build's one readback
     return HSC_OK;
 }
 
@@ -586,7 +585,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, c->d_flags.ensure(cap * 4 + 64));
     size_t scratch = std::max(radix_scratch_bytes(n_in, W), scan_scratch_bytes(n_in) + 64);
     HIPCHK(c, c->d_scratch.ensure(scratch));
-    HIPCHK(c, c->d_count.ensure(64));
+    HIPCHK(c, c->d_count.ensure(256));
 
     hipEvent_t e0 = nullptr, e1 = nullptr;
     HIPCHK(c, hipEventCreate(&e0));
@@ -613,9 +612,30 @@ static int device_build(hsc_ctx *c, size_t n_in)
         std::swap(c->d_words, c->d_words2);
         std::swap(c->d_lsn, c->d_lsn2);
     }
-    uint32_t nu = 0;
-    HIPCHK(c, hipMemcpyAsync(&nu, c->d_count.p, 4, hipMemcpyDeviceToHost, s));
+    // one readback for the sizes the host plans with: distinct rows, commits,
+    // the commit span and the window's end rows (all computed on the device)
+    const bool commits = c->layout != HSC_LAYOUT_WIDE && n_in > 0;
+    HIPCHK(c, c->d_nbase.ensure(16 * ((size_t)W + 1)));
+    std::vector<uint64_t> ends(2 * ((size_t)W + 1), 0);
+    uint32_t hc[24] = {0};
+    if (commits) {
+        WinView wc{};
+        wc.words = c->d_words.as<uint64_t>();
+        wc.stride = cap;
+        wc.gid = c->d_gid.as<uint32_t>();
+        wc.W = W;
+        HIPCHK(c, narrow_end_rows(wc, c->d_count.as<uint32_t>(), c->d_nbase.as<uint64_t>(), s));
+        HIPCHK(c, narrow_commit_span(c->d_commits.as<uint64_t>(), c->d_count.as<uint32_t>() + 12,
+                                     (uint64_t *)(c->d_count.as<uint32_t>() + 16), s));
+        HIPCHK(c, hipMemcpyAsync(ends.data(), c->d_nbase.p, 8 * ends.size(), hipMemcpyDeviceToHost, s));
+    }
+    HIPCHK(c, hipMemcpyAsync(hc, c->d_count.p, sizeof hc, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
+    const uint32_t nu = hc[0];
+    if (commits) {
+        c->ncommit = hc[12];
+        memcpy(c->commit_span, hc + 16, 16);
+    }
     c->n = n_in ? nu : 0;
     c->n_all = n_in;  // every version, key-sorted, stays in d_gid2 / d_words2 / d_lsn2
     // narrow layout if the whole window fits 62-bit codes (hsc_narrow.hip)
@@ -633,17 +653,6 @@ static int device_build(hsc_ctx *c, size_t n_in)
                 break;
             }
         }
-        WinView wc{};
-        wc.words = c->d_words.as<uint64_t>();
-        wc.stride = cap;
-        wc.gid = c->d_gid.as<uint32_t>();
-        wc.n = (uint32_t)c->n;
-        wc.W = W;
-        HIPCHK(c, c->d_nbase.ensure(16 * ((size_t)W + 1)));
-        HIPCHK(c, narrow_end_rows(wc, c->d_nbase.as<uint64_t>(), s));
-        std::vector<uint64_t> ends(2 * ((size_t)W + 1));
-        HIPCHK(c, hipMemcpyAsync(ends.data(), c->d_nbase.p, 8 * ends.size(), hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipStreamSynchronize(s));
         c->narrow = narrow_span_fits(W, c->lw, c->tz, ends.data(), ends.data() + W + 1);
     }
     c->log2T = tile_log2(W);
@@ -681,6 +690,8 @@ static int device_build(hsc_ctx *c, size_t n_in)
                               c->d_table_max.as<uint64_t>(), c->d_sp_g.as<uint32_t>(),
                               c->d_sp_w.as<uint64_t>(), s));
     c->compact = false;
+    uint32_t wide32 = 1;   // narrow tiles: a tile spans >= 2^32 codes (device flag)
+    bool tiles32 = false;
     if (!c->narrow && c->layout == HSC_LAYOUT_AUTO && c->n > 0 && W > 1 && ng > 0)
         HIPCHK_RC(c, build_compact(c, w));
     if (c->narrow) {
@@ -748,11 +759,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
         c->trad_m = 0;
         if (wn.log2T == 12 && wn.ntiles <= (uint32_t)kHistCap && c->ncommit > 0) {
             // commit span: rank-free rows (lsn - oldest commit + 1) when it fits 32 bits
-            uint64_t span[2] = {0, 0};
-            HIPCHK(c, hipMemcpyAsync(&span[0], c->d_commits.as<uint64_t>(), 8, hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipMemcpyAsync(&span[1], c->d_commits.as<uint64_t>() + c->ncommit - 1, 8,
-                                     hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipStreamSynchronize(s));
+            const uint64_t *span = c->commit_span;
             c->rank_lsn32 = span[1] - span[0] <= kLsn32MaxSpan && !getenv("HSC_RANK_DIR");
             c->rank_base = span[0];
             c->cdir = Dir16{};
@@ -772,14 +779,13 @@ static int device_build(hsc_ctx *c, size_t n_in)
                                          c->cdir, c->rank_lsn32, c->rank_base,
                                          c->d_key32.as<uint32_t>(), c->d_rank32.as<uint32_t>(),
                                          flag, s));
-            uint32_t wide32 = 1;
-            HIPCHK(c, hipMemcpyAsync(&wide32, flag, 4, hipMemcpyDeviceToHost, s));
-            HIPCHK(c, hipStreamSynchronize(s));
-            c->ntiles32 = wide32 == 0;
+            HIPCHK(c, hipMemcpyAsync(&wide32, flag, 4, hipMemcpyDeviceToHost, s));  // read below
+            tiles32 = true;
         }
     }
     HIPCHK(c, hipEventRecord(e1, s));
     HIPCHK(c, hipStreamSynchronize(s));
+    if (tiles32) c->ntiles32 = wide32 == 0;
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
     c->last.ingest_ms = ms;

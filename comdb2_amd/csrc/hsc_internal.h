@@ -189,7 +189,9 @@ struct NarrowView {
     uint32_t ntables;
 };
 bool narrow_span_fits(int W, int lw, int tz, const uint64_t *first, const uint64_t *last);
-hipError_t narrow_end_rows(const WinView &w, uint64_t *out, hipStream_t s);
+hipError_t narrow_end_rows(const WinView &w, const uint32_t *n_dev, uint64_t *out, hipStream_t s);
+hipError_t narrow_commit_span(const uint64_t *commits, const uint32_t *m_dev, uint64_t *out,
+                              hipStream_t s);
 hipError_t narrow_build(const WinView &w, const NarrowView &nv, hipStream_t s);
 hipError_t launch_probe_narrow(const NarrowView &nv, const ProbeView &p, uint8_t *verdict,
                                hipStream_t s);

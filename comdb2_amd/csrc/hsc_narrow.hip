@@ -126,18 +126,37 @@ bool narrow_span_fits(int W, int lw, int tz, const uint64_t *first, const uint64
 // window build
 // ============================================================================
 // rows 0 and n-1 as limbs (gid, words) -> out[0 .. W], out[W+1 .. 2W+1]
-__global__ void k_end_rows(WinView w, uint64_t *out)
+// (n_dev: the row count on the device, read there -- no host round trip)
+__global__ void k_end_rows(WinView w, const uint32_t *n_dev, uint64_t *out)
 {
     const int j = threadIdx.x;
     if (j > w.W) return;
-    const size_t r[2] = {0, (size_t)w.n - 1};
+    const uint32_t n = n_dev ? *n_dev : w.n;
+    const size_t r[2] = {0, n ? (size_t)n - 1 : 0};
     for (int k = 0; k < 2; ++k)
-        out[k * (w.W + 1) + j] = j ? w.words[(size_t)(j - 1) * w.stride + r[k]] : w.gid[r[k]];
+        out[k * (w.W + 1) + j] =
+            !n ? 0 : j ? w.words[(size_t)(j - 1) * w.stride + r[k]] : w.gid[r[k]];
 }
 
-hipError_t narrow_end_rows(const WinView &w, uint64_t *out, hipStream_t s)
+hipError_t narrow_end_rows(const WinView &w, const uint32_t *n_dev, uint64_t *out, hipStream_t s)
 {
-    k_end_rows<<<1, 128, 0, s>>>(w, out);
+    k_end_rows<<<1, 128, 0, s>>>(w, n_dev, out);
+    return hipGetLastError();
+}
+
+// first and last of the m_dev sorted commit LSNs -> out[0], out[1]
+__global__ void k_commit_span(const uint64_t *commits, const uint32_t *m_dev, uint64_t *out)
+{
+    if (threadIdx.x) return;
+    const uint32_t m = *m_dev;
+    out[0] = m ? commits[0] : 0;
+    out[1] = m ? commits[m - 1] : 0;
+}
+
+hipError_t narrow_commit_span(const uint64_t *commits, const uint32_t *m_dev, uint64_t *out,
+                              hipStream_t s)
+{
+    k_commit_span<<<1, 64, 0, s>>>(commits, m_dev, out);
     return hipGetLastError();
 }
 
