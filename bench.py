@@ -8,9 +8,10 @@ the timed region starts; marshalling (CurRangeArr -> probe SoA, done by the
 native library) happens before it.
 
 Multi-GPU (weak scaling): the key space is range-partitioned; rank r owns the
-window keys [r, r+1) * 2^40 and probes only the ranges that overlap its shard;
-the global batch is N x 100k read sets.  Verdict bytes (1 = not serializable)
-are merged with all_reduce(MAX) == bitwise OR.
+window keys [r, r+1) * 2^40 (config 5: sampled global splitters) and probes
+only the ranges that overlap its shard; the global batch is N x 100k read
+sets.  Each shard's verdict bitmap is all-gathered (N x n_txn / 8 bytes) and
+the N bitmaps OR-ed on the GPU (hsc_or_bitmaps): RCCL has no bitwise OR.
 
 Prints ONE JSON line on rank 0.
 """
@@ -651,8 +652,12 @@ def main():
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
     comm = torch.cuda.Stream(device=dev) if world > 1 else None
     verdicts = [torch.zeros(T, dtype=torch.uint8, device=dev) for _ in range(S)]
-    bitmaps = [torch.zeros((T + 63) // 64, dtype=torch.int64, device=dev) for _ in range(S)]
-    structs = [[probe_struct(hsc, b, verdicts[si], bitmaps[si] if world == 1 else None, T)
+    W64 = (T + 63) // 64
+    bitmaps = [torch.zeros(W64, dtype=torch.int64, device=dev) for _ in range(S)]
+    # N > 1: each shard's verdict bitmap, all-gathered and OR-ed (hsc_or_bitmaps)
+    lbits = [torch.zeros(W64, dtype=torch.int64, device=dev) for _ in range(S)] if world > 1 else None
+    gath = [torch.zeros(world * W64, dtype=torch.int64, device=dev) for _ in range(S)] if world > 1 else None
+    structs = [[probe_struct(hsc, b, verdicts[si], bitmaps[si] if world == 1 else lbits[si], T)
                 for si in range(S)] for b in batches]
     torch.cuda.synchronize()
 
@@ -673,11 +678,11 @@ def main():
             e.record(st)
             comm.wait_event(e)
             with torch.cuda.stream(comm):
-                shard.merge_verdicts(verdicts[si])
+                shard.gather_bitmaps(lbits[si], gath[si])
             e2 = torch.cuda.Event()
             e2.record(comm)
             st.wait_event(e2)
-            v.pack_verdicts(verdicts[si].data_ptr(), T, bitmaps[si].data_ptr())
+            v.or_bitmaps(gath[si].data_ptr(), world, W64, bitmaps[si].data_ptr())
 
     def timed(nstreams, nbatch):
         for k in range(args.warmup):
@@ -713,7 +718,11 @@ def main():
     # verdicts of batch 0 (for the conflict rate and the CPU parity sample)
     step(0, 1, NB)
     torch.cuda.synchronize()
-    v0 = verdicts[0].cpu().numpy().copy()
+    if world > 1:  # the merged verdicts are the OR-ed bitmap
+        bits = bitmaps[0].cpu().numpy().view(np.uint8)
+        v0 = np.unpackbits(bits, bitorder="little")[:T].astype(np.uint8)
+    else:
+        v0 = verdicts[0].cpu().numpy().copy()
     forced = batches[0]["forced"]
     v0 = np.maximum(v0, forced)
 
@@ -767,7 +776,7 @@ def main():
             "ranges_per_gpu": n_r,
             "window_keys_per_gpu": n_keys,
             "logged_writes_per_gpu": n_w,
-            "parallelism": f"key-range shards x{world}" + (" + RCCL max all-reduce" if world > 1 else ""),
+            "parallelism": f"key-range shards x{world}" + (" + RCCL all-gather of verdict bitmaps" if world > 1 else ""),
             "streams": S,
             "serial_ms_per_step": serial_elapsed / args.steps * 1e3,
             "ring_batches": NB,
@@ -822,7 +831,7 @@ def main():
         out["roofline"]["traffic_detail"] = traffic
     if args.config == 3:
         out["config"]["parallelism"] = f"(table, index) group shards (LPT) x{world}" + (
-            " + RCCL max all-reduce" if world > 1 else "")
+            " + RCCL all-gather of verdict bitmaps" if world > 1 else "")
         out["config"]["groups_per_rank"] = len(mine)
         if args.check and world == 1:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))

@@ -2652,6 +2652,16 @@ int hsc_pack_verdicts(hsc_ctx *c, const uint8_t *verdict, size_t n_txn, uint64_t
     return HSC_OK;
 }
 
+int hsc_or_bitmaps(hsc_ctx *c, const uint64_t *parts, int nparts, size_t words, uint64_t *out)
+{
+    if (!c || nparts < 1 || (words && (!parts || !out))) return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    HIPCHK(c, launch_or_bitmaps(parts, nparts, words, out, c->stream));
+    return HSC_OK;
+}
+
 int hsc_synchronize(hsc_ctx *c)
 {
     if (!c) return HSC_EINVAL;

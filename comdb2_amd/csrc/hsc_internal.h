@@ -452,5 +452,7 @@ int decode_serial_msgs(const hsc_serial_msgs *m, DecodedReadSets &out, std::stri
 
 hipError_t launch_pack(const uint8_t *verdict, uint32_t n_txn, uint64_t *bitmap,
                        hipStream_t s);
+hipError_t launch_or_bitmaps(const uint64_t *parts, int nparts, size_t words, uint64_t *out,
+                             hipStream_t s);
 
 }  // namespace hsc

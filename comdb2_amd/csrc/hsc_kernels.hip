@@ -1155,4 +1155,22 @@ hipError_t launch_pack(const uint8_t *verdict, uint32_t n_txn, uint64_t *bitmap,
     return hipGetLastError();
 }
 
+// ---- OR of per-shard verdict bitmaps (after an all-gather) -----------------
+__global__ void k_or_bitmaps(const uint64_t *parts, int nparts, size_t words, uint64_t *out)
+{
+    const size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= words) return;
+    uint64_t m = 0;
+    for (int k = 0; k < nparts; ++k) m |= parts[(size_t)k * words + w];
+    out[w] = m;
+}
+
+hipError_t launch_or_bitmaps(const uint64_t *parts, int nparts, size_t words, uint64_t *out,
+                             hipStream_t s)
+{
+    if (words == 0) return hipSuccess;
+    k_or_bitmaps<<<(unsigned)((words + 255) / 256), 256, 0, s>>>(parts, nparts, words, out);
+    return hipGetLastError();
+}
+
 }  // namespace hsc

@@ -134,7 +134,8 @@ EXPORTS = [
     "hsc_window_keys", "hsc_window_end", "hsc_window_max_commit", "hsc_table_id",
     "hsc_table_name", "hsc_group_info", "hsc_table_max", "hsc_merge_table_max",
     "hip_bdb_osql_serial_check", "hip_serial_check_batch", "hsc_check_readsets",
-    "hsc_marshal_readsets", "hsc_probe_device", "hsc_pack_verdicts", "hsc_synchronize",
+    "hsc_marshal_readsets", "hsc_probe_device", "hsc_pack_verdicts", "hsc_or_bitmaps",
+    "hsc_synchronize",
     "hsc_get_timing",
     "hsc_enable_timing", "hsc_dep_graph_scc", "hsc_dep_graph_edges",
     "hsc_window_ingest_raw", "hsc_decode_log", "hsc_decode_serial", "hsc_check_serial",
@@ -194,6 +195,7 @@ def load() -> C.CDLL:
         "hsc_marshal_readsets": (C.c_int, [_p, C.POINTER(_ReadSets), C.POINTER(C.POINTER(Marshalled))]),
         "hsc_probe_device": (C.c_int, [_p, C.POINTER(ProbeBatch)]),
         "hsc_pack_verdicts": (C.c_int, [_p, _p, C.c_size_t, _p]),
+        "hsc_or_bitmaps": (C.c_int, [_p, _p, C.c_int, C.c_size_t, _p]),
         "hsc_synchronize": (C.c_int, [_p]),
         "hsc_get_timing": (C.c_int, [_p, C.POINTER(Timing)]),
         "hsc_enable_timing": (C.c_int, [_p, C.c_int]),
@@ -802,6 +804,11 @@ class Validator:
     def pack_verdicts(self, verdict_ptr: int, n_txn: int, bitmap_ptr: int) -> None:
         self._chk(self.lib.hsc_pack_verdicts(self.ctx, verdict_ptr, n_txn, bitmap_ptr),
                   "hsc_pack_verdicts")
+
+    def or_bitmaps(self, parts_ptr: int, nparts: int, words: int, out_ptr: int) -> None:
+        """out[w] = OR of the nparts bitmaps parts[k * words + w] (device)."""
+        self._chk(self.lib.hsc_or_bitmaps(self.ctx, parts_ptr, nparts, words, out_ptr),
+                  "hsc_or_bitmaps")
 
     def set_stream(self, stream_handle: int) -> None:
         self._chk(self.lib.hsc_set_stream(self.ctx, stream_handle), "hsc_set_stream")

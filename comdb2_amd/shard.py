@@ -251,6 +251,20 @@ def merge_verdicts(verdict, group=None) -> None:
     dist.all_reduce(verdict, op=dist.ReduceOp.MAX, group=group)
 
 
+def gather_bitmaps(bitmap, gathered, group=None) -> None:
+    """gathered[k * words ...] := rank k's verdict bitmap (one all-gather of
+    n_txn / 8 bytes per rank; RCCL has no bitwise-OR reduction, so the ranks
+    OR the N bitmaps themselves: hsc_or_bitmaps).  Per rank a ring all-gather
+    moves (N - 1) n_txn / 8 bytes, a byte-wise max all-reduce 2 (N - 1) / N
+    n_txn."""
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    if dist.get_backend(group) == "nccl":
+        dist.all_gather_into_tensor(gathered, bitmap, group=group)
+    else:
+        dist.all_gather(list(gathered.view(world, -1).unbind(0)), bitmap, group=group)
+
+
 # ---- config 4: dependency graph + SCC sharded by key -----------------------
 # Every WW / WR / RW edge belongs to one key (hsc_graph.hip), so a history
 # split by key gives each rank an exact part of the edge set with no

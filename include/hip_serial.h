@@ -426,6 +426,12 @@ int hsc_probe_device(hsc_ctx *ctx, const hsc_probe_batch *b);
 /* verdict bytes -> bitmap (e.g. after a cross-GPU max all-reduce). */
 int hsc_pack_verdicts(hsc_ctx *ctx, const uint8_t *verdict, size_t n_txn,
                       uint64_t *bitmap);
+/* Multi-GPU verdict merge: out_dev[w] = OR over k < nparts of
+ * parts_dev[k * words + w] -- the per-shard verdict bitmaps after an
+ * all-gather (N x n_txn / 8 bytes per rank instead of a byte-wise max
+ * all-reduce of N x n_txn).  Asynchronous on the context's stream. */
+int hsc_or_bitmaps(hsc_ctx *ctx, const uint64_t *parts_dev, int nparts, size_t words,
+                   uint64_t *out_dev);
 int hsc_synchronize(hsc_ctx *ctx);
 int hsc_get_timing(hsc_ctx *ctx, hsc_timing *t);
 /* Enable per-kernel HIP event timing of probes (adds event records). */

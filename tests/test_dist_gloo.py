@@ -92,8 +92,18 @@ def _worker(rank, world, port, mode, out_path):
     merged_tm = shard.allreduce_table_max(tm)
     sub = shard.route(m, sh.range_mask(m, rank), sh.lock_mask(m, rank))
     verdict = evaluate(v, sub, local, table_max_by_name=dict(zip(names, merged_tm.tolist())))
+    # the bench's merge: all-gather of the shards' verdict bitmaps, OR-ed
+    n = len(verdict)
+    words = (n + 63) // 64
+    bits = np.zeros(words * 8, np.uint8)
+    bits[: (n + 7) // 8] = np.packbits(verdict != 0, bitorder="little")
+    gathered = torch.zeros(world * words, dtype=torch.int64)
+    shard.gather_bitmaps(torch.from_numpy(bits.view(np.int64).copy()), gathered)
+    ored = np.bitwise_or.reduce(gathered.numpy().reshape(world, words), axis=0)
+    by_bits = np.unpackbits(ored.view(np.uint8), bitorder="little")[:n]
     t = torch.from_numpy(verdict.copy())
     shard.merge_verdicts(t)
+    assert np.array_equal(by_bits != 0, t.numpy() != 0)  # both merges agree
     if rank == 0:
         np.save(out_path, np.maximum(t.numpy(), m["forced"]))
     dist.barrier()
