@@ -153,15 +153,20 @@ def sampled_splitters(local_keys: np.ndarray, range_keys: np.ndarray, world: int
     [0, 2^key_bits) for comparison, in the caller's units)."""
     import torch
     import torch.distributed as dist
-    uk = np.unique(np.asarray(local_keys, np.int64))
+    uk, cnt = np.unique(np.asarray(local_keys, np.int64), return_counts=True)
     rk = np.sort(np.asarray(range_keys, np.int64)[rank::world])
     s_w = min(samples, len(uk))
     s_r = min(samples, len(rk))
-    # evenly spaced order statistics; each stands for an equal share of the rows
-    pick = lambda a, k: a[(np.arange(k) * len(a)) // max(k, 1)] if k else a[:0]
-    keys = np.concatenate([pick(uk, s_w), pick(rk, s_r)])
-    wts = np.concatenate([np.full(s_w, w_row * len(uk) / max(s_w, 1)),
-                          np.full(s_r, w_range * len(rk) / max(s_r, 1))])
+    # evenly spaced order statistics of the distinct keys; each stands for the
+    # keys up to the next one.  A key this rank wrote more than once is hot:
+    # every rank almost surely holds it too, and it is one row after the
+    # exchange -- so it counts 1 / world here (the tail's keys count 1).
+    iw = (np.arange(s_w) * len(uk)) // max(s_w, 1)
+    cum = np.concatenate([[0.0], np.cumsum(np.where(cnt >= 2, 1.0 / world, 1.0))])
+    row_w = w_row * (cum[np.append(iw[1:], len(uk))] - cum[iw]) if s_w else np.zeros(0)
+    ir = (np.arange(s_r) * len(rk)) // max(s_r, 1)
+    keys = np.concatenate([uk[iw], rk[ir]])
+    wts = np.concatenate([row_w, np.full(s_r, w_range * len(rk) / max(s_r, 1))])
     if world > 1 and dist.is_initialized():
         n = 2 * samples
         kb = torch.full((n,), INT64_MAX, dtype=torch.int64)
