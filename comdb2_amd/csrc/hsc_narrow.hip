@@ -1093,19 +1093,22 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_t(ProbeWork work, uint32_
         col[e / 4 + 1] = ob;
     }
     const uint32_t total = __shfl(x, 63, 64);
-    if (lane == 0) {
-        work.counts[t] = total;
-        if (total > kTileCap) {  // hot tile: overflow run + one join item per kTileCap records
-            const uint32_t over = total - kTileCap;
-            const uint32_t base = atomicAdd(&ctl[0], over);
+    if (lane == 0) work.counts[t] = total;
+    if (total > kTileCap) {  // hot tile: overflow run + one join item per kJoinChunk records
+        const uint32_t over = total - kTileCap;
+        const uint32_t nx = (over + kJoinChunk - 1) / kJoinChunk;
+        uint32_t base = 0, ib = 0;
+        if (lane == 0) {
+            base = atomicAdd(&ctl[0], over);
+            ib = atomicAdd(&ctl[1], nx);
             work.bucket_off[t] = base;
-            const uint32_t nx = (over + kJoinChunk - 1) / kJoinChunk;
-            const uint32_t ib = atomicAdd(&ctl[1], nx);
-            const uint32_t o0 = ntiles * kTileCap + base;
-            for (uint32_t j = 0; j < nx; ++j)
-                work.item_desc[ib + j] = make_uint4(t, o0 + j * kJoinChunk,
-                                                    o0 + min((j + 1) * kJoinChunk, over), 0);
         }
+        base = __shfl(base, 0, 64);
+        ib = __shfl(ib, 0, 64);
+        const uint32_t o0 = ntiles * kTileCap + base;
+        for (uint32_t j = lane; j < nx; j += 64)  // the wave writes the items together
+            work.item_desc[ib + j] = make_uint4(t, o0 + j * kJoinChunk,
+                                                o0 + min((j + 1) * kJoinChunk, over), 0);
     }
 }
 
