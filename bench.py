@@ -295,7 +295,7 @@ def graph_cpu_baseline(args):
                       f"oracle/scc_oracle.c edges + Tarjan, {dt:.1f} s"}
 
 
-def kernel_bytes(layout, W, n_keys, n_r, T, tm):
+def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0):
     """Per-kernel event times and each kernel's own algorithmic bytes (what it
     must read and write in this build's layout) for the probe phase.  Events
     add a few microseconds per slot; the rocprofv3 summaries in profiles/ give
@@ -310,6 +310,14 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm):
             "k_plan_t": hist,
             "k_scatter_t": n_r * (16 + 4) + recs * 16,
             "k_join_t": 8 * n_keys + 16 * recs,
+            "k_pack_flags": 2 * T + (T + 7) // 8,
+        }
+    elif WG:  # compact tiles: raw W-word bounds in, 64-byte probe entries, 4-byte bucket entries
+        own = {
+            "k_compact_bounds+k_locate_c": n_r * (4 + 8 + 4 + 16 * W) + 72 * n_r + hist,
+            "k_plan_t": hist,
+            "k_scatter_c": 8 * n_r + 4 * recs,
+            "k_join_c": n_keys * (8 * WG + 4) + recs * (4 + 64),
             "k_pack_flags": 2 * T + (T + 7) // 8,
         }
     else:  # wide tiles (compact: W = code words): key words + lsn + gid per row
@@ -406,6 +414,7 @@ def box_cpus():
 
 
 PROBE_KERNELS = ("k_locate_t", "k_plan_t", "k_scatter_t", "k_join_t", "k_pack_flags",  # narrow
+                 "k_locate_c", "k_scatter_c", "k_join_c",  # compact tiles
                  "k_compact_bounds", "k_locate", "k_colscan", "k_plan", "k_scatter", "k_join",
                  "k_pack", "k_probe_delta")  # compact / wide, delta run
 
@@ -432,7 +441,7 @@ def pmc_traffic(args):
                "csv", "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__),
                "--pmc-child", "--config", str(args.config), "--n-commits", str(args.n_commits),
                "--n-txn", str(args.n_txn), "--c3-writes", str(args.c3_writes),
-               "--c5-keys", str(args.c5_keys)]
+               "--c5-keys", str(args.c5_keys)] + (["--compact-wide"] if args.compact_wide else [])
         print(f"[bench] pmc pass {ctr}", file=sys.stderr, flush=True)
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
@@ -486,6 +495,9 @@ def main():
                     help="skip the drop-in entry leg (hip_serial_check_batch end to end)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--wide", action="store_true", help="force the wide window layout")
+    ap.add_argument("--compact-wide", action="store_true",
+                    help="compact windows: probe through the wide tile pipeline instead of "
+                         "the compact tiles (A/B)")
     ap.add_argument("--streams", type=int, default=2,
                     help="HIP streams the batches rotate over (each with its own outputs and "
                          "probe lane), so consecutive batches' kernels can overlap")
@@ -549,6 +561,8 @@ def main():
     v = hsc.Validator(local)
     if args.wide:
         v.set_layout(hsc.LAYOUT_WIDE)
+    elif args.compact_wide:
+        v.set_layout(hsc.LAYOUT_COMPACT_WIDE)
     if args.config != 3:
         gid_t = v.register_group("t1", 0, 9)
         assert gid_t == 0
@@ -753,7 +767,8 @@ def main():
         rng_g = np.mean([np.bincount(host(b["gid"]), minlength=len(c3.groups)) for b in batches],
                         axis=0)
         B = int((keys_g * (lhat + 12)).sum() + (rng_g * (2 * lhat + 16)).sum() + (T + 7) // 8)
-    kern = kernel_bytes(v.layout, v.code_words, n_keys, n_r, T, tm)
+    WG = v.tile_key_words if v.layout == hsc.LAYOUT_COMPACT and not args.compact_wide else 0
+    kern = kernel_bytes(v.layout, W if WG else v.code_words, n_keys, n_r, T, tm, WG)
     ms_per_step = elapsed / args.steps * 1e3
     frac = lambda el: B / (el / args.steps) / 1e9 / HBM_PEAK_GBS
     checks = T * args.steps
@@ -781,8 +796,11 @@ def main():
             "serial_ms_per_step": serial_elapsed / args.steps * 1e3,
             "ring_batches": NB,
             "window_layout": {hsc.LAYOUT_NARROW: "narrow (u32 tile-relative keys)",
-                              hsc.LAYOUT_COMPACT: f"compact ({v.code_words}-word codes of "
-                                                  f"{W}-word keys)",
+                              hsc.LAYOUT_COMPACT: (f"compact tiles ({WG}-word keys gid || code, "
+                                                   f"{v.code_words}-word codes of {W}-word keys)"
+                                                   if WG else
+                                                   f"compact ({v.code_words}-word codes of "
+                                                   f"{W}-word keys, wide tile pipeline)"),
                               hsc.LAYOUT_WIDE: "wide"}.get(v.layout, "?"),
             "conflict_rate": float((v0 != 0).mean()),
         },

@@ -1,0 +1,474 @@
+// hsc_ctiles.hip -- compact tiles: the dense-batch tile pipeline for wide
+// windows whose compact codes (hsc_compact.hip) plus the group id fit in at
+// most 3 words (config 3's composite keys: 184 varying bits + 5 group bits).
+//
+// Every row becomes one key of WG words, K = gid || code (the group id in the
+// top gb bits, then the group's varying bits, most significant first).  Rows
+// are sorted by (gid, key words) and the code keeps the words' order inside a
+// group, so the keys are sorted, and a range [lo, hi] of group g maps exactly
+// onto [g || lo', g || hi'] with lo', hi' the code bounds of compact_probes.
+// The window is then ONE sorted array of WG-word keys with 32-bit commit
+// times (lsn - oldest commit + 1; the window's commits span < 2^32 of log),
+// cut into 2048-row tiles, and the narrow tile pipeline (hsc_narrow.hip)
+// carries over with wide records:
+//   locate  (4096 probes per workgroup): keys of lo / hi, their end tiles by a
+//           bucket table over the tiles' first word 0 plus a full-key binary
+//           search of the bucket (first keys in LDS), the whole tiles between
+//           them from the tile-max sparse table, the chunk's tile histogram;
+//           writes the probe's 64-byte entry {lo, hi, r(S), read set} once and
+//           its one or two (tile, in-chunk rank) slots
+//   plan    k_plan_t (fixed-capacity tile buckets, overflow runs for hot tiles)
+//   scatter 4-byte bucket entries (probe index | record kind)
+//   join    a workgroup per tile: its keys (Eytzinger order, every word) and
+//           ranks in LDS (56 KiB), each record's probe entry gathered (one
+//           64-byte line), #keys < lo and #keys <= hi by two lockstep
+//           root-to-leaf walks, any rank > r(S) over [pa, pb) via 16- and
+//           128-row maxima
+//   pack    k_pack_flags
+// Every key compare is exact (all WG words are in LDS), so unlike the wide
+// pipeline's word-0 join a probe equal to a row never reads the window again.
+#include "hsc_device.h"
+#include "hsc_internal.h"
+
+#include <hip/hip_runtime.h>
+
+namespace hsc {
+
+namespace {
+
+constexpr uint32_t kCTRows = 1u << kCTLog2;  // rows per tile
+constexpr int kCLocThreads = 1024;
+constexpr int kCLocP = 4;                    // probes per locate thread
+constexpr uint32_t kCChunk = kCLocThreads * kCLocP;
+static_assert(kCChunk <= 4096, "in-chunk ranks are 12 bits");
+constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
+constexpr uint32_t kSecondRec = 1u << 31;
+// record kinds (top two bits of a bucket entry): search lo and hi / lo only
+// (the range runs past the tile) / hi only (it starts before the tile)
+constexpr uint32_t kCFull = 0, kCHead = 1, kCTail = 2;
+
+// Eytzinger (BFS) slot of sorted row r of a 2^L-row tile: rows 0 .. 2^L - 2
+// form a perfect binary tree at slots 1 .. 2^L - 1, the last row at slot 0.
+template <int L>
+__device__ __forceinline__ uint32_t eyt(uint32_t r)
+{
+    const uint32_t i = r + 1;
+    const int tz = __builtin_ctz(i);
+    return i == (1u << L) ? 0 : (1u << (L - 1 - tz)) + (i >> (tz + 1));
+}
+
+// K = g || code: the WC code words shifted right by gb bits under the group id
+template <int WG>
+__device__ __forceinline__ void compose(uint32_t g, int gb, const uint64_t (&c)[WG],
+                                        uint64_t (&k)[WG])
+{
+    if (gb == 0) {
+#pragma unroll
+        for (int j = 0; j < WG; ++j) k[j] = c[j];
+        return;
+    }
+    k[0] = ((uint64_t)g << (64 - gb)) | (c[0] >> gb);
+#pragma unroll
+    for (int j = 1; j < WG; ++j) k[j] = (c[j - 1] << (64 - gb)) | (c[j] >> gb);
+}
+
+template <int WG>
+__device__ __forceinline__ bool key_lt(const uint64_t (&a)[WG], const uint64_t (&b)[WG])
+{
+#pragma unroll
+    for (int j = 0; j < WG - 1; ++j)
+        if (a[j] != b[j]) return a[j] < b[j];
+    return a[WG - 1] < b[WG - 1];
+}
+
+// ---- build: row keys (Eytzinger order per tile), ranks, tiles' first keys ----
+template <int WG>
+__global__ __launch_bounds__(256) void k_ct_rows(const uint64_t *cw, size_t cs, int WC,
+                                                 const uint32_t *gid, const uint64_t *lsn,
+                                                 CTiles ct, uint64_t *key, uint32_t *rank,
+                                                 uint64_t *first)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ct.len) return;
+    uint64_t k[WG];
+    uint32_t r = 0;
+    if (i < ct.n) {
+        uint64_t c[WG];
+#pragma unroll
+        for (int j = 0; j < WG; ++j) c[j] = j < WC ? cw[(size_t)j * cs + i] : 0;
+        compose<WG>(gid[i], ct.gb, c, k);
+        r = (uint32_t)(lsn[i] - ct.rank_base) + 1;
+    } else {
+#pragma unroll
+        for (int j = 0; j < WG; ++j) k[j] = ~0ull;  // padding: above every bound
+    }
+    const uint32_t t = i >> kCTLog2, o = i & (kCTRows - 1);
+    const size_t dst = ((size_t)t << kCTLog2) + eyt<kCTLog2>(o);
+#pragma unroll
+    for (int j = 0; j < WG; ++j) key[(size_t)j * ct.len + dst] = k[j];
+    rank[i] = r;
+    if (o == 0 && t < ct.ntiles)
+#pragma unroll
+        for (int j = 0; j < WG; ++j) first[(size_t)j * ct.ntiles + t] = k[j];
+}
+
+// word 0 of every tile's first key relative to tile 0's (the bucket table's input)
+__global__ void k_ct_rel(const uint64_t *first0, uint32_t ntiles, uint64_t *rel)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < ntiles) rel[t] = first0[t] - first0[0];
+}
+
+// ---- locate ----
+struct CLocLds {
+    uint32_t first, trad, hist, bytes;
+};
+__host__ __device__ inline CLocLds cloc_lds(const CTiles &ct)
+{
+    CLocLds L{};
+    uint32_t o = 0;
+    L.first = o;
+    o += 8 * ct.WG * ((ct.ntiles + 1) & ~1u);
+    L.trad = o;
+    o += 2 * ((ct.trad_m + 1 + 7) & ~7u);
+    L.hist = o;
+    o += 4 * ((ct.ntiles + 3) & ~3u);
+    L.bytes = o;
+    return L;
+}
+
+// #tiles whose first key is < x (LE: <= x): the bucket of x's word 0, then a
+// binary search inside it with full-key compares (typically 0-2 steps)
+template <int WG, bool LE>
+__device__ __forceinline__ uint32_t ct_count(const uint64_t *lf, uint32_t nt, const uint16_t *T,
+                                             uint32_t m, int shift, uint64_t base0,
+                                             const uint64_t (&x)[WG])
+{
+    if (x[0] < base0) return 0;  // below tile 0's first word: below every first key
+    const uint64_t b = (x[0] - base0) >> shift;
+    uint32_t l = b < m ? T[b] : T[m], h = b < m ? T[b + 1] : nt;
+    while (l < h) {
+        const uint32_t mid = (l + h) >> 1;
+        uint64_t f[WG];
+#pragma unroll
+        for (int j = 0; j < WG; ++j) f[j] = lf[(size_t)j * nt + mid];
+        const bool below = LE ? !key_lt<WG>(x, f) : key_lt<WG>(f, x);
+        l = below ? mid + 1 : l;
+        h = below ? h : mid;
+    }
+    return l;
+}
+
+template <int WG>
+__global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt, ProbeView p,
+                                                           const uint64_t *clo,
+                                                           const uint64_t *chi, ProbeWork work,
+                                                           uint8_t *flags)
+{
+    extern __shared__ __attribute__((aligned(16))) uint64_t lds64[];
+    const uint32_t nt = ct.ntiles;
+    const CLocLds L = cloc_lds(ct);
+    char *lb = (char *)lds64;
+    uint64_t *lf = (uint64_t *)(lb + L.first);
+    uint16_t *T = (uint16_t *)(lb + L.trad);
+    uint32_t *hist = (uint32_t *)(lb + L.hist);
+    const uint32_t g = xcd_chunk(blockIdx.x, (work.G + 7) / 8);
+    if (g >= work.G) return;
+    if (g == 0 && threadIdx.x < 2) work.item_off[threadIdx.x] = 0;  // the plan's overflow counters
+    const uint32_t c0 = g * work.chunk, c1 = min(p.n, c0 + work.chunk);
+    // every probe load of the chunk first (read-once inputs: non-temporal)
+    uint64_t lo[kCLocP][WG], hi[kCLocP][WG], snap[kCLocP];
+    uint32_t gg[kCLocP];
+#pragma unroll
+    for (int k = 0; k < kCLocP; ++k) {
+        const uint32_t q0 = c0 + threadIdx.x + kCLocThreads * k;
+        const uint32_t q = q0 < c1 ? q0 : 0;  // chunks past the ranges (lock probes only) read row 0
+        const bool v = p.n != 0;
+        gg[k] = v ? __builtin_nontemporal_load(p.gid + q) : 0;
+        snap[k] = v ? __builtin_nontemporal_load(p.snap + q) : 0;
+#pragma unroll
+        for (int j = 0; j < WG; ++j) {
+            const bool u = v && j < ct.WC;
+            lo[k][j] = u ? __builtin_nontemporal_load(clo + (size_t)j * p.n + q) : 0;
+            hi[k][j] = u ? __builtin_nontemporal_load(chi + (size_t)j * p.n + q) : 0;
+        }
+    }
+    {  // first keys, bucket table, histogram into LDS
+        const uint32_t nf = WG * nt;
+        for (uint32_t i = threadIdx.x; i < nf; i += kCLocThreads) lf[i] = ct.first[i];
+        for (uint32_t i = threadIdx.x; i <= ct.trad_m; i += kCLocThreads) T[i] = (uint16_t)ct.trad[i];
+        for (uint32_t i = threadIdx.x; i < nt; i += kCLocThreads) hist[i] = 0;
+    }
+    const int shift = (int)ct.trad[ct.trad_m + 1];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kCLocP; ++k) {
+        const uint32_t q = c0 + threadIdx.x + kCLocThreads * k;
+        if (q >= c1) continue;
+        uint64_t a_[WG], b_[WG];
+        compose<WG>(gg[k], ct.gb, lo[k], a_);
+        compose<WG>(gg[k], ct.gb, hi[k], b_);
+        uint2 sl = make_uint2(kNoSlot, kNoSlot);
+        if (!key_lt<WG>(b_, a_)) {
+            const uint32_t ca = ct_count<WG, false>(lf, nt, T, ct.trad_m, shift, ct.base0, a_);
+            const uint32_t cb = ct_count<WG, true>(lf, nt, T, ct.trad_m, shift, ct.base0, b_);
+            if (cb > 0) {
+                const uint32_t a = ca ? ca - 1 : 0, bt = cb - 1;
+                const uint32_t txn = p.txn[q];
+                // tiles strictly between the end tiles lie inside the range
+                if (bt > a + 1 && tiles_max(wt, a + 1, bt - 1) > snap[k]) flags[txn] = 1;
+                sl.x = a << 12 | atomicAdd(&hist[a], 1u);
+                if (bt > a) {
+                    sl.x |= kSecondRec;
+                    sl.y = bt << 12 | atomicAdd(&hist[bt], 1u);
+                }
+                // entry: lo[0..2], hi[0..2] (words past WG zero), r(S) | read set << 32
+                uint64_t f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+                for (int j = 0; j < WG; ++j) f[j] = a_[j], f[3 + j] = b_[j];
+                f[6] = (uint64_t)lsn32_rank(snap[k], ct.rank_base) | (uint64_t)txn << 32;
+                u64x2 *e = (u64x2 *)(ct.ent + (size_t)q * 8);
+#pragma unroll
+                for (int h = 0; h < 4; ++h) e[h] = u64x2{f[2 * h], f[2 * h + 1]};
+            }
+        }
+        ct.slot[q] = sl;
+    }
+    // table locks: any write to a locked table after the snapshot
+    for (uint32_t q = g * kCLocThreads + threadIdx.x; q < p.n_lock; q += work.G * kCLocThreads) {
+        const uint32_t t = p.lock_table[q];
+        if (t < wt.ntables && wt.table_max[t] > p.lock_snap[q]) flags[p.lock_txn[q]] = 1;
+    }
+    __syncthreads();
+    const uint32_t hs = hist_stride(work.G);
+    for (uint32_t i = threadIdx.x; i < nt; i += kCLocThreads) work.hist[(size_t)i * hs + g] = hist[i];
+}
+
+// ---- scatter: 4-byte bucket entries ----
+__device__ __forceinline__ uint32_t ct_bucket_slot(const ProbeWork &work, uint32_t ntiles, uint32_t t,
+                                                   uint32_t pos)
+{
+    return pos < kTileCap ? t * kTileCap + pos
+                          : ntiles * kTileCap + work.bucket_off[t] + (pos - kTileCap);
+}
+
+__global__ __launch_bounds__(kCLocThreads) void k_scatter_c(CTiles ct, ProbeWork work, uint32_t n)
+{
+    extern __shared__ uint32_t soff[];  // [ntiles] this chunk's offset in each bucket
+    const uint32_t g = xcd_chunk(blockIdx.x, (work.G + 7) / 8);
+    if (g >= work.G) return;
+    const uint32_t nt = ct.ntiles;
+    const uint32_t c0 = g * work.chunk, c1 = min(n, c0 + work.chunk);
+    uint2 s[kCLocP];
+#pragma unroll
+    for (int k = 0; k < kCLocP; ++k) {
+        const uint32_t q = c0 + threadIdx.x + kCLocThreads * k;
+        s[k] = q < c1 ? ct.slot[q] : make_uint2(kNoSlot, kNoSlot);
+    }
+    const size_t hs = hist_stride(work.G);
+    for (uint32_t t = threadIdx.x; t < nt; t += kCLocThreads) soff[t] = work.hist[t * hs + g];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kCLocP; ++k) {
+        if (s[k].x == kNoSlot) continue;
+        const uint32_t q = c0 + threadIdx.x + kCLocThreads * k;
+        const bool two = (s[k].x & kSecondRec) != 0;
+        const uint32_t ta = (s[k].x & ~kSecondRec) >> 12;
+        ct.recs[ct_bucket_slot(work, nt, ta, soff[ta] + (s[k].x & 0xFFFu))] =
+            q | (two ? kCHead : kCFull) << 30;
+        if (two) {
+            const uint32_t tb = s[k].y >> 12;
+            ct.recs[ct_bucket_slot(work, nt, tb, soff[tb] + (s[k].y & 0xFFFu))] = q | kCTail << 30;
+        }
+    }
+}
+
+// ---- join ----
+// key at Eytzinger slot j vs x: word 0 decides unless equal
+template <int WG>
+__device__ __forceinline__ bool slot_lt(const uint64_t *kw, uint32_t j, const uint64_t (&x)[WG])
+{
+#pragma unroll
+    for (int w = 0; w < WG - 1; ++w) {
+        const uint64_t v = kw[(size_t)w * kCTRows + j];
+        if (v != x[w]) return v < x[w];
+    }
+    return kw[(size_t)(WG - 1) * kCTRows + j] < x[WG - 1];
+}
+
+template <int WG>
+__device__ __forceinline__ bool slot_le(const uint64_t *kw, uint32_t j, const uint64_t (&x)[WG])
+{
+#pragma unroll
+    for (int w = 0; w < WG - 1; ++w) {
+        const uint64_t v = kw[(size_t)w * kCTRows + j];
+        if (v != x[w]) return v < x[w];
+    }
+    return kw[(size_t)(WG - 1) * kCTRows + j] <= x[WG - 1];
+}
+
+template <int WG>
+__global__ __launch_bounds__(kJoinThreads) void k_join_c(ProbeWork work, CTiles ct, uint8_t *flags)
+{
+    constexpr uint32_t T = kCTRows;
+    constexpr int RQ = T / (4 * kJoinThreads);  // row quads per thread (1)
+    constexpr int kRec = kJoinChunk / kJoinThreads;
+    static_assert(RQ >= 1, "a row quad per thread");
+    extern __shared__ __attribute__((aligned(16))) uint64_t jl[];
+    uint64_t *kw = jl;                                   // [WG][T], Eytzinger order
+    uint32_t *rank = (uint32_t *)(jl + (size_t)WG * T);  // [T], sorted order
+    uint32_t *b16 = rank + T;                            // [T / 16]
+    uint32_t *b128 = b16 + T / 16;                       // [T / 128]
+    const uint32_t ntiles = ct.ntiles;
+    // blocks past the tiles take the hot tiles' overflow items in turn
+    const uint32_t nextra = blockIdx.x < ntiles ? 1 : work.item_off[1];
+    const uint32_t stride = gridDim.x > ntiles ? gridDim.x - ntiles : 1;  // >= 1: every loop ends
+    for (uint32_t xi = blockIdx.x < ntiles ? 0 : blockIdx.x - ntiles; xi < nextra; xi += stride) {
+        __syncthreads();  // the previous item's LDS reads are done
+        uint32_t tile, r0, r1;
+        if (blockIdx.x < ntiles) {
+            tile = blockIdx.x;
+        } else {
+            const uint4 d = work.item_desc[xi];
+            tile = d.x, r0 = d.y, r1 = d.z;
+        }
+        const size_t ts = (size_t)tile << kCTLog2;
+        u64x2 kv[RQ][WG][2];
+        u32x4 rr[RQ];
+#pragma unroll
+        for (int v = 0; v < RQ; ++v) {
+            const size_t row = ts + 4 * (threadIdx.x + kJoinThreads * v);
+#pragma unroll
+            for (int w = 0; w < WG; ++w) {
+                kv[v][w][0] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row);
+                kv[v][w][1] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row + 2);
+            }
+            rr[v] = *(const u32x4 *)(ct.rank + row);
+        }
+        if (blockIdx.x < ntiles) {
+            r0 = tile * kTileCap;
+            r1 = r0 + min(kTileCap, work.counts[tile]);
+        }
+        if (r0 >= r1) continue;  // a tile no range reaches (uniform across the block)
+        uint32_t ev[kRec];
+#pragma unroll
+        for (int k = 0; k < kRec; ++k) ev[k] = ct.recs[min(r0 + k * kJoinThreads + threadIdx.x, r1 - 1)];
+        u64x2 pe[kRec][4];
+#pragma unroll
+        for (int k = 0; k < kRec; ++k) {
+            const u64x2 *e = (const u64x2 *)(ct.ent + (size_t)(ev[k] & 0x3FFFFFFFu) * 8);
+#pragma unroll
+            for (int h = 0; h < 4; ++h) pe[k][h] = e[h];
+        }
+#pragma unroll
+        for (int v = 0; v < RQ; ++v) {
+            const uint32_t quad = threadIdx.x + kJoinThreads * v;
+#pragma unroll
+            for (int w = 0; w < WG; ++w) {
+                *(u64x2 *)(kw + (size_t)w * T + 4 * quad) = kv[v][w][0];
+                *(u64x2 *)(kw + (size_t)w * T + 4 * quad + 2) = kv[v][w][1];
+            }
+            ((u32x4 *)rank)[quad] = rr[v];
+            uint32_t m = max(max(rr[v].x, rr[v].y), max(rr[v].z, rr[v].w));
+            m = max(m, (uint32_t)__shfl_xor((int)m, 1, 64));
+            m = max(m, (uint32_t)__shfl_xor((int)m, 2, 64));
+            if ((threadIdx.x & 3) == 0) b16[quad >> 2] = m;
+#pragma unroll
+            for (int d = 4; d < 32; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+            if ((threadIdx.x & 31) == 0) b128[quad >> 5] = m;
+        }
+        __syncthreads();
+        const uint32_t tn = min(T, ct.n - (uint32_t)ts);
+#pragma unroll
+        for (int k = 0; k < kRec; ++k) {
+            const uint32_t r = r0 + k * kJoinThreads + threadIdx.x;
+            if (r >= r1) continue;
+            const uint32_t kind = ev[k] >> 30;
+            uint64_t lo[WG], hi[WG];
+            const uint64_t f[6] = {pe[k][0].x, pe[k][0].y, pe[k][1].x,
+                                   pe[k][1].y, pe[k][2].x, pe[k][2].y};
+#pragma unroll
+            for (int w = 0; w < WG; ++w) lo[w] = f[w], hi[w] = f[3 + w];
+            const uint32_t rs = (uint32_t)pe[k][3].x, txn = (uint32_t)(pe[k][3].x >> 32);
+            // pa = #keys < lo, pb = #keys <= hi: root-to-leaf walks of the
+            // Eytzinger tree in lockstep; padding keys (~0) are above every bound
+            uint32_t ja = 1, jb = 1;
+#pragma unroll
+            for (int d = 0; d < kCTLog2; ++d) {
+                const bool ga = slot_lt<WG>(kw, ja, lo), gb = slot_le<WG>(kw, jb, hi);
+                ja = 2 * ja + ga;
+                jb = 2 * jb + gb;
+            }
+            uint32_t pa = min(ja - T + slot_lt<WG>(kw, 0, lo), tn);
+            uint32_t pb = min(jb - T + slot_le<WG>(kw, 0, hi), tn);
+            if (kind == kCTail) pa = 0;
+            if (kind == kCHead) pb = tn;
+            if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) flags[txn] = 1;
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *gid,
+                        const uint64_t *lsn, const CTiles &ct, uint64_t *key, uint32_t *rank,
+                        uint64_t *first, uint64_t *rel, uint32_t *trad, hipStream_t s)
+{
+    if (ct.len == 0 || ct.ntiles == 0) return hipSuccess;
+    const uint32_t blocks = (uint32_t)((ct.len + 255) / 256);
+    switch (ct.WG) {
+    case 1: k_ct_rows<1><<<blocks, 256, 0, s>>>(cw, cs, WC, gid, lsn, ct, key, rank, first); break;
+    case 2: k_ct_rows<2><<<blocks, 256, 0, s>>>(cw, cs, WC, gid, lsn, ct, key, rank, first); break;
+    case 3: k_ct_rows<3><<<blocks, 256, 0, s>>>(cw, cs, WC, gid, lsn, ct, key, rank, first); break;
+    default: return hipErrorInvalidValue;
+    }
+    k_ct_rel<<<(ct.ntiles + 255) / 256, 256, 0, s>>>(first, ct.ntiles, rel);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return narrow_trad_build(rel, ct.ntiles, ct.trad_m, trad, s);
+}
+
+size_t ctiles_locate_lds(const CTiles &ct) { return cloc_lds(ct).bytes; }
+uint32_t ctiles_chunk() { return kCChunk; }
+
+hipError_t launch_locate_c(const CTiles &ct, const WinView &wt, const ProbeView &p,
+                           const uint64_t *clo, const uint64_t *chi, const ProbeWork &work,
+                           uint8_t *flags, hipStream_t s)
+{
+    if (p.n == 0 && p.n_lock == 0) return hipSuccess;
+    const size_t lds = cloc_lds(ct).bytes;
+    const uint32_t blocks = 8 * ((work.G + 7) / 8);
+    switch (ct.WG) {
+    case 1: k_locate_c<1><<<blocks, kCLocThreads, lds, s>>>(ct, wt, p, clo, chi, work, flags); break;
+    case 2: k_locate_c<2><<<blocks, kCLocThreads, lds, s>>>(ct, wt, p, clo, chi, work, flags); break;
+    case 3: k_locate_c<3><<<blocks, kCLocThreads, lds, s>>>(ct, wt, p, clo, chi, work, flags); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter_c(const CTiles &ct, const ProbeWork &work, uint32_t n, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    k_scatter_c<<<8 * ((work.G + 7) / 8), kCLocThreads, 4 * (size_t)ct.ntiles, s>>>(ct, work, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_items,
+                         uint8_t *flags, hipStream_t s)
+{
+    if (max_items == 0 || ct.n == 0 || ct.ntiles == 0) return hipSuccess;
+    const uint32_t extra = max_items - ct.ntiles;
+    const uint32_t blocks = ct.ntiles + (extra < 512 ? extra : 512);
+    const size_t lds = 8 * (size_t)ct.WG * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
+                       4 * (kCTRows / 128);
+    switch (ct.WG) {
+    case 1: k_join_c<1><<<blocks, kJoinThreads, lds, s>>>(work, ct, flags); break;
+    case 2: k_join_c<2><<<blocks, kJoinThreads, lds, s>>>(work, ct, flags); break;
+    case 3: k_join_c<3><<<blocks, kJoinThreads, lds, s>>>(work, ct, flags); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace hsc

@@ -217,4 +217,40 @@ __device__ __forceinline__ bool lds_any_after(const uint64_t *lsn, const uint64_
            any_gt<NB256>(b256, bp256 >> 4, bq256 >> 4, snap);
 }
 
+// u32 variants over 32-bit commit times (narrow and compact tiles): any
+// rank > s in [from, to) (to - from <= N), and in rows [p, q) of a tile with
+// 16- and 128-row block maxima b16 / b128.
+template <int N>
+__device__ __forceinline__ bool any_gt32(const uint32_t *a, uint32_t from, uint32_t to, uint32_t s)
+{
+    bool r = false;
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const uint32_t i = from + k;
+        const uint32_t v = a[i < to ? i : from];
+        r |= (i < to) & (v > s);
+    }
+    return r;
+}
+
+__device__ __forceinline__ bool any_after32(const uint32_t *rank, const uint32_t *b16,
+                                            const uint32_t *b128, uint32_t p, uint32_t q,
+                                            uint32_t s)
+{
+    const uint32_t q1 = q - 1;
+    const bool hot_p = b16[p >> 4] > s, hot_q = b16[q1 >> 4] > s;
+    if (!hot_p && !hot_q && (q1 >> 4) <= (p >> 4) + 1) return false;
+    if (q - p <= 16) return any_gt32<16>(rank, p, q, s);
+    const uint32_t p16 = (p + 15) & ~15u, q16 = q & ~15u;
+    const uint32_t bp = p16 >> 4, bq = q16 >> 4;
+    const uint32_t bp8 = min((bp + 7) & ~7u, bq), bq8 = max(bq & ~7u, bp8);
+    bool r = false;
+    if (hot_p) r |= any_gt32<15>(rank, p, p16, s);
+    if (hot_q) r |= any_gt32<15>(rank, q16, q, s);
+    r |= any_gt32<7>(b16, bp, bp8, s);
+    r |= any_gt32<7>(b16, bq8, bq, s);
+    if (bp8 < bq8) r |= any_gt32<32>(b128, bp8 >> 3, bq8 >> 3, s);
+    return r;
+}
+
 }  // namespace hsc

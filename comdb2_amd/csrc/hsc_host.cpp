@@ -227,6 +227,11 @@ struct hsc_ctx {
     CompactTables ct{};
     WinView wc{};
     DBuf d_cmask, d_cpat, d_cmv, d_cbits, d_cwords, d_ctmax, d_csp_g, d_csp_w;
+    int ct_maxbits = 0;  // most varying bits of any group
+    // compact tiles (hsc_ctiles.hip): the compact window as gid || code keys
+    bool ctiles = false;
+    CTiles ctv{};
+    DBuf d_ckey, d_crank, d_cfirst, d_crel, d_ctrad;
 
     // probe workspace
     DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;
@@ -540,6 +545,7 @@ static int build_compact(hsc_ctx *c, const WinView &w)
         maxbits = std::max(maxbits, b);
     }
     const int WC = maxbits / 64 + 1;  // >= 1 spare bit: all-ones is above every code
+    c->ct_maxbits = maxbits;
     if (WC >= W || WC > kMaxCompactWords) return HSC_OK;
     HIPCHK(c, c->d_cmv.ensure(8 * gw * 6));
     HIPCHK(c, c->d_cbits.ensure(4 * (size_t)ng));
@@ -570,6 +576,51 @@ static int build_compact(hsc_ctx *c, const WinView &w)
     v.gstart = c->d_gstart.as<uint32_t>();
     v.gend = c->d_gend.as<uint32_t>();
     c->compact = true;
+    return HSC_OK;
+}
+
+// Compact tiles over the compact view c->wc (hsc_ctiles.hip): keys gid ||
+// code of WG <= 3 words, 32-bit commit times.  Needs the view's 2048-row
+// tiles, commits spanning < 2^32 of log, a tile count the locate's bucket
+// table and LDS take; otherwise dense batches stay on the wide pipeline.
+static int build_ctiles(hsc_ctx *c)
+{
+    const WinView &v = c->wc;
+    const int ng = (int)c->groups.size();
+    int gb = 0;
+    while (gb < 32 && ((size_t)1 << gb) < (size_t)ng) gb++;
+    const int WG = (c->ct_maxbits + gb + 1 + 63) / 64;  // a spare bit: ~0 is above every key
+    if (v.log2T != kCTLog2 || WG > 3 || WG < c->ct.WC || c->ncommit == 0 ||
+        c->commit_span[1] - c->commit_span[0] > kLsn32MaxSpan)
+        return HSC_OK;
+    CTiles &ct = c->ctv;
+    ct = CTiles{};
+    ct.n = (uint32_t)c->n;
+    ct.ntiles = v.ntiles;
+    ct.len = (size_t)v.ntiles << kCTLog2;
+    ct.WG = WG;
+    ct.WC = c->ct.WC;
+    ct.gb = gb;
+    ct.rank_base = c->commit_span[0];
+    ct.trad_m = narrow_trad_buckets(ct.ntiles);
+    if (ct.trad_m == 0 || ct.ntiles > (uint32_t)kHistCap || ctiles_locate_lds(ct) > 65536)
+        return HSC_OK;
+    hipStream_t s = c->stream;
+    HIPCHK(c, c->d_ckey.ensure(8 * (size_t)WG * ct.len));
+    HIPCHK(c, c->d_crank.ensure(4 * ct.len));
+    HIPCHK(c, c->d_cfirst.ensure(8 * (size_t)WG * ct.ntiles));
+    HIPCHK(c, c->d_crel.ensure(8 * (size_t)ct.ntiles));
+    HIPCHK(c, c->d_ctrad.ensure(4 * ((size_t)ct.trad_m + 2)));
+    ct.key = c->d_ckey.as<uint64_t>();
+    ct.rank = c->d_crank.as<uint32_t>();
+    ct.first = c->d_cfirst.as<uint64_t>();
+    ct.trad = c->d_ctrad.as<uint32_t>();
+    HIPCHK(c, ctiles_build(v.words, v.stride, ct.WC, v.gid, v.lsn, ct, c->d_ckey.as<uint64_t>(),
+                           c->d_crank.as<uint32_t>(), c->d_cfirst.as<uint64_t>(),
+                           c->d_crel.as<uint64_t>(), c->d_ctrad.as<uint32_t>(), s));
+    HIPCHK(c, hipMemcpyAsync(&ct.base0, c->d_cfirst.p, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    c->ctiles = true;
     return HSC_OK;
 }
 
@@ -692,8 +743,12 @@ static int device_build(hsc_ctx *c, size_t n_in)
     c->compact = false;
     uint32_t wide32 = 1;   // narrow tiles: a tile spans >= 2^32 codes (device flag)
     bool tiles32 = false;
-    if (!c->narrow && c->layout == HSC_LAYOUT_AUTO && c->n > 0 && W > 1 && ng > 0)
+    c->ctiles = false;
+    if (!c->narrow && (c->layout == HSC_LAYOUT_AUTO || c->layout == HSC_LAYOUT_COMPACT_WIDE) &&
+        c->n > 0 && W > 1 && ng > 0) {
         HIPCHK_RC(c, build_compact(c, w));
+        if (c->compact) HIPCHK_RC(c, build_ctiles(c));
+    }
     if (c->narrow) {
         // level sizes: level 0 = n + 1 rounded up to whole tiles (at least one
         // pad; the tile pipeline stages whole tiles), then roundup16(len / 16)
@@ -1681,6 +1736,76 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     return HSC_OK;
 }
 
+// Compact tiles (dense or sparse batch over a compact window): code bounds
+// (compact_probes) -> locate (gid || code keys, end tiles, 64-byte probe
+// entries) -> plan -> scatter (4-byte bucket entries) -> join -> pack.
+static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p)
+{
+    hipStream_t s = c->stream;
+    const WinView w = win_view(c);
+    CTiles ct = c->ctv;
+    c->probe_ntiles = ct.ntiles;
+    c->probe_buckets = true;
+    const uint32_t nt = std::max<uint32_t>(ct.ntiles, 1);
+    ProbeWork work{};
+    work.lds_mode = 1;
+    work.chunk = ctiles_chunk();
+    work.G = (uint32_t)std::max<size_t>(1, (std::max<size_t>(p.n, p.n_lock) + work.chunk - 1) / work.chunk);
+    const size_t n1 = std::max<uint32_t>(p.n, 1);
+    const int WC = c->ct.WC;
+    HIPCHK(c, c->p_code_lo.ensure(8 * (size_t)WC * n1));
+    HIPCHK(c, c->p_code_hi.ensure(8 * (size_t)WC * n1));
+    HIPCHK(c, c->w_hist.ensure(4 * (size_t)hist_stride(work.G) * nt));
+    HIPCHK(c, c->w_counts.ensure(4 * ((size_t)nt + 1)));
+    HIPCHK(c, c->w_bucket.ensure(4 * ((size_t)nt + 1)));
+    HIPCHK(c, c->w_items.ensure(4 * std::max<size_t>((size_t)nt + 1, 4)));
+    const uint32_t extra_items = 2 * (uint32_t)((2 * n1 + kJoinChunk - 1) / kJoinChunk);
+    const uint32_t max_items = nt + extra_items;
+    HIPCHK(c, c->w_item_desc.ensure(16 * (size_t)extra_items + 16));
+    HIPCHK(c, c->w_tcode.ensure(64 * n1));   // probe entries
+    HIPCHK(c, c->w_tcode2.ensure(8 * n1));   // slots
+    HIPCHK(c, c->w_trecs.ensure(4 * ((size_t)nt * kTileCap + 2 * n1)));
+    work.hist = c->w_hist.as<uint32_t>();
+    work.counts = c->w_counts.as<uint32_t>();
+    work.bucket_off = c->w_bucket.as<uint32_t>();
+    work.item_off = c->w_items.as<uint32_t>();
+    work.item_desc = c->w_item_desc.as<uint4>();
+    ct.ent = c->w_tcode.as<uint64_t>();
+    ct.slot = c->w_tcode2.as<uint2>();
+    ct.recs = c->w_trecs.as<uint32_t>();
+    const size_t had = c->w_vflags.bytes;
+    HIPCHK(c, c->w_vflags.ensure(std::max<size_t>(b->n_txn, 1)));
+    if (c->w_vflags.bytes != had) HIPCHK(c, hipMemsetAsync(c->w_vflags.p, 0, c->w_vflags.bytes, s));
+    uint8_t *flags = c->w_vflags.as<uint8_t>();
+    WinView wt = c->wc;  // tile maxima of the same 2048-row tiles
+    wt.table_max = w.table_max;
+    wt.ntables = w.ntables;
+    const bool tm = c->timing;
+    if (tm)
+        for (int i = 0; i < 6; ++i)
+            if (!c->ev[i]) HIPCHK(c, hipEventCreate(&c->ev[i]));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
+    if (p.n)
+        HIPCHK(c, compact_probes(p, c->ct, c->p_code_lo.as<uint64_t>(), c->p_code_hi.as<uint64_t>(), s));
+    HIPCHK(c, launch_locate_c(ct, wt, p, c->p_code_lo.as<uint64_t>(), c->p_code_hi.as<uint64_t>(),
+                              work, flags, s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
+    if (p.n && ct.ntiles) {
+        HIPCHK(c, launch_plan_t(work, ct.ntiles, c->w_items.as<uint32_t>(), s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
+        HIPCHK(c, launch_scatter_c(ct, work, p.n, s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
+        HIPCHK(c, launch_join_c(ct, work, max_items, flags, s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
+    } else if (tm) {
+        for (int i = 2; i <= 4; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
+    }
+    HIPCHK_RC(c, probe_delta(c, flags));
+    HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
+    if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
+    return HSC_OK;
+}
+
 static int probe_lane(hsc_ctx *c, const hsc_probe_batch *b);
 static int probe(hsc_ctx *c, const hsc_probe_batch *b)
 {
@@ -1725,6 +1850,10 @@ static int probe_lane(hsc_ctx *c, const hsc_probe_batch *b)
     p.n_lock = (uint32_t)b->n_lock;
     c->raw_probe = p;
     c->raw_probe.n = (uint32_t)b->n;  // the delta may hold keys of an empty main window
+    if (!c->narrow && c->compact && c->ctiles && c->layout != HSC_LAYOUT_COMPACT_WIDE &&
+        p.n < (1u << 30) &&
+        (std::max<size_t>(p.n, p.n_lock) + ctiles_chunk() - 1) / ctiles_chunk() <= (size_t)kMaxChunks)
+        return probe_ctiles(c, b, p);
     if (!c->narrow && c->compact) {
         // wide keys as compact codes: map the bounds, then the tile pipeline
         const int WC = c->ct.WC;
@@ -2209,8 +2338,8 @@ int hsc_window_ingest_device(hsc_ctx *c, size_t n, int words, const uint32_t *gi
 
 int hsc_set_layout(hsc_ctx *c, int layout)
 {
-    if (!c || layout < HSC_LAYOUT_AUTO || layout > HSC_LAYOUT_NARROW_CODES ||
-        layout == HSC_LAYOUT_NARROW)
+    if (!c || layout < HSC_LAYOUT_AUTO || layout > HSC_LAYOUT_COMPACT_WIDE ||
+        layout == HSC_LAYOUT_NARROW || layout == HSC_LAYOUT_COMPACT)
         return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     const bool rebuild = (c->layout == HSC_LAYOUT_WIDE) != (layout == HSC_LAYOUT_WIDE);
@@ -2229,6 +2358,7 @@ int hsc_window_layout(hsc_ctx *c)
 }
 
 int hsc_window_code_words(hsc_ctx *c) { return c && c->compact ? c->ct.WC : c ? c->W : 0; }
+int hsc_window_tile_key_words(hsc_ctx *c) { return c && c->compact && c->ctiles ? c->ctv.WG : 0; }
 
 int hsc_window_words(hsc_ctx *c) { return c ? c->W : 0; }
 size_t hsc_window_keys(hsc_ctx *c) { return c ? c->n : 0; }

@@ -408,6 +408,36 @@ hipError_t compact_rows(const uint64_t *words, size_t stride, const uint32_t *gi
 // miss their group's rows become (~0, 0)
 hipError_t compact_probes(const ProbeView &p, const CompactTables &t, uint64_t *clo, uint64_t *chi,
                           hipStream_t s);
+// Compact tiles (hsc_ctiles.hip): the compact window as one sorted array of
+// WG-word keys gid || code (WG <= 3) with 32-bit commit times, 2048-row
+// tiles, for dense batches.
+constexpr int kCTLog2 = 11;
+struct CTiles {
+    const uint64_t *key;     // [WG][len] row keys, Eytzinger order per tile (padding ~0)
+    const uint32_t *rank;    // [len] lsn - rank_base + 1 in row order (padding 0)
+    const uint64_t *first;   // [WG][ntiles] first key of every tile
+    const uint32_t *trad;    // [trad_m + 2] bucket table over first word 0 - base0
+    uint32_t trad_m;
+    uint64_t base0;          // word 0 of tile 0's first key
+    uint64_t rank_base;      // oldest commit LSN of the window
+    size_t len;              // row stride (n rounded up to whole tiles)
+    uint32_t n, ntiles;
+    int WG, WC, gb;          // key words, code words, group bits
+    uint64_t *ent;           // [n][8] probe entries {lo[3], hi[3], r(S) | read set << 32, 0}
+    uint2 *slot;             // [n] (tile << 12 | in-chunk rank) of the first / second record
+    uint32_t *recs;          // bucket entries: probe | kind << 30
+};
+hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *gid,
+                        const uint64_t *lsn, const CTiles &ct, uint64_t *key, uint32_t *rank,
+                        uint64_t *first, uint64_t *rel, uint32_t *trad, hipStream_t s);
+size_t ctiles_locate_lds(const CTiles &ct);
+uint32_t ctiles_chunk();
+hipError_t launch_locate_c(const CTiles &ct, const WinView &wt, const ProbeView &p,
+                           const uint64_t *clo, const uint64_t *chi, const ProbeWork &work,
+                           uint8_t *flags, hipStream_t s);
+hipError_t launch_scatter_c(const CTiles &ct, const ProbeWork &work, uint32_t n, hipStream_t s);
+hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_items,
+                         uint8_t *flags, hipStream_t s);
 // Sharded SCC (hsc_graph.hip): cover[v] = 1 iff v lies inside [dst, src] of a
 // backward edge of g; the edges of g between covered nodes -> g.cut rows
 // (src << 32 | dst, *m of them); SCC of the graph induced on the cover by

@@ -140,7 +140,7 @@ EXPORTS = [
     "hsc_enable_timing", "hsc_dep_graph_scc", "hsc_dep_graph_edges",
     "hsc_window_ingest_raw", "hsc_decode_log", "hsc_decode_serial", "hsc_check_serial",
     "hsc_set_layout", "hsc_window_layout", "hsc_coalesce_readsets", "hsc_rw_edges",
-    "hsc_window_code_words", "hsc_window_append_log", "hsc_window_append_raw",
+    "hsc_window_code_words", "hsc_window_tile_key_words", "hsc_window_append_log", "hsc_window_append_raw",
     "hsc_window_delta_rows", "hsc_set_threads", "hsc_currangearrs_build",
     "hsc_currangearrs_free", "hsc_collector_create", "hsc_collector_destroy",
     "hsc_collector_check", "hsc_collector_get_stats", "hsc_harness_concurrent",
@@ -148,7 +148,7 @@ EXPORTS = [
 ]
 
 (LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES,
- LAYOUT_NARROW_CODES, LAYOUT_COMPACT) = 0, 1, 2, 3, 4, 5, 6
+ LAYOUT_NARROW_CODES, LAYOUT_COMPACT, LAYOUT_COMPACT_WIDE) = 0, 1, 2, 3, 4, 5, 6, 7
 
 _lib: Optional[C.CDLL] = None
 
@@ -178,6 +178,7 @@ def load() -> C.CDLL:
         "hsc_window_ingest_device": (C.c_int, [_p, C.c_size_t, C.c_int, _p, _p, _p, C.c_uint64]),
         "hsc_window_words": (C.c_int, [_p]),
         "hsc_window_code_words": (C.c_int, [_p]),
+        "hsc_window_tile_key_words": (C.c_int, [_p]),
         "hsc_window_keys": (C.c_size_t, [_p]),
         "hsc_window_end": (C.c_uint64, [_p]),
         "hsc_window_max_commit": (C.c_uint64, [_p]),
@@ -550,6 +551,12 @@ class Validator:
     def code_words(self) -> int:
         """Words per probed window row (compact codes: WC < words)."""
         return self.lib.hsc_window_code_words(self.ctx)
+
+    @property
+    def tile_key_words(self) -> int:
+        """Compact windows: words of the compact-tile keys gid || code that
+        batches probe (hsc_ctiles.hip); 0 when the window has none."""
+        return self.lib.hsc_window_tile_key_words(self.ctx)
 
     @property
     def keys(self) -> int:

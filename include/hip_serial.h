@@ -311,11 +311,16 @@ enum {
     HSC_LAYOUT_NARROW_DIRECT = 3,
     HSC_LAYOUT_NARROW_TILES = 4,
     HSC_LAYOUT_NARROW_CODES = 5,
-    HSC_LAYOUT_COMPACT = 6  /* reported only: AUTO's wide window as per-group compact codes */
+    HSC_LAYOUT_COMPACT = 6, /* reported only: AUTO's wide window as per-group compact codes */
+    HSC_LAYOUT_COMPACT_WIDE = 7 /* AUTO, but compact windows probe through the wide tile
+                                   pipeline instead of the compact tiles -- testing */
 };
 int hsc_set_layout(hsc_ctx *ctx, int layout);
 int hsc_window_layout(hsc_ctx *ctx);         /* HSC_LAYOUT_WIDE, _NARROW or _COMPACT */
 int hsc_window_code_words(hsc_ctx *ctx);     /* words per probed row (compact: WC) */
+/* Compact windows: words of the compact-tile keys gid || code (1..3) that
+ * dense batches probe (hsc_ctiles.hip), 0 if the window has none. */
+int hsc_window_tile_key_words(hsc_ctx *ctx);
 int hsc_window_words(hsc_ctx *ctx);          /* key words per key (>= 1)     */
 size_t hsc_window_keys(hsc_ctx *ctx);        /* distinct (group, key) rows   */
 uint64_t hsc_window_end(hsc_ctx *ctx);

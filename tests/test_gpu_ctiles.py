@@ -1,0 +1,169 @@
+"""Compact tiles (hsc_ctiles.hip): compact windows whose gid || code keys fit
+<= 3 words are probed as one sorted array of wide keys with 32-bit commit
+times -- bucket-table locate, fixed-capacity tile buckets, 4-byte bucket
+entries, full-key Eytzinger joins.  Verdicts must equal the oracle's and the
+wide compact pipeline's (LAYOUT_COMPACT_WIDE) on the same windows: config 3,
+short composite keys with ties at every word, hot tiles that overflow their
+bucket, sparse batches and appended rows."""
+import numpy as np
+import pytest
+
+from comdb2_amd import formats as F
+from comdb2_amd.formats import LogBuilder, Range, ReadSets
+from comdb2_amd.hsc import LAYOUT_AUTO, LAYOUT_COMPACT, LAYOUT_COMPACT_WIDE, Validator
+
+pytestmark = pytest.mark.gpu
+
+ROWS = [0x00, 0x08, 0x61, 0x62]
+PROBE = [0x00, 0x07, 0x08, 0x09, 0x60, 0x61, 0x62, 0x63, 0xFF]
+
+
+def _short_case(seed, n_commits=3000, n_txn=900, lens=(9, 17, 23), n_tabs=4, hot=0.0):
+    """Keys of few varying bits per byte (codes + group id fit 3 words), probes
+    equal to rows, prefixes, one-byte edits, inverted and open ranges; hot > 0:
+    that share of ranges are points on a handful of keys (overflowing tiles)."""
+    rng = np.random.default_rng(seed)
+    lb = LogBuilder()
+    snaps = [lb.next_lsn()]
+    tabs = [f"t{i}" for i in range(n_tabs)]
+    keys = {}
+    for c in range(n_commits):
+        lb.begin(c)
+        for _ in range(int(rng.integers(1, 9))):
+            tb = tabs[int(rng.integers(0, n_tabs - 1))]  # the last table is never written
+            ix = int(rng.integers(0, len(lens)))
+            k = bytes([8]) + rng.choice(ROWS, size=lens[ix] - 1).astype(np.uint8).tobytes()
+            keys.setdefault((tb, ix), []).append(k)
+            lb.write(c, F.REC_UNDO_ADD_IX_LK, tb, ix, k)
+        snaps.append(lb.commit(c))
+    log = lb.build()
+    hot_keys = [(tb, ix, ks[int(rng.integers(0, len(ks)))]) for (tb, ix), ks in
+                sorted(keys.items())[:3]]
+
+    def key(tb, ix):
+        kl = lens[ix]
+        ks = keys.get((tb, ix))
+        if ks and rng.random() < 0.6:
+            k = bytearray(ks[int(rng.integers(0, len(ks)))])
+            if rng.random() < 0.3:
+                k[int(rng.integers(0, kl))] = int(rng.choice(PROBE))
+            cut = int(rng.integers(1, kl + 1)) if rng.random() < 0.25 else kl
+            return bytes(k[:cut])
+        return bytes(rng.choice(PROBE, size=int(rng.integers(1, kl + 1))).astype(np.uint8))
+
+    sets, ss = [], []
+    for t in range(n_txn):
+        rs = []
+        for _ in range(int(rng.integers(1, 9))):
+            if rng.random() < hot:
+                tb, ix, k = hot_keys[int(rng.integers(0, len(hot_keys)))]
+                rs.append(Range(tb, ix, k, k))
+                continue
+            tb = tabs[int(rng.integers(0, n_tabs))]
+            ix = int(rng.integers(0, len(lens)))
+            a, b = key(tb, ix), key(tb, ix)
+            u = rng.random()
+            if u < 0.4:
+                rs.append(Range(tb, ix, a, a))
+            elif u < 0.85:
+                rs.append(Range(tb, ix, min(a, b), max(a, b)))
+            elif u < 0.9:
+                rs.append(Range(tb, ix, max(a, b), min(a, b)))
+            elif u < 0.95:
+                rs.append(Range(tb, ix, None, a, lflag=1))
+            else:
+                rs.append(Range(tb, ix, a, None, rflag=1))
+        if rng.random() < 0.02:
+            rs.append(Range.locked(tabs[int(rng.integers(0, n_tabs))]))
+        rs.sort(key=lambda r: (r.tbname, -r.islocked, r.idxnum, r.lkey or b""))
+        sets.append(rs)
+        ss.append(snaps[int(rng.integers(max(0, len(snaps) - 300), len(snaps)))])
+    return log, ReadSets.from_lists(sets, ss, tbnames=lb.tbnames)
+
+
+def _both(v, log, rs):
+    """Verdicts through the compact tiles and through the wide compact pipeline."""
+    v.set_layout(LAYOUT_AUTO)
+    v.ingest_log(log)
+    assert v.layout == LAYOUT_COMPACT
+    assert 1 <= v.tile_key_words <= 3
+    got = v.check_readsets(rs) != 0
+    v.set_layout(LAYOUT_COMPACT_WIDE)
+    ref = v.check_readsets(rs) != 0
+    v.set_layout(LAYOUT_AUTO)
+    return got, ref
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_short_keys_match_oracle(oracle_mod, seed):
+    log, rs = _short_case(seed)
+    want = oracle_mod.check(log, rs, nthreads=8)[0] != 0
+    v = Validator(0)
+    try:
+        got, ref = _both(v, log, rs)
+    finally:
+        v.close()
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(ref, want)
+    assert 0.05 < want.mean() < 0.95
+
+
+def test_hot_tiles_overflow_match_oracle(oracle_mod):
+    """Half the ranges are points on three keys: their tiles take far more than
+    a bucket's 1024 records (overflow runs, extra join items)."""
+    log, rs = _short_case(21, n_commits=4000, n_txn=6000, hot=0.5)
+    want = oracle_mod.check(log, rs, nthreads=8)[0] != 0
+    v = Validator(0)
+    try:
+        got, ref = _both(v, log, rs)
+    finally:
+        v.close()
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(ref, want)
+
+
+def test_sparse_batch_matches_oracle(oracle_mod):
+    log, rs = _short_case(5, n_commits=6000, n_txn=20)
+    want = oracle_mod.check(log, rs, nthreads=8)[0] != 0
+    v = Validator(0)
+    try:
+        got, _ = _both(v, log, rs)
+    finally:
+        v.close()
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("kw", [dict(n_writes=40000, n_txn=2000),
+                                dict(seed=5, n_writes=80000, n_txn=3000, keys_per_commit=3)])
+def test_config3_matches_oracle(oracle_mod, kw):
+    from comdb2_amd.workloads import config3
+    log, rs = config3(**kw)
+    want = oracle_mod.check(log, rs, nthreads=8)[0] != 0
+    v = Validator(0)
+    try:
+        got, ref = _both(v, log, rs)
+        assert v.tile_key_words == 3 and v.code_words == 3
+    finally:
+        v.close()
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(ref, want)
+
+
+def test_appended_rows_match_oracle(oracle_mod):
+    """Rows appended after the build sit in the delta run, probed beside the
+    compact tiles into the same flags."""
+    from test_incremental import log_slice
+    log, rs = _short_case(9, n_commits=3000, n_txn=800)
+    want = oracle_mod.check(log, rs, nthreads=8)[0] != 0
+    cut = log.nrec * 3 // 4
+    v = Validator(0)
+    try:
+        v.ingest_log(log_slice(log, 0, cut))
+        v.check_readsets(rs)  # built: the rest goes to the delta run
+        assert v.layout == LAYOUT_COMPACT and v.tile_key_words >= 1
+        v.append_log(log_slice(log, cut, log.nrec))
+        assert v.delta_rows > 0
+        got = v.check_readsets(rs) != 0
+    finally:
+        v.close()
+    np.testing.assert_array_equal(got, want)
