@@ -117,6 +117,7 @@ __device__ __forceinline__ void fill_ones(uint64_t (&out)[WC], int from, int to)
 struct CompactMeta {
     const uint64_t *mask, *pat, *mv;  // [ng][W], [ng][W], [ng][W][6]
     const uint32_t *bits;             // [ng]: varying bits, kNoRows = group has no rows
+    const uint32_t *wlen;             // [ng]: words inside the group's key length
     int W, ng;
 };
 constexpr uint32_t kNoRows = 0xFFFFFFFFu;
@@ -339,7 +340,7 @@ constexpr int kBoundThreads = 256;
 constexpr uint32_t kBoundLdsBytes = 48 * 1024;
 __host__ __device__ inline uint32_t bound_lds_bytes(int ng, int W)
 {
-    return (uint32_t)ng * (uint32_t)W * 8 * 8 + 4 * (uint32_t)ng;
+    return (uint32_t)ng * (uint32_t)W * 8 * 8 + 8 * (uint32_t)ng;
 }
 
 struct BoundIn {
@@ -347,13 +348,18 @@ struct BoundIn {
     uint64_t xl[kProbeWords], xh[kProbeWords];
 };
 
-__device__ __forceinline__ void bound_load(const ProbeView &p, int W, uint32_t q, BoundIn &in)
+// Words past the group's key length are zero in every bound and row (the
+// marshal pads with zeros), so they are neither loaded nor mapped; the
+// marshal groups a batch's probes by that length, so whole waves skip them.
+__device__ __forceinline__ void bound_load(const ProbeView &p, const CompactMeta &cm, uint32_t q,
+                                           BoundIn &in)
 {
     const bool v = q < p.n;
     in.g = v ? p.gid[q] : 0;
+    const int wl = v ? (int)cm.wlen[in.g] : 0;
 #pragma unroll
     for (int j = 0; j < kProbeWords; ++j) {
-        const bool u = v && j < W;
+        const bool u = v && j < wl;
         in.xl[j] = u ? __builtin_nontemporal_load(p.lo + (size_t)j * p.n + q) : 0;
         in.xh[j] = u ? __builtin_nontemporal_load(p.hi + (size_t)j * p.n + q) : 0;
     }
@@ -372,10 +378,11 @@ __device__ __forceinline__ void bound_map(const ProbeView &p, const CompactMeta 
     if (ok) {
         const uint64_t *mk = cm.mask + (size_t)g * cm.W, *pt = cm.pat + (size_t)g * cm.W;
         const uint64_t *mvg = cm.mv + (size_t)g * cm.W * 6;
+        const int wl = (int)cm.wlen[g];
         int pos = 0, npl = -1, nph = -1, xbl = 0, xbh = 0;
 #pragma unroll
         for (int j = 0; j < kProbeWords; ++j) {
-            if (j >= cm.W) break;
+            if (j >= wl) break;  // past the key length: zero bound, zero mask
             const uint64_t m = mk[j], pj = pt[j];
             uint64_t mv[6];
 #pragma unroll
@@ -416,30 +423,34 @@ __global__ __launch_bounds__(kBoundThreads) void k_compact_bounds(ProbeView p, C
 {
     const uint32_t q0 = blockIdx.x * (kBoundThreads * P) + threadIdx.x;
     BoundIn cur;
-    bound_load(p, cm.W, q0, cur);
+    bound_load(p, cm, q0, cur);
     if constexpr (kLds) {
         extern __shared__ __attribute__((aligned(16))) uint64_t blds[];
         const uint32_t gw = (uint32_t)cm.ng * cm.W;
         uint64_t *lm = blds, *lp = blds + gw, *lv = blds + 2 * gw;
-        uint32_t *lb = (uint32_t *)(blds + 8 * gw);
+        uint32_t *lb = (uint32_t *)(blds + 8 * gw), *lw = lb + cm.ng;
         for (uint32_t i = threadIdx.x; i < gw; i += kBoundThreads) {
             lm[i] = cm.mask[i];
             lp[i] = cm.pat[i];
         }
         for (uint32_t i = threadIdx.x; i < 6 * gw; i += kBoundThreads) lv[i] = cm.mv[i];
-        for (uint32_t i = threadIdx.x; i < (uint32_t)cm.ng; i += kBoundThreads) lb[i] = cm.bits[i];
+        for (uint32_t i = threadIdx.x; i < (uint32_t)cm.ng; i += kBoundThreads) {
+            lb[i] = cm.bits[i];
+            lw[i] = cm.wlen[i];
+        }
         __syncthreads();
         cm.mask = lm;
         cm.pat = lp;
         cm.mv = lv;
         cm.bits = lb;
+        cm.wlen = lw;
     }
 #pragma unroll 1
     for (int j = 0; j < P; ++j) {
         const uint32_t q = q0 + j * kBoundThreads;
         if (q >= p.n) break;
         BoundIn nxt;
-        if (j + 1 < P) bound_load(p, cm.W, q + kBoundThreads, nxt);
+        if (j + 1 < P) bound_load(p, cm, q + kBoundThreads, nxt);
         bound_map<WC>(p, cm, q, cur, clo, chi);
         if (j + 1 < P) cur = nxt;
     }
@@ -477,7 +488,7 @@ hipError_t launch_probes_wc(const ProbeView &p, const CompactMeta &cm, uint64_t 
 
 CompactMeta meta_of(const CompactTables &t)
 {
-    return CompactMeta{t.mask, t.pat, t.mv, t.bits, t.W, t.ng};
+    return CompactMeta{t.mask, t.pat, t.mv, t.bits, t.wlen, t.W, t.ng};
 }
 
 }  // namespace

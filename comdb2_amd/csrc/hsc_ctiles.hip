@@ -307,104 +307,114 @@ __device__ __forceinline__ bool slot_le(const uint64_t *kw, uint32_t j, const ui
     return kw[(size_t)(WG - 1) * kCTRows + j] <= x[WG - 1];
 }
 
-template <int WG>
-__global__ __launch_bounds__(kJoinThreads) void k_join_c(ProbeWork work, CTiles ct, uint8_t *flags)
+// Block-uniform load through the constant address space: a scalar load,
+// counted apart from the vector loads (waiting for it does not drain them).
+template <class T>
+__device__ __forceinline__ T sload(const T *p)
+{
+    return *(const __attribute__((address_space(4))) T *)p;
+}
+
+// 1024 threads, one record and one row pair each: two 57 KiB workgroups per
+// CU hold 32 waves (the CU's limit)
+constexpr int kCJT = 1024;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// One tile's records (kTile: tile blockIdx.x, its bucket's first kTileCap
+// records; else overflow item xi of a hot tile).  The tile's record count /
+// the item's descriptor come by scalar loads and this thread's bucket entry
+// by a vector load issued before the tile's rows; the entry retires first
+// (vector counters retire in order), so the probe gather is issued while the
+// rows are in flight, and waiting for the scalar count drains no vector load.
+template <int WG, bool kTile>
+__device__ __forceinline__ void join_item(const ProbeWork &work, const CTiles &ct, uint8_t *flags,
+                                          uint32_t xi, uint64_t *kw, uint32_t *rank,
+                                          uint32_t *b16, uint32_t *b128)
 {
     constexpr uint32_t T = kCTRows;
-    constexpr int RQ = T / (4 * kJoinThreads);  // row quads per thread (1)
-    constexpr int kRec = kJoinChunk / kJoinThreads;
-    static_assert(RQ >= 1, "a row quad per thread");
+    const uint32_t tid = threadIdx.x;
+    uint32_t tile, r0, r1, ev;
+    if constexpr (kTile) {
+        tile = blockIdx.x;
+        r0 = tile * kTileCap;
+        ev = ct.recs[r0 + tid];  // a bucket always has kTileCap slots
+    } else {
+        const uint32_t *d = (const uint32_t *)(work.item_desc + xi);
+        tile = sload(d), r0 = sload(d + 1), r1 = sload(d + 2);
+        ev = ct.recs[min(r0 + tid, r1 - 1)];
+    }
+    const size_t row = ((size_t)tile << kCTLog2) + 2 * tid;
+    u64x2 kv[WG];
+#pragma unroll
+    for (int w = 0; w < WG; ++w) kv[w] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row);
+    const u32x2 rr = *(const u32x2 *)(ct.rank + row);
+    if constexpr (kTile) r1 = r0 + min(kTileCap, sload(work.counts + tile));
+    // no early exit for a tile without records: it would let the compiler sink
+    // the row loads below the count's wait
+    const bool live = r0 + tid < r1;
+    if (!live) ev = 0;  // probe 0's entry stands in (no verdict is taken from it)
+    const u64x2 *e = (const u64x2 *)(ct.ent + (size_t)(ev & 0x3FFFFFFFu) * 8);
+    u64x2 pe[4] = {};
+    if (live)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) pe[h] = e[h];
+#pragma unroll
+    for (int w = 0; w < WG; ++w) *(u64x2 *)(kw + (size_t)w * T + 2 * tid) = kv[w];
+    *(u32x2 *)(rank + 2 * tid) = rr;
+    uint32_t m = max(rr.x, rr.y);
+#pragma unroll
+    for (int d = 1; d < 8; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+    if ((tid & 7) == 0) b16[tid >> 3] = m;
+#pragma unroll
+    for (int d = 8; d < 64; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+    if ((tid & 63) == 0) b128[tid >> 6] = m;
+    __syncthreads();
+    if (!live) return;
+    const uint32_t tn = min(T, ct.n - (tile << kCTLog2));
+    const uint32_t kind = ev >> 30;
+    uint64_t lo[WG], hi[WG];
+    const uint64_t f[6] = {pe[0].x, pe[0].y, pe[1].x, pe[1].y, pe[2].x, pe[2].y};
+#pragma unroll
+    for (int w = 0; w < WG; ++w) lo[w] = f[w], hi[w] = f[3 + w];
+    const uint32_t rs = (uint32_t)pe[3].x, txn = (uint32_t)(pe[3].x >> 32);
+    // pa = #keys < lo, pb = #keys <= hi: root-to-leaf walks of the Eytzinger
+    // tree in lockstep; padding keys (~0) are above every bound
+    uint32_t ja = 1, jb = 1;
+#pragma unroll
+    for (int d = 0; d < kCTLog2; ++d) {
+        const bool ga = slot_lt<WG>(kw, ja, lo), gb = slot_le<WG>(kw, jb, hi);
+        ja = 2 * ja + ga;
+        jb = 2 * jb + gb;
+    }
+    uint32_t pa = min(ja - T + slot_lt<WG>(kw, 0, lo), tn);
+    uint32_t pb = min(jb - T + slot_le<WG>(kw, 0, hi), tn);
+    if (kind == kCTail) pa = 0;
+    if (kind == kCHead) pb = tn;
+    if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) flags[txn] = 1;
+}
+
+template <int WG>
+__global__ __launch_bounds__(kCJT) void k_join_c(ProbeWork work, CTiles ct, uint8_t *flags)
+{
+    constexpr uint32_t T = kCTRows;
+    static_assert(T == 2 * kCJT, "a row pair per thread");
+    static_assert(kJoinChunk == kCJT && kTileCap == kCJT, "a record per thread");
     extern __shared__ __attribute__((aligned(16))) uint64_t jl[];
     uint64_t *kw = jl;                                   // [WG][T], Eytzinger order
     uint32_t *rank = (uint32_t *)(jl + (size_t)WG * T);  // [T], sorted order
     uint32_t *b16 = rank + T;                            // [T / 16]
     uint32_t *b128 = b16 + T / 16;                       // [T / 128]
     const uint32_t ntiles = ct.ntiles;
+    if (blockIdx.x < ntiles) {
+        join_item<WG, true>(work, ct, flags, 0, kw, rank, b16, b128);
+        return;
+    }
     // blocks past the tiles take the hot tiles' overflow items in turn
-    const uint32_t nextra = blockIdx.x < ntiles ? 1 : work.item_off[1];
-    const uint32_t stride = gridDim.x > ntiles ? gridDim.x - ntiles : 1;  // >= 1: every loop ends
-    for (uint32_t xi = blockIdx.x < ntiles ? 0 : blockIdx.x - ntiles; xi < nextra; xi += stride) {
+    const uint32_t nextra = work.item_off[1];
+    const uint32_t stride = gridDim.x - ntiles;
+    for (uint32_t xi = blockIdx.x - ntiles; xi < nextra; xi += stride) {
         __syncthreads();  // the previous item's LDS reads are done
-        uint32_t tile, r0, r1;
-        if (blockIdx.x < ntiles) {
-            tile = blockIdx.x;
-        } else {
-            const uint4 d = work.item_desc[xi];
-            tile = d.x, r0 = d.y, r1 = d.z;
-        }
-        const size_t ts = (size_t)tile << kCTLog2;
-        u64x2 kv[RQ][WG][2];
-        u32x4 rr[RQ];
-#pragma unroll
-        for (int v = 0; v < RQ; ++v) {
-            const size_t row = ts + 4 * (threadIdx.x + kJoinThreads * v);
-#pragma unroll
-            for (int w = 0; w < WG; ++w) {
-                kv[v][w][0] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row);
-                kv[v][w][1] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row + 2);
-            }
-            rr[v] = *(const u32x4 *)(ct.rank + row);
-        }
-        if (blockIdx.x < ntiles) {
-            r0 = tile * kTileCap;
-            r1 = r0 + min(kTileCap, work.counts[tile]);
-        }
-        if (r0 >= r1) continue;  // a tile no range reaches (uniform across the block)
-        uint32_t ev[kRec];
-#pragma unroll
-        for (int k = 0; k < kRec; ++k) ev[k] = ct.recs[min(r0 + k * kJoinThreads + threadIdx.x, r1 - 1)];
-        u64x2 pe[kRec][4];
-#pragma unroll
-        for (int k = 0; k < kRec; ++k) {
-            const u64x2 *e = (const u64x2 *)(ct.ent + (size_t)(ev[k] & 0x3FFFFFFFu) * 8);
-#pragma unroll
-            for (int h = 0; h < 4; ++h) pe[k][h] = e[h];
-        }
-#pragma unroll
-        for (int v = 0; v < RQ; ++v) {
-            const uint32_t quad = threadIdx.x + kJoinThreads * v;
-#pragma unroll
-            for (int w = 0; w < WG; ++w) {
-                *(u64x2 *)(kw + (size_t)w * T + 4 * quad) = kv[v][w][0];
-                *(u64x2 *)(kw + (size_t)w * T + 4 * quad + 2) = kv[v][w][1];
-            }
-            ((u32x4 *)rank)[quad] = rr[v];
-            uint32_t m = max(max(rr[v].x, rr[v].y), max(rr[v].z, rr[v].w));
-            m = max(m, (uint32_t)__shfl_xor((int)m, 1, 64));
-            m = max(m, (uint32_t)__shfl_xor((int)m, 2, 64));
-            if ((threadIdx.x & 3) == 0) b16[quad >> 2] = m;
-#pragma unroll
-            for (int d = 4; d < 32; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
-            if ((threadIdx.x & 31) == 0) b128[quad >> 5] = m;
-        }
-        __syncthreads();
-        const uint32_t tn = min(T, ct.n - (uint32_t)ts);
-#pragma unroll
-        for (int k = 0; k < kRec; ++k) {
-            const uint32_t r = r0 + k * kJoinThreads + threadIdx.x;
-            if (r >= r1) continue;
-            const uint32_t kind = ev[k] >> 30;
-            uint64_t lo[WG], hi[WG];
-            const uint64_t f[6] = {pe[k][0].x, pe[k][0].y, pe[k][1].x,
-                                   pe[k][1].y, pe[k][2].x, pe[k][2].y};
-#pragma unroll
-            for (int w = 0; w < WG; ++w) lo[w] = f[w], hi[w] = f[3 + w];
-            const uint32_t rs = (uint32_t)pe[k][3].x, txn = (uint32_t)(pe[k][3].x >> 32);
-            // pa = #keys < lo, pb = #keys <= hi: root-to-leaf walks of the
-            // Eytzinger tree in lockstep; padding keys (~0) are above every bound
-            uint32_t ja = 1, jb = 1;
-#pragma unroll
-            for (int d = 0; d < kCTLog2; ++d) {
-                const bool ga = slot_lt<WG>(kw, ja, lo), gb = slot_le<WG>(kw, jb, hi);
-                ja = 2 * ja + ga;
-                jb = 2 * jb + gb;
-            }
-            uint32_t pa = min(ja - T + slot_lt<WG>(kw, 0, lo), tn);
-            uint32_t pb = min(jb - T + slot_le<WG>(kw, 0, hi), tn);
-            if (kind == kCTail) pa = 0;
-            if (kind == kCHead) pb = tn;
-            if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) flags[txn] = 1;
-        }
+        join_item<WG, false>(work, ct, flags, xi, kw, rank, b16, b128);
     }
 }
 
@@ -463,9 +473,9 @@ hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_i
     const size_t lds = 8 * (size_t)ct.WG * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
                        4 * (kCTRows / 128);
     switch (ct.WG) {
-    case 1: k_join_c<1><<<blocks, kJoinThreads, lds, s>>>(work, ct, flags); break;
-    case 2: k_join_c<2><<<blocks, kJoinThreads, lds, s>>>(work, ct, flags); break;
-    case 3: k_join_c<3><<<blocks, kJoinThreads, lds, s>>>(work, ct, flags); break;
+    case 1: k_join_c<1><<<blocks, kCJT, lds, s>>>(work, ct, flags); break;
+    case 2: k_join_c<2><<<blocks, kCJT, lds, s>>>(work, ct, flags); break;
+    case 3: k_join_c<3><<<blocks, kCJT, lds, s>>>(work, ct, flags); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -548,11 +548,21 @@ static int build_compact(hsc_ctx *c, const WinView &w)
     c->ct_maxbits = maxbits;
     if (WC >= W || WC > kMaxCompactWords) return HSC_OK;
     HIPCHK(c, c->d_cmv.ensure(8 * gw * 6));
-    HIPCHK(c, c->d_cbits.ensure(4 * (size_t)ng));
+    // bits[g] then wlen[g] (words inside the group's key length) in one upload
+    bits.resize(2 * (size_t)ng);
+    for (int g = 0; g < ng; ++g) bits[ng + g] = (uint32_t)std::min(W, (c->groups[g].klen + 7) / 8);
+    HIPCHK(c, c->d_cbits.ensure(8 * (size_t)ng));
     HIPCHK(c, hipMemcpyAsync(c->d_cmv.p, mv.data(), 8 * gw * 6, hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipMemcpyAsync(c->d_cbits.p, bits.data(), 4 * (size_t)ng, hipMemcpyHostToDevice, s));
-    c->ct = CompactTables{c->d_cmask.as<uint64_t>(), c->d_cpat.as<uint64_t>(), c->d_cmv.as<uint64_t>(),
-                          c->d_cbits.as<uint32_t>(), W, WC, ng};
+    HIPCHK(c, hipMemcpyAsync(c->d_cbits.p, bits.data(), 8 * (size_t)ng, hipMemcpyHostToDevice, s));
+    c->ct = CompactTables{};
+    c->ct.mask = c->d_cmask.as<uint64_t>();
+    c->ct.pat = c->d_cpat.as<uint64_t>();
+    c->ct.mv = c->d_cmv.as<uint64_t>();
+    c->ct.bits = c->d_cbits.as<uint32_t>();
+    c->ct.wlen = c->d_cbits.as<uint32_t>() + ng;
+    c->ct.W = W;
+    c->ct.WC = WC;
+    c->ct.ng = ng;
     HIPCHK(c, c->d_cwords.ensure(8 * (size_t)WC * c->cap));
     HIPCHK(c, compact_rows(w.words, w.stride, w.gid, w.n, c->ct, c->d_cwords.as<uint64_t>(), s));
     WinView &v = c->wc;
@@ -1497,18 +1507,46 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
     uint32_t *gid = st.col<uint32_t>(st.L.gid), *txn = st.col<uint32_t>(st.L.txn);
     uint32_t *ltab = st.col<uint32_t>(st.L.lock_table), *ltxn = st.col<uint32_t>(st.L.lock_txn);
     uint64_t *lsnap = st.col<uint64_t>(st.L.lock_snap);
+    // Groups of different key lengths (in words): each part's probes are laid
+    // out grouped by that length (stable), so the compact bound kernel's waves
+    // skip the zero words past it together.  One length: read-set order.
+    std::vector<uint8_t> gcls(c->groups.size());
+    int ncls = 0, cls0 = -1;
+    for (size_t g = 0; g < c->groups.size(); ++g) {
+        gcls[g] = (uint8_t)std::min(W, (c->groups[g].klen + 7) / 8);
+        if (cls0 < 0) cls0 = gcls[g];
+        ncls = std::max(ncls, (int)gcls[g] + 1);
+        if (gcls[g] != cls0) cls0 = kMaxWords + 1;
+    }
+    const bool by_len = cls0 == kMaxWords + 1;
     par_for(n >= (size_t)kMarshalParallelMin ? c->threads : 1, nwork, [&](int w) {
         const MarshalPart &mp = c->parts[w];
         const size_t o = mp.out0, k = mp.gid.size();
-        for (size_t i = 0; i < k; ++i)
-            for (int j = 0; j < W; ++j) {
-                lo[(size_t)j * n + o + i] = mp.lohi[i * 2 * W + j];
-                hi[(size_t)j * n + o + i] = mp.lohi[i * 2 * W + W + j];
+        if (by_len) {
+            size_t cnt[kMaxWords + 2] = {0};
+            for (size_t i = 0; i < k; ++i) cnt[gcls[mp.gid[i]] + 1]++;
+            for (int q = 1; q <= ncls; ++q) cnt[q] += cnt[q - 1];
+            for (size_t i = 0; i < k; ++i) {
+                const size_t d = o + cnt[gcls[mp.gid[i]]]++;
+                for (int j = 0; j < W; ++j) {
+                    lo[(size_t)j * n + d] = mp.lohi[i * 2 * W + j];
+                    hi[(size_t)j * n + d] = mp.lohi[i * 2 * W + W + j];
+                }
+                gid[d] = mp.gid[i];
+                sn[d] = mp.snap[i];
+                txn[d] = mp.txn[i];
             }
-        if (k) {
-            memcpy(gid + o, mp.gid.data(), 4 * k);
-            memcpy(sn + o, mp.snap.data(), 8 * k);
-            memcpy(txn + o, mp.txn.data(), 4 * k);
+        } else {
+            for (size_t i = 0; i < k; ++i)
+                for (int j = 0; j < W; ++j) {
+                    lo[(size_t)j * n + o + i] = mp.lohi[i * 2 * W + j];
+                    hi[(size_t)j * n + o + i] = mp.lohi[i * 2 * W + W + j];
+                }
+            if (k) {
+                memcpy(gid + o, mp.gid.data(), 4 * k);
+                memcpy(sn + o, mp.snap.data(), 8 * k);
+                memcpy(txn + o, mp.txn.data(), 4 * k);
+            }
         }
         const size_t lo0 = mp.lock0, kl = mp.lock_table.size();
         if (kl) {

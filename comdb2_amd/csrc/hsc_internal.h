@@ -395,6 +395,8 @@ struct CompactTables {
     const uint64_t *mask, *pat, *mv;  // [ng][W] varying bits, first row, compress moves [ng][W][6]
     const uint32_t *bits;             // [ng] varying bits (0xFFFFFFFF: no rows)
     int W, WC;
+    const uint32_t *wlen;             // [ng] words inside the group's key length (bounds
+                                      // are zero past it, like its rows)
     int ng;                           // groups
 };
 constexpr int kMaxCompactWords = 6;
