@@ -18,7 +18,7 @@ ROWS = [0x00, 0x08, 0x61, 0x62]
 PROBE = [0x00, 0x07, 0x08, 0x09, 0x60, 0x61, 0x62, 0x63, 0xFF]
 
 
-def _short_case(seed, n_commits=3000, n_txn=900, lens=(9, 17, 23), n_tabs=4, hot=0.0):
+def _short_case(seed, n_commits=3000, n_txn=900, lens=(9, 17, 23), n_tabs=4, hot=0.0, var=None):
     """Keys of few varying bits per byte (codes + group id fit 3 words), probes
     equal to rows, prefixes, one-byte edits, inverted and open ranges; hot > 0:
     that share of ranges are points on a handful of keys (overflowing tiles)."""
@@ -32,7 +32,9 @@ def _short_case(seed, n_commits=3000, n_txn=900, lens=(9, 17, 23), n_tabs=4, hot
         for _ in range(int(rng.integers(1, 9))):
             tb = tabs[int(rng.integers(0, n_tabs - 1))]  # the last table is never written
             ix = int(rng.integers(0, len(lens)))
-            k = bytes([8]) + rng.choice(ROWS, size=lens[ix] - 1).astype(np.uint8).tobytes()
+            nv = lens[ix] - 1 if var is None else min(var, lens[ix] - 1)  # varying bytes, then 0x01s
+            k = bytes([8]) + rng.choice(ROWS, size=nv).astype(np.uint8).tobytes()
+            k += b"\x01" * (lens[ix] - len(k))
             keys.setdefault((tb, ix), []).append(k)
             lb.write(c, F.REC_UNDO_ADD_IX_LK, tb, ix, k)
         snaps.append(lb.commit(c))
@@ -167,3 +169,18 @@ def test_appended_rows_match_oracle(oracle_mod):
     finally:
         v.close()
     np.testing.assert_array_equal(got, want)
+
+
+def test_long_keys_unfused_locate_match_oracle(oracle_mod):
+    """72-byte keys (W = 9 words) whose varying bytes fit 3-word keys: the
+    bounds go through the generic bound kernel and the unfused locate."""
+    log, rs = _short_case(13, n_commits=2500, n_txn=800, lens=(9, 72), var=20)
+    want = oracle_mod.check(log, rs, nthreads=8)[0] != 0
+    v = Validator(0)
+    try:
+        got, ref = _both(v, log, rs)
+        assert v.words == 9
+    finally:
+        v.close()
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(ref, want)
