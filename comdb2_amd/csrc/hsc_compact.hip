@@ -221,7 +221,7 @@ hipError_t launch_probes_wc(const ProbeView &p, const CompactMeta &cm, uint64_t 
 
 CompactMeta meta_of(const CompactTables &t)
 {
-    return CompactMeta{t.mask, t.pat, t.mv, t.bits, t.wlen, t.W, t.ng};
+    return CompactMeta{t.mask, t.pat, t.mv, t.bits, t.wlen, t.W, t.ng, t.W, 6, 1};
 }
 
 }  // namespace

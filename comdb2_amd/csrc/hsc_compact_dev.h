@@ -84,10 +84,14 @@ __device__ __forceinline__ void fill_ones(uint64_t (&out)[WC], int from, int to)
 }
 
 struct CompactMeta {
-    const uint64_t *mask, *pat, *mv;  // [ng][W], [ng][W], [ng][W][6]
+    const uint64_t *mask, *pat, *mv;  // mask / pattern of word j of group g at [g * gs + j],
+                                      // compress move i at mv[(g * gs + j) * vm + i * vs]
     const uint32_t *bits;             // [ng]: varying bits, kNoRows = group has no rows
     const uint32_t *wlen;             // [ng]: words inside the group's key length
     int W, ng;
+    int gs, vm, vs;                   // global: W, 6, 1 ([ng][W][6]); LDS (stage_bound_tables):
+                                      // odd gs, 1, ng * gs -- lanes of different groups hit
+                                      // different banks
 };
 constexpr uint32_t kNoRows = 0xFFFFFFFFu;
 
@@ -186,7 +190,7 @@ constexpr int kBoundThreads = 256;
 constexpr uint32_t kBoundLdsBytes = 48 * 1024;
 __host__ __device__ inline uint32_t bound_lds_bytes(int ng, int W)
 {
-    return (uint32_t)ng * (uint32_t)W * 8 * 8 + 8 * (uint32_t)ng;
+    return (uint32_t)ng * (uint32_t)(W | 1) * 8 * 8 + 8 * (uint32_t)ng;
 }
 
 struct BoundIn {
@@ -223,8 +227,8 @@ __device__ __forceinline__ bool bound_codes(const CompactMeta &cm, const BoundIn
     for (int k = 0; k < WC; ++k) al[k] = ah[k] = 0;
     bool ok = bits != kNoRows;
     if (ok) {
-        const uint64_t *mk = cm.mask + (size_t)g * cm.W, *pt = cm.pat + (size_t)g * cm.W;
-        const uint64_t *mvg = cm.mv + (size_t)g * cm.W * 6;
+        const uint64_t *mk = cm.mask + (size_t)g * cm.gs, *pt = cm.pat + (size_t)g * cm.gs;
+        const uint64_t *mvg = cm.mv + (size_t)g * cm.gs * cm.vm;
         const int wl = (int)cm.wlen[g];
         int pos = 0, npl = -1, nph = -1, xbl = 0, xbh = 0;
 #pragma unroll
@@ -233,7 +237,7 @@ __device__ __forceinline__ bool bound_codes(const CompactMeta &cm, const BoundIn
             const uint64_t m = mk[j], pj = pt[j];
             uint64_t mv[6];
 #pragma unroll
-            for (int i = 0; i < 6; ++i) mv[i] = mvg[6 * j + i];
+            for (int i = 0; i < 6; ++i) mv[i] = mvg[j * cm.vm + i * cm.vs];
             const int c = __popcll(m);
             acc_push<WC>(al, bound_word(in.xl[j], m, pj, mv, pos, npl, xbl), c);
             acc_push<WC>(ah, bound_word(in.xh[j], m, pj, mv, pos, nph, xbh), c);
@@ -278,14 +282,18 @@ __device__ __forceinline__ void bound_map(const ProbeView &p, const CompactMeta 
 template <int NT>
 __device__ __forceinline__ void stage_bound_tables(CompactMeta &cm, uint64_t *blds)
 {
-    const uint32_t gw = (uint32_t)cm.ng * cm.W;
+    const uint32_t W = (uint32_t)cm.W, gs = W | 1, gw = (uint32_t)cm.ng * gs;
     uint64_t *lm = blds, *lp = blds + gw, *lv = blds + 2 * gw;
     uint32_t *lb = (uint32_t *)(blds + 8 * gw), *lw = lb + cm.ng;
-    for (uint32_t i = threadIdx.x; i < gw; i += NT) {
-        lm[i] = cm.mask[i];
-        lp[i] = cm.pat[i];
+    for (uint32_t i = threadIdx.x; i < (uint32_t)cm.ng * W; i += NT) {
+        const uint32_t g = i / W, j = i - g * W;
+        lm[g * gs + j] = cm.mask[i];
+        lp[g * gs + j] = cm.pat[i];
     }
-    for (uint32_t i = threadIdx.x; i < 6 * gw; i += NT) lv[i] = cm.mv[i];
+    for (uint32_t i = threadIdx.x; i < 6 * (uint32_t)cm.ng * W; i += NT) {
+        const uint32_t gj = i / 6, k = i - 6 * gj, g = gj / W, j = gj - g * W;
+        lv[k * gw + g * gs + j] = cm.mv[i];
+    }
     for (uint32_t i = threadIdx.x; i < (uint32_t)cm.ng; i += NT) {
         lb[i] = cm.bits[i];
         lw[i] = cm.wlen[i];
@@ -295,6 +303,9 @@ __device__ __forceinline__ void stage_bound_tables(CompactMeta &cm, uint64_t *bl
     cm.mv = lv;
     cm.bits = lb;
     cm.wlen = lw;
+    cm.gs = (int)gs;
+    cm.vm = 1;
+    cm.vs = (int)gw;
 }
 
 }  // namespace

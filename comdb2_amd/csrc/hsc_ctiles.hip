@@ -37,25 +37,18 @@ namespace hsc {
 namespace {
 
 constexpr uint32_t kCTRows = 1u << kCTLog2;  // rows per tile
-constexpr int kCLocThreads = 1024;
+// 2048-probe chunks: config 3's ~600k ranges make ~290 locate / scatter
+// workgroups, enough for every CU (4096-probe chunks left 110 of 256 idle)
+constexpr int kCLocThreads = 512;
 constexpr int kCLocP = 4;                    // probes per locate thread
 constexpr uint32_t kCChunk = kCLocThreads * kCLocP;
 static_assert(kCChunk <= 4096, "in-chunk ranks are 12 bits");
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
-constexpr uint32_t kSecondRec = 1u << 31;
+constexpr uint32_t kSecondRec = 1u << 31, kPointRec = 1u << 30;
 // record kinds (top two bits of a bucket entry): search lo and hi / lo only
-// (the range runs past the tile) / hi only (it starts before the tile)
-constexpr uint32_t kCFull = 0, kCHead = 1, kCTail = 2;
-
-// Eytzinger (BFS) slot of sorted row r of a 2^L-row tile: rows 0 .. 2^L - 2
-// form a perfect binary tree at slots 1 .. 2^L - 1, the last row at slot 0.
-template <int L>
-__device__ __forceinline__ uint32_t eyt(uint32_t r)
-{
-    const uint32_t i = r + 1;
-    const int tz = __builtin_ctz(i);
-    return i == (1u << L) ? 0 : (1u << (L - 1 - tz)) + (i >> (tz + 1));
-}
+// (the range runs past the tile) / hi only (it starts before the tile) / a
+// point (lo == hi: one search, then an equality test)
+constexpr uint32_t kCFull = 0, kCHead = 1, kCTail = 2, kCPoint = 3;
 
 // K = g || code: the WC code words shifted right by gb bits under the group id
 template <int WG>
@@ -81,7 +74,7 @@ __device__ __forceinline__ bool key_lt(const uint64_t (&a)[WG], const uint64_t (
     return a[WG - 1] < b[WG - 1];
 }
 
-// ---- build: row keys (Eytzinger order per tile), ranks, tiles' first keys ----
+// ---- build: row keys, ranks, tiles' first keys ----
 template <int WG>
 __global__ __launch_bounds__(256) void k_ct_rows(const uint64_t *cw, size_t cs, int WC,
                                                  const uint32_t *gid, const uint64_t *lsn,
@@ -103,9 +96,8 @@ __global__ __launch_bounds__(256) void k_ct_rows(const uint64_t *cw, size_t cs, 
         for (int j = 0; j < WG; ++j) k[j] = ~0ull;  // padding: above every bound
     }
     const uint32_t t = i >> kCTLog2, o = i & (kCTRows - 1);
-    const size_t dst = ((size_t)t << kCTLog2) + eyt<kCTLog2>(o);
 #pragma unroll
-    for (int j = 0; j < WG; ++j) key[(size_t)j * ct.len + dst] = k[j];
+    for (int j = 0; j < WG; ++j) key[(size_t)j * ct.len + i] = k[j];
     rank[i] = r;
     if (o == 0 && t < ct.ntiles)
 #pragma unroll
@@ -117,6 +109,36 @@ __global__ void k_ct_rel(const uint64_t *first0, uint32_t ntiles, uint64_t *rel)
 {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t < ntiles) rel[t] = first0[t] - first0[0];
+}
+
+// Per tile: kTB buckets over word 0 of its rows relative to the first row's,
+// shift = the least that puts the last row's below kTB << shift;
+// tb[t * kTBS + k] = #rows of the tile whose bucket is < k (k <= kTB), then
+// the shift.  A join search starts inside one bucket (a few rows) instead of
+// walking the tile's 11 levels.
+__global__ __launch_bounds__(256) void k_ct_tbuckets(CTiles ct, const uint64_t *key0, uint16_t *tb)
+{
+    __shared__ uint32_t cnt[kTB];
+    const uint32_t t = blockIdx.x, tid = threadIdx.x;
+    const size_t r0 = (size_t)t << kCTLog2;
+    const uint32_t tn = min(kCTRows, ct.n - (uint32_t)r0);
+    const uint64_t f0 = key0[r0], span = key0[r0 + tn - 1] - f0;
+    const int bits = span ? 64 - __clzll(span) : 0;
+    const int shift = bits > kTBLog2 ? bits - kTBLog2 : 0;
+    cnt[tid] = 0;
+    __syncthreads();
+    for (uint32_t i = tid; i < tn; i += 256) atomicAdd(&cnt[(uint32_t)((key0[r0 + i] - f0) >> shift)], 1u);
+    __syncthreads();
+    const uint32_t mine = cnt[tid];
+    __syncthreads();  // every count read before the scan reuses cnt as scratch
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan<256>(mine, cnt, tot);
+    uint16_t *o = tb + (size_t)t * kTBS;
+    o[tid] = (uint16_t)pre;
+    if (tid == 0) {
+        o[kTB] = (uint16_t)tn;
+        o[kTB + 1] = (uint16_t)shift;
+    }
 }
 
 // ---- locate ----
@@ -149,10 +171,17 @@ __device__ __forceinline__ uint32_t ct_count(const uint64_t *lf, uint32_t nt, co
     uint32_t l = b < m ? T[b] : T[m], h = b < m ? T[b + 1] : nt;
     while (l < h) {
         const uint32_t mid = (l + h) >> 1;
-        uint64_t f[WG];
+        // word 0 decides unless equal; later words are read only on a tie
+        uint64_t v = lf[mid];
+        bool below = v < x[0], eq = v == x[0];
 #pragma unroll
-        for (int j = 0; j < WG; ++j) f[j] = lf[(size_t)j * nt + mid];
-        const bool below = LE ? !key_lt<WG>(x, f) : key_lt<WG>(f, x);
+        for (int j = 1; j < WG; ++j)
+            if (eq) {
+                v = lf[(size_t)j * nt + mid];
+                below = v < x[j];
+                eq = v == x[j];
+            }
+        below = eq ? LE : below;
         l = below ? mid + 1 : l;
         h = below ? h : mid;
     }
@@ -218,18 +247,28 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
                 // tiles strictly between the end tiles lie inside the range
                 if (bt > a + 1 && tiles_max(wt, a + 1, bt - 1) > snap[k]) flags[txn] = 1;
                 sl.x = a << 12 | atomicAdd(&hist[a], 1u);
+                bool point = true;
+#pragma unroll
+                for (int j = 0; j < WG; ++j) point &= a_[j] == b_[j];
                 if (bt > a) {
                     sl.x |= kSecondRec;
                     sl.y = bt << 12 | atomicAdd(&hist[bt], 1u);
+                } else if (point) {
+                    sl.x |= kPointRec;
                 }
-                // entry: lo[0..2], hi[0..2] (words past WG zero), r(S) | read set << 32
-                uint64_t f[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                // entries {lo[0..2], r(S) | read set << 32}, {hi[0..2], ...} (words past WG zero)
+                const uint64_t rt = (uint64_t)lsn32_rank(snap[k], ct.rank_base) | (uint64_t)txn << 32;
+                uint64_t f[8] = {0, 0, 0, rt, 0, 0, 0, rt};
 #pragma unroll
-                for (int j = 0; j < WG; ++j) f[j] = a_[j], f[3 + j] = b_[j];
-                f[6] = (uint64_t)lsn32_rank(snap[k], ct.rank_base) | (uint64_t)txn << 32;
-                u64x2 *e = (u64x2 *)(ct.ent + (size_t)q * 8);
-#pragma unroll
-                for (int h = 0; h < 4; ++h) e[h] = u64x2{f[2 * h], f[2 * h + 1]};
+                for (int j = 0; j < WG; ++j) f[j] = a_[j], f[4 + j] = b_[j];
+                u64x2 *el = (u64x2 *)(ct.ent + (size_t)q * 4);
+                u64x2 *eh = (u64x2 *)(ct.ent + ((size_t)ct.np + q) * 4);
+                el[0] = u64x2{f[0], f[1]};
+                el[1] = u64x2{f[2], f[3]};
+                if (!point || bt > a) {  // a point's hi entry is never read
+                    eh[0] = u64x2{f[4], f[5]};
+                    eh[1] = u64x2{f[6], f[7]};
+                }
             }
         }
         ct.slot[q] = sl;
@@ -273,9 +312,9 @@ __global__ __launch_bounds__(kCLocThreads) void k_scatter_c(CTiles ct, ProbeWork
         if (s[k].x == kNoSlot) continue;
         const uint32_t q = c0 + threadIdx.x + kCLocThreads * k;
         const bool two = (s[k].x & kSecondRec) != 0;
-        const uint32_t ta = (s[k].x & ~kSecondRec) >> 12;
-        ct.recs[ct_bucket_slot(work, nt, ta, soff[ta] + (s[k].x & 0xFFFu))] =
-            q | (two ? kCHead : kCFull) << 30;
+        const uint32_t ta = (s[k].x & ~(kSecondRec | kPointRec)) >> 12;
+        const uint32_t kind = two ? kCHead : (s[k].x & kPointRec) ? kCPoint : kCFull;
+        ct.recs[ct_bucket_slot(work, nt, ta, soff[ta] + (s[k].x & 0xFFFu))] = q | kind << 30;
         if (two) {
             const uint32_t tb = s[k].y >> 12;
             ct.recs[ct_bucket_slot(work, nt, tb, soff[tb] + (s[k].y & 0xFFFu))] = q | kCTail << 30;
@@ -284,27 +323,45 @@ __global__ __launch_bounds__(kCLocThreads) void k_scatter_c(CTiles ct, ProbeWork
 }
 
 // ---- join ----
-// key at Eytzinger slot j vs x: word 0 decides unless equal
-template <int WG>
-__device__ __forceinline__ bool slot_lt(const uint64_t *kw, uint32_t j, const uint64_t (&x)[WG])
+// #rows < x (LE: <= x) of the tile: x's word-0 bucket, then a binary search
+// of that bucket's rows (sorted order, full-key compares)
+template <int WG, bool LE>
+__device__ __forceinline__ uint32_t tile_count(const uint64_t *kw, const uint16_t *B, int shift,
+                                               uint32_t tn, const uint64_t (&x)[WG])
 {
+    constexpr uint32_t T = kCTRows;
+    const uint64_t f0 = kw[0];
+    if (x[0] < f0) return 0;
+    const uint64_t d = (x[0] - f0) >> shift;
+    if (d >= (uint64_t)kTB) return tn;
+    uint32_t l = B[d], h = B[d + 1];
+    while (l < h) {
+        const uint32_t mid = (l + h) >> 1;
+        // word 0 decides unless equal; later words are read only on a tie
+        uint64_t v = kw[mid];
+        bool below = v < x[0], eq = v == x[0];
 #pragma unroll
-    for (int w = 0; w < WG - 1; ++w) {
-        const uint64_t v = kw[(size_t)w * kCTRows + j];
-        if (v != x[w]) return v < x[w];
+        for (int w = 1; w < WG; ++w)
+            if (eq) {
+                v = kw[(size_t)w * T + mid];
+                below = v < x[w];
+                eq = v == x[w];
+            }
+        below = eq ? LE : below;
+        l = below ? mid + 1 : l;
+        h = below ? h : mid;
     }
-    return kw[(size_t)(WG - 1) * kCTRows + j] < x[WG - 1];
+    return l;
 }
 
+// row r of the tile == x
 template <int WG>
-__device__ __forceinline__ bool slot_le(const uint64_t *kw, uint32_t j, const uint64_t (&x)[WG])
+__device__ __forceinline__ bool row_eq(const uint64_t *kw, uint32_t r, const uint64_t (&x)[WG])
 {
+    bool eq = true;
 #pragma unroll
-    for (int w = 0; w < WG - 1; ++w) {
-        const uint64_t v = kw[(size_t)w * kCTRows + j];
-        if (v != x[w]) return v < x[w];
-    }
-    return kw[(size_t)(WG - 1) * kCTRows + j] <= x[WG - 1];
+    for (int w = 0; w < WG; ++w) eq &= kw[(size_t)w * kCTRows + r] == x[w];
+    return eq;
 }
 
 // Block-uniform load through the constant address space: a scalar load,
@@ -315,27 +372,67 @@ __device__ __forceinline__ T sload(const T *p)
     return *(const __attribute__((address_space(4))) T *)p;
 }
 
-// 1024 threads, one record and one row pair each: two 57 KiB workgroups per
+// 1024 threads, one record and one row pair each: two 58 KiB workgroups per
 // CU hold 32 waves (the CU's limit)
 constexpr int kCJT = 1024;
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
-// One tile's records (kTile: tile blockIdx.x, its bucket's first kTileCap
-// records; else overflow item xi of a hot tile).  The tile's record count /
-// the item's descriptor come by scalar loads and this thread's bucket entry
-// by a vector load issued before the tile's rows; the entry retires first
-// (vector counters retire in order), so the probe gather is issued while the
-// rows are in flight, and waiting for the scalar count drains no vector load.
+// the searches of one record after its tile is staged
+template <int WG>
+__device__ __forceinline__ void join_search(const ProbeWork &work, const CTiles &ct, uint8_t *flags,
+                                            const uint64_t *kw, const uint32_t *rank,
+                                            const uint32_t *b16, const uint32_t *b128,
+                                            const uint16_t *B, uint32_t kind, const u64x2 (&pl)[2],
+                                            const u64x2 ph0, const uint64_t ph1)
+{
+    const uint32_t tn = B[kTB];
+    const int shift = B[kTB + 1];
+    uint64_t lo[WG], hi[WG];
+    const uint64_t fl[3] = {pl[0].x, pl[0].y, pl[1].x}, fh[3] = {ph0.x, ph0.y, ph1};
+#pragma unroll
+    for (int w = 0; w < WG; ++w) lo[w] = fl[w], hi[w] = fh[w];
+    const uint64_t rt = pl[1].y;
+    const uint32_t rs = (uint32_t)rt, txn = (uint32_t)(rt >> 32);
+#ifdef HSC_STAMPS
+    if (threadIdx.x == 0 && work.stamps && rs == 0x7FFFFFFF) flags[0] = 1;  // wait for the entry
+#endif
+    HSC_STAMP(work, 1, 3);
+    uint32_t pa = 0, pb = tn;
+    if (kind != kCTail) pa = tile_count<WG, false>(kw, B, shift, tn, lo);
+    if (kind == kCPoint)
+        pb = pa + (pa < tn && row_eq<WG>(kw, pa, lo));
+    else if (kind != kCHead)
+        pb = tile_count<WG, true>(kw, B, shift, tn, hi);
+#ifdef HSC_STAMPS
+    if (threadIdx.x == 0 && work.stamps && pa + pb == 0x7FFFFFFF) flags[0] = 1;
+#endif
+    HSC_STAMP(work, 1, 4);
+    // any rank > r(S) in [pa, pb) (a point reads its row); measured: tile
+    // prefix / suffix rank maxima for head / tail records cost more in the
+    // staging (scans, a barrier, registers) than they saved here
+    const bool hit = kind == kCPoint ? pa < pb && rank[pa] > rs
+                                     : pa < pb && any_after32(rank, b16, b128, pa, pb, rs);
+    if (hit) flags[txn] = 1;
+    HSC_STAMP(work, 1, 5);
+}
+
+// One tile's records (kTile: tile xi, its bucket's first kTileCap records;
+// else overflow item xi of a hot tile).  The tile's record count / the item's
+// descriptor come by scalar loads and this thread's bucket entry by a vector
+// load issued before the tile's rows; the entry retires first (vector
+// counters retire in order), so the probe gather is issued while the rows
+// are in flight, and waiting for the scalar count drains no vector load.
 template <int WG, bool kTile>
 __device__ __forceinline__ void join_item(const ProbeWork &work, const CTiles &ct, uint8_t *flags,
                                           uint32_t xi, uint64_t *kw, uint32_t *rank,
-                                          uint32_t *b16, uint32_t *b128)
+                                          uint32_t *b16, uint32_t *b128, uint16_t *B)
 {
     constexpr uint32_t T = kCTRows;
     const uint32_t tid = threadIdx.x;
+    HSC_STAMP(work, 1, 0);
     uint32_t tile, r0, r1, ev;
     if constexpr (kTile) {
-        tile = blockIdx.x;
+        tile = xi;
         r0 = tile * kTileCap;
         ev = ct.recs[r0 + tid];  // a bucket always has kTileCap slots
     } else {
@@ -348,19 +445,29 @@ __device__ __forceinline__ void join_item(const ProbeWork &work, const CTiles &c
 #pragma unroll
     for (int w = 0; w < WG; ++w) kv[w] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row);
     const u32x2 rr = *(const u32x2 *)(ct.rank + row);
+    u32x2 bt = {0, 0};
+    if (tid < kTBS / 4) bt = *(const u32x2 *)(ct.tb + (size_t)tile * kTBS + 4 * tid);
     if constexpr (kTile) r1 = r0 + min(kTileCap, sload(work.counts + tile));
     // no early exit for a tile without records: it would let the compiler sink
     // the row loads below the count's wait
     const bool live = r0 + tid < r1;
-    if (!live) ev = 0;  // probe 0's entry stands in (no verdict is taken from it)
-    const u64x2 *e = (const u64x2 *)(ct.ent + (size_t)(ev & 0x3FFFFFFFu) * 8);
-    u64x2 pe[4] = {};
-    if (live)
-#pragma unroll
-        for (int h = 0; h < 4; ++h) pe[h] = e[h];
+    const uint32_t kind = live ? ev >> 30 : kCPoint;
+    const uint32_t q = live ? ev & 0x3FFFFFFFu : 0;  // probe 0's entry stands in (no verdict is taken)
+    // a point or head record reads the lo entry, a tail record the hi entry, a
+    // full record both
+    const u64x2 *el = (const u64x2 *)(ct.ent + (size_t)q * 4);
+    const u64x2 *eh = (const u64x2 *)(ct.ent + ((size_t)ct.np + q) * 4);
+    u64x2 pl[2] = {}, ph0 = {};
+    uint64_t ph1 = 0;  // hi word 2 (a tail record's r(S) | read set comes from pl[1].y)
+    if (live && ct.dbg < 2) {
+        if (kind != kCTail) pl[0] = el[0], pl[1] = el[1];
+        if (kind == kCTail) pl[1].y = ((const uint64_t *)eh)[3];
+        if (kind == kCTail || kind == kCFull) ph0 = eh[0], ph1 = ((const uint64_t *)eh)[2];
+    }
 #pragma unroll
     for (int w = 0; w < WG; ++w) *(u64x2 *)(kw + (size_t)w * T + 2 * tid) = kv[w];
     *(u32x2 *)(rank + 2 * tid) = rr;
+    if (tid < kTBS / 4) *(u32x2 *)(B + 4 * tid) = bt;
     uint32_t m = max(rr.x, rr.y);
 #pragma unroll
     for (int d = 1; d < 8; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
@@ -368,53 +475,41 @@ __device__ __forceinline__ void join_item(const ProbeWork &work, const CTiles &c
 #pragma unroll
     for (int d = 8; d < 64; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
     if ((tid & 63) == 0) b128[tid >> 6] = m;
+    HSC_STAMP(work, 1, 1);
     __syncthreads();
-    if (!live) return;
-    const uint32_t tn = min(T, ct.n - (tile << kCTLog2));
-    const uint32_t kind = ev >> 30;
-    uint64_t lo[WG], hi[WG];
-    const uint64_t f[6] = {pe[0].x, pe[0].y, pe[1].x, pe[1].y, pe[2].x, pe[2].y};
-#pragma unroll
-    for (int w = 0; w < WG; ++w) lo[w] = f[w], hi[w] = f[3 + w];
-    const uint32_t rs = (uint32_t)pe[3].x, txn = (uint32_t)(pe[3].x >> 32);
-    // pa = #keys < lo, pb = #keys <= hi: root-to-leaf walks of the Eytzinger
-    // tree in lockstep; padding keys (~0) are above every bound
-    uint32_t ja = 1, jb = 1;
-#pragma unroll
-    for (int d = 0; d < kCTLog2; ++d) {
-        const bool ga = slot_lt<WG>(kw, ja, lo), gb = slot_le<WG>(kw, jb, hi);
-        ja = 2 * ja + ga;
-        jb = 2 * jb + gb;
-    }
-    uint32_t pa = min(ja - T + slot_lt<WG>(kw, 0, lo), tn);
-    uint32_t pb = min(jb - T + slot_le<WG>(kw, 0, hi), tn);
-    if (kind == kCTail) pa = 0;
-    if (kind == kCHead) pb = tn;
-    if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) flags[txn] = 1;
+    HSC_STAMP(work, 1, 2);
+    if (live && !ct.dbg)
+        join_search<WG>(work, ct, flags, kw, rank, b16, b128, B, kind, pl, ph0, ph1);
+    else if (live && (pl[1].y | ph1 | kv[0].x) == 0x5A5A5A5A5A5A5A5Aull) flags[0] = 1;  // keep the loads
+#ifdef HSC_STAMPS
+    __syncthreads();
+    HSC_STAMP(work, 1, 6);
+#endif
 }
 
 template <int WG>
-__global__ __launch_bounds__(kCJT) void k_join_c(ProbeWork work, CTiles ct, uint8_t *flags)
+__global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_join_c(ProbeWork work, CTiles ct, uint8_t *flags)
 {
     constexpr uint32_t T = kCTRows;
     static_assert(T == 2 * kCJT, "a row pair per thread");
     static_assert(kJoinChunk == kCJT && kTileCap == kCJT, "a record per thread");
     extern __shared__ __attribute__((aligned(16))) uint64_t jl[];
-    uint64_t *kw = jl;                                   // [WG][T], Eytzinger order
+    uint64_t *kw = jl;                                   // [WG][T], sorted
     uint32_t *rank = (uint32_t *)(jl + (size_t)WG * T);  // [T], sorted order
     uint32_t *b16 = rank + T;                            // [T / 16]
     uint32_t *b128 = b16 + T / 16;                       // [T / 128]
-    const uint32_t ntiles = ct.ntiles;
-    if (blockIdx.x < ntiles) {
-        join_item<WG, true>(work, ct, flags, 0, kw, rank, b16, b128);
+    uint16_t *B = (uint16_t *)(b128 + T / 128);          // [kTBS] the tile's bucket table
+    // the first xb blocks take the hot tiles' overflow items in turn (dispatched
+    // first: they are the fullest), then one block per tile
+    const uint32_t xb = gridDim.x - ct.ntiles;
+    if (blockIdx.x >= xb) {
+        join_item<WG, true>(work, ct, flags, blockIdx.x - xb, kw, rank, b16, b128, B);
         return;
     }
-    // blocks past the tiles take the hot tiles' overflow items in turn
     const uint32_t nextra = work.item_off[1];
-    const uint32_t stride = gridDim.x - ntiles;
-    for (uint32_t xi = blockIdx.x - ntiles; xi < nextra; xi += stride) {
+    for (uint32_t xi = blockIdx.x; xi < nextra; xi += xb) {
         __syncthreads();  // the previous item's LDS reads are done
-        join_item<WG, false>(work, ct, flags, xi, kw, rank, b16, b128);
+        join_item<WG, false>(work, ct, flags, xi, kw, rank, b16, b128, B);
     }
 }
 
@@ -422,7 +517,8 @@ __global__ __launch_bounds__(kCJT) void k_join_c(ProbeWork work, CTiles ct, uint
 
 hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *gid,
                         const uint64_t *lsn, const CTiles &ct, uint64_t *key, uint32_t *rank,
-                        uint64_t *first, uint64_t *rel, uint32_t *trad, hipStream_t s)
+                        uint64_t *first, uint64_t *rel, uint32_t *trad, uint16_t *tb,
+                        hipStream_t s)
 {
     if (ct.len == 0 || ct.ntiles == 0) return hipSuccess;
     const uint32_t blocks = (uint32_t)((ct.len + 255) / 256);
@@ -433,6 +529,7 @@ hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *g
     default: return hipErrorInvalidValue;
     }
     k_ct_rel<<<(ct.ntiles + 255) / 256, 256, 0, s>>>(first, ct.ntiles, rel);
+    k_ct_tbuckets<<<ct.ntiles, 256, 0, s>>>(ct, key, tb);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return narrow_trad_build(rel, ct.ntiles, ct.trad_m, trad, s);
@@ -471,7 +568,7 @@ hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_i
     const uint32_t extra = max_items - ct.ntiles;
     const uint32_t blocks = ct.ntiles + (extra < 512 ? extra : 512);
     const size_t lds = 8 * (size_t)ct.WG * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
-                       4 * (kCTRows / 128);
+                       4 * (kCTRows / 128) + 2 * kTBS;
     switch (ct.WG) {
     case 1: k_join_c<1><<<blocks, kCJT, lds, s>>>(work, ct, flags); break;
     case 2: k_join_c<2><<<blocks, kCJT, lds, s>>>(work, ct, flags); break;

@@ -240,7 +240,11 @@ __device__ __forceinline__ bool any_after32(const uint32_t *rank, const uint32_t
     const uint32_t q1 = q - 1;
     const bool hot_p = b16[p >> 4] > s, hot_q = b16[q1 >> 4] > s;
     if (!hot_p && !hot_q && (q1 >> 4) <= (p >> 4) + 1) return false;
-    if (q - p <= 16) return any_gt32<16>(rank, p, q, s);
+    if (q - p <= 16) {  // short range: only its own rows (a wave runs its longest lane's count)
+        bool r = false;
+        for (uint32_t i = p; i < q; ++i) r |= rank[i] > s;
+        return r;
+    }
     const uint32_t p16 = (p + 15) & ~15u, q16 = q & ~15u;
     const uint32_t bp = p16 >> 4, bq = q16 >> 4;
     const uint32_t bp8 = min((bp + 7) & ~7u, bq), bq8 = max(bq & ~7u, bp8);

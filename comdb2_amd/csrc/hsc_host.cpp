@@ -231,7 +231,7 @@ struct hsc_ctx {
     // compact tiles (hsc_ctiles.hip): the compact window as gid || code keys
     bool ctiles = false;
     CTiles ctv{};
-    DBuf d_ckey, d_crank, d_cfirst, d_crel, d_ctrad;
+    DBuf d_ckey, d_crank, d_cfirst, d_crel, d_ctrad, d_ctb;
 
     // probe workspace
     DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;
@@ -621,13 +621,16 @@ static int build_ctiles(hsc_ctx *c)
     HIPCHK(c, c->d_cfirst.ensure(8 * (size_t)WG * ct.ntiles));
     HIPCHK(c, c->d_crel.ensure(8 * (size_t)ct.ntiles));
     HIPCHK(c, c->d_ctrad.ensure(4 * ((size_t)ct.trad_m + 2)));
+    HIPCHK(c, c->d_ctb.ensure(2 * (size_t)kTBS * ct.ntiles));
+    ct.tb = c->d_ctb.as<uint16_t>();
     ct.key = c->d_ckey.as<uint64_t>();
     ct.rank = c->d_crank.as<uint32_t>();
     ct.first = c->d_cfirst.as<uint64_t>();
     ct.trad = c->d_ctrad.as<uint32_t>();
     HIPCHK(c, ctiles_build(v.words, v.stride, ct.WC, v.gid, v.lsn, ct, c->d_ckey.as<uint64_t>(),
                            c->d_crank.as<uint32_t>(), c->d_cfirst.as<uint64_t>(),
-                           c->d_crel.as<uint64_t>(), c->d_ctrad.as<uint32_t>(), s));
+                           c->d_crel.as<uint64_t>(), c->d_ctrad.as<uint32_t>(),
+                           c->d_ctb.as<uint16_t>(), s));
     HIPCHK(c, hipMemcpyAsync(&ct.base0, c->d_cfirst.p, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     c->ctiles = true;
@@ -1648,6 +1651,57 @@ static int probe_narrow(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w,
 static int probe_tiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w, const ProbeView &p,
                        bool started = false);
 
+#ifdef HSC_STAMPS
+// Diagnostic builds: phase durations of the locate (np0 stamps) and the join
+// (np1 stamps), median over blocks, in shader cycles; clears the stamps.
+static int stamp_report(hsc_ctx *c, const ProbeWork &work, uint32_t max_items, int np0, int np1)
+{
+    hipStream_t s = c->stream;
+    if (!work.stamps) return HSC_OK;
+    std::vector<uint64_t> h(2 * 8192 * 8);
+    HIPCHK(c, hipMemcpyAsync(h.data(), work.stamps, 8 * h.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    const uint32_t nb[2] = {8 * ((work.G + 7) / 8), max_items};
+    const int np[2] = {np0, np1};
+    for (int k = 0; k < 2; ++k) {
+        fprintf(stderr, "[stamps] %s blocks %u:", k ? "join" : "locate", nb[k]);
+        uint64_t t0 = ~0ull, t1 = 0;
+        for (uint32_t b = 0; b < nb[k] && b < 8192; ++b) {
+            const uint64_t *r = &h[((size_t)k * 8192 + b) * 8];
+            if (!r[0]) continue;
+            t0 = std::min(t0, r[0]);
+            t1 = std::max(t1, r[np[k] - 1]);
+        }
+        for (int q = 1; q < np[k]; ++q) {
+            std::vector<uint64_t> d;
+            for (uint32_t b = 0; b < nb[k] && b < 8192; ++b) {
+                const uint64_t *r = &h[((size_t)k * 8192 + b) * 8];
+                if (r[q] && r[q - 1]) d.push_back(r[q] - r[q - 1]);
+            }
+            std::sort(d.begin(), d.end());
+            fprintf(stderr, " p%d %llu", q, d.empty() ? 0ull : (unsigned long long)d[d.size() / 2]);
+        }
+        std::vector<uint64_t> st;
+        for (uint32_t b = 0; b < nb[k] && b < 8192; ++b) {
+            const uint64_t *r = &h[((size_t)k * 8192 + b) * 8];
+            if (r[0]) st.push_back(r[0] - t0);
+        }
+        std::sort(st.begin(), st.end());
+        fprintf(stderr, " | span %llu, start p50 %llu p90 %llu\n", (unsigned long long)(t1 - t0),
+                st.empty() ? 0ull : (unsigned long long)st[st.size() / 2],
+                st.empty() ? 0ull : (unsigned long long)st[st.size() * 9 / 10]);
+    }
+    HIPCHK(c, hipMemsetAsync(work.stamps, 0, 8 * h.size(), s));
+    return HSC_OK;
+}
+
+static DBuf &stamp_buffer()
+{
+    static DBuf b;
+    return b;
+}
+#endif
+
 // Narrow tiles (dense batch): locate (codes, snapshot ranks, per-chunk tile
 // histograms) -> column scan + plan -> scatter (16-byte records) -> join
 // (8-byte rows) -> pack.
@@ -1687,7 +1741,7 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     work.item_tile = c->w_item_tile.as<uint32_t>();
     work.item_desc = c->w_item_desc.as<uint4>();
 #ifdef HSC_STAMPS
-    static DBuf stamp_buf;
+    DBuf &stamp_buf = stamp_buffer();
     if (getenv("HSC_STAMPS")) {
         if (!stamp_buf.p) {
             HIPCHK(c, stamp_buf.ensure(8 * 2 * 8192 * 8));
@@ -1734,42 +1788,7 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
 #ifdef HSC_STAMPS
-    if (work.stamps) {  // diagnostic build: phase durations (median over blocks, cycles)
-        std::vector<uint64_t> h(2 * 8192 * 8);
-        HIPCHK(c, hipMemcpyAsync(h.data(), work.stamps, 8 * h.size(), hipMemcpyDeviceToHost, s));
-        HIPCHK(c, hipStreamSynchronize(s));
-        const uint32_t nb[2] = {8 * ((work.G + 7) / 8), max_items};
-        const int np[2] = {5, 3};
-        for (int k = 0; k < 2; ++k) {
-            fprintf(stderr, "[stamps] %s blocks %u:", k ? "join" : "locate", nb[k]);
-            uint64_t t0 = ~0ull, t1 = 0;
-            for (uint32_t b = 0; b < nb[k] && b < 8192; ++b) {
-                const uint64_t *r = &h[((size_t)k * 8192 + b) * 8];
-                if (!r[0]) continue;
-                t0 = std::min(t0, r[0]);
-                t1 = std::max(t1, r[np[k] - 1]);
-            }
-            for (int q = 1; q < np[k]; ++q) {
-                std::vector<uint64_t> d;
-                for (uint32_t b = 0; b < nb[k] && b < 8192; ++b) {
-                    const uint64_t *r = &h[((size_t)k * 8192 + b) * 8];
-                    if (r[q] && r[q - 1]) d.push_back(r[q] - r[q - 1]);
-                }
-                std::sort(d.begin(), d.end());
-                fprintf(stderr, " p%d %llu", q, d.empty() ? 0ull : (unsigned long long)d[d.size() / 2]);
-            }
-            std::vector<uint64_t> st;
-            for (uint32_t b = 0; b < nb[k] && b < 8192; ++b) {
-                const uint64_t *r = &h[((size_t)k * 8192 + b) * 8];
-                if (r[0]) st.push_back(r[0] - t0);
-            }
-            std::sort(st.begin(), st.end());
-            fprintf(stderr, " | span %llu, start p50 %llu p90 %llu\n", (unsigned long long)(t1 - t0),
-                    st.empty() ? 0ull : (unsigned long long)st[st.size() / 2],
-                    st.empty() ? 0ull : (unsigned long long)st[st.size() * 9 / 10]);
-        }
-        HIPCHK(c, hipMemsetAsync(work.stamps, 0, 8 * h.size(), s));
-    }
+    HIPCHK_RC(c, stamp_report(c, work, max_items, 5, 3));
 #endif
     return HSC_OK;
 }
@@ -1811,6 +1830,19 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
     ct.ent = c->w_tcode.as<uint64_t>();
     ct.slot = c->w_tcode2.as<uint2>();
     ct.recs = c->w_trecs.as<uint32_t>();
+    ct.np = p.n;
+#ifdef HSC_STAMPS
+    DBuf &stamp_buf = stamp_buffer();
+    if (getenv("HSC_STAMPS")) {
+        if (!stamp_buf.p) {
+            HIPCHK(c, stamp_buf.ensure(8 * 2 * 8192 * 8));
+            HIPCHK(c, hipMemsetAsync(stamp_buf.p, 0, 8 * 2 * 8192 * 8, s));
+        }
+        work.stamps = stamp_buf.as<uint64_t>();
+    }
+#endif
+    static const int dbg = getenv("HSC_CT_DBG") ? atoi(getenv("HSC_CT_DBG")) : 0;
+    ct.dbg = dbg;
     const size_t had = c->w_vflags.bytes;
     HIPCHK(c, c->w_vflags.ensure(std::max<size_t>(b->n_txn, 1)));
     if (c->w_vflags.bytes != had) HIPCHK(c, hipMemsetAsync(c->w_vflags.p, 0, c->w_vflags.bytes, s));
@@ -1843,6 +1875,9 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
     HIPCHK_RC(c, probe_delta(c, flags));
     HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
+#ifdef HSC_STAMPS
+    HIPCHK_RC(c, stamp_report(c, work, max_items, 2, 7));
+#endif
     return HSC_OK;
 }
 

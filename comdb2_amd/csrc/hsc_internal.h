@@ -414,9 +414,12 @@ hipError_t compact_probes(const ProbeView &p, const CompactTables &t, uint64_t *
 // WG-word keys gid || code (WG <= 3) with 32-bit commit times, 2048-row
 // tiles, for dense batches.
 constexpr int kCTLog2 = 11;
+constexpr int kTBLog2 = 8, kTB = 1 << kTBLog2;  // word-0 buckets per tile
+constexpr int kTBS = kTB + 4;                     // u16 per tile: kTB + 1 counts, the shift, pad
 struct CTiles {
-    const uint64_t *key;     // [WG][len] row keys, Eytzinger order per tile (padding ~0)
+    const uint64_t *key;     // [WG][len] row keys, sorted (padding ~0)
     const uint32_t *rank;    // [len] lsn - rank_base + 1 in row order (padding 0)
+    const uint16_t *tb;      // [ntiles][kTBS] per-tile word-0 bucket table (k_ct_tbuckets)
     const uint64_t *first;   // [WG][ntiles] first key of every tile
     const uint32_t *trad;    // [trad_m + 2] bucket table over first word 0 - base0
     uint32_t trad_m;
@@ -425,13 +428,17 @@ struct CTiles {
     size_t len;              // row stride (n rounded up to whole tiles)
     uint32_t n, ntiles;
     int WG, WC, gb;          // key words, code words, group bits
-    uint64_t *ent;           // [n][8] probe entries {lo[3], hi[3], r(S) | read set << 32, 0}
+    uint64_t *ent;           // [2][np][4] probe entries: {lo[3], r(S) | read set << 32}, then
+                             // {hi[3], r(S) | read set << 32}
+    uint32_t np;             // probes of the batch
     uint2 *slot;             // [n] (tile << 12 | in-chunk rank) of the first / second record
     uint32_t *recs;          // bucket entries: probe | kind << 30
+    int dbg;                 // diagnostics (HSC_CT_DBG): 1 join skips the searches, 2 also the gathers
 };
 hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *gid,
                         const uint64_t *lsn, const CTiles &ct, uint64_t *key, uint32_t *rank,
-                        uint64_t *first, uint64_t *rel, uint32_t *trad, hipStream_t s);
+                        uint64_t *first, uint64_t *rel, uint32_t *trad, uint16_t *tb,
+                        hipStream_t s);
 size_t ctiles_locate_lds(const CTiles &ct);
 uint32_t ctiles_chunk();
 hipError_t launch_locate_c(const CTiles &ct, const WinView &wt, const ProbeView &p,
