@@ -801,9 +801,14 @@ __device__ __forceinline__ void loc_defer_run(const WinView &wt, const ProbeView
 #define HSC_LOC_SUB 2
 #endif
 constexpr int kLocSub = HSC_LOC_SUB;
+#ifndef HSC_LOC_WPE
+#define HSC_LOC_ATTR
+#else  // A/B builds: hold the locate to HSC_LOC_WPE waves per SIMD
+#define HSC_LOC_ATTR __attribute__((amdgpu_waves_per_eu(HSC_LOC_WPE, HSC_LOC_WPE)))
+#endif
 static_assert(kLocTP % kLocSub == 0, "whole sub-chunks");
 template <int W, bool kTrad>
-__global__ __launch_bounds__(kLocTThreads) void k_locate_t(NarrowView nv, WinView wt,
+__global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowView nv, WinView wt,
                                                              ProbeView p, ProbeWork work,
                                                              NarrowTiles nt, uint8_t *verdict)
 {
