@@ -1925,8 +1925,11 @@ static int probe_lane(hsc_ctx *c, const hsc_probe_batch *b)
     p.n_lock = (uint32_t)b->n_lock;
     c->raw_probe = p;
     c->raw_probe.n = (uint32_t)b->n;  // the delta may hold keys of an empty main window
+    // compact tiles for dense batches; a sparse one (fewer than kDirectPerTile
+    // ranges per tile) takes the wide pipeline, which stages only the tiles
+    // its ranges reach (the compact-tile join stages every tile)
     if (!c->narrow && c->compact && c->ctiles && c->layout != HSC_LAYOUT_COMPACT_WIDE &&
-        p.n < (1u << 30) &&
+        p.n < (1u << 30) && (size_t)p.n >= kDirectPerTile * (size_t)c->ctv.ntiles &&
         (std::max<size_t>(p.n, p.n_lock) + ctiles_chunk() - 1) / ctiles_chunk() <= (size_t)kMaxChunks)
         return probe_ctiles(c, b, p);
     if (!c->narrow && c->compact) {

@@ -125,6 +125,8 @@ def test_hot_tiles_overflow_match_oracle(oracle_mod):
 
 
 def test_sparse_batch_matches_oracle(oracle_mod):
+    """A sparse batch (fewer ranges than 8 per tile) on a compact-tile window
+    takes the wide pipeline, which stages only the tiles its ranges reach."""
     log, rs = _short_case(5, n_commits=6000, n_txn=20)
     want = oracle_mod.check(log, rs, nthreads=8)[0] != 0
     v = Validator(0)
