@@ -570,7 +570,7 @@ static int build_compact(hsc_ctx *c, const WinView &w)
     v.words = c->d_cwords.as<uint64_t>();
     v.W = WC;
     v.compact = 1;
-    v.log2T = tile_log2(WC);
+    v.log2T = std::min(tile_log2(WC), kCTLog2);  // the compact tiles share these tiles' maxima
     v.ntiles = (uint32_t)((c->n + ((size_t)1 << v.log2T) - 1) >> v.log2T);
     v.levels = 0;
     while (((size_t)1 << v.levels) <= v.ntiles) v.levels++;

@@ -18,7 +18,8 @@ ROWS = [0x00, 0x08, 0x61, 0x62]
 PROBE = [0x00, 0x07, 0x08, 0x09, 0x60, 0x61, 0x62, 0x63, 0xFF]
 
 
-def _short_case(seed, n_commits=3000, n_txn=900, lens=(9, 17, 23), n_tabs=4, hot=0.0, var=None):
+def _short_case(seed, n_commits=3000, n_txn=900, lens=(9, 17, 23), n_tabs=4, hot=0.0, var=None,
+                ends=False):
     """Keys of few varying bits per byte (codes + group id fit 3 words), probes
     equal to rows, prefixes, one-byte edits, inverted and open ranges; hot > 0:
     that share of ranges are points on a handful of keys (overflowing tiles)."""
@@ -35,6 +36,8 @@ def _short_case(seed, n_commits=3000, n_txn=900, lens=(9, 17, 23), n_tabs=4, hot
             nv = lens[ix] - 1 if var is None else min(var, lens[ix] - 1)  # varying bytes, then 0x01s
             k = bytes([8]) + rng.choice(ROWS, size=nv).astype(np.uint8).tobytes()
             k += b"\x01" * (lens[ix] - len(k))
+            if ends:  # ... and two more varying bytes at the key's end
+                k = k[:-2] + rng.choice(ROWS, size=2).astype(np.uint8).tobytes()
             keys.setdefault((tb, ix), []).append(k)
             lb.write(c, F.REC_UNDO_ADD_IX_LK, tb, ix, k)
         snaps.append(lb.commit(c))
@@ -186,3 +189,58 @@ def test_long_keys_unfused_locate_match_oracle(oracle_mod):
         v.close()
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(ref, want)
+
+
+def test_one_word_keys_match_oracle(oracle_mod):
+    """Varying bytes at both ends of 17-byte keys: too far apart for the
+    narrow 62-bit codes, but the compact codes plus the group id fit one word
+    (WG = 1)."""
+    log, rs = _short_case(17, n_commits=2500, n_txn=800, lens=(9, 17), var=2, ends=True)
+    want = oracle_mod.check(log, rs, nthreads=8)[0] != 0
+    v = Validator(0)
+    try:
+        got, ref = _both(v, log, rs)
+        assert v.tile_key_words == 1
+    finally:
+        v.close()
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(ref, want)
+    assert 0.02 < want.mean() < 0.98
+
+
+def test_config3_full_size_matches_sortjoin():
+    """BASELINE config 3 at full size (4M index writes, 100k read sets) through
+    the compact tiles: equal to the CPU sort-join over the same window
+    (oracle/sortjoin.c) and to the wide compact pipeline."""
+    import sys, os
+    torch = pytest.importorskip("torch")
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
+    import oracle
+    from comdb2_amd.workloads import config3_arrays
+    a = config3_arrays(n_writes=4_000_000, n_txn=100_000)
+    v = Validator(0)
+    try:
+        for g, (tb, ix, L) in enumerate(a.groups):
+            assert v.register_group(tb, ix, L) == g
+        gid, words, lsn = a.window()
+        dev = torch.device("cuda", 0)
+        tg = torch.from_numpy(gid).to(dev)
+        tw = torch.from_numpy(words.reshape(-1).view(np.int64)).to(dev)
+        tl = torch.from_numpy(lsn.view(np.int64)).to(dev)
+        v.ingest_device(len(lsn), words.shape[0], tg.data_ptr(), tw.data_ptr(), tl.data_ptr(),
+                        a.end_lsn)
+        torch.cuda.synchronize()
+        v.merge_table_max(a.table_max)
+        assert v.tile_key_words == 3
+        m = v.marshal(a.readsets)
+        got = v.check_readsets(a.readsets) != 0
+        v.set_layout(LAYOUT_COMPACT_WIDE)
+        ref = v.check_readsets(a.readsets) != 0
+        sj = oracle.SortJoin(gid, words, lsn, len(a.groups))
+        want, _ = sj.probe(m, v.table_max(), nthreads=8)
+        sj.close()
+    finally:
+        v.close()
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(got, want != 0)
+    assert 0.05 < got.mean() < 0.99
