@@ -212,9 +212,11 @@ struct hsc_ctx {
     bool probe_buckets = false; // the last probe ran the narrow tiles (fixed-capacity buckets)
     // narrow tiles: u32 key deltas + commit ranks (dense batches)
     bool ntiles32 = false;
+    DBuf d_trad2;  // the other bucket-table mode (narrow_trad_pick)
     DBuf d_commits, d_cdir, d_tdir, d_trad, d_done, w_vflags, d_key32, d_rank32, d_ctmp[4];
     Dir16 cdir{}, tdir{};
     uint32_t trad_m = 0;       // tile bucket table size (0: none)
+    bool trad_log = false;     // the table is in log mode (narrow_trad_pick)
     uint32_t ncommit = 0;
     uint64_t commit_span[2] = {0, 0};  // oldest / newest distinct commit LSN of the window
     bool rank_lsn32 = false;   // narrow tiles: rows carry lsn - rank_base + 1 (NarrowTiles)
@@ -637,6 +639,28 @@ static int build_ctiles(hsc_ctx *c)
     return HSC_OK;
 }
 
+// Narrow tiles' bucket table: linear buckets (uniform keys) or log buckets
+// (keys dense near the window's first, e.g. Zipf hot keys) -- whichever mode's
+// fullest bucket holds fewer tiles (the locate's in-bucket search is
+// log2 of it).  HSC_TRAD_MODE=lin|log forces one (tests).
+static int narrow_trad_pick(hsc_ctx *c)
+{
+    const uint32_t m = c->trad_m;
+    std::vector<uint32_t> a(m + 2), b(m + 2);
+    HIPCHK(c, hipMemcpy(a.data(), c->d_trad.p, 4 * a.size(), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(b.data(), c->d_trad2.p, 4 * b.size(), hipMemcpyDeviceToHost));
+    auto fullest = [m](const std::vector<uint32_t> &t) {
+        uint32_t w = 0;
+        for (uint32_t k = 0; k < m; ++k) w = std::max(w, t[k + 1] - t[k]);
+        return w;
+    };
+    const char *f = getenv("HSC_TRAD_MODE");
+    const bool log = f ? strcmp(f, "log") == 0 : fullest(b) < fullest(a);
+    if (log) std::swap(c->d_trad, c->d_trad2);
+    c->trad_log = log;
+    return HSC_OK;
+}
+
 static int device_build(hsc_ctx *c, size_t n_in)
 {
     HIPCHK(c, wait_lanes(c));
@@ -839,6 +863,11 @@ static int device_build(hsc_ctx *c, size_t n_in)
             if (c->trad_m) {
                 HIPCHK(c, c->d_trad.ensure(4 * ((size_t)c->trad_m + 2)));
                 HIPCHK(c, narrow_trad_build(wn.sp_w, wn.ntiles, c->trad_m, c->d_trad.as<uint32_t>(), s));
+                if (c->trad_m >= 64) {  // the log-mode table too; picked after the build's sync
+                    HIPCHK(c, c->d_trad2.ensure(4 * ((size_t)c->trad_m + 2)));
+                    HIPCHK(c, narrow_trad_build(wn.sp_w, wn.ntiles, c->trad_m,
+                                                c->d_trad2.as<uint32_t>(), s, 1));
+                }
             }
             HIPCHK(c, c->d_key32.ensure(4 * (size_t)nv.len[0]));
             HIPCHK(c, c->d_rank32.ensure(4 * (size_t)nv.len[0]));
@@ -854,6 +883,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, hipEventRecord(e1, s));
     HIPCHK(c, hipStreamSynchronize(s));
     if (tiles32) c->ntiles32 = wide32 == 0;
+    if (c->narrow && c->trad_m >= 64) HIPCHK_RC(c, narrow_trad_pick(c));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
     c->last.ingest_ms = ms;

@@ -254,7 +254,17 @@ uint32_t narrow_tiles_chunk();
 // returns the bucket count m (0: too many tiles, use the directory).
 uint32_t narrow_trad_buckets(uint32_t ntiles);
 hipError_t narrow_trad_build(const uint64_t *first, uint32_t ntiles, uint32_t m, uint32_t *trad,
-                             hipStream_t s);
+                             hipStream_t s, int logmode = 0);
+// log-mode bucket of a code (see k_trad): exponent << sv | sv mantissa bits
+constexpr uint32_t kTradLog = 1u << 16;
+__host__ __device__ inline uint32_t trad_log_bucket(uint64_t x, int sv)
+{
+    if (x == 0) return 0;
+    const int e = 63 - __builtin_clzll(x);
+    const uint64_t mask = (1ull << sv) - 1;
+    const uint64_t mant = e >= sv ? (x >> (e - sv)) & mask : (x << (sv - e)) & mask;
+    return ((uint32_t)e << sv) | (uint32_t)mant;
+}
 uint32_t narrow_tiles_dir_lds();
 // Read/write conflict pairs (hsc_edges.hip) over every window version: the
 // build's key-sorted rows before dedupe.

@@ -682,13 +682,36 @@ uint32_t narrow_trad_buckets(uint32_t ntiles)
     return m;
 }
 
-__global__ void k_trad(const uint64_t *first, uint32_t ntiles, uint32_t m, uint32_t *trad)
+// Log mode (trad[m + 1] = kTradLog | s, m = 64 << s): bucket of x = its
+// exponent and s mantissa bits, like a float -- monotone, with the resolution
+// where the codes are dense near zero (hot keys of a Zipf window crowd a few
+// linear buckets); the build picks the mode whose fullest bucket holds fewer
+// tiles (narrow_trad_pick).
+__global__ void k_trad(const uint64_t *first, uint32_t ntiles, uint32_t m, int logmode,
+                       uint32_t *trad)
 {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k > m + 1) return;
+    const int lg = 31 - __clz(m);
+    if (logmode) {
+        const int sv = lg - 6;
+        if (k == m + 1) {
+            trad[k] = kTradLog | (uint32_t)sv;
+            return;
+        }
+        uint32_t lo = 0, hi = ntiles;  // #tiles whose first code's bucket < k
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (trad_log_bucket(first[mid], sv) < k)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        trad[k] = lo;
+        return;
+    }
     const uint64_t span = first[ntiles - 1];
     const int bits = span ? 64 - __clzll(span) : 0;
-    const int lg = 31 - __clz(m);
     const int shift = bits > lg ? bits - lg : 0;
     if (k == m + 1) {
         trad[k] = (uint32_t)shift;
@@ -707,9 +730,10 @@ __global__ void k_trad(const uint64_t *first, uint32_t ntiles, uint32_t m, uint3
 }
 
 hipError_t narrow_trad_build(const uint64_t *first, uint32_t ntiles, uint32_t m, uint32_t *trad,
-                             hipStream_t s)
+                             hipStream_t s, int logmode)
 {
-    k_trad<<<(m + 2 + 255) / 256, 256, 0, s>>>(first, ntiles, m, trad);
+    if (logmode && m < 64) return hipErrorInvalidValue;
+    k_trad<<<(m + 2 + 255) / 256, 256, 0, s>>>(first, ntiles, m, logmode, trad);
     return hipGetLastError();
 }
 
@@ -748,9 +772,11 @@ __device__ __forceinline__ void trad_count(const uint64_t *first, const uint16_t
                                            const bool (&act)[K], uint32_t (&out)[K])
 {
     uint32_t l[K], h[K];
+    const bool lg = (shift & kTradLog) != 0;
+    const int sv = shift & 0xFFFF;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-        const uint64_t b = x[k] >> shift;
+        const uint64_t b = lg ? trad_log_bucket(x[k], sv) : x[k] >> sv;
         const bool in = b < m;
         const uint32_t bi = in ? (uint32_t)b : 0;
         l[k] = in ? T[bi] : ntiles;

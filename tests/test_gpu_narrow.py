@@ -30,24 +30,28 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
     # (layout, build knob): locate finds tiles through the LDS bucket table by
     # default and through the 16-ary directory with HSC_TILE_DIR set; rows
     # carry lsn - oldest commit + 1 when the window spans < 2^32 of log, the
-    # commit rank (directory search of snapshots) with HSC_RANK_DIR set
+    # commit rank (directory search of snapshots) with HSC_RANK_DIR set; the
+    # bucket table in linear or log mode (HSC_TRAD_MODE; by default the build
+    # picks the mode whose fullest bucket is smaller)
     runs = [(LAYOUT_NARROW_DIRECT, None), (LAYOUT_NARROW_TILES, None),
             (LAYOUT_NARROW_TILES, "HSC_TILE_DIR"), (LAYOUT_NARROW_TILES, "HSC_RANK_DIR"),
+            (LAYOUT_NARROW_TILES, "HSC_TRAD_MODE=log"), (LAYOUT_NARROW_TILES, "HSC_TRAD_MODE=lin"),
             (LAYOUT_NARROW_CODES, None), (LAYOUT_WIDE, None)]
     try:
         for layout, knob in runs:
+            var, _, val = (knob or "").partition("=")
             if knob:
-                os.environ[knob] = "1"
+                os.environ[var] = val or "1"
             v.set_layout(layout)
             v.ingest_log(log)
             if knob:
-                os.environ.pop(knob, None)
+                os.environ.pop(var, None)
             assert v.layout == (LAYOUT_WIDE if layout == LAYOUT_WIDE else expect_auto)
             got[layout] = v.check_readsets(rs)
             np.testing.assert_array_equal(got[layout] != 0, want != 0,
                                           err_msg=f"layout {layout} knob {knob}")
     finally:
-        for knob in ("HSC_TILE_DIR", "HSC_RANK_DIR"):
+        for knob in ("HSC_TILE_DIR", "HSC_RANK_DIR", "HSC_TRAD_MODE"):
             os.environ.pop(knob, None)
         v.set_layout(LAYOUT_AUTO)
     return want
