@@ -203,7 +203,7 @@ hipError_t launch_probes_wc(const ProbeView &p, const CompactMeta &cm, uint64_t 
 {
     static const bool generic = getenv("HSC_COMPACT_GENERIC") != nullptr;  // tests: old kernel
     if (cm.W <= kProbeWords && !generic) {
-        static const int P = getenv("HSC_BOUND_P") ? atoi(getenv("HSC_BOUND_P")) : 2;  // A/B knob
+        static const int P = getenv("HSC_BOUND_P") ? atoi(getenv("HSC_BOUND_P")) : 1;  // A/B knob (r02: 1 beat 2 and 4 on config 3)
         const uint32_t per = kBoundThreads * (P == 1 ? 1 : P == 4 ? 4 : 2);
         const uint32_t blocks = (p.n + per - 1) / per;
         const bool in_lds = bound_lds_bytes(cm.ng, cm.W) <= kBoundLdsBytes;
