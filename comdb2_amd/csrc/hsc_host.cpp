@@ -635,6 +635,24 @@ static int build_ctiles(hsc_ctx *c)
                            c->d_ctb.as<uint16_t>(), s));
     HIPCHK(c, hipMemcpyAsync(&ct.base0, c->d_cfirst.p, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
+    if (getenv("HSC_CT_STATS")) {  // diagnostics: fullest buckets of the locate's and the join's tables
+        std::vector<uint32_t> t(ct.trad_m + 2);
+        std::vector<uint16_t> tb((size_t)kTBS * ct.ntiles);
+        HIPCHK(c, hipMemcpy(t.data(), c->d_ctrad.p, 4 * t.size(), hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(tb.data(), c->d_ctb.p, 2 * tb.size(), hipMemcpyDeviceToHost));
+        uint32_t w = 0;
+        for (uint32_t k = 0; k < ct.trad_m; ++k) w = std::max(w, t[k + 1] - t[k]);
+        std::vector<uint32_t> fb;
+        for (uint32_t x = 0; x < ct.ntiles; ++x) {
+            uint32_t f = 0;
+            for (int k = 0; k < kTB; ++k)
+                f = std::max<uint32_t>(f, tb[(size_t)x * kTBS + k + 1] - tb[(size_t)x * kTBS + k]);
+            fb.push_back(f);
+        }
+        std::sort(fb.begin(), fb.end());
+        fprintf(stderr, "[ct] tiles %u, locate buckets %u fullest %u; join fullest bucket per tile p50 %u p90 %u max %u\n",
+                ct.ntiles, ct.trad_m, w, fb[fb.size() / 2], fb[fb.size() * 9 / 10], fb.back());
+    }
     c->ctiles = true;
     return HSC_OK;
 }

@@ -717,6 +717,10 @@ __global__ void k_trad(const uint64_t *first, uint32_t ntiles, uint32_t m, int l
         trad[k] = (uint32_t)shift;
         return;
     }
+    if (k == m) {  // every first code is below m << shift (which overflows when span >= 2^63)
+        trad[k] = ntiles;
+        return;
+    }
     const uint64_t x = (uint64_t)k << shift;
     uint32_t lo = 0, hi = ntiles;  // #first < x
     while (lo < hi) {

@@ -13,17 +13,21 @@ from comdb2_amd.formats import LogBuilder, Range, ReadSets
 from comdb2_amd.hsc import LAYOUT_AUTO, LAYOUT_COMPACT, LAYOUT_COMPACT_WIDE, Validator
 
 pytestmark = pytest.mark.gpu
+# torch (device arrays for hsc_window_ingest_device) is imported before any
+# test initialises HIP in this process
+torch = pytest.importorskip("torch")
 
 ROWS = [0x00, 0x08, 0x61, 0x62]
 PROBE = [0x00, 0x07, 0x08, 0x09, 0x60, 0x61, 0x62, 0x63, 0xFF]
 
 
 def _short_case(seed, n_commits=3000, n_txn=900, lens=(9, 17, 23), n_tabs=4, hot=0.0, var=None,
-                ends=False):
+                ends=False, rows=None, probe=None):
     """Keys of few varying bits per byte (codes + group id fit 3 words), probes
     equal to rows, prefixes, one-byte edits, inverted and open ranges; hot > 0:
     that share of ranges are points on a handful of keys (overflowing tiles)."""
     rng = np.random.default_rng(seed)
+    ROWS_, PROBE_ = rows or ROWS, probe or PROBE
     lb = LogBuilder()
     snaps = [lb.next_lsn()]
     tabs = [f"t{i}" for i in range(n_tabs)]
@@ -34,10 +38,10 @@ def _short_case(seed, n_commits=3000, n_txn=900, lens=(9, 17, 23), n_tabs=4, hot
             tb = tabs[int(rng.integers(0, n_tabs - 1))]  # the last table is never written
             ix = int(rng.integers(0, len(lens)))
             nv = lens[ix] - 1 if var is None else min(var, lens[ix] - 1)  # varying bytes, then 0x01s
-            k = bytes([8]) + rng.choice(ROWS, size=nv).astype(np.uint8).tobytes()
+            k = bytes([8]) + rng.choice(ROWS_, size=nv).astype(np.uint8).tobytes()
             k += b"\x01" * (lens[ix] - len(k))
             if ends:  # ... and two more varying bytes at the key's end
-                k = k[:-2] + rng.choice(ROWS, size=2).astype(np.uint8).tobytes()
+                k = k[:-2] + rng.choice(ROWS_, size=2).astype(np.uint8).tobytes()
             keys.setdefault((tb, ix), []).append(k)
             lb.write(c, F.REC_UNDO_ADD_IX_LK, tb, ix, k)
         snaps.append(lb.commit(c))
@@ -51,10 +55,10 @@ def _short_case(seed, n_commits=3000, n_txn=900, lens=(9, 17, 23), n_tabs=4, hot
         if ks and rng.random() < 0.6:
             k = bytearray(ks[int(rng.integers(0, len(ks)))])
             if rng.random() < 0.3:
-                k[int(rng.integers(0, kl))] = int(rng.choice(PROBE))
+                k[int(rng.integers(0, kl))] = int(rng.choice(PROBE_))
             cut = int(rng.integers(1, kl + 1)) if rng.random() < 0.25 else kl
             return bytes(k[:cut])
-        return bytes(rng.choice(PROBE, size=int(rng.integers(1, kl + 1))).astype(np.uint8))
+        return bytes(rng.choice(PROBE_, size=int(rng.integers(1, kl + 1))).astype(np.uint8))
 
     sets, ss = [], []
     for t in range(n_txn):
@@ -213,7 +217,6 @@ def test_config3_full_size_matches_sortjoin():
     the compact tiles: equal to the CPU sort-join over the same window
     (oracle/sortjoin.c) and to the wide compact pipeline."""
     import sys, os
-    torch = pytest.importorskip("torch")
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
     import oracle
     from comdb2_amd.workloads import config3_arrays
@@ -244,3 +247,20 @@ def test_config3_full_size_matches_sortjoin():
     np.testing.assert_array_equal(got, ref)
     np.testing.assert_array_equal(got, want != 0)
     assert 0.05 < got.mean() < 0.99
+
+
+def test_keys_in_the_top_bucket_match_oracle(oracle_mod):
+    """32 groups (5 group bits) whose keys' varying bytes are 0x00 / 0xFF: the
+    last group's keys reach the top of the key space, so the locate's bucket
+    table spans 2^64 (its last bucket boundary overflows)."""
+    log, rs = _short_case(23, n_commits=3000, n_txn=900, lens=(9, 12, 17, 20), n_tabs=9, var=10,
+                          rows=[0x00, 0xFF], probe=[0x00, 0x01, 0xFE, 0xFF])
+    want = oracle_mod.check(log, rs, nthreads=8)[0] != 0
+    v = Validator(0)
+    try:
+        got, ref = _both(v, log, rs)
+    finally:
+        v.close()
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(ref, want)
+    assert 0.02 < want.mean() < 0.98
