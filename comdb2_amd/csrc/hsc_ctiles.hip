@@ -113,10 +113,11 @@ __global__ void k_ct_rel(const uint64_t *first0, uint32_t ntiles, uint64_t *rel)
 
 // Per tile: kTB buckets over word 0 of its rows relative to the first row's,
 // shift = the least that puts the last row's below kTB << shift;
-// tb[t * kTBS + k] = #rows of the tile whose bucket is < k (k <= kTB), then
-// the shift.  A join search starts inside one bucket (a few rows) instead of
+// tb[t * kTBS + k] = B(k) | B(k + 1) << 16 for k < kTB, B(k) = #rows of the
+// tile whose bucket is < k (one LDS read gives a bucket's row span), then
+// tn | shift << 16.  A join search starts inside one bucket (a few rows) instead of
 // walking the tile's 11 levels.
-__global__ __launch_bounds__(256) void k_ct_tbuckets(CTiles ct, const uint64_t *key0, uint16_t *tb)
+__global__ __launch_bounds__(256) void k_ct_tbuckets(CTiles ct, const uint64_t *key0, uint32_t *tb)
 {
     __shared__ uint32_t cnt[kTB];
     const uint32_t t = blockIdx.x, tid = threadIdx.x;
@@ -133,12 +134,9 @@ __global__ __launch_bounds__(256) void k_ct_tbuckets(CTiles ct, const uint64_t *
     __syncthreads();  // every count read before the scan reuses cnt as scratch
     uint32_t tot;
     const uint32_t pre = block_excl_scan<256>(mine, cnt, tot);
-    uint16_t *o = tb + (size_t)t * kTBS;
-    o[tid] = (uint16_t)pre;
-    if (tid == 0) {
-        o[kTB] = (uint16_t)tn;
-        o[kTB + 1] = (uint16_t)shift;
-    }
+    uint32_t *o = tb + (size_t)t * kTBS;
+    o[tid] = pre | (pre + mine) << 16;
+    if (tid == 0) o[kTB] = tn | (uint32_t)shift << 16;
 }
 
 // ---- locate ----
@@ -326,15 +324,16 @@ __global__ __launch_bounds__(kCLocThreads) void k_scatter_c(CTiles ct, ProbeWork
 // #rows < x (LE: <= x) of the tile: x's word-0 bucket, then a binary search
 // of that bucket's rows (sorted order, full-key compares)
 template <int WG, bool LE>
-__device__ __forceinline__ uint32_t tile_count(const uint64_t *kw, const uint16_t *B, int shift,
-                                               uint32_t tn, const uint64_t (&x)[WG])
+__device__ __forceinline__ uint32_t tile_count(const uint64_t *kw, const uint32_t *B, int shift,
+                                               uint32_t tn, const uint64_t (&x)[WG], bool &found)
 {
     constexpr uint32_t T = kCTRows;
     const uint64_t f0 = kw[0];
     if (x[0] < f0) return 0;
     const uint64_t d = (x[0] - f0) >> shift;
     if (d >= (uint64_t)kTB) return tn;
-    uint32_t l = B[d], h = B[d + 1];
+    const uint32_t span = B[d];
+    uint32_t l = span & 0xFFFF, h = span >> 16;
     while (l < h) {
         const uint32_t mid = (l + h) >> 1;
         // word 0 decides unless equal; later words are read only on a tie
@@ -347,6 +346,7 @@ __device__ __forceinline__ uint32_t tile_count(const uint64_t *kw, const uint16_
                 below = v < x[w];
                 eq = v == x[w];
             }
+        found |= eq;  // a row equal to x was compared (lower bound: it is the result)
         below = eq ? LE : below;
         l = below ? mid + 1 : l;
         h = below ? h : mid;
@@ -382,11 +382,11 @@ template <int WG>
 __device__ __forceinline__ void join_search(const ProbeWork &work, const CTiles &ct, uint8_t *flags,
                                             const uint64_t *kw, const uint32_t *rank,
                                             const uint32_t *b16, const uint32_t *b128,
-                                            const uint16_t *B, uint32_t kind, const u64x2 (&pl)[2],
+                                            const uint32_t *B, uint32_t kind, const u64x2 (&pl)[2],
                                             const u64x2 ph0, const uint64_t ph1)
 {
-    const uint32_t tn = B[kTB];
-    const int shift = B[kTB + 1];
+    const uint32_t tn = B[kTB] & 0xFFFF;
+    const int shift = (int)(B[kTB] >> 16);
     uint64_t lo[WG], hi[WG];
     const uint64_t fl[3] = {pl[0].x, pl[0].y, pl[1].x}, fh[3] = {ph0.x, ph0.y, ph1};
 #pragma unroll
@@ -398,11 +398,14 @@ __device__ __forceinline__ void join_search(const ProbeWork &work, const CTiles 
 #endif
     HSC_STAMP(work, 1, 3);
     uint32_t pa = 0, pb = tn;
-    if (kind != kCTail) pa = tile_count<WG, false>(kw, B, shift, tn, lo);
+    // a point: #rows <= lo = #rows < lo + (a row equals lo), and a lower-bound
+    // search compares the equal row if there is one
+    bool eqa = false, eqb = false;
+    if (kind != kCTail) pa = tile_count<WG, false>(kw, B, shift, tn, lo, eqa);
     if (kind == kCPoint)
-        pb = pa + (pa < tn && row_eq<WG>(kw, pa, lo));
+        pb = pa + eqa;
     else if (kind != kCHead)
-        pb = tile_count<WG, true>(kw, B, shift, tn, hi);
+        pb = tile_count<WG, true>(kw, B, shift, tn, hi, eqb);
 #ifdef HSC_STAMPS
     if (threadIdx.x == 0 && work.stamps && pa + pb == 0x7FFFFFFF) flags[0] = 1;
 #endif
@@ -425,7 +428,7 @@ __device__ __forceinline__ void join_search(const ProbeWork &work, const CTiles 
 template <int WG, bool kTile>
 __device__ __forceinline__ void join_item(const ProbeWork &work, const CTiles &ct, uint8_t *flags,
                                           uint32_t xi, uint64_t *kw, uint32_t *rank,
-                                          uint32_t *b16, uint32_t *b128, uint16_t *B)
+                                          uint32_t *b16, uint32_t *b128, uint32_t *B)
 {
     constexpr uint32_t T = kCTRows;
     const uint32_t tid = threadIdx.x;
@@ -446,7 +449,7 @@ __device__ __forceinline__ void join_item(const ProbeWork &work, const CTiles &c
     for (int w = 0; w < WG; ++w) kv[w] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row);
     const u32x2 rr = *(const u32x2 *)(ct.rank + row);
     u32x2 bt = {0, 0};
-    if (tid < kTBS / 4) bt = *(const u32x2 *)(ct.tb + (size_t)tile * kTBS + 4 * tid);
+    if (tid < kTBS / 2) bt = *(const u32x2 *)(ct.tb + (size_t)tile * kTBS + 2 * tid);
     if constexpr (kTile) r1 = r0 + min(kTileCap, sload(work.counts + tile));
     // no early exit for a tile without records: it would let the compiler sink
     // the row loads below the count's wait
@@ -467,7 +470,7 @@ __device__ __forceinline__ void join_item(const ProbeWork &work, const CTiles &c
 #pragma unroll
     for (int w = 0; w < WG; ++w) *(u64x2 *)(kw + (size_t)w * T + 2 * tid) = kv[w];
     *(u32x2 *)(rank + 2 * tid) = rr;
-    if (tid < kTBS / 4) *(u32x2 *)(B + 4 * tid) = bt;
+    if (tid < kTBS / 2) *(u32x2 *)(B + 2 * tid) = bt;
     uint32_t m = max(rr.x, rr.y);
 #pragma unroll
     for (int d = 1; d < 8; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
@@ -498,7 +501,7 @@ __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     uint32_t *rank = (uint32_t *)(jl + (size_t)WG * T);  // [T], sorted order
     uint32_t *b16 = rank + T;                            // [T / 16]
     uint32_t *b128 = b16 + T / 16;                       // [T / 128]
-    uint16_t *B = (uint16_t *)(b128 + T / 128);          // [kTBS] the tile's bucket table
+    uint32_t *B = b128 + T / 128;                        // [kTBS] the tile's bucket table
     // the first xb blocks take the hot tiles' overflow items in turn (dispatched
     // first: they are the fullest), then one block per tile
     const uint32_t xb = gridDim.x - ct.ntiles;
@@ -517,7 +520,7 @@ __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 
 hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *gid,
                         const uint64_t *lsn, const CTiles &ct, uint64_t *key, uint32_t *rank,
-                        uint64_t *first, uint64_t *rel, uint32_t *trad, uint16_t *tb,
+                        uint64_t *first, uint64_t *rel, uint32_t *trad, uint32_t *tb,
                         hipStream_t s)
 {
     if (ct.len == 0 || ct.ntiles == 0) return hipSuccess;
@@ -529,7 +532,7 @@ hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *g
     default: return hipErrorInvalidValue;
     }
     k_ct_rel<<<(ct.ntiles + 255) / 256, 256, 0, s>>>(first, ct.ntiles, rel);
-    k_ct_tbuckets<<<ct.ntiles, 256, 0, s>>>(ct, key, tb);
+    k_ct_tbuckets<<<ct.ntiles, 256, 0, s>>>(ct, key, tb);  // kTB == 256: a thread per bucket
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return narrow_trad_build(rel, ct.ntiles, ct.trad_m, trad, s);
@@ -568,7 +571,7 @@ hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_i
     const uint32_t extra = max_items - ct.ntiles;
     const uint32_t blocks = ct.ntiles + (extra < 512 ? extra : 512);
     const size_t lds = 8 * (size_t)ct.WG * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
-                       4 * (kCTRows / 128) + 2 * kTBS;
+                       4 * (kCTRows / 128) + 4 * kTBS;
     switch (ct.WG) {
     case 1: k_join_c<1><<<blocks, kCJT, lds, s>>>(work, ct, flags); break;
     case 2: k_join_c<2><<<blocks, kCJT, lds, s>>>(work, ct, flags); break;

@@ -623,8 +623,8 @@ static int build_ctiles(hsc_ctx *c)
     HIPCHK(c, c->d_cfirst.ensure(8 * (size_t)WG * ct.ntiles));
     HIPCHK(c, c->d_crel.ensure(8 * (size_t)ct.ntiles));
     HIPCHK(c, c->d_ctrad.ensure(4 * ((size_t)ct.trad_m + 2)));
-    HIPCHK(c, c->d_ctb.ensure(2 * (size_t)kTBS * ct.ntiles));
-    ct.tb = c->d_ctb.as<uint16_t>();
+    HIPCHK(c, c->d_ctb.ensure(4 * (size_t)kTBS * ct.ntiles));
+    ct.tb = c->d_ctb.as<uint32_t>();
     ct.key = c->d_ckey.as<uint64_t>();
     ct.rank = c->d_crank.as<uint32_t>();
     ct.first = c->d_cfirst.as<uint64_t>();
@@ -632,21 +632,21 @@ static int build_ctiles(hsc_ctx *c)
     HIPCHK(c, ctiles_build(v.words, v.stride, ct.WC, v.gid, v.lsn, ct, c->d_ckey.as<uint64_t>(),
                            c->d_crank.as<uint32_t>(), c->d_cfirst.as<uint64_t>(),
                            c->d_crel.as<uint64_t>(), c->d_ctrad.as<uint32_t>(),
-                           c->d_ctb.as<uint16_t>(), s));
+                           c->d_ctb.as<uint32_t>(), s));
     HIPCHK(c, hipMemcpyAsync(&ct.base0, c->d_cfirst.p, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     if (getenv("HSC_CT_STATS")) {  // diagnostics: fullest buckets of the locate's and the join's tables
         std::vector<uint32_t> t(ct.trad_m + 2);
-        std::vector<uint16_t> tb((size_t)kTBS * ct.ntiles);
+        std::vector<uint32_t> tb((size_t)kTBS * ct.ntiles);
         HIPCHK(c, hipMemcpy(t.data(), c->d_ctrad.p, 4 * t.size(), hipMemcpyDeviceToHost));
-        HIPCHK(c, hipMemcpy(tb.data(), c->d_ctb.p, 2 * tb.size(), hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(tb.data(), c->d_ctb.p, 4 * tb.size(), hipMemcpyDeviceToHost));
         uint32_t w = 0;
         for (uint32_t k = 0; k < ct.trad_m; ++k) w = std::max(w, t[k + 1] - t[k]);
         std::vector<uint32_t> fb;
         for (uint32_t x = 0; x < ct.ntiles; ++x) {
             uint32_t f = 0;
             for (int k = 0; k < kTB; ++k)
-                f = std::max<uint32_t>(f, tb[(size_t)x * kTBS + k + 1] - tb[(size_t)x * kTBS + k]);
+                f = std::max<uint32_t>(f, (tb[(size_t)x * kTBS + k] >> 16) - (tb[(size_t)x * kTBS + k] & 0xFFFF));
             fb.push_back(f);
         }
         std::sort(fb.begin(), fb.end());

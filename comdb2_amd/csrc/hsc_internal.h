@@ -425,11 +425,11 @@ hipError_t compact_probes(const ProbeView &p, const CompactTables &t, uint64_t *
 // tiles, for dense batches.
 constexpr int kCTLog2 = 11;
 constexpr int kTBLog2 = 8, kTB = 1 << kTBLog2;  // word-0 buckets per tile
-constexpr int kTBS = kTB + 4;                     // u16 per tile: kTB + 1 counts, the shift, pad
+constexpr int kTBS = kTB + 4;                     // u32 per tile: kTB spans, tn | shift, pad
 struct CTiles {
     const uint64_t *key;     // [WG][len] row keys, sorted (padding ~0)
     const uint32_t *rank;    // [len] lsn - rank_base + 1 in row order (padding 0)
-    const uint16_t *tb;      // [ntiles][kTBS] per-tile word-0 bucket table (k_ct_tbuckets)
+    const uint32_t *tb;      // [ntiles][kTBS] per-tile word-0 bucket table (k_ct_tbuckets)
     const uint64_t *first;   // [WG][ntiles] first key of every tile
     const uint32_t *trad;    // [trad_m + 2] bucket table over first word 0 - base0
     uint32_t trad_m;
@@ -447,7 +447,7 @@ struct CTiles {
 };
 hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *gid,
                         const uint64_t *lsn, const CTiles &ct, uint64_t *key, uint32_t *rank,
-                        uint64_t *first, uint64_t *rel, uint32_t *trad, uint16_t *tb,
+                        uint64_t *first, uint64_t *rel, uint32_t *trad, uint32_t *tb,
                         hipStream_t s);
 size_t ctiles_locate_lds(const CTiles &ct);
 uint32_t ctiles_chunk();
