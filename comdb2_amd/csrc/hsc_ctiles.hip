@@ -119,23 +119,28 @@ __global__ void k_ct_rel(const uint64_t *first0, uint32_t ntiles, uint64_t *rel)
 // walking the tile's 11 levels.
 __global__ __launch_bounds__(256) void k_ct_tbuckets(CTiles ct, const uint64_t *key0, uint32_t *tb)
 {
+    constexpr int PER = kTB / 256;  // buckets per thread
     __shared__ uint32_t cnt[kTB];
+    __shared__ uint32_t scr[8];
     const uint32_t t = blockIdx.x, tid = threadIdx.x;
     const size_t r0 = (size_t)t << kCTLog2;
     const uint32_t tn = min(kCTRows, ct.n - (uint32_t)r0);
     const uint64_t f0 = key0[r0], span = key0[r0 + tn - 1] - f0;
     const int bits = span ? 64 - __clzll(span) : 0;
     const int shift = bits > kTBLog2 ? bits - kTBLog2 : 0;
-    cnt[tid] = 0;
+    for (int k = 0; k < PER; ++k) cnt[tid * PER + k] = 0;
     __syncthreads();
     for (uint32_t i = tid; i < tn; i += 256) atomicAdd(&cnt[(uint32_t)((key0[r0 + i] - f0) >> shift)], 1u);
     __syncthreads();
-    const uint32_t mine = cnt[tid];
-    __syncthreads();  // every count read before the scan reuses cnt as scratch
+    uint32_t mine[PER], sum = 0;
+    for (int k = 0; k < PER; ++k) sum += mine[k] = cnt[tid * PER + k];
     uint32_t tot;
-    const uint32_t pre = block_excl_scan<256>(mine, cnt, tot);
+    uint32_t pre = block_excl_scan<256>(sum, scr, tot);
     uint32_t *o = tb + (size_t)t * kTBS;
-    o[tid] = pre | (pre + mine) << 16;
+    for (int k = 0; k < PER; ++k) {
+        o[tid * PER + k] = pre | (pre + mine[k]) << 16;
+        pre += mine[k];
+    }
     if (tid == 0) o[kTB] = tn | (uint32_t)shift << 16;
 }
 
@@ -532,7 +537,7 @@ hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *g
     default: return hipErrorInvalidValue;
     }
     k_ct_rel<<<(ct.ntiles + 255) / 256, 256, 0, s>>>(first, ct.ntiles, rel);
-    k_ct_tbuckets<<<ct.ntiles, 256, 0, s>>>(ct, key, tb);  // kTB == 256: a thread per bucket
+    k_ct_tbuckets<<<ct.ntiles, 256, 0, s>>>(ct, key, tb);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return narrow_trad_build(rel, ct.ntiles, ct.trad_m, trad, s);

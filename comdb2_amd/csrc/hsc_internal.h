@@ -424,7 +424,7 @@ hipError_t compact_probes(const ProbeView &p, const CompactTables &t, uint64_t *
 // WG-word keys gid || code (WG <= 3) with 32-bit commit times, 2048-row
 // tiles, for dense batches.
 constexpr int kCTLog2 = 11;
-constexpr int kTBLog2 = 8, kTB = 1 << kTBLog2;  // word-0 buckets per tile
+constexpr int kTBLog2 = 10, kTB = 1 << kTBLog2;  // word-0 buckets per tile
 constexpr int kTBS = kTB + 4;                     // u32 per tile: kTB spans, tn | shift, pad
 struct CTiles {
     const uint64_t *key;     // [WG][len] row keys, sorted (padding ~0)
