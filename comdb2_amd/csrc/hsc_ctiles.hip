@@ -369,14 +369,6 @@ __device__ __forceinline__ bool row_eq(const uint64_t *kw, uint32_t r, const uin
     return eq;
 }
 
-// Block-uniform load through the constant address space: a scalar load,
-// counted apart from the vector loads (waiting for it does not drain them).
-template <class T>
-__device__ __forceinline__ T sload(const T *p)
-{
-    return *(const __attribute__((address_space(4))) T *)p;
-}
-
 // 1024 threads, one record and one row pair each: two 58 KiB workgroups per
 // CU hold 32 waves (the CU's limit)
 constexpr int kCJT = 1024;

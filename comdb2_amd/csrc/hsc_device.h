@@ -257,4 +257,12 @@ __device__ __forceinline__ bool any_after32(const uint32_t *rank, const uint32_t
     return r;
 }
 
+// Block-uniform load through the constant address space: a scalar load,
+// counted apart from the vector loads (waiting for it drains none of them).
+template <class T>
+__device__ __forceinline__ T sload(const T *p)
+{
+    return *(const __attribute__((address_space(4))) T *)p;
+}
+
 }  // namespace hsc

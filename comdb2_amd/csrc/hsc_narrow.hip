@@ -1224,32 +1224,35 @@ hipError_t launch_scatter_t(const ProbeView &p, const ProbeWork &work, const Nar
 // rows are requested before anything else is known); blocks past the tiles
 // loop over the further kJoinChunk-record chunks of hot tiles' overflow runs
 // (item_desc).
-__global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowTiles nt,
-                                                         uint32_t n, uint32_t ntiles,
-                                                         uint8_t *verdict)
+// One tile's records (kTile: tile xi's bucket, at most kTileCap records) or
+// overflow item xi of a hot tile.  The records are loaded first (a tile's
+// bucket always has kTileCap slots; the count, a scalar load, masks them
+// later), then the tile's rows, so both round trips overlap (vector loads
+// retire in order: a count read between them would wait for the rows).
+template <bool kTile>
+__device__ __forceinline__ void join_t_item(const ProbeWork &work, const NarrowTiles &nt,
+                                            uint32_t n, uint32_t xi, uint8_t *verdict,
+                                            uint32_t *keys, uint32_t *rank, uint32_t *b16,
+                                            uint32_t *b128)
 {
     constexpr uint32_t T = 1u << kTLog2;
     constexpr int RQ = T / (4 * kJoinThreads);  // row quads per thread (2)
     constexpr int kRec = kJoinChunk / kJoinThreads;
-    __shared__ __attribute__((aligned(16))) uint32_t keys[T];
-    __shared__ __attribute__((aligned(16))) uint32_t rank[T];
-    __shared__ uint32_t b16[T / 16];
-    __shared__ uint32_t b128[T / 128];
-
-    HSC_STAMP(work, 1, 0);
-    // blocks past the tiles take the hot tiles' overflow items in turn
-    const uint32_t nextra = blockIdx.x < ntiles ? 1 : work.item_off[1];
-    const uint32_t stride = gridDim.x > ntiles ? gridDim.x - ntiles : 1;  // >= 1: every loop ends
-    for (uint32_t xi = blockIdx.x < ntiles ? 0 : blockIdx.x - ntiles; xi < nextra; xi += stride) {
-    __syncthreads();  // the previous item's LDS reads are done
     uint32_t tile, r0, r1;
-    if (blockIdx.x < ntiles) {
-        tile = blockIdx.x;
-    } else {  // a further kJoinChunk records of a hot tile's overflow run
-        const uint4 d = work.item_desc[xi];
-        tile = d.x, r0 = d.y, r1 = d.z;
-    }
     u32x4 rk[RQ], rr[RQ], rec[kRec];
+    if constexpr (kTile) {
+        tile = xi;
+        r0 = tile * kTileCap;
+#pragma unroll
+        for (int k = 0; k < kRec; ++k)
+            rec[k] = *(const u32x4 *)(nt.recs + r0 + k * kJoinThreads + threadIdx.x);
+    } else {  // a further kJoinChunk records of a hot tile's overflow run
+        const uint32_t *d = (const uint32_t *)(work.item_desc + xi);
+        tile = sload(d), r0 = sload(d + 1), r1 = sload(d + 2);
+#pragma unroll
+        for (int k = 0; k < kRec; ++k)
+            rec[k] = *(const u32x4 *)(nt.recs + min(r0 + k * kJoinThreads + threadIdx.x, r1 - 1));
+    }
     const size_t ts = (size_t)tile << kTLog2;
 #pragma unroll
     for (int v = 0; v < RQ; ++v) {
@@ -1257,14 +1260,7 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
         rk[v] = *(const u32x4 *)(nt.key32 + row);
         rr[v] = *(const u32x4 *)(nt.rank32 + row);
     }
-    if (blockIdx.x < ntiles) {  // the tile's bucket
-        r0 = tile * kTileCap;
-        r1 = r0 + min(kTileCap, work.counts[tile]);
-    }
-    if (r0 >= r1) continue;  // a tile no range reaches (uniform across the block)
-#pragma unroll
-    for (int k = 0; k < kRec; ++k)
-        rec[k] = *(const u32x4 *)(nt.recs + min(r0 + k * kJoinThreads + threadIdx.x, r1 - 1));
+    if constexpr (kTile) r1 = r0 + min(kTileCap, sload(work.counts + tile));
 #pragma unroll
     for (int v = 0; v < RQ; ++v) {
         const uint32_t quad = threadIdx.x + kJoinThreads * v;
@@ -1301,6 +1297,28 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
         const uint32_t pb = min(jb - T + (kl <= hi), tn);
         if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) verdict[rec[k].w] = 1;
     }
+}
+
+__global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowTiles nt,
+                                                         uint32_t n, uint32_t ntiles,
+                                                         uint8_t *verdict)
+{
+    constexpr uint32_t T = 1u << kTLog2;
+    __shared__ __attribute__((aligned(16))) uint32_t keys[T];
+    __shared__ __attribute__((aligned(16))) uint32_t rank[T];
+    __shared__ uint32_t b16[T / 16];
+    __shared__ uint32_t b128[T / 128];
+
+    HSC_STAMP(work, 1, 0);
+    if (blockIdx.x < ntiles) {
+        join_t_item<true>(work, nt, n, blockIdx.x, verdict, keys, rank, b16, b128);
+    } else {  // blocks past the tiles take the hot tiles' overflow items in turn
+        const uint32_t nextra = work.item_off[1];
+        const uint32_t stride = gridDim.x - ntiles;
+        for (uint32_t xi = blockIdx.x - ntiles; xi < nextra; xi += stride) {
+            __syncthreads();  // the previous item's LDS reads are done
+            join_t_item<false>(work, nt, n, xi, verdict, keys, rank, b16, b128);
+        }
     }
     HSC_STAMP(work, 1, 2);
 }
