@@ -295,7 +295,7 @@ def graph_cpu_baseline(args):
                       f"oracle/scc_oracle.c edges + Tarjan, {dt:.1f} s"}
 
 
-def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0):
+def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0, bitmap=False):
     """Per-kernel event times and each kernel's own algorithmic bytes (what it
     must read and write in this build's layout) for the probe phase.  Events
     add a few microseconds per slot; the rocprofv3 summaries in profiles/ give
@@ -307,18 +307,18 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0):
     if layout == 2:  # narrow tiles: 8-byte window rows, 16-byte records
         own = {
             "k_locate_t": n_r * (4 + 8 + 16 * W) + 16 * n_r + hist,
-            "k_plan_t": hist,
+            "k_plan_t": hist + 2 * T,  # + the verdict bytes from the locate's flags
             "k_scatter_t": n_r * (16 + 4) + recs * 16,
             "k_join_t": 8 * n_keys + 16 * recs,
-            "k_pack_flags": 2 * T + (T + 7) // 8,
+            "k_pack": (T + (T + 7) // 8) if bitmap else 0,  # N > 1: the verdict bitmap
         }
     elif WG:  # compact tiles: raw W-word bounds in, 64-byte probe entries, 4-byte bucket entries
         own = {
             "k_compact_bounds+k_locate_c": n_r * (4 + 8 + 4 + 16 * W) + 72 * n_r + hist,
-            "k_plan_t": hist,
+            "k_plan_t": hist + 2 * T,
             "k_scatter_c": 8 * n_r + 4 * recs,
             "k_join_c": n_keys * (8 * WG + 4) + recs * (4 + 64),
-            "k_pack_flags": 2 * T + (T + 7) // 8,
+            "k_pack": (T + (T + 7) // 8) if bitmap else 0,
         }
     else:  # wide tiles (compact: W = code words): key words + lsn + gid per row
         own = {
@@ -671,7 +671,9 @@ def main():
     # N > 1: each shard's verdict bitmap, all-gathered and OR-ed (hsc_or_bitmaps)
     lbits = [torch.zeros(W64, dtype=torch.int64, device=dev) for _ in range(S)] if world > 1 else None
     gath = [torch.zeros(world * W64, dtype=torch.int64, device=dev) for _ in range(S)] if world > 1 else None
-    structs = [[probe_struct(hsc, b, verdicts[si], bitmaps[si] if world == 1 else lbits[si], T)
+    # N = 1: the verdict bytes are the result, no bitmap (the pack is folded
+    # into the plan kernel); N > 1: each shard's bitmap for the merge
+    structs = [[probe_struct(hsc, b, verdicts[si], None if world == 1 else lbits[si], T)
                 for si in range(S)] for b in batches]
     torch.cuda.synchronize()
 
@@ -768,7 +770,7 @@ def main():
                         axis=0)
         B = int((keys_g * (lhat + 12)).sum() + (rng_g * (2 * lhat + 16)).sum() + (T + 7) // 8)
     WG = v.tile_key_words if v.layout == hsc.LAYOUT_COMPACT and not args.compact_wide else 0
-    kern = kernel_bytes(v.layout, W if WG else v.code_words, n_keys, n_r, T, tm, WG)
+    kern = kernel_bytes(v.layout, W if WG else v.code_words, n_keys, n_r, T, tm, WG, world > 1)
     ms_per_step = elapsed / args.steps * 1e3
     frac = lambda el: B / (el / args.steps) / 1e9 / HBM_PEAK_GBS
     checks = T * args.steps

@@ -1823,17 +1823,23 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     HIPCHK(c, launch_locate_t(c->nv, wn, p, work, ntl, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     if (p.n && wn.ntiles) {
-        HIPCHK(c, launch_plan_t(work, wn.ntiles, c->w_items.as<uint32_t>(), s));
+        // the plan writes the verdict bytes from the locate's flags; the join
+        // and the delta probe then mark the verdict itself
+        HIPCHK(c, launch_plan_t(work, wn.ntiles, c->w_items.as<uint32_t>(), s, flags,
+                                (uint32_t)b->n_txn, b->verdict));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
         HIPCHK(c, launch_scatter_t(p, work, ntl, wn.ntiles, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
-        HIPCHK(c, launch_join_t(work, ntl, wn.n, wn.ntiles, max_items, flags, s));
+        HIPCHK(c, launch_join_t(work, ntl, wn.n, wn.ntiles, max_items, b->verdict, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
-    } else if (tm) {
-        for (int i = 2; i <= 4; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
+        HIPCHK_RC(c, probe_delta(c, b->verdict));
+        HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
+    } else {
+        if (tm)
+            for (int i = 2; i <= 4; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
+        HIPCHK_RC(c, probe_delta(c, flags));
+        HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
     }
-    HIPCHK_RC(c, probe_delta(c, flags));
-    HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
 #ifdef HSC_STAMPS
     HIPCHK_RC(c, stamp_report(c, work, max_items, 5, 3));
@@ -1911,17 +1917,22 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
                               work, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     if (p.n && ct.ntiles) {
-        HIPCHK(c, launch_plan_t(work, ct.ntiles, c->w_items.as<uint32_t>(), s));
+        // pack folded into the plan, as probe_ntiles
+        HIPCHK(c, launch_plan_t(work, ct.ntiles, c->w_items.as<uint32_t>(), s, flags,
+                                (uint32_t)b->n_txn, b->verdict));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
         HIPCHK(c, launch_scatter_c(ct, work, p.n, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
-        HIPCHK(c, launch_join_c(ct, work, max_items, flags, s));
+        HIPCHK(c, launch_join_c(ct, work, max_items, b->verdict, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
-    } else if (tm) {
-        for (int i = 2; i <= 4; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
+        HIPCHK_RC(c, probe_delta(c, b->verdict));
+        HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
+    } else {
+        if (tm)
+            for (int i = 2; i <= 4; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
+        HIPCHK_RC(c, probe_delta(c, flags));
+        HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
     }
-    HIPCHK_RC(c, probe_delta(c, flags));
-    HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
 #ifdef HSC_STAMPS
     HIPCHK_RC(c, stamp_report(c, work, max_items, 2, 7));

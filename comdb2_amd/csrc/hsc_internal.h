@@ -339,7 +339,12 @@ __host__ __device__ inline uint32_t hist_stride(uint32_t G) { return (G + 7) & ~
 __host__ __device__ inline uint32_t xcd_chunk(uint32_t b, uint32_t per) { return (b & 7) * per + (b >> 3); }
 // Column scans of the tile-major histogram into fixed-capacity tile buckets
 // (ctl[0..1]: overflow records / extra join items, zeroed by the locate).
-hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, hipStream_t s);
+// verdict != nullptr: the plan also writes the batch's verdict bytes from the
+// locate's flags (clearing them), so the join and the delta probe mark the
+// verdict directly and no pack pass is needed (pack folded into the plan)
+hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, hipStream_t s,
+                         uint8_t *flags = nullptr, uint32_t n_txn = 0,
+                         uint8_t *verdict = nullptr);
 // Verdict bytes + bitmap from the internal conflict flags; clears the flags.
 hipError_t launch_pack_flags(uint8_t *flags, uint32_t n_txn, uint8_t *verdict, uint64_t *bitmap,
                              hipStream_t s);

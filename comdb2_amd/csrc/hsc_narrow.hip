@@ -1086,11 +1086,20 @@ uint32_t narrow_tiles_dir_lds() { return kDirLds; }
 constexpr int kPlanThreads = 512;
 static_assert(kMaxChunks <= 512, "one 512-entry column pass per wave");
 __global__ __launch_bounds__(kPlanThreads) void k_plan_t(ProbeWork work, uint32_t ntiles,
-                                                         uint32_t *ctl)
+                                                         uint32_t *ctl, uint8_t *flags,
+                                                         uint32_t n_txn, uint8_t *verdict)
 {
     const int lane = threadIdx.x & 63;
     const uint32_t t = blockIdx.x * (kPlanThreads / 64) + (threadIdx.x >> 6);
     const uint32_t hs = hist_stride(work.G);
+    if (verdict) {  // the pack folded in: verdict = the locate's flags, flags cleared
+        const uint32_t stride = gridDim.x * kPlanThreads;
+        for (uint32_t i = blockIdx.x * kPlanThreads + threadIdx.x; i < n_txn; i += stride) {
+            const uint8_t f = flags[i];
+            verdict[i] = f != 0;
+            if (f) flags[i] = 0;
+        }
+    }
     if (t >= ntiles) return;
     u32x4 *col = (u32x4 *)(work.hist + (size_t)t * hs);
     const uint32_t e = 8 * lane;
@@ -1147,11 +1156,13 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_t(ProbeWork work, uint32_
     }
 }
 
-hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, hipStream_t s)
+hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, hipStream_t s,
+                         uint8_t *flags, uint32_t n_txn, uint8_t *verdict)
 {
     if (ntiles == 0) return hipSuccess;
     constexpr uint32_t per = kPlanThreads / 64;
-    k_plan_t<<<(ntiles + per - 1) / per, kPlanThreads, 0, s>>>(work, ntiles, ctl);
+    k_plan_t<<<(ntiles + per - 1) / per, kPlanThreads, 0, s>>>(work, ntiles, ctl, flags, n_txn,
+                                                               verdict);
     return hipGetLastError();
 }
 
