@@ -1778,9 +1778,20 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     const uint32_t extra_items = 2 * (uint32_t)((2 * n1 + kJoinChunk - 1) / kJoinChunk);
     const uint32_t max_items = nt + extra_items;
     HIPCHK(c, c->w_item_desc.ensure(16 * (size_t)extra_items + 16));
-    HIPCHK(c, c->w_tcode.ensure(16 * n1));
-    HIPCHK(c, c->w_tcode2.ensure(16 * n1));
-    HIPCHK(c, c->w_trecs.ensure(16 * ((size_t)nt * kTileCap + 2 * n1)));
+    // chunk-sorted records (default; HSC_NT_SORT=0: probe-order records + the
+    // scatter into tile buckets): each chunk's records in an area of its own,
+    // no scatter pass
+    static const bool sorted = !getenv("HSC_NT_SORT") || atoi(getenv("HSC_NT_SORT")) != 0;
+    work.local_items = sorted;
+    if (sorted) {
+        HIPCHK(c, c->w_tcode2.ensure(2 * (size_t)hist_stride(work.G) * nt));  // cst
+        HIPCHK(c, c->w_trecs.ensure(16 * 2 * (size_t)work.chunk * work.G));
+        work.cst = c->w_tcode2.as<uint16_t>();
+    } else {
+        HIPCHK(c, c->w_tcode.ensure(16 * n1));
+        HIPCHK(c, c->w_tcode2.ensure(16 * n1));
+        HIPCHK(c, c->w_trecs.ensure(16 * ((size_t)nt * kTileCap + 2 * n1)));
+    }
     work.hist = c->w_hist.as<uint32_t>();
     work.counts = c->w_counts.as<uint32_t>();
     work.bucket_off = c->w_bucket.as<uint32_t>();
@@ -1828,7 +1839,7 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
         HIPCHK(c, launch_plan_t(work, wn.ntiles, c->w_items.as<uint32_t>(), s, flags,
                                 (uint32_t)b->n_txn, b->verdict));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
-        HIPCHK(c, launch_scatter_t(p, work, ntl, wn.ntiles, s));
+        if (!sorted) HIPCHK(c, launch_scatter_t(p, work, ntl, wn.ntiles, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
         HIPCHK(c, launch_join_t(work, ntl, wn.n, wn.ntiles, max_items, b->verdict, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));

@@ -146,6 +146,11 @@ struct ProbeWork {
     uint32_t G, chunk;     // probe chunks (one workgroup each in locate/scatter)
     int lds_mode;          // ntiles <= kHistCap: LDS histograms, no global atomics
     uint64_t *stamps;      // diagnostic builds (HSC_STAMPS): [kernel][block][8] s_memtime
+    // chunk-sorted narrow records (no scatter pass): chunk g's records sit in
+    // its own area of 2 * chunk records sorted by tile; cst[t][g] = where tile
+    // t's run starts in it; join items are tile-local record ranges
+    uint16_t *cst;
+    int local_items;
 };
 // Diagnostic phase stamps (HSC_STAMPS builds only): thread 0 of a block
 // records s_memtime at phase boundaries into a buffer of its own (never an

@@ -837,7 +837,7 @@ constexpr int kLocSub = HSC_LOC_SUB;
 #define HSC_LOC_ATTR __attribute__((amdgpu_waves_per_eu(HSC_LOC_WPE, HSC_LOC_WPE)))
 #endif
 static_assert(kLocTP % kLocSub == 0, "whole sub-chunks");
-template <int W, bool kTrad>
+template <int W, bool kTrad, bool kSort>
 __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowView nv, WinView wt,
                                                              ProbeView p, ProbeWork work,
                                                              NarrowTiles nt, uint8_t *verdict)
@@ -863,9 +863,13 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
     const uint32_t c1 = min(p.n, c0 + work.chunk);
     // probe registers: buffer 0 / 1 alternate between sub-chunks (the loop
     // below is unrolled, so every index is a compile-time constant)
-    uint32_t qq[2][K], gg[2][K];
+    uint32_t qq[2][K], gg[2][K], tx[2][K];
     bool valid[2][K];
     uint64_t snap[2][K], xl[2][K][WR], xh[2][K][WR];
+    // kSort: the chunk's records stay in registers until its histogram is
+    // complete, then go to their tile-sorted places in the chunk's area
+    uint4 R0[S][K], R1[S][K];
+    uint32_t RT[S][K];
     auto load = [&](int s, int buf) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -877,6 +881,7 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
             // rows out of the caches between batches
             gg[buf][k] = p.n ? __builtin_nontemporal_load(p.gid + q) : 0;
             snap[buf][k] = p.n ? __builtin_nontemporal_load(p.snap + q) : 0;
+            if constexpr (kSort) tx[buf][k] = p.n ? __builtin_nontemporal_load(p.txn + q) : 0;
 #pragma unroll
             for (int w = 0; w < W; ++w) {
                 xl[buf][k][w] = p.n ? __builtin_nontemporal_load(p.lo + (size_t)w * p.n + q) : 0;
@@ -985,6 +990,10 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             dfr.x[k] = 1, dfr.y[k] = 0;
+            if constexpr (kSort) {
+                R0[s][k].x = R1[s][k].x = kNoTile32;
+                RT[s][k] = tx[cb][k];
+            }
             if (!valid[cb][k]) continue;
             const uint32_t q = qq[cb][k];
             const uint32_t ca = cnt[2 * k], cbt = cnt[2 * k + 1];
@@ -1012,7 +1021,9 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
                 if (use_b && !full_b) {
                     const uint4 rb2 = make_uint4(bt << 12 | atomicAdd(&hist[bt], 1u), 0,
                                                  (uint32_t)hi_b, rs[k]);
-                    if (r0.x == kNoTile32) {
+                    if (kSort) {
+                        r1 = rb2;
+                    } else if (r0.x == kNoTile32) {
                         r0 = rb2;
                     } else {
                         r0.x |= kHasSecond;
@@ -1020,8 +1031,13 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
                     }
                 }
             }
-            if (r0.x & kHasSecond) nt.code2[q] = r1;
-            nt.code[q] = r0;
+            if constexpr (kSort) {
+                R0[s][k] = r0;
+                R1[s][k] = r1;
+            } else {
+                if (r0.x & kHasSecond) nt.code2[q] = r1;
+                nt.code[q] = r0;
+            }
         }
     }
     loc_defer_run<K>(wt, p, dfr, verdict);
@@ -1036,7 +1052,48 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
     // column g of the tile-major histogram (neighbouring chunks of a line are
     // written from the same XCD)
     const uint32_t hs = hist_stride(work.G);
-    for (uint32_t i = threadIdx.x; i < ntiles; i += kLocTThreads) work.hist[(size_t)i * hs + g] = hist[i];
+    if constexpr (!kSort) {
+        for (uint32_t i = threadIdx.x; i < ntiles; i += kLocTThreads)
+            work.hist[(size_t)i * hs + g] = hist[i];
+    } else {
+        // exclusive scan of the chunk's tile counts (thread = a run of
+        // consecutive tiles): the runs' starts in the chunk's record area go
+        // to column g of cst and replace the counts in LDS
+        const uint32_t per = (ntiles + kLocTThreads - 1) / kLocTThreads;
+        const uint32_t i0 = min(ntiles, threadIdx.x * per), i1 = min(ntiles, i0 + per);
+        uint32_t sum = 0;
+        for (uint32_t i = i0; i < i1; ++i) sum += hist[i];
+        uint32_t x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        uint32_t *wtot = (uint32_t *)(lb + L.rbuf);
+        if (lane == 63) wtot[threadIdx.x >> 6] = x;
+        __syncthreads();
+        uint32_t run = x - sum;
+        for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) run += wtot[w];
+        for (uint32_t i = i0; i < i1; ++i) {
+            const uint32_t c = hist[i];
+            work.hist[(size_t)i * hs + g] = c;
+            work.cst[(size_t)i * hs + g] = (uint16_t)run;
+            hist[i] = run;
+            run += c;
+        }
+        __syncthreads();
+        uint4 *area = nt.recs + (size_t)g * 2 * work.chunk;
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint4 a = R0[s][k], b = R1[s][k];
+                if (a.x != kNoTile32)
+                    area[hist[a.x >> 12] + (a.x & 0xFFFu)] = make_uint4(a.y, a.z, a.w, RT[s][k]);
+                if (b.x != kNoTile32)
+                    area[hist[b.x >> 12] + (b.x & 0xFFFu)] = make_uint4(b.y, b.z, b.w, RT[s][k]);
+            }
+    }
     HSC_STAMP(work, 0, 4);
 }
 
@@ -1049,8 +1106,14 @@ hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeV
     const bool tr = nt.trad != nullptr;
     const int w = nv.W == 1 || nv.W == 2 ? nv.W : 0;
 #define HSC_LOCATE(W_, TR_)                                                                        \
-    k_locate_t<W_, TR_><<<8 * ((work.G + 7) / 8), kLocTThreads, lds, s>>>(nv, wt, p, work, nt,   \
-                                                                            verdict)
+    do {                                                                                           \
+        if (work.local_items)                                                                      \
+            k_locate_t<W_, TR_, true><<<8 * ((work.G + 7) / 8), kLocTThreads, lds, s>>>(            \
+                nv, wt, p, work, nt, verdict);                                                     \
+        else                                                                                       \
+            k_locate_t<W_, TR_, false><<<8 * ((work.G + 7) / 8), kLocTThreads, lds, s>>>(           \
+                nv, wt, p, work, nt, verdict);                                                     \
+    } while (0)
     if (w == 1 && tr)
         HSC_LOCATE(1, true);
     else if (w == 1)
@@ -1143,13 +1206,17 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_t(ProbeWork work, uint32_
         const uint32_t nx = (over + kJoinChunk - 1) / kJoinChunk;
         uint32_t base = 0, ib = 0;
         if (lane == 0) {
-            base = atomicAdd(&ctl[0], over);
+            if (!work.local_items) {
+                base = atomicAdd(&ctl[0], over);
+                work.bucket_off[t] = base;
+            }
             ib = atomicAdd(&ctl[1], nx);
-            work.bucket_off[t] = base;
         }
         base = __shfl(base, 0, 64);
         ib = __shfl(ib, 0, 64);
-        const uint32_t o0 = ntiles * kTileCap + base;
+        // chunk-sorted records: items are ranges of the tile's own record
+        // numbers; bucketed records: ranges of the overflow area
+        const uint32_t o0 = work.local_items ? kTileCap : ntiles * kTileCap + base;
         for (uint32_t j = lane; j < nx; j += 64)  // the wave writes the items together
             work.item_desc[ib + j] = make_uint4(t, o0 + j * kJoinChunk,
                                                 o0 + min((j + 1) * kJoinChunk, over), 0);
@@ -1310,7 +1377,102 @@ __device__ __forceinline__ void join_t_item(const ProbeWork &work, const NarrowT
     }
 }
 
-__global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowTiles nt,
+// The join is held to 8 waves per SIMD: at 85-99 SGPRs the hardware admits
+// only 6-7 (measured on config 2: join 34 -> 31.7 us, one stream 71.3 -> 69 us)
+#ifndef HSC_JOIN_WPE
+#define HSC_JOIN_WPE 8
+#endif
+#define HSC_JOIN_ATTR __attribute__((amdgpu_waves_per_eu(HSC_JOIN_WPE, HSC_JOIN_WPE)))
+// Chunk-sorted records (work.local_items): record j of tile t lives in the
+// run of the chunk g whose offset inside the tile (the plan's scan of column
+// t) is the last one <= j, at chunk g's area + cst[t][g] + (j - that offset).
+// The tile's column is staged first (its loads ahead of the rows'), each
+// thread finds its records' chunks by a 9-step search of it in LDS and issues
+// the record loads while the rows are still arriving.
+template <bool kTile>
+__device__ __forceinline__ void join_s_item(const ProbeWork &work, const NarrowTiles &nt,
+                                            uint32_t n, uint32_t xi, uint8_t *verdict,
+                                            uint32_t *keys, uint32_t *rank, uint32_t *b16,
+                                            uint32_t *b128, uint32_t *Es, uint32_t *Cs)
+{
+    constexpr uint32_t T = 1u << kTLog2;
+    constexpr int RQ = T / (4 * kJoinThreads);
+    constexpr int kRec = kJoinChunk / kJoinThreads;
+    static_assert(kMaxChunks <= kJoinThreads, "one column entry per thread");
+    uint32_t tile, j0, j1;
+    if constexpr (kTile) {
+        tile = xi, j0 = 0;
+    } else {
+        const uint32_t *d = (const uint32_t *)(work.item_desc + xi);
+        tile = sload(d), j0 = sload(d + 1), j1 = sload(d + 2);
+    }
+    const uint32_t G = work.G;
+    const size_t col = (size_t)tile * hist_stride(G);
+    uint32_t e = 0, cs = 0;
+    if (threadIdx.x < G) {
+        e = work.hist[col + threadIdx.x];
+        cs = work.cst[col + threadIdx.x];
+    }
+    u32x4 rk[RQ], rr[RQ], rec[kRec];
+    const size_t ts = (size_t)tile << kTLog2;
+#pragma unroll
+    for (int v = 0; v < RQ; ++v) {
+        const size_t row = ts + 4 * (threadIdx.x + kJoinThreads * v);
+        rk[v] = *(const u32x4 *)(nt.key32 + row);
+        rr[v] = *(const u32x4 *)(nt.rank32 + row);
+    }
+    if constexpr (kTile) j1 = min(kTileCap, sload(work.counts + tile));
+    if (threadIdx.x < G) Es[threadIdx.x] = e, Cs[threadIdx.x] = cs;
+    __syncthreads();
+    const size_t area = 2 * (size_t)work.chunk;
+#pragma unroll
+    for (int k = 0; k < kRec; ++k) {
+        const uint32_t j = j0 + k * kJoinThreads + threadIdx.x;
+        uint32_t g = 0;  // Es[0] = 0 <= j
+#pragma unroll
+        for (int b = 8; b >= 0; --b) {
+            const uint32_t c = g + (1u << b);
+            if (c < G && Es[c] <= j) g = c;
+        }
+        rec[k] = j < j1 ? *(const u32x4 *)(nt.recs + g * area + Cs[g] + (j - Es[g]))
+                        : u32x4{0, 0, 0, 0};
+    }
+#pragma unroll
+    for (int v = 0; v < RQ; ++v) {
+        const uint32_t quad = threadIdx.x + kJoinThreads * v;
+        ((u32x4 *)keys)[quad] = rk[v];
+        ((u32x4 *)rank)[quad] = rr[v];
+        uint32_t m = max(max(rr[v].x, rr[v].y), max(rr[v].z, rr[v].w));
+        m = max(m, (uint32_t)__shfl_xor((int)m, 1, 64));
+        m = max(m, (uint32_t)__shfl_xor((int)m, 2, 64));
+        if ((threadIdx.x & 3) == 0) b16[quad >> 2] = m;
+#pragma unroll
+        for (int d = 4; d < 32; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+        if ((threadIdx.x & 31) == 0) b128[quad >> 5] = m;
+    }
+    __syncthreads();
+    const uint32_t tn = min(T, n - (tile << kTLog2));
+#pragma unroll
+    for (int k = 0; k < kRec; ++k) {
+        const uint32_t j = j0 + k * kJoinThreads + threadIdx.x;
+        if (j >= j1) continue;
+        const uint32_t lo = rec[k].x, hi = rec[k].y, rs = rec[k].z;
+        uint32_t ja = 1, jb = 1;
+#pragma unroll
+        for (int d = 0; d < kTLog2; ++d) {
+            const uint32_t ka = keys[ja], kb = keys[jb];
+            ja = 2 * ja + (ka < lo);
+            jb = 2 * jb + (kb <= hi);
+        }
+        const uint32_t kl = keys[0];
+        const uint32_t pa = min(ja - T + (kl < lo), tn);
+        const uint32_t pb = min(jb - T + (kl <= hi), tn);
+        if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) verdict[rec[k].w] = 1;
+    }
+}
+
+template <bool srt>
+__global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_t(ProbeWork work, NarrowTiles nt,
                                                          uint32_t n, uint32_t ntiles,
                                                          uint8_t *verdict)
 {
@@ -1319,16 +1481,23 @@ __global__ __launch_bounds__(kJoinThreads) void k_join_t(ProbeWork work, NarrowT
     __shared__ __attribute__((aligned(16))) uint32_t rank[T];
     __shared__ uint32_t b16[T / 16];
     __shared__ uint32_t b128[T / 128];
+    __shared__ uint32_t Es[kMaxChunks], Cs[kMaxChunks];
 
     HSC_STAMP(work, 1, 0);
     if (blockIdx.x < ntiles) {
-        join_t_item<true>(work, nt, n, blockIdx.x, verdict, keys, rank, b16, b128);
+        if constexpr (srt)
+            join_s_item<true>(work, nt, n, blockIdx.x, verdict, keys, rank, b16, b128, Es, Cs);
+        else
+            join_t_item<true>(work, nt, n, blockIdx.x, verdict, keys, rank, b16, b128);
     } else {  // blocks past the tiles take the hot tiles' overflow items in turn
         const uint32_t nextra = work.item_off[1];
         const uint32_t stride = gridDim.x - ntiles;
         for (uint32_t xi = blockIdx.x - ntiles; xi < nextra; xi += stride) {
             __syncthreads();  // the previous item's LDS reads are done
-            join_t_item<false>(work, nt, n, xi, verdict, keys, rank, b16, b128);
+            if constexpr (srt)
+                join_s_item<false>(work, nt, n, xi, verdict, keys, rank, b16, b128, Es, Cs);
+            else
+                join_t_item<false>(work, nt, n, xi, verdict, keys, rank, b16, b128);
         }
     }
     HSC_STAMP(work, 1, 2);
@@ -1342,7 +1511,10 @@ hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t 
     // (measured: one block per tile beats persistent blocks that prefetch
     // their next tile -- 27.8 vs 32 us on config 2)
     const uint32_t blocks = ntiles + std::min<uint32_t>(max_items - ntiles, 512);
-    k_join_t<<<blocks, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
+    if (work.local_items)
+        k_join_t<true><<<blocks, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
+    else
+        k_join_t<false><<<blocks, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
     return hipGetLastError();
 }
 
