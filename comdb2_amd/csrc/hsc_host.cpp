@@ -220,6 +220,7 @@ struct hsc_ctx {
     uint32_t ncommit = 0;
     uint64_t commit_span[2] = {0, 0};  // oldest / newest distinct commit LSN of the window
     bool rank_lsn32 = false;   // narrow tiles: rows carry lsn - rank_base + 1 (NarrowTiles)
+    bool nt_sorted = true;     // narrow tiles: chunk-sorted records (HSC_NT_SORT=0 at build: scatter)
     uint64_t rank_base = 0;
     DBuf w_tcode, w_tcode2, w_trecs;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
@@ -871,6 +872,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
             // commit span: rank-free rows (lsn - oldest commit + 1) when it fits 32 bits
             const uint64_t *span = c->commit_span;
             c->rank_lsn32 = span[1] - span[0] <= kLsn32MaxSpan && !getenv("HSC_RANK_DIR");
+            c->nt_sorted = !getenv("HSC_NT_SORT") || atoi(getenv("HSC_NT_SORT")) != 0;
             c->rank_base = span[0];
             c->cdir = Dir16{};
             if (!c->rank_lsn32)
@@ -1778,15 +1780,17 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     const uint32_t extra_items = 2 * (uint32_t)((2 * n1 + kJoinChunk - 1) / kJoinChunk);
     const uint32_t max_items = nt + extra_items;
     HIPCHK(c, c->w_item_desc.ensure(16 * (size_t)extra_items + 16));
-    // chunk-sorted records (default; HSC_NT_SORT=0: probe-order records + the
-    // scatter into tile buckets): each chunk's records in an area of its own,
-    // no scatter pass
-    static const bool sorted = !getenv("HSC_NT_SORT") || atoi(getenv("HSC_NT_SORT")) != 0;
+    // chunk-sorted records (default; HSC_NT_SORT=0 at the window build:
+    // probe-order records + the scatter into tile buckets): each chunk's
+    // records in an area of its own, no scatter pass
+    const bool sorted = c->nt_sorted;
     work.local_items = sorted;
     if (sorted) {
         HIPCHK(c, c->w_tcode2.ensure(2 * (size_t)hist_stride(work.G) * nt));  // cst
+        HIPCHK(c, c->w_tcode.ensure(4 * (size_t)work.G * ((nt + 3) & ~3u)));  // chunk-major rows
         HIPCHK(c, c->w_trecs.ensure(16 * 2 * (size_t)work.chunk * work.G));
         work.cst = c->w_tcode2.as<uint16_t>();
+        work.cm = c->w_tcode.as<uint32_t>();
     } else {
         HIPCHK(c, c->w_tcode.ensure(16 * n1));
         HIPCHK(c, c->w_tcode2.ensure(16 * n1));
@@ -1836,8 +1840,9 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     if (p.n && wn.ntiles) {
         // the plan writes the verdict bytes from the locate's flags; the join
         // and the delta probe then mark the verdict itself
-        HIPCHK(c, launch_plan_t(work, wn.ntiles, c->w_items.as<uint32_t>(), s, flags,
-                                (uint32_t)b->n_txn, b->verdict));
+        HIPCHK(c, (sorted ? launch_plan_s : launch_plan_t)(work, wn.ntiles,
+                                                          c->w_items.as<uint32_t>(), s, flags,
+                                                          (uint32_t)b->n_txn, b->verdict));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
         if (!sorted) HIPCHK(c, launch_scatter_t(p, work, ntl, wn.ntiles, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
@@ -1853,7 +1858,7 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     }
     if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
 #ifdef HSC_STAMPS
-    HIPCHK_RC(c, stamp_report(c, work, max_items, 5, 3));
+    HIPCHK_RC(c, stamp_report(c, work, max_items, sorted ? 6 : 5, 4));
 #endif
     return HSC_OK;
 }

@@ -150,6 +150,7 @@ struct ProbeWork {
     // its own area of 2 * chunk records sorted by tile; cst[t][g] = where tile
     // t's run starts in it; join items are tile-local record ranges
     uint16_t *cst;
+    uint32_t *cm;  // [G][round4(ntiles)] chunk-major (run start << 16 | count), the locate's rows
     int local_items;
 };
 // Diagnostic phase stamps (HSC_STAMPS builds only): thread 0 of a block
@@ -350,6 +351,10 @@ __host__ __device__ inline uint32_t xcd_chunk(uint32_t b, uint32_t per) { return
 hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, hipStream_t s,
                          uint8_t *flags = nullptr, uint32_t n_txn = 0,
                          uint8_t *verdict = nullptr);
+// the plan of chunk-sorted narrow records (work.local_items): transposes the
+// locate's chunk-major table into the tile-major offsets and run starts
+hipError_t launch_plan_s(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, hipStream_t s,
+                         uint8_t *flags, uint32_t n_txn, uint8_t *verdict);
 // Verdict bytes + bitmap from the internal conflict flags; clears the flags.
 hipError_t launch_pack_flags(uint8_t *flags, uint32_t n_txn, uint8_t *verdict, uint64_t *bitmap,
                              hipStream_t s);

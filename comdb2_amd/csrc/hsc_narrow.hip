@@ -1057,8 +1057,9 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
             work.hist[(size_t)i * hs + g] = hist[i];
     } else {
         // exclusive scan of the chunk's tile counts (thread = a run of
-        // consecutive tiles): the runs' starts in the chunk's record area go
-        // to column g of cst and replace the counts in LDS
+        // consecutive tiles): row g of the chunk-major table gets (run start
+        // << 16 | count) per tile (contiguous stores; the plan transposes),
+        // the runs' starts replace the counts in LDS
         const uint32_t per = (ntiles + kLocTThreads - 1) / kLocTThreads;
         const uint32_t i0 = min(ntiles, threadIdx.x * per), i1 = min(ntiles, i0 + per);
         uint32_t sum = 0;
@@ -1074,14 +1075,15 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
         __syncthreads();
         uint32_t run = x - sum;
         for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) run += wtot[w];
+        uint32_t *row = work.cm + (size_t)g * ((ntiles + 3) & ~3u);
         for (uint32_t i = i0; i < i1; ++i) {
             const uint32_t c = hist[i];
-            work.hist[(size_t)i * hs + g] = c;
-            work.cst[(size_t)i * hs + g] = (uint16_t)run;
+            row[i] = run << 16 | c;
             hist[i] = run;
             run += c;
         }
         __syncthreads();
+        HSC_STAMP(work, 0, 4);
         uint4 *area = nt.recs + (size_t)g * 2 * work.chunk;
 #pragma unroll
         for (int s = 0; s < S; ++s)
@@ -1094,7 +1096,7 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
                     area[hist[b.x >> 12] + (b.x & 0xFFFu)] = make_uint4(b.y, b.z, b.w, RT[s][k]);
             }
     }
-    HSC_STAMP(work, 0, 4);
+    HSC_STAMP(work, 0, kSort ? 5 : 4);
 }
 
 hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeView &p,
@@ -1229,6 +1231,98 @@ hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, 
     if (ntiles == 0) return hipSuccess;
     constexpr uint32_t per = kPlanThreads / 64;
     k_plan_t<<<(ntiles + per - 1) / per, kPlanThreads, 0, s>>>(work, ntiles, ctl, flags, n_txn,
+                                                               verdict);
+    return hipGetLastError();
+}
+
+// Plan of chunk-sorted records: block = 8 tiles.  The block reads the 8
+// tiles' entries of every chunk row of the locate's chunk-major table (32
+// contiguous bytes per row), transposes them through LDS, and wave w scans
+// tile t0 + w's column as k_plan_t does; it writes the tile-major exclusive
+// offsets (hist) and run starts (cst) the join stages, the tile's count and,
+// for a hot tile, join items over its own record numbers.  The verdict pack
+// is folded in as in k_plan_t.
+__global__ __launch_bounds__(kPlanThreads) void k_plan_s(ProbeWork work, uint32_t ntiles,
+                                                         uint32_t *ctl, uint8_t *flags,
+                                                         uint32_t n_txn, uint8_t *verdict)
+{
+    constexpr int TB = kPlanThreads / 64;  // tiles per block
+    constexpr uint32_t SR = kMaxChunks + 4;
+    __shared__ __attribute__((aligned(16))) uint32_t sh[TB][SR];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t t0 = blockIdx.x * TB, t = t0 + w;
+    const uint32_t G = work.G, hs = hist_stride(G), rs = (ntiles + 3) & ~3u;
+    for (uint32_t g = threadIdx.x; g < G; g += kPlanThreads) {
+        const uint32_t *row = work.cm + (size_t)g * rs + t0;
+        const u32x4 a = *(const u32x4 *)row;
+        const u32x4 b = t0 + 4 < rs ? *(const u32x4 *)(row + 4) : u32x4{0, 0, 0, 0};
+        sh[0][g] = a.x, sh[1][g] = a.y, sh[2][g] = a.z, sh[3][g] = a.w;
+        sh[4][g] = b.x, sh[5][g] = b.y, sh[6][g] = b.z, sh[7][g] = b.w;
+    }
+    if (verdict) {
+        const uint32_t stride = gridDim.x * kPlanThreads;
+        for (uint32_t i = blockIdx.x * kPlanThreads + threadIdx.x; i < n_txn; i += stride) {
+            const uint8_t f = flags[i];
+            verdict[i] = f != 0;
+            if (f) flags[i] = 0;
+        }
+    }
+    __syncthreads();
+    if (t >= ntiles) return;
+    const uint32_t e = 8 * lane;
+    uint32_t v[8], c[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t x = e + k < G ? sh[w][e + k] : 0;
+        v[k] = x & 0xFFFFu;
+        c[k] = x >> 16;
+    }
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sum += v[k];
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    uint32_t run = x - sum;
+    if (e < hs) {
+        u32x4 oa, ob;
+        oa.x = run; run += v[0];
+        oa.y = run; run += v[1];
+        oa.z = run; run += v[2];
+        oa.w = run; run += v[3];
+        ob.x = run; run += v[4];
+        ob.y = run; run += v[5];
+        ob.z = run; run += v[6];
+        ob.w = run;
+        u32x4 *col = (u32x4 *)(work.hist + (size_t)t * hs);
+        col[e / 4] = oa;
+        col[e / 4 + 1] = ob;
+        *(u32x4 *)(work.cst + (size_t)t * hs + e) =
+            u32x4{c[0] | c[1] << 16, c[2] | c[3] << 16, c[4] | c[5] << 16, c[6] | c[7] << 16};
+    }
+    const uint32_t total = __shfl(x, 63, 64);
+    if (lane == 0) work.counts[t] = total;
+    if (total > kTileCap) {  // hot tile: join items over its record numbers past kTileCap
+        const uint32_t over = total - kTileCap;
+        const uint32_t nx = (over + kJoinChunk - 1) / kJoinChunk;
+        uint32_t ib = 0;
+        if (lane == 0) ib = atomicAdd(&ctl[1], nx);
+        ib = __shfl(ib, 0, 64);
+        for (uint32_t j = lane; j < nx; j += 64)
+            work.item_desc[ib + j] = make_uint4(t, kTileCap + j * kJoinChunk,
+                                                kTileCap + min((j + 1) * kJoinChunk, over), 0);
+    }
+}
+
+hipError_t launch_plan_s(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, hipStream_t s,
+                         uint8_t *flags, uint32_t n_txn, uint8_t *verdict)
+{
+    if (ntiles == 0) return hipSuccess;
+    constexpr uint32_t per = kPlanThreads / 64;
+    k_plan_s<<<(ntiles + per - 1) / per, kPlanThreads, 0, s>>>(work, ntiles, ctl, flags, n_txn,
                                                                verdict);
     return hipGetLastError();
 }
@@ -1424,6 +1518,7 @@ __device__ __forceinline__ void join_s_item(const ProbeWork &work, const NarrowT
     if constexpr (kTile) j1 = min(kTileCap, sload(work.counts + tile));
     if (threadIdx.x < G) Es[threadIdx.x] = e, Cs[threadIdx.x] = cs;
     __syncthreads();
+    HSC_STAMP(work, 1, 1);
     const size_t area = 2 * (size_t)work.chunk;
 #pragma unroll
     for (int k = 0; k < kRec; ++k) {
@@ -1451,6 +1546,7 @@ __device__ __forceinline__ void join_s_item(const ProbeWork &work, const NarrowT
         if ((threadIdx.x & 31) == 0) b128[quad >> 5] = m;
     }
     __syncthreads();
+    HSC_STAMP(work, 1, 2);
     const uint32_t tn = min(T, n - (tile << kTLog2));
 #pragma unroll
     for (int k = 0; k < kRec; ++k) {
@@ -1500,7 +1596,7 @@ __global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_t(ProbeWork
                 join_t_item<false>(work, nt, n, xi, verdict, keys, rank, b16, b128);
         }
     }
-    HSC_STAMP(work, 1, 2);
+    HSC_STAMP(work, 1, 3);
 }
 
 hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t n,

@@ -32,10 +32,12 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
     # carry lsn - oldest commit + 1 when the window spans < 2^32 of log, the
     # commit rank (directory search of snapshots) with HSC_RANK_DIR set; the
     # bucket table in linear or log mode (HSC_TRAD_MODE; by default the build
-    # picks the mode whose fullest bucket is smaller)
+    # picks the mode whose fullest bucket is smaller); records chunk-sorted
+    # (default) or scattered into tile buckets (HSC_NT_SORT=0)
     runs = [(LAYOUT_NARROW_DIRECT, None), (LAYOUT_NARROW_TILES, None),
             (LAYOUT_NARROW_TILES, "HSC_TILE_DIR"), (LAYOUT_NARROW_TILES, "HSC_RANK_DIR"),
             (LAYOUT_NARROW_TILES, "HSC_TRAD_MODE=log"), (LAYOUT_NARROW_TILES, "HSC_TRAD_MODE=lin"),
+            (LAYOUT_NARROW_TILES, "HSC_NT_SORT=0"),
             (LAYOUT_NARROW_CODES, None), (LAYOUT_WIDE, None)]
     try:
         for layout, knob in runs:
@@ -51,7 +53,7 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
             np.testing.assert_array_equal(got[layout] != 0, want != 0,
                                           err_msg=f"layout {layout} knob {knob}")
     finally:
-        for knob in ("HSC_TILE_DIR", "HSC_RANK_DIR", "HSC_TRAD_MODE"):
+        for knob in ("HSC_TILE_DIR", "HSC_RANK_DIR", "HSC_TRAD_MODE", "HSC_NT_SORT"):
             os.environ.pop(knob, None)
         v.set_layout(LAYOUT_AUTO)
     return want
