@@ -827,8 +827,8 @@ __device__ __forceinline__ void loc_defer_run(const WinView &wt, const ProbeView
 // kLocSub probes per thread: the loads of sub-chunk s + 1 are in flight while
 // sub-chunk s is located (codes, snapshot ranks, end tiles, records), so the
 // chunk's HBM reads overlap its LDS / VALU work instead of preceding it.
-#ifndef HSC_LOC_SUB
-#define HSC_LOC_SUB 2
+#ifndef HSC_LOC_SUB  // (r02, chunk-sorted records: 1 probe per sub-chunk 2.10 G vs 2 probes 2.00 G)
+#define HSC_LOC_SUB 1
 #endif
 constexpr int kLocSub = HSC_LOC_SUB;
 #ifndef HSC_LOC_WPE
