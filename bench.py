@@ -302,15 +302,36 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0, bitmap=False):
     the undisturbed durations."""
     recs = tm["records"]
     tiles = tm["tiles"]
-    chunks = (n_r + 4095) // 4096
+    chunk = 2048 if WG else 4096  # probes per locate workgroup
+    chunks = (n_r + chunk - 1) // chunk
     hist = 4 * tiles * ((chunks + 7) // 8 * 8)
-    if layout == 2:  # narrow tiles: 8-byte window rows, 16-byte records
+    if layout == 2 and os.environ.get("HSC_NT_SORT", "1") != "0":
+        # narrow tiles, chunk-sorted records: the locate writes them in place
+        # (+ its chunk's row of run starts / counts), no scatter pass
+        own = {
+            "k_locate_t": n_r * (4 + 8 + 4 + 16 * W) + 16 * recs + hist,
+            "k_plan_s": hist + 6 * tiles * ((chunks + 7) // 8 * 8) + 2 * T,
+            None: 0,
+            "k_join_t": 8 * n_keys + 16 * recs + 6 * tiles * ((chunks + 7) // 8 * 8),
+            "k_pack": (T + (T + 7) // 8) if bitmap else 0,
+        }
+    elif layout == 2:  # narrow tiles: 8-byte window rows, 16-byte records
         own = {
             "k_locate_t": n_r * (4 + 8 + 16 * W) + 16 * n_r + hist,
             "k_plan_t": hist + 2 * T,  # + the verdict bytes from the locate's flags
             "k_scatter_t": n_r * (16 + 4) + recs * 16,
             "k_join_t": 8 * n_keys + 16 * recs,
             "k_pack": (T + (T + 7) // 8) if bitmap else 0,  # N > 1: the verdict bitmap
+        }
+    elif WG and os.environ.get("HSC_CT_SORT", "1") != "0":
+        # compact tiles, chunk-sorted 64-byte records written by the locate
+        cols = 6 * tiles * ((chunks + 7) // 8 * 8)
+        own = {
+            "k_compact_bounds+k_locate_c": n_r * (4 + 8 + 4 + 16 * W) + 64 * recs + hist,
+            "k_plan_s": hist + cols + 2 * T,
+            None: 0,
+            "k_join_c": n_keys * (8 * WG + 4) + 64 * recs + cols,
+            "k_pack": (T + (T + 7) // 8) if bitmap else 0,
         }
     elif WG:  # compact tiles: raw W-word bounds in, 64-byte probe entries, 4-byte bucket entries
         own = {
@@ -331,6 +352,8 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0, bitmap=False):
     ms = [tm["locate_ms"], tm["plan_ms"], tm["scatter_ms"], tm["join_ms"], tm["pack_ms"]]
     out = {}
     for (name, b), t in zip(own.items(), ms):
+        if name is None:  # no such pass in this layout
+            continue
         out[name] = {"event_ms": t, "bytes": int(b),
                      "GBps": b / (t * 1e-3) / 1e9 if t > 0 else None}
     return out
@@ -413,7 +436,7 @@ def box_cpus():
                 cpu=cpu_model())
 
 
-PROBE_KERNELS = ("k_locate_t", "k_plan_t", "k_scatter_t", "k_join_t", "k_pack_flags",  # narrow
+PROBE_KERNELS = ("k_locate_t", "k_plan_t", "k_plan_s", "k_scatter_t", "k_join_t", "k_pack_flags",  # narrow
                  "k_locate_c", "k_scatter_c", "k_join_c",  # compact tiles
                  "k_compact_bounds", "k_locate", "k_colscan", "k_plan", "k_scatter", "k_join",
                  "k_pack", "k_probe_delta")  # compact / wide, delta run

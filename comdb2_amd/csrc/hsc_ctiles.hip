@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void k_ct_tbuckets(CTiles ct, const uint64_t *
 
 // ---- locate ----
 struct CLocLds {
-    uint32_t first, trad, hist, bytes;
+    uint32_t first, trad, hist, wtot, bytes;
 };
 __host__ __device__ inline CLocLds cloc_lds(const CTiles &ct)
 {
@@ -158,6 +158,8 @@ __host__ __device__ inline CLocLds cloc_lds(const CTiles &ct)
     o += 2 * ((ct.trad_m + 1 + 7) & ~7u);
     L.hist = o;
     o += 4 * ((ct.ntiles + 3) & ~3u);
+    L.wtot = o;  // the tail's scan: one total per wave
+    o += 4 * (kCLocThreads / 64);
     L.bytes = o;
     return L;
 }
@@ -191,7 +193,13 @@ __device__ __forceinline__ uint32_t ct_count(const uint64_t *lf, uint32_t nt, co
     return l;
 }
 
-template <int WG>
+// kSort (work.local_items): no probe entries, slots or scatter -- the chunk's
+// records stay in registers until its tile histogram is complete, then each
+// goes whole (64 bytes: {key x, r(S) | read set | kind << 62} + {hi key} for a
+// full record; x = lo, or hi for a tail record) to its tile-sorted place in
+// the chunk's own area, and row g of the chunk-major table gets (run start
+// << 16 | count) per tile for k_plan_s (as the narrow locate)
+template <int WG, bool kSort>
 __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt, ProbeView p,
                                                            const uint64_t *clo,
                                                            const uint64_t *chi, ProbeWork work,
@@ -233,9 +241,12 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
     }
     const int shift = (int)ct.trad[ct.trad_m + 1];
     __syncthreads();
+    uint64_t KA[kCLocP][WG], KB[kCLocP][WG], RT[kCLocP];
+    uint2 SL[kCLocP];
 #pragma unroll
     for (int k = 0; k < kCLocP; ++k) {
         const uint32_t q = c0 + threadIdx.x + kCLocThreads * k;
+        SL[k] = make_uint2(kNoSlot, kNoSlot);
         if (q >= c1) continue;
         uint64_t a_[WG], b_[WG];
         compose<WG>(gg[k], ct.gb, lo[k], a_);
@@ -261,6 +272,13 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
                 }
                 // entries {lo[0..2], r(S) | read set << 32}, {hi[0..2], ...} (words past WG zero)
                 const uint64_t rt = (uint64_t)lsn32_rank(snap[k], ct.rank_base) | (uint64_t)txn << 32;
+                if constexpr (kSort) {
+#pragma unroll
+                    for (int j = 0; j < WG; ++j) KA[k][j] = a_[j], KB[k][j] = b_[j];
+                    RT[k] = rt;
+                    SL[k] = sl;
+                    continue;
+                }
                 uint64_t f[8] = {0, 0, 0, rt, 0, 0, 0, rt};
 #pragma unroll
                 for (int j = 0; j < WG; ++j) f[j] = a_[j], f[4 + j] = b_[j];
@@ -274,7 +292,7 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
                 }
             }
         }
-        ct.slot[q] = sl;
+        if constexpr (!kSort) ct.slot[q] = sl;
     }
     // table locks: any write to a locked table after the snapshot
     for (uint32_t q = g * kCLocThreads + threadIdx.x; q < p.n_lock; q += work.G * kCLocThreads) {
@@ -282,8 +300,60 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
         if (t < wt.ntables && wt.table_max[t] > p.lock_snap[q]) flags[p.lock_txn[q]] = 1;
     }
     __syncthreads();
-    const uint32_t hs = hist_stride(work.G);
-    for (uint32_t i = threadIdx.x; i < nt; i += kCLocThreads) work.hist[(size_t)i * hs + g] = hist[i];
+    if constexpr (!kSort) {
+        const uint32_t hs = hist_stride(work.G);
+        for (uint32_t i = threadIdx.x; i < nt; i += kCLocThreads) work.hist[(size_t)i * hs + g] = hist[i];
+    } else {
+        const int lane = threadIdx.x & 63;
+        uint32_t *wtot = (uint32_t *)(lb + L.wtot);
+        const uint32_t per = (nt + kCLocThreads - 1) / kCLocThreads;
+        const uint32_t i0 = min(nt, threadIdx.x * per), i1 = min(nt, i0 + per);
+        uint32_t sum = 0;
+        for (uint32_t i = i0; i < i1; ++i) sum += hist[i];
+        uint32_t x = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) wtot[threadIdx.x >> 6] = x;
+        __syncthreads();
+        uint32_t run = x - sum;
+        for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) run += wtot[w];
+        uint32_t *row = work.cm + (size_t)g * ((nt + 3) & ~3u);
+        for (uint32_t i = i0; i < i1; ++i) {
+            const uint32_t c = hist[i];
+            row[i] = run << 16 | c;
+            hist[i] = run;
+            run += c;
+        }
+        __syncthreads();
+        u64x2 *area = (u64x2 *)ct.recs + (size_t)g * 2 * work.chunk * 4;
+#pragma unroll
+        for (int k = 0; k < kCLocP; ++k) {
+            const uint2 sl = SL[k];
+            if (sl.x == kNoSlot) continue;
+            uint64_t a[3] = {0, 0, 0}, b[3] = {0, 0, 0};
+#pragma unroll
+            for (int j = 0; j < WG; ++j) a[j] = KA[k][j], b[j] = KB[k][j];
+            const bool two = (sl.x & kSecondRec) != 0;
+            const uint32_t ta = (sl.x & ~(kSecondRec | kPointRec)) >> 12;
+            const uint64_t kind = two ? kCHead : (sl.x & kPointRec) ? kCPoint : kCFull;
+            u64x2 *r = area + 4 * (size_t)(hist[ta] + (sl.x & 0xFFFu));
+            r[0] = u64x2{a[0], a[1]};
+            r[1] = u64x2{a[2], RT[k] | kind << 62};
+            if (kind == kCFull) {
+                r[2] = u64x2{b[0], b[1]};
+                r[3] = u64x2{b[2], 0};
+            }
+            if (two) {
+                const uint32_t tb = sl.y >> 12;
+                u64x2 *r2 = area + 4 * (size_t)(hist[tb] + (sl.y & 0xFFFu));
+                r2[0] = u64x2{b[0], b[1]};
+                r2[1] = u64x2{b[2], RT[k] | (uint64_t)kCTail << 62};
+            }
+        }
+    }
 }
 
 // ---- scatter: 4-byte bucket entries ----
@@ -487,7 +557,76 @@ __device__ __forceinline__ void join_item(const ProbeWork &work, const CTiles &c
 #endif
 }
 
-template <int WG>
+// Chunk-sorted records (work.local_items): record j of the tile is in the run
+// of the chunk whose offset inside the tile (k_plan_s's scan of the tile's
+// column) is the last one <= j.  The column is loaded first, staged, each
+// thread finds its record's chunk by a 9-step LDS search and loads the whole
+// 64-byte record (no bucket entry, no gather) while the rows are in flight.
+template <int WG, bool kTile>
+__device__ __forceinline__ void join_item_s(const ProbeWork &work, const CTiles &ct, uint8_t *flags,
+                                            uint32_t xi, uint64_t *kw, uint32_t *rank,
+                                            uint32_t *b16, uint32_t *b128, uint32_t *B,
+                                            uint32_t *Es, uint16_t *Cs)
+{
+    constexpr uint32_t T = kCTRows;
+    const uint32_t tid = threadIdx.x;
+    uint32_t tile, j0, j1;
+    if constexpr (kTile) {
+        tile = xi, j0 = 0;
+    } else {
+        const uint32_t *d = (const uint32_t *)(work.item_desc + xi);
+        tile = sload(d), j0 = sload(d + 1), j1 = sload(d + 2);
+    }
+    const uint32_t G = work.G;
+    const size_t col = (size_t)tile * hist_stride(G);
+    uint32_t e = 0, cs = 0;
+    if (tid < G) e = work.hist[col + tid], cs = work.cst[col + tid];
+    const size_t row = ((size_t)tile << kCTLog2) + 2 * tid;
+    u64x2 kv[WG];
+#pragma unroll
+    for (int w = 0; w < WG; ++w) kv[w] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row);
+    const u32x2 rr = *(const u32x2 *)(ct.rank + row);
+    u32x2 bt = {0, 0};
+    if (tid < kTBS / 2) bt = *(const u32x2 *)(ct.tb + (size_t)tile * kTBS + 2 * tid);
+    if constexpr (kTile) j1 = min(kTileCap, sload(work.counts + tile));
+    if (tid < G) Es[tid] = e, Cs[tid] = (uint16_t)cs;
+    __syncthreads();
+    const uint32_t j = j0 + tid;
+    const bool live = j < j1;
+    u64x2 A0 = {}, A1 = {}, B0 = {}, B1 = {};
+    if (live) {
+        uint32_t g = 0;  // Es[0] = 0 <= j
+#pragma unroll
+        for (int b = 8; b >= 0; --b) {
+            const uint32_t c = g + (1u << b);
+            if (c < G && Es[c] <= j) g = c;
+        }
+        const u64x2 *r = (const u64x2 *)ct.recs +
+                         4 * ((size_t)g * 2 * work.chunk + Cs[g] + (j - Es[g]));
+        A0 = r[0], A1 = r[1], B0 = r[2], B1 = r[3];
+    }
+#pragma unroll
+    for (int w = 0; w < WG; ++w) *(u64x2 *)(kw + (size_t)w * T + 2 * tid) = kv[w];
+    *(u32x2 *)(rank + 2 * tid) = rr;
+    if (tid < kTBS / 2) *(u32x2 *)(B + 2 * tid) = bt;
+    uint32_t m = max(rr.x, rr.y);
+#pragma unroll
+    for (int d = 1; d < 8; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+    if ((tid & 7) == 0) b16[tid >> 3] = m;
+#pragma unroll
+    for (int d = 8; d < 64; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+    if ((tid & 63) == 0) b128[tid >> 6] = m;
+    __syncthreads();
+    if (!live) return;
+    const uint32_t kind = (uint32_t)(A1.y >> 62);
+    const uint64_t rt = A1.y & ((1ull << 62) - 1);
+    u64x2 pl[2] = {A0, u64x2{A1.x, rt}}, ph0 = B0;
+    uint64_t ph1 = B1.x;
+    if (kind == kCTail) ph0 = A0, ph1 = A1.x;  // a tail record carries hi in its first half
+    join_search<WG>(work, ct, flags, kw, rank, b16, b128, B, kind, pl, ph0, ph1);
+}
+
+template <int WG, bool kSort>
 __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_join_c(ProbeWork work, CTiles ct, uint8_t *flags)
 {
     constexpr uint32_t T = kCTRows;
@@ -499,17 +638,25 @@ __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     uint32_t *b16 = rank + T;                            // [T / 16]
     uint32_t *b128 = b16 + T / 16;                       // [T / 128]
     uint32_t *B = b128 + T / 128;                        // [kTBS] the tile's bucket table
+    uint32_t *Es = B + kTBS;                              // kSort: the tile's column
+    uint16_t *Cs = (uint16_t *)(Es + kMaxChunks);         // (run starts < 2 * kCChunk)
     // the first xb blocks take the hot tiles' overflow items in turn (dispatched
     // first: they are the fullest), then one block per tile
     const uint32_t xb = gridDim.x - ct.ntiles;
     if (blockIdx.x >= xb) {
-        join_item<WG, true>(work, ct, flags, blockIdx.x - xb, kw, rank, b16, b128, B);
+        if constexpr (kSort)
+            join_item_s<WG, true>(work, ct, flags, blockIdx.x - xb, kw, rank, b16, b128, B, Es, Cs);
+        else
+            join_item<WG, true>(work, ct, flags, blockIdx.x - xb, kw, rank, b16, b128, B);
         return;
     }
     const uint32_t nextra = work.item_off[1];
     for (uint32_t xi = blockIdx.x; xi < nextra; xi += xb) {
         __syncthreads();  // the previous item's LDS reads are done
-        join_item<WG, false>(work, ct, flags, xi, kw, rank, b16, b128, B);
+        if constexpr (kSort)
+            join_item_s<WG, false>(work, ct, flags, xi, kw, rank, b16, b128, B, Es, Cs);
+        else
+            join_item<WG, false>(work, ct, flags, xi, kw, rank, b16, b128, B);
     }
 }
 
@@ -545,12 +692,21 @@ hipError_t launch_locate_c(const CTiles &ct, const WinView &wt, const ProbeView 
     if (p.n == 0 && p.n_lock == 0) return hipSuccess;
     const size_t lds = cloc_lds(ct).bytes;
     const uint32_t blocks = 8 * ((work.G + 7) / 8);
+#define HSC_LOC_C(WG_)                                                                              \
+    do {                                                                                            \
+        if (work.local_items)                                                                       \
+            k_locate_c<WG_, true><<<blocks, kCLocThreads, lds, s>>>(ct, wt, p, clo, chi, work, flags); \
+        else                                                                                        \
+            k_locate_c<WG_, false><<<blocks, kCLocThreads, lds, s>>>(ct, wt, p, clo, chi, work,      \
+                                                                     flags);                        \
+    } while (0)
     switch (ct.WG) {
-    case 1: k_locate_c<1><<<blocks, kCLocThreads, lds, s>>>(ct, wt, p, clo, chi, work, flags); break;
-    case 2: k_locate_c<2><<<blocks, kCLocThreads, lds, s>>>(ct, wt, p, clo, chi, work, flags); break;
-    case 3: k_locate_c<3><<<blocks, kCLocThreads, lds, s>>>(ct, wt, p, clo, chi, work, flags); break;
+    case 1: HSC_LOC_C(1); break;
+    case 2: HSC_LOC_C(2); break;
+    case 3: HSC_LOC_C(3); break;
     default: return hipErrorInvalidValue;
     }
+#undef HSC_LOC_C
     return hipGetLastError();
 }
 
@@ -567,14 +723,23 @@ hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_i
     if (max_items == 0 || ct.n == 0 || ct.ntiles == 0) return hipSuccess;
     const uint32_t extra = max_items - ct.ntiles;
     const uint32_t blocks = ct.ntiles + (extra < 512 ? extra : 512);
+    const bool srt = work.local_items != 0;
     const size_t lds = 8 * (size_t)ct.WG * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
-                       4 * (kCTRows / 128) + 4 * kTBS;
+                       4 * (kCTRows / 128) + 4 * kTBS + (srt ? 6 * (size_t)kMaxChunks : 0);
+#define HSC_JOIN_C(WG_)                                                                   \
+    do {                                                                                  \
+        if (srt)                                                                          \
+            k_join_c<WG_, true><<<blocks, kCJT, lds, s>>>(work, ct, flags);               \
+        else                                                                              \
+            k_join_c<WG_, false><<<blocks, kCJT, lds, s>>>(work, ct, flags);              \
+    } while (0)
     switch (ct.WG) {
-    case 1: k_join_c<1><<<blocks, kCJT, lds, s>>>(work, ct, flags); break;
-    case 2: k_join_c<2><<<blocks, kCJT, lds, s>>>(work, ct, flags); break;
-    case 3: k_join_c<3><<<blocks, kCJT, lds, s>>>(work, ct, flags); break;
+    case 1: HSC_JOIN_C(1); break;
+    case 2: HSC_JOIN_C(2); break;
+    case 3: HSC_JOIN_C(3); break;
     default: return hipErrorInvalidValue;
     }
+#undef HSC_JOIN_C
     return hipGetLastError();
 }
 

@@ -221,6 +221,7 @@ struct hsc_ctx {
     uint64_t commit_span[2] = {0, 0};  // oldest / newest distinct commit LSN of the window
     bool rank_lsn32 = false;   // narrow tiles: rows carry lsn - rank_base + 1 (NarrowTiles)
     bool nt_sorted = true;     // narrow tiles: chunk-sorted records (HSC_NT_SORT=0 at build: scatter)
+    bool ct_sorted = true;     // compact tiles: chunk-sorted records (HSC_CT_SORT=0 at build: scatter)
     uint64_t rank_base = 0;
     DBuf w_tcode, w_tcode2, w_trecs;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
@@ -608,6 +609,7 @@ static int build_ctiles(hsc_ctx *c)
         return HSC_OK;
     CTiles &ct = c->ctv;
     ct = CTiles{};
+    c->ct_sorted = !getenv("HSC_CT_SORT") || atoi(getenv("HSC_CT_SORT")) != 0;
     ct.n = (uint32_t)c->n;
     ct.ntiles = v.ntiles;
     ct.len = (size_t)v.ntiles << kCTLog2;
@@ -1889,9 +1891,22 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
     const uint32_t extra_items = 2 * (uint32_t)((2 * n1 + kJoinChunk - 1) / kJoinChunk);
     const uint32_t max_items = nt + extra_items;
     HIPCHK(c, c->w_item_desc.ensure(16 * (size_t)extra_items + 16));
-    HIPCHK(c, c->w_tcode.ensure(64 * n1));   // probe entries
-    HIPCHK(c, c->w_tcode2.ensure(8 * n1));   // slots
-    HIPCHK(c, c->w_trecs.ensure(4 * ((size_t)nt * kTileCap + 2 * n1)));
+    // chunk-sorted 64-byte records (default; the read set number shares its
+    // word with the record kind, so batches of >= 2^30 read sets and
+    // HSC_CT_SORT=0 windows take probe entries + the scatter)
+    const bool sorted = c->ct_sorted && b->n_txn < (1u << 30);
+    work.local_items = sorted;
+    if (sorted) {
+        HIPCHK(c, c->w_tcode.ensure(4 * (size_t)work.G * ((nt + 3) & ~3u)));  // chunk-major rows
+        HIPCHK(c, c->w_tcode2.ensure(2 * (size_t)hist_stride(work.G) * nt));  // run starts
+        HIPCHK(c, c->w_trecs.ensure(64 * 2 * (size_t)work.chunk * work.G));
+        work.cm = c->w_tcode.as<uint32_t>();
+        work.cst = c->w_tcode2.as<uint16_t>();
+    } else {
+        HIPCHK(c, c->w_tcode.ensure(64 * n1));  // probe entries
+        HIPCHK(c, c->w_tcode2.ensure(8 * n1));  // slots
+        HIPCHK(c, c->w_trecs.ensure(4 * ((size_t)nt * kTileCap + 2 * n1)));
+    }
     work.hist = c->w_hist.as<uint32_t>();
     work.counts = c->w_counts.as<uint32_t>();
     work.bucket_off = c->w_bucket.as<uint32_t>();
@@ -1934,10 +1949,11 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     if (p.n && ct.ntiles) {
         // pack folded into the plan, as probe_ntiles
-        HIPCHK(c, launch_plan_t(work, ct.ntiles, c->w_items.as<uint32_t>(), s, flags,
-                                (uint32_t)b->n_txn, b->verdict));
+        HIPCHK(c, (sorted ? launch_plan_s : launch_plan_t)(work, ct.ntiles,
+                                                          c->w_items.as<uint32_t>(), s, flags,
+                                                          (uint32_t)b->n_txn, b->verdict));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
-        HIPCHK(c, launch_scatter_c(ct, work, p.n, s));
+        if (!sorted) HIPCHK(c, launch_scatter_c(ct, work, p.n, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
         HIPCHK(c, launch_join_c(ct, work, max_items, b->verdict, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));

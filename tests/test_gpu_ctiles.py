@@ -5,6 +5,8 @@ entries, full-key Eytzinger joins.  Verdicts must equal the oracle's and the
 wide compact pipeline's (LAYOUT_COMPACT_WIDE) on the same windows: config 3,
 short composite keys with ties at every word, hot tiles that overflow their
 bucket, sparse batches and appended rows."""
+import os
+
 import numpy as np
 import pytest
 
@@ -91,12 +93,22 @@ def _short_case(seed, n_commits=3000, n_txn=900, lens=(9, 17, 23), n_tabs=4, hot
 
 
 def _both(v, log, rs):
-    """Verdicts through the compact tiles and through the wide compact pipeline."""
+    """Verdicts through the compact tiles and through the wide compact pipeline;
+    the compact tiles' scatter path (HSC_CT_SORT=0 at the build: probe
+    entries + bucket entries instead of chunk-sorted records) must agree."""
+    os.environ["HSC_CT_SORT"] = "0"
+    try:
+        v.set_layout(LAYOUT_AUTO)
+        v.ingest_log(log)
+    finally:
+        os.environ.pop("HSC_CT_SORT", None)
+    scat = v.check_readsets(rs) != 0
     v.set_layout(LAYOUT_AUTO)
     v.ingest_log(log)
     assert v.layout == LAYOUT_COMPACT
     assert 1 <= v.tile_key_words <= 3
     got = v.check_readsets(rs) != 0
+    np.testing.assert_array_equal(scat, got, err_msg="chunk-sorted vs scattered records")
     v.set_layout(LAYOUT_COMPACT_WIDE)
     ref = v.check_readsets(rs) != 0
     v.set_layout(LAYOUT_AUTO)
