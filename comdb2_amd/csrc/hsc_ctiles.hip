@@ -626,6 +626,17 @@ __device__ __forceinline__ void join_item_s(const ProbeWork &work, const CTiles 
     join_search<WG>(work, ct, flags, kw, rank, b16, b128, B, kind, pl, ph0, ph1);
 }
 
+// XCD-contiguous tiles (as the narrow join): measured neutral on config 3
+// (1.100 vs 1.108 G checks/s, r02c), so off by default
+#ifndef HSC_CJOIN_XCD
+#define HSC_CJOIN_XCD 0
+#endif
+constexpr bool kCJoinXcd = HSC_CJOIN_XCD != 0;
+__host__ __device__ inline uint32_t ct_tile_blocks(bool srt, uint32_t ntiles)
+{
+    return srt && kCJoinXcd ? 8 * ((ntiles + 7) / 8) : ntiles;
+}
+
 template <int WG, bool kSort>
 __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_join_c(ProbeWork work, CTiles ct, uint8_t *flags)
 {
@@ -642,11 +653,15 @@ __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     uint16_t *Cs = (uint16_t *)(Es + kMaxChunks);         // (run starts < 2 * kCChunk)
     // the first xb blocks take the hot tiles' overflow items in turn (dispatched
     // first: they are the fullest), then one block per tile
-    const uint32_t xb = gridDim.x - ct.ntiles;
+    const uint32_t xb = gridDim.x - ct_tile_blocks(kSort, ct.ntiles);
     if (blockIdx.x >= xb) {
-        if constexpr (kSort)
-            join_item_s<WG, true>(work, ct, flags, blockIdx.x - xb, kw, rank, b16, b128, B, Es, Cs);
-        else
+        if constexpr (kSort) {
+            // neighbouring tiles on one XCD (they share lines of the chunk areas)
+            const uint32_t b = blockIdx.x - xb, tb = gridDim.x - xb;
+            const uint32_t tile = kCJoinXcd ? xcd_chunk(b, tb / 8) : b;
+            if (tile < ct.ntiles)
+                join_item_s<WG, true>(work, ct, flags, tile, kw, rank, b16, b128, B, Es, Cs);
+        } else
             join_item<WG, true>(work, ct, flags, blockIdx.x - xb, kw, rank, b16, b128, B);
         return;
     }
@@ -722,7 +737,8 @@ hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_i
 {
     if (max_items == 0 || ct.n == 0 || ct.ntiles == 0) return hipSuccess;
     const uint32_t extra = max_items - ct.ntiles;
-    const uint32_t blocks = ct.ntiles + (extra < 512 ? extra : 512);
+    const uint32_t blocks =
+        ct_tile_blocks(work.local_items != 0, ct.ntiles) + (extra < 512 ? extra : 512);
     const bool srt = work.local_items != 0;
     const size_t lds = 8 * (size_t)ct.WG * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
                        4 * (kCTRows / 128) + 4 * kTBS + (srt ? 6 * (size_t)kMaxChunks : 0);

@@ -1567,6 +1567,15 @@ __device__ __forceinline__ void join_s_item(const ProbeWork &work, const NarrowT
     }
 }
 
+#ifndef HSC_JOIN_XCD  // (r02c: config 2 2.09 -> 2.16 G checks/s, join 31.7 -> 29.6 us)
+#define HSC_JOIN_XCD 1
+#endif
+constexpr bool kJoinXcd = HSC_JOIN_XCD != 0;
+__host__ __device__ inline uint32_t join_tile_blocks(bool srt, uint32_t ntiles)
+{
+    return srt && kJoinXcd ? 8 * ((ntiles + 7) / 8) : ntiles;
+}
+
 template <bool srt>
 __global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_t(ProbeWork work, NarrowTiles nt,
                                                          uint32_t n, uint32_t ntiles,
@@ -1580,15 +1589,21 @@ __global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_t(ProbeWork
     __shared__ uint32_t Es[kMaxChunks], Cs[kMaxChunks];
 
     HSC_STAMP(work, 1, 0);
-    if (blockIdx.x < ntiles) {
-        if constexpr (srt)
-            join_s_item<true>(work, nt, n, blockIdx.x, verdict, keys, rank, b16, b128, Es, Cs);
-        else
+    // chunk-sorted records: neighbouring tiles on one XCD (their runs of a
+    // chunk share lines of its record area, which that XCD's L2 then serves)
+    const uint32_t tb = join_tile_blocks(srt, ntiles);
+    if (blockIdx.x < tb) {
+        if constexpr (srt) {
+            const uint32_t tile = kJoinXcd ? xcd_chunk(blockIdx.x, tb / 8) : blockIdx.x;
+            if (tile < ntiles)
+                join_s_item<true>(work, nt, n, tile, verdict, keys, rank, b16, b128, Es, Cs);
+        } else {
             join_t_item<true>(work, nt, n, blockIdx.x, verdict, keys, rank, b16, b128);
+        }
     } else {  // blocks past the tiles take the hot tiles' overflow items in turn
         const uint32_t nextra = work.item_off[1];
-        const uint32_t stride = gridDim.x - ntiles;
-        for (uint32_t xi = blockIdx.x - ntiles; xi < nextra; xi += stride) {
+        const uint32_t stride = gridDim.x - tb;
+        for (uint32_t xi = blockIdx.x - tb; xi < nextra; xi += stride) {
             __syncthreads();  // the previous item's LDS reads are done
             if constexpr (srt)
                 join_s_item<false>(work, nt, n, xi, verdict, keys, rank, b16, b128, Es, Cs);
@@ -1606,7 +1621,8 @@ hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t 
     // one block per tile + up to 512 blocks looping over the overflow items
     // (measured: one block per tile beats persistent blocks that prefetch
     // their next tile -- 27.8 vs 32 us on config 2)
-    const uint32_t blocks = ntiles + std::min<uint32_t>(max_items - ntiles, 512);
+    const uint32_t blocks = join_tile_blocks(work.local_items != 0, ntiles) +
+                            std::min<uint32_t>(max_items - ntiles, 512);
     if (work.local_items)
         k_join_t<true><<<blocks, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
     else
