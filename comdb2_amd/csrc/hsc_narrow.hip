@@ -914,7 +914,16 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
         const int cb = s & 1;
         // 1. the previous sub-chunk's whole-tile checks: their loads are
         //    younger than this sub-chunk's probe loads, which are needed now
-        if (s > 0) loc_defer_run<K>(wt, p, dfr, verdict);
+        if (s > 0) {
+            if constexpr (kSort) {  // the read sets are in registers
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (dfr.x[k] <= dfr.y[k] && tiles_max(wt, dfr.x[k], dfr.y[k]) > dfr.snap[k])
+                        verdict[RT[s - 1][k]] = 1;
+            } else {
+                loc_defer_run<K>(wt, p, dfr, verdict);
+            }
+        }
         // 2. the next sub-chunk's probe loads stay in flight through step 3
         if (s + 1 < S) load(s + 1, cb ^ 1);
         // 3. locate this sub-chunk from registers and LDS
@@ -1040,7 +1049,16 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
             }
         }
     }
-    loc_defer_run<K>(wt, p, dfr, verdict);
+    // kSort: the last sub-chunk's range-maximum loads are issued here and
+    // compared after the tail (scan, row and record stores), which they overlap
+    uint64_t dmax[K];
+    if constexpr (kSort) {
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            dmax[k] = dfr.x[k] <= dfr.y[k] ? tiles_max(wt, dfr.x[k], dfr.y[k]) : 0;
+    } else {
+        loc_defer_run<K>(wt, p, dfr, verdict);
+    }
     HSC_STAMP(work, 0, 2);
     // table locks: any write to a locked table after the snapshot
     for (uint32_t q = g * kLocTThreads + threadIdx.x; q < p.n_lock; q += work.G * kLocTThreads) {
@@ -1095,6 +1113,9 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
                 if (b.x != kNoTile32)
                     area[hist[b.x >> 12] + (b.x & 0xFFFu)] = make_uint4(b.y, b.z, b.w, RT[s][k]);
             }
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            if (dfr.x[k] <= dfr.y[k] && dmax[k] > dfr.snap[k]) verdict[RT[S - 1][k]] = 1;
     }
     HSC_STAMP(work, 0, kSort ? 5 : 4);
 }
