@@ -1256,33 +1256,41 @@ hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, 
     return hipGetLastError();
 }
 
-// Plan of chunk-sorted records: block = 8 tiles.  The block reads the 8
-// tiles' entries of every chunk row of the locate's chunk-major table (32
-// contiguous bytes per row), transposes them through LDS, and wave w scans
+// Plan of chunk-sorted records: block = 8 tiles (HSC_PLAN_S_THREADS / 64).
+// The block reads the tiles' entries of every chunk row of the locate's
+// chunk-major table (32 contiguous bytes per row), transposes them through LDS, and wave w scans
 // tile t0 + w's column as k_plan_t does; it writes the tile-major exclusive
 // offsets (hist) and run starts (cst) the join stages, the tile's count and,
 // for a hot tile, join items over its own record numbers.  The verdict pack
 // is folded in as in k_plan_t.
-__global__ __launch_bounds__(kPlanThreads) void k_plan_s(ProbeWork work, uint32_t ntiles,
-                                                         uint32_t *ctl, uint8_t *flags,
-                                                         uint32_t n_txn, uint8_t *verdict)
+// 512 threads (8 tiles, 32-byte row pieces) vs 1024 (16 tiles, 64-byte
+// pieces): one stream 62.1 vs 61.1 us, two streams 2.22 vs 2.17 G checks/s
+// (r02d) -- the headline is the two-stream number
+#ifndef HSC_PLAN_S_THREADS
+#define HSC_PLAN_S_THREADS 512
+#endif
+constexpr int kPlanSThreads = HSC_PLAN_S_THREADS;  // a wave per tile
+__global__ __launch_bounds__(kPlanSThreads) void k_plan_s(ProbeWork work, uint32_t ntiles,
+                                                          uint32_t *ctl, uint8_t *flags,
+                                                          uint32_t n_txn, uint8_t *verdict)
 {
-    constexpr int TB = kPlanThreads / 64;  // tiles per block
+    constexpr int TB = kPlanSThreads / 64;  // tiles per block
+    static_assert(TB % 4 == 0, "16-byte row pieces");
     constexpr uint32_t SR = kMaxChunks + 4;
     __shared__ __attribute__((aligned(16))) uint32_t sh[TB][SR];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t t0 = blockIdx.x * TB, t = t0 + w;
     const uint32_t G = work.G, hs = hist_stride(G), rs = (ntiles + 3) & ~3u;
-    for (uint32_t g = threadIdx.x; g < G; g += kPlanThreads) {
-        const uint32_t *row = work.cm + (size_t)g * rs + t0;
-        const u32x4 a = *(const u32x4 *)row;
-        const u32x4 b = t0 + 4 < rs ? *(const u32x4 *)(row + 4) : u32x4{0, 0, 0, 0};
-        sh[0][g] = a.x, sh[1][g] = a.y, sh[2][g] = a.z, sh[3][g] = a.w;
-        sh[4][g] = b.x, sh[5][g] = b.y, sh[6][g] = b.z, sh[7][g] = b.w;
+    // (g, piece) pairs: TB / 4 16-byte pieces of every chunk row
+    for (uint32_t i = threadIdx.x; i < G * (TB / 4); i += kPlanSThreads) {
+        const uint32_t g = i / (TB / 4), pc = i % (TB / 4);
+        const uint32_t c = t0 + 4 * pc;
+        const u32x4 a = c < rs ? *(const u32x4 *)(work.cm + (size_t)g * rs + c) : u32x4{0, 0, 0, 0};
+        sh[4 * pc][g] = a.x, sh[4 * pc + 1][g] = a.y, sh[4 * pc + 2][g] = a.z, sh[4 * pc + 3][g] = a.w;
     }
     if (verdict) {
-        const uint32_t stride = gridDim.x * kPlanThreads;
-        for (uint32_t i = blockIdx.x * kPlanThreads + threadIdx.x; i < n_txn; i += stride) {
+        const uint32_t stride = gridDim.x * kPlanSThreads;
+        for (uint32_t i = blockIdx.x * kPlanSThreads + threadIdx.x; i < n_txn; i += stride) {
             const uint8_t f = flags[i];
             verdict[i] = f != 0;
             if (f) flags[i] = 0;
@@ -1342,9 +1350,9 @@ hipError_t launch_plan_s(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, 
                          uint8_t *flags, uint32_t n_txn, uint8_t *verdict)
 {
     if (ntiles == 0) return hipSuccess;
-    constexpr uint32_t per = kPlanThreads / 64;
-    k_plan_s<<<(ntiles + per - 1) / per, kPlanThreads, 0, s>>>(work, ntiles, ctl, flags, n_txn,
-                                                               verdict);
+    constexpr uint32_t per = kPlanSThreads / 64;
+    k_plan_s<<<(ntiles + per - 1) / per, kPlanSThreads, 0, s>>>(work, ntiles, ctl, flags, n_txn,
+                                                                verdict);
     return hipGetLastError();
 }
 
