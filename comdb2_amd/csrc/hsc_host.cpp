@@ -184,6 +184,7 @@ struct hsc_ctx {
     // build, kept on the device as a sorted delta run probed beside the main
     // window; live = a built window takes appends into the delta
     bool live = false, merge_pending = false;
+    size_t ng_built = 0;  // groups the per-group device tables were sized for
     DBuf d_dgid[2], d_dwords[2], d_dlsn[2], d_dbmax, d_agid, d_awords, d_alsn;
     size_t dn = 0, dcap = 0;
     int dcur = 0;
@@ -253,6 +254,7 @@ struct hsc_ctx {
 
     // raw log / wire decode output
     DecodedLog decoded;
+    PhysStore phys;  // records key reconstruction walks may visit (hsc_logdec.cpp)
     DecodedReadSets wire;
 
     // rw conflict pairs: every window version (pre-dedupe rows in d_*2)
@@ -274,6 +276,7 @@ struct hsc_ctx {
     GraphBufs graph;
     GraphBufs subgraph;  // the graph induced on a cover (sharded SCC)
     uint32_t graph_ntxn = 0;
+    uint32_t x_max_txn = 0;  // largest txn id a staged rw pair can name (stage_rw_pairs)
 
     // Probe lanes: the probe scratch above belongs to the active lane; other
     // lanes park theirs here.  A lane is bound to the stream that last used
@@ -770,6 +773,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
     while (((size_t)1 << c->levels) <= c->ntiles) c->levels++;
     const int ng = (int)c->groups.size();
     const int nt = (int)c->table_names.size();
+    c->ng_built = (size_t)ng;
     HIPCHK(c, c->d_gstart.ensure(4 * (size_t)std::max(ng, 1)));
     HIPCHK(c, c->d_gend.ensure(4 * (size_t)std::max(ng, 1)));
     HIPCHK(c, c->d_tmax.ensure(8 * (size_t)std::max(1, c->levels) * std::max<uint32_t>(1, c->ntiles)));
@@ -1012,7 +1016,8 @@ static int flush_appends(hsc_ctx *c)
     if (!c->live || c->host_only) return HSC_OK;
     hipStream_t s = c->stream;
     const size_t k = c->app_gid.size();
-    if (k && (window_words(c) > c->W || c->dn + k > kDeltaCap || c->merge_pending)) {
+    if (k && (window_words(c) > c->W || c->dn + k > kDeltaCap || c->merge_pending ||
+              c->groups.size() > c->ng_built)) {
         c->merge_pending = true;
         c->dirty = true;  // rows stay in app_* for merge_delta (or in h_* for a host rebuild)
         return HSC_OK;
@@ -1133,6 +1138,14 @@ static int ensure_built(hsc_ctx *c)
     if (c->host_only) {  // dictionaries + marshalling only
         c->W = window_words(c);
         return HSC_OK;
+    }
+    // A group first seen after the build (the first write to an index, or
+    // hsc_register_group) has no entry in the per-group tables, which are
+    // sized at the build: the marshal would emit probes with its gid, so the
+    // window is rebuilt before any probe runs.
+    if (!c->dirty && c->groups.size() > c->ng_built) {
+        c->dirty = true;
+        if (!c->host_staged) c->merge_pending = true;
     }
     if (!c->dirty) return HSC_OK;
     if (c->host_staged) return build_from_host(c);  // staged rows include the appended ones
@@ -2343,18 +2356,25 @@ int hsc_window_reset(hsc_ctx *c)
     if (!c) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     clear_window(c);
+    c->phys.clear();
     c->end_lsn = 0;
     return HSC_OK;
+}
+
+static int ingest_log_locked(hsc_ctx *c, const hsc_llog *log)
+{
+    if (!c->host_only) (void)hipSetDevice(c->device);
+    int rc = ingest_log(c, log);
+    if (rc) return rc;
+    return ensure_built(c);
 }
 
 int hsc_window_ingest_log(hsc_ctx *c, const hsc_llog *log)
 {
     if (!c || !log) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    if (!c->host_only) (void)hipSetDevice(c->device);
-    int rc = ingest_log(c, log);
-    if (rc) return rc;
-    return ensure_built(c);
+    c->phys.clear();  // a decoded log brings no physical records for later walks
+    return ingest_log_locked(c, log);
 }
 
 int hsc_window_append(hsc_ctx *c, const hsc_write *w, size_t n)
@@ -2373,6 +2393,10 @@ int hsc_window_append(hsc_ctx *c, const hsc_write *w, size_t n)
     c->lg_rule = false;
     for (size_t i = 0; i < n; ++i) {
         c->last_append_lsn = w[i].commit_lsn;
+        // the log ends past every commit it holds: a snapshot in [old end,
+        // commit] must still see this write even if the caller skips
+        // hsc_window_set_end (which can only raise the end further)
+        if (w[i].commit_lsn >= c->end_lsn) c->end_lsn = w[i].commit_lsn + 1;
         int tid = table_id_or_add(c, w[i].tbname);
         add_write(c, tid, w[i].idxnum, (const uint8_t *)w[i].key, w[i].keylen, w[i].key != nullptr,
                   w[i].commit_lsn);
@@ -2412,25 +2436,36 @@ int hsc_window_set_end(hsc_ctx *c, uint64_t end_lsn)
     return HSC_OK;
 }
 
+static bool raw_args_ok(const hsc_raw_log *raw)
+{
+    return !((raw->nrec && (!raw->lsn || !raw->off || !raw->len || !raw->buf)) ||
+             (raw->nrecon && (!raw->recon_lsn || !raw->recon_off || !raw->recon_len || !raw->recon_keys)));
+}
+
+static int decode_locked(hsc_ctx *c, const hsc_raw_log *raw, bool reset)
+{
+    std::string err;
+    int rc = decode_raw_log(raw, c->decoded, c->phys, reset, err);
+    return rc ? fail(c, rc, err.c_str()) : HSC_OK;
+}
+
 int hsc_decode_log(hsc_ctx *c, const hsc_raw_log *raw, const hsc_llog **out)
 {
-    if (!c || !raw || !out || (raw->nrec && (!raw->lsn || !raw->off || !raw->len || !raw->buf)) ||
-        (raw->nrecon && (!raw->recon_lsn || !raw->recon_off || !raw->recon_len || !raw->recon_keys)))
-        return HSC_EINVAL;
+    if (!c || !raw || !out || !raw_args_ok(raw)) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
-    std::string err;
-    int rc = decode_raw_log(raw, c->decoded, err);
-    if (rc) return fail(c, rc, err.c_str());
+    int rc = decode_locked(c, raw, false);
+    if (rc) return rc;
     *out = &c->decoded.llog;
     return HSC_OK;
 }
 
 int hsc_window_ingest_raw(hsc_ctx *c, const hsc_raw_log *raw)
 {
-    const hsc_llog *lg = nullptr;
-    int rc = hsc_decode_log(c, raw, &lg);
+    if (!c || !raw || !raw_args_ok(raw)) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    int rc = decode_locked(c, raw, true);  // a new log: walks see only its records
     if (rc) return rc;
-    return hsc_window_ingest_log(c, lg);
+    return ingest_log_locked(c, &c->decoded.llog);
 }
 
 int hsc_decode_serial(hsc_ctx *c, const hsc_serial_msgs *m, const hsc_readsets **out)
@@ -2483,6 +2518,7 @@ int hsc_window_ingest_device(hsc_ctx *c, size_t n, int words, const uint32_t *gi
     std::lock_guard<std::mutex> g(c->mu);
     if (!c->host_only) (void)hipSetDevice(c->device);
     clear_window(c);
+    c->phys.clear();
     c->host_staged = false;
     c->end_lsn = end_lsn;
     if (words < window_words(c)) return fail(c, HSC_EINVAL, "fewer key words than a registered group needs");
@@ -2996,6 +3032,12 @@ static int graph_build_timed(hsc_ctx *c, const GraphInput &in, bool full, float 
     HIPCHK(c, hipEventCreate(&e1));
     HIPCHK(c, hipEventRecord(e0, s));
     GraphInput gi = in;
+    if (gb.n_extra && c->x_max_txn >= in.ntxn) {  // staged rows would index past the CSR arrays
+        gb.n_extra = 0;
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        return fail(c, HSC_EINVAL, "a staged rw pair names a txn >= the build's ntxn");
+    }
     if (gb.n_extra) {  // staged edges join this build, once
         gi.x_rows = gb.x_rows.as<uint64_t>();
         gi.x_type = gb.x_type.as<uint64_t>();
@@ -3159,6 +3201,12 @@ int hsc_dep_graph_stage_rw_pairs(hsc_ctx *c, uint32_t nrs, const uint32_t *reads
     GraphBufs &gb = c->graph;
     const size_t n = c->e_dev_n;
     gb.n_extra = 0;
+    // every endpoint a pair can map to; graph_build_timed rejects the staged
+    // rows if the build's ntxn does not cover them
+    uint32_t xm = 0;
+    for (uint32_t i = 0; i < nrs; ++i) xm = std::max(xm, readset_txn[i]);
+    for (size_t i = 0; i < ncommit; ++i) xm = std::max(xm, commit_txn[i]);
+    c->x_max_txn = xm;
     if (n == 0) return HSC_OK;
     // mapping tables next to each other: rs_txn[nrs] | commit_txn[ncommit] | commit_lsn[ncommit]
     const size_t o_ct = ((size_t)nrs + 1) & ~(size_t)1, o_cl = o_ct + ncommit + (ncommit & 1);

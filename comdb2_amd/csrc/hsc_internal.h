@@ -499,7 +499,29 @@ struct DecodedLog {
     hsc_llog llog{};
     void view();  // point llog at the vectors
 };
-int decode_raw_log(const hsc_raw_log *raw, DecodedLog &out, std::string &err);
+// Physical records (every record, header fields; whole bytes of __db_addrem
+// and __db_big) that the index-key reconstruction walk may visit
+// (bdb/rowlocks.c:209-617): the decoded raw logs since the last ingest, so a
+// walk reaches records of earlier appends.  LSNs ascending.
+struct PhysStore {
+    std::vector<uint64_t> lsn, prev, off;
+    std::vector<uint32_t> type, len;
+    std::vector<uint8_t> bytes;
+    void clear()
+    {
+        lsn.clear(), prev.clear(), off.clear(), type.clear(), len.clear(), bytes.clear();
+    }
+    long find(uint64_t l) const;
+    void truncate(size_t n, size_t nbytes)
+    {
+        lsn.resize(n), prev.resize(n), off.resize(n), type.resize(n), len.resize(n);
+        bytes.resize(nbytes);
+    }
+};
+// reset: the raw log starts a new log (ingest), else it continues the stored
+// records (append; a log whose first LSN is not above them starts anew).
+int decode_raw_log(const hsc_raw_log *raw, DecodedLog &out, PhysStore &ps, bool reset,
+                   std::string &err);
 
 // OSQL_SERIAL wire decoder (hsc_wire.cpp): payloads -> hsc_readsets SoA.
 struct DecodedReadSets {

@@ -255,7 +255,7 @@ def _dbt(b: bytes) -> bytes:
 
 def encode_record(rectype: int, prev: int, isabort: int, tbname: Optional[str], ix: int,
                   key: Optional[bytes], hdr_prev: int, txnid: int = 0x80000001,
-                  salt: int = 0) -> bytes:
+                  salt: int = 0, dtalen: Optional[int] = None) -> bytes:
     """One log record in the gen_rec_endian.awk encoding of a little-endian
     host (berkdb/dist/gen_rec_endian.awk:550-630): u32/short fields and LSNs
     big-endian, genid_t native (little-endian), DBT = u32 BE size + bytes."""
@@ -272,7 +272,12 @@ def encode_record(rectype: int, prev: int, isabort: int, tbname: Optional[str], 
                     (salt * 7).to_bytes(8, "big"), salt.to_bytes(8, "big"), _be32(0), _be32(3),
                     _dbt(b""), _dbt(b"")]
         return b"".join(out)
+    after_k = False
     for f in prog:
+        if f == "i" and after_k and dtalen is not None:
+            out.append(_be32(dtalen))  # dtalen of the keyless index records
+            continue
+        after_k = f == "k"
         if f == "T":
             out.append(_dbt((tbname or "").encode() + b"\x00"))
         elif f == "D":
@@ -294,6 +299,51 @@ def encode_record(rectype: int, prev: int, isabort: int, tbname: Optional[str], 
         elif f == "A":
             out.append(_be32(isabort))
     return b"".join(out)
+
+
+# berkdb physical records (berkdb/db/db.src) and page items
+# (berkdb/dbinc/db_page.h:606-679) that the index-key reconstruction walks
+# (bdb/rowlocks.c:209-617)
+REC_DB_ADDREM, REC_DB_BIG, REC_DB_DEBUG, REC_DB_PG_ALLOC = 41, 43, 47, 49
+REC_DB_PG_FREE, REC_DB_PG_FREEDATA = 50, 52
+DB_ADD_DUP, DB_REM_DUP, DB_ADD_BIG, DB_REM_BIG = 1, 2, 3, 4   # berkdb/dbinc/db_am.h:23-26
+B_KEYDATA, B_DUPLICATE, B_OVERFLOW = 1, 2, 3
+
+
+def bkeydata(item: bytes, flags: int = 0) -> bytes:
+    """BKEYDATA {u16 len, u8 type, data} as it sits on a page (native LE)."""
+    return len(item).to_bytes(2, "little") + bytes([B_KEYDATA | flags]) + item
+
+
+def boverflow(tlen: int, pgno: int = 7, flags: int = 0) -> bytes:
+    """BOVERFLOW {u16 unused, u8 type, u8 unused, u32 pgno, u32 tlen}."""
+    return (b"\x00\x00" + bytes([B_OVERFLOW | flags, 0]) + pgno.to_bytes(4, "little")
+            + tlen.to_bytes(4, "little"))
+
+
+def encode_addrem(prev: int, opcode: int, hdr: bytes, dbt: bytes, pgno: int = 3,
+                  indx: int = 0, txnid: int = 0x80000001) -> bytes:
+    """__db_addrem (db.src:47-57): opcode, fileid, pgno, indx, nbytes, hdr
+    DBT, dbt DBT, pagelsn."""
+    return b"".join([_be32(REC_DB_ADDREM), _be32(txnid), _lsn_bytes(prev), _be32(opcode),
+                     _be32(5), _be32(pgno), _be32(indx), _be32(len(hdr) + len(dbt)),
+                     _dbt(hdr), _dbt(dbt), _lsn_bytes(prev)])
+
+
+def encode_big(prev: int, opcode: int, chunk: bytes, pgno: int = 9,
+               txnid: int = 0x80000001) -> bytes:
+    """__db_big (db.src:73-83): opcode, fileid, pgno, prev_pgno, next_pgno,
+    dbt, pagelsn, prevlsn, nextlsn."""
+    return b"".join([_be32(REC_DB_BIG), _be32(txnid), _lsn_bytes(prev), _be32(opcode), _be32(5),
+                     _be32(pgno), _be32(pgno - 1), _be32(pgno + 1), _dbt(chunk),
+                     _lsn_bytes(prev), _lsn_bytes(0), _lsn_bytes(0)])
+
+
+def encode_phys_other(rectype: int, prev: int, txnid: int = 0x80000001) -> bytes:
+    """A physical record the walk only steps over (debug, pg_alloc, pg_free,
+    pg_freedata): header plus a few fields."""
+    return b"".join([_be32(rectype), _be32(txnid), _lsn_bytes(prev), _be32(5), _be32(11),
+                     _lsn_bytes(prev), _be32(0), _dbt(b"\x01\x02\x03\x04"), _be32(0)])
 
 
 def encode_raw(log: LLog) -> RawLog:
@@ -489,3 +539,151 @@ def encode_serial(rs: "ReadSets") -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         pos += len(msg)
     return (np.frombuffer(b"".join(chunks) or b"\x00", np.uint8).copy(),
             np.array(offs, np.uint64), np.array(lens, np.uint64))
+
+
+def encode_raw_physical(log: LLog, seed: int = 0, overflow: float = 0.3, noise: bool = True,
+                        adversarial: float = 0.0) -> RawLog:
+    """The raw stream of `log` as a server logs it, with the berkdb physical
+    records that carry the keys of undo_add_ix / undo_del_ix / undo_del_ix_lk
+    (which the logical records do not) and no recon side table: every
+    record's header prev_lsn follows its transaction's chain, and before each
+    keyless index record the transaction logs the key and data items
+    (bdb/rowlocks.c:171-201):
+      add    key then data as DB_ADD_DUP addrems (item in dbt; header empty or
+             with type 0), or the key as DB_ADD_BIG pages + an addrem whose
+             header is a BOVERFLOW (tlen)
+      delete key then data as DB_REM_DUP addrems whose header is the page item
+             (BKEYDATA, flag bits set at random), or the key as DB_REM_BIG
+             pages + a BOVERFLOW addrem
+    with noise the walk must step over: split addrems logged before the key,
+    debug / pg_alloc records, an "unexpected type" (B_DUPLICATE) addrem, and
+    the pg_free pattern (pg_alloc, addrem, pg_free between key and data: the
+    addrem after the pg_free is skipped, bdb/rowlocks.c:275-289).  Physical
+    records take free LSNs inside the gap before the keyless record (the
+    LogBuilder step is 64), so the logical records keep their LSNs.
+
+    adversarial > 0: that fraction of keyless records gets a pattern whose
+    walk does not find the intended key (pg_free right after the data item,
+    a missing key item, an item of the wrong length, an overflow item with
+    missing pages, a header too short for its item, a REM_DUP addrem with an
+    empty header) -- for decoder-vs-oracle agreement, not verdicts."""
+    rng = np.random.default_rng(seed)
+    txn_of: dict = {}
+    last: dict = {}
+    recs = []  # (lsn, bytes)
+    nrec = log.nrec
+
+    def key_of(i):
+        o = int(log.key_off[i])
+        return bytes(log.keys[o:o + int(log.keylen[i])])
+
+    for i in range(nrec):
+        t = int(log.rectype[i])
+        l = int(log.lsn[i])
+        p = int(log.prev[i])
+        if t in LLOG_LAYOUTS:
+            txn = txn_of.get(p, ("t", l)) if t != REC_LTRAN_START and p else ("t", l)
+        else:
+            txn = txn_of.get(p, ("r", l))
+        txn_of[l] = txn
+        chain = last.get(txn, 0)
+        prev_rec = int(log.lsn[i - 1]) if i else 0
+        slots = [l - 4 * k for k in range(15, 0, -1) if l - 4 * k > prev_rec + 1]
+        tb = log.tbnames[int(log.table[i])] if 0 <= int(log.table[i]) < len(log.tbnames) else None
+        if t in KEYLESS_IX:
+            key = key_of(i)
+            seq = _phys_items(rng, t == REC_UNDO_ADD_IX, key, overflow, noise,
+                              rng.random() < adversarial)
+            seq = seq[-len(slots):] if len(seq) > len(slots) else seq
+            for (kind, a, b, c, _), sl in zip(seq, slots[len(slots) - len(seq):]):
+                if kind == "addrem":
+                    rec = encode_addrem(chain, a, b, c)
+                elif kind == "big":
+                    rec = encode_big(chain, a, b)
+                else:
+                    rec = encode_phys_other(a, chain)
+                recs.append((sl, rec))
+                chain = sl
+            rec = encode_record(t, p, int(log.isabort[i]), tb, int(log.ix[i]), key, chain,
+                                salt=i, dtalen=8)
+        elif t in LLOG_LAYOUTS:
+            key = key_of(i) if t in IX_TYPES else None
+            hdr_prev = 0 if t == REC_LTRAN_START else chain
+            rec = encode_record(t, p, int(log.isabort[i]), tb, int(log.ix[i]), key, hdr_prev,
+                                salt=i)
+        else:
+            rec = encode_record(t, p, int(log.isabort[i]), tb, int(log.ix[i]), None, p, salt=i)
+        recs.append((l, rec))
+        last[txn] = l
+    recs.sort(key=lambda r: r[0])
+    off = np.cumsum([0] + [len(r) for _, r in recs])[:-1]
+    e = np.zeros(0, np.uint64)
+    return RawLog(lsn=np.array([x for x, _ in recs], np.uint64), off=np.asarray(off, np.uint64),
+                  len=np.array([len(r) for _, r in recs], np.uint32),
+                  buf=np.frombuffer(b"".join(r for _, r in recs) or b"\x00", np.uint8).copy(),
+                  end_lsn=int(log.end_lsn), recon_lsn=e, recon_off=e.copy(),
+                  recon_len=np.zeros(0, np.int32), recon_keys=np.zeros(1, np.uint8))
+
+
+def _phys_items(rng, is_add: bool, key: bytes, overflow: float, noise: bool, bad: bool):
+    """Physical records (log order) carrying one index op's key and data item:
+    ("addrem", opcode, hdr, dbt, role), ("big", opcode, chunk, None, role) or
+    ("other", rectype, None, None, role); role is "key", "data" or "noise"."""
+    genid = bytes(rng.integers(0, 256, size=8).astype(np.uint8))
+    op = DB_ADD_DUP if is_add else DB_REM_DUP
+    seq = []
+    if noise and rng.random() < 0.3:  # a split's addrem into the parent, before the item
+        seq.append(("addrem", op, b"" if is_add else bkeydata(b"split"),
+                    b"\x09" * 5 if is_add else b"", "noise"))
+    big_op = DB_ADD_BIG if is_add else DB_REM_BIG
+    if key and rng.random() < overflow:
+        cuts = sorted(set(int(x) for x in rng.integers(1, max(len(key), 2), size=2)))
+        bounds = [0] + [c for c in cuts if 0 < c < len(key)] + [len(key)]
+        for x, y in zip(bounds, bounds[1:]):
+            seq.append(("big", big_op, key[x:y], None, "key"))
+        seq.append(("addrem", op, boverflow(len(key), flags=int(rng.choice([0, 0x80]))), b"",
+                    "key"))
+    elif is_add:
+        hdr = b"" if rng.random() < 0.7 else b"\x00\x00\x00"   # B_TYPE == 0: item in dbt
+        seq.append(("addrem", op, hdr, key, "key"))
+    else:
+        seq.append(("addrem", op, bkeydata(key, int(rng.choice([0, 0x80, 0x40]))), b"", "key"))
+    if noise:
+        r = rng.random()
+        if r < 0.25:
+            seq.append(("other", REC_DB_DEBUG, None, None, "noise"))
+        elif r < 0.45:
+            seq += [("other", REC_DB_PG_ALLOC, None, None, "noise"),
+                    ("addrem", DB_REM_DUP, bkeydata(b"freed"), b"", "noise"),
+                    ("other", int(rng.choice([REC_DB_PG_FREE, REC_DB_PG_FREEDATA])), None, None,
+                     "noise")]
+        elif r < 0.6:
+            seq.append(("addrem", DB_REM_DUP, bytes([4, 0, B_DUPLICATE]) + b"dupx", b"", "noise"))
+    if is_add:
+        seq.append(("addrem", op, b"" if rng.random() < 0.8 else bkeydata(genid), genid, "data"))
+    else:
+        seq.append(("addrem", op, bkeydata(genid), b"", "data"))
+    if noise and rng.random() < 0.3:
+        seq.append(("other", int(rng.choice([REC_DB_DEBUG, REC_DB_PG_ALLOC])), None, None, "noise"))
+    if bad:
+        k = int(rng.integers(0, 6))
+        data_at = max(j for j, x in enumerate(seq) if x[4] == "data")
+        if k == 0:    # pg_free right after the data item: the data addrem is skipped
+            seq.insert(data_at + 1, ("other", REC_DB_PG_FREE, None, None, "noise"))
+        elif k == 1:  # no key item at all
+            seq = [x for x in seq if x[4] != "key"]
+        elif k == 2:  # the key item one byte short / long
+            kk = key[:-1] if key and rng.random() < 0.5 else key + b"\x7f"
+            seq = [(x[0], x[1], bkeydata(kk) if not is_add and x[0] == "addrem" else x[2],
+                    kk if is_add and x[0] == "addrem" else x[3], x[4])
+                   if x[4] == "key" and x[0] == "addrem" and (is_add or x[2][2:3] != b"\x03") else x
+                   for x in seq]
+        elif k == 3:  # an overflow item missing its first page
+            bigs = [j for j, x in enumerate(seq) if x[0] == "big"]
+            if bigs:
+                seq.pop(bigs[0])
+        elif k == 4:  # a header too short for the item it announces
+            seq.insert(data_at, ("addrem", DB_REM_DUP, b"\xff\x00\x01", b"", "noise"))
+        else:         # REM_DUP with an empty header: hdr.data aliases the dbt size
+            seq.insert(data_at, ("addrem", DB_REM_DUP, b"", b"\x00\x03\x01\x00", "noise"))
+    return seq

@@ -87,7 +87,14 @@ enum {
     HSC_REC_UNDO_DEL_DTA_LK = 10015,
     HSC_REC_UNDO_DEL_IX_LK = 10016,
     HSC_REC_UNDO_UPD_DTA_LK = 10017,
-    HSC_REC_UNDO_UPD_IX_LK = 10018
+    HSC_REC_UNDO_UPD_IX_LK = 10018,
+    /* berkdb physical records the index-key reconstruction walks
+     * (bdb/rowlocks.c:209-426; layouts berkdb/db/db.src) */
+    HSC_REC_DB_ADDREM = 41,          /* db.src:47-57                          */
+    HSC_REC_DB_BIG = 43,             /* db.src:73-83                          */
+    HSC_REC_DB_DEBUG = 47,           /* db.src:131                            */
+    HSC_REC_DB_PG_FREE = 50,         /* db.src:177-184                        */
+    HSC_REC_DB_PG_FREEDATA = 52      /* db.src:206-214                        */
 };
 
 typedef struct hsc_llog {
@@ -223,15 +230,21 @@ int hsc_device_count(void);
  * key) at the regop's LSN.  Replaces the window. */
 int hsc_window_ingest_log(hsc_ctx *ctx, const hsc_llog *log);
 /* Raw log records as a log cursor returns them (DB_LOGC->get data): the
- * bdb/llog.src:26-225 layouts and the txn regop records
- * (berkdb/dbinc_auto/txn_auto.h:6-86) in the gen_rec_endian.awk on-disk
- * encoding of a little-endian host: u32/short fields and DB_LSNs big-endian,
- * genid_t native, DBT = u32 BE size + bytes.  Record i is lsn[i] (strictly
- * increasing), bytes buf[off[i] .. off[i] + len[i]).  undo_add_ix /
- * undo_del_ix / undo_del_ix_lk carry no key: the reference rebuilds it from
- * the physical log at undolsn = the record's header prev_lsn
- * (bdb/serializable.c:123-130,174-181); the caller passes those keys as
- * recon_* sorted by undolsn (a missing key is HSC_ELOG). */
+ * bdb/llog.src:26-225 layouts, the txn regop records
+ * (berkdb/dbinc_auto/txn_auto.h:6-86) and any berkdb physical records, in the
+ * gen_rec_endian.awk on-disk encoding of a little-endian host: u32/short
+ * fields and DB_LSNs big-endian, genid_t native, DBT = u32 BE size + bytes.
+ * Record i is lsn[i] (strictly increasing), bytes buf[off[i] .. off[i] +
+ * len[i]).  undo_add_ix / undo_del_ix / undo_del_ix_lk carry no key: the
+ * reference rebuilds it from the physical log at undolsn = the record's header
+ * prev_lsn (bdb/serializable.c:123-130,174-181), walking the header prev_lsn
+ * chain over __db_addrem / __db_big / __db_pg_free[data] records
+ * (bdb_reconstruct_add / _delete, bdb/rowlocks.c:209-617); the decoder runs
+ * the same walk over the records of this log and, for appends, of every raw
+ * log decoded since the last ingest.  A key the walk does not fully define
+ * (the reference would read its uninitialised key buffer) is HSC_ELOG.
+ * recon_* (optional, sorted by undolsn) supplies keys directly: an entry for
+ * a record's undolsn takes precedence over the walk. */
 typedef struct hsc_raw_log {
     size_t nrec;
     const uint64_t *lsn;
@@ -260,7 +273,10 @@ int hsc_decode_log(hsc_ctx *ctx, const hsc_raw_log *log, const hsc_llog **out);
  * than the window's words, the next check folds the delta into the main
  * window with one device rebuild.  Decoded writes carry no record LSNs, so
  * after one the DB_SET-on-a-non-record rule (bdb/serializable.c:417-421) is
- * off for the window.  Call hsc_window_set_end for the new end of the log. */
+ * off for the window.  The window's end LSN advances to at least
+ * commit_lsn + 1 of every appended write (a snapshot at or past the old end
+ * must still see it: fail closed); hsc_window_set_end sets the exact end of
+ * the log (curlsn of full checks). */
 int hsc_window_append(hsc_ctx *ctx, const hsc_write *w, size_t n);
 /* Append log records: the continuation of the window's log (LSNs above every
  * record taken so far; log->end_lsn is the new end).  Every txn a new regop

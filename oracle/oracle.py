@@ -37,6 +37,10 @@ class _SjProbes(C.Structure):
                 ("table_max", _p), ("ntables", C.c_uint32)]
 
 
+class _RoLog(C.Structure):
+    _fields_ = [("nrec", C.c_size_t), ("lsn", _p), ("off", _p), ("len", _p), ("buf", _p)]
+
+
 def build() -> str:
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
     return LIB_PATH
@@ -70,6 +74,9 @@ def load():
         lib.co_coalesce.restype = C.c_long
         lib.co_coalesce.argtypes = [C.c_int] + [_p] * 10 + [_p, C.c_uint64, C.POINTER(C.c_char_p),
                                                             C.c_int] + [_p] * 10
+        lib.ro_reconstruct.restype = C.c_int
+        lib.ro_reconstruct.argtypes = [C.POINTER(_RoLog), C.c_int, C.c_uint64, C.c_int, C.c_int,
+                                       _p, C.POINTER(C.c_int)]
         lib.or_serial_check.restype = C.c_int
         lib.or_serial_check.argtypes = [C.POINTER(_OrLog), _p, C.POINTER(C.c_uint),
                                         C.POINTER(C.c_uint), C.c_int]
@@ -221,3 +228,104 @@ def coalesce(rs: ReadSets) -> ReadSets:
     return dataclasses.replace(rs, txn_off=out_off, table=o[0], idxnum=o[1], lflag=o[2], rflag=o[3],
                                islocked=o[4], lkeylen=o[5], rkeylen=o[6], lkey_off=o[7],
                                rkey_off=o[8])
+
+
+# ---------------------------------------------------------------------------
+# raw log decode with index-key reconstruction (recon_oracle.c)
+# ---------------------------------------------------------------------------
+class OracleUndefined(Exception):
+    """A keyless index record whose key the reference would leave
+    (partly) uninitialised, or a walk over malformed physical bytes."""
+
+
+_LAYOUTS = {  # bdb/llog.src:26-225 field programs (formats.LLOG_LAYOUTS letters)
+    10003: "TiiGGPD", 10004: "TIGGPkd", 10005: "GPGA", 10006: "Gi", 10007: "GPL",
+    10008: "TGGPiiiD", 10009: "TGIGPDkd", 10010: "TGGGPiiDDi", 10011: "TGGGPIKi",
+    10013: "TiiGGP", 10014: "TIGGPKi", 10015: "TGGPiii", 10016: "TGIGPkd",
+    10017: "TGGGPiii", 10018: "TGGGPIKi"}
+
+
+def decode_raw(raw) -> LLog:
+    """Oracle decode of a raw log (formats.RawLog): llog records by their
+    bdb/llog.src layouts; the keys of undo_add_ix / undo_del_ix[_lk] by the
+    restated bdb_reconstruct_add / _delete walk from undolsn = the header
+    prev_lsn (bdb/serializable.c:120-133,170-184,242-258) -- or from the
+    recon side table when it names undolsn.  Raises OracleUndefined when a
+    key is not fully defined by the walk."""
+    lib = load()
+    cols = [np.ascontiguousarray(raw.lsn, np.uint64), np.ascontiguousarray(raw.off, np.uint64),
+            np.ascontiguousarray(raw.len, np.uint32), np.ascontiguousarray(raw.buf, np.uint8)]
+    rl = _RoLog(len(cols[0]), *[c.ctypes.data for c in cols])
+    recon = {int(u): bytes(raw.recon_keys[int(o):int(o) + int(n)])
+             for u, o, n in zip(raw.recon_lsn, raw.recon_off, raw.recon_len)}
+    buf = bytes(raw.buf)
+    be = lambda b, o: int.from_bytes(b[o:o + 4], "big")  # noqa: E731
+    rows, keys, names, tid = [], bytearray(), [], {}
+    for i in range(len(cols[0])):
+        o, n = int(raw.off[i]), int(raw.len[i])
+        r = buf[o:o + n]
+        if n < 16:
+            raise OracleUndefined(f"record {i}: truncated header")
+        t, hprev = be(r, 0), (be(r, 8) << 32) | be(r, 12)
+        row = dict(lsn=int(raw.lsn[i]), t=t, prev=hprev, isabort=0, table=-1, ix=0, koff=0,
+                   klen=0)
+        prog = _LAYOUTS.get(t)
+        if prog is not None:
+            row["prev"] = 0
+            q, key, klen, dtalen = 16, None, 0, 0
+            for f in prog:
+                if f in "TDK":
+                    sz = be(r, q)
+                    d = r[q + 4:q + 4 + sz]
+                    if len(d) < sz:
+                        raise OracleUndefined(f"record {i}: truncated")
+                    q += 4 + sz
+                    if f == "T":
+                        nm = d.split(b"\x00")[0].decode("utf-8", "surrogateescape")
+                        row["table"] = tid.setdefault(nm, len(names))
+                        if row["table"] == len(names):
+                            names.append(nm)
+                    elif f == "K":
+                        key, klen = d, sz
+                elif f == "G":
+                    q += 8
+                elif f in "PL":
+                    v = (be(r, q) << 32) | be(r, q + 4)
+                    q += 8
+                    if f == "P":
+                        row["prev"] = v
+                else:
+                    v = be(r, q)
+                    q += 4
+                    if f == "I":
+                        row["ix"] = int(np.int16(np.uint16(v & 0xFFFF)))
+                    elif f == "k":
+                        klen = v
+                    elif f == "d":
+                        dtalen = v
+                    elif f == "A":
+                        row["isabort"] = int(np.int16(np.uint16(v & 0xFFFF)))
+                if q > n:
+                    raise OracleUndefined(f"record {i}: truncated")
+            if t in (10004, 10009, 10016):
+                if hprev in recon:
+                    key = recon[hprev]
+                else:
+                    kb = np.zeros(max(klen, 1), np.uint8)
+                    defined = C.c_int(0)
+                    lib.ro_reconstruct(C.byref(rl), 0 if t == 10004 else 1, hprev, klen, dtalen,
+                                       kb.ctypes.data, C.byref(defined))
+                    if not defined.value:
+                        raise OracleUndefined(f"record {i}: key not reconstructed")
+                    key = bytes(kb[:klen])
+            if key is not None:
+                row["koff"], row["klen"] = len(keys), len(key)
+                keys += key
+        rows.append(row)
+    col = lambda k, dt: np.array([x[k] for x in rows], dtype=dt)  # noqa: E731
+    return LLog(lsn=col("lsn", np.uint64), rectype=col("t", np.uint32), prev=col("prev", np.uint64),
+                isabort=col("isabort", np.int16), table=col("table", np.int32),
+                ix=col("ix", np.int16), key_off=col("koff", np.uint64),
+                keylen=col("klen", np.int32),
+                keys=np.frombuffer(bytes(keys) or b"\x00", np.uint8).copy(), tbnames=names,
+                end_lsn=int(raw.end_lsn))

@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SAN_LIB = os.path.join(ROOT, "comdb2_amd", "lib", "san", "libhsc_san.so")
 HOST_TESTS = ["tests/test_decoder_fuzz.py", "tests/test_logdec.py", "tests/test_wire.py",
               "tests/test_marshal.py", "tests/test_incremental.py", "tests/test_abi.py",
-              "tests/test_coalesce.py"]
+              "tests/test_coalesce.py", "tests/test_recon.py"]
 
 
 def asan_runtime():
