@@ -580,8 +580,9 @@ class Config3Arrays:
 
 def config3_arrays(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4,
                    n_writes: int = 200_000, keys_per_commit: int = 8, n_txn: int = 20_000,
-                   ranges_per_txn: int = 10, vmax: int = 1 << 12, snap_recent: float = 0.05,
-                   lock_frac: float = 0.01, rs_seed: Optional[int] = None) -> Config3Arrays:
+                   ranges_per_txn: int = 10, vmax: int = 1 << 12, snap_recent: float = 0.01,
+                   lock_frac: float = 0.01, rs_seed: Optional[int] = None,
+                   range_rows: int = 8, prefix_drop: int = 2) -> Config3Arrays:
     """Config 3 as arrays (no log): n_tables x n_ix composite-key groups with
     log-normal sizes, commits of keys_per_commit index writes (30% also write
     a data row of a random table), LSNs exactly as LogBuilder assigns them
@@ -589,7 +590,11 @@ def config3_arrays(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4,
     read sets of point / range / prefix ranges (and a few table locks) over
     1-3 tables each.  config3() builds the same workload as a log.  rs_seed
     draws the read sets from their own generator (another batch over the same
-    window)."""
+    window).  range_rows > 0: a range spans 1..range_rows neighbouring keys of
+    its group (in key order) instead of two random keys, and prefix_drop > 0:
+    a prefix range drops 1..prefix_drop trailing bytes of a key instead of
+    keeping a random 1..L-1 of them -- narrow read sets, as config 2's
+    (conflict rate 20-60 %)."""
     rng = np.random.default_rng(seed)
     tb = [f"t{i}" for i in range(n_tables)]
     G = n_tables * n_ix
@@ -627,6 +632,9 @@ def config3_arrays(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4,
     recent = max(1, int(len(commits) * snap_recent))
     if rs_seed is not None:
         rng = np.random.default_rng([seed, rs_seed])
+    sorted_keys = None
+    if range_rows > 0:
+        sorted_keys = [kg[np.lexsort(kg.T[::-1])] for kg in keys_of]
     sets, snaps = [], []
     for t in range(n_txn):
         rs = []
@@ -642,10 +650,19 @@ def config3_arrays(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4,
                 if u < 0.5:
                     rs.append(Range(tb[tt], ix, a, a))
                 elif u < 0.8:
-                    b = bytes(keys_of[g][int(rng.integers(0, len(keys_of[g])))])
-                    rs.append(Range(tb[tt], ix, min(a, b), max(a, b)))
+                    if sorted_keys is not None:
+                        sk = sorted_keys[g]
+                        i = int(rng.integers(0, len(sk)))
+                        j = min(len(sk) - 1, i + int(rng.integers(0, range_rows)))
+                        rs.append(Range(tb[tt], ix, bytes(sk[i]), bytes(sk[j])))
+                    else:
+                        b = bytes(keys_of[g][int(rng.integers(0, len(keys_of[g])))])
+                        rs.append(Range(tb[tt], ix, min(a, b), max(a, b)))
                 else:
-                    p = a[: int(rng.integers(1, len(a)))]
+                    if prefix_drop > 0:
+                        p = a[: max(1, len(a) - int(rng.integers(1, prefix_drop + 1)))]
+                    else:
+                        p = a[: int(rng.integers(1, len(a)))]
                     rs.append(Range(tb[tt], ix, p, p))
         rs.sort(key=lambda r: (r.tbname, -r.islocked, r.idxnum, r.lkey or b""))
         sets.append(rs)
@@ -657,14 +674,15 @@ def config3_arrays(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4,
 
 def config3(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4, n_writes: int = 200_000,
             keys_per_commit: int = 8, n_txn: int = 20_000, ranges_per_txn: int = 10,
-            vmax: int = 1 << 12, snap_recent: float = 0.05, lock_frac: float = 0.01):
+            vmax: int = 1 << 12, snap_recent: float = 0.01, lock_frac: float = 0.01,
+            range_rows: int = 8, prefix_drop: int = 2):
     """Log of commits writing composite index keys (upd_ix) plus dta records
     over n_tables x n_ix groups with log-normal group sizes, and read sets of
     point / range / prefix ranges (and a few full-scan table locks) over 1-3
     tables each (ranges sorted per table like coalesced arrays).  Returns
     (LLog, ReadSets); config3_arrays() is the same workload as arrays."""
     a = config3_arrays(seed, n_tables, n_ix, n_writes, keys_per_commit, n_txn, ranges_per_txn,
-                       vmax, snap_recent, lock_frac)
+                       vmax, snap_recent, lock_frac, range_rows=range_rows, prefix_drop=prefix_drop)
     n_ix_ = n_ix
     lb = LogBuilder(a.tbnames)
     dta = dict(a.dta)
@@ -678,6 +696,63 @@ def config3(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4, n_writes
         l = lb.commit(c)
         assert l == int(a.commit_lsn[c])
     return lb.build(), a.readsets
+
+
+def config3_log(a: Config3Arrays, from_commit: int = 0) -> LLog:
+    """The log of config3_arrays' workload (the records config3() logs, with
+    the same LSNs), vectorised, from commit `from_commit` on: a tail of the
+    log is enough for the oracle to check read sets whose snapshots fall
+    inside it (each check only reads records after its snapshot)."""
+    n_tab = len(a.tbnames)
+    n_ix = len(a.groups) // n_tab
+    K = a.keys_per_commit
+    nc = len(a.commit_lsn)
+    kc = np.minimum(K, len(a.w_group) - np.arange(nc, dtype=np.int64) * K)
+    has = np.zeros(nc, bool)
+    dt = np.full(nc, -1, np.int64)
+    for c, t in a.dta:
+        has[c], dt[c] = True, t
+    nrec = 1 + kc + has.astype(np.int64) + 2
+    base = np.concatenate([[0], np.cumsum(nrec)[:-1]])
+    c0 = int(from_commit)
+    cs = np.arange(c0, nc)
+    commit_of = np.repeat(cs, nrec[c0:])
+    idx = base[c0] + np.arange(int(nrec[c0:].sum()), dtype=np.int64)
+    j = idx - base[commit_of]
+    k_of, n_of = kc[commit_of], nrec[commit_of]
+    lsns = lsn_of_index(idx.astype(np.uint64))
+    rectype = np.full(len(idx), F.REC_UNDO_UPD_IX, np.uint32)
+    rectype[j == 0] = F.REC_LTRAN_START
+    is_dta = has[commit_of] & (j == k_of + 1)
+    rectype[is_dta] = F.REC_UNDO_UPD_DTA
+    rectype[j == n_of - 2] = F.REC_LTRAN_COMMIT
+    rectype[j == n_of - 1] = F.REC_TXN_REGOP
+    prev = lsn_of_index(np.maximum(idx - 1, 0).astype(np.uint64))
+    prev[j == 0] = 0
+    is_ix = rectype == F.REC_UNDO_UPD_IX
+    w = commit_of[is_ix] * K + (j[is_ix] - 1)
+    g, r = a.w_group[w], a.w_row[w]
+    table = np.full(len(idx), -1, np.int32)
+    ix = np.zeros(len(idx), np.int16)
+    table[is_ix] = (g // n_ix).astype(np.int32)
+    ix[is_ix] = (g % n_ix).astype(np.int16)
+    table[is_dta] = dt[commit_of[is_dta]].astype(np.int32)
+    glen = np.array([kg.shape[1] for kg in a.keys_of], np.int64)
+    klen = glen[g]
+    koff = np.concatenate([[0], np.cumsum(klen)[:-1]]).astype(np.int64)
+    blob = np.zeros(max(int(klen.sum()), 1), np.uint8)
+    for gg in np.unique(g):
+        m = g == gg
+        L = int(glen[gg])
+        blob[(koff[m][:, None] + np.arange(L)[None, :]).reshape(-1)] = a.keys_of[gg][r[m]].reshape(-1)
+    key_off = np.zeros(len(idx), np.uint64)
+    keylen = np.zeros(len(idx), np.int32)
+    key_off[is_ix] = koff.astype(np.uint64)
+    keylen[is_ix] = klen.astype(np.int32)
+    regop = rectype == F.REC_TXN_REGOP
+    assert np.array_equal(lsns[regop], a.commit_lsn[c0:])
+    return LLog(lsns, rectype, prev, np.zeros(len(idx), np.int16), table, ix, key_off, keylen,
+                blob, list(a.tbnames), int(a.end_lsn))
 
 
 @dataclasses.dataclass
@@ -723,7 +798,8 @@ def zipf_keys(rng, n: int, s: float, key_bits: int) -> np.ndarray:
 def config5_scaled(seed: int = SEED_CONFIG5, keys_per_gpu: int = 125_000_000,
                    keys_per_commit: int = 10, n_txn: int = 100_000, ranges_per_txn: int = 10,
                    zipf_s: float = 1.2, key_bits: int = 32, snap_recent: float = 0.01,
-                   rank: int = 0, world: int = 1, window: bool = True) -> Config5Scaled:
+                   rank: int = 0, world: int = 1, window: bool = True,
+                   hot_frac: float = 0.03) -> Config5Scaled:
     """Config 5 (a 1B-key log window, Zipf s = 1.2 over 2^32
     keys, ranges as config 2 scaled), weak-scaled: ONE global Zipf(s) law over
     2^key_bits key values (hot keys are the small values, so a fixed split of
@@ -734,8 +810,8 @@ def config5_scaled(seed: int = SEED_CONFIG5, keys_per_gpu: int = 125_000_000,
     sampled global splitters (shard.sampled_splitters / exchange_rows).  The
     read sets are global: config 2's kind mix over the whole key space, range
     width scaled to the mean key density (about 10 logged writes per range),
-    half of the point ranges on Zipf-drawn hot keys.  window=False: another
-    batch of read sets over the same log (no rows)."""
+    a hot_frac share of the point ranges on Zipf-drawn hot keys.  window=False:
+    another batch of read sets over the same log (no rows)."""
     K = keys_per_commit
     R = K + 3
     n_commits = keys_per_gpu // K
@@ -752,7 +828,7 @@ def config5_scaled(seed: int = SEED_CONFIG5, keys_per_gpu: int = 125_000_000,
     width = max(1, int(round(10 * space / max(world * n_commits * K, 1))))
     kind = rng.choice(4, size=nr, p=[0.5, 0.4, 0.08, 0.02])
     v = rng.integers(0, space, size=nr, dtype=np.int64)
-    aim = np.nonzero((kind == 0) & (rng.random(nr) < 0.5))[0]
+    aim = np.nonzero((kind == 0) & (rng.random(nr) < hot_frac))[0]
     v[aim] = zipf_keys(rng, len(aim), zipf_s, key_bits)
     lo = F.enc_int64_array(v)
     hi = F.enc_int64_array(np.where(kind == 1, v + width, v))
@@ -790,19 +866,21 @@ def config5_scaled(seed: int = SEED_CONFIG5, keys_per_gpu: int = 125_000_000,
                               keys_per_commit=K))
 
 
-def config5_log(segments: Sequence[np.ndarray], keys_per_commit: int = 10) -> LLog:
+def config5_log(segments: Sequence[np.ndarray], keys_per_commit: int = 10,
+                from_commit: int = 0) -> LLog:
     """The global log of config5_scaled's per-rank key segments (rank r's
     commit c is global commit c * world + r): per commit ltran_start, one
     undo_upd_ix per key, ltran_commit, regop -- the LSNs config5_scaled gives
-    its rows and snapshots.  For oracle checks of small cases."""
+    its rows and snapshots -- from global commit `from_commit` on (a tail
+    serves read sets whose snapshots fall inside it).  For oracle checks."""
     world, K = len(segments), keys_per_commit
     R = K + 3
     n_commits = len(segments[0]) // K
     ncg = world * n_commits
     gkeys = np.stack([np.asarray(sg, np.int64).reshape(n_commits, K) for sg in segments], axis=1)
-    gkeys = gkeys.reshape(ncg * K)  # global commit order: (c, r) -> c * world + r
-    nrec = ncg * R
-    idx = np.arange(nrec, dtype=np.uint64)
+    gkeys = gkeys.reshape(ncg * K)[from_commit * K:]  # global commit order: (c, r) -> c * world + r
+    nrec = (ncg - from_commit) * R
+    idx = np.arange(nrec, dtype=np.uint64) + np.uint64(from_commit * R)
     lsns = lsn_of_index(idx)
     j = (idx % np.uint64(R)).astype(np.int64)
     rectype = np.full(nrec, F.REC_UNDO_UPD_IX, dtype=np.uint32)
@@ -814,11 +892,11 @@ def config5_log(segments: Sequence[np.ndarray], keys_per_commit: int = 10) -> LL
     prev[j == 0] = 0
     is_undo = (j >= 1) & (j <= K)
     key_off = np.zeros(nrec, dtype=np.uint64)
-    key_off[is_undo] = np.arange(ncg * K, dtype=np.uint64) * np.uint64(9)
+    key_off[is_undo] = np.arange((ncg - from_commit) * K, dtype=np.uint64) * np.uint64(9)
     return LLog(lsns, rectype, prev, np.zeros(nrec, np.int16),
                 np.where(is_undo, 0, -1).astype(np.int32), np.zeros(nrec, np.int16), key_off,
                 np.where(is_undo, 9, 0).astype(np.int32), F.enc_int64_array(gkeys).reshape(-1),
-                ["t1"], int(lsn_of_index(np.array([nrec]))[0]))
+                ["t1"], int(lsn_of_index(np.array([ncg * R]))[0]))
 
 
 def config5(seed: int = SEED_CONFIG5, n_commits: int = 100_000, keys_per_commit: int = 10,
