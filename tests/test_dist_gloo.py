@@ -211,6 +211,6 @@ def test_config5_sampled_splitters_match_oracle(tmp_path, oracle_mod):
     want, _, _ = oracle_mod.check(glog, segs[0].readsets, nthreads=8)
     np.testing.assert_array_equal(got != 0, want != 0)
     assert 0 < int((want != 0).sum()) < len(want)
-    assert st["fixed_span_est_max_over_mean"] > 1.4   # the skew is real (2.0 = all on one rank)
+    assert st["fixed_span_est_max_over_mean"] > 1.25  # the skew is real (2.0 = all on one rank)
     assert st["work_max_over_mean"] < 1.25            # and the splitters balance it
     assert "time_max_over_mean" in st
