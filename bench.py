@@ -596,10 +596,21 @@ def main():
                             n_txn=args.n_txn * world)
         for g, (tbn, ix, L) in enumerate(c3.groups):
             assert v.register_group(tbn, ix, L) == g
-        sizes = {g: int(n) for g, n in enumerate(np.bincount(c3.w_group, minlength=len(c3.groups)))}
-        gshards = shard.GroupShards(sizes, world)
-        mine = [g for g, r in gshards.owner.items() if r == rank]
-        gid, words, lsn = c3.window(mine)
+        gid, words, lsn = c3.window()
+        if world > 1:
+            # work per group from the rows and the first batch's ranges (every
+            # rank computes the same plan), hot groups cut into key-range pieces
+            hv = hsc.Validator(-1)
+            for g, (tbn, ix, L) in enumerate(c3.groups):
+                hv.register_group(tbn, ix, L)
+            hv.set_end(c3.end_lsn)
+            gshards = shard.group_work(gid, words, hv.marshal(c3.readsets), world)
+            hv.close()
+        else:
+            gshards = shard.group_work(gid, words, None, world)
+        sel = gshards.row_mask(gid, words, rank)
+        gid, words, lsn = gid[sel], np.ascontiguousarray(words[:, sel]), lsn[sel]
+        mine = sorted({g for g, _, _, r, _ in gshards.pieces if r == rank})
         end_lsn = c3.end_lsn
         first_rs = c3.readsets
         more_rs = lambda bi: config3_arrays(seed=SEED_CONFIG3, n_writes=args.c3_writes * world,
@@ -608,7 +619,7 @@ def main():
         workload = (f"config3: {len(c3.groups)} (table, index) groups of composite keys "
                     f"(9-64 B, log-normal sizes), {args.c3_writes} index writes and "
                     f"{args.n_txn} read sets per GPU (points, ranges, prefixes, table locks), "
-                    f"LPT group shards")
+                    f"LPT group shards, hot groups cut into key-range pieces")
         data = "synthetic (config 3 generator, seed 0xC0FFEE03, weak scaling per GPU)"
     elif args.config == 2:
         value_bits = 40
@@ -876,6 +887,12 @@ def main():
         out["config"]["parallelism"] = f"(table, index) group shards (LPT) x{world}" + (
             " + RCCL all-gather of verdict bitmaps" if world > 1 else "")
         out["config"]["groups_per_rank"] = len(mine)
+        out["imbalance"] = {"partition": "LPT over (table, index) groups by rows + "
+                                         f"{shard.RANGE_COST} x ranges; groups heavier than "
+                                         "total / (2N) cut into key-range pieces",
+                            "work_max_over_mean": gshards.imbalance(),
+                            "split_groups": sorted(gshards.split),
+                            "pieces": len(gshards.pieces)}
         if args.check and world == 1:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle

@@ -578,6 +578,18 @@ class Config3Arrays:
         return g.astype(np.uint32), words, lsn.copy()
 
 
+def config3_group_sizes(rng, n_groups: int, n_writes: int) -> np.ndarray:
+    """Log-normal group sizes of config 3 (the first draw of its generator)."""
+    w = rng.lognormal(0.0, 1.0, size=n_groups)
+    return np.maximum(1, (w / w.sum() * n_writes).astype(np.int64))
+
+
+def config3_group_keys(seed: int, g: int, n_ix: int, size: int, vmax: int) -> np.ndarray:
+    """Group g's distinct-row keys (each written once), from its own stream:
+    one group's keys can be drawn without the others'."""
+    return _enc_fields(np.random.default_rng([seed, 3, g]), INDEX_SHAPES[g % n_ix], size, vmax)
+
+
 def config3_arrays(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4,
                    n_writes: int = 200_000, keys_per_commit: int = 8, n_txn: int = 20_000,
                    ranges_per_txn: int = 10, vmax: int = 1 << 12, snap_recent: float = 0.01,
@@ -598,11 +610,8 @@ def config3_arrays(seed: int = SEED_CONFIG3, n_tables: int = 8, n_ix: int = 4,
     rng = np.random.default_rng(seed)
     tb = [f"t{i}" for i in range(n_tables)]
     G = n_tables * n_ix
-    w = rng.lognormal(0.0, 1.0, size=G)
-    gsize = np.maximum(1, (w / w.sum() * n_writes).astype(np.int64))
-    keys_of = []
-    for g in range(G):
-        keys_of.append(_enc_fields(rng, INDEX_SHAPES[g % n_ix], int(gsize[g]), vmax))
+    gsize = config3_group_sizes(rng, G, n_writes)
+    keys_of = [config3_group_keys(seed, g, n_ix, int(gsize[g]), vmax) for g in range(G)]
     gid = np.concatenate([np.full(int(gsize[g]), g) for g in range(G)])
     row = np.concatenate([np.arange(int(gsize[g])) for g in range(G)])
     perm = rng.permutation(len(gid))

@@ -1,7 +1,9 @@
-"""CPU, world_size 2 over gloo: the sharded check (comdb2_amd/shard.py) --
-marshal the global batch, route probes to key-range / group shards, evaluate
-each shard's probes against only that shard's window, merge verdict bytes
-with all_reduce(MAX) -- must equal the unsharded oracle verdicts."""
+"""CPU, world sizes 2, 4 and 8 over gloo: the sharded check
+(comdb2_amd/shard.py) -- marshal the global batch, route probes to key-range
+/ group shards, evaluate each shard's probes against only that shard's
+window, merge verdict bytes with all_reduce(MAX) -- must equal the unsharded
+oracle verdicts; configs 3 and 5 also report and bound the per-rank work
+imbalance (max / mean)."""
 import os
 import socket
 import sys
@@ -53,8 +55,8 @@ def _worker(rank, world, port, mode, out_path):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     v = Validator(-1)
-    if mode == "config5":
-        _config5_rank(rank, world, v, out_path)
+    if mode in ("config5", "config3"):
+        (_config5_rank if mode == "config5" else _config3_rank)(rank, world, v, out_path)
         dist.barrier()
         dist.destroy_process_group()
         v.close()
@@ -169,10 +171,55 @@ def _config5_rank(rank, world, v, out_path):
                       f)
 
 
-def _run(mode, tmp_path):
+C3_KW = dict(n_writes=120_000, n_txn=600)
+
+
+def _config3_rank(rank, world, v, out_path):
+    """Config 3 over `world` ranks: every rank builds the same plan
+    (shard.group_work + GroupShards: LPT over groups by rows + 3 x ranges,
+    hot groups cut into key-range pieces), keeps the rows of its pieces,
+    probes the ranges routed to them (oracle/sortjoin.c, the CPU stand-in for
+    the HIP join) and the verdicts are merged with all_reduce(MAX)."""
+    import json
+
+    import torch
+    import torch.distributed as dist
+
+    from comdb2_amd import shard
+    from comdb2_amd.workloads import config3_arrays
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    a = config3_arrays(**C3_KW)
+    gid, words, lsn = a.window()
+    for g, (tb, ix, L) in enumerate(a.groups):
+        assert v.register_group(tb, ix, L) == g
+    v.set_end(a.end_lsn)
+    m = v.marshal(a.readsets)
+    gs = shard.group_work(gid, words, m, world)
+    sel = gs.row_mask(gid, words, rank)
+    sub = shard.route(m, gs.range_mask(m, rank), gs.lock_mask(m, rank))
+    sj = oracle.SortJoin(gid[sel], np.ascontiguousarray(words[:, sel]), lsn[sel], len(a.groups))
+    verdict, _ = sj.probe(sub, a.table_max, nthreads=1)
+    sj.close()
+    t = torch.from_numpy(verdict.copy())
+    shard.merge_verdicts(t)
+    loc = torch.tensor([float(sel.sum()), float(sub["n"])], dtype=torch.float64)
+    allg = [torch.zeros_like(loc) for _ in range(world)]
+    dist.all_gather(allg, loc)
+    per = torch.stack(allg).numpy()
+    if rank == 0:
+        np.save(out_path, t.numpy())
+        work = per[:, 0] * shard.ROW_COST + per[:, 1] * shard.RANGE_COST
+        with open(out_path + ".json", "w") as f:
+            json.dump({"plan_max_over_mean": gs.imbalance(), "split_groups": sorted(gs.split),
+                       "rows_per_rank": per[:, 0].tolist(), "ranges_per_rank": per[:, 1].tolist(),
+                       "work_max_over_mean": float(work.max() / work.mean())}, f)
+
+
+def _run(mode, tmp_path, world=2):
     import torch.multiprocessing as mp
-    out = str(tmp_path / f"verdict_{mode}.npy")
-    mp.start_processes(_worker, args=(2, _free_port(), mode, out), nprocs=2, join=True,
+    out = str(tmp_path / f"verdict_{mode}_{world}.npy")
+    mp.start_processes(_worker, args=(world, _free_port(), mode, out), nprocs=world, join=True,
                        start_method="spawn")
     return np.load(out)
 
@@ -197,20 +244,70 @@ def test_group_shards_match_oracle(tmp_path, oracle_mod):
     np.testing.assert_array_equal(got != 0, want != 0)
 
 
-def test_config5_sampled_splitters_match_oracle(tmp_path, oracle_mod):
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_config5_sampled_splitters_match_oracle(tmp_path, oracle_mod, world):
     """one global Zipf(1.2) over 2^32 keys; sampled global
     splitters balance the shards (a fixed split would not) and the merged
     verdicts equal the oracle's over the global log."""
     import json
 
     from comdb2_amd.workloads import config5_log, config5_scaled
-    got = _run("config5", tmp_path)
-    st = json.load(open(str(tmp_path / "verdict_config5.npy") + ".json"))
-    segs = [config5_scaled(rank=r, world=2, **C5_KW) for r in range(2)]
+    got = _run("config5", tmp_path, world)
+    st = json.load(open(str(tmp_path / f"verdict_config5_{world}.npy") + ".json"))
+    segs = [config5_scaled(rank=r, world=world, **C5_KW) for r in range(world)]
     glog = config5_log([s.keys for s in segs])
     want, _, _ = oracle_mod.check(glog, segs[0].readsets, nthreads=8)
     np.testing.assert_array_equal(got != 0, want != 0)
     assert 0 < int((want != 0).sum()) < len(want)
-    assert st["fixed_span_est_max_over_mean"] > 1.25  # the skew is real (2.0 = all on one rank)
+    assert st["fixed_span_est_max_over_mean"] > 1.25  # the skew is real (world = all on one rank)
     assert st["work_max_over_mean"] < 1.25            # and the splitters balance it
     assert "time_max_over_mean" in st
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_config3_split_group_shards_match_oracle(tmp_path, oracle_mod, world):
+    """Config 3's (table, index) groups over 2 / 4 / 8 ranks: the merged
+    verdicts equal the log oracle's, and the planned and the routed work stay
+    balanced (max / mean <= 1.15) -- at 8 ranks only because the hot groups
+    are cut into key-range pieces (whole groups by LPT: 1.7)."""
+    import json
+
+    from comdb2_amd import shard
+    from comdb2_amd.workloads import config3_arrays, config3_log
+    got = _run("config3", tmp_path, world)
+    st = json.load(open(str(tmp_path / f"verdict_config3_{world}.npy") + ".json"))
+    a = config3_arrays(**C3_KW)
+    want, _, _ = oracle_mod.check(config3_log(a), a.readsets, nthreads=8)
+    np.testing.assert_array_equal(got != 0, want != 0)
+    assert 0 < int((want != 0).sum()) < len(want)
+    assert st["plan_max_over_mean"] <= 1.15, st
+    assert st["work_max_over_mean"] <= 1.15, st
+    if world == 8:
+        assert st["split_groups"], st
+        gid, _, _ = a.window()
+        whole = shard.GroupShards({g: float(n) for g, n in enumerate(np.bincount(gid))}, world)
+        assert whole.imbalance() > 1.3  # without splitting
+
+
+def test_config3_real_size_plan_balances_at_8():
+    """The plan at config 3's bench size for 8 GPUs (8 x 4M index writes, the
+    generator's group sizes; keys drawn only for the groups the plan cuts):
+    LPT over whole groups is capped by the largest group (max / mean 1.72);
+    with hot groups cut into key-range pieces it is <= 1.15."""
+    from comdb2_amd import shard
+    from comdb2_amd.workloads import SEED_CONFIG3, config3_group_keys, config3_group_sizes
+    n_ix = 4
+    sizes = config3_group_sizes(np.random.default_rng(SEED_CONFIG3), 8 * n_ix, 32_000_000)
+    W = 8
+
+    def keys_of(g):
+        kb = config3_group_keys(SEED_CONFIG3, g, n_ix, int(sizes[g]), 1 << 12)
+        pad = np.zeros((len(kb), 8 * W), np.uint8)
+        pad[:, :kb.shape[1]] = kb
+        words = pad.view(">u8").astype(np.uint64).reshape(len(kb), W).T
+        return words, np.ones(len(kb))
+    whole = shard.GroupShards({g: float(n) for g, n in enumerate(sizes)}, 8)
+    split = shard.plan_groups(sizes, None, 8, keys_of)
+    assert whole.imbalance() > 1.5
+    assert split.imbalance() <= 1.15, split.imbalance()
+    assert split.split
