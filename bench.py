@@ -58,25 +58,30 @@ def cpu_model():
     return platform.processor()
 
 
-def cpu_baseline(c2, gpu_verdict, threads, target_s, m0=None):
+def cpu_baseline(log, readsets, gpu_verdict, threads, target_s, m0=None, window=None,
+                 table_max=None, ngroups=1, log_note=""):
     """Oracle port of bdb_osql_serial_check (per-read-set log rescan, hash
     lookups, linear range scan, early exit) on a deterministic evenly spaced
     sample of the same batch, on `threads` pthreads and on one core; also
-    checks those verdicts against the GPU's.  With m0 (the marshalled batch)
-    adds the build's own CPU sort-join over the full batch (SURVEY.md §8(d)
-    second CPU line: same algorithm class as the GPU, on the host cores)."""
+    checks those verdicts against the GPU's.  `log` may be a tail of the log
+    that starts before the batch's oldest snapshot: a check only reads the
+    records after its snapshot (bdb/serializable.c:390-539), so the tail gives
+    the same verdicts and the same work.  With m0 (the marshalled batch) and
+    window (gid, words, lsn rows) adds the build's own CPU sort-join over the
+    full batch (SURVEY.md §8(d) second CPU line: same algorithm class as the
+    GPU, on the host cores)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
-    ol = oracle.OracleLog(c2.log)
-    T = c2.readsets.ntxn
+    ol = oracle.OracleLog(log)
+    T = readsets.ntxn
 
     def timed_sample(nthreads, budget_s):
         cal = np.arange(0, T, max(1, T // (8 * nthreads)))[: 8 * nthreads]
-        _, _, secs = oracle.check(ol, c2.readsets.subset(cal), nthreads=nthreads)
+        _, _, secs = oracle.check(ol, readsets.subset(cal), nthreads=nthreads)
         rate = len(cal) / max(secs, 1e-6)
         n = int(min(T, max(len(cal), rate * budget_s)))
         sample = np.unique(np.linspace(0, T - 1, n).astype(np.int64))
-        rc, _, secs = oracle.check(ol, c2.readsets.subset(sample), nthreads=nthreads)
+        rc, _, secs = oracle.check(ol, readsets.subset(sample), nthreads=nthreads)
         ok = bool(np.array_equal(rc != 0, gpu_verdict[sample] != 0))
         return sample, secs, ok
 
@@ -85,16 +90,17 @@ def cpu_baseline(c2, gpu_verdict, threads, target_s, m0=None):
     out = dict(value=len(sample) / secs, unit="checks/s", cores=threads, kind="port",
                sample=f"{len(sample)} of {T} read sets (evenly spaced, 1 in {step:.1f}), "
                       f"oracle/serial_oracle.c restatement of bdb_osql_serial_check over the "
-                      f"{c2.log.nrec}-record log, {threads} pthreads, {secs:.1f} s; cpu: {cpu_model()}",
+                      f"{log.nrec}-record log{log_note}, {threads} pthreads, {secs:.1f} s; "
+                      f"cpu: {cpu_model()}",
                parity_with_gpu=ok)
     s1, secs1, ok1 = timed_sample(1, max(2.0, target_s / 3))
     out["single_core"] = dict(value=len(s1) / secs1, unit="checks/s", cores=1,
                               sample=f"{len(s1)} read sets, {secs1:.1f} s", parity_with_gpu=ok1)
-    if m0 is not None:
-        from comdb2_amd.workloads import config2_device_window
-        gid, words, lsn = config2_device_window(c2)
-        sj = oracle.SortJoin(gid, words, lsn, 1)
-        table_max = np.array([lsn.max() if len(lsn) else 0], np.uint64)  # one table (t1)
+    if m0 is not None and window is not None:
+        gid, words, lsn = window
+        sj = oracle.SortJoin(gid, words, lsn, ngroups)
+        if table_max is None:
+            table_max = np.array([lsn.max() if len(lsn) else 0], np.uint64)  # one table (t1)
         res = {}
         for nt in (threads, 1):
             verdict, secs_sj = sj.probe(m0, table_max, nthreads=nt)
@@ -112,6 +118,16 @@ def cpu_baseline(c2, gpu_verdict, threads, target_s, m0=None):
                    f"oracle/sortjoin.c")
         sj.close()
     return out
+
+
+def log_tail_commit(commit_lsn, snaps):
+    """First commit of the log tail a batch's checks read: the commit whose
+    regop is the oldest snapshot (or the one before it)."""
+    s = int(np.min(snaps))
+    c0 = int(np.searchsorted(commit_lsn, s))
+    if c0 >= len(commit_lsn) or int(commit_lsn[c0]) != s:
+        c0 = max(0, c0 - 1)
+    return c0
 
 
 def bench_commit_stream(args):
@@ -189,6 +205,7 @@ def bench_commit_stream(args):
            "append_us_per_commit": {"mean": float(ta.mean() * 1e6), "p50": float(np.median(ta) * 1e6),
                                     "p99": float(np.percentile(ta, 99) * 1e6)},
            "stream_wall_s": wall, "parity_with_oracle_golden": parity,
+           "cpu_baseline": None if args.no_cpu else commit_stream_cpu_baseline(args),
            "note": "value = commits / (time inside the check and append calls); the wall time "
                    "also holds the Python log builder that stands in for comdb2's logging"}
     print(json.dumps(out), flush=True)
@@ -277,22 +294,67 @@ def bench_graph(args):
         print(json.dumps(out), flush=True)
 
 
-def graph_cpu_baseline(args):
-    """oracle/scc_oracle.c (Adya edges + Tarjan, one core) on a smaller
-    history of the same generator, sized to finish in seconds."""
+def graph_cpu_baseline(args, threads=None):
+    """oracle/scc_oracle.c (Adya edges + Tarjan) on histories of the same
+    generator, sized to finish in seconds: one history on one core, and on
+    every host CPU at once (one independent history per thread -- Tarjan is
+    sequential, so the box's throughput is the per-core work side by side;
+    ctypes drops the GIL inside the C calls)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from comdb2_amd.workloads import config4_history
-    sys.path.insert(0, ROOT)
-    from oracle import oracle as O
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
     n = max(1000, min(args.history_txns, 1_000_000))
-    h = config4_history(n_txn=n, n_keys=args.c4_keys or max(1000, n // 10),
-                        concurrent_frac=args.c4_concurrent, max_lag=args.c4_max_lag)
+    mk = lambda seed: config4_history(seed=seed, n_txn=n, n_keys=args.c4_keys or max(1000, n // 10),
+                                      concurrent_frac=args.c4_concurrent, max_lag=args.c4_max_lag)
+
+    def run(h):
+        t0 = time.perf_counter()
+        s_, d_, _ = O.dep_edges(h.txn, h.key, h.is_write, h.observed)
+        O.scc(h.ntxn, s_, d_)
+        return h.nops, time.perf_counter() - t0
+    h = mk(0xC0FFEE04)
+    ops1, dt1 = run(h)
+    threads = threads or box_cpus()["threads"]
+    hs = [mk(0xC0FFEE04 + i) for i in range(threads)]
     t0 = time.perf_counter()
-    s_, d_, _ = O.dep_edges(h.txn, h.key, h.is_write, h.observed)
-    O.scc(h.ntxn, s_, d_)
-    dt = time.perf_counter() - t0
-    return {"value": h.nops / dt, "unit": "ops/s", "cores": 1, "kind": "port",
-            "sample": f"{h.ntxn} txns / {h.nops} ops of the config-4 generator, "
-                      f"oracle/scc_oracle.c edges + Tarjan, {dt:.1f} s"}
+    with ThreadPoolExecutor(threads) as ex:
+        res = list(ex.map(run, hs))
+    wall = time.perf_counter() - t0
+    tot = sum(r[0] for r in res)
+    return {"value": tot / wall, "unit": "ops/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} independent histories of {n} txns (~{h.nops} ops each) of the "
+                      f"config-4 generator, oracle/scc_oracle.c edges + Tarjan, one per thread, "
+                      f"{wall:.1f} s wall; cpu: {cpu_model()}",
+            "single_core": {"value": ops1 / dt1, "unit": "ops/s", "cores": 1,
+                            "sample": f"{h.ntxn} txns / {ops1} ops, {dt1:.1f} s"}}
+
+
+def commit_stream_cpu_baseline(args):
+    """Config 1 on the host: the oracle (oracle/serial_oracle.c, the
+    reference algorithm: per check a log rescan from the snapshot, chain walks,
+    range scans) replayed over a bounded stream of the same generator -- each
+    commit checked against the whole log so far, passing txns logged -- timing
+    only the checks (the Python log builder stands in for comdb2's logging)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    from comdb2_amd.workloads import SEED_CONFIG1, config1_events, replay
+    n = min(args.n_txn_c1, 2000)
+    acc = [0.0, 0]
+
+    def chk(log, rs):
+        rc, _, secs = oracle.check(log, rs)
+        acc[0] += secs
+        acc[1] += 1
+        return rc
+    replay(config1_events(seed=SEED_CONFIG1, n_txn=n), chk)
+    return {"value": acc[1] / acc[0], "unit": "commits/s", "cores": 1, "kind": "port",
+            "sample": f"the first {n}-txn stream of the config-1 generator ({acc[1]} checks, "
+                      f"{acc[0]:.2f} s inside the checks), one core: the reference checks one "
+                      f"commit at a time under commit_lock (db/toblock.c:4757-4836); "
+                      f"cpu: {cpu_model()}"}
 
 
 def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0, bitmap=False):
@@ -444,8 +506,9 @@ PROBE_KERNELS = ("k_locate_t", "k_plan_t", "k_plan_s", "k_scatter_t", "k_join_t"
 
 def pmc_traffic(args):
     """HBM bytes per probe batch from rocprofv3 PMC passes of this same
-    workload (`bench.py --pmc-child`: the window and the first ring batch,
-    probed on one stream), one pass per counter as MI355X_MICROARCH.md
+    workload (`bench.py --pmc-child`: the window and the same ring of distinct
+    batches as the timed loop, each probed once, rotating over the same
+    streams), one pass per counter as MI355X_MICROARCH.md
     prescribes (FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2).  FETCH_SIZE /
     WRITE_SIZE are KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide
     coalesced read, so read bytes = 2 x 1024 x FETCH_SIZE, write bytes = 1024 x
@@ -456,7 +519,8 @@ def pmc_traffic(args):
     import shutil
     import tempfile
     out = {"kind": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --pmc-child "
-                   "(same window and batch shape, one stream)", "kernels": {}}
+                   "(same window, the timed loop's ring of batches and streams; per-kernel "
+                   "means over the ring's launches)", "kernels": {}}
     per = {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="hsc_pmc_")
@@ -464,7 +528,8 @@ def pmc_traffic(args):
                "csv", "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__),
                "--pmc-child", "--config", str(args.config), "--n-commits", str(args.n_commits),
                "--n-txn", str(args.n_txn), "--c3-writes", str(args.c3_writes),
-               "--c5-keys", str(args.c5_keys)] + (["--compact-wide"] if args.compact_wide else [])
+               "--c5-keys", str(args.c5_keys), "--ring-gb", str(args.ring_gb),
+               "--streams", str(args.streams)] + (["--compact-wide"] if args.compact_wide else [])
         print(f"[bench] pmc pass {ctr}", file=sys.stderr, flush=True)
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
@@ -545,7 +610,7 @@ def main():
     ap.add_argument("--c4-keys", type=int, default=0, help="config 4: keys (0: txns / 10)")
     args = ap.parse_args()
     if args.ring_gb is None:
-        args.ring_gb = 1.1 if args.config in (2, 3, 5) and not args.pmc_child else 0.0
+        args.ring_gb = 1.1 if args.config in (2, 3, 5) else 0.0
 
     if args.config == 4:
         return bench_graph(args)
@@ -578,7 +643,7 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    want_cpu = (rank == 0 and world == 1 and not args.no_cpu and args.config == 2
+    want_cpu = (rank == 0 and world == 1 and not args.no_cpu and args.config in (2, 3, 5)
                 and not args.pmc_child)
     batches = []
     v = hsc.Validator(local)
@@ -659,7 +724,7 @@ def main():
         make_shards = lambda W: shard.KeyRangeShards.int64_splitters(c5_split["splitters"], W)
         workload = (f"config5: one global Zipf(1.2) law over 2^32 keys, {args.c5_keys} logged "
                     f"writes per GPU (hot keys collapse under dedupe), sampled global splitters, "
-                    f"100k read sets x 10 ranges per GPU (width {c5.params['width']}, half the "
+                    f"100k read sets x 10 ranges per GPU (width {c5.params['width']}, 3 % of the "
                     f"points on Zipf-drawn hot keys)")
         data = "synthetic (config 5 generator, seed 0xC0FFEE05, weak scaling per GPU)"
     n_w = len(lsn)
@@ -679,7 +744,7 @@ def main():
     m0 = None
     ring_bytes = 0
     bi = 0
-    nb_min = 2 if args.pmc_child else max(2, args.batches)
+    nb_min = max(2, args.batches)
     while bi < nb_min or ring_bytes < args.ring_gb * 1e9:
         rs = first_rs if bi == 0 else more_rs(bi)
         m = v.marshal(rs)
@@ -711,9 +776,10 @@ def main():
                 for si in range(S)] for b in batches]
     torch.cuda.synchronize()
 
-    if args.pmc_child:  # profiled by the parent's rocprofv3 --pmc pass: batch 0, one stream
-        for k in range(10):
-            v.probe_device(structs[0][0])
+    if args.pmc_child:  # profiled by the parent's rocprofv3 --pmc pass: the ring, S streams
+        for k in range(len(batches)):
+            v.set_stream(streams[k % S].cuda_stream)
+            v.probe_device(structs[k][k % S])
         v.synchronize()
         v.close()
         return
@@ -851,6 +917,11 @@ def main():
             "frac": frac(elapsed),
             "frac_1stream": frac(serial_elapsed),
             "traffic": traffic.get("bytes_per_batch") if traffic else None,
+            # the same time against the PMC-measured bytes (FETCH_SIZE counts
+            # Infinity-Cache hits too): how much of HBM's peak the probe phase
+            # actually moves; frac above is the algorithmic-bytes roofline
+            "measured_frac": (traffic["bytes_per_batch"] / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS
+                              if traffic and traffic.get("bytes_per_batch") else None),
             "algorithmic_bytes": B,
             "avg_ms": ms_per_step,
             "working_set": {
@@ -942,7 +1013,26 @@ def main():
         cpus = box_cpus()
         threads = args.cpu_threads or cpus["threads"]
         print(f"[bench] cpu baseline on {threads} threads ({cpus})", file=sys.stderr, flush=True)
-        out["cpu_baseline"] = cpu_baseline(c2, v0, threads, args.cpu_seconds, m0=m0)
+        if args.config == 2:
+            out["cpu_baseline"] = cpu_baseline(c2.log, c2.readsets, v0, threads, args.cpu_seconds,
+                                               m0=m0, window=config2_device_window(c2))
+        elif args.config == 3:
+            from comdb2_amd.workloads import config3_log
+            c0 = log_tail_commit(c3.commit_lsn, first_rs.snap)
+            out["cpu_baseline"] = cpu_baseline(
+                config3_log(c3, from_commit=c0), first_rs, v0, threads, args.cpu_seconds, m0=m0,
+                window=(gid, words, lsn), table_max=c3.table_max, ngroups=len(c3.groups),
+                log_note=f" (the tail from commit {c0} of {len(c3.commit_lsn)}: every record "
+                         f"after the batch's oldest snapshot)")
+        else:
+            from comdb2_amd.workloads import config5_log
+            K5 = c5.params["keys_per_commit"]
+            c0 = log_tail_commit(c5.lsn[K5 - 1::K5], first_rs.snap)
+            out["cpu_baseline"] = cpu_baseline(
+                config5_log([c5.keys], keys_per_commit=K5, from_commit=c0), first_rs, v0,
+                threads, args.cpu_seconds, m0=m0, window=(gid, words, lsn),
+                log_note=f" (the tail from commit {c0} of {len(c5.lsn) // K5}: every record "
+                         f"after the batch's oldest snapshot)")
         out["cpu_baseline"]["host"] = cpus
     if rank == 0:
         print(json.dumps(out), flush=True)
