@@ -20,36 +20,6 @@ namespace hsc {
 
 namespace {
 
-// (gid, words) of row i of a [W][stride] SoA against (g, key words)
-__device__ __forceinline__ int row_cmp(const uint32_t *gid, const uint64_t *words, size_t stride,
-                                       int W, uint32_t i, uint32_t g, const uint64_t *key,
-                                       size_t kstride)
-{
-    const uint32_t rg = gid[i];
-    if (rg != g) return rg < g ? -1 : 1;
-    for (int j = 0; j < W; ++j) {
-        const uint64_t a = words[(size_t)j * stride + i], b = key[(size_t)j * kstride];
-        if (a != b) return a < b ? -1 : 1;
-    }
-    return 0;
-}
-
-// #rows of d < key (strict = true) or <= key (strict = false)
-__device__ __forceinline__ uint32_t delta_count(const DeltaView &d, uint32_t g, const uint64_t *key,
-                                                size_t kstride, bool strict)
-{
-    uint32_t lo = 0, hi = d.n;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        const int c = row_cmp(d.gid, d.words, d.stride, d.W, mid, g, key, kstride);
-        if (c < 0 || (!strict && c == 0))
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    return lo;
-}
-
 // out = merge of the delta (d.n rows) and the appended rows a (a.n rows,
 // sorted), stable: equal keys keep delta rows first.  One thread per row.
 __global__ void k_delta_merge(DeltaView d, DeltaView a, uint32_t *ogid, uint64_t *owords,
@@ -101,17 +71,7 @@ __global__ __launch_bounds__(256) void k_probe_delta(DeltaView d, ProbeView p, u
 {
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= p.n) return;
-    const uint32_t g = p.gid[q];
-    const uint32_t pa = delta_count(d, g, p.lo + q, p.n, true);
-    const uint32_t pb = delta_count(d, g, p.hi + q, p.n, false);
-    if (pa >= pb) return;
-    const uint64_t s = p.snap[q];
-    bool hit = false;
-    uint32_t i = pa;
-    for (; i < pb && (i & 63) && !hit; ++i) hit = d.lsn[i] > s;  // to a block boundary
-    for (; i + 64 <= pb && !hit; i += 64) hit = d.bmax[i >> 6] > s;
-    for (; i < pb && !hit; ++i) hit = d.lsn[i] > s;
-    if (hit) flags[p.txn[q]] = 1;
+    if (delta_hit(d, p, q)) flags[p.txn[q]] = 1;
 }
 
 }  // namespace

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -50,17 +51,26 @@ inline uint64_t ixkey(int tid, int ix) { return ((uint64_t)(uint32_t)tid << 32) 
 // one.  Grows, never shrinks.
 struct HBuf {
     void *p = nullptr;
+    void *dp = nullptr;  // coherent buffers: the device's address of p
     size_t bytes = 0;
-    bool pinned = false;
-    // 0 or -1 (out of memory)
-    int ensure(size_t want, bool pin)
+    bool pinned = false, coherent = false;
+    // 0 or -1 (out of memory).  coherent: fine-grained pinned memory the GPU
+    // maps (kernels read and write it directly, the host sees their
+    // system-scope stores while they run).
+    int ensure(size_t want, bool pin, bool coh = false)
     {
-        if (want <= bytes && pin == pinned) return 0;
+        if (want <= bytes && pin == pinned && coh == coherent) return 0;
         release();
         const size_t b = want + want / 8 + 256;
         if (pin) {
-            if (hipHostMalloc(&p, b, hipHostMallocDefault) != hipSuccess) {
+            const unsigned flags = coh ? hipHostMallocMapped | hipHostMallocCoherent : hipHostMallocDefault;
+            if (hipHostMalloc(&p, b, flags) != hipSuccess) {
                 p = nullptr;
+                return -1;
+            }
+            if (coh && hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) {
+                (void)hipHostFree(p);
+                p = dp = nullptr;
                 return -1;
             }
         } else if (!(p = malloc(b))) {
@@ -68,6 +78,7 @@ struct HBuf {
         }
         bytes = b;
         pinned = pin;
+        coherent = coh && pin;
         return 0;
     }
     void release()
@@ -78,7 +89,7 @@ struct HBuf {
             else
                 free(p);
         }
-        p = nullptr;
+        p = dp = nullptr;
         bytes = 0;
     }
     template <class T> T *as() const { return (T *)p; }
@@ -293,6 +304,14 @@ struct hsc_ctx {
     Lane lanes[kLanes];
     int lane = 0;
     uint64_t lane_tick = 0;
+
+    // small batches (k_small_narrow): probe columns, verdict bytes and the
+    // done word in fine-grained pinned memory; the kernel's block counter
+    HBuf small_io;
+    DBuf small_blocks;
+    bool small_blocks_zeroed = false;
+    bool no_small = false;  // HSC_NO_SMALL=1 at context creation: the staged path
+    uint32_t small_seq = 0;
 
     // timing
     bool timing = false;
@@ -2223,6 +2242,79 @@ static int finish_stage(hsc_ctx *c, Stage &st, int *rc_out)
     return HSC_OK;
 }
 
+// Small batches (a lone bdb_osql_serial_check, a collector's batch): one
+// k_small_narrow launch reads the marshalled columns from fine-grained pinned
+// memory and writes the verdict bytes into it, and the host polls the
+// kernel's done word -- no copies, no event (the per-call
+// latency db/toblock.c:4779-4836 sees).  Narrow windows (the direct probe's
+// key and max trees); HSC_NO_SMALL=1 turns it off.
+constexpr int kSmallMaxTxns = 1024;
+constexpr size_t kSmallMaxRanges = 16384;
+
+static bool small_path(hsc_ctx *c, int T)
+{
+    return !c->no_small && c->narrow && !c->timing && T <= kSmallMaxTxns && c->n > 0;
+}
+
+static int run_small(hsc_ctx *c, Stage &st, int *rc_out)
+{
+    const size_t vo = (st.L.total + 63) & ~(size_t)63;
+    const size_t dn = (vo + st.n_txn + 63) & ~(size_t)63;
+    if (c->small_io.ensure(dn + 64, true, true)) return fail(c, HSC_ENOMEM, "small-batch staging");
+    HIPCHK(c, c->small_blocks.ensure(64));
+    hipStream_t s = c->stream;
+    if (!c->small_blocks_zeroed) {
+        HIPCHK(c, hipMemsetAsync(c->small_blocks.p, 0, 64, s));
+        c->small_blocks_zeroed = true;
+    }
+    uint8_t *io = c->small_io.as<uint8_t>(), *dio = (uint8_t *)c->small_io.dp;
+    if (st.L.total) memcpy(io, st.arena.p, st.L.total);
+    memset(io + vo, 0, st.n_txn);
+    volatile uint32_t *done = (volatile uint32_t *)(io + dn);
+    if (++c->small_seq == 0) c->small_seq = 1;
+    const uint32_t seq = c->small_seq;
+    *done = 0;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    ProbeView p{};
+    p.lo = (const uint64_t *)(dio + st.L.lo);
+    p.hi = (const uint64_t *)(dio + st.L.hi);
+    p.gid = (const uint32_t *)(dio + st.L.gid);
+    p.snap = (const uint64_t *)(dio + st.L.snap);
+    p.txn = (const uint32_t *)(dio + st.L.txn);
+    p.lock_table = (const uint32_t *)(dio + st.L.lock_table);
+    p.lock_snap = (const uint64_t *)(dio + st.L.lock_snap);
+    p.lock_txn = (const uint32_t *)(dio + st.L.lock_txn);
+    p.n = (uint32_t)st.n;
+    p.n_lock = (uint32_t)st.n_lock;
+    NarrowView nv = c->nv;
+    nv.table_max = c->d_table_max.as<uint64_t>();
+    nv.ntables = (uint32_t)c->table_names.size();
+    DeltaView d{};
+    if (c->dn) d = delta_view(c);
+    HIPCHK(c, launch_small_narrow(nv, d, p, dio + vo, c->small_blocks.as<uint32_t>(),
+                                  (uint32_t *)(dio + dn), seq, s));
+    // poll the done word; every few thousand spins ask the stream whether it
+    // failed (a fault never releases the word)
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 1; *done != seq; ++spin) {
+        __builtin_ia32_pause();
+        if ((spin & 4095) == 0) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
+                return fail(c, HSC_EDEVICE, "small batch did not finish within 30 s");
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipSuccess) {
+                if (*done != seq) return fail(c, HSC_EDEVICE, "small batch finished without its done word");
+                break;
+            }
+            if (e != hipErrorNotReady) return fail(c, HSC_EDEVICE, "small batch", e);
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const uint8_t *f = st.forced.as<uint8_t>(), *v = io + vo;
+    for (size_t t = 0; t < st.n_txn; ++t) rc_out[t] = (f[t] | v[t]) ? 1 : 0;
+    return HSC_OK;
+}
+
 // Full checks of every read set of src: marshal (host threads) -> upload ->
 // join -> download.  A large batch runs as a pipeline of chunks over the two
 // staging sets: chunk i + 1 is marshalled on the host while chunk i is
@@ -2234,6 +2326,16 @@ static int check_src(hsc_ctx *c, const Src &src, int *rc_out)
     const int T = src.ntxn();
     const int nchunks = T >= 2 * kPipeTxns ? (T + kPipeTxns - 1) / kPipeTxns : 1;
     const int per = std::max(1, (T + nchunks - 1) / nchunks);
+    if (nchunks == 1 && small_path(c, T)) {
+        Stage &st = c->stage[0];
+        int rc = marshal_into(c, src, 0, T, st);
+        if (rc == HSC_OK && st.n <= kSmallMaxRanges && st.n_lock <= kSmallMaxRanges)
+            return run_small(c, st, rc_out);
+        if (rc == HSC_OK) rc = launch_stage(c, st);
+        if (rc == HSC_OK) rc = finish_stage(c, st, rc_out);
+        if (rc != HSC_OK) (void)hipStreamSynchronize(c->stream);
+        return rc;
+    }
     int pending[2] = {-1, -1};
     int rc = HSC_OK;
     for (int i = 0; i < nchunks && rc == HSC_OK; ++i) {
@@ -2287,6 +2389,7 @@ int hsc_ctx_create(int device, hsc_ctx **out)
     if (!c) return HSC_ENOMEM;
     c->device = device;
     c->threads = default_threads();
+    c->no_small = getenv("HSC_NO_SMALL") && atoi(getenv("HSC_NO_SMALL")) != 0;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return HSC_EDEVICE;
@@ -2322,6 +2425,8 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->w_tcode2, &c->w_trecs};
     for (DBuf *b : bufs) b->release();
     for (Stage &st : c->stage) st.release();
+    c->small_io.release();
+    c->small_blocks.release();
     for (DBuf *b : {&c->d_dgid[0], &c->d_dgid[1], &c->d_dwords[0], &c->d_dwords[1], &c->d_dlsn[0],
                     &c->d_dlsn[1], &c->d_dbmax, &c->d_agid, &c->d_awords, &c->d_alsn})
         b->release();

@@ -203,6 +203,12 @@ hipError_t launch_probe_narrow(const NarrowView &nv, const ProbeView &p, uint8_t
                                hipStream_t s);
 hipError_t narrow_codes(const NarrowView &nv, const ProbeView &p, uint64_t *lo64, uint64_t *hi64,
                         hipStream_t s);
+// The small-batch form (one launch: ranges, delta run, locks; inputs and
+// verdicts in host-mapped memory; the last block releases seq into *done).
+struct DeltaView;
+hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const ProbeView &p,
+                               uint8_t *verdict, uint32_t *blocks_done, uint32_t *done,
+                               uint32_t seq, hipStream_t s);
 // 16-ary directory over a sorted u64 array A (hsc_narrow.hip): level 0 = A
 // padded with ~0 to a multiple of 16, level l+1 [i] = level l [16 i + 15]
 // (the last entry of every 16-entry block), up to one block; levels >=

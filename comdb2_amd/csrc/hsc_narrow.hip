@@ -215,22 +215,19 @@ hipError_t narrow_build(const WinView &w, const NarrowView &nv, hipStream_t s)
 constexpr int kProbeThreads = 256;
 constexpr int kNP = 4;  // ranges per 16-lane group in flight
 
-__global__ __launch_bounds__(kProbeThreads) void k_probe_narrow(NarrowView nv, ProbeView p,
-                                                                uint8_t *verdict)
+// The ranges of p answered by 16-lane groups, kNP ranges each: wave w of the
+// grid starts at range wave0 and strides by wstride.  Levels >= lds_from are
+// read from top (LDS, lds_base = their offset), the rest from the window.
+__device__ __forceinline__ void narrow_probe_ranges(const NarrowView &nv, const ProbeView &p,
+                                                    uint8_t *verdict, const uint64_t *top,
+                                                    uint64_t lds_base, int lds_from,
+                                                    uint32_t wave0, uint32_t wstride)
 {
-    extern __shared__ __attribute__((aligned(16))) uint64_t top[];  // levels >= lds_from
-    const uint64_t lds_base = nv.off[nv.lds_from];
-    for (uint32_t i = threadIdx.x; i < nv.lds_entries; i += kProbeThreads)
-        top[i] = nv.keys[lds_base + i];
-    __syncthreads();
-
     const int lane = threadIdx.x & 63;
     const int sub = lane >> 4, l16 = lane & 15;
-    const uint32_t groups = gridDim.x * (kProbeThreads / 16);
     const size_t ks = p.n;
     // every wave runs the same number of iterations (ballots need all lanes)
-    const uint32_t wave0 = (blockIdx.x * (kProbeThreads / 16) + ((threadIdx.x >> 6) << 2)) * kNP;
-    for (uint32_t wbase = wave0; wbase < p.n; wbase += groups * kNP) {
+    for (uint32_t wbase = wave0; wbase < p.n; wbase += wstride) {
         const uint32_t base = wbase + sub * kNP;
         // lane k < kNP of the group maps range base + k to codes
         uint64_t mlo = kSat, mhi = 0, msnap = 0;
@@ -273,7 +270,7 @@ __global__ __launch_bounds__(kProbeThreads) void k_probe_narrow(NarrowView nv, P
         for (int j = 0; j < 2 * kNP; ++j) c[j] = 0;
         for (int l = nv.levels - 1; l >= 0; --l) {
             uint64_t e[2 * kNP];
-            if (l >= nv.lds_from) {
+            if (l >= lds_from) {
                 const uint64_t *lv = top + (nv.off[l] - lds_base);
 #pragma unroll
                 for (int j = 0; j < 2 * kNP; ++j) e[j] = lv[16 * c[j] + l16];
@@ -331,12 +328,78 @@ __global__ __launch_bounds__(kProbeThreads) void k_probe_narrow(NarrowView nv, P
                 if (found[k]) verdict[txn[k]] = 1;
         }
     }
-    // table locks: any write to a locked table after the snapshot
-    for (uint32_t q = blockIdx.x * kProbeThreads + threadIdx.x; q < p.n_lock;
-         q += gridDim.x * kProbeThreads) {
+}
+
+// table locks q = first, first + stride, ...: any write to a locked table
+// after the snapshot
+__device__ __forceinline__ void narrow_probe_locks(const NarrowView &nv, const ProbeView &p,
+                                                   uint8_t *verdict, uint32_t first, uint32_t stride)
+{
+    for (uint32_t q = first; q < p.n_lock; q += stride) {
         const uint32_t t = p.lock_table[q];
         if (t < nv.ntables && nv.table_max[t] > p.lock_snap[q]) verdict[p.lock_txn[q]] = 1;
     }
+}
+
+__global__ __launch_bounds__(kProbeThreads) void k_probe_narrow(NarrowView nv, ProbeView p,
+                                                                uint8_t *verdict)
+{
+    extern __shared__ __attribute__((aligned(16))) uint64_t top[];  // levels >= lds_from
+    const uint64_t lds_base = nv.off[nv.lds_from];
+    for (uint32_t i = threadIdx.x; i < nv.lds_entries; i += kProbeThreads)
+        top[i] = nv.keys[lds_base + i];
+    __syncthreads();
+    const uint32_t groups = gridDim.x * (kProbeThreads / 16);
+    const uint32_t wave0 = (blockIdx.x * (kProbeThreads / 16) + ((threadIdx.x >> 6) << 2)) * kNP;
+    narrow_probe_ranges(nv, p, verdict, top, lds_base, nv.lds_from, wave0, groups * kNP);
+    narrow_probe_locks(nv, p, verdict, blockIdx.x * kProbeThreads + threadIdx.x,
+                       gridDim.x * kProbeThreads);
+}
+
+// Small batches of the drop-in entry (a lone bdb_osql_serial_check, a
+// collector's batch of concurrent calls): one launch answers the ranges from
+// the key and max trees (no LDS staging: a handful of searches would not pay
+// for it), the delta run and the table locks.  The probe columns are read
+// straight from the caller's pinned staging and the verdict bytes written into
+// it (fine-grained host memory the GPU maps: no copies); the last block to
+// finish releases `seq` into *done at system scope, which the host polls.
+constexpr int kSmallThreads = 256;
+
+__global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, DeltaView d,
+                                                                ProbeView p, uint8_t *verdict,
+                                                                uint32_t *blocks_done,
+                                                                uint32_t *done, uint32_t seq)
+{
+    const uint32_t groups = gridDim.x * (kSmallThreads / 16);
+    const uint32_t wave0 = (blockIdx.x * (kSmallThreads / 16) + ((threadIdx.x >> 6) << 2)) * kNP;
+    narrow_probe_ranges(nv, p, verdict, nullptr, 0, nv.levels, wave0, groups * kNP);
+    const uint32_t tid = blockIdx.x * kSmallThreads + threadIdx.x, nth = gridDim.x * kSmallThreads;
+    if (d.n)
+        for (uint32_t q = tid; q < p.n; q += nth)
+            if (delta_hit(d, p, q)) verdict[p.txn[q]] = 1;
+    narrow_probe_locks(nv, p, verdict, tid, nth);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();  // this block's verdict bytes reach the host first
+        if (atomicAdd(blocks_done, 1u) == gridDim.x - 1) {
+            *blocks_done = 0;  // the next launch on the stream counts from zero
+            __threadfence_system();
+            __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
+hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const ProbeView &p,
+                               uint8_t *verdict, uint32_t *blocks_done, uint32_t *done,
+                               uint32_t seq, hipStream_t s)
+{
+    // one pass of kNP ranges per 16-lane group, at most one block per CU
+    const size_t per_block = (kSmallThreads / 16) * kNP;
+    const size_t work = std::max<size_t>({(p.n + per_block - 1) / per_block,
+                                          (p.n_lock + kSmallThreads - 1) / kSmallThreads, 1});
+    k_small_narrow<<<(unsigned)std::min<size_t>(work, 256), kSmallThreads, 0, s>>>(
+        nv, d, p, verdict, blocks_done, done, seq);
+    return hipGetLastError();
 }
 
 hipError_t launch_probe_narrow(const NarrowView &nv, const ProbeView &p, uint8_t *verdict,
