@@ -141,6 +141,7 @@ struct Stage {
 };
 
 constexpr int kMarshalTxns = 2048;         // read sets per marshal work item
+constexpr size_t kTailPackMax = 1u << 18;  // fused join: verdict bytes by its last block up to this
 constexpr int kMarshalParallelMin = 4096;  // fewer read sets: marshal on the caller's thread
 constexpr int kPipeTxns = 32768;           // read sets per pipeline chunk of a large batch
 
@@ -233,6 +234,7 @@ struct hsc_ctx {
     uint64_t commit_span[2] = {0, 0};  // oldest / newest distinct commit LSN of the window
     bool rank_lsn32 = false;   // narrow tiles: rows carry lsn - rank_base + 1 (NarrowTiles)
     bool nt_sorted = true;     // narrow tiles: chunk-sorted records (HSC_NT_SORT=0 at build: scatter)
+    bool nt_fused = true;      // chunk-sorted narrow tiles: plan-free join (HSC_NT_FUSED=0 at build: plan + join)
     bool ct_sorted = true;     // compact tiles: chunk-sorted records (HSC_CT_SORT=0 at build: scatter)
     uint64_t rank_base = 0;
     DBuf w_tcode, w_tcode2, w_trecs;
@@ -898,6 +900,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
             const uint64_t *span = c->commit_span;
             c->rank_lsn32 = span[1] - span[0] <= kLsn32MaxSpan && !getenv("HSC_RANK_DIR");
             c->nt_sorted = !getenv("HSC_NT_SORT") || atoi(getenv("HSC_NT_SORT")) != 0;
+            c->nt_fused = !getenv("HSC_NT_FUSED") || atoi(getenv("HSC_NT_FUSED")) != 0;
             c->rank_base = span[0];
             c->cdir = Dir16{};
             if (!c->rank_lsn32)
@@ -1861,7 +1864,7 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     ntl.recs = c->w_trecs.as<uint4>();
     // conflict flags: internal, all zero between batches (the pack clears them)
     const size_t had = c->w_vflags.bytes;
-    HIPCHK(c, c->w_vflags.ensure(std::max<size_t>(b->n_txn, 1)));
+    HIPCHK(c, c->w_vflags.ensure((std::max<size_t>(b->n_txn, 1) + 15) & ~(size_t)15));
     if (c->w_vflags.bytes != had) HIPCHK(c, hipMemsetAsync(c->w_vflags.p, 0, c->w_vflags.bytes, s));
     uint8_t *flags = c->w_vflags.as<uint8_t>();
     const bool tm = c->timing;
@@ -1871,7 +1874,19 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
     HIPCHK(c, launch_locate_t(c->nv, wn, p, work, ntl, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
-    if (p.n && wn.ntiles) {
+    if (p.n && wn.ntiles && sorted && c->nt_fused) {
+        // plan-free: the join scans its tile's column itself, marks the flags
+        // and its last block writes the verdict bytes (large batches: a pack
+        // launch after it); the delta probe marks the flags before it
+        if (tm)
+            for (int i = 2; i <= 3; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
+        HIPCHK_RC(c, probe_delta(c, flags));
+        const bool tail = b->n_txn <= kTailPackMax;
+        HIPCHK(c, launch_join_f(work, ntl, wn.n, wn.ntiles, flags, (uint32_t)b->n_txn, b->verdict,
+                                b->bitmap, tail, s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
+        if (!tail) HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
+    } else if (p.n && wn.ntiles) {
         // the plan writes the verdict bytes from the locate's flags; the join
         // and the delta probe then mark the verdict itself
         HIPCHK(c, (sorted ? launch_plan_s : launch_plan_t)(work, wn.ntiles,

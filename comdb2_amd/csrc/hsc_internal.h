@@ -369,6 +369,12 @@ hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeV
                            hipStream_t s);
 hipError_t launch_scatter_t(const ProbeView &p, const ProbeWork &work, const NarrowTiles &nt,
                             uint32_t ntiles, hipStream_t s);
+// Plan-free join of chunk-sorted records (tile columns scanned in the join;
+// conflicts into flags; tail_pack: the last block writes the verdict bytes /
+// bitmap from the flags and clears them).
+hipError_t launch_join_f(const ProbeWork &work, const NarrowTiles &nt, uint32_t n, uint32_t ntiles,
+                         uint8_t *flags, uint32_t n_txn, uint8_t *verdict, uint64_t *bitmap,
+                         bool tail_pack, hipStream_t s);
 hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t n,
                          uint32_t ntiles, uint32_t max_items, uint8_t *verdict, hipStream_t s);
 // Dependency graph + SCC (hsc_graph.hip).

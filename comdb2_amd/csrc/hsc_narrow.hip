@@ -921,7 +921,7 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
     const uint32_t g = xcd_chunk(blockIdx.x, (work.G + 7) / 8);
     if (g >= work.G) return;
     HSC_STAMP(work, 0, 0);
-    if (g == 0 && threadIdx.x < 2) work.item_off[threadIdx.x] = 0;  // the plan's overflow counters
+    if (g == 0 && threadIdx.x < 3) work.item_off[threadIdx.x] = 0;  // the plan's / join's counters
     const uint32_t c0 = g * work.chunk;
     const uint32_t c1 = min(p.n, c0 + work.chunk);
     // probe registers: buffer 0 / 1 alternate between sub-chunks (the loop
@@ -1719,6 +1719,186 @@ hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t 
         k_join_t<true><<<blocks, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
     else
         k_join_t<false><<<blocks, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
+    return hipGetLastError();
+}
+
+// ---- plan-free join (chunk-sorted records) ----
+// The plan kernel's work moves into the join: tile t's column of the locate's
+// chunk-major table (run start << 16 | count per chunk) is read straight from
+// the table -- one strided load per chunk, issued with the tile's rows; the
+// tiles of a block's XCD neighbour each other, so the column's lines are
+// shared in that XCD's L2 -- and scanned in LDS.  A hot tile's records past
+// the first kJoinChunk are joined by the same block in further rounds over
+// its staged rows (no overflow items).  Conflicts mark the batch's flags; the
+// last block to finish writes the verdict bytes from them (and clears them),
+// so a batch is two launches: locate -> join.
+constexpr int kPackVec = 16;  // flags per thread and load in the tail pack
+
+__device__ __forceinline__ uint32_t join_f_records(const NarrowTiles &nt, const ProbeWork &work,
+                                                   const uint32_t *Es, const uint32_t *Cs,
+                                                   uint32_t G, uint32_t j, uint32_t j1, u32x4 &rec)
+{
+    uint32_t g = 0;  // Es[0] = 0 <= j
+#pragma unroll
+    for (int b = 8; b >= 0; --b) {
+        const uint32_t c = g + (1u << b);
+        if (c < G && Es[c] <= j) g = c;
+    }
+    const size_t area = 2 * (size_t)work.chunk;
+    rec = j < j1 ? *(const u32x4 *)(nt.recs + g * area + Cs[g] + (j - Es[g])) : u32x4{0, 0, 0, 0};
+    return g;
+}
+
+__global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_f(
+    ProbeWork work, NarrowTiles nt, uint32_t n, uint32_t ntiles, uint8_t *flags, uint32_t n_txn,
+    uint8_t *verdict, uint64_t *bitmap, int tail_pack)
+{
+    constexpr uint32_t T = 1u << kTLog2;
+    constexpr int RQ = T / (4 * kJoinThreads);
+    constexpr int kRec = kJoinChunk / kJoinThreads;
+    __shared__ __attribute__((aligned(16))) uint32_t keys[T];
+    __shared__ __attribute__((aligned(16))) uint32_t rank[T];
+    __shared__ uint32_t b16[T / 16];
+    __shared__ uint32_t b128[T / 128];
+    __shared__ uint32_t Es[kMaxChunks], Cs[kMaxChunks];
+    __shared__ uint32_t wsum[kJoinThreads / 64];
+    __shared__ uint32_t last;
+    static_assert(kMaxChunks <= kJoinThreads, "one column entry per thread");
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t tb = join_tile_blocks(true, ntiles);
+    const uint32_t tile = kJoinXcd ? xcd_chunk(blockIdx.x, tb / 8) : blockIdx.x;
+    if (tile < ntiles) {
+        const uint32_t G = work.G, rs = (ntiles + 3) & ~3u;
+        const uint32_t x = threadIdx.x < G ? work.cm[(size_t)threadIdx.x * rs + tile] : 0;
+        u32x4 rk[RQ], rr[RQ], rec[kRec];
+        const size_t ts = (size_t)tile << kTLog2;
+#pragma unroll
+        for (int v = 0; v < RQ; ++v) {
+            const size_t row = ts + 4 * (threadIdx.x + kJoinThreads * v);
+            rk[v] = *(const u32x4 *)(nt.key32 + row);
+            rr[v] = *(const u32x4 *)(nt.rank32 + row);
+        }
+        // exclusive scan of the column's counts: chunk g's run starts at
+        // record Es[g] of the tile, at Cs[g] of the chunk's area
+        const uint32_t cnt = x & 0xFFFFu;
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) wsum[wv] = inc;
+        __syncthreads();
+        uint32_t base = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kJoinThreads / 64; ++w) {
+            base += w < wv ? wsum[w] : 0;
+            total += wsum[w];
+        }
+        if (threadIdx.x < G) Es[threadIdx.x] = base + inc - cnt, Cs[threadIdx.x] = x >> 16;
+        __syncthreads();
+        // the first round's records are requested while the rows arrive
+#pragma unroll
+        for (int k = 0; k < kRec; ++k)
+            join_f_records(nt, work, Es, Cs, G, k * kJoinThreads + threadIdx.x, total, rec[k]);
+#pragma unroll
+        for (int v = 0; v < RQ; ++v) {
+            const uint32_t quad = threadIdx.x + kJoinThreads * v;
+            ((u32x4 *)keys)[quad] = rk[v];
+            ((u32x4 *)rank)[quad] = rr[v];
+            uint32_t m = max(max(rr[v].x, rr[v].y), max(rr[v].z, rr[v].w));
+            m = max(m, (uint32_t)__shfl_xor((int)m, 1, 64));
+            m = max(m, (uint32_t)__shfl_xor((int)m, 2, 64));
+            if ((threadIdx.x & 3) == 0) b16[quad >> 2] = m;
+#pragma unroll
+            for (int d = 4; d < 32; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+            if ((threadIdx.x & 31) == 0) b128[quad >> 5] = m;
+        }
+        __syncthreads();
+        const uint32_t tn = min(T, n - (tile << kTLog2));
+        for (uint32_t j0 = 0; j0 < total; j0 += kJoinChunk) {
+            if (j0)  // a hot tile's further rounds
+#pragma unroll
+                for (int k = 0; k < kRec; ++k)
+                    join_f_records(nt, work, Es, Cs, G, j0 + k * kJoinThreads + threadIdx.x, total,
+                                   rec[k]);
+#pragma unroll
+            for (int k = 0; k < kRec; ++k) {
+                const uint32_t j = j0 + k * kJoinThreads + threadIdx.x;
+                if (j >= total) continue;
+                const uint32_t lo = rec[k].x, hi = rec[k].y, r_s = rec[k].z;
+                uint32_t ja = 1, jb = 1;
+#pragma unroll
+                for (int d = 0; d < kTLog2; ++d) {
+                    const uint32_t ka = keys[ja], kb = keys[jb];
+                    ja = 2 * ja + (ka < lo);
+                    jb = 2 * jb + (kb <= hi);
+                }
+                const uint32_t kl = keys[0];
+                const uint32_t pa = min(ja - T + (kl < lo), tn);
+                const uint32_t pb = min(jb - T + (kl <= hi), tn);
+                if (pa < pb && any_after32(rank, b16, b128, pa, pb, r_s)) flags[rec[k].w] = 1;
+            }
+        }
+    }
+    if (!tail_pack) return;
+    // the last block to finish turns the flags into the verdict bytes
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        last = atomicAdd(&work.item_off[2], 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const uint32_t nv = (n_txn + kPackVec - 1) / kPackVec;  // flags are padded to kPackVec
+    for (uint32_t i0 = 0; i0 < nv; i0 += 4 * kJoinThreads) {
+        u32x4 f[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = i0 + u * kJoinThreads + threadIdx.x;
+            f[u] = i < nv ? ((const u32x4 *)flags)[i] : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t i = i0 + u * kJoinThreads + threadIdx.x;
+            // 16 flag bytes -> 16 verdict bytes (0 / 1) and 16 bitmap bits
+            u32x4 o;
+            uint32_t bits = 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t w = f[u][c];
+                uint32_t b = 0;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) b |= ((w >> (8 * k)) & 0xFFu) ? 1u << (8 * k) : 0u;
+                o[c] = b;
+                bits |= ((b & 1u) | ((b >> 7) & 2u) | ((b >> 14) & 4u) | ((b >> 21) & 8u)) << (4 * c);
+            }
+            // 4 neighbouring lanes hold one 64-bit bitmap word (every lane shuffles)
+            uint64_t word = (uint64_t)bits << (16 * (i & 3));
+            word |= __shfl_xor(word, 1, 64);
+            word |= __shfl_xor(word, 2, 64);
+            if (i >= nv) continue;
+            const uint32_t t0 = i * kPackVec;
+            if (t0 + kPackVec <= n_txn) {
+                *(u32x4 *)(verdict + t0) = o;
+            } else {
+                for (uint32_t t = t0; t < n_txn; ++t)
+                    verdict[t] = (o[(t - t0) >> 2] >> (8 * ((t - t0) & 3))) & 1u;
+            }
+            if (f[u][0] | f[u][1] | f[u][2] | f[u][3]) ((u32x4 *)flags)[i] = u32x4{0, 0, 0, 0};
+            if (bitmap && (i & 3) == 0 && 64 * (i >> 2) < n_txn) bitmap[i >> 2] = word;
+        }
+    }
+}
+
+hipError_t launch_join_f(const ProbeWork &work, const NarrowTiles &nt, uint32_t n, uint32_t ntiles,
+                         uint8_t *flags, uint32_t n_txn, uint8_t *verdict, uint64_t *bitmap,
+                         bool tail_pack, hipStream_t s)
+{
+    if (ntiles == 0) return hipSuccess;
+    k_join_f<<<join_tile_blocks(true, ntiles), kJoinThreads, 0, s>>>(work, nt, n, ntiles, flags, n_txn,
+                                                                      verdict, bitmap, tail_pack ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -94,25 +94,28 @@ def test_groups_first_seen_after_the_build(validator, oracle_mod, layout, mode):
     validator.set_layout(LAYOUT_AUTO)
 
 
-def test_group_registered_after_device_ingest(validator):
+def test_group_registered_after_device_ingest():
     """A device-ingested window (one group) takes a second group registered
     after the build: the next check folds it in (no out-of-range gid)."""
+    from comdb2_amd.hsc import Validator
     from comdb2_amd.workloads import int64_words
-    validator.set_layout(LAYOUT_AUTO)
-    g0 = validator.register_group("dev_t", 0, 9)
-    vals = np.arange(0, 4000, 4, dtype=np.int64)
-    words = torch.tensor(int64_words(vals).astype(np.uint64).view(np.int64), device="cuda")
-    gid = torch.full((len(vals),), g0, dtype=torch.int32, device="cuda")
-    lsn = torch.tensor(np.arange(1, len(vals) + 1, dtype=np.int64) * 64 + (1 << 32), device="cuda")
-    end = int((len(vals) + 1) * 64 + (1 << 32))
-    validator.ingest_device(len(vals), 2, gid.data_ptr(), words.data_ptr(), lsn.data_ptr(), end)
-    g1 = validator.register_group("dev_t2", 1, 9)
-    assert g1 != g0
-    k = F.enc_int64(8)
-    rs = ReadSets.from_lists([[Range("dev_t", 0, k, k)], [Range("dev_t2", 1, k, k)]],
-                             [1 << 32, 1 << 32], tbnames=["dev_t", "dev_t2"])
-    got = validator.check_readsets(rs)
-    assert got.tolist() == [1, 0]
-    validator.append_writes([("dev_t2", 1, k, end + 64)], end_lsn=end + 128)
-    got = validator.check_readsets(rs)
-    assert got.tolist() == [1, 1]
+    v = Validator(0)  # its own dictionaries: 9-byte keys only
+    try:
+        g0 = v.register_group("dev_t", 0, 9)
+        vals = np.arange(0, 4000, 4, dtype=np.int64)
+        words = torch.tensor(int64_words(vals).astype(np.uint64).view(np.int64), device="cuda")
+        gid = torch.full((len(vals),), g0, dtype=torch.int32, device="cuda")
+        lsn = torch.tensor(np.arange(1, len(vals) + 1, dtype=np.int64) * 64 + (1 << 32), device="cuda")
+        end = int((len(vals) + 1) * 64 + (1 << 32))
+        torch.cuda.synchronize()
+        v.ingest_device(len(vals), 2, gid.data_ptr(), words.data_ptr(), lsn.data_ptr(), end)
+        g1 = v.register_group("dev_t2", 1, 9)
+        assert g1 != g0
+        k = F.enc_int64(8)
+        rs = ReadSets.from_lists([[Range("dev_t", 0, k, k)], [Range("dev_t2", 1, k, k)]],
+                                 [1 << 32, 1 << 32], tbnames=["dev_t", "dev_t2"])
+        assert v.check_readsets(rs).tolist() == [1, 0]
+        v.append_writes([("dev_t2", 1, k, end + 64)], end_lsn=end + 128)
+        assert v.check_readsets(rs).tolist() == [1, 1]
+    finally:
+        v.close()
