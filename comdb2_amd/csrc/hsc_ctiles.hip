@@ -214,7 +214,7 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
     uint32_t *hist = (uint32_t *)(lb + L.hist);
     const uint32_t g = xcd_chunk(blockIdx.x, (work.G + 7) / 8);
     if (g >= work.G) return;
-    if (g == 0 && threadIdx.x < 2) work.item_off[threadIdx.x] = 0;  // the plan's overflow counters
+    if (g == 0 && threadIdx.x < 3) work.item_off[threadIdx.x] = 0;  // the plan's / join's counters
     const uint32_t c0 = g * work.chunk, c1 = min(p.n, c0 + work.chunk);
     // every probe load of the chunk first (read-once inputs: non-temporal)
     uint64_t lo[kCLocP][WG], hi[kCLocP][WG], snap[kCLocP];
@@ -675,6 +675,96 @@ __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     }
 }
 
+// Plan-free compact join (chunk-sorted records), as k_join_f of the narrow
+// tiles: the tile's column of the locate's chunk-major table is read and
+// scanned here, a hot tile's records past the first kCJT are joined by the
+// same block in further rounds, conflicts mark the flags and the last block
+// writes the verdict bytes.  Two launches per batch besides the bound mapping:
+// locate -> join.
+template <int WG>
+__global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_join_cf(
+    ProbeWork work, CTiles ct, uint8_t *flags, uint32_t n_txn, uint8_t *verdict, uint64_t *bitmap,
+    int tail_pack)
+{
+    constexpr uint32_t T = kCTRows;
+    extern __shared__ __attribute__((aligned(16))) uint64_t jl[];
+    uint64_t *kw = jl;                                   // [WG][T], sorted
+    uint32_t *rank = (uint32_t *)(jl + (size_t)WG * T);  // [T], sorted order
+    uint32_t *b16 = rank + T;                            // [T / 16]
+    uint32_t *b128 = b16 + T / 16;                       // [T / 128]
+    uint32_t *B = b128 + T / 128;                        // [kTBS] the tile's bucket table
+    uint32_t *Es = B + kTBS;                             // the tile's column: offsets
+    uint16_t *Cs = (uint16_t *)(Es + kMaxChunks);        // and run starts
+    __shared__ uint32_t wsum[kCJT / 64];
+    const uint32_t tid = threadIdx.x, tile = blockIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
+    if (tile < ct.ntiles) {
+        const uint32_t G = work.G, rs = (ct.ntiles + 3) & ~3u;
+        const uint32_t x = tid < G ? work.cm[(size_t)tid * rs + tile] : 0;
+        const size_t row = ((size_t)tile << kCTLog2) + 2 * tid;
+        u64x2 kv[WG];
+#pragma unroll
+        for (int w = 0; w < WG; ++w) kv[w] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row);
+        const u32x2 rr = *(const u32x2 *)(ct.rank + row);
+        u32x2 bt = {0, 0};
+        if (tid < kTBS / 2) bt = *(const u32x2 *)(ct.tb + (size_t)tile * kTBS + 2 * tid);
+        // exclusive scan of the column's counts
+        const uint32_t cnt = x & 0xFFFFu;
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) wsum[wv] = inc;
+        __syncthreads();
+        uint32_t base = 0, total = 0;
+#pragma unroll
+        for (int w = 0; w < kCJT / 64; ++w) {
+            base += w < wv ? wsum[w] : 0;
+            total += wsum[w];
+        }
+        if (tid < G) Es[tid] = base + inc - cnt, Cs[tid] = (uint16_t)(x >> 16);
+        __syncthreads();
+        auto fetch = [&](uint32_t j, u64x2 &A0, u64x2 &A1, u64x2 &B0, u64x2 &B1) {
+            uint32_t g = 0;  // Es[0] = 0 <= j
+#pragma unroll
+            for (int b = 8; b >= 0; --b) {
+                const uint32_t c = g + (1u << b);
+                if (c < G && Es[c] <= j) g = c;
+            }
+            const u64x2 *r = (const u64x2 *)ct.recs + 4 * ((size_t)g * 2 * work.chunk + Cs[g] + (j - Es[g]));
+            A0 = r[0], A1 = r[1], B0 = r[2], B1 = r[3];
+        };
+        u64x2 A0 = {}, A1 = {}, B0 = {}, B1 = {};
+        if (tid < total) fetch(tid, A0, A1, B0, B1);  // while the rows arrive
+#pragma unroll
+        for (int w = 0; w < WG; ++w) *(u64x2 *)(kw + (size_t)w * T + 2 * tid) = kv[w];
+        *(u32x2 *)(rank + 2 * tid) = rr;
+        if (tid < kTBS / 2) *(u32x2 *)(B + 2 * tid) = bt;
+        uint32_t m = max(rr.x, rr.y);
+#pragma unroll
+        for (int d = 1; d < 8; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+        if ((tid & 7) == 0) b16[tid >> 3] = m;
+#pragma unroll
+        for (int d = 8; d < 64; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+        if ((tid & 63) == 0) b128[tid >> 6] = m;
+        __syncthreads();
+        for (uint32_t j0 = 0; j0 < total; j0 += kCJT) {
+            const uint32_t j = j0 + tid;
+            if (j >= total) continue;
+            if (j0) fetch(j, A0, A1, B0, B1);  // a hot tile's further rounds
+            const uint32_t kind = (uint32_t)(A1.y >> 62);
+            const uint64_t rt = A1.y & ((1ull << 62) - 1);
+            u64x2 pl[2] = {A0, u64x2{A1.x, rt}}, ph0 = B0;
+            uint64_t ph1 = B1.x;
+            if (kind == kCTail) ph0 = A0, ph1 = A1.x;  // a tail record carries hi in its first half
+            join_search<WG>(work, ct, flags, kw, rank, b16, b128, B, kind, pl, ph0, ph1);
+        }
+    }
+    if (tail_pack) flags_tail_pack<kCJT>(&work.item_off[2], flags, n_txn, verdict, bitmap);
+}
+
 }  // namespace
 
 hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *gid,
@@ -729,6 +819,22 @@ hipError_t launch_scatter_c(const CTiles &ct, const ProbeWork &work, uint32_t n,
 {
     if (n == 0) return hipSuccess;
     k_scatter_c<<<8 * ((work.G + 7) / 8), kCLocThreads, 4 * (size_t)ct.ntiles, s>>>(ct, work, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_join_cf(const CTiles &ct, const ProbeWork &work, uint8_t *flags, uint32_t n_txn,
+                          uint8_t *verdict, uint64_t *bitmap, bool tail_pack, hipStream_t s)
+{
+    if (ct.ntiles == 0) return hipSuccess;
+    const size_t lds = 8 * (size_t)ct.WG * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
+                       4 * (kCTRows / 128) + 4 * kTBS + 6 * (size_t)kMaxChunks;
+    const int tp = tail_pack ? 1 : 0;
+    switch (ct.WG) {
+    case 1: k_join_cf<1><<<ct.ntiles, kCJT, lds, s>>>(work, ct, flags, n_txn, verdict, bitmap, tp); break;
+    case 2: k_join_cf<2><<<ct.ntiles, kCJT, lds, s>>>(work, ct, flags, n_txn, verdict, bitmap, tp); break;
+    case 3: k_join_cf<3><<<ct.ntiles, kCJT, lds, s>>>(work, ct, flags, n_txn, verdict, bitmap, tp); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -236,6 +236,7 @@ struct hsc_ctx {
     bool nt_sorted = true;     // narrow tiles: chunk-sorted records (HSC_NT_SORT=0 at build: scatter)
     bool nt_fused = true;      // chunk-sorted narrow tiles: plan-free join (HSC_NT_FUSED=0 at build: plan + join)
     bool ct_sorted = true;     // compact tiles: chunk-sorted records (HSC_CT_SORT=0 at build: scatter)
+    bool ct_fused = true;      // ... and the plan-free join (HSC_CT_FUSED=0 at build: plan + join)
     uint64_t rank_base = 0;
     DBuf w_tcode, w_tcode2, w_trecs;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
@@ -634,6 +635,7 @@ static int build_ctiles(hsc_ctx *c)
     CTiles &ct = c->ctv;
     ct = CTiles{};
     c->ct_sorted = !getenv("HSC_CT_SORT") || atoi(getenv("HSC_CT_SORT")) != 0;
+    c->ct_fused = !getenv("HSC_CT_FUSED") || atoi(getenv("HSC_CT_FUSED")) != 0;
     ct.n = (uint32_t)c->n;
     ct.ntiles = v.ntiles;
     ct.len = (size_t)v.ntiles << kCTLog2;
@@ -1976,7 +1978,7 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
     static const int dbg = getenv("HSC_CT_DBG") ? atoi(getenv("HSC_CT_DBG")) : 0;
     ct.dbg = dbg;
     const size_t had = c->w_vflags.bytes;
-    HIPCHK(c, c->w_vflags.ensure(std::max<size_t>(b->n_txn, 1)));
+    HIPCHK(c, c->w_vflags.ensure((std::max<size_t>(b->n_txn, 1) + 15) & ~(size_t)15));
     if (c->w_vflags.bytes != had) HIPCHK(c, hipMemsetAsync(c->w_vflags.p, 0, c->w_vflags.bytes, s));
     uint8_t *flags = c->w_vflags.as<uint8_t>();
     WinView wt = c->wc;  // tile maxima of the same 2048-row tiles
@@ -1994,7 +1996,17 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
     HIPCHK(c, launch_locate_c(ct, wt, p, c->p_code_lo.as<uint64_t>(), c->p_code_hi.as<uint64_t>(),
                               work, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
-    if (p.n && ct.ntiles) {
+    if (p.n && ct.ntiles && sorted && c->ct_fused) {
+        // plan-free, as probe_ntiles: the join scans its column, marks the
+        // flags and its last block writes the verdict bytes
+        if (tm)
+            for (int i = 2; i <= 3; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
+        HIPCHK_RC(c, probe_delta(c, flags));
+        const bool tail = b->n_txn <= kTailPackMax;
+        HIPCHK(c, launch_join_cf(ct, work, flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, tail, s));
+        if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
+        if (!tail) HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
+    } else if (p.n && ct.ntiles) {
         // pack folded into the plan, as probe_ntiles
         HIPCHK(c, (sorted ? launch_plan_s : launch_plan_t)(work, ct.ntiles,
                                                           c->w_items.as<uint32_t>(), s, flags,

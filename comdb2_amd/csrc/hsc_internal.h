@@ -482,6 +482,9 @@ hipError_t launch_locate_c(const CTiles &ct, const WinView &wt, const ProbeView 
                            const uint64_t *clo, const uint64_t *chi, const ProbeWork &work,
                            uint8_t *flags, hipStream_t s);
 hipError_t launch_scatter_c(const CTiles &ct, const ProbeWork &work, uint32_t n, hipStream_t s);
+// Plan-free compact join (chunk-sorted records), as launch_join_f.
+hipError_t launch_join_cf(const CTiles &ct, const ProbeWork &work, uint8_t *flags, uint32_t n_txn,
+                          uint8_t *verdict, uint64_t *bitmap, bool tail_pack, hipStream_t s);
 hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_items,
                          uint8_t *flags, hipStream_t s);
 // Sharded SCC (hsc_graph.hip): cover[v] = 1 iff v lies inside [dst, src] of a

@@ -1732,8 +1732,6 @@ hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t 
 // its staged rows (no overflow items).  Conflicts mark the batch's flags; the
 // last block to finish writes the verdict bytes from them (and clears them),
 // so a batch is two launches: locate -> join.
-constexpr int kPackVec = 16;  // flags per thread and load in the tail pack
-
 __device__ __forceinline__ uint32_t join_f_records(const NarrowTiles &nt, const ProbeWork &work,
                                                    const uint32_t *Es, const uint32_t *Cs,
                                                    uint32_t G, uint32_t j, uint32_t j1, u32x4 &rec)
@@ -1762,7 +1760,6 @@ __global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_f(
     __shared__ uint32_t b128[T / 128];
     __shared__ uint32_t Es[kMaxChunks], Cs[kMaxChunks];
     __shared__ uint32_t wsum[kJoinThreads / 64];
-    __shared__ uint32_t last;
     static_assert(kMaxChunks <= kJoinThreads, "one column entry per thread");
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t tb = join_tile_blocks(true, ntiles);
@@ -1841,55 +1838,7 @@ __global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_f(
             }
         }
     }
-    if (!tail_pack) return;
-    // the last block to finish turns the flags into the verdict bytes
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();
-        last = atomicAdd(&work.item_off[2], 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    const uint32_t nv = (n_txn + kPackVec - 1) / kPackVec;  // flags are padded to kPackVec
-    for (uint32_t i0 = 0; i0 < nv; i0 += 4 * kJoinThreads) {
-        u32x4 f[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t i = i0 + u * kJoinThreads + threadIdx.x;
-            f[u] = i < nv ? ((const u32x4 *)flags)[i] : u32x4{0, 0, 0, 0};
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t i = i0 + u * kJoinThreads + threadIdx.x;
-            // 16 flag bytes -> 16 verdict bytes (0 / 1) and 16 bitmap bits
-            u32x4 o;
-            uint32_t bits = 0;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const uint32_t w = f[u][c];
-                uint32_t b = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) b |= ((w >> (8 * k)) & 0xFFu) ? 1u << (8 * k) : 0u;
-                o[c] = b;
-                bits |= ((b & 1u) | ((b >> 7) & 2u) | ((b >> 14) & 4u) | ((b >> 21) & 8u)) << (4 * c);
-            }
-            // 4 neighbouring lanes hold one 64-bit bitmap word (every lane shuffles)
-            uint64_t word = (uint64_t)bits << (16 * (i & 3));
-            word |= __shfl_xor(word, 1, 64);
-            word |= __shfl_xor(word, 2, 64);
-            if (i >= nv) continue;
-            const uint32_t t0 = i * kPackVec;
-            if (t0 + kPackVec <= n_txn) {
-                *(u32x4 *)(verdict + t0) = o;
-            } else {
-                for (uint32_t t = t0; t < n_txn; ++t)
-                    verdict[t] = (o[(t - t0) >> 2] >> (8 * ((t - t0) & 3))) & 1u;
-            }
-            if (f[u][0] | f[u][1] | f[u][2] | f[u][3]) ((u32x4 *)flags)[i] = u32x4{0, 0, 0, 0};
-            if (bitmap && (i & 3) == 0 && 64 * (i >> 2) < n_txn) bitmap[i >> 2] = word;
-        }
-    }
+    if (tail_pack) flags_tail_pack<kJoinThreads>(&work.item_off[2], flags, n_txn, verdict, bitmap);
 }
 
 hipError_t launch_join_f(const ProbeWork &work, const NarrowTiles &nt, uint32_t n, uint32_t ntiles,
