@@ -240,6 +240,8 @@ struct hsc_ctx {
     uint64_t rank_base = 0;
     DBuf w_tcode, w_tcode2, w_trecs;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
+    DBuf d_pk[2];              // packed-key sort: the keys, ping-pong (hsc_ingest.hip)
+    bool packed_sort = false;  // the last build sorted packed keys
     DBuf d_gstart, d_gend, d_tmax, d_table_max, d_group_table, d_count, d_sp_g, d_sp_w;
     // compact codes of a wide window (hsc_compact.hip): WinView wc over them
     bool compact = false;
@@ -708,8 +710,37 @@ static int narrow_trad_pick(hsc_ctx *c)
     return HSC_OK;
 }
 
+// HSC_BUILD_TRACE=1: wall time of each stage of a window build on stderr
+// (every stamp synchronises the stream first; diagnostics only).
+struct BuildTrace {
+    bool on;
+    hipStream_t s;
+    std::chrono::steady_clock::time_point t;
+    std::string out;
+    explicit BuildTrace(hipStream_t s_) : on(getenv("HSC_BUILD_TRACE") != nullptr), s(s_)
+    {
+        if (on) (void)hipStreamSynchronize(s);
+        t = std::chrono::steady_clock::now();
+    }
+    void stamp(const char *what)
+    {
+        if (!on) return;
+        (void)hipStreamSynchronize(s);
+        const auto n = std::chrono::steady_clock::now();
+        char b[64];
+        snprintf(b, sizeof b, " %s=%.0f", what, std::chrono::duration<double, std::micro>(n - t).count());
+        out += b;
+        t = n;
+    }
+    ~BuildTrace()
+    {
+        if (on && !out.empty()) fprintf(stderr, "[build us]%s\n", out.c_str());
+    }
+};
+
 static int device_build(hsc_ctx *c, size_t n_in)
 {
+    BuildTrace bt(c->stream);
     HIPCHK(c, wait_lanes(c));
     hipStream_t s = c->stream;
     const int W = c->W;
@@ -718,34 +749,65 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, c->d_words2.ensure(cap * 8 * W));
     HIPCHK(c, c->d_lsn2.ensure(cap * 8));
     HIPCHK(c, c->d_flags.ensure(cap * 4 + 64));
+    // packed-key sort (hsc_ingest.hip) unless HSC_PACKED_SORT=0 or the key
+    // has more words than it takes
+    const bool try_packed = W <= kPackMaxWords && n_in > 0 &&
+                            (!getenv("HSC_PACKED_SORT") || atoi(getenv("HSC_PACKED_SORT")) != 0);
     size_t scratch = std::max(radix_scratch_bytes(n_in, W), scan_scratch_bytes(n_in) + 64);
+    if (try_packed) {
+        scratch = std::max(scratch, packed_scratch_bytes(n_in));
+        for (auto &b : c->d_pk) HIPCHK(c, b.ensure(8 * cap));
+    }
     HIPCHK(c, c->d_scratch.ensure(scratch));
     HIPCHK(c, c->d_count.ensure(256));
+    bt.stamp("alloc");
 
     hipEvent_t e0 = nullptr, e1 = nullptr;
     HIPCHK(c, hipEventCreate(&e0));
     HIPCHK(c, hipEventCreate(&e1));
     HIPCHK(c, hipEventRecord(e0, s));
     if (c->layout != HSC_LAYOUT_WIDE && n_in > 0) HIPCHK_RC(c, build_commits(c, n_in));
-    bool in_alt = false;
+    bt.stamp("commits");
     uint64_t vary[kMaxWords + 1];
-    HIPCHK(c, radix_sort_rows(W, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
-                              c->d_lsn.as<uint64_t>(), cap, c->d_gid2.as<uint32_t>(),
-                              c->d_words2.as<uint64_t>(), c->d_lsn2.as<uint64_t>(),
-                              c->d_scratch.p, c->d_scratch.bytes, &in_alt, vary, s));
-    // dedupe from wherever the sort left the rows into the other buffer set
-    DBuf *sg = in_alt ? &c->d_gid2 : &c->d_gid, *sw = in_alt ? &c->d_words2 : &c->d_words,
-         *sl = in_alt ? &c->d_lsn2 : &c->d_lsn;
-    DBuf *dg = in_alt ? &c->d_gid : &c->d_gid2, *dw = in_alt ? &c->d_words : &c->d_words2,
-         *dl = in_alt ? &c->d_lsn : &c->d_lsn2;
-    HIPCHK(c, dedupe_rows(W, n_in, sg->as<uint32_t>(), sw->as<uint64_t>(), sl->as<uint64_t>(), cap,
-                          dg->as<uint32_t>(), dw->as<uint64_t>(), dl->as<uint64_t>(), cap,
-                          c->d_flags.as<uint32_t>(), c->d_scratch.p, c->d_scratch.bytes,
-                          c->d_count.as<uint32_t>(), s));
-    if (!in_alt) {  // final rows must live in d_gid/d_words/d_lsn
-        std::swap(c->d_gid, c->d_gid2);
-        std::swap(c->d_words, c->d_words2);
-        std::swap(c->d_lsn, c->d_lsn2);
+    HIPCHK(c, vary_mask_rows(W, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(), cap,
+                             c->d_scratch.p, vary, s));
+    bt.stamp("vary");
+    PackPlan plan;
+    c->packed_sort = try_packed && packed_plan(W, n_in, vary, &plan);
+    if (c->packed_sort) {
+        // every version, key-sorted, into d_*2; the distinct rows into d_*
+        HIPCHK(c, packed_sort_rows(plan, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
+                                   c->d_lsn.as<uint64_t>(), cap, c->d_pk[0].as<uint64_t>(),
+                                   c->d_pk[1].as<uint64_t>(), c->d_gid2.as<uint32_t>(),
+                                   c->d_words2.as<uint64_t>(), c->d_lsn2.as<uint64_t>(), cap,
+                                   c->d_flags.as<uint32_t>(), c->d_scratch.p, c->d_scratch.bytes, s));
+        bt.stamp("sort");
+        HIPCHK(c, dedupe_flagged(W, n_in, c->d_gid2.as<uint32_t>(), c->d_words2.as<uint64_t>(),
+                                 c->d_lsn2.as<uint64_t>(), cap, c->d_gid.as<uint32_t>(),
+                                 c->d_words.as<uint64_t>(), c->d_lsn.as<uint64_t>(), cap,
+                                 c->d_flags.as<uint32_t>(), c->d_scratch.p, c->d_scratch.bytes,
+                                 c->d_count.as<uint32_t>(), s));
+    } else {
+        bool in_alt = false;
+        HIPCHK(c, radix_sort_known(W, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
+                                   c->d_lsn.as<uint64_t>(), cap, c->d_gid2.as<uint32_t>(),
+                                   c->d_words2.as<uint64_t>(), c->d_lsn2.as<uint64_t>(),
+                                   c->d_scratch.p, c->d_scratch.bytes, &in_alt, vary, s));
+        bt.stamp("sort");
+        // dedupe from wherever the sort left the rows into the other buffer set
+        DBuf *sg = in_alt ? &c->d_gid2 : &c->d_gid, *sw = in_alt ? &c->d_words2 : &c->d_words,
+             *sl = in_alt ? &c->d_lsn2 : &c->d_lsn;
+        DBuf *dg = in_alt ? &c->d_gid : &c->d_gid2, *dw = in_alt ? &c->d_words : &c->d_words2,
+             *dl = in_alt ? &c->d_lsn : &c->d_lsn2;
+        HIPCHK(c, dedupe_rows(W, n_in, sg->as<uint32_t>(), sw->as<uint64_t>(), sl->as<uint64_t>(), cap,
+                              dg->as<uint32_t>(), dw->as<uint64_t>(), dl->as<uint64_t>(), cap,
+                              c->d_flags.as<uint32_t>(), c->d_scratch.p, c->d_scratch.bytes,
+                              c->d_count.as<uint32_t>(), s));
+        if (!in_alt) {  // final rows must live in d_gid/d_words/d_lsn
+            std::swap(c->d_gid, c->d_gid2);
+            std::swap(c->d_words, c->d_words2);
+            std::swap(c->d_lsn, c->d_lsn2);
+        }
     }
     // one readback for the sizes the host plans with: distinct rows, commits,
     // the commit span and the window's end rows (all computed on the device)
@@ -766,6 +828,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
     }
     HIPCHK(c, hipMemcpyAsync(hc, c->d_count.p, sizeof hc, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
+    bt.stamp("dedupe");
     const uint32_t nu = hc[0];
     if (commits) {
         c->ncommit = hc[12];
@@ -825,6 +888,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
                               c->d_tmax.as<uint64_t>(), c->d_group_table.as<uint32_t>(),
                               c->d_table_max.as<uint64_t>(), c->d_sp_g.as<uint32_t>(),
                               c->d_sp_w.as<uint64_t>(), s));
+    bt.stamp("summaries");
     c->compact = false;
     uint32_t wide32 = 1;   // narrow tiles: a tile spans >= 2^32 codes (device flag)
     bool tiles32 = false;
@@ -833,6 +897,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
         c->n > 0 && W > 1 && ng > 0) {
         HIPCHK_RC(c, build_compact(c, w));
         if (c->compact) HIPCHK_RC(c, build_ctiles(c));
+        bt.stamp("compact");
     }
     if (c->narrow) {
         // level sizes: level 0 = n + 1 rounded up to whole tiles (at least one
@@ -867,6 +932,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
         nv.tz = c->tz;
         nv.n = (uint32_t)c->n;
         HIPCHK(c, narrow_build(w, nv, s));
+        bt.stamp("narrow");
         // one-word tile view of the codes: rows (gid 0, key64), lsn
         WinView &wn = c->wn;
         wn = WinView{};
@@ -897,6 +963,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
         // 8-byte tile rows when every 4096-row tile spans < 2^32 codes
         c->ntiles32 = false;
         c->trad_m = 0;
+        bt.stamp("codes");
         if (wn.log2T == 12 && wn.ntiles <= (uint32_t)kHistCap && c->ncommit > 0) {
             // commit span: rank-free rows (lsn - oldest commit + 1) when it fits 32 bits
             const uint64_t *span = c->commit_span;
@@ -933,6 +1000,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, hipEventRecord(e1, s));
     HIPCHK(c, hipStreamSynchronize(s));
     if (tiles32) c->ntiles32 = wide32 == 0;
+    bt.stamp("tiles");
     if (c->narrow && c->trad_m >= 64) HIPCHK_RC(c, narrow_trad_pick(c));
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
@@ -945,6 +1013,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
         HIPCHK(c, hipMemcpy(tm.data(), c->d_table_max.p, 8 * (size_t)nt, hipMemcpyDeviceToHost));
         for (int t = 0; t < nt; ++t) c->h_table_max[t] = std::max(c->h_table_max[t], tm[t]);
     }
+    bt.stamp("finish");
     c->dirty = false;
     c->live = true;
     c->merge_pending = false;
@@ -2759,6 +2828,36 @@ int hsc_marshal_readsets(hsc_ctx *c, const hsc_readsets *rs, const hsc_marshalle
     rc = marshal_readsets(c, rs);
     *out = &c->m;
     return rc;
+}
+
+long hsc_window_export(hsc_ctx *c, int all_versions, uint32_t *gid, uint64_t *key_words,
+                       uint64_t *lsn, size_t cap)
+{
+    if (!c) return HSC_EINVAL;
+    if (c->host_only) return HSC_EDEVICE;
+    const bool copy = gid || key_words || lsn;
+    if (copy && !(gid && key_words && lsn)) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    if (c->live && (c->dn || !c->app_gid.empty())) {  // the snapshot includes the delta run
+        c->merge_pending = true;
+        c->dirty = true;
+    }
+    int rc = ensure_built(c);
+    if (rc) return rc;
+    const size_t n = all_versions ? c->n_all : c->n;
+    if (!copy || n == 0 || n > cap) return (long)n;
+    const DBuf &dg = all_versions ? c->d_gid2 : c->d_gid;
+    const DBuf &dw = all_versions ? c->d_words2 : c->d_words;
+    const DBuf &dl = all_versions ? c->d_lsn2 : c->d_lsn;
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipMemcpyAsync(gid, dg.p, 4 * n, hipMemcpyDeviceToHost, s));
+    for (int j = 0; j < c->W; ++j)
+        HIPCHK(c, hipMemcpyAsync(key_words + (size_t)j * cap, dw.as<uint64_t>() + (size_t)j * c->cap, 8 * n,
+                                 hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(lsn, dl.p, 8 * n, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    return (long)n;
 }
 
 int hsc_rw_edges(hsc_ctx *c, const hsc_readsets *rs, size_t *n_pairs, const uint32_t **txn,

@@ -1,0 +1,338 @@
+// hsc_ingest.hip -- packed-key window sort (gfx950).
+//
+// A window build sorts its rows by (gid, key words), keeps every version in
+// key order (rw pairs, the delta fold) and the last version of each key
+// (device_build).  The generic path (hsc_kernels.hip radix_sort_rows) moves
+// whole rows -- gid, W key words and the LSN, 20+ bytes -- through one LSD
+// pass per varying key byte.  When the key bits that vary across the window
+// (gid and words together) plus the bits of a row index fit one 64-bit word
+// -- config 2's 40-bit keys with 24 index bits, config 5's 33 + 27 -- each row
+// travels as a single word instead:
+//   pack     key = compress(varying bits, most significant limb first) << I
+//            | row index, one pass over the varying limbs only; it also counts
+//            digit 0 of its 8192-row block;
+//   scatter  one stable LSD pass per varying key byte: the block's keys are
+//            ranked per wave with ballots, staged in LDS in sorted order and
+//            leave as coalesced runs per digit (k_pk_count counts the next
+//            digit of the permuted keys);
+//   unpack   every sorted key back to gid / words (expand of the kept bits
+//            over row 0's constant bits) with the LSN gathered by row index,
+//            plus the "last version of its key" flag;
+// then the usual scan + compaction (dedupe_flagged) gives the distinct rows.
+// Per row and pass that is 8 B read + 8 B written instead of a whole row.
+#include "hsc_device.h"
+#include "hsc_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+namespace hsc {
+namespace {
+
+constexpr int kPkThreads = 512;
+constexpr int kPkItems = 16;
+constexpr int kPkTile = kPkThreads * kPkItems;  // rows per block (8192)
+constexpr int kPkWaves = kPkThreads / 64;
+
+__device__ __forceinline__ uint64_t pk_compress(uint64_t x, uint64_t m, const uint64_t (&mv)[6])
+{
+    x &= m;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const uint64_t t = x & mv[i];
+        x = (x ^ t) | (t >> (1 << i));
+    }
+    return x;
+}
+
+// inverse of pk_compress (Hacker's Delight expand: the same moves, reversed)
+__device__ __forceinline__ uint64_t pk_expand(uint64_t x, uint64_t m, const uint64_t (&mv)[6])
+{
+#pragma unroll
+    for (int i = 5; i >= 0; --i) x = (x & ~mv[i]) | ((x << (1 << i)) & mv[i]);
+    return x & m;
+}
+
+__device__ __forceinline__ uint64_t pk_limb(const PackPlan &P, int l, size_t i, const uint32_t *gid,
+                                            const uint64_t *words, size_t stride)
+{
+    const int id = P.limb[l];
+    return id == P.W ? (uint64_t)gid[i] : words[(size_t)id * stride + i];
+}
+
+__global__ __launch_bounds__(kPkThreads) void k_pk_pack(PackPlan P, size_t n, const uint32_t *gid,
+                                                        const uint64_t *words, size_t stride,
+                                                        uint64_t *keys, uint32_t *counts,
+                                                        uint32_t nblocks)
+{
+    __shared__ uint32_t h[256];
+    if (threadIdx.x < 256) h[threadIdx.x] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * kPkTile;
+    uint64_t key[kPkItems];
+#pragma unroll
+    for (int k = 0; k < kPkItems; ++k) {  // every load in flight before the first store
+        const size_t i = base + (size_t)k * kPkThreads + threadIdx.x;
+        uint64_t kb = 0;
+        if (i < n) {
+#pragma unroll
+            for (int l = 0; l < kPackLimbs; ++l) {
+                if (l < P.nl) {
+                    uint64_t mv[6];
+#pragma unroll
+                    for (int q = 0; q < 6; ++q) mv[q] = P.mv[l][q];
+                    kb = (kb << P.bits[l]) |
+                         pk_compress(pk_limb(P, l, i, gid, words, stride), P.mask[l], mv);
+                }
+            }
+        }
+        key[k] = (kb << P.I) | (uint64_t)i;
+    }
+#pragma unroll
+    for (int k = 0; k < kPkItems; ++k) {
+        const size_t i = base + (size_t)k * kPkThreads + threadIdx.x;
+        if (i < n) {
+            keys[i] = key[k];
+            atomicAdd(&h[(uint32_t)(key[k] >> P.I) & 0xFFu], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 256) counts[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+// Per-block counts of digit (key >> sh) & 255, digit-major.
+__global__ __launch_bounds__(kPkThreads) void k_pk_count(int sh, size_t n, const uint64_t *keys,
+                                                         uint32_t *counts, uint32_t nblocks)
+{
+    __shared__ uint32_t h[256];
+    if (threadIdx.x < 256) h[threadIdx.x] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * kPkTile;
+    uint32_t d[kPkItems];
+#pragma unroll
+    for (int k = 0; k < kPkItems; ++k) {
+        const size_t i = base + (size_t)k * kPkThreads + threadIdx.x;
+        d[k] = i < n ? (uint32_t)(__builtin_nontemporal_load(keys + i) >> sh) & 0xFFu : 0x100u;
+    }
+#pragma unroll
+    for (int k = 0; k < kPkItems; ++k)
+        if (d[k] < 0x100u) atomicAdd(&h[d[k]], 1u);
+    __syncthreads();
+    if (threadIdx.x < 256) counts[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+}
+
+// Stable scatter of one digit.  Phase 1: wave w ranks keys [1024 w, 1024 w +
+// 1024) of the block in index order against wave-private digit counters (16
+// rounds of 64 lanes, 8 ballots per round), the per-wave counts become
+// per-(wave, digit) starts and every key is written to its place of the
+// block's sorted order in LDS.  Phase 2 reads LDS in order, so consecutive
+// threads store consecutive addresses of each digit's run.
+__global__ __launch_bounds__(kPkThreads) void k_pk_scatter(int sh, size_t n, const uint64_t *keys,
+                                                           uint64_t *keys_o, const uint32_t *offsets,
+                                                           uint32_t nblocks)
+{
+    constexpr uint32_t kWaveRows = kPkTile / kPkWaves;
+    __shared__ uint32_t gbase[256];
+    __shared__ uint32_t loff[256];
+    __shared__ uint32_t wcnt[kPkWaves][256];
+    __shared__ uint64_t stage[kPkTile];
+    __shared__ uint32_t lds16[16];
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    const size_t base = (size_t)blockIdx.x * kPkTile;
+    const uint32_t wbase = wid * kWaveRows;
+    uint64_t key[kPkItems];
+#pragma unroll
+    for (int k = 0; k < kPkItems; ++k) {  // the block's keys first: their loads overlap the offsets'
+        const size_t i = base + wbase + k * 64 + lane;
+        key[k] = i < n ? __builtin_nontemporal_load(keys + i) : 0;
+    }
+    uint32_t cnt = 0;
+    if (threadIdx.x < 256) {
+        const uint32_t dg = threadIdx.x;
+        const size_t at = (size_t)dg * nblocks + blockIdx.x;
+        const uint32_t mine = offsets[at];
+        const uint32_t nxt = at + 1 < (size_t)256 * nblocks ? offsets[at + 1] : (uint32_t)n;
+        cnt = nxt - mine;
+        gbase[dg] = mine;
+    }
+    uint32_t tot;
+    const uint32_t lo = block_excl_scan<kPkThreads>(cnt, lds16, tot);
+    if (threadIdx.x < 256) {
+        loff[threadIdx.x] = lo;
+#pragma unroll
+        for (int w = 0; w < kPkWaves; ++w) wcnt[w][threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const uint64_t lt_mask = (lane ? (~0ull >> (64 - lane)) : 0ull);
+    uint32_t *wc = wcnt[wid];
+    uint32_t dig[kPkItems], lp[kPkItems];
+#pragma unroll
+    for (int k = 0; k < kPkItems; ++k) {
+        const size_t i = base + wbase + k * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t dk = (uint32_t)(key[k] >> sh) & 0xFFu;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const uint64_t m = __ballot((dk >> b) & 1u);
+            peers &= ((dk >> b) & 1u) ? m : ~m;
+        }
+        const uint32_t before = wc[dk];
+        lp[k] = before + __popcll(peers & lt_mask);
+        dig[k] = valid ? dk : 0xFFFFFFFFu;
+        // every lane has read the counter before the group's first lane bumps it
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (valid && (peers & lt_mask) == 0) wc[dk] = before + __popcll(peers);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();
+    if (threadIdx.x < 256) {  // per-(wave, digit) start inside the block's sorted order
+        uint32_t acc = loff[threadIdx.x];
+#pragma unroll
+        for (int w = 0; w < kPkWaves; ++w) {
+            const uint32_t t = wcnt[w][threadIdx.x];
+            wcnt[w][threadIdx.x] = acc;
+            acc += t;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPkItems; ++k)
+        if (dig[k] != 0xFFFFFFFFu) stage[wc[dig[k]] + lp[k]] = key[k];
+    __syncthreads();
+    const uint32_t nrows = (uint32_t)min((size_t)kPkTile, n - base);
+#pragma unroll 4
+    for (uint32_t j = threadIdx.x; j < nrows; j += kPkThreads) {
+        const uint64_t kj = stage[j];
+        const uint32_t dj = (uint32_t)(kj >> sh) & 0xFFu;
+        __builtin_nontemporal_store(kj, keys_o + gbase[dj] + (j - loff[dj]));
+    }
+}
+
+// Sorted keys -> rows (every version, key order) + last-of-key flags.
+constexpr int kUnpackThreads = 256;
+template <int WT>  // key words 1..3, 0 = any (<= kPackMaxWords)
+__global__ __launch_bounds__(kUnpackThreads) void k_pk_unpack(
+    PackPlan P, size_t n, const uint64_t *keys, const uint32_t *gid_in, const uint64_t *words_in,
+    const uint64_t *lsn_in, size_t stride_in, uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o,
+    size_t stride_o, uint32_t *flags)
+{
+    const size_t i = (size_t)blockIdx.x * kUnpackThreads + threadIdx.x;
+    if (i >= n) return;
+    const int W = WT ? WT : P.W;
+    const uint64_t key = keys[i];
+    const uint64_t imask = P.I >= 64 ? ~0ull : (1ull << P.I) - 1;
+    uint64_t kb = key >> P.I;
+    const uint64_t idx = key & imask;
+    const bool last = i + 1 == n || (keys[i + 1] >> P.I) != kb;
+    const uint64_t lv = lsn_in[idx];
+    // limbs: row 0's value (the constant bits), varying bits expanded over it
+    uint64_t limb[kPackMaxWords + 1];
+#pragma unroll
+    for (int j = 0; j <= kPackMaxWords; ++j) {
+        if (j > W) break;
+        limb[j] = j == W ? (uint64_t)gid_in[0] : words_in[(size_t)j * stride_in];
+    }
+#pragma unroll
+    for (int l = kPackLimbs - 1; l >= 0; --l) {  // least significant varying limb first
+        if (l >= P.nl) continue;
+        const int b = P.bits[l];
+        const uint64_t part = b >= 64 ? kb : kb & ((1ull << b) - 1);
+        kb = b >= 64 ? 0 : kb >> b;
+        uint64_t mv[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) mv[q] = P.mv[l][q];
+        const int id = P.limb[l];
+        const uint64_t v = pk_expand(part, P.mask[l], mv);
+#pragma unroll
+        for (int j = 0; j <= kPackMaxWords; ++j)
+            if (j == id) limb[j] = (limb[j] & ~P.mask[l]) | v;
+    }
+    gid_o[i] = (uint32_t)limb[W];
+#pragma unroll
+    for (int j = 0; j < kPackMaxWords; ++j) {
+        if (j >= W) break;
+        words_o[(size_t)j * stride_o + i] = limb[j];
+    }
+    lsn_o[i] = lv;
+    flags[i] = last ? 1u : 0u;
+}
+
+}  // namespace
+
+size_t packed_scratch_bytes(size_t n)
+{
+    const size_t nblocks = (n + kPkTile - 1) / kPkTile;
+    return 256 * nblocks * sizeof(uint32_t) + scan_scratch_bytes(256 * nblocks) + 1024;
+}
+
+bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P)
+{
+    if (W > kPackMaxWords || n >= 0xFFFFFFFFull) return false;
+    *P = PackPlan{};
+    P->W = W;
+    int I = 1;
+    while (I < 32 && ((size_t)1 << I) < n) ++I;
+    P->I = I;
+    int B = 0, nl = 0;
+    // limb order, most significant first: gid, then word 0 .. W - 1
+    for (int k = 0; k <= W; ++k) {
+        const int id = k == 0 ? W : k - 1;
+        const uint64_t m = vary[id];
+        if (!m) continue;
+        P->limb[nl] = id;
+        P->mask[nl] = m;
+        P->bits[nl] = __builtin_popcountll(m);
+        compress_moves(m, P->mv[nl]);
+        B += P->bits[nl];
+        ++nl;
+    }
+    P->nl = nl;
+    P->B = B;
+    return B + I <= 64;
+}
+
+hipError_t packed_sort_rows(const PackPlan &P, size_t n, const uint32_t *gid, const uint64_t *words,
+                            const uint64_t *lsn, size_t stride, uint64_t *k0, uint64_t *k1,
+                            uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
+                            uint32_t *flags, void *scratch, size_t scratch_bytes, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    if (scratch_bytes < packed_scratch_bytes(n)) return hipErrorInvalidValue;
+    const uint32_t nblocks = (uint32_t)((n + kPkTile - 1) / kPkTile);
+    uint32_t *counts = (uint32_t *)scratch;
+    uint32_t *scan_tmp = counts + (size_t)256 * nblocks;
+    k_pk_pack<<<nblocks, kPkThreads, 0, s>>>(P, n, gid, words, stride, k0, counts, nblocks);
+    hipError_t e = hipGetLastError();
+    const int passes = (P.B + 7) / 8;
+    for (int p = 0; p < passes && e == hipSuccess; ++p) {
+        const int sh = P.I + 8 * p;
+        if (p > 0) k_pk_count<<<nblocks, kPkThreads, 0, s>>>(sh, n, k0, counts, nblocks);
+        e = scan_exclusive_u32(counts, (size_t)256 * nblocks, scan_tmp, s);
+        if (e != hipSuccess) break;
+        k_pk_scatter<<<nblocks, kPkThreads, 0, s>>>(sh, n, k0, k1, counts, nblocks);
+        e = hipGetLastError();
+        std::swap(k0, k1);
+    }
+    if (e != hipSuccess) return e;
+    const unsigned g = (unsigned)((n + kUnpackThreads - 1) / kUnpackThreads);
+#define HSC_UNPACK(WT_) k_pk_unpack<WT_><<<g, kUnpackThreads, 0, s>>>(P, n, k0, gid, words, lsn, stride, \
+                                                                    gid_o, words_o, lsn_o, stride_o, flags)
+    if (P.W == 1)
+        HSC_UNPACK(1);
+    else if (P.W == 2)
+        HSC_UNPACK(2);
+    else if (P.W == 3)
+        HSC_UNPACK(3);
+    else
+        HSC_UNPACK(0);
+#undef HSC_UNPACK
+    return hipGetLastError();
+}
+
+}  // namespace hsc

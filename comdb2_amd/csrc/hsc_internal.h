@@ -123,11 +123,44 @@ hipError_t radix_sort_rows(int W, size_t n, uint32_t *gid, uint64_t *words, uint
                            uint64_t *lsn_alt, void *scratch, size_t scratch_bytes,
                            bool *result_in_alt, uint64_t *vary_mask, hipStream_t s);
 size_t radix_scratch_bytes(size_t n, int W);
+// vary[j] (host, j <= W): bits of word j / of the gid (j == W) that differ
+// between rows (one kernel + readback; scratch >= 8 (W + 1) bytes)
+hipError_t vary_mask_rows(int W, size_t n, const uint32_t *gid, const uint64_t *words, size_t stride,
+                          void *scratch, uint64_t *vary, hipStream_t s);
+// radix_sort_rows with the vary masks already known
+hipError_t radix_sort_known(int W, size_t n, uint32_t *gid, uint64_t *words, uint64_t *lsn,
+                            size_t stride, uint32_t *gid_alt, uint64_t *words_alt,
+                            uint64_t *lsn_alt, void *scratch, size_t scratch_bytes,
+                            bool *result_in_alt, const uint64_t *vary, hipStream_t s);
 hipError_t dedupe_rows(int W, size_t n, const uint32_t *gid, const uint64_t *words,
                        const uint64_t *lsn, size_t stride_in, uint32_t *gid_out,
                        uint64_t *words_out, uint64_t *lsn_out, size_t stride_out,
                        uint32_t *flags, void *scratch, size_t scratch_bytes,
                        uint32_t *d_count, hipStream_t s);
+// dedupe_rows with the last-of-key flags already in flags (scanned in place)
+hipError_t dedupe_flagged(int W, size_t n, const uint32_t *gid, const uint64_t *words,
+                          const uint64_t *lsn, size_t stride_in, uint32_t *gid_out,
+                          uint64_t *words_out, uint64_t *lsn_out, size_t stride_out,
+                          uint32_t *flags, void *scratch, size_t scratch_bytes,
+                          uint32_t *d_count, hipStream_t s);
+// Packed-key sort (hsc_ingest.hip): rows whose varying key bits plus a row
+// index fit 64 bits sort as single words.
+constexpr int kPackMaxWords = 8;
+constexpr int kPackLimbs = kPackMaxWords + 1;
+struct PackPlan {
+    int W, I, B, nl;            // key words, index bits, packed key bits, varying limbs
+    int limb[kPackLimbs];       // most significant first: W = the gid, j < W = word j
+    int bits[kPackLimbs];
+    uint64_t mask[kPackLimbs];  // the limb's varying bits
+    uint64_t mv[kPackLimbs][6]; // their compress moves
+};
+bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P);  // false: does not fit
+size_t packed_scratch_bytes(size_t n);
+// sorted rows (every version, stride_o) + last-of-key flags; k0 / k1: n words each
+hipError_t packed_sort_rows(const PackPlan &P, size_t n, const uint32_t *gid, const uint64_t *words,
+                            const uint64_t *lsn, size_t stride, uint64_t *k0, uint64_t *k1,
+                            uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
+                            uint32_t *flags, void *scratch, size_t scratch_bytes, hipStream_t s);
 size_t scan_scratch_bytes(size_t n);
 hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, int ngroups,
                            uint64_t *tmax, const uint32_t *group_table,

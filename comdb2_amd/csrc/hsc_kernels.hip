@@ -54,13 +54,22 @@ __global__ __launch_bounds__(256) void k_vary_mask(int W, size_t n, const uint32
                                                    const uint64_t *words, size_t stride,
                                                    unsigned long long *mask)
 {
+    constexpr int U = 8;  // independent loads in flight per thread
     __shared__ uint64_t part[256 / 64];
     for (int j = 0; j <= W; ++j) {
         const uint64_t ref = j < W ? words[(size_t)j * stride] : gid[0];
         uint64_t m = 0;
-        for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-             i += (size_t)gridDim.x * blockDim.x)
-            m |= (j < W ? words[(size_t)j * stride + i] : gid[i]) ^ ref;
+        for (size_t i0 = (size_t)blockIdx.x * blockDim.x * U + threadIdx.x; i0 < n;
+             i0 += (size_t)gridDim.x * blockDim.x * U) {
+            uint64_t v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const size_t i = i0 + (size_t)u * blockDim.x;
+                v[u] = i >= n ? ref : j < W ? words[(size_t)j * stride + i] : gid[i];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) m |= v[u] ^ ref;
+        }
         for (int o = 32; o > 0; o >>= 1) m |= __shfl_xor(m, o, 64);
         // one atomic per block and word: all blocks OR into the same W + 1
         // words, so per-wave atomics would queue behind each other
@@ -309,33 +318,52 @@ size_t radix_scratch_bytes(size_t n, int W)
            scan_scratch_bytes(256 * nblocks) + 1024;
 }
 
+hipError_t vary_mask_rows(int W, size_t n, const uint32_t *gid, const uint64_t *words, size_t stride,
+                          void *scratch, uint64_t *vary, hipStream_t s)
+{
+    for (int j = 0; j <= W; ++j) vary[j] = 0;
+    if (n <= 1) return hipSuccess;
+    unsigned long long *dmask = (unsigned long long *)scratch;  // [W + 1]
+    hipError_t e = hipMemsetAsync(dmask, 0, 8 * ((size_t)W + 1), s);
+    if (e != hipSuccess) return e;
+    const unsigned hgrid = (unsigned)std::min<size_t>((n + 2047) / 2048, 2048);
+    k_vary_mask<<<hgrid, 256, 0, s>>>(W, n, gid, words, stride, dmask);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    e = hipMemcpyAsync(vary, dmask, 8 * ((size_t)W + 1), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return e;
+}
+
 hipError_t radix_sort_rows(int W, size_t n, uint32_t *gid, uint64_t *words, uint64_t *lsn,
                            size_t stride, uint32_t *gid_alt, uint64_t *words_alt,
                            uint64_t *lsn_alt, void *scratch, size_t scratch_bytes,
                            bool *result_in_alt, uint64_t *vary_mask, hipStream_t s)
 {
+    uint64_t hm[kMaxWords + 1];
     *result_in_alt = false;
+    if (scratch_bytes < radix_scratch_bytes(n, W)) return hipErrorInvalidValue;
+    hipError_t e = vary_mask_rows(W, n, gid, words, stride, scratch, hm, s);
+    if (e != hipSuccess) return e;
     if (vary_mask)
-        for (int j = 0; j <= W; ++j) vary_mask[j] = 0;
+        for (int j = 0; j <= W; ++j) vary_mask[j] = hm[j];
+    return radix_sort_known(W, n, gid, words, lsn, stride, gid_alt, words_alt, lsn_alt, scratch,
+                            scratch_bytes, result_in_alt, hm, s);
+}
+
+hipError_t radix_sort_known(int W, size_t n, uint32_t *gid, uint64_t *words, uint64_t *lsn,
+                            size_t stride, uint32_t *gid_alt, uint64_t *words_alt,
+                            uint64_t *lsn_alt, void *scratch, size_t scratch_bytes,
+                            bool *result_in_alt, const uint64_t *hm, hipStream_t s)
+{
+    *result_in_alt = false;
     if (n <= 1) return hipSuccess;
     if (scratch_bytes < radix_scratch_bytes(n, W)) return hipErrorInvalidValue;
     const int ndig = 8 * W + 4;
     const uint32_t nblocks = (uint32_t)((n + kSortTile - 1) / kSortTile);
-    unsigned long long *dmask = (unsigned long long *)scratch;  // [W + 1]
     uint32_t *counts = (uint32_t *)scratch + (size_t)ndig * 256;
     uint32_t *scan_tmp = counts + (size_t)256 * nblocks;
-    hipError_t e = hipMemsetAsync(dmask, 0, 8 * ((size_t)W + 1), s);
-    if (e != hipSuccess) return e;
-    const unsigned hgrid = (unsigned)std::min<size_t>((n + 255) / 256, 1024);
-    k_vary_mask<<<hgrid, 256, 0, s>>>(W, n, gid, words, stride, dmask);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    unsigned long long hm[kMaxWords + 1];
-    e = hipMemcpyAsync(hm, dmask, 8 * ((size_t)W + 1), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) return e;
-    if (vary_mask)
-        for (int j = 0; j <= W; ++j) vary_mask[j] = hm[j];
+    hipError_t e = hipSuccess;
     bool alt = false;
     uint32_t *g0 = gid, *g1 = gid_alt;
     uint64_t *w0 = words, *w1 = words_alt, *l0 = lsn, *l1 = lsn_alt;
@@ -408,24 +436,34 @@ __global__ void k_copy_last_flag(const uint32_t *flags, size_t n, uint32_t *out)
     out[0] = flags[n - 1];
 }
 
-hipError_t dedupe_rows(int W, size_t n, const uint32_t *gid, const uint64_t *words,
-                       const uint64_t *lsn, size_t stride_in, uint32_t *gid_out,
-                       uint64_t *words_out, uint64_t *lsn_out, size_t stride_out,
-                       uint32_t *flags, void *scratch, size_t scratch_bytes,
-                       uint32_t *d_count, hipStream_t s)
+hipError_t dedupe_flagged(int W, size_t n, const uint32_t *gid, const uint64_t *words,
+                          const uint64_t *lsn, size_t stride_in, uint32_t *gid_out,
+                          uint64_t *words_out, uint64_t *lsn_out, size_t stride_out,
+                          uint32_t *flags, void *scratch, size_t scratch_bytes,
+                          uint32_t *d_count, hipStream_t s)
 {
     if (n == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
     if (scratch_bytes < scan_scratch_bytes(n) + 16) return hipErrorInvalidValue;
     uint32_t *last = (uint32_t *)scratch;
     uint32_t *tmp = last + 4;
     const unsigned g = (unsigned)((n + 255) / 256);
-    k_flag_last<<<g, 256, 0, s>>>(W, n, gid, words, stride_in, flags);
     k_copy_last_flag<<<1, 1, 0, s>>>(flags, n, last);
     hipError_t e = scan_u32(flags, n, tmp, s);
     if (e != hipSuccess) return e;
     k_compact<<<g, 256, 0, s>>>(W, n, gid, words, lsn, stride_in, flags, last, gid_out, words_out,
                                 lsn_out, stride_out, d_count);
     return hipGetLastError();
+}
+
+hipError_t dedupe_rows(int W, size_t n, const uint32_t *gid, const uint64_t *words,
+                       const uint64_t *lsn, size_t stride_in, uint32_t *gid_out,
+                       uint64_t *words_out, uint64_t *lsn_out, size_t stride_out,
+                       uint32_t *flags, void *scratch, size_t scratch_bytes,
+                       uint32_t *d_count, hipStream_t s)
+{
+    if (n) k_flag_last<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(W, n, gid, words, stride_in, flags);
+    return dedupe_flagged(W, n, gid, words, lsn, stride_in, gid_out, words_out, lsn_out, stride_out,
+                          flags, scratch, scratch_bytes, d_count, s);
 }
 
 // ---- summaries: group spans, tile maxima, sparse table, table maxima ------

@@ -131,7 +131,7 @@ EXPORTS = [
     "hsc_ctx_create", "hsc_ctx_destroy", "hsc_set_stream", "hsc_last_error", "hsc_device_count",
     "hsc_window_ingest_log", "hsc_window_append", "hsc_window_set_end", "hsc_window_reset",
     "hsc_window_build", "hsc_register_group", "hsc_window_ingest_device", "hsc_window_words",
-    "hsc_window_keys", "hsc_window_end", "hsc_window_max_commit", "hsc_table_id",
+    "hsc_window_keys", "hsc_window_end", "hsc_window_max_commit", "hsc_window_export", "hsc_table_id",
     "hsc_table_name", "hsc_group_info", "hsc_table_max", "hsc_merge_table_max",
     "hip_bdb_osql_serial_check", "hip_serial_check_batch", "hsc_check_readsets",
     "hsc_marshal_readsets", "hsc_probe_device", "hsc_pack_verdicts", "hsc_or_bitmaps",
@@ -182,6 +182,7 @@ def load() -> C.CDLL:
         "hsc_window_keys": (C.c_size_t, [_p]),
         "hsc_window_end": (C.c_uint64, [_p]),
         "hsc_window_max_commit": (C.c_uint64, [_p]),
+        "hsc_window_export": (C.c_long, [_p, C.c_int, _p, _p, _p, C.c_size_t]),
         "hsc_table_id": (C.c_int, [_p, C.c_char_p]),
         "hsc_table_name": (C.c_char_p, [_p, C.c_int]),
         "hsc_group_info": (C.c_int, [_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
@@ -565,6 +566,23 @@ class Validator:
     @property
     def end_lsn(self) -> int:
         return self.lib.hsc_window_end(self.ctx)
+
+    def export_window(self, all_versions: bool = False):
+        """(gid u32[n], words u64[W, n], lsn u64[n]) of the built window in
+        (group, key) order: the newest version per key, or every version
+        (hsc_window_export; the delta run is folded in first)."""
+        n = self.lib.hsc_window_export(self.ctx, int(all_versions), None, None, None, 0)
+        self._chk(min(int(n), 0), "hsc_window_export")
+        W = self.words
+        gid = np.zeros(max(n, 1), np.uint32)
+        words = np.zeros((W, max(n, 1)), np.uint64)
+        lsn = np.zeros(max(n, 1), np.uint64)
+        if n:
+            m = self.lib.hsc_window_export(self.ctx, int(all_versions), gid.ctypes.data,
+                                           words.ctypes.data, lsn.ctypes.data, n)
+            self._chk(min(int(m), 0), "hsc_window_export")
+            assert m == n
+        return gid[:n], words[:, :n], lsn[:n]
 
     # checks
     def check_readsets(self, rs: ReadSets) -> np.ndarray:

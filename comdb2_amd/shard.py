@@ -309,7 +309,7 @@ def sampled_splitters(local_keys: np.ndarray, range_keys: np.ndarray, world: int
     ir = (np.arange(s_r) * len(rk)) // max(s_r, 1)
     keys = np.concatenate([uk[iw], rk[ir]])
     wts = np.concatenate([row_w, np.full(s_r, w_range * len(rk) / max(s_r, 1))])
-    if world > 1 and dist.is_initialized():
+    if dist.is_initialized():  # world 1 with a process group: a one-rank gather (RCCL smoke)
         n = 2 * samples
         kb = torch.full((n,), INT64_MAX, dtype=torch.int64)
         wb = torch.zeros(n, dtype=torch.float64)
@@ -350,7 +350,7 @@ def exchange_rows(keys: np.ndarray, lsn: np.ndarray, splitters: np.ndarray, grou
     import torch
     import torch.distributed as dist
     world = len(splitters) + 1
-    if world == 1 or not dist.is_initialized():
+    if not dist.is_initialized():
         return keys, lsn
     own = np.searchsorted(splitters, keys, side="right")
     order = np.argsort(own, kind="stable")

@@ -297,7 +297,8 @@ int hsc_register_group(hsc_ctx *ctx, const char *tbname, int idxnum, int keylen)
 /* Device-side ingest of pre-padded keys (bench / sharded driver path):
  * gid[n], words[words][n], lsn[n] are DEVICE pointers, keys already packed as
  * described for hsc_probe_batch; gid values come from hsc_register_group.
- * Replaces the window. */
+ * Rows are versions in log order: of equal (gid, key) rows the last one is
+ * the key's newest version.  Replaces the window. */
 int hsc_window_ingest_device(hsc_ctx *ctx, size_t n, int words,
                              const uint32_t *gid, const uint64_t *key_words,
                              const uint64_t *lsn, uint64_t end_lsn);
@@ -341,6 +342,15 @@ int hsc_window_words(hsc_ctx *ctx);          /* key words per key (>= 1)     */
 size_t hsc_window_keys(hsc_ctx *ctx);        /* distinct (group, key) rows   */
 uint64_t hsc_window_end(hsc_ctx *ctx);
 uint64_t hsc_window_max_commit(hsc_ctx *ctx);
+/* Window snapshot (checkpoint of the resident state; the reference keeps
+ * none -- its state is the log): the rows of the built window in (group, key)
+ * order, after folding any delta run.  all_versions = 0: one row per (group,
+ * key), its newest version; 1: every version.  gid[cap], key_words[words *
+ * cap] (word j of row i at [j * cap + i], big-endian key order), lsn[cap];
+ * all three NULL returns only the count.  Returns the row count (> cap:
+ * nothing copied) or a negative HSC_E* code. */
+long hsc_window_export(hsc_ctx *ctx, int all_versions, uint32_t *gid, uint64_t *key_words,
+                       uint64_t *lsn, size_t cap);
 int hsc_table_id(hsc_ctx *ctx, const char *tbname); /* -1 if never written   */
 const char *hsc_table_name(hsc_ctx *ctx, int table_id); /* NULL if unknown   */
 /* Key group gid -> (table id, index, key length); 0 or HSC_EINVAL. */
