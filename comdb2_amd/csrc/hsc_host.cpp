@@ -142,6 +142,7 @@ struct Stage {
 
 constexpr int kMarshalTxns = 2048;         // read sets per marshal work item
 constexpr size_t kTailPackMax = 1u << 18;  // fused join: verdict bytes by its last block up to this
+enum { kFoldIdle = 0, kFoldRunning = 1, kFoldDone = 2 };  // hsc_ctx::fold_state
 constexpr int kMarshalParallelMin = 4096;  // fewer read sets: marshal on the caller's thread
 constexpr int kPipeTxns = 32768;           // read sets per pipeline chunk of a large batch
 
@@ -206,6 +207,23 @@ struct hsc_ctx {
     bool app_tmax = false;           // table maxima changed since the last upload
     HBuf h_app;                      // pinned staging of appended rows / table maxima
     ProbeView raw_probe{};           // the batch being probed, untransformed (delta probe)
+    // background fold: once the live run holds fold_rows rows it
+    // is frozen, and a shadow context rebuilds the main window from the main
+    // window's versions + the frozen run on its own stream and host thread;
+    // checks probe main + frozen + live runs until a call after the build
+    // swaps the shadow's window in (fold_poll).  fold_bg = false: the run is
+    // merged inline by the next check instead (the pre-fold behaviour).
+    hsc_ctx *shadow = nullptr;
+    std::thread fold_thread;
+    std::atomic<int> fold_state{0};  // kFoldIdle / kFoldRunning / kFoldDone
+    int fold_rc = 0;
+    DBuf f_dgid, f_dwords, f_dlsn, f_dbmax;  // the frozen run (fn rows, stride dcap)
+    size_t fn = 0;
+    size_t fold_rows = kDeltaCap / 2;
+    bool fold_bg = true;
+    hipEvent_t fold_ev = nullptr;  // the old window's last readers (the next fold waits)
+    uint64_t folds_started = 0, folds_swapped = 0, folds_inline = 0;
+    float fold_ms = 0;  // build time of the last background fold
 
     // device window
     int W = 1;
@@ -429,8 +447,11 @@ static int group_id_or_add(hsc_ctx *c, int tid, int ix, int klen)
     return g;
 }
 
+static void fold_discard(hsc_ctx *c);
+
 static void clear_window(hsc_ctx *c)
 {
+    fold_discard(c);
     c->h_gid.clear();
     c->h_keyoff.clear();
     c->h_keys.clear();
@@ -1104,13 +1125,22 @@ static DeltaView delta_view(const hsc_ctx *c)
 // asynchronous on c->stream) and the table maxima into d_table_max.  A delta
 // past kDeltaCap, or a key longer than the window's words, schedules a merge
 // into the main window instead (at the next check).
+static int fold_start(hsc_ctx *c);
+static int fold_finish(hsc_ctx *c, bool wait);
+
 static int flush_appends(hsc_ctx *c)
 {
     if (!c->live || c->host_only) return HSC_OK;
     hipStream_t s = c->stream;
+    HIPCHK_RC(c, fold_finish(c, false));
     const size_t k = c->app_gid.size();
-    if (k && (window_words(c) > c->W || c->dn + k > kDeltaCap || c->merge_pending ||
-              c->groups.size() > c->ng_built)) {
+    const bool sync_only = window_words(c) > c->W || c->merge_pending || c->groups.size() > c->ng_built;
+    if (k && !sync_only && c->fold_bg && c->dn + k > kDeltaCap && k <= kDeltaCap) {
+        // the live run is full: wait for a running fold, then fold the run
+        HIPCHK_RC(c, fold_finish(c, true));
+        if (c->dn + k > kDeltaCap && c->dn && !c->merge_pending) HIPCHK_RC(c, fold_start(c));
+    }
+    if (k && (sync_only || c->merge_pending || c->dn + k > kDeltaCap)) {
         c->merge_pending = true;
         c->dirty = true;  // rows stay in app_* for merge_delta (or in h_* for a host rebuild)
         return HSC_OK;
@@ -1168,6 +1198,14 @@ static int flush_appends(hsc_ctx *c)
     c->dcur = o;
     c->dn += k;
     c->app_gid.clear(), c->app_keys.clear(), c->app_koff.clear(), c->app_lsn.clear();
+    if (c->dn >= c->fold_rows) {
+        if (!c->fold_bg) {  // inline: the next check folds
+            c->merge_pending = true;
+            c->dirty = true;
+        } else if (c->fold_state.load(std::memory_order_acquire) == kFoldIdle) {
+            HIPCHK_RC(c, fold_start(c));
+        }
+    }
     return HSC_OK;
 }
 
@@ -1178,11 +1216,14 @@ static int flush_appends(hsc_ctx *c)
 static int merge_delta(hsc_ctx *c)
 {
     hipStream_t s = c->stream;
+    (void)fold_finish(c, true);  // a failed fold leaves its rows in the frozen run, merged below
+    c->folds_inline++;
     HIPCHK(c, wait_lanes(c));
     const int W0 = c->W, W = std::max(c->W, window_words(c));
     size_t k = 0;
     HIPCHK_RC(c, stage_appends(c, W, &k));
-    const size_t na = c->n_all, nd = c->dn, n_in = na + nd + k;
+    const size_t nf = c->fn;
+    const size_t na = c->n_all + nf, nd = c->dn, n_in = na + nd + k;
     if (n_in >= 0xFFFFFFFFull) return fail(c, HSC_EINVAL, "window too large");
     const size_t cap = window_cap(n_in);
     DBuf g, wd, l;
@@ -1190,12 +1231,21 @@ static int merge_delta(hsc_ctx *c)
     HIPCHK(c, wd.ensure(8 * (size_t)W * cap));
     HIPCHK(c, l.ensure(8 * cap));
     if (W > W0) HIPCHK(c, hipMemsetAsync(wd.p, 0, 8 * (size_t)W * cap, s));
-    if (na) {
-        HIPCHK(c, hipMemcpyAsync(g.p, c->d_gid2.p, 4 * na, hipMemcpyDeviceToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(l.p, c->d_lsn2.p, 8 * na, hipMemcpyDeviceToDevice, s));
+    const size_t nm = c->n_all;  // the main window's versions, then the frozen run's rows
+    if (nm) {
+        HIPCHK(c, hipMemcpyAsync(g.p, c->d_gid2.p, 4 * nm, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(l.p, c->d_lsn2.p, 8 * nm, hipMemcpyDeviceToDevice, s));
         for (int j = 0; j < W0; ++j)
             HIPCHK(c, hipMemcpyAsync(wd.as<uint64_t>() + (size_t)j * cap,
-                                     c->d_words2.as<uint64_t>() + (size_t)j * c->cap, 8 * na,
+                                     c->d_words2.as<uint64_t>() + (size_t)j * c->cap, 8 * nm,
+                                     hipMemcpyDeviceToDevice, s));
+    }
+    if (nf) {
+        HIPCHK(c, hipMemcpyAsync(g.as<uint32_t>() + nm, c->f_dgid.p, 4 * nf, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(l.as<uint64_t>() + nm, c->f_dlsn.p, 8 * nf, hipMemcpyDeviceToDevice, s));
+        for (int j = 0; j < W0; ++j)
+            HIPCHK(c, hipMemcpyAsync(wd.as<uint64_t>() + (size_t)j * cap + nm,
+                                     c->f_dwords.as<uint64_t>() + (size_t)j * c->dcap, 8 * nf,
                                      hipMemcpyDeviceToDevice, s));
     }
     if (nd) {
@@ -1217,6 +1267,7 @@ static int merge_delta(hsc_ctx *c)
                                  hipMemcpyHostToDevice, s));
     }
     HIPCHK(c, hipStreamSynchronize(s));  // the staging and the old rows are consumed
+    c->fn = 0;
     std::swap(c->d_gid, g);
     std::swap(c->d_words, wd);
     std::swap(c->d_lsn, l);
@@ -1226,12 +1277,180 @@ static int merge_delta(hsc_ctx *c)
     return device_build(c, n_in);
 }
 
+// ---- background fold -------------------------------------------------------
+// The device window: every field a build sets and a probe reads (swapped
+// whole between a context and its shadow when a background fold finishes).
+static void swap_window(hsc_ctx *a, hsc_ctx *b)
+{
+    using std::swap;
+    swap(a->W, b->W), swap(a->n, b->n), swap(a->cap, b->cap), swap(a->n_all, b->n_all);
+    swap(a->ng_built, b->ng_built);
+    swap(a->ntiles, b->ntiles), swap(a->log2T, b->log2T), swap(a->levels, b->levels);
+    swap(a->narrow, b->narrow), swap(a->lw, b->lw), swap(a->tz, b->tz);
+    swap(a->d_nkeys, b->d_nkeys), swap(a->d_nmaxs, b->d_nmaxs), swap(a->d_nbase, b->d_nbase);
+    swap(a->nv, b->nv), swap(a->wn, b->wn);
+    swap(a->d_nzero, b->d_nzero), swap(a->d_ntmax, b->d_ntmax), swap(a->d_nsp_g, b->d_nsp_g);
+    swap(a->d_nsp_w, b->d_nsp_w), swap(a->d_ngs, b->d_ngs), swap(a->d_nscratch, b->d_nscratch);
+    swap(a->ntiles32, b->ntiles32), swap(a->d_trad2, b->d_trad2), swap(a->d_commits, b->d_commits);
+    swap(a->d_cdir, b->d_cdir), swap(a->d_tdir, b->d_tdir), swap(a->d_trad, b->d_trad);
+    swap(a->d_key32, b->d_key32), swap(a->d_rank32, b->d_rank32);
+    for (int i = 0; i < 4; ++i) swap(a->d_ctmp[i], b->d_ctmp[i]);
+    swap(a->cdir, b->cdir), swap(a->tdir, b->tdir), swap(a->trad_m, b->trad_m);
+    swap(a->trad_log, b->trad_log), swap(a->ncommit, b->ncommit);
+    swap(a->commit_span[0], b->commit_span[0]), swap(a->commit_span[1], b->commit_span[1]);
+    swap(a->rank_lsn32, b->rank_lsn32), swap(a->nt_sorted, b->nt_sorted), swap(a->nt_fused, b->nt_fused);
+    swap(a->ct_sorted, b->ct_sorted), swap(a->ct_fused, b->ct_fused), swap(a->rank_base, b->rank_base);
+    swap(a->d_gid, b->d_gid), swap(a->d_words, b->d_words), swap(a->d_lsn, b->d_lsn);
+    swap(a->d_gid2, b->d_gid2), swap(a->d_words2, b->d_words2), swap(a->d_lsn2, b->d_lsn2);
+    swap(a->d_flags, b->d_flags), swap(a->d_scratch, b->d_scratch);
+    swap(a->d_pk[0], b->d_pk[0]), swap(a->d_pk[1], b->d_pk[1]), swap(a->packed_sort, b->packed_sort);
+    swap(a->d_gstart, b->d_gstart), swap(a->d_gend, b->d_gend), swap(a->d_tmax, b->d_tmax);
+    swap(a->d_table_max, b->d_table_max), swap(a->d_group_table, b->d_group_table);
+    swap(a->d_count, b->d_count), swap(a->d_sp_g, b->d_sp_g), swap(a->d_sp_w, b->d_sp_w);
+    swap(a->compact, b->compact), swap(a->ct, b->ct), swap(a->wc, b->wc);
+    swap(a->d_cmask, b->d_cmask), swap(a->d_cpat, b->d_cpat), swap(a->d_cmv, b->d_cmv);
+    swap(a->d_cbits, b->d_cbits), swap(a->d_cwords, b->d_cwords), swap(a->d_ctmax, b->d_ctmax);
+    swap(a->d_csp_g, b->d_csp_g), swap(a->d_csp_w, b->d_csp_w), swap(a->ct_maxbits, b->ct_maxbits);
+    swap(a->ctiles, b->ctiles), swap(a->ctv, b->ctv);
+    swap(a->d_ckey, b->d_ckey), swap(a->d_crank, b->d_crank), swap(a->d_cfirst, b->d_cfirst);
+    swap(a->d_crel, b->d_crel), swap(a->d_ctrad, b->d_ctrad), swap(a->d_ctb, b->d_ctb);
+}
+
+static DeltaView frozen_view(const hsc_ctx *c)
+{
+    DeltaView d{};
+    d.gid = c->f_dgid.as<uint32_t>();
+    d.words = c->f_dwords.as<uint64_t>();
+    d.lsn = c->f_dlsn.as<uint64_t>();
+    d.bmax = c->f_dbmax.as<uint64_t>();
+    d.stride = c->dcap;
+    d.n = (uint32_t)c->fn;
+    d.W = c->W;
+    return d;
+}
+
+static int shadow_ctx(hsc_ctx *c)
+{
+    if (c->shadow) return HSC_OK;
+    hsc_ctx *s = new (std::nothrow) hsc_ctx();
+    if (!s) return fail(c, HSC_ENOMEM, "fold context");
+    s->device = c->device;
+    if (hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking) != hipSuccess) {
+        delete s;
+        return fail(c, HSC_EDEVICE, "fold stream");
+    }
+    s->stream = s->own_stream;
+    c->shadow = s;
+    if (!c->fold_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fold_ev, hipEventDisableTiming));
+    return HSC_OK;
+}
+
+// Freeze the live run and start rebuilding the main window with it in the
+// background: the shadow's stream copies the main window's versions (d_*2)
+// and the frozen rows after everything queued on c->stream so far (the run's
+// last merge, and the readers of the shadow's buffers -- the window before
+// the last swap), and a host thread runs the build.
+static int fold_start(hsc_ctx *c)
+{
+    HIPCHK_RC(c, shadow_ctx(c));
+    hsc_ctx *s = c->shadow;
+    std::swap(c->d_dgid[c->dcur], c->f_dgid);
+    std::swap(c->d_dwords[c->dcur], c->f_dwords);
+    std::swap(c->d_dlsn[c->dcur], c->f_dlsn);
+    std::swap(c->d_dbmax, c->f_dbmax);
+    c->fn = c->dn;
+    c->dn = 0;
+    s->groups = c->groups;  // what device_build reads of the dictionaries
+    s->table_names = c->table_names;
+    s->h_table_max = c->h_table_max;
+    s->layout = c->layout;
+    s->W = c->W;
+    const size_t nm = c->n_all, nf = c->fn, n_in = nm + nf;
+    s->cap = window_cap(n_in);
+    const int W = c->W;
+    HIPCHK(c, s->d_gid.ensure(4 * s->cap));
+    HIPCHK(c, s->d_words.ensure(8 * (size_t)W * s->cap));
+    HIPCHK(c, s->d_lsn.ensure(8 * s->cap));
+    HIPCHK(c, hipEventRecord(c->fold_ev, c->stream));
+    hipStream_t ss = s->stream;
+    HIPCHK(c, hipStreamWaitEvent(ss, c->fold_ev, 0));
+    HIPCHK(c, hipMemcpyAsync(s->d_gid.p, c->d_gid2.p, 4 * nm, hipMemcpyDeviceToDevice, ss));
+    HIPCHK(c, hipMemcpyAsync(s->d_lsn.p, c->d_lsn2.p, 8 * nm, hipMemcpyDeviceToDevice, ss));
+    HIPCHK(c, hipMemcpyAsync(s->d_gid.as<uint32_t>() + nm, c->f_dgid.p, 4 * nf, hipMemcpyDeviceToDevice, ss));
+    HIPCHK(c, hipMemcpyAsync(s->d_lsn.as<uint64_t>() + nm, c->f_dlsn.p, 8 * nf, hipMemcpyDeviceToDevice, ss));
+    for (int j = 0; j < W; ++j) {
+        uint64_t *dst = s->d_words.as<uint64_t>() + (size_t)j * s->cap;
+        HIPCHK(c, hipMemcpyAsync(dst, c->d_words2.as<uint64_t>() + (size_t)j * c->cap, 8 * nm,
+                                 hipMemcpyDeviceToDevice, ss));
+        HIPCHK(c, hipMemcpyAsync(dst + nm, c->f_dwords.as<uint64_t>() + (size_t)j * c->dcap, 8 * nf,
+                                 hipMemcpyDeviceToDevice, ss));
+    }
+    c->fold_rc = HSC_OK;
+    c->fold_state.store(kFoldRunning, std::memory_order_release);
+    c->folds_started++;
+    try {
+        c->fold_thread = std::thread([c, s, n_in] {
+            (void)hipSetDevice(s->device);
+            const int rc = device_build(s, n_in);
+            c->fold_rc = rc;
+            c->fold_state.store(kFoldDone, std::memory_order_release);
+        });
+    } catch (...) {
+        c->fold_state.store(kFoldIdle, std::memory_order_release);
+        (void)hipStreamSynchronize(ss);
+        c->merge_pending = c->dirty = true;  // the frozen run is merged inline instead
+        return HSC_OK;
+    }
+    return HSC_OK;
+}
+
+// A finished background fold (or, wait = true, a running one once done):
+// swap the shadow's window in.  On failure the frozen run stays probed and
+// the next check merges it inline.
+static int fold_finish(hsc_ctx *c, bool wait)
+{
+    const int st = c->fold_state.load(std::memory_order_acquire);
+    if (st == kFoldIdle || (st == kFoldRunning && !wait)) return HSC_OK;
+    c->fold_thread.join();
+    c->fold_state.store(kFoldIdle, std::memory_order_relaxed);
+    hsc_ctx *s = c->shadow;
+    if (c->fold_rc != HSC_OK) {
+        c->merge_pending = c->dirty = true;
+        (void)fail(c, c->fold_rc, ("background fold: " + s->err).c_str());
+        return HSC_OK;
+    }
+    HIPCHK(c, wait_lanes(c));  // batches of other streams finish on the old window
+    swap_window(c, s);
+    // table maxima raised while the fold ran (the shadow's are as of its start)
+    const int nt = (int)c->table_names.size();
+    for (int t = 0; t < nt && t < (int)s->h_table_max.size(); ++t)
+        c->h_table_max[t] = std::max(c->h_table_max[t], s->h_table_max[t]);
+    HIPCHK(c, c->d_table_max.ensure(8 * (size_t)std::max(nt, 1)));
+    if (nt) HIPCHK(c, hipMemcpy(c->d_table_max.p, c->h_table_max.data(), 8 * (size_t)nt, hipMemcpyHostToDevice));
+    c->app_tmax = false;
+    c->fn = 0;
+    HIPCHK(c, hipEventRecord(c->fold_ev, c->stream));  // the old window's last readers
+    c->folds_swapped++;
+    c->fold_ms = s->last.ingest_ms;
+    return HSC_OK;
+}
+
+static void fold_discard(hsc_ctx *c)
+{
+    if (c->fold_state.load(std::memory_order_acquire) != kFoldIdle) {
+        c->fold_thread.join();
+        c->fold_state.store(kFoldIdle, std::memory_order_relaxed);
+    }
+    c->fn = 0;
+}
+
 static int ensure_built(hsc_ctx *c)
 {
     if (c->host_only) {  // dictionaries + marshalling only
         c->W = window_words(c);
         return HSC_OK;
     }
+    HIPCHK_RC(c, fold_finish(c, false));
     // A group first seen after the build (the first write to an index, or
     // hsc_register_group) has no entry in the per-group tables, which are
     // sized at the build: the marshal would emit probes with its gid, so the
@@ -2121,8 +2340,9 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
 // build) into the path's verdict target, before its pack.
 static int probe_delta(hsc_ctx *c, uint8_t *target)
 {
-    if (!c->dn || !c->raw_probe.n) return HSC_OK;
-    HIPCHK(c, launch_probe_delta(delta_view(c), c->raw_probe, target, c->stream));
+    if (!c->raw_probe.n) return HSC_OK;
+    if (c->fn) HIPCHK(c, launch_probe_delta(frozen_view(c), c->raw_probe, target, c->stream));
+    if (c->dn) HIPCHK(c, launch_probe_delta(delta_view(c), c->raw_probe, target, c->stream));
     return HSC_OK;
 }
 
@@ -2385,9 +2605,10 @@ static int run_small(hsc_ctx *c, Stage &st, int *rc_out)
     NarrowView nv = c->nv;
     nv.table_max = c->d_table_max.as<uint64_t>();
     nv.ntables = (uint32_t)c->table_names.size();
-    DeltaView d{};
+    DeltaView d{}, d2{};
     if (c->dn) d = delta_view(c);
-    HIPCHK(c, launch_small_narrow(nv, d, p, dio + vo, c->small_blocks.as<uint32_t>(),
+    if (c->fn) d2 = frozen_view(c);
+    HIPCHK(c, launch_small_narrow(nv, d, d2, p, dio + vo, c->small_blocks.as<uint32_t>(),
                                   (uint32_t *)(dio + dn), seq, s));
     // poll the done word; every few thousand spins ask the stream whether it
     // failed (a fault never releases the word)
@@ -2504,9 +2725,14 @@ void hsc_ctx_destroy(hsc_ctx *c)
         return;
     }
     (void)hipSetDevice(c->device);
+    fold_discard(c);
+    if (c->shadow) hsc_ctx_destroy(c->shadow);
+    c->shadow = nullptr;
     (void)hipStreamSynchronize(c->stream);
     for (auto &L : c->lanes)
         if (L.done) (void)hipEventSynchronize(L.done);
+    for (DBuf *b : {&c->f_dgid, &c->f_dwords, &c->f_dlsn, &c->f_dbmax, &c->d_pk[0], &c->d_pk[1]}) b->release();
+    if (c->fold_ev) (void)hipEventDestroy(c->fold_ev);
     DBuf *bufs[] = {&c->d_gid, &c->d_words, &c->d_lsn, &c->d_gid2, &c->d_words2, &c->d_lsn2,
                     &c->d_flags, &c->d_scratch, &c->d_gstart, &c->d_gend, &c->d_tmax,
                     &c->d_table_max, &c->d_group_table, &c->d_count, &c->d_sp_g, &c->d_sp_w,
@@ -2627,7 +2853,27 @@ int hsc_window_append_raw(hsc_ctx *c, const hsc_raw_log *raw)
     return hsc_window_append_log(c, lg);
 }
 
-size_t hsc_window_delta_rows(hsc_ctx *c) { return c ? c->dn : 0; }
+size_t hsc_window_delta_rows(hsc_ctx *c) { return c ? c->dn + c->fn : 0; }
+
+int hsc_set_fold(hsc_ctx *c, size_t rows, int background)
+{
+    if (!c || rows > kDeltaCap) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->fold_rows = rows ? rows : kDeltaCap / 2;
+    c->fold_bg = background != 0;
+    return HSC_OK;
+}
+
+int hsc_fold_stats(hsc_ctx *c, uint64_t out[4])
+{
+    if (!c || !out) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    out[0] = c->folds_started;
+    out[1] = c->folds_swapped;
+    out[2] = c->folds_inline;
+    out[3] = (uint64_t)(c->fold_ms * 1000.0f);
+    return HSC_OK;
+}
 
 int hsc_window_set_end(hsc_ctx *c, uint64_t end_lsn)
 {

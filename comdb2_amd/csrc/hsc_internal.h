@@ -239,7 +239,8 @@ hipError_t narrow_codes(const NarrowView &nv, const ProbeView &p, uint64_t *lo64
 // The small-batch form (one launch: ranges, delta run, locks; inputs and
 // verdicts in host-mapped memory; the last block releases seq into *done).
 struct DeltaView;
-hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const ProbeView &p,
+hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const DeltaView &d2,
+                               const ProbeView &p,
                                uint8_t *verdict, uint32_t *blocks_done, uint32_t *done,
                                uint32_t seq, hipStream_t s);
 // 16-ary directory over a sorted u64 array A (hsc_narrow.hip): level 0 = A

@@ -366,6 +366,7 @@ __global__ __launch_bounds__(kProbeThreads) void k_probe_narrow(NarrowView nv, P
 constexpr int kSmallThreads = 256;
 
 __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, DeltaView d,
+                                                                DeltaView d2,
                                                                 ProbeView p, uint8_t *verdict,
                                                                 uint32_t *blocks_done,
                                                                 uint32_t *done, uint32_t seq)
@@ -374,9 +375,9 @@ __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, D
     const uint32_t wave0 = (blockIdx.x * (kSmallThreads / 16) + ((threadIdx.x >> 6) << 2)) * kNP;
     narrow_probe_ranges(nv, p, verdict, nullptr, 0, nv.levels, wave0, groups * kNP);
     const uint32_t tid = blockIdx.x * kSmallThreads + threadIdx.x, nth = gridDim.x * kSmallThreads;
-    if (d.n)
+    if (d.n || d2.n)  // the live run and a frozen one (background fold)
         for (uint32_t q = tid; q < p.n; q += nth)
-            if (delta_hit(d, p, q)) verdict[p.txn[q]] = 1;
+            if ((d.n && delta_hit(d, p, q)) || (d2.n && delta_hit(d2, p, q))) verdict[p.txn[q]] = 1;
     narrow_probe_locks(nv, p, verdict, tid, nth);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -389,7 +390,8 @@ __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, D
     }
 }
 
-hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const ProbeView &p,
+hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const DeltaView &d2,
+                               const ProbeView &p,
                                uint8_t *verdict, uint32_t *blocks_done, uint32_t *done,
                                uint32_t seq, hipStream_t s)
 {
@@ -398,7 +400,7 @@ hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const P
     const size_t work = std::max<size_t>({(p.n + per_block - 1) / per_block,
                                           (p.n_lock + kSmallThreads - 1) / kSmallThreads, 1});
     k_small_narrow<<<(unsigned)std::min<size_t>(work, 256), kSmallThreads, 0, s>>>(
-        nv, d, p, verdict, blocks_done, done, seq);
+        nv, d, d2, p, verdict, blocks_done, done, seq);
     return hipGetLastError();
 }
 

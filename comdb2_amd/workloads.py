@@ -189,14 +189,16 @@ def replay(events: Sequence[Tuple[str, Txn]], check: Callable[[LLog, ReadSets], 
 
 
 def replay_incremental(events: Sequence[Tuple[str, Txn]], v, tbnames: Sequence[str] = (),
-                       mode: str = "log", on_check=None) -> dict:
+                       mode: str = "log", on_check=None, check_times=None) -> dict:
     """The commit stream of :func:`replay` against one validator whose window
     is kept up to date incrementally: an empty log is ingested once, then
     every passing write txn's records are appended -- as the continuation of
     the log (``mode="log"``: hsc_window_append_log, the chains decoded on the
     device side's host decoder) or as decoded writes (``mode="writes"``:
     hsc_window_append + hsc_window_set_end).  Each check is the drop-in entry
-    bdb_osql_serial_check on a CurRangeArr.  Returns {txn name: rc}."""
+    bdb_osql_serial_check on a CurRangeArr.  Returns {txn name: rc};
+    check_times (a list) collects each check's wall time in seconds."""
+    import time
     from .hsc import CurRangeArrays, bdb_osql_serial_check
     lb = LogBuilder(tbnames)
     v.ingest_log(lb.build())
@@ -210,7 +212,10 @@ def replay_incremental(events: Sequence[Tuple[str, Txn]], v, tbnames: Sequence[s
         arrs = CurRangeArrays([t.reads], [snaps[t.name]])
         if on_check:
             on_check()
+        t0 = time.perf_counter()
         rc = int(bdb_osql_serial_check(v, arrs.arrs[0]))
+        if check_times is not None:
+            check_times.append(time.perf_counter() - t0)
         rcs[t.name] = rc
         if rc == 0:
             start = len(lb.rows)

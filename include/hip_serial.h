@@ -288,6 +288,18 @@ int hsc_window_append_log(hsc_ctx *ctx, const hsc_llog *log);
 int hsc_window_append_raw(hsc_ctx *ctx, const hsc_raw_log *log);
 /* Rows in the delta run (appended since the last build of the main window). */
 size_t hsc_window_delta_rows(hsc_ctx *ctx);
+/* Delta folding.  Appended rows live in a sorted delta run beside the main
+ * window; once it holds `rows` rows (0 = the default, half the run's
+ * capacity of 65536) it is folded into the main window.  background = 1
+ * (default): the run is frozen and the main window rebuilt with it on a
+ * second stream and host thread while checks go on against the old window +
+ * frozen run + a fresh run; the rebuilt window is swapped in by the first
+ * call after it finished.  background = 0: the next check merges the run
+ * inline (a full rebuild on the check's path). */
+int hsc_set_fold(hsc_ctx *ctx, size_t rows, int background);
+/* out[4]: background folds started, background folds swapped in, inline
+ * merges, build time of the last background fold in microseconds. */
+int hsc_fold_stats(hsc_ctx *ctx, uint64_t out[4]);
 int hsc_window_set_end(hsc_ctx *ctx, uint64_t end_lsn);
 int hsc_window_reset(hsc_ctx *ctx);
 /* Sort + dedupe + summaries on the device; implied by the check calls. */

@@ -51,6 +51,14 @@ def test_config2_window_with_decoded_appends_and_merge(validator, oracle_mod):
     log = c2.log
     R = 13  # records per commit (ltran_start, 10 undo, ltran_commit, regop)
     n0 = 12_000
+    validator.set_fold(65536, background=False)  # the inline merge at the run's cap
+    try:
+        _config2_appends(validator, oracle_mod, c2, log, R, n0)
+    finally:
+        validator.set_fold(0, background=True)
+
+
+def _config2_appends(validator, oracle_mod, c2, log, R, n0):
     validator.ingest_log(log_slice(log, 0, n0 * R))
     validator.check_readsets(c2.readsets.with_snaps(np.minimum(c2.readsets.snap, log.lsn[n0 * R - 1])))
     keys = F.enc_int64_array(c2.key_values)
@@ -91,6 +99,7 @@ def test_device_ingested_window_appends_and_device_merge(oracle_mod):
     from comdb2_amd.hsc import Validator
     from comdb2_amd.workloads import config2_device_window
     validator = Validator(0)  # own dictionaries: one 9-byte group, 2 key words
+    validator.set_fold(65536, background=False)  # the inline merge at the run's cap
     c2 = config2(n_commits=12_000, n_txn=2000, value_bits=26, width=1 << 9, snap_recent=0.5)
     gid, words, lsn = config2_device_window(c2)
     n0 = 4000 * 10  # rows of the first 4000 commits
@@ -120,3 +129,80 @@ def test_device_ingested_window_appends_and_device_merge(oracle_mod):
     np.testing.assert_array_equal(got != 0, want != 0)
     assert 0.05 < (want != 0).mean() < 0.95
     validator.close()
+
+
+def _device_c2(rows_per_fold, background):
+    from comdb2_amd.hsc import Validator
+    from comdb2_amd.workloads import config2_device_window
+    v = Validator(0)
+    v.set_fold(rows_per_fold, background=background)
+    c2 = config2(n_commits=12_000, n_txn=2000, value_bits=26, width=1 << 9, snap_recent=0.5)
+    gid, words, lsn = config2_device_window(c2)
+    n0 = 4000 * 10
+    dev = torch.device("cuda", 0)
+    tg = torch.from_numpy(gid[:n0].copy()).to(dev)
+    tw = torch.from_numpy(np.ascontiguousarray(words[:, :n0]).reshape(-1).view(np.int64)).to(dev)
+    tl = torch.from_numpy(lsn[:n0].view(np.int64).copy()).to(dev)
+    v.register_group("t1", 0, 9)
+    v.ingest_device(n0, 2, tg.data_ptr(), tw.data_ptr(), tl.data_ptr(), int(c2.log.end_lsn))
+    torch.cuda.synchronize()
+    return v, c2, lsn
+
+
+def test_background_folds_keep_verdicts(oracle_mod):
+    """Background folds (hsc_set_fold: every 3000 delta rows, rebuilt on a
+    second stream while checks go on against main + frozen + live runs):
+    after every batch of appends the verdicts equal the inline-fold context's
+    and, at checkpoints, the oracle's on the log so far."""
+    bg, c2, lsn = _device_c2(3000, True)
+    il, _, _ = _device_c2(3000, False)
+    keys = F.enc_int64_array(c2.key_values)
+    R = 13
+    try:
+        for c0 in range(4000, 12_000, 400):
+            writes = [("t1", 0, bytes(keys[i]), int(lsn[i])) for i in range(c0 * 10, (c0 + 400) * 10)]
+            bg.append_writes(writes)
+            il.append_writes(writes)
+            sub_end = (c0 + 400) * R
+            rs = c2.readsets.with_snaps(np.minimum(c2.readsets.snap, c2.log.lsn[sub_end - 1]))
+            got = bg.check_readsets(rs)
+            np.testing.assert_array_equal(got != 0, il.check_readsets(rs) != 0, err_msg=f"commit {c0}")
+            if c0 % 2000 == 0:
+                want, _, _ = oracle_mod.check(log_slice(c2.log, 0, sub_end), rs, nthreads=8)
+                np.testing.assert_array_equal(got != 0, want != 0, err_msg=f"commit {c0}")
+        st = bg.fold_stats()
+        assert st["started"] >= 10 and st["swapped"] >= 5, st
+        assert il.fold_stats()["inline"] >= 10
+        # every row is in the window + runs: a full fold gives the oracle's verdicts
+        want, _, _ = oracle_mod.check(c2.log, c2.readsets, nthreads=8)
+        np.testing.assert_array_equal(bg.check_readsets(c2.readsets) != 0, want != 0)
+        g_all = bg.export_window(all_versions=True)
+        assert len(g_all[0]) == 12_000 * 10
+    finally:
+        bg.close()
+        il.close()
+
+
+def test_config1_replay_with_background_folds():
+    """The 10k-txn config-1 stream with a fold every ~1000 commits, background
+    and inline: both equal the golden verdicts; the background run's slowest
+    checks are reported beside the inline run's (the inline fold sits on the
+    check path)."""
+    import time
+
+    from comdb2_amd.hsc import Validator
+    g = json.load(open(GOLDEN))
+    ev = config1_events(n_txn=g["n_txn"])
+    lat = {}
+    for bgmode in (True, False):
+        v = Validator(0)
+        v.set_fold(2000, background=bgmode)
+        t = []
+        got = replay_incremental(ev, v, mode="log", check_times=t)
+        st = v.fold_stats()
+        v.close()
+        assert got == g["rc"]
+        assert (st["swapped"] if bgmode else st["inline"]) >= 3, st
+        lat[bgmode] = np.array(t) * 1e6
+    print({k: {"p50": float(np.median(x)), "p99": float(np.percentile(x, 99)), "max": float(x.max())}
+           for k, x in lat.items()})
