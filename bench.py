@@ -130,6 +130,24 @@ def log_tail_commit(commit_lsn, snaps):
     return c0
 
 
+def _commit_stream_fold_leg(ev, rows, background):
+    """The config-1 stream again with the delta folded every `rows` rows
+    (about one fold per `rows` commits: one keyed write per commit), in the
+    background or inline: per-check latency and the fold counts."""
+    from comdb2_amd import hsc
+    from comdb2_amd.workloads import replay_incremental
+    v = hsc.Validator(0)
+    v.set_fold(rows, background=background)
+    t = []
+    replay_incremental(ev, v, mode="log", check_times=t)
+    st = v.fold_stats()
+    v.close()
+    x = np.array(t) * 1e6
+    return {"check_us": {"p50": float(np.median(x)), "p99": float(np.percentile(x, 99)),
+                         "p999": float(np.percentile(x, 99.9)), "max": float(x.max())},
+            "folds": st}
+
+
 def bench_commit_stream(args):
     """Config 1: the tests/tools/serial.c-shaped commit stream (10k txns, 20
     ids x 5 accounts, seed 0xC0FFEE01) replayed through the drop-in entry on
@@ -206,6 +224,9 @@ def bench_commit_stream(args):
                                     "p99": float(np.percentile(ta, 99) * 1e6)},
            "stream_wall_s": wall, "parity_with_oracle_golden": parity,
            "cpu_baseline": None if args.no_cpu else commit_stream_cpu_baseline(args),
+           "fold_every_1k_commits": {
+               "background": _commit_stream_fold_leg(ev, 1000, True),
+               "inline": _commit_stream_fold_leg(ev, 1000, False)},
            "note": "value = commits / (time inside the check and append calls); the wall time "
                    "also holds the Python log builder that stands in for comdb2's logging"}
     print(json.dumps(out), flush=True)

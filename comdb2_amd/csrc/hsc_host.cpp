@@ -1135,6 +1135,10 @@ static int flush_appends(hsc_ctx *c)
     HIPCHK_RC(c, fold_finish(c, false));
     const size_t k = c->app_gid.size();
     const bool sync_only = window_words(c) > c->W || c->merge_pending || c->groups.size() > c->ng_built;
+    if (getenv("HSC_FOLD_TRACE"))
+        fprintf(stderr, "[fold] k %zu dn %zu fn %zu ww %d W %d mp %d groups %zu/%zu state %d\n", k, c->dn, c->fn,
+                window_words(c), c->W, (int)c->merge_pending, c->groups.size(), c->ng_built,
+                c->fold_state.load());
     if (k && !sync_only && c->fold_bg && c->dn + k > kDeltaCap && k <= kDeltaCap) {
         // the live run is full: wait for a running fold, then fold the run
         HIPCHK_RC(c, fold_finish(c, true));
@@ -1217,7 +1221,6 @@ static int merge_delta(hsc_ctx *c)
 {
     hipStream_t s = c->stream;
     (void)fold_finish(c, true);  // a failed fold leaves its rows in the frozen run, merged below
-    c->folds_inline++;
     HIPCHK(c, wait_lanes(c));
     const int W0 = c->W, W = std::max(c->W, window_words(c));
     size_t k = 0;
@@ -1460,7 +1463,11 @@ static int ensure_built(hsc_ctx *c)
         if (!c->host_staged) c->merge_pending = true;
     }
     if (!c->dirty) return HSC_OK;
-    if (c->host_staged) return build_from_host(c);  // staged rows include the appended ones
+    if (c->merge_pending) c->folds_inline++;
+    if (c->host_staged) {  // staged rows include the appended ones (and a frozen run's)
+        fold_discard(c);
+        return build_from_host(c);
+    }
     if (c->merge_pending) return merge_delta(c);
     return fail(c, HSC_ESTATE, "device window must be re-ingested");
 }
