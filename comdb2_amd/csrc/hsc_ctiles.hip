@@ -678,13 +678,11 @@ __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
 // Plan-free compact join (chunk-sorted records), as k_join_f of the narrow
 // tiles: the tile's column of the locate's chunk-major table is read and
 // scanned here, a hot tile's records past the first kCJT are joined by the
-// same block in further rounds, conflicts mark the flags and the last block
-// writes the verdict bytes.  Two launches per batch besides the bound mapping:
-// locate -> join.
+// same block in further rounds, conflicts mark the flags (packed into the
+// verdict bytes by launch_pack_flags): locate -> join -> pack.
 template <int WG>
 __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_join_cf(
-    ProbeWork work, CTiles ct, uint8_t *flags, uint32_t n_txn, uint8_t *verdict, uint64_t *bitmap,
-    int tail_pack)
+    ProbeWork work, CTiles ct, uint8_t *flags)
 {
     constexpr uint32_t T = kCTRows;
     extern __shared__ __attribute__((aligned(16))) uint64_t jl[];
@@ -762,7 +760,6 @@ __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
             join_search<WG>(work, ct, flags, kw, rank, b16, b128, B, kind, pl, ph0, ph1);
         }
     }
-    if (tail_pack) flags_tail_pack<kCJT>(&work.item_off[2], flags, n_txn, verdict, bitmap);
 }
 
 }  // namespace
@@ -822,17 +819,15 @@ hipError_t launch_scatter_c(const CTiles &ct, const ProbeWork &work, uint32_t n,
     return hipGetLastError();
 }
 
-hipError_t launch_join_cf(const CTiles &ct, const ProbeWork &work, uint8_t *flags, uint32_t n_txn,
-                          uint8_t *verdict, uint64_t *bitmap, bool tail_pack, hipStream_t s)
+hipError_t launch_join_cf(const CTiles &ct, const ProbeWork &work, uint8_t *flags, hipStream_t s)
 {
     if (ct.ntiles == 0) return hipSuccess;
     const size_t lds = 8 * (size_t)ct.WG * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
                        4 * (kCTRows / 128) + 4 * kTBS + 6 * (size_t)kMaxChunks;
-    const int tp = tail_pack ? 1 : 0;
     switch (ct.WG) {
-    case 1: k_join_cf<1><<<ct.ntiles, kCJT, lds, s>>>(work, ct, flags, n_txn, verdict, bitmap, tp); break;
-    case 2: k_join_cf<2><<<ct.ntiles, kCJT, lds, s>>>(work, ct, flags, n_txn, verdict, bitmap, tp); break;
-    case 3: k_join_cf<3><<<ct.ntiles, kCJT, lds, s>>>(work, ct, flags, n_txn, verdict, bitmap, tp); break;
+    case 1: k_join_cf<1><<<ct.ntiles, kCJT, lds, s>>>(work, ct, flags); break;
+    case 2: k_join_cf<2><<<ct.ntiles, kCJT, lds, s>>>(work, ct, flags); break;
+    case 3: k_join_cf<3><<<ct.ntiles, kCJT, lds, s>>>(work, ct, flags); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

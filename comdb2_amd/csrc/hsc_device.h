@@ -313,66 +313,4 @@ __device__ __forceinline__ bool delta_hit(const DeltaView &d, const ProbeView &p
     return hit;
 }
 
-// ---- verdicts packed by a kernel's last block ------------------------------
-// Called by every thread of every block at the end of a kernel whose blocks
-// mark conflict flags: the last block to arrive (counter, zero before the
-// launch) turns the batch's flags (zero-padded to a multiple of 16) into
-// verdict bytes 0 / 1 and bitmap bits (bitmap may be NULL) and clears them
-// for the next batch -- the pack without a launch of its own.
-template <int NT>
-__device__ __forceinline__ void flags_tail_pack(uint32_t *counter, uint8_t *flags, uint32_t n_txn,
-                                                uint8_t *verdict, uint64_t *bitmap)
-{
-    typedef unsigned int v4 __attribute__((ext_vector_type(4)));
-    constexpr uint32_t kVec = 16;  // flags per thread and load
-    __shared__ uint32_t last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence();  // this block's flags before its arrival
-        last = atomicAdd(counter, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    const uint32_t nv = (n_txn + kVec - 1) / kVec;
-    for (uint32_t i0 = 0; i0 < nv; i0 += 4 * NT) {
-        v4 f[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t i = i0 + u * NT + threadIdx.x;
-            f[u] = i < nv ? ((const v4 *)flags)[i] : v4{0, 0, 0, 0};
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t i = i0 + u * NT + threadIdx.x;
-            // 16 flag bytes -> 16 verdict bytes (0 / 1) and 16 bitmap bits
-            v4 o;
-            uint32_t bits = 0;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const uint32_t w = f[u][c];
-                uint32_t b = 0;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) b |= ((w >> (8 * k)) & 0xFFu) ? 1u << (8 * k) : 0u;
-                o[c] = b;
-                bits |= ((b & 1u) | ((b >> 7) & 2u) | ((b >> 14) & 4u) | ((b >> 21) & 8u)) << (4 * c);
-            }
-            // 4 neighbouring lanes hold one 64-bit bitmap word (every lane shuffles)
-            uint64_t word = (uint64_t)bits << (16 * (i & 3));
-            word |= __shfl_xor(word, 1, 64);
-            word |= __shfl_xor(word, 2, 64);
-            if (i >= nv) continue;
-            const uint32_t t0 = i * kVec;
-            if (t0 + kVec <= n_txn) {
-                *(v4 *)(verdict + t0) = o;
-            } else {
-                for (uint32_t t = t0; t < n_txn; ++t)
-                    verdict[t] = (o[(t - t0) >> 2] >> (8 * ((t - t0) & 3))) & 1u;
-            }
-            if (f[u][0] | f[u][1] | f[u][2] | f[u][3]) ((v4 *)flags)[i] = v4{0, 0, 0, 0};
-            if (bitmap && (i & 3) == 0 && 64 * (i >> 2) < n_txn) bitmap[i >> 2] = word;
-        }
-    }
-}
-
 }  // namespace hsc

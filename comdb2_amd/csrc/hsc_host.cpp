@@ -141,7 +141,6 @@ struct Stage {
 };
 
 constexpr int kMarshalTxns = 2048;         // read sets per marshal work item
-constexpr size_t kTailPackMax = 1u << 18;  // fused join: verdict bytes by its last block up to this
 enum { kFoldIdle = 0, kFoldRunning = 1, kFoldDone = 2 };  // hsc_ctx::fold_state
 constexpr int kMarshalParallelMin = 4096;  // fewer read sets: marshal on the caller's thread
 constexpr int kPipeTxns = 32768;           // read sets per pipeline chunk of a large batch
@@ -248,7 +247,8 @@ struct hsc_ctx {
     Dir16 cdir{}, tdir{};
     uint32_t trad_m = 0;       // tile bucket table size (0: none)
     bool trad_log = false;     // the table is in log mode (narrow_trad_pick)
-    uint32_t ncommit = 0;
+    uint32_t ncommit = 0;      // distinct commit LSNs in d_commits (built only for the rank directory)
+    bool has_commits = false;  // the window has rows and a commit span (narrow / compact tiles)
     uint64_t commit_span[2] = {0, 0};  // oldest / newest distinct commit LSN of the window
     bool rank_lsn32 = false;   // narrow tiles: rows carry lsn - rank_base + 1 (NarrowTiles)
     bool nt_sorted = true;     // narrow tiles: chunk-sorted records (HSC_NT_SORT=0 at build: scatter)
@@ -557,8 +557,8 @@ static int build_commits(hsc_ctx *c, size_t n_in)
                           c->d_gid2.as<uint32_t>(), c->d_commits.as<uint64_t>(),
                           c->d_commits.as<uint64_t>(), n_in, c->d_flags.as<uint32_t>(),
                           c->d_scratch.p, c->d_scratch.bytes, c->d_count.as<uint32_t>() + 12, s));
-    // the count (d_count[12]) and the span (narrow_commit_span) come back with
-    // the window's own sizes, in device_build's one readback
+    // the count (d_count[12]) comes back with the window's own sizes, in
+    // device_build's one readback
     return HSC_OK;
 }
 
@@ -652,7 +652,7 @@ static int build_ctiles(hsc_ctx *c)
     int gb = 0;
     while (gb < 32 && ((size_t)1 << gb) < (size_t)ng) gb++;
     const int WG = (c->ct_maxbits + gb + 1 + 63) / 64;  // a spare bit: ~0 is above every key
-    if (v.log2T != kCTLog2 || WG > 3 || WG < c->ct.WC || c->ncommit == 0 ||
+    if (v.log2T != kCTLog2 || WG > 3 || WG < c->ct.WC || !c->has_commits ||
         c->commit_span[1] - c->commit_span[0] > kLsn32MaxSpan)
         return HSC_OK;
     CTiles &ct = c->ctv;
@@ -787,12 +787,20 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, hipEventCreate(&e0));
     HIPCHK(c, hipEventCreate(&e1));
     HIPCHK(c, hipEventRecord(e0, s));
-    if (c->layout != HSC_LAYOUT_WIDE && n_in > 0) HIPCHK_RC(c, build_commits(c, n_in));
-    bt.stamp("commits");
-    uint64_t vary[kMaxWords + 1];
+    // varying key bits and the LSN span in one pass; the distinct commit list
+    // only when snapshot ranks need its directory (a window spanning >= 2^32
+    // of log, or HSC_RANK_DIR): otherwise rows carry lsn - oldest + 1
+    uint64_t vary[kMaxWords + 1], span[2];
     HIPCHK(c, vary_mask_rows(W, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(), cap,
-                             c->d_scratch.p, vary, s));
+                             c->d_scratch.p, vary, s, c->d_lsn.as<uint64_t>(), span));
     bt.stamp("vary");
+    const bool commits = c->layout != HSC_LAYOUT_WIDE && n_in > 0;
+    const bool rank_dir = commits && (span[1] - span[0] > kLsn32MaxSpan || getenv("HSC_RANK_DIR"));
+    c->has_commits = commits;
+    c->ncommit = 0;
+    if (commits) memcpy(c->commit_span, span, 16);
+    if (rank_dir) HIPCHK_RC(c, build_commits(c, n_in));
+    bt.stamp("commits");
     PackPlan plan;
     c->packed_sort = try_packed && packed_plan(W, n_in, vary, &plan);
     if (c->packed_sort) {
@@ -832,7 +840,6 @@ static int device_build(hsc_ctx *c, size_t n_in)
     }
     // one readback for the sizes the host plans with: distinct rows, commits,
     // the commit span and the window's end rows (all computed on the device)
-    const bool commits = c->layout != HSC_LAYOUT_WIDE && n_in > 0;
     HIPCHK(c, c->d_nbase.ensure(16 * ((size_t)W + 1)));
     std::vector<uint64_t> ends(2 * ((size_t)W + 1), 0);
     uint32_t hc[24] = {0};
@@ -843,18 +850,13 @@ static int device_build(hsc_ctx *c, size_t n_in)
         wc.gid = c->d_gid.as<uint32_t>();
         wc.W = W;
         HIPCHK(c, narrow_end_rows(wc, c->d_count.as<uint32_t>(), c->d_nbase.as<uint64_t>(), s));
-        HIPCHK(c, narrow_commit_span(c->d_commits.as<uint64_t>(), c->d_count.as<uint32_t>() + 12,
-                                     (uint64_t *)(c->d_count.as<uint32_t>() + 16), s));
         HIPCHK(c, hipMemcpyAsync(ends.data(), c->d_nbase.p, 8 * ends.size(), hipMemcpyDeviceToHost, s));
     }
     HIPCHK(c, hipMemcpyAsync(hc, c->d_count.p, sizeof hc, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     bt.stamp("dedupe");
     const uint32_t nu = hc[0];
-    if (commits) {
-        c->ncommit = hc[12];
-        memcpy(c->commit_span, hc + 16, 16);
-    }
+    if (rank_dir) c->ncommit = hc[12];
     c->n = n_in ? nu : 0;
     c->n_all = n_in;  // every version, key-sorted, stays in d_gid2 / d_words2 / d_lsn2
     // narrow layout if the whole window fits 62-bit codes (hsc_narrow.hip)
@@ -985,7 +987,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
         c->ntiles32 = false;
         c->trad_m = 0;
         bt.stamp("codes");
-        if (wn.log2T == 12 && wn.ntiles <= (uint32_t)kHistCap && c->ncommit > 0) {
+        if (wn.log2T == 12 && wn.ntiles <= (uint32_t)kHistCap && c->has_commits) {
             // commit span: rank-free rows (lsn - oldest commit + 1) when it fits 32 bits
             const uint64_t *span = c->commit_span;
             c->rank_lsn32 = span[1] - span[0] <= kLsn32MaxSpan && !getenv("HSC_RANK_DIR");
@@ -1299,7 +1301,7 @@ static void swap_window(hsc_ctx *a, hsc_ctx *b)
     swap(a->d_key32, b->d_key32), swap(a->d_rank32, b->d_rank32);
     for (int i = 0; i < 4; ++i) swap(a->d_ctmp[i], b->d_ctmp[i]);
     swap(a->cdir, b->cdir), swap(a->tdir, b->tdir), swap(a->trad_m, b->trad_m);
-    swap(a->trad_log, b->trad_log), swap(a->ncommit, b->ncommit);
+    swap(a->trad_log, b->trad_log), swap(a->ncommit, b->ncommit), swap(a->has_commits, b->has_commits);
     swap(a->commit_span[0], b->commit_span[0]), swap(a->commit_span[1], b->commit_span[1]);
     swap(a->rank_lsn32, b->rank_lsn32), swap(a->nt_sorted, b->nt_sorted), swap(a->nt_fused, b->nt_fused);
     swap(a->ct_sorted, b->ct_sorted), swap(a->ct_fused, b->ct_fused), swap(a->rank_base, b->rank_base);
@@ -2172,17 +2174,17 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     HIPCHK(c, launch_locate_t(c->nv, wn, p, work, ntl, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     if (p.n && wn.ntiles && sorted && c->nt_fused) {
-        // plan-free: the join scans its tile's column itself, marks the flags
-        // and its last block writes the verdict bytes (large batches: a pack
-        // launch after it); the delta probe marks the flags before it
+        // plan-free: the join scans its tile's column itself and marks the
+        // flags (as the delta probe before it); the pack writes the verdict
+        // bytes.  (A last-block pack inside the join measured 2x slower: every
+        // block's device-scope release before its arrival count writes back
+        // its XCD's L2.)
         if (tm)
             for (int i = 2; i <= 3; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
         HIPCHK_RC(c, probe_delta(c, flags));
-        const bool tail = b->n_txn <= kTailPackMax;
-        HIPCHK(c, launch_join_f(work, ntl, wn.n, wn.ntiles, flags, (uint32_t)b->n_txn, b->verdict,
-                                b->bitmap, tail, s));
+        HIPCHK(c, launch_join_f(work, ntl, wn.n, wn.ntiles, flags, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
-        if (!tail) HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
+        HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
     } else if (p.n && wn.ntiles) {
         // the plan writes the verdict bytes from the locate's flags; the join
         // and the delta probe then mark the verdict itself
@@ -2292,15 +2294,14 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
                               work, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     if (p.n && ct.ntiles && sorted && c->ct_fused) {
-        // plan-free, as probe_ntiles: the join scans its column, marks the
-        // flags and its last block writes the verdict bytes
+        // plan-free, as probe_ntiles: the join scans its column and marks
+        // the flags; the pack writes the verdict bytes
         if (tm)
             for (int i = 2; i <= 3; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
         HIPCHK_RC(c, probe_delta(c, flags));
-        const bool tail = b->n_txn <= kTailPackMax;
-        HIPCHK(c, launch_join_cf(ct, work, flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, tail, s));
+        HIPCHK(c, launch_join_cf(ct, work, flags, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
-        if (!tail) HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
+        HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
     } else if (p.n && ct.ntiles) {
         // pack folded into the plan, as probe_ntiles
         HIPCHK(c, (sorted ? launch_plan_s : launch_plan_t)(work, ct.ntiles,

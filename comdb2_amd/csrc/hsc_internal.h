@@ -124,9 +124,11 @@ hipError_t radix_sort_rows(int W, size_t n, uint32_t *gid, uint64_t *words, uint
                            bool *result_in_alt, uint64_t *vary_mask, hipStream_t s);
 size_t radix_scratch_bytes(size_t n, int W);
 // vary[j] (host, j <= W): bits of word j / of the gid (j == W) that differ
-// between rows (one kernel + readback; scratch >= 8 (W + 1) bytes)
+// between rows, and with lsn_span the rows' min / max LSN (0, 0 if every LSN
+// is 0) -- one kernel + readback; scratch >= 8 (W + 3) bytes
 hipError_t vary_mask_rows(int W, size_t n, const uint32_t *gid, const uint64_t *words, size_t stride,
-                          void *scratch, uint64_t *vary, hipStream_t s);
+                          void *scratch, uint64_t *vary, hipStream_t s, const uint64_t *lsn = nullptr,
+                          uint64_t *lsn_span = nullptr);
 // radix_sort_rows with the vary masks already known
 hipError_t radix_sort_known(int W, size_t n, uint32_t *gid, uint64_t *words, uint64_t *lsn,
                             size_t stride, uint32_t *gid_alt, uint64_t *words_alt,
@@ -229,8 +231,6 @@ struct NarrowView {
 };
 bool narrow_span_fits(int W, int lw, int tz, const uint64_t *first, const uint64_t *last);
 hipError_t narrow_end_rows(const WinView &w, const uint32_t *n_dev, uint64_t *out, hipStream_t s);
-hipError_t narrow_commit_span(const uint64_t *commits, const uint32_t *m_dev, uint64_t *out,
-                              hipStream_t s);
 hipError_t narrow_build(const WinView &w, const NarrowView &nv, hipStream_t s);
 hipError_t launch_probe_narrow(const NarrowView &nv, const ProbeView &p, uint8_t *verdict,
                                hipStream_t s);
@@ -404,11 +404,9 @@ hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeV
 hipError_t launch_scatter_t(const ProbeView &p, const ProbeWork &work, const NarrowTiles &nt,
                             uint32_t ntiles, hipStream_t s);
 // Plan-free join of chunk-sorted records (tile columns scanned in the join;
-// conflicts into flags; tail_pack: the last block writes the verdict bytes /
-// bitmap from the flags and clears them).
+// conflicts into flags, packed by launch_pack_flags).
 hipError_t launch_join_f(const ProbeWork &work, const NarrowTiles &nt, uint32_t n, uint32_t ntiles,
-                         uint8_t *flags, uint32_t n_txn, uint8_t *verdict, uint64_t *bitmap,
-                         bool tail_pack, hipStream_t s);
+                         uint8_t *flags, hipStream_t s);
 hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t n,
                          uint32_t ntiles, uint32_t max_items, uint8_t *verdict, hipStream_t s);
 // Dependency graph + SCC (hsc_graph.hip).
@@ -517,8 +515,7 @@ hipError_t launch_locate_c(const CTiles &ct, const WinView &wt, const ProbeView 
                            uint8_t *flags, hipStream_t s);
 hipError_t launch_scatter_c(const CTiles &ct, const ProbeWork &work, uint32_t n, hipStream_t s);
 // Plan-free compact join (chunk-sorted records), as launch_join_f.
-hipError_t launch_join_cf(const CTiles &ct, const ProbeWork &work, uint8_t *flags, uint32_t n_txn,
-                          uint8_t *verdict, uint64_t *bitmap, bool tail_pack, hipStream_t s);
+hipError_t launch_join_cf(const CTiles &ct, const ProbeWork &work, uint8_t *flags, hipStream_t s);
 hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_items,
                          uint8_t *flags, hipStream_t s);
 // Sharded SCC (hsc_graph.hip): cover[v] = 1 iff v lies inside [dst, src] of a

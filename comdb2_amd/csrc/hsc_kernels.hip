@@ -52,7 +52,7 @@ __device__ __forceinline__ uint32_t row_digit(int W, int d, size_t i, const uint
 // the same in every row and its pass is skipped.
 __global__ __launch_bounds__(256) void k_vary_mask(int W, size_t n, const uint32_t *gid,
                                                    const uint64_t *words, size_t stride,
-                                                   unsigned long long *mask)
+                                                   const uint64_t *lsn, unsigned long long *mask)
 {
     constexpr int U = 8;  // independent loads in flight per thread
     __shared__ uint64_t part[256 / 64];
@@ -80,6 +80,32 @@ __global__ __launch_bounds__(256) void k_vary_mask(int W, size_t n, const uint32
             if (b) atomicOr(&mask[j], (unsigned long long)b);
         }
         __syncthreads();
+    }
+    if (!lsn) return;
+    // the rows' LSN span: mask[W + 1] = min, mask[W + 2] = max
+    uint64_t lo = ~0ull, hi = 0;
+    for (size_t i0 = (size_t)blockIdx.x * blockDim.x * U + threadIdx.x; i0 < n;
+         i0 += (size_t)gridDim.x * blockDim.x * U) {
+        uint64_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = i0 + (size_t)u * blockDim.x;
+            v[u] = i < n ? lsn[i] : lsn[i0];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            lo = v[u] < lo ? v[u] : lo;
+            hi = v[u] > hi ? v[u] : hi;
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if (lane_id() == 0 && hi) {
+        atomicMin(&mask[W + 1], (unsigned long long)lo);
+        atomicMax(&mask[W + 2], (unsigned long long)hi);
     }
 }
 
@@ -319,20 +345,30 @@ size_t radix_scratch_bytes(size_t n, int W)
 }
 
 hipError_t vary_mask_rows(int W, size_t n, const uint32_t *gid, const uint64_t *words, size_t stride,
-                          void *scratch, uint64_t *vary, hipStream_t s)
+                          void *scratch, uint64_t *vary, hipStream_t s, const uint64_t *lsn,
+                          uint64_t *lsn_span)
 {
     for (int j = 0; j <= W; ++j) vary[j] = 0;
-    if (n <= 1) return hipSuccess;
-    unsigned long long *dmask = (unsigned long long *)scratch;  // [W + 1]
-    hipError_t e = hipMemsetAsync(dmask, 0, 8 * ((size_t)W + 1), s);
+    if (lsn_span) lsn_span[0] = lsn_span[1] = 0;
+    if (n == 0) return hipSuccess;
+    unsigned long long *dmask = (unsigned long long *)scratch;  // [W + 1] masks, min, max
+    hipError_t e = hipMemsetAsync(dmask, 0, 8 * ((size_t)W + 3), s);
+    if (e == hipSuccess) e = hipMemsetAsync(dmask + W + 1, 0xFF, 8, s);
     if (e != hipSuccess) return e;
     const unsigned hgrid = (unsigned)std::min<size_t>((n + 2047) / 2048, 2048);
-    k_vary_mask<<<hgrid, 256, 0, s>>>(W, n, gid, words, stride, dmask);
+    k_vary_mask<<<hgrid, 256, 0, s>>>(W, n, gid, words, stride, lsn_span ? lsn : nullptr, dmask);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    e = hipMemcpyAsync(vary, dmask, 8 * ((size_t)W + 1), hipMemcpyDeviceToHost, s);
+    uint64_t hm[kMaxWords + 3];
+    e = hipMemcpyAsync(hm, dmask, 8 * ((size_t)W + 3), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    return e;
+    if (e != hipSuccess) return e;
+    for (int j = 0; j <= W; ++j) vary[j] = hm[j];
+    if (lsn_span) {
+        lsn_span[0] = hm[W + 2] ? hm[W + 1] : 0;
+        lsn_span[1] = hm[W + 2];
+    }
+    return hipSuccess;
 }
 
 hipError_t radix_sort_rows(int W, size_t n, uint32_t *gid, uint64_t *words, uint64_t *lsn,

@@ -144,22 +144,6 @@ hipError_t narrow_end_rows(const WinView &w, const uint32_t *n_dev, uint64_t *ou
     return hipGetLastError();
 }
 
-// first and last of the m_dev sorted commit LSNs -> out[0], out[1]
-__global__ void k_commit_span(const uint64_t *commits, const uint32_t *m_dev, uint64_t *out)
-{
-    if (threadIdx.x) return;
-    const uint32_t m = *m_dev;
-    out[0] = m ? commits[0] : 0;
-    out[1] = m ? commits[m - 1] : 0;
-}
-
-hipError_t narrow_commit_span(const uint64_t *commits, const uint32_t *m_dev, uint64_t *out,
-                              hipStream_t s)
-{
-    k_commit_span<<<1, 64, 0, s>>>(commits, m_dev, out);
-    return hipGetLastError();
-}
-
 // level 0: key64 of every row (padding above n), lsn (padding 0)
 __global__ void k_level0(WinView w, const uint64_t *base, int lw, int tz, uint32_t len,
                          uint64_t *key0, uint64_t *max0)
@@ -1731,9 +1715,8 @@ hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t 
 // tiles of a block's XCD neighbour each other, so the column's lines are
 // shared in that XCD's L2 -- and scanned in LDS.  A hot tile's records past
 // the first kJoinChunk are joined by the same block in further rounds over
-// its staged rows (no overflow items).  Conflicts mark the batch's flags; the
-// last block to finish writes the verdict bytes from them (and clears them),
-// so a batch is two launches: locate -> join.
+// its staged rows (no overflow items).  Conflicts mark the batch's flags,
+// which the pack turns into verdict bytes: locate -> join -> pack.
 __device__ __forceinline__ uint32_t join_f_records(const NarrowTiles &nt, const ProbeWork &work,
                                                    const uint32_t *Es, const uint32_t *Cs,
                                                    uint32_t G, uint32_t j, uint32_t j1, u32x4 &rec)
@@ -1750,8 +1733,7 @@ __device__ __forceinline__ uint32_t join_f_records(const NarrowTiles &nt, const 
 }
 
 __global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_f(
-    ProbeWork work, NarrowTiles nt, uint32_t n, uint32_t ntiles, uint8_t *flags, uint32_t n_txn,
-    uint8_t *verdict, uint64_t *bitmap, int tail_pack)
+    ProbeWork work, NarrowTiles nt, uint32_t n, uint32_t ntiles, uint8_t *flags)
 {
     constexpr uint32_t T = 1u << kTLog2;
     constexpr int RQ = T / (4 * kJoinThreads);
@@ -1840,16 +1822,13 @@ __global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_f(
             }
         }
     }
-    if (tail_pack) flags_tail_pack<kJoinThreads>(&work.item_off[2], flags, n_txn, verdict, bitmap);
 }
 
 hipError_t launch_join_f(const ProbeWork &work, const NarrowTiles &nt, uint32_t n, uint32_t ntiles,
-                         uint8_t *flags, uint32_t n_txn, uint8_t *verdict, uint64_t *bitmap,
-                         bool tail_pack, hipStream_t s)
+                         uint8_t *flags, hipStream_t s)
 {
     if (ntiles == 0) return hipSuccess;
-    k_join_f<<<join_tile_blocks(true, ntiles), kJoinThreads, 0, s>>>(work, nt, n, ntiles, flags, n_txn,
-                                                                      verdict, bitmap, tail_pack ? 1 : 0);
+    k_join_f<<<join_tile_blocks(true, ntiles), kJoinThreads, 0, s>>>(work, nt, n, ntiles, flags);
     return hipGetLastError();
 }
 
