@@ -254,7 +254,7 @@ struct hsc_ctx {
     bool nt_sorted = true;     // narrow tiles: chunk-sorted records (HSC_NT_SORT=0 at build: scatter)
     bool nt_fused = true;      // chunk-sorted narrow tiles: plan-free join (HSC_NT_FUSED=0 at build: plan + join)
     bool ct_sorted = true;     // compact tiles: chunk-sorted records (HSC_CT_SORT=0 at build: scatter)
-    bool ct_fused = true;      // ... and the plan-free join (HSC_CT_FUSED=0 at build: plan + join)
+    bool ct_fused = false;     // ... and the plan-free join (HSC_CT_FUSED=1 at build; measured slower)
     uint64_t rank_base = 0;
     DBuf w_tcode, w_tcode2, w_trecs;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
@@ -658,7 +658,7 @@ static int build_ctiles(hsc_ctx *c)
     CTiles &ct = c->ctv;
     ct = CTiles{};
     c->ct_sorted = !getenv("HSC_CT_SORT") || atoi(getenv("HSC_CT_SORT")) != 0;
-    c->ct_fused = !getenv("HSC_CT_FUSED") || atoi(getenv("HSC_CT_FUSED")) != 0;
+    c->ct_fused = getenv("HSC_CT_FUSED") && atoi(getenv("HSC_CT_FUSED")) != 0;
     ct.n = (uint32_t)c->n;
     ct.ntiles = v.ntiles;
     ct.len = (size_t)v.ntiles << kCTLog2;

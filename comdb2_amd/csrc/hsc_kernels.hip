@@ -103,9 +103,18 @@ __global__ __launch_bounds__(256) void k_vary_mask(int W, size_t n, const uint32
         lo = a < lo ? a : lo;
         hi = b > hi ? b : hi;
     }
-    if (lane_id() == 0 && hi) {
-        atomicMin(&mask[W + 1], (unsigned long long)lo);
-        atomicMax(&mask[W + 2], (unsigned long long)hi);
+    __shared__ uint64_t plo[256 / 64], phi[256 / 64];
+    if (lane_id() == 0) plo[threadIdx.x >> 6] = lo, phi[threadIdx.x >> 6] = hi;
+    __syncthreads();
+    if (threadIdx.x == 0) {  // one atomic pair per block (same-address atomics serialise)
+        for (int w = 1; w < 256 / 64; ++w) {
+            lo = plo[w] < lo ? plo[w] : lo;
+            hi = phi[w] > hi ? phi[w] : hi;
+        }
+        if (hi) {
+            atomicMin(&mask[W + 1], (unsigned long long)lo);
+            atomicMax(&mask[W + 2], (unsigned long long)hi);
+        }
     }
 }
 
@@ -355,7 +364,7 @@ hipError_t vary_mask_rows(int W, size_t n, const uint32_t *gid, const uint64_t *
     hipError_t e = hipMemsetAsync(dmask, 0, 8 * ((size_t)W + 3), s);
     if (e == hipSuccess) e = hipMemsetAsync(dmask + W + 1, 0xFF, 8, s);
     if (e != hipSuccess) return e;
-    const unsigned hgrid = (unsigned)std::min<size_t>((n + 2047) / 2048, 2048);
+    const unsigned hgrid = (unsigned)std::min<size_t>((n + 2047) / 2048, 512);
     k_vary_mask<<<hgrid, 256, 0, s>>>(W, n, gid, words, stride, lsn_span ? lsn : nullptr, dmask);
     e = hipGetLastError();
     if (e != hipSuccess) return e;

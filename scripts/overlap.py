@@ -5,7 +5,7 @@ spends alone vs. beside another probe kernel."""
 import csv, os, sys, collections
 tag = sys.argv[1] if len(sys.argv) > 1 else "kt"
 path = os.path.join(os.path.dirname(__file__), "..", "gpurun_out", tag, "run_kernel_trace.csv")
-PROBE = ("k_locate_t", "k_plan_t", "k_plan_s", "k_scatter_t", "k_join_t", "k_pack_flags", "k_pack")
+PROBE = ("k_locate_t", "k_plan_t", "k_plan_s", "k_scatter_t", "k_join_t", "k_join_f", "k_pack_flags", "k_pack", "k_probe_delta")
 rows = []
 for r in csv.DictReader(open(path)):
     n = r["Kernel_Name"].split("(")[0].replace("hsc::", "").split("<")[0]

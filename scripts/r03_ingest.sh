@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-r03}
 mkdir -p gpurun_out
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_ingest.py tests/test_gpu_rccl.py -x -v --timeout 200 --timeout-method thread > gpurun_out/${TAG}_ingest_tests.log 2>&1
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_ingest.py tests/test_gpu_rccl.py tests/test_gpu_incremental.py -x -v -s --timeout 200 --timeout-method thread > gpurun_out/${TAG}_ingest_tests.log 2>&1
 rc=$?
 tail -3 gpurun_out/${TAG}_ingest_tests.log
 [ $rc -ne 0 ] && { grep -E "FAILED|Error|assert" gpurun_out/${TAG}_ingest_tests.log | head -30; exit $rc; }
