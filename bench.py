@@ -388,7 +388,19 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0, bitmap=False):
     chunk = 2048 if WG else 4096  # probes per locate workgroup
     chunks = (n_r + chunk - 1) // chunk
     hist = 4 * tiles * ((chunks + 7) // 8 * 8)
-    if layout == 2 and os.environ.get("HSC_NT_SORT", "1") != "0":
+    if layout == 2 and os.environ.get("HSC_NT_SORT", "1") != "0" and \
+            os.environ.get("HSC_NT_FUSED", "1") != "0":
+        # plan-free join (default): the join reads its tile's column of the
+        # locate's chunk-major table (4 B per chunk) itself; the pack turns the
+        # conflict flags into verdict bytes (+ the bitmap for N > 1)
+        own = {
+            "k_locate_t": n_r * (4 + 8 + 4 + 16 * W) + 16 * recs + hist,
+            None: 0,  # no plan
+            "": 0,    # no scatter
+            "k_join_f": 8 * n_keys + 16 * recs + hist,
+            "k_pack_flags": 2 * T + ((T + 7) // 8 if bitmap else 0),
+        }
+    elif layout == 2 and os.environ.get("HSC_NT_SORT", "1") != "0":
         # narrow tiles, chunk-sorted records: the locate writes them in place
         # (+ its chunk's row of run starts / counts), no scatter pass
         own = {
@@ -435,7 +447,7 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0, bitmap=False):
     ms = [tm["locate_ms"], tm["plan_ms"], tm["scatter_ms"], tm["join_ms"], tm["pack_ms"]]
     out = {}
     for (name, b), t in zip(own.items(), ms):
-        if name is None:  # no such pass in this layout
+        if not name:  # no such pass in this layout
             continue
         out[name] = {"event_ms": t, "bytes": int(b),
                      "GBps": b / (t * 1e-3) / 1e9 if t > 0 else None}
@@ -519,8 +531,9 @@ def box_cpus():
                 cpu=cpu_model())
 
 
-PROBE_KERNELS = ("k_locate_t", "k_plan_t", "k_plan_s", "k_scatter_t", "k_join_t", "k_pack_flags",  # narrow
-                 "k_locate_c", "k_scatter_c", "k_join_c",  # compact tiles
+PROBE_KERNELS = ("k_locate_t", "k_plan_t", "k_plan_s", "k_scatter_t", "k_join_t", "k_join_f",
+                 "k_pack_flags",  # narrow
+                 "k_locate_c", "k_scatter_c", "k_join_c", "k_join_cf",  # compact tiles
                  "k_compact_bounds", "k_locate", "k_colscan", "k_plan", "k_scatter", "k_join",
                  "k_pack", "k_probe_delta")  # compact / wide, delta run
 
