@@ -389,7 +389,7 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0, bitmap=False):
     chunks = (n_r + chunk - 1) // chunk
     hist = 4 * tiles * ((chunks + 7) // 8 * 8)
     if layout == 2 and os.environ.get("HSC_NT_SORT", "1") != "0" and \
-            os.environ.get("HSC_NT_FUSED", "1") != "0":
+            os.environ.get("HSC_NT_FUSED", "0") != "0":
         # plan-free join (default): the join reads its tile's column of the
         # locate's chunk-major table (4 B per chunk) itself; the pack turns the
         # conflict flags into verdict bytes (+ the bitmap for N > 1)
@@ -484,6 +484,10 @@ def api_leg(hsc, v, rs, device_verdict, args):
         got, st = v.concurrent_check(arrs, nth)
         st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want))
         conc[f"threads_{nth}"] = st
+    # one batch on the device at a time (the collector before round 3)
+    got, st = v.concurrent_check(arrs, 64, inflight=1)
+    st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want))
+    conc["threads_64_inflight1"] = st
     m = min(T, 2000)  # uncollected: one device pass per call, a bounded sample
     sub = hsc.NativeCurRangeArrs(_readsets_head(rs, m))
     for nth in (1, 64):

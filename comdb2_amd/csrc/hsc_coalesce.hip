@@ -1053,4 +1053,13 @@ hipError_t launch_coalesce(const CoView &v, const uint32_t *isbig, const uint32_
     return hipGetLastError();
 }
 
+// load this file's code object now (HIP loads it lazily at the first launch
+// of one of its kernels: ~1 ms, which would land inside the first build or
+// probe -- hsc_ctx_create calls every warm_* once)
+hipError_t warm_coalesce()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void *)k_coalesce);
+}
+
 }  // namespace hsc

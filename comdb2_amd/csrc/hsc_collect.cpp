@@ -6,7 +6,7 @@
 // time from many threads at once.  One device pass costs about the same for
 // 1 read set as for a few thousand, so the collector turns those calls into
 // batches, group-commit style: every caller queues its request; the first
-// caller that finds no batch running becomes the leader, takes everything
+// caller that finds no leader elected becomes the leader, takes everything
 // queued (up to max_batch, after an optional gather window of max_wait_us),
 // runs it as one hip_serial_check_batch and hands each caller its verdict.
 // Requests that arrive while a batch runs form the next batch, led by one of
@@ -16,39 +16,78 @@
 // Each request keeps bdb_osql_serial_check's contract: ranges == NULL -> 0
 // (no queueing), regop_only requests get the commit-after-snapshot verdict,
 // full requests get *file,*offset := end LSN, errors count as 1.
+//
+// Up to max_inflight batches run at once: hip_serial_check_batch releases the
+// context lock while a small batch's kernel runs, so the next leader marshals
+// and launches its batch meanwhile (the kernels queue on the context's
+// stream).  A caller sleeps on a futex word of its own request; a finished
+// batch sets its callers' done bits after dropping the collector lock (the
+// set is the last touch of a request: its caller may return right after).
 #include "../../include/hip_serial.h"
 
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <climits>
 #include <condition_variable>
+#include <cstdlib>
 #include <deque>
 #include <mutex>
 #include <vector>
+
+namespace {
+
+constexpr uint32_t kDone = 1u;  // Req::word: bit 0 = verdict ready, the rest counts wake-ups
+
+void futex_wait(std::atomic<uint32_t> *w, uint32_t seen)
+{
+    syscall(SYS_futex, (uint32_t *)w, FUTEX_WAIT_PRIVATE, seen, nullptr, nullptr, 0);
+}
+
+void futex_wake(std::atomic<uint32_t> *w)
+{
+    syscall(SYS_futex, (uint32_t *)w, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+}
+
+}  // namespace
 
 struct hsc_collector {
     hsc_ctx *ctx = nullptr;
     int max_batch = 0;
     int max_wait_us = 0;
+    int max_inflight = 2;
     std::mutex m;
     struct Req {
         void *ranges;
         unsigned int *file, *offset;
         int regop_only;
         int rc;
-        bool done;
-        std::condition_variable cv;  // this caller's wake-up: done, or elected leader
+        bool queued;  // in q (under m): not yet taken into a batch
+        std::atomic<uint32_t> word{0};
     };
     std::deque<Req *> q;
     bool elected = false;  // a leader is waiting to take the next batch
-    bool running = false;  // a batch is on the device
-    std::condition_variable run_cv;     // the running batch finished (elected leader waits)
-    std::condition_variable arrive_cv;  // a request queued (gathering leader waits)
+    int running = 0;       // batches on the device
+    std::condition_variable run_cv;     // a batch finished (the elected leader waits)
+    std::condition_variable arrive_cv;  // a request queued (a gathering leader waits)
     int inside = 0;                     // callers inside hsc_collector_check
     std::condition_variable idle_cv;    // inside dropped to 0 (destroy waits)
     hsc_collector_stats st{};
 };
 
 namespace {
+
+// wake a queued request's caller to re-check (it is elected leader); the
+// caller is alive: it cannot return before its done bit
+void poke(hsc_collector::Req *q)
+{
+    q->word.fetch_add(2, std::memory_order_release);
+    futex_wake(&q->word);
+}
 
 // one device pass over a group of requests that share regop_only
 void run_group(hsc_collector *k, std::vector<hsc_collector::Req *> &g, int regop_only)
@@ -84,7 +123,17 @@ int hsc_collector_create(hsc_ctx *ctx, int max_batch, int max_wait_us, hsc_colle
     k->ctx = ctx;
     k->max_batch = max_batch ? max_batch : 65536;
     k->max_wait_us = max_wait_us;
+    if (const char *e = getenv("HSC_COLLECT_INFLIGHT")) k->max_inflight = std::max(1, std::min(atoi(e), 4));
     *out = k;
+    return HSC_OK;
+}
+
+int hsc_collector_set_inflight(hsc_collector *k, int n)
+{
+    if (!k || n < 1 || n > 4) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(k->m);
+    k->max_inflight = n;
+    k->run_cv.notify_all();
     return HSC_OK;
 }
 
@@ -110,53 +159,64 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
     r.offset = offset ? offset : &a->offset;
     r.regop_only = regop_only;
     r.rc = 1;
-    r.done = false;
+    r.queued = true;
     std::unique_lock<std::mutex> lk(k->m);
     k->q.push_back(&r);
     k->st.calls++;
     k->inside++;
-    k->arrive_cv.notify_one();
-    // Waiters sleep on their own condition variable: a finished batch wakes
-    // exactly its callers, and the next leader is elected (and waiting for the
-    // device) while the current batch still runs, so its wake-up latency hides
-    // behind the device pass.
-    while (!r.done) {
-        if (k->elected) {
-            r.cv.wait(lk);
+    if (k->max_wait_us > 0) k->arrive_cv.notify_one();
+    for (;;) {
+        const uint32_t w = r.word.load(std::memory_order_acquire);
+        if (w & kDone) break;
+        // a request already in some batch waits for its verdict; a queued one
+        // leads when no leader is elected (futex: no lost wake-up)
+        if (k->elected || !r.queued) {
+            lk.unlock();
+            futex_wait(&r.word, w);
+            lk.lock();
             continue;
         }
         k->elected = true;  // this caller leads the next batch
-        k->run_cv.wait(lk, [k] { return !k->running; });
+        k->run_cv.wait(lk, [k] { return k->running < k->max_inflight; });
         if (k->max_wait_us > 0 && (int)k->q.size() < k->max_batch)
             k->arrive_cv.wait_for(lk, std::chrono::microseconds(k->max_wait_us),
                                   [k] { return (int)k->q.size() >= k->max_batch; });
         const size_t take = std::min(k->q.size(), (size_t)k->max_batch);
         std::vector<hsc_collector::Req *> full, regop;
+        bool mine = false;  // max_batch may leave this caller's own request queued
         for (size_t i = 0; i < take; ++i) {
             hsc_collector::Req *q = k->q.front();
             k->q.pop_front();
+            q->queued = false;
+            mine |= q == &r;
             (q->regop_only ? regop : full).push_back(q);
         }
-        k->running = true;
+        k->running++;
         k->elected = false;
-        if (!k->q.empty()) k->q.front()->cv.notify_one();  // elect the next leader now
+        if (!k->q.empty()) poke(k->q.front());  // elect the next leader now
         lk.unlock();
         const auto t0 = std::chrono::steady_clock::now();
         run_group(k, regop, 1);
         run_group(k, full, 0);
         const auto t1 = std::chrono::steady_clock::now();
         lk.lock();
-        k->running = false;
+        k->running--;
         k->st.busy_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
         k->st.batches++;
         k->st.max_batch = std::max<uint64_t>(k->st.max_batch, take);
+        k->run_cv.notify_one();
+        if (!k->elected && !k->q.empty()) poke(k->q.front());
+        lk.unlock();
+        // hand out the verdicts: each done bit is the last touch of its
+        // request (the futex wake only names the address)
         for (auto *g : {&regop, &full})
             for (hsc_collector::Req *q : *g) {
-                q->done = true;
-                if (q != &r) q->cv.notify_one();
+                if (q == &r) continue;
+                q->word.fetch_or(kDone, std::memory_order_release);
+                futex_wake(&q->word);
             }
-        k->run_cv.notify_one();
-        if (!k->elected && !k->q.empty()) k->q.front()->cv.notify_one();
+        lk.lock();
+        if (mine) break;
     }
     if (--k->inside == 0) k->idle_cv.notify_all();
     return r.rc;

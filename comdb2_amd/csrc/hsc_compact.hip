@@ -288,4 +288,13 @@ hipError_t compact_probes(const ProbeView &p, const CompactTables &t, uint64_t *
     }
 }
 
+// load this file's code object now (HIP loads it lazily at the first launch
+// of one of its kernels: ~1 ms, which would land inside the first build or
+// probe -- hsc_ctx_create calls every warm_* once)
+hipError_t warm_compact()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void *)k_group_pattern);
+}
+
 }  // namespace hsc

@@ -860,4 +860,13 @@ hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_i
     return hipGetLastError();
 }
 
+// load this file's code object now (HIP loads it lazily at the first launch
+// of one of its kernels: ~1 ms, which would land inside the first build or
+// probe -- hsc_ctx_create calls every warm_* once)
+hipError_t warm_ctiles()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void *)k_ct_rel);
+}
+
 }  // namespace hsc

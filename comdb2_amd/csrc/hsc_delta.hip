@@ -94,4 +94,13 @@ hipError_t launch_probe_delta(const DeltaView &d, const ProbeView &p, uint8_t *f
     return hipGetLastError();
 }
 
+// load this file's code object now (HIP loads it lazily at the first launch
+// of one of its kernels: ~1 ms, which would land inside the first build or
+// probe -- hsc_ctx_create calls every warm_* once)
+hipError_t warm_delta()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void *)k_delta_bmax);
+}
+
 }  // namespace hsc

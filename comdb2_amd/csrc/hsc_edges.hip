@@ -140,4 +140,13 @@ hipError_t launch_edge_emit(const EdgeView &w, const ProbeView &p, const uint2 *
     return hipGetLastError();
 }
 
+// load this file's code object now (HIP loads it lazily at the first launch
+// of one of its kernels: ~1 ms, which would land inside the first build or
+// probe -- hsc_ctx_create calls every warm_* once)
+hipError_t warm_edges()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void *)k_edge_count);
+}
+
 }  // namespace hsc

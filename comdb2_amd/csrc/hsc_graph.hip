@@ -767,4 +767,13 @@ hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *row
     return hipSuccess;
 }
 
+// load this file's code object now (HIP loads it lazily at the first launch
+// of one of its kernels: ~1 ms, which would land inside the first build or
+// probe -- hsc_ctx_create calls every warm_* once)
+hipError_t warm_graph()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void *)k_write_flags);
+}
+
 }  // namespace hsc

@@ -252,7 +252,8 @@ struct hsc_ctx {
     uint64_t commit_span[2] = {0, 0};  // oldest / newest distinct commit LSN of the window
     bool rank_lsn32 = false;   // narrow tiles: rows carry lsn - rank_base + 1 (NarrowTiles)
     bool nt_sorted = true;     // narrow tiles: chunk-sorted records (HSC_NT_SORT=0 at build: scatter)
-    bool nt_fused = true;      // chunk-sorted narrow tiles: plan-free join (HSC_NT_FUSED=0 at build: plan + join)
+    bool nt_fused = false;     // chunk-sorted narrow tiles: plan-free join (HSC_NT_FUSED=1 at build;
+                               // r03: one stream 61.9 -> 60.2 us, two streams 45.3 -> 47.7 us)
     bool ct_sorted = true;     // compact tiles: chunk-sorted records (HSC_CT_SORT=0 at build: scatter)
     bool ct_fused = false;     // ... and the plan-free join (HSC_CT_FUSED=1 at build; measured slower)
     uint64_t rank_base = 0;
@@ -328,13 +329,28 @@ struct hsc_ctx {
     int lane = 0;
     uint64_t lane_tick = 0;
 
-    // small batches (k_small_narrow): probe columns, verdict bytes and the
-    // done word in fine-grained pinned memory; the kernel's block counter
-    HBuf small_io;
+    // small batches (k_small_narrow): a ring of slots, each with the probe
+    // columns, verdict bytes and done word in fine-grained pinned memory and
+    // its own block counter.  A slot belongs to one call from its launch
+    // (under mu) until that call has read its verdicts (without mu), so a
+    // second call can marshal and launch while the first one's kernel runs.
+    static constexpr int kSmallSlots = 4;
+    struct SmallSlot {
+        HBuf io;
+        std::vector<uint8_t> forced;
+        size_t n_txn = 0, vo = 0, dn = 0;
+        uint32_t seq = 0;
+        std::atomic<bool> busy{false};
+    };
+    SmallSlot small[kSmallSlots];
+    uint32_t small_next = 0;
     DBuf small_blocks;
     bool small_blocks_zeroed = false;
     bool no_small = false;  // HSC_NO_SMALL=1 at context creation: the staged path
     uint32_t small_seq = 0;
+    // small-path phase times (hsc_small_stats)
+    std::atomic<uint64_t> sm_calls{0}, sm_marshal_ns{0}, sm_launch_ns{0}, sm_wait_ns{0},
+        sm_slot_waits{0};
 
     // timing
     bool timing = false;
@@ -992,7 +1008,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
             const uint64_t *span = c->commit_span;
             c->rank_lsn32 = span[1] - span[0] <= kLsn32MaxSpan && !getenv("HSC_RANK_DIR");
             c->nt_sorted = !getenv("HSC_NT_SORT") || atoi(getenv("HSC_NT_SORT")) != 0;
-            c->nt_fused = !getenv("HSC_NT_FUSED") || atoi(getenv("HSC_NT_FUSED")) != 0;
+            c->nt_fused = getenv("HSC_NT_FUSED") && atoi(getenv("HSC_NT_FUSED")) != 0;
             c->rank_base = span[0];
             c->cdir = Dir16{};
             if (!c->rank_lsn32)
@@ -2580,23 +2596,51 @@ static bool small_path(hsc_ctx *c, int T)
     return !c->no_small && c->narrow && !c->timing && T <= kSmallMaxTxns && c->n > 0;
 }
 
-static int run_small(hsc_ctx *c, Stage &st, int *rc_out)
+using SteadyClock = std::chrono::steady_clock;
+static uint64_t ns_since(SteadyClock::time_point t0)
 {
-    const size_t vo = (st.L.total + 63) & ~(size_t)63;
-    const size_t dn = (vo + st.n_txn + 63) & ~(size_t)63;
-    if (c->small_io.ensure(dn + 64, true, true)) return fail(c, HSC_ENOMEM, "small-batch staging");
-    HIPCHK(c, c->small_blocks.ensure(64));
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(SteadyClock::now() - t0).count();
+}
+
+// Under c->mu: copy the marshalled batch st into a free slot and launch its
+// kernel on c->stream.  With every slot taken, wait for the oldest launch's
+// owner to release it (owners release without c->mu, so this cannot block
+// them).  -> slot index, or < 0 (an HSC_ error code, already recorded).
+static int small_launch(hsc_ctx *c, Stage &st)
+{
+    int k = -1;
+    for (int i = 0; i < hsc_ctx::kSmallSlots && k < 0; ++i) {
+        const int j = (int)((c->small_next + i) % hsc_ctx::kSmallSlots);
+        if (!c->small[j].busy.load(std::memory_order_acquire)) k = j;
+    }
+    if (k < 0) {
+        c->sm_slot_waits.fetch_add(1, std::memory_order_relaxed);
+        k = (int)(c->small_next % hsc_ctx::kSmallSlots);  // launched first, finishes first
+        const auto t0 = SteadyClock::now();
+        while (c->small[k].busy.load(std::memory_order_acquire)) {
+            __builtin_ia32_pause();
+            if (SteadyClock::now() - t0 > std::chrono::seconds(60))
+                return fail(c, HSC_EDEVICE, "small-batch slot not released within 60 s");
+        }
+    }
+    hsc_ctx::SmallSlot &sl = c->small[k];
+    sl.vo = (st.L.total + 63) & ~(size_t)63;
+    sl.dn = (sl.vo + st.n_txn + 63) & ~(size_t)63;
+    sl.n_txn = st.n_txn;
+    if (sl.io.ensure(sl.dn + 64, true, true)) return fail(c, HSC_ENOMEM, "small-batch staging");
+    HIPCHK(c, c->small_blocks.ensure(64 * hsc_ctx::kSmallSlots));
     hipStream_t s = c->stream;
     if (!c->small_blocks_zeroed) {
-        HIPCHK(c, hipMemsetAsync(c->small_blocks.p, 0, 64, s));
+        HIPCHK(c, hipMemsetAsync(c->small_blocks.p, 0, 64 * hsc_ctx::kSmallSlots, s));
         c->small_blocks_zeroed = true;
     }
-    uint8_t *io = c->small_io.as<uint8_t>(), *dio = (uint8_t *)c->small_io.dp;
+    uint8_t *io = sl.io.as<uint8_t>(), *dio = (uint8_t *)sl.io.dp;
     if (st.L.total) memcpy(io, st.arena.p, st.L.total);
-    memset(io + vo, 0, st.n_txn);
-    volatile uint32_t *done = (volatile uint32_t *)(io + dn);
+    memset(io + sl.vo, 0, st.n_txn);
+    sl.forced.assign(st.forced.as<uint8_t>(), st.forced.as<uint8_t>() + st.n_txn);
+    volatile uint32_t *done = (volatile uint32_t *)(io + sl.dn);
     if (++c->small_seq == 0) c->small_seq = 1;
-    const uint32_t seq = c->small_seq;
+    sl.seq = c->small_seq;
     *done = 0;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     ProbeView p{};
@@ -2616,36 +2660,66 @@ static int run_small(hsc_ctx *c, Stage &st, int *rc_out)
     DeltaView d{}, d2{};
     if (c->dn) d = delta_view(c);
     if (c->fn) d2 = frozen_view(c);
-    HIPCHK(c, launch_small_narrow(nv, d, d2, p, dio + vo, c->small_blocks.as<uint32_t>(),
-                                  (uint32_t *)(dio + dn), seq, s));
-    // poll the done word; every few thousand spins ask the stream whether it
-    // failed (a fault never releases the word)
-    const auto t0 = std::chrono::steady_clock::now();
+    HIPCHK(c, launch_small_narrow(nv, d, d2, p, dio + sl.vo, c->small_blocks.as<uint32_t>() + 16 * k,
+                                  (uint32_t *)(dio + sl.dn), sl.seq, s));
+    sl.busy.store(true, std::memory_order_release);
+    c->small_next = (uint32_t)(k + 1);
+    return k;
+}
+
+// Without c->mu: poll slot k's done word (every few thousand spins ask the
+// stream whether it failed: a fault never releases the word), read the
+// verdicts, release the slot.  Errors come back as (code, message) for the
+// caller to record under c->mu.
+static int small_wait(hsc_ctx *c, int k, hipStream_t s, int *rc_out, const char **why,
+                      hipError_t *herr)
+{
+    hsc_ctx::SmallSlot &sl = c->small[k];
+    const uint8_t *io = sl.io.as<uint8_t>();
+    volatile const uint32_t *done = (volatile const uint32_t *)(io + sl.dn);
+    const uint32_t seq = sl.seq;
+    const auto t0 = SteadyClock::now();
+    int rc = HSC_OK;
+    bool running = false;  // timed out: the kernel may still write the slot
     for (uint32_t spin = 1; *done != seq; ++spin) {
         __builtin_ia32_pause();
         if ((spin & 4095) == 0) {
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30))
-                return fail(c, HSC_EDEVICE, "small batch did not finish within 30 s");
-            const hipError_t e = hipStreamQuery(s);
-            if (e == hipSuccess) {
-                if (*done != seq) return fail(c, HSC_EDEVICE, "small batch finished without its done word");
+            if (SteadyClock::now() - t0 > std::chrono::seconds(30)) {
+                rc = HSC_EDEVICE, *why = "small batch did not finish within 30 s";
+                running = true;
                 break;
             }
-            if (e != hipErrorNotReady) return fail(c, HSC_EDEVICE, "small batch", e);
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipSuccess) {
+                if (*done != seq) rc = HSC_EDEVICE, *why = "small batch finished without its done word";
+                break;
+            }
+            if (e != hipErrorNotReady) {
+                rc = HSC_EDEVICE, *why = "small batch", *herr = e;
+                break;
+            }
         }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
-    const uint8_t *f = st.forced.as<uint8_t>(), *v = io + vo;
-    for (size_t t = 0; t < st.n_txn; ++t) rc_out[t] = (f[t] | v[t]) ? 1 : 0;
-    return HSC_OK;
+    if (rc == HSC_OK) {
+        const uint8_t *v = io + sl.vo;
+        for (size_t t = 0; t < sl.n_txn; ++t) rc_out[t] = (sl.forced[t] | v[t]) ? 1 : 0;
+    }
+    // a slot whose kernel may still write it stays taken
+    if (!running) sl.busy.store(false, std::memory_order_release);
+    c->sm_wait_ns.fetch_add(ns_since(t0), std::memory_order_relaxed);
+    return rc;
 }
 
 // Full checks of every read set of src: marshal (host threads) -> upload ->
 // join -> download.  A large batch runs as a pipeline of chunks over the two
 // staging sets: chunk i + 1 is marshalled on the host while chunk i is
 // uploaded, probed and read back.
+// lk (the caller's hold on c->mu, may be null): a small batch releases it
+// while its kernel runs and returns without it.
 template <class Src>
-static int check_src(hsc_ctx *c, const Src &src, int *rc_out)
+static int check_src(hsc_ctx *c, const Src &src, int *rc_out,
+                     std::unique_lock<std::mutex> *lk = nullptr)
 {
     if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
     const int T = src.ntxn();
@@ -2653,9 +2727,28 @@ static int check_src(hsc_ctx *c, const Src &src, int *rc_out)
     const int per = std::max(1, (T + nchunks - 1) / nchunks);
     if (nchunks == 1 && small_path(c, T)) {
         Stage &st = c->stage[0];
+        const auto t0 = SteadyClock::now();
         int rc = marshal_into(c, src, 0, T, st);
-        if (rc == HSC_OK && st.n <= kSmallMaxRanges && st.n_lock <= kSmallMaxRanges)
-            return run_small(c, st, rc_out);
+        if (rc == HSC_OK && st.n <= kSmallMaxRanges && st.n_lock <= kSmallMaxRanges) {
+            const auto t1 = SteadyClock::now();
+            const int k = small_launch(c, st);
+            if (k < 0) return k;
+            c->sm_calls.fetch_add(1, std::memory_order_relaxed);
+            c->sm_marshal_ns.fetch_add(
+                (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count(),
+                std::memory_order_relaxed);
+            c->sm_launch_ns.fetch_add(ns_since(t1), std::memory_order_relaxed);
+            hipStream_t s = c->stream;
+            if (lk) lk->unlock();
+            const char *why = nullptr;
+            hipError_t herr = hipSuccess;
+            rc = small_wait(c, k, s, rc_out, &why, &herr);
+            if (rc != HSC_OK) {
+                if (lk) lk->lock();
+                return fail(c, rc, why, herr);
+            }
+            return HSC_OK;
+        }
         if (rc == HSC_OK) rc = launch_stage(c, st);
         if (rc == HSC_OK) rc = finish_stage(c, st, rc_out);
         if (rc != HSC_OK) (void)hipStreamSynchronize(c->stream);
@@ -2720,6 +2813,19 @@ int hsc_ctx_create(int device, hsc_ctx **out)
         return HSC_EDEVICE;
     }
     c->stream = c->own_stream;
+    // every file's code object now, not lazily inside the first build / probe
+    static std::mutex warm_mu;
+    static std::vector<bool> warmed;
+    {
+        std::lock_guard<std::mutex> g(warm_mu);
+        if (warmed.size() < (size_t)n) warmed.resize(n, false);
+        if (!warmed[device]) {
+            for (auto f : {warm_kernels, warm_ingest, warm_narrow, warm_ctiles, warm_delta,
+                           warm_compact, warm_coalesce, warm_edges, warm_graph})
+                (void)f();
+            warmed[device] = true;
+        }
+    }
     *out = c;
     return HSC_OK;
 }
@@ -2755,7 +2861,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->w_tcode2, &c->w_trecs};
     for (DBuf *b : bufs) b->release();
     for (Stage &st : c->stage) st.release();
-    c->small_io.release();
+    for (auto &sl : c->small) sl.io.release();
     c->small_blocks.release();
     for (DBuf *b : {&c->d_dgid[0], &c->d_dgid[1], &c->d_dwords[0], &c->d_dwords[1], &c->d_dlsn[0],
                     &c->d_dlsn[1], &c->d_dbmax, &c->d_agid, &c->d_awords, &c->d_alsn})
@@ -3398,7 +3504,7 @@ int hip_serial_check_batch(void *vctx, void *const *ranges, unsigned int *file,
 {
     hsc_ctx *c = (hsc_ctx *)vctx;
     if (!c || n < 0 || (n && (!ranges || !rc_out)) || (!file) != (!offset)) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    std::unique_lock<std::mutex> lk(c->mu);  // a small batch drops it while its kernel runs
     if (!c->host_only) (void)hipSetDevice(c->device);
     int rc = ensure_built(c);
     if (rc) {
@@ -3429,10 +3535,21 @@ int hip_serial_check_batch(void *vctx, void *const *ranges, unsigned int *file,
     }
     if (full.empty()) return HSC_OK;
     std::vector<int> rcs(full.size(), 1);
-    rc = check_src(c, ArrSrc{full.data(), snaps.data(), (int)full.size()}, rcs.data());
+    rc = check_src(c, ArrSrc{full.data(), snaps.data(), (int)full.size()}, rcs.data(), &lk);
     for (int i = 0; i < n; ++i)
         if (slot[i] >= 0) rc_out[i] = rc ? 1 : rcs[slot[i]];
     return rc;
+}
+
+int hsc_small_stats(hsc_ctx *c, hsc_small_stats_t *out)
+{
+    if (!c || !out) return HSC_EINVAL;
+    out->calls = c->sm_calls.load();
+    out->marshal_ns = c->sm_marshal_ns.load();
+    out->launch_ns = c->sm_launch_ns.load();
+    out->wait_ns = c->sm_wait_ns.load();
+    out->slot_waits = c->sm_slot_waits.load();
+    return HSC_OK;
 }
 
 int hsc_set_threads(hsc_ctx *c, int n)

@@ -335,4 +335,13 @@ hipError_t packed_sort_rows(const PackPlan &P, size_t n, const uint32_t *gid, co
     return hipGetLastError();
 }
 
+// load this file's code object now (HIP loads it lazily at the first launch
+// of one of its kernels: ~1 ms, which would land inside the first build or
+// probe -- hsc_ctx_create calls every warm_* once)
+hipError_t warm_ingest()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void *)k_pk_count);
+}
+
 }  // namespace hsc

@@ -587,4 +587,15 @@ hipError_t launch_pack(const uint8_t *verdict, uint32_t n_txn, uint64_t *bitmap,
 hipError_t launch_or_bitmaps(const uint64_t *parts, int nparts, size_t words, uint64_t *out,
                              hipStream_t s);
 
+// per-file code-object warm-up (hsc_ctx_create)
+hipError_t warm_kernels();
+hipError_t warm_ingest();
+hipError_t warm_narrow();
+hipError_t warm_ctiles();
+hipError_t warm_delta();
+hipError_t warm_compact();
+hipError_t warm_coalesce();
+hipError_t warm_edges();
+hipError_t warm_graph();
+
 }  // namespace hsc

@@ -549,6 +549,41 @@ __global__ void k_sparse_level(uint32_t ntiles, int level, uint64_t *tmax)
     tmax[(size_t)level * ntiles + t] = a > b ? a : b;
 }
 
+// Every level l >= 1 of the sparse table in one workgroup (windows of up to
+// kSparseLdsTiles tiles): level l - 1 lives in LDS, each thread takes its
+// pairs into registers, a barrier, then the level is written over it (and out).
+// One launch instead of one ~4.6 us launch per level.
+constexpr uint32_t kSparseLdsTiles = 8192;
+constexpr int kSparseThreads = 1024;
+__global__ __launch_bounds__(kSparseThreads) void k_sparse_all(uint32_t ntiles, int levels,
+                                                               uint64_t *tmax)
+{
+    extern __shared__ uint64_t lv[];
+    constexpr int R = kSparseLdsTiles / kSparseThreads;
+    for (uint32_t t = threadIdx.x; t < ntiles; t += kSparseThreads) lv[t] = tmax[t];
+    __syncthreads();
+    for (int l = 1; l < levels; ++l) {
+        const uint32_t h = 1u << (l - 1);
+        uint64_t m[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t t = threadIdx.x + r * kSparseThreads;
+            const uint64_t a = t < ntiles ? lv[t] : 0, b = t + h < ntiles ? lv[t + h] : 0;
+            m[r] = a > b ? a : b;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t t = threadIdx.x + r * kSparseThreads;
+            if (t < ntiles) {
+                lv[t] = m[r];
+                tmax[(size_t)l * ntiles + t] = m[r];
+            }
+        }
+        __syncthreads();
+    }
+}
+
 // Per-table max commit LSN over the key rows: one workgroup per group, whole
 // tiles of its row span from the tile-max sparse table, the partial tiles at
 // both ends scanned; one atomic per group (rows of a group are contiguous).
@@ -602,8 +637,11 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
     if (w.n == 0) return hipSuccess;
     k_group_bounds<<<(w.n + 255) / 256, 256, 0, s>>>(w.n, w.gid, gstart, gend);
     k_tile_max<<<w.ntiles, 256, 0, s>>>(w.n, w.log2T, w.lsn, tmax);
-    for (int l = 1; l < w.levels; ++l)
-        k_sparse_level<<<(w.ntiles + 255) / 256, 256, 0, s>>>(w.ntiles, l, tmax);
+    if (w.levels > 1 && w.ntiles <= kSparseLdsTiles)
+        k_sparse_all<<<1, kSparseThreads, 8 * (size_t)w.ntiles, s>>>(w.ntiles, w.levels, tmax);
+    else
+        for (int l = 1; l < w.levels; ++l)
+            k_sparse_level<<<(w.ntiles + 255) / 256, 256, 0, s>>>(w.ntiles, l, tmax);
     if (ngroups > 0 && table_max) {
         WinView wt = w;
         wt.tmax = tmax;
@@ -1254,6 +1292,15 @@ hipError_t launch_or_bitmaps(const uint64_t *parts, int nparts, size_t words, ui
     if (words == 0) return hipSuccess;
     k_or_bitmaps<<<(unsigned)((words + 255) / 256), 256, 0, s>>>(parts, nparts, words, out);
     return hipGetLastError();
+}
+
+// load this file's code object now (HIP loads it lazily at the first launch
+// of one of its kernels: ~1 ms, which would land inside the first build or
+// probe -- hsc_ctx_create calls every warm_* once)
+hipError_t warm_kernels()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void *)k_compact);
 }
 
 }  // namespace hsc

@@ -1854,4 +1854,13 @@ hipError_t launch_pack_flags(uint8_t *flags, uint32_t n_txn, uint8_t *verdict, u
     return hipGetLastError();
 }
 
+// load this file's code object now (HIP loads it lazily at the first launch
+// of one of its kernels: ~1 ms, which would land inside the first build or
+// probe -- hsc_ctx_create calls every warm_* once)
+hipError_t warm_narrow()
+{
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, (const void *)k_end_rows);
+}
+
 }  // namespace hsc

@@ -121,6 +121,11 @@ class CollectorStats(C.Structure):
                 ("busy_ns", C.c_uint64)]
 
 
+class SmallStats(C.Structure):
+    _fields_ = [("calls", C.c_uint64), ("marshal_ns", C.c_uint64), ("launch_ns", C.c_uint64),
+                ("wait_ns", C.c_uint64), ("slot_waits", C.c_uint64)]
+
+
 class ConcurrentResult(C.Structure):
     _fields_ = [("seconds", C.c_double), ("calls", C.c_uint64), ("lat_mean_us", C.c_double),
                 ("lat_p50_us", C.c_double), ("lat_p99_us", C.c_double)]
@@ -143,7 +148,8 @@ EXPORTS = [
     "hsc_window_code_words", "hsc_window_tile_key_words", "hsc_window_append_log", "hsc_window_append_raw",
     "hsc_window_delta_rows", "hsc_set_threads", "hsc_currangearrs_build",
     "hsc_currangearrs_free", "hsc_collector_create", "hsc_collector_destroy",
-    "hsc_collector_check", "hsc_collector_get_stats", "hsc_harness_concurrent",
+    "hsc_collector_check", "hsc_collector_get_stats", "hsc_collector_set_inflight",
+    "hsc_small_stats", "hsc_harness_concurrent",
     "hsc_dep_graph_build", "hsc_dep_graph_stage_rw_pairs", "hsc_dep_graph_scc_built", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
 ]
 
@@ -231,6 +237,8 @@ def load() -> C.CDLL:
         "hsc_collector_check": (C.c_int, [_p, _p, C.POINTER(C.c_uint), C.POINTER(C.c_uint),
                                           C.c_int]),
         "hsc_collector_get_stats": (C.c_int, [_p, C.POINTER(CollectorStats)]),
+        "hsc_collector_set_inflight": (C.c_int, [_p, C.c_int]),
+        "hsc_small_stats": (C.c_int, [_p, C.POINTER(SmallStats)]),
         "hsc_harness_concurrent": (C.c_int, [_p, _p, C.POINTER(_p), C.c_int, C.c_int, C.c_int,
                                              C.c_int, C.POINTER(C.c_int),
                                              C.POINTER(ConcurrentResult)]),
@@ -624,8 +632,19 @@ class Validator:
         self._chk(rc, "hip_serial_check_batch")
         return out[:n]
 
+    def small_stats(self) -> dict:
+        """Small-batch path phase totals (hsc_small_stats): calls and the mean
+        host marshal, slot copy + launch and done-word wait per call (us)."""
+        st = SmallStats()
+        self._chk(self.lib.hsc_small_stats(self.ctx, C.byref(st)), "hsc_small_stats")
+        n = max(1, st.calls)
+        return {"calls": st.calls, "marshal_us": st.marshal_ns / 1e3 / n,
+                "launch_us": st.launch_ns / 1e3 / n, "wait_us": st.wait_ns / 1e3 / n,
+                "slot_waits": st.slot_waits}
+
     def concurrent_check(self, arrs, nthreads: int, rounds: int = 1, regop_only: int = 0,
-                         collect: bool = True, max_batch: int = 0, max_wait_us: int = 0):
+                         collect: bool = True, max_batch: int = 0, max_wait_us: int = 0,
+                         inflight: int = 0):
         """nthreads native caller threads checking arrs concurrently
         (hsc_harness_concurrent), each call one read set through a batching
         collector (hsc_collector_check) or, collect=False, one
@@ -636,7 +655,12 @@ class Validator:
         if collect:
             self._chk(self.lib.hsc_collector_create(self.ctx, max_batch, max_wait_us,
                                                     C.byref(col)), "hsc_collector_create")
+            if inflight:
+                self._chk(self.lib.hsc_collector_set_inflight(col, inflight),
+                          "hsc_collector_set_inflight")
         res = ConcurrentResult()
+        sm0 = SmallStats()
+        self._chk(self.lib.hsc_small_stats(self.ctx, C.byref(sm0)), "hsc_small_stats")
         try:
             rc = self.lib.hsc_harness_concurrent(self.ctx, col, arrs.pointers(), n, nthreads,
                                                  rounds, regop_only,
@@ -655,6 +679,15 @@ class Validator:
                           mean_batch=cs.calls / max(1, cs.batches),
                           device_pass_us=cs.busy_ns / 1e3 / max(1, cs.batches),
                           busy_frac=cs.busy_ns / 1e9 / max(res.seconds, 1e-9))
+            sm = SmallStats()
+            self._chk(self.lib.hsc_small_stats(self.ctx, C.byref(sm)), "hsc_small_stats")
+            k = sm.calls - sm0.calls
+            if k:  # device passes that took the small-batch path: mean phase times
+                st["small_path"] = {"passes": k,
+                                    "marshal_us": (sm.marshal_ns - sm0.marshal_ns) / 1e3 / k,
+                                    "launch_us": (sm.launch_ns - sm0.launch_ns) / 1e3 / k,
+                                    "wait_us": (sm.wait_ns - sm0.wait_ns) / 1e3 / k,
+                                    "slot_waits": sm.slot_waits - sm0.slot_waits}
         finally:
             if collect:
                 self.lib.hsc_collector_destroy(col)

@@ -401,11 +401,25 @@ typedef struct hsc_collector_stats {
     uint64_t max_batch;  /* largest batch */
     uint64_t busy_ns;    /* time inside the batches' device passes */
 } hsc_collector_stats;
+/* Small-batch path (batches of <= 1024 read sets over a narrow window: one
+ * k_small_narrow launch over fine-grained host memory) phase totals since
+ * the context was created: host marshal, slot copy + launch, and the wait
+ * for the kernel's done word (hip_serial_check_batch releases the context
+ * lock while it waits, so concurrent callers overlap). */
+typedef struct hsc_small_stats_t {
+    uint64_t calls, marshal_ns, launch_ns, wait_ns;
+    uint64_t slot_waits; /* launches that found every slot in flight */
+} hsc_small_stats_t;
+int hsc_small_stats(hsc_ctx *ctx, hsc_small_stats_t *out);
 int hsc_collector_create(hsc_ctx *ctx, int max_batch, int max_wait_us, hsc_collector **out);
 void hsc_collector_destroy(hsc_collector *col);
 int hsc_collector_check(hsc_collector *col, void *ranges, unsigned int *file,
                         unsigned int *offset, int regop_only);
 int hsc_collector_get_stats(hsc_collector *col, hsc_collector_stats *out);
+/* Batches allowed on the device at once (1..4; default 2, or
+ * HSC_COLLECT_INFLIGHT at creation): with 2, the next leader marshals and
+ * launches while the previous batch's kernel runs. */
+int hsc_collector_set_inflight(hsc_collector *col, int n);
 /* Read/write conflict pairs before the OR-reduction:
  * every (read set t, writer commit LSN c) such that a write committed at c
  * (c > t's snapshot) has a key inside one of t's ranges -- all the pairs the

@@ -33,13 +33,13 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
     # commit rank (directory search of snapshots) with HSC_RANK_DIR set; the
     # bucket table in linear or log mode (HSC_TRAD_MODE; by default the build
     # picks the mode whose fullest bucket is smaller); records chunk-sorted
-    # (default) or scattered into tile buckets (HSC_NT_SORT=0); the join scans
-    # its tile's column itself and packs the verdicts in its last block
-    # (default) or after a plan kernel (HSC_NT_FUSED=0)
+    # (default) or scattered into tile buckets (HSC_NT_SORT=0); the join reads
+    # its tile's column from a plan kernel (default) or scans it itself, the
+    # verdicts packed after it (HSC_NT_FUSED=1)
     runs = [(LAYOUT_NARROW_DIRECT, None), (LAYOUT_NARROW_TILES, None),
             (LAYOUT_NARROW_TILES, "HSC_TILE_DIR"), (LAYOUT_NARROW_TILES, "HSC_RANK_DIR"),
             (LAYOUT_NARROW_TILES, "HSC_TRAD_MODE=log"), (LAYOUT_NARROW_TILES, "HSC_TRAD_MODE=lin"),
-            (LAYOUT_NARROW_TILES, "HSC_NT_SORT=0"), (LAYOUT_NARROW_TILES, "HSC_NT_FUSED=0"),
+            (LAYOUT_NARROW_TILES, "HSC_NT_SORT=0"), (LAYOUT_NARROW_TILES, "HSC_NT_FUSED=1"),
             (LAYOUT_NARROW_CODES, None), (LAYOUT_WIDE, None)]
     try:
         for layout, knob in runs:
