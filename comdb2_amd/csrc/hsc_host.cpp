@@ -1795,6 +1795,7 @@ struct FlatSrc {
             return x;
         });
     }
+    void prefetch(int, int) const {}
 };
 
 // ... or CurRangeArr pointers (the drop-in entry; db/comdb2.h:1105-1124)
@@ -1824,6 +1825,24 @@ struct ArrSrc {
             x.islocked = r->islocked;
             return x;
         });
+    }
+    // A small batch's CurRangeArrs come from other threads' heaps (a
+    // collector's callers): touch them level by level -- arrays, range
+    // pointers, ranges, keys and names -- so each level's cache misses are
+    // in flight together instead of one after another in the marshal.
+    void prefetch(int t0, int t1) const
+    {
+        for (int t = t0; t < t1; ++t) __builtin_prefetch(arr[t]);
+        for (int t = t0; t < t1; ++t) __builtin_prefetch(arr[t]->ranges);
+        for (int t = t0; t < t1; ++t)
+            for (int k = 0; k < arr[t]->size; ++k) __builtin_prefetch(arr[t]->ranges[k]);
+        for (int t = t0; t < t1; ++t)
+            for (int k = 0; k < arr[t]->size; ++k) {
+                const hsc_currange *r = arr[t]->ranges[k];
+                __builtin_prefetch(r->tbname);
+                if (r->lkey) __builtin_prefetch(r->lkey);
+                if (r->rkey) __builtin_prefetch(r->rkey);
+            }
     }
 };
 
@@ -1883,6 +1902,7 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
     if ((int)c->parts.size() < nwork) c->parts.resize(nwork);
     if (st.forced.ensure((size_t)std::max(nt, 1), !c->host_only)) return fail(c, HSC_ENOMEM, "staging");
     uint8_t *forced = st.forced.as<uint8_t>();
+    if (nt < kMarshalParallelMin) src.prefetch(t0, t1);
     par_for(nt >= kMarshalParallelMin ? c->threads : 1, nwork, [&](int w) {
         MarshalPart &mp = c->parts[w];
         mp.clear();

@@ -199,9 +199,22 @@ hipError_t narrow_build(const WinView &w, const NarrowView &nv, hipStream_t s)
 constexpr int kProbeThreads = 256;
 constexpr int kNP = 4;  // ranges per 16-lane group in flight
 
+// A conflict mark.  kHost: the verdict bytes live in fine-grained host memory
+// (the small-batch path) -- a system-scope store writes through to it, so the
+// kernel's completion needs no L2 write-back.
+template <bool kHost>
+__device__ __forceinline__ void mark_verdict(uint8_t *v)
+{
+    if constexpr (kHost)
+        __hip_atomic_store(v, (uint8_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else
+        *v = 1;
+}
+
 // The ranges of p answered by 16-lane groups, kNP ranges each: wave w of the
 // grid starts at range wave0 and strides by wstride.  Levels >= lds_from are
 // read from top (LDS, lds_base = their offset), the rest from the window.
+template <bool kHost = false>
 __device__ __forceinline__ void narrow_probe_ranges(const NarrowView &nv, const ProbeView &p,
                                                     uint8_t *verdict, const uint64_t *top,
                                                     uint64_t lds_base, int lds_from,
@@ -309,19 +322,20 @@ __device__ __forceinline__ void narrow_probe_ranges(const NarrowView &nv, const 
         if (l16 == 0) {
 #pragma unroll
             for (int k = 0; k < kNP; ++k)
-                if (found[k]) verdict[txn[k]] = 1;
+                if (found[k]) mark_verdict<kHost>(verdict + txn[k]);
         }
     }
 }
 
 // table locks q = first, first + stride, ...: any write to a locked table
 // after the snapshot
+template <bool kHost = false>
 __device__ __forceinline__ void narrow_probe_locks(const NarrowView &nv, const ProbeView &p,
                                                    uint8_t *verdict, uint32_t first, uint32_t stride)
 {
     for (uint32_t q = first; q < p.n_lock; q += stride) {
         const uint32_t t = p.lock_table[q];
-        if (t < nv.ntables && nv.table_max[t] > p.lock_snap[q]) verdict[p.lock_txn[q]] = 1;
+        if (t < nv.ntables && nv.table_max[t] > p.lock_snap[q]) mark_verdict<kHost>(verdict + p.lock_txn[q]);
     }
 }
 
@@ -346,7 +360,11 @@ __global__ __launch_bounds__(kProbeThreads) void k_probe_narrow(NarrowView nv, P
 // for it), the delta run and the table locks.  The probe columns are read
 // straight from the caller's pinned staging and the verdict bytes written into
 // it (fine-grained host memory the GPU maps: no copies); the last block to
-// finish releases `seq` into *done at system scope, which the host polls.
+// finish stores `seq` into *done, which the host polls.  Completion needs no
+// cache write-back: every verdict byte is a write-through system-scope store,
+// each thread waits for its stores before the block counts itself done, and
+// the done word is written (write-through, same path to the host) after the
+// last block's count.
 constexpr int kSmallThreads = 256;
 
 __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, DeltaView d,
@@ -357,19 +375,21 @@ __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, D
 {
     const uint32_t groups = gridDim.x * (kSmallThreads / 16);
     const uint32_t wave0 = (blockIdx.x * (kSmallThreads / 16) + ((threadIdx.x >> 6) << 2)) * kNP;
-    narrow_probe_ranges(nv, p, verdict, nullptr, 0, nv.levels, wave0, groups * kNP);
+    narrow_probe_ranges<true>(nv, p, verdict, nullptr, 0, nv.levels, wave0, groups * kNP);
     const uint32_t tid = blockIdx.x * kSmallThreads + threadIdx.x, nth = gridDim.x * kSmallThreads;
     if (d.n || d2.n)  // the live run and a frozen one (background fold)
         for (uint32_t q = tid; q < p.n; q += nth)
-            if ((d.n && delta_hit(d, p, q)) || (d2.n && delta_hit(d2, p, q))) verdict[p.txn[q]] = 1;
-    narrow_probe_locks(nv, p, verdict, tid, nth);
+            if ((d.n && delta_hit(d, p, q)) || (d2.n && delta_hit(d2, p, q)))
+                mark_verdict<true>(verdict + p.txn[q]);
+    narrow_probe_locks<true>(nv, p, verdict, tid, nth);
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's verdict stores are done
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence_system();  // this block's verdict bytes reach the host first
-        if (atomicAdd(blocks_done, 1u) == gridDim.x - 1) {
-            *blocks_done = 0;  // the next launch on the stream counts from zero
-            __threadfence_system();
-            __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (__hip_atomic_fetch_add(blocks_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            gridDim.x - 1) {
+            // the next launch of this slot counts from zero (stream order)
+            __hip_atomic_store(blocks_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
