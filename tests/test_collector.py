@@ -18,13 +18,14 @@ def host():
     v.close()
 
 
-@pytest.mark.parametrize("nthreads", [1, 4, 16])
-def test_regop_only_through_collector(host, oracle_mod, nthreads):
+@pytest.mark.parametrize("nthreads,inflight", [(1, 0), (4, 0), (16, 0), (16, 1), (16, 4), (32, 3)])
+def test_regop_only_through_collector(host, oracle_mod, nthreads, inflight):
+    # inflight: batches the collector lets run at once (0 = its default, 2)
     log, rs = random_case(321 + nthreads, broken=True, n_txn=400)
     host.ingest_log(log)
     want, _, _ = oracle_mod.check(log, rs, regop_only=1)
     arrs = NativeCurRangeArrs(rs)
-    got, st = host.concurrent_check(arrs, nthreads, rounds=3, regop_only=1)
+    got, st = host.concurrent_check(arrs, nthreads, rounds=3, regop_only=1, inflight=inflight)
     np.testing.assert_array_equal(got != 0, want != 0)
     assert st["calls"] == 3 * rs.ntxn
     assert 1 <= st["batches"] <= st["calls"] and st["max_batch"] <= nthreads
@@ -56,16 +57,50 @@ def test_full_checks_fail_closed_without_device(host):
     arrs.close()
 
 
+def test_collector_inflight_bounds():
+    from comdb2_amd.hsc import load
+    import ctypes as C
+    lib = load()
+    assert lib.hsc_collector_set_inflight(None, 2) != 0
+    host = Validator(-1)
+    col = C.c_void_p()
+    assert lib.hsc_collector_create(host.ctx, 0, 0, C.byref(col)) == 0
+    try:
+        for bad in (0, 5, -1):
+            assert lib.hsc_collector_set_inflight(col, bad) != 0
+        for ok in (1, 4):
+            assert lib.hsc_collector_set_inflight(col, ok) == 0
+    finally:
+        lib.hsc_collector_destroy(col)
+        host.close()
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("nthreads", [2, 16, 64])
-def test_gpu_full_checks_through_collector(validator, oracle_mod, nthreads):
+@pytest.mark.parametrize("nthreads,inflight", [(2, 0), (16, 0), (64, 0), (64, 1), (64, 4)])
+def test_gpu_full_checks_through_collector(validator, oracle_mod, nthreads, inflight):
+    # the small-batch kernels of up to `inflight` batches queue on the stream
+    # while their callers wait without the context lock
     log, rs = random_case(700 + nthreads, broken=(nthreads == 16), n_txn=600, max_ranges=12)
     validator.ingest_log(log)
     want, _, _ = oracle_mod.check(log, rs)
     arrs = NativeCurRangeArrs(rs)
-    got, st = validator.concurrent_check(arrs, nthreads, rounds=2)
+    got, st = validator.concurrent_check(arrs, nthreads, rounds=2, inflight=inflight)
     np.testing.assert_array_equal(got != 0, want != 0)
     assert st["calls"] == 2 * rs.ntxn and st["max_batch"] <= nthreads
+    arrs.close()
+
+
+@pytest.mark.gpu
+def test_gpu_uncollected_callers_share_small_slots(validator, oracle_mod):
+    # 32 threads calling hip_bdb_osql_serial_check directly: each releases the
+    # context lock while its kernel runs, so up to 4 slots are in flight
+    log, rs = random_case(811, n_txn=800, max_ranges=12)
+    validator.ingest_log(log)
+    want, _, _ = oracle_mod.check(log, rs)
+    arrs = NativeCurRangeArrs(rs)
+    got, st = validator.concurrent_check(arrs, 32, rounds=2, collect=False)
+    np.testing.assert_array_equal(got != 0, want != 0)
+    assert st["small_path"]["passes"] > 0
     arrs.close()
 
 
