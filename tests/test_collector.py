@@ -91,17 +91,22 @@ def test_gpu_full_checks_through_collector(validator, oracle_mod, nthreads, infl
 
 
 @pytest.mark.gpu
-def test_gpu_uncollected_callers_share_small_slots(validator, oracle_mod):
-    # 32 threads calling hip_bdb_osql_serial_check directly: each releases the
-    # context lock while its kernel runs, so up to 4 slots are in flight
-    log, rs = random_case(811, n_txn=800, max_ranges=12)
-    validator.ingest_log(log)
-    want, _, _ = oracle_mod.check(log, rs)
-    arrs = NativeCurRangeArrs(rs)
-    got, st = validator.concurrent_check(arrs, 32, rounds=2, collect=False)
-    np.testing.assert_array_equal(got != 0, want != 0)
-    assert st["small_path"]["passes"] > 0
-    arrs.close()
+def test_gpu_uncollected_callers_share_small_slots(oracle_mod):
+    # 32 threads calling hip_bdb_osql_serial_check directly on a narrow window
+    # (the small-batch path): each releases the context lock while its kernel
+    # runs, so up to 4 slots are in flight
+    v = Validator(0)
+    try:
+        wl = config2(n_commits=20_000, n_txn=2_000, seed=13)
+        v.ingest_log(wl.log)
+        want, _, _ = oracle_mod.check(wl.log, wl.readsets)
+        arrs = NativeCurRangeArrs(wl.readsets)
+        got, st = v.concurrent_check(arrs, 32, rounds=2, collect=False)
+        np.testing.assert_array_equal(got != 0, want != 0)
+        assert st["small_path"]["passes"] == 2 * wl.readsets.ntxn
+        arrs.close()
+    finally:
+        v.close()
 
 
 @pytest.mark.gpu
