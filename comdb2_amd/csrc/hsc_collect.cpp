@@ -24,6 +24,7 @@
 // batch sets its callers' done bits after dropping the collector lock (the
 // set is the last touch of a request: its caller may return right after).
 #include "../../include/hip_serial.h"
+#include "hsc_internal.h"
 
 #include <linux/futex.h>
 #include <sys/syscall.h>
@@ -36,6 +37,7 @@
 #include <condition_variable>
 #include <cstdlib>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <vector>
 
@@ -59,13 +61,15 @@ struct hsc_collector {
     hsc_ctx *ctx = nullptr;
     int max_batch = 0;
     int max_wait_us = 0;
-    int max_inflight = 2;
+    int max_inflight = 1;
+    bool premarshal = true;  // callers marshal their own read set before queueing (HSC_PREMARSHAL=0: off)
     std::mutex m;
     struct Req {
         void *ranges;
         unsigned int *file, *offset;
         int regop_only;
         int rc;
+        hsc::PreMarshal *pm;  // the caller's marshalled rows, or null
         bool queued;  // in q (under m): not yet taken into a batch
         std::atomic<uint32_t> word{0};
     };
@@ -95,15 +99,19 @@ void run_group(hsc_collector *k, std::vector<hsc_collector::Req *> &g, int regop
     const int n = (int)g.size();
     if (!n) return;
     std::vector<void *> ranges(n);
+    std::vector<hsc::PreMarshal *> pm(n);
     std::vector<unsigned int> file(n), offset(n);
     std::vector<int> rc_out(n, 1);
     for (int i = 0; i < n; ++i) {
         ranges[i] = g[i]->ranges;
+        pm[i] = g[i]->pm;
         file[i] = *g[i]->file;
         offset[i] = *g[i]->offset;
     }
-    const int rc = hip_serial_check_batch(k->ctx, ranges.data(), file.data(), offset.data(),
-                                          regop_only, n, rc_out.data());
+    const int rc = regop_only ? hip_serial_check_batch(k->ctx, ranges.data(), file.data(),
+                                                       offset.data(), 1, n, rc_out.data())
+                              : hsc::check_batch_pre(k->ctx, ranges.data(), pm.data(), file.data(),
+                                                     offset.data(), n, rc_out.data());
     for (int i = 0; i < n; ++i) {
         *g[i]->file = file[i];  // full mode wrote curlsn back; regop_only left it
         *g[i]->offset = offset[i];
@@ -124,6 +132,7 @@ int hsc_collector_create(hsc_ctx *ctx, int max_batch, int max_wait_us, hsc_colle
     k->max_batch = max_batch ? max_batch : 65536;
     k->max_wait_us = max_wait_us;
     if (const char *e = getenv("HSC_COLLECT_INFLIGHT")) k->max_inflight = std::max(1, std::min(atoi(e), 4));
+    if (const char *e = getenv("HSC_PREMARSHAL")) k->premarshal = atoi(e) != 0;
     *out = k;
     return HSC_OK;
 }
@@ -160,6 +169,16 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
     r.regop_only = regop_only;
     r.rc = 1;
     r.queued = true;
+    r.pm = nullptr;
+    // Marshal this caller's own read set now, in its own thread, against the
+    // context's dictionary snapshot: the leader then copies rows instead of
+    // walking every caller's CurRanges.  The object is the thread's own and
+    // stays untouched by it until this call returns.
+    static thread_local std::unique_ptr<hsc::PreMarshal, void (*)(hsc::PreMarshal *)> tl_pm(
+        hsc::premarshal_new(), hsc::premarshal_free);
+    if (!regop_only && k->premarshal && tl_pm &&
+        hsc::premarshal(k->ctx, a, ((uint64_t)*r.file << 32) | *r.offset, tl_pm.get()))
+        r.pm = tl_pm.get();
     std::unique_lock<std::mutex> lk(k->m);
     k->q.push_back(&r);
     k->st.calls++;

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <memory>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -149,6 +150,18 @@ constexpr int kPipeTxns = 32768;           // read sets per pipeline chunk of a 
 
 struct MarshalPart;
 
+// The dictionaries a marshal reads (key words, groups, table ids) as an
+// immutable snapshot: a collector's callers marshal their own read set
+// against it before they queue (premarshal, no context lock), and a batch
+// takes those rows only if the context's dictionary epoch has not moved.
+struct MarshalDict {
+    uint64_t epoch = 0;
+    int W = 1;
+    std::unordered_map<std::string, int> table_ids;
+    std::vector<GroupInfo> groups;
+    std::unordered_map<uint64_t, std::vector<int>> ix_groups;
+};
+
 struct hsc_ctx {
     int device = 0;
     bool host_only = false;
@@ -163,6 +176,8 @@ struct hsc_ctx {
     std::unordered_map<uint64_t, int> group_ids;                    // (tid,ix,klen)
     std::vector<GroupInfo> groups;
     std::unordered_map<uint64_t, std::vector<int>> ix_groups;       // (tid,ix) -> gids
+    uint64_t dict_epoch = 1;  // bumped when a table, a group or W changes
+    std::shared_ptr<const MarshalDict> dict_snap;  // published under mu
 
     // host staging of the window (host ingest paths)
     std::vector<uint32_t> h_gid;
@@ -443,10 +458,17 @@ static int table_id_or_add(hsc_ctx *c, const char *name)
     auto it = c->table_ids.find(name);
     if (it != c->table_ids.end()) return it->second;
     int tid = (int)c->table_names.size();
+    c->dict_epoch++;
     c->table_ids.emplace(name, tid);
     c->table_names.emplace_back(name);
     c->h_table_max.push_back(0);
     return tid;
+}
+
+static void set_words(hsc_ctx *c, int W)
+{
+    if (c->W != W) c->dict_epoch++;
+    c->W = W;
 }
 
 static int group_id_or_add(hsc_ctx *c, int tid, int ix, int klen)
@@ -457,6 +479,7 @@ static int group_id_or_add(hsc_ctx *c, int tid, int ix, int klen)
     auto it = c->group_ids.find(k);
     if (it != c->group_ids.end()) return it->second;
     int g = (int)c->groups.size();
+    c->dict_epoch++;
     c->groups.push_back({tid, ix, klen});
     c->group_ids.emplace(k, g);
     c->ix_groups[ixkey(tid, ix)].push_back(g);
@@ -1065,7 +1088,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
 static int build_from_host(hsc_ctx *c)
 {
     const size_t n_in = c->h_gid.size();
-    c->W = window_words(c);
+    set_words(c, window_words(c));
     const int W = c->W;
     c->cap = window_cap(n_in);
     const size_t cap = c->cap;
@@ -1293,7 +1316,7 @@ static int merge_delta(hsc_ctx *c)
     std::swap(c->d_words, wd);
     std::swap(c->d_lsn, l);
     g.release(), wd.release(), l.release();
-    c->W = W;
+    set_words(c, W);
     c->cap = cap;
     return device_build(c, n_in);
 }
@@ -1304,6 +1327,7 @@ static int merge_delta(hsc_ctx *c)
 static void swap_window(hsc_ctx *a, hsc_ctx *b)
 {
     using std::swap;
+    if (a->W != b->W) a->dict_epoch++, b->dict_epoch++;
     swap(a->W, b->W), swap(a->n, b->n), swap(a->cap, b->cap), swap(a->n_all, b->n_all);
     swap(a->ng_built, b->ng_built);
     swap(a->ntiles, b->ntiles), swap(a->log2T, b->log2T), swap(a->levels, b->levels);
@@ -1468,7 +1492,7 @@ static void fold_discard(hsc_ctx *c)
 static int ensure_built(hsc_ctx *c)
 {
     if (c->host_only) {  // dictionaries + marshalling only
-        c->W = window_words(c);
+        set_words(c, window_words(c));
         return HSC_OK;
     }
     HIPCHK_RC(c, fold_finish(c, false));
@@ -1689,9 +1713,8 @@ struct MarshalPart {
     }
 };
 
-template <class Get>
-static void marshal_txn(const hsc_ctx *c, MarshalPart &mp, uint32_t txn, uint64_t S, int nr,
-                        Get get)
+template <class D, class Get>  // D: hsc_ctx or a MarshalDict snapshot
+static void marshal_txn(const D *c, MarshalPart &mp, uint32_t txn, uint64_t S, int nr, Get get)
 {
     const int W = c->W;
     auto &tabs = mp.tabs;
@@ -1753,8 +1776,9 @@ static void marshal_txn(const hsc_ctx *c, MarshalPart &mp, uint32_t txn, uint64_
 
 // Table name -> window table id, with a one-entry cache (a read set names a
 // few tables; comdb2 strdup's every CurRange's name, so pointers differ).
-struct TableLookup {
-    const hsc_ctx *c;
+template <class D>
+struct TableLookupT {
+    const D *c;
     const char *last = nullptr;
     int last_tid = -1;
     int operator()(const char *name)
@@ -1766,6 +1790,14 @@ struct TableLookup {
         last_tid = it == c->table_ids.end() ? -1 : it->second;
         return last_tid;
     }
+};
+using TableLookup = TableLookupT<hsc_ctx>;
+
+// A caller's own read set marshalled ahead of its batch (hsc_collect.cpp):
+// the rows of marshal_txn (txn 0) against the snapshot of epoch `epoch`.
+struct hsc::PreMarshal {
+    uint64_t epoch = 0;
+    MarshalPart mp;
 };
 
 // Source of read sets: flat arrays (hsc_readsets) ...
@@ -1796,13 +1828,36 @@ struct FlatSrc {
         });
     }
     void prefetch(int, int) const {}
+    bool premarshalled(const hsc_ctx *, int, MarshalPart &, uint32_t) const { return false; }
 };
+
+// append a premarshalled read set's rows as read set `txn` of the batch
+static void append_pre(const PreMarshal &pm, MarshalPart &mp, uint32_t txn)
+{
+    const MarshalPart &q = pm.mp;
+    mp.lohi.insert(mp.lohi.end(), q.lohi.begin(), q.lohi.end());
+    mp.gid.insert(mp.gid.end(), q.gid.begin(), q.gid.end());
+    mp.snap.insert(mp.snap.end(), q.snap.begin(), q.snap.end());
+    mp.txn.insert(mp.txn.end(), q.txn.size(), txn);
+    mp.lock_table.insert(mp.lock_table.end(), q.lock_table.begin(), q.lock_table.end());
+    mp.lock_snap.insert(mp.lock_snap.end(), q.lock_snap.begin(), q.lock_snap.end());
+    mp.lock_txn.insert(mp.lock_txn.end(), q.lock_txn.size(), txn);
+}
 
 // ... or CurRangeArr pointers (the drop-in entry; db/comdb2.h:1105-1124)
 struct ArrSrc {
     hsc_currangearr *const *arr;
     const uint64_t *snaps;
     int n;
+    PreMarshal *const *pre = nullptr;  // per read set, may be null: marshalled by its caller
+    uint64_t epoch = 0;                // the context's dictionary epoch now
+    bool pre_ok(int t) const { return pre && pre[t] && pre[t]->epoch == epoch; }
+    bool premarshalled(const hsc_ctx *, int t, MarshalPart &mp, uint32_t txn) const
+    {
+        if (!pre_ok(t)) return false;
+        append_pre(*pre[t], mp, txn);
+        return true;
+    }
     int ntxn() const { return n; }
     uint64_t snap(int t) const { return snaps[t]; }
     template <class F>
@@ -1832,12 +1887,14 @@ struct ArrSrc {
     // in flight together instead of one after another in the marshal.
     void prefetch(int t0, int t1) const
     {
-        for (int t = t0; t < t1; ++t) __builtin_prefetch(arr[t]);
-        for (int t = t0; t < t1; ++t) __builtin_prefetch(arr[t]->ranges);
         for (int t = t0; t < t1; ++t)
-            for (int k = 0; k < arr[t]->size; ++k) __builtin_prefetch(arr[t]->ranges[k]);
+            if (!pre_ok(t)) __builtin_prefetch(arr[t]);
         for (int t = t0; t < t1; ++t)
-            for (int k = 0; k < arr[t]->size; ++k) {
+            if (!pre_ok(t)) __builtin_prefetch(arr[t]->ranges);
+        for (int t = t0; t < t1; ++t)
+            for (int k = 0; !pre_ok(t) && k < arr[t]->size; ++k) __builtin_prefetch(arr[t]->ranges[k]);
+        for (int t = t0; t < t1; ++t)
+            for (int k = 0; !pre_ok(t) && k < arr[t]->size; ++k) {
                 const hsc_currange *r = arr[t]->ranges[k];
                 __builtin_prefetch(r->tbname);
                 if (r->lkey) __builtin_prefetch(r->lkey);
@@ -1913,6 +1970,7 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
             const int f = full_forced(c, S);
             forced[t - t0] = f > 0;
             if (f >= 0) continue;
+            if (src.premarshalled(c, t, mp, (uint32_t)(t - t0))) continue;
             src.each(t, tl, [&](int nr, auto get) { marshal_txn(c, mp, (uint32_t)(t - t0), S, nr, get); });
         }
     });
@@ -3103,7 +3161,7 @@ int hsc_window_ingest_device(hsc_ctx *c, size_t n, int words, const uint32_t *gi
     c->host_staged = false;
     c->end_lsn = end_lsn;
     if (words < window_words(c)) return fail(c, HSC_EINVAL, "fewer key words than a registered group needs");
-    c->W = words;
+    set_words(c, words);
     c->cap = window_cap(n);
     HIPCHK(c, c->d_gid.ensure(c->cap * 4));
     HIPCHK(c, c->d_words.ensure(c->cap * 8 * (size_t)words));
@@ -3519,10 +3577,74 @@ int hsc_check_readsets(hsc_ctx *c, const hsc_readsets *rs, int *rc_out)
     return rc;
 }
 
+// Publish the dictionaries as a snapshot for premarshal (under c->mu; only
+// when the epoch moved).
+static void publish_dict(hsc_ctx *c)
+{
+    const std::shared_ptr<const MarshalDict> cur = std::atomic_load(&c->dict_snap);
+    if (cur && cur->epoch == c->dict_epoch) return;
+    auto d = std::make_shared<MarshalDict>();
+    d->epoch = c->dict_epoch;
+    d->W = c->W;
+    d->table_ids = c->table_ids;
+    d->groups = c->groups;
+    d->ix_groups = c->ix_groups;
+    std::atomic_store(&c->dict_snap, std::shared_ptr<const MarshalDict>(std::move(d)));
+}
+
+static int check_batch(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, unsigned int *file,
+                       unsigned int *offset, int regop_only, int n, int *rc_out);
+
 int hip_serial_check_batch(void *vctx, void *const *ranges, unsigned int *file,
                            unsigned int *offset, int regop_only, int n, int *rc_out)
 {
-    hsc_ctx *c = (hsc_ctx *)vctx;
+    return check_batch((hsc_ctx *)vctx, ranges, nullptr, file, offset, regop_only, n, rc_out);
+}
+
+}  // extern "C"
+
+namespace hsc {
+PreMarshal *premarshal_new() { return new (std::nothrow) PreMarshal; }
+void premarshal_free(PreMarshal *pm) { delete pm; }
+
+// A caller's read set marshalled against the published dictionary snapshot,
+// without the context lock.  false: no snapshot yet (the batch marshals it).
+bool premarshal(hsc_ctx *c, const hsc_currangearr *a, uint64_t S, PreMarshal *pm)
+{
+    const std::shared_ptr<const MarshalDict> d = std::atomic_load(&c->dict_snap);
+    if (!d || !a || !pm) return false;
+    pm->epoch = d->epoch;
+    pm->mp.clear();
+    TableLookupT<MarshalDict> tl{d.get()};
+    marshal_txn(d.get(), pm->mp, 0, S, a->size, [&, a](int k) {
+        const hsc_currange *r = a->ranges[k];
+        RangeRef x;
+        x.tid = tl(r->tbname);
+        x.idxnum = r->idxnum;
+        x.lkey = (const uint8_t *)r->lkey;
+        x.rkey = (const uint8_t *)r->rkey;
+        x.lkeylen = r->lkeylen;
+        x.rkeylen = r->rkeylen;
+        x.lflag = r->lflag;
+        x.rflag = r->rflag;
+        x.islocked = r->islocked;
+        return x;
+    });
+    return true;
+}
+
+int check_batch_pre(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, unsigned int *file,
+                    unsigned int *offset, int n, int *rc_out)
+{
+    return check_batch(c, ranges, pre, file, offset, 0, n, rc_out);
+}
+}  // namespace hsc
+
+extern "C" {
+
+static int check_batch(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, unsigned int *file,
+                       unsigned int *offset, int regop_only, int n, int *rc_out)
+{
     if (!c || n < 0 || (n && (!ranges || !rc_out)) || (!file) != (!offset)) return HSC_EINVAL;
     std::unique_lock<std::mutex> lk(c->mu);  // a small batch drops it while its kernel runs
     if (!c->host_only) (void)hipSetDevice(c->device);
@@ -3531,11 +3653,14 @@ int hip_serial_check_batch(void *vctx, void *const *ranges, unsigned int *file,
         for (int i = 0; i < n; ++i) rc_out[i] = 1;
         return rc;
     }
+    publish_dict(c);
     std::vector<int> slot(n, -1);  // element -> txn index in the device batch
     std::vector<hsc_currangearr *> full;
+    std::vector<PreMarshal *> fpre;
     std::vector<uint64_t> snaps;
     full.reserve(n);
     snaps.reserve(n);
+    if (pre) fpre.reserve(n);
     for (int i = 0; i < n; ++i) {
         hsc_currangearr *a = (hsc_currangearr *)ranges[i];
         rc_out[i] = 0;
@@ -3552,10 +3677,13 @@ int hip_serial_check_batch(void *vctx, void *const *ranges, unsigned int *file,
         slot[i] = (int)full.size();
         full.push_back(a);
         snaps.push_back(S);
+        if (pre) fpre.push_back(pre[i]);
     }
     if (full.empty()) return HSC_OK;
     std::vector<int> rcs(full.size(), 1);
-    rc = check_src(c, ArrSrc{full.data(), snaps.data(), (int)full.size()}, rcs.data(), &lk);
+    ArrSrc src{full.data(), snaps.data(), (int)full.size()};
+    if (pre) src.pre = fpre.data(), src.epoch = c->dict_epoch;
+    rc = check_src(c, src, rcs.data(), &lk);
     for (int i = 0; i < n; ++i)
         if (slot[i] >= 0) rc_out[i] = rc ? 1 : rcs[slot[i]];
     return rc;

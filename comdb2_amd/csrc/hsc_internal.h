@@ -587,6 +587,17 @@ hipError_t launch_pack(const uint8_t *verdict, uint32_t n_txn, uint64_t *bitmap,
 hipError_t launch_or_bitmaps(const uint64_t *parts, int nparts, size_t words, uint64_t *out,
                              hipStream_t s);
 
+// Premarshal (hsc_collect.cpp): a caller marshals its own read set against
+// the context's published dictionary snapshot before it queues; the batch
+// (check_batch_pre = hip_serial_check_batch, full checks) takes those rows
+// while the snapshot's epoch is current and marshals the rest itself.
+struct PreMarshal;
+PreMarshal *premarshal_new();
+void premarshal_free(PreMarshal *pm);
+bool premarshal(hsc_ctx *c, const hsc_currangearr *a, uint64_t S, PreMarshal *pm);
+int check_batch_pre(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, unsigned int *file,
+                    unsigned int *offset, int n, int *rc_out);
+
 // per-file code-object warm-up (hsc_ctx_create)
 hipError_t warm_kernels();
 hipError_t warm_ingest();

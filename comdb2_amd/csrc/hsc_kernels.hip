@@ -512,13 +512,32 @@ hipError_t dedupe_rows(int W, size_t n, const uint32_t *gid, const uint64_t *wor
 }
 
 // ---- summaries: group spans, tile maxima, sparse table, table maxima ------
-__global__ void k_group_bounds(uint32_t n, const uint32_t *gid, uint32_t *gstart, uint32_t *gend)
+// Rows are sorted by gid: group g's span is [#gid < g, #gid <= g), two binary
+// searches per group (a group with no rows gets an empty span) instead of a
+// pass over every row's gid.  gid == nullptr: one group holding every row.
+__global__ void k_group_bounds(uint32_t n, const uint32_t *gid, int ngroups, uint32_t *gstart,
+                               uint32_t *gend)
 {
-    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t g = gid[i];
-    if (i == 0 || gid[i - 1] != g) gstart[g] = i;
-    if (i + 1 == n || gid[i + 1] != g) gend[g] = i + 1;
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (uint32_t)ngroups) return;
+    if (!gid) {
+        gstart[g] = 0;
+        gend[g] = n;
+        return;
+    }
+    uint32_t lo = 0, hi = n;  // #gid < g
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (gid[mid] < g) lo = mid + 1; else hi = mid;
+    }
+    const uint32_t a = lo;
+    hi = n;  // #gid <= g
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (gid[mid] <= g) lo = mid + 1; else hi = mid;
+    }
+    gstart[g] = a;
+    gend[g] = lo;
 }
 
 __global__ __launch_bounds__(256) void k_tile_max(uint32_t n, int log2T, const uint64_t *lsn,
@@ -631,11 +650,14 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
                            uint64_t *tmax, const uint32_t *group_table, uint64_t *table_max,
                            uint32_t *sp_g, uint64_t *sp_w, hipStream_t s)
 {
-    hipError_t e = hipMemsetAsync(gstart, 0, sizeof(uint32_t) * (size_t)ngroups, s);
-    if (e == hipSuccess) e = hipMemsetAsync(gend, 0, sizeof(uint32_t) * (size_t)ngroups, s);
-    if (e != hipSuccess) return e;
-    if (w.n == 0) return hipSuccess;
-    k_group_bounds<<<(w.n + 255) / 256, 256, 0, s>>>(w.n, w.gid, gstart, gend);
+    if (w.n == 0) {
+        hipError_t e = hipMemsetAsync(gstart, 0, sizeof(uint32_t) * (size_t)ngroups, s);
+        if (e == hipSuccess) e = hipMemsetAsync(gend, 0, sizeof(uint32_t) * (size_t)ngroups, s);
+        return e;
+    }
+    if (ngroups > 0)
+        k_group_bounds<<<(ngroups + 255) / 256, 256, 0, s>>>(w.n, ngroups == 1 ? nullptr : w.gid,
+                                                             ngroups, gstart, gend);
     k_tile_max<<<w.ntiles, 256, 0, s>>>(w.n, w.log2T, w.lsn, tmax);
     if (w.levels > 1 && w.ntiles <= kSparseLdsTiles)
         k_sparse_all<<<1, kSparseThreads, 8 * (size_t)w.ntiles, s>>>(w.ntiles, w.levels, tmax);
