@@ -770,6 +770,9 @@ def main():
     tw = torch.from_numpy(words.reshape(-1).view(np.int64)).to(dev)
     tl = torch.from_numpy(lsn.view(np.int64)).to(dev)
     v.ingest_device(n_w, words.shape[0], tg.data_ptr(), tw.data_ptr(), tl.data_ptr(), end_lsn)
+    ingest_cold_ms = v.timing()["ingest_ms"]  # first build: its buffers are allocated inside
+    # the same rows again: a rebuild over allocated buffers (a fold, a re-ingest)
+    v.ingest_device(n_w, words.shape[0], tg.data_ptr(), tw.data_ptr(), tl.data_ptr(), end_lsn)
     ingest_ms = v.timing()["ingest_ms"]
     del tg, tw, tl
     if c3 is not None:
@@ -986,8 +989,12 @@ def main():
         # window build (sort + dedupe + summaries), SURVEY 8(d): reported apart
         # from the probe phase; bytes = N_w * (L^ + 8 LSN + 4 group)
         "ingest": {"rows": int(n_w), "algorithmic_bytes": int(n_w) * (8 * W + 12),
-                   "GBps": int(n_w) * (8 * W + 12) / (ingest_ms * 1e-3) / 1e9 if ingest_ms else None},
-        "cold_e2e_ms": ingest_ms + ms_per_step,
+                   "GBps": int(n_w) * (8 * W + 12) / (ingest_ms * 1e-3) / 1e9 if ingest_ms else None,
+                   "ms": ingest_ms, "cold_ms": ingest_cold_ms,
+                   "note": "window build (device_build: sort, dedupe, summaries, narrow index) "
+                           "of rows already in HBM, timed by events around it; ms = a rebuild "
+                           "over allocated buffers, cold_ms = the context's first build"},
+        "cold_e2e_ms": ingest_cold_ms + ms_per_step,
         "cpu_baseline": None,
     }
     if traffic:

@@ -2732,6 +2732,8 @@ static int small_launch(hsc_ctx *c, Stage &st)
     p.lock_txn = (const uint32_t *)(dio + st.L.lock_txn);
     p.n = (uint32_t)st.n;
     p.n_lock = (uint32_t)st.n_lock;
+    static const bool empty = getenv("HSC_SMALL_EMPTY") != nullptr;  // diagnostics: the
+    if (empty) p.n = p.n_lock = 0;  // launch + done-word floor (verdicts all 0: wrong answers)
     NarrowView nv = c->nv;
     nv.table_max = c->d_table_max.as<uint64_t>();
     nv.ntables = (uint32_t)c->table_names.size();
