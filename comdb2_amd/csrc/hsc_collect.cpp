@@ -61,7 +61,7 @@ struct hsc_collector {
     hsc_ctx *ctx = nullptr;
     int max_batch = 0;
     int max_wait_us = 0;
-    int max_inflight = 1;
+    int max_inflight = 2;
     bool premarshal = true;  // callers marshal their own read set before queueing (HSC_PREMARSHAL=0: off)
     std::mutex m;
     struct Req {

@@ -842,7 +842,24 @@ static int device_build(hsc_ctx *c, size_t n_in)
     bt.stamp("commits");
     PackPlan plan;
     c->packed_sort = try_packed && packed_plan(W, n_in, vary, &plan);
-    if (c->packed_sort) {
+    const bool fused_dd = !getenv("HSC_PK_DD") || atoi(getenv("HSC_PK_DD")) != 0;
+    if (c->packed_sort && fused_dd) {
+        // every version, key-sorted, into d_*2; the distinct rows straight from
+        // the unpack into d_gid / d_words (in place) and a free key buffer,
+        // which becomes d_lsn (the input LSNs are gathered while it is written)
+        uint64_t *dl = nullptr;
+        HIPCHK(c, packed_sort_dedupe(plan, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
+                                     c->d_lsn.as<uint64_t>(), cap, c->d_pk[0].as<uint64_t>(),
+                                     c->d_pk[1].as<uint64_t>(), c->d_gid2.as<uint32_t>(),
+                                     c->d_words2.as<uint64_t>(), c->d_lsn2.as<uint64_t>(), cap,
+                                     c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(), cap, &dl,
+                                     c->d_count.as<uint32_t>(), c->d_scratch.p, c->d_scratch.bytes, s));
+        if (dl == c->d_pk[0].p)
+            std::swap(c->d_lsn, c->d_pk[0]);
+        else if (dl == c->d_pk[1].p)
+            std::swap(c->d_lsn, c->d_pk[1]);
+        bt.stamp("sort");
+    } else if (c->packed_sort) {
         // every version, key-sorted, into d_*2; the distinct rows into d_*
         HIPCHK(c, packed_sort_rows(plan, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
                                    c->d_lsn.as<uint64_t>(), cap, c->d_pk[0].as<uint64_t>(),

@@ -263,12 +263,167 @@ __global__ __launch_bounds__(kUnpackThreads) void k_pk_unpack(
     flags[i] = last ? 1u : 0u;
 }
 
+// ---- unpack fused with the dedupe ----
+// Every version goes to (gid_o, words_o, lsn_o) as in k_pk_unpack, and the
+// last version of each key straight to its place among the distinct rows
+// (gid_d, words_d, lsn_d): a block's place is the exclusive scan of the
+// blocks' distinct counts (k_pk_bcount), a row's inside the block a scan in
+// LDS -- no flag array, no 10M-entry scan, no compaction pass re-reading every
+// version.  The distinct outputs may overwrite the input gid / words (only row
+// 0's limbs are read, from r0), not the input LSNs (gathered by row index).
+constexpr int kUdThreads = 256;
+constexpr int kUdRows = 8;                            // rows per thread
+constexpr int kUdTile = kUdThreads * kUdRows;         // rows per block
+
+__device__ __forceinline__ bool pk_last(const uint64_t *keys, size_t n, size_t i, int I)
+{
+    return i + 1 >= n || (keys[i + 1] >> I) != (keys[i] >> I);
+}
+
+__global__ __launch_bounds__(kUdThreads) void k_pk_bcount(size_t n, const uint64_t *keys, int I,
+                                                          uint32_t *bc)
+{
+    __shared__ uint32_t wsum[kUdThreads / 64];
+    const size_t base = (size_t)blockIdx.x * kUdTile;
+    uint32_t c = 0;
+#pragma unroll
+    for (int r = 0; r < kUdRows; ++r) {
+        const size_t i = base + (size_t)r * kUdThreads + threadIdx.x;
+        if (i < n) c += pk_last(keys, n, i, I);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < kUdThreads / 64; ++w) t += wsum[w];
+        bc[blockIdx.x] = t;
+    }
+}
+
+__global__ void k_pk_row0(int W, const uint32_t *gid_in, const uint64_t *words_in, size_t stride_in,
+                          uint64_t *r0)
+{
+    const int j = threadIdx.x;
+    if (j < W) r0[j] = words_in[(size_t)j * stride_in];
+    if (j == W) r0[W] = gid_in[0];
+}
+
+template <int WT>  // key words 1..3, 0 = any (<= kPackMaxWords)
+__global__ __launch_bounds__(kUdThreads) void k_pk_unpack_dd(
+    PackPlan P, size_t n, const uint64_t *keys, const uint64_t *r0, const uint64_t *lsn_in,
+    uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o, const uint32_t *boff,
+    uint32_t *gid_d, uint64_t *words_d, uint64_t *lsn_d, size_t stride_d, uint32_t *d_count)
+{
+    __shared__ uint64_t K[kUdTile + 1];
+    __shared__ uint32_t pos[kUdTile];
+    __shared__ uint32_t wsum[kUdThreads / 64];
+    const int W = WT ? WT : P.W;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const size_t base = (size_t)blockIdx.x * kUdTile;
+    const uint32_t nrows = (uint32_t)min((size_t)kUdTile, n - base);
+#pragma unroll
+    for (int r = 0; r < kUdRows; ++r) {
+        const uint32_t j = r * kUdThreads + threadIdx.x;
+        if (j < nrows) K[j] = keys[base + j];
+    }
+    if (threadIdx.x == 0 && base + nrows < n) K[nrows] = keys[base + nrows];
+    __syncthreads();
+    // thread t ranks rows 8t .. 8t + 7 of the block (contiguous): last-of-key
+    // flags, their count, a wave scan and a block scan
+    const uint64_t lim = P.I >= 64 ? 0 : ~0ull << P.I;  // the key bits
+    uint32_t fl = 0, cnt = 0;
+#pragma unroll
+    for (int r = 0; r < kUdRows; ++r) {
+        const uint32_t j = threadIdx.x * kUdRows + r;
+        const bool last = j < nrows && (base + j + 1 >= n || ((K[j] ^ K[j + 1]) & lim) != 0);
+        fl |= (uint32_t)last << r;
+        cnt += last;
+    }
+    uint32_t inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t run = inc - cnt, total = 0;
+#pragma unroll
+    for (int w = 0; w < kUdThreads / 64; ++w) {
+        run += w < wv ? wsum[w] : 0;
+        total += wsum[w];
+    }
+#pragma unroll
+    for (int r = 0; r < kUdRows; ++r) {
+        const uint32_t j = threadIdx.x * kUdRows + r;
+        if (j < nrows) pos[j] = (fl >> r & 1u) ? run : 0xFFFFFFFFu;
+        run += fl >> r & 1u;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *d_count = boff[blockIdx.x] + total;
+    __syncthreads();
+    const uint32_t b0 = boff[blockIdx.x];
+    const uint64_t imask = P.I >= 64 ? ~0ull : (1ull << P.I) - 1;
+#pragma unroll 2
+    for (int r = 0; r < kUdRows; ++r) {
+        const uint32_t j = r * kUdThreads + threadIdx.x;
+        if (j >= nrows) break;
+        const size_t i = base + j;
+        const uint64_t key = K[j];
+        uint64_t kb = key >> P.I;
+        const uint64_t lv = lsn_in[key & imask];
+        uint64_t limb[kPackMaxWords + 1];
+#pragma unroll
+        for (int q = 0; q <= kPackMaxWords; ++q) {
+            if (q > W) break;
+            limb[q] = r0[q];
+        }
+#pragma unroll
+        for (int l = kPackLimbs - 1; l >= 0; --l) {  // least significant varying limb first
+            if (l >= P.nl) continue;
+            const int b = P.bits[l];
+            const uint64_t part = b >= 64 ? kb : kb & ((1ull << b) - 1);
+            kb = b >= 64 ? 0 : kb >> b;
+            uint64_t mv[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) mv[q] = P.mv[l][q];
+            const int id = P.limb[l];
+            const uint64_t v = pk_expand(part, P.mask[l], mv);
+#pragma unroll
+            for (int q = 0; q <= kPackMaxWords; ++q)
+                if (q == id) limb[q] = (limb[q] & ~P.mask[l]) | v;
+        }
+        gid_o[i] = (uint32_t)limb[W];
+#pragma unroll
+        for (int q = 0; q < kPackMaxWords; ++q) {
+            if (q >= W) break;
+            words_o[(size_t)q * stride_o + i] = limb[q];
+        }
+        lsn_o[i] = lv;
+        const uint32_t p = pos[j];
+        if (p != 0xFFFFFFFFu) {
+            const size_t d = (size_t)b0 + p;
+            gid_d[d] = (uint32_t)limb[W];
+#pragma unroll
+            for (int q = 0; q < kPackMaxWords; ++q) {
+                if (q >= W) break;
+                words_d[(size_t)q * stride_d + d] = limb[q];
+            }
+            lsn_d[d] = lv;
+        }
+    }
+}
+
 }  // namespace
 
 size_t packed_scratch_bytes(size_t n)
 {
     const size_t nblocks = (n + kPkTile - 1) / kPkTile;
-    return 256 * nblocks * sizeof(uint32_t) + scan_scratch_bytes(256 * nblocks) + 1024;
+    const size_t ud = (n + kUdTile - 1) / kUdTile;
+    return 256 * nblocks * sizeof(uint32_t) + scan_scratch_bytes(256 * nblocks) + 1024 +
+           (ud + 16) * sizeof(uint32_t) + scan_scratch_bytes(ud) + 8 * (kPackMaxWords + 1) + 64;
 }
 
 bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P)
@@ -297,13 +452,12 @@ bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P)
     return B + I <= 64;
 }
 
-hipError_t packed_sort_rows(const PackPlan &P, size_t n, const uint32_t *gid, const uint64_t *words,
-                            const uint64_t *lsn, size_t stride, uint64_t *k0, uint64_t *k1,
-                            uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
-                            uint32_t *flags, void *scratch, size_t scratch_bytes, hipStream_t s)
+// The LSD passes of the packed keys; the sorted keys end in *kf, the other
+// key buffer is *kfree.
+static hipError_t packed_passes(const PackPlan &P, size_t n, const uint32_t *gid,
+                                const uint64_t *words, size_t stride, uint64_t *k0, uint64_t *k1,
+                                void *scratch, hipStream_t s, uint64_t **kf, uint64_t **kfree)
 {
-    if (n == 0) return hipSuccess;
-    if (scratch_bytes < packed_scratch_bytes(n)) return hipErrorInvalidValue;
     const uint32_t nblocks = (uint32_t)((n + kPkTile - 1) / kPkTile);
     uint32_t *counts = (uint32_t *)scratch;
     uint32_t *scan_tmp = counts + (size_t)256 * nblocks;
@@ -319,9 +473,66 @@ hipError_t packed_sort_rows(const PackPlan &P, size_t n, const uint32_t *gid, co
         e = hipGetLastError();
         std::swap(k0, k1);
     }
+    *kf = k0;
+    *kfree = k1;
+    return e;
+}
+
+hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, const uint64_t *words,
+                              const uint64_t *lsn, size_t stride, uint64_t *k0, uint64_t *k1,
+                              uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
+                              uint32_t *gid_d, uint64_t *words_d, size_t stride_d,
+                              uint64_t **lsn_d, uint32_t *d_count, void *scratch,
+                              size_t scratch_bytes, hipStream_t s)
+{
+    *lsn_d = nullptr;
+    if (n == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
+    if (scratch_bytes < packed_scratch_bytes(n)) return hipErrorInvalidValue;
+    uint64_t *kf, *kfree;
+    hipError_t e = packed_passes(P, n, gid, words, stride, k0, k1, scratch, s, &kf, &kfree);
+    if (e != hipSuccess) return e;
+    // scratch after the passes' counters: block counts, their scan, row 0
+    const uint32_t nblocks = (uint32_t)((n + kPkTile - 1) / kPkTile);
+    uint8_t *sp = (uint8_t *)scratch + 256 * (size_t)nblocks * sizeof(uint32_t) +
+                  scan_scratch_bytes(256 * (size_t)nblocks) + 1024;
+    const uint32_t ud = (uint32_t)((n + kUdTile - 1) / kUdTile);
+    uint32_t *bc = (uint32_t *)sp;
+    uint32_t *btmp = bc + ud + 16;
+    uint64_t *r0 = (uint64_t *)(((uintptr_t)((uint8_t *)btmp + scan_scratch_bytes(ud)) + 15) & ~(uintptr_t)15);
+    k_pk_row0<<<1, 64, 0, s>>>(P.W, gid, words, stride, r0);
+    k_pk_bcount<<<ud, kUdThreads, 0, s>>>(n, kf, P.I, bc);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = scan_exclusive_u32(bc, ud, btmp, s);
+    if (e != hipSuccess) return e;
+#define HSC_UNPACK_DD(WT_)                                                                          \
+    k_pk_unpack_dd<WT_><<<ud, kUdThreads, 0, s>>>(P, n, kf, r0, lsn, gid_o, words_o, lsn_o,       \
+                                                   stride_o, bc, gid_d, words_d, kfree, stride_d,  \
+                                                   d_count)
+    if (P.W == 1)
+        HSC_UNPACK_DD(1);
+    else if (P.W == 2)
+        HSC_UNPACK_DD(2);
+    else if (P.W == 3)
+        HSC_UNPACK_DD(3);
+    else
+        HSC_UNPACK_DD(0);
+#undef HSC_UNPACK_DD
+    *lsn_d = kfree;
+    return hipGetLastError();
+}
+
+hipError_t packed_sort_rows(const PackPlan &P, size_t n, const uint32_t *gid, const uint64_t *words,
+                            const uint64_t *lsn, size_t stride, uint64_t *k0, uint64_t *k1,
+                            uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
+                            uint32_t *flags, void *scratch, size_t scratch_bytes, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    if (scratch_bytes < packed_scratch_bytes(n)) return hipErrorInvalidValue;
+    uint64_t *kf, *kfree;
+    hipError_t e = packed_passes(P, n, gid, words, stride, k0, k1, scratch, s, &kf, &kfree);
     if (e != hipSuccess) return e;
     const unsigned g = (unsigned)((n + kUnpackThreads - 1) / kUnpackThreads);
-#define HSC_UNPACK(WT_) k_pk_unpack<WT_><<<g, kUnpackThreads, 0, s>>>(P, n, k0, gid, words, lsn, stride, \
+#define HSC_UNPACK(WT_) k_pk_unpack<WT_><<<g, kUnpackThreads, 0, s>>>(P, n, kf, gid, words, lsn, stride, \
                                                                     gid_o, words_o, lsn_o, stride_o, flags)
     if (P.W == 1)
         HSC_UNPACK(1);

@@ -163,6 +163,16 @@ hipError_t packed_sort_rows(const PackPlan &P, size_t n, const uint32_t *gid, co
                             const uint64_t *lsn, size_t stride, uint64_t *k0, uint64_t *k1,
                             uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
                             uint32_t *flags, void *scratch, size_t scratch_bytes, hipStream_t s);
+// the same sort with the dedupe fused into the unpack: every version to
+// (gid_o, words_o, lsn_o), the distinct rows to (gid_d, words_d) -- which may
+// be the input gid / words -- and to *lsn_d = whichever of k0 / k1 the sorted
+// keys did not end in; d_count[0] = distinct rows
+hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, const uint64_t *words,
+                              const uint64_t *lsn, size_t stride, uint64_t *k0, uint64_t *k1,
+                              uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
+                              uint32_t *gid_d, uint64_t *words_d, size_t stride_d,
+                              uint64_t **lsn_d, uint32_t *d_count, void *scratch,
+                              size_t scratch_bytes, hipStream_t s);
 size_t scan_scratch_bytes(size_t n);
 hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, int ngroups,
                            uint64_t *tmax, const uint32_t *group_table,

@@ -327,100 +327,6 @@ __device__ __forceinline__ void narrow_probe_ranges(const NarrowView &nv, const 
     }
 }
 
-// The small-batch form of narrow_probe_ranges (window levels all read from
-// memory): the range maximum is taken during the descent instead of a second
-// walk up the max tree.  At level l the entries strictly between the lo and
-// hi paths (#entries with last key < lo + 1 .. #entries with last key <= hi;
-// at level 0 the rows [#< lo, #<= hi)) lie wholly inside the range (keys are
-// distinct and sorted); those in the two blocks the paths read are checked at
-// that level -- their max-tree entries load together with the key entries --
-// and the rest lay inside an entry checked one level up.  So a range costs one
-// dependent load round per level, where the walk up cost up to one more per
-// level (the per-call latency of a lone bdb_osql_serial_check).
-template <bool kHost>
-__device__ __forceinline__ void narrow_probe_ranges_td(const NarrowView &nv, const ProbeView &p,
-                                                       uint8_t *verdict, uint32_t wave0,
-                                                       uint32_t wstride)
-{
-    const int lane = threadIdx.x & 63;
-    const int sub = lane >> 4, l16 = lane & 15;
-    const size_t ks = p.n;
-    for (uint32_t wbase = wave0; wbase < p.n; wbase += wstride) {
-        const uint32_t base = wbase + sub * kNP;
-        uint64_t mlo = kSat, mhi = 0, msnap = 0;
-        uint32_t mtxn = 0;
-        bool mlive = false;
-        {
-            const uint32_t q = base + l16;
-            if (l16 < kNP && q < p.n) {
-                const uint32_t g = p.gid[q];
-                msnap = p.snap[q];
-                mtxn = p.txn[q];
-                uint64_t v;
-                bool rem;
-                mlo = rel_diff(nv.W, nv.lw, nv.tz, g, p.lo + q, ks, nv.base[0], nv.base + 1, 1,
-                               kSat, v, rem)
-                          ? (v >= kSat ? kSat : v + (rem ? 1 : 0))
-                          : 0;
-                mlive = rel_diff(nv.W, nv.lw, nv.tz, g, p.hi + q, ks, nv.base[0], nv.base + 1, 1,
-                                 kSat, v, rem);
-                mhi = mlive ? v : 0;
-            }
-        }
-        uint64_t x[2 * kNP], snap[kNP];
-        uint32_t txn[kNP];
-        bool live[kNP], found[kNP];
-#pragma unroll
-        for (int k = 0; k < kNP; ++k) {
-            const int src = (lane & 48) + k;
-            x[2 * k] = __shfl(mlo, src, 64);
-            x[2 * k + 1] = __shfl(mhi, src, 64);
-            snap[k] = __shfl(msnap, src, 64);
-            txn[k] = __shfl(mtxn, src, 64);
-            live[k] = __shfl((int)mlive, src, 64) != 0 && x[2 * k] <= x[2 * k + 1];
-            found[k] = false;
-        }
-        uint32_t c[2 * kNP];
-#pragma unroll
-        for (int j = 0; j < 2 * kNP; ++j) c[j] = 0;
-        for (int l = nv.levels - 1; l >= 0; --l) {
-            const uint64_t *kv = nv.keys + nv.off[l], *mv = nv.maxs + nv.off[l];
-            uint64_t e[2 * kNP], m[2 * kNP];
-#pragma unroll
-            for (int j = 0; j < 2 * kNP; ++j) {
-                const size_t i = 16 * (size_t)c[j] + l16;
-                const int k = j >> 1;
-                // the hi path's max block only where it is not the lo path's
-                const bool want = live[k] && !found[k] && (!(j & 1) || c[j] != c[j - 1]);
-                e[j] = kv[i];
-                m[j] = want ? mv[i] : 0;
-            }
-            uint32_t cn[2 * kNP];
-#pragma unroll
-            for (int j = 0; j < 2 * kNP; ++j) {
-                const bool below = (j & 1) ? e[j] <= x[j] : e[j] < x[j];
-                const uint32_t bm = (uint32_t)(__ballot(below) >> (16 * sub)) & 0xFFFFu;
-                cn[j] = 16 * c[j] + __popc(bm);
-            }
-#pragma unroll
-            for (int k = 0; k < kNP; ++k) {
-                const uint32_t a = cn[2 * k] + (l ? 1u : 0u), b = cn[2 * k + 1];  // inside: [a, b)
-                const uint32_t il = 16 * c[2 * k] + l16, ih = 16 * c[2 * k + 1] + l16;
-                const bool hit = (il >= a && il < b && m[2 * k] > snap[k]) ||
-                                 (ih >= a && ih < b && m[2 * k + 1] > snap[k]);
-                found[k] |= ((uint32_t)(__ballot(hit) >> (16 * sub)) & 0xFFFFu) != 0;
-            }
-#pragma unroll
-            for (int j = 0; j < 2 * kNP; ++j) c[j] = cn[j];
-        }
-        if (l16 == 0) {
-#pragma unroll
-            for (int k = 0; k < kNP; ++k)
-                if (found[k]) mark_verdict<kHost>(verdict + txn[k]);
-        }
-    }
-}
-
 // table locks q = first, first + stride, ...: any write to a locked table
 // after the snapshot
 template <bool kHost = false>
@@ -469,7 +375,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, D
 {
     const uint32_t groups = gridDim.x * (kSmallThreads / 16);
     const uint32_t wave0 = (blockIdx.x * (kSmallThreads / 16) + ((threadIdx.x >> 6) << 2)) * kNP;
-    narrow_probe_ranges_td<true>(nv, p, verdict, wave0, groups * kNP);
+    narrow_probe_ranges<true>(nv, p, verdict, nullptr, 0, nv.levels, wave0, groups * kNP);
     const uint32_t tid = blockIdx.x * kSmallThreads + threadIdx.x, nth = gridDim.x * kSmallThreads;
     if (d.n || d2.n)  // the live run and a frozen one (background fold)
         for (uint32_t q = tid; q < p.n; q += nth)

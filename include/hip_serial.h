@@ -416,7 +416,7 @@ void hsc_collector_destroy(hsc_collector *col);
 int hsc_collector_check(hsc_collector *col, void *ranges, unsigned int *file,
                         unsigned int *offset, int regop_only);
 int hsc_collector_get_stats(hsc_collector *col, hsc_collector_stats *out);
-/* Batches allowed on the device at once (1..4; default 1, or
+/* Batches allowed on the device at once (1..4; default 2, or
  * HSC_COLLECT_INFLIGHT at creation): with 2, the next leader launches while
  * the previous batch's kernel runs.  Full checks are marshalled by their own
  * callers before they queue (HSC_PREMARSHAL=0 at creation: by the leader). */

@@ -4,7 +4,9 @@ version in stable (gid, key words) order and the newest version per key,
 read back through hsc_window_export.  Cases cover one and several words,
 several groups, varying bits scattered over the words, heavy duplication,
 unsorted LSNs, block-boundary row counts and a window whose varying bits
-plus row index do not fit 64 bits (the packed path declines it)."""
+plus row index do not fit 64 bits (the packed path declines it); the packed
+sort runs with its dedupe fused into the unpack and with the separate
+flag / scan / compaction dedupe."""
 import os
 
 import numpy as np
@@ -51,7 +53,11 @@ def _case(rng, n, W, ngroups, pattern):
 
 
 def _build(gid, words, lsn, ngroups, packed):
+    # packed: "dd" the packed sort with the dedupe fused into its unpack
+    # (default), "flags" the packed sort + the flag/scan/compact dedupe,
+    # False the whole-row radix sort
     os.environ["HSC_PACKED_SORT"] = "1" if packed else "0"
+    os.environ["HSC_PK_DD"] = "0" if packed == "flags" else "1"
     try:
         v = Validator(0)
         W = words.shape[0]
@@ -68,6 +74,7 @@ def _build(gid, words, lsn, ngroups, packed):
         return out
     finally:
         os.environ.pop("HSC_PACKED_SORT", None)
+        os.environ.pop("HSC_PK_DD", None)
 
 
 CASES = [
@@ -83,7 +90,7 @@ def test_build_rows_match_numpy(n, W, ngroups, pattern):
     rng = np.random.default_rng(n * 31 + W * 7 + ngroups)
     gid, words, lsn = _case(rng, n, W, ngroups, pattern)
     want_all, want_u = _reference(gid, words, lsn)
-    for packed in (True, False):
+    for packed in ("dd", "flags", False):
         got_all, got_u = _build(gid, words, lsn, ngroups, packed)
         for got, want in ((got_all, want_all), (got_u, want_u)):
             np.testing.assert_array_equal(got[0], want[0])
