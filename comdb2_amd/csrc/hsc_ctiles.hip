@@ -218,7 +218,7 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
     const uint32_t c0 = g * work.chunk, c1 = min(p.n, c0 + work.chunk);
     // every probe load of the chunk first (read-once inputs: non-temporal)
     uint64_t lo[kCLocP][WG], hi[kCLocP][WG], snap[kCLocP];
-    uint32_t gg[kCLocP], tx[kCLocP];
+    uint32_t gg[kCLocP];
 #pragma unroll
     for (int k = 0; k < kCLocP; ++k) {
         const uint32_t q0 = c0 + threadIdx.x + kCLocThreads * k;
@@ -226,7 +226,6 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
         const bool v = p.n != 0;
         gg[k] = v ? __builtin_nontemporal_load(p.gid + q) : 0;
         snap[k] = v ? __builtin_nontemporal_load(p.snap + q) : 0;
-        tx[k] = v ? __builtin_nontemporal_load(p.txn + q) : 0;
 #pragma unroll
         for (int j = 0; j < WG; ++j) {
             const bool u = v && j < ct.WC;
@@ -244,14 +243,10 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
     __syncthreads();
     uint64_t KA[kCLocP][WG], KB[kCLocP][WG], RT[kCLocP];
     uint2 SL[kCLocP];
-    // tiles strictly inside a range [DX, DY]: their range maxima are loaded
-    // after the loop (no global round trip inside it) and compared at the end
-    uint32_t DX[kCLocP], DY[kCLocP];
 #pragma unroll
     for (int k = 0; k < kCLocP; ++k) {
         const uint32_t q = c0 + threadIdx.x + kCLocThreads * k;
         SL[k] = make_uint2(kNoSlot, kNoSlot);
-        DX[k] = 1, DY[k] = 0;
         if (q >= c1) continue;
         uint64_t a_[WG], b_[WG];
         compose<WG>(gg[k], ct.gb, lo[k], a_);
@@ -262,9 +257,9 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
             const uint32_t cb = ct_count<WG, true>(lf, nt, T, ct.trad_m, shift, ct.base0, b_);
             if (cb > 0) {
                 const uint32_t a = ca ? ca - 1 : 0, bt = cb - 1;
-                const uint32_t txn = tx[k];
+                const uint32_t txn = p.txn[q];
                 // tiles strictly between the end tiles lie inside the range
-                if (bt > a + 1) DX[k] = a + 1, DY[k] = bt - 1;
+                if (bt > a + 1 && tiles_max(wt, a + 1, bt - 1) > snap[k]) flags[txn] = 1;
                 sl.x = a << 12 | atomicAdd(&hist[a], 1u);
                 bool point = true;
 #pragma unroll
@@ -299,18 +294,10 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
         }
         if constexpr (!kSort) ct.slot[q] = sl;
     }
-    uint64_t dmax[kCLocP];
-#pragma unroll
-    for (int k = 0; k < kCLocP; ++k) dmax[k] = DX[k] <= DY[k] ? tiles_max(wt, DX[k], DY[k]) : 0;
     // table locks: any write to a locked table after the snapshot
     for (uint32_t q = g * kCLocThreads + threadIdx.x; q < p.n_lock; q += work.G * kCLocThreads) {
         const uint32_t t = p.lock_table[q];
         if (t < wt.ntables && wt.table_max[t] > p.lock_snap[q]) flags[p.lock_txn[q]] = 1;
-    }
-    if constexpr (!kSort) {
-#pragma unroll
-        for (int k = 0; k < kCLocP; ++k)
-            if (DX[k] <= DY[k] && dmax[k] > snap[k]) flags[tx[k]] = 1;
     }
     __syncthreads();
     if constexpr (!kSort) {
@@ -366,10 +353,6 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
                 r2[1] = u64x2{b[2], RT[k] | (uint64_t)kCTail << 62};
             }
         }
-        // the inner tiles' maxima, loaded before the scan, compared now
-#pragma unroll
-        for (int k = 0; k < kCLocP; ++k)
-            if (DX[k] <= DY[k] && dmax[k] > snap[k]) flags[tx[k]] = 1;
     }
 }
 
