@@ -631,7 +631,7 @@ __device__ __forceinline__ void join_item_s(const ProbeWork &work, const CTiles 
     join_search<WG>(work, ct, flags, kw, rank, b16, b128, B, kind, pl, ph0, ph1);
 }
 
-// Chunk-sorted records, 512 threads, key words 0 and 1 staged (word 2 of a
+// (HSC_CJOIN2=1, off: measured slower) Chunk-sorted records, 512 threads, key words 0 and 1 staged (word 2 of a
 // 3-word key read from the window on a two-word tie): 49 KiB of LDS, so three
 // workgroups fit a CU where the 1024-thread join's 64 KiB fit two -- more
 // tiles in flight (config 3: 1475 tiles over 768 slots instead of 512), and
@@ -970,7 +970,9 @@ hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_i
     const uint32_t blocks =
         ct_tile_blocks(work.local_items != 0, ct.ntiles) + (extra < 512 ? extra : 512);
     const bool srt = work.local_items != 0;
-    const bool j2 = !getenv("HSC_CJOIN2") || atoi(getenv("HSC_CJOIN2")) != 0;
+    // the 512-thread join (HSC_CJOIN2=1): measured slower on config 3 (two
+    // streams 78.2 -> 80.4 us per batch, one stream 108 -> 112 us; r03h)
+    const bool j2 = getenv("HSC_CJOIN2") && atoi(getenv("HSC_CJOIN2")) != 0;
     if (srt && j2 && !kCJoinXcd) {  // 512 threads, words 0-1 staged
         const int wl = ct.WG < 2 ? ct.WG : 2;
         const size_t lds2 = 8 * (size_t)wl * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +

@@ -219,7 +219,14 @@ struct hsc_ctx {
     std::vector<uint8_t> app_keys;   // their key bytes (klen of the group each)
     std::vector<uint64_t> app_koff, app_lsn;
     bool app_tmax = false;           // table maxima changed since the last upload
-    HBuf h_app;                      // pinned staging of appended rows / table maxima
+    // pinned staging of appended rows / table maxima: a ring of two, each
+    // reused only after the copies that read it ran (its event), so an append
+    // returns without waiting for its upload and delta merge
+    HBuf h_appq[2];
+    hipEvent_t app_ev[2] = {};
+    int app_i = 0;
+    HBuf *h_app = nullptr;          // the buffer of the append being staged
+    hipEvent_t app_last = nullptr;  // recorded behind the last append's device work
     ProbeView raw_probe{};           // the batch being probed, untransformed (delta probe)
     // background fold: once the live run holds fold_rows rows it
     // is frozen, and a shadow context rebuilds the main window from the main
@@ -436,7 +443,33 @@ static hipError_t wait_lanes(hsc_ctx *c)
     return hipSuccess;
 }
 
-static int fail(hsc_ctx *c, int code, const char *what, hipError_t e = hipSuccess)
+static int fail(hsc_ctx *c, int code, const char *what, hipError_t e = hipSuccess);
+
+// the next append staging buffer of the ring (waits only if the copies that
+// read it two appends ago have not run yet)
+static int app_stage(hsc_ctx *c, size_t bytes)
+{
+    const int i = c->app_i;
+    if (c->app_ev[i] && hipEventSynchronize(c->app_ev[i]) != hipSuccess)
+        return fail(c, HSC_EDEVICE, "append staging event");
+    if (c->h_appq[i].ensure(bytes, true)) return fail(c, HSC_ENOMEM, "append staging");
+    c->h_app = &c->h_appq[i];
+    return HSC_OK;
+}
+
+// the staged buffer's copies (and the work behind them) are on stream s
+static int app_staged(hsc_ctx *c, hipStream_t s)
+{
+    const int i = c->app_i;
+    if (!c->app_ev[i] && hipEventCreateWithFlags(&c->app_ev[i], hipEventDisableTiming) != hipSuccess)
+        return fail(c, HSC_EDEVICE, "append event");
+    if (hipEventRecord(c->app_ev[i], s) != hipSuccess) return fail(c, HSC_EDEVICE, "append event");
+    c->app_last = c->app_ev[i];
+    c->app_i ^= 1;
+    return HSC_OK;
+}
+
+static int fail(hsc_ctx *c, int code, const char *what, hipError_t e)
 {
     char buf[256];
     if (e != hipSuccess)
@@ -1152,10 +1185,9 @@ static int stage_appends(hsc_ctx *c, int W, size_t *k_out)
             if (rw[a * W + j] != rw[b * W + j]) return rw[a * W + j] < rw[b * W + j];
         return false;
     });
-    if (c->h_app.ensure(k * (4 + 8 * (size_t)W + 8) + 16, true))
-        return fail(c, HSC_ENOMEM, "append staging");
-    uint32_t *g = c->h_app.as<uint32_t>();
-    uint64_t *wd = (uint64_t *)(c->h_app.as<uint8_t>() + ((4 * k + 15) & ~(size_t)15));
+    HIPCHK_RC(c, app_stage(c, k * (4 + 8 * (size_t)W + 8) + 16));
+    uint32_t *g = c->h_app->as<uint32_t>();
+    uint64_t *wd = (uint64_t *)(c->h_app->as<uint8_t>() + ((4 * k + 15) & ~(size_t)15));
     uint64_t *ls = wd + (size_t)W * k;
     for (size_t i = 0; i < k; ++i) {
         const uint32_t r = ord[i];
@@ -1212,11 +1244,10 @@ static int flush_appends(hsc_ctx *c)
     if (c->app_tmax) {
         const int nt = (int)c->table_names.size();
         HIPCHK(c, c->d_table_max.ensure(8 * (size_t)std::max(nt, 1)));
-        if (c->h_app.ensure(8 * (size_t)std::max(nt, 1), true)) return fail(c, HSC_ENOMEM, "staging");
-        memcpy(c->h_app.p, c->h_table_max.data(), 8 * (size_t)nt);
-        if (nt) HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, c->h_app.p, 8 * (size_t)nt, hipMemcpyHostToDevice, s));
-        // the next staging must not overwrite h_app before the copy ran
-        HIPCHK(c, hipStreamSynchronize(s));
+        HIPCHK_RC(c, app_stage(c, 8 * (size_t)std::max(nt, 1)));
+        memcpy(c->h_app->p, c->h_table_max.data(), 8 * (size_t)nt);
+        if (nt) HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, c->h_app->p, 8 * (size_t)nt, hipMemcpyHostToDevice, s));
+        HIPCHK_RC(c, app_staged(c, s));  // the ring keeps the buffer until the copy ran
         c->app_tmax = false;
     }
     if (!k) return HSC_OK;
@@ -1226,7 +1257,7 @@ static int flush_appends(hsc_ctx *c)
     HIPCHK(c, c->d_agid.ensure(4 * k));
     HIPCHK(c, c->d_awords.ensure(8 * (size_t)W * k));
     HIPCHK(c, c->d_alsn.ensure(8 * k));
-    const uint8_t *hb = c->h_app.as<uint8_t>();
+    const uint8_t *hb = c->h_app->as<uint8_t>();
     const size_t woff = (4 * k + 15) & ~(size_t)15;
     HIPCHK(c, hipMemcpyAsync(c->d_agid.p, hb, 4 * k, hipMemcpyHostToDevice, s));
     HIPCHK(c, hipMemcpyAsync(c->d_awords.p, hb + woff, 8 * (size_t)W * k, hipMemcpyHostToDevice, s));
@@ -1255,8 +1286,9 @@ static int flush_appends(hsc_ctx *c)
     const int o = c->dcur ^ 1;
     HIPCHK(c, delta_merge(d, a, c->d_dgid[o].as<uint32_t>(), c->d_dwords[o].as<uint64_t>(),
                           c->d_dlsn[o].as<uint64_t>(), c->dcap, c->d_dbmax.as<uint64_t>(), s));
-    // h_app is read by the copies above: finish them before the next staging
-    HIPCHK(c, hipStreamSynchronize(s));
+    // no wait: the ring keeps h_app until its copies ran, and every later use
+    // of the run is on this stream (hsc_set_stream orders a new stream after it)
+    HIPCHK_RC(c, app_staged(c, s));
     c->dcur = o;
     c->dn += k;
     c->app_gid.clear(), c->app_keys.clear(), c->app_koff.clear(), c->app_lsn.clear();
@@ -1318,7 +1350,7 @@ static int merge_delta(hsc_ctx *c)
                                      8 * nd, hipMemcpyDeviceToDevice, s));
     }
     if (k) {
-        const uint8_t *hb = c->h_app.as<uint8_t>();
+        const uint8_t *hb = c->h_app->as<uint8_t>();
         const size_t woff = (4 * k + 15) & ~(size_t)15;
         HIPCHK(c, hipMemcpyAsync(g.as<uint32_t>() + na + nd, hb, 4 * k, hipMemcpyHostToDevice, s));
         for (int j = 0; j < W; ++j)
@@ -2963,7 +2995,9 @@ void hsc_ctx_destroy(hsc_ctx *c)
     for (DBuf *b : {&c->d_dgid[0], &c->d_dgid[1], &c->d_dwords[0], &c->d_dwords[1], &c->d_dlsn[0],
                     &c->d_dlsn[1], &c->d_dbmax, &c->d_agid, &c->d_awords, &c->d_alsn})
         b->release();
-    c->h_app.release();
+    for (HBuf &b : c->h_appq) b.release();
+    for (hipEvent_t &e : c->app_ev)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
     for (DBuf &b : c->co_dev) b.release();
     for (DBuf *b : {&c->e_span, &c->e_cnt, &c->e_txn, &c->e_lsn, &c->e_txn2, &c->e_lsn2, &c->e_gid,
                     &c->e_scratch, &c->e_flags, &c->e_after})
@@ -2983,7 +3017,12 @@ int hsc_set_stream(hsc_ctx *c, void *st)
 {
     if (!c) return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    c->stream = st ? (hipStream_t)st : c->own_stream;
+    std::lock_guard<std::mutex> g(c->mu);
+    hipStream_t ns = st ? (hipStream_t)st : c->own_stream;
+    // appends return before their upload and merge ran: the new stream waits
+    if (c->app_last && ns != c->stream && hipStreamWaitEvent(ns, c->app_last, 0) != hipSuccess)
+        return fail(c, HSC_EDEVICE, "set_stream: order after the appends");
+    c->stream = ns;
     return HSC_OK;
 }
 
