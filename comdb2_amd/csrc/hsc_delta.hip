@@ -16,53 +16,56 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 namespace hsc {
 
 namespace {
 
 // out = merge of the delta (d.n rows) and the appended rows a (a.n rows,
-// sorted), stable: equal keys keep delta rows first.  One thread per row.
+// sorted), stable: equal keys keep delta rows first.  One thread per output
+// row: its co-rank (how many delta rows precede it, a binary search on its
+// merge-path diagonal) names the source row, so a wave writes 64 consecutive
+// rows and takes their 64-row LSN maximum with it (no second pass).  Block 0
+// also copies the table maxima staged with the rows (nt of them) into place.
 __global__ void k_delta_merge(DeltaView d, DeltaView a, uint32_t *ogid, uint64_t *owords,
-                              uint64_t *olsn, size_t ostride)
+                              uint64_t *olsn, size_t ostride, uint64_t *bmax,
+                              const uint64_t *tmax_src, uint64_t *tmax_dst, uint32_t nt)
 {
+    if (blockIdx.x == 0)
+        for (uint32_t t = threadIdx.x; t < nt; t += blockDim.x) tmax_dst[t] = tmax_src[t];
+    const uint32_t n = d.n + a.n;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t pos;
-    const DeltaView *src;
-    uint32_t r;
-    if (i < d.n) {  // delta row i: + appended rows strictly below it
-        uint32_t lo = 0, hi = a.n;
+    uint64_t lv = 0;
+    if (i < n) {
+        // x = delta rows among outputs [0, i): the least x with d[x] > a[i - 1 - x]
+        uint32_t lo = i > a.n ? i - a.n : 0, hi = min(i, d.n);
         while (lo < hi) {
             const uint32_t mid = (lo + hi) >> 1;
-            // a[mid] < d[i] <=> d[i] > a[mid]
-            if (row_cmp(d.gid, d.words, d.stride, d.W, i, a.gid[mid], a.words + mid, a.stride) > 0)
+            const uint32_t y = i - 1 - mid;
+            // d[mid] <= a[y]: delta row mid precedes appended row y (ties: delta first)
+            if (row_cmp(d.gid, d.words, d.stride, d.W, mid, a.gid[y], a.words + y, a.stride) <= 0)
                 lo = mid + 1;
             else
                 hi = mid;
         }
-        pos = i + lo;
-        src = &d;
-        r = i;
-    } else if (i < d.n + a.n) {  // appended row j: + delta rows <= it
-        const uint32_t j = i - d.n;
-        pos = j + delta_count(d, a.gid[j], a.words + j, a.stride, false);
-        src = &a;
-        r = j;
-    } else {
-        return;
+        const uint32_t x = lo, y = i - x;
+        const bool from_d = x < d.n && (y >= a.n || row_cmp(d.gid, d.words, d.stride, d.W, x, a.gid[y],
+                                                             a.words + y, a.stride) <= 0);
+        const DeltaView &src = from_d ? d : a;
+        const uint32_t r = from_d ? x : y;
+        ogid[i] = src.gid[r];
+        for (int w = 0; w < d.W; ++w) owords[(size_t)w * ostride + i] = src.words[(size_t)w * src.stride + r];
+        lv = src.lsn[r];
+        olsn[i] = lv;
     }
-    ogid[pos] = src->gid[r];
-    for (int w = 0; w < d.W; ++w) owords[(size_t)w * ostride + pos] = src->words[(size_t)w * src->stride + r];
-    olsn[pos] = src->lsn[r];
-}
-
-__global__ void k_delta_bmax(const uint64_t *lsn, uint32_t n, uint64_t *bmax)
-{
-    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-    if ((size_t)b * 64 >= n) return;
-    uint64_t m = 0;
-    const uint32_t e = min(n, (b + 1) * 64);
-    for (uint32_t i = b * 64; i < e; ++i) m = lsn[i] > m ? lsn[i] : m;
-    bmax[b] = m;
+    // rows [64 b, 64 b + 64) are one wave's (blocks start at multiples of 64)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t v = __shfl_xor(lv, o, 64);
+        lv = v > lv ? v : lv;
+    }
+    if ((threadIdx.x & 63) == 0 && i < n) bmax[i >> 6] = lv;
 }
 
 // Range probes against the delta: any row of the range's group inside
@@ -77,13 +80,13 @@ __global__ __launch_bounds__(256) void k_probe_delta(DeltaView d, ProbeView p, u
 }  // namespace
 
 hipError_t delta_merge(const DeltaView &d, const DeltaView &a, uint32_t *ogid, uint64_t *owords,
-                       uint64_t *olsn, size_t ostride, uint64_t *bmax, hipStream_t s)
+                       uint64_t *olsn, size_t ostride, uint64_t *bmax, hipStream_t s,
+                       const uint64_t *tmax_src, uint64_t *tmax_dst, uint32_t nt)
 {
     const uint32_t n = d.n + a.n;
-    if (n == 0) return hipSuccess;
-    k_delta_merge<<<(n + 255) / 256, 256, 0, s>>>(d, a, ogid, owords, olsn, ostride);
-    const uint32_t nb = (n + 63) / 64;
-    k_delta_bmax<<<(nb + 255) / 256, 256, 0, s>>>(olsn, n, bmax);
+    if (n == 0 && nt == 0) return hipSuccess;
+    k_delta_merge<<<std::max(1u, (n + 255) / 256), 256, 0, s>>>(d, a, ogid, owords, olsn, ostride,
+                                                                 bmax, tmax_src, tmax_dst, nt);
     return hipGetLastError();
 }
 
@@ -100,7 +103,7 @@ hipError_t launch_probe_delta(const DeltaView &d, const ProbeView &p, uint8_t *f
 hipError_t warm_delta()
 {
     hipFuncAttributes a;
-    return hipFuncGetAttributes(&a, (const void *)k_delta_bmax);
+    return hipFuncGetAttributes(&a, (const void *)k_probe_delta);
 }
 
 }  // namespace hsc

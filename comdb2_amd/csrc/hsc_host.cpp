@@ -1164,7 +1164,14 @@ static int build_from_host(hsc_ctx *c)
 
 // Appended rows (app_*) as a sorted SoA (gid, W words, lsn) in pinned
 // staging: returns the row count.
-static int stage_appends(hsc_ctx *c, int W, size_t *k_out)
+// Staged rows: [gid: 4k, padded to 16][words: 8Wk][lsn: 8k] then, nt > 0,
+// [table maxima: 8nt] -- one upload for an append.
+static size_t stage_bytes(size_t k, int W, int nt)
+{
+    return ((4 * k + 15) & ~(size_t)15) + 8 * (size_t)W * k + 8 * k + 8 * (size_t)nt;
+}
+
+static int stage_appends(hsc_ctx *c, int W, size_t *k_out, int nt = 0)
 {
     const size_t k = c->app_gid.size();
     *k_out = k;
@@ -1185,7 +1192,7 @@ static int stage_appends(hsc_ctx *c, int W, size_t *k_out)
             if (rw[a * W + j] != rw[b * W + j]) return rw[a * W + j] < rw[b * W + j];
         return false;
     });
-    HIPCHK_RC(c, app_stage(c, k * (4 + 8 * (size_t)W + 8) + 16));
+    HIPCHK_RC(c, app_stage(c, stage_bytes(k, W, nt) + 16));
     uint32_t *g = c->h_app->as<uint32_t>();
     uint64_t *wd = (uint64_t *)(c->h_app->as<uint8_t>() + ((4 * k + 15) & ~(size_t)15));
     uint64_t *ls = wd + (size_t)W * k;
@@ -1195,6 +1202,7 @@ static int stage_appends(hsc_ctx *c, int W, size_t *k_out)
         for (int j = 0; j < W; ++j) wd[(size_t)j * k + i] = rw[(size_t)r * W + j];
         ls[i] = c->app_lsn[r];
     }
+    if (nt) memcpy(ls + k, c->h_table_max.data(), 8 * (size_t)nt);
     return HSC_OK;
 }
 
@@ -1241,27 +1249,25 @@ static int flush_appends(hsc_ctx *c)
     }
     if (!k && !c->app_tmax) return HSC_OK;
     HIPCHK(c, wait_lanes(c));  // probes in flight on other streams keep reading the old run
-    if (c->app_tmax) {
-        const int nt = (int)c->table_names.size();
-        HIPCHK(c, c->d_table_max.ensure(8 * (size_t)std::max(nt, 1)));
+    const int nt = c->app_tmax ? (int)c->table_names.size() : 0;
+    if (c->app_tmax) HIPCHK(c, c->d_table_max.ensure(8 * (size_t)std::max(nt, 1)));
+    if (!k) {  // table maxima only
         HIPCHK_RC(c, app_stage(c, 8 * (size_t)std::max(nt, 1)));
         memcpy(c->h_app->p, c->h_table_max.data(), 8 * (size_t)nt);
         if (nt) HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, c->h_app->p, 8 * (size_t)nt, hipMemcpyHostToDevice, s));
         HIPCHK_RC(c, app_staged(c, s));  // the ring keeps the buffer until the copy ran
         c->app_tmax = false;
+        return HSC_OK;
     }
-    if (!k) return HSC_OK;
     const int W = c->W;
     size_t kk = 0;
-    HIPCHK_RC(c, stage_appends(c, W, &kk));
-    HIPCHK(c, c->d_agid.ensure(4 * k));
-    HIPCHK(c, c->d_awords.ensure(8 * (size_t)W * k));
-    HIPCHK(c, c->d_alsn.ensure(8 * k));
-    const uint8_t *hb = c->h_app->as<uint8_t>();
+    HIPCHK_RC(c, stage_appends(c, W, &kk, nt));
+    // one upload: rows, then the table maxima the merge kernel copies out
     const size_t woff = (4 * k + 15) & ~(size_t)15;
-    HIPCHK(c, hipMemcpyAsync(c->d_agid.p, hb, 4 * k, hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipMemcpyAsync(c->d_awords.p, hb + woff, 8 * (size_t)W * k, hipMemcpyHostToDevice, s));
-    HIPCHK(c, hipMemcpyAsync(c->d_alsn.p, hb + woff + 8 * (size_t)W * k, 8 * k, hipMemcpyHostToDevice, s));
+    const size_t sb = stage_bytes(k, W, nt);
+    HIPCHK(c, c->d_agid.ensure(sb));
+    HIPCHK(c, hipMemcpyAsync(c->d_agid.p, c->h_app->p, sb, hipMemcpyHostToDevice, s));
+    uint8_t *db = c->d_agid.as<uint8_t>();
     // both run buffers at full size for the window's words: merges never
     // reallocate a run holding rows (a wider key schedules a rebuild above)
     const size_t wbytes = 8 * (size_t)W * kDeltaCap;
@@ -1276,16 +1282,19 @@ static int flush_appends(hsc_ctx *c)
         HIPCHK(c, c->d_dbmax.ensure(8 * (size_t)(kDeltaCap / 64 + 1)));
     }
     DeltaView a{};
-    a.gid = c->d_agid.as<uint32_t>();
-    a.words = c->d_awords.as<uint64_t>();
-    a.lsn = c->d_alsn.as<uint64_t>();
+    a.gid = (const uint32_t *)db;
+    a.words = (const uint64_t *)(db + woff);
+    a.lsn = (const uint64_t *)(db + woff + 8 * (size_t)W * k);
     a.stride = k;
     a.n = (uint32_t)k;
     a.W = W;
     const DeltaView d = delta_view(c);
     const int o = c->dcur ^ 1;
     HIPCHK(c, delta_merge(d, a, c->d_dgid[o].as<uint32_t>(), c->d_dwords[o].as<uint64_t>(),
-                          c->d_dlsn[o].as<uint64_t>(), c->dcap, c->d_dbmax.as<uint64_t>(), s));
+                          c->d_dlsn[o].as<uint64_t>(), c->dcap, c->d_dbmax.as<uint64_t>(), s,
+                          nt ? a.lsn + k : nullptr, nt ? c->d_table_max.as<uint64_t>() : nullptr,
+                          (uint32_t)nt));
+    if (nt) c->app_tmax = false;
     // no wait: the ring keeps h_app until its copies ran, and every later use
     // of the run is on this stream (hsc_set_stream orders a new stream after it)
     HIPCHK_RC(c, app_staged(c, s));
