@@ -1499,33 +1499,6 @@ hipError_t launch_scatter_t(const ProbeView &p, const ProbeWork &work, const Nar
 // bucket always has kTileCap slots; the count, a scalar load, masks them
 // later), then the tile's rows, so both round trips overlap (vector loads
 // retire in order: a count read between them would wait for the rows).
-// The two Eytzinger walks of a record (#keys < lo and #keys <= hi, as leaf
-// slots) in one pass: while both sit on the same node one LDS read serves
-// both, and a point (lo == hi) reads nothing past the node where they part --
-// below it every key of the lo walk's subtree is < lo and every key of the hi
-// walk's is > hi (tile keys are distinct; the padding repeats 0xFFFFFFFF, and
-// the callers clamp the counts to the tile's rows).
-__device__ __forceinline__ void eyt_walks(const uint32_t *keys, uint32_t lo, uint32_t hi,
-                                          uint32_t &ja_out, uint32_t &jb_out)
-{
-    uint32_t ja = 1, jb = 1;
-    const bool point = lo == hi;
-#pragma unroll
-    for (int d = 0; d < kTLog2; ++d) {
-        const bool same = ja == jb;
-        uint32_t ka = 0, kb = ~0u;
-        if (same || !point) ka = keys[ja];
-        if (same)
-            kb = ka;
-        else if (!point)
-            kb = keys[jb];
-        ja = 2 * ja + (ka < lo);
-        jb = 2 * jb + (kb <= hi);
-    }
-    ja_out = ja;
-    jb_out = jb;
-}
-
 template <bool kTile>
 __device__ __forceinline__ void join_t_item(const ProbeWork &work, const NarrowTiles &nt,
                                             uint32_t n, uint32_t xi, uint8_t *verdict,
@@ -1582,8 +1555,13 @@ __device__ __forceinline__ void join_t_item(const ProbeWork &work, const NarrowT
         // pa = #keys < lo, pb = #keys <= hi: root-to-leaf walks of the
         // Eytzinger tree, both reads of a level in flight together; rows
         // past tn are padding (0xFFFFFFFF, never below lo)
-        uint32_t ja, jb;
-        eyt_walks(keys, lo, hi, ja, jb);
+        uint32_t ja = 1, jb = 1;
+#pragma unroll
+        for (int d = 0; d < kTLog2; ++d) {
+            const uint32_t ka = keys[ja], kb = keys[jb];
+            ja = 2 * ja + (ka < lo);
+            jb = 2 * jb + (kb <= hi);
+        }
         const uint32_t kl = keys[0];  // the tile's last (largest) row
         const uint32_t pa = min(ja - T + (kl < lo), tn);
         const uint32_t pb = min(jb - T + (kl <= hi), tn);
@@ -1673,8 +1651,13 @@ __device__ __forceinline__ void join_s_item(const ProbeWork &work, const NarrowT
         const uint32_t j = j0 + k * kJoinThreads + threadIdx.x;
         if (j >= j1) continue;
         const uint32_t lo = rec[k].x, hi = rec[k].y, rs = rec[k].z;
-        uint32_t ja, jb;
-        eyt_walks(keys, lo, hi, ja, jb);
+        uint32_t ja = 1, jb = 1;
+#pragma unroll
+        for (int d = 0; d < kTLog2; ++d) {
+            const uint32_t ka = keys[ja], kb = keys[jb];
+            ja = 2 * ja + (ka < lo);
+            jb = 2 * jb + (kb <= hi);
+        }
         const uint32_t kl = keys[0];
         const uint32_t pa = min(ja - T + (kl < lo), tn);
         const uint32_t pb = min(jb - T + (kl <= hi), tn);
@@ -1845,8 +1828,13 @@ __global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_f(
                 const uint32_t j = j0 + k * kJoinThreads + threadIdx.x;
                 if (j >= total) continue;
                 const uint32_t lo = rec[k].x, hi = rec[k].y, r_s = rec[k].z;
-                uint32_t ja, jb;
-                eyt_walks(keys, lo, hi, ja, jb);
+                uint32_t ja = 1, jb = 1;
+#pragma unroll
+                for (int d = 0; d < kTLog2; ++d) {
+                    const uint32_t ka = keys[ja], kb = keys[jb];
+                    ja = 2 * ja + (ka < lo);
+                    jb = 2 * jb + (kb <= hi);
+                }
                 const uint32_t kl = keys[0];
                 const uint32_t pa = min(ja - T + (kl < lo), tn);
                 const uint32_t pb = min(jb - T + (kl <= hi), tn);
