@@ -205,6 +205,9 @@ def bench_commit_stream(args):
             if rca != 0:
                 raise RuntimeError(f"hsc_window_append_log -> {rca}")
     wall = time.perf_counter() - t0
+    layout = {hsc.LAYOUT_NARROW: "narrow", hsc.LAYOUT_COMPACT: "compact",
+              hsc.LAYOUT_WIDE: "wide"}.get(v.layout, str(v.layout))
+    small = v.small_stats()
     v.close()
     parity = None
     gpath = os.path.join(ROOT, "tests", "golden", "config1_replay.json")
@@ -217,6 +220,7 @@ def bench_commit_stream(args):
            "warmup": 0, "ms_per_step": native / len(tc) * 1e3, "higher_is_better": True,
            "scaling": "none", "vs_baseline": None, "dtype": "u64",
            "data": "synthetic config 1 stream (seed 0xC0FFEE01)",
+           "window_layout": layout, "small_path": small,
            "config": {"workload": f"config1: {args.n_txn_c1} txns of tests/tools/serial.c shape, "
                                   "one check per commit, passing txns appended",
                       "checks": len(tc), "not_serializable": int(sum(r != 0 for r in rcs.values())),

@@ -373,15 +373,24 @@ __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, D
                                                                 uint32_t *blocks_done,
                                                                 uint32_t *done, uint32_t seq)
 {
-    const uint32_t groups = gridDim.x * (kSmallThreads / 16);
-    const uint32_t wave0 = (blockIdx.x * (kSmallThreads / 16) + ((threadIdx.x >> 6) << 2)) * kNP;
-    narrow_probe_ranges<true>(nv, p, verdict, nullptr, 0, nv.levels, wave0, groups * kNP);
-    const uint32_t tid = blockIdx.x * kSmallThreads + threadIdx.x, nth = gridDim.x * kSmallThreads;
-    if (d.n || d2.n)  // the live run and a frozen one (background fold)
+    // with appended rows pending, the second half of the grid searches the
+    // delta runs while the first half searches the window (both dependent
+    // load chains run side by side instead of one after the other)
+    const bool split = d.n || d2.n;
+    const uint32_t half = split ? gridDim.x / 2 : gridDim.x;
+    if (blockIdx.x < half) {
+        const uint32_t groups = half * (kSmallThreads / 16);
+        const uint32_t wave0 = (blockIdx.x * (kSmallThreads / 16) + ((threadIdx.x >> 6) << 2)) * kNP;
+        narrow_probe_ranges<true>(nv, p, verdict, nullptr, 0, nv.levels, wave0, groups * kNP);
+        const uint32_t tid = blockIdx.x * kSmallThreads + threadIdx.x, nth = half * kSmallThreads;
+        narrow_probe_locks<true>(nv, p, verdict, tid, nth);
+    } else {  // the live run and a frozen one (background fold)
+        const uint32_t tid = (blockIdx.x - half) * kSmallThreads + threadIdx.x;
+        const uint32_t nth = (gridDim.x - half) * kSmallThreads;
         for (uint32_t q = tid; q < p.n; q += nth)
             if ((d.n && delta_hit(d, p, q)) || (d2.n && delta_hit(d2, p, q)))
                 mark_verdict<true>(verdict + p.txn[q]);
-    narrow_probe_locks<true>(nv, p, verdict, tid, nth);
+    }
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's verdict stores are done
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -403,8 +412,9 @@ hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const D
     const size_t per_block = (kSmallThreads / 16) * kNP;
     const size_t work = std::max<size_t>({(p.n + per_block - 1) / per_block,
                                           (p.n_lock + kSmallThreads - 1) / kSmallThreads, 1});
-    k_small_narrow<<<(unsigned)std::min<size_t>(work, 256), kSmallThreads, 0, s>>>(
-        nv, d, d2, p, verdict, blocks_done, done, seq);
+    const size_t blocks = std::min<size_t>(work, 128) * (d.n || d2.n ? 2 : 1);
+    k_small_narrow<<<(unsigned)blocks, kSmallThreads, 0, s>>>(nv, d, d2, p, verdict, blocks_done,
+                                                               done, seq);
     return hipGetLastError();
 }
 
