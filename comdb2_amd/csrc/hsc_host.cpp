@@ -212,7 +212,8 @@ struct hsc_ctx {
     // window; live = a built window takes appends into the delta
     bool live = false, merge_pending = false;
     size_t ng_built = 0;  // groups the per-group device tables were sized for
-    DBuf d_dgid[2], d_dwords[2], d_dlsn[2], d_dbmax, d_agid, d_awords, d_alsn;
+    DBuf d_dgid[2], d_dwords[2], d_dlsn[2], d_dbmax;
+    DBuf d_agid;  // an append's upload: rows + table maxima (stage_bytes layout)
     size_t dn = 0, dcap = 0;
     int dcur = 0;
     std::vector<uint32_t> app_gid;   // appended rows not yet on the device
@@ -3002,7 +3003,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
     for (auto &sl : c->small) sl.io.release();
     c->small_blocks.release();
     for (DBuf *b : {&c->d_dgid[0], &c->d_dgid[1], &c->d_dwords[0], &c->d_dwords[1], &c->d_dlsn[0],
-                    &c->d_dlsn[1], &c->d_dbmax, &c->d_agid, &c->d_awords, &c->d_alsn})
+                    &c->d_dlsn[1], &c->d_dbmax, &c->d_agid})
         b->release();
     for (HBuf &b : c->h_appq) b.release();
     for (hipEvent_t &e : c->app_ev)
