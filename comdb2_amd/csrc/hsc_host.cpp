@@ -280,7 +280,7 @@ struct hsc_ctx {
     bool ct_sorted = true;     // compact tiles: chunk-sorted records (HSC_CT_SORT=0 at build: scatter)
     bool ct_fused = false;     // ... and the plan-free join (HSC_CT_FUSED=1 at build; measured slower)
     uint64_t rank_base = 0;
-    DBuf w_tcode, w_tcode2, w_trecs;
+    DBuf w_tcode, w_tcode2, w_trecs, w_prank;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
     DBuf d_pk[2];              // packed-key sort: the keys, ping-pong (hsc_ingest.hip)
     bool packed_sort = false;  // the last build sorted packed keys
@@ -342,7 +342,7 @@ struct hsc_ctx {
     // concurrently; a lane taken over by another stream first waits for the
     // lane's last batch (its done event).
     struct Lane {
-        DBuf b[16];
+        DBuf b[20];
         hipStream_t stream = nullptr;
         hipEvent_t done = nullptr;
         uint64_t tick = 0;
@@ -381,13 +381,14 @@ struct hsc_ctx {
     hsc_timing last{};
 };
 
-// probe scratch that moves with a lane (hsc_ctx::Lane::b holds at most 16)
+// probe scratch that moves with a lane (hsc_ctx::Lane::b holds at most 20)
 static DBuf hsc_ctx::*const kLaneBufs[] = {
     &hsc_ctx::w_code,      &hsc_ctx::w_hist,      &hsc_ctx::w_counts, &hsc_ctx::w_bucket,
     &hsc_ctx::w_cursor,    &hsc_ctx::w_items,     &hsc_ctx::w_item_tile, &hsc_ctx::w_item_desc,
     &hsc_ctx::w_recs,      &hsc_ctx::w_tcode,     &hsc_ctx::w_tcode2, &hsc_ctx::w_trecs,
-    &hsc_ctx::w_vflags,    &hsc_ctx::d_done,      &hsc_ctx::p_code_lo, &hsc_ctx::p_code_hi};
-static_assert(sizeof kLaneBufs / sizeof kLaneBufs[0] <= 16, "Lane::b size");
+    &hsc_ctx::w_vflags,    &hsc_ctx::d_done,      &hsc_ctx::p_code_lo, &hsc_ctx::p_code_hi,
+    &hsc_ctx::w_prank};
+static_assert(sizeof kLaneBufs / sizeof kLaneBufs[0] <= 20, "Lane::b size");
 
 // Make the lane of c->stream active (the least recently used lane if the
 // stream has none).
@@ -2314,6 +2315,12 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     ntl.code = c->w_tcode.as<uint4>();
     ntl.code2 = c->w_tcode2.as<uint4>();
     ntl.recs = c->w_trecs.as<uint4>();
+    ntl.prank = nullptr;
+    const bool prepass = !c->rank_lsn32 && p.n && (!getenv("HSC_SNAP_PREPASS") || atoi(getenv("HSC_SNAP_PREPASS")) != 0);
+    if (prepass) {  // snapshot ranks ahead of the locate (k_snap_rank)
+        HIPCHK(c, c->w_prank.ensure(4 * (size_t)p.n));
+        ntl.prank = c->w_prank.as<uint32_t>();
+    }
     // conflict flags: internal, all zero between batches (the pack clears them)
     const size_t had = c->w_vflags.bytes;
     HIPCHK(c, c->w_vflags.ensure((std::max<size_t>(b->n_txn, 1) + 15) & ~(size_t)15));
@@ -2324,6 +2331,7 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
         for (int i = 0; i < 6; ++i)
             if (!c->ev[i]) HIPCHK(c, hipEventCreate(&c->ev[i]));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
+    if (ntl.prank) HIPCHK(c, launch_snap_rank(ntl, p, c->w_prank.as<uint32_t>(), s));
     HIPCHK(c, launch_locate_t(c->nv, wn, p, work, ntl, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     if (p.n && wn.ntiles && sorted && c->nt_fused) {
@@ -2730,7 +2738,10 @@ constexpr size_t kSmallMaxRanges = 16384;
 
 static bool small_path(hsc_ctx *c, int T)
 {
-    return !c->no_small && c->narrow && !c->timing && T <= kSmallMaxTxns && c->n > 0;
+    // a layout forced to the tile or code pipeline (tests, A/B) keeps it
+    const bool direct_ok = c->layout == HSC_LAYOUT_AUTO || c->layout == HSC_LAYOUT_NARROW ||
+                           c->layout == HSC_LAYOUT_NARROW_DIRECT;
+    return !c->no_small && c->narrow && direct_ok && !c->timing && T <= kSmallMaxTxns && c->n > 0;
 }
 
 using SteadyClock = std::chrono::steady_clock;
@@ -2997,7 +3008,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->d_nsp_g, &c->d_nsp_w, &c->d_ngs, &c->d_nscratch, &c->p_code_lo,
                     &c->p_code_hi, &c->p_zero, &c->d_commits, &c->d_cdir, &c->d_tdir, &c->d_trad, &c->d_done, &c->w_vflags, &c->d_key32, &c->d_rank32,
                     &c->d_ctmp[0], &c->d_ctmp[1], &c->d_ctmp[2], &c->d_ctmp[3], &c->w_tcode,
-                    &c->w_tcode2, &c->w_trecs};
+                    &c->w_tcode2, &c->w_trecs, &c->w_prank};
     for (DBuf *b : bufs) b->release();
     for (Stage &st : c->stage) st.release();
     for (auto &sl : c->small) sl.io.release();
