@@ -2335,8 +2335,10 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     ntl.code2 = c->w_tcode2.as<uint4>();
     ntl.recs = c->w_trecs.as<uint4>();
     ntl.prank = nullptr;
-    const bool prepass = !c->rank_lsn32 && p.n && (!getenv("HSC_SNAP_PREPASS") || atoi(getenv("HSC_SNAP_PREPASS")) != 0);
-    if (prepass) {  // snapshot ranks ahead of the locate (k_snap_rank)
+    // snapshot ranks ahead of the locate (k_snap_rank, HSC_SNAP_PREPASS=1):
+    // measured slower on config 5 (two streams 59.0 -> 63-73 us per batch)
+    const bool prepass = !c->rank_lsn32 && p.n && getenv("HSC_SNAP_PREPASS") && atoi(getenv("HSC_SNAP_PREPASS")) != 0;
+    if (prepass) {
         HIPCHK(c, c->w_prank.ensure(4 * (size_t)p.n));
         ntl.prank = c->w_prank.as<uint32_t>();
     }

@@ -36,13 +36,13 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
     # (default) or scattered into tile buckets (HSC_NT_SORT=0); the join reads
     # its tile's column from a plan kernel (default) or scans it itself, the
     # verdicts packed after it (HSC_NT_FUSED=1); snapshot ranks through the
-    # commit directory (HSC_RANK_DIR) from a pre-pass (default) or searched in
-    # the locate (HSC_SNAP_PREPASS=0)
+    # commit directory (HSC_RANK_DIR) searched in the locate (default) or by a
+    # pre-pass (HSC_SNAP_PREPASS=1)
     runs = [(LAYOUT_NARROW_DIRECT, None), (LAYOUT_NARROW_TILES, None),
             (LAYOUT_NARROW_TILES, "HSC_TILE_DIR"), (LAYOUT_NARROW_TILES, "HSC_RANK_DIR"),
             (LAYOUT_NARROW_TILES, "HSC_TRAD_MODE=log"), (LAYOUT_NARROW_TILES, "HSC_TRAD_MODE=lin"),
             (LAYOUT_NARROW_TILES, "HSC_NT_SORT=0"), (LAYOUT_NARROW_TILES, "HSC_NT_FUSED=1"),
-            (LAYOUT_NARROW_TILES, "HSC_RANK_DIR+HSC_SNAP_PREPASS=0"),
+            (LAYOUT_NARROW_TILES, "HSC_RANK_DIR+HSC_SNAP_PREPASS=1"),
             (LAYOUT_NARROW_CODES, None), (LAYOUT_WIDE, None)]
     try:
         for layout, knob in runs:
