@@ -631,130 +631,6 @@ __device__ __forceinline__ void join_item_s(const ProbeWork &work, const CTiles 
     join_search<WG>(work, ct, flags, kw, rank, b16, b128, B, kind, pl, ph0, ph1);
 }
 
-// (HSC_CJOIN2=1, off: measured slower) Chunk-sorted records, 512 threads, key words 0 and 1 staged (word 2 of a
-// 3-word key read from the window on a two-word tie): 49 KiB of LDS, so three
-// workgroups fit a CU where the 1024-thread join's 64 KiB fit two -- more
-// tiles in flight (config 3: 1475 tiles over 768 slots instead of 512), and
-// a tile's ~410 records keep most of its 512 lanes busy (each thread takes
-// records j and j + 512 of its item).
-constexpr int kCJ2 = 512;
-constexpr int kCJ2Rows = kCTRows / kCJ2;  // rows staged per thread (4)
-template <int WG>
-__device__ __forceinline__ void join_item_s2(const ProbeWork &work, const CTiles &ct, uint8_t *flags,
-                                             uint32_t xi, bool whole_tile, uint64_t *kw,
-                                             uint32_t *rank, uint32_t *b16, uint32_t *b128,
-                                             uint32_t *B, uint32_t *Es, uint16_t *Cs)
-{
-    constexpr uint32_t T = kCTRows;
-    constexpr int WL = WG < 2 ? WG : 2;
-    const uint32_t tid = threadIdx.x;
-    uint32_t tile, j0, j1;
-    if (whole_tile) {
-        tile = xi, j0 = 0, j1 = 0;
-    } else {
-        const uint32_t *d = (const uint32_t *)(work.item_desc + xi);
-        tile = sload(d), j0 = sload(d + 1), j1 = sload(d + 2);
-    }
-    const uint32_t G = work.G;
-    const size_t col = (size_t)tile * hist_stride(G);
-    uint32_t e = 0, cs = 0;
-    if (tid < G) e = work.hist[col + tid], cs = work.cst[col + tid];
-    const size_t row = ((size_t)tile << kCTLog2) + kCJ2Rows * tid;
-    u64x2 kv[WL][2];
-#pragma unroll
-    for (int w = 0; w < WL; ++w) {
-        const u64x2 *src = (const u64x2 *)(ct.key + (size_t)w * ct.len + row);
-        kv[w][0] = src[0];
-        kv[w][1] = src[1];
-    }
-    const u32x4 rr = *(const u32x4 *)(ct.rank + row);
-    u32x2 bt[2] = {{0, 0}, {0, 0}};
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const uint32_t o = 2 * (tid + k * kCJ2);
-        if (o < (uint32_t)kTBS) bt[k] = *(const u32x2 *)(ct.tb + (size_t)tile * kTBS + o);
-    }
-    if (whole_tile) j1 = min(kTileCap, sload(work.counts + tile));
-    if (tid < G) Es[tid] = e, Cs[tid] = (uint16_t)cs;
-    __syncthreads();
-    constexpr int R = kTileCap / kCJ2;  // records per thread (2)
-    u64x2 A0[R], A1[R], B0[R], B1[R];
-    bool live[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const uint32_t j = j0 + r * kCJ2 + tid;
-        live[r] = j < j1;
-        A0[r] = A1[r] = B0[r] = B1[r] = u64x2{0, 0};
-        if (live[r]) {
-            uint32_t g = 0;  // Es[0] = 0 <= j
-#pragma unroll
-            for (int b = 8; b >= 0; --b) {
-                const uint32_t c = g + (1u << b);
-                if (c < G && Es[c] <= j) g = c;
-            }
-            const u64x2 *rp = (const u64x2 *)ct.recs +
-                              4 * ((size_t)g * 2 * work.chunk + Cs[g] + (j - Es[g]));
-            A0[r] = rp[0], A1[r] = rp[1], B0[r] = rp[2], B1[r] = rp[3];
-        }
-    }
-#pragma unroll
-    for (int w = 0; w < WL; ++w) {
-        *(u64x2 *)(kw + (size_t)w * T + kCJ2Rows * tid) = kv[w][0];
-        *(u64x2 *)(kw + (size_t)w * T + kCJ2Rows * tid + 2) = kv[w][1];
-    }
-    *(u32x4 *)(rank + kCJ2Rows * tid) = rr;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const uint32_t o = 2 * (tid + k * kCJ2);
-        if (o < (uint32_t)kTBS) *(u32x2 *)(B + o) = bt[k];
-    }
-    uint32_t m = max(max(rr.x, rr.y), max(rr.z, rr.w));
-#pragma unroll
-    for (int d = 1; d < 4; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
-    if ((tid & 3) == 0) b16[tid >> 2] = m;
-#pragma unroll
-    for (int d = 4; d < 32; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
-    if ((tid & 31) == 0) b128[tid >> 5] = m;
-    __syncthreads();
-    const uint64_t *kg = WG > WL ? ct.key + (size_t)WL * ct.len + ((size_t)tile << kCTLog2) : nullptr;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        if (!live[r]) continue;
-        const uint32_t kind = (uint32_t)(A1[r].y >> 62);
-        const uint64_t rt = A1[r].y & ((1ull << 62) - 1);
-        u64x2 pl[2] = {A0[r], u64x2{A1[r].x, rt}}, ph0 = B0[r];
-        uint64_t ph1 = B1[r].x;
-        if (kind == kCTail) ph0 = A0[r], ph1 = A1[r].x;  // a tail record carries hi in its first half
-        join_search<WG, WL>(work, ct, flags, kw, rank, b16, b128, B, kind, pl, ph0, ph1, kg);
-    }
-}
-
-template <int WG>
-__global__ __launch_bounds__(kCJ2) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_join_c2(
-    ProbeWork work, CTiles ct, uint8_t *flags)
-{
-    constexpr uint32_t T = kCTRows;
-    constexpr int WL = WG < 2 ? WG : 2;
-    extern __shared__ __attribute__((aligned(16))) uint64_t jl[];
-    uint64_t *kw = jl;                                   // [WL][T], sorted
-    uint32_t *rank = (uint32_t *)(jl + (size_t)WL * T);  // [T], sorted order
-    uint32_t *b16 = rank + T;                            // [T / 16]
-    uint32_t *b128 = b16 + T / 16;                       // [T / 128]
-    uint32_t *B = b128 + T / 128;                        // [kTBS] the tile's bucket table
-    uint32_t *Es = B + kTBS;                              // the tile's column
-    uint16_t *Cs = (uint16_t *)(Es + kMaxChunks);
-    const uint32_t xb = gridDim.x - ct.ntiles;  // overflow items first (the fullest tiles)
-    if (blockIdx.x >= xb) {
-        join_item_s2<WG>(work, ct, flags, blockIdx.x - xb, true, kw, rank, b16, b128, B, Es, Cs);
-        return;
-    }
-    const uint32_t nextra = work.item_off[1];
-    for (uint32_t xi = blockIdx.x; xi < nextra; xi += xb) {
-        __syncthreads();  // the previous item's LDS reads are done
-        join_item_s2<WG>(work, ct, flags, xi, false, kw, rank, b16, b128, B, Es, Cs);
-    }
-}
-
 // XCD-contiguous tiles (as the narrow join): measured neutral on config 3
 // (1.100 vs 1.108 G checks/s, r02c), so off by default
 #ifndef HSC_CJOIN_XCD
@@ -970,22 +846,6 @@ hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_i
     const uint32_t blocks =
         ct_tile_blocks(work.local_items != 0, ct.ntiles) + (extra < 512 ? extra : 512);
     const bool srt = work.local_items != 0;
-    // the 512-thread join (HSC_CJOIN2=1): measured slower on config 3 (two
-    // streams 78.2 -> 80.4 us per batch, one stream 108 -> 112 us; r03h)
-    const bool j2 = getenv("HSC_CJOIN2") && atoi(getenv("HSC_CJOIN2")) != 0;
-    if (srt && j2 && !kCJoinXcd) {  // 512 threads, words 0-1 staged
-        const int wl = ct.WG < 2 ? ct.WG : 2;
-        const size_t lds2 = 8 * (size_t)wl * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
-                            4 * (kCTRows / 128) + 4 * kTBS + 6 * (size_t)kMaxChunks;
-        const uint32_t b2 = ct.ntiles + (extra < 512 ? extra : 512);
-        switch (ct.WG) {
-        case 1: k_join_c2<1><<<b2, kCJ2, lds2, s>>>(work, ct, flags); break;
-        case 2: k_join_c2<2><<<b2, kCJ2, lds2, s>>>(work, ct, flags); break;
-        case 3: k_join_c2<3><<<b2, kCJ2, lds2, s>>>(work, ct, flags); break;
-        default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
     const size_t lds = 8 * (size_t)ct.WG * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
                        4 * (kCTRows / 128) + 4 * kTBS + (srt ? 6 * (size_t)kMaxChunks : 0);
 #define HSC_JOIN_C(WG_)                                                                   \

@@ -280,7 +280,7 @@ struct hsc_ctx {
     bool ct_sorted = true;     // compact tiles: chunk-sorted records (HSC_CT_SORT=0 at build: scatter)
     bool ct_fused = false;     // ... and the plan-free join (HSC_CT_FUSED=1 at build; measured slower)
     uint64_t rank_base = 0;
-    DBuf w_tcode, w_tcode2, w_trecs, w_prank;
+    DBuf w_tcode, w_tcode2, w_trecs;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
     DBuf d_pk[2];              // packed-key sort: the keys, ping-pong (hsc_ingest.hip)
     bool packed_sort = false;  // the last build sorted packed keys
@@ -386,8 +386,7 @@ static DBuf hsc_ctx::*const kLaneBufs[] = {
     &hsc_ctx::w_code,      &hsc_ctx::w_hist,      &hsc_ctx::w_counts, &hsc_ctx::w_bucket,
     &hsc_ctx::w_cursor,    &hsc_ctx::w_items,     &hsc_ctx::w_item_tile, &hsc_ctx::w_item_desc,
     &hsc_ctx::w_recs,      &hsc_ctx::w_tcode,     &hsc_ctx::w_tcode2, &hsc_ctx::w_trecs,
-    &hsc_ctx::w_vflags,    &hsc_ctx::d_done,      &hsc_ctx::p_code_lo, &hsc_ctx::p_code_hi,
-    &hsc_ctx::w_prank};
+    &hsc_ctx::w_vflags,    &hsc_ctx::d_done,      &hsc_ctx::p_code_lo, &hsc_ctx::p_code_hi};
 static_assert(sizeof kLaneBufs / sizeof kLaneBufs[0] <= 20, "Lane::b size");
 
 // Make the lane of c->stream active (the least recently used lane if the
@@ -2334,14 +2333,6 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     ntl.code = c->w_tcode.as<uint4>();
     ntl.code2 = c->w_tcode2.as<uint4>();
     ntl.recs = c->w_trecs.as<uint4>();
-    ntl.prank = nullptr;
-    // snapshot ranks ahead of the locate (k_snap_rank, HSC_SNAP_PREPASS=1):
-    // measured slower on config 5 (two streams 59.0 -> 63-73 us per batch)
-    const bool prepass = !c->rank_lsn32 && p.n && getenv("HSC_SNAP_PREPASS") && atoi(getenv("HSC_SNAP_PREPASS")) != 0;
-    if (prepass) {
-        HIPCHK(c, c->w_prank.ensure(4 * (size_t)p.n));
-        ntl.prank = c->w_prank.as<uint32_t>();
-    }
     // conflict flags: internal, all zero between batches (the pack clears them)
     const size_t had = c->w_vflags.bytes;
     HIPCHK(c, c->w_vflags.ensure((std::max<size_t>(b->n_txn, 1) + 15) & ~(size_t)15));
@@ -2352,7 +2343,6 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
         for (int i = 0; i < 6; ++i)
             if (!c->ev[i]) HIPCHK(c, hipEventCreate(&c->ev[i]));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
-    if (ntl.prank) HIPCHK(c, launch_snap_rank(ntl, p, c->w_prank.as<uint32_t>(), s));
     HIPCHK(c, launch_locate_t(c->nv, wn, p, work, ntl, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     if (p.n && wn.ntiles && sorted && c->nt_fused) {
@@ -3029,7 +3019,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->d_nsp_g, &c->d_nsp_w, &c->d_ngs, &c->d_nscratch, &c->p_code_lo,
                     &c->p_code_hi, &c->p_zero, &c->d_commits, &c->d_cdir, &c->d_tdir, &c->d_trad, &c->d_done, &c->w_vflags, &c->d_key32, &c->d_rank32,
                     &c->d_ctmp[0], &c->d_ctmp[1], &c->d_ctmp[2], &c->d_ctmp[3], &c->w_tcode,
-                    &c->w_tcode2, &c->w_trecs, &c->w_prank};
+                    &c->w_tcode2, &c->w_trecs};
     for (DBuf *b : bufs) b->release();
     for (Stage &st : c->stage) st.release();
     for (auto &sl : c->small) sl.io.release();

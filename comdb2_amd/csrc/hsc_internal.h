@@ -291,13 +291,7 @@ struct NarrowTiles {
     uint4 *code;               // [n] first record {tile << 12 | rank, lo, hi, r(S)}
     uint4 *code2;              // [n] second record (flag kHasSecond in code.x)
     uint4 *recs;               // [2n] {lo delta, hi delta, snapshot rank, read set}
-    const uint32_t *prank;     // [n] r(S) of every probe (k_snap_rank), or nullptr:
-                               // the locate searches cdir itself
 };
-// r(S) of every probe of p (windows whose commits span >= 2^32 of log): a
-// lockstep search of the commit directory, 4 probes per thread
-hipError_t launch_snap_rank(const NarrowTiles &nt, const ProbeView &p, uint32_t *prank,
-                            hipStream_t s);
 hipError_t check_sorted_u64(const uint64_t *v, size_t n, uint32_t *flag, hipStream_t s);
 // rank32 by a search of cdir (the 16-ary directory over the commit LSNs C)
 hipError_t narrow_tiles_build(const uint64_t *key64, const uint64_t *lsn, uint32_t n, uint32_t len,

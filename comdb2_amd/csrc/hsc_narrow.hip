@@ -744,46 +744,6 @@ __device__ __forceinline__ void locate_codes(const NarrowView &nv, const ProbeVi
     hi = live ? v : 0;
 }
 
-// ---- snapshot ranks ahead of the locate ----
-// r(S) = #distinct commit LSNs <= S for every probe, for windows whose commits
-// span >= 2^32 of log (config 5): the locate otherwise searches the commit
-// directory per sub-chunk, a chain of dependent loads its 4 waves per SIMD
-// cannot hide; here each thread runs its 4 probes' searches in lockstep, and
-// with two batches in flight the kernel overlaps the other batch's join.
-constexpr int kRankPThreads = 1024, kRankPK = 4;
-__global__ __launch_bounds__(kRankPThreads) void k_snap_rank(NarrowTiles nt, ProbeView p,
-                                                             uint32_t *prank)
-{
-    extern __shared__ __attribute__((aligned(16))) uint64_t cl[];
-    const uint32_t base = blockIdx.x * (kRankPThreads * kRankPK) + threadIdx.x;
-    uint64_t xs[kRankPK];
-    bool act[kRankPK];
-#pragma unroll
-    for (int k = 0; k < kRankPK; ++k) {
-        const uint32_t q = base + k * kRankPThreads;
-        act[k] = q < p.n;
-        xs[k] = act[k] ? dir_le(__builtin_nontemporal_load(p.snap + q)) : 0;
-    }
-    dir16_stage(nt.cdir, cl);
-    __syncthreads();
-    uint32_t r[kRankPK];
-    dir16_count<kRankPK>(nt.cdir, cl, xs, act, r);
-#pragma unroll
-    for (int k = 0; k < kRankPK; ++k) {
-        const uint32_t q = base + k * kRankPThreads;
-        if (act[k]) prank[q] = r[k];
-    }
-}
-
-hipError_t launch_snap_rank(const NarrowTiles &nt, const ProbeView &p, uint32_t *prank, hipStream_t s)
-{
-    if (p.n == 0) return hipSuccess;
-    const uint32_t per = kRankPThreads * kRankPK;
-    k_snap_rank<<<(p.n + per - 1) / per, kRankPThreads, 8 * (size_t)dir16_lds_entries(nt.cdir), s>>>(
-        nt, p, prank);
-    return hipGetLastError();
-}
-
 // ---- bucket table over the tiles' first codes ----
 // first[0] = 0 (codes are relative to the window's first row), so bucket k
 // covers codes [k << shift, (k + 1) << shift) with shift the least that puts
@@ -874,7 +834,7 @@ __host__ __device__ inline LocLds loc_lds(const NarrowTiles &nt, uint32_t ntiles
     L.first = o;
     o += 8 * (nt.trad ? ((ntiles + 1) & ~1u) : dir16_lds_entries(nt.tdir));
     L.cdir = o;
-    o += nt.rank_lsn32 || nt.prank ? 0 : 8 * dir16_lds_entries(nt.cdir);
+    o += nt.rank_lsn32 ? 0 : 8 * dir16_lds_entries(nt.cdir);
     L.hist = o;
     o += 4 * ((ntiles + 3) & ~3u);
     L.trad = o;
@@ -982,7 +942,7 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
     const uint32_t c1 = min(p.n, c0 + work.chunk);
     // probe registers: buffer 0 / 1 alternate between sub-chunks (the loop
     // below is unrolled, so every index is a compile-time constant)
-    uint32_t qq[2][K], gg[2][K], tx[2][K], pr[2][K];
+    uint32_t qq[2][K], gg[2][K], tx[2][K];
     bool valid[2][K];
     uint64_t snap[2][K], xl[2][K][WR], xh[2][K][WR];
     // kSort: the chunk's records stay in registers until its histogram is
@@ -1001,7 +961,6 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
             gg[buf][k] = p.n ? __builtin_nontemporal_load(p.gid + q) : 0;
             snap[buf][k] = p.n ? __builtin_nontemporal_load(p.snap + q) : 0;
             if constexpr (kSort) tx[buf][k] = p.n ? __builtin_nontemporal_load(p.txn + q) : 0;
-            pr[buf][k] = nt.prank && p.n ? __builtin_nontemporal_load(nt.prank + q) : 0;
 #pragma unroll
             for (int w = 0; w < W; ++w) {
                 xl[buf][k][w] = p.n ? __builtin_nontemporal_load(p.lo + (size_t)w * p.n + q) : 0;
@@ -1021,7 +980,7 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
     } else {
         dir16_stage(nt.tdir, tfirst);
     }
-    if (!nt.rank_lsn32 && !nt.prank) dir16_stage(nt.cdir, cdir);
+    if (!nt.rank_lsn32) dir16_stage(nt.cdir, cdir);
     for (uint32_t i = threadIdx.x; i < ntiles; i += kLocTThreads) hist[i] = 0;
     __syncthreads();  // directories staged, histogram zeroed
     HSC_STAMP(work, 0, 1);
@@ -1060,9 +1019,6 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
         if (nt.rank_lsn32) {
 #pragma unroll
             for (int k = 0; k < K; ++k) rs[k] = lsn32_rank(snap[cb][k], nt.rank_base);
-        } else if (nt.prank) {  // k_snap_rank ran ahead
-#pragma unroll
-            for (int k = 0; k < K; ++k) rs[k] = pr[cb][k];
         } else {
             const uint64_t le_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
             bool head[K];

@@ -96,9 +96,8 @@ def _both(v, log, rs):
     """Verdicts through the compact tiles and through the wide compact pipeline;
     the compact tiles' scatter path (HSC_CT_SORT=0 at the build: probe
     entries + bucket entries instead of chunk-sorted records) and the planned
-    join of chunk-sorted records and the plan-free one (HSC_CT_FUSED=1), and
-    the 1024-thread join and the 512-thread one (two key words in LDS,
-    HSC_CJOIN2=1) must agree."""
+    join of chunk-sorted records and the plan-free one (HSC_CT_FUSED=1)
+    must agree."""
     os.environ["HSC_CT_SORT"] = "0"
     try:
         v.set_layout(LAYOUT_AUTO)
@@ -112,12 +111,6 @@ def _both(v, log, rs):
     assert 1 <= v.tile_key_words <= 3
     got = v.check_readsets(rs) != 0
     np.testing.assert_array_equal(scat, got, err_msg="chunk-sorted vs scattered records")
-    os.environ["HSC_CJOIN2"] = "1"  # the 512-thread join staging key words 0-1
-    try:
-        j512 = v.check_readsets(rs) != 0
-    finally:
-        os.environ.pop("HSC_CJOIN2", None)
-    np.testing.assert_array_equal(j512, got, err_msg="512- vs 1024-thread join")
     os.environ["HSC_CT_FUSED"] = "1"  # chunk-sorted records through the plan-free join
     try:
         v.ingest_log(log)

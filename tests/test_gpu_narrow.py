@@ -35,14 +35,11 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
     # picks the mode whose fullest bucket is smaller); records chunk-sorted
     # (default) or scattered into tile buckets (HSC_NT_SORT=0); the join reads
     # its tile's column from a plan kernel (default) or scans it itself, the
-    # verdicts packed after it (HSC_NT_FUSED=1); snapshot ranks through the
-    # commit directory (HSC_RANK_DIR) searched in the locate (default) or by a
-    # pre-pass (HSC_SNAP_PREPASS=1)
+    # verdicts packed after it (HSC_NT_FUSED=1)
     runs = [(LAYOUT_NARROW_DIRECT, None), (LAYOUT_NARROW_TILES, None),
             (LAYOUT_NARROW_TILES, "HSC_TILE_DIR"), (LAYOUT_NARROW_TILES, "HSC_RANK_DIR"),
             (LAYOUT_NARROW_TILES, "HSC_TRAD_MODE=log"), (LAYOUT_NARROW_TILES, "HSC_TRAD_MODE=lin"),
             (LAYOUT_NARROW_TILES, "HSC_NT_SORT=0"), (LAYOUT_NARROW_TILES, "HSC_NT_FUSED=1"),
-            (LAYOUT_NARROW_TILES, "HSC_RANK_DIR+HSC_SNAP_PREPASS=1"),
             (LAYOUT_NARROW_CODES, None), (LAYOUT_WIDE, None)]
     try:
         for layout, knob in runs:
@@ -51,18 +48,14 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
                 os.environ[var] = val or "1"
             v.set_layout(layout)
             v.ingest_log(log)
-            # (HSC_SNAP_PREPASS is read per batch: it stays set for the check)
             for var, _, _ in kv:
-                if var != "HSC_SNAP_PREPASS":
-                    os.environ.pop(var, None)
+                os.environ.pop(var, None)
             assert v.layout == (LAYOUT_WIDE if layout == LAYOUT_WIDE else expect_auto)
             got[layout] = v.check_readsets(rs)
-            os.environ.pop("HSC_SNAP_PREPASS", None)
             np.testing.assert_array_equal(got[layout] != 0, want != 0,
                                           err_msg=f"layout {layout} knob {knob}")
     finally:
-        for knob in ("HSC_TILE_DIR", "HSC_RANK_DIR", "HSC_TRAD_MODE", "HSC_NT_SORT", "HSC_NT_FUSED",
-                     "HSC_SNAP_PREPASS"):
+        for knob in ("HSC_TILE_DIR", "HSC_RANK_DIR", "HSC_TRAD_MODE", "HSC_NT_SORT", "HSC_NT_FUSED"):
             os.environ.pop(knob, None)
         v.set_layout(LAYOUT_AUTO)
     return want
