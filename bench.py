@@ -877,10 +877,14 @@ def main():
     # the ring: every timed step probes a batch no other step of the region touches
     # (warmup + steps <= NB) or, with a longer run, the least recently probed one
     elapsed = timed(S, NB)
-    serial_elapsed = timed(1, NB) if S > 1 else elapsed
+    # the secondary legs (one stream; cache-resident): the median of 5 timed
+    # regions each, so one host hiccup inside a ~1 ms region does not move them
+    def med(nstreams, nbatch):
+        return float(np.median([timed(nstreams, nbatch) for _ in range(5)]))
+    serial_elapsed = med(1, NB) if S > 1 else elapsed
     # L3-resident: two batches alternate (window + both batches fit the 256 MiB cache)
-    l3_elapsed = timed(S, 2) if NB > 2 else elapsed
-    l3_serial = timed(1, 2) if NB > 2 else serial_elapsed
+    l3_elapsed = med(S, 2) if NB > 2 else elapsed
+    l3_serial = med(1, 2) if NB > 2 else serial_elapsed
     v.set_stream(streams[0].cuda_stream)
 
     # verdicts of batch 0 (for the conflict rate and the CPU parity sample)
@@ -968,6 +972,7 @@ def main():
             "unit": "GB/s",
             "frac": frac(elapsed),
             "frac_1stream": frac(serial_elapsed),
+            "secondary_legs": "frac_1stream and l3_resident: the median of 5 timed regions each",
             "traffic": traffic.get("bytes_per_batch") if traffic else None,
             # the same time against the PMC-measured bytes (FETCH_SIZE counts
             # Infinity-Cache hits too): how much of HBM's peak the probe phase

@@ -20,9 +20,12 @@
 // Up to max_inflight batches run at once: hip_serial_check_batch releases the
 // context lock while a small batch's kernel runs, so the next leader marshals
 // and launches its batch meanwhile (the kernels queue on the context's
-// stream).  A caller sleeps on a futex word of its own request; a finished
-// batch sets its callers' done bits after dropping the collector lock (the
-// set is the last touch of a request: its caller may return right after).
+// stream).  Callers sleep on the futex word of their batch (a request takes
+// the id of the batch open when it queues); a finished batch sets its
+// callers' done bits after dropping the collector lock (the set is the last
+// touch of a request: its caller may return right after), then wakes the
+// whole batch with one futex call, and the woken callers return without
+// taking the collector lock.
 #include "../../include/hip_serial.h"
 #include "hsc_internal.h"
 
@@ -39,20 +42,22 @@
 #include <deque>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 namespace {
 
-constexpr uint32_t kDone = 1u;  // Req::word: bit 0 = verdict ready, the rest counts wake-ups
+constexpr uint32_t kDone = 1u;  // Req::word: the verdict is ready
+constexpr uint32_t kChans = 16;  // batch wait words (more than batches alive at once: <= 4 + 1)
 
 void futex_wait(std::atomic<uint32_t> *w, uint32_t seen)
 {
     syscall(SYS_futex, (uint32_t *)w, FUTEX_WAIT_PRIVATE, seen, nullptr, nullptr, 0);
 }
 
-void futex_wake(std::atomic<uint32_t> *w)
+void futex_wake_all(std::atomic<uint32_t> *w)
 {
-    syscall(SYS_futex, (uint32_t *)w, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0);
+    syscall(SYS_futex, (uint32_t *)w, FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
 }
 
 }  // namespace
@@ -70,27 +75,35 @@ struct hsc_collector {
         int regop_only;
         int rc;
         hsc::PreMarshal *pm;  // the caller's marshalled rows, or null
-        bool queued;  // in q (under m): not yet taken into a batch
+        bool queued;    // in q (under m): not yet taken into a batch
+        uint32_t chan;  // the batch id open when it queued (its wait word: chan % kChans)
         std::atomic<uint32_t> word{0};
     };
     std::deque<Req *> q;
     bool elected = false;  // a leader is waiting to take the next batch
     int running = 0;       // batches on the device
+    uint32_t open_id = 0;  // the batch queued requests will join
+    std::atomic<uint32_t> chan[kChans];  // per-batch wait words (bumped at each wake)
     std::condition_variable run_cv;     // a batch finished (the elected leader waits)
     std::condition_variable arrive_cv;  // a request queued (a gathering leader waits)
-    int inside = 0;                     // callers inside hsc_collector_check
-    std::condition_variable idle_cv;    // inside dropped to 0 (destroy waits)
-    hsc_collector_stats st{};
+    std::atomic<int> inside{0};         // callers inside hsc_collector_check (last touch: the decrement)
+    hsc_collector_stats st{};           // (under m, but handout_ns:)
+    std::atomic<uint64_t> st_handout_ns{0};
+    hsc_collector()
+    {
+        for (auto &c : chan) c.store(0, std::memory_order_relaxed);
+    }
 };
 
 namespace {
 
-// wake a queued request's caller to re-check (it is elected leader); the
-// caller is alive: it cannot return before its done bit
-void poke(hsc_collector::Req *q)
+// wake the callers sleeping on batch word `id` to re-check (the queued ones
+// elect a leader; the others sleep again)
+void wake(hsc_collector *k, uint32_t id)
 {
-    q->word.fetch_add(2, std::memory_order_release);
-    futex_wake(&q->word);
+    std::atomic<uint32_t> &w = k->chan[id % kChans];
+    w.fetch_add(1, std::memory_order_acq_rel);
+    futex_wake_all(&w);
 }
 
 // one device pass over a group of requests that share regop_only
@@ -149,10 +162,11 @@ int hsc_collector_set_inflight(hsc_collector *k, int n)
 void hsc_collector_destroy(hsc_collector *k)
 {
     if (!k) return;
-    {  // callers still inside hsc_collector_check are a caller bug; drain them anyway
-        std::unique_lock<std::mutex> lk(k->m);
-        k->idle_cv.wait(lk, [k] { return k->inside == 0; });
-    }
+    // callers still inside hsc_collector_check are a caller bug; drain them
+    // anyway (a returning caller's last touch of k is its decrement)
+    while (k->inside.load(std::memory_order_acquire) != 0)
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    { std::lock_guard<std::mutex> g(k->m); }  // a leader still unlocking
     delete k;
 }
 
@@ -179,40 +193,63 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
     if (!regop_only && k->premarshal && tl_pm &&
         hsc::premarshal(k->ctx, a, ((uint64_t)*r.file << 32) | *r.offset, tl_pm.get()))
         r.pm = tl_pm.get();
+    k->inside.fetch_add(1, std::memory_order_relaxed);
     std::unique_lock<std::mutex> lk(k->m);
+    r.chan = k->open_id;
     k->q.push_back(&r);
     k->st.calls++;
-    k->inside++;
     if (k->max_wait_us > 0) k->arrive_cv.notify_one();
-    for (;;) {
-        const uint32_t w = r.word.load(std::memory_order_acquire);
-        if (w & kDone) break;
-        // a request already in some batch waits for its verdict; a queued one
-        // leads when no leader is elected (futex: no lost wake-up)
-        if (k->elected || !r.queued) {
+    for (;;) {  // under lk
+        if (!r.queued) {
+            // in a batch: wait for the done bit without the lock (the batch's
+            // leader sets it, then bumps and wakes the batch word)
+            std::atomic<uint32_t> &w = k->chan[r.chan % kChans];
             lk.unlock();
-            futex_wait(&r.word, w);
+            for (;;) {
+                const uint32_t seen = w.load(std::memory_order_acquire);
+                if (r.word.load(std::memory_order_acquire) & kDone) break;
+                futex_wait(&w, seen);
+            }
+            break;
+        }
+        if (k->elected) {  // queued behind an elected leader: sleep until woken
+            std::atomic<uint32_t> &w = k->chan[r.chan % kChans];
+            const uint32_t seen = w.load(std::memory_order_acquire);
+            lk.unlock();
+            futex_wait(&w, seen);
+            if (r.word.load(std::memory_order_acquire) & kDone) break;  // taken and answered meanwhile
             lk.lock();
             continue;
         }
         k->elected = true;  // this caller leads the next batch
+        const auto tg = std::chrono::steady_clock::now();
         k->run_cv.wait(lk, [k] { return k->running < k->max_inflight; });
+        k->st.gate_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                             std::chrono::steady_clock::now() - tg).count();
         if (k->max_wait_us > 0 && (int)k->q.size() < k->max_batch)
             k->arrive_cv.wait_for(lk, std::chrono::microseconds(k->max_wait_us),
                                   [k] { return (int)k->q.size() >= k->max_batch; });
         const size_t take = std::min(k->q.size(), (size_t)k->max_batch);
         std::vector<hsc_collector::Req *> full, regop;
+        std::vector<uint32_t> ids;  // batch words of the taken requests (one, or two after a max_batch cut)
         bool mine = false;  // max_batch may leave this caller's own request queued
         for (size_t i = 0; i < take; ++i) {
             hsc_collector::Req *q = k->q.front();
             k->q.pop_front();
             q->queued = false;
             mine |= q == &r;
+            if (std::find(ids.begin(), ids.end(), q->chan) == ids.end()) ids.push_back(q->chan);
             (q->regop_only ? regop : full).push_back(q);
         }
+        const uint32_t taken_id = k->open_id++;  // later arrivals form the next batch
         k->running++;
         k->elected = false;
-        if (!k->q.empty()) poke(k->q.front());  // elect the next leader now
+        // requests max_batch left queued (they sleep on this batch's word):
+        // they join the next batch, and wake to elect its leader
+        if (!k->q.empty()) {
+            for (hsc_collector::Req *q : k->q) q->chan = k->open_id;
+            wake(k, taken_id);
+        }
         lk.unlock();
         const auto t0 = std::chrono::steady_clock::now();
         run_group(k, regop, 1);
@@ -224,21 +261,25 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
         k->st.batches++;
         k->st.max_batch = std::max<uint64_t>(k->st.max_batch, take);
         k->run_cv.notify_one();
-        if (!k->elected && !k->q.empty()) poke(k->q.front());
+        const bool elect = !k->elected && !k->q.empty();
+        const uint32_t next = elect ? k->q.front()->chan : 0;
         lk.unlock();
+        if (elect) wake(k, next);
         // hand out the verdicts: each done bit is the last touch of its
-        // request (the futex wake only names the address)
+        // request, then one wake per batch word
         for (auto *g : {&regop, &full})
-            for (hsc_collector::Req *q : *g) {
-                if (q == &r) continue;
-                q->word.fetch_or(kDone, std::memory_order_release);
-                futex_wake(&q->word);
-            }
-        lk.lock();
+            for (hsc_collector::Req *q : *g)
+                if (q != &r) q->word.fetch_or(kDone, std::memory_order_release);
+        for (uint32_t id : ids) wake(k, id);
+        k->st_handout_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                       std::chrono::steady_clock::now() - t1).count(),
+                                   std::memory_order_relaxed);
         if (mine) break;
+        lk.lock();
     }
-    if (--k->inside == 0) k->idle_cv.notify_all();
-    return r.rc;
+    const int rc = r.rc;
+    k->inside.fetch_sub(1, std::memory_order_release);  // last touch of k
+    return rc;
 }
 
 int hsc_collector_get_stats(hsc_collector *k, hsc_collector_stats *out)
@@ -246,6 +287,7 @@ int hsc_collector_get_stats(hsc_collector *k, hsc_collector_stats *out)
     if (!k || !out) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(k->m);
     *out = k->st;
+    out->handout_ns = k->st_handout_ns.load(std::memory_order_relaxed);
     return HSC_OK;
 }
 

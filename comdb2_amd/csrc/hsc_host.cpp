@@ -123,10 +123,18 @@ static StageLayout stage_layout(int W, size_t n, size_t nl)
     return L;
 }
 
+// Room a small batch's slot needs past the columns: the verdict bytes and the
+// done word, each 64-byte aligned (hsc_ctx::SmallSlot).
+static size_t small_tail(size_t n_txn) { return 64 + ((n_txn + 63) & ~(size_t)63) + 64; }
+
 struct Stage {
     HBuf arena, forced, verdict;
     StageLayout L;
     size_t n = 0, n_lock = 0, n_txn = 0;
+    // the small-batch stage: its arena is fine-grained pinned memory with room
+    // for the slot's verdicts and done word, and moves into the slot at launch
+    // (the kernel reads the columns where the marshal wrote them)
+    bool coh = false;
     hipEvent_t done = nullptr;  // the chunk's verdict download
     template <class T>
     T *col(size_t off) const
@@ -366,6 +374,7 @@ struct hsc_ctx {
         std::atomic<bool> busy{false};
     };
     SmallSlot small[kSmallSlots];
+    Stage small_st;  // marshal target of the small path (coh: its arena swaps into a slot)
     uint32_t small_next = 0;
     DBuf small_blocks;
     bool small_blocks_zeroed = false;
@@ -373,7 +382,7 @@ struct hsc_ctx {
     uint32_t small_seq = 0;
     // small-path phase times (hsc_small_stats)
     std::atomic<uint64_t> sm_calls{0}, sm_marshal_ns{0}, sm_launch_ns{0}, sm_wait_ns{0},
-        sm_slot_waits{0};
+        sm_slot_waits{0}, sm_lock_ns{0};
 
     // timing
     bool timing = false;
@@ -2061,7 +2070,8 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
     }
     const bool pin = !c->host_only;
     st.L = stage_layout(W, n, nl);
-    if (st.arena.ensure(std::max<size_t>(st.L.total, 256), pin))
+    if (st.arena.ensure(std::max<size_t>(st.L.total + (st.coh ? small_tail((size_t)nt) : 0), 256), pin,
+                        st.coh && pin))
         return fail(c, HSC_ENOMEM, "staging buffers");
     uint64_t *lo = st.col<uint64_t>(st.L.lo), *hi = st.col<uint64_t>(st.L.hi);
     uint64_t *sn = st.col<uint64_t>(st.L.snap);
@@ -2786,7 +2796,11 @@ static int small_launch(hsc_ctx *c, Stage &st)
     sl.vo = (st.L.total + 63) & ~(size_t)63;
     sl.dn = (sl.vo + st.n_txn + 63) & ~(size_t)63;
     sl.n_txn = st.n_txn;
-    if (sl.io.ensure(sl.dn + 64, true, true)) return fail(c, HSC_ENOMEM, "small-batch staging");
+    // the columns stay where the marshal wrote them: the stage's arena becomes
+    // the slot's, the slot's old buffer the stage's next arena
+    if (!st.arena.coherent || st.arena.bytes < sl.dn + 64)
+        return fail(c, HSC_EINVAL, "small batch marshalled outside the small stage");
+    std::swap(sl.io, st.arena);
     HIPCHK(c, c->small_blocks.ensure(64 * hsc_ctx::kSmallSlots));
     hipStream_t s = c->stream;
     if (!c->small_blocks_zeroed) {
@@ -2794,7 +2808,6 @@ static int small_launch(hsc_ctx *c, Stage &st)
         c->small_blocks_zeroed = true;
     }
     uint8_t *io = sl.io.as<uint8_t>(), *dio = (uint8_t *)sl.io.dp;
-    if (st.L.total) memcpy(io, st.arena.p, st.L.total);
     memset(io + sl.vo, 0, st.n_txn);
     sl.forced.assign(st.forced.as<uint8_t>(), st.forced.as<uint8_t>() + st.n_txn);
     volatile uint32_t *done = (volatile uint32_t *)(io + sl.dn);
@@ -2887,7 +2900,8 @@ static int check_src(hsc_ctx *c, const Src &src, int *rc_out,
     const int nchunks = T >= 2 * kPipeTxns ? (T + kPipeTxns - 1) / kPipeTxns : 1;
     const int per = std::max(1, (T + nchunks - 1) / nchunks);
     if (nchunks == 1 && small_path(c, T)) {
-        Stage &st = c->stage[0];
+        Stage &st = c->small_st;
+        st.coh = true;
         const auto t0 = SteadyClock::now();
         int rc = marshal_into(c, src, 0, T, st);
         if (rc == HSC_OK && st.n <= kSmallMaxRanges && st.n_lock <= kSmallMaxRanges) {
@@ -2996,6 +3010,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
     if (!c) return;
     if (c->host_only) {
         for (Stage &st : c->stage) st.release();
+    c->small_st.release();
         delete c;
         return;
     }
@@ -3022,6 +3037,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
                     &c->w_tcode2, &c->w_trecs};
     for (DBuf *b : bufs) b->release();
     for (Stage &st : c->stage) st.release();
+    c->small_st.release();
     for (auto &sl : c->small) sl.io.release();
     c->small_blocks.release();
     for (DBuf *b : {&c->d_dgid[0], &c->d_dgid[1], &c->d_dwords[0], &c->d_dwords[1], &c->d_dlsn[0],
@@ -3736,7 +3752,9 @@ static int check_batch(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, 
                        unsigned int *offset, int regop_only, int n, int *rc_out)
 {
     if (!c || n < 0 || (n && (!ranges || !rc_out)) || (!file) != (!offset)) return HSC_EINVAL;
+    const auto tl0 = SteadyClock::now();
     std::unique_lock<std::mutex> lk(c->mu);  // a small batch drops it while its kernel runs
+    c->sm_lock_ns.fetch_add(ns_since(tl0), std::memory_order_relaxed);
     if (!c->host_only) (void)hipSetDevice(c->device);
     int rc = ensure_built(c);
     if (rc) {
@@ -3787,6 +3805,7 @@ int hsc_small_stats(hsc_ctx *c, hsc_small_stats_t *out)
     out->launch_ns = c->sm_launch_ns.load();
     out->wait_ns = c->sm_wait_ns.load();
     out->slot_waits = c->sm_slot_waits.load();
+    out->lock_ns = c->sm_lock_ns.load();
     return HSC_OK;
 }
 

@@ -409,10 +409,11 @@ hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const D
                                uint32_t seq, hipStream_t s)
 {
     // one pass of kNP ranges per 16-lane group, at most one block per CU
+    // (two with appended rows pending: one per half of the grid)
     const size_t per_block = (kSmallThreads / 16) * kNP;
     const size_t work = std::max<size_t>({(p.n + per_block - 1) / per_block,
                                           (p.n_lock + kSmallThreads - 1) / kSmallThreads, 1});
-    const size_t blocks = std::min<size_t>(work, 128) * (d.n || d2.n ? 2 : 1);
+    const size_t blocks = std::min<size_t>(work, 256) * (d.n || d2.n ? 2 : 1);
     k_small_narrow<<<(unsigned)blocks, kSmallThreads, 0, s>>>(nv, d, d2, p, verdict, blocks_done,
                                                                done, seq);
     return hipGetLastError();

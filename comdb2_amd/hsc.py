@@ -118,12 +118,12 @@ class Marshalled(C.Structure):
 
 class CollectorStats(C.Structure):
     _fields_ = [("calls", C.c_uint64), ("batches", C.c_uint64), ("max_batch", C.c_uint64),
-                ("busy_ns", C.c_uint64)]
+                ("busy_ns", C.c_uint64), ("gate_ns", C.c_uint64), ("handout_ns", C.c_uint64)]
 
 
 class SmallStats(C.Structure):
     _fields_ = [("calls", C.c_uint64), ("marshal_ns", C.c_uint64), ("launch_ns", C.c_uint64),
-                ("wait_ns", C.c_uint64), ("slot_waits", C.c_uint64)]
+                ("wait_ns", C.c_uint64), ("slot_waits", C.c_uint64), ("lock_ns", C.c_uint64)]
 
 
 class ConcurrentResult(C.Structure):
@@ -634,13 +634,14 @@ class Validator:
 
     def small_stats(self) -> dict:
         """Small-batch path phase totals (hsc_small_stats): calls and the mean
-        host marshal, slot copy + launch and done-word wait per call (us)."""
+        host marshal, slot launch and done-word wait per call (us), and the
+        mean wait for the context lock per hip_serial_check_batch call."""
         st = SmallStats()
         self._chk(self.lib.hsc_small_stats(self.ctx, C.byref(st)), "hsc_small_stats")
         n = max(1, st.calls)
         return {"calls": st.calls, "marshal_us": st.marshal_ns / 1e3 / n,
                 "launch_us": st.launch_ns / 1e3 / n, "wait_us": st.wait_ns / 1e3 / n,
-                "slot_waits": st.slot_waits}
+                "slot_waits": st.slot_waits, "lock_us": st.lock_ns / 1e3 / n}
 
     def concurrent_check(self, arrs, nthreads: int, rounds: int = 1, regop_only: int = 0,
                          collect: bool = True, max_batch: int = 0, max_wait_us: int = 0,
@@ -678,7 +679,9 @@ class Validator:
                 st.update(batches=cs.batches, max_batch=cs.max_batch,
                           mean_batch=cs.calls / max(1, cs.batches),
                           device_pass_us=cs.busy_ns / 1e3 / max(1, cs.batches),
-                          busy_frac=cs.busy_ns / 1e9 / max(res.seconds, 1e-9))
+                          busy_frac=cs.busy_ns / 1e9 / max(res.seconds, 1e-9),
+                          gate_us=cs.gate_ns / 1e3 / max(1, cs.batches),
+                          handout_us=cs.handout_ns / 1e3 / max(1, cs.batches))
             sm = SmallStats()
             self._chk(self.lib.hsc_small_stats(self.ctx, C.byref(sm)), "hsc_small_stats")
             k = sm.calls - sm0.calls
@@ -687,7 +690,8 @@ class Validator:
                                     "marshal_us": (sm.marshal_ns - sm0.marshal_ns) / 1e3 / k,
                                     "launch_us": (sm.launch_ns - sm0.launch_ns) / 1e3 / k,
                                     "wait_us": (sm.wait_ns - sm0.wait_ns) / 1e3 / k,
-                                    "slot_waits": sm.slot_waits - sm0.slot_waits}
+                                    "slot_waits": sm.slot_waits - sm0.slot_waits,
+                                    "lock_us": (sm.lock_ns - sm0.lock_ns) / 1e3 / k}
         finally:
             if collect:
                 self.lib.hsc_collector_destroy(col)

@@ -400,6 +400,8 @@ typedef struct hsc_collector_stats {
     uint64_t batches;    /* device passes run for them */
     uint64_t max_batch;  /* largest batch */
     uint64_t busy_ns;    /* time inside the batches' device passes */
+    uint64_t gate_ns;    /* leaders waiting for a device pass to end (in-flight bound) */
+    uint64_t handout_ns; /* leaders waking their batches' callers */
 } hsc_collector_stats;
 /* Small-batch path (batches of <= 1024 read sets over a narrow window: one
  * k_small_narrow launch over fine-grained host memory) phase totals since
@@ -409,6 +411,7 @@ typedef struct hsc_collector_stats {
 typedef struct hsc_small_stats_t {
     uint64_t calls, marshal_ns, launch_ns, wait_ns;
     uint64_t slot_waits; /* launches that found every slot in flight */
+    uint64_t lock_ns;    /* hip_serial_check_batch calls (any path) waiting for the context lock */
 } hsc_small_stats_t;
 int hsc_small_stats(hsc_ctx *ctx, hsc_small_stats_t *out);
 int hsc_collector_create(hsc_ctx *ctx, int max_batch, int max_wait_us, hsc_collector **out);

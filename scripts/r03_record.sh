@@ -34,4 +34,11 @@ python3 scripts/benchsum.py gpurun_out/${T}_config3.log
 run config5 700 python3 bench.py --config 5 --check
 python3 scripts/benchsum.py gpurun_out/${T}_config5.log
 run config1 400 python3 bench.py --config 1
+# the N > 1 path rehearsed with two ranks on this one GPU (gloo barrier and
+# max-over-ranks; the 8-GPU node runs are the driver's)
+for cfg in 2 5; do
+  HSC_BENCH_BACKEND=gloo run dist2_c$cfg 400 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+    --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --config $cfg --no-cpu --no-pmc --no-api
+  python3 scripts/benchsum.py gpurun_out/${T}_dist2_c$cfg.log
+done
 echo record done

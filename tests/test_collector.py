@@ -46,6 +46,22 @@ def test_collector_bounds_batches(host, oracle_mod):
     arrs.close()
 
 
+@pytest.mark.parametrize("max_batch,inflight", [(5, 3), (1, 1), (64, 4)])
+def test_collector_many_threads_cut_batches(host, oracle_mod, max_batch, inflight):
+    # 128 callers on the container's few CPUs, batches cut by max_batch
+    # without a gather window: the requests left queued move to the next
+    # batch's wait word and elect its leader
+    log, rs = random_case(77, n_txn=500)
+    host.ingest_log(log)
+    want, _, _ = oracle_mod.check(log, rs, regop_only=1)
+    arrs = NativeCurRangeArrs(rs)
+    got, st = host.concurrent_check(arrs, 128, rounds=4, regop_only=1, max_batch=max_batch,
+                                    inflight=inflight)
+    np.testing.assert_array_equal(got != 0, want != 0)
+    assert st["calls"] == 4 * rs.ntxn and st["max_batch"] <= max_batch
+    arrs.close()
+
+
 def test_full_checks_fail_closed_without_device(host):
     # a host-only context cannot run the join: every full check answers 1
     # (errors are "not serializable"), through the collector as directly
