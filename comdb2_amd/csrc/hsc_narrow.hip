@@ -950,6 +950,7 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
     // complete, then go to their tile-sorted places in the chunk's area
     uint4 R0[S][K], R1[S][K];
     uint32_t RT[S][K];
+    uint64_t SS[S][K];  // kSort, ranks through the commit directory: the snapshots, ranked after the loop
     auto load = [&](int s, int buf) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -1020,6 +1021,11 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
         if (nt.rank_lsn32) {
 #pragma unroll
             for (int k = 0; k < K; ++k) rs[k] = lsn32_rank(snap[cb][k], nt.rank_base);
+        } else if constexpr (kSort) {
+            // the records stay in registers: every sub-chunk's heads are
+            // searched together after the loop (one directory walk, not S)
+#pragma unroll
+            for (int k = 0; k < K; ++k) rs[k] = 0, SS[s][k] = snap[cb][k];
         } else {
             const uint64_t le_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
             bool head[K];
@@ -1138,6 +1144,50 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
             dmax[k] = dfr.x[k] <= dfr.y[k] ? tiles_max(wt, dfr.x[k], dfr.y[k]) : 0;
     } else {
         loc_defer_run<K>(wt, p, dfr, verdict);
+    }
+    if constexpr (kSort) {
+        if (!nt.rank_lsn32) {  // the chunk's snapshot ranks: heads of all sub-chunks in one list
+            const uint64_t le_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
+            bool head[S][K];
+            uint32_t slot[S][K];
+            uint32_t H = 0;
+#pragma unroll
+            for (int s = 0; s < S; ++s)
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const uint64_t prev = __shfl_up(SS[s][k], 1, 64);
+                    head[s][k] = lane == 0 || prev != SS[s][k];
+                    const uint64_t m = __ballot(head[s][k]);
+                    slot[s][k] = H + __popcll(m & le_mask) - 1;  // this lane's head
+                    H += __popcll(m);
+                }
+            for (uint32_t b0 = 0; b0 < H; b0 += 64) {
+#pragma unroll
+                for (int s = 0; s < S; ++s)
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        if (head[s][k] && slot[s][k] - b0 < 64) sb[slot[s][k] - b0] = SS[s][k];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const bool act[1] = {lane < H - b0};
+                const uint64_t xs[1] = {act[0] ? dir_le(sb[lane]) : 0};
+                uint32_t r[1];
+                dir16_count<1>(nt.cdir, cdir, xs, act, r);
+                rb[lane] = r[0];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+                for (int s = 0; s < S; ++s)
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        if (slot[s][k] - b0 < 64) R0[s][k].w = R1[s][k].w = rb[slot[s][k] - b0];
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            }
+        }
     }
     HSC_STAMP(work, 0, 2);
     // table locks: any write to a locked table after the snapshot
