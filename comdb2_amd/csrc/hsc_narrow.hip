@@ -994,13 +994,17 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
     for (int s = 0; s < S; ++s) {
         const int cb = s & 1;
         // 1. the previous sub-chunk's whole-tile checks: their loads are
-        //    younger than this sub-chunk's probe loads, which are needed now
+        //    younger than this sub-chunk's probe loads, which are needed now;
+        //    kSort compares them at the end of this sub-chunk (the loads
+        //    overlap its LDS work)
+        uint64_t pm[K], psn[K];
         if (s > 0) {
             if constexpr (kSort) {  // the read sets are in registers
 #pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if (dfr.x[k] <= dfr.y[k] && tiles_max(wt, dfr.x[k], dfr.y[k]) > dfr.snap[k])
-                        verdict[RT[s - 1][k]] = 1;
+                for (int k = 0; k < K; ++k) {
+                    pm[k] = dfr.x[k] <= dfr.y[k] ? tiles_max(wt, dfr.x[k], dfr.y[k]) : 0;
+                    psn[k] = dfr.snap[k];
+                }
             } else {
                 loc_defer_run<K>(wt, p, dfr, verdict);
             }
@@ -1132,6 +1136,13 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
             } else {
                 if (r0.x & kHasSecond) nt.code2[q] = r1;
                 nt.code[q] = r0;
+            }
+        }
+        if constexpr (kSort) {  // step 1's compares (pm = 0 where there was no check)
+            if (s > 0) {
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (pm[k] > psn[k]) verdict[RT[s - 1][k]] = 1;
             }
         }
     }
