@@ -28,12 +28,26 @@ namespace {
 // merge-path diagonal) names the source row, so a wave writes 64 consecutive
 // rows and takes their 64-row LSN maximum with it (no second pass).  Block 0
 // also copies the table maxima staged with the rows (nt of them) into place.
+// kStage: a lives in the host's pinned staging (a commit's few rows, no
+// upload): every block first copies it into LDS, and the searches read that.
+template <bool kStage>
 __global__ void k_delta_merge(DeltaView d, DeltaView a, uint32_t *ogid, uint64_t *owords,
                               uint64_t *olsn, size_t ostride, uint64_t *bmax,
                               const uint64_t *tmax_src, uint64_t *tmax_dst, uint32_t nt)
 {
     if (blockIdx.x == 0)
         for (uint32_t t = threadIdx.x; t < nt; t += blockDim.x) tmax_dst[t] = tmax_src[t];
+    if constexpr (kStage) {
+        extern __shared__ __attribute__((aligned(16))) uint64_t sa[];  // words [W][n], lsn [n], gid [n]
+        const uint32_t k = a.n;
+        uint64_t *sw = sa, *sl = sa + (size_t)a.W * k;
+        uint32_t *sg = (uint32_t *)(sl + k);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)a.W * k; i += blockDim.x)
+            sw[i] = a.words[(size_t)(i / k) * a.stride + i % k];
+        for (uint32_t i = threadIdx.x; i < k; i += blockDim.x) sl[i] = a.lsn[i], sg[i] = a.gid[i];
+        __syncthreads();
+        a.words = sw, a.lsn = sl, a.gid = sg, a.stride = k;
+    }
     const uint32_t n = d.n + a.n;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t lv = 0;
@@ -81,12 +95,20 @@ __global__ __launch_bounds__(256) void k_probe_delta(DeltaView d, ProbeView p, u
 
 hipError_t delta_merge(const DeltaView &d, const DeltaView &a, uint32_t *ogid, uint64_t *owords,
                        uint64_t *olsn, size_t ostride, uint64_t *bmax, hipStream_t s,
-                       const uint64_t *tmax_src, uint64_t *tmax_dst, uint32_t nt)
+                       const uint64_t *tmax_src, uint64_t *tmax_dst, uint32_t nt, bool stage_a)
 {
     const uint32_t n = d.n + a.n;
     if (n == 0 && nt == 0) return hipSuccess;
-    k_delta_merge<<<std::max(1u, (n + 255) / 256), 256, 0, s>>>(d, a, ogid, owords, olsn, ostride,
-                                                                 bmax, tmax_src, tmax_dst, nt);
+    const uint32_t blocks = std::max(1u, (n + 255) / 256);
+    if (stage_a) {
+        if (a.n > kDeltaStageRows) return hipErrorInvalidValue;
+        const size_t lds = (8 * (size_t)a.W + 8 + 4) * a.n + 16;
+        k_delta_merge<true><<<blocks, 256, lds, s>>>(d, a, ogid, owords, olsn, ostride, bmax, tmax_src,
+                                                     tmax_dst, nt);
+    } else {
+        k_delta_merge<false><<<blocks, 256, 0, s>>>(d, a, ogid, owords, olsn, ostride, bmax, tmax_src,
+                                                    tmax_dst, nt);
+    }
     return hipGetLastError();
 }
 

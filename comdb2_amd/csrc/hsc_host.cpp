@@ -462,7 +462,8 @@ static int app_stage(hsc_ctx *c, size_t bytes)
     const int i = c->app_i;
     if (c->app_ev[i] && hipEventSynchronize(c->app_ev[i]) != hipSuccess)
         return fail(c, HSC_EDEVICE, "append staging event");
-    if (c->h_appq[i].ensure(bytes, true)) return fail(c, HSC_ENOMEM, "append staging");
+    // fine-grained and mapped: a commit's few rows are read in place by the merge
+    if (c->h_appq[i].ensure(bytes, true, true)) return fail(c, HSC_ENOMEM, "append staging");
     c->h_app = &c->h_appq[i];
     return HSC_OK;
 }
@@ -1275,9 +1276,15 @@ static int flush_appends(hsc_ctx *c)
     // one upload: rows, then the table maxima the merge kernel copies out
     const size_t woff = (4 * k + 15) & ~(size_t)15;
     const size_t sb = stage_bytes(k, W, nt);
-    HIPCHK(c, c->d_agid.ensure(sb));
-    HIPCHK(c, hipMemcpyAsync(c->d_agid.p, c->h_app->p, sb, hipMemcpyHostToDevice, s));
-    uint8_t *db = c->d_agid.as<uint8_t>();
+    // a commit's rows (at most kDeltaStageRows) stay in the mapped staging,
+    // the merge reads them there; more are uploaded first
+    const bool in_place = k <= kDeltaStageRows && c->h_app->coherent;
+    uint8_t *db = (uint8_t *)c->h_app->dp;
+    if (!in_place) {
+        HIPCHK(c, c->d_agid.ensure(sb));
+        HIPCHK(c, hipMemcpyAsync(c->d_agid.p, c->h_app->p, sb, hipMemcpyHostToDevice, s));
+        db = c->d_agid.as<uint8_t>();
+    }
     // both run buffers at full size for the window's words: merges never
     // reallocate a run holding rows (a wider key schedules a rebuild above)
     const size_t wbytes = 8 * (size_t)W * kDeltaCap;
@@ -1303,7 +1310,7 @@ static int flush_appends(hsc_ctx *c)
     HIPCHK(c, delta_merge(d, a, c->d_dgid[o].as<uint32_t>(), c->d_dwords[o].as<uint64_t>(),
                           c->d_dlsn[o].as<uint64_t>(), c->dcap, c->d_dbmax.as<uint64_t>(), s,
                           nt ? a.lsn + k : nullptr, nt ? c->d_table_max.as<uint64_t>() : nullptr,
-                          (uint32_t)nt));
+                          (uint32_t)nt, in_place));
     if (nt) c->app_tmax = false;
     // no wait: the ring keeps h_app until its copies ran, and every later use
     // of the run is on this stream (hsc_set_stream orders a new stream after it)

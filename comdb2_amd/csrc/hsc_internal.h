@@ -356,7 +356,11 @@ constexpr uint32_t kDeltaCap = 1u << 16;  // delta rows before a merge into the 
 hipError_t delta_merge(const DeltaView &d, const DeltaView &a, uint32_t *ogid, uint64_t *owords,
                        uint64_t *olsn, size_t ostride, uint64_t *bmax, hipStream_t s,
                        const uint64_t *tmax_src = nullptr, uint64_t *tmax_dst = nullptr,
-                       uint32_t nt = 0);
+                       uint32_t nt = 0, bool stage_a = false);
+// stage_a: a (at most kDeltaStageRows rows) is read from mapped pinned host
+// memory, each merge block copying it into LDS first (a commit's rows need no
+// upload)
+constexpr uint32_t kDeltaStageRows = 256;
 // flags[txn] = 1 for every range probe with a delta row of its group in
 // [lo, hi] committed after its snapshot (raw W-word bounds)
 hipError_t launch_probe_delta(const DeltaView &d, const ProbeView &p, uint8_t *flags, hipStream_t s);
