@@ -1,6 +1,8 @@
 #!/bin/bash
 # Locate changes: narrow / full-config parity tests, locate phase stamps
-# (configs 2 and 5, one stream), config 5 and config 2 benches.
+# (configs 2 and 5, one stream), config 5 and config 2 benches.  Needs the
+# diagnostic build first (here, on the CPU):
+#   make -C comdb2_amd/csrc OUT=../lib/diag/stamps.so BUILD=build_stamps EXTRA=-DHSC_STAMPS
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 T=${TAG:-r03y}
