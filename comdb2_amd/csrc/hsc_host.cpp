@@ -32,363 +32,8 @@
 
 using namespace hsc;
 
-namespace {
+#include "hsc_ctx.h"
 
-struct GroupInfo {
-    int tid, ix, klen;
-};
-
-inline uint64_t load_be64(const uint8_t *b)
-{
-    uint64_t v = 0;
-    for (int i = 0; i < 8; ++i) v = (v << 8) | b[i];
-    return v;
-}
-
-inline uint64_t ixkey(int tid, int ix) { return ((uint64_t)(uint32_t)tid << 32) | (uint32_t)ix; }
-
-// Host staging buffer: pinned (hipHostMalloc) on a device context, so that
-// uploads and verdict downloads are DMA from / to it; malloc on a host-only
-// one.  Grows, never shrinks.
-struct HBuf {
-    void *p = nullptr;
-    void *dp = nullptr;  // coherent buffers: the device's address of p
-    size_t bytes = 0;
-    bool pinned = false, coherent = false;
-    // 0 or -1 (out of memory).  coherent: fine-grained pinned memory the GPU
-    // maps (kernels read and write it directly, the host sees their
-    // system-scope stores while they run).
-    int ensure(size_t want, bool pin, bool coh = false)
-    {
-        if (want <= bytes && pin == pinned && coh == coherent) return 0;
-        release();
-        const size_t b = want + want / 8 + 256;
-        if (pin) {
-            const unsigned flags = coh ? hipHostMallocMapped | hipHostMallocCoherent : hipHostMallocDefault;
-            if (hipHostMalloc(&p, b, flags) != hipSuccess) {
-                p = nullptr;
-                return -1;
-            }
-            if (coh && hipHostGetDevicePointer(&dp, p, 0) != hipSuccess) {
-                (void)hipHostFree(p);
-                p = dp = nullptr;
-                return -1;
-            }
-        } else if (!(p = malloc(b))) {
-            return -1;
-        }
-        bytes = b;
-        pinned = pin;
-        coherent = coh && pin;
-        return 0;
-    }
-    void release()
-    {
-        if (p) {
-            if (pinned)
-                (void)hipHostFree(p);
-            else
-                free(p);
-        }
-        p = dp = nullptr;
-        bytes = 0;
-    }
-    template <class T> T *as() const { return (T *)p; }
-};
-
-// One marshalled batch (or pipeline chunk) in host memory: probe SoA,
-// forced verdicts, and the verdict bytes read back.
-// Byte offsets of a marshalled batch's columns inside one staging arena (and
-// the device arena it is uploaded to with ONE copy): a small batch -- the
-// collector's usual tens of read sets -- pays one transfer, not eight.
-struct StageLayout {
-    size_t lo = 0, hi = 0, snap = 0, lock_snap = 0, gid = 0, txn = 0, lock_table = 0,
-           lock_txn = 0, total = 0;
-};
-
-static StageLayout stage_layout(int W, size_t n, size_t nl)
-{
-    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    StageLayout L;
-    size_t o = 0;
-    L.lo = o, o = al(o + 8 * (size_t)W * n);
-    L.hi = o, o = al(o + 8 * (size_t)W * n);
-    L.snap = o, o = al(o + 8 * n);
-    L.lock_snap = o, o = al(o + 8 * nl);
-    L.gid = o, o = al(o + 4 * n);
-    L.txn = o, o = al(o + 4 * n);
-    L.lock_table = o, o = al(o + 4 * nl);
-    L.lock_txn = o, o = al(o + 4 * nl);
-    L.total = o;
-    return L;
-}
-
-// Room a small batch's slot needs past the columns: the verdict bytes and the
-// done word, each 64-byte aligned (hsc_ctx::SmallSlot).
-static size_t small_tail(size_t n_txn) { return 64 + ((n_txn + 63) & ~(size_t)63) + 64; }
-
-struct Stage {
-    HBuf arena, forced, verdict;
-    StageLayout L;
-    size_t n = 0, n_lock = 0, n_txn = 0;
-    // the small-batch stage: its arena is fine-grained pinned memory with room
-    // for the slot's verdicts and done word, and moves into the slot at launch
-    // (the kernel reads the columns where the marshal wrote them)
-    bool coh = false;
-    hipEvent_t done = nullptr;  // the chunk's verdict download
-    template <class T>
-    T *col(size_t off) const
-    {
-        return (T *)((uint8_t *)arena.p + off);
-    }
-    void release()
-    {
-        for (HBuf *b : {&arena, &forced, &verdict}) b->release();
-        if (done) (void)hipEventDestroy(done);
-        done = nullptr;
-    }
-};
-
-constexpr int kMarshalTxns = 2048;         // read sets per marshal work item
-enum { kFoldIdle = 0, kFoldRunning = 1, kFoldDone = 2 };  // hsc_ctx::fold_state
-constexpr int kMarshalParallelMin = 4096;  // fewer read sets: marshal on the caller's thread
-constexpr int kPipeTxns = 32768;           // read sets per pipeline chunk of a large batch
-
-}  // namespace
-
-struct MarshalPart;
-
-// The dictionaries a marshal reads (key words, groups, table ids) as an
-// immutable snapshot: a collector's callers marshal their own read set
-// against it before they queue (premarshal, no context lock), and a batch
-// takes those rows only if the context's dictionary epoch has not moved.
-struct MarshalDict {
-    uint64_t epoch = 0;
-    int W = 1;
-    std::unordered_map<std::string, int> table_ids;
-    std::vector<GroupInfo> groups;
-    std::unordered_map<uint64_t, std::vector<int>> ix_groups;
-};
-
-struct hsc_ctx {
-    int device = 0;
-    bool host_only = false;
-    hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-    std::string err;
-    std::mutex mu;  // one check at a time per context (re-entrant callers queue)
-
-    // dictionaries
-    std::unordered_map<std::string, int> table_ids;
-    std::vector<std::string> table_names;
-    std::unordered_map<uint64_t, int> group_ids;                    // (tid,ix,klen)
-    std::vector<GroupInfo> groups;
-    std::unordered_map<uint64_t, std::vector<int>> ix_groups;       // (tid,ix) -> gids
-    uint64_t dict_epoch = 1;  // bumped when a table, a group or W changes
-    std::shared_ptr<const MarshalDict> dict_snap;  // published under mu
-
-    // host staging of the window (host ingest paths)
-    std::vector<uint32_t> h_gid;
-    std::vector<uint64_t> h_keyoff;
-    std::vector<uint8_t> h_keys;
-    std::vector<uint64_t> h_lsn;
-    std::vector<uint64_t> h_table_max;
-    bool host_staged = true;
-    bool dirty = true;
-    uint64_t end_lsn = 0, max_commit = 0;
-    uint64_t poison_regop = 0;  // max regop LSN whose prev record cannot be read
-    uint64_t poison_chain = 0;  // max commit LSN whose logical chain is broken
-    // the log a log-based window was decoded from (record LSNs for the
-    // DB_SET rule, records for chain walks of txns committed by appends);
-    // table = window table id
-    struct LogStore {
-        std::vector<uint64_t> lsn, prev, key_off;
-        std::vector<uint32_t> rectype;
-        std::vector<int16_t> isabort, ix;
-        std::vector<int32_t> table, keylen;
-        std::vector<uint8_t> keys;
-        void clear()
-        {
-            lsn.clear(), prev.clear(), key_off.clear(), rectype.clear(), isabort.clear();
-            ix.clear(), table.clear(), keylen.clear(), keys.clear();
-        }
-    } lg;
-    bool lg_rule = false;  // every record LSN of the window is in lg (DB_SET rule on)
-    uint64_t last_append_lsn = 0;
-    // incremental window (hsc_delta.hip): writes committed after the last
-    // build, kept on the device as a sorted delta run probed beside the main
-    // window; live = a built window takes appends into the delta
-    bool live = false, merge_pending = false;
-    size_t ng_built = 0;  // groups the per-group device tables were sized for
-    DBuf d_dgid[2], d_dwords[2], d_dlsn[2], d_dbmax;
-    DBuf d_agid;  // an append's upload: rows + table maxima (stage_bytes layout)
-    size_t dn = 0, dcap = 0;
-    int dcur = 0;
-    std::vector<uint32_t> app_gid;   // appended rows not yet on the device
-    std::vector<uint8_t> app_keys;   // their key bytes (klen of the group each)
-    std::vector<uint64_t> app_koff, app_lsn;
-    bool app_tmax = false;           // table maxima changed since the last upload
-    // pinned staging of appended rows / table maxima: a ring of two, each
-    // reused only after the copies that read it ran (its event), so an append
-    // returns without waiting for its upload and delta merge
-    HBuf h_appq[2];
-    hipEvent_t app_ev[2] = {};
-    int app_i = 0;
-    HBuf *h_app = nullptr;          // the buffer of the append being staged
-    hipEvent_t app_last = nullptr;  // recorded behind the last append's device work
-    ProbeView raw_probe{};           // the batch being probed, untransformed (delta probe)
-    // background fold: once the live run holds fold_rows rows it
-    // is frozen, and a shadow context rebuilds the main window from the main
-    // window's versions + the frozen run on its own stream and host thread;
-    // checks probe main + frozen + live runs until a call after the build
-    // swaps the shadow's window in (fold_poll).  fold_bg = false: the run is
-    // merged inline by the next check instead (the pre-fold behaviour).
-    hsc_ctx *shadow = nullptr;
-    std::thread fold_thread;
-    std::atomic<int> fold_state{0};  // kFoldIdle / kFoldRunning / kFoldDone
-    int fold_rc = 0;
-    DBuf f_dgid, f_dwords, f_dlsn, f_dbmax;  // the frozen run (fn rows, stride dcap)
-    size_t fn = 0;
-    size_t fold_rows = kDeltaCap / 2;
-    bool fold_bg = true;
-    hipEvent_t fold_ev = nullptr;  // the old window's last readers (the next fold waits)
-    uint64_t folds_started = 0, folds_swapped = 0, folds_inline = 0;
-    float fold_ms = 0;  // build time of the last background fold
-
-    // device window
-    int W = 1;
-    size_t n = 0, cap = 0;
-    uint32_t ntiles = 0;
-    int log2T = 11, levels = 0;
-    int layout = HSC_LAYOUT_AUTO;  // hsc_set_layout
-    bool narrow = false;           // 64-bit codes + 16-ary index (hsc_narrow.hip)
-    int lw = 0, tz = 0;  // least significant varying limb / its constant low bits
-    DBuf d_nkeys, d_nmaxs, d_nbase;
-    NarrowView nv{};
-    // the narrow window as one-word tile rows (codes) for the tile pipeline
-    WinView wn{};
-    DBuf d_nzero, d_ntmax, d_nsp_g, d_nsp_w, d_ngs, d_nscratch;
-    DBuf p_code_lo, p_code_hi, p_zero;
-    uint32_t probe_ntiles = 0;  // tiles of the view the last probe ran on
-    bool probe_buckets = false; // the last probe ran the narrow tiles (fixed-capacity buckets)
-    // narrow tiles: u32 key deltas + commit ranks (dense batches)
-    bool ntiles32 = false;
-    DBuf d_trad2;  // the other bucket-table mode (narrow_trad_pick)
-    DBuf d_commits, d_cdir, d_tdir, d_trad, d_done, w_vflags, d_key32, d_rank32, d_ctmp[4];
-    Dir16 cdir{}, tdir{};
-    uint32_t trad_m = 0;       // tile bucket table size (0: none)
-    bool trad_log = false;     // the table is in log mode (narrow_trad_pick)
-    uint32_t ncommit = 0;      // distinct commit LSNs in d_commits (built only for the rank directory)
-    bool has_commits = false;  // the window has rows and a commit span (narrow / compact tiles)
-    uint64_t commit_span[2] = {0, 0};  // oldest / newest distinct commit LSN of the window
-    bool rank_lsn32 = false;   // narrow tiles: rows carry lsn - rank_base + 1 (NarrowTiles)
-    bool nt_sorted = true;     // narrow tiles: chunk-sorted records (HSC_NT_SORT=0 at build: scatter)
-    bool nt_fused = false;     // chunk-sorted narrow tiles: plan-free join (HSC_NT_FUSED=1 at build;
-                               // r03: one stream 61.9 -> 60.2 us, two streams 45.3 -> 47.7 us)
-    bool ct_sorted = true;     // compact tiles: chunk-sorted records (HSC_CT_SORT=0 at build: scatter)
-    bool ct_fused = false;     // ... and the plan-free join (HSC_CT_FUSED=1 at build; measured slower)
-    uint64_t rank_base = 0;
-    DBuf w_tcode, w_tcode2, w_trecs;
-    DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;
-    DBuf d_pk[2];              // packed-key sort: the keys, ping-pong (hsc_ingest.hip)
-    bool packed_sort = false;  // the last build sorted packed keys
-    DBuf d_gstart, d_gend, d_tmax, d_table_max, d_group_table, d_count, d_sp_g, d_sp_w;
-    // compact codes of a wide window (hsc_compact.hip): WinView wc over them
-    bool compact = false;
-    CompactTables ct{};
-    WinView wc{};
-    DBuf d_cmask, d_cpat, d_cmv, d_cbits, d_cwords, d_ctmax, d_csp_g, d_csp_w;
-    int ct_maxbits = 0;  // most varying bits of any group
-    // compact tiles (hsc_ctiles.hip): the compact window as gid || code keys
-    bool ctiles = false;
-    CTiles ctv{};
-    DBuf d_ckey, d_crank, d_cfirst, d_crel, d_ctrad, d_ctb;
-
-    // probe workspace
-    DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;
-    DBuf p_arena;  // a staged batch's columns, uploaded in one copy (StageLayout)
-    DBuf p_verdict, p_bitmap;
-    DBuf w_code, w_hist, w_counts, w_bucket, w_cursor, w_items, w_item_tile, w_item_desc, w_recs;
-
-    // marshal output: staging sets (two: a large batch is checked as a
-    // pipeline of chunks, one marshalled while the other is on the GPU),
-    // per-worker parts, host threads
-    hsc_marshalled m{};
-    Stage stage[2];
-    std::vector<MarshalPart> parts;
-    int threads = 1;
-
-    // raw log / wire decode output
-    DecodedLog decoded;
-    PhysStore phys;  // records key reconstruction walks may visit (hsc_logdec.cpp)
-    DecodedReadSets wire;
-
-    // rw conflict pairs: every window version (pre-dedupe rows in d_*2)
-    size_t n_all = 0;
-    DBuf e_span, e_cnt, e_txn, e_lsn, e_txn2, e_lsn2, e_gid, e_scratch, e_flags, e_after;
-    std::vector<uint32_t> e_out_txn;
-    std::vector<uint64_t> e_out_lsn;
-    const uint32_t *e_dev_txn = nullptr;  // the last hsc_rw_edges pairs, on the device
-    const uint64_t *e_dev_lsn = nullptr;
-    size_t e_dev_n = 0;
-
-    // replicant coalesce: device inputs / working arrays, host outputs
-    DBuf co_dev[25];
-    std::vector<int64_t> co_off;
-    std::vector<int32_t> co_i32[7];
-    std::vector<uint64_t> co_u64[2];
-
-    // dependency graph
-    GraphBufs graph;
-    GraphBufs subgraph;  // the graph induced on a cover (sharded SCC)
-    uint32_t graph_ntxn = 0;
-    uint32_t x_max_txn = 0;  // largest txn id a staged rw pair can name (stage_rw_pairs)
-
-    // Probe lanes: the probe scratch above belongs to the active lane; other
-    // lanes park theirs here.  A lane is bound to the stream that last used
-    // it, so batches on different streams never share scratch and can run
-    // concurrently; a lane taken over by another stream first waits for the
-    // lane's last batch (its done event).
-    struct Lane {
-        DBuf b[20];
-        hipStream_t stream = nullptr;
-        hipEvent_t done = nullptr;
-        uint64_t tick = 0;
-    };
-    static constexpr int kLanes = 4;
-    Lane lanes[kLanes];
-    int lane = 0;
-    uint64_t lane_tick = 0;
-
-    // small batches (k_small_narrow): a ring of slots, each with the probe
-    // columns, verdict bytes and done word in fine-grained pinned memory and
-    // its own block counter.  A slot belongs to one call from its launch
-    // (under mu) until that call has read its verdicts (without mu), so a
-    // second call can marshal and launch while the first one's kernel runs.
-    static constexpr int kSmallSlots = 4;
-    struct SmallSlot {
-        HBuf io;
-        std::vector<uint8_t> forced;
-        size_t n_txn = 0, vo = 0, dn = 0;
-        uint32_t seq = 0;
-        std::atomic<bool> busy{false};
-    };
-    SmallSlot small[kSmallSlots];
-    Stage small_st;  // marshal target of the small path (coh: its arena swaps into a slot)
-    uint32_t small_next = 0;
-    DBuf small_blocks;
-    bool small_blocks_zeroed = false;
-    bool no_small = false;  // HSC_NO_SMALL=1 at context creation: the staged path
-    uint32_t small_seq = 0;
-    // small-path phase times (hsc_small_stats)
-    std::atomic<uint64_t> sm_calls{0}, sm_marshal_ns{0}, sm_launch_ns{0}, sm_wait_ns{0},
-        sm_slot_waits{0}, sm_lock_ns{0};
-
-    // timing
-    bool timing = false;
-    hipEvent_t ev[8] = {};
-    hsc_timing last{};
-};
 
 // probe scratch that moves with a lane (hsc_ctx::Lane::b holds at most 20)
 static DBuf hsc_ctx::*const kLaneBufs[] = {
@@ -1239,6 +884,7 @@ static int fold_finish(hsc_ctx *c, bool wait);
 
 static int flush_appends(hsc_ctx *c)
 {
+    if (c->multi) return multi_flush_appends(c);
     if (!c->live || c->host_only) return HSC_OK;
     hipStream_t s = c->stream;
     HIPCHK_RC(c, fold_finish(c, false));
@@ -1566,6 +1212,10 @@ static void fold_discard(hsc_ctx *c)
 
 static int ensure_built(hsc_ctx *c)
 {
+    if (c->multi) {  // the window lives on the member contexts (hsc_multi.cpp)
+        if (!c->dirty && c->groups.size() <= c->ng_built) return HSC_OK;
+        return multi_build(c);
+    }
     if (c->host_only) {  // dictionaries + marshalling only
         set_words(c, window_words(c));
         return HSC_OK;
@@ -1762,31 +1412,6 @@ static int regop_rc(hsc_ctx *c, uint64_t S)
     if (c->lg_rule && !std::binary_search(c->lg.lsn.begin(), c->lg.lsn.end(), S)) return 1;
     return (c->max_commit > S || c->poison_regop > S) ? 1 : 0;
 }
-
-// One table of a read set: islocked of its first range (db/sqlglue.c:322-326)
-// and its index spans [b, e] in array order (:327-349), spans[s0 .. s0 + ns).
-struct TxnTable {
-    int tid, islocked, s0, ns;
-};
-struct IdxSpan {
-    int idx, b, e;
-};
-
-// One worker's share of a marshal (read sets [t0, t1) of the batch): probes
-// as AoS rows (W words of lo, W of hi) plus the scratch of the span builder.
-struct MarshalPart {
-    std::vector<uint64_t> lohi;  // [n][2W]
-    std::vector<uint64_t> snap, lock_snap;
-    std::vector<uint32_t> gid, txn, lock_table, lock_txn;
-    std::vector<TxnTable> tabs;
-    std::vector<IdxSpan> spans;
-    size_t out0 = 0, lock0 = 0;  // output offsets (assembly)
-    void clear()
-    {
-        lohi.clear(), snap.clear(), lock_snap.clear(), gid.clear(), txn.clear();
-        lock_table.clear(), lock_txn.clear();
-    }
-};
 
 template <class D, class Get>  // D: hsc_ctx or a MarshalDict snapshot
 static void marshal_txn(const D *c, MarshalPart &mp, uint32_t txn, uint64_t S, int nr, Get get)
@@ -2050,7 +1675,8 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
     const int per = std::max(1, std::min(kMarshalTxns, (nt + c->threads - 1) / std::max(1, c->threads)));
     const int nwork = std::max(1, (nt + per - 1) / per);
     if ((int)c->parts.size() < nwork) c->parts.resize(nwork);
-    if (st.forced.ensure((size_t)std::max(nt, 1), !c->host_only)) return fail(c, HSC_ENOMEM, "staging");
+    const bool pin = !c->host_only || c->multi;  // a multi context uploads from it
+    if (st.forced.ensure((size_t)std::max(nt, 1), pin)) return fail(c, HSC_ENOMEM, "staging");
     uint8_t *forced = st.forced.as<uint8_t>();
     if (nt < kMarshalParallelMin) src.prefetch(t0, t1);
     par_for(nt >= kMarshalParallelMin ? c->threads : 1, nwork, [&](int w) {
@@ -2075,7 +1701,6 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
         n += c->parts[w].gid.size();
         nl += c->parts[w].lock_table.size();
     }
-    const bool pin = !c->host_only;
     st.L = stage_layout(W, n, nl);
     if (st.arena.ensure(std::max<size_t>(st.L.total + (st.coh ? small_tail((size_t)nt) : 0), 256), pin,
                         st.coh && pin))
@@ -2902,6 +2527,10 @@ template <class Src>
 static int check_src(hsc_ctx *c, const Src &src, int *rc_out,
                      std::unique_lock<std::mutex> *lk = nullptr)
 {
+    if (c->multi) {  // the members' routed pipeline (hsc_multi.cpp)
+        const int rc = marshal_into(c, src, 0, src.ntxn(), c->stage[0]);
+        return rc ? rc : multi_check_stage(c, c->stage[0], rc_out);
+    }
     if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
     const int T = src.ntxn();
     const int nchunks = T >= 2 * kPipeTxns ? (T + kPipeTxns - 1) / kPipeTxns : 1;
@@ -3003,7 +2632,7 @@ int hsc_ctx_create(int device, hsc_ctx **out)
         if (warmed.size() < (size_t)n) warmed.resize(n, false);
         if (!warmed[device]) {
             for (auto f : {warm_kernels, warm_ingest, warm_narrow, warm_ctiles, warm_delta,
-                           warm_compact, warm_coalesce, warm_edges, warm_graph})
+                           warm_compact, warm_coalesce, warm_edges, warm_graph, warm_route})
                 (void)f();
             warmed[device] = true;
         }
@@ -3015,6 +2644,7 @@ int hsc_ctx_create(int device, hsc_ctx **out)
 void hsc_ctx_destroy(hsc_ctx *c)
 {
     if (!c) return;
+    if (c->multi) multi_destroy(c);  // the members first; the front is host-only
     if (c->host_only) {
         for (Stage &st : c->stage) st.release();
     c->small_st.release();
@@ -3255,9 +2885,11 @@ int hsc_window_build(hsc_ctx *c)
 int hsc_register_group(hsc_ctx *c, const char *tbname, int idxnum, int keylen)
 {
     if (!c || !tbname || keylen < 0 || keylen > kMaxWords * 8) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::mutex> lk(c->mu);
     int tid = table_id_or_add(c, tbname);
-    return group_id_or_add(c, tid, idxnum, keylen);
+    const int g = group_id_or_add(c, tid, idxnum, keylen);
+    if (c->multi) multi_sync_dict(c);  // members keep the same table ids and gids
+    return g;
 }
 
 int hsc_window_ingest_device(hsc_ctx *c, size_t n, int words, const uint32_t *gid,
@@ -3360,6 +2992,12 @@ int hsc_merge_table_max(hsc_ctx *c, const uint64_t *in, int n)
         c->h_table_max[t] = std::max(c->h_table_max[t], in[t]);
         c->max_commit = std::max(c->max_commit, in[t]);
     }
+    if (c->multi)
+        for (int m = 0; m < hsc_multi_local(c); ++m) {
+            hsc_ctx *mc = hsc_multi_member(c, m);
+            const int rc = hsc_merge_table_max(mc, in, std::min(n, (int)mc->table_names.size()));
+            if (rc) return fail(c, rc, "merge_table_max: member");
+        }
     if (!c->host_only && !c->dirty && n > 0) {
         (void)hipSetDevice(c->device);
         HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, c->h_table_max.data(), 8 * (size_t)n,
@@ -4217,3 +3855,18 @@ int hsc_dep_graph_edges(hsc_ctx *c, uint32_t *src, uint32_t *dst, uint32_t *type
 }
 
 }  // extern "C"
+
+// ---- internals the multi-GPU context drives its members with (hsc_ctx.h) ----
+namespace hsc {
+int ctx_fail(hsc_ctx *c, int code, const char *what, hipError_t e) { return fail(c, code, what, e); }
+int ctx_window_words(hsc_ctx *c) { return window_words(c); }
+void ctx_clear_window(hsc_ctx *c) { clear_window(c); }
+int ctx_ensure_built(hsc_ctx *c) { return ensure_built(c); }
+void ctx_add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keylen, bool has_key, uint64_t lsn)
+{
+    add_write(c, tid, ix, key, keylen, has_key, lsn);
+}
+int ctx_flush_appends(hsc_ctx *c) { return flush_appends(c); }
+int ctx_probe(hsc_ctx *c, const hsc_probe_batch *b) { return probe(c, b); }
+int ctx_default_threads() { return default_threads(); }
+}  // namespace hsc

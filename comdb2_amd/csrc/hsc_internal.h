@@ -614,6 +614,55 @@ bool premarshal(hsc_ctx *c, const hsc_currangearr *a, uint64_t S, PreMarshal *pm
 int check_batch_pre(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, unsigned int *file,
                     unsigned int *offset, int n, int *rc_out);
 
+// Multi-GPU routing (hsc_route.hip, hsc_multi.cpp): the window cut into
+// world <= kMultiMax contiguous pieces of the composite key space (gid, key
+// words) at world - 1 ascending splitters.
+constexpr int kMultiMax = 16;
+struct RouteSplit {
+    const uint32_t *gid;  // [S]
+    const uint64_t *w;    // [W][S]
+    int S, W;
+};
+// Where a destination's rows go: probe columns with a row stride, and (member
+// 0 only) the table-lock columns.
+struct RouteTarget {
+    uint64_t *lo, *hi, *snap;
+    uint32_t *gid, *txn;
+    size_t stride;
+    uint64_t *lock_snap;
+    uint32_t *lock_table, *lock_txn;
+};
+struct RouteArgs {
+    RouteTarget t[kMultiMax];
+    int N;
+    uint32_t tbase;      // added to every read-set number (the batch-wide numbering)
+    uint32_t lock_base;  // this source's first row in member 0's lock columns
+};
+// Received send blocks (RCCL): source s's block at byte boff[s], n[s] probes
+// and nl[s] locks; rows [roff[s], roff[s + 1]) / locks [loff[s], loff[s + 1]).
+struct RouteUnpack {
+    uint64_t boff[kMultiMax];
+    uint32_t n[kMultiMax], nl[kMultiMax], roff[kMultiMax + 1], loff[kMultiMax + 1];
+    int N;
+};
+struct RouteParts {
+    const uint64_t *p[kMultiMax];
+    int n;
+};
+// bytes of one send block: probe columns lo[W] hi[W] snap, gid txn; locks
+__host__ __device__ inline size_t route_block_bytes(int W, size_t n, size_t nl)
+{
+    return 8 * (size_t)(2 * W + 2) * n + 16 * nl;
+}
+uint32_t route_blocks(size_t n);  // chunks (hist rows) of a routed batch
+hipError_t launch_route_count(const ProbeView &p, const RouteSplit &sp, int N, uint32_t *hist,
+                              uint32_t *totals, hipStream_t s);
+hipError_t launch_route_scatter(const ProbeView &p, const RouteSplit &sp, const RouteArgs &a,
+                                const uint32_t *hist, uint32_t *cursor, hipStream_t s);
+hipError_t launch_route_unpack(const uint8_t *raw, const RouteUnpack &u, const RouteTarget &t, int W,
+                               hipStream_t s);
+hipError_t launch_or_slices(const RouteParts &parts, size_t words, uint64_t *out, hipStream_t s);
+
 // per-file code-object warm-up (hsc_ctx_create)
 hipError_t warm_kernels();
 hipError_t warm_ingest();
@@ -624,5 +673,6 @@ hipError_t warm_compact();
 hipError_t warm_coalesce();
 hipError_t warm_edges();
 hipError_t warm_graph();
+hipError_t warm_route();
 
 }  // namespace hsc

@@ -151,7 +151,11 @@ EXPORTS = [
     "hsc_collector_check", "hsc_collector_get_stats", "hsc_collector_set_inflight",
     "hsc_small_stats", "hsc_harness_concurrent",
     "hsc_dep_graph_build", "hsc_dep_graph_stage_rw_pairs", "hsc_dep_graph_scc_built", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
+    "hsc_multi_create", "hsc_multi_unique_ids", "hsc_multi_create_rank", "hsc_multi_world",
+    "hsc_multi_rank", "hsc_multi_local", "hsc_multi_member", "hsc_multi_set_splitters",
+    "hsc_multi_adopt", "hsc_multi_probe_device", "hsc_multi_stats", "hsc_multi_last_counts",
 ]
+MULTI_ID_BYTES = 2 * 128  # hsc_multi_unique_ids: one RCCL id per lane
 
 (LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES,
  LAYOUT_NARROW_CODES, LAYOUT_COMPACT, LAYOUT_COMPACT_WIDE) = 0, 1, 2, 3, 4, 5, 6, 7
@@ -243,6 +247,18 @@ def load() -> C.CDLL:
                                              C.c_int, C.POINTER(C.c_int),
                                              C.POINTER(ConcurrentResult)]),
         "hsc_window_layout": (C.c_int, [_p]),
+        "hsc_multi_create": (C.c_int, [C.POINTER(C.c_int), C.c_int, ctx_pp]),
+        "hsc_multi_unique_ids": (C.c_int, [_p, C.c_size_t]),
+        "hsc_multi_create_rank": (C.c_int, [C.c_int, C.c_int, C.c_int, _p, C.c_size_t, ctx_pp]),
+        "hsc_multi_world": (C.c_int, [_p]),
+        "hsc_multi_rank": (C.c_int, [_p]),
+        "hsc_multi_local": (C.c_int, [_p]),
+        "hsc_multi_member": (_p, [_p, C.c_int]),
+        "hsc_multi_set_splitters": (C.c_int, [_p, C.c_size_t, _p, _p, C.c_int]),
+        "hsc_multi_adopt": (C.c_int, [_p]),
+        "hsc_multi_probe_device": (C.c_int, [_p, _p, C.c_int]),
+        "hsc_multi_stats": (C.c_int, [_p, _p]),
+        "hsc_multi_last_counts": (C.c_int, [_p, _p, C.c_int]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("HSC_LIB"):
@@ -898,6 +914,104 @@ class Validator:
         t = Timing()
         self._chk(self.lib.hsc_get_timing(self.ctx, C.byref(t)), "hsc_get_timing")
         return t.as_dict()
+
+
+class MultiValidator(Validator):
+    """A multi-GPU context (hsc_multi_create / hsc_multi_create_rank): every
+    Validator method that the C ABI allows on a multi context works on it
+    (the drop-in checks, the collector, log ingest / appends); the window is
+    spread over member contexts by composite-key splitters and every batch is
+    routed between them on the GPUs.
+
+    devices: members in this process (a device may repeat: several members on
+    one GPU).  Or rank / world / ids (hsc_multi_unique_ids bytes, identical on
+    every rank) and device: this process is one member of a per-rank context
+    exchanging over RCCL."""
+
+    def __init__(self, devices: Optional[Sequence[int]] = None, rank: Optional[int] = None,
+                 world: Optional[int] = None, ids: Optional[bytes] = None, device: int = 0):
+        self.lib = load()
+        self._keep = None
+        self.ctx = None
+        ctx = _p()
+        if devices is not None:
+            devs = (C.c_int * len(devices))(*devices)
+            rc = self.lib.hsc_multi_create(devs, len(devices), C.byref(ctx))
+            what = f"hsc_multi_create({list(devices)})"
+        else:
+            buf = C.create_string_buffer(bytes(ids), len(ids))
+            rc = self.lib.hsc_multi_create_rank(device, rank, world, buf, len(ids), C.byref(ctx))
+            what = f"hsc_multi_create_rank(device {device}, rank {rank}, world {world})"
+        if rc != HSC_OK:
+            raise HscError(f"{what} = {rc}")
+        self.ctx = ctx
+
+    @staticmethod
+    def unique_ids() -> bytes:
+        lib = load()
+        buf = C.create_string_buffer(MULTI_ID_BYTES)
+        rc = lib.hsc_multi_unique_ids(buf, MULTI_ID_BYTES)
+        if rc != HSC_OK:
+            raise HscError(f"hsc_multi_unique_ids -> {rc}")
+        return buf.raw
+
+    @property
+    def world(self) -> int:
+        return self.lib.hsc_multi_world(self.ctx)
+
+    @property
+    def rank(self) -> int:
+        return self.lib.hsc_multi_rank(self.ctx)
+
+    @property
+    def nlocal(self) -> int:
+        return self.lib.hsc_multi_local(self.ctx)
+
+    def member(self, i: int) -> Validator:
+        """Member context i (owned by the multi context: not closed by the
+        returned wrapper)."""
+        v = Validator.__new__(_Member)
+        v.lib, v._keep = self.lib, None
+        v.ctx = _p(self.lib.hsc_multi_member(self.ctx, i))
+        if not v.ctx:
+            raise HscError(f"no member {i}")
+        return v
+
+    def set_splitters(self, gid: np.ndarray, words: np.ndarray) -> None:
+        """world - 1 ascending composite splitters: gid u32[S], words u64[W, S]."""
+        gid = np.ascontiguousarray(gid, np.uint32)
+        words = np.ascontiguousarray(words, np.uint64).reshape(-1, len(gid)) if len(gid) else \
+            np.zeros((1, 0), np.uint64)
+        self._chk(self.lib.hsc_multi_set_splitters(self.ctx, len(gid), gid.ctypes.data,
+                                                   words.ctypes.data, words.shape[0]),
+                  "hsc_multi_set_splitters")
+
+    def adopt(self) -> None:
+        self._chk(self.lib.hsc_multi_adopt(self.ctx), "hsc_multi_adopt")
+
+    def probe_device_multi(self, batches: Sequence[ProbeBatch], lane: int = 0) -> None:
+        arr = (ProbeBatch * len(batches))(*batches)
+        self._chk(self.lib.hsc_multi_probe_device(self.ctx, arr, lane), "hsc_multi_probe_device")
+
+    def multi_stats(self) -> dict:
+        out = np.zeros(4, np.uint64)
+        self._chk(self.lib.hsc_multi_stats(self.ctx, out.ctypes.data), "hsc_multi_stats")
+        return {"batches": int(out[0]), "probes": int(out[1]), "routed": int(out[2]),
+                "local_members": int(out[3])}
+
+    def last_counts(self) -> np.ndarray:
+        n = self.world
+        out = np.zeros(n * n, np.uint32)
+        self._chk(self.lib.hsc_multi_last_counts(self.ctx, out.ctypes.data, n * n),
+                  "hsc_multi_last_counts")
+        return out.reshape(n, n)
+
+
+class _Member(Validator):
+    """A member context of a MultiValidator (not owned: close() is a no-op)."""
+
+    def close(self) -> None:
+        self.ctx = None
 
 
 def bdb_osql_serial_check(v: Validator, arr: Optional[CurRangeArr], regop_only: int = 0) -> int:

@@ -498,6 +498,63 @@ int hsc_get_timing(hsc_ctx *ctx, hsc_timing *t);
 /* Enable per-kernel HIP event timing of probes (adds event records). */
 int hsc_enable_timing(hsc_ctx *ctx, int on);
 
+/* ---- multi-GPU context ---------------------------------
+ * A multi context is an hsc_ctx: hip_serial_check_batch,
+ * hip_bdb_osql_serial_check, hsc_collector_*, hsc_check_readsets /
+ * _serial, hsc_window_ingest_log / _raw, hsc_window_append[_log|_raw],
+ * hsc_register_group and the window accessors take it unchanged.  Its window
+ * is cut into `world` contiguous pieces of the composite key space (gid, key
+ * words) -- member d holds the keys K with sp[d-1] <= K < sp[d] -- one per
+ * member context.  The context itself keeps the log decode, dictionaries and
+ * window rules and marshals every batch on the host; each member then routes
+ * its share of the probes on its GPU to the members whose pieces their
+ * [lo, hi] overlap, every member joins what it received against its piece,
+ * and the members' verdict bitmaps are OR-ed per read-set owner.  Members in
+ * one process exchange by direct stores into each other's memory (xGMI peer
+ * access, enabled at creation; several members may share one GPU); members
+ * in different processes (one per GPU, hsc_multi_create_rank) exchange over
+ * RCCL (grouped ncclSend / ncclRecv, librccl loaded at run time).  Verdicts
+ * equal those of one context holding the whole window.  Not on a multi
+ * context: hsc_set_stream, hsc_probe_device, hsc_window_ingest_device (ingest
+ * the members directly, then hsc_multi_adopt), hsc_rw_edges, the graph and
+ * coalesce calls (use a member). */
+/* n members on devices[0..n-1] (n <= 16; a device may repeat) in this
+ * process.  Returns the context in *out (destroy with hsc_ctx_destroy). */
+int hsc_multi_create(const int *devices, int n, hsc_ctx **out);
+/* One member per process: this process is member `rank` of `world` on
+ * `device`.  ids: the bytes hsc_multi_unique_ids wrote on one rank (every
+ * rank passes the same ones; 2 x 128 bytes: one RCCL communicator per lane). */
+int hsc_multi_unique_ids(void *out, size_t bytes);
+int hsc_multi_create_rank(int device, int rank, int world, const void *ids, size_t bytes,
+                          hsc_ctx **out);
+int hsc_multi_world(hsc_ctx *ctx);   /* members of the partition */
+int hsc_multi_rank(hsc_ctx *ctx);    /* global index of this process's first member */
+int hsc_multi_local(hsc_ctx *ctx);   /* members in this process */
+hsc_ctx *hsc_multi_member(hsc_ctx *ctx, int i);  /* i < hsc_multi_local */
+/* The world - 1 ascending splitters (gid[S], words[W][S] big-endian key
+ * words); default: equal-row quantiles of the ingested log's rows.  A
+ * host-staged window is re-partitioned at the next check. */
+int hsc_multi_set_splitters(hsc_ctx *ctx, size_t S, const uint32_t *gid, const uint64_t *words,
+                            int W);
+/* The members' windows, ingested directly (hsc_window_ingest_device on
+ * hsc_multi_member, each holding exactly its piece's rows), become the
+ * context's window; table maxima are max-merged over all members (an RCCL
+ * all-reduce across ranks).  Collective on a per-rank context. */
+int hsc_multi_adopt(hsc_ctx *ctx);
+/* Device-resident batches, one per local member (pointers on its GPU), each
+ * numbering its own read sets 0..b[i].n_txn-1: routed, probed and merged;
+ * b[i].bitmap (ceil(n_txn / 64) words) receives the merged verdict bits of
+ * member i's read sets.  lane (0 or 1): scratch set, so two batches can be in
+ * flight; a lane is reused after its previous batch finished.  Returns once
+ * the work is enqueued (the host waits for the routing counts only).
+ * Collective on a per-rank context. */
+int hsc_multi_probe_device(hsc_ctx *ctx, const hsc_probe_batch *b, int lane);
+/* out[4]: routed batches, probes routed (sources), probe rows received
+ * (destinations; > probes when ranges straddle pieces), local members. */
+int hsc_multi_stats(hsc_ctx *ctx, uint64_t out[4]);
+/* counts[s * world + d]: probes member s sent member d in the last batch. */
+int hsc_multi_last_counts(hsc_ctx *ctx, uint32_t *counts, int n);
+
 /* ---- OSQL_SERIAL wire path --------------------------------------------
  * Decode only: *out points at context-owned read sets, valid until the next
  * decode on this context (HSC_EINVAL names the malformed message). */
