@@ -2,16 +2,16 @@
 
 One step = one batch of read sets (config 2: 100k read sets x 10 ranges per
 GPU) fully verdicted against the resident write window (1M commits x 10
-int64 keys per GPU) by the HIP join, plus -- on N > 1 GPUs -- the RCCL max
-all-reduce that merges per-shard verdicts.  Inputs are resident in HBM when
-the timed region starts; marshalling (CurRangeArr -> probe SoA, done by the
+int64 keys per GPU) by the HIP join.  Inputs are resident in HBM when the
+timed region starts; marshalling (CurRangeArr -> probe SoA, done by the
 native library) happens before it.
 
-Multi-GPU (weak scaling): the key space is range-partitioned; rank r owns the
-window keys [r, r+1) * 2^40 (config 5: sampled global splitters) and probes
-only the ranges that overlap its shard; the global batch is N x 100k read
-sets.  Each shard's verdict bitmap is all-gathered (N x n_txn / 8 bytes) and
-the N bitmaps OR-ed on the GPU (hsc_or_bitmaps): RCCL has no bitwise OR.
+Multi-GPU (weak scaling, bench_multi): the native multi-GPU context
+(hsc_multi_*, one process per GPU over RCCL under torchrun, or --inproc N
+members in one process): every GPU holds its piece of an N-times larger
+window and its own batch of 100k read sets; a step routes every GPU's probes
+on the device to the pieces they overlap, exchanges them, probes, and ORs the
+verdict bitmaps onto each read set's owner -- all inside the timed region.
 
 Prints ONE JSON line on rank 0.
 """
@@ -610,6 +610,278 @@ def pmc_traffic(args):
     return out
 
 
+def bench_multi(args):
+    """N > 1: the native multi-GPU context (include/hip_serial.h hsc_multi_*).
+    Weak scaling: every member holds its piece of an N-times larger window
+    (composite-key splitters: config 2 key ranges, config 5 sampled global
+    splitters, config 3 work quantiles over the 32 groups' rows and ranges)
+    and its own resident batch of 100k read sets (its share of the global
+    batch, in arrival order, NOT routed on the host).  One timed step =
+    hsc_multi_probe_device on every member: device-side routing of each
+    member's probes to the pieces their [lo, hi] overlaps (k_route_count,
+    counts all-gathered, k_route_scatter), the exchange (RCCL grouped
+    send / receive across ranks; direct stores between members of one
+    process), the probe pipeline on every member, and the OR-merge of the
+    members' verdict bitmaps onto each read set's owner.  Under torchrun:
+    one process per GPU (RCCL).  --inproc N without torchrun: N members in
+    this process on the visible GPUs round robin (several members share a GPU
+    when there are fewer: a rehearsal of the in-process path)."""
+    import torch
+    import torch.distributed as dist
+
+    from comdb2_amd import hsc, shard
+    from comdb2_amd.workloads import SEED_CONFIG2, config2, config2_device_window
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    inproc = world_env == 1 and not args.rank_path
+    if inproc:
+        N = args.inproc
+        ndev = torch.cuda.device_count()
+        devs = [i % ndev for i in range(N)]
+        v = hsc.MultiValidator(devs)
+        mine = list(range(N))
+        dev_of = {g: torch.device("cuda", devs[g]) for g in mine}
+    else:
+        N = world_env
+        torch.cuda.set_device(local)
+        dev0 = torch.device("cuda", local)
+        dist.init_process_group("nccl", device_id=dev0)
+        ids = torch.zeros(hsc.MULTI_ID_BYTES, dtype=torch.uint8, device=dev0)
+        if rank == 0:
+            ids.copy_(torch.frombuffer(bytearray(hsc.MultiValidator.unique_ids()), dtype=torch.uint8))
+        dist.broadcast(ids, 0)
+        v = hsc.MultiValidator(rank=rank, world=N, ids=bytes(ids.cpu().numpy().tobytes()),
+                               device=local)
+        mine = [rank]
+        dev_of = {rank: dev0}
+        devs = [local]
+
+    def sync_all():
+        for d in sorted(set(dev_of[g].index for g in mine)):
+            torch.cuda.synchronize(d)
+
+    T = args.n_txn
+    rows = {}  # member -> (gid, words, lsn)
+    if args.config == 2:
+        value_bits = 40
+        assert v.register_group("t1", 0, 9) == 0
+        for g in mine:
+            c2 = config2(seed=SEED_CONFIG2, n_commits=args.n_commits, n_txn=T, rank=g, world=N,
+                         build_log=False)
+            rows[g] = config2_device_window(c2)
+            end_lsn = c2.params["end_lsn"]
+            first_rs = c2.readsets
+        more_rs = lambda bi: config2(seed=SEED_CONFIG2 + 7919 * bi, n_commits=args.n_commits,
+                                     n_txn=T, rank=0, world=N, build_log=False).readsets
+        sp_g, sp_w = shard.int64_splitter_keys([j << value_bits for j in range(1, N)], 2)
+        workload = (f"config2 x{N}: per member 100k read sets x 10 ranges vs its key-range piece "
+                    f"of an {N}x window (1M commits x 10 int64 keys per member), one index")
+        data = "synthetic (BASELINE config 2 generator, seed 0xC0FFEE02, weak scaling per member)"
+        groups = [("t1", 0, 9)]
+    elif args.config == 5:
+        from comdb2_amd.workloads import SEED_CONFIG5, config5_scaled, int64_words
+        assert v.register_group("t1", 0, 9) == 0
+        segs = {}
+        for g in mine:
+            c5 = config5_scaled(seed=SEED_CONFIG5, keys_per_gpu=args.c5_keys, n_txn=T, rank=g,
+                                world=N)
+            segs[g] = (c5.keys, c5.lsn)
+            end_lsn = c5.end_lsn
+            first_rs = c5.readsets
+            range_keys = c5.range_keys
+        if inproc:
+            allk = np.concatenate([segs[g][0] for g in mine])
+            alll = np.concatenate([segs[g][1] for g in mine])
+            split = shard.sampled_splitters(allk, range_keys, N, 0, shard.ROW_COST,
+                                            shard.RANGE_COST)["splitters"]
+            own = np.searchsorted(split, allk, side="right")
+            for g in mine:
+                sel = own == g
+                k = allk[sel]
+                rows[g] = (np.zeros(len(k), np.uint32), int64_words(k), alll[sel])
+        else:
+            k, l = segs[rank]
+            split = shard.sampled_splitters(k, range_keys, N, rank, shard.ROW_COST,
+                                            shard.RANGE_COST)["splitters"]
+            k, l = shard.exchange_rows(k, l, split)
+            rows[rank] = (np.zeros(len(k), np.uint32), int64_words(k), l)
+        segs = None
+        more_rs = lambda bi: config5_scaled(seed=SEED_CONFIG5 + 7919 * bi, keys_per_gpu=args.c5_keys,
+                                            n_txn=T, rank=0, world=N, window=False).readsets
+        sp_g, sp_w = shard.int64_splitter_keys(split, 2)
+        workload = (f"config5 x{N}: one global Zipf(1.2) law over 2^32 keys, {args.c5_keys} logged "
+                    f"writes per member, sampled global splitters, 100k read sets x 10 ranges "
+                    f"per member")
+        data = "synthetic (config 5 generator, seed 0xC0FFEE05, weak scaling per member)"
+        groups = [("t1", 0, 9)]
+    else:
+        from comdb2_amd.workloads import SEED_CONFIG3, config3_arrays
+        c3 = config3_arrays(seed=SEED_CONFIG3, n_writes=args.c3_writes * N, n_txn=T * N)
+        for g, (tbn, ix, L) in enumerate(c3.groups):
+            assert v.register_group(tbn, ix, L) == g
+        gid, words, lsn = c3.window()
+        hv = hsc.Validator(-1)
+        for (tbn, ix, L) in c3.groups:
+            hv.register_group(tbn, ix, L)
+        hv.set_end(c3.end_lsn)
+        sp_g, sp_w = shard.composite_splitters(gid, words, N, hv.marshal(c3.readsets))
+        hv.close()
+        own = shard.composite_owner(gid, words, sp_g, sp_w)
+        for g in mine:
+            sel = own == g
+            rows[g] = (gid[sel], np.ascontiguousarray(words[:, sel]), lsn[sel])
+        end_lsn = c3.end_lsn
+        first_rs = c3.readsets
+        more_rs = lambda bi: config3_arrays(seed=SEED_CONFIG3, n_writes=args.c3_writes * N,
+                                            n_txn=T * N, rs_seed=bi).readsets
+        workload = (f"config3 x{N}: {len(c3.groups)} (table, index) groups of composite keys "
+                    f"(9-64 B), {args.c3_writes} index writes and {T} read sets per member, "
+                    f"composite-key pieces at work quantiles (hot groups cut)")
+        data = "synthetic (config 3 generator, seed 0xC0FFEE03, weak scaling per member)"
+        groups = c3.groups
+    v.set_splitters(sp_g, sp_w)
+    for i, g in enumerate(mine):
+        gid, words, lsn = rows[g]
+        d = dev_of[g]
+        tg = torch.from_numpy(np.ascontiguousarray(gid)).to(d)
+        tw = torch.from_numpy(np.ascontiguousarray(words).reshape(-1).view(np.int64)).to(d)
+        tl = torch.from_numpy(np.ascontiguousarray(lsn).view(np.int64)).to(d)
+        sync_all()
+        v.member(i).ingest_device(len(lsn), words.shape[0], tg.data_ptr(), tw.data_ptr(),
+                                  tl.data_ptr(), end_lsn)
+        del tg, tw, tl
+    n_w = {g: len(rows[g][2]) for g in mine}
+    rows = None
+    v.adopt()
+    if args.config == 3:
+        v.merge_table_max(c3.table_max)  # data-row writes lock tables too
+    W = v.words
+    # resident batches: member g's share of each global batch
+    batches, ring_bytes, bi = [], 0, 0
+    while bi < max(2, args.batches) or ring_bytes < args.ring_gb * 1e9:
+        rs = first_rs if bi == 0 else more_rs(bi)
+        per = {}
+        for g in mine:
+            m = v.marshal(rs.subset(np.arange(g * T, (g + 1) * T)))
+            b = upload_batch(torch, dev_of[g], m)
+            b["bits"] = torch.zeros((T + 63) // 64, dtype=torch.int64, device=dev_of[g])
+            b["verdict"] = torch.zeros(T, dtype=torch.uint8, device=dev_of[g])
+            b["struct"] = probe_struct(hsc, b, b["verdict"], b["bits"], T)
+            b["bytes"] = sum(int(b[k].numel() * b[k].element_size())
+                             for k in ("lo", "hi", "gid", "snap", "txn", "lock_table", "lock_snap",
+                                       "lock_txn"))
+            per[g] = b
+        ring_bytes += per[mine[0]]["bytes"]
+        batches.append(per)
+        bi += 1
+        if bi % 8 == 0:
+            print(f"[bench] {bi} batches, {ring_bytes / 1e9:.2f} GB per member", file=sys.stderr,
+                  flush=True)
+    NB = len(batches)
+    sync_all()
+
+    def step(k, lanes, nbatch):
+        v.probe_device_multi([batches[k % nbatch][g]["struct"] for g in mine], lane=k % lanes)
+
+    def timed(lanes, nbatch):
+        for k in range(args.warmup):
+            step(k, lanes, nbatch)
+        sync_all()
+        if not inproc:
+            dist.barrier()
+        sync_all()
+        t0 = time.perf_counter()
+        for k in range(args.warmup, args.warmup + args.steps):
+            step(k, lanes, nbatch)
+        sync_all()
+        if not inproc:
+            dist.barrier()
+        sync_all()
+        el = time.perf_counter() - t0
+        if not inproc:
+            e = torch.tensor([el], dtype=torch.float64, device=dev_of[rank])
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            el = float(e.item())
+        return el
+
+    elapsed = timed(2, NB)
+    serial = float(np.median([timed(1, NB) for _ in range(3)]))
+    # merged verdicts of batch 0 (member mine[0]'s read sets)
+    step(0, 1, NB)
+    sync_all()
+    b0 = batches[0][mine[0]]
+    bits = b0["bits"].cpu().numpy().view(np.uint8)
+    v0 = np.maximum(np.unpackbits(bits, bitorder="little")[:T], b0["forced"])
+    cnt = v.last_counts().astype(np.int64)
+    st = v.multi_stats()
+    n_keys = v.member(0).keys
+    n_r = int(batches[0][mine[0]]["n"])
+    Lhat = 8 * W
+    B = n_keys * (Lhat + 12) + n_r * (2 * Lhat + 16) + (T + 7) // 8
+    ms = elapsed / args.steps * 1e3
+    rec = 16 * W + 16
+    off_diag = int(cnt.sum() - np.trace(cnt))
+    out = {
+        "metric": METRIC,
+        "value": N * T * args.steps / elapsed,
+        "unit": "checks/s",
+        "n_gpus": len(set(devs)) if inproc else N,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": data,
+        "config": {
+            "workload": workload,
+            "members": N,
+            "transport": "in-process stores (xGMI peer / same GPU)" if inproc else "RCCL (C, grouped send/recv)",
+            "read_sets_per_step_per_member": T,
+            "ranges_per_member": n_r,
+            "window_keys_member0": n_keys,
+            "logged_writes_per_member": n_w,
+            "parallelism": f"composite-key pieces x{N}, device-side routing + exchange + "
+                           "bitmap OR per owner, all inside the timed step",
+            "lanes": 2,
+            "serial_ms_per_step": serial / args.steps * 1e3,
+            "ring_batches": NB,
+            "groups": len(groups),
+            "conflict_rate": float((v0 != 0).mean()),
+        },
+        "routing": {
+            "counts_last_batch": cnt.tolist(),
+            "routed_over_probes": st["routed"] / max(st["probes"], 1),
+            "exchanged_bytes_per_step": off_diag * rec,
+            "exchanged_rows_per_step": off_diag,
+            "note": "counts[s][d]: probes member s routed to member d in the last batch; "
+                    "off-diagonal rows crossed GPUs (RCCL) or were stored into another "
+                    "member's columns",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "routed step (route count + scatter, exchange, probe phase, OR merge) per member",
+            "achieved": B / (ms * 1e-3) / 1e9,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": B / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            "frac_1lane": B / (serial / args.steps) / 1e9 / HBM_PEAK_GBS,
+            "traffic": None,
+            "algorithmic_bytes": B,
+            "note": "B = member 0's probe-phase bytes (SURVEY 8(d): its window keys and its own "
+                    "ranges); the routing and exchange bytes come on top",
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    v.close()
+    if not inproc:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -657,6 +929,13 @@ def main():
                     help="config 4: fraction of txns reading a stale snapshot")
     ap.add_argument("--c4-max-lag", type=int, default=64, help="config 4: max snapshot lag")
     ap.add_argument("--c4-keys", type=int, default=0, help="config 4: keys (0: txns / 10)")
+    ap.add_argument("--inproc", type=int, default=0,
+                    help="without torchrun: N members of one multi context in this process "
+                         "(the visible GPUs round robin; members share a GPU when there are "
+                         "fewer) -- the in-process multi-GPU path")
+    ap.add_argument("--rank-path", action="store_true",
+                    help="run the per-rank (RCCL) multi-GPU path even at WORLD_SIZE 1 (its "
+                         "world-1 rehearsal on one GPU)")
     args = ap.parse_args()
     if args.ring_gb is None:
         args.ring_gb = 1.1 if args.config in (2, 3, 5) else 0.0
@@ -665,35 +944,23 @@ def main():
         return bench_graph(args)
     if args.config == 1:
         return bench_commit_stream(args)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.inproc > 1 or args.rank_path:
+        return bench_multi(args)
+    # one GPU (N > 1 runs bench_multi)
+    world, rank = 1, 0
     traffic = None
-    if (args.config in (2, 3, 5) and world == 1 and not args.no_pmc and not args.pmc_child
-            and not args.wide):
+    if args.config in (2, 3, 5) and not args.no_pmc and not args.pmc_child and not args.wide:
         traffic = pmc_traffic(args)  # child processes, before this one touches the GPU
     import torch
-    import torch.distributed as dist
 
     from comdb2_amd import hsc, shard
     from comdb2_amd.workloads import SEED_CONFIG2, config2, config2_device_window
 
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        world = max(world, 1)
-    if os.environ.get("HSC_BENCH_BACKEND", "nccl") != "nccl":
-        local = 0  # rehearsal: every rank on cuda:0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        # HSC_BENCH_BACKEND=gloo rehearses the N > 1 path with every rank on one GPU
-        backend = os.environ.get("HSC_BENCH_BACKEND", "nccl")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
 
-    want_cpu = (rank == 0 and world == 1 and not args.no_cpu and args.config in (2, 3, 5)
-                and not args.pmc_child)
+    want_cpu = not args.no_cpu and args.config in (2, 3, 5) and not args.pmc_child
     batches = []
     v = hsc.Validator(local)
     if args.wide:
@@ -711,29 +978,14 @@ def main():
         for g, (tbn, ix, L) in enumerate(c3.groups):
             assert v.register_group(tbn, ix, L) == g
         gid, words, lsn = c3.window()
-        if world > 1:
-            # work per group from the rows and the first batch's ranges (every
-            # rank computes the same plan), hot groups cut into key-range pieces
-            hv = hsc.Validator(-1)
-            for g, (tbn, ix, L) in enumerate(c3.groups):
-                hv.register_group(tbn, ix, L)
-            hv.set_end(c3.end_lsn)
-            gshards = shard.group_work(gid, words, hv.marshal(c3.readsets), world)
-            hv.close()
-        else:
-            gshards = shard.group_work(gid, words, None, world)
-        sel = gshards.row_mask(gid, words, rank)
-        gid, words, lsn = gid[sel], np.ascontiguousarray(words[:, sel]), lsn[sel]
-        mine = sorted({g for g, _, _, r, _ in gshards.pieces if r == rank})
+        mine = list(range(len(c3.groups)))
         end_lsn = c3.end_lsn
         first_rs = c3.readsets
         more_rs = lambda bi: config3_arrays(seed=SEED_CONFIG3, n_writes=args.c3_writes * world,
                                             n_txn=args.n_txn * world, rs_seed=bi).readsets
-        make_shards = lambda W: gshards
         workload = (f"config3: {len(c3.groups)} (table, index) groups of composite keys "
                     f"(9-64 B, log-normal sizes), {args.c3_writes} index writes and "
-                    f"{args.n_txn} read sets per GPU (points, ranges, prefixes, table locks), "
-                    f"LPT group shards, hot groups cut into key-range pieces")
+                    f"{args.n_txn} read sets per GPU (points, ranges, prefixes, table locks)")
         data = "synthetic (config 3 generator, seed 0xC0FFEE03, weak scaling per GPU)"
     elif args.config == 2:
         value_bits = 40
@@ -745,7 +997,6 @@ def main():
         more_rs = lambda bi: config2(seed=SEED_CONFIG2 + 7919 * bi, n_commits=args.n_commits,
                                      n_txn=args.n_txn, rank=rank, world=world,
                                      build_log=False).readsets
-        make_shards = lambda W: shard.KeyRangeShards.int64_uniform(world, value_bits, W)
         workload = ("config2: per GPU 100k read sets x 10 ranges (1M ranges) vs a window of "
                     "1M commits x 10 int64 index keys (10M logged keys), one index")
         data = ("synthetic (BASELINE config 2 generator, seed 0xC0FFEE02; int64 keys in memcmp "
@@ -759,18 +1010,9 @@ def main():
         more_rs = lambda bi: config5_scaled(seed=SEED_CONFIG5 + 7919 * bi,
                                             keys_per_gpu=args.c5_keys, n_txn=args.n_txn,
                                             rank=rank, world=world, window=False).readsets
-        # sampled global splitters over the probe work, rows to owners
-        if world > 1:
-            c5_split = shard.sampled_splitters(keys5, c5.range_keys, world, rank,
-                                               shard.ROW_COST, shard.RANGE_COST)
-            keys5, lsn = shard.exchange_rows(keys5, lsn, c5_split["splitters"])
-        else:
-            c5_split = dict(splitters=np.zeros(0, np.int64), est_load=np.ones(1),
-                            load=lambda b: np.ones(1))
         words = int64_words(keys5)
         gid = np.zeros(len(keys5), dtype=np.uint32)
         del keys5
-        make_shards = lambda W: shard.KeyRangeShards.int64_splitters(c5_split["splitters"], W)
         workload = (f"config5: one global Zipf(1.2) law over 2^32 keys, {args.c5_keys} logged "
                     f"writes per GPU (hot keys collapse under dedupe), sampled global splitters, "
                     f"100k read sets x 10 ranges per GPU (width {c5.params['width']}, 3 % of the "
@@ -789,9 +1031,6 @@ def main():
     if c3 is not None:
         v.merge_table_max(c3.table_max)  # data-row writes lock tables too
     W = v.words
-    shards = make_shards(W)
-    if world > 1:  # lock probes see the table-wide max commit LSN
-        v.merge_table_max(shard.allreduce_table_max(v.table_max()))
     T = first_rs.ntxn
     m0 = None
     ring_bytes = 0
@@ -802,8 +1041,6 @@ def main():
         m = v.marshal(rs)
         if bi == 0 and (want_cpu or args.check):
             m0 = m
-        if world > 1:
-            m = shard.route(m, shards.range_mask(m, rank), shards.lock_mask(m, rank))
         b = upload_batch(torch, dev, m)
         b["bytes"] = sum(int(b[k].numel() * b[k].element_size())
                          for k in ("lo", "hi", "gid", "snap", "txn", "lock_table", "lock_snap",
@@ -815,17 +1052,9 @@ def main():
             print(f"[bench] {bi} batches, {ring_bytes / 1e9:.2f} GB", file=sys.stderr, flush=True)
     S = max(1, args.streams)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(S - 1)]
-    comm = torch.cuda.Stream(device=dev) if world > 1 else None
     verdicts = [torch.zeros(T, dtype=torch.uint8, device=dev) for _ in range(S)]
-    W64 = (T + 63) // 64
-    bitmaps = [torch.zeros(W64, dtype=torch.int64, device=dev) for _ in range(S)]
-    # N > 1: each shard's verdict bitmap, all-gathered and OR-ed (hsc_or_bitmaps)
-    lbits = [torch.zeros(W64, dtype=torch.int64, device=dev) for _ in range(S)] if world > 1 else None
-    gath = [torch.zeros(world * W64, dtype=torch.int64, device=dev) for _ in range(S)] if world > 1 else None
-    # N = 1: the verdict bytes are the result, no bitmap (the pack is folded
-    # into the plan kernel); N > 1: each shard's bitmap for the merge
-    structs = [[probe_struct(hsc, b, verdicts[si], None if world == 1 else lbits[si], T)
-                for si in range(S)] for b in batches]
+    # the verdict bytes are the result, no bitmap (the pack is folded into the plan kernel)
+    structs = [[probe_struct(hsc, b, verdicts[si], None, T) for si in range(S)] for b in batches]
     torch.cuda.synchronize()
 
     if args.pmc_child:  # profiled by the parent's rocprofv3 --pmc pass: the ring, S streams
@@ -841,36 +1070,16 @@ def main():
         st = streams[si]
         v.set_stream(st.cuda_stream)
         v.probe_device(structs[k % nbatch][si])
-        if world > 1:  # verdict merge on one comm stream: the same collective order on every rank
-            e = torch.cuda.Event()
-            e.record(st)
-            comm.wait_event(e)
-            with torch.cuda.stream(comm):
-                shard.gather_bitmaps(lbits[si], gath[si])
-            e2 = torch.cuda.Event()
-            e2.record(comm)
-            st.wait_event(e2)
-            v.or_bitmaps(gath[si].data_ptr(), world, W64, bitmaps[si].data_ptr())
 
     def timed(nstreams, nbatch):
         for k in range(args.warmup):
             step(k, nstreams, nbatch)
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
         t0 = time.perf_counter()
         for k in range(args.warmup, args.warmup + args.steps):
             step(k, nstreams, nbatch)
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        if world > 1:
-            e = torch.tensor([el], dtype=torch.float64, device=dev)
-            dist.all_reduce(e, op=dist.ReduceOp.MAX)
-            el = float(e.item())
         return el
 
     NB = len(batches)
@@ -890,11 +1099,7 @@ def main():
     # verdicts of batch 0 (for the conflict rate and the CPU parity sample)
     step(0, 1, NB)
     torch.cuda.synchronize()
-    if world > 1:  # the merged verdicts are the OR-ed bitmap
-        bits = bitmaps[0].cpu().numpy().view(np.uint8)
-        v0 = np.unpackbits(bits, bitorder="little")[:T].astype(np.uint8)
-    else:
-        v0 = verdicts[0].cpu().numpy().copy()
+    v0 = verdicts[0].cpu().numpy().copy()
     forced = batches[0]["forced"]
     v0 = np.maximum(v0, forced)
 
@@ -926,7 +1131,7 @@ def main():
                         axis=0)
         B = int((keys_g * (lhat + 12)).sum() + (rng_g * (2 * lhat + 16)).sum() + (T + 7) // 8)
     WG = v.tile_key_words if v.layout == hsc.LAYOUT_COMPACT and not args.compact_wide else 0
-    kern = kernel_bytes(v.layout, W if WG else v.code_words, n_keys, n_r, T, tm, WG, world > 1)
+    kern = kernel_bytes(v.layout, W if WG else v.code_words, n_keys, n_r, T, tm, WG, False)
     ms_per_step = elapsed / args.steps * 1e3
     frac = lambda el: B / (el / args.steps) / 1e9 / HBM_PEAK_GBS
     checks = T * args.steps
@@ -949,7 +1154,7 @@ def main():
             "ranges_per_gpu": n_r,
             "window_keys_per_gpu": n_keys,
             "logged_writes_per_gpu": n_w,
-            "parallelism": f"key-range shards x{world}" + (" + RCCL all-gather of verdict bitmaps" if world > 1 else ""),
+            "parallelism": "one GPU (bench.py --gpus N: the multi-GPU context, bench_multi)",
             "streams": S,
             "serial_ms_per_step": serial_elapsed / args.steps * 1e3,
             "ring_batches": NB,
@@ -1016,16 +1221,7 @@ def main():
     if traffic:
         out["roofline"]["traffic_detail"] = traffic
     if args.config == 3:
-        out["config"]["parallelism"] = f"(table, index) group shards (LPT) x{world}" + (
-            " + RCCL all-gather of verdict bitmaps" if world > 1 else "")
-        out["config"]["groups_per_rank"] = len(mine)
-        out["imbalance"] = {"partition": "LPT over (table, index) groups by rows + "
-                                         f"{shard.RANGE_COST} x ranges; groups heavier than "
-                                         "total / (2N) cut into key-range pieces",
-                            "work_max_over_mean": gshards.imbalance(),
-                            "split_groups": sorted(gshards.split),
-                            "pieces": len(gshards.pieces)}
-        if args.check and world == 1:
+        if args.check:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle
             sj = oracle.SortJoin(gid, words, lsn, len(c3.groups))
@@ -1034,31 +1230,7 @@ def main():
             out["parity"] = {"kind": "full batch 0 vs oracle/sortjoin.c (CPU sort-join)",
                              "equal": bool(np.array_equal(want != 0, v0 != 0)), "cpu_s": secs}
     if args.config == 5:
-        # per-GPU imbalance: routed ranges and 1-stream probe time per rank
-        loc = np.array([n_r, tm["probe_total_ms"], n_keys], dtype=np.float64)
-        if world > 1:
-            g = torch.from_numpy(loc).to(dev)
-            allg = [torch.zeros_like(g) for _ in range(world)]
-            dist.all_gather(allg, g)
-            loc = torch.stack(allg).cpu().numpy()
-        else:
-            loc = loc[None, :]
-        fixed = np.array([(j << 32) // world for j in range(1, world)], np.int64)
-        est_fixed = c5_split["load"](fixed)
-        est = c5_split["est_load"]
-        out["imbalance"] = {"partition": "sampled global splitters (distinct window keys x "
-                                         f"{shard.ROW_COST} + range lower bounds x "
-                                         f"{shard.RANGE_COST}, one all_gather)",
-                            "splitters": c5_split["splitters"].tolist(),
-                            "ranges_per_rank": loc[:, 0].tolist(),
-                            "window_keys_per_rank": loc[:, 2].tolist(),
-                            "probe_ms_per_rank": loc[:, 1].tolist(),
-                            "ranges_max_over_mean": float(loc[:, 0].max() / loc[:, 0].mean()),
-                            "time_max_over_mean": float(loc[:, 1].max() / loc[:, 1].mean()),
-                            "sample_est_max_over_mean": float(est.max() / est.mean()),
-                            "fixed_span_sample_est_max_over_mean":
-                                float(est_fixed.max() / max(est_fixed.mean(), 1e-9))}
-        if args.check and world == 1:
+        if args.check:
             sys.path.insert(0, os.path.join(ROOT, "oracle"))
             import oracle
             sj = oracle.SortJoin(gid, words, lsn, 1)
@@ -1068,7 +1240,7 @@ def main():
             out["parity"] = {"kind": "full batch 0 vs oracle/sortjoin.c (CPU sort-join)",
                              "equal": bool(np.array_equal(want != 0, v0 != 0)),
                              "cpu_s": secs}
-    if args.config == 2 and world == 1 and not args.no_api:
+    if args.config == 2 and not args.no_api:
         out["api"] = api_leg(hsc, v, first_rs, v0, args)
     if want_cpu:
         cpus = box_cpus()
@@ -1095,11 +1267,8 @@ def main():
                 log_note=f" (the tail from commit {c0} of {len(c5.lsn) // K5}: every record "
                          f"after the batch's oldest snapshot)")
         out["cpu_baseline"]["host"] = cpus
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    print(json.dumps(out), flush=True)
     v.close()
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

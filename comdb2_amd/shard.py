@@ -412,6 +412,66 @@ def gather_bitmaps(bitmap, gathered, group=None) -> None:
         dist.all_gather(list(gathered.view(world, -1).unbind(0)), bitmap, group=group)
 
 
+# ---- the C multi-GPU context (hsc_multi_*): composite splitters -------------
+# The native multi context cuts the window into contiguous pieces of the
+# composite key space (gid, key words); a piece boundary may fall inside a
+# group (a hot group is cut) or between groups.  These helpers compute such
+# splitters from rows (and optionally range lower bounds, weighted by their
+# probe cost) and the owner of each row, with the C routing rule
+# owner(K) = #splitters <= K.
+
+def _composite_ge(gid, words, g, w):
+    """rows (gid [n], words [W][n]) >= the composite key (g, w[W])."""
+    gid = np.asarray(gid, np.int64)
+    return (gid > int(g)) | ((gid == int(g)) & _geq(words, [int(x) for x in w]))
+
+
+def composite_owner(gid, words, sp_gid, sp_w) -> np.ndarray:
+    """Owner of every row: the number of splitters <= its composite key."""
+    own = np.zeros(len(gid), np.int64)
+    for k in range(len(sp_gid)):
+        own += _composite_ge(gid, words, sp_gid[k], sp_w[:, k])
+    return own
+
+
+def composite_splitters(gid, words, world: int, m: Optional[dict] = None):
+    """world - 1 ascending composite splitters (gid u32[S], words u64[W][S]) at
+    equal-work quantiles of the rows (ROW_COST each) and, with a marshalled
+    batch m, its range lower bounds (RANGE_COST each)."""
+    gid = np.asarray(gid, np.int64)
+    W = words.shape[0]
+    g_all, w_all, wt = [gid], [words], [np.full(len(gid), ROW_COST)]
+    if m is not None and m["n"]:
+        g_all.append(np.asarray(m["gid"], np.int64))
+        w_all.append(np.asarray(m["lo"], np.uint64)[:W])
+        wt.append(np.full(m["n"], RANGE_COST))
+    g = np.concatenate(g_all)
+    w = np.concatenate(w_all, axis=1)
+    wt = np.concatenate(wt)
+    order = np.lexsort(tuple(w[::-1]) + (g,)) if len(g) else np.zeros(0, np.int64)
+    cum = np.cumsum(wt[order])
+    sp_g = np.zeros(world - 1, np.uint32)
+    sp_w = np.zeros((W, world - 1), np.uint64)
+    for j in range(1, world):
+        i = int(np.searchsorted(cum, cum[-1] * j / world, side="left")) if len(cum) else 0
+        i = min(i, len(order) - 1)
+        if i >= 0 and len(order):
+            sp_g[j - 1] = g[order[i]]
+            sp_w[:, j - 1] = w[:, order[i]]
+    return sp_g, sp_w
+
+
+def int64_splitter_keys(splitters, W: int):
+    """int64 key-value splitters (rank j owns [s[j-1], s[j])) as composite
+    splitters of group 0 (9-byte memcmp keys, formats.enc_int64)."""
+    sp = [int(x) for x in splitters]
+    sp_g = np.zeros(len(sp), np.uint32)
+    sp_w = np.zeros((W, len(sp)), np.uint64)
+    for k, v in enumerate(sp):
+        sp_w[:, k] = key_words(F.enc_int64(v), W)
+    return sp_g, sp_w
+
+
 # ---- config 4: dependency graph + SCC sharded by key -----------------------
 # Every WW / WR / RW edge belongs to one key (hsc_graph.hip), so a history
 # split by key gives each rank an exact part of the edge set with no
