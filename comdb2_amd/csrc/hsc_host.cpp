@@ -87,9 +87,28 @@ static hipError_t lane_done(hsc_ctx *c)
     return hipEventRecord(L.done, c->stream);
 }
 
-// Before the window changes: c->stream waits for every lane's last batch.
+// Small batches (k_small_narrow) run on the stream current at their launch
+// without a probe lane, and their callers read the verdicts without c->mu:
+// before the window changes or the stream switches, the host waits until no
+// small slot is in flight (a slot is released by its caller once its kernel's
+// done word is seen, which needs no c->mu).  Called under c->mu.
+static hipError_t wait_small(hsc_ctx *c)
+{
+    const auto t0 = std::chrono::steady_clock::now();
+    for (auto &sl : c->small)
+        while (sl.busy.load(std::memory_order_acquire)) {
+            __builtin_ia32_pause();
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60))
+                return hipErrorLaunchTimeOut;  // a slot whose kernel never finished
+        }
+    return hipSuccess;
+}
+
+// Before the window changes: c->stream waits for every lane's last batch
+// (and the host for every small batch in flight).
 static hipError_t wait_lanes(hsc_ctx *c)
 {
+    if (const hipError_t e = wait_small(c); e != hipSuccess) return e;
     for (auto &L : c->lanes)
         if (L.done && L.tick && L.stream != c->stream) {
             hipError_t e = hipStreamWaitEvent(c->stream, L.done, 0);
@@ -924,7 +943,12 @@ static int flush_appends(hsc_ctx *c)
     const size_t sb = stage_bytes(k, W, nt);
     // a commit's rows (at most kDeltaStageRows) stay in the mapped staging,
     // the merge reads them there; more are uploaded first
-    const bool in_place = k <= kDeltaStageRows && c->h_app->coherent;
+    // (in place: every merge block stages the k rows from host memory into
+    // LDS -- (8W + 12) k + 16 bytes of LDS and that many bytes over PCIe per
+    // block; wide keys or a long run upload the rows once instead)
+    const size_t merge_blocks = (c->dn + k + 255) / 256;
+    const bool in_place = k <= kDeltaStageRows && c->h_app->coherent && W <= 8 &&
+                          (size_t)k * (8 * (size_t)W + 12) * merge_blocks <= ((size_t)1 << 20);
     uint8_t *db = (uint8_t *)c->h_app->dp;
     if (!in_place) {
         HIPCHK(c, c->d_agid.ensure(sb));
@@ -2704,6 +2728,10 @@ int hsc_set_stream(hsc_ctx *c, void *st)
     if (c->host_only) return HSC_EDEVICE;
     std::lock_guard<std::mutex> g(c->mu);
     hipStream_t ns = st ? (hipStream_t)st : c->own_stream;
+    // small batches launched on the old stream may still read the delta run
+    // a later append on the new stream rewrites: let them finish first
+    if (ns != c->stream && wait_small(c) != hipSuccess)
+        return fail(c, HSC_EDEVICE, "set_stream: a small batch did not finish");
     // appends return before their upload and merge ran: the new stream waits
     if (c->app_last && ns != c->stream && hipStreamWaitEvent(ns, c->app_last, 0) != hipSuccess)
         return fail(c, HSC_EDEVICE, "set_stream: order after the appends");

@@ -98,3 +98,49 @@ class _Sub:
 
     def pointers(self):
         return self._p
+
+
+def test_small_batches_race_stream_switches_and_appends(oracle_mod):
+    """One thread runs small batches (k_small_narrow, verdicts read without
+    the context lock) while another switches the context's stream and
+    appends commits: a stream switch or a delta merge waits for the small
+    kernels in flight (wait_small), so no probe reads a run being rewritten;
+    every call succeeds and the final verdicts equal the oracle's."""
+    import threading
+    c2 = config2(seed=4242, n_commits=3000, n_txn=300, value_bits=22, width=1 << 8,
+                 snap_recent=0.05)
+    log, rs = c2.log, c2.readsets
+    R = 13
+    want, _, _ = oracle_mod.check(log, rs)
+    v = Validator(0)
+    errors = []
+    stop = threading.Event()
+    try:
+        v.ingest_log(log_slice(log, 0, 1500 * R))
+        v.check_readsets(rs.subset([0]))  # built: appends go to the delta run
+        side = torch.cuda.Stream(device=0)
+
+        def checker():
+            k = 0
+            while not stop.is_set():
+                try:
+                    v.check_readsets(rs.subset(np.arange(k % 290, k % 290 + 1 + k % 7)))
+                except Exception as e:  # noqa: BLE001
+                    errors.append(e)
+                    return
+                k += 1
+
+        th = threading.Thread(target=checker)
+        th.start()
+        try:
+            for i, c in enumerate(range(1500, 3000, 100)):
+                v.set_stream(side.cuda_stream if i % 2 else 0)
+                v.append_log(log_slice(log, c * R, min(c + 100, 3000) * R))
+        finally:
+            stop.set()
+            th.join()
+        v.set_stream(0)
+        assert not errors, errors
+        np.testing.assert_array_equal(v.check_readsets(rs) != 0, want != 0)
+    finally:
+        v.close()
