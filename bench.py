@@ -399,19 +399,7 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0, bitmap=False):
     chunk = 2048 if WG else 4096  # probes per locate workgroup
     chunks = (n_r + chunk - 1) // chunk
     hist = 4 * tiles * ((chunks + 7) // 8 * 8)
-    if layout == 2 and os.environ.get("HSC_NT_SORT", "1") != "0" and \
-            os.environ.get("HSC_NT_FUSED", "0") != "0":
-        # plan-free join (default): the join reads its tile's column of the
-        # locate's chunk-major table (4 B per chunk) itself; the pack turns the
-        # conflict flags into verdict bytes (+ the bitmap for N > 1)
-        own = {
-            "k_locate_t": n_r * (4 + 8 + 4 + 16 * W) + 16 * recs + hist,
-            None: 0,  # no plan
-            "": 0,    # no scatter
-            "k_join_f": 8 * n_keys + 16 * recs + hist,
-            "k_pack_flags": 2 * T + ((T + 7) // 8 if bitmap else 0),
-        }
-    elif layout == 2 and os.environ.get("HSC_NT_SORT", "1") != "0":
+    if layout == 2:
         # narrow tiles, chunk-sorted records: the locate writes them in place
         # (+ its chunk's row of run starts / counts), no scatter pass
         own = {
@@ -421,15 +409,7 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0, bitmap=False):
             "k_join_t": 8 * n_keys + 16 * recs + 6 * tiles * ((chunks + 7) // 8 * 8),
             "k_pack": (T + (T + 7) // 8) if bitmap else 0,
         }
-    elif layout == 2:  # narrow tiles: 8-byte window rows, 16-byte records
-        own = {
-            "k_locate_t": n_r * (4 + 8 + 16 * W) + 16 * n_r + hist,
-            "k_plan_t": hist + 2 * T,  # + the verdict bytes from the locate's flags
-            "k_scatter_t": n_r * (16 + 4) + recs * 16,
-            "k_join_t": 8 * n_keys + 16 * recs,
-            "k_pack": (T + (T + 7) // 8) if bitmap else 0,  # N > 1: the verdict bitmap
-        }
-    elif WG and os.environ.get("HSC_CT_SORT", "1") != "0":
+    elif WG:
         # compact tiles, chunk-sorted 64-byte records written by the locate
         cols = 6 * tiles * ((chunks + 7) // 8 * 8)
         own = {
@@ -437,14 +417,6 @@ def kernel_bytes(layout, W, n_keys, n_r, T, tm, WG=0, bitmap=False):
             "k_plan_s": hist + cols + 2 * T,
             None: 0,
             "k_join_c": n_keys * (8 * WG + 4) + 64 * recs + cols,
-            "k_pack": (T + (T + 7) // 8) if bitmap else 0,
-        }
-    elif WG:  # compact tiles: raw W-word bounds in, 64-byte probe entries, 4-byte bucket entries
-        own = {
-            "k_compact_bounds+k_locate_c": n_r * (4 + 8 + 4 + 16 * W) + 72 * n_r + hist,
-            "k_plan_t": hist + 2 * T,
-            "k_scatter_c": 8 * n_r + 4 * recs,
-            "k_join_c": n_keys * (8 * WG + 4) + recs * (4 + 64),
             "k_pack": (T + (T + 7) // 8) if bitmap else 0,
         }
     else:  # wide tiles (compact: W = code words): key words + lsn + gid per row
@@ -546,9 +518,8 @@ def box_cpus():
                 cpu=cpu_model())
 
 
-PROBE_KERNELS = ("k_locate_t", "k_plan_t", "k_plan_s", "k_scatter_t", "k_join_t", "k_join_f",
-                 "k_pack_flags",  # narrow
-                 "k_locate_c", "k_scatter_c", "k_join_c", "k_join_cf",  # compact tiles
+PROBE_KERNELS = ("k_locate_t", "k_plan_s", "k_join_t", "k_pack_flags",  # narrow
+                 "k_locate_c", "k_join_c",  # compact tiles
                  "k_compact_bounds", "k_locate", "k_colscan", "k_plan", "k_scatter", "k_join",
                  "k_pack", "k_probe_delta")  # compact / wide, delta run
 

@@ -67,7 +67,7 @@ struct hsc_collector {
     int max_batch = 0;
     int max_wait_us = 0;
     int max_inflight = 2;
-    bool premarshal = true;  // callers marshal their own read set before queueing (HSC_PREMARSHAL=0: off)
+    bool premarshal = true;  // callers marshal their own read set before queueing
     std::mutex m;
     struct Req {
         void *ranges;
@@ -144,8 +144,6 @@ int hsc_collector_create(hsc_ctx *ctx, int max_batch, int max_wait_us, hsc_colle
     k->ctx = ctx;
     k->max_batch = max_batch ? max_batch : 65536;
     k->max_wait_us = max_wait_us;
-    if (const char *e = getenv("HSC_COLLECT_INFLIGHT")) k->max_inflight = std::max(1, std::min(atoi(e), 4));
-    if (const char *e = getenv("HSC_PREMARSHAL")) k->premarshal = atoi(e) != 0;
     *out = k;
     return HSC_OK;
 }

@@ -166,27 +166,19 @@ __global__ __launch_bounds__(256) void k_compact_probes(ProbeView p, CompactMeta
     }
 }
 
-template <int WC, bool kLds, int P>
+template <int WC, bool kLds>
 __global__ __launch_bounds__(kBoundThreads) void k_compact_bounds(ProbeView p, CompactMeta cm,
                                                                   uint64_t *clo, uint64_t *chi)
 {
-    const uint32_t q0 = blockIdx.x * (kBoundThreads * P) + threadIdx.x;
+    const uint32_t q = blockIdx.x * kBoundThreads + threadIdx.x;
     BoundIn cur;
-    bound_load(p, cm, q0, cur);
+    bound_load(p, cm, q, cur);
     if constexpr (kLds) {
         extern __shared__ __attribute__((aligned(16))) uint64_t blds[];
         stage_bound_tables<kBoundThreads>(cm, blds);
         __syncthreads();
     }
-#pragma unroll 1
-    for (int j = 0; j < P; ++j) {
-        const uint32_t q = q0 + j * kBoundThreads;
-        if (q >= p.n) break;
-        BoundIn nxt;
-        if (j + 1 < P) bound_load(p, cm, q + kBoundThreads, nxt);
-        bound_map<WC>(p, cm, q, cur, clo, chi);
-        if (j + 1 < P) cur = nxt;
-    }
+    if (q < p.n) bound_map<WC>(p, cm, q, cur, clo, chi);
 }
 
 template <int WC>
@@ -201,19 +193,15 @@ template <int WC>
 hipError_t launch_probes_wc(const ProbeView &p, const CompactMeta &cm, uint64_t *clo,
                             uint64_t *chi, hipStream_t s)
 {
-    static const bool generic = getenv("HSC_COMPACT_GENERIC") != nullptr;  // tests: old kernel
-    if (cm.W <= kProbeWords && !generic) {
-        static const int P = getenv("HSC_BOUND_P") ? atoi(getenv("HSC_BOUND_P")) : 1;  // A/B knob (r02: 1 beat 2 and 4 on config 3)
-        const uint32_t per = kBoundThreads * (P == 1 ? 1 : P == 4 ? 4 : 2);
-        const uint32_t blocks = (p.n + per - 1) / per;
+    // (r02: one probe per thread beat 2 and 4 in flight on config 3)
+    if (cm.W <= kProbeWords) {
+        const uint32_t blocks = (p.n + kBoundThreads - 1) / kBoundThreads;
         const bool in_lds = bound_lds_bytes(cm.ng, cm.W) <= kBoundLdsBytes;
         const uint32_t lds = in_lds ? bound_lds_bytes(cm.ng, cm.W) : 0;
-#define HSC_BOUNDS(L_, P_) k_compact_bounds<WC, L_, P_><<<blocks, kBoundThreads, lds, s>>>(p, cm, clo, chi)
         if (in_lds)
-            P == 1 ? HSC_BOUNDS(true, 1) : P == 4 ? HSC_BOUNDS(true, 4) : HSC_BOUNDS(true, 2);
+            k_compact_bounds<WC, true><<<blocks, kBoundThreads, lds, s>>>(p, cm, clo, chi);
         else
-            P == 1 ? HSC_BOUNDS(false, 1) : P == 4 ? HSC_BOUNDS(false, 4) : HSC_BOUNDS(false, 2);
-#undef HSC_BOUNDS
+            k_compact_bounds<WC, false><<<blocks, kBoundThreads, lds, s>>>(p, cm, clo, chi);
     } else
         k_compact_probes<WC><<<(p.n + 255) / 256, 256, 0, s>>>(p, cm, clo, chi);
     return hipGetLastError();

@@ -193,13 +193,12 @@ __device__ __forceinline__ uint32_t ct_count(const uint64_t *lf, uint32_t nt, co
     return l;
 }
 
-// kSort (work.local_items): no probe entries, slots or scatter -- the chunk's
-// records stay in registers until its tile histogram is complete, then each
+// No probe entries, slots or scatter: the chunk's records stay in registers until its tile histogram is complete, then each
 // goes whole (64 bytes: {key x, r(S) | read set | kind << 62} + {hi key} for a
 // full record; x = lo, or hi for a tail record) to its tile-sorted place in
 // the chunk's own area, and row g of the chunk-major table gets (run start
 // << 16 | count) per tile for k_plan_s (as the narrow locate)
-template <int WG, bool kSort>
+template <int WG>
 __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt, ProbeView p,
                                                            const uint64_t *clo,
                                                            const uint64_t *chi, ProbeWork work,
@@ -272,27 +271,12 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
                 }
                 // entries {lo[0..2], r(S) | read set << 32}, {hi[0..2], ...} (words past WG zero)
                 const uint64_t rt = (uint64_t)lsn32_rank(snap[k], ct.rank_base) | (uint64_t)txn << 32;
-                if constexpr (kSort) {
 #pragma unroll
-                    for (int j = 0; j < WG; ++j) KA[k][j] = a_[j], KB[k][j] = b_[j];
-                    RT[k] = rt;
-                    SL[k] = sl;
-                    continue;
-                }
-                uint64_t f[8] = {0, 0, 0, rt, 0, 0, 0, rt};
-#pragma unroll
-                for (int j = 0; j < WG; ++j) f[j] = a_[j], f[4 + j] = b_[j];
-                u64x2 *el = (u64x2 *)(ct.ent + (size_t)q * 4);
-                u64x2 *eh = (u64x2 *)(ct.ent + ((size_t)ct.np + q) * 4);
-                el[0] = u64x2{f[0], f[1]};
-                el[1] = u64x2{f[2], f[3]};
-                if (!point || bt > a) {  // a point's hi entry is never read
-                    eh[0] = u64x2{f[4], f[5]};
-                    eh[1] = u64x2{f[6], f[7]};
-                }
+                for (int j = 0; j < WG; ++j) KA[k][j] = a_[j], KB[k][j] = b_[j];
+                RT[k] = rt;
+                SL[k] = sl;
             }
         }
-        if constexpr (!kSort) ct.slot[q] = sl;
     }
     // table locks: any write to a locked table after the snapshot
     for (uint32_t q = g * kCLocThreads + threadIdx.x; q < p.n_lock; q += work.G * kCLocThreads) {
@@ -300,10 +284,7 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
         if (t < wt.ntables && wt.table_max[t] > p.lock_snap[q]) flags[p.lock_txn[q]] = 1;
     }
     __syncthreads();
-    if constexpr (!kSort) {
-        const uint32_t hs = hist_stride(work.G);
-        for (uint32_t i = threadIdx.x; i < nt; i += kCLocThreads) work.hist[(size_t)i * hs + g] = hist[i];
-    } else {
+    {
         const int lane = threadIdx.x & 63;
         uint32_t *wtot = (uint32_t *)(lb + L.wtot);
         const uint32_t per = (nt + kCLocThreads - 1) / kCLocThreads;
@@ -352,45 +333,6 @@ __global__ __launch_bounds__(kCLocThreads) void k_locate_c(CTiles ct, WinView wt
                 r2[0] = u64x2{b[0], b[1]};
                 r2[1] = u64x2{b[2], RT[k] | (uint64_t)kCTail << 62};
             }
-        }
-    }
-}
-
-// ---- scatter: 4-byte bucket entries ----
-__device__ __forceinline__ uint32_t ct_bucket_slot(const ProbeWork &work, uint32_t ntiles, uint32_t t,
-                                                   uint32_t pos)
-{
-    return pos < kTileCap ? t * kTileCap + pos
-                          : ntiles * kTileCap + work.bucket_off[t] + (pos - kTileCap);
-}
-
-__global__ __launch_bounds__(kCLocThreads) void k_scatter_c(CTiles ct, ProbeWork work, uint32_t n)
-{
-    extern __shared__ uint32_t soff[];  // [ntiles] this chunk's offset in each bucket
-    const uint32_t g = xcd_chunk(blockIdx.x, (work.G + 7) / 8);
-    if (g >= work.G) return;
-    const uint32_t nt = ct.ntiles;
-    const uint32_t c0 = g * work.chunk, c1 = min(n, c0 + work.chunk);
-    uint2 s[kCLocP];
-#pragma unroll
-    for (int k = 0; k < kCLocP; ++k) {
-        const uint32_t q = c0 + threadIdx.x + kCLocThreads * k;
-        s[k] = q < c1 ? ct.slot[q] : make_uint2(kNoSlot, kNoSlot);
-    }
-    const size_t hs = hist_stride(work.G);
-    for (uint32_t t = threadIdx.x; t < nt; t += kCLocThreads) soff[t] = work.hist[t * hs + g];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kCLocP; ++k) {
-        if (s[k].x == kNoSlot) continue;
-        const uint32_t q = c0 + threadIdx.x + kCLocThreads * k;
-        const bool two = (s[k].x & kSecondRec) != 0;
-        const uint32_t ta = (s[k].x & ~(kSecondRec | kPointRec)) >> 12;
-        const uint32_t kind = two ? kCHead : (s[k].x & kPointRec) ? kCPoint : kCFull;
-        ct.recs[ct_bucket_slot(work, nt, ta, soff[ta] + (s[k].x & 0xFFFu))] = q | kind << 30;
-        if (two) {
-            const uint32_t tb = s[k].y >> 12;
-            ct.recs[ct_bucket_slot(work, nt, tb, soff[tb] + (s[k].y & 0xFFFu))] = q | kCTail << 30;
         }
     }
 }
@@ -491,78 +433,7 @@ __device__ __forceinline__ void join_search(const ProbeWork &work, const CTiles 
     HSC_STAMP(work, 1, 5);
 }
 
-// One tile's records (kTile: tile xi, its bucket's first kTileCap records;
-// else overflow item xi of a hot tile).  The tile's record count / the item's
-// descriptor come by scalar loads and this thread's bucket entry by a vector
-// load issued before the tile's rows; the entry retires first (vector
-// counters retire in order), so the probe gather is issued while the rows
-// are in flight, and waiting for the scalar count drains no vector load.
-template <int WG, bool kTile>
-__device__ __forceinline__ void join_item(const ProbeWork &work, const CTiles &ct, uint8_t *flags,
-                                          uint32_t xi, uint64_t *kw, uint32_t *rank,
-                                          uint32_t *b16, uint32_t *b128, uint32_t *B)
-{
-    constexpr uint32_t T = kCTRows;
-    const uint32_t tid = threadIdx.x;
-    HSC_STAMP(work, 1, 0);
-    uint32_t tile, r0, r1, ev;
-    if constexpr (kTile) {
-        tile = xi;
-        r0 = tile * kTileCap;
-        ev = ct.recs[r0 + tid];  // a bucket always has kTileCap slots
-    } else {
-        const uint32_t *d = (const uint32_t *)(work.item_desc + xi);
-        tile = sload(d), r0 = sload(d + 1), r1 = sload(d + 2);
-        ev = ct.recs[min(r0 + tid, r1 - 1)];
-    }
-    const size_t row = ((size_t)tile << kCTLog2) + 2 * tid;
-    u64x2 kv[WG];
-#pragma unroll
-    for (int w = 0; w < WG; ++w) kv[w] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row);
-    const u32x2 rr = *(const u32x2 *)(ct.rank + row);
-    u32x2 bt = {0, 0};
-    if (tid < kTBS / 2) bt = *(const u32x2 *)(ct.tb + (size_t)tile * kTBS + 2 * tid);
-    if constexpr (kTile) r1 = r0 + min(kTileCap, sload(work.counts + tile));
-    // no early exit for a tile without records: it would let the compiler sink
-    // the row loads below the count's wait
-    const bool live = r0 + tid < r1;
-    const uint32_t kind = live ? ev >> 30 : kCPoint;
-    const uint32_t q = live ? ev & 0x3FFFFFFFu : 0;  // probe 0's entry stands in (no verdict is taken)
-    // a point or head record reads the lo entry, a tail record the hi entry, a
-    // full record both
-    const u64x2 *el = (const u64x2 *)(ct.ent + (size_t)q * 4);
-    const u64x2 *eh = (const u64x2 *)(ct.ent + ((size_t)ct.np + q) * 4);
-    u64x2 pl[2] = {}, ph0 = {};
-    uint64_t ph1 = 0;  // hi word 2 (a tail record's r(S) | read set comes from pl[1].y)
-    if (live && ct.dbg < 2) {
-        if (kind != kCTail) pl[0] = el[0], pl[1] = el[1];
-        if (kind == kCTail) pl[1].y = ((const uint64_t *)eh)[3];
-        if (kind == kCTail || kind == kCFull) ph0 = eh[0], ph1 = ((const uint64_t *)eh)[2];
-    }
-#pragma unroll
-    for (int w = 0; w < WG; ++w) *(u64x2 *)(kw + (size_t)w * T + 2 * tid) = kv[w];
-    *(u32x2 *)(rank + 2 * tid) = rr;
-    if (tid < kTBS / 2) *(u32x2 *)(B + 2 * tid) = bt;
-    uint32_t m = max(rr.x, rr.y);
-#pragma unroll
-    for (int d = 1; d < 8; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
-    if ((tid & 7) == 0) b16[tid >> 3] = m;
-#pragma unroll
-    for (int d = 8; d < 64; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
-    if ((tid & 63) == 0) b128[tid >> 6] = m;
-    HSC_STAMP(work, 1, 1);
-    __syncthreads();
-    HSC_STAMP(work, 1, 2);
-    if (live && !ct.dbg)
-        join_search<WG>(work, ct, flags, kw, rank, b16, b128, B, kind, pl, ph0, ph1);
-    else if (live && (pl[1].y | ph1 | kv[0].x) == 0x5A5A5A5A5A5A5A5Aull) flags[0] = 1;  // keep the loads
-#ifdef HSC_STAMPS
-    __syncthreads();
-    HSC_STAMP(work, 1, 6);
-#endif
-}
-
-// Chunk-sorted records (work.local_items): record j of the tile is in the run
+// Chunk-sorted records: record j of the tile is in the run
 // of the chunk whose offset inside the tile (k_plan_s's scan of the tile's
 // column) is the last one <= j.  The column is loaded first, staged, each
 // thread finds its record's chunk by a 9-step LDS search and loads the whole
@@ -637,12 +508,12 @@ __device__ __forceinline__ void join_item_s(const ProbeWork &work, const CTiles 
 #define HSC_CJOIN_XCD 0
 #endif
 constexpr bool kCJoinXcd = HSC_CJOIN_XCD != 0;
-__host__ __device__ inline uint32_t ct_tile_blocks(bool srt, uint32_t ntiles)
+__host__ __device__ inline uint32_t ct_tile_blocks(uint32_t ntiles)
 {
-    return srt && kCJoinXcd ? 8 * ((ntiles + 7) / 8) : ntiles;
+    return kCJoinXcd ? 8 * ((ntiles + 7) / 8) : ntiles;
 }
 
-template <int WG, bool kSort>
+template <int WG>
 __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_join_c(ProbeWork work, CTiles ct, uint8_t *flags)
 {
     constexpr uint32_t T = kCTRows;
@@ -654,116 +525,22 @@ __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
     uint32_t *b16 = rank + T;                            // [T / 16]
     uint32_t *b128 = b16 + T / 16;                       // [T / 128]
     uint32_t *B = b128 + T / 128;                        // [kTBS] the tile's bucket table
-    uint32_t *Es = B + kTBS;                              // kSort: the tile's column
+    uint32_t *Es = B + kTBS;                              // the tile's column
     uint16_t *Cs = (uint16_t *)(Es + kMaxChunks);         // (run starts < 2 * kCChunk)
     // the first xb blocks take the hot tiles' overflow items in turn (dispatched
     // first: they are the fullest), then one block per tile
-    const uint32_t xb = gridDim.x - ct_tile_blocks(kSort, ct.ntiles);
+    const uint32_t xb = gridDim.x - ct_tile_blocks(ct.ntiles);
     if (blockIdx.x >= xb) {
-        if constexpr (kSort) {
-            // neighbouring tiles on one XCD (they share lines of the chunk areas)
-            const uint32_t b = blockIdx.x - xb, tb = gridDim.x - xb;
-            const uint32_t tile = kCJoinXcd ? xcd_chunk(b, tb / 8) : b;
-            if (tile < ct.ntiles)
-                join_item_s<WG, true>(work, ct, flags, tile, kw, rank, b16, b128, B, Es, Cs);
-        } else
-            join_item<WG, true>(work, ct, flags, blockIdx.x - xb, kw, rank, b16, b128, B);
+        // neighbouring tiles on one XCD (they share lines of the chunk areas)
+        const uint32_t b = blockIdx.x - xb, tb = gridDim.x - xb;
+        const uint32_t tile = kCJoinXcd ? xcd_chunk(b, tb / 8) : b;
+        if (tile < ct.ntiles) join_item_s<WG, true>(work, ct, flags, tile, kw, rank, b16, b128, B, Es, Cs);
         return;
     }
     const uint32_t nextra = work.item_off[1];
     for (uint32_t xi = blockIdx.x; xi < nextra; xi += xb) {
         __syncthreads();  // the previous item's LDS reads are done
-        if constexpr (kSort)
-            join_item_s<WG, false>(work, ct, flags, xi, kw, rank, b16, b128, B, Es, Cs);
-        else
-            join_item<WG, false>(work, ct, flags, xi, kw, rank, b16, b128, B);
-    }
-}
-
-// Plan-free compact join (chunk-sorted records), as k_join_f of the narrow
-// tiles: the tile's column of the locate's chunk-major table is read and
-// scanned here, a hot tile's records past the first kCJT are joined by the
-// same block in further rounds, conflicts mark the flags (packed into the
-// verdict bytes by launch_pack_flags): locate -> join -> pack.
-template <int WG>
-__global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_join_cf(
-    ProbeWork work, CTiles ct, uint8_t *flags)
-{
-    constexpr uint32_t T = kCTRows;
-    extern __shared__ __attribute__((aligned(16))) uint64_t jl[];
-    uint64_t *kw = jl;                                   // [WG][T], sorted
-    uint32_t *rank = (uint32_t *)(jl + (size_t)WG * T);  // [T], sorted order
-    uint32_t *b16 = rank + T;                            // [T / 16]
-    uint32_t *b128 = b16 + T / 16;                       // [T / 128]
-    uint32_t *B = b128 + T / 128;                        // [kTBS] the tile's bucket table
-    uint32_t *Es = B + kTBS;                             // the tile's column: offsets
-    uint16_t *Cs = (uint16_t *)(Es + kMaxChunks);        // and run starts
-    __shared__ uint32_t wsum[kCJT / 64];
-    const uint32_t tid = threadIdx.x, tile = blockIdx.x;
-    const int lane = tid & 63, wv = tid >> 6;
-    if (tile < ct.ntiles) {
-        const uint32_t G = work.G, rs = (ct.ntiles + 3) & ~3u;
-        const uint32_t x = tid < G ? work.cm[(size_t)tid * rs + tile] : 0;
-        const size_t row = ((size_t)tile << kCTLog2) + 2 * tid;
-        u64x2 kv[WG];
-#pragma unroll
-        for (int w = 0; w < WG; ++w) kv[w] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row);
-        const u32x2 rr = *(const u32x2 *)(ct.rank + row);
-        u32x2 bt = {0, 0};
-        if (tid < kTBS / 2) bt = *(const u32x2 *)(ct.tb + (size_t)tile * kTBS + 2 * tid);
-        // exclusive scan of the column's counts
-        const uint32_t cnt = x & 0xFFFFu;
-        uint32_t inc = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += y;
-        }
-        if (lane == 63) wsum[wv] = inc;
-        __syncthreads();
-        uint32_t base = 0, total = 0;
-#pragma unroll
-        for (int w = 0; w < kCJT / 64; ++w) {
-            base += w < wv ? wsum[w] : 0;
-            total += wsum[w];
-        }
-        if (tid < G) Es[tid] = base + inc - cnt, Cs[tid] = (uint16_t)(x >> 16);
-        __syncthreads();
-        auto fetch = [&](uint32_t j, u64x2 &A0, u64x2 &A1, u64x2 &B0, u64x2 &B1) {
-            uint32_t g = 0;  // Es[0] = 0 <= j
-#pragma unroll
-            for (int b = 8; b >= 0; --b) {
-                const uint32_t c = g + (1u << b);
-                if (c < G && Es[c] <= j) g = c;
-            }
-            const u64x2 *r = (const u64x2 *)ct.recs + 4 * ((size_t)g * 2 * work.chunk + Cs[g] + (j - Es[g]));
-            A0 = r[0], A1 = r[1], B0 = r[2], B1 = r[3];
-        };
-        u64x2 A0 = {}, A1 = {}, B0 = {}, B1 = {};
-        if (tid < total) fetch(tid, A0, A1, B0, B1);  // while the rows arrive
-#pragma unroll
-        for (int w = 0; w < WG; ++w) *(u64x2 *)(kw + (size_t)w * T + 2 * tid) = kv[w];
-        *(u32x2 *)(rank + 2 * tid) = rr;
-        if (tid < kTBS / 2) *(u32x2 *)(B + 2 * tid) = bt;
-        uint32_t m = max(rr.x, rr.y);
-#pragma unroll
-        for (int d = 1; d < 8; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
-        if ((tid & 7) == 0) b16[tid >> 3] = m;
-#pragma unroll
-        for (int d = 8; d < 64; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
-        if ((tid & 63) == 0) b128[tid >> 6] = m;
-        __syncthreads();
-        for (uint32_t j0 = 0; j0 < total; j0 += kCJT) {
-            const uint32_t j = j0 + tid;
-            if (j >= total) continue;
-            if (j0) fetch(j, A0, A1, B0, B1);  // a hot tile's further rounds
-            const uint32_t kind = (uint32_t)(A1.y >> 62);
-            const uint64_t rt = A1.y & ((1ull << 62) - 1);
-            u64x2 pl[2] = {A0, u64x2{A1.x, rt}}, ph0 = B0;
-            uint64_t ph1 = B1.x;
-            if (kind == kCTail) ph0 = A0, ph1 = A1.x;  // a tail record carries hi in its first half
-            join_search<WG>(work, ct, flags, kw, rank, b16, b128, B, kind, pl, ph0, ph1);
-        }
+        join_item_s<WG, false>(work, ct, flags, xi, kw, rank, b16, b128, B, Es, Cs);
     }
 }
 
@@ -799,14 +576,8 @@ hipError_t launch_locate_c(const CTiles &ct, const WinView &wt, const ProbeView 
     if (p.n == 0 && p.n_lock == 0) return hipSuccess;
     const size_t lds = cloc_lds(ct).bytes;
     const uint32_t blocks = 8 * ((work.G + 7) / 8);
-#define HSC_LOC_C(WG_)                                                                              \
-    do {                                                                                            \
-        if (work.local_items)                                                                       \
-            k_locate_c<WG_, true><<<blocks, kCLocThreads, lds, s>>>(ct, wt, p, clo, chi, work, flags); \
-        else                                                                                        \
-            k_locate_c<WG_, false><<<blocks, kCLocThreads, lds, s>>>(ct, wt, p, clo, chi, work,      \
-                                                                     flags);                        \
-    } while (0)
+#define HSC_LOC_C(WG_) \
+    k_locate_c<WG_><<<blocks, kCLocThreads, lds, s>>>(ct, wt, p, clo, chi, work, flags)
     switch (ct.WG) {
     case 1: HSC_LOC_C(1); break;
     case 2: HSC_LOC_C(2); break;
@@ -817,44 +588,15 @@ hipError_t launch_locate_c(const CTiles &ct, const WinView &wt, const ProbeView 
     return hipGetLastError();
 }
 
-hipError_t launch_scatter_c(const CTiles &ct, const ProbeWork &work, uint32_t n, hipStream_t s)
-{
-    if (n == 0) return hipSuccess;
-    k_scatter_c<<<8 * ((work.G + 7) / 8), kCLocThreads, 4 * (size_t)ct.ntiles, s>>>(ct, work, n);
-    return hipGetLastError();
-}
-
-hipError_t launch_join_cf(const CTiles &ct, const ProbeWork &work, uint8_t *flags, hipStream_t s)
-{
-    if (ct.ntiles == 0) return hipSuccess;
-    const size_t lds = 8 * (size_t)ct.WG * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
-                       4 * (kCTRows / 128) + 4 * kTBS + 6 * (size_t)kMaxChunks;
-    switch (ct.WG) {
-    case 1: k_join_cf<1><<<ct.ntiles, kCJT, lds, s>>>(work, ct, flags); break;
-    case 2: k_join_cf<2><<<ct.ntiles, kCJT, lds, s>>>(work, ct, flags); break;
-    case 3: k_join_cf<3><<<ct.ntiles, kCJT, lds, s>>>(work, ct, flags); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
 hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_items,
                          uint8_t *flags, hipStream_t s)
 {
     if (max_items == 0 || ct.n == 0 || ct.ntiles == 0) return hipSuccess;
     const uint32_t extra = max_items - ct.ntiles;
-    const uint32_t blocks =
-        ct_tile_blocks(work.local_items != 0, ct.ntiles) + (extra < 512 ? extra : 512);
-    const bool srt = work.local_items != 0;
+    const uint32_t blocks = ct_tile_blocks(ct.ntiles) + (extra < 512 ? extra : 512);
     const size_t lds = 8 * (size_t)ct.WG * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
-                       4 * (kCTRows / 128) + 4 * kTBS + (srt ? 6 * (size_t)kMaxChunks : 0);
-#define HSC_JOIN_C(WG_)                                                                   \
-    do {                                                                                  \
-        if (srt)                                                                          \
-            k_join_c<WG_, true><<<blocks, kCJT, lds, s>>>(work, ct, flags);               \
-        else                                                                              \
-            k_join_c<WG_, false><<<blocks, kCJT, lds, s>>>(work, ct, flags);              \
-    } while (0)
+                       4 * (kCTRows / 128) + 4 * kTBS + 6 * (size_t)kMaxChunks;
+#define HSC_JOIN_C(WG_) k_join_c<WG_><<<blocks, kCJT, lds, s>>>(work, ct, flags)
     switch (ct.WG) {
     case 1: HSC_JOIN_C(1); break;
     case 2: HSC_JOIN_C(2); break;

@@ -301,11 +301,6 @@ struct hsc_ctx {
     bool has_commits = false;  // the window has rows and a commit span (narrow / compact tiles)
     uint64_t commit_span[2] = {0, 0};  // oldest / newest distinct commit LSN of the window
     bool rank_lsn32 = false;   // narrow tiles: rows carry lsn - rank_base + 1 (NarrowTiles)
-    bool nt_sorted = true;     // narrow tiles: chunk-sorted records (HSC_NT_SORT=0 at build: scatter)
-    bool nt_fused = false;     // chunk-sorted narrow tiles: plan-free join (HSC_NT_FUSED=1 at build;
-                               // r03: one stream 61.9 -> 60.2 us, two streams 45.3 -> 47.7 us)
-    bool ct_sorted = true;     // compact tiles: chunk-sorted records (HSC_CT_SORT=0 at build: scatter)
-    bool ct_fused = false;     // ... and the plan-free join (HSC_CT_FUSED=1 at build; measured slower)
     uint64_t rank_base = 0;
     DBuf w_tcode, w_tcode2, w_trecs;
     DBuf d_gid, d_words, d_lsn, d_gid2, d_words2, d_lsn2, d_flags, d_scratch;

@@ -404,8 +404,6 @@ static int build_ctiles(hsc_ctx *c)
         return HSC_OK;
     CTiles &ct = c->ctv;
     ct = CTiles{};
-    c->ct_sorted = !getenv("HSC_CT_SORT") || atoi(getenv("HSC_CT_SORT")) != 0;
-    c->ct_fused = getenv("HSC_CT_FUSED") && atoi(getenv("HSC_CT_FUSED")) != 0;
     ct.n = (uint32_t)c->n;
     ct.ntiles = v.ntiles;
     ct.len = (size_t)v.ntiles << kCTLog2;
@@ -459,7 +457,7 @@ static int build_ctiles(hsc_ctx *c)
 // Narrow tiles' bucket table: linear buckets (uniform keys) or log buckets
 // (keys dense near the window's first, e.g. Zipf hot keys) -- whichever mode's
 // fullest bucket holds fewer tiles (the locate's in-bucket search is
-// log2 of it).  HSC_TRAD_MODE=lin|log forces one (tests).
+// log2 of it).
 static int narrow_trad_pick(hsc_ctx *c)
 {
     const uint32_t m = c->trad_m;
@@ -471,8 +469,7 @@ static int narrow_trad_pick(hsc_ctx *c)
         for (uint32_t k = 0; k < m; ++k) w = std::max(w, t[k + 1] - t[k]);
         return w;
     };
-    const char *f = getenv("HSC_TRAD_MODE");
-    const bool log = f ? strcmp(f, "log") == 0 : fullest(b) < fullest(a);
+    const bool log = fullest(b) < fullest(a);
     if (log) std::swap(c->d_trad, c->d_trad2);
     c->trad_log = log;
     return HSC_OK;
@@ -536,13 +533,13 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, hipEventRecord(e0, s));
     // varying key bits and the LSN span in one pass; the distinct commit list
     // only when snapshot ranks need its directory (a window spanning >= 2^32
-    // of log, or HSC_RANK_DIR): otherwise rows carry lsn - oldest + 1
+    // of log): otherwise rows carry lsn - oldest + 1
     uint64_t vary[kMaxWords + 1], span[2];
     HIPCHK(c, vary_mask_rows(W, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(), cap,
                              c->d_scratch.p, vary, s, c->d_lsn.as<uint64_t>(), span));
     bt.stamp("vary");
     const bool commits = c->layout != HSC_LAYOUT_WIDE && n_in > 0;
-    const bool rank_dir = commits && (span[1] - span[0] > kLsn32MaxSpan || getenv("HSC_RANK_DIR"));
+    const bool rank_dir = commits && span[1] - span[0] > kLsn32MaxSpan;
     c->has_commits = commits;
     c->ncommit = 0;
     if (commits) memcpy(c->commit_span, span, 16);
@@ -550,8 +547,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
     bt.stamp("commits");
     PackPlan plan;
     c->packed_sort = try_packed && packed_plan(W, n_in, vary, &plan);
-    const bool fused_dd = !getenv("HSC_PK_DD") || atoi(getenv("HSC_PK_DD")) != 0;
-    if (c->packed_sort && fused_dd) {
+    if (c->packed_sort) {
         // every version, key-sorted, into d_*2; the distinct rows straight from
         // the unpack into d_gid / d_words (in place) and a free key buffer,
         // which becomes d_lsn (the input LSNs are gathered while it is written)
@@ -567,19 +563,6 @@ static int device_build(hsc_ctx *c, size_t n_in)
         else if (dl == c->d_pk[1].p)
             std::swap(c->d_lsn, c->d_pk[1]);
         bt.stamp("sort");
-    } else if (c->packed_sort) {
-        // every version, key-sorted, into d_*2; the distinct rows into d_*
-        HIPCHK(c, packed_sort_rows(plan, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
-                                   c->d_lsn.as<uint64_t>(), cap, c->d_pk[0].as<uint64_t>(),
-                                   c->d_pk[1].as<uint64_t>(), c->d_gid2.as<uint32_t>(),
-                                   c->d_words2.as<uint64_t>(), c->d_lsn2.as<uint64_t>(), cap,
-                                   c->d_flags.as<uint32_t>(), c->d_scratch.p, c->d_scratch.bytes, s));
-        bt.stamp("sort");
-        HIPCHK(c, dedupe_flagged(W, n_in, c->d_gid2.as<uint32_t>(), c->d_words2.as<uint64_t>(),
-                                 c->d_lsn2.as<uint64_t>(), cap, c->d_gid.as<uint32_t>(),
-                                 c->d_words.as<uint64_t>(), c->d_lsn.as<uint64_t>(), cap,
-                                 c->d_flags.as<uint32_t>(), c->d_scratch.p, c->d_scratch.bytes,
-                                 c->d_count.as<uint32_t>(), s));
     } else {
         bool in_alt = false;
         HIPCHK(c, radix_sort_known(W, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
@@ -754,9 +737,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
         if (wn.log2T == 12 && wn.ntiles <= (uint32_t)kHistCap && c->has_commits) {
             // commit span: rank-free rows (lsn - oldest commit + 1) when it fits 32 bits
             const uint64_t *span = c->commit_span;
-            c->rank_lsn32 = span[1] - span[0] <= kLsn32MaxSpan && !getenv("HSC_RANK_DIR");
-            c->nt_sorted = !getenv("HSC_NT_SORT") || atoi(getenv("HSC_NT_SORT")) != 0;
-            c->nt_fused = getenv("HSC_NT_FUSED") && atoi(getenv("HSC_NT_FUSED")) != 0;
+            c->rank_lsn32 = span[1] - span[0] <= kLsn32MaxSpan;
             c->rank_base = span[0];
             c->cdir = Dir16{};
             if (!c->rank_lsn32)
@@ -1088,8 +1069,7 @@ static void swap_window(hsc_ctx *a, hsc_ctx *b)
     swap(a->cdir, b->cdir), swap(a->tdir, b->tdir), swap(a->trad_m, b->trad_m);
     swap(a->trad_log, b->trad_log), swap(a->ncommit, b->ncommit), swap(a->has_commits, b->has_commits);
     swap(a->commit_span[0], b->commit_span[0]), swap(a->commit_span[1], b->commit_span[1]);
-    swap(a->rank_lsn32, b->rank_lsn32), swap(a->nt_sorted, b->nt_sorted), swap(a->nt_fused, b->nt_fused);
-    swap(a->ct_sorted, b->ct_sorted), swap(a->ct_fused, b->ct_fused), swap(a->rank_base, b->rank_base);
+    swap(a->rank_lsn32, b->rank_lsn32), swap(a->rank_base, b->rank_base);
     swap(a->d_gid, b->d_gid), swap(a->d_words, b->d_words), swap(a->d_lsn, b->d_lsn);
     swap(a->d_gid2, b->d_gid2), swap(a->d_words2, b->d_words2), swap(a->d_lsn2, b->d_lsn2);
     swap(a->d_flags, b->d_flags), swap(a->d_scratch, b->d_scratch);
@@ -1954,22 +1934,13 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     const uint32_t extra_items = 2 * (uint32_t)((2 * n1 + kJoinChunk - 1) / kJoinChunk);
     const uint32_t max_items = nt + extra_items;
     HIPCHK(c, c->w_item_desc.ensure(16 * (size_t)extra_items + 16));
-    // chunk-sorted records (default; HSC_NT_SORT=0 at the window build:
-    // probe-order records + the scatter into tile buckets): each chunk's
-    // records in an area of its own, no scatter pass
-    const bool sorted = c->nt_sorted;
-    work.local_items = sorted;
-    if (sorted) {
-        HIPCHK(c, c->w_tcode2.ensure(2 * (size_t)hist_stride(work.G) * nt));  // cst
-        HIPCHK(c, c->w_tcode.ensure(4 * (size_t)work.G * ((nt + 3) & ~3u)));  // chunk-major rows
-        HIPCHK(c, c->w_trecs.ensure(16 * 2 * (size_t)work.chunk * work.G));
-        work.cst = c->w_tcode2.as<uint16_t>();
-        work.cm = c->w_tcode.as<uint32_t>();
-    } else {
-        HIPCHK(c, c->w_tcode.ensure(16 * n1));
-        HIPCHK(c, c->w_tcode2.ensure(16 * n1));
-        HIPCHK(c, c->w_trecs.ensure(16 * ((size_t)nt * kTileCap + 2 * n1)));
-    }
+    // chunk-sorted records: each chunk's records in an area of its own, tile
+    // runs found by the join through the plan's scan (no scatter pass)
+    HIPCHK(c, c->w_tcode2.ensure(2 * (size_t)hist_stride(work.G) * nt));  // cst
+    HIPCHK(c, c->w_tcode.ensure(4 * (size_t)work.G * ((nt + 3) & ~3u)));  // chunk-major rows
+    HIPCHK(c, c->w_trecs.ensure(16 * 2 * (size_t)work.chunk * work.G));
+    work.cst = c->w_tcode2.as<uint16_t>();
+    work.cm = c->w_tcode.as<uint32_t>();
     work.hist = c->w_hist.as<uint32_t>();
     work.counts = c->w_counts.as<uint32_t>();
     work.bucket_off = c->w_bucket.as<uint32_t>();
@@ -1996,8 +1967,6 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     ntl.tdir = c->tdir;
     ntl.trad = c->trad_m ? c->d_trad.as<uint32_t>() : nullptr;
     ntl.trad_m = c->trad_m;
-    ntl.code = c->w_tcode.as<uint4>();
-    ntl.code2 = c->w_tcode2.as<uint4>();
     ntl.recs = c->w_trecs.as<uint4>();
     // conflict flags: internal, all zero between batches (the pack clears them)
     const size_t had = c->w_vflags.bytes;
@@ -2011,26 +1980,12 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
     HIPCHK(c, launch_locate_t(c->nv, wn, p, work, ntl, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
-    if (p.n && wn.ntiles && sorted && c->nt_fused) {
-        // plan-free: the join scans its tile's column itself and marks the
-        // flags (as the delta probe before it); the pack writes the verdict
-        // bytes.  (A last-block pack inside the join measured 2x slower: every
-        // block's device-scope release before its arrival count writes back
-        // its XCD's L2.)
-        if (tm)
-            for (int i = 2; i <= 3; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
-        HIPCHK_RC(c, probe_delta(c, flags));
-        HIPCHK(c, launch_join_f(work, ntl, wn.n, wn.ntiles, flags, s));
-        if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
-        HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
-    } else if (p.n && wn.ntiles) {
+    if (p.n && wn.ntiles) {
         // the plan writes the verdict bytes from the locate's flags; the join
         // and the delta probe then mark the verdict itself
-        HIPCHK(c, (sorted ? launch_plan_s : launch_plan_t)(work, wn.ntiles,
-                                                          c->w_items.as<uint32_t>(), s, flags,
-                                                          (uint32_t)b->n_txn, b->verdict));
+        HIPCHK(c, launch_plan_s(work, wn.ntiles, c->w_items.as<uint32_t>(), s, flags,
+                                (uint32_t)b->n_txn, b->verdict));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
-        if (!sorted) HIPCHK(c, launch_scatter_t(p, work, ntl, wn.ntiles, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
         HIPCHK(c, launch_join_t(work, ntl, wn.n, wn.ntiles, max_items, b->verdict, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
@@ -2044,7 +1999,7 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     }
     if (tm) HIPCHK(c, hipEventRecord(c->ev[5], s));
 #ifdef HSC_STAMPS
-    HIPCHK_RC(c, stamp_report(c, work, max_items, sorted ? 6 : 5, 4));
+    HIPCHK_RC(c, stamp_report(c, work, max_items, 6, 4));
 #endif
     return HSC_OK;
 }
@@ -2075,29 +2030,19 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
     const uint32_t extra_items = 2 * (uint32_t)((2 * n1 + kJoinChunk - 1) / kJoinChunk);
     const uint32_t max_items = nt + extra_items;
     HIPCHK(c, c->w_item_desc.ensure(16 * (size_t)extra_items + 16));
-    // chunk-sorted 64-byte records (default; the read set number shares its
-    // word with the record kind, so batches of >= 2^30 read sets and
-    // HSC_CT_SORT=0 windows take probe entries + the scatter)
-    const bool sorted = c->ct_sorted && b->n_txn < (1u << 30);
-    work.local_items = sorted;
-    if (sorted) {
-        HIPCHK(c, c->w_tcode.ensure(4 * (size_t)work.G * ((nt + 3) & ~3u)));  // chunk-major rows
-        HIPCHK(c, c->w_tcode2.ensure(2 * (size_t)hist_stride(work.G) * nt));  // run starts
-        HIPCHK(c, c->w_trecs.ensure(64 * 2 * (size_t)work.chunk * work.G));
-        work.cm = c->w_tcode.as<uint32_t>();
-        work.cst = c->w_tcode2.as<uint16_t>();
-    } else {
-        HIPCHK(c, c->w_tcode.ensure(64 * n1));  // probe entries
-        HIPCHK(c, c->w_tcode2.ensure(8 * n1));  // slots
-        HIPCHK(c, c->w_trecs.ensure(4 * ((size_t)nt * kTileCap + 2 * n1)));
-    }
+    // chunk-sorted 64-byte records (the read set number shares its word with
+    // the record kind: the caller sends batches of >= 2^30 read sets down the
+    // wide pipeline)
+    HIPCHK(c, c->w_tcode.ensure(4 * (size_t)work.G * ((nt + 3) & ~3u)));  // chunk-major rows
+    HIPCHK(c, c->w_tcode2.ensure(2 * (size_t)hist_stride(work.G) * nt));  // run starts
+    HIPCHK(c, c->w_trecs.ensure(64 * 2 * (size_t)work.chunk * work.G));
+    work.cm = c->w_tcode.as<uint32_t>();
+    work.cst = c->w_tcode2.as<uint16_t>();
     work.hist = c->w_hist.as<uint32_t>();
     work.counts = c->w_counts.as<uint32_t>();
     work.bucket_off = c->w_bucket.as<uint32_t>();
     work.item_off = c->w_items.as<uint32_t>();
     work.item_desc = c->w_item_desc.as<uint4>();
-    ct.ent = c->w_tcode.as<uint64_t>();
-    ct.slot = c->w_tcode2.as<uint2>();
     ct.recs = c->w_trecs.as<uint32_t>();
     ct.np = p.n;
 #ifdef HSC_STAMPS
@@ -2131,22 +2076,11 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
     HIPCHK(c, launch_locate_c(ct, wt, p, c->p_code_lo.as<uint64_t>(), c->p_code_hi.as<uint64_t>(),
                               work, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
-    if (p.n && ct.ntiles && sorted && c->ct_fused) {
-        // plan-free, as probe_ntiles: the join scans its column and marks
-        // the flags; the pack writes the verdict bytes
-        if (tm)
-            for (int i = 2; i <= 3; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
-        HIPCHK_RC(c, probe_delta(c, flags));
-        HIPCHK(c, launch_join_cf(ct, work, flags, s));
-        if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
-        HIPCHK(c, launch_pack_flags(flags, (uint32_t)b->n_txn, b->verdict, b->bitmap, s));
-    } else if (p.n && ct.ntiles) {
+    if (p.n && ct.ntiles) {
         // pack folded into the plan, as probe_ntiles
-        HIPCHK(c, (sorted ? launch_plan_s : launch_plan_t)(work, ct.ntiles,
-                                                          c->w_items.as<uint32_t>(), s, flags,
-                                                          (uint32_t)b->n_txn, b->verdict));
+        HIPCHK(c, launch_plan_s(work, ct.ntiles, c->w_items.as<uint32_t>(), s, flags,
+                                (uint32_t)b->n_txn, b->verdict));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
-        if (!sorted) HIPCHK(c, launch_scatter_c(ct, work, p.n, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
         HIPCHK(c, launch_join_c(ct, work, max_items, b->verdict, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
@@ -2214,7 +2148,7 @@ static int probe_lane(hsc_ctx *c, const hsc_probe_batch *b)
     // ranges per tile) takes the wide pipeline, which stages only the tiles
     // its ranges reach (the compact-tile join stages every tile)
     if (!c->narrow && c->compact && c->ctiles && c->layout != HSC_LAYOUT_COMPACT_WIDE &&
-        p.n < (1u << 30) && (size_t)p.n >= kDirectPerTile * (size_t)c->ctv.ntiles &&
+        p.n < (1u << 30) && b->n_txn < (1u << 30) && (size_t)p.n >= kDirectPerTile * (size_t)c->ctv.ntiles &&
         (std::max<size_t>(p.n, p.n_lock) + ctiles_chunk() - 1) / ctiles_chunk() <= (size_t)kMaxChunks)
         return probe_ctiles(c, b, p);
     if (!c->narrow && c->compact) {

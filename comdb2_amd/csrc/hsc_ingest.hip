@@ -214,57 +214,8 @@ __global__ __launch_bounds__(kPkThreads) void k_pk_scatter(int sh, size_t n, con
     }
 }
 
-// Sorted keys -> rows (every version, key order) + last-of-key flags.
-constexpr int kUnpackThreads = 256;
-template <int WT>  // key words 1..3, 0 = any (<= kPackMaxWords)
-__global__ __launch_bounds__(kUnpackThreads) void k_pk_unpack(
-    PackPlan P, size_t n, const uint64_t *keys, const uint32_t *gid_in, const uint64_t *words_in,
-    const uint64_t *lsn_in, size_t stride_in, uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o,
-    size_t stride_o, uint32_t *flags)
-{
-    const size_t i = (size_t)blockIdx.x * kUnpackThreads + threadIdx.x;
-    if (i >= n) return;
-    const int W = WT ? WT : P.W;
-    const uint64_t key = keys[i];
-    const uint64_t imask = P.I >= 64 ? ~0ull : (1ull << P.I) - 1;
-    uint64_t kb = key >> P.I;
-    const uint64_t idx = key & imask;
-    const bool last = i + 1 == n || (keys[i + 1] >> P.I) != kb;
-    const uint64_t lv = lsn_in[idx];
-    // limbs: row 0's value (the constant bits), varying bits expanded over it
-    uint64_t limb[kPackMaxWords + 1];
-#pragma unroll
-    for (int j = 0; j <= kPackMaxWords; ++j) {
-        if (j > W) break;
-        limb[j] = j == W ? (uint64_t)gid_in[0] : words_in[(size_t)j * stride_in];
-    }
-#pragma unroll
-    for (int l = kPackLimbs - 1; l >= 0; --l) {  // least significant varying limb first
-        if (l >= P.nl) continue;
-        const int b = P.bits[l];
-        const uint64_t part = b >= 64 ? kb : kb & ((1ull << b) - 1);
-        kb = b >= 64 ? 0 : kb >> b;
-        uint64_t mv[6];
-#pragma unroll
-        for (int q = 0; q < 6; ++q) mv[q] = P.mv[l][q];
-        const int id = P.limb[l];
-        const uint64_t v = pk_expand(part, P.mask[l], mv);
-#pragma unroll
-        for (int j = 0; j <= kPackMaxWords; ++j)
-            if (j == id) limb[j] = (limb[j] & ~P.mask[l]) | v;
-    }
-    gid_o[i] = (uint32_t)limb[W];
-#pragma unroll
-    for (int j = 0; j < kPackMaxWords; ++j) {
-        if (j >= W) break;
-        words_o[(size_t)j * stride_o + i] = limb[j];
-    }
-    lsn_o[i] = lv;
-    flags[i] = last ? 1u : 0u;
-}
-
 // ---- unpack fused with the dedupe ----
-// Every version goes to (gid_o, words_o, lsn_o) as in k_pk_unpack, and the
+// Every version goes to (gid_o, words_o, lsn_o) in key order, and the
 // last version of each key straight to its place among the distinct rows
 // (gid_d, words_d, lsn_d): a block's place is the exclusive scan of the
 // blocks' distinct counts (k_pk_bcount), a row's inside the block a scan in
@@ -518,31 +469,6 @@ hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, 
         HSC_UNPACK_DD(0);
 #undef HSC_UNPACK_DD
     *lsn_d = kfree;
-    return hipGetLastError();
-}
-
-hipError_t packed_sort_rows(const PackPlan &P, size_t n, const uint32_t *gid, const uint64_t *words,
-                            const uint64_t *lsn, size_t stride, uint64_t *k0, uint64_t *k1,
-                            uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
-                            uint32_t *flags, void *scratch, size_t scratch_bytes, hipStream_t s)
-{
-    if (n == 0) return hipSuccess;
-    if (scratch_bytes < packed_scratch_bytes(n)) return hipErrorInvalidValue;
-    uint64_t *kf, *kfree;
-    hipError_t e = packed_passes(P, n, gid, words, stride, k0, k1, scratch, s, &kf, &kfree);
-    if (e != hipSuccess) return e;
-    const unsigned g = (unsigned)((n + kUnpackThreads - 1) / kUnpackThreads);
-#define HSC_UNPACK(WT_) k_pk_unpack<WT_><<<g, kUnpackThreads, 0, s>>>(P, n, kf, gid, words, lsn, stride, \
-                                                                    gid_o, words_o, lsn_o, stride_o, flags)
-    if (P.W == 1)
-        HSC_UNPACK(1);
-    else if (P.W == 2)
-        HSC_UNPACK(2);
-    else if (P.W == 3)
-        HSC_UNPACK(3);
-    else
-        HSC_UNPACK(0);
-#undef HSC_UNPACK
     return hipGetLastError();
 }
 

@@ -158,12 +158,7 @@ struct PackPlan {
 };
 bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P);  // false: does not fit
 size_t packed_scratch_bytes(size_t n);
-// sorted rows (every version, stride_o) + last-of-key flags; k0 / k1: n words each
-hipError_t packed_sort_rows(const PackPlan &P, size_t n, const uint32_t *gid, const uint64_t *words,
-                            const uint64_t *lsn, size_t stride, uint64_t *k0, uint64_t *k1,
-                            uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
-                            uint32_t *flags, void *scratch, size_t scratch_bytes, hipStream_t s);
-// the same sort with the dedupe fused into the unpack: every version to
+// The packed sort with the dedupe fused into the unpack: every version to
 // (gid_o, words_o, lsn_o), the distinct rows to (gid_d, words_d) -- which may
 // be the input gid / words -- and to *lsn_d = whichever of k0 / k1 the sorted
 // keys did not end in; d_count[0] = distinct rows
@@ -182,7 +177,7 @@ struct ProbeWork {
     uint64_t *code;        // [n] a | b << 31 | kind << 62
     uint32_t *hist;        // [G][ntiles] per-chunk record counts -> offsets
     uint32_t *counts;      // [ntiles + 1] records per tile
-    uint32_t *bucket_off;  // [ntiles + 1]
+    uint32_t *bucket_off;  // [ntiles + 1] (wide pipeline)
     uint32_t *cursor;      // [ntiles] (global-atomic mode, ntiles > kHistCap)
     uint32_t *item_off;    // [ntiles + 1]
     uint32_t *item_tile;   // [max items]
@@ -191,12 +186,11 @@ struct ProbeWork {
     uint32_t G, chunk;     // probe chunks (one workgroup each in locate/scatter)
     int lds_mode;          // ntiles <= kHistCap: LDS histograms, no global atomics
     uint64_t *stamps;      // diagnostic builds (HSC_STAMPS): [kernel][block][8] s_memtime
-    // chunk-sorted narrow records (no scatter pass): chunk g's records sit in
+    // chunk-sorted records (narrow / compact tiles, no scatter pass): chunk g's records sit in
     // its own area of 2 * chunk records sorted by tile; cst[t][g] = where tile
     // t's run starts in it; join items are tile-local record ranges
     uint16_t *cst;
     uint32_t *cm;  // [G][round4(ntiles)] chunk-major (run start << 16 | count), the locate's rows
-    int local_items;
 };
 // Diagnostic phase stamps (HSC_STAMPS builds only): thread 0 of a block
 // records s_memtime at phase boundaries into a buffer of its own (never an
@@ -288,9 +282,7 @@ struct NarrowTiles {
                                // (trad[k] = #first < k << shift; trad[m + 1] = shift),
                                // nullptr: search tdir instead
     uint32_t trad_m;           // buckets (power of two)
-    uint4 *code;               // [n] first record {tile << 12 | rank, lo, hi, r(S)}
-    uint4 *code2;              // [n] second record (flag kHasSecond in code.x)
-    uint4 *recs;               // [2n] {lo delta, hi delta, snapshot rank, read set}
+    uint4 *recs;               // chunk areas of 2 x chunk records {lo delta, hi delta, r(S), read set}
 };
 hipError_t check_sorted_u64(const uint64_t *v, size_t n, uint32_t *flag, hipStream_t s);
 // rank32 by a search of cdir (the 16-ary directory over the commit LSNs C)
@@ -399,16 +391,12 @@ __host__ __device__ inline uint32_t hist_stride(uint32_t G) { return (G + 7) & ~
 // XCD-contiguous chunk order: block b of a grid of 8 * per blocks runs on XCD
 // b % 8 and takes chunk (b % 8) * per + b / 8.
 __host__ __device__ inline uint32_t xcd_chunk(uint32_t b, uint32_t per) { return (b & 7) * per + (b >> 3); }
-// Column scans of the tile-major histogram into fixed-capacity tile buckets
-// (ctl[0..1]: overflow records / extra join items, zeroed by the locate).
-// verdict != nullptr: the plan also writes the batch's verdict bytes from the
-// locate's flags (clearing them), so the join and the delta probe mark the
-// verdict directly and no pack pass is needed (pack folded into the plan)
-hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, hipStream_t s,
-                         uint8_t *flags = nullptr, uint32_t n_txn = 0,
-                         uint8_t *verdict = nullptr);
-// the plan of chunk-sorted narrow records (work.local_items): transposes the
+// The plan of chunk-sorted records (narrow and compact tiles): transposes the
 // locate's chunk-major table into the tile-major offsets and run starts
+// (ctl[1]: extra join items of hot tiles, zeroed by the locate).  It also
+// writes the batch's verdict bytes from the locate's flags (clearing them),
+// so the join and the delta probe mark the verdict directly and no pack pass
+// is needed (pack folded into the plan)
 hipError_t launch_plan_s(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, hipStream_t s,
                          uint8_t *flags, uint32_t n_txn, uint8_t *verdict);
 // Verdict bytes + bitmap from the internal conflict flags; clears the flags.
@@ -417,12 +405,6 @@ hipError_t launch_pack_flags(uint8_t *flags, uint32_t n_txn, uint8_t *verdict, u
 hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeView &p,
                            const ProbeWork &work, const NarrowTiles &nt, uint8_t *verdict,
                            hipStream_t s);
-hipError_t launch_scatter_t(const ProbeView &p, const ProbeWork &work, const NarrowTiles &nt,
-                            uint32_t ntiles, hipStream_t s);
-// Plan-free join of chunk-sorted records (tile columns scanned in the join;
-// conflicts into flags, packed by launch_pack_flags).
-hipError_t launch_join_f(const ProbeWork &work, const NarrowTiles &nt, uint32_t n, uint32_t ntiles,
-                         uint8_t *flags, hipStream_t s);
 hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t n,
                          uint32_t ntiles, uint32_t max_items, uint8_t *verdict, hipStream_t s);
 // Dependency graph + SCC (hsc_graph.hip).
@@ -513,11 +495,8 @@ struct CTiles {
     size_t len;              // row stride (n rounded up to whole tiles)
     uint32_t n, ntiles;
     int WG, WC, gb;          // key words, code words, group bits
-    uint64_t *ent;           // [2][np][4] probe entries: {lo[3], r(S) | read set << 32}, then
-                             // {hi[3], r(S) | read set << 32}
     uint32_t np;             // probes of the batch
-    uint2 *slot;             // [n] (tile << 12 | in-chunk rank) of the first / second record
-    uint32_t *recs;          // bucket entries: probe | kind << 30
+    uint32_t *recs;          // chunk areas of 2 x chunk 64-byte records (k_locate_c)
     int dbg;                 // diagnostics (HSC_CT_DBG): 1 join skips the searches, 2 also the gathers
 };
 hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *gid,
@@ -529,9 +508,6 @@ uint32_t ctiles_chunk();
 hipError_t launch_locate_c(const CTiles &ct, const WinView &wt, const ProbeView &p,
                            const uint64_t *clo, const uint64_t *chi, const ProbeWork &work,
                            uint8_t *flags, hipStream_t s);
-hipError_t launch_scatter_c(const CTiles &ct, const ProbeWork &work, uint32_t n, hipStream_t s);
-// Plan-free compact join (chunk-sorted records), as launch_join_f.
-hipError_t launch_join_cf(const CTiles &ct, const ProbeWork &work, uint8_t *flags, hipStream_t s);
 hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_items,
                          uint8_t *flags, hipStream_t s);
 // Sharded SCC (hsc_graph.hip): cover[v] = 1 iff v lies inside [dst, src] of a

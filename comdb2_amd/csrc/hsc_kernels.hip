@@ -1263,8 +1263,8 @@ hipError_t launch_join(const WinView &w, const ProbeWork &work, uint32_t max_ite
 {
     if (max_items == 0 || w.n == 0) return hipSuccess;
     const size_t T = (size_t)1 << w.log2T;
-    static const bool all_words = getenv("HSC_JOIN_ALL_WORDS") != nullptr;  // A/B: stage every word
-    const bool w0 = w.W == 3 && w.log2T == 11 && w.compact && !all_words;
+    // compact 3-word codes: only word 0 staged, later words read on a tie
+    const bool w0 = w.W == 3 && w.log2T == 11 && w.compact;
     const size_t lds = T * 8 * (size_t)(w0 ? 1 : w.W) + T * 8 + (T / 16) * 8 +
                        std::max<size_t>(T / 256, 16) * 8;
     if (w.W == 1 && w.log2T == 12)

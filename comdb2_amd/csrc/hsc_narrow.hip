@@ -713,7 +713,6 @@ constexpr int kLocTP = HSC_LOC_TP;
 #endif
 constexpr int kLocTThreads = HSC_LOC_THREADS;  // <= 4096 probes per chunk (in-chunk ranks fit 12 bits)
 static_assert(kLocTP * kLocTThreads <= 4096, "in-chunk ranks are 12 bits");
-constexpr uint32_t kHasSecond = 1u << 31;
 constexpr int kDirLds = HSC_DIR_LDS;  // directory entries staged in LDS per directory
 
 template <int W>
@@ -893,15 +892,6 @@ struct LocDefer {
     uint64_t snap[K];
 };
 
-template <int K>
-__device__ __forceinline__ void loc_defer_run(const WinView &wt, const ProbeView &p,
-                                              const LocDefer<K> &d, uint8_t *verdict)
-{
-#pragma unroll
-    for (int k = 0; k < K; ++k)
-        if (d.x[k] <= d.y[k] && tiles_max(wt, d.x[k], d.y[k]) > d.snap[k]) verdict[p.txn[d.q[k]]] = 1;
-}
-
 // W = key words held in registers (1 or 2), 0 = read from memory (any W).
 // The chunk's kLocTP probes per thread run as kLocTP / kLocSub sub-chunks of
 // kLocSub probes per thread: the loads of sub-chunk s + 1 are in flight while
@@ -917,7 +907,7 @@ constexpr int kLocSub = HSC_LOC_SUB;
 #define HSC_LOC_ATTR __attribute__((amdgpu_waves_per_eu(HSC_LOC_WPE, HSC_LOC_WPE)))
 #endif
 static_assert(kLocTP % kLocSub == 0, "whole sub-chunks");
-template <int W, bool kTrad, bool kSort>
+template <int W, bool kTrad>
 __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowView nv, WinView wt,
                                                              ProbeView p, ProbeWork work,
                                                              NarrowTiles nt, uint8_t *verdict)
@@ -946,11 +936,11 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
     uint32_t qq[2][K], gg[2][K], tx[2][K];
     bool valid[2][K];
     uint64_t snap[2][K], xl[2][K][WR], xh[2][K][WR];
-    // kSort: the chunk's records stay in registers until its histogram is
-    // complete, then go to their tile-sorted places in the chunk's area
+    // the chunk's records stay in registers until its histogram is complete,
+    // then go to their tile-sorted places in the chunk's area
     uint4 R0[S][K], R1[S][K];
     uint32_t RT[S][K];
-    uint64_t SS[S][K];  // kSort, ranks through the commit directory: the snapshots, ranked after the loop
+    uint64_t SS[S][K];  // ranks through the commit directory: the snapshots, ranked after the loop
     auto load = [&](int s, int buf) {
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -962,7 +952,7 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
             // rows out of the caches between batches
             gg[buf][k] = p.n ? __builtin_nontemporal_load(p.gid + q) : 0;
             snap[buf][k] = p.n ? __builtin_nontemporal_load(p.snap + q) : 0;
-            if constexpr (kSort) tx[buf][k] = p.n ? __builtin_nontemporal_load(p.txn + q) : 0;
+            tx[buf][k] = p.n ? __builtin_nontemporal_load(p.txn + q) : 0;
 #pragma unroll
             for (int w = 0; w < W; ++w) {
                 xl[buf][k][w] = p.n ? __builtin_nontemporal_load(p.lo + (size_t)w * p.n + q) : 0;
@@ -995,18 +985,14 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
         const int cb = s & 1;
         // 1. the previous sub-chunk's whole-tile checks: their loads are
         //    younger than this sub-chunk's probe loads, which are needed now;
-        //    kSort compares them at the end of this sub-chunk (the loads
-        //    overlap its LDS work)
+        //    they are compared at the end of this sub-chunk (the loads
+        //    overlap its LDS work; the read sets are in registers)
         uint64_t pm[K], psn[K];
         if (s > 0) {
-            if constexpr (kSort) {  // the read sets are in registers
 #pragma unroll
-                for (int k = 0; k < K; ++k) {
-                    pm[k] = dfr.x[k] <= dfr.y[k] ? tiles_max(wt, dfr.x[k], dfr.y[k]) : 0;
-                    psn[k] = dfr.snap[k];
-                }
-            } else {
-                loc_defer_run<K>(wt, p, dfr, verdict);
+            for (int k = 0; k < K; ++k) {
+                pm[k] = dfr.x[k] <= dfr.y[k] ? tiles_max(wt, dfr.x[k], dfr.y[k]) : 0;
+                psn[k] = dfr.snap[k];
             }
         }
         // 2. the next sub-chunk's probe loads stay in flight through step 3
@@ -1025,46 +1011,11 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
         if (nt.rank_lsn32) {
 #pragma unroll
             for (int k = 0; k < K; ++k) rs[k] = lsn32_rank(snap[cb][k], nt.rank_base);
-        } else if constexpr (kSort) {
+        } else {
             // the records stay in registers: every sub-chunk's heads are
             // searched together after the loop (one directory walk, not S)
 #pragma unroll
             for (int k = 0; k < K; ++k) rs[k] = 0, SS[s][k] = snap[cb][k];
-        } else {
-            const uint64_t le_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
-            bool head[K];
-            uint32_t slot[K];
-            uint32_t H = 0;
-#pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const uint64_t prev = __shfl_up(snap[cb][k], 1, 64);
-                head[k] = lane == 0 || prev != snap[cb][k];
-                const uint64_t m = __ballot(head[k]);
-                slot[k] = H + __popcll(m & le_mask) - 1;  // this lane's head
-                H += __popcll(m);
-            }
-            for (uint32_t b0 = 0; b0 < H; b0 += 64) {
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if (head[k] && slot[k] - b0 < 64) sb[slot[k] - b0] = snap[cb][k];
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const bool act[1] = {lane < H - b0};
-                const uint64_t xs[1] = {act[0] ? dir_le(sb[lane]) : 0};
-                uint32_t r[1];
-                dir16_count<1>(nt.cdir, cdir, xs, act, r);
-                rb[lane] = r[0];
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if (slot[k] - b0 < 64) rs[k] = rb[slot[k] - b0];
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            }
         }
         // end tiles: a = #first < lo - 1 (the tile holding the first row >=
         // lo), bt = #first <= hi - 1 (the tile holding the last row <= hi)
@@ -1089,10 +1040,8 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
 #pragma unroll
         for (int k = 0; k < K; ++k) {
             dfr.x[k] = 1, dfr.y[k] = 0;
-            if constexpr (kSort) {
-                R0[s][k].x = R1[s][k].x = kNoTile32;
-                RT[s][k] = tx[cb][k];
-            }
+            R0[s][k].x = R1[s][k].x = kNoTile32;
+            RT[s][k] = tx[cb][k];
             if (!valid[cb][k]) continue;
             const uint32_t q = qq[cb][k];
             const uint32_t ca = cnt[2 * k], cbt = cnt[2 * k + 1];
@@ -1117,46 +1066,24 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
                 if (use_a && !full_a)
                     r0 = make_uint4(a << 12 | atomicAdd(&hist[a], 1u), (uint32_t)lo_a,
                                     (uint32_t)min(hi_a, 0xFFFFFFFFull), rs[k]);
-                if (use_b && !full_b) {
-                    const uint4 rb2 = make_uint4(bt << 12 | atomicAdd(&hist[bt], 1u), 0,
-                                                 (uint32_t)hi_b, rs[k]);
-                    if (kSort) {
-                        r1 = rb2;
-                    } else if (r0.x == kNoTile32) {
-                        r0 = rb2;
-                    } else {
-                        r0.x |= kHasSecond;
-                        r1 = rb2;
-                    }
-                }
+                if (use_b && !full_b)
+                    r1 = make_uint4(bt << 12 | atomicAdd(&hist[bt], 1u), 0, (uint32_t)hi_b, rs[k]);
             }
-            if constexpr (kSort) {
-                R0[s][k] = r0;
-                R1[s][k] = r1;
-            } else {
-                if (r0.x & kHasSecond) nt.code2[q] = r1;
-                nt.code[q] = r0;
-            }
+            R0[s][k] = r0;
+            R1[s][k] = r1;
         }
-        if constexpr (kSort) {  // step 1's compares (pm = 0 where there was no check)
-            if (s > 0) {
+        if (s > 0) {  // step 1's compares (pm = 0 where there was no check)
 #pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if (pm[k] > psn[k]) verdict[RT[s - 1][k]] = 1;
-            }
+            for (int k = 0; k < K; ++k)
+                if (pm[k] > psn[k]) verdict[RT[s - 1][k]] = 1;
         }
     }
-    // kSort: the last sub-chunk's range-maximum loads are issued here and
-    // compared after the tail (scan, row and record stores), which they overlap
+    // the last sub-chunk's range-maximum loads are issued here and compared
+    // after the tail (scan, row and record stores), which they overlap
     uint64_t dmax[K];
-    if constexpr (kSort) {
 #pragma unroll
-        for (int k = 0; k < K; ++k)
-            dmax[k] = dfr.x[k] <= dfr.y[k] ? tiles_max(wt, dfr.x[k], dfr.y[k]) : 0;
-    } else {
-        loc_defer_run<K>(wt, p, dfr, verdict);
-    }
-    if constexpr (kSort) {
+    for (int k = 0; k < K; ++k) dmax[k] = dfr.x[k] <= dfr.y[k] ? tiles_max(wt, dfr.x[k], dfr.y[k]) : 0;
+    {
         if (!nt.rank_lsn32) {  // the chunk's snapshot ranks: heads of all sub-chunks in one list
             const uint64_t le_mask = lane == 63 ? ~0ull : ((2ull << lane) - 1);
             bool head[S][K];
@@ -1210,11 +1137,7 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
     HSC_STAMP(work, 0, 3);
     // column g of the tile-major histogram (neighbouring chunks of a line are
     // written from the same XCD)
-    const uint32_t hs = hist_stride(work.G);
-    if constexpr (!kSort) {
-        for (uint32_t i = threadIdx.x; i < ntiles; i += kLocTThreads)
-            work.hist[(size_t)i * hs + g] = hist[i];
-    } else {
+    {
         // exclusive scan of the chunk's tile counts (thread = a run of
         // consecutive tiles): row g of the chunk-major table gets (run start
         // << 16 | count) per tile (contiguous stores; the plan transposes),
@@ -1258,7 +1181,7 @@ __global__ __launch_bounds__(kLocTThreads) HSC_LOC_ATTR void k_locate_t(NarrowVi
         for (int k = 0; k < K; ++k)
             if (dfr.x[k] <= dfr.y[k] && dmax[k] > dfr.snap[k]) verdict[RT[S - 1][k]] = 1;
     }
-    HSC_STAMP(work, 0, kSort ? 5 : 4);
+    HSC_STAMP(work, 0, 5);
 }
 
 hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeView &p,
@@ -1269,15 +1192,8 @@ hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeV
     const size_t lds = loc_lds(nt, wt.ntiles).bytes;
     const bool tr = nt.trad != nullptr;
     const int w = nv.W == 1 || nv.W == 2 ? nv.W : 0;
-#define HSC_LOCATE(W_, TR_)                                                                        \
-    do {                                                                                           \
-        if (work.local_items)                                                                      \
-            k_locate_t<W_, TR_, true><<<8 * ((work.G + 7) / 8), kLocTThreads, lds, s>>>(            \
-                nv, wt, p, work, nt, verdict);                                                     \
-        else                                                                                       \
-            k_locate_t<W_, TR_, false><<<8 * ((work.G + 7) / 8), kLocTThreads, lds, s>>>(           \
-                nv, wt, p, work, nt, verdict);                                                     \
-    } while (0)
+#define HSC_LOCATE(W_, TR_) \
+    k_locate_t<W_, TR_><<<8 * ((work.G + 7) / 8), kLocTThreads, lds, s>>>(nv, wt, p, work, nt, verdict)
     if (w == 1 && tr)
         HSC_LOCATE(1, true);
     else if (w == 1)
@@ -1298,105 +1214,8 @@ hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeV
 uint32_t narrow_tiles_chunk() { return kLocTP * kLocTThreads; }
 uint32_t narrow_tiles_dir_lds() { return kDirLds; }
 
-// ---- plan: column scans; fixed-capacity tile buckets ----
-// Tile t's bucket is recs[t * kTileCap, (t + 1) * kTileCap): a record's place
-// is its chunk's offset inside the tile (the exclusive scan of the tile's
-// histogram column over chunks) + its in-chunk rank, so no scan over tiles
-// (and no last-block tail) is needed.  Records past kTileCap of a tile spill
-// to the overflow area after the buckets: the tile's wave reserves a run
-// there with one atomic and appends join items for it (hot tiles only).
-// Wave w of block b scans tile 8 b + w: its column hist[t][0 .. G) (lane l
-// owns entries 8 l .. 8 l + 7, two 16-byte loads; G <= kMaxChunks = 512)
-// becomes exclusive chunk offsets inside the tile; counts[t] = its records.
-// ctl[0] (overflow records) and ctl[1] (extra join items) were zeroed by
-// this batch's locate.
-constexpr int kPlanThreads = 512;
-static_assert(kMaxChunks <= 512, "one 512-entry column pass per wave");
-__global__ __launch_bounds__(kPlanThreads) void k_plan_t(ProbeWork work, uint32_t ntiles,
-                                                         uint32_t *ctl, uint8_t *flags,
-                                                         uint32_t n_txn, uint8_t *verdict)
-{
-    const int lane = threadIdx.x & 63;
-    const uint32_t t = blockIdx.x * (kPlanThreads / 64) + (threadIdx.x >> 6);
-    const uint32_t hs = hist_stride(work.G);
-    if (verdict) {  // the pack folded in: verdict = the locate's flags, flags cleared
-        const uint32_t stride = gridDim.x * kPlanThreads;
-        for (uint32_t i = blockIdx.x * kPlanThreads + threadIdx.x; i < n_txn; i += stride) {
-            const uint8_t f = flags[i];
-            verdict[i] = f != 0;
-            if (f) flags[i] = 0;
-        }
-    }
-    if (t >= ntiles) return;
-    u32x4 *col = (u32x4 *)(work.hist + (size_t)t * hs);
-    const uint32_t e = 8 * lane;
-    u32x4 a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
-    if (e < hs) {
-        a = col[e / 4];
-        b = col[e / 4 + 1];
-    }
-    // entries past G are never written: mask them
-    const uint32_t v[8] = {e + 0 < work.G ? a.x : 0, e + 1 < work.G ? a.y : 0,
-                           e + 2 < work.G ? a.z : 0, e + 3 < work.G ? a.w : 0,
-                           e + 4 < work.G ? b.x : 0, e + 5 < work.G ? b.y : 0,
-                           e + 6 < work.G ? b.z : 0, e + 7 < work.G ? b.w : 0};
-    uint32_t sum = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sum += v[k];
-    uint32_t x = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    uint32_t run = x - sum;
-    if (e < hs) {
-        u32x4 oa, ob;
-        oa.x = run; run += v[0];
-        oa.y = run; run += v[1];
-        oa.z = run; run += v[2];
-        oa.w = run; run += v[3];
-        ob.x = run; run += v[4];
-        ob.y = run; run += v[5];
-        ob.z = run; run += v[6];
-        ob.w = run;
-        col[e / 4] = oa;
-        col[e / 4 + 1] = ob;
-    }
-    const uint32_t total = __shfl(x, 63, 64);
-    if (lane == 0) work.counts[t] = total;
-    if (total > kTileCap) {  // hot tile: overflow run + one join item per kJoinChunk records
-        const uint32_t over = total - kTileCap;
-        const uint32_t nx = (over + kJoinChunk - 1) / kJoinChunk;
-        uint32_t base = 0, ib = 0;
-        if (lane == 0) {
-            if (!work.local_items) {
-                base = atomicAdd(&ctl[0], over);
-                work.bucket_off[t] = base;
-            }
-            ib = atomicAdd(&ctl[1], nx);
-        }
-        base = __shfl(base, 0, 64);
-        ib = __shfl(ib, 0, 64);
-        // chunk-sorted records: items are ranges of the tile's own record
-        // numbers; bucketed records: ranges of the overflow area
-        const uint32_t o0 = work.local_items ? kTileCap : ntiles * kTileCap + base;
-        for (uint32_t j = lane; j < nx; j += 64)  // the wave writes the items together
-            work.item_desc[ib + j] = make_uint4(t, o0 + j * kJoinChunk,
-                                                o0 + min((j + 1) * kJoinChunk, over), 0);
-    }
-}
-
-hipError_t launch_plan_t(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, hipStream_t s,
-                         uint8_t *flags, uint32_t n_txn, uint8_t *verdict)
-{
-    if (ntiles == 0) return hipSuccess;
-    constexpr uint32_t per = kPlanThreads / 64;
-    k_plan_t<<<(ntiles + per - 1) / per, kPlanThreads, 0, s>>>(work, ntiles, ctl, flags, n_txn,
-                                                               verdict);
-    return hipGetLastError();
-}
-
+// ---- plan ----
+// ctl[1] (extra join items) was zeroed by this batch's locate.
 // Plan of chunk-sorted records: block = 8 tiles (HSC_PLAN_S_THREADS / 64).
 // The block reads the tiles' entries of every chunk row of the locate's
 // chunk-major table (32 contiguous bytes per row), transposes them through LDS, and wave w scans
@@ -1497,149 +1316,11 @@ hipError_t launch_plan_s(const ProbeWork &work, uint32_t ntiles, uint32_t *ctl, 
     return hipGetLastError();
 }
 
-// ---- scatter: 16-byte records into tile buckets ----
-// One block per locate chunk (XCD-contiguous chunk order, as the locate): the
-// chunk's offsets inside every tile bucket (its column of the scanned
-// histogram) are staged in LDS once, so a record's place costs an LDS read;
-// the record and read-set loads of all the chunk's probes are issued before
-// that staging completes.  A bucket holds its records in chunk order, so the
-// neighbouring records of a bucket come from one XCD and their partial-line
-// writes merge in that XCD's L2.
-__device__ __forceinline__ uint32_t bucket_slot(const ProbeWork &work, uint32_t ntiles, uint32_t t,
-                                                uint32_t pos)
-{
-    return pos < kTileCap ? t * kTileCap + pos
-                          : ntiles * kTileCap + work.bucket_off[t] + (pos - kTileCap);
-}
-
-constexpr int kScatThreads = kLocTThreads;
-__global__ __launch_bounds__(kScatThreads) void k_scatter_t(ProbeView p, ProbeWork work,
-                                                             NarrowTiles nt, uint32_t ntiles)
-{
-    extern __shared__ uint32_t soff[];  // [ntiles] this chunk's offset in each bucket
-    const uint32_t g = xcd_chunk(blockIdx.x, (work.G + 7) / 8);
-    if (g >= work.G) return;
-    constexpr int P = kLocTP;
-    const uint32_t c0 = g * work.chunk, c1 = min(p.n, c0 + work.chunk);
-    uint4 a[P];
-    uint32_t txn[P];
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const uint32_t q = c0 + threadIdx.x + kScatThreads * j;
-        a[j] = q < c1 ? nt.code[q] : make_uint4(kNoTile32, 0, 0, 0);
-        txn[j] = q < c1 ? p.txn[q] : 0;
-    }
-    const size_t hs = hist_stride(work.G);
-    for (uint32_t t = threadIdx.x; t < ntiles; t += kScatThreads) soff[t] = work.hist[t * hs + g];
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        if (a[j].x == kNoTile32) continue;
-        const uint32_t q = c0 + threadIdx.x + kScatThreads * j;
-        const uint32_t ta = (a[j].x & ~kHasSecond) >> 12;
-        nt.recs[bucket_slot(work, ntiles, ta, soff[ta] + (a[j].x & 0xFFFu))] =
-            make_uint4(a[j].y, a[j].z, a[j].w, txn[j]);
-        if (a[j].x & kHasSecond) {
-            const uint4 c = nt.code2[q];
-            const uint32_t tb = c.x >> 12;
-            nt.recs[bucket_slot(work, ntiles, tb, soff[tb] + (c.x & 0xFFFu))] =
-                make_uint4(c.y, c.z, c.w, txn[j]);
-        }
-    }
-}
-
-hipError_t launch_scatter_t(const ProbeView &p, const ProbeWork &work, const NarrowTiles &nt,
-                            uint32_t ntiles, hipStream_t s)
-{
-    if (p.n == 0) return hipSuccess;
-    k_scatter_t<<<8 * ((work.G + 7) / 8), kScatThreads, 4 * (size_t)ntiles, s>>>(p, work, nt, ntiles);
-    return hipGetLastError();
-}
-
 // ---- join: 8-byte rows ----
 // Row quad v of thread t = rows 4 (t + kJoinThreads v) .. + 3: one 16-byte
 // load of keys (already in Eytzinger order, k_key32) and one of ranks per
 // quad, stored to LDS as they are; 16-row maxima over 4 lanes, 128-row maxima
 // over 32 lanes.
-
-// One workgroup per tile: its bucket (at most kTileCap records; the tile's
-// rows are requested before anything else is known); blocks past the tiles
-// loop over the further kJoinChunk-record chunks of hot tiles' overflow runs
-// (item_desc).
-// One tile's records (kTile: tile xi's bucket, at most kTileCap records) or
-// overflow item xi of a hot tile.  The records are loaded first (a tile's
-// bucket always has kTileCap slots; the count, a scalar load, masks them
-// later), then the tile's rows, so both round trips overlap (vector loads
-// retire in order: a count read between them would wait for the rows).
-template <bool kTile>
-__device__ __forceinline__ void join_t_item(const ProbeWork &work, const NarrowTiles &nt,
-                                            uint32_t n, uint32_t xi, uint8_t *verdict,
-                                            uint32_t *keys, uint32_t *rank, uint32_t *b16,
-                                            uint32_t *b128)
-{
-    constexpr uint32_t T = 1u << kTLog2;
-    constexpr int RQ = T / (4 * kJoinThreads);  // row quads per thread (2)
-    constexpr int kRec = kJoinChunk / kJoinThreads;
-    uint32_t tile, r0, r1;
-    u32x4 rk[RQ], rr[RQ], rec[kRec];
-    if constexpr (kTile) {
-        tile = xi;
-        r0 = tile * kTileCap;
-#pragma unroll
-        for (int k = 0; k < kRec; ++k)
-            rec[k] = *(const u32x4 *)(nt.recs + r0 + k * kJoinThreads + threadIdx.x);
-    } else {  // a further kJoinChunk records of a hot tile's overflow run
-        const uint32_t *d = (const uint32_t *)(work.item_desc + xi);
-        tile = sload(d), r0 = sload(d + 1), r1 = sload(d + 2);
-#pragma unroll
-        for (int k = 0; k < kRec; ++k)
-            rec[k] = *(const u32x4 *)(nt.recs + min(r0 + k * kJoinThreads + threadIdx.x, r1 - 1));
-    }
-    const size_t ts = (size_t)tile << kTLog2;
-#pragma unroll
-    for (int v = 0; v < RQ; ++v) {
-        const size_t row = ts + 4 * (threadIdx.x + kJoinThreads * v);
-        rk[v] = *(const u32x4 *)(nt.key32 + row);
-        rr[v] = *(const u32x4 *)(nt.rank32 + row);
-    }
-    if constexpr (kTile) r1 = r0 + min(kTileCap, sload(work.counts + tile));
-#pragma unroll
-    for (int v = 0; v < RQ; ++v) {
-        const uint32_t quad = threadIdx.x + kJoinThreads * v;
-        ((u32x4 *)keys)[quad] = rk[v];  // already in Eytzinger order (k_key32)
-        ((u32x4 *)rank)[quad] = rr[v];
-        uint32_t m = max(max(rr[v].x, rr[v].y), max(rr[v].z, rr[v].w));
-        m = max(m, (uint32_t)__shfl_xor((int)m, 1, 64));
-        m = max(m, (uint32_t)__shfl_xor((int)m, 2, 64));
-        if ((threadIdx.x & 3) == 0) b16[quad >> 2] = m;
-#pragma unroll
-        for (int d = 4; d < 32; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
-        if ((threadIdx.x & 31) == 0) b128[quad >> 5] = m;
-    }
-    __syncthreads();
-    HSC_STAMP(work, 1, 1);
-    const uint32_t tn = min(T, n - (tile << kTLog2));
-#pragma unroll
-    for (int k = 0; k < kRec; ++k) {
-        const uint32_t r = r0 + k * kJoinThreads + threadIdx.x;
-        if (r >= r1) continue;
-        const uint32_t lo = rec[k].x, hi = rec[k].y, rs = rec[k].z;
-        // pa = #keys < lo, pb = #keys <= hi: root-to-leaf walks of the
-        // Eytzinger tree, both reads of a level in flight together; rows
-        // past tn are padding (0xFFFFFFFF, never below lo)
-        uint32_t ja = 1, jb = 1;
-#pragma unroll
-        for (int d = 0; d < kTLog2; ++d) {
-            const uint32_t ka = keys[ja], kb = keys[jb];
-            ja = 2 * ja + (ka < lo);
-            jb = 2 * jb + (kb <= hi);
-        }
-        const uint32_t kl = keys[0];  // the tile's last (largest) row
-        const uint32_t pa = min(ja - T + (kl < lo), tn);
-        const uint32_t pb = min(jb - T + (kl <= hi), tn);
-        if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) verdict[rec[k].w] = 1;
-    }
-}
 
 // The join is held to 8 waves per SIMD: at 85-99 SGPRs the hardware admits
 // only 6-7 (measured on config 2: join 34 -> 31.7 us, one stream 71.3 -> 69 us)
@@ -1647,7 +1328,7 @@ __device__ __forceinline__ void join_t_item(const ProbeWork &work, const NarrowT
 #define HSC_JOIN_WPE 8
 #endif
 #define HSC_JOIN_ATTR __attribute__((amdgpu_waves_per_eu(HSC_JOIN_WPE, HSC_JOIN_WPE)))
-// Chunk-sorted records (work.local_items): record j of tile t lives in the
+// Chunk-sorted records: record j of tile t lives in the
 // run of the chunk g whose offset inside the tile (the plan's scan of column
 // t) is the last one <= j, at chunk g's area + cst[t][g] + (j - that offset).
 // The tile's column is staged first (its loads ahead of the rows'), each
@@ -1741,12 +1422,11 @@ __device__ __forceinline__ void join_s_item(const ProbeWork &work, const NarrowT
 #define HSC_JOIN_XCD 1
 #endif
 constexpr bool kJoinXcd = HSC_JOIN_XCD != 0;
-__host__ __device__ inline uint32_t join_tile_blocks(bool srt, uint32_t ntiles)
+__host__ __device__ inline uint32_t join_tile_blocks(uint32_t ntiles)
 {
-    return srt && kJoinXcd ? 8 * ((ntiles + 7) / 8) : ntiles;
+    return kJoinXcd ? 8 * ((ntiles + 7) / 8) : ntiles;
 }
 
-template <bool srt>
 __global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_t(ProbeWork work, NarrowTiles nt,
                                                          uint32_t n, uint32_t ntiles,
                                                          uint8_t *verdict)
@@ -1761,24 +1441,16 @@ __global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_t(ProbeWork
     HSC_STAMP(work, 1, 0);
     // chunk-sorted records: neighbouring tiles on one XCD (their runs of a
     // chunk share lines of its record area, which that XCD's L2 then serves)
-    const uint32_t tb = join_tile_blocks(srt, ntiles);
+    const uint32_t tb = join_tile_blocks(ntiles);
     if (blockIdx.x < tb) {
-        if constexpr (srt) {
-            const uint32_t tile = kJoinXcd ? xcd_chunk(blockIdx.x, tb / 8) : blockIdx.x;
-            if (tile < ntiles)
-                join_s_item<true>(work, nt, n, tile, verdict, keys, rank, b16, b128, Es, Cs);
-        } else {
-            join_t_item<true>(work, nt, n, blockIdx.x, verdict, keys, rank, b16, b128);
-        }
+        const uint32_t tile = kJoinXcd ? xcd_chunk(blockIdx.x, tb / 8) : blockIdx.x;
+        if (tile < ntiles) join_s_item<true>(work, nt, n, tile, verdict, keys, rank, b16, b128, Es, Cs);
     } else {  // blocks past the tiles take the hot tiles' overflow items in turn
         const uint32_t nextra = work.item_off[1];
         const uint32_t stride = gridDim.x - tb;
         for (uint32_t xi = blockIdx.x - tb; xi < nextra; xi += stride) {
             __syncthreads();  // the previous item's LDS reads are done
-            if constexpr (srt)
-                join_s_item<false>(work, nt, n, xi, verdict, keys, rank, b16, b128, Es, Cs);
-            else
-                join_t_item<false>(work, nt, n, xi, verdict, keys, rank, b16, b128);
+            join_s_item<false>(work, nt, n, xi, verdict, keys, rank, b16, b128, Es, Cs);
         }
     }
     HSC_STAMP(work, 1, 3);
@@ -1791,136 +1463,8 @@ hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t 
     // one block per tile + up to 512 blocks looping over the overflow items
     // (measured: one block per tile beats persistent blocks that prefetch
     // their next tile -- 27.8 vs 32 us on config 2)
-    const uint32_t blocks = join_tile_blocks(work.local_items != 0, ntiles) +
-                            std::min<uint32_t>(max_items - ntiles, 512);
-    if (work.local_items)
-        k_join_t<true><<<blocks, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
-    else
-        k_join_t<false><<<blocks, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
-    return hipGetLastError();
-}
-
-// ---- plan-free join (chunk-sorted records) ----
-// The plan kernel's work moves into the join: tile t's column of the locate's
-// chunk-major table (run start << 16 | count per chunk) is read straight from
-// the table -- one strided load per chunk, issued with the tile's rows; the
-// tiles of a block's XCD neighbour each other, so the column's lines are
-// shared in that XCD's L2 -- and scanned in LDS.  A hot tile's records past
-// the first kJoinChunk are joined by the same block in further rounds over
-// its staged rows (no overflow items).  Conflicts mark the batch's flags,
-// which the pack turns into verdict bytes: locate -> join -> pack.
-__device__ __forceinline__ uint32_t join_f_records(const NarrowTiles &nt, const ProbeWork &work,
-                                                   const uint32_t *Es, const uint32_t *Cs,
-                                                   uint32_t G, uint32_t j, uint32_t j1, u32x4 &rec)
-{
-    uint32_t g = 0;  // Es[0] = 0 <= j
-#pragma unroll
-    for (int b = 8; b >= 0; --b) {
-        const uint32_t c = g + (1u << b);
-        if (c < G && Es[c] <= j) g = c;
-    }
-    const size_t area = 2 * (size_t)work.chunk;
-    rec = j < j1 ? *(const u32x4 *)(nt.recs + g * area + Cs[g] + (j - Es[g])) : u32x4{0, 0, 0, 0};
-    return g;
-}
-
-__global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_f(
-    ProbeWork work, NarrowTiles nt, uint32_t n, uint32_t ntiles, uint8_t *flags)
-{
-    constexpr uint32_t T = 1u << kTLog2;
-    constexpr int RQ = T / (4 * kJoinThreads);
-    constexpr int kRec = kJoinChunk / kJoinThreads;
-    __shared__ __attribute__((aligned(16))) uint32_t keys[T];
-    __shared__ __attribute__((aligned(16))) uint32_t rank[T];
-    __shared__ uint32_t b16[T / 16];
-    __shared__ uint32_t b128[T / 128];
-    __shared__ uint32_t Es[kMaxChunks], Cs[kMaxChunks];
-    __shared__ uint32_t wsum[kJoinThreads / 64];
-    static_assert(kMaxChunks <= kJoinThreads, "one column entry per thread");
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t tb = join_tile_blocks(true, ntiles);
-    const uint32_t tile = kJoinXcd ? xcd_chunk(blockIdx.x, tb / 8) : blockIdx.x;
-    if (tile < ntiles) {
-        const uint32_t G = work.G, rs = (ntiles + 3) & ~3u;
-        const uint32_t x = threadIdx.x < G ? work.cm[(size_t)threadIdx.x * rs + tile] : 0;
-        u32x4 rk[RQ], rr[RQ], rec[kRec];
-        const size_t ts = (size_t)tile << kTLog2;
-#pragma unroll
-        for (int v = 0; v < RQ; ++v) {
-            const size_t row = ts + 4 * (threadIdx.x + kJoinThreads * v);
-            rk[v] = *(const u32x4 *)(nt.key32 + row);
-            rr[v] = *(const u32x4 *)(nt.rank32 + row);
-        }
-        // exclusive scan of the column's counts: chunk g's run starts at
-        // record Es[g] of the tile, at Cs[g] of the chunk's area
-        const uint32_t cnt = x & 0xFFFFu;
-        uint32_t inc = cnt;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += y;
-        }
-        if (lane == 63) wsum[wv] = inc;
-        __syncthreads();
-        uint32_t base = 0, total = 0;
-#pragma unroll
-        for (int w = 0; w < kJoinThreads / 64; ++w) {
-            base += w < wv ? wsum[w] : 0;
-            total += wsum[w];
-        }
-        if (threadIdx.x < G) Es[threadIdx.x] = base + inc - cnt, Cs[threadIdx.x] = x >> 16;
-        __syncthreads();
-        // the first round's records are requested while the rows arrive
-#pragma unroll
-        for (int k = 0; k < kRec; ++k)
-            join_f_records(nt, work, Es, Cs, G, k * kJoinThreads + threadIdx.x, total, rec[k]);
-#pragma unroll
-        for (int v = 0; v < RQ; ++v) {
-            const uint32_t quad = threadIdx.x + kJoinThreads * v;
-            ((u32x4 *)keys)[quad] = rk[v];
-            ((u32x4 *)rank)[quad] = rr[v];
-            uint32_t m = max(max(rr[v].x, rr[v].y), max(rr[v].z, rr[v].w));
-            m = max(m, (uint32_t)__shfl_xor((int)m, 1, 64));
-            m = max(m, (uint32_t)__shfl_xor((int)m, 2, 64));
-            if ((threadIdx.x & 3) == 0) b16[quad >> 2] = m;
-#pragma unroll
-            for (int d = 4; d < 32; d <<= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
-            if ((threadIdx.x & 31) == 0) b128[quad >> 5] = m;
-        }
-        __syncthreads();
-        const uint32_t tn = min(T, n - (tile << kTLog2));
-        for (uint32_t j0 = 0; j0 < total; j0 += kJoinChunk) {
-            if (j0)  // a hot tile's further rounds
-#pragma unroll
-                for (int k = 0; k < kRec; ++k)
-                    join_f_records(nt, work, Es, Cs, G, j0 + k * kJoinThreads + threadIdx.x, total,
-                                   rec[k]);
-#pragma unroll
-            for (int k = 0; k < kRec; ++k) {
-                const uint32_t j = j0 + k * kJoinThreads + threadIdx.x;
-                if (j >= total) continue;
-                const uint32_t lo = rec[k].x, hi = rec[k].y, r_s = rec[k].z;
-                uint32_t ja = 1, jb = 1;
-#pragma unroll
-                for (int d = 0; d < kTLog2; ++d) {
-                    const uint32_t ka = keys[ja], kb = keys[jb];
-                    ja = 2 * ja + (ka < lo);
-                    jb = 2 * jb + (kb <= hi);
-                }
-                const uint32_t kl = keys[0];
-                const uint32_t pa = min(ja - T + (kl < lo), tn);
-                const uint32_t pb = min(jb - T + (kl <= hi), tn);
-                if (pa < pb && any_after32(rank, b16, b128, pa, pb, r_s)) flags[rec[k].w] = 1;
-            }
-        }
-    }
-}
-
-hipError_t launch_join_f(const ProbeWork &work, const NarrowTiles &nt, uint32_t n, uint32_t ntiles,
-                         uint8_t *flags, hipStream_t s)
-{
-    if (ntiles == 0) return hipSuccess;
-    k_join_f<<<join_tile_blocks(true, ntiles), kJoinThreads, 0, s>>>(work, nt, n, ntiles, flags);
+    const uint32_t blocks = join_tile_blocks(ntiles) + std::min<uint32_t>(max_items - ntiles, 512);
+    k_join_t<<<blocks, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
     return hipGetLastError();
 }
 

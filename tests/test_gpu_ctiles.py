@@ -93,31 +93,13 @@ def _short_case(seed, n_commits=3000, n_txn=900, lens=(9, 17, 23), n_tabs=4, hot
 
 
 def _both(v, log, rs):
-    """Verdicts through the compact tiles and through the wide compact pipeline;
-    the compact tiles' scatter path (HSC_CT_SORT=0 at the build: probe
-    entries + bucket entries instead of chunk-sorted records) and the planned
-    join of chunk-sorted records and the plan-free one (HSC_CT_FUSED=1)
-    must agree."""
-    os.environ["HSC_CT_SORT"] = "0"
-    try:
-        v.set_layout(LAYOUT_AUTO)
-        v.ingest_log(log)
-    finally:
-        os.environ.pop("HSC_CT_SORT", None)
-    scat = v.check_readsets(rs) != 0
+    """Verdicts through the compact tiles and through the wide compact
+    pipeline (which must agree)."""
     v.set_layout(LAYOUT_AUTO)
     v.ingest_log(log)
     assert v.layout == LAYOUT_COMPACT
     assert 1 <= v.tile_key_words <= 3
     got = v.check_readsets(rs) != 0
-    np.testing.assert_array_equal(scat, got, err_msg="chunk-sorted vs scattered records")
-    os.environ["HSC_CT_FUSED"] = "1"  # chunk-sorted records through the plan-free join
-    try:
-        v.ingest_log(log)
-    finally:
-        os.environ.pop("HSC_CT_FUSED", None)
-    fused = v.check_readsets(rs) != 0
-    np.testing.assert_array_equal(fused, got, err_msg="plan-free vs planned join")
     v.ingest_log(log)
     v.set_layout(LAYOUT_COMPACT_WIDE)
     ref = v.check_readsets(rs) != 0

@@ -53,11 +53,9 @@ def _case(rng, n, W, ngroups, pattern):
 
 
 def _build(gid, words, lsn, ngroups, packed):
-    # packed: "dd" the packed sort with the dedupe fused into its unpack
-    # (default), "flags" the packed sort + the flag/scan/compact dedupe,
-    # False the whole-row radix sort
+    # packed: the packed sort with the dedupe fused into its unpack (the
+    # default when the varying bits fit), False the whole-row radix sort
     os.environ["HSC_PACKED_SORT"] = "1" if packed else "0"
-    os.environ["HSC_PK_DD"] = "0" if packed == "flags" else "1"
     try:
         v = Validator(0)
         W = words.shape[0]
@@ -74,7 +72,6 @@ def _build(gid, words, lsn, ngroups, packed):
         return out
     finally:
         os.environ.pop("HSC_PACKED_SORT", None)
-        os.environ.pop("HSC_PK_DD", None)
 
 
 CASES = [
@@ -90,7 +87,7 @@ def test_build_rows_match_numpy(n, W, ngroups, pattern):
     rng = np.random.default_rng(n * 31 + W * 7 + ngroups)
     gid, words, lsn = _case(rng, n, W, ngroups, pattern)
     want_all, want_u = _reference(gid, words, lsn)
-    for packed in ("dd", "flags", False):
+    for packed in (True, False):
         got_all, got_u = _build(gid, words, lsn, ngroups, packed)
         for got, want in ((got_all, want_all), (got_u, want_u)):
             np.testing.assert_array_equal(got[0], want[0])

@@ -28,19 +28,14 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
     want, _, _ = oracle_mod.check(log, rs, nthreads=8)
     got = {}
     # (layout, build knob): locate finds tiles through the LDS bucket table by
-    # default and through the 16-ary directory with HSC_TILE_DIR set; rows
-    # carry lsn - oldest commit + 1 when the window spans < 2^32 of log, the
-    # commit rank (directory search of snapshots) with HSC_RANK_DIR set; the
-    # bucket table in linear or log mode (HSC_TRAD_MODE; by default the build
-    # picks the mode whose fullest bucket is smaller); records chunk-sorted
-    # (default) or scattered into tile buckets (HSC_NT_SORT=0); the join reads
-    # its tile's column from a plan kernel (default) or scans it itself, the
-    # verdicts packed after it (HSC_NT_FUSED=1)
+    # default and through the 16-ary directory with HSC_TILE_DIR set (the path
+    # of windows with too many tiles for the table).  Rows carry lsn - oldest
+    # commit + 1 when the window spans < 2^32 of log, else commit ranks
+    # (test_multi_file_window_commit_ranks); the bucket table's mode (linear
+    # or log) is picked per window by its fullest bucket (config 5's Zipf keys
+    # take log mode)
     runs = [(LAYOUT_NARROW_DIRECT, None), (LAYOUT_NARROW_TILES, None),
-            (LAYOUT_NARROW_TILES, "HSC_TILE_DIR"), (LAYOUT_NARROW_TILES, "HSC_RANK_DIR"),
-            (LAYOUT_NARROW_TILES, "HSC_TRAD_MODE=log"), (LAYOUT_NARROW_TILES, "HSC_TRAD_MODE=lin"),
-            (LAYOUT_NARROW_TILES, "HSC_NT_SORT=0"), (LAYOUT_NARROW_TILES, "HSC_NT_FUSED=1"),
-            (LAYOUT_NARROW_CODES, None), (LAYOUT_WIDE, None)]
+            (LAYOUT_NARROW_TILES, "HSC_TILE_DIR"), (LAYOUT_NARROW_CODES, None), (LAYOUT_WIDE, None)]
     try:
         for layout, knob in runs:
             kv = [k.partition("=") for k in knob.split("+")] if knob else []
@@ -55,8 +50,7 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
             np.testing.assert_array_equal(got[layout] != 0, want != 0,
                                           err_msg=f"layout {layout} knob {knob}")
     finally:
-        for knob in ("HSC_TILE_DIR", "HSC_RANK_DIR", "HSC_TRAD_MODE", "HSC_NT_SORT", "HSC_NT_FUSED"):
-            os.environ.pop(knob, None)
+        os.environ.pop("HSC_TILE_DIR", None)
         v.set_layout(LAYOUT_AUTO)
     return want
 
@@ -192,8 +186,8 @@ def test_multi_file_window_commit_ranks(validator, oracle_mod):
 
 def test_hot_tile_bucket_overflow(validator, oracle_mod):
     """Most ranges of a dense batch land in one 4096-row tile: its fixed
-    bucket (1024 records) spills into the overflow area, which the join
-    covers with extra items (hsc_narrow.hip k_plan_t)."""
+    bucket (1024 records) spills, and the join covers the tile's further
+    records with extra items (hsc_narrow.hip k_plan_s)."""
     key = lambda rng: F.enc_int64(int(rng.integers(0, 1 << 24)))
 
     def rng_range(rng):
