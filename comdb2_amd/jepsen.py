@@ -14,16 +14,20 @@ per process:
   the key and inserts its row into one of them only if both were empty; the
   G2 checker (:57-83) flags a key with more than one ``:ok`` insert.
 
-:func:`history_from_jepsen_edn` pairs each invoke with its completion, drops
-``:fail`` (not committed) and ``:info`` (indeterminate) ops, and turns every
-``:ok`` op into one committed transaction of a :class:`workloads.History`:
+:func:`history_from_jepsen_edn` pairs each invoke with its completion (a
+history may also be one EDN vector of ops, as knossos reads it:
+linearizable/filetest/src/jepsen/filetest.clj, ``history.txt``), drops
+``:fail`` ops (not committed), and turns every ``:ok`` op into one committed
+transaction of a :class:`workloads.History`:
 
 * txn ids = commit order, taken as the order of the completions (their
   ``:time``, else their line order); a key's version order is its writers'
   txn order;
-* register read: a read of the version whose ``(uid, value)`` it returned
-  (the latest such writer before it, else the earliest after it; ``nil`` =
-  the initial, empty register) -- WR comes from the uid;
+* register read: a read of the version it returned -- the writer with the
+  same ``:uid`` and value when the op carries a ``:uid`` (register.c), else
+  the writer of the same value (a knossos register history of unique
+  values); the latest such writer before it, else the earliest after it;
+  ``nil`` = the initial, empty register;
 * register write: a write of the register;
 * register cas ``[cur new]``: a read of the latest earlier version whose value
   is ``cur`` (the version the ``where val = cur`` matched: the CAS chain)
@@ -31,10 +35,14 @@ per process:
 * insert ``[k [a b]]``: reads of ``(k, a)`` and ``(k, b)`` that saw the
   initial (absent) rows, plus a write of ``(k, a)`` or ``(k, b)``.
 
-Reads whose version no ``:ok`` writer produced are dropped and counted
-(``dangling``).  hsc_dep_graph_* then builds the WR / WW / RW edges and the
-SCCs; a nontrivial SCC is a dependency cycle (two ``:ok`` inserts of one G2
-key form the 2-cycle of rw edges the G2 checker looks for).
+``:info`` ops are indeterminate: they may have committed.  Their writes stay
+candidate versions, and one that a read observed (no ``:ok`` writer produced
+that version) did commit -- it joins the history as a transaction ordered at
+its invoke (``info_recovered``); the others are dropped.  Reads whose version
+no writer produced are dropped and counted (``dangling``).  hsc_dep_graph_*
+then builds the WR / WW / RW edges and the SCCs; a nontrivial SCC is a
+dependency cycle (two ``:ok`` inserts of one G2 key form the 2-cycle of rw
+edges the G2 checker looks for).
 """
 from __future__ import annotations
 
@@ -104,19 +112,29 @@ def parse_edn(text: str) -> List:
 class JepsenOps:
     """What the conversion kept and dropped."""
     history: History
-    ok: int                  # completed :ok ops = committed txns
+    ok: int                  # completed :ok ops (committed txns)
     failed: int              # :fail completions (dropped)
-    info: int                # :info completions (indeterminate, dropped)
+    info: int                # :info completions (indeterminate)
     unpaired: int            # invokes without a completion
-    dangling: int            # reads of a version no :ok op wrote (dropped)
+    dangling: int            # reads of a version no writer produced (dropped)
     g2_keys: Dict[int, int]  # insert key -> :ok inserts (adya.clj g2-checker input)
-    txn_ops: List[dict]      # the :ok completion of each txn (txn id order)
+    txn_ops: List[dict]      # the completion of each txn (txn id order)
+    info_recovered: int = 0  # :info ops whose write a read observed (committed)
 
 
-def _pairs(forms) -> Tuple[List[Tuple[dict, dict, int]], int, int, int]:
+def _flatten(forms):
+    for f in forms:
+        if isinstance(f, list):  # a history vector [op op ...]
+            yield from _flatten(f)
+        else:
+            yield f
+
+
+def _pairs(forms):
+    """(ok, info, failed, unpaired): ok / info = [(invoke, completion, line)]."""
     pending: Dict[object, Tuple[dict, int]] = {}
-    done, failed, info = [], 0, 0
-    for i, op in enumerate(forms):
+    done, infos, failed = [], [], 0
+    for i, op in enumerate(_flatten(forms)):
         if not isinstance(op, dict):
             continue
         t, p = op.get(":type"), op.get(":process")
@@ -127,71 +145,126 @@ def _pairs(forms) -> Tuple[List[Tuple[dict, dict, int]], int, int, int]:
             if t == ":fail":
                 failed += 1
             elif t == ":info":
-                info += 1
+                infos.append((inv or {}, op, i))
             else:
                 done.append((inv or {}, op, i))
-    return done, failed, info, len(pending)
+    return done, infos, failed, len(pending)
 
 
 _INSERT_TABLES = 2  # adya.clj: tables a and b
+
+
+def _time(op, line):
+    t = op.get(":time")
+    return t if isinstance(t, int) else line
 
 
 def history_from_jepsen_edn(text: str) -> JepsenOps:
     """See the module docstring.  Register keys are ``:key`` when an op
     carries one (the reference's client has a single register, id 1); G2
     insert keys become (key, table) = 2 key + {0: a, 1: b}."""
-    done, failed, info, unpaired = _pairs(parse_edn(text))
-    # commit order: completion :time (line order breaks ties / stands in)
-    done.sort(key=lambda d: (d[1].get(":time", d[2]) if isinstance(d[1].get(":time"), int)
-                             else d[2], d[2]))
-    txn, key, isw, obs = [], [], [], []
-    writers: Dict[int, List[Tuple[int, object, object]]] = {}  # key -> [(txn, uid, value)]
-    reads: List[Tuple[int, int, str, object, object]] = []     # (op index, txn, kind, a, b)
+    done, infos, failed, unpaired = _pairs(parse_edn(text))
+    # every op that may be a txn: (order time, line, invoke, completion, is :ok)
+    # -- an :ok op commits at its completion, an :info op (if at all) by its
+    # completion, taken as its invoke
+    cands = [(_time(op, i), i, inv, op, True) for inv, op, i in done]
+    cands += [(_time(inv, i) if inv else i, i, inv, op, False) for inv, op, i in infos
+              if op.get(":f", inv.get(":f")) in (":write", ":cas")]
+    cands.sort(key=lambda c: (c[0], c[1]))
+    # per candidate: its ops as (key, is_write, read kind, a, b)
+    ops_of: List[List[tuple]] = []
+    writers: Dict[int, List[Tuple[int, object, object]]] = {}  # key -> [(cand, uid, value)]
     g2: Dict[int, int] = {}
-    for t, (inv, op, _) in enumerate(done):
+    for c, (_, _, inv, op, ok) in enumerate(cands):
         f = op.get(":f", inv.get(":f"))
+        mine = []
         if f in (":read", ":write", ":cas"):
             k = int(op.get(":key", inv.get(":key", 1)))
             if f == ":read":
-                reads.append((len(txn), t, "uid", op.get(":uid"), op.get(":value")))
-                txn.append(t), key.append(k), isw.append(0), obs.append(-1)
+                if ":uid" in op:
+                    mine.append((k, 0, "uid", op.get(":uid"), op.get(":value")))
+                else:
+                    mine.append((k, 0, "value", op.get(":value"), None))
             else:
                 val = op.get(":value", inv.get(":value"))
                 if f == ":cas":
-                    cur, new = val
-                    reads.append((len(txn), t, "cas", cur, None))
-                    txn.append(t), key.append(k), isw.append(0), obs.append(-1)
-                    val = new
-                writers.setdefault(k, []).append((t, op.get(":uid", inv.get(":uid")), val))
-                txn.append(t), key.append(k), isw.append(1), obs.append(-1)
+                    cur, val = val
+                    mine.append((k, 0, "cas", cur, None))
+                writers.setdefault(k, []).append((c, op.get(":uid", inv.get(":uid")), val))
+                mine.append((k, 1, None, None, None))
         elif f == ":insert":
             k, (a_id, b_id) = op.get(":value", inv.get(":value"))
             g2[int(k)] = g2.get(int(k), 0) + 1
             for tb in range(_INSERT_TABLES):  # both tables read empty
-                txn.append(t), key.append(2 * int(k) + tb), isw.append(0), obs.append(-1)
-            txn.append(t), key.append(2 * int(k) + (0 if a_id is not None else 1))
-            isw.append(1), obs.append(-1)
-    dangling, drop = 0, set()
-    for i, t, kind, a, b in reads:
-        ws = writers.get(int(key[i]), [])
+                mine.append((2 * int(k) + tb, 0, "none", None, None))
+            mine.append((2 * int(k) + (0 if a_id is not None else 1), 1, None, None, None))
+        ops_of.append(mine)
+
+    def observed(c, k, kind, a, b):
+        """The candidate whose version a read of candidate c saw (None:
+        initial; -1: no writer produced it)."""
+        if kind == "none" or (kind in ("uid", "value") and a is None):
+            return None
+        ws = writers.get(k, [])
+        if kind == "cas":
+            hits = [w for w, u, v in reversed(ws) if w < c and v == a]
+            hits = [w for w in hits if cands[w][4]] or hits  # :ok writers first
+            return hits[0] if hits else -1
         if kind == "uid":
-            if a is None:
-                continue  # the initial (empty) register
-            cand = [w for w, u, v in ws if u == a and (b is None or v == b)]
-            before = [w for w in cand if w < t]
-            hit = before[-1] if before else (cand[0] if cand else None)
-        else:  # cas: the latest earlier version holding cur
-            hit = next((w for w, u, v in reversed(ws) if w < t and v == a), None)
-        if hit is None:
-            dangling += 1
-            drop.add(i)
+            match = [w for w, u, v in ws if u == a and (b is None or v == b)]
         else:
-            obs[i] = hit
-    keep = [i for i in range(len(txn)) if i not in drop]
-    h = History(np.array([txn[i] for i in keep], np.uint32), np.array([key[i] for i in keep], np.uint64),
-                np.array([isw[i] for i in keep], np.uint8), np.array([obs[i] for i in keep], np.int64),
-                len(done))
-    return JepsenOps(h, len(done), failed, info, unpaired, dangling, g2, [d[1] for d in done])
+            match = [w for w, u, v in ws if v == a]
+        for pool in ([w for w in match if cands[w][4]], match):  # :ok writers first
+            before = [w for w in pool if w < c]
+            if before:
+                return before[-1]
+            if pool:
+                return pool[0]
+        return -1
+
+    keep = [c[4] for c in cands]  # :ok ops; observed :info writes join below
+    seen: Dict[Tuple[int, int], object] = {}
+    for c, mine in enumerate(ops_of):
+        if not cands[c][4]:
+            continue
+        for j, (k, w, kind, a, b) in enumerate(mine):
+            if not w:
+                seen[(c, j)] = observed(c, k, kind, a, b)
+    # an :info write a committed read observed did commit (and its own reads
+    # then count too)
+    changed = True
+    while changed:
+        changed = False
+        for (c, j), hit in list(seen.items()):
+            if isinstance(hit, int) and hit >= 0 and not keep[hit]:
+                keep[hit] = True
+                changed = True
+                for jj, (k, w, kind, a, b) in enumerate(ops_of[hit]):
+                    if not w:
+                        seen[(hit, jj)] = observed(hit, k, kind, a, b)
+    tid = {}
+    for c in range(len(cands)):
+        if keep[c]:
+            tid[c] = len(tid)
+    txn, key, isw, obs = [], [], [], []
+    dangling = 0
+    for c, mine in enumerate(ops_of):
+        if not keep[c]:
+            continue
+        for j, (k, w, kind, a, b) in enumerate(mine):
+            o = -1
+            if not w:
+                hit = seen.get((c, j))
+                if hit is not None and (hit < 0 or not keep[hit]):
+                    dangling += 1
+                    continue
+                o = -1 if hit is None else tid[hit]
+            txn.append(tid[c]), key.append(k), isw.append(w), obs.append(o)
+    h = History(np.array(txn, np.uint32), np.array(key, np.uint64), np.array(isw, np.uint8),
+                np.array(obs, np.int64), len(tid))
+    recovered = sum(1 for c in range(len(cands)) if keep[c] and not cands[c][4])
+    return JepsenOps(h, len(done), failed, len(infos), unpaired, dangling, g2,
+                     [cands[c][3] for c in range(len(cands)) if keep[c]], recovered)
 
 
 def g2_illegal(ops: JepsenOps) -> Dict[int, int]:

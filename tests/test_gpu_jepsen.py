@@ -40,3 +40,16 @@ def test_adya_g2_history_scc_equals_tarjan_and_the_g2_checker(validator, oracle_
     keys = sorted({ops.txn_ops[int(t)][":value"][0] for t in np.nonzero(sizes[scc] > 1)[0]})
     assert keys == bad == sorted(J.g2_illegal(ops))
     assert st["nontrivial_sccs"] == len(bad)
+
+
+def test_reference_filetest_history_on_the_gpu(validator, oracle_mod):
+    """linearizable/filetest/history.txt (the reference's knossos fixture, as
+    data in tests/golden/): the GPU graph has the one wr edge and no cycle."""
+    import os
+    path = os.path.join(os.path.dirname(__file__), "golden", "jepsen_filetest_history.txt")
+    h = J.history_from_jepsen_edn(open(path).read()).history
+    scc, st = validator.dep_graph_scc(h)
+    assert scc.tolist() == [0, 1] and st["nontrivial_sccs"] == 0
+    s, d, t = validator.dep_graph_edges()
+    assert (s.tolist(), d.tolist(), t.tolist()) == ([0], [1], [2])  # type 2 = wr
+    np.testing.assert_array_equal(scc, _tarjan(oracle_mod, h))

@@ -127,6 +127,8 @@ def test_gpu_known_cycles(validator, oracle_mod, h):
     dict(n_txn=200000, n_keys=5000, concurrent_frac=0.05, max_lag=32),
     dict(n_txn=100000, n_keys=300, concurrent_frac=0.3, max_lag=8, zipf=1.2),  # hot keys
     dict(n_txn=1000000, n_keys=100000),
+    # the per-GPU share of BASELINE config 4 at 8 GPUs: 100M ops / 8 = 12.6M ops
+    dict(n_txn=2_100_000, n_keys=210_000),
 ])
 def test_gpu_graph_matches_oracle(validator, oracle_mod, kw):
     h = config4_history(**kw)

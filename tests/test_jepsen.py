@@ -86,3 +86,46 @@ def test_register_lost_updates_are_cycles(oracle_mod, seed):
     clean, _ = J.register_history_edn(seed, n_ops=3000, lost_update=0.0, stale_read=0.0)
     _, none = components(oracle_mod, J.history_from_jepsen_edn(clean).history)
     assert not none  # a serial execution without anomalies has no cycle
+
+
+GOLDEN_FILETEST = __import__("os").path.join(__import__("os").path.dirname(__file__), "golden",
+                                              "jepsen_filetest_history.txt")
+
+
+def test_reference_filetest_history(oracle_mod):
+    """The reference's own knossos fixture (linearizable/filetest/history.txt,
+    copied as data to tests/golden/): one EDN vector of a cas-register history
+    without :uid -- a write of 1, then a read returning 1.  The read observed
+    the write by its value: a 2-txn graph with one wr edge and no cycle, as
+    filetest.clj's knossos check finds it valid."""
+    ops = J.history_from_jepsen_edn(open(GOLDEN_FILETEST).read())
+    assert (ops.ok, ops.failed, ops.info, ops.unpaired, ops.dangling) == (2, 0, 0, 0, 0)
+    h = ops.history
+    assert h.ntxn == 2
+    rows = list(zip(h.txn.tolist(), h.is_write.tolist(), h.observed.tolist()))
+    assert rows == [(0, 1, -1), (1, 0, 0)]
+    s, d, t = oracle_mod.dep_edges(h.txn, h.key, h.is_write, h.observed)
+    assert list(zip(s.tolist(), d.tolist())) == [(0, 1)]
+    scc, comps = components(oracle_mod, h)
+    assert not comps and scc.tolist() == [0, 1]
+
+
+def test_info_writes_observed_by_a_read_committed():
+    """:info ops are indeterminate: a write a later read observed did commit
+    (it joins at its invoke), an unobserved one is dropped -- otherwise the
+    read would dangle and its edges (here the rw edge of a lost update) would
+    vanish."""
+    text = "\n".join([
+        "{:type :invoke :f :write :value 1 :process 0 :uid 5 :time 1}",
+        "{:type :info :f :write :process 0 :value 1 :uid 5 :time 3}",
+        "{:type :invoke :f :write :value 2 :process 1 :uid 6 :time 4}",
+        "{:type :info :f :write :process 1 :value 2 :uid 6 :time 5}",
+        "{:type :invoke :f :read :value nil :process 2 :time 6}",
+        "{:type :ok :f :read :process 2 :value 1 :uid 5 :time 7}",
+    ])
+    ops = J.history_from_jepsen_edn(text)
+    assert (ops.ok, ops.info, ops.info_recovered, ops.dangling) == (1, 2, 1, 0)
+    h = ops.history
+    assert h.ntxn == 2
+    rows = list(zip(h.txn.tolist(), h.is_write.tolist(), h.observed.tolist()))
+    assert rows == [(0, 1, -1), (1, 0, 0)]
