@@ -8,7 +8,9 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <cstdlib>
+#include <functional>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -152,21 +154,108 @@ struct IdxSpan {
 
 // One worker's share of a marshal (read sets [t0, t1) of the batch): probes
 // as AoS rows (W words of lo, W of hi) plus the scratch of the span builder.
-struct MarshalPart {
+// One range of a read set as the marshal reads it (window table id, -1 if
+// the table was never written).
+struct RangeRef {
+    int tid;
+    int idxnum;
+    const uint8_t *lkey, *rkey;
+    int lkeylen, rkeylen, lflag, rflag, islocked;
+};
+struct alignas(128) MarshalPart {  // one per worker: no shared cache lines
     std::vector<uint64_t> lohi;  // [n][2W]
     std::vector<uint64_t> snap, lock_snap;
     std::vector<uint32_t> gid, txn, lock_table, lock_txn;
     std::vector<TxnTable> tabs;
     std::vector<IdxSpan> spans;
+    std::vector<RangeRef> refs;  // the read set's ranges, read once
+    uint64_t ix_last = ~0ull;    // cache of the last (table, index) group lookup
+    const std::vector<int> *ix_groups = nullptr;
     size_t out0 = 0, lock0 = 0;  // output offsets (assembly)
     void clear()
     {
         lohi.clear(), snap.clear(), lock_snap.clear(), gid.clear(), txn.clear();
         lock_table.clear(), lock_txn.clear();
+        ix_last = ~0ull;  // the dictionary may have changed since the last marshal
+        ix_groups = nullptr;
     }
 };
 
 struct Multi;  // hsc_multi.cpp: the members of a multi-GPU context
+
+// Persistent marshal workers (one pool per context, created on first use):
+// run(nwork, f) calls f(0 .. nwork - 1) on the pool's threads and the
+// caller's, dynamically scheduled, and returns when all are done.  A large
+// batch runs two parallel phases per pipeline chunk; spawning threads for
+// each cost tens of microseconds per thread.
+class WorkPool {
+  public:
+    explicit WorkPool(int nthreads) : size_(std::max(1, nthreads))
+    {
+        for (int i = 1; i < size_; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~WorkPool()
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int size() const { return size_; }
+    void run(int nwork, const std::function<void(int)> &f)
+    {
+        if (nwork <= 0) return;
+        if (th_.empty() || nwork == 1) {
+            for (int i = 0; i < nwork; ++i) f(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &f;
+            nwork_ = nwork;
+            next_.store(0, std::memory_order_relaxed);
+            busy_ = (int)th_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        work();
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return busy_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void work()
+    {
+        for (int i = next_.fetch_add(1); i < nwork_; i = next_.fetch_add(1)) (*job_)(i);
+    }
+    void loop()
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            work();
+            std::lock_guard<std::mutex> g(m_);
+            if (--busy_ == 0) done_.notify_one();
+        }
+    }
+    const int size_;
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)> *job_ = nullptr;
+    std::atomic<int> next_{0};
+    int nwork_ = 0, busy_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
 
 }  // namespace hsc
 
@@ -331,6 +420,7 @@ struct hsc_ctx {
     Stage stage[2];
     std::vector<MarshalPart> parts;
     int threads = 1;
+    std::unique_ptr<WorkPool> pool;  // `threads` workers (created by the first parallel marshal)
 
     // raw log / wire decode output
     DecodedLog decoded;
@@ -395,6 +485,9 @@ struct hsc_ctx {
     bool no_small = false;  // HSC_NO_SMALL=1 at context creation: the staged path
     uint32_t small_seq = 0;
     // small-path phase times (hsc_small_stats)
+    // marshal / batch phase totals (hsc_batch_stats)
+    std::atomic<uint64_t> mb_marshals{0}, mb_txns{0}, mb_ranges{0}, mb_parts_ns{0}, mb_alloc_ns{0},
+        mb_assemble_ns{0}, mb_launch_ns{0}, mb_wait_ns{0};
     std::atomic<uint64_t> sm_calls{0}, sm_marshal_ns{0}, sm_launch_ns{0}, sm_wait_ns{0},
         sm_slot_waits{0}, sm_lock_ns{0};
 

@@ -1374,29 +1374,41 @@ static int ingest_log(hsc_ctx *c, const hsc_llog *log)
 // ---------------------------------------------------------------------------
 // marshalling
 // ---------------------------------------------------------------------------
-struct RangeRef {
-    int tid;  // window table id or -1
-    int idxnum;
-    const uint8_t *lkey, *rkey;
-    int lkeylen, rkeylen, lflag, rflag, islocked;
-};
-
 // Bound normalised to the group's key length klen (padding lemma, SURVEY
 // §8(a) A0): lower = lkey[0..min) ++ 0x00.., upper = rkey[0..min) ++ 0xFF..;
 // open bounds become 0x00^klen / 0xFF^klen.  Then zero padded to W words.
-static void norm_bound(const uint8_t *key, int keylen, int flag, int klen, bool upper, int W,
-                       uint64_t *out)
+static inline void norm_bound(const uint8_t *key, int keylen, int flag, int klen, bool upper, int W,
+                              uint64_t *out)
 {
-    uint8_t buf[kMaxWords * 8];
-    memset(buf, 0, (size_t)W * 8);
-    if (flag) {
-        if (upper) memset(buf, 0xFF, (size_t)klen);
-    } else {
-        int m = (key && keylen > 0) ? std::min(keylen, klen) : 0;
-        if (m) memcpy(buf, key, (size_t)m);
-        if (upper && klen > m) memset(buf + m, 0xFF, (size_t)(klen - m));
+    // bytes [0, m) from the key, [m, klen) padding (0xFF for an upper bound),
+    // [klen, 8W) zero -- built word by word (a key word is one big-endian
+    // load when all its 8 bytes are key bytes)
+    const int m = flag ? 0 : ((key && keylen > 0) ? std::min(keylen, klen) : 0);
+    for (int j = 0; j < W; ++j) {
+        const int lo = 8 * j;
+        uint64_t v = 0;
+        const int nk = std::min(std::max(m - lo, 0), 8);
+        if (nk == 8) {
+            uint64_t x;
+            memcpy(&x, key + lo, 8);
+            v = __builtin_bswap64(x);
+        } else if (nk > 0) {
+            uint8_t b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            memcpy(b, key + lo, (size_t)nk);
+            uint64_t x;
+            memcpy(&x, b, 8);
+            v = __builtin_bswap64(x);
+        }
+        if (upper) {  // 0xFF over bytes [max(lo, m), min(lo + 8, klen)) of this word
+            const int p0 = std::max(lo, m) - lo, p1 = std::min(lo + 8, klen) - lo;
+            if (p1 > p0) {
+                const uint64_t a = p0 >= 8 ? 0 : ~0ull >> (8 * p0);
+                const uint64_t b = p1 >= 8 ? 0 : ~0ull >> (8 * p1);
+                v |= a & ~b;
+            }
+        }
+        out[j] = v;
     }
-    for (int j = 0; j < W; ++j) out[j] = load_be64(buf + 8 * j);
 }
 
 // Forced verdicts of a full check that do not depend on the ranges.
@@ -1423,13 +1435,17 @@ static void marshal_txn(const D *c, MarshalPart &mp, uint32_t txn, uint64_t S, i
     const int W = c->W;
     auto &tabs = mp.tabs;
     auto &spans = mp.spans;
+    auto &refs = mp.refs;
     tabs.clear();
     spans.clear();
+    if ((int)refs.size() < nr) refs.resize(nr);
     // pass 1: tables (first range fixes islocked) and per-index [begin, end]
     // spans in array order (currangearr_build_hash, db/sqlglue.c:312-351);
-    // spans of one table are kept contiguous by moving later tables' spans
+    // spans of one table are kept contiguous by moving later tables' spans.
+    // Every range is read once (refs) for both passes.
+    size_t slots = 0;
     for (int k = 0; k < nr; ++k) {
-        const RangeRef r = get(k);
+        const RangeRef r = refs[k] = get(k);
         if (r.tid < 0) continue;  // table never written: nothing can conflict
         int ti = 0;
         while (ti < (int)tabs.size() && tabs[ti].tid != r.tid) ++ti;
@@ -1446,7 +1462,9 @@ static void marshal_txn(const D *c, MarshalPart &mp, uint32_t txn, uint64_t S, i
         tt.ns++;
         for (int q = ti + 1; q < (int)tabs.size(); ++q) tabs[q].s0++;
     }
-    uint64_t w2[2 * kMaxWords];
+    // pass 2: the probes, written in place (room for every span slot x group;
+    // empty ranges are dropped by not advancing)
+    size_t n = mp.gid.size();
     for (const TxnTable &t : tabs) {
         if (t.islocked) {
             mp.lock_table.push_back((uint32_t)t.tid);
@@ -1456,26 +1474,51 @@ static void marshal_txn(const D *c, MarshalPart &mp, uint32_t txn, uint64_t S, i
         }
         for (int j = 0; j < t.ns; ++j) {
             const IdxSpan &sp = spans[t.s0 + j];
+            const uint64_t ik = ixkey(t.tid, sp.idx);
+            if (ik != mp.ix_last) {  // one-entry cache of the (table, index) -> groups lookup
+                auto it = c->ix_groups.find(ik);
+                mp.ix_last = ik;
+                mp.ix_groups = it == c->ix_groups.end() ? nullptr : &it->second;
+            }
+            if (!mp.ix_groups) continue;
+            slots += mp.ix_groups->size() * (size_t)(sp.e - sp.b + 1);
+        }
+    }
+    if (!slots) return;
+    mp.lohi.resize((n + slots) * 2 * (size_t)W);
+    mp.gid.resize(n + slots);
+    mp.snap.resize(n + slots);
+    mp.txn.resize(n + slots);
+    uint64_t *lohi = mp.lohi.data();
+    for (const TxnTable &t : tabs) {
+        if (t.islocked) continue;
+        for (int j = 0; j < t.ns; ++j) {
+            const IdxSpan &sp = spans[t.s0 + j];
             auto it = c->ix_groups.find(ixkey(t.tid, sp.idx));
             if (it == c->ix_groups.end()) continue;
             for (int g : it->second) {
                 const int klen = c->groups[g].klen;
                 for (int k = sp.b; k <= sp.e; ++k) {  // span quirk: every array slot
-                    const RangeRef r = get(k);
+                    const RangeRef &r = refs[k];
+                    uint64_t *w2 = lohi + n * 2 * (size_t)W;
                     norm_bound(r.lkey, r.lkeylen, r.lflag, klen, false, W, w2);
                     norm_bound(r.rkey, r.rkeylen, r.rflag, klen, true, W, w2 + W);
                     int cmp = 0;
                     for (int q = 0; q < W && !cmp; ++q)
                         if (w2[q] != w2[W + q]) cmp = w2[q] < w2[W + q] ? -1 : 1;
                     if (cmp > 0) continue;  // empty range never matches
-                    mp.lohi.insert(mp.lohi.end(), w2, w2 + 2 * W);
-                    mp.gid.push_back((uint32_t)g);
-                    mp.snap.push_back(S);
-                    mp.txn.push_back(txn);
+                    mp.gid[n] = (uint32_t)g;
+                    mp.snap[n] = S;
+                    mp.txn[n] = txn;
+                    ++n;
                 }
             }
         }
     }
+    mp.lohi.resize(n * 2 * (size_t)W);
+    mp.gid.resize(n);
+    mp.snap.resize(n);
+    mp.txn.resize(n);
 }
 
 // Table name -> window table id, with a one-entry cache (a read set names a
@@ -1646,25 +1689,17 @@ static int default_threads()
     return std::max(1, std::min(n, 64));
 }
 
-// Runs f(i) for i in [0, nwork) on up to nthreads threads (the caller's
-// included).
+// Runs f(i) for i in [0, nwork) on the context's worker pool (parallel) or
+// on the caller's thread.
 template <class F>
-static void par_for(int nthreads, int nwork, F f)
+static void par_for(hsc_ctx *c, bool parallel, int nwork, F f)
 {
-    const int nt = std::max(1, std::min(nthreads, nwork));
-    if (nt == 1) {
+    if (!parallel || c->threads <= 1 || nwork <= 1) {
         for (int i = 0; i < nwork; ++i) f(i);
         return;
     }
-    std::atomic<int> next{0};
-    auto body = [&] {
-        for (int i = next.fetch_add(1); i < nwork; i = next.fetch_add(1)) f(i);
-    };
-    std::vector<std::thread> th;
-    th.reserve(nt - 1);
-    for (int k = 1; k < nt; ++k) th.emplace_back(body);
-    body();
-    for (auto &t : th) t.join();
+    if (!c->pool || c->pool->size() != c->threads) c->pool.reset(new WorkPool(c->threads));
+    c->pool->run(nwork, std::function<void(int)>(f));
 }
 
 // Marshal read sets [t0, t1) of src into the staging set st: parts in
@@ -1682,8 +1717,9 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
     const bool pin = !c->host_only || c->multi;  // a multi context uploads from it
     if (st.forced.ensure((size_t)std::max(nt, 1), pin)) return fail(c, HSC_ENOMEM, "staging");
     uint8_t *forced = st.forced.as<uint8_t>();
+    const auto tp0 = std::chrono::steady_clock::now();
     if (nt < kMarshalParallelMin) src.prefetch(t0, t1);
-    par_for(nt >= kMarshalParallelMin ? c->threads : 1, nwork, [&](int w) {
+    par_for(c, nt >= kMarshalParallelMin, nwork, [&](int w) {
         MarshalPart &mp = c->parts[w];
         mp.clear();
         TableLookup tl{c};
@@ -1705,6 +1741,7 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
         n += c->parts[w].gid.size();
         nl += c->parts[w].lock_table.size();
     }
+    const auto tp1 = std::chrono::steady_clock::now();
     st.L = stage_layout(W, n, nl);
     if (st.arena.ensure(std::max<size_t>(st.L.total + (st.coh ? small_tail((size_t)nt) : 0), 256), pin,
                         st.coh && pin))
@@ -1726,7 +1763,8 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
         if (gcls[g] != cls0) cls0 = kMaxWords + 1;
     }
     const bool by_len = cls0 == kMaxWords + 1;
-    par_for(n >= (size_t)kMarshalParallelMin ? c->threads : 1, nwork, [&](int w) {
+    const auto tp2 = std::chrono::steady_clock::now();
+    par_for(c, n >= (size_t)kMarshalParallelMin, nwork, [&](int w) {
         const MarshalPart &mp = c->parts[w];
         const size_t o = mp.out0, k = mp.gid.size();
         if (by_len) {
@@ -1762,6 +1800,16 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
             memcpy(ltxn + lo0, mp.lock_txn.data(), 4 * kl);
         }
     });
+    const auto tp3 = std::chrono::steady_clock::now();
+    auto ns = [](auto a, auto b) {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+    };
+    c->mb_marshals.fetch_add(1, std::memory_order_relaxed);
+    c->mb_txns.fetch_add((uint64_t)nt, std::memory_order_relaxed);
+    c->mb_ranges.fetch_add(n, std::memory_order_relaxed);
+    c->mb_parts_ns.fetch_add(ns(tp0, tp1), std::memory_order_relaxed);
+    c->mb_alloc_ns.fetch_add(ns(tp1, tp2), std::memory_order_relaxed);
+    c->mb_assemble_ns.fetch_add(ns(tp2, tp3), std::memory_order_relaxed);
     st.n = n;
     st.n_lock = nl;
     st.n_txn = (size_t)nt;
@@ -2525,17 +2573,25 @@ static int check_src(hsc_ctx *c, const Src &src, int *rc_out,
     }
     int pending[2] = {-1, -1};
     int rc = HSC_OK;
+    auto timed = [&](std::atomic<uint64_t> &acc, auto f) {
+        const auto a = SteadyClock::now();
+        const int r = f();
+        acc.fetch_add(ns_since(a), std::memory_order_relaxed);
+        return r;
+    };
     for (int i = 0; i < nchunks && rc == HSC_OK; ++i) {
         Stage &st = c->stage[i & 1];
-        if (pending[i & 1] >= 0) rc = finish_stage(c, st, rc_out + pending[i & 1]);
+        if (pending[i & 1] >= 0)
+            rc = timed(c->mb_wait_ns, [&] { return finish_stage(c, st, rc_out + pending[i & 1]); });
         pending[i & 1] = -1;
         const int t0 = i * per, t1 = std::min(T, t0 + per);
         if (rc == HSC_OK) rc = marshal_into(c, src, t0, t1, st);
-        if (rc == HSC_OK) rc = launch_stage(c, st);
+        if (rc == HSC_OK) rc = timed(c->mb_launch_ns, [&] { return launch_stage(c, st); });
         if (rc == HSC_OK) pending[i & 1] = t0;
     }
     for (int i = nchunks; i < nchunks + 2 && rc == HSC_OK; ++i)
-        if (pending[i & 1] >= 0) rc = finish_stage(c, c->stage[i & 1], rc_out + pending[i & 1]);
+        if (pending[i & 1] >= 0)
+            rc = timed(c->mb_wait_ns, [&] { return finish_stage(c, c->stage[i & 1], rc_out + pending[i & 1]); });
     if (rc != HSC_OK) {
         (void)hipStreamSynchronize(c->stream);  // nothing in flight on the staging sets
         return rc;
@@ -2981,6 +3037,22 @@ int hsc_marshal_readsets(hsc_ctx *c, const hsc_readsets *rs, const hsc_marshalle
     return rc;
 }
 
+int hsc_marshal_arrs(hsc_ctx *c, void *const *ranges, const uint64_t *snaps, int n,
+                     const hsc_marshalled **out)
+{
+    if (!c || n < 0 || (n && (!ranges || !snaps)) || !out) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->host_only) (void)hipSetDevice(c->device);
+    int rc = ensure_built(c);
+    if (rc) return rc;
+    for (int i = 0; i < n; ++i)
+        if (!ranges[i]) return fail(c, HSC_EINVAL, "marshal: NULL CurRangeArr");
+    ArrSrc src{(hsc_currangearr *const *)ranges, snaps, n};
+    rc = marshal_into(c, src, 0, n, c->stage[0]);
+    *out = &c->m;
+    return rc;
+}
+
 long hsc_window_export(hsc_ctx *c, int all_versions, uint32_t *gid, uint64_t *key_words,
                        uint64_t *lsn, size_t cap)
 {
@@ -3413,6 +3485,20 @@ int hsc_small_stats(hsc_ctx *c, hsc_small_stats_t *out)
     out->wait_ns = c->sm_wait_ns.load();
     out->slot_waits = c->sm_slot_waits.load();
     out->lock_ns = c->sm_lock_ns.load();
+    return HSC_OK;
+}
+
+int hsc_batch_stats(hsc_ctx *c, hsc_batch_stats_t *out)
+{
+    if (!c || !out) return HSC_EINVAL;
+    out->marshals = c->mb_marshals.load();
+    out->read_sets = c->mb_txns.load();
+    out->ranges = c->mb_ranges.load();
+    out->parts_ns = c->mb_parts_ns.load();
+    out->alloc_ns = c->mb_alloc_ns.load();
+    out->assemble_ns = c->mb_assemble_ns.load();
+    out->launch_ns = c->mb_launch_ns.load();
+    out->wait_ns = c->mb_wait_ns.load();
     return HSC_OK;
 }
 

@@ -126,6 +126,11 @@ class SmallStats(C.Structure):
                 ("wait_ns", C.c_uint64), ("slot_waits", C.c_uint64), ("lock_ns", C.c_uint64)]
 
 
+class BatchStats(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("marshals", "read_sets", "ranges", "parts_ns", "alloc_ns",
+                                          "assemble_ns", "launch_ns", "wait_ns")]
+
+
 class ConcurrentResult(C.Structure):
     _fields_ = [("seconds", C.c_double), ("calls", C.c_uint64), ("lat_mean_us", C.c_double),
                 ("lat_p50_us", C.c_double), ("lat_p99_us", C.c_double)]
@@ -154,6 +159,7 @@ EXPORTS = [
     "hsc_multi_create", "hsc_multi_unique_ids", "hsc_multi_create_rank", "hsc_multi_world",
     "hsc_multi_rank", "hsc_multi_local", "hsc_multi_member", "hsc_multi_set_splitters",
     "hsc_multi_adopt", "hsc_multi_probe_device", "hsc_multi_stats", "hsc_multi_last_counts",
+    "hsc_marshal_arrs", "hsc_batch_stats",
 ]
 MULTI_ID_BYTES = 2 * 128  # hsc_multi_unique_ids: one RCCL id per lane
 
@@ -247,6 +253,9 @@ def load() -> C.CDLL:
                                              C.c_int, C.POINTER(C.c_int),
                                              C.POINTER(ConcurrentResult)]),
         "hsc_window_layout": (C.c_int, [_p]),
+        "hsc_batch_stats": (C.c_int, [_p, C.POINTER(BatchStats)]),
+        "hsc_marshal_arrs": (C.c_int, [_p, C.POINTER(_p), _p, C.c_int,
+                                       C.POINTER(C.POINTER(Marshalled))]),
         "hsc_multi_create": (C.c_int, [C.POINTER(C.c_int), C.c_int, ctx_pp]),
         "hsc_multi_unique_ids": (C.c_int, [_p, C.c_size_t]),
         "hsc_multi_create_rank": (C.c_int, [C.c_int, C.c_int, C.c_int, _p, C.c_size_t, ctx_pp]),
@@ -648,6 +657,13 @@ class Validator:
         self._chk(rc, "hip_serial_check_batch")
         return out[:n]
 
+    def batch_stats(self) -> dict:
+        """Marshal / batch phase totals (hsc_batch_stats), in ms and counts."""
+        st = BatchStats()
+        self._chk(self.lib.hsc_batch_stats(self.ctx, C.byref(st)), "hsc_batch_stats")
+        d = {k: getattr(st, k) for k, _ in BatchStats._fields_}
+        return {k: (v / 1e6 if k.endswith("_ns") else v) for k, v in d.items()}
+
     def small_stats(self) -> dict:
         """Small-batch path phase totals (hsc_small_stats): calls and the mean
         host marshal, slot launch and done-word wait per call (us), and the
@@ -754,13 +770,26 @@ class Validator:
             rkeylen=i32(out.rkeylen), lkey_off=arr(out.lkey_off, C.c_uint64, np.uint64),
             rkey_off=arr(out.rkey_off, C.c_uint64, np.uint64))
 
+    def marshal_arrs(self, arrs, snaps, copy: bool = True):
+        """hsc_marshal_arrs over NativeCurRangeArrs / CurRangeArrays (the host
+        half of hip_serial_check_batch); copy=False returns only the counts."""
+        n = len(arrs.arrs) if hasattr(arrs, "arrs") else arrs.n
+        sn = np.ascontiguousarray(snaps, np.uint64)
+        mp = C.POINTER(Marshalled)()
+        self._chk(self.lib.hsc_marshal_arrs(self.ctx, arrs.pointers(), sn.ctypes.data, n,
+                                            C.byref(mp)), "hsc_marshal_arrs")
+        return self._marshalled(mp.contents) if copy else (mp.contents.n, mp.contents.n_lock)
+
     def marshal(self, rs: ReadSets) -> dict:
         """Marshal read sets into probe SoA (numpy copies)."""
         s, keep = readsets_struct(rs)
         mp = C.POINTER(Marshalled)()
         self._chk(self.lib.hsc_marshal_readsets(self.ctx, C.byref(s), C.byref(mp)),
                   "hsc_marshal_readsets")
-        m = mp.contents
+        return self._marshalled(mp.contents)
+
+    @staticmethod
+    def _marshalled(m) -> dict:
         W, n, nl, nt = m.words, m.n, m.n_lock, m.n_txn
 
         def arr(p, cnt, dt):

@@ -414,6 +414,19 @@ typedef struct hsc_small_stats_t {
     uint64_t lock_ns;    /* hip_serial_check_batch calls (any path) waiting for the context lock */
 } hsc_small_stats_t;
 int hsc_small_stats(hsc_ctx *ctx, hsc_small_stats_t *out);
+/* Marshal and batch phase totals since the context was created: marshal
+ * calls (one per pipeline chunk), read sets, range probes written; the
+ * parallel walk of the read sets into per-worker parts (CurRange pointer
+ * walk, dictionary lookups, bound padding), the staging allocation, the SoA
+ * assembly; and for the staged path the upload + launch and the wait for a
+ * chunk's verdicts (device time + transfers not hidden behind the next
+ * chunk's marshal). */
+typedef struct hsc_batch_stats_t {
+    uint64_t marshals, read_sets, ranges;
+    uint64_t parts_ns, alloc_ns, assemble_ns, launch_ns, wait_ns;
+} hsc_batch_stats_t;
+int hsc_batch_stats(hsc_ctx *ctx, hsc_batch_stats_t *out);
+
 int hsc_collector_create(hsc_ctx *ctx, int max_batch, int max_wait_us, hsc_collector **out);
 void hsc_collector_destroy(hsc_collector *col);
 int hsc_collector_check(hsc_collector *col, void *ranges, unsigned int *file,
@@ -481,6 +494,11 @@ typedef struct hsc_marshalled {
  * memory owned by the library; valid until the next marshal / ctx destroy). */
 int hsc_marshal_readsets(hsc_ctx *ctx, const hsc_readsets *rs,
                          const hsc_marshalled **out);
+/* The host half of hip_serial_check_batch: CurRangeArr* ranges[n] (none
+ * NULL) with snapshot LSNs snaps[n], marshalled as hsc_marshal_readsets does
+ * (works on host-only contexts; the timing harness of the batch entry). */
+int hsc_marshal_arrs(hsc_ctx *ctx, void *const *ranges, const uint64_t *snaps, int n,
+                     const hsc_marshalled **out);
 /* Run the join for a device-resident batch, asynchronously on the stream. */
 int hsc_probe_device(hsc_ctx *ctx, const hsc_probe_batch *b);
 /* verdict bytes -> bitmap (e.g. after a cross-GPU max all-reduce). */
