@@ -26,6 +26,15 @@
 // touch of a request: its caller may return right after), then wakes the
 // whole batch with one futex call, and the woken callers return without
 // taking the collector lock.
+//
+// The next leader is designated, not raced for: when a leader takes its
+// batch (or a batch ends with requests queued and none elected), the oldest
+// queued request is marked to lead and only waiters whose wake bit matches
+// its (FUTEX_WAKE_BITSET, one of 32 bits per request) are woken -- waking the
+// whole queue to elect one of them made every election a thundering herd of
+// lock acquisitions, which on a CPU-quota'd host (256 caller threads, 16 CPUs
+// of quota) burnt the quota and stalled every thread for the rest of the
+// period (p99 77 ms in r03).
 #include "../../include/hip_serial.h"
 #include "hsc_internal.h"
 
@@ -50,14 +59,15 @@ namespace {
 constexpr uint32_t kDone = 1u;  // Req::word: the verdict is ready
 constexpr uint32_t kChans = 16;  // batch wait words (more than batches alive at once: <= 4 + 1)
 
-void futex_wait(std::atomic<uint32_t> *w, uint32_t seen)
+// wait on w while it holds `seen`, for a wake whose bitset meets `bits`
+void futex_wait(std::atomic<uint32_t> *w, uint32_t seen, uint32_t bits = FUTEX_BITSET_MATCH_ANY)
 {
-    syscall(SYS_futex, (uint32_t *)w, FUTEX_WAIT_PRIVATE, seen, nullptr, nullptr, 0);
+    syscall(SYS_futex, (uint32_t *)w, FUTEX_WAIT_BITSET_PRIVATE, seen, nullptr, nullptr, bits);
 }
 
-void futex_wake_all(std::atomic<uint32_t> *w)
+void futex_wake(std::atomic<uint32_t> *w, uint32_t bits = FUTEX_BITSET_MATCH_ANY)
 {
-    syscall(SYS_futex, (uint32_t *)w, FUTEX_WAKE_PRIVATE, INT_MAX, nullptr, nullptr, 0);
+    syscall(SYS_futex, (uint32_t *)w, FUTEX_WAKE_BITSET_PRIVATE, INT_MAX, nullptr, nullptr, bits);
 }
 
 }  // namespace
@@ -76,6 +86,8 @@ struct hsc_collector {
         int rc;
         hsc::PreMarshal *pm;  // the caller's marshalled rows, or null
         bool queued;    // in q (under m): not yet taken into a batch
+        bool lead;      // (under m) designated to lead the next batch
+        uint32_t bit;   // its futex wake bit (leader designation wakes only that bit)
         uint32_t chan;  // the batch id open when it queued (its wait word: chan % kChans)
         std::atomic<uint32_t> word{0};
     };
@@ -83,6 +95,7 @@ struct hsc_collector {
     bool elected = false;  // a leader is waiting to take the next batch
     int running = 0;       // batches on the device
     uint32_t open_id = 0;  // the batch queued requests will join
+    uint32_t next_bit = 0;  // round-robin wake bits
     std::atomic<uint32_t> chan[kChans];  // per-batch wait words (bumped at each wake)
     std::condition_variable run_cv;     // a batch finished (the elected leader waits)
     std::condition_variable arrive_cv;  // a request queued (a gathering leader waits)
@@ -97,13 +110,25 @@ struct hsc_collector {
 
 namespace {
 
-// wake the callers sleeping on batch word `id` to re-check (the queued ones
-// elect a leader; the others sleep again)
-void wake(hsc_collector *k, uint32_t id)
+// wake the callers sleeping on batch word `id` (bits: only those whose wake
+// bit is among them) to re-check
+void wake(hsc_collector *k, uint32_t id, uint32_t bits = FUTEX_BITSET_MATCH_ANY)
 {
     std::atomic<uint32_t> &w = k->chan[id % kChans];
     w.fetch_add(1, std::memory_order_acq_rel);
-    futex_wake_all(&w);
+    futex_wake(&w, bits);
+}
+
+// (under m) the oldest queued request leads the next batch: mark it and wake
+// the waiters of its word that share its bit.  Returns the (word, bit) to
+// wake once the lock is dropped, or bit 0 when there is nothing to do.
+std::pair<uint32_t, uint32_t> designate(hsc_collector *k)
+{
+    if (k->elected || k->q.empty()) return {0, 0};
+    hsc_collector::Req *q = k->q.front();
+    q->lead = true;
+    k->elected = true;
+    return {q->chan, q->bit};
 }
 
 // one device pass over a group of requests that share regop_only
@@ -194,9 +219,15 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
     k->inside.fetch_add(1, std::memory_order_relaxed);
     std::unique_lock<std::mutex> lk(k->m);
     r.chan = k->open_id;
+    r.bit = 1u << (k->next_bit++ & 31);
+    r.lead = false;
     k->q.push_back(&r);
     k->st.calls++;
     if (k->max_wait_us > 0) k->arrive_cv.notify_one();
+    if (!k->elected) {  // nobody leads the next batch yet: this caller does
+        k->elected = true;
+        r.lead = true;
+    }
     for (;;) {  // under lk
         if (!r.queued) {
             // in a batch: wait for the done bit without the lock (the batch's
@@ -210,16 +241,16 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
             }
             break;
         }
-        if (k->elected) {  // queued behind an elected leader: sleep until woken
+        if (!r.lead) {  // queued: sleep until taken into a batch or designated
             std::atomic<uint32_t> &w = k->chan[r.chan % kChans];
             const uint32_t seen = w.load(std::memory_order_acquire);
             lk.unlock();
-            futex_wait(&w, seen);
+            futex_wait(&w, seen, r.bit);
             if (r.word.load(std::memory_order_acquire) & kDone) break;  // taken and answered meanwhile
             lk.lock();
             continue;
         }
-        k->elected = true;  // this caller leads the next batch
+        // this caller leads the next batch
         const auto tg = std::chrono::steady_clock::now();
         k->run_cv.wait(lk, [k] { return k->running < k->max_inflight; });
         k->st.gate_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(
@@ -235,20 +266,21 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
             hsc_collector::Req *q = k->q.front();
             k->q.pop_front();
             q->queued = false;
+            q->lead = false;
             mine |= q == &r;
             if (std::find(ids.begin(), ids.end(), q->chan) == ids.end()) ids.push_back(q->chan);
             (q->regop_only ? regop : full).push_back(q);
         }
-        const uint32_t taken_id = k->open_id++;  // later arrivals form the next batch
+        r.lead = false;
+        k->open_id++;  // later arrivals form the next batch
         k->running++;
         k->elected = false;
-        // requests max_batch left queued (they sleep on this batch's word):
-        // they join the next batch, and wake to elect its leader
-        if (!k->q.empty()) {
-            for (hsc_collector::Req *q : k->q) q->chan = k->open_id;
-            wake(k, taken_id);
-        }
+        // requests max_batch left queued join the next batch
+        for (hsc_collector::Req *q : k->q) q->chan = k->open_id;
+        // the next batch's leader: designated now, it gathers while this one runs
+        const auto nl = designate(k);
         lk.unlock();
+        if (nl.second) wake(k, nl.first, nl.second);
         const auto t0 = std::chrono::steady_clock::now();
         run_group(k, regop, 1);
         run_group(k, full, 0);
@@ -259,10 +291,9 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
         k->st.batches++;
         k->st.max_batch = std::max<uint64_t>(k->st.max_batch, take);
         k->run_cv.notify_one();
-        const bool elect = !k->elected && !k->q.empty();
-        const uint32_t next = elect ? k->q.front()->chan : 0;
+        const auto nl2 = designate(k);
         lk.unlock();
-        if (elect) wake(k, next);
+        if (nl2.second) wake(k, nl2.first, nl2.second);
         // hand out the verdicts: each done bit is the last touch of its
         // request, then one wake per batch word
         for (auto *g : {&regop, &full})
