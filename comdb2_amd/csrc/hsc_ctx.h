@@ -344,6 +344,19 @@ struct hsc_ctx {
     int app_i = 0;
     HBuf *h_app = nullptr;          // the buffer of the append being staged
     hipEvent_t app_last = nullptr;  // recorded behind the last append's device work
+    // pending tail (narrow windows, the small-batch path): an append's rows
+    // and raised table maxima are mirrored into mapped pinned memory that
+    // k_small_narrow scans beside the delta runs, and stay in app_* until
+    // kPendRows of them (or a batch that is not small) merge them into the
+    // live run with one launch.  A ring of two: a buffer is refilled only
+    // after the launch that retired it ran (its event); rows [0, pend_n) of
+    // the current one never change while it is current.
+    HBuf h_pend[2];
+    hipEvent_t pend_ev[2] = {};
+    int pend_i = 0;
+    uint32_t pend_n = 0, pend_t = 0;   // rows / table entries mirrored
+    std::vector<uint32_t> app_tchg;    // tables whose maximum rose since the last mirror
+    uint64_t pend_appends = 0, pend_merges = 0;
     ProbeView raw_probe{};           // the batch being probed, untransformed (delta probe)
     // background fold: once the live run holds fold_rows rows it
     // is frozen, and a shadow context rebuilds the main window from the main
@@ -396,6 +409,7 @@ struct hsc_ctx {
     DBuf d_pk[2];              // packed-key sort: the keys, ping-pong (hsc_ingest.hip)
     bool packed_sort = false;  // the last build sorted packed keys
     DBuf d_gstart, d_gend, d_tmax, d_table_max, d_group_table, d_count, d_sp_g, d_sp_w;
+    uint32_t nt_dev = 0;  // tables whose maxima d_table_max holds (later ones: the pending tail)
     // compact codes of a wide window (hsc_compact.hip): WinView wc over them
     bool compact = false;
     CompactTables ct{};

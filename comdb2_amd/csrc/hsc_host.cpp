@@ -196,6 +196,24 @@ static int group_id_or_add(hsc_ctx *c, int tid, int ix, int klen)
 
 static void fold_discard(hsc_ctx *c);
 
+// The pending tail's rows and table entries are all in app_* / the uploaded
+// table maxima now (or dropped with them): the next append mirrors into the
+// other buffer, this one is refilled once the launches queued so far ran.
+static void pend_retire(hsc_ctx *c)
+{
+    c->app_tchg.clear();
+    if (!c->pend_n && !c->pend_t) return;
+    const int i = c->pend_i;
+    if ((!c->pend_ev[i] && hipEventCreateWithFlags(&c->pend_ev[i], hipEventDisableTiming) != hipSuccess) ||
+        hipEventRecord(c->pend_ev[i], c->stream) != hipSuccess) {
+        if (c->pend_ev[i]) (void)hipEventDestroy(c->pend_ev[i]);
+        c->pend_ev[i] = nullptr;
+        (void)hipStreamSynchronize(c->stream);  // no event: nothing may still read the buffer
+    }
+    c->pend_i ^= 1;
+    c->pend_n = c->pend_t = 0;
+}
+
 static void clear_window(hsc_ctx *c)
 {
     fold_discard(c);
@@ -216,6 +234,7 @@ static void clear_window(hsc_ctx *c)
     c->dn = 0;
     c->app_gid.clear(), c->app_keys.clear(), c->app_koff.clear(), c->app_lsn.clear();
     c->app_tmax = false;
+    pend_retire(c);
     c->n = 0;
 }
 
@@ -225,6 +244,8 @@ static void add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keyle
     if (lsn > c->h_table_max[tid]) {
         c->h_table_max[tid] = lsn;
         c->app_tmax = true;
+        if (c->live && !c->host_only && (c->app_tchg.empty() || c->app_tchg.back() != (uint32_t)tid))
+            c->app_tchg.push_back((uint32_t)tid);
     }
     if (lsn > c->max_commit) c->max_commit = lsn;
     if (!has_key) return;
@@ -643,6 +664,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
     std::vector<uint64_t> tm(std::max(nt, 1), 0);
     for (int t = 0; t < nt; ++t) tm[t] = c->h_table_max[t];
     HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, tm.data(), 8 * tm.size(), hipMemcpyHostToDevice, s));
+    c->nt_dev = (uint32_t)nt;
     WinView w{};
     w.words = c->d_words.as<uint64_t>();
     w.stride = cap;
@@ -788,6 +810,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
     c->dn = 0;  // every appended row is in the rebuilt window
     c->app_gid.clear(), c->app_keys.clear(), c->app_koff.clear(), c->app_lsn.clear();
     c->app_tmax = false;
+    pend_retire(c);
     return HSC_OK;
 }
 
@@ -881,8 +904,62 @@ static DeltaView delta_view(const hsc_ctx *c)
 // into the main window instead (at the next check).
 static int fold_start(hsc_ctx *c);
 static int fold_finish(hsc_ctx *c, bool wait);
+static bool small_path(hsc_ctx *c, int T);
 
-static int flush_appends(hsc_ctx *c)
+// An append that can stay in the pending tail: k = every unmerged row
+// (mirrored ones included).  The next small check scans them; the merge waits
+// for kPendRows of them or a batch that is not small (probe -> settle).
+static bool pend_fits(hsc_ctx *c, size_t k, bool sync_only)
+{
+    return !sync_only && small_path(c, 1) && c->W <= kPendMaxWords && k <= kPendRows &&
+           c->dn + k <= kDeltaCap && c->pend_t + c->app_tchg.size() <= kPendRows;
+}
+
+// Mirror rows [pend_n, k) of app_* and the raised table maxima into the
+// current pending buffer (rows below pend_n are never rewritten while a
+// launch may read them).
+static int pend_mirror(hsc_ctx *c)
+{
+    const int i = c->pend_i;
+    HBuf &b = c->h_pend[i];
+    if (!c->pend_n && !c->pend_t) {  // a buffer being refilled: its last readers ran
+        if (c->pend_ev[i] && hipEventSynchronize(c->pend_ev[i]) != hipSuccess)
+            return fail(c, HSC_EDEVICE, "pending tail event");
+        if (b.ensure(kPendBytes, true, true)) return fail(c, HSC_ENOMEM, "pending tail");
+    }
+    uint8_t *p = b.as<uint8_t>();
+    const size_t k = c->app_gid.size();
+    const int W = c->W;
+    uint8_t buf[kPendMaxWords * 8];
+    for (size_t r = c->pend_n; r < k; ++r) {
+        const int klen = c->groups[c->app_gid[r]].klen;
+        memset(buf, 0, sizeof buf);
+        if (klen) memcpy(buf, c->app_keys.data() + c->app_koff[r], (size_t)std::min(klen, 8 * W));
+        ((uint32_t *)p)[r] = c->app_gid[r];
+        ((uint64_t *)(p + kPendLsn))[r] = c->app_lsn[r];
+        for (int j = 0; j < W; ++j) ((uint64_t *)(p + kPendWords))[(size_t)j * kPendRows + r] = load_be64(buf + 8 * j);
+    }
+    uint32_t *tt = (uint32_t *)(p + kPendTtid);
+    uint64_t *tl = (uint64_t *)(p + kPendTlsn);
+    for (uint32_t t : c->app_tchg) {
+        bool seen = false;  // one entry per table and append, its latest maximum
+        for (uint32_t e = c->pend_t; e-- > 0 && !seen;) seen = tt[e] == t && tl[e] == c->h_table_max[t];
+        if (seen) continue;
+        tt[c->pend_t] = t;
+        tl[c->pend_t] = c->h_table_max[t];
+        ++c->pend_t;
+    }
+    c->app_tchg.clear();
+    std::atomic_thread_fence(std::memory_order_release);
+    c->pend_n = (uint32_t)k;
+    c->pend_appends++;
+    return HSC_OK;
+}
+
+// lazy (the append entries): an append that fits stays in the pending tail.
+// Otherwise -- and for every caller that probes outside k_small_narrow --
+// the unmerged rows go to the delta run now.
+static int flush_appends(hsc_ctx *c, bool lazy = false)
 {
     if (c->multi) return multi_flush_appends(c);
     if (!c->live || c->host_only) return HSC_OK;
@@ -890,6 +967,7 @@ static int flush_appends(hsc_ctx *c)
     HIPCHK_RC(c, fold_finish(c, false));
     const size_t k = c->app_gid.size();
     const bool sync_only = window_words(c) > c->W || c->merge_pending || c->groups.size() > c->ng_built;
+    if (lazy && (k || c->app_tmax) && pend_fits(c, k, sync_only)) return pend_mirror(c);
     if (getenv("HSC_FOLD_TRACE"))
         fprintf(stderr, "[fold] k %zu dn %zu fn %zu ww %d W %d mp %d groups %zu/%zu state %d\n", k, c->dn, c->fn,
                 window_words(c), c->W, (int)c->merge_pending, c->groups.size(), c->ng_built,
@@ -914,6 +992,8 @@ static int flush_appends(hsc_ctx *c)
         if (nt) HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, c->h_app->p, 8 * (size_t)nt, hipMemcpyHostToDevice, s));
         HIPCHK_RC(c, app_staged(c, s));  // the ring keeps the buffer until the copy ran
         c->app_tmax = false;
+        c->nt_dev = (uint32_t)nt;
+        pend_retire(c);
         return HSC_OK;
     }
     const int W = c->W;
@@ -962,13 +1042,15 @@ static int flush_appends(hsc_ctx *c)
                           c->d_dlsn[o].as<uint64_t>(), c->dcap, c->d_dbmax.as<uint64_t>(), s,
                           nt ? a.lsn + k : nullptr, nt ? c->d_table_max.as<uint64_t>() : nullptr,
                           (uint32_t)nt, in_place));
-    if (nt) c->app_tmax = false;
+    if (nt) c->app_tmax = false, c->nt_dev = (uint32_t)nt;
     // no wait: the ring keeps h_app until its copies ran, and every later use
     // of the run is on this stream (hsc_set_stream orders a new stream after it)
     HIPCHK_RC(c, app_staged(c, s));
     c->dcur = o;
     c->dn += k;
     c->app_gid.clear(), c->app_keys.clear(), c->app_koff.clear(), c->app_lsn.clear();
+    if (c->pend_n || c->pend_t) c->pend_merges++;
+    pend_retire(c);
     if (c->dn >= c->fold_rows) {
         if (!c->fold_bg) {  // inline: the next check folds
             c->merge_pending = true;
@@ -1076,6 +1158,7 @@ static void swap_window(hsc_ctx *a, hsc_ctx *b)
     swap(a->d_pk[0], b->d_pk[0]), swap(a->d_pk[1], b->d_pk[1]), swap(a->packed_sort, b->packed_sort);
     swap(a->d_gstart, b->d_gstart), swap(a->d_gend, b->d_gend), swap(a->d_tmax, b->d_tmax);
     swap(a->d_table_max, b->d_table_max), swap(a->d_group_table, b->d_group_table);
+    swap(a->nt_dev, b->nt_dev);
     swap(a->d_count, b->d_count), swap(a->d_sp_g, b->d_sp_g), swap(a->d_sp_w, b->d_sp_w);
     swap(a->compact, b->compact), swap(a->ct, b->ct), swap(a->wc, b->wc);
     swap(a->d_cmask, b->d_cmask), swap(a->d_cpat, b->d_cpat), swap(a->d_cmv, b->d_cmv);
@@ -1197,6 +1280,7 @@ static int fold_finish(hsc_ctx *c, bool wait)
         c->h_table_max[t] = std::max(c->h_table_max[t], s->h_table_max[t]);
     HIPCHK(c, c->d_table_max.ensure(8 * (size_t)std::max(nt, 1)));
     if (nt) HIPCHK(c, hipMemcpy(c->d_table_max.p, c->h_table_max.data(), 8 * (size_t)nt, hipMemcpyHostToDevice));
+    c->nt_dev = (uint32_t)nt;
     c->app_tmax = false;
     c->fn = 0;
     HIPCHK(c, hipEventRecord(c->fold_ev, c->stream));  // the old window's last readers
@@ -2151,6 +2235,7 @@ static int probe_lane(hsc_ctx *c, const hsc_probe_batch *b);
 static int probe(hsc_ctx *c, const hsc_probe_batch *b)
 {
     if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
+    if (c->pend_n || c->pend_t) HIPCHK_RC(c, flush_appends(c));  // the pending tail is k_small_narrow's only
     HIPCHK(c, select_lane(c));
     const int rc = probe_lane(c, b);
     // the lane's done event fences whatever probe_lane launched, also when it
@@ -2468,11 +2553,18 @@ static int small_launch(hsc_ctx *c, Stage &st)
     if (empty) p.n = p.n_lock = 0;  // launch + done-word floor (verdicts all 0: wrong answers)
     NarrowView nv = c->nv;
     nv.table_max = c->d_table_max.as<uint64_t>();
-    nv.ntables = (uint32_t)c->table_names.size();
+    // tables past nt_dev have their maxima in the pending tail only
+    nv.ntables = std::min((uint32_t)c->table_names.size(), c->nt_dev);
     DeltaView d{}, d2{};
     if (c->dn) d = delta_view(c);
     if (c->fn) d2 = frozen_view(c);
-    HIPCHK(c, launch_small_narrow(nv, d, d2, p, dio + sl.vo, c->small_blocks.as<uint32_t>() + 16 * k,
+    PendView pd{};
+    if (c->pend_n || c->pend_t) {
+        pd.base = (const uint8_t *)c->h_pend[c->pend_i].dp;
+        pd.n = c->pend_n;
+        pd.nt = c->pend_t;
+    }
+    HIPCHK(c, launch_small_narrow(nv, d, d2, pd, p, dio + sl.vo, c->small_blocks.as<uint32_t>() + 16 * k,
                                   (uint32_t *)(dio + sl.dn), sl.seq, s));
     sl.busy.store(true, std::memory_order_release);
     c->small_next = (uint32_t)(k + 1);
@@ -2697,6 +2789,9 @@ void hsc_ctx_destroy(hsc_ctx *c)
     for (HBuf &b : c->h_appq) b.release();
     for (hipEvent_t &e : c->app_ev)
         if (e) (void)hipEventDestroy(e), e = nullptr;
+    for (HBuf &b : c->h_pend) b.release();
+    for (hipEvent_t &e : c->pend_ev)
+        if (e) (void)hipEventDestroy(e), e = nullptr;
     for (DBuf &b : c->co_dev) b.release();
     for (DBuf *b : {&c->e_span, &c->e_cnt, &c->e_txn, &c->e_lsn, &c->e_txn2, &c->e_lsn2, &c->e_gid,
                     &c->e_scratch, &c->e_flags, &c->e_after})
@@ -2785,7 +2880,7 @@ int hsc_window_append(hsc_ctx *c, const hsc_write *w, size_t n)
         c->dirty = true;
         return HSC_OK;
     }
-    return flush_appends(c);
+    return flush_appends(c, true);
 }
 
 int hsc_window_append_log(hsc_ctx *c, const hsc_llog *log)
@@ -2795,7 +2890,7 @@ int hsc_window_append_log(hsc_ctx *c, const hsc_llog *log)
     if (!c->host_only) (void)hipSetDevice(c->device);
     int rc = append_log(c, log);
     if (rc) return rc;
-    return c->live ? flush_appends(c) : HSC_OK;
+    return c->live ? flush_appends(c, true) : HSC_OK;
 }
 
 int hsc_window_append_raw(hsc_ctx *c, const hsc_raw_log *raw)
@@ -2806,7 +2901,7 @@ int hsc_window_append_raw(hsc_ctx *c, const hsc_raw_log *raw)
     return hsc_window_append_log(c, lg);
 }
 
-size_t hsc_window_delta_rows(hsc_ctx *c) { return c ? c->dn + c->fn : 0; }
+size_t hsc_window_delta_rows(hsc_ctx *c) { return c ? c->dn + c->fn + c->pend_n : 0; }
 
 int hsc_set_fold(hsc_ctx *c, size_t rows, int background)
 {
@@ -2825,6 +2920,16 @@ int hsc_fold_stats(hsc_ctx *c, uint64_t out[4])
     out[1] = c->folds_swapped;
     out[2] = c->folds_inline;
     out[3] = (uint64_t)(c->fold_ms * 1000.0f);
+    return HSC_OK;
+}
+
+int hsc_append_stats(hsc_ctx *c, uint64_t out[3])
+{
+    if (!c || !out) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    out[0] = c->pend_appends;
+    out[1] = c->pend_merges;
+    out[2] = c->pend_n;
     return HSC_OK;
 }
 
@@ -3018,9 +3123,13 @@ int hsc_merge_table_max(hsc_ctx *c, const uint64_t *in, int n)
         }
     if (!c->host_only && !c->dirty && n > 0) {
         (void)hipSetDevice(c->device);
-        HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, c->h_table_max.data(), 8 * (size_t)n,
+        const size_t nt = c->table_names.size();
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // no reader of the old buffer in flight
+        HIPCHK(c, c->d_table_max.ensure(8 * nt));
+        HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, c->h_table_max.data(), 8 * nt,
                                  hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipStreamSynchronize(c->stream));
+        c->nt_dev = (uint32_t)nt;
     }
     return HSC_OK;
 }

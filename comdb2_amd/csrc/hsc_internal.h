@@ -243,8 +243,20 @@ hipError_t narrow_codes(const NarrowView &nv, const ProbeView &p, uint64_t *lo64
 // The small-batch form (one launch: ranges, delta run, locks; inputs and
 // verdicts in host-mapped memory; the last block releases seq into *done).
 struct DeltaView;
+// The pending tail of appends (hsc_ctx.h h_pend): unsorted rows in mapped
+// pinned memory, [gid: 4P][lsn: 8P][words: [W][P], W <= kPendMaxWords]
+// [table ids: 4P][table maxima: 8P] with P = kPendRows.
+constexpr uint32_t kPendRows = 256;
+constexpr int kPendMaxWords = 4;
+constexpr size_t kPendLsn = 4 * (size_t)kPendRows, kPendWords = kPendLsn + 8 * (size_t)kPendRows,
+                 kPendTtid = kPendWords + 8 * (size_t)kPendMaxWords * kPendRows,
+                 kPendTlsn = kPendTtid + 4 * (size_t)kPendRows, kPendBytes = kPendTlsn + 8 * (size_t)kPendRows;
+struct PendView {
+    const uint8_t *base;  // device address of the buffer (nullptr: none)
+    uint32_t n, nt;       // rows, table entries
+};
 hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const DeltaView &d2,
-                               const ProbeView &p,
+                               const PendView &pd, const ProbeView &p,
                                uint8_t *verdict, uint32_t *blocks_done, uint32_t *done,
                                uint32_t seq, hipStream_t s);
 // 16-ary directory over a sorted u64 array A (hsc_narrow.hip): level 0 = A

@@ -367,16 +367,179 @@ __global__ __launch_bounds__(kProbeThreads) void k_probe_narrow(NarrowView nv, P
 // last block's count.
 constexpr int kSmallThreads = 256;
 
+// ---- the appended rows: delta runs and the pending tail --------------------
+// Keys as full composites (gid, W words) held in registers, W <= kPendMaxWords.
+
+// row i of d below the key: (gid, words) < (g, k), or <= with !strict
+template <int W>
+__device__ __forceinline__ bool row_below(const DeltaView &d, uint32_t i, uint32_t g,
+                                          const uint64_t (&k)[W], bool strict)
+{
+    const uint32_t rg = d.gid[i];
+    uint64_t w[W];
+#pragma unroll
+    for (int j = 0; j < W; ++j) w[j] = d.words[(size_t)j * d.stride + i];
+    if (rg != g) return rg < g;
+#pragma unroll
+    for (int j = 0; j < W; ++j)
+        if (w[j] != k[j]) return w[j] < k[j];
+    return !strict;
+}
+
+__device__ __forceinline__ bool group_any(bool x, int sub)
+{
+    return ((uint32_t)(__ballot(x) >> (16 * sub)) & 0xFFFFu) != 0;
+}
+
+// A 16-lane group (sub of the wave) asks: a row of d in [lo, hi] of group g
+// committed after snap?  Both bounds come from 16-ary searches run in
+// lockstep -- each round every lane reads one sample row, a ballot counts the
+// samples below the bound and the interval shrinks 16-fold (4 rounds for a
+// full 65536-row run, against 16 dependent steps of a binary search) -- then
+// the LSNs between them 16 units at a time: rows at the ends, the 64-row
+// maxima between.  Every lane of the wave runs the same rounds (ballots).
+template <int W>
+__device__ bool delta_range16(const DeltaView &d, bool act, uint32_t g, const uint64_t (&lo)[W],
+                              const uint64_t (&hi)[W], uint64_t snap, int l16, int sub)
+{
+    uint32_t a0 = 0, al = act ? d.n : 0, b0 = 0, bl = al;  // count in [x0, x0 + xl]
+    while (__any((al | bl) != 0)) {
+        const uint32_t as = (al + 15) >> 4, bs = (bl + 15) >> 4;
+        const uint32_t sa = (uint32_t)(l16 + 1) * as, sb = (uint32_t)(l16 + 1) * bs;
+        const bool ab = al && sa <= al && row_below<W>(d, a0 + sa - 1, g, lo, true);
+        const bool bb = bl && sb <= bl && row_below<W>(d, b0 + sb - 1, g, hi, false);
+        const uint32_t ma = __popc((uint32_t)(__ballot(ab) >> (16 * sub)) & 0xFFFFu);
+        const uint32_t mb = __popc((uint32_t)(__ballot(bb) >> (16 * sub)) & 0xFFFFu);
+        if (al) {
+            const uint32_t n0 = a0 + ma * as;
+            al = min(as - 1, a0 + al - n0), a0 = n0;
+        }
+        if (bl) {
+            const uint32_t n0 = b0 + mb * bs;
+            bl = min(bs - 1, b0 + bl - n0), b0 = n0;
+        }
+    }
+    // rows [pa, pb): h head rows, nb whole 64-row blocks, t tail rows
+    const uint32_t pa = a0, pb = b0;
+    uint32_t h = 0, nb = 0, t = 0, hend = pa, ts = pb;
+    if (pa < pb) {
+        hend = min(pb, (pa + 63) & ~63u);
+        const uint32_t bend = pb & ~63u;
+        nb = hend < bend ? (bend - hend) >> 6 : 0;
+        ts = max(hend, bend);
+        h = hend - pa, t = pb - ts;
+    }
+    const uint32_t U = h + nb + t;
+    bool found = false;
+    for (uint32_t k = 0; __any(k < U && !found); k += 16) {
+        const uint32_t u = k + l16;
+        bool hit = false;
+        if (u < U && !found) {
+            const uint64_t v = u < h        ? d.lsn[pa + u]
+                               : u < h + nb ? d.bmax[(hend >> 6) + (u - h)]
+                                            : d.lsn[ts + (u - h - nb)];
+            hit = v > snap;
+        }
+        found |= group_any(hit, sub);
+    }
+    return found;
+}
+
+// the pending tail staged in LDS by every block of the second half
+struct PendLds {
+    uint32_t gid[kPendRows];
+    uint64_t lsn[kPendRows];
+    uint64_t words[kPendMaxWords][kPendRows];
+    uint32_t ttid[kPendRows];
+    uint64_t tlsn[kPendRows];
+};
+
+template <int W>
+__device__ __forceinline__ bool pend_range16(const PendLds &s, uint32_t n, bool act, uint32_t g,
+                                             const uint64_t (&lo)[W], const uint64_t (&hi)[W],
+                                             uint64_t snap, int l16, int sub)
+{
+    bool hit = false;
+    for (uint32_t r = l16; act && r < n; r += 16) {
+        if (s.gid[r] != g || s.lsn[r] <= snap) continue;
+        int cl = 0, ch = 0;  // sign of row - lo, row - hi (first differing word)
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            const uint64_t w = s.words[j][r];
+            if (!cl && w != lo[j]) cl = w < lo[j] ? -1 : 1;
+            if (!ch && w != hi[j]) ch = w < hi[j] ? -1 : 1;
+        }
+        hit |= cl >= 0 && ch <= 0;
+    }
+    return group_any(hit, sub);
+}
+
+// The second half of k_small_narrow with W <= kPendMaxWords: a 16-lane group
+// per range over the live run, a frozen one and the pending tail; a thread per
+// table lock over the pending table maxima.
+template <int W>
+__device__ void small_appended16(const DeltaView &d, const DeltaView &d2, const PendView &pd,
+                                 const ProbeView &p, uint8_t *verdict, uint32_t blk, uint32_t nblk)
+{
+    __shared__ PendLds s;
+    if (pd.n || pd.nt) {
+        const uint8_t *b = pd.base;
+        for (uint32_t r = threadIdx.x; r < pd.n; r += kSmallThreads) {
+            s.gid[r] = ((const uint32_t *)b)[r];
+            s.lsn[r] = ((const uint64_t *)(b + kPendLsn))[r];
+#pragma unroll
+            for (int j = 0; j < W; ++j) s.words[j][r] = ((const uint64_t *)(b + kPendWords))[j * kPendRows + r];
+        }
+        for (uint32_t r = threadIdx.x; r < pd.nt; r += kSmallThreads) {
+            s.ttid[r] = ((const uint32_t *)(b + kPendTtid))[r];
+            s.tlsn[r] = ((const uint64_t *)(b + kPendTlsn))[r];
+        }
+        __syncthreads();
+    }
+    const int lane = threadIdx.x & 63, sub = lane >> 4, l16 = lane & 15;
+    const uint32_t wave = blk * (kSmallThreads / 64) + (threadIdx.x >> 6);
+    const uint32_t nwaves = nblk * (kSmallThreads / 64);
+    for (uint32_t base = 4 * wave; base < p.n; base += 4 * nwaves) {
+        const uint32_t q = base + sub;
+        const bool act = q < p.n;
+        uint32_t g = 0;
+        uint64_t lo[W], hi[W], snap = 0;
+#pragma unroll
+        for (int j = 0; j < W; ++j) lo[j] = hi[j] = 0;
+        if (act) {
+            g = p.gid[q];
+            snap = p.snap[q];
+#pragma unroll
+            for (int j = 0; j < W; ++j) lo[j] = p.lo[(size_t)j * p.n + q], hi[j] = p.hi[(size_t)j * p.n + q];
+        }
+        bool hit = false;
+        if (d.n) hit |= delta_range16<W>(d, act, g, lo, hi, snap, l16, sub);
+        if (d2.n) hit |= delta_range16<W>(d2, act && !hit, g, lo, hi, snap, l16, sub);
+        if (pd.n) hit |= pend_range16<W>(s, pd.n, act && !hit, g, lo, hi, snap, l16, sub);
+        if (act && hit && l16 == 0) mark_verdict<true>(verdict + p.txn[q]);
+    }
+    for (uint32_t q = blk * kSmallThreads + threadIdx.x; pd.nt && q < p.n_lock; q += nblk * kSmallThreads) {
+        const uint32_t t = p.lock_table[q];
+        const uint64_t ls = p.lock_snap[q];
+        bool hit = false;
+        for (uint32_t e = 0; e < pd.nt && !hit; ++e) hit = s.ttid[e] == t && s.tlsn[e] > ls;
+        if (hit) mark_verdict<true>(verdict + p.lock_txn[q]);
+    }
+}
+
+// WD = 0: keys wider than kPendMaxWords (no pending tail), a thread per range
+// and binary searches; WD = 1..4: small_appended16<WD>.
+template <int WD>
 __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, DeltaView d,
-                                                                DeltaView d2,
+                                                                DeltaView d2, PendView pd,
                                                                 ProbeView p, uint8_t *verdict,
                                                                 uint32_t *blocks_done,
                                                                 uint32_t *done, uint32_t seq)
 {
-    // with appended rows pending, the second half of the grid searches the
-    // delta runs while the first half searches the window (both dependent
+    // with appended rows not in the window, the second half of the grid
+    // searches them while the first half searches the window (both dependent
     // load chains run side by side instead of one after the other)
-    const bool split = d.n || d2.n;
+    const bool split = d.n || d2.n || pd.n || pd.nt;
     const uint32_t half = split ? gridDim.x / 2 : gridDim.x;
     if (blockIdx.x < half) {
         const uint32_t groups = half * (kSmallThreads / 16);
@@ -384,6 +547,8 @@ __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, D
         narrow_probe_ranges<true>(nv, p, verdict, nullptr, 0, nv.levels, wave0, groups * kNP);
         const uint32_t tid = blockIdx.x * kSmallThreads + threadIdx.x, nth = half * kSmallThreads;
         narrow_probe_locks<true>(nv, p, verdict, tid, nth);
+    } else if constexpr (WD > 0) {
+        small_appended16<WD>(d, d2, pd, p, verdict, blockIdx.x - half, gridDim.x - half);
     } else {  // the live run and a frozen one (background fold)
         const uint32_t tid = (blockIdx.x - half) * kSmallThreads + threadIdx.x;
         const uint32_t nth = (gridDim.x - half) * kSmallThreads;
@@ -404,7 +569,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, D
 }
 
 hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const DeltaView &d2,
-                               const ProbeView &p,
+                               const PendView &pd, const ProbeView &p,
                                uint8_t *verdict, uint32_t *blocks_done, uint32_t *done,
                                uint32_t seq, hipStream_t s)
 {
@@ -413,9 +578,19 @@ hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const D
     const size_t per_block = (kSmallThreads / 16) * kNP;
     const size_t work = std::max<size_t>({(p.n + per_block - 1) / per_block,
                                           (p.n_lock + kSmallThreads - 1) / kSmallThreads, 1});
-    const size_t blocks = std::min<size_t>(work, 256) * (d.n || d2.n ? 2 : 1);
-    k_small_narrow<<<(unsigned)blocks, kSmallThreads, 0, s>>>(nv, d, d2, p, verdict, blocks_done,
-                                                               done, seq);
+    const bool split = d.n || d2.n || pd.n || pd.nt;
+    const unsigned blocks = (unsigned)(std::min<size_t>(work, 256) * (split ? 2 : 1));
+    const int WD = split && nv.W <= kPendMaxWords ? nv.W : 0;
+    if ((pd.n || pd.nt) && (WD == 0 || !pd.base || pd.n > kPendRows || pd.nt > kPendRows))
+        return hipErrorInvalidValue;  // the host mirrors a tail only for W <= kPendMaxWords
+    if ((d.n && d.W != nv.W) || (d2.n && d2.W != nv.W)) return hipErrorInvalidValue;
+    switch (WD) {
+    case 1: k_small_narrow<1><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq); break;
+    case 2: k_small_narrow<2><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq); break;
+    case 3: k_small_narrow<3><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq); break;
+    case 4: k_small_narrow<4><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq); break;
+    default: k_small_narrow<0><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq);
+    }
     return hipGetLastError();
 }
 

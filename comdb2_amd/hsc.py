@@ -141,7 +141,7 @@ EXPORTS = [
     "hsc_ctx_create", "hsc_ctx_destroy", "hsc_set_stream", "hsc_last_error", "hsc_device_count",
     "hsc_window_ingest_log", "hsc_window_append", "hsc_window_set_end", "hsc_window_reset",
     "hsc_window_build", "hsc_register_group", "hsc_window_ingest_device", "hsc_window_words",
-    "hsc_window_keys", "hsc_window_end", "hsc_window_max_commit", "hsc_window_export", "hsc_set_fold", "hsc_fold_stats", "hsc_table_id",
+    "hsc_window_keys", "hsc_window_end", "hsc_window_max_commit", "hsc_window_export", "hsc_set_fold", "hsc_fold_stats", "hsc_append_stats", "hsc_table_id",
     "hsc_table_name", "hsc_group_info", "hsc_table_max", "hsc_merge_table_max",
     "hip_bdb_osql_serial_check", "hip_serial_check_batch", "hsc_check_readsets",
     "hsc_marshal_readsets", "hsc_probe_device", "hsc_pack_verdicts", "hsc_or_bitmaps",
@@ -201,6 +201,7 @@ def load() -> C.CDLL:
         "hsc_window_export": (C.c_long, [_p, C.c_int, _p, _p, _p, C.c_size_t]),
         "hsc_set_fold": (C.c_int, [_p, C.c_size_t, C.c_int]),
         "hsc_fold_stats": (C.c_int, [_p, _p]),
+        "hsc_append_stats": (C.c_int, [_p, _p]),
         "hsc_table_id": (C.c_int, [_p, C.c_char_p]),
         "hsc_table_name": (C.c_char_p, [_p, C.c_int]),
         "hsc_group_info": (C.c_int, [_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
@@ -612,6 +613,14 @@ class Validator:
         self._chk(self.lib.hsc_fold_stats(self.ctx, out.ctypes.data), "hsc_fold_stats")
         return {"started": int(out[0]), "swapped": int(out[1]), "inline": int(out[2]),
                 "last_fold_us": int(out[3])}
+
+    def append_stats(self) -> dict:
+        """Appends kept in the pending tail, merges of the tail into the
+        delta run, rows waiting now (hsc_append_stats)."""
+        out = np.zeros(3, np.uint64)
+        self._chk(self.lib.hsc_append_stats(self.ctx, out.ctypes.data), "hsc_append_stats")
+        return {"pending_appends": int(out[0]), "pending_merges": int(out[1]),
+                "pending_rows": int(out[2])}
 
     def export_window(self, all_versions: bool = False):
         """(gid u32[n], words u64[W, n], lsn u64[n]) of the built window in

@@ -300,6 +300,12 @@ int hsc_set_fold(hsc_ctx *ctx, size_t rows, int background);
 /* out[4]: background folds started, background folds swapped in, inline
  * merges, build time of the last background fold in microseconds. */
 int hsc_fold_stats(hsc_ctx *ctx, uint64_t out[4]);
+/* The pending tail (narrow windows whose keys fit 4 words): an append's rows
+ * are mirrored into mapped host memory that the small-batch kernel scans
+ * beside the delta runs, and merged into the live run once 256 rows wait or a
+ * batch that is not small runs.  out[3]: appends kept in the tail, merges of
+ * the tail into the run, rows waiting now. */
+int hsc_append_stats(hsc_ctx *ctx, uint64_t out[3]);
 int hsc_window_set_end(hsc_ctx *ctx, uint64_t end_lsn);
 int hsc_window_reset(hsc_ctx *ctx);
 /* Sort + dedupe + summaries on the device; implied by the check calls. */
