@@ -459,10 +459,18 @@ def api_leg(hsc, v, rs, device_verdict, args):
            np.ascontiguousarray(snaps & np.uint64(0xFFFFFFFF), np.uint32)) for _ in range(K + 1)]
     v.set_stream(0)  # the context's own stream
     rc = v.check_batch(arrs, file=fo[0][0], offset=fo[0][1])
+    b0 = v.batch_stats()
     t0 = time.perf_counter()
     for k in range(K):
         v.check_batch(arrs, file=fo[k + 1][0], offset=fo[k + 1][1])
     el = time.perf_counter() - t0
+    b1 = v.batch_stats()
+    # phase split of a call (hsc_batch_stats: wall time of each phase summed
+    # over the call's pipeline chunks; launch and wait overlap the next
+    # chunk's marshal)
+    phases = {k[:-3] + "_ms": (b1[k] - b0[k]) / K for k in b1 if k.endswith("_ns")}
+    phases["ranges_per_call"] = (b1["ranges"] - b0["ranges"]) / K
+    phases["chunks_per_call"] = (b1["marshals"] - b0["marshals"]) / K
     # the per-transaction call pattern: C threads each calling the one-set
     # entry (hsc_collector_check, bdb_osql_serial_check's signature) on their
     # share of the read sets; the collector batches whatever arrives together
@@ -489,7 +497,7 @@ def api_leg(hsc, v, rs, device_verdict, args):
     return {"entry": "hip_serial_check_batch (CurRangeArr* x n, full checks)",
             "value": T * K / el, "unit": "checks/s", "calls": K, "read_sets_per_call": T,
             "ms_per_call": el / K * 1e3, "host_threads": box_cpus()["threads"],
-            "parity_with_device_batch": ok,
+            "phases": phases, "parity_with_device_batch": ok,
             "note": "marshal + pinned upload + probe + download + rc_out, timed over whole calls",
             "concurrent_callers": conc}
 

@@ -496,7 +496,8 @@ struct hsc_ctx {
     uint32_t small_next = 0;
     DBuf small_blocks;
     bool small_blocks_zeroed = false;
-    bool no_small = false;  // HSC_NO_SMALL=1 at context creation: the staged path
+    bool no_small = false;  // hsc_set_paths(HSC_PATH_NO_SMALL): the staged path
+    unsigned paths = 0;     // hsc_set_paths flags (tests, A/B)
     uint32_t small_seq = 0;
     // small-path phase times (hsc_small_stats)
     // marshal / batch phase totals (hsc_batch_stats)

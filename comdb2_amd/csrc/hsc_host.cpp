@@ -432,7 +432,7 @@ static int build_ctiles(hsc_ctx *c)
     ct.WC = c->ct.WC;
     ct.gb = gb;
     ct.rank_base = c->commit_span[0];
-    ct.trad_m = narrow_trad_buckets(ct.ntiles);
+    ct.trad_m = narrow_trad_buckets(ct.ntiles, c->paths & HSC_PATH_TILE_DIR);
     if (ct.trad_m == 0 || ct.ntiles > (uint32_t)kHistCap || ctiles_locate_lds(ct) > 65536)
         return HSC_OK;
     hipStream_t s = c->stream;
@@ -535,10 +535,9 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, c->d_words2.ensure(cap * 8 * W));
     HIPCHK(c, c->d_lsn2.ensure(cap * 8));
     HIPCHK(c, c->d_flags.ensure(cap * 4 + 64));
-    // packed-key sort (hsc_ingest.hip) unless HSC_PACKED_SORT=0 or the key
-    // has more words than it takes
-    const bool try_packed = W <= kPackMaxWords && n_in > 0 &&
-                            (!getenv("HSC_PACKED_SORT") || atoi(getenv("HSC_PACKED_SORT")) != 0);
+    // packed-key sort (hsc_ingest.hip) unless turned off (HSC_PATH_NO_PACKED_SORT)
+    // or the key has more words than it takes
+    const bool try_packed = W <= kPackMaxWords && n_in > 0 && !(c->paths & HSC_PATH_NO_PACKED_SORT);
     size_t scratch = std::max(radix_scratch_bytes(n_in, W), scan_scratch_bytes(n_in) + 64);
     if (try_packed) {
         scratch = std::max(scratch, packed_scratch_bytes(n_in));
@@ -766,7 +765,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
                 HIPCHK(c, dir16_build(c->d_commits.as<uint64_t>(), c->ncommit, c->d_cdir, c->cdir,
                                       narrow_tiles_dir_lds(), s));
             HIPCHK(c, dir16_build(wn.sp_w, wn.ntiles, c->d_tdir, c->tdir, narrow_tiles_dir_lds(), s));
-            c->trad_m = narrow_trad_buckets(wn.ntiles);
+            c->trad_m = narrow_trad_buckets(wn.ntiles, c->paths & HSC_PATH_TILE_DIR);
             if (c->trad_m) {
                 HIPCHK(c, c->d_trad.ensure(4 * ((size_t)c->trad_m + 2)));
                 HIPCHK(c, narrow_trad_build(wn.sp_w, wn.ntiles, c->trad_m, c->d_trad.as<uint32_t>(), s));
@@ -1217,6 +1216,7 @@ static int fold_start(hsc_ctx *c)
     s->table_names = c->table_names;
     s->h_table_max = c->h_table_max;
     s->layout = c->layout;
+    s->paths = c->paths;
     s->W = c->W;
     const size_t nm = c->n_all, nf = c->fn, n_in = nm + nf;
     s->cap = window_cap(n_in);
@@ -2476,7 +2476,7 @@ static int finish_stage(hsc_ctx *c, Stage &st, int *rc_out)
 // memory and writes the verdict bytes into it, and the host polls the
 // kernel's done word -- no copies, no event (the per-call
 // latency db/toblock.c:4779-4836 sees).  Narrow windows (the direct probe's
-// key and max trees); HSC_NO_SMALL=1 turns it off.
+// key and max trees); hsc_set_paths(HSC_PATH_NO_SMALL) turns it off.
 constexpr int kSmallMaxTxns = 1024;
 constexpr size_t kSmallMaxRanges = 16384;
 
@@ -2724,7 +2724,6 @@ int hsc_ctx_create(int device, hsc_ctx **out)
     if (!c) return HSC_ENOMEM;
     c->device = device;
     c->threads = default_threads();
-    c->no_small = getenv("HSC_NO_SMALL") && atoi(getenv("HSC_NO_SMALL")) != 0;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return HSC_EDEVICE;
@@ -2920,6 +2919,22 @@ int hsc_fold_stats(hsc_ctx *c, uint64_t out[4])
     out[1] = c->folds_swapped;
     out[2] = c->folds_inline;
     out[3] = (uint64_t)(c->fold_ms * 1000.0f);
+    return HSC_OK;
+}
+
+int hsc_set_paths(hsc_ctx *c, unsigned flags)
+{
+    if (!c || (flags & ~(unsigned)HSC_PATH_ALL)) return HSC_EINVAL;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (!c->host_only && (flags & HSC_PATH_NO_SMALL) && !c->no_small && wait_small(c) != hipSuccess)
+        return fail(c, HSC_EDEVICE, "set_paths: a small batch did not finish");
+    if (((flags ^ c->paths) & (HSC_PATH_NO_PACKED_SORT | HSC_PATH_TILE_DIR)) && c->live) {
+        c->dirty = true;  // the next check rebuilds the window the new way
+        if (!c->host_staged) c->merge_pending = true;
+    }
+    c->paths = flags;
+    c->no_small = (flags & HSC_PATH_NO_SMALL) != 0;
+    if (c->no_small && (c->pend_n || c->pend_t)) return flush_appends(c);  // the tail is the small kernel's
     return HSC_OK;
 }
 
@@ -3379,7 +3394,7 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
     std::vector<uint32_t> isbig((size_t)std::max(T, 1), 0), bset, bpre(1, 0);
     uint32_t bmax = 0;
     bool ties = false;
-    if (!getenv("HSC_CO_SERIAL")) {  // test knob: every set on the per-thread path
+    if (!(c->paths & HSC_PATH_CO_SERIAL)) {  // else every set on the per-thread path
         for (int t = 0; t < T; ++t) {
             const size_t b = (size_t)rs->txn_off[t], e = (size_t)rs->txn_off[t + 1];
             if (e - b < kCoBig || bpre.back() + (e - b) > 0xFFFFFFFFull) continue;
@@ -3408,8 +3423,8 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
         HIPCHK(c, hipMemcpyAsync(d[20].p, bpre.data(), 4 * ((size_t)nbig + 1), hipMemcpyHostToDevice, s));
     }
     if (ties) HIPCHK(c, d[23].ensure(coalesce_tie_scratch_bytes(bpre.back())));
-    // HSC_CO_RUNSCAN=0: one thread per run in the merge scan (A/B, tests)
-    static const bool run_chunks = !getenv("HSC_CO_RUNSCAN") || atoi(getenv("HSC_CO_RUNSCAN")) != 0;
+    // HSC_PATH_CO_RUN_THREAD: one thread per run in the merge scan (A/B, tests)
+    const bool run_chunks = !(c->paths & HSC_PATH_CO_RUN_THREAD);
     if (nbig && run_chunks) HIPCHK(c, d[24].ensure(coalesce_run_scratch_bytes(bpre.back())));
     HIPCHK(c, launch_coalesce(v, d[18].as<uint32_t>(), d[19].as<uint32_t>(), d[20].as<uint32_t>(),
                               nbig, bpre.back(), bmax, d[21].as<uint32_t>(), d[22].as<uint32_t>(),

@@ -312,7 +312,7 @@ constexpr uint64_t kLsn32MaxSpan = 0xFFFFFFFDull;  // rows: lsn - base + 1 <= 0x
 uint32_t narrow_tiles_chunk();
 // Bucket table of the tiles' first codes (locate's tile search from LDS);
 // returns the bucket count m (0: too many tiles, use the directory).
-uint32_t narrow_trad_buckets(uint32_t ntiles);
+uint32_t narrow_trad_buckets(uint32_t ntiles, bool force_dir = false);
 hipError_t narrow_trad_build(const uint64_t *first, uint32_t ntiles, uint32_t m, uint32_t *trad,
                              hipStream_t s, int logmode = 0);
 // log-mode bucket of a code (see k_trad): exponent << sv | sv mantissa bits

@@ -927,10 +927,9 @@ __device__ __forceinline__ void locate_codes(const NarrowView &nv, const ProbeVi
 constexpr uint32_t kTradMaxTiles = 4096;   // first codes staged in LDS (32 KiB)
 constexpr uint32_t kTradMax = 4096;        // buckets (u16 in LDS: 8 KiB)
 
-uint32_t narrow_trad_buckets(uint32_t ntiles)
+uint32_t narrow_trad_buckets(uint32_t ntiles, bool force_dir)
 {
-    const bool off = getenv("HSC_TILE_DIR") != nullptr;  // tests: force the directory
-    if (off || ntiles == 0 || ntiles > kTradMaxTiles) return 0;
+    if (force_dir || ntiles == 0 || ntiles > kTradMaxTiles) return 0;  // force_dir: tests
     uint32_t m = 16;
     while (m < 2 * ntiles && m < kTradMax) m *= 2;
     return m;

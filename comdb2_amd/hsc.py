@@ -141,7 +141,7 @@ EXPORTS = [
     "hsc_ctx_create", "hsc_ctx_destroy", "hsc_set_stream", "hsc_last_error", "hsc_device_count",
     "hsc_window_ingest_log", "hsc_window_append", "hsc_window_set_end", "hsc_window_reset",
     "hsc_window_build", "hsc_register_group", "hsc_window_ingest_device", "hsc_window_words",
-    "hsc_window_keys", "hsc_window_end", "hsc_window_max_commit", "hsc_window_export", "hsc_set_fold", "hsc_fold_stats", "hsc_append_stats", "hsc_table_id",
+    "hsc_window_keys", "hsc_window_end", "hsc_window_max_commit", "hsc_window_export", "hsc_set_fold", "hsc_fold_stats", "hsc_append_stats", "hsc_set_paths", "hsc_table_id",
     "hsc_table_name", "hsc_group_info", "hsc_table_max", "hsc_merge_table_max",
     "hip_bdb_osql_serial_check", "hip_serial_check_batch", "hsc_check_readsets",
     "hsc_marshal_readsets", "hsc_probe_device", "hsc_pack_verdicts", "hsc_or_bitmaps",
@@ -165,6 +165,9 @@ MULTI_ID_BYTES = 2 * 128  # hsc_multi_unique_ids: one RCCL id per lane
 
 (LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES,
  LAYOUT_NARROW_CODES, LAYOUT_COMPACT, LAYOUT_COMPACT_WIDE) = 0, 1, 2, 3, 4, 5, 6, 7
+# hsc_set_paths flags (include/hip_serial.h)
+(PATH_NO_SMALL, PATH_NO_PACKED_SORT, PATH_TILE_DIR, PATH_CO_SERIAL,
+ PATH_CO_RUN_THREAD) = 1, 2, 4, 8, 16
 
 _lib: Optional[C.CDLL] = None
 
@@ -202,6 +205,7 @@ def load() -> C.CDLL:
         "hsc_set_fold": (C.c_int, [_p, C.c_size_t, C.c_int]),
         "hsc_fold_stats": (C.c_int, [_p, _p]),
         "hsc_append_stats": (C.c_int, [_p, _p]),
+        "hsc_set_paths": (C.c_int, [_p, C.c_uint]),
         "hsc_table_id": (C.c_int, [_p, C.c_char_p]),
         "hsc_table_name": (C.c_char_p, [_p, C.c_int]),
         "hsc_group_info": (C.c_int, [_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
@@ -613,6 +617,11 @@ class Validator:
         self._chk(self.lib.hsc_fold_stats(self.ctx, out.ctypes.data), "hsc_fold_stats")
         return {"started": int(out[0]), "swapped": int(out[1]), "inline": int(out[2]),
                 "last_fold_us": int(out[3])}
+
+    def set_paths(self, flags: int) -> None:
+        """Restrict the context's paths (PATH_* flags; 0 = automatic):
+        hsc_set_paths, for tests and A/B runs."""
+        self._chk(self.lib.hsc_set_paths(self.ctx, int(flags)), "hsc_set_paths")
 
     def append_stats(self) -> dict:
         """Appends kept in the pending tail, merges of the tail into the

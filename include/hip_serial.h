@@ -306,6 +306,20 @@ int hsc_fold_stats(hsc_ctx *ctx, uint64_t out[4]);
  * batch that is not small runs.  out[3]: appends kept in the tail, merges of
  * the tail into the run, rows waiting now. */
 int hsc_append_stats(hsc_ctx *ctx, uint64_t out[3]);
+/* Path restrictions of one context, for tests and A/B runs (0 = every path
+ * the library picks by itself).  NO_SMALL: batches skip the small-batch
+ * kernel (and appends its pending tail); NO_PACKED_SORT: window builds use
+ * the whole-row radix sort; TILE_DIR: narrow / compact tile locates search
+ * the 16-ary directory instead of the bucket table (set before the build);
+ * CO_SERIAL: every coalesced read set takes the per-thread msort replay;
+ * CO_RUN_THREAD: one thread per run in the coalesce merge scan. */
+#define HSC_PATH_NO_SMALL 1u
+#define HSC_PATH_NO_PACKED_SORT 2u
+#define HSC_PATH_TILE_DIR 4u
+#define HSC_PATH_CO_SERIAL 8u
+#define HSC_PATH_CO_RUN_THREAD 16u
+#define HSC_PATH_ALL 31u
+int hsc_set_paths(hsc_ctx *ctx, unsigned flags);
 int hsc_window_set_end(hsc_ctx *ctx, uint64_t end_lsn);
 int hsc_window_reset(hsc_ctx *ctx);
 /* Sort + dedupe + summaries on the device; implied by the check calls. */

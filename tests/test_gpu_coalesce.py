@@ -11,6 +11,8 @@ import pytest
 sys.path.insert(0, os.path.dirname(__file__))
 from coalesce_model import as_rows, long_run_readsets, random_readsets  # noqa: E402
 
+from comdb2_amd.hsc import PATH_CO_RUN_THREAD, PATH_CO_SERIAL  # noqa: E402
+
 pytestmark = pytest.mark.gpu
 
 
@@ -39,15 +41,18 @@ def test_gpu_coalesce_large_sets(validator, oracle_mod, monkeypatch, seed, ntxn,
                                  ntables):
     """Large sets take the level-parallel sort (hsc_coalesce.hip, CoBig; with
     NULL lower keys the replay of glibc's merge tree, CoTie): equal to the
-    oracle and to the per-thread glibc-msort path (HSC_CO_SERIAL)."""
+    oracle and to the per-thread glibc-msort path (PATH_CO_SERIAL)."""
     rs = random_readsets(seed, ntxn=ntxn, max_ranges=hi, min_ranges=lo, null_lo=null_lo,
                          tables=tuple(f"t{i:02d}" for i in range(ntables)))
     want = oracle_mod.coalesce(rs)
     got = validator.coalesce(rs)
     assert list(got.txn_off) == list(want.txn_off)
     assert as_rows(got) == as_rows(want)
-    monkeypatch.setenv("HSC_CO_SERIAL", "1")
-    ser = validator.coalesce(rs)
+    validator.set_paths(PATH_CO_SERIAL)
+    try:
+        ser = validator.coalesce(rs)
+    finally:
+        validator.set_paths(0)
     assert as_rows(ser) == as_rows(want)
 
 
@@ -62,12 +67,16 @@ def test_gpu_coalesce_empty(validator, oracle_mod):
 def test_gpu_coalesce_long_runs(validator, oracle_mod, monkeypatch, seed, ntxn, n, overlap):
     """Sets that are one long (table, index) run: the merge scan splits into
     chunks stitched per run (k_run_local / k_run_stitch / k_run_pack); equal
-    to the oracle and to one thread per run (HSC_CO_RUNSCAN=0 is read once
-    per process, so the serial path is checked through HSC_CO_SERIAL)."""
+    to the oracle, to one thread per run (PATH_CO_RUN_THREAD) and to the
+    per-thread msort path (PATH_CO_SERIAL)."""
     rs = long_run_readsets(seed, ntxn=ntxn, n=n, overlap=overlap)
     want = oracle_mod.coalesce(rs)
     got = validator.coalesce(rs)
     assert list(got.txn_off) == list(want.txn_off)
     assert as_rows(got) == as_rows(want)
-    monkeypatch.setenv("HSC_CO_SERIAL", "1")
-    assert as_rows(validator.coalesce(rs)) == as_rows(want)
+    try:
+        for flags in (PATH_CO_RUN_THREAD, PATH_CO_SERIAL):
+            validator.set_paths(flags)
+            assert as_rows(validator.coalesce(rs)) == as_rows(want), flags
+    finally:
+        validator.set_paths(0)

@@ -7,12 +7,11 @@ unsorted LSNs, block-boundary row counts and a window whose varying bits
 plus row index do not fit 64 bits (the packed path declines it); the packed
 sort runs with its dedupe fused into the unpack and with the separate
 flag / scan / compaction dedupe."""
-import os
 
 import numpy as np
 import pytest
 
-from comdb2_amd.hsc import Validator
+from comdb2_amd.hsc import PATH_NO_PACKED_SORT, Validator
 
 pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
@@ -55,9 +54,9 @@ def _case(rng, n, W, ngroups, pattern):
 def _build(gid, words, lsn, ngroups, packed):
     # packed: the packed sort with the dedupe fused into its unpack (the
     # default when the varying bits fit), False the whole-row radix sort
-    os.environ["HSC_PACKED_SORT"] = "1" if packed else "0"
     try:
         v = Validator(0)
+        v.set_paths(0 if packed else PATH_NO_PACKED_SORT)
         W = words.shape[0]
         for g in range(ngroups):
             assert v.register_group(f"t{g}", 0, 8 * W) == g
@@ -71,7 +70,7 @@ def _build(gid, words, lsn, ngroups, packed):
         v.close()
         return out
     finally:
-        os.environ.pop("HSC_PACKED_SORT", None)
+        pass
 
 
 CASES = [

@@ -8,14 +8,13 @@ wide layout keeps every key as its big-endian words.  All four must give
 verdicts bit-identical to the oracle (oracle/serial_oracle.c, the
 bdb_osql_serial_check restatement): every case runs four times on the same
 context."""
-import os
 
 import numpy as np
 import pytest
 
 from comdb2_amd import formats as F
 from comdb2_amd.formats import LogBuilder, Range, ReadSets
-from comdb2_amd.hsc import (LAYOUT_AUTO, LAYOUT_NARROW, LAYOUT_NARROW_CODES,
+from comdb2_amd.hsc import (PATH_TILE_DIR, LAYOUT_AUTO, LAYOUT_NARROW, LAYOUT_NARROW_CODES,
                             LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES, LAYOUT_WIDE)
 from comdb2_amd.workloads import config2, config5
 
@@ -28,29 +27,25 @@ def both_layouts(v, oracle_mod, log, rs, expect_auto):
     want, _, _ = oracle_mod.check(log, rs, nthreads=8)
     got = {}
     # (layout, build knob): locate finds tiles through the LDS bucket table by
-    # default and through the 16-ary directory with HSC_TILE_DIR set (the path
+    # default and through the 16-ary directory with PATH_TILE_DIR set (the path
     # of windows with too many tiles for the table).  Rows carry lsn - oldest
     # commit + 1 when the window spans < 2^32 of log, else commit ranks
     # (test_multi_file_window_commit_ranks); the bucket table's mode (linear
     # or log) is picked per window by its fullest bucket (config 5's Zipf keys
     # take log mode)
     runs = [(LAYOUT_NARROW_DIRECT, None), (LAYOUT_NARROW_TILES, None),
-            (LAYOUT_NARROW_TILES, "HSC_TILE_DIR"), (LAYOUT_NARROW_CODES, None), (LAYOUT_WIDE, None)]
+            (LAYOUT_NARROW_TILES, PATH_TILE_DIR), (LAYOUT_NARROW_CODES, None), (LAYOUT_WIDE, None)]
     try:
         for layout, knob in runs:
-            kv = [k.partition("=") for k in knob.split("+")] if knob else []
-            for var, _, val in kv:
-                os.environ[var] = val or "1"
+            v.set_paths(knob or 0)
             v.set_layout(layout)
             v.ingest_log(log)
-            for var, _, _ in kv:
-                os.environ.pop(var, None)
             assert v.layout == (LAYOUT_WIDE if layout == LAYOUT_WIDE else expect_auto)
             got[layout] = v.check_readsets(rs)
             np.testing.assert_array_equal(got[layout] != 0, want != 0,
                                           err_msg=f"layout {layout} knob {knob}")
     finally:
-        os.environ.pop("HSC_TILE_DIR", None)
+        v.set_paths(0)
         v.set_layout(LAYOUT_AUTO)
     return want
 

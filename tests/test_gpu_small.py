@@ -1,17 +1,16 @@
 """GPU: the small-batch path of the drop-in entry (k_small_narrow: one launch
 for ranges, delta run and table locks, probe columns and verdicts in
 fine-grained host memory, completion by a polled done word) against the
-staged path (HSC_NO_SMALL=1 at context creation) and the oracle
+staged path (hsc_set_paths(PATH_NO_SMALL)) and the oracle
 (oracle/serial_oracle.c): lone calls, collector-sized batches, batches with a
 delta run pending and with table locks."""
-import os
 
 import numpy as np
 import pytest
 
 from comdb2_amd import formats as F
 from comdb2_amd.formats import Range, ReadSets
-from comdb2_amd.hsc import LAYOUT_NARROW, NativeCurRangeArrs, Validator
+from comdb2_amd.hsc import LAYOUT_NARROW, PATH_NO_SMALL, NativeCurRangeArrs, Validator
 from comdb2_amd.workloads import config2
 from test_incremental import log_slice
 
@@ -21,11 +20,8 @@ torch = pytest.importorskip("torch")
 
 @pytest.fixture(scope="module")
 def staged():
-    os.environ["HSC_NO_SMALL"] = "1"
-    try:
-        v = Validator(0)
-    finally:
-        del os.environ["HSC_NO_SMALL"]
+    v = Validator(0)
+    v.set_paths(PATH_NO_SMALL)
     yield v
     v.close()
 
