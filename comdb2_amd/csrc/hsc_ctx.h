@@ -7,12 +7,14 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdlib>
 #include <functional>
 #include <cstring>
 #include <memory>
+#include <new>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -150,6 +152,48 @@ struct TxnTable {
 };
 struct IdxSpan {
     int idx, b, e;
+    const std::vector<int> *groups;  // the (table, index)'s key groups, null: none
+};
+
+// Growable array of trivially copyable T whose growth does not initialise
+// the new elements (the marshal writes every one it keeps).
+template <class T>
+struct PodVec {
+    T *p = nullptr;
+    size_t n = 0, cap = 0;
+    PodVec() = default;
+    PodVec(const PodVec &) = delete;
+    PodVec &operator=(const PodVec &) = delete;
+    PodVec(PodVec &&o) noexcept : p(o.p), n(o.n), cap(o.cap) { o.p = nullptr, o.n = o.cap = 0; }
+    ~PodVec() { free(p); }
+    void reserve(size_t k)
+    {
+        if (k <= cap) return;
+        const size_t c = std::max(k, 2 * cap + 64);
+        T *q = (T *)realloc(p, c * sizeof(T));
+        if (!q) throw std::bad_alloc();
+        p = q, cap = c;
+    }
+    void resize(size_t k) { reserve(k), n = k; }
+    void clear() { n = 0; }
+    size_t size() const { return n; }
+    T *data() { return p; }
+    const T *data() const { return p; }
+    T &operator[](size_t i) { return p[i]; }
+    const T &operator[](size_t i) const { return p[i]; }
+    void push_back(const T &v) { reserve(n + 1), p[n++] = v; }
+    void append(const T *src, size_t k)
+    {
+        reserve(n + k);
+        if (k) memcpy(p + n, src, k * sizeof(T));
+        n += k;
+    }
+    void append_fill(size_t k, const T &v)
+    {
+        reserve(n + k);
+        for (size_t i = 0; i < k; ++i) p[n + i] = v;
+        n += k;
+    }
 };
 
 // One worker's share of a marshal (read sets [t0, t1) of the batch): probes
@@ -163,9 +207,9 @@ struct RangeRef {
     int lkeylen, rkeylen, lflag, rflag, islocked;
 };
 struct alignas(128) MarshalPart {  // one per worker: no shared cache lines
-    std::vector<uint64_t> lohi;  // [n][2W]
-    std::vector<uint64_t> snap, lock_snap;
-    std::vector<uint32_t> gid, txn, lock_table, lock_txn;
+    PodVec<uint64_t> lohi;  // [n][2W]
+    PodVec<uint64_t> snap, lock_snap;
+    PodVec<uint32_t> gid, txn, lock_table, lock_txn;
     std::vector<TxnTable> tabs;
     std::vector<IdxSpan> spans;
     std::vector<RangeRef> refs;  // the read set's ranges, read once

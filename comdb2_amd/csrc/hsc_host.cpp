@@ -1461,6 +1461,33 @@ static int ingest_log(hsc_ctx *c, const hsc_llog *log)
 // Bound normalised to the group's key length klen (padding lemma, SURVEY
 // §8(a) A0): lower = lkey[0..min) ++ 0x00.., upper = rkey[0..min) ++ 0xFF..;
 // open bounds become 0x00^klen / 0xFF^klen.  Then zero padded to W words.
+// The first nk (0..8) bytes at p as the high bytes of a big-endian word
+// (reads exactly nk bytes: fixed-size loads, no variable-length copy).
+static inline uint64_t be_head(const uint8_t *p, int nk)
+{
+    if (nk >= 8) {
+        uint64_t x;
+        memcpy(&x, p, 8);
+        return __builtin_bswap64(x);
+    }
+    uint64_t v = 0;
+    int sh = 56;
+    if (nk & 4) {
+        uint32_t x;
+        memcpy(&x, p, 4);
+        v = (uint64_t)__builtin_bswap32(x) << 32;
+        p += 4, sh = 24;
+    }
+    if (nk & 2) {
+        uint16_t x;
+        memcpy(&x, p, 2);
+        v |= (uint64_t)__builtin_bswap16(x) << (sh - 8);
+        p += 2, sh -= 16;
+    }
+    if (nk & 1) v |= (uint64_t)*p << sh;
+    return v;
+}
+
 static inline void norm_bound(const uint8_t *key, int keylen, int flag, int klen, bool upper, int W,
                               uint64_t *out)
 {
@@ -1470,19 +1497,8 @@ static inline void norm_bound(const uint8_t *key, int keylen, int flag, int klen
     const int m = flag ? 0 : ((key && keylen > 0) ? std::min(keylen, klen) : 0);
     for (int j = 0; j < W; ++j) {
         const int lo = 8 * j;
-        uint64_t v = 0;
         const int nk = std::min(std::max(m - lo, 0), 8);
-        if (nk == 8) {
-            uint64_t x;
-            memcpy(&x, key + lo, 8);
-            v = __builtin_bswap64(x);
-        } else if (nk > 0) {
-            uint8_t b[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            memcpy(b, key + lo, (size_t)nk);
-            uint64_t x;
-            memcpy(&x, b, 8);
-            v = __builtin_bswap64(x);
-        }
+        uint64_t v = nk ? be_head(key + lo, nk) : 0;
         if (upper) {  // 0xFF over bytes [max(lo, m), min(lo + 8, klen)) of this word
             const int p0 = std::max(lo, m) - lo, p1 = std::min(lo + 8, klen) - lo;
             if (p1 > p0) {
@@ -1541,8 +1557,15 @@ static void marshal_txn(const D *c, MarshalPart &mp, uint32_t txn, uint64_t S, i
             spans[tt.s0 + j].e = k;
             continue;
         }
-        // new index of table ti: insert at tt.s0 + tt.ns (shifts later tables)
-        spans.insert(spans.begin() + tt.s0 + tt.ns, IdxSpan{r.idxnum, k, k});
+        // new index of table ti: insert at tt.s0 + tt.ns (shifts later tables);
+        // its key groups are looked up once here (one-entry cache across sets)
+        const uint64_t ik = ixkey(r.tid, r.idxnum);
+        if (ik != mp.ix_last) {
+            auto it = c->ix_groups.find(ik);
+            mp.ix_last = ik;
+            mp.ix_groups = it == c->ix_groups.end() ? nullptr : &it->second;
+        }
+        spans.insert(spans.begin() + tt.s0 + tt.ns, IdxSpan{r.idxnum, k, k, mp.ix_groups});
         tt.ns++;
         for (int q = ti + 1; q < (int)tabs.size(); ++q) tabs[q].s0++;
     }
@@ -1558,14 +1581,7 @@ static void marshal_txn(const D *c, MarshalPart &mp, uint32_t txn, uint64_t S, i
         }
         for (int j = 0; j < t.ns; ++j) {
             const IdxSpan &sp = spans[t.s0 + j];
-            const uint64_t ik = ixkey(t.tid, sp.idx);
-            if (ik != mp.ix_last) {  // one-entry cache of the (table, index) -> groups lookup
-                auto it = c->ix_groups.find(ik);
-                mp.ix_last = ik;
-                mp.ix_groups = it == c->ix_groups.end() ? nullptr : &it->second;
-            }
-            if (!mp.ix_groups) continue;
-            slots += mp.ix_groups->size() * (size_t)(sp.e - sp.b + 1);
+            if (sp.groups) slots += sp.groups->size() * (size_t)(sp.e - sp.b + 1);
         }
     }
     if (!slots) return;
@@ -1578,15 +1594,26 @@ static void marshal_txn(const D *c, MarshalPart &mp, uint32_t txn, uint64_t S, i
         if (t.islocked) continue;
         for (int j = 0; j < t.ns; ++j) {
             const IdxSpan &sp = spans[t.s0 + j];
-            auto it = c->ix_groups.find(ixkey(t.tid, sp.idx));
-            if (it == c->ix_groups.end()) continue;
-            for (int g : it->second) {
+            if (!sp.groups) continue;
+            for (int g : *sp.groups) {
                 const int klen = c->groups[g].klen;
+                // key bytes per word of a bound that holds the whole key length
+                // (a bound key at least klen long: the common case, no padding)
+                int nkw[kMaxWords];
+                for (int q = 0; q < W; ++q) nkw[q] = std::min(std::max(klen - 8 * q, 0), 8);
                 for (int k = sp.b; k <= sp.e; ++k) {  // span quirk: every array slot
                     const RangeRef &r = refs[k];
                     uint64_t *w2 = lohi + n * 2 * (size_t)W;
-                    norm_bound(r.lkey, r.lkeylen, r.lflag, klen, false, W, w2);
-                    norm_bound(r.rkey, r.rkeylen, r.rflag, klen, true, W, w2 + W);
+                    if (!r.lflag && r.lkey && r.lkeylen >= klen) {
+                        for (int q = 0; q < W; ++q) w2[q] = nkw[q] ? be_head(r.lkey + 8 * q, nkw[q]) : 0;
+                    } else {
+                        norm_bound(r.lkey, r.lkeylen, r.lflag, klen, false, W, w2);
+                    }
+                    if (!r.rflag && r.rkey && r.rkeylen >= klen) {
+                        for (int q = 0; q < W; ++q) w2[W + q] = nkw[q] ? be_head(r.rkey + 8 * q, nkw[q]) : 0;
+                    } else {
+                        norm_bound(r.rkey, r.rkeylen, r.rflag, klen, true, W, w2 + W);
+                    }
                     int cmp = 0;
                     for (int q = 0; q < W && !cmp; ++q)
                         if (w2[q] != w2[W + q]) cmp = w2[q] < w2[W + q] ? -1 : 1;
@@ -1615,7 +1642,11 @@ struct TableLookupT {
     int operator()(const char *name)
     {
         if (!name) return -1;
-        if (last && strcmp(name, last) == 0) return last_tid;
+        if (last) {  // names are short: an inline compare, no strcmp call
+            const char *a = name, *b = last;
+            while (*a && *a == *b) ++a, ++b;
+            if (*a == *b) return last_tid;
+        }
         auto it = c->table_ids.find(name);
         last = name;
         last_tid = it == c->table_ids.end() ? -1 : it->second;
@@ -1667,13 +1698,13 @@ struct FlatSrc {
 static void append_pre(const PreMarshal &pm, MarshalPart &mp, uint32_t txn)
 {
     const MarshalPart &q = pm.mp;
-    mp.lohi.insert(mp.lohi.end(), q.lohi.begin(), q.lohi.end());
-    mp.gid.insert(mp.gid.end(), q.gid.begin(), q.gid.end());
-    mp.snap.insert(mp.snap.end(), q.snap.begin(), q.snap.end());
-    mp.txn.insert(mp.txn.end(), q.txn.size(), txn);
-    mp.lock_table.insert(mp.lock_table.end(), q.lock_table.begin(), q.lock_table.end());
-    mp.lock_snap.insert(mp.lock_snap.end(), q.lock_snap.begin(), q.lock_snap.end());
-    mp.lock_txn.insert(mp.lock_txn.end(), q.lock_txn.size(), txn);
+    mp.lohi.append(q.lohi.data(), q.lohi.size());
+    mp.gid.append(q.gid.data(), q.gid.size());
+    mp.snap.append(q.snap.data(), q.snap.size());
+    mp.txn.append_fill(q.txn.size(), txn);
+    mp.lock_table.append(q.lock_table.data(), q.lock_table.size());
+    mp.lock_snap.append(q.lock_snap.data(), q.lock_snap.size());
+    mp.lock_txn.append_fill(q.lock_txn.size(), txn);
 }
 
 // ... or CurRangeArr pointers (the drop-in entry; db/comdb2.h:1105-1124)
