@@ -5,36 +5,40 @@
 // 4779-4836 -> bdb/serializable.c:571), so the calls arrive one read set at a
 // time from many threads at once.  One device pass costs about the same for
 // 1 read set as for a few thousand, so the collector turns those calls into
-// batches, group-commit style: every caller queues its request; the first
-// caller that finds no leader elected becomes the leader, takes everything
-// queued (up to max_batch, after an optional gather window of max_wait_us),
-// runs it as one hip_serial_check_batch and hands each caller its verdict.
-// Requests that arrive while a batch runs form the next batch, led by one of
-// their own callers -- there is no collector thread, and a lone caller pays
-// one ordinary single-set check.
+// batches, group-commit style: every caller pushes its request; a caller that
+// finds no leader becomes the leader, takes every pushed request (after an
+// optional gather window of max_wait_us), runs them as hip_serial_check_batch
+// passes of at most max_batch and hands each caller its verdict.  Requests
+// that arrive while a batch runs form the next batch, led by one of their own
+// callers -- there is no collector thread, and a lone caller pays one
+// ordinary single-set check.
 //
 // Each request keeps bdb_osql_serial_check's contract: ranges == NULL -> 0
 // (no queueing), regop_only requests get the commit-after-snapshot verdict,
 // full requests get *file,*offset := end LSN, errors count as 1.
 //
-// Up to max_inflight batches run at once: hip_serial_check_batch releases the
-// context lock while a small batch's kernel runs, so the next leader marshals
-// and launches its batch meanwhile (the kernels queue on the context's
-// stream).  Callers sleep on the futex word of their batch (a request takes
-// the id of the batch open when it queues); a finished batch sets its
-// callers' done bits after dropping the collector lock (the set is the last
-// touch of a request: its caller may return right after), then wakes the
-// whole batch with one futex call, and the woken callers return without
-// taking the collector lock.
+// No lock on the request path.  The pending requests and the leader flag
+// share one atomic word (a Treiber stack of requests, bit 0 = a leader is
+// gathering): a push that finds the bit clear sets it in the same CAS and
+// makes its caller the leader, and the leader takes the whole stack and
+// clears the bit with one exchange -- so no request is ever left without a
+// leader, and no election, queue lock or wake-up is needed to hand the role
+// on.  Up to max_inflight batches run at once (hip_serial_check_batch
+// releases the context lock while a small batch's kernel runs, so the next
+// leader marshals and launches meanwhile); a leader that finds the device
+// full sleeps on the gate word until a batch ends, gathering meanwhile.
+// Callers sleep on their own request word; the leader stores each verdict
+// and wakes that one caller (its store is the last touch of the request: the
+// caller may return right after; a wake of a stale stack address is at worst
+// spurious for its thread, whose waits all re-check).
 //
-// The next leader is designated, not raced for: when a leader takes its
-// batch (or a batch ends with requests queued and none elected), the oldest
-// queued request is marked to lead and only waiters whose wake bit matches
-// its (FUTEX_WAKE_BITSET, one of 32 bits per request) are woken -- waking the
-// whole queue to elect one of them made every election a thundering herd of
-// lock acquisitions, which on a CPU-quota'd host (256 caller threads, 16 CPUs
-// of quota) burnt the quota and stalled every thread for the rest of the
-// period (p99 77 ms in r03).
+// r03's collector queued under a mutex and elected leaders by waking
+// waiters: with 256 caller threads on a host whose cgroup grants 16 CPUs but
+// lets threads run on all 256, the mutex handoffs (a futex wake per queued
+// call, serialised) and elections took 120 µs of kernel time per call, the
+// quota ran out early in every 100 ms period and every thread stalled for the
+// rest of it (p99 77 ms, `scripts/collector_diag.py`: 8 of 8 periods
+// throttled, 12 s of system time for 100k calls).
 #include "../../include/hip_serial.h"
 #include "hsc_internal.h"
 
@@ -46,28 +50,29 @@
 #include <atomic>
 #include <chrono>
 #include <climits>
-#include <condition_variable>
 #include <cstdlib>
-#include <deque>
 #include <memory>
-#include <mutex>
 #include <thread>
 #include <vector>
 
 namespace {
 
-constexpr uint32_t kDone = 1u;  // Req::word: the verdict is ready
-constexpr uint32_t kChans = 16;  // batch wait words (more than batches alive at once: <= 4 + 1)
+constexpr uint32_t kDone = 1u;       // Req::word: the verdict is ready
+constexpr uintptr_t kLead = 1u;      // hsc_collector::state: a leader is gathering
 
-// wait on w while it holds `seen`, for a wake whose bitset meets `bits`
-void futex_wait(std::atomic<uint32_t> *w, uint32_t seen, uint32_t bits = FUTEX_BITSET_MATCH_ANY)
+void futex_wait(std::atomic<uint32_t> *w, uint32_t seen)
 {
-    syscall(SYS_futex, (uint32_t *)w, FUTEX_WAIT_BITSET_PRIVATE, seen, nullptr, nullptr, bits);
+    syscall(SYS_futex, (uint32_t *)w, FUTEX_WAIT_PRIVATE, seen, nullptr, nullptr, 0);
 }
 
-void futex_wake(std::atomic<uint32_t> *w, uint32_t bits = FUTEX_BITSET_MATCH_ANY)
+void futex_wake(std::atomic<uint32_t> *w, int n)
 {
-    syscall(SYS_futex, (uint32_t *)w, FUTEX_WAKE_BITSET_PRIVATE, INT_MAX, nullptr, nullptr, bits);
+    syscall(SYS_futex, (uint32_t *)w, FUTEX_WAKE_PRIVATE, n, nullptr, nullptr, 0);
+}
+
+uint64_t ns_between(std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b)
+{
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
 }
 
 }  // namespace
@@ -76,65 +81,34 @@ struct hsc_collector {
     hsc_ctx *ctx = nullptr;
     int max_batch = 0;
     int max_wait_us = 0;
-    int max_inflight = 2;
+    std::atomic<int> max_inflight{2};
     bool premarshal = true;  // callers marshal their own read set before queueing
-    std::mutex m;
-    struct Req {
+    struct alignas(64) Req {
         void *ranges;
         unsigned int *file, *offset;
         int regop_only;
         int rc;
         hsc::PreMarshal *pm;  // the caller's marshalled rows, or null
-        bool queued;    // in q (under m): not yet taken into a batch
-        bool lead;      // (under m) designated to lead the next batch
-        uint32_t bit;   // its futex wake bit (leader designation wakes only that bit)
-        uint32_t chan;  // the batch id open when it queued (its wait word: chan % kChans)
+        Req *next;            // the stack below it
         std::atomic<uint32_t> word{0};
     };
-    std::deque<Req *> q;
-    bool elected = false;  // a leader is waiting to take the next batch
-    int running = 0;       // batches on the device
-    uint32_t open_id = 0;  // the batch queued requests will join
-    uint32_t next_bit = 0;  // round-robin wake bits
-    std::atomic<uint32_t> chan[kChans];  // per-batch wait words (bumped at each wake)
-    std::condition_variable run_cv;     // a batch finished (the elected leader waits)
-    std::condition_variable arrive_cv;  // a request queued (a gathering leader waits)
-    std::atomic<int> inside{0};         // callers inside hsc_collector_check (last touch: the decrement)
-    hsc_collector_stats st{};           // (under m, but handout_ns:)
-    std::atomic<uint64_t> st_handout_ns{0};
-    hsc_collector()
-    {
-        for (auto &c : chan) c.store(0, std::memory_order_relaxed);
-    }
+    // pending requests (a stack of Req*, aligned) | kLead
+    alignas(64) std::atomic<uintptr_t> state{0};
+    alignas(64) std::atomic<int> running{0};     // batches on the device
+    std::atomic<uint32_t> gate{0};               // bumped when a batch ends
+    std::atomic<int> gate_waiting{0};            // a leader sleeps on gate
+    alignas(64) std::atomic<int> inside{0};      // callers inside hsc_collector_check (last touch: the decrement)
+    std::atomic<uint64_t> st_calls{0}, st_batches{0}, st_max_batch{0}, st_busy_ns{0}, st_gate_ns{0},
+        st_handout_ns{0};
 };
 
 namespace {
 
-// wake the callers sleeping on batch word `id` (bits: only those whose wake
-// bit is among them) to re-check
-void wake(hsc_collector *k, uint32_t id, uint32_t bits = FUTEX_BITSET_MATCH_ANY)
-{
-    std::atomic<uint32_t> &w = k->chan[id % kChans];
-    w.fetch_add(1, std::memory_order_acq_rel);
-    futex_wake(&w, bits);
-}
-
-// (under m) the oldest queued request leads the next batch: mark it and wake
-// the waiters of its word that share its bit.  Returns the (word, bit) to
-// wake once the lock is dropped, or bit 0 when there is nothing to do.
-std::pair<uint32_t, uint32_t> designate(hsc_collector *k)
-{
-    if (k->elected || k->q.empty()) return {0, 0};
-    hsc_collector::Req *q = k->q.front();
-    q->lead = true;
-    k->elected = true;
-    return {q->chan, q->bit};
-}
+using Req = hsc_collector::Req;
 
 // one device pass over a group of requests that share regop_only
-void run_group(hsc_collector *k, std::vector<hsc_collector::Req *> &g, int regop_only)
+void run_group(hsc_collector *k, Req *const *g, int n, int regop_only)
 {
-    const int n = (int)g.size();
     if (!n) return;
     std::vector<void *> ranges(n);
     std::vector<hsc::PreMarshal *> pm(n);
@@ -157,6 +131,65 @@ void run_group(hsc_collector *k, std::vector<hsc_collector::Req *> &g, int regop
     }
 }
 
+void max_into(std::atomic<uint64_t> &a, uint64_t v)
+{
+    uint64_t cur = a.load(std::memory_order_relaxed);
+    while (v > cur && !a.compare_exchange_weak(cur, v, std::memory_order_relaxed)) {
+    }
+}
+
+// The leader (holding kLead): wait for room on the device, take every
+// pending request, run them, hand out the verdicts.  `me` is the leader's own
+// request (in the stack it takes: it pushed before it led).
+void lead(hsc_collector *k, Req *me)
+{
+    using clk = std::chrono::steady_clock;
+    const auto tg = clk::now();
+    for (;;) {  // the in-flight bound: requests keep piling up on the stack meanwhile
+        const uint32_t seen = k->gate.load(std::memory_order_acquire);
+        if (k->running.load(std::memory_order_acquire) < k->max_inflight.load(std::memory_order_relaxed))
+            break;
+        k->gate_waiting.store(1, std::memory_order_seq_cst);
+        if (k->running.load(std::memory_order_seq_cst) >= k->max_inflight.load(std::memory_order_relaxed))
+            futex_wait(&k->gate, seen);
+        k->gate_waiting.store(0, std::memory_order_relaxed);
+    }
+    if (k->max_wait_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(k->max_wait_us));
+    k->running.fetch_add(1, std::memory_order_acq_rel);
+    // take the stack and give up the lead in one exchange: the next push
+    // becomes the next leader
+    const uintptr_t taken = k->state.exchange(0, std::memory_order_acq_rel);
+    std::vector<Req *> all;
+    for (Req *q = (Req *)(taken & ~kLead); q; q = q->next) all.push_back(q);
+    std::reverse(all.begin(), all.end());  // arrival order
+    const auto t0 = clk::now();
+    k->st_gate_ns.fetch_add(ns_between(tg, t0), std::memory_order_relaxed);
+    // regop_only and full requests run as separate passes, max_batch each
+    std::stable_partition(all.begin(), all.end(), [](const Req *q) { return q->regop_only != 0; });
+    const int nreg = (int)std::count_if(all.begin(), all.end(), [](const Req *q) { return q->regop_only != 0; });
+    const int n = (int)all.size();
+    for (int a = 0; a < n;) {
+        const int end_grp = a < nreg ? nreg : n;
+        const int b = std::min(end_grp, a + k->max_batch);
+        run_group(k, all.data() + a, b - a, a < nreg ? 1 : 0);
+        k->st_batches.fetch_add(1, std::memory_order_relaxed);
+        max_into(k->st_max_batch, (uint64_t)(b - a));
+        a = b;
+    }
+    const auto t1 = clk::now();
+    k->st_busy_ns.fetch_add(ns_between(t0, t1), std::memory_order_relaxed);
+    k->running.fetch_sub(1, std::memory_order_seq_cst);
+    k->gate.fetch_add(1, std::memory_order_seq_cst);
+    if (k->gate_waiting.load(std::memory_order_seq_cst)) futex_wake(&k->gate, 1);
+    // hand out: each store is the last touch of its request
+    for (Req *q : all) {
+        if (q == me) continue;
+        q->word.store(kDone, std::memory_order_release);
+        futex_wake(&q->word, 1);
+    }
+    k->st_handout_ns.fetch_add(ns_between(t1, clk::now()), std::memory_order_relaxed);
+}
+
 }  // namespace
 
 extern "C" {
@@ -176,9 +209,9 @@ int hsc_collector_create(hsc_ctx *ctx, int max_batch, int max_wait_us, hsc_colle
 int hsc_collector_set_inflight(hsc_collector *k, int n)
 {
     if (!k || n < 1 || n > 4) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(k->m);
-    k->max_inflight = n;
-    k->run_cv.notify_all();
+    k->max_inflight.store(n, std::memory_order_relaxed);
+    k->gate.fetch_add(1, std::memory_order_seq_cst);
+    futex_wake(&k->gate, INT_MAX);
     return HSC_OK;
 }
 
@@ -189,7 +222,6 @@ void hsc_collector_destroy(hsc_collector *k)
     // anyway (a returning caller's last touch of k is its decrement)
     while (k->inside.load(std::memory_order_acquire) != 0)
         std::this_thread::sleep_for(std::chrono::microseconds(50));
-    { std::lock_guard<std::mutex> g(k->m); }  // a leader still unlocking
     delete k;
 }
 
@@ -199,13 +231,12 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
     if (!ranges) return 0;  // bdb_osql_serial_check: nothing read -> serializable
     if (!k) return 1;
     hsc_currangearr *a = (hsc_currangearr *)ranges;
-    hsc_collector::Req r;
+    Req r;
     r.ranges = ranges;
     r.file = file ? file : &a->file;
     r.offset = offset ? offset : &a->offset;
     r.regop_only = regop_only;
     r.rc = 1;
-    r.queued = true;
     r.pm = nullptr;
     // Marshal this caller's own read set now, in its own thread, against the
     // context's dictionary snapshot: the leader then copies rows instead of
@@ -217,94 +248,21 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
         hsc::premarshal(k->ctx, a, ((uint64_t)*r.file << 32) | *r.offset, tl_pm.get()))
         r.pm = tl_pm.get();
     k->inside.fetch_add(1, std::memory_order_relaxed);
-    std::unique_lock<std::mutex> lk(k->m);
-    r.chan = k->open_id;
-    r.bit = 1u << (k->next_bit++ & 31);
-    r.lead = false;
-    k->q.push_back(&r);
-    k->st.calls++;
-    if (k->max_wait_us > 0) k->arrive_cv.notify_one();
-    if (!k->elected) {  // nobody leads the next batch yet: this caller does
-        k->elected = true;
-        r.lead = true;
-    }
-    for (;;) {  // under lk
-        if (!r.queued) {
-            // in a batch: wait for the done bit without the lock (the batch's
-            // leader sets it, then bumps and wakes the batch word)
-            std::atomic<uint32_t> &w = k->chan[r.chan % kChans];
-            lk.unlock();
-            for (;;) {
-                const uint32_t seen = w.load(std::memory_order_acquire);
-                if (r.word.load(std::memory_order_acquire) & kDone) break;
-                futex_wait(&w, seen);
-            }
+    k->st_calls.fetch_add(1, std::memory_order_relaxed);
+    // push; a push onto a stack with no leader makes this caller the leader
+    uintptr_t old = k->state.load(std::memory_order_relaxed);
+    bool leader;
+    for (;;) {
+        r.next = (Req *)(old & ~kLead);
+        leader = !(old & kLead);
+        if (k->state.compare_exchange_weak(old, (uintptr_t)&r | kLead, std::memory_order_acq_rel,
+                                           std::memory_order_relaxed))
             break;
-        }
-        if (!r.lead) {  // queued: sleep until taken into a batch or designated
-            std::atomic<uint32_t> &w = k->chan[r.chan % kChans];
-            const uint32_t seen = w.load(std::memory_order_acquire);
-            lk.unlock();
-            futex_wait(&w, seen, r.bit);
-            if (r.word.load(std::memory_order_acquire) & kDone) break;  // taken and answered meanwhile
-            lk.lock();
-            continue;
-        }
-        // this caller leads the next batch
-        const auto tg = std::chrono::steady_clock::now();
-        k->run_cv.wait(lk, [k] { return k->running < k->max_inflight; });
-        k->st.gate_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(
-                             std::chrono::steady_clock::now() - tg).count();
-        if (k->max_wait_us > 0 && (int)k->q.size() < k->max_batch)
-            k->arrive_cv.wait_for(lk, std::chrono::microseconds(k->max_wait_us),
-                                  [k] { return (int)k->q.size() >= k->max_batch; });
-        const size_t take = std::min(k->q.size(), (size_t)k->max_batch);
-        std::vector<hsc_collector::Req *> full, regop;
-        std::vector<uint32_t> ids;  // batch words of the taken requests (one, or two after a max_batch cut)
-        bool mine = false;  // max_batch may leave this caller's own request queued
-        for (size_t i = 0; i < take; ++i) {
-            hsc_collector::Req *q = k->q.front();
-            k->q.pop_front();
-            q->queued = false;
-            q->lead = false;
-            mine |= q == &r;
-            if (std::find(ids.begin(), ids.end(), q->chan) == ids.end()) ids.push_back(q->chan);
-            (q->regop_only ? regop : full).push_back(q);
-        }
-        r.lead = false;
-        k->open_id++;  // later arrivals form the next batch
-        k->running++;
-        k->elected = false;
-        // requests max_batch left queued join the next batch
-        for (hsc_collector::Req *q : k->q) q->chan = k->open_id;
-        // the next batch's leader: designated now, it gathers while this one runs
-        const auto nl = designate(k);
-        lk.unlock();
-        if (nl.second) wake(k, nl.first, nl.second);
-        const auto t0 = std::chrono::steady_clock::now();
-        run_group(k, regop, 1);
-        run_group(k, full, 0);
-        const auto t1 = std::chrono::steady_clock::now();
-        lk.lock();
-        k->running--;
-        k->st.busy_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
-        k->st.batches++;
-        k->st.max_batch = std::max<uint64_t>(k->st.max_batch, take);
-        k->run_cv.notify_one();
-        const auto nl2 = designate(k);
-        lk.unlock();
-        if (nl2.second) wake(k, nl2.first, nl2.second);
-        // hand out the verdicts: each done bit is the last touch of its
-        // request, then one wake per batch word
-        for (auto *g : {&regop, &full})
-            for (hsc_collector::Req *q : *g)
-                if (q != &r) q->word.fetch_or(kDone, std::memory_order_release);
-        for (uint32_t id : ids) wake(k, id);
-        k->st_handout_ns.fetch_add(std::chrono::duration_cast<std::chrono::nanoseconds>(
-                                       std::chrono::steady_clock::now() - t1).count(),
-                                   std::memory_order_relaxed);
-        if (mine) break;
-        lk.lock();
+    }
+    if (leader) {
+        lead(k, &r);  // r was taken with the rest (it is in the stack the leader took)
+    } else {
+        while (!(r.word.load(std::memory_order_acquire) & kDone)) futex_wait(&r.word, 0);
     }
     const int rc = r.rc;
     k->inside.fetch_sub(1, std::memory_order_release);  // last touch of k
@@ -314,8 +272,11 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
 int hsc_collector_get_stats(hsc_collector *k, hsc_collector_stats *out)
 {
     if (!k || !out) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(k->m);
-    *out = k->st;
+    out->calls = k->st_calls.load(std::memory_order_relaxed);
+    out->batches = k->st_batches.load(std::memory_order_relaxed);
+    out->max_batch = k->st_max_batch.load(std::memory_order_relaxed);
+    out->busy_ns = k->st_busy_ns.load(std::memory_order_relaxed);
+    out->gate_ns = k->st_gate_ns.load(std::memory_order_relaxed);
     out->handout_ns = k->st_handout_ns.load(std::memory_order_relaxed);
     return HSC_OK;
 }

@@ -1488,6 +1488,22 @@ static inline uint64_t be_head(const uint8_t *p, int nk)
     return v;
 }
 
+// Word q of a bound key that holds the group's whole key length: its nk
+// (0..8) key bytes, big-endian.  One 8-byte load when the 8 bytes from p stay
+// inside p's page (bytes past the key are masked off, the page is mapped);
+// at a page end the exact-length form.
+__attribute__((no_sanitize("address"))) static inline uint64_t key_word(const uint8_t *p, int nk)
+{
+    if (nk <= 0) return 0;
+    if (nk >= 8 || ((uintptr_t)p & 4095) <= 4096 - 8) {
+        uint64_t x;
+        memcpy(&x, p, 8);
+        x = __builtin_bswap64(x);
+        return nk >= 8 ? x : x & ~(~0ull >> (8 * nk));
+    }
+    return be_head(p, nk);
+}
+
 static inline void norm_bound(const uint8_t *key, int keylen, int flag, int klen, bool upper, int W,
                               uint64_t *out)
 {
@@ -1601,27 +1617,39 @@ static void marshal_txn(const D *c, MarshalPart &mp, uint32_t txn, uint64_t S, i
                 // (a bound key at least klen long: the common case, no padding)
                 int nkw[kMaxWords];
                 for (int q = 0; q < W; ++q) nkw[q] = std::min(std::max(klen - 8 * q, 0), 8);
-                for (int k = sp.b; k <= sp.e; ++k) {  // span quirk: every array slot
-                    const RangeRef &r = refs[k];
-                    uint64_t *w2 = lohi + n * 2 * (size_t)W;
-                    if (!r.lflag && r.lkey && r.lkeylen >= klen) {
-                        for (int q = 0; q < W; ++q) w2[q] = nkw[q] ? be_head(r.lkey + 8 * q, nkw[q]) : 0;
-                    } else {
-                        norm_bound(r.lkey, r.lkeylen, r.lflag, klen, false, W, w2);
+                // WT: W as a compile-time constant (unrolled word loops) up to 4
+                auto fill = [&](auto wt) {
+                    constexpr int WT = decltype(wt)::value;
+                    const int Wn = WT ? WT : W;
+                    for (int k = sp.b; k <= sp.e; ++k) {  // span quirk: every array slot
+                        const RangeRef &r = refs[k];
+                        uint64_t *w2 = lohi + n * 2 * (size_t)Wn;
+                        if (!r.lflag && r.lkey && r.lkeylen >= klen) {
+                            for (int q = 0; q < Wn; ++q) w2[q] = key_word(r.lkey + 8 * q, nkw[q]);
+                        } else {
+                            norm_bound(r.lkey, r.lkeylen, r.lflag, klen, false, Wn, w2);
+                        }
+                        if (!r.rflag && r.rkey && r.rkeylen >= klen) {
+                            for (int q = 0; q < Wn; ++q) w2[Wn + q] = key_word(r.rkey + 8 * q, nkw[q]);
+                        } else {
+                            norm_bound(r.rkey, r.rkeylen, r.rflag, klen, true, Wn, w2 + Wn);
+                        }
+                        int cmp = 0;
+                        for (int q = 0; q < Wn && !cmp; ++q)
+                            if (w2[q] != w2[Wn + q]) cmp = w2[q] < w2[Wn + q] ? -1 : 1;
+                        if (cmp > 0) continue;  // empty range never matches
+                        mp.gid[n] = (uint32_t)g;
+                        mp.snap[n] = S;
+                        mp.txn[n] = txn;
+                        ++n;
                     }
-                    if (!r.rflag && r.rkey && r.rkeylen >= klen) {
-                        for (int q = 0; q < W; ++q) w2[W + q] = nkw[q] ? be_head(r.rkey + 8 * q, nkw[q]) : 0;
-                    } else {
-                        norm_bound(r.rkey, r.rkeylen, r.rflag, klen, true, W, w2 + W);
-                    }
-                    int cmp = 0;
-                    for (int q = 0; q < W && !cmp; ++q)
-                        if (w2[q] != w2[W + q]) cmp = w2[q] < w2[W + q] ? -1 : 1;
-                    if (cmp > 0) continue;  // empty range never matches
-                    mp.gid[n] = (uint32_t)g;
-                    mp.snap[n] = S;
-                    mp.txn[n] = txn;
-                    ++n;
+                };
+                switch (W) {
+                case 1: fill(std::integral_constant<int, 1>{}); break;
+                case 2: fill(std::integral_constant<int, 2>{}); break;
+                case 3: fill(std::integral_constant<int, 3>{}); break;
+                case 4: fill(std::integral_constant<int, 4>{}); break;
+                default: fill(std::integral_constant<int, 0>{});
                 }
             }
         }
@@ -1897,11 +1925,24 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
                 txn[d] = mp.txn[i];
             }
         } else {
-            for (size_t i = 0; i < k; ++i)
-                for (int j = 0; j < W; ++j) {
-                    lo[(size_t)j * n + o + i] = mp.lohi[i * 2 * W + j];
-                    hi[(size_t)j * n + o + i] = mp.lohi[i * 2 * W + W + j];
-                }
+            // AoS rows -> SoA columns, W unrolled up to 4
+            auto cols = [&](auto wt) {
+                constexpr int WT = decltype(wt)::value;
+                const int Wn = WT ? WT : W;
+                const uint64_t *src = mp.lohi.data();
+                for (size_t i = 0; i < k; ++i, src += 2 * (size_t)Wn)
+                    for (int j = 0; j < Wn; ++j) {
+                        lo[(size_t)j * n + o + i] = src[j];
+                        hi[(size_t)j * n + o + i] = src[Wn + j];
+                    }
+            };
+            switch (W) {
+            case 1: cols(std::integral_constant<int, 1>{}); break;
+            case 2: cols(std::integral_constant<int, 2>{}); break;
+            case 3: cols(std::integral_constant<int, 3>{}); break;
+            case 4: cols(std::integral_constant<int, 4>{}); break;
+            default: cols(std::integral_constant<int, 0>{});
+            }
             if (k) {
                 memcpy(gid + o, mp.gid.data(), 4 * k);
                 memcpy(sn + o, mp.snap.data(), 8 * k);
