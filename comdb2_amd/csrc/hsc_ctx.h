@@ -337,7 +337,15 @@ struct hsc_ctx {
     std::vector<GroupInfo> groups;
     std::unordered_map<uint64_t, std::vector<int>> ix_groups;       // (tid,ix) -> gids
     uint64_t dict_epoch = 1;  // bumped when a table, a group or W changes
-    std::shared_ptr<const MarshalDict> dict_snap;  // published under mu
+    // the dictionary snapshot callers premarshal against, published under mu;
+    // read without a lock (one atomic load: the shared_ptr atomics go through
+    // one global spinlock that hundreds of concurrent callers contend on).
+    // Every version stays alive until the context is destroyed (a new one is
+    // published only when a table, group or the key width changes).
+    std::atomic<const MarshalDict *> dict_cur{nullptr};
+    std::vector<std::unique_ptr<MarshalDict>> dict_all;
+    std::vector<uint8_t> gcls;   // marshal: key-length class of every group (gcls_epoch)
+    uint64_t gcls_epoch = ~0ull;
 
     // host staging of the window (host ingest paths)
     std::vector<uint32_t> h_gid;

@@ -1897,10 +1897,14 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
     // Groups of different key lengths (in words): each part's probes are laid
     // out grouped by that length (stable), so the compact bound kernel's waves
     // skip the zero words past it together.  One length: read-set order.
-    std::vector<uint8_t> gcls(c->groups.size());
+    std::vector<uint8_t> &gcls = c->gcls;  // per dictionary epoch (groups and W fixed by it)
+    if (c->gcls_epoch != c->dict_epoch || gcls.size() != c->groups.size()) {
+        gcls.resize(c->groups.size());
+        for (size_t g = 0; g < c->groups.size(); ++g) gcls[g] = (uint8_t)std::min(W, (c->groups[g].klen + 7) / 8);
+        c->gcls_epoch = c->dict_epoch;
+    }
     int ncls = 0, cls0 = -1;
-    for (size_t g = 0; g < c->groups.size(); ++g) {
-        gcls[g] = (uint8_t)std::min(W, (c->groups[g].klen + 7) / 8);
+    for (size_t g = 0; g < gcls.size(); ++g) {
         if (cls0 < 0) cls0 = gcls[g];
         ncls = std::max(ncls, (int)gcls[g] + 1);
         if (gcls[g] != cls0) cls0 = kMaxWords + 1;
@@ -3562,15 +3566,16 @@ int hsc_check_readsets(hsc_ctx *c, const hsc_readsets *rs, int *rc_out)
 // when the epoch moved).
 static void publish_dict(hsc_ctx *c)
 {
-    const std::shared_ptr<const MarshalDict> cur = std::atomic_load(&c->dict_snap);
+    const MarshalDict *cur = c->dict_cur.load(std::memory_order_acquire);
     if (cur && cur->epoch == c->dict_epoch) return;
-    auto d = std::make_shared<MarshalDict>();
+    auto d = std::make_unique<MarshalDict>();
     d->epoch = c->dict_epoch;
     d->W = c->W;
     d->table_ids = c->table_ids;
     d->groups = c->groups;
     d->ix_groups = c->ix_groups;
-    std::atomic_store(&c->dict_snap, std::shared_ptr<const MarshalDict>(std::move(d)));
+    c->dict_cur.store(d.get(), std::memory_order_release);
+    c->dict_all.push_back(std::move(d));
 }
 
 static int check_batch(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, unsigned int *file,
@@ -3592,12 +3597,12 @@ void premarshal_free(PreMarshal *pm) { delete pm; }
 // without the context lock.  false: no snapshot yet (the batch marshals it).
 bool premarshal(hsc_ctx *c, const hsc_currangearr *a, uint64_t S, PreMarshal *pm)
 {
-    const std::shared_ptr<const MarshalDict> d = std::atomic_load(&c->dict_snap);
+    const MarshalDict *d = c->dict_cur.load(std::memory_order_acquire);
     if (!d || !a || !pm) return false;
     pm->epoch = d->epoch;
     pm->mp.clear();
-    TableLookupT<MarshalDict> tl{d.get()};
-    marshal_txn(d.get(), pm->mp, 0, S, a->size, [&, a](int k) {
+    TableLookupT<MarshalDict> tl{d};
+    marshal_txn(d, pm->mp, 0, S, a->size, [&, a](int k) {
         const hsc_currange *r = a->ranges[k];
         RangeRef x;
         x.tid = tl(r->tbname);
@@ -3637,13 +3642,13 @@ static int check_batch(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, 
         return rc;
     }
     publish_dict(c);
-    std::vector<int> slot(n, -1);  // element -> txn index in the device batch
-    std::vector<hsc_currangearr *> full;
-    std::vector<PreMarshal *> fpre;
-    std::vector<uint64_t> snaps;
-    full.reserve(n);
-    snaps.reserve(n);
-    if (pre) fpre.reserve(n);
+    // per-thread scratch, reused across calls (a lone call allocates nothing)
+    static thread_local std::vector<int> slot, rcs;  // slot: element -> txn index in the device batch
+    static thread_local std::vector<hsc_currangearr *> full;
+    static thread_local std::vector<PreMarshal *> fpre;
+    static thread_local std::vector<uint64_t> snaps;
+    slot.assign(n, -1);
+    full.clear(), fpre.clear(), snaps.clear();
     for (int i = 0; i < n; ++i) {
         hsc_currangearr *a = (hsc_currangearr *)ranges[i];
         rc_out[i] = 0;
@@ -3663,7 +3668,7 @@ static int check_batch(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, 
         if (pre) fpre.push_back(pre[i]);
     }
     if (full.empty()) return HSC_OK;
-    std::vector<int> rcs(full.size(), 1);
+    rcs.assign(full.size(), 1);
     ArrSrc src{full.data(), snaps.data(), (int)full.size()};
     if (pre) src.pre = fpre.data(), src.epoch = c->dict_epoch;
     rc = check_src(c, src, rcs.data(), &lk);
