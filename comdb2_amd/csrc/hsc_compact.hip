@@ -212,7 +212,188 @@ CompactMeta meta_of(const CompactTables &t)
     return CompactMeta{t.mask, t.pat, t.mv, t.bits, t.wlen, t.W, t.ng, t.W, 6, 1};
 }
 
+// ---- compact tables of unsorted rows, sort keys, unpack (hsc_csort.hip) ----
+// rep[g] = the smallest row index of group g (rep preset to ~0): a workgroup
+// takes the minimum of its kCsRepRows rows per group in LDS, then one global
+// atomic per group it saw (one atomic per row on a few dozen group words
+// serialised the whole pass)
+constexpr int kCsRepRows = 8192;
+__global__ __launch_bounds__(256) void k_cs_rep(const uint32_t *gid, uint32_t n, int ng, uint32_t *rep)
+{
+    extern __shared__ uint32_t rl[];
+    for (int g = threadIdx.x; g < ng; g += blockDim.x) rl[g] = 0xFFFFFFFFu;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * kCsRepRows;
+    for (uint32_t r = threadIdx.x; r < (uint32_t)kCsRepRows; r += blockDim.x) {
+        const size_t i = base + r;
+        if (i >= n) break;
+        const uint32_t g = gid[i];
+        if ((uint32_t)i < rl[g]) atomicMin(&rl[g], (uint32_t)i);
+    }
+    __syncthreads();
+    for (int g = threadIdx.x; g < ng; g += blockDim.x)
+        if (rl[g] != 0xFFFFFFFFu) atomicMin(&rep[g], rl[g]);
+}
+
+// pat[g][j] = word j of group g's representative row (0 for a group without rows)
+__global__ void k_cs_pat(const uint64_t *words, size_t stride, int W, int ng, const uint32_t *rep,
+                         uint64_t *pat)
+{
+    const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (uint32_t)(ng * W)) return;
+    const uint32_t g = e / W, j = e - g * W, r = rep[g];
+    pat[e] = r != 0xFFFFFFFFu ? words[(size_t)j * stride + r] : 0;
+}
+
+// mask[g][j] |= row XOR pattern over unsorted rows: a workgroup ORs its rows
+// into LDS accumulators (one 64-bit LDS atomic per nonzero word), then one
+// global atomic per nonzero accumulator
+constexpr int kCsVaryRows = 4096;
+__global__ __launch_bounds__(256) void k_cs_vary(const uint64_t *words, size_t stride, const uint32_t *gid,
+                                                 uint32_t n, int W, int ng, const uint64_t *pat,
+                                                 uint64_t *mask)
+{
+    extern __shared__ __attribute__((aligned(16))) uint64_t cl[];  // [ng W] pattern, [ng W] acc
+    const uint32_t gw = (uint32_t)(ng * W);
+    uint64_t *pl = cl, *acc = cl + gw;
+    for (uint32_t e = threadIdx.x; e < gw; e += blockDim.x) pl[e] = pat[e], acc[e] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * kCsVaryRows;
+    for (uint32_t r = threadIdx.x; r < (uint32_t)kCsVaryRows; r += blockDim.x) {
+        const size_t i = base + r;
+        if (i >= n) break;
+        const uint32_t g = gid[i];
+        for (int j = 0; j < W; ++j) {
+            const uint64_t m = words[(size_t)j * stride + i] ^ pl[g * W + j];
+            if (m) atomicOr((unsigned long long *)&acc[g * W + j], (unsigned long long)m);
+        }
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < gw; e += blockDim.x)
+        if (acc[e]) atomicOr((unsigned long long *)&mask[e], (unsigned long long)acc[e]);
+}
+
+// sort key of every row: gid (32) || code (64 WC) || row index (32), WC + 1 words
+template <int WC>
+__global__ __launch_bounds__(256) void k_cs_keys(const uint64_t *words, size_t stride, const uint32_t *gid,
+                                                 uint32_t n, CompactMeta cm, uint64_t *keys)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t g = gid[i];
+    uint64_t c[WC];
+    code_of<WC>(cm, g, words + i, stride, 0, c);
+    uint64_t *k = keys + (size_t)i * (WC + 1);
+    k[0] = (uint64_t)g << 32 | c[0] >> 32;
+#pragma unroll
+    for (int m = 1; m < WC; ++m) k[m] = c[m - 1] << 32 | c[m] >> 32;
+    k[WC] = c[WC - 1] << 32 | i;
+}
+
+// inverse of compress (Hacker's Delight expand: the same moves, reversed)
+__device__ __forceinline__ uint64_t expand(uint64_t x, uint64_t m, const uint64_t *mv)
+{
+#pragma unroll
+    for (int i = 5; i >= 0; --i) x = (x & ~mv[i]) | ((x << (1 << i)) & mv[i]);
+    return x & m;
+}
+
+// bits [pos, pos + cnt) (MSB-first, cnt <= 64) of the WC-word number c, right-aligned
+template <int WC>
+__device__ __forceinline__ uint64_t code_bits(const uint64_t (&c)[WC], int pos, int cnt)
+{
+    if (cnt == 0) return 0;
+    const int w = pos >> 6, off = pos & 63;
+    uint64_t x = 0, nx = 0;
+#pragma unroll
+    for (int k = 0; k < WC; ++k) {
+        x = k == w ? c[k] : x;
+        nx = k == w + 1 ? c[k] : nx;
+    }
+    const uint64_t v = off ? (x << off) | (nx >> (64 - off)) : x;
+    return cnt == 64 ? v : v >> (64 - cnt);
+}
+
+// sorted keys back to rows: gid, words = pattern outside the mask | the
+// expanded code bits inside it, the LSN gathered by row index
+template <int WC>
+__global__ __launch_bounds__(256) void k_cs_unpack(const uint64_t *keys, uint32_t n, CompactMeta cm,
+                                                   const uint64_t *lsn_in, uint32_t *gid_o,
+                                                   uint64_t *words_o, uint64_t *lsn_o, size_t stride)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t *k = keys + (size_t)i * (WC + 1);
+    uint64_t kk[WC + 1];
+#pragma unroll
+    for (int m = 0; m <= WC; ++m) kk[m] = k[m];
+    const uint32_t g = (uint32_t)(kk[0] >> 32), idx = (uint32_t)kk[WC];
+    uint64_t c[WC];
+#pragma unroll
+    for (int m = 0; m < WC; ++m) c[m] = kk[m] << 32 | kk[m + 1] >> 32;
+    lsn_o[i] = lsn_in[idx];
+    gid_o[i] = g;
+    const uint64_t *mk = cm.mask + (size_t)g * cm.W, *pt = cm.pat + (size_t)g * cm.W;
+    const uint64_t *mv = cm.mv + (size_t)g * cm.W * 6;
+    int pos = 0;
+    for (int j = 0; j < cm.W; ++j) {
+        const uint64_t m = mk[j];
+        const int cnt = __popcll(m);
+        const uint64_t part = code_bits<WC>(c, pos, cnt);
+        pos += cnt;
+        words_o[(size_t)j * stride + i] = (pt[j] & ~m) | (m ? expand(part, m, mv + 6 * j) : 0);
+    }
+}
+
 }  // namespace
+
+hipError_t compact_masks_unsorted(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
+                                  int W, int ng, uint32_t *rep, uint64_t *mask, uint64_t *pat,
+                                  hipStream_t s)
+{
+    const size_t gw = (size_t)ng * W;
+    if (2 * 8 * gw > kCsVaryLds) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(rep, 0xFF, 4 * (size_t)ng, s);
+    if (e == hipSuccess) e = hipMemsetAsync(mask, 0, 8 * gw, s);
+    if (e != hipSuccess) return e;
+    if (n) k_cs_rep<<<(n + kCsRepRows - 1) / kCsRepRows, 256, 4 * (size_t)ng, s>>>(gid, n, ng, rep);
+    if (gw) k_cs_pat<<<(uint32_t)((gw + 255) / 256), 256, 0, s>>>(words, stride, W, ng, rep, pat);
+    if (n)
+        k_cs_vary<<<(n + kCsVaryRows - 1) / kCsVaryRows, 256, 2 * 8 * gw, s>>>(words, stride, gid, n, W,
+                                                                             ng, pat, mask);
+    return hipGetLastError();
+}
+
+hipError_t compact_sort_keys(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
+                             const CompactTables &t, uint64_t *keys, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    const CompactMeta cm = meta_of(t);
+    const uint32_t b = (n + 255) / 256;
+    switch (t.WC) {
+    case 1: k_cs_keys<1><<<b, 256, 0, s>>>(words, stride, gid, n, cm, keys); break;
+    case 2: k_cs_keys<2><<<b, 256, 0, s>>>(words, stride, gid, n, cm, keys); break;
+    case 3: k_cs_keys<3><<<b, 256, 0, s>>>(words, stride, gid, n, cm, keys); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t compact_unpack_sorted(const uint64_t *keys, uint32_t n, const CompactTables &t,
+                                 const uint64_t *lsn_in, uint32_t *gid_o, uint64_t *words_o,
+                                 uint64_t *lsn_o, size_t stride, hipStream_t s)
+{
+    if (n == 0) return hipSuccess;
+    const CompactMeta cm = meta_of(t);
+    const uint32_t b = (n + 255) / 256;
+    switch (t.WC) {
+    case 1: k_cs_unpack<1><<<b, 256, 0, s>>>(keys, n, cm, lsn_in, gid_o, words_o, lsn_o, stride); break;
+    case 2: k_cs_unpack<2><<<b, 256, 0, s>>>(keys, n, cm, lsn_in, gid_o, words_o, lsn_o, stride); break;
+    case 3: k_cs_unpack<3><<<b, 256, 0, s>>>(keys, n, cm, lsn_in, gid_o, words_o, lsn_o, stride); break;
+    default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
 
 // Hacker's Delight compress move masks of m (host).
 void compress_moves(uint64_t m, uint64_t mv[6])

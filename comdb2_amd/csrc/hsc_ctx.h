@@ -467,6 +467,12 @@ struct hsc_ctx {
     CompactTables ct{};
     WinView wc{};
     DBuf d_cmask, d_cpat, d_cmv, d_cbits, d_cwords, d_ctmax, d_csp_g, d_csp_w;
+    // the code sort's tables and keys (device_build: wide rows whose per-group
+    // varying bits fit 3 words)
+    DBuf d_csrep, d_csmask, d_cspat, d_csmv, d_csbits, d_cskeys[2];
+    bool code_sorted = false;  // the last build sorted by compact codes
+    std::vector<uint64_t> cs_mask;     // its varying bits per (group, word) (host copy)
+    std::vector<uint8_t> cs_has_rows;  // its groups with rows
     int ct_maxbits = 0;  // most varying bits of any group
     // compact tiles (hsc_ctiles.hip): the compact window as gid || code keys
     bool ctiles = false;

@@ -339,15 +339,24 @@ static int build_compact(hsc_ctx *c, const WinView &w)
     const size_t gw = (size_t)ng * W;
     HIPCHK(c, c->d_cmask.ensure(8 * gw));
     HIPCHK(c, c->d_cpat.ensure(8 * gw));
-    HIPCHK(c, compact_masks(w.words, w.stride, w.gid, w.n, W, ng, c->d_gstart.as<uint32_t>(),
-                            c->d_gend.as<uint32_t>(), c->d_cmask.as<uint64_t>(),
-                            c->d_cpat.as<uint64_t>(), s));
     std::vector<uint64_t> mask(gw);
     std::vector<uint32_t> gs(ng), ge(ng);
-    HIPCHK(c, hipMemcpyAsync(mask.data(), c->d_cmask.p, 8 * gw, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipMemcpyAsync(gs.data(), c->d_gstart.p, 4 * (size_t)ng, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipMemcpyAsync(ge.data(), c->d_gend.p, 4 * (size_t)ng, hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
+    if (c->code_sorted) {
+        // the code sort's tables of the same rows (its pattern rows differ,
+        // any row of a group serves): copied, not recomputed
+        HIPCHK(c, hipMemcpyAsync(c->d_cmask.p, c->d_csmask.p, 8 * gw, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->d_cpat.p, c->d_cspat.p, 8 * gw, hipMemcpyDeviceToDevice, s));
+        mask = c->cs_mask;
+        for (int g = 0; g < ng; ++g) ge[g] = c->cs_has_rows[g] ? 1 : 0;
+    } else {
+        HIPCHK(c, compact_masks(w.words, w.stride, w.gid, w.n, W, ng, c->d_gstart.as<uint32_t>(),
+                                c->d_gend.as<uint32_t>(), c->d_cmask.as<uint64_t>(),
+                                c->d_cpat.as<uint64_t>(), s));
+        HIPCHK(c, hipMemcpyAsync(mask.data(), c->d_cmask.p, 8 * gw, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(gs.data(), c->d_gstart.p, 4 * (size_t)ng, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipMemcpyAsync(ge.data(), c->d_gend.p, 4 * (size_t)ng, hipMemcpyDeviceToHost, s));
+        HIPCHK(c, hipStreamSynchronize(s));
+    }
     std::vector<uint32_t> bits(ng);
     std::vector<uint64_t> mv(gw * 6);
     int maxbits = 0;
@@ -524,6 +533,76 @@ struct BuildTrace {
     }
 };
 
+// Sort the n_in input rows (d_gid / d_words / d_lsn) by their compact codes
+// into d_gid2 / d_words2 / d_lsn2 (hsc_csort.hip), when the keys do not fit
+// the packed sort but every group's varying bits fit 3 code words.  *done =
+// false: not applicable (the caller takes the whole-row radix sort).
+static int code_sort(hsc_ctx *c, size_t n_in, bool *done)
+{
+    *done = false;
+    const int W = c->W, ng = (int)c->groups.size();
+    const size_t gw = (size_t)ng * W;
+    if (W < 2 || ng == 0 || n_in == 0 || n_in >= 0xFFFFFFFFull || 16 * gw > kCsVaryLds) return HSC_OK;
+    hipStream_t s = c->stream;
+    HIPCHK(c, c->d_csrep.ensure(4 * (size_t)ng));
+    HIPCHK(c, c->d_csmask.ensure(8 * gw));
+    HIPCHK(c, c->d_cspat.ensure(8 * gw));
+    HIPCHK(c, compact_masks_unsorted(c->d_words.as<uint64_t>(), c->cap, c->d_gid.as<uint32_t>(),
+                                     (uint32_t)n_in, W, ng, c->d_csrep.as<uint32_t>(),
+                                     c->d_csmask.as<uint64_t>(), c->d_cspat.as<uint64_t>(), s));
+    std::vector<uint64_t> mask(gw);
+    std::vector<uint32_t> rep(ng);
+    HIPCHK(c, hipMemcpyAsync(mask.data(), c->d_csmask.p, 8 * gw, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(rep.data(), c->d_csrep.p, 4 * (size_t)ng, hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+    std::vector<uint32_t> bits(2 * (size_t)ng);
+    std::vector<uint64_t> mv(gw * 6);
+    int maxbits = 0;
+    c->cs_mask = mask;  // build_compact takes these tables over
+    c->cs_has_rows.assign(ng, 0);
+    for (int g = 0; g < ng; ++g) c->cs_has_rows[g] = rep[g] != 0xFFFFFFFFu;
+    for (int g = 0; g < ng; ++g) {
+        int b = 0;
+        for (int j = 0; j < W; ++j) {
+            b += __builtin_popcountll(mask[(size_t)g * W + j]);
+            compress_moves(mask[(size_t)g * W + j], &mv[((size_t)g * W + j) * 6]);
+        }
+        bits[g] = rep[g] == 0xFFFFFFFFu ? 0xFFFFFFFFu : (uint32_t)b;
+        bits[ng + g] = (uint32_t)std::min(W, (c->groups[g].klen + 7) / 8);
+        maxbits = std::max(maxbits, b);
+    }
+    const int WC = maxbits / 64 + 1;
+    if (WC > 3) return HSC_OK;
+    HIPCHK(c, c->d_csmv.ensure(8 * gw * 6));
+    HIPCHK(c, c->d_csbits.ensure(8 * (size_t)ng));
+    HIPCHK(c, hipMemcpyAsync(c->d_csmv.p, mv.data(), 8 * gw * 6, hipMemcpyHostToDevice, s));
+    HIPCHK(c, hipMemcpyAsync(c->d_csbits.p, bits.data(), 8 * (size_t)ng, hipMemcpyHostToDevice, s));
+    CompactTables t{};
+    t.mask = c->d_csmask.as<uint64_t>();
+    t.pat = c->d_cspat.as<uint64_t>();
+    t.mv = c->d_csmv.as<uint64_t>();
+    t.bits = c->d_csbits.as<uint32_t>();
+    t.wlen = c->d_csbits.as<uint32_t>() + ng;
+    t.W = W;
+    t.WC = WC;
+    t.ng = ng;
+    const int KW = WC + 1;
+    for (auto &b : c->d_cskeys) HIPCHK(c, b.ensure(8 * (size_t)KW * n_in));
+    HIPCHK(c, compact_sort_keys(c->d_words.as<uint64_t>(), c->cap, c->d_gid.as<uint32_t>(), (uint32_t)n_in,
+                                t, c->d_cskeys[0].as<uint64_t>(), s));
+    uint64_t *sorted = nullptr;
+    HIPCHK(c, code_keys_sort(c->d_cskeys[0].as<uint64_t>(), c->d_cskeys[1].as<uint64_t>(), n_in, KW, s,
+                             &sorted));
+    HIPCHK(c, compact_unpack_sorted(sorted, (uint32_t)n_in, t, c->d_lsn.as<uint64_t>(),
+                                    c->d_gid2.as<uint32_t>(), c->d_words2.as<uint64_t>(),
+                                    c->d_lsn2.as<uint64_t>(), c->cap, s));
+    // the tables stay valid until the next build: mv / bits are host vectors
+    // uploaded above, so the stream must have read them before they go
+    HIPCHK(c, hipStreamSynchronize(s));
+    *done = true;
+    return HSC_OK;
+}
+
 static int device_build(hsc_ctx *c, size_t n_in)
 {
     BuildTrace bt(c->stream);
@@ -567,6 +646,10 @@ static int device_build(hsc_ctx *c, size_t n_in)
     bt.stamp("commits");
     PackPlan plan;
     c->packed_sort = try_packed && packed_plan(W, n_in, vary, &plan);
+    // too many varying bits for the packed sort: by compact codes if they fit
+    bool code_sorted = false;
+    if (!c->packed_sort && try_packed) HIPCHK_RC(c, code_sort(c, n_in, &code_sorted));
+    c->code_sorted = code_sorted;
     if (c->packed_sort) {
         // every version, key-sorted, into d_*2; the distinct rows straight from
         // the unpack into d_gid / d_words (in place) and a free key buffer,
@@ -583,6 +666,14 @@ static int device_build(hsc_ctx *c, size_t n_in)
         else if (dl == c->d_pk[1].p)
             std::swap(c->d_lsn, c->d_pk[1]);
         bt.stamp("sort");
+    } else if (code_sorted) {
+        // every version, key-sorted, in d_*2; the distinct rows into d_*
+        bt.stamp("sort");
+        HIPCHK(c, dedupe_rows(W, n_in, c->d_gid2.as<uint32_t>(), c->d_words2.as<uint64_t>(),
+                              c->d_lsn2.as<uint64_t>(), cap, c->d_gid.as<uint32_t>(),
+                              c->d_words.as<uint64_t>(), c->d_lsn.as<uint64_t>(), cap,
+                              c->d_flags.as<uint32_t>(), c->d_scratch.p, c->d_scratch.bytes,
+                              c->d_count.as<uint32_t>(), s));
     } else {
         bool in_alt = false;
         HIPCHK(c, radix_sort_known(W, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
@@ -2813,7 +2904,7 @@ int hsc_ctx_create(int device, hsc_ctx **out)
         if (warmed.size() < (size_t)n) warmed.resize(n, false);
         if (!warmed[device]) {
             for (auto f : {warm_kernels, warm_ingest, warm_narrow, warm_ctiles, warm_delta,
-                           warm_compact, warm_coalesce, warm_edges, warm_graph, warm_route})
+                           warm_compact, warm_csort, warm_coalesce, warm_edges, warm_graph, warm_route})
                 (void)f();
             warmed[device] = true;
         }
@@ -2858,6 +2949,9 @@ void hsc_ctx_destroy(hsc_ctx *c)
     c->small_st.release();
     for (auto &sl : c->small) sl.io.release();
     c->small_blocks.release();
+    for (DBuf *b : {&c->d_csrep, &c->d_csmask, &c->d_cspat, &c->d_csmv, &c->d_csbits, &c->d_cskeys[0],
+                    &c->d_cskeys[1], &c->d_cmask, &c->d_cpat, &c->d_cmv, &c->d_cbits, &c->d_cwords})
+        b->release();
     for (DBuf *b : {&c->d_dgid[0], &c->d_dgid[1], &c->d_dwords[0], &c->d_dwords[1], &c->d_dlsn[0],
                     &c->d_dlsn[1], &c->d_dbmax, &c->d_agid})
         b->release();
@@ -3164,6 +3258,7 @@ int hsc_window_code_words(hsc_ctx *c) { return c && c->compact ? c->ct.WC : c ? 
 int hsc_window_tile_key_words(hsc_ctx *c) { return c && c->compact && c->ctiles ? c->ctv.WG : 0; }
 
 int hsc_window_words(hsc_ctx *c) { return c ? c->W : 0; }
+int hsc_window_sort_path(hsc_ctx *c) { return !c ? 0 : c->packed_sort ? 1 : c->code_sorted ? 2 : 0; }
 size_t hsc_window_keys(hsc_ctx *c) { return c ? c->n : 0; }
 uint64_t hsc_window_end(hsc_ctx *c) { return c ? c->end_lsn : 0; }
 uint64_t hsc_window_max_commit(hsc_ctx *c) { return c ? c->max_commit : 0; }

@@ -485,6 +485,22 @@ hipError_t compact_masks(const uint64_t *words, size_t stride, const uint32_t *g
                          uint64_t *mask, uint64_t *pat, hipStream_t s);
 hipError_t compact_rows(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
                         const CompactTables &t, uint64_t *cw, hipStream_t s);
+// The code sort of wide rows (hsc_csort.hip): the compact tables of UNSORTED
+// rows (each group's pattern = its lowest-index row; ng W <= kCsVaryLds / 16
+// for the LDS accumulators), the (WC + 1)-word key of every row (gid ||
+// code || row index), the keys' sort, and the sorted keys back to rows.
+constexpr size_t kCsVaryLds = 64 * 1024;
+hipError_t compact_masks_unsorted(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
+                                  int W, int ng, uint32_t *rep, uint64_t *mask, uint64_t *pat,
+                                  hipStream_t s);
+hipError_t compact_sort_keys(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
+                             const CompactTables &t, uint64_t *keys, hipStream_t s);
+hipError_t code_keys_sort(uint64_t *keys, uint64_t *tmp, size_t n, int KW, hipStream_t s,
+                          uint64_t **sorted);
+hipError_t compact_unpack_sorted(const uint64_t *keys, uint32_t n, const CompactTables &t,
+                                 const uint64_t *lsn_in, uint32_t *gid_o, uint64_t *words_o,
+                                 uint64_t *lsn_o, size_t stride, hipStream_t s);
+hipError_t warm_csort();
 // lo/hi bounds (W words) -> code bounds (WC words, SoA [WC][n]); ranges that
 // miss their group's rows become (~0, 0)
 hipError_t compact_probes(const ProbeView &p, const CompactTables &t, uint64_t *clo, uint64_t *chi,

@@ -141,7 +141,7 @@ EXPORTS = [
     "hsc_ctx_create", "hsc_ctx_destroy", "hsc_set_stream", "hsc_last_error", "hsc_device_count",
     "hsc_window_ingest_log", "hsc_window_append", "hsc_window_set_end", "hsc_window_reset",
     "hsc_window_build", "hsc_register_group", "hsc_window_ingest_device", "hsc_window_words",
-    "hsc_window_keys", "hsc_window_end", "hsc_window_max_commit", "hsc_window_export", "hsc_set_fold", "hsc_fold_stats", "hsc_append_stats", "hsc_set_paths", "hsc_table_id",
+    "hsc_window_keys", "hsc_window_end", "hsc_window_max_commit", "hsc_window_export", "hsc_set_fold", "hsc_fold_stats", "hsc_append_stats", "hsc_set_paths", "hsc_window_sort_path", "hsc_table_id",
     "hsc_table_name", "hsc_group_info", "hsc_table_max", "hsc_merge_table_max",
     "hip_bdb_osql_serial_check", "hip_serial_check_batch", "hsc_check_readsets",
     "hsc_marshal_readsets", "hsc_probe_device", "hsc_pack_verdicts", "hsc_or_bitmaps",
@@ -206,6 +206,7 @@ def load() -> C.CDLL:
         "hsc_fold_stats": (C.c_int, [_p, _p]),
         "hsc_append_stats": (C.c_int, [_p, _p]),
         "hsc_set_paths": (C.c_int, [_p, C.c_uint]),
+        "hsc_window_sort_path": (C.c_int, [_p]),
         "hsc_table_id": (C.c_int, [_p, C.c_char_p]),
         "hsc_table_name": (C.c_char_p, [_p, C.c_int]),
         "hsc_group_info": (C.c_int, [_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
@@ -587,6 +588,11 @@ class Validator:
     def layout(self) -> int:
         """LAYOUT_NARROW, LAYOUT_COMPACT or LAYOUT_WIDE: the current window's."""
         return self.lib.hsc_window_layout(self.ctx)
+
+    @property
+    def sort_path(self) -> str:
+        """How the last build sorted its rows: "radix", "packed" or "codes"."""
+        return ("radix", "packed", "codes")[self.lib.hsc_window_sort_path(self.ctx)]
 
     @property
     def code_words(self) -> int:

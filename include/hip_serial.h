@@ -320,6 +320,9 @@ int hsc_append_stats(hsc_ctx *ctx, uint64_t out[3]);
 #define HSC_PATH_CO_RUN_THREAD 16u
 #define HSC_PATH_ALL 31u
 int hsc_set_paths(hsc_ctx *ctx, unsigned flags);
+/* How the last window build sorted its rows: 0 whole-row radix sort, 1 the
+ * packed 64-bit key sort, 2 the compact-code merge sort (wide keys). */
+int hsc_window_sort_path(hsc_ctx *ctx);
 int hsc_window_set_end(hsc_ctx *ctx, uint64_t end_lsn);
 int hsc_window_reset(hsc_ctx *ctx);
 /* Sort + dedupe + summaries on the device; implied by the check calls. */

@@ -4,9 +4,10 @@ version in stable (gid, key words) order and the newest version per key,
 read back through hsc_window_export.  Cases cover one and several words,
 several groups, varying bits scattered over the words, heavy duplication,
 unsorted LSNs, block-boundary row counts and a window whose varying bits
-plus row index do not fit 64 bits (the packed path declines it); the packed
-sort runs with its dedupe fused into the unpack and with the separate
-flag / scan / compaction dedupe."""
+plus row index do not fit 64 bits (the packed path declines it: the
+compact-code merge sort of hsc_csort.hip takes it, config-3-like keys too);
+the packed sort runs with its dedupe fused into the unpack and with the
+separate flag / scan / compaction dedupe."""
 
 import numpy as np
 import pytest
@@ -42,18 +43,30 @@ def _case(rng, n, W, ngroups, pattern):
             m = np.uint64(0x8000_0100_0040_1001 >> j)
             r = rng.integers(0, 1 << 63, n, dtype=np.uint64)
             words[j] = (base[j] & ~m) | (r & m)
-    elif pattern == "wide":  # > 64 varying bits: generic sort
+    elif pattern == "wide":  # > 64 varying bits: the code sort (or the radix sort)
         for j in range(W):
             words[j] = rng.integers(0, 1 << 63, n, dtype=np.uint64)
+    elif pattern == "c3":  # config-3-like: per-group key lengths, lumpy bytes, repeats
+        klen = rng.integers(9, min(8 * W, 32) + 1, ngroups)  # <= 160 varying bits: 3 code words
+        letters = np.array([0x41, 0x43, 0x47, 0x4B, 0x52, 0x53, 0x5A], np.uint8)
+        pool = rng.integers(0, max(2, n // 3), n)  # about 3 versions per key
+        kb = np.zeros((n, 8 * W), np.uint8)
+        for g in range(ngroups):
+            sel = gid == g
+            r = np.random.default_rng(1000 + g)
+            keys_g = letters[r.integers(0, 7, (max(2, n // 3), int(klen[g])))]
+            kb[sel, :klen[g]] = keys_g[pool[sel] % len(keys_g)]
+        words = np.ascontiguousarray(kb.view(">u8").astype(np.uint64).T)
     lsn = np.sort(rng.integers(1, 1 << 40, n, dtype=np.uint64))
     if pattern in ("dups", "scattered"):
         rng.shuffle(lsn)  # not in log order
     return gid, words, lsn
 
 
-def _build(gid, words, lsn, ngroups, packed):
+def _build(gid, words, lsn, ngroups, packed, path=None):
     # packed: the packed sort with the dedupe fused into its unpack (the
-    # default when the varying bits fit), False the whole-row radix sort
+    # default when the varying bits fit) or, for wider varying bits, the
+    # compact-code merge sort; False the whole-row radix sort
     try:
         v = Validator(0)
         v.set_paths(0 if packed else PATH_NO_PACKED_SORT)
@@ -67,6 +80,8 @@ def _build(gid, words, lsn, ngroups, packed):
         v.ingest_device(len(lsn), W, tg.data_ptr(), tw.data_ptr(), tl.data_ptr(), int(lsn.max()) + 1)
         torch.cuda.synchronize()
         out = v.export_window(True), v.export_window(False)
+        if path is not None:
+            path.append(v.sort_path)
         v.close()
         return out
     finally:
@@ -77,7 +92,7 @@ CASES = [
     (1, 1, 1, "low40"), (2, 1, 1, "dups"), (1000, 1, 1, "low40"), (8191, 1, 3, "dups"),
     (8192, 2, 1, "low40"), (8193, 1, 2, "scattered"), (100_000, 3, 5, "scattered"),
     (300_000, 1, 1, "dups"), (1 << 20, 1, 1, "low40"), (50_000, 2, 3, "wide"),
-    (70_000, 5, 2, "scattered"),
+    (70_000, 5, 2, "scattered"), (300_000, 8, 32, "c3"), (5000, 8, 3, "c3"), (1025, 4, 2, "wide"),
 ]
 
 
@@ -87,7 +102,11 @@ def test_build_rows_match_numpy(n, W, ngroups, pattern):
     gid, words, lsn = _case(rng, n, W, ngroups, pattern)
     want_all, want_u = _reference(gid, words, lsn)
     for packed in (True, False):
-        got_all, got_u = _build(gid, words, lsn, ngroups, packed)
+        path = []
+        got_all, got_u = _build(gid, words, lsn, ngroups, packed, path)
+        if pattern in ("wide", "c3") and n > 1:  # codes when the varying bits fit 3 words
+            fits = pattern == "c3" or W <= 2
+            assert path == ["codes" if packed and fits else "radix"], path
         for got, want in ((got_all, want_all), (got_u, want_u)):
             np.testing.assert_array_equal(got[0], want[0])
             np.testing.assert_array_equal(got[1], want[1])
