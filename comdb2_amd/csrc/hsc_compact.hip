@@ -273,11 +273,34 @@ __global__ __launch_bounds__(256) void k_cs_vary(const uint64_t *words, size_t s
         if (acc[e]) atomicOr((unsigned long long *)&mask[e], (unsigned long long)acc[e]);
 }
 
+// The tables of cm copied into LDS in their global layout ([ng][W] masks and
+// patterns, [ng][W][6] moves, [ng] bits) when they fit kCsTabLds; cm then
+// points at the copies (the lanes of a wave read different groups' entries,
+// gathers that L1 serves poorly).  Callers synchronize before use.
+constexpr uint32_t kCsTabLds = 48 * 1024;
+__host__ __device__ inline uint32_t cs_tab_bytes(int ng, int W) { return (uint32_t)(64 * ng * W + 4 * ng); }
+
+__device__ __forceinline__ void cs_stage_tables(CompactMeta &cm, uint64_t *lds)
+{
+    const uint32_t gw = (uint32_t)(cm.ng * cm.W);
+    uint64_t *m = lds, *p = lds + gw, *v = lds + 2 * gw;
+    uint32_t *b = (uint32_t *)(lds + 8 * gw);
+    for (uint32_t e = threadIdx.x; e < gw; e += blockDim.x) m[e] = cm.mask[e], p[e] = cm.pat[e];
+    for (uint32_t e = threadIdx.x; e < 6 * gw; e += blockDim.x) v[e] = cm.mv[e];
+    for (uint32_t e = threadIdx.x; e < (uint32_t)cm.ng; e += blockDim.x) b[e] = cm.bits[e];
+    cm.mask = m, cm.pat = p, cm.mv = v, cm.bits = b;
+}
+
 // sort key of every row: gid (32) || code (64 WC) || row index (32), WC + 1 words
 template <int WC>
 __global__ __launch_bounds__(256) void k_cs_keys(const uint64_t *words, size_t stride, const uint32_t *gid,
-                                                 uint32_t n, CompactMeta cm, uint64_t *keys)
+                                                 uint32_t n, CompactMeta cm, uint64_t *keys, bool lds)
 {
+    extern __shared__ __attribute__((aligned(16))) uint64_t tl[];
+    if (lds) {
+        cs_stage_tables(cm, tl);
+        __syncthreads();
+    }
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint32_t g = gid[i];
@@ -314,38 +337,163 @@ __device__ __forceinline__ uint64_t code_bits(const uint64_t (&c)[WC], int pos, 
     return cnt == 64 ? v : v >> (64 - cnt);
 }
 
-// sorted keys back to rows: gid, words = pattern outside the mask | the
-// expanded code bits inside it, the LSN gathered by row index
-template <int WC>
-__global__ __launch_bounds__(256) void k_cs_unpack(const uint64_t *keys, uint32_t n, CompactMeta cm,
-                                                   const uint64_t *lsn_in, uint32_t *gid_o,
-                                                   uint64_t *words_o, uint64_t *lsn_o, size_t stride)
+// ---- the unpack fused with the dedupe (as the packed sort's, hsc_ingest.hip) ----
+// The last version of a key is the last of its run of equal (gid, code):
+// the keys minus their row-index bits.  Blocks of kCsUdTile sorted rows: one
+// pass counts the blocks' distinct rows (their exclusive scan gives each
+// block's place), the next writes every version to the *_o rows and the last
+// of each key to its place among the *_d rows.
+constexpr int kCsUdThreads = 256;
+constexpr int kCsUdRows = 8;
+constexpr int kCsUdTile = kCsUdThreads * kCsUdRows;
+
+template <int KW>
+__device__ __forceinline__ bool cs_last(const uint64_t *keys, size_t n, size_t i)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint64_t *k = keys + (size_t)i * (WC + 1);
-    uint64_t kk[WC + 1];
+    if (i + 1 >= n) return true;
+    const uint64_t *a = keys + i * KW, *b = a + KW;
 #pragma unroll
-    for (int m = 0; m <= WC; ++m) kk[m] = k[m];
-    const uint32_t g = (uint32_t)(kk[0] >> 32), idx = (uint32_t)kk[WC];
-    uint64_t c[WC];
+    for (int k = 0; k < KW - 1; ++k)
+        if (a[k] != b[k]) return true;
+    return (a[KW - 1] >> 32) != (b[KW - 1] >> 32);
+}
+
+template <int KW>
+__global__ __launch_bounds__(kCsUdThreads) void k_cs_bcount(const uint64_t *keys, size_t n, uint32_t *bc)
+{
+    __shared__ uint32_t wsum[kCsUdThreads / 64];
+    const size_t base = (size_t)blockIdx.x * kCsUdTile;
+    uint32_t c = 0;
 #pragma unroll
-    for (int m = 0; m < WC; ++m) c[m] = kk[m] << 32 | kk[m + 1] >> 32;
-    lsn_o[i] = lsn_in[idx];
-    gid_o[i] = g;
-    const uint64_t *mk = cm.mask + (size_t)g * cm.W, *pt = cm.pat + (size_t)g * cm.W;
-    const uint64_t *mv = cm.mv + (size_t)g * cm.W * 6;
-    int pos = 0;
-    for (int j = 0; j < cm.W; ++j) {
-        const uint64_t m = mk[j];
-        const int cnt = __popcll(m);
-        const uint64_t part = code_bits<WC>(c, pos, cnt);
-        pos += cnt;
-        words_o[(size_t)j * stride + i] = (pt[j] & ~m) | (m ? expand(part, m, mv + 6 * j) : 0);
+    for (int r = 0; r < kCsUdRows; ++r) {
+        const size_t i = base + (size_t)r * kCsUdThreads + threadIdx.x;
+        if (i < n) c += cs_last<KW>(keys, n, i);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < kCsUdThreads / 64; ++w) t += wsum[w];
+        bc[blockIdx.x] = t;
+    }
+}
+
+template <int WC>
+__global__ __launch_bounds__(kCsUdThreads) void k_cs_unpack_dd(
+    const uint64_t *keys, size_t n, CompactMeta cm, const uint64_t *lsn_in, uint32_t *gid_o,
+    uint64_t *words_o, uint64_t *lsn_o, size_t stride_o, const uint32_t *boff, uint32_t *gid_d,
+    uint64_t *words_d, uint64_t *lsn_d, size_t stride_d, uint32_t *d_count, bool lds)
+{
+    constexpr int KW = WC + 1;
+    extern __shared__ __attribute__((aligned(16))) uint64_t tl[];
+    if (lds) cs_stage_tables(cm, tl);  // synchronized by the scan's barrier below
+    __shared__ uint32_t pos[kCsUdTile];
+    __shared__ uint32_t wsum[kCsUdThreads / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const size_t base = (size_t)blockIdx.x * kCsUdTile;
+    const uint32_t nrows = (uint32_t)min((size_t)kCsUdTile, n - base);
+    // thread t ranks rows 8t .. 8t + 7 of the block: flags, wave scan, block scan
+    uint32_t fl = 0, cnt = 0;
+#pragma unroll
+    for (int r = 0; r < kCsUdRows; ++r) {
+        const uint32_t j = threadIdx.x * kCsUdRows + r;
+        const bool last = j < nrows && cs_last<KW>(keys, n, base + j);
+        fl |= (uint32_t)last << r;
+        cnt += last;
+    }
+    uint32_t inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t run = inc - cnt, total = 0;
+#pragma unroll
+    for (int w = 0; w < kCsUdThreads / 64; ++w) {
+        run += w < wv ? wsum[w] : 0;
+        total += wsum[w];
+    }
+#pragma unroll
+    for (int r = 0; r < kCsUdRows; ++r) {
+        const uint32_t j = threadIdx.x * kCsUdRows + r;
+        if (j < nrows) pos[j] = (fl >> r & 1u) ? run : 0xFFFFFFFFu;
+        run += fl >> r & 1u;
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *d_count = boff[blockIdx.x] + total;
+    __syncthreads();
+    const uint32_t b0 = boff[blockIdx.x];
+    for (uint32_t j = threadIdx.x; j < nrows; j += kCsUdThreads) {  // consecutive rows per wave
+        const size_t i = base + j;
+        const uint64_t *k = keys + i * KW;
+        uint64_t kk[KW];
+#pragma unroll
+        for (int m = 0; m < KW; ++m) kk[m] = k[m];
+        const uint32_t g = (uint32_t)(kk[0] >> 32), idx = (uint32_t)kk[WC];
+        uint64_t c[WC];
+#pragma unroll
+        for (int m = 0; m < WC; ++m) c[m] = kk[m] << 32 | kk[m + 1] >> 32;
+        const uint64_t lv = lsn_in[idx];
+        const uint32_t d = pos[j];
+        const bool last = d != 0xFFFFFFFFu;
+        lsn_o[i] = lv;
+        gid_o[i] = g;
+        if (last) lsn_d[b0 + d] = lv, gid_d[b0 + d] = g;
+        const uint64_t *mk = cm.mask + (size_t)g * cm.W, *pt = cm.pat + (size_t)g * cm.W;
+        const uint64_t *mv = cm.mv + (size_t)g * cm.W * 6;
+        int p = 0;
+        for (int w = 0; w < cm.W; ++w) {
+            const uint64_t m = mk[w];
+            const int cn = __popcll(m);
+            const uint64_t part = code_bits<WC>(c, p, cn);
+            p += cn;
+            const uint64_t v = (pt[w] & ~m) | (m ? expand(part, m, mv + 6 * w) : 0);
+            words_o[(size_t)w * stride_o + i] = v;
+            if (last) words_d[(size_t)w * stride_d + b0 + d] = v;
+        }
     }
 }
 
 }  // namespace
+
+hipError_t compact_unpack_dedupe(const uint64_t *keys, size_t n, const CompactTables &t,
+                                 const uint64_t *lsn_in, uint32_t *gid_o, uint64_t *words_o,
+                                 uint64_t *lsn_o, size_t stride_o, uint32_t *gid_d, uint64_t *words_d,
+                                 uint64_t *lsn_d, size_t stride_d, uint32_t *d_count, uint32_t *scratch,
+                                 hipStream_t s)
+{
+    if (n == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
+    const CompactMeta cm = meta_of(t);
+    const uint32_t ud = (uint32_t)((n + kCsUdTile - 1) / kCsUdTile);
+    uint32_t *bc = scratch, *btmp = scratch + ud + 16;
+    switch (t.WC) {
+    case 1: k_cs_bcount<2><<<ud, kCsUdThreads, 0, s>>>(keys, n, bc); break;
+    case 2: k_cs_bcount<3><<<ud, kCsUdThreads, 0, s>>>(keys, n, bc); break;
+    case 3: k_cs_bcount<4><<<ud, kCsUdThreads, 0, s>>>(keys, n, bc); break;
+    default: return hipErrorInvalidValue;
+    }
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = scan_exclusive_u32(bc, ud, btmp, s);
+    if (e != hipSuccess) return e;
+    const uint32_t tb = cs_tab_bytes(t.ng, t.W);
+    const bool lds = tb <= kCsTabLds;
+#define HSC_CS_UD(WC_)                                                            \
+    k_cs_unpack_dd<WC_><<<ud, kCsUdThreads, lds ? tb : 0, s>>>(keys, n, cm, lsn_in, gid_o, words_o, \
+                                                               lsn_o, stride_o, bc, gid_d, words_d, \
+                                                               lsn_d, stride_d, d_count, lds)
+    if (t.WC == 1)
+        HSC_CS_UD(1);
+    else if (t.WC == 2)
+        HSC_CS_UD(2);
+    else
+        HSC_CS_UD(3);
+#undef HSC_CS_UD
+    return hipGetLastError();
+}
 
 hipError_t compact_masks_unsorted(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
                                   int W, int ng, uint32_t *rep, uint64_t *mask, uint64_t *pat,
@@ -370,26 +518,13 @@ hipError_t compact_sort_keys(const uint64_t *words, size_t stride, const uint32_
     if (n == 0) return hipSuccess;
     const CompactMeta cm = meta_of(t);
     const uint32_t b = (n + 255) / 256;
+    const uint32_t tb = cs_tab_bytes(t.ng, t.W);
+    const bool lds = tb <= kCsTabLds;
+    const uint32_t ldsb = lds ? tb : 0;
     switch (t.WC) {
-    case 1: k_cs_keys<1><<<b, 256, 0, s>>>(words, stride, gid, n, cm, keys); break;
-    case 2: k_cs_keys<2><<<b, 256, 0, s>>>(words, stride, gid, n, cm, keys); break;
-    case 3: k_cs_keys<3><<<b, 256, 0, s>>>(words, stride, gid, n, cm, keys); break;
-    default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-hipError_t compact_unpack_sorted(const uint64_t *keys, uint32_t n, const CompactTables &t,
-                                 const uint64_t *lsn_in, uint32_t *gid_o, uint64_t *words_o,
-                                 uint64_t *lsn_o, size_t stride, hipStream_t s)
-{
-    if (n == 0) return hipSuccess;
-    const CompactMeta cm = meta_of(t);
-    const uint32_t b = (n + 255) / 256;
-    switch (t.WC) {
-    case 1: k_cs_unpack<1><<<b, 256, 0, s>>>(keys, n, cm, lsn_in, gid_o, words_o, lsn_o, stride); break;
-    case 2: k_cs_unpack<2><<<b, 256, 0, s>>>(keys, n, cm, lsn_in, gid_o, words_o, lsn_o, stride); break;
-    case 3: k_cs_unpack<3><<<b, 256, 0, s>>>(keys, n, cm, lsn_in, gid_o, words_o, lsn_o, stride); break;
+    case 1: k_cs_keys<1><<<b, 256, ldsb, s>>>(words, stride, gid, n, cm, keys, lds); break;
+    case 2: k_cs_keys<2><<<b, 256, ldsb, s>>>(words, stride, gid, n, cm, keys, lds); break;
+    case 3: k_cs_keys<3><<<b, 256, ldsb, s>>>(words, stride, gid, n, cm, keys, lds); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

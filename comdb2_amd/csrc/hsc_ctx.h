@@ -473,6 +473,8 @@ struct hsc_ctx {
     bool code_sorted = false;  // the last build sorted by compact codes
     std::vector<uint64_t> cs_mask;     // its varying bits per (group, word) (host copy)
     std::vector<uint8_t> cs_has_rows;  // its groups with rows
+    std::vector<uint32_t> cs_bits_h;   // host sources of its table uploads
+    std::vector<uint64_t> cs_mv_h;
     int ct_maxbits = 0;  // most varying bits of any group
     // compact tiles (hsc_ctiles.hip): the compact window as gid || code keys
     bool ctiles = false;

@@ -555,8 +555,12 @@ static int code_sort(hsc_ctx *c, size_t n_in, bool *done)
     HIPCHK(c, hipMemcpyAsync(mask.data(), c->d_csmask.p, 8 * gw, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipMemcpyAsync(rep.data(), c->d_csrep.p, 4 * (size_t)ng, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
-    std::vector<uint32_t> bits(2 * (size_t)ng);
-    std::vector<uint64_t> mv(gw * 6);
+    // (host sources of the uploads below: the context's, alive past the
+    // asynchronous copies)
+    std::vector<uint32_t> &bits = c->cs_bits_h;
+    std::vector<uint64_t> &mv = c->cs_mv_h;
+    bits.assign(2 * (size_t)ng, 0);
+    mv.assign(gw * 6, 0);
     int maxbits = 0;
     c->cs_mask = mask;  // build_compact takes these tables over
     c->cs_has_rows.assign(ng, 0);
@@ -587,18 +591,23 @@ static int code_sort(hsc_ctx *c, size_t n_in, bool *done)
     t.WC = WC;
     t.ng = ng;
     const int KW = WC + 1;
-    for (auto &b : c->d_cskeys) HIPCHK(c, b.ensure(8 * (size_t)KW * n_in));
+    // (the free key buffer becomes d_lsn below: at least the window's capacity)
+    for (auto &b : c->d_cskeys) HIPCHK(c, b.ensure(8 * std::max((size_t)KW * n_in, c->cap)));
     HIPCHK(c, compact_sort_keys(c->d_words.as<uint64_t>(), c->cap, c->d_gid.as<uint32_t>(), (uint32_t)n_in,
                                 t, c->d_cskeys[0].as<uint64_t>(), s));
     uint64_t *sorted = nullptr;
     HIPCHK(c, code_keys_sort(c->d_cskeys[0].as<uint64_t>(), c->d_cskeys[1].as<uint64_t>(), n_in, KW, s,
                              &sorted));
-    HIPCHK(c, compact_unpack_sorted(sorted, (uint32_t)n_in, t, c->d_lsn.as<uint64_t>(),
-                                    c->d_gid2.as<uint32_t>(), c->d_words2.as<uint64_t>(),
-                                    c->d_lsn2.as<uint64_t>(), c->cap, s));
-    // the tables stay valid until the next build: mv / bits are host vectors
-    // uploaded above, so the stream must have read them before they go
-    HIPCHK(c, hipStreamSynchronize(s));
+    // every version, key-sorted, into d_*2; the distinct rows into d_gid /
+    // d_words (the unpack reads only the input LSNs) and the free key
+    // buffer, which becomes d_lsn
+    DBuf &kfree = sorted == c->d_cskeys[0].as<uint64_t>() ? c->d_cskeys[1] : c->d_cskeys[0];
+    HIPCHK(c, compact_unpack_dedupe(sorted, n_in, t, c->d_lsn.as<uint64_t>(), c->d_gid2.as<uint32_t>(),
+                                    c->d_words2.as<uint64_t>(), c->d_lsn2.as<uint64_t>(), c->cap,
+                                    c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
+                                    kfree.as<uint64_t>(), c->cap, c->d_count.as<uint32_t>(),
+                                    c->d_scratch.as<uint32_t>(), s));
+    std::swap(c->d_lsn, kfree);
     *done = true;
     return HSC_OK;
 }
@@ -667,13 +676,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
             std::swap(c->d_lsn, c->d_pk[1]);
         bt.stamp("sort");
     } else if (code_sorted) {
-        // every version, key-sorted, in d_*2; the distinct rows into d_*
-        bt.stamp("sort");
-        HIPCHK(c, dedupe_rows(W, n_in, c->d_gid2.as<uint32_t>(), c->d_words2.as<uint64_t>(),
-                              c->d_lsn2.as<uint64_t>(), cap, c->d_gid.as<uint32_t>(),
-                              c->d_words.as<uint64_t>(), c->d_lsn.as<uint64_t>(), cap,
-                              c->d_flags.as<uint32_t>(), c->d_scratch.p, c->d_scratch.bytes,
-                              c->d_count.as<uint32_t>(), s));
+        bt.stamp("sort");  // every version in d_*2, the distinct rows in d_* (code_sort)
     } else {
         bool in_alt = false;
         HIPCHK(c, radix_sort_known(W, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),

@@ -497,9 +497,15 @@ hipError_t compact_sort_keys(const uint64_t *words, size_t stride, const uint32_
                              const CompactTables &t, uint64_t *keys, hipStream_t s);
 hipError_t code_keys_sort(uint64_t *keys, uint64_t *tmp, size_t n, int KW, hipStream_t s,
                           uint64_t **sorted);
-hipError_t compact_unpack_sorted(const uint64_t *keys, uint32_t n, const CompactTables &t,
+// sorted keys back to rows, with the dedupe fused in: every version to *_o, the last of
+// each key to *_d (which may be the input gid / words -- only lsn_in is read
+// by index), d_count[0] = distinct rows; scratch >= n / 2048 + 16 +
+// scan_scratch_bytes(n / 2048 + 1) / 4 words
+hipError_t compact_unpack_dedupe(const uint64_t *keys, size_t n, const CompactTables &t,
                                  const uint64_t *lsn_in, uint32_t *gid_o, uint64_t *words_o,
-                                 uint64_t *lsn_o, size_t stride, hipStream_t s);
+                                 uint64_t *lsn_o, size_t stride_o, uint32_t *gid_d, uint64_t *words_d,
+                                 uint64_t *lsn_d, size_t stride_d, uint32_t *d_count, uint32_t *scratch,
+                                 hipStream_t s);
 hipError_t warm_csort();
 // lo/hi bounds (W words) -> code bounds (WC words, SoA [WC][n]); ranges that
 // miss their group's rows become (~0, 0)
