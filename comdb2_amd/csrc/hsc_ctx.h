@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <functional>
@@ -236,19 +237,27 @@ class WorkPool {
   public:
     explicit WorkPool(int nthreads) : size_(std::max(1, nthreads))
     {
-        for (int i = 1; i < size_; ++i) th_.emplace_back([this] { loop(); });
+        for (int i = 1; i < size_; ++i) th_.emplace_back([this, i] { loop(i); });
     }
     ~WorkPool()
     {
         {
             std::lock_guard<std::mutex> g(m_);
             stop_ = true;
+            gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
         for (auto &t : th_) t.join();
     }
     int size() const { return size_; }
-    void run(int nwork, const std::function<void(int)> &f)
+    // f(0 .. nwork - 1), dynamically scheduled
+    void run(int nwork, const std::function<void(int)> &f) { go(nwork, f, false); }
+    // f(i) on participant i % size() (0 = the caller): two runs over the same
+    // items touch each item's data from the same core
+    void run_static(int nwork, const std::function<void(int)> &f) { go(nwork, f, true); }
+
+  private:
+    void go(int nwork, const std::function<void(int)> &f, bool stat)
     {
         if (nwork <= 0) return;
         if (th_.empty() || nwork == 1) {
@@ -259,45 +268,61 @@ class WorkPool {
             std::lock_guard<std::mutex> g(m_);
             job_ = &f;
             nwork_ = nwork;
+            static_ = stat;
             next_.store(0, std::memory_order_relaxed);
-            busy_ = (int)th_.size();
-            ++gen_;
+            busy_.store((int)th_.size(), std::memory_order_relaxed);
+            gen_.fetch_add(1, std::memory_order_release);
         }
-        cv_.notify_all();
-        work();
-        std::unique_lock<std::mutex> lk(m_);
-        done_.wait(lk, [this] { return busy_ == 0; });
+        if (sleeping_.load(std::memory_order_acquire)) cv_.notify_all();
+        work(0);
+        // the workers finish their share (they spin between back-to-back jobs)
+        while (busy_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
         job_ = nullptr;
     }
-
-  private:
-    void work()
+    void work(int me)
     {
-        for (int i = next_.fetch_add(1); i < nwork_; i = next_.fetch_add(1)) (*job_)(i);
+        if (static_) {
+            for (int i = me; i < nwork_; i += size_) (*job_)(i);
+        } else {
+            for (int i = next_.fetch_add(1); i < nwork_; i = next_.fetch_add(1)) (*job_)(i);
+        }
     }
-    void loop()
+    // A worker spins up to kSpin for the next job (a marshal runs its phases
+    // back to back: a futex wake per phase cost tens of microseconds on a
+    // large host), then sleeps on the condition variable.
+    void loop(int me)
     {
         uint64_t seen = 0;
         for (;;) {
-            {
+            const auto t0 = std::chrono::steady_clock::now();
+            while (gen_.load(std::memory_order_acquire) == seen &&
+                   std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(kSpinUs))
+                __builtin_ia32_pause();
+            if (gen_.load(std::memory_order_acquire) == seen) {
                 std::unique_lock<std::mutex> lk(m_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
+                sleeping_.fetch_add(1, std::memory_order_acq_rel);
+                cv_.wait(lk, [&] { return stop_ || gen_.load(std::memory_order_acquire) != seen; });
+                sleeping_.fetch_sub(1, std::memory_order_acq_rel);
             }
-            work();
-            std::lock_guard<std::mutex> g(m_);
-            if (--busy_ == 0) done_.notify_one();
+            {
+                std::lock_guard<std::mutex> g(m_);
+                if (stop_) return;
+                seen = gen_.load(std::memory_order_acquire);
+            }
+            work(me);
+            busy_.fetch_sub(1, std::memory_order_acq_rel);
         }
     }
+    static constexpr int kSpinUs = 200;
     const int size_;
     std::vector<std::thread> th_;
     std::mutex m_;
-    std::condition_variable cv_, done_;
+    std::condition_variable cv_;
     const std::function<void(int)> *job_ = nullptr;
-    std::atomic<int> next_{0};
-    int nwork_ = 0, busy_ = 0;
-    uint64_t gen_ = 0;
+    std::atomic<int> next_{0}, busy_{0}, sleeping_{0};
+    std::atomic<uint64_t> gen_{0};
+    int nwork_ = 0;
+    bool static_ = false;
     bool stop_ = false;
 };
 

@@ -1929,14 +1929,17 @@ static int default_threads()
 // Runs f(i) for i in [0, nwork) on the context's worker pool (parallel) or
 // on the caller's thread.
 template <class F>
-static void par_for(hsc_ctx *c, bool parallel, int nwork, F f)
+static void par_for(hsc_ctx *c, bool parallel, int nwork, F f, bool stat = false)
 {
     if (!parallel || c->threads <= 1 || nwork <= 1) {
         for (int i = 0; i < nwork; ++i) f(i);
         return;
     }
     if (!c->pool || c->pool->size() != c->threads) c->pool.reset(new WorkPool(c->threads));
-    c->pool->run(nwork, std::function<void(int)>(f));
+    if (stat)
+        c->pool->run_static(nwork, std::function<void(int)>(f));
+    else
+        c->pool->run(nwork, std::function<void(int)>(f));
 }
 
 // Marshal read sets [t0, t1) of src into the staging set st: parts in
@@ -1970,7 +1973,7 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
             if (src.premarshalled(c, t, mp, (uint32_t)(t - t0))) continue;
             src.each(t, tl, [&](int nr, auto get) { marshal_txn(c, mp, (uint32_t)(t - t0), S, nr, get); });
         }
-    });
+    }, true);  // static: part w marshalled and assembled on one core
     size_t n = 0, nl = 0;
     for (int w = 0; w < nwork; ++w) {
         c->parts[w].out0 = n;
@@ -2053,7 +2056,7 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
             memcpy(lsnap + lo0, mp.lock_snap.data(), 8 * kl);
             memcpy(ltxn + lo0, mp.lock_txn.data(), 4 * kl);
         }
-    });
+    }, true);  // static: part w marshalled and assembled on one core
     const auto tp3 = std::chrono::steady_clock::now();
     auto ns = [](auto a, auto b) {
         return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
@@ -3745,6 +3748,27 @@ static int check_batch(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, 
     static thread_local std::vector<hsc_currangearr *> full;
     static thread_local std::vector<PreMarshal *> fpre;
     static thread_local std::vector<uint64_t> snaps;
+    // every element a full check (the batch entry's usual call): the caller's
+    // arrays are the device batch as they are, verdicts land in rc_out
+    bool dense = !regop_only;
+    for (int i = 0; i < n && dense; ++i) dense = ranges[i] != nullptr;
+    if (dense && n) {
+        snaps.resize(n);
+        const unsigned int ef = (unsigned int)(c->end_lsn >> 32), eo = (unsigned int)c->end_lsn;
+        for (int i = 0; i < n; ++i) {
+            hsc_currangearr *a = (hsc_currangearr *)ranges[i];
+            unsigned int *pf = file ? &file[i] : &a->file;
+            unsigned int *po = offset ? &offset[i] : &a->offset;
+            snaps[i] = ((uint64_t)*pf << 32) | *po;
+            *pf = ef, *po = eo;  // full mode: *file,*offset := curlsn
+        }
+        ArrSrc src{(hsc_currangearr *const *)ranges, snaps.data(), n};
+        if (pre) src.pre = pre, src.epoch = c->dict_epoch;
+        rc = check_src(c, src, rc_out, &lk);
+        if (rc)
+            for (int i = 0; i < n; ++i) rc_out[i] = 1;
+        return rc;
+    }
     slot.assign(n, -1);
     full.clear(), fpre.clear(), snaps.clear();
     for (int i = 0; i < n; ++i) {
