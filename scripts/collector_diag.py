@@ -45,7 +45,7 @@ want = v.check_readsets(c2.readsets) != 0
 print(f"cpu.max {cpu_max()}  affinity {len(os.sched_getaffinity(0))}  nproc {os.cpu_count()}  "
       , flush=True)
 for nth in threads:
-    for inflight in (0,):
+    for inflight in [int(x) for x in os.environ.get("DIAG_INFLIGHT", "0").split(",")]:
         s0 = cpu_stat()
         t0 = time.perf_counter()
         got, st = v.concurrent_check(arrs, nth, inflight=inflight)
@@ -55,7 +55,7 @@ for nth in threads:
                                                      "usage_usec", "user_usec", "system_usec")}
         keep = ("checks_per_s", "lat_p50_us", "lat_p99_us", "mean_batch", "device_pass_us",
                 "busy_frac", "gate_us", "handout_us")
-        print(f"threads {nth}: parity {bool(np.array_equal(got != 0, want))} wall {el:.2f}s "
+        print(f"threads {nth} inflight {inflight or 2}: parity {bool(np.array_equal(got != 0, want))} wall {el:.2f}s "
               f"cpu {d['usage_usec'] / 1e6 / max(el, 1e-9):.2f} cores "
               f"(user {d['user_usec'] / 1e6:.2f}s sys {d['system_usec'] / 1e6:.2f}s) "
               f"periods {d['nr_periods']} throttled {d['nr_throttled']} ({d['throttled_usec'] / 1e3:.1f} ms) | "
