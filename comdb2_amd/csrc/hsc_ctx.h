@@ -574,11 +574,21 @@ struct hsc_ctx {
         std::vector<uint8_t> forced;
         size_t n_txn = 0, vo = 0, dn = 0;
         uint32_t seq = 0;
+        hipStream_t stream = nullptr;  // the stream its kernel was launched on
         std::atomic<bool> busy{false};
     };
     SmallSlot small[kSmallSlots];
+    // Small batches run on side streams of their own, one per slot, so that
+    // concurrent ones overlap on the device instead of queueing behind each
+    // other on c->stream.  What they read of the window is complete when they
+    // launch -- builds, folds and table-maxima uploads synchronize -- except
+    // an append's merge / upload, so a slot's stream waits on app_last once
+    // per append (app_seq); every window change waits on the host until no
+    // slot is in flight (wait_small), so a kernel never overlaps a change.
+    hipStream_t small_side[kSmallSlots] = {};
+    uint64_t small_app_seq[kSmallSlots] = {};
+    uint64_t app_seq = 0;  // appends whose device work app_last follows
     Stage small_st;  // marshal target of the small path (coh: its arena swaps into a slot)
-    uint32_t small_next = 0;
     DBuf small_blocks;
     bool small_blocks_zeroed = false;
     bool no_small = false;  // hsc_set_paths(HSC_PATH_NO_SMALL): the staged path

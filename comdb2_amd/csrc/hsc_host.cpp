@@ -140,6 +140,7 @@ static int app_staged(hsc_ctx *c, hipStream_t s)
         return fail(c, HSC_EDEVICE, "append event");
     if (hipEventRecord(c->app_ev[i], s) != hipSuccess) return fail(c, HSC_EDEVICE, "append event");
     c->app_last = c->app_ev[i];
+    c->app_seq++;
     c->app_i ^= 1;
     return HSC_OK;
 }
@@ -203,6 +204,7 @@ static void pend_retire(hsc_ctx *c)
 {
     c->app_tchg.clear();
     if (!c->pend_n && !c->pend_t) return;
+    (void)wait_small(c);  // small batches on side streams read the tail too
     const int i = c->pend_i;
     if ((!c->pend_ev[i] && hipEventCreateWithFlags(&c->pend_ev[i], hipEventDisableTiming) != hipSuccess) ||
         hipEventRecord(c->pend_ev[i], c->stream) != hipSuccess) {
@@ -2673,14 +2675,15 @@ static uint64_t ns_since(SteadyClock::time_point t0)
 // them).  -> slot index, or < 0 (an HSC_ error code, already recorded).
 static int small_launch(hsc_ctx *c, Stage &st)
 {
+    // the lowest free slot; with every slot taken, the oldest launch's
     int k = -1;
-    for (int i = 0; i < hsc_ctx::kSmallSlots && k < 0; ++i) {
-        const int j = (int)((c->small_next + i) % hsc_ctx::kSmallSlots);
-        if (!c->small[j].busy.load(std::memory_order_acquire)) k = j;
-    }
+    for (int i = 0; i < hsc_ctx::kSmallSlots && k < 0; ++i)
+        if (!c->small[i].busy.load(std::memory_order_acquire)) k = i;
     if (k < 0) {
         c->sm_slot_waits.fetch_add(1, std::memory_order_relaxed);
-        k = (int)(c->small_next % hsc_ctx::kSmallSlots);  // launched first, finishes first
+        k = 0;
+        for (int i = 1; i < hsc_ctx::kSmallSlots; ++i)
+            if ((int32_t)(c->small[i].seq - c->small[k].seq) < 0) k = i;
         const auto t0 = SteadyClock::now();
         while (c->small[k].busy.load(std::memory_order_acquire)) {
             __builtin_ia32_pause();
@@ -2698,9 +2701,16 @@ static int small_launch(hsc_ctx *c, Stage &st)
         return fail(c, HSC_EINVAL, "small batch marshalled outside the small stage");
     std::swap(sl.io, st.arena);
     HIPCHK(c, c->small_blocks.ensure(64 * hsc_ctx::kSmallSlots));
-    hipStream_t s = c->stream;
-    if (!c->small_blocks_zeroed) {
+    if (!c->small_side[k]) HIPCHK(c, hipStreamCreateWithFlags(&c->small_side[k], hipStreamNonBlocking));
+    hipStream_t s = c->small_side[k];
+    if (c->app_last && c->small_app_seq[k] != c->app_seq) {  // after the appends' device work
+        HIPCHK(c, hipStreamWaitEvent(s, c->app_last, 0));
+        c->small_app_seq[k] = c->app_seq;
+    }
+    sl.stream = s;
+    if (!c->small_blocks_zeroed) {  // every slot's counters, before any slot's first launch
         HIPCHK(c, hipMemsetAsync(c->small_blocks.p, 0, 64 * hsc_ctx::kSmallSlots, s));
+        HIPCHK(c, hipStreamSynchronize(s));
         c->small_blocks_zeroed = true;
     }
     uint8_t *io = sl.io.as<uint8_t>(), *dio = (uint8_t *)sl.io.dp;
@@ -2740,7 +2750,6 @@ static int small_launch(hsc_ctx *c, Stage &st)
     HIPCHK(c, launch_small_narrow(nv, d, d2, pd, p, dio + sl.vo, c->small_blocks.as<uint32_t>() + 16 * k,
                                   (uint32_t *)(dio + sl.dn), sl.seq, s));
     sl.busy.store(true, std::memory_order_release);
-    c->small_next = (uint32_t)(k + 1);
     return k;
 }
 
@@ -2820,7 +2829,7 @@ static int check_src(hsc_ctx *c, const Src &src, int *rc_out,
                 (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count(),
                 std::memory_order_relaxed);
             c->sm_launch_ns.fetch_add(ns_since(t1), std::memory_order_relaxed);
-            hipStream_t s = c->stream;
+            hipStream_t s = c->small[k].stream;
             if (lk) lk->unlock();
             const char *why = nullptr;
             hipError_t herr = hipSuccess;
@@ -2930,6 +2939,9 @@ void hsc_ctx_destroy(hsc_ctx *c)
         return;
     }
     (void)hipSetDevice(c->device);
+    (void)wait_small(c);
+    for (hipStream_t &st : c->small_side)
+        if (st) (void)hipStreamSynchronize(st), (void)hipStreamDestroy(st), st = nullptr;
     fold_discard(c);
     if (c->shadow) hsc_ctx_destroy(c->shadow);
     c->shadow = nullptr;
@@ -3316,7 +3328,8 @@ int hsc_merge_table_max(hsc_ctx *c, const uint64_t *in, int n)
     if (!c->host_only && !c->dirty && n > 0) {
         (void)hipSetDevice(c->device);
         const size_t nt = c->table_names.size();
-        HIPCHK(c, hipStreamSynchronize(c->stream));  // no reader of the old buffer in flight
+        HIPCHK(c, wait_small(c));  // no reader of the old buffer in flight
+        HIPCHK(c, hipStreamSynchronize(c->stream));
         HIPCHK(c, c->d_table_max.ensure(8 * nt));
         HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, c->h_table_max.data(), 8 * nt,
                                  hipMemcpyHostToDevice, c->stream));

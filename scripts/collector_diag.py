@@ -60,6 +60,9 @@ for nth in threads:
               f"(user {d['user_usec'] / 1e6:.2f}s sys {d['system_usec'] / 1e6:.2f}s) "
               f"periods {d['nr_periods']} throttled {d['nr_throttled']} ({d['throttled_usec'] / 1e3:.1f} ms) | "
               + " ".join(f"{k} {st[k]:.1f}" if isinstance(st.get(k), float) else f"{k} {st.get(k)}"
-                         for k in keep), flush=True)
+                         for k in keep)
+              + (" | small " + " ".join(f"{k} {v:.1f}" for k, v in st["small_path"].items()
+                                       if isinstance(v, float)) if "small_path" in st else ""),
+              flush=True)
 arrs.close()
 v.close()
