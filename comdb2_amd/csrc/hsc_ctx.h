@@ -575,6 +575,13 @@ struct hsc_ctx {
         size_t n_txn = 0, vo = 0, dn = 0;
         uint32_t seq = 0;
         hipStream_t stream = nullptr;  // the stream its kernel was launched on
+        hipEvent_t wait_ev = nullptr;  // the stream waits on it before the launch (appends)
+        // the launch's arguments, captured under c->mu (the launch itself is
+        // issued after the lock is dropped: small_fire)
+        NarrowView nv{};
+        DeltaView d{}, d2{};
+        PendView pd{};
+        ProbeView p{};
         std::atomic<bool> busy{false};
     };
     SmallSlot small[kSmallSlots];

@@ -1891,6 +1891,26 @@ struct ArrSrc {
     // in flight together instead of one after another in the marshal.
     void prefetch(int t0, int t1) const
     {
+        // callers' premarshalled rows (written on other cores): the objects,
+        // then every line of their rows, all in flight before the copies
+        if (pre) {
+            for (int t = t0; t < t1; ++t)
+                if (pre[t]) __builtin_prefetch(pre[t]);
+            auto lines = [](const void *p, size_t bytes) {
+                for (size_t o = 0; o < bytes; o += 64) __builtin_prefetch((const char *)p + o);
+            };
+            for (int t = t0; t < t1; ++t)
+                if (pre_ok(t)) {
+                    const MarshalPart &q = pre[t]->mp;
+                    lines(q.lohi.data(), 8 * q.lohi.size());
+                    lines(q.gid.data(), 4 * q.gid.size());
+                    lines(q.snap.data(), 8 * q.snap.size());
+                    if (q.lock_table.size()) {
+                        lines(q.lock_table.data(), 4 * q.lock_table.size());
+                        lines(q.lock_snap.data(), 8 * q.lock_snap.size());
+                    }
+                }
+        }
         for (int t = t0; t < t1; ++t)
             if (!pre_ok(t)) __builtin_prefetch(arr[t]);
         for (int t = t0; t < t1; ++t)
@@ -2703,8 +2723,9 @@ static int small_launch(hsc_ctx *c, Stage &st)
     HIPCHK(c, c->small_blocks.ensure(64 * hsc_ctx::kSmallSlots));
     if (!c->small_side[k]) HIPCHK(c, hipStreamCreateWithFlags(&c->small_side[k], hipStreamNonBlocking));
     hipStream_t s = c->small_side[k];
+    sl.wait_ev = nullptr;
     if (c->app_last && c->small_app_seq[k] != c->app_seq) {  // after the appends' device work
-        HIPCHK(c, hipStreamWaitEvent(s, c->app_last, 0));
+        sl.wait_ev = c->app_last;  // not re-recorded while a slot is busy (wait_small)
         c->small_app_seq[k] = c->app_seq;
     }
     sl.stream = s;
@@ -2721,7 +2742,8 @@ static int small_launch(hsc_ctx *c, Stage &st)
     sl.seq = c->small_seq;
     *done = 0;
     std::atomic_thread_fence(std::memory_order_seq_cst);
-    ProbeView p{};
+    ProbeView &p = sl.p;
+    p = ProbeView{};
     p.lo = (const uint64_t *)(dio + st.L.lo);
     p.hi = (const uint64_t *)(dio + st.L.hi);
     p.gid = (const uint32_t *)(dio + st.L.gid);
@@ -2734,23 +2756,37 @@ static int small_launch(hsc_ctx *c, Stage &st)
     p.n_lock = (uint32_t)st.n_lock;
     static const bool empty = getenv("HSC_SMALL_EMPTY") != nullptr;  // diagnostics: the
     if (empty) p.n = p.n_lock = 0;  // launch + done-word floor (verdicts all 0: wrong answers)
-    NarrowView nv = c->nv;
-    nv.table_max = c->d_table_max.as<uint64_t>();
+    sl.nv = c->nv;
+    sl.nv.table_max = c->d_table_max.as<uint64_t>();
     // tables past nt_dev have their maxima in the pending tail only
-    nv.ntables = std::min((uint32_t)c->table_names.size(), c->nt_dev);
-    DeltaView d{}, d2{};
-    if (c->dn) d = delta_view(c);
-    if (c->fn) d2 = frozen_view(c);
-    PendView pd{};
+    sl.nv.ntables = std::min((uint32_t)c->table_names.size(), c->nt_dev);
+    sl.d = c->dn ? delta_view(c) : DeltaView{};
+    sl.d2 = c->fn ? frozen_view(c) : DeltaView{};
+    sl.pd = PendView{};
     if (c->pend_n || c->pend_t) {
-        pd.base = (const uint8_t *)c->h_pend[c->pend_i].dp;
-        pd.n = c->pend_n;
-        pd.nt = c->pend_t;
+        sl.pd.base = (const uint8_t *)c->h_pend[c->pend_i].dp;
+        sl.pd.n = c->pend_n;
+        sl.pd.nt = c->pend_t;
     }
-    HIPCHK(c, launch_small_narrow(nv, d, d2, pd, p, dio + sl.vo, c->small_blocks.as<uint32_t>() + 16 * k,
-                                  (uint32_t *)(dio + sl.dn), sl.seq, s));
+    // busy before the lock is dropped: a window change waits for the slot
+    // (wait_small), so what the captured views point at stays as it is until
+    // the kernel finished
     sl.busy.store(true, std::memory_order_release);
     return k;
+}
+
+// The launch of slot k (prepared by small_launch), without c->mu.
+static hipError_t small_fire(hsc_ctx *c, int k)
+{
+    hsc_ctx::SmallSlot &sl = c->small[k];
+    if (sl.wait_ev) {
+        const hipError_t e = hipStreamWaitEvent(sl.stream, sl.wait_ev, 0);
+        if (e != hipSuccess) return e;
+    }
+    uint8_t *dio = (uint8_t *)sl.io.dp;
+    return launch_small_narrow(sl.nv, sl.d, sl.d2, sl.pd, sl.p, dio + sl.vo,
+                               c->small_blocks.as<uint32_t>() + 16 * k, (uint32_t *)(dio + sl.dn), sl.seq,
+                               sl.stream);
 }
 
 // Without c->mu: poll slot k's done word (every few thousand spins ask the
@@ -2828,9 +2864,14 @@ static int check_src(hsc_ctx *c, const Src &src, int *rc_out,
             c->sm_marshal_ns.fetch_add(
                 (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count(),
                 std::memory_order_relaxed);
-            c->sm_launch_ns.fetch_add(ns_since(t1), std::memory_order_relaxed);
             hipStream_t s = c->small[k].stream;
             if (lk) lk->unlock();
+            if (const hipError_t e = small_fire(c, k); e != hipSuccess) {
+                c->small[k].busy.store(false, std::memory_order_release);
+                if (lk) lk->lock();
+                return fail(c, HSC_EDEVICE, "small batch launch", e);
+            }
+            c->sm_launch_ns.fetch_add(ns_since(t1), std::memory_order_relaxed);  // slot + launch
             const char *why = nullptr;
             hipError_t herr = hipSuccess;
             rc = small_wait(c, k, s, rc_out, &why, &herr);
