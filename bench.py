@@ -840,6 +840,7 @@ def bench_multi(args):
             "routed_over_probes": st["routed"] / max(st["probes"], 1),
             "exchanged_bytes_per_step": off_diag * rec,
             "exchanged_rows_per_step": off_diag,
+            "host_phases_us": v.phase_stats(),
             "note": "counts[s][d]: probes member s routed to member d in the last batch; "
                     "off-diagonal rows crossed GPUs (RCCL) or were stored into another "
                     "member's columns",

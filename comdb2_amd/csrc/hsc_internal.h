@@ -644,15 +644,19 @@ struct RouteTarget {
 };
 struct RouteArgs {
     RouteTarget t[kMultiMax];
+    uint32_t base[kMultiMax];  // this source's first row in each target
     int N;
     uint32_t tbase;      // added to every read-set number (the batch-wide numbering)
     uint32_t lock_base;  // this source's first row in member 0's lock columns
 };
 // Received send blocks (RCCL): source s's block at byte boff[s], n[s] probes
-// and nl[s] locks; rows [roff[s], roff[s + 1]) / locks [loff[s], loff[s + 1]).
+// and nl[s] locks, numbered [roff[s], roff[s + 1]) / [loff[s], loff[s + 1])
+// over the received blocks; they land at target rows dst[s] + k / lock rows
+// ldst[s] + k (the receiver's own rows are stored there by its scatter).
 struct RouteUnpack {
     uint64_t boff[kMultiMax];
     uint32_t n[kMultiMax], nl[kMultiMax], roff[kMultiMax + 1], loff[kMultiMax + 1];
+    uint32_t dst[kMultiMax], ldst[kMultiMax];
     int N;
 };
 struct RouteParts {
@@ -665,8 +669,22 @@ __host__ __device__ inline size_t route_block_bytes(int W, size_t n, size_t nl)
     return 8 * (size_t)(2 * W + 2) * n + 16 * nl;
 }
 uint32_t route_blocks(size_t n);  // chunks (hist rows) of a routed batch
+// k_route_count's outputs (published by a one-workgroup k_route_total after
+// it).  ctl (device): ctl[N + 1, 2N + 1) the scatter's cursors, zeroed for it.
+// totals[0, N) = the counts, totals[N] = n_lock, totals[N + 1] = n_txn and,
+// when host is set (fine-grained pinned memory mapped for the device), the
+// same N + 2 words to host[] and then seq to host[N + 2] with a system-scope
+// release -- the host spins on that word instead of a copy and an event.
+struct RouteCountOut {
+    uint32_t *ctl, *totals, *host;
+    uint32_t seq, n_lock, n_txn;
+};
 hipError_t launch_route_count(const ProbeView &p, const RouteSplit &sp, int N, uint32_t *hist,
-                              uint32_t *totals, hipStream_t s);
+                              const RouteCountOut &o, hipStream_t s);
+// words u32 of src to host[0, words), then seq to host[words] (system scope)
+hipError_t launch_route_publish(const uint32_t *src, uint32_t words, uint32_t *host, uint32_t seq,
+                                hipStream_t s);
+// cursor: ctl + N + 1 of the count launch (zero)
 hipError_t launch_route_scatter(const ProbeView &p, const RouteSplit &sp, const RouteArgs &a,
                                 const uint32_t *hist, uint32_t *cursor, hipStream_t s);
 hipError_t launch_route_unpack(const uint8_t *raw, const RouteUnpack &u, const RouteTarget &t, int W,

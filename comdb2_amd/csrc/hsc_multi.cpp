@@ -24,7 +24,7 @@
 //      read sets numbered batch-wide, and packs its verdict bitmap;
 //   5. the bitmaps are OR-ed per read-set owner (k_or_slices over the
 //      members' bitmaps in one process; RCCL send / receive of each owner's
-//      slice + k_or_bitmaps across ranks).
+//      slice, then k_or_slices with the owner's own slice, across ranks).
 // A read set's verdict is the OR of its probes' verdicts and a member holding
 // none of a probe's keys cannot report a conflict for it, so the verdicts are
 // those of one context holding the whole window.
@@ -34,9 +34,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 
 namespace hsc {
+
+using SteadyClock = std::chrono::steady_clock;
 
 // ---- RCCL, resolved at run time ---------------------------------------------
 // librccl.so.1 is dlopen'ed on first use (the copy torch loaded, when it did),
@@ -96,13 +99,15 @@ struct MLane {
     hipStream_t stream = nullptr;
     DBuf src;             // API path: the member's share of the batch (StageLayout `srcL`)
     StageLayout srcL;
-    DBuf hist, totals, cursor;
+    DBuf hist, totals, ctl;  // ctl: the scatter's cursors (zeroed by k_route_total)
     DBuf send, raw;       // RCCL: send blocks / received blocks
     DBuf recv;            // the probe columns routed to this member (StageLayout `recvL`)
     StageLayout recvL;
     DBuf verdict, bitmap; // this member's probe outputs over the batch-wide read sets
     DBuf gather, out;     // owner merge (RCCL gather) / the merged bitmap (API path)
-    HBuf h_io;            // pinned: counts, cursors, the merged bitmap's download
+    HBuf h_io;            // pinned: the merged bitmap's download (API path)
+    HBuf h_cnt;           // fine-grained pinned: the counts the device publishes, + seq word
+    uint32_t seq = 0;
     hipEvent_t ev_count = nullptr, ev_scatter = nullptr, ev_probe = nullptr, ev_done = nullptr;
     bool used = false;    // ev_done recorded
 };
@@ -130,6 +135,9 @@ struct Multi {
     // host copies of the last pipeline's counts
     std::vector<uint32_t> cnt;   // [world][world + 2]: per source s: to each d, n_lock, n_txn
     uint64_t batches = 0, routed = 0, probes = 0;
+    // host phase split of run_pipeline (ns): waiting for the lane's previous
+    // batch, launching the counts, waiting for them, enqueueing the rest
+    uint64_t ns_lane = 0, ns_count = 0, ns_count_wait = 0, ns_enqueue = 0;
 };
 
 static int mfail(hsc_ctx *c, int code, const char *what, hipError_t e = hipSuccess)
@@ -446,15 +454,21 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
     Multi *M = f->multi;
     const int N = M->world, NL = M->nlocal, W = f->W;
     const int C = N + 2;
+    const auto t0 = SteadyClock::now();
     if (M->d_sp_W != W) MRC(upload_splitters(f, M, W));
     for (int m = 0; m < NL; ++m) {
         MRC(lane_stream(f, M, L, m));
         MLane &ml = M->lane[L][m];
         if (ml.used) MCHK(f, hipEventSynchronize(ml.ev_done));  // this lane's last batch
     }
+    const auto t1 = SteadyClock::now();
     Rccl &R = rccl();
-    // 1. counts per destination
+    // 1. counts per destination: the count kernel's last block (or, across
+    // ranks, a one-block copy after the all-gather) stores them to pinned host
+    // memory with a sequence word the host spins on -- no copy, no event wait
     M->cnt.assign((size_t)N * C, 0);
+    const bool gather = M->rccl && N > 1;
+    const size_t hw = gather ? (size_t)C * N : (size_t)C;  // words published
     for (int m = 0; m < NL; ++m) {
         MLane &ml = M->lane[L][m];
         hipStream_t s = ml.stream;
@@ -462,35 +476,42 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
         const uint32_t nb = std::max<uint32_t>(route_blocks(src[m].p.n), 1);
         MCHK(f, ml.hist.ensure(4 * (size_t)nb * N));
         MCHK(f, ml.totals.ensure(4 * (size_t)C * (N + 1)));
-        if (ml.h_io.ensure(4 * (size_t)C * N + 4 * (size_t)N + 256, true)) return mfail(f, HSC_ENOMEM, "multi staging");
-        uint32_t *h = ml.h_io.as<uint32_t>();
-        h[N] = src[m].p.n_lock;
-        h[N + 1] = src[m].n_txn;
-        MCHK(f, hipMemsetAsync(ml.totals.p, 0, 4 * (size_t)N, s));
-        MCHK(f, hipMemcpyAsync(ml.totals.as<uint32_t>() + N, h + N, 8, hipMemcpyHostToDevice, s));
-        MCHK(f, launch_route_count(src[m].p, split_view(M, m, W), N, ml.hist.as<uint32_t>(),
-                                   ml.totals.as<uint32_t>(), s));
-        if (M->rccl) {
+        if (!ml.ctl.p) {
+            MCHK(f, ml.ctl.ensure(4 * (2 * (size_t)kMultiMax + 2)));
+            MCHK(f, hipMemsetAsync(ml.ctl.p, 0, ml.ctl.bytes, s));
+        }
+        if (ml.h_cnt.ensure(4 * ((size_t)C * kMultiMax + 1), true, true))
+            return mfail(f, HSC_ENOMEM, "multi staging");
+        uint32_t *hd = (uint32_t *)ml.h_cnt.dp;
+        const RouteCountOut o{ml.ctl.as<uint32_t>(), ml.totals.as<uint32_t>(), gather ? nullptr : hd, ++ml.seq,
+                              src[m].p.n_lock, src[m].n_txn};
+        MCHK(f, launch_route_count(src[m].p, split_view(M, m, W), N, ml.hist.as<uint32_t>(), o, s));
+        if (gather) {
             uint32_t *mat = ml.totals.as<uint32_t>() + C;
             NCHK(f, R.AllGather(ml.totals.p, mat, C, ncclUint32, M->comm[L], s));
-            MCHK(f, hipMemcpyAsync(h, mat, 4 * (size_t)C * N, hipMemcpyDeviceToHost, s));
-        } else {
-            MCHK(f, hipMemcpyAsync(h, ml.totals.p, 4 * (size_t)N, hipMemcpyDeviceToHost, s));
+            MCHK(f, launch_route_publish(mat, (uint32_t)hw, hd, ml.seq, s));
         }
         MCHK(f, hipEventRecord(ml.ev_count, s));
     }
+    const auto t2 = SteadyClock::now();
     for (int m = 0; m < NL; ++m) {
         MLane &ml = M->lane[L][m];
-        MCHK(f, hipEventSynchronize(ml.ev_count));
-        const uint32_t *h = ml.h_io.as<uint32_t>();
-        if (M->rccl)
-            std::copy(h, h + (size_t)C * N, M->cnt.begin());
-        else {
-            std::copy(h, h + N, M->cnt.begin() + (size_t)(M->rank + m) * C);
-            M->cnt[(size_t)(M->rank + m) * C + N] = src[m].p.n_lock;
-            M->cnt[(size_t)(M->rank + m) * C + N + 1] = src[m].n_txn;
+        volatile const uint32_t *h = ml.h_cnt.as<uint32_t>();
+        for (uint32_t spin = 1; h[hw] != ml.seq; ++spin) {
+            __builtin_ia32_pause();
+            if ((spin & 4095) == 0) {  // a fault never publishes: ask the stream
+                const hipError_t e = hipEventQuery(ml.ev_count);
+                if (e == hipSuccess && h[hw] != ml.seq) return mfail(f, HSC_EDEVICE, "route counts not published");
+                if (e != hipSuccess && e != hipErrorNotReady) return mfail(f, HSC_EDEVICE, "route count", e);
+            }
         }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (gather)
+            for (size_t i = 0; i < (size_t)C * N; ++i) M->cnt[i] = h[i];
+        else
+            for (int i = 0; i < C; ++i) M->cnt[(size_t)(M->rank + m) * C + i] = h[i];
     }
+    const auto t3 = SteadyClock::now();
     auto cnt = [&](int s, int d) -> size_t { return M->cnt[(size_t)s * C + d]; };
     auto nlk = [&](int s) -> size_t { return M->cnt[(size_t)s * C + N]; };
     auto ntx = [&](int s) -> size_t { return M->cnt[(size_t)s * C + N + 1]; };
@@ -528,18 +549,26 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
         RouteArgs a{};
         a.N = N;
         a.tbase = (uint32_t)tbase[s];
-        uint32_t *hc = ml.h_io.as<uint32_t>() + (size_t)C * N;  // cursors (pinned)
+        uint32_t *hc = a.base;
         if (M->rccl) {
+            // one send block per other rank; this rank's own probes go straight
+            // into its probe columns, at the rows its unpack leaves for them
             size_t sb = 0;
-            for (int d = 0; d < N; ++d) sb += route_block_bytes(W, cnt(s, d), d == 0 ? nlk(s) : 0);
+            for (int d = 0; d < N; ++d)
+                if (d != s) sb += route_block_bytes(W, cnt(s, d), d == 0 ? nlk(s) : 0);
             MCHK(f, ml.send.ensure(std::max<size_t>(sb, 256)));
             size_t o = 0;
             for (int d = 0; d < N; ++d) {
+                if (d == s) {
+                    a.t[d] = arena_target(ml.recv.as<uint8_t>(), ml.recvL, nd[d]);
+                    hc[d] = (uint32_t)off[(size_t)s * N + d];
+                    continue;
+                }
                 a.t[d] = block_target(ml.send.as<uint8_t>() + o, W, cnt(s, d), d == 0 ? nlk(s) : 0);
                 o += route_block_bytes(W, cnt(s, d), d == 0 ? nlk(s) : 0);
                 hc[d] = 0;
             }
-            a.lock_base = 0;
+            a.lock_base = 0;  // rank 0's own locks first in its lock columns, else a block's
         } else {
             for (int d = 0; d < N; ++d) {
                 MLane &dl = M->lane[L][d];
@@ -548,10 +577,8 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
             }
             a.lock_base = (uint32_t)lbase[s];
         }
-        MCHK(f, ml.cursor.ensure(4 * (size_t)N));
-        MCHK(f, hipMemcpyAsync(ml.cursor.p, hc, 4 * (size_t)N, hipMemcpyHostToDevice, st));
         MCHK(f, launch_route_scatter(src[m].p, split_view(M, m, W), a, ml.hist.as<uint32_t>(),
-                                     ml.cursor.as<uint32_t>(), st));
+                                     ml.ctl.as<uint32_t>() + N + 1, st));
         MCHK(f, hipEventRecord(ml.ev_scatter, st));
     }
     // 5. exchange
@@ -564,27 +591,32 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
         size_t rb = 0;
         for (int s = 0; s < N; ++s) {
             u.boff[s] = rb;
-            u.n[s] = (uint32_t)cnt(s, me);
-            u.nl[s] = me == 0 ? (uint32_t)nlk(s) : 0;
+            u.n[s] = s == me ? 0 : (uint32_t)cnt(s, me);
+            u.nl[s] = me == 0 && s != me ? (uint32_t)nlk(s) : 0;
+            u.dst[s] = (uint32_t)off[(size_t)s * N + me];
+            u.ldst[s] = (uint32_t)lbase[s];
             u.roff[s + 1] = u.roff[s] + u.n[s];
             u.loff[s + 1] = u.loff[s] + u.nl[s];
             rb += route_block_bytes(W, u.n[s], u.nl[s]);
         }
-        MCHK(f, ml.raw.ensure(std::max<size_t>(rb, 256)));
-        NCHK(f, R.GroupStart());
-        size_t o = 0;
-        for (int d = 0; d < N; ++d) {
-            const size_t b = route_block_bytes(W, cnt(me, d), d == 0 ? nlk(me) : 0);
-            if (b) NCHK(f, R.Send(ml.send.as<uint8_t>() + o, b, ncclUint8, d, M->comm[L], st));
-            o += b;
+        if (N > 1) {
+            MCHK(f, ml.raw.ensure(std::max<size_t>(rb, 256)));
+            NCHK(f, R.GroupStart());
+            size_t o = 0;
+            for (int d = 0; d < N; ++d) {
+                if (d == me) continue;
+                const size_t b = route_block_bytes(W, cnt(me, d), d == 0 ? nlk(me) : 0);
+                if (b) NCHK(f, R.Send(ml.send.as<uint8_t>() + o, b, ncclUint8, d, M->comm[L], st));
+                o += b;
+            }
+            for (int s = 0; s < N; ++s) {
+                const size_t b = route_block_bytes(W, u.n[s], u.nl[s]);
+                if (b) NCHK(f, R.Recv(ml.raw.as<uint8_t>() + u.boff[s], b, ncclUint8, s, M->comm[L], st));
+            }
+            NCHK(f, R.GroupEnd());
+            MCHK(f, launch_route_unpack(ml.raw.as<uint8_t>(), u,
+                                        arena_target(ml.recv.as<uint8_t>(), ml.recvL, nd[me]), W, st));
         }
-        for (int s = 0; s < N; ++s) {
-            const size_t b = route_block_bytes(W, u.n[s], u.nl[s]);
-            if (b) NCHK(f, R.Recv(ml.raw.as<uint8_t>() + u.boff[s], b, ncclUint8, s, M->comm[L], st));
-        }
-        NCHK(f, R.GroupEnd());
-        MCHK(f, launch_route_unpack(ml.raw.as<uint8_t>(), u,
-                                    arena_target(ml.recv.as<uint8_t>(), ml.recvL, nd[me]), W, st));
     } else {
         for (int d = 0; d < NL; ++d)
             for (int s = 0; s < NL; ++s)
@@ -627,15 +659,27 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
         const int me = M->rank;
         hipStream_t st = ml.stream;
         const size_t wme = ow(me);
+        // the other ranks' verdicts on this rank's read sets, OR-ed with its own
         MCHK(f, ml.gather.ensure(8 * std::max<size_t>(wme * N, 1)));
-        NCHK(f, R.GroupStart());
-        for (int o = 0; o < N; ++o)
-            if (ow(o)) NCHK(f, R.Send(ml.bitmap.as<uint64_t>() + ob(o), 8 * ow(o), ncclUint8, o, M->comm[L], st));
-        if (wme)
+        if (N > 1) {
+            NCHK(f, R.GroupStart());
+            for (int o = 0; o < N; ++o)
+                if (o != me && ow(o))
+                    NCHK(f, R.Send(ml.bitmap.as<uint64_t>() + ob(o), 8 * ow(o), ncclUint8, o, M->comm[L], st));
+            if (wme)
+                for (int d = 0; d < N; ++d)
+                    if (d != me)
+                        NCHK(f, R.Recv(ml.gather.as<uint64_t>() + (size_t)d * wme, 8 * wme, ncclUint8, d,
+                                       M->comm[L], st));
+            NCHK(f, R.GroupEnd());
+        }
+        if (src[0].out && wme) {
+            RouteParts parts{};
+            parts.n = N;
             for (int d = 0; d < N; ++d)
-                NCHK(f, R.Recv(ml.gather.as<uint64_t>() + (size_t)d * wme, 8 * wme, ncclUint8, d, M->comm[L], st));
-        NCHK(f, R.GroupEnd());
-        if (src[0].out && wme) MCHK(f, launch_or_bitmaps(ml.gather.as<uint64_t>(), N, wme, src[0].out, st));
+                parts.p[d] = d == me ? ml.bitmap.as<uint64_t>() + ob(me) : ml.gather.as<uint64_t>() + (size_t)d * wme;
+            MCHK(f, launch_or_slices(parts, wme, src[0].out, st));
+        }
         MCHK(f, hipEventRecord(ml.ev_done, st));
         ml.used = true;
     } else {
@@ -663,6 +707,14 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
         }
     }
     M->batches++;
+    const auto t4 = SteadyClock::now();
+    auto ns = [](SteadyClock::time_point a, SteadyClock::time_point b) {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
+    };
+    M->ns_lane += ns(t0, t1);
+    M->ns_count += ns(t1, t2);
+    M->ns_count_wait += ns(t2, t3);
+    M->ns_enqueue += ns(t3, t4);
     for (int d = 0; d < N; ++d) M->routed += nd[d];
     for (int m = 0; m < NL; ++m) M->probes += src[m].p.n;
     return HSC_OK;
@@ -722,11 +774,8 @@ int multi_check_stage(hsc_ctx *f, Stage &st, int *rc_out)
     MCHK(f, o.out.ensure(8 * std::max<size_t>(words, 1)));
     src[0].out = o.out.as<uint64_t>();
     MRC(run_pipeline(f, L, src, !M->rccl));
-    if (o.h_io.ensure(4 * (size_t)(M->world + 2) * M->world + 4 * (size_t)M->world + 256 + 8 * words, true))
-        return mfail(f, HSC_ENOMEM, "multi staging");
-    uint64_t *hb = (uint64_t *)(o.h_io.as<uint8_t>() + 4 * (size_t)(M->world + 2) * M->world +
-                                4 * (size_t)M->world + 64);
-    hb = (uint64_t *)(((uintptr_t)hb + 63) & ~(uintptr_t)63);
+    if (o.h_io.ensure(8 * words + 64, true)) return mfail(f, HSC_ENOMEM, "multi staging");
+    uint64_t *hb = o.h_io.as<uint64_t>();
     if (words) MCHK(f, hipMemcpyAsync(hb, o.out.p, 8 * words, hipMemcpyDeviceToHost, o.stream));
     MCHK(f, hipStreamSynchronize(o.stream));
     for (int m = 1; m < NL; ++m) MCHK(f, hipEventSynchronize(M->lane[L][m].ev_done));
@@ -745,10 +794,11 @@ void multi_destroy(hsc_ctx *f)
             if (!ml.stream) continue;
             (void)hipSetDevice(M->mem[m]->device);
             (void)hipStreamSynchronize(ml.stream);
-            for (DBuf *b : {&ml.src, &ml.hist, &ml.totals, &ml.cursor, &ml.send, &ml.raw, &ml.recv,
+            for (DBuf *b : {&ml.src, &ml.hist, &ml.totals, &ml.ctl, &ml.send, &ml.raw, &ml.recv,
                             &ml.verdict, &ml.bitmap, &ml.gather, &ml.out})
                 b->release();
             ml.h_io.release();
+            ml.h_cnt.release();
             for (hipEvent_t e : {ml.ev_count, ml.ev_scatter, ml.ev_probe, ml.ev_done})
                 if (e) (void)hipEventDestroy(e);
             (void)hipStreamDestroy(ml.stream);
@@ -975,6 +1025,19 @@ int hsc_multi_stats(hsc_ctx *f, uint64_t out[4])
     out[1] = M->probes;
     out[2] = M->routed;
     out[3] = M->nlocal;
+    return HSC_OK;
+}
+
+int hsc_multi_phase_stats(hsc_ctx *f, double out[5])
+{
+    if (!f || !f->multi || !out) return HSC_EINVAL;
+    Multi *M = f->multi;
+    const double b = (double)std::max<uint64_t>(M->batches, 1) * 1e3;
+    out[0] = (double)M->batches;
+    out[1] = (double)M->ns_lane / b;
+    out[2] = (double)M->ns_count / b;
+    out[3] = (double)M->ns_count_wait / b;
+    out[4] = (double)M->ns_enqueue / b;
     return HSC_OK;
 }
 

@@ -159,6 +159,7 @@ EXPORTS = [
     "hsc_multi_create", "hsc_multi_unique_ids", "hsc_multi_create_rank", "hsc_multi_world",
     "hsc_multi_rank", "hsc_multi_local", "hsc_multi_member", "hsc_multi_set_splitters",
     "hsc_multi_adopt", "hsc_multi_probe_device", "hsc_multi_stats", "hsc_multi_last_counts",
+    "hsc_multi_phase_stats",
     "hsc_marshal_arrs", "hsc_batch_stats",
 ]
 MULTI_ID_BYTES = 2 * 128  # hsc_multi_unique_ids: one RCCL id per lane
@@ -274,6 +275,7 @@ def load() -> C.CDLL:
         "hsc_multi_probe_device": (C.c_int, [_p, _p, C.c_int]),
         "hsc_multi_stats": (C.c_int, [_p, _p]),
         "hsc_multi_last_counts": (C.c_int, [_p, _p, C.c_int]),
+        "hsc_multi_phase_stats": (C.c_int, [_p, _p]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("HSC_LIB"):
@@ -1051,6 +1053,13 @@ class MultiValidator(Validator):
         self._chk(self.lib.hsc_multi_stats(self.ctx, out.ctypes.data), "hsc_multi_stats")
         return {"batches": int(out[0]), "probes": int(out[1]), "routed": int(out[2]),
                 "local_members": int(out[3])}
+
+    def phase_stats(self) -> dict:
+        """Host time per routed batch, mean us (hsc_multi_phase_stats)."""
+        out = np.zeros(5, np.float64)
+        self._chk(self.lib.hsc_multi_phase_stats(self.ctx, out.ctypes.data), "hsc_multi_phase_stats")
+        return {"batches": int(out[0]), "lane_wait_us": float(out[1]), "count_launch_us": float(out[2]),
+                "count_wait_us": float(out[3]), "enqueue_us": float(out[4])}
 
     def last_counts(self) -> np.ndarray:
         n = self.world

@@ -595,6 +595,10 @@ int hsc_multi_probe_device(hsc_ctx *ctx, const hsc_probe_batch *b, int lane);
 int hsc_multi_stats(hsc_ctx *ctx, uint64_t out[4]);
 /* counts[s * world + d]: probes member s sent member d in the last batch. */
 int hsc_multi_last_counts(hsc_ctx *ctx, uint32_t *counts, int n);
+/* Host time per routed batch (diagnostics): out[0] batches, then mean us
+ * waiting for the lane's previous batch, launching the route counts, waiting
+ * for the counts the device publishes, enqueueing the rest of the batch. */
+int hsc_multi_phase_stats(hsc_ctx *ctx, double out[5]);
 
 /* ---- OSQL_SERIAL wire path --------------------------------------------
  * Decode only: *out points at context-owned read sets, valid until the next
