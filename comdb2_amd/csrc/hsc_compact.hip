@@ -385,7 +385,7 @@ template <int WC>
 __global__ __launch_bounds__(kCsUdThreads) void k_cs_unpack_dd(
     const uint64_t *keys, size_t n, CompactMeta cm, const uint64_t *lsn_in, uint32_t *gid_o,
     uint64_t *words_o, uint64_t *lsn_o, size_t stride_o, const uint32_t *boff, uint32_t *gid_d,
-    uint64_t *words_d, uint64_t *lsn_d, size_t stride_d, uint32_t *d_count, bool lds)
+    uint64_t *words_d, uint64_t *lsn_d, size_t stride_d, uint32_t *d_count, uint64_t *codes_d, bool lds)
 {
     constexpr int KW = WC + 1;
     extern __shared__ __attribute__((aligned(16))) uint64_t tl[];
@@ -442,7 +442,12 @@ __global__ __launch_bounds__(kCsUdThreads) void k_cs_unpack_dd(
         const bool last = d != 0xFFFFFFFFu;
         lsn_o[i] = lv;
         gid_o[i] = g;
-        if (last) lsn_d[b0 + d] = lv, gid_d[b0 + d] = g;
+        if (last) {
+            lsn_d[b0 + d] = lv, gid_d[b0 + d] = g;
+            if (codes_d)  // the compact tiles' row codes (k_compact_rows of these rows)
+#pragma unroll
+                for (int m = 0; m < WC; ++m) codes_d[(size_t)m * stride_d + b0 + d] = c[m];
+        }
         const uint64_t *mk = cm.mask + (size_t)g * cm.W, *pt = cm.pat + (size_t)g * cm.W;
         const uint64_t *mv = cm.mv + (size_t)g * cm.W * 6;
         int p = 0;
@@ -464,7 +469,7 @@ hipError_t compact_unpack_dedupe(const uint64_t *keys, size_t n, const CompactTa
                                  const uint64_t *lsn_in, uint32_t *gid_o, uint64_t *words_o,
                                  uint64_t *lsn_o, size_t stride_o, uint32_t *gid_d, uint64_t *words_d,
                                  uint64_t *lsn_d, size_t stride_d, uint32_t *d_count, uint32_t *scratch,
-                                 hipStream_t s)
+                                 uint64_t *codes_d, hipStream_t s)
 {
     if (n == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
     const CompactMeta cm = meta_of(t);
@@ -484,7 +489,7 @@ hipError_t compact_unpack_dedupe(const uint64_t *keys, size_t n, const CompactTa
 #define HSC_CS_UD(WC_)                                                            \
     k_cs_unpack_dd<WC_><<<ud, kCsUdThreads, lds ? tb : 0, s>>>(keys, n, cm, lsn_in, gid_o, words_o, \
                                                                lsn_o, stride_o, bc, gid_d, words_d, \
-                                                               lsn_d, stride_d, d_count, lds)
+                                                               lsn_d, stride_d, d_count, codes_d, lds)
     if (t.WC == 1)
         HSC_CS_UD(1);
     else if (t.WC == 2)

@@ -496,6 +496,7 @@ struct hsc_ctx {
     // varying bits fit 3 words)
     DBuf d_csrep, d_csmask, d_cspat, d_csmv, d_csbits, d_cskeys[2];
     bool code_sorted = false;  // the last build sorted by compact codes
+    int cs_codes_wc = 0;       // its unpack wrote the distinct rows' codes (d_cwords) of this width
     std::vector<uint64_t> cs_mask;     // its varying bits per (group, word) (host copy)
     std::vector<uint8_t> cs_has_rows;  // its groups with rows
     std::vector<uint32_t> cs_bits_h;   // host sources of its table uploads

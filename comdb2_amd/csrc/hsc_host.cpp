@@ -395,7 +395,8 @@ static int build_compact(hsc_ctx *c, const WinView &w)
     c->ct.WC = WC;
     c->ct.ng = ng;
     HIPCHK(c, c->d_cwords.ensure(8 * (size_t)WC * c->cap));
-    HIPCHK(c, compact_rows(w.words, w.stride, w.gid, w.n, c->ct, c->d_cwords.as<uint64_t>(), s));
+    if (!(c->code_sorted && c->cs_codes_wc == WC))  // (the code sort's unpack wrote them)
+        HIPCHK(c, compact_rows(w.words, w.stride, w.gid, w.n, c->ct, c->d_cwords.as<uint64_t>(), s));
     WinView &v = c->wc;
     v = w;
     v.words = c->d_cwords.as<uint64_t>();
@@ -604,12 +605,21 @@ static int code_sort(hsc_ctx *c, size_t n_in, bool *done)
     // d_words (the unpack reads only the input LSNs) and the free key
     // buffer, which becomes d_lsn
     DBuf &kfree = sorted == c->d_cskeys[0].as<uint64_t>() ? c->d_cskeys[1] : c->d_cskeys[0];
+    // the distinct rows' codes are the compact tiles' row codes (build_compact
+    // uses the same masks and width): written here, not recomputed from the
+    // unpacked words
+    uint64_t *codes = nullptr;
+    if (WC < W) {
+        HIPCHK(c, c->d_cwords.ensure(8 * (size_t)WC * c->cap));
+        codes = c->d_cwords.as<uint64_t>();
+    }
     HIPCHK(c, compact_unpack_dedupe(sorted, n_in, t, c->d_lsn.as<uint64_t>(), c->d_gid2.as<uint32_t>(),
                                     c->d_words2.as<uint64_t>(), c->d_lsn2.as<uint64_t>(), c->cap,
                                     c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(),
                                     kfree.as<uint64_t>(), c->cap, c->d_count.as<uint32_t>(),
-                                    c->d_scratch.as<uint32_t>(), s));
+                                    c->d_scratch.as<uint32_t>(), codes, s));
     std::swap(c->d_lsn, kfree);
+    c->cs_codes_wc = codes ? WC : 0;
     *done = true;
     return HSC_OK;
 }
@@ -659,6 +669,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
     c->packed_sort = try_packed && packed_plan(W, n_in, vary, &plan);
     // too many varying bits for the packed sort: by compact codes if they fit
     bool code_sorted = false;
+    c->cs_codes_wc = 0;
     if (!c->packed_sort && try_packed) HIPCHK_RC(c, code_sort(c, n_in, &code_sorted));
     c->code_sorted = code_sorted;
     if (c->packed_sort) {
@@ -2680,7 +2691,8 @@ static bool small_path(hsc_ctx *c, int T)
     // a layout forced to the tile or code pipeline (tests, A/B) keeps it
     const bool direct_ok = c->layout == HSC_LAYOUT_AUTO || c->layout == HSC_LAYOUT_NARROW ||
                            c->layout == HSC_LAYOUT_NARROW_DIRECT;
-    return !c->no_small && c->narrow && direct_ok && !c->timing && T <= kSmallMaxTxns && c->n > 0;
+    return !c->no_small && c->narrow && direct_ok && !c->timing && T <= kSmallMaxTxns && c->n > 0 &&
+           c->nv.levels <= kSmallMaxLevels;
 }
 
 using SteadyClock = std::chrono::steady_clock;
@@ -2737,7 +2749,7 @@ static int small_launch(hsc_ctx *c, Stage &st)
     uint8_t *io = sl.io.as<uint8_t>(), *dio = (uint8_t *)sl.io.dp;
     memset(io + sl.vo, 0, st.n_txn);
     sl.forced.assign(st.forced.as<uint8_t>(), st.forced.as<uint8_t>() + st.n_txn);
-    volatile uint32_t *done = (volatile uint32_t *)(io + sl.dn);
+    volatile uint64_t *done = (volatile uint64_t *)(io + sl.dn);
     if (++c->small_seq == 0) c->small_seq = 1;
     sl.seq = c->small_seq;
     *done = 0;
@@ -2785,8 +2797,8 @@ static hipError_t small_fire(hsc_ctx *c, int k)
     }
     uint8_t *dio = (uint8_t *)sl.io.dp;
     return launch_small_narrow(sl.nv, sl.d, sl.d2, sl.pd, sl.p, dio + sl.vo,
-                               c->small_blocks.as<uint32_t>() + 16 * k, (uint32_t *)(dio + sl.dn), sl.seq,
-                               sl.stream);
+                               c->small_blocks.as<uint32_t>() + 16 * k, (uint64_t *)(dio + sl.dn), sl.seq,
+                               sl.n_txn <= kSmallPackTxns, sl.stream);
 }
 
 // Without c->mu: poll slot k's done word (every few thousand spins ask the
@@ -2798,12 +2810,12 @@ static int small_wait(hsc_ctx *c, int k, hipStream_t s, int *rc_out, const char 
 {
     hsc_ctx::SmallSlot &sl = c->small[k];
     const uint8_t *io = sl.io.as<uint8_t>();
-    volatile const uint32_t *done = (volatile const uint32_t *)(io + sl.dn);
+    volatile const uint64_t *done = (volatile const uint64_t *)(io + sl.dn);
     const uint32_t seq = sl.seq;
     const auto t0 = SteadyClock::now();
     int rc = HSC_OK;
     bool running = false;  // timed out: the kernel may still write the slot
-    for (uint32_t spin = 1; *done != seq; ++spin) {
+    for (uint32_t spin = 1; (uint32_t)(*done >> 32) != seq; ++spin) {
         __builtin_ia32_pause();
         if ((spin & 4095) == 0) {
             if (SteadyClock::now() - t0 > std::chrono::seconds(30)) {
@@ -2813,7 +2825,8 @@ static int small_wait(hsc_ctx *c, int k, hipStream_t s, int *rc_out, const char 
             }
             const hipError_t e = hipStreamQuery(s);
             if (e == hipSuccess) {
-                if (*done != seq) rc = HSC_EDEVICE, *why = "small batch finished without its done word";
+                if ((uint32_t)(*done >> 32) != seq)
+                    rc = HSC_EDEVICE, *why = "small batch finished without its done word";
                 break;
             }
             if (e != hipErrorNotReady) {
@@ -2824,8 +2837,13 @@ static int small_wait(hsc_ctx *c, int k, hipStream_t s, int *rc_out, const char 
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     if (rc == HSC_OK) {
-        const uint8_t *v = io + sl.vo;
-        for (size_t t = 0; t < sl.n_txn; ++t) rc_out[t] = (sl.forced[t] | v[t]) ? 1 : 0;
+        const uint32_t low = (uint32_t)*done;
+        if (low & kSmallPacked) {  // one block: the verdict bits came with the done word
+            for (size_t t = 0; t < sl.n_txn; ++t) rc_out[t] = (sl.forced[t] || ((low >> t) & 1)) ? 1 : 0;
+        } else {
+            const uint8_t *v = io + sl.vo;
+            for (size_t t = 0; t < sl.n_txn; ++t) rc_out[t] = (sl.forced[t] | v[t]) ? 1 : 0;
+        }
     }
     // a slot whose kernel may still write it stays taken
     if (!running) sl.busy.store(false, std::memory_order_release);

@@ -255,10 +255,15 @@ struct PendView {
     const uint8_t *base;  // device address of the buffer (nullptr: none)
     uint32_t n, nt;       // rows, table entries
 };
+constexpr int kSmallMaxLevels = 8;  // key-tree levels k_small_narrow descends (16^8 = 2^32 rows)
+// The done word: seq << 32, and with `pack` (at most kSmallPackTxns read sets)
+// on a one-block grid the verdicts too: bit 31 set and bit t = read set t's
+// verdict (no verdict bytes written: one store ends the call).
+constexpr uint32_t kSmallPackTxns = 31, kSmallPacked = 1u << 31;
 hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const DeltaView &d2,
                                const PendView &pd, const ProbeView &p,
-                               uint8_t *verdict, uint32_t *blocks_done, uint32_t *done,
-                               uint32_t seq, hipStream_t s);
+                               uint8_t *verdict, uint32_t *blocks_done, uint64_t *done,
+                               uint32_t seq, bool pack, hipStream_t s);
 // 16-ary directory over a sorted u64 array A (hsc_narrow.hip): level 0 = A
 // padded with ~0 to a multiple of 16, level l+1 [i] = level l [16 i + 15]
 // (the last entry of every 16-entry block), up to one block; levels >=
@@ -499,13 +504,14 @@ hipError_t code_keys_sort(uint64_t *keys, uint64_t *tmp, size_t n, int KW, hipSt
                           uint64_t **sorted);
 // sorted keys back to rows, with the dedupe fused in: every version to *_o, the last of
 // each key to *_d (which may be the input gid / words -- only lsn_in is read
-// by index), d_count[0] = distinct rows; scratch >= n / 2048 + 16 +
+// by index), d_count[0] = distinct rows, and (codes_d set) the distinct rows'
+// codes as [WC][stride_d] (what compact_rows computes); scratch >= n / 2048 + 16 +
 // scan_scratch_bytes(n / 2048 + 1) / 4 words
 hipError_t compact_unpack_dedupe(const uint64_t *keys, size_t n, const CompactTables &t,
                                  const uint64_t *lsn_in, uint32_t *gid_o, uint64_t *words_o,
                                  uint64_t *lsn_o, size_t stride_o, uint32_t *gid_d, uint64_t *words_d,
                                  uint64_t *lsn_d, size_t stride_d, uint32_t *d_count, uint32_t *scratch,
-                                 hipStream_t s);
+                                 uint64_t *codes_d, hipStream_t s);
 hipError_t warm_csort();
 // lo/hi bounds (W words) -> code bounds (WC words, SoA [WC][n]); ranges that
 // miss their group's rows become (~0, 0)

@@ -367,6 +367,145 @@ __global__ __launch_bounds__(kProbeThreads) void k_probe_narrow(NarrowView nv, P
 // last block's count.
 constexpr int kSmallThreads = 256;
 
+// The small batches' range search, latency first: one range per 16-lane group
+// (a lone call's ten ranges fill ten groups at once).  Lane 0 maps lo, lane 1
+// hi.  The key tree is descended two levels per dependent step: the 256
+// entries of level l - 1 under one entry of level l + 1 are contiguous (16 per
+// lane, 2 KiB per group), so their count below the bound skips level l.  The
+// range maximum needs no dependent chain at all: the partial blocks of every
+// level follow from pa, pb by arithmetic, so kSmallRound levels' loads are
+// issued together.
+constexpr int kSmallRound = 4;
+constexpr int kSmallLevels = kSmallMaxLevels;  // the host keeps deeper windows off this path
+static_assert(kSmallLevels <= kMaxLevels, "level offsets");
+
+__device__ __forceinline__ uint32_t group_sum16(uint32_t v)
+{
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 1, 64);
+    return v;
+}
+
+// #entries of the 16 at e (a lane's run of a level) below x (LE: <= x); none
+// when the run starts at or past the level's end
+template <bool LE>
+__device__ __forceinline__ uint32_t run_below(const uint64_t *e, bool in, uint64_t x)
+{
+    if (!in) return 0;
+    uint32_t n = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i += 2) {
+        const ulonglong2 v = *(const ulonglong2 *)(e + i);
+        n += LE ? (v.x <= x) + (v.y <= x) : (v.x < x) + (v.y < x);
+    }
+    return n;
+}
+
+// KW = 1, 2: the bound's words loaded together into registers (they live in
+// host memory: one PCIe round trip, not one per word) and mapped by
+// rel_diff_w; KW = 0: any width through rel_diff
+// a small batch's conflict mark: the verdict byte (system-scope store), or
+// with vmask (a packed one-block batch) the read set's bit in LDS
+__device__ __forceinline__ void small_mark(uint8_t *verdict, uint32_t *vmask, uint32_t txn)
+{
+    if (vmask)
+        atomicOr(vmask, 1u << txn);
+    else
+        mark_verdict<true>(verdict + txn);
+}
+
+template <int KW>
+__device__ __forceinline__ void narrow_small_ranges(const NarrowView &nv, const ProbeView &p,
+                                                    uint8_t *verdict, uint32_t *vmask, uint32_t wave0,
+                                                    uint32_t wstride)
+{
+    const int lane = threadIdx.x & 63, sub = lane >> 4, l16 = lane & 15, g0 = lane & 48;
+    const size_t ks = p.n;
+    for (uint32_t wbase = wave0; wbase < p.n; wbase += wstride) {
+        const uint32_t q = wbase + sub;
+        const bool act = q < p.n;
+        uint64_t xv = 0, sn = 0;
+        uint32_t tx = 0;
+        int ok = 0;
+        if (act && l16 < 2) {
+            uint64_t v;
+            bool rem;
+            const uint64_t *xp = l16 ? p.hi + q : p.lo + q;
+            if constexpr (KW > 0) {
+                const uint32_t g = p.gid[q];
+                uint64_t xw[KW];
+#pragma unroll
+                for (int j = 0; j < KW; ++j) xw[j] = xp[(size_t)j * ks];
+                ok = rel_diff_w<KW>(nv.lw, nv.tz, g, xw, nv.base[0], nv.base + 1, kSat, v, rem);
+            } else {
+                ok = rel_diff(nv.W, nv.lw, nv.tz, p.gid[q], xp, ks, nv.base[0], nv.base + 1, 1, kSat, v,
+                              rem);
+            }
+            // lower bound: ceil((lo - K0) >> s), 0 below the window; upper:
+            // floor((hi - K0) >> s), none below the window
+            xv = !ok ? 0 : l16 ? v : (v >= kSat ? kSat : v + (rem ? 1 : 0));
+        } else if (act && l16 == 2) {
+            sn = p.snap[q];
+            tx = p.txn[q];
+        }
+        const uint64_t xlo = __shfl(xv, g0, 64), xhi = __shfl(xv, g0 + 1, 64);
+        const bool live = act && __shfl(ok, g0 + 1, 64) != 0;
+        const uint64_t snap = __shfl(sn, g0 + 2, 64);
+        const uint32_t txn = __shfl(tx, g0 + 2, 64);
+        // ca / cb: the block index at level l (the count below the bound at
+        // l + 1).  Levels are compile-time indices (a window of < 2^32 rows
+        // has at most kSmallLevels): every level's offset is a kernel-argument
+        // load the prologue issues at once, not one per step.
+        uint32_t ca = 0, cb = 0;
+        const int top = nv.levels - 1;
+#pragma unroll
+        for (int l = kSmallLevels - 1; l >= 1; --l) {
+            if (l > top || ((top - l) & 1)) continue;  // uniform
+            const uint64_t *lv = nv.keys + nv.off[l - 1];
+            const size_t len = nv.len[l - 1];
+            const size_t ia = 256 * (size_t)ca + 16 * l16, ib = 256 * (size_t)cb + 16 * l16;
+            const uint32_t na = run_below<false>(lv + ia, ia < len, xlo);
+            const uint32_t nb = run_below<true>(lv + ib, ib < len, xhi);
+            ca = 256 * ca + group_sum16(na);
+            cb = 256 * cb + group_sum16(nb);
+        }
+        if ((top & 1) == 0) {  // level 0 left: a 16-ary step
+            const uint64_t *lv = nv.keys;
+            const bool ba = lv[16 * (size_t)ca + l16] < xlo, bb = lv[16 * (size_t)cb + l16] <= xhi;
+            ca = 16 * ca + __popc((uint32_t)(__ballot(ba) >> (16 * sub)) & 0xFFFFu);
+            cb = 16 * cb + __popc((uint32_t)(__ballot(bb) >> (16 * sub)) & 0xFFFFu);
+        }
+        // any lsn > snapshot over rows [P, Q): level L's partial blocks
+        uint32_t P = ca, Q = live ? cb : 0;
+        bool on = act && P < Q, found = false;
+#pragma unroll
+        for (int lev = 0; lev < kSmallLevels; lev += kSmallRound) {
+            if (!__any(on)) break;
+            uint64_t vl[kSmallRound], vr[kSmallRound];
+#pragma unroll
+            for (int r = 0; r < kSmallRound; ++r) {
+                const int L = lev + r;
+                const bool a = on && L < nv.levels;
+                const uint64_t *lv = nv.maxs + nv.off[L];
+                const uint32_t il = (P & ~15u) + l16, ir = ((Q - 1) & ~15u) + l16;
+                vl[r] = a && il >= P && il < Q ? lv[il] : 0;
+                vr[r] = a && ir >= P && ir < Q ? lv[ir] : 0;
+                const uint32_t np = (P + 15) >> 4, nq = Q >> 4;
+                on = a && (P >> 4) != ((Q - 1) >> 4) && np < nq;
+                P = np, Q = nq;
+            }
+            bool hit = false;
+#pragma unroll
+            for (int r = 0; r < kSmallRound; ++r) hit |= vl[r] > snap || vr[r] > snap;
+            found |= ((uint32_t)(__ballot(hit) >> (16 * sub)) & 0xFFFFu) != 0;
+            on = on && !found;
+        }
+        if (act && found && l16 == 0) small_mark(verdict, vmask, txn);
+    }
+}
+
 // ---- the appended rows: delta runs and the pending tail --------------------
 // Keys as full composites (gid, W words) held in registers, W <= kPendMaxWords.
 
@@ -534,19 +673,33 @@ __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, D
                                                                 DeltaView d2, PendView pd,
                                                                 ProbeView p, uint8_t *verdict,
                                                                 uint32_t *blocks_done,
-                                                                uint32_t *done, uint32_t seq)
+                                                                uint64_t *done, uint32_t seq, uint32_t pack)
 {
     // with appended rows not in the window, the second half of the grid
     // searches them while the first half searches the window (both dependent
     // load chains run side by side instead of one after the other)
     const bool split = d.n || d2.n || pd.n || pd.nt;
     const uint32_t half = split ? gridDim.x / 2 : gridDim.x;
+    __shared__ uint32_t vbits;
+    const bool packed = pack && gridDim.x == 1;  // (split grids have two blocks at least)
+    if (packed) {
+        if (threadIdx.x == 0) vbits = 0;
+        __syncthreads();
+    }
+    uint32_t *vmask = packed ? &vbits : nullptr;
     if (blockIdx.x < half) {
         const uint32_t groups = half * (kSmallThreads / 16);
-        const uint32_t wave0 = (blockIdx.x * (kSmallThreads / 16) + ((threadIdx.x >> 6) << 2)) * kNP;
-        narrow_probe_ranges<true>(nv, p, verdict, nullptr, 0, nv.levels, wave0, groups * kNP);
-        const uint32_t tid = blockIdx.x * kSmallThreads + threadIdx.x, nth = half * kSmallThreads;
-        narrow_probe_locks<true>(nv, p, verdict, tid, nth);
+        const uint32_t wave0 = blockIdx.x * (kSmallThreads / 16) + ((threadIdx.x >> 6) << 2);
+        if (nv.W == 2)
+            narrow_small_ranges<2>(nv, p, verdict, vmask, wave0, groups);
+        else if (nv.W == 1)
+            narrow_small_ranges<1>(nv, p, verdict, vmask, wave0, groups);
+        else
+            narrow_small_ranges<0>(nv, p, verdict, vmask, wave0, groups);
+        for (uint32_t q = blockIdx.x * kSmallThreads + threadIdx.x; q < p.n_lock; q += half * kSmallThreads) {
+            const uint32_t t = p.lock_table[q];
+            if (t < nv.ntables && nv.table_max[t] > p.lock_snap[q]) small_mark(verdict, vmask, p.lock_txn[q]);
+        }
     } else if constexpr (WD > 0) {
         small_appended16<WD>(d, d2, pd, p, verdict, blockIdx.x - half, gridDim.x - half);
     } else {  // the live run and a frozen one (background fold)
@@ -559,23 +712,26 @@ __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, D
     __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's verdict stores are done
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (__hip_atomic_fetch_add(blocks_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-            gridDim.x - 1) {
+        if (gridDim.x == 1) {  // a lone call: no count to take; packed, the verdicts ride along
+            const uint64_t w = (uint64_t)seq << 32 | (packed ? kSmallPacked | vbits : 0u);
+            __hip_atomic_store(done, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else if (__hip_atomic_fetch_add(blocks_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   gridDim.x - 1) {
             // the next launch of this slot counts from zero (stream order)
             __hip_atomic_store(blocks_done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(done, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(done, (uint64_t)seq << 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
 
 hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const DeltaView &d2,
                                const PendView &pd, const ProbeView &p,
-                               uint8_t *verdict, uint32_t *blocks_done, uint32_t *done,
-                               uint32_t seq, hipStream_t s)
+                               uint8_t *verdict, uint32_t *blocks_done, uint64_t *done,
+                               uint32_t seq, bool pack, hipStream_t s)
 {
-    // one pass of kNP ranges per 16-lane group, at most one block per CU
-    // (two with appended rows pending: one per half of the grid)
-    const size_t per_block = (kSmallThreads / 16) * kNP;
+    // one pass of a range per 16-lane group, at most one block per CU (two
+    // with appended rows pending: one per half of the grid)
+    const size_t per_block = kSmallThreads / 16;
     const size_t work = std::max<size_t>({(p.n + per_block - 1) / per_block,
                                           (p.n_lock + kSmallThreads - 1) / kSmallThreads, 1});
     const bool split = d.n || d2.n || pd.n || pd.nt;
@@ -585,11 +741,11 @@ hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const D
         return hipErrorInvalidValue;  // the host mirrors a tail only for W <= kPendMaxWords
     if ((d.n && d.W != nv.W) || (d2.n && d2.W != nv.W)) return hipErrorInvalidValue;
     switch (WD) {
-    case 1: k_small_narrow<1><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq); break;
-    case 2: k_small_narrow<2><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq); break;
-    case 3: k_small_narrow<3><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq); break;
-    case 4: k_small_narrow<4><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq); break;
-    default: k_small_narrow<0><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq);
+    case 1: k_small_narrow<1><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq, pack); break;
+    case 2: k_small_narrow<2><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq, pack); break;
+    case 3: k_small_narrow<3><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq, pack); break;
+    case 4: k_small_narrow<4><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq, pack); break;
+    default: k_small_narrow<0><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq, pack);
     }
     return hipGetLastError();
 }
