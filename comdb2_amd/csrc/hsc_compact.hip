@@ -313,6 +313,60 @@ __global__ __launch_bounds__(256) void k_cs_keys(const uint64_t *words, size_t s
     k[WC] = c[WC - 1] << 32 | i;
 }
 
+// k_cs_keys for keys of at most kProbeWords words with the tables in LDS: a
+// row's words up to its group's last varying one are loaded together (one
+// round of loads instead of one per word of a run-time loop), mapped in
+// registers (shift-in accumulator, as bound_codes), and words past the last
+// varying one -- config 3's zero padding -- are neither loaded nor mapped.
+template <int WC>
+__global__ __launch_bounds__(256) void k_cs_keys_r(const uint64_t *words, size_t stride, const uint32_t *gid,
+                                                   uint32_t n, CompactMeta cm, uint64_t *keys)
+{
+    extern __shared__ __attribute__((aligned(16))) uint64_t tl[];
+    cs_stage_tables(cm, tl);
+    uint32_t *lnw = (uint32_t *)(tl + 8 * (size_t)cm.ng * cm.W) + cm.ng;  // after the bits
+    __syncthreads();
+    for (int g = threadIdx.x; g < cm.ng; g += blockDim.x) {
+        int nw = 0;
+        for (int j = 0; j < cm.W; ++j)
+            if (cm.mask[(size_t)g * cm.W + j]) nw = j + 1;
+        lnw[g] = (uint32_t)nw;
+    }
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t g = gid[i];
+    const int nw = (int)lnw[g];
+    uint64_t x[kProbeWords];
+#pragma unroll
+    for (int j = 0; j < kProbeWords; ++j) x[j] = j < nw ? words[(size_t)j * stride + i] : 0;
+    uint64_t c[WC];
+#pragma unroll
+    for (int k = 0; k < WC; ++k) c[k] = 0;
+    int pos = 0;
+    const uint64_t *mk = cm.mask + (size_t)g * cm.W, *mvg = cm.mv + (size_t)g * cm.W * 6;
+#pragma unroll
+    for (int j = 0; j < kProbeWords; ++j) {
+        if (j >= nw) break;
+        const uint64_t m = mk[j];
+        uint64_t v = x[j] & m;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+            const uint64_t t = v & mvg[j * 6 + q];
+            v = (v ^ t) | (t >> (1 << q));
+        }
+        const int cnt = __popcll(m);
+        acc_push<WC>(c, v, cnt);
+        pos += cnt;
+    }
+    acc_align<WC>(c, pos);
+    uint64_t *k = keys + (size_t)i * (WC + 1);
+    k[0] = (uint64_t)g << 32 | c[0] >> 32;
+#pragma unroll
+    for (int m = 1; m < WC; ++m) k[m] = c[m - 1] << 32 | c[m] >> 32;
+    k[WC] = c[WC - 1] << 32 | i;
+}
+
 // inverse of compress (Hacker's Delight expand: the same moves, reversed)
 __device__ __forceinline__ uint64_t expand(uint64_t x, uint64_t m, const uint64_t *mv)
 {
@@ -427,17 +481,31 @@ __global__ __launch_bounds__(kCsUdThreads) void k_cs_unpack_dd(
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *d_count = boff[blockIdx.x] + total;
     __syncthreads();
     const uint32_t b0 = boff[blockIdx.x];
-    for (uint32_t j = threadIdx.x; j < nrows; j += kCsUdThreads) {  // consecutive rows per wave
-        const size_t i = base + j;
-        const uint64_t *k = keys + i * KW;
-        uint64_t kk[KW];
+    // every key of the thread's rows first, then their LSN gathers, then the
+    // stores (a loop that loads after the previous row's stores waits on two
+    // dependent loads per row: the compiler cannot move loads above stores
+    // that may alias them)
+    uint64_t kr[kCsUdRows][KW], lr[kCsUdRows];
 #pragma unroll
-        for (int m = 0; m < KW; ++m) kk[m] = k[m];
-        const uint32_t g = (uint32_t)(kk[0] >> 32), idx = (uint32_t)kk[WC];
+    for (int r = 0; r < kCsUdRows; ++r) {
+        const uint32_t j = threadIdx.x + r * kCsUdThreads;  // consecutive rows per wave
+        const uint64_t *k = keys + (base + (j < nrows ? j : 0)) * KW;
+#pragma unroll
+        for (int m = 0; m < KW; ++m) kr[r][m] = k[m];
+    }
+#pragma unroll
+    for (int r = 0; r < kCsUdRows; ++r) lr[r] = lsn_in[(uint32_t)kr[r][WC]];
+#pragma unroll
+    for (int r = 0; r < kCsUdRows; ++r) {
+        const uint32_t j = threadIdx.x + r * kCsUdThreads;
+        if (j >= nrows) break;
+        const size_t i = base + j;
+        const uint64_t(&kk)[KW] = kr[r];
+        const uint32_t g = (uint32_t)(kk[0] >> 32);
         uint64_t c[WC];
 #pragma unroll
         for (int m = 0; m < WC; ++m) c[m] = kk[m] << 32 | kk[m + 1] >> 32;
-        const uint64_t lv = lsn_in[idx];
+        const uint64_t lv = lr[r];
         const uint32_t d = pos[j];
         const bool last = d != 0xFFFFFFFFu;
         lsn_o[i] = lv;
@@ -526,6 +594,16 @@ hipError_t compact_sort_keys(const uint64_t *words, size_t stride, const uint32_
     const uint32_t tb = cs_tab_bytes(t.ng, t.W);
     const bool lds = tb <= kCsTabLds;
     const uint32_t ldsb = lds ? tb : 0;
+    if (lds && t.W <= kProbeWords) {
+        const uint32_t lb = tb + 4 * (uint32_t)t.ng;  // + each group's words to its last varying one
+        switch (t.WC) {
+        case 1: k_cs_keys_r<1><<<b, 256, lb, s>>>(words, stride, gid, n, cm, keys); break;
+        case 2: k_cs_keys_r<2><<<b, 256, lb, s>>>(words, stride, gid, n, cm, keys); break;
+        case 3: k_cs_keys_r<3><<<b, 256, lb, s>>>(words, stride, gid, n, cm, keys); break;
+        default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     switch (t.WC) {
     case 1: k_cs_keys<1><<<b, 256, ldsb, s>>>(words, stride, gid, n, cm, keys, lds); break;
     case 2: k_cs_keys<2><<<b, 256, ldsb, s>>>(words, stride, gid, n, cm, keys, lds); break;

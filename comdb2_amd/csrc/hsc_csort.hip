@@ -12,9 +12,10 @@
 // the last version of a key is the last of its run), sorted here by
 //   block sort   1024 keys per workgroup: 4-key networks in registers, then
 //                merge levels in LDS;
-//   merges       runs of 1024, 2048, ... merged pairwise by merge path: a
-//                workgroup finds its 1024-output tile's split of the two
-//                runs (two binary searches), stages those keys in LDS, and
+//   merges       runs of 1024, 2048, ... merged pairwise by merge path: the
+//                splits of every 1024-output tile first (k_cs_splits, all
+//                tiles at once), then a workgroup per tile stages its keys
+//                of the two runs in LDS, and
 //                every thread merges 4 outputs from its own split into an
 //                LDS permutation that the tile then writes out in order,
 // i.e. log2(n / 1024) passes of 2 x 8 KW bytes per row, then unpacked back
@@ -186,15 +187,34 @@ __device__ __forceinline__ uint32_t merge_split16(const uint64_t *A, uint32_t la
     return lo;
 }
 
+// The split of every merge tile's first output (one 16-lane group per tile,
+// all tiles at once): the merge's workgroups then start from a load instead
+// of a chain of dependent global reads each (which left the pass latency-
+// bound: 4 rounds of workgroups per CU, each waiting ~6 search rounds).
+template <int KW>
+__global__ __launch_bounds__(kCsThreads) void k_cs_splits(const uint64_t *src, size_t n, size_t L,
+                                                          uint32_t ntiles, uint32_t *split)
+{
+    const int lane = threadIdx.x & 63, sub = lane >> 4, l16 = lane & 15;
+    const uint32_t t = (blockIdx.x * kCsThreads + threadIdx.x) >> 4;
+    const bool act = t < ntiles;
+    const size_t o0 = act ? (size_t)t * kCsBlock : 0;
+    const size_t p0 = o0 / (2 * L) * (2 * L);
+    const uint32_t la = (uint32_t)min(L, n - p0);
+    const uint32_t lb = (uint32_t)min(L, n - min(n, p0 + L));
+    const uint64_t *A = src + p0 * KW, *B = A + (size_t)la * KW;
+    const uint32_t sp = merge_split16<KW>(A, la, B, lb, (uint32_t)(o0 - p0), act, l16, sub);
+    if (act && l16 == 0) split[t] = sp;
+}
+
 // One merge pass: runs of L keys of src merged pairwise into dst, 1024
-// outputs per workgroup.
+// outputs per workgroup, from the splits k_cs_splits left.
 template <int KW>
 __global__ __launch_bounds__(kCsThreads) void k_cs_merge(const uint64_t *src, uint64_t *dst, size_t n,
-                                                         size_t L)
+                                                         size_t L, const uint32_t *split)
 {
     __shared__ uint64_t S[kCsBlock * KW];
     __shared__ uint16_t pos[kCsBlock];  // output r of the tile = staged key pos[r]
-    __shared__ uint32_t split[2];
     const size_t o0 = (size_t)blockIdx.x * kCsBlock;
     if (o0 >= n) return;
     const size_t p0 = o0 / (2 * L) * (2 * L);  // the pair's first key
@@ -202,13 +222,9 @@ __global__ __launch_bounds__(kCsThreads) void k_cs_merge(const uint64_t *src, ui
     const uint32_t lb = (uint32_t)min(L, n - min(n, p0 + L));
     const uint64_t *A = src + p0 * KW, *B = A + (size_t)la * KW;
     const uint32_t d0 = (uint32_t)(o0 - p0), d1 = min(d0 + (uint32_t)kCsBlock, la + lb);
-    if (threadIdx.x < 64) {  // wave 0: lanes 0-15 split d0, lanes 16-31 split d1
-        const int lane = threadIdx.x, sub = lane >> 4, l16 = lane & 15;
-        const uint32_t sp = merge_split16<KW>(A, la, B, lb, sub ? d1 : d0, sub < 2, l16, sub);
-        if (sub < 2 && l16 == 0) split[sub] = sp;
-    }
-    __syncthreads();
-    const uint32_t i0 = split[0], i1 = split[1], j0 = d0 - i0, j1 = d1 - i1;
+    // the pair's last tile ends with every key of A taken
+    const uint32_t i0 = split[blockIdx.x], i1 = d1 == la + lb ? la : split[blockIdx.x + 1];
+    const uint32_t j0 = d0 - i0, j1 = d1 - i1;
     const uint32_t na = i1 - i0, nb = j1 - j0;
     // stage A[i0, i1) then B[j0, j1)
     for (uint32_t e = threadIdx.x; e < (na + nb) * KW; e += kCsThreads) {
@@ -235,13 +251,16 @@ __global__ __launch_bounds__(kCsThreads) void k_cs_merge(const uint64_t *src, ui
 }
 
 template <int KW>
-hipError_t sort_kw(uint64_t *keys, uint64_t *tmp, size_t n, hipStream_t s, uint64_t **sorted)
+hipError_t sort_kw(uint64_t *keys, uint64_t *tmp, uint32_t *split, size_t n, hipStream_t s,
+                   uint64_t **sorted)
 {
     const uint32_t blocks = (uint32_t)((n + kCsBlock - 1) / kCsBlock);
     k_cs_block_sort<KW><<<blocks, kCsThreads, 0, s>>>(keys, tmp, n);
     uint64_t *src = tmp, *dst = keys;
+    const uint32_t sb = (blocks + kCsThreads / 16 - 1) / (kCsThreads / 16);
     for (size_t L = kCsBlock; L < n; L *= 2) {
-        k_cs_merge<KW><<<blocks, kCsThreads, 0, s>>>(src, dst, n, L);
+        k_cs_splits<KW><<<sb, kCsThreads, 0, s>>>(src, n, L, blocks, split);
+        k_cs_merge<KW><<<blocks, kCsThreads, 0, s>>>(src, dst, n, L, split);
         std::swap(src, dst);
     }
     *sorted = src;
@@ -250,15 +269,17 @@ hipError_t sort_kw(uint64_t *keys, uint64_t *tmp, size_t n, hipStream_t s, uint6
 
 }  // namespace
 
-hipError_t code_keys_sort(uint64_t *keys, uint64_t *tmp, size_t n, int KW, hipStream_t s,
+size_t code_sort_split_words(size_t n) { return (n + kCsBlock - 1) / kCsBlock + 1; }
+
+hipError_t code_keys_sort(uint64_t *keys, uint64_t *tmp, uint32_t *split, size_t n, int KW, hipStream_t s,
                           uint64_t **sorted)
 {
     *sorted = keys;
     if (n == 0) return hipSuccess;
     switch (KW) {
-    case 2: return sort_kw<2>(keys, tmp, n, s, sorted);
-    case 3: return sort_kw<3>(keys, tmp, n, s, sorted);
-    case 4: return sort_kw<4>(keys, tmp, n, s, sorted);
+    case 2: return sort_kw<2>(keys, tmp, split, n, s, sorted);
+    case 3: return sort_kw<3>(keys, tmp, split, n, s, sorted);
+    case 4: return sort_kw<4>(keys, tmp, split, n, s, sorted);
     default: return hipErrorInvalidValue;
     }
 }

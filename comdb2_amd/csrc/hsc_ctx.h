@@ -494,7 +494,7 @@ struct hsc_ctx {
     DBuf d_cmask, d_cpat, d_cmv, d_cbits, d_cwords, d_ctmax, d_csp_g, d_csp_w;
     // the code sort's tables and keys (device_build: wide rows whose per-group
     // varying bits fit 3 words)
-    DBuf d_csrep, d_csmask, d_cspat, d_csmv, d_csbits, d_cskeys[2];
+    DBuf d_csrep, d_csmask, d_cspat, d_csmv, d_csbits, d_cskeys[2], d_cssplit;
     bool code_sorted = false;  // the last build sorted by compact codes
     int cs_codes_wc = 0;       // its unpack wrote the distinct rows' codes (d_cwords) of this width
     std::vector<uint64_t> cs_mask;     // its varying bits per (group, word) (host copy)

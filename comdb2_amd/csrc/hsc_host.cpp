@@ -599,7 +599,9 @@ static int code_sort(hsc_ctx *c, size_t n_in, bool *done)
     HIPCHK(c, compact_sort_keys(c->d_words.as<uint64_t>(), c->cap, c->d_gid.as<uint32_t>(), (uint32_t)n_in,
                                 t, c->d_cskeys[0].as<uint64_t>(), s));
     uint64_t *sorted = nullptr;
-    HIPCHK(c, code_keys_sort(c->d_cskeys[0].as<uint64_t>(), c->d_cskeys[1].as<uint64_t>(), n_in, KW, s,
+    HIPCHK(c, c->d_cssplit.ensure(4 * code_sort_split_words(n_in)));
+    HIPCHK(c, code_keys_sort(c->d_cskeys[0].as<uint64_t>(), c->d_cskeys[1].as<uint64_t>(),
+                             c->d_cssplit.as<uint32_t>(), n_in, KW, s,
                              &sorted));
     // every version, key-sorted, into d_*2; the distinct rows into d_gid /
     // d_words (the unpack reads only the input LSNs) and the free key
@@ -3027,7 +3029,8 @@ void hsc_ctx_destroy(hsc_ctx *c)
     for (auto &sl : c->small) sl.io.release();
     c->small_blocks.release();
     for (DBuf *b : {&c->d_csrep, &c->d_csmask, &c->d_cspat, &c->d_csmv, &c->d_csbits, &c->d_cskeys[0],
-                    &c->d_cskeys[1], &c->d_cmask, &c->d_cpat, &c->d_cmv, &c->d_cbits, &c->d_cwords})
+                    &c->d_cskeys[1], &c->d_cssplit, &c->d_cmask, &c->d_cpat, &c->d_cmv, &c->d_cbits,
+                    &c->d_cwords})
         b->release();
     for (DBuf *b : {&c->d_dgid[0], &c->d_dgid[1], &c->d_dwords[0], &c->d_dwords[1], &c->d_dlsn[0],
                     &c->d_dlsn[1], &c->d_dbmax, &c->d_agid})

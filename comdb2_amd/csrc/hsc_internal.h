@@ -500,7 +500,9 @@ hipError_t compact_masks_unsorted(const uint64_t *words, size_t stride, const ui
                                   hipStream_t s);
 hipError_t compact_sort_keys(const uint64_t *words, size_t stride, const uint32_t *gid, uint32_t n,
                              const CompactTables &t, uint64_t *keys, hipStream_t s);
-hipError_t code_keys_sort(uint64_t *keys, uint64_t *tmp, size_t n, int KW, hipStream_t s,
+// split: code_sort_split_words(n) u32 of device scratch
+size_t code_sort_split_words(size_t n);
+hipError_t code_keys_sort(uint64_t *keys, uint64_t *tmp, uint32_t *split, size_t n, int KW, hipStream_t s,
                           uint64_t **sorted);
 // sorted keys back to rows, with the dedupe fused in: every version to *_o, the last of
 // each key to *_d (which may be the input gid / words -- only lsn_in is read
