@@ -667,8 +667,10 @@ __device__ void small_appended16(const DeltaView &d, const DeltaView &d2, const 
 }
 
 // WD = 0: keys wider than kPendMaxWords (no pending tail), a thread per range
-// and binary searches; WD = 1..4: small_appended16<WD>.
-template <int WD>
+// and binary searches; WD = 1..4: small_appended16<WD>.  KW: the window's
+// search form (narrow_small_ranges<KW>), one per kernel (the code a launch
+// runs stays small: its first instruction fetches are on the call's path).
+template <int WD, int KW>
 __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, DeltaView d,
                                                                 DeltaView d2, PendView pd,
                                                                 ProbeView p, uint8_t *verdict,
@@ -690,12 +692,7 @@ __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, D
     if (blockIdx.x < half) {
         const uint32_t groups = half * (kSmallThreads / 16);
         const uint32_t wave0 = blockIdx.x * (kSmallThreads / 16) + ((threadIdx.x >> 6) << 2);
-        if (nv.W == 2)
-            narrow_small_ranges<2>(nv, p, verdict, vmask, wave0, groups);
-        else if (nv.W == 1)
-            narrow_small_ranges<1>(nv, p, verdict, vmask, wave0, groups);
-        else
-            narrow_small_ranges<0>(nv, p, verdict, vmask, wave0, groups);
+        narrow_small_ranges<KW>(nv, p, verdict, vmask, wave0, groups);
         for (uint32_t q = blockIdx.x * kSmallThreads + threadIdx.x; q < p.n_lock; q += half * kSmallThreads) {
             const uint32_t t = p.lock_table[q];
             if (t < nv.ntables && nv.table_max[t] > p.lock_snap[q]) small_mark(verdict, vmask, p.lock_txn[q]);
@@ -740,13 +737,28 @@ hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const D
     if ((pd.n || pd.nt) && (WD == 0 || !pd.base || pd.n > kPendRows || pd.nt > kPendRows))
         return hipErrorInvalidValue;  // the host mirrors a tail only for W <= kPendMaxWords
     if ((d.n && d.W != nv.W) || (d2.n && d2.W != nv.W)) return hipErrorInvalidValue;
+    const int KW = nv.W == 1 || nv.W == 2 ? nv.W : 0;
+#define HSC_SMALL(WD_, KW_)                                                                              \
+    k_small_narrow<WD_, KW_><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, \
+                                                              seq, pack)
+#define HSC_SMALL_KW(WD_)                  \
+    do {                                   \
+        if (KW == 2)                       \
+            HSC_SMALL(WD_, 2);             \
+        else if (KW == 1)                  \
+            HSC_SMALL(WD_, 1);             \
+        else                               \
+            HSC_SMALL(WD_, 0);             \
+    } while (0)
     switch (WD) {
-    case 1: k_small_narrow<1><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq, pack); break;
-    case 2: k_small_narrow<2><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq, pack); break;
-    case 3: k_small_narrow<3><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq, pack); break;
-    case 4: k_small_narrow<4><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq, pack); break;
-    default: k_small_narrow<0><<<blocks, kSmallThreads, 0, s>>>(nv, d, d2, pd, p, verdict, blocks_done, done, seq, pack);
+    case 1: HSC_SMALL_KW(1); break;
+    case 2: HSC_SMALL_KW(2); break;
+    case 3: HSC_SMALL_KW(3); break;
+    case 4: HSC_SMALL_KW(4); break;
+    default: HSC_SMALL_KW(0);
     }
+#undef HSC_SMALL_KW
+#undef HSC_SMALL
     return hipGetLastError();
 }
 
