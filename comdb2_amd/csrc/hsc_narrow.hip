@@ -692,7 +692,11 @@ __global__ __launch_bounds__(kSmallThreads) void k_small_narrow(NarrowView nv, D
     if (blockIdx.x < half) {
         const uint32_t groups = half * (kSmallThreads / 16);
         const uint32_t wave0 = blockIdx.x * (kSmallThreads / 16) + ((threadIdx.x >> 6) << 2);
-        narrow_small_ranges<KW>(nv, p, verdict, vmask, wave0, groups);
+        if (split) {  // (measured: the appended rows' half sets the pace; kNP ranges per group)
+            narrow_probe_ranges<true>(nv, p, verdict, nullptr, 0, nv.levels, wave0 * kNP, groups * kNP);
+        } else {
+            narrow_small_ranges<KW>(nv, p, verdict, vmask, wave0, groups);
+        }
         for (uint32_t q = blockIdx.x * kSmallThreads + threadIdx.x; q < p.n_lock; q += half * kSmallThreads) {
             const uint32_t t = p.lock_table[q];
             if (t < nv.ntables && nv.table_max[t] > p.lock_snap[q]) small_mark(verdict, vmask, p.lock_txn[q]);
@@ -728,10 +732,10 @@ hipError_t launch_small_narrow(const NarrowView &nv, const DeltaView &d, const D
 {
     // one pass of a range per 16-lane group, at most one block per CU (two
     // with appended rows pending: one per half of the grid)
-    const size_t per_block = kSmallThreads / 16;
+    const bool split = d.n || d2.n || pd.n || pd.nt;
+    const size_t per_block = (kSmallThreads / 16) * (split ? kNP : 1);
     const size_t work = std::max<size_t>({(p.n + per_block - 1) / per_block,
                                           (p.n_lock + kSmallThreads - 1) / kSmallThreads, 1});
-    const bool split = d.n || d2.n || pd.n || pd.nt;
     const unsigned blocks = (unsigned)(std::min<size_t>(work, 256) * (split ? 2 : 1));
     const int WD = split && nv.W <= kPendMaxWords ? nv.W : 0;
     if ((pd.n || pd.nt) && (WD == 0 || !pd.base || pd.n > kPendRows || pd.nt > kPendRows))
