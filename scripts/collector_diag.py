@@ -55,7 +55,7 @@ for nth in threads:
                                                      "usage_usec", "user_usec", "system_usec")}
         keep = ("checks_per_s", "lat_p50_us", "lat_p99_us", "mean_batch", "device_pass_us",
                 "busy_frac", "gate_us", "handout_us")
-        print(f"threads {nth} inflight {inflight or 2}: parity {bool(np.array_equal(got != 0, want))} wall {el:.2f}s "
+        print(f"threads {nth} inflight {inflight or 4}: parity {bool(np.array_equal(got != 0, want))} wall {el:.2f}s "
               f"cpu {d['usage_usec'] / 1e6 / max(el, 1e-9):.2f} cores "
               f"(user {d['user_usec'] / 1e6:.2f}s sys {d['system_usec'] / 1e6:.2f}s) "
               f"periods {d['nr_periods']} throttled {d['nr_throttled']} ({d['throttled_usec'] / 1e3:.1f} ms) | "
