@@ -397,8 +397,8 @@ __device__ __forceinline__ uint64_t code_bits(const uint64_t (&c)[WC], int pos, 
 // pass counts the blocks' distinct rows (their exclusive scan gives each
 // block's place), the next writes every version to the *_o rows and the last
 // of each key to its place among the *_d rows.
-constexpr int kCsUdThreads = 256;
-constexpr int kCsUdRows = 8;
+constexpr int kCsUdThreads = 1024;
+constexpr int kCsUdRows = 2;
 constexpr int kCsUdTile = kCsUdThreads * kCsUdRows;
 
 template <int KW>
