@@ -6,6 +6,7 @@
 # limit; stops at the first fault / abort / timeout (exit codes other than 0
 # and 1).
 tag=${1:-r04f}
+part=${2:-all}  # a: suite + bench lines, b: multi-GPU rehearsals, traces, PMC
 out=gpurun_out; mkdir -p $out
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 step() {  # name limit cmd...
@@ -15,6 +16,7 @@ step() {  # name limit cmd...
   echo "$name rc=$rc"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -5 $out/${tag}_$name.err; exit $rc; fi
 }
+if [ $part != b ]; then
 step pytest 600 python -u -m pytest tests/ -m gpu -q --timeout 300 --timeout-method thread
 tail -2 $out/${tag}_pytest.log
 step bench 600 python -u bench.py
@@ -22,6 +24,8 @@ step config1 300 python -u bench.py --config 1
 step config3 400 python -u bench.py --config 3
 step config5 500 python -u bench.py --config 5
 step config4 500 python -u bench.py --config 4
+fi
+[ $part = a ] && exit 0
 step inproc2 300 python -u bench.py --inproc 2 --steps 30
 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29531 step rank1 300 python -u bench.py --rank-path --steps 50
 step trace 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/${tag}_trace -o k -- python3 bench.py --steps 10 --no-cpu --no-pmc --no-api
