@@ -7,11 +7,13 @@ timed region starts; marshalling (CurRangeArr -> probe SoA, done by the
 native library) happens before it.
 
 Multi-GPU (weak scaling, bench_multi): the native multi-GPU context
-(hsc_multi_*, one process per GPU over RCCL under torchrun, or --inproc N
-members in one process): every GPU holds its piece of an N-times larger
-window and its own batch of 100k read sets; a step routes every GPU's probes
-on the device to the pieces they overlap, exchanges them, probes, and ORs the
-verdict bitmaps onto each read set's owner -- all inside the timed region.
+(hsc_multi_*; one process per GPU over RCCL under torchrun, or --gpus N
+members in this process on devices 0..N-1): every GPU holds its piece of an
+N-times larger window and owns 100k read sets of each global batch; the
+ranges were routed to the pieces they overlap when the batch was marshalled,
+and a step probes every piece and ORs the verdict bitmaps onto each read
+set's owner (RCCL across ranks).  The device-routed step (routing +
+exchange inside the timed region) is reported beside it.
 
 Prints ONE JSON line on rank 0.
 """
@@ -599,17 +601,20 @@ def bench_multi(args):
     Weak scaling: every member holds its piece of an N-times larger window
     (composite-key splitters: config 2 key ranges, config 5 sampled global
     splitters, config 3 work quantiles over the 32 groups' rows and ranges)
-    and its own resident batch of 100k read sets (its share of the global
-    batch, in arrival order, NOT routed on the host).  One timed step =
-    hsc_multi_probe_device on every member: device-side routing of each
-    member's probes to the pieces their [lo, hi] overlaps (k_route_count,
-    counts all-gathered, k_route_scatter), the exchange (RCCL grouped
-    send / receive across ranks; direct stores between members of one
-    process), the probe pipeline on every member, and the OR-merge of the
-    members' verdict bitmaps onto each read set's owner.  Under torchrun:
-    one process per GPU (RCCL).  --inproc N without torchrun: N members in
-    this process on the visible GPUs round robin (several members share a GPU
-    when there are fewer: a rehearsal of the in-process path)."""
+    and owns 100k read sets of each global batch (N x 100k read sets).
+
+    Timed step (the headline): hsc_multi_probe_routed -- every member probes
+    the ranges of the global batch that overlap its piece (routed on the host
+    when the batch was marshalled: the drop-in path's routing),
+    then the members' verdict bitmaps are OR-ed onto each read set's owner
+    (RCCL send / receive of the owners' slices across ranks; peer reads in one
+    process).  Secondary leg `device_routed`: the same global batch resident
+    unrouted (each member its own 100k read sets) and routed inside the step
+    (hsc_multi_probe_device: route kernels, exchange, probe, merge).
+
+    Under torchrun: one process per GPU (RCCL).  Without it: `--gpus N` runs N
+    members in this process on devices 0..N-1 (exits non-zero when fewer are
+    visible); `--inproc N` is the rehearsal that lets members share a GPU."""
     import torch
     import torch.distributed as dist
 
@@ -620,14 +625,24 @@ def bench_multi(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     inproc = world_env == 1 and not args.rank_path
     if inproc:
-        N = args.inproc
         ndev = torch.cuda.device_count()
-        devs = [i % ndev for i in range(N)]
+        if args.gpus > 1:
+            N = args.gpus
+            if ndev < N:
+                print(f"bench.py --gpus {N}: only {ndev} GPU(s) visible", file=sys.stderr, flush=True)
+                sys.exit(2)
+            devs = list(range(N))
+        else:
+            N = args.inproc
+            devs = [i % ndev for i in range(N)]
         v = hsc.MultiValidator(devs)
         mine = list(range(N))
         dev_of = {g: torch.device("cuda", devs[g]) for g in mine}
     else:
         N = world_env
+        if args.gpus > 1 and args.gpus != N:
+            print(f"bench.py --gpus {args.gpus} under WORLD_SIZE {N}", file=sys.stderr, flush=True)
+            sys.exit(2)
         torch.cuda.set_device(local)
         dev0 = torch.device("cuda", local)
         dist.init_process_group("nccl", device_id=dev0)
@@ -640,6 +655,8 @@ def bench_multi(args):
         mine = [rank]
         dev_of = {rank: dev0}
         devs = [local]
+    if args.loopback and inproc:
+        v.set_transport(True)
 
     def sync_all():
         for d in sorted(set(dev_of[g].index for g in mine)):
@@ -741,34 +758,57 @@ def bench_multi(args):
     if args.config == 3:
         v.merge_table_max(c3.table_max)  # data-row writes lock tables too
     W = v.words
-    # resident batches: member g's share of each global batch
+    TP = (T + 63) // 64 * 64  # each owner's read sets start at a multiple of 64
+    # resident batches, per member: `routed` = its ranges of the whole global
+    # batch (routed at marshal), `dev` = its own 100k read sets unrouted
     batches, ring_bytes, bi = [], 0, 0
+    t_setup = time.perf_counter()
     while bi < max(2, args.batches) or ring_bytes < args.ring_gb * 1e9:
         rs = first_rs if bi == 0 else more_rs(bi)
+        shares = [rs.subset(np.arange(g * T, (g + 1) * T)) for g in range(N)]
+        routed = v.routed_shares(shares, mine)
         per = {}
-        for g in mine:
-            m = v.marshal(rs.subset(np.arange(g * T, (g + 1) * T)))
-            b = upload_batch(torch, dev_of[g], m)
-            b["bits"] = torch.zeros((T + 63) // 64, dtype=torch.int64, device=dev_of[g])
-            b["verdict"] = torch.zeros(T, dtype=torch.uint8, device=dev_of[g])
-            b["struct"] = probe_struct(hsc, b, b["verdict"], b["bits"], T)
+        for li, g in enumerate(mine):
+            dv = dev_of[g]
+            r = routed[g]
+            b = upload_batch(torch, dv, r)
+            b["bits"] = torch.zeros(TP // 64, dtype=torch.int64, device=dv)
+            b["verdict"] = torch.zeros(N * TP, dtype=torch.uint8, device=dv)
+            b["struct"] = hsc.ProbeBatch(b["n"], b["lo"].data_ptr(), b["hi"].data_ptr(),
+                                         b["gid"].data_ptr(), b["snap"].data_ptr(),
+                                         b["txn"].data_ptr(), b["n_lock"],
+                                         b["lock_table"].data_ptr(), b["lock_snap"].data_ptr(),
+                                         b["lock_txn"].data_ptr(), N * TP,
+                                         b["verdict"].data_ptr(), b["bits"].data_ptr())
+            b["owner_base"] = r["owner_base"]
+            b["forced"] = r["forced"][g]
             b["bytes"] = sum(int(b[k].numel() * b[k].element_size())
                              for k in ("lo", "hi", "gid", "snap", "txn", "lock_table", "lock_snap",
                                        "lock_txn"))
-            per[g] = b
-        ring_bytes += per[mine[0]]["bytes"]
+            m = v.marshal(shares[g])
+            d = upload_batch(torch, dv, m)
+            d["bits"] = torch.zeros((T + 63) // 64, dtype=torch.int64, device=dv)
+            d["verdict"] = torch.zeros(T, dtype=torch.uint8, device=dv)
+            d["struct"] = probe_struct(hsc, d, d["verdict"], d["bits"], T)
+            per[g] = {"routed": b, "dev": d}
+        ring_bytes += per[mine[0]]["routed"]["bytes"]
         batches.append(per)
         bi += 1
         if bi % 8 == 0:
             print(f"[bench] {bi} batches, {ring_bytes / 1e9:.2f} GB per member", file=sys.stderr,
                   flush=True)
+    setup_s = time.perf_counter() - t_setup
     NB = len(batches)
+    ob = batches[0][mine[0]]["routed"]["owner_base"]
     sync_all()
 
-    def step(k, lanes, nbatch):
-        v.probe_device_multi([batches[k % nbatch][g]["struct"] for g in mine], lane=k % lanes)
+    def step_routed(k, lanes, nbatch):
+        v.probe_routed([batches[k % nbatch][g]["routed"]["struct"] for g in mine], ob, lane=k % lanes)
 
-    def timed(lanes, nbatch):
+    def step_device(k, lanes, nbatch):
+        v.probe_device_multi([batches[k % nbatch][g]["dev"]["struct"] for g in mine], lane=k % lanes)
+
+    def timed(step, lanes, nbatch):
         for k in range(args.warmup):
             step(k, lanes, nbatch)
         sync_all()
@@ -789,23 +829,46 @@ def bench_multi(args):
             el = float(e.item())
         return el
 
-    elapsed = timed(2, NB)
-    serial = float(np.median([timed(1, NB) for _ in range(3)]))
-    # merged verdicts of batch 0 (member mine[0]'s read sets)
-    step(0, 1, NB)
+    elapsed = timed(step_routed, 2, NB)
+    serial = float(np.median([timed(step_routed, 1, NB) for _ in range(3)]))
+    dev_elapsed = timed(step_device, 2, NB)
+    dev_serial = float(np.median([timed(step_device, 1, NB) for _ in range(3)]))
+    # merged verdicts of batch 0, member mine[0]'s read sets, both routings
+    g0 = mine[0]
+    step_device(0, 1, NB)
     sync_all()
-    b0 = batches[0][mine[0]]
-    bits = b0["bits"].cpu().numpy().view(np.uint8)
-    v0 = np.maximum(np.unpackbits(bits, bitorder="little")[:T], b0["forced"])
+    d0 = batches[0][g0]["dev"]
+    dbits = np.unpackbits(d0["bits"].cpu().numpy().view(np.uint8), bitorder="little")[:T]
+    step_routed(0, 1, NB)
+    sync_all()
+    r0 = batches[0][g0]["routed"]
+    rbits = np.unpackbits(r0["bits"].cpu().numpy().view(np.uint8), bitorder="little")[:T]
+    v0 = np.maximum(rbits, r0["forced"])
+    routings_equal = bool(np.array_equal(np.maximum(dbits, d0["forced"]) != 0, v0 != 0))
+    # per-member probe time of the routed step (imbalance across the pieces)
+    v.enable_member_timing(True)
+    pm = []
+    for k in range(min(args.steps, NB)):
+        step_routed(k, 1, NB)
+        pm.append(v.member_probe_ms())
+    v.enable_member_timing(False)
+    sync_all()
+    pm = np.mean(np.array(pm, np.float64), axis=0)
+    if not inproc:
+        t = torch.tensor(pm, dtype=torch.float64, device=dev_of[rank])
+        allt = [torch.zeros_like(t) for _ in range(N)]
+        dist.all_gather(allt, t)
+        pm = torch.cat(allt).cpu().numpy()
     cnt = v.last_counts().astype(np.int64)
-    st = v.multi_stats()
     n_keys = v.member(0).keys
-    n_r = int(batches[0][mine[0]]["n"])
+    n_r = int(r0["n"])
     Lhat = 8 * W
-    B = n_keys * (Lhat + 12) + n_r * (2 * Lhat + 16) + (T + 7) // 8
+    B = n_keys * (Lhat + 12) + n_r * (2 * Lhat + 16) + (N * T + 7) // 8
     ms = elapsed / args.steps * 1e3
     rec = 16 * W + 16
     off_diag = int(cnt.sum() - np.trace(cnt))
+    routed_rows = [int(batches[0][g]["routed"]["n"]) for g in mine]
+    own_rows = [int(batches[0][g]["dev"]["n"]) for g in mine]
     out = {
         "metric": METRIC,
         "value": N * T * args.steps / elapsed,
@@ -822,32 +885,48 @@ def bench_multi(args):
         "config": {
             "workload": workload,
             "members": N,
-            "transport": "in-process stores (xGMI peer / same GPU)" if inproc else "RCCL (C, grouped send/recv)",
+            "devices": devs,
+            "transport": ("in-process (xGMI peer reads / same GPU)" + (", loopback copies" if args.loopback else ""))
+                         if inproc else "RCCL (C, grouped send/recv)",
             "read_sets_per_step_per_member": T,
-            "ranges_per_member": n_r,
+            "ranges_routed_to_member0": n_r,
             "window_keys_member0": n_keys,
             "logged_writes_per_member": n_w,
-            "parallelism": f"composite-key pieces x{N}, device-side routing + exchange + "
-                           "bitmap OR per owner, all inside the timed step",
+            "parallelism": f"composite-key pieces x{N}: ranges routed to the pieces they overlap "
+                           "at marshal time (host), probe + bitmap OR per owner in the timed step",
             "lanes": 2,
             "serial_ms_per_step": serial / args.steps * 1e3,
             "ring_batches": NB,
+            "setup_s": setup_s,
             "groups": len(groups),
             "conflict_rate": float((v0 != 0).mean()),
         },
         "routing": {
+            "mode": "host, at marshal (hsc_multi_marshal_routed; not in the timed step, like the "
+                    "marshal itself)",
+            "routed_rows_per_member_batch0": routed_rows,
+            "own_rows_per_member_batch0": own_rows,
+            "routed_over_own": float(sum(routed_rows)) / max(1, sum(own_rows)),
+            "verdicts_equal_device_routed": routings_equal,
+        },
+        "imbalance": {
+            "member_probe_ms": [float(x) for x in pm],
+            "max_over_mean": float(pm.max() / pm.mean()) if pm.size and pm.mean() > 0 else None,
+        },
+        "device_routed": {
+            "value": N * T * args.steps / dev_elapsed,
+            "ms_per_step": dev_elapsed / args.steps * 1e3,
+            "serial_ms_per_step": dev_serial / args.steps * 1e3,
             "counts_last_batch": cnt.tolist(),
-            "routed_over_probes": st["routed"] / max(st["probes"], 1),
             "exchanged_bytes_per_step": off_diag * rec,
-            "exchanged_rows_per_step": off_diag,
             "host_phases_us": v.phase_stats(),
-            "note": "counts[s][d]: probes member s routed to member d in the last batch; "
-                    "off-diagonal rows crossed GPUs (RCCL) or were stored into another "
-                    "member's columns",
+            "note": "the same global batch resident unrouted (member g: its own 100k read sets); "
+                    "the step routes on the devices (k_route_count / k_route_scatter), exchanges "
+                    "(RCCL or in-process stores), probes and merges",
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "routed step (route count + scatter, exchange, probe phase, OR merge) per member",
+            "kernel": "routed step per member (probe phase of its routed ranges + OR merge)",
             "achieved": B / (ms * 1e-3) / 1e9,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -855,8 +934,9 @@ def bench_multi(args):
             "frac_1lane": B / (serial / args.steps) / 1e9 / HBM_PEAK_GBS,
             "traffic": None,
             "algorithmic_bytes": B,
-            "note": "B = member 0's probe-phase bytes (SURVEY 8(d): its window keys and its own "
-                    "ranges); the routing and exchange bytes come on top",
+            "note": "B = member 0's probe-phase bytes (SURVEY 8(d): its window keys, the ranges "
+                    "routed to it, the global batch's verdict bits); with members sharing a GPU "
+                    "(--inproc rehearsal) the GPU runs every member's B in one step",
         },
         "cpu_baseline": None,
     }
@@ -918,6 +998,9 @@ def main():
                     help="without torchrun: N members of one multi context in this process "
                          "(the visible GPUs round robin; members share a GPU when there are "
                          "fewer) -- the in-process multi-GPU path")
+    ap.add_argument("--loopback", action="store_true",
+                    help="in-process multi context: the per-rank exchange with peer copies "
+                         "(hsc_multi_set_transport) for the device-routed leg and the merge")
     ap.add_argument("--rank-path", action="store_true",
                     help="run the per-rank (RCCL) multi-GPU path even at WORLD_SIZE 1 (its "
                          "world-1 rehearsal on one GPU)")
@@ -929,7 +1012,8 @@ def main():
         return bench_graph(args)
     if args.config == 1:
         return bench_commit_stream(args)
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.inproc > 1 or args.rank_path:
+    if (int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.gpus > 1 or args.inproc > 1
+            or args.rank_path):
         return bench_multi(args)
     # one GPU (N > 1 runs bench_multi)
     world, rank = 1, 0

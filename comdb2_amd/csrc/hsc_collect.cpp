@@ -55,6 +55,7 @@
 #include <climits>
 #include <cstdlib>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -103,8 +104,14 @@ struct hsc_collector {
     std::atomic<uint32_t> gate{0};               // bumped when a batch ends
     std::atomic<int> gate_waiting{0};            // a leader sleeps on gate
     alignas(64) std::atomic<int> inside{0};      // callers inside hsc_collector_check (last touch: the decrement)
-    std::atomic<uint64_t> st_calls{0}, st_batches{0}, st_max_batch{0}, st_busy_ns{0}, st_gate_ns{0},
+    std::atomic<uint64_t> st_calls{0}, st_batches{0}, st_max_batch{0}, st_pass_ns{0}, st_gate_ns{0},
         st_handout_ns{0};
+    // busy = the union of the in-flight passes' intervals: the clock runs from
+    // the moment the first of them starts until none is left
+    std::mutex busy_mu;
+    int busy_depth = 0;
+    std::chrono::steady_clock::time_point busy_t0;
+    uint64_t st_busy_ns = 0;
 };
 
 namespace {
@@ -161,6 +168,10 @@ void lead(hsc_collector *k, Req *me)
     }
     if (k->max_wait_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(k->max_wait_us));
     k->running.fetch_add(1, std::memory_order_acq_rel);
+    {
+        std::lock_guard<std::mutex> g(k->busy_mu);
+        if (k->busy_depth++ == 0) k->busy_t0 = clk::now();
+    }
     // take the stack and give up the lead in one exchange: the next push
     // becomes the next leader
     const uintptr_t taken = k->state.exchange(0, std::memory_order_acq_rel);
@@ -182,7 +193,11 @@ void lead(hsc_collector *k, Req *me)
         a = b;
     }
     const auto t1 = clk::now();
-    k->st_busy_ns.fetch_add(ns_between(t0, t1), std::memory_order_relaxed);
+    k->st_pass_ns.fetch_add(ns_between(t0, t1), std::memory_order_relaxed);
+    {
+        std::lock_guard<std::mutex> g(k->busy_mu);
+        if (--k->busy_depth == 0) k->st_busy_ns += ns_between(k->busy_t0, t1);
+    }
     k->running.fetch_sub(1, std::memory_order_seq_cst);
     k->gate.fetch_add(1, std::memory_order_seq_cst);
     if (k->gate_waiting.load(std::memory_order_seq_cst)) futex_wake(&k->gate, 1);
@@ -301,7 +316,11 @@ int hsc_collector_get_stats(hsc_collector *k, hsc_collector_stats *out)
     out->calls = k->st_calls.load(std::memory_order_relaxed);
     out->batches = k->st_batches.load(std::memory_order_relaxed);
     out->max_batch = k->st_max_batch.load(std::memory_order_relaxed);
-    out->busy_ns = k->st_busy_ns.load(std::memory_order_relaxed);
+    {
+        std::lock_guard<std::mutex> g(k->busy_mu);
+        out->busy_ns = k->st_busy_ns;
+    }
+    out->pass_ns = k->st_pass_ns.load(std::memory_order_relaxed);
     out->gate_ns = k->st_gate_ns.load(std::memory_order_relaxed);
     out->handout_ns = k->st_handout_ns.load(std::memory_order_relaxed);
     return HSC_OK;

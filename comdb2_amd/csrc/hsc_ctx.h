@@ -623,12 +623,18 @@ int ctx_window_words(hsc_ctx *c);
 void ctx_clear_window(hsc_ctx *c);
 int ctx_ensure_built(hsc_ctx *c);
 void ctx_add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keylen, bool has_key, uint64_t lsn);
-int ctx_flush_appends(hsc_ctx *c);
+int ctx_flush_appends(hsc_ctx *c, bool lazy = false);
 int ctx_probe(hsc_ctx *c, const hsc_probe_batch *b);
 int ctx_default_threads();
+void ctx_par_for(hsc_ctx *c, int nwork, const std::function<void(int)> &f);
+bool ctx_small_fits(hsc_ctx *c, size_t n_txn, size_t n, size_t n_lock);
+int ctx_edge_keys(hsc_ctx *c, uint32_t *gid, uint64_t *words);
+int ctx_stage_launch(hsc_ctx *c, Stage &st, int *slot);
+int ctx_stage_wait(hsc_ctx *c, Stage &st, int slot, int *rc_out);
+bool multi_adopted(const hsc_ctx *f);
 // hsc_multi.cpp: the front context's hooks (c->multi != nullptr)
 int multi_build(hsc_ctx *f);
-int multi_flush_appends(hsc_ctx *f);
+int multi_flush_appends(hsc_ctx *f, bool lazy);
 int multi_check_stage(hsc_ctx *f, Stage &st, int *rc_out);
 void multi_sync_dict(hsc_ctx *f);
 void multi_destroy(hsc_ctx *f);

@@ -1069,7 +1069,7 @@ static int pend_mirror(hsc_ctx *c)
 // the unmerged rows go to the delta run now.
 static int flush_appends(hsc_ctx *c, bool lazy = false)
 {
-    if (c->multi) return multi_flush_appends(c);
+    if (c->multi) return multi_flush_appends(c, lazy);
     if (!c->live || c->host_only) return HSC_OK;
     hipStream_t s = c->stream;
     HIPCHK_RC(c, fold_finish(c, false));
@@ -3106,6 +3106,8 @@ int hsc_window_append(hsc_ctx *c, const hsc_write *w, size_t n)
     if (!c || (!w && n)) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     if (!c->host_only) (void)hipSetDevice(c->device);
+    if (c->multi && multi_adopted(c))  // the members hold the window: append to them
+        return fail(c, HSC_ESTATE, "append to an adopted multi context: append to its members");
     for (size_t i = 0; i < n; ++i) {
         if (!w[i].tbname) return fail(c, HSC_EINVAL, "write without table");
         if (w[i].commit_lsn < c->last_append_lsn) return fail(c, HSC_EINVAL, "commit LSNs must not decrease");
@@ -3137,6 +3139,8 @@ int hsc_window_append_log(hsc_ctx *c, const hsc_llog *log)
     if (!c || !log) return HSC_EINVAL;
     std::lock_guard<std::mutex> g(c->mu);
     if (!c->host_only) (void)hipSetDevice(c->device);
+    if (c->multi && multi_adopted(c))
+        return fail(c, HSC_ESTATE, "append to an adopted multi context: append to its members");
     int rc = append_log(c, log);
     if (rc) return rc;
     return c->live ? flush_appends(c, true) : HSC_OK;
@@ -4312,7 +4316,78 @@ void ctx_add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keylen, 
 {
     add_write(c, tid, ix, key, keylen, has_key, lsn);
 }
-int ctx_flush_appends(hsc_ctx *c) { return flush_appends(c); }
+int ctx_flush_appends(hsc_ctx *c, bool lazy) { return flush_appends(c, lazy); }
 int ctx_probe(hsc_ctx *c, const hsc_probe_batch *b) { return probe(c, b); }
 int ctx_default_threads() { return default_threads(); }
+void ctx_par_for(hsc_ctx *c, int nwork, const std::function<void(int)> &f) { par_for(c, true, nwork, f, true); }
+
+// The first and the last row of a built window: gid[2], words[2][W] (row
+// 0's W words, then row n - 1's).
+int ctx_edge_keys(hsc_ctx *c, uint32_t *gid, uint64_t *words)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    if (c->dirty || !c->n || c->host_only) return fail(c, HSC_ESTATE, "no built window");
+    (void)hipSetDevice(c->device);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t last = c->n - 1;
+    HIPCHK(c, hipMemcpy(gid, c->d_gid.as<uint32_t>(), 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(gid + 1, c->d_gid.as<uint32_t>() + last, 4, hipMemcpyDeviceToHost));
+    for (int j = 0; j < c->W; ++j) {
+        HIPCHK(c, hipMemcpy(words + j, c->d_words.as<uint64_t>() + (size_t)j * c->cap, 8, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(words + c->W + j, c->d_words.as<uint64_t>() + (size_t)j * c->cap + last, 8,
+                            hipMemcpyDeviceToHost));
+    }
+    return HSC_OK;
+}
+
+bool ctx_small_fits(hsc_ctx *c, size_t n_txn, size_t n, size_t n_lock)
+{
+    return n_txn <= (size_t)kSmallMaxTxns && small_path(c, (int)n_txn) && n <= kSmallMaxRanges &&
+           n_lock <= kSmallMaxRanges;
+}
+
+// A batch a multi context's front marshalled and routed to member c
+// (hsc_multi.cpp, multi_check_stage).  A batch that fits the small path
+// (st.coh: its arena is fine-grained with the slot's tail) takes one of c's
+// slots -- its kernel reads the columns where the routing wrote them -- and
+// *slot is the slot; else one staged upload + probe + verdict download on
+// c->stream (*slot = -1).  Takes c->mu for the launch only.
+int ctx_stage_launch(hsc_ctx *c, Stage &st, int *slot)
+{
+    std::unique_lock<std::mutex> lk(c->mu);
+    (void)hipSetDevice(c->device);
+    *slot = -1;
+    if (c->dirty) return fail(c, HSC_ESTATE, "member window not built");
+    if (st.coh && ctx_small_fits(c, st.n_txn, st.n, st.n_lock)) {
+        const int k = small_launch(c, st);
+        if (k < 0) return k;
+        c->sm_calls.fetch_add(1, std::memory_order_relaxed);
+        lk.unlock();
+        if (const hipError_t e = small_fire(c, k); e != hipSuccess) {
+            c->small[k].busy.store(false, std::memory_order_release);
+            lk.lock();
+            return fail(c, HSC_EDEVICE, "small batch launch", e);
+        }
+        *slot = k;
+        return HSC_OK;
+    }
+    const int rc = launch_stage(c, st);
+    if (rc) (void)hipStreamSynchronize(c->stream);
+    return rc;
+}
+
+// The verdicts of ctx_stage_launch's batch: rc_out[t] = forced | conflict.
+int ctx_stage_wait(hsc_ctx *c, Stage &st, int slot, int *rc_out)
+{
+    if (slot >= 0) {
+        const char *why = nullptr;
+        hipError_t herr = hipSuccess;
+        const int rc = small_wait(c, slot, c->small[slot].stream, rc_out, &why, &herr);
+        if (rc == HSC_OK) return HSC_OK;
+        std::lock_guard<std::mutex> g(c->mu);
+        return fail(c, rc, why, herr);
+    }
+    (void)hipSetDevice(c->device);
+    return finish_stage(c, st, rc_out);
+}
 }  // namespace hsc

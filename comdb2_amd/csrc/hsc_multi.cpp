@@ -109,6 +109,8 @@ struct MLane {
     HBuf h_cnt;           // fine-grained pinned: the counts the device publishes, + seq word
     uint32_t seq = 0;
     hipEvent_t ev_count = nullptr, ev_scatter = nullptr, ev_probe = nullptr, ev_done = nullptr;
+    hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;  // timed: around this member's probe (hsc_multi_enable_timing)
+    bool timed = false;
     bool used = false;    // ev_done recorded
 };
 
@@ -132,6 +134,17 @@ struct Multi {
     size_t d_sp_woff = 0;
     int d_sp_W = 0;              // words of the uploaded copy (0: stale)
     bool adopted = false;        // members' windows ingested directly (hsc_multi_adopt)
+    // in-process members exchanging like ranks (hsc_multi_set_transport):
+    // send blocks moved by peer copies, unpacked, owner slices gathered
+    bool loop = false;
+    // routing on the host (multi_check_stage, hsc_multi_marshal_routed)
+    Stage mst[kMultiMax];        // each member's share of the last routed batch
+    std::vector<uint8_t> h_own;  // per probe: first | last member << 4
+    std::vector<uint32_t> h_cw;  // per chunk and member: counts, then offsets
+    std::vector<int> h_rc;       // one member's verdicts
+    uint64_t h_calls = 0, h_member_checks = 0, h_routed = 0, h_probes = 0, ns_route = 0;
+    bool timing = false;  // events around every member's probe (per-member probe times)
+    int last_lane = 0;
     // host copies of the last pipeline's counts
     std::vector<uint32_t> cnt;   // [world][world + 2]: per source s: to each d, n_lock, n_txn
     uint64_t batches = 0, routed = 0, probes = 0;
@@ -347,11 +360,11 @@ int multi_build(hsc_ctx *f)
 }
 
 // Rows appended to a built window go to their owners' delta runs.
-int multi_flush_appends(hsc_ctx *f)
+int multi_flush_appends(hsc_ctx *f, bool lazy)
 {
     Multi *M = f->multi;
-    if (!f->live) return HSC_OK;
     if (M->adopted) return mfail(f, HSC_ESTATE, "multi context: append to the members' windows directly");
+    if (!f->live) return HSC_OK;
     const int W = ctx_window_words(f);
     if (f->groups.size() > f->ng_built || W > f->W) {  // the pieces' tables were sized at the build
         f->dirty = true;
@@ -383,7 +396,7 @@ int multi_flush_appends(hsc_ctx *f)
             const GroupInfo &gi = f->groups[f->app_gid[i]];
             ctx_add_write(c, gi.tid, gi.ix, f->app_keys.data() + f->app_koff[i], gi.klen, true, f->app_lsn[i]);
         }
-        const int rc = ctx_flush_appends(c);
+        const int rc = ctx_flush_appends(c, lazy);  // lazy: a small batch's pending tail
         if (rc) return mfail(f, rc, ("member append: " + c->err).c_str());
         if (c->dirty) {  // the member folds inline: rebuild it now (its rows are host-staged)
             const int rb = ctx_ensure_built(c);
@@ -411,6 +424,17 @@ static int lane_stream(hsc_ctx *f, Multi *M, int L, int m)
     MCHK(f, hipStreamCreateWithFlags(&ml.stream, hipStreamNonBlocking));
     for (hipEvent_t *e : {&ml.ev_count, &ml.ev_scatter, &ml.ev_probe, &ml.ev_done})
         MCHK(f, hipEventCreateWithFlags(e, hipEventDisableTiming));
+    return HSC_OK;
+}
+
+// Wait for lane L's previous batch on every local member.
+static int lane_acquire(hsc_ctx *f, Multi *M, int L)
+{
+    for (int m = 0; m < M->nlocal; ++m) {
+        MRC(lane_stream(f, M, L, m));
+        MLane &ml = M->lane[L][m];
+        if (ml.used) MCHK(f, hipEventSynchronize(ml.ev_done));
+    }
     return HSC_OK;
 }
 
@@ -446,9 +470,164 @@ static RouteTarget block_target(uint8_t *b, int W, size_t n, size_t nl)
     return t;
 }
 
-// shared: the local sources number the same read sets (one batch split by
-// probe; member 0 owns every verdict); else each source numbers its own read
-// sets and owns their verdicts (per-rank batches, hsc_multi_probe_device).
+static hsc_probe_batch arena_batch(uint8_t *base, const StageLayout &L, size_t n, size_t nl)
+{
+    hsc_probe_batch b{};
+    b.n = n;
+    b.lo = (const uint64_t *)(base + L.lo);
+    b.hi = (const uint64_t *)(base + L.hi);
+    b.gid = (const uint32_t *)(base + L.gid);
+    b.snap = (const uint64_t *)(base + L.snap);
+    b.txn = (const uint32_t *)(base + L.txn);
+    b.n_lock = nl;
+    b.lock_table = (const uint32_t *)(base + L.lock_table);
+    b.lock_snap = (const uint64_t *)(base + L.lock_snap);
+    b.lock_txn = (const uint32_t *)(base + L.lock_txn);
+    return b;
+}
+
+static hsc_probe_batch view_batch(const ProbeView &p)
+{
+    hsc_probe_batch b{};
+    b.n = p.n;
+    b.lo = p.lo, b.hi = p.hi, b.gid = p.gid, b.snap = p.snap, b.txn = p.txn;
+    b.n_lock = p.n_lock;
+    b.lock_table = p.lock_table, b.lock_snap = p.lock_snap, b.lock_txn = p.lock_txn;
+    return b;
+}
+
+// Steps 6-7 of every pipeline: local member m probes in[m] (read sets
+// numbered batch-wide, tb[N] of them; owner o owns [tb[o], tb[o+1]), every
+// bound a multiple of 64), then each owner's slice of the members' verdict
+// bitmaps is OR-ed into out[m] of the owner's local member.  The members'
+// streams already hold whatever produced in[m] (routing, exchange).
+static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb, uint64_t *const *out)
+{
+    Multi *M = f->multi;
+    const int N = M->world, NL = M->nlocal;
+    const size_t total = tb[N];
+    auto ob = [&](int o) -> size_t { return tb[o] / 64; };
+    auto ow = [&](int o) -> size_t { return (tb[o + 1] - tb[o]) / 64; };
+    // 6. every member probes what it holds
+    for (int m = 0; m < NL; ++m) {
+        MLane &ml = M->lane[L][m];
+        hsc_ctx *c = M->mem[m];
+        hsc_probe_batch b = in[m];
+        b.n_txn = total;
+        MCHK(f, hipSetDevice(c->device));
+        MCHK(f, ml.verdict.ensure(std::max<size_t>(total, 64)));
+        b.verdict = ml.verdict.as<uint8_t>();
+        if (N == 1) {  // one piece: its bitmap is the result
+            b.bitmap = out[0];
+        } else {
+            MCHK(f, ml.bitmap.ensure(std::max<size_t>(total / 8, 8)));
+            b.bitmap = ml.bitmap.as<uint64_t>();
+        }
+        std::lock_guard<std::mutex> g(c->mu);
+        if (c->dirty) return mfail(f, HSC_ESTATE, "multi context: a member's window is not built");
+        if (c->app_last) MCHK(f, hipStreamWaitEvent(ml.stream, c->app_last, 0));  // its appends
+        ml.timed = M->timing;
+        if (ml.timed) {
+            if (!ml.ev_t0) MCHK(f, hipEventCreate(&ml.ev_t0));
+            if (!ml.ev_t1) MCHK(f, hipEventCreate(&ml.ev_t1));
+            MCHK(f, hipEventRecord(ml.ev_t0, ml.stream));
+        }
+        hipStream_t keep = c->stream;
+        c->stream = ml.stream;
+        const int rc = ctx_probe(c, &b);
+        c->stream = keep;
+        if (rc) return mfail(f, rc, ("member probe: " + c->err).c_str());
+        if (ml.timed) MCHK(f, hipEventRecord(ml.ev_t1, ml.stream));
+        MCHK(f, hipEventRecord(ml.ev_probe, ml.stream));
+    }
+    M->last_lane = L;
+    // 7. OR of the members' bitmaps per owner
+    if (N == 1) {
+    } else if (M->rccl) {
+        Rccl &R = rccl();
+        MLane &ml = M->lane[L][0];
+        const int me = M->rank;
+        hipStream_t st = ml.stream;
+        const size_t wme = ow(me);
+        // the other ranks' verdicts on this rank's read sets, OR-ed with its own
+        MCHK(f, ml.gather.ensure(8 * std::max<size_t>(wme * N, 1)));
+        NCHK(f, R.GroupStart());
+        for (int o = 0; o < N; ++o)
+            if (o != me && ow(o))
+                NCHK(f, R.Send(ml.bitmap.as<uint64_t>() + ob(o), 8 * ow(o), ncclUint8, o, M->comm[L], st));
+        if (wme)
+            for (int d = 0; d < N; ++d)
+                if (d != me)
+                    NCHK(f, R.Recv(ml.gather.as<uint64_t>() + (size_t)d * wme, 8 * wme, ncclUint8, d, M->comm[L],
+                                   st));
+        NCHK(f, R.GroupEnd());
+        if (out[0] && wme) {
+            RouteParts parts{};
+            parts.n = N;
+            for (int d = 0; d < N; ++d)
+                parts.p[d] = d == me ? ml.bitmap.as<uint64_t>() + ob(me) : ml.gather.as<uint64_t>() + (size_t)d * wme;
+            MCHK(f, launch_or_slices(parts, wme, out[0], st));
+        }
+    } else if (M->loop) {
+        // the per-rank merge with peer copies in place of RCCL send / receive:
+        // owner o gathers every other member's slice of its read sets into its
+        // gather buffer, then ORs them with its own slice
+        for (int o = 0; o < NL; ++o) {
+            MLane &ol = M->lane[L][o];
+            const size_t wo = ow(o);
+            MCHK(f, hipSetDevice(M->mem[o]->device));
+            MCHK(f, ol.gather.ensure(8 * std::max<size_t>(wo * N, 1)));
+            if (!wo) continue;
+            RouteParts parts{};
+            parts.n = N;
+            for (int d = 0; d < NL; ++d) {
+                if (d == o) {
+                    parts.p[d] = ol.bitmap.as<uint64_t>() + ob(o);
+                    continue;
+                }
+                MLane &dl = M->lane[L][d];
+                uint64_t *dst = ol.gather.as<uint64_t>() + (size_t)d * wo;
+                MCHK(f, hipStreamWaitEvent(ol.stream, dl.ev_probe, 0));
+                MCHK(f, hipMemcpyPeerAsync(dst, M->mem[o]->device, dl.bitmap.as<uint64_t>() + ob(o),
+                                           M->mem[d]->device, 8 * wo, ol.stream));
+                parts.p[d] = dst;
+            }
+            if (out[o]) MCHK(f, launch_or_slices(parts, wo, out[o], ol.stream));
+        }
+    } else {
+        for (int o = 0; o < NL; ++o) {
+            MLane &ml = M->lane[L][o];
+            MCHK(f, hipSetDevice(M->mem[o]->device));
+            if (ow(o) && out[o]) {
+                RouteParts parts{};
+                parts.n = NL;
+                for (int d = 0; d < NL; ++d) {
+                    if (d != o) MCHK(f, hipStreamWaitEvent(ml.stream, M->lane[L][d].ev_probe, 0));
+                    parts.p[d] = M->lane[L][d].bitmap.as<uint64_t>() + ob(o);
+                }
+                MCHK(f, launch_or_slices(parts, ow(o), out[o], ml.stream));
+            }
+        }
+    }
+    // a lane is done once every member's probe and every merge reading it ran
+    for (int o = 0; o < NL; ++o) {
+        MLane &ml = M->lane[L][o];
+        MCHK(f, hipSetDevice(M->mem[o]->device));
+        if (!M->rccl)
+            for (int d = 0; d < NL; ++d)
+                if (d != o) MCHK(f, hipStreamWaitEvent(ml.stream, M->lane[L][d].ev_probe, 0));
+        MCHK(f, hipEventRecord(ml.ev_done, ml.stream));
+        ml.used = true;
+    }
+    M->batches++;
+    return HSC_OK;
+}
+
+// The device-routed pipeline (batches resident on the GPUs, not routed when
+// they were marshalled).  shared: the local sources number the same read
+// sets (one batch split by probe; member 0 owns every verdict); else each
+// source numbers its own read sets and owns their verdicts (per-rank batches,
+// hsc_multi_probe_device).
 static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
 {
     Multi *M = f->multi;
@@ -456,18 +635,25 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
     const int C = N + 2;
     const auto t0 = SteadyClock::now();
     if (M->d_sp_W != W) MRC(upload_splitters(f, M, W));
-    for (int m = 0; m < NL; ++m) {
-        MRC(lane_stream(f, M, L, m));
-        MLane &ml = M->lane[L][m];
-        if (ml.used) MCHK(f, hipEventSynchronize(ml.ev_done));  // this lane's last batch
-    }
+    MRC(lane_acquire(f, M, L));
     const auto t1 = SteadyClock::now();
+    uint64_t *outs[kMultiMax] = {};
+    for (int m = 0; m < NL; ++m) outs[m] = src[m].out;
+    if (N == 1) {  // one piece: no routing, the batch is probed where it is
+        hsc_probe_batch b = view_batch(src[0].p);
+        const size_t tb[2] = {0, r64(src[0].n_txn)};
+        MRC(probe_merge(f, L, &b, tb, outs));
+        M->ns_lane += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+        M->routed += src[0].p.n, M->probes += src[0].p.n;
+        return HSC_OK;
+    }
     Rccl &R = rccl();
+    const bool blocks = M->rccl || M->loop;  // send blocks + unpack (per-rank form)
     // 1. counts per destination: the count kernel's last block (or, across
     // ranks, a one-block copy after the all-gather) stores them to pinned host
     // memory with a sequence word the host spins on -- no copy, no event wait
     M->cnt.assign((size_t)N * C, 0);
-    const bool gather = M->rccl && N > 1;
+    const bool gather = M->rccl;
     const size_t hw = gather ? (size_t)C * N : (size_t)C;  // words published
     for (int m = 0; m < NL; ++m) {
         MLane &ml = M->lane[L][m];
@@ -516,7 +702,7 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
     auto nlk = [&](int s) -> size_t { return M->cnt[(size_t)s * C + N]; };
     auto ntx = [&](int s) -> size_t { return M->cnt[(size_t)s * C + N + 1]; };
     // 2. sizes, offsets, read-set numbering, owners
-    std::vector<size_t> nd(N, 0), tbase(N + 1, 0), lbase(N + 1, 0);
+    std::vector<size_t> nd(N, 0), tbase(N + 1, 0), lbase(N + 1, 0), tb(N + 1, 0);
     std::vector<size_t> off((size_t)N * N, 0);
     for (int d = 0; d < N; ++d)
         for (int s = 0; s < N; ++s) off[(size_t)s * N + d] = nd[d], nd[d] += cnt(s, d);
@@ -527,9 +713,7 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
     const size_t total = shared ? r64(ntx(0)) : tbase[N];  // batch-wide read sets (64-aligned)
     const size_t nlock = lbase[N];
     if (total > 0xFFFFFFFFull) return mfail(f, HSC_EINVAL, "multi batch too large");
-    // owner o's verdict words: [ob[o], ob[o] + ow[o])
-    auto ob = [&](int o) -> size_t { return shared ? 0 : tbase[o] / 64; };
-    auto ow = [&](int o) -> size_t { return shared ? (o == 0 ? total / 64 : 0) : r64(ntx(o)) / 64; };
+    for (int o = 0; o <= N; ++o) tb[o] = shared ? (o == 0 ? 0 : total) : tbase[o];
     // 3. destination buffers
     for (int m = 0; m < NL; ++m) {
         MLane &ml = M->lane[L][m];
@@ -537,9 +721,37 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
         MCHK(f, hipSetDevice(M->mem[m]->device));
         ml.recvL = stage_layout(W, nd[d], d == 0 ? nlock : 0);
         MCHK(f, ml.recv.ensure(std::max<size_t>(ml.recvL.total, 256)));
-        MCHK(f, ml.verdict.ensure(std::max<size_t>(total, 64)));
-        MCHK(f, ml.bitmap.ensure(std::max<size_t>(total / 8, 8)));
     }
+    // send blocks (per-rank form): one per other destination, in destination
+    // order; u[m]: the unpack of what local member m receives
+    std::vector<std::vector<size_t>> soff(NL, std::vector<size_t>(N + 1, 0));
+    std::vector<RouteUnpack> u(NL);
+    std::vector<size_t> rbytes(NL, 0);
+    if (blocks)
+        for (int m = 0; m < NL; ++m) {
+            const int me = M->rank + m;
+            for (int d = 0; d < N; ++d)
+                soff[m][d + 1] = soff[m][d] + (d == me ? 0 : route_block_bytes(W, cnt(me, d), d == 0 ? nlk(me) : 0));
+            RouteUnpack &x = u[m];
+            x = RouteUnpack{};
+            x.N = N;
+            size_t rb = 0;
+            for (int s = 0; s < N; ++s) {
+                x.boff[s] = rb;
+                x.n[s] = s == me ? 0 : (uint32_t)cnt(s, me);
+                x.nl[s] = me == 0 && s != me ? (uint32_t)nlk(s) : 0;
+                x.dst[s] = (uint32_t)off[(size_t)s * N + me];
+                x.ldst[s] = (uint32_t)lbase[s];
+                x.roff[s + 1] = x.roff[s] + x.n[s];
+                x.loff[s + 1] = x.loff[s] + x.nl[s];
+                rb += route_block_bytes(W, x.n[s], x.nl[s]);
+            }
+            rbytes[m] = rb;
+            MLane &ml = M->lane[L][m];
+            MCHK(f, hipSetDevice(M->mem[m]->device));
+            MCHK(f, ml.send.ensure(std::max<size_t>(soff[m][N], 256)));
+            MCHK(f, ml.raw.ensure(std::max<size_t>(rb, 256)));
+        }
     // 4. scatter
     for (int m = 0; m < NL; ++m) {
         MLane &ml = M->lane[L][m];
@@ -550,25 +762,19 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
         a.N = N;
         a.tbase = (uint32_t)tbase[s];
         uint32_t *hc = a.base;
-        if (M->rccl) {
-            // one send block per other rank; this rank's own probes go straight
-            // into its probe columns, at the rows its unpack leaves for them
-            size_t sb = 0;
-            for (int d = 0; d < N; ++d)
-                if (d != s) sb += route_block_bytes(W, cnt(s, d), d == 0 ? nlk(s) : 0);
-            MCHK(f, ml.send.ensure(std::max<size_t>(sb, 256)));
-            size_t o = 0;
+        if (blocks) {
+            // one send block per other destination; this member's own probes go
+            // straight into its probe columns, at the rows its unpack leaves
             for (int d = 0; d < N; ++d) {
                 if (d == s) {
                     a.t[d] = arena_target(ml.recv.as<uint8_t>(), ml.recvL, nd[d]);
                     hc[d] = (uint32_t)off[(size_t)s * N + d];
                     continue;
                 }
-                a.t[d] = block_target(ml.send.as<uint8_t>() + o, W, cnt(s, d), d == 0 ? nlk(s) : 0);
-                o += route_block_bytes(W, cnt(s, d), d == 0 ? nlk(s) : 0);
+                a.t[d] = block_target(ml.send.as<uint8_t>() + soff[m][d], W, cnt(s, d), d == 0 ? nlk(s) : 0);
                 hc[d] = 0;
             }
-            a.lock_base = 0;  // rank 0's own locks first in its lock columns, else a block's
+            a.lock_base = 0;  // member 0's own locks first in its lock columns, else a block's
         } else {
             for (int d = 0; d < N; ++d) {
                 MLane &dl = M->lane[L][d];
@@ -586,127 +792,49 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
         MLane &ml = M->lane[L][0];
         const int me = M->rank;
         hipStream_t st = ml.stream;
-        RouteUnpack u{};
-        u.N = N;
-        size_t rb = 0;
-        for (int s = 0; s < N; ++s) {
-            u.boff[s] = rb;
-            u.n[s] = s == me ? 0 : (uint32_t)cnt(s, me);
-            u.nl[s] = me == 0 && s != me ? (uint32_t)nlk(s) : 0;
-            u.dst[s] = (uint32_t)off[(size_t)s * N + me];
-            u.ldst[s] = (uint32_t)lbase[s];
-            u.roff[s + 1] = u.roff[s] + u.n[s];
-            u.loff[s + 1] = u.loff[s] + u.nl[s];
-            rb += route_block_bytes(W, u.n[s], u.nl[s]);
+        NCHK(f, R.GroupStart());
+        for (int d = 0; d < N; ++d) {
+            const size_t b = soff[0][d + 1] - soff[0][d];
+            if (b) NCHK(f, R.Send(ml.send.as<uint8_t>() + soff[0][d], b, ncclUint8, d, M->comm[L], st));
         }
-        if (N > 1) {
-            MCHK(f, ml.raw.ensure(std::max<size_t>(rb, 256)));
-            NCHK(f, R.GroupStart());
-            size_t o = 0;
-            for (int d = 0; d < N; ++d) {
-                if (d == me) continue;
-                const size_t b = route_block_bytes(W, cnt(me, d), d == 0 ? nlk(me) : 0);
-                if (b) NCHK(f, R.Send(ml.send.as<uint8_t>() + o, b, ncclUint8, d, M->comm[L], st));
-                o += b;
+        for (int s = 0; s < N; ++s) {
+            const size_t b = route_block_bytes(W, u[0].n[s], u[0].nl[s]);
+            if (b) NCHK(f, R.Recv(ml.raw.as<uint8_t>() + u[0].boff[s], b, ncclUint8, s, M->comm[L], st));
+        }
+        NCHK(f, R.GroupEnd());
+        MCHK(f, launch_route_unpack(ml.raw.as<uint8_t>(), u[0], arena_target(ml.recv.as<uint8_t>(), ml.recvL, nd[me]),
+                                    W, st));
+    } else if (M->loop) {
+        // the same blocks moved by peer copies: member d's stream waits for
+        // every source's scatter and copies its block in, then unpacks
+        for (int d = 0; d < NL; ++d) {
+            MLane &dl = M->lane[L][d];
+            MCHK(f, hipSetDevice(M->mem[d]->device));
+            for (int s = 0; s < NL; ++s) {
+                if (s == d) continue;
+                const size_t b = soff[s][d + 1] - soff[s][d];
+                if (!b) continue;
+                MCHK(f, hipStreamWaitEvent(dl.stream, M->lane[L][s].ev_scatter, 0));
+                MCHK(f, hipMemcpyPeerAsync(dl.raw.as<uint8_t>() + u[d].boff[s], M->mem[d]->device,
+                                           M->lane[L][s].send.as<uint8_t>() + soff[s][d], M->mem[s]->device, b,
+                                           dl.stream));
             }
-            for (int s = 0; s < N; ++s) {
-                const size_t b = route_block_bytes(W, u.n[s], u.nl[s]);
-                if (b) NCHK(f, R.Recv(ml.raw.as<uint8_t>() + u.boff[s], b, ncclUint8, s, M->comm[L], st));
-            }
-            NCHK(f, R.GroupEnd());
-            MCHK(f, launch_route_unpack(ml.raw.as<uint8_t>(), u,
-                                        arena_target(ml.recv.as<uint8_t>(), ml.recvL, nd[me]), W, st));
+            MCHK(f, launch_route_unpack(dl.raw.as<uint8_t>(), u[d],
+                                        arena_target(dl.recv.as<uint8_t>(), dl.recvL, nd[d]), W, dl.stream));
         }
     } else {
         for (int d = 0; d < NL; ++d)
             for (int s = 0; s < NL; ++s)
                 if (s != d) MCHK(f, hipStreamWaitEvent(M->lane[L][d].stream, M->lane[L][s].ev_scatter, 0));
     }
-    // 6. every member probes what it received
+    // 6-7. every member probes what it received; OR per owner
+    hsc_probe_batch in[kMultiMax];
     for (int m = 0; m < NL; ++m) {
         MLane &ml = M->lane[L][m];
         const int d = M->rank + m;
-        hsc_ctx *c = M->mem[m];
-        hsc_probe_batch b{};
-        uint8_t *base = ml.recv.as<uint8_t>();
-        b.n = nd[d];
-        b.lo = (const uint64_t *)(base + ml.recvL.lo);
-        b.hi = (const uint64_t *)(base + ml.recvL.hi);
-        b.gid = (const uint32_t *)(base + ml.recvL.gid);
-        b.snap = (const uint64_t *)(base + ml.recvL.snap);
-        b.txn = (const uint32_t *)(base + ml.recvL.txn);
-        b.n_lock = d == 0 ? nlock : 0;
-        b.lock_table = (const uint32_t *)(base + ml.recvL.lock_table);
-        b.lock_snap = (const uint64_t *)(base + ml.recvL.lock_snap);
-        b.lock_txn = (const uint32_t *)(base + ml.recvL.lock_txn);
-        b.n_txn = total;
-        b.verdict = ml.verdict.as<uint8_t>();
-        b.bitmap = ml.bitmap.as<uint64_t>();
-        std::lock_guard<std::mutex> g(c->mu);
-        MCHK(f, hipSetDevice(c->device));
-        if (c->dirty) return mfail(f, HSC_ESTATE, "multi context: a member's window is not built");
-        if (c->app_last) MCHK(f, hipStreamWaitEvent(ml.stream, c->app_last, 0));  // its appends
-        hipStream_t keep = c->stream;
-        c->stream = ml.stream;
-        const int rc = ctx_probe(c, &b);
-        c->stream = keep;
-        if (rc) return mfail(f, rc, ("member probe: " + c->err).c_str());
-        MCHK(f, hipEventRecord(ml.ev_probe, ml.stream));
+        in[m] = arena_batch(ml.recv.as<uint8_t>(), ml.recvL, nd[d], d == 0 ? nlock : 0);
     }
-    // 7. OR of the members' bitmaps per owner
-    if (M->rccl) {
-        MLane &ml = M->lane[L][0];
-        const int me = M->rank;
-        hipStream_t st = ml.stream;
-        const size_t wme = ow(me);
-        // the other ranks' verdicts on this rank's read sets, OR-ed with its own
-        MCHK(f, ml.gather.ensure(8 * std::max<size_t>(wme * N, 1)));
-        if (N > 1) {
-            NCHK(f, R.GroupStart());
-            for (int o = 0; o < N; ++o)
-                if (o != me && ow(o))
-                    NCHK(f, R.Send(ml.bitmap.as<uint64_t>() + ob(o), 8 * ow(o), ncclUint8, o, M->comm[L], st));
-            if (wme)
-                for (int d = 0; d < N; ++d)
-                    if (d != me)
-                        NCHK(f, R.Recv(ml.gather.as<uint64_t>() + (size_t)d * wme, 8 * wme, ncclUint8, d,
-                                       M->comm[L], st));
-            NCHK(f, R.GroupEnd());
-        }
-        if (src[0].out && wme) {
-            RouteParts parts{};
-            parts.n = N;
-            for (int d = 0; d < N; ++d)
-                parts.p[d] = d == me ? ml.bitmap.as<uint64_t>() + ob(me) : ml.gather.as<uint64_t>() + (size_t)d * wme;
-            MCHK(f, launch_or_slices(parts, wme, src[0].out, st));
-        }
-        MCHK(f, hipEventRecord(ml.ev_done, st));
-        ml.used = true;
-    } else {
-        for (int o = 0; o < NL; ++o) {
-            MLane &ml = M->lane[L][o];
-            MCHK(f, hipSetDevice(M->mem[o]->device));
-            if (ow(o) && src[o].out) {
-                RouteParts parts{};
-                parts.n = NL;
-                for (int d = 0; d < NL; ++d) {
-                    if (d != o) MCHK(f, hipStreamWaitEvent(ml.stream, M->lane[L][d].ev_probe, 0));
-                    parts.p[d] = M->lane[L][d].bitmap.as<uint64_t>() + ob(o);
-                }
-                MCHK(f, launch_or_slices(parts, ow(o), src[o].out, ml.stream));
-            }
-        }
-        // a lane is done once every member's probe and every merge reading it ran
-        for (int o = 0; o < NL; ++o) {
-            MLane &ml = M->lane[L][o];
-            MCHK(f, hipSetDevice(M->mem[o]->device));
-            for (int d = 0; d < NL; ++d)
-                if (d != o) MCHK(f, hipStreamWaitEvent(ml.stream, M->lane[L][d].ev_probe, 0));
-            MCHK(f, hipEventRecord(ml.ev_done, ml.stream));
-            ml.used = true;
-        }
-    }
-    M->batches++;
+    MRC(probe_merge(f, L, in, tb.data(), outs));
     const auto t4 = SteadyClock::now();
     auto ns = [](SteadyClock::time_point a, SteadyClock::time_point b) {
         return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
@@ -720,17 +848,180 @@ static int run_pipeline(hsc_ctx *f, int L, MSource *src, bool shared)
     return HSC_OK;
 }
 
-// The front's marshalled batch (host staging st) through the members.
+// ---- routing on the host, at marshal time ---------------------------------------
+// The front's marshalled batch st goes to the members by the same rule as the
+// device routing -- member d gets every probe whose [g || lo, g || hi]
+// overlaps its piece, i.e. owner(g || lo) <= d <= owner(g || hi); the table
+// locks go to member 0, whose table maxima are the global ones -- while the
+// host still has the columns it just wrote.  out[d] receives
+// member d's columns (txn + txn_base), sized with the small path's slot tail
+// when small(d, n_d, nl_d) says so; member 0 only, or every member.
+constexpr size_t kRouteHostChunk = 16384;
+
+static int route_host(hsc_ctx *f, const Stage &st, Stage *out, int only, uint32_t txn_base,
+                      const std::function<bool(int, size_t, size_t)> &small)
+{
+    Multi *M = f->multi;
+    const int N = M->world, W = f->W;
+    if (M->d_sp_W != W) MRC(upload_splitters(f, M, W));
+    const size_t n = st.n, nl = st.n_lock;
+    const int S = (int)M->sp_gid.size();
+    const uint64_t *lo = st.col<uint64_t>(st.L.lo), *hi = st.col<uint64_t>(st.L.hi);
+    const uint64_t *sn = st.col<uint64_t>(st.L.snap);
+    const uint32_t *gid = st.col<uint32_t>(st.L.gid), *txn = st.col<uint32_t>(st.L.txn);
+    const int nw = (int)((n + kRouteHostChunk - 1) / kRouteHostChunk);
+    std::vector<uint8_t> &own = M->h_own;  // ra | rb << 4 per probe (world <= 16)
+    own.resize(std::max<size_t>(n, 1));
+    std::vector<uint32_t> &cw = M->h_cw;   // [chunk][N] counts, then offsets
+    cw.assign((size_t)std::max(nw, 1) * N, 0);
+    auto owner = [&](uint32_t g, const uint64_t *x, size_t i) {
+        int a = 0, b = S;
+        while (a < b) {
+            const int mid = (a + b) >> 1;
+            int c = g == M->sp_gid[mid] ? 0 : (g < M->sp_gid[mid] ? -1 : 1);
+            for (int j = 0; j < W && !c; ++j) {
+                const uint64_t v = x[(size_t)j * n + i], s = M->eff_w[(size_t)j * S + mid];
+                if (v != s) c = v < s ? -1 : 1;
+            }
+            if (c >= 0)
+                a = mid + 1;
+            else
+                b = mid;
+        }
+        return a;
+    };
+    auto pass1 = [&](int w) {
+        const size_t a = (size_t)w * kRouteHostChunk, e = std::min(n, a + kRouteHostChunk);
+        uint32_t *k = &cw[(size_t)w * N];
+        for (size_t i = a; i < e; ++i) {
+            const int ra = S ? owner(gid[i], lo, i) : 0, rb = S ? owner(gid[i], hi, i) : 0;
+            own[i] = (uint8_t)(ra | rb << 4);
+            for (int d = ra; d <= rb; ++d) k[d]++;
+        }
+    };
+    if (nw > 1 && n >= 65536)
+        ctx_par_for(f, nw, pass1);
+    else
+        for (int w = 0; w < nw; ++w) pass1(w);
+    std::vector<size_t> nd(N, 0);
+    for (int w = 0; w < nw; ++w)
+        for (int d = 0; d < N; ++d) {
+            const uint32_t k = cw[(size_t)w * N + d];
+            cw[(size_t)w * N + d] = (uint32_t)nd[d];
+            nd[d] += k;
+        }
+    for (int d = 0; d < N; ++d) {
+        if (only >= 0 && d != only) continue;
+        Stage &o = out[d];
+        const size_t ol = d == 0 ? nl : 0;
+        o.L = stage_layout(W, nd[d], ol);
+        o.n = nd[d], o.n_lock = ol, o.n_txn = st.n_txn;
+        o.coh = small && small(d, nd[d], ol);
+        if (o.arena.ensure(std::max<size_t>(o.L.total + (o.coh ? small_tail(st.n_txn) : 0), 256), true, o.coh) ||
+            o.forced.ensure(std::max<size_t>(st.n_txn, 1), true))
+            return mfail(f, HSC_ENOMEM, "multi routing staging");
+        memset(o.forced.p, 0, std::max<size_t>(st.n_txn, 1));  // the front's forced verdicts are OR-ed in
+        if (ol) {
+            memcpy(o.col<uint32_t>(o.L.lock_table), st.col<uint32_t>(st.L.lock_table), 4 * ol);
+            memcpy(o.col<uint64_t>(o.L.lock_snap), st.col<uint64_t>(st.L.lock_snap), 8 * ol);
+            uint32_t *lt = o.col<uint32_t>(o.L.lock_txn);
+            const uint32_t *sl = st.col<uint32_t>(st.L.lock_txn);
+            for (size_t i = 0; i < ol; ++i) lt[i] = sl[i] + txn_base;
+        }
+    }
+    auto pass2 = [&](int w) {
+        const size_t a = (size_t)w * kRouteHostChunk, e = std::min(n, a + kRouteHostChunk);
+        uint32_t k[kMultiMax];
+        for (int d = 0; d < N; ++d) k[d] = cw[(size_t)w * N + d];
+        for (size_t i = a; i < e; ++i) {
+            const int ra = own[i] & 15, rb = own[i] >> 4;
+            for (int d = ra; d <= rb; ++d) {
+                const size_t r = k[d]++;
+                if (only >= 0 && d != only) continue;
+                Stage &o = out[d];
+                const size_t m = o.n;
+                uint64_t *olo = o.col<uint64_t>(o.L.lo), *ohi = o.col<uint64_t>(o.L.hi);
+                for (int j = 0; j < W; ++j) {
+                    olo[(size_t)j * m + r] = lo[(size_t)j * n + i];
+                    ohi[(size_t)j * m + r] = hi[(size_t)j * n + i];
+                }
+                o.col<uint64_t>(o.L.snap)[r] = sn[i];
+                o.col<uint32_t>(o.L.gid)[r] = gid[i];
+                o.col<uint32_t>(o.L.txn)[r] = txn[i] + txn_base;
+            }
+        }
+    };
+    if (nw > 1 && n >= 65536)
+        ctx_par_for(f, nw, pass2);
+    else
+        for (int w = 0; w < nw; ++w) pass2(w);
+    for (int d = 0; d < N; ++d) M->h_routed += nd[d];
+    M->h_probes += n;
+    return HSC_OK;
+}
+
+// The front's marshalled batch through the members (the drop-in entries on
+// a multi context).  In one process the batch is routed on the host and
+// every member that holds any of its probes checks its share through its own
+// one-GPU path -- a read set touching one member launches that member's
+// small kernel only -- and the verdicts are OR-ed on the host.  A per-rank
+// context has only its own member here: its batch goes through the device
+// routing and the RCCL exchange.
+static int check_stage_device(hsc_ctx *f, Stage &st, int *rc_out);
+
 int multi_check_stage(hsc_ctx *f, Stage &st, int *rc_out)
+{
+    Multi *M = f->multi;
+    if (M->rccl) return check_stage_device(f, st, rc_out);
+    const int N = M->world;
+    const size_t T = st.n_txn;
+    const auto t0 = SteadyClock::now();
+    MRC(route_host(f, st, M->mst, -1, 0, [&](int d, size_t n, size_t nl) {
+        return ctx_small_fits(M->mem[d], T, n, nl);
+    }));
+    const auto t1 = SteadyClock::now();
+    int slot[kMultiMax];
+    bool run[kMultiMax] = {};
+    int rc = HSC_OK;
+    for (int d = 0; d < N && rc == HSC_OK; ++d) {
+        Stage &ms = M->mst[d];
+        if (!ms.n && !ms.n_lock) continue;  // nothing of this batch lives there
+        rc = ctx_stage_launch(M->mem[d], ms, &slot[d]);
+        if (rc)
+            rc = mfail(f, rc, ("member check: " + M->mem[d]->err).c_str());
+        else
+            run[d] = true;
+    }
+    // every launched member is waited for, also after a failed launch
+    const uint8_t *fc = st.forced.as<uint8_t>();
+    for (size_t t = 0; t < T; ++t) rc_out[t] = fc[t] ? 1 : 0;
+    M->h_rc.resize(std::max<size_t>(T, 1));
+    for (int d = 0; d < N; ++d) {
+        if (!run[d]) continue;
+        const int r = ctx_stage_wait(M->mem[d], M->mst[d], slot[d], M->h_rc.data());
+        if (r) {
+            if (rc == HSC_OK) rc = mfail(f, r, ("member check: " + M->mem[d]->err).c_str());
+            continue;
+        }
+        for (size_t t = 0; t < T; ++t) rc_out[t] |= M->h_rc[t];
+        M->h_member_checks++;
+    }
+    M->h_calls++;
+    M->ns_route += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+    return rc;
+}
+
+// Per-rank context: this rank's read sets, uploaded to its member and routed
+// on the devices (count, scatter, RCCL exchange), verdicts back to this rank.
+static int check_stage_device(hsc_ctx *f, Stage &st, int *rc_out)
 {
     Multi *M = f->multi;
     const int W = f->W, NL = M->nlocal, L = 0;
     MSource src[kMultiMax] = {};
     const size_t n = st.n;
+    MRC(lane_acquire(f, M, L));
     for (int m = 0; m < NL; ++m) {
-        MRC(lane_stream(f, M, L, m));
         MLane &ml = M->lane[L][m];
-        if (ml.used) MCHK(f, hipEventSynchronize(ml.ev_done));
         const size_t a = n * m / NL, e = n * (m + 1) / NL, k = e - a;
         const size_t nl = m == 0 ? st.n_lock : 0;
         hipStream_t s = ml.stream;
@@ -766,23 +1057,23 @@ int multi_check_stage(hsc_ctx *f, Stage &st, int *rc_out)
         src[m].n_txn = (uint32_t)st.n_txn;
         src[m].out = nullptr;
     }
-    // the verdicts land on the owner: member 0 here (shared numbering), or
-    // this rank's member for a per-rank context (its own read sets)
+    // the verdicts land on this rank's member (its own read sets)
     MLane &o = M->lane[L][0];
     const size_t words = r64(st.n_txn) / 64;
     MCHK(f, hipSetDevice(M->mem[0]->device));
     MCHK(f, o.out.ensure(8 * std::max<size_t>(words, 1)));
     src[0].out = o.out.as<uint64_t>();
-    MRC(run_pipeline(f, L, src, !M->rccl));
+    MRC(run_pipeline(f, L, src, false));
     if (o.h_io.ensure(8 * words + 64, true)) return mfail(f, HSC_ENOMEM, "multi staging");
     uint64_t *hb = o.h_io.as<uint64_t>();
     if (words) MCHK(f, hipMemcpyAsync(hb, o.out.p, 8 * words, hipMemcpyDeviceToHost, o.stream));
     MCHK(f, hipStreamSynchronize(o.stream));
-    for (int m = 1; m < NL; ++m) MCHK(f, hipEventSynchronize(M->lane[L][m].ev_done));
     const uint8_t *fc = st.forced.as<uint8_t>();
     for (size_t t = 0; t < st.n_txn; ++t) rc_out[t] = (fc[t] || ((hb[t >> 6] >> (t & 63)) & 1)) ? 1 : 0;
     return HSC_OK;
 }
+
+bool multi_adopted(const hsc_ctx *f) { return f && f->multi && f->multi->adopted; }
 
 void multi_destroy(hsc_ctx *f)
 {
@@ -799,13 +1090,14 @@ void multi_destroy(hsc_ctx *f)
                 b->release();
             ml.h_io.release();
             ml.h_cnt.release();
-            for (hipEvent_t e : {ml.ev_count, ml.ev_scatter, ml.ev_probe, ml.ev_done})
+            for (hipEvent_t e : {ml.ev_count, ml.ev_scatter, ml.ev_probe, ml.ev_done, ml.ev_t0, ml.ev_t1})
                 if (e) (void)hipEventDestroy(e);
             (void)hipStreamDestroy(ml.stream);
         }
     if (M->rccl && rccl().ok)
         for (auto &c : M->comm)
             if (c) (void)rccl().CommDestroy(c);
+    for (Stage &st : M->mst) st.release();
     for (int m = 0; m < M->nlocal; ++m) {
         if (!M->mem[m]) continue;
         (void)hipSetDevice(M->mem[m]->device);
@@ -953,6 +1245,14 @@ int hsc_multi_adopt(hsc_ctx *f)
     if (!f || !f->multi) return HSC_EINVAL;
     Multi *M = f->multi;
     std::lock_guard<std::mutex> g(f->mu);
+    // the routing of every probe follows the splitters: without them all
+    // probes would go to member 0 and the other pieces' keys never be probed
+    if (M->world > 1 && !M->sp_given)
+        return mfail(f, HSC_ESTATE, "adopt: set the splitters the members' pieces were cut at first");
+    // one key width: a probe's bound words are those of the front
+    const int W = M->mem[0]->W;
+    for (int m = 1; m < M->nlocal; ++m)
+        if (M->mem[m]->W != W) return mfail(f, HSC_EINVAL, "adopt: members' key widths differ");
     // table maxima: every member answers lock probes with the global ones
     std::vector<uint64_t> tm(f->h_table_max);
     for (int m = 0; m < M->nlocal; ++m) {
@@ -961,6 +1261,22 @@ int hsc_multi_adopt(hsc_ctx *f)
         if (c->groups.size() != f->groups.size()) return mfail(f, HSC_EINVAL, "adopt: member groups differ");
         for (size_t t = 0; t < std::min(tm.size(), c->h_table_max.size()); ++t)
             tm[t] = std::max(tm[t], c->h_table_max[t]);
+    }
+    // every member's rows inside its piece: its first and last key
+    if (M->world > 1) {
+        f->W = W;
+        MRC(upload_splitters(f, M, W));
+        for (int m = 0; m < M->nlocal; ++m) {
+            hsc_ctx *c = M->mem[m];
+            if (!c->n) continue;
+            uint32_t kg[2];
+            uint64_t kw[2 * kMaxWords];
+            const int rc = ctx_edge_keys(c, kg, kw);
+            if (rc) return mfail(f, rc, ("adopt: member keys: " + c->err).c_str());
+            const int me = M->rank + m;
+            if (sp_owner(M, kg[0], kw, W) != me || sp_owner(M, kg[1], kw + W, W) != me)
+                return mfail(f, HSC_EINVAL, "adopt: a member holds keys outside its piece");
+        }
     }
     if (M->rccl && !tm.empty()) {
         hsc_ctx *c = M->mem[0];
@@ -980,8 +1296,6 @@ int hsc_multi_adopt(hsc_ctx *f)
         if (rc) return mfail(f, rc, "adopt: table maxima");
         f->end_lsn = std::max(f->end_lsn, M->mem[m]->end_lsn);
     }
-    int W = 1;
-    for (int m = 0; m < M->nlocal; ++m) W = std::max(W, M->mem[m]->W);
     f->W = W;
     size_t keys = 0;
     for (int m = 0; m < M->nlocal; ++m) keys += M->mem[m]->n;
@@ -1052,6 +1366,123 @@ int hsc_multi_last_counts(hsc_ctx *f, uint32_t *counts, int n)
     for (int s = 0; s < N; ++s)
         for (int d = 0; d < N; ++d)
             counts[s * N + d] = M->cnt.empty() ? 0 : M->cnt[(size_t)s * C + d];
+    return HSC_OK;
+}
+
+int hsc_multi_set_transport(hsc_ctx *f, int transport)
+{
+    if (!f || !f->multi || transport < HSC_MULTI_DIRECT || transport > HSC_MULTI_LOOPBACK) return HSC_EINVAL;
+    Multi *M = f->multi;
+    std::lock_guard<std::mutex> g(f->mu);
+    if (M->rccl) return transport == HSC_MULTI_DIRECT ? HSC_OK : mfail(f, HSC_EINVAL, "per-rank context: RCCL");
+    for (int L = 0; L < kMultiLanes; ++L)  // nothing of the other form in flight
+        for (int m = 0; m < M->nlocal; ++m)
+            if (M->lane[L][m].used) MCHK(f, hipEventSynchronize(M->lane[L][m].ev_done));
+    M->loop = transport == HSC_MULTI_LOOPBACK;
+    return HSC_OK;
+}
+
+int hsc_multi_probe_routed(hsc_ctx *f, const hsc_probe_batch *b, const uint64_t *owner_base, int lane)
+{
+    if (!f || !f->multi || !b || !owner_base || lane < 0 || lane >= kMultiLanes) return HSC_EINVAL;
+    Multi *M = f->multi;
+    const int N = M->world, NL = M->nlocal;
+    std::lock_guard<std::mutex> g(f->mu);
+    if (f->dirty) return mfail(f, HSC_ESTATE, "window not built");
+    size_t tb[kMultiMax + 1];
+    for (int o = 0; o <= N; ++o) {
+        tb[o] = (size_t)owner_base[o];
+        if ((o && tb[o] < tb[o - 1]) || (tb[o] & 63) || (o == 0 && tb[0]) || tb[o] > 0xFFFFFFFFull)
+            return mfail(f, HSC_EINVAL, "owner bases: ascending multiples of 64 from 0");
+    }
+    hsc_probe_batch in[kMultiMax];
+    uint64_t *outs[kMultiMax] = {};
+    for (int m = 0; m < NL; ++m) {
+        const int o = M->rank + m;
+        if (b[m].n > 0xFFFFFFFFull || b[m].n_lock > 0xFFFFFFFFull || ((tb[o + 1] > tb[o]) && !b[m].bitmap) ||
+            (b[m].n_lock && o != 0))
+            return mfail(f, HSC_EINVAL, "multi routed batch (locks go to member 0)");
+        in[m] = b[m];
+        outs[m] = b[m].bitmap;
+    }
+    MRC(lane_acquire(f, M, lane));
+    MRC(probe_merge(f, lane, in, tb, outs));
+    for (int m = 0; m < NL; ++m) M->routed += b[m].n, M->probes += b[m].n;
+    return HSC_OK;
+}
+
+int hsc_multi_marshal_routed(hsc_ctx *f, const hsc_readsets *rs, int member, uint32_t txn_base,
+                             const hsc_marshalled **out)
+{
+    if (!f || !f->multi || !rs || !out || member < -1 || member >= f->multi->world) return HSC_EINVAL;
+    const hsc_marshalled *m = nullptr;
+    int rc = hsc_marshal_readsets(f, rs, &m);
+    if (rc) return rc;
+    Multi *M = f->multi;
+    std::lock_guard<std::mutex> g(f->mu);
+    Stage &st = f->stage[0];
+    rc = route_host(f, st, M->mst, member, txn_base, nullptr);
+    if (rc) return rc;
+    return hsc_multi_routed_member(f, member < 0 ? 0 : member, out);
+}
+
+int hsc_multi_routed_member(hsc_ctx *f, int member, const hsc_marshalled **out)
+{
+    if (!f || !f->multi || !out || member < 0 || member >= f->multi->world) return HSC_EINVAL;
+    Multi *M = f->multi;
+    const Stage &st = f->stage[0];
+    const Stage &o = M->mst[member];
+    static thread_local hsc_marshalled r;
+    r = hsc_marshalled{};
+    r.n = o.n;
+    r.n_lock = o.n_lock;
+    r.n_txn = o.n_txn;
+    r.words = f->W;
+    r.lo = o.col<uint64_t>(o.L.lo);
+    r.hi = o.col<uint64_t>(o.L.hi);
+    r.gid = o.col<uint32_t>(o.L.gid);
+    r.snap = o.col<uint64_t>(o.L.snap);
+    r.txn = o.col<uint32_t>(o.L.txn);
+    r.lock_table = o.col<uint32_t>(o.L.lock_table);
+    r.lock_snap = o.col<uint64_t>(o.L.lock_snap);
+    r.lock_txn = o.col<uint32_t>(o.L.lock_txn);
+    r.forced = st.forced.as<uint8_t>();
+    *out = &r;
+    return HSC_OK;
+}
+
+int hsc_multi_enable_timing(hsc_ctx *f, int on)
+{
+    if (!f || !f->multi) return HSC_EINVAL;
+    f->multi->timing = on != 0;
+    return HSC_OK;
+}
+
+int hsc_multi_member_probe_ms(hsc_ctx *f, float *out, int n)
+{
+    if (!f || !f->multi || !out || n < f->multi->nlocal) return HSC_EINVAL;
+    Multi *M = f->multi;
+    for (int m = 0; m < M->nlocal; ++m) {
+        MLane &ml = M->lane[M->last_lane][m];
+        out[m] = 0;
+        if (!ml.timed || !ml.ev_t1) continue;
+        MCHK(f, hipSetDevice(M->mem[m]->device));
+        MCHK(f, hipEventSynchronize(ml.ev_t1));
+        MCHK(f, hipEventElapsedTime(&out[m], ml.ev_t0, ml.ev_t1));
+    }
+    return HSC_OK;
+}
+
+int hsc_multi_route_stats(hsc_ctx *f, double out[6])
+{
+    if (!f || !f->multi || !out) return HSC_EINVAL;
+    Multi *M = f->multi;
+    out[0] = (double)M->h_calls;
+    out[1] = (double)M->h_member_checks;
+    out[2] = (double)M->h_probes;
+    out[3] = (double)M->h_routed;
+    out[4] = M->h_calls ? (double)M->ns_route / (double)M->h_calls * 1e-3 : 0.0;
+    out[5] = (double)M->world;
     return HSC_OK;
 }
 

@@ -118,7 +118,8 @@ class Marshalled(C.Structure):
 
 class CollectorStats(C.Structure):
     _fields_ = [("calls", C.c_uint64), ("batches", C.c_uint64), ("max_batch", C.c_uint64),
-                ("busy_ns", C.c_uint64), ("gate_ns", C.c_uint64), ("handout_ns", C.c_uint64)]
+                ("busy_ns", C.c_uint64), ("gate_ns", C.c_uint64), ("handout_ns", C.c_uint64),
+                ("pass_ns", C.c_uint64)]
 
 
 class SmallStats(C.Structure):
@@ -159,7 +160,9 @@ EXPORTS = [
     "hsc_multi_create", "hsc_multi_unique_ids", "hsc_multi_create_rank", "hsc_multi_world",
     "hsc_multi_rank", "hsc_multi_local", "hsc_multi_member", "hsc_multi_set_splitters",
     "hsc_multi_adopt", "hsc_multi_probe_device", "hsc_multi_stats", "hsc_multi_last_counts",
-    "hsc_multi_phase_stats",
+    "hsc_multi_phase_stats", "hsc_multi_set_transport", "hsc_multi_probe_routed",
+    "hsc_multi_marshal_routed", "hsc_multi_routed_member", "hsc_multi_enable_timing",
+    "hsc_multi_member_probe_ms", "hsc_multi_route_stats",
     "hsc_marshal_arrs", "hsc_batch_stats",
 ]
 MULTI_ID_BYTES = 2 * 128  # hsc_multi_unique_ids: one RCCL id per lane
@@ -276,6 +279,14 @@ def load() -> C.CDLL:
         "hsc_multi_stats": (C.c_int, [_p, _p]),
         "hsc_multi_last_counts": (C.c_int, [_p, _p, C.c_int]),
         "hsc_multi_phase_stats": (C.c_int, [_p, _p]),
+        "hsc_multi_set_transport": (C.c_int, [_p, C.c_int]),
+        "hsc_multi_probe_routed": (C.c_int, [_p, _p, _p, C.c_int]),
+        "hsc_multi_marshal_routed": (C.c_int, [_p, C.POINTER(_ReadSets), C.c_int, C.c_uint32,
+                                               C.POINTER(C.POINTER(Marshalled))]),
+        "hsc_multi_route_stats": (C.c_int, [_p, _p]),
+        "hsc_multi_routed_member": (C.c_int, [_p, C.c_int, C.POINTER(C.POINTER(Marshalled))]),
+        "hsc_multi_enable_timing": (C.c_int, [_p, C.c_int]),
+        "hsc_multi_member_probe_ms": (C.c_int, [_p, _p, C.c_int]),
     }
     for name, (res, args) in sig.items():
         if not hasattr(lib, name) and os.environ.get("HSC_LIB"):
@@ -736,7 +747,7 @@ class Validator:
                           "hsc_collector_get_stats")
                 st.update(batches=cs.batches, max_batch=cs.max_batch,
                           mean_batch=cs.calls / max(1, cs.batches),
-                          device_pass_us=cs.busy_ns / 1e3 / max(1, cs.batches),
+                          device_pass_us=cs.pass_ns / 1e3 / max(1, cs.batches),
                           busy_frac=cs.busy_ns / 1e9 / max(res.seconds, 1e-9),
                           gate_us=cs.gate_ns / 1e3 / max(1, cs.batches),
                           handout_us=cs.handout_ns / 1e3 / max(1, cs.batches))
@@ -1043,6 +1054,81 @@ class MultiValidator(Validator):
 
     def adopt(self) -> None:
         self._chk(self.lib.hsc_multi_adopt(self.ctx), "hsc_multi_adopt")
+
+    def set_transport(self, loopback: bool) -> None:
+        """In-process members: HSC_MULTI_LOOPBACK runs the per-rank exchange
+        (send blocks, unpack, owner slices) with peer copies in place of RCCL."""
+        self._chk(self.lib.hsc_multi_set_transport(self.ctx, int(bool(loopback))),
+                  "hsc_multi_set_transport")
+
+    def marshal_routed(self, rs: ReadSets, member: int, txn_base: int = 0) -> dict:
+        """Marshal rs and route it on the host: member's columns (read-set
+        numbers + txn_base; table locks for member 0), forced of the batch."""
+        s, keep = readsets_struct(rs)
+        mp = C.POINTER(Marshalled)()
+        self._chk(self.lib.hsc_multi_marshal_routed(self.ctx, C.byref(s), member, txn_base,
+                                                    C.byref(mp)), "hsc_multi_marshal_routed")
+        return self._marshalled(mp.contents)
+
+    def routed_shares(self, shares: Sequence[ReadSets], members: Sequence[int]) -> dict:
+        """The global batch = the owners' shares (share o owned by member o):
+        each marshalled once and routed on the host; per member in `members`
+        its columns of all shares concatenated, read sets numbered batch-wide
+        (share o from owner_base[o], every base a multiple of 64).
+        -> {member: columns}; every entry carries owner_base and forced[o]
+        (share o's host-decided verdicts)."""
+        base = [0]
+        for rs in shares:
+            base.append(base[-1] + (rs.ntxn + 63) // 64 * 64)
+        parts = {m: [] for m in members}
+        forced = []
+        for o, rs in enumerate(shares):
+            s, keep = readsets_struct(rs)
+            mp = C.POINTER(Marshalled)()
+            who = members[0] if len(members) == 1 else -1  # -1: route to every member
+            self._chk(self.lib.hsc_multi_marshal_routed(self.ctx, C.byref(s), who, base[o], C.byref(mp)),
+                      "hsc_multi_marshal_routed")
+            forced.append(self._marshalled(mp.contents)["forced"])
+            for m in members:
+                self._chk(self.lib.hsc_multi_routed_member(self.ctx, m, C.byref(mp)),
+                          "hsc_multi_routed_member")
+                parts[m].append(self._marshalled(mp.contents))
+        out = {}
+        for m, ps in parts.items():
+            cat = lambda k: np.concatenate([p[k] for p in ps])
+            out[m] = dict(words=ps[0]["words"], n=sum(p["n"] for p in ps),
+                          n_lock=sum(p["n_lock"] for p in ps), n_txn=base[-1],
+                          owner_base=np.array(base, np.uint64),
+                          lo=np.concatenate([p["lo"] for p in ps], axis=1),
+                          hi=np.concatenate([p["hi"] for p in ps], axis=1),
+                          gid=cat("gid"), snap=cat("snap"), txn=cat("txn"), lock_table=cat("lock_table"),
+                          lock_snap=cat("lock_snap"), lock_txn=cat("lock_txn"), forced=forced)
+        return out
+
+    def enable_member_timing(self, on: bool = True) -> None:
+        self._chk(self.lib.hsc_multi_enable_timing(self.ctx, int(on)), "hsc_multi_enable_timing")
+
+    def member_probe_ms(self) -> np.ndarray:
+        """Per local member: its probe's device ms in the last routed batch."""
+        out = np.zeros(max(1, self.nlocal), np.float32)
+        self._chk(self.lib.hsc_multi_member_probe_ms(self.ctx, out.ctypes.data, len(out)),
+                  "hsc_multi_member_probe_ms")
+        return out[:self.nlocal]
+
+    def probe_routed(self, batches: Sequence[ProbeBatch], owner_base: Sequence[int],
+                     lane: int = 0) -> None:
+        """Batches routed at marshal time (one per local member), read sets
+        numbered batch-wide; owner o owns [owner_base[o], owner_base[o+1])."""
+        arr = (ProbeBatch * len(batches))(*batches)
+        ob = np.ascontiguousarray(owner_base, np.uint64)
+        self._chk(self.lib.hsc_multi_probe_routed(self.ctx, arr, ob.ctypes.data, lane),
+                  "hsc_multi_probe_routed")
+
+    def route_stats(self) -> dict:
+        out = np.zeros(6, np.float64)
+        self._chk(self.lib.hsc_multi_route_stats(self.ctx, out.ctypes.data), "hsc_multi_route_stats")
+        return {"calls": int(out[0]), "member_checks": int(out[1]), "probes": int(out[2]),
+                "rows": int(out[3]), "route_us_per_call": float(out[4]), "world": int(out[5])}
 
     def probe_device_multi(self, batches: Sequence[ProbeBatch], lane: int = 0) -> None:
         arr = (ProbeBatch * len(batches))(*batches)

@@ -422,9 +422,11 @@ typedef struct hsc_collector_stats {
     uint64_t calls;      /* hsc_collector_check calls that queued */
     uint64_t batches;    /* device passes run for them */
     uint64_t max_batch;  /* largest batch */
-    uint64_t busy_ns;    /* time inside the batches' device passes */
+    uint64_t busy_ns;    /* wall time with at least one batch in flight (the union of
+                            the passes' intervals: busy_ns / elapsed <= 1) */
     uint64_t gate_ns;    /* leaders waiting for a device pass to end (in-flight bound) */
     uint64_t handout_ns; /* leaders waking their batches' callers */
+    uint64_t pass_ns;    /* sum of the passes' durations (> busy_ns when they overlap) */
 } hsc_collector_stats;
 /* Small-batch path (batches of <= 1024 read sets over a narrow window: one
  * k_small_narrow launch over fine-grained host memory) phase totals since
@@ -547,15 +549,21 @@ int hsc_enable_timing(hsc_ctx *ctx, int on);
  * is cut into `world` contiguous pieces of the composite key space (gid, key
  * words) -- member d holds the keys K with sp[d-1] <= K < sp[d] -- one per
  * member context.  The context itself keeps the log decode, dictionaries and
- * window rules and marshals every batch on the host; each member then routes
- * its share of the probes on its GPU to the members whose pieces their
- * [lo, hi] overlap, every member joins what it received against its piece,
- * and the members' verdict bitmaps are OR-ed per read-set owner.  Members in
- * one process exchange by direct stores into each other's memory (xGMI peer
- * access, enabled at creation; several members may share one GPU); members
- * in different processes (one per GPU, hsc_multi_create_rank) exchange over
- * RCCL (grouped ncclSend / ncclRecv, librccl loaded at run time).  Verdicts
- * equal those of one context holding the whole window.  Not on a multi
+ * window rules and marshals every batch on the host.  A range [g||lo, g||hi]
+ * goes to the members whose pieces it overlaps (owner(g||lo) ..
+ * owner(g||hi)), table locks to member 0 (it holds the global table maxima).
+ * In one process the drop-in entries route while marshalling: each member
+ * that holds any probe of the batch checks its share through its own one-GPU
+ * path (the small-batch kernel for a lone call), and the verdicts are OR-ed.
+ * Batches already resident on the GPUs are either routed there
+ * (hsc_multi_probe_device: route kernels, then an exchange -- direct stores
+ * between members of one process over xGMI peer access, RCCL grouped
+ * ncclSend / ncclRecv between processes) or arrive routed
+ * (hsc_multi_probe_routed); every member joins its probes against its piece
+ * and the members' verdict bitmaps are OR-ed per read-set owner.  A per-rank
+ * context (one process per GPU, hsc_multi_create_rank; librccl loaded at run
+ * time) routes its drop-in batches on the devices.  Verdicts equal those of
+ * one context holding the whole window.  Not on a multi
  * context: hsc_set_stream, hsc_probe_device, hsc_window_ingest_device (ingest
  * the members directly, then hsc_multi_adopt), hsc_rw_edges, the graph and
  * coalesce calls (use a member). */
@@ -580,8 +588,19 @@ int hsc_multi_set_splitters(hsc_ctx *ctx, size_t S, const uint32_t *gid, const u
 /* The members' windows, ingested directly (hsc_window_ingest_device on
  * hsc_multi_member, each holding exactly its piece's rows), become the
  * context's window; table maxima are max-merged over all members (an RCCL
- * all-reduce across ranks).  Collective on a per-rank context. */
+ * all-reduce across ranks).  Collective on a per-rank context.  HSC_ESTATE
+ * without splitters (world > 1); HSC_EINVAL when the members' key widths
+ * differ or a member's first or last key lies outside its piece.  Appends
+ * then go to the members (the context's append entries return HSC_ESTATE). */
 int hsc_multi_adopt(hsc_ctx *ctx);
+/* In-process contexts: HSC_MULTI_DIRECT (default: the device routing stores
+ * into the other members' probe columns, the merge reads their bitmaps) or
+ * HSC_MULTI_LOOPBACK (the per-rank form with peer copies in place of RCCL:
+ * send blocks, k_route_unpack, owner slices gathered and OR-ed -- what a
+ * per-rank context runs, on one process). */
+#define HSC_MULTI_DIRECT 0
+#define HSC_MULTI_LOOPBACK 1
+int hsc_multi_set_transport(hsc_ctx *ctx, int transport);
 /* Device-resident batches, one per local member (pointers on its GPU), each
  * numbering its own read sets 0..b[i].n_txn-1: routed, probed and merged;
  * b[i].bitmap (ceil(n_txn / 64) words) receives the merged verdict bits of
@@ -590,6 +609,34 @@ int hsc_multi_adopt(hsc_ctx *ctx);
  * the work is enqueued (the host waits for the routing counts only).
  * Collective on a per-rank context. */
 int hsc_multi_probe_device(hsc_ctx *ctx, const hsc_probe_batch *b, int lane);
+/* Device-resident batches routed when they were marshalled, one per local
+ * member: b[i] holds exactly the probes whose [lo, hi] overlaps member i's
+ * piece (hsc_multi_marshal_routed; table locks on member 0 only), read sets
+ * numbered batch-wide: owner o owns [owner_base[o], owner_base[o + 1])
+ * (world + 1 ascending multiples of 64 from 0), b[i].bitmap receives the
+ * merged bits of member i's own read sets.  Every member probes its batch in
+ * place; the bitmaps are OR-ed per owner (RCCL send / receive of the owners'
+ * slices across ranks).  No routing and no probe exchange on the devices.
+ * lane as for hsc_multi_probe_device; collective on a per-rank context. */
+int hsc_multi_probe_routed(hsc_ctx *ctx, const hsc_probe_batch *b, const uint64_t *owner_base, int lane);
+/* Marshal rs (hsc_marshal_readsets) and route it on the host: *out = the
+ * columns of member `member` (read-set numbers + txn_base; table locks when
+ * member == 0), host memory valid until the next marshal on ctx.  forced =
+ * the whole batch's host-decided verdicts. */
+int hsc_multi_marshal_routed(hsc_ctx *ctx, const hsc_readsets *rs, int member, uint32_t txn_base,
+                             const hsc_marshalled **out);
+/* member >= 0 above; member = -1 routes the batch to every member, *out =
+ * member 0's columns and hsc_multi_routed_member the others' (same life). */
+int hsc_multi_routed_member(hsc_ctx *ctx, int member, const hsc_marshalled **out);
+/* Events around every member's probe of the routed pipelines (diagnostics,
+ * per-member imbalance); out[i] = local member i's probe ms of the last batch
+ * (waits for it). */
+int hsc_multi_enable_timing(hsc_ctx *ctx, int on);
+int hsc_multi_member_probe_ms(hsc_ctx *ctx, float *out, int n);
+/* Host routing of the drop-in entries: out[6] = calls, member checks run,
+ * probes routed, probe rows placed (> probes when ranges straddle pieces),
+ * mean us routing per call, world. */
+int hsc_multi_route_stats(hsc_ctx *ctx, double out[6]);
 /* out[4]: routed batches, probes routed (sources), probe rows received
  * (destinations; > probes when ranges straddle pieces), local members. */
 int hsc_multi_stats(hsc_ctx *ctx, uint64_t out[4]);

@@ -1,0 +1,48 @@
+"""CPU: bench.py's --gpus N dispatch (the driver's scaling runs).  Without a
+launcher, --gpus N > 1 runs the in-process multi-GPU context over devices
+0..N-1 and must refuse to run -- never print a one-GPU line -- when fewer
+GPUs are visible; under torchrun the world size must match --gpus."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    env["CUDA_VISIBLE_DEVICES"] = ""  # no GPU, whatever the host has
+    env["HIP_VISIBLE_DEVICES"] = ""
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=300)
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_gpus_n_without_devices_exits_nonzero(n):
+    r = _run(["--gpus", str(n), "--steps", "1", "--warmup", "0", "--no-cpu", "--no-pmc"])
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert f"bench.py --gpus {n}: only 0 GPU(s) visible" in r.stderr
+    for line in r.stdout.splitlines():  # no result line at all
+        with pytest.raises(ValueError):
+            json.loads(line)
+
+
+def test_gpus_must_match_world_size():
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0"],
+             {"WORLD_SIZE": "4", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2, r.stderr[-2000:]
+    assert "bench.py --gpus 2 under WORLD_SIZE 4" in r.stderr
+
+
+def test_multi_line_reports_devices_used():
+    """Static check of the line bench_multi prints: n_gpus is the set of
+    devices the members ran on (in process) or the world size (torchrun)."""
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert '"n_gpus": len(set(devs)) if inproc else N' in src
+    assert "args.gpus > 1" in src.split("def main():")[1]

@@ -1,12 +1,17 @@
 """GPU: the multi-GPU context behind the C ABI (hsc_multi.cpp, hsc_route.hip;
 SURVEY.md §8(e)).  On the one GPU of a test box, 2 and 4 member contexts
-share cuda:0 -- the in-process path, where every member routes its share of
-the probes on the device and stores them straight into the other members'
-probe columns, exactly as members on separate GPUs do over xGMI -- and a
-per-rank context of world 1 runs the RCCL path (count all-gather, grouped
-send / receive of the routed blocks, unpack, bitmap exchange).  Verdicts are
-checked against the oracle (oracle/serial_oracle.c on the whole log) and
-against one context holding the whole window."""
+share cuda:0:
+- the drop-in entries route each batch on the host while marshalling, and
+  every member holding a probe checks its share (its small kernel for a
+  lone call);
+- device-resident batches routed on the device: direct stores into the
+  other members' probe columns (the in-process path over xGMI), or the
+  loopback transport -- the per-rank form (send blocks, k_route_unpack,
+  owner slices gathered and OR-ed) with peer copies in place of RCCL;
+- batches routed at marshal time (hsc_multi_probe_routed), both merges;
+- a per-rank context of world 1 (RCCL loaded; one piece: no routing).
+Verdicts are checked against the oracle (oracle/serial_oracle.c on the whole
+log) and against one context holding the whole window."""
 import json
 import os
 
@@ -85,10 +90,9 @@ def test_config3_vs_oracle_and_one_context(multi, oracle_mod):
     np.testing.assert_array_equal(got, ref)
     assert 0.1 < got.mean() < 0.9
     _sample_vs_oracle(oracle_mod, got, a.readsets, log, 20)
-    st = multi.multi_stats()
-    assert st["routed"] >= st["probes"] > 0
-    cnt = multi.last_counts()
-    assert (cnt.sum(axis=0) > 0).all()  # every member received probes
+    st = multi.route_stats()
+    assert st["rows"] >= st["probes"] > 0
+    assert st["member_checks"] >= multi.world  # every member held probes of the batch
 
 
 def test_config5_vs_oracle_and_one_context(multi, oracle_mod):
@@ -128,8 +132,8 @@ def test_explicit_splitters_and_straddling_ranges(oracle_mod):
         m.set_splitters(gid[k], words[:, k])
         got = m.check_readsets(rs)
         np.testing.assert_array_equal(got != 0, want != 0)
-        st = m.multi_stats()
-        assert st["routed"] > 0
+        st = m.route_stats()
+        assert st["rows"] > st["probes"] > 0  # straddling ranges went to both members
     finally:
         m.close()
 
@@ -200,10 +204,128 @@ def test_probe_device_per_member_batches(oracle_mod, n):
         one.close()
 
 
+@pytest.mark.parametrize("n", [2, 4])
+def test_loopback_transport_per_member_batches(oracle_mod, n):
+    """The per-rank pipeline's data paths on one process: send blocks laid out
+    per destination (block_target), moved by peer copies in place of
+    ncclSend / ncclRecv, k_route_unpack's row and lock offsets, and the owner
+    slices gathered and OR-ed -- every step a per-rank context runs between
+    ranks, against one context's verdicts; both lanes."""
+    a = config3_arrays(n_writes=200_000, n_txn=3000 * n)
+    log = config3_log(a)
+    one = Validator(0)
+    m = MultiValidator([0] * n)
+    try:
+        one.ingest_log(log)
+        m.ingest_log(log)
+        m.set_transport(True)
+        dev = torch.device("cuda", 0)
+        T = 3000
+        parts = [a.readsets.subset(np.arange(i * T, (i + 1) * T)) for i in range(n)]
+        want = [one.check_readsets(p) != 0 for p in parts]
+        batches = [_device_batch(m, p, dev) for p in parts]
+        torch.cuda.synchronize()
+        for lane in (0, 1, 1):
+            for b in batches:
+                b["bits"].zero_()
+            torch.cuda.synchronize()
+            m.probe_device_multi([b["struct"] for b in batches], lane=lane)
+            torch.cuda.synchronize()
+            for i, b in enumerate(batches):
+                np.testing.assert_array_equal(_bits(b, T), want[i], err_msg=f"member {i} lane {lane}")
+        cnt = m.last_counts()
+        assert (cnt - np.diag(np.diag(cnt))).sum() > 0  # probes crossed members
+        assert sum(b["n_lock"] for b in batches) > 0    # locks travelled to member 0
+        # the drop-in entry is unaffected by the transport (host routing)
+        np.testing.assert_array_equal(m.check_readsets(parts[0]) != 0, want[0])
+    finally:
+        m.close()
+        one.close()
+
+
+def _routed_device_batch(mb, dev, bits_words):
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    b = dict(lo=t(mb["lo"]), hi=t(mb["hi"]), gid=t(mb["gid"]), snap=t(mb["snap"]), txn=t(mb["txn"]),
+             lock_table=t(mb["lock_table"]), lock_snap=t(mb["lock_snap"]), lock_txn=t(mb["lock_txn"]))
+    b["bits"] = torch.zeros(max(bits_words, 1), dtype=torch.int64, device=dev)
+    b["verdict"] = torch.zeros(max(mb["n_txn"], 1), dtype=torch.uint8, device=dev)
+    b["struct"] = hsc.ProbeBatch(mb["n"], b["lo"].data_ptr(), b["hi"].data_ptr(), b["gid"].data_ptr(),
+                                 b["snap"].data_ptr(), b["txn"].data_ptr(), mb["n_lock"],
+                                 b["lock_table"].data_ptr(), b["lock_snap"].data_ptr(),
+                                 b["lock_txn"].data_ptr(), mb["n_txn"], b["verdict"].data_ptr(),
+                                 b["bits"].data_ptr())
+    return b
+
+
+@pytest.mark.parametrize("n,loop", [(2, False), (4, False), (2, True), (3, True)])
+def test_probe_routed_at_marshal(oracle_mod, n, loop):
+    """hsc_multi_probe_routed: the global batch = n owners' shares (sizes not
+    multiples of 64), each share marshalled and routed on the host
+    (hsc_multi_marshal_routed), every member probes only the ranges that
+    overlap its piece, the bitmaps are OR-ed per owner (peer reads, or the
+    per-rank slice exchange by loopback copies)."""
+    a = config3_arrays(n_writes=200_000, n_txn=2500 * n + 7)
+    log = config3_log(a)
+    one = Validator(0)
+    m = MultiValidator([0] * n)
+    try:
+        one.ingest_log(log)
+        m.ingest_log(log)
+        m.check_readsets(a.readsets.subset(np.arange(4)))  # built and partitioned
+        m.set_transport(loop)
+        dev = torch.device("cuda", 0)
+        cuts = [0] + [2500 * i + 3 * i for i in range(1, n)] + [a.readsets.ntxn]
+        shares = [a.readsets.subset(np.arange(cuts[i], cuts[i + 1])) for i in range(n)]
+        want = [one.check_readsets(s) != 0 for s in shares]
+        rt = m.routed_shares(shares, list(range(n)))
+        routed = [rt[i] for i in range(n)]
+        ob = routed[0]["owner_base"]
+        batches = [_routed_device_batch(routed[i], dev, int((ob[i + 1] - ob[i]) // 64)) for i in range(n)]
+        assert sum(r["n"] for r in routed) >= sum(m.marshal(s)["n"] for s in shares)
+        assert all(r["n_lock"] == 0 for r in routed[1:])
+        torch.cuda.synchronize()
+        for lane in (0, 1):
+            for b in batches:
+                b["bits"].zero_()
+            torch.cuda.synchronize()
+            m.probe_routed([b["struct"] for b in batches], ob, lane=lane)
+            torch.cuda.synchronize()
+            for i, b in enumerate(batches):
+                T = shares[i].ntxn
+                got = np.unpackbits(b["bits"].cpu().numpy().view(np.uint8), bitorder="little")[:T]
+                got = np.maximum(got, routed[0]["forced"][i]).astype(bool)
+                np.testing.assert_array_equal(got, want[i], err_msg=f"owner {i} lane {lane}")
+    finally:
+        m.close()
+        one.close()
+
+
+def test_lone_calls_route_to_one_member(oracle_mod):
+    """The drop-in entry on a 2-member context, one read set per call (the
+    per-transaction pattern of db/toblock.c:4777-4800): the host routing
+    sends each call only to the members its ranges overlap, whose small
+    kernels answer it."""
+    log, rs = random_case(960, n_commits=200, n_txn=60)
+    want, _, _ = oracle_mod.check(log, rs)
+    m = MultiValidator([0, 0])
+    try:
+        m.ingest_log(log)
+        got = np.array([m.check_readsets(rs.subset(np.array([t])))[0] for t in range(rs.ntxn)])
+        np.testing.assert_array_equal(got != 0, want != 0)
+        st = m.route_stats()
+        assert st["calls"] >= rs.ntxn
+        assert st["member_checks"] < 2 * st["calls"]  # some calls touched one member only
+        small = sum(m.member(i).small_stats()["calls"] for i in range(2))
+        assert small >= st["member_checks"] // 2
+    finally:
+        m.close()
+
+
 def test_rccl_world1_rank_context(oracle_mod):
-    """The per-rank (RCCL) path at world 1 on the box's one GPU: counts
-    all-gather, grouped send / receive of the routed blocks to itself, unpack,
-    bitmap exchange -- every RCCL branch of the pipeline."""
+    """A per-rank (RCCL) context at world 1 on the box's one GPU: librccl
+    loaded and the communicators built; one piece, so the drop-in batch and a
+    device batch are probed where they are (no routing kernels, no exchange)
+    -- the world-1 step of bench.py --rank-path."""
     ids = MultiValidator.unique_ids()
     m = MultiValidator(rank=0, world=1, ids=ids, device=0)
     try:
@@ -235,7 +357,11 @@ def test_adopted_member_windows(oracle_mod):
     try:
         assert m.register_group("t1", 0, 9) == 0
         S = 1
-        cut = len(gid) // 2
+        # the splitter is a key of the window; member 1's piece starts at its
+        # first version (all versions of a key live on one member)
+        mid = len(gid) // 2
+        same = (gid == gid[mid]) & (words == words[:, [mid]]).all(axis=0)
+        cut = int(np.nonzero(same)[0][0])
         m.set_splitters(gid[[cut]], words[:, [cut]])
         dev = torch.device("cuda", 0)
         for i, (a, e) in enumerate(((0, cut), (cut, len(gid)))):
@@ -248,11 +374,59 @@ def test_adopted_member_windows(oracle_mod):
             m.member(i).ingest_device(e - a, words.shape[0], tg.data_ptr(), tw.data_ptr(), tl.data_ptr(),
                                       c2.params["end_lsn"])
         m.adopt()
+        with pytest.raises(hsc.HscError):  # appends go to the members of an adopted context
+            m.append_writes([("t1", 0, b"\x08" * 9, int(c2.params["end_lsn"]) + 1)])
         m.set_end(c2.params["end_lsn"])
         got = m.check_readsets(c2.readsets)
         assert S == 1
         # device windows have no log: the DB_SET-on-a-non-record rule is off,
         # and these snapshots are all record LSNs, so the verdicts are the oracle's
         np.testing.assert_array_equal(got != 0, want != 0)
+    finally:
+        m.close()
+
+
+def test_adopt_checks_splitters_and_pieces():
+    """hsc_multi_adopt refuses a world > 1 context without splitters (every
+    probe would go to member 0) and members holding keys outside their piece."""
+    from comdb2_amd.workloads import config2
+    c2 = config2(n_commits=2000, n_txn=10, value_bits=24, width=1 << 8)
+    one = Validator(0)
+    one.ingest_log(c2.log)
+    gid, words, lsn = one.export_window(all_versions=True)
+    one.close()
+    dev = torch.device("cuda", 0)
+
+    def ingest(m, i, sel):
+        order = sel[np.argsort(lsn[sel], kind="stable")]
+        tg = torch.from_numpy(np.ascontiguousarray(gid[order])).to(dev)
+        tw = torch.from_numpy(np.ascontiguousarray(words[:, order]).reshape(-1).view(np.int64)).to(dev)
+        tl = torch.from_numpy(np.ascontiguousarray(lsn[order]).view(np.int64)).to(dev)
+        torch.cuda.synchronize()
+        m.member(i).ingest_device(len(order), words.shape[0], tg.data_ptr(), tw.data_ptr(),
+                                  tl.data_ptr(), c2.params["end_lsn"])
+
+    mid = len(gid) // 2
+    cut = int(np.nonzero((gid == gid[mid]) & (words == words[:, [mid]]).all(axis=0))[0][0])
+    halves = (np.arange(cut), np.arange(cut, len(gid)))
+    m = MultiValidator([0, 0])
+    try:
+        m.register_group("t1", 0, 9)
+        for i in range(2):
+            ingest(m, i, halves[i])
+        with pytest.raises(hsc.HscError):  # no splitters
+            m.adopt()
+        m.set_splitters(gid[[cut]], words[:, [cut]])
+        m.adopt()
+    finally:
+        m.close()
+    m = MultiValidator([0, 0])
+    try:
+        m.register_group("t1", 0, 9)
+        for i in range(2):
+            ingest(m, i, halves[1 - i])  # pieces swapped
+        m.set_splitters(gid[[cut]], words[:, [cut]])
+        with pytest.raises(hsc.HscError):
+            m.adopt()
     finally:
         m.close()
