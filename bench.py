@@ -280,19 +280,36 @@ def bench_graph(args):
                         concurrent_frac=args.c4_concurrent, max_lag=args.c4_max_lag)
     hs = shard.history_shard(h, rank, world)
     dh = shard.device_history(hs, dev)
-    v = hsc.Validator(local)
+    native = backend == "nccl"  # the sharded step behind the C ABI (hsc_multi_graph_scc)
+    if native and world > 1:
+        ids = torch.zeros(hsc.MULTI_ID_BYTES, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            ids.copy_(torch.frombuffer(bytearray(hsc.MultiValidator.unique_ids()), dtype=torch.uint8))
+        dist.broadcast(ids, 0)
+        mv = hsc.MultiValidator(rank=rank, world=world, ids=bytes(ids.cpu().numpy().tobytes()),
+                                device=local)
+    elif native:
+        mv = hsc.MultiValidator([local])
+    else:
+        mv = None
+    v = mv.member(0) if mv is not None else hsc.Validator(local)
     g = shard.GpuGraph(v, dev)
+    scc = torch.zeros(max(h.ntxn, 1), dtype=torch.int32, device=dev)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    times, st, scc = [], None, None
+    times, st = [], None
     for k in range(args.warmup + args.steps):
         barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        scc, st = shard.sharded_scc(g, dh, h.ntxn, dev)
+        if mv is not None:
+            ss = mv.graph_scc([dh], h.ntxn, [scc.data_ptr()])
+            st = {"build": {"build_ms": ss["build_ms"]}, "scc": ss, "cut_rows": ss["edges"]}
+        else:
+            scc, st = shard.sharded_scc(g, dh, h.ntxn, dev)
         torch.cuda.synchronize(dev)
         dt = time.perf_counter() - t0
         barrier()
@@ -307,7 +324,11 @@ def bench_graph(args):
     if rank == 0:
         # the unsharded call on the whole history must give the same components
         full, fst = v.dep_graph_scc(h)
-        same = bool(np.array_equal(full, scc.cpu().numpy().astype(np.uint32)))
+        same = bool(np.array_equal(full, scc[:h.ntxn].cpu().numpy().astype(np.uint32)))
+        # algorithmic bytes: every op's columns read once (txn u32, key u64,
+        # is_write u8, observed u32 = 17 B) + per txn the cover byte and the
+        # scc word written (5 B); the build's sorts come on top
+        B4 = h.nops * 17 + h.ntxn * 5
         out = {"metric": "dependency-graph ops analysed/sec (WR/WW/RW edges + SCC)",
                "value": h.nops / (ms * 1e-3), "unit": "ops/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
@@ -322,10 +343,21 @@ def bench_graph(args):
                           "rank0_ops": hs.nops, "rank0_build_ms": st["build"]["build_ms"],
                           "scc_cut_ms": st["scc"]["scc_ms"], "rounds": st["scc"]["rounds"],
                           "unsharded_build_ms": fst["build_ms"], "unsharded_scc_ms": fst["scc_ms"],
-                          "parity_with_unsharded_gpu": same}}
+                          "parity_with_unsharded_gpu": same,
+                          "path": ("hsc_multi_graph_scc (C ABI; RCCL cover all-reduce + cut "
+                                   "all-gather across ranks)" if mv is not None else
+                                   "shard.sharded_scc over torch.distributed (" + backend + ")"),
+                          "phase_ms": st["scc"].get("phase_ms") if mv is not None else None},
+               "roofline": {"bound": "hbm", "kernel": "sharded SCC step (raw build: writer sort + "
+                                                        "edge rows; cover; cut; colouring SCC)",
+                            "achieved": B4 / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": B4 / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                            "algorithmic_bytes": B4,
+                            "note": "B = ops x 17 B (txn, key, is_write, observed read once) + "
+                                    "txns x 5 B (cover byte, scc word); rank 0's step time"}}
         if world == 1 and not args.no_cpu:
             out["cpu_baseline"] = graph_cpu_baseline(args)
-    v.close()
+    (mv if mv is not None else v).close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -908,6 +940,7 @@ def bench_multi(args):
             "own_rows_per_member_batch0": own_rows,
             "routed_over_own": float(sum(routed_rows)) / max(1, sum(own_rows)),
             "verdicts_equal_device_routed": routings_equal,
+            "host_enqueue_us_per_step": v.phase_stats()["routed_enqueue_us"],
         },
         "imbalance": {
             "member_probe_ms": [float(x) for x in pm],
@@ -940,11 +973,47 @@ def bench_multi(args):
         },
         "cpu_baseline": None,
     }
+    if inproc and args.config == 2 and not args.no_api:
+        out["api"] = multi_api_leg(hsc, v, first_rs.subset(np.arange(0, T)), v0)
     if rank == 0:
         print(json.dumps(out), flush=True)
     v.close()
     if not inproc:
         dist.destroy_process_group()
+
+
+def multi_api_leg(hsc, v, rs, want):
+    """The drop-in entry on the in-process multi context, the per-transaction
+    call pattern of db/toblock.c:4777-4800: a lone caller (one
+    hip_bdb_osql_serial_check at a time), 64 threads through the collector,
+    64 uncollected.  Each call is routed on the host while marshalled; only
+    the members its ranges overlap run their small kernels."""
+    arrs = hsc.NativeCurRangeArrs(rs)
+    want = np.asarray(want) != 0
+    conc = {}
+    r0 = v.route_stats()
+    got, st = v.concurrent_check(arrs, 64)
+    st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want))
+    conc["threads_64"] = st
+    m = min(rs.ntxn, 2000)
+    sub = hsc.NativeCurRangeArrs(_readsets_head(rs, m))
+    for nth in (1, 64):
+        got, st = v.concurrent_check(sub, nth, collect=False)
+        st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want[:m]))
+        st["sample"] = f"first {m} read sets"
+        conc[f"threads_{nth}_uncollected"] = st
+    r1 = v.route_stats()
+    sub.close()
+    arrs.close()
+    calls = max(1, r1["calls"] - r0["calls"])
+    return {"entry": "hip_bdb_osql_serial_check / hsc_collector_check on the multi context",
+            "members": v.world, "concurrent_callers": conc,
+            "members_per_call": (r1["member_checks"] - r0["member_checks"]) / calls,
+            "host_route_us_per_call": r1["route_us_per_call"],
+            "host_launch_us_per_call": r1["launch_us_per_call"],
+            "wait_us_per_call": r1["wait_us_per_call"],
+            "front_small_stats": v.small_stats(), "front_batch_stats": v.batch_stats(),
+            "member_small_stats": [v.member(i).small_stats() for i in range(v.nlocal)]}
 
 
 def main():

@@ -624,6 +624,7 @@ void ctx_clear_window(hsc_ctx *c);
 int ctx_ensure_built(hsc_ctx *c);
 void ctx_add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keylen, bool has_key, uint64_t lsn);
 int ctx_flush_appends(hsc_ctx *c, bool lazy = false);
+void ctx_raise_table_max(hsc_ctx *c, int tid, uint64_t lsn);
 int ctx_probe(hsc_ctx *c, const hsc_probe_batch *b);
 int ctx_default_threads();
 void ctx_par_for(hsc_ctx *c, int nwork, const std::function<void(int)> &f);
@@ -635,7 +636,9 @@ bool multi_adopted(const hsc_ctx *f);
 // hsc_multi.cpp: the front context's hooks (c->multi != nullptr)
 int multi_build(hsc_ctx *f);
 int multi_flush_appends(hsc_ctx *f, bool lazy);
-int multi_check_stage(hsc_ctx *f, Stage &st, int *rc_out);
+// lk (may be null): the caller's hold on f->mu; released while the members'
+// small kernels run when every member of the batch took that path
+int multi_check_stage(hsc_ctx *f, Stage &st, int *rc_out, std::unique_lock<std::mutex> *lk = nullptr);
 void multi_sync_dict(hsc_ctx *f);
 void multi_destroy(hsc_ctx *f);
 }  // namespace hsc

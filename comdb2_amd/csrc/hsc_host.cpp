@@ -240,8 +240,9 @@ static void clear_window(hsc_ctx *c)
     c->n = 0;
 }
 
-static void add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keylen, bool has_key,
-                      uint64_t lsn)
+// A write committed at lsn to table tid: its maximum rises (the pending
+// tail mirrors the tables whose maximum rose since its last mirror).
+static void raise_table_max(hsc_ctx *c, int tid, uint64_t lsn)
 {
     if (lsn > c->h_table_max[tid]) {
         c->h_table_max[tid] = lsn;
@@ -249,6 +250,12 @@ static void add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keyle
         if (c->live && !c->host_only && (c->app_tchg.empty() || c->app_tchg.back() != (uint32_t)tid))
             c->app_tchg.push_back((uint32_t)tid);
     }
+}
+
+static void add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keylen, bool has_key,
+                      uint64_t lsn)
+{
+    raise_table_max(c, tid, lsn);
     if (lsn > c->max_commit) c->max_commit = lsn;
     if (!has_key) return;
     if (keylen < 0) keylen = 0;
@@ -2865,7 +2872,7 @@ static int check_src(hsc_ctx *c, const Src &src, int *rc_out,
 {
     if (c->multi) {  // the members' routed pipeline (hsc_multi.cpp)
         const int rc = marshal_into(c, src, 0, src.ntxn(), c->stage[0]);
-        return rc ? rc : multi_check_stage(c, c->stage[0], rc_out);
+        return rc ? rc : multi_check_stage(c, c->stage[0], rc_out, lk);
     }
     if (c->host_only) return fail(c, HSC_EDEVICE, "host-only context");
     const int T = src.ntxn();
@@ -4317,6 +4324,7 @@ void ctx_add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keylen, 
     add_write(c, tid, ix, key, keylen, has_key, lsn);
 }
 int ctx_flush_appends(hsc_ctx *c, bool lazy) { return flush_appends(c, lazy); }
+void ctx_raise_table_max(hsc_ctx *c, int tid, uint64_t lsn) { raise_table_max(c, tid, lsn); }
 int ctx_probe(hsc_ctx *c, const hsc_probe_batch *b) { return probe(c, b); }
 int ctx_default_threads() { return default_threads(); }
 void ctx_par_for(hsc_ctx *c, int nwork, const std::function<void(int)> &f) { par_for(c, true, nwork, f, true); }

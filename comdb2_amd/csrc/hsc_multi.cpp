@@ -118,6 +118,7 @@ struct Multi {
     int world = 1;   // members of the partition
     int nlocal = 1;  // members in this process
     int rank = 0;    // global member index of local member 0
+    int ndev = 1;    // distinct GPUs of the local members
     bool rccl = false;
     hsc_ctx *mem[kMultiMax] = {};
     ncclComm_t comm[kMultiLanes] = {};
@@ -138,11 +139,27 @@ struct Multi {
     // send blocks moved by peer copies, unpacked, owner slices gathered
     bool loop = false;
     // routing on the host (multi_check_stage, hsc_multi_marshal_routed)
-    Stage mst[kMultiMax];        // each member's share of the last routed batch
+    Stage mst[kMultiMax];        // each member's share of the last routed batch (hsc_multi_marshal_routed)
+    // the drop-in entries' routed shares: one set per call in flight (the
+    // front lock is dropped once a batch is routed; its set is the call's
+    // until the members' verdicts are in)
+    struct StageSet {
+        Stage s[kMultiMax];
+    };
+    std::mutex set_mu;
+    std::vector<std::unique_ptr<StageSet>> sets;
+    std::vector<StageSet *> free_sets;
     std::vector<uint8_t> h_own;  // per probe: first | last member << 4
     std::vector<uint32_t> h_cw;  // per chunk and member: counts, then offsets
     std::vector<int> h_rc;       // one member's verdicts
-    uint64_t h_calls = 0, h_member_checks = 0, h_routed = 0, h_probes = 0, ns_route = 0;
+    uint64_t h_calls = 0, h_routed = 0, h_probes = 0, ns_route = 0;
+    // accumulated after the front lock is dropped
+    std::atomic<uint64_t> ns_launch_a{0}, ns_wait{0}, members_run{0};
+    std::atomic<uint64_t> part_epoch{0};  // bumped before the members' pieces change
+    // sharded SCC (hsc_multi_graph_scc): per local member its cover, its cut
+    // rows and (the SCC's member) every member's cut rows
+    DBuf g_cover[kMultiMax], g_rows[kMultiMax], g_all[kMultiMax], g_sz[kMultiMax];
+    double g_ms[4] = {};  // host ms of its last call: build + cover, cover merge, cuts + gather, SCC
     bool timing = false;  // events around every member's probe (per-member probe times)
     int last_lane = 0;
     // host copies of the last pipeline's counts
@@ -151,6 +168,7 @@ struct Multi {
     // host phase split of run_pipeline (ns): waiting for the lane's previous
     // batch, launching the counts, waiting for them, enqueueing the rest
     uint64_t ns_lane = 0, ns_count = 0, ns_count_wait = 0, ns_enqueue = 0;
+    uint64_t pr_batches = 0, ns_pr = 0;  // hsc_multi_probe_routed: batches, host time enqueueing them
 };
 
 static int mfail(hsc_ctx *c, int code, const char *what, hipError_t e = hipSuccess)
@@ -311,6 +329,7 @@ int multi_build(hsc_ctx *f)
         return mfail(f, HSC_ESTATE, "multi context: members were ingested directly; re-ingest them");
     }
     M->adopted = false;
+    M->part_epoch.fetch_add(1, std::memory_order_acq_rel);
     const int W = ctx_window_words(f);
     if (f->W != W) f->dict_epoch++;
     f->W = W;
@@ -388,8 +407,8 @@ int multi_flush_appends(hsc_ctx *f, bool lazy)
         hsc_ctx *c = M->mem[m];
         std::lock_guard<std::mutex> g(c->mu);
         (void)hipSetDevice(c->device);
-        for (size_t t = 0; t < f->h_table_max.size(); ++t)
-            if (f->h_table_max[t] > c->h_table_max[t]) c->h_table_max[t] = f->h_table_max[t], c->app_tmax = true;
+        for (size_t t = 0; t < f->h_table_max.size(); ++t)  // (mirrored by a pending tail)
+            ctx_raise_table_max(c, (int)t, f->h_table_max[t]);
         c->max_commit = std::max(c->max_commit, f->max_commit);
         c->end_lsn = f->end_lsn;
         for (size_t i : rows[m]) {
@@ -427,13 +446,18 @@ static int lane_stream(hsc_ctx *f, Multi *M, int L, int m)
     return HSC_OK;
 }
 
-// Wait for lane L's previous batch on every local member.
+// Lane L's next batch runs after its previous one on every local member:
+// each member's lane stream waits (on the device, no host wait) for every
+// member's done event of the lane -- a member's buffers of the lane are
+// written by the others' scatters / copies and read by their merges.
 static int lane_acquire(hsc_ctx *f, Multi *M, int L)
 {
+    for (int m = 0; m < M->nlocal; ++m) MRC(lane_stream(f, M, L, m));
     for (int m = 0; m < M->nlocal; ++m) {
-        MRC(lane_stream(f, M, L, m));
         MLane &ml = M->lane[L][m];
-        if (ml.used) MCHK(f, hipEventSynchronize(ml.ev_done));
+        MCHK(f, hipSetDevice(M->mem[m]->device));
+        for (int d = 0; d < M->nlocal; ++d)
+            if (M->lane[L][d].used) MCHK(f, hipStreamWaitEvent(ml.stream, M->lane[L][d].ev_done, 0));
     }
     return HSC_OK;
 }
@@ -508,38 +532,48 @@ static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb,
     const size_t total = tb[N];
     auto ob = [&](int o) -> size_t { return tb[o] / 64; };
     auto ow = [&](int o) -> size_t { return (tb[o + 1] - tb[o]) / 64; };
-    // 6. every member probes what it holds
-    for (int m = 0; m < NL; ++m) {
+    // 6. every member probes what it holds -- the members' launches issued
+    // from one host thread each (a probe is several launches; eight GPUs'
+    // worth from one thread would outlast the probes themselves)
+    auto probe_one = [&](int m) -> int {
         MLane &ml = M->lane[L][m];
         hsc_ctx *c = M->mem[m];
         hsc_probe_batch b = in[m];
         b.n_txn = total;
-        MCHK(f, hipSetDevice(c->device));
-        MCHK(f, ml.verdict.ensure(std::max<size_t>(total, 64)));
+        MCHK(c, hipSetDevice(c->device));
+        MCHK(c, ml.verdict.ensure(std::max<size_t>(total, 64)));
         b.verdict = ml.verdict.as<uint8_t>();
         if (N == 1) {  // one piece: its bitmap is the result
             b.bitmap = out[0];
         } else {
-            MCHK(f, ml.bitmap.ensure(std::max<size_t>(total / 8, 8)));
+            MCHK(c, ml.bitmap.ensure(std::max<size_t>(total / 8, 8)));
             b.bitmap = ml.bitmap.as<uint64_t>();
         }
         std::lock_guard<std::mutex> g(c->mu);
-        if (c->dirty) return mfail(f, HSC_ESTATE, "multi context: a member's window is not built");
-        if (c->app_last) MCHK(f, hipStreamWaitEvent(ml.stream, c->app_last, 0));  // its appends
+        if (c->dirty) return ctx_fail(c, HSC_ESTATE, "window not built");
+        if (c->app_last) MCHK(c, hipStreamWaitEvent(ml.stream, c->app_last, 0));  // its appends
         ml.timed = M->timing;
         if (ml.timed) {
-            if (!ml.ev_t0) MCHK(f, hipEventCreate(&ml.ev_t0));
-            if (!ml.ev_t1) MCHK(f, hipEventCreate(&ml.ev_t1));
-            MCHK(f, hipEventRecord(ml.ev_t0, ml.stream));
+            if (!ml.ev_t0) MCHK(c, hipEventCreate(&ml.ev_t0));
+            if (!ml.ev_t1) MCHK(c, hipEventCreate(&ml.ev_t1));
+            MCHK(c, hipEventRecord(ml.ev_t0, ml.stream));
         }
         hipStream_t keep = c->stream;
         c->stream = ml.stream;
         const int rc = ctx_probe(c, &b);
         c->stream = keep;
-        if (rc) return mfail(f, rc, ("member probe: " + c->err).c_str());
-        if (ml.timed) MCHK(f, hipEventRecord(ml.ev_t1, ml.stream));
-        MCHK(f, hipEventRecord(ml.ev_probe, ml.stream));
-    }
+        if (rc) return rc;
+        if (ml.timed) MCHK(c, hipEventRecord(ml.ev_t1, ml.stream));
+        MCHK(c, hipEventRecord(ml.ev_probe, ml.stream));
+        return HSC_OK;
+    };
+    int prc[kMultiMax] = {};
+    if (M->ndev > 1)  // (members sharing a GPU: one thread -- its launches serialise anyway)
+        ctx_par_for(f, NL, [&](int m) { prc[m] = probe_one(m); });
+    else
+        for (int m = 0; m < NL; ++m) prc[m] = probe_one(m);
+    for (int m = 0; m < NL; ++m)
+        if (prc[m]) return mfail(f, prc[m], ("member probe: " + M->mem[m]->err).c_str());
     M->last_lane = L;
     // 7. OR of the members' bitmaps per owner
     if (N == 1) {
@@ -969,46 +1003,90 @@ static int route_host(hsc_ctx *f, const Stage &st, Stage *out, int only, uint32_
 // routing and the RCCL exchange.
 static int check_stage_device(hsc_ctx *f, Stage &st, int *rc_out);
 
-int multi_check_stage(hsc_ctx *f, Stage &st, int *rc_out)
+int multi_check_stage(hsc_ctx *f, Stage &st, int *rc_out, std::unique_lock<std::mutex> *lk)
 {
     Multi *M = f->multi;
     if (M->rccl) return check_stage_device(f, st, rc_out);
     const int N = M->world;
     const size_t T = st.n_txn;
     const auto t0 = SteadyClock::now();
-    MRC(route_host(f, st, M->mst, -1, 0, [&](int d, size_t n, size_t nl) {
-        return ctx_small_fits(M->mem[d], T, n, nl);
-    }));
-    const auto t1 = SteadyClock::now();
-    int slot[kMultiMax];
-    bool run[kMultiMax] = {};
-    int rc = HSC_OK;
-    for (int d = 0; d < N && rc == HSC_OK; ++d) {
-        Stage &ms = M->mst[d];
-        if (!ms.n && !ms.n_lock) continue;  // nothing of this batch lives there
-        rc = ctx_stage_launch(M->mem[d], ms, &slot[d]);
-        if (rc)
-            rc = mfail(f, rc, ("member check: " + M->mem[d]->err).c_str());
-        else
-            run[d] = true;
+    Multi::StageSet *set = nullptr;
+    {
+        std::lock_guard<std::mutex> g(M->set_mu);
+        if (M->free_sets.empty()) {
+            M->sets.emplace_back(new (std::nothrow) Multi::StageSet());
+            if (!M->sets.back()) {
+                M->sets.pop_back();
+                return mfail(f, HSC_ENOMEM, "multi routing staging");
+            }
+            M->free_sets.push_back(M->sets.back().get());
+        }
+        set = M->free_sets.back();
+        M->free_sets.pop_back();
     }
-    // every launched member is waited for, also after a failed launch
+    auto give_back = [&] {
+        std::lock_guard<std::mutex> g(M->set_mu);
+        M->free_sets.push_back(set);
+    };
+    Stage *ms = set->s;
+    const uint64_t epoch = M->part_epoch.load(std::memory_order_acquire);
+    int rc = route_host(f, st, ms, -1, 0, [&](int d, size_t n, size_t nl) {
+        return ctx_small_fits(M->mem[d], T, n, nl);
+    });
+    if (rc) {
+        give_back();
+        return rc;
+    }
+    const auto t1 = SteadyClock::now();
     const uint8_t *fc = st.forced.as<uint8_t>();
     for (size_t t = 0; t < T; ++t) rc_out[t] = fc[t] ? 1 : 0;
-    M->h_rc.resize(std::max<size_t>(T, 1));
-    for (int d = 0; d < N; ++d) {
-        if (!run[d]) continue;
-        const int r = ctx_stage_wait(M->mem[d], M->mst[d], slot[d], M->h_rc.data());
-        if (r) {
-            if (rc == HSC_OK) rc = mfail(f, r, ("member check: " + M->mem[d]->err).c_str());
-            continue;
-        }
-        for (size_t t = 0; t < T; ++t) rc_out[t] |= M->h_rc[t];
-        M->h_member_checks++;
-    }
     M->h_calls++;
     M->ns_route += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
-    return rc;
+    // the batch is in the call's own set now: the next caller marshals and
+    // routes while this one launches and waits (the members take their own
+    // locks; the window cannot change under a check: every change takes the
+    // front lock and waits for the members' slots)
+    if (lk) lk->unlock();
+    int slot[kMultiMax];
+    bool run[kMultiMax] = {};
+    int nrun = 0;
+    for (int d = 0; d < N && rc == HSC_OK; ++d) {
+        if (!ms[d].n && !ms[d].n_lock) continue;  // nothing of this batch lives there
+        rc = ctx_stage_launch(M->mem[d], ms[d], &slot[d]);
+        if (rc == HSC_OK) run[d] = true, nrun++;
+    }
+    const auto t2 = SteadyClock::now();
+    // every launched member is waited for, also after a failed launch
+    static thread_local std::vector<int> rcm;
+    rcm.resize(std::max<size_t>(T, 1));
+    int fail_d = rc ? N : -1;
+    for (int d = 0; d < N; ++d) {
+        if (!run[d]) continue;
+        const int r = ctx_stage_wait(M->mem[d], ms[d], slot[d], rcm.data());
+        if (r) {
+            if (rc == HSC_OK) rc = r, fail_d = d;
+            continue;
+        }
+        for (size_t t = 0; t < T; ++t) rc_out[t] |= rcm[t];
+    }
+    give_back();
+    const auto t3 = SteadyClock::now();
+    M->ns_launch_a.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count(),
+                             std::memory_order_relaxed);
+    M->ns_wait.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t3 - t2).count(),
+                         std::memory_order_relaxed);
+    M->members_run.fetch_add((uint64_t)nrun, std::memory_order_relaxed);
+    // a re-partition (new splitters, a rebuild) between the routing and the
+    // launches would have sent ranges to members that no longer hold them:
+    // fail closed
+    const bool moved = M->part_epoch.load(std::memory_order_acquire) != epoch;
+    if (rc == HSC_OK && !moved) return HSC_OK;  // (lk stays released)
+    if (lk) lk->lock();  // the caller's contract: failures are recorded under the lock
+    if (rc == HSC_OK) return mfail(f, HSC_ESTATE, "multi context re-partitioned during the check");
+    for (int d = 0; d < N; ++d)  // the failing member's message
+        if (d == fail_d || (fail_d == N && !run[d] && (ms[d].n || ms[d].n_lock)))
+            return mfail(f, rc, ("member check: " + M->mem[d]->err).c_str());
+    return mfail(f, rc, "member check");
 }
 
 // Per-rank context: this rank's read sets, uploaded to its member and routed
@@ -1098,6 +1176,13 @@ void multi_destroy(hsc_ctx *f)
         for (auto &c : M->comm)
             if (c) (void)rccl().CommDestroy(c);
     for (Stage &st : M->mst) st.release();
+    for (auto &ss : M->sets)
+        for (Stage &st : ss->s) st.release();
+    for (int m = 0; m < M->nlocal; ++m) {
+        if (!M->mem[m]) continue;
+        (void)hipSetDevice(M->mem[m]->device);
+        for (DBuf *b : {&M->g_cover[m], &M->g_rows[m], &M->g_all[m], &M->g_sz[m]}) b->release();
+    }
     for (int m = 0; m < M->nlocal; ++m) {
         if (!M->mem[m]) continue;
         (void)hipSetDevice(M->mem[m]->device);
@@ -1150,6 +1235,12 @@ int hsc_multi_create(const int *devices, int n, hsc_ctx **out)
     Multi *M = f->multi;
     M->world = M->nlocal = n;
     M->rank = 0;
+    M->ndev = 0;
+    for (int i = 0; i < n; ++i) {
+        bool seen = false;
+        for (int j = 0; j < i; ++j) seen |= devices[j] == devices[i];
+        M->ndev += !seen;
+    }
     for (int i = 0; i < n; ++i) {
         const int rc = hsc_ctx_create(devices[i], &M->mem[i]);
         if (rc) {
@@ -1231,6 +1322,7 @@ int hsc_multi_set_splitters(hsc_ctx *f, size_t S, const uint32_t *gid, const uin
                 c = words[(size_t)j * S + k - 1] < words[(size_t)j * S + k] ? -1 : 1;
         if (c > 0) return mfail(f, HSC_EINVAL, "splitters not ascending");
     }
+    M->part_epoch.fetch_add(1, std::memory_order_acq_rel);
     M->sp_given = true;
     M->sp_W = W;
     M->sp_gid.assign(gid, gid + S);
@@ -1300,6 +1392,7 @@ int hsc_multi_adopt(hsc_ctx *f)
     size_t keys = 0;
     for (int m = 0; m < M->nlocal; ++m) keys += M->mem[m]->n;
     f->n = keys;
+    M->part_epoch.fetch_add(1, std::memory_order_acq_rel);
     M->adopted = true;
     M->d_sp_W = 0;
     f->host_staged = false;
@@ -1342,16 +1435,19 @@ int hsc_multi_stats(hsc_ctx *f, uint64_t out[4])
     return HSC_OK;
 }
 
-int hsc_multi_phase_stats(hsc_ctx *f, double out[5])
+int hsc_multi_phase_stats(hsc_ctx *f, double out[7])
 {
     if (!f || !f->multi || !out) return HSC_EINVAL;
     Multi *M = f->multi;
-    const double b = (double)std::max<uint64_t>(M->batches, 1) * 1e3;
-    out[0] = (double)M->batches;
+    const uint64_t routed_dev = M->batches - M->pr_batches;  // run_pipeline batches
+    const double b = (double)std::max<uint64_t>(routed_dev, 1) * 1e3;
+    out[0] = (double)routed_dev;
     out[1] = (double)M->ns_lane / b;
     out[2] = (double)M->ns_count / b;
     out[3] = (double)M->ns_count_wait / b;
     out[4] = (double)M->ns_enqueue / b;
+    out[5] = (double)M->pr_batches;
+    out[6] = (double)M->ns_pr / ((double)std::max<uint64_t>(M->pr_batches, 1) * 1e3);
     return HSC_OK;
 }
 
@@ -1405,9 +1501,12 @@ int hsc_multi_probe_routed(hsc_ctx *f, const hsc_probe_batch *b, const uint64_t 
         in[m] = b[m];
         outs[m] = b[m].bitmap;
     }
+    const auto t0 = SteadyClock::now();
     MRC(lane_acquire(f, M, lane));
     MRC(probe_merge(f, lane, in, tb, outs));
     for (int m = 0; m < NL; ++m) M->routed += b[m].n, M->probes += b[m].n;
+    M->pr_batches++;
+    M->ns_pr += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(SteadyClock::now() - t0).count();
     return HSC_OK;
 }
 
@@ -1473,16 +1572,143 @@ int hsc_multi_member_probe_ms(hsc_ctx *f, float *out, int n)
     return HSC_OK;
 }
 
-int hsc_multi_route_stats(hsc_ctx *f, double out[6])
+int hsc_multi_route_stats(hsc_ctx *f, double out[8])
 {
     if (!f || !f->multi || !out) return HSC_EINVAL;
     Multi *M = f->multi;
+    const double c = M->h_calls ? (double)M->h_calls : 1.0;
     out[0] = (double)M->h_calls;
-    out[1] = (double)M->h_member_checks;
+    out[1] = (double)M->members_run.load();
     out[2] = (double)M->h_probes;
     out[3] = (double)M->h_routed;
-    out[4] = M->h_calls ? (double)M->ns_route / (double)M->h_calls * 1e-3 : 0.0;
+    out[4] = (double)M->ns_route / c * 1e-3;
     out[5] = (double)M->world;
+    out[6] = (double)M->ns_launch_a.load() / c * 1e-3;
+    out[7] = (double)M->ns_wait.load() / c * 1e-3;
+    return HSC_OK;
+}
+
+int hsc_multi_graph_scc(hsc_ctx *f, const hsc_ops_dev *ops, uint32_t ntxn, uint32_t *const *scc_dev,
+                        hsc_graph_stats *st)
+{
+    if (!f || !f->multi || !ops || !scc_dev || !scc_dev[0]) return HSC_EINVAL;
+    Multi *M = f->multi;
+    const int N = M->world, NL = M->nlocal;
+    std::lock_guard<std::mutex> g(f->mu);
+    const auto t0 = SteadyClock::now();
+    for (int m = 0; m < NL; ++m) MRC(lane_stream(f, M, 0, m));
+    const size_t cb = r64(std::max<uint32_t>(ntxn, 1));  // cover bytes, whole u64 words
+    float build_ms = 0;
+    // 1. every member builds the raw edges of its key shard and its cover
+    for (int m = 0; m < NL; ++m) {
+        hsc_ctx *c = M->mem[m];
+        hsc_graph_stats bs{};
+        int rc = hsc_dep_graph_build_device(c, ops[m].nops, ntxn, ops[m].txn, ops[m].key, ops[m].is_write,
+                                            ops[m].observed, 0, &bs);
+        if (rc) return mfail(f, rc, ("graph build: " + c->err).c_str());
+        build_ms = std::max(build_ms, bs.build_ms);
+        MCHK(f, hipSetDevice(c->device));
+        MCHK(f, M->g_cover[m].ensure(cb));
+        MCHK(f, hipMemset(M->g_cover[m].p, 0, cb));
+        rc = hsc_dep_graph_cover(c, M->g_cover[m].as<uint8_t>());
+        if (rc) return mfail(f, rc, ("graph cover: " + c->err).c_str());
+    }
+    const auto t1 = SteadyClock::now();
+    // 2. the covers OR-ed (0 / 1 bytes: MAX) over every member
+    Rccl &R = rccl();
+    MLane &l0 = M->lane[0][0];
+    if (M->rccl) {
+        if (N > 1) {
+            MCHK(f, hipSetDevice(M->mem[0]->device));
+            NCHK(f, R.AllReduce(M->g_cover[0].p, M->g_cover[0].p, cb, ncclUint8, ncclMax, M->comm[0], l0.stream));
+            MCHK(f, hipStreamSynchronize(l0.stream));
+        }
+    } else if (NL > 1) {
+        RouteParts parts{};
+        parts.n = NL;
+        for (int d = 0; d < NL; ++d) parts.p[d] = M->g_cover[d].as<uint64_t>();
+        MCHK(f, hipSetDevice(M->mem[0]->device));
+        MCHK(f, launch_or_slices(parts, cb / 8, M->g_cover[0].as<uint64_t>(), l0.stream));
+        MCHK(f, hipStreamSynchronize(l0.stream));
+        for (int d = 1; d < NL; ++d)
+            MCHK(f, hipMemcpyPeer(M->g_cover[d].p, M->mem[d]->device, M->g_cover[0].p, M->mem[0]->device, cb));
+    }
+    const auto t2 = SteadyClock::now();
+    // 3. every member's edges between covered txns
+    size_t k[kMultiMax] = {};
+    for (int m = 0; m < NL; ++m) {
+        hsc_ctx *c = M->mem[m];
+        int rc = hsc_dep_graph_cut(c, M->g_cover[m].as<uint8_t>(), nullptr, 0, &k[m]);
+        if (!rc) {
+            MCHK(f, hipSetDevice(c->device));
+            MCHK(f, M->g_rows[m].ensure(8 * std::max<size_t>(k[m], 1)));
+            rc = hsc_dep_graph_cut(c, M->g_cover[m].as<uint8_t>(), M->g_rows[m].as<uint64_t>(), k[m], &k[m]);
+        }
+        if (rc) return mfail(f, rc, ("graph cut: " + c->err).c_str());
+    }
+    // 4. the union of the cuts where the SCC runs: every rank (all-gather,
+    // each rank's rows padded with ~0 to the largest), or member 0 here
+    const uint64_t *rows = M->g_rows[0].as<uint64_t>();
+    size_t total = k[0], cut_rows = k[0];
+    if (M->rccl && N > 1) {
+        MCHK(f, hipSetDevice(M->mem[0]->device));
+        MCHK(f, M->g_sz[0].ensure(8 * (size_t)(N + 1)));
+        uint64_t mine = k[0];
+        MCHK(f, hipMemcpy(M->g_sz[0].p, &mine, 8, hipMemcpyHostToDevice));
+        NCHK(f, R.AllGather(M->g_sz[0].p, M->g_sz[0].as<uint64_t>() + 1, 1, ncclUint64, M->comm[0], l0.stream));
+        MCHK(f, hipStreamSynchronize(l0.stream));
+        std::vector<uint64_t> sz(N);
+        MCHK(f, hipMemcpy(sz.data(), M->g_sz[0].as<uint64_t>() + 1, 8 * (size_t)N, hipMemcpyDeviceToHost));
+        size_t mx = 1;
+        cut_rows = 0;
+        for (int r = 0; r < N; ++r) mx = std::max<size_t>(mx, sz[r]), cut_rows += sz[r];
+        MCHK(f, M->g_rows[0].ensure(8 * mx));
+        if (mx > k[0]) MCHK(f, hipMemset(M->g_rows[0].as<uint64_t>() + k[0], 0xFF, 8 * (mx - k[0])));
+        MCHK(f, M->g_all[0].ensure(8 * mx * (size_t)N));
+        NCHK(f, R.AllGather(M->g_rows[0].p, M->g_all[0].p, mx, ncclUint64, M->comm[0], l0.stream));
+        MCHK(f, hipStreamSynchronize(l0.stream));
+        rows = M->g_all[0].as<uint64_t>();
+        total = mx * (size_t)N;
+    } else if (NL > 1) {
+        total = 0;
+        for (int d = 0; d < NL; ++d) total += k[d];
+        cut_rows = total;
+        MCHK(f, hipSetDevice(M->mem[0]->device));
+        MCHK(f, M->g_all[0].ensure(8 * std::max<size_t>(total, 1)));
+        size_t o = 0;
+        for (int d = 0; d < NL; ++d) {
+            if (k[d])
+                MCHK(f, hipMemcpyPeer(M->g_all[0].as<uint64_t>() + o, M->mem[0]->device, M->g_rows[d].p,
+                                      M->mem[d]->device, 8 * k[d]));
+            o += k[d];
+        }
+        rows = M->g_all[0].as<uint64_t>();
+    }
+    const auto t3 = SteadyClock::now();
+    // 5. SCC of the cut union (components of >= 2 txns live there)
+    hsc_graph_stats ss{};
+    int rc = hsc_dep_graph_scc_cut(M->mem[0], ntxn, M->g_cover[0].as<uint8_t>(), rows, total, scc_dev[0], &ss);
+    if (rc) return mfail(f, rc, ("graph scc: " + M->mem[0]->err).c_str());
+    for (int d = 1; d < NL; ++d)  // in process: the same components on every member that asked
+        if (scc_dev[d])
+            MCHK(f, hipMemcpyPeer(scc_dev[d], M->mem[d]->device, scc_dev[0], M->mem[0]->device, 4 * (size_t)ntxn));
+    const auto t4 = SteadyClock::now();
+    if (st) {
+        *st = ss;
+        st->build_ms = build_ms;
+        st->edges = cut_rows;  // rows of the cut union (every shard's)
+    }
+    auto ms = [](SteadyClock::time_point a, SteadyClock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    M->g_ms[0] = ms(t0, t1), M->g_ms[1] = ms(t1, t2), M->g_ms[2] = ms(t2, t3), M->g_ms[3] = ms(t3, t4);
+    return HSC_OK;
+}
+
+int hsc_multi_graph_phase_ms(hsc_ctx *f, double out[4])
+{
+    if (!f || !f->multi || !out) return HSC_EINVAL;
+    for (int i = 0; i < 4; ++i) out[i] = f->multi->g_ms[i];
     return HSC_OK;
 }
 

@@ -108,6 +108,11 @@ class GraphStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class OpsDev(C.Structure):
+    """hsc_ops_dev: one key shard's history ops on its member's GPU."""
+    _fields_ = [("nops", C.c_size_t), ("txn", _p), ("key", _p), ("is_write", _p), ("observed", _p)]
+
+
 class Marshalled(C.Structure):
     _fields_ = [("n", C.c_size_t), ("n_lock", C.c_size_t), ("n_txn", C.c_size_t),
                 ("words", C.c_int), ("lo", _u64p), ("hi", _u64p),
@@ -162,7 +167,8 @@ EXPORTS = [
     "hsc_multi_adopt", "hsc_multi_probe_device", "hsc_multi_stats", "hsc_multi_last_counts",
     "hsc_multi_phase_stats", "hsc_multi_set_transport", "hsc_multi_probe_routed",
     "hsc_multi_marshal_routed", "hsc_multi_routed_member", "hsc_multi_enable_timing",
-    "hsc_multi_member_probe_ms", "hsc_multi_route_stats",
+    "hsc_multi_member_probe_ms", "hsc_multi_route_stats", "hsc_multi_graph_scc",
+    "hsc_multi_graph_phase_ms",
     "hsc_marshal_arrs", "hsc_batch_stats",
 ]
 MULTI_ID_BYTES = 2 * 128  # hsc_multi_unique_ids: one RCCL id per lane
@@ -284,6 +290,8 @@ def load() -> C.CDLL:
         "hsc_multi_marshal_routed": (C.c_int, [_p, C.POINTER(_ReadSets), C.c_int, C.c_uint32,
                                                C.POINTER(C.POINTER(Marshalled))]),
         "hsc_multi_route_stats": (C.c_int, [_p, _p]),
+        "hsc_multi_graph_scc": (C.c_int, [_p, _p, C.c_uint32, _p, C.POINTER(GraphStats)]),
+        "hsc_multi_graph_phase_ms": (C.c_int, [_p, _p]),
         "hsc_multi_routed_member": (C.c_int, [_p, C.c_int, C.POINTER(C.POINTER(Marshalled))]),
         "hsc_multi_enable_timing": (C.c_int, [_p, C.c_int]),
         "hsc_multi_member_probe_ms": (C.c_int, [_p, _p, C.c_int]),
@@ -1105,6 +1113,28 @@ class MultiValidator(Validator):
                           lock_snap=cat("lock_snap"), lock_txn=cat("lock_txn"), forced=forced)
         return out
 
+    def graph_scc(self, shards, ntxn: int, scc_ptrs) -> dict:
+        """hsc_multi_graph_scc: shards[i] = local member i's key shard of the
+        history on its GPU (shard.DeviceHistory or an object with nops / txn /
+        key / is_write / observed tensors), scc_ptrs[i] = device u32[ntxn]
+        (index 0 required).  -> member 0's SCC stats + host phase ms."""
+        ops = (OpsDev * len(shards))()
+        for i, h in enumerate(shards):
+            ops[i].nops = h.nops
+            ops[i].txn = h.txn.data_ptr()
+            ops[i].key = h.key.data_ptr()
+            ops[i].is_write = h.is_write.data_ptr()
+            ops[i].observed = h.observed.data_ptr()
+        ptrs = (_p * len(shards))(*[C.c_void_p(x) if x else None for x in scc_ptrs])
+        st = GraphStats()
+        self._chk(self.lib.hsc_multi_graph_scc(self.ctx, ops, ntxn, ptrs, C.byref(st)),
+                  "hsc_multi_graph_scc")
+        out = st.as_dict()
+        ph = np.zeros(4, np.float64)
+        self._chk(self.lib.hsc_multi_graph_phase_ms(self.ctx, ph.ctypes.data), "hsc_multi_graph_phase_ms")
+        out["phase_ms"] = {"build_cover": ph[0], "cover_merge": ph[1], "cut_union": ph[2], "scc": ph[3]}
+        return out
+
     def enable_member_timing(self, on: bool = True) -> None:
         self._chk(self.lib.hsc_multi_enable_timing(self.ctx, int(on)), "hsc_multi_enable_timing")
 
@@ -1125,10 +1155,11 @@ class MultiValidator(Validator):
                   "hsc_multi_probe_routed")
 
     def route_stats(self) -> dict:
-        out = np.zeros(6, np.float64)
+        out = np.zeros(8, np.float64)
         self._chk(self.lib.hsc_multi_route_stats(self.ctx, out.ctypes.data), "hsc_multi_route_stats")
         return {"calls": int(out[0]), "member_checks": int(out[1]), "probes": int(out[2]),
-                "rows": int(out[3]), "route_us_per_call": float(out[4]), "world": int(out[5])}
+                "rows": int(out[3]), "route_us_per_call": float(out[4]), "world": int(out[5]),
+                "launch_us_per_call": float(out[6]), "wait_us_per_call": float(out[7])}
 
     def probe_device_multi(self, batches: Sequence[ProbeBatch], lane: int = 0) -> None:
         arr = (ProbeBatch * len(batches))(*batches)
@@ -1142,10 +1173,11 @@ class MultiValidator(Validator):
 
     def phase_stats(self) -> dict:
         """Host time per routed batch, mean us (hsc_multi_phase_stats)."""
-        out = np.zeros(5, np.float64)
+        out = np.zeros(7, np.float64)
         self._chk(self.lib.hsc_multi_phase_stats(self.ctx, out.ctypes.data), "hsc_multi_phase_stats")
         return {"batches": int(out[0]), "lane_wait_us": float(out[1]), "count_launch_us": float(out[2]),
-                "count_wait_us": float(out[3]), "enqueue_us": float(out[4])}
+                "count_wait_us": float(out[3]), "enqueue_us": float(out[4]),
+                "routed_batches": int(out[5]), "routed_enqueue_us": float(out[6])}
 
     def last_counts(self) -> np.ndarray:
         n = self.world

@@ -633,19 +633,22 @@ int hsc_multi_routed_member(hsc_ctx *ctx, int member, const hsc_marshalled **out
  * (waits for it). */
 int hsc_multi_enable_timing(hsc_ctx *ctx, int on);
 int hsc_multi_member_probe_ms(hsc_ctx *ctx, float *out, int n);
-/* Host routing of the drop-in entries: out[6] = calls, member checks run,
+/* Host routing of the drop-in entries: out[8] = calls, member checks run,
  * probes routed, probe rows placed (> probes when ranges straddle pieces),
- * mean us routing per call, world. */
-int hsc_multi_route_stats(hsc_ctx *ctx, double out[6]);
+ * mean us routing per call, world, mean us launching the members, mean us
+ * waiting for their verdicts. */
+int hsc_multi_route_stats(hsc_ctx *ctx, double out[8]);
 /* out[4]: routed batches, probes routed (sources), probe rows received
  * (destinations; > probes when ranges straddle pieces), local members. */
 int hsc_multi_stats(hsc_ctx *ctx, uint64_t out[4]);
 /* counts[s * world + d]: probes member s sent member d in the last batch. */
 int hsc_multi_last_counts(hsc_ctx *ctx, uint32_t *counts, int n);
-/* Host time per routed batch (diagnostics): out[0] batches, then mean us
- * waiting for the lane's previous batch, launching the route counts, waiting
- * for the counts the device publishes, enqueueing the rest of the batch. */
-int hsc_multi_phase_stats(hsc_ctx *ctx, double out[5]);
+/* Host time per routed batch (diagnostics): out[0] device-routed batches,
+ * then mean us enqueueing the lane waits, launching the route counts,
+ * waiting for the counts the device publishes, enqueueing the rest of the
+ * batch; out[5] hsc_multi_probe_routed batches, out[6] mean us enqueueing
+ * one. */
+int hsc_multi_phase_stats(hsc_ctx *ctx, double out[7]);
 
 /* ---- OSQL_SERIAL wire path --------------------------------------------
  * Decode only: *out points at context-owned read sets, valid until the next
@@ -741,6 +744,30 @@ int hsc_dep_graph_cut(hsc_ctx *ctx, const uint8_t *cover_dev, uint64_t *rows_dev
 int hsc_dep_graph_scc_cut(hsc_ctx *ctx, uint32_t ntxn, const uint8_t *cover_dev,
                           const uint64_t *rows_dev, size_t m, uint32_t *scc_dev,
                           hsc_graph_stats *stats);
+
+/* Sharded SCC on a multi context (config 4 over N GPUs behind the C ABI):
+ * ops[i] = local member i's key shard of the history, device-resident on its
+ * GPU (every WW/WR/RW edge belongs to one key).  Per member: raw build and
+ * cover; covers OR-ed (RCCL MAX all-reduce across ranks, an OR over peer
+ * buffers in one process); cuts; the union of the cuts (RCCL all-gather,
+ * padded with ~0 rows, across ranks; peer copies to member 0 in one
+ * process); its colouring SCC.  scc_dev[i] (ntxn u32 on member i's GPU;
+ * scc_dev[0] required, others may be NULL) = the largest txn of each txn's
+ * component, as hsc_dep_graph_scc of the whole history.  stats: member 0's
+ * SCC stats, build_ms = the slowest local build, edges = rows of the cut
+ * union.  Collective on a per-rank context. */
+typedef struct hsc_ops_dev {
+    size_t nops;
+    const uint32_t *txn;       /* [nops] */
+    const uint64_t *key;       /* [nops] */
+    const uint8_t *is_write;   /* [nops] */
+    const uint32_t *observed;  /* [nops] writer txn, 0xFFFFFFFF = initial version */
+} hsc_ops_dev;
+int hsc_multi_graph_scc(hsc_ctx *ctx, const hsc_ops_dev *ops, uint32_t ntxn, uint32_t *const *scc_dev,
+                        hsc_graph_stats *stats);
+/* Host ms of the last hsc_multi_graph_scc: build + cover, cover merge, cuts +
+ * their union, SCC. */
+int hsc_multi_graph_phase_ms(hsc_ctx *ctx, double out[4]);
 
 /* ---- harness support (tests / bench; not on the check path) --------------
  * CurRangeArr objects as comdb2 holds a received read set (db/comdb2.h:1105-1124;

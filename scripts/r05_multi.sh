@@ -15,14 +15,17 @@ step() {  # name limit cmd...
   echo "$name rc=$rc"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -5 $out/${tag}_$name.err; exit $rc; fi
 }
-if [ $part != b ]; then
-step pytest_multi 400 python -u -m pytest tests/test_gpu_multi.py -x -v --timeout 120 --timeout-method thread
+if [ $part = full ]; then
+step pytest 700 python -u -m pytest tests/ -m gpu -q -x --timeout 300 --timeout-method thread
+tail -2 $out/${tag}_pytest.log
+elif [ $part != b ]; then
+step pytest_multi 500 python -u -m pytest tests/test_gpu_multi.py tests/test_graph_shard.py -m gpu -k "multi or Multi or adopt or routed or lone or rccl or loopback" -v --timeout 120 --timeout-method thread
 tail -3 $out/${tag}_pytest_multi.log
 fi
 [ $part = a ] && exit 0
 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29531 step rank1 300 python -u bench.py --rank-path --steps 50
 step inproc2 400 python -u bench.py --inproc 2 --steps 30
-[ $part = ab ] && exit 0
+[ $part = ab ] || [ $part = full ] && exit 0
 step inproc2_loop 400 python -u bench.py --inproc 2 --steps 30 --loopback
 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29532 step trace_rank1 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/${tag}_trace_rank1 -o k -- python3 bench.py --rank-path --steps 20
 step trace_inproc2 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/${tag}_trace_inproc2 -o k -- python3 bench.py --inproc 2 --steps 20

@@ -305,7 +305,12 @@ def test_lone_calls_route_to_one_member(oracle_mod):
     per-transaction pattern of db/toblock.c:4777-4800): the host routing
     sends each call only to the members its ranges overlap, whose small
     kernels answer it."""
-    log, rs = random_case(960, n_commits=200, n_txn=60)
+    from comdb2_amd.workloads import config2
+    # one int64 index (narrow windows: the small path); one range per read
+    # set, so most calls touch one member (a read set of 10 uniform ranges
+    # nearly always touches both halves of the key space)
+    c2 = config2(n_commits=4000, n_txn=60, value_bits=24, width=1 << 10, ranges_per_txn=1)
+    log, rs = c2.log, c2.readsets
     want, _, _ = oracle_mod.check(log, rs)
     m = MultiValidator([0, 0])
     try:

@@ -209,3 +209,41 @@ def test_gpu_scc_cut_rejects_rows_outside_cover():
         assert scc.cpu().tolist() == [3, 3, 2, 3]
     finally:
         v.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("kw", CASES + [
+    dict(n_txn=300000, n_keys=300, concurrent_frac=0.3, max_lag=8, zipf=1.2),
+    dict(n_txn=1000000, n_keys=100000),
+])
+def test_gpu_multi_graph_scc_matches_oracle(oracle_mod, kw, world):
+    """hsc_multi_graph_scc: the sharded step behind the C ABI -- members of an
+    in-process multi context on the one GPU, each with its key shard's
+    device-resident ops: covers OR-ed over the members, cuts gathered to
+    member 0, its colouring SCC copied to every member = Tarjan over the
+    whole history (oracle/scc_oracle.c)."""
+    import torch
+    from comdb2_amd.hsc import MultiValidator
+    h = config4_history(**kw)
+    dev = torch.device("cuda", 0)
+    m = MultiValidator([0] * world)
+    try:
+        shards = [shard.device_history(shard.history_shard(h, r, world), dev) for r in range(world)]
+        sccs = [torch.zeros(h.ntxn, dtype=torch.int32, device=dev) for _ in range(world)]
+        torch.cuda.synchronize()
+        st = m.graph_scc(shards, h.ntxn, [x.data_ptr() for x in sccs])
+        s, d, _ = oracle_mod.dep_edges(h.txn, h.key, h.is_write, h.observed)
+        want = oracle_mod.scc(h.ntxn, s, d)
+        for r in range(world):
+            np.testing.assert_array_equal(sccs[r].cpu().numpy().astype(np.uint32), want,
+                                          err_msg=f"member {r}")
+        cyc = np.bincount(want, minlength=h.ntxn)[want] > 1
+        assert st["txns_in_cycles"] == int(cyc.sum())
+        assert set(st["phase_ms"]) == {"build_cover", "cover_merge", "cut_union", "scc"}
+        # a second call over the same members (buffers reused) agrees
+        st2 = m.graph_scc(shards, h.ntxn, [sccs[0].data_ptr()] + [None] * (world - 1))
+        np.testing.assert_array_equal(sccs[0].cpu().numpy().astype(np.uint32), want)
+        assert st2["cut_nodes"] == st["cut_nodes"]
+    finally:
+        m.close()
