@@ -132,52 +132,25 @@ def log_tail_commit(commit_lsn, snaps):
     return c0
 
 
-def _commit_stream_fold_leg(ev, rows, background):
-    """The config-1 stream again with the delta folded every `rows` rows
-    (about one fold per `rows` commits: one keyed write per commit), in the
-    background or inline: per-check latency and the fold counts."""
-    from comdb2_amd import hsc
-    from comdb2_amd.workloads import replay_incremental
-    v = hsc.Validator(0)
-    v.set_fold(rows, background=background)
-    t = []
-    replay_incremental(ev, v, mode="log", check_times=t)
-    st = v.fold_stats()
-    v.close()
-    x = np.array(t) * 1e6
-    return {"check_us": {"p50": float(np.median(x)), "p99": float(np.percentile(x, 99)),
-                         "p999": float(np.percentile(x, 99.9)), "max": float(x.max())},
-            "folds": st}
-
-
-def bench_commit_stream(args):
-    """Config 1: the tests/tools/serial.c-shaped commit stream (10k txns, 20
-    ids x 5 accounts, seed 0xC0FFEE01) replayed through the drop-in entry on
-    one GPU with the window kept up to date incrementally: per commit one
-    bdb_osql_serial_check (CurRangeArr, regop_only = 0) and, when it passes,
-    its log records appended (hsc_window_append_log: decoded on the host,
-    rows into the device delta run).  The reference path per commit is the
-    same check + the txn's logging (db/toblock.c:4779-4836,
-    bdb/tran.c:1545-1560).  Reports the stream rate and the per-call times of
-    checks and appends; verdicts are compared with the oracle replay's golden
-    (tests/golden/config1_replay.json)."""
+def _native_stream(ev, v):
+    """Replay a config-1 event stream through the drop-in entry of v, timing
+    only the native calls: per commit one hip_bdb_osql_serial_check on a
+    prebuilt CurRangeArr (snapshot = the log's end at the txn's begin) and,
+    when it passes, one hsc_window_append_log of its records (the C struct
+    built outside the timed call, as comdb2 hands it over).
+    -> (check seconds[], append seconds[], {txn: rc}, wall seconds)."""
     import ctypes as C
 
     from comdb2_amd import formats as F
     from comdb2_amd import hsc
-    from comdb2_amd.workloads import SEED_CONFIG1, config1_events
-    ev = config1_events(seed=SEED_CONFIG1, n_txn=args.n_txn_c1)
-    v = hsc.Validator(0)
     lb = F.LogBuilder()
     v.ingest_log(lb.build())
-    # CurRangeArr objects built ahead; the snapshot is set at begin time
     names = [t.name for e, t in ev if e == "begin"]
     txns = {t.name: t for e, t in ev if e == "begin"}
     arrs = {nm: hsc.CurRangeArrays([txns[nm].reads], [0]) for nm in names}
-    lib = v.lib
     f, o = C.c_uint(), C.c_uint()
     pf, po = C.byref(f), C.byref(o)
-    check, append, ctx = lib.hip_bdb_osql_serial_check, lib.hsc_window_append_log, v.ctx
+    check, append, ctx = v.lib.hip_bdb_osql_serial_check, v.lib.hsc_window_append_log, v.ctx
     t_check, t_app, rcs = [], [], {}
     t0 = time.perf_counter()
     for e, t in ev:
@@ -209,7 +182,57 @@ def bench_commit_stream(args):
             t_app.append(time.perf_counter() - c0)
             if rca != 0:
                 raise RuntimeError(f"hsc_window_append_log -> {rca}")
-    wall = time.perf_counter() - t0
+        del arrs[t.name]
+    return np.array(t_check), np.array(t_app), rcs, time.perf_counter() - t0
+
+
+def _pct(x, slow_us=None):
+    x = np.asarray(x) * 1e6
+    out = {"mean": float(x.mean()), "p50": float(np.median(x)), "p99": float(np.percentile(x, 99)),
+           "p999": float(np.percentile(x, 99.9)), "max": float(x.max()), "max_at": int(np.argmax(x))}
+    if slow_us is not None:  # the calls above slow_us: (index, us), at most 20
+        idx = np.nonzero(x > slow_us)[0]
+        out["slow"] = [(int(i), round(float(x[i]), 1)) for i in idx[:20]]
+        out["n_slow"] = int(len(idx))
+    return out
+
+
+def _commit_stream_fold_leg(ev, rows, background):
+    """The stream with the delta run folded into the main window every `rows`
+    rows (one keyed write per commit: about one fold per `rows` commits), in
+    the background or inline, timed natively like the main leg."""
+    from comdb2_amd import hsc
+    v = hsc.Validator(0)
+    if rows:
+        v.set_fold(rows, background=background)
+    tc, ta, rcs, wall = _native_stream(ev, v)
+    st = v.fold_stats()
+    v.close()
+    w = min(1000, len(tc) // 10)  # the stream's start: the first write to the index builds the window
+    return {"check_us": _pct(tc, slow_us=500), "append_us": _pct(ta, slow_us=500),
+            "check_us_after_first_1000": _pct(tc[w:]), "folds": st,
+            "value": len(tc) / (tc.sum() + ta.sum()), "unit": "commits/s", "checks": len(tc),
+            "wall_s": wall}, rcs
+
+
+def bench_commit_stream(args):
+    """Config 1: the tests/tools/serial.c-shaped commit stream (10k txns, 20
+    ids x 5 accounts, seed 0xC0FFEE01) replayed through the drop-in entry on
+    one GPU with the window kept up to date incrementally: per commit one
+    bdb_osql_serial_check (CurRangeArr, regop_only = 0) and, when it passes,
+    its log records appended (hsc_window_append_log: decoded on the host,
+    rows into the device delta run).  The reference path per commit is the
+    same check + the txn's logging (db/toblock.c:4779-4836,
+    bdb/tran.c:1545-1560).  Reports the stream rate and the per-call times of
+    checks and appends; verdicts are compared with the oracle replay's golden
+    (tests/golden/config1_replay.json).  `steady_state`: a 100k-txn stream of
+    the same generator with the default fold threshold (32768 rows), so the
+    window folds during the run, background vs inline folds (same verdicts)."""
+    from comdb2_amd import hsc
+    from comdb2_amd.workloads import SEED_CONFIG1, config1_events
+    ev = config1_events(seed=SEED_CONFIG1, n_txn=args.n_txn_c1)
+    v = hsc.Validator(0)
+    tc, ta, rcs, wall = _native_stream(ev, v)
     layout = {hsc.LAYOUT_NARROW: "narrow", hsc.LAYOUT_COMPACT: "compact",
               hsc.LAYOUT_WIDE: "wide"}.get(v.layout, str(v.layout))
     small = v.small_stats()
@@ -219,8 +242,22 @@ def bench_commit_stream(args):
     gpath = os.path.join(ROOT, "tests", "golden", "config1_replay.json")
     if os.path.exists(gpath) and args.n_txn_c1 == 10_000:
         parity = json.load(open(gpath))["rc"] == rcs
-    tc, ta = np.array(t_check), np.array(t_app)
     native = tc.sum() + ta.sum()
+    fb, rb = _commit_stream_fold_leg(ev, 1000, True)
+    fi, ri = _commit_stream_fold_leg(ev, 1000, False)
+    fb["parity_with_oracle_golden"] = parity is not None and rb == rcs and parity
+    fi["parity_with_oracle_golden"] = parity is not None and ri == rcs and parity
+    steady = None
+    if args.c1_steady:
+        ev2 = config1_events(seed=SEED_CONFIG1 + 1, n_txn=args.c1_steady)
+        sb, rsb = _commit_stream_fold_leg(ev2, 0, True)      # default threshold, background
+        si, rsi = _commit_stream_fold_leg(ev2, 32768, False)  # the same threshold, inline
+        steady = {"txns": args.c1_steady, "fold_rows": 32768, "background": sb, "inline": si,
+                  "verdicts_equal": rsb == rsi,
+                  "not_serializable": int(sum(r != 0 for r in rsb.values())),
+                  "note": "seed 0xC0FFEE02 stream of the config-1 generator; the default fold "
+                          "threshold folds the delta run into the main window every 32768 "
+                          "appended rows (two keyed rows per passing commit)"}
     out = {"metric": "commit-stream serializable checks/sec (drop-in entry + incremental window)",
            "value": len(tc) / native, "unit": "commits/s", "n_gpus": 1, "steps": len(tc),
            "warmup": 0, "ms_per_step": native / len(tc) * 1e3, "higher_is_better": True,
@@ -231,15 +268,11 @@ def bench_commit_stream(args):
                                   "one check per commit, passing txns appended",
                       "checks": len(tc), "not_serializable": int(sum(r != 0 for r in rcs.values())),
                       "appends": len(ta)},
-           "check_us": {"mean": float(tc.mean() * 1e6), "p50": float(np.median(tc) * 1e6),
-                        "p99": float(np.percentile(tc, 99) * 1e6)},
-           "append_us_per_commit": {"mean": float(ta.mean() * 1e6), "p50": float(np.median(ta) * 1e6),
-                                    "p99": float(np.percentile(ta, 99) * 1e6)},
+           "check_us": _pct(tc), "append_us_per_commit": _pct(ta),
            "stream_wall_s": wall, "parity_with_oracle_golden": parity,
            "cpu_baseline": None if args.no_cpu else commit_stream_cpu_baseline(args),
-           "fold_every_1k_commits": {
-               "background": _commit_stream_fold_leg(ev, 1000, True),
-               "inline": _commit_stream_fold_leg(ev, 1000, False)},
+           "fold_every_1k_commits": {"background": fb, "inline": fi},
+           "steady_state": steady,
            "note": "value = commits / (time inside the native check and append calls: "
                    "hip_bdb_osql_serial_check and hsc_window_append_log on prebuilt C structs); "
                    "the wall time also holds the Python log builder and struct marshalling that "
@@ -1051,6 +1084,8 @@ def main():
                          "groups, group shards; 4: dependency graph + SCC of a history; "
                          "5: Zipf hot keys over a large window (per-GPU imbalance reported)")
     ap.add_argument("--n-txn-c1", type=int, default=10_000, help="config 1: txns in the stream")
+    ap.add_argument("--c1-steady", type=int, default=100_000,
+                    help="config 1: txns of the steady-state leg (default fold threshold; 0: skip)")
     ap.add_argument("--c3-writes", type=int, default=4_000_000,
                     help="config 3: index writes per GPU (log-normal group sizes)")
     ap.add_argument("--c5-keys", type=int, default=125_000_000,

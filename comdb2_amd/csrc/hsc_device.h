@@ -7,6 +7,28 @@
 
 namespace hsc {
 
+// Hacker's Delight compress / expand of the bits of x under mask m, with the
+// moves of compress_moves(m) (the packed sorts, hsc_ingest.hip; the graph's
+// packed writer search, hsc_graph.hip): compress keeps the order of values
+// that agree outside m.
+__device__ __forceinline__ uint64_t bits_compress(uint64_t x, uint64_t m, const uint64_t (&mv)[6])
+{
+    x &= m;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        const uint64_t t = x & mv[i];
+        x = (x ^ t) | (t >> (1 << i));
+    }
+    return x;
+}
+
+__device__ __forceinline__ uint64_t bits_expand(uint64_t x, uint64_t m, const uint64_t (&mv)[6])
+{
+#pragma unroll
+    for (int i = 5; i >= 0; --i) x = (x & ~mv[i]) | ((x << (1 << i)) & mv[i]);
+    return x & m;
+}
+
 // Native vectors: register arrays of these stay in VGPRs (arrays of the HIP
 // uint4 / ulonglong2 structs can be demoted to scratch).
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));

@@ -19,12 +19,14 @@
 // with scc = colour.  In a dependency graph almost every edge goes forward in
 // commit order, so colours only move across stale-read (rw) windows and the
 // rounds are few.
+#include "hsc_device.h"
 #include "hsc_internal.h"
 
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <utility>
+#include <vector>
 
 namespace hsc {
 
@@ -54,6 +56,7 @@ __global__ void k_write_flags(size_t nops, const uint8_t *is_write, uint32_t *fl
 // Edge rows: word = src << 32 | dst, payload = type; invalid = ~0.
 // Slots [0, nu): ww of unique writer i -> i+1; slots nu + 2i, nu + 2i + 1:
 // wr / rw of op i.
+// (et / eg null: a raw build -- the rows alone; the type is the slot's)
 __global__ void k_edges_ww(uint32_t nu, const uint64_t *wkey, const uint64_t *wtxn,
                            uint64_t *ew, uint64_t *et, uint32_t *eg)
 {
@@ -62,8 +65,10 @@ __global__ void k_edges_ww(uint32_t nu, const uint64_t *wkey, const uint64_t *wt
     uint64_t e = ~0ull;
     if (i + 1 < nu && wkey[i] == wkey[i + 1]) e = (wtxn[i] << 32) | wtxn[i + 1];
     ew[i] = e;
-    et[i] = kDepWW;
-    eg[i] = 0;
+    if (et) {
+        et[i] = kDepWW;
+        eg[i] = 0;
+    }
 }
 
 __global__ void k_edges_reads(size_t nops, const uint32_t *txn, const uint64_t *key,
@@ -94,11 +99,144 @@ __global__ void k_edges_reads(size_t nops, const uint32_t *txn, const uint64_t *
     }
     const size_t s = (size_t)nu + 2 * i;
     ew[s] = wr;
-    et[s] = kDepWR;
-    eg[s] = 0;
     ew[s + 1] = rw;
-    et[s + 1] = kDepRW;
-    eg[s + 1] = 0;
+    if (et) {
+        et[s] = kDepWR;
+        eg[s] = 0;
+        et[s + 1] = kDepRW;
+        eg[s + 1] = 0;
+    }
+}
+
+// ---- packed writer search ----
+// When the writers sorted as packed (key, txn) words (graph_build), every
+// distinct writer is one u64 pk[i] = compress(key) << tb | compress(txn),
+// ascending, and a directory of 2^D buckets over [pk[0], pk[nu - 1]] gives
+// each bucket's first writer: a read's "first writer after (k, ob)" is one
+// directory line plus a binary search inside its bucket (~30 writers on
+// uniform keys) instead of ~26 dependent steps over the 16-byte rows.
+struct PairPack {
+    uint64_t km, tm;          // the writers' varying key / txn bits
+    uint64_t kc, tc;          // their constant bits (the same in every writer)
+    uint64_t kmv[6], tmv[6];  // compress moves
+    uint64_t base, last;      // pk[0], pk[nu - 1]
+    int tb, D, shift;         // txn bits, directory bits, bucket = (pk - base) >> shift
+};
+
+// bucket of x: 0 below the range, 2^D past it
+__device__ __forceinline__ uint64_t pair_bucket(const PairPack &pp, uint64_t x)
+{
+    if (x <= pp.base) return 0;
+    const uint64_t b = pp.shift >= 64 ? 0 : (x - pp.base) >> pp.shift;
+    return b < (1ull << pp.D) ? b : (1ull << pp.D);
+}
+
+__device__ __forceinline__ uint64_t pair_key(const PairPack &pp, uint64_t kp) { return pp.tb >= 64 ? 0 : kp << pp.tb; }
+
+__global__ void k_pair_keys(uint32_t nu, const uint64_t *wkey, const uint64_t *wtxn, PairPack pp, uint64_t *pk)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nu) return;
+    uint64_t km[6], tm[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) km[q] = pp.kmv[q], tm[q] = pp.tmv[q];
+    pk[i] = pair_key(pp, bits_compress(wkey[i], pp.km, km)) | bits_compress(wtxn[i], pp.tm, tm);
+}
+
+// dir[b] = first writer >= base + (b << shift), b in [0, 2^D + 1] (one
+// binary search per bucket: the same cost for any key distribution -- a
+// thread per writer filling the buckets up to the next one serialises on
+// empty stretches)
+__global__ void k_pair_dir(uint32_t nu, const uint64_t *pk, PairPack pp, uint32_t *dir)
+{
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > (1ull << pp.D) + 1) return;
+    uint32_t lo = nu;
+    if (b == 0) {
+        lo = 0;
+    } else if (pp.shift < 64 && b <= ((pp.last - pp.base) >> pp.shift)) {
+        const uint64_t x = pp.base + (b << pp.shift);
+        uint32_t hi = nu;
+        lo = 0;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pk[mid] < x)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+    }
+    dir[b] = lo;
+}
+
+__global__ void k_edges_reads_pk(size_t nops, const uint32_t *txn, const uint64_t *key,
+                                 const uint8_t *is_write, const uint32_t *observed, uint32_t nu,
+                                 const uint64_t *wkey, const uint64_t *wtxn, const uint64_t *pk,
+                                 const uint32_t *dir, PairPack pp, uint64_t *ew, uint64_t *et,
+                                 uint32_t *eg, int skip_rw)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nops) return;
+    uint64_t wr = ~0ull, rw = ~0ull;
+    if (!is_write[i]) {
+        const uint32_t r = txn[i], ob = observed[i];
+        const uint64_t k = key[i];
+        if (ob != kNone && ob != r) wr = ((uint64_t)ob << 32) | r;
+        // a key outside the writers' constant bits has no writer at all
+        if (!skip_rw && (k & ~pp.km) == pp.kc) {
+            uint32_t lo = 0, hi = nu;
+            bool found = false;
+            if (ob == kNone || (ob & ~pp.tm) == pp.tc) {
+                uint64_t km[6], tm[6];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) km[q] = pp.kmv[q], tm[q] = pp.tmv[q];
+                const uint64_t kp = bits_compress(k, pp.km, km);
+                // initial version: first writer >= (k, any); else first > (k, ob)
+                const uint64_t x = pair_key(pp, kp) | (ob == kNone ? 0 : bits_compress(ob, pp.tm, tm));
+                const bool strict = ob != kNone;
+                const uint64_t b = pair_bucket(pp, x);
+                lo = dir[b];
+                hi = dir[b + 1];
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    const uint64_t v = pk[mid];
+                    if (strict ? v <= x : v < x)
+                        lo = mid + 1;
+                    else
+                        hi = mid;
+                }
+                if (lo < nu) {
+                    const uint64_t v = pk[lo];
+                    const uint64_t tmask = pp.tb >= 64 ? ~0ull : (1ull << pp.tb) - 1;
+                    if ((pp.tb >= 64 ? 0 : v >> pp.tb) == kp) {
+                        const uint32_t wt = (uint32_t)(bits_expand(v & tmask, pp.tm, tm) | pp.tc);
+                        if (wt != r) rw = ((uint64_t)r << 32) | wt;
+                    }
+                }
+                found = true;
+            }
+            if (!found) {  // an observed txn outside the writers' bits: the row search
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    const uint64_t mk = wkey[mid], mt = wtxn[mid];
+                    if (mk < k || (mk == k && mt <= ob))
+                        lo = mid + 1;
+                    else
+                        hi = mid;
+                }
+                if (lo < nu && wkey[lo] == k && wtxn[lo] != r) rw = ((uint64_t)r << 32) | wtxn[lo];
+            }
+        }
+    }
+    const size_t s = (size_t)nu + 2 * i;
+    ew[s] = wr;
+    ew[s + 1] = rw;
+    if (et) {
+        et[s] = kDepWR;
+        eg[s] = 0;
+        et[s + 1] = kDepRW;
+        eg[s + 1] = 0;
+    }
 }
 
 // Merge runs of equal edges (rows sorted, invalid ~0 rows at the end):
@@ -334,18 +472,41 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
                                                       g.ww.as<uint64_t>(), g.wl.as<uint64_t>(), wcap);
     CK(hipGetLastError());
     size_t rsb = std::max(radix_scratch_bytes(nw, 2), scan_scratch_bytes(nw) + 64);
+    rsb = std::max(rsb, packed_scratch_bytes(nw));
     CK(g.scratch.ensure(rsb));
-    bool alt = false;
-    CK(radix_sort_rows(2, nw, g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), g.wl.as<uint64_t>(), wcap,
-                       g.wg2.as<uint32_t>(), g.ww2.as<uint64_t>(), g.wl2.as<uint64_t>(),
-                       g.scratch.p, g.scratch.bytes, &alt, nullptr, s));
-    DBuf *sg = alt ? &g.wg2 : &g.wg, *sw = alt ? &g.ww2 : &g.ww, *sl = alt ? &g.wl2 : &g.wl;
-    DBuf *dg = alt ? &g.wg : &g.wg2, *dw = alt ? &g.ww : &g.ww2, *dl = alt ? &g.wl : &g.wl2;
-    CK(g.flags.ensure(4 * (wcap + 64)));
     CK(g.count.ensure(64));
-    CK(dedupe_rows(2, nw, sg->as<uint32_t>(), sw->as<uint64_t>(), sl->as<uint64_t>(), wcap,
-                   dg->as<uint32_t>(), dw->as<uint64_t>(), dl->as<uint64_t>(), wcap,
-                   g.flags.as<uint32_t>(), g.scratch.p, g.scratch.bytes, g.count.as<uint32_t>(), s));
+    // (key, txn) pairs whose varying bits fit 64 sort as single words, the
+    // pair itself being the key (no row index, nothing to gather): one 8-byte
+    // read + write per pass and varying byte, the dedupe fused into the
+    // unpack (hsc_ingest.hip).  Else the whole-row sort + dedupe.
+    uint64_t vary[3] = {~0ull, ~0ull, ~0ull};
+    PackPlan P{};
+    bool packed = false;
+    if (nw) {
+        CK(vary_mask_rows(2, nw, g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), wcap, g.count.p, vary, s));
+        packed = packed_plan(2, nw, vary, &P, false);
+    }
+    DBuf *dw = &g.ww2;
+    if (packed) {
+        uint64_t *lsn_d = nullptr;
+        CK(packed_sort_dedupe(P, nw, g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), nullptr, wcap,
+                              g.wl.as<uint64_t>(), g.wl2.as<uint64_t>(), nullptr, nullptr, nullptr, 0,
+                              g.wg2.as<uint32_t>(), g.ww2.as<uint64_t>(), wcap, &lsn_d,
+                              g.count.as<uint32_t>(), g.scratch.p, g.scratch.bytes, s));
+    } else {
+        bool alt = false;
+        CK(radix_sort_rows(2, nw, g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), g.wl.as<uint64_t>(), wcap,
+                           g.wg2.as<uint32_t>(), g.ww2.as<uint64_t>(), g.wl2.as<uint64_t>(),
+                           g.scratch.p, g.scratch.bytes, &alt, nullptr, s));
+        DBuf *sg = alt ? &g.wg2 : &g.wg, *sw = alt ? &g.ww2 : &g.ww, *sl = alt ? &g.wl2 : &g.wl;
+        DBuf *dg = alt ? &g.wg : &g.wg2, *dl = alt ? &g.wl : &g.wl2;
+        dw = alt ? &g.ww : &g.ww2;
+        CK(g.flags.ensure(4 * (wcap + 64)));
+        CK(dedupe_rows(2, nw, sg->as<uint32_t>(), sw->as<uint64_t>(), sl->as<uint64_t>(), wcap,
+                       dg->as<uint32_t>(), dw->as<uint64_t>(), dl->as<uint64_t>(), wcap,
+                       g.flags.as<uint32_t>(), g.scratch.p, g.scratch.bytes, g.count.as<uint32_t>(), s));
+    }
+    g.writer_packed = packed;
     uint32_t nu = 0;
     CK(hipMemcpyAsync(&nu, g.count.p, 4, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
@@ -360,13 +521,41 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     CK(g.ew2.ensure(8 * ecap));
     CK(g.et2.ensure(8 * ecap));
     CK(g.eg2.ensure(4 * ecap));
-    if (nu) k_edges_ww<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, g.ew.as<uint64_t>(),
-                                                   g.et.as<uint64_t>(), g.eg.as<uint32_t>());
-    if (nops)
+    uint64_t *et = full || in.n_extra ? g.et.as<uint64_t>() : nullptr;  // raw: rows only
+    uint32_t *eg = full || in.n_extra ? g.eg.as<uint32_t>() : nullptr;
+    if (nu) k_edges_ww<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, g.ew.as<uint64_t>(), et, eg);
+    if (nops && packed && nu) {
+        PairPack pp{};
+        uint64_t r0[2];
+        CK(hipMemcpyAsync(&r0[0], wkey, 8, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpyAsync(&r0[1], wtxn, 8, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        pp.km = vary[0], pp.tm = vary[1];
+        pp.kc = r0[0] & ~pp.km, pp.tc = r0[1] & ~pp.tm;
+        compress_moves(pp.km, pp.kmv);
+        compress_moves(pp.tm, pp.tmv);
+        pp.tb = __builtin_popcountll(pp.tm);
+        // about 32 writers per bucket, at most 2^20 buckets
+        pp.D = 1;
+        while (pp.D < 20 && ((size_t)32 << pp.D) < nu) ++pp.D;
+        CK(g.pk.ensure(8 * (size_t)nu));
+        CK(g.pdir.ensure(4 * (((size_t)1 << pp.D) + 2)));
+        k_pair_keys<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, pp, g.pk.as<uint64_t>());
+        CK(hipMemcpyAsync(&pp.base, g.pk.as<uint64_t>(), 8, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpyAsync(&pp.last, g.pk.as<uint64_t>() + nu - 1, 8, hipMemcpyDeviceToHost, s));
+        CK(hipStreamSynchronize(s));
+        pp.shift = 0;  // (last - base) >> shift < 2^D
+        while (pp.shift < 64 && ((pp.last - pp.base) >> pp.shift) >= ((uint64_t)1 << pp.D)) ++pp.shift;
+        k_pair_dir<<<blocks(((size_t)1 << pp.D) + 2), 256, 0, s>>>(nu, g.pk.as<uint64_t>(), pp,
+                                                                 g.pdir.as<uint32_t>());
+        k_edges_reads_pk<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu,
+                                                      wkey, wtxn, g.pk.as<uint64_t>(), g.pdir.as<uint32_t>(),
+                                                      pp, g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0);
+    } else if (nops) {
         k_edges_reads<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed,
-                                                   nu, wkey, wtxn, g.ew.as<uint64_t>(),
-                                                   g.et.as<uint64_t>(), g.eg.as<uint32_t>(),
+                                                   nu, wkey, wtxn, g.ew.as<uint64_t>(), et, eg,
                                                    in.skip_rw ? 1 : 0);
+    }
     CK(hipGetLastError());
     if (in.n_extra) {  // staged edges (rw pairs of the validator's join) after the history's
         const size_t o = (size_t)nu + 2 * nops;
@@ -686,12 +875,53 @@ hipError_t graph_cover(GraphBufs &g, uint32_t nn, uint8_t *cover, hipStream_t s)
     return hipGetLastError();
 }
 
+// One pass for the usual tiny cut: edges with both ends covered appended
+// at a wave-aggregated atomic cursor (rows beyond cap are counted, not
+// stored: the caller then takes the flag + scan path).
+__global__ void k_cut_append(EdgeSet es, const uint8_t *cover, uint64_t *rows, uint32_t *cnt, uint32_t cap)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t a = 0, b = 0;
+    const bool hit = i < es.n && es.get(i, a, b) && cover[a] && cover[b];
+    const uint64_t m = __ballot(hit);
+    if (!m) return;
+    const int lane = threadIdx.x & 63, first = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    base = __shfl(base, first, 64);
+    const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    if (hit && slot < cap) rows[slot] = ((uint64_t)a << 32) | b;
+}
+
+constexpr uint32_t kCutFastCap = 1u << 16;
+
 hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s)
 {
     hipError_t e = hipSuccess;
     const EdgeSet es = edge_set(g);
     const size_t ne = es.n;
     *m = 0;
+    {
+        // the usual tiny cut: one pass, then sorted on the host
+        if ((e = g.cut.ensure(8 * (size_t)kCutFastCap)) != hipSuccess) return e;
+        if ((e = g.count.ensure(64)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(g.count.p, 0, 4, s)) != hipSuccess) return e;
+        if (ne) k_cut_append<<<blocks(ne), 256, 0, s>>>(es, cover, g.cut.as<uint64_t>(), g.count.as<uint32_t>(),
+                                                        kCutFastCap);
+        uint32_t k = 0;
+        if ((e = hipMemcpyAsync(&k, g.count.p, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        if (k <= kCutFastCap) {
+            std::vector<uint64_t> h(k);
+            if (k) {
+                if ((e = hipMemcpy(h.data(), g.cut.p, 8 * (size_t)k, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+                std::sort(h.begin(), h.end());
+                if ((e = hipMemcpy(g.cut.p, h.data(), 8 * (size_t)k, hipMemcpyHostToDevice)) != hipSuccess) return e;
+            }
+            *m = k;
+            return hipGetLastError();
+        }
+    }
     if ((e = g.flags.ensure(4 * (ne + 64))) != hipSuccess) return e;
     if ((e = g.scratch.ensure(std::max(scan_scratch_bytes(ne + 1), (size_t)1024))) != hipSuccess)
         return e;

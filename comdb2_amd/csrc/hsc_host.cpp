@@ -1297,13 +1297,24 @@ static DeltaView frozen_view(const hsc_ctx *c)
     return d;
 }
 
+// Stream priorities: the small-batch streams (a lone check's latency) get
+// the device's highest, a background fold's build the lowest, so a fold's
+// kernels never sit in front of a check's in a hardware queue.
+static hipError_t create_stream(hipStream_t *st, bool high)
+{
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest)
+        return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+    return hipStreamCreateWithPriority(st, hipStreamNonBlocking, high ? greatest : least);
+}
+
 static int shadow_ctx(hsc_ctx *c)
 {
     if (c->shadow) return HSC_OK;
     hsc_ctx *s = new (std::nothrow) hsc_ctx();
     if (!s) return fail(c, HSC_ENOMEM, "fold context");
     s->device = c->device;
-    if (hipStreamCreateWithFlags(&s->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    if (create_stream(&s->own_stream, false) != hipSuccess) {
         delete s;
         return fail(c, HSC_EDEVICE, "fold stream");
     }
@@ -2742,7 +2753,7 @@ static int small_launch(hsc_ctx *c, Stage &st)
         return fail(c, HSC_EINVAL, "small batch marshalled outside the small stage");
     std::swap(sl.io, st.arena);
     HIPCHK(c, c->small_blocks.ensure(64 * hsc_ctx::kSmallSlots));
-    if (!c->small_side[k]) HIPCHK(c, hipStreamCreateWithFlags(&c->small_side[k], hipStreamNonBlocking));
+    if (!c->small_side[k]) HIPCHK(c, create_stream(&c->small_side[k], true));
     hipStream_t s = c->small_side[k];
     sl.wait_ev = nullptr;
     if (c->app_last && c->small_app_seq[k] != c->app_seq) {  // after the appends' device work
@@ -4345,6 +4356,18 @@ int ctx_edge_keys(hsc_ctx *c, uint32_t *gid, uint64_t *words)
         HIPCHK(c, hipMemcpy(words + c->W + j, c->d_words.as<uint64_t>() + (size_t)j * c->cap + last, 8,
                             hipMemcpyDeviceToHost));
     }
+    return HSC_OK;
+}
+
+// The cut of the last build under cover (one pass: count + rows); *rows
+// points into the context's own buffer until its next graph call.
+int ctx_graph_cut(hsc_ctx *c, const uint8_t *cover, size_t *m, const uint64_t **rows)
+{
+    std::lock_guard<std::mutex> g(c->mu);
+    (void)hipSetDevice(c->device);
+    HIPCHK(c, graph_cut(c->graph, cover, m, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    *rows = c->graph.cut.as<uint64_t>();
     return HSC_OK;
 }
 

@@ -37,21 +37,13 @@ constexpr int kPkWaves = kPkThreads / 64;
 
 __device__ __forceinline__ uint64_t pk_compress(uint64_t x, uint64_t m, const uint64_t (&mv)[6])
 {
-    x &= m;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        const uint64_t t = x & mv[i];
-        x = (x ^ t) | (t >> (1 << i));
-    }
-    return x;
+    return bits_compress(x, m, mv);
 }
 
 // inverse of pk_compress (Hacker's Delight expand: the same moves, reversed)
 __device__ __forceinline__ uint64_t pk_expand(uint64_t x, uint64_t m, const uint64_t (&mv)[6])
 {
-#pragma unroll
-    for (int i = 5; i >= 0; --i) x = (x & ~mv[i]) | ((x << (1 << i)) & mv[i]);
-    return x & m;
+    return bits_expand(x, m, mv);
 }
 
 __device__ __forceinline__ uint64_t pk_limb(const PackPlan &P, int l, size_t i, const uint32_t *gid,
@@ -87,7 +79,7 @@ __global__ __launch_bounds__(kPkThreads) void k_pk_pack(PackPlan P, size_t n, co
                 }
             }
         }
-        key[k] = (kb << P.I) | (uint64_t)i;
+        key[k] = P.I ? (kb << P.I) | (uint64_t)i : kb;  // I = 0: the key is the whole row
     }
 #pragma unroll
     for (int k = 0; k < kPkItems; ++k) {
@@ -324,7 +316,7 @@ __global__ __launch_bounds__(kUdThreads) void k_pk_unpack_dd(
         const size_t i = base + j;
         const uint64_t key = K[j];
         uint64_t kb = key >> P.I;
-        const uint64_t lv = lsn_in[key & imask];
+        const uint64_t lv = lsn_in ? lsn_in[key & imask] : 0;
         uint64_t limb[kPackMaxWords + 1];
 #pragma unroll
         for (int q = 0; q <= kPackMaxWords; ++q) {
@@ -346,13 +338,15 @@ __global__ __launch_bounds__(kUdThreads) void k_pk_unpack_dd(
             for (int q = 0; q <= kPackMaxWords; ++q)
                 if (q == id) limb[q] = (limb[q] & ~P.mask[l]) | v;
         }
-        gid_o[i] = (uint32_t)limb[W];
+        if (gid_o) {  // (null: the distinct rows only)
+            gid_o[i] = (uint32_t)limb[W];
 #pragma unroll
-        for (int q = 0; q < kPackMaxWords; ++q) {
-            if (q >= W) break;
-            words_o[(size_t)q * stride_o + i] = limb[q];
+            for (int q = 0; q < kPackMaxWords; ++q) {
+                if (q >= W) break;
+                words_o[(size_t)q * stride_o + i] = limb[q];
+            }
+            lsn_o[i] = lv;
         }
-        lsn_o[i] = lv;
         const uint32_t p = pos[j];
         if (p != 0xFFFFFFFFu) {
             const size_t d = (size_t)b0 + p;
@@ -377,13 +371,14 @@ size_t packed_scratch_bytes(size_t n)
            (ud + 16) * sizeof(uint32_t) + scan_scratch_bytes(ud) + 8 * (kPackMaxWords + 1) + 64;
 }
 
-bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P)
+bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P, bool index)
 {
     if (W > kPackMaxWords || n >= 0xFFFFFFFFull) return false;
     *P = PackPlan{};
     P->W = W;
     int I = 1;
     while (I < 32 && ((size_t)1 << I) < n) ++I;
+    if (!index) I = 0;
     P->I = I;
     int B = 0, nl = 0;
     // limb order, most significant first: gid, then word 0 .. W - 1

@@ -156,10 +156,13 @@ struct PackPlan {
     uint64_t mask[kPackLimbs];  // the limb's varying bits
     uint64_t mv[kPackLimbs][6]; // their compress moves
 };
-bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P);  // false: does not fit
+// false: does not fit.  index = false: no row index (I = 0) -- the packed
+// key is the whole row (no LSN to gather; equal rows are duplicates)
+bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P, bool index = true);
 size_t packed_scratch_bytes(size_t n);
 // The packed sort with the dedupe fused into the unpack: every version to
-// (gid_o, words_o, lsn_o), the distinct rows to (gid_d, words_d) -- which may
+// (gid_o, words_o, lsn_o) (gid_o null: not written; lsn null: LSNs 0), the
+// distinct rows to (gid_d, words_d) -- which may
 // be the input gid / words -- and to *lsn_d = whichever of k0 / k1 the sorted
 // keys did not end in; d_count[0] = distinct rows
 hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, const uint64_t *words,
@@ -447,17 +450,19 @@ struct GraphBufs {
     DBuf h_txn, h_key, h_isw, h_obs;           // uploaded history
     DBuf diff, cut, cut_id, txn_of;            // sharded SCC: cover, cut rows, cut ids
     DBuf x_rows, x_type, x_map;                // staged extra edges (rw pairs)
+    DBuf pk, pdir;                             // packed distinct writers + their directory
     size_t n_extra = 0;
     size_t ne = 0;
     size_t ne_raw = 0;  // raw edge slots in ew
     bool raw = false;   // last build kept raw rows only (no sort / CSR)
+    bool writer_packed = false;  // last build sorted its writers as packed (key, txn) words
     void release_all()
     {
         DBuf *all[] = {&flags, &flags2, &scratch, &count, &wg, &ww, &wl, &wg2, &ww2, &wl2,
                        &ew, &et, &eg, &ew2, &et2, &eg2, &swap_rows, &src, &out_dst, &type,
                        &in_src, &in_dst, &out_off, &in_off, &scc, &active, &color, &mark,
                        &front, &front2, &h_txn, &h_key, &h_isw, &h_obs, &diff, &cut,
-                       &cut_id, &txn_of, &x_rows, &x_type, &x_map};
+                       &cut_id, &txn_of, &x_rows, &x_type, &x_map, &pk, &pdir};
         for (DBuf *b : all) b->release();
     }
 };

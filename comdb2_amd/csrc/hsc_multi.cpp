@@ -1636,19 +1636,15 @@ int hsc_multi_graph_scc(hsc_ctx *f, const hsc_ops_dev *ops, uint32_t ntxn, uint3
     const auto t2 = SteadyClock::now();
     // 3. every member's edges between covered txns
     size_t k[kMultiMax] = {};
+    const uint64_t *cut[kMultiMax] = {};
     for (int m = 0; m < NL; ++m) {
         hsc_ctx *c = M->mem[m];
-        int rc = hsc_dep_graph_cut(c, M->g_cover[m].as<uint8_t>(), nullptr, 0, &k[m]);
-        if (!rc) {
-            MCHK(f, hipSetDevice(c->device));
-            MCHK(f, M->g_rows[m].ensure(8 * std::max<size_t>(k[m], 1)));
-            rc = hsc_dep_graph_cut(c, M->g_cover[m].as<uint8_t>(), M->g_rows[m].as<uint64_t>(), k[m], &k[m]);
-        }
+        const int rc = ctx_graph_cut(c, M->g_cover[m].as<uint8_t>(), &k[m], &cut[m]);
         if (rc) return mfail(f, rc, ("graph cut: " + c->err).c_str());
     }
     // 4. the union of the cuts where the SCC runs: every rank (all-gather,
     // each rank's rows padded with ~0 to the largest), or member 0 here
-    const uint64_t *rows = M->g_rows[0].as<uint64_t>();
+    const uint64_t *rows = cut[0];
     size_t total = k[0], cut_rows = k[0];
     if (M->rccl && N > 1) {
         MCHK(f, hipSetDevice(M->mem[0]->device));
@@ -1663,6 +1659,7 @@ int hsc_multi_graph_scc(hsc_ctx *f, const hsc_ops_dev *ops, uint32_t ntxn, uint3
         cut_rows = 0;
         for (int r = 0; r < N; ++r) mx = std::max<size_t>(mx, sz[r]), cut_rows += sz[r];
         MCHK(f, M->g_rows[0].ensure(8 * mx));
+        if (k[0]) MCHK(f, hipMemcpy(M->g_rows[0].p, cut[0], 8 * k[0], hipMemcpyDeviceToDevice));
         if (mx > k[0]) MCHK(f, hipMemset(M->g_rows[0].as<uint64_t>() + k[0], 0xFF, 8 * (mx - k[0])));
         MCHK(f, M->g_all[0].ensure(8 * mx * (size_t)N));
         NCHK(f, R.AllGather(M->g_rows[0].p, M->g_all[0].p, mx, ncclUint64, M->comm[0], l0.stream));
@@ -1678,7 +1675,7 @@ int hsc_multi_graph_scc(hsc_ctx *f, const hsc_ops_dev *ops, uint32_t ntxn, uint3
         size_t o = 0;
         for (int d = 0; d < NL; ++d) {
             if (k[d])
-                MCHK(f, hipMemcpyPeer(M->g_all[0].as<uint64_t>() + o, M->mem[0]->device, M->g_rows[d].p,
+                MCHK(f, hipMemcpyPeer(M->g_all[0].as<uint64_t>() + o, M->mem[0]->device, cut[d],
                                       M->mem[d]->device, 8 * k[d]));
             o += k[d];
         }

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Config 4 after the packed writer search: graph GPU tests, bench line, trace.
+tag=${1:-r05c4b}
+out=gpurun_out; mkdir -p $out
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+step() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 $lim "$@" > $out/${tag}_$name.log 2> $out/${tag}_$name.err
+  local rc=$?
+  echo "$name rc=$rc"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then tail -5 $out/${tag}_$name.err; exit $rc; fi
+}
+step pytest 400 python -u -m pytest tests/test_graph.py tests/test_graph_shard.py tests/test_gpu_jepsen.py -m gpu -q -x --timeout 200 --timeout-method thread
+tail -2 $out/${tag}_pytest.log
+step bench 500 python -u bench.py --config 4 --no-cpu
+step trace 500 rocprofv3 --kernel-trace --stats --output-format csv -d $out/${tag}_trace -o k -- python3 bench.py --config 4 --steps 3 --warmup 1 --no-cpu

@@ -142,6 +142,34 @@ def test_gpu_graph_matches_oracle(validator, oracle_mod, kw):
     assert st["edges"] == len(s)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("keymap", ["clusters", "hashed", "shifted"])
+def test_gpu_graph_key_layouts_match_oracle(validator, oracle_mod, keymap):
+    """The writers' (key, txn) pairs sort as packed words when their varying
+    bits fit 64 (a bucket directory over the packed range then answers each
+    read's next-writer search), else as whole rows with a plain binary
+    search: keys in two far-apart clusters (packed, a huge empty stretch
+    between the directory's buckets), 64-bit hashed keys (rows), keys
+    shifted to the top bits of the word (packed)."""
+    from comdb2_amd.workloads import History
+    h = config4_history(n_txn=60000, n_keys=3000, concurrent_frac=0.1, max_lag=16)
+    k = h.key.astype(np.uint64)
+    if keymap == "clusters":
+        k = np.where(k % 2 == 1, k + np.uint64(1 << 40), k)
+    elif keymap == "hashed":
+        k = (k * np.uint64(0x9E3779B97F4A7C15)) ^ np.uint64(0xD1B54A32D192ED03)
+    else:
+        k = k << np.uint64(50)
+    h = History(h.txn, k, h.is_write, h.observed, h.ntxn)
+    scc, st = validator.dep_graph_scc(h)
+    s, d, t = oracle_mod.dep_edges(h.txn, h.key, h.is_write, h.observed)
+    gs, gd, gt = validator.dep_graph_edges()
+    np.testing.assert_array_equal(gs, s)
+    np.testing.assert_array_equal(gd, d)
+    np.testing.assert_array_equal(gt, t)
+    np.testing.assert_array_equal(scc, oracle_mod.scc(h.ntxn, s, d))
+
+
 def _cover_frac(h, s, d):
     back = s > d
     diff = np.zeros(h.ntxn + 1, np.int64)
