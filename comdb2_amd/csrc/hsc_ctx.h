@@ -461,6 +461,9 @@ struct hsc_ctx {
     int layout = HSC_LAYOUT_AUTO;  // hsc_set_layout
     bool narrow = false;           // 64-bit codes + 16-ary index (hsc_narrow.hip)
     int lw = 0, tz = 0;  // least significant varying limb / its constant low bits
+    bool ncomp = false;  // narrow over compressed codes (NarrowView::comp)
+    uint64_t nc0 = 0;
+    DBuf d_ncmeta;       // its per-limb masks, patterns, compress moves
     DBuf d_nkeys, d_nmaxs, d_nbase;
     NarrowView nv{};
     // the narrow window as one-word tile rows (codes) for the tile pipeline
@@ -597,6 +600,11 @@ struct hsc_ctx {
     uint64_t small_app_seq[kSmallSlots] = {};
     uint64_t app_seq = 0;  // appends whose device work app_last follows
     Stage small_st;  // marshal target of the small path (coh: its arena swaps into a slot)
+    // collector batches assembled from premarshalled rows before the context
+    // lock (check_batch_assembled): a stage per batch in flight
+    std::mutex pre_mu;
+    std::vector<std::unique_ptr<Stage>> pre_stages;
+    std::vector<Stage *> pre_free;
     DBuf small_blocks;
     bool small_blocks_zeroed = false;
     bool no_small = false;  // hsc_set_paths(HSC_PATH_NO_SMALL): the staged path

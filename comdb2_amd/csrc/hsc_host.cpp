@@ -162,6 +162,15 @@ static int fail(hsc_ctx *c, int code, const char *what, hipError_t e)
         if (e_ != hipSuccess) return fail((c), HSC_EDEVICE, #call, e_); \
     } while (0)
 
+// the bits of x under mask m, packed to the low end (MSB order kept)
+static uint64_t host_compress(uint64_t x, uint64_t m)
+{
+    uint64_t r = 0;
+    for (int b = 63; b >= 0; --b)
+        if ((m >> b) & 1) r = (r << 1) | ((x >> b) & 1);
+    return r;
+}
+
 static int table_id_or_add(hsc_ctx *c, const char *name)
 {
     auto it = c->table_ids.find(name);
@@ -744,6 +753,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
     c->n_all = n_in;  // every version, key-sorted, stays in d_gid2 / d_words2 / d_lsn2
     // narrow layout if the whole window fits 62-bit codes (hsc_narrow.hip)
     c->narrow = false;
+    c->ncomp = false;
     c->lw = W;
     c->tz = 63;
     if (c->layout != HSC_LAYOUT_WIDE && c->n > 0) {
@@ -758,6 +768,27 @@ static int device_build(hsc_ctx *c, size_t n_in)
             }
         }
         c->narrow = narrow_span_fits(W, c->lw, c->tz, ends.data(), ends.data() + W + 1);
+        // composite keys whose varying bits sit far apart but total <= 62:
+        // the narrow index over compressed codes (hsc_narrow.hip cnarrow_bound)
+        int vb = 0;
+        for (int l = 0; l <= W; ++l) vb += __builtin_popcountll(l ? vary[l - 1] : vary[W]);
+        c->ncomp = !c->narrow && vb <= 62 && !(c->paths & HSC_PATH_NO_COMP_NARROW);
+        if (c->ncomp) {
+            std::vector<uint64_t> cm(8 * (size_t)(W + 1), 0);
+            uint64_t c0 = 0;
+            for (int l = 0; l <= W; ++l) {
+                const uint64_t m = l ? vary[l - 1] : vary[W], r0 = ends[l];  // ends[0] = gid, ends[1 + j] = word j
+                cm[8 * l] = m;
+                cm[8 * l + 1] = r0;
+                compress_moves(m, &cm[8 * l + 2]);
+                const int cnt = __builtin_popcountll(m);
+                if (cnt) c0 = (cnt >= 64 ? 0 : c0 << cnt) | host_compress(r0, m);
+            }
+            c->nc0 = c0;
+            HIPCHK(c, c->d_ncmeta.ensure(8 * cm.size()));
+            HIPCHK(c, hipMemcpyAsync(c->d_ncmeta.p, cm.data(), 8 * cm.size(), hipMemcpyHostToDevice, s));
+            c->narrow = true;
+        }
     }
     c->log2T = tile_log2(W);
     c->ntiles = (uint32_t)((c->n + ((size_t)1 << c->log2T) - 1) >> c->log2T);
@@ -837,6 +868,9 @@ static int device_build(hsc_ctx *c, size_t n_in)
         nv.W = W;
         nv.lw = c->lw;
         nv.tz = c->tz;
+        nv.comp = c->ncomp ? 1 : 0;
+        nv.cmeta = c->d_ncmeta.as<uint64_t>();
+        nv.c0 = c->nc0;
         nv.n = (uint32_t)c->n;
         HIPCHK(c, narrow_build(w, nv, s));
         bt.stamp("narrow");
@@ -1255,6 +1289,7 @@ static void swap_window(hsc_ctx *a, hsc_ctx *b)
     swap(a->ng_built, b->ng_built);
     swap(a->ntiles, b->ntiles), swap(a->log2T, b->log2T), swap(a->levels, b->levels);
     swap(a->narrow, b->narrow), swap(a->lw, b->lw), swap(a->tz, b->tz);
+    swap(a->ncomp, b->ncomp), swap(a->nc0, b->nc0), swap(a->d_ncmeta, b->d_ncmeta);
     swap(a->d_nkeys, b->d_nkeys), swap(a->d_nmaxs, b->d_nmaxs), swap(a->d_nbase, b->d_nbase);
     swap(a->nv, b->nv), swap(a->wn, b->wn);
     swap(a->d_nzero, b->d_nzero), swap(a->d_ntmax, b->d_ntmax), swap(a->d_nsp_g, b->d_nsp_g);
@@ -3044,6 +3079,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
     for (DBuf *b : bufs) b->release();
     for (Stage &st : c->stage) st.release();
     c->small_st.release();
+    for (auto &ps : c->pre_stages) ps->release();
     for (auto &sl : c->small) sl.io.release();
     c->small_blocks.release();
     for (DBuf *b : {&c->d_csrep, &c->d_csmask, &c->d_cspat, &c->d_csmv, &c->d_csbits, &c->d_cskeys[0],
@@ -3826,10 +3862,145 @@ int check_batch_pre(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, uns
 
 extern "C" {
 
+// A collector batch whose read sets were all premarshalled against the
+// current dictionary snapshot: its columns are assembled into a stage of the
+// context's pool BEFORE the context lock (the rows live in the callers'
+// caches: copying them under the lock made every other leader wait), and
+// the lock covers the window rules, the slot and the launch.  Rows of read
+// sets the window rules decide are kept: a snapshot at or past the end of
+// the log (rule 0) sees no write after it, so they cannot conflict; a forced
+// conflict ORs in.  -> true when the batch was handled (rc set).
+static bool check_batch_assembled(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, unsigned int *file,
+                                  unsigned int *offset, int n, int *rc_out, int *rc)
+{
+    const MarshalDict *d = c->dict_cur.load(std::memory_order_acquire);
+    if (!d || n > kSmallMaxTxns || c->multi || c->host_only) return false;
+    size_t nr = 0, nl = 0;
+    for (int i = 0; i < n; ++i) {
+        if (!ranges[i] || !pre[i] || pre[i]->epoch != d->epoch) return false;
+        nr += pre[i]->mp.gid.size();
+        nl += pre[i]->mp.lock_table.size();
+    }
+    if (nr > kSmallMaxRanges || nl > kSmallMaxRanges) return false;
+    Stage *st = nullptr;
+    {
+        std::lock_guard<std::mutex> g(c->pre_mu);
+        if (c->pre_free.empty()) {
+            c->pre_stages.emplace_back(new (std::nothrow) Stage());
+            if (!c->pre_stages.back()) {
+                c->pre_stages.pop_back();
+                return false;
+            }
+            c->pre_free.push_back(c->pre_stages.back().get());
+        }
+        st = c->pre_free.back();
+        c->pre_free.pop_back();
+    }
+    auto give_back = [&] {
+        std::lock_guard<std::mutex> g(c->pre_mu);
+        c->pre_free.push_back(st);
+    };
+    const int W = d->W;
+    st->coh = true;
+    st->L = stage_layout(W, nr, nl);
+    if (st->arena.ensure(std::max<size_t>(st->L.total + small_tail((size_t)n), 256), true, true) ||
+        st->forced.ensure((size_t)std::max(n, 1), true)) {
+        give_back();
+        return false;
+    }
+    uint64_t *lo = st->col<uint64_t>(st->L.lo), *hi = st->col<uint64_t>(st->L.hi);
+    uint64_t *sn = st->col<uint64_t>(st->L.snap), *lsnap = st->col<uint64_t>(st->L.lock_snap);
+    uint32_t *gid = st->col<uint32_t>(st->L.gid), *txn = st->col<uint32_t>(st->L.txn);
+    uint32_t *ltab = st->col<uint32_t>(st->L.lock_table), *ltxn = st->col<uint32_t>(st->L.lock_txn);
+    size_t o = 0, ol = 0;
+    for (int i = 0; i < n; ++i) {
+        const MarshalPart &q = pre[i]->mp;
+        const size_t k = q.gid.size();
+        for (size_t r = 0; r < k; ++r)
+            for (int j = 0; j < W; ++j) {
+                lo[(size_t)j * nr + o + r] = q.lohi[r * 2 * W + j];
+                hi[(size_t)j * nr + o + r] = q.lohi[r * 2 * W + W + j];
+            }
+        if (k) {
+            memcpy(gid + o, q.gid.data(), 4 * k);
+            memcpy(sn + o, q.snap.data(), 8 * k);
+            for (size_t r = 0; r < k; ++r) txn[o + r] = (uint32_t)i;
+        }
+        const size_t kl = q.lock_table.size();
+        if (kl) {
+            memcpy(ltab + ol, q.lock_table.data(), 4 * kl);
+            memcpy(lsnap + ol, q.lock_snap.data(), 8 * kl);
+            for (size_t r = 0; r < kl; ++r) ltxn[ol + r] = (uint32_t)i;
+        }
+        o += k, ol += kl;
+    }
+    st->n = nr, st->n_lock = nl, st->n_txn = (size_t)n;
+    const auto tl0 = SteadyClock::now();
+    std::unique_lock<std::mutex> lk(c->mu);
+    c->sm_lock_ns.fetch_add(ns_since(tl0), std::memory_order_relaxed);
+    (void)hipSetDevice(c->device);
+    int r = ensure_built(c);
+    // the snapshot the rows were marshalled against must still be the
+    // dictionaries (a new group or a wider key since: the usual path)
+    if (r != HSC_OK || c->dict_epoch != d->epoch || c->W != W || !small_path(c, n)) {
+        lk.unlock();
+        give_back();
+        if (r == HSC_OK) return false;
+        for (int i = 0; i < n; ++i) rc_out[i] = 1;
+        *rc = r;
+        return true;
+    }
+    publish_dict(c);
+    const unsigned int ef = (unsigned int)(c->end_lsn >> 32), eo = (unsigned int)c->end_lsn;
+    uint8_t *forced = st->forced.as<uint8_t>();
+    for (int i = 0; i < n; ++i) {
+        hsc_currangearr *a = (hsc_currangearr *)ranges[i];
+        unsigned int *pf = file ? &file[i] : &a->file;
+        unsigned int *po = offset ? &offset[i] : &a->offset;
+        const uint64_t S = ((uint64_t)*pf << 32) | *po;
+        *pf = ef, *po = eo;  // full mode: *file,*offset := curlsn
+        forced[i] = full_forced(c, S) > 0;
+    }
+    const int k = small_launch(c, *st);
+    if (k < 0) {
+        lk.unlock();
+        give_back();
+        for (int i = 0; i < n; ++i) rc_out[i] = 1;
+        *rc = k;
+        return true;
+    }
+    c->sm_calls.fetch_add(1, std::memory_order_relaxed);
+    hipStream_t s = c->small[k].stream;
+    lk.unlock();
+    give_back();  // the slot owns the columns now (its arena swapped in)
+    if (const hipError_t e = small_fire(c, k); e != hipSuccess) {
+        c->small[k].busy.store(false, std::memory_order_release);
+        std::lock_guard<std::mutex> g(c->mu);
+        for (int i = 0; i < n; ++i) rc_out[i] = 1;
+        *rc = fail(c, HSC_EDEVICE, "small batch launch", e);
+        return true;
+    }
+    const char *why = nullptr;
+    hipError_t herr = hipSuccess;
+    r = small_wait(c, k, s, rc_out, &why, &herr);
+    if (r != HSC_OK) {
+        std::lock_guard<std::mutex> g(c->mu);
+        for (int i = 0; i < n; ++i) rc_out[i] = 1;
+        *rc = fail(c, r, why, herr);
+        return true;
+    }
+    *rc = HSC_OK;
+    return true;
+}
+
 static int check_batch(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, unsigned int *file,
                        unsigned int *offset, int regop_only, int n, int *rc_out)
 {
     if (!c || n < 0 || (n && (!ranges || !rc_out)) || (!file) != (!offset)) return HSC_EINVAL;
+    if (pre && !regop_only && n > 0) {
+        int rc = HSC_OK;
+        if (check_batch_assembled(c, ranges, pre, file, offset, n, rc_out, &rc)) return rc;
+    }
     const auto tl0 = SteadyClock::now();
     std::unique_lock<std::mutex> lk(c->mu);  // a small batch drops it while its kernel runs
     c->sm_lock_ns.fetch_add(ns_since(tl0), std::memory_order_relaxed);

@@ -235,6 +235,13 @@ struct NarrowView {
     uint32_t n;
     const uint64_t *table_max;
     uint32_t ntables;
+    // compressed codes (comp != 0): the rows' varying bits of every limb
+    // (gid, words) packed MSB first, minus row 0's -- for windows whose rows
+    // differ in <= 62 bits spread beyond one 62-bit span (composite keys).
+    // cmeta[8 l ..]: limb l's mask, pattern (row 0), 6 compress moves.
+    int comp;
+    const uint64_t *cmeta;
+    uint64_t c0;               // compress(row 0)
 };
 bool narrow_span_fits(int W, int lw, int tz, const uint64_t *first, const uint64_t *last);
 hipError_t narrow_end_rows(const WinView &w, const uint32_t *n_dev, uint64_t *out, hipStream_t s);

@@ -113,6 +113,81 @@ __device__ __forceinline__ bool rel_diff_w(int lw, int tz, uint64_t xg, const ui
     return true;
 }
 
+// Compressed codes (nv.comp): code(X) = compress(X over the rows' varying
+// bits) - c0.  Rows map exactly; a bound X that leaves the rows' constant
+// pattern maps by its first differing constant bit b (MSB first): with the
+// varying bits above b as prefix, X is above every row of that prefix when
+// its bit is 1 (#rows < X = #codes < (prefix + 1) << rest) and below them
+// when 0 (#codes < prefix << rest) -- the compact codes' rule
+// (hsc_compact_dev.h bound_word) on one word.  upper = false: the lower code
+// (ceil: #codes < it = #rows < X), else the upper (floor: #codes <= it =
+// #rows <= X); false = no row <= X (upper only).
+__device__ __forceinline__ bool cnarrow_bound(const NarrowView &nv, uint64_t xg, const uint64_t *xw,
+                                              size_t xs, bool upper, uint64_t &code)
+{
+    uint64_t acc = 0;
+    int pos = 0, np = -1, xb = 0;
+    for (int l = 0; l <= nv.W; ++l) {
+        const uint64_t *cm = nv.cmeta + 8 * l;
+        const uint64_t m = cm[0], pt = cm[1];
+        uint64_t x = l ? xw[(size_t)(l - 1) * xs] : xg;
+        if (np < 0) {
+            const uint64_t d = (x ^ pt) & ~m;
+            if (d) {
+                const int b = 63 - __clzll(d);
+                const uint64_t above = b == 63 ? 0 : ~0ull << (b + 1);
+                np = pos + __popcll(m & above);
+                xb = (int)((x >> b) & 1);
+                x &= above;
+            }
+        } else {
+            x = 0;
+        }
+        const int c = __popcll(m);
+        if (c) {
+            uint64_t mv[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) mv[q] = cm[2 + q];
+            acc = (c >= 64 ? 0 : acc << c) | bits_compress(x, m, mv);
+            pos += c;
+        }
+    }
+    uint64_t lo, hi;
+    bool live = true;
+    if (np < 0) {
+        lo = hi = acc;
+    } else {
+        const int low = pos - np;
+        const uint64_t pre = low >= 64 ? 0 : acc >> low;
+        lo = (xb ? pre + 1 : pre) << low;
+        live = lo != 0;
+        hi = lo - 1;
+    }
+    if (upper) {
+        if (!live || hi < nv.c0) return false;
+        code = hi - nv.c0 < kSat ? hi - nv.c0 : kSat;
+        return true;
+    }
+    code = lo <= nv.c0 ? 0 : (lo - nv.c0 < kSat ? lo - nv.c0 : kSat);
+    return true;
+}
+
+// A probe bound as a code, either form: lower (ceil) / upper (floor); false
+// (upper only) = no row at or below X.  Generic width (rel_diff).
+__device__ __forceinline__ bool narrow_bound(const NarrowView &nv, uint64_t xg, const uint64_t *xw,
+                                             size_t xs, bool upper, uint64_t &code)
+{
+    if (nv.comp) return cnarrow_bound(nv, xg, xw, xs, upper, code);
+    uint64_t v;
+    bool rem;
+    if (!rel_diff(nv.W, nv.lw, nv.tz, xg, xw, xs, nv.base[0], nv.base + 1, 1, kSat, v, rem)) {
+        code = 0;
+        return !upper;  // below the window: lower 0, upper none
+    }
+    code = upper ? v : (v >= kSat ? kSat : v + (rem ? 1 : 0));
+    return true;
+}
+
 bool narrow_span_fits(int W, int lw, int tz, const uint64_t *first, const uint64_t *last)
 {
     uint64_t v;
@@ -145,15 +220,18 @@ hipError_t narrow_end_rows(const WinView &w, const uint32_t *n_dev, uint64_t *ou
 }
 
 // level 0: key64 of every row (padding above n), lsn (padding 0)
-__global__ void k_level0(WinView w, const uint64_t *base, int lw, int tz, uint32_t len,
-                         uint64_t *key0, uint64_t *max0)
+__global__ void k_level0(WinView w, NarrowView nv, uint32_t len, uint64_t *key0, uint64_t *max0)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= len) return;
     uint64_t v = kKeyPad, m = 0;
     if (i < w.n) {
         bool rem;
-        rel_diff(w.W, lw, tz, w.gid[i], w.words + i, w.stride, base[0], base + 1, 1, kSat, v, rem);
+        if (nv.comp)
+            cnarrow_bound(nv, w.gid[i], w.words + i, w.stride, false, v);
+        else
+            rel_diff(w.W, nv.lw, nv.tz, w.gid[i], w.words + i, w.stride, nv.base[0], nv.base + 1, 1, kSat,
+                     v, rem);
         m = w.lsn[i];
     }
     key0[i] = v;
@@ -184,8 +262,7 @@ __global__ void k_level_up(const uint64_t *key_src, const uint64_t *max_src, uin
 hipError_t narrow_build(const WinView &w, const NarrowView &nv, hipStream_t s)
 {
     const uint32_t len0 = nv.len[0];
-    k_level0<<<(len0 + 255) / 256, 256, 0, s>>>(w, nv.base, nv.lw, nv.tz, len0,
-                                                 (uint64_t *)nv.keys, (uint64_t *)nv.maxs);
+    k_level0<<<(len0 + 255) / 256, 256, 0, s>>>(w, nv, len0, (uint64_t *)nv.keys, (uint64_t *)nv.maxs);
     for (int l = 1; l < nv.levels; ++l)
         k_level_up<<<(nv.len[l] + 255) / 256, 256, 0, s>>>(
             nv.keys + nv.off[l - 1], nv.maxs + nv.off[l - 1], nv.len[l - 1],
@@ -236,17 +313,11 @@ __device__ __forceinline__ void narrow_probe_ranges(const NarrowView &nv, const 
                 const uint32_t g = p.gid[q];
                 msnap = p.snap[q];
                 mtxn = p.txn[q];
-                uint64_t v;
-                bool rem;
-                // lower bound: ceil((lo - K0) >> s), 0 below the window
-                mlo = rel_diff(nv.W, nv.lw, nv.tz, g, p.lo + q, ks, nv.base[0], nv.base + 1, 1,
-                               kSat, v, rem)
-                          ? (v >= kSat ? kSat : v + (rem ? 1 : 0))
-                          : 0;
-                // upper bound: floor((hi - K0) >> s); none below the window
-                mlive = rel_diff(nv.W, nv.lw, nv.tz, g, p.hi + q, ks, nv.base[0], nv.base + 1, 1,
-                                 kSat, v, rem);
-                mhi = mlive ? v : 0;
+                // lower bound: ceil((lo - K0) >> s), 0 below the window;
+                // upper bound: floor((hi - K0) >> s), none below the window
+                narrow_bound(nv, g, p.lo + q, ks, false, mlo);
+                mlive = narrow_bound(nv, g, p.hi + q, ks, true, mhi);
+                if (!mlive) mhi = 0;
             }
         }
         uint64_t x[2 * kNP], snap[kNP];
@@ -430,22 +501,27 @@ __device__ __forceinline__ void narrow_small_ranges(const NarrowView &nv, const 
         uint32_t tx = 0;
         int ok = 0;
         if (act && l16 < 2) {
-            uint64_t v;
-            bool rem;
+            uint64_t v = 0;
+            bool rem = false;
             const uint64_t *xp = l16 ? p.hi + q : p.lo + q;
-            if constexpr (KW > 0) {
-                const uint32_t g = p.gid[q];
-                uint64_t xw[KW];
-#pragma unroll
-                for (int j = 0; j < KW; ++j) xw[j] = xp[(size_t)j * ks];
-                ok = rel_diff_w<KW>(nv.lw, nv.tz, g, xw, nv.base[0], nv.base + 1, kSat, v, rem);
+            if (nv.comp) {  // compressed codes: the bound's code either way
+                ok = narrow_bound(nv, p.gid[q], xp, ks, l16 != 0, v);
+                xv = ok ? v : 0;
             } else {
-                ok = rel_diff(nv.W, nv.lw, nv.tz, p.gid[q], xp, ks, nv.base[0], nv.base + 1, 1, kSat, v,
-                              rem);
+                if constexpr (KW > 0) {
+                    const uint32_t g = p.gid[q];
+                    uint64_t xw[KW];
+#pragma unroll
+                    for (int j = 0; j < KW; ++j) xw[j] = xp[(size_t)j * ks];
+                    ok = rel_diff_w<KW>(nv.lw, nv.tz, g, xw, nv.base[0], nv.base + 1, kSat, v, rem);
+                } else {
+                    ok = rel_diff(nv.W, nv.lw, nv.tz, p.gid[q], xp, ks, nv.base[0], nv.base + 1, 1, kSat,
+                                  v, rem);
+                }
+                // lower bound: ceil((lo - K0) >> s), 0 below the window; upper:
+                // floor((hi - K0) >> s), none below the window
+                xv = !ok ? 0 : l16 ? v : (v >= kSat ? kSat : v + (rem ? 1 : 0));
             }
-            // lower bound: ceil((lo - K0) >> s), 0 below the window; upper:
-            // floor((hi - K0) >> s), none below the window
-            xv = !ok ? 0 : l16 ? v : (v >= kSat ? kSat : v + (rem ? 1 : 0));
         } else if (act && l16 == 2) {
             sn = p.snap[q];
             tx = p.txn[q];
@@ -787,14 +863,9 @@ __global__ void k_codes(NarrowView nv, ProbeView p, uint64_t *lo64, uint64_t *hi
     const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= p.n) return;
     const uint32_t g = p.gid[q];
-    uint64_t v;
-    bool rem;
-    const uint64_t lo = rel_diff(nv.W, nv.lw, nv.tz, g, p.lo + q, p.n, nv.base[0], nv.base + 1, 1,
-                                 kSat, v, rem)
-                            ? (v >= kSat ? kSat : v + (rem ? 1 : 0))
-                            : 0;
-    const bool live = rel_diff(nv.W, nv.lw, nv.tz, g, p.hi + q, p.n, nv.base[0], nv.base + 1, 1,
-                               kSat, v, rem);
+    uint64_t lo = 0, v = 0;
+    narrow_bound(nv, g, p.lo + q, p.n, false, lo);
+    const bool live = narrow_bound(nv, g, p.hi + q, p.n, true, v);
     lo64[q] = live ? lo : kSat;
     hi64[q] = live ? v : 0;
 }
@@ -1068,11 +1139,14 @@ __device__ __forceinline__ void locate_codes(const NarrowView &nv, const ProbeVi
                                              const uint64_t (&xh)[2 > W ? 2 : W], uint64_t &lo,
                                              uint64_t &hi)
 {
-    uint64_t v;
+    uint64_t v = 0;
     bool rem;
-    uint64_t a;
+    uint64_t a = 0;
     bool live;
-    if constexpr (W > 0) {
+    if (nv.comp) {  // compressed codes (the loaded words live at p.lo / p.hi + q too)
+        narrow_bound(nv, g, p.lo + q, p.n, false, a);
+        live = narrow_bound(nv, g, p.hi + q, p.n, true, v);
+    } else if constexpr (W > 0) {
         const uint64_t(&wl)[W] = *(const uint64_t(*)[W])xl;
         const uint64_t(&wh)[W] = *(const uint64_t(*)[W])xh;
         a = rel_diff_w<W>(nv.lw, nv.tz, g, wl, nv.base[0], nv.base + 1, kSat, v, rem)

@@ -312,13 +312,17 @@ int hsc_append_stats(hsc_ctx *ctx, uint64_t out[3]);
  * the whole-row radix sort; TILE_DIR: narrow / compact tile locates search
  * the 16-ary directory instead of the bucket table (set before the build);
  * CO_SERIAL: every coalesced read set takes the per-thread msort replay;
- * CO_RUN_THREAD: one thread per run in the coalesce merge scan. */
+ * CO_RUN_THREAD: one thread per run in the coalesce merge scan;
+ * NO_COMP_NARROW: composite keys whose varying bits total <= 62 but span
+ * more keep the compact / wide layouts instead of the narrow index over
+ * compressed codes (set before the build). */
 #define HSC_PATH_NO_SMALL 1u
 #define HSC_PATH_NO_PACKED_SORT 2u
 #define HSC_PATH_TILE_DIR 4u
 #define HSC_PATH_CO_SERIAL 8u
 #define HSC_PATH_CO_RUN_THREAD 16u
-#define HSC_PATH_ALL 31u
+#define HSC_PATH_NO_COMP_NARROW 32u
+#define HSC_PATH_ALL 63u
 int hsc_set_paths(hsc_ctx *ctx, unsigned flags);
 /* How the last window build sorted its rows: 0 whole-row radix sort, 1 the
  * packed 64-bit key sort, 2 the compact-code merge sort (wide keys). */

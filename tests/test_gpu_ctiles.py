@@ -12,7 +12,8 @@ import pytest
 
 from comdb2_amd import formats as F
 from comdb2_amd.formats import LogBuilder, Range, ReadSets
-from comdb2_amd.hsc import LAYOUT_AUTO, LAYOUT_COMPACT, LAYOUT_COMPACT_WIDE, Validator
+from comdb2_amd.hsc import (LAYOUT_AUTO, LAYOUT_COMPACT, LAYOUT_COMPACT_WIDE, LAYOUT_NARROW,
+                            PATH_NO_COMP_NARROW, Validator)
 
 pytestmark = pytest.mark.gpu
 # torch (device arrays for hsc_window_ingest_device) is imported before any
@@ -207,6 +208,12 @@ def test_one_word_keys_match_oracle(oracle_mod):
     want = oracle_mod.check(log, rs, nthreads=8)[0] != 0
     v = Validator(0)
     try:
+        # (by default such a window takes the narrow index over compressed
+        # codes: its varying bits total <= 62 -- checked there too)
+        v.ingest_log(log)
+        assert v.layout == LAYOUT_NARROW
+        np.testing.assert_array_equal(v.check_readsets(rs) != 0, want)
+        v.set_paths(PATH_NO_COMP_NARROW)
         got, ref = _both(v, log, rs)
         assert v.tile_key_words == 1
     finally:

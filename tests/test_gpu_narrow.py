@@ -14,7 +14,7 @@ import pytest
 
 from comdb2_amd import formats as F
 from comdb2_amd.formats import LogBuilder, Range, ReadSets
-from comdb2_amd.hsc import (PATH_TILE_DIR, LAYOUT_AUTO, LAYOUT_NARROW, LAYOUT_NARROW_CODES,
+from comdb2_amd.hsc import (PATH_NO_COMP_NARROW, PATH_TILE_DIR, LAYOUT_AUTO, LAYOUT_NARROW, LAYOUT_NARROW_CODES,
                             LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES, LAYOUT_WIDE)
 from comdb2_amd.workloads import config2, config5
 
@@ -123,6 +123,45 @@ def test_three_word_keys_prefix_ranges(validator, oracle_mod):
         return Range("t1", 0, lo, hi)
     log, rs = keyed_case(12, 4000, 5, key, rng_range, 800)
     both_layouts(validator, oracle_mod, log, rs, LAYOUT_NARROW)
+
+
+@pytest.mark.parametrize("ids,accts", [(20, 5), (3000, 300), (1 << 20, 7)])
+def test_composite_keys_compressed_codes(validator, oracle_mod, ids, accts):
+    """Two-field keys enc(id) || enc(acct) (the config-1 / serial.c index):
+    their varying bits sit ~64 bits apart, too far for one 62-bit span, but
+    total <= 62, so the narrow index runs over compressed codes (NarrowView
+    comp).  Bounds leave the rows' constant pattern anywhere: ids and accts
+    past the written ones, negative values, 9-byte id prefixes and cut keys,
+    open ends -- every narrow path (small kernel, direct, tiles, codes) vs
+    the oracle, and the compact / wide layouts with the mode off."""
+    key = lambda rng: F.enc_int64(int(rng.integers(0, ids))) + F.enc_int64(int(rng.integers(0, accts)))
+
+    def rng_range(rng):
+        i = int(rng.integers(-2, ids + 2))
+        a = int(rng.integers(-2, accts + 2))
+        u = rng.random()
+        if u < 0.3:  # the point read of one account
+            k = F.enc_int64(i) + F.enc_int64(a)
+            return Range("t1", 0, k, k)
+        if u < 0.5:  # sum(bal) where id = ?: a 9-byte prefix range
+            return Range("t1", 0, F.enc_int64(i), F.enc_int64(i))
+        if u < 0.6:
+            return Range("t1", 0, None, F.enc_int64(i) + F.enc_int64(a), 1, 0)
+        if u < 0.7:
+            return Range("t1", 0, F.enc_int64(i) + F.enc_int64(a), None, 0, 1)
+        lo = F.enc_int64(i) + F.enc_int64(a)
+        hi = F.enc_int64(i + int(rng.integers(0, 3))) + F.enc_int64(int(rng.integers(-1, accts + 1)))
+        return Range("t1", 0, lo[: int(rng.integers(1, 19))], hi[: int(rng.integers(1, 19))])
+    log, rs = keyed_case(21 + ids, 3000, 3, key, rng_range, 700)
+    want = both_layouts(validator, oracle_mod, log, rs, LAYOUT_NARROW)
+    assert int((want != 0).sum()) > 0
+    validator.set_paths(PATH_NO_COMP_NARROW)
+    try:
+        validator.ingest_log(log)
+        assert validator.layout != LAYOUT_NARROW
+        np.testing.assert_array_equal(validator.check_readsets(rs) != 0, want != 0)
+    finally:
+        validator.set_paths(0)
 
 
 def test_low_bits_vary_tz0(validator, oracle_mod):
