@@ -543,9 +543,17 @@ def api_leg(hsc, v, rs, device_verdict, args):
     # share of the read sets; the collector batches whatever arrives together
     conc = {}
     want = np.asarray(device_verdict) != 0
+    v.concurrent_check(arrs, 64)  # warm-up: the callers' threads, slots and staging
     for nth in (64, 256):
-        got, st = v.concurrent_check(arrs, nth)
-        st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want))
+        runs = []
+        for _ in range(3):  # the median run of three (run-to-run spread ~5 %)
+            got, st = v.concurrent_check(arrs, nth)
+            st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want))
+            runs.append(st)
+        runs.sort(key=lambda x: x["checks_per_s"])
+        st = dict(runs[1])
+        st["runs_checks_per_s"] = [r["checks_per_s"] for r in runs]
+        st["parity_with_device_batch"] = all(r["parity_with_device_batch"] for r in runs)
         conc[f"threads_{nth}"] = st
     # one batch on the device at a time (the collector before round 3)
     got, st = v.concurrent_check(arrs, 64, inflight=1)
@@ -1024,6 +1032,7 @@ def multi_api_leg(hsc, v, rs, want):
     arrs = hsc.NativeCurRangeArrs(rs)
     want = np.asarray(want) != 0
     conc = {}
+    v.concurrent_check(arrs, 64)  # warm-up
     r0 = v.route_stats()
     got, st = v.concurrent_check(arrs, 64)
     st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want))

@@ -1337,8 +1337,9 @@ static DeltaView frozen_view(const hsc_ctx *c)
 // kernels never sit in front of a check's in a hardware queue.
 static hipError_t create_stream(hipStream_t *st, bool high)
 {
+    static const bool prio = getenv("HSC_NO_STREAM_PRIO") == nullptr;  // (A/B diagnostics)
     int least = 0, greatest = 0;
-    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest)
+    if (!prio || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest)
         return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
     return hipStreamCreateWithPriority(st, hipStreamNonBlocking, high ? greatest : least);
 }
@@ -3997,7 +3998,8 @@ static int check_batch(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, 
                        unsigned int *offset, int regop_only, int n, int *rc_out)
 {
     if (!c || n < 0 || (n && (!ranges || !rc_out)) || (!file) != (!offset)) return HSC_EINVAL;
-    if (pre && !regop_only && n > 0) {
+    static const bool assemble = getenv("HSC_NO_PRE_ASSEMBLE") == nullptr;  // (A/B diagnostics)
+    if (assemble && pre && !regop_only && n > 0) {
         int rc = HSC_OK;
         if (check_batch_assembled(c, ranges, pre, file, offset, n, rc_out, &rc)) return rc;
     }
