@@ -555,6 +555,14 @@ def api_leg(hsc, v, rs, device_verdict, args):
         st["runs_checks_per_s"] = [r["checks_per_s"] for r in runs]
         st["parity_with_device_batch"] = all(r["parity_with_device_batch"] for r in runs)
         conc[f"threads_{nth}"] = st
+    # passes in flight other than the default 4 (one run each)
+    sweep = {}
+    for inf in (2, 6, 8):
+        got, s2 = v.concurrent_check(arrs, 64, inflight=inf)
+        sweep[str(inf)] = {"checks_per_s": s2["checks_per_s"], "lat_p50_us": s2["lat_p50_us"],
+                           "lat_p99_us": s2["lat_p99_us"], "mean_batch": s2.get("mean_batch"),
+                           "parity_with_device_batch": bool(np.array_equal(got != 0, want))}
+    conc["threads_64_inflight"] = sweep
     # one batch on the device at a time (the collector before round 3)
     got, st = v.concurrent_check(arrs, 64, inflight=1)
     st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want))
@@ -1037,6 +1045,15 @@ def multi_api_leg(hsc, v, rs, want):
     got, st = v.concurrent_check(arrs, 64)
     st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want))
     conc["threads_64"] = st
+    # collector passes in flight (default 4): each pass launches and waits on
+    # every member its ranges touch, so a multi pass is longer than a one-GPU one
+    sweep = {}
+    for inf in (6, 8):
+        got, s2 = v.concurrent_check(arrs, 64, inflight=inf)
+        sweep[str(inf)] = {"checks_per_s": s2["checks_per_s"], "lat_p50_us": s2["lat_p50_us"],
+                           "lat_p99_us": s2["lat_p99_us"], "mean_batch": s2.get("mean_batch"),
+                           "parity_with_device_batch": bool(np.array_equal(got != 0, want))}
+    conc["threads_64_inflight"] = sweep
     m = min(rs.ntxn, 2000)
     sub = hsc.NativeCurRangeArrs(_readsets_head(rs, m))
     for nth in (1, 64):

@@ -239,7 +239,7 @@ int hsc_collector_create(hsc_ctx *ctx, int max_batch, int max_wait_us, hsc_colle
 
 int hsc_collector_set_inflight(hsc_collector *k, int n)
 {
-    if (!k || n < 1 || n > 4) return HSC_EINVAL;
+    if (!k || n < 1 || n > 8) return HSC_EINVAL;
     k->max_inflight.store(n, std::memory_order_relaxed);
     k->gate.fetch_add(1, std::memory_order_seq_cst);
     futex_wake(&k->gate, INT_MAX);

@@ -225,6 +225,13 @@ __device__ __forceinline__ bool bound_codes(const CompactMeta &cm, const BoundIn
     const uint32_t bits = cm.bits[g];
 #pragma unroll
     for (int k = 0; k < WC; ++k) al[k] = ah[k] = 0;
+    // a wave of points (lo == hi in every lane: the marshal lays a length's
+    // points out together) maps one bound for both; lo and hi differ only in
+    // the adjustments after the loop
+    bool pt = true;
+#pragma unroll
+    for (int j = 0; j < kProbeWords; ++j) pt &= in.xl[j] == in.xh[j];
+    const bool wpt = __all(pt);
     bool ok = bits != kNoRows;
     if (ok) {
         const uint64_t *mk = cm.mask + (size_t)g * cm.gs, *pt = cm.pat + (size_t)g * cm.gs;
@@ -239,10 +246,14 @@ __device__ __forceinline__ bool bound_codes(const CompactMeta &cm, const BoundIn
 #pragma unroll
             for (int i = 0; i < 6; ++i) mv[i] = mvg[j * cm.vm + i * cm.vs];
             const int c = __popcll(m);
-            acc_push<WC>(al, bound_word(in.xl[j], m, pj, mv, pos, npl, xbl), c);
-            acc_push<WC>(ah, bound_word(in.xh[j], m, pj, mv, pos, nph, xbh), c);
+            const uint64_t vl = bound_word(in.xl[j], m, pj, mv, pos, npl, xbl);
+            acc_push<WC>(al, vl, c);
+            uint64_t vh = vl;
+            if (!wpt) vh = bound_word(in.xh[j], m, pj, mv, pos, nph, xbh);
+            acc_push<WC>(ah, vh, c);
             pos += c;
         }
+        if (wpt) nph = npl, xbh = xbl;
         acc_align<WC>(al, pos);
         acc_align<WC>(ah, pos);
         // lo: #rows < X = #codes < lo'

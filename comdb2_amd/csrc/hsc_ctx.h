@@ -522,6 +522,7 @@ struct hsc_ctx {
     hsc_marshalled m{};
     Stage stage[2];
     std::vector<MarshalPart> parts;
+    std::vector<std::vector<uint8_t>> parts_cls;  // per part: probe class (length, point) in marshal_into
     int threads = 1;
     std::unique_ptr<WorkPool> pool;  // `threads` workers (created by the first parallel marshal)
 
@@ -572,7 +573,7 @@ struct hsc_ctx {
     // its own block counter.  A slot belongs to one call from its launch
     // (under mu) until that call has read its verdicts (without mu), so a
     // second call can marshal and launch while the first one's kernel runs.
-    static constexpr int kSmallSlots = 4;
+    static constexpr int kSmallSlots = 8;
     struct SmallSlot {
         HBuf io;
         std::vector<uint8_t> forced;

@@ -2043,6 +2043,7 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
     const int per = std::max(1, std::min(kMarshalTxns, (nt + c->threads - 1) / std::max(1, c->threads)));
     const int nwork = std::max(1, (nt + per - 1) / per);
     if ((int)c->parts.size() < nwork) c->parts.resize(nwork);
+    if (c->parts_cls.size() < c->parts.size()) c->parts_cls.resize(c->parts.size());
     const bool pin = !c->host_only || c->multi;  // a multi context uploads from it
     if (st.forced.ensure((size_t)std::max(nt, 1), pin)) return fail(c, HSC_ENOMEM, "staging");
     uint8_t *forced = st.forced.as<uint8_t>();
@@ -2082,7 +2083,9 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
     uint64_t *lsnap = st.col<uint64_t>(st.L.lock_snap);
     // Groups of different key lengths (in words): each part's probes are laid
     // out grouped by that length (stable), so the compact bound kernel's waves
-    // skip the zero words past it together.  One length: read-set order.
+    // skip the zero words past it together, and inside a length the points (lo
+    // == hi) after the ranges, so its waves of points map one bound for both.
+    // One length: read-set order.
     std::vector<uint8_t> &gcls = c->gcls;  // per dictionary epoch (groups and W fixed by it)
     if (c->gcls_epoch != c->dict_epoch || gcls.size() != c->groups.size()) {
         gcls.resize(c->groups.size());
@@ -2101,11 +2104,18 @@ static int marshal_into(hsc_ctx *c, const Src &src, int t0, int t1, Stage &st)
         const MarshalPart &mp = c->parts[w];
         const size_t o = mp.out0, k = mp.gid.size();
         if (by_len) {
-            size_t cnt[kMaxWords + 2] = {0};
-            for (size_t i = 0; i < k; ++i) cnt[gcls[mp.gid[i]] + 1]++;
-            for (int q = 1; q <= ncls; ++q) cnt[q] += cnt[q - 1];
+            size_t cnt[2 * kMaxWords + 4] = {0};
+            std::vector<uint8_t> &cls = c->parts_cls[w];
+            cls.resize(k);
             for (size_t i = 0; i < k; ++i) {
-                const size_t d = o + cnt[gcls[mp.gid[i]]]++;
+                const uint64_t *r = &mp.lohi[i * 2 * W];
+                const int kc = gcls[mp.gid[i]];
+                cls[i] = (uint8_t)(2 * kc + (memcmp(r, r + W, 8 * (size_t)kc) == 0));
+                cnt[cls[i] + 1]++;
+            }
+            for (int q = 1; q <= 2 * ncls; ++q) cnt[q] += cnt[q - 1];
+            for (size_t i = 0; i < k; ++i) {
+                const size_t d = o + cnt[cls[i]]++;
                 for (int j = 0; j < W; ++j) {
                     lo[(size_t)j * n + d] = mp.lohi[i * 2 * W + j];
                     hi[(size_t)j * n + d] = mp.lohi[i * 2 * W + W + j];

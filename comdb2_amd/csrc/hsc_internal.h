@@ -710,6 +710,12 @@ hipError_t launch_route_scatter(const ProbeView &p, const RouteSplit &sp, const 
 hipError_t launch_route_unpack(const uint8_t *raw, const RouteUnpack &u, const RouteTarget &t, int W,
                                hipStream_t s);
 hipError_t launch_or_slices(const RouteParts &parts, size_t words, uint64_t *out, hipStream_t s);
+// verdict bytes (64 per output word, 8-byte aligned) of several members OR-ed into a bitmap
+struct RouteBytes {
+    const uint8_t *p[kMultiMax];
+    int n;
+};
+hipError_t launch_or_bytes(const RouteBytes &parts, size_t words, uint64_t *out, hipStream_t s);
 
 // per-file code-object warm-up (hsc_ctx_create)
 hipError_t warm_kernels();

@@ -456,8 +456,8 @@ static int lane_acquire(hsc_ctx *f, Multi *M, int L)
     for (int m = 0; m < M->nlocal; ++m) {
         MLane &ml = M->lane[L][m];
         MCHK(f, hipSetDevice(M->mem[m]->device));
-        for (int d = 0; d < M->nlocal; ++d)
-            if (M->lane[L][d].used) MCHK(f, hipStreamWaitEvent(ml.stream, M->lane[L][d].ev_done, 0));
+        for (int d = 0; d < M->nlocal; ++d)  // (its own stream is in order)
+            if (d != m && M->lane[L][d].used) MCHK(f, hipStreamWaitEvent(ml.stream, M->lane[L][d].ev_done, 0));
     }
     return HSC_OK;
 }
@@ -532,6 +532,7 @@ static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb,
     const size_t total = tb[N];
     auto ob = [&](int o) -> size_t { return tb[o] / 64; };
     auto ow = [&](int o) -> size_t { return (tb[o + 1] - tb[o]) / 64; };
+    const bool direct = !M->rccl && !M->loop;
     // 6. every member probes what it holds -- the members' launches issued
     // from one host thread each (a probe is several launches; eight GPUs'
     // worth from one thread would outlast the probes themselves)
@@ -545,6 +546,8 @@ static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb,
         b.verdict = ml.verdict.as<uint8_t>();
         if (N == 1) {  // one piece: its bitmap is the result
             b.bitmap = out[0];
+        } else if (direct) {  // in process: the owners OR the verdict bytes themselves
+            b.bitmap = nullptr;
         } else {
             MCHK(c, ml.bitmap.ensure(std::max<size_t>(total / 8, 8)));
             b.bitmap = ml.bitmap.as<uint64_t>();
@@ -564,11 +567,16 @@ static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb,
         c->stream = keep;
         if (rc) return rc;
         if (ml.timed) MCHK(c, hipEventRecord(ml.ev_t1, ml.stream));
+        // (not the context's own lane event: a concurrent caller of the member
+        // may take that lane and record it again before the merges wait)
         MCHK(c, hipEventRecord(ml.ev_probe, ml.stream));
         return HSC_OK;
     };
     int prc[kMultiMax] = {};
-    if (M->ndev > 1)  // (members sharing a GPU: one thread -- its launches serialise anyway)
+    // (members sharing a GPU: one thread -- its launches serialise anyway;
+    // HSC_MULTI_PAR_LAUNCH=1 issues them from the pool there too, an A/B)
+    static const bool par_env = getenv("HSC_MULTI_PAR_LAUNCH") != nullptr;
+    if (M->ndev > 1 || (par_env && NL > 1))
         ctx_par_for(f, NL, [&](int m) { prc[m] = probe_one(m); });
     else
         for (int m = 0; m < NL; ++m) prc[m] = probe_one(m);
@@ -633,21 +641,23 @@ static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb,
             MLane &ml = M->lane[L][o];
             MCHK(f, hipSetDevice(M->mem[o]->device));
             if (ow(o) && out[o]) {
-                RouteParts parts{};
+                RouteBytes parts{};
                 parts.n = NL;
                 for (int d = 0; d < NL; ++d) {
                     if (d != o) MCHK(f, hipStreamWaitEvent(ml.stream, M->lane[L][d].ev_probe, 0));
-                    parts.p[d] = M->lane[L][d].bitmap.as<uint64_t>() + ob(o);
+                    parts.p[d] = M->lane[L][d].verdict.as<uint8_t>() + tb[o];
                 }
-                MCHK(f, launch_or_slices(parts, ow(o), out[o], ml.stream));
+                MCHK(f, launch_or_bytes(parts, ow(o), out[o], ml.stream));
             }
         }
     }
     // a lane is done once every member's probe and every merge reading it ran
+    // (an owner whose merge read every member has waited for them already)
     for (int o = 0; o < NL; ++o) {
         MLane &ml = M->lane[L][o];
         MCHK(f, hipSetDevice(M->mem[o]->device));
-        if (!M->rccl)
+        const bool merged = (M->loop || (!M->rccl && !M->loop && out[o])) && ow(o);
+        if (!M->rccl && !merged)
             for (int d = 0; d < NL; ++d)
                 if (d != o) MCHK(f, hipStreamWaitEvent(ml.stream, M->lane[L][d].ev_probe, 0));
         MCHK(f, hipEventRecord(ml.ev_done, ml.stream));

@@ -431,6 +431,34 @@ __global__ void k_or_slices(RouteParts parts, size_t words, uint64_t *out)
     out[w] = m;
 }
 
+// out[w] = bit i set iff verdict byte 64 w + i of any part is nonzero: the
+// members' verdict bytes OR-ed and packed in one pass (in-process merges:
+// no per-member pack kernel)
+__global__ void k_or_bytes(RouteBytes parts, size_t words, uint64_t *out)
+{
+    const size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= words) return;
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < parts.n; ++k) {
+        const uint64_t *v = (const uint64_t *)(parts.p[k] + 64 * w);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[j] |= v[j];
+    }
+    uint64_t m = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) m |= (uint64_t)(((acc[j] >> (8 * b)) & 0xFF) != 0) << (8 * j + b);
+    out[w] = m;
+}
+
+hipError_t launch_or_bytes(const RouteBytes &parts, size_t words, uint64_t *out, hipStream_t s)
+{
+    if (!words) return hipSuccess;
+    k_or_bytes<<<(unsigned)((words + 255) / 256), 256, 0, s>>>(parts, words, out);
+    return hipGetLastError();
+}
+
 static size_t route_lds(const RouteSplit &sp) { return 8 * (size_t)sp.W * sp.S + 4 * (size_t)sp.S + 8; }
 
 uint32_t route_blocks(size_t n) { return (uint32_t)((n + kRouteChunk - 1) / kRouteChunk); }

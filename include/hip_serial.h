@@ -461,7 +461,7 @@ void hsc_collector_destroy(hsc_collector *col);
 int hsc_collector_check(hsc_collector *col, void *ranges, unsigned int *file,
                         unsigned int *offset, int regop_only);
 int hsc_collector_get_stats(hsc_collector *col, hsc_collector_stats *out);
-/* Batches allowed on the device at once (1..4; default 4): their small-batch
+/* Batches allowed on the device at once (1..8; default 4): their small-batch
  * kernels run side by side on streams of their own, and the next leader
  * marshals and launches while earlier batches' kernels run.  Full checks are
  * marshalled by their own callers before they queue. */

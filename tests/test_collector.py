@@ -82,9 +82,9 @@ def test_collector_inflight_bounds():
     col = C.c_void_p()
     assert lib.hsc_collector_create(host.ctx, 0, 0, C.byref(col)) == 0
     try:
-        for bad in (0, 5, -1):
+        for bad in (0, 9, -1):
             assert lib.hsc_collector_set_inflight(col, bad) != 0
-        for ok in (1, 4):
+        for ok in (1, 4, 8):
             assert lib.hsc_collector_set_inflight(col, ok) == 0
     finally:
         lib.hsc_collector_destroy(col)
