@@ -41,8 +41,14 @@ constexpr uint32_t kCTRows = 1u << kCTLog2;  // rows per tile
 // enough for every CU (4096-probe chunks left 110 of 256 idle; chunks sized
 // to one workgroup per CU -- 2560 probes, 232 workgroups -- measured the same,
 // 32.4 vs 32.9 us (r05): a workgroup's time is not its probes in series)
-constexpr int kCLocThreads = 512;
-constexpr int kCLocP = 4;                    // probes per locate thread
+#ifndef HSC_CLOC_THREADS
+#define HSC_CLOC_THREADS 512
+#endif
+#ifndef HSC_CLOC_P
+#define HSC_CLOC_P 4
+#endif
+constexpr int kCLocThreads = HSC_CLOC_THREADS;
+constexpr int kCLocP = HSC_CLOC_P;           // probes per locate thread
 constexpr uint32_t kCChunk = kCLocThreads * kCLocP;
 static_assert(kCChunk <= 4096, "in-chunk ranks are 12 bits");
 constexpr uint32_t kNoSlot = 0xFFFFFFFFu;

@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <utility>
 #include <vector>
 
@@ -535,9 +537,16 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         compress_moves(pp.km, pp.kmv);
         compress_moves(pp.tm, pp.tmv);
         pp.tb = __builtin_popcountll(pp.tm);
-        // about 32 writers per bucket, at most 2^20 buckets
+        // about kPer writers per bucket, at most 2^kDMax buckets (diagnostics:
+        // HSC_GRAPH_DIR = "per,dmax")
+        static int kPer = 32, kDMax = 20;
+        static const bool env_read = [] {
+            if (const char *v = getenv("HSC_GRAPH_DIR")) sscanf(v, "%d,%d", &kPer, &kDMax);
+            return true;
+        }();
+        (void)env_read;
         pp.D = 1;
-        while (pp.D < 20 && ((size_t)32 << pp.D) < nu) ++pp.D;
+        while (pp.D < kDMax && ((size_t)kPer << pp.D) < nu) ++pp.D;
         CK(g.pk.ensure(8 * (size_t)nu));
         CK(g.pdir.ensure(4 * (((size_t)1 << pp.D) + 2)));
         k_pair_keys<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, pp, g.pk.as<uint64_t>());

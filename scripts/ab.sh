@@ -1,12 +1,14 @@
 #!/bin/bash
 # A/B of library builds on one GPU box: bench.py (no CPU leg) alternating
-# between the in-tree libhsc.so and each comdb2_amd/lib/ab/*.so, ROUNDS times.
+# between the in-tree libhsc.so and each $AB_DIR/*.so (default
+# comdb2_amd/lib/ab), ROUNDS times.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 ARGS=${AB_ARGS:---steps 20 --warmup 3 --no-cpu}
 ROUNDS=${ROUNDS:-2}
+AB_DIR=${AB_DIR:-comdb2_amd/lib/ab}
 for r in $(seq 1 $ROUNDS); do
-  for lib in cur comdb2_amd/lib/ab/*.so; do
+  for lib in cur $AB_DIR/*.so; do
     name=$(basename "$lib" .so)
     if [ "$lib" = cur ]; then env=""; else env="HSC_LIB=$PWD/$lib"; fi
     echo "== $name round $r"
