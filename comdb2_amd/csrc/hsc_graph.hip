@@ -538,8 +538,11 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         compress_moves(pp.tm, pp.tmv);
         pp.tb = __builtin_popcountll(pp.tm);
         // about kPer writers per bucket, at most 2^kDMax buckets (diagnostics:
-        // HSC_GRAPH_DIR = "per,dmax")
-        static int kPer = 32, kDMax = 20;
+        // HSC_GRAPH_DIR = "per,dmax").  Config 4 (33M writers, r05o): 32 / 2^20
+        // 11.2 ms per step, 8 / 2^23 10.4 ms (a read's search touches the
+        // directory line and one line of pk instead of ~3), 4 / 2^24 10.4,
+        // 2 / 2^25 10.6 (the directory's own build grows)
+        static int kPer = 8, kDMax = 23;
         static const bool env_read = [] {
             if (const char *v = getenv("HSC_GRAPH_DIR")) sscanf(v, "%d,%d", &kPer, &kDMax);
             return true;
