@@ -440,7 +440,10 @@ __device__ __forceinline__ void join_search(const ProbeWork &work, const CTiles 
     // staging (scans, a barrier, registers) than they saved here
     const bool hit = kind == kCPoint ? pa < pb && rank[pa] > rs
                                      : pa < pb && any_after32(rank, b16, b128, pa, pb, rs);
-    if (hit) flags[txn] = 1;
+    if (hit) {
+        flags[txn] = 1;
+        if (work.bitmap) atomicOr((unsigned long long *)&work.bitmap[txn >> 6], 1ull << (txn & 63));
+    }
     HSC_STAMP(work, 1, 5);
 }
 

@@ -2230,6 +2230,8 @@ static WinView win_view(hsc_ctx *c)
 }
 
 static int probe_delta(hsc_ctx *c, uint8_t *target);
+// the batch's delta probe will mark verdict bytes (then a pack pass builds the bitmap)
+static bool pack_after_delta(const hsc_ctx *c) { return c->raw_probe.n && (c->fn || c->dn); }
 
 // Narrow layout: one kernel answers every range and table lock.
 static int probe_narrow(hsc_ctx *c, const hsc_probe_batch *b, const WinView &w,
@@ -2385,8 +2387,12 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
     HIPCHK(c, launch_locate_t(c->nv, wn, p, work, ntl, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     if (p.n && wn.ntiles) {
-        // the plan writes the verdict bytes from the locate's flags; the join
-        // and the delta probe then mark the verdict itself
+        // the plan writes the verdict bytes (and bitmap words) from the
+        // locate's flags; the join and the delta probe then mark the verdict
+        // itself, the join its bitmap bits too (no pack pass unless the delta
+        // probe ran: it marks bytes only)
+        const bool delta = pack_after_delta(c);
+        work.bitmap = delta ? nullptr : b->bitmap;
         HIPCHK(c, launch_plan_s(work, wn.ntiles, c->w_items.as<uint32_t>(), s, flags,
                                 (uint32_t)b->n_txn, b->verdict));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
@@ -2394,7 +2400,7 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
         HIPCHK(c, launch_join_t(work, ntl, wn.n, wn.ntiles, max_items, b->verdict, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
         HIPCHK_RC(c, probe_delta(c, b->verdict));
-        HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
+        if (delta) HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
     } else {
         if (tm)
             for (int i = 2; i <= 4; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));
@@ -2481,7 +2487,9 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
                               work, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
     if (p.n && ct.ntiles) {
-        // pack folded into the plan, as probe_ntiles
+        // verdict bytes and bitmap from the plan and the join, as probe_ntiles
+        const bool delta = pack_after_delta(c);
+        work.bitmap = delta ? nullptr : b->bitmap;
         HIPCHK(c, launch_plan_s(work, ct.ntiles, c->w_items.as<uint32_t>(), s, flags,
                                 (uint32_t)b->n_txn, b->verdict));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
@@ -2489,7 +2497,7 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
         HIPCHK(c, launch_join_c(ct, work, max_items, b->verdict, s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
         HIPCHK_RC(c, probe_delta(c, b->verdict));
-        HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
+        if (delta) HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));
     } else {
         if (tm)
             for (int i = 2; i <= 4; ++i) HIPCHK(c, hipEventRecord(c->ev[i], s));

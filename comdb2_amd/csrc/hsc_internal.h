@@ -194,6 +194,10 @@ struct ProbeWork {
     // t's run starts in it; join items are tile-local record ranges
     uint16_t *cst;
     uint32_t *cm;  // [G][round4(ntiles)] chunk-major (run start << 16 | count), the locate's rows
+    // the batch's verdict bitmap, built in place of a pack pass (narrow and
+    // compact tiles): k_plan_s writes the locate's flags as whole words, the
+    // join ORs its hits in (null: verdict bytes only)
+    uint64_t *bitmap;
 };
 // Diagnostic phase stamps (HSC_STAMPS builds only): thread 0 of a block
 // records s_memtime at phase boundaries into a buffer of its own (never an

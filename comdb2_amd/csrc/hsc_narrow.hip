@@ -1669,11 +1669,14 @@ __global__ __launch_bounds__(kPlanSThreads) void k_plan_s(ProbeWork work, uint32
         sh[4 * pc][g] = a.x, sh[4 * pc + 1][g] = a.y, sh[4 * pc + 2][g] = a.z, sh[4 * pc + 3][g] = a.w;
     }
     if (verdict) {
+        // (a wave covers 64 consecutive read sets, 64-aligned: one bitmap word)
         const uint32_t stride = gridDim.x * kPlanSThreads;
         for (uint32_t i = blockIdx.x * kPlanSThreads + threadIdx.x; i < n_txn; i += stride) {
             const uint8_t f = flags[i];
             verdict[i] = f != 0;
             if (f) flags[i] = 0;
+            const uint64_t m = __ballot(f != 0);
+            if (work.bitmap && lane == 0) work.bitmap[i >> 6] = m;
         }
     }
     __syncthreads();
@@ -1834,7 +1837,10 @@ __device__ __forceinline__ void join_s_item(const ProbeWork &work, const NarrowT
         const uint32_t kl = keys[0];
         const uint32_t pa = min(ja - T + (kl < lo), tn);
         const uint32_t pb = min(jb - T + (kl <= hi), tn);
-        if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) verdict[rec[k].w] = 1;
+        if (pa < pb && any_after32(rank, b16, b128, pa, pb, rs)) {
+            verdict[rec[k].w] = 1;
+            if (work.bitmap) atomicOr((unsigned long long *)&work.bitmap[rec[k].w >> 6], 1ull << (rec[k].w & 63));
+        }
     }
 }
 

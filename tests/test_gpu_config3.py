@@ -83,4 +83,7 @@ def probe_sub(v, m):
                         bitmap.data_ptr())
     v.probe_device(pb)
     v.synchronize()
+    # the bitmap comes from the plan + join (no pack pass): equal to the bytes
+    bits = np.unpackbits(bitmap.cpu().numpy().view(np.uint8), bitorder="little")[:T]
+    np.testing.assert_array_equal(bits.astype(bool), verdict.cpu().numpy() != 0)
     return np.maximum(verdict.cpu().numpy(), m["forced"]) != 0

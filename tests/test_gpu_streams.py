@@ -95,3 +95,34 @@ def test_streams_interleaved_match_oracle(validator, oracle_mod, nstreams):
         bits = np.unpackbits(bitmap.cpu().numpy().view(np.uint8), bitorder="little")[:len(got)]
         np.testing.assert_array_equal(bits.astype(bool), verdict.cpu().numpy() != 0)
     assert sum(int(w.sum()) for w in want) > 0
+
+
+@pytest.mark.parametrize("layout", ["tiles", "auto"])
+def test_tile_path_bitmap_equals_verdict(validator, oracle_mod, layout):
+    """The tile pipeline builds the verdict bitmap itself (k_plan_s writes the
+    locate's flags as whole words, the join ORs its hits in; no pack pass):
+    a bitmap holding garbage from before must come back equal to the verdict
+    bytes, and the bytes to the oracle's verdicts."""
+    from comdb2_amd.hsc import LAYOUT_AUTO, LAYOUT_NARROW_TILES
+    dev = torch.device("cuda", 0)
+    log, batches = one_log_two_batches(31, n_txn=4000, ranges=10)
+    want = [oracle_mod.check(log, rs, nthreads=8)[0] != 0 for rs in batches]
+    v = validator
+    v.set_layout(LAYOUT_NARROW_TILES if layout == "tiles" else LAYOUT_AUTO)
+    try:
+        v.ingest_log(log)
+        for bi, rs in enumerate(batches):
+            m = v.marshal(rs)
+            u = upload(dev, m)
+            T = u["n_txn"]
+            verdict = torch.full((T,), 7, dtype=torch.uint8, device=dev)
+            bitmap = torch.full(((T + 63) // 64,), -1, dtype=torch.int64, device=dev)
+            for _ in range(2):  # the second pass over the first one's outputs
+                v.probe_device(probe_struct(u, verdict, bitmap))
+                torch.cuda.synchronize()
+                got = np.maximum(verdict.cpu().numpy(), m["forced"]) != 0
+                np.testing.assert_array_equal(got, want[bi])
+                bits = np.unpackbits(bitmap.cpu().numpy().view(np.uint8), bitorder="little")[:T]
+                np.testing.assert_array_equal(bits.astype(bool), verdict.cpu().numpy() != 0)
+    finally:
+        v.set_layout(LAYOUT_AUTO)
