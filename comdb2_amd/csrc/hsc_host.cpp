@@ -2397,7 +2397,14 @@ static int probe_ntiles(hsc_ctx *c, const hsc_probe_batch *b, const WinView &wn,
                                 (uint32_t)b->n_txn, b->verdict));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[2], s));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[3], s));
-        HIPCHK(c, launch_join_t(work, ntl, wn.n, wn.ntiles, max_items, b->verdict, s));
+        // blocks past the tiles for the hot tiles' overflow items: 512, or 2048
+        // on a skewed window (the bucket table took log mode: Zipf keys crowd
+        // a few tiles -- r03: config 5 one stream 83 -> 80 us with 2048, while
+        // config 2's idle extra blocks cost its overlapped batch); diagnostics:
+        // HSC_JOIN_EXTRA
+        static const int extra_env = getenv("HSC_JOIN_EXTRA") ? atoi(getenv("HSC_JOIN_EXTRA")) : 0;
+        const uint32_t extra = extra_env > 0 ? (uint32_t)extra_env : c->trad_log ? 2048u : 512u;
+        HIPCHK(c, launch_join_t(work, ntl, wn.n, wn.ntiles, max_items, b->verdict, s, extra));
         if (tm) HIPCHK(c, hipEventRecord(c->ev[4], s));
         HIPCHK_RC(c, probe_delta(c, b->verdict));
         if (delta) HIPCHK(c, launch_pack(b->verdict, (uint32_t)b->n_txn, b->bitmap, s));

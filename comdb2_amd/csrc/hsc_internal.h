@@ -437,7 +437,8 @@ hipError_t launch_locate_t(const NarrowView &nv, const WinView &wt, const ProbeV
                            const ProbeWork &work, const NarrowTiles &nt, uint8_t *verdict,
                            hipStream_t s);
 hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t n,
-                         uint32_t ntiles, uint32_t max_items, uint8_t *verdict, hipStream_t s);
+                         uint32_t ntiles, uint32_t max_items, uint8_t *verdict, hipStream_t s,
+                         uint32_t extra_blocks = 512);
 // Dependency graph + SCC (hsc_graph.hip).
 constexpr uint64_t kDepWW = 1, kDepWR = 2, kDepRW = 4;
 struct GraphInput {              // device pointers

@@ -1883,13 +1883,14 @@ __global__ __launch_bounds__(kJoinThreads) HSC_JOIN_ATTR void k_join_t(ProbeWork
 }
 
 hipError_t launch_join_t(const ProbeWork &work, const NarrowTiles &nt, uint32_t n,
-                         uint32_t ntiles, uint32_t max_items, uint8_t *verdict, hipStream_t s)
+                         uint32_t ntiles, uint32_t max_items, uint8_t *verdict, hipStream_t s,
+                         uint32_t extra_blocks)
 {
     if (max_items == 0 || n == 0 || ntiles == 0) return hipSuccess;
-    // one block per tile + up to 512 blocks looping over the overflow items
-    // (measured: one block per tile beats persistent blocks that prefetch
-    // their next tile -- 27.8 vs 32 us on config 2)
-    const uint32_t blocks = join_tile_blocks(ntiles) + std::min<uint32_t>(max_items - ntiles, 512);
+    // one block per tile + up to extra_blocks blocks looping over the
+    // overflow items (measured: one block per tile beats persistent blocks
+    // that prefetch their next tile -- 27.8 vs 32 us on config 2)
+    const uint32_t blocks = join_tile_blocks(ntiles) + std::min<uint32_t>(max_items - ntiles, extra_blocks);
     k_join_t<<<blocks, kJoinThreads, 0, s>>>(work, nt, n, ntiles, verdict);
     return hipGetLastError();
 }

@@ -1154,6 +1154,28 @@ class MultiValidator(Validator):
         self._chk(self.lib.hsc_multi_probe_routed(self.ctx, arr, ob.ctypes.data, lane),
                   "hsc_multi_probe_routed")
 
+    def prepare_routed(self, batches: Sequence[ProbeBatch], owner_base: Sequence[int]):
+        """The arguments of hsc_multi_probe_routed built once (the ctypes
+        array of member batches and the owner bases), for a caller that
+        probes the same resident batches many times (bench.py's ring): the
+        step is then one foreign call, no per-call marshalling in Python."""
+        arr = (ProbeBatch * len(batches))(*batches)
+        ob = np.ascontiguousarray(owner_base, np.uint64)
+        return (arr, ob, C.c_void_p(ob.ctypes.data))
+
+    def probe_routed_prepared(self, prep, lane: int = 0) -> None:
+        rc = self.lib.hsc_multi_probe_routed(self.ctx, prep[0], prep[2], lane)
+        if rc:
+            self._chk(rc, "hsc_multi_probe_routed")
+
+    def prepare_device(self, batches: Sequence[ProbeBatch]):
+        return (ProbeBatch * len(batches))(*batches)
+
+    def probe_device_prepared(self, arr, lane: int = 0) -> None:
+        rc = self.lib.hsc_multi_probe_device(self.ctx, arr, lane)
+        if rc:
+            self._chk(rc, "hsc_multi_probe_device")
+
     def route_stats(self) -> dict:
         out = np.zeros(8, np.float64)
         self._chk(self.lib.hsc_multi_route_stats(self.ctx, out.ctypes.data), "hsc_multi_route_stats")
