@@ -567,13 +567,25 @@ def api_leg(hsc, v, rs, device_verdict, args):
     got, st = v.concurrent_check(arrs, 64, inflight=1)
     st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want))
     conc["threads_64_inflight1"] = st
+    # the plain drop-in entry (hip_bdb_osql_serial_check) from 64 threads: by
+    # default it joins the context's own collector
+    got, st = v.concurrent_check(arrs, 64, collect=False)
+    st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want))
+    st["entry"] = "hip_bdb_osql_serial_check (context-owned collector, the default)"
+    conc["threads_64_dropin"] = st
     m = min(T, 2000)  # uncollected: one device pass per call, a bounded sample
     sub = hsc.NativeCurRangeArrs(_readsets_head(rs, m))
+    got, st = v.concurrent_check(sub, 1, collect=False)  # a lone caller of the default entry
+    st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want[:m]))
+    st["sample"] = f"first {m} read sets"
+    conc["threads_1_dropin"] = st
+    v.set_autocollect(False)
     for nth in (1, 64):
         got, st = v.concurrent_check(sub, nth, collect=False)
         st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want[:m]))
         st["sample"] = f"first {m} read sets"
         conc[f"threads_{nth}_uncollected"] = st
+    v.set_autocollect(True)
     sub.close()
     arrs.close()
     ok = bool(np.array_equal(rc != 0, want))
@@ -1062,11 +1074,13 @@ def multi_api_leg(hsc, v, rs, want):
     conc["threads_64_inflight"] = sweep
     m = min(rs.ntxn, 2000)
     sub = hsc.NativeCurRangeArrs(_readsets_head(rs, m))
+    v.set_autocollect(False)
     for nth in (1, 64):
         got, st = v.concurrent_check(sub, nth, collect=False)
         st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want[:m]))
         st["sample"] = f"first {m} read sets"
         conc[f"threads_{nth}_uncollected"] = st
+    v.set_autocollect(True)
     r1 = v.route_stats()
     sub.close()
     arrs.close()

@@ -521,6 +521,10 @@ struct hsc_ctx {
     // per-worker parts, host threads
     hsc_marshalled m{};
     Stage stage[2];
+    // the drop-in entry's own collector (hsc_set_autocollect), created at the
+    // first collected call
+    std::atomic<int> autocollect{1};
+    std::atomic<hsc_collector *> auto_col{nullptr};
     std::vector<MarshalPart> parts;
     std::vector<std::vector<uint8_t>> parts_cls;  // per part: probe class (length, point) in marshal_into
     int threads = 1;

@@ -3071,6 +3071,7 @@ int hsc_ctx_create(int device, hsc_ctx **out)
 void hsc_ctx_destroy(hsc_ctx *c)
 {
     if (!c) return;
+    if (hsc_collector *k = c->auto_col.exchange(nullptr)) hsc_collector_destroy(k);
     if (c->multi) multi_destroy(c);  // the members first; the front is host-only
     if (c->host_only) {
         for (Stage &st : c->stage) st.release();
@@ -4128,10 +4129,33 @@ int hsc_set_threads(hsc_ctx *c, int n)
     return HSC_OK;
 }
 
+int hsc_set_autocollect(hsc_ctx *c, int on)
+{
+    if (!c || (on != 0 && on != 1)) return HSC_EINVAL;
+    c->autocollect.store(on, std::memory_order_relaxed);
+    return HSC_OK;
+}
+
+// The context's collector, created by the first call that needs it (a racing
+// creator keeps the winner's and drops its own).
+static hsc_collector *auto_collector(hsc_ctx *c)
+{
+    hsc_collector *k = c->auto_col.load(std::memory_order_acquire);
+    if (k) return k;
+    hsc_collector *mine = nullptr;
+    if (hsc_collector_create(c, 0, 0, &mine) != HSC_OK) return nullptr;
+    if (c->auto_col.compare_exchange_strong(k, mine, std::memory_order_acq_rel)) return mine;
+    hsc_collector_destroy(mine);
+    return k;
+}
+
 int hip_bdb_osql_serial_check(void *ctx, void *ranges, unsigned int *file, unsigned int *offset,
                               int regop_only)
 {
     if (!ranges) return 0;
+    hsc_ctx *c = (hsc_ctx *)ctx;
+    if (c && c->autocollect.load(std::memory_order_relaxed))
+        if (hsc_collector *k = auto_collector(c)) return hsc_collector_check(k, ranges, file, offset, regop_only);
     int rc_out = 1;
     void *arr[1] = {ranges};
     int rc = hip_serial_check_batch(ctx, arr, file, offset, regop_only, 1, &rc_out);

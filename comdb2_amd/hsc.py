@@ -160,6 +160,7 @@ EXPORTS = [
     "hsc_window_delta_rows", "hsc_set_threads", "hsc_currangearrs_build",
     "hsc_currangearrs_free", "hsc_collector_create", "hsc_collector_destroy",
     "hsc_collector_check", "hsc_collector_get_stats", "hsc_collector_set_inflight",
+    "hsc_set_autocollect",
     "hsc_small_stats", "hsc_harness_concurrent",
     "hsc_dep_graph_build", "hsc_dep_graph_stage_rw_pairs", "hsc_dep_graph_scc_built", "hsc_dep_graph_build_device", "hsc_dep_graph_cover", "hsc_dep_graph_cut", "hsc_dep_graph_scc_cut",
     "hsc_multi_create", "hsc_multi_unique_ids", "hsc_multi_create_rank", "hsc_multi_world",
@@ -264,6 +265,7 @@ def load() -> C.CDLL:
                                           C.c_int]),
         "hsc_collector_get_stats": (C.c_int, [_p, C.POINTER(CollectorStats)]),
         "hsc_collector_set_inflight": (C.c_int, [_p, C.c_int]),
+        "hsc_set_autocollect": (C.c_int, [_p, C.c_int]),
         "hsc_small_stats": (C.c_int, [_p, C.POINTER(SmallStats)]),
         "hsc_harness_concurrent": (C.c_int, [_p, _p, C.POINTER(_p), C.c_int, C.c_int, C.c_int,
                                              C.c_int, C.POINTER(C.c_int),
@@ -974,6 +976,11 @@ class Validator:
         """out[w] = OR of the nparts bitmaps parts[k * words + w] (device)."""
         self._chk(self.lib.hsc_or_bitmaps(self.ctx, parts_ptr, nparts, words, out_ptr),
                   "hsc_or_bitmaps")
+
+    def set_autocollect(self, on: bool) -> None:
+        """hip_bdb_osql_serial_check through the context's own collector
+        (the default) or one device pass per call."""
+        self._chk(self.lib.hsc_set_autocollect(self.ctx, 1 if on else 0), "hsc_set_autocollect")
 
     def set_stream(self, stream_handle: int) -> None:
         self._chk(self.lib.hsc_set_stream(self.ctx, stream_handle), "hsc_set_stream")

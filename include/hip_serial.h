@@ -403,9 +403,17 @@ int hsc_merge_table_max(hsc_ctx *ctx, const uint64_t *in, int n);
 /* ---- drop-in checks ----------------------------------------------------- */
 /* Exactly bdb_osql_serial_check (bdb/serializable.c:571-579) for one read set:
  * ranges == NULL -> 0; regop_only -> nonzero iff a committed write txn follows
- * (*file,*offset); otherwise (*file,*offset) := end LSN, then the full check. */
+ * (*file,*offset); otherwise (*file,*offset) := end LSN, then the full check.
+ * Concurrent callers (one per committing transaction, db/toblock.c:4777-4800)
+ * are batched by a collector the context owns (hsc_collector_check below):
+ * a lone caller runs its own single-set pass, callers that arrive while a pass
+ * runs form the next one -- none waits on another's context lock.
+ * hsc_set_autocollect(ctx, 0) makes every call its own pass instead. */
 int hip_bdb_osql_serial_check(void *ctx, void *ranges, unsigned int *file,
                               unsigned int *offset, int regop_only);
+/* The drop-in entry through the context's own collector (1, the default) or
+ * one pass per call (0).  0 or HSC_EINVAL. */
+int hsc_set_autocollect(hsc_ctx *ctx, int on);
 /* n read sets in one device pass.  ranges[i] is a CurRangeArr* (may be NULL);
  * file/offset are arrays of n in/out snapshot LSNs, or NULL to use (and
  * update) ranges[i]->file / ->offset in place.  Per element the semantics and

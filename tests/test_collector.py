@@ -107,19 +107,25 @@ def test_gpu_full_checks_through_collector(validator, oracle_mod, nthreads, infl
 
 
 @pytest.mark.gpu
-def test_gpu_uncollected_callers_share_small_slots(oracle_mod):
-    # 32 threads calling hip_bdb_osql_serial_check directly on a narrow window
-    # (the small-batch path): each releases the context lock while its kernel
-    # runs, so up to 4 slots are in flight
+@pytest.mark.parametrize("autocollect", [False, True])
+def test_gpu_uncollected_callers_share_small_slots(oracle_mod, autocollect):
+    # 32 threads calling hip_bdb_osql_serial_check on a narrow window (the
+    # small-batch path).  autocollect off: one pass per call, each releasing
+    # the context lock while its kernel runs (up to 8 slots in flight); on
+    # (the default): the calls join the context's own collector
     v = Validator(0)
     try:
+        v.set_autocollect(autocollect)
         wl = config2(n_commits=20_000, n_txn=2_000, seed=13)
         v.ingest_log(wl.log)
         want, _, _ = oracle_mod.check(wl.log, wl.readsets)
         arrs = NativeCurRangeArrs(wl.readsets)
         got, st = v.concurrent_check(arrs, 32, rounds=2, collect=False)
         np.testing.assert_array_equal(got != 0, want != 0)
-        assert st["small_path"]["passes"] == 2 * wl.readsets.ntxn
+        if autocollect:
+            assert 0 < st["small_path"]["passes"] <= 2 * wl.readsets.ntxn
+        else:
+            assert st["small_path"]["passes"] == 2 * wl.readsets.ntxn
         arrs.close()
     finally:
         v.close()
