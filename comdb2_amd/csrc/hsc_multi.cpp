@@ -568,8 +568,9 @@ static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb,
         if (rc) return rc;
         if (ml.timed) MCHK(c, hipEventRecord(ml.ev_t1, ml.stream));
         // (not the context's own lane event: a concurrent caller of the member
-        // may take that lane and record it again before the merges wait)
-        MCHK(c, hipEventRecord(ml.ev_probe, ml.stream));
+        // may take that lane and record it again before the merges wait);
+        // only other local members' streams wait on it
+        if (NL > 1) MCHK(c, hipEventRecord(ml.ev_probe, ml.stream));
         return HSC_OK;
     };
     int prc[kMultiMax] = {};
