@@ -111,7 +111,7 @@ struct MLane {
     hipEvent_t ev_count = nullptr, ev_scatter = nullptr, ev_probe = nullptr, ev_done = nullptr;
     hipEvent_t ev_t0 = nullptr, ev_t1 = nullptr;  // timed: around this member's probe (hsc_multi_enable_timing)
     bool timed = false;
-    bool used = false;    // ev_done recorded
+    bool used = false;    // the lane ran a batch (ev_done recorded when nlocal > 1)
 };
 
 struct Multi {
@@ -661,7 +661,10 @@ static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb,
         if (!M->rccl && !merged)
             for (int d = 0; d < NL; ++d)
                 if (d != o) MCHK(f, hipStreamWaitEvent(ml.stream, M->lane[L][d].ev_probe, 0));
-        MCHK(f, hipEventRecord(ml.ev_done, ml.stream));
+        // (only the other local members' next use of the lane waits on it: one
+        // member orders its lane by its stream alone -- the world-1 step 51 ->
+        // 48 us without the probe event, r05x)
+        if (NL > 1) MCHK(f, hipEventRecord(ml.ev_done, ml.stream));
         ml.used = true;
     }
     M->batches++;
@@ -1484,7 +1487,9 @@ int hsc_multi_set_transport(hsc_ctx *f, int transport)
     if (M->rccl) return transport == HSC_MULTI_DIRECT ? HSC_OK : mfail(f, HSC_EINVAL, "per-rank context: RCCL");
     for (int L = 0; L < kMultiLanes; ++L)  // nothing of the other form in flight
         for (int m = 0; m < M->nlocal; ++m)
-            if (M->lane[L][m].used) MCHK(f, hipEventSynchronize(M->lane[L][m].ev_done));
+            if (M->lane[L][m].used)
+                MCHK(f, M->nlocal > 1 ? hipEventSynchronize(M->lane[L][m].ev_done)
+                                      : hipStreamSynchronize(M->lane[L][m].stream));
     M->loop = transport == HSC_MULTI_LOOPBACK;
     return HSC_OK;
 }
