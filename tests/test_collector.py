@@ -145,3 +145,26 @@ def test_gpu_collector_config2_sample(oracle_mod):
         arrs.close()
     finally:
         v.close()
+
+
+@pytest.mark.parametrize("autocollect", [True, False])
+def test_dropin_entry_autocollect_regop(host, oracle_mod, autocollect):
+    """hip_bdb_osql_serial_check through the context's own collector (the
+    default) and one pass per call give the same verdicts; bad switch
+    values are refused."""
+    import ctypes as C
+    from comdb2_amd.hsc import load
+    lib = load()
+    assert lib.hsc_set_autocollect(host.ctx, 2) != 0
+    assert lib.hsc_set_autocollect(None, 1) != 0
+    host.set_autocollect(autocollect)
+    try:
+        log, rs = random_case(4242, broken=True, n_txn=300)
+        host.ingest_log(log)
+        want, _, _ = oracle_mod.check(log, rs, regop_only=1)
+        arrs = NativeCurRangeArrs(rs)
+        got, _ = host.concurrent_check(arrs, 8, rounds=2, regop_only=1, collect=False)
+        np.testing.assert_array_equal(got != 0, want != 0)
+        arrs.close()
+    finally:
+        host.set_autocollect(True)
