@@ -3026,6 +3026,30 @@ int hsc_device_count(void)
     return n;
 }
 
+// The drop-in entry's first calls without allocations: slot 0's stream and
+// counters, and fine-grained staging for two small batches (the marshal's
+// stage and slot 0 trade arenas at every launch) on both the direct and the
+// collector's premarshalled path.  Failures here only leave it to the first
+// call, as before.
+static void warm_small(hsc_ctx *c)
+{
+    constexpr size_t kWarmBytes = 64 * 1024;
+    if (create_stream(&c->small_side[0], true) != hipSuccess) c->small_side[0] = nullptr;
+    if (c->small_side[0] && c->small_blocks.ensure(64 * hsc_ctx::kSmallSlots) == hipSuccess &&
+        hipMemsetAsync(c->small_blocks.p, 0, 64 * hsc_ctx::kSmallSlots, c->small_side[0]) == hipSuccess &&
+        hipStreamSynchronize(c->small_side[0]) == hipSuccess)
+        c->small_blocks_zeroed = true;
+    (void)c->small[0].io.ensure(kWarmBytes, true, true);
+    (void)c->small_st.arena.ensure(kWarmBytes, true, true);
+    (void)c->small_st.forced.ensure(1024, true);
+    Stage *ps = new (std::nothrow) Stage();
+    if (!ps) return;
+    (void)ps->arena.ensure(kWarmBytes, true, true);
+    (void)ps->forced.ensure(1024, true);
+    c->pre_stages.emplace_back(ps);
+    c->pre_free.push_back(ps);
+}
+
 int hsc_ctx_create(int device, hsc_ctx **out)
 {
     if (!out) return HSC_EINVAL;
@@ -3051,6 +3075,7 @@ int hsc_ctx_create(int device, hsc_ctx **out)
         return HSC_EDEVICE;
     }
     c->stream = c->own_stream;
+    warm_small(c);
     // every file's code object now, not lazily inside the first build / probe
     static std::mutex warm_mu;
     static std::vector<bool> warmed;
