@@ -561,11 +561,17 @@ struct hsc_ctx {
     // it, so batches on different streams never share scratch and can run
     // concurrently; a lane taken over by another stream first waits for the
     // lane's last batch (its done event).
+    // The done event is recorded when the context leaves the lane's stream
+    // (hsc_set_stream, the multi context's member probes), not after every
+    // batch: batches on one stream are ordered by it, and a record per batch
+    // cost a one-stream config-2 batch 3 us (r05ab: 0.683 -> 0.718 of peak).
+    // pend: batches on the stream since the last record.
     struct Lane {
         DBuf b[20];
         hipStream_t stream = nullptr;
         hipEvent_t done = nullptr;
         uint64_t tick = 0;
+        bool pend = false;
     };
     static constexpr int kLanes = 4;
     Lane lanes[kLanes];
@@ -639,6 +645,9 @@ void ctx_add_write(hsc_ctx *c, int tid, int ix, const uint8_t *key, int keylen, 
 int ctx_flush_appends(hsc_ctx *c, bool lazy = false);
 void ctx_raise_table_max(hsc_ctx *c, int tid, uint64_t lsn);
 int ctx_probe(hsc_ctx *c, const hsc_probe_batch *b);
+// c->stream := s, the active lane's batches on the stream left fenced by its
+// done event first (callers hold c->mu)
+hipError_t ctx_switch_stream(hsc_ctx *c, hipStream_t s);
 int ctx_default_threads();
 void ctx_par_for(hsc_ctx *c, int nwork, const std::function<void(int)> &f);
 bool ctx_small_fits(hsc_ctx *c, size_t n_txn, size_t n, size_t n_lock);

@@ -84,7 +84,27 @@ static hipError_t lane_done(hsc_ctx *c)
         hipError_t e = hipEventCreateWithFlags(&L.done, hipEventDisableTiming);
         if (e != hipSuccess) return e;
     }
+    L.pend = false;
     return hipEventRecord(L.done, c->stream);
+}
+
+// A batch of the active lane went onto c->stream: its done event is recorded
+// when the context leaves the stream (lane_leave) -- a take-over of the lane
+// or a window change from another stream happens only after that.
+static void lane_mark(hsc_ctx *c) { c->lanes[c->lane].pend = true; }
+
+static hipError_t lane_leave(hsc_ctx *c)
+{
+    hsc_ctx::Lane &L = c->lanes[c->lane];
+    return L.pend && L.stream == c->stream ? lane_done(c) : hipSuccess;
+}
+
+hipError_t hsc::ctx_switch_stream(hsc_ctx *c, hipStream_t s)
+{
+    if (s == c->stream) return hipSuccess;
+    const hipError_t e = lane_leave(c);
+    c->stream = s;
+    return e;
 }
 
 // Small batches (k_small_narrow) run on the stream current at their launch
@@ -2526,13 +2546,10 @@ static int probe(hsc_ctx *c, const hsc_probe_batch *b)
     HIPCHK(c, select_lane(c));
     const int rc = probe_lane(c, b);
     // the lane's done event fences whatever probe_lane launched, also when it
-    // failed part way: a later take-over of the lane or a window rebuild
-    // waits on it before touching the lane's scratch
-    const hipError_t e = lane_done(c);
-    if (e != hipSuccess) {
-        (void)hipStreamSynchronize(c->stream);
-        if (rc == HSC_OK) return fail(c, HSC_EDEVICE, "lane_done", e);
-    }
+    // failed part way: a later take-over of the lane or a window rebuild from
+    // another stream waits on it before touching the lane's scratch; it is
+    // recorded when the context leaves this stream (ctx_switch_stream)
+    lane_mark(c);
     return rc;
 }
 
@@ -3175,7 +3192,7 @@ int hsc_set_stream(hsc_ctx *c, void *st)
     // appends return before their upload and merge ran: the new stream waits
     if (c->app_last && ns != c->stream && hipStreamWaitEvent(ns, c->app_last, 0) != hipSuccess)
         return fail(c, HSC_EDEVICE, "set_stream: order after the appends");
-    c->stream = ns;
+    if (ctx_switch_stream(c, ns) != hipSuccess) return fail(c, HSC_EDEVICE, "set_stream: lane fence");
     return HSC_OK;
 }
 

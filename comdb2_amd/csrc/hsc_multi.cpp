@@ -562,9 +562,9 @@ static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb,
             MCHK(c, hipEventRecord(ml.ev_t0, ml.stream));
         }
         hipStream_t keep = c->stream;
-        c->stream = ml.stream;
+        MCHK(c, ctx_switch_stream(c, ml.stream));
         const int rc = ctx_probe(c, &b);
-        c->stream = keep;
+        MCHK(c, ctx_switch_stream(c, keep));  // (fences the member's lane of ml.stream)
         if (rc) return rc;
         if (ml.timed) MCHK(c, hipEventRecord(ml.ev_t1, ml.stream));
         // (not the context's own lane event: a concurrent caller of the member

@@ -218,7 +218,9 @@ void hsc_ctx_destroy(hsc_ctx *ctx);
  * takes over the least recently used lane after waiting for that lane's last
  * batch), so batches probed on different streams may run concurrently.
  * Window builds wait for every lane's last batch; the caller orders a window
- * change against later probes on other streams. */
+ * change against later probes on other streams.  A stream stays in use by the
+ * context until the next hsc_set_stream (which records its lane's fence on
+ * it) or hsc_ctx_destroy: keep it valid until then. */
 int hsc_set_stream(hsc_ctx *ctx, void *hip_stream);
 const char *hsc_last_error(hsc_ctx *ctx);
 int hsc_device_count(void);
