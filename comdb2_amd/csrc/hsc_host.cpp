@@ -3043,18 +3043,19 @@ int hsc_device_count(void)
     return n;
 }
 
-// The drop-in entry's first calls without allocations: slot 0's stream and
-// counters, and fine-grained staging for two small batches (the marshal's
-// stage and slot 0 trade arenas at every launch) on both the direct and the
+// The drop-in entry's first calls without allocations: the slots' counters
+// and fine-grained staging for two small batches (the marshal's stage and
+// slot 0 trade arenas at every launch) on both the direct and the
 // collector's premarshalled path.  Failures here only leave it to the first
-// call, as before.
+// call, as before.  (Not slot 0's stream: a stream made here took a hardware
+// queue from the caller's streams -- GPU_MAX_HW_QUEUES is 4 -- and config 3's
+// three bench streams then shared one, 72.6 -> 99 us per batch, r05ac.)
 static void warm_small(hsc_ctx *c)
 {
     constexpr size_t kWarmBytes = 64 * 1024;
-    if (create_stream(&c->small_side[0], true) != hipSuccess) c->small_side[0] = nullptr;
-    if (c->small_side[0] && c->small_blocks.ensure(64 * hsc_ctx::kSmallSlots) == hipSuccess &&
-        hipMemsetAsync(c->small_blocks.p, 0, 64 * hsc_ctx::kSmallSlots, c->small_side[0]) == hipSuccess &&
-        hipStreamSynchronize(c->small_side[0]) == hipSuccess)
+    if (c->small_blocks.ensure(64 * hsc_ctx::kSmallSlots) == hipSuccess &&
+        hipMemsetAsync(c->small_blocks.p, 0, 64 * hsc_ctx::kSmallSlots, c->own_stream) == hipSuccess &&
+        hipStreamSynchronize(c->own_stream) == hipSuccess)
         c->small_blocks_zeroed = true;
     (void)c->small[0].io.ensure(kWarmBytes, true, true);
     (void)c->small_st.arena.ensure(kWarmBytes, true, true);
