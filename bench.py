@@ -1168,6 +1168,13 @@ def main():
         return bench_commit_stream(args)
     if (int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.gpus > 1 or args.inproc > 1
             or args.rank_path):
+        # the multi context runs more streams per process than HIP's default 4
+        # hardware queues (per member: its lanes' streams, its small-batch
+        # slots; RCCL's): with 4, streams share queues and serialise (r05ae:
+        # 2 members on one GPU 119.5 -> 100.7 us per step with 8).  Read by the
+        # HIP runtime at its initialisation, so set before anything touches the
+        # GPU; an explicit setting wins.
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
         return bench_multi(args)
     # one GPU (N > 1 runs bench_multi)
     world, rank = 1, 0
