@@ -1173,8 +1173,12 @@ def main():
         # slots; RCCL's): with 4, streams share queues and serialise (r05ae:
         # 2 members on one GPU 119.5 -> 100.7 us per step with 8).  Read by the
         # HIP runtime at its initialisation, so set before anything touches the
-        # GPU; an explicit setting wins.
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+        # GPU; a larger setting is kept.
+        try:
+            q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+        except ValueError:
+            q = 4
+        os.environ["GPU_MAX_HW_QUEUES"] = str(max(q, 8))
         return bench_multi(args)
     # one GPU (N > 1 runs bench_multi)
     world, rank = 1, 0
