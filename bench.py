@@ -1072,6 +1072,11 @@ def multi_api_leg(hsc, v, rs, want):
                            "lat_p99_us": s2["lat_p99_us"], "mean_batch": s2.get("mean_batch"),
                            "parity_with_device_batch": bool(np.array_equal(got != 0, want))}
     conc["threads_64_inflight"] = sweep
+    # the plain drop-in entry from 64 threads (the context's own collector)
+    got, st = v.concurrent_check(arrs, 64, collect=False)
+    st["parity_with_device_batch"] = bool(np.array_equal(got != 0, want))
+    st["entry"] = "hip_bdb_osql_serial_check (context-owned collector, the default)"
+    conc["threads_64_dropin"] = st
     m = min(rs.ntxn, 2000)
     sub = hsc.NativeCurRangeArrs(_readsets_head(rs, m))
     v.set_autocollect(False)
