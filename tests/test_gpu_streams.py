@@ -126,3 +126,45 @@ def test_tile_path_bitmap_equals_verdict(validator, oracle_mod, layout):
                 np.testing.assert_array_equal(bits.astype(bool), verdict.cpu().numpy() != 0)
     finally:
         v.set_layout(LAYOUT_AUTO)
+
+
+def test_window_change_waits_for_other_streams(validator, oracle_mod):
+    """Lane fences are recorded when the context leaves a stream: a batch
+    probed on stream A, then a switch to stream B and a window rebuild there,
+    must still finish against the old window (the rebuild waits on A's lane),
+    and probes after the rebuild see the new one -- on A and on B."""
+    dev = torch.device("cuda", 0)
+    log1, b1 = one_log_two_batches(101)
+    log2, b2 = one_log_two_batches(202)
+    want1 = [oracle_mod.check(log1, rs, nthreads=8)[0] != 0 for rs in b1]
+    want2 = [oracle_mod.check(log2, rs, nthreads=8)[0] != 0 for rs in b2]
+    v = validator
+    sa, sb = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    try:
+        v.ingest_log(log1)
+        ms = [v.marshal(rs) for rs in b1]
+        ups = [upload(dev, m) for m in ms]
+        outs = [(torch.zeros(u["n_txn"], dtype=torch.uint8, device=dev),
+                 torch.zeros((u["n_txn"] + 63) // 64, dtype=torch.int64, device=dev)) for u in ups]
+        torch.cuda.synchronize()
+        v.set_stream(sa.cuda_stream)
+        v.probe_device(probe_struct(ups[0], *outs[0]))
+        v.probe_device(probe_struct(ups[1], *outs[1]))
+        v.set_stream(sb.cuda_stream)      # leaves A: its lane's fence goes onto A
+        v.ingest_log(log2)                # the rebuild on B waits for A's batches
+        ms2 = [v.marshal(rs) for rs in b2]
+        ups2 = [upload(dev, m) for m in ms2]
+        outs2 = [(torch.zeros(u["n_txn"], dtype=torch.uint8, device=dev),
+                  torch.zeros((u["n_txn"] + 63) // 64, dtype=torch.int64, device=dev)) for u in ups2]
+        torch.cuda.synchronize()
+        v.probe_device(probe_struct(ups2[0], *outs2[0]))  # on B
+        v.set_stream(sa.cuda_stream)
+        v.probe_device(probe_struct(ups2[1], *outs2[1]))  # on A, after the rebuild
+        torch.cuda.synchronize()
+        for i in range(2):
+            got = np.maximum(outs[i][0].cpu().numpy(), ms[i]["forced"]) != 0
+            np.testing.assert_array_equal(got, want1[i], err_msg=f"old window batch {i}")
+            got2 = np.maximum(outs2[i][0].cpu().numpy(), ms2[i]["forced"]) != 0
+            np.testing.assert_array_equal(got2, want2[i], err_msg=f"new window batch {i}")
+    finally:
+        v.set_stream(0)
