@@ -215,6 +215,46 @@ def _commit_stream_fold_leg(ev, rows, background):
             "wall_s": wall}, rcs
 
 
+def _protocol_leg(args, golden):
+    """The master's commit protocol (db/toblock.c:4757-4836) replayed natively
+    over the config-1 stream at 1 / 16 / 64 threads (hsc_harness_commit_protocol):
+    per commit a regop_only probe under the commit_lock write lock, a full
+    check outside it when newer commits exist (then the probe again), the
+    writes appended under the lock.  Verdicts: 1 thread = the oracle replay's
+    golden; every thread count checked by workloads.protocol_replay_check
+    against oracle/serial_oracle.c on the log as it stood at each verdict."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    from comdb2_amd import formats as F
+    from comdb2_amd import hsc
+    from comdb2_amd.workloads import SEED_CONFIG1, config1_events, protocol_replay_check
+    ev = config1_events(seed=SEED_CONFIG1, n_txn=args.n_txn_c1)
+    txns = [t for e, t in ev if e == "begin"]
+    out = {}
+    for nth in (1, 16, 64):
+        v = hsc.Validator(0)
+        v.ingest_log(F.LogBuilder().build())
+        e0 = v.end_lsn
+        rc, seq, snap, cend, st = v.commit_protocol(txns, ev, nth)
+        v.close()
+        chk = protocol_replay_check(txns, rc, seq, snap, cend, e0,
+                                    lambda log, rs: oracle.check(log, rs)[0])
+        st["parity_with_oracle"] = chk["mismatches"] == 0
+        st["oracle_checked"] = chk["checked"]
+        st["not_serializable"] = int((rc != 0).sum())
+        if nth == 1 and golden is not None:
+            st["parity_with_oracle_golden"] = golden == {t.name: int(rc[i]) for i, t in enumerate(txns)
+                                                          if t.writes}
+        out[f"threads_{nth}"] = st
+    out["note"] = ("commits_per_s = (commits + aborts) / wall time of the run; regop_* = the "
+                   "regop_only probe under the write lock (answered from the context's published "
+                   "snapshot: no collector queue, no context lock); hold_* = commit_lock write-held "
+                   "time per commit; full_* = full checks (the context's collector batches "
+                   "concurrent ones)")
+    return out
+
+
 def bench_commit_stream(args):
     """Config 1: the tests/tools/serial.c-shaped commit stream (10k txns, 20
     ids x 5 accounts, seed 0xC0FFEE01) replayed through the drop-in entry on
@@ -247,6 +287,8 @@ def bench_commit_stream(args):
     fi, ri = _commit_stream_fold_leg(ev, 1000, False)
     fb["parity_with_oracle_golden"] = parity is not None and rb == rcs and parity
     fi["parity_with_oracle_golden"] = parity is not None and ri == rcs and parity
+    golden = json.load(open(gpath))["rc"] if os.path.exists(gpath) and args.n_txn_c1 == 10_000 else None
+    protocol = _protocol_leg(args, golden)
     steady = None
     if args.c1_steady:
         ev2 = config1_events(seed=SEED_CONFIG1 + 1, n_txn=args.c1_steady)
@@ -272,6 +314,7 @@ def bench_commit_stream(args):
            "stream_wall_s": wall, "parity_with_oracle_golden": parity,
            "cpu_baseline": None if args.no_cpu else commit_stream_cpu_baseline(args),
            "fold_every_1k_commits": {"background": fb, "inline": fi},
+           "commit_protocol": protocol,
            "steady_state": steady,
            "note": "value = commits / (time inside the native check and append calls: "
                    "hip_bdb_osql_serial_check and hsc_window_append_log on prebuilt C structs); "
@@ -296,15 +339,34 @@ def bench_graph(args):
 
     from comdb2_amd import hsc, shard
     from comdb2_amd.workloads import config4_history
-    world = max(1, int(os.environ.get("WORLD_SIZE", "1")))
+    world_env = max(1, int(os.environ.get("WORLD_SIZE", "1")))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("HSC_BENCH_BACKEND", "nccl")
+    if world_env > 1 and args.gpus > 1 and args.gpus != world_env:
+        print(f"bench.py --gpus {args.gpus} under WORLD_SIZE {world_env}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    # without a launcher, --gpus N (devices 0..N-1) / --inproc N (the visible
+    # GPUs round robin): N members of one in-process multi context
+    devs = None
+    if world_env == 1 and (args.gpus > 1 or args.inproc > 1):
+        if backend != "nccl":
+            print("bench.py --config 4 --gpus N: in-process members need the HIP path",
+                  file=sys.stderr, flush=True)
+            sys.exit(2)
+        ndev = torch.cuda.device_count()
+        if args.gpus > 1 and ndev < args.gpus:
+            print(f"bench.py --gpus {args.gpus}: only {ndev} GPU(s) visible", file=sys.stderr, flush=True)
+            sys.exit(2)
+        devs = list(range(args.gpus)) if args.gpus > 1 else [i % ndev for i in range(args.inproc)]
+    world = len(devs) if devs else world_env
     if backend != "nccl":
         local = 0
+    if devs:
+        local = devs[0]
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world_env > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -313,8 +375,14 @@ def bench_graph(args):
                         concurrent_frac=args.c4_concurrent, max_lag=args.c4_max_lag)
     hs = shard.history_shard(h, rank, world)
     dh = shard.device_history(hs, dev)
+    dhs = [dh]
+    if devs:  # every member's key shard on its device
+        dhs += [shard.device_history(shard.history_shard(h, r, world), torch.device("cuda", devs[r]))
+                for r in range(1, world)]
     native = backend == "nccl"  # the sharded step behind the C ABI (hsc_multi_graph_scc)
-    if native and world > 1:
+    if devs:
+        mv = hsc.MultiValidator(devs)
+    elif native and world > 1:
         ids = torch.zeros(hsc.MULTI_ID_BYTES, dtype=torch.uint8, device=dev)
         if rank == 0:
             ids.copy_(torch.frombuffer(bytearray(hsc.MultiValidator.unique_ids()), dtype=torch.uint8))
@@ -330,27 +398,32 @@ def bench_graph(args):
     scc = torch.zeros(max(h.ntxn, 1), dtype=torch.int32, device=dev)
 
     def barrier():
-        if world > 1:
+        if world_env > 1:
             dist.barrier()
 
+    def sync():
+        for d in sorted(set(devs or [local])):
+            torch.cuda.synchronize(d)
+
+    ptrs = [scc.data_ptr()] + [None] * (len(dhs) - 1)
     times, st = [], None
     for k in range(args.warmup + args.steps):
         barrier()
-        torch.cuda.synchronize(dev)
+        sync()
         t0 = time.perf_counter()
         if mv is not None:
-            ss = mv.graph_scc([dh], h.ntxn, [scc.data_ptr()])
+            ss = mv.graph_scc(dhs, h.ntxn, ptrs)
             st = {"build": {"build_ms": ss["build_ms"]}, "scc": ss, "cut_rows": ss["edges"]}
         else:
             scc, st = shard.sharded_scc(g, dh, h.ntxn, dev)
-        torch.cuda.synchronize(dev)
+        sync()
         dt = time.perf_counter() - t0
         barrier()
         if k >= args.warmup:
             times.append(dt)
     dt = torch.tensor([float(np.mean(times))], dtype=torch.float64,
                       device=dev if backend == "nccl" else "cpu")
-    if world > 1:
+    if world_env > 1:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     ms = float(dt.item()) * 1e3
     out = None
@@ -363,7 +436,8 @@ def bench_graph(args):
         # scc word written (5 B); the build's sorts come on top
         B4 = h.nops * 17 + h.ntxn * 5
         out = {"metric": "dependency-graph ops analysed/sec (WR/WW/RW edges + SCC)",
-               "value": h.nops / (ms * 1e-3), "unit": "ops/s", "n_gpus": world,
+               "value": h.nops / (ms * 1e-3), "unit": "ops/s",
+               "n_gpus": len(set(devs)) if devs else world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
                "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
                "dtype": "u32/u64", "data": "synthetic config-4 history (seed 0xC0FFEE04)",
@@ -377,7 +451,10 @@ def bench_graph(args):
                           "scc_cut_ms": st["scc"]["scc_ms"], "rounds": st["scc"]["rounds"],
                           "unsharded_build_ms": fst["build_ms"], "unsharded_scc_ms": fst["scc_ms"],
                           "parity_with_unsharded_gpu": same,
-                          "path": ("hsc_multi_graph_scc (C ABI; RCCL cover all-reduce + cut "
+                          "members": world, "devices": devs or [local],
+                          "path": ("hsc_multi_graph_scc (C ABI; in-process members: cover OR "
+                                   "kernel + peer copies of the cuts)" if devs else
+                                   "hsc_multi_graph_scc (C ABI; RCCL cover all-reduce + cut "
                                    "all-gather across ranks)" if mv is not None else
                                    "shard.sharded_scc over torch.distributed (" + backend + ")"),
                           "phase_ms": st["scc"].get("phase_ms") if mv is not None else None},
@@ -388,13 +465,13 @@ def bench_graph(args):
                             "algorithmic_bytes": B4,
                             "note": "B = ops x 17 B (txn, key, is_write, observed read once) + "
                                     "txns x 5 B (cover byte, scc word); rank 0's step time"}}
-        if world == 1 and not args.no_cpu:
-            out["cpu_baseline"] = graph_cpu_baseline(args)
     (mv if mv is not None else v).close()
-    if world > 1:
+    if world_env > 1:
         dist.barrier()
         dist.destroy_process_group()
     if out is not None:
+        if not args.no_cpu:  # the host's throughput: the same line at every N
+            out["cpu_baseline"] = graph_cpu_baseline(args)
         print(json.dumps(out), flush=True)
 
 
@@ -632,11 +709,13 @@ PROBE_KERNELS = ("k_locate_t", "k_plan_s", "k_join_t", "k_pack_flags",  # narrow
                  "k_pack", "k_probe_delta")  # compact / wide, delta run
 
 
-def pmc_traffic(args):
+def pmc_traffic(args, members=1, device=0):
     """HBM bytes per probe batch from rocprofv3 PMC passes of this same
     workload (`bench.py --pmc-child`: the window and the same ring of distinct
     batches as the timed loop, each probed once, rotating over the same
-    streams), one pass per counter as MI355X_MICROARCH.md
+    streams; members > 1: `--multi-pmc`, the N-member partition on `device`
+    with member 0 probing its routed share of two batches), one pass per
+    counter as MI355X_MICROARCH.md
     prescribes (FETCH_SIZE takes 3 TCC slots, WRITE_SIZE 2).  FETCH_SIZE /
     WRITE_SIZE are KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide
     coalesced read, so read bytes = 2 x 1024 x FETCH_SIZE, write bytes = 1024 x
@@ -656,11 +735,20 @@ def pmc_traffic(args):
                "csv", "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__),
                "--pmc-child", "--config", str(args.config), "--n-commits", str(args.n_commits),
                "--n-txn", str(args.n_txn), "--c3-writes", str(args.c3_writes),
-               "--c5-keys", str(args.c5_keys), "--ring-gb", str(args.ring_gb),
-               "--streams", str(args.streams)] + (["--compact-wide"] if args.compact_wide else [])
+               "--c5-keys", str(args.c5_keys), "--streams", str(args.streams)]
+        cmd += (["--compact-wide"] if args.compact_wide else [])
+        if members > 1:
+            cmd += ["--multi-pmc", str(members), "--pmc-device", str(device), "--batches", "2",
+                    "--ring-gb", "0"]
+        else:
+            cmd += ["--ring-gb", str(args.ring_gb)]
+        # the child is a one-process run whatever launched this one
+        env = {k: v for k, v in os.environ.items()
+               if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                            "ROLE_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
         print(f"[bench] pmc pass {ctr}", file=sys.stderr, flush=True)
         try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
             path = os.path.join(d, "run_counter_collection.csv")
             if r.returncode != 0 or not os.path.exists(path):
                 out["error"] = f"{ctr}: rc {r.returncode}: {(r.stderr or '')[-300:]}"
@@ -712,22 +800,37 @@ def bench_multi(args):
     import torch.distributed as dist
 
     from comdb2_amd import hsc, shard
-    from comdb2_amd.workloads import SEED_CONFIG2, config2, config2_device_window
+    from comdb2_amd.workloads import (SEED_CONFIG2, config2, config2_rank_window, config5_log,
+                                      lsn_to_index)
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    inproc = world_env == 1 and not args.rank_path
-    if inproc:
+    # --pmc-child --multi-pmc N: the rocprofv3 counter pass of member 0's
+    # probes (pmc_traffic): N members in this process on one device, every
+    # ring batch's routed share probed once by member 0
+    pmc_child = bool(args.pmc_child and args.multi_pmc > 1)
+    inproc = pmc_child or (world_env == 1 and not args.rank_path)
+    traffic = None
+    if inproc and not pmc_child:
+        ndev = torch.cuda.device_count()  # (does not initialise the GPU on this image)
+        N = args.gpus if args.gpus > 1 else args.inproc
+        if args.gpus > 1 and ndev < N:
+            print(f"bench.py --gpus {N}: only {ndev} GPU(s) visible", file=sys.stderr, flush=True)
+            sys.exit(2)
+    else:
+        N = args.multi_pmc if pmc_child else world_env
+    if (not pmc_child and not args.no_pmc and args.config in (2, 3) and (inproc or rank == 0)):
+        # member 0's HBM bytes per step, before this process touches the GPU
+        # (under torchrun the other ranks wait for rank 0 at the rendezvous)
+        traffic = pmc_traffic(args, members=N, device=local if not inproc else 0)
+    if pmc_child:
+        devs = [args.pmc_device] * N
+        v = hsc.MultiValidator(devs)
+        mine = list(range(N))
+        dev_of = {g: torch.device("cuda", devs[g]) for g in mine}
+    elif inproc:
         ndev = torch.cuda.device_count()
-        if args.gpus > 1:
-            N = args.gpus
-            if ndev < N:
-                print(f"bench.py --gpus {N}: only {ndev} GPU(s) visible", file=sys.stderr, flush=True)
-                sys.exit(2)
-            devs = list(range(N))
-        else:
-            N = args.inproc
-            devs = [i % ndev for i in range(N)]
+        devs = list(range(N)) if args.gpus > 1 else [i % ndev for i in range(N)]
         v = hsc.MultiValidator(devs)
         mine = list(range(N))
         dev_of = {g: torch.device("cuda", devs[g]) for g in mine}
@@ -757,15 +860,18 @@ def bench_multi(args):
 
     T = args.n_txn
     rows = {}  # member -> (gid, words, lsn)
+    seg_vals = {}  # member -> its written int64 values in its commit order (configs 2 / 5: the log)
     if args.config == 2:
         value_bits = 40
         assert v.register_group("t1", 0, 9) == 0
-        for g in mine:
-            c2 = config2(seed=SEED_CONFIG2, n_commits=args.n_commits, n_txn=T, rank=g, world=N,
-                         build_log=False)
-            rows[g] = config2_device_window(c2)
-            end_lsn = c2.params["end_lsn"]
-            first_rs = c2.readsets
+        c2 = config2(seed=SEED_CONFIG2, n_commits=args.n_commits, n_txn=T, rank=mine[0], world=N,
+                     build_log=False)
+        end_lsn = c2.params["end_lsn"]
+        first_rs = c2.readsets
+        c2 = None
+        for g in mine:  # (the same rows as config2(rank=g), without its read sets)
+            gid_, words_, lsn_, seg_vals[g] = config2_rank_window(SEED_CONFIG2, args.n_commits, g, N)
+            rows[g] = (gid_, words_, lsn_)
         more_rs = lambda bi: config2(seed=SEED_CONFIG2 + 7919 * bi, n_commits=args.n_commits,
                                      n_txn=T, rank=0, world=N, build_log=False).readsets
         sp_g, sp_w = shard.int64_splitter_keys([j << value_bits for j in range(1, N)], 2)
@@ -781,6 +887,7 @@ def bench_multi(args):
             c5 = config5_scaled(seed=SEED_CONFIG5, keys_per_gpu=args.c5_keys, n_txn=T, rank=g,
                                 world=N)
             segs[g] = (c5.keys, c5.lsn)
+            seg_vals[g] = c5.keys
             end_lsn = c5.end_lsn
             first_rs = c5.readsets
             range_keys = c5.range_keys
@@ -834,6 +941,23 @@ def bench_multi(args):
                     f"composite-key pieces at work quantiles (hot groups cut)")
         data = "synthetic (config 3 generator, seed 0xC0FFEE03, weak scaling per member)"
         groups = c3.groups
+    # the CPU baseline's log (rank 0): every record after the oldest snapshot
+    # of owner 0's read sets -- configs 2 / 5: the members' writes from local
+    # commit c_start on, gathered across ranks (config 3: the global arrays)
+    want_cpu = not args.no_cpu and not pmc_child
+    tails, c_start = None, 0
+    if want_cpu and args.config in (2, 5):
+        K5 = 10
+        snap0 = np.asarray(first_rs.snap[:T], np.uint64)
+        gc0 = int((int(lsn_to_index(snap0.min())) - (K5 + 2)) // (K5 + 3))  # its regop's commit
+        c_start = max(0, gc0) // N
+        mine_tail = {g: np.ascontiguousarray(seg_vals[g][c_start * K5:]) for g in mine}
+        if inproc:
+            tails = [mine_tail[g] for g in range(N)]
+        else:
+            tails = [None] * N
+            dist.all_gather_object(tails, mine_tail[rank])
+    seg_vals = None
     v.set_splitters(sp_g, sp_w)
     for i, g in enumerate(mine):
         gid, words, lsn = rows[g]
@@ -878,6 +1002,9 @@ def bench_multi(args):
             b["bytes"] = sum(int(b[k].numel() * b[k].element_size())
                              for k in ("lo", "hi", "gid", "snap", "txn", "lock_table", "lock_snap",
                                        "lock_txn"))
+            if pmc_child:
+                per[g] = {"routed": b}
+                continue
             m = v.marshal(shares[g])
             d = upload_batch(torch, dv, m)
             d["bits"] = torch.zeros((T + 63) // 64, dtype=torch.int64, device=dv)
@@ -894,6 +1021,16 @@ def bench_multi(args):
     NB = len(batches)
     ob = batches[0][mine[0]]["routed"]["owner_base"]
     sync_all()
+    if pmc_child:
+        # counted by the parent's rocprofv3 --pmc pass: member 0 probes its
+        # routed share of every ring batch once (the kernels of its step's probe)
+        m0 = v.member(0)
+        for i in range(NB):
+            b = batches[i][0]["routed"]
+            m0.probe_device(probe_struct(hsc, b, b["verdict"], None, N * TP))
+        m0.synchronize()
+        v.close()
+        return
 
     # each batch's call arguments built once: a step is one foreign call (the
     # Python list + ctypes array per call cost ~30 us, more than the C enqueue)
@@ -1032,21 +1169,54 @@ def bench_multi(args):
             "unit": "GB/s",
             "frac": B / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
             "frac_1lane": B / (serial / args.steps) / 1e9 / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": traffic.get("bytes_per_batch") if traffic else None,
+            "measured_frac": (traffic["bytes_per_batch"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                              if traffic and traffic.get("bytes_per_batch") else None),
             "algorithmic_bytes": B,
             "note": "B = member 0's probe-phase bytes (SURVEY 8(d): its window keys, the ranges "
                     "routed to it, the global batch's verdict bits); with members sharing a GPU "
-                    "(--inproc rehearsal) the GPU runs every member's B in one step",
+                    "(--inproc rehearsal) the GPU runs every member's B in one step.  traffic = "
+                    "member 0's probe kernels' FETCH_SIZE + WRITE_SIZE bytes per batch "
+                    "(rocprofv3 --pmc passes of bench.py --pmc-child --multi-pmc N: the same "
+                    "partition, member 0 probing its routed share of each batch)",
         },
         "cpu_baseline": None,
     }
+    if traffic:
+        out["roofline"]["traffic_detail"] = traffic
     if inproc and args.config == 2 and not args.no_api:
         out["api"] = multi_api_leg(hsc, v, first_rs.subset(np.arange(0, T)), v0)
-    if rank == 0:
-        print(json.dumps(out), flush=True)
     v.close()
     if not inproc:
         dist.destroy_process_group()
+    if want_cpu and rank == 0:
+        # the reference algorithm over the N-times larger log, owner 0's read
+        # sets (an evenly spaced sample), against the merged GPU verdicts
+        cpus = box_cpus()
+        threads = args.cpu_threads or cpus["threads"]
+        share0 = first_rs.subset(np.arange(0, T))
+        print(f"[bench] cpu baseline on {threads} threads ({cpus})", file=sys.stderr, flush=True)
+        if args.config == 3:
+            from comdb2_amd.workloads import config3_log
+            c0 = log_tail_commit(c3.commit_lsn, share0.snap)
+            log = config3_log(c3, from_commit=c0)
+            note = (f" (the global log's tail from commit {c0} of {len(c3.commit_lsn)}: every "
+                    f"record after the oldest snapshot of owner 0's read sets)")
+        else:
+            log = config5_log(tails, keys_per_commit=10, commit_base=c_start)
+            note = (f" (the global log of all {N} members' writes from global commit "
+                    f"{c_start * N} on: every record after the oldest snapshot of owner 0's "
+                    f"read sets)")
+        tails = None
+        cpu = cpu_baseline(log, share0, v0, threads, args.cpu_seconds, log_note=note)
+        cpu["host"] = cpus
+        cpu["read_sets"] = "owner 0's share of the global batch (member 0's merged verdicts)"
+        out["cpu_baseline"] = cpu
+        out["parity"] = {"kind": "owner 0's merged verdicts vs oracle/serial_oracle.c on the "
+                                 "cpu_baseline sample (the global log)",
+                         "equal": bool(cpu["parity_with_gpu"] and cpu["single_core"]["parity_with_gpu"])}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
 
 
 def multi_api_leg(hsc, v, rs, want):
@@ -1121,6 +1291,8 @@ def main():
     ap.add_argument("--no-api", action="store_true",
                     help="skip the drop-in entry leg (hip_serial_check_batch end to end)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--multi-pmc", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-device", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--wide", action="store_true", help="force the wide window layout")
     ap.add_argument("--compact-wide", action="store_true",
                     help="compact windows: probe through the wide tile pipeline instead of "
@@ -1172,7 +1344,7 @@ def main():
     if args.config == 1:
         return bench_commit_stream(args)
     if (int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.gpus > 1 or args.inproc > 1
-            or args.rank_path):
+            or args.rank_path or args.multi_pmc > 1):
         # the multi context runs more streams per process than HIP's default 4
         # hardware queues (per member: its lanes' streams, its small-batch
         # slots; RCCL's): with 4, streams share queues and serialise (r05ae:

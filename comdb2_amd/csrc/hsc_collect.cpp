@@ -261,6 +261,10 @@ int hsc_collector_check(hsc_collector *k, void *ranges, unsigned int *file, unsi
 {
     if (!ranges) return 0;  // bdb_osql_serial_check: nothing read -> serializable
     if (!k) return 1;
+    // regop_only: answered from the context's published snapshot in the
+    // caller's thread, never queued behind full passes (db/toblock.c:4779-4785
+    // holds the commit_lock write lock around it)
+    if (regop_only) return hsc::ctx_regop_probe(k->ctx, ranges, file, offset);
     hsc_currangearr *a = (hsc_currangearr *)ranges;
     Req r;
     r.ranges = ranges;

@@ -400,6 +400,14 @@ struct hsc_ctx {
     } lg;
     bool lg_rule = false;  // every record LSN of the window is in lg (DB_SET rule on)
     uint64_t last_append_lsn = 0;
+    // The regop_only answer's inputs (end_lsn, max_commit, poison_regop,
+    // lg_rule), republished by MuGuard whenever a mutating entry releases mu
+    // and read lock-free by the regop_only probes (a seqlock: odd while a
+    // writer stores).  db/toblock.c:4779-4785 runs that probe under the
+    // commit_lock write lock, so it must not queue or wait for mu.
+    std::atomic<uint64_t> rg_seq{0}, rg_end{0}, rg_max{0}, rg_poison{0};
+    std::atomic<uint32_t> rg_lgrule{0};
+    std::atomic<uint64_t> rg_fast{0}, rg_slow{0};  // regop probes answered without / with mu
     // incremental window (hsc_delta.hip): writes committed after the last
     // build, kept on the device as a sorted delta run probed beside the main
     // window; live = a built window takes appends into the delta
@@ -664,4 +672,64 @@ int multi_flush_appends(hsc_ctx *f, bool lazy);
 int multi_check_stage(hsc_ctx *f, Stage &st, int *rc_out, std::unique_lock<std::mutex> *lk = nullptr);
 void multi_sync_dict(hsc_ctx *f);
 void multi_destroy(hsc_ctx *f);
+
+// Publish the regop_only inputs (caller holds c->mu; the only writer).
+inline void ctx_publish_regop(hsc_ctx *c)
+{
+    const uint64_t s = c->rg_seq.load(std::memory_order_relaxed);
+    c->rg_seq.store(s + 1, std::memory_order_relaxed);
+    std::atomic_thread_fence(std::memory_order_release);
+    c->rg_end.store(c->end_lsn, std::memory_order_relaxed);
+    c->rg_max.store(c->max_commit, std::memory_order_relaxed);
+    c->rg_poison.store(c->poison_regop, std::memory_order_relaxed);
+    c->rg_lgrule.store(c->lg_rule ? 1u : 0u, std::memory_order_relaxed);
+    c->rg_seq.store(s + 2, std::memory_order_release);
+}
+
+// The published (end, max commit, poison, lg_rule), consistent with each other.
+inline void ctx_read_regop(const hsc_ctx *c, uint64_t *end, uint64_t *mx, uint64_t *po, uint32_t *lg)
+{
+    for (;;) {
+        const uint64_t s1 = c->rg_seq.load(std::memory_order_acquire);
+        if (s1 & 1) {
+            __builtin_ia32_pause();
+            continue;
+        }
+        *end = c->rg_end.load(std::memory_order_relaxed);
+        *mx = c->rg_max.load(std::memory_order_relaxed);
+        *po = c->rg_poison.load(std::memory_order_relaxed);
+        *lg = c->rg_lgrule.load(std::memory_order_relaxed);
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (c->rg_seq.load(std::memory_order_relaxed) == s1) return;
+    }
+}
+
+// regop_only (bdb/serializable.c:382-416, 531-534) without mu: S at or past
+// the end -> 0 (DB_SET finds nothing); a committed write txn (or an
+// unreadable regop) after S -> 1, whether or not S is a record LSN; else 0,
+// unless the DB_SET-on-a-non-record rule needs the log's record LSNs: -1
+// (the caller takes mu and answers from the log).
+inline int ctx_regop_fast(const hsc_ctx *c, uint64_t S)
+{
+    uint64_t end, mx, po;
+    uint32_t lg;
+    ctx_read_regop(c, &end, &mx, &po, &lg);
+    if (S >= end) return 0;
+    if (mx > S || po > S) return 1;
+    return lg ? -1 : 0;
+}
+
+// std::lock_guard on c->mu for the entries that change the window: the
+// regop_only snapshot is republished before mu is released.
+class MuGuard {
+  public:
+    explicit MuGuard(hsc_ctx *c) : c_(c), g_(c->mu) {}
+    ~MuGuard() { ctx_publish_regop(c_); }
+    MuGuard(const MuGuard &) = delete;
+    MuGuard &operator=(const MuGuard &) = delete;
+
+  private:
+    hsc_ctx *c_;
+    std::lock_guard<std::mutex> g_;
+};
 }  // namespace hsc

@@ -3184,7 +3184,7 @@ int hsc_set_stream(hsc_ctx *c, void *st)
 {
     if (!c) return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     hipStream_t ns = st ? (hipStream_t)st : c->own_stream;
     // small batches launched on the old stream may still read the delta run
     // a later append on the new stream rewrites: let them finish first
@@ -3202,7 +3202,7 @@ const char *hsc_last_error(hsc_ctx *c) { return c ? c->err.c_str() : "null conte
 int hsc_window_reset(hsc_ctx *c)
 {
     if (!c) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     clear_window(c);
     c->phys.clear();
     c->end_lsn = 0;
@@ -3220,7 +3220,7 @@ static int ingest_log_locked(hsc_ctx *c, const hsc_llog *log)
 int hsc_window_ingest_log(hsc_ctx *c, const hsc_llog *log)
 {
     if (!c || !log) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     c->phys.clear();  // a decoded log brings no physical records for later walks
     return ingest_log_locked(c, log);
 }
@@ -3228,7 +3228,7 @@ int hsc_window_ingest_log(hsc_ctx *c, const hsc_llog *log)
 int hsc_window_append(hsc_ctx *c, const hsc_write *w, size_t n)
 {
     if (!c || (!w && n)) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     if (!c->host_only) (void)hipSetDevice(c->device);
     if (c->multi && multi_adopted(c))  // the members hold the window: append to them
         return fail(c, HSC_ESTATE, "append to an adopted multi context: append to its members");
@@ -3261,7 +3261,7 @@ int hsc_window_append(hsc_ctx *c, const hsc_write *w, size_t n)
 int hsc_window_append_log(hsc_ctx *c, const hsc_llog *log)
 {
     if (!c || !log) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     if (!c->host_only) (void)hipSetDevice(c->device);
     if (c->multi && multi_adopted(c))
         return fail(c, HSC_ESTATE, "append to an adopted multi context: append to its members");
@@ -3283,7 +3283,7 @@ size_t hsc_window_delta_rows(hsc_ctx *c) { return c ? c->dn + c->fn + c->pend_n 
 int hsc_set_fold(hsc_ctx *c, size_t rows, int background)
 {
     if (!c || rows > kDeltaCap) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     c->fold_rows = rows ? rows : kDeltaCap / 2;
     c->fold_bg = background != 0;
     return HSC_OK;
@@ -3292,7 +3292,7 @@ int hsc_set_fold(hsc_ctx *c, size_t rows, int background)
 int hsc_fold_stats(hsc_ctx *c, uint64_t out[4])
 {
     if (!c || !out) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     out[0] = c->folds_started;
     out[1] = c->folds_swapped;
     out[2] = c->folds_inline;
@@ -3303,7 +3303,7 @@ int hsc_fold_stats(hsc_ctx *c, uint64_t out[4])
 int hsc_set_paths(hsc_ctx *c, unsigned flags)
 {
     if (!c || (flags & ~(unsigned)HSC_PATH_ALL)) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     if (!c->host_only && (flags & HSC_PATH_NO_SMALL) && !c->no_small && wait_small(c) != hipSuccess)
         return fail(c, HSC_EDEVICE, "set_paths: a small batch did not finish");
     if (((flags ^ c->paths) & (HSC_PATH_NO_PACKED_SORT | HSC_PATH_TILE_DIR)) && c->live) {
@@ -3319,7 +3319,7 @@ int hsc_set_paths(hsc_ctx *c, unsigned flags)
 int hsc_append_stats(hsc_ctx *c, uint64_t out[3])
 {
     if (!c || !out) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     out[0] = c->pend_appends;
     out[1] = c->pend_merges;
     out[2] = c->pend_n;
@@ -3329,7 +3329,7 @@ int hsc_append_stats(hsc_ctx *c, uint64_t out[3])
 int hsc_window_set_end(hsc_ctx *c, uint64_t end_lsn)
 {
     if (!c) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     c->end_lsn = end_lsn;
     return HSC_OK;
 }
@@ -3350,7 +3350,7 @@ static int decode_locked(hsc_ctx *c, const hsc_raw_log *raw, bool reset)
 int hsc_decode_log(hsc_ctx *c, const hsc_raw_log *raw, const hsc_llog **out)
 {
     if (!c || !raw || !out || !raw_args_ok(raw)) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     int rc = decode_locked(c, raw, false);
     if (rc) return rc;
     *out = &c->decoded.llog;
@@ -3360,7 +3360,7 @@ int hsc_decode_log(hsc_ctx *c, const hsc_raw_log *raw, const hsc_llog **out)
 int hsc_window_ingest_raw(hsc_ctx *c, const hsc_raw_log *raw)
 {
     if (!c || !raw || !raw_args_ok(raw)) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     int rc = decode_locked(c, raw, true);  // a new log: walks see only its records
     if (rc) return rc;
     return ingest_log_locked(c, &c->decoded.llog);
@@ -3370,7 +3370,7 @@ int hsc_decode_serial(hsc_ctx *c, const hsc_serial_msgs *m, const hsc_readsets *
 {
     if (!c || !m || !out || (m->nmsg && (!m->buf || !m->off || !m->len)) || m->nmsg > 0x7FFFFFFF)
         return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     std::string err;
     int rc = decode_serial_msgs(m, c->wire, err);
     if (rc) return fail(c, rc, err.c_str());
@@ -3393,7 +3393,7 @@ int hsc_check_serial(hsc_ctx *c, const hsc_serial_msgs *m, int *rc_out)
 int hsc_window_build(hsc_ctx *c)
 {
     if (!c) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     if (!c->host_only) (void)hipSetDevice(c->device);
     return ensure_built(c);
 }
@@ -3401,7 +3401,7 @@ int hsc_window_build(hsc_ctx *c)
 int hsc_register_group(hsc_ctx *c, const char *tbname, int idxnum, int keylen)
 {
     if (!c || !tbname || keylen < 0 || keylen > kMaxWords * 8) return HSC_EINVAL;
-    std::lock_guard<std::mutex> lk(c->mu);
+    MuGuard lk(c);
     int tid = table_id_or_add(c, tbname);
     const int g = group_id_or_add(c, tid, idxnum, keylen);
     if (c->multi) multi_sync_dict(c);  // members keep the same table ids and gids
@@ -3415,7 +3415,7 @@ int hsc_window_ingest_device(hsc_ctx *c, size_t n, int words, const uint32_t *gi
     if (!c || words < 1 || words > kMaxWords || (n && (!gid || !key_words || !lsn)))
         return HSC_EINVAL;
     if (n >= 0xFFFFFFFFull) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     if (!c->host_only) (void)hipSetDevice(c->device);
     clear_window(c);
     c->phys.clear();
@@ -3446,7 +3446,7 @@ int hsc_set_layout(hsc_ctx *c, int layout)
     if (!c || layout < HSC_LAYOUT_AUTO || layout > HSC_LAYOUT_COMPACT_WIDE ||
         layout == HSC_LAYOUT_NARROW || layout == HSC_LAYOUT_COMPACT)
         return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     const bool rebuild = (c->layout == HSC_LAYOUT_WIDE) != (layout == HSC_LAYOUT_WIDE);
     c->layout = layout;
     if (rebuild) {
@@ -3468,8 +3468,9 @@ int hsc_window_tile_key_words(hsc_ctx *c) { return c && c->compact && c->ctiles 
 int hsc_window_words(hsc_ctx *c) { return c ? c->W : 0; }
 int hsc_window_sort_path(hsc_ctx *c) { return !c ? 0 : c->packed_sort ? 1 : c->code_sorted ? 2 : 0; }
 size_t hsc_window_keys(hsc_ctx *c) { return c ? c->n : 0; }
-uint64_t hsc_window_end(hsc_ctx *c) { return c ? c->end_lsn : 0; }
-uint64_t hsc_window_max_commit(hsc_ctx *c) { return c ? c->max_commit : 0; }
+// (the published values: callers read them without the context lock)
+uint64_t hsc_window_end(hsc_ctx *c) { return c ? c->rg_end.load(std::memory_order_acquire) : 0; }
+uint64_t hsc_window_max_commit(hsc_ctx *c) { return c ? c->rg_max.load(std::memory_order_acquire) : 0; }
 
 int hsc_table_id(hsc_ctx *c, const char *tbname)
 {
@@ -3504,7 +3505,7 @@ int hsc_table_max(hsc_ctx *c, uint64_t *out, int n)
 int hsc_merge_table_max(hsc_ctx *c, const uint64_t *in, int n)
 {
     if (!c || n < 0 || (n && !in) || n > (int)c->table_names.size()) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     for (int t = 0; t < n; ++t) {
         c->h_table_max[t] = std::max(c->h_table_max[t], in[t]);
         c->max_commit = std::max(c->max_commit, in[t]);
@@ -3532,7 +3533,7 @@ int hsc_merge_table_max(hsc_ctx *c, const uint64_t *in, int n)
 int hsc_marshal_readsets(hsc_ctx *c, const hsc_readsets *rs, const hsc_marshalled **out)
 {
     if (!c || !rs || !out) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     if (!c->host_only) (void)hipSetDevice(c->device);
     int rc = ensure_built(c);
     if (rc) return rc;
@@ -3545,7 +3546,7 @@ int hsc_marshal_arrs(hsc_ctx *c, void *const *ranges, const uint64_t *snaps, int
                      const hsc_marshalled **out)
 {
     if (!c || n < 0 || (n && (!ranges || !snaps)) || !out) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     if (!c->host_only) (void)hipSetDevice(c->device);
     int rc = ensure_built(c);
     if (rc) return rc;
@@ -3564,7 +3565,7 @@ long hsc_window_export(hsc_ctx *c, int all_versions, uint32_t *gid, uint64_t *ke
     if (c->host_only) return HSC_EDEVICE;
     const bool copy = gid || key_words || lsn;
     if (copy && !(gid && key_words && lsn)) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     (void)hipSetDevice(c->device);
     if (c->live && (c->dn || !c->app_gid.empty())) {  // the snapshot includes the delta run
         c->merge_pending = true;
@@ -3592,7 +3593,7 @@ int hsc_rw_edges(hsc_ctx *c, const hsc_readsets *rs, size_t *n_pairs, const uint
 {
     if (!c || !rs || !n_pairs || !txn || !writer_lsn) return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     (void)hipSetDevice(c->device);
     if (c->dn || !c->app_gid.empty()) {  // pairs need every version: fold the delta in first
         c->merge_pending = true;
@@ -3713,7 +3714,7 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
 {
     if (!c || !rs || !out || rs->ntxn < 0) return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     (void)hipSetDevice(c->device);
     const int T = rs->ntxn;
     const size_t nr = T ? (size_t)rs->txn_off[T] : 0;
@@ -3854,7 +3855,7 @@ int hsc_coalesce_readsets(hsc_ctx *c, const hsc_readsets *rs, hsc_coalesced *out
 int hsc_check_readsets(hsc_ctx *c, const hsc_readsets *rs, int *rc_out)
 {
     if (!c || !rs || (!rc_out && rs->ntxn)) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     if (!c->host_only) (void)hipSetDevice(c->device);
     int rc = ensure_built(c);
     if (!rc) {
@@ -4045,7 +4046,7 @@ static bool check_batch_assembled(hsc_ctx *c, void *const *ranges, PreMarshal *c
     give_back();  // the slot owns the columns now (its arena swapped in)
     if (const hipError_t e = small_fire(c, k); e != hipSuccess) {
         c->small[k].busy.store(false, std::memory_order_release);
-        std::lock_guard<std::mutex> g(c->mu);
+        MuGuard g(c);
         for (int i = 0; i < n; ++i) rc_out[i] = 1;
         *rc = fail(c, HSC_EDEVICE, "small batch launch", e);
         return true;
@@ -4054,7 +4055,7 @@ static bool check_batch_assembled(hsc_ctx *c, void *const *ranges, PreMarshal *c
     hipError_t herr = hipSuccess;
     r = small_wait(c, k, s, rc_out, &why, &herr);
     if (r != HSC_OK) {
-        std::lock_guard<std::mutex> g(c->mu);
+        MuGuard g(c);
         for (int i = 0; i < n; ++i) rc_out[i] = 1;
         *rc = fail(c, r, why, herr);
         return true;
@@ -4067,6 +4068,27 @@ static int check_batch(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, 
                        unsigned int *offset, int regop_only, int n, int *rc_out)
 {
     if (!c || n < 0 || (n && (!ranges || !rc_out)) || (!file) != (!offset)) return HSC_EINVAL;
+    if (regop_only && n > 0) {
+        // every element from the published snapshot, without mu (the locked
+        // path below only when some snapshot needs the log's record LSNs)
+        bool all = true;
+        for (int i = 0; i < n && all; ++i) {
+            const hsc_currangearr *a = (const hsc_currangearr *)ranges[i];
+            if (!a) {
+                rc_out[i] = 0;
+                continue;
+            }
+            const unsigned int f = file ? file[i] : a->file, o = offset ? offset[i] : a->offset;
+            const int r = ctx_regop_fast(c, ((uint64_t)f << 32) | o);
+            if (r < 0) all = false;
+            rc_out[i] = r;
+        }
+        if (all) {
+            c->rg_fast.fetch_add((uint64_t)n, std::memory_order_relaxed);
+            return HSC_OK;
+        }
+        c->rg_slow.fetch_add((uint64_t)n, std::memory_order_relaxed);
+    }
     static const bool assemble = getenv("HSC_NO_PRE_ASSEMBLE") == nullptr;  // (A/B diagnostics)
     if (assemble && pre && !regop_only && n > 0) {
         int rc = HSC_OK;
@@ -4138,6 +4160,34 @@ static int check_batch(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, 
     return rc;
 }
 
+}  // extern "C"
+
+int hsc::ctx_regop_probe(hsc_ctx *c, void *ranges, unsigned int *file, unsigned int *offset)
+{
+    if (!ranges) return 0;
+    hsc_currangearr *a = (hsc_currangearr *)ranges;
+    const unsigned int f = file ? *file : a->file, o = offset ? *offset : a->offset;
+    const int r = ctx_regop_fast(c, ((uint64_t)f << 32) | o);
+    if (r >= 0) {
+        c->rg_fast.fetch_add(1, std::memory_order_relaxed);
+        return r;  // (regop_only leaves *file, *offset as they are)
+    }
+    int rc_out = 1;
+    void *arr[1] = {ranges};
+    const int rc = check_batch(c, arr, nullptr, file, offset, 1, 1, &rc_out);
+    return rc ? 1 : rc_out;  // errors are "not serializable"
+}
+
+extern "C" {
+
+int hsc_regop_stats(hsc_ctx *c, uint64_t out[2])
+{
+    if (!c || !out) return HSC_EINVAL;
+    out[0] = c->rg_fast.load(std::memory_order_relaxed);
+    out[1] = c->rg_slow.load(std::memory_order_relaxed);
+    return HSC_OK;
+}
+
 int hsc_small_stats(hsc_ctx *c, hsc_small_stats_t *out)
 {
     if (!c || !out) return HSC_EINVAL;
@@ -4167,7 +4217,7 @@ int hsc_batch_stats(hsc_ctx *c, hsc_batch_stats_t *out)
 int hsc_set_threads(hsc_ctx *c, int n)
 {
     if (!c || n < 0) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     c->threads = n ? std::min(n, 256) : default_threads();
     return HSC_OK;
 }
@@ -4197,6 +4247,7 @@ int hip_bdb_osql_serial_check(void *ctx, void *ranges, unsigned int *file, unsig
 {
     if (!ranges) return 0;
     hsc_ctx *c = (hsc_ctx *)ctx;
+    if (c && regop_only) return ctx_regop_probe(c, ranges, file, offset);  // never queued
     if (c && c->autocollect.load(std::memory_order_relaxed))
         if (hsc_collector *k = auto_collector(c)) return hsc_collector_check(k, ranges, file, offset, regop_only);
     int rc_out = 1;
@@ -4208,7 +4259,7 @@ int hip_bdb_osql_serial_check(void *ctx, void *ranges, unsigned int *file, unsig
 int hsc_probe_device(hsc_ctx *c, const hsc_probe_batch *b)
 {
     if (!c || !b) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     if (!c->host_only) (void)hipSetDevice(c->device);
     if (c->dirty) return fail(c, HSC_ESTATE, "window not built");
     return probe(c, b);
@@ -4218,7 +4269,7 @@ int hsc_pack_verdicts(hsc_ctx *c, const uint8_t *verdict, size_t n_txn, uint64_t
 {
     if (!c || (n_txn && (!verdict || !bitmap)) || n_txn > 0xFFFFFFFFull) return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     if (!c->host_only) (void)hipSetDevice(c->device);
     HIPCHK(c, launch_pack(verdict, (uint32_t)n_txn, bitmap, c->stream));
     return HSC_OK;
@@ -4228,7 +4279,7 @@ int hsc_or_bitmaps(hsc_ctx *c, const uint64_t *parts, int nparts, size_t words, 
 {
     if (!c || nparts < 1 || (words && (!parts || !out))) return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     (void)hipSetDevice(c->device);
     HIPCHK(c, launch_or_bitmaps(parts, nparts, words, out, c->stream));
     return HSC_OK;
@@ -4356,7 +4407,7 @@ extern "C" {
 int hsc_dep_graph_scc(hsc_ctx *c, const hsc_history *h, uint32_t *scc_out, hsc_graph_stats *st)
 {
     if (!c || !h || (h->ntxn && !scc_out)) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     float build_ms = 0;
     int rc = graph_upload_build(c, h, true, &build_ms);
     if (rc) return rc;
@@ -4390,7 +4441,7 @@ int hsc_dep_graph_scc(hsc_ctx *c, const hsc_history *h, uint32_t *scc_out, hsc_g
 int hsc_dep_graph_build(hsc_ctx *c, const hsc_history *h, int flags, hsc_graph_stats *st)
 {
     if (!c || !h) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     float build_ms = 0;
     int rc = graph_upload_build(c, h, (flags & HSC_GRAPH_FULL) != 0, &build_ms,
                                 (flags & HSC_GRAPH_NO_RW) != 0);
@@ -4408,7 +4459,7 @@ int hsc_dep_graph_build_device(hsc_ctx *c, size_t nops, uint32_t ntxn, const uin
         nops > 0x7FFFFFFFull)
         return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     (void)hipSetDevice(c->device);
     GraphInput in{txn_dev, key_dev, is_write_dev, observed_dev, nops, ntxn};
     in.skip_rw = (flags & HSC_GRAPH_NO_RW) != 0;
@@ -4430,7 +4481,7 @@ int hsc_dep_graph_stage_rw_pairs(hsc_ctx *c, uint32_t nrs, const uint32_t *reads
     if (!c || (nrs && !readset_txn) || (ncommit && (!commit_lsn || !commit_txn)))
         return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     (void)hipSetDevice(c->device);
     for (size_t i = 1; i < ncommit; ++i)
         if (commit_lsn[i] <= commit_lsn[i - 1]) return fail(c, HSC_EINVAL, "commit LSNs not sorted");
@@ -4473,7 +4524,7 @@ int hsc_dep_graph_scc_built(hsc_ctx *c, uint32_t *scc_out, hsc_graph_stats *st)
 {
     if (!c) return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     (void)hipSetDevice(c->device);
     GraphBufs &gb = c->graph;
     const uint32_t nn = c->graph_ntxn;
@@ -4507,7 +4558,7 @@ int hsc_dep_graph_cover(hsc_ctx *c, uint8_t *cover_dev)
 {
     if (!c || (c->graph_ntxn && !cover_dev)) return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     (void)hipSetDevice(c->device);
     HIPCHK(c, graph_cover(c->graph, c->graph_ntxn, cover_dev, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -4519,7 +4570,7 @@ int hsc_dep_graph_cut(hsc_ctx *c, const uint8_t *cover_dev, uint64_t *rows_dev, 
 {
     if (!c || !m || (c->graph_ntxn && !cover_dev)) return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     (void)hipSetDevice(c->device);
     HIPCHK(c, graph_cut(c->graph, cover_dev, m, c->stream));
     const size_t k = std::min(cap, *m);
@@ -4536,7 +4587,7 @@ int hsc_dep_graph_scc_cut(hsc_ctx *c, uint32_t ntxn, const uint8_t *cover_dev,
     if (!c || (ntxn && (!cover_dev || !scc_dev)) || (m && !rows_dev) || m > 0xFFFFFFFFull)
         return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     (void)hipSetDevice(c->device);
     hipStream_t s = c->stream;
     hipEvent_t e1, e2;
@@ -4576,7 +4627,7 @@ int hsc_dep_graph_edges(hsc_ctx *c, uint32_t *src, uint32_t *dst, uint32_t *type
 {
     if (!c || !n) return HSC_EINVAL;
     if (c->host_only) return HSC_EDEVICE;
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     (void)hipSetDevice(c->device);
     GraphBufs &gb = c->graph;
     *n = gb.ne;
@@ -4609,7 +4660,7 @@ void ctx_par_for(hsc_ctx *c, int nwork, const std::function<void(int)> &f) { par
 // 0's W words, then row n - 1's).
 int ctx_edge_keys(hsc_ctx *c, uint32_t *gid, uint64_t *words)
 {
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     if (c->dirty || !c->n || c->host_only) return fail(c, HSC_ESTATE, "no built window");
     (void)hipSetDevice(c->device);
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -4628,7 +4679,7 @@ int ctx_edge_keys(hsc_ctx *c, uint32_t *gid, uint64_t *words)
 // points into the context's own buffer until its next graph call.
 int ctx_graph_cut(hsc_ctx *c, const uint8_t *cover, size_t *m, const uint64_t **rows)
 {
-    std::lock_guard<std::mutex> g(c->mu);
+    MuGuard g(c);
     (void)hipSetDevice(c->device);
     HIPCHK(c, graph_cut(c->graph, cover, m, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -4680,7 +4731,7 @@ int ctx_stage_wait(hsc_ctx *c, Stage &st, int slot, int *rc_out)
         hipError_t herr = hipSuccess;
         const int rc = small_wait(c, slot, c->small[slot].stream, rc_out, &why, &herr);
         if (rc == HSC_OK) return HSC_OK;
-        std::lock_guard<std::mutex> g(c->mu);
+        MuGuard g(c);
         return fail(c, rc, why, herr);
     }
     (void)hipSetDevice(c->device);

@@ -646,6 +646,9 @@ struct PreMarshal;
 PreMarshal *premarshal_new();
 void premarshal_free(PreMarshal *pm);
 bool premarshal(hsc_ctx *c, const hsc_currangearr *a, uint64_t S, PreMarshal *pm);
+// bdb_osql_serial_check(..., regop_only = 1) on one read set: the context's
+// published snapshot without its lock, or the locked path; errors -> 1
+int ctx_regop_probe(hsc_ctx *c, void *ranges, unsigned int *file, unsigned int *offset);
 int check_batch_pre(hsc_ctx *c, void *const *ranges, PreMarshal *const *pre, unsigned int *file,
                     unsigned int *offset, int n, int *rc_out);
 

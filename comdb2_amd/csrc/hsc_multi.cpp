@@ -306,7 +306,7 @@ void multi_sync_dict(hsc_ctx *f)
     Multi *M = f->multi;
     for (int m = 0; m < M->nlocal; ++m) {
         hsc_ctx *c = M->mem[m];
-        std::lock_guard<std::mutex> g(c->mu);
+        MuGuard g(c);
         if (c->table_names.size() != f->table_names.size() || c->groups.size() != f->groups.size())
             c->dict_epoch++;
         c->table_ids = f->table_ids;
@@ -346,7 +346,7 @@ int multi_build(hsc_ctx *f)
     for (int m = 0; m < M->nlocal; ++m) {
         hsc_ctx *c = M->mem[m];
         const int me = M->rank + m;
-        std::lock_guard<std::mutex> g(c->mu);
+        MuGuard g(c);
         (void)hipSetDevice(c->device);
         ctx_clear_window(c);
         c->end_lsn = f->end_lsn;
@@ -405,7 +405,7 @@ int multi_flush_appends(hsc_ctx *f, bool lazy)
     }
     for (int m = 0; m < M->nlocal; ++m) {
         hsc_ctx *c = M->mem[m];
-        std::lock_guard<std::mutex> g(c->mu);
+        MuGuard g(c);
         (void)hipSetDevice(c->device);
         for (size_t t = 0; t < f->h_table_max.size(); ++t)  // (mirrored by a pending tail)
             ctx_raise_table_max(c, (int)t, f->h_table_max[t]);
@@ -552,7 +552,7 @@ static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb,
             MCHK(c, ml.bitmap.ensure(std::max<size_t>(total / 8, 8)));
             b.bitmap = ml.bitmap.as<uint64_t>();
         }
-        std::lock_guard<std::mutex> g(c->mu);
+        MuGuard g(c);
         if (c->dirty) return ctx_fail(c, HSC_ESTATE, "window not built");
         if (c->app_last) MCHK(c, hipStreamWaitEvent(ml.stream, c->app_last, 0));  // its appends
         ml.timed = M->timing;
@@ -1328,7 +1328,7 @@ int hsc_multi_set_splitters(hsc_ctx *f, size_t S, const uint32_t *gid, const uin
     if (!f || !f->multi) return HSC_EINVAL;
     Multi *M = f->multi;
     if (S != (size_t)M->world - 1 || W < 1 || W > kMaxWords || (S && (!gid || !words))) return HSC_EINVAL;
-    std::lock_guard<std::mutex> g(f->mu);
+    MuGuard g(f);
     for (size_t k = 1; k < S; ++k) {  // ascending (equal: an empty piece)
         int c = gid[k - 1] < gid[k] ? -1 : gid[k - 1] > gid[k] ? 1 : 0;
         for (int j = 0; j < W && !c; ++j)
@@ -1350,7 +1350,7 @@ int hsc_multi_adopt(hsc_ctx *f)
 {
     if (!f || !f->multi) return HSC_EINVAL;
     Multi *M = f->multi;
-    std::lock_guard<std::mutex> g(f->mu);
+    MuGuard g(f);
     // the routing of every probe follows the splitters: without them all
     // probes would go to member 0 and the other pieces' keys never be probed
     if (M->world > 1 && !M->sp_given)
@@ -1420,7 +1420,7 @@ int hsc_multi_probe_device(hsc_ctx *f, const hsc_probe_batch *b, int lane)
 {
     if (!f || !f->multi || !b || lane < 0 || lane >= kMultiLanes) return HSC_EINVAL;
     Multi *M = f->multi;
-    std::lock_guard<std::mutex> g(f->mu);
+    MuGuard g(f);
     if (f->dirty) return mfail(f, HSC_ESTATE, "window not built");
     MSource src[kMultiMax] = {};
     for (int m = 0; m < M->nlocal; ++m) {
@@ -1483,7 +1483,7 @@ int hsc_multi_set_transport(hsc_ctx *f, int transport)
 {
     if (!f || !f->multi || transport < HSC_MULTI_DIRECT || transport > HSC_MULTI_LOOPBACK) return HSC_EINVAL;
     Multi *M = f->multi;
-    std::lock_guard<std::mutex> g(f->mu);
+    MuGuard g(f);
     if (M->rccl) return transport == HSC_MULTI_DIRECT ? HSC_OK : mfail(f, HSC_EINVAL, "per-rank context: RCCL");
     for (int L = 0; L < kMultiLanes; ++L)  // nothing of the other form in flight
         for (int m = 0; m < M->nlocal; ++m)
@@ -1499,7 +1499,7 @@ int hsc_multi_probe_routed(hsc_ctx *f, const hsc_probe_batch *b, const uint64_t 
     if (!f || !f->multi || !b || !owner_base || lane < 0 || lane >= kMultiLanes) return HSC_EINVAL;
     Multi *M = f->multi;
     const int N = M->world, NL = M->nlocal;
-    std::lock_guard<std::mutex> g(f->mu);
+    MuGuard g(f);
     if (f->dirty) return mfail(f, HSC_ESTATE, "window not built");
     size_t tb[kMultiMax + 1];
     for (int o = 0; o <= N; ++o) {
@@ -1534,7 +1534,7 @@ int hsc_multi_marshal_routed(hsc_ctx *f, const hsc_readsets *rs, int member, uin
     int rc = hsc_marshal_readsets(f, rs, &m);
     if (rc) return rc;
     Multi *M = f->multi;
-    std::lock_guard<std::mutex> g(f->mu);
+    MuGuard g(f);
     Stage &st = f->stage[0];
     rc = route_host(f, st, M->mst, member, txn_base, nullptr);
     if (rc) return rc;
@@ -1610,7 +1610,7 @@ int hsc_multi_graph_scc(hsc_ctx *f, const hsc_ops_dev *ops, uint32_t ntxn, uint3
     if (!f || !f->multi || !ops || !scc_dev || !scc_dev[0]) return HSC_EINVAL;
     Multi *M = f->multi;
     const int N = M->world, NL = M->nlocal;
-    std::lock_guard<std::mutex> g(f->mu);
+    MuGuard g(f);
     const auto t0 = SteadyClock::now();
     for (int m = 0; m < NL; ++m) MRC(lane_stream(f, M, 0, m));
     const size_t cb = r64(std::max<uint32_t>(ntxn, 1));  // cover bytes, whole u64 words

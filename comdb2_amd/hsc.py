@@ -137,6 +137,21 @@ class BatchStats(C.Structure):
                                           "assemble_ns", "launch_ns", "wait_ns")]
 
 
+class ProtocolTxn(C.Structure):
+    """hsc_protocol_txn: one txn of the commit-protocol harness."""
+    _fields_ = [("arr", _p), ("writes", _p), ("nwrites", C.c_int)]
+
+
+class ProtocolResult(C.Structure):
+    _fields_ = [("seconds", C.c_double), ("commits", C.c_uint64), ("aborts", C.c_uint64),
+                ("regop_probes", C.c_uint64), ("full_checks", C.c_uint64),
+                ("regop_p50_us", C.c_double), ("regop_p99_us", C.c_double),
+                ("regop_p999_us", C.c_double), ("regop_max_us", C.c_double),
+                ("full_p50_us", C.c_double), ("full_p99_us", C.c_double),
+                ("hold_p50_us", C.c_double), ("hold_p99_us", C.c_double),
+                ("commit_p50_us", C.c_double), ("commit_p99_us", C.c_double)]
+
+
 class ConcurrentResult(C.Structure):
     _fields_ = [("seconds", C.c_double), ("calls", C.c_uint64), ("lat_mean_us", C.c_double),
                 ("lat_p50_us", C.c_double), ("lat_p99_us", C.c_double)]
@@ -170,7 +185,7 @@ EXPORTS = [
     "hsc_multi_marshal_routed", "hsc_multi_routed_member", "hsc_multi_enable_timing",
     "hsc_multi_member_probe_ms", "hsc_multi_route_stats", "hsc_multi_graph_scc",
     "hsc_multi_graph_phase_ms",
-    "hsc_marshal_arrs", "hsc_batch_stats",
+    "hsc_marshal_arrs", "hsc_batch_stats", "hsc_regop_stats", "hsc_harness_commit_protocol",
 ]
 MULTI_ID_BYTES = 2 * 128  # hsc_multi_unique_ids: one RCCL id per lane
 
@@ -270,6 +285,9 @@ def load() -> C.CDLL:
         "hsc_harness_concurrent": (C.c_int, [_p, _p, C.POINTER(_p), C.c_int, C.c_int, C.c_int,
                                              C.c_int, C.POINTER(C.c_int),
                                              C.POINTER(ConcurrentResult)]),
+        "hsc_regop_stats": (C.c_int, [_p, _p]),
+        "hsc_harness_commit_protocol": (C.c_int, [_p, _p, C.c_int, _p, C.c_int, C.c_int, _p, _p,
+                                                  _p, _p, C.POINTER(ProtocolResult)]),
         "hsc_window_layout": (C.c_int, [_p]),
         "hsc_batch_stats": (C.c_int, [_p, C.POINTER(BatchStats)]),
         "hsc_marshal_arrs": (C.c_int, [_p, C.POINTER(_p), _p, C.c_int,
@@ -721,6 +739,65 @@ class Validator:
         return {"calls": st.calls, "marshal_us": st.marshal_ns / 1e3 / n,
                 "launch_us": st.launch_ns / 1e3 / n, "wait_us": st.wait_ns / 1e3 / n,
                 "slot_waits": st.slot_waits, "lock_us": st.lock_ns / 1e3 / n}
+
+    def regop_stats(self) -> dict:
+        """regop_only probes answered from the published snapshot / locked."""
+        out = np.zeros(2, np.uint64)
+        self._chk(self.lib.hsc_regop_stats(self.ctx, out.ctypes.data), "hsc_regop_stats")
+        return {"fast": int(out[0]), "locked": int(out[1])}
+
+    def commit_protocol(self, txns, events, nthreads: int):
+        """db/toblock.c:4757-4836 replayed natively (hsc_harness_commit_protocol)
+        by nthreads threads over events [('begin' | 'commit', workloads.Txn)]:
+        snapshots taken at begin, commits through the commit_lock protocol
+        (regop probe under the write lock, full check outside it, append).
+        -> (rc int32[n], commit_seq int64[n], snap u64[n], check_end u64[n],
+        stats dict); txns indexed as in `txns`."""
+        from .formats import DTA_TYPES
+        n = len(txns)
+        idx = {t.name: i for i, t in enumerate(txns)}
+        rs = ReadSets.from_lists([t.reads for t in txns], [0] * n)
+        arrs = NativeCurRangeArrs(rs)
+        keep = []
+        pt = (ProtocolTxn * max(1, n))()
+        ptrs = arrs.pointers()
+        for i, t in enumerate(txns):
+            ws = (_Write * max(1, len(t.writes)))()
+            for j, (rt, tb, ix, key) in enumerate(t.writes):
+                nm = C.create_string_buffer(tb.encode())
+                dta = rt in DTA_TYPES or key is None
+                kb = None if dta else C.create_string_buffer(bytes(key), max(1, len(key)))
+                keep += [nm, kb]
+                ws[j].tbname = C.cast(nm, C.c_char_p)
+                ws[j].idxnum = -2 if dta else ix
+                ws[j].key = None if dta else C.cast(kb, _p)
+                ws[j].keylen = 0 if dta else len(key)
+            keep.append(ws)
+            pt[i].arr = ptrs[i]
+            pt[i].writes = C.cast(ws, _p)
+            pt[i].nwrites = len(t.writes)
+        ev = np.array([idx[t.name] if e == "begin" else ~idx[t.name] for e, t in events], np.int32)
+        rc = np.zeros(max(1, n), np.int32)
+        seq = np.zeros(max(1, n), np.int64)
+        snap = np.zeros(max(1, n), np.uint64)
+        cend = np.zeros(max(1, n), np.uint64)
+        res = ProtocolResult()
+        r0 = self.regop_stats()
+        try:
+            self._chk(self.lib.hsc_harness_commit_protocol(
+                self.ctx, pt, n, ev.ctypes.data, len(ev), nthreads, rc.ctypes.data, seq.ctypes.data,
+                snap.ctypes.data, cend.ctypes.data, C.byref(res)), "hsc_harness_commit_protocol")
+        finally:
+            arrs.close()
+        r1 = self.regop_stats()
+        st = {k: getattr(res, k) for k, _ in ProtocolResult._fields_}
+        st["threads"] = nthreads
+        sec = max(res.seconds, 1e-9)
+        st["commits_per_s"] = (res.commits + res.aborts) / sec  # commit attempts (checked txns)
+        st["committed_per_s"] = res.commits / sec
+        st["regop_fast"] = r1["fast"] - r0["fast"]
+        st["regop_locked"] = r1["locked"] - r0["locked"]
+        return rc[:n], seq[:n], snap[:n], cend[:n], st
 
     def concurrent_check(self, arrs, nthreads: int, rounds: int = 1, regop_only: int = 0,
                          collect: bool = True, max_batch: int = 0, max_wait_us: int = 0,

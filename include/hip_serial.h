@@ -413,6 +413,15 @@ int hsc_merge_table_max(hsc_ctx *ctx, const uint64_t *in, int n);
  * hsc_set_autocollect(ctx, 0) makes every call its own pass instead. */
 int hip_bdb_osql_serial_check(void *ctx, void *ranges, unsigned int *file,
                               unsigned int *offset, int regop_only);
+/* regop_only (here, in hip_serial_check_batch and hsc_collector_check) is
+ * answered in the caller's thread from a snapshot (end LSN, max commit LSN,
+ * unreadable-regop LSN, DB_SET rule) that every entry changing the window
+ * republishes before it returns: no collector queue, no context lock, no
+ * window build (db/toblock.c:4779-4785 probes under the commit_lock write
+ * lock).  Only a snapshot the published values cannot decide -- no commit
+ * after it, inside a log whose record LSNs must be searched -- takes the
+ * locked path.  out[0] = probes answered from the snapshot, out[1] = locked. */
+int hsc_regop_stats(hsc_ctx *ctx, uint64_t out[2]);
 /* The drop-in entry through the context's own collector (1, the default) or
  * one pass per call (0).  0 or HSC_EINVAL. */
 int hsc_set_autocollect(hsc_ctx *ctx, int on);
@@ -802,6 +811,36 @@ typedef struct hsc_concurrent_result {
 int hsc_harness_concurrent(hsc_ctx *ctx, hsc_collector *col, void *const *arrs, int n,
                            int nthreads, int rounds, int regop_only, int *rc_out,
                            hsc_concurrent_result *res);
+/* The master's commit protocol (db/toblock.c:4757-4836) replayed by nthreads
+ * threads over a stream of events: events[k] >= 0 -- txn events[k] begins (its
+ * CurRangeArr's snapshot := hsc_window_end); events[k] < 0 -- txn ~events[k]
+ * commits.  Threads take events in order (a commit waits for its txn's begin).
+ * A commit: commit_lock (a pthread rwlock) read-locked, released and
+ * write-locked; while hip_bdb_osql_serial_check(regop_only = 1) on
+ * &arr->file / &arr->offset says a newer commit exists: unlock, full check
+ * (regop_only = 0; conflict -> abort, rc 1), write-lock again; then the txn's
+ * writes are appended at commit LSN hsc_window_end + 1 (hsc_window_append)
+ * and the lock released.  Per txn: rc_out (0 committed, 1 aborted),
+ * commit_seq (its commit's index, -1 if aborted or without writes),
+ * snap_out (the snapshot it began with), check_end_out (the end LSN its last
+ * full check returned, 0 if none ran). */
+typedef struct hsc_protocol_txn {
+    void *arr;                /* CurRangeArr* (file / offset set at begin)   */
+    const hsc_write *writes;  /* the txn's writes (commit_lsn ignored)       */
+    int nwrites;
+} hsc_protocol_txn;
+typedef struct hsc_protocol_result {
+    double seconds;           /* first event to last commit                  */
+    uint64_t commits, aborts, regop_probes, full_checks;
+    double regop_p50_us, regop_p99_us, regop_p999_us, regop_max_us;
+    double full_p50_us, full_p99_us;
+    double hold_p50_us, hold_p99_us;  /* commit_lock write-held per commit   */
+    double commit_p50_us, commit_p99_us;  /* commit event: first lock to done */
+} hsc_protocol_result;
+int hsc_harness_commit_protocol(hsc_ctx *ctx, const hsc_protocol_txn *txns, int ntxn,
+                                const int *events, int nevents, int nthreads, int *rc_out,
+                                int64_t *commit_seq, uint64_t *snap_out, uint64_t *check_end_out,
+                                hsc_protocol_result *res);
 
 #ifdef __cplusplus
 }

@@ -1,9 +1,12 @@
 """Batching collector (hsc_collector_check): many native caller threads, one
 read set per call, as comdb2's block processors call bdb_osql_serial_check
 (db/toblock.c:4779-4836 -> bdb/serializable.c:571).  Verdicts and the
-(file, offset) side effect must be exactly the single call's; the host-only
-tests drive the regop_only mode (decided on the host) and the fail-closed
-rule, the GPU tests the full check against the oracle."""
+(file, offset) side effect must be exactly the single call's.  regop_only
+probes are answered from the context's published snapshot in the caller's
+thread and never queue (no collector pass runs for them); the host-only
+tests drive them against the oracle, and the batching itself with full
+checks, which a host-only context fails closed (every verdict 1); the GPU
+tests run the full check against the oracle."""
 import numpy as np
 import pytest
 
@@ -27,10 +30,13 @@ def test_regop_only_through_collector(host, oracle_mod, nthreads, inflight):
     arrs = NativeCurRangeArrs(rs)
     got, st = host.concurrent_check(arrs, nthreads, rounds=3, regop_only=1, inflight=inflight)
     np.testing.assert_array_equal(got != 0, want != 0)
-    assert st["calls"] == 3 * rs.ntxn
-    assert 1 <= st["batches"] <= st["calls"] and st["max_batch"] <= nthreads
+    assert st["calls"] == 3 * rs.ntxn and st["batches"] == 0  # never queued
     direct, _ = host.concurrent_check(arrs, nthreads, regop_only=1, collect=False)
     np.testing.assert_array_equal(direct, got)
+    # the batching: full checks (failed closed on a host-only context)
+    full, st = host.concurrent_check(arrs, nthreads, rounds=3, regop_only=0, inflight=inflight)
+    assert (full == 1).all() and st["calls"] == 3 * rs.ntxn
+    assert 1 <= st["batches"] <= st["calls"] and st["max_batch"] <= nthreads
     arrs.close()
 
 
@@ -42,6 +48,9 @@ def test_collector_bounds_batches(host, oracle_mod):
     got, st = host.concurrent_check(arrs, 16, rounds=2, regop_only=1, max_batch=3,
                                     max_wait_us=200)
     np.testing.assert_array_equal(got != 0, want != 0)
+    got, st = host.concurrent_check(arrs, 16, rounds=2, regop_only=0, max_batch=3,
+                                    max_wait_us=200)
+    assert (got == 1).all()
     assert st["max_batch"] <= 3 and st["batches"] >= st["calls"] / 3
     arrs.close()
 
@@ -58,6 +67,9 @@ def test_collector_many_threads_cut_batches(host, oracle_mod, max_batch, infligh
     got, st = host.concurrent_check(arrs, 128, rounds=4, regop_only=1, max_batch=max_batch,
                                     inflight=inflight)
     np.testing.assert_array_equal(got != 0, want != 0)
+    got, st = host.concurrent_check(arrs, 128, rounds=4, regop_only=0, max_batch=max_batch,
+                                    inflight=inflight)
+    assert (got == 1).all()
     assert st["calls"] == 4 * rs.ntxn and st["max_batch"] <= max_batch
     arrs.close()
 

@@ -49,3 +49,68 @@ def test_config5_tail_gives_the_whole_logs_verdicts(oracle_mod):
     want, _, _ = oracle_mod.check(whole, c5.readsets)
     got, _, _ = oracle_mod.check(tail, c5.readsets)
     np.testing.assert_array_equal(got, want)
+
+
+def _sharded_tail(vals, snaps, world, K=10):
+    """bench_multi's CPU-baseline log: every member's writes from local commit
+    c_start on, c_start from the oldest snapshot's commit."""
+    from comdb2_amd.workloads import lsn_to_index
+    gc0 = int((int(lsn_to_index(np.asarray(snaps, np.uint64).min())) - (K + 2)) // (K + 3))
+    c_start = max(0, gc0) // world
+    return config5_log([v[c_start * K:] for v in vals], keys_per_commit=K, commit_base=c_start), c_start
+
+
+def test_lsn_to_index_inverts_lsn_of_index():
+    from comdb2_amd.workloads import lsn_of_index, lsn_to_index
+    idx = np.array([0, 1, 5, (1 << 26) - 1, 1 << 26, 3 * (1 << 26) + 17], np.uint64)
+    np.testing.assert_array_equal(lsn_to_index(lsn_of_index(idx)), idx)
+
+
+def test_config2_rank_window_equals_the_full_call():
+    from comdb2_amd.workloads import config2, config2_device_window, config2_rank_window
+    for r in (0, 2):
+        c2 = config2(n_commits=3000, n_txn=50, rank=r, world=3, build_log=False)
+        want = config2_device_window(c2)
+        got = config2_rank_window(n_commits=3000, rank=r, world=3)
+        for a, b in zip(got[:3], want):
+            np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(got[3], c2.key_values)
+
+
+def test_sharded_config2_tail_log_equals_the_global_log(oracle_mod):
+    """The world-3 config-2 log rebuilt from the ranks' tails (bench_multi's
+    CPU baseline at N > 1) is record for record the merge of the ranks' own
+    logs after c_start, and gives owner 0's read sets the same verdicts."""
+    from comdb2_amd.formats import LLog
+    from comdb2_amd.workloads import config2
+    world = 3
+    cs = [config2(n_commits=4000, n_txn=300, rank=r, world=world, snap_recent=0.2)
+          for r in range(world)]
+    rs0 = cs[0].readsets.subset(np.arange(0, 300))
+    tail, c_start = _sharded_tail([c.key_values for c in cs], rs0.snap, world)
+    assert c_start > 0 and tail.end_lsn == cs[0].log.end_lsn
+    # the ranks' own logs merged by LSN, from global commit c_start * world on
+    logs = [c.log for c in cs]
+    lsn = np.concatenate([l.lsn for l in logs])
+    o = np.argsort(lsn, kind="stable")
+    keep = lsn[o] >= tail.lsn[0]
+    cat = lambda f: np.concatenate([getattr(l, f) for l in logs])[o][keep]
+    kcat = np.concatenate([l.keys for l in logs])
+    koff = np.concatenate([l.key_off + np.uint64(sum(len(x.keys) for x in logs[:i]))
+                           for i, l in enumerate(logs)])[o][keep]
+    merged = LLog(cat("lsn"), cat("rectype"), cat("prev"), cat("isabort"), cat("table"), cat("ix"),
+                  koff, cat("keylen"), kcat, ["t1"], cs[0].log.end_lsn)
+    np.testing.assert_array_equal(merged.lsn, tail.lsn)
+    np.testing.assert_array_equal(merged.rectype, tail.rectype)
+    # (prev of each commit's first record is 0 in both; inside a commit it chains)
+    np.testing.assert_array_equal(merged.prev[1:], tail.prev[1:])
+    whole = LLog(lsn[o], np.concatenate([l.rectype for l in logs])[o],
+                 np.concatenate([l.prev for l in logs])[o], np.concatenate([l.isabort for l in logs])[o],
+                 np.concatenate([l.table for l in logs])[o], np.concatenate([l.ix for l in logs])[o],
+                 np.concatenate([l.key_off + np.uint64(sum(len(x.keys) for x in logs[:i]))
+                                 for i, l in enumerate(logs)])[o],
+                 np.concatenate([l.keylen for l in logs])[o], kcat, ["t1"], cs[0].log.end_lsn)
+    want, _, _ = oracle_mod.check(whole, rs0)
+    got, _, _ = oracle_mod.check(tail, rs0)
+    np.testing.assert_array_equal(got, want)
+    assert 0.02 < (want != 0).mean() < 0.98
