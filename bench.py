@@ -364,6 +364,13 @@ def bench_graph(args):
         local = 0
     if devs:
         local = devs[0]
+    if args.pmc_child:  # one step of member 0's shard under rocprofv3 --pmc (graph_pmc_traffic)
+        return graph_pmc_child(args)
+    h = config4_history(n_txn=args.history_txns, n_keys=args.c4_keys or max(1000, args.history_txns // 10),
+                        concurrent_frac=args.c4_concurrent, max_lag=args.c4_max_lag)
+    traffic = None
+    if rank == 0 and backend == "nccl" and not args.no_pmc:
+        traffic = graph_pmc_traffic(args, h, world, local)  # before this process touches the GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world_env > 1:
@@ -371,8 +378,6 @@ def bench_graph(args):
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    h = config4_history(n_txn=args.history_txns, n_keys=args.c4_keys or max(1000, args.history_txns // 10),
-                        concurrent_frac=args.c4_concurrent, max_lag=args.c4_max_lag)
     hs = shard.history_shard(h, rank, world)
     dh = shard.device_history(hs, dev)
     dhs = [dh]
@@ -461,10 +466,19 @@ def bench_graph(args):
                "roofline": {"bound": "hbm", "kernel": "sharded SCC step (raw build: writer sort + "
                                                         "edge rows; cover; cut; colouring SCC)",
                             "achieved": B4 / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                            "frac": B4 / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                            "frac": B4 / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                            "traffic": traffic.get("bytes_per_step") if traffic else None,
+                            "measured_frac": (traffic["bytes_per_step"] / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                              if traffic and traffic.get("bytes_per_step") else None),
                             "algorithmic_bytes": B4,
                             "note": "B = ops x 17 B (txn, key, is_write, observed read once) + "
-                                    "txns x 5 B (cover byte, scc word); rank 0's step time"}}
+                                    "txns x 5 B (cover byte, scc word); rank 0's step time.  "
+                                    "traffic = FETCH_SIZE + WRITE_SIZE bytes of every hsc:: kernel "
+                                    "of one step of member 0's shard (rocprofv3 --pmc passes of "
+                                    "bench.py --config 4 --pmc-child; at N > 1 the SCC runs over "
+                                    "that shard's cut only, not the union of the cuts)"}}
+        if traffic:
+            out["roofline"]["traffic_detail"] = traffic
     (mv if mv is not None else v).close()
     if world_env > 1:
         dist.barrier()
@@ -473,6 +487,80 @@ def bench_graph(args):
         if not args.no_cpu:  # the host's throughput: the same line at every N
             out["cpu_baseline"] = graph_cpu_baseline(args)
         print(json.dumps(out), flush=True)
+
+
+def graph_pmc_traffic(args, h, world, device):
+    """HBM bytes of one config-4 step (member 0's key shard: raw build, cover,
+    cut, colouring SCC) from rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE passes
+    of `bench.py --config 4 --pmc-child` over the same history (saved for the
+    child with numpy, no pickles), summed over every hsc:: kernel of the
+    step; the gfx950 FETCH_SIZE correction as in pmc_traffic."""
+    import csv
+    import shutil
+    import tempfile
+    d = tempfile.mkdtemp(prefix="hsc_c4_")
+    out = {"kind": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of bench.py --config 4 "
+                   "--pmc-child (one step of member 0's shard, every hsc:: kernel)", "kernels": {}}
+    try:
+        for k in ("txn", "key", "is_write", "observed"):
+            np.save(os.path.join(d, k + ".npy"), getattr(h, k))
+        per = {}
+        for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+            od = os.path.join(d, "pmc_" + ctr)
+            cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", ctr, "-T", "--output-format",
+                   "csv", "-d", od, "-o", "run", "--", sys.executable, os.path.abspath(__file__),
+                   "--pmc-child", "--config", "4", "--c4-dir", d, "--c4-ntxn", str(h.ntxn),
+                   "--c4-world", str(world), "--pmc-device", str(device)]
+            env = {k: v for k, v in os.environ.items()
+                   if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                                "ROLE_RANK", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+            print(f"[bench] config-4 pmc pass {ctr}", file=sys.stderr, flush=True)
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+            path = os.path.join(od, "run_counter_collection.csv")
+            if r.returncode != 0 or not os.path.exists(path):
+                out["error"] = f"{ctr}: rc {r.returncode}: {(r.stderr or '')[-300:]}"
+                return out
+            vals = {}
+            for row in csv.DictReader(open(path)):
+                name = row["Kernel_Name"]
+                if "hsc::" not in name or row["Counter_Name"] != ctr:
+                    continue
+                k = name.split("(")[0].replace("hsc::", "").replace("(anonymous namespace)::", "")
+                k = (k[5:] if k.startswith("void ") else k).split("<")[0]
+                vals[k] = vals.get(k, 0.0) + float(row["Counter_Value"])
+            per[ctr] = vals
+        tot = 0.0
+        for k in sorted(set(per["FETCH_SIZE"]) | set(per["WRITE_SIZE"])):
+            rd, wr = 2 * 1024 * per["FETCH_SIZE"].get(k, 0.0), 1024 * per["WRITE_SIZE"].get(k, 0.0)
+            out["kernels"][k] = {"read_bytes": rd, "write_bytes": wr}
+            tot += rd + wr
+        out["bytes_per_step"] = tot
+    except (OSError, subprocess.SubprocessError) as e:
+        out["error"] = str(e)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    return out
+
+
+def graph_pmc_child(args):
+    """The profiled child of graph_pmc_traffic: member 0's shard of the saved
+    history, one hsc_multi_graph_scc step on one GPU."""
+    import torch
+
+    from comdb2_amd import hsc, shard
+    from comdb2_amd.workloads import History
+    ld = lambda k: np.load(os.path.join(args.c4_dir, k + ".npy"))
+    h = History(ld("txn"), ld("key"), ld("is_write"), ld("observed"), args.c4_ntxn)
+    hs = shard.history_shard(h, 0, max(1, args.c4_world))
+    torch.cuda.set_device(args.pmc_device)
+    dev = torch.device("cuda", args.pmc_device)
+    dh = shard.device_history(hs, dev)
+    scc = torch.zeros(max(h.ntxn, 1), dtype=torch.int32, device=dev)
+    mv = hsc.MultiValidator([args.pmc_device])
+    torch.cuda.synchronize(dev)
+    mv.graph_scc([dh], h.ntxn, [scc.data_ptr()])
+    torch.cuda.synchronize(dev)
+    mv.close()
 
 
 def graph_cpu_baseline(args, threads=None):
@@ -970,6 +1058,10 @@ def bench_multi(args):
                                   tl.data_ptr(), end_lsn)
         del tg, tw, tl
     n_w = {g: len(rows[g][2]) for g in mine}
+    # the replicated drop-in leg (in process, config 2): every member holds
+    # the whole global window
+    rows_all = ([rows[g] for g in mine] if inproc and not pmc_child and args.config == 2
+                and not args.no_api else None)
     rows = None
     v.adopt()
     if args.config == 3:
@@ -1081,6 +1173,16 @@ def bench_multi(args):
     rbits = np.unpackbits(r0["bits"].cpu().numpy().view(np.uint8), bitorder="little")[:T]
     v0 = np.maximum(rbits, r0["forced"])
     routings_equal = bool(np.array_equal(np.maximum(dbits, d0["forced"]) != 0, v0 != 0))
+    # the routed step's host cost: its phases over the timed legs, and the
+    # pure enqueue -- calls that start on an idle GPU (no queue backpressure)
+    rps = v.routed_phase_stats()
+    idle = []
+    for k in range(min(max(args.steps, 5), NB)):
+        sync_all()
+        t0 = time.perf_counter()
+        step_routed(k, 1, NB)
+        idle.append(time.perf_counter() - t0)
+    sync_all()
     # per-member probe time of the routed step (imbalance across the pieces)
     v.enable_member_timing(True)
     pm = []
@@ -1145,6 +1247,11 @@ def bench_multi(args):
             "routed_over_own": float(sum(routed_rows)) / max(1, sum(own_rows)),
             "verdicts_equal_device_routed": routings_equal,
             "host_enqueue_us_per_step": v.phase_stats()["routed_enqueue_us"],
+            "host_phases_us_per_step": rps,
+            "host_enqueue_idle_us": {"p50": float(np.median(idle) * 1e6), "min": float(np.min(idle) * 1e6),
+                                     "per_member_p50": float(np.median(idle) * 1e6) / max(1, len(mine)),
+                                     "note": "hsc_multi_probe_routed calls that start on an idle GPU "
+                                             "(no queue backpressure): the pure host enqueue"},
         },
         "imbalance": {
             "member_probe_ms": [float(x) for x in pm],
@@ -1186,6 +1293,10 @@ def bench_multi(args):
         out["roofline"]["traffic_detail"] = traffic
     if inproc and args.config == 2 and not args.no_api:
         out["api"] = multi_api_leg(hsc, v, first_rs.subset(np.arange(0, T)), v0)
+        v.close()
+        out["api_replicas"] = replicas_api_leg(hsc, torch, devs, rows_all, end_lsn,
+                                               first_rs.subset(np.arange(0, T)), v0)
+        rows_all = None
     v.close()
     if not inproc:
         dist.destroy_process_group()
@@ -1217,6 +1328,37 @@ def bench_multi(args):
                          "equal": bool(cpu["parity_with_gpu"] and cpu["single_core"]["parity_with_gpu"])}
     if rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def replicas_api_leg(hsc, torch, devs, rows_all, end_lsn, rs, want):
+    """The drop-in entry on a replicated multi context (HSC_MULTI_REPLICAS):
+    every member ingests the whole global window from device rows, a lone
+    call or a collector pass goes whole to one member (the one with the
+    fewest passes in flight), a large batch is sliced over the members -- the
+    same legs as multi_api_leg, same read sets, same expected verdicts."""
+    rv = hsc.MultiValidator(devs)
+    try:
+        assert rv.register_group("t1", 0, 9) == 0
+        rv.set_mode(hsc.MULTI_REPLICAS)
+        gid = np.concatenate([r[0] for r in rows_all])
+        words = np.concatenate([r[1] for r in rows_all], axis=1)
+        lsn = np.concatenate([r[2] for r in rows_all])
+        for i, d in enumerate(devs):
+            dv = torch.device("cuda", d)
+            tg = torch.from_numpy(np.ascontiguousarray(gid)).to(dv)
+            tw = torch.from_numpy(np.ascontiguousarray(words).reshape(-1).view(np.int64)).to(dv)
+            tl = torch.from_numpy(np.ascontiguousarray(lsn).view(np.int64)).to(dv)
+            torch.cuda.synchronize(dv)
+            rv.member(i).ingest_device(len(lsn), words.shape[0], tg.data_ptr(), tw.data_ptr(),
+                                       tl.data_ptr(), end_lsn)
+            del tg, tw, tl
+        rv.adopt()
+        out = multi_api_leg(hsc, rv, rs, want)
+        out["mode"] = "replicas" if rv.mode == hsc.MULTI_REPLICAS else "pieces"
+        out["window_keys_per_member"] = rv.member(0).keys
+        return out
+    finally:
+        rv.close()
 
 
 def multi_api_leg(hsc, v, rs, want):
@@ -1293,6 +1435,9 @@ def main():
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--multi-pmc", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--pmc-device", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--c4-dir", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--c4-ntxn", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--c4-world", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--wide", action="store_true", help="force the wide window layout")
     ap.add_argument("--compact-wide", action="store_true",
                     help="compact windows: probe through the wide tile pipeline instead of "

@@ -6,6 +6,7 @@
 #include "hsc_internal.h"
 
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <atomic>
@@ -197,6 +198,64 @@ struct PodVec {
     }
 };
 
+// Append-only array of trivially copyable T for the stores that grow with
+// every commit (the log records, the host-staged rows): its pages are mapped
+// directly and grown with mremap, which moves page tables instead of copying
+// the contents, so an append never pays a copy of everything before it
+// (std::vector's doubling cost a 0.6-1.2 ms stall per doubling at 2^17 and
+// 2^18 records of a commit stream).
+template <class T>
+struct MapVec {
+    T *p = nullptr;
+    size_t n = 0, cap = 0;
+    MapVec() = default;
+    MapVec(const MapVec &) = delete;
+    MapVec &operator=(const MapVec &) = delete;
+    ~MapVec()
+    {
+        if (p) munmap(p, cap * sizeof(T));
+    }
+    void reserve(size_t k)
+    {
+        if (k <= cap) return;
+        const size_t page = 4096 / sizeof(T) ? 4096 / sizeof(T) : 1;
+        size_t c = std::max(k, std::max(2 * cap, (size_t)65536));
+        c = (c + page - 1) / page * page;
+        void *q = p ? mremap(p, cap * sizeof(T), c * sizeof(T), MREMAP_MAYMOVE)
+                    : mmap(nullptr, c * sizeof(T), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (q == MAP_FAILED) throw std::bad_alloc();
+        p = (T *)q, cap = c;
+    }
+    void push_back(const T &v)
+    {
+        if (n == cap) reserve(n + 1);
+        p[n++] = v;
+    }
+    // append [a, b) (pos must be end())
+    void insert(T *pos, const T *a, const T *b)
+    {
+        (void)pos;
+        const size_t k = (size_t)(b - a);
+        if (!k) return;
+        reserve(n + k);
+        memcpy(p + n, a, k * sizeof(T));
+        n += k;
+    }
+    void clear() { n = 0; }
+    size_t size() const { return n; }
+    bool empty() const { return n == 0; }
+    T *data() { return p; }
+    const T *data() const { return p; }
+    T *begin() { return p; }
+    T *end() { return p + n; }
+    const T *begin() const { return p; }
+    const T *end() const { return p + n; }
+    T &back() { return p[n - 1]; }
+    const T &back() const { return p[n - 1]; }
+    T &operator[](size_t i) { return p[i]; }
+    const T &operator[](size_t i) const { return p[i]; }
+};
+
 // One worker's share of a marshal (read sets [t0, t1) of the batch): probes
 // as AoS rows (W words of lo, W of hi) plus the scratch of the span builder.
 // One range of a read set as the marshal reads it (window table id, -1 if
@@ -373,10 +432,10 @@ struct hsc_ctx {
     uint64_t gcls_epoch = ~0ull;
 
     // host staging of the window (host ingest paths)
-    std::vector<uint32_t> h_gid;
-    std::vector<uint64_t> h_keyoff;
-    std::vector<uint8_t> h_keys;
-    std::vector<uint64_t> h_lsn;
+    MapVec<uint32_t> h_gid;
+    MapVec<uint64_t> h_keyoff;
+    MapVec<uint8_t> h_keys;
+    MapVec<uint64_t> h_lsn;
     std::vector<uint64_t> h_table_max;
     bool host_staged = true;
     bool dirty = true;
@@ -387,11 +446,11 @@ struct hsc_ctx {
     // DB_SET rule, records for chain walks of txns committed by appends);
     // table = window table id
     struct LogStore {
-        std::vector<uint64_t> lsn, prev, key_off;
-        std::vector<uint32_t> rectype;
-        std::vector<int16_t> isabort, ix;
-        std::vector<int32_t> table, keylen;
-        std::vector<uint8_t> keys;
+        MapVec<uint64_t> lsn, prev, key_off;
+        MapVec<uint32_t> rectype;
+        MapVec<int16_t> isabort, ix;
+        MapVec<int32_t> table, keylen;
+        MapVec<uint8_t> keys;
         void clear()
         {
             lsn.clear(), prev.clear(), key_off.clear(), rectype.clear(), isabort.clear();
@@ -449,16 +508,31 @@ struct hsc_ctx {
     // checks probe main + frozen + live runs until a call after the build
     // swaps the shadow's window in (fold_poll).  fold_bg = false: the run is
     // merged inline by the next check instead (the pre-fold behaviour).
-    hsc_ctx *shadow = nullptr;
-    std::thread fold_thread;
+    hsc_ctx *shadow = nullptr;     // created by the fold worker (its stream too)
+    std::thread fold_thread;       // the fold worker: one per context, started by its first fold
+    std::mutex fold_mu;
+    std::condition_variable fold_cv;
+    bool fold_job = false, fold_quit = false;
+    struct FoldJob {  // one fold, captured by fold_start on the caller's thread
+        size_t nm = 0, nf = 0, cap = 0, dcap = 0;
+        int W = 1, layout = 0;
+        unsigned paths = 0;
+        const void *gid2 = nullptr, *lsn2 = nullptr, *words2 = nullptr;  // main window versions
+        const void *fgid = nullptr, *flsn = nullptr, *fwords = nullptr;  // the frozen run
+        std::vector<GroupInfo> groups;
+        std::vector<std::string> table_names;
+        std::vector<uint64_t> table_max;
+    } fold_jobv;
     std::atomic<int> fold_state{0};  // kFoldIdle / kFoldRunning / kFoldDone
     int fold_rc = 0;
+    std::string fold_err;
     DBuf f_dgid, f_dwords, f_dlsn, f_dbmax;  // the frozen run (fn rows, stride dcap)
     size_t fn = 0;
     size_t fold_rows = kDeltaCap / 2;
     bool fold_bg = true;
     hipEvent_t fold_ev = nullptr;  // the old window's last readers (the next fold waits)
     uint64_t folds_started = 0, folds_swapped = 0, folds_inline = 0;
+    bool merge_is_fold = false;  // merge_pending for a full delta run (not a new group / wider key)
     float fold_ms = 0;  // build time of the last background fold
 
     // device window

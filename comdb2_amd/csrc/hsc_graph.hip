@@ -49,6 +49,61 @@ __global__ void k_gather_writers(size_t nops, const uint32_t *txn, const uint64_
     lsn[p] = 0;
 }
 
+// Writers gathered without a flag array or a scan over the ops: a block of
+// kGwThreads x kGwItems ops counts its writers (wave ballots, one LDS scan),
+// takes its range with ONE atomic on the cursor and writes them in op order
+// inside the range (blocks land in atomic order: the writers are sorted by
+// (key, txn) next, so their order here does not matter).
+constexpr int kGwThreads = 256, kGwItems = 16;
+__global__ __launch_bounds__(kGwThreads) void k_gather_writers_blk(size_t nops, const uint32_t *txn,
+                                                                    const uint64_t *key,
+                                                                    const uint8_t *is_write, uint32_t *cursor,
+                                                                    uint32_t *gid, uint64_t *words,
+                                                                    uint64_t *lsn, size_t stride)
+{
+    __shared__ uint32_t wsum[kGwThreads / 64];
+    __shared__ uint32_t bbase;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const size_t base = (size_t)blockIdx.x * (kGwThreads * kGwItems);
+    uint32_t cnt = 0;
+    uint32_t w = 0;  // bit k: op k of this thread writes
+#pragma unroll
+    for (int k = 0; k < kGwItems; ++k) {
+        const size_t i = base + (size_t)k * kGwThreads + threadIdx.x;
+        const bool wr = i < nops && is_write[i];
+        w |= (uint32_t)wr << k;
+        cnt += wr;
+    }
+    uint32_t inc = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int q = 0; q < kGwThreads / 64; ++q) t += wsum[q];
+        bbase = t ? atomicAdd(cursor, t) : 0;
+    }
+    __syncthreads();
+    uint32_t p = bbase + inc - cnt;
+#pragma unroll
+    for (int q = 0; q < kGwThreads / 64; ++q) p += q < wv ? wsum[q] : 0;
+#pragma unroll
+    for (int k = 0; k < kGwItems; ++k) {
+        if (!((w >> k) & 1u)) continue;
+        const size_t i = base + (size_t)k * kGwThreads + threadIdx.x;
+        gid[p] = 0;
+        words[p] = key[i];
+        words[stride + p] = txn[i];
+        lsn[p] = 0;
+        ++p;
+    }
+}
+
 __global__ void k_write_flags(size_t nops, const uint8_t *is_write, uint32_t *flags)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -238,6 +293,197 @@ __global__ void k_edges_reads_pk(size_t nops, const uint32_t *txn, const uint64_
         eg[s] = 0;
         et[s + 1] = kDepRW;
         eg[s + 1] = 0;
+    }
+}
+
+// ---- partitioned read search (the packed writers) ----
+// k_edges_reads_pk answers each read with a directory line and a search of
+// pk: two dependent random lines per read over a 33M-writer array (config 4:
+// 3.4 ms of a 10.5 ms step).  Instead the reads are partitioned by directory
+// range (2^14 partitions of ~2k writers): one pass counts, one scatters the
+// search items (x, reader) into their partitions, and a workgroup per
+// partition stages its writers in LDS once and answers every item there --
+// the reads' random accesses become streams plus LDS searches.  Edge rows:
+// [nu, nu + nops) the wr edge of op i, [nu + nops, + items + fallbacks) the
+// rw edges in partition order (raw rows carry no slot meaning; a full build
+// sorts them).
+constexpr int kRpBitsMax = 14;        // at most 2^14 partitions
+constexpr uint32_t kRpLds = 6144;     // writers a partition stages (48 KiB of LDS)
+constexpr int kRpThreads = 256;
+
+struct RpArgs {
+    size_t nops;
+    const uint32_t *txn;
+    const uint64_t *key;
+    const uint8_t *is_write;
+    const uint32_t *observed;
+    uint32_t nu;
+    const uint64_t *wkey, *wtxn, *pk;
+    const uint32_t *dir;
+    uint32_t ps;         // partition = bucket >> ps
+    uint32_t np;         // partitions (incl. the one past the range)
+    uint32_t *cnt;       // [np + 1] counts, then offsets (exclusive scan; [np] = items)
+    uint32_t *cur;       // [np + 1] cursors; cur[np] = fallback rows
+    ulonglong2 *items;   // (x, reader | strict << 32)
+    uint64_t *ew;        // edge rows
+    uint64_t *et;        // types (full builds) or null
+    uint32_t *eg;
+    uint32_t *diff;      // raw builds: the cover's interval diffs of backward edges (else null)
+    int skip_rw;
+};
+
+// a backward edge a -> b (a > b) covers [b, a] (graph_cover's k_back_diff,
+// done while the raw build emits the row)
+__device__ __forceinline__ void rp_back(uint32_t *diff, uint64_t row)
+{
+    if (!diff || row == ~0ull) return;
+    const uint32_t a = (uint32_t)(row >> 32), b = (uint32_t)row;
+    if (a > b) {
+        atomicAdd(&diff[b], 1u);
+        atomicAdd(&diff[a + 1], 0xFFFFFFFFu);
+    }
+}
+
+// x of a read's "first writer after (k, ob)" search, or false when it needs
+// none (key without writers) / the row search (an observed txn outside the
+// writers' bits).  *fb: the row search is needed.
+__device__ __forceinline__ bool rp_x(const PairPack &pp, uint64_t k, uint32_t ob, uint64_t *x, bool *fb)
+{
+    *fb = false;
+    if ((k & ~pp.km) != pp.kc) return false;
+    if (ob != kNone && (ob & ~pp.tm) != pp.tc) {
+        *fb = true;
+        return false;
+    }
+    uint64_t km[6], tm[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) km[q] = pp.kmv[q], tm[q] = pp.tmv[q];
+    *x = pair_key(pp, bits_compress(k, pp.km, km)) | (ob == kNone ? 0 : bits_compress(ob, pp.tm, tm));
+    return true;
+}
+
+__global__ __launch_bounds__(kRpThreads) void k_rp_count(RpArgs a, PairPack pp)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.nops || a.skip_rw || a.is_write[i]) return;
+    uint64_t x;
+    bool fb;
+    if (rp_x(pp, a.key[i], a.observed[i], &x, &fb))
+        atomicAdd(&a.cnt[(uint32_t)(pair_bucket(pp, x) >> a.ps)], 1u);
+}
+
+// exclusive scan of cnt[0, np) in place, cnt[np] = total; cur zeroed
+__global__ __launch_bounds__(1024) void k_rp_scan(RpArgs a)
+{
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x, per = (a.np + 1023) / 1024;
+    const uint32_t b = t * per, e = min(a.np, b + per);
+    uint32_t s = 0;
+    for (uint32_t i = b; i < e; ++i) s += a.cnt[i];
+    part[t] = s;
+    __syncthreads();
+    for (uint32_t o = 1; o < 1024; o <<= 1) {  // inclusive scan of the parts
+        const uint32_t v = t >= o ? part[t - o] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - s;
+    for (uint32_t i = b; i < e; ++i) {
+        const uint32_t c = a.cnt[i];
+        a.cnt[i] = run;
+        run += c;
+    }
+    if (t == 1023) a.cnt[a.np] = part[1023];
+    for (uint32_t i = t; i <= a.np; i += 1024) a.cur[i] = 0;
+}
+
+__global__ __launch_bounds__(kRpThreads) void k_rp_scatter(RpArgs a, PairPack pp)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.nops) return;
+    uint64_t wr = ~0ull;
+    if (!a.is_write[i]) {
+        const uint32_t r = a.txn[i], ob = a.observed[i];
+        const uint64_t k = a.key[i];
+        if (ob != kNone && ob != r) wr = ((uint64_t)ob << 32) | r;
+        uint64_t x;
+        bool fb;
+        if (!a.skip_rw && rp_x(pp, k, ob, &x, &fb)) {
+            const uint32_t p = (uint32_t)(pair_bucket(pp, x) >> a.ps);
+            const uint32_t slot = a.cnt[p] + atomicAdd(&a.cur[p], 1u);
+            a.items[slot] = make_ulonglong2(x, (uint64_t)r | (ob != kNone ? 1ull << 32 : 0));
+        } else if (!a.skip_rw && fb) {  // the row search (rare): its rw row after the items
+            uint32_t lo = 0, hi = a.nu;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                const uint64_t mk = a.wkey[mid], mt = a.wtxn[mid];
+                if (mk < k || (mk == k && mt <= ob))
+                    lo = mid + 1;
+                else
+                    hi = mid;
+            }
+            if (lo < a.nu && a.wkey[lo] == k && a.wtxn[lo] != r) {
+                const size_t o = (size_t)a.nu + a.nops + a.cnt[a.np] + atomicAdd(&a.cur[a.np], 1u);
+                const uint64_t row = ((uint64_t)r << 32) | a.wtxn[lo];
+                a.ew[o] = row;
+                if (a.et) a.et[o] = kDepRW, a.eg[o] = 0;
+                rp_back(a.diff, row);
+            }
+        }
+    }
+    const size_t s = (size_t)a.nu + i;
+    a.ew[s] = wr;
+    if (a.et) a.et[s] = kDepWR, a.eg[s] = 0;
+    rp_back(a.diff, wr);
+}
+
+__global__ __launch_bounds__(kRpThreads) void k_rp_join(RpArgs a, PairPack pp)
+{
+    __shared__ uint64_t sw[kRpLds];
+    const uint32_t p = blockIdx.x;
+    const uint32_t i0 = a.cnt[p], i1 = p + 1 < a.np ? a.cnt[p + 1] : a.cnt[a.np];
+    if (i0 == i1) return;
+    const uint64_t nb = (1ull << pp.D) + 1;  // dir entries [0, 2^D + 1]
+    const uint32_t w0 = a.dir[min((uint64_t)p << a.ps, nb)];
+    const uint32_t w1 = a.dir[min(((uint64_t)p + 1) << a.ps, nb)];
+    const uint32_t n = w1 - w0;
+    const bool lds = n <= kRpLds;
+    if (lds)
+        for (uint32_t j = threadIdx.x; j < n; j += kRpThreads) sw[j] = a.pk[w0 + j];
+    __syncthreads();
+    uint64_t tm[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) tm[q] = pp.tmv[q];
+    const uint64_t tmask = pp.tb >= 64 ? ~0ull : (1ull << pp.tb) - 1;
+    for (uint32_t it = i0 + threadIdx.x; it < i1; it += kRpThreads) {
+        const ulonglong2 q = a.items[it];
+        const uint64_t x = q.x;
+        const uint32_t r = (uint32_t)q.y;
+        const bool strict = (q.y >> 32) & 1;
+        uint32_t lo = 0, hi = n;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            const uint64_t v = lds ? sw[mid] : a.pk[w0 + mid];
+            if (strict ? v <= x : v < x)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        uint64_t rw = ~0ull;
+        const uint32_t g = w0 + lo;
+        if (g < a.nu) {
+            const uint64_t v = lo < n && lds ? sw[lo] : a.pk[g];
+            const uint64_t kp = pp.tb >= 64 ? 0 : x >> pp.tb;
+            if ((pp.tb >= 64 ? 0 : v >> pp.tb) == kp) {
+                const uint32_t wt = (uint32_t)(bits_expand(v & tmask, pp.tm, tm) | pp.tc);
+                if (wt != r) rw = ((uint64_t)r << 32) | wt;
+            }
+        }
+        const size_t o = (size_t)a.nu + a.nops + it;
+        a.ew[o] = rw;
+        if (a.et) a.et[o] = kDepRW, a.eg[o] = 0;
+        rp_back(a.diff, rw);
     }
 }
 
@@ -452,27 +698,26 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         if (e != hipSuccess) return e;        \
     } while (0)
     const size_t nops = in.nops;
-    // 1. writers -> unique sorted (key, txn)
-    CK(g.flags.ensure(4 * (nops + 1)));
-    CK(g.scratch.ensure(std::max(scan_scratch_bytes(nops + 1), (size_t)1024)));
-    if (nops) k_write_flags<<<blocks(nops), 256, 0, s>>>(nops, in.is_write, g.flags.as<uint32_t>());
-    CK(hipMemsetAsync(g.flags.as<uint32_t>() + nops, 0, 4, s));
-    CK(scan_exclusive_u32(g.flags.as<uint32_t>(), nops + 1, g.scratch.as<uint32_t>(), s));
-    uint32_t nw = 0;
-    CK(hipMemcpyAsync(&nw, g.flags.as<uint32_t>() + nops, 4, hipMemcpyDeviceToHost, s));
-    CK(hipStreamSynchronize(s));
-    const size_t wcap = std::max<size_t>(64, (nw + 63) & ~(size_t)63);
+    // 1. writers -> unique sorted (key, txn); room for every op (the count
+    // comes back with the gather)
+    const size_t wcap = std::max<size_t>(64, (nops + 63) & ~(size_t)63);
     CK(g.wg.ensure(4 * wcap));
     CK(g.ww.ensure(16 * wcap));
     CK(g.wl.ensure(8 * wcap));
     CK(g.wg2.ensure(4 * wcap));
     CK(g.ww2.ensure(16 * wcap));
     CK(g.wl2.ensure(8 * wcap));
+    CK(g.count.ensure(64));
+    CK(hipMemsetAsync(g.count.as<uint32_t>() + 8, 0, 4, s));
     if (nops)
-        k_gather_writers<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write,
-                                                      g.flags.as<uint32_t>(), g.wg.as<uint32_t>(),
-                                                      g.ww.as<uint64_t>(), g.wl.as<uint64_t>(), wcap);
+        k_gather_writers_blk<<<(unsigned)((nops + kGwThreads * kGwItems - 1) / (kGwThreads * kGwItems)),
+                               kGwThreads, 0, s>>>(nops, in.txn, in.key, in.is_write, g.count.as<uint32_t>() + 8,
+                                                   g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), g.wl.as<uint64_t>(),
+                                                   wcap);
     CK(hipGetLastError());
+    uint32_t nw = 0;
+    CK(hipMemcpyAsync(&nw, g.count.as<uint32_t>() + 8, 4, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
     size_t rsb = std::max(radix_scratch_bytes(nw, 2), scan_scratch_bytes(nw) + 64);
     rsb = std::max(rsb, packed_scratch_bytes(nw));
     CK(g.scratch.ensure(rsb));
@@ -514,9 +759,11 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     CK(hipStreamSynchronize(s));
     if (!nw) nu = 0;
     const uint64_t *wkey = dw->as<uint64_t>(), *wtxn = dw->as<uint64_t>() + wcap;
-    // 2. edges
-    const size_t ne_raw = (size_t)nu + 2 * nops + in.n_extra;
-    const size_t ecap = std::max<size_t>(64, (ne_raw + 63) & ~(size_t)63);
+    // 2. edges (capacity for the widest layout: nu + 2 nops + extras)
+    const size_t ne_cap = (size_t)nu + 2 * nops + in.n_extra;
+    const size_t ecap = std::max<size_t>(64, (ne_cap + 63) & ~(size_t)63);
+    size_t rw_rows = 0;
+    bool slot_layout = false, diff_done = false;
     CK(g.ew.ensure(8 * ecap));
     CK(g.et.ensure(8 * ecap));
     CK(g.eg.ensure(4 * ecap));
@@ -560,17 +807,55 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         while (pp.shift < 64 && ((pp.last - pp.base) >> pp.shift) >= ((uint64_t)1 << pp.D)) ++pp.shift;
         k_pair_dir<<<blocks(((size_t)1 << pp.D) + 2), 256, 0, s>>>(nu, g.pk.as<uint64_t>(), pp,
                                                                  g.pdir.as<uint32_t>());
-        k_edges_reads_pk<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu,
-                                                      wkey, wtxn, g.pk.as<uint64_t>(), g.pdir.as<uint32_t>(),
-                                                      pp, g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0);
+        static const bool rp = getenv("HSC_GRAPH_RP") == nullptr || atoi(getenv("HSC_GRAPH_RP")) != 0;  // (A/B)
+        if (rp) {
+            RpArgs a{};
+            a.nops = nops, a.txn = in.txn, a.key = in.key, a.is_write = in.is_write, a.observed = in.observed;
+            a.nu = nu, a.wkey = wkey, a.wtxn = wtxn, a.pk = g.pk.as<uint64_t>(), a.dir = g.pdir.as<uint32_t>();
+            a.ps = pp.D > kRpBitsMax ? (uint32_t)(pp.D - kRpBitsMax) : 0;
+            a.np = (uint32_t)((((uint64_t)1 << pp.D) >> a.ps) + 1);
+            CK(g.rp_cnt.ensure(8 * ((size_t)a.np + 2)));
+            a.cnt = g.rp_cnt.as<uint32_t>();
+            a.cur = a.cnt + a.np + 1;
+            CK(g.rp_items.ensure(16 * std::max<size_t>(nops, 1)));
+            a.items = g.rp_items.as<ulonglong2>();
+            a.ew = g.ew.as<uint64_t>(), a.et = et, a.eg = eg, a.skip_rw = in.skip_rw ? 1 : 0;
+            // raw builds (the sharded SCC's): the cover's backward-edge diffs as
+            // the rows are emitted (ww rows are forward: txns ascend inside a key)
+            if (!full && !in.n_extra && in.ntxn) {
+                CK(g.diff.ensure(4 * ((size_t)in.ntxn + 2)));
+                CK(hipMemsetAsync(g.diff.p, 0, 4 * ((size_t)in.ntxn + 2), s));
+                a.diff = g.diff.as<uint32_t>();
+                diff_done = true;
+            }
+            CK(hipMemsetAsync(a.cnt, 0, 4 * ((size_t)a.np + 1), s));
+            k_rp_count<<<blocks(nops), kRpThreads, 0, s>>>(a, pp);
+            k_rp_scan<<<1, 1024, 0, s>>>(a);
+            k_rp_scatter<<<blocks(nops), kRpThreads, 0, s>>>(a, pp);
+            k_rp_join<<<a.np, kRpThreads, 0, s>>>(a, pp);
+            CK(hipGetLastError());
+            uint32_t tot[2];
+            CK(hipMemcpyAsync(&tot[0], a.cnt + a.np, 4, hipMemcpyDeviceToHost, s));
+            CK(hipMemcpyAsync(&tot[1], a.cur + a.np, 4, hipMemcpyDeviceToHost, s));
+            CK(hipStreamSynchronize(s));
+            rw_rows = (size_t)tot[0] + tot[1];
+            slot_layout = true;
+        } else {
+            k_edges_reads_pk<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu,
+                                                          wkey, wtxn, g.pk.as<uint64_t>(), g.pdir.as<uint32_t>(),
+                                                          pp, g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0);
+        }
     } else if (nops) {
         k_edges_reads<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed,
                                                    nu, wkey, wtxn, g.ew.as<uint64_t>(), et, eg,
                                                    in.skip_rw ? 1 : 0);
     }
     CK(hipGetLastError());
+    // the partitioned search filled [nu, nu + nops + rw_rows) (else [nu, nu + 2 nops))
+    const size_t ne_hist = slot_layout ? (size_t)nu + nops + rw_rows : (size_t)nu + 2 * nops;
+    const size_t ne_raw = ne_hist + in.n_extra;
     if (in.n_extra) {  // staged edges (rw pairs of the validator's join) after the history's
-        const size_t o = (size_t)nu + 2 * nops;
+        const size_t o = ne_hist;
         CK(hipMemcpyAsync(g.ew.as<uint64_t>() + o, in.x_rows, 8 * in.n_extra,
                           hipMemcpyDeviceToDevice, s));
         CK(hipMemcpyAsync(g.et.as<uint64_t>() + o, in.x_type, 8 * in.n_extra,
@@ -579,6 +864,8 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     }
     g.raw = !full;
     g.ne_raw = ne_raw;
+    g.diff_nn = diff_done ? in.ntxn : 0;  // graph_cover: the diffs are there already
+    g.cover_nn = in.ntxn;
     if (!full) {  // raw edge rows only (duplicates, ~0 holes): enough for cover / cut
         g.ne = 0;
         return hipSuccess;
@@ -877,9 +1164,12 @@ hipError_t graph_cover(GraphBufs &g, uint32_t nn, uint8_t *cover, hipStream_t s)
     if ((e = diff.ensure(4 * ((size_t)nn + 2))) != hipSuccess) return e;
     if ((e = scratch.ensure(std::max(scan_scratch_bytes((size_t)nn + 1), (size_t)1024))) != hipSuccess)
         return e;
-    if ((e = hipMemsetAsync(diff.p, 0, 4 * ((size_t)nn + 2), s)) != hipSuccess) return e;
-    const EdgeSet es = edge_set(g);
-    if (es.n) k_back_diff<<<blocks(es.n), 256, 0, s>>>(es, diff.as<uint32_t>());
+    if (!(g.raw && g.diff_nn == nn)) {  // (a raw build accumulated them while emitting its rows)
+        if ((e = hipMemsetAsync(diff.p, 0, 4 * ((size_t)nn + 2), s)) != hipSuccess) return e;
+        const EdgeSet es = edge_set(g);
+        if (es.n) k_back_diff<<<blocks(es.n), 256, 0, s>>>(es, diff.as<uint32_t>());
+    }
+    g.diff_nn = 0;  // (the scan below consumes them)
     if ((e = scan_exclusive_u32(diff.as<uint32_t>(), (size_t)nn + 1, scratch.as<uint32_t>(), s)) !=
         hipSuccess)
         return e;
@@ -890,11 +1180,23 @@ hipError_t graph_cover(GraphBufs &g, uint32_t nn, uint8_t *cover, hipStream_t s)
 // One pass for the usual tiny cut: edges with both ends covered appended
 // at a wave-aggregated atomic cursor (rows beyond cap are counted, not
 // stored: the caller then takes the flag + scan path).
-__global__ void k_cut_append(EdgeSet es, const uint8_t *cover, uint64_t *rows, uint32_t *cnt, uint32_t cap)
+// The cover as a bitmap (bit v of word v / 64): 2 MB for 16.7M txns stays in
+// L2, where the byte array's 16.7 MB did not (the cut tests both ends of
+// every edge row).
+__global__ void k_cover_bits(uint32_t nn, const uint8_t *cover, uint64_t *bits)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t m = __ballot(v < nn && cover[v] != 0);
+    if ((threadIdx.x & 63) == 0 && v < nn) bits[v >> 6] = m;
+}
+
+__device__ __forceinline__ bool cover_bit(const uint64_t *bits, uint32_t v) { return (bits[v >> 6] >> (v & 63)) & 1; }
+
+__global__ void k_cut_append(EdgeSet es, const uint64_t *cover, uint64_t *rows, uint32_t *cnt, uint32_t cap)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t a = 0, b = 0;
-    const bool hit = i < es.n && es.get(i, a, b) && cover[a] && cover[b];
+    const bool hit = i < es.n && es.get(i, a, b) && cover_bit(cover, a) && cover_bit(cover, b);
     const uint64_t m = __ballot(hit);
     if (!m) return;
     const int lane = threadIdx.x & 63, first = __ffsll((unsigned long long)m) - 1;
@@ -918,8 +1220,11 @@ hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t 
         if ((e = g.cut.ensure(8 * (size_t)kCutFastCap)) != hipSuccess) return e;
         if ((e = g.count.ensure(64)) != hipSuccess) return e;
         if ((e = hipMemsetAsync(g.count.p, 0, 4, s)) != hipSuccess) return e;
-        if (ne) k_cut_append<<<blocks(ne), 256, 0, s>>>(es, cover, g.cut.as<uint64_t>(), g.count.as<uint32_t>(),
-                                                        kCutFastCap);
+        const uint32_t nn = g.cover_nn;
+        if ((e = g.cover_bits.ensure(8 * ((size_t)nn / 64 + 2))) != hipSuccess) return e;
+        if (nn) k_cover_bits<<<blocks(nn), 256, 0, s>>>(nn, cover, g.cover_bits.as<uint64_t>());
+        if (ne) k_cut_append<<<blocks(ne), 256, 0, s>>>(es, g.cover_bits.as<uint64_t>(), g.cut.as<uint64_t>(),
+                                                        g.count.as<uint32_t>(), kCutFastCap);
         uint32_t k = 0;
         if ((e = hipMemcpyAsync(&k, g.count.p, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;

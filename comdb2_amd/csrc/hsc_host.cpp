@@ -1147,6 +1147,7 @@ static int flush_appends(hsc_ctx *c, bool lazy = false)
         if (c->dn + k > kDeltaCap && c->dn && !c->merge_pending) HIPCHK_RC(c, fold_start(c));
     }
     if (k && (sync_only || c->merge_pending || c->dn + k > kDeltaCap)) {
+        if (!sync_only && c->dn + k > kDeltaCap) c->merge_is_fold = true;  // the run is full
         c->merge_pending = true;
         c->dirty = true;  // rows stay in app_* for merge_delta (or in h_* for a host rebuild)
         return HSC_OK;
@@ -1223,6 +1224,7 @@ static int flush_appends(hsc_ctx *c, bool lazy = false)
     if (c->dn >= c->fold_rows) {
         if (!c->fold_bg) {  // inline: the next check folds
             c->merge_pending = true;
+            c->merge_is_fold = true;
             c->dirty = true;
         } else if (c->fold_state.load(std::memory_order_acquire) == kFoldIdle) {
             HIPCHK_RC(c, fold_start(c));
@@ -1364,79 +1366,146 @@ static hipError_t create_stream(hipStream_t *st, bool high)
     return hipStreamCreateWithPriority(st, hipStreamNonBlocking, high ? greatest : least);
 }
 
-static int shadow_ctx(hsc_ctx *c)
+// The fold worker (one host thread per context, started by its first fold):
+// it creates the shadow context and its low-priority stream itself, then
+// for every job copies the main window's versions and the frozen run into
+// the shadow's buffers on the shadow's stream -- after the event fold_start
+// recorded behind everything queued on the context's stream -- and rebuilds
+// there.  An append that triggers a fold only captures the job and records
+// that event (no stream creation, allocation or copy on the commit path).
+static void fold_worker(hsc_ctx *c)
 {
-    if (c->shadow) return HSC_OK;
-    hsc_ctx *s = new (std::nothrow) hsc_ctx();
-    if (!s) return fail(c, HSC_ENOMEM, "fold context");
-    s->device = c->device;
-    if (create_stream(&s->own_stream, false) != hipSuccess) {
-        delete s;
-        return fail(c, HSC_EDEVICE, "fold stream");
+    for (;;) {
+        hsc_ctx::FoldJob j;
+        {
+            std::unique_lock<std::mutex> g(c->fold_mu);
+            c->fold_cv.wait(g, [c] { return c->fold_job || c->fold_quit; });
+            if (c->fold_quit) return;
+            c->fold_job = false;
+            j = std::move(c->fold_jobv);
+        }
+        (void)hipSetDevice(c->device);
+        int rc = HSC_OK;
+        std::string why;
+        hsc_ctx *s = c->shadow;
+        if (!s) {
+            s = new (std::nothrow) hsc_ctx();
+            if (s) {
+                s->device = c->device;
+                if (create_stream(&s->own_stream, false) != hipSuccess) {
+                    delete s;
+                    s = nullptr;
+                } else {
+                    s->stream = s->own_stream;
+                }
+            }
+            if (!s) rc = HSC_EDEVICE, why = "fold context";
+            c->shadow = s;  // (read by the caller's thread only after kFoldDone)
+        }
+        if (rc == HSC_OK) {
+            s->groups = std::move(j.groups);  // what device_build reads of the dictionaries
+            s->table_names = std::move(j.table_names);
+            s->h_table_max = std::move(j.table_max);
+            s->layout = j.layout;
+            s->paths = j.paths;
+            s->W = j.W;
+            const size_t nm = j.nm, nf = j.nf, n_in = nm + nf;
+            const int W = j.W;
+            s->cap = window_cap(n_in);
+            hipStream_t ss = s->stream;
+            hipError_t e = s->d_gid.ensure(4 * s->cap);
+            if (e == hipSuccess) e = s->d_words.ensure(8 * (size_t)W * s->cap);
+            if (e == hipSuccess) e = s->d_lsn.ensure(8 * s->cap);
+            if (e == hipSuccess) e = hipStreamWaitEvent(ss, c->fold_ev, 0);
+            auto cp = [&](void *dst, const void *src, size_t b) {
+                if (e == hipSuccess && b) e = hipMemcpyAsync(dst, src, b, hipMemcpyDeviceToDevice, ss);
+            };
+            cp(s->d_gid.p, j.gid2, 4 * nm);
+            cp(s->d_lsn.p, j.lsn2, 8 * nm);
+            cp(s->d_gid.as<uint32_t>() + nm, j.fgid, 4 * nf);
+            cp(s->d_lsn.as<uint64_t>() + nm, j.flsn, 8 * nf);
+            for (int w = 0; w < W; ++w) {
+                uint64_t *dst = s->d_words.as<uint64_t>() + (size_t)w * s->cap;
+                cp(dst, (const uint64_t *)j.words2 + (size_t)w * j.cap, 8 * nm);
+                cp(dst + nm, (const uint64_t *)j.fwords + (size_t)w * j.dcap, 8 * nf);
+            }
+            if (e != hipSuccess) {
+                rc = HSC_EDEVICE, why = std::string("fold copies: ") + hipGetErrorString(e);
+            } else {
+                rc = device_build(s, n_in);
+                if (rc) why = s->err;
+            }
+        }
+        {
+            std::lock_guard<std::mutex> g(c->fold_mu);
+            c->fold_rc = rc;
+            c->fold_err = why;
+            c->fold_state.store(kFoldDone, std::memory_order_release);
+        }
+        c->fold_cv.notify_all();
     }
-    s->stream = s->own_stream;
-    c->shadow = s;
-    if (!c->fold_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fold_ev, hipEventDisableTiming));
-    return HSC_OK;
 }
 
-// Freeze the live run and start rebuilding the main window with it in the
-// background: the shadow's stream copies the main window's versions (d_*2)
-// and the frozen rows after everything queued on c->stream so far (the run's
-// last merge, and the readers of the shadow's buffers -- the window before
-// the last swap), and a host thread runs the build.
+// Until a running fold's job is done.
+static void fold_wait(hsc_ctx *c)
+{
+    std::unique_lock<std::mutex> g(c->fold_mu);
+    c->fold_cv.wait(g, [c] { return c->fold_state.load(std::memory_order_acquire) != kFoldRunning; });
+}
+
+static void fold_stop(hsc_ctx *c)
+{
+    if (!c->fold_thread.joinable()) return;
+    fold_wait(c);
+    {
+        std::lock_guard<std::mutex> g(c->fold_mu);
+        c->fold_quit = true;
+    }
+    c->fold_cv.notify_all();
+    c->fold_thread.join();
+}
+
+// Freeze the live run and hand the rebuild of the main window with it to the
+// fold worker: the run's buffers become the frozen run (probed beside the
+// main window and a fresh live run until the swap), the job captures what
+// the build reads, and an event behind everything queued on the context's
+// stream so far (the run's last merge, and the readers of the shadow's
+// buffers -- the window before the last swap) orders the worker's copies.
 static int fold_start(hsc_ctx *c)
 {
-    HIPCHK_RC(c, shadow_ctx(c));
-    hsc_ctx *s = c->shadow;
+    if (!c->fold_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fold_ev, hipEventDisableTiming));
+    if (!c->fold_thread.joinable()) {
+        try {
+            c->fold_thread = std::thread(fold_worker, c);
+        } catch (...) {
+            c->merge_pending = c->dirty = true;  // no worker: the run is merged inline
+            c->merge_is_fold = true;
+            return HSC_OK;
+        }
+    }
     std::swap(c->d_dgid[c->dcur], c->f_dgid);
     std::swap(c->d_dwords[c->dcur], c->f_dwords);
     std::swap(c->d_dlsn[c->dcur], c->f_dlsn);
     std::swap(c->d_dbmax, c->f_dbmax);
     c->fn = c->dn;
     c->dn = 0;
-    s->groups = c->groups;  // what device_build reads of the dictionaries
-    s->table_names = c->table_names;
-    s->h_table_max = c->h_table_max;
-    s->layout = c->layout;
-    s->paths = c->paths;
-    s->W = c->W;
-    const size_t nm = c->n_all, nf = c->fn, n_in = nm + nf;
-    s->cap = window_cap(n_in);
-    const int W = c->W;
-    HIPCHK(c, s->d_gid.ensure(4 * s->cap));
-    HIPCHK(c, s->d_words.ensure(8 * (size_t)W * s->cap));
-    HIPCHK(c, s->d_lsn.ensure(8 * s->cap));
     HIPCHK(c, hipEventRecord(c->fold_ev, c->stream));
-    hipStream_t ss = s->stream;
-    HIPCHK(c, hipStreamWaitEvent(ss, c->fold_ev, 0));
-    HIPCHK(c, hipMemcpyAsync(s->d_gid.p, c->d_gid2.p, 4 * nm, hipMemcpyDeviceToDevice, ss));
-    HIPCHK(c, hipMemcpyAsync(s->d_lsn.p, c->d_lsn2.p, 8 * nm, hipMemcpyDeviceToDevice, ss));
-    HIPCHK(c, hipMemcpyAsync(s->d_gid.as<uint32_t>() + nm, c->f_dgid.p, 4 * nf, hipMemcpyDeviceToDevice, ss));
-    HIPCHK(c, hipMemcpyAsync(s->d_lsn.as<uint64_t>() + nm, c->f_dlsn.p, 8 * nf, hipMemcpyDeviceToDevice, ss));
-    for (int j = 0; j < W; ++j) {
-        uint64_t *dst = s->d_words.as<uint64_t>() + (size_t)j * s->cap;
-        HIPCHK(c, hipMemcpyAsync(dst, c->d_words2.as<uint64_t>() + (size_t)j * c->cap, 8 * nm,
-                                 hipMemcpyDeviceToDevice, ss));
-        HIPCHK(c, hipMemcpyAsync(dst + nm, c->f_dwords.as<uint64_t>() + (size_t)j * c->dcap, 8 * nf,
-                                 hipMemcpyDeviceToDevice, ss));
+    {
+        std::lock_guard<std::mutex> g(c->fold_mu);
+        hsc_ctx::FoldJob &j = c->fold_jobv;
+        j.nm = c->n_all, j.nf = c->fn, j.cap = c->cap, j.dcap = c->dcap;
+        j.W = c->W, j.layout = c->layout, j.paths = c->paths;
+        j.gid2 = c->d_gid2.p, j.lsn2 = c->d_lsn2.p, j.words2 = c->d_words2.p;
+        j.fgid = c->f_dgid.p, j.flsn = c->f_dlsn.p, j.fwords = c->f_dwords.p;
+        j.groups = c->groups;
+        j.table_names = c->table_names;
+        j.table_max = c->h_table_max;
+        c->fold_rc = HSC_OK;
+        c->fold_state.store(kFoldRunning, std::memory_order_release);
+        c->fold_job = true;
     }
-    c->fold_rc = HSC_OK;
-    c->fold_state.store(kFoldRunning, std::memory_order_release);
+    c->fold_cv.notify_all();
     c->folds_started++;
-    try {
-        c->fold_thread = std::thread([c, s, n_in] {
-            (void)hipSetDevice(s->device);
-            const int rc = device_build(s, n_in);
-            c->fold_rc = rc;
-            c->fold_state.store(kFoldDone, std::memory_order_release);
-        });
-    } catch (...) {
-        c->fold_state.store(kFoldIdle, std::memory_order_release);
-        (void)hipStreamSynchronize(ss);
-        c->merge_pending = c->dirty = true;  // the frozen run is merged inline instead
-        return HSC_OK;
-    }
     return HSC_OK;
 }
 
@@ -1447,12 +1516,13 @@ static int fold_finish(hsc_ctx *c, bool wait)
 {
     const int st = c->fold_state.load(std::memory_order_acquire);
     if (st == kFoldIdle || (st == kFoldRunning && !wait)) return HSC_OK;
-    c->fold_thread.join();
+    fold_wait(c);
     c->fold_state.store(kFoldIdle, std::memory_order_relaxed);
     hsc_ctx *s = c->shadow;
-    if (c->fold_rc != HSC_OK) {
+    if (c->fold_rc != HSC_OK || !s) {
         c->merge_pending = c->dirty = true;
-        (void)fail(c, c->fold_rc, ("background fold: " + s->err).c_str());
+        c->merge_is_fold = true;
+        (void)fail(c, c->fold_rc ? c->fold_rc : HSC_EDEVICE, ("background fold: " + c->fold_err).c_str());
         return HSC_OK;
     }
     HIPCHK(c, wait_lanes(c));  // batches of other streams finish on the old window
@@ -1475,7 +1545,7 @@ static int fold_finish(hsc_ctx *c, bool wait)
 static void fold_discard(hsc_ctx *c)
 {
     if (c->fold_state.load(std::memory_order_acquire) != kFoldIdle) {
-        c->fold_thread.join();
+        fold_wait(c);
         c->fold_state.store(kFoldIdle, std::memory_order_relaxed);
     }
     c->fn = 0;
@@ -1501,7 +1571,8 @@ static int ensure_built(hsc_ctx *c)
         if (!c->host_staged) c->merge_pending = true;
     }
     if (!c->dirty) return HSC_OK;
-    if (c->merge_pending) c->folds_inline++;
+    if (c->merge_pending && c->merge_is_fold) c->folds_inline++;  // (a new group / wider key: a rebuild)
+    c->merge_is_fold = false;
     if (c->host_staged) {  // staged rows include the appended ones (and a frozen run's)
         fold_discard(c);
         return build_from_host(c);
@@ -3127,6 +3198,7 @@ void hsc_ctx_destroy(hsc_ctx *c)
     for (hipStream_t &st : c->small_side)
         if (st) (void)hipStreamSynchronize(st), (void)hipStreamDestroy(st), st = nullptr;
     fold_discard(c);
+    fold_stop(c);
     if (c->shadow) hsc_ctx_destroy(c->shadow);
     c->shadow = nullptr;
     (void)hipStreamSynchronize(c->stream);

@@ -463,18 +463,23 @@ struct GraphBufs {
     DBuf diff, cut, cut_id, txn_of;            // sharded SCC: cover, cut rows, cut ids
     DBuf x_rows, x_type, x_map;                // staged extra edges (rw pairs)
     DBuf pk, pdir;                             // packed distinct writers + their directory
+    DBuf rp_cnt, rp_items;                     // partitioned read search: counts / cursors, items
     size_t n_extra = 0;
     size_t ne = 0;
     size_t ne_raw = 0;  // raw edge slots in ew
     bool raw = false;   // last build kept raw rows only (no sort / CSR)
     bool writer_packed = false;  // last build sorted its writers as packed (key, txn) words
+    uint32_t diff_nn = 0;        // raw build: diff holds the cover's backward-edge diffs over diff_nn txns
+    uint32_t cover_nn = 0;       // txns of the covers graph_cut tests (the build's ntxn)
+    DBuf cover_bits;             // graph_cut: the cover as a bitmap
     void release_all()
     {
         DBuf *all[] = {&flags, &flags2, &scratch, &count, &wg, &ww, &wl, &wg2, &ww2, &wl2,
                        &ew, &et, &eg, &ew2, &et2, &eg2, &swap_rows, &src, &out_dst, &type,
                        &in_src, &in_dst, &out_off, &in_off, &scc, &active, &color, &mark,
                        &front, &front2, &h_txn, &h_key, &h_isw, &h_obs, &diff, &cut,
-                       &cut_id, &txn_of, &x_rows, &x_type, &x_map, &pk, &pdir};
+                       &cut_id, &txn_of, &x_rows, &x_type, &x_map, &pk, &pdir, &rp_cnt,
+                       &rp_items, &cover_bits};
         for (DBuf *b : all) b->release();
     }
 };

@@ -160,6 +160,12 @@ struct Multi {
     // rows and (the SCC's member) every member's cut rows
     DBuf g_cover[kMultiMax], g_rows[kMultiMax], g_all[kMultiMax], g_sz[kMultiMax];
     double g_ms[4] = {};  // host ms of its last call: build + cover, cover merge, cuts + gather, SCC
+    // window placement (hsc_multi_set_mode): pieces or replicas
+    int mode = HSC_MULTI_AUTO;
+    bool replicated = false;            // in force since the last build / adopt
+    std::atomic<int> inflight[kMultiMax] = {};  // replicas: drop-in batches running per member
+    std::atomic<uint32_t> rr{0};
+    std::atomic<uint64_t> rep_calls{0}, rep_sliced{0};
     bool timing = false;  // events around every member's probe (per-member probe times)
     int last_lane = 0;
     // host copies of the last pipeline's counts
@@ -169,6 +175,10 @@ struct Multi {
     // batch, launching the counts, waiting for them, enqueueing the rest
     uint64_t ns_lane = 0, ns_count = 0, ns_count_wait = 0, ns_enqueue = 0;
     uint64_t pr_batches = 0, ns_pr = 0;  // hsc_multi_probe_routed: batches, host time enqueueing them
+    // its split: lane_acquire (the members' cross-lane event waits), the
+    // members' probe launches, the owners' merges + done events
+    uint64_t ns_pr_lane = 0, ns_pr_probe = 0, ns_pr_merge = 0;
+    uint64_t ns_pm_probe = 0, ns_pm_merge = 0;  // probe_merge's last call: probes, merges
 };
 
 static int mfail(hsc_ctx *c, int code, const char *what, hipError_t e = hipSuccess)
@@ -319,6 +329,25 @@ void multi_sync_dict(hsc_ctx *f)
 }
 
 // ---- window -------------------------------------------------------------------
+// Placement of a host-staged window of n rows of W key words: replicas when
+// asked, or (AUTO) when n x (8 W + 16) bytes fit an eighth of the smallest
+// local member's device memory (every rank of a per-rank context sees the
+// same log and the same GPUs, so all choose alike).
+static bool choose_replicas(hsc_ctx *f, Multi *M, size_t n, int W)
+{
+    if (M->mode != HSC_MULTI_AUTO) return M->mode == HSC_MULTI_REPLICAS;
+    if (M->sp_given) return false;  // splitters were set: the caller cut pieces
+    size_t lim = ~(size_t)0;
+    for (int m = 0; m < M->nlocal; ++m) {
+        size_t fr = 0, tot = 0;
+        if (hipSetDevice(M->mem[m]->device) != hipSuccess || hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
+        lim = std::min(lim, tot / 8);
+    }
+    (void)hipSetDevice(f->device);
+    return (double)n * (8.0 * W + 16.0) <= (double)lim;
+}
+
+
 // Build the members' windows from the front's host-staged rows (a decoded log
 // or appended writes): the rows of each member's piece, in log order.
 int multi_build(hsc_ctx *f)
@@ -333,16 +362,19 @@ int multi_build(hsc_ctx *f)
     const int W = ctx_window_words(f);
     if (f->W != W) f->dict_epoch++;
     f->W = W;
-    if (!M->sp_given) auto_splitters(f, M, W);
-    MRC(upload_splitters(f, M, W));  // before the rows are placed: one routing rule
-    multi_sync_dict(f);
     const size_t n = f->h_gid.size();
-    std::vector<int> own(n);
-    std::vector<uint64_t> x((size_t)W);
-    for (size_t i = 0; i < n; ++i) {
-        row_key(f, i, W, x.data());
-        own[i] = sp_owner(M, f->h_gid[i], x.data(), W);
+    M->replicated = choose_replicas(f, M, n, W);
+    std::vector<int> own(M->replicated ? 0 : n);
+    if (!M->replicated) {
+        if (!M->sp_given) auto_splitters(f, M, W);
+        MRC(upload_splitters(f, M, W));  // before the rows are placed: one routing rule
+        std::vector<uint64_t> x((size_t)W);
+        for (size_t i = 0; i < n; ++i) {
+            row_key(f, i, W, x.data());
+            own[i] = sp_owner(M, f->h_gid[i], x.data(), W);
+        }
     }
+    multi_sync_dict(f);
     for (int m = 0; m < M->nlocal; ++m) {
         hsc_ctx *c = M->mem[m];
         const int me = M->rank + m;
@@ -353,7 +385,7 @@ int multi_build(hsc_ctx *f)
         c->h_table_max = f->h_table_max;
         c->max_commit = f->max_commit;
         for (size_t i = 0; i < n; ++i) {
-            if (own[i] != me) continue;
+            if (!M->replicated && own[i] != me) continue;  // (replicas: every row)
             c->h_gid.push_back(f->h_gid[i]);
             c->h_keyoff.push_back(c->h_keys.size());
             const int klen = f->groups[f->h_gid[i]].klen;
@@ -368,7 +400,7 @@ int multi_build(hsc_ctx *f)
     }
     size_t keys = 0;
     for (int m = 0; m < M->nlocal; ++m) keys += M->mem[m]->n;
-    f->n = keys;
+    f->n = M->replicated ? M->mem[0]->n : keys;
     f->dirty = false;
     f->live = true;
     f->merge_pending = false;
@@ -400,6 +432,10 @@ int multi_flush_appends(hsc_ctx *f, bool lazy)
         memset(buf, 0, (size_t)W * 8);
         if (klen) memcpy(buf, f->app_keys.data() + f->app_koff[i], (size_t)klen);
         for (int j = 0; j < W; ++j) x[j] = load_be64(buf + 8 * j);
+        if (M->replicated) {  // every member holds every row
+            for (int m = 0; m < M->nlocal; ++m) rows[m].push_back(i);
+            continue;
+        }
         const int o = sp_owner(M, f->app_gid[i], x.data(), W) - M->rank;
         if (o >= 0 && o < M->nlocal) rows[o].push_back(i);
     }
@@ -574,6 +610,7 @@ static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb,
         return HSC_OK;
     };
     int prc[kMultiMax] = {};
+    const auto tp0 = SteadyClock::now();
     // (members sharing a GPU: one thread -- its launches serialise anyway;
     // HSC_MULTI_PAR_LAUNCH=1 issues them from the pool there too, an A/B)
     static const bool par_env = getenv("HSC_MULTI_PAR_LAUNCH") != nullptr;
@@ -583,6 +620,7 @@ static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb,
         for (int m = 0; m < NL; ++m) prc[m] = probe_one(m);
     for (int m = 0; m < NL; ++m)
         if (prc[m]) return mfail(f, prc[m], ("member probe: " + M->mem[m]->err).c_str());
+    const auto tp1 = SteadyClock::now();
     M->last_lane = L;
     // 7. OR of the members' bitmaps per owner
     if (N == 1) {
@@ -668,6 +706,9 @@ static int probe_merge(hsc_ctx *f, int L, hsc_probe_batch *in, const size_t *tb,
         ml.used = true;
     }
     M->batches++;
+    const auto tp2 = SteadyClock::now();
+    M->ns_pm_probe = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(tp1 - tp0).count();
+    M->ns_pm_merge = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(tp2 - tp1).count();
     return HSC_OK;
 }
 
@@ -1017,9 +1058,191 @@ static int route_host(hsc_ctx *f, const Stage &st, Stage *out, int only, uint32_
 // routing and the RCCL exchange.
 static int check_stage_device(hsc_ctx *f, Stage &st, int *rc_out);
 
+// ---- replicas: whole batches (or read-set slices) to single members ------------
+// The member with the fewest drop-in batches in flight, round robin among
+// equals (a lone caller alternates members; concurrent callers spread).
+static int pick_member(Multi *M)
+{
+    const int NL = M->nlocal;
+    const int start = (int)(M->rr.fetch_add(1, std::memory_order_relaxed) % (uint32_t)NL);
+    int best = start, bv = M->inflight[start].load(std::memory_order_relaxed);
+    for (int k = 1; k < NL && bv > 0; ++k) {
+        const int m = (start + k) % NL;
+        const int x = M->inflight[m].load(std::memory_order_relaxed);
+        if (x < bv) best = m, bv = x;
+    }
+    return best;
+}
+
+// Read sets [t0, t1) of the marshalled batch st (probes and lock probes are in
+// read-set order) into o for member c: the columns copied, read sets
+// renumbered from 0, sized for c's small path when it fits.
+static int replica_slice(hsc_ctx *f, hsc_ctx *c, const Stage &st, size_t t0, size_t t1, Stage &o)
+{
+    const int W = f->W;
+    const size_t n = st.n, nl = st.n_lock;
+    const uint32_t *txn = st.col<uint32_t>(st.L.txn), *ltx = st.col<uint32_t>(st.L.lock_txn);
+    const size_t a = (size_t)(std::lower_bound(txn, txn + n, (uint32_t)t0) - txn);
+    const size_t e = (size_t)(std::lower_bound(txn + a, txn + n, (uint32_t)t1) - txn);
+    const size_t la = (size_t)(std::lower_bound(ltx, ltx + nl, (uint32_t)t0) - ltx);
+    const size_t le = (size_t)(std::lower_bound(ltx + la, ltx + nl, (uint32_t)t1) - ltx);
+    const size_t k = e - a, kl = le - la, T = t1 - t0;
+    o.L = stage_layout(W, k, kl);
+    o.n = k, o.n_lock = kl, o.n_txn = T;
+    o.coh = ctx_small_fits(c, T, k, kl);
+    if (o.arena.ensure(std::max<size_t>(o.L.total + (o.coh ? small_tail(T) : 0), 256), true, o.coh) ||
+        o.forced.ensure(std::max<size_t>(T, 1), true))
+        return mfail(f, HSC_ENOMEM, "multi replica staging");
+    memset(o.forced.p, 0, std::max<size_t>(T, 1));  // the front's forced verdicts are OR-ed in
+    for (int j = 0; j < W; ++j) {
+        memcpy(o.col<uint64_t>(o.L.lo) + (size_t)j * k, st.col<uint64_t>(st.L.lo) + (size_t)j * n + a, 8 * k);
+        memcpy(o.col<uint64_t>(o.L.hi) + (size_t)j * k, st.col<uint64_t>(st.L.hi) + (size_t)j * n + a, 8 * k);
+    }
+    memcpy(o.col<uint64_t>(o.L.snap), st.col<uint64_t>(st.L.snap) + a, 8 * k);
+    memcpy(o.col<uint32_t>(o.L.gid), st.col<uint32_t>(st.L.gid) + a, 4 * k);
+    uint32_t *ot = o.col<uint32_t>(o.L.txn);
+    for (size_t i = 0; i < k; ++i) ot[i] = txn[a + i] - (uint32_t)t0;
+    memcpy(o.col<uint64_t>(o.L.lock_snap), st.col<uint64_t>(st.L.lock_snap) + la, 8 * kl);
+    memcpy(o.col<uint32_t>(o.L.lock_table), st.col<uint32_t>(st.L.lock_table) + la, 4 * kl);
+    uint32_t *olt = o.col<uint32_t>(o.L.lock_txn);
+    for (size_t i = 0; i < kl; ++i) olt[i] = ltx[la + i] - (uint32_t)t0;
+    return HSC_OK;
+}
+
+// A drop-in batch on a replicated window: one member checks it whole when it
+// fits the small path (one member kernel per call), else its read sets are
+// cut into one slice per local member.  The members' verdicts land in their
+// slices of rc_out (no OR across members: each read set is checked once).
+static int replica_check(hsc_ctx *f, Stage &st, int *rc_out, std::unique_lock<std::mutex> *lk)
+{
+    Multi *M = f->multi;
+    const int NL = M->nlocal;
+    const size_t T = st.n_txn;
+    const auto t0 = SteadyClock::now();
+    Multi::StageSet *set = nullptr;
+    {
+        std::lock_guard<std::mutex> g(M->set_mu);
+        if (M->free_sets.empty()) {
+            M->sets.emplace_back(new (std::nothrow) Multi::StageSet());
+            if (!M->sets.back()) {
+                M->sets.pop_back();
+                return mfail(f, HSC_ENOMEM, "multi replica staging");
+            }
+            M->free_sets.push_back(M->sets.back().get());
+        }
+        set = M->free_sets.back();
+        M->free_sets.pop_back();
+    }
+    auto give_back = [&] {
+        std::lock_guard<std::mutex> g(M->set_mu);
+        M->free_sets.push_back(set);
+    };
+    const uint64_t epoch = M->part_epoch.load(std::memory_order_acquire);
+    int parts = 1, mem_of[kMultiMax];
+    size_t tb[kMultiMax + 1] = {0, T};
+    if (NL > 1 && !ctx_small_fits(M->mem[0], T, st.n, st.n_lock)) {
+        parts = (int)std::min<size_t>((size_t)NL, std::max<size_t>(1, T / 64));
+        const int first = (int)(M->rr.fetch_add(1, std::memory_order_relaxed) % (uint32_t)NL);
+        for (int p = 0; p < parts; ++p) mem_of[p] = (first + p) % NL, tb[p] = T * (size_t)p / (size_t)parts;
+        tb[parts] = T;
+        M->rep_sliced.fetch_add(1, std::memory_order_relaxed);
+    } else {
+        mem_of[0] = pick_member(M);
+    }
+    Stage *ms = set->s;
+    int rc = HSC_OK;
+    for (int p = 0; p < parts && rc == HSC_OK; ++p) rc = replica_slice(f, M->mem[mem_of[p]], st, tb[p], tb[p + 1], ms[p]);
+    if (rc) {
+        give_back();
+        return rc;
+    }
+    const uint8_t *fc = st.forced.as<uint8_t>();
+    for (size_t t = 0; t < T; ++t) rc_out[t] = fc[t] ? 1 : 0;
+    const auto t1 = SteadyClock::now();
+    M->h_calls++;
+    M->ns_route += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+    M->rep_calls.fetch_add(1, std::memory_order_relaxed);
+    if (lk) lk->unlock();  // the batch is in the call's own set
+    int slot[kMultiMax];
+    bool run[kMultiMax] = {};
+    int nrun = 0, fail_p = -1;
+    for (int p = 0; p < parts && rc == HSC_OK; ++p) {
+        M->inflight[mem_of[p]].fetch_add(1, std::memory_order_relaxed);
+        rc = ctx_stage_launch(M->mem[mem_of[p]], ms[p], &slot[p]);
+        if (rc == HSC_OK) {
+            run[p] = true, nrun++;
+        } else {
+            M->inflight[mem_of[p]].fetch_sub(1, std::memory_order_relaxed);
+            fail_p = p;
+        }
+    }
+    const auto t2 = SteadyClock::now();
+    static thread_local std::vector<int> rcm;
+    for (int p = 0; p < parts; ++p) {
+        if (!run[p]) continue;
+        rcm.resize(std::max<size_t>(tb[p + 1] - tb[p], 1));
+        const int r = ctx_stage_wait(M->mem[mem_of[p]], ms[p], slot[p], rcm.data());
+        M->inflight[mem_of[p]].fetch_sub(1, std::memory_order_relaxed);
+        if (r) {
+            if (rc == HSC_OK) rc = r, fail_p = p;
+            continue;
+        }
+        for (size_t t = tb[p]; t < tb[p + 1]; ++t) rc_out[t] |= rcm[t - tb[p]];
+    }
+    give_back();
+    const auto t3 = SteadyClock::now();
+    M->ns_launch_a.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t2 - t1).count(),
+                             std::memory_order_relaxed);
+    M->ns_wait.fetch_add((uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t3 - t2).count(),
+                         std::memory_order_relaxed);
+    M->members_run.fetch_add((uint64_t)nrun, std::memory_order_relaxed);
+    const bool moved = M->part_epoch.load(std::memory_order_acquire) != epoch;
+    if (rc == HSC_OK && !moved) return HSC_OK;
+    if (lk) lk->lock();
+    if (rc == HSC_OK) return mfail(f, HSC_ESTATE, "multi context re-placed during the check");
+    return mfail(f, rc, ("member check: " + M->mem[mem_of[fail_p < 0 ? 0 : fail_p]]->err).c_str());
+}
+
+// Device-resident batches on a replicated window (hsc_multi_probe_device):
+// each local member probes its own batch against its replica; its verdict
+// bits go straight to b[m].bitmap (no routing, no exchange, no merge).
+static int replica_probe_device(hsc_ctx *f, const hsc_probe_batch *b, int L)
+{
+    Multi *M = f->multi;
+    const int NL = M->nlocal;
+    for (int m = 0; m < NL; ++m)
+        if (b[m].n > 0xFFFFFFFFull || b[m].n_lock > 0xFFFFFFFFull || b[m].n_txn > 0x7FFFFFFFull ||
+            (b[m].n_txn && !b[m].bitmap))
+            return mfail(f, HSC_EINVAL, "multi probe batch");
+    MRC(lane_acquire(f, M, L));
+    for (int m = 0; m < NL; ++m) {
+        MLane &ml = M->lane[L][m];
+        hsc_ctx *c = M->mem[m];
+        hsc_probe_batch x = b[m];
+        MCHK(f, hipSetDevice(c->device));
+        MCHK(f, ml.verdict.ensure(std::max<size_t>(x.n_txn, 64)));
+        x.verdict = ml.verdict.as<uint8_t>();
+        MuGuard g(c);
+        if (c->dirty) return mfail(f, HSC_ESTATE, "member window not built");
+        if (c->app_last) MCHK(f, hipStreamWaitEvent(ml.stream, c->app_last, 0));
+        hipStream_t keep = c->stream;
+        MCHK(f, ctx_switch_stream(c, ml.stream));
+        const int rc = ctx_probe(c, &x);
+        MCHK(f, ctx_switch_stream(c, keep));
+        if (rc) return mfail(f, rc, ("member probe: " + c->err).c_str());
+        if (NL > 1) MCHK(f, hipEventRecord(ml.ev_done, ml.stream));
+        ml.used = true;
+        M->probes += x.n, M->routed += x.n;
+    }
+    M->last_lane = L;
+    M->batches++;
+    return HSC_OK;
+}
+
 int multi_check_stage(hsc_ctx *f, Stage &st, int *rc_out, std::unique_lock<std::mutex> *lk)
 {
     Multi *M = f->multi;
+    if (M->replicated) return replica_check(f, st, rc_out, lk);
     if (M->rccl) return check_stage_device(f, st, rc_out);
     const int N = M->world;
     const size_t T = st.n_txn;
@@ -1351,9 +1574,10 @@ int hsc_multi_adopt(hsc_ctx *f)
     if (!f || !f->multi) return HSC_EINVAL;
     Multi *M = f->multi;
     MuGuard g(f);
+    const bool rep = M->mode == HSC_MULTI_REPLICAS;
     // the routing of every probe follows the splitters: without them all
     // probes would go to member 0 and the other pieces' keys never be probed
-    if (M->world > 1 && !M->sp_given)
+    if (M->world > 1 && !M->sp_given && !rep)
         return mfail(f, HSC_ESTATE, "adopt: set the splitters the members' pieces were cut at first");
     // one key width: a probe's bound words are those of the front
     const int W = M->mem[0]->W;
@@ -1368,8 +1592,26 @@ int hsc_multi_adopt(hsc_ctx *f)
         for (size_t t = 0; t < std::min(tm.size(), c->h_table_max.size()); ++t)
             tm[t] = std::max(tm[t], c->h_table_max[t]);
     }
-    // every member's rows inside its piece: its first and last key
-    if (M->world > 1) {
+    // replicas: every member holds the same window (its row count and first
+    // and last keys); pieces: every member's rows inside its piece
+    if (rep) {
+        uint32_t g0[2];
+        uint64_t w0[2 * kMaxWords];
+        for (int m = 0; m < M->nlocal; ++m) {
+            hsc_ctx *c = M->mem[m];
+            if (c->n != M->mem[0]->n) return mfail(f, HSC_EINVAL, "adopt: replicas hold different rows");
+            if (!c->n) continue;
+            uint32_t kg[2];
+            uint64_t kw[2 * kMaxWords];
+            const int rc = ctx_edge_keys(c, kg, kw);
+            if (rc) return mfail(f, rc, ("adopt: member keys: " + c->err).c_str());
+            if (m == 0) {
+                memcpy(g0, kg, sizeof g0), memcpy(w0, kw, sizeof w0);
+            } else if (memcmp(g0, kg, sizeof g0) || memcmp(w0, kw, 16 * (size_t)W)) {
+                return mfail(f, HSC_EINVAL, "adopt: replicas hold different rows");
+            }
+        }
+    } else if (M->world > 1) {
         f->W = W;
         MRC(upload_splitters(f, M, W));
         for (int m = 0; m < M->nlocal; ++m) {
@@ -1405,9 +1647,10 @@ int hsc_multi_adopt(hsc_ctx *f)
     f->W = W;
     size_t keys = 0;
     for (int m = 0; m < M->nlocal; ++m) keys += M->mem[m]->n;
-    f->n = keys;
+    f->n = rep ? M->mem[0]->n : keys;
     M->part_epoch.fetch_add(1, std::memory_order_acq_rel);
     M->adopted = true;
+    M->replicated = rep;
     M->d_sp_W = 0;
     f->host_staged = false;
     f->dirty = false;
@@ -1422,6 +1665,7 @@ int hsc_multi_probe_device(hsc_ctx *f, const hsc_probe_batch *b, int lane)
     Multi *M = f->multi;
     MuGuard g(f);
     if (f->dirty) return mfail(f, HSC_ESTATE, "window not built");
+    if (M->replicated) return replica_probe_device(f, b, lane);
     MSource src[kMultiMax] = {};
     for (int m = 0; m < M->nlocal; ++m) {
         if (b[m].n > 0xFFFFFFFFull || b[m].n_lock > 0xFFFFFFFFull || b[m].n_txn > 0x7FFFFFFFull ||
@@ -1494,6 +1738,36 @@ int hsc_multi_set_transport(hsc_ctx *f, int transport)
     return HSC_OK;
 }
 
+int hsc_multi_routed_phase_stats(hsc_ctx *f, double out[4])
+{
+    if (!f || !f->multi || !out) return HSC_EINVAL;
+    Multi *M = f->multi;
+    const double b = (double)std::max<uint64_t>(M->pr_batches, 1) * 1e3;
+    out[0] = (double)M->pr_batches;
+    out[1] = (double)M->ns_pr_lane / b;
+    out[2] = (double)M->ns_pr_probe / b;
+    out[3] = (double)M->ns_pr_merge / b;
+    return HSC_OK;
+}
+
+int hsc_multi_set_mode(hsc_ctx *f, int mode)
+{
+    if (!f || !f->multi || mode < HSC_MULTI_AUTO || mode > HSC_MULTI_REPLICAS) return HSC_EINVAL;
+    Multi *M = f->multi;
+    MuGuard g(f);
+    if (M->mode == mode) return HSC_OK;
+    M->mode = mode;
+    M->part_epoch.fetch_add(1, std::memory_order_acq_rel);
+    if (f->host_staged) f->dirty = true;  // re-placed at the next check
+    return HSC_OK;
+}
+
+int hsc_multi_mode(hsc_ctx *f)
+{
+    if (!f || !f->multi) return HSC_EINVAL;
+    return f->multi->replicated ? HSC_MULTI_REPLICAS : HSC_MULTI_PIECES;
+}
+
 int hsc_multi_probe_routed(hsc_ctx *f, const hsc_probe_batch *b, const uint64_t *owner_base, int lane)
 {
     if (!f || !f->multi || !b || !owner_base || lane < 0 || lane >= kMultiLanes) return HSC_EINVAL;
@@ -1501,6 +1775,7 @@ int hsc_multi_probe_routed(hsc_ctx *f, const hsc_probe_batch *b, const uint64_t 
     const int N = M->world, NL = M->nlocal;
     MuGuard g(f);
     if (f->dirty) return mfail(f, HSC_ESTATE, "window not built");
+    if (M->replicated) return mfail(f, HSC_ESTATE, "replicated window: probe each member (hsc_probe_device)");
     size_t tb[kMultiMax + 1];
     for (int o = 0; o <= N; ++o) {
         tb[o] = (size_t)owner_base[o];
@@ -1519,10 +1794,14 @@ int hsc_multi_probe_routed(hsc_ctx *f, const hsc_probe_batch *b, const uint64_t 
     }
     const auto t0 = SteadyClock::now();
     MRC(lane_acquire(f, M, lane));
+    const auto t1 = SteadyClock::now();
     MRC(probe_merge(f, lane, in, tb, outs));
     for (int m = 0; m < NL; ++m) M->routed += b[m].n, M->probes += b[m].n;
     M->pr_batches++;
     M->ns_pr += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(SteadyClock::now() - t0).count();
+    M->ns_pr_lane += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count();
+    M->ns_pr_probe += M->ns_pm_probe;
+    M->ns_pr_merge += M->ns_pm_merge;
     return HSC_OK;
 }
 

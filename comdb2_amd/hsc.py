@@ -186,7 +186,9 @@ EXPORTS = [
     "hsc_multi_member_probe_ms", "hsc_multi_route_stats", "hsc_multi_graph_scc",
     "hsc_multi_graph_phase_ms",
     "hsc_marshal_arrs", "hsc_batch_stats", "hsc_regop_stats", "hsc_harness_commit_protocol",
+    "hsc_multi_set_mode", "hsc_multi_mode", "hsc_multi_routed_phase_stats",
 ]
+MULTI_AUTO, MULTI_PIECES, MULTI_REPLICAS = 0, 1, 2
 MULTI_ID_BYTES = 2 * 128  # hsc_multi_unique_ids: one RCCL id per lane
 
 (LAYOUT_AUTO, LAYOUT_WIDE, LAYOUT_NARROW, LAYOUT_NARROW_DIRECT, LAYOUT_NARROW_TILES,
@@ -305,6 +307,9 @@ def load() -> C.CDLL:
         "hsc_multi_stats": (C.c_int, [_p, _p]),
         "hsc_multi_last_counts": (C.c_int, [_p, _p, C.c_int]),
         "hsc_multi_phase_stats": (C.c_int, [_p, _p]),
+        "hsc_multi_routed_phase_stats": (C.c_int, [_p, _p]),
+        "hsc_multi_set_mode": (C.c_int, [_p, C.c_int]),
+        "hsc_multi_mode": (C.c_int, [_p]),
         "hsc_multi_set_transport": (C.c_int, [_p, C.c_int]),
         "hsc_multi_probe_routed": (C.c_int, [_p, _p, _p, C.c_int]),
         "hsc_multi_marshal_routed": (C.c_int, [_p, C.POINTER(_ReadSets), C.c_int, C.c_uint32,
@@ -1147,6 +1152,16 @@ class MultiValidator(Validator):
     def adopt(self) -> None:
         self._chk(self.lib.hsc_multi_adopt(self.ctx), "hsc_multi_adopt")
 
+    def set_mode(self, mode: int) -> None:
+        """Window placement: MULTI_AUTO, MULTI_PIECES or MULTI_REPLICAS
+        (hsc_multi_set_mode)."""
+        self._chk(self.lib.hsc_multi_set_mode(self.ctx, int(mode)), "hsc_multi_set_mode")
+
+    @property
+    def mode(self) -> int:
+        """The placement in force: MULTI_PIECES or MULTI_REPLICAS."""
+        return self.lib.hsc_multi_mode(self.ctx)
+
     def set_transport(self, loopback: bool) -> None:
         """In-process members: HSC_MULTI_LOOPBACK runs the per-rank exchange
         (send blocks, unpack, owner slices) with peer copies in place of RCCL."""
@@ -1284,6 +1299,15 @@ class MultiValidator(Validator):
         return {"batches": int(out[0]), "lane_wait_us": float(out[1]), "count_launch_us": float(out[2]),
                 "count_wait_us": float(out[3]), "enqueue_us": float(out[4]),
                 "routed_batches": int(out[5]), "routed_enqueue_us": float(out[6])}
+
+    def routed_phase_stats(self) -> dict:
+        """hsc_multi_probe_routed's host us per batch: lane waits, member probe
+        launches, merges (hsc_multi_routed_phase_stats)."""
+        out = np.zeros(4, np.float64)
+        self._chk(self.lib.hsc_multi_routed_phase_stats(self.ctx, out.ctypes.data),
+                  "hsc_multi_routed_phase_stats")
+        return {"batches": int(out[0]), "lane_us": float(out[1]), "probe_launch_us": float(out[2]),
+                "merge_us": float(out[3])}
 
     def last_counts(self) -> np.ndarray:
         n = self.world

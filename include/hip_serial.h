@@ -624,6 +624,25 @@ int hsc_multi_adopt(hsc_ctx *ctx);
 #define HSC_MULTI_DIRECT 0
 #define HSC_MULTI_LOOPBACK 1
 int hsc_multi_set_transport(hsc_ctx *ctx, int transport);
+/* Window placement.  HSC_MULTI_PIECES: each member holds its key-range piece
+ * (the splitters); a batch's probes go to the pieces they overlap and the
+ * verdicts are OR-ed.  HSC_MULTI_REPLICAS: every member holds the whole
+ * window (builds and appends go to every member); a drop-in batch that fits
+ * the small path goes whole to ONE member (the one with the fewest batches in
+ * flight, round robin among equals: one member kernel per call), a larger
+ * one is cut into per-member slices of its read sets, each checked by one
+ * member against its replica -- no routing, no exchange, no OR across
+ * members.  HSC_MULTI_AUTO (default): replicas when a host-staged window's
+ * rows x (8 W + 16) bytes fit an eighth of the smallest member's device
+ * memory, else pieces; an adopted window is pieces unless REPLICAS was set
+ * (hsc_multi_adopt then needs every member to hold the same rows, no
+ * splitters).  A host-staged window is re-placed at the next check.
+ * hsc_multi_mode returns the placement in force (PIECES or REPLICAS). */
+#define HSC_MULTI_AUTO 0
+#define HSC_MULTI_PIECES 1
+#define HSC_MULTI_REPLICAS 2
+int hsc_multi_set_mode(hsc_ctx *ctx, int mode);
+int hsc_multi_mode(hsc_ctx *ctx);
 /* Device-resident batches, one per local member (pointers on its GPU), each
  * numbering its own read sets 0..b[i].n_txn-1: routed, probed and merged;
  * b[i].bitmap (ceil(n_txn / 64) words) receives the merged verdict bits of
@@ -672,6 +691,13 @@ int hsc_multi_last_counts(hsc_ctx *ctx, uint32_t *counts, int n);
  * batch; out[5] hsc_multi_probe_routed batches, out[6] mean us enqueueing
  * one. */
 int hsc_multi_phase_stats(hsc_ctx *ctx, double out[7]);
+/* hsc_multi_probe_routed's host time per batch, split (us): out[0] batches,
+ * out[1] lane_acquire (the members' cross-lane event waits), out[2] the
+ * members' probe launches, out[3] the owners' merges and done events.  An
+ * enqueue blocks when a hardware queue is full, so each phase holds that
+ * wait too; bench.py times calls that start on an idle GPU for the pure
+ * enqueue cost. */
+int hsc_multi_routed_phase_stats(hsc_ctx *ctx, double out[4]);
 
 /* ---- OSQL_SERIAL wire path --------------------------------------------
  * Decode only: *out points at context-owned read sets, valid until the next

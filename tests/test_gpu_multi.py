@@ -9,7 +9,10 @@ share cuda:0:
   loopback transport -- the per-rank form (send blocks, k_route_unpack,
   owner slices gathered and OR-ed) with peer copies in place of RCCL;
 - batches routed at marshal time (hsc_multi_probe_routed), both merges;
-- a per-rank context of world 1 (RCCL loaded; one piece: no routing).
+- a per-rank context of world 1 (RCCL loaded; one piece: no routing);
+- replicated windows (HSC_MULTI_REPLICAS, the AUTO choice for a window that
+  fits): every member holds the whole window, a lone call runs one member's
+  kernel, a large batch is cut into per-member slices of read sets.
 Verdicts are checked against the oracle (oracle/serial_oracle.c on the whole
 log) and against one context holding the whole window."""
 import json
@@ -29,9 +32,14 @@ torch = pytest.importorskip("torch")
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "config1_replay.json")
 
 
-@pytest.fixture(scope="module", params=[2, 4])
+@pytest.fixture(scope="module", params=[(2, hsc.MULTI_PIECES), (4, hsc.MULTI_PIECES),
+                                        (2, hsc.MULTI_REPLICAS), (3, hsc.MULTI_REPLICAS)],
+                ids=["pieces2", "pieces4", "replicas2", "replicas3"])
 def multi(request):
-    m = MultiValidator([0] * request.param)
+    n, mode = request.param
+    m = MultiValidator([0] * n)
+    m.set_mode(mode)
+    m.want_mode = mode
     yield m
     m.close()
 
@@ -50,6 +58,7 @@ def test_random_logs_vs_oracle(multi, oracle_mod, seed):
     finally:
         arrs.close()
     np.testing.assert_array_equal(got2 != 0, want != 0)
+    assert multi.mode == multi.want_mode
 
 
 @pytest.mark.parametrize("seed", range(4))
@@ -91,8 +100,9 @@ def test_config3_vs_oracle_and_one_context(multi, oracle_mod):
     assert 0.1 < got.mean() < 0.9
     _sample_vs_oracle(oracle_mod, got, a.readsets, log, 20)
     st = multi.route_stats()
-    assert st["rows"] >= st["probes"] > 0
-    assert st["member_checks"] >= multi.world  # every member held probes of the batch
+    assert st["member_checks"] >= multi.world  # every member checked a share of the batch
+    if multi.want_mode == hsc.MULTI_PIECES:
+        assert st["rows"] >= st["probes"] > 0
 
 
 def test_config5_vs_oracle_and_one_context(multi, oracle_mod):
@@ -138,14 +148,18 @@ def test_explicit_splitters_and_straddling_ranges(oracle_mod):
         m.close()
 
 
-def test_config1_commit_stream_golden():
+@pytest.mark.parametrize("mode", [hsc.MULTI_PIECES, hsc.MULTI_REPLICAS])
+def test_config1_commit_stream_golden(mode):
     """BASELINE config 1's 10k-txn stream through a 2-member context: one
     check per commit, every passing txn's log records appended (routed to the
-    owners' delta runs); verdicts equal the oracle replay's golden."""
+    owners' delta runs, or to every replica); verdicts equal the oracle
+    replay's golden."""
     gold = json.load(open(GOLDEN))
     m = MultiValidator([0, 0])
     try:
+        m.set_mode(mode)
         rc = replay_incremental(config1_events(n_txn=gold["n_txn"]), m, mode="log")
+        assert m.mode == mode
     finally:
         m.close()
     assert rc == gold["rc"]
@@ -183,6 +197,7 @@ def test_probe_device_per_member_batches(oracle_mod, n):
     one = Validator(0)
     m = MultiValidator([0] * n)
     try:
+        m.set_mode(hsc.MULTI_PIECES)
         one.ingest_log(log)
         m.ingest_log(log)
         dev = torch.device("cuda", 0)
@@ -216,6 +231,7 @@ def test_loopback_transport_per_member_batches(oracle_mod, n):
     one = Validator(0)
     m = MultiValidator([0] * n)
     try:
+        m.set_mode(hsc.MULTI_PIECES)
         one.ingest_log(log)
         m.ingest_log(log)
         m.set_transport(True)
@@ -269,6 +285,7 @@ def test_probe_routed_at_marshal(oracle_mod, n, loop):
     one = Validator(0)
     m = MultiValidator([0] * n)
     try:
+        m.set_mode(hsc.MULTI_PIECES)
         one.ingest_log(log)
         m.ingest_log(log)
         m.check_readsets(a.readsets.subset(np.arange(4)))  # built and partitioned
@@ -314,6 +331,7 @@ def test_lone_calls_route_to_one_member(oracle_mod):
     want, _, _ = oracle_mod.check(log, rs)
     m = MultiValidator([0, 0])
     try:
+        m.set_mode(hsc.MULTI_PIECES)
         m.ingest_log(log)
         got = np.array([m.check_readsets(rs.subset(np.array([t])))[0] for t in range(rs.ntxn)])
         np.testing.assert_array_equal(got != 0, want != 0)
@@ -322,6 +340,92 @@ def test_lone_calls_route_to_one_member(oracle_mod):
         assert st["member_checks"] < 2 * st["calls"]  # some calls touched one member only
         small = sum(m.member(i).small_stats()["calls"] for i in range(2))
         assert small >= st["member_checks"] // 2
+    finally:
+        m.close()
+
+
+def test_replicas_lone_calls_run_one_member_each(oracle_mod):
+    """A replicated window (AUTO: the window fits): every lone drop-in call
+    runs exactly one member's small kernel, the members taking turns; a large
+    batch is cut into one slice per member.  Verdicts equal the oracle."""
+    from comdb2_amd.workloads import config2
+    c2 = config2(n_commits=4000, n_txn=400, value_bits=24, width=1 << 10)
+    log, rs = c2.log, c2.readsets
+    want, _, _ = oracle_mod.check(log, rs)
+    m = MultiValidator([0, 0, 0])
+    try:
+        m.ingest_log(log)
+        got = np.array([m.check_readsets(rs.subset(np.array([t])))[0] for t in range(60)])
+        np.testing.assert_array_equal(got != 0, want[:60] != 0)
+        assert m.mode == hsc.MULTI_REPLICAS
+        st = m.route_stats()
+        assert st["member_checks"] == st["calls"] == 60  # one member per call
+        small = [m.member(i).small_stats()["calls"] for i in range(3)]
+        assert sum(small) == 60 and min(small) > 0  # every member took calls
+        # the whole batch through the drop-in batch entry: sliced over the members
+        arrs = hsc.NativeCurRangeArrs(rs)
+        try:
+            big = m.check_batch(arrs)
+        finally:
+            arrs.close()
+        np.testing.assert_array_equal(big != 0, want != 0)
+        # concurrent callers through the context's collector
+        arrs = hsc.NativeCurRangeArrs(rs)
+        try:
+            got, cst = m.concurrent_check(arrs, 16, collect=False)
+        finally:
+            arrs.close()
+        np.testing.assert_array_equal(got[:rs.ntxn] != 0, want != 0)
+    finally:
+        m.close()
+
+
+def test_replicas_adopted_and_device_batches(oracle_mod):
+    """Every member ingests the whole window from device rows; with
+    HSC_MULTI_REPLICAS hsc_multi_adopt needs no splitters and refuses members
+    holding different rows; device batches are probed by each member against
+    its replica (no routing)."""
+    from comdb2_amd.workloads import config2
+    c2 = config2(n_commits=20_000, n_txn=2000, value_bits=24, width=1 << 8)
+    want, _, _ = oracle_mod.check(c2.log, c2.readsets)
+    one = Validator(0)
+    one.ingest_log(c2.log)
+    gid, words, lsn = one.export_window(all_versions=True)
+    one.close()
+    order = np.argsort(lsn, kind="stable")
+    dev = torch.device("cuda", 0)
+
+    def ingest(m, i, sel):
+        tg = torch.from_numpy(np.ascontiguousarray(gid[sel])).to(dev)
+        tw = torch.from_numpy(np.ascontiguousarray(words[:, sel]).reshape(-1).view(np.int64)).to(dev)
+        tl = torch.from_numpy(np.ascontiguousarray(lsn[sel]).view(np.int64)).to(dev)
+        torch.cuda.synchronize()
+        m.member(i).ingest_device(len(sel), words.shape[0], tg.data_ptr(), tw.data_ptr(), tl.data_ptr(),
+                                  c2.params["end_lsn"])
+
+    m = MultiValidator([0, 0])
+    try:
+        m.register_group("t1", 0, 9)
+        m.set_mode(hsc.MULTI_REPLICAS)
+        ingest(m, 0, order)
+        ingest(m, 1, order[: len(order) // 2])  # not a replica
+        with pytest.raises(hsc.HscError):
+            m.adopt()
+        ingest(m, 1, order)
+        m.adopt()
+        assert m.mode == hsc.MULTI_REPLICAS
+        m.set_end(c2.params["end_lsn"])
+        np.testing.assert_array_equal(m.check_readsets(c2.readsets) != 0, want != 0)
+        # device batches: member i probes read sets [i T/2, (i+1) T/2) against its replica
+        T = c2.readsets.ntxn
+        halves = [c2.readsets.subset(np.arange(i * T // 2, (i + 1) * T // 2)) for i in range(2)]
+        batches = [_device_batch(m.member(i), halves[i], dev) for i in range(2)]
+        torch.cuda.synchronize()
+        m.probe_device_multi([b["struct"] for b in batches], lane=0)
+        torch.cuda.synchronize()
+        for i in range(2):
+            np.testing.assert_array_equal(_bits(batches[i], halves[i].ntxn),
+                                          want[i * T // 2:(i + 1) * T // 2] != 0)
     finally:
         m.close()
 
