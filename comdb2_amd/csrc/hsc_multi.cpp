@@ -1074,19 +1074,27 @@ static int pick_member(Multi *M)
     return best;
 }
 
-// Read sets [t0, t1) of the marshalled batch st (probes and lock probes are in
-// read-set order) into o for member c: the columns copied, read sets
-// renumbered from 0, sized for c's small path when it fits.
+// Read sets [t0, t1) of the marshalled batch st into o for member c: the
+// probes (and lock probes) whose read set falls in the slice, in the batch's
+// order -- which is NOT read-set order in general (the marshal lays a key
+// length's points after its ranges, config 3), so the slice is a filter, not
+// a subrange -- read sets renumbered from 0, sized for c's small path when it
+// fits.  A whole batch (t0 = 0, t1 = T) copies the columns as they are.
 static int replica_slice(hsc_ctx *f, hsc_ctx *c, const Stage &st, size_t t0, size_t t1, Stage &o)
 {
     const int W = f->W;
-    const size_t n = st.n, nl = st.n_lock;
+    const size_t n = st.n, nl = st.n_lock, T = t1 - t0;
     const uint32_t *txn = st.col<uint32_t>(st.L.txn), *ltx = st.col<uint32_t>(st.L.lock_txn);
-    const size_t a = (size_t)(std::lower_bound(txn, txn + n, (uint32_t)t0) - txn);
-    const size_t e = (size_t)(std::lower_bound(txn + a, txn + n, (uint32_t)t1) - txn);
-    const size_t la = (size_t)(std::lower_bound(ltx, ltx + nl, (uint32_t)t0) - ltx);
-    const size_t le = (size_t)(std::lower_bound(ltx + la, ltx + nl, (uint32_t)t1) - ltx);
-    const size_t k = e - a, kl = le - la, T = t1 - t0;
+    const bool whole = t0 == 0 && t1 >= st.n_txn;
+    static thread_local std::vector<uint32_t> pi, li;
+    pi.clear(), li.clear();
+    if (!whole) {
+        for (size_t i = 0; i < n; ++i)
+            if (txn[i] >= t0 && txn[i] < t1) pi.push_back((uint32_t)i);
+        for (size_t i = 0; i < nl; ++i)
+            if (ltx[i] >= t0 && ltx[i] < t1) li.push_back((uint32_t)i);
+    }
+    const size_t k = whole ? n : pi.size(), kl = whole ? nl : li.size();
     o.L = stage_layout(W, k, kl);
     o.n = k, o.n_lock = kl, o.n_txn = T;
     o.coh = ctx_small_fits(c, T, k, kl);
@@ -1094,18 +1102,34 @@ static int replica_slice(hsc_ctx *f, hsc_ctx *c, const Stage &st, size_t t0, siz
         o.forced.ensure(std::max<size_t>(T, 1), true))
         return mfail(f, HSC_ENOMEM, "multi replica staging");
     memset(o.forced.p, 0, std::max<size_t>(T, 1));  // the front's forced verdicts are OR-ed in
-    for (int j = 0; j < W; ++j) {
-        memcpy(o.col<uint64_t>(o.L.lo) + (size_t)j * k, st.col<uint64_t>(st.L.lo) + (size_t)j * n + a, 8 * k);
-        memcpy(o.col<uint64_t>(o.L.hi) + (size_t)j * k, st.col<uint64_t>(st.L.hi) + (size_t)j * n + a, 8 * k);
+    if (whole) {
+        for (int j = 0; j < W; ++j) {
+            memcpy(o.col<uint64_t>(o.L.lo) + (size_t)j * k, st.col<uint64_t>(st.L.lo) + (size_t)j * n, 8 * k);
+            memcpy(o.col<uint64_t>(o.L.hi) + (size_t)j * k, st.col<uint64_t>(st.L.hi) + (size_t)j * n, 8 * k);
+        }
+        memcpy(o.col<uint64_t>(o.L.snap), st.col<uint64_t>(st.L.snap), 8 * k);
+        memcpy(o.col<uint32_t>(o.L.gid), st.col<uint32_t>(st.L.gid), 4 * k);
+        memcpy(o.col<uint32_t>(o.L.txn), txn, 4 * k);
+        memcpy(o.col<uint64_t>(o.L.lock_snap), st.col<uint64_t>(st.L.lock_snap), 8 * kl);
+        memcpy(o.col<uint32_t>(o.L.lock_table), st.col<uint32_t>(st.L.lock_table), 4 * kl);
+        memcpy(o.col<uint32_t>(o.L.lock_txn), ltx, 4 * kl);
+        return HSC_OK;
     }
-    memcpy(o.col<uint64_t>(o.L.snap), st.col<uint64_t>(st.L.snap) + a, 8 * k);
-    memcpy(o.col<uint32_t>(o.L.gid), st.col<uint32_t>(st.L.gid) + a, 4 * k);
-    uint32_t *ot = o.col<uint32_t>(o.L.txn);
-    for (size_t i = 0; i < k; ++i) ot[i] = txn[a + i] - (uint32_t)t0;
-    memcpy(o.col<uint64_t>(o.L.lock_snap), st.col<uint64_t>(st.L.lock_snap) + la, 8 * kl);
-    memcpy(o.col<uint32_t>(o.L.lock_table), st.col<uint32_t>(st.L.lock_table) + la, 4 * kl);
-    uint32_t *olt = o.col<uint32_t>(o.L.lock_txn);
-    for (size_t i = 0; i < kl; ++i) olt[i] = ltx[la + i] - (uint32_t)t0;
+    for (int j = 0; j < W; ++j) {
+        const uint64_t *slo = st.col<uint64_t>(st.L.lo) + (size_t)j * n, *shi = st.col<uint64_t>(st.L.hi) + (size_t)j * n;
+        uint64_t *dlo = o.col<uint64_t>(o.L.lo) + (size_t)j * k, *dhi = o.col<uint64_t>(o.L.hi) + (size_t)j * k;
+        for (size_t i = 0; i < k; ++i) dlo[i] = slo[pi[i]], dhi[i] = shi[pi[i]];
+    }
+    const uint64_t *ssn = st.col<uint64_t>(st.L.snap);
+    const uint32_t *sg = st.col<uint32_t>(st.L.gid);
+    uint64_t *osn = o.col<uint64_t>(o.L.snap);
+    uint32_t *og = o.col<uint32_t>(o.L.gid), *ot = o.col<uint32_t>(o.L.txn);
+    for (size_t i = 0; i < k; ++i) osn[i] = ssn[pi[i]], og[i] = sg[pi[i]], ot[i] = txn[pi[i]] - (uint32_t)t0;
+    const uint64_t *sls = st.col<uint64_t>(st.L.lock_snap);
+    const uint32_t *slt = st.col<uint32_t>(st.L.lock_table);
+    uint64_t *ols = o.col<uint64_t>(o.L.lock_snap);
+    uint32_t *olt = o.col<uint32_t>(o.L.lock_table), *olx = o.col<uint32_t>(o.L.lock_txn);
+    for (size_t i = 0; i < kl; ++i) ols[i] = sls[li[i]], olt[i] = slt[li[i]], olx[i] = ltx[li[i]] - (uint32_t)t0;
     return HSC_OK;
 }
 
