@@ -152,6 +152,11 @@ def _native_stream(ev, v):
     pf, po = C.byref(f), C.byref(o)
     check, append, ctx = v.lib.hip_bdb_osql_serial_check, v.lib.hsc_window_append_log, v.ctx
     t_check, t_app, rcs = [], [], {}
+    # the collector would pause this loop at random calls (a gen-2 pass over
+    # the log builder's rows takes milliseconds): off while the stream runs
+    import gc
+    gc.collect()
+    gc.disable()
     t0 = time.perf_counter()
     for e, t in ev:
         if e == "begin":
@@ -183,7 +188,9 @@ def _native_stream(ev, v):
             if rca != 0:
                 raise RuntimeError(f"hsc_window_append_log -> {rca}")
         del arrs[t.name]
-    return np.array(t_check), np.array(t_app), rcs, time.perf_counter() - t0
+    wall = time.perf_counter() - t0
+    gc.enable()
+    return np.array(t_check), np.array(t_app), rcs, wall
 
 
 def _pct(x, slow_us=None):
@@ -522,11 +529,12 @@ def graph_pmc_traffic(args, h, world, device):
                 return out
             vals = {}
             for row in csv.DictReader(open(path)):
+                # (-T: truncated names, no namespace; every kernel of the library is k_*)
                 name = row["Kernel_Name"]
-                if "hsc::" not in name or row["Counter_Name"] != ctr:
-                    continue
                 k = name.split("(")[0].replace("hsc::", "").replace("(anonymous namespace)::", "")
                 k = (k[5:] if k.startswith("void ") else k).split("<")[0]
+                if not k.startswith("k_") or row["Counter_Name"] != ctr:
+                    continue
                 vals[k] = vals.get(k, 0.0) + float(row["Counter_Value"])
             per[ctr] = vals
         tot = 0.0
@@ -823,7 +831,7 @@ def pmc_traffic(args, members=1, device=0):
                "csv", "-d", d, "-o", "run", "--", sys.executable, os.path.abspath(__file__),
                "--pmc-child", "--config", str(args.config), "--n-commits", str(args.n_commits),
                "--n-txn", str(args.n_txn), "--c3-writes", str(args.c3_writes),
-               "--c5-keys", str(args.c5_keys), "--streams", str(args.streams)]
+               "--c5-keys", str(args.c5_keys), "--streams", str(args.streams), "--paths", str(args.paths)]
         cmd += (["--compact-wide"] if args.compact_wide else [])
         if members > 1:
             cmd += ["--multi-pmc", str(members), "--pmc-device", str(device), "--batches", "2",
@@ -1439,6 +1447,9 @@ def main():
     ap.add_argument("--c4-ntxn", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--c4-world", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--wide", action="store_true", help="force the wide window layout")
+    ap.add_argument("--paths", type=int, default=0,
+                    help="hsc_set_paths flags of the one-GPU context, set before the build (A/B runs; "
+                         "64 = HSC_PATH_NO_CT_POINTS)")
     ap.add_argument("--compact-wide", action="store_true",
                     help="compact windows: probe through the wide tile pipeline instead of "
                          "the compact tiles (A/B)")
@@ -1519,6 +1530,8 @@ def main():
     want_cpu = not args.no_cpu and args.config in (2, 3, 5) and not args.pmc_child
     batches = []
     v = hsc.Validator(local)
+    if args.paths:
+        v.set_paths(args.paths)
     if args.wide:
         v.set_layout(hsc.LAYOUT_WIDE)
     elif args.compact_wide:

@@ -166,19 +166,128 @@ __global__ __launch_bounds__(256) void k_compact_probes(ProbeView p, CompactMeta
     }
 }
 
+// ---- exact-key index for point probes (PointHash, hsc_internal.h) ----
+__device__ __forceinline__ uint64_t ph_mix(uint64_t k0, uint64_t k1, uint64_t k2)
+{
+    uint64_t h = k0 * 0x9E3779B97F4A7C15ull;
+    h ^= (k1 + 0x632BE59BD9B4E019ull) * 0xC2B2AE3D27D4EB4Full;
+    h ^= (k2 + 0x165667B19E3779F9ull) * 0xD6E8FEB86659FD93ull;
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ull;
+    return h ^ (h >> 29);
+}
+
+// the tiles' key of code c in group g (hsc_ctiles.hip compose), 3 words with
+// the words past WG zero
+template <int WC>
+__device__ __forceinline__ void ph_key(uint32_t g, int gb, int WG, const uint64_t (&c)[WC], uint64_t (&k)[3])
+{
+    uint64_t x[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = j < WC ? c[j < WC ? j : 0] : 0;
+    if (gb == 0) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) k[j] = x[j];
+    } else {
+        k[0] = ((uint64_t)g << (64 - gb)) | (x[0] >> gb);
+        k[1] = (x[0] << (64 - gb)) | (x[1] >> gb);
+        k[2] = (x[1] << (64 - gb)) | (x[2] >> gb);
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) k[j] = j < WG ? k[j] : 0;
+}
+
+// rank of key k in the index (false: not a window key).  A bucket is one
+// 128-byte line of four entries; a lookup reads its home line and goes on
+// only past a full one
+__device__ __forceinline__ bool ph_find(const PointHash &ph, const uint64_t (&k)[3], uint32_t &rank)
+{
+    uint64_t b = __umul64hi(ph_mix(k[0], k[1], k[2]), ph.nb);
+    for (uint64_t it = 0; it < ph.nb; ++it) {
+        const u64x2 *e = (const u64x2 *)(ph.e + 16 * b);
+        u64x2 x[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] = e[q];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const u64x2 a0 = x[2 * s], a1 = x[2 * s + 1];
+            if (a1.y == 0) return false;
+            if (a0.x == k[0] && a0.y == k[1] && a1.x == k[2]) {
+                rank = (uint32_t)a1.y;
+                return true;
+            }
+        }
+        b = b + 1 == ph.nb ? 0 : b + 1;
+    }
+    return false;
+}
+
+// one thread per window key: claim a slot by its rank word (never 0: bit 32
+// set), then write the key words
+__global__ __launch_bounds__(256) void k_ph_insert(CTiles ct, uint64_t *e, uint64_t nb)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ct.n) return;
+    uint64_t k[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) k[j] = j < ct.WG ? ct.key[(size_t)j * ct.len + i] : 0;
+    const unsigned long long r = (unsigned long long)ct.rank[i] | (1ull << 32);
+    uint64_t b = __umul64hi(ph_mix(k[0], k[1], k[2]), nb);
+    for (uint64_t it = 0; it < nb; ++it) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            uint64_t *x = e + 16 * b + 4 * s;
+            if (atomicCAS((unsigned long long *)(x + 3), 0ull, r) == 0ull) {
+                x[0] = k[0], x[1] = k[1], x[2] = k[2];
+                return;
+            }
+        }
+        b = b + 1 == nb ? 0 : b + 1;
+    }
+}
+
 template <int WC, bool kLds>
 __global__ __launch_bounds__(kBoundThreads) void k_compact_bounds(ProbeView p, CompactMeta cm,
-                                                                  uint64_t *clo, uint64_t *chi)
+                                                                  uint64_t *clo, uint64_t *chi,
+                                                                  PointHash ph)
 {
     const uint32_t q = blockIdx.x * kBoundThreads + threadIdx.x;
     BoundIn cur;
     bound_load(p, cm, q, cur);
+    uint64_t snap = 0;
+    uint32_t txn = 0;
+    if (ph.nb && q < p.n) snap = p.snap[q], txn = p.txn[q];  // (used by points only)
     if constexpr (kLds) {
         extern __shared__ __attribute__((aligned(16))) uint64_t blds[];
         stage_bound_tables<kBoundThreads>(cm, blds);
         __syncthreads();
     }
-    if (q < p.n) bound_map<WC>(p, cm, q, cur, clo, chi);
+    if (q >= p.n) return;
+    if constexpr (WC <= 3) {
+        if (ph.nb) {
+            uint64_t al[WC], ah[WC];
+            const bool ok = bound_codes<WC>(cm, cur, al, ah);
+            bool point = ok;
+#pragma unroll
+            for (int k = 0; k < WC; ++k) point &= al[k] == ah[k];
+            if (point) {  // answered here: an empty code range for the locate
+                uint64_t key[3];
+                ph_key<WC>(cur.g, ph.gb, ph.WG, al, key);
+                uint32_t rk = 0;
+                if (ph_find(ph, key, rk) && rk > lsn32_rank(snap, ph.rank_base)) ph.flags[txn] = 1;
+                clo[q] = ~0ull;  // word 0 decides: lo above hi whatever the others hold
+                chi[q] = 0;
+                return;
+            }
+#pragma unroll
+            for (int k = 0; k < WC; ++k) {
+                clo[(size_t)k * p.n + q] = ok ? al[k] : ~0ull;
+                chi[(size_t)k * p.n + q] = ok ? ah[k] : 0;
+            }
+            return;
+        }
+    }
+    bound_map<WC>(p, cm, q, cur, clo, chi);
 }
 
 template <int WC>
@@ -191,7 +300,7 @@ hipError_t launch_rows_wc(const uint64_t *words, size_t stride, const uint32_t *
 
 template <int WC>
 hipError_t launch_probes_wc(const ProbeView &p, const CompactMeta &cm, uint64_t *clo,
-                            uint64_t *chi, hipStream_t s)
+                            uint64_t *chi, hipStream_t s, const PointHash &ph)
 {
     // (r02: one probe per thread beat 2 and 4 in flight on config 3)
     if (cm.W <= kProbeWords) {
@@ -202,9 +311,9 @@ hipError_t launch_probes_wc(const ProbeView &p, const CompactMeta &cm, uint64_t 
         const bool in_lds = bound_lds_bytes(cm.ng, cm.W) <= kBoundLdsBytes;
         const uint32_t lds = in_lds ? bound_lds_bytes(cm.ng, cm.W) : 0;
         if (in_lds)
-            k_compact_bounds<WC, true><<<blocks, kBoundThreads, lds, s>>>(p, cm, clo, chi);
+            k_compact_bounds<WC, true><<<blocks, kBoundThreads, lds, s>>>(p, cm, clo, chi, ph);
         else
-            k_compact_bounds<WC, false><<<blocks, kBoundThreads, lds, s>>>(p, cm, clo, chi);
+            k_compact_bounds<WC, false><<<blocks, kBoundThreads, lds, s>>>(p, cm, clo, chi, ph);
     } else
         k_compact_probes<WC><<<(p.n + 255) / 256, 256, 0, s>>>(p, cm, clo, chi);
     return hipGetLastError();
@@ -663,19 +772,35 @@ hipError_t compact_rows(const uint64_t *words, size_t stride, const uint32_t *gi
 }
 
 hipError_t compact_probes(const ProbeView &p, const CompactTables &t, uint64_t *clo, uint64_t *chi,
-                          hipStream_t s)
+                          hipStream_t s, const PointHash *php)
 {
     if (p.n == 0) return hipSuccess;
     const CompactMeta cm = meta_of(t);
+    PointHash ph{};
+    if (php && php->nb && php->e && php->flags && t.WC <= 3 && t.W <= kProbeWords) ph = *php;
     switch (t.WC) {
-    case 1: return launch_probes_wc<1>(p, cm, clo, chi, s);
-    case 2: return launch_probes_wc<2>(p, cm, clo, chi, s);
-    case 3: return launch_probes_wc<3>(p, cm, clo, chi, s);
-    case 4: return launch_probes_wc<4>(p, cm, clo, chi, s);
-    case 5: return launch_probes_wc<5>(p, cm, clo, chi, s);
-    case 6: return launch_probes_wc<6>(p, cm, clo, chi, s);
+    case 1: return launch_probes_wc<1>(p, cm, clo, chi, s, ph);
+    case 2: return launch_probes_wc<2>(p, cm, clo, chi, s, ph);
+    case 3: return launch_probes_wc<3>(p, cm, clo, chi, s, ph);
+    case 4: return launch_probes_wc<4>(p, cm, clo, chi, s, ph);
+    case 5: return launch_probes_wc<5>(p, cm, clo, chi, s, ph);
+    case 6: return launch_probes_wc<6>(p, cm, clo, chi, s, ph);
     default: return hipErrorInvalidValue;
     }
+}
+
+// one four-slot bucket per key: a quarter full, so a lookup of a key the
+// window does not hold -- half of config 3's points -- stops at its home
+// line nearly always (two-slot buckets three quarters full walked ~4 of
+// them: the bound kernel 30 -> 59 us, r06d)
+uint64_t point_hash_buckets(uint32_t n) { return (uint64_t)n + 64; }
+
+hipError_t point_hash_build(const CTiles &ct, uint64_t *e, uint64_t nb, hipStream_t s)
+{
+    hipError_t r = hipMemsetAsync(e, 0, 128 * nb, s);
+    if (r != hipSuccess || ct.n == 0) return r;
+    k_ph_insert<<<(ct.n + 255) / 256, 256, 0, s>>>(ct, e, nb);
+    return hipGetLastError();
 }
 
 // load this file's code object now (HIP loads it lazily at the first launch

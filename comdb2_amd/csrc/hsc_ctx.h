@@ -215,10 +215,26 @@ struct MapVec {
     {
         if (p) munmap(p, cap * sizeof(T));
     }
+    // The first reserve maps a large range of address space without
+    // reserving memory (MAP_NORESERVE: pages are backed as they are first
+    // written), so the store never moves; an mremap of tens of MB of page
+    // tables still cost an append ~0.3 ms (r06e).  If the system refuses the
+    // range, the store grows by mremap as before.
+    static constexpr size_t kVirtBytes = (size_t)1 << 36;
     void reserve(size_t k)
     {
         if (k <= cap) return;
         const size_t page = 4096 / sizeof(T) ? 4096 / sizeof(T) : 1;
+        if (!p) {
+            const size_t cv = std::max(k, kVirtBytes / sizeof(T)) / page * page;
+            void *q = mmap(nullptr, cv * sizeof(T), PROT_READ | PROT_WRITE,
+                           MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+            if (q != MAP_FAILED && cv >= k) {
+                p = (T *)q, cap = cv;
+                return;
+            }
+            if (q != MAP_FAILED) munmap(q, cv * sizeof(T));
+        }
         size_t c = std::max(k, std::max(2 * cap, (size_t)65536));
         c = (c + page - 1) / page * page;
         void *q = p ? mremap(p, cap * sizeof(T), c * sizeof(T), MREMAP_MAYMOVE)
@@ -591,6 +607,8 @@ struct hsc_ctx {
     bool ctiles = false;
     CTiles ctv{};
     DBuf d_ckey, d_crank, d_cfirst, d_crel, d_ctrad, d_ctb;
+    DBuf d_cph;               // the tiles' point index (PointHash), cph_nb buckets
+    uint64_t cph_nb = 0;
 
     // probe workspace
     DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;

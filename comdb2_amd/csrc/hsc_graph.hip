@@ -34,39 +34,18 @@ namespace hsc {
 
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
-// writers of the history -> rows (gid 0, words (key, txn), lsn 0) at the
-// positions of an exclusive scan of the write flags
-__global__ void k_gather_writers(size_t nops, const uint32_t *txn, const uint64_t *key,
-                                 const uint8_t *is_write, const uint32_t *pos, uint32_t *gid,
-                                 uint64_t *words, uint64_t *lsn, size_t stride)
-{
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nops || !is_write[i]) return;
-    const uint32_t p = pos[i];
-    gid[p] = 0;
-    words[p] = key[i];
-    words[stride + p] = txn[i];
-    lsn[p] = 0;
-}
-
-// Writers gathered without a flag array or a scan over the ops: a block of
-// kGwThreads x kGwItems ops counts its writers (wave ballots, one LDS scan),
-// takes its range with ONE atomic on the cursor and writes them in op order
-// inside the range (blocks land in atomic order: the writers are sorted by
-// (key, txn) next, so their order here does not matter).
+// Writers of the history -> rows (gid 0, words (key, txn), lsn 0), gathered
+// without a flag array or a scan over the ops: a block of
+// kGwThreads x kGwItems ops counts its writers (k_gw_count: no atomics, one
+// word per block), the block counts are scanned (24k words for 100M ops), and
+// k_gw_place writes each block's writers in op order at its offset (wave
+// ballots + one LDS scan).  (r06: one atomic per block on a single cursor
+// instead of the count pass serialised 24k blocks: 1.48 ms per 100M ops.)
 constexpr int kGwThreads = 256, kGwItems = 16;
-__global__ __launch_bounds__(kGwThreads) void k_gather_writers_blk(size_t nops, const uint32_t *txn,
-                                                                    const uint64_t *key,
-                                                                    const uint8_t *is_write, uint32_t *cursor,
-                                                                    uint32_t *gid, uint64_t *words,
-                                                                    uint64_t *lsn, size_t stride)
+__device__ __forceinline__ uint32_t gw_bits(size_t nops, const uint8_t *is_write, size_t base, uint32_t &cnt)
 {
-    __shared__ uint32_t wsum[kGwThreads / 64];
-    __shared__ uint32_t bbase;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const size_t base = (size_t)blockIdx.x * (kGwThreads * kGwItems);
-    uint32_t cnt = 0;
     uint32_t w = 0;  // bit k: op k of this thread writes
+    cnt = 0;
 #pragma unroll
     for (int k = 0; k < kGwItems; ++k) {
         const size_t i = base + (size_t)k * kGwThreads + threadIdx.x;
@@ -74,6 +53,41 @@ __global__ __launch_bounds__(kGwThreads) void k_gather_writers_blk(size_t nops, 
         w |= (uint32_t)wr << k;
         cnt += wr;
     }
+    return w;
+}
+
+__global__ __launch_bounds__(kGwThreads) void k_gw_count(size_t nops, const uint8_t *is_write, uint32_t *bc)
+{
+    __shared__ uint32_t wsum[kGwThreads / 64];
+    uint32_t cnt;
+    (void)gw_bits(nops, is_write, (size_t)blockIdx.x * (kGwThreads * kGwItems), cnt);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int q = 0; q < kGwThreads / 64; ++q) t += wsum[q];
+        bc[blockIdx.x] = t;
+    }
+}
+
+__global__ __launch_bounds__(kGwThreads) void k_gw_place(size_t nops, const uint32_t *txn, const uint64_t *key,
+                                                         const uint8_t *is_write, const uint32_t *boff,
+                                                         uint32_t *gid, uint64_t *words, uint64_t *lsn,
+                                                         size_t stride)
+{
+    // the block's writers in op order through LDS, then coalesced stores
+    // (each thread storing its own writers at p, p + 1, ... scattered every
+    // store instruction over ~5 x 64 words: 5.8 GB of partial-line writes
+    // per 100M ops, r06d PMC)
+    __shared__ uint64_t sk[kGwThreads * kGwItems], st[kGwThreads * kGwItems];
+    __shared__ uint32_t wsum[kGwThreads / 64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const size_t base = (size_t)blockIdx.x * (kGwThreads * kGwItems);
+    uint32_t cnt;
+    const uint32_t w = gw_bits(nops, is_write, base, cnt);
     uint32_t inc = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -82,32 +96,41 @@ __global__ __launch_bounds__(kGwThreads) void k_gather_writers_blk(size_t nops, 
     }
     if (lane == 63) wsum[wv] = inc;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t t = 0;
+    uint32_t p = inc - cnt, tot = 0;
 #pragma unroll
-        for (int q = 0; q < kGwThreads / 64; ++q) t += wsum[q];
-        bbase = t ? atomicAdd(cursor, t) : 0;
+    for (int q = 0; q < kGwThreads / 64; ++q) {
+        p += q < wv ? wsum[q] : 0;
+        tot += wsum[q];
     }
-    __syncthreads();
-    uint32_t p = bbase + inc - cnt;
-#pragma unroll
-    for (int q = 0; q < kGwThreads / 64; ++q) p += q < wv ? wsum[q] : 0;
 #pragma unroll
     for (int k = 0; k < kGwItems; ++k) {
         if (!((w >> k) & 1u)) continue;
         const size_t i = base + (size_t)k * kGwThreads + threadIdx.x;
-        gid[p] = 0;
-        words[p] = key[i];
-        words[stride + p] = txn[i];
-        lsn[p] = 0;
+        sk[p] = key[i];
+        st[p] = txn[i];
         ++p;
+    }
+    __syncthreads();
+    const size_t b0 = boff[blockIdx.x];
+    for (uint32_t j = threadIdx.x; j < tot; j += kGwThreads) {
+        words[b0 + j] = sk[j];
+        words[stride + b0 + j] = st[j];
+        gid[b0 + j] = 0;
+        lsn[b0 + j] = 0;
     }
 }
 
-__global__ void k_write_flags(size_t nops, const uint8_t *is_write, uint32_t *flags)
+
+// a backward edge a -> b (a > b) covers [b, a] (graph_cover's k_back_diff,
+// done while a raw build emits the row: one pass over the raw rows less)
+__device__ __forceinline__ void back_row(uint32_t *diff, uint64_t row)
 {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nops) flags[i] = is_write[i] ? 1u : 0u;
+    if (!diff || row == ~0ull) return;
+    const uint32_t a = (uint32_t)(row >> 32), b = (uint32_t)row;
+    if (a > b) {
+        atomicAdd(&diff[b], 1u);
+        atomicAdd(&diff[a + 1], 0xFFFFFFFFu);
+    }
 }
 
 // Edge rows: word = src << 32 | dst, payload = type; invalid = ~0.
@@ -230,7 +253,7 @@ __global__ void k_edges_reads_pk(size_t nops, const uint32_t *txn, const uint64_
                                  const uint8_t *is_write, const uint32_t *observed, uint32_t nu,
                                  const uint64_t *wkey, const uint64_t *wtxn, const uint64_t *pk,
                                  const uint32_t *dir, PairPack pp, uint64_t *ew, uint64_t *et,
-                                 uint32_t *eg, int skip_rw)
+                                 uint32_t *eg, int skip_rw, uint32_t *diff)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nops) return;
@@ -288,6 +311,8 @@ __global__ void k_edges_reads_pk(size_t nops, const uint32_t *txn, const uint64_
     const size_t s = (size_t)nu + 2 * i;
     ew[s] = wr;
     ew[s + 1] = rw;
+    back_row(diff, wr);
+    back_row(diff, rw);
     if (et) {
         et[s] = kDepWR;
         eg[s] = 0;
@@ -331,18 +356,6 @@ struct RpArgs {
     uint32_t *diff;      // raw builds: the cover's interval diffs of backward edges (else null)
     int skip_rw;
 };
-
-// a backward edge a -> b (a > b) covers [b, a] (graph_cover's k_back_diff,
-// done while the raw build emits the row)
-__device__ __forceinline__ void rp_back(uint32_t *diff, uint64_t row)
-{
-    if (!diff || row == ~0ull) return;
-    const uint32_t a = (uint32_t)(row >> 32), b = (uint32_t)row;
-    if (a > b) {
-        atomicAdd(&diff[b], 1u);
-        atomicAdd(&diff[a + 1], 0xFFFFFFFFu);
-    }
-}
 
 // x of a read's "first writer after (k, ob)" search, or false when it needs
 // none (key without writers) / the row search (an observed txn outside the
@@ -428,14 +441,14 @@ __global__ __launch_bounds__(kRpThreads) void k_rp_scatter(RpArgs a, PairPack pp
                 const uint64_t row = ((uint64_t)r << 32) | a.wtxn[lo];
                 a.ew[o] = row;
                 if (a.et) a.et[o] = kDepRW, a.eg[o] = 0;
-                rp_back(a.diff, row);
+                back_row(a.diff, row);
             }
         }
     }
     const size_t s = (size_t)a.nu + i;
     a.ew[s] = wr;
     if (a.et) a.et[s] = kDepWR, a.eg[s] = 0;
-    rp_back(a.diff, wr);
+    back_row(a.diff, wr);
 }
 
 __global__ __launch_bounds__(kRpThreads) void k_rp_join(RpArgs a, PairPack pp)
@@ -483,7 +496,7 @@ __global__ __launch_bounds__(kRpThreads) void k_rp_join(RpArgs a, PairPack pp)
         const size_t o = (size_t)a.nu + a.nops + it;
         a.ew[o] = rw;
         if (a.et) a.et[o] = kDepRW, a.eg[o] = 0;
-        rp_back(a.diff, rw);
+        back_row(a.diff, rw);
     }
 }
 
@@ -707,16 +720,19 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     CK(g.wg2.ensure(4 * wcap));
     CK(g.ww2.ensure(16 * wcap));
     CK(g.wl2.ensure(8 * wcap));
-    CK(g.count.ensure(64));
-    CK(hipMemsetAsync(g.count.as<uint32_t>() + 8, 0, 4, s));
-    if (nops)
-        k_gather_writers_blk<<<(unsigned)((nops + kGwThreads * kGwItems - 1) / (kGwThreads * kGwItems)),
-                               kGwThreads, 0, s>>>(nops, in.txn, in.key, in.is_write, g.count.as<uint32_t>() + 8,
-                                                   g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), g.wl.as<uint64_t>(),
-                                                   wcap);
+    const size_t gwb = (nops + kGwThreads * kGwItems - 1) / (kGwThreads * kGwItems);
+    CK(g.flags.ensure(4 * (gwb + 1)));
+    CK(g.scratch.ensure(std::max(scan_scratch_bytes(gwb + 1), (size_t)1024)));
+    uint32_t *bc = g.flags.as<uint32_t>();
+    if (gwb) k_gw_count<<<(unsigned)gwb, kGwThreads, 0, s>>>(nops, in.is_write, bc);
+    CK(hipMemsetAsync(bc + gwb, 0, 4, s));
+    CK(scan_exclusive_u32(bc, gwb + 1, g.scratch.as<uint32_t>(), s));
+    if (gwb)
+        k_gw_place<<<(unsigned)gwb, kGwThreads, 0, s>>>(nops, in.txn, in.key, in.is_write, bc, g.wg.as<uint32_t>(),
+                                                         g.ww.as<uint64_t>(), g.wl.as<uint64_t>(), wcap);
     CK(hipGetLastError());
     uint32_t nw = 0;
-    CK(hipMemcpyAsync(&nw, g.count.as<uint32_t>() + 8, 4, hipMemcpyDeviceToHost, s));
+    CK(hipMemcpyAsync(&nw, bc + gwb, 4, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
     size_t rsb = std::max(radix_scratch_bytes(nw, 2), scan_scratch_bytes(nw) + 64);
     rsb = std::max(rsb, packed_scratch_bytes(nw));
@@ -807,7 +823,20 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         while (pp.shift < 64 && ((pp.last - pp.base) >> pp.shift) >= ((uint64_t)1 << pp.D)) ++pp.shift;
         k_pair_dir<<<blocks(((size_t)1 << pp.D) + 2), 256, 0, s>>>(nu, g.pk.as<uint64_t>(), pp,
                                                                  g.pdir.as<uint32_t>());
-        static const bool rp = getenv("HSC_GRAPH_RP") == nullptr || atoi(getenv("HSC_GRAPH_RP")) != 0;  // (A/B)
+        // the partitioned read search: measured slower on config 4 (r06c trace:
+        // count 3.0 + scatter 3.2 + join 1.0 ms against 3.5 ms for the
+        // directory search -- the count's per-read global atomics on 16k
+        // partition counters), so off unless HSC_GRAPH_RP=1 (A/B)
+        static const bool rp = getenv("HSC_GRAPH_RP") != nullptr && atoi(getenv("HSC_GRAPH_RP")) != 0;
+        // raw builds (the sharded SCC's): the cover's backward-edge diffs as
+        // the rows are emitted (ww rows are forward: txns ascend inside a key)
+        uint32_t *diff = nullptr;
+        if (!full && !in.n_extra && in.ntxn) {
+            CK(g.diff.ensure(4 * ((size_t)in.ntxn + 2)));
+            CK(hipMemsetAsync(g.diff.p, 0, 4 * ((size_t)in.ntxn + 2), s));
+            diff = g.diff.as<uint32_t>();
+            diff_done = true;
+        }
         if (rp) {
             RpArgs a{};
             a.nops = nops, a.txn = in.txn, a.key = in.key, a.is_write = in.is_write, a.observed = in.observed;
@@ -820,14 +849,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
             CK(g.rp_items.ensure(16 * std::max<size_t>(nops, 1)));
             a.items = g.rp_items.as<ulonglong2>();
             a.ew = g.ew.as<uint64_t>(), a.et = et, a.eg = eg, a.skip_rw = in.skip_rw ? 1 : 0;
-            // raw builds (the sharded SCC's): the cover's backward-edge diffs as
-            // the rows are emitted (ww rows are forward: txns ascend inside a key)
-            if (!full && !in.n_extra && in.ntxn) {
-                CK(g.diff.ensure(4 * ((size_t)in.ntxn + 2)));
-                CK(hipMemsetAsync(g.diff.p, 0, 4 * ((size_t)in.ntxn + 2), s));
-                a.diff = g.diff.as<uint32_t>();
-                diff_done = true;
-            }
+            a.diff = diff;
             CK(hipMemsetAsync(a.cnt, 0, 4 * ((size_t)a.np + 1), s));
             k_rp_count<<<blocks(nops), kRpThreads, 0, s>>>(a, pp);
             k_rp_scan<<<1, 1024, 0, s>>>(a);
@@ -843,7 +865,8 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         } else {
             k_edges_reads_pk<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu,
                                                           wkey, wtxn, g.pk.as<uint64_t>(), g.pdir.as<uint32_t>(),
-                                                          pp, g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0);
+                                                          pp, g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0,
+                                                          diff);
         }
     } else if (nops) {
         k_edges_reads<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed,
@@ -1258,6 +1281,85 @@ hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t 
     return hipGetLastError();
 }
 
+// The SCC of a small cut in ONE workgroup, every array in LDS: the same
+// colouring as graph_scc (colour = the largest id reaching a node, roots =
+// nodes of their own colour, a backward sweep inside each colour; repeat on
+// what is left), with edge sweeps instead of frontiers and barriers instead
+// of host round trips (graph_scc: a launch, a copy and a stream sync per
+// frontier step -- 1.4 ms for config 4's ~1k-node cut).  Rows: cut-id edges
+// (a << 32 | b, ~0 = none).  Labels = the largest node id of each SCC, as
+// graph_scc's.  out[0] rounds, out[1] sweeps.
+constexpr uint32_t kSccSmallNodes = 4096, kSccSmallEdges = 24576;
+constexpr int kSccSmallThreads = 1024;
+__global__ __launch_bounds__(kSccSmallThreads) void k_scc_small(uint32_t nn, size_t m, const uint64_t *rows,
+                                                               uint32_t *scc, uint32_t *out)
+{
+    __shared__ uint32_t E[kSccSmallEdges];  // a << 16 | b
+    __shared__ uint32_t col[kSccSmallNodes];
+    __shared__ uint8_t act[kSccSmallNodes], mk[kSccSmallNodes];
+    __shared__ uint32_t ne, changed, left, rounds, sweeps;
+    const uint32_t t = threadIdx.x;
+    if (t == 0) ne = 0, rounds = 0, sweeps = 0;
+    for (uint32_t v = t; v < nn; v += kSccSmallThreads) act[v] = 1, mk[v] = 0;
+    __syncthreads();
+    for (size_t i = t; i < m; i += kSccSmallThreads) {
+        const uint64_t r = rows[i];
+        if (r == ~0ull) continue;
+        const uint32_t a = (uint32_t)(r >> 32), b = (uint32_t)r;
+        if (a >= nn || b >= nn || a == b) continue;
+        E[atomicAdd(&ne, 1u)] = a << 16 | b;
+    }
+    __syncthreads();
+    const uint32_t n_e = ne;
+    for (;;) {
+        if (t == 0) rounds++, left = 0;
+        for (uint32_t v = t; v < nn; v += kSccSmallThreads)
+            if (act[v]) col[v] = v;
+        __syncthreads();
+        do {  // forward: colour = the largest active id reaching the node
+            __syncthreads();
+            if (t == 0) changed = 0, sweeps++;
+            __syncthreads();
+            for (uint32_t i = t; i < n_e; i += kSccSmallThreads) {
+                const uint32_t a = E[i] >> 16, b = E[i] & 0xFFFFu;
+                if (!act[a] || !act[b]) continue;
+                const uint32_t ca = col[a];
+                if (ca > col[b] && atomicMax(&col[b], ca) < ca) changed = 1;
+            }
+            __syncthreads();
+        } while (changed);
+        for (uint32_t v = t; v < nn; v += kSccSmallThreads)
+            if (act[v] && col[v] == v) mk[v] = 1;
+        __syncthreads();
+        do {  // backward from the roots, inside a colour
+            __syncthreads();
+            if (t == 0) changed = 0, sweeps++;
+            __syncthreads();
+            for (uint32_t i = t; i < n_e; i += kSccSmallThreads) {
+                const uint32_t a = E[i] >> 16, b = E[i] & 0xFFFFu;
+                if (!act[a] || !act[b] || mk[a] || !mk[b] || col[a] != col[b]) continue;
+                mk[a] = 1;
+                changed = 1;
+            }
+            __syncthreads();
+        } while (changed);
+        for (uint32_t v = t; v < nn; v += kSccSmallThreads) {
+            if (!act[v]) continue;
+            if (mk[v]) {
+                scc[v] = col[v];
+                act[v] = 0;
+                mk[v] = 0;
+            } else {
+                left = 1;
+            }
+        }
+        __syncthreads();
+        if (!left) break;
+        __syncthreads();
+    }
+    if (t == 0) out[0] = rounds, out[1] = sweeps;
+}
+
 hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *rows, size_t m,
                           GraphBufs &g, uint32_t *scc_out, uint32_t *n_cut, uint32_t *rounds,
                           uint32_t *iterations, hipStream_t s)
@@ -1304,6 +1406,19 @@ hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *row
     CK(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
     if (hbad) return hipErrorInvalidValue;  // a row outside the cover: not a cut of it
+    if (nc <= kSccSmallNodes && m <= kSccSmallEdges) {  // the usual small cut: one workgroup
+        CK(g.scc.ensure(4 * ((size_t)nc + 1)));
+        k_scc_small<<<1, kSccSmallThreads, 0, s>>>(nc, m, g.ew.as<uint64_t>(), g.scc.as<uint32_t>(),
+                                                   g.count.as<uint32_t>() + 4);
+        CK(hipGetLastError());
+        uint32_t ri[2] = {0, 0};
+        CK(hipMemcpyAsync(ri, g.count.as<uint32_t>() + 4, 8, hipMemcpyDeviceToHost, s));
+        k_scc_out<<<blocks(nn), 256, 0, s>>>(nn, cover, id, g.scc.as<uint32_t>(), txn_of, scc_out);
+        CK(hipGetLastError());
+        CK(hipStreamSynchronize(s));
+        *rounds = ri[0], *iterations = ri[1];
+        return hipSuccess;
+    }
     CK(graph_rows_csr(m, ecap, nc, g, s));
     CK(graph_scc(nc, g, rounds, iterations, s));
     // sub_scc lives in g.scc (nc entries); the caller's scc_out gets all nn
@@ -1320,7 +1435,7 @@ hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *row
 hipError_t warm_graph()
 {
     hipFuncAttributes a;
-    return hipFuncGetAttributes(&a, (const void *)k_write_flags);
+    return hipFuncGetAttributes(&a, (const void *)k_gw_count);
 }
 
 }  // namespace hsc

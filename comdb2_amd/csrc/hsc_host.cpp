@@ -463,6 +463,7 @@ static int build_compact(hsc_ctx *c, const WinView &w)
 // table and LDS take; otherwise dense batches stay on the wide pipeline.
 static int build_ctiles(hsc_ctx *c)
 {
+    c->cph_nb = 0;
     const WinView &v = c->wc;
     const int ng = (int)c->groups.size();
     int gb = 0;
@@ -499,6 +500,14 @@ static int build_ctiles(hsc_ctx *c)
                            c->d_crank.as<uint32_t>(), c->d_cfirst.as<uint64_t>(),
                            c->d_crel.as<uint64_t>(), c->d_ctrad.as<uint32_t>(),
                            c->d_ctb.as<uint32_t>(), s));
+    // the point index (hsc_compact.hip PointHash): points are answered by the
+    // bound kernel (HSC_PATH_NO_CT_POINTS: they take join records, the r05 path)
+    if (!(c->paths & HSC_PATH_NO_CT_POINTS) && ct.n) {
+        const uint64_t nb = point_hash_buckets(ct.n);
+        HIPCHK(c, c->d_cph.ensure(128 * nb));
+        HIPCHK(c, point_hash_build(ct, c->d_cph.as<uint64_t>(), nb, s));
+        c->cph_nb = nb;
+    }
     HIPCHK(c, hipMemcpyAsync(&ct.base0, c->d_cfirst.p, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     if (getenv("HSC_CT_STATS")) {  // diagnostics: fullest buckets of the locate's and the join's tables
@@ -1125,6 +1134,61 @@ static int pend_mirror(hsc_ctx *c)
     return HSC_OK;
 }
 
+// Both delta-run buffers at full size for the window's words: merges never
+// reallocate a run holding rows (a wider key schedules a rebuild).  Called by
+// the first merge, or ahead of it by append_prepare.
+static int delta_alloc(hsc_ctx *c, int W)
+{
+    const size_t wbytes = 8 * (size_t)W * kDeltaCap;
+    if (c->dcap >= kDeltaCap && c->d_dwords[0].bytes >= wbytes && c->d_dwords[1].bytes >= wbytes) return HSC_OK;
+    if (c->dn) return fail(c, HSC_EINVAL, "delta run resized while holding rows");
+    c->dcap = kDeltaCap;
+    for (int b = 0; b < 2; ++b) {
+        HIPCHK(c, c->d_dgid[b].ensure(4 * (size_t)kDeltaCap));
+        HIPCHK(c, c->d_dwords[b].ensure(wbytes));
+        HIPCHK(c, c->d_dlsn[b].ensure(8 * (size_t)kDeltaCap));
+    }
+    HIPCHK(c, c->d_dbmax.ensure(8 * (size_t)(kDeltaCap / 64 + 1)));
+    return HSC_OK;
+}
+
+static void fold_worker(hsc_ctx *c);
+static hipError_t create_stream(hipStream_t *st, bool high);
+
+// What the append path would otherwise set up on a commit's clock the first
+// time it needs it: the delta-run buffers (hipMallocs, at the first merge of
+// the pending tail) and, with background folds, the fold's shadow context
+// with its stream, the worker thread and its event.  Run after every window
+// build, so a commit stream pays them at its first check, which builds the
+// window anyway.  (A stream created by the worker at the first fold stalled
+// the checks running meanwhile by 1.6 ms: r06e, scripts/fold_diag.py.)
+static int append_prepare(hsc_ctx *c)
+{
+    if (c->multi || c->host_only || !c->live || c->W <= 0) return HSC_OK;
+    HIPCHK_RC(c, delta_alloc(c, c->W));
+    if (!c->fold_bg) return HSC_OK;
+    if (!c->fold_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fold_ev, hipEventDisableTiming));
+    if (!c->shadow && c->fold_state.load(std::memory_order_acquire) == kFoldIdle) {
+        hsc_ctx *s = new (std::nothrow) hsc_ctx();
+        if (!s) return fail(c, HSC_ENOMEM, "fold context");
+        s->device = c->device;
+        if (create_stream(&s->own_stream, false) != hipSuccess) {
+            delete s;
+            return fail(c, HSC_EDEVICE, "fold stream");
+        }
+        s->stream = s->own_stream;
+        c->shadow = s;
+    }
+    if (!c->fold_thread.joinable()) {
+        try {
+            c->fold_thread = std::thread(fold_worker, c);
+        } catch (...) {
+            // fold_start tries again (and folds inline when it cannot)
+        }
+    }
+    return HSC_OK;
+}
+
 // lazy (the append entries): an append that fits stays in the pending tail.
 // Otherwise -- and for every caller that probes outside k_small_narrow --
 // the unmerged rows go to the delta run now.
@@ -1186,19 +1250,7 @@ static int flush_appends(hsc_ctx *c, bool lazy = false)
         HIPCHK(c, hipMemcpyAsync(c->d_agid.p, c->h_app->p, sb, hipMemcpyHostToDevice, s));
         db = c->d_agid.as<uint8_t>();
     }
-    // both run buffers at full size for the window's words: merges never
-    // reallocate a run holding rows (a wider key schedules a rebuild above)
-    const size_t wbytes = 8 * (size_t)W * kDeltaCap;
-    if (c->dcap < kDeltaCap || c->d_dwords[0].bytes < wbytes || c->d_dwords[1].bytes < wbytes) {
-        if (c->dn) return fail(c, HSC_EINVAL, "delta run resized while holding rows");
-        c->dcap = kDeltaCap;
-        for (int b = 0; b < 2; ++b) {
-            HIPCHK(c, c->d_dgid[b].ensure(4 * (size_t)kDeltaCap));
-            HIPCHK(c, c->d_dwords[b].ensure(wbytes));
-            HIPCHK(c, c->d_dlsn[b].ensure(8 * (size_t)kDeltaCap));
-        }
-        HIPCHK(c, c->d_dbmax.ensure(8 * (size_t)(kDeltaCap / 64 + 1)));
-    }
+    HIPCHK_RC(c, delta_alloc(c, W));
     DeltaView a{};
     a.gid = (const uint32_t *)db;
     a.words = (const uint64_t *)(db + woff);
@@ -1339,6 +1391,7 @@ static void swap_window(hsc_ctx *a, hsc_ctx *b)
     swap(a->ctiles, b->ctiles), swap(a->ctv, b->ctv);
     swap(a->d_ckey, b->d_ckey), swap(a->d_crank, b->d_crank), swap(a->d_cfirst, b->d_cfirst);
     swap(a->d_crel, b->d_crel), swap(a->d_ctrad, b->d_ctrad), swap(a->d_ctb, b->d_ctb);
+    swap(a->d_cph, b->d_cph), swap(a->cph_nb, b->cph_nb);
 }
 
 static DeltaView frozen_view(const hsc_ctx *c)
@@ -1366,6 +1419,17 @@ static hipError_t create_stream(hipStream_t *st, bool high)
     return hipStreamCreateWithPriority(st, hipStreamNonBlocking, high ? greatest : least);
 }
 
+// HSC_FOLD_TRACE: fold events with a steady-clock stamp (diagnostics)
+static bool fold_trace()
+{
+    static const bool on = getenv("HSC_FOLD_TRACE") != nullptr;
+    return on;
+}
+static double trace_us()
+{
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 // The fold worker (one host thread per context, started by its first fold):
 // it creates the shadow context and its low-priority stream itself, then
 // for every job copies the main window's versions and the frozen run into
@@ -1387,21 +1451,8 @@ static void fold_worker(hsc_ctx *c)
         (void)hipSetDevice(c->device);
         int rc = HSC_OK;
         std::string why;
-        hsc_ctx *s = c->shadow;
-        if (!s) {
-            s = new (std::nothrow) hsc_ctx();
-            if (s) {
-                s->device = c->device;
-                if (create_stream(&s->own_stream, false) != hipSuccess) {
-                    delete s;
-                    s = nullptr;
-                } else {
-                    s->stream = s->own_stream;
-                }
-            }
-            if (!s) rc = HSC_EDEVICE, why = "fold context";
-            c->shadow = s;  // (read by the caller's thread only after kFoldDone)
-        }
+        hsc_ctx *s = c->shadow;  // (made by append_prepare when the window was built)
+        if (!s) rc = HSC_EDEVICE, why = "fold context";
         if (rc == HSC_OK) {
             s->groups = std::move(j.groups);  // what device_build reads of the dictionaries
             s->table_names = std::move(j.table_names);
@@ -1409,9 +1460,12 @@ static void fold_worker(hsc_ctx *c)
             s->layout = j.layout;
             s->paths = j.paths;
             s->W = j.W;
+            const double tw0 = fold_trace() ? trace_us() : 0;
             const size_t nm = j.nm, nf = j.nf, n_in = nm + nf;
             const int W = j.W;
-            s->cap = window_cap(n_in);
+            // the shadow's buffers (its own, or the main window's after a
+            // swap) are kept while they fit, and grow with room for later folds
+            if (s->cap < n_in) s->cap = window_cap(n_in + n_in / 2 + c->fold_rows);
             hipStream_t ss = s->stream;
             hipError_t e = s->d_gid.ensure(4 * s->cap);
             if (e == hipSuccess) e = s->d_words.ensure(8 * (size_t)W * s->cap);
@@ -1429,12 +1483,16 @@ static void fold_worker(hsc_ctx *c)
                 cp(dst, (const uint64_t *)j.words2 + (size_t)w * j.cap, 8 * nm);
                 cp(dst + nm, (const uint64_t *)j.fwords + (size_t)w * j.dcap, 8 * nf);
             }
+            const double tb0 = fold_trace() ? trace_us() : 0;
             if (e != hipSuccess) {
                 rc = HSC_EDEVICE, why = std::string("fold copies: ") + hipGetErrorString(e);
             } else {
                 rc = device_build(s, n_in);
                 if (rc) why = s->err;
             }
+            if (fold_trace())
+                fprintf(stderr, "[fold] %.0f worker: n_in %zu cap %zu copies+allocs %.0f us build %.0f us\n", trace_us(),
+                        n_in, s->cap, tb0 - tw0, trace_us() - tb0);
         }
         {
             std::lock_guard<std::mutex> g(c->fold_mu);
@@ -1473,6 +1531,7 @@ static void fold_stop(hsc_ctx *c)
 // buffers -- the window before the last swap) orders the worker's copies.
 static int fold_start(hsc_ctx *c)
 {
+    if (!c->shadow) HIPCHK_RC(c, append_prepare(c));  // (normally made at the build)
     if (!c->fold_ev) HIPCHK(c, hipEventCreateWithFlags(&c->fold_ev, hipEventDisableTiming));
     if (!c->fold_thread.joinable()) {
         try {
@@ -1506,6 +1565,7 @@ static int fold_start(hsc_ctx *c)
     }
     c->fold_cv.notify_all();
     c->folds_started++;
+    if (fold_trace()) fprintf(stderr, "[fold] %.0f start: main %zu frozen %zu\n", trace_us(), c->n_all, c->fn);
     return HSC_OK;
 }
 
@@ -1525,6 +1585,7 @@ static int fold_finish(hsc_ctx *c, bool wait)
         (void)fail(c, c->fold_rc ? c->fold_rc : HSC_EDEVICE, ("background fold: " + c->fold_err).c_str());
         return HSC_OK;
     }
+    const double ts0 = fold_trace() ? trace_us() : 0;
     HIPCHK(c, wait_lanes(c));  // batches of other streams finish on the old window
     swap_window(c, s);
     // table maxima raised while the fold ran (the shadow's are as of its start)
@@ -1539,6 +1600,7 @@ static int fold_finish(hsc_ctx *c, bool wait)
     HIPCHK(c, hipEventRecord(c->fold_ev, c->stream));  // the old window's last readers
     c->folds_swapped++;
     c->fold_ms = s->last.ingest_ms;
+    if (fold_trace()) fprintf(stderr, "[fold] %.0f swap %.0f us (n %zu)\n", trace_us(), trace_us() - ts0, c->n);
     return HSC_OK;
 }
 
@@ -1573,12 +1635,16 @@ static int ensure_built(hsc_ctx *c)
     if (!c->dirty) return HSC_OK;
     if (c->merge_pending && c->merge_is_fold) c->folds_inline++;  // (a new group / wider key: a rebuild)
     c->merge_is_fold = false;
+    int rc;
     if (c->host_staged) {  // staged rows include the appended ones (and a frozen run's)
         fold_discard(c);
-        return build_from_host(c);
+        rc = build_from_host(c);
+    } else if (c->merge_pending) {
+        rc = merge_delta(c);
+    } else {
+        return fail(c, HSC_ESTATE, "device window must be re-ingested");
     }
-    if (c->merge_pending) return merge_delta(c);
-    return fail(c, HSC_ESTATE, "device window must be re-ingested");
+    return rc ? rc : append_prepare(c);
 }
 
 // ---------------------------------------------------------------------------
@@ -2579,8 +2645,17 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
     if (tm) HIPCHK(c, hipEventRecord(c->ev[0], s));
     // (measured: the bound mapping fused into the locate -- code bounds kept in
     // registers -- ran 83 us against 67 us for the two kernels on config 3)
+    PointHash ph{};
+    if (c->cph_nb) {
+        ph.e = c->d_cph.as<uint64_t>();
+        ph.nb = c->cph_nb;
+        ph.WG = ct.WG;
+        ph.gb = ct.gb;
+        ph.rank_base = ct.rank_base;
+        ph.flags = flags;
+    }
     if (p.n)
-        HIPCHK(c, compact_probes(p, c->ct, c->p_code_lo.as<uint64_t>(), c->p_code_hi.as<uint64_t>(), s));
+        HIPCHK(c, compact_probes(p, c->ct, c->p_code_lo.as<uint64_t>(), c->p_code_hi.as<uint64_t>(), s, &ph));
     HIPCHK(c, launch_locate_c(ct, wt, p, c->p_code_lo.as<uint64_t>(), c->p_code_hi.as<uint64_t>(),
                               work, flags, s));
     if (tm) HIPCHK(c, hipEventRecord(c->ev[1], s));
@@ -3358,7 +3433,7 @@ int hsc_set_fold(hsc_ctx *c, size_t rows, int background)
     MuGuard g(c);
     c->fold_rows = rows ? rows : kDeltaCap / 2;
     c->fold_bg = background != 0;
-    return HSC_OK;
+    return c->dirty ? HSC_OK : append_prepare(c);  // (a built window: the worker starts now)
 }
 
 int hsc_fold_stats(hsc_ctx *c, uint64_t out[4])

@@ -34,7 +34,10 @@ struct DBuf {
         if (p) (void)hipFree(p);
         p = nullptr;
         bytes = 0;
-        size_t b = want + want / 8 + 256;
+        // half again as much: a window that keeps growing (folds of a commit
+        // stream) reallocates O(log n) times -- a hipFree synchronises the
+        // device, which a fold's worker thread must not do on every fold
+        size_t b = want + want / 2 + 256;
         hipError_t e = hipMalloc(&p, b);
         if (e == hipSuccess) bytes = b;
         return e;
@@ -539,8 +542,9 @@ hipError_t compact_unpack_dedupe(const uint64_t *keys, size_t n, const CompactTa
 hipError_t warm_csort();
 // lo/hi bounds (W words) -> code bounds (WC words, SoA [WC][n]); ranges that
 // miss their group's rows become (~0, 0)
+struct PointHash;
 hipError_t compact_probes(const ProbeView &p, const CompactTables &t, uint64_t *clo, uint64_t *chi,
-                          hipStream_t s);
+                          hipStream_t s, const PointHash *ph = nullptr);
 // Compact tiles (hsc_ctiles.hip): the compact window as one sorted array of
 // WG-word keys gid || code (WG <= 3) with 32-bit commit times, 2048-row
 // tiles, for dense batches.
@@ -563,6 +567,23 @@ struct CTiles {
     uint32_t *recs;          // chunk areas of 2 x chunk 64-byte records (k_locate_c)
     int dbg;                 // diagnostics (HSC_CT_DBG): 1 join skips the searches, 2 also the gathers
 };
+// Exact-key index of the compact tiles' keys for point probes (lo == hi):
+// open addressing over 128-byte buckets of four 32-byte entries {key words
+// 0-2, rank} (rank 0 = empty; a row's rank is >= 1), linear probing by bucket.
+// The bound kernel answers a point whose code bounds meet by one lookup --
+// conflict iff the key is present with rank > r(S) -- sets the read set's flag
+// and writes the probe an empty code range, so the locate makes no record for
+// it and the join never searches it (the join's answer for a point record is
+// the same: the row equal to the key, its rank against r(S)).
+struct PointHash {
+    const uint64_t *e;   // [nb][4][4]
+    uint64_t nb;         // buckets (0: no index)
+    int WG, gb;          // the tiles' key words and group bits
+    uint64_t rank_base;  // CTiles::rank_base
+    uint8_t *flags;      // the batch's conflict flags (the locate's)
+};
+uint64_t point_hash_buckets(uint32_t n);
+hipError_t point_hash_build(const CTiles &ct, uint64_t *e, uint64_t nb, hipStream_t s);
 hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *gid,
                         const uint64_t *lsn, const CTiles &ct, uint64_t *key, uint32_t *rank,
                         uint64_t *first, uint64_t *rel, uint32_t *trad, uint32_t *tb,

@@ -118,6 +118,75 @@ __global__ __launch_bounds__(256) void k_vary_mask(int W, size_t n, const uint32
     }
 }
 
+// The same masks and LSN span in ONE pass for keys of WT <= 4 words: every
+// row's words, gid and LSN are loaded together (U rows per thread, all loads
+// in flight before the first OR), 8 workgroups per CU.  k_vary_mask above
+// walks the rows once per word with 2 workgroups per CU: 100 us for config
+// 2's 280 MB (2.8 TB/s).
+template <int WT>
+__global__ __launch_bounds__(256) void k_vary_mask_w(size_t n, const uint32_t *gid, const uint64_t *words,
+                                                     size_t stride, const uint64_t *lsn,
+                                                     unsigned long long *mask)
+{
+    constexpr int U = 4;
+    __shared__ uint64_t part[256 / 64][WT + 3];
+    uint64_t ref[WT + 1], m[WT + 1];
+#pragma unroll
+    for (int j = 0; j < WT; ++j) ref[j] = words[(size_t)j * stride], m[j] = 0;
+    ref[WT] = gid[0], m[WT] = 0;
+    uint64_t lo = ~0ull, hi = 0;
+    for (size_t i0 = (size_t)blockIdx.x * 256 * U + threadIdx.x; i0 < n; i0 += (size_t)gridDim.x * 256 * U) {
+        uint64_t v[U][WT + 1], l[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = i0 + (size_t)u * 256;
+            const bool ok = i < n;
+#pragma unroll
+            for (int j = 0; j < WT; ++j) v[u][j] = ok ? words[(size_t)j * stride + i] : ref[j];
+            v[u][WT] = ok ? gid[i] : ref[WT];
+            l[u] = lsn ? lsn[ok ? i : i0] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int j = 0; j <= WT; ++j) m[j] |= v[u][j] ^ ref[j];
+            lo = l[u] < lo ? l[u] : lo;
+            hi = l[u] > hi ? l[u] : hi;
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+#pragma unroll
+        for (int j = 0; j <= WT; ++j) m[j] |= __shfl_xor(m[j], o, 64);
+        const uint64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if (lane_id() == 0) {
+#pragma unroll
+        for (int j = 0; j <= WT; ++j) part[threadIdx.x >> 6][j] = m[j];
+        part[threadIdx.x >> 6][WT + 1] = lo;
+        part[threadIdx.x >> 6][WT + 2] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x <= WT) {  // one atomic per block and word
+        const int j = threadIdx.x;
+        const uint64_t b = part[0][j] | part[1][j] | part[2][j] | part[3][j];
+        if (b) atomicOr(&mask[j], (unsigned long long)b);
+    } else if (threadIdx.x == 64 && lsn) {  // (another wave: the min / max pair)
+        uint64_t a = part[0][WT + 1], b = part[0][WT + 2];
+#pragma unroll
+        for (int w = 1; w < 256 / 64; ++w) {
+            a = part[w][WT + 1] < a ? part[w][WT + 1] : a;
+            b = part[w][WT + 2] > b ? part[w][WT + 2] : b;
+        }
+        if (b) {
+            atomicMin(&mask[WT + 1], (unsigned long long)a);
+            atomicMax(&mask[WT + 2], (unsigned long long)b);
+        }
+    }
+}
+
 // Per-block digit counts, digit-major: counts[digit * nblocks + block].
 __global__ __launch_bounds__(kSortThreads) void k_rs_count(int W, int d, size_t n,
                                                            const uint32_t *gid,
@@ -364,8 +433,18 @@ hipError_t vary_mask_rows(int W, size_t n, const uint32_t *gid, const uint64_t *
     hipError_t e = hipMemsetAsync(dmask, 0, 8 * ((size_t)W + 3), s);
     if (e == hipSuccess) e = hipMemsetAsync(dmask + W + 1, 0xFF, 8, s);
     if (e != hipSuccess) return e;
-    const unsigned hgrid = (unsigned)std::min<size_t>((n + 2047) / 2048, 512);
-    k_vary_mask<<<hgrid, 256, 0, s>>>(W, n, gid, words, stride, lsn_span ? lsn : nullptr, dmask);
+    const uint64_t *ls = lsn_span ? lsn : nullptr;
+    const unsigned wgrid = (unsigned)std::min<size_t>((n + 1023) / 1024, 2048);
+    switch (W) {
+    case 1: k_vary_mask_w<1><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask); break;
+    case 2: k_vary_mask_w<2><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask); break;
+    case 3: k_vary_mask_w<3><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask); break;
+    case 4: k_vary_mask_w<4><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask); break;
+    default: {
+        const unsigned hgrid = (unsigned)std::min<size_t>((n + 2047) / 2048, 512);
+        k_vary_mask<<<hgrid, 256, 0, s>>>(W, n, gid, words, stride, ls, dmask);
+    }
+    }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     uint64_t hm[kMaxWords + 3];

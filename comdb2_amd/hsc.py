@@ -195,7 +195,7 @@ MULTI_ID_BYTES = 2 * 128  # hsc_multi_unique_ids: one RCCL id per lane
  LAYOUT_NARROW_CODES, LAYOUT_COMPACT, LAYOUT_COMPACT_WIDE) = 0, 1, 2, 3, 4, 5, 6, 7
 # hsc_set_paths flags (include/hip_serial.h)
 (PATH_NO_SMALL, PATH_NO_PACKED_SORT, PATH_TILE_DIR, PATH_CO_SERIAL, PATH_CO_RUN_THREAD,
- PATH_NO_COMP_NARROW) = 1, 2, 4, 8, 16, 32
+ PATH_NO_COMP_NARROW, PATH_NO_CT_POINTS) = 1, 2, 4, 8, 16, 32, 64
 
 _lib: Optional[C.CDLL] = None
 

@@ -317,14 +317,16 @@ int hsc_append_stats(hsc_ctx *ctx, uint64_t out[3]);
  * CO_RUN_THREAD: one thread per run in the coalesce merge scan;
  * NO_COMP_NARROW: composite keys whose varying bits total <= 62 but span
  * more keep the compact / wide layouts instead of the narrow index over
- * compressed codes (set before the build). */
+ * compressed codes (set before the build); NO_CT_POINTS: compact tiles build
+ * no point index, so point probes take join records (set before the build). */
 #define HSC_PATH_NO_SMALL 1u
 #define HSC_PATH_NO_PACKED_SORT 2u
 #define HSC_PATH_TILE_DIR 4u
 #define HSC_PATH_CO_SERIAL 8u
 #define HSC_PATH_CO_RUN_THREAD 16u
 #define HSC_PATH_NO_COMP_NARROW 32u
-#define HSC_PATH_ALL 63u
+#define HSC_PATH_NO_CT_POINTS 64u
+#define HSC_PATH_ALL 127u
 int hsc_set_paths(hsc_ctx *ctx, unsigned flags);
 /* How the last window build sorted its rows: 0 whole-row radix sort, 1 the
  * packed 64-bit key sort, 2 the compact-code merge sort (wide keys). */

@@ -13,7 +13,7 @@ import pytest
 from comdb2_amd import formats as F
 from comdb2_amd.formats import LogBuilder, Range, ReadSets
 from comdb2_amd.hsc import (LAYOUT_AUTO, LAYOUT_COMPACT, LAYOUT_COMPACT_WIDE, LAYOUT_NARROW,
-                            PATH_NO_COMP_NARROW, Validator)
+                            PATH_NO_COMP_NARROW, PATH_NO_CT_POINTS, Validator)
 
 pytestmark = pytest.mark.gpu
 # torch (device arrays for hsc_window_ingest_device) is imported before any
@@ -221,6 +221,44 @@ def test_one_word_keys_match_oracle(oracle_mod):
     np.testing.assert_array_equal(got, want)
     np.testing.assert_array_equal(ref, want)
     assert 0.02 < want.mean() < 0.98
+
+
+@pytest.mark.parametrize("case", ["short", "hot", "one_word", "config3"])
+def test_point_index_matches_join_records(oracle_mod, case):
+    """Point probes (lo == hi) answered by the compact tiles' point index in
+    the bound kernel (no join record) give the verdicts of the join-record
+    path (HSC_PATH_NO_CT_POINTS) and of the oracle, and the join gets fewer
+    records: random short keys, three hot keys taking half the ranges, one-word
+    keys (WG = 1) and config 3."""
+    paths = 0
+    if case == "short":
+        log, rs = _short_case(31, n_commits=3000, n_txn=900)
+    elif case == "hot":
+        log, rs = _short_case(32, n_commits=4000, n_txn=3000, hot=0.5)
+    elif case == "one_word":
+        log, rs = _short_case(33, n_commits=2500, n_txn=800, lens=(9, 17), var=2, ends=True)
+        paths = PATH_NO_COMP_NARROW
+    else:
+        from comdb2_amd.workloads import config3
+        log, rs = config3(n_writes=60000, n_txn=3000, seed=7)
+    want = oracle_mod.check(log, rs, nthreads=8)[0] != 0
+    v = Validator(0)
+    try:
+        recs = []
+        got = []
+        for p in (paths, paths | PATH_NO_CT_POINTS):
+            v.set_paths(p)
+            v.ingest_log(log)
+            assert v.layout == LAYOUT_COMPACT and 1 <= v.tile_key_words <= 3
+            v.enable_timing(True)
+            got.append(v.check_readsets(rs) != 0)
+            recs.append(v.timing()["records"])
+            v.enable_timing(False)
+    finally:
+        v.close()
+    np.testing.assert_array_equal(got[0], want)
+    np.testing.assert_array_equal(got[1], want)
+    assert recs[0] < recs[1], recs  # the points took no join records
 
 
 def test_config3_full_size_matches_sortjoin():
