@@ -1486,6 +1486,8 @@ def main():
     ap.add_argument("--loopback", action="store_true",
                     help="in-process multi context: the per-rank exchange with peer copies "
                          "(hsc_multi_set_transport) for the device-routed leg and the merge")
+    ap.add_argument("--hw-queues", type=int, default=0,
+                    help="multi legs: GPU_MAX_HW_QUEUES for this process (0: max(the box's, 8))")
     ap.add_argument("--rank-path", action="store_true",
                     help="run the per-rank (RCCL) multi-GPU path even at WORLD_SIZE 1 (its "
                          "world-1 rehearsal on one GPU)")
@@ -1511,7 +1513,8 @@ def main():
             q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
         except ValueError:
             q = 4
-        os.environ["GPU_MAX_HW_QUEUES"] = str(max(q, 8))
+        # (--hw-queues N: exactly N, e.g. the box's default 4 for an A/B)
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues if args.hw_queues > 0 else max(q, 8))
         return bench_multi(args)
     # one GPU (N > 1 runs bench_multi)
     world, rank = 1, 0

@@ -230,6 +230,10 @@ struct MapVec {
             void *q = mmap(nullptr, cv * sizeof(T), PROT_READ | PROT_WRITE,
                            MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
             if (q != MAP_FAILED && cv >= k) {
+                // 4 KiB pages: a transparent huge page is zeroed whole at its
+                // first write -- a 0.3 ms stall of the append that crosses
+                // into the next 2 MiB of the store (r06f, scripts/fold_diag.py)
+                (void)madvise(q, cv * sizeof(T), MADV_NOHUGEPAGE);
                 p = (T *)q, cap = cv;
                 return;
             }
@@ -240,6 +244,7 @@ struct MapVec {
         void *q = p ? mremap(p, cap * sizeof(T), c * sizeof(T), MREMAP_MAYMOVE)
                     : mmap(nullptr, c * sizeof(T), PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
         if (q == MAP_FAILED) throw std::bad_alloc();
+        (void)madvise(q, c * sizeof(T), MADV_NOHUGEPAGE);
         p = (T *)q, cap = c;
     }
     void push_back(const T &v)
