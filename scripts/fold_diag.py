@@ -29,6 +29,7 @@ def main():
     arrs = {nm: hsc.CurRangeArrays([t.reads], [0]) for nm, t in txns.items()}
     f, o = C.c_uint(), C.c_uint()
     check, append, ctx = v.lib.hip_bdb_osql_serial_check, v.lib.hsc_window_append_log, v.ctx
+    nul = v.lib.hsc_window_delta_rows
     log = []
     gc.collect()
     gc.disable()
@@ -58,6 +59,11 @@ def main():
             append(ctx, C.byref(st))
             c1 = time.monotonic_ns()
             log.append(("append", k, c0 / 1e3, (c1 - c0) / 1e3))
+        # host noise baseline: a native call that touches no GPU and no lock
+        c0 = time.monotonic_ns()
+        nul(ctx)
+        c1 = time.monotonic_ns()
+        log.append(("null", k, c0 / 1e3, (c1 - c0) / 1e3))
         k += 1
     gc.enable()
     print("fold stats", v.fold_stats(), file=sys.stderr)
@@ -67,6 +73,9 @@ def main():
         print(f"[call] {x[2]:.0f} {x[0]} #{x[1]} {x[3]:.0f} us", file=sys.stderr)
     ch = np.array([x[3] for x in log if x[0] == "check"][1000:])
     ap = np.array([x[3] for x in log if x[0] == "append"])
+    nu = np.array([x[3] for x in log if x[0] == "null"])
+    print(f"null native call: p50 {np.median(nu):.2f} p99.9 {np.percentile(nu, 99.9):.1f} max {nu.max():.0f} us, "
+          f"{int((nu > 100).sum())} calls over 100 us", file=sys.stderr)
     print(f"checks after 1000: p50 {np.median(ch):.1f} max {ch.max():.0f}; appends p50 {np.median(ap):.1f} "
           f"max {ap.max():.0f}", file=sys.stderr)
 
