@@ -32,6 +32,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 namespace hsc {
 
 namespace {
@@ -452,7 +454,7 @@ __device__ __forceinline__ void join_search(const ProbeWork &work, const CTiles 
 // column) is the last one <= j.  The column is loaded first, staged, each
 // thread finds its record's chunk by a 9-step LDS search and loads the whole
 // 64-byte record (no bucket entry, no gather) while the rows are in flight.
-template <int WG, bool kTile>
+template <int WG, bool kTile, int WL = WG>
 __device__ __forceinline__ void join_item_s(const ProbeWork &work, const CTiles &ct, uint8_t *flags,
                                             uint32_t xi, uint64_t *kw, uint32_t *rank,
                                             uint32_t *b16, uint32_t *b128, uint32_t *B,
@@ -472,9 +474,9 @@ __device__ __forceinline__ void join_item_s(const ProbeWork &work, const CTiles 
     uint32_t e = 0, cs = 0;
     if (tid < G) e = work.hist[col + tid], cs = work.cst[col + tid];
     const size_t row = ((size_t)tile << kCTLog2) + 2 * tid;
-    u64x2 kv[WG];
+    u64x2 kv[WL];
 #pragma unroll
-    for (int w = 0; w < WG; ++w) kv[w] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row);
+    for (int w = 0; w < WL; ++w) kv[w] = *(const u64x2 *)(ct.key + (size_t)w * ct.len + row);
     const u32x2 rr = *(const u32x2 *)(ct.rank + row);
     u32x2 bt = {0, 0};
     if (tid < kTBS / 2) bt = *(const u32x2 *)(ct.tb + (size_t)tile * kTBS + 2 * tid);
@@ -496,7 +498,7 @@ __device__ __forceinline__ void join_item_s(const ProbeWork &work, const CTiles 
         A0 = r[0], A1 = r[1], B0 = r[2], B1 = r[3];
     }
 #pragma unroll
-    for (int w = 0; w < WG; ++w) *(u64x2 *)(kw + (size_t)w * T + 2 * tid) = kv[w];
+    for (int w = 0; w < WL; ++w) *(u64x2 *)(kw + (size_t)w * T + 2 * tid) = kv[w];
     *(u32x2 *)(rank + 2 * tid) = rr;
     if (tid < kTBS / 2) *(u32x2 *)(B + 2 * tid) = bt;
     uint32_t m = max(rr.x, rr.y);
@@ -513,7 +515,9 @@ __device__ __forceinline__ void join_item_s(const ProbeWork &work, const CTiles 
     u64x2 pl[2] = {A0, u64x2{A1.x, rt}}, ph0 = B0;
     uint64_t ph1 = B1.x;
     if (kind == kCTail) ph0 = A0, ph1 = A1.x;  // a tail record carries hi in its first half
-    join_search<WG>(work, ct, flags, kw, rank, b16, b128, B, kind, pl, ph0, ph1);
+    // words past WL: read from the window on a tie (the tile's row 0 of word WL)
+    const uint64_t *kg = WL < WG ? ct.key + (size_t)WL * ct.len + ((size_t)tile << kCTLog2) : nullptr;
+    join_search<WG, WL>(work, ct, flags, kw, rank, b16, b128, B, kind, pl, ph0, ph1, kg);
 }
 
 // XCD-contiguous tiles (as the narrow join): measured neutral on config 3
@@ -527,15 +531,15 @@ __host__ __device__ inline uint32_t ct_tile_blocks(uint32_t ntiles)
     return kCJoinXcd ? 8 * ((ntiles + 7) / 8) : ntiles;
 }
 
-template <int WG>
+template <int WG, int WL = WG>
 __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_join_c(ProbeWork work, CTiles ct, uint8_t *flags)
 {
     constexpr uint32_t T = kCTRows;
     static_assert(T == 2 * kCJT, "a row pair per thread");
     static_assert(kJoinChunk == kCJT && kTileCap == kCJT, "a record per thread");
     extern __shared__ __attribute__((aligned(16))) uint64_t jl[];
-    uint64_t *kw = jl;                                   // [WG][T], sorted
-    uint32_t *rank = (uint32_t *)(jl + (size_t)WG * T);  // [T], sorted order
+    uint64_t *kw = jl;                                   // [WL][T], sorted
+    uint32_t *rank = (uint32_t *)(jl + (size_t)WL * T);  // [T], sorted order
     uint32_t *b16 = rank + T;                            // [T / 16]
     uint32_t *b128 = b16 + T / 16;                       // [T / 128]
     uint32_t *B = b128 + T / 128;                        // [kTBS] the tile's bucket table
@@ -548,13 +552,13 @@ __global__ __launch_bounds__(kCJT) __attribute__((amdgpu_waves_per_eu(8, 8))) vo
         // neighbouring tiles on one XCD (they share lines of the chunk areas)
         const uint32_t b = blockIdx.x - xb, tb = gridDim.x - xb;
         const uint32_t tile = kCJoinXcd ? xcd_chunk(b, tb / 8) : b;
-        if (tile < ct.ntiles) join_item_s<WG, true>(work, ct, flags, tile, kw, rank, b16, b128, B, Es, Cs);
+        if (tile < ct.ntiles) join_item_s<WG, true, WL>(work, ct, flags, tile, kw, rank, b16, b128, B, Es, Cs);
         return;
     }
     const uint32_t nextra = work.item_off[1];
     for (uint32_t xi = blockIdx.x; xi < nextra; xi += xb) {
         __syncthreads();  // the previous item's LDS reads are done
-        join_item_s<WG, false>(work, ct, flags, xi, kw, rank, b16, b128, B, Es, Cs);
+        join_item_s<WG, false, WL>(work, ct, flags, xi, kw, rank, b16, b128, B, Es, Cs);
     }
 }
 
@@ -608,13 +612,20 @@ hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_i
     if (max_items == 0 || ct.n == 0 || ct.ntiles == 0) return hipSuccess;
     const uint32_t extra = max_items - ct.ntiles;
     const uint32_t blocks = ct_tile_blocks(ct.ntiles) + (extra < 512 ? extra : 512);
-    const size_t lds = 8 * (size_t)ct.WG * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
+    // key words staged per tile (HSC_CJOIN_WL, A/B; default all): the rest
+    // are read from the window on a tie
+    static const int wl_env = getenv("HSC_CJOIN_WL") ? atoi(getenv("HSC_CJOIN_WL")) : 0;
+    const int WL = wl_env >= 1 && wl_env < ct.WG ? wl_env : ct.WG;
+    const size_t lds = 8 * (size_t)WL * kCTRows + 4 * (size_t)kCTRows + 4 * (kCTRows / 16) +
                        4 * (kCTRows / 128) + 4 * kTBS + 6 * (size_t)kMaxChunks;
-#define HSC_JOIN_C(WG_) k_join_c<WG_><<<blocks, kCJT, lds, s>>>(work, ct, flags)
-    switch (ct.WG) {
-    case 1: HSC_JOIN_C(1); break;
-    case 2: HSC_JOIN_C(2); break;
-    case 3: HSC_JOIN_C(3); break;
+#define HSC_JOIN_C(WG_, WL_) k_join_c<WG_, WL_><<<blocks, kCJT, lds, s>>>(work, ct, flags)
+    switch (ct.WG * 4 + WL) {
+    case 1 * 4 + 1: HSC_JOIN_C(1, 1); break;
+    case 2 * 4 + 1: HSC_JOIN_C(2, 1); break;
+    case 2 * 4 + 2: HSC_JOIN_C(2, 2); break;
+    case 3 * 4 + 1: HSC_JOIN_C(3, 1); break;
+    case 3 * 4 + 2: HSC_JOIN_C(3, 2); break;
+    case 3 * 4 + 3: HSC_JOIN_C(3, 3); break;
     default: return hipErrorInvalidValue;
     }
 #undef HSC_JOIN_C

@@ -42,17 +42,26 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 // ballots + one LDS scan).  (r06: one atomic per block on a single cursor
 // instead of the count pass serialised 24k blocks: 1.48 ms per 100M ops.)
 constexpr int kGwThreads = 256, kGwItems = 16;
+// thread t of a block takes ops base + 16 t .. base + 16 t + 15 (one 16-byte
+// load of is_write): the block's writers come out in op order, so writers of
+// txn-ordered ops stay txn-ordered (the writer sort then skips the txn bits)
 __device__ __forceinline__ uint32_t gw_bits(size_t nops, const uint8_t *is_write, size_t base, uint32_t &cnt)
 {
-    uint32_t w = 0;  // bit k: op k of this thread writes
-    cnt = 0;
+    const size_t i0 = base + (size_t)threadIdx.x * kGwItems;
+    uint32_t w = 0;  // bit k: op i0 + k writes
+    if (i0 + kGwItems <= nops && ((uintptr_t)(is_write + i0) & 15) == 0) {
+        const uint4 v = *(const uint4 *)(is_write + i0);
+        const uint32_t x[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int k = 0; k < kGwItems; ++k) {
-        const size_t i = base + (size_t)k * kGwThreads + threadIdx.x;
-        const bool wr = i < nops && is_write[i];
-        w |= (uint32_t)wr << k;
-        cnt += wr;
+        for (int k = 0; k < kGwItems; ++k) w |= (uint32_t)(((x[k >> 2] >> (8 * (k & 3))) & 0xFFu) != 0) << k;
+    } else {
+#pragma unroll
+        for (int k = 0; k < kGwItems; ++k) {
+            const size_t i = i0 + k;
+            w |= (uint32_t)(i < nops && is_write[i]) << k;
+        }
     }
+    cnt = (uint32_t)__popc(w);
     return w;
 }
 
@@ -102,12 +111,12 @@ __global__ __launch_bounds__(kGwThreads) void k_gw_place(size_t nops, const uint
         p += q < wv ? wsum[q] : 0;
         tot += wsum[q];
     }
+    const size_t i0 = base + (size_t)threadIdx.x * kGwItems;
 #pragma unroll
     for (int k = 0; k < kGwItems; ++k) {
         if (!((w >> k) & 1u)) continue;
-        const size_t i = base + (size_t)k * kGwThreads + threadIdx.x;
-        sk[p] = key[i];
-        st[p] = txn[i];
+        sk[p] = key[i0 + k];
+        st[p] = txn[i0 + k];
         ++p;
     }
     __syncthreads();
@@ -748,6 +757,11 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     if (nw) {
         CK(vary_mask_rows(2, nw, g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), wcap, g.count.p, vary, s));
         packed = packed_plan(2, nw, vary, &P, false);
+        // writers gathered in op order from txn-ordered ops are ordered by
+        // txn already: the stable passes need only the key bits (config 4:
+        // 3 passes instead of 6)
+        static const bool no_skip = getenv("HSC_GRAPH_NO_TXN_SKIP") != nullptr;  // (A/B)
+        if (packed && in.txn_sorted && !no_skip && P.nl > 0 && P.limb[P.nl - 1] == 1) P.skip = P.bits[P.nl - 1];
     }
     DBuf *dw = &g.ww2;
     if (packed) {
@@ -1026,15 +1040,20 @@ hipError_t graph_scc(uint32_t nn, GraphBufs &g, uint32_t *rounds, uint32_t *iter
     return hipSuccess;
 }
 
+// bit 0: an op names a txn >= ntxn; bit 1: ops not in nondecreasing txn order
 __global__ void k_check_ops(GraphInput in, uint32_t *bad)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= in.nops) return;
-    const uint32_t o = in.observed[i];
-    if (in.txn[i] >= in.ntxn || (o != kNone && o >= in.ntxn)) atomicOr(bad, 1u);
+    const uint32_t o = in.observed[i], t = in.txn[i];
+    uint32_t b = (t >= in.ntxn || (o != kNone && o >= in.ntxn)) ? 1u : 0u;
+    if (i + 1 < in.nops && in.txn[i + 1] < t) b |= 2u;
+    const uint64_t any = __ballot(b != 0);
+    if (any && b) atomicOr(bad, b);
 }
 
-// *bad_out := 1 if an op names a txn (or observed writer) >= ntxn
+// *bad_out: bit 0 if an op names a txn (or observed writer) >= ntxn, bit 1 if
+// the ops are not in nondecreasing txn order
 hipError_t graph_check_input(const GraphInput &in, GraphBufs &g, uint32_t *bad_out, hipStream_t s)
 {
     hipError_t e = g.count.ensure(64);
@@ -1254,9 +1273,17 @@ hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t 
         if (k <= kCutFastCap) {
             std::vector<uint64_t> h(k);
             if (k) {
-                if ((e = hipMemcpy(h.data(), g.cut.p, 8 * (size_t)k, hipMemcpyDeviceToHost)) != hipSuccess) return e;
+                // both copies on the caller's stream, then a sync: a NULL-stream
+                // hipMemcpy from pageable memory may return before its DMA
+                // lands, and the next reader of the rows (k_relabel, the
+                // multi step's copies) runs on a non-blocking stream
+                if ((e = hipMemcpyAsync(h.data(), g.cut.p, 8 * (size_t)k, hipMemcpyDeviceToHost, s)) != hipSuccess)
+                    return e;
+                if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
                 std::sort(h.begin(), h.end());
-                if ((e = hipMemcpy(g.cut.p, h.data(), 8 * (size_t)k, hipMemcpyHostToDevice)) != hipSuccess) return e;
+                if ((e = hipMemcpyAsync(g.cut.p, h.data(), 8 * (size_t)k, hipMemcpyHostToDevice, s)) != hipSuccess)
+                    return e;
+                if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
             }
             *m = k;
             return hipGetLastError();

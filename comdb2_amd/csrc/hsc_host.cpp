@@ -540,6 +540,7 @@ static int narrow_trad_pick(hsc_ctx *c)
 {
     const uint32_t m = c->trad_m;
     std::vector<uint32_t> a(m + 2), b(m + 2);
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // (the tables come from c->stream, a non-blocking stream)
     HIPCHK(c, hipMemcpy(a.data(), c->d_trad.p, 4 * a.size(), hipMemcpyDeviceToHost));
     HIPCHK(c, hipMemcpy(b.data(), c->d_trad2.p, 4 * b.size(), hipMemcpyDeviceToHost));
     auto fullest = [m](const std::vector<uint32_t> &t) {
@@ -1593,7 +1594,10 @@ static int fold_finish(hsc_ctx *c, bool wait)
     for (int t = 0; t < nt && t < (int)s->h_table_max.size(); ++t)
         c->h_table_max[t] = std::max(c->h_table_max[t], s->h_table_max[t]);
     HIPCHK(c, c->d_table_max.ensure(8 * (size_t)std::max(nt, 1)));
-    if (nt) HIPCHK(c, hipMemcpy(c->d_table_max.p, c->h_table_max.data(), 8 * (size_t)nt, hipMemcpyHostToDevice));
+    // (on c->stream: the probes that read the maxima are queued there)
+    if (nt)
+        HIPCHK(c, hipMemcpyAsync(c->d_table_max.p, c->h_table_max.data(), 8 * (size_t)nt, hipMemcpyHostToDevice,
+                                 c->stream));
     c->nt_dev = (uint32_t)nt;
     c->app_tmax = false;
     c->fn = 0;
@@ -4612,7 +4616,8 @@ int hsc_dep_graph_build_device(hsc_ctx *c, size_t nops, uint32_t ntxn, const uin
     in.skip_rw = (flags & HSC_GRAPH_NO_RW) != 0;
     uint32_t bad = 0;
     HIPCHK(c, graph_check_input(in, c->graph, &bad, c->stream));
-    if (bad) return fail(c, HSC_EINVAL, "history op out of range");
+    if (bad & 1) return fail(c, HSC_EINVAL, "history op out of range");
+    in.txn_sorted = !(bad & 2);
     float build_ms = 0;
     int rc = graph_build_timed(c, in, (flags & HSC_GRAPH_FULL) != 0, &build_ms);
     if (rc || !st) return rc;
@@ -4779,6 +4784,7 @@ int hsc_dep_graph_edges(hsc_ctx *c, uint32_t *src, uint32_t *dst, uint32_t *type
     GraphBufs &gb = c->graph;
     *n = gb.ne;
     const size_t m = std::min(cap, gb.ne);
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     if (m && src) HIPCHK(c, hipMemcpy(src, gb.src.p, 4 * m, hipMemcpyDeviceToHost));
     if (m && dst) HIPCHK(c, hipMemcpy(dst, gb.out_dst.p, 4 * m, hipMemcpyDeviceToHost));
     if (m && type) HIPCHK(c, hipMemcpy(type, gb.type.p, 4 * m, hipMemcpyDeviceToHost));

@@ -86,7 +86,7 @@ __global__ __launch_bounds__(kPkThreads) void k_pk_pack(PackPlan P, size_t n, co
         const size_t i = base + (size_t)k * kPkThreads + threadIdx.x;
         if (i < n) {
             keys[i] = key[k];
-            atomicAdd(&h[(uint32_t)(key[k] >> P.I) & 0xFFu], 1u);
+            atomicAdd(&h[(uint32_t)(key[k] >> (P.I + P.skip)) & 0xFFu], 1u);
         }
     }
     __syncthreads();
@@ -309,14 +309,23 @@ __global__ __launch_bounds__(kUdThreads) void k_pk_unpack_dd(
     __syncthreads();
     const uint32_t b0 = boff[blockIdx.x];
     const uint64_t imask = P.I >= 64 ? ~0ull : (1ull << P.I) - 1;
-#pragma unroll 2
+    // every row's LSN gather issued before the first store (10M random 8-byte
+    // reads for config 2: two in flight per thread left the unpack
+    // latency-bound)
+    uint64_t lvs[kUdRows];
+#pragma unroll
+    for (int r = 0; r < kUdRows; ++r) {
+        const uint32_t j = r * kUdThreads + threadIdx.x;
+        lvs[r] = lsn_in && j < nrows ? lsn_in[K[j] & imask] : 0;
+    }
+#pragma unroll  // (whole: lvs stays in registers)
     for (int r = 0; r < kUdRows; ++r) {
         const uint32_t j = r * kUdThreads + threadIdx.x;
         if (j >= nrows) break;
         const size_t i = base + j;
         const uint64_t key = K[j];
         uint64_t kb = key >> P.I;
-        const uint64_t lv = lsn_in ? lsn_in[key & imask] : 0;
+        const uint64_t lv = lvs[r];
         uint64_t limb[kPackMaxWords + 1];
 #pragma unroll
         for (int q = 0; q <= kPackMaxWords; ++q) {
@@ -409,9 +418,11 @@ static hipError_t packed_passes(const PackPlan &P, size_t n, const uint32_t *gid
     uint32_t *scan_tmp = counts + (size_t)256 * nblocks;
     k_pk_pack<<<nblocks, kPkThreads, 0, s>>>(P, n, gid, words, stride, k0, counts, nblocks);
     hipError_t e = hipGetLastError();
-    const int passes = (P.B + 7) / 8;
+    // (P.skip: the low bits the input is already ordered by need no pass --
+    // the passes are stable)
+    const int passes = (P.B - P.skip + 7) / 8;
     for (int p = 0; p < passes && e == hipSuccess; ++p) {
-        const int sh = P.I + 8 * p;
+        const int sh = P.I + P.skip + 8 * p;
         if (p > 0) k_pk_count<<<nblocks, kPkThreads, 0, s>>>(sh, n, k0, counts, nblocks);
         e = scan_exclusive_u32(counts, (size_t)256 * nblocks, scan_tmp, s);
         if (e != hipSuccess) break;

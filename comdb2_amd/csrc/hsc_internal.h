@@ -158,6 +158,8 @@ struct PackPlan {
     int bits[kPackLimbs];
     uint64_t mask[kPackLimbs];  // the limb's varying bits
     uint64_t mv[kPackLimbs][6]; // their compress moves
+    int skip = 0;               // low packed bits the rows are already ordered by (stable
+                                // passes skip them: a txn-ordered writer list sorted by key)
 };
 // false: does not fit.  index = false: no row index (I = 0) -- the packed
 // key is the whole row (no LSN to gather; equal rows are duplicates)
@@ -455,6 +457,7 @@ struct GraphInput {              // device pointers
     const uint64_t *x_rows = nullptr, *x_type = nullptr;
     size_t n_extra = 0;
     bool skip_rw = false;  // reads give wr edges only (rw come from x_rows)
+    bool txn_sorted = false;  // ops in nondecreasing txn order (graph_check_input's bit 2)
 };
 struct GraphBufs {
     DBuf flags, flags2, scratch, count;

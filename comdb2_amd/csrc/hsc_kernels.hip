@@ -120,15 +120,14 @@ __global__ __launch_bounds__(256) void k_vary_mask(int W, size_t n, const uint32
 
 // The same masks and LSN span in ONE pass for keys of WT <= 4 words: every
 // row's words, gid and LSN are loaded together (U rows per thread, all loads
-// in flight before the first OR), 8 workgroups per CU.  k_vary_mask above
-// walks the rows once per word with 2 workgroups per CU: 100 us for config
-// 2's 280 MB (2.8 TB/s).
+// in flight before the first OR).  k_vary_mask above walks the rows once per
+// word: 100 us for config 2's 280 MB (2.8 TB/s).
 template <int WT>
 __global__ __launch_bounds__(256) void k_vary_mask_w(size_t n, const uint32_t *gid, const uint64_t *words,
                                                      size_t stride, const uint64_t *lsn,
                                                      unsigned long long *mask)
 {
-    constexpr int U = 4;
+    constexpr int U = 8;
     __shared__ uint64_t part[256 / 64][WT + 3];
     uint64_t ref[WT + 1], m[WT + 1];
 #pragma unroll
@@ -434,7 +433,11 @@ hipError_t vary_mask_rows(int W, size_t n, const uint32_t *gid, const uint64_t *
     if (e == hipSuccess) e = hipMemsetAsync(dmask + W + 1, 0xFF, 8, s);
     if (e != hipSuccess) return e;
     const uint64_t *ls = lsn_span ? lsn : nullptr;
-    const unsigned wgrid = (unsigned)std::min<size_t>((n + 1023) / 1024, 2048);
+    // 512 workgroups of 8 rows x (W + 2) loads in flight per thread: all
+    // workgroups OR into the same W + 3 words, one atomic each per word (2048
+    // workgroups of 4 rows measured 109 us on config 2, the per-word kernel
+    // 100 us)
+    const unsigned wgrid = (unsigned)std::min<size_t>((n + 2047) / 2048, 512);
     switch (W) {
     case 1: k_vary_mask_w<1><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask); break;
     case 2: k_vary_mask_w<2><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask); break;

@@ -292,6 +292,9 @@ static int upload_splitters(hsc_ctx *f, Multi *M, int W)
             MCHK(f, hipMemcpy(M->d_sp[m].p, M->sp_gid.data(), 4 * S, hipMemcpyHostToDevice));
             MCHK(f, hipMemcpy(M->d_sp[m].as<uint8_t>() + M->d_sp_woff, w.data(), 8 * w.size(),
                               hipMemcpyHostToDevice));
+            // (a NULL-stream copy from pageable memory may return before it
+            // lands; the route kernels run on non-blocking lane streams)
+            MCHK(f, hipDeviceSynchronize());
         }
     }
     M->d_sp_W = W;
@@ -1656,10 +1659,10 @@ int hsc_multi_adopt(hsc_ctx *f)
         MRC(lane_stream(f, M, 0, 0));
         MLane &ml = M->lane[0][0];
         MCHK(f, ml.gather.ensure(8 * tm.size()));
-        MCHK(f, hipMemcpy(ml.gather.p, tm.data(), 8 * tm.size(), hipMemcpyHostToDevice));
+        MCHK(f, hipMemcpyAsync(ml.gather.p, tm.data(), 8 * tm.size(), hipMemcpyHostToDevice, ml.stream));
         NCHK(f, rccl().AllReduce(ml.gather.p, ml.gather.p, tm.size(), ncclUint64, ncclMax, M->comm[0], ml.stream));
+        MCHK(f, hipMemcpyAsync(tm.data(), ml.gather.p, 8 * tm.size(), hipMemcpyDeviceToHost, ml.stream));
         MCHK(f, hipStreamSynchronize(ml.stream));
-        MCHK(f, hipMemcpy(tm.data(), ml.gather.p, 8 * tm.size(), hipMemcpyDeviceToHost));
     }
     f->h_table_max = tm;
     for (uint64_t v : tm) f->max_commit = std::max(f->max_commit, v);
@@ -1928,7 +1931,9 @@ int hsc_multi_graph_scc(hsc_ctx *f, const hsc_ops_dev *ops, uint32_t ntxn, uint3
         build_ms = std::max(build_ms, bs.build_ms);
         MCHK(f, hipSetDevice(c->device));
         MCHK(f, M->g_cover[m].ensure(cb));
-        MCHK(f, hipMemset(M->g_cover[m].p, 0, cb));
+        // on the member's stream, ahead of its cover kernels (a NULL-stream
+        // memset is not ordered with the members' non-blocking streams)
+        MCHK(f, hipMemsetAsync(M->g_cover[m].p, 0, cb, c->stream));
         rc = hsc_dep_graph_cover(c, M->g_cover[m].as<uint8_t>());
         if (rc) return mfail(f, rc, ("graph cover: " + c->err).c_str());
     }
@@ -1948,9 +1953,10 @@ int hsc_multi_graph_scc(hsc_ctx *f, const hsc_ops_dev *ops, uint32_t ntxn, uint3
         for (int d = 0; d < NL; ++d) parts.p[d] = M->g_cover[d].as<uint64_t>();
         MCHK(f, hipSetDevice(M->mem[0]->device));
         MCHK(f, launch_or_slices(parts, cb / 8, M->g_cover[0].as<uint64_t>(), l0.stream));
-        MCHK(f, hipStreamSynchronize(l0.stream));
         for (int d = 1; d < NL; ++d)
-            MCHK(f, hipMemcpyPeer(M->g_cover[d].p, M->mem[d]->device, M->g_cover[0].p, M->mem[0]->device, cb));
+            MCHK(f, hipMemcpyPeerAsync(M->g_cover[d].p, M->mem[d]->device, M->g_cover[0].p, M->mem[0]->device, cb,
+                                       l0.stream));
+        MCHK(f, hipStreamSynchronize(l0.stream));
     }
     const auto t2 = SteadyClock::now();
     // 3. every member's edges between covered txns
@@ -1969,17 +1975,18 @@ int hsc_multi_graph_scc(hsc_ctx *f, const hsc_ops_dev *ops, uint32_t ntxn, uint3
         MCHK(f, hipSetDevice(M->mem[0]->device));
         MCHK(f, M->g_sz[0].ensure(8 * (size_t)(N + 1)));
         uint64_t mine = k[0];
-        MCHK(f, hipMemcpy(M->g_sz[0].p, &mine, 8, hipMemcpyHostToDevice));
+        MCHK(f, hipMemcpyAsync(M->g_sz[0].p, &mine, 8, hipMemcpyHostToDevice, l0.stream));
         NCHK(f, R.AllGather(M->g_sz[0].p, M->g_sz[0].as<uint64_t>() + 1, 1, ncclUint64, M->comm[0], l0.stream));
-        MCHK(f, hipStreamSynchronize(l0.stream));
         std::vector<uint64_t> sz(N);
-        MCHK(f, hipMemcpy(sz.data(), M->g_sz[0].as<uint64_t>() + 1, 8 * (size_t)N, hipMemcpyDeviceToHost));
+        MCHK(f, hipMemcpyAsync(sz.data(), M->g_sz[0].as<uint64_t>() + 1, 8 * (size_t)N, hipMemcpyDeviceToHost,
+                               l0.stream));
+        MCHK(f, hipStreamSynchronize(l0.stream));
         size_t mx = 1;
         cut_rows = 0;
         for (int r = 0; r < N; ++r) mx = std::max<size_t>(mx, sz[r]), cut_rows += sz[r];
         MCHK(f, M->g_rows[0].ensure(8 * mx));
-        if (k[0]) MCHK(f, hipMemcpy(M->g_rows[0].p, cut[0], 8 * k[0], hipMemcpyDeviceToDevice));
-        if (mx > k[0]) MCHK(f, hipMemset(M->g_rows[0].as<uint64_t>() + k[0], 0xFF, 8 * (mx - k[0])));
+        if (k[0]) MCHK(f, hipMemcpyAsync(M->g_rows[0].p, cut[0], 8 * k[0], hipMemcpyDeviceToDevice, l0.stream));
+        if (mx > k[0]) MCHK(f, hipMemsetAsync(M->g_rows[0].as<uint64_t>() + k[0], 0xFF, 8 * (mx - k[0]), l0.stream));
         MCHK(f, M->g_all[0].ensure(8 * mx * (size_t)N));
         NCHK(f, R.AllGather(M->g_rows[0].p, M->g_all[0].p, mx, ncclUint64, M->comm[0], l0.stream));
         MCHK(f, hipStreamSynchronize(l0.stream));
@@ -1994,10 +2001,11 @@ int hsc_multi_graph_scc(hsc_ctx *f, const hsc_ops_dev *ops, uint32_t ntxn, uint3
         size_t o = 0;
         for (int d = 0; d < NL; ++d) {
             if (k[d])
-                MCHK(f, hipMemcpyPeer(M->g_all[0].as<uint64_t>() + o, M->mem[0]->device, cut[d],
-                                      M->mem[d]->device, 8 * k[d]));
+                MCHK(f, hipMemcpyPeerAsync(M->g_all[0].as<uint64_t>() + o, M->mem[0]->device, cut[d],
+                                           M->mem[d]->device, 8 * k[d], l0.stream));
             o += k[d];
         }
+        MCHK(f, hipStreamSynchronize(l0.stream));  // (the SCC runs on member 0's own stream)
         rows = M->g_all[0].as<uint64_t>();
     }
     const auto t3 = SteadyClock::now();
@@ -2007,7 +2015,9 @@ int hsc_multi_graph_scc(hsc_ctx *f, const hsc_ops_dev *ops, uint32_t ntxn, uint3
     if (rc) return mfail(f, rc, ("graph scc: " + M->mem[0]->err).c_str());
     for (int d = 1; d < NL; ++d)  // in process: the same components on every member that asked
         if (scc_dev[d])
-            MCHK(f, hipMemcpyPeer(scc_dev[d], M->mem[d]->device, scc_dev[0], M->mem[0]->device, 4 * (size_t)ntxn));
+            MCHK(f, hipMemcpyPeerAsync(scc_dev[d], M->mem[d]->device, scc_dev[0], M->mem[0]->device,
+                                       4 * (size_t)ntxn, l0.stream));
+    if (NL > 1) MCHK(f, hipStreamSynchronize(l0.stream));
     const auto t4 = SteadyClock::now();
     if (st) {
         *st = ss;
