@@ -13,6 +13,7 @@
 //   sp_g[t], sp_w[j * ntiles + t]  group / key words of tile t's first row
 //   table_max[tid]      max commit LSN of any write to table tid (dta too)
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -25,6 +26,17 @@
 namespace hsc {
 
 // Growable device buffer (reallocated only when a larger size is needed).
+// growth headroom of a device buffer: want / dbuf_slack() more (default 2;
+// HSC_DBUF_SLACK=8 the r05 eighth, an A/B)
+inline size_t dbuf_slack()
+{
+    static const size_t k = [] {
+        const char *v = getenv("HSC_DBUF_SLACK");
+        const long x = v ? atol(v) : 2;
+        return (size_t)(x >= 1 ? x : 2);
+    }();
+    return k;
+}
 struct DBuf {
     void *p = nullptr;
     size_t bytes = 0;
@@ -37,7 +49,7 @@ struct DBuf {
         // half again as much: a window that keeps growing (folds of a commit
         // stream) reallocates O(log n) times -- a hipFree synchronises the
         // device, which a fold's worker thread must not do on every fold
-        size_t b = want + want / 2 + 256;
+        size_t b = want + want / dbuf_slack() + 256;
         hipError_t e = hipMalloc(&p, b);
         if (e == hipSuccess) bytes = b;
         return e;
