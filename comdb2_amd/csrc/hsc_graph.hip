@@ -330,6 +330,142 @@ __global__ void k_edges_reads_pk(size_t nops, const uint32_t *txn, const uint64_
     }
 }
 
+// ---- bucket lines: the directory's buckets inline ----
+// k_edges_reads_pk reads a directory line, then one or two lines of pk: ~2.5
+// random lines and ~4 dependent loads per read (config 4: 3.5 ms, 22 GB).
+// Here bucket b is one 64-byte line: a header lo << 32 | has_next << 31 | n
+// (lo = the bucket's first writer in pk, n its writers), the first writer
+// after the bucket (the answer when every writer of the bucket is <= the
+// read's x), then its first kPtE writers as 32-bit offsets from the bucket's
+// start base + (b << shift) -- writers of one bucket differ only in their low
+// shift bits.  Config 4's 4M buckets are 256 MB: the Infinity Cache's size.
+// A read is one line; a bucket of more than kPtE writers (~5 % at 8 per
+// bucket) searches pk as before.  (A first form with 14 full 8-byte entries
+// per 128-byte line, 512 MB: the search 3.5 -> 2.85 ms, but stored a u64 per
+// thread 128 bytes apart -- 5 GB of partial-line writes, 1.05 ms.)
+constexpr int kPtE = 12;
+__device__ __forceinline__ uint64_t bucket_start(const PairPack &pp, uint64_t b)
+{
+    return pp.base + (pp.shift >= 64 ? 0 : b << pp.shift);
+}
+
+// 8 threads per bucket, one 8-byte word each: coalesced lines
+__global__ void k_pair_table(uint32_t nu, const uint64_t *pk, const uint32_t *dir, uint64_t nb, PairPack pp,
+                             uint64_t *tab)
+{
+    const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t b = id >> 3;
+    const int w = (int)(id & 7);
+    if (b >= nb) return;
+    const uint32_t lo = dir[b], hi = dir[b + 1], n = hi - lo;
+    uint64_t v;
+    if (w == 0) {
+        v = ((uint64_t)lo << 32) | ((uint64_t)(hi < nu) << 31) | (uint64_t)min(n, 0x7FFFFFFFu);
+    } else if (w == 1) {
+        v = hi < nu ? pk[hi] : ~0ull;
+    } else {
+        const uint64_t s0 = bucket_start(pp, b);
+        const uint32_t j0 = 2 * (uint32_t)(w - 2), j1 = j0 + 1;
+        const uint32_t e0 = j0 < n ? (uint32_t)(pk[lo + j0] - s0) : 0xFFFFFFFFu;
+        const uint32_t e1 = j1 < n ? (uint32_t)(pk[lo + j1] - s0) : 0xFFFFFFFFu;
+        v = (uint64_t)e0 | ((uint64_t)e1 << 32);
+    }
+    tab[8 * b + w] = v;
+}
+
+__global__ void k_edges_reads_pt(size_t nops, const uint32_t *txn, const uint64_t *key,
+                                 const uint8_t *is_write, const uint32_t *observed, uint32_t nu,
+                                 const uint64_t *wkey, const uint64_t *wtxn, const uint64_t *pk,
+                                 const uint64_t *tab, PairPack pp, uint64_t *ew, uint64_t *et,
+                                 uint32_t *eg, int skip_rw, uint32_t *diff)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nops) return;
+    uint64_t wr = ~0ull, rw = ~0ull;
+    if (!is_write[i]) {
+        const uint32_t r = txn[i], ob = observed[i];
+        const uint64_t k = key[i];
+        if (ob != kNone && ob != r) wr = ((uint64_t)ob << 32) | r;
+        if (!skip_rw && (k & ~pp.km) == pp.kc) {
+            uint64_t km[6], tm[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) km[q] = pp.kmv[q], tm[q] = pp.tmv[q];
+            if (ob == kNone || (ob & ~pp.tm) == pp.tc) {
+                const uint64_t kp = bits_compress(k, pp.km, km);
+                const uint64_t x = pair_key(pp, kp) | (ob == kNone ? 0 : bits_compress(ob, pp.tm, tm));
+                const bool strict = ob != kNone;
+                const uint64_t b = pair_bucket(pp, x);
+                const u64x2 *line = (const u64x2 *)(tab + 8 * b);
+                u64x2 e[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) e[q] = line[q];
+                const uint64_t hd = e[0].x;
+                const uint32_t n = (uint32_t)(hd & 0x7FFFFFFFu), lo = (uint32_t)(hd >> 32);
+                bool have = false;
+                uint64_t v = 0;
+                if (n <= (uint32_t)kPtE) {
+                    // the first entry > x (>= x for the initial version), in
+                    // offsets from the bucket's start (x below it: every entry)
+                    const uint64_t s0 = bucket_start(pp, b);
+                    const int64_t xr = x < s0 ? -1 : (int64_t)(x - s0);
+                    uint32_t ent[kPtE];
+#pragma unroll
+                    for (int q = 0; q < kPtE / 2; ++q) {
+                        const uint64_t pw = (q & 1) ? e[1 + q / 2].y : e[1 + q / 2].x;  // word 2 + q
+                        ent[2 * q] = (uint32_t)pw, ent[2 * q + 1] = (uint32_t)(pw >> 32);
+                    }
+#pragma unroll
+                    for (int j = kPtE - 1; j >= 0; --j) {
+                        const int64_t ej = ent[j];
+                        if ((uint32_t)j < n && (strict ? ej > xr : ej >= xr)) v = s0 + (uint64_t)ent[j], have = true;
+                    }
+                    if (!have && ((hd >> 31) & 1)) v = e[0].y, have = true;  // the next bucket's first
+                } else {  // an overflowing bucket: its writers in pk
+                    uint32_t a = lo, h = lo + n;
+                    while (a < h) {
+                        const uint32_t mid = (a + h) >> 1;
+                        const uint64_t pv = pk[mid];
+                        if (strict ? pv <= x : pv < x)
+                            a = mid + 1;
+                        else
+                            h = mid;
+                    }
+                    if (a < nu) v = pk[a], have = true;
+                }
+                if (have) {
+                    const uint64_t tmask = pp.tb >= 64 ? ~0ull : (1ull << pp.tb) - 1;
+                    if ((pp.tb >= 64 ? 0 : v >> pp.tb) == kp) {
+                        const uint32_t wt = (uint32_t)(bits_expand(v & tmask, pp.tm, tm) | pp.tc);
+                        if (wt != r) rw = ((uint64_t)r << 32) | wt;
+                    }
+                }
+            } else {  // an observed txn outside the writers' bits: the row search
+                uint32_t lo = 0, hi = nu;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    const uint64_t mk = wkey[mid], mt = wtxn[mid];
+                    if (mk < k || (mk == k && mt <= ob))
+                        lo = mid + 1;
+                    else
+                        hi = mid;
+                }
+                if (lo < nu && wkey[lo] == k && wtxn[lo] != r) rw = ((uint64_t)r << 32) | wtxn[lo];
+            }
+        }
+    }
+    const size_t s = (size_t)nu + 2 * i;
+    ew[s] = wr;
+    ew[s + 1] = rw;
+    back_row(diff, wr);
+    back_row(diff, rw);
+    if (et) {
+        et[s] = kDepWR;
+        eg[s] = 0;
+        et[s + 1] = kDepRW;
+        eg[s + 1] = 0;
+    }
+}
+
 // ---- partitioned read search (the packed writers) ----
 // k_edges_reads_pk answers each read with a directory line and a search of
 // pk: two dependent random lines per read over a 33M-writer array (config 4:
@@ -842,6 +978,8 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         // directory search -- the count's per-read global atomics on 16k
         // partition counters), so off unless HSC_GRAPH_RP=1 (A/B)
         static const bool rp = getenv("HSC_GRAPH_RP") != nullptr && atoi(getenv("HSC_GRAPH_RP")) != 0;
+        // bucket lines (HSC_GRAPH_PT=0: the directory + pk search, an A/B)
+        static const bool pt = getenv("HSC_GRAPH_PT") == nullptr || atoi(getenv("HSC_GRAPH_PT")) != 0;
         // raw builds (the sharded SCC's): the cover's backward-edge diffs as
         // the rows are emitted (ww rows are forward: txns ascend inside a key)
         uint32_t *diff = nullptr;
@@ -876,6 +1014,15 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
             CK(hipStreamSynchronize(s));
             rw_rows = (size_t)tot[0] + tot[1];
             slot_layout = true;
+        } else if (pt && pp.shift <= 31) {  // (a bucket's offsets fit 32 bits)
+            const uint64_t nb = ((uint64_t)1 << pp.D) + 1;
+            CK(g.ptab.ensure(64 * nb));
+            k_pair_table<<<blocks(8 * nb), 256, 0, s>>>(nu, g.pk.as<uint64_t>(), g.pdir.as<uint32_t>(), nb, pp,
+                                                        g.ptab.as<uint64_t>());
+            k_edges_reads_pt<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu,
+                                                          wkey, wtxn, g.pk.as<uint64_t>(), g.ptab.as<uint64_t>(),
+                                                          pp, g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0,
+                                                          diff);
         } else {
             k_edges_reads_pk<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu,
                                                           wkey, wtxn, g.pk.as<uint64_t>(), g.pdir.as<uint32_t>(),

@@ -481,6 +481,7 @@ struct GraphBufs {
     DBuf diff, cut, cut_id, txn_of;            // sharded SCC: cover, cut rows, cut ids
     DBuf x_rows, x_type, x_map;                // staged extra edges (rw pairs)
     DBuf pk, pdir;                             // packed distinct writers + their directory
+    DBuf ptab;                                 // the directory's buckets inline, one line each
     DBuf rp_cnt, rp_items;                     // partitioned read search: counts / cursors, items
     size_t n_extra = 0;
     size_t ne = 0;
@@ -496,7 +497,7 @@ struct GraphBufs {
                        &ew, &et, &eg, &ew2, &et2, &eg2, &swap_rows, &src, &out_dst, &type,
                        &in_src, &in_dst, &out_off, &in_off, &scc, &active, &color, &mark,
                        &front, &front2, &h_txn, &h_key, &h_isw, &h_obs, &diff, &cut,
-                       &cut_id, &txn_of, &x_rows, &x_type, &x_map, &pk, &pdir, &rp_cnt,
+                       &cut_id, &txn_of, &x_rows, &x_type, &x_map, &pk, &pdir, &ptab, &rp_cnt,
                        &rp_items, &cover_bits};
         for (DBuf *b : all) b->release();
     }
