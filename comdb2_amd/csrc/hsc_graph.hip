@@ -125,8 +125,8 @@ __global__ __launch_bounds__(kGwThreads) void k_gw_place(size_t nops, const uint
         words[b0 + j] = sk[j];
         words[stride + b0 + j] = st[j];
         gid[b0 + j] = 0;
-        lsn[b0 + j] = 0;
     }
+    (void)lsn;  // (zeroed by the whole-row sort's caller only: the packed sort reads none)
 }
 
 
@@ -900,14 +900,15 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         if (packed && in.txn_sorted && !no_skip && P.nl > 0 && P.limb[P.nl - 1] == 1) P.skip = P.bits[P.nl - 1];
     }
     DBuf *dw = &g.ww2;
+    uint64_t *lsn_d = nullptr;  // packed: the distinct packed keys themselves (no LSN input, I = 0)
     if (packed) {
-        uint64_t *lsn_d = nullptr;
         CK(packed_sort_dedupe(P, nw, g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), nullptr, wcap,
                               g.wl.as<uint64_t>(), g.wl2.as<uint64_t>(), nullptr, nullptr, nullptr, 0,
                               g.wg2.as<uint32_t>(), g.ww2.as<uint64_t>(), wcap, &lsn_d,
                               g.count.as<uint32_t>(), g.scratch.p, g.scratch.bytes, s));
     } else {
         bool alt = false;
+        if (nw) CK(hipMemsetAsync(g.wl.p, 0, 8 * (size_t)nw, s));  // (k_gw_place writes no LSNs)
         CK(radix_sort_rows(2, nw, g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), g.wl.as<uint64_t>(), wcap,
                            g.wg2.as<uint32_t>(), g.ww2.as<uint64_t>(), g.wl2.as<uint64_t>(),
                            g.scratch.p, g.scratch.bytes, &alt, nullptr, s));
@@ -963,15 +964,21 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         (void)env_read;
         pp.D = 1;
         while (pp.D < kDMax && ((size_t)kPer << pp.D) < nu) ++pp.D;
-        CK(g.pk.ensure(8 * (size_t)nu));
         CK(g.pdir.ensure(4 * (((size_t)1 << pp.D) + 2)));
-        k_pair_keys<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, pp, g.pk.as<uint64_t>());
-        CK(hipMemcpyAsync(&pp.base, g.pk.as<uint64_t>(), 8, hipMemcpyDeviceToHost, s));
-        CK(hipMemcpyAsync(&pp.last, g.pk.as<uint64_t>() + nu - 1, 8, hipMemcpyDeviceToHost, s));
+        // the sort's unpack left the distinct packed keys -- compress(key) <<
+        // tb | compress(txn), the same words (no gid limb: gid is 0) -- in lsn_d
+        const uint64_t *pkv = lsn_d;
+        if (!pkv) {
+            CK(g.pk.ensure(8 * (size_t)nu));
+            k_pair_keys<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, pp, g.pk.as<uint64_t>());
+            pkv = g.pk.as<uint64_t>();
+        }
+        CK(hipMemcpyAsync(&pp.base, pkv, 8, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpyAsync(&pp.last, pkv + nu - 1, 8, hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));
         pp.shift = 0;  // (last - base) >> shift < 2^D
         while (pp.shift < 64 && ((pp.last - pp.base) >> pp.shift) >= ((uint64_t)1 << pp.D)) ++pp.shift;
-        k_pair_dir<<<blocks(((size_t)1 << pp.D) + 2), 256, 0, s>>>(nu, g.pk.as<uint64_t>(), pp,
+        k_pair_dir<<<blocks(((size_t)1 << pp.D) + 2), 256, 0, s>>>(nu, pkv, pp,
                                                                  g.pdir.as<uint32_t>());
         // the partitioned read search: measured slower on config 4 (r06c trace:
         // count 3.0 + scatter 3.2 + join 1.0 ms against 3.5 ms for the
@@ -992,7 +999,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         if (rp) {
             RpArgs a{};
             a.nops = nops, a.txn = in.txn, a.key = in.key, a.is_write = in.is_write, a.observed = in.observed;
-            a.nu = nu, a.wkey = wkey, a.wtxn = wtxn, a.pk = g.pk.as<uint64_t>(), a.dir = g.pdir.as<uint32_t>();
+            a.nu = nu, a.wkey = wkey, a.wtxn = wtxn, a.pk = pkv, a.dir = g.pdir.as<uint32_t>();
             a.ps = pp.D > kRpBitsMax ? (uint32_t)(pp.D - kRpBitsMax) : 0;
             a.np = (uint32_t)((((uint64_t)1 << pp.D) >> a.ps) + 1);
             CK(g.rp_cnt.ensure(8 * ((size_t)a.np + 2)));
@@ -1017,15 +1024,15 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         } else if (pt && pp.shift <= 31) {  // (a bucket's offsets fit 32 bits)
             const uint64_t nb = ((uint64_t)1 << pp.D) + 1;
             CK(g.ptab.ensure(64 * nb));
-            k_pair_table<<<blocks(8 * nb), 256, 0, s>>>(nu, g.pk.as<uint64_t>(), g.pdir.as<uint32_t>(), nb, pp,
+            k_pair_table<<<blocks(8 * nb), 256, 0, s>>>(nu, pkv, g.pdir.as<uint32_t>(), nb, pp,
                                                         g.ptab.as<uint64_t>());
             k_edges_reads_pt<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu,
-                                                          wkey, wtxn, g.pk.as<uint64_t>(), g.ptab.as<uint64_t>(),
+                                                          wkey, wtxn, pkv, g.ptab.as<uint64_t>(),
                                                           pp, g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0,
                                                           diff);
         } else {
             k_edges_reads_pk<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu,
-                                                          wkey, wtxn, g.pk.as<uint64_t>(), g.pdir.as<uint32_t>(),
+                                                          wkey, wtxn, pkv, g.pdir.as<uint32_t>(),
                                                           pp, g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0,
                                                           diff);
         }
@@ -1381,11 +1388,14 @@ __global__ void k_cover_bits(uint32_t nn, const uint8_t *cover, uint64_t *bits)
 
 __device__ __forceinline__ bool cover_bit(const uint64_t *bits, uint32_t v) { return (bits[v >> 6] >> (v & 63)) & 1; }
 
-__global__ void k_cut_append(EdgeSet es, const uint64_t *cover, uint64_t *rows, uint32_t *cnt, uint32_t cap)
+// kCutRows rows per thread (one wave covers 64 x kCutRows consecutive rows
+// per step): every row's words and both cover words in flight together --
+// one row per thread left the pass latency-bound (0.67 ms for config 4's
+// 233M raw rows, 2.8 TB/s)
+constexpr int kCutRows = 4;
+__device__ __forceinline__ void cut_emit(bool hit, uint32_t a, uint32_t b, uint64_t *rows, uint32_t *cnt,
+                                         uint32_t cap)
 {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t a = 0, b = 0;
-    const bool hit = i < es.n && es.get(i, a, b) && cover_bit(cover, a) && cover_bit(cover, b);
     const uint64_t m = __ballot(hit);
     if (!m) return;
     const int lane = threadIdx.x & 63, first = __ffsll((unsigned long long)m) - 1;
@@ -1394,6 +1404,28 @@ __global__ void k_cut_append(EdgeSet es, const uint64_t *cover, uint64_t *rows, 
     base = __shfl(base, first, 64);
     const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
     if (hit && slot < cap) rows[slot] = ((uint64_t)a << 32) | b;
+}
+
+__global__ void k_cut_append(EdgeSet es, const uint64_t *cover, uint64_t *rows, uint32_t *cnt, uint32_t cap)
+{
+    const size_t w0 = ((size_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u)) * kCutRows;
+    const int lane = threadIdx.x & 63;
+    uint32_t a[kCutRows], b[kCutRows];
+    bool v[kCutRows];
+#pragma unroll
+    for (int k = 0; k < kCutRows; ++k) {  // row w0 + 64 k + lane: coalesced per k
+        const size_t i = w0 + (size_t)k * 64 + lane;
+        v[k] = i < es.n && es.get(i, a[k], b[k]);
+    }
+    uint64_t ca[kCutRows], cb[kCutRows];
+#pragma unroll
+    for (int k = 0; k < kCutRows; ++k) {
+        ca[k] = v[k] ? cover[a[k] >> 6] : 0;
+        cb[k] = v[k] ? cover[b[k] >> 6] : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kCutRows; ++k)
+        cut_emit(v[k] && ((ca[k] >> (a[k] & 63)) & 1) && ((cb[k] >> (b[k] & 63)) & 1), a[k], b[k], rows, cnt, cap);
 }
 
 constexpr uint32_t kCutFastCap = 1u << 16;
@@ -1412,7 +1444,7 @@ hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t 
         const uint32_t nn = g.cover_nn;
         if ((e = g.cover_bits.ensure(8 * ((size_t)nn / 64 + 2))) != hipSuccess) return e;
         if (nn) k_cover_bits<<<blocks(nn), 256, 0, s>>>(nn, cover, g.cover_bits.as<uint64_t>());
-        if (ne) k_cut_append<<<blocks(ne), 256, 0, s>>>(es, g.cover_bits.as<uint64_t>(), g.cut.as<uint64_t>(),
+        if (ne) k_cut_append<<<blocks((ne + kCutRows - 1) / kCutRows), 256, 0, s>>>(es, g.cover_bits.as<uint64_t>(), g.cut.as<uint64_t>(),
                                                         g.count.as<uint32_t>(), kCutFastCap);
         uint32_t k = 0;
         if ((e = hipMemcpyAsync(&k, g.count.p, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;

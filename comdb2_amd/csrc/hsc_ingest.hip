@@ -316,7 +316,10 @@ __global__ __launch_bounds__(kUdThreads) void k_pk_unpack_dd(
 #pragma unroll
     for (int r = 0; r < kUdRows; ++r) {
         const uint32_t j = r * kUdThreads + threadIdx.x;
-        lvs[r] = lsn_in && j < nrows ? lsn_in[K[j] & imask] : 0;
+        // (no LSNs and no index bits -- the packed key is the whole row: the
+        // distinct rows' "LSN" slot gets the packed key itself, which the
+        // dependency graph takes as its packed writer array)
+        lvs[r] = j >= nrows ? 0 : lsn_in ? lsn_in[K[j] & imask] : P.I == 0 ? K[j] : 0;
     }
 #pragma unroll  // (whole: lvs stays in registers)
     for (int r = 0; r < kUdRows; ++r) {

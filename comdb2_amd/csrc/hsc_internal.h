@@ -178,7 +178,8 @@ struct PackPlan {
 bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P, bool index = true);
 size_t packed_scratch_bytes(size_t n);
 // The packed sort with the dedupe fused into the unpack: every version to
-// (gid_o, words_o, lsn_o) (gid_o null: not written; lsn null: LSNs 0), the
+// (gid_o, words_o, lsn_o) (gid_o null: not written; lsn null: LSNs 0, or with no index bits the
+// packed keys themselves), the
 // distinct rows to (gid_d, words_d) -- which may
 // be the input gid / words -- and to *lsn_d = whichever of k0 / k1 the sorted
 // keys did not end in; d_count[0] = distinct rows
