@@ -1389,10 +1389,9 @@ __global__ void k_cover_bits(uint32_t nn, const uint8_t *cover, uint64_t *bits)
 __device__ __forceinline__ bool cover_bit(const uint64_t *bits, uint32_t v) { return (bits[v >> 6] >> (v & 63)) & 1; }
 
 // kCutRows rows per thread (one wave covers 64 x kCutRows consecutive rows
-// per step): every row's words and both cover words in flight together --
-// one row per thread left the pass latency-bound (0.67 ms for config 4's
-// 233M raw rows, 2.8 TB/s)
-constexpr int kCutRows = 4;
+// per step).  Measured on config 4's 233M raw rows (r06o): 1 row 0.67 ms,
+// 4 rows with every row's words and cover words in flight together 1.02 ms.
+constexpr int kCutRows = 1;
 __device__ __forceinline__ void cut_emit(bool hit, uint32_t a, uint32_t b, uint64_t *rows, uint32_t *cnt,
                                          uint32_t cap)
 {
