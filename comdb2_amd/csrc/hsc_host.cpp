@@ -141,6 +141,17 @@ static int fail(hsc_ctx *c, int code, const char *what, hipError_t e = hipSucces
 
 // the next append staging buffer of the ring (waits only if the copies that
 // read it two appends ago have not run yet)
+// HSC_FOLD_TRACE: fold events with a steady-clock stamp (diagnostics)
+static bool fold_trace()
+{
+    static const bool on = getenv("HSC_FOLD_TRACE") != nullptr;
+    return on;
+}
+static double trace_us()
+{
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 static int app_stage(hsc_ctx *c, size_t bytes)
 {
     const int i = c->app_i;
@@ -1218,7 +1229,9 @@ static int flush_appends(hsc_ctx *c, bool lazy = false)
         return HSC_OK;
     }
     if (!k && !c->app_tmax) return HSC_OK;
+    const double tf0 = fold_trace() ? trace_us() : 0;
     HIPCHK(c, wait_lanes(c));  // probes in flight on other streams keep reading the old run
+    const double tf1 = fold_trace() ? trace_us() : 0;
     const int nt = c->app_tmax ? (int)c->table_names.size() : 0;
     if (c->app_tmax) HIPCHK(c, c->d_table_max.ensure(8 * (size_t)std::max(nt, 1)));
     if (!k) {  // table maxima only
@@ -1234,6 +1247,7 @@ static int flush_appends(hsc_ctx *c, bool lazy = false)
     const int W = c->W;
     size_t kk = 0;
     HIPCHK_RC(c, stage_appends(c, W, &kk, nt));
+    const double tf2 = fold_trace() ? trace_us() : 0;
     // one upload: rows, then the table maxima the merge kernel copies out
     const size_t woff = (4 * k + 15) & ~(size_t)15;
     const size_t sb = stage_bytes(k, W, nt);
@@ -1266,9 +1280,13 @@ static int flush_appends(hsc_ctx *c, bool lazy = false)
                           nt ? a.lsn + k : nullptr, nt ? c->d_table_max.as<uint64_t>() : nullptr,
                           (uint32_t)nt, in_place));
     if (nt) c->app_tmax = false, c->nt_dev = (uint32_t)nt;
+    const double tf3 = fold_trace() ? trace_us() : 0;
     // no wait: the ring keeps h_app until its copies ran, and every later use
     // of the run is on this stream (hsc_set_stream orders a new stream after it)
     HIPCHK_RC(c, app_staged(c, s));
+    if (fold_trace() && trace_us() - tf0 > 120)
+        fprintf(stderr, "[merge] %.0f lanes %.0f stage %.0f merge %.0f staged %.0f us (k %zu dn %zu in_place %d)\n", tf0,
+                tf1 - tf0, tf2 - tf1, tf3 - tf2, trace_us() - tf3, k, c->dn, (int)in_place);
     c->dcur = o;
     c->dn += k;
     c->app_gid.clear(), c->app_keys.clear(), c->app_koff.clear(), c->app_lsn.clear();
@@ -1418,17 +1436,6 @@ static hipError_t create_stream(hipStream_t *st, bool high)
     if (!prio || hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess || least == greatest)
         return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
     return hipStreamCreateWithPriority(st, hipStreamNonBlocking, high ? greatest : least);
-}
-
-// HSC_FOLD_TRACE: fold events with a steady-clock stamp (diagnostics)
-static bool fold_trace()
-{
-    static const bool on = getenv("HSC_FOLD_TRACE") != nullptr;
-    return on;
-}
-static double trace_us()
-{
-    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 // The fold worker (one host thread per context, started by its first fold):
@@ -3416,9 +3423,16 @@ int hsc_window_append_log(hsc_ctx *c, const hsc_llog *log)
     if (!c->host_only) (void)hipSetDevice(c->device);
     if (c->multi && multi_adopted(c))
         return fail(c, HSC_ESTATE, "append to an adopted multi context: append to its members");
+    const double t0 = fold_trace() ? trace_us() : 0;
     int rc = append_log(c, log);
     if (rc) return rc;
-    return c->live ? flush_appends(c, true) : HSC_OK;
+    const double t1 = fold_trace() ? trace_us() : 0;
+    const size_t pend0 = c->pend_merges;
+    rc = c->live ? flush_appends(c, true) : HSC_OK;
+    if (fold_trace() && trace_us() - t0 > 150)  // (diagnostics: where a slow append went)
+        fprintf(stderr, "[append] %.0f slow: decode %.0f us, flush %.0f us (merged %d)\n", t0, t1 - t0,
+                trace_us() - t1, (int)(c->pend_merges - pend0));
+    return rc;
 }
 
 int hsc_window_append_raw(hsc_ctx *c, const hsc_raw_log *raw)
