@@ -211,7 +211,7 @@ __device__ __forceinline__ bool ph_find(const PointHash &ph, const uint64_t (&k)
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             const u64x2 a0 = x[2 * s], a1 = x[2 * s + 1];
-            if (a1.y == 0) return false;
+            if ((a1.y >> 40) != ph.ep) return false;  // empty: a slot of an older build
             if (a0.x == k[0] && a0.y == k[1] && a1.x == k[2]) {
                 rank = (uint32_t)a1.y;
                 return true;
@@ -222,24 +222,30 @@ __device__ __forceinline__ bool ph_find(const PointHash &ph, const uint64_t (&k)
     return false;
 }
 
-// one thread per window key: claim a slot by its rank word (never 0: bit 32
-// set), then write the key words
-__global__ __launch_bounds__(256) void k_ph_insert(CTiles ct, uint64_t *e, uint64_t nb)
+// one thread per window key: claim a slot by its rank word (ep << 40 | 1 <<
+// 32 | rank; a slot whose epoch is not this build's is empty, so a rebuild
+// needs no clearing pass), then write the key words
+__global__ __launch_bounds__(256) void k_ph_insert(CTiles ct, uint64_t *e, uint64_t nb, uint32_t ep)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= ct.n) return;
     uint64_t k[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) k[j] = j < ct.WG ? ct.key[(size_t)j * ct.len + i] : 0;
-    const unsigned long long r = (unsigned long long)ct.rank[i] | (1ull << 32);
+    const unsigned long long r = (unsigned long long)ct.rank[i] | (1ull << 32) | ((unsigned long long)ep << 40);
     uint64_t b = __umul64hi(ph_mix(k[0], k[1], k[2]), nb);
     for (uint64_t it = 0; it < nb; ++it) {
-#pragma unroll
         for (int s = 0; s < 4; ++s) {
-            uint64_t *x = e + 16 * b + 4 * s;
-            if (atomicCAS((unsigned long long *)(x + 3), 0ull, r) == 0ull) {
-                x[0] = k[0], x[1] = k[1], x[2] = k[2];
-                return;
+            unsigned long long *w = (unsigned long long *)(e + 16 * b + 4 * s + 3);
+            unsigned long long cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while ((cur >> 40) != ep) {  // empty this build: claim it
+                const unsigned long long was = atomicCAS(w, cur, r);
+                if (was == cur) {
+                    uint64_t *x = e + 16 * b + 4 * s;
+                    x[0] = k[0], x[1] = k[1], x[2] = k[2];
+                    return;
+                }
+                cur = was;  // another key took it (or its epoch moved): look again
             }
         }
         b = b + 1 == nb ? 0 : b + 1;
@@ -795,11 +801,11 @@ hipError_t compact_probes(const ProbeView &p, const CompactTables &t, uint64_t *
 // them: the bound kernel 30 -> 59 us, r06d)
 uint64_t point_hash_buckets(uint32_t n) { return (uint64_t)n + 64; }
 
-hipError_t point_hash_build(const CTiles &ct, uint64_t *e, uint64_t nb, hipStream_t s)
+hipError_t point_hash_build(const CTiles &ct, uint64_t *e, uint64_t nb, uint32_t ep, bool clear, hipStream_t s)
 {
-    hipError_t r = hipMemsetAsync(e, 0, 128 * nb, s);
+    hipError_t r = clear ? hipMemsetAsync(e, 0, 128 * nb, s) : hipSuccess;
     if (r != hipSuccess || ct.n == 0) return r;
-    k_ph_insert<<<(ct.n + 255) / 256, 256, 0, s>>>(ct, e, nb);
+    k_ph_insert<<<(ct.n + 255) / 256, 256, 0, s>>>(ct, e, nb, ep);
     return hipGetLastError();
 }
 

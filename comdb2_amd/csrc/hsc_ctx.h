@@ -614,6 +614,7 @@ struct hsc_ctx {
     DBuf d_ckey, d_crank, d_cfirst, d_crel, d_ctrad, d_ctb;
     DBuf d_cph;               // the tiles' point index (PointHash), cph_nb buckets
     uint64_t cph_nb = 0;
+    uint32_t cph_ep = 0;      // its epoch (1..2^24-1; 0 = the buffer was never cleared)
 
     // probe workspace
     DBuf p_lo, p_hi, p_gid, p_snap, p_txn, p_lock_table, p_lock_snap, p_lock_txn;

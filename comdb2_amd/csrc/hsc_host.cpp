@@ -515,8 +515,13 @@ static int build_ctiles(hsc_ctx *c)
     // bound kernel (HSC_PATH_NO_CT_POINTS: they take join records, the r05 path)
     if (!(c->paths & HSC_PATH_NO_CT_POINTS) && ct.n) {
         const uint64_t nb = point_hash_buckets(ct.n);
+        void *old = c->d_cph.p;
         HIPCHK(c, c->d_cph.ensure(128 * nb));
-        HIPCHK(c, point_hash_build(ct, c->d_cph.as<uint64_t>(), nb, s));
+        // a rebuild over the same buffer only bumps the epoch (its entries
+        // read as empty); a new buffer -- or 2^24 builds -- is cleared once
+        const bool clear = c->d_cph.p != old || c->cph_ep == 0 || c->cph_ep >= (1u << 24) - 1;
+        c->cph_ep = clear ? 1 : c->cph_ep + 1;
+        HIPCHK(c, point_hash_build(ct, c->d_cph.as<uint64_t>(), nb, c->cph_ep, clear, s));
         c->cph_nb = nb;
     }
     HIPCHK(c, hipMemcpyAsync(&ct.base0, c->d_cfirst.p, 8, hipMemcpyDeviceToHost, s));
@@ -1410,7 +1415,7 @@ static void swap_window(hsc_ctx *a, hsc_ctx *b)
     swap(a->ctiles, b->ctiles), swap(a->ctv, b->ctv);
     swap(a->d_ckey, b->d_ckey), swap(a->d_crank, b->d_crank), swap(a->d_cfirst, b->d_cfirst);
     swap(a->d_crel, b->d_crel), swap(a->d_ctrad, b->d_ctrad), swap(a->d_ctb, b->d_ctb);
-    swap(a->d_cph, b->d_cph), swap(a->cph_nb, b->cph_nb);
+    swap(a->d_cph, b->d_cph), swap(a->cph_nb, b->cph_nb), swap(a->cph_ep, b->cph_ep);
 }
 
 static DeltaView frozen_view(const hsc_ctx *c)
@@ -2664,6 +2669,7 @@ static int probe_ctiles(hsc_ctx *c, const hsc_probe_batch *b, const ProbeView &p
         ph.gb = ct.gb;
         ph.rank_base = ct.rank_base;
         ph.flags = flags;
+        ph.ep = c->cph_ep;
     }
     if (p.n)
         HIPCHK(c, compact_probes(p, c->ct, c->p_code_lo.as<uint64_t>(), c->p_code_hi.as<uint64_t>(), s, &ph));

@@ -598,9 +598,11 @@ struct PointHash {
     int WG, gb;          // the tiles' key words and group bits
     uint64_t rank_base;  // CTiles::rank_base
     uint8_t *flags;      // the batch's conflict flags (the locate's)
+    uint32_t ep;         // the build's epoch (bits 40..63 of a live entry's rank word)
 };
 uint64_t point_hash_buckets(uint32_t n);
-hipError_t point_hash_build(const CTiles &ct, uint64_t *e, uint64_t nb, hipStream_t s);
+// clear: the buffer is new (epochs restart at 1); else entries of older epochs read as empty
+hipError_t point_hash_build(const CTiles &ct, uint64_t *e, uint64_t nb, uint32_t ep, bool clear, hipStream_t s);
 hipError_t ctiles_build(const uint64_t *cw, size_t cs, int WC, const uint32_t *gid,
                         const uint64_t *lsn, const CTiles &ct, uint64_t *key, uint32_t *rank,
                         uint64_t *first, uint64_t *rel, uint32_t *trad, uint32_t *tb,
