@@ -65,11 +65,30 @@ __device__ __forceinline__ uint32_t gw_bits(size_t nops, const uint8_t *is_write
     return w;
 }
 
-__global__ __launch_bounds__(kGwThreads) void k_gw_count(size_t nops, const uint8_t *is_write, uint32_t *bc)
+// (bad != null: also the input check of graph_check_input over the same ops --
+// bit 0 an id >= ntxn, bit 1 txns out of order -- so the build needs no
+// separate pass and sync for it)
+__global__ __launch_bounds__(kGwThreads) void k_gw_count(size_t nops, const uint8_t *is_write, uint32_t *bc,
+                                                         const uint32_t *txn, const uint32_t *observed,
+                                                         uint32_t ntxn, uint32_t *bad)
 {
     __shared__ uint32_t wsum[kGwThreads / 64];
     uint32_t cnt;
-    (void)gw_bits(nops, is_write, (size_t)blockIdx.x * (kGwThreads * kGwItems), cnt);
+    const size_t base = (size_t)blockIdx.x * (kGwThreads * kGwItems);
+    (void)gw_bits(nops, is_write, base, cnt);
+    if (bad) {  // (coalesced: op base + 256 k + t; its predecessor is the lane before's)
+        uint32_t b = 0;
+#pragma unroll
+        for (int k = 0; k < kGwItems; ++k) {
+            const size_t i = base + (size_t)k * kGwThreads + threadIdx.x;
+            if (i >= nops) break;
+            const uint32_t t = txn[i], o = observed[i], prev = i > 0 ? txn[i - 1] : 0;
+            b |= (t >= ntxn || (o != kNone && o >= ntxn)) ? 1u : 0u;
+            b |= t < prev ? 2u : 0u;
+        }
+        const uint64_t any = __ballot(b != 0);
+        if (any && b) atomicOr(bad, b);
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = cnt;
@@ -866,19 +885,25 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     CK(g.ww2.ensure(16 * wcap));
     CK(g.wl2.ensure(8 * wcap));
     const size_t gwb = (nops + kGwThreads * kGwItems - 1) / (kGwThreads * kGwItems);
-    CK(g.flags.ensure(4 * (gwb + 1)));
+    CK(g.flags.ensure(4 * (gwb + 2)));
     CK(g.scratch.ensure(std::max(scan_scratch_bytes(gwb + 1), (size_t)1024)));
     uint32_t *bc = g.flags.as<uint32_t>();
-    if (gwb) k_gw_count<<<(unsigned)gwb, kGwThreads, 0, s>>>(nops, in.is_write, bc);
-    CK(hipMemsetAsync(bc + gwb, 0, 4, s));
+    CK(hipMemsetAsync(bc + gwb, 0, 8, s));  // the total slot and the check's bits
+    if (gwb)
+        k_gw_count<<<(unsigned)gwb, kGwThreads, 0, s>>>(nops, in.is_write, bc, in.txn, in.observed, in.ntxn,
+                                                         in.check ? bc + gwb + 1 : nullptr);
     CK(scan_exclusive_u32(bc, gwb + 1, g.scratch.as<uint32_t>(), s));
     if (gwb)
         k_gw_place<<<(unsigned)gwb, kGwThreads, 0, s>>>(nops, in.txn, in.key, in.is_write, bc, g.wg.as<uint32_t>(),
                                                          g.ww.as<uint64_t>(), g.wl.as<uint64_t>(), wcap);
     CK(hipGetLastError());
-    uint32_t nw = 0;
-    CK(hipMemcpyAsync(&nw, bc + gwb, 4, hipMemcpyDeviceToHost, s));
+    uint32_t nwb[2] = {0, 0};  // writers, the check's bits
+    CK(hipMemcpyAsync(nwb, bc + gwb, 8, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
+    const uint32_t nw = nwb[0];
+    g.bad = in.check ? nwb[1] : 0;
+    if (g.bad & 1) return hipErrorInvalidValue;  // an op out of range: the caller reports it
+    const bool txn_sorted = in.check ? !(g.bad & 2) : in.txn_sorted;
     size_t rsb = std::max(radix_scratch_bytes(nw, 2), scan_scratch_bytes(nw) + 64);
     rsb = std::max(rsb, packed_scratch_bytes(nw));
     CK(g.scratch.ensure(rsb));
@@ -897,7 +922,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         // txn already: the stable passes need only the key bits (config 4:
         // 3 passes instead of 6)
         static const bool no_skip = getenv("HSC_GRAPH_NO_TXN_SKIP") != nullptr;  // (A/B)
-        if (packed && in.txn_sorted && !no_skip && P.nl > 0 && P.limb[P.nl - 1] == 1) P.skip = P.bits[P.nl - 1];
+        if (packed && txn_sorted && !no_skip && P.nl > 0 && P.limb[P.nl - 1] == 1) P.skip = P.bits[P.nl - 1];
     }
     DBuf *dw = &g.ww2;
     uint64_t *lsn_d = nullptr;  // packed: the distinct packed keys themselves (no LSN input, I = 0)

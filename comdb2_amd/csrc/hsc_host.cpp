@@ -4634,12 +4634,10 @@ int hsc_dep_graph_build_device(hsc_ctx *c, size_t nops, uint32_t ntxn, const uin
     (void)hipSetDevice(c->device);
     GraphInput in{txn_dev, key_dev, is_write_dev, observed_dev, nops, ntxn};
     in.skip_rw = (flags & HSC_GRAPH_NO_RW) != 0;
-    uint32_t bad = 0;
-    HIPCHK(c, graph_check_input(in, c->graph, &bad, c->stream));
-    if (bad & 1) return fail(c, HSC_EINVAL, "history op out of range");
-    in.txn_sorted = !(bad & 2);
+    in.check = true;  // the ids and the txn order, in the build's first pass
     float build_ms = 0;
     int rc = graph_build_timed(c, in, (flags & HSC_GRAPH_FULL) != 0, &build_ms);
+    if (rc && (c->graph.bad & 1)) return fail(c, HSC_EINVAL, "history op out of range");
     if (rc || !st) return rc;
     memset(st, 0, sizeof *st);
     st->build_ms = build_ms;

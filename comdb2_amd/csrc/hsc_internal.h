@@ -471,6 +471,8 @@ struct GraphInput {              // device pointers
     size_t n_extra = 0;
     bool skip_rw = false;  // reads give wr edges only (rw come from x_rows)
     bool txn_sorted = false;  // ops in nondecreasing txn order (graph_check_input's bit 2)
+    bool check = false;       // graph_build checks the ops itself (GraphBufs::bad; an op
+                              // out of range: hipErrorInvalidValue before any edge work)
 };
 struct GraphBufs {
     DBuf flags, flags2, scratch, count;
@@ -491,6 +493,7 @@ struct GraphBufs {
     bool writer_packed = false;  // last build sorted its writers as packed (key, txn) words
     uint32_t diff_nn = 0;        // raw build: diff holds the cover's backward-edge diffs over diff_nn txns
     uint32_t cover_nn = 0;       // txns of the covers graph_cut tests (the build's ntxn)
+    uint32_t bad = 0;            // the last checked build's input bits (GraphInput::check)
     DBuf cover_bits;             // graph_cut: the cover as a bitmap
     void release_all()
     {
