@@ -65,7 +65,7 @@ __device__ __forceinline__ uint32_t gw_bits(size_t nops, const uint8_t *is_write
     return w;
 }
 
-// (bad != null: also the input check of graph_check_input over the same ops --
+// (bad != null: also the check of the ops themselves --
 // bit 0 an id >= ntxn, bit 1 txns out of order -- so the build needs no
 // separate pass and sync for it)
 __global__ __launch_bounds__(kGwThreads) void k_gw_count(size_t nops, const uint8_t *is_write, uint32_t *bc,
@@ -1219,31 +1219,6 @@ hipError_t graph_scc(uint32_t nn, GraphBufs &g, uint32_t *rounds, uint32_t *iter
     return hipSuccess;
 }
 
-// bit 0: an op names a txn >= ntxn; bit 1: ops not in nondecreasing txn order
-__global__ void k_check_ops(GraphInput in, uint32_t *bad)
-{
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= in.nops) return;
-    const uint32_t o = in.observed[i], t = in.txn[i];
-    uint32_t b = (t >= in.ntxn || (o != kNone && o >= in.ntxn)) ? 1u : 0u;
-    if (i + 1 < in.nops && in.txn[i + 1] < t) b |= 2u;
-    const uint64_t any = __ballot(b != 0);
-    if (any && b) atomicOr(bad, b);
-}
-
-// *bad_out: bit 0 if an op names a txn (or observed writer) >= ntxn, bit 1 if
-// the ops are not in nondecreasing txn order
-hipError_t graph_check_input(const GraphInput &in, GraphBufs &g, uint32_t *bad_out, hipStream_t s)
-{
-    hipError_t e = g.count.ensure(64);
-    if (e != hipSuccess) return e;
-    uint32_t *bad = g.count.as<uint32_t>() + 12;
-    if ((e = hipMemsetAsync(bad, 0, 4, s)) != hipSuccess) return e;
-    if (in.nops) k_check_ops<<<blocks(in.nops), 256, 0, s>>>(in, bad);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(bad_out, bad, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-    return hipStreamSynchronize(s);
-}
 
 // ---- sharded SCC: cover, cut, SCC of the cut --------------------------------
 // Txn ids are commit order.  Every node of a cycle lies inside [dst, src] of

@@ -470,7 +470,7 @@ struct GraphInput {              // device pointers
     const uint64_t *x_rows = nullptr, *x_type = nullptr;
     size_t n_extra = 0;
     bool skip_rw = false;  // reads give wr edges only (rw come from x_rows)
-    bool txn_sorted = false;  // ops in nondecreasing txn order (graph_check_input's bit 2)
+    bool txn_sorted = false;  // ops in nondecreasing txn order (set by the check when it runs)
     bool check = false;       // graph_build checks the ops itself (GraphBufs::bad; an op
                               // out of range: hipErrorInvalidValue before any edge work)
 };
@@ -621,7 +621,6 @@ hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_i
 // backward edge of g; the edges of g between covered nodes -> g.cut rows
 // (src << 32 | dst, *m of them); SCC of the graph induced on the cover by
 // explicit rows (~0 = padding) into scc_out[nn] (device).
-hipError_t graph_check_input(const GraphInput &in, GraphBufs &g, uint32_t *bad_out, hipStream_t s);
 hipError_t graph_cover(GraphBufs &g, uint32_t nn, uint8_t *cover, hipStream_t s);
 hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s);
 hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *rows, size_t m,

@@ -247,3 +247,52 @@ def test_gpu_multi_graph_scc_matches_oracle(oracle_mod, kw, world):
         assert st2["cut_nodes"] == st["cut_nodes"]
     finally:
         m.close()
+
+
+def _multi_scc(h, world=1):
+    import torch
+    from comdb2_amd.hsc import MultiValidator
+    dev = torch.device("cuda", 0)
+    m = MultiValidator([0] * world)
+    try:
+        shards = [shard.device_history(shard.history_shard(h, r, world), dev) for r in range(world)]
+        scc = torch.zeros(max(h.ntxn, 1), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        m.graph_scc(shards, h.ntxn, [scc.data_ptr()] + [None] * (world - 1))
+        return scc[:h.ntxn].cpu().numpy().astype(np.uint32)
+    finally:
+        m.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["shuffled", "hot_key", "hot_key_shuffled"])
+def test_gpu_multi_graph_scc_build_paths(oracle_mod, case):
+    """The raw build's paths: ops out of txn order (the writer sort then takes
+    every pass: the txn bits are not skipped), and one hot key whose writers
+    crowd single directory buckets past a bucket line's 12 entries (the
+    overflow search of pk).  Components = Tarjan's."""
+    from comdb2_amd.workloads import History
+    kw = dict(n_txn=20000, n_keys=4, concurrent_frac=0.3, max_lag=16) if case.startswith("hot") else \
+        dict(seed=9, n_txn=20000, n_keys=2000, concurrent_frac=0.2, max_lag=16)
+    h = config4_history(**kw)
+    if case.endswith("shuffled"):
+        p = np.random.default_rng(4).permutation(len(h.txn))
+        h = History(h.txn[p], h.key[p], h.is_write[p], h.observed[p], h.ntxn)
+    s, d, _ = oracle_mod.dep_edges(h.txn, h.key, h.is_write, h.observed)
+    want = oracle_mod.scc(h.ntxn, s, d)
+    np.testing.assert_array_equal(_multi_scc(h), want)
+    np.testing.assert_array_equal(_multi_scc(h, world=2), want)
+
+
+@pytest.mark.gpu
+def test_gpu_multi_graph_scc_rejects_ids_out_of_range():
+    """An op naming a txn >= ntxn fails the call (the count pass's check),
+    before any edge is built."""
+    from comdb2_amd.hsc import HscError
+    from comdb2_amd.workloads import History
+    h = config4_history(n_txn=3000, n_keys=100)
+    obs = h.observed.copy()
+    i = int(np.nonzero(obs >= 0)[0][7])
+    obs[i] = h.ntxn + 5
+    with pytest.raises(HscError, match="out of range"):
+        _multi_scc(History(h.txn, h.key, h.is_write, obs, h.ntxn))
