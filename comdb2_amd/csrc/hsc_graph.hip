@@ -65,26 +65,24 @@ __device__ __forceinline__ uint32_t gw_bits(size_t nops, const uint8_t *is_write
     return w;
 }
 
-// (bad != null: also the check of the ops themselves --
-// bit 0 an id >= ntxn, bit 1 txns out of order -- so the build needs no
-// separate pass and sync for it)
+// (bad != null: the observed ids' range check here too -- bit 0 -- for the
+// builds whose edge pass does not check them itself; the txns' range and order
+// are k_gw_place's)
 __global__ __launch_bounds__(kGwThreads) void k_gw_count(size_t nops, const uint8_t *is_write, uint32_t *bc,
-                                                         const uint32_t *txn, const uint32_t *observed,
-                                                         uint32_t ntxn, uint32_t *bad)
+                                                         const uint32_t *observed, uint32_t ntxn, uint32_t *bad)
 {
     __shared__ uint32_t wsum[kGwThreads / 64];
     uint32_t cnt;
     const size_t base = (size_t)blockIdx.x * (kGwThreads * kGwItems);
     (void)gw_bits(nops, is_write, base, cnt);
-    if (bad) {  // (coalesced: op base + 256 k + t; its predecessor is the lane before's)
+    if (bad) {  // (coalesced: op base + 256 k + t)
         uint32_t b = 0;
 #pragma unroll
         for (int k = 0; k < kGwItems; ++k) {
             const size_t i = base + (size_t)k * kGwThreads + threadIdx.x;
             if (i >= nops) break;
-            const uint32_t t = txn[i], o = observed[i], prev = i > 0 ? txn[i - 1] : 0;
-            b |= (t >= ntxn || (o != kNone && o >= ntxn)) ? 1u : 0u;
-            b |= t < prev ? 2u : 0u;
+            const uint32_t o = observed[i];
+            b |= (o != kNone && o >= ntxn) ? 1u : 0u;
         }
         const uint64_t any = __ballot(b != 0);
         if (any && b) atomicOr(bad, b);
@@ -101,51 +99,84 @@ __global__ __launch_bounds__(kGwThreads) void k_gw_count(size_t nops, const uint
     }
 }
 
+// Coalesced: round k of wave v takes the 64 ops base + 256 k + 64 v + lane
+// -- 64 segments in op order, each one ballot -- so a writer's place in the
+// block is its segment's exclusive count (one wave scans the 64) plus the
+// writers before it in the ballot.  (A thread taking 16 consecutive ops, the
+// count pass's shape, issued every key / txn load over 64 lines: 0.57 ms per
+// 100M ops.)  bad != null: the txns' check -- bit 0 a txn >= ntxn, bit 1 a
+// txn below its predecessor's -- on the txn words it loads anyway.
 __global__ __launch_bounds__(kGwThreads) void k_gw_place(size_t nops, const uint32_t *txn, const uint64_t *key,
                                                          const uint8_t *is_write, const uint32_t *boff,
-                                                         uint32_t *gid, uint64_t *words, uint64_t *lsn,
-                                                         size_t stride)
+                                                         uint32_t *gid, uint64_t *words, size_t stride,
+                                                         uint32_t ntxn, uint32_t *bad)
 {
-    // the block's writers in op order through LDS, then coalesced stores
-    // (each thread storing its own writers at p, p + 1, ... scattered every
-    // store instruction over ~5 x 64 words: 5.8 GB of partial-line writes
-    // per 100M ops, r06d PMC)
+    constexpr int kSeg = kGwItems * (kGwThreads / 64);
+    static_assert(kSeg == 64, "one wave scans the segments");
     __shared__ uint64_t sk[kGwThreads * kGwItems], st[kGwThreads * kGwItems];
-    __shared__ uint32_t wsum[kGwThreads / 64];
+    __shared__ uint32_t segc[kSeg];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const size_t base = (size_t)blockIdx.x * (kGwThreads * kGwItems);
-    uint32_t cnt;
-    const uint32_t w = gw_bits(nops, is_write, base, cnt);
-    uint32_t inc = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += y;
-    }
-    if (lane == 63) wsum[wv] = inc;
-    __syncthreads();
-    uint32_t p = inc - cnt, tot = 0;
-#pragma unroll
-    for (int q = 0; q < kGwThreads / 64; ++q) {
-        p += q < wv ? wsum[q] : 0;
-        tot += wsum[q];
-    }
-    const size_t i0 = base + (size_t)threadIdx.x * kGwItems;
+    // every load issued before the first use (2 blocks per CU by the LDS:
+    // the latency is hidden by the loads in flight, not by waves)
+    uint64_t m[kGwItems], kv[kGwItems];
+    uint32_t tv[kGwItems];
+    uint8_t wv8[kGwItems];
 #pragma unroll
     for (int k = 0; k < kGwItems; ++k) {
-        if (!((w >> k) & 1u)) continue;
-        sk[p] = key[i0 + k];
-        st[p] = txn[i0 + k];
-        ++p;
+        const size_t i = base + (size_t)k * kGwThreads + threadIdx.x;
+        const bool in = i < nops;
+        wv8[k] = in ? is_write[i] : 0;
+        tv[k] = in ? txn[i] : 0;
+        kv[k] = in ? key[i] : 0;
+    }
+    uint32_t b = 0;
+#pragma unroll
+    for (int k = 0; k < kGwItems; ++k) {
+        const size_t i = base + (size_t)k * kGwThreads + threadIdx.x;
+        m[k] = __ballot(wv8[k] != 0);
+        if (lane == 0) segc[k * 4 + wv] = (uint32_t)__popcll(m[k]);
+        if (bad) {  // (the predecessor: the lane before's, lane 0 loads it)
+            uint32_t prev = __shfl_up(tv[k], 1, 64);
+            if (lane == 0) prev = i > 0 && i < nops ? txn[i - 1] : 0;
+            if (i < nops) {
+                b |= tv[k] >= ntxn ? 1u : 0u;
+                b |= tv[k] < prev ? 2u : 0u;
+            }
+        }
+    }
+    if (bad) {
+        const uint64_t any = __ballot(b != 0);
+        if (any && b) atomicOr(bad, b);
+    }
+    __syncthreads();
+    if (wv == 0) {
+        const uint32_t v = segc[lane];
+        uint32_t inc = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        segc[lane] = inc - v;
+    }
+    __syncthreads();
+    const uint64_t lt = (1ull << lane) - 1;
+#pragma unroll
+    for (int k = 0; k < kGwItems; ++k) {
+        if (!((m[k] >> lane) & 1ull)) continue;
+        const uint32_t p = segc[k * 4 + wv] + (uint32_t)__popcll(m[k] & lt);
+        sk[p] = kv[k];
+        st[p] = tv[k];
     }
     __syncthreads();
     const size_t b0 = boff[blockIdx.x];
+    const uint32_t tot = boff[blockIdx.x + 1] - boff[blockIdx.x];
     for (uint32_t j = threadIdx.x; j < tot; j += kGwThreads) {
         words[b0 + j] = sk[j];
         words[stride + b0 + j] = st[j];
         gid[b0 + j] = 0;
     }
-    (void)lsn;  // (zeroed by the whole-row sort's caller only: the packed sort reads none)
 }
 
 
@@ -179,15 +210,24 @@ __global__ void k_edges_ww(uint32_t nu, const uint64_t *wkey, const uint64_t *wt
     }
 }
 
+// chk_n != 0: an observed id >= chk_n sets bit 0 of *bad and the op gives no
+// rows (the build's check: the txns are k_gw_place's)
+__device__ __forceinline__ bool obs_bad(uint32_t ob, uint32_t chk_n, uint32_t *bad)
+{
+    if (chk_n == 0 || ob == kNone || ob < chk_n) return false;
+    atomicOr(bad, 1u);
+    return true;
+}
+
 __global__ void k_edges_reads(size_t nops, const uint32_t *txn, const uint64_t *key,
                               const uint8_t *is_write, const uint32_t *observed, uint32_t nu,
                               const uint64_t *wkey, const uint64_t *wtxn, uint64_t *ew,
-                              uint64_t *et, uint32_t *eg, int skip_rw)
+                              uint64_t *et, uint32_t *eg, int skip_rw, uint32_t chk_n, uint32_t *bad)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nops) return;
     uint64_t wr = ~0ull, rw = ~0ull;
-    if (!is_write[i]) {
+    if (!is_write[i] && !obs_bad(observed[i], chk_n, bad)) {
         const uint32_t r = txn[i], ob = observed[i];
         const uint64_t k = key[i];
         if (ob != kNone && ob != r) wr = ((uint64_t)ob << 32) | r;
@@ -281,12 +321,13 @@ __global__ void k_edges_reads_pk(size_t nops, const uint32_t *txn, const uint64_
                                  const uint8_t *is_write, const uint32_t *observed, uint32_t nu,
                                  const uint64_t *wkey, const uint64_t *wtxn, const uint64_t *pk,
                                  const uint32_t *dir, PairPack pp, uint64_t *ew, uint64_t *et,
-                                 uint32_t *eg, int skip_rw, uint32_t *diff)
+                                 uint32_t *eg, int skip_rw, uint32_t *diff, uint32_t chk_n,
+                                 uint32_t *bad)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nops) return;
     uint64_t wr = ~0ull, rw = ~0ull;
-    if (!is_write[i]) {
+    if (!is_write[i] && !obs_bad(observed[i], chk_n, bad)) {
         const uint32_t r = txn[i], ob = observed[i];
         const uint64_t k = key[i];
         if (ob != kNone && ob != r) wr = ((uint64_t)ob << 32) | r;
@@ -362,19 +403,23 @@ __global__ void k_edges_reads_pk(size_t nops, const uint32_t *txn, const uint64_
 // bucket) searches pk as before.  (A first form with 14 full 8-byte entries
 // per 128-byte line, 512 MB: the search 3.5 -> 2.85 ms, but stored a u64 per
 // thread 128 bytes apart -- 5 GB of partial-line writes, 1.05 ms.)
-constexpr int kPtE = 12;
+// LW = 8: 64-byte lines, 12 offsets, about 8 writers per bucket (default);
+// LW = 16: 128-byte lines, 28 offsets, about 16 writers per bucket -- the same
+// table bytes, ~0.3 % of the buckets overflow instead of ~5 %, but measured
+// slower (r06x).
 __device__ __forceinline__ uint64_t bucket_start(const PairPack &pp, uint64_t b)
 {
     return pp.base + (pp.shift >= 64 ? 0 : b << pp.shift);
 }
 
-// 8 threads per bucket, one 8-byte word each: coalesced lines
+// LW threads per bucket, one 8-byte word each: coalesced lines
+template <int LW>
 __global__ void k_pair_table(uint32_t nu, const uint64_t *pk, const uint32_t *dir, uint64_t nb, PairPack pp,
                              uint64_t *tab)
 {
     const uint64_t id = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t b = id >> 3;
-    const int w = (int)(id & 7);
+    const uint64_t b = id / LW;
+    const int w = (int)(id % LW);
     if (b >= nb) return;
     const uint32_t lo = dir[b], hi = dir[b + 1], n = hi - lo;
     uint64_t v;
@@ -389,19 +434,21 @@ __global__ void k_pair_table(uint32_t nu, const uint64_t *pk, const uint32_t *di
         const uint32_t e1 = j1 < n ? (uint32_t)(pk[lo + j1] - s0) : 0xFFFFFFFFu;
         v = (uint64_t)e0 | ((uint64_t)e1 << 32);
     }
-    tab[8 * b + w] = v;
+    tab[(uint64_t)LW * b + w] = v;
 }
 
+template <int LW>
 __global__ void k_edges_reads_pt(size_t nops, const uint32_t *txn, const uint64_t *key,
                                  const uint8_t *is_write, const uint32_t *observed, uint32_t nu,
                                  const uint64_t *wkey, const uint64_t *wtxn, const uint64_t *pk,
                                  const uint64_t *tab, PairPack pp, uint64_t *ew, uint64_t *et,
-                                 uint32_t *eg, int skip_rw, uint32_t *diff)
+                                 uint32_t *eg, int skip_rw, uint32_t *diff, uint32_t chk_n,
+                                 uint32_t *bad)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nops) return;
     uint64_t wr = ~0ull, rw = ~0ull;
-    if (!is_write[i]) {
+    if (!is_write[i] && !obs_bad(observed[i], chk_n, bad)) {
         const uint32_t r = txn[i], ob = observed[i];
         const uint64_t k = key[i];
         if (ob != kNone && ob != r) wr = ((uint64_t)ob << 32) | r;
@@ -414,10 +461,11 @@ __global__ void k_edges_reads_pt(size_t nops, const uint32_t *txn, const uint64_
                 const uint64_t x = pair_key(pp, kp) | (ob == kNone ? 0 : bits_compress(ob, pp.tm, tm));
                 const bool strict = ob != kNone;
                 const uint64_t b = pair_bucket(pp, x);
-                const u64x2 *line = (const u64x2 *)(tab + 8 * b);
-                u64x2 e[4];
+                constexpr int kPtE = 2 * (LW - 2);
+                const u64x2 *line = (const u64x2 *)(tab + (uint64_t)LW * b);
+                u64x2 e[LW / 2];
 #pragma unroll
-                for (int q = 0; q < 4; ++q) e[q] = line[q];
+                for (int q = 0; q < LW / 2; ++q) e[q] = line[q];
                 const uint64_t hd = e[0].x;
                 const uint32_t n = (uint32_t)(hd & 0x7FFFFFFFu), lo = (uint32_t)(hd >> 32);
                 bool have = false;
@@ -866,6 +914,20 @@ static hipError_t graph_rows_csr(size_t ne_raw, size_t ecap, uint32_t nn, GraphB
     return hipSuccess;
 }
 
+// out = {distinct writers, wkey[0], wtxn[0], pk[0], pk[nu - 1]} (pk null: 0s)
+__global__ void k_graph_meta(const uint32_t *count, const uint64_t *wkey, const uint64_t *wtxn, const uint64_t *pk,
+                             uint64_t *out, uint32_t *ebad)
+{
+    if (threadIdx.x != 0) return;
+    *ebad = 0;
+    const uint32_t nu = count[0];
+    out[0] = nu;
+    out[1] = nu ? wkey[0] : 0;
+    out[2] = nu ? wtxn[0] : 0;
+    out[3] = nu && pk ? pk[0] : 0;
+    out[4] = nu && pk ? pk[nu - 1] : 0;
+}
+
 hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_t s)
 {
     hipError_t e = hipSuccess;
@@ -885,17 +947,22 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     CK(g.ww2.ensure(16 * wcap));
     CK(g.wl2.ensure(8 * wcap));
     const size_t gwb = (nops + kGwThreads * kGwItems - 1) / (kGwThreads * kGwItems);
+    // the partitioned read search (A/B, HSC_GRAPH_RP=1) does not check the
+    // observed ids: the count pass does then (else the edge pass, guarded)
+    static const bool rp_env = getenv("HSC_GRAPH_RP") != nullptr && atoi(getenv("HSC_GRAPH_RP")) != 0;
+    const bool obs_in_count = rp_env;
     CK(g.flags.ensure(4 * (gwb + 2)));
     CK(g.scratch.ensure(std::max(scan_scratch_bytes(gwb + 1), (size_t)1024)));
     uint32_t *bc = g.flags.as<uint32_t>();
     CK(hipMemsetAsync(bc + gwb, 0, 8, s));  // the total slot and the check's bits
     if (gwb)
-        k_gw_count<<<(unsigned)gwb, kGwThreads, 0, s>>>(nops, in.is_write, bc, in.txn, in.observed, in.ntxn,
-                                                         in.check ? bc + gwb + 1 : nullptr);
+        k_gw_count<<<(unsigned)gwb, kGwThreads, 0, s>>>(nops, in.is_write, bc, in.observed, in.ntxn,
+                                                         in.check && obs_in_count ? bc + gwb + 1 : nullptr);
     CK(scan_exclusive_u32(bc, gwb + 1, g.scratch.as<uint32_t>(), s));
     if (gwb)
         k_gw_place<<<(unsigned)gwb, kGwThreads, 0, s>>>(nops, in.txn, in.key, in.is_write, bc, g.wg.as<uint32_t>(),
-                                                         g.ww.as<uint64_t>(), g.wl.as<uint64_t>(), wcap);
+                                                         g.ww.as<uint64_t>(), wcap, in.ntxn,
+                                                         in.check ? bc + gwb + 1 : nullptr);
     CK(hipGetLastError());
     uint32_t nwb[2] = {0, 0};  // writers, the check's bits
     CK(hipMemcpyAsync(nwb, bc + gwb, 8, hipMemcpyDeviceToHost, s));
@@ -907,7 +974,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     size_t rsb = std::max(radix_scratch_bytes(nw, 2), scan_scratch_bytes(nw) + 64);
     rsb = std::max(rsb, packed_scratch_bytes(nw));
     CK(g.scratch.ensure(rsb));
-    CK(g.count.ensure(64));
+    CK(g.count.ensure(128));  // (+ the meta words below)
     // (key, txn) pairs whose varying bits fit 64 sort as single words, the
     // pair itself being the key (no row index, nothing to gather): one 8-byte
     // read + write per pass and varying byte, the dedupe fused into the
@@ -946,11 +1013,19 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
                        g.flags.as<uint32_t>(), g.scratch.p, g.scratch.bytes, g.count.as<uint32_t>(), s));
     }
     g.writer_packed = packed;
-    uint32_t nu = 0;
-    CK(hipMemcpyAsync(&nu, g.count.p, 4, hipMemcpyDeviceToHost, s));
-    CK(hipStreamSynchronize(s));
-    if (!nw) nu = 0;
     const uint64_t *wkey = dw->as<uint64_t>(), *wtxn = dw->as<uint64_t>() + wcap;
+    // the distinct count with what the packed search's parameters need -- the
+    // first writer row, the first and last packed writer -- in one read
+    uint64_t meta[5] = {0, 0, 0, 0, 0};
+    // (the edge pass's check word, g.count's u32 30, cleared by the same kernel)
+    uint32_t *ebad = g.count.as<uint32_t>() + 30;
+    const uint32_t chk_n = in.check && !obs_in_count ? std::max<uint32_t>(in.ntxn, 1) : 0;
+    g.edge_bad = chk_n ? ebad : nullptr;
+    k_graph_meta<<<1, 64, 0, s>>>(g.count.as<uint32_t>(), wkey, wtxn, packed ? lsn_d : nullptr,
+                                  g.count.as<uint64_t>() + 8, ebad);
+    CK(hipMemcpyAsync(meta, g.count.as<uint64_t>() + 8, sizeof meta, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    uint32_t nu = nw ? (uint32_t)meta[0] : 0;
     // 2. edges (capacity for the widest layout: nu + 2 nops + extras)
     const size_t ne_cap = (size_t)nu + 2 * nops + in.n_extra;
     const size_t ecap = std::max<size_t>(64, (ne_cap + 63) & ~(size_t)63);
@@ -967,10 +1042,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     if (nu) k_edges_ww<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, g.ew.as<uint64_t>(), et, eg);
     if (nops && packed && nu) {
         PairPack pp{};
-        uint64_t r0[2];
-        CK(hipMemcpyAsync(&r0[0], wkey, 8, hipMemcpyDeviceToHost, s));
-        CK(hipMemcpyAsync(&r0[1], wtxn, 8, hipMemcpyDeviceToHost, s));
-        CK(hipStreamSynchronize(s));
+        const uint64_t r0[2] = {meta[1], meta[2]};
         pp.km = vary[0], pp.tm = vary[1];
         pp.kc = r0[0] & ~pp.km, pp.tc = r0[1] & ~pp.tm;
         compress_moves(pp.km, pp.kmv);
@@ -981,8 +1053,14 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         // 11.2 ms per step, 8 / 2^23 10.4 ms (a read's search touches the
         // directory line and one line of pk instead of ~3), 4 / 2^24 10.4,
         // 2 / 2^25 10.6 (the directory's own build grows)
-        static int kPer = 8, kDMax = 23;
+        // bucket lines of kLine words (HSC_GRAPH_PT_LINE = 8 | 16, an A/B):
+        // twice the writers per bucket with the 128-byte lines -- slower
+        // (r06x, config 4: the search 2.28 -> 2.62 ms; a random 64-byte line
+        // costs less than a 128-byte one, the overflow searches saved less)
+        static int kPer = 8, kDMax = 23, kLine = 8;
         static const bool env_read = [] {
+            if (const char *v = getenv("HSC_GRAPH_PT_LINE")) kLine = atoi(v) == 16 ? 16 : 8;
+            if (kLine == 16) kPer = 16, kDMax = 22;
             if (const char *v = getenv("HSC_GRAPH_DIR")) sscanf(v, "%d,%d", &kPer, &kDMax);
             return true;
         }();
@@ -993,14 +1071,15 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         // the sort's unpack left the distinct packed keys -- compress(key) <<
         // tb | compress(txn), the same words (no gid limb: gid is 0) -- in lsn_d
         const uint64_t *pkv = lsn_d;
+        pp.base = meta[3], pp.last = meta[4];
         if (!pkv) {
             CK(g.pk.ensure(8 * (size_t)nu));
             k_pair_keys<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, pp, g.pk.as<uint64_t>());
             pkv = g.pk.as<uint64_t>();
+            CK(hipMemcpyAsync(&pp.base, pkv, 8, hipMemcpyDeviceToHost, s));
+            CK(hipMemcpyAsync(&pp.last, pkv + nu - 1, 8, hipMemcpyDeviceToHost, s));
+            CK(hipStreamSynchronize(s));
         }
-        CK(hipMemcpyAsync(&pp.base, pkv, 8, hipMemcpyDeviceToHost, s));
-        CK(hipMemcpyAsync(&pp.last, pkv + nu - 1, 8, hipMemcpyDeviceToHost, s));
-        CK(hipStreamSynchronize(s));
         pp.shift = 0;  // (last - base) >> shift < 2^D
         while (pp.shift < 64 && ((pp.last - pp.base) >> pp.shift) >= ((uint64_t)1 << pp.D)) ++pp.shift;
         k_pair_dir<<<blocks(((size_t)1 << pp.D) + 2), 256, 0, s>>>(nu, pkv, pp,
@@ -1009,7 +1088,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         // count 3.0 + scatter 3.2 + join 1.0 ms against 3.5 ms for the
         // directory search -- the count's per-read global atomics on 16k
         // partition counters), so off unless HSC_GRAPH_RP=1 (A/B)
-        static const bool rp = getenv("HSC_GRAPH_RP") != nullptr && atoi(getenv("HSC_GRAPH_RP")) != 0;
+        const bool rp = rp_env;
         // bucket lines (HSC_GRAPH_PT=0: the directory + pk search, an A/B)
         static const bool pt = getenv("HSC_GRAPH_PT") == nullptr || atoi(getenv("HSC_GRAPH_PT")) != 0;
         // raw builds (the sharded SCC's): the cover's backward-edge diffs as
@@ -1048,23 +1127,30 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
             slot_layout = true;
         } else if (pt && pp.shift <= 31) {  // (a bucket's offsets fit 32 bits)
             const uint64_t nb = ((uint64_t)1 << pp.D) + 1;
-            CK(g.ptab.ensure(64 * nb));
-            k_pair_table<<<blocks(8 * nb), 256, 0, s>>>(nu, pkv, g.pdir.as<uint32_t>(), nb, pp,
-                                                        g.ptab.as<uint64_t>());
-            k_edges_reads_pt<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu,
-                                                          wkey, wtxn, pkv, g.ptab.as<uint64_t>(),
-                                                          pp, g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0,
-                                                          diff);
+            CK(g.ptab.ensure(8 * (size_t)kLine * nb));
+#define HSC_PT(LW_)                                                                                       \
+    k_pair_table<LW_><<<blocks(LW_ * nb), 256, 0, s>>>(nu, pkv, g.pdir.as<uint32_t>(), nb, pp,              \
+                                                       g.ptab.as<uint64_t>());                             \
+    k_edges_reads_pt<LW_><<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu, \
+                                                       wkey, wtxn, pkv, g.ptab.as<uint64_t>(), pp,          \
+                                                       g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0, diff, chk_n, \
+                                                       ebad)
+            if (kLine == 16) {
+                HSC_PT(16);
+            } else {
+                HSC_PT(8);
+            }
+#undef HSC_PT
         } else {
             k_edges_reads_pk<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu,
                                                           wkey, wtxn, pkv, g.pdir.as<uint32_t>(),
                                                           pp, g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0,
-                                                          diff);
+                                                          diff, chk_n, ebad);
         }
     } else if (nops) {
         k_edges_reads<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed,
                                                    nu, wkey, wtxn, g.ew.as<uint64_t>(), et, eg,
-                                                   in.skip_rw ? 1 : 0);
+                                                   in.skip_rw ? 1 : 0, chk_n, ebad);
     }
     CK(hipGetLastError());
     // the partitioned search filled [nu, nu + nops + rw_rows) (else [nu, nu + 2 nops))
@@ -1080,6 +1166,8 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     }
     g.raw = !full;
     g.ne_raw = ne_raw;
+    g.op_cut = !full && !slot_layout && txn_sorted;
+    g.op_at = nu, g.op_n = nops, g.x_at = ne_hist, g.x_n = in.n_extra;
     g.diff_nn = diff_done ? in.ntxn : 0;  // graph_cover: the diffs are there already
     g.cover_nn = in.ntxn;
     if (!full) {  // raw edge rows only (duplicates, ~0 holes): enough for cover / cut
@@ -1408,8 +1496,60 @@ __global__ void k_cut_append(EdgeSet es, const uint64_t *cover, uint64_t *rows, 
 }
 
 constexpr uint32_t kCutFastCap = 1u << 16;
+constexpr uint32_t kCoverListCap = 1u << 16;
 
-hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s)
+// the cover as a bitmap and as a list of its txns (wave-aggregated appends;
+// past cap counted only)
+__global__ void k_cover_list(uint32_t nn, const uint8_t *cover, uint64_t *bits, uint32_t *list,
+                             uint32_t *cnt, uint32_t cap)
+{
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool on = v < nn && cover[v] != 0;
+    const uint64_t m = __ballot(on);
+    const int lane = threadIdx.x & 63;
+    if (lane == 0 && v < nn) bits[v >> 6] = m;
+    if (!m) return;
+    const int first = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(cnt, (uint32_t)__popcll(m));
+    base = __shfl(base, first, 64);
+    const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    if (on && slot < cap) list[slot] = v;
+}
+
+// one thread per covered txn t: its ops (txn-sorted: one run, found by a
+// binary search) and their two rows each -- a cut row at op i has its reader
+// t as one end, so a row whose txn is not covered is never in the cut
+__global__ void k_cut_txn_ops(const uint32_t *list, const uint32_t *lcnt, const uint32_t *op_txn, size_t nops,
+                              const uint64_t *op_rows, const uint64_t *cover, uint64_t *rows, uint32_t *cnt,
+                              uint32_t cap)
+{
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= min(*lcnt, kCoverListCap)) return;
+    const uint32_t t = list[j];
+    size_t lo = 0, hi = nops;
+    while (lo < hi) {
+        const size_t mid = (lo + hi) >> 1;
+        if (op_txn[mid] < t)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    for (size_t i = lo; i < nops && op_txn[i] == t; ++i) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint64_t r = op_rows[2 * i + q];
+            if (r == ~0ull) continue;
+            const uint32_t a = (uint32_t)(r >> 32), b = (uint32_t)r;
+            if (cover_bit(cover, a) && cover_bit(cover, b)) {
+                const uint32_t slot = atomicAdd(cnt, 1u);
+                if (slot < cap) rows[slot] = r;
+            }
+        }
+    }
+}
+
+hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s, const uint32_t *op_txn)
 {
     hipError_t e = hipSuccess;
     const EdgeSet es = edge_set(g);
@@ -1419,15 +1559,50 @@ hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t 
         // the usual tiny cut: one pass, then sorted on the host
         if ((e = g.cut.ensure(8 * (size_t)kCutFastCap)) != hipSuccess) return e;
         if ((e = g.count.ensure(64)) != hipSuccess) return e;
-        if ((e = hipMemsetAsync(g.count.p, 0, 4, s)) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(g.count.p, 0, 8, s)) != hipSuccess) return e;
         const uint32_t nn = g.cover_nn;
         if ((e = g.cover_bits.ensure(8 * ((size_t)nn / 64 + 2))) != hipSuccess) return e;
-        if (nn) k_cover_bits<<<blocks(nn), 256, 0, s>>>(nn, cover, g.cover_bits.as<uint64_t>());
-        if (ne) k_cut_append<<<blocks(ne), 256, 0, s>>>(es, g.cover_bits.as<uint64_t>(), g.cut.as<uint64_t>(),
-                                                        g.count.as<uint32_t>(), kCutFastCap);
         uint32_t k = 0;
-        if ((e = hipMemcpyAsync(&k, g.count.p, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        // by the covered txns' ops (config 4: 1179 covered of 16.7M txns --
+        // the ww rows and ~7k op rows tested instead of all 233M rows), unless
+        // the cover has more than kCoverListCap txns (then every row, below)
+        static const bool no_op_cut = getenv("HSC_GRAPH_NO_OP_CUT") != nullptr;  // (A/B)
+        bool done = false;
+        if (op_txn && g.raw && g.op_cut && !no_op_cut && nn) {
+            if ((e = g.cover_list.ensure(4 * (size_t)kCoverListCap)) != hipSuccess) return e;
+            uint32_t *cnt = g.count.as<uint32_t>();  // [0] cut rows, [1] covered txns
+            k_cover_list<<<blocks(nn), 256, 0, s>>>(nn, cover, g.cover_bits.as<uint64_t>(),
+                                                    g.cover_list.as<uint32_t>(), cnt + 1, kCoverListCap);
+            const uint64_t *ew = g.ew.as<uint64_t>();
+            if (g.op_at)
+                k_cut_append<<<blocks(g.op_at), 256, 0, s>>>(EdgeSet{ew, nullptr, nullptr, g.op_at},
+                                                             g.cover_bits.as<uint64_t>(), g.cut.as<uint64_t>(), cnt,
+                                                             kCutFastCap);
+            if (g.x_n)
+                k_cut_append<<<blocks(g.x_n), 256, 0, s>>>(EdgeSet{ew + g.x_at, nullptr, nullptr, g.x_n},
+                                                           g.cover_bits.as<uint64_t>(), g.cut.as<uint64_t>(), cnt,
+                                                           kCutFastCap);
+            if (g.op_n)
+                k_cut_txn_ops<<<blocks(kCoverListCap), 256, 0, s>>>(g.cover_list.as<uint32_t>(), cnt + 1, op_txn,
+                                                                    g.op_n, ew + g.op_at, g.cover_bits.as<uint64_t>(),
+                                                                    g.cut.as<uint64_t>(), cnt, kCutFastCap);
+            uint32_t kc[2] = {0, 0};
+            if ((e = hipMemcpyAsync(kc, g.count.p, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+            done = kc[1] <= kCoverListCap;
+            if (done)
+                k = kc[0];
+            else if ((e = hipMemsetAsync(g.count.p, 0, 8, s)) != hipSuccess)
+                return e;
+        }
+        if (!done) {
+            if (nn) k_cover_bits<<<blocks(nn), 256, 0, s>>>(nn, cover, g.cover_bits.as<uint64_t>());
+            if (ne)
+                k_cut_append<<<blocks(ne), 256, 0, s>>>(es, g.cover_bits.as<uint64_t>(), g.cut.as<uint64_t>(),
+                                                        g.count.as<uint32_t>(), kCutFastCap);
+            if ((e = hipMemcpyAsync(&k, g.count.p, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+        }
         if (k <= kCutFastCap) {
             std::vector<uint64_t> h(k);
             if (k) {

@@ -4503,13 +4503,22 @@ static int graph_build_timed(hsc_ctx *c, const GraphInput &in, bool full, float 
         gi.n_extra = gb.n_extra;
         gb.n_extra = 0;
     }
+    gb.edge_bad = nullptr;
     hipError_t e = graph_build(gi, gb, full, s);
     if (e == hipSuccess) e = hipEventRecord(e1, s);
+    // the edge pass's check of the observed ids (in.check), read with the sync
+    uint32_t ebad = 0;
+    if (e == hipSuccess && gb.edge_bad) e = hipMemcpyAsync(&ebad, gb.edge_bad, 4, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e == hipSuccess) (void)hipEventElapsedTime(build_ms, e0, e1);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     HIPCHK(c, e);
+    gb.bad |= ebad;
+    if (ebad & 1) {
+        c->graph_ntxn = 0;
+        return fail(c, HSC_EINVAL, "history op out of range");
+    }
     c->graph_ntxn = in.ntxn;
     return HSC_OK;
 }
@@ -4848,11 +4857,11 @@ int ctx_edge_keys(hsc_ctx *c, uint32_t *gid, uint64_t *words)
 
 // The cut of the last build under cover (one pass: count + rows); *rows
 // points into the context's own buffer until its next graph call.
-int ctx_graph_cut(hsc_ctx *c, const uint8_t *cover, size_t *m, const uint64_t **rows)
+int ctx_graph_cut(hsc_ctx *c, const uint8_t *cover, size_t *m, const uint64_t **rows, const uint32_t *op_txn)
 {
     MuGuard g(c);
     (void)hipSetDevice(c->device);
-    HIPCHK(c, graph_cut(c->graph, cover, m, c->stream));
+    HIPCHK(c, graph_cut(c->graph, cover, m, c->stream, op_txn));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     *rows = c->graph.cut.as<uint64_t>();
     return HSC_OK;

@@ -494,7 +494,15 @@ struct GraphBufs {
     uint32_t diff_nn = 0;        // raw build: diff holds the cover's backward-edge diffs over diff_nn txns
     uint32_t cover_nn = 0;       // txns of the covers graph_cut tests (the build's ntxn)
     uint32_t bad = 0;            // the last checked build's input bits (GraphInput::check)
+    uint32_t *edge_bad = nullptr;  // device word of the edge pass's observed-id check (graph_build_timed
+                                   // reads it after the build), or null
     DBuf cover_bits;             // graph_cut: the cover as a bitmap
+    DBuf cover_list;             // graph_cut: the covered txns (the op-range cut)
+    // raw build over txn-sorted ops in the op-slot layout (ww rows [0, op_at),
+    // op i's rows op_at + 2i, + 1, staged rows from x_at): graph_cut given the
+    // ops' txn array visits the covered txns' ops only
+    bool op_cut = false;
+    size_t op_at = 0, op_n = 0, x_at = 0, x_n = 0;
     void release_all()
     {
         DBuf *all[] = {&flags, &flags2, &scratch, &count, &wg, &ww, &wl, &wg2, &ww2, &wl2,
@@ -502,7 +510,7 @@ struct GraphBufs {
                        &in_src, &in_dst, &out_off, &in_off, &scc, &active, &color, &mark,
                        &front, &front2, &h_txn, &h_key, &h_isw, &h_obs, &diff, &cut,
                        &cut_id, &txn_of, &x_rows, &x_type, &x_map, &pk, &pdir, &ptab, &rp_cnt,
-                       &rp_items, &cover_bits};
+                       &rp_items, &cover_bits, &cover_list};
         for (DBuf *b : all) b->release();
     }
 };
@@ -622,7 +630,11 @@ hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_i
 // (src << 32 | dst, *m of them); SCC of the graph induced on the cover by
 // explicit rows (~0 = padding) into scc_out[nn] (device).
 hipError_t graph_cover(GraphBufs &g, uint32_t nn, uint8_t *cover, hipStream_t s);
-hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s);
+// op_txn: the last build's ops' txn array (still live), or null -- with it a
+// raw build over txn-sorted ops tests the ww / staged rows and the covered
+// txns' own op rows instead of every row
+hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s,
+                     const uint32_t *op_txn = nullptr);
 hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *rows, size_t m,
                           GraphBufs &g, uint32_t *scc_out, uint32_t *n_cut, uint32_t *rounds,
                           uint32_t *iterations, hipStream_t s);

@@ -265,16 +265,25 @@ def _multi_scc(h, world=1):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["shuffled", "hot_key", "hot_key_shuffled"])
+@pytest.mark.parametrize("case", ["shuffled", "hot_key", "hot_key_shuffled", "hot_mix", "wide_cover"])
 def test_gpu_multi_graph_scc_build_paths(oracle_mod, case):
     """The raw build's paths: ops out of txn order (the writer sort then takes
-    every pass: the txn bits are not skipped), and one hot key whose writers
-    crowd single directory buckets past a bucket line's 12 entries (the
-    overflow search of pk).  Components = Tarjan's."""
+    every pass: the txn bits are not skipped), and hot keys whose writers
+    crowd single directory buckets past a bucket line's entries (the overflow
+    search of pk): four keys only, or half of 2000 keys' ops moved onto key 0
+    (its writers ~1000x denser than the buckets are sized for).  Components =
+    Tarjan's.  The cut: by the covered txns' op ranges (txn-sorted ops), by
+    every row (shuffled), and every row again after the op-range pass finds
+    more covered txns than its list holds (wide_cover: > 65536)."""
     from comdb2_amd.workloads import History
-    kw = dict(n_txn=20000, n_keys=4, concurrent_frac=0.3, max_lag=16) if case.startswith("hot") else \
+    kw = dict(n_txn=20000, n_keys=4, concurrent_frac=0.3, max_lag=16) if case.startswith("hot_key") else \
         dict(seed=9, n_txn=20000, n_keys=2000, concurrent_frac=0.2, max_lag=16)
+    if case == "wide_cover":
+        kw = dict(seed=11, n_txn=200000, n_keys=2000, concurrent_frac=0.9, max_lag=64)  # ~185k covered
     h = config4_history(**kw)
+    if case == "hot_mix":
+        hot = np.random.default_rng(5).random(len(h.key)) < 0.5
+        h = History(h.txn, np.where(hot, np.zeros_like(h.key), h.key), h.is_write, h.observed, h.ntxn)
     if case.endswith("shuffled"):
         p = np.random.default_rng(4).permutation(len(h.txn))
         h = History(h.txn[p], h.key[p], h.is_write[p], h.observed[p], h.ntxn)
