@@ -68,6 +68,32 @@ __device__ __forceinline__ uint32_t gw_bits(size_t nops, const uint8_t *is_write
 // (bad != null: the observed ids' range check here too -- bit 0 -- for the
 // builds whose edge pass does not check them itself; the txns' range and order
 // are k_gw_place's)
+// out[0] / out[1] = the varying bits of the writers' key / txn, out[2] = 0
+// (their gid): OR & ~AND over k_gw_place's block partials
+__global__ __launch_bounds__(1024) void k_vary_reduce(uint32_t nb, const uint64_t *vp, uint64_t *out)
+{
+    __shared__ uint64_t red[16][4];
+    uint64_t ko = 0, ka = ~0ull, to = 0, ta = ~0ull;
+    for (uint32_t b = threadIdx.x; b < nb; b += 1024) {
+        ko |= vp[4 * (size_t)b], ka &= vp[4 * (size_t)b + 1];
+        to |= vp[4 * (size_t)b + 2], ta &= vp[4 * (size_t)b + 3];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        ko |= __shfl_xor(ko, o, 64), ka &= __shfl_xor(ka, o, 64);
+        to |= __shfl_xor(to, o, 64), ta &= __shfl_xor(ta, o, 64);
+    }
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) red[wv][0] = ko, red[wv][1] = ka, red[wv][2] = to, red[wv][3] = ta;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) ko |= red[w][0], ka &= red[w][1], to |= red[w][2], ta &= red[w][3];
+        out[0] = ko & ~ka;
+        out[1] = to & ~ta;
+        out[2] = 0;
+    }
+}
+
 __global__ __launch_bounds__(kGwThreads) void k_gw_count(size_t nops, const uint8_t *is_write, uint32_t *bc,
                                                          const uint32_t *observed, uint32_t ntxn, uint32_t *bad)
 {
@@ -106,11 +132,15 @@ __global__ __launch_bounds__(kGwThreads) void k_gw_count(size_t nops, const uint
 // count pass's shape, issued every key / txn load over 64 lines: 0.57 ms per
 // 100M ops.)  bad != null: the txns' check -- bit 0 a txn >= ntxn, bit 1 a
 // txn below its predecessor's -- on the txn words it loads anyway.
+// vp: the block's writers' OR and AND of key and txn (vp[4 b + 0..3]), which
+// k_vary_reduce turns into the writer rows' varying bits (no pass over the
+// gathered rows for them)
 __global__ __launch_bounds__(kGwThreads) void k_gw_place(size_t nops, const uint32_t *txn, const uint64_t *key,
                                                          const uint8_t *is_write, const uint32_t *boff,
                                                          uint32_t *gid, uint64_t *words, size_t stride,
-                                                         uint32_t ntxn, uint32_t *bad)
+                                                         uint32_t ntxn, uint32_t *bad, uint64_t *vp)
 {
+    __shared__ uint64_t vred[kGwThreads / 64][4];
     constexpr int kSeg = kGwItems * (kGwThreads / 64);
     static_assert(kSeg == 64, "one wave scans the segments");
     __shared__ uint64_t sk[kGwThreads * kGwItems], st[kGwThreads * kGwItems];
@@ -149,7 +179,26 @@ __global__ __launch_bounds__(kGwThreads) void k_gw_place(size_t nops, const uint
         const uint64_t any = __ballot(b != 0);
         if (any && b) atomicOr(bad, b);
     }
+    uint64_t ko = 0, ka = ~0ull, to = 0, ta = ~0ull;
+#pragma unroll
+    for (int k = 0; k < kGwItems; ++k) {
+        if (!wv8[k]) continue;
+        ko |= kv[k], ka &= kv[k], to |= tv[k], ta &= tv[k];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        ko |= __shfl_xor(ko, o, 64), ka &= __shfl_xor(ka, o, 64);
+        to |= __shfl_xor(to, o, 64), ta &= __shfl_xor(ta, o, 64);
+    }
+    if (lane == 0) vred[wv][0] = ko, vred[wv][1] = ka, vred[wv][2] = to, vred[wv][3] = ta;
     __syncthreads();
+    if (vp && threadIdx.x < 4) {
+        const int q = threadIdx.x;
+        uint64_t v = vred[0][q];
+#pragma unroll
+        for (int w = 1; w < kGwThreads / 64; ++w) v = (q & 1) ? (v & vred[w][q]) : (v | vred[w][q]);
+        vp[4 * (size_t)blockIdx.x + q] = v;
+    }
     if (wv == 0) {
         const uint32_t v = segc[lane];
         uint32_t inc = v;
@@ -412,7 +461,10 @@ __device__ __forceinline__ uint64_t bucket_start(const PairPack &pp, uint64_t b)
     return pp.base + (pp.shift >= 64 ? 0 : b << pp.shift);
 }
 
-// LW threads per bucket, one 8-byte word each: coalesced lines
+// LW threads per bucket, one 8-byte word each: coalesced lines.  (The bucket
+// bounds searched here instead of by k_pair_dir -- lane 0 of each bucket,
+// shuffled to the rest -- measured 1.07 ms against 0.28 ms for the two
+// passes, r06aa: 8 searches per wave instead of 64.)
 template <int LW>
 __global__ void k_pair_table(uint32_t nu, const uint64_t *pk, const uint32_t *dir, uint64_t nb, PairPack pp,
                              uint64_t *tab)
@@ -421,7 +473,8 @@ __global__ void k_pair_table(uint32_t nu, const uint64_t *pk, const uint32_t *di
     const uint64_t b = id / LW;
     const int w = (int)(id % LW);
     if (b >= nb) return;
-    const uint32_t lo = dir[b], hi = dir[b + 1], n = hi - lo;
+    const uint32_t lo = dir[b], hi = dir[b + 1];
+    const uint32_t n = hi - lo;
     uint64_t v;
     if (w == 0) {
         v = ((uint64_t)lo << 32) | ((uint64_t)(hi < nu) << 31) | (uint64_t)min(n, 0x7FFFFFFFu);
@@ -952,6 +1005,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     static const bool rp_env = getenv("HSC_GRAPH_RP") != nullptr && atoi(getenv("HSC_GRAPH_RP")) != 0;
     const bool obs_in_count = rp_env;
     CK(g.flags.ensure(4 * (gwb + 2)));
+    CK(g.gvary.ensure(32 * (gwb + 1)));
     CK(g.scratch.ensure(std::max(scan_scratch_bytes(gwb + 1), (size_t)1024)));
     uint32_t *bc = g.flags.as<uint32_t>();
     CK(hipMemsetAsync(bc + gwb, 0, 8, s));  // the total slot and the check's bits
@@ -962,10 +1016,14 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     if (gwb)
         k_gw_place<<<(unsigned)gwb, kGwThreads, 0, s>>>(nops, in.txn, in.key, in.is_write, bc, g.wg.as<uint32_t>(),
                                                          g.ww.as<uint64_t>(), wcap, in.ntxn,
-                                                         in.check ? bc + gwb + 1 : nullptr);
+                                                         in.check ? bc + gwb + 1 : nullptr, g.gvary.as<uint64_t>());
+    uint64_t *dvary = g.gvary.as<uint64_t>() + 4 * gwb;
+    k_vary_reduce<<<1, 1024, 0, s>>>((uint32_t)gwb, g.gvary.as<uint64_t>(), dvary);
     CK(hipGetLastError());
     uint32_t nwb[2] = {0, 0};  // writers, the check's bits
+    uint64_t hvary[3] = {0, 0, 0};  // the writers' varying bits: key, txn, gid
     CK(hipMemcpyAsync(nwb, bc + gwb, 8, hipMemcpyDeviceToHost, s));
+    CK(hipMemcpyAsync(hvary, dvary, sizeof hvary, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
     const uint32_t nw = nwb[0];
     g.bad = in.check ? nwb[1] : 0;
@@ -983,7 +1041,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     PackPlan P{};
     bool packed = false;
     if (nw) {
-        CK(vary_mask_rows(2, nw, g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), wcap, g.count.p, vary, s));
+        for (int j = 0; j < 3; ++j) vary[j] = hvary[j];
         packed = packed_plan(2, nw, vary, &P, false);
         // writers gathered in op order from txn-ordered ops are ordered by
         // txn already: the stable passes need only the key bits (config 4:
@@ -1082,8 +1140,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         }
         pp.shift = 0;  // (last - base) >> shift < 2^D
         while (pp.shift < 64 && ((pp.last - pp.base) >> pp.shift) >= ((uint64_t)1 << pp.D)) ++pp.shift;
-        k_pair_dir<<<blocks(((size_t)1 << pp.D) + 2), 256, 0, s>>>(nu, pkv, pp,
-                                                                 g.pdir.as<uint32_t>());
+        k_pair_dir<<<blocks(((size_t)1 << pp.D) + 2), 256, 0, s>>>(nu, pkv, pp, g.pdir.as<uint32_t>());
         // the partitioned read search: measured slower on config 4 (r06c trace:
         // count 3.0 + scatter 3.2 + join 1.0 ms against 3.5 ms for the
         // directory search -- the count's per-read global atomics on 16k

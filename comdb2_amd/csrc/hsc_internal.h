@@ -498,6 +498,7 @@ struct GraphBufs {
                                    // reads it after the build), or null
     DBuf cover_bits;             // graph_cut: the cover as a bitmap
     DBuf cover_list;             // graph_cut: the covered txns (the op-range cut)
+    DBuf gvary;                  // k_gw_place's per-block OR / AND of the writers' key and txn
     // raw build over txn-sorted ops in the op-slot layout (ww rows [0, op_at),
     // op i's rows op_at + 2i, + 1, staged rows from x_at): graph_cut given the
     // ops' txn array visits the covered txns' ops only
@@ -510,7 +511,7 @@ struct GraphBufs {
                        &in_src, &in_dst, &out_off, &in_off, &scc, &active, &color, &mark,
                        &front, &front2, &h_txn, &h_key, &h_isw, &h_obs, &diff, &cut,
                        &cut_id, &txn_of, &x_rows, &x_type, &x_map, &pk, &pdir, &ptab, &rp_cnt,
-                       &rp_items, &cover_bits, &cover_list};
+                       &rp_items, &cover_bits, &cover_list, &gvary};
         for (DBuf *b : all) b->release();
     }
 };
