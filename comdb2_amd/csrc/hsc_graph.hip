@@ -69,7 +69,8 @@ __device__ __forceinline__ uint32_t gw_bits(size_t nops, const uint8_t *is_write
 // builds whose edge pass does not check them itself; the txns' range and order
 // are k_gw_place's)
 // out[0] / out[1] = the varying bits of the writers' key / txn, out[2] = 0
-// (their gid): OR & ~AND over k_gw_place's block partials
+// (their gid): OR & ~AND over k_gw_place's block partials; out[3] / out[4]
+// the ANDs
 __global__ __launch_bounds__(1024) void k_vary_reduce(uint32_t nb, const uint64_t *vp, uint64_t *out)
 {
     __shared__ uint64_t red[16][4];
@@ -91,6 +92,8 @@ __global__ __launch_bounds__(1024) void k_vary_reduce(uint32_t nb, const uint64_
         out[0] = ko & ~ka;
         out[1] = to & ~ta;
         out[2] = 0;
+        out[3] = ka;  // (their constant bits: AND & ~varying)
+        out[4] = ta;
     }
 }
 
@@ -128,9 +131,11 @@ __global__ __launch_bounds__(kGwThreads) void k_gw_count(size_t nops, const uint
 // Coalesced: round k of wave v takes the 64 ops base + 256 k + 64 v + lane
 // -- 64 segments in op order, each one ballot -- so a writer's place in the
 // block is its segment's exclusive count (one wave scans the 64) plus the
-// writers before it in the ballot.  (A thread taking 16 consecutive ops, the
-// count pass's shape, issued every key / txn load over 64 lines: 0.57 ms per
-// 100M ops.)  bad != null: the txns' check -- bit 0 a txn >= ntxn, bit 1 a
+// writers before it in the ballot; a segment's writers store as one
+// contiguous run straight from the lanes (no LDS staging: the 64 KB of it held
+// the kernel to 2 workgroups per CU).  (A thread taking 16 consecutive ops,
+// the count pass's shape, issued every key / txn load over 64 lines: 0.57 ms
+// per 100M ops.)  bad != null: the txns' check -- bit 0 a txn >= ntxn, bit 1 a
 // txn below its predecessor's -- on the txn words it loads anyway.
 // vp: the block's writers' OR and AND of key and txn (vp[4 b + 0..3]), which
 // k_vary_reduce turns into the writer rows' varying bits (no pass over the
@@ -143,7 +148,6 @@ __global__ __launch_bounds__(kGwThreads) void k_gw_place(size_t nops, const uint
     __shared__ uint64_t vred[kGwThreads / 64][4];
     constexpr int kSeg = kGwItems * (kGwThreads / 64);
     static_assert(kSeg == 64, "one wave scans the segments");
-    __shared__ uint64_t sk[kGwThreads * kGwItems], st[kGwThreads * kGwItems];
     __shared__ uint32_t segc[kSeg];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const size_t base = (size_t)blockIdx.x * (kGwThreads * kGwItems);
@@ -211,20 +215,14 @@ __global__ __launch_bounds__(kGwThreads) void k_gw_place(size_t nops, const uint
     }
     __syncthreads();
     const uint64_t lt = (1ull << lane) - 1;
+    const size_t b0 = boff[blockIdx.x];
 #pragma unroll
     for (int k = 0; k < kGwItems; ++k) {
         if (!((m[k] >> lane) & 1ull)) continue;
-        const uint32_t p = segc[k * 4 + wv] + (uint32_t)__popcll(m[k] & lt);
-        sk[p] = kv[k];
-        st[p] = tv[k];
-    }
-    __syncthreads();
-    const size_t b0 = boff[blockIdx.x];
-    const uint32_t tot = boff[blockIdx.x + 1] - boff[blockIdx.x];
-    for (uint32_t j = threadIdx.x; j < tot; j += kGwThreads) {
-        words[b0 + j] = sk[j];
-        words[stride + b0 + j] = st[j];
-        gid[b0 + j] = 0;
+        const size_t p = b0 + segc[k * 4 + wv] + (uint32_t)__popcll(m[k] & lt);
+        words[p] = kv[k];
+        words[stride + p] = tv[k];
+        gid[p] = 0;
     }
 }
 
@@ -330,6 +328,54 @@ __device__ __forceinline__ uint64_t pair_bucket(const PairPack &pp, uint64_t x)
 
 __device__ __forceinline__ uint64_t pair_key(const PairPack &pp, uint64_t kp) { return pp.tb >= 64 ? 0 : kp << pp.tb; }
 
+// the first writer of key kp (compressed) with txn > ob, ob having bits
+// outside the writers' txn bits (so not compressible): a search of pk on the
+// expanded txns (compress / expand keep the order of values sharing the
+// constant bits); the rw row r -> it, or ~0
+__device__ __forceinline__ uint64_t pk_rw_slow(uint32_t nu, const uint64_t *pk, const PairPack &pp,
+                                               const uint64_t (&tmv)[6], uint64_t kp, uint32_t ob, uint32_t r)
+{
+    const uint64_t tmask = pp.tb >= 64 ? ~0ull : (1ull << pp.tb) - 1;
+    uint32_t lo = 0, hi = nu;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint64_t v = pk[mid], kv = pp.tb >= 64 ? 0 : v >> pp.tb;
+        if (kv < kp || (kv == kp && (bits_expand(v & tmask, pp.tm, tmv) | pp.tc) <= ob))
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    if (lo >= nu) return ~0ull;
+    const uint64_t v = pk[lo];
+    if ((pp.tb >= 64 ? 0 : v >> pp.tb) != kp) return ~0ull;
+    const uint32_t wt = (uint32_t)(bits_expand(v & tmask, pp.tm, tmv) | pp.tc);
+    return wt != r ? ((uint64_t)r << 32) | wt : ~0ull;
+}
+
+// k_edges_ww over the packed distinct writers
+__global__ void k_edges_ww_pk(uint32_t nu, const uint64_t *pk, PairPack pp, uint64_t *ew, uint64_t *et,
+                              uint32_t *eg)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nu) return;
+    uint64_t e = ~0ull;
+    if (i + 1 < nu) {
+        const uint64_t a = pk[i], b = pk[i + 1];
+        if (pp.tb >= 64 || (a >> pp.tb) == (b >> pp.tb)) {
+            uint64_t tm[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) tm[q] = pp.tmv[q];
+            const uint64_t tmask = pp.tb >= 64 ? ~0ull : (1ull << pp.tb) - 1;
+            e = ((bits_expand(a & tmask, pp.tm, tm) | pp.tc) << 32) | (bits_expand(b & tmask, pp.tm, tm) | pp.tc);
+        }
+    }
+    ew[i] = e;
+    if (et) {
+        et[i] = kDepWW;
+        eg[i] = 0;
+    }
+}
+
 __global__ void k_pair_keys(uint32_t nu, const uint64_t *wkey, const uint64_t *wtxn, PairPack pp, uint64_t *pk)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -413,16 +459,11 @@ __global__ void k_edges_reads_pk(size_t nops, const uint32_t *txn, const uint64_
                 }
                 found = true;
             }
-            if (!found) {  // an observed txn outside the writers' bits: the row search
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    const uint64_t mk = wkey[mid], mt = wtxn[mid];
-                    if (mk < k || (mk == k && mt <= ob))
-                        lo = mid + 1;
-                    else
-                        hi = mid;
-                }
-                if (lo < nu && wkey[lo] == k && wtxn[lo] != r) rw = ((uint64_t)r << 32) | wtxn[lo];
+            if (!found) {  // an observed txn outside the writers' bits
+                uint64_t km[6], tm[6];
+#pragma unroll
+                for (int q = 0; q < 6; ++q) km[q] = pp.kmv[q], tm[q] = pp.tmv[q];
+                rw = pk_rw_slow(nu, pk, pp, tm, bits_compress(k, pp.km, km), ob, r);
             }
         }
     }
@@ -559,17 +600,8 @@ __global__ void k_edges_reads_pt(size_t nops, const uint32_t *txn, const uint64_
                         if (wt != r) rw = ((uint64_t)r << 32) | wt;
                     }
                 }
-            } else {  // an observed txn outside the writers' bits: the row search
-                uint32_t lo = 0, hi = nu;
-                while (lo < hi) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    const uint64_t mk = wkey[mid], mt = wtxn[mid];
-                    if (mk < k || (mk == k && mt <= ob))
-                        lo = mid + 1;
-                    else
-                        hi = mid;
-                }
-                if (lo < nu && wkey[lo] == k && wtxn[lo] != r) rw = ((uint64_t)r << 32) | wtxn[lo];
+            } else {  // an observed txn outside the writers' bits
+                rw = pk_rw_slow(nu, pk, pp, tm, bits_compress(k, pp.km, km), ob, r);
             }
         }
     }
@@ -1005,7 +1037,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     static const bool rp_env = getenv("HSC_GRAPH_RP") != nullptr && atoi(getenv("HSC_GRAPH_RP")) != 0;
     const bool obs_in_count = rp_env;
     CK(g.flags.ensure(4 * (gwb + 2)));
-    CK(g.gvary.ensure(32 * (gwb + 1)));
+    CK(g.gvary.ensure(32 * (gwb + 2)));
     CK(g.scratch.ensure(std::max(scan_scratch_bytes(gwb + 1), (size_t)1024)));
     uint32_t *bc = g.flags.as<uint32_t>();
     CK(hipMemsetAsync(bc + gwb, 0, 8, s));  // the total slot and the check's bits
@@ -1021,7 +1053,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     k_vary_reduce<<<1, 1024, 0, s>>>((uint32_t)gwb, g.gvary.as<uint64_t>(), dvary);
     CK(hipGetLastError());
     uint32_t nwb[2] = {0, 0};  // writers, the check's bits
-    uint64_t hvary[3] = {0, 0, 0};  // the writers' varying bits: key, txn, gid
+    uint64_t hvary[5] = {0, 0, 0, 0, 0};  // the writers' varying bits: key, txn, gid; key / txn ANDs
     CK(hipMemcpyAsync(nwb, bc + gwb, 8, hipMemcpyDeviceToHost, s));
     CK(hipMemcpyAsync(hvary, dvary, sizeof hvary, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
@@ -1051,10 +1083,14 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     }
     DBuf *dw = &g.ww2;
     uint64_t *lsn_d = nullptr;  // packed: the distinct packed keys themselves (no LSN input, I = 0)
+    // the packed build reads its writers as the packed keys alone (the ww
+    // rows, the searches and their fallbacks): the distinct rows are written
+    // for the partitioned search's A/B only
+    const bool writer_rows = !packed || rp_env;
     if (packed) {
         CK(packed_sort_dedupe(P, nw, g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), nullptr, wcap,
                               g.wl.as<uint64_t>(), g.wl2.as<uint64_t>(), nullptr, nullptr, nullptr, 0,
-                              g.wg2.as<uint32_t>(), g.ww2.as<uint64_t>(), wcap, &lsn_d,
+                              writer_rows ? g.wg2.as<uint32_t>() : nullptr, g.ww2.as<uint64_t>(), wcap, &lsn_d,
                               g.count.as<uint32_t>(), g.scratch.p, g.scratch.bytes, s));
     } else {
         bool alt = false;
@@ -1097,10 +1133,11 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     CK(g.eg2.ensure(4 * ecap));
     uint64_t *et = full || in.n_extra ? g.et.as<uint64_t>() : nullptr;  // raw: rows only
     uint32_t *eg = full || in.n_extra ? g.eg.as<uint32_t>() : nullptr;
-    if (nu) k_edges_ww<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, g.ew.as<uint64_t>(), et, eg);
+    if (nu && !(packed && nops)) k_edges_ww<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, g.ew.as<uint64_t>(), et, eg);
     if (nops && packed && nu) {
         PairPack pp{};
-        const uint64_t r0[2] = {meta[1], meta[2]};
+        // (constant bits: any writer's, the ANDs of the place pass)
+        const uint64_t r0[2] = {hvary[3], hvary[4]};
         pp.km = vary[0], pp.tm = vary[1];
         pp.kc = r0[0] & ~pp.km, pp.tc = r0[1] & ~pp.tm;
         compress_moves(pp.km, pp.kmv);
@@ -1129,15 +1166,9 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         // the sort's unpack left the distinct packed keys -- compress(key) <<
         // tb | compress(txn), the same words (no gid limb: gid is 0) -- in lsn_d
         const uint64_t *pkv = lsn_d;
+        if (!pkv) return hipErrorInvalidValue;  // (a packed sort leaves them)
         pp.base = meta[3], pp.last = meta[4];
-        if (!pkv) {
-            CK(g.pk.ensure(8 * (size_t)nu));
-            k_pair_keys<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, pp, g.pk.as<uint64_t>());
-            pkv = g.pk.as<uint64_t>();
-            CK(hipMemcpyAsync(&pp.base, pkv, 8, hipMemcpyDeviceToHost, s));
-            CK(hipMemcpyAsync(&pp.last, pkv + nu - 1, 8, hipMemcpyDeviceToHost, s));
-            CK(hipStreamSynchronize(s));
-        }
+        k_edges_ww_pk<<<blocks(nu), 256, 0, s>>>(nu, pkv, pp, g.ew.as<uint64_t>(), et, eg);
         pp.shift = 0;  // (last - base) >> shift < 2^D
         while (pp.shift < 64 && ((pp.last - pp.base) >> pp.shift) >= ((uint64_t)1 << pp.D)) ++pp.shift;
         k_pair_dir<<<blocks(((size_t)1 << pp.D) + 2), 256, 0, s>>>(nu, pkv, pp, g.pdir.as<uint32_t>());

@@ -362,11 +362,13 @@ __global__ __launch_bounds__(kUdThreads) void k_pk_unpack_dd(
         const uint32_t p = pos[j];
         if (p != 0xFFFFFFFFu) {
             const size_t d = (size_t)b0 + p;
-            gid_d[d] = (uint32_t)limb[W];
+            if (gid_d) {  // (null: the distinct packed keys only)
+                gid_d[d] = (uint32_t)limb[W];
 #pragma unroll
-            for (int q = 0; q < kPackMaxWords; ++q) {
-                if (q >= W) break;
-                words_d[(size_t)q * stride_d + d] = limb[q];
+                for (int q = 0; q < kPackMaxWords; ++q) {
+                    if (q >= W) break;
+                    words_d[(size_t)q * stride_d + d] = limb[q];
+                }
             }
             lsn_d[d] = lv;
         }

@@ -181,7 +181,7 @@ size_t packed_scratch_bytes(size_t n);
 // (gid_o, words_o, lsn_o) (gid_o null: not written; lsn null: LSNs 0, or with no index bits the
 // packed keys themselves), the
 // distinct rows to (gid_d, words_d) -- which may
-// be the input gid / words -- and to *lsn_d = whichever of k0 / k1 the sorted
+// be the input gid / words; gid_d null: not written -- and to *lsn_d = whichever of k0 / k1 the sorted
 // keys did not end in; d_count[0] = distinct rows
 hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, const uint64_t *words,
                               const uint64_t *lsn, size_t stride, uint64_t *k0, uint64_t *k1,
