@@ -226,7 +226,6 @@ __global__ __launch_bounds__(kGwThreads) void k_gw_place(size_t nops, const uint
     }
 }
 
-
 // a backward edge a -> b (a > b) covers [b, a] (graph_cover's k_back_diff,
 // done while a raw build emits the row: one pass over the raw rows less)
 __device__ __forceinline__ void back_row(uint32_t *diff, uint64_t row)
@@ -237,6 +236,35 @@ __device__ __forceinline__ void back_row(uint32_t *diff, uint64_t row)
         atomicAdd(&diff[b], 1u);
         atomicAdd(&diff[a + 1], 0xFFFFFFFFu);
     }
+}
+
+// Where a raw build's backward edges go: the interval diffs (diff), or a
+// list of the rows themselves (list: config 4 has a few thousand among 95M
+// edges -- the cover is then their intervals marked in place of a scan of
+// ntxn diffs; past cap only counted, and graph_cover takes the diffs)
+struct BackSink {
+    uint32_t *diff;
+    uint64_t *list;
+    uint32_t *cnt;
+    uint32_t cap;
+};
+
+// (every active lane calls it: one wave-aggregated atomic for the list)
+__device__ __forceinline__ void back_push(const BackSink &bs, uint64_t row)
+{
+    if (!bs.list) {
+        back_row(bs.diff, row);
+        return;
+    }
+    const bool is = row != ~0ull && (uint32_t)(row >> 32) > (uint32_t)row;
+    const uint64_t m = __ballot(is);
+    if (!m) return;
+    const int lane = threadIdx.x & 63, first = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(bs.cnt, (uint32_t)__popcll(m));
+    base = __shfl(base, first, 64);
+    const uint32_t slot = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    if (is && slot < bs.cap) bs.list[slot] = row;
 }
 
 // Edge rows: word = src << 32 | dst, payload = type; invalid = ~0.
@@ -416,7 +444,7 @@ __global__ void k_edges_reads_pk(size_t nops, const uint32_t *txn, const uint64_
                                  const uint8_t *is_write, const uint32_t *observed, uint32_t nu,
                                  const uint64_t *wkey, const uint64_t *wtxn, const uint64_t *pk,
                                  const uint32_t *dir, PairPack pp, uint64_t *ew, uint64_t *et,
-                                 uint32_t *eg, int skip_rw, uint32_t *diff, uint32_t chk_n,
+                                 uint32_t *eg, int skip_rw, BackSink diff, uint32_t chk_n,
                                  uint32_t *bad)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -470,8 +498,8 @@ __global__ void k_edges_reads_pk(size_t nops, const uint32_t *txn, const uint64_
     const size_t s = (size_t)nu + 2 * i;
     ew[s] = wr;
     ew[s + 1] = rw;
-    back_row(diff, wr);
-    back_row(diff, rw);
+    back_push(diff, wr);
+    back_push(diff, rw);
     if (et) {
         et[s] = kDepWR;
         eg[s] = 0;
@@ -536,7 +564,7 @@ __global__ void k_edges_reads_pt(size_t nops, const uint32_t *txn, const uint64_
                                  const uint8_t *is_write, const uint32_t *observed, uint32_t nu,
                                  const uint64_t *wkey, const uint64_t *wtxn, const uint64_t *pk,
                                  const uint64_t *tab, PairPack pp, uint64_t *ew, uint64_t *et,
-                                 uint32_t *eg, int skip_rw, uint32_t *diff, uint32_t chk_n,
+                                 uint32_t *eg, int skip_rw, BackSink diff, uint32_t chk_n,
                                  uint32_t *bad)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -608,8 +636,8 @@ __global__ void k_edges_reads_pt(size_t nops, const uint32_t *txn, const uint64_
     const size_t s = (size_t)nu + 2 * i;
     ew[s] = wr;
     ew[s + 1] = rw;
-    back_row(diff, wr);
-    back_row(diff, rw);
+    back_push(diff, wr);
+    back_push(diff, rw);
     if (et) {
         et[s] = kDepWR;
         eg[s] = 0;
@@ -1004,7 +1032,8 @@ __global__ void k_graph_meta(const uint32_t *count, const uint64_t *wkey, const 
                              uint64_t *out, uint32_t *ebad)
 {
     if (threadIdx.x != 0) return;
-    *ebad = 0;
+    ebad[0] = 0;
+    ebad[-1] = 0;  // (the backward-row list's count)
     const uint32_t nu = count[0];
     out[0] = nu;
     out[1] = nu ? wkey[0] : 0;
@@ -1115,6 +1144,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     uint32_t *ebad = g.count.as<uint32_t>() + 30;
     const uint32_t chk_n = in.check && !obs_in_count ? std::max<uint32_t>(in.ntxn, 1) : 0;
     g.edge_bad = chk_n ? ebad : nullptr;
+    g.post = g.count.as<uint32_t>() + 29;  // [0] backward rows listed, [1] the edge check's bits
     k_graph_meta<<<1, 64, 0, s>>>(g.count.as<uint32_t>(), wkey, wtxn, packed ? lsn_d : nullptr,
                                   g.count.as<uint64_t>() + 8, ebad);
     CK(hipMemcpyAsync(meta, g.count.as<uint64_t>() + 8, sizeof meta, hipMemcpyDeviceToHost, s));
@@ -1124,7 +1154,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     const size_t ne_cap = (size_t)nu + 2 * nops + in.n_extra;
     const size_t ecap = std::max<size_t>(64, (ne_cap + 63) & ~(size_t)63);
     size_t rw_rows = 0;
-    bool slot_layout = false, diff_done = false;
+    bool slot_layout = false, diff_done = false, back_listed = false;
     CK(g.ew.ensure(8 * ecap));
     CK(g.et.ensure(8 * ecap));
     CK(g.eg.ensure(4 * ecap));
@@ -1182,11 +1212,18 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         // raw builds (the sharded SCC's): the cover's backward-edge diffs as
         // the rows are emitted (ww rows are forward: txns ascend inside a key)
         uint32_t *diff = nullptr;
+        BackSink sink{nullptr, nullptr, nullptr, 0};
         if (!full && !in.n_extra && in.ntxn) {
-            CK(g.diff.ensure(4 * ((size_t)in.ntxn + 2)));
-            CK(hipMemsetAsync(g.diff.p, 0, 4 * ((size_t)in.ntxn + 2), s));
-            diff = g.diff.as<uint32_t>();
-            diff_done = true;
+            if (rp) {  // (the partitioned search's kernels: the diffs)
+                CK(g.diff.ensure(4 * ((size_t)in.ntxn + 2)));
+                CK(hipMemsetAsync(g.diff.p, 0, 4 * ((size_t)in.ntxn + 2), s));
+                diff = g.diff.as<uint32_t>();
+                diff_done = true;
+            } else {  // the rows themselves (the counter: g.count's u32 29, cleared by k_graph_meta)
+                CK(g.back.ensure(8 * (size_t)kBackCap));
+                sink = BackSink{nullptr, g.back.as<uint64_t>(), g.count.as<uint32_t>() + 29, kBackCap};
+                back_listed = true;
+            }
         }
         if (rp) {
             RpArgs a{};
@@ -1221,7 +1258,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
                                                        g.ptab.as<uint64_t>());                             \
     k_edges_reads_pt<LW_><<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu, \
                                                        wkey, wtxn, pkv, g.ptab.as<uint64_t>(), pp,          \
-                                                       g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0, diff, chk_n, \
+                                                       g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0, sink, chk_n, \
                                                        ebad)
             if (kLine == 16) {
                 HSC_PT(16);
@@ -1233,7 +1270,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
             k_edges_reads_pk<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu,
                                                           wkey, wtxn, pkv, g.pdir.as<uint32_t>(),
                                                           pp, g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0,
-                                                          diff, chk_n, ebad);
+                                                          sink, chk_n, ebad);
         }
     } else if (nops) {
         k_edges_reads<<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed,
@@ -1257,6 +1294,8 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     g.op_cut = !full && !slot_layout && txn_sorted;
     g.op_at = nu, g.op_n = nops, g.x_at = ne_hist, g.x_n = in.n_extra;
     g.diff_nn = diff_done ? in.ntxn : 0;  // graph_cover: the diffs are there already
+    g.back_listed = back_listed;          // graph_cover: the backward rows (count: graph_build_timed)
+    g.back_n = 0;
     g.cover_nn = in.ntxn;
     if (!full) {  // raw edge rows only (duplicates, ~0 holes): enough for cover / cut
         g.ne = 0;
@@ -1487,22 +1526,39 @@ hipError_t graph_type_counts(GraphBufs &g, uint64_t out[3], hipStream_t s)
     return hipStreamSynchronize(s);
 }
 
-__global__ void k_cover_u32(uint32_t nn, const uint8_t *cover, uint32_t *id)
+// The cut's node ids from the cover as a bitmap: word w's bits and their
+// exclusive count wc[w] (a scan of nn / 64 words, not of nn) -- covered v is
+// cut node wc[v / 64] + (its bit's rank in its word)
+__global__ void k_cover_words(uint32_t nn, const uint8_t *cover, uint64_t *bits, uint32_t *wc)
 {
     const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v < nn) id[v] = cover[v] != 0;
+    const uint64_t m = __ballot(v < nn && cover[v] != 0);
+    if ((threadIdx.x & 63) == 0 && v < nn) bits[v >> 6] = m, wc[v >> 6] = (uint32_t)__popcll(m);
 }
 
-// id = exclusive scan of the cover: covered node v is node id[v] of the cut
-__global__ void k_txn_of(uint32_t nn, const uint8_t *cover, const uint32_t *id, uint32_t *txn_of)
+__device__ __forceinline__ bool cover_has(const uint64_t *bits, uint32_t v) { return (bits[v >> 6] >> (v & 63)) & 1; }
+
+__device__ __forceinline__ uint32_t cover_id(const uint64_t *bits, const uint32_t *wc, uint32_t v)
 {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v < nn && cover[v]) txn_of[id[v]] = v;
+    return wc[v >> 6] + (uint32_t)__popcll(bits[v >> 6] & ((1ull << (v & 63)) - 1));
+}
+
+// txn_of[cut id] = txn, a thread per bitmap word
+__global__ void k_txn_of_w(uint32_t nw, const uint64_t *bits, const uint32_t *wc, uint32_t *txn_of)
+{
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nw) return;
+    uint64_t m = bits[w];
+    uint32_t id = wc[w];
+    while (m) {
+        txn_of[id++] = w * 64 + (uint32_t)(__ffsll((unsigned long long)m) - 1);
+        m &= m - 1;
+    }
 }
 
 // cut rows (txn ids; ~0 = padding) -> edge rows over cut node ids
-__global__ void k_relabel(size_t m, uint32_t nn, const uint64_t *rows, const uint8_t *cover,
-                          const uint32_t *id, uint64_t *ew, uint64_t *et, uint32_t *eg,
+__global__ void k_relabel(size_t m, uint32_t nn, const uint64_t *rows, const uint64_t *bits,
+                          const uint32_t *wc, uint64_t *ew, uint64_t *et, uint32_t *eg,
                           uint32_t *bad)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1511,8 +1567,8 @@ __global__ void k_relabel(size_t m, uint32_t nn, const uint64_t *rows, const uin
     uint64_t e = ~0ull;
     if (r != ~0ull) {
         const uint32_t a = (uint32_t)(r >> 32), b = (uint32_t)r;
-        if (a < nn && b < nn && cover[a] && cover[b] && a != b)
-            e = ((uint64_t)id[a] << 32) | id[b];
+        if (a < nn && b < nn && cover_has(bits, a) && cover_has(bits, b) && a != b)
+            e = ((uint64_t)cover_id(bits, wc, a) << 32) | cover_id(bits, wc, b);
         else
             atomicOr(bad, 1u);
     }
@@ -1521,17 +1577,35 @@ __global__ void k_relabel(size_t m, uint32_t nn, const uint64_t *rows, const uin
     eg[i] = 0;
 }
 
-__global__ void k_scc_out(uint32_t nn, const uint8_t *cover, const uint32_t *id,
-                          const uint32_t *sub_scc, const uint32_t *txn_of, uint32_t *scc)
+__global__ void k_scc_out(uint32_t nn, const uint64_t *bits, const uint32_t *wc, const uint32_t *sub_scc,
+                          const uint32_t *txn_of, uint32_t *scc)
 {
     const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v < nn) scc[v] = cover[v] ? txn_of[sub_scc[id[v]]] : v;
+    if (v < nn) scc[v] = cover_has(bits, v) ? txn_of[sub_scc[cover_id(bits, wc, v)]] : v;
+}
+
+// one workgroup per listed backward row: its interval [b, a] marked covered
+__global__ void k_mark_intervals(const uint64_t *list, uint32_t n, uint8_t *cover)
+{
+    for (uint32_t j = blockIdx.x; j < n; j += gridDim.x) {
+        const uint64_t r = list[j];
+        const uint32_t a = (uint32_t)(r >> 32), b = (uint32_t)r;
+        for (uint32_t v = b + threadIdx.x; v <= a; v += blockDim.x) cover[v] = 1;
+    }
 }
 
 hipError_t graph_cover(GraphBufs &g, uint32_t nn, uint8_t *cover, hipStream_t s)
 {
     hipError_t e = hipSuccess;
     if (nn == 0) return hipSuccess;
+    if (g.raw && g.back_listed && g.cover_nn == nn && g.back_n <= kBackCap) {
+        // the listed backward rows' intervals (no diffs, no scan of nn)
+        if ((e = hipMemsetAsync(cover, 0, nn, s)) != hipSuccess) return e;
+        if (g.back_n)
+            k_mark_intervals<<<std::min<uint32_t>(g.back_n, 65535), 256, 0, s>>>(g.back.as<uint64_t>(), g.back_n,
+                                                                               cover);
+        return hipGetLastError();
+    }
     DBuf &diff = g.diff, &scratch = g.scratch;
     if ((e = diff.ensure(4 * ((size_t)nn + 2))) != hipSuccess) return e;
     if ((e = scratch.ensure(std::max(scan_scratch_bytes((size_t)nn + 1), (size_t)1024))) != hipSuccess)
@@ -1584,6 +1658,7 @@ __global__ void k_cut_append(EdgeSet es, const uint64_t *cover, uint64_t *rows, 
 }
 
 constexpr uint32_t kCutFastCap = 1u << 16;
+
 constexpr uint32_t kCoverListCap = 1u << 16;
 
 // the cover as a bitmap and as a list of its txns (wave-aggregated appends;
@@ -1821,21 +1896,24 @@ hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *row
     *rounds = *iterations = 0;
     *n_cut = 0;
     if (nn == 0) return hipSuccess;
-    // cut node ids
-    CK(g.cut_id.ensure(4 * ((size_t)nn + 64)));
-    CK(g.txn_of.ensure(4 * ((size_t)nn + 64)));
-    CK(g.scratch.ensure(std::max(scan_scratch_bytes((size_t)nn + 1), (size_t)1024)));
+    // cut node ids: the cover's bitmap words and their scan
+    const uint32_t nwd = (nn + 63) / 64;
+    CK(g.cut_id.ensure(4 * ((size_t)nwd + 64)));
+    CK(g.cover_bits.ensure(8 * ((size_t)nwd + 1)));
+    CK(g.scratch.ensure(std::max(scan_scratch_bytes((size_t)nwd + 1), (size_t)1024)));
     CK(g.count.ensure(64));
-    uint32_t *id = g.cut_id.as<uint32_t>();
-    k_cover_u32<<<blocks(nn), 256, 0, s>>>(nn, cover, id);
-    CK(hipMemsetAsync(id + nn, 0, 4, s));
-    CK(scan_exclusive_u32(id, (size_t)nn + 1, g.scratch.as<uint32_t>(), s));
+    uint32_t *wc = g.cut_id.as<uint32_t>();
+    uint64_t *bits = g.cover_bits.as<uint64_t>();
+    k_cover_words<<<blocks(nn), 256, 0, s>>>(nn, cover, bits, wc);
+    CK(hipMemsetAsync(wc + nwd, 0, 4, s));
+    CK(scan_exclusive_u32(wc, (size_t)nwd + 1, g.scratch.as<uint32_t>(), s));
     uint32_t nc = 0;
-    CK(hipMemcpyAsync(&nc, id + nn, 4, hipMemcpyDeviceToHost, s));
+    CK(hipMemcpyAsync(&nc, wc + nwd, 4, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
     *n_cut = nc;
+    CK(g.txn_of.ensure(4 * ((size_t)nc + 64)));
     uint32_t *txn_of = g.txn_of.as<uint32_t>();
-    k_txn_of<<<blocks(nn), 256, 0, s>>>(nn, cover, id, txn_of);
+    k_txn_of_w<<<blocks(nwd), 256, 0, s>>>(nwd, bits, wc, txn_of);
     // edge rows over cut ids -> sorted unique CSR / CSC
     const size_t ecap = std::max<size_t>(64, (m + 63) & ~(size_t)63);
     CK(g.ew.ensure(8 * ecap));
@@ -1847,7 +1925,7 @@ hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *row
     uint32_t *bad = g.count.as<uint32_t>() + 8;
     CK(hipMemsetAsync(bad, 0, 4, s));
     if (m)
-        k_relabel<<<blocks(m), 256, 0, s>>>(m, nn, rows, cover, id, g.ew.as<uint64_t>(),
+        k_relabel<<<blocks(m), 256, 0, s>>>(m, nn, rows, bits, wc, g.ew.as<uint64_t>(),
                                             g.et.as<uint64_t>(), g.eg.as<uint32_t>(), bad);
     CK(hipGetLastError());
     uint32_t hbad = 0;
@@ -1861,7 +1939,7 @@ hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *row
         CK(hipGetLastError());
         uint32_t ri[2] = {0, 0};
         CK(hipMemcpyAsync(ri, g.count.as<uint32_t>() + 4, 8, hipMemcpyDeviceToHost, s));
-        k_scc_out<<<blocks(nn), 256, 0, s>>>(nn, cover, id, g.scc.as<uint32_t>(), txn_of, scc_out);
+        k_scc_out<<<blocks(nn), 256, 0, s>>>(nn, bits, wc, g.scc.as<uint32_t>(), txn_of, scc_out);
         CK(hipGetLastError());
         CK(hipStreamSynchronize(s));
         *rounds = ri[0], *iterations = ri[1];
@@ -1870,7 +1948,7 @@ hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *row
     CK(graph_rows_csr(m, ecap, nc, g, s));
     CK(graph_scc(nc, g, rounds, iterations, s));
     // sub_scc lives in g.scc (nc entries); the caller's scc_out gets all nn
-    k_scc_out<<<blocks(nn), 256, 0, s>>>(nn, cover, id, g.scc.as<uint32_t>(), txn_of, scc_out);
+    k_scc_out<<<blocks(nn), 256, 0, s>>>(nn, bits, wc, g.scc.as<uint32_t>(), txn_of, scc_out);
     CK(hipGetLastError());
     CK(hipStreamSynchronize(s));
 #undef CK

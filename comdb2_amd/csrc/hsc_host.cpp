@@ -4504,16 +4504,20 @@ static int graph_build_timed(hsc_ctx *c, const GraphInput &in, bool full, float 
         gb.n_extra = 0;
     }
     gb.edge_bad = nullptr;
+    gb.post = nullptr;
     hipError_t e = graph_build(gi, gb, full, s);
     if (e == hipSuccess) e = hipEventRecord(e1, s);
-    // the edge pass's check of the observed ids (in.check), read with the sync
-    uint32_t ebad = 0;
-    if (e == hipSuccess && gb.edge_bad) e = hipMemcpyAsync(&ebad, gb.edge_bad, 4, hipMemcpyDeviceToHost, s);
+    // with the sync: the backward rows listed and the edge pass's check of the
+    // observed ids (in.check)
+    uint32_t post[2] = {0, 0};
+    if (e == hipSuccess && gb.post) e = hipMemcpyAsync(post, gb.post, 8, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e == hipSuccess) (void)hipEventElapsedTime(build_ms, e0, e1);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     HIPCHK(c, e);
+    gb.back_n = post[0];
+    const uint32_t ebad = gb.edge_bad ? post[1] : 0;
     gb.bad |= ebad;
     if (ebad & 1) {
         c->graph_ntxn = 0;

@@ -474,6 +474,7 @@ struct GraphInput {              // device pointers
     bool check = false;       // graph_build checks the ops itself (GraphBufs::bad; an op
                               // out of range: hipErrorInvalidValue before any edge work)
 };
+constexpr uint32_t kBackCap = 1u << 20;  // GraphBufs::back rows
 struct GraphBufs {
     DBuf flags, flags2, scratch, count;
     DBuf wg, ww, wl, wg2, ww2, wl2;            // writer rows
@@ -496,6 +497,10 @@ struct GraphBufs {
     uint32_t bad = 0;            // the last checked build's input bits (GraphInput::check)
     uint32_t *edge_bad = nullptr;  // device word of the edge pass's observed-id check (graph_build_timed
                                    // reads it after the build), or null
+    uint32_t *post = nullptr;      // device words read after a build: [0] backward rows listed, [1] = edge_bad's
+    DBuf back;                     // a raw build's backward rows (graph_cover marks their intervals)
+    bool back_listed = false;
+    uint32_t back_n = 0;           // listed rows (> kBackCap: only counted -- graph_cover takes the diffs)
     DBuf cover_bits;             // graph_cut: the cover as a bitmap
     DBuf cover_list;             // graph_cut: the covered txns (the op-range cut)
     DBuf gvary;                  // k_gw_place's per-block OR / AND of the writers' key and txn
@@ -511,7 +516,7 @@ struct GraphBufs {
                        &in_src, &in_dst, &out_off, &in_off, &scc, &active, &color, &mark,
                        &front, &front2, &h_txn, &h_key, &h_isw, &h_obs, &diff, &cut,
                        &cut_id, &txn_of, &x_rows, &x_type, &x_map, &pk, &pdir, &ptab, &rp_cnt,
-                       &rp_items, &cover_bits, &cover_list, &gvary};
+                       &rp_items, &cover_bits, &cover_list, &gvary, &back};
         for (DBuf *b : all) b->release();
     }
 };
