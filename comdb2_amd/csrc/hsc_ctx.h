@@ -760,7 +760,8 @@ bool ctx_small_fits(hsc_ctx *c, size_t n_txn, size_t n, size_t n_lock);
 int ctx_edge_keys(hsc_ctx *c, uint32_t *gid, uint64_t *words);
 // op_txn: the last build's ops' txn array when still live (the op-range cut)
 int ctx_graph_cut(hsc_ctx *c, const uint8_t *cover, size_t *m, const uint64_t **rows,
-                  const uint32_t *op_txn = nullptr);
+                  const uint32_t *op_txn = nullptr, const uint64_t *op_key = nullptr,
+                  const uint8_t *op_isw = nullptr);
 int ctx_stage_launch(hsc_ctx *c, Stage &st, int *slot);
 int ctx_stage_wait(hsc_ctx *c, Stage &st, int slot, int *rc_out);
 bool multi_adopted(const hsc_ctx *f);

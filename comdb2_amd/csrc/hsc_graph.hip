@@ -338,13 +338,7 @@ __global__ void k_edges_reads(size_t nops, const uint32_t *txn, const uint64_t *
 // each bucket's first writer: a read's "first writer after (k, ob)" is one
 // directory line plus a binary search inside its bucket (~30 writers on
 // uniform keys) instead of ~26 dependent steps over the 16-byte rows.
-struct PairPack {
-    uint64_t km, tm;          // the writers' varying key / txn bits
-    uint64_t kc, tc;          // their constant bits (the same in every writer)
-    uint64_t kmv[6], tmv[6];  // compress moves
-    uint64_t base, last;      // pk[0], pk[nu - 1]
-    int tb, D, shift;         // txn bits, directory bits, bucket = (pk - base) >> shift
-};
+// (struct PairPack: hsc_internal.h -- GraphBufs keeps the last build's)
 
 // bucket of x: 0 below the range, 2^D past it
 __device__ __forceinline__ uint64_t pair_bucket(const PairPack &pp, uint64_t x)
@@ -1136,6 +1130,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
                        g.flags.as<uint32_t>(), g.scratch.p, g.scratch.bytes, g.count.as<uint32_t>(), s));
     }
     g.writer_packed = packed;
+    g.ww_pk = false;
     const uint64_t *wkey = dw->as<uint64_t>(), *wtxn = dw->as<uint64_t>() + wcap;
     // the distinct count with what the packed search's parameters need -- the
     // first writer row, the first and last packed writer -- in one read
@@ -1199,6 +1194,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         if (!pkv) return hipErrorInvalidValue;  // (a packed sort leaves them)
         pp.base = meta[3], pp.last = meta[4];
         k_edges_ww_pk<<<blocks(nu), 256, 0, s>>>(nu, pkv, pp, g.ew.as<uint64_t>(), et, eg);
+        g.ww_pk = true, g.pp = pp, g.ppk = pkv, g.pnu = nu;  // (graph_cut: ww rows by their source)
         pp.shift = 0;  // (last - base) >> shift < 2^D
         while (pp.shift < 64 && ((pp.last - pp.base) >> pp.shift) >= ((uint64_t)1 << pp.D)) ++pp.shift;
         k_pair_dir<<<blocks(((size_t)1 << pp.D) + 2), 256, 0, s>>>(nu, pkv, pp, g.pdir.as<uint32_t>());
@@ -1683,9 +1679,14 @@ __global__ void k_cover_list(uint32_t nn, const uint8_t *cover, uint64_t *bits, 
 // one thread per covered txn t: its ops (txn-sorted: one run, found by a
 // binary search) and their two rows each -- a cut row at op i has its reader
 // t as one end, so a row whose txn is not covered is never in the cut
+// pk != null: the ww rows too, from their source side -- a ww row j (writer
+// j -> j + 1 of one key) is emitted by the covered txn of writer j, found
+// by an exact search of pk for (key, txn) of each of its write ops (a txn's
+// repeated write of a key: once) -- so no pass over the nu ww rows
 __global__ void k_cut_txn_ops(const uint32_t *list, const uint32_t *lcnt, const uint32_t *op_txn, size_t nops,
                               const uint64_t *op_rows, const uint64_t *cover, uint64_t *rows, uint32_t *cnt,
-                              uint32_t cap)
+                              uint32_t cap, const uint64_t *op_key, const uint8_t *op_isw, const uint64_t *pk,
+                              uint32_t nu, const uint64_t *ww, PairPack pp)
 {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= min(*lcnt, kCoverListCap)) return;
@@ -1698,10 +1699,34 @@ __global__ void k_cut_txn_ops(const uint32_t *list, const uint32_t *lcnt, const 
         else
             hi = mid;
     }
+    const size_t first = lo;
     for (size_t i = lo; i < nops && op_txn[i] == t; ++i) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint64_t r = op_rows[2 * i + q];
+        for (int q = 0; q < 3; ++q) {
+            uint64_t r = ~0ull;
+            if (q < 2) {
+                r = op_rows[2 * i + q];
+            } else if (pk && op_isw[i]) {
+                const uint64_t k = op_key[i];
+                bool dup = false;
+                for (size_t i2 = first; i2 < i && !dup; ++i2) dup = op_isw[i2] && op_key[i2] == k;
+                if (!dup && (k & ~pp.km) == pp.kc && (t & ~pp.tm) == pp.tc) {
+                    uint64_t km[6], tm[6];
+#pragma unroll
+                    for (int z = 0; z < 6; ++z) km[z] = pp.kmv[z], tm[z] = pp.tmv[z];
+                    const uint64_t x =
+                        (pp.tb >= 64 ? 0 : bits_compress(k, pp.km, km) << pp.tb) | bits_compress(t, pp.tm, tm);
+                    uint32_t a = 0, h = nu;
+                    while (a < h) {
+                        const uint32_t mid = (a + h) >> 1;
+                        if (pk[mid] < x)
+                            a = mid + 1;
+                        else
+                            h = mid;
+                    }
+                    if (a < nu && pk[a] == x) r = ww[a];
+                }
+            }
             if (r == ~0ull) continue;
             const uint32_t a = (uint32_t)(r >> 32), b = (uint32_t)r;
             if (cover_bit(cover, a) && cover_bit(cover, b)) {
@@ -1712,7 +1737,8 @@ __global__ void k_cut_txn_ops(const uint32_t *list, const uint32_t *lcnt, const 
     }
 }
 
-hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s, const uint32_t *op_txn)
+hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s, const uint32_t *op_txn,
+                     const uint64_t *op_key, const uint8_t *op_isw)
 {
     hipError_t e = hipSuccess;
     const EdgeSet es = edge_set(g);
@@ -1737,7 +1763,10 @@ hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t 
             k_cover_list<<<blocks(nn), 256, 0, s>>>(nn, cover, g.cover_bits.as<uint64_t>(),
                                                     g.cover_list.as<uint32_t>(), cnt + 1, kCoverListCap);
             const uint64_t *ew = g.ew.as<uint64_t>();
-            if (g.op_at)
+            // the ww rows from the covered txns' write ops when the build's
+            // writers are packed keys (else a pass over them)
+            const bool ww_src = g.ww_pk && op_key && op_isw && g.op_at == g.pnu;
+            if (g.op_at && !ww_src)
                 k_cut_append<<<blocks(g.op_at), 256, 0, s>>>(EdgeSet{ew, nullptr, nullptr, g.op_at},
                                                              g.cover_bits.as<uint64_t>(), g.cut.as<uint64_t>(), cnt,
                                                              kCutFastCap);
@@ -1748,7 +1777,9 @@ hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t 
             if (g.op_n)
                 k_cut_txn_ops<<<blocks(kCoverListCap), 256, 0, s>>>(g.cover_list.as<uint32_t>(), cnt + 1, op_txn,
                                                                     g.op_n, ew + g.op_at, g.cover_bits.as<uint64_t>(),
-                                                                    g.cut.as<uint64_t>(), cnt, kCutFastCap);
+                                                                    g.cut.as<uint64_t>(), cnt, kCutFastCap, op_key,
+                                                                    op_isw, ww_src ? g.ppk : nullptr, g.pnu, ew,
+                                                                    g.pp);
             uint32_t kc[2] = {0, 0};
             if ((e = hipMemcpyAsync(kc, g.count.p, 8, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
             if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;

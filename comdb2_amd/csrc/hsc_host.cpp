@@ -4861,11 +4861,12 @@ int ctx_edge_keys(hsc_ctx *c, uint32_t *gid, uint64_t *words)
 
 // The cut of the last build under cover (one pass: count + rows); *rows
 // points into the context's own buffer until its next graph call.
-int ctx_graph_cut(hsc_ctx *c, const uint8_t *cover, size_t *m, const uint64_t **rows, const uint32_t *op_txn)
+int ctx_graph_cut(hsc_ctx *c, const uint8_t *cover, size_t *m, const uint64_t **rows, const uint32_t *op_txn,
+                  const uint64_t *op_key, const uint8_t *op_isw)
 {
     MuGuard g(c);
     (void)hipSetDevice(c->device);
-    HIPCHK(c, graph_cut(c->graph, cover, m, c->stream, op_txn));
+    HIPCHK(c, graph_cut(c->graph, cover, m, c->stream, op_txn, op_key, op_isw));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     *rows = c->graph.cut.as<uint64_t>();
     return HSC_OK;

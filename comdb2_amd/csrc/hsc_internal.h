@@ -474,6 +474,16 @@ struct GraphInput {              // device pointers
     bool check = false;       // graph_build checks the ops itself (GraphBufs::bad; an op
                               // out of range: hipErrorInvalidValue before any edge work)
 };
+// The packed writers' layout (hsc_graph.hip): every distinct writer is one
+// u64 pk = compress(key) << tb | compress(txn), ascending; a directory of
+// 2^D buckets over [pk[0], pk[nu - 1]]
+struct PairPack {
+    uint64_t km, tm;          // the writers' varying key / txn bits
+    uint64_t kc, tc;          // their constant bits (the same in every writer)
+    uint64_t kmv[6], tmv[6];  // compress moves
+    uint64_t base, last;      // pk[0], pk[nu - 1]
+    int tb, D, shift;         // txn bits, directory bits, bucket = (pk - base) >> shift
+};
 constexpr uint32_t kBackCap = 1u << 20;  // GraphBufs::back rows
 struct GraphBufs {
     DBuf flags, flags2, scratch, count;
@@ -499,6 +509,10 @@ struct GraphBufs {
                                    // reads it after the build), or null
     uint32_t *post = nullptr;      // device words read after a build: [0] backward rows listed, [1] = edge_bad's
     DBuf back;                     // a raw build's backward rows (graph_cover marks their intervals)
+    bool ww_pk = false;            // the last build's ww rows came from its packed writers:
+    PairPack pp{};                 // their layout, array (in the build's buffers) and count
+    const uint64_t *ppk = nullptr;
+    uint32_t pnu = 0;
     bool back_listed = false;
     uint32_t back_n = 0;           // listed rows (> kBackCap: only counted -- graph_cover takes the diffs)
     DBuf cover_bits;             // graph_cut: the cover as a bitmap
@@ -638,9 +652,11 @@ hipError_t launch_join_c(const CTiles &ct, const ProbeWork &work, uint32_t max_i
 hipError_t graph_cover(GraphBufs &g, uint32_t nn, uint8_t *cover, hipStream_t s);
 // op_txn: the last build's ops' txn array (still live), or null -- with it a
 // raw build over txn-sorted ops tests the ww / staged rows and the covered
-// txns' own op rows instead of every row
+// txns' own op rows instead of every row (with op_key / op_isw too, the ww
+// rows from the covered txns' write ops)
 hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s,
-                     const uint32_t *op_txn = nullptr);
+                     const uint32_t *op_txn = nullptr, const uint64_t *op_key = nullptr,
+                     const uint8_t *op_isw = nullptr);
 hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *rows, size_t m,
                           GraphBufs &g, uint32_t *scc_out, uint32_t *n_cut, uint32_t *rounds,
                           uint32_t *iterations, hipStream_t s);

@@ -1965,7 +1965,8 @@ int hsc_multi_graph_scc(hsc_ctx *f, const hsc_ops_dev *ops, uint32_t ntxn, uint3
     for (int m = 0; m < NL; ++m) {
         hsc_ctx *c = M->mem[m];
         // (the build's ops are the caller's, live for this call)
-        const int rc = ctx_graph_cut(c, M->g_cover[m].as<uint8_t>(), &k[m], &cut[m], ops[m].txn);
+        const int rc = ctx_graph_cut(c, M->g_cover[m].as<uint8_t>(), &k[m], &cut[m], ops[m].txn, ops[m].key,
+                                     ops[m].is_write);
         if (rc) return mfail(f, rc, ("graph cut: " + c->err).c_str());
     }
     // 4. the union of the cuts where the SCC runs: every rank (all-gather,
