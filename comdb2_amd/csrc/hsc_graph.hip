@@ -302,7 +302,8 @@ __global__ void k_edges_reads(size_t nops, const uint32_t *txn, const uint64_t *
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nops) return;
     uint64_t wr = ~0ull, rw = ~0ull;
-    if (!is_write[i] && !obs_bad(observed[i], chk_n, bad)) {
+    // (every op's observed id checked, a write's too: the build's contract)
+    if (!obs_bad(observed[i], chk_n, bad) && !is_write[i]) {
         const uint32_t r = txn[i], ob = observed[i];
         const uint64_t k = key[i];
         if (ob != kNone && ob != r) wr = ((uint64_t)ob << 32) | r;
@@ -444,7 +445,8 @@ __global__ void k_edges_reads_pk(size_t nops, const uint32_t *txn, const uint64_
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nops) return;
     uint64_t wr = ~0ull, rw = ~0ull;
-    if (!is_write[i] && !obs_bad(observed[i], chk_n, bad)) {
+    // (every op's observed id checked, a write's too: the build's contract)
+    if (!obs_bad(observed[i], chk_n, bad) && !is_write[i]) {
         const uint32_t r = txn[i], ob = observed[i];
         const uint64_t k = key[i];
         if (ob != kNone && ob != r) wr = ((uint64_t)ob << 32) | r;
@@ -564,7 +566,8 @@ __global__ void k_edges_reads_pt(size_t nops, const uint32_t *txn, const uint64_
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nops) return;
     uint64_t wr = ~0ull, rw = ~0ull;
-    if (!is_write[i] && !obs_bad(observed[i], chk_n, bad)) {
+    // (every op's observed id checked, a write's too: the build's contract)
+    if (!obs_bad(observed[i], chk_n, bad) && !is_write[i]) {
         const uint32_t r = txn[i], ob = observed[i];
         const uint64_t k = key[i];
         if (ob != kNone && ob != r) wr = ((uint64_t)ob << 32) | r;

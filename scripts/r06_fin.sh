@@ -25,3 +25,4 @@ step trace_c5s1 500 rocprofv3 --kernel-trace --stats --output-format csv -d $out
 step c1 500 python -u bench.py --config 1
 step c4 500 python -u bench.py --config 4
 step inproc2 500 python -u bench.py --inproc 2 --steps 30
+step trace_c4 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/${tag}_trace_c4 -o k -- python3 bench.py --config 4 --no-cpu --no-pmc --steps 3 --warmup 1

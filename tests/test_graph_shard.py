@@ -294,14 +294,19 @@ def test_gpu_multi_graph_scc_build_paths(oracle_mod, case):
 
 
 @pytest.mark.gpu
-def test_gpu_multi_graph_scc_rejects_ids_out_of_range():
-    """An op naming a txn >= ntxn fails the call (the count pass's check),
-    before any edge is built."""
+@pytest.mark.parametrize("field", ["read_observed", "write_observed", "txn"])
+def test_gpu_multi_graph_scc_rejects_ids_out_of_range(field):
+    """An op naming a txn >= ntxn fails the call: its txn (the place pass's
+    check, before any edge is built) or its observed writer, a read's or a
+    write's (the edge pass's check, which emits no row for it)."""
     from comdb2_amd.hsc import HscError
     from comdb2_amd.workloads import History
     h = config4_history(n_txn=3000, n_keys=100)
-    obs = h.observed.copy()
-    i = int(np.nonzero(obs >= 0)[0][7])
-    obs[i] = h.ntxn + 5
+    obs, txn = h.observed.copy(), h.txn.copy()
+    if field == "txn":
+        txn[-1] = h.ntxn + 5  # (the last op: the txn order stays)
+    else:
+        i = int(np.nonzero(h.is_write == (1 if field == "write_observed" else 0))[0][7])
+        obs[i] = h.ntxn + 5
     with pytest.raises(HscError, match="out of range"):
-        _multi_scc(History(h.txn, h.key, h.is_write, obs, h.ntxn))
+        _multi_scc(History(txn, h.key, h.is_write, obs, h.ntxn))
