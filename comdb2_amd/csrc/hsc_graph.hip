@@ -1219,8 +1219,13 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
                 diff = g.diff.as<uint32_t>();
                 diff_done = true;
             } else {  // the rows themselves (the counter: g.count's u32 29, cleared by k_graph_meta)
-                CK(g.back.ensure(8 * (size_t)kBackCap));
-                sink = BackSink{nullptr, g.back.as<uint64_t>(), g.count.as<uint32_t>() + 29, kBackCap};
+                // (HSC_GRAPH_BACK_CAP: a smaller list, read per build -- the
+                // tests' way to the diff fallback)
+                uint32_t cap = kBackCap;
+                if (const char *v = getenv("HSC_GRAPH_BACK_CAP")) cap = std::min<uint32_t>(kBackCap, (uint32_t)atoi(v));
+                CK(g.back.ensure(8 * (size_t)std::max<uint32_t>(cap, 1)));
+                sink = BackSink{nullptr, g.back.as<uint64_t>(), g.count.as<uint32_t>() + 29, cap};
+                g.back_cap = cap;
                 back_listed = true;
             }
         }
@@ -1597,7 +1602,7 @@ hipError_t graph_cover(GraphBufs &g, uint32_t nn, uint8_t *cover, hipStream_t s)
 {
     hipError_t e = hipSuccess;
     if (nn == 0) return hipSuccess;
-    if (g.raw && g.back_listed && g.cover_nn == nn && g.back_n <= kBackCap) {
+    if (g.raw && g.back_listed && g.cover_nn == nn && g.back_n <= g.back_cap) {
         // the listed backward rows' intervals (no diffs, no scan of nn)
         if ((e = hipMemsetAsync(cover, 0, nn, s)) != hipSuccess) return e;
         if (g.back_n)

@@ -514,7 +514,8 @@ struct GraphBufs {
     const uint64_t *ppk = nullptr;
     uint32_t pnu = 0;
     bool back_listed = false;
-    uint32_t back_n = 0;           // listed rows (> kBackCap: only counted -- graph_cover takes the diffs)
+    uint32_t back_n = 0;           // listed rows (> back_cap: only counted -- graph_cover takes the diffs)
+    uint32_t back_cap = kBackCap;
     DBuf cover_bits;             // graph_cut: the cover as a bitmap
     DBuf cover_list;             // graph_cut: the covered txns (the op-range cut)
     DBuf gvary;                  // k_gw_place's per-block OR / AND of the writers' key and txn

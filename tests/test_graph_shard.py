@@ -265,8 +265,9 @@ def _multi_scc(h, world=1):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["shuffled", "hot_key", "hot_key_shuffled", "hot_mix", "wide_cover"])
-def test_gpu_multi_graph_scc_build_paths(oracle_mod, case):
+@pytest.mark.parametrize("case", ["shuffled", "hot_key", "hot_key_shuffled", "hot_mix", "wide_cover",
+                                  "back_overflow"])
+def test_gpu_multi_graph_scc_build_paths(oracle_mod, case, monkeypatch):
     """The raw build's paths: ops out of txn order (the writer sort then takes
     every pass: the txn bits are not skipped), and hot keys whose writers
     crowd single directory buckets past a bucket line's entries (the overflow
@@ -274,10 +275,14 @@ def test_gpu_multi_graph_scc_build_paths(oracle_mod, case):
     (its writers ~1000x denser than the buckets are sized for).  Components =
     Tarjan's.  The cut: by the covered txns' op ranges (txn-sorted ops), by
     every row (shuffled), and every row again after the op-range pass finds
-    more covered txns than its list holds (wide_cover: > 65536)."""
+    more covered txns than its list holds (wide_cover: > 65536).  The cover:
+    from the listed backward rows, or from interval diffs of every raw row
+    once the list overflows (back_overflow: a 16-row list)."""
     from comdb2_amd.workloads import History
     kw = dict(n_txn=20000, n_keys=4, concurrent_frac=0.3, max_lag=16) if case.startswith("hot_key") else \
         dict(seed=9, n_txn=20000, n_keys=2000, concurrent_frac=0.2, max_lag=16)
+    if case == "back_overflow":
+        monkeypatch.setenv("HSC_GRAPH_BACK_CAP", "16")
     if case == "wide_cover":
         kw = dict(seed=11, n_txn=200000, n_keys=2000, concurrent_frac=0.9, max_lag=64)  # ~185k covered
     h = config4_history(**kw)
