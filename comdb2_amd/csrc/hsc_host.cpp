@@ -718,9 +718,9 @@ static int device_build(hsc_ctx *c, size_t n_in)
     // varying key bits and the LSN span in one pass; the distinct commit list
     // only when snapshot ranks need its directory (a window spanning >= 2^32
     // of log): otherwise rows carry lsn - oldest + 1
-    uint64_t vary[kMaxWords + 1], span[2];
+    uint64_t vary[kMaxWords + 1], span[2], lvary = 0;
     HIPCHK(c, vary_mask_rows(W, n_in, c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(), cap,
-                             c->d_scratch.p, vary, s, c->d_lsn.as<uint64_t>(), span));
+                             c->d_scratch.p, vary, s, c->d_lsn.as<uint64_t>(), span, &lvary));
     bt.stamp("vary");
     const bool commits = c->layout != HSC_LAYOUT_WIDE && n_in > 0;
     const bool rank_dir = commits && span[1] - span[0] > kLsn32MaxSpan;
@@ -730,7 +730,10 @@ static int device_build(hsc_ctx *c, size_t n_in)
     if (rank_dir) HIPCHK_RC(c, build_commits(c, n_in));
     bt.stamp("commits");
     PackPlan plan;
-    c->packed_sort = try_packed && packed_plan(W, n_in, vary, &plan);
+    // (the LSNs' varying bits beside the key's: the min LSN is a row's, so its
+    // bits outside them are every row's)
+    const uint64_t lbits[2] = {lvary, span[0]};
+    c->packed_sort = try_packed && packed_plan(W, n_in, vary, &plan, true, lbits);
     // too many varying bits for the packed sort: by compact codes if they fit
     bool code_sorted = false;
     c->cs_codes_wc = 0;

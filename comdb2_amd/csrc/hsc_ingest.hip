@@ -16,7 +16,10 @@
 //            leave as coalesced runs per digit (k_pk_count counts the next
 //            digit of the permuted keys);
 //   unpack   every sorted key back to gid / words (expand of the kept bits
-//            over row 0's constant bits) with the LSN gathered by row index,
+//            over row 0's constant bits) with the LSN gathered by row index
+//            -- or, when the LSNs' varying bits fit beside the key bits, the
+//            LSN itself rides in the low bits instead of the index (packed by
+//            k_pk_pack's coalesced read, expanded here: no random gather) --
 //            plus the "last version of its key" flag;
 // then the usual scan + compaction (dedupe_flagged) gives the distinct rows.
 // Per row and pass that is 8 B read + 8 B written instead of a whole row.
@@ -26,6 +29,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace hsc {
 namespace {
@@ -55,7 +59,7 @@ __device__ __forceinline__ uint64_t pk_limb(const PackPlan &P, int l, size_t i, 
 
 __global__ __launch_bounds__(kPkThreads) void k_pk_pack(PackPlan P, size_t n, const uint32_t *gid,
                                                         const uint64_t *words, size_t stride,
-                                                        uint64_t *keys, uint32_t *counts,
+                                                        const uint64_t *lsn, uint64_t *keys, uint32_t *counts,
                                                         uint32_t nblocks)
 {
     __shared__ uint32_t h[256];
@@ -79,7 +83,14 @@ __global__ __launch_bounds__(kPkThreads) void k_pk_pack(PackPlan P, size_t n, co
                 }
             }
         }
-        key[k] = P.I ? (kb << P.I) | (uint64_t)i : kb;  // I = 0: the key is the whole row
+        uint64_t low = (uint64_t)i;
+        if (P.lsn_packed) {
+            uint64_t lm[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) lm[q] = P.lmv[q];
+            low = i < n ? pk_compress(lsn[i], P.lmask, lm) : 0;
+        }
+        key[k] = P.I ? (kb << P.I) | low : kb;  // (I = 0, no LSN field: the key is the whole row)
     }
 #pragma unroll
     for (int k = 0; k < kPkItems; ++k) {
@@ -319,7 +330,14 @@ __global__ __launch_bounds__(kUdThreads) void k_pk_unpack_dd(
         // (no LSNs and no index bits -- the packed key is the whole row: the
         // distinct rows' "LSN" slot gets the packed key itself, which the
         // dependency graph takes as its packed writer array)
-        lvs[r] = j >= nrows ? 0 : lsn_in ? lsn_in[K[j] & imask] : P.I == 0 ? K[j] : 0;
+        if (P.lsn_packed) {  // the LSN rode in the key's low bits
+            uint64_t lm[6];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) lm[q] = P.lmv[q];
+            lvs[r] = j >= nrows ? 0 : pk_expand(K[j] & imask, P.lmask, lm) | P.lconst;
+        } else {
+            lvs[r] = j >= nrows ? 0 : lsn_in ? lsn_in[K[j] & imask] : P.I == 0 ? K[j] : 0;
+        }
     }
 #pragma unroll  // (whole: lvs stays in registers)
     for (int r = 0; r < kUdRows; ++r) {
@@ -385,7 +403,7 @@ size_t packed_scratch_bytes(size_t n)
            (ud + 16) * sizeof(uint32_t) + scan_scratch_bytes(ud) + 8 * (kPackMaxWords + 1) + 64;
 }
 
-bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P, bool index)
+bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P, bool index, const uint64_t *lsn_bits)
 {
     if (W > kPackMaxWords || n >= 0xFFFFFFFFull) return false;
     *P = PackPlan{};
@@ -409,19 +427,32 @@ bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P, bool index)
     }
     P->nl = nl;
     P->B = B;
+    static const bool no_lsn_pack = getenv("HSC_NO_LSN_PACK") != nullptr;  // (A/B)
+    if (index && lsn_bits && !no_lsn_pack) {
+        const int L = __builtin_popcountll(lsn_bits[0]);
+        if (B + L <= 64) {  // the LSN itself in the low bits: no gather in the unpack
+            P->I = L;
+            P->lsn_packed = true;
+            P->lmask = lsn_bits[0];
+            P->lconst = lsn_bits[1] & ~lsn_bits[0];
+            compress_moves(P->lmask, P->lmv);
+            return true;
+        }
+    }
     return B + I <= 64;
 }
 
 // The LSD passes of the packed keys; the sorted keys end in *kf, the other
 // key buffer is *kfree.
 static hipError_t packed_passes(const PackPlan &P, size_t n, const uint32_t *gid,
-                                const uint64_t *words, size_t stride, uint64_t *k0, uint64_t *k1,
-                                void *scratch, hipStream_t s, uint64_t **kf, uint64_t **kfree)
+                                const uint64_t *words, size_t stride, const uint64_t *lsn, uint64_t *k0,
+                                uint64_t *k1, void *scratch, hipStream_t s, uint64_t **kf, uint64_t **kfree)
 {
     const uint32_t nblocks = (uint32_t)((n + kPkTile - 1) / kPkTile);
     uint32_t *counts = (uint32_t *)scratch;
     uint32_t *scan_tmp = counts + (size_t)256 * nblocks;
-    k_pk_pack<<<nblocks, kPkThreads, 0, s>>>(P, n, gid, words, stride, k0, counts, nblocks);
+    if (P.lsn_packed && !lsn) return hipErrorInvalidValue;
+    k_pk_pack<<<nblocks, kPkThreads, 0, s>>>(P, n, gid, words, stride, lsn, k0, counts, nblocks);
     hipError_t e = hipGetLastError();
     // (P.skip: the low bits the input is already ordered by need no pass --
     // the passes are stable)
@@ -451,7 +482,7 @@ hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, 
     if (n == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
     if (scratch_bytes < packed_scratch_bytes(n)) return hipErrorInvalidValue;
     uint64_t *kf, *kfree;
-    hipError_t e = packed_passes(P, n, gid, words, stride, k0, k1, scratch, s, &kf, &kfree);
+    hipError_t e = packed_passes(P, n, gid, words, stride, lsn, k0, k1, scratch, s, &kf, &kfree);
     if (e != hipSuccess) return e;
     // scratch after the passes' counters: block counts, their scan, row 0
     const uint32_t nblocks = (uint32_t)((n + kPkTile - 1) / kPkTile);

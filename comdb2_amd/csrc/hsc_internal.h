@@ -143,7 +143,7 @@ size_t radix_scratch_bytes(size_t n, int W);
 // is 0) -- one kernel + readback; scratch >= 8 (W + 3) bytes
 hipError_t vary_mask_rows(int W, size_t n, const uint32_t *gid, const uint64_t *words, size_t stride,
                           void *scratch, uint64_t *vary, hipStream_t s, const uint64_t *lsn = nullptr,
-                          uint64_t *lsn_span = nullptr);
+                          uint64_t *lsn_span = nullptr, uint64_t *lsn_vary = nullptr);
 // radix_sort_rows with the vary masks already known
 hipError_t radix_sort_known(int W, size_t n, uint32_t *gid, uint64_t *words, uint64_t *lsn,
                             size_t stride, uint32_t *gid_alt, uint64_t *words_alt,
@@ -172,10 +172,19 @@ struct PackPlan {
     uint64_t mv[kPackLimbs][6]; // their compress moves
     int skip = 0;               // low packed bits the rows are already ordered by (stable
                                 // passes skip them: a txn-ordered writer list sorted by key)
+    // the low I bits hold the row's LSN compressed by its varying bits instead
+    // of the row index (the passes never sort them: equal keys keep input
+    // order either way) -- the unpack expands it, no gather by row index
+    bool lsn_packed = false;
+    uint64_t lmask = 0, lconst = 0;  // the LSNs' varying / constant bits
+    uint64_t lmv[6] = {};
 };
 // false: does not fit.  index = false: no row index (I = 0) -- the packed
 // key is the whole row (no LSN to gather; equal rows are duplicates)
-bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P, bool index = true);
+// lsn_bits (index only): {varying, constant} bits of the rows' LSNs -- when
+// they fit beside the key bits they take the index's place (PackPlan::lsn_packed)
+bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P, bool index = true,
+                 const uint64_t *lsn_bits = nullptr);
 size_t packed_scratch_bytes(size_t n);
 // The packed sort with the dedupe fused into the unpack: every version to
 // (gid_o, words_o, lsn_o) (gid_o null: not written; lsn null: LSNs 0, or with no index bits the

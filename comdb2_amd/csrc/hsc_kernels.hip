@@ -82,8 +82,10 @@ __global__ __launch_bounds__(256) void k_vary_mask(int W, size_t n, const uint32
         __syncthreads();
     }
     if (!lsn) return;
-    // the rows' LSN span: mask[W + 1] = min, mask[W + 2] = max
-    uint64_t lo = ~0ull, hi = 0;
+    // the rows' LSN span: mask[W + 1] = min, mask[W + 2] = max; mask[W + 3] =
+    // the LSN bits that vary (OR of lsn XOR lsn[0])
+    const uint64_t lref = lsn[0];
+    uint64_t lo = ~0ull, hi = 0, lv = 0;
     for (size_t i0 = (size_t)blockIdx.x * blockDim.x * U + threadIdx.x; i0 < n;
          i0 += (size_t)gridDim.x * blockDim.x * U) {
         uint64_t v[U];
@@ -96,25 +98,29 @@ __global__ __launch_bounds__(256) void k_vary_mask(int W, size_t n, const uint32
         for (int u = 0; u < U; ++u) {
             lo = v[u] < lo ? v[u] : lo;
             hi = v[u] > hi ? v[u] : hi;
+            lv |= v[u] ^ lref;
         }
     }
     for (int o = 32; o > 0; o >>= 1) {
         const uint64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
         lo = a < lo ? a : lo;
         hi = b > hi ? b : hi;
+        lv |= __shfl_xor(lv, o, 64);
     }
-    __shared__ uint64_t plo[256 / 64], phi[256 / 64];
-    if (lane_id() == 0) plo[threadIdx.x >> 6] = lo, phi[threadIdx.x >> 6] = hi;
+    __shared__ uint64_t plo[256 / 64], phi[256 / 64], plv[256 / 64];
+    if (lane_id() == 0) plo[threadIdx.x >> 6] = lo, phi[threadIdx.x >> 6] = hi, plv[threadIdx.x >> 6] = lv;
     __syncthreads();
     if (threadIdx.x == 0) {  // one atomic pair per block (same-address atomics serialise)
         for (int w = 1; w < 256 / 64; ++w) {
             lo = plo[w] < lo ? plo[w] : lo;
             hi = phi[w] > hi ? phi[w] : hi;
+            lv |= plv[w];
         }
         if (hi) {
             atomicMin(&mask[W + 1], (unsigned long long)lo);
             atomicMax(&mask[W + 2], (unsigned long long)hi);
         }
+        if (lv) atomicOr(&mask[W + 3], (unsigned long long)lv);
     }
 }
 
@@ -128,12 +134,13 @@ __global__ __launch_bounds__(256) void k_vary_mask_w(size_t n, const uint32_t *g
                                                      unsigned long long *mask)
 {
     constexpr int U = 8;
-    __shared__ uint64_t part[256 / 64][WT + 3];
+    __shared__ uint64_t part[256 / 64][WT + 4];
     uint64_t ref[WT + 1], m[WT + 1];
 #pragma unroll
     for (int j = 0; j < WT; ++j) ref[j] = words[(size_t)j * stride], m[j] = 0;
     ref[WT] = gid[0], m[WT] = 0;
-    uint64_t lo = ~0ull, hi = 0;
+    const uint64_t lref = lsn ? lsn[0] : 0;
+    uint64_t lo = ~0ull, hi = 0, lv = 0;
     for (size_t i0 = (size_t)blockIdx.x * 256 * U + threadIdx.x; i0 < n; i0 += (size_t)gridDim.x * 256 * U) {
         uint64_t v[U][WT + 1], l[U];
 #pragma unroll
@@ -151,6 +158,7 @@ __global__ __launch_bounds__(256) void k_vary_mask_w(size_t n, const uint32_t *g
             for (int j = 0; j <= WT; ++j) m[j] |= v[u][j] ^ ref[j];
             lo = l[u] < lo ? l[u] : lo;
             hi = l[u] > hi ? l[u] : hi;
+            lv |= l[u] ^ lref;
         }
     }
 #pragma unroll
@@ -160,12 +168,14 @@ __global__ __launch_bounds__(256) void k_vary_mask_w(size_t n, const uint32_t *g
         const uint64_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
         lo = a < lo ? a : lo;
         hi = b > hi ? b : hi;
+        lv |= __shfl_xor(lv, o, 64);
     }
     if (lane_id() == 0) {
 #pragma unroll
         for (int j = 0; j <= WT; ++j) part[threadIdx.x >> 6][j] = m[j];
         part[threadIdx.x >> 6][WT + 1] = lo;
         part[threadIdx.x >> 6][WT + 2] = hi;
+        part[threadIdx.x >> 6][WT + 3] = lv;
     }
     __syncthreads();
     if (threadIdx.x <= WT) {  // one atomic per block and word
@@ -183,6 +193,9 @@ __global__ __launch_bounds__(256) void k_vary_mask_w(size_t n, const uint32_t *g
             atomicMin(&mask[WT + 1], (unsigned long long)a);
             atomicMax(&mask[WT + 2], (unsigned long long)b);
         }
+    } else if (threadIdx.x == 128 && lsn) {  // (a third wave: the LSN's varying bits)
+        const uint64_t v = part[0][WT + 3] | part[1][WT + 3] | part[2][WT + 3] | part[3][WT + 3];
+        if (v) atomicOr(&mask[WT + 3], (unsigned long long)v);
     }
 }
 
@@ -423,13 +436,14 @@ size_t radix_scratch_bytes(size_t n, int W)
 
 hipError_t vary_mask_rows(int W, size_t n, const uint32_t *gid, const uint64_t *words, size_t stride,
                           void *scratch, uint64_t *vary, hipStream_t s, const uint64_t *lsn,
-                          uint64_t *lsn_span)
+                          uint64_t *lsn_span, uint64_t *lsn_vary)
 {
     for (int j = 0; j <= W; ++j) vary[j] = 0;
     if (lsn_span) lsn_span[0] = lsn_span[1] = 0;
+    if (lsn_vary) *lsn_vary = 0;
     if (n == 0) return hipSuccess;
-    unsigned long long *dmask = (unsigned long long *)scratch;  // [W + 1] masks, min, max
-    hipError_t e = hipMemsetAsync(dmask, 0, 8 * ((size_t)W + 3), s);
+    unsigned long long *dmask = (unsigned long long *)scratch;  // [W + 1] masks, min, max, LSN vary
+    hipError_t e = hipMemsetAsync(dmask, 0, 8 * ((size_t)W + 4), s);
     if (e == hipSuccess) e = hipMemsetAsync(dmask + W + 1, 0xFF, 8, s);
     if (e != hipSuccess) return e;
     const uint64_t *ls = lsn_span ? lsn : nullptr;
@@ -450,14 +464,15 @@ hipError_t vary_mask_rows(int W, size_t n, const uint32_t *gid, const uint64_t *
     }
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    uint64_t hm[kMaxWords + 3];
-    e = hipMemcpyAsync(hm, dmask, 8 * ((size_t)W + 3), hipMemcpyDeviceToHost, s);
+    uint64_t hm[kMaxWords + 4];
+    e = hipMemcpyAsync(hm, dmask, 8 * ((size_t)W + 4), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
     for (int j = 0; j <= W; ++j) vary[j] = hm[j];
     if (lsn_span) {
         lsn_span[0] = hm[W + 2] ? hm[W + 1] : 0;
         lsn_span[1] = hm[W + 2];
+        if (lsn_vary) *lsn_vary = hm[W + 3];
     }
     return hipSuccess;
 }
