@@ -1117,7 +1117,8 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         CK(packed_sort_dedupe(P, nw, g.wg.as<uint32_t>(), g.ww.as<uint64_t>(), nullptr, wcap,
                               g.wl.as<uint64_t>(), g.wl2.as<uint64_t>(), nullptr, nullptr, nullptr, 0,
                               writer_rows ? g.wg2.as<uint32_t>() : nullptr, g.ww2.as<uint64_t>(), wcap, &lsn_d,
-                              g.count.as<uint32_t>(), g.scratch.p, g.scratch.bytes, s));
+                              g.count.as<uint32_t>(), g.scratch.p, g.scratch.bytes, s,
+                              g.count.as<uint32_t>() + 28));  // (its stall flag: read after the build)
     } else {
         bool alt = false;
         if (nw) CK(hipMemsetAsync(g.wl.p, 0, 8 * (size_t)nw, s));  // (k_gw_place writes no LSNs)
@@ -1142,7 +1143,8 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     uint32_t *ebad = g.count.as<uint32_t>() + 30;
     const uint32_t chk_n = in.check && !obs_in_count ? std::max<uint32_t>(in.ntxn, 1) : 0;
     g.edge_bad = chk_n ? ebad : nullptr;
-    g.post = g.count.as<uint32_t>() + 29;  // [0] backward rows listed, [1] the edge check's bits
+    g.post = g.count.as<uint32_t>() + 29;  // [-1] the writer sort's stall flag, [0] backward rows
+                                           // listed, [1] the edge check's bits
     k_graph_meta<<<1, 64, 0, s>>>(g.count.as<uint32_t>(), wkey, wtxn, packed ? lsn_d : nullptr,
                                   g.count.as<uint64_t>() + 8, ebad);
     CK(hipMemcpyAsync(meta, g.count.as<uint64_t>() + 8, sizeof meta, hipMemcpyDeviceToHost, s));

@@ -749,7 +749,8 @@ static int device_build(hsc_ctx *c, size_t n_in)
                                      c->d_pk[1].as<uint64_t>(), c->d_gid2.as<uint32_t>(),
                                      c->d_words2.as<uint64_t>(), c->d_lsn2.as<uint64_t>(), cap,
                                      c->d_gid.as<uint32_t>(), c->d_words.as<uint64_t>(), cap, &dl,
-                                     c->d_count.as<uint32_t>(), c->d_scratch.p, c->d_scratch.bytes, s));
+                                     c->d_count.as<uint32_t>(), c->d_scratch.p, c->d_scratch.bytes, s,
+                                     c->d_count.as<uint32_t>() + 20));
         if (dl == c->d_pk[0].p)
             std::swap(c->d_lsn, c->d_pk[0]);
         else if (dl == c->d_pk[1].p)
@@ -796,6 +797,8 @@ static int device_build(hsc_ctx *c, size_t n_in)
     HIPCHK(c, hipMemcpyAsync(hc, c->d_count.p, sizeof hc, hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
     bt.stamp("dedupe");
+    // (hc[20]: the packed sort's one-sweep stall flag -- never expected)
+    if (c->packed_sort && hc[20]) return fail(c, HSC_EDEVICE, "window sort: a tile's look-back stalled");
     const uint32_t nu = hc[0];
     if (rank_dir) c->ncommit = hc[12];
     c->n = n_in ? nu : 0;
@@ -4512,15 +4515,16 @@ static int graph_build_timed(hsc_ctx *c, const GraphInput &in, bool full, float 
     if (e == hipSuccess) e = hipEventRecord(e1, s);
     // with the sync: the backward rows listed and the edge pass's check of the
     // observed ids (in.check)
-    uint32_t post[2] = {0, 0};
-    if (e == hipSuccess && gb.post) e = hipMemcpyAsync(post, gb.post, 8, hipMemcpyDeviceToHost, s);
+    uint32_t post[3] = {0, 0, 0};
+    if (e == hipSuccess && gb.post) e = hipMemcpyAsync(post, gb.post - 1, 12, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e == hipSuccess) (void)hipEventElapsedTime(build_ms, e0, e1);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     HIPCHK(c, e);
-    gb.back_n = post[0];
-    const uint32_t ebad = gb.edge_bad ? post[1] : 0;
+    if (post[0] && gb.writer_packed) return fail(c, HSC_EDEVICE, "graph build: the writer sort's look-back stalled");
+    gb.back_n = post[1];
+    const uint32_t ebad = gb.edge_bad ? post[2] : 0;
     gb.bad |= ebad;
     if (ebad & 1) {
         c->graph_ntxn = 0;

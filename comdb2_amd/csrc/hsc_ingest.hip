@@ -57,13 +57,19 @@ __device__ __forceinline__ uint64_t pk_limb(const PackPlan &P, int l, size_t i, 
     return id == P.W ? (uint64_t)gid[i] : words[(size_t)id * stride + i];
 }
 
+// ghist != null (the one-sweep passes): instead of pass 0's per-block counts,
+// the global digit histograms of all np passes (ghist[p * 256 + digit])
+constexpr int kOsMaxPasses = 8;
 __global__ __launch_bounds__(kPkThreads) void k_pk_pack(PackPlan P, size_t n, const uint32_t *gid,
                                                         const uint64_t *words, size_t stride,
                                                         const uint64_t *lsn, uint64_t *keys, uint32_t *counts,
-                                                        uint32_t nblocks)
+                                                        uint32_t nblocks, uint32_t *ghist, int np)
 {
     __shared__ uint32_t h[256];
+    __shared__ uint32_t hh[kOsMaxPasses][256];
     if (threadIdx.x < 256) h[threadIdx.x] = 0;
+    if (ghist)
+        for (int j = threadIdx.x; j < np * 256; j += kPkThreads) hh[j >> 8][j & 255] = 0;
     __syncthreads();
     const size_t base = (size_t)blockIdx.x * kPkTile;
     uint64_t key[kPkItems];
@@ -97,11 +103,21 @@ __global__ __launch_bounds__(kPkThreads) void k_pk_pack(PackPlan P, size_t n, co
         const size_t i = base + (size_t)k * kPkThreads + threadIdx.x;
         if (i < n) {
             keys[i] = key[k];
-            atomicAdd(&h[(uint32_t)(key[k] >> (P.I + P.skip)) & 0xFFu], 1u);
+            if (ghist) {
+                for (int p = 0; p < np; ++p)
+                    atomicAdd(&hh[p][(uint32_t)(key[k] >> (P.I + P.skip + 8 * p)) & 0xFFu], 1u);
+            } else {
+                atomicAdd(&h[(uint32_t)(key[k] >> (P.I + P.skip)) & 0xFFu], 1u);
+            }
         }
     }
     __syncthreads();
-    if (threadIdx.x < 256) counts[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+    if (ghist) {
+        for (int j = threadIdx.x; j < np * 256; j += kPkThreads)
+            if (hh[j >> 8][j & 255]) atomicAdd(&ghist[j], hh[j >> 8][j & 255]);
+    } else if (threadIdx.x < 256) {
+        counts[(size_t)threadIdx.x * nblocks + blockIdx.x] = h[threadIdx.x];
+    }
 }
 
 // Per-block counts of digit (key >> sh) & 255, digit-major.
@@ -209,6 +225,129 @@ __global__ __launch_bounds__(kPkThreads) void k_pk_scatter(int sh, size_t n, con
         if (dig[k] != 0xFFFFFFFFu) stage[wc[dig[k]] + lp[k]] = key[k];
     __syncthreads();
     const uint32_t nrows = (uint32_t)min((size_t)kPkTile, n - base);
+#pragma unroll 4
+    for (uint32_t j = threadIdx.x; j < nrows; j += kPkThreads) {
+        const uint64_t kj = stage[j];
+        const uint32_t dj = (uint32_t)(kj >> sh) & 0xFFu;
+        __builtin_nontemporal_store(kj, keys_o + gbase[dj] + (j - loff[dj]));
+    }
+}
+
+// One pass of the one-sweep sort (no count pass, no scan): tiles are taken in
+// ticket order; each ranks its keys as k_pk_scatter does, publishes its digit
+// counts (flag 1 = this tile's count, 2 = the inclusive prefix through it) and
+// looks back over the tiles before it -- one thread per digit, summing counts
+// until a prefix -- for its runs' global starts (the digit's base from the
+// pass's histogram, which k_pk_pack counted, + the prefix).  Earlier tickets
+// are resident or done, so the look-back always ends; a look-back that spins
+// past kOsSpin reads sets *err (the build fails loudly) and goes on.
+constexpr uint32_t kOsAgg = 1u << 30, kOsInc = 2u << 30, kOsVal = (1u << 30) - 1;
+constexpr uint32_t kOsSpin = 1u << 24;
+__global__ __launch_bounds__(kPkThreads) void k_pk_onesweep(int sh, size_t n, const uint64_t *keys,
+                                                            uint64_t *keys_o, const uint32_t *hist,
+                                                            uint32_t *status, uint32_t *ticket, uint32_t *err)
+{
+    constexpr uint32_t kWaveRows = kPkTile / kPkWaves;
+    __shared__ uint32_t gbase[256];
+    __shared__ uint32_t loff[256];
+    __shared__ uint32_t wcnt[kPkWaves][256];
+    __shared__ uint64_t stage[kPkTile];
+    __shared__ uint32_t lds16[16];
+    __shared__ uint32_t tile_id;
+    const int lane = lane_id(), wid = threadIdx.x >> 6;
+    if (threadIdx.x == 0) tile_id = atomicAdd(ticket, 1u);
+    if (threadIdx.x < 256) {
+#pragma unroll
+        for (int w = 0; w < kPkWaves; ++w) wcnt[w][threadIdx.x] = 0;
+    }
+    __syncthreads();
+    const uint32_t b = tile_id;
+    const size_t base = (size_t)b * kPkTile;
+    const uint32_t wbase = wid * kWaveRows;
+    uint64_t key[kPkItems];
+#pragma unroll
+    for (int k = 0; k < kPkItems; ++k) {
+        const size_t i = base + wbase + k * 64 + lane;
+        key[k] = i < n ? __builtin_nontemporal_load(keys + i) : 0;
+    }
+    // the digits' global bases: the exclusive scan of the pass's histogram
+    uint32_t dtot;
+    const uint32_t dbase = block_excl_scan<kPkThreads>(threadIdx.x < 256 ? hist[threadIdx.x] : 0u, lds16, dtot);
+    const uint64_t lt_mask = (lane ? (~0ull >> (64 - lane)) : 0ull);
+    uint32_t *wc = wcnt[wid];
+    uint32_t dig[kPkItems], lp[kPkItems];
+#pragma unroll
+    for (int k = 0; k < kPkItems; ++k) {
+        const size_t i = base + wbase + k * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t dk = (uint32_t)(key[k] >> sh) & 0xFFu;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t m = __ballot((dk >> q) & 1u);
+            peers &= ((dk >> q) & 1u) ? m : ~m;
+        }
+        const uint32_t before = wc[dk];
+        lp[k] = before + __popcll(peers & lt_mask);
+        dig[k] = valid ? dk : 0xFFFFFFFFu;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (valid && (peers & lt_mask) == 0) wc[dk] = before + __popcll(peers);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __syncthreads();
+    uint32_t cnt = 0;
+    if (threadIdx.x < 256) {
+        const uint32_t d = threadIdx.x;
+#pragma unroll
+        for (int w = 0; w < kPkWaves; ++w) cnt += wcnt[w][d];
+        // publish, look back, publish the prefix
+        uint32_t *my = status + (size_t)b * 256 + d;
+        uint32_t excl = 0;
+        if (b > 0) {
+            __hip_atomic_store(my, kOsAgg | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t j = (int64_t)b - 1;
+            uint32_t spins = 0;
+            while (j >= 0) {
+                const uint32_t v =
+                    __hip_atomic_load(status + (size_t)j * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((v & ~kOsVal) == 0) {
+                    if (++spins > kOsSpin) {
+                        atomicOr(err, 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += v & kOsVal;
+                if ((v & ~kOsVal) == kOsInc) break;
+                --j;
+            }
+        }
+        __hip_atomic_store(my, kOsInc | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        gbase[d] = dbase + excl;
+    }
+    uint32_t tot;
+    const uint32_t lo = block_excl_scan<kPkThreads>(cnt, lds16, tot);
+    if (threadIdx.x < 256) {
+        loff[threadIdx.x] = lo;
+        uint32_t acc = lo;  // per-(wave, digit) start inside the tile's sorted order
+#pragma unroll
+        for (int w = 0; w < kPkWaves; ++w) {
+            const uint32_t t = wcnt[w][threadIdx.x];
+            wcnt[w][threadIdx.x] = acc;
+            acc += t;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPkItems; ++k)
+        if (dig[k] != 0xFFFFFFFFu) stage[wc[dig[k]] + lp[k]] = key[k];
+    __syncthreads();
+    const uint32_t nrows = base < n ? (uint32_t)min((size_t)kPkTile, n - base) : 0u;
 #pragma unroll 4
     for (uint32_t j = threadIdx.x; j < nrows; j += kPkThreads) {
         const uint64_t kj = stage[j];
@@ -395,12 +534,23 @@ __global__ __launch_bounds__(kUdThreads) void k_pk_unpack_dd(
 
 }  // namespace
 
-size_t packed_scratch_bytes(size_t n)
+// scratch: pass 0's per-block counts + their scan, the unpack's block counts
+// + scan + row 0, then (16-byte aligned) the one-sweep region: the passes'
+// histograms, their tickets, and kOsMaxPasses x tiles x 256 status words
+static size_t packed_base_bytes(size_t n)
 {
     const size_t nblocks = (n + kPkTile - 1) / kPkTile;
     const size_t ud = (n + kUdTile - 1) / kUdTile;
     return 256 * nblocks * sizeof(uint32_t) + scan_scratch_bytes(256 * nblocks) + 1024 +
            (ud + 16) * sizeof(uint32_t) + scan_scratch_bytes(ud) + 8 * (kPackMaxWords + 1) + 64;
+}
+
+static size_t os_offset(size_t n) { return (packed_base_bytes(n) + 255) & ~(size_t)255; }
+
+size_t packed_scratch_bytes(size_t n)
+{
+    const size_t nblocks = (n + kPkTile - 1) / kPkTile;
+    return os_offset(n) + 4 * ((size_t)kOsMaxPasses * 256 + 64 + (size_t)kOsMaxPasses * 256 * nblocks);
 }
 
 bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P, bool index, const uint64_t *lsn_bits)
@@ -444,19 +594,48 @@ bool packed_plan(int W, size_t n, const uint64_t *vary, PackPlan *P, bool index,
 
 // The LSD passes of the packed keys; the sorted keys end in *kf, the other
 // key buffer is *kfree.
+// (err != null: the one-sweep passes, their stall flag -- cleared here)
 static hipError_t packed_passes(const PackPlan &P, size_t n, const uint32_t *gid,
                                 const uint64_t *words, size_t stride, const uint64_t *lsn, uint64_t *k0,
-                                uint64_t *k1, void *scratch, hipStream_t s, uint64_t **kf, uint64_t **kfree)
+                                uint64_t *k1, void *scratch, hipStream_t s, uint64_t **kf, uint64_t **kfree,
+                                uint32_t *err)
 {
     const uint32_t nblocks = (uint32_t)((n + kPkTile - 1) / kPkTile);
     uint32_t *counts = (uint32_t *)scratch;
     uint32_t *scan_tmp = counts + (size_t)256 * nblocks;
     if (P.lsn_packed && !lsn) return hipErrorInvalidValue;
-    k_pk_pack<<<nblocks, kPkThreads, 0, s>>>(P, n, gid, words, stride, lsn, k0, counts, nblocks);
-    hipError_t e = hipGetLastError();
     // (P.skip: the low bits the input is already ordered by need no pass --
     // the passes are stable)
     const int passes = (P.B - P.skip + 7) / 8;
+    // one-sweep passes (HSC_NO_ONESWEEP: the count + scan + scatter passes, an A/B)
+    static const bool no_os = getenv("HSC_NO_ONESWEEP") != nullptr;
+    if (err) {
+        const hipError_t e = hipMemsetAsync(err, 0, 4, s);
+        if (e != hipSuccess) return e;
+    }
+    if (err && !no_os && passes > 0 && passes <= kOsMaxPasses && n < (size_t)kOsVal) {
+        uint32_t *ghist = (uint32_t *)((uint8_t *)scratch + os_offset(n));
+        uint32_t *tickets = ghist + kOsMaxPasses * 256;
+        uint32_t *status = tickets + 64;
+        hipError_t e =
+            hipMemsetAsync(ghist, 0, 4 * ((size_t)kOsMaxPasses * 256 + 64 + (size_t)passes * 256 * nblocks), s);
+        if (e != hipSuccess) return e;
+        k_pk_pack<<<nblocks, kPkThreads, 0, s>>>(P, n, gid, words, stride, lsn, k0, counts, nblocks, ghist,
+                                                 passes);
+        e = hipGetLastError();
+        for (int p = 0; p < passes && e == hipSuccess; ++p) {
+            const int sh = P.I + P.skip + 8 * p;
+            k_pk_onesweep<<<nblocks, kPkThreads, 0, s>>>(sh, n, k0, k1, ghist + 256 * p,
+                                                         status + (size_t)p * 256 * nblocks, tickets + p, err);
+            e = hipGetLastError();
+            std::swap(k0, k1);
+        }
+        *kf = k0;
+        *kfree = k1;
+        return e;
+    }
+    k_pk_pack<<<nblocks, kPkThreads, 0, s>>>(P, n, gid, words, stride, lsn, k0, counts, nblocks, nullptr, 0);
+    hipError_t e = hipGetLastError();
     for (int p = 0; p < passes && e == hipSuccess; ++p) {
         const int sh = P.I + P.skip + 8 * p;
         if (p > 0) k_pk_count<<<nblocks, kPkThreads, 0, s>>>(sh, n, k0, counts, nblocks);
@@ -476,13 +655,13 @@ hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, 
                               uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
                               uint32_t *gid_d, uint64_t *words_d, size_t stride_d,
                               uint64_t **lsn_d, uint32_t *d_count, void *scratch,
-                              size_t scratch_bytes, hipStream_t s)
+                              size_t scratch_bytes, hipStream_t s, uint32_t *err)
 {
     *lsn_d = nullptr;
     if (n == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
     if (scratch_bytes < packed_scratch_bytes(n)) return hipErrorInvalidValue;
     uint64_t *kf, *kfree;
-    hipError_t e = packed_passes(P, n, gid, words, stride, lsn, k0, k1, scratch, s, &kf, &kfree);
+    hipError_t e = packed_passes(P, n, gid, words, stride, lsn, k0, k1, scratch, s, &kf, &kfree, err);
     if (e != hipSuccess) return e;
     // scratch after the passes' counters: block counts, their scan, row 0
     const uint32_t nblocks = (uint32_t)((n + kPkTile - 1) / kPkTile);

@@ -197,7 +197,9 @@ hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, 
                               uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
                               uint32_t *gid_d, uint64_t *words_d, size_t stride_d,
                               uint64_t **lsn_d, uint32_t *d_count, void *scratch,
-                              size_t scratch_bytes, hipStream_t s);
+                              size_t scratch_bytes, hipStream_t s, uint32_t *err = nullptr);
+// (err != null: the one-sweep passes -- no count pass or scan per digit --
+// with *err set if a tile's look-back stalled; the caller fails the build)
 size_t scan_scratch_bytes(size_t n);
 hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, int ngroups,
                            uint64_t *tmax, const uint32_t *group_table,
@@ -516,7 +518,8 @@ struct GraphBufs {
     uint32_t bad = 0;            // the last checked build's input bits (GraphInput::check)
     uint32_t *edge_bad = nullptr;  // device word of the edge pass's observed-id check (graph_build_timed
                                    // reads it after the build), or null
-    uint32_t *post = nullptr;      // device words read after a build: [0] backward rows listed, [1] = edge_bad's
+    uint32_t *post = nullptr;      // device words read after a build: [-1] the packed writer sort's stall
+                                   // flag, [0] backward rows listed, [1] = edge_bad's
     DBuf back;                     // a raw build's backward rows (graph_cover marks their intervals)
     bool ww_pk = false;            // the last build's ww rows came from its packed writers:
     PairPack pp{};                 // their layout, array (in the build's buffers) and count
