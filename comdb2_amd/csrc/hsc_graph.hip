@@ -555,7 +555,11 @@ __global__ void k_pair_table(uint32_t nu, const uint64_t *pk, const uint32_t *di
     tab[(uint64_t)LW * b + w] = v;
 }
 
-template <int LW>
+// NT: the op columns (read once) and the rows (not read back by this step's
+// cover or cut on the usual path) move with non-temporal loads / stores, so
+// they do not push the bucket lines -- the only re-read data -- out of the
+// caches
+template <int LW, bool NT>
 __global__ void k_edges_reads_pt(size_t nops, const uint32_t *txn, const uint64_t *key,
                                  const uint8_t *is_write, const uint32_t *observed, uint32_t nu,
                                  const uint64_t *wkey, const uint64_t *wtxn, const uint64_t *pk,
@@ -566,10 +570,12 @@ __global__ void k_edges_reads_pt(size_t nops, const uint32_t *txn, const uint64_
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nops) return;
     uint64_t wr = ~0ull, rw = ~0ull;
+    const uint32_t ob0 = NT ? __builtin_nontemporal_load(observed + i) : observed[i];
+    const bool isw = (NT ? __builtin_nontemporal_load(is_write + i) : is_write[i]) != 0;
     // (every op's observed id checked, a write's too: the build's contract)
-    if (!obs_bad(observed[i], chk_n, bad) && !is_write[i]) {
-        const uint32_t r = txn[i], ob = observed[i];
-        const uint64_t k = key[i];
+    if (!obs_bad(ob0, chk_n, bad) && !isw) {
+        const uint32_t r = NT ? __builtin_nontemporal_load(txn + i) : txn[i], ob = ob0;
+        const uint64_t k = NT ? __builtin_nontemporal_load(key + i) : key[i];
         if (ob != kNone && ob != r) wr = ((uint64_t)ob << 32) | r;
         if (!skip_rw && (k & ~pp.km) == pp.kc) {
             uint64_t km[6], tm[6];
@@ -631,8 +637,13 @@ __global__ void k_edges_reads_pt(size_t nops, const uint32_t *txn, const uint64_
         }
     }
     const size_t s = (size_t)nu + 2 * i;
-    ew[s] = wr;
-    ew[s + 1] = rw;
+    if (NT) {
+        __builtin_nontemporal_store(wr, ew + s);
+        __builtin_nontemporal_store(rw, ew + s + 1);
+    } else {
+        ew[s] = wr;
+        ew[s + 1] = rw;
+    }
     back_push(diff, wr);
     back_push(diff, rw);
     if (et) {
@@ -1259,17 +1270,21 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         } else if (pt && pp.shift <= 31) {  // (a bucket's offsets fit 32 bits)
             const uint64_t nb = ((uint64_t)1 << pp.D) + 1;
             CK(g.ptab.ensure(8 * (size_t)kLine * nb));
-#define HSC_PT(LW_)                                                                                       \
+            // (HSC_GRAPH_NT=0: cached op loads and row stores, an A/B)
+            static const bool nt = getenv("HSC_GRAPH_NT") == nullptr || atoi(getenv("HSC_GRAPH_NT")) != 0;
+#define HSC_PT(LW_, NT_)                                                                                  \
     k_pair_table<LW_><<<blocks(LW_ * nb), 256, 0, s>>>(nu, pkv, g.pdir.as<uint32_t>(), nb, pp,              \
                                                        g.ptab.as<uint64_t>());                             \
-    k_edges_reads_pt<LW_><<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, nu, \
-                                                       wkey, wtxn, pkv, g.ptab.as<uint64_t>(), pp,          \
-                                                       g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0, sink, chk_n, \
-                                                       ebad)
+    k_edges_reads_pt<LW_, NT_><<<blocks(nops), 256, 0, s>>>(nops, in.txn, in.key, in.is_write, in.observed, \
+                                                            nu, wkey, wtxn, pkv, g.ptab.as<uint64_t>(), pp, \
+                                                            g.ew.as<uint64_t>(), et, eg, in.skip_rw ? 1 : 0, \
+                                                            sink, chk_n, ebad)
             if (kLine == 16) {
-                HSC_PT(16);
+                HSC_PT(16, false);
+            } else if (nt) {
+                HSC_PT(8, true);
             } else {
-                HSC_PT(8);
+                HSC_PT(8, false);
             }
 #undef HSC_PT
         } else {
