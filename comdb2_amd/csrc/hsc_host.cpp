@@ -704,7 +704,10 @@ static int device_build(hsc_ctx *c, size_t n_in)
     const bool try_packed = W <= kPackMaxWords && n_in > 0 && !(c->paths & HSC_PATH_NO_PACKED_SORT);
     size_t scratch = std::max(radix_scratch_bytes(n_in, W), scan_scratch_bytes(n_in) + 64);
     if (try_packed) {
-        scratch = std::max(scratch, packed_scratch_bytes(n_in));
+        // (sized by the capacity, not this build's rows: the one-sweep status
+        // region grows with the rows, and a scratch that grew on a merge of a
+        // few more rows would reallocate -- a hipFree's sync -- inside a check)
+        scratch = std::max(scratch, packed_scratch_bytes(cap));
         for (auto &b : c->d_pk) HIPCHK(c, b.ensure(8 * cap));
     }
     HIPCHK(c, c->d_scratch.ensure(scratch));

@@ -243,6 +243,7 @@ __global__ __launch_bounds__(kPkThreads) void k_pk_scatter(int sh, size_t n, con
 // past kOsSpin reads sets *err (the build fails loudly) and goes on.
 constexpr uint32_t kOsAgg = 1u << 30, kOsInc = 2u << 30, kOsVal = (1u << 30) - 1;
 constexpr uint32_t kOsSpin = 1u << 24;
+constexpr size_t kOsMinRows = (size_t)1 << 21;
 __global__ __launch_bounds__(kPkThreads) void k_pk_onesweep(int sh, size_t n, const uint64_t *keys,
                                                             uint64_t *keys_o, const uint32_t *hist,
                                                             uint32_t *status, uint32_t *ticket, uint32_t *err)
@@ -613,7 +614,9 @@ static hipError_t packed_passes(const PackPlan &P, size_t n, const uint32_t *gid
         const hipError_t e = hipMemsetAsync(err, 0, 4, s);
         if (e != hipSuccess) return e;
     }
-    if (err && !no_os && passes > 0 && passes <= kOsMaxPasses && n < (size_t)kOsVal) {
+    // (small sorts -- a commit stream's windows and folds, < 2M rows -- keep
+    // the count + scan passes: a few tiles gain nothing from the look-back)
+    if (err && !no_os && passes > 0 && passes <= kOsMaxPasses && n >= kOsMinRows && n < (size_t)kOsVal) {
         uint32_t *ghist = (uint32_t *)((uint8_t *)scratch + os_offset(n));
         uint32_t *tickets = ghist + kOsMaxPasses * 256;
         uint32_t *status = tickets + 64;

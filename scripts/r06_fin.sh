@@ -26,3 +26,4 @@ step c1 500 python -u bench.py --config 1
 step c4 500 python -u bench.py --config 4
 step inproc2 500 python -u bench.py --inproc 2 --steps 30
 step trace_c4 400 rocprofv3 --kernel-trace --stats --output-format csv -d $out/${tag}_trace_c4 -o k -- python3 bench.py --config 4 --no-cpu --no-pmc --steps 3 --warmup 1
+step inproc4q4 500 python -u bench.py --inproc 4 --steps 30 --no-cpu --no-pmc --no-api --hw-queues 4

@@ -60,6 +60,12 @@ def _case(rng, n, W, ngroups, pattern):
     lsn = np.sort(rng.integers(1, 1 << 40, n, dtype=np.uint64))
     if pattern in ("dups", "scattered"):
         rng.shuffle(lsn)  # not in log order
+    if pattern == "log":  # 24 varying key bits (with repeats), commit LSNs of a log:
+        # file << 32 | 28 + 64 k, four rows per commit -- the LSNs' varying bits
+        # fit beside the key's, so they ride in the sort key (no gather)
+        words[W - 1] = (base[W - 1] & ~np.uint64((1 << 24) - 1)) | rng.integers(0, 1 << 20, n, dtype=np.uint64)
+        k = np.arange(n, dtype=np.uint64) // np.uint64(4)
+        lsn = (np.uint64(3) << np.uint64(32)) | (np.uint64(28) + np.uint64(64) * k)
     return gid, words, lsn
 
 
@@ -93,6 +99,8 @@ CASES = [
     (8192, 2, 1, "low40"), (8193, 1, 2, "scattered"), (100_000, 3, 5, "scattered"),
     (300_000, 1, 1, "dups"), (1 << 20, 1, 1, "low40"), (50_000, 2, 3, "wide"),
     (70_000, 5, 2, "scattered"), (300_000, 8, 32, "c3"), (5000, 8, 3, "c3"), (1025, 4, 2, "wide"),
+    # the LSN in the sort key; >= 2M rows: the one-sweep passes (index / LSN in the low bits)
+    (300_000, 1, 2, "log"), (2_500_000, 1, 1, "log"), (2_200_000, 1, 1, "low40"), (2_100_000, 2, 3, "scattered"),
 ]
 
 
