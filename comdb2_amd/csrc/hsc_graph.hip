@@ -71,7 +71,8 @@ __device__ __forceinline__ uint32_t gw_bits(size_t nops, const uint8_t *is_write
 // out[0] / out[1] = the varying bits of the writers' key / txn, out[2] = 0
 // (their gid): OR & ~AND over k_gw_place's block partials; out[3] / out[4]
 // the ANDs
-__global__ __launch_bounds__(1024) void k_vary_reduce(uint32_t nb, const uint64_t *vp, uint64_t *out)
+__global__ __launch_bounds__(1024) void k_vary_reduce(uint32_t nb, const uint64_t *vp, uint64_t *out,
+                                                       const uint32_t *nwb)
 {
     __shared__ uint64_t red[16][4];
     uint64_t ko = 0, ka = ~0ull, to = 0, ta = ~0ull;
@@ -94,6 +95,8 @@ __global__ __launch_bounds__(1024) void k_vary_reduce(uint32_t nb, const uint64_
         out[2] = 0;
         out[3] = ka;  // (their constant bits: AND & ~varying)
         out[4] = ta;
+        out[5] = nwb[0];  // (the writer count and the place pass's check bits: one read)
+        out[6] = nwb[1];
     }
 }
 
@@ -1074,7 +1077,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     static const bool rp_env = getenv("HSC_GRAPH_RP") != nullptr && atoi(getenv("HSC_GRAPH_RP")) != 0;
     const bool obs_in_count = rp_env;
     CK(g.flags.ensure(4 * (gwb + 2)));
-    CK(g.gvary.ensure(32 * (gwb + 2)));
+    CK(g.gvary.ensure(32 * (gwb + 3)));
     CK(g.scratch.ensure(std::max(scan_scratch_bytes(gwb + 1), (size_t)1024)));
     uint32_t *bc = g.flags.as<uint32_t>();
     CK(hipMemsetAsync(bc + gwb, 0, 8, s));  // the total slot and the check's bits
@@ -1087,13 +1090,14 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
                                                          g.ww.as<uint64_t>(), wcap, in.ntxn,
                                                          in.check ? bc + gwb + 1 : nullptr, g.gvary.as<uint64_t>());
     uint64_t *dvary = g.gvary.as<uint64_t>() + 4 * gwb;
-    k_vary_reduce<<<1, 1024, 0, s>>>((uint32_t)gwb, g.gvary.as<uint64_t>(), dvary);
+    k_vary_reduce<<<1, 1024, 0, s>>>((uint32_t)gwb, g.gvary.as<uint64_t>(), dvary, bc + gwb);
     CK(hipGetLastError());
-    uint32_t nwb[2] = {0, 0};  // writers, the check's bits
-    uint64_t hvary[5] = {0, 0, 0, 0, 0};  // the writers' varying bits: key, txn, gid; key / txn ANDs
-    CK(hipMemcpyAsync(nwb, bc + gwb, 8, hipMemcpyDeviceToHost, s));
+    // the writers' varying bits (key, txn, gid), the key / txn ANDs, the
+    // writer count and the check's bits
+    uint64_t hvary[7] = {0, 0, 0, 0, 0, 0, 0};
     CK(hipMemcpyAsync(hvary, dvary, sizeof hvary, hipMemcpyDeviceToHost, s));
     CK(hipStreamSynchronize(s));
+    const uint32_t nwb[2] = {(uint32_t)hvary[5], (uint32_t)hvary[6]};
     const uint32_t nw = nwb[0];
     g.bad = in.check ? nwb[1] : 0;
     if (g.bad & 1) return hipErrorInvalidValue;  // an op out of range: the caller reports it
@@ -1763,7 +1767,7 @@ __global__ void k_cut_txn_ops(const uint32_t *list, const uint32_t *lcnt, const 
 }
 
 hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s, const uint32_t *op_txn,
-                     const uint64_t *op_key, const uint8_t *op_isw)
+                     const uint64_t *op_key, const uint8_t *op_isw, bool host_sort)
 {
     hipError_t e = hipSuccess;
     const EdgeSet es = edge_set(g);
@@ -1824,7 +1828,7 @@ hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t 
         }
         if (k <= kCutFastCap) {
             std::vector<uint64_t> h(k);
-            if (k) {
+            if (k && host_sort) {
                 // both copies on the caller's stream, then a sync: a NULL-stream
                 // hipMemcpy from pageable memory may return before its DMA
                 // lands, and the next reader of the rows (k_relabel, the
@@ -1985,22 +1989,26 @@ hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *row
                                             g.et.as<uint64_t>(), g.eg.as<uint32_t>(), bad);
     CK(hipGetLastError());
     uint32_t hbad = 0;
-    CK(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
-    CK(hipStreamSynchronize(s));
-    if (hbad) return hipErrorInvalidValue;  // a row outside the cover: not a cut of it
     if (nc <= kSccSmallNodes && m <= kSccSmallEdges) {  // the usual small cut: one workgroup
+        // (the relabel's check read with the result: one sync; a row outside
+        // the cover fails the call, whatever the SCC made of its ~0)
         CK(g.scc.ensure(4 * ((size_t)nc + 1)));
         k_scc_small<<<1, kSccSmallThreads, 0, s>>>(nc, m, g.ew.as<uint64_t>(), g.scc.as<uint32_t>(),
                                                    g.count.as<uint32_t>() + 4);
         CK(hipGetLastError());
-        uint32_t ri[2] = {0, 0};
-        CK(hipMemcpyAsync(ri, g.count.as<uint32_t>() + 4, 8, hipMemcpyDeviceToHost, s));
+        uint32_t ri[3] = {0, 0, 0};
         k_scc_out<<<blocks(nn), 256, 0, s>>>(nn, bits, wc, g.scc.as<uint32_t>(), txn_of, scc_out);
         CK(hipGetLastError());
+        CK(hipMemcpyAsync(ri, g.count.as<uint32_t>() + 4, 8, hipMemcpyDeviceToHost, s));
+        CK(hipMemcpyAsync(&ri[2], bad, 4, hipMemcpyDeviceToHost, s));
         CK(hipStreamSynchronize(s));
+        if (ri[2]) return hipErrorInvalidValue;  // a row outside the cover: not a cut of it
         *rounds = ri[0], *iterations = ri[1];
         return hipSuccess;
     }
+    CK(hipMemcpyAsync(&hbad, bad, 4, hipMemcpyDeviceToHost, s));
+    CK(hipStreamSynchronize(s));
+    if (hbad) return hipErrorInvalidValue;  // a row outside the cover: not a cut of it
     CK(graph_rows_csr(m, ecap, nc, g, s));
     CK(graph_scc(nc, g, rounds, iterations, s));
     // sub_scc lives in g.scc (nc entries); the caller's scc_out gets all nn

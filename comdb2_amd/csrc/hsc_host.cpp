@@ -4876,7 +4876,7 @@ int ctx_graph_cut(hsc_ctx *c, const uint8_t *cover, size_t *m, const uint64_t **
 {
     MuGuard g(c);
     (void)hipSetDevice(c->device);
-    HIPCHK(c, graph_cut(c->graph, cover, m, c->stream, op_txn, op_key, op_isw));
+    HIPCHK(c, graph_cut(c->graph, cover, m, c->stream, op_txn, op_key, op_isw, false));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     *rows = c->graph.cut.as<uint64_t>();
     return HSC_OK;

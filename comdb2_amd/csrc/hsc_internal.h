@@ -669,7 +669,9 @@ hipError_t graph_cover(GraphBufs &g, uint32_t nn, uint8_t *cover, hipStream_t s)
 // rows from the covered txns' write ops)
 hipError_t graph_cut(GraphBufs &g, const uint8_t *cover, size_t *m, hipStream_t s,
                      const uint32_t *op_txn = nullptr, const uint64_t *op_key = nullptr,
-                     const uint8_t *op_isw = nullptr);
+                     const uint8_t *op_isw = nullptr, bool host_sort = true);
+// (host_sort false: the cut rows in no particular order -- the SCC of a cut
+// does not depend on it -- without the sort's two copies and syncs)
 hipError_t graph_scc_rows(uint32_t nn, const uint8_t *cover, const uint64_t *rows, size_t m,
                           GraphBufs &g, uint32_t *scc_out, uint32_t *n_cut, uint32_t *rounds,
                           uint32_t *iterations, hipStream_t s);
