@@ -405,7 +405,8 @@ __global__ void k_pk_row0(int W, const uint32_t *gid_in, const uint64_t *words_i
     if (j == W) r0[W] = gid_in[0];
 }
 
-template <int WT>  // key words 1..3, 0 = any (<= kPackMaxWords)
+// KO: the distinct packed keys only (no rows, no LSNs: the graph's writers)
+template <int WT, bool KO>  // key words 1..3, 0 = any (<= kPackMaxWords)
 __global__ __launch_bounds__(kUdThreads) void k_pk_unpack_dd(
     PackPlan P, size_t n, const uint64_t *keys, const uint64_t *r0, const uint64_t *lsn_in,
     uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o, const uint32_t *boff,
@@ -459,6 +460,14 @@ __global__ __launch_bounds__(kUdThreads) void k_pk_unpack_dd(
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *d_count = boff[blockIdx.x] + total;
     __syncthreads();
     const uint32_t b0 = boff[blockIdx.x];
+    if (KO) {
+#pragma unroll
+        for (int r = 0; r < kUdRows; ++r) {
+            const uint32_t j = r * kUdThreads + threadIdx.x;
+            if (j < nrows && pos[j] != 0xFFFFFFFFu) lsn_d[(size_t)b0 + pos[j]] = K[j];
+        }
+        return;
+    }
     const uint64_t imask = P.I >= 64 ? ~0ull : (1ull << P.I) - 1;
     // every row's LSN gather issued before the first store (10M random 8-byte
     // reads for config 2: two in flight per thread left the unpack
@@ -680,10 +689,15 @@ hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, 
     if (e == hipSuccess) e = scan_exclusive_u32(bc, ud, btmp, s);
     if (e != hipSuccess) return e;
 #define HSC_UNPACK_DD(WT_)                                                                          \
-    k_pk_unpack_dd<WT_><<<ud, kUdThreads, 0, s>>>(P, n, kf, r0, lsn, gid_o, words_o, lsn_o,       \
+    k_pk_unpack_dd<WT_, false><<<ud, kUdThreads, 0, s>>>(P, n, kf, r0, lsn, gid_o, words_o, lsn_o,     \
                                                    stride_o, bc, gid_d, words_d, kfree, stride_d,  \
                                                    d_count)
-    if (P.W == 1)
+    // (the distinct packed keys only -- no rows, no LSNs: a copy of the
+    // last-of-key words, no expand)
+    if (!gid_o && !gid_d && !lsn && P.I == 0 && !P.lsn_packed)
+        k_pk_unpack_dd<0, true><<<ud, kUdThreads, 0, s>>>(P, n, kf, r0, lsn, gid_o, words_o, lsn_o, stride_o, bc,
+                                                          gid_d, words_d, kfree, stride_d, d_count);
+    else if (P.W == 1)
         HSC_UNPACK_DD(1);
     else if (P.W == 2)
         HSC_UNPACK_DD(2);
