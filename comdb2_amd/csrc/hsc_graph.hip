@@ -1122,6 +1122,23 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         static const bool no_skip = getenv("HSC_GRAPH_NO_TXN_SKIP") != nullptr;  // (A/B)
         if (packed && txn_sorted && !no_skip && P.nl > 0 && P.limb[P.nl - 1] == 1) P.skip = P.bits[P.nl - 1];
     }
+    // the packed writers' layout (PairPack's key / txn bits) is known from the
+    // place pass's masks: a raw build's ww rows come out of the sort's unpack
+    // (edge slots [0, nu); capacity for every writer)
+    PairPack pp{};
+    if (packed) {
+        pp.km = vary[0], pp.tm = vary[1];
+        pp.kc = hvary[3] & ~pp.km, pp.tc = hvary[4] & ~pp.tm;  // (constant bits: the place pass's ANDs)
+        compress_moves(pp.km, pp.kmv);
+        compress_moves(pp.tm, pp.tmv);
+        pp.tb = __builtin_popcountll(pp.tm);
+    }
+    static const bool no_ww_fuse = getenv("HSC_GRAPH_NO_WW_FUSE") != nullptr;  // (A/B)
+    const bool ww_fused = packed && nops && !full && !in.n_extra && !rp_env && !no_ww_fuse;
+    if (ww_fused) {
+        const size_t ecap0 = std::max<size_t>(64, ((size_t)nw + 2 * nops + 63) & ~(size_t)63);
+        CK(g.ew.ensure(8 * ecap0));
+    }
     DBuf *dw = &g.ww2;
     uint64_t *lsn_d = nullptr;  // packed: the distinct packed keys themselves (no LSN input, I = 0)
     // the packed build reads its writers as the packed keys alone (the ww
@@ -1133,7 +1150,8 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
                               g.wl.as<uint64_t>(), g.wl2.as<uint64_t>(), nullptr, nullptr, nullptr, 0,
                               writer_rows ? g.wg2.as<uint32_t>() : nullptr, g.ww2.as<uint64_t>(), wcap, &lsn_d,
                               g.count.as<uint32_t>(), g.scratch.p, g.scratch.bytes, s,
-                              g.count.as<uint32_t>() + 28));  // (its stall flag: read after the build)
+                              g.count.as<uint32_t>() + 28,  // (its stall flag: read after the build)
+                              ww_fused ? g.ew.as<uint64_t>() : nullptr, ww_fused ? &pp : nullptr));
     } else {
         bool alt = false;
         if (nw) CK(hipMemsetAsync(g.wl.p, 0, 8 * (size_t)nw, s));  // (k_gw_place writes no LSNs)
@@ -1180,14 +1198,6 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
     uint32_t *eg = full || in.n_extra ? g.eg.as<uint32_t>() : nullptr;
     if (nu && !(packed && nops)) k_edges_ww<<<blocks(nu), 256, 0, s>>>(nu, wkey, wtxn, g.ew.as<uint64_t>(), et, eg);
     if (nops && packed && nu) {
-        PairPack pp{};
-        // (constant bits: any writer's, the ANDs of the place pass)
-        const uint64_t r0[2] = {hvary[3], hvary[4]};
-        pp.km = vary[0], pp.tm = vary[1];
-        pp.kc = r0[0] & ~pp.km, pp.tc = r0[1] & ~pp.tm;
-        compress_moves(pp.km, pp.kmv);
-        compress_moves(pp.tm, pp.tmv);
-        pp.tb = __builtin_popcountll(pp.tm);
         // about kPer writers per bucket, at most 2^kDMax buckets (diagnostics:
         // HSC_GRAPH_DIR = "per,dmax").  Config 4 (33M writers, r05o): 32 / 2^20
         // 11.2 ms per step, 8 / 2^23 10.4 ms (a read's search touches the
@@ -1213,7 +1223,7 @@ hipError_t graph_build(const GraphInput &in, GraphBufs &g, bool full, hipStream_
         const uint64_t *pkv = lsn_d;
         if (!pkv) return hipErrorInvalidValue;  // (a packed sort leaves them)
         pp.base = meta[3], pp.last = meta[4];
-        k_edges_ww_pk<<<blocks(nu), 256, 0, s>>>(nu, pkv, pp, g.ew.as<uint64_t>(), et, eg);
+        if (!ww_fused) k_edges_ww_pk<<<blocks(nu), 256, 0, s>>>(nu, pkv, pp, g.ew.as<uint64_t>(), et, eg);
         g.ww_pk = true, g.pp = pp, g.ppk = pkv, g.pnu = nu;  // (graph_cut: ww rows by their source)
         pp.shift = 0;  // (last - base) >> shift < 2^D
         while (pp.shift < 64 && ((pp.last - pp.base) >> pp.shift) >= ((uint64_t)1 << pp.D)) ++pp.shift;

@@ -410,7 +410,8 @@ template <int WT, bool KO>  // key words 1..3, 0 = any (<= kPackMaxWords)
 __global__ __launch_bounds__(kUdThreads) void k_pk_unpack_dd(
     PackPlan P, size_t n, const uint64_t *keys, const uint64_t *r0, const uint64_t *lsn_in,
     uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o, const uint32_t *boff,
-    uint32_t *gid_d, uint64_t *words_d, uint64_t *lsn_d, size_t stride_d, uint32_t *d_count)
+    uint32_t *gid_d, uint64_t *words_d, uint64_t *lsn_d, size_t stride_d, uint32_t *d_count,
+    uint64_t *ww, PairPack wp)
 {
     __shared__ uint64_t K[kUdTile + 1];
     __shared__ uint32_t pos[kUdTile];
@@ -461,10 +462,31 @@ __global__ __launch_bounds__(kUdThreads) void k_pk_unpack_dd(
     __syncthreads();
     const uint32_t b0 = boff[blockIdx.x];
     if (KO) {
+        // ww != null: also the writers' ww rows (writer d -> d + 1 of the same
+        // key, ~0 else) -- with no index bits a run is one repeated word, so
+        // the next distinct writer is simply the next row (K[nrows]: the next
+        // tile's first)
+        uint64_t tm[6];
+#pragma unroll
+        for (int q = 0; q < 6; ++q) tm[q] = wp.tmv[q];
+        const uint64_t tmask = wp.tb >= 64 ? ~0ull : (1ull << wp.tb) - 1;
 #pragma unroll
         for (int r = 0; r < kUdRows; ++r) {
             const uint32_t j = r * kUdThreads + threadIdx.x;
-            if (j < nrows && pos[j] != 0xFFFFFFFFu) lsn_d[(size_t)b0 + pos[j]] = K[j];
+            if (j >= nrows || pos[j] == 0xFFFFFFFFu) continue;
+            const uint64_t kj = K[j];
+            const size_t d = (size_t)b0 + pos[j];
+            lsn_d[d] = kj;
+            if (ww) {
+                uint64_t e = ~0ull;
+                if (base + j + 1 < n) {
+                    const uint64_t nx = K[j + 1];
+                    if (wp.tb >= 64 || (kj >> wp.tb) == (nx >> wp.tb))
+                        e = ((bits_expand(kj & tmask, wp.tm, tm) | wp.tc) << 32) |
+                            (bits_expand(nx & tmask, wp.tm, tm) | wp.tc);
+                }
+                ww[d] = e;
+            }
         }
         return;
     }
@@ -667,7 +689,8 @@ hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, 
                               uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
                               uint32_t *gid_d, uint64_t *words_d, size_t stride_d,
                               uint64_t **lsn_d, uint32_t *d_count, void *scratch,
-                              size_t scratch_bytes, hipStream_t s, uint32_t *err)
+                              size_t scratch_bytes, hipStream_t s, uint32_t *err, uint64_t *ww_rows,
+                              const PairPack *ww_pp)
 {
     *lsn_d = nullptr;
     if (n == 0) return hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
@@ -688,15 +711,18 @@ hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, 
     e = hipGetLastError();
     if (e == hipSuccess) e = scan_exclusive_u32(bc, ud, btmp, s);
     if (e != hipSuccess) return e;
+    const PairPack wp = ww_pp ? *ww_pp : PairPack{};
 #define HSC_UNPACK_DD(WT_)                                                                          \
     k_pk_unpack_dd<WT_, false><<<ud, kUdThreads, 0, s>>>(P, n, kf, r0, lsn, gid_o, words_o, lsn_o,     \
                                                    stride_o, bc, gid_d, words_d, kfree, stride_d,  \
-                                                   d_count)
+                                                   d_count, nullptr, wp)
     // (the distinct packed keys only -- no rows, no LSNs: a copy of the
-    // last-of-key words, no expand)
-    if (!gid_o && !gid_d && !lsn && P.I == 0 && !P.lsn_packed)
+    // last-of-key words, no expand; with ww_rows their ww rows too)
+    const bool ko = !gid_o && !gid_d && !lsn && P.I == 0 && !P.lsn_packed;
+    if (ww_rows && !(ko && ww_pp)) return hipErrorInvalidValue;
+    if (ko)
         k_pk_unpack_dd<0, true><<<ud, kUdThreads, 0, s>>>(P, n, kf, r0, lsn, gid_o, words_o, lsn_o, stride_o, bc,
-                                                          gid_d, words_d, kfree, stride_d, d_count);
+                                                          gid_d, words_d, kfree, stride_d, d_count, ww_rows, wp);
     else if (P.W == 1)
         HSC_UNPACK_DD(1);
     else if (P.W == 2)

@@ -160,6 +160,16 @@ hipError_t dedupe_flagged(int W, size_t n, const uint32_t *gid, const uint64_t *
                           uint64_t *words_out, uint64_t *lsn_out, size_t stride_out,
                           uint32_t *flags, void *scratch, size_t scratch_bytes,
                           uint32_t *d_count, hipStream_t s);
+// The packed writers' layout (hsc_graph.hip): every distinct writer is one
+// u64 pk = compress(key) << tb | compress(txn), ascending; a directory of
+// 2^D buckets over [pk[0], pk[nu - 1]]
+struct PairPack {
+    uint64_t km, tm;          // the writers' varying key / txn bits
+    uint64_t kc, tc;          // their constant bits (the same in every writer)
+    uint64_t kmv[6], tmv[6];  // compress moves
+    uint64_t base, last;      // pk[0], pk[nu - 1]
+    int tb, D, shift;         // txn bits, directory bits, bucket = (pk - base) >> shift
+};
 // Packed-key sort (hsc_ingest.hip): rows whose varying key bits plus a row
 // index fit 64 bits sort as single words.
 constexpr int kPackMaxWords = 8;
@@ -197,7 +207,10 @@ hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, 
                               uint32_t *gid_o, uint64_t *words_o, uint64_t *lsn_o, size_t stride_o,
                               uint32_t *gid_d, uint64_t *words_d, size_t stride_d,
                               uint64_t **lsn_d, uint32_t *d_count, void *scratch,
-                              size_t scratch_bytes, hipStream_t s, uint32_t *err = nullptr);
+                              size_t scratch_bytes, hipStream_t s, uint32_t *err = nullptr,
+                              uint64_t *ww_rows = nullptr, const PairPack *ww_pp = nullptr);
+// (ww_rows: for a key-only sort of packed (key, txn) writers -- no rows, no
+// LSNs, no index -- also each distinct writer's ww row, decoded by ww_pp)
 // (err != null: the one-sweep passes -- no count pass or scan per digit --
 // with *err set if a tile's look-back stalled; the caller fails the build)
 size_t scan_scratch_bytes(size_t n);
@@ -484,16 +497,6 @@ struct GraphInput {              // device pointers
     bool txn_sorted = false;  // ops in nondecreasing txn order (set by the check when it runs)
     bool check = false;       // graph_build checks the ops itself (GraphBufs::bad; an op
                               // out of range: hipErrorInvalidValue before any edge work)
-};
-// The packed writers' layout (hsc_graph.hip): every distinct writer is one
-// u64 pk = compress(key) << tb | compress(txn), ascending; a directory of
-// 2^D buckets over [pk[0], pk[nu - 1]]
-struct PairPack {
-    uint64_t km, tm;          // the writers' varying key / txn bits
-    uint64_t kc, tc;          // their constant bits (the same in every writer)
-    uint64_t kmv[6], tmv[6];  // compress moves
-    uint64_t base, last;      // pk[0], pk[nu - 1]
-    int tb, D, shift;         // txn bits, directory bits, bucket = (pk - base) >> shift
 };
 constexpr uint32_t kBackCap = 1u << 20;  // GraphBufs::back rows
 struct GraphBufs {
