@@ -244,41 +244,47 @@ __global__ __launch_bounds__(kPkThreads) void k_pk_scatter(int sh, size_t n, con
 constexpr uint32_t kOsAgg = 1u << 30, kOsInc = 2u << 30, kOsVal = (1u << 30) - 1;
 constexpr uint32_t kOsSpin = 1u << 24;
 constexpr size_t kOsMinRows = (size_t)1 << 21;
-__global__ __launch_bounds__(kPkThreads) void k_pk_onesweep(int sh, size_t n, const uint64_t *keys,
+constexpr size_t kOsMinTile = (size_t)kPkThreads * 8;  // rows per one-sweep tile, at least
+// LA: the look-back reads LA tiles' statuses per step, all loads in flight
+// together (the status words are agent-scope: a read that misses the XCD's L2
+// costs a trip to memory, so a serial walk pays one per tile)
+template <int LA, int IT, int TH>
+__global__ __launch_bounds__(TH) void k_pk_onesweep(int sh, size_t n, const uint64_t *keys,
                                                             uint64_t *keys_o, const uint32_t *hist,
                                                             uint32_t *status, uint32_t *ticket, uint32_t *err)
 {
-    constexpr uint32_t kWaveRows = kPkTile / kPkWaves;
+    constexpr int kOsTile = TH * IT;
+    constexpr uint32_t kWaveRows = kOsTile / (TH / 64);
     __shared__ uint32_t gbase[256];
     __shared__ uint32_t loff[256];
-    __shared__ uint32_t wcnt[kPkWaves][256];
-    __shared__ uint64_t stage[kPkTile];
+    __shared__ uint32_t wcnt[(TH / 64)][256];
+    __shared__ uint64_t stage[kOsTile];
     __shared__ uint32_t lds16[16];
     __shared__ uint32_t tile_id;
     const int lane = lane_id(), wid = threadIdx.x >> 6;
     if (threadIdx.x == 0) tile_id = atomicAdd(ticket, 1u);
     if (threadIdx.x < 256) {
 #pragma unroll
-        for (int w = 0; w < kPkWaves; ++w) wcnt[w][threadIdx.x] = 0;
+        for (int w = 0; w < (TH / 64); ++w) wcnt[w][threadIdx.x] = 0;
     }
     __syncthreads();
     const uint32_t b = tile_id;
-    const size_t base = (size_t)b * kPkTile;
+    const size_t base = (size_t)b * kOsTile;
     const uint32_t wbase = wid * kWaveRows;
-    uint64_t key[kPkItems];
+    uint64_t key[IT];
 #pragma unroll
-    for (int k = 0; k < kPkItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
         const size_t i = base + wbase + k * 64 + lane;
         key[k] = i < n ? __builtin_nontemporal_load(keys + i) : 0;
     }
     // the digits' global bases: the exclusive scan of the pass's histogram
     uint32_t dtot;
-    const uint32_t dbase = block_excl_scan<kPkThreads>(threadIdx.x < 256 ? hist[threadIdx.x] : 0u, lds16, dtot);
+    const uint32_t dbase = block_excl_scan<TH>(threadIdx.x < 256 ? hist[threadIdx.x] : 0u, lds16, dtot);
     const uint64_t lt_mask = (lane ? (~0ull >> (64 - lane)) : 0ull);
     uint32_t *wc = wcnt[wid];
-    uint32_t dig[kPkItems], lp[kPkItems];
+    uint32_t dig[IT], lp[IT];
 #pragma unroll
-    for (int k = 0; k < kPkItems; ++k) {
+    for (int k = 0; k < IT; ++k) {
         const size_t i = base + wbase + k * 64 + lane;
         const bool valid = i < n;
         const uint32_t dk = (uint32_t)(key[k] >> sh) & 0xFFu;
@@ -304,7 +310,7 @@ __global__ __launch_bounds__(kPkThreads) void k_pk_onesweep(int sh, size_t n, co
     if (threadIdx.x < 256) {
         const uint32_t d = threadIdx.x;
 #pragma unroll
-        for (int w = 0; w < kPkWaves; ++w) cnt += wcnt[w][d];
+        for (int w = 0; w < (TH / 64); ++w) cnt += wcnt[w][d];
         // publish, look back, publish the prefix
         uint32_t *my = status + (size_t)b * 256 + d;
         uint32_t excl = 0;
@@ -313,9 +319,26 @@ __global__ __launch_bounds__(kPkThreads) void k_pk_onesweep(int sh, size_t n, co
             int64_t j = (int64_t)b - 1;
             uint32_t spins = 0;
             while (j >= 0) {
-                const uint32_t v =
-                    __hip_atomic_load(status + (size_t)j * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((v & ~kOsVal) == 0) {
+                uint32_t v[LA];
+#pragma unroll
+                for (int q = 0; q < LA; ++q)  // (before tile 0: an inclusive 0)
+                    v[q] = j - q >= 0 ? __hip_atomic_load(status + (size_t)(j - q) * 256 + d, __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT)
+                                      : kOsInc;
+                int q = 0;
+                bool done = false;
+#pragma unroll
+                for (int r = 0; r < LA; ++r) {
+                    if (q != r || done) continue;
+                    const uint32_t f = v[r] & ~kOsVal;
+                    if (f == 0) continue;  // not published yet: the next step starts at tile j - r
+                    excl += v[r] & kOsVal;
+                    done = f == kOsInc;
+                    ++q;
+                }
+                if (done) break;
+                if (q < LA) {
+                    j -= q;
                     if (++spins > kOsSpin) {
                         atomicOr(err, 1u);
                         break;
@@ -323,21 +346,19 @@ __global__ __launch_bounds__(kPkThreads) void k_pk_onesweep(int sh, size_t n, co
                     __builtin_amdgcn_s_sleep(1);
                     continue;
                 }
-                excl += v & kOsVal;
-                if ((v & ~kOsVal) == kOsInc) break;
-                --j;
+                j -= LA;
             }
         }
         __hip_atomic_store(my, kOsInc | (excl + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         gbase[d] = dbase + excl;
     }
     uint32_t tot;
-    const uint32_t lo = block_excl_scan<kPkThreads>(cnt, lds16, tot);
+    const uint32_t lo = block_excl_scan<TH>(cnt, lds16, tot);
     if (threadIdx.x < 256) {
         loff[threadIdx.x] = lo;
         uint32_t acc = lo;  // per-(wave, digit) start inside the tile's sorted order
 #pragma unroll
-        for (int w = 0; w < kPkWaves; ++w) {
+        for (int w = 0; w < (TH / 64); ++w) {
             const uint32_t t = wcnt[w][threadIdx.x];
             wcnt[w][threadIdx.x] = acc;
             acc += t;
@@ -345,12 +366,12 @@ __global__ __launch_bounds__(kPkThreads) void k_pk_onesweep(int sh, size_t n, co
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < kPkItems; ++k)
+    for (int k = 0; k < IT; ++k)
         if (dig[k] != 0xFFFFFFFFu) stage[wc[dig[k]] + lp[k]] = key[k];
     __syncthreads();
-    const uint32_t nrows = base < n ? (uint32_t)min((size_t)kPkTile, n - base) : 0u;
+    const uint32_t nrows = base < n ? (uint32_t)min((size_t)kOsTile, n - base) : 0u;
 #pragma unroll 4
-    for (uint32_t j = threadIdx.x; j < nrows; j += kPkThreads) {
+    for (uint32_t j = threadIdx.x; j < nrows; j += TH) {
         const uint64_t kj = stage[j];
         const uint32_t dj = (uint32_t)(kj >> sh) & 0xFFu;
         __builtin_nontemporal_store(kj, keys_o + gbase[dj] + (j - loff[dj]));
@@ -581,7 +602,7 @@ static size_t os_offset(size_t n) { return (packed_base_bytes(n) + 255) & ~(size
 
 size_t packed_scratch_bytes(size_t n)
 {
-    const size_t nblocks = (n + kPkTile - 1) / kPkTile;
+    const size_t nblocks = (n + kOsMinTile - 1) / kOsMinTile;  // (status words for the smallest tiles)
     return os_offset(n) + 4 * ((size_t)kOsMaxPasses * 256 + 64 + (size_t)kOsMaxPasses * 256 * nblocks);
 }
 
@@ -641,6 +662,13 @@ static hipError_t packed_passes(const PackPlan &P, size_t n, const uint32_t *gid
     const int passes = (P.B - P.skip + 7) / 8;
     // one-sweep passes (HSC_NO_ONESWEEP: the count + scan + scatter passes, an A/B)
     static const bool no_os = getenv("HSC_NO_ONESWEEP") != nullptr;
+    // look-back width (HSC_OS_LOOK=1: one tile per step, an A/B)
+    static const int os_look = getenv("HSC_OS_LOOK") ? atoi(getenv("HSC_OS_LOOK")) : 4;
+    // rows per one-sweep tile (HSC_OS_TILE = 4096 / 8192 / 16384, an A/B)
+    static const size_t os_tile = [] {
+        const size_t t = getenv("HSC_OS_TILE") ? (size_t)atoi(getenv("HSC_OS_TILE")) : 8192;
+        return t == 4096 || t == 16384 ? t : (size_t)8192;
+    }();
     if (err) {
         const hipError_t e = hipMemsetAsync(err, 0, 4, s);
         if (e != hipSuccess) return e;
@@ -651,16 +679,24 @@ static hipError_t packed_passes(const PackPlan &P, size_t n, const uint32_t *gid
         uint32_t *ghist = (uint32_t *)((uint8_t *)scratch + os_offset(n));
         uint32_t *tickets = ghist + kOsMaxPasses * 256;
         uint32_t *status = tickets + 64;
+        const uint32_t nbos = (uint32_t)((n + os_tile - 1) / os_tile);
         hipError_t e =
-            hipMemsetAsync(ghist, 0, 4 * ((size_t)kOsMaxPasses * 256 + 64 + (size_t)passes * 256 * nblocks), s);
+            hipMemsetAsync(ghist, 0, 4 * ((size_t)kOsMaxPasses * 256 + 64 + (size_t)passes * 256 * nbos), s);
         if (e != hipSuccess) return e;
         k_pk_pack<<<nblocks, kPkThreads, 0, s>>>(P, n, gid, words, stride, lsn, k0, counts, nblocks, ghist,
                                                  passes);
         e = hipGetLastError();
         for (int p = 0; p < passes && e == hipSuccess; ++p) {
             const int sh = P.I + P.skip + 8 * p;
-            k_pk_onesweep<<<nblocks, kPkThreads, 0, s>>>(sh, n, k0, k1, ghist + 256 * p,
-                                                         status + (size_t)p * 256 * nblocks, tickets + p, err);
+            uint32_t *st = status + (size_t)p * 256 * nbos;
+            if (os_tile == 4096)
+                k_pk_onesweep<4, 8, 512><<<nbos, 512, 0, s>>>(sh, n, k0, k1, ghist + 256 * p, st, tickets + p, err);
+            else if (os_tile == 16384)
+                k_pk_onesweep<4, 16, 1024><<<nbos, 1024, 0, s>>>(sh, n, k0, k1, ghist + 256 * p, st, tickets + p, err);
+            else if (os_look == 1)
+                k_pk_onesweep<1, 16, 512><<<nbos, 512, 0, s>>>(sh, n, k0, k1, ghist + 256 * p, st, tickets + p, err);
+            else
+                k_pk_onesweep<4, 16, 512><<<nbos, 512, 0, s>>>(sh, n, k0, k1, ghist + 256 * p, st, tickets + p, err);
             e = hipGetLastError();
             std::swap(k0, k1);
         }
