@@ -927,7 +927,23 @@ static int device_build(hsc_ctx *c, size_t n_in)
         nv.cmeta = c->d_ncmeta.as<uint64_t>();
         nv.c0 = c->nc0;
         nv.n = (uint32_t)c->n;
-        HIPCHK(c, narrow_build(w, nv, s));
+        // the narrow tiles (below) when their 4096-row tiles fit the locate's
+        // histogram: key32 -- and rank32 in lsn32 mode -- from the level pass
+        const int wn_log2T = tile_log2(1);
+        const uint32_t wn_ntiles = (uint32_t)((c->n + ((size_t)1 << wn_log2T) - 1) >> wn_log2T);
+        const bool tiles_on = wn_log2T == 12 && wn_ntiles <= (uint32_t)kHistCap && c->has_commits;
+        const bool tiles_lsn32 = c->commit_span[1] - c->commit_span[0] <= kLsn32MaxSpan;
+        const bool tiles_fused = tiles_on && narrow_level01_tiles(nv);
+        uint32_t *tiles_flag = c->d_count.as<uint32_t>() + 4;
+        if (tiles_fused) {
+            HIPCHK(c, c->d_key32.ensure(4 * (size_t)nv.len[0]));
+            HIPCHK(c, c->d_rank32.ensure(4 * (size_t)nv.len[0]));
+            HIPCHK(c, narrow_build(w, nv, s, c->d_key32.as<uint32_t>(),
+                                   tiles_lsn32 ? c->d_rank32.as<uint32_t>() : nullptr, c->commit_span[0],
+                                   tiles_flag));
+        } else {
+            HIPCHK(c, narrow_build(w, nv, s));
+        }
         bt.stamp("narrow");
         // one-word tile view of the codes: rows (gid 0, key64), lsn
         WinView &wn = c->wn;
@@ -949,9 +965,17 @@ static int device_build(hsc_ctx *c, size_t n_in)
         HIPCHK(c, c->d_ngs.ensure(16));
         wn.gid = c->d_nzero.as<uint32_t>();
         wn.tmax = c->d_ntmax.as<uint64_t>();
+        // (the window's LSNs over tiles as long or twice as long as the
+        // window's: its sparse table folded, HSC_NTMAX_REBUILD=1 rebuilds it
+        // from the LSNs, an A/B)
+        static const bool ntmax_rebuild = getenv("HSC_NTMAX_REBUILD") != nullptr;
+        TmaxFrom from;
+        const int tsh = wn.log2T - c->log2T;
+        if (!ntmax_rebuild && (tsh == 0 || tsh == 1) && wn.ntiles > 0 && c->ntiles > 0 && c->levels >= wn.levels)
+            from = TmaxFrom{c->d_tmax.as<uint64_t>(), c->ntiles, tsh};
         HIPCHK(c, build_summaries(wn, c->d_ngs.as<uint32_t>(), c->d_ngs.as<uint32_t>() + 1, 1,
                                   c->d_ntmax.as<uint64_t>(), nullptr, nullptr,
-                                  c->d_nsp_g.as<uint32_t>(), c->d_nsp_w.as<uint64_t>(), s));
+                                  c->d_nsp_g.as<uint32_t>(), c->d_nsp_w.as<uint64_t>(), s, from));
         wn.gstart = c->d_ngs.as<uint32_t>();
         wn.gend = c->d_ngs.as<uint32_t>() + 1;
         wn.sp_g = c->d_nsp_g.as<uint32_t>();
@@ -960,7 +984,7 @@ static int device_build(hsc_ctx *c, size_t n_in)
         c->ntiles32 = false;
         c->trad_m = 0;
         bt.stamp("codes");
-        if (wn.log2T == 12 && wn.ntiles <= (uint32_t)kHistCap && c->has_commits) {
+        if (tiles_on) {
             // commit span: rank-free rows (lsn - oldest commit + 1) when it fits 32 bits
             const uint64_t *span = c->commit_span;
             c->rank_lsn32 = span[1] - span[0] <= kLsn32MaxSpan;
@@ -982,12 +1006,12 @@ static int device_build(hsc_ctx *c, size_t n_in)
             }
             HIPCHK(c, c->d_key32.ensure(4 * (size_t)nv.len[0]));
             HIPCHK(c, c->d_rank32.ensure(4 * (size_t)nv.len[0]));
-            uint32_t *flag = c->d_count.as<uint32_t>() + 4;
+            // (fused: key32 and the flag are written, the ranks too in lsn32 mode)
             HIPCHK(c, narrow_tiles_build(nv.keys, c->d_lsn.as<uint64_t>(), (uint32_t)c->n, nv.len[0],
                                          c->cdir, c->rank_lsn32, c->rank_base,
                                          c->d_key32.as<uint32_t>(), c->d_rank32.as<uint32_t>(),
-                                         flag, s));
-            HIPCHK(c, hipMemcpyAsync(&wide32, flag, 4, hipMemcpyDeviceToHost, s));  // read below
+                                         tiles_fused ? nullptr : tiles_flag, s));
+            HIPCHK(c, hipMemcpyAsync(&wide32, tiles_flag, 4, hipMemcpyDeviceToHost, s));  // read below
             tiles32 = true;
         }
     }

@@ -214,9 +214,19 @@ hipError_t packed_sort_dedupe(const PackPlan &P, size_t n, const uint32_t *gid, 
 // (err != null: the one-sweep passes -- no count pass or scan per digit --
 // with *err set if a tile's look-back stalled; the caller fails the build)
 size_t scan_scratch_bytes(size_t n);
+// (src != null: the tile-max sparse table derived from one over the same rows'
+// LSNs with tiles 2^shift times shorter (shift 0 or 1, at least as many
+// levels) instead of rebuilt -- the narrow tile view's, whose LSNs are the
+// window's)
+struct TmaxFrom {
+    const uint64_t *src = nullptr;
+    uint32_t ntiles = 0;
+    int shift = 0;
+};
 hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, int ngroups,
                            uint64_t *tmax, const uint32_t *group_table,
-                           uint64_t *table_max, uint32_t *sp_g, uint64_t *sp_w, hipStream_t s);
+                           uint64_t *table_max, uint32_t *sp_g, uint64_t *sp_w, hipStream_t s,
+                           const TmaxFrom &from = TmaxFrom{});
 // Probe.
 struct ProbeWork {
     uint64_t *code;        // [n] a | b << 31 | kind << 62
@@ -291,7 +301,11 @@ struct NarrowView {
 };
 bool narrow_span_fits(int W, int lw, int tz, const uint64_t *first, const uint64_t *last);
 hipError_t narrow_end_rows(const WinView &w, const uint32_t *n_dev, uint64_t *out, hipStream_t s);
-hipError_t narrow_build(const WinView &w, const NarrowView &nv, hipStream_t s);
+// (key32 != null: the narrow tiles' key32 -- and rank32 unless null, lsn32
+// mode -- written by the same pass, *flag as narrow_tiles_build's)
+bool narrow_level01_tiles(const NarrowView &nv);  // can narrow_build write key32 (levels 0 + 1 fused)
+hipError_t narrow_build(const WinView &w, const NarrowView &nv, hipStream_t s, uint32_t *key32 = nullptr,
+                        uint32_t *rank32 = nullptr, uint64_t rank_base = 0, uint32_t *flag = nullptr);
 hipError_t launch_probe_narrow(const NarrowView &nv, const ProbeView &p, uint8_t *verdict,
                                hipStream_t s);
 hipError_t narrow_codes(const NarrowView &nv, const ProbeView &p, uint64_t *lo64, uint64_t *hi64,

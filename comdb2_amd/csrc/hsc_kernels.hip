@@ -451,7 +451,8 @@ hipError_t vary_mask_rows(int W, size_t n, const uint32_t *gid, const uint64_t *
     // workgroups OR into the same W + 3 words, one atomic each per word (2048
     // workgroups of 4 rows measured 109 us on config 2, the per-word kernel
     // 100 us)
-    const unsigned wgrid = (unsigned)std::min<size_t>((n + 2047) / 2048, 512);
+    static const size_t vary_wg = getenv("HSC_VARY_WG") ? (size_t)atoi(getenv("HSC_VARY_WG")) : 512;  // (A/B)
+    const unsigned wgrid = (unsigned)std::min<size_t>((n + 2047) / 2048, std::max<size_t>(vary_wg, 1));
     switch (W) {
     case 1: k_vary_mask_w<1><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask); break;
     case 2: k_vary_mask_w<2><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask); break;
@@ -743,9 +744,31 @@ __global__ void k_splitters(WinView w, uint32_t *sp_g, uint64_t *sp_w)
     for (int j = 0; j < w.W; ++j) sp_w[(size_t)j * w.ntiles + t] = w.words[(size_t)j * w.stride + pos];
 }
 
+// Level l of a sparse table over tiles twice as long (shift 1) or as long
+// (shift 0) as the source's, from the source's level l: entry t covers source
+// tiles [t << shift, (t << shift) + 2^(l + shift)), i.e. one source entry or two
+// (the second when it starts inside the source).
+__global__ __launch_bounds__(256) void k_tmax_from(const uint64_t *src, uint32_t ns, int shift, uint64_t *dst,
+                                                   uint32_t nt)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int l = blockIdx.y;
+    if (t >= nt) return;
+    const uint32_t a = t << shift;
+    uint64_t m = src[(size_t)l * ns + a];
+    if (shift) {
+        const uint32_t b = a + (1u << l);
+        if (b < ns) {
+            const uint64_t y = src[(size_t)l * ns + b];
+            m = y > m ? y : m;
+        }
+    }
+    dst[(size_t)l * nt + t] = m;
+}
+
 hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, int ngroups,
                            uint64_t *tmax, const uint32_t *group_table, uint64_t *table_max,
-                           uint32_t *sp_g, uint64_t *sp_w, hipStream_t s)
+                           uint32_t *sp_g, uint64_t *sp_w, hipStream_t s, const TmaxFrom &from)
 {
     if (w.n == 0) {
         hipError_t e = hipMemsetAsync(gstart, 0, sizeof(uint32_t) * (size_t)ngroups, s);
@@ -755,12 +778,17 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
     if (ngroups > 0)
         k_group_bounds<<<(ngroups + 255) / 256, 256, 0, s>>>(w.n, ngroups == 1 ? nullptr : w.gid,
                                                              ngroups, gstart, gend);
-    k_tile_max<<<w.ntiles, 256, 0, s>>>(w.n, w.log2T, w.lsn, tmax);
-    if (w.levels > 1 && w.ntiles <= kSparseLdsTiles)
-        k_sparse_all<<<1, kSparseThreads, 8 * (size_t)w.ntiles, s>>>(w.ntiles, w.levels, tmax);
-    else
-        for (int l = 1; l < w.levels; ++l)
-            k_sparse_level<<<(w.ntiles + 255) / 256, 256, 0, s>>>(w.ntiles, l, tmax);
+    if (from.src && w.levels >= 1) {
+        k_tmax_from<<<dim3((w.ntiles + 255) / 256, (unsigned)w.levels), 256, 0, s>>>(from.src, from.ntiles, from.shift,
+                                                                                   tmax, w.ntiles);
+    } else {
+        k_tile_max<<<w.ntiles, 256, 0, s>>>(w.n, w.log2T, w.lsn, tmax);
+        if (w.levels > 1 && w.ntiles <= kSparseLdsTiles)
+            k_sparse_all<<<1, kSparseThreads, 8 * (size_t)w.ntiles, s>>>(w.ntiles, w.levels, tmax);
+        else
+            for (int l = 1; l < w.levels; ++l)
+                k_sparse_level<<<(w.ntiles + 255) / 256, 256, 0, s>>>(w.ntiles, l, tmax);
+    }
     if (ngroups > 0 && table_max) {
         WinView wt = w;
         wt.tmax = tmax;

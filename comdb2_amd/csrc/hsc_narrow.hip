@@ -219,6 +219,24 @@ hipError_t narrow_end_rows(const WinView &w, const uint32_t *n_dev, uint64_t *ou
     return hipGetLastError();
 }
 
+namespace {
+constexpr uint32_t kNoTile32 = 0xFFFFFFFFu;
+constexpr int kTLog2 = 12;  // 4096-row tiles (= the code view's tiles)
+}  // namespace
+
+// Eytzinger (BFS) slot of sorted row r of a 4096-row tile: rows 0 .. 4094
+// form a perfect binary tree at slots 1 .. 4095 (in-order index i = r + 1 sits
+// at level 11 - ctz(i)), row 4095 at slot 0.  A root-to-leaf walk touches
+// slots spread over a level instead of the power-of-two strides of a binary
+// search over sorted rows, which all fall in one or two LDS banks.
+static_assert(kTLog2 == 12, "eyt12 assumes 4096-row tiles");
+__device__ __forceinline__ uint32_t eyt12(uint32_t r)
+{
+    const uint32_t i = r + 1;
+    const int tz = __builtin_ctz(i);
+    return i == 4096 ? 0 : (1u << (11 - tz)) + (i >> (tz + 1));
+}
+
 // level 0: key64 of every row (padding above n), lsn (padding 0)
 __global__ void k_level0(WinView w, NarrowView nv, uint32_t len, uint64_t *key0, uint64_t *max0)
 {
@@ -236,6 +254,104 @@ __global__ void k_level0(WinView w, NarrowView nv, uint32_t len, uint64_t *key0,
     }
     key0[i] = v;
     max0[i] = m;
+}
+
+// levels 0 and 1 in one pass: level 1's entry of every 16 rows from the 16
+// lanes that hold them (last key, LSN maximum by shuffles) -- no second pass
+// re-reading level 0's LSN column.  len0 is a multiple of the block size (whole
+// tiles), level 1's entries past len0 / 16 are padding.
+__device__ __forceinline__ uint64_t level0_key(const WinView &w, const NarrowView &nv, size_t i)
+{
+    uint64_t v = kKeyPad;
+    bool rem;
+    if (nv.comp)
+        cnarrow_bound(nv, w.gid[i], w.words + i, w.stride, false, v);
+    else
+        rel_diff(w.W, nv.lw, nv.tz, w.gid[i], w.words + i, w.stride, nv.base[0], nv.base + 1, 1, kSat, v, rem);
+    return v;
+}
+
+// The narrow tiles' rows from the same pass (narrow_build with key32): one
+// 4096-row tile per workgroup, 4 rows per thread -- key32 = key64 - the tile's
+// first key64, staged in LDS in the tile's Eytzinger order and stored
+// coalesced; rank32 = LSN - base + 1 in lsn32 mode; *flag if a tile spans
+// >= 2^32 (what k_key32 / k_rank_lsn32 write, without their passes over level 0)
+struct Level01Tiles {
+    uint32_t *key32, *rank32, *flag;
+    uint64_t rank_base;
+};
+
+__global__ __launch_bounds__(256) void k_level01(WinView w, NarrowView nv, uint32_t len, uint64_t *key0,
+                                                 uint64_t *max0, uint64_t *key1, uint64_t *max1, uint32_t len1)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t v = kKeyPad, m = 0;
+    if (i < w.n) v = level0_key(w, nv, i), m = w.lsn[i];
+    if (i < len) key0[i] = v, max0[i] = m;
+    uint64_t mm = m;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+        const uint64_t y = __shfl_xor(mm, o, 16);
+        mm = y > mm ? y : mm;
+    }
+    if ((i & 15) == 15 && i < len) key1[i >> 4] = v, max1[i >> 4] = mm;
+    const size_t pad = len / 16 + i;
+    if (pad < len1) key1[pad] = kKeyPad, max1[pad] = 0;
+}
+
+constexpr int kL01TThreads = 1024;
+__global__ __launch_bounds__(kL01TThreads) void k_level01t(WinView w, NarrowView nv, uint32_t len,
+                                                           uint64_t *key0, uint64_t *max0, uint64_t *key1,
+                                                           uint64_t *max1, uint32_t len1, Level01Tiles T)
+{
+    constexpr int R = (1 << kTLog2) / kL01TThreads;
+    __shared__ uint32_t st[1 << kTLog2];
+    __shared__ uint64_t tfirst;
+    const size_t base = (size_t)blockIdx.x << kTLog2;
+    uint64_t v[R], m[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const size_t i = base + (size_t)k * kL01TThreads + threadIdx.x;
+        v[k] = kKeyPad, m[k] = 0;
+        if (i < w.n) v[k] = level0_key(w, nv, i), m[k] = w.lsn[i];
+    }
+    if (threadIdx.x == 0) tfirst = v[0];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const size_t i = base + (size_t)k * kL01TThreads + threadIdx.x;  // (< len: whole tiles)
+        key0[i] = v[k], max0[i] = m[k];
+        uint64_t mm = m[k];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+            const uint64_t y = __shfl_xor(mm, o, 16);
+            mm = y > mm ? y : mm;
+        }
+        if ((i & 15) == 15) key1[i >> 4] = v[k], max1[i >> 4] = mm;
+        if (T.rank32) T.rank32[i] = i < w.n ? (uint32_t)(m[k] - T.rank_base) + 1 : 0;
+    }
+    if (blockIdx.x == 0 && len / 16 + threadIdx.x < len1)
+        key1[len / 16 + threadIdx.x] = kKeyPad, max1[len / 16 + threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t f = tfirst;
+    bool wide = false;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const uint32_t r = k * kL01TThreads + threadIdx.x;
+        uint32_t x = 0xFFFFFFFFu;
+        if (base + r < w.n) {
+            const uint64_t d = v[k] - f;
+            wide |= d > 0xFFFFFFFFull;
+            x = (uint32_t)d;
+        }
+        st[eyt12(r)] = x;
+    }
+    if (wide) atomicOr(T.flag, 1u);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+        const uint32_t r = k * kL01TThreads + threadIdx.x;
+        T.key32[base + r] = st[r];
+    }
 }
 
 // level l + 1 from level l: last key / max lsn of every 16-entry block
@@ -259,11 +375,37 @@ __global__ void k_level_up(const uint64_t *key_src, const uint64_t *max_src, uin
     max_dst[i] = m;
 }
 
-hipError_t narrow_build(const WinView &w, const NarrowView &nv, hipStream_t s)
+bool narrow_level01_tiles(const NarrowView &nv)
+{
+    static const bool sep = getenv("HSC_LEVEL_SEP") != nullptr;
+    return !sep && nv.levels >= 2 && nv.len[0] % (1u << kTLog2) == 0;
+}
+
+hipError_t narrow_build(const WinView &w, const NarrowView &nv, hipStream_t s, uint32_t *key32,
+                        uint32_t *rank32, uint64_t rank_base, uint32_t *flag)
 {
     const uint32_t len0 = nv.len[0];
-    k_level0<<<(len0 + 255) / 256, 256, 0, s>>>(w, nv, len0, (uint64_t *)nv.keys, (uint64_t *)nv.maxs);
-    for (int l = 1; l < nv.levels; ++l)
+    static const bool sep = getenv("HSC_LEVEL_SEP") != nullptr;  // (A/B: level 1 by its own pass)
+    int l = 1;
+    if (key32 && !narrow_level01_tiles(nv)) return hipErrorInvalidValue;
+    if (nv.levels >= 2 && len0 % 256 == 0 && !sep) {
+        if (key32) {
+            const hipError_t e = hipMemsetAsync(flag, 0, 4, s);
+            if (e != hipSuccess) return e;
+        }
+        uint64_t *k1 = (uint64_t *)nv.keys + nv.off[1], *m1 = (uint64_t *)nv.maxs + nv.off[1];
+        if (key32)
+            k_level01t<<<len0 >> kTLog2, kL01TThreads, 0, s>>>(w, nv, len0, (uint64_t *)nv.keys, (uint64_t *)nv.maxs,
+                                                               k1, m1, nv.len[1],
+                                                               Level01Tiles{key32, rank32, flag, rank_base});
+        else
+            k_level01<<<len0 / 256, 256, 0, s>>>(w, nv, len0, (uint64_t *)nv.keys, (uint64_t *)nv.maxs, k1, m1,
+                                                 nv.len[1]);
+        l = 2;
+    } else {
+        k_level0<<<(len0 + 255) / 256, 256, 0, s>>>(w, nv, len0, (uint64_t *)nv.keys, (uint64_t *)nv.maxs);
+    }
+    for (; l < nv.levels; ++l)
         k_level_up<<<(nv.len[l] + 255) / 256, 256, 0, s>>>(
             nv.keys + nv.off[l - 1], nv.maxs + nv.off[l - 1], nv.len[l - 1],
             (uint64_t *)nv.keys + nv.off[l], (uint64_t *)nv.maxs + nv.off[l], nv.len[l]);
@@ -895,10 +1037,6 @@ hipError_t narrow_codes(const NarrowView &nv, const ProbeView &p, uint64_t *lo64
 //               r(S) = #{c in C : c <= S} and  lsn > S  <=>  rank > r(S).
 //
 // Join records are 16 bytes: {lo delta, hi delta, r(S), read set}.
-namespace {
-constexpr uint32_t kNoTile32 = 0xFFFFFFFFu;
-constexpr int kTLog2 = 12;  // 4096-row tiles (= the code view's tiles)
-}  // namespace
 
 __global__ void k_check_sorted(const uint64_t *v, size_t n, uint32_t *flag)
 {
@@ -922,18 +1060,6 @@ __host__ __device__ inline uint32_t dir16_lds_entries(const Dir16 &d);
 __global__ __launch_bounds__(kRankThreads) void k_rank32(const uint64_t *lsn, uint32_t n,
                                                          uint32_t len, Dir16 d, uint32_t *rank);
 
-// Eytzinger (BFS) slot of sorted row r of a 4096-row tile: rows 0 .. 4094
-// form a perfect binary tree at slots 1 .. 4095 (in-order index i = r + 1 sits
-// at level 11 - ctz(i)), row 4095 at slot 0.  A root-to-leaf walk touches
-// slots spread over a level instead of the power-of-two strides of a binary
-// search over sorted rows, which all fall in one or two LDS banks.
-static_assert(kTLog2 == 12, "eyt12 assumes 4096-row tiles");
-__device__ __forceinline__ uint32_t eyt12(uint32_t r)
-{
-    const uint32_t i = r + 1;
-    const int tz = __builtin_ctz(i);
-    return i == 4096 ? 0 : (1u << (11 - tz)) + (i >> (tz + 1));
-}
 
 // key32 = key64 - first key64 of the tile, stored in the tile's Eytzinger
 // order (the join copies a tile's keys into LDS as they lie); flag := 1 if a
@@ -965,9 +1091,13 @@ hipError_t narrow_tiles_build(const uint64_t *key64, const uint64_t *lsn, uint32
                               const Dir16 &cdir, int rank_lsn32, uint64_t rank_base,
                               uint32_t *key32, uint32_t *rank32, uint32_t *flag, hipStream_t s)
 {
-    hipError_t e = hipMemsetAsync(flag, 0, 4, s);
-    if (e != hipSuccess || len == 0) return e;
-    k_key32<<<(len + 255) / 256, 256, 0, s>>>(key64, n, len, key32, flag);
+    if (!flag) {  // (key32 and the flag written by the level pass: the ranks only)
+        if (len == 0 || rank_lsn32) return hipSuccess;
+    } else {
+        hipError_t e = hipMemsetAsync(flag, 0, 4, s);
+        if (e != hipSuccess || len == 0) return e;
+        k_key32<<<(len + 255) / 256, 256, 0, s>>>(key64, n, len, key32, flag);
+    }
     if (rank_lsn32) {
         k_rank_lsn32<<<(len + 255) / 256, 256, 0, s>>>(lsn, n, len, rank_base, rank32);
     } else {
