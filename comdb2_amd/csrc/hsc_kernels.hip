@@ -128,12 +128,11 @@ __global__ __launch_bounds__(256) void k_vary_mask(int W, size_t n, const uint32
 // row's words, gid and LSN are loaded together (U rows per thread, all loads
 // in flight before the first OR).  k_vary_mask above walks the rows once per
 // word: 100 us for config 2's 280 MB (2.8 TB/s).
-template <int WT>
+template <int WT, int U = 8>
 __global__ __launch_bounds__(256) void k_vary_mask_w(size_t n, const uint32_t *gid, const uint64_t *words,
                                                      size_t stride, const uint64_t *lsn,
                                                      unsigned long long *mask)
 {
-    constexpr int U = 8;
     __shared__ uint64_t part[256 / 64][WT + 4];
     uint64_t ref[WT + 1], m[WT + 1];
 #pragma unroll
@@ -452,10 +451,16 @@ hipError_t vary_mask_rows(int W, size_t n, const uint32_t *gid, const uint64_t *
     // workgroups of 4 rows measured 109 us on config 2, the per-word kernel
     // 100 us)
     static const size_t vary_wg = getenv("HSC_VARY_WG") ? (size_t)atoi(getenv("HSC_VARY_WG")) : 512;  // (A/B)
+    static const int vary_u = getenv("HSC_VARY_U") ? atoi(getenv("HSC_VARY_U")) : 8;  // rows per thread (A/B: 16)
     const unsigned wgrid = (unsigned)std::min<size_t>((n + 2047) / 2048, std::max<size_t>(vary_wg, 1));
     switch (W) {
     case 1: k_vary_mask_w<1><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask); break;
-    case 2: k_vary_mask_w<2><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask); break;
+    case 2:
+        if (vary_u == 16)
+            k_vary_mask_w<2, 16><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask);
+        else
+            k_vary_mask_w<2><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask);
+        break;
     case 3: k_vary_mask_w<3><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask); break;
     case 4: k_vary_mask_w<4><<<wgrid, 256, 0, s>>>(n, gid, words, stride, ls, dmask); break;
     default: {
