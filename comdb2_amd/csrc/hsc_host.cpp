@@ -877,21 +877,11 @@ static int device_build(hsc_ctx *c, size_t n_in)
     w.W = W;
     w.log2T = c->log2T;
     w.levels = c->levels;
-    HIPCHK(c, build_summaries(w, c->d_gstart.as<uint32_t>(), c->d_gend.as<uint32_t>(), ng,
-                              c->d_tmax.as<uint64_t>(), c->d_group_table.as<uint32_t>(),
-                              c->d_table_max.as<uint64_t>(), c->d_sp_g.as<uint32_t>(),
-                              c->d_sp_w.as<uint64_t>(), s));
-    bt.stamp("summaries");
-    c->compact = false;
-    uint32_t wide32 = 1;   // narrow tiles: a tile spans >= 2^32 codes (device flag)
-    bool tiles32 = false;
-    c->ctiles = false;
-    if (!c->narrow && (c->layout == HSC_LAYOUT_AUTO || c->layout == HSC_LAYOUT_COMPACT_WIDE) &&
-        c->n > 0 && W > 1 && ng > 0) {
-        HIPCHK_RC(c, build_compact(c, w));
-        if (c->compact) HIPCHK_RC(c, build_ctiles(c));
-        bt.stamp("compact");
-    }
+    // the narrow index before the summaries: its level-1 LSN maxima (one per
+    // 16 rows) give the window's tile maxima, read instead of every row's LSN
+    // (HSC_NTMAX_REBUILD=1: from the LSNs, an A/B)
+    bool tiles_on = false, tiles_fused = false;
+    uint32_t *tiles_flag = c->d_count.as<uint32_t>() + 4;
     if (c->narrow) {
         // level sizes: level 0 = n + 1 rounded up to whole tiles (at least one
         // pad; the tile pipeline stages whole tiles), then roundup16(len / 16)
@@ -931,10 +921,9 @@ static int device_build(hsc_ctx *c, size_t n_in)
         // histogram: key32 -- and rank32 in lsn32 mode -- from the level pass
         const int wn_log2T = tile_log2(1);
         const uint32_t wn_ntiles = (uint32_t)((c->n + ((size_t)1 << wn_log2T) - 1) >> wn_log2T);
-        const bool tiles_on = wn_log2T == 12 && wn_ntiles <= (uint32_t)kHistCap && c->has_commits;
+        tiles_on = wn_log2T == 12 && wn_ntiles <= (uint32_t)kHistCap && c->has_commits;
         const bool tiles_lsn32 = c->commit_span[1] - c->commit_span[0] <= kLsn32MaxSpan;
-        const bool tiles_fused = tiles_on && narrow_level01_tiles(nv);
-        uint32_t *tiles_flag = c->d_count.as<uint32_t>() + 4;
+        tiles_fused = tiles_on && narrow_level01_tiles(nv);
         if (tiles_fused) {
             HIPCHK(c, c->d_key32.ensure(4 * (size_t)nv.len[0]));
             HIPCHK(c, c->d_rank32.ensure(4 * (size_t)nv.len[0]));
@@ -945,6 +934,27 @@ static int device_build(hsc_ctx *c, size_t n_in)
             HIPCHK(c, narrow_build(w, nv, s));
         }
         bt.stamp("narrow");
+    }
+    static const bool tmax_rows = getenv("HSC_NTMAX_REBUILD") != nullptr;
+    TmaxFrom wfrom;
+    if (c->narrow && !tmax_rows && c->nv.levels >= 2 && c->log2T >= 4) wfrom.lsn16 = c->nv.maxs + c->nv.off[1];
+    HIPCHK(c, build_summaries(w, c->d_gstart.as<uint32_t>(), c->d_gend.as<uint32_t>(), ng,
+                              c->d_tmax.as<uint64_t>(), c->d_group_table.as<uint32_t>(),
+                              c->d_table_max.as<uint64_t>(), c->d_sp_g.as<uint32_t>(),
+                              c->d_sp_w.as<uint64_t>(), s, wfrom));
+    bt.stamp("summaries");
+    c->compact = false;
+    uint32_t wide32 = 1;   // narrow tiles: a tile spans >= 2^32 codes (device flag)
+    bool tiles32 = false;
+    c->ctiles = false;
+    if (!c->narrow && (c->layout == HSC_LAYOUT_AUTO || c->layout == HSC_LAYOUT_COMPACT_WIDE) &&
+        c->n > 0 && W > 1 && ng > 0) {
+        HIPCHK_RC(c, build_compact(c, w));
+        if (c->compact) HIPCHK_RC(c, build_ctiles(c));
+        bt.stamp("compact");
+    }
+    if (c->narrow) {
+        NarrowView &nv = c->nv;
         // one-word tile view of the codes: rows (gid 0, key64), lsn
         WinView &wn = c->wn;
         wn = WinView{};

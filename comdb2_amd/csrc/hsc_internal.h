@@ -218,10 +218,13 @@ size_t scan_scratch_bytes(size_t n);
 // LSNs with tiles 2^shift times shorter (shift 0 or 1, at least as many
 // levels) instead of rebuilt -- the narrow tile view's, whose LSNs are the
 // window's)
+// (lsn16 != null: the same rows' LSN maxima per 16 rows -- the narrow
+// index's level 1 -- read instead of every row's LSN for the tile maxima)
 struct TmaxFrom {
     const uint64_t *src = nullptr;
     uint32_t ntiles = 0;
     int shift = 0;
+    const uint64_t *lsn16 = nullptr;
 };
 hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, int ngroups,
                            uint64_t *tmax, const uint32_t *group_table,

@@ -787,7 +787,10 @@ hipError_t build_summaries(const WinView &w, uint32_t *gstart, uint32_t *gend, i
         k_tmax_from<<<dim3((w.ntiles + 255) / 256, (unsigned)w.levels), 256, 0, s>>>(from.src, from.ntiles, from.shift,
                                                                                    tmax, w.ntiles);
     } else {
-        k_tile_max<<<w.ntiles, 256, 0, s>>>(w.n, w.log2T, w.lsn, tmax);
+        if (from.lsn16 && w.log2T >= 4)
+            k_tile_max<<<w.ntiles, 256, 0, s>>>((w.n + 15) / 16, w.log2T - 4, from.lsn16, tmax);
+        else
+            k_tile_max<<<w.ntiles, 256, 0, s>>>(w.n, w.log2T, w.lsn, tmax);
         if (w.levels > 1 && w.ntiles <= kSparseLdsTiles)
             k_sparse_all<<<1, kSparseThreads, 8 * (size_t)w.ntiles, s>>>(w.ntiles, w.levels, tmax);
         else
